@@ -1,0 +1,440 @@
+/*
+ * dynamics.c -- oracle restatement of DYNAMICS (model/src/dynamics.F:21-739):
+ * MOM_FLUXFORM (pkg/mom_fluxform/mom_fluxform.F:42-1064) and TIMESTEP
+ * (model/src/timestep.F:10-429) with ADAMS_BASHFORTH2
+ * (model/src/adams_bashforth2.F:6-92), per tile and per level k.
+ * TEST INFRASTRUCTURE (see oracle.h).
+ */
+#include "oracle.h"
+#include <math.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+/* tile-local 2-D scratch, Fortran indexing (i,j) */
+#define L(a, i, j) (a)[(long)((i) + OLx - 1) + (long)((j) + OLy - 1) * nx]
+
+static void check_supported(const OModel *m) {
+  if (m->useBiharmonicVisc || m->viscA4D != 0.0 || m->viscA4Z != 0.0) {
+    fprintf(stderr, "oracle_dynamics: biharmonic viscosity not yet restated\n"); abort();
+  }
+  if (m->implicitViscosity) { fprintf(stderr, "oracle_dynamics: implicitViscosity not yet restated\n"); abort(); }
+  if (!m->usingCartesianGrid) { fprintf(stderr, "oracle_dynamics: metric terms not yet restated\n"); abort(); }
+}
+
+void oracle_dynamics(OModel *m) {
+  check_supported(m);
+  const int sNx = m->sNx, sNy = m->sNy, OLx = m->OLx, OLy = m->OLy, Nr = m->Nr, nx = m->nx;
+  const long n2 = m->n2;
+  const int iMin = 0, iMax = sNx + 1, jMin = 0, jMax = sNy + 1; /* dynamics.F:191-192 */
+  double *fVerU[2], *fVerV[2];
+  for (int q = 0; q < 2; q++) { fVerU[q] = calloc(n2, 8); fVerV[q] = calloc(n2, 8); }
+  double *hFacZ = calloc(n2, 8), *r_hFacZ = calloc(n2, 8), *xA = calloc(n2, 8), *yA = calloc(n2, 8);
+  double *uTrans = calloc(n2, 8), *vTrans = calloc(n2, 8), *rTransU = calloc(n2, 8), *rTransV = calloc(n2, 8);
+  double *fZon = calloc(n2, 8), *fMer = calloc(n2, 8), *fVrUp = calloc(n2, 8), *fVrDw = calloc(n2, 8);
+  double *uCf = calloc(n2, 8), *vCf = calloc(n2, 8), *vF = calloc(n2, 8), *cDrag = calloc(n2, 8);
+  double *guDiss = calloc(n2, 8), *gvDiss = calloc(n2, 8), *guExt = calloc(n2, 8), *gvExt = calloc(n2, 8);
+  double *gUtmp = calloc(n2, 8), *gVtmp = calloc(n2, 8), *ab = calloc(n2, 8);
+  double *kappaRU = calloc(n2 * (Nr + 1), 8), *kappaRV = calloc(n2 * (Nr + 1), 8);
+
+  /* MOM_FLUXFORM factors (mom_fluxform.F:236-277) */
+  const double uDudxFac = m->afFacMom, vDudyFac = m->afFacMom, rVelDudrFac = m->afFacMom;
+  const double AhDudxFac = m->vfFacMom, AhDudyFac = m->vfFacMom;
+  const double ArDudrFac = m->implicitViscosity ? 0.0 : m->vfFacMom;
+  const double fuFac = m->cfFacMom, fvFac = m->cfFacMom;
+  const int bottomDragTerms = m->no_slip_bottom; /* selectBotDragQuadr=-1, bottomDragLinear=0 */
+
+  for (int t = 0; t < m->nTiles; t++) {
+    double *gU = m->gU + t * m->n3, *gV = m->gV + t * m->n3;
+    double *uVel = m->uVel + t * m->n3, *vVel = m->vVel + t * m->n3, *wVel = m->wVel + t * m->n3;
+    double *guNm1 = m->guNm1 + t * m->n3, *gvNm1 = m->gvNm1 + t * m->n3;
+    const double *hFacW = m->hFacW + t * m->n3, *hFacS = m->hFacS + t * m->n3, *hFacC = m->hFacC + t * m->n3;
+    const double *maskW = m->maskW + t * m->n3, *maskS = m->maskS + t * m->n3, *maskC = m->maskC + t * m->n3;
+    const double *rhFacW = m->recip_hFacW + t * m->n3, *rhFacS = m->recip_hFacS + t * m->n3;
+    const double *dxG = m->dxG + t * n2, *dyG = m->dyG + t * n2, *dxF = m->dxF + t * n2, *dyF = m->dyF + t * n2;
+    const double *dxV = m->dxV + t * n2, *dyU = m->dyU + t * n2, *rA = m->rA + t * n2, *rAw = m->rAw + t * n2;
+    const double *rAs = m->rAs + t * n2;
+    const double *recip_dxF = m->recip_dxF + t * n2, *recip_dyF = m->recip_dyF + t * n2;
+    const double *recip_dxV = m->recip_dxV + t * n2, *recip_dyU = m->recip_dyU + t * n2;
+    const double *recip_rAw = m->recip_rAw + t * n2, *recip_rAs = m->recip_rAs + t * n2;
+    const double *fCori = m->fCori + t * n2;
+    const double *sfU = m->surfaceForcingU + t * n2, *sfV = m->surfaceForcingV + t * n2;
+#define W3(a, i, j, k) (a)[(long)((i) + OLx - 1) + (long)((j) + OLy - 1) * nx + (long)((k) - 1) * n2]
+
+    /* dynamics.F:288-343: zero gU/gV and the ping-pong flux buffers */
+    for (long p = 0; p < m->n3; p++) { gU[p] = 0.0; gV[p] = 0.0; }
+    for (long p = 0; p < n2; p++) { fVerU[0][p] = fVerU[1][p] = fVerV[0][p] = fVerV[1][p] = 0.0; }
+    /* CALC_VISCOSITY (model/src/calc_viscosity.F): kappaRU = viscArNr(k) */
+    for (long p = 0; p < n2 * (Nr + 1); p++) { kappaRU[p] = m->viscAr; kappaRV[p] = m->viscAr; }
+
+    for (int k = 1; k <= Nr; k++) {
+      const int kUp = 1 + (k + 1) % 2, kDown = 1 + k % 2; /* dynamics.F:425-426 */
+      double *fVerUkm = fVerU[kUp - 1], *fVerVkm = fVerV[kUp - 1];
+      double *fVerUkp = fVerU[kDown - 1], *fVerVkp = fVerV[kDown - 1];
+      /* dPhiHydX/Y: CALC_PHI_HYD -- zero for the supported (uniform-density) configs */
+      for (long p = 0; p < n2; p++) {
+        guDiss[p] = gvDiss[p] = 0.0; fZon[p] = fMer[p] = fVrUp[p] = fVrDw[p] = 0.0;
+        uCf[p] = vCf[p] = vF[p] = 0.0; rTransU[p] = rTransV[p] = 0.0;
+      }
+      /* MOM_CALC_HFACZ (pkg/mom_common/mom_calc_hfacz.F:158-371, hZoption=0) */
+      for (int i = 1 - OLx; i <= sNx + OLx; i++) L(hFacZ, i, 1 - OLy) = 0.0;
+      for (int j = 2 - OLy; j <= sNy + OLy; j++) L(hFacZ, 1 - OLx, j) = 0.0;
+      for (int j = 2 - OLy; j <= sNy + OLy; j++)
+        for (int i = 2 - OLx; i <= sNx + OLx; i++) {
+          double h = fmin(W3(hFacW, i, j, k), W3(hFacW, i, j - 1, k));
+          h = fmin(W3(hFacS, i, j, k), h);
+          h = fmin(W3(hFacS, i - 1, j, k), h);
+          L(hFacZ, i, j) = h;
+        }
+      for (int j = 1 - OLy; j <= sNy + OLy; j++)
+        for (int i = 1 - OLx; i <= sNx + OLx; i++)
+          L(r_hFacZ, i, j) = (L(hFacZ, i, j) == 0.0) ? 0.0 : 1.0 / L(hFacZ, i, j);
+      /* xA, yA, uTrans, vTrans (mom_fluxform.F:287-327) */
+      for (int j = 1 - OLy; j <= sNy + OLy; j++)
+        for (int i = 1 - OLx; i <= sNx + OLx; i++) {
+          L(xA, i, j) = L(dyG, i, j) * m->drF[k - 1] * W3(hFacW, i, j, k);
+          L(yA, i, j) = L(dxG, i, j) * m->drF[k - 1] * W3(hFacS, i, j, k);
+          L(uTrans, i, j) = W3(uVel, i, j, k) * L(xA, i, j);
+          L(vTrans, i, j) = W3(vVel, i, j, k) * L(yA, i, j);
+        }
+      if (m->momAdvection && k == 1) {
+        /* MOM_CALC_RTRANS(k=1) (mom_calc_rtrans.F:92-105), MOM_U/V_ADV_WU/WV(k=1) surface flux */
+        for (int j = 2 - OLy; j <= sNy + OLy; j++)
+          for (int i = 2 - OLx; i <= sNx + OLx; i++) {
+            L(rTransU, i, j) = 0.5 * (W3(wVel, i - 1, j, 1) * L(rA, i - 1, j) + W3(wVel, i, j, 1) * L(rA, i, j));
+            L(rTransV, i, j) = 0.5 * (W3(wVel, i, j - 1, 1) * L(rA, i, j - 1) + W3(wVel, i, j, 1) * L(rA, i, j));
+          }
+        for (int j = 2 - OLy; j <= sNy + OLy; j++)
+          for (int i = 2 - OLx; i <= sNx + OLx; i++) {
+            L(fVerUkm, i, j) = L(rTransU, i, j) * W3(uVel, i, j, 1); /* mom_u_adv_wu.F:65-72 */
+            L(fVerVkm, i, j) = L(rTransV, i, j) * W3(vVel, i, j, 1);
+          }
+      }
+      if (m->momAdvection) {
+        /* MOM_CALC_RTRANS(k+1) */
+        if (k + 1 > Nr) {
+          for (int j = 2 - OLy; j <= sNy + OLy; j++)
+            for (int i = 2 - OLx; i <= sNx + OLx; i++) L(rTransU, i, j) = L(rTransV, i, j) = 0.0;
+        } else {
+          for (int j = 2 - OLy; j <= sNy + OLy; j++)
+            for (int i = 2 - OLx; i <= sNx + OLx; i++) {
+              L(rTransU, i, j) = 0.5 * (W3(wVel, i - 1, j, k + 1) * L(rA, i - 1, j) + W3(wVel, i, j, k + 1) * L(rA, i, j));
+              L(rTransV, i, j) = 0.5 * (W3(wVel, i, j - 1, k + 1) * L(rA, i, j - 1) + W3(wVel, i, j, k + 1) * L(rA, i, j));
+            }
+        }
+      }
+      /* ================= U component ================= */
+      if (m->momAdvection) {
+        /* MOM_U_ADV_UU (mom_u_adv_uu.F:46-57) */
+        for (int j = 1 - OLy; j <= sNy + OLy - 1; j++)
+          for (int i = 1 - OLx; i <= sNx + OLx - 1; i++)
+            L(fZon, i, j) = 0.25 * (L(uTrans, i, j) + L(uTrans, i + 1, j)) * (W3(uVel, i, j, k) + W3(uVel, i + 1, j, k));
+        /* MOM_U_ADV_VU (mom_u_adv_vu.F:46-61) */
+        for (int j = 2 - OLy; j <= sNy + OLy; j++)
+          for (int i = 2 - OLx; i <= sNx + OLx; i++)
+            L(fMer, i, j) = 0.25 * (L(vTrans, i, j) + L(vTrans, i - 1, j)) * (W3(uVel, i, j, k) + W3(uVel, i, j - 1, k));
+        /* MOM_U_ADV_WU(k+1) (mom_u_adv_wu.F:56-105), select_rStar=0 branch */
+        if (k + 1 > Nr) {
+          for (int j = 1 - OLy; j <= sNy + OLy; j++)
+            for (int i = 1 - OLx; i <= sNx + OLx; i++) L(fVerUkp, i, j) = 0.0;
+        } else {
+          const int kk = k + 1;
+          for (int j = 2 - OLy; j <= sNy + OLy; j++)
+            for (int i = 2 - OLx; i <= sNx + OLx; i++) {
+              double f = L(rTransU, i, j) * (0.5 * (W3(uVel, i, j, kk) + W3(uVel, i, j, kk - 1)));
+              f = f + 0.25 * (W3(wVel, i, j, kk) * L(rA, i, j) * (W3(maskC, i, j, kk) - W3(maskC, i, j, kk - 1)) +
+                              W3(wVel, i - 1, j, kk) * L(rA, i - 1, j) * (W3(maskC, i - 1, j, kk) - W3(maskC, i - 1, j, kk - 1))) *
+                          W3(uVel, i, j, kk);
+              L(fVerUkp, i, j) = f;
+            }
+        }
+        /* gU (mom_fluxform.F:502-517) */
+        for (int j = jMin; j <= jMax; j++)
+          for (int i = iMin; i <= iMax; i++)
+            W3(gU, i, j, k) = -W3(rhFacW, i, j, k) * m->recip_drF[k - 1] * L(recip_rAw, i, j) *
+                              ((L(fZon, i, j) - L(fZon, i - 1, j)) * uDudxFac +
+                               (L(fMer, i, j + 1) - L(fMer, i, j)) * vDudyFac +
+                               (L(fVerUkp, i, j) - L(fVerUkm, i, j)) * m->rkSign * rVelDudrFac);
+      } else {
+        for (int j = 1 - OLy; j <= sNy + OLy; j++)
+          for (int i = 1 - OLx; i <= sNx + OLx; i++) W3(gU, i, j, k) = 0.0;
+      }
+      if (m->momViscosity) {
+        /* MOM_U_XVISCFLUX (mom_u_xviscflux.F:51-68), del2u=0 (no biharmonic) */
+        for (int j = 1 - OLy; j <= sNy + OLy - 1; j++)
+          for (int i = 1 - OLx; i <= sNx + OLx - 1; i++)
+            L(fZon, i, j) = L(dyF, i, j) * m->drF[k - 1] * W3(hFacC, i, j, k) *
+                            (-m->viscAhD * (W3(uVel, i + 1, j, k) - W3(uVel, i, j, k)) * 1.0 + m->viscA4D * 0.0 * 1.0) *
+                            L(recip_dxF, i, j);
+        /* MOM_U_YVISCFLUX (mom_u_yviscflux.F:52-73) */
+        for (int j = 2 - OLy; j <= sNy + OLy; j++)
+          for (int i = 1 - OLx; i <= sNx + OLx; i++)
+            L(fMer, i, j) = L(dxV, i, j) * m->drF[k - 1] * L(hFacZ, i, j) *
+                            (-m->viscAhZ * (W3(uVel, i, j, k) - W3(uVel, i, j - 1, k)) + m->viscA4Z * 0.0) *
+                            L(recip_dyU, i, j);
+        /* MOM_U_RVISCFLUX(k) and (k+1) (mom_u_rviscflux.F) */
+        for (int q = 0; q < 2; q++) {
+          int kk = k + q; double *fl = q ? fVrDw : fVrUp;
+          if (kk <= 1 || kk > Nr) {
+            for (long p = 0; p < n2; p++) fl[p] = 0.0;
+          } else {
+            for (int j = 1 - OLy; j <= sNy + OLy - 1; j++)
+              for (int i = 1 - OLx; i <= sNx + OLx - 1; i++)
+                L(fl, i, j) = -kappaRU[(long)(kk - 1) * n2 + (i + OLx - 1) + (long)(j + OLy - 1) * nx] * L(rAw, i, j) *
+                              (W3(uVel, i, j, kk) - W3(uVel, i, j, kk - 1)) * m->rkSign * m->recip_drC[kk - 1] *
+                              W3(maskW, i, j, kk) * W3(maskW, i, j, kk - 1);
+          }
+        }
+        /* guDiss (mom_fluxform.F:602-618) */
+        for (int j = jMin; j <= jMax; j++)
+          for (int i = iMin; i <= iMax; i++)
+            L(guDiss, i, j) = -W3(rhFacW, i, j, k) * m->recip_drF[k - 1] * L(recip_rAw, i, j) *
+                              ((L(fZon, i, j) - L(fZon, i - 1, j)) * AhDudxFac +
+                               (L(fMer, i, j + 1) - L(fMer, i, j)) * AhDudyFac +
+                               (L(fVrDw, i, j) - L(fVrUp, i, j)) * m->rkSign * ArDudrFac);
+        if (m->no_slip_sides) {
+          /* MOM_U_SIDEDRAG (pkg/mom_common/mom_u_sidedrag.F:100-145), variable-viscosity form */
+          for (int j = 2 - OLy; j <= sNy + OLy - 1; j++)
+            for (int i = 2 - OLx; i <= sNx + OLx - 1; i++) {
+              double hS = W3(hFacW, i, j, k) - L(hFacZ, i, j);
+              double hN = W3(hFacW, i, j, k) - L(hFacZ, i, j + 1);
+              L(vF, i, j) = -W3(rhFacW, i, j, k) * m->recip_drF[k - 1] * L(recip_rAw, i, j) *
+                            (hS * L(dxV, i, j) * L(recip_dyU, i, j) * (m->viscAhZ * W3(uVel, i, j, k) - m->viscA4Z * 0.0) +
+                             hN * L(dxV, i, j + 1) * L(recip_dyU, i, j + 1) * (m->viscAhZ * W3(uVel, i, j, k) - m->viscA4Z * 0.0)) *
+                            m->drF[k - 1] * m->sideDragFactor;
+            }
+          for (int j = jMin; j <= jMax; j++)
+            for (int i = iMin; i <= iMax; i++) L(guDiss, i, j) = L(guDiss, i, j) + L(vF, i, j);
+        }
+        if (bottomDragTerms) {
+          /* MOM_U_BOTDRAG_COEFF (pkg/mom_common/mom_u_botdrag_coeff.F), z-coords, no quadratic drag */
+          const int kBottom = Nr, kDn = (k + 1 < Nr) ? k + 1 : Nr, kLowF = k + 1;
+          const double recDrC = (k == kBottom) ? m->recip_drF[k - 1] : m->recip_drC[kLowF - 1];
+          const double viscFac = m->no_slip_bottom ? 2.0 : 0.0;
+          for (int j = 1 - OLy; j <= sNy + OLy; j++)
+            for (int i = 2 - OLx; i <= sNx + OLx; i++) L(cDrag, i, j) = 0.0 * 1.0;
+          for (int j = 1 - OLy; j <= sNy + OLy - 1; j++)
+            for (int i = 2 - OLx; i <= sNx + OLx - 1; i++)
+              L(cDrag, i, j) = L(cDrag, i, j) + kappaRU[(long)(kLowF - 1) * n2 + (i + OLx - 1) + (long)(j + OLy - 1) * nx] * recDrC * viscFac;
+          for (int j = 1 - OLy; j <= sNy + OLy; j++)
+            for (int i = 2 - OLx; i <= sNx + OLx; i++)
+              L(cDrag, i, j) = (k == kBottom) ? L(cDrag, i, j) * W3(maskW, i, j, k)
+                                              : L(cDrag, i, j) * W3(maskW, i, j, k) * (1.0 - W3(maskW, i, j, kDn));
+          for (int j = jMin; j <= jMax; j++)
+            for (int i = iMin; i <= iMax; i++)
+              L(guDiss, i, j) = L(guDiss, i, j) - L(cDrag, i, j) * W3(uVel, i, j, k) * W3(rhFacW, i, j, k) * m->recip_drF[k - 1];
+        }
+      }
+      /* ================= V component ================= */
+      if (m->momAdvection) {
+        /* MOM_V_ADV_UV (mom_v_adv_uv.F:45-60) */
+        for (int j = 2 - OLy; j <= sNy + OLy; j++)
+          for (int i = 2 - OLx; i <= sNx + OLx; i++)
+            L(fZon, i, j) = 0.25 * (L(uTrans, i, j) + L(uTrans, i, j - 1)) * (W3(vVel, i, j, k) + W3(vVel, i - 1, j, k));
+        /* MOM_V_ADV_VV (mom_v_adv_vv.F:46-57) */
+        for (int j = 1 - OLy; j <= sNy + OLy - 1; j++)
+          for (int i = 1 - OLx; i <= sNx + OLx - 1; i++)
+            L(fMer, i, j) = 0.25 * (L(vTrans, i, j) + L(vTrans, i, j + 1)) * (W3(vVel, i, j, k) + W3(vVel, i, j + 1, k));
+        /* MOM_V_ADV_WV(k+1) */
+        if (k + 1 > Nr) {
+          for (int j = 1 - OLy; j <= sNy + OLy; j++)
+            for (int i = 1 - OLx; i <= sNx + OLx; i++) L(fVerVkp, i, j) = 0.0;
+        } else {
+          const int kk = k + 1;
+          for (int j = 2 - OLy; j <= sNy + OLy; j++)
+            for (int i = 2 - OLx; i <= sNx + OLx; i++) {
+              double f = L(rTransV, i, j) * (0.5 * (W3(vVel, i, j, kk) + W3(vVel, i, j, kk - 1)));
+              f = f + 0.25 * (W3(wVel, i, j, kk) * L(rA, i, j) * (W3(maskC, i, j, kk) - W3(maskC, i, j, kk - 1)) +
+                              W3(wVel, i, j - 1, kk) * L(rA, i, j - 1) * (W3(maskC, i, j - 1, kk) - W3(maskC, i, j - 1, kk - 1))) *
+                          W3(vVel, i, j, kk);
+              L(fVerVkp, i, j) = f;
+            }
+        }
+        /* gV (mom_fluxform.F:762-777) */
+        for (int j = jMin; j <= jMax; j++)
+          for (int i = iMin; i <= iMax; i++)
+            W3(gV, i, j, k) = -W3(rhFacS, i, j, k) * m->recip_drF[k - 1] * L(recip_rAs, i, j) *
+                              ((L(fZon, i + 1, j) - L(fZon, i, j)) * uDudxFac +
+                               (L(fMer, i, j) - L(fMer, i, j - 1)) * vDudyFac +
+                               (L(fVerVkp, i, j) - L(fVerVkm, i, j)) * m->rkSign * rVelDudrFac);
+      } else {
+        for (int j = 1 - OLy; j <= sNy + OLy; j++)
+          for (int i = 1 - OLx; i <= sNx + OLx; i++) W3(gV, i, j, k) = 0.0;
+      }
+      if (m->momViscosity) {
+        /* MOM_V_XVISCFLUX (mom_v_xviscflux.F:52-69) */
+        for (int j = 1 - OLy; j <= sNy + OLy; j++)
+          for (int i = 2 - OLx; i <= sNx + OLx; i++)
+            L(fZon, i, j) = L(dyU, i, j) * m->drF[k - 1] * L(hFacZ, i, j) *
+                            (-m->viscAhZ * (W3(vVel, i, j, k) - W3(vVel, i - 1, j, k)) * 1.0 + m->viscA4Z * 0.0 * 1.0) *
+                            L(recip_dxV, i, j);
+        /* MOM_V_YVISCFLUX (mom_v_yviscflux.F:51-73) */
+        for (int j = 1 - OLy; j <= sNy + OLy - 1; j++)
+          for (int i = 1 - OLx; i <= sNx + OLx - 1; i++)
+            L(fMer, i, j) = L(dxF, i, j) * m->drF[k - 1] * W3(hFacC, i, j, k) *
+                            (-m->viscAhD * (W3(vVel, i, j + 1, k) - W3(vVel, i, j, k)) + m->viscA4D * 0.0) *
+                            L(recip_dyF, i, j);
+        for (int q = 0; q < 2; q++) {
+          int kk = k + q; double *fl = q ? fVrDw : fVrUp;
+          if (kk <= 1 || kk > Nr) {
+            for (long p = 0; p < n2; p++) fl[p] = 0.0;
+          } else {
+            for (int j = 1 - OLy; j <= sNy + OLy - 1; j++)
+              for (int i = 1 - OLx; i <= sNx + OLx - 1; i++)
+                L(fl, i, j) = -kappaRV[(long)(kk - 1) * n2 + (i + OLx - 1) + (long)(j + OLy - 1) * nx] * L(rAs, i, j) *
+                              (W3(vVel, i, j, kk) - W3(vVel, i, j, kk - 1)) * m->rkSign * m->recip_drC[kk - 1] *
+                              W3(maskS, i, j, kk) * W3(maskS, i, j, kk - 1);
+          }
+        }
+        /* gvDiss (mom_fluxform.F:861-877) */
+        for (int j = jMin; j <= jMax; j++)
+          for (int i = iMin; i <= iMax; i++)
+            L(gvDiss, i, j) = -W3(rhFacS, i, j, k) * m->recip_drF[k - 1] * L(recip_rAs, i, j) *
+                              ((L(fZon, i + 1, j) - L(fZon, i, j)) * AhDudxFac +
+                               (L(fMer, i, j) - L(fMer, i, j - 1)) * AhDudyFac +
+                               (L(fVrDw, i, j) - L(fVrUp, i, j)) * m->rkSign * ArDudrFac);
+        if (m->no_slip_sides) {
+          /* MOM_V_SIDEDRAG (pkg/mom_common/mom_v_sidedrag.F) */
+          for (int j = 2 - OLy; j <= sNy + OLy - 1; j++)
+            for (int i = 2 - OLx; i <= sNx + OLx - 1; i++) {
+              double hW = W3(hFacS, i, j, k) - L(hFacZ, i, j);
+              double hE = W3(hFacS, i, j, k) - L(hFacZ, i + 1, j);
+              L(vF, i, j) = -W3(rhFacS, i, j, k) * m->recip_drF[k - 1] * L(recip_rAs, i, j) *
+                            (hW * L(dyU, i, j) * L(recip_dxV, i, j) * (m->viscAhZ * W3(vVel, i, j, k) - m->viscA4Z * 0.0) +
+                             hE * L(dyU, i + 1, j) * L(recip_dxV, i + 1, j) * (m->viscAhZ * W3(vVel, i, j, k) - m->viscA4Z * 0.0)) *
+                            m->drF[k - 1] * m->sideDragFactor;
+            }
+          for (int j = jMin; j <= jMax; j++)
+            for (int i = iMin; i <= iMax; i++) L(gvDiss, i, j) = L(gvDiss, i, j) + L(vF, i, j);
+        }
+        if (bottomDragTerms) {
+          const int kBottom = Nr, kDn = (k + 1 < Nr) ? k + 1 : Nr, kLowF = k + 1;
+          const double recDrC = (k == kBottom) ? m->recip_drF[k - 1] : m->recip_drC[kLowF - 1];
+          const double viscFac = m->no_slip_bottom ? 2.0 : 0.0;
+          for (int j = 2 - OLy; j <= sNy + OLy; j++)
+            for (int i = 1 - OLx; i <= sNx + OLx; i++) L(cDrag, i, j) = 0.0 * 1.0;
+          for (int j = 2 - OLy; j <= sNy + OLy - 1; j++)
+            for (int i = 1 - OLx; i <= sNx + OLx - 1; i++)
+              L(cDrag, i, j) = L(cDrag, i, j) + kappaRV[(long)(kLowF - 1) * n2 + (i + OLx - 1) + (long)(j + OLy - 1) * nx] * recDrC * viscFac;
+          for (int j = 2 - OLy; j <= sNy + OLy; j++)
+            for (int i = 1 - OLx; i <= sNx + OLx; i++)
+              L(cDrag, i, j) = (k == kBottom) ? L(cDrag, i, j) * W3(maskS, i, j, k)
+                                              : L(cDrag, i, j) * W3(maskS, i, j, k) * (1.0 - W3(maskS, i, j, kDn));
+          for (int j = jMin; j <= jMax; j++)
+            for (int i = iMin; i <= iMax; i++)
+              L(gvDiss, i, j) = L(gvDiss, i, j) - L(cDrag, i, j) * W3(vVel, i, j, k) * W3(rhFacS, i, j, k) * m->recip_drF[k - 1];
+        }
+      }
+      /* Coriolis (mom_fluxform.F:995-1022; mom_u_coriolis.F, mom_v_coriolis.F) */
+      if (m->useCoriolis) {
+        const int sc = m->selectCoriScheme;
+        for (int j = 1 - OLy; j <= sNy + OLy - 1; j++)
+          for (int i = 2 - OLx; i <= sNx + OLx; i++) {
+            double c;
+            if (sc >= 2)
+              c = 0.5 * (L(fCori, i, j) * 0.5 * (W3(vVel, i, j, k) + W3(vVel, i, j + 1, k)) +
+                         L(fCori, i - 1, j) * 0.5 * (W3(vVel, i - 1, j, k) + W3(vVel, i - 1, j + 1, k)));
+            else
+              c = 0.5 * (L(fCori, i, j) + L(fCori, i - 1, j)) *
+                  0.25 * (W3(vVel, i, j, k) + W3(vVel, i, j + 1, k) + W3(vVel, i - 1, j, k) + W3(vVel, i - 1, j + 1, k));
+            if (sc == 1 || sc == 3)
+              c = c * 4.0 / fmax(1.0, W3(maskS, i, j, k) + W3(maskS, i, j + 1, k) + W3(maskS, i - 1, j, k) + W3(maskS, i - 1, j + 1, k));
+            L(uCf, i, j) = c;
+          }
+        for (int j = 2 - OLy; j <= sNy + OLy; j++)
+          for (int i = 1 - OLx; i <= sNx + OLx - 1; i++) {
+            double c;
+            if (sc >= 2)
+              c = -0.5 * (L(fCori, i, j) * 0.5 * (W3(uVel, i, j, k) + W3(uVel, i + 1, j, k)) +
+                          L(fCori, i, j - 1) * 0.5 * (W3(uVel, i, j - 1, k) + W3(uVel, i + 1, j - 1, k)));
+            else
+              c = -0.5 * (L(fCori, i, j) + L(fCori, i, j - 1)) *
+                  0.25 * (W3(uVel, i, j, k) + W3(uVel, i + 1, j, k) + W3(uVel, i, j - 1, k) + W3(uVel, i + 1, j - 1, k));
+            if (sc == 1 || sc == 3)
+              c = c * 4.0 / fmax(1.0, W3(maskW, i, j, k) + W3(maskW, i + 1, j, k) + W3(maskW, i, j - 1, k) + W3(maskW, i + 1, j - 1, k));
+            L(vCf, i, j) = c;
+          }
+        for (int j = jMin; j <= jMax; j++)
+          for (int i = iMin; i <= iMax; i++) {
+            W3(gU, i, j, k) = W3(gU, i, j, k) + fuFac * L(uCf, i, j);
+            W3(gV, i, j, k) = W3(gV, i, j, k) + fvFac * L(vCf, i, j);
+          }
+      }
+      /* masks (mom_fluxform.F:1044-1051) */
+      for (int j = jMin; j <= jMax; j++)
+        for (int i = iMin; i <= iMax; i++) {
+          W3(gU, i, j, k) = W3(gU, i, j, k) * W3(maskW, i, j, k);
+          L(guDiss, i, j) = L(guDiss, i, j) * W3(maskW, i, j, k);
+          W3(gV, i, j, k) = W3(gV, i, j, k) * W3(maskS, i, j, k);
+          L(gvDiss, i, j) = L(gvDiss, i, j) * W3(maskS, i, j, k);
+        }
+
+      /* ======================== TIMESTEP (timestep.F) ======================== */
+      for (long p = 0; p < n2; p++) guExt[p] = gvExt[p] = gUtmp[p] = gVtmp[p] = 0.0;
+      if (m->momForcing) {
+        /* APPLY_FORCING_U/V (model/src/apply_forcing.F:81-88), kSurface=1 */
+        if (k == 1) {
+          for (int j = 0; j <= sNy + 1; j++)
+            for (int i = 1; i <= sNx + 1; i++)
+              L(guExt, i, j) = L(guExt, i, j) + m->foFacMom * L(sfU, i, j) * m->recip_drF[k - 1] * W3(rhFacW, i, j, k);
+          for (int j = 1; j <= sNy + 1; j++)
+            for (int i = 0; i <= sNx + 1; i++)
+              L(gvExt, i, j) = L(gvExt, i, j) + m->foFacMom * L(sfV, i, j) * m->recip_drF[k - 1] * W3(rhFacS, i, j, k);
+        }
+      }
+      /* timestep.F:116-126: - phFac*dPhiHydX (zero here) */
+      if (m->momViscosity && m->momDissip_In_AB)
+        for (int j = jMin; j <= jMax; j++)
+          for (int i = iMin; i <= iMax; i++) {
+            W3(gU, i, j, k) = W3(gU, i, j, k) + L(guDiss, i, j);
+            W3(gV, i, j, k) = W3(gV, i, j, k) + L(gvDiss, i, j);
+          }
+      if (m->momForcing && m->momForcingOutAB != 1)
+        for (int j = jMin; j <= jMax; j++)
+          for (int i = iMin; i <= iMax; i++) {
+            W3(gU, i, j, k) = W3(gU, i, j, k) + L(guExt, i, j);
+            W3(gV, i, j, k) = W3(gV, i, j, k) + L(gvExt, i, j);
+          }
+      /* ADAMS_BASHFORTH2 (adams_bashforth2.F:61-88), kArg = k */
+      {
+        const double abFac = (m->myIter == m->nIter0 && m->nIter0 == 0) ? 0.0 : 0.5 + m->abEps;
+        for (int j = 1 - OLy; j <= sNy + OLy; j++)
+          for (int i = 1 - OLx; i <= sNx + OLx; i++) {
+            double a = abFac * (W3(gU, i, j, k) - W3(guNm1, i, j, k));
+            W3(guNm1, i, j, k) = W3(gU, i, j, k);
+            W3(gU, i, j, k) = W3(gU, i, j, k) + a;
+            a = abFac * (W3(gV, i, j, k) - W3(gvNm1, i, j, k));
+            W3(gvNm1, i, j, k) = W3(gV, i, j, k);
+            W3(gV, i, j, k) = W3(gV, i, j, k) + a;
+          }
+      }
+      for (int j = jMin; j <= jMax; j++)
+        for (int i = iMin; i <= iMax; i++) { L(gUtmp, i, j) = W3(gU, i, j, k); L(gVtmp, i, j) = W3(gV, i, j, k); }
+      if (m->momForcing && m->momForcingOutAB == 1)
+        for (int j = jMin; j <= jMax; j++)
+          for (int i = iMin; i <= iMax; i++) {
+            L(gUtmp, i, j) = L(gUtmp, i, j) + L(guExt, i, j);
+            L(gVtmp, i, j) = L(gVtmp, i, j) + L(gvExt, i, j);
+          }
+      if (m->momViscosity && !m->momDissip_In_AB)
+        for (int j = jMin; j <= jMax; j++)
+          for (int i = iMin; i <= iMax; i++) {
+            L(gUtmp, i, j) = L(gUtmp, i, j) + L(guDiss, i, j);
+            L(gVtmp, i, j) = L(gVtmp, i, j) + L(gvDiss, i, j);
+          }
+      /* u* = u + dt*(gUtmp + gUdPx)*maskW, gUdPx = 0 for implicSurfPress = 1 (timestep.F:373-388) */
+      for (int j = jMin; j <= jMax; j++)
+        for (int i = iMin; i <= iMax; i++) {
+          W3(gU, i, j, k) = W3(uVel, i, j, k) + m->deltaTMom * (L(gUtmp, i, j) + 0.0) * W3(maskW, i, j, k);
+          W3(gV, i, j, k) = W3(vVel, i, j, k) + m->deltaTMom * (L(gVtmp, i, j) + 0.0) * W3(maskS, i, j, k);
+        }
+    }
+#undef W3
+  }
+  (void)ab;
+  for (int q = 0; q < 2; q++) { free(fVerU[q]); free(fVerV[q]); }
+  free(hFacZ); free(r_hFacZ); free(xA); free(yA); free(uTrans); free(vTrans); free(rTransU); free(rTransV);
+  free(fZon); free(fMer); free(fVrUp); free(fVrDw); free(uCf); free(vCf); free(vF); free(cDrag);
+  free(guDiss); free(gvDiss); free(guExt); free(gvExt); free(gUtmp); free(gVtmp); free(ab);
+  free(kappaRU); free(kappaRV);
+}

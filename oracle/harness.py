@@ -1,0 +1,186 @@
+"""ctypes harness around liboracle.so -- TEST INFRASTRUCTURE.
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may import
+this module.  It drives the CPU restatement (oracle/*.c) of the reference's hot
+path and reproduces the reference's %MON statistics for comparison.
+"""
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB = os.path.join(HERE, "liboracle.so")
+_lib = None
+
+
+def build():
+    subprocess.check_call(["make", "-s", "-C", HERE])
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB):
+            build()
+        L = ctypes.CDLL(LIB)
+        vp, c_int, c_dbl, c_char_p = ctypes.c_void_p, ctypes.c_int, ctypes.c_double, ctypes.c_char_p
+        L.oracle_new.restype = vp
+        L.oracle_new.argtypes = [c_int] * 7
+        L.oracle_free.argtypes = [vp]
+        L.oracle_set_param.argtypes = [vp, c_char_p, c_dbl]
+        L.oracle_set_param.restype = c_int
+        L.oracle_get_param.argtypes = [vp, c_char_p]
+        L.oracle_get_param.restype = c_dbl
+        L.oracle_array.argtypes = [vp, c_char_p, ctypes.POINTER(ctypes.c_long)]
+        L.oracle_array.restype = ctypes.POINTER(c_dbl)
+        L.oracle_iarray.argtypes = [vp, c_char_p, ctypes.POINTER(ctypes.c_long)]
+        L.oracle_iarray.restype = ctypes.POINTER(c_int)
+        for fn in ("oracle_ini_grid", "oracle_ini_cg2d"):
+            getattr(L, fn).argtypes = [vp]
+            getattr(L, fn).restype = c_int
+        L.oracle_ini_depths.argtypes = [vp, ctypes.POINTER(c_dbl)]
+        L.oracle_ini_depths.restype = c_int
+        for fn in ("oracle_dynamics", "oracle_solve_for_pressure", "oracle_momentum_correction_step",
+                   "oracle_integr_continuity", "oracle_forward_step"):
+            getattr(L, fn).argtypes = [vp]
+        P = ctypes.POINTER(c_dbl)
+        L.oracle_cg2d.argtypes = [vp, P, P, P, P, P, ctypes.POINTER(c_int), ctypes.POINTER(c_int)]
+        L.oracle_mon_stats.argtypes = [vp, P, c_int, P, c_int, P, P, P, P]
+        L.oracle_exch_xy.argtypes = [vp, P]
+        _lib = L
+    return _lib
+
+
+def _dp(a):
+    return a.ctypes.data_as(ctypes.POINTER(ctypes.c_double))
+
+
+class Oracle:
+    """One oracle model instance (one process, nSx x nSy tiles)."""
+
+    def __init__(self, sNx, sNy, OLx, OLy, Nr, nSx=1, nSy=1):
+        self.L = lib()
+        self.sNx, self.sNy, self.OLx, self.OLy, self.Nr, self.nSx, self.nSy = sNx, sNy, OLx, OLy, Nr, nSx, nSy
+        self.nx, self.ny = sNx + 2 * OLx, sNy + 2 * OLy
+        self.h = self.L.oracle_new(sNx, sNy, OLx, OLy, Nr, nSx, nSy)
+
+    def __del__(self):
+        if getattr(self, "h", None):
+            self.L.oracle_free(self.h)
+            self.h = None
+
+    def set(self, **kw):
+        for k, v in kw.items():
+            if self.L.oracle_set_param(self.h, k.encode(), float(v)) != 0:
+                raise KeyError(k)
+
+    def get(self, name):
+        return self.L.oracle_get_param(self.h, name.encode())
+
+    def arr(self, name):
+        """Live numpy view of an oracle array, shaped (tiles, [Nr,] ny, nx) for fields."""
+        n = ctypes.c_long()
+        p = self.L.oracle_array(self.h, name.encode(), ctypes.byref(n))
+        if not p:
+            raise KeyError(name)
+        a = np.ctypeslib.as_array(p, shape=(n.value,))
+        nt = self.nSx * self.nSy
+        n2 = self.nx * self.ny
+        if n.value == nt * n2:
+            return a.reshape(nt, self.ny, self.nx)
+        if n.value == nt * n2 * self.Nr:
+            return a.reshape(nt, self.Nr, self.ny, self.nx)
+        return a
+
+    def iarr(self, name):
+        n = ctypes.c_long()
+        p = self.L.oracle_iarray(self.h, name.encode(), ctypes.byref(n))
+        return np.ctypeslib.as_array(p, shape=(n.value,)).reshape(self.nSx * self.nSy, self.ny, self.nx)
+
+    # --- phases ---
+    def ini_grid(self):
+        assert self.L.oracle_ini_grid(self.h) == 0
+
+    def ini_depths(self, bathy):
+        b = np.ascontiguousarray(bathy, dtype=np.float64)
+        assert self.L.oracle_ini_depths(self.h, _dp(b)) == 0
+
+    def ini_cg2d(self):
+        assert self.L.oracle_ini_cg2d(self.h) == 0
+
+    def forward_step(self):
+        self.L.oracle_forward_step(self.h)
+
+    def cg2d(self, b, x, maxIters, nIterMin=-1):
+        """CG2D on full halo-inclusive (tiles, ny, nx) arrays; returns (x, first, minSq, last, its, itMin)."""
+        b = np.ascontiguousarray(b, dtype=np.float64).copy()
+        x = np.ascontiguousarray(x, dtype=np.float64).copy()
+        f, mn, la = ctypes.c_double(), ctypes.c_double(), ctypes.c_double()
+        it, itm = ctypes.c_int(maxIters), ctypes.c_int(nIterMin)
+        self.L.oracle_cg2d(self.h, _dp(b), _dp(x), ctypes.byref(f), ctypes.byref(mn), ctypes.byref(la),
+                           ctypes.byref(it), ctypes.byref(itm))
+        return x, f.value, mn.value, la.value, it.value, itm.value
+
+    def stats(self, field, nr, hfac, hfac3d, mask, area, dr):
+        out = np.zeros(6)
+        f = np.ascontiguousarray(field, dtype=np.float64)
+        h = np.ascontiguousarray(hfac, dtype=np.float64)
+        mk = np.ascontiguousarray(mask, dtype=np.float64)
+        ar = np.ascontiguousarray(area, dtype=np.float64)
+        d = np.ascontiguousarray(dr, dtype=np.float64)
+        self.L.oracle_mon_stats(self.h, _dp(f), nr, _dp(h), int(hfac3d), _dp(mk), _dp(ar), _dp(d), _dp(out))
+        return out
+
+    def dynstat(self):
+        """The dynstat block of MONITOR (pkg/monitor/monitor.F:103-129) for eta, u, v, w."""
+        res = {}
+        Nr = self.Nr
+        drF = self.arr("drF")[:Nr].copy()
+        drC = self.arr("drC")[:Nr].copy()
+        mC, mW, mS = self.arr("maskInC"), self.arr("maskInW"), self.arr("maskInS")
+        for name, fld, hf, h3, mask, area, dr, nr in (
+                ("eta", self.arr("etaN"), mC, 0, mC, self.arr("rA"), drF, 1),
+                ("uvel", self.arr("uVel"), self.arr("hFacW"), 1, mW, self.arr("rAw"), drF, Nr),
+                ("vvel", self.arr("vVel"), self.arr("hFacS"), 1, mS, self.arr("rAs"), drF, Nr),
+                ("wvel", self.arr("wVel"), self.arr("maskC"), 1, mC, self.arr("rA"), drC, Nr)):
+            st = self.stats(fld, nr, hf, h3, mask, area, dr)
+            for key, v in zip(("min", "max", "mean", "sd", "del2"), st[:5]):
+                res["dynstat_%s_%s" % (name, key)] = float(v)
+        res["cg2d_init_res"] = self.get("firstResidual")
+        res["cg2d_iters"] = int(self.get("numIters"))
+        res["cg2d_last_res"] = self.get("lastResidual")
+        res["cg2d_rhs_max"] = self.get("rhsMax")
+        return res
+
+
+GOLDEN = os.path.join(os.path.dirname(HERE), "tests", "golden")
+
+
+def read_bin(path, shape, dtype=">f4"):
+    return np.fromfile(path, dtype=dtype).astype(np.float64).reshape(shape)
+
+
+def gyre_oracle():
+    """verification/tutorial_barotropic_gyre as the oracle: input/data namelist
+    resolved with set_defaults.F / ini_parms.F (values pinned by params.json)."""
+    o = Oracle(62, 62, 2, 2, 1)
+    o.set(deltaTMom=1200.0, deltaTFreeSurf=1200.0, deltaTClock=1200.0, abEps=0.01,
+          viscAhD=400.0, viscAhZ=400.0, f0=1e-4, beta=1e-11, rhoConst=1000.0, gBaro=9.81,
+          cg2dTargetResidual=1e-7, cg2dMaxIters=1000, cg2dUseMinResSol=0,
+          xgOrigin=-20e3, ygOrigin=-20e3, selectCoriScheme=0, momForcingOutAB=0)
+    o.arr("delX")[:] = 20e3
+    o.arr("delY")[:] = 20e3
+    o.arr("drF")[0] = 5000.0
+    o.ini_grid()
+    d = os.path.join(GOLDEN, "tutorial_barotropic_gyre")
+    o.ini_depths(read_bin(os.path.join(d, "bathy.bin"), (62, 62)))
+    o.ini_cg2d()
+    fu = read_bin(os.path.join(d, "windx_cosy.bin"), (62, 62))
+    F = o.arr("fu")
+    F[0, o.OLy:o.OLy + 62, o.OLx:o.OLx + 62] = fu
+    o.L.oracle_exch_xy(o.h, _dp(o.arr("fu")))
+    o.arr("theta")[:] = 20.0
+    o.arr("salt")[:] = 30.0
+    return o

@@ -1,0 +1,446 @@
+/*
+ * model.c -- oracle state, parameters, exchanges and grid/mask initialisation.
+ * TEST INFRASTRUCTURE (see oracle.h): never linked into the product.
+ */
+#include "oracle.h"
+#include <math.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+static double *zalloc(long n) { return (double *)calloc((size_t)(n > 0 ? n : 1), sizeof(double)); }
+static int *izalloc(long n) { return (int *)calloc((size_t)(n > 0 ? n : 1), sizeof(int)); }
+
+OModel *oracle_new(int sNx, int sNy, int OLx, int OLy, int Nr, int nSx, int nSy) {
+  OModel *m = (OModel *)calloc(1, sizeof(OModel));
+  m->sNx = sNx; m->sNy = sNy; m->OLx = OLx; m->OLy = OLy; m->Nr = Nr;
+  m->nSx = nSx; m->nSy = nSy; m->nTiles = nSx * nSy;
+  m->nx = sNx + 2 * OLx; m->ny = sNy + 2 * OLy;
+  m->n2 = (long)m->nx * m->ny; m->n3 = m->n2 * Nr;
+  long N2 = m->n2 * m->nTiles, N3 = m->n3 * m->nTiles;
+  int Nx = sNx * nSx, Ny = sNy * nSy;
+  /* defaults of set_defaults.F / ini_parms.F resolution for the supported subset */
+  m->abEps = 0.01; m->gravity = 9.81; m->rhoNil = 999.8; m->rhoConst = 999.8; m->gBaro = 9.81;
+  m->f0 = 1.e-4; m->beta = 1.e-11; m->sideDragFactor = 2.0;
+  m->cg2dTargetResWunit = -1.0; m->cg2dpcOffDFac = 0.51; m->cg2dMaxIters = 150;
+  m->freeSurfFac = 1.0; m->implicSurfPress = 1.0; m->implicDiv2DFlow = 1.0; m->rkSign = -1.0;
+  m->afFacMom = m->vfFacMom = m->pfFacMom = m->cfFacMom = m->foFacMom = m->mtFacMom = 1.0;
+  m->hFacMin = 1.0; m->hFacMinDr = 0.0;
+  m->momAdvection = m->momViscosity = m->momForcing = m->useCoriolis = 1;
+  m->no_slip_sides = 1; m->no_slip_bottom = 1; m->momDissip_In_AB = 1; m->momForcingOutAB = 0;
+  m->useHarmonicVisc = 1; m->selectCoriMap = 1; m->usingCartesianGrid = 1;
+
+  m->drF = zalloc(Nr + 1); m->drC = zalloc(Nr + 1); m->rF = zalloc(Nr + 1); m->rC = zalloc(Nr + 1);
+  m->recip_drF = zalloc(Nr + 1); m->recip_drC = zalloc(Nr + 1);
+  m->delX = zalloc(Nx); m->delY = zalloc(Ny);
+#define A2(f) m->f = zalloc(N2)
+  A2(xC); A2(yC); A2(xG); A2(yG); A2(dxF); A2(dyF); A2(dxG); A2(dyG); A2(dxC); A2(dyC); A2(dxV); A2(dyU);
+  A2(rA); A2(rAw); A2(rAs); A2(rAz);
+  A2(recip_dxF); A2(recip_dyF); A2(recip_dxG); A2(recip_dyG); A2(recip_dxC); A2(recip_dyC);
+  A2(recip_dxV); A2(recip_dyU); A2(recip_rA); A2(recip_rAw); A2(recip_rAs); A2(recip_rAz);
+  A2(fCori); A2(fCoriG); A2(Bo_surf); A2(recip_Bo); A2(R_low); A2(Ro_surf);
+  A2(maskInC); A2(maskInW); A2(maskInS);
+  A2(aW2d); A2(aS2d); A2(aC2d); A2(pW); A2(pS); A2(pC);
+  A2(etaN); A2(fu); A2(fv); A2(surfaceForcingU); A2(surfaceForcingV);
+#undef A2
+  m->kSurfC = izalloc(N2); m->kSurfW = izalloc(N2); m->kSurfS = izalloc(N2); m->kLowC = izalloc(N2);
+#define A3(f) m->f = zalloc(N3)
+  A3(hFacC); A3(hFacW); A3(hFacS); A3(recip_hFacC); A3(recip_hFacW); A3(recip_hFacS);
+  A3(maskC); A3(maskW); A3(maskS);
+  A3(uVel); A3(vVel); A3(wVel); A3(theta); A3(salt); A3(gU); A3(gV); A3(guNm1); A3(gvNm1);
+#undef A3
+  return m;
+}
+
+void oracle_free(OModel *m) {
+  if (!m) return;
+  double **dp[] = {&m->drF, &m->drC, &m->rF, &m->rC, &m->recip_drF, &m->recip_drC, &m->delX, &m->delY,
+                   &m->xC, &m->yC, &m->xG, &m->yG, &m->dxF, &m->dyF, &m->dxG, &m->dyG, &m->dxC, &m->dyC,
+                   &m->dxV, &m->dyU, &m->rA, &m->rAw, &m->rAs, &m->rAz, &m->recip_dxF, &m->recip_dyF,
+                   &m->recip_dxG, &m->recip_dyG, &m->recip_dxC, &m->recip_dyC, &m->recip_dxV,
+                   &m->recip_dyU, &m->recip_rA, &m->recip_rAw, &m->recip_rAs, &m->recip_rAz,
+                   &m->fCori, &m->fCoriG, &m->Bo_surf, &m->recip_Bo, &m->R_low, &m->Ro_surf,
+                   &m->maskInC, &m->maskInW, &m->maskInS, &m->aW2d, &m->aS2d, &m->aC2d, &m->pW,
+                   &m->pS, &m->pC, &m->etaN, &m->fu, &m->fv, &m->surfaceForcingU,
+                   &m->surfaceForcingV, &m->hFacC, &m->hFacW, &m->hFacS, &m->recip_hFacC,
+                   &m->recip_hFacW, &m->recip_hFacS, &m->maskC, &m->maskW, &m->maskS, &m->uVel,
+                   &m->vVel, &m->wVel, &m->theta, &m->salt, &m->gU, &m->gV, &m->guNm1, &m->gvNm1};
+  for (size_t i = 0; i < sizeof(dp) / sizeof(dp[0]); i++) free(*dp[i]);
+  free(m->kSurfC); free(m->kSurfW); free(m->kSurfS); free(m->kLowC);
+  free(m);
+}
+
+/* ------------------------------------------------------------------ params */
+typedef struct { const char *name; size_t off; int isint; } PDesc;
+#define PD(f) {#f, offsetof(OModel, f), 0}
+#define PI_(f) {#f, offsetof(OModel, f), 1}
+static const PDesc PTAB[] = {
+  PD(deltaTMom), PD(deltaTFreeSurf), PD(deltaTClock), PD(abEps), PD(gBaro), PD(gravity),
+  PD(rhoConst), PD(rhoNil), PD(f0), PD(beta), PD(viscAhD), PD(viscAhZ), PD(viscA4D), PD(viscA4Z),
+  PD(viscAr), PD(sideDragFactor), PD(cg2dTargetResidual), PD(cg2dTargetResWunit), PD(cg2dpcOffDFac),
+  PD(freeSurfFac), PD(implicSurfPress), PD(implicDiv2DFlow), PD(rkSign), PD(afFacMom), PD(vfFacMom),
+  PD(pfFacMom), PD(cfFacMom), PD(foFacMom), PD(mtFacMom), PD(hFacMin), PD(hFacMinDr), PD(xgOrigin),
+  PD(ygOrigin), PD(cg2dNorm), PD(cg2dTolerance_sq), PD(globalArea), PD(myTime),
+  PD(firstResidual), PD(minResidualSq), PD(lastResidual), PD(sumRHS), PD(rhsMax),
+  PI_(momAdvection), PI_(momViscosity), PI_(momForcing), PI_(useCoriolis), PI_(no_slip_sides),
+  PI_(no_slip_bottom), PI_(selectCoriScheme), PI_(momForcingOutAB), PI_(momDissip_In_AB),
+  PI_(useHarmonicVisc), PI_(useBiharmonicVisc), PI_(implicitViscosity), PI_(selectCoriMap),
+  PI_(cg2dMaxIters), PI_(cg2dUseMinResSol), PI_(exactConserv), PI_(nIter0), PI_(usingCartesianGrid),
+  PI_(cg2dNormaliseRHS), PI_(myIter), PI_(numIters), PI_(nIterMin),
+};
+#undef PD
+#undef PI_
+
+int oracle_set_param(OModel *m, const char *name, double value) {
+  for (size_t i = 0; i < sizeof(PTAB) / sizeof(PTAB[0]); i++)
+    if (!strcmp(PTAB[i].name, name)) {
+      char *p = (char *)m + PTAB[i].off;
+      if (PTAB[i].isint) *(int *)p = (int)value; else *(double *)p = value;
+      return 0;
+    }
+  fprintf(stderr, "oracle_set_param: unknown parameter %s\n", name);
+  return -1;
+}
+
+double oracle_get_param(OModel *m, const char *name) {
+  for (size_t i = 0; i < sizeof(PTAB) / sizeof(PTAB[0]); i++)
+    if (!strcmp(PTAB[i].name, name)) {
+      char *p = (char *)m + PTAB[i].off;
+      return PTAB[i].isint ? (double)*(int *)p : *(double *)p;
+    }
+  fprintf(stderr, "oracle_get_param: unknown parameter %s\n", name);
+  return NAN;
+}
+
+double *oracle_array(OModel *m, const char *name, long *count) {
+  long N2 = m->n2 * m->nTiles, N3 = m->n3 * m->nTiles;
+  struct { const char *n; double *p; long c; } t[] = {
+    {"drF", m->drF, m->Nr + 1}, {"drC", m->drC, m->Nr + 1}, {"rF", m->rF, m->Nr + 1},
+    {"rC", m->rC, m->Nr + 1}, {"recip_drF", m->recip_drF, m->Nr + 1},
+    {"delX", m->delX, (long)m->sNx * m->nSx}, {"delY", m->delY, (long)m->sNy * m->nSy},
+    {"xC", m->xC, N2}, {"yC", m->yC, N2}, {"xG", m->xG, N2}, {"yG", m->yG, N2},
+    {"dxF", m->dxF, N2}, {"dyF", m->dyF, N2}, {"dxG", m->dxG, N2}, {"dyG", m->dyG, N2},
+    {"dxC", m->dxC, N2}, {"dyC", m->dyC, N2}, {"dxV", m->dxV, N2}, {"dyU", m->dyU, N2},
+    {"rA", m->rA, N2}, {"rAw", m->rAw, N2}, {"rAs", m->rAs, N2}, {"rAz", m->rAz, N2},
+    {"recip_dxC", m->recip_dxC, N2}, {"recip_dyC", m->recip_dyC, N2},
+    {"recip_dxF", m->recip_dxF, N2}, {"recip_dyF", m->recip_dyF, N2},
+    {"recip_dxG", m->recip_dxG, N2}, {"recip_dyG", m->recip_dyG, N2},
+    {"recip_dxV", m->recip_dxV, N2}, {"recip_dyU", m->recip_dyU, N2},
+    {"recip_rA", m->recip_rA, N2}, {"recip_rAw", m->recip_rAw, N2}, {"recip_rAs", m->recip_rAs, N2},
+    {"fCori", m->fCori, N2}, {"fCoriG", m->fCoriG, N2}, {"Bo_surf", m->Bo_surf, N2},
+    {"recip_Bo", m->recip_Bo, N2}, {"R_low", m->R_low, N2}, {"Ro_surf", m->Ro_surf, N2},
+    {"maskInC", m->maskInC, N2}, {"maskInW", m->maskInW, N2}, {"maskInS", m->maskInS, N2},
+    {"aW2d", m->aW2d, N2}, {"aS2d", m->aS2d, N2}, {"aC2d", m->aC2d, N2},
+    {"pW", m->pW, N2}, {"pS", m->pS, N2}, {"pC", m->pC, N2},
+    {"etaN", m->etaN, N2}, {"fu", m->fu, N2}, {"fv", m->fv, N2},
+    {"hFacC", m->hFacC, N3}, {"hFacW", m->hFacW, N3}, {"hFacS", m->hFacS, N3},
+    {"recip_hFacC", m->recip_hFacC, N3}, {"recip_hFacW", m->recip_hFacW, N3},
+    {"recip_hFacS", m->recip_hFacS, N3},
+    {"maskC", m->maskC, N3}, {"maskW", m->maskW, N3}, {"maskS", m->maskS, N3},
+    {"uVel", m->uVel, N3}, {"vVel", m->vVel, N3}, {"wVel", m->wVel, N3},
+    {"theta", m->theta, N3}, {"salt", m->salt, N3}, {"gU", m->gU, N3}, {"gV", m->gV, N3},
+    {"guNm1", m->guNm1, N3}, {"gvNm1", m->gvNm1, N3},
+  };
+  for (size_t i = 0; i < sizeof(t) / sizeof(t[0]); i++)
+    if (!strcmp(t[i].n, name)) { if (count) *count = t[i].c; return t[i].p; }
+  fprintf(stderr, "oracle_array: unknown array %s\n", name);
+  if (count) *count = 0;
+  return NULL;
+}
+
+int *oracle_iarray(OModel *m, const char *name, long *count) {
+  long N2 = m->n2 * m->nTiles;
+  if (count) *count = N2;
+  if (!strcmp(name, "kSurfC")) return m->kSurfC;
+  if (!strcmp(name, "kSurfW")) return m->kSurfW;
+  if (!strcmp(name, "kSurfS")) return m->kSurfS;
+  if (!strcmp(name, "kLowC")) return m->kLowC;
+  if (count) *count = 0;
+  return NULL;
+}
+
+/* ------------------------------------------------------------- exchanges */
+/* EXCH1_RX (eesupp/src/exch1_rx.template:8-276): lat-lon, periodic in both
+ * directions over the nSx x nSy tile layout.  X pass fills W/E halos of the
+ * interior rows, Y pass fills S/N halos over the full width (corners
+ * included, :170-198).  For a periodic lat-lon layout this equals copying,
+ * for every halo point, the interior point of the wrapped global index. */
+void oracle_exch_xyz(OModel *m, double *a, int nz) {
+  const int sNx = m->sNx, sNy = m->sNy, OLx = m->OLx, OLy = m->OLy;
+  const int Nx = sNx * m->nSx, Ny = sNy * m->nSy;
+  for (int t = 0; t < m->nTiles; t++) {
+    int bi = t % m->nSx, bj = t / m->nSx;
+    for (int k = 1; k <= nz; k++)
+      for (int j = 1 - OLy; j <= sNy + OLy; j++)
+        for (int i = 1 - OLx; i <= sNx + OLx; i++) {
+          if (i >= 1 && i <= sNx && j >= 1 && j <= sNy) continue;
+          int iG = bi * sNx + i - 1, jG = bj * sNy + j - 1;
+          iG = ((iG % Nx) + Nx) % Nx; jG = ((jG % Ny) + Ny) % Ny;
+          int st = (jG / sNy) * m->nSx + iG / sNx;
+          int si = iG % sNx + 1, sj = jG % sNy + 1;
+          long dst = (long)(i + OLx - 1) + (long)(j + OLy - 1) * m->nx + (long)(k - 1) * m->n2 +
+                     (long)t * m->n2 * nz;
+          long src = (long)(si + OLx - 1) + (long)(sj + OLy - 1) * m->nx + (long)(k - 1) * m->n2 +
+                     (long)st * m->n2 * nz;
+          a[dst] = a[src];
+        }
+  }
+}
+void oracle_exch_xy(OModel *m, double *a) { oracle_exch_xyz(m, a, 1); }
+
+/* ---------------------------------------------------------- grid & masks */
+int oracle_ini_grid(OModel *m) {
+  const int sNx = m->sNx, sNy = m->sNy, OLx = m->OLx, OLy = m->OLy, Nr = m->Nr;
+  const int Nx = sNx * m->nSx, Ny = sNy * m->nSy;
+  if (!m->usingCartesianGrid) { fprintf(stderr, "oracle: only usingCartesianGrid supported\n"); return -1; }
+  /* INI_VERTICAL_GRID (model/src/ini_vertical_grid.F): drF=delR, drC, rF, rC */
+  m->drC[0] = 0.5 * m->drF[0];
+  for (int k = 2; k <= Nr; k++) m->drC[k - 1] = 0.5 * (m->drF[k - 2] + m->drF[k - 1]);
+  m->drC[Nr] = 0.5 * m->drF[Nr - 1];
+  m->rF[0] = 0.0; /* seaLev_Z */
+  for (int k = 1; k <= Nr; k++) m->rF[k] = m->rF[k - 1] + m->rkSign * m->drF[k - 1];
+  m->rC[0] = m->rF[0] + m->rkSign * m->drC[0];
+  for (int k = 2; k <= Nr; k++) m->rC[k - 1] = m->rC[k - 2] + m->rkSign * m->drC[k - 1];
+  for (int k = 0; k <= Nr; k++) m->recip_drC[k] = 1.0 / m->drC[k];
+  for (int k = 0; k < Nr; k++) m->recip_drF[k] = 1.0 / m->drF[k];
+
+  for (int t = 0; t < m->nTiles; t++) {
+    int bi = t % m->nSx, bj = t / m->nSx;
+    /* INI_LOCAL_GRID (model/src/ini_local_grid.F): extrapolated corner coords, periodic spacing */
+    int iG0 = bi * sNx, jG0 = bj * sNy;
+    double xG0 = m->xgOrigin, yG0 = m->ygOrigin;
+    for (int i = 1; i <= iG0; i++) xG0 += m->delX[i - 1];
+    for (int i = 1; i <= OLx; i++) xG0 -= m->delX[(iG0 - i + OLx * Nx) % Nx];
+    for (int j = 1; j <= jG0; j++) yG0 += m->delY[j - 1];
+    for (int j = 1; j <= OLy; j++) yG0 -= m->delY[(jG0 - j + OLy * Ny) % Ny];
+    int nxl = sNx + 2 * OLx + 2, nyl = sNy + 2 * OLy + 2;
+    double *dXl = zalloc(nxl), *dYl = zalloc(nyl);          /* index i -> i+OLx */
+    double *xGl = zalloc((long)nxl * nyl), *yGl = zalloc((long)nxl * nyl);
+#define DXL(i) dXl[(i) + OLx]
+#define DYL(j) dYl[(j) + OLy]
+#define XGL(i, j) xGl[((i) + OLx) + ((j) + OLy) * nxl]
+#define YGL(i, j) yGl[((i) + OLx) + ((j) + OLy) * nxl]
+    for (int i = -OLx; i <= sNx + OLx; i++) DXL(i) = m->delX[(iG0 + i - 1 + OLx * Nx) % Nx];
+    for (int j = -OLy; j <= sNy + OLy; j++) DYL(j) = m->delY[(jG0 + j - 1 + OLy * Ny) % Ny];
+    for (int j = 1 - OLy; j <= sNy + OLy + 1; j++) {
+      XGL(1 - OLx, j) = xG0;
+      for (int i = 1 - OLx; i <= sNx + OLx; i++) XGL(i + 1, j) = XGL(i, j) + DXL(i);
+    }
+    for (int i = 1 - OLx; i <= sNx + OLx + 1; i++) {
+      YGL(i, 1 - OLy) = yG0;
+      for (int j = 1 - OLy; j <= sNy + OLy; j++) YGL(i, j + 1) = YGL(i, j) + DYL(j);
+    }
+    /* INI_CARTESIAN_GRID (model/src/ini_cartesian_grid.F) */
+    for (int j = 1 - OLy; j <= sNy + OLy; j++)
+      for (int i = 1 - OLx; i <= sNx + OLx; i++) {
+        long p = O2(m, i, j, t);
+        m->xG[p] = XGL(i, j); m->yG[p] = YGL(i, j);
+        m->xC[p] = 0.25 * (XGL(i, j) + XGL(i + 1, j) + XGL(i, j + 1) + XGL(i + 1, j + 1));
+        m->yC[p] = 0.25 * (YGL(i, j) + YGL(i + 1, j) + YGL(i, j + 1) + YGL(i + 1, j + 1));
+        m->dxF[p] = DXL(i); m->dyF[p] = DYL(j);
+        m->dxG[p] = DXL(i); m->dyG[p] = DYL(j);
+      }
+    for (int j = 1 - OLy; j <= sNy + OLy; j++)
+      for (int i = 2 - OLx; i <= sNx + OLx; i++)
+        m->dxC[O2(m, i, j, t)] = 0.5 * (m->dxF[O2(m, i, j, t)] + m->dxF[O2(m, i - 1, j, t)]);
+    for (int j = 2 - OLy; j <= sNy + OLy; j++)
+      for (int i = 1 - OLx; i <= sNx + OLx; i++)
+        m->dyC[O2(m, i, j, t)] = 0.5 * (m->dyF[O2(m, i, j, t)] + m->dyF[O2(m, i, j - 1, t)]);
+    for (int j = 2 - OLy; j <= sNy + OLy; j++)
+      for (int i = 2 - OLx; i <= sNx + OLx; i++) {
+        m->dxV[O2(m, i, j, t)] = 0.5 * (m->dxG[O2(m, i, j, t)] + m->dxG[O2(m, i - 1, j, t)]);
+        m->dyU[O2(m, i, j, t)] = 0.5 * (m->dyG[O2(m, i, j, t)] + m->dyG[O2(m, i, j - 1, t)]);
+      }
+    for (int j = 1 - OLy; j <= sNy + OLy; j++)
+      for (int i = 1 - OLx; i <= sNx + OLx; i++) {
+        long p = O2(m, i, j, t);
+        m->rA[p] = m->dxF[p] * m->dyF[p];
+        m->rAw[p] = m->dxC[p] * m->dyG[p];
+        m->rAs[p] = m->dxG[p] * m->dyC[p];
+        m->rAz[p] = m->dxV[p] * m->dyU[p];
+      }
+#undef DXL
+#undef DYL
+#undef XGL
+#undef YGL
+    free(dXl); free(dYl); free(xGl); free(yGl);
+    /* INI_GRID reciprocals (model/src/ini_grid.F): 1/x where x != 0 else 0 */
+    for (long p = O2(m, 1 - OLx, 1 - OLy, t); p < (long)(t + 1) * m->n2; p++) {
+#define RCP(a) m->recip_##a[p] = (m->a[p] != 0.0) ? 1.0 / m->a[p] : 0.0
+      RCP(dxG); RCP(dyG); RCP(dxC); RCP(dyC); RCP(dxF); RCP(dyF); RCP(dxV); RCP(dyU);
+      RCP(rA); RCP(rAs); RCP(rAw); RCP(rAz);
+#undef RCP
+    }
+    /* INI_CORI selectCoriMap=1 (model/src/ini_cori.F): beta plane on yC / yG */
+    for (long p = O2(m, 1 - OLx, 1 - OLy, t); p < (long)(t + 1) * m->n2; p++) {
+      if (m->selectCoriMap == 1) {
+        m->fCori[p] = m->f0 + m->beta * m->yC[p];
+        m->fCoriG[p] = m->f0 + m->beta * m->yG[p];
+      } else if (m->selectCoriMap == 0) {
+        m->fCori[p] = m->f0; m->fCoriG[p] = m->f0;
+      } else {
+        m->fCori[p] = 0.0; m->fCoriG[p] = 0.0;
+      }
+    }
+  }
+  return 0;
+}
+
+/* INI_DEPTHS (model/src/ini_depths.F:91-179) + INI_MASKS_ETC
+ * (model/src/ini_masks_etc.F) + INI_LINEAR_PHISURF (ini_linear_phisurf.F:78-88).
+ * bathyGlobal: Nx*Ny (i fastest), negative below sea level. */
+int oracle_ini_depths(OModel *m, const double *bathyGlobal) {
+  const int sNx = m->sNx, sNy = m->sNy, OLx = m->OLx, OLy = m->OLy, Nr = m->Nr;
+  const int Nx = sNx * m->nSx;
+  const double zero = 0.0, one = 1.0, half = 0.5;
+  long N2 = m->n2 * m->nTiles;
+  for (long p = 0; p < N2; p++) { m->R_low[p] = 0.0; m->Ro_surf[p] = 0.0; }
+  for (int t = 0; t < m->nTiles; t++) {
+    int bi = t % m->nSx, bj = t / m->nSx;
+    for (int j = 1; j <= sNy; j++)
+      for (int i = 1; i <= sNx; i++) {
+        m->R_low[O2(m, i, j, t)] = bathyGlobal[(long)(bj * sNy + j - 1) * Nx + bi * sNx + i - 1];
+        m->Ro_surf[O2(m, i, j, t)] = m->rF[0];
+      }
+  }
+  oracle_exch_xy(m, m->R_low);
+  oracle_exch_xy(m, m->Ro_surf);
+
+  double *rLowW = zalloc(N2), *rLowS = zalloc(N2), *rSurfW = zalloc(N2), *rSurfS = zalloc(N2);
+  double *tmp = zalloc(m->n2);
+  const double rEmpty = m->rF[0];
+  for (int t = 0; t < m->nTiles; t++) {
+    /* ini_masks_etc.F: rLowW/S, rSurfW/S before hFacC adjustments */
+    for (int j = 1 - OLy; j <= sNy + OLy; j++) {
+      rLowW[O2(m, 1 - OLx, j, t)] = rEmpty; rSurfW[O2(m, 1 - OLx, j, t)] = rEmpty;
+    }
+    for (int i = 1 - OLx; i <= sNx + OLx; i++) {
+      rLowS[O2(m, i, 1 - OLy, t)] = rEmpty; rSurfS[O2(m, i, 1 - OLy, t)] = rEmpty;
+    }
+    for (int j = 1 - OLy; j <= sNy + OLy; j++)
+      for (int i = 2 - OLx; i <= sNx + OLx; i++) {
+        rLowW[O2(m, i, j, t)] = fmax(m->R_low[O2(m, i - 1, j, t)], m->R_low[O2(m, i, j, t)]);
+        rSurfW[O2(m, i, j, t)] = fmin(m->Ro_surf[O2(m, i - 1, j, t)], m->Ro_surf[O2(m, i, j, t)]);
+      }
+    for (int j = 2 - OLy; j <= sNy + OLy; j++)
+      for (int i = 1 - OLx; i <= sNx + OLx; i++) {
+        rLowS[O2(m, i, j, t)] = fmax(m->R_low[O2(m, i, j - 1, t)], m->R_low[O2(m, i, j, t)]);
+        rSurfS[O2(m, i, j, t)] = fmin(m->Ro_surf[O2(m, i, j - 1, t)], m->Ro_surf[O2(m, i, j, t)]);
+      }
+    /* hFacC from R_low */
+    for (int k = 1; k <= Nr; k++) {
+      double hFacMnSz = fmax(m->hFacMin, fmin(m->hFacMinDr * m->recip_drF[k - 1], one));
+      for (int j = 1 - OLy; j <= sNy + OLy; j++)
+        for (int i = 1 - OLx; i <= sNx + OLx; i++) {
+          long p = O2(m, i, j, t);
+          double hl = (m->rF[k - 1] - m->R_low[p]) * m->recip_drF[k - 1];
+          hl = fmin(fmax(hl, zero), one);
+          m->hFacC[O3(m, i, j, k, t)] =
+              (hl < hFacMnSz * half || m->R_low[p] >= m->Ro_surf[p]) ? zero : fmax(hl, hFacMnSz);
+        }
+    }
+    for (long q = 0; q < m->n2; q++) tmp[q] = 0.0;
+    for (int k = 1; k <= Nr; k++)
+      for (int j = 1 - OLy; j <= sNy + OLy; j++)
+        for (int i = 1 - OLx; i <= sNx + OLx; i++)
+          tmp[O2(m, i, j, 0)] += m->drF[k - 1] * m->hFacC[O3(m, i, j, k, t)];
+    for (int j = 1 - OLy; j <= sNy + OLy; j++)
+      for (int i = 1 - OLx; i <= sNx + OLx; i++)
+        m->R_low[O2(m, i, j, t)] = m->rF[0] - tmp[O2(m, i, j, 0)];
+    /* adjust hFacC at the surface from Ro_surf */
+    for (int k = 1; k <= Nr; k++) {
+      double hFacMnSz = fmax(m->hFacMin, fmin(m->hFacMinDr * m->recip_drF[k - 1], one));
+      for (int j = 1 - OLy; j <= sNy + OLy; j++)
+        for (int i = 1 - OLx; i <= sNx + OLx; i++) {
+          long p3 = O3(m, i, j, k, t);
+          double hl = (m->rF[k - 1] - m->Ro_surf[O2(m, i, j, t)]) * m->recip_drF[k - 1];
+          hl = m->hFacC[p3] - fmax(hl, zero);
+          hl = fmax(hl, zero);
+          m->hFacC[p3] = (hl < hFacMnSz * half) ? zero : fmax(hl, hFacMnSz);
+        }
+    }
+    for (long q = 0; q < m->n2; q++) tmp[q] = 0.0;
+    for (int j = 1 - OLy; j <= sNy + OLy; j++)
+      for (int i = 1 - OLx; i <= sNx + OLx; i++) {
+        m->kSurfC[O2(m, i, j, t)] = Nr + 1; m->kLowC[O2(m, i, j, t)] = 0;
+      }
+    for (int k = 1; k <= Nr; k++)
+      for (int j = 1 - OLy; j <= sNy + OLy; j++)
+        for (int i = 1 - OLx; i <= sNx + OLx; i++) {
+          tmp[O2(m, i, j, 0)] += m->drF[k - 1] * m->hFacC[O3(m, i, j, k, t)];
+          if (m->hFacC[O3(m, i, j, k, t)] != zero) m->kLowC[O2(m, i, j, t)] = k;
+        }
+    for (int k = Nr; k >= 1; k--)
+      for (int j = 1 - OLy; j <= sNy + OLy; j++)
+        for (int i = 1 - OLx; i <= sNx + OLx; i++)
+          if (m->hFacC[O3(m, i, j, k, t)] != zero) m->kSurfC[O2(m, i, j, t)] = k;
+    for (int j = 1 - OLy; j <= sNy + OLy; j++)
+      for (int i = 1 - OLx; i <= sNx + OLx; i++) {
+        long p = O2(m, i, j, t);
+        m->Ro_surf[p] = m->R_low[p] + tmp[O2(m, i, j, 0)];
+        m->maskInC[p] = (m->kSurfC[p] <= Nr) ? 1.0 : 0.0;
+      }
+    /* hFacW, hFacS (useMin4hFacEdges = .FALSE. branch) */
+    for (int k = 1; k <= Nr; k++) {
+      double hFacMnSz = fmax(m->hFacMin, fmin(m->hFacMinDr * m->recip_drF[k - 1], one));
+      for (int j = 1 - OLy; j <= sNy + OLy; j++)
+        for (int i = 1 - OLx; i <= sNx + OLx; i++) {
+          long p = O2(m, i, j, t);
+          double h1 = (m->rF[k - 1] - rLowW[p]) * m->recip_drF[k - 1];
+          double hl = fmin(h1, one);
+          h1 = (hl < hFacMnSz * half || rLowW[p] >= rSurfW[p]) ? 0.0 : fmax(hl, hFacMnSz);
+          double h2 = (m->rF[k - 1] - rSurfW[p]) * m->recip_drF[k - 1];
+          hl = h1 - fmax(h2, zero);
+          m->hFacW[O3(m, i, j, k, t)] = (hl < hFacMnSz * half) ? zero : fmax(hl, hFacMnSz);
+          h1 = (m->rF[k - 1] - rLowS[p]) * m->recip_drF[k - 1];
+          hl = fmin(h1, one);
+          h1 = (hl < hFacMnSz * half || rLowS[p] >= rSurfS[p]) ? 0.0 : fmax(hl, hFacMnSz);
+          h2 = (m->rF[k - 1] - rSurfS[p]) * m->recip_drF[k - 1];
+          hl = h1 - fmax(h2, zero);
+          m->hFacS[O3(m, i, j, k, t)] = (hl < hFacMnSz * half) ? zero : fmax(hl, hFacMnSz);
+        }
+    }
+  }
+  oracle_exch_xyz(m, m->hFacW, Nr);
+  oracle_exch_xyz(m, m->hFacS, Nr);
+  for (int t = 0; t < m->nTiles; t++) {
+    for (int j = 1 - OLy; j <= sNy + OLy; j++)
+      for (int i = 1 - OLx; i <= sNx + OLx; i++) {
+        long p = O2(m, i, j, t);
+        m->kSurfW[p] = Nr + 1; m->kSurfS[p] = Nr + 1;
+        for (int k = Nr; k >= 1; k--) {
+          if (m->hFacW[O3(m, i, j, k, t)] != zero) m->kSurfW[p] = k;
+          if (m->hFacS[O3(m, i, j, k, t)] != zero) m->kSurfS[p] = k;
+        }
+        m->maskInW[p] = (m->kSurfW[p] <= Nr) ? one : zero;
+        m->maskInS[p] = (m->kSurfS[p] <= Nr) ? one : zero;
+      }
+    for (int k = 1; k <= Nr; k++)
+      for (int j = 1 - OLy; j <= sNy + OLy; j++)
+        for (int i = 1 - OLx; i <= sNx + OLx; i++) {
+          long p = O3(m, i, j, k, t);
+#define RM(c)                                                   \
+  if (m->hFac##c[p] != zero) { m->recip_hFac##c[p] = 1.0 / m->hFac##c[p]; m->mask##c[p] = one; } \
+  else { m->recip_hFac##c[p] = zero; m->mask##c[p] = zero; }
+          RM(C) RM(W) RM(S)
+#undef RM
+        }
+    /* INI_LINEAR_PHISURF, z-coordinates */
+    for (int j = 1 - OLy; j <= sNy + OLy; j++)
+      for (int i = 1 - OLx; i <= sNx + OLx; i++) {
+        m->Bo_surf[O2(m, i, j, t)] = m->gBaro;
+        m->recip_Bo[O2(m, i, j, t)] = 1.0 / m->gBaro;
+      }
+  }
+  /* globalArea (ini_masks_etc / ini_global_domain): sum rA*maskInC over interior, tile order */
+  double ga = 0.0;
+  for (int t = 0; t < m->nTiles; t++) {
+    double tileA = 0.0;
+    for (int j = 1; j <= sNy; j++)
+      for (int i = 1; i <= sNx; i++) tileA += m->rA[O2(m, i, j, t)] * m->maskInC[O2(m, i, j, t)];
+    ga += tileA;
+  }
+  m->globalArea = ga;
+  free(rLowW); free(rLowS); free(rSurfW); free(rSurfS); free(tmp);
+  return 0;
+}

@@ -1,0 +1,125 @@
+/*
+ * oracle.h -- CPU restatement of MITgcm's dynamical hot path (TEST INFRASTRUCTURE).
+ *
+ * This directory is the parity CHECKER, never the product: only tests/,
+ * __graft_entry__.smoke() and bench.py's cpu_baseline leg may load it.
+ * Every routine restates the reference Fortran loop-for-loop (same index
+ * ranges, same evaluation order, no FMA contraction: build with
+ * -ffp-contract=off) and cites the file:line under /root/reference it follows.
+ *
+ * Parity pin: oracle_run_gyre() reproduces the committed %MON / cg2d_* lines of
+ * verification/tutorial_barotropic_gyre/results/output.txt (tests/test_oracle.py).
+ *
+ * Layout (identical to the reference, and to the device mirror):
+ *   2-D field  a(i,j,tile)    i in 1-OLx..sNx+OLx fastest, then j, then tile
+ *   3-D field  a(i,j,k,tile)  i fastest, then j, then k, then tile
+ * Multiplications by the deep-atmosphere / anelastic factors (deepFac*,
+ * rhoFac*) are dropped: they are exactly 1.0 for every supported config, so
+ * dropping them is bit-exact.
+ */
+#ifndef MITGCM_ORACLE_H
+#define MITGCM_ORACLE_H
+#include <stddef.h>
+
+typedef struct OModel {
+  /* --- sizes (SIZE.h) --- */
+  int sNx, sNy, OLx, OLy, Nr, nSx, nSy, nTiles;
+  int nx, ny;          /* halo-inclusive tile extents */
+  long n2, n3;         /* points per tile: 2-D, 3-D */
+
+  /* --- run-time parameters (PARAMS.h), already resolved as ini_parms.F does --- */
+  double deltaTMom, deltaTFreeSurf, deltaTClock, abEps;
+  double gBaro, gravity, rhoConst, rhoNil, f0, beta;
+  double viscAhD, viscAhZ, viscA4D, viscA4Z, viscAr, sideDragFactor;
+  double cg2dTargetResidual, cg2dTargetResWunit, cg2dpcOffDFac;
+  double freeSurfFac, implicSurfPress, implicDiv2DFlow, rkSign;
+  double afFacMom, vfFacMom, pfFacMom, cfFacMom, foFacMom, mtFacMom;
+  double hFacMin, hFacMinDr;
+  double xgOrigin, ygOrigin;
+  int momAdvection, momViscosity, momForcing, useCoriolis, no_slip_sides;
+  int no_slip_bottom, selectCoriScheme, momForcingOutAB, momDissip_In_AB;
+  int useHarmonicVisc, useBiharmonicVisc, implicitViscosity, selectCoriMap;
+  int cg2dMaxIters, cg2dUseMinResSol, exactConserv, nIter0;
+  int usingCartesianGrid;
+
+  /* --- vertical grid (GRID.h), 1-based in the reference; here [0..Nr] --- */
+  double *drF, *drC, *rF, *rC, *recip_drF, *recip_drC;
+  double *delX, *delY;   /* global spacing, length Nx / Ny */
+
+  /* --- horizontal grid, per tile 2-D (GRID.h) --- */
+  double *xC, *yC, *xG, *yG, *dxF, *dyF, *dxG, *dyG, *dxC, *dyC, *dxV, *dyU;
+  double *rA, *rAw, *rAs, *rAz;
+  double *recip_dxF, *recip_dyF, *recip_dxG, *recip_dyG, *recip_dxC, *recip_dyC;
+  double *recip_dxV, *recip_dyU, *recip_rA, *recip_rAw, *recip_rAs, *recip_rAz;
+  double *fCori, *fCoriG, *Bo_surf, *recip_Bo;
+  double *R_low, *Ro_surf, *maskInC, *maskInW, *maskInS;
+  int *kSurfC, *kSurfW, *kSurfS, *kLowC;
+
+  /* --- 3-D masks --- */
+  double *hFacC, *hFacW, *hFacS, *recip_hFacC, *recip_hFacW, *recip_hFacS;
+  double *maskC, *maskW, *maskS;
+
+  /* --- CG2D operator (CG2D.h) --- */
+  double *aW2d, *aS2d, *aC2d, *pW, *pS, *pC;
+  double cg2dNorm, cg2dTolerance_sq, globalArea;
+  int cg2dNormaliseRHS;
+
+  /* --- state (DYNVARS.h, FFIELDS.h, SURFACE.h) --- */
+  double *uVel, *vVel, *wVel, *theta, *salt, *etaN;
+  double *gU, *gV, *guNm1, *gvNm1;
+  double *fu, *fv, *surfaceForcingU, *surfaceForcingV;
+  int myIter;
+  double myTime;
+
+  /* --- outputs of the last SOLVE_FOR_PRESSURE --- */
+  double firstResidual, minResidualSq, lastResidual, sumRHS, rhsMax;
+  int numIters, nIterMin;
+} OModel;
+
+/* index helpers: Fortran (i,j[,k]) of tile t -> flat offset */
+#define O2(m, i, j, t) \
+  ((long)((i) + (m)->OLx - 1) + (long)((j) + (m)->OLy - 1) * (m)->nx + (long)(t) * (m)->n2)
+#define O3(m, i, j, k, t) \
+  ((long)((i) + (m)->OLx - 1) + (long)((j) + (m)->OLy - 1) * (m)->nx + \
+   (long)((k) - 1) * (m)->n2 + (long)(t) * (m)->n3)
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* construction / parameters / array access (ctypes-facing) */
+OModel *oracle_new(int sNx, int sNy, int OLx, int OLy, int Nr, int nSx, int nSy);
+void oracle_free(OModel *m);
+int oracle_set_param(OModel *m, const char *name, double value);
+double oracle_get_param(OModel *m, const char *name);
+double *oracle_array(OModel *m, const char *name, long *count);
+int *oracle_iarray(OModel *m, const char *name, long *count);
+
+/* initialisation (INITIALISE_FIXED / INITIALISE_VARIA subset) */
+int oracle_ini_grid(OModel *m);                      /* INI_VERTICAL_GRID + INI_CARTESIAN_GRID + INI_CORI */
+int oracle_ini_depths(OModel *m, const double *bathyGlobal); /* INI_DEPTHS + INI_MASKS_ETC + INI_LINEAR_PHISURF */
+int oracle_ini_cg2d(OModel *m);                      /* INI_CG2D */
+
+/* exchanges (EXCH1, lat-lon, periodic over the nSx x nSy tile layout) */
+void oracle_exch_xy(OModel *m, double *a);
+void oracle_exch_xyz(OModel *m, double *a, int nz);
+
+/* hot path */
+void oracle_dynamics(OModel *m);                     /* DYNAMICS  (dynamics.F:21)  */
+void oracle_solve_for_pressure(OModel *m);           /* SOLVE_FOR_PRESSURE (solve_for_pressure.F:7) */
+void oracle_cg2d(OModel *m, double *cg2d_b, double *cg2d_x,
+                 double *firstResidual, double *minResidualSq, double *lastResidual,
+                 int *numIters, int *nIterMin);      /* CG2D (cg2d.F:13) */
+void oracle_momentum_correction_step(OModel *m);     /* momentum_correction_step.F:7 */
+void oracle_integr_continuity(OModel *m);            /* integr_continuity.F:13 */
+void oracle_forward_step(OModel *m);                 /* forward_step.F:64 (supported subset) */
+
+/* monitor (pkg/monitor/mon_calc_stats_rl.F): out[6] = min,max,mean,sd,del2,vol */
+void oracle_mon_stats(OModel *m, const double *arr, int myNr, const double *arrhFac,
+                      int hfac3d, const double *arrMask, const double *arrArea,
+                      const double *arrDr, double out[6]);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,382 @@
+/*
+ * solver.c -- oracle restatement of the 2-D elliptic surface-pressure solve and
+ * the steps around it:
+ *   INI_CG2D               model/src/ini_cg2d.F:61-237
+ *   SOLVE_FOR_PRESSURE     model/src/solve_for_pressure.F:7-468
+ *   CALC_DIV_GHAT          model/src/calc_div_ghat.F:6-201
+ *   CG2D                   model/src/cg2d.F:13-415
+ *   GLOBAL_SUM_TILE_RL     eesupp/src/global_sum_tile.F:161-191 (fixed tile order)
+ *   MOMENTUM_CORRECTION_STEP / CORRECTION_STEP / CALC_GRAD_PHI_SURF
+ *   INTEGR_CONTINUITY / INTEGRATE_FOR_W
+ *   FORWARD_STEP (supported subset), MON_CALC_STATS_RL
+ * TEST INFRASTRUCTURE (see oracle.h).
+ */
+#include "oracle.h"
+#include <math.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+/* GLOBAL_SUM_TILE_RL: sum = 0; DO bj; DO bi; sum = sum + tile(bi,bj) */
+static double gsum_tiles(const double *tile, int nTiles) {
+  double s = 0.0;
+  for (int t = 0; t < nTiles; t++) s = s + tile[t];
+  return s;
+}
+
+int oracle_ini_cg2d(OModel *m) {
+  const int sNx = m->sNx, sNy = m->sNy, OLx = m->OLx, OLy = m->OLy, Nr = m->Nr;
+  long N2 = m->n2 * m->nTiles;
+  for (long p = 0; p < N2; p++) m->aW2d[p] = m->aS2d[p] = m->aC2d[p] = m->pW[p] = m->pS[p] = m->pC[p] = 0.0;
+  double myNorm = 0.0;
+  for (int t = 0; t < m->nTiles; t++) {
+    for (int k = 1; k <= Nr; k++)
+      for (int j = 1; j <= sNy; j++)
+        for (int i = 1; i <= sNx; i++) {
+          long p = O2(m, i, j, t);
+          double faceArea = m->dyG[p] * m->drF[k - 1] * m->hFacW[O3(m, i, j, k, t)];
+          m->aW2d[p] = m->aW2d[p] + m->implicSurfPress * m->implicDiv2DFlow * faceArea * m->recip_dxC[p];
+          faceArea = m->dxG[p] * m->drF[k - 1] * m->hFacS[O3(m, i, j, k, t)];
+          m->aS2d[p] = m->aS2d[p] + m->implicSurfPress * m->implicDiv2DFlow * faceArea * m->recip_dyC[p];
+        }
+    for (int j = 1; j <= sNy; j++)
+      for (int i = 1; i <= sNx; i++) {
+        myNorm = fmax(fabs(m->aW2d[O2(m, i, j, t)]), myNorm);
+        myNorm = fmax(fabs(m->aS2d[O2(m, i, j, t)]), myNorm);
+      }
+  }
+  myNorm = (myNorm != 0.0) ? 1.0 / myNorm : 1.0;
+  for (int t = 0; t < m->nTiles; t++)
+    for (int j = 1; j <= sNy; j++)
+      for (int i = 1; i <= sNx; i++) {
+        m->aW2d[O2(m, i, j, t)] = m->aW2d[O2(m, i, j, t)] * myNorm;
+        m->aS2d[O2(m, i, j, t)] = m->aS2d[O2(m, i, j, t)] * myNorm;
+      }
+  oracle_exch_xy(m, m->aW2d); /* EXCH_UV_XY_RS(aW2d,aS2d,.FALSE.): lat-lon = scalar copies */
+  oracle_exch_xy(m, m->aS2d);
+  m->cg2dNorm = myNorm;
+  m->cg2dNormaliseRHS = (m->cg2dTargetResWunit <= 0.0);
+  double tol = m->cg2dNormaliseRHS ? m->cg2dTargetResidual
+                                   : m->cg2dNorm * m->cg2dTargetResWunit * m->globalArea / m->deltaTMom;
+  m->cg2dTolerance_sq = tol * tol;
+  for (int t = 0; t < m->nTiles; t++) {
+    for (int j = 0; j <= sNy; j++)
+      for (int i = 0; i <= sNx; i++) {
+        long p = O2(m, i, j, t);
+        m->aC2d[p] = -(m->aW2d[p] + m->aW2d[O2(m, i + 1, j, t)] + m->aS2d[p] + m->aS2d[O2(m, i, j + 1, t)] +
+                       m->freeSurfFac * myNorm * m->recip_Bo[p] * m->rA[p] / m->deltaTMom / m->deltaTFreeSurf);
+      }
+    for (int j = 1; j <= sNy; j++)
+      for (int i = 1; i <= sNx; i++) {
+        long p = O2(m, i, j, t);
+        double aC = m->aC2d[p], aCs = m->aC2d[O2(m, i, j - 1, t)], aCw = m->aC2d[O2(m, i - 1, j, t)];
+        m->pC[p] = (aC == 0.0) ? 1.0 : 1.0 / aC;
+        if (aC + aCw == 0.0) m->pW[p] = 0.0;
+        else { double d = m->cg2dpcOffDFac * (aCw + aC); m->pW[p] = -m->aW2d[p] / (d * d); }
+        if (aC + aCs == 0.0) m->pS[p] = 0.0;
+        else { double d = m->cg2dpcOffDFac * (aCs + aC); m->pS[p] = -m->aS2d[p] / (d * d); }
+      }
+  }
+  oracle_exch_xy(m, m->pC);
+  oracle_exch_xy(m, m->pW);
+  oracle_exch_xy(m, m->pS);
+  (void)OLx; (void)OLy;
+  return 0;
+}
+
+/* CG2D (model/src/cg2d.F:13-415), default branch (no CG2D_SINGLECPU_SUM) */
+void oracle_cg2d(OModel *m, double *cg2d_b, double *cg2d_x, double *firstResidual,
+                 double *minResidualSq, double *lastResidual, int *numIters, int *nIterMin) {
+  const int sNx = m->sNx, sNy = m->sNy, nT = m->nTiles;
+  const long N2 = m->n2 * nT;
+  double *r = calloc(N2, 8), *s = calloc(N2, 8), *q = calloc(N2, 8), *xmin = calloc(N2, 8);
+  double *tile = calloc(nT, 8), *tile2 = calloc(nT, 8);
+  const double *aW = m->aW2d, *aS = m->aS2d, *aC = m->aC2d, *pW = m->pW, *pS = m->pS, *pC = m->pC;
+  double err_sq, eta_qrN, eta_qrNM1 = 1.0, cgBeta, alpha, sumRHS, rhsMax = 0.0, rhsNorm = 1.0;
+  int actualIts = 0;
+  *minResidualSq = -1.0;
+  for (int t = 0; t < nT; t++)
+    for (int j = 1; j <= sNy; j++)
+      for (int i = 1; i <= sNx; i++) {
+        long p = O2(m, i, j, t);
+        cg2d_b[p] = cg2d_b[p] * m->cg2dNorm;
+        rhsMax = fmax(fabs(cg2d_b[p]), rhsMax);
+      }
+  if (m->cg2dNormaliseRHS) {
+    rhsNorm = 1.0;
+    if (rhsMax != 0.0) rhsNorm = 1.0 / rhsMax;
+    for (int t = 0; t < nT; t++)
+      for (int j = 1; j <= sNy; j++)
+        for (int i = 1; i <= sNx; i++) {
+          long p = O2(m, i, j, t);
+          cg2d_b[p] = cg2d_b[p] * rhsNorm;
+          cg2d_x[p] = cg2d_x[p] * rhsNorm;
+        }
+  }
+  oracle_exch_xy(m, cg2d_x);
+  for (int t = 0; t < nT; t++) {
+    if (*nIterMin >= 0)
+      for (int j = 1; j <= sNy; j++)
+        for (int i = 1; i <= sNx; i++) xmin[O2(m, i, j, t)] = cg2d_x[O2(m, i, j, t)];
+    double sumT = 0.0, errT = 0.0;
+    for (int j = 1; j <= sNy; j++)
+      for (int i = 1; i <= sNx; i++) {
+        long p = O2(m, i, j, t);
+        r[p] = cg2d_b[p] - (aW[p] * cg2d_x[O2(m, i - 1, j, t)] + aW[O2(m, i + 1, j, t)] * cg2d_x[O2(m, i + 1, j, t)] +
+                            aS[p] * cg2d_x[O2(m, i, j - 1, t)] + aS[O2(m, i, j + 1, t)] * cg2d_x[O2(m, i, j + 1, t)] +
+                            aC[p] * cg2d_x[p]);
+        errT = errT + r[p] * r[p];
+        sumT = sumT + cg2d_b[p];
+      }
+    tile[t] = errT; tile2[t] = sumT;
+  }
+  /* EXCH_S3D_RL(cg2d_r, 1): halo width 1 fill; the full-halo periodic copy is a superset */
+  oracle_exch_xy(m, r);
+  err_sq = gsum_tiles(tile, nT);
+  sumRHS = gsum_tiles(tile2, nT);
+  *firstResidual = sqrt(err_sq);
+  if (*nIterMin >= 0) { *nIterMin = 0; *minResidualSq = err_sq; }
+  m->sumRHS = sumRHS; m->rhsMax = rhsMax;
+  if (!(err_sq < m->cg2dTolerance_sq)) {
+    for (int it2d = 1; it2d <= *numIters; it2d++) {
+      for (int t = 0; t < nT; t++) {
+        double e = 0.0;
+        for (int j = 1; j <= sNy; j++)
+          for (int i = 1; i <= sNx; i++) {
+            long p = O2(m, i, j, t);
+            q[p] = pC[p] * r[p] + pW[p] * r[O2(m, i - 1, j, t)] + pW[O2(m, i + 1, j, t)] * r[O2(m, i + 1, j, t)] +
+                   pS[p] * r[O2(m, i, j - 1, t)] + pS[O2(m, i, j + 1, t)] * r[O2(m, i, j + 1, t)];
+            e = e + q[p] * r[p];
+          }
+        tile[t] = e;
+      }
+      eta_qrN = gsum_tiles(tile, nT);
+      cgBeta = eta_qrN / eta_qrNM1;
+      eta_qrNM1 = eta_qrN;
+      for (int t = 0; t < nT; t++)
+        for (int j = 1; j <= sNy; j++)
+          for (int i = 1; i <= sNx; i++) {
+            long p = O2(m, i, j, t);
+            s[p] = q[p] + cgBeta * s[p];
+          }
+      oracle_exch_xy(m, s);
+      for (int t = 0; t < nT; t++) {
+        double a = 0.0;
+        for (int j = 1; j <= sNy; j++)
+          for (int i = 1; i <= sNx; i++) {
+            long p = O2(m, i, j, t);
+            q[p] = aW[p] * s[O2(m, i - 1, j, t)] + aW[O2(m, i + 1, j, t)] * s[O2(m, i + 1, j, t)] +
+                   aS[p] * s[O2(m, i, j - 1, t)] + aS[O2(m, i, j + 1, t)] * s[O2(m, i, j + 1, t)] + aC[p] * s[p];
+            a = a + s[p] * q[p];
+          }
+        tile[t] = a;
+      }
+      alpha = gsum_tiles(tile, nT);
+      alpha = eta_qrN / alpha;
+      for (int t = 0; t < nT; t++) {
+        double e = 0.0;
+        for (int j = 1; j <= sNy; j++)
+          for (int i = 1; i <= sNx; i++) {
+            long p = O2(m, i, j, t);
+            cg2d_x[p] = cg2d_x[p] + alpha * s[p];
+            r[p] = r[p] - alpha * q[p];
+            e = e + r[p] * r[p];
+          }
+        tile[t] = e;
+      }
+      actualIts = it2d;
+      err_sq = gsum_tiles(tile, nT);
+      if (err_sq < m->cg2dTolerance_sq) break;
+      if (err_sq < *minResidualSq) {
+        *minResidualSq = err_sq;
+        *nIterMin = it2d;
+        for (int t = 0; t < nT; t++)
+          for (int j = 1; j <= sNy; j++)
+            for (int i = 1; i <= sNx; i++) xmin[O2(m, i, j, t)] = cg2d_x[O2(m, i, j, t)];
+      }
+      oracle_exch_xy(m, r);
+    }
+  }
+  if (*nIterMin >= 0 && err_sq > *minResidualSq)
+    for (int t = 0; t < nT; t++)
+      for (int j = 1; j <= sNy; j++)
+        for (int i = 1; i <= sNx; i++) cg2d_x[O2(m, i, j, t)] = xmin[O2(m, i, j, t)];
+  if (m->cg2dNormaliseRHS)
+    for (int t = 0; t < nT; t++)
+      for (int j = 1; j <= sNy; j++)
+        for (int i = 1; i <= sNx; i++) cg2d_x[O2(m, i, j, t)] = cg2d_x[O2(m, i, j, t)] / rhsNorm;
+  *lastResidual = sqrt(err_sq);
+  *numIters = actualIts;
+  free(r); free(s); free(q); free(xmin); free(tile); free(tile2);
+}
+
+/* SOLVE_FOR_PRESSURE (solve_for_pressure.F:122-385), hydrostatic, no OBCS, linear FS */
+void oracle_solve_for_pressure(OModel *m) {
+  const int sNx = m->sNx, sNy = m->sNy, OLx = m->OLx, OLy = m->OLy, Nr = m->Nr, nx = m->nx;
+  const long N2 = m->n2 * m->nTiles, n2 = m->n2;
+  double *cg2d_x = calloc(N2, 8), *cg2d_b = calloc(N2, 8), *pf = calloc(n2, 8);
+  for (long p = 0; p < N2; p++) { cg2d_x[p] = m->Bo_surf[p] * m->etaN[p]; cg2d_b[p] = 0.0; }
+#define PF(i, j) pf[(long)((i) + OLx - 1) + (long)((j) + OLy - 1) * nx]
+  for (int t = 0; t < m->nTiles; t++) {
+    for (int k = Nr; k >= 1; k--) {
+      /* CALC_DIV_GHAT (calc_div_ghat.F:62-166), implicDiv2DFlow = 1 */
+      for (int j = 1; j <= sNy; j++)
+        for (int i = 1; i <= sNx + 1; i++) {
+          double xA = m->dyG[O2(m, i, j, t)] * m->drF[k - 1] * m->hFacW[O3(m, i, j, k, t)];
+          PF(i, j) = xA * m->gU[O3(m, i, j, k, t)] / m->deltaTMom;
+        }
+      for (int j = 1; j <= sNy; j++)
+        for (int i = 1; i <= sNx; i++)
+          cg2d_b[O2(m, i, j, t)] = cg2d_b[O2(m, i, j, t)] + PF(i + 1, j) - PF(i, j);
+      for (int j = 1; j <= sNy + 1; j++)
+        for (int i = 1; i <= sNx; i++) {
+          double yA = m->dxG[O2(m, i, j, t)] * m->drF[k - 1] * m->hFacS[O3(m, i, j, k, t)];
+          PF(i, j) = yA * m->gV[O3(m, i, j, k, t)] / m->deltaTMom;
+        }
+      for (int j = 1; j <= sNy; j++)
+        for (int i = 1; i <= sNx; i++)
+          cg2d_b[O2(m, i, j, t)] = cg2d_b[O2(m, i, j, t)] + PF(i, j + 1) - PF(i, j);
+    }
+  }
+#undef PF
+  for (int t = 0; t < m->nTiles; t++)
+    for (int j = 1; j <= sNy; j++)
+      for (int i = 1; i <= sNx; i++) {
+        long p = O2(m, i, j, t);
+        cg2d_b[p] = cg2d_b[p] - m->freeSurfFac * m->rA[p] / m->deltaTMom / m->deltaTFreeSurf * m->etaN[p];
+      }
+  int numIters = m->cg2dMaxIters, nIterMin = m->cg2dUseMinResSol - 1;
+  double firstRes, minResSq, lastRes;
+  oracle_cg2d(m, cg2d_b, cg2d_x, &firstRes, &minResSq, &lastRes, &numIters, &nIterMin);
+  oracle_exch_xy(m, cg2d_x);
+  m->firstResidual = firstRes; m->lastResidual = lastRes; m->numIters = numIters; m->nIterMin = nIterMin;
+  m->minResidualSq = (minResSq >= 0.0) ? sqrt(minResSq) : minResSq;
+  for (long p = 0; p < N2; p++) m->etaN[p] = m->recip_Bo[p] * cg2d_x[p];
+  free(cg2d_x); free(cg2d_b); free(pf);
+}
+
+/* MOMENTUM_CORRECTION_STEP (momentum_correction_step.F:60-91) -> CALC_GRAD_PHI_SURF
+ * (calc_grad_phi_surf.F:46-61) -> CORRECTION_STEP (correction_step.F:150-234) */
+void oracle_momentum_correction_step(OModel *m) {
+  const int sNx = m->sNx, sNy = m->sNy, OLx = m->OLx, OLy = m->OLy, Nr = m->Nr;
+  const int iMin = 1 - OLx + 1, iMax = sNx + OLx, jMin = 1 - OLy + 1, jMax = sNy + OLy;
+  const double psFac = m->pfFacMom * m->implicSurfPress;
+  for (int t = 0; t < m->nTiles; t++) {
+    for (int k = 1; k <= Nr; k++)
+      for (int j = jMin; j <= jMax; j++)
+        for (int i = iMin; i <= iMax; i++) {
+          long p = O2(m, i, j, t), p3 = O3(m, i, j, k, t);
+          double phiSurfX = m->recip_dxC[p] * (m->Bo_surf[p] * m->etaN[p] - m->Bo_surf[O2(m, i - 1, j, t)] * m->etaN[O2(m, i - 1, j, t)]);
+          double phiSurfY = m->recip_dyC[p] * (m->Bo_surf[p] * m->etaN[p] - m->Bo_surf[O2(m, i, j - 1, t)] * m->etaN[O2(m, i, j - 1, t)]);
+          double gU_dpx = -psFac * phiSurfX * m->maskW[p3];
+          double gV_dpy = -psFac * phiSurfY * m->maskS[p3];
+          m->uVel[p3] = (m->gU[p3] + m->deltaTMom * gU_dpx) * m->maskW[p3];
+          m->vVel[p3] = (m->gV[p3] + m->deltaTMom * gV_dpy) * m->maskS[p3];
+        }
+  }
+}
+
+/* INTEGR_CONTINUITY (integr_continuity.F:276-314) -> INTEGRATE_FOR_W
+ * (integrate_for_w.F:61-195), linear free surface, no exactConserv */
+void oracle_integr_continuity(OModel *m) {
+  const int sNx = m->sNx, sNy = m->sNy, Nr = m->Nr;
+  if (m->exactConserv) { fprintf(stderr, "oracle: exactConserv not yet restated\n"); abort(); }
+  for (int t = 0; t < m->nTiles; t++)
+    for (int k = Nr; k >= 1; k--)
+      for (int j = 1; j <= sNy; j++)
+        for (int i = 1; i <= sNx; i++) {
+          long p = O2(m, i, j, t);
+          double uT1 = m->uVel[O3(m, i + 1, j, k, t)] * m->dyG[O2(m, i + 1, j, t)] * m->drF[k - 1] * m->hFacW[O3(m, i + 1, j, k, t)];
+          double uT0 = m->uVel[O3(m, i, j, k, t)] * m->dyG[p] * m->drF[k - 1] * m->hFacW[O3(m, i, j, k, t)];
+          double vT1 = m->vVel[O3(m, i, j + 1, k, t)] * m->dxG[O2(m, i, j + 1, t)] * m->drF[k - 1] * m->hFacS[O3(m, i, j + 1, k, t)];
+          double vT0 = m->vVel[O3(m, i, j, k, t)] * m->dxG[p] * m->drF[k - 1] * m->hFacS[O3(m, i, j, k, t)];
+          double conv2d = -(uT1 - uT0 + vT1 - vT0);
+          if (k == Nr)
+            m->wVel[O3(m, i, j, k, t)] = conv2d * m->recip_rA[p] * m->maskC[O3(m, i, j, k, t)];
+          else
+            m->wVel[O3(m, i, j, k, t)] = (m->wVel[O3(m, i, j, k + 1, t)] + conv2d * m->recip_rA[p]) * m->maskC[O3(m, i, j, k, t)];
+        }
+  if (m->myIter == m->nIter0) oracle_exch_xyz(m, m->wVel, Nr);
+}
+
+/* FORWARD_STEP (model/src/forward_step.F:64-1256) for the supported subset:
+ * EXTERNAL_FORCING_SURF (momentum part) -> DYNAMICS -> SOLVE_FOR_PRESSURE ->
+ * MOMENTUM_CORRECTION_STEP -> INTEGR_CONTINUITY -> DO_FIELDS_BLOCKING_EXCHANGES */
+void oracle_forward_step(OModel *m) {
+  const long N2 = m->n2 * m->nTiles;
+  /* external_forcing_surf.F:214-216: surfaceForcingU = fu*mass2rUnit */
+  const double mass2rUnit = 1.0 / m->rhoConst;
+  for (long p = 0; p < N2; p++) {
+    m->surfaceForcingU[p] = m->fu[p] * mass2rUnit;
+    m->surfaceForcingV[p] = m->fv[p] * mass2rUnit;
+  }
+  oracle_dynamics(m);
+  oracle_solve_for_pressure(m);
+  oracle_momentum_correction_step(m);
+  oracle_integr_continuity(m);
+  /* do_fields_blocking_exchanges.F:54-97 */
+  oracle_exch_xyz(m, m->uVel, m->Nr);
+  oracle_exch_xyz(m, m->vVel, m->Nr);
+  oracle_exch_xyz(m, m->wVel, m->Nr);
+  oracle_exch_xyz(m, m->theta, m->Nr);
+  oracle_exch_xyz(m, m->salt, m->Nr);
+  m->myIter = m->myIter + 1;
+  m->myTime = m->myTime + m->deltaTClock;
+}
+
+/* MON_CALC_STATS_RL (pkg/monitor/mon_calc_stats_rl.F). arrhFac is 3-D
+ * (myNr levels) when hfac3d, else a 2-D mask reused for every level. */
+void oracle_mon_stats(OModel *m, const double *arr, int myNr, const double *arrhFac, int hfac3d,
+                      const double *arrMask, const double *arrArea, const double *arrDr, double out[6]) {
+  const int sNx = m->sNx, sNy = m->sNy, nT = m->nTiles;
+  const long n2 = m->n2, nz = (long)myNr * n2;
+  double theMin = 0, theMax = 0, theMean = 0, theSD = 0, theDel2 = 0, theVol = 0, theNbPt = 0;
+  int noPnts = 1;
+  double *tNb = calloc(nT, 8), *tDel2 = calloc(nT, 8), *tVol = calloc(nT, 8), *tMean = calloc(nT, 8), *tSD = calloc(nT, 8);
+#define H(i, j, k) (hfac3d ? arrhFac[O2(m, i, j, t) - (long)t * n2 + (long)((k) - 1) * n2 + (long)t * nz] : arrhFac[O2(m, i, j, t)])
+#define A(i, j, k) arr[O2(m, i, j, t) - (long)t * n2 + (long)((k) - 1) * n2 + (long)t * nz]
+  for (int t = 0; t < nT; t++) {
+    for (int k = 1; k <= myNr; k++)
+      for (int j = 1; j <= sNy; j++)
+        for (int i = 1; i <= sNx; i++) {
+          double v = A(i, j, k);
+          double msk = arrMask[O2(m, i, j, t)] * H(i, j, k);
+          if (msk > 0.0 && noPnts) { theMin = v; theMax = v; noPnts = 0; }
+          if (msk > 0.0) {
+            theMin = fmin(theMin, v); theMax = fmax(theMax, v);
+            double ddx = H(i + 1, j, k) * H(i - 1, j, k);
+            if (ddx > 0.0) ddx = (A(i + 1, j, k) - v) + (A(i - 1, j, k) - v);
+            double ddy = H(i, j + 1, k) * H(i, j - 1, k);
+            if (ddy > 0.0) ddy = (A(i, j + 1, k) - v) + (A(i, j - 1, k) - v);
+            tDel2[t] = tDel2[t] + ddx * ddx + ddy * ddy;
+            tNb[t] = tNb[t] + 1.0;
+            double vol = arrArea[O2(m, i, j, t)] * arrDr[k - 1] * msk;
+            tVol[t] = tVol[t] + vol;
+            tMean[t] = tMean[t] + vol * v;
+          }
+        }
+  }
+  theNbPt = gsum_tiles(tNb, nT); theDel2 = gsum_tiles(tDel2, nT);
+  theVol = gsum_tiles(tVol, nT); theMean = gsum_tiles(tMean, nT);
+  if (theNbPt > 0.0) theDel2 = sqrt(theDel2) / theNbPt;
+  if (theVol > 0.0) {
+    theMean = theMean / theVol;
+    if (noPnts) { theMin = theMean; theMax = theMean; }
+    for (int t = 0; t < nT; t++)
+      for (int k = 1; k <= myNr; k++)
+        for (int j = 1; j <= sNy; j++)
+          for (int i = 1; i <= sNx; i++) {
+            double v = A(i, j, k), msk = arrMask[O2(m, i, j, t)] * H(i, j, k);
+            if (msk > 0.0) {
+              double vol = arrArea[O2(m, i, j, t)] * arrDr[k - 1] * msk;
+              tSD[t] = tSD[t] + vol * (v - theMean) * (v - theMean);
+            }
+          }
+    theSD = gsum_tiles(tSD, nT);
+    theSD = sqrt(theSD / theVol);
+  }
+#undef H
+#undef A
+  out[0] = theMin; out[1] = theMax; out[2] = theMean; out[3] = theSD; out[4] = theDel2; out[5] = theVol;
+  free(tNb); free(tDel2); free(tVol); free(tMean); free(tSD);
+}

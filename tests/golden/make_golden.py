@@ -1,0 +1,113 @@
+"""Extract golden fixtures for the parity tests from the reference checkout.
+
+Run in the build container only (it reads /root/reference, which does not exist
+on the GPU box):  python tests/golden/make_golden.py
+
+What it writes (data only -- inputs and expected outputs, no reference source):
+  tests/golden/<exp>/*.bin            the experiment's own binary input fields, verbatim
+  tests/golden/<exp>/monitor.json     per-step %MON / cg2d_* values parsed from the
+                                      committed verification/<exp>/results/output.txt
+  tests/golden/<exp>/params.json      resolved run-time parameters parsed from the
+                                      "Model configuration" dump of the same output.txt
+"""
+import json
+import os
+import re
+import shutil
+import sys
+
+REF = "/root/reference/verification"
+HERE = os.path.dirname(os.path.abspath(__file__))
+
+EXPERIMENTS = {
+    "tutorial_barotropic_gyre": {
+        "inputs": ["input/bathy.bin", "input/windx_cosy.bin"],
+        "output": "results/output.txt",
+    },
+}
+
+_num = r"[-+]?\d*\.?\d+(?:[EeDd][-+]?\d+)?"
+
+
+def parse_monitor(path):
+    """Return a list of per-step dicts: {'time_tsnumber': n, 'dynstat_eta_max': x, ...,
+    'cg2d_init_res': ..., 'cg2d_iters': ..., 'cg2d_last_res': ...}.  The cg2d lines that
+    precede a monitor block belong to the step that block reports."""
+    steps, pending, cur = [], {}, None
+    with open(path) as f:
+        for line in f:
+            m = re.search(r"%MON (\S+)\s*=\s*(" + _num + ")", line)
+            if m:
+                key, val = m.group(1), m.group(2).replace("D", "E")
+                if key == "time_tsnumber":
+                    cur = {"time_tsnumber": int(val)}
+                    cur.update(pending)
+                    pending = {}
+                    steps.append(cur)
+                elif cur is not None:
+                    cur[key] = float(val)
+                continue
+            m = re.search(r"cg2d_init_res =\s*(" + _num + ")", line)
+            if m:
+                pending["cg2d_init_res"] = float(m.group(1))
+                continue
+            m = re.search(r"cg2d_iters\(min,last\) =\s*(-?\d+)\s+(\d+)", line)
+            if m:
+                pending["cg2d_iters_min"] = int(m.group(1))
+                pending["cg2d_iters"] = int(m.group(2))
+                continue
+            m = re.search(r"cg2d_last_res =\s*(" + _num + ")", line)
+            if m:
+                pending["cg2d_last_res"] = float(m.group(1))
+                continue
+            m = re.search(r"cg2d: Sum\(rhs\),rhsMax =\s*(" + _num + r")\s+(" + _num + ")", line)
+            if m:
+                pending["cg2d_sum_rhs"] = float(m.group(1))
+                pending["cg2d_rhs_max"] = float(m.group(2))
+    return steps
+
+
+def parse_params(path):
+    """Parse the 'name = /* description */' + value lines of the configuration dump."""
+    params = {}
+    lines = open(path).read().splitlines()
+    pref = "(PID.TID 0000.0001) "
+    for n, line in enumerate(lines):
+        if not line.startswith(pref):
+            continue
+        body = line[len(pref):]
+        m = re.match(r"(\w+)\s*=\s*/\*", body)
+        if not m or n + 1 >= len(lines):
+            continue
+        name, vals = m.group(1), []
+        for nxt in lines[n + 1:n + 40]:
+            v = nxt[len(pref):].strip() if nxt.startswith(pref) else ""
+            if v.startswith(";") or not v:
+                break
+            tok = v.split("/*")[0].strip()
+            mm = re.match(r"(\d+)\s*@\s*(" + _num + r"|[TF])", tok)
+            if mm:
+                vals += [mm.group(2)] * int(mm.group(1))
+            else:
+                vals.append(tok)
+        if vals:
+            params[name] = vals[0] if len(vals) == 1 else vals
+    return params
+
+
+def main():
+    for exp, spec in EXPERIMENTS.items():
+        out = os.path.join(HERE, exp)
+        os.makedirs(out, exist_ok=True)
+        for rel in spec["inputs"]:
+            shutil.copyfile(os.path.join(REF, exp, rel), os.path.join(out, os.path.basename(rel)))
+        res = os.path.join(REF, exp, spec["output"])
+        with open(os.path.join(out, "monitor.json"), "w") as f:
+            json.dump(parse_monitor(res), f, indent=1)
+        with open(os.path.join(out, "params.json"), "w") as f:
+            json.dump(parse_params(res), f, indent=1, sort_keys=True)
+        print("wrote", out)
+
+
+if __name__ == "__main__":
+    sys.exit(main())
