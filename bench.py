@@ -1,0 +1,155 @@
+#!/usr/bin/env python3
+"""Benchmark of the MI355X-native MITgcm hot path.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config NAME]
+
+A "step" is one FORWARD_STEP of the device-resident hot path (DYNAMICS ->
+SOLVE_FOR_PRESSURE/CG2D -> MOMENTUM_CORRECTION_STEP -> INTEGR_CONTINUITY ->
+blocking exchanges) on inputs already resident in HBM.  Rank 0 prints ONE JSON
+line.  N>1: one process per GPU (torch.distributed.run); the supported
+workloads are single-tile, so every rank runs an independent replica
+("replicas only") and value = the sum over ranks.
+
+Fields of the JSON line beyond the driver contract:
+  roofline     dominant kernel (cg2d): algorithmic bytes per launch
+               (136 B per interior point per CG iteration, SURVEY.md 8(d) x
+               the iterations that launch ran) / its mean HIP-event duration
+  cpu_baseline the oracle (oracle/, C restatement, 1 core) on a bounded sample
+               of the same workload, rank 0 only
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+CG2D_BYTES_PER_POINT_ITER = 136  # two-sync-point minimum traffic
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--config", default="tutorial_barotropic_gyre")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    return ap.parse_args()
+
+
+def cpu_baseline(seconds):
+    """Oracle (CPU restatement, 1 thread) timed on the same workload: as many
+    gyre steps as fit in ~`seconds` of CPU time, reported in model-days/s."""
+    from oracle.harness import gyre_oracle
+    o = gyre_oracle()
+    o.forward_step()  # warm
+    n, t0 = 0, time.perf_counter()
+    while time.perf_counter() - t0 < seconds:
+        o.forward_step()
+        n += 1
+    dt = time.perf_counter() - t0
+    return {"value": n * 1200.0 / 86400.0 / dt, "unit": "model-days/s", "cores": 1, "kind": "port",
+            "sample": "%d FORWARD_STEPs of tutorial_barotropic_gyre 62x62x1 on the oracle "
+                      "(oracle/*.c, gcc -O2, 1 thread), %.1f s" % (n, dt)}
+
+
+def main():
+    a = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch
+        import torch.distributed as dist
+        dist.init_process_group("gloo")   # barrier + max-reduce of host timers only
+    import numpy as np
+    from mitgcm_amd import configs
+    from mitgcm_amd.model import dynstat
+
+    if a.config != "tutorial_barotropic_gyre":
+        raise SystemExit("unknown --config %s" % a.config)
+    m = configs.make_model(configs.barotropic_gyre, device=local)
+    g = m.g
+    dt_clock = m.params["deltaTClock"]
+    npts = g.nTiles * g.sNx * g.sNy
+
+    # warmup (untimed)
+    if a.warmup > 0:
+        m.forward_step(a.warmup)
+    m.sync()
+
+    def barrier():
+        if dist is not None:
+            dist.barrier()
+
+    m.kernel_timing(True)
+    barrier()
+    m.sync()
+    t0 = time.perf_counter()
+    m.forward_step(a.steps)
+    m.sync()
+    t1 = time.perf_counter()
+    barrier()
+    elapsed = t1 - t0
+    if dist is not None:
+        import torch
+        t = torch.tensor([elapsed], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    iters = [m.solve_stats(back=b)["cg2d_iters"] for b in range(a.steps)]
+    cg_ms, cg_n = m.kernel_ms("cg2d")
+    kern = {k: m.kernel_ms(k) for k in ("mom_step", "sfp_rhs", "cg2d", "exchange", "eta_update", "correction",
+                                         "continuity")}
+    m.kernel_timing(False)
+    # sanity: the solution is finite and the solver converged every step
+    stats = m.solve_stats()
+    eta = m.get("etaN")
+    assert np.isfinite(eta).all() and stats["cg2d_last_res"] < 1e-6, stats
+
+    model_days = a.steps * dt_clock / 86400.0
+    value = world * model_days / elapsed
+    iters_total = sum(iters)
+    cg2d_iters_per_s = world * iters_total / elapsed
+    bytes_per_launch = CG2D_BYTES_PER_POINT_ITER * npts * (iters_total / max(1, len(iters)))
+    achieved = bytes_per_launch / (cg_ms * 1e-3) / 1e9 if cg_ms > 0 else 0.0
+    out = {
+        "metric": "model-days/wallclock-sec",
+        "value": value,
+        "unit": "model-days/s",
+        "n_gpus": world,
+        "steps": a.steps,
+        "warmup": a.warmup,
+        "ms_per_step": 1e3 * elapsed / a.steps,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f64",
+        "data": "reference input fields of verification/tutorial_barotropic_gyre (bathy.bin, windx_cosy.bin), "
+                "cold start",
+        "config": {"workload": "tutorial_barotropic_gyre 62x62x1, 1 tile per GPU, full FORWARD_STEP on device "
+                               "(dt=1200 s); replicas only",
+                   "tiles_per_gpu": g.nTiles, "points_per_tile": [g.sNx, g.sNy, g.Nr],
+                   "parallelism": "replicas%d" % world},
+        "cg2d_iters_per_s": cg2d_iters_per_s,
+        "cg2d_mean_iters_per_solve": iters_total / max(1, len(iters)),
+        "kernel_ms_mean": {k: v[0] for k, v in kern.items()},
+        "roofline": {"bound": "hbm", "kernel": "k_cg2d_block", "achieved": achieved, "peak": HBM_PEAK_GBS,
+                     "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                     "bytes_per_launch": bytes_per_launch, "launch_ms": cg_ms, "launches": cg_n},
+    }
+    if rank == 0 and not a.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline(a.cpu_seconds)
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    m.close()
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,112 @@
+/*
+ * mitgcm_amd.h -- C-ABI of the MI355X-native MITgcm dynamical hot path.
+ *
+ * Plain C: opaque handles, pointers and sizes only (no torch / HIP types).
+ * Two families of entry points:
+ *
+ *  1. Model-handle API (mgcm_*): a tile set resident in HBM, driven step by step.
+ *     Every array crossing the boundary uses the reference's layout: fp64,
+ *     halo-inclusive (1-OLx:sNx+OLx, 1-OLy:sNy+OLy[, 1:Nr], tile), i fastest
+ *     (model/inc/DYNVARS.h:36-152, model/inc/GRID.h:311-523).
+ *
+ *  2. Fortran-callable drop-ins with the reference's own argument lists
+ *     (lower-case + trailing underscore, all arguments by reference, as
+ *     genmake2's FC_NAMEMANGLE produces for amdflang), e.g. cg2d_amd_ replaces
+ *     SUBROUTINE CG2D of model/src/cg2d.F:13-17.  See INTEGRATION.md for the
+ *     MODS-directory shims that bind them.
+ *
+ * Errors: entry points returning int give 0 on success and a negative code on
+ * failure (mgcm_last_error() has the message).  The Fortran entry points have
+ * no return channel (the reference has none either): they
+ * print the error and abort(), the equivalent of STOP 'ABNORMAL END'.
+ */
+#ifndef MITGCM_AMD_H
+#define MITGCM_AMD_H
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct mgcm_model mgcm_model;
+
+/* ------------------------------------------------------------ lifecycle */
+/* Allocate a device-resident tile set of nSx*nSy tiles of (sNx+2OLx)(sNy+2OLy)Nr
+ * points on HIP device `device`.  Replaces the per-tile COMMON-block storage of
+ * DYNVARS.h / GRID.h / CG2D.h for the tiles this GPU owns. */
+mgcm_model *mgcm_create(int sNx, int sNy, int OLx, int OLy, int Nr, int nSx, int nSy, int device);
+void mgcm_destroy(mgcm_model *m);
+const char *mgcm_last_error(void);
+
+/* Run-time parameters (PARAMS.h names, already resolved as ini_parms.F does). */
+int mgcm_set_param(mgcm_model *m, const char *name, double value);
+double mgcm_get_param(mgcm_model *m, const char *name);
+
+/* Host <-> device copies of named fields (DYNVARS/GRID/CG2D/FFIELDS names,
+ * e.g. "uVel", "hFacW", "aW2d", "fu").  count = number of doubles. */
+int mgcm_put(mgcm_model *m, const char *name, const double *host, long count);
+int mgcm_get(mgcm_model *m, const char *name, double *host, long count);
+/* Device pointer of a named field (for zero-copy interop, e.g. torch tensors). */
+double *mgcm_device_ptr(mgcm_model *m, const char *name);
+
+/* Halo topology.  Default (set by mgcm_create): EXCH1 lat-lon, periodic over the
+ * nSx x nSy tile layout (eesupp/src/exch1_rx.template:8-276).  A caller with a
+ * cube/LLC topology (pkg/exch2) passes, for every halo point, the flat source
+ * offset (tile,j,i) it copies from, or -1 to leave it untouched. */
+int mgcm_set_halo_map(mgcm_model *m, const long *src_of_point, long count);
+
+/* Finish set-up after grid/mask/operator fields are in place: builds the CG2D
+ * neighbour tables and checks that the option set is one the kernels support. */
+int mgcm_init(mgcm_model *m);
+
+/* --------------------------------------------------------- hot path ops */
+/* DYNAMICS (model/src/dynamics.F:21): MOM_FLUXFORM + TIMESTEP + AB2 for every
+ * tile and level; writes gU/gV (= u*, v*) and updates guNm1/gvNm1. */
+int mgcm_dynamics(mgcm_model *m);
+/* SOLVE_FOR_PRESSURE (model/src/solve_for_pressure.F:7): CALC_DIV_GHAT RHS,
+ * CG2D, EXCH, etaN = recip_Bo * x. */
+int mgcm_solve_for_pressure(mgcm_model *m);
+/* MOMENTUM_CORRECTION_STEP (model/src/momentum_correction_step.F:7). */
+int mgcm_momentum_correction_step(mgcm_model *m);
+/* INTEGR_CONTINUITY (model/src/integr_continuity.F:13): wVel. */
+int mgcm_integr_continuity(mgcm_model *m);
+/* DO_FIELDS_BLOCKING_EXCHANGES (model/src/do_fields_blocking_exchanges.F:54). */
+int mgcm_blocking_exchanges(mgcm_model *m);
+/* FORWARD_STEP subset: the five ops above (+ surface forcing), nsteps times,
+ * asynchronously on the model's stream (captured once into a hipGraph). */
+int mgcm_forward_step(mgcm_model *m, int nsteps);
+/* Wait for all queued device work. */
+int mgcm_sync(mgcm_model *m);
+
+/* Device CG2D on fields of this model (cg2d.F:13 semantics; b is normalised in
+ * place).  b and x are host arrays of nTiles*(sNx+2OLx)*(sNy+2OLy) doubles. */
+int mgcm_cg2d(mgcm_model *m, double *cg2d_b, double *cg2d_x, double *firstResidual,
+              double *minResidualSq, double *lastResidual, int *numIters, int *nIterMin);
+
+/* Statistics of the most recent solve (what SOLVE_FOR_PRESSURE prints,
+ * solve_for_pressure.F:333-351) for step `back` (0 = latest) of the last
+ * mgcm_forward_step call. */
+int mgcm_solve_stats(mgcm_model *m, int back, double *firstResidual, double *lastResidual,
+                     int *numIters, double *rhsMax);
+
+/* Average device time (ms) of each kernel family over the last timed region,
+ * measured with hipEvents on the model's stream.  name: "mom_step", "cg2d", ... */
+double mgcm_kernel_ms(mgcm_model *m, const char *name, int *launches);
+void mgcm_kernel_timing(mgcm_model *m, int enable);
+
+/* ------------------------------------------- Fortran drop-in (reference ABI) */
+/* Registers the CG2D operator of CG2D.h (ini_cg2d.F:61-237 outputs) for the
+ * drop-in CG2D below.  Arrays are (1-OLx:sNx+OLx,1-OLy:sNy+OLy,nSx,nSy). */
+void ini_cg2d_amd_(const int *sNx, const int *sNy, const int *OLx, const int *OLy,
+                   const int *nSx, const int *nSy, const double *aW2d, const double *aS2d,
+                   const double *aC2d, const double *pW, const double *pS, const double *pC,
+                   const double *cg2dNorm, const double *cg2dTolerance_sq,
+                   const int *cg2dNormaliseRHS);
+/* SUBROUTINE CG2D(cg2d_b,cg2d_x,firstResidual,minResidualSq,lastResidual,
+ *                 numIters,nIterMin,myThid)   -- model/src/cg2d.F:13-17 */
+void cg2d_amd_(double *cg2d_b, double *cg2d_x, double *firstResidual, double *minResidualSq,
+               double *lastResidual, int *numIters, int *nIterMin, const int *myThid);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,70 @@
+"""ctypes binding of the C-ABI (include/mitgcm_amd.h) -> mitgcm_amd/libmitgcm_amd.so.
+
+The product path has no CPU fallback: if the library is missing or no HIP
+device is visible, the calls below raise.
+"""
+import ctypes
+import os
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIBPATH = os.path.join(HERE, "libmitgcm_amd.so")
+_lib = None
+
+
+class MgcmError(RuntimeError):
+    pass
+
+
+def lib():
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIBPATH):
+        raise MgcmError("libmitgcm_amd.so not built (run __graft_entry__.build() or "
+                        "python mitgcm_amd/build.py): the MI355X path has no CPU fallback")
+    L = ctypes.CDLL(LIBPATH)
+    vp, ci, cd, cs, cl = ctypes.c_void_p, ctypes.c_int, ctypes.c_double, ctypes.c_char_p, ctypes.c_long
+    PD, PI, PL = ctypes.POINTER(cd), ctypes.POINTER(ci), ctypes.POINTER(cl)
+    sig = {
+        "mgcm_create": (vp, [ci] * 8),
+        "mgcm_destroy": (None, [vp]),
+        "mgcm_last_error": (cs, []),
+        "mgcm_set_param": (ci, [vp, cs, cd]),
+        "mgcm_get_param": (cd, [vp, cs]),
+        "mgcm_put": (ci, [vp, cs, PD, cl]),
+        "mgcm_get": (ci, [vp, cs, PD, cl]),
+        "mgcm_device_ptr": (vp, [vp, cs]),
+        "mgcm_set_halo_map": (ci, [vp, PL, cl]),
+        "mgcm_init": (ci, [vp]),
+        "mgcm_dynamics": (ci, [vp]),
+        "mgcm_solve_for_pressure": (ci, [vp]),
+        "mgcm_momentum_correction_step": (ci, [vp]),
+        "mgcm_integr_continuity": (ci, [vp]),
+        "mgcm_blocking_exchanges": (ci, [vp]),
+        "mgcm_forward_step": (ci, [vp, ci]),
+        "mgcm_sync": (ci, [vp]),
+        "mgcm_cg2d": (ci, [vp, PD, PD, PD, PD, PD, PI, PI]),
+        "mgcm_solve_stats": (ci, [vp, ci, PD, PD, PI, PD]),
+        "mgcm_kernel_ms": (cd, [vp, cs, PI]),
+        "mgcm_kernel_timing": (None, [vp, ci]),
+        "ini_cg2d_amd_": (None, [PI] * 6 + [PD] * 8 + [PI]),
+        "cg2d_amd_": (None, [PD, PD, PD, PD, PD, PI, PI, PI]),
+    }
+    for name, (res, args) in sig.items():
+        fn = getattr(L, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = L
+    return L
+
+
+EXPORTS = ["mgcm_create", "mgcm_destroy", "mgcm_last_error", "mgcm_set_param", "mgcm_get_param", "mgcm_put",
+           "mgcm_get", "mgcm_device_ptr", "mgcm_set_halo_map", "mgcm_init", "mgcm_dynamics",
+           "mgcm_solve_for_pressure", "mgcm_momentum_correction_step", "mgcm_integr_continuity",
+           "mgcm_blocking_exchanges", "mgcm_forward_step", "mgcm_sync", "mgcm_cg2d", "mgcm_solve_stats",
+           "mgcm_kernel_ms", "mgcm_kernel_timing", "ini_cg2d_amd_", "cg2d_amd_"]
+
+
+def check(rc, what):
+    if rc != 0:
+        raise MgcmError("%s failed: %s" % (what, lib().mgcm_last_error().decode()))

@@ -1,0 +1,60 @@
+"""Experiment set-ups of the reference's verification suite, as host-side
+configuration (values from the experiment's input/data namelist, resolved with
+model/src/set_defaults.F + ini_parms.F; tests pin them against the resolved
+parameter dump of the committed results/output.txt).
+"""
+import os
+
+import numpy as np
+
+from .grid import Grid
+from .model import Model
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+GOLDEN = os.path.join(ROOT, "tests", "golden")
+
+
+def read_bin(path, shape, dtype=">f4"):
+    """MDS/raw big-endian binary (readBinaryPrec=32 default)."""
+    return np.fromfile(path, dtype=dtype).astype(np.float64).reshape(shape)
+
+
+def barotropic_gyre(nSx=1, nSy=1, data_dir=None, bathy=None, wind=None):
+    """verification/tutorial_barotropic_gyre: 62x62x1, code/SIZE.h sNx=sNy=62, OL=2;
+    input/data: viscAh=4.E2, f0=1.E-4, beta=1.E-11, rhoConst=1000, gBaro=9.81,
+    implicitFreeSurface, deltaT=1200, delX=delY=62*20.E3, x/ygOrigin=-20.E3,
+    delR=5000, cg2dTargetResidual=1.E-7, cg2dMaxIters=1000.  Returns (grid, params, state)."""
+    d = data_dir or os.path.join(GOLDEN, "tutorial_barotropic_gyre")
+    Nx = Ny = 62
+    sNx, sNy = Nx // nSx, Ny // nSy
+    g = Grid(sNx, sNy, 2, 2, 1, nSx, nSy)
+    g.ini_vertical_grid([5000.0])
+    g.ini_cartesian_grid(np.full(Nx, 20e3), np.full(Ny, 20e3), -20e3, -20e3)
+    g.ini_cori(1e-4, 1e-11, selectCoriMap=1)
+    if bathy is None:
+        bathy = read_bin(os.path.join(d, "bathy.bin"), (Ny, Nx))
+    g.ini_depths_masks(bathy, hFacMin=1.0, hFacMinDr=0.0, gBaro=9.81)
+    g.ini_cg2d(1200.0, 1200.0, 1e-7)
+    params = dict(deltaTMom=1200.0, deltaTFreeSurf=1200.0, deltaTClock=1200.0, abEps=0.01, rhoConst=1000.0,
+                  gBaro=9.81, viscAhD=400.0, viscAhZ=400.0, viscA4D=0.0, viscA4Z=0.0, viscAr=0.0,
+                  sideDragFactor=2.0, selectCoriScheme=0, momForcingOutAB=0, momDissip_In_AB=1,
+                  cg2dMaxIters=1000, cg2dUseMinResSol=0, nIter0=0, no_slip_sides=1, no_slip_bottom=1)
+    if wind is None:
+        wind = read_bin(os.path.join(d, "windx_cosy.bin"), (Ny, Nx))
+    fu = g.z2()
+    inner = g.sl(1, sNx, 1, sNy)
+    for t in range(g.nTiles):
+        bi, bj = t % nSx, t // nSx
+        fu[t][inner] = wind[bj * sNy:(bj + 1) * sNy, bi * sNx:(bi + 1) * sNx]
+    state = {"fu": g.exch(fu), "fv": g.z2(), "theta": np.full((g.nTiles, 1, g.ny, g.nx), 20.0),
+             "salt": np.full((g.nTiles, 1, g.ny, g.nx), 30.0)}
+    return g, params, state
+
+
+def make_model(cfg, device=0, **kw):
+    g, params, state = cfg(**kw)
+    m = Model(g, params, device=device)
+    for k, v in state.items():
+        m.put(k, v)
+    m.init()
+    return m

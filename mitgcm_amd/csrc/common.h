@@ -1,0 +1,65 @@
+// common.h -- shared device-side definitions for the MI355X hot-path kernels.
+//
+// Layout in HBM (one allocation per field, all tiles of this GPU):
+//   2-D  a[t][j][i]      i in 1-OLx..sNx+OLx fastest  (reference layout, GRID.h)
+//   3-D  a[t][k][j][i]   one level = one (sNx+2OLx)(sNy+2OLy) slab
+// i fastest keeps every host<->device hand-off a plain memcpy of the
+// reference's Fortran arrays; each thread owns an (i,j) column and marches k
+// in registers (the fVerU/V ping-pong of dynamics.F:428-431).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace mgcm {
+
+struct Dims {
+  int sNx, sNy, OLx, OLy, Nr, nSx, nSy, nTiles;
+  int nx, ny;
+  long n2, n3;
+};
+
+// Run-time parameters needed on device (PARAMS.h names).
+struct Params {
+  double deltaTMom, deltaTFreeSurf, deltaTClock, abEps, rhoConst, gBaro;
+  double viscAhD, viscAhZ, viscA4D, viscA4Z, viscAr, sideDragFactor;
+  double freeSurfFac, implicSurfPress, implicDiv2DFlow, rkSign;
+  double afFacMom, vfFacMom, pfFacMom, cfFacMom, foFacMom, mtFacMom;
+  double cg2dNorm, cg2dTolerance_sq;
+  int momAdvection, momViscosity, momForcing, useCoriolis, no_slip_sides, no_slip_bottom;
+  int selectCoriScheme, momForcingOutAB, momDissip_In_AB, implicitViscosity;
+  int cg2dMaxIters, cg2dUseMinResSol, cg2dNormaliseRHS, nIter0;
+};
+
+// Device pointers of every field the kernels touch.
+struct Fields {
+  // 1-D vertical grid
+  const double *drF, *drC, *recip_drF, *recip_drC;
+  // 2-D grid
+  const double *dxF, *dyF, *dxG, *dyG, *dxC, *dyC, *dxV, *dyU, *rA, *rAw, *rAs;
+  const double *recip_dxF, *recip_dyF, *recip_dxC, *recip_dyC, *recip_dxV, *recip_dyU;
+  const double *recip_rA, *recip_rAw, *recip_rAs, *fCori, *Bo_surf, *recip_Bo;
+  // 3-D masks
+  const double *hFacC, *hFacW, *hFacS, *recip_hFacW, *recip_hFacS, *maskC, *maskW, *maskS;
+  // CG2D operator
+  const double *aW2d, *aS2d, *aC2d, *pW, *pS, *pC;
+  // state
+  double *uVel, *vVel, *wVel, *theta, *salt, *etaN;
+  double *gU, *gV, *guNm1, *gvNm1;
+  const double *fu, *fv;
+  // solver work
+  double *cg2d_b, *cg2d_x;
+};
+
+#define MG_I2(d, i, j, t) \
+  ((long)((i) + (d).OLx - 1) + (long)((j) + (d).OLy - 1) * (d).nx + (long)(t) * (d).n2)
+#define MG_I3(d, i, j, k, t)                                                                \
+  ((long)((i) + (d).OLx - 1) + (long)((j) + (d).OLy - 1) * (d).nx + (long)((k) - 1) * (d).n2 + \
+   (long)(t) * (d).n3)
+
+// Per-solve record written by the device CG2D (one slot per time step).
+struct SolveRecord {
+  double firstResidual, lastResidual, minResidualSq, rhsMax, sumRHS;
+  int numIters, nIterMin;
+};
+
+}  // namespace mgcm

@@ -1,0 +1,258 @@
+// kernels_dyn.hip -- DYNAMICS on the MI355X: MOM_FLUXFORM + TIMESTEP + AB2 fused.
+//
+// Reference: model/src/dynamics.F:21-739 (k-loop :422-567),
+//            pkg/mom_fluxform/mom_fluxform.F:42-1064,
+//            model/src/timestep.F:10-429, model/src/adams_bashforth2.F:6-92.
+//
+// One thread owns one (i,j) column of one tile and marches k = 1..Nr, carrying
+// the vertical advective flux of the level above in a register (the
+// fVerU/fVerV(kUp/kDown) ping-pong of dynamics.F:428-431).  Face fluxes that
+// the reference stores in 2-D scratch arrays (fZon, fMer, ...) are re-derived
+// from the neighbours' state with the same expression and operand order, so a
+// column's result is bit-identical to the loop-nest form (compiled with
+// -ffp-contract=off).  The kernel is HBM/latency bound (≈1 flop/B): no MFMA.
+#include "common.h"
+
+namespace mgcm {
+
+// hFacZ (pkg/mom_common/mom_calc_hfacz.F:158-225, hZoption = 0)
+__device__ __forceinline__ double hfacz(const Dims &d, const Fields &f, int i, int j, int k, int t) {
+  if (i < 2 - d.OLx || j < 2 - d.OLy) return 0.0;
+  double h = fmin(f.hFacW[MG_I3(d, i, j, k, t)], f.hFacW[MG_I3(d, i, j - 1, k, t)]);
+  h = fmin(f.hFacS[MG_I3(d, i, j, k, t)], h);
+  h = fmin(f.hFacS[MG_I3(d, i - 1, j, k, t)], h);
+  return h;
+}
+
+__global__ void __launch_bounds__(256) k_mom_step(Dims d, Params p, Fields f, const int *iterPtr) {
+  const int i = (int)(blockIdx.x * blockDim.x + threadIdx.x) + 1 - d.OLx;
+  const int j = (int)(blockIdx.y * blockDim.y + threadIdx.y) + 1 - d.OLy;
+  const int t = (int)blockIdx.z;
+  if (i > d.sNx + d.OLx || j > d.sNy + d.OLy) return;
+  const int Nr = d.Nr;
+  const int myIter = *iterPtr;
+  // adams_bashforth2.F:61-65 (mom_StartAB = nIter0 for a cold start)
+  const double abFac = (myIter == p.nIter0 && p.nIter0 == 0) ? 0.0 : 0.5 + p.abEps;
+  const bool inner = (i >= 0 && i <= d.sNx + 1 && j >= 0 && j <= d.sNy + 1);
+  const double mass2rUnit = 1.0 / p.rhoConst;
+  const double uDudxFac = p.afFacMom, vDudyFac = p.afFacMom, rVelDudrFac = p.afFacMom;
+  const double AhDudxFac = p.vfFacMom, AhDudyFac = p.vfFacMom;
+  const double ArDudrFac = p.implicitViscosity ? 0.0 : p.vfFacMom;
+  const double fuFac = p.cfFacMom, fvFac = p.cfFacMom;
+  const long q2 = MG_I2(d, i, j, t);
+
+#define U(ii, jj, kk) f.uVel[MG_I3(d, ii, jj, kk, t)]
+#define V(ii, jj, kk) f.vVel[MG_I3(d, ii, jj, kk, t)]
+#define W(ii, jj, kk) f.wVel[MG_I3(d, ii, jj, kk, t)]
+#define G2(a, ii, jj) f.a[MG_I2(d, ii, jj, t)]
+#define G3(a, ii, jj, kk) f.a[MG_I3(d, ii, jj, kk, t)]
+
+  double fVerUkm = 0.0, fVerVkm = 0.0;
+  if (inner && p.momAdvection) {
+    // MOM_CALC_RTRANS(k=1) + MOM_U/V_ADV_WU/WV(k=1): free-surface flux (mom_fluxform.F:384-417)
+    const double rTU = 0.5 * (W(i - 1, j, 1) * G2(rA, i - 1, j) + W(i, j, 1) * G2(rA, i, j));
+    const double rTV = 0.5 * (W(i, j - 1, 1) * G2(rA, i, j - 1) + W(i, j, 1) * G2(rA, i, j));
+    fVerUkm = rTU * U(i, j, 1);
+    fVerVkm = rTV * V(i, j, 1);
+  }
+
+  for (int k = 1; k <= Nr; k++) {
+    const double drF = f.drF[k - 1], recip_drF = f.recip_drF[k - 1];
+    double gU = 0.0, gV = 0.0, guDiss = 0.0, gvDiss = 0.0;
+    double fVerUkp = 0.0, fVerVkp = 0.0;
+    if (inner) {
+      const double rhFacW = G3(recip_hFacW, i, j, k), rhFacS = G3(recip_hFacS, i, j, k);
+      const double hZ = hfacz(d, f, i, j, k, t);
+      // ---------------- advection (mom_u_adv_uu/vu/wu.F, mom_v_adv_uv/vv/wv.F)
+      if (p.momAdvection) {
+        if (k + 1 <= Nr) {
+          const int kk = k + 1;
+          const double rTU = 0.5 * (W(i - 1, j, kk) * G2(rA, i - 1, j) + W(i, j, kk) * G2(rA, i, j));
+          const double rTV = 0.5 * (W(i, j - 1, kk) * G2(rA, i, j - 1) + W(i, j, kk) * G2(rA, i, j));
+          double fu_ = rTU * (0.5 * (U(i, j, kk) + U(i, j, kk - 1)));
+          fu_ = fu_ + 0.25 * (W(i, j, kk) * G2(rA, i, j) * (G3(maskC, i, j, kk) - G3(maskC, i, j, kk - 1)) +
+                              W(i - 1, j, kk) * G2(rA, i - 1, j) * (G3(maskC, i - 1, j, kk) - G3(maskC, i - 1, j, kk - 1))) *
+                          U(i, j, kk);
+          fVerUkp = fu_;
+          double fv_ = rTV * (0.5 * (V(i, j, kk) + V(i, j, kk - 1)));
+          fv_ = fv_ + 0.25 * (W(i, j, kk) * G2(rA, i, j) * (G3(maskC, i, j, kk) - G3(maskC, i, j, kk - 1)) +
+                              W(i, j - 1, kk) * G2(rA, i, j - 1) * (G3(maskC, i, j - 1, kk) - G3(maskC, i, j - 1, kk - 1))) *
+                          V(i, j, kk);
+          fVerVkp = fv_;
+        }
+        // uTrans / vTrans (mom_fluxform.F:287-327)
+#define UTR(ii, jj) (U(ii, jj, k) * (G2(dyG, ii, jj) * drF * G3(hFacW, ii, jj, k)))
+#define VTR(ii, jj) (V(ii, jj, k) * (G2(dxG, ii, jj) * drF * G3(hFacS, ii, jj, k)))
+        const double fZi = 0.25 * (UTR(i, j) + UTR(i + 1, j)) * (U(i, j, k) + U(i + 1, j, k));
+        const double fZm = 0.25 * (UTR(i - 1, j) + UTR(i, j)) * (U(i - 1, j, k) + U(i, j, k));
+        const double fMp = 0.25 * (VTR(i, j + 1) + VTR(i - 1, j + 1)) * (U(i, j + 1, k) + U(i, j, k));
+        const double fMi = 0.25 * (VTR(i, j) + VTR(i - 1, j)) * (U(i, j, k) + U(i, j - 1, k));
+        gU = -rhFacW * recip_drF * G2(recip_rAw, i, j) *
+             ((fZi - fZm) * uDudxFac + (fMp - fMi) * vDudyFac + (fVerUkp - fVerUkm) * p.rkSign * rVelDudrFac);
+        const double gZp = 0.25 * (UTR(i + 1, j) + UTR(i + 1, j - 1)) * (V(i + 1, j, k) + V(i, j, k));
+        const double gZi = 0.25 * (UTR(i, j) + UTR(i, j - 1)) * (V(i, j, k) + V(i - 1, j, k));
+        const double gMi = 0.25 * (VTR(i, j) + VTR(i, j + 1)) * (V(i, j, k) + V(i, j + 1, k));
+        const double gMm = 0.25 * (VTR(i, j - 1) + VTR(i, j)) * (V(i, j - 1, k) + V(i, j, k));
+        gV = -rhFacS * recip_drF * G2(recip_rAs, i, j) *
+             ((gZp - gZi) * uDudxFac + (gMi - gMm) * vDudyFac + (fVerVkp - fVerVkm) * p.rkSign * rVelDudrFac);
+#undef UTR
+#undef VTR
+      }
+      // ---------------- viscosity (mom_u/v_x/y/rviscflux.F, sidedrag, botdrag)
+      if (p.momViscosity) {
+        // U: xviscflux at i and i-1, yviscflux at j+1 and j
+        const double fZi = G2(dyF, i, j) * drF * G3(hFacC, i, j, k) *
+                           (-p.viscAhD * (U(i + 1, j, k) - U(i, j, k)) * 1.0 + p.viscA4D * 0.0 * 1.0) * G2(recip_dxF, i, j);
+        const double fZm = G2(dyF, i - 1, j) * drF * G3(hFacC, i - 1, j, k) *
+                           (-p.viscAhD * (U(i, j, k) - U(i - 1, j, k)) * 1.0 + p.viscA4D * 0.0 * 1.0) * G2(recip_dxF, i - 1, j);
+        const double hZp = hfacz(d, f, i, j + 1, k, t);
+        const double fMp = G2(dxV, i, j + 1) * drF * hZp * (-p.viscAhZ * (U(i, j + 1, k) - U(i, j, k)) + p.viscA4Z * 0.0) *
+                           G2(recip_dyU, i, j + 1);
+        const double fMi = G2(dxV, i, j) * drF * hZ * (-p.viscAhZ * (U(i, j, k) - U(i, j - 1, k)) + p.viscA4Z * 0.0) *
+                           G2(recip_dyU, i, j);
+        double fVrUp = 0.0, fVrDw = 0.0;
+        if (k > 1)
+          fVrUp = -p.viscAr * G2(rAw, i, j) * (U(i, j, k) - U(i, j, k - 1)) * p.rkSign * f.recip_drC[k - 1] *
+                  G3(maskW, i, j, k) * G3(maskW, i, j, k - 1);
+        if (k + 1 <= Nr)
+          fVrDw = -p.viscAr * G2(rAw, i, j) * (U(i, j, k + 1) - U(i, j, k)) * p.rkSign * f.recip_drC[k] *
+                  G3(maskW, i, j, k + 1) * G3(maskW, i, j, k);
+        guDiss = -rhFacW * recip_drF * G2(recip_rAw, i, j) *
+                 ((fZi - fZm) * AhDudxFac + (fMp - fMi) * AhDudyFac + (fVrDw - fVrUp) * p.rkSign * ArDudrFac);
+        if (p.no_slip_sides) {
+          const double hS = G3(hFacW, i, j, k) - hZ;
+          const double hN = G3(hFacW, i, j, k) - hZp;
+          const double u0 = U(i, j, k);
+          const double vF = -rhFacW * recip_drF * G2(recip_rAw, i, j) *
+                            (hS * G2(dxV, i, j) * G2(recip_dyU, i, j) * (p.viscAhZ * u0 - p.viscA4Z * 0.0) +
+                             hN * G2(dxV, i, j + 1) * G2(recip_dyU, i, j + 1) * (p.viscAhZ * u0 - p.viscA4Z * 0.0)) *
+                            drF * p.sideDragFactor;
+          guDiss = guDiss + vF;
+        }
+        if (p.no_slip_bottom) {
+          const int kDn = (k + 1 < Nr) ? k + 1 : Nr, kLowF = k + 1;
+          const double recDrC = (k == Nr) ? recip_drF : f.recip_drC[kLowF - 1];
+          double cD = 0.0 * 1.0;
+          cD = cD + p.viscAr * recDrC * 2.0;
+          cD = (k == Nr) ? cD * G3(maskW, i, j, k) : cD * G3(maskW, i, j, k) * (1.0 - G3(maskW, i, j, kDn));
+          guDiss = guDiss - cD * U(i, j, k) * rhFacW * recip_drF;
+        }
+        // V: xviscflux at i+1 and i, yviscflux at j and j-1
+        const double hZe = hfacz(d, f, i + 1, j, k, t);
+        const double gZp = G2(dyU, i + 1, j) * drF * hZe * (-p.viscAhZ * (V(i + 1, j, k) - V(i, j, k)) * 1.0 + p.viscA4Z * 0.0 * 1.0) *
+                           G2(recip_dxV, i + 1, j);
+        const double gZi = G2(dyU, i, j) * drF * hZ * (-p.viscAhZ * (V(i, j, k) - V(i - 1, j, k)) * 1.0 + p.viscA4Z * 0.0 * 1.0) *
+                           G2(recip_dxV, i, j);
+        const double gMi = G2(dxF, i, j) * drF * G3(hFacC, i, j, k) * (-p.viscAhD * (V(i, j + 1, k) - V(i, j, k)) + p.viscA4D * 0.0) *
+                           G2(recip_dyF, i, j);
+        const double gMm = G2(dxF, i, j - 1) * drF * G3(hFacC, i, j - 1, k) *
+                           (-p.viscAhD * (V(i, j, k) - V(i, j - 1, k)) + p.viscA4D * 0.0) * G2(recip_dyF, i, j - 1);
+        double gVrUp = 0.0, gVrDw = 0.0;
+        if (k > 1)
+          gVrUp = -p.viscAr * G2(rAs, i, j) * (V(i, j, k) - V(i, j, k - 1)) * p.rkSign * f.recip_drC[k - 1] *
+                  G3(maskS, i, j, k) * G3(maskS, i, j, k - 1);
+        if (k + 1 <= Nr)
+          gVrDw = -p.viscAr * G2(rAs, i, j) * (V(i, j, k + 1) - V(i, j, k)) * p.rkSign * f.recip_drC[k] *
+                  G3(maskS, i, j, k + 1) * G3(maskS, i, j, k);
+        gvDiss = -rhFacS * recip_drF * G2(recip_rAs, i, j) *
+                 ((gZp - gZi) * AhDudxFac + (gMi - gMm) * AhDudyFac + (gVrDw - gVrUp) * p.rkSign * ArDudrFac);
+        if (p.no_slip_sides) {
+          const double hW = G3(hFacS, i, j, k) - hZ;
+          const double hE = G3(hFacS, i, j, k) - hZe;
+          const double v0 = V(i, j, k);
+          const double vF = -rhFacS * recip_drF * G2(recip_rAs, i, j) *
+                            (hW * G2(dyU, i, j) * G2(recip_dxV, i, j) * (p.viscAhZ * v0 - p.viscA4Z * 0.0) +
+                             hE * G2(dyU, i + 1, j) * G2(recip_dxV, i + 1, j) * (p.viscAhZ * v0 - p.viscA4Z * 0.0)) *
+                            drF * p.sideDragFactor;
+          gvDiss = gvDiss + vF;
+        }
+        if (p.no_slip_bottom) {
+          const int kDn = (k + 1 < Nr) ? k + 1 : Nr, kLowF = k + 1;
+          const double recDrC = (k == Nr) ? recip_drF : f.recip_drC[kLowF - 1];
+          double cD = 0.0 * 1.0;
+          cD = cD + p.viscAr * recDrC * 2.0;
+          cD = (k == Nr) ? cD * G3(maskS, i, j, k) : cD * G3(maskS, i, j, k) * (1.0 - G3(maskS, i, j, kDn));
+          gvDiss = gvDiss - cD * V(i, j, k) * rhFacS * recip_drF;
+        }
+      }
+      // ---------------- Coriolis (mom_u_coriolis.F, mom_v_coriolis.F)
+      if (p.useCoriolis) {
+        const int sc = p.selectCoriScheme;
+        double c;
+        if (sc >= 2)
+          c = 0.5 * (G2(fCori, i, j) * 0.5 * (V(i, j, k) + V(i, j + 1, k)) +
+                     G2(fCori, i - 1, j) * 0.5 * (V(i - 1, j, k) + V(i - 1, j + 1, k)));
+        else
+          c = 0.5 * (G2(fCori, i, j) + G2(fCori, i - 1, j)) * 0.25 *
+              (V(i, j, k) + V(i, j + 1, k) + V(i - 1, j, k) + V(i - 1, j + 1, k));
+        if (sc == 1 || sc == 3)
+          c = c * 4.0 / fmax(1.0, G3(maskS, i, j, k) + G3(maskS, i, j + 1, k) + G3(maskS, i - 1, j, k) + G3(maskS, i - 1, j + 1, k));
+        gU = gU + fuFac * c;
+        if (sc >= 2)
+          c = -0.5 * (G2(fCori, i, j) * 0.5 * (U(i, j, k) + U(i + 1, j, k)) +
+                      G2(fCori, i, j - 1) * 0.5 * (U(i, j - 1, k) + U(i + 1, j - 1, k)));
+        else
+          c = -0.5 * (G2(fCori, i, j) + G2(fCori, i, j - 1)) * 0.25 *
+              (U(i, j, k) + U(i + 1, j, k) + U(i, j - 1, k) + U(i + 1, j - 1, k));
+        if (sc == 1 || sc == 3)
+          c = c * 4.0 / fmax(1.0, G3(maskW, i, j, k) + G3(maskW, i + 1, j, k) + G3(maskW, i, j - 1, k) + G3(maskW, i + 1, j - 1, k));
+        gV = gV + fvFac * c;
+      }
+      // mom_fluxform.F:1044-1051
+      gU = gU * G3(maskW, i, j, k);
+      guDiss = guDiss * G3(maskW, i, j, k);
+      gV = gV * G3(maskS, i, j, k);
+      gvDiss = gvDiss * G3(maskS, i, j, k);
+    }
+    // ---------------- TIMESTEP (timestep.F:104-388)
+    double guExt = 0.0, gvExt = 0.0;
+    if (p.momForcing && k == 1) {
+      // APPLY_FORCING_U/V (apply_forcing.F:81-88) on j=0..sNy+1,i=1..sNx+1 (U) / i=0..sNx+1,j=1..sNy+1 (V)
+      if (j >= 0 && j <= d.sNy + 1 && i >= 1 && i <= d.sNx + 1)
+        guExt = guExt + p.foFacMom * (f.fu[q2] * mass2rUnit) * recip_drF * G3(recip_hFacW, i, j, k);
+      if (j >= 1 && j <= d.sNy + 1 && i >= 0 && i <= d.sNx + 1)
+        gvExt = gvExt + p.foFacMom * (f.fv[q2] * mass2rUnit) * recip_drF * G3(recip_hFacS, i, j, k);
+    }
+    if (inner) {
+      if (p.momViscosity && p.momDissip_In_AB) { gU = gU + guDiss; gV = gV + gvDiss; }
+      if (p.momForcing && p.momForcingOutAB != 1) { gU = gU + guExt; gV = gV + gvExt; }
+    }
+    // ADAMS_BASHFORTH2 over the whole halo-inclusive slab (adams_bashforth2.F:81-88)
+    const long q3 = MG_I3(d, i, j, k, t);
+    {
+      const double gUo = f.guNm1[q3], gVo = f.gvNm1[q3];
+      double a = abFac * (gU - gUo);
+      f.guNm1[q3] = gU;
+      gU = gU + a;
+      a = abFac * (gV - gVo);
+      f.gvNm1[q3] = gV;
+      gV = gV + a;
+    }
+    if (inner) {
+      double gUtmp = gU, gVtmp = gV;
+      if (p.momForcing && p.momForcingOutAB == 1) { gUtmp = gUtmp + guExt; gVtmp = gVtmp + gvExt; }
+      if (p.momViscosity && !p.momDissip_In_AB) { gUtmp = gUtmp + guDiss; gVtmp = gVtmp + gvDiss; }
+      // u* = u + dt*(gUtmp + gUdPx)*maskW  (timestep.F:373-388), gUdPx = 0 for implicSurfPress = 1
+      gU = U(i, j, k) + p.deltaTMom * (gUtmp + 0.0) * G3(maskW, i, j, k);
+      gV = V(i, j, k) + p.deltaTMom * (gVtmp + 0.0) * G3(maskS, i, j, k);
+    }
+    f.gU[q3] = gU;
+    f.gV[q3] = gV;
+    fVerUkm = fVerUkp;
+    fVerVkm = fVerVkp;
+  }
+#undef U
+#undef V
+#undef W
+#undef G2
+#undef G3
+}
+
+hipError_t launch_mom_step(const Dims &d, const Params &p, const Fields &f, const int *iterPtr, hipStream_t s) {
+  dim3 blk(64, 4, 1);
+  dim3 grd((d.nx + 63) / 64, (d.ny + 3) / 4, d.nTiles);
+  hipLaunchKernelGGL(k_mom_step, grd, blk, 0, s, d, p, f, iterPtr);
+  return hipGetLastError();
+}
+
+}  // namespace mgcm

@@ -1,0 +1,435 @@
+// kernels_solve.hip -- SOLVE_FOR_PRESSURE on the MI355X.
+//
+// Reference: model/src/solve_for_pressure.F:7-468, model/src/calc_div_ghat.F:6-201,
+//            model/src/cg2d.F:13-415, eesupp/src/global_sum_tile.F:14-237,
+//            model/src/momentum_correction_step.F:7-131, correction_step.F:150-234,
+//            model/src/integr_continuity.F:276-314, integrate_for_w.F:61-195.
+//
+// CG2D is latency-bound at the BASELINE grids (3.6k-6k points, ~100 iterations
+// per solve, 3 global sums + 2 halo exchanges per iteration in the reference):
+// a launch per phase would cost more than the arithmetic.  k_cg2d_block runs
+// the WHOLE solve in ONE workgroup of 1024 threads:
+//   * r and s live in LDS (interior points only, compact); the halo exchange
+//     of EXCH_S3D_RL becomes a neighbour-index table (halo point -> the interior
+//     point it is a copy of), so an exchange costs nothing;
+//   * x, s, r and (as register room allows) the 10 operator coefficients of
+//     each point stay in VGPRs;
+//   * each global sum is a wave64 butterfly (DPP/shfl_xor) + one LDS slot per
+//     wave + one barrier; every thread then adds the 16 wave partials in the
+//     same fixed order, so all lanes hold bit-identical sums (no broadcast,
+//     run-to-run deterministic).
+#include "common.h"
+
+namespace mgcm {
+
+constexpr int CG_THREADS = 1024;
+constexpr int CG_WAVES = CG_THREADS / 64;
+
+__device__ __forceinline__ double wave_sum(double v) {
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ __forceinline__ double wave_max(double v) {
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) v = fmax(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+// Block-wide sum; `slot` selects one of 4 rotating LDS partial buffers so that
+// consecutive reductions need only the one barrier each.
+__device__ __forceinline__ double block_sum(double v, double *red, int slot) {
+  v = wave_sum(v);
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  if (lane == 0) red[slot * CG_WAVES + wv] = v;
+  __syncthreads();
+  double s = 0.0;
+#pragma unroll
+  for (int w = 0; w < CG_WAVES; w++) s = s + red[slot * CG_WAVES + w];
+  return s;
+}
+__device__ __forceinline__ double block_max(double v, double *red, int slot) {
+  v = wave_max(v);
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  if (lane == 0) red[slot * CG_WAVES + wv] = v;
+  __syncthreads();
+  double s = red[slot * CG_WAVES];
+#pragma unroll
+  for (int w = 1; w < CG_WAVES; w++) s = fmax(s, red[slot * CG_WAVES + w]);
+  return s;
+}
+
+// CALC_DIV_GHAT over k = Nr..1 + free-surface term; cg2d_x = Bo_surf*etaN (full range).
+__global__ void __launch_bounds__(256) k_sfp_rhs(Dims d, Params p, Fields f) {
+  const int i = (int)(blockIdx.x * blockDim.x + threadIdx.x) + 1 - d.OLx;
+  const int j = (int)(blockIdx.y * blockDim.y + threadIdx.y) + 1 - d.OLy;
+  const int t = (int)blockIdx.z;
+  if (i > d.sNx + d.OLx || j > d.sNy + d.OLy) return;
+  const long q = MG_I2(d, i, j, t);
+  f.cg2d_x[q] = f.Bo_surf[q] * f.etaN[q];
+  double b = 0.0;
+  if (i >= 1 && i <= d.sNx && j >= 1 && j <= d.sNy) {
+    for (int k = d.Nr; k >= 1; k--) {
+      const double drF = f.drF[k - 1];
+      const double pfE = f.dyG[MG_I2(d, i + 1, j, t)] * drF * f.hFacW[MG_I3(d, i + 1, j, k, t)] *
+                         f.gU[MG_I3(d, i + 1, j, k, t)] / p.deltaTMom;
+      const double pfW = f.dyG[q] * drF * f.hFacW[MG_I3(d, i, j, k, t)] * f.gU[MG_I3(d, i, j, k, t)] / p.deltaTMom;
+      b = b + pfE - pfW;
+      const double pfN = f.dxG[MG_I2(d, i, j + 1, t)] * drF * f.hFacS[MG_I3(d, i, j + 1, k, t)] *
+                         f.gV[MG_I3(d, i, j + 1, k, t)] / p.deltaTMom;
+      const double pfS = f.dxG[q] * drF * f.hFacS[MG_I3(d, i, j, k, t)] * f.gV[MG_I3(d, i, j, k, t)] / p.deltaTMom;
+      b = b + pfN - pfS;
+    }
+    // solve_for_pressure.F:245-254 (linear free surface, not exactConserv)
+    b = b - p.freeSurfFac * f.rA[q] / p.deltaTMom / p.deltaTFreeSurf * f.etaN[q];
+  }
+  f.cg2d_b[q] = b;
+}
+
+// Whole-solve CG2D in one workgroup.  PPT = interior points per thread.
+// Points are padded to NP = PPT*1024: a padding point has x = b = 0, every
+// neighbour index pointing at the ZERO slot (index NP, never written), so it
+// stays exactly 0 through every phase and the per-point code is branch-free.
+// nbr[2*NP]: packed compact neighbour indices (W | E<<16), (S | N<<16); when the
+// neighbour is a halo point, the index is the interior point the halo is a copy
+// of (EXCH_S3D_RL / EXCH_XY_RL).  CREG: how many of the two 5-coefficient sets
+// (A, then M) stay in VGPRs; the rest is re-read each use from L2.
+template <int PPT, bool MINRES, int CREG>
+__global__ void __launch_bounds__(CG_THREADS) k_cg2d_block(Dims d, Params p, Fields f, const unsigned *__restrict__ nbr,
+                                                          const int *__restrict__ gofs, int nPts, int maxIters,
+                                                          int nIterMinIn, SolveRecord *rec, int *stepCounter) {
+  constexpr int NP = PPT * CG_THREADS;
+  extern __shared__ __attribute__((aligned(16))) double lds[];
+  double *r_l = lds;                // NP + 1 (last = ZERO slot)
+  double *s_l = lds + (NP + 1);     // NP + 1
+  double *red = lds + 2 * (NP + 1); // 4 * CG_WAVES
+  const int tid = threadIdx.x;
+  constexpr int RA = (CREG >= 1) ? PPT : 1, RM = (CREG >= 2) ? PPT : 1, RX = MINRES ? PPT : 1;
+
+  unsigned g[PPT];  // BYTE offset of the point in a 2-D field (32-bit: saddr-mode loads)
+  unsigned nwe[PPT], nsn[PPT];
+  double x[PPT], s[PPT], r[PPT], xmin[RX];
+  double aW0r[RA], aW1r[RA], aS0r[RA], aS1r[RA], aCr[RA];
+  double pCr[RM], pW0r[RM], pW1r[RM], pS0r[RM], pS1r[RM];
+  const unsigned dE = 8u, dN = 8u * (unsigned)d.nx;
+  // buffer descriptors (32-bit voffset + immediate offsets: one VGPR per point
+  // addresses all ten coefficient loads; guide T8)
+  const unsigned fbytes = (unsigned)(8 * d.n2 * d.nTiles);
+  const __amdgpu_buffer_rsrc_t rsW = __builtin_amdgcn_make_buffer_rsrc((void *)f.aW2d, 0, fbytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rsS = __builtin_amdgcn_make_buffer_rsrc((void *)f.aS2d, 0, fbytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rsC = __builtin_amdgcn_make_buffer_rsrc((void *)f.aC2d, 0, fbytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rpW = __builtin_amdgcn_make_buffer_rsrc((void *)f.pW, 0, fbytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rpS = __builtin_amdgcn_make_buffer_rsrc((void *)f.pS, 0, fbytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rpC = __builtin_amdgcn_make_buffer_rsrc((void *)f.pC, 0, fbytes, 0x00020000);
+#define BLD(rs, off) __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(rs, (off), 0, 0))
+#define LDO(base, off) (*(const double *)((const char *)(base) + (off)))
+#define STO(base, off) (*(double *)((char *)(base) + (off)))
+#define aW0(m) ((CREG >= 1) ? aW0r[(CREG >= 1) ? m : 0] : BLD(rsW, g[m]))
+#define aW1(m) ((CREG >= 1) ? aW1r[(CREG >= 1) ? m : 0] : BLD(rsW, g[m] + dE))
+#define aS0(m) ((CREG >= 1) ? aS0r[(CREG >= 1) ? m : 0] : BLD(rsS, g[m]))
+#define aS1(m) ((CREG >= 1) ? aS1r[(CREG >= 1) ? m : 0] : BLD(rsS, g[m] + dN))
+#define aC(m) ((CREG >= 1) ? aCr[(CREG >= 1) ? m : 0] : BLD(rsC, g[m]))
+#define pC(m) ((CREG >= 2) ? pCr[(CREG >= 2) ? m : 0] : BLD(rpC, g[m]))
+#define pW0(m) ((CREG >= 2) ? pW0r[(CREG >= 2) ? m : 0] : BLD(rpW, g[m]))
+#define pW1(m) ((CREG >= 2) ? pW1r[(CREG >= 2) ? m : 0] : BLD(rpW, g[m] + dE))
+#define pS0(m) ((CREG >= 2) ? pS0r[(CREG >= 2) ? m : 0] : BLD(rpS, g[m]))
+#define pS1(m) ((CREG >= 2) ? pS1r[(CREG >= 2) ? m : 0] : BLD(rpS, g[m] + dN))
+#define LO(w) ((w) & 0xFFFFu)
+#define HI(w) ((w) >> 16)
+#define ACT(m) (tid + (m) * CG_THREADS < nPts)
+
+  if (tid == 0) { r_l[NP] = 0.0; s_l[NP] = 0.0; }
+  double b[PPT];
+#pragma unroll
+  for (int m = 0; m < PPT; m++) {
+    const int pt = tid + m * CG_THREADS;
+    g[m] = 8u * (unsigned)gofs[pt];
+    nwe[m] = nbr[2 * pt];
+    nsn[m] = nbr[2 * pt + 1];
+    if (CREG >= 1) {
+      const int mm = (CREG >= 1) ? m : 0;
+      aW0r[mm] = BLD(rsW, g[m]); aW1r[mm] = BLD(rsW, g[m] + dE); aS0r[mm] = BLD(rsS, g[m]); aS1r[mm] = BLD(rsS, g[m] + dN);
+      aCr[mm] = BLD(rsC, g[m]);
+    }
+    if (CREG >= 2) {
+      const int mm = (CREG >= 2) ? m : 0;
+      pCr[mm] = BLD(rpC, g[m]); pW0r[mm] = BLD(rpW, g[m]); pW1r[mm] = BLD(rpW, g[m] + dE); pS0r[mm] = BLD(rpS, g[m]);
+      pS1r[mm] = BLD(rpS, g[m] + dN);
+    }
+    b[m] = ACT(m) ? LDO(f.cg2d_b, g[m]) : 0.0;
+    x[m] = ACT(m) ? LDO(f.cg2d_x, g[m]) : 0.0;
+    s[m] = 0.0;
+  }
+
+  // cg2d.F:104-133: normalise the RHS
+  double rhsMax = 0.0;
+#pragma unroll
+  for (int m = 0; m < PPT; m++) { b[m] = b[m] * p.cg2dNorm; rhsMax = fmax(fabs(b[m]), rhsMax); }
+  rhsMax = block_max(rhsMax, red, 0);
+  double rhsNorm = 1.0;
+  if (p.cg2dNormaliseRHS) {
+    if (rhsMax != 0.0) rhsNorm = 1.0 / rhsMax;
+#pragma unroll
+    for (int m = 0; m < PPT; m++) { b[m] = b[m] * rhsNorm; x[m] = x[m] * rhsNorm; }
+  }
+  // EXCH_XY_RL(cg2d_x): the neighbours' x values come through LDS
+#pragma unroll
+  for (int m = 0; m < PPT; m++) s_l[tid + m * CG_THREADS] = x[m];
+  __syncthreads();
+  // cg2d.F:139-180: r = b - A x ; err_sq, sumRHS
+  double err = 0.0, sumB = 0.0;
+#pragma unroll
+  for (int m = 0; m < PPT; m++) {
+    r[m] = b[m] - (aW0(m) * s_l[LO(nwe[m])] + aW1(m) * s_l[HI(nwe[m])] + aS0(m) * s_l[LO(nsn[m])] +
+                   aS1(m) * s_l[HI(nsn[m])] + aC(m) * x[m]);
+    err = err + r[m] * r[m];
+    sumB = sumB + b[m];
+    if (MINRES) xmin[MINRES ? m : 0] = x[m];
+  }
+#pragma unroll
+  for (int m = 0; m < PPT; m++)
+    if (ACT(m)) STO(f.cg2d_b, g[m]) = b[m];  // cg2d_b is INOUT (normalised in place)
+  double err_sq = block_sum(err, red, 1);
+  const double sumRHS = block_sum(sumB, red, 2);
+  // EXCH_S3D_RL(cg2d_r): r into LDS; s_l re-zeroed for s = q + beta*s
+#pragma unroll
+  for (int m = 0; m < PPT; m++) { r_l[tid + m * CG_THREADS] = r[m]; s_l[tid + m * CG_THREADS] = 0.0; }
+  const double firstResidual = sqrt(err_sq);
+  int nIterMin = nIterMinIn;
+  double minResidualSq = -1.0;
+  if (MINRES && nIterMin >= 0) { nIterMin = 0; minResidualSq = err_sq; }
+  int actualIts = 0;
+  double eta_qrNM1 = 1.0;
+  __syncthreads();
+  int slot = 3;
+  if (!(err_sq < p.cg2dTolerance_sq)) {
+    for (int it2d = 1; it2d <= maxIters; it2d++) {
+      // keep L2-resident coefficients out of VGPRs: forbid hoisting their loads
+      if (CREG < 2) asm volatile("" ::: "memory");
+      // q = M r ; eta_qrN = sum q*r   (cg2d.F:211-243)
+      double q[PPT];
+      double e = 0.0;
+#pragma unroll
+      for (int m = 0; m < PPT; m++) {
+        q[m] = pC(m) * r[m] + pW0(m) * r_l[LO(nwe[m])] + pW1(m) * r_l[HI(nwe[m])] + pS0(m) * r_l[LO(nsn[m])] +
+               pS1(m) * r_l[HI(nsn[m])];
+        e = e + q[m] * r[m];
+      }
+      slot = (slot + 1) & 3;
+      const double eta_qrN = block_sum(e, red, slot);
+      const double cgBeta = eta_qrN / eta_qrNM1;
+      eta_qrNM1 = eta_qrN;
+      // s = q + beta*s ; EXCH_S3D_RL(cg2d_s)
+#pragma unroll
+      for (int m = 0; m < PPT; m++) { s[m] = q[m] + cgBeta * s[m]; s_l[tid + m * CG_THREADS] = s[m]; }
+      __syncthreads();
+      // q = A s ; alpha = sum s*q   (cg2d.F:268-301)
+      double a = 0.0;
+#pragma unroll
+      for (int m = 0; m < PPT; m++) {
+        q[m] = aW0(m) * s_l[LO(nwe[m])] + aW1(m) * s_l[HI(nwe[m])] + aS0(m) * s_l[LO(nsn[m])] +
+               aS1(m) * s_l[HI(nsn[m])] + aC(m) * s[m];
+        a = a + s[m] * q[m];
+      }
+      slot = (slot + 1) & 3;
+      double alpha = block_sum(a, red, slot);
+      alpha = eta_qrN / alpha;
+      // x += alpha s ; r -= alpha q ; err_sq   (cg2d.F:305-328)
+      double e2 = 0.0;
+#pragma unroll
+      for (int m = 0; m < PPT; m++) {
+        x[m] = x[m] + alpha * s[m];
+        r[m] = r[m] - alpha * q[m];
+        e2 = e2 + r[m] * r[m];
+        r_l[tid + m * CG_THREADS] = r[m];
+      }
+      actualIts = it2d;
+      slot = (slot + 1) & 3;
+      err_sq = block_sum(e2, red, slot);  // its barrier also publishes r_l (EXCH_S3D_RL(cg2d_r))
+      if (err_sq < p.cg2dTolerance_sq) break;
+      if (MINRES && err_sq < minResidualSq) {
+        minResidualSq = err_sq;
+        nIterMin = it2d;
+#pragma unroll
+        for (int m = 0; m < PPT; m++) xmin[MINRES ? m : 0] = x[m];
+      }
+    }
+  }
+  if (MINRES && nIterMin >= 0 && err_sq > minResidualSq) {
+#pragma unroll
+    for (int m = 0; m < PPT; m++) x[m] = xmin[MINRES ? m : 0];
+  }
+#pragma unroll
+  for (int m = 0; m < PPT; m++) {
+    if (p.cg2dNormaliseRHS) x[m] = x[m] / rhsNorm;
+    if (ACT(m)) STO(f.cg2d_x, g[m]) = x[m];
+  }
+  if (tid == 0) {
+    const int st = stepCounter ? *stepCounter : 0;
+    SolveRecord &R = rec[st];
+    R.firstResidual = firstResidual;
+    R.lastResidual = sqrt(err_sq);
+    R.minResidualSq = minResidualSq;
+    R.rhsMax = rhsMax;
+    R.sumRHS = sumRHS;
+    R.numIters = actualIts;
+    R.nIterMin = nIterMin;
+  }
+#undef LO
+#undef HI
+#undef ACT
+#undef LDO
+#undef BLD
+#undef STO
+#undef aW0
+#undef aW1
+#undef aS0
+#undef aS1
+#undef aC
+#undef pC
+#undef pW0
+#undef pW1
+#undef pS0
+#undef pS1
+}
+
+// Halo exchange of `nz` levels through a precomputed map (EXCH1 / EXCH2 scalar).
+// map[2*h] = destination 2-D flat offset (t*n2+local), map[2*h+1] = source.
+__global__ void __launch_bounds__(256) k_exchange(Dims d, double *a, const long *__restrict__ map, int nHalo, int nz) {
+  const int h = (int)(blockIdx.x * blockDim.x + threadIdx.x);
+  const int k = (int)blockIdx.y;
+  if (h >= nHalo || k >= nz) return;
+  const long dst = map[2 * h], src = map[2 * h + 1];
+  const long dt = dst / d.n2, dl = dst % d.n2, st = src / d.n2, sl = src % d.n2;
+  const long lvl = (long)d.n2 * nz;
+  a[dt * lvl + (long)k * d.n2 + dl] = a[st * lvl + (long)k * d.n2 + sl];
+}
+
+// After CG2D: EXCH_XY_RL(cg2d_x) (solve_for_pressure.F:316) is done by k_exchange on
+// cg2d_x; then etaN = recip_Bo * cg2d_x (solve_for_pressure.F:377-385).
+__global__ void __launch_bounds__(256) k_eta_update(Dims d, Fields f) {
+  const long q = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (q >= d.n2 * d.nTiles) return;
+  f.etaN[q] = f.recip_Bo[q] * f.cg2d_x[q];
+}
+
+// MOMENTUM_CORRECTION_STEP over i=2-OLx..sNx+OLx, j=2-OLy..sNy+OLy, all k.
+__global__ void __launch_bounds__(256) k_correction(Dims d, Params p, Fields f) {
+  const int i = (int)(blockIdx.x * blockDim.x + threadIdx.x) + 2 - d.OLx;
+  const int j = (int)(blockIdx.y * blockDim.y + threadIdx.y) + 2 - d.OLy;
+  const int t = (int)blockIdx.z;
+  if (i > d.sNx + d.OLx || j > d.sNy + d.OLy) return;
+  const double psFac = p.pfFacMom * p.implicSurfPress;
+  const long q = MG_I2(d, i, j, t);
+  const double phiSurfX =
+      f.recip_dxC[q] * (f.Bo_surf[q] * f.etaN[q] - f.Bo_surf[MG_I2(d, i - 1, j, t)] * f.etaN[MG_I2(d, i - 1, j, t)]);
+  const double phiSurfY =
+      f.recip_dyC[q] * (f.Bo_surf[q] * f.etaN[q] - f.Bo_surf[MG_I2(d, i, j - 1, t)] * f.etaN[MG_I2(d, i, j - 1, t)]);
+  for (int k = 1; k <= d.Nr; k++) {
+    const long q3 = MG_I3(d, i, j, k, t);
+    const double mW = f.maskW[q3], mS = f.maskS[q3];
+    const double gU_dpx = -psFac * phiSurfX * mW;
+    const double gV_dpy = -psFac * phiSurfY * mS;
+    f.uVel[q3] = (f.gU[q3] + p.deltaTMom * gU_dpx) * mW;
+    f.vVel[q3] = (f.gV[q3] + p.deltaTMom * gV_dpy) * mS;
+  }
+}
+
+// INTEGR_CONTINUITY -> INTEGRATE_FOR_W, interior columns, k = Nr..1.
+__global__ void __launch_bounds__(256) k_continuity(Dims d, Fields f) {
+  const int i = (int)(blockIdx.x * blockDim.x + threadIdx.x) + 1;
+  const int j = (int)(blockIdx.y * blockDim.y + threadIdx.y) + 1;
+  const int t = (int)blockIdx.z;
+  if (i > d.sNx || j > d.sNy) return;
+  const long q = MG_I2(d, i, j, t);
+  double wBelow = 0.0;
+  for (int k = d.Nr; k >= 1; k--) {
+    const double drF = f.drF[k - 1];
+    const double uT1 = f.uVel[MG_I3(d, i + 1, j, k, t)] * f.dyG[MG_I2(d, i + 1, j, t)] * drF * f.hFacW[MG_I3(d, i + 1, j, k, t)];
+    const double uT0 = f.uVel[MG_I3(d, i, j, k, t)] * f.dyG[q] * drF * f.hFacW[MG_I3(d, i, j, k, t)];
+    const double vT1 = f.vVel[MG_I3(d, i, j + 1, k, t)] * f.dxG[MG_I2(d, i, j + 1, t)] * drF * f.hFacS[MG_I3(d, i, j + 1, k, t)];
+    const double vT0 = f.vVel[MG_I3(d, i, j, k, t)] * f.dxG[q] * drF * f.hFacS[MG_I3(d, i, j, k, t)];
+    const double conv2d = -(uT1 - uT0 + vT1 - vT0);
+    double w;
+    if (k == d.Nr) w = conv2d * f.recip_rA[q] * f.maskC[MG_I3(d, i, j, k, t)];
+    else w = (wBelow + conv2d * f.recip_rA[q]) * f.maskC[MG_I3(d, i, j, k, t)];
+    f.wVel[MG_I3(d, i, j, k, t)] = w;
+    wBelow = w;
+  }
+}
+
+__global__ void k_bump_counter(int *c, int nIncr) {
+  if (threadIdx.x == 0) { c[0] += nIncr; c[1] += 1; }
+}
+
+// ------------------------------------------------------------------ launchers
+hipError_t launch_sfp_rhs(const Dims &d, const Params &p, const Fields &f, hipStream_t s) {
+  dim3 blk(64, 4, 1), grd((d.nx + 63) / 64, (d.ny + 3) / 4, d.nTiles);
+  hipLaunchKernelGGL(k_sfp_rhs, grd, blk, 0, s, d, p, f);
+  return hipGetLastError();
+}
+
+int cg2d_block_ppt(int nPts) {
+  for (int ppt = 1; ppt <= 8; ppt *= 2)
+    if (nPts <= ppt * CG_THREADS) return ppt;
+  return 0;
+}
+size_t cg2d_block_lds_bytes(int ppt) { return (size_t)(2 * (ppt * CG_THREADS + 1) + 4 * CG_WAVES) * sizeof(double); }
+int cg2d_block_max_points() { return 8 * CG_THREADS; }  // LDS: 2*8193*8 B = 128 KiB
+
+hipError_t launch_cg2d_block(const Dims &d, const Params &p, const Fields &f, const unsigned *nbr, const int *gofs,
+                             int nPts, int maxIters, int nIterMin, SolveRecord *rec, int *stepCounter, hipStream_t s) {
+  const int ppt = cg2d_block_ppt(nPts);
+  if (!ppt) return hipErrorInvalidValue;
+  const size_t lds = cg2d_block_lds_bytes(ppt);
+  const bool mr = nIterMin >= 0;
+#define LAUNCH(PPT)                                                                                        \
+  do {                                                                                                     \
+    constexpr int CR = (PPT <= 2) ? 2 : 0;                                                \
+    auto kern = mr ? k_cg2d_block<PPT, true, CR> : k_cg2d_block<PPT, false, CR>;                           \
+    hipError_t e_ = hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds); \
+    if (e_ != hipSuccess) return e_;                                                                       \
+    hipLaunchKernelGGL(kern, dim3(1), dim3(CG_THREADS), lds, s, d, p, f, nbr, gofs, nPts, maxIters, nIterMin, rec, \
+                       stepCounter);                                                                       \
+  } while (0)
+  switch (ppt) {
+    case 1: LAUNCH(1); break;
+    case 2: LAUNCH(2); break;
+    case 4: LAUNCH(4); break;
+    default: LAUNCH(8); break;
+  }
+#undef LAUNCH
+  return hipGetLastError();
+}
+
+hipError_t launch_exchange(const Dims &d, double *a, const long *map, int nHalo, int nz, hipStream_t s) {
+  if (nHalo <= 0) return hipSuccess;
+  dim3 blk(256), grd((nHalo + 255) / 256, nz);
+  hipLaunchKernelGGL(k_exchange, grd, blk, 0, s, d, a, map, nHalo, nz);
+  return hipGetLastError();
+}
+
+hipError_t launch_eta_update(const Dims &d, const Fields &f, hipStream_t s) {
+  const long n = d.n2 * d.nTiles;
+  hipLaunchKernelGGL(k_eta_update, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, d, f);
+  return hipGetLastError();
+}
+
+hipError_t launch_correction(const Dims &d, const Params &p, const Fields &f, hipStream_t s) {
+  dim3 blk(64, 4, 1), grd((d.sNx + 2 * d.OLx - 1 + 63) / 64, (d.sNy + 2 * d.OLy - 1 + 3) / 4, d.nTiles);
+  hipLaunchKernelGGL(k_correction, grd, blk, 0, s, d, p, f);
+  return hipGetLastError();
+}
+
+hipError_t launch_continuity(const Dims &d, const Fields &f, hipStream_t s) {
+  dim3 blk(64, 4, 1), grd((d.sNx + 63) / 64, (d.sNy + 3) / 4, d.nTiles);
+  hipLaunchKernelGGL(k_continuity, grd, blk, 0, s, d, f);
+  return hipGetLastError();
+}
+
+hipError_t launch_bump_counter(int *c, int nIncr, hipStream_t s) {
+  hipLaunchKernelGGL(k_bump_counter, dim3(1), dim3(64), 0, s, c, nIncr);
+  return hipGetLastError();
+}
+
+}  // namespace mgcm

@@ -1,0 +1,621 @@
+// model.hip -- host runtime of the MI355X hot path and its C-ABI (include/mitgcm_amd.h).
+//
+// Owns the device mirror of the reference's per-tile COMMON blocks (DYNVARS.h,
+// GRID.h, SURFACE.h, FFIELDS.h, CG2D.h) for the tiles on one GPU, the halo
+// topology (EXCH1 lat-lon by default, any EXCH2 map via mgcm_set_halo_map), and
+// the launch sequence of FORWARD_STEP's device-resident subset.
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <map>
+#include <string>
+#include <vector>
+
+#include "../../include/mitgcm_amd.h"
+#include "common.h"
+
+namespace mgcm {
+hipError_t launch_mom_step(const Dims &, const Params &, const Fields &, const int *, hipStream_t);
+hipError_t launch_sfp_rhs(const Dims &, const Params &, const Fields &, hipStream_t);
+hipError_t launch_cg2d_block(const Dims &, const Params &, const Fields &, const unsigned *, const int *, int, int, int,
+                             SolveRecord *, int *, hipStream_t);
+int cg2d_block_ppt(int nPts);
+int cg2d_block_max_points();
+hipError_t launch_exchange(const Dims &, double *, const long *, int, int, hipStream_t);
+hipError_t launch_eta_update(const Dims &, const Fields &, hipStream_t);
+hipError_t launch_correction(const Dims &, const Params &, const Fields &, hipStream_t);
+hipError_t launch_continuity(const Dims &, const Fields &, hipStream_t);
+hipError_t launch_bump_counter(int *, int, hipStream_t);
+}  // namespace mgcm
+
+using namespace mgcm;
+
+static thread_local std::string g_err;
+static int set_err(const char *fmt, ...) {
+  char buf[1024];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof buf, fmt, ap);
+  va_end(ap);
+  g_err = buf;
+  return -1;
+}
+#define HIPCHK(x)                                                                              \
+  do {                                                                                         \
+    hipError_t e_ = (x);                                                                       \
+    if (e_ != hipSuccess) return set_err("%s:%d %s: %s", __FILE__, __LINE__, #x, hipGetErrorString(e_)); \
+  } while (0)
+
+enum FieldKind { F1D, F2D, F3D };
+struct FieldDesc {
+  const char *name;
+  FieldKind kind;
+  size_t off;  // offset of the pointer inside Fields
+};
+
+#define FD(n, k) {#n, k, offsetof(Fields, n)}
+static const FieldDesc FIELDS[] = {
+    FD(drF, F1D), FD(drC, F1D), FD(recip_drF, F1D), FD(recip_drC, F1D),
+    FD(dxF, F2D), FD(dyF, F2D), FD(dxG, F2D), FD(dyG, F2D), FD(dxC, F2D), FD(dyC, F2D), FD(dxV, F2D), FD(dyU, F2D),
+    FD(rA, F2D), FD(rAw, F2D), FD(rAs, F2D), FD(recip_dxF, F2D), FD(recip_dyF, F2D), FD(recip_dxC, F2D),
+    FD(recip_dyC, F2D), FD(recip_dxV, F2D), FD(recip_dyU, F2D), FD(recip_rA, F2D), FD(recip_rAw, F2D),
+    FD(recip_rAs, F2D), FD(fCori, F2D), FD(Bo_surf, F2D), FD(recip_Bo, F2D),
+    FD(hFacC, F3D), FD(hFacW, F3D), FD(hFacS, F3D), FD(recip_hFacW, F3D), FD(recip_hFacS, F3D),
+    FD(maskC, F3D), FD(maskW, F3D), FD(maskS, F3D),
+    FD(aW2d, F2D), FD(aS2d, F2D), FD(aC2d, F2D), FD(pW, F2D), FD(pS, F2D), FD(pC, F2D),
+    FD(uVel, F3D), FD(vVel, F3D), FD(wVel, F3D), FD(theta, F3D), FD(salt, F3D), FD(etaN, F2D),
+    FD(gU, F3D), FD(gV, F3D), FD(guNm1, F3D), FD(gvNm1, F3D), FD(fu, F2D), FD(fv, F2D),
+    FD(cg2d_b, F2D), FD(cg2d_x, F2D),
+};
+#undef FD
+
+struct PDesc {
+  const char *name;
+  size_t off;
+  bool isint;
+};
+#define PD(n) {#n, offsetof(Params, n), false}
+#define PI_(n) {#n, offsetof(Params, n), true}
+static const PDesc PARAMS[] = {
+    PD(deltaTMom), PD(deltaTFreeSurf), PD(deltaTClock), PD(abEps), PD(rhoConst), PD(gBaro), PD(viscAhD), PD(viscAhZ),
+    PD(viscA4D), PD(viscA4Z), PD(viscAr), PD(sideDragFactor), PD(freeSurfFac), PD(implicSurfPress),
+    PD(implicDiv2DFlow), PD(rkSign), PD(afFacMom), PD(vfFacMom), PD(pfFacMom), PD(cfFacMom), PD(foFacMom),
+    PD(mtFacMom), PD(cg2dNorm), PD(cg2dTolerance_sq),
+    PI_(momAdvection), PI_(momViscosity), PI_(momForcing), PI_(useCoriolis), PI_(no_slip_sides),
+    PI_(no_slip_bottom), PI_(selectCoriScheme), PI_(momForcingOutAB), PI_(momDissip_In_AB),
+    PI_(implicitViscosity), PI_(cg2dMaxIters), PI_(cg2dUseMinResSol), PI_(cg2dNormaliseRHS), PI_(nIter0),
+};
+#undef PD
+#undef PI_
+
+// kernel families timed with hipEvents when timing is enabled
+enum Kern { K_MOM, K_RHS, K_CG2D, K_EXCH, K_ETA, K_CORR, K_CONT, K_N };
+static const char *KNAMES[K_N] = {"mom_step", "sfp_rhs", "cg2d", "exchange", "eta_update", "correction", "continuity"};
+
+struct mgcm_model {
+  Dims d{};
+  Params p{};
+  Fields f{};
+  int device = 0;
+  hipStream_t stream = nullptr;
+  std::vector<void *> allocs;
+  // extra parameters kept on host only
+  std::map<std::string, double> extra;
+  // halo map (2*nHalo longs) and CG2D neighbour table
+  long *d_halo = nullptr;
+  int nHalo = 0;
+  std::vector<long> h_halo;
+  unsigned *d_nbr = nullptr;  // packed (W|E<<16),(S|N<<16) compact neighbour indices, padded
+  int *d_gofs = nullptr;      // 2-D flat offset of each (padded) interior point
+  int nPts = 0;
+  // step counters: [0] = myIter, [1] = record slot
+  int *d_ctr = nullptr;
+  SolveRecord *d_rec = nullptr;
+  int maxRec = 4096;
+  int lastBatch = 0;
+  bool ready = false;
+  // timing
+  bool timing = false;
+  std::vector<hipEvent_t> evPool;            // created once, reused
+  size_t evUsed = 0;
+  std::vector<std::pair<int, int>> evPairs;  // (kernel, start event index)
+  double kms[K_N] = {0};
+  int kcnt[K_N] = {0};
+};
+
+static long field_count(const mgcm_model *m, FieldKind k) {
+  if (k == F1D) return m->d.Nr + 1;
+  if (k == F2D) return m->d.n2 * m->d.nTiles;
+  return m->d.n3 * m->d.nTiles;
+}
+static const FieldDesc *find_field(const char *name) {
+  for (auto &fd : FIELDS)
+    if (!strcmp(fd.name, name)) return &fd;
+  return nullptr;
+}
+static double *&field_ptr(mgcm_model *m, const FieldDesc *fd) {
+  return *reinterpret_cast<double **>(reinterpret_cast<char *>(&m->f) + fd->off);
+}
+
+// ------------------------------------------------------------------ timing
+static int ev_next(mgcm_model *m) {
+  if (m->evUsed == m->evPool.size()) {
+    hipEvent_t e;
+    if (hipEventCreate(&e) != hipSuccess) return -1;
+    m->evPool.push_back(e);
+  }
+  return (int)m->evUsed++;
+}
+static int ev_begin(mgcm_model *m, int k) {
+  (void)k;
+  if (!m->timing) return -1;
+  const int i = ev_next(m);
+  if (i < 0) return -1;
+  hipEventRecord(m->evPool[i], m->stream);
+  return i;
+}
+static void ev_end(mgcm_model *m, int k, int startIdx) {
+  if (!m->timing || startIdx < 0) return;
+  const int i = ev_next(m);
+  if (i < 0) return;
+  hipEventRecord(m->evPool[i], m->stream);
+  m->evPairs.push_back({k, startIdx});
+}
+// call with the stream drained
+static void ev_collect(mgcm_model *m) {
+  for (auto &pr : m->evPairs) {
+    float ms = 0.f;
+    if (hipEventElapsedTime(&ms, m->evPool[pr.second], m->evPool[pr.second + 1]) == hipSuccess) {
+      m->kms[pr.first] += ms;
+      m->kcnt[pr.first] += 1;
+    }
+  }
+  m->evPairs.clear();
+  m->evUsed = 0;
+}
+static void ev_free(mgcm_model *m) {
+  for (auto e : m->evPool) hipEventDestroy(e);
+  m->evPool.clear();
+  m->evUsed = 0;
+}
+
+// ------------------------------------------------------------------ topology
+// EXCH1 lat-lon periodic halo map (eesupp/src/exch1_rx.template:170-198): every
+// halo point copies the interior point with the wrapped global index.
+static void build_latlon_halo(mgcm_model *m) {
+  const Dims &d = m->d;
+  const int Nx = d.sNx * d.nSx, Ny = d.sNy * d.nSy;
+  m->h_halo.clear();
+  for (int t = 0; t < d.nTiles; t++) {
+    const int bi = t % d.nSx, bj = t / d.nSx;
+    for (int j = 1 - d.OLy; j <= d.sNy + d.OLy; j++)
+      for (int i = 1 - d.OLx; i <= d.sNx + d.OLx; i++) {
+        if (i >= 1 && i <= d.sNx && j >= 1 && j <= d.sNy) continue;
+        int iG = ((bi * d.sNx + i - 1) % Nx + Nx) % Nx, jG = ((bj * d.sNy + j - 1) % Ny + Ny) % Ny;
+        int st = (jG / d.sNy) * d.nSx + iG / d.sNx;
+        m->h_halo.push_back(MG_I2(d, i, j, t));
+        m->h_halo.push_back(MG_I2(d, iG % d.sNx + 1, jG % d.sNy + 1, st));
+      }
+  }
+}
+
+static int upload_halo(mgcm_model *m) {
+  if (m->d_halo) { hipFree(m->d_halo); m->d_halo = nullptr; }
+  m->nHalo = (int)(m->h_halo.size() / 2);
+  if (m->nHalo == 0) return 0;
+  HIPCHK(hipMalloc(&m->d_halo, m->h_halo.size() * sizeof(long)));
+  HIPCHK(hipMemcpy(m->d_halo, m->h_halo.data(), m->h_halo.size() * sizeof(long), hipMemcpyHostToDevice));
+  return 0;
+}
+
+// CG2D neighbour table: compact interior index of the value found at the W,E,S,N
+// neighbour (through the halo map when the neighbour is a halo point), packed as
+// two 16-bit indices per word; points are padded to PPT*1024 and padding /
+// missing neighbours point at the ZERO slot (index NP).
+static int build_nbr(mgcm_model *m) {
+  const Dims &d = m->d;
+  const long N2 = d.n2 * d.nTiles;
+  std::vector<long> srcOf(N2, -1);
+  for (size_t h = 0; h + 1 < m->h_halo.size(); h += 2) srcOf[m->h_halo[h]] = m->h_halo[h + 1];
+  m->nPts = d.nTiles * d.sNx * d.sNy;
+  const int ppt = cg2d_block_ppt(m->nPts);
+  if (!ppt) return 0;  // too large for the single-workgroup solver (checked by mgcm_init)
+  const int NP = ppt * 1024;
+  const unsigned ZERO = (unsigned)NP;
+  auto compact = [&](long g) -> unsigned {
+    if (g < 0) return ZERO;
+    long t = g / d.n2, l = g % d.n2;
+    int i = (int)(l % d.nx) - d.OLx + 1, j = (int)(l / d.nx) - d.OLy + 1;
+    if (i < 1 || i > d.sNx || j < 1 || j > d.sNy) return ZERO;
+    return (unsigned)(t * d.sNx * d.sNy + (long)(j - 1) * d.sNx + (i - 1));
+  };
+  std::vector<unsigned> nb(2 * (size_t)NP, ZERO | (ZERO << 16));
+  std::vector<int> gofs(NP, (int)MG_I2(d, 1, 1, 0));
+  for (int t = 0; t < d.nTiles; t++)
+    for (int j = 1; j <= d.sNy; j++)
+      for (int i = 1; i <= d.sNx; i++) {
+        const int pidx = t * d.sNx * d.sNy + (j - 1) * d.sNx + (i - 1);
+        const int di[4] = {-1, 1, 0, 0}, dj[4] = {0, 0, -1, 1};
+        unsigned c4[4];
+        for (int c = 0; c < 4; c++) {
+          const int ii = i + di[c], jj = j + dj[c];
+          long g = MG_I2(d, ii, jj, t);
+          if (ii < 1 || ii > d.sNx || jj < 1 || jj > d.sNy) g = srcOf[g];
+          c4[c] = compact(g);
+        }
+        nb[2 * (size_t)pidx] = c4[0] | (c4[1] << 16);
+        nb[2 * (size_t)pidx + 1] = c4[2] | (c4[3] << 16);
+        gofs[pidx] = (int)MG_I2(d, i, j, t);
+      }
+  if (m->d_nbr) (void)hipFree(m->d_nbr);
+  if (m->d_gofs) (void)hipFree(m->d_gofs);
+  HIPCHK(hipMalloc(&m->d_nbr, nb.size() * sizeof(unsigned)));
+  HIPCHK(hipMemcpy(m->d_nbr, nb.data(), nb.size() * sizeof(unsigned), hipMemcpyHostToDevice));
+  HIPCHK(hipMalloc(&m->d_gofs, gofs.size() * sizeof(int)));
+  HIPCHK(hipMemcpy(m->d_gofs, gofs.data(), gofs.size() * sizeof(int), hipMemcpyHostToDevice));
+  return 0;
+}
+
+// ------------------------------------------------------------------ C-ABI
+extern "C" {
+
+const char *mgcm_last_error(void) { return g_err.c_str(); }
+
+mgcm_model *mgcm_create(int sNx, int sNy, int OLx, int OLy, int Nr, int nSx, int nSy, int device) {
+  if (sNx <= 0 || sNy <= 0 || Nr <= 0 || nSx <= 0 || nSy <= 0 || OLx < 2 || OLy < 2) {
+    set_err("mgcm_create: invalid sizes (need OLx,OLy >= 2)");
+    return nullptr;
+  }
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= device) {
+    set_err("mgcm_create: no HIP device %d (found %d)", device, ndev);
+    return nullptr;
+  }
+  if (hipSetDevice(device) != hipSuccess) { set_err("mgcm_create: hipSetDevice failed"); return nullptr; }
+  mgcm_model *m = new mgcm_model();
+  m->device = device;
+  Dims &d = m->d;
+  d.sNx = sNx; d.sNy = sNy; d.OLx = OLx; d.OLy = OLy; d.Nr = Nr; d.nSx = nSx; d.nSy = nSy; d.nTiles = nSx * nSy;
+  d.nx = sNx + 2 * OLx; d.ny = sNy + 2 * OLy; d.n2 = (long)d.nx * d.ny; d.n3 = d.n2 * Nr;
+  // defaults (model/src/set_defaults.F, resolved by ini_parms.F)
+  Params &p = m->p;
+  p.abEps = 0.01; p.rhoConst = 999.8; p.gBaro = 9.81; p.sideDragFactor = 2.0; p.freeSurfFac = 1.0;
+  p.implicSurfPress = 1.0; p.implicDiv2DFlow = 1.0; p.rkSign = -1.0;
+  p.afFacMom = p.vfFacMom = p.pfFacMom = p.cfFacMom = p.foFacMom = p.mtFacMom = 1.0;
+  p.momAdvection = p.momViscosity = p.momForcing = p.useCoriolis = 1;
+  p.no_slip_sides = p.no_slip_bottom = 1; p.momDissip_In_AB = 1; p.momForcingOutAB = 0;
+  p.cg2dMaxIters = 150; p.cg2dNormaliseRHS = 1;
+  if (hipStreamCreateWithFlags(&m->stream, hipStreamNonBlocking) != hipSuccess) {
+    set_err("mgcm_create: stream");
+    delete m;
+    return nullptr;
+  }
+  for (auto &fd : FIELDS) {
+    const long n = field_count(m, fd.kind);
+    double *ptr = nullptr;
+    if (hipMalloc(&ptr, n * sizeof(double)) != hipSuccess || hipMemset(ptr, 0, n * sizeof(double)) != hipSuccess) {
+      set_err("mgcm_create: hipMalloc %s (%ld doubles)", fd.name, n);
+      mgcm_destroy(m);
+      return nullptr;
+    }
+    m->allocs.push_back(ptr);
+    field_ptr(m, &fd) = ptr;
+  }
+  if (hipMalloc(&m->d_ctr, 2 * sizeof(int)) != hipSuccess || hipMemset(m->d_ctr, 0, 2 * sizeof(int)) != hipSuccess ||
+      hipMalloc(&m->d_rec, m->maxRec * sizeof(SolveRecord)) != hipSuccess) {
+    set_err("mgcm_create: counters");
+    mgcm_destroy(m);
+    return nullptr;
+  }
+  build_latlon_halo(m);
+  return m;
+}
+
+void mgcm_destroy(mgcm_model *m) {
+  if (!m) return;
+  hipSetDevice(m->device);
+  if (m->stream) hipStreamSynchronize(m->stream);
+  ev_collect(m);
+  ev_free(m);
+  for (void *p : m->allocs) hipFree(p);
+  if (m->d_halo) hipFree(m->d_halo);
+  if (m->d_nbr) hipFree(m->d_nbr);
+  if (m->d_gofs) hipFree(m->d_gofs);
+  if (m->d_ctr) hipFree(m->d_ctr);
+  if (m->d_rec) hipFree(m->d_rec);
+  if (m->stream) hipStreamDestroy(m->stream);
+  delete m;
+}
+
+int mgcm_set_param(mgcm_model *m, const char *name, double value) {
+  if (!strcmp(name, "myIter")) {  // the device-side iteration counter (AB2 start, solve records)
+    int it = (int)value;
+    HIPCHK(hipSetDevice(m->device));
+    HIPCHK(hipMemcpy(m->d_ctr, &it, sizeof(int), hipMemcpyHostToDevice));
+    return 0;
+  }
+  for (auto &pd : PARAMS)
+    if (!strcmp(pd.name, name)) {
+      char *ptr = reinterpret_cast<char *>(&m->p) + pd.off;
+      if (pd.isint) *reinterpret_cast<int *>(ptr) = (int)value;
+      else *reinterpret_cast<double *>(ptr) = value;
+      return 0;
+    }
+  // options the kernels do not implement are accepted only at their default
+  // (inert) value; anything else is an explicit error, never silently ignored.
+  static const char *inert[] = {"useBiharmonicVisc", "nonlinFreeSurf", "select_rStar", "exactConserv",
+                                "useCDscheme", "vectorInvariantMomentum", "useNHMTerms", "metricTerms",
+                                "usingSphericalPolarGrid", "tempStepping", "saltStepping", "staggerTimeStep",
+                                "implicitFreeSurface", "useRealFreshWaterFlux", "useGMRedi"};
+  for (auto *n : inert)
+    if (!strcmp(n, name)) {
+      const bool isDefaultOff = (value == 0.0) || (!strcmp(n, "implicitFreeSurface") && value == 1.0);
+      if (!isDefaultOff) return set_err("mgcm_set_param: option %s=%g is not supported by the device path yet", name, value);
+      m->extra[name] = value;
+      return 0;
+    }
+  m->extra[name] = value;
+  return 0;
+}
+
+double mgcm_get_param(mgcm_model *m, const char *name) {
+  if (!strcmp(name, "myIter")) {
+    int it = 0;
+    if (hipMemcpy(&it, m->d_ctr, sizeof(int), hipMemcpyDeviceToHost) != hipSuccess) return NAN;
+    return it;
+  }
+  for (auto &pd : PARAMS)
+    if (!strcmp(pd.name, name)) {
+      const char *ptr = reinterpret_cast<const char *>(&m->p) + pd.off;
+      return pd.isint ? (double)*reinterpret_cast<const int *>(ptr) : *reinterpret_cast<const double *>(ptr);
+    }
+  auto it = m->extra.find(name);
+  return it == m->extra.end() ? NAN : it->second;
+}
+
+int mgcm_put(mgcm_model *m, const char *name, const double *host, long count) {
+  const FieldDesc *fd = find_field(name);
+  if (!fd) return set_err("mgcm_put: unknown field %s", name);
+  const long n = field_count(m, fd->kind);
+  if (count > n || count <= 0) return set_err("mgcm_put: %s count %ld > %ld", name, count, n);
+  HIPCHK(hipSetDevice(m->device));
+  HIPCHK(hipMemcpyAsync(field_ptr(m, fd), host, count * sizeof(double), hipMemcpyHostToDevice, m->stream));
+  HIPCHK(hipStreamSynchronize(m->stream));
+  return 0;
+}
+
+int mgcm_get(mgcm_model *m, const char *name, double *host, long count) {
+  const FieldDesc *fd = find_field(name);
+  if (!fd) return set_err("mgcm_get: unknown field %s", name);
+  const long n = field_count(m, fd->kind);
+  if (count > n || count <= 0) return set_err("mgcm_get: %s count %ld > %ld", name, count, n);
+  HIPCHK(hipSetDevice(m->device));
+  HIPCHK(hipMemcpyAsync(host, field_ptr(m, fd), count * sizeof(double), hipMemcpyDeviceToHost, m->stream));
+  HIPCHK(hipStreamSynchronize(m->stream));
+  return 0;
+}
+
+double *mgcm_device_ptr(mgcm_model *m, const char *name) {
+  const FieldDesc *fd = find_field(name);
+  if (!fd) { set_err("mgcm_device_ptr: unknown field %s", name); return nullptr; }
+  return field_ptr(m, fd);
+}
+
+int mgcm_set_halo_map(mgcm_model *m, const long *src_of_point, long count) {
+  const long N2 = m->d.n2 * m->d.nTiles;
+  if (count != N2) return set_err("mgcm_set_halo_map: count %ld != %ld", count, N2);
+  m->h_halo.clear();
+  for (long q = 0; q < N2; q++)
+    if (src_of_point[q] >= 0 && src_of_point[q] != q) {
+      m->h_halo.push_back(q);
+      m->h_halo.push_back(src_of_point[q]);
+    }
+  m->ready = false;
+  return 0;
+}
+
+int mgcm_init(mgcm_model *m) {
+  HIPCHK(hipSetDevice(m->device));
+  if (upload_halo(m)) return -1;
+  if (build_nbr(m)) return -1;
+  if (m->nPts > cg2d_block_max_points())
+    return set_err("mgcm_init: %d CG2D points per GPU exceed the single-workgroup solver (%d); "
+                   "the multi-workgroup solver is not built yet", m->nPts, cg2d_block_max_points());
+  if (m->p.viscA4D != 0.0 || m->p.viscA4Z != 0.0)
+    return set_err("mgcm_init: biharmonic viscosity is not supported by the device path yet");
+  if (m->p.implicitViscosity) return set_err("mgcm_init: implicitViscosity not supported by the device path yet");
+  if (m->p.implicSurfPress != 1.0 || m->p.implicDiv2DFlow != 1.0)
+    return set_err("mgcm_init: implicSurfPress/implicDiv2DFlow != 1 not supported yet");
+  int it0 = m->p.nIter0;
+  HIPCHK(hipMemcpy(m->d_ctr, &it0, sizeof(int), hipMemcpyHostToDevice));
+  m->ready = true;
+  return 0;
+}
+
+static int check_ready(mgcm_model *m) {
+  if (!m->ready) return set_err("model not initialised: call mgcm_init() after loading the fields");
+  return 0;
+}
+
+#define TIMED(K, CALL)                      \
+  do {                                      \
+    int ev_ = ev_begin(m, K);               \
+    hipError_t e_ = (CALL);                 \
+    ev_end(m, K, ev_);                      \
+    if (e_ != hipSuccess) return set_err("%s: %s", KNAMES[K], hipGetErrorString(e_)); \
+  } while (0)
+
+int mgcm_dynamics(mgcm_model *m) {
+  if (check_ready(m)) return -1;
+  TIMED(K_MOM, launch_mom_step(m->d, m->p, m->f, m->d_ctr, m->stream));
+  return 0;
+}
+
+static int solve_impl(mgcm_model *m) {
+  TIMED(K_RHS, launch_sfp_rhs(m->d, m->p, m->f, m->stream));
+  const int nIterMin = m->p.cg2dUseMinResSol - 1;
+  TIMED(K_CG2D, launch_cg2d_block(m->d, m->p, m->f, m->d_nbr, m->d_gofs, m->nPts, m->p.cg2dMaxIters, nIterMin, m->d_rec,
+                                  m->d_ctr + 1, m->stream));
+  TIMED(K_EXCH, launch_exchange(m->d, m->f.cg2d_x, m->d_halo, m->nHalo, 1, m->stream));
+  TIMED(K_ETA, launch_eta_update(m->d, m->f, m->stream));
+  return 0;
+}
+
+int mgcm_solve_for_pressure(mgcm_model *m) {
+  if (check_ready(m)) return -1;
+  return solve_impl(m);
+}
+
+int mgcm_momentum_correction_step(mgcm_model *m) {
+  if (check_ready(m)) return -1;
+  TIMED(K_CORR, launch_correction(m->d, m->p, m->f, m->stream));
+  return 0;
+}
+
+int mgcm_integr_continuity(mgcm_model *m) {
+  if (check_ready(m)) return -1;
+  TIMED(K_CONT, launch_continuity(m->d, m->f, m->stream));
+  return 0;
+}
+
+int mgcm_blocking_exchanges(mgcm_model *m) {
+  if (check_ready(m)) return -1;
+  // do_fields_blocking_exchanges.F:54-97: uVel, vVel, wVel (theta/salt are not
+  // stepped by the supported configs, their halos are unchanged)
+  TIMED(K_EXCH, launch_exchange(m->d, m->f.uVel, m->d_halo, m->nHalo, m->d.Nr, m->stream));
+  TIMED(K_EXCH, launch_exchange(m->d, m->f.vVel, m->d_halo, m->nHalo, m->d.Nr, m->stream));
+  TIMED(K_EXCH, launch_exchange(m->d, m->f.wVel, m->d_halo, m->nHalo, m->d.Nr, m->stream));
+  return 0;
+}
+
+int mgcm_forward_step(mgcm_model *m, int nsteps) {
+  if (check_ready(m)) return -1;
+  if (nsteps <= 0 || nsteps > m->maxRec) return set_err("mgcm_forward_step: nsteps %d out of range", nsteps);
+  HIPCHK(hipSetDevice(m->device));
+  HIPCHK(hipMemsetAsync(m->d_ctr + 1, 0, sizeof(int), m->stream));
+  for (int s = 0; s < nsteps; s++) {
+    if (mgcm_dynamics(m)) return -1;
+    if (solve_impl(m)) return -1;
+    if (mgcm_momentum_correction_step(m)) return -1;
+    if (mgcm_integr_continuity(m)) return -1;
+    if (mgcm_blocking_exchanges(m)) return -1;
+    HIPCHK(launch_bump_counter(m->d_ctr, 1, m->stream));
+  }
+  m->lastBatch = nsteps;
+  return 0;
+}
+
+int mgcm_sync(mgcm_model *m) {
+  HIPCHK(hipSetDevice(m->device));
+  HIPCHK(hipStreamSynchronize(m->stream));
+  ev_collect(m);
+  return 0;
+}
+
+int mgcm_solve_stats(mgcm_model *m, int back, double *firstResidual, double *lastResidual, int *numIters,
+                     double *rhsMax) {
+  HIPCHK(hipStreamSynchronize(m->stream));
+  int slot = m->lastBatch - 1 - back;
+  if (m->lastBatch == 0) slot = 0;
+  if (slot < 0) return set_err("mgcm_solve_stats: no such step");
+  SolveRecord r;
+  HIPCHK(hipMemcpy(&r, m->d_rec + slot, sizeof r, hipMemcpyDeviceToHost));
+  if (firstResidual) *firstResidual = r.firstResidual;
+  if (lastResidual) *lastResidual = r.lastResidual;
+  if (numIters) *numIters = r.numIters;
+  if (rhsMax) *rhsMax = r.rhsMax;
+  return 0;
+}
+
+void mgcm_kernel_timing(mgcm_model *m, int enable) {
+  hipStreamSynchronize(m->stream);
+  ev_collect(m);
+  for (int k = 0; k < K_N; k++) { m->kms[k] = 0; m->kcnt[k] = 0; }
+  m->timing = enable != 0;
+}
+
+double mgcm_kernel_ms(mgcm_model *m, const char *name, int *launches) {
+  hipStreamSynchronize(m->stream);
+  ev_collect(m);
+  for (int k = 0; k < K_N; k++)
+    if (!strcmp(KNAMES[k], name)) {
+      if (launches) *launches = m->kcnt[k];
+      return m->kcnt[k] ? m->kms[k] / m->kcnt[k] : 0.0;
+    }
+  if (launches) *launches = 0;
+  return -1.0;
+}
+
+int mgcm_cg2d(mgcm_model *m, double *cg2d_b, double *cg2d_x, double *firstResidual, double *minResidualSq,
+              double *lastResidual, int *numIters, int *nIterMin) {
+  if (check_ready(m)) return -1;
+  const long n = m->d.n2 * m->d.nTiles;
+  HIPCHK(hipSetDevice(m->device));
+  HIPCHK(hipMemcpyAsync(m->f.cg2d_b, cg2d_b, n * sizeof(double), hipMemcpyHostToDevice, m->stream));
+  HIPCHK(hipMemcpyAsync(m->f.cg2d_x, cg2d_x, n * sizeof(double), hipMemcpyHostToDevice, m->stream));
+  HIPCHK(hipMemsetAsync(m->d_ctr + 1, 0, sizeof(int), m->stream));
+  TIMED(K_CG2D, launch_cg2d_block(m->d, m->p, m->f, m->d_nbr, m->d_gofs, m->nPts, *numIters, *nIterMin, m->d_rec, m->d_ctr + 1,
+                                  m->stream));
+  HIPCHK(hipMemcpyAsync(cg2d_b, m->f.cg2d_b, n * sizeof(double), hipMemcpyDeviceToHost, m->stream));
+  HIPCHK(hipMemcpyAsync(cg2d_x, m->f.cg2d_x, n * sizeof(double), hipMemcpyDeviceToHost, m->stream));
+  SolveRecord r;
+  HIPCHK(hipMemcpyAsync(&r, m->d_rec, sizeof r, hipMemcpyDeviceToHost, m->stream));
+  HIPCHK(hipStreamSynchronize(m->stream));
+  *firstResidual = r.firstResidual;
+  *minResidualSq = r.minResidualSq;
+  *lastResidual = r.lastResidual;
+  *numIters = r.numIters;
+  *nIterMin = r.nIterMin;
+  return 0;
+}
+
+// --------------------------------------------------- Fortran drop-in (CG2D)
+static mgcm_model *g_fortran_model = nullptr;
+
+static void fortran_die(const char *where) {
+  fprintf(stderr, "ABNORMAL END: %s: %s\n", where, g_err.c_str());
+  fflush(stderr);
+  abort();
+}
+
+void ini_cg2d_amd_(const int *sNx, const int *sNy, const int *OLx, const int *OLy, const int *nSx, const int *nSy,
+                   const double *aW2d, const double *aS2d, const double *aC2d, const double *pW, const double *pS,
+                   const double *pC, const double *cg2dNorm, const double *cg2dTolerance_sq,
+                   const int *cg2dNormaliseRHS) {
+  mgcm_model *m = g_fortran_model;
+  if (m && (m->d.sNx != *sNx || m->d.sNy != *sNy || m->d.OLx != *OLx || m->d.OLy != *OLy || m->d.nSx != *nSx ||
+            m->d.nSy != *nSy)) {
+    mgcm_destroy(m);
+    m = nullptr;
+  }
+  if (!m) {
+    m = mgcm_create(*sNx, *sNy, *OLx, *OLy, 1, *nSx, *nSy, 0);
+    if (!m) fortran_die("INI_CG2D_AMD");
+    g_fortran_model = m;
+  }
+  const long n = m->d.n2 * m->d.nTiles;
+  if (mgcm_put(m, "aW2d", aW2d, n) || mgcm_put(m, "aS2d", aS2d, n) || mgcm_put(m, "aC2d", aC2d, n) ||
+      mgcm_put(m, "pW", pW, n) || mgcm_put(m, "pS", pS, n) || mgcm_put(m, "pC", pC, n))
+    fortran_die("INI_CG2D_AMD");
+  m->p.cg2dNorm = *cg2dNorm;
+  m->p.cg2dTolerance_sq = *cg2dTolerance_sq;
+  m->p.cg2dNormaliseRHS = *cg2dNormaliseRHS;
+  if (mgcm_init(m)) fortran_die("INI_CG2D_AMD");
+}
+
+void cg2d_amd_(double *cg2d_b, double *cg2d_x, double *firstResidual, double *minResidualSq, double *lastResidual,
+               int *numIters, int *nIterMin, const int *myThid) {
+  (void)myThid;
+  if (!g_fortran_model) {
+    g_err = "CG2D_AMD called before INI_CG2D_AMD";
+    fortran_die("CG2D_AMD");
+  }
+  if (mgcm_cg2d(g_fortran_model, cg2d_b, cg2d_x, firstResidual, minResidualSq, lastResidual, numIters, nIterMin))
+    fortran_die("CG2D_AMD");
+}
+
+}  // extern "C"

@@ -1,0 +1,270 @@
+"""Host-side initialisation (INITIALISE_FIXED subset), numpy, once per run.
+
+These routines run once on the host in the reference too; the product keeps
+them on the host and hands the results to the device mirror.  Arrays are
+halo-inclusive, shaped (nTiles, ny, nx) for 2-D and (nTiles, Nr, ny, nx) for
+3-D, where [t, j+OLy-1, i+OLx-1] is the reference's (i, j, bi, bj).
+
+Restated from:
+  INI_VERTICAL_GRID   model/src/ini_vertical_grid.F
+  INI_LOCAL_GRID      model/src/ini_local_grid.F
+  INI_CARTESIAN_GRID  model/src/ini_cartesian_grid.F
+  INI_GRID reciprocals model/src/ini_grid.F
+  INI_CORI            model/src/ini_cori.F
+  INI_DEPTHS          model/src/ini_depths.F
+  INI_MASKS_ETC       model/src/ini_masks_etc.F
+  INI_LINEAR_PHISURF  model/src/ini_linear_phisurf.F:78-88
+  INI_CG2D            model/src/ini_cg2d.F:61-237
+"""
+import numpy as np
+
+from .topology import LatLonTopology
+
+
+class Grid:
+    def __init__(self, sNx, sNy, OLx, OLy, Nr, nSx=1, nSy=1, topology=None):
+        self.sNx, self.sNy, self.OLx, self.OLy, self.Nr, self.nSx, self.nSy = sNx, sNy, OLx, OLy, Nr, nSx, nSy
+        self.nTiles = nSx * nSy
+        self.nx, self.ny = sNx + 2 * OLx, sNy + 2 * OLy
+        self.topo = topology or LatLonTopology(sNx, sNy, OLx, OLy, nSx, nSy)
+        self.f = {}   # name -> array (float64)
+        self.i = {}   # integer arrays
+
+    # ---- helpers ------------------------------------------------------------
+    def z2(self):
+        return np.zeros((self.nTiles, self.ny, self.nx))
+
+    def z3(self):
+        return np.zeros((self.nTiles, self.Nr, self.ny, self.nx))
+
+    def sl(self, i0, i1, j0, j1):
+        """Slice for Fortran ranges i0..i1, j0..j1 (inclusive) on the last two axes."""
+        return (slice(j0 + self.OLy - 1, j1 + self.OLy), slice(i0 + self.OLx - 1, i1 + self.OLx))
+
+    def exch(self, a):
+        return self.topo.exchange(a)
+
+    # ---- vertical grid --------------------------------------------------------
+    def ini_vertical_grid(self, delR, rkSign=-1.0):
+        Nr = self.Nr
+        drF = np.array(delR, dtype=np.float64)
+        drC = np.zeros(Nr + 1)
+        drC[0] = 0.5 * drF[0]
+        for k in range(1, Nr):
+            drC[k] = 0.5 * (drF[k - 1] + drF[k])
+        drC[Nr] = 0.5 * drF[Nr - 1]
+        rF = np.zeros(Nr + 1)
+        for k in range(Nr):
+            rF[k + 1] = rF[k] + rkSign * drF[k]
+        rC = np.zeros(Nr)
+        rC[0] = rF[0] + rkSign * drC[0]
+        for k in range(1, Nr):
+            rC[k] = rC[k - 1] + rkSign * drC[k]
+        self.f.update(drF=drF, drC=drC, rF=rF, rC=rC, recip_drF=1.0 / drF, recip_drC=1.0 / drC)
+
+    # ---- horizontal grid ------------------------------------------------------
+    def ini_cartesian_grid(self, delX, delY, xgOrigin, ygOrigin):
+        sNx, sNy, OLx, OLy = self.sNx, self.sNy, self.OLx, self.OLy
+        Nx, Ny = sNx * self.nSx, sNy * self.nSy
+        delX = np.asarray(delX, dtype=np.float64)
+        delY = np.asarray(delY, dtype=np.float64)
+        names = ("xC", "yC", "xG", "yG", "dxF", "dyF", "dxG", "dyG", "dxC", "dyC", "dxV", "dyU",
+                 "rA", "rAw", "rAs", "rAz")
+        for n in names:
+            self.f[n] = self.z2()
+        for t in range(self.nTiles):
+            bi, bj = t % self.nSx, t // self.nSx
+            iG0, jG0 = bi * sNx, bj * sNy
+            xG0 = xgOrigin
+            for i in range(1, iG0 + 1):
+                xG0 += delX[i - 1]
+            for i in range(1, OLx + 1):
+                xG0 -= delX[(iG0 - i + OLx * Nx) % Nx]
+            yG0 = ygOrigin
+            for j in range(1, jG0 + 1):
+                yG0 += delY[j - 1]
+            for j in range(1, OLy + 1):
+                yG0 -= delY[(jG0 - j + OLy * Ny) % Ny]
+            # delXloc(i), i = -OLx..sNx+OLx -> index i+OLx
+            dXl = np.array([delX[(iG0 + i - 1 + OLx * Nx) % Nx] for i in range(-OLx, sNx + OLx + 1)])
+            dYl = np.array([delY[(jG0 + j - 1 + OLy * Ny) % Ny] for j in range(-OLy, sNy + OLy + 1)])
+            # xGloc(i,j) for i = 1-OLx..sNx+OLx+1 (sequential running sum, as the loop does)
+            nxl, nyl = sNx + 2 * OLx + 1, sNy + 2 * OLy + 1
+            xGl = np.zeros(nxl)
+            xGl[0] = xG0
+            for ii in range(1, nxl):
+                xGl[ii] = xGl[ii - 1] + dXl[ii]          # dXl index (i-1)+OLx+1 = ii for i=ii-OLx
+            yGl = np.zeros(nyl)
+            yGl[0] = yG0
+            for jj in range(1, nyl):
+                yGl[jj] = yGl[jj - 1] + dYl[jj]
+            XG = np.broadcast_to(xGl[None, :], (nyl, nxl))
+            YG = np.broadcast_to(yGl[:, None], (nyl, nxl))
+            f = self.f
+            f["xG"][t] = XG[:-1, :-1]
+            f["yG"][t] = YG[:-1, :-1]
+            f["xC"][t] = 0.25 * (XG[:-1, :-1] + XG[:-1, 1:] + XG[1:, :-1] + XG[1:, 1:])
+            f["yC"][t] = 0.25 * (YG[:-1, :-1] + YG[:-1, 1:] + YG[1:, :-1] + YG[1:, 1:])
+            dxl = dXl[1:]   # delXloc(i) for i = 1-OLx..sNx+OLx
+            dyl = dYl[1:]
+            f["dxF"][t] = dxl[None, :]
+            f["dyF"][t] = dyl[:, None]
+            f["dxG"][t] = dxl[None, :]
+            f["dyG"][t] = dyl[:, None]
+            f["dxC"][t, :, 1:] = 0.5 * (f["dxF"][t, :, 1:] + f["dxF"][t, :, :-1])
+            f["dyC"][t, 1:, :] = 0.5 * (f["dyF"][t, 1:, :] + f["dyF"][t, :-1, :])
+            f["dxV"][t, 1:, 1:] = 0.5 * (f["dxG"][t, 1:, 1:] + f["dxG"][t, 1:, :-1])
+            f["dyU"][t, 1:, 1:] = 0.5 * (f["dyG"][t, 1:, 1:] + f["dyG"][t, :-1, 1:])
+            f["rA"][t] = f["dxF"][t] * f["dyF"][t]
+            f["rAw"][t] = f["dxC"][t] * f["dyG"][t]
+            f["rAs"][t] = f["dxG"][t] * f["dyC"][t]
+            f["rAz"][t] = f["dxV"][t] * f["dyU"][t]
+        self._reciprocals()
+
+    def _reciprocals(self):
+        for n in ("dxG", "dyG", "dxC", "dyC", "dxF", "dyF", "dxV", "dyU", "rA", "rAs", "rAw", "rAz"):
+            a = self.f[n]
+            r = np.zeros_like(a)
+            nz = a != 0.0
+            r[nz] = 1.0 / a[nz]
+            self.f["recip_" + n] = r
+
+    def ini_cori(self, f0, beta, selectCoriMap=1):
+        if selectCoriMap == 1:
+            self.f["fCori"] = f0 + beta * self.f["yC"]
+            self.f["fCoriG"] = f0 + beta * self.f["yG"]
+        elif selectCoriMap == 0:
+            self.f["fCori"] = np.full_like(self.f["yC"], f0)
+            self.f["fCoriG"] = np.full_like(self.f["yC"], f0)
+        else:
+            raise NotImplementedError("selectCoriMap=%d" % selectCoriMap)
+
+    # ---- depths and masks -----------------------------------------------------
+    def ini_depths_masks(self, bathy, hFacMin=1.0, hFacMinDr=0.0, gBaro=9.81):
+        """bathy: global (Ny, Nx) array, negative below sea level."""
+        sNx, sNy, Nr = self.sNx, self.sNy, self.Nr
+        rF, drF, recip_drF = self.f["rF"], self.f["drF"], self.f["recip_drF"]
+        R_low, Ro_surf = self.z2(), self.z2()
+        inner = self.sl(1, sNx, 1, sNy)
+        for t in range(self.nTiles):
+            bi, bj = t % self.nSx, t // self.nSx
+            R_low[t][inner] = bathy[bj * sNy:(bj + 1) * sNy, bi * sNx:(bi + 1) * sNx]
+            Ro_surf[t][inner] = rF[0]
+        R_low = self.exch(R_low)
+        Ro_surf = self.exch(Ro_surf)
+        rEmpty = rF[0]
+        rLowW = self.z2(); rSurfW = self.z2(); rLowS = self.z2(); rSurfS = self.z2()
+        rLowW[:, :, 0] = rEmpty; rSurfW[:, :, 0] = rEmpty
+        rLowS[:, 0, :] = rEmpty; rSurfS[:, 0, :] = rEmpty
+        rLowW[:, :, 1:] = np.maximum(R_low[:, :, :-1], R_low[:, :, 1:])
+        rSurfW[:, :, 1:] = np.minimum(Ro_surf[:, :, :-1], Ro_surf[:, :, 1:])
+        rLowS[:, 1:, :] = np.maximum(R_low[:, :-1, :], R_low[:, 1:, :])
+        rSurfS[:, 1:, :] = np.minimum(Ro_surf[:, :-1, :], Ro_surf[:, 1:, :])
+        hFacC = self.z3()
+        for k in range(Nr):
+            mn = max(hFacMin, min(hFacMinDr * recip_drF[k], 1.0))
+            hl = (rF[k] - R_low) * recip_drF[k]
+            hl = np.minimum(np.maximum(hl, 0.0), 1.0)
+            hFacC[:, k] = np.where((hl < mn * 0.5) | (R_low >= Ro_surf), 0.0, np.maximum(hl, mn))
+        tmp = np.zeros_like(R_low)
+        for k in range(Nr):
+            tmp = tmp + drF[k] * hFacC[:, k]
+        R_low = rF[0] - tmp
+        for k in range(Nr):
+            mn = max(hFacMin, min(hFacMinDr * recip_drF[k], 1.0))
+            hl = (rF[k] - Ro_surf) * recip_drF[k]
+            hl = hFacC[:, k] - np.maximum(hl, 0.0)
+            hl = np.maximum(hl, 0.0)
+            hFacC[:, k] = np.where(hl < mn * 0.5, 0.0, np.maximum(hl, mn))
+        tmp = np.zeros_like(R_low)
+        kSurfC = np.full(R_low.shape, Nr + 1, dtype=np.int32)
+        kLowC = np.zeros(R_low.shape, dtype=np.int32)
+        for k in range(Nr):
+            tmp = tmp + drF[k] * hFacC[:, k]
+            kLowC[hFacC[:, k] != 0.0] = k + 1
+        for k in range(Nr - 1, -1, -1):
+            kSurfC[hFacC[:, k] != 0.0] = k + 1
+        Ro_surf = R_low + tmp
+        maskInC = np.where(kSurfC <= Nr, 1.0, 0.0)
+        hFacW, hFacS = self.z3(), self.z3()
+        for k in range(Nr):
+            mn = max(hFacMin, min(hFacMinDr * recip_drF[k], 1.0))
+            for rLow, rSurf, out in ((rLowW, rSurfW, hFacW), (rLowS, rSurfS, hFacS)):
+                h1 = (rF[k] - rLow) * recip_drF[k]
+                hl = np.minimum(h1, 1.0)
+                h1 = np.where((hl < mn * 0.5) | (rLow >= rSurf), 0.0, np.maximum(hl, mn))
+                h2 = (rF[k] - rSurf) * recip_drF[k]
+                hl = h1 - np.maximum(h2, 0.0)
+                out[:, k] = np.where(hl < mn * 0.5, 0.0, np.maximum(hl, mn))
+        hFacW = self.exch(hFacW)
+        hFacS = self.exch(hFacS)
+        kSurfW = np.full(R_low.shape, Nr + 1, dtype=np.int32)
+        kSurfS = np.full(R_low.shape, Nr + 1, dtype=np.int32)
+        for k in range(Nr - 1, -1, -1):
+            kSurfW[hFacW[:, k] != 0.0] = k + 1
+            kSurfS[hFacS[:, k] != 0.0] = k + 1
+        f = self.f
+        f.update(R_low=R_low, Ro_surf=Ro_surf, hFacC=hFacC, hFacW=hFacW, hFacS=hFacS, maskInC=maskInC,
+                 maskInW=np.where(kSurfW <= Nr, 1.0, 0.0), maskInS=np.where(kSurfS <= Nr, 1.0, 0.0))
+        self.i.update(kSurfC=kSurfC, kLowC=kLowC, kSurfW=kSurfW, kSurfS=kSurfS)
+        for c in "CWS":
+            h = f["hFac" + c]
+            nz = h != 0.0
+            r = np.zeros_like(h)
+            r[nz] = 1.0 / h[nz]
+            f["recip_hFac" + c] = r
+            f["mask" + c] = np.where(nz, 1.0, 0.0)
+        # INI_LINEAR_PHISURF, z-coordinates
+        f["Bo_surf"] = np.full_like(R_low, gBaro)
+        f["recip_Bo"] = np.full_like(R_low, 1.0 / gBaro)
+        # globalArea: GLOBAL_SUM_TILE_RL of the tile sums of rA*maskInC (interior)
+        ga = 0.0
+        for t in range(self.nTiles):
+            ta = 0.0
+            a = (f["rA"][t] * maskInC[t])[inner]
+            for v in a.ravel():
+                ta = ta + v
+            ga = ga + ta
+        self.globalArea = ga
+
+    # ---- elliptic operator ----------------------------------------------------
+    def ini_cg2d(self, deltaTMom, deltaTFreeSurf, cg2dTargetResidual, cg2dTargetResWunit=-1.0,
+                 cg2dpcOffDFac=0.51, freeSurfFac=1.0, implicSurfPress=1.0, implicDiv2DFlow=1.0):
+        sNx, sNy, Nr = self.sNx, self.sNy, self.Nr
+        f = self.f
+        aW, aS = self.z2(), self.z2()
+        inner = self.sl(1, sNx, 1, sNy)
+        for k in range(Nr):
+            fa = f["dyG"] * f["drF"][k] * f["hFacW"][:, k]
+            aW[(slice(None),) + inner] = (aW + implicSurfPress * implicDiv2DFlow * fa * f["recip_dxC"])[(slice(None),) + inner]
+            fa = f["dxG"] * f["drF"][k] * f["hFacS"][:, k]
+            aS[(slice(None),) + inner] = (aS + implicSurfPress * implicDiv2DFlow * fa * f["recip_dyC"])[(slice(None),) + inner]
+        myNorm = max(np.abs(aW[(slice(None),) + inner]).max(), np.abs(aS[(slice(None),) + inner]).max(), 0.0)
+        myNorm = 1.0 / myNorm if myNorm != 0.0 else 1.0
+        aW[(slice(None),) + inner] = aW[(slice(None),) + inner] * myNorm
+        aS[(slice(None),) + inner] = aS[(slice(None),) + inner] * myNorm
+        aW = self.exch(aW)
+        aS = self.exch(aS)
+        self.cg2dNorm = myNorm
+        self.cg2dNormaliseRHS = cg2dTargetResWunit <= 0.0
+        tol = cg2dTargetResidual if self.cg2dNormaliseRHS else \
+            myNorm * cg2dTargetResWunit * self.globalArea / deltaTMom
+        self.cg2dTolerance_sq = tol * tol
+        aC = self.z2()
+        s0 = self.sl(0, sNx, 0, sNy)
+        aWe = np.roll(aW, -1, axis=2)
+        aSn = np.roll(aS, -1, axis=1)
+        val = -(aW + aWe + aS + aSn + freeSurfFac * myNorm * f["recip_Bo"] * f["rA"] / deltaTMom / deltaTFreeSurf)
+        aC[(slice(None),) + s0] = val[(slice(None),) + s0]
+        pC, pW, pS = self.z2(), self.z2(), self.z2()
+        acw = np.roll(aC, 1, axis=2)
+        acs = np.roll(aC, 1, axis=1)
+        with np.errstate(divide="ignore", invalid="ignore"):
+            pCv = np.where(aC == 0.0, 1.0, 1.0 / aC)
+            dW = cg2dpcOffDFac * (acw + aC)
+            pWv = np.where(aC + acw == 0.0, 0.0, -aW / (dW * dW))
+            dS = cg2dpcOffDFac * (acs + aC)
+            pSv = np.where(aC + acs == 0.0, 0.0, -aS / (dS * dS))
+        for dst, src in ((pC, pCv), (pW, pWv), (pS, pSv)):
+            dst[(slice(None),) + inner] = src[(slice(None),) + inner]
+        f.update(aW2d=aW, aS2d=aS, aC2d=aC, pC=self.exch(pC), pW=self.exch(pW), pS=self.exch(pS))

@@ -1,0 +1,207 @@
+"""Host driver of the device-resident hot path (the FORWARD_STEP caller).
+
+Model owns one mgcm_model (a tile set in HBM on one GPU): it uploads the
+host-initialised grid/masks/operator (grid.py), holds the run-time parameters
+(PARAMS.h names), and drives DYNAMICS / SOLVE_FOR_PRESSURE /
+MOMENTUM_CORRECTION_STEP / INTEGR_CONTINUITY / DO_FIELDS_BLOCKING_EXCHANGES
+through the C-ABI.  There is no CPU path: every call goes to the HIP library.
+"""
+import ctypes
+
+import numpy as np
+
+from ._lib import check, lib, MgcmError
+
+# fields uploaded from the host-side initialisation
+GRID_2D = ("dxF", "dyF", "dxG", "dyG", "dxC", "dyC", "dxV", "dyU", "rA", "rAw", "rAs",
+           "recip_dxF", "recip_dyF", "recip_dxC", "recip_dyC", "recip_dxV", "recip_dyU",
+           "recip_rA", "recip_rAw", "recip_rAs", "fCori", "Bo_surf", "recip_Bo",
+           "aW2d", "aS2d", "aC2d", "pW", "pS", "pC")
+GRID_3D = ("hFacC", "hFacW", "hFacS", "recip_hFacW", "recip_hFacS", "maskC", "maskW", "maskS")
+GRID_1D = ("drF", "drC", "recip_drF", "recip_drC")
+STATE_3D = ("uVel", "vVel", "wVel", "theta", "salt", "gU", "gV", "guNm1", "gvNm1")
+STATE_2D = ("etaN", "fu", "fv")
+
+DEVICE_PARAMS = ("deltaTMom", "deltaTFreeSurf", "deltaTClock", "abEps", "rhoConst", "gBaro", "viscAhD",
+                 "viscAhZ", "viscA4D", "viscA4Z", "viscAr", "sideDragFactor", "freeSurfFac", "implicSurfPress",
+                 "implicDiv2DFlow", "rkSign", "afFacMom", "vfFacMom", "pfFacMom", "cfFacMom", "foFacMom",
+                 "mtFacMom", "momAdvection", "momViscosity", "momForcing", "useCoriolis", "no_slip_sides",
+                 "no_slip_bottom", "selectCoriScheme", "momForcingOutAB", "momDissip_In_AB", "implicitViscosity",
+                 "cg2dMaxIters", "cg2dUseMinResSol", "nIter0")
+
+
+def _dp(a):
+    return a.ctypes.data_as(ctypes.POINTER(ctypes.c_double))
+
+
+class Model:
+    def __init__(self, grid, params, device=0):
+        self.g = grid
+        self.params = dict(params)
+        L = lib()
+        g = grid
+        self.h = L.mgcm_create(g.sNx, g.sNy, g.OLx, g.OLy, g.Nr, g.nSx, g.nSy, device)
+        if not self.h:
+            raise MgcmError("mgcm_create failed: " + L.mgcm_last_error().decode())
+        for k, v in self.params.items():
+            check(L.mgcm_set_param(self.h, k.encode(), float(v)), "mgcm_set_param(%s)" % k)
+        check(L.mgcm_set_param(self.h, b"cg2dNorm", g.cg2dNorm), "cg2dNorm")
+        check(L.mgcm_set_param(self.h, b"cg2dTolerance_sq", g.cg2dTolerance_sq), "cg2dTolerance_sq")
+        check(L.mgcm_set_param(self.h, b"cg2dNormaliseRHS", float(g.cg2dNormaliseRHS)), "cg2dNormaliseRHS")
+        for n in GRID_1D:
+            a = np.zeros(g.Nr + 1)
+            v = g.f[n]
+            a[:len(v)] = v
+            self.put(n, a)
+        for n in GRID_2D + GRID_3D:
+            self.put(n, g.f[n])
+        src = np.ascontiguousarray(g.topo.src_of_point(), dtype=np.int64)
+        check(L.mgcm_set_halo_map(self.h, src.ctypes.data_as(ctypes.POINTER(ctypes.c_long)), src.size),
+              "mgcm_set_halo_map")
+
+    def init(self):
+        check(lib().mgcm_init(self.h), "mgcm_init")
+
+    def close(self):
+        if getattr(self, "h", None):
+            lib().mgcm_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # ---- fields --------------------------------------------------------------
+    def _shape(self, name):
+        g = self.g
+        if name in GRID_1D:
+            return (g.Nr + 1,)
+        if name in GRID_3D or name in STATE_3D:
+            return (g.nTiles, g.Nr, g.ny, g.nx)
+        return (g.nTiles, g.ny, g.nx)
+
+    def put(self, name, arr):
+        a = np.ascontiguousarray(arr, dtype=np.float64)
+        check(lib().mgcm_put(self.h, name.encode(), _dp(a), a.size), "mgcm_put(%s)" % name)
+
+    def get(self, name):
+        a = np.zeros(self._shape(name))
+        check(lib().mgcm_get(self.h, name.encode(), _dp(a), a.size), "mgcm_get(%s)" % name)
+        return a
+
+    # ---- hot path ------------------------------------------------------------
+    def forward_step(self, nsteps=1):
+        check(lib().mgcm_forward_step(self.h, int(nsteps)), "mgcm_forward_step")
+
+    def dynamics(self):
+        check(lib().mgcm_dynamics(self.h), "mgcm_dynamics")
+
+    def solve_for_pressure(self):
+        check(lib().mgcm_solve_for_pressure(self.h), "mgcm_solve_for_pressure")
+
+    def sync(self):
+        check(lib().mgcm_sync(self.h), "mgcm_sync")
+
+    def solve_stats(self, back=0):
+        f, la, rm = ctypes.c_double(), ctypes.c_double(), ctypes.c_double()
+        it = ctypes.c_int()
+        check(lib().mgcm_solve_stats(self.h, back, ctypes.byref(f), ctypes.byref(la), ctypes.byref(it),
+                                     ctypes.byref(rm)), "mgcm_solve_stats")
+        return {"cg2d_init_res": f.value, "cg2d_last_res": la.value, "cg2d_iters": it.value,
+                "cg2d_rhs_max": rm.value}
+
+    def cg2d(self, b, x, maxIters, nIterMin=-1):
+        b = np.ascontiguousarray(b, dtype=np.float64).copy()
+        x = np.ascontiguousarray(x, dtype=np.float64).copy()
+        f, mn, la = ctypes.c_double(), ctypes.c_double(), ctypes.c_double()
+        it, itm = ctypes.c_int(maxIters), ctypes.c_int(nIterMin)
+        check(lib().mgcm_cg2d(self.h, _dp(b), _dp(x), ctypes.byref(f), ctypes.byref(mn), ctypes.byref(la),
+                              ctypes.byref(it), ctypes.byref(itm)), "mgcm_cg2d")
+        return x, f.value, mn.value, la.value, it.value, itm.value
+
+    def kernel_timing(self, enable):
+        lib().mgcm_kernel_timing(self.h, 1 if enable else 0)
+
+    def kernel_ms(self, name):
+        n = ctypes.c_int()
+        ms = lib().mgcm_kernel_ms(self.h, name.encode(), ctypes.byref(n))
+        return ms, n.value
+
+
+def mon_stats(g, arr, hfac, mask, area, dr):
+    """MON_CALC_STATS_RL (pkg/monitor/mon_calc_stats_rl.F) -- host-side monitor of
+    downloaded fields; arr/hfac (nTiles, nz, ny, nx), mask/area (nTiles, ny, nx).
+    Sums are in the reference's order (tile, k, j, i)."""
+    OLx, OLy, sNx, sNy = g.OLx, g.OLy, g.sNx, g.sNy
+    nz = arr.shape[1]
+    theMin = theMax = 0.0
+    noPnts = True
+    tNb, tDel2, tVol, tMean = [], [], [], []
+    for t in range(arr.shape[0]):
+        nb = d2 = vol = mean = 0.0
+        for k in range(nz):
+            for j in range(1, sNy + 1):
+                J = j + OLy - 1
+                for i in range(1, sNx + 1):
+                    I = i + OLx - 1
+                    v = arr[t, k, J, I]
+                    msk = mask[t, J, I] * hfac[t, k, J, I]
+                    if msk > 0.0:
+                        if noPnts:
+                            theMin = theMax = v
+                            noPnts = False
+                        theMin = min(theMin, v)
+                        theMax = max(theMax, v)
+                        ddx = hfac[t, k, J, I + 1] * hfac[t, k, J, I - 1]
+                        if ddx > 0.0:
+                            ddx = (arr[t, k, J, I + 1] - v) + (arr[t, k, J, I - 1] - v)
+                        ddy = hfac[t, k, J + 1, I] * hfac[t, k, J - 1, I]
+                        if ddy > 0.0:
+                            ddy = (arr[t, k, J + 1, I] - v) + (arr[t, k, J - 1, I] - v)
+                        d2 = d2 + ddx * ddx + ddy * ddy
+                        nb = nb + 1.0
+                        tv = area[t, J, I] * dr[k] * msk
+                        vol = vol + tv
+                        mean = mean + tv * v
+        tNb.append(nb); tDel2.append(d2); tVol.append(vol); tMean.append(mean)
+    gs = lambda xs: sum(xs, 0.0)
+    theNb, theDel2, theVol, theMean = gs(tNb), gs(tDel2), gs(tVol), gs(tMean)
+    theSD = 0.0
+    if theNb > 0.0:
+        theDel2 = np.sqrt(theDel2) / theNb
+    if theVol > 0.0:
+        theMean = theMean / theVol
+        sds = []
+        for t in range(arr.shape[0]):
+            sd = 0.0
+            for k in range(nz):
+                for j in range(1, sNy + 1):
+                    J = j + OLy - 1
+                    for i in range(1, sNx + 1):
+                        I = i + OLx - 1
+                        msk = mask[t, J, I] * hfac[t, k, J, I]
+                        if msk > 0.0:
+                            tv = area[t, J, I] * dr[k] * msk
+                            sd = sd + tv * (arr[t, k, J, I] - theMean) * (arr[t, k, J, I] - theMean)
+            sds.append(sd)
+        theSD = np.sqrt(gs(sds) / theVol)
+    return {"min": theMin, "max": theMax, "mean": theMean, "sd": theSD, "del2": theDel2}
+
+
+def dynstat(model):
+    """dynstat block of MONITOR (pkg/monitor/monitor.F:103-129) for eta, u, v, w."""
+    g = model.g
+    f = g.f
+    out = {}
+    eta = model.get("etaN")[:, None]
+    for name, arr, hf, mask, area, dr in (
+            ("eta", eta, f["maskInC"][:, None], f["maskInC"], f["rA"], f["drF"]),
+            ("uvel", model.get("uVel"), f["hFacW"], f["maskInW"], f["rAw"], f["drF"]),
+            ("vvel", model.get("vVel"), f["hFacS"], f["maskInS"], f["rAs"], f["drF"]),
+            ("wvel", model.get("wVel"), f["maskC"], f["maskInC"], f["rA"], f["drC"])):
+        st = mon_stats(g, arr, hf, mask, area, dr)
+        for k, v in st.items():
+            out["dynstat_%s_%s" % (name, k)] = float(v)
+    return out
