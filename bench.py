@@ -138,7 +138,7 @@ def main():
         "cg2d_iters_per_s": cg2d_iters_per_s,
         "cg2d_mean_iters_per_solve": iters_total / max(1, len(iters)),
         "kernel_ms_mean": {k: v[0] for k, v in kern.items()},
-        "roofline": {"bound": "hbm", "kernel": "k_cg2d_block", "achieved": achieved, "peak": HBM_PEAK_GBS,
+        "roofline": {"bound": "hbm", "kernel": "k_cg2d_blk2 (k_cg2d_block for odd tile sizes)", "achieved": achieved, "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": None,
                      "bytes_per_launch": bytes_per_launch, "launch_ms": cg_ms, "launches": cg_n},
     }

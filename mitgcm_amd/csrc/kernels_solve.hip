@@ -14,10 +14,12 @@
 //     point it is a copy of), so an exchange costs nothing;
 //   * x, s, r and (as register room allows) the 10 operator coefficients of
 //     each point stay in VGPRs;
-//   * each global sum is a wave64 butterfly (DPP/shfl_xor) + one LDS slot per
-//     wave + one barrier; every thread then adds the 16 wave partials in the
-//     same fixed order, so all lanes hold bit-identical sums (no broadcast,
+//   * each global sum is a DPP row reduction + 4 readlanes per wave, one LDS
+//     slot per wave, one barrier, and a DPP row reduction of the 16 wave
+//     partials; every lane ends with the bit-identical sum (no broadcast,
 //     run-to-run deterministic).
+#include <cstdlib>
+
 #include "common.h"
 
 namespace mgcm {
@@ -25,38 +27,65 @@ namespace mgcm {
 constexpr int CG_THREADS = 1024;
 constexpr int CG_WAVES = CG_THREADS / 64;
 
-__device__ __forceinline__ double wave_sum(double v) {
-#pragma unroll
-  for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
+// ---- wave64 reductions on the DPP path (no LDS round trips) --------------
+// One DPP step moves a 64-bit value between lanes of a 16-lane row as two
+// v_mov_b32_dpp.  Butterfly xor1 (quad_perm 1,0,3,2), xor2 (quad_perm 2,3,0,1),
+// row_half_mirror, row_mirror: after the four steps every lane of a row holds
+// the row's sum, bit-identical across the row (each step adds a commuted pair).
+template <int CTRL>
+__device__ __forceinline__ double dpp_f64(double v) {
+  const long long b = __builtin_bit_cast(long long, v);
+  const int lo = __builtin_amdgcn_update_dpp(0, (int)(b & 0xffffffff), CTRL, 0xF, 0xF, false);
+  const int hi = __builtin_amdgcn_update_dpp(0, (int)(b >> 32), CTRL, 0xF, 0xF, false);
+  return __builtin_bit_cast(double, ((long long)hi << 32) | (unsigned)lo);
+}
+__device__ __forceinline__ double row_sum16(double v) {
+  v = v + dpp_f64<0xB1>(v);   // quad_perm [1,0,3,2]
+  v = v + dpp_f64<0x4E>(v);   // quad_perm [2,3,0,1]
+  v = v + dpp_f64<0x141>(v);  // row_half_mirror
+  v = v + dpp_f64<0x140>(v);  // row_mirror
   return v;
+}
+__device__ __forceinline__ double row_max16(double v) {
+  v = fmax(v, dpp_f64<0xB1>(v));
+  v = fmax(v, dpp_f64<0x4E>(v));
+  v = fmax(v, dpp_f64<0x141>(v));
+  v = fmax(v, dpp_f64<0x140>(v));
+  return v;
+}
+__device__ __forceinline__ double lane_f64(double v, int l) {
+  const long long b = __builtin_bit_cast(long long, v);
+  const int lo = __builtin_amdgcn_readlane((int)(b & 0xffffffff), l);
+  const int hi = __builtin_amdgcn_readlane((int)(b >> 32), l);
+  return __builtin_bit_cast(double, ((long long)hi << 32) | (unsigned)lo);
+}
+// wave sum, identical in every lane: rows by DPP, then (r0+r1)+(r2+r3)
+__device__ __forceinline__ double wave_sum(double v) {
+  v = row_sum16(v);
+  return (lane_f64(v, 0) + lane_f64(v, 16)) + (lane_f64(v, 32) + lane_f64(v, 48));
 }
 __device__ __forceinline__ double wave_max(double v) {
-#pragma unroll
-  for (int o = 32; o >= 1; o >>= 1) v = fmax(v, __shfl_xor(v, o, 64));
-  return v;
+  v = row_max16(v);
+  return fmax(fmax(lane_f64(v, 0), lane_f64(v, 16)), fmax(lane_f64(v, 32), lane_f64(v, 48)));
 }
 
-// Block-wide sum; `slot` selects one of 4 rotating LDS partial buffers so that
-// consecutive reductions need only the one barrier each.
+// Block-wide sum over the 16 waves; `slot` selects one of 4 rotating LDS
+// partial buffers so consecutive reductions need only one barrier each.  After
+// the barrier lane l of every wave reads partial[l & 15] and reduces its row:
+// every lane of the block ends with the same, bit-identical sum.
 __device__ __forceinline__ double block_sum(double v, double *red, int slot) {
   v = wave_sum(v);
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   if (lane == 0) red[slot * CG_WAVES + wv] = v;
   __syncthreads();
-  double s = 0.0;
-#pragma unroll
-  for (int w = 0; w < CG_WAVES; w++) s = s + red[slot * CG_WAVES + w];
-  return s;
+  return row_sum16(red[slot * CG_WAVES + (lane & 15)]);
 }
 __device__ __forceinline__ double block_max(double v, double *red, int slot) {
   v = wave_max(v);
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   if (lane == 0) red[slot * CG_WAVES + wv] = v;
   __syncthreads();
-  double s = red[slot * CG_WAVES];
-#pragma unroll
-  for (int w = 1; w < CG_WAVES; w++) s = fmax(s, red[slot * CG_WAVES + w]);
-  return s;
+  return row_max16(red[slot * CG_WAVES + (lane & 15)]);
 }
 
 // CALC_DIV_GHAT over k = Nr..1 + free-surface term; cg2d_x = Bo_surf*etaN (full range).
@@ -293,6 +322,252 @@ __global__ void __launch_bounds__(CG_THREADS) k_cg2d_block(Dims d, Params p, Fie
 #undef pS1
 }
 
+// 2x2-blocked whole-solve CG2D (tiles with even sNx, sNy; <= 4096 points):
+// each thread owns the 2x2 block (i0..i0+1, j0..j0+1), i0 and j0 odd, of one
+// tile.  The block's four in-block neighbour values come from its own
+// registers; only the eight out-of-block ones (two per side) are LDS reads
+// through the neighbour table, and all 32 operator coefficients of the block
+// (aW/pW at i0..i0+2, aS/pS at j0..j0+2, aC, pC) stay in VGPRs.  Products are
+// FMA-contracted here: CG2D's parity bar is roundoff agreement (its global
+// sums are re-ordered anyway), not bit-exactness.
+// nb4[4*T]: packed 16-bit compact indices (W0|W1<<16), (E0|E1<<16),
+// (S0|S1<<16), (N0|N1<<16); blk[T] = 2-D offset of (i0,j0) (T = #blocks,
+// padding blocks: offset of a real block, neighbours -> ZERO slot, inactive).
+template <bool MINRES>
+__global__ void __launch_bounds__(CG_THREADS) k_cg2d_blk2(Dims d, Params p, Fields f, const unsigned *__restrict__ nb4,
+                                                         const int *__restrict__ blk, int nBlk, int maxIters,
+                                                         int nIterMinIn, SolveRecord *rec, int *stepCounter) {
+#pragma clang fp contract(fast)
+  constexpr int NP = 4 * CG_THREADS;
+  extern __shared__ __attribute__((aligned(16))) double lds[];
+  double *r_l = lds;                // NP + 1 (last = ZERO slot)
+  double *s_l = lds + (NP + 1);
+  double *red = lds + 2 * (NP + 1);
+  const int tid = threadIdx.x;
+  const bool act = tid < nBlk;
+  const int bt = act ? tid : 0;
+  const long g = blk[bt];
+  const long nx = d.nx;
+  // compact LDS slots of the block's own points: tile-major, row-major in the tile
+  const int t0 = (int)(g / d.n2), l0 = (int)(g % d.n2);
+  const int i0 = l0 % d.nx - d.OLx + 1, j0 = l0 / d.nx - d.OLy + 1;
+  const int c00 = act ? t0 * d.sNx * d.sNy + (j0 - 1) * d.sNx + (i0 - 1) : NP;
+  const int c10 = act ? c00 + 1 : NP, c01 = act ? c00 + d.sNx : NP, c11 = act ? c00 + d.sNx + 1 : NP;
+  const unsigned wW = nb4[4 * bt], wE = nb4[4 * bt + 1], wS = nb4[4 * bt + 2], wN = nb4[4 * bt + 3];
+#define LO(w) ((w) & 0xFFFFu)
+#define HI(w) ((w) >> 16)
+  // coefficients (halo-inclusive arrays: the i0+2 / j0+2 entries may be halo values,
+  // exactly what the reference reads after EXCH_UV_XY_RS / EXCH_XY_RS)
+  const double az = act ? 1.0 : 0.0;
+  // A (aW, aS, aC) and pW stay in VGPRs; pS and pC (10 values) live in LDS,
+  // structure-of-arrays over threads (conflict-free), to stay under 128 VGPRs.
+  double *pl = red + 4 * CG_WAVES;  // 10 * CG_THREADS
+  double aW[2][3], pW[2][3], aS[2][3], aC[2][2];
+#pragma unroll
+  for (int b = 0; b < 2; b++)
+#pragma unroll
+    for (int a = 0; a < 3; a++) {
+      aW[b][a] = az * f.aW2d[g + a + b * nx];
+      pW[b][a] = az * f.pW[g + a + b * nx];
+      aS[b][a] = az * f.aS2d[g + b + a * nx];  // [column b][row a]
+      pl[(b * 3 + a) * CG_THREADS + tid] = az * f.pS[g + b + a * nx];
+    }
+#pragma unroll
+  for (int b = 0; b < 2; b++)
+#pragma unroll
+    for (int a = 0; a < 2; a++) {
+      aC[b][a] = az * f.aC2d[g + a + b * nx];   // [row b][col a]
+      pl[(6 + b * 2 + a) * CG_THREADS + tid] = az * f.pC[g + a + b * nx];
+    }
+#define pS(b, a) pl[((b) * 3 + (a)) * CG_THREADS + tid]
+#define pC(b, a) pl[(6 + (b) * 2 + (a)) * CG_THREADS + tid]
+  // state of the 4 points, index [row b][col a]
+  double x[2][2], r[2][2], s[2][2], b_[2][2];
+#pragma unroll
+  for (int b = 0; b < 2; b++)
+#pragma unroll
+    for (int a = 0; a < 2; a++) {
+      b_[b][a] = act ? f.cg2d_b[g + a + b * nx] : 0.0;
+      x[b][a] = act ? f.cg2d_x[g + a + b * nx] : 0.0;
+      s[b][a] = 0.0;
+    }
+  if (tid == 0) { r_l[NP] = 0.0; s_l[NP] = 0.0; }
+  const int cs[2][2] = {{c00, c10}, {c01, c11}};
+
+  // 5-point operator on the block: out[b][a] = sum of coef*value (reference order C?:
+  // A: aW*v(i-1)+aW(i+1)*v(i+1)+aS*v(j-1)+aS(j+1)*v(j+1)+aC*v ; M: pC*v+pW*..+pS*..)
+#define NEIGH(arr, v, vW0, vW1, vE0, vE1, vS0, vS1, vN0, vN1)                                              \
+  const double vW0 = arr[LO(wW)], vW1 = arr[HI(wW)], vE0 = arr[LO(wE)], vE1 = arr[HI(wE)];                \
+  const double vS0 = arr[LO(wS)], vS1 = arr[HI(wS)], vN0 = arr[LO(wN)], vN1 = arr[HI(wN)];
+#define APPLY_A(out, v, vW0, vW1, vE0, vE1, vS0, vS1, vN0, vN1)                                            \
+  out[0][0] = aW[0][0] * vW0 + aW[0][1] * v[0][1] + aS[0][0] * vS0 + aS[0][1] * v[1][0] + aC[0][0] * v[0][0]; \
+  out[0][1] = aW[0][1] * v[0][0] + aW[0][2] * vE0 + aS[1][0] * vS1 + aS[1][1] * v[1][1] + aC[0][1] * v[0][1]; \
+  out[1][0] = aW[1][0] * vW1 + aW[1][1] * v[1][1] + aS[0][1] * v[0][0] + aS[0][2] * vN0 + aC[1][0] * v[1][0]; \
+  out[1][1] = aW[1][1] * v[1][0] + aW[1][2] * vE1 + aS[1][1] * v[0][1] + aS[1][2] * vN1 + aC[1][1] * v[1][1];
+#define APPLY_M(out, v, vW0, vW1, vE0, vE1, vS0, vS1, vN0, vN1)                                            \
+  out[0][0] = pC(0, 0) * v[0][0] + pW[0][0] * vW0 + pW[0][1] * v[0][1] + pS(0, 0) * vS0 + pS(0, 1) * v[1][0]; \
+  out[0][1] = pC(0, 1) * v[0][1] + pW[0][1] * v[0][0] + pW[0][2] * vE0 + pS(1, 0) * vS1 + pS(1, 1) * v[1][1]; \
+  out[1][0] = pC(1, 0) * v[1][0] + pW[1][0] * vW1 + pW[1][1] * v[1][1] + pS(0, 1) * v[0][0] + pS(0, 2) * vN0; \
+  out[1][1] = pC(1, 1) * v[1][1] + pW[1][1] * v[1][0] + pW[1][2] * vE1 + pS(1, 1) * v[0][1] + pS(1, 2) * vN1;
+
+  // cg2d.F:104-133: normalise the RHS
+  double rhsMax = 0.0;
+#pragma unroll
+  for (int b = 0; b < 2; b++)
+#pragma unroll
+    for (int a = 0; a < 2; a++) { b_[b][a] = b_[b][a] * p.cg2dNorm; rhsMax = fmax(fabs(b_[b][a]), rhsMax); }
+  rhsMax = block_max(rhsMax, red, 0);
+  double rhsNorm = 1.0;
+  if (p.cg2dNormaliseRHS) {
+    if (rhsMax != 0.0) rhsNorm = 1.0 / rhsMax;
+#pragma unroll
+    for (int b = 0; b < 2; b++)
+#pragma unroll
+      for (int a = 0; a < 2; a++) { b_[b][a] = b_[b][a] * rhsNorm; x[b][a] = x[b][a] * rhsNorm; }
+  }
+  // EXCH_XY_RL(cg2d_x) through LDS
+#pragma unroll
+  for (int b = 0; b < 2; b++)
+#pragma unroll
+    for (int a = 0; a < 2; a++) s_l[cs[b][a]] = x[b][a];
+  if (tid == 0) s_l[NP] = 0.0;
+  __syncthreads();
+  double err = 0.0, sumB = 0.0;
+  {
+    double ax[2][2];
+    NEIGH(s_l, x, xW0, xW1, xE0, xE1, xS0, xS1, xN0, xN1)
+    APPLY_A(ax, x, xW0, xW1, xE0, xE1, xS0, xS1, xN0, xN1)
+#pragma unroll
+    for (int b = 0; b < 2; b++)
+#pragma unroll
+      for (int a = 0; a < 2; a++) {
+        r[b][a] = b_[b][a] - ax[b][a];
+        err = err + r[b][a] * r[b][a];
+        sumB = sumB + b_[b][a];
+      }
+  }
+  double xmin[2][2];
+  if (MINRES) {
+#pragma unroll
+    for (int b = 0; b < 2; b++)
+#pragma unroll
+      for (int a = 0; a < 2; a++) xmin[b][a] = x[b][a];
+  }
+  if (act) {
+#pragma unroll
+    for (int b = 0; b < 2; b++)
+#pragma unroll
+      for (int a = 0; a < 2; a++) f.cg2d_b[g + a + b * nx] = b_[b][a];
+  }
+  double err_sq = block_sum(err, red, 1);
+  const double sumRHS = block_sum(sumB, red, 2);
+#pragma unroll
+  for (int b = 0; b < 2; b++)
+#pragma unroll
+    for (int a = 0; a < 2; a++) { r_l[cs[b][a]] = r[b][a]; s_l[cs[b][a]] = 0.0; }
+  if (tid == 0) { r_l[NP] = 0.0; s_l[NP] = 0.0; }
+  const double firstResidual = sqrt(err_sq);
+  int nIterMin = nIterMinIn;
+  double minResidualSq = -1.0;
+  if (MINRES && nIterMin >= 0) { nIterMin = 0; minResidualSq = err_sq; }
+  int actualIts = 0;
+  double eta_qrNM1 = 1.0;
+  __syncthreads();
+  int slot = 3;
+  if (!(err_sq < p.cg2dTolerance_sq)) {
+    for (int it2d = 1; it2d <= maxIters; it2d++) {
+      asm volatile("" ::: "memory");  // re-read pS/pC from LDS every iteration (no hoisting into VGPRs)
+      double q[2][2];
+      double e = 0.0;
+      {
+        NEIGH(r_l, r, rW0, rW1, rE0, rE1, rS0, rS1, rN0, rN1)
+        APPLY_M(q, r, rW0, rW1, rE0, rE1, rS0, rS1, rN0, rN1)
+      }
+#pragma unroll
+      for (int b = 0; b < 2; b++)
+#pragma unroll
+        for (int a = 0; a < 2; a++) e = e + q[b][a] * r[b][a];
+      slot = (slot + 1) & 3;
+      const double eta_qrN = block_sum(e, red, slot);
+      const double cgBeta = eta_qrN / eta_qrNM1;
+      eta_qrNM1 = eta_qrN;
+#pragma unroll
+      for (int b = 0; b < 2; b++)
+#pragma unroll
+        for (int a = 0; a < 2; a++) { s[b][a] = q[b][a] + cgBeta * s[b][a]; s_l[cs[b][a]] = s[b][a]; }
+      __syncthreads();
+      double aa = 0.0;
+      {
+        NEIGH(s_l, s, sW0, sW1, sE0, sE1, sS0, sS1, sN0, sN1)
+        APPLY_A(q, s, sW0, sW1, sE0, sE1, sS0, sS1, sN0, sN1)
+      }
+#pragma unroll
+      for (int b = 0; b < 2; b++)
+#pragma unroll
+        for (int a = 0; a < 2; a++) aa = aa + s[b][a] * q[b][a];
+      slot = (slot + 1) & 3;
+      double alpha = block_sum(aa, red, slot);
+      alpha = eta_qrN / alpha;
+      double e2 = 0.0;
+#pragma unroll
+      for (int b = 0; b < 2; b++)
+#pragma unroll
+        for (int a = 0; a < 2; a++) {
+          x[b][a] = x[b][a] + alpha * s[b][a];
+          r[b][a] = r[b][a] - alpha * q[b][a];
+          e2 = e2 + r[b][a] * r[b][a];
+          r_l[cs[b][a]] = r[b][a];
+        }
+      actualIts = it2d;
+      slot = (slot + 1) & 3;
+      err_sq = block_sum(e2, red, slot);
+      if (err_sq < p.cg2dTolerance_sq) break;
+      if (MINRES && err_sq < minResidualSq) {
+        minResidualSq = err_sq;
+        nIterMin = it2d;
+#pragma unroll
+        for (int b = 0; b < 2; b++)
+#pragma unroll
+          for (int a = 0; a < 2; a++) xmin[b][a] = x[b][a];
+      }
+    }
+  }
+  if (MINRES && nIterMin >= 0 && err_sq > minResidualSq) {
+#pragma unroll
+    for (int b = 0; b < 2; b++)
+#pragma unroll
+      for (int a = 0; a < 2; a++) x[b][a] = xmin[b][a];
+  }
+  if (act) {
+#pragma unroll
+    for (int b = 0; b < 2; b++)
+#pragma unroll
+      for (int a = 0; a < 2; a++) {
+        double xv = x[b][a];
+        if (p.cg2dNormaliseRHS) xv = xv / rhsNorm;
+        f.cg2d_x[g + a + b * nx] = xv;
+      }
+  }
+  if (tid == 0) {
+    const int st = stepCounter ? *stepCounter : 0;
+    SolveRecord &R = rec[st];
+    R.firstResidual = firstResidual;
+    R.lastResidual = sqrt(err_sq);
+    R.minResidualSq = minResidualSq;
+    R.rhsMax = rhsMax;
+    R.sumRHS = sumRHS;
+    R.numIters = actualIts;
+    R.nIterMin = nIterMin;
+  }
+#undef LO
+#undef HI
+#undef NEIGH
+#undef APPLY_A
+#undef APPLY_M
+#undef pS
+#undef pC
+}
+
 // Halo exchange of `nz` levels through a precomputed map (EXCH1 / EXCH2 scalar).
 // map[2*h] = destination 2-D flat offset (t*n2+local), map[2*h+1] = source.
 __global__ void __launch_bounds__(256) k_exchange(Dims d, double *a, const long *__restrict__ map, int nHalo, int nz) {
@@ -383,10 +658,15 @@ hipError_t launch_cg2d_block(const Dims &d, const Params &p, const Fields &f, co
   if (!ppt) return hipErrorInvalidValue;
   const size_t lds = cg2d_block_lds_bytes(ppt);
   const bool mr = nIterMin >= 0;
+  // experiment knob: MGCM_CG2D_CREG=0/1/2 forces the coefficient caching tier at PPT=4
+  static int creg_override = [] { const char *e = getenv("MGCM_CG2D_CREG"); return e ? atoi(e) : -1; }();
 #define LAUNCH(PPT)                                                                                        \
   do {                                                                                                     \
-    constexpr int CR = (PPT <= 2) ? 2 : 0;                                                \
+    constexpr int CR = (PPT <= 2) ? 2 : (PPT <= 4 ? 1 : 0);                                                                 \
     auto kern = mr ? k_cg2d_block<PPT, true, CR> : k_cg2d_block<PPT, false, CR>;                           \
+    if (PPT == 4 && creg_override >= 0)                                                                    \
+      kern = creg_override == 2 ? (mr ? k_cg2d_block<4, true, 2> : k_cg2d_block<4, false, 2>)             \
+           : creg_override == 1 ? (mr ? k_cg2d_block<4, true, 1> : k_cg2d_block<4, false, 1>) : kern;     \
     hipError_t e_ = hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds); \
     if (e_ != hipSuccess) return e_;                                                                       \
     hipLaunchKernelGGL(kern, dim3(1), dim3(CG_THREADS), lds, s, d, p, f, nbr, gofs, nPts, maxIters, nIterMin, rec, \
@@ -399,6 +679,18 @@ hipError_t launch_cg2d_block(const Dims &d, const Params &p, const Fields &f, co
     default: LAUNCH(8); break;
   }
 #undef LAUNCH
+  return hipGetLastError();
+}
+
+hipError_t launch_cg2d_blk2(const Dims &d, const Params &p, const Fields &f, const unsigned *nb4, const int *blk,
+                            int nBlk, int maxIters, int nIterMin, SolveRecord *rec, int *stepCounter, hipStream_t s) {
+  if (nBlk > CG_THREADS) return hipErrorInvalidValue;
+  const size_t lds = cg2d_block_lds_bytes(4) + 10 * CG_THREADS * sizeof(double);  // 146 KiB
+  auto kern = nIterMin >= 0 ? k_cg2d_blk2<true> : k_cg2d_blk2<false>;
+  hipError_t e = hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(kern, dim3(1), dim3(CG_THREADS), lds, s, d, p, f, nb4, blk, nBlk, maxIters, nIterMin, rec,
+                     stepCounter);
   return hipGetLastError();
 }
 

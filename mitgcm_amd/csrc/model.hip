@@ -24,6 +24,8 @@ hipError_t launch_sfp_rhs(const Dims &, const Params &, const Fields &, hipStrea
 hipError_t launch_cg2d_block(const Dims &, const Params &, const Fields &, const unsigned *, const int *, int, int, int,
                              SolveRecord *, int *, hipStream_t);
 int cg2d_block_ppt(int nPts);
+hipError_t launch_cg2d_blk2(const Dims &, const Params &, const Fields &, const unsigned *, const int *, int, int, int,
+                            SolveRecord *, int *, hipStream_t);
 int cg2d_block_max_points();
 hipError_t launch_exchange(const Dims &, double *, const long *, int, int, hipStream_t);
 hipError_t launch_eta_update(const Dims &, const Fields &, hipStream_t);
@@ -112,6 +114,10 @@ struct mgcm_model {
   unsigned *d_nbr = nullptr;  // packed (W|E<<16),(S|N<<16) compact neighbour indices, padded
   int *d_gofs = nullptr;      // 2-D flat offset of each (padded) interior point
   int nPts = 0;
+  // 2x2-blocked solver tables (even sNx, sNy; <= 1024 blocks)
+  unsigned *d_nb4 = nullptr;
+  int *d_blk = nullptr;
+  int nBlk = 0;
   // step counters: [0] = myIter, [1] = record slot
   int *d_ctr = nullptr;
   SolveRecord *d_rec = nullptr;
@@ -257,6 +263,40 @@ static int build_nbr(mgcm_model *m) {
   HIPCHK(hipMemcpy(m->d_nbr, nb.data(), nb.size() * sizeof(unsigned), hipMemcpyHostToDevice));
   HIPCHK(hipMalloc(&m->d_gofs, gofs.size() * sizeof(int)));
   HIPCHK(hipMemcpy(m->d_gofs, gofs.data(), gofs.size() * sizeof(int), hipMemcpyHostToDevice));
+  // 2x2 blocks: only for even tile sizes and <= 1024 blocks; ZERO slot = 4*1024
+  m->nBlk = 0;
+  const int nBk = d.nTiles * (d.sNx / 2) * (d.sNy / 2);
+  if (d.sNx % 2 == 0 && d.sNy % 2 == 0 && nBk <= 1024 && !getenv("MGCM_CG2D_NOBLK")) {
+    const unsigned Z = 4096u;
+    auto cmp = [&](long g) -> unsigned {
+      unsigned c = compact(g);
+      return c == ZERO ? Z : c;
+    };
+    auto nbv = [&](int i, int j, int t) -> unsigned {  // value slot of the point (i,j,t), via halo map
+      long g = MG_I2(d, i, j, t);
+      if (i < 1 || i > d.sNx || j < 1 || j > d.sNy) g = srcOf[g];
+      return cmp(g);
+    };
+    std::vector<unsigned> nb4(4 * 1024, Z | (Z << 16));
+    std::vector<int> blk(1024, (int)MG_I2(d, 1, 1, 0));
+    int q = 0;
+    for (int t = 0; t < d.nTiles; t++)
+      for (int j0 = 1; j0 <= d.sNy; j0 += 2)
+        for (int i0 = 1; i0 <= d.sNx; i0 += 2, q++) {
+          blk[q] = (int)MG_I2(d, i0, j0, t);
+          nb4[4 * q + 0] = nbv(i0 - 1, j0, t) | (nbv(i0 - 1, j0 + 1, t) << 16);
+          nb4[4 * q + 1] = nbv(i0 + 2, j0, t) | (nbv(i0 + 2, j0 + 1, t) << 16);
+          nb4[4 * q + 2] = nbv(i0, j0 - 1, t) | (nbv(i0 + 1, j0 - 1, t) << 16);
+          nb4[4 * q + 3] = nbv(i0, j0 + 2, t) | (nbv(i0 + 1, j0 + 2, t) << 16);
+        }
+    if (m->d_nb4) (void)hipFree(m->d_nb4);
+    if (m->d_blk) (void)hipFree(m->d_blk);
+    HIPCHK(hipMalloc(&m->d_nb4, nb4.size() * sizeof(unsigned)));
+    HIPCHK(hipMemcpy(m->d_nb4, nb4.data(), nb4.size() * sizeof(unsigned), hipMemcpyHostToDevice));
+    HIPCHK(hipMalloc(&m->d_blk, blk.size() * sizeof(int)));
+    HIPCHK(hipMemcpy(m->d_blk, blk.data(), blk.size() * sizeof(int), hipMemcpyHostToDevice));
+    m->nBlk = nBk;
+  }
   return 0;
 }
 
@@ -325,6 +365,8 @@ void mgcm_destroy(mgcm_model *m) {
   if (m->d_halo) hipFree(m->d_halo);
   if (m->d_nbr) hipFree(m->d_nbr);
   if (m->d_gofs) hipFree(m->d_gofs);
+  if (m->d_nb4) hipFree(m->d_nb4);
+  if (m->d_blk) hipFree(m->d_blk);
   if (m->d_ctr) hipFree(m->d_ctr);
   if (m->d_rec) hipFree(m->d_rec);
   if (m->stream) hipStreamDestroy(m->stream);
@@ -436,6 +478,14 @@ int mgcm_init(mgcm_model *m) {
   return 0;
 }
 
+static hipError_t launch_cg2d(mgcm_model *m, int maxIters, int nIterMin) {
+  if (m->nBlk > 0)
+    return launch_cg2d_blk2(m->d, m->p, m->f, m->d_nb4, m->d_blk, m->nBlk, maxIters, nIterMin, m->d_rec, m->d_ctr + 1,
+                            m->stream);
+  return launch_cg2d_block(m->d, m->p, m->f, m->d_nbr, m->d_gofs, m->nPts, maxIters, nIterMin, m->d_rec, m->d_ctr + 1,
+                           m->stream);
+}
+
 static int check_ready(mgcm_model *m) {
   if (!m->ready) return set_err("model not initialised: call mgcm_init() after loading the fields");
   return 0;
@@ -458,8 +508,7 @@ int mgcm_dynamics(mgcm_model *m) {
 static int solve_impl(mgcm_model *m) {
   TIMED(K_RHS, launch_sfp_rhs(m->d, m->p, m->f, m->stream));
   const int nIterMin = m->p.cg2dUseMinResSol - 1;
-  TIMED(K_CG2D, launch_cg2d_block(m->d, m->p, m->f, m->d_nbr, m->d_gofs, m->nPts, m->p.cg2dMaxIters, nIterMin, m->d_rec,
-                                  m->d_ctr + 1, m->stream));
+  TIMED(K_CG2D, launch_cg2d(m, m->p.cg2dMaxIters, nIterMin));
   TIMED(K_EXCH, launch_exchange(m->d, m->f.cg2d_x, m->d_halo, m->nHalo, 1, m->stream));
   TIMED(K_ETA, launch_eta_update(m->d, m->f, m->stream));
   return 0;
@@ -558,8 +607,7 @@ int mgcm_cg2d(mgcm_model *m, double *cg2d_b, double *cg2d_x, double *firstResidu
   HIPCHK(hipMemcpyAsync(m->f.cg2d_b, cg2d_b, n * sizeof(double), hipMemcpyHostToDevice, m->stream));
   HIPCHK(hipMemcpyAsync(m->f.cg2d_x, cg2d_x, n * sizeof(double), hipMemcpyHostToDevice, m->stream));
   HIPCHK(hipMemsetAsync(m->d_ctr + 1, 0, sizeof(int), m->stream));
-  TIMED(K_CG2D, launch_cg2d_block(m->d, m->p, m->f, m->d_nbr, m->d_gofs, m->nPts, *numIters, *nIterMin, m->d_rec, m->d_ctr + 1,
-                                  m->stream));
+  TIMED(K_CG2D, launch_cg2d(m, *numIters, *nIterMin));
   HIPCHK(hipMemcpyAsync(cg2d_b, m->f.cg2d_b, n * sizeof(double), hipMemcpyDeviceToHost, m->stream));
   HIPCHK(hipMemcpyAsync(cg2d_x, m->f.cg2d_x, n * sizeof(double), hipMemcpyDeviceToHost, m->stream));
   SolveRecord r;
