@@ -140,3 +140,39 @@ def test_gyre_fields_vs_oracle_after_10_steps(gyre):
         err = np.abs(dev - st[n]).max()
         assert err <= 1e-10 * sc, (n, err, sc)
     m.close()
+
+
+def test_fortran_cg2d_dropin(gyre, tmp_path):
+    """Fortran host -> CG2D_AMD (reference CG2D argument list) -> HIP, against the oracle."""
+    import os
+    import subprocess
+    from oracle.harness import gyre_oracle
+    g, params, state = gyre.barotropic_gyre()
+    o = gyre_oracle()
+    rng = np.random.default_rng(11)
+    inner = g.sl(1, g.sNx, 1, g.sNy)
+    b = np.zeros((1, g.ny, g.nx))
+    b[0][inner] = rng.standard_normal((g.sNy, g.sNx))
+    b[0] *= g.f["maskInC"][0]
+    x0 = np.zeros_like(b)
+    hdr = np.array([g.sNx, g.sNy, g.OLx, g.OLy, g.nSx, g.nSy, 1000, int(g.cg2dNormaliseRHS)], dtype=np.int32)
+    with open(tmp_path / "cg2d_in.bin", "wb") as fh:
+        fh.write(hdr.tobytes())
+        fh.write(np.array([g.cg2dNorm, g.cg2dTolerance_sq]).tobytes())
+        for n in ("aW2d", "aS2d", "aC2d", "pW", "pS", "pC"):
+            fh.write(np.ascontiguousarray(g.f[n]).tobytes())
+        fh.write(b.tobytes())
+        fh.write(x0.tobytes())
+    exe = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "mitgcm_amd", "fortran",
+                       "cg2d_host")
+    r = subprocess.run([exe, str(tmp_path)], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr
+    raw = open(tmp_path / "cg2d_out.bin", "rb").read()
+    its, itmin = np.frombuffer(raw[:8], dtype=np.int32)
+    first, minsq, last = np.frombuffer(raw[8:32], dtype=np.float64)
+    xf = np.frombuffer(raw[32:], dtype=np.float64).reshape(b.shape)
+    xo, fo, mo, lo, ito, imo = o.cg2d(b, x0, 1000, -1)
+    assert its == ito
+    assert abs(first - fo) <= 1e-12 * abs(fo)
+    sc = np.abs(xo[0][inner]).max()
+    assert np.abs(xf[0][inner] - xo[0][inner]).max() <= 1e-12 * sc
