@@ -38,6 +38,8 @@ def parse():
     ap.add_argument("--config", default="tutorial_barotropic_gyre")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--pmc-summary", default=os.path.join(ROOT, "profiles", "r01", "pmc_summary.json"),
+                    help="tools/pmc_summary.py output of rocprofv3 --pmc passes of this command (roofline.traffic)")
     return ap.parse_args()
 
 
@@ -55,6 +57,20 @@ def cpu_baseline(seconds):
     return {"value": n * 1200.0 / 86400.0 / dt, "unit": "model-days/s", "cores": 1, "kind": "port",
             "sample": "%d FORWARD_STEPs of tutorial_barotropic_gyre 62x62x1 on the oracle "
                       "(oracle/*.c, gcc -O2, 1 thread), %.1f s" % (n, dt)}
+
+
+def pmc_traffic(path, kernel_prefix):
+    """HBM bytes per launch of the dominant kernel from the committed PMC passes
+    (FETCH_SIZE x2 + WRITE_SIZE, tools/pmc_summary.py); None when absent."""
+    try:
+        import json as _j
+        ks = _j.load(open(path))["kernels"]
+    except (OSError, ValueError, KeyError):
+        return None
+    for k, v in ks.items():
+        if kernel_prefix in k:
+            return v["hbm_bytes_per_launch"]
+    return None
 
 
 def main():
@@ -138,8 +154,11 @@ def main():
         "cg2d_iters_per_s": cg2d_iters_per_s,
         "cg2d_mean_iters_per_solve": iters_total / max(1, len(iters)),
         "kernel_ms_mean": {k: v[0] for k, v in kern.items()},
-        "roofline": {"bound": "hbm", "kernel": "k_cg2d_blk2 (k_cg2d_block for odd tile sizes)", "achieved": achieved, "peak": HBM_PEAK_GBS,
-                     "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+        "roofline": {"bound": "hbm", "kernel": "k_cg2d_" + m.cg2d_kernel(), "achieved": achieved, "peak": HBM_PEAK_GBS,
+                     "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
+                     "traffic": pmc_traffic(a.pmc_summary, "k_cg2d_blk2" if m.cg2d_kernel() == "blk2" else
+                                            "k_cg2d_block"),
+                     "traffic_unit": "bytes per launch (rocprofv3 --pmc, %s)" % os.path.relpath(a.pmc_summary, ROOT),
                      "bytes_per_launch": bytes_per_launch, "launch_ms": cg_ms, "launches": cg_n},
     }
     if rank == 0 and not a.no_cpu_baseline:

@@ -410,6 +410,7 @@ double mgcm_get_param(mgcm_model *m, const char *name) {
     if (hipMemcpy(&it, m->d_ctr, sizeof(int), hipMemcpyDeviceToHost) != hipSuccess) return NAN;
     return it;
   }
+  if (!strcmp(name, "cg2dKernel")) return m->nBlk > 0 ? 2.0 : 1.0;  // 2: k_cg2d_blk2, 1: k_cg2d_block
   for (auto &pd : PARAMS)
     if (!strcmp(pd.name, name)) {
       const char *ptr = reinterpret_cast<const char *>(&m->p) + pd.off;

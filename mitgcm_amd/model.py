@@ -121,6 +121,10 @@ class Model:
                               ctypes.byref(it), ctypes.byref(itm)), "mgcm_cg2d")
         return x, f.value, mn.value, la.value, it.value, itm.value
 
+    def cg2d_kernel(self):
+        """Which CG2D kernel mgcm_init selected: 'blk2' (2x2-blocked) or 'block'."""
+        return "blk2" if lib().mgcm_get_param(self.h, b"cg2dKernel") == 2.0 else "block"
+
     def kernel_timing(self, enable):
         lib().mgcm_kernel_timing(self.h, 1 if enable else 0)
 
