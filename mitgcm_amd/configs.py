@@ -51,6 +51,53 @@ def barotropic_gyre(nSx=1, nSy=1, data_dir=None, bathy=None, wind=None):
     return g, params, state
 
 
+BAROCLINIC_DELR = [50., 60., 70., 80., 90., 100., 110., 120., 130., 140., 150., 160., 170., 180., 190.]
+BAROCLINIC_TREF = [30., 27., 24., 21., 18., 15., 13., 11., 9., 7., 6., 5., 4., 3., 2.]
+
+
+def baroclinic_gyre(nSx=2, nSy=2, data_dir=None, tempAdvScheme=2):
+    """verification/tutorial_baroclinic_gyre: 62x62x15 on a 1-degree spherical-polar
+    grid, code/SIZE.h sNx=sNy=31, OL=2, nSx=nSy=2; input/data: viscAh=5000,
+    viscAr=1e-2, no_slip_bottom=F, diffKhT=1000, diffKrT=1e-5, ivdc_kappa=1,
+    implicitDiffusion, LINEAR EOS tAlpha=2e-4 sBeta=0, rhoNil=999.8, exactConserv,
+    saltStepping=F, deltaT=1200, tauThetaClimRelax=2592000 (SST_relax.bin),
+    xgOrigin=-1, ygOrigin=14, delR as below.  Resolved parameters are pinned
+    against the output.txt dump (tests/test_oracle_3d.py)."""
+    d = data_dir or os.path.join(GOLDEN, "tutorial_baroclinic_gyre")
+    Nx = Ny = 62
+    Nr = 15
+    sNx, sNy = Nx // nSx, Ny // nSy
+    g = Grid(sNx, sNy, 2, 2, Nr, nSx, nSy)
+    g.ini_vertical_grid(BAROCLINIC_DELR)
+    g.ini_spherical_polar_grid(np.full(Nx, 1.0), np.full(Ny, 1.0), -1.0, 14.0)
+    g.ini_cori(selectCoriMap=2)
+    bathy = read_bin(os.path.join(d, "bathy.bin"), (Ny, Nx))
+    g.ini_depths_masks(bathy, hFacMin=1.0, hFacMinDr=0.0, gBaro=9.81)
+    g.ini_cg2d(1200.0, 1200.0, 1e-7)
+    tRef = np.array(BAROCLINIC_TREF)
+    params = dict(deltaTMom=1200.0, deltaTFreeSurf=1200.0, deltaTClock=1200.0, deltaTtracer=1200.0, abEps=0.01,
+                  rhoConst=999.8, rhoNil=999.8, gravity=9.81, gBaro=9.81, viscAhD=5000.0, viscAhZ=5000.0,
+                  viscA4D=0.0, viscA4Z=0.0, viscAr=1e-2, sideDragFactor=2.0, selectCoriScheme=0,
+                  momForcingOutAB=0, momDissip_In_AB=1, cg2dMaxIters=1000, cg2dUseMinResSol=0, nIter0=0,
+                  no_slip_sides=1, no_slip_bottom=0, exactConserv=1, tempStepping=1, tempAdvection=1,
+                  tempForcing=1, tempAdvScheme=tempAdvScheme, tempVertAdvScheme=tempAdvScheme, diffKhT=1000.0,
+                  diffKrT=1e-5, ivdc_kappa=1.0, implicitDiffusion=1, tAlpha=2e-4, sBeta=0.0,
+                  usingSphericalPolarGrid=1, selectMetricTerms=1, rSphere=g.rSphere, integr_GeoPot=2)
+    wind = read_bin(os.path.join(d, "windx_cosy.bin"), (Ny, Nx))
+    sst = read_bin(os.path.join(d, "SST_relax.bin"), (Ny, Nx))
+    fu, SST = g.z2(), g.z2()
+    inner = g.sl(1, sNx, 1, sNy)
+    for t in range(g.nTiles):
+        bi, bj = t % nSx, t // nSx
+        fu[t][inner] = wind[bj * sNy:(bj + 1) * sNy, bi * sNx:(bi + 1) * sNx]
+        SST[t][inner] = sst[bj * sNy:(bj + 1) * sNy, bi * sNx:(bi + 1) * sNx]
+    theta = np.broadcast_to(tRef[None, :, None, None], (g.nTiles, Nr, g.ny, g.nx)).copy()
+    lam = np.full((g.nTiles, g.ny, g.nx), 1.0 / 2592000.0)      # ini_forcing.F:46-51
+    state = {"fu": g.exch(fu), "fv": g.z2(), "theta": theta, "salt": np.full_like(theta, 30.0),
+             "SST": g.exch(SST), "lambdaThetaClimRelax": lam, "tRef": tRef, "sRef": np.full(Nr, 30.0)}
+    return g, params, state
+
+
 def make_model(cfg, device=0, **kw):
     g, params, state = cfg(**kw)
     m = Model(g, params, device=device)

@@ -63,43 +63,51 @@ class Grid:
         self.f.update(drF=drF, drC=drC, rF=rF, rC=rC, recip_drF=1.0 / drF, recip_drC=1.0 / drC)
 
     # ---- horizontal grid ------------------------------------------------------
-    def ini_cartesian_grid(self, delX, delY, xgOrigin, ygOrigin):
+    def _local_grid(self, t, delX, delY, xgOrigin, ygOrigin):
+        """INI_LOCAL_GRID (model/src/ini_local_grid.F): corner coordinates
+        xGloc/yGloc (sNx+2OLx+1, sNy+2OLy+1) as sequential running sums, and
+        delXloc(i) / delYloc(j) for i = -OLx..sNx+OLx (index i+OLx)."""
         sNx, sNy, OLx, OLy = self.sNx, self.sNy, self.OLx, self.OLy
         Nx, Ny = sNx * self.nSx, sNy * self.nSy
+        bi, bj = t % self.nSx, t // self.nSx
+        iG0, jG0 = bi * sNx, bj * sNy
+        xG0 = xgOrigin
+        for i in range(1, iG0 + 1):
+            xG0 += delX[i - 1]
+        for i in range(1, OLx + 1):
+            xG0 -= delX[(iG0 - i + OLx * Nx) % Nx]
+        yG0 = ygOrigin
+        for j in range(1, jG0 + 1):
+            yG0 += delY[j - 1]
+        for j in range(1, OLy + 1):
+            yG0 -= delY[(jG0 - j + OLy * Ny) % Ny]
+        dXl = np.array([delX[(iG0 + i - 1 + OLx * Nx) % Nx] for i in range(-OLx, sNx + OLx + 1)])
+        dYl = np.array([delY[(jG0 + j - 1 + OLy * Ny) % Ny] for j in range(-OLy, sNy + OLy + 1)])
+        nxl, nyl = sNx + 2 * OLx + 1, sNy + 2 * OLy + 1
+        xGl = np.zeros(nxl)
+        xGl[0] = xG0
+        for ii in range(1, nxl):
+            xGl[ii] = xGl[ii - 1] + dXl[ii]
+        yGl = np.zeros(nyl)
+        yGl[0] = yG0
+        for jj in range(1, nyl):
+            yGl[jj] = yGl[jj - 1] + dYl[jj]
+        XG = np.broadcast_to(xGl[None, :], (nyl, nxl))
+        YG = np.broadcast_to(yGl[:, None], (nyl, nxl))
+        return XG, YG, dXl, dYl
+
+    _GRID_NAMES = ("xC", "yC", "xG", "yG", "dxF", "dyF", "dxG", "dyG", "dxC", "dyC", "dxV", "dyU",
+                   "rA", "rAw", "rAs", "rAz")
+
+    def ini_cartesian_grid(self, delX, delY, xgOrigin, ygOrigin):
+        """INI_CARTESIAN_GRID (model/src/ini_cartesian_grid.F)."""
         delX = np.asarray(delX, dtype=np.float64)
         delY = np.asarray(delY, dtype=np.float64)
-        names = ("xC", "yC", "xG", "yG", "dxF", "dyF", "dxG", "dyG", "dxC", "dyC", "dxV", "dyU",
-                 "rA", "rAw", "rAs", "rAz")
-        for n in names:
+        for n in self._GRID_NAMES:
             self.f[n] = self.z2()
+        self.usingSphericalPolarGrid = False
         for t in range(self.nTiles):
-            bi, bj = t % self.nSx, t // self.nSx
-            iG0, jG0 = bi * sNx, bj * sNy
-            xG0 = xgOrigin
-            for i in range(1, iG0 + 1):
-                xG0 += delX[i - 1]
-            for i in range(1, OLx + 1):
-                xG0 -= delX[(iG0 - i + OLx * Nx) % Nx]
-            yG0 = ygOrigin
-            for j in range(1, jG0 + 1):
-                yG0 += delY[j - 1]
-            for j in range(1, OLy + 1):
-                yG0 -= delY[(jG0 - j + OLy * Ny) % Ny]
-            # delXloc(i), i = -OLx..sNx+OLx -> index i+OLx
-            dXl = np.array([delX[(iG0 + i - 1 + OLx * Nx) % Nx] for i in range(-OLx, sNx + OLx + 1)])
-            dYl = np.array([delY[(jG0 + j - 1 + OLy * Ny) % Ny] for j in range(-OLy, sNy + OLy + 1)])
-            # xGloc(i,j) for i = 1-OLx..sNx+OLx+1 (sequential running sum, as the loop does)
-            nxl, nyl = sNx + 2 * OLx + 1, sNy + 2 * OLy + 1
-            xGl = np.zeros(nxl)
-            xGl[0] = xG0
-            for ii in range(1, nxl):
-                xGl[ii] = xGl[ii - 1] + dXl[ii]          # dXl index (i-1)+OLx+1 = ii for i=ii-OLx
-            yGl = np.zeros(nyl)
-            yGl[0] = yG0
-            for jj in range(1, nyl):
-                yGl[jj] = yGl[jj - 1] + dYl[jj]
-            XG = np.broadcast_to(xGl[None, :], (nyl, nxl))
-            YG = np.broadcast_to(yGl[:, None], (nyl, nxl))
+            XG, YG, dXl, dYl = self._local_grid(t, delX, delY, xgOrigin, ygOrigin)
             f = self.f
             f["xG"][t] = XG[:-1, :-1]
             f["yG"][t] = YG[:-1, :-1]
@@ -121,6 +129,64 @@ class Grid:
             f["rAz"][t] = f["dxV"][t] * f["dyU"][t]
         self._reciprocals()
 
+    def ini_spherical_polar_grid(self, delX, delY, xgOrigin, ygOrigin, rSphere=6370.0e3):
+        """INI_SPHERICAL_POLAR_GRID (model/src/ini_spherical_polar_grid.F:60-250),
+        rotateGrid=F, cosPower=0.  Transcendentals go through the C library
+        (math.sin/cos/tan) element by element, as the compiled reference does,
+        not through numpy's vectorised kernels."""
+        from math import cos, sin, tan
+        deg2rad = 2.0 * np.pi / 360.0          # PARAMS.h:18, PI = 3.14159265358979323844D0
+        delX = np.asarray(delX, dtype=np.float64)
+        delY = np.asarray(delY, dtype=np.float64)
+        for n in self._GRID_NAMES + ("tanPhiAtU", "tanPhiAtV"):
+            self.f[n] = self.z2()
+        self.usingSphericalPolarGrid = True
+        self.rSphere = rSphere
+        self.recip_rSphere = 1.0 / rSphere
+        nx, ny = self.nx, self.ny
+        for t in range(self.nTiles):
+            XG, YG, dXl, dYl = self._local_grid(t, delX, delY, xgOrigin, ygOrigin)
+            f = self.f
+            f["xG"][t] = XG[:-1, :-1]
+            f["yG"][t] = YG[:-1, :-1]
+            f["xC"][t] = 0.25 * (XG[:-1, :-1] + XG[:-1, 1:] + XG[1:, :-1] + XG[1:, 1:])
+            f["yC"][t] = 0.25 * (YG[:-1, :-1] + YG[:-1, 1:] + YG[1:, :-1] + YG[1:, 1:])
+            dxl = dXl          # delXloc(i), i = -OLx.. ; Fortran i (1-OLx based) -> index I+1
+            dyl = dYl
+            dxF, dyF, dxG, dyG = f["dxF"][t], f["dyF"][t], f["dxG"][t], f["dyG"][t]
+            rA, rAs, rAz = f["rA"][t], f["rAs"][t], f["rAz"][t]
+            for J in range(ny):
+                for I in range(nx):
+                    lat = f["yC"][t, J, I]
+                    dlon, dlat = dxl[I + 1], dyl[J + 1]
+                    dxF[J, I] = rSphere * cos(lat * deg2rad) * dlon * deg2rad
+                    dyF[J, I] = rSphere * dlat * deg2rad
+                    lat = 0.5 * (YG[J, I] + YG[J, I + 1])
+                    v = rSphere * cos(deg2rad * lat) * dlon * deg2rad
+                    dxG[J, I] = 0.0 if v < 1.0 else v
+                    dyG[J, I] = rSphere * dlat * deg2rad
+                    # rA (ini_spherical_polar_grid.F:158-170)
+                    rA[J, I] = rSphere * rSphere * dlon * deg2rad * abs(sin((lat + dlat) * deg2rad) - sin(lat * deg2rad))
+                    # rAs (:183-197)
+                    latc = f["yC"][t, J, I]
+                    dlat2 = 0.5 * (dyl[J + 1] + dyl[J])
+                    v = rSphere * rSphere * dlon * deg2rad * abs(sin(latc * deg2rad) - sin((latc - dlat2) * deg2rad))
+                    rAs[J, I] = 0.0 if (abs(latc) > 90.0 or abs(latc - dlat2) > 90.0) else v
+                    # rAz (:200-213)
+                    latz = 0.5 * (YG[J, I] + YG[J + 1, I])
+                    dlonz = 0.5 * (dxl[I + 1] + dxl[I])
+                    v = rSphere * rSphere * dlonz * deg2rad * abs(sin(latz * deg2rad) - sin((latz - dlat2) * deg2rad))
+                    rAz[J, I] = 0.0 if (abs(latz) > 90.0 or abs(latz - dlat2) > 90.0) else v
+                    # tanPhiAtU/V (:216-223)
+                    f["tanPhiAtU"][t, J, I] = tan(latz * deg2rad)
+                    f["tanPhiAtV"][t, J, I] = tan(lat * deg2rad)
+            f["dxC"][t, :, 1:] = 0.5 * (dxF[:, 1:] + dxF[:, :-1])
+            f["dyC"][t, 1:, :] = 0.5 * (dyF[1:, :] + dyF[:-1, :])
+            f["dxV"][t, 1:, 1:] = 0.5 * (dxG[1:, 1:] + dxG[1:, :-1])
+            f["dyU"][t, 1:, 1:] = 0.5 * (dyG[1:, 1:] + dyG[:-1, 1:])
+            f["rAw"][t, :, 1:] = 0.5 * (rA[:, 1:] + rA[:, :-1])
+        self._reciprocals()
+
     def _reciprocals(self):
         for n in ("dxG", "dyG", "dxC", "dyC", "dxF", "dyF", "dxV", "dyU", "rA", "rAs", "rAw", "rAz"):
             a = self.f[n]
@@ -129,7 +195,20 @@ class Grid:
             r[nz] = 1.0 / a[nz]
             self.f["recip_" + n] = r
 
-    def ini_cori(self, f0, beta, selectCoriMap=1):
+    def ini_cori(self, f0=1e-4, beta=1e-11, selectCoriMap=1, omega=None):
+        """INI_CORI (model/src/ini_cori.F:29-83)."""
+        if selectCoriMap == 2:
+            from math import cos, sin
+            deg2rad = 2.0 * np.pi / 360.0
+            if omega is None:
+                omega = 2.0 * np.pi / 86164.0      # ini_parms.F:481-483, rotationPeriod default
+            self.omega = omega
+            sinv = np.vectorize(lambda x: sin(x * deg2rad), otypes=[np.float64])
+            cosv = np.vectorize(lambda x: cos(x * deg2rad), otypes=[np.float64])
+            self.f["fCori"] = 2.0 * omega * sinv(self.f["yC"])
+            self.f["fCoriG"] = 2.0 * omega * sinv(self.f["yG"])
+            self.f["fCoriCos"] = 2.0 * omega * cosv(self.f["yC"])
+            return
         if selectCoriMap == 1:
             self.f["fCori"] = f0 + beta * self.f["yC"]
             self.f["fCoriG"] = f0 + beta * self.f["yG"]

@@ -19,7 +19,10 @@ static void check_supported(const OModel *m) {
     fprintf(stderr, "oracle_dynamics: biharmonic viscosity not yet restated\n"); abort();
   }
   if (m->implicitViscosity) { fprintf(stderr, "oracle_dynamics: implicitViscosity not yet restated\n"); abort(); }
-  if (!m->usingCartesianGrid) { fprintf(stderr, "oracle_dynamics: metric terms not yet restated\n"); abort(); }
+  if (!m->usingCartesianGrid && !m->usingSphericalPolarGrid) {
+    fprintf(stderr, "oracle_dynamics: only cartesian and spherical-polar grids restated\n"); abort();
+  }
+  if (m->integr_GeoPot != 2) { fprintf(stderr, "oracle_dynamics: integr_GeoPot=%d not restated\n", m->integr_GeoPot); abort(); }
 }
 
 void oracle_dynamics(OModel *m) {
@@ -36,6 +39,11 @@ void oracle_dynamics(OModel *m) {
   double *guDiss = calloc(n2, 8), *gvDiss = calloc(n2, 8), *guExt = calloc(n2, 8), *gvExt = calloc(n2, 8);
   double *gUtmp = calloc(n2, 8), *gVtmp = calloc(n2, 8), *ab = calloc(n2, 8);
   double *kappaRU = calloc(n2 * (Nr + 1), 8), *kappaRV = calloc(n2 * (Nr + 1), 8);
+  double *phiHydF = calloc(n2, 8), *phiHydC = calloc(n2, 8), *dPhiHydX = calloc(n2, 8), *dPhiHydY = calloc(n2, 8);
+  double *mT = calloc(n2, 8);
+  const int metricSphere = m->usingSphericalPolarGrid && m->selectMetricTerms >= 1;
+  const double recip_rSphere = m->usingSphericalPolarGrid ? 1.0 / m->rSphere : 0.0; /* ini_parms.F:1334 */
+  const double recip_rhoConst = 1.0 / m->rhoConst;
 
   /* MOM_FLUXFORM factors (mom_fluxform.F:236-277) */
   const double uDudxFac = m->afFacMom, vDudyFac = m->afFacMom, rVelDudrFac = m->afFacMom;
@@ -58,6 +66,9 @@ void oracle_dynamics(OModel *m) {
     const double *recip_dxV = m->recip_dxV + t * n2, *recip_dyU = m->recip_dyU + t * n2;
     const double *recip_rAw = m->recip_rAw + t * n2, *recip_rAs = m->recip_rAs + t * n2;
     const double *fCori = m->fCori + t * n2;
+    const double *tanPhiAtU = m->tanPhiAtU + t * n2, *tanPhiAtV = m->tanPhiAtV + t * n2;
+    const double *recip_dxC = m->recip_dxC + t * n2, *recip_dyC = m->recip_dyC + t * n2;
+    const double *rhoInSitu = m->rhoInSitu + t * m->n3;
     const double *sfU = m->surfaceForcingU + t * n2, *sfV = m->surfaceForcingV + t * n2;
 #define W3(a, i, j, k) (a)[(long)((i) + OLx - 1) + (long)((j) + OLy - 1) * nx + (long)((k) - 1) * n2]
 
@@ -66,12 +77,34 @@ void oracle_dynamics(OModel *m) {
     for (long p = 0; p < n2; p++) { fVerU[0][p] = fVerU[1][p] = fVerV[0][p] = fVerV[1][p] = 0.0; }
     /* CALC_VISCOSITY (model/src/calc_viscosity.F): kappaRU = viscArNr(k) */
     for (long p = 0; p < n2 * (Nr + 1); p++) { kappaRU[p] = m->viscAr; kappaRV[p] = m->viscAr; }
+    /* CALC_PHI_HYD (calc_phi_hyd.F:167-172): phiHydF = 0 at k = 1 */
+    for (long p = 0; p < n2; p++) phiHydF[p] = 0.0;
 
     for (int k = 1; k <= Nr; k++) {
       const int kUp = 1 + (k + 1) % 2, kDown = 1 + k % 2; /* dynamics.F:425-426 */
       double *fVerUkm = fVerU[kUp - 1], *fVerVkm = fVerV[kUp - 1];
       double *fVerUkp = fVerU[kDown - 1], *fVerVkp = fVerV[kDown - 1];
-      /* dPhiHydX/Y: CALC_PHI_HYD -- zero for the supported (uniform-density) configs */
+      /* CALC_PHI_HYD (calc_phi_hyd.F:175-327), OCEANIC, integr_GeoPot = 2, uniformFreeSurfLev,
+       * alphaRho = rhoInSitu from DO_OCEANIC_PHYS; gravFac* = 1; iMin..iMax = 0..sNx+1 */
+      {
+        double dRlocM = 0.5 * m->drC[k - 1];
+        if (k == 1) dRlocM = m->rF[0] - m->rC[0];
+        double dRlocP = (k == Nr) ? (m->rC[k - 1] - m->rF[k]) : 0.5 * m->drC[k];
+        for (int j = jMin; j <= jMax; j++)
+          for (int i = iMin; i <= iMax; i++) {
+            double a = W3(rhoInSitu, i, j, k);
+            L(phiHydC, i, j) = L(phiHydF, i, j) + dRlocM * m->gravity * a * recip_rhoConst;
+            L(phiHydF, i, j) = L(phiHydC, i, j) + dRlocP * m->gravity * a * recip_rhoConst;
+          }
+        /* CALC_GRAD_PHI_HYD (calc_grad_phi_hyd.F:152-171), phi0surf = 0 */
+        for (long p = 0; p < n2; p++) dPhiHydX[p] = dPhiHydY[p] = 0.0;
+        for (int j = jMin; j <= jMax; j++)
+          for (int i = iMin + 1; i <= iMax; i++)
+            L(dPhiHydX, i, j) = L(recip_dxC, i, j) * ((L(phiHydC, i, j) + 0.0) - (L(phiHydC, i - 1, j) + 0.0));
+        for (int j = jMin + 1; j <= jMax; j++)
+          for (int i = iMin; i <= iMax; i++)
+            L(dPhiHydY, i, j) = L(recip_dyC, i, j) * ((L(phiHydC, i, j) + 0.0) - (L(phiHydC, i, j - 1) + 0.0));
+      }
       for (long p = 0; p < n2; p++) {
         guDiss[p] = gvDiss[p] = 0.0; fZon[p] = fMer[p] = fVrUp[p] = fVrDw[p] = 0.0;
         uCf[p] = vCf[p] = vF[p] = 0.0; rTransU[p] = rTransV[p] = 0.0;
@@ -225,6 +258,16 @@ void oracle_dynamics(OModel *m) {
               L(guDiss, i, j) = L(guDiss, i, j) - L(cDrag, i, j) * W3(uVel, i, j, k) * W3(rhFacW, i, j, k) * m->recip_drF[k - 1];
         }
       }
+      if (metricSphere) {
+        /* MOM_U_METRIC_SPHERE (pkg/mom_fluxform/mom_u_metric_sphere.F), mom_fluxform.F:714-721 */
+        for (int j = 1 - OLy; j <= sNy + OLy - 1; j++)
+          for (int i = 2 - OLx; i <= sNx + OLx; i++)
+            L(mT, i, j) = W3(uVel, i, j, k) * recip_rSphere * 0.25 *
+                          (W3(vVel, i, j, k) + W3(vVel, i - 1, j, k) + W3(vVel, i, j + 1, k) + W3(vVel, i - 1, j + 1, k)) *
+                          L(tanPhiAtU, i, j);
+        for (int j = jMin; j <= jMax; j++)
+          for (int i = iMin; i <= iMax; i++) W3(gU, i, j, k) = W3(gU, i, j, k) + m->mtFacMom * L(mT, i, j);
+      }
       /* ================= V component ================= */
       if (m->momAdvection) {
         /* MOM_V_ADV_UV (mom_v_adv_uv.F:45-60) */
@@ -325,6 +368,16 @@ void oracle_dynamics(OModel *m) {
               L(gvDiss, i, j) = L(gvDiss, i, j) - L(cDrag, i, j) * W3(vVel, i, j, k) * W3(rhFacS, i, j, k) * m->recip_drF[k - 1];
         }
       }
+      if (metricSphere) {
+        /* MOM_V_METRIC_SPHERE (pkg/mom_fluxform/mom_v_metric_sphere.F), mom_fluxform.F:973-980 */
+        for (int j = 2 - OLy; j <= sNy + OLy; j++)
+          for (int i = 1 - OLx; i <= sNx + OLx - 1; i++) {
+            double ub = W3(uVel, i, j, k) + W3(uVel, i + 1, j, k) + W3(uVel, i, j - 1, k) + W3(uVel, i + 1, j - 1, k);
+            L(mT, i, j) = -(recip_rSphere * 0.25 * ub * 0.25 * ub * L(tanPhiAtV, i, j));
+          }
+        for (int j = jMin; j <= jMax; j++)
+          for (int i = iMin; i <= iMax; i++) W3(gV, i, j, k) = W3(gV, i, j, k) + m->mtFacMom * L(mT, i, j);
+      }
       /* Coriolis (mom_fluxform.F:995-1022; mom_u_coriolis.F, mom_v_coriolis.F) */
       if (m->useCoriolis) {
         const int sc = m->selectCoriScheme;
@@ -382,7 +435,12 @@ void oracle_dynamics(OModel *m) {
               L(gvExt, i, j) = L(gvExt, i, j) + m->foFacMom * L(sfV, i, j) * m->recip_drF[k - 1] * W3(rhFacS, i, j, k);
         }
       }
-      /* timestep.F:116-126: - phFac*dPhiHydX (zero here) */
+      /* timestep.F:116-126: synchronous time step, gU -= phFac*dPhiHydX */
+      for (int j = jMin; j <= jMax; j++)
+        for (int i = iMin; i <= iMax; i++) {
+          W3(gU, i, j, k) = W3(gU, i, j, k) - m->pfFacMom * L(dPhiHydX, i, j);
+          W3(gV, i, j, k) = W3(gV, i, j, k) - m->pfFacMom * L(dPhiHydY, i, j);
+        }
       if (m->momViscosity && m->momDissip_In_AB)
         for (int j = jMin; j <= jMax; j++)
           for (int i = iMin; i <= iMax; i++) {
@@ -437,4 +495,5 @@ void oracle_dynamics(OModel *m) {
   free(fZon); free(fMer); free(fVrUp); free(fVrDw); free(uCf); free(vCf); free(vF); free(cDrag);
   free(guDiss); free(gvDiss); free(guExt); free(gvExt); free(gUtmp); free(gVtmp); free(ab);
   free(kappaRU); free(kappaRV);
+  free(phiHydF); free(phiHydC); free(dPhiHydX); free(dPhiHydY); free(mT);
 }

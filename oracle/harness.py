@@ -43,7 +43,8 @@ def lib():
         L.oracle_ini_depths.argtypes = [vp, ctypes.POINTER(c_dbl)]
         L.oracle_ini_depths.restype = c_int
         for fn in ("oracle_dynamics", "oracle_solve_for_pressure", "oracle_momentum_correction_step",
-                   "oracle_integr_continuity", "oracle_forward_step"):
+                   "oracle_integr_continuity", "oracle_forward_step", "oracle_oceanic_phys",
+                   "oracle_thermodynamics"):
             getattr(L, fn).argtypes = [vp]
         P = ctypes.POINTER(c_dbl)
         L.oracle_cg2d.argtypes = [vp, P, P, P, P, P, ctypes.POINTER(c_int), ctypes.POINTER(c_int)]
@@ -144,7 +145,8 @@ class Oracle:
                 ("eta", self.arr("etaN"), mC, 0, mC, self.arr("rA"), drF, 1),
                 ("uvel", self.arr("uVel"), self.arr("hFacW"), 1, mW, self.arr("rAw"), drF, Nr),
                 ("vvel", self.arr("vVel"), self.arr("hFacS"), 1, mS, self.arr("rAs"), drF, Nr),
-                ("wvel", self.arr("wVel"), self.arr("maskC"), 1, mC, self.arr("rA"), drC, Nr)):
+                ("wvel", self.arr("wVel"), self.arr("maskC"), 1, mC, self.arr("rA"), drC, Nr),
+                ("theta", self.arr("theta"), self.arr("hFacC"), 1, mC, self.arr("rA"), drF, Nr)):
             st = self.stats(fld, nr, hf, h3, mask, area, dr)
             for key, v in zip(("min", "max", "mean", "sd", "del2"), st[:5]):
                 res["dynstat_%s_%s" % (name, key)] = float(v)
@@ -156,6 +158,38 @@ class Oracle:
 
 
 GOLDEN = os.path.join(os.path.dirname(HERE), "tests", "golden")
+
+# host Grid arrays the oracle takes as they are (grid set-up is host-side in the
+# product too; the spherical grid is pinned separately by tests/test_grid_sphere.py)
+_GRID2 = ("xC", "yC", "xG", "yG", "dxF", "dyF", "dxG", "dyG", "dxC", "dyC", "dxV", "dyU", "rA", "rAw", "rAs",
+          "rAz", "recip_dxF", "recip_dyF", "recip_dxG", "recip_dyG", "recip_dxC", "recip_dyC", "recip_dxV",
+          "recip_dyU", "recip_rA", "recip_rAw", "recip_rAs", "recip_rAz", "fCori", "fCoriG", "Bo_surf",
+          "recip_Bo", "R_low", "Ro_surf", "maskInC", "maskInW", "maskInS", "aW2d", "aS2d", "aC2d", "pW", "pS",
+          "pC", "fCoriCos", "tanPhiAtU", "tanPhiAtV")
+_GRID3 = ("hFacC", "hFacW", "hFacS", "recip_hFacC", "recip_hFacW", "recip_hFacS", "maskC", "maskW", "maskS")
+
+
+def oracle_from_config(cfg, **kw):
+    """Oracle instance for a mitgcm_amd.configs experiment: parameters and state as
+    the config resolves them, grid/masks/CG2D operator copied from the host Grid."""
+    g, params, state = cfg(**kw)
+    o = Oracle(g.sNx, g.sNy, g.OLx, g.OLy, g.Nr, g.nSx, g.nSy)
+    if getattr(g, "usingSphericalPolarGrid", False):
+        o.set(usingCartesianGrid=0, usingSphericalPolarGrid=1)
+    for k, v in params.items():
+        o.set(**{k: v})
+    for n in ("drF", "drC", "rF", "rC", "recip_drF", "recip_drC"):
+        o.arr(n)[:len(g.f[n])] = g.f[n]
+    for n in _GRID2 + _GRID3:
+        if n in g.f:
+            o.arr(n)[:] = g.f[n]
+    for n in ("kSurfC", "kSurfW", "kSurfS", "kLowC"):
+        o.iarr(n)[:] = g.i[n]
+    o.set(cg2dNorm=g.cg2dNorm, cg2dTolerance_sq=g.cg2dTolerance_sq, cg2dNormaliseRHS=int(g.cg2dNormaliseRHS),
+          globalArea=g.globalArea)
+    for k, v in state.items():
+        o.arr(k)[:] = v
+    return o, g
 
 
 def read_bin(path, shape, dtype=">f4"):

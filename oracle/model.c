@@ -29,10 +29,13 @@ OModel *oracle_new(int sNx, int sNy, int OLx, int OLy, int Nr, int nSx, int nSy)
   m->momAdvection = m->momViscosity = m->momForcing = m->useCoriolis = 1;
   m->no_slip_sides = 1; m->no_slip_bottom = 1; m->momDissip_In_AB = 1; m->momForcingOutAB = 0;
   m->useHarmonicVisc = 1; m->selectCoriMap = 1; m->usingCartesianGrid = 1;
+  m->integr_GeoPot = 2; m->rSphere = 6370.0e3; m->gravitySign = -1.0; m->tAlpha = 2.0e-4;
+  m->tempAdvScheme = 2; m->tempVertAdvScheme = 2;
 
   m->drF = zalloc(Nr + 1); m->drC = zalloc(Nr + 1); m->rF = zalloc(Nr + 1); m->rC = zalloc(Nr + 1);
   m->recip_drF = zalloc(Nr + 1); m->recip_drC = zalloc(Nr + 1);
   m->delX = zalloc(Nx); m->delY = zalloc(Ny);
+  m->tRef = zalloc(Nr); m->sRef = zalloc(Nr);
 #define A2(f) m->f = zalloc(N2)
   A2(xC); A2(yC); A2(xG); A2(yG); A2(dxF); A2(dyF); A2(dxG); A2(dyG); A2(dxC); A2(dyC); A2(dxV); A2(dyU);
   A2(rA); A2(rAw); A2(rAs); A2(rAz);
@@ -42,12 +45,15 @@ OModel *oracle_new(int sNx, int sNy, int OLx, int OLy, int Nr, int nSx, int nSy)
   A2(maskInC); A2(maskInW); A2(maskInS);
   A2(aW2d); A2(aS2d); A2(aC2d); A2(pW); A2(pS); A2(pC);
   A2(etaN); A2(fu); A2(fv); A2(surfaceForcingU); A2(surfaceForcingV);
+  A2(fCoriCos); A2(tanPhiAtU); A2(tanPhiAtV); A2(surfaceForcingT); A2(SST); A2(lambdaThetaClimRelax);
+  A2(etaH); A2(dEtaHdt);
 #undef A2
   m->kSurfC = izalloc(N2); m->kSurfW = izalloc(N2); m->kSurfS = izalloc(N2); m->kLowC = izalloc(N2);
 #define A3(f) m->f = zalloc(N3)
   A3(hFacC); A3(hFacW); A3(hFacS); A3(recip_hFacC); A3(recip_hFacW); A3(recip_hFacS);
   A3(maskC); A3(maskW); A3(maskS);
   A3(uVel); A3(vVel); A3(wVel); A3(theta); A3(salt); A3(gU); A3(gV); A3(guNm1); A3(gvNm1);
+  A3(gtNm1); A3(rhoInSitu); A3(IVDConvCount);
 #undef A3
   return m;
 }
@@ -64,7 +70,10 @@ void oracle_free(OModel *m) {
                    &m->pS, &m->pC, &m->etaN, &m->fu, &m->fv, &m->surfaceForcingU,
                    &m->surfaceForcingV, &m->hFacC, &m->hFacW, &m->hFacS, &m->recip_hFacC,
                    &m->recip_hFacW, &m->recip_hFacS, &m->maskC, &m->maskW, &m->maskS, &m->uVel,
-                   &m->vVel, &m->wVel, &m->theta, &m->salt, &m->gU, &m->gV, &m->guNm1, &m->gvNm1};
+                   &m->vVel, &m->wVel, &m->theta, &m->salt, &m->gU, &m->gV, &m->guNm1, &m->gvNm1,
+                   &m->tRef, &m->sRef, &m->fCoriCos, &m->tanPhiAtU, &m->tanPhiAtV, &m->surfaceForcingT,
+                   &m->SST, &m->lambdaThetaClimRelax, &m->etaH, &m->dEtaHdt, &m->gtNm1, &m->rhoInSitu,
+                   &m->IVDConvCount};
   for (size_t i = 0; i < sizeof(dp) / sizeof(dp[0]); i++) free(*dp[i]);
   free(m->kSurfC); free(m->kSurfW); free(m->kSurfS); free(m->kLowC);
   free(m);
@@ -87,6 +96,9 @@ static const PDesc PTAB[] = {
   PI_(useHarmonicVisc), PI_(useBiharmonicVisc), PI_(implicitViscosity), PI_(selectCoriMap),
   PI_(cg2dMaxIters), PI_(cg2dUseMinResSol), PI_(exactConserv), PI_(nIter0), PI_(usingCartesianGrid),
   PI_(cg2dNormaliseRHS), PI_(myIter), PI_(numIters), PI_(nIterMin),
+  PI_(usingSphericalPolarGrid), PI_(selectMetricTerms), PI_(integr_GeoPot), PI_(tempStepping),
+  PI_(tempAdvection), PI_(tempForcing), PI_(tempAdvScheme), PI_(tempVertAdvScheme), PI_(implicitDiffusion),
+  PD(rSphere), PD(deltaTtracer), PD(diffKhT), PD(diffKrT), PD(ivdc_kappa), PD(tAlpha), PD(sBeta), PD(gravitySign),
 };
 #undef PD
 #undef PI_
@@ -117,6 +129,13 @@ double *oracle_array(OModel *m, const char *name, long *count) {
   struct { const char *n; double *p; long c; } t[] = {
     {"drF", m->drF, m->Nr + 1}, {"drC", m->drC, m->Nr + 1}, {"rF", m->rF, m->Nr + 1},
     {"rC", m->rC, m->Nr + 1}, {"recip_drF", m->recip_drF, m->Nr + 1},
+    {"recip_drC", m->recip_drC, m->Nr + 1}, {"tRef", m->tRef, m->Nr}, {"sRef", m->sRef, m->Nr},
+    {"recip_rAz", m->recip_rAz, N2}, {"fCoriCos", m->fCoriCos, N2}, {"tanPhiAtU", m->tanPhiAtU, N2},
+    {"tanPhiAtV", m->tanPhiAtV, N2}, {"surfaceForcingT", m->surfaceForcingT, N2}, {"SST", m->SST, N2},
+    {"lambdaThetaClimRelax", m->lambdaThetaClimRelax, N2}, {"etaH", m->etaH, N2},
+    {"dEtaHdt", m->dEtaHdt, N2}, {"surfaceForcingU", m->surfaceForcingU, N2},
+    {"surfaceForcingV", m->surfaceForcingV, N2}, {"gtNm1", m->gtNm1, N3}, {"rhoInSitu", m->rhoInSitu, N3},
+    {"IVDConvCount", m->IVDConvCount, N3},
     {"delX", m->delX, (long)m->sNx * m->nSx}, {"delY", m->delY, (long)m->sNy * m->nSy},
     {"xC", m->xC, N2}, {"yC", m->yC, N2}, {"xG", m->xG, N2}, {"yG", m->yG, N2},
     {"dxF", m->dxF, N2}, {"dyF", m->dyF, N2}, {"dxG", m->dxG, N2}, {"dyG", m->dyG, N2},

@@ -41,6 +41,10 @@ typedef struct OModel {
   int useHarmonicVisc, useBiharmonicVisc, implicitViscosity, selectCoriMap;
   int cg2dMaxIters, cg2dUseMinResSol, exactConserv, nIter0;
   int usingCartesianGrid;
+  /* 3-D / tracer path (THERMODYNAMICS, CALC_PHI_HYD, spherical grid, exactConserv) */
+  int usingSphericalPolarGrid, selectMetricTerms, integr_GeoPot;
+  int tempStepping, tempAdvection, tempForcing, tempAdvScheme, tempVertAdvScheme, implicitDiffusion;
+  double rSphere, deltaTtracer, diffKhT, diffKrT, ivdc_kappa, tAlpha, sBeta, gravitySign;
 
   /* --- vertical grid (GRID.h), 1-based in the reference; here [0..Nr] --- */
   double *drF, *drC, *rF, *rC, *recip_drF, *recip_drC;
@@ -51,7 +55,8 @@ typedef struct OModel {
   double *rA, *rAw, *rAs, *rAz;
   double *recip_dxF, *recip_dyF, *recip_dxG, *recip_dyG, *recip_dxC, *recip_dyC;
   double *recip_dxV, *recip_dyU, *recip_rA, *recip_rAw, *recip_rAs, *recip_rAz;
-  double *fCori, *fCoriG, *Bo_surf, *recip_Bo;
+  double *fCori, *fCoriG, *fCoriCos, *Bo_surf, *recip_Bo, *tanPhiAtU, *tanPhiAtV;
+  double *tRef, *sRef;   /* [Nr] */
   double *R_low, *Ro_surf, *maskInC, *maskInW, *maskInS;
   int *kSurfC, *kSurfW, *kSurfS, *kLowC;
 
@@ -68,6 +73,8 @@ typedef struct OModel {
   double *uVel, *vVel, *wVel, *theta, *salt, *etaN;
   double *gU, *gV, *guNm1, *gvNm1;
   double *fu, *fv, *surfaceForcingU, *surfaceForcingV;
+  double *surfaceForcingT, *SST, *lambdaThetaClimRelax, *etaH, *dEtaHdt;   /* 2-D */
+  double *gtNm1, *rhoInSitu, *IVDConvCount;                                /* 3-D */
   int myIter;
   double myTime;
 
@@ -112,7 +119,9 @@ void oracle_cg2d(OModel *m, double *cg2d_b, double *cg2d_x,
                  int *numIters, int *nIterMin);      /* CG2D (cg2d.F:13) */
 void oracle_momentum_correction_step(OModel *m);     /* momentum_correction_step.F:7 */
 void oracle_integr_continuity(OModel *m);            /* integr_continuity.F:13 */
-void oracle_forward_step(OModel *m);                 /* forward_step.F:64 (supported subset) */
+void oracle_forward_step(OModel *m);
+void oracle_oceanic_phys(OModel *m);                 /* DO_OCEANIC_PHYS subset (do_oceanic_phys.F:555-882) */
+void oracle_thermodynamics(OModel *m);               /* THERMODYNAMICS -> TEMP_INTEGRATE (temp_integrate.F) */                 /* forward_step.F:64 (supported subset) */
 
 /* monitor (pkg/monitor/mon_calc_stats_rl.F): out[6] = min,max,mean,sd,del2,vol */
 void oracle_mon_stats(OModel *m, const double *arr, int myNr, const double *arrhFac,

@@ -243,7 +243,9 @@ void oracle_solve_for_pressure(OModel *m) {
     for (int j = 1; j <= sNy; j++)
       for (int i = 1; i <= sNx; i++) {
         long p = O2(m, i, j, t);
-        cg2d_b[p] = cg2d_b[p] - m->freeSurfFac * m->rA[p] / m->deltaTMom / m->deltaTFreeSurf * m->etaN[p];
+        /* solve_for_pressure.F:214-236: etaH with exactConserv, else etaN */
+        const double eta = m->exactConserv ? m->etaH[p] : m->etaN[p];
+        cg2d_b[p] = cg2d_b[p] - m->freeSurfFac * m->rA[p] / m->deltaTMom / m->deltaTFreeSurf * eta;
       }
   int numIters = m->cg2dMaxIters, nIterMin = m->cg2dUseMinResSol - 1;
   double firstRes, minResSq, lastRes;
@@ -276,11 +278,37 @@ void oracle_momentum_correction_step(OModel *m) {
   }
 }
 
-/* INTEGR_CONTINUITY (integr_continuity.F:276-314) -> INTEGRATE_FOR_W
- * (integrate_for_w.F:61-195), linear free surface, no exactConserv */
+/* INTEGR_CONTINUITY (integr_continuity.F:66-314) -> INTEGRATE_FOR_W
+ * (integrate_for_w.F:61-195), linear free surface.  With exactConserv
+ * (EXACT_CONSERV defined, myIter > nIter0, no fresh-water flux, no OBCS):
+ * dEtaHdt = -hDivFlow/rA, etaN = etaH + implicDiv2Dflow*dEtaHdt*dtFS on the
+ * interior, EXCH, then UPDATE_ETAH (update_etah.F:55-73). */
 void oracle_integr_continuity(OModel *m) {
   const int sNx = m->sNx, sNy = m->sNy, Nr = m->Nr;
-  if (m->exactConserv) { fprintf(stderr, "oracle: exactConserv not yet restated\n"); abort(); }
+  const long N2 = m->n2 * m->nTiles;
+  if (m->exactConserv) {
+    for (int t = 0; t < m->nTiles; t++) {
+      double *hDiv = calloc(m->n2, 8);
+#define HD(i, j) hDiv[O2(m, i, j, 0)]
+      for (int k = 1; k <= Nr; k++)
+        for (int j = 1; j <= sNy; j++)
+          for (int i = 1; i <= sNx; i++) {
+            double uT1 = m->uVel[O3(m, i + 1, j, k, t)] * m->dyG[O2(m, i + 1, j, t)] * m->drF[k - 1] * m->hFacW[O3(m, i + 1, j, k, t)];
+            double uT0 = m->uVel[O3(m, i, j, k, t)] * m->dyG[O2(m, i, j, t)] * m->drF[k - 1] * m->hFacW[O3(m, i, j, k, t)];
+            double vT1 = m->vVel[O3(m, i, j + 1, k, t)] * m->dxG[O2(m, i, j + 1, t)] * m->drF[k - 1] * m->hFacS[O3(m, i, j + 1, k, t)];
+            double vT0 = m->vVel[O3(m, i, j, k, t)] * m->dxG[O2(m, i, j, t)] * m->drF[k - 1] * m->hFacS[O3(m, i, j, k, t)];
+            HD(i, j) = HD(i, j) + m->maskC[O3(m, i, j, k, t)] * (uT1 - uT0 + vT1 - vT0);
+          }
+      for (int j = 1; j <= sNy; j++)
+        for (int i = 1; i <= sNx; i++) {
+          long p = O2(m, i, j, t);
+          m->dEtaHdt[p] = -(HD(i, j) * m->recip_rA[p]) - 0.0 * 0.0;  /* - facEmP*EmPmR, both 0 */
+          m->etaN[p] = m->etaH[p] + m->implicDiv2DFlow * m->dEtaHdt[p] * m->deltaTFreeSurf;
+        }
+#undef HD
+      free(hDiv);
+    }
+  }
   for (int t = 0; t < m->nTiles; t++)
     for (int k = Nr; k >= 1; k--)
       for (int j = 1; j <= sNy; j++)
@@ -296,6 +324,10 @@ void oracle_integr_continuity(OModel *m) {
           else
             m->wVel[O3(m, i, j, k, t)] = (m->wVel[O3(m, i, j, k + 1, t)] + conv2d * m->recip_rA[p]) * m->maskC[O3(m, i, j, k, t)];
         }
+  if (m->exactConserv) {
+    oracle_exch_xy(m, m->etaN);
+    for (long p = 0; p < N2; p++) m->etaH[p] = m->etaN[p];   /* UPDATE_ETAH, implicDiv2Dflow = 1 */
+  }
   if (m->myIter == m->nIter0) oracle_exch_xyz(m, m->wVel, Nr);
 }
 
@@ -310,7 +342,13 @@ void oracle_forward_step(OModel *m) {
     m->surfaceForcingU[p] = m->fu[p] * mass2rUnit;
     m->surfaceForcingV[p] = m->fv[p] * mass2rUnit;
   }
+  if (m->tempStepping) {
+    /* forward_step.F:656 DO_OCEANIC_PHYS, :732 THERMODYNAMICS (staggerTimeStep = F) */
+    oracle_oceanic_phys(m);
+    oracle_thermodynamics(m);
+  }
   oracle_dynamics(m);
+  /* forward_step.F:806: myIter/myTime advance before SOLVE_FOR_PRESSURE */
   oracle_solve_for_pressure(m);
   oracle_momentum_correction_step(m);
   oracle_integr_continuity(m);

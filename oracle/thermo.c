@@ -1,0 +1,241 @@
+/*
+ * thermo.c -- oracle restatement of the tracer half of the step.
+ * TEST INFRASTRUCTURE (see oracle.h): never linked into the product.
+ *
+ *   oracle_oceanic_phys   DO_OCEANIC_PHYS subset (model/src/do_oceanic_phys.F:555-882):
+ *                         EXTERNAL_FORCING_SURF (external_forcing_surf.F:95-186) with
+ *                         FORCING_SURF_RELAX (forcing_surf_relax.F:52-80),
+ *                         FIND_RHO_2D LINEAR (find_rho.F:125-136) for rhoInSitu,
+ *                         GRAD_SIGMA sigmaR (grad_sigma.F:103-117) + CALC_IVDC (calc_ivdc.F:60-71)
+ *   oracle_thermodynamics THERMODYNAMICS (thermodynamics.F) -> TEMP_INTEGRATE (temp_integrate.F):
+ *                         CALC_3D_DIFFUSIVITY (calc_3d_diffusivity.F:99-156),
+ *                         CALC_ADV_FLOW (calc_adv_flow.F:60-113), APPLY_FORCING_T
+ *                         (apply_forcing.F:687-695), GAD_CALC_RHS (gad_calc_rhs.F) with
+ *                         GAD_C2_ADV_X/Y/R and GAD_DIFF_X/Y, ADAMS_BASHFORTH2
+ *                         (adams_bashforth2.F:61-88), TIMESTEP_TRACER (timestep_tracer.F),
+ *                         GAD_IMPLICIT_R (gad_implicit_r.F:96-140) -> SOLVE_TRIDIAGONAL
+ *                         (solve_tridiagonal.F, default branch), CYCLE_TRACER (cycle_tracer.F)
+ * Multiplications by deepFac/rhoFac factors (= 1) and additions of identically-zero
+ * terms of disabled packages are dropped (bit-exact).
+ */
+#include "oracle.h"
+#include <math.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#define L(a, i, j) (a)[(long)((i) + OLx - 1) + (long)((j) + OLy - 1) * nx]
+#define W3(a, i, j, k) (a)[(long)((i) + OLx - 1) + (long)((j) + OLy - 1) * nx + (long)((k) - 1) * n2]
+
+/* FIND_RHO_2D, equationOfState = 'LINEAR' (find_rho.F:125-136) */
+static double rho_linear(const OModel *m, int kRef, double t, double s) {
+  const double refTemp = m->tRef[kRef - 1], refSalt = m->sRef[kRef - 1];
+  const double dRho = m->rhoNil - m->rhoConst;
+  return m->rhoNil * (m->sBeta * (s - refSalt) - m->tAlpha * (t - refTemp)) + dRho;
+}
+
+void oracle_oceanic_phys(OModel *m) {
+  const int sNx = m->sNx, sNy = m->sNy, OLx = m->OLx, OLy = m->OLy, Nr = m->Nr, nx = m->nx;
+  const long n2 = m->n2;
+  for (int t = 0; t < m->nTiles; t++) {
+    const double *theta = m->theta + t * m->n3, *salt = m->salt + t * m->n3;
+    const double *hFacC = m->hFacC + t * m->n3, *maskC = m->maskC + t * m->n3;
+    double *rhoInSitu = m->rhoInSitu + t * m->n3, *conv = m->IVDConvCount + t * m->n3;
+    double *sfT = m->surfaceForcingT + t * n2;
+    const double *lam = m->lambdaThetaClimRelax + t * n2, *SST = m->SST + t * n2;
+    /* EXTERNAL_FORCING_SURF: surfaceForcingT = 0, then FORCING_SURF_RELAX (ks = 1),
+     * full range iMin..iMax = 1-OLx..sNx+OLx (do_oceanic_phys.F:555-558); Qnet = 0 */
+    for (int j = 1 - OLy; j <= sNy + OLy; j++)
+      for (int i = 1 - OLx; i <= sNx + OLx; i++)
+        L(sfT, i, j) = -(L(lam, i, j) * (W3(theta, i, j, 1) - L(SST, i, j)) * m->drF[0] * W3(hFacC, i, j, 1));
+    /* FIND_RHO_2D for every level, kRef = k (do_oceanic_phys.F:753-761) */
+    for (int k = 1; k <= Nr; k++)
+      for (int j = 1 - OLy; j <= sNy + OLy; j++)
+        for (int i = 1 - OLx; i <= sNx + OLx; i++)
+          W3(rhoInSitu, i, j, k) = rho_linear(m, k, W3(theta, i, j, k), W3(salt, i, j, k));
+    /* IVDConvCount = 0, then k = Nr..2: sigmaR from rho(k) and rho(theta(k-1), kRef = k) */
+    for (long p = 0; p < m->n3; p++) conv[p] = 0.0;
+    if (m->ivdc_kappa != 0.0) {
+      for (int k = Nr; k >= 2; k--)
+        for (int j = 1 - OLy; j <= sNy + OLy; j++)
+          for (int i = 1 - OLx; i <= sNx + OLx; i++) {
+            double rhoKp1 = W3(rhoInSitu, i, j, k);
+            double rhoKm1 = rho_linear(m, k, W3(theta, i, j, k - 1), W3(salt, i, j, k - 1));
+            double sigmaR = W3(maskC, i, j, k) * W3(maskC, i, j, k - 1) * m->recip_drC[k - 1] * m->rkSign *
+                            (rhoKp1 - rhoKm1);
+            W3(conv, i, j, k) = (-sigmaR * m->gravitySign > 0.0) ? 1.0 : 0.0;
+          }
+    }
+  }
+}
+
+void oracle_thermodynamics(OModel *m) {
+  const int sNx = m->sNx, sNy = m->sNy, OLx = m->OLx, OLy = m->OLy, Nr = m->Nr, nx = m->nx;
+  const long n2 = m->n2, n3 = m->n3;
+  if (m->tempAdvScheme != 2 || m->tempVertAdvScheme != 2) {
+    fprintf(stderr, "oracle_thermodynamics: only tempAdvScheme = 2 restated here\n"); abort();
+  }
+  if (!m->implicitDiffusion) { fprintf(stderr, "oracle_thermodynamics: explicit vertical diffusion not restated\n"); abort(); }
+  double *gT = calloc(n3, 8), *kappaRT = calloc(n3, 8);
+  double *a3 = calloc(n3, 8), *b3 = calloc(n3, 8), *c3 = calloc(n3, 8), *cp = calloc(n3, 8), *yp = calloc(n3, 8);
+  double *fVer[2], *xA = calloc(n2, 8), *yA = calloc(n2, 8), *uTrans = calloc(n2, 8), *vTrans = calloc(n2, 8);
+  double *rTrans = calloc(n2, 8), *rTransKp = calloc(n2, 8), *maskUp = calloc(n2, 8), *gtForc = calloc(n2, 8);
+  double *fZon = calloc(n2, 8), *fMer = calloc(n2, 8), *af = calloc(n2, 8), *df = calloc(n2, 8);
+  fVer[0] = calloc(n2, 8); fVer[1] = calloc(n2, 8);
+  const double advFac = m->tempAdvection ? 1.0 : 0.0, rAdvFac = m->rkSign * advFac;
+  const double abFac = (m->myIter == m->nIter0 && m->nIter0 == 0) ? 0.0 : 0.5 + m->abEps; /* tempStartAB = nIter0 */
+
+  for (int t = 0; t < m->nTiles; t++) {
+    double *theta = m->theta + t * n3, *gtNm1 = m->gtNm1 + t * n3;
+    const double *uVel = m->uVel + t * n3, *vVel = m->vVel + t * n3, *wVel = m->wVel + t * n3;
+    const double *hFacW = m->hFacW + t * n3, *hFacS = m->hFacS + t * n3, *maskC = m->maskC + t * n3;
+    const double *rhFacC = m->recip_hFacC + t * n3, *conv = m->IVDConvCount + t * n3;
+    const double *dxG = m->dxG + t * n2, *dyG = m->dyG + t * n2, *rA = m->rA + t * n2;
+    const double *recip_rA = m->recip_rA + t * n2, *recip_dxC = m->recip_dxC + t * n2;
+    const double *recip_dyC = m->recip_dyC + t * n2, *maskInC = m->maskInC + t * n2;
+    const double *sfT = m->surfaceForcingT + t * n2;
+
+    /* CALC_3D_DIFFUSIVITY: KappaRT = IVDConvCount*ivdc_kappa + KbryanLewis79(=0) + diffKrNrT(k) */
+    for (int k = 1; k <= Nr; k++)
+      for (int j = 1 - OLy; j <= sNy + OLy; j++)
+        for (int i = 1 - OLx; i <= sNx + OLx; i++)
+          W3(kappaRT, i, j, k) = (W3(conv, i, j, k) * m->ivdc_kappa + 0.0) + m->diffKrT;
+    for (long p = 0; p < n3; p++) gT[p] = 0.0;
+    for (long p = 0; p < n2; p++) { fVer[0][p] = fVer[1][p] = 0.0; rTrans[p] = 0.0; }
+
+    for (int k = Nr; k >= 1; k--) {
+      const int kM1 = k > 1 ? k - 1 : 1, kUp = 1 + (k + 1) % 2, kDown = 1 + k % 2;
+      double *fVerUp = fVer[kUp - 1], *fVerDn = fVer[kDown - 1];
+      /* CALC_ADV_FLOW */
+      for (int j = 1 - OLy; j <= sNy + OLy; j++)
+        for (int i = 1 - OLx; i <= sNx + OLx; i++) {
+          L(xA, i, j) = L(dyG, i, j) * m->drF[k - 1] * W3(hFacW, i, j, k);
+          L(yA, i, j) = L(dxG, i, j) * m->drF[k - 1] * W3(hFacS, i, j, k);
+          L(rTransKp, i, j) = (k == Nr) ? 0.0 : L(rTrans, i, j);
+          L(uTrans, i, j) = W3(uVel, i, j, k) * L(xA, i, j);
+          L(vTrans, i, j) = W3(vVel, i, j, k) * L(yA, i, j);
+          if (k == 1) {
+            L(maskUp, i, j) = 0.0; L(rTrans, i, j) = 0.0;
+          } else {
+            L(maskUp, i, j) = W3(maskC, i, j, k - 1) * W3(maskC, i, j, k);
+            L(rTrans, i, j) = W3(wVel, i, j, k) * L(rA, i, j) * L(maskUp, i, j);
+          }
+        }
+      /* APPLY_FORCING_T: surface flux at k = kSurface = 1 over 0..sNx+1 */
+      for (long p = 0; p < n2; p++) gtForc[p] = 0.0;
+      if (m->tempForcing && k == 1)
+        for (int j = 0; j <= sNy + 1; j++)
+          for (int i = 0; i <= sNx + 1; i++)
+            L(gtForc, i, j) = L(gtForc, i, j) + L(sfT, i, j) * m->recip_drF[k - 1] * W3(rhFacC, i, j, k);
+      /* GAD_CALC_RHS */
+      for (long p = 0; p < n2; p++) { fZon[p] = 0.0; fMer[p] = 0.0; fVerUp[p] = 0.0; df[p] = 0.0; }
+      if (m->tempAdvection) { /* GAD_C2_ADV_X */
+        for (int j = 1 - OLy; j <= sNy + OLy; j++) {
+          L(af, 1 - OLx, j) = 0.0;
+          for (int i = 2 - OLx; i <= sNx + OLx; i++)
+            L(af, i, j) = L(uTrans, i, j) * (W3(theta, i, j, k) + W3(theta, i - 1, j, k)) * 0.5;
+        }
+        for (long p = 0; p < n2; p++) fZon[p] = fZon[p] + af[p];
+      }
+      if (m->diffKhT != 0.0) { /* GAD_DIFF_X, cosFacU = 1 */
+        for (int j = 1 - OLy; j <= sNy + OLy; j++) {
+          L(df, 1 - OLx, j) = 0.0;
+          for (int i = 2 - OLx; i <= sNx + OLx; i++)
+            L(df, i, j) = -m->diffKhT * L(xA, i, j) * L(recip_dxC, i, j) * (W3(theta, i, j, k) - W3(theta, i - 1, j, k));
+        }
+      } else {
+        for (long p = 0; p < n2; p++) df[p] = 0.0;
+      }
+      for (long p = 0; p < n2; p++) fZon[p] = fZon[p] + df[p];
+      if (m->tempAdvection) { /* GAD_C2_ADV_Y */
+        for (int i = 1 - OLx; i <= sNx + OLx; i++) L(af, i, 1 - OLy) = 0.0;
+        for (int j = 2 - OLy; j <= sNy + OLy; j++)
+          for (int i = 1 - OLx; i <= sNx + OLx; i++)
+            L(af, i, j) = L(vTrans, i, j) * (W3(theta, i, j, k) + W3(theta, i, j - 1, k)) * 0.5;
+        for (long p = 0; p < n2; p++) fMer[p] = fMer[p] + af[p];
+      }
+      if (m->diffKhT != 0.0) { /* GAD_DIFF_Y */
+        for (int i = 1 - OLx; i <= sNx + OLx; i++) L(df, i, 1 - OLy) = 0.0;
+        for (int j = 2 - OLy; j <= sNy + OLy; j++)
+          for (int i = 1 - OLx; i <= sNx + OLx; i++)
+            L(df, i, j) = -m->diffKhT * L(yA, i, j) * L(recip_dyC, i, j) * (W3(theta, i, j, k) - W3(theta, i, j - 1, k));
+      } else {
+        for (long p = 0; p < n2; p++) df[p] = 0.0;
+      }
+      for (long p = 0; p < n2; p++) fMer[p] = fMer[p] + df[p];
+      if (m->tempAdvection && k >= 2) { /* GAD_C2_ADV_R */
+        for (int j = 1 - OLy; j <= sNy + OLy; j++)
+          for (int i = 1 - OLx; i <= sNx + OLx; i++) {
+            double wT = W3(maskC, i, j, kM1) * L(rTrans, i, j) * (W3(theta, i, j, k) + W3(theta, i, j, kM1)) * 0.5;
+            L(fVerUp, i, j) = L(fVerUp, i, j) + wT * L(maskInC, i, j);
+          }
+      }
+      /* implicitDiffusion: explicit vertical diffusive flux df = 0 -> fVerT(kUp) + 0 */
+      for (int j = 1 - OLy; j <= sNy + OLy - 1; j++)
+        for (int i = 1 - OLx; i <= sNx + OLx - 1; i++) {
+          double T = W3(theta, i, j, k);
+          W3(gT, i, j, k) = W3(gT, i, j, k) -
+              W3(rhFacC, i, j, k) * m->recip_drF[k - 1] * L(recip_rA, i, j) *
+              ((L(fZon, i + 1, j) - L(fZon, i, j)) * L(maskInC, i, j) +
+               (L(fMer, i, j + 1) - L(fMer, i, j)) * L(maskInC, i, j) +
+               (L(fVerDn, i, j) - L(fVerUp, i, j)) * m->rkSign -
+               T * ((L(uTrans, i + 1, j) - L(uTrans, i, j)) * advFac + (L(vTrans, i, j + 1) - L(vTrans, i, j)) * advFac +
+                    (L(rTransKp, i, j) - L(rTrans, i, j)) * rAdvFac) * L(maskInC, i, j));
+        }
+      /* temp_integrate.F: gT += gtForc (tracForcingOutAB = 0), then ADAMS_BASHFORTH2(k) */
+      for (int j = 1 - OLy; j <= sNy + OLy; j++)
+        for (int i = 1 - OLx; i <= sNx + OLx; i++) {
+          W3(gT, i, j, k) = W3(gT, i, j, k) + L(gtForc, i, j);
+          double ab = abFac * (W3(gT, i, j, k) - W3(gtNm1, i, j, k));
+          W3(gtNm1, i, j, k) = W3(gT, i, j, k);
+          W3(gT, i, j, k) = W3(gT, i, j, k) + ab;
+        }
+    }
+    /* TIMESTEP_TRACER: gT = theta + dTtracerLev(k)*gT */
+    for (long p = 0; p < n3; p++) gT[p] = theta[p] + m->deltaTtracer * gT[p];
+    /* GAD_IMPLICIT_R, implicitDiffusion: b5d (sub), c5d (diag), d5d (super) on 1..sNx, 1..sNy */
+    for (long p = 0; p < n3; p++) { a3[p] = 0.0; b3[p] = 1.0; c3[p] = 0.0; }
+    for (int k = 1; k <= Nr; k++)
+      for (int j = 1; j <= sNy; j++)
+        for (int i = 1; i <= sNx; i++) {
+          double sub = 0.0, sup = 0.0;
+          if (k >= 2)
+            sub = -(m->deltaTtracer * W3(maskC, i, j, k - 1) * W3(rhFacC, i, j, k) * m->recip_drF[k - 1] *
+                    W3(kappaRT, i, j, k) * m->recip_drC[k - 1]);
+          if (k <= Nr - 1)
+            sup = -(m->deltaTtracer * W3(maskC, i, j, k + 1) * W3(rhFacC, i, j, k) * m->recip_drF[k - 1] *
+                    W3(kappaRT, i, j, k + 1) * m->recip_drC[k]);
+          W3(a3, i, j, k) = sub; W3(c3, i, j, k) = sup;
+          W3(b3, i, j, k) = 1.0 - (sub + sup);
+        }
+    /* SOLVE_TRIDIAGONAL (default: neither LOWMEMORY nor KINNER), whole tile */
+    for (int k = 1; k <= Nr; k++)
+      for (int j = 1 - OLy; j <= sNy + OLy; j++)
+        for (int i = 1 - OLx; i <= sNx + OLx; i++) {
+          double y = W3(gT, i, j, k);
+          if (k == 1) {
+            if (W3(b3, i, j, 1) != 0.0) {
+              double rec = 1.0 / W3(b3, i, j, 1);
+              W3(cp, i, j, 1) = W3(c3, i, j, 1) * rec;
+              W3(yp, i, j, 1) = y * rec;
+            } else { W3(cp, i, j, 1) = 0.0; W3(yp, i, j, 1) = 0.0; }
+          } else {
+            double tmp = W3(b3, i, j, k) - W3(a3, i, j, k) * W3(cp, i, j, k - 1);
+            if (tmp != 0.0) {
+              double rec = 1.0 / tmp;
+              W3(cp, i, j, k) = W3(c3, i, j, k) * rec;
+              W3(yp, i, j, k) = (y - W3(a3, i, j, k) * W3(yp, i, j, k - 1)) * rec;
+            } else { W3(cp, i, j, k) = 0.0; W3(yp, i, j, k) = 0.0; }
+          }
+        }
+    for (int k = Nr; k >= 1; k--)
+      for (int j = 1 - OLy; j <= sNy + OLy; j++)
+        for (int i = 1 - OLx; i <= sNx + OLx; i++)
+          W3(gT, i, j, k) = (k == Nr) ? W3(yp, i, j, k) : W3(yp, i, j, k) - W3(cp, i, j, k) * W3(gT, i, j, k + 1);
+    /* CYCLE_TRACER */
+    for (long p = 0; p < n3; p++) theta[p] = gT[p];
+  }
+  free(gT); free(kappaRT); free(a3); free(b3); free(c3); free(cp); free(yp);
+  free(fVer[0]); free(fVer[1]); free(xA); free(yA); free(uTrans); free(vTrans); free(rTrans); free(rTransKp);
+  free(maskUp); free(gtForc); free(fZon); free(fMer); free(af); free(df);
+}

@@ -24,9 +24,27 @@ EXPERIMENTS = {
         "inputs": ["input/bathy.bin", "input/windx_cosy.bin"],
         "output": "results/output.txt",
     },
+    "tutorial_baroclinic_gyre": {
+        "inputs": ["input/bathy.bin", "input/windx_cosy.bin", "input/SST_relax.bin"],
+        "output": "results/output.txt",
+    },
 }
 
 _num = r"[-+]?\d*\.?\d+(?:[EeDd][-+]?\d+)?"
+
+
+def parse_grid_monitor(path):
+    """%MON lines printed before the first time step (INI_GRID / INI_CORI grid
+    statistics, model/src/ini_grid.F:128-145)."""
+    grid = {}
+    with open(path) as f:
+        for line in f:
+            m = re.search(r"%MON (\S+)\s*=\s*(" + _num + ")", line)
+            if m:
+                if m.group(1) == "time_tsnumber":
+                    break
+                grid[m.group(1)] = float(m.group(2).replace("D", "E"))
+    return grid
 
 
 def parse_monitor(path):
@@ -104,6 +122,8 @@ def main():
         res = os.path.join(REF, exp, spec["output"])
         with open(os.path.join(out, "monitor.json"), "w") as f:
             json.dump(parse_monitor(res), f, indent=1)
+        with open(os.path.join(out, "grid_monitor.json"), "w") as f:
+            json.dump(parse_grid_monitor(res), f, indent=1)
         with open(os.path.join(out, "params.json"), "w") as f:
             json.dump(parse_params(res), f, indent=1, sort_keys=True)
         print("wrote", out)
