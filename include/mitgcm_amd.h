@@ -59,6 +59,11 @@ int mgcm_set_halo_map(mgcm_model *m, const long *src_of_point, long count);
 int mgcm_init(mgcm_model *m);
 
 /* --------------------------------------------------------- hot path ops */
+/* DO_OCEANIC_PHYS subset (model/src/do_oceanic_phys.F:555-882: surface
+ * relaxation forcing, FIND_RHO_2D, IVDC) followed by THERMODYNAMICS
+ * (model/src/thermodynamics.F:25 -> temp_integrate.F: GAD advection/diffusion,
+ * AB2, implicit vertical diffusion) for theta.  No-op unless tempStepping. */
+int mgcm_thermodynamics(mgcm_model *m);
 /* DYNAMICS (model/src/dynamics.F:21): MOM_FLUXFORM + TIMESTEP + AB2 for every
  * tile and level; writes gU/gV (= u*, v*) and updates guNm1/gvNm1. */
 int mgcm_dynamics(mgcm_model *m);
@@ -71,7 +76,7 @@ int mgcm_momentum_correction_step(mgcm_model *m);
 int mgcm_integr_continuity(mgcm_model *m);
 /* DO_FIELDS_BLOCKING_EXCHANGES (model/src/do_fields_blocking_exchanges.F:54). */
 int mgcm_blocking_exchanges(mgcm_model *m);
-/* FORWARD_STEP subset: the five ops above (+ surface forcing), nsteps times,
+/* FORWARD_STEP subset: the six ops above (+ surface forcing), nsteps times,
  * asynchronously on the model's stream (captured once into a hipGraph). */
 int mgcm_forward_step(mgcm_model *m, int nsteps);
 /* Wait for all queued device work. */

@@ -37,6 +37,7 @@ def lib():
         "mgcm_set_halo_map": (ci, [vp, PL, cl]),
         "mgcm_init": (ci, [vp]),
         "mgcm_dynamics": (ci, [vp]),
+        "mgcm_thermodynamics": (ci, [vp]),
         "mgcm_solve_for_pressure": (ci, [vp]),
         "mgcm_momentum_correction_step": (ci, [vp]),
         "mgcm_integr_continuity": (ci, [vp]),
@@ -59,7 +60,7 @@ def lib():
 
 
 EXPORTS = ["mgcm_create", "mgcm_destroy", "mgcm_last_error", "mgcm_set_param", "mgcm_get_param", "mgcm_put",
-           "mgcm_get", "mgcm_device_ptr", "mgcm_set_halo_map", "mgcm_init", "mgcm_dynamics",
+           "mgcm_get", "mgcm_device_ptr", "mgcm_set_halo_map", "mgcm_init", "mgcm_dynamics", "mgcm_thermodynamics",
            "mgcm_solve_for_pressure", "mgcm_momentum_correction_step", "mgcm_integr_continuity",
            "mgcm_blocking_exchanges", "mgcm_forward_step", "mgcm_sync", "mgcm_cg2d", "mgcm_solve_stats",
            "mgcm_kernel_ms", "mgcm_kernel_timing", "ini_cg2d_amd_", "cg2d_amd_"]

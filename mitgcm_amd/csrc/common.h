@@ -28,24 +28,32 @@ struct Params {
   int momAdvection, momViscosity, momForcing, useCoriolis, no_slip_sides, no_slip_bottom;
   int selectCoriScheme, momForcingOutAB, momDissip_In_AB, implicitViscosity;
   int cg2dMaxIters, cg2dUseMinResSol, cg2dNormaliseRHS, nIter0;
+  // 3-D / tracer path
+  double gravity, gravitySign, rhoNil, tAlpha, sBeta, ivdc_kappa, diffKhT, diffKrT, deltaTtracer;
+  double recip_rSphere;
+  int exactConserv, tempStepping, tempAdvection, tempForcing, implicitDiffusion, tempAdvScheme;
+  int metricSphere;   // usingSphericalPolarGrid && selectMetricTerms >= 1
 };
 
 // Device pointers of every field the kernels touch.
 struct Fields {
   // 1-D vertical grid
-  const double *drF, *drC, *recip_drF, *recip_drC;
+  const double *drF, *drC, *recip_drF, *recip_drC, *rF, *rC, *tRef, *sRef;
   // 2-D grid
   const double *dxF, *dyF, *dxG, *dyG, *dxC, *dyC, *dxV, *dyU, *rA, *rAw, *rAs;
   const double *recip_dxF, *recip_dyF, *recip_dxC, *recip_dyC, *recip_dxV, *recip_dyU;
   const double *recip_rA, *recip_rAw, *recip_rAs, *fCori, *Bo_surf, *recip_Bo;
+  const double *tanPhiAtU, *tanPhiAtV, *maskInC, *SST, *lambdaThetaClimRelax;
   // 3-D masks
-  const double *hFacC, *hFacW, *hFacS, *recip_hFacW, *recip_hFacS, *maskC, *maskW, *maskS;
+  const double *hFacC, *hFacW, *hFacS, *recip_hFacC, *recip_hFacW, *recip_hFacS, *maskC, *maskW, *maskS;
   // CG2D operator
   const double *aW2d, *aS2d, *aC2d, *pW, *pS, *pC;
   // state
   double *uVel, *vVel, *wVel, *theta, *salt, *etaN;
   double *gU, *gV, *guNm1, *gvNm1;
   const double *fu, *fv;
+  double *etaH, *surfaceForcingT, *rhoInSitu, *IVDConvCount, *gtNm1;
+  double *thetaNext, *gTscr, *cpScr;   // tracer ping-pong buffer and per-column scratch
   // solver work
   double *cg2d_b, *cg2d_x;
 };

@@ -47,6 +47,11 @@ __global__ void __launch_bounds__(256) k_mom_step(Dims d, Params p, Fields f, co
 #define G2(a, ii, jj) f.a[MG_I2(d, ii, jj, t)]
 #define G3(a, ii, jj, kk) f.a[MG_I3(d, ii, jj, kk, t)]
 
+  // CALC_PHI_HYD (calc_phi_hyd.F:175-327, OCEANIC, integr_GeoPot = 2, uniformFreeSurfLev):
+  // phiHydF is integrated down this column and the west / south neighbours',
+  // which CALC_GRAD_PHI_HYD differences (calc_grad_phi_hyd.F:152-171).
+  double phF = 0.0, phFw = 0.0, phFs = 0.0;
+  const double recip_rhoConst = 1.0 / p.rhoConst;
   double fVerUkm = 0.0, fVerVkm = 0.0;
   if (inner && p.momAdvection) {
     // MOM_CALC_RTRANS(k=1) + MOM_U/V_ADV_WU/WV(k=1): free-surface flux (mom_fluxform.F:384-417)
@@ -60,6 +65,27 @@ __global__ void __launch_bounds__(256) k_mom_step(Dims d, Params p, Fields f, co
     const double drF = f.drF[k - 1], recip_drF = f.recip_drF[k - 1];
     double gU = 0.0, gV = 0.0, guDiss = 0.0, gvDiss = 0.0;
     double fVerUkp = 0.0, fVerVkp = 0.0;
+    double dPhiHydX = 0.0, dPhiHydY = 0.0;
+    if (inner) {
+      double dRlocM = 0.5 * f.drC[k - 1];
+      if (k == 1) dRlocM = f.rF[0] - f.rC[0];
+      const double dRlocP = (k == Nr) ? (f.rC[k - 1] - f.rF[k]) : 0.5 * f.drC[k];
+      const double a0 = f.rhoInSitu[MG_I3(d, i, j, k, t)];
+      const double phC = phF + dRlocM * p.gravity * a0 * recip_rhoConst;
+      phF = phC + dRlocP * p.gravity * a0 * recip_rhoConst;
+      if (i >= 1) {
+        const double aw = f.rhoInSitu[MG_I3(d, i - 1, j, k, t)];
+        const double phCw = phFw + dRlocM * p.gravity * aw * recip_rhoConst;
+        phFw = phCw + dRlocP * p.gravity * aw * recip_rhoConst;
+        dPhiHydX = G2(recip_dxC, i, j) * ((phC + 0.0) - (phCw + 0.0));
+      }
+      if (j >= 1) {
+        const double as = f.rhoInSitu[MG_I3(d, i, j - 1, k, t)];
+        const double phCs = phFs + dRlocM * p.gravity * as * recip_rhoConst;
+        phFs = phCs + dRlocP * p.gravity * as * recip_rhoConst;
+        dPhiHydY = G2(recip_dyC, i, j) * ((phC + 0.0) - (phCs + 0.0));
+      }
+    }
     if (inner) {
       const double rhFacW = G3(recip_hFacW, i, j, k), rhFacS = G3(recip_hFacS, i, j, k);
       const double hZ = hfacz(d, f, i, j, k, t);
@@ -175,6 +201,15 @@ __global__ void __launch_bounds__(256) k_mom_step(Dims d, Params p, Fields f, co
           gvDiss = gvDiss - cD * V(i, j, k) * rhFacS * recip_drF;
         }
       }
+      // ---------------- spherical metric terms (mom_u/v_metric_sphere.F, mom_fluxform.F:714-721, 973-980)
+      if (p.metricSphere) {
+        const double mTu = U(i, j, k) * p.recip_rSphere * 0.25 *
+                           (V(i, j, k) + V(i - 1, j, k) + V(i, j + 1, k) + V(i - 1, j + 1, k)) * G2(tanPhiAtU, i, j);
+        gU = gU + p.mtFacMom * mTu;
+        const double ub = U(i, j, k) + U(i + 1, j, k) + U(i, j - 1, k) + U(i + 1, j - 1, k);
+        const double mTv = -(p.recip_rSphere * 0.25 * ub * 0.25 * ub * G2(tanPhiAtV, i, j));
+        gV = gV + p.mtFacMom * mTv;
+      }
       // ---------------- Coriolis (mom_u_coriolis.F, mom_v_coriolis.F)
       if (p.useCoriolis) {
         const int sc = p.selectCoriScheme;
@@ -214,6 +249,9 @@ __global__ void __launch_bounds__(256) k_mom_step(Dims d, Params p, Fields f, co
         gvExt = gvExt + p.foFacMom * (f.fv[q2] * mass2rUnit) * recip_drF * G3(recip_hFacS, i, j, k);
     }
     if (inner) {
+      // timestep.F:116-126 synchronous time step: gU -= phFac*dPhiHydX
+      gU = gU - p.pfFacMom * dPhiHydX;
+      gV = gV - p.pfFacMom * dPhiHydY;
       if (p.momViscosity && p.momDissip_In_AB) { gU = gU + guDiss; gV = gV + gvDiss; }
       if (p.momForcing && p.momForcingOutAB != 1) { gU = gU + guExt; gV = gV + gvExt; }
     }

@@ -109,8 +109,8 @@ __global__ void __launch_bounds__(256) k_sfp_rhs(Dims d, Params p, Fields f) {
       const double pfS = f.dxG[q] * drF * f.hFacS[MG_I3(d, i, j, k, t)] * f.gV[MG_I3(d, i, j, k, t)] / p.deltaTMom;
       b = b + pfN - pfS;
     }
-    // solve_for_pressure.F:245-254 (linear free surface, not exactConserv)
-    b = b - p.freeSurfFac * f.rA[q] / p.deltaTMom / p.deltaTFreeSurf * f.etaN[q];
+    // solve_for_pressure.F:214-236 (linear free surface): etaH with exactConserv, else etaN
+    b = b - p.freeSurfFac * f.rA[q] / p.deltaTMom / p.deltaTFreeSurf * (p.exactConserv ? f.etaH[q] : f.etaN[q]);
   }
   f.cg2d_b[q] = b;
 }
@@ -633,6 +633,43 @@ __global__ void __launch_bounds__(256) k_continuity(Dims d, Fields f) {
   }
 }
 
+// INTEGR_CONTINUITY with exactConserv (integr_continuity.F:66-150, myIter > nIter0,
+// no fresh-water flux): hDivFlow summed k = 1..Nr, dEtaHdt = -hDivFlow/rA,
+// etaN = etaH + implicDiv2Dflow*dEtaHdt*deltaTFreeSurf; then INTEGRATE_FOR_W as k_continuity.
+__global__ void __launch_bounds__(256) k_continuity_ec(Dims d, Params p, Fields f) {
+  const int i = (int)(blockIdx.x * blockDim.x + threadIdx.x) + 1;
+  const int j = (int)(blockIdx.y * blockDim.y + threadIdx.y) + 1;
+  const int t = (int)blockIdx.z;
+  if (i > d.sNx || j > d.sNy) return;
+  const long q = MG_I2(d, i, j, t);
+  auto div = [&](int k) {
+    const double drF = f.drF[k - 1];
+    const double uT1 = f.uVel[MG_I3(d, i + 1, j, k, t)] * f.dyG[MG_I2(d, i + 1, j, t)] * drF * f.hFacW[MG_I3(d, i + 1, j, k, t)];
+    const double uT0 = f.uVel[MG_I3(d, i, j, k, t)] * f.dyG[q] * drF * f.hFacW[MG_I3(d, i, j, k, t)];
+    const double vT1 = f.vVel[MG_I3(d, i, j + 1, k, t)] * f.dxG[MG_I2(d, i, j + 1, t)] * drF * f.hFacS[MG_I3(d, i, j + 1, k, t)];
+    const double vT0 = f.vVel[MG_I3(d, i, j, k, t)] * f.dxG[q] * drF * f.hFacS[MG_I3(d, i, j, k, t)];
+    return uT1 - uT0 + vT1 - vT0;
+  };
+  double hDiv = 0.0;
+  for (int k = 1; k <= d.Nr; k++) hDiv = hDiv + f.maskC[MG_I3(d, i, j, k, t)] * div(k);
+  const double dEtaHdt = -(hDiv * f.recip_rA[q]) - 0.0 * 0.0;
+  f.etaN[q] = f.etaH[q] + p.implicDiv2DFlow * dEtaHdt * p.deltaTFreeSurf;
+  double wBelow = 0.0;
+  for (int k = d.Nr; k >= 1; k--) {
+    const double conv2d = -div(k);
+    double w;
+    if (k == d.Nr) w = conv2d * f.recip_rA[q] * f.maskC[MG_I3(d, i, j, k, t)];
+    else w = (wBelow + conv2d * f.recip_rA[q]) * f.maskC[MG_I3(d, i, j, k, t)];
+    f.wVel[MG_I3(d, i, j, k, t)] = w;
+    wBelow = w;
+  }
+}
+
+__global__ void __launch_bounds__(256) k_copy(double *dst, const double *src, long n) {
+  const long q = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (q < n) dst[q] = src[q];
+}
+
 __global__ void k_bump_counter(int *c, int nIncr) {
   if (threadIdx.x == 0) { c[0] += nIncr; c[1] += 1; }
 }
@@ -716,6 +753,17 @@ hipError_t launch_correction(const Dims &d, const Params &p, const Fields &f, hi
 hipError_t launch_continuity(const Dims &d, const Fields &f, hipStream_t s) {
   dim3 blk(64, 4, 1), grd((d.sNx + 63) / 64, (d.sNy + 3) / 4, d.nTiles);
   hipLaunchKernelGGL(k_continuity, grd, blk, 0, s, d, f);
+  return hipGetLastError();
+}
+
+hipError_t launch_continuity_ec(const Dims &d, const Params &p, const Fields &f, hipStream_t s) {
+  dim3 blk(64, 4, 1), grd((d.sNx + 63) / 64, (d.sNy + 3) / 4, d.nTiles);
+  hipLaunchKernelGGL(k_continuity_ec, grd, blk, 0, s, d, p, f);
+  return hipGetLastError();
+}
+
+hipError_t launch_copy(double *dst, const double *src, long n, hipStream_t s) {
+  hipLaunchKernelGGL(k_copy, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, dst, src, n);
   return hipGetLastError();
 }
 

@@ -12,6 +12,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <map>
+#include <utility>
 #include <string>
 #include <vector>
 
@@ -32,6 +33,10 @@ hipError_t launch_eta_update(const Dims &, const Fields &, hipStream_t);
 hipError_t launch_correction(const Dims &, const Params &, const Fields &, hipStream_t);
 hipError_t launch_continuity(const Dims &, const Fields &, hipStream_t);
 hipError_t launch_bump_counter(int *, int, hipStream_t);
+hipError_t launch_oceanic_phys(const Dims &, const Params &, const Fields &, hipStream_t);
+hipError_t launch_temp_step(const Dims &, const Params &, const Fields &, const int *, hipStream_t);
+hipError_t launch_continuity_ec(const Dims &, const Params &, const Fields &, hipStream_t);
+hipError_t launch_copy(double *, const double *, long, hipStream_t);
 }  // namespace mgcm
 
 using namespace mgcm;
@@ -61,16 +66,20 @@ struct FieldDesc {
 
 #define FD(n, k) {#n, k, offsetof(Fields, n)}
 static const FieldDesc FIELDS[] = {
-    FD(drF, F1D), FD(drC, F1D), FD(recip_drF, F1D), FD(recip_drC, F1D),
+    FD(drF, F1D), FD(drC, F1D), FD(recip_drF, F1D), FD(recip_drC, F1D), FD(rF, F1D), FD(rC, F1D),
+    FD(tRef, F1D), FD(sRef, F1D),
     FD(dxF, F2D), FD(dyF, F2D), FD(dxG, F2D), FD(dyG, F2D), FD(dxC, F2D), FD(dyC, F2D), FD(dxV, F2D), FD(dyU, F2D),
     FD(rA, F2D), FD(rAw, F2D), FD(rAs, F2D), FD(recip_dxF, F2D), FD(recip_dyF, F2D), FD(recip_dxC, F2D),
     FD(recip_dyC, F2D), FD(recip_dxV, F2D), FD(recip_dyU, F2D), FD(recip_rA, F2D), FD(recip_rAw, F2D),
     FD(recip_rAs, F2D), FD(fCori, F2D), FD(Bo_surf, F2D), FD(recip_Bo, F2D),
-    FD(hFacC, F3D), FD(hFacW, F3D), FD(hFacS, F3D), FD(recip_hFacW, F3D), FD(recip_hFacS, F3D),
+    FD(tanPhiAtU, F2D), FD(tanPhiAtV, F2D), FD(maskInC, F2D), FD(SST, F2D), FD(lambdaThetaClimRelax, F2D),
+    FD(hFacC, F3D), FD(hFacW, F3D), FD(hFacS, F3D), FD(recip_hFacC, F3D), FD(recip_hFacW, F3D), FD(recip_hFacS, F3D),
     FD(maskC, F3D), FD(maskW, F3D), FD(maskS, F3D),
     FD(aW2d, F2D), FD(aS2d, F2D), FD(aC2d, F2D), FD(pW, F2D), FD(pS, F2D), FD(pC, F2D),
     FD(uVel, F3D), FD(vVel, F3D), FD(wVel, F3D), FD(theta, F3D), FD(salt, F3D), FD(etaN, F2D),
     FD(gU, F3D), FD(gV, F3D), FD(guNm1, F3D), FD(gvNm1, F3D), FD(fu, F2D), FD(fv, F2D),
+    FD(etaH, F2D), FD(surfaceForcingT, F2D), FD(rhoInSitu, F3D), FD(IVDConvCount, F3D), FD(gtNm1, F3D),
+    FD(thetaNext, F3D), FD(gTscr, F3D), FD(cpScr, F3D),
     FD(cg2d_b, F2D), FD(cg2d_x, F2D),
 };
 #undef FD
@@ -90,13 +99,17 @@ static const PDesc PARAMS[] = {
     PI_(momAdvection), PI_(momViscosity), PI_(momForcing), PI_(useCoriolis), PI_(no_slip_sides),
     PI_(no_slip_bottom), PI_(selectCoriScheme), PI_(momForcingOutAB), PI_(momDissip_In_AB),
     PI_(implicitViscosity), PI_(cg2dMaxIters), PI_(cg2dUseMinResSol), PI_(cg2dNormaliseRHS), PI_(nIter0),
+    PD(gravity), PD(gravitySign), PD(rhoNil), PD(tAlpha), PD(sBeta), PD(ivdc_kappa), PD(diffKhT), PD(diffKrT),
+    PD(deltaTtracer), PI_(exactConserv), PI_(tempStepping), PI_(tempAdvection), PI_(tempForcing),
+    PI_(implicitDiffusion), PI_(tempAdvScheme),
 };
 #undef PD
 #undef PI_
 
 // kernel families timed with hipEvents when timing is enabled
-enum Kern { K_MOM, K_RHS, K_CG2D, K_EXCH, K_ETA, K_CORR, K_CONT, K_N };
-static const char *KNAMES[K_N] = {"mom_step", "sfp_rhs", "cg2d", "exchange", "eta_update", "correction", "continuity"};
+enum Kern { K_MOM, K_RHS, K_CG2D, K_EXCH, K_ETA, K_CORR, K_CONT, K_PHYS, K_TEMP, K_N };
+static const char *KNAMES[K_N] = {"mom_step", "sfp_rhs",    "cg2d",         "exchange", "eta_update",
+                                  "correction", "continuity", "oceanic_phys", "temp_step"};
 
 struct mgcm_model {
   Dims d{};
@@ -329,6 +342,8 @@ mgcm_model *mgcm_create(int sNx, int sNy, int OLx, int OLy, int Nr, int nSx, int
   p.momAdvection = p.momViscosity = p.momForcing = p.useCoriolis = 1;
   p.no_slip_sides = p.no_slip_bottom = 1; p.momDissip_In_AB = 1; p.momForcingOutAB = 0;
   p.cg2dMaxIters = 150; p.cg2dNormaliseRHS = 1;
+  p.gravity = 9.81; p.gravitySign = -1.0; p.rhoNil = 999.8; p.tAlpha = 2.0e-4; p.tempAdvection = 1;
+  p.tempForcing = 1; p.tempAdvScheme = 2; p.implicitDiffusion = 0;
   if (hipStreamCreateWithFlags(&m->stream, hipStreamNonBlocking) != hipSuccess) {
     set_err("mgcm_create: stream");
     delete m;
@@ -389,9 +404,9 @@ int mgcm_set_param(mgcm_model *m, const char *name, double value) {
     }
   // options the kernels do not implement are accepted only at their default
   // (inert) value; anything else is an explicit error, never silently ignored.
-  static const char *inert[] = {"useBiharmonicVisc", "nonlinFreeSurf", "select_rStar", "exactConserv",
-                                "useCDscheme", "vectorInvariantMomentum", "useNHMTerms", "metricTerms",
-                                "usingSphericalPolarGrid", "tempStepping", "saltStepping", "staggerTimeStep",
+  static const char *inert[] = {"useBiharmonicVisc", "nonlinFreeSurf", "select_rStar",
+                                "useCDscheme", "vectorInvariantMomentum", "useNHMTerms",
+                                "saltStepping", "staggerTimeStep",
                                 "implicitFreeSurface", "useRealFreshWaterFlux", "useGMRedi"};
   for (auto *n : inert)
     if (!strcmp(n, name)) {
@@ -473,8 +488,20 @@ int mgcm_init(mgcm_model *m) {
   if (m->p.implicitViscosity) return set_err("mgcm_init: implicitViscosity not supported by the device path yet");
   if (m->p.implicSurfPress != 1.0 || m->p.implicDiv2DFlow != 1.0)
     return set_err("mgcm_init: implicSurfPress/implicDiv2DFlow != 1 not supported yet");
+  auto ext = [&](const char *n, double dflt) { auto it = m->extra.find(n); return it == m->extra.end() ? dflt : it->second; };
+  const bool sph = ext("usingSphericalPolarGrid", 0.0) != 0.0;
+  m->p.metricSphere = sph && ext("selectMetricTerms", 1.0) >= 1.0;
+  m->p.recip_rSphere = sph ? 1.0 / ext("rSphere", 6370.0e3) : 0.0;   // ini_parms.F:1334
+  if (ext("integr_GeoPot", 2.0) != 2.0) return set_err("mgcm_init: only integr_GeoPot = 2 is implemented");
+  if (m->p.tempStepping) {
+    if (m->p.tempAdvScheme != 2 || ext("tempVertAdvScheme", 2.0) != 2.0)
+      return set_err("mgcm_init: tempAdvScheme %d not implemented on the device yet", m->p.tempAdvScheme);
+    if (!m->p.implicitDiffusion) return set_err("mgcm_init: explicit vertical tracer diffusion not implemented yet");
+  }
   int it0 = m->p.nIter0;
   HIPCHK(hipMemcpy(m->d_ctr, &it0, sizeof(int), hipMemcpyHostToDevice));
+  // INI_PSURF (ini_psurf.F:84): etaH = etaN
+  HIPCHK(hipMemcpy(m->f.etaH, m->f.etaN, m->d.n2 * m->d.nTiles * sizeof(double), hipMemcpyDeviceToDevice));
   m->ready = true;
   return 0;
 }
@@ -506,6 +533,16 @@ int mgcm_dynamics(mgcm_model *m) {
   return 0;
 }
 
+int mgcm_thermodynamics(mgcm_model *m) {
+  if (check_ready(m)) return -1;
+  if (!m->p.tempStepping) return 0;
+  // forward_step.F:656 DO_OCEANIC_PHYS, :732 THERMODYNAMICS (staggerTimeStep = F)
+  TIMED(K_PHYS, launch_oceanic_phys(m->d, m->p, m->f, m->stream));
+  TIMED(K_TEMP, launch_temp_step(m->d, m->p, m->f, m->d_ctr, m->stream));
+  std::swap(m->f.theta, m->f.thetaNext);   // CYCLE_TRACER: the new theta is the other buffer
+  return 0;
+}
+
 static int solve_impl(mgcm_model *m) {
   TIMED(K_RHS, launch_sfp_rhs(m->d, m->p, m->f, m->stream));
   const int nIterMin = m->p.cg2dUseMinResSol - 1;
@@ -528,17 +565,26 @@ int mgcm_momentum_correction_step(mgcm_model *m) {
 
 int mgcm_integr_continuity(mgcm_model *m) {
   if (check_ready(m)) return -1;
-  TIMED(K_CONT, launch_continuity(m->d, m->f, m->stream));
+  if (m->p.exactConserv) {
+    // integr_continuity.F:66-150 + EXCH etaN + UPDATE_ETAH (update_etah.F:55-73)
+    TIMED(K_CONT, launch_continuity_ec(m->d, m->p, m->f, m->stream));
+    TIMED(K_EXCH, launch_exchange(m->d, m->f.etaN, m->d_halo, m->nHalo, 1, m->stream));
+    TIMED(K_ETA, launch_copy(m->f.etaH, m->f.etaN, m->d.n2 * m->d.nTiles, m->stream));
+  } else {
+    TIMED(K_CONT, launch_continuity(m->d, m->f, m->stream));
+  }
   return 0;
 }
 
 int mgcm_blocking_exchanges(mgcm_model *m) {
   if (check_ready(m)) return -1;
-  // do_fields_blocking_exchanges.F:54-97: uVel, vVel, wVel (theta/salt are not
-  // stepped by the supported configs, their halos are unchanged)
+  // do_fields_blocking_exchanges.F:54-97: uVel, vVel, wVel, theta (salt is not
+  // stepped by the supported configs, its halo is unchanged)
   TIMED(K_EXCH, launch_exchange(m->d, m->f.uVel, m->d_halo, m->nHalo, m->d.Nr, m->stream));
   TIMED(K_EXCH, launch_exchange(m->d, m->f.vVel, m->d_halo, m->nHalo, m->d.Nr, m->stream));
   TIMED(K_EXCH, launch_exchange(m->d, m->f.wVel, m->d_halo, m->nHalo, m->d.Nr, m->stream));
+  if (m->p.tempStepping)
+    TIMED(K_EXCH, launch_exchange(m->d, m->f.theta, m->d_halo, m->nHalo, m->d.Nr, m->stream));
   return 0;
 }
 
@@ -548,6 +594,7 @@ int mgcm_forward_step(mgcm_model *m, int nsteps) {
   HIPCHK(hipSetDevice(m->device));
   HIPCHK(hipMemsetAsync(m->d_ctr + 1, 0, sizeof(int), m->stream));
   for (int s = 0; s < nsteps; s++) {
+    if (mgcm_thermodynamics(m)) return -1;
     if (mgcm_dynamics(m)) return -1;
     if (solve_impl(m)) return -1;
     if (mgcm_momentum_correction_step(m)) return -1;

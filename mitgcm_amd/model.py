@@ -16,11 +16,13 @@ from ._lib import check, lib, MgcmError
 GRID_2D = ("dxF", "dyF", "dxG", "dyG", "dxC", "dyC", "dxV", "dyU", "rA", "rAw", "rAs",
            "recip_dxF", "recip_dyF", "recip_dxC", "recip_dyC", "recip_dxV", "recip_dyU",
            "recip_rA", "recip_rAw", "recip_rAs", "fCori", "Bo_surf", "recip_Bo",
-           "aW2d", "aS2d", "aC2d", "pW", "pS", "pC")
-GRID_3D = ("hFacC", "hFacW", "hFacS", "recip_hFacW", "recip_hFacS", "maskC", "maskW", "maskS")
-GRID_1D = ("drF", "drC", "recip_drF", "recip_drC")
-STATE_3D = ("uVel", "vVel", "wVel", "theta", "salt", "gU", "gV", "guNm1", "gvNm1")
-STATE_2D = ("etaN", "fu", "fv")
+           "aW2d", "aS2d", "aC2d", "pW", "pS", "pC", "maskInC", "tanPhiAtU", "tanPhiAtV")
+GRID_3D = ("hFacC", "hFacW", "hFacS", "recip_hFacC", "recip_hFacW", "recip_hFacS", "maskC", "maskW", "maskS")
+GRID_1D = ("drF", "drC", "recip_drF", "recip_drC", "rF", "rC")
+STATE_1D = ("tRef", "sRef")
+STATE_3D = ("uVel", "vVel", "wVel", "theta", "salt", "gU", "gV", "guNm1", "gvNm1", "gtNm1", "rhoInSitu",
+            "IVDConvCount")
+STATE_2D = ("etaN", "etaH", "fu", "fv", "SST", "lambdaThetaClimRelax", "surfaceForcingT")
 
 DEVICE_PARAMS = ("deltaTMom", "deltaTFreeSurf", "deltaTClock", "abEps", "rhoConst", "gBaro", "viscAhD",
                  "viscAhZ", "viscA4D", "viscA4Z", "viscAr", "sideDragFactor", "freeSurfFac", "implicSurfPress",
@@ -54,7 +56,8 @@ class Model:
             a[:len(v)] = v
             self.put(n, a)
         for n in GRID_2D + GRID_3D:
-            self.put(n, g.f[n])
+            if n in g.f:        # tanPhiAtU/V exist on spherical grids only
+                self.put(n, g.f[n])
         src = np.ascontiguousarray(g.topo.src_of_point(), dtype=np.int64)
         check(L.mgcm_set_halo_map(self.h, src.ctypes.data_as(ctypes.POINTER(ctypes.c_long)), src.size),
               "mgcm_set_halo_map")
@@ -76,7 +79,7 @@ class Model:
     # ---- fields --------------------------------------------------------------
     def _shape(self, name):
         g = self.g
-        if name in GRID_1D:
+        if name in GRID_1D or name in STATE_1D:
             return (g.Nr + 1,)
         if name in GRID_3D or name in STATE_3D:
             return (g.nTiles, g.Nr, g.ny, g.nx)
@@ -94,6 +97,9 @@ class Model:
     # ---- hot path ------------------------------------------------------------
     def forward_step(self, nsteps=1):
         check(lib().mgcm_forward_step(self.h, int(nsteps)), "mgcm_forward_step")
+
+    def thermodynamics(self):
+        check(lib().mgcm_thermodynamics(self.h), "mgcm_thermodynamics")
 
     def dynamics(self):
         check(lib().mgcm_dynamics(self.h), "mgcm_dynamics")
@@ -195,7 +201,7 @@ def mon_stats(g, arr, hfac, mask, area, dr):
 
 
 def dynstat(model):
-    """dynstat block of MONITOR (pkg/monitor/monitor.F:103-129) for eta, u, v, w."""
+    """dynstat block of MONITOR (pkg/monitor/monitor.F:103-129) for eta, u, v, w, theta."""
     g = model.g
     f = g.f
     out = {}
@@ -204,7 +210,8 @@ def dynstat(model):
             ("eta", eta, f["maskInC"][:, None], f["maskInC"], f["rA"], f["drF"]),
             ("uvel", model.get("uVel"), f["hFacW"], f["maskInW"], f["rAw"], f["drF"]),
             ("vvel", model.get("vVel"), f["hFacS"], f["maskInS"], f["rAs"], f["drF"]),
-            ("wvel", model.get("wVel"), f["maskC"], f["maskInC"], f["rA"], f["drC"])):
+            ("wvel", model.get("wVel"), f["maskC"], f["maskInC"], f["rA"], f["drC"]),
+            ("theta", model.get("theta"), f["hFacC"], f["maskInC"], f["rA"], f["drF"])):
         st = mon_stats(g, arr, hf, mask, area, dr)
         for k, v in st.items():
             out["dynstat_%s_%s" % (name, k)] = float(v)

@@ -1,0 +1,136 @@
+"""GPU parity of the 3-D path (tutorial_baroclinic_gyre: 4 tiles of 31x31x15 on a
+spherical-polar grid, linear EOS, IVDC, GAD C2 tracer advection, implicit
+vertical diffusion, exactConserv) through the C-ABI.
+
+Bars:
+  * DO_OCEANIC_PHYS + THERMODYNAMICS and DYNAMICS (CALC_PHI_HYD, metric terms):
+    bit-exact against the oracle from the same state (interior points for the
+    tracer fields, whose halo the end-of-step EXCH refills);
+  * CG2D on the 4-tile operator: same iterations, residual within 1e-12;
+  * 10 steps against results/output.txt: cg2d_iters identical every step, >= 11
+    testreport digits on the check list (cg2d_init_res, theta/uvel/vvel min,
+    max, sd), >= 10 on the other dynstat values; *_mean not asserted
+    (roundoff-level means of zero-mean fields).
+"""
+import json
+import os
+
+import numpy as np
+import pytest
+
+from conftest import digits
+
+pytestmark = pytest.mark.gpu
+
+F3 = ("uVel", "vVel", "wVel", "theta", "gU", "gV", "guNm1", "gvNm1", "gtNm1", "rhoInSitu", "IVDConvCount")
+F2 = ("etaN", "etaH", "surfaceForcingT")
+
+
+def _stepped_oracle(n):
+    from mitgcm_amd import configs
+    from oracle.harness import oracle_from_config
+    o, g = oracle_from_config(configs.baroclinic_gyre)
+    for _ in range(n):
+        o.forward_step()
+    return o, g
+
+
+def _model_from_oracle(o, g, names):
+    from mitgcm_amd import configs
+    from mitgcm_amd._lib import lib
+    m = configs.make_model(configs.baroclinic_gyre)
+    for n in names:
+        m.put(n, np.array(o.arr(n)))
+    lib().mgcm_set_param(m.h, b"myIter", float(o.get("myIter")))
+    return m
+
+
+def test_thermodynamics_bitexact_vs_oracle():
+    o, g = _stepped_oracle(3)
+    # a warm anomaly under the surface level: statically unstable columns, so
+    # the IVDC branch (convective kappa) is exercised
+    o.arr("theta")[:, 1, 10:16, 8:20] += 12.0
+    m = _model_from_oracle(o, g, ("uVel", "vVel", "wVel", "theta", "gtNm1", "etaN"))
+    m.thermodynamics()
+    o.L.oracle_oceanic_phys(o.h)
+    o.L.oracle_thermodynamics(o.h)
+    inner = (slice(None), slice(None)) + g.sl(1, g.sNx, 1, g.sNy)
+    for n in ("rhoInSitu", "IVDConvCount"):
+        assert np.array_equal(m.get(n), np.array(o.arr(n))), n
+    assert np.array_equal(m.get("surfaceForcingT"), np.array(o.arr("surfaceForcingT")))
+    for n in ("theta", "gtNm1"):
+        dev, ref = m.get(n)[inner], np.array(o.arr(n))[inner]
+        assert np.array_equal(dev, ref), (n, np.abs(dev - ref).max())
+    assert np.array(o.arr("IVDConvCount")).sum() > 0   # the convective branch is exercised
+    m.close()
+
+
+def test_dynamics_3d_bitexact_vs_oracle():
+    o, g = _stepped_oracle(3)
+    # DO_OCEANIC_PHYS first so rhoInSitu is that of the current theta
+    o.L.oracle_oceanic_phys(o.h)
+    m = _model_from_oracle(o, g, ("uVel", "vVel", "wVel", "guNm1", "gvNm1", "etaN", "rhoInSitu"))
+    m.dynamics()
+    o.L.oracle_dynamics(o.h)
+    for n in ("gU", "gV", "guNm1", "gvNm1"):
+        dev, ref = m.get(n), np.array(o.arr(n))
+        assert np.array_equal(dev, ref), (n, np.abs(dev - ref).max())
+    m.close()
+
+
+def test_cg2d_four_tiles_vs_oracle():
+    o, g = _stepped_oracle(0)
+    from mitgcm_amd import configs
+    m = configs.make_model(configs.baroclinic_gyre)
+    rng = np.random.default_rng(5)
+    b = np.zeros((g.nTiles, g.ny, g.nx))
+    inner = g.sl(1, g.sNx, 1, g.sNy)
+    for t in range(g.nTiles):
+        b[t][inner] = rng.standard_normal((g.sNy, g.sNx)) * g.f["maskInC"][t][inner]
+    x0 = np.zeros_like(b)
+    xo, fo, mo, lo, ito, imo = o.cg2d(b, x0, 1000, -1)
+    xd, fd, md, ld, itd, imd = m.cg2d(b, x0, 1000, -1)
+    assert itd == ito and abs(fd - fo) <= 1e-12 * abs(fo)
+    sc = max(np.abs(xo[t][inner]).max() for t in range(g.nTiles))
+    assert max(np.abs(xd[t][inner] - xo[t][inner]).max() for t in range(g.nTiles)) <= 1e-12 * sc
+    m.close()
+
+
+def test_baroclinic_10_steps_vs_reference_output(golden_dir):
+    from mitgcm_amd import configs
+    from mitgcm_amd.model import dynstat
+    gold = json.load(open(os.path.join(golden_dir, "tutorial_baroclinic_gyre", "monitor.json")))
+    m = configs.make_model(configs.baroclinic_gyre)
+    worst = {"check": (99.0, None), "other": (99.0, None)}
+    for n in range(1, 11):
+        m.forward_step(1)
+        r = m.solve_stats()
+        r.update(dynstat(m))
+        gs = gold[n]
+        assert r["cg2d_iters"] == gs["cg2d_iters"], (n, r["cg2d_iters"], gs["cg2d_iters"])
+        for k, v in r.items():
+            if k not in gs or k in ("cg2d_iters", "cg2d_last_res") or k.endswith("_mean"):
+                continue
+            cls = "check" if (k == "cg2d_init_res" or (k.split("_")[1] in ("uvel", "vvel", "theta", "salt")
+                                                       and not k.endswith("del2"))) else "other"
+            d = digits(v, gs[k])
+            if d < worst[cls][0]:
+                worst[cls] = (d, (n, k))
+    print("baroclinic gyre 10 steps: worst digits on the check list %.2f at %s; other %.2f at %s"
+          % (worst["check"] + worst["other"]))
+    assert worst["check"][0] >= 11.0, worst["check"]
+    assert worst["other"][0] >= 10.0, worst["other"]
+    m.close()
+
+
+def test_baroclinic_fields_vs_oracle_after_10_steps():
+    from mitgcm_amd import configs
+    o, g = _stepped_oracle(10)
+    m = configs.make_model(configs.baroclinic_gyre)
+    m.forward_step(10)
+    m.sync()
+    for n in ("uVel", "vVel", "wVel", "theta", "etaN"):
+        dev, ref = m.get(n), np.array(o.arr(n))
+        sc = np.abs(ref).max()
+        assert np.abs(dev - ref).max() <= 1e-10 * sc, (n, np.abs(dev - ref).max(), sc)
+    m.close()
