@@ -35,7 +35,8 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=20)
-    ap.add_argument("--config", default="tutorial_barotropic_gyre")
+    ap.add_argument("--config", default="tutorial_baroclinic_gyre",
+                    choices=["tutorial_baroclinic_gyre", "tutorial_barotropic_gyre"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--pmc-summary", default=os.path.join(ROOT, "profiles", "r01", "pmc_summary.json"),
@@ -43,11 +44,22 @@ def parse():
     return ap.parse_args()
 
 
-def cpu_baseline(seconds):
+WORKLOADS = {
+    "tutorial_baroclinic_gyre": "tutorial_baroclinic_gyre 62x62x15 (4 tiles of 31x31, spherical-polar), "
+                                "full FORWARD_STEP on device incl. THERMODYNAMICS (dt=1200 s)",
+    "tutorial_barotropic_gyre": "tutorial_barotropic_gyre 62x62x1, 1 tile, full FORWARD_STEP on device (dt=1200 s)",
+}
+
+
+def cpu_baseline(config, seconds):
     """Oracle (CPU restatement, 1 thread) timed on the same workload: as many
-    gyre steps as fit in ~`seconds` of CPU time, reported in model-days/s."""
-    from oracle.harness import gyre_oracle
-    o = gyre_oracle()
+    steps as fit in ~`seconds` of CPU time, reported in model-days/s."""
+    from mitgcm_amd import configs
+    from oracle.harness import gyre_oracle, oracle_from_config
+    if config == "tutorial_barotropic_gyre":
+        o = gyre_oracle()
+    else:
+        o, _ = oracle_from_config(configs.baroclinic_gyre)
     o.forward_step()  # warm
     n, t0 = 0, time.perf_counter()
     while time.perf_counter() - t0 < seconds:
@@ -55,8 +67,8 @@ def cpu_baseline(seconds):
         n += 1
     dt = time.perf_counter() - t0
     return {"value": n * 1200.0 / 86400.0 / dt, "unit": "model-days/s", "cores": 1, "kind": "port",
-            "sample": "%d FORWARD_STEPs of tutorial_barotropic_gyre 62x62x1 on the oracle "
-                      "(oracle/*.c, gcc -O2, 1 thread), %.1f s" % (n, dt)}
+            "sample": "%d FORWARD_STEPs of %s on the oracle (oracle/*.c, gcc -O2, 1 thread), %.1f s"
+                      % (n, config, dt)}
 
 
 def pmc_traffic(path, kernel_prefix):
@@ -87,9 +99,8 @@ def main():
     from mitgcm_amd import configs
     from mitgcm_amd.model import dynstat
 
-    if a.config != "tutorial_barotropic_gyre":
-        raise SystemExit("unknown --config %s" % a.config)
-    m = configs.make_model(configs.barotropic_gyre, device=local)
+    cfg = configs.baroclinic_gyre if a.config == "tutorial_baroclinic_gyre" else configs.barotropic_gyre
+    m = configs.make_model(cfg, device=local)
     g = m.g
     dt_clock = m.params["deltaTClock"]
     npts = g.nTiles * g.sNx * g.sNy
@@ -119,8 +130,8 @@ def main():
         elapsed = float(t.item())
     iters = [m.solve_stats(back=b)["cg2d_iters"] for b in range(a.steps)]
     cg_ms, cg_n = m.kernel_ms("cg2d")
-    kern = {k: m.kernel_ms(k) for k in ("mom_step", "sfp_rhs", "cg2d", "exchange", "eta_update", "correction",
-                                         "continuity")}
+    kern = {k: m.kernel_ms(k) for k in ("oceanic_phys", "temp_step", "mom_step", "sfp_rhs", "cg2d", "exchange",
+                                         "eta_update", "correction", "continuity")}
     m.kernel_timing(False)
     # sanity: the solution is finite and the solver converged every step
     stats = m.solve_stats()
@@ -145,10 +156,9 @@ def main():
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "f64",
-        "data": "reference input fields of verification/tutorial_barotropic_gyre (bathy.bin, windx_cosy.bin), "
-                "cold start",
-        "config": {"workload": "tutorial_barotropic_gyre 62x62x1, 1 tile per GPU, full FORWARD_STEP on device "
-                               "(dt=1200 s); replicas only",
+        "data": "reference input fields of verification/%s (bathy, wind%s), cold start"
+                % (a.config, ", SST_relax" if a.config == "tutorial_baroclinic_gyre" else ""),
+        "config": {"workload": WORKLOADS[a.config] + "; replicas only",
                    "tiles_per_gpu": g.nTiles, "points_per_tile": [g.sNx, g.sNy, g.Nr],
                    "parallelism": "replicas%d" % world},
         "cg2d_iters_per_s": cg2d_iters_per_s,
@@ -162,7 +172,7 @@ def main():
                      "bytes_per_launch": bytes_per_launch, "launch_ms": cg_ms, "launches": cg_n},
     }
     if rank == 0 and not a.no_cpu_baseline:
-        out["cpu_baseline"] = cpu_baseline(a.cpu_seconds)
+        out["cpu_baseline"] = cpu_baseline(a.config, a.cpu_seconds)
     if rank == 0:
         print(json.dumps(out), flush=True)
     m.close()

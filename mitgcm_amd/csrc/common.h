@@ -54,6 +54,7 @@ struct Fields {
   const double *fu, *fv;
   double *etaH, *surfaceForcingT, *rhoInSitu, *IVDConvCount, *gtNm1;
   double *thetaNext, *gTscr, *cpScr;   // tracer ping-pong buffer and per-column scratch
+  double *phiHydC;                     // CALC_PHI_HYD output at cell centres (k_phi_hyd)
   // solver work
   double *cg2d_b, *cg2d_x;
 };

@@ -4,13 +4,14 @@
 //            pkg/mom_fluxform/mom_fluxform.F:42-1064,
 //            model/src/timestep.F:10-429, model/src/adams_bashforth2.F:6-92.
 //
-// One thread owns one (i,j) column of one tile and marches k = 1..Nr, carrying
-// the vertical advective flux of the level above in a register (the
-// fVerU/fVerV(kUp/kDown) ping-pong of dynamics.F:428-431).  Face fluxes that
-// the reference stores in 2-D scratch arrays (fZon, fMer, ...) are re-derived
-// from the neighbours' state with the same expression and operand order, so a
-// column's result is bit-identical to the loop-nest form (compiled with
-// -ffp-contract=off).  The kernel is HBM/latency bound (≈1 flop/B): no MFMA.
+// k_phi_hyd integrates CALC_PHI_HYD down each column (a k-scan, one thread per
+// column) into phiHydC.  k_mom_step then runs one thread per (i,j,k) point: the
+// vertical advective fluxes of both faces of the level (the fVerU/fVerV(kUp/kDown)
+// ping-pong of dynamics.F:428-431) and every horizontal face flux that the
+// reference keeps in 2-D scratch arrays (fZon, fMer, ...) are re-derived from the
+// neighbours' state with the same expression and operand order, so each point is
+// bit-identical to the loop-nest form (compiled with -ffp-contract=off).  The
+// kernel is HBM/latency bound (about 1 flop/B): no MFMA.
 #include "common.h"
 
 namespace mgcm {
@@ -24,10 +25,32 @@ __device__ __forceinline__ double hfacz(const Dims &d, const Fields &f, int i, i
   return h;
 }
 
+// CALC_PHI_HYD (calc_phi_hyd.F:175-327, OCEANIC, integr_GeoPot = 2, uniformFreeSurfLev,
+// gravFac = 1, alphaRho = rhoInSitu) on the dynamics range iMin..iMax = 0..sNx+1.
+__global__ void __launch_bounds__(256) k_phi_hyd(Dims d, Params p, Fields f) {
+  const int i = (int)(blockIdx.x * blockDim.x + threadIdx.x);
+  const int j = (int)(blockIdx.y * blockDim.y + threadIdx.y);
+  const int t = (int)blockIdx.z;
+  if (i > d.sNx + 1 || j > d.sNy + 1) return;
+  const double recip_rhoConst = 1.0 / p.rhoConst;
+  double phF = 0.0;
+  for (int k = 1; k <= d.Nr; k++) {
+    double dRlocM = 0.5 * f.drC[k - 1];
+    if (k == 1) dRlocM = f.rF[0] - f.rC[0];
+    const double dRlocP = (k == d.Nr) ? (f.rC[k - 1] - f.rF[k]) : 0.5 * f.drC[k];
+    const long q3 = MG_I3(d, i, j, k, t);
+    const double a = f.rhoInSitu[q3];
+    const double phC = phF + dRlocM * p.gravity * a * recip_rhoConst;
+    phF = phC + dRlocP * p.gravity * a * recip_rhoConst;
+    f.phiHydC[q3] = phC;
+  }
+}
+
 __global__ void __launch_bounds__(256) k_mom_step(Dims d, Params p, Fields f, const int *iterPtr) {
   const int i = (int)(blockIdx.x * blockDim.x + threadIdx.x) + 1 - d.OLx;
   const int j = (int)(blockIdx.y * blockDim.y + threadIdx.y) + 1 - d.OLy;
-  const int t = (int)blockIdx.z;
+  const int t = (int)blockIdx.z / d.Nr;
+  const int k = (int)blockIdx.z % d.Nr + 1;
   if (i > d.sNx + d.OLx || j > d.sNy + d.OLy) return;
   const int Nr = d.Nr;
   const int myIter = *iterPtr;
@@ -47,65 +70,46 @@ __global__ void __launch_bounds__(256) k_mom_step(Dims d, Params p, Fields f, co
 #define G2(a, ii, jj) f.a[MG_I2(d, ii, jj, t)]
 #define G3(a, ii, jj, kk) f.a[MG_I3(d, ii, jj, kk, t)]
 
-  // CALC_PHI_HYD (calc_phi_hyd.F:175-327, OCEANIC, integr_GeoPot = 2, uniformFreeSurfLev):
-  // phiHydF is integrated down this column and the west / south neighbours',
-  // which CALC_GRAD_PHI_HYD differences (calc_grad_phi_hyd.F:152-171).
-  double phF = 0.0, phFw = 0.0, phFs = 0.0;
-  const double recip_rhoConst = 1.0 / p.rhoConst;
-  double fVerUkm = 0.0, fVerVkm = 0.0;
-  if (inner && p.momAdvection) {
-    // MOM_CALC_RTRANS(k=1) + MOM_U/V_ADV_WU/WV(k=1): free-surface flux (mom_fluxform.F:384-417)
-    const double rTU = 0.5 * (W(i - 1, j, 1) * G2(rA, i - 1, j) + W(i, j, 1) * G2(rA, i, j));
-    const double rTV = 0.5 * (W(i, j - 1, 1) * G2(rA, i, j - 1) + W(i, j, 1) * G2(rA, i, j));
-    fVerUkm = rTU * U(i, j, 1);
-    fVerVkm = rTV * V(i, j, 1);
-  }
+  // vertical advective flux of momentum through the top of level kk (fVerU/V(kUp)):
+  // MOM_CALC_RTRANS + MOM_U/V_ADV_WU/WV (mom_fluxform.F:384-424), select_rStar = 0
+  auto fverU = [&](int kk) -> double {
+    if (kk > Nr) return 0.0;
+    const double rTU = 0.5 * (W(i - 1, j, kk) * G2(rA, i - 1, j) + W(i, j, kk) * G2(rA, i, j));
+    if (kk == 1) return rTU * U(i, j, 1);
+    double fu_ = rTU * (0.5 * (U(i, j, kk) + U(i, j, kk - 1)));
+    fu_ = fu_ + 0.25 * (W(i, j, kk) * G2(rA, i, j) * (G3(maskC, i, j, kk) - G3(maskC, i, j, kk - 1)) +
+                        W(i - 1, j, kk) * G2(rA, i - 1, j) * (G3(maskC, i - 1, j, kk) - G3(maskC, i - 1, j, kk - 1))) *
+                    U(i, j, kk);
+    return fu_;
+  };
+  auto fverV = [&](int kk) -> double {
+    if (kk > Nr) return 0.0;
+    const double rTV = 0.5 * (W(i, j - 1, kk) * G2(rA, i, j - 1) + W(i, j, kk) * G2(rA, i, j));
+    if (kk == 1) return rTV * V(i, j, 1);
+    double fv_ = rTV * (0.5 * (V(i, j, kk) + V(i, j, kk - 1)));
+    fv_ = fv_ + 0.25 * (W(i, j, kk) * G2(rA, i, j) * (G3(maskC, i, j, kk) - G3(maskC, i, j, kk - 1)) +
+                        W(i, j - 1, kk) * G2(rA, i, j - 1) * (G3(maskC, i, j - 1, kk) - G3(maskC, i, j - 1, kk - 1))) *
+                    V(i, j, kk);
+    return fv_;
+  };
 
-  for (int k = 1; k <= Nr; k++) {
+  {
     const double drF = f.drF[k - 1], recip_drF = f.recip_drF[k - 1];
     double gU = 0.0, gV = 0.0, guDiss = 0.0, gvDiss = 0.0;
-    double fVerUkp = 0.0, fVerVkp = 0.0;
     double dPhiHydX = 0.0, dPhiHydY = 0.0;
     if (inner) {
-      double dRlocM = 0.5 * f.drC[k - 1];
-      if (k == 1) dRlocM = f.rF[0] - f.rC[0];
-      const double dRlocP = (k == Nr) ? (f.rC[k - 1] - f.rF[k]) : 0.5 * f.drC[k];
-      const double a0 = f.rhoInSitu[MG_I3(d, i, j, k, t)];
-      const double phC = phF + dRlocM * p.gravity * a0 * recip_rhoConst;
-      phF = phC + dRlocP * p.gravity * a0 * recip_rhoConst;
-      if (i >= 1) {
-        const double aw = f.rhoInSitu[MG_I3(d, i - 1, j, k, t)];
-        const double phCw = phFw + dRlocM * p.gravity * aw * recip_rhoConst;
-        phFw = phCw + dRlocP * p.gravity * aw * recip_rhoConst;
-        dPhiHydX = G2(recip_dxC, i, j) * ((phC + 0.0) - (phCw + 0.0));
-      }
-      if (j >= 1) {
-        const double as = f.rhoInSitu[MG_I3(d, i, j - 1, k, t)];
-        const double phCs = phFs + dRlocM * p.gravity * as * recip_rhoConst;
-        phFs = phCs + dRlocP * p.gravity * as * recip_rhoConst;
-        dPhiHydY = G2(recip_dyC, i, j) * ((phC + 0.0) - (phCs + 0.0));
-      }
+      // CALC_GRAD_PHI_HYD (calc_grad_phi_hyd.F:152-171), phi0surf = 0
+      const double phC = G3(phiHydC, i, j, k);
+      if (i >= 1) dPhiHydX = G2(recip_dxC, i, j) * ((phC + 0.0) - (G3(phiHydC, i - 1, j, k) + 0.0));
+      if (j >= 1) dPhiHydY = G2(recip_dyC, i, j) * ((phC + 0.0) - (G3(phiHydC, i, j - 1, k) + 0.0));
     }
     if (inner) {
       const double rhFacW = G3(recip_hFacW, i, j, k), rhFacS = G3(recip_hFacS, i, j, k);
       const double hZ = hfacz(d, f, i, j, k, t);
       // ---------------- advection (mom_u_adv_uu/vu/wu.F, mom_v_adv_uv/vv/wv.F)
       if (p.momAdvection) {
-        if (k + 1 <= Nr) {
-          const int kk = k + 1;
-          const double rTU = 0.5 * (W(i - 1, j, kk) * G2(rA, i - 1, j) + W(i, j, kk) * G2(rA, i, j));
-          const double rTV = 0.5 * (W(i, j - 1, kk) * G2(rA, i, j - 1) + W(i, j, kk) * G2(rA, i, j));
-          double fu_ = rTU * (0.5 * (U(i, j, kk) + U(i, j, kk - 1)));
-          fu_ = fu_ + 0.25 * (W(i, j, kk) * G2(rA, i, j) * (G3(maskC, i, j, kk) - G3(maskC, i, j, kk - 1)) +
-                              W(i - 1, j, kk) * G2(rA, i - 1, j) * (G3(maskC, i - 1, j, kk) - G3(maskC, i - 1, j, kk - 1))) *
-                          U(i, j, kk);
-          fVerUkp = fu_;
-          double fv_ = rTV * (0.5 * (V(i, j, kk) + V(i, j, kk - 1)));
-          fv_ = fv_ + 0.25 * (W(i, j, kk) * G2(rA, i, j) * (G3(maskC, i, j, kk) - G3(maskC, i, j, kk - 1)) +
-                              W(i, j - 1, kk) * G2(rA, i, j - 1) * (G3(maskC, i, j - 1, kk) - G3(maskC, i, j - 1, kk - 1))) *
-                          V(i, j, kk);
-          fVerVkp = fv_;
-        }
+        const double fVerUkm = fverU(k), fVerUkp = fverU(k + 1);
+        const double fVerVkm = fverV(k), fVerVkp = fverV(k + 1);
         // uTrans / vTrans (mom_fluxform.F:287-327)
 #define UTR(ii, jj) (U(ii, jj, k) * (G2(dyG, ii, jj) * drF * G3(hFacW, ii, jj, k)))
 #define VTR(ii, jj) (V(ii, jj, k) * (G2(dxG, ii, jj) * drF * G3(hFacS, ii, jj, k)))
@@ -276,8 +280,6 @@ __global__ void __launch_bounds__(256) k_mom_step(Dims d, Params p, Fields f, co
     }
     f.gU[q3] = gU;
     f.gV[q3] = gV;
-    fVerUkm = fVerUkp;
-    fVerVkm = fVerVkp;
   }
 #undef U
 #undef V
@@ -287,8 +289,10 @@ __global__ void __launch_bounds__(256) k_mom_step(Dims d, Params p, Fields f, co
 }
 
 hipError_t launch_mom_step(const Dims &d, const Params &p, const Fields &f, const int *iterPtr, hipStream_t s) {
+  dim3 pblk(64, 4, 1), pgrd((d.sNx + 2 + 63) / 64, (d.sNy + 2 + 3) / 4, d.nTiles);
+  hipLaunchKernelGGL(k_phi_hyd, pgrd, pblk, 0, s, d, p, f);
   dim3 blk(64, 4, 1);
-  dim3 grd((d.nx + 63) / 64, (d.ny + 3) / 4, d.nTiles);
+  dim3 grd((d.nx + 63) / 64, (d.ny + 3) / 4, d.nTiles * d.Nr);
   hipLaunchKernelGGL(k_mom_step, grd, blk, 0, s, d, p, f, iterPtr);
   return hipGetLastError();
 }

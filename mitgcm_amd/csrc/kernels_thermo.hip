@@ -11,15 +11,15 @@
 //                   (gad_implicit_r.F:96-140) solved by the Thomas sweep of
 //                   SOLVE_TRIDIAGONAL (solve_tridiagonal.F, default branch), CYCLE_TRACER.
 //
-// One thread owns one interior (i,j) column of one tile.  The RHS pass marches
-// k = Nr..1 carrying the vertical flux of the face below and rTrans(k+1) in
-// registers (the fVerT(kUp/kDown) ping-pong of temp_integrate.F); horizontal
-// face fluxes are recomputed from the neighbours' state with the reference's
-// operand order (bit-exact under -ffp-contract=off).  The new theta goes to the
-// other buffer of a ping-pong pair (neighbours still read the old one); gT and
-// the Thomas coefficients live in per-column scratch that the same thread
-// writes and re-reads (L2-resident).  Only the interior is produced: the halo
-// of theta is refilled by the end-of-step EXCH (do_fields_blocking_exchanges.F).
+// k_temp_rhs runs one thread per interior (i,j,k) point: both vertical faces of
+// the level (the fVerT(kUp/kDown) ping-pong of temp_integrate.F) and the four
+// horizontal faces are recomputed from the neighbours' state with the
+// reference's operand order (bit-exact under -ffp-contract=off).  k_temp_impl
+// then runs the implicit vertical solve one thread per column.  The new theta
+// goes to the other buffer of a ping-pong pair (neighbours still read the old
+// one); the Thomas coefficients live in per-column scratch (L2-resident).  Only
+// the interior is produced: the halo of theta is refilled by the end-of-step
+// EXCH (do_fields_blocking_exchanges.F).
 #include "common.h"
 
 namespace mgcm {
@@ -56,10 +56,14 @@ __global__ void __launch_bounds__(256) k_oceanic_phys(Dims d, Params p, Fields f
   (void)rhoUp;
 }
 
-__global__ void __launch_bounds__(256) k_temp_step(Dims d, Params p, Fields f, const int *iterPtr) {
+// GAD_CALC_RHS + forcing + AB2 + TIMESTEP_TRACER for one interior (i,j,k) point:
+// writes gtNm1 and gTscr = theta + dTtracer*gT (the right-hand side of the
+// implicit vertical solve).
+__global__ void __launch_bounds__(256) k_temp_rhs(Dims d, Params p, Fields f, const int *iterPtr) {
   const int i = (int)(blockIdx.x * blockDim.x + threadIdx.x) + 1;
   const int j = (int)(blockIdx.y * blockDim.y + threadIdx.y) + 1;
-  const int t = (int)blockIdx.z;
+  const int t = (int)blockIdx.z / d.Nr;
+  const int k = (int)blockIdx.z % d.Nr + 1;
   if (i > d.sNx || j > d.sNy) return;
   const int Nr = d.Nr;
   const int myIter = *iterPtr;
@@ -71,8 +75,9 @@ __global__ void __launch_bounds__(256) k_temp_step(Dims d, Params p, Fields f, c
 #define T3(ii, jj, kk) T[MG_I3(d, ii, jj, kk, t)]
 #define G2(a, ii, jj) f.a[MG_I2(d, ii, jj, t)]
 #define G3(a, ii, jj, kk) f.a[MG_I3(d, ii, jj, kk, t)]
-  // face flux at west face of column ii (fZon(ii)), at level k
-  auto fzon = [&](int ii, int k, double drF) {
+  const double drF = f.drF[k - 1];
+  // west / south face fluxes of the column (fZon, fMer): GAD_C2_ADV_X/Y + GAD_DIFF_X/Y
+  auto fzon = [&](int ii) {
     const double xA = G2(dyG, ii, j) * drF * G3(hFacW, ii, j, k);
     double fz = 0.0;
     if (p.tempAdvection) fz = fz + (G3(uVel, ii, j, k) * xA) * (T3(ii, j, k) + T3(ii - 1, j, k)) * 0.5;
@@ -80,7 +85,7 @@ __global__ void __launch_bounds__(256) k_temp_step(Dims d, Params p, Fields f, c
     if (p.diffKhT != 0.0) df = -p.diffKhT * xA * G2(recip_dxC, ii, j) * (T3(ii, j, k) - T3(ii - 1, j, k));
     return fz + df;
   };
-  auto fmer = [&](int jj, int k, double drF) {
+  auto fmer = [&](int jj) {
     const double yA = G2(dxG, i, jj) * drF * G3(hFacS, i, jj, k);
     double fm = 0.0;
     if (p.tempAdvection) fm = fm + (G3(vVel, i, jj, k) * yA) * (T3(i, jj, k) + T3(i, jj - 1, k)) * 0.5;
@@ -88,47 +93,57 @@ __global__ void __launch_bounds__(256) k_temp_step(Dims d, Params p, Fields f, c
     if (p.diffKhT != 0.0) df = -p.diffKhT * yA * G2(recip_dyC, i, jj) * (T3(i, jj, k) - T3(i, jj - 1, k));
     return fm + df;
   };
-
-  // ---- RHS pass, k = Nr..1 (temp_integrate.F k-loop)
-  double fVerDn = 0.0;   // fVerT(kDown): flux through the bottom face of level k
-  double rTransKp = 0.0; // rTrans of level k+1 (calc_adv_flow.F rTransKp = rTrans)
-  for (int k = Nr; k >= 1; k--) {
-    const long q3 = MG_I3(d, i, j, k, t);
-    const double drF = f.drF[k - 1];
-    const double Tk = T[q3];
-    // CALC_ADV_FLOW at (i,j),(i+1,j),(i,j+1)
-    const double uT0 = G3(uVel, i, j, k) * (G2(dyG, i, j) * drF * G3(hFacW, i, j, k));
-    const double uT1 = G3(uVel, i + 1, j, k) * (G2(dyG, i + 1, j) * drF * G3(hFacW, i + 1, j, k));
-    const double vT0 = G3(vVel, i, j, k) * (G2(dxG, i, j) * drF * G3(hFacS, i, j, k));
-    const double vT1 = G3(vVel, i, j + 1, k) * (G2(dxG, i, j + 1) * drF * G3(hFacS, i, j + 1, k));
-    double rTrans = 0.0, fVerUp = 0.0;
-    if (k > 1) {
-      const double maskUp = G3(maskC, i, j, k - 1) * G3(maskC, i, j, k);
-      rTrans = G3(wVel, i, j, k) * rA * maskUp;
-      if (p.tempAdvection) {   // GAD_C2_ADV_R, kM1 = k-1
-        const double wT = G3(maskC, i, j, k - 1) * rTrans * (Tk + T3(i, j, k - 1)) * 0.5;
-        fVerUp = fVerUp + wT * maskInC;
-      }
+  // CALC_ADV_FLOW rTrans of level kk (0 at the surface and below the bottom level)
+  auto rtrans = [&](int kk) {
+    if (kk <= 1 || kk > Nr) return 0.0;
+    const double maskUp = G3(maskC, i, j, kk - 1) * G3(maskC, i, j, kk);
+    return G3(wVel, i, j, kk) * rA * maskUp;
+  };
+  // fVerT through the top face of level kk: GAD_C2_ADV_R (k >= 2) + explicit diffusive flux (0)
+  auto fvert = [&](int kk, double rTr) {
+    double fv = 0.0;
+    if (kk >= 2 && kk <= Nr && p.tempAdvection) {
+      const double wT = G3(maskC, i, j, kk - 1) * rTr * (T3(i, j, kk) + T3(i, j, kk - 1)) * 0.5;
+      fv = fv + wT * maskInC;
     }
-    fVerUp = fVerUp + 0.0;   // implicitDiffusion: explicit vertical diffusive flux is 0
-    const double fZi = fzon(i, k, drF), fZe = fzon(i + 1, k, drF);
-    const double fMi = fmer(j, k, drF), fMn = fmer(j + 1, k, drF);
-    double gT = 0.0 - f.recip_hFacC[q3] * f.recip_drF[k - 1] * recip_rA *
-                          ((fZe - fZi) * maskInC + (fMn - fMi) * maskInC + (fVerDn - fVerUp) * p.rkSign -
-                           Tk * ((uT1 - uT0) * advFac + (vT1 - vT0) * advFac + (rTransKp - rTrans) * rAdvFac) * maskInC);
-    double gtForc = 0.0;
-    if (p.tempForcing && k == 1) gtForc = gtForc + f.surfaceForcingT[q] * f.recip_drF[0] * f.recip_hFacC[q3];
-    gT = gT + gtForc;
-    // ADAMS_BASHFORTH2(k)
-    const double ab = abFac * (gT - f.gtNm1[q3]);
-    f.gtNm1[q3] = gT;
-    gT = gT + ab;
-    // TIMESTEP_TRACER
-    f.gTscr[q3] = Tk + p.deltaTtracer * gT;
-    fVerDn = fVerUp;
-    rTransKp = rTrans;
-  }
-  // ---- GAD_IMPLICIT_R + SOLVE_TRIDIAGONAL (Thomas, forward k = 1..Nr)
+    return fv + 0.0;
+  };
+  const long q3 = MG_I3(d, i, j, k, t);
+  const double Tk = T[q3];
+  const double uT0 = G3(uVel, i, j, k) * (G2(dyG, i, j) * drF * G3(hFacW, i, j, k));
+  const double uT1 = G3(uVel, i + 1, j, k) * (G2(dyG, i + 1, j) * drF * G3(hFacW, i + 1, j, k));
+  const double vT0 = G3(vVel, i, j, k) * (G2(dxG, i, j) * drF * G3(hFacS, i, j, k));
+  const double vT1 = G3(vVel, i, j + 1, k) * (G2(dxG, i, j + 1) * drF * G3(hFacS, i, j + 1, k));
+  const double rTrans = rtrans(k), rTransKp = rtrans(k + 1);
+  const double fVerUp = fvert(k, rTrans), fVerDn = fvert(k + 1, rTransKp);
+  const double fZi = fzon(i), fZe = fzon(i + 1);
+  const double fMi = fmer(j), fMn = fmer(j + 1);
+  double gT = 0.0 - f.recip_hFacC[q3] * f.recip_drF[k - 1] * recip_rA *
+                        ((fZe - fZi) * maskInC + (fMn - fMi) * maskInC + (fVerDn - fVerUp) * p.rkSign -
+                         Tk * ((uT1 - uT0) * advFac + (vT1 - vT0) * advFac + (rTransKp - rTrans) * rAdvFac) * maskInC);
+  double gtForc = 0.0;
+  if (p.tempForcing && k == 1) gtForc = gtForc + f.surfaceForcingT[q] * f.recip_drF[0] * f.recip_hFacC[q3];
+  gT = gT + gtForc;
+  // ADAMS_BASHFORTH2(k)
+  const double ab = abFac * (gT - f.gtNm1[q3]);
+  f.gtNm1[q3] = gT;
+  gT = gT + ab;
+  // TIMESTEP_TRACER
+  f.gTscr[q3] = Tk + p.deltaTtracer * gT;
+#undef T3
+#undef G2
+#undef G3
+}
+
+// GAD_IMPLICIT_R (implicitDiffusion) + SOLVE_TRIDIAGONAL (Thomas) + CYCLE_TRACER,
+// one thread per interior column; writes the new theta into thetaNext.
+__global__ void __launch_bounds__(256) k_temp_impl(Dims d, Params p, Fields f) {
+  const int i = (int)(blockIdx.x * blockDim.x + threadIdx.x) + 1;
+  const int j = (int)(blockIdx.y * blockDim.y + threadIdx.y) + 1;
+  const int t = (int)blockIdx.z;
+  if (i > d.sNx || j > d.sNy) return;
+  const int Nr = d.Nr;
+#define G3(a, ii, jj, kk) f.a[MG_I3(d, ii, jj, kk, t)]
   double cpPrev = 0.0, ypPrev = 0.0;
   for (int k = 1; k <= Nr; k++) {
     const long q3 = MG_I3(d, i, j, k, t);
@@ -155,7 +170,6 @@ __global__ void __launch_bounds__(256) k_temp_step(Dims d, Params p, Fields f, c
     f.cpScr[q3] = cp;
     cpPrev = cp; ypPrev = yp;
   }
-  // back substitution k = Nr..1, CYCLE_TRACER into the other theta buffer
   double below = 0.0;
   for (int k = Nr; k >= 1; k--) {
     const long q3 = MG_I3(d, i, j, k, t);
@@ -163,8 +177,6 @@ __global__ void __launch_bounds__(256) k_temp_step(Dims d, Params p, Fields f, c
     f.thetaNext[q3] = v;
     below = v;
   }
-#undef T3
-#undef G2
 #undef G3
 }
 
@@ -175,8 +187,10 @@ hipError_t launch_oceanic_phys(const Dims &d, const Params &p, const Fields &f, 
 }
 
 hipError_t launch_temp_step(const Dims &d, const Params &p, const Fields &f, const int *iterPtr, hipStream_t s) {
-  dim3 blk(64, 4, 1), grd((d.sNx + 63) / 64, (d.sNy + 3) / 4, d.nTiles);
-  hipLaunchKernelGGL(k_temp_step, grd, blk, 0, s, d, p, f, iterPtr);
+  dim3 blk(64, 4, 1), grd((d.sNx + 63) / 64, (d.sNy + 3) / 4, d.nTiles * d.Nr);
+  hipLaunchKernelGGL(k_temp_rhs, grd, blk, 0, s, d, p, f, iterPtr);
+  dim3 cgrd((d.sNx + 63) / 64, (d.sNy + 3) / 4, d.nTiles);
+  hipLaunchKernelGGL(k_temp_impl, cgrd, blk, 0, s, d, p, f);
   return hipGetLastError();
 }
 

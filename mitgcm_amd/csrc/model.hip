@@ -79,7 +79,7 @@ static const FieldDesc FIELDS[] = {
     FD(uVel, F3D), FD(vVel, F3D), FD(wVel, F3D), FD(theta, F3D), FD(salt, F3D), FD(etaN, F2D),
     FD(gU, F3D), FD(gV, F3D), FD(guNm1, F3D), FD(gvNm1, F3D), FD(fu, F2D), FD(fv, F2D),
     FD(etaH, F2D), FD(surfaceForcingT, F2D), FD(rhoInSitu, F3D), FD(IVDConvCount, F3D), FD(gtNm1, F3D),
-    FD(thetaNext, F3D), FD(gTscr, F3D), FD(cpScr, F3D),
+    FD(thetaNext, F3D), FD(gTscr, F3D), FD(cpScr, F3D), FD(phiHydC, F3D),
     FD(cg2d_b, F2D), FD(cg2d_x, F2D),
 };
 #undef FD
