@@ -98,6 +98,41 @@ def baroclinic_gyre(nSx=2, nSy=2, data_dir=None, tempAdvScheme=2):
     return g, params, state
 
 
+def advect_xy(nSx=1, nSy=2):
+    """verification/advect_xy: 20x20x1 doubly-periodic cartesian box (10 km cells,
+    code/SIZE.h sNx=20, sNy=10, OL=3, nSy=2), momStepping=F, uniform u = v = 1 m/s
+    (code/ini_vel.F), a salt disc of +1 psu (code/ini_salt.F), saltAdvScheme=33
+    (DST3 flux-limited, multi-dimensional), deltaT=2500.  Only salt is stepped here
+    (theta uses scheme 80 in the reference and does not feed back)."""
+    Nx = Ny = 20
+    sNx, sNy = Nx // nSx, Ny // nSy
+    g = Grid(sNx, sNy, 3, 3, 1, nSx, nSy)
+    g.ini_vertical_grid([10.0e3])
+    g.ini_cartesian_grid(np.full(Nx, 10.0e3), np.full(Ny, 10.0e3), 0.0, 0.0)
+    g.ini_cori(0.0, 0.0, selectCoriMap=1)
+    g.ini_depths_masks(np.full((Ny, Nx), g.f["rF"][1]), hFacMin=1.0, hFacMinDr=0.0, gBaro=9.81)
+    g.ini_cg2d(2500.0, 2500.0, 1e-13)
+    params = dict(deltaTMom=2500.0, deltaTFreeSurf=2500.0, deltaTClock=2500.0, deltaTtracer=2500.0, abEps=0.1,
+                  rhoConst=999.8, gravity=9.81, gBaro=9.81, momStepping=0, tempStepping=0, saltStepping=1,
+                  saltAdvScheme=33, saltVertAdvScheme=33, multiDimAdvection=1, diffKhS=0.0, diffKrS=0.0,
+                  implicitDiffusion=0, ivdc_kappa=0.0, exactConserv=0, saltForcing=0, cg2dMaxIters=100)
+    u = np.ones((g.nTiles, 1, g.ny, g.nx)) * g.f["maskW"]
+    v = np.ones((g.nTiles, 1, g.ny, g.nx)) * g.f["maskS"]
+    salt = np.full((g.nTiles, 1, g.ny, g.nx), 35.0)
+    rC = g.f["rC"][0]
+    from math import sqrt
+    for t in range(g.nTiles):
+        for J in range(g.ny):
+            for I in range(g.nx):
+                x, y = g.f["xC"][t, J, I], g.f["yC"][t, J, I]
+                rD = sqrt((x - 40.0e3) ** 2 + (y - 40.0e3) ** 2 + (rC + 50.0e3) ** 2)
+                if rD <= 60.0e3:
+                    salt[t, 0, J, I] = 35.0 + 1.0
+    state = {"uVel": u, "vVel": v, "salt": g.exch(salt), "theta": np.full_like(salt, 20.0),
+             "tRef": np.array([20.0]), "sRef": np.array([35.0])}
+    return g, params, state
+
+
 def make_model(cfg, device=0, **kw):
     g, params, state = cfg(**kw)
     m = Model(g, params, device=device)

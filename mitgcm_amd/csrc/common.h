@@ -33,6 +33,8 @@ struct Params {
   double recip_rSphere;
   int exactConserv, tempStepping, tempAdvection, tempForcing, implicitDiffusion, tempAdvScheme;
   int metricSphere;   // usingSphericalPolarGrid && selectMetricTerms >= 1
+  double diffKhS, diffKrS;
+  int saltStepping, saltAdvection, saltForcing, saltAdvScheme, multiDimAdvection, momStepping;
 };
 
 // Device pointers of every field the kernels touch.
@@ -55,6 +57,8 @@ struct Fields {
   double *etaH, *surfaceForcingT, *rhoInSitu, *IVDConvCount, *gtNm1;
   double *thetaNext, *gTscr, *cpScr;   // tracer ping-pong buffer and per-column scratch
   double *phiHydC;                     // CALC_PHI_HYD output at cell centres (k_phi_hyd)
+  double *saltNext, *gsNm1, *surfaceForcingS;
+  double *advScr1, *advScr2, *gAdv;     // multi-dim advection passes and its tendency
   // solver work
   double *cg2d_b, *cg2d_x;
 };
@@ -64,6 +68,16 @@ struct Fields {
 #define MG_I3(d, i, j, k, t)                                                                \
   ((long)((i) + (d).OLx - 1) + (long)((j) + (d).OLy - 1) * (d).nx + (long)((k) - 1) * (d).n2 + \
    (long)(t) * (d).n3)
+
+// One tracer of TEMP_INTEGRATE / SALT_INTEGRATE (temp_integrate.F, salt_integrate.F).
+struct TracerArgs {
+  const double *tr;     // tracer at the start of the step (halo-exchanged)
+  double *trNext;       // where CYCLE_TRACER writes the new tracer (ping-pong partner)
+  double *gNm1;         // AB2 history of the tendency
+  const double *sfc;    // surface forcing (surfaceForcingT/S), or null
+  double diffKh, diffKr, dT;
+  int advection, multiDim, useAB, forcing;
+};
 
 // Per-solve record written by the device CG2D (one slot per time step).
 struct SolveRecord {

@@ -34,7 +34,7 @@ hipError_t launch_correction(const Dims &, const Params &, const Fields &, hipSt
 hipError_t launch_continuity(const Dims &, const Fields &, hipStream_t);
 hipError_t launch_bump_counter(int *, int, hipStream_t);
 hipError_t launch_oceanic_phys(const Dims &, const Params &, const Fields &, hipStream_t);
-hipError_t launch_temp_step(const Dims &, const Params &, const Fields &, const int *, hipStream_t);
+hipError_t launch_tracer_step(const Dims &, const Params &, const Fields &, const TracerArgs &, const int *, hipStream_t);
 hipError_t launch_continuity_ec(const Dims &, const Params &, const Fields &, hipStream_t);
 hipError_t launch_copy(double *, const double *, long, hipStream_t);
 }  // namespace mgcm
@@ -79,7 +79,8 @@ static const FieldDesc FIELDS[] = {
     FD(uVel, F3D), FD(vVel, F3D), FD(wVel, F3D), FD(theta, F3D), FD(salt, F3D), FD(etaN, F2D),
     FD(gU, F3D), FD(gV, F3D), FD(guNm1, F3D), FD(gvNm1, F3D), FD(fu, F2D), FD(fv, F2D),
     FD(etaH, F2D), FD(surfaceForcingT, F2D), FD(rhoInSitu, F3D), FD(IVDConvCount, F3D), FD(gtNm1, F3D),
-    FD(thetaNext, F3D), FD(gTscr, F3D), FD(cpScr, F3D), FD(phiHydC, F3D),
+    FD(thetaNext, F3D), FD(gTscr, F3D), FD(cpScr, F3D), FD(phiHydC, F3D), FD(saltNext, F3D), FD(gsNm1, F3D),
+    FD(surfaceForcingS, F2D), FD(advScr1, F3D), FD(advScr2, F3D), FD(gAdv, F3D),
     FD(cg2d_b, F2D), FD(cg2d_x, F2D),
 };
 #undef FD
@@ -101,7 +102,8 @@ static const PDesc PARAMS[] = {
     PI_(implicitViscosity), PI_(cg2dMaxIters), PI_(cg2dUseMinResSol), PI_(cg2dNormaliseRHS), PI_(nIter0),
     PD(gravity), PD(gravitySign), PD(rhoNil), PD(tAlpha), PD(sBeta), PD(ivdc_kappa), PD(diffKhT), PD(diffKrT),
     PD(deltaTtracer), PI_(exactConserv), PI_(tempStepping), PI_(tempAdvection), PI_(tempForcing),
-    PI_(implicitDiffusion), PI_(tempAdvScheme),
+    PI_(implicitDiffusion), PI_(tempAdvScheme), PI_(saltStepping), PI_(saltAdvection), PI_(saltForcing),
+    PI_(saltAdvScheme), PD(diffKhS), PD(diffKrS), PI_(multiDimAdvection), PI_(momStepping),
 };
 #undef PD
 #undef PI_
@@ -344,6 +346,7 @@ mgcm_model *mgcm_create(int sNx, int sNy, int OLx, int OLy, int Nr, int nSx, int
   p.cg2dMaxIters = 150; p.cg2dNormaliseRHS = 1;
   p.gravity = 9.81; p.gravitySign = -1.0; p.rhoNil = 999.8; p.tAlpha = 2.0e-4; p.tempAdvection = 1;
   p.tempForcing = 1; p.tempAdvScheme = 2; p.implicitDiffusion = 0;
+  p.saltAdvection = 1; p.saltForcing = 1; p.saltAdvScheme = 2; p.multiDimAdvection = 1; p.momStepping = 1;
   if (hipStreamCreateWithFlags(&m->stream, hipStreamNonBlocking) != hipSuccess) {
     set_err("mgcm_create: stream");
     delete m;
@@ -406,7 +409,7 @@ int mgcm_set_param(mgcm_model *m, const char *name, double value) {
   // (inert) value; anything else is an explicit error, never silently ignored.
   static const char *inert[] = {"useBiharmonicVisc", "nonlinFreeSurf", "select_rStar",
                                 "useCDscheme", "vectorInvariantMomentum", "useNHMTerms",
-                                "saltStepping", "staggerTimeStep",
+                                "staggerTimeStep",
                                 "implicitFreeSurface", "useRealFreshWaterFlux", "useGMRedi"};
   for (auto *n : inert)
     if (!strcmp(n, name)) {
@@ -493,11 +496,15 @@ int mgcm_init(mgcm_model *m) {
   m->p.metricSphere = sph && ext("selectMetricTerms", 1.0) >= 1.0;
   m->p.recip_rSphere = sph ? 1.0 / ext("rSphere", 6370.0e3) : 0.0;   // ini_parms.F:1334
   if (ext("integr_GeoPot", 2.0) != 2.0) return set_err("mgcm_init: only integr_GeoPot = 2 is implemented");
-  if (m->p.tempStepping) {
-    if (m->p.tempAdvScheme != 2 || ext("tempVertAdvScheme", 2.0) != 2.0)
-      return set_err("mgcm_init: tempAdvScheme %d not implemented on the device yet", m->p.tempAdvScheme);
-    if (!m->p.implicitDiffusion) return set_err("mgcm_init: explicit vertical tracer diffusion not implemented yet");
-  }
+  // tracer advection schemes implemented on the device: 2 (C2, AB2) and 33 (DST3 flux-limited,
+  // multi-dimensional); the vertical scheme must match the horizontal one
+  auto okScheme = [&](int s, const char *vname) {
+    return (s == 2 || s == 33) && ext(vname, (double)s) == (double)s;
+  };
+  if (m->p.tempStepping && !okScheme(m->p.tempAdvScheme, "tempVertAdvScheme"))
+    return set_err("mgcm_init: tempAdvScheme %d not implemented on the device", m->p.tempAdvScheme);
+  if (m->p.saltStepping && !okScheme(m->p.saltAdvScheme, "saltVertAdvScheme"))
+    return set_err("mgcm_init: saltAdvScheme %d not implemented on the device", m->p.saltAdvScheme);
   int it0 = m->p.nIter0;
   HIPCHK(hipMemcpy(m->d_ctr, &it0, sizeof(int), hipMemcpyHostToDevice));
   // INI_PSURF (ini_psurf.F:84): etaH = etaN
@@ -533,13 +540,38 @@ int mgcm_dynamics(mgcm_model *m) {
   return 0;
 }
 
+static TracerArgs tracer_args(mgcm_model *m, bool salt) {
+  const Params &p = m->p;
+  TracerArgs a{};
+  const int scheme = salt ? p.saltAdvScheme : p.tempAdvScheme;
+  a.tr = salt ? m->f.salt : m->f.theta;
+  a.trNext = salt ? m->f.saltNext : m->f.thetaNext;
+  a.gNm1 = salt ? m->f.gsNm1 : m->f.gtNm1;
+  a.sfc = salt ? m->f.surfaceForcingS : m->f.surfaceForcingT;
+  a.diffKh = salt ? p.diffKhS : p.diffKhT;
+  a.diffKr = salt ? p.diffKrS : p.diffKrT;
+  a.dT = p.deltaTtracer;
+  a.advection = salt ? p.saltAdvection : p.tempAdvection;
+  a.forcing = salt ? p.saltForcing : p.tempForcing;
+  // gad_init_fixed.F:126-162: multi-dim advection for non-C2 schemes, AB2 on the tendency for C2
+  a.multiDim = p.multiDimAdvection && a.advection && scheme != 2;
+  a.useAB = scheme == 2;
+  return a;
+}
+
 int mgcm_thermodynamics(mgcm_model *m) {
   if (check_ready(m)) return -1;
-  if (!m->p.tempStepping) return 0;
+  if (!m->p.tempStepping && !m->p.saltStepping) return 0;
   // forward_step.F:656 DO_OCEANIC_PHYS, :732 THERMODYNAMICS (staggerTimeStep = F)
   TIMED(K_PHYS, launch_oceanic_phys(m->d, m->p, m->f, m->stream));
-  TIMED(K_TEMP, launch_temp_step(m->d, m->p, m->f, m->d_ctr, m->stream));
-  std::swap(m->f.theta, m->f.thetaNext);   // CYCLE_TRACER: the new theta is the other buffer
+  if (m->p.tempStepping) {
+    TIMED(K_TEMP, launch_tracer_step(m->d, m->p, m->f, tracer_args(m, false), m->d_ctr, m->stream));
+    std::swap(m->f.theta, m->f.thetaNext);   // CYCLE_TRACER: the new theta is the other buffer
+  }
+  if (m->p.saltStepping) {
+    TIMED(K_TEMP, launch_tracer_step(m->d, m->p, m->f, tracer_args(m, true), m->d_ctr, m->stream));
+    std::swap(m->f.salt, m->f.saltNext);
+  }
   return 0;
 }
 
@@ -585,6 +617,8 @@ int mgcm_blocking_exchanges(mgcm_model *m) {
   TIMED(K_EXCH, launch_exchange(m->d, m->f.wVel, m->d_halo, m->nHalo, m->d.Nr, m->stream));
   if (m->p.tempStepping)
     TIMED(K_EXCH, launch_exchange(m->d, m->f.theta, m->d_halo, m->nHalo, m->d.Nr, m->stream));
+  if (m->p.saltStepping)
+    TIMED(K_EXCH, launch_exchange(m->d, m->f.salt, m->d_halo, m->nHalo, m->d.Nr, m->stream));
   return 0;
 }
 
@@ -595,9 +629,11 @@ int mgcm_forward_step(mgcm_model *m, int nsteps) {
   HIPCHK(hipMemsetAsync(m->d_ctr + 1, 0, sizeof(int), m->stream));
   for (int s = 0; s < nsteps; s++) {
     if (mgcm_thermodynamics(m)) return -1;
-    if (mgcm_dynamics(m)) return -1;
-    if (solve_impl(m)) return -1;
-    if (mgcm_momentum_correction_step(m)) return -1;
+    if (m->p.momStepping) {
+      if (mgcm_dynamics(m)) return -1;
+      if (solve_impl(m)) return -1;
+      if (mgcm_momentum_correction_step(m)) return -1;
+    }
     if (mgcm_integr_continuity(m)) return -1;
     if (mgcm_blocking_exchanges(m)) return -1;
     HIPCHK(launch_bump_counter(m->d_ctr, 1, m->stream));

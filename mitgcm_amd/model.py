@@ -20,9 +20,9 @@ GRID_2D = ("dxF", "dyF", "dxG", "dyG", "dxC", "dyC", "dxV", "dyU", "rA", "rAw", 
 GRID_3D = ("hFacC", "hFacW", "hFacS", "recip_hFacC", "recip_hFacW", "recip_hFacS", "maskC", "maskW", "maskS")
 GRID_1D = ("drF", "drC", "recip_drF", "recip_drC", "rF", "rC")
 STATE_1D = ("tRef", "sRef")
-STATE_3D = ("uVel", "vVel", "wVel", "theta", "salt", "gU", "gV", "guNm1", "gvNm1", "gtNm1", "rhoInSitu",
+STATE_3D = ("uVel", "vVel", "wVel", "theta", "salt", "gU", "gV", "guNm1", "gvNm1", "gtNm1", "gsNm1", "rhoInSitu",
             "IVDConvCount")
-STATE_2D = ("etaN", "etaH", "fu", "fv", "SST", "lambdaThetaClimRelax", "surfaceForcingT")
+STATE_2D = ("etaN", "etaH", "fu", "fv", "SST", "lambdaThetaClimRelax", "surfaceForcingT", "surfaceForcingS")
 
 DEVICE_PARAMS = ("deltaTMom", "deltaTFreeSurf", "deltaTClock", "abEps", "rhoConst", "gBaro", "viscAhD",
                  "viscAhZ", "viscA4D", "viscA4Z", "viscAr", "sideDragFactor", "freeSurfFac", "implicSurfPress",
@@ -211,7 +211,8 @@ def dynstat(model):
             ("uvel", model.get("uVel"), f["hFacW"], f["maskInW"], f["rAw"], f["drF"]),
             ("vvel", model.get("vVel"), f["hFacS"], f["maskInS"], f["rAs"], f["drF"]),
             ("wvel", model.get("wVel"), f["maskC"], f["maskInC"], f["rA"], f["drC"]),
-            ("theta", model.get("theta"), f["hFacC"], f["maskInC"], f["rA"], f["drF"])):
+            ("theta", model.get("theta"), f["hFacC"], f["maskInC"], f["rA"], f["drF"]),
+            ("salt", model.get("salt"), f["hFacC"], f["maskInC"], f["rA"], f["drF"])):
         st = mon_stats(g, arr, hf, mask, area, dr)
         for k, v in st.items():
             out["dynstat_%s_%s" % (name, k)] = float(v)

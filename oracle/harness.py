@@ -182,13 +182,13 @@ def oracle_from_config(cfg, **kw):
         o.arr(n)[:len(g.f[n])] = g.f[n]
     for n in _GRID2 + _GRID3:
         if n in g.f:
-            o.arr(n)[:] = g.f[n]
+            o.arr(n).reshape(-1)[:] = np.ravel(g.f[n])
     for n in ("kSurfC", "kSurfW", "kSurfS", "kLowC"):
         o.iarr(n)[:] = g.i[n]
     o.set(cg2dNorm=g.cg2dNorm, cg2dTolerance_sq=g.cg2dTolerance_sq, cg2dNormaliseRHS=int(g.cg2dNormaliseRHS),
           globalArea=g.globalArea)
     for k, v in state.items():
-        o.arr(k)[:] = v
+        o.arr(k).reshape(-1)[:len(np.ravel(v))] = np.ravel(v)
     return o, g
 
 

@@ -30,7 +30,9 @@ OModel *oracle_new(int sNx, int sNy, int OLx, int OLy, int Nr, int nSx, int nSy)
   m->no_slip_sides = 1; m->no_slip_bottom = 1; m->momDissip_In_AB = 1; m->momForcingOutAB = 0;
   m->useHarmonicVisc = 1; m->selectCoriMap = 1; m->usingCartesianGrid = 1;
   m->integr_GeoPot = 2; m->rSphere = 6370.0e3; m->gravitySign = -1.0; m->tAlpha = 2.0e-4;
-  m->tempAdvScheme = 2; m->tempVertAdvScheme = 2;
+  m->tempAdvScheme = 2; m->tempVertAdvScheme = 2; m->saltAdvScheme = 2; m->saltVertAdvScheme = 2;
+  m->tempAdvection = 1; m->saltAdvection = 1; m->tempForcing = 1; m->saltForcing = 1; m->momStepping = 1;
+  m->multiDimAdvection = 1;
 
   m->drF = zalloc(Nr + 1); m->drC = zalloc(Nr + 1); m->rF = zalloc(Nr + 1); m->rC = zalloc(Nr + 1);
   m->recip_drF = zalloc(Nr + 1); m->recip_drC = zalloc(Nr + 1);
@@ -46,14 +48,14 @@ OModel *oracle_new(int sNx, int sNy, int OLx, int OLy, int Nr, int nSx, int nSy)
   A2(aW2d); A2(aS2d); A2(aC2d); A2(pW); A2(pS); A2(pC);
   A2(etaN); A2(fu); A2(fv); A2(surfaceForcingU); A2(surfaceForcingV);
   A2(fCoriCos); A2(tanPhiAtU); A2(tanPhiAtV); A2(surfaceForcingT); A2(SST); A2(lambdaThetaClimRelax);
-  A2(etaH); A2(dEtaHdt);
+  A2(etaH); A2(dEtaHdt); A2(surfaceForcingS);
 #undef A2
   m->kSurfC = izalloc(N2); m->kSurfW = izalloc(N2); m->kSurfS = izalloc(N2); m->kLowC = izalloc(N2);
 #define A3(f) m->f = zalloc(N3)
   A3(hFacC); A3(hFacW); A3(hFacS); A3(recip_hFacC); A3(recip_hFacW); A3(recip_hFacS);
   A3(maskC); A3(maskW); A3(maskS);
   A3(uVel); A3(vVel); A3(wVel); A3(theta); A3(salt); A3(gU); A3(gV); A3(guNm1); A3(gvNm1);
-  A3(gtNm1); A3(rhoInSitu); A3(IVDConvCount);
+  A3(gtNm1); A3(gsNm1); A3(rhoInSitu); A3(IVDConvCount);
 #undef A3
   return m;
 }
@@ -73,7 +75,7 @@ void oracle_free(OModel *m) {
                    &m->vVel, &m->wVel, &m->theta, &m->salt, &m->gU, &m->gV, &m->guNm1, &m->gvNm1,
                    &m->tRef, &m->sRef, &m->fCoriCos, &m->tanPhiAtU, &m->tanPhiAtV, &m->surfaceForcingT,
                    &m->SST, &m->lambdaThetaClimRelax, &m->etaH, &m->dEtaHdt, &m->gtNm1, &m->rhoInSitu,
-                   &m->IVDConvCount};
+                   &m->IVDConvCount, &m->gsNm1, &m->surfaceForcingS};
   for (size_t i = 0; i < sizeof(dp) / sizeof(dp[0]); i++) free(*dp[i]);
   free(m->kSurfC); free(m->kSurfW); free(m->kSurfS); free(m->kLowC);
   free(m);
@@ -98,6 +100,8 @@ static const PDesc PTAB[] = {
   PI_(cg2dNormaliseRHS), PI_(myIter), PI_(numIters), PI_(nIterMin),
   PI_(usingSphericalPolarGrid), PI_(selectMetricTerms), PI_(integr_GeoPot), PI_(tempStepping),
   PI_(tempAdvection), PI_(tempForcing), PI_(tempAdvScheme), PI_(tempVertAdvScheme), PI_(implicitDiffusion),
+  PI_(saltStepping), PI_(saltAdvection), PI_(saltForcing), PI_(saltAdvScheme), PI_(saltVertAdvScheme),
+  PI_(multiDimAdvection), PI_(momStepping), PD(diffKhS), PD(diffKrS),
   PD(rSphere), PD(deltaTtracer), PD(diffKhT), PD(diffKrT), PD(ivdc_kappa), PD(tAlpha), PD(sBeta), PD(gravitySign),
 };
 #undef PD
@@ -135,7 +139,7 @@ double *oracle_array(OModel *m, const char *name, long *count) {
     {"lambdaThetaClimRelax", m->lambdaThetaClimRelax, N2}, {"etaH", m->etaH, N2},
     {"dEtaHdt", m->dEtaHdt, N2}, {"surfaceForcingU", m->surfaceForcingU, N2},
     {"surfaceForcingV", m->surfaceForcingV, N2}, {"gtNm1", m->gtNm1, N3}, {"rhoInSitu", m->rhoInSitu, N3},
-    {"IVDConvCount", m->IVDConvCount, N3},
+    {"IVDConvCount", m->IVDConvCount, N3}, {"gsNm1", m->gsNm1, N3}, {"surfaceForcingS", m->surfaceForcingS, N2},
     {"delX", m->delX, (long)m->sNx * m->nSx}, {"delY", m->delY, (long)m->sNy * m->nSy},
     {"xC", m->xC, N2}, {"yC", m->yC, N2}, {"xG", m->xG, N2}, {"yG", m->yG, N2},
     {"dxF", m->dxF, N2}, {"dyF", m->dyF, N2}, {"dxG", m->dxG, N2}, {"dyG", m->dyG, N2},

@@ -44,6 +44,8 @@ typedef struct OModel {
   /* 3-D / tracer path (THERMODYNAMICS, CALC_PHI_HYD, spherical grid, exactConserv) */
   int usingSphericalPolarGrid, selectMetricTerms, integr_GeoPot;
   int tempStepping, tempAdvection, tempForcing, tempAdvScheme, tempVertAdvScheme, implicitDiffusion;
+  int saltStepping, saltAdvection, saltForcing, saltAdvScheme, saltVertAdvScheme, multiDimAdvection, momStepping;
+  double diffKhS, diffKrS;
   double rSphere, deltaTtracer, diffKhT, diffKrT, ivdc_kappa, tAlpha, sBeta, gravitySign;
 
   /* --- vertical grid (GRID.h), 1-based in the reference; here [0..Nr] --- */
@@ -74,7 +76,8 @@ typedef struct OModel {
   double *gU, *gV, *guNm1, *gvNm1;
   double *fu, *fv, *surfaceForcingU, *surfaceForcingV;
   double *surfaceForcingT, *SST, *lambdaThetaClimRelax, *etaH, *dEtaHdt;   /* 2-D */
-  double *gtNm1, *rhoInSitu, *IVDConvCount;                                /* 3-D */
+  double *gtNm1, *gsNm1, *rhoInSitu, *IVDConvCount;                        /* 3-D */
+  double *surfaceForcingS;                                                 /* 2-D */
   int myIter;
   double myTime;
 

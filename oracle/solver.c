@@ -342,15 +342,17 @@ void oracle_forward_step(OModel *m) {
     m->surfaceForcingU[p] = m->fu[p] * mass2rUnit;
     m->surfaceForcingV[p] = m->fv[p] * mass2rUnit;
   }
-  if (m->tempStepping) {
+  if (m->tempStepping || m->saltStepping) {
     /* forward_step.F:656 DO_OCEANIC_PHYS, :732 THERMODYNAMICS (staggerTimeStep = F) */
     oracle_oceanic_phys(m);
     oracle_thermodynamics(m);
   }
-  oracle_dynamics(m);
-  /* forward_step.F:806: myIter/myTime advance before SOLVE_FOR_PRESSURE */
-  oracle_solve_for_pressure(m);
-  oracle_momentum_correction_step(m);
+  if (m->momStepping) {
+    oracle_dynamics(m);
+    /* forward_step.F:806: myIter/myTime advance before SOLVE_FOR_PRESSURE */
+    oracle_solve_for_pressure(m);
+    oracle_momentum_correction_step(m);
+  }
   oracle_integr_continuity(m);
   /* do_fields_blocking_exchanges.F:54-97 */
   oracle_exch_xyz(m, m->uVel, m->Nr);

@@ -69,38 +69,170 @@ void oracle_oceanic_phys(OModel *m) {
   }
 }
 
-void oracle_thermodynamics(OModel *m) {
+/* ---------------------------------------------------------------------------
+ * GAD_DST3FL_ADV_X/Y/R (gad_dst3fl_adv_x.F:47-99, _y, _r.F:70-119): face flux
+ * of the 3rd-order direct-space-time scheme with flux limiter.  Returns the
+ * flux through the face between cells "m1" (upstream for positive transport)
+ * and "p0", given the four cells m2, m1, p0, p1 along the transport direction
+ * (for R: m2 = km2 .. p1 = kp1 as the reference orders them).
+ */
+static const double thetaMax = 1.0e+20, oneSixth = 1.0 / 6.0;
+
+static double dst3fl_limit(double d0, double d1, double theta, double cfl) {
+  double psi = d0 + d1 * theta;
+  return fmax(0.0, fmin(fmin(1.0, psi), theta * (1.0 - cfl) / (cfl + 1.0e-20)));
+}
+static double dst3fl_theta(double Rj, double Rother) {
+  if (fabs(Rj) * thetaMax <= fabs(Rother)) return copysign(thetaMax, Rother * Rj);
+  return Rother / Rj;
+}
+/* horizontal: Rjp = (T(i+1)-T(i))*mW(i+1), Rj = (T(i)-T(i-1))*mW(i), Rjm = (T(i-1)-T(i-2))*mW(i-1) */
+static double dst3fl_h(double uTr, double cfl, double tm2, double tm1, double t0, double tp1,
+                       double mWm1, double mW0, double mWp1) {
+  const double Rjp = (tp1 - t0) * mWp1, Rj = (t0 - tm1) * mW0, Rjm = (tm1 - tm2) * mWm1;
+  const double d0 = (2.0 - cfl) * (1.0 - cfl) * oneSixth, d1 = (1.0 - cfl * cfl) * oneSixth;
+  const double psiP = dst3fl_limit(d0, d1, dst3fl_theta(Rj, Rjm), cfl);
+  const double psiM = dst3fl_limit(d0, d1, dst3fl_theta(Rj, Rjp), cfl);
+  return 0.5 * (uTr + fabs(uTr)) * (tm1 + psiP * Rj) + 0.5 * (uTr - fabs(uTr)) * (t0 - psiM * Rj);
+}
+
+/* GAD_ADVECTION (gad_advection.F) for one tile, lat-lon (npass = 2: X then Y),
+ * GAD_MULTIDIM_COMPRESSIBLE undefined, explicit; advectionScheme = 33 only.
+ * Writes the advective tendency into gTr (whole tile, as the reference). */
+static void gad_advection_dst3fl(const OModel *m, int t, const double *tr, const double *uVel, const double *vVel,
+                                 const double *wVel, double *gTr, double dT) {
   const int sNx = m->sNx, sNy = m->sNy, OLx = m->OLx, OLy = m->OLy, Nr = m->Nr, nx = m->nx;
   const long n2 = m->n2, n3 = m->n3;
-  if (m->tempAdvScheme != 2 || m->tempVertAdvScheme != 2) {
-    fprintf(stderr, "oracle_thermodynamics: only tempAdvScheme = 2 restated here\n"); abort();
+  const double *hFacW = m->hFacW + t * n3, *hFacS = m->hFacS + t * n3, *maskW = m->maskW + t * n3;
+  const double *maskS = m->maskS + t * n3, *maskC = m->maskC + t * n3, *rhFacC = m->recip_hFacC + t * n3;
+  const double *dxG = m->dxG + t * n2, *dyG = m->dyG + t * n2, *rA = m->rA + t * n2, *recip_rA = m->recip_rA + t * n2;
+  const double *recip_dxC = m->recip_dxC + t * n2, *recip_dyC = m->recip_dyC + t * n2, *maskInC = m->maskInC + t * n2;
+  double *uTrans = calloc(n2, 8), *vTrans = calloc(n2, 8), *loc = calloc(n2, 8), *af = calloc(n2, 8);
+  double *locT3d = calloc(n3, 8), *rTrans = calloc(n2, 8), *rTransKp = calloc(n2, 8), *fV[2];
+  fV[0] = calloc(n2, 8); fV[1] = calloc(n2, 8);
+  for (int k = 1; k <= Nr; k++) {
+    for (int j = 1 - OLy; j <= sNy + OLy; j++)
+      for (int i = 1 - OLx; i <= sNx + OLx; i++) {
+        const double xA = L(dyG, i, j) * m->drF[k - 1] * W3(hFacW, i, j, k);
+        const double yA = L(dxG, i, j) * m->drF[k - 1] * W3(hFacS, i, j, k);
+        L(uTrans, i, j) = W3(uVel, i, j, k) * xA;
+        L(vTrans, i, j) = W3(vVel, i, j, k) * yA;
+        L(loc, i, j) = W3(tr, i, j, k);
+      }
+    /* ipass 1: X fluxes (uT = 0 at i = 1-OLx, 2-OLx, sNx+OLx), update j = all, i = 2-OLx..sNx+OLx-1 */
+    for (long p = 0; p < n2; p++) af[p] = 0.0;
+    for (int j = 1 - OLy; j <= sNy + OLy; j++)
+      for (int i = 3 - OLx; i <= sNx + OLx - 1; i++) {
+        const double cfl = fabs(W3(uVel, i, j, k) * dT * L(recip_dxC, i, j));
+        L(af, i, j) = dst3fl_h(L(uTrans, i, j), cfl, L(loc, i - 2, j), L(loc, i - 1, j), L(loc, i, j), L(loc, i + 1, j),
+                               W3(maskW, i - 1, j, k), W3(maskW, i, j, k), W3(maskW, i + 1, j, k));
+      }
+    for (int j = 1 - OLy; j <= sNy + OLy; j++)
+      for (int i = 2 - OLx; i <= sNx + OLx - 1; i++)
+        L(loc, i, j) = L(loc, i, j) - dT * W3(rhFacC, i, j, k) * m->recip_drF[k - 1] * L(recip_rA, i, j) *
+                                          (L(af, i + 1, j) - L(af, i, j) -
+                                           W3(tr, i, j, k) * (L(uTrans, i + 1, j) - L(uTrans, i, j))) *
+                                          L(maskInC, i, j);
+    /* ipass 2: Y fluxes (vT = 0 at j = 1-OLy, 2-OLy, sNy+OLy), update j = 2-OLy..sNy+OLy-1, i = all */
+    for (long p = 0; p < n2; p++) af[p] = 0.0;
+    for (int j = 3 - OLy; j <= sNy + OLy - 1; j++)
+      for (int i = 1 - OLx; i <= sNx + OLx; i++) {
+        const double cfl = fabs(W3(vVel, i, j, k) * dT * L(recip_dyC, i, j));
+        L(af, i, j) = dst3fl_h(L(vTrans, i, j), cfl, L(loc, i, j - 2), L(loc, i, j - 1), L(loc, i, j), L(loc, i, j + 1),
+                               W3(maskS, i, j - 1, k), W3(maskS, i, j, k), W3(maskS, i, j + 1, k));
+      }
+    for (int j = 2 - OLy; j <= sNy + OLy - 1; j++)
+      for (int i = 1 - OLx; i <= sNx + OLx; i++)
+        L(loc, i, j) = L(loc, i, j) - dT * W3(rhFacC, i, j, k) * m->recip_drF[k - 1] * L(recip_rA, i, j) *
+                                          (L(af, i, j + 1) - L(af, i, j) -
+                                           W3(tr, i, j, k) * (L(vTrans, i, j + 1) - L(vTrans, i, j))) *
+                                          L(maskInC, i, j);
+    for (int j = 1 - OLy; j <= sNy + OLy; j++)
+      for (int i = 1 - OLx; i <= sNx + OLx; i++) W3(locT3d, i, j, k) = L(loc, i, j);
   }
-  if (!m->implicitDiffusion) { fprintf(stderr, "oracle_thermodynamics: explicit vertical diffusion not restated\n"); abort(); }
+  /* vertical: k = Nr..1, GAD_DST3FL_ADV_R on the horizontally-updated tracer */
+  for (long p = 0; p < n2; p++) { rTrans[p] = 0.0; fV[0][p] = fV[1][p] = 0.0; }
+  for (int k = Nr; k >= 1; k--) {
+    const int kUp = 1 + (k + 1) % 2, kDown = 1 + k % 2;
+    const double kp1Msk = (k == Nr) ? 0.0 : 1.0;
+    double *fUp = fV[kUp - 1], *fDn = fV[kDown - 1];
+    const int km2 = k - 2 > 1 ? k - 2 : 1, km1 = k - 1 > 1 ? k - 1 : 1, kp1 = k + 1 < Nr ? k + 1 : Nr;
+    for (int j = 1 - OLy; j <= sNy + OLy; j++)
+      for (int i = 1 - OLx; i <= sNx + OLx; i++) {
+        L(rTransKp, i, j) = kp1Msk * L(rTrans, i, j);
+        if (k == 1) {
+          L(rTrans, i, j) = 0.0;
+          L(fUp, i, j) = 0.0;
+        } else {
+          L(rTrans, i, j) = W3(wVel, i, j, k) * L(rA, i, j) * W3(maskC, i, j, k - 1);
+          L(fUp, i, j) = 0.0;
+          const double Rjp = (W3(locT3d, i, j, k) - W3(locT3d, i, j, kp1)) * W3(maskC, i, j, kp1);
+          const double Rj = (W3(locT3d, i, j, km1) - W3(locT3d, i, j, k)) * W3(maskC, i, j, k) * W3(maskC, i, j, km1);
+          const double Rjm = (W3(locT3d, i, j, km2) - W3(locT3d, i, j, km1)) * W3(maskC, i, j, km1);
+          const double cfl = fabs(W3(wVel, i, j, k) * dT * m->recip_drC[k - 1]);
+          const double d0 = (2.0 - cfl) * (1.0 - cfl) * oneSixth, d1 = (1.0 - cfl * cfl) * oneSixth;
+          const double psiP = dst3fl_limit(d0, d1, dst3fl_theta(Rj, Rjm), cfl);
+          const double psiM = dst3fl_limit(d0, d1, dst3fl_theta(Rj, Rjp), cfl);
+          const double rT = L(rTrans, i, j);
+          L(fUp, i, j) = 0.5 * (rT + fabs(rT)) * (W3(locT3d, i, j, k) + psiM * Rj) +
+                         0.5 * (rT - fabs(rT)) * (W3(locT3d, i, j, km1) - psiP * Rj);
+        }
+      }
+    for (int j = 1 - OLy; j <= sNy + OLy; j++)
+      for (int i = 1 - OLx; i <= sNx + OLx; i++) {
+        const double lt = W3(locT3d, i, j, k) -
+                          dT * W3(rhFacC, i, j, k) * m->recip_drF[k - 1] * L(recip_rA, i, j) *
+                              (L(fDn, i, j) - L(fUp, i, j) - W3(tr, i, j, k) * (L(rTransKp, i, j) - L(rTrans, i, j))) *
+                              m->rkSign * L(maskInC, i, j);
+        W3(gTr, i, j, k) = (lt - W3(tr, i, j, k)) / dT;
+      }
+  }
+  free(uTrans); free(vTrans); free(loc); free(af); free(locT3d); free(rTrans); free(rTransKp); free(fV[0]); free(fV[1]);
+}
+
+/* One tracer through TEMP_INTEGRATE / SALT_INTEGRATE (temp_integrate.F, salt_integrate.F). */
+typedef struct {
+  double *tr, *gNm1;        /* tracer, its AB2 tendency history */
+  const double *sfc;        /* surface forcing (surfaceForcingT/S), may be NULL */
+  double diffKh, diffKr;
+  int advScheme, vAdvScheme, advection, forcing;
+} TracerSpec;
+
+static void tracer_integrate(OModel *m, const TracerSpec *c) {
+  const int sNx = m->sNx, sNy = m->sNy, OLx = m->OLx, OLy = m->OLy, Nr = m->Nr, nx = m->nx;
+  const long n2 = m->n2, n3 = m->n3;
+  const int multiDim = m->multiDimAdvection && c->advection && c->advScheme != 2 && c->advScheme != 3 && c->advScheme != 4;
+  const int useAB = (c->advScheme == 2 || c->advScheme == 3 || c->advScheme == 4);   /* gad_init_fixed.F:144-162 */
+  if (!(c->advScheme == 2 || c->advScheme == 33) || c->vAdvScheme != c->advScheme) {
+    fprintf(stderr, "oracle tracer_integrate: advection scheme %d/%d not restated\n", c->advScheme, c->vAdvScheme); abort();
+  }
   double *gT = calloc(n3, 8), *kappaRT = calloc(n3, 8);
   double *a3 = calloc(n3, 8), *b3 = calloc(n3, 8), *c3 = calloc(n3, 8), *cp = calloc(n3, 8), *yp = calloc(n3, 8);
   double *fVer[2], *xA = calloc(n2, 8), *yA = calloc(n2, 8), *uTrans = calloc(n2, 8), *vTrans = calloc(n2, 8);
   double *rTrans = calloc(n2, 8), *rTransKp = calloc(n2, 8), *maskUp = calloc(n2, 8), *gtForc = calloc(n2, 8);
   double *fZon = calloc(n2, 8), *fMer = calloc(n2, 8), *af = calloc(n2, 8), *df = calloc(n2, 8);
   fVer[0] = calloc(n2, 8); fVer[1] = calloc(n2, 8);
-  const double advFac = m->tempAdvection ? 1.0 : 0.0, rAdvFac = m->rkSign * advFac;
-  const double abFac = (m->myIter == m->nIter0 && m->nIter0 == 0) ? 0.0 : 0.5 + m->abEps; /* tempStartAB = nIter0 */
+  const int calcAdvection = c->advection && !multiDim;
+  const double advFac = calcAdvection ? 1.0 : 0.0, rAdvFac = m->rkSign * advFac;
+  const double abFac = (m->myIter == m->nIter0 && m->nIter0 == 0) ? 0.0 : 0.5 + m->abEps; /* startAB = nIter0 */
 
   for (int t = 0; t < m->nTiles; t++) {
-    double *theta = m->theta + t * n3, *gtNm1 = m->gtNm1 + t * n3;
+    double *theta = c->tr + t * n3, *gtNm1 = c->gNm1 + t * n3;
     const double *uVel = m->uVel + t * n3, *vVel = m->vVel + t * n3, *wVel = m->wVel + t * n3;
     const double *hFacW = m->hFacW + t * n3, *hFacS = m->hFacS + t * n3, *maskC = m->maskC + t * n3;
     const double *rhFacC = m->recip_hFacC + t * n3, *conv = m->IVDConvCount + t * n3;
     const double *dxG = m->dxG + t * n2, *dyG = m->dyG + t * n2, *rA = m->rA + t * n2;
     const double *recip_rA = m->recip_rA + t * n2, *recip_dxC = m->recip_dxC + t * n2;
     const double *recip_dyC = m->recip_dyC + t * n2, *maskInC = m->maskInC + t * n2;
-    const double *sfT = m->surfaceForcingT + t * n2;
+    const double *sfT = c->sfc ? c->sfc + t * n2 : NULL;
 
-    /* CALC_3D_DIFFUSIVITY: KappaRT = IVDConvCount*ivdc_kappa + KbryanLewis79(=0) + diffKrNrT(k) */
+    /* CALC_3D_DIFFUSIVITY: KappaR = IVDConvCount*ivdc_kappa + KbryanLewis79(=0) + diffKrNr(k) */
     for (int k = 1; k <= Nr; k++)
       for (int j = 1 - OLy; j <= sNy + OLy; j++)
         for (int i = 1 - OLx; i <= sNx + OLx; i++)
-          W3(kappaRT, i, j, k) = (W3(conv, i, j, k) * m->ivdc_kappa + 0.0) + m->diffKrT;
+          W3(kappaRT, i, j, k) = (W3(conv, i, j, k) * m->ivdc_kappa + 0.0) + c->diffKr;
     for (long p = 0; p < n3; p++) gT[p] = 0.0;
+    if (multiDim) gad_advection_dst3fl(m, t, theta, uVel, vVel, wVel, gT, m->deltaTtracer);
     for (long p = 0; p < n2; p++) { fVer[0][p] = fVer[1][p] = 0.0; rTrans[p] = 0.0; }
 
     for (int k = Nr; k >= 1; k--) {
@@ -121,15 +253,15 @@ void oracle_thermodynamics(OModel *m) {
             L(rTrans, i, j) = W3(wVel, i, j, k) * L(rA, i, j) * L(maskUp, i, j);
           }
         }
-      /* APPLY_FORCING_T: surface flux at k = kSurface = 1 over 0..sNx+1 */
+      /* APPLY_FORCING_T/S: surface flux at k = kSurface = 1 over 0..sNx+1 */
       for (long p = 0; p < n2; p++) gtForc[p] = 0.0;
-      if (m->tempForcing && k == 1)
+      if (c->forcing && sfT && k == 1)
         for (int j = 0; j <= sNy + 1; j++)
           for (int i = 0; i <= sNx + 1; i++)
             L(gtForc, i, j) = L(gtForc, i, j) + L(sfT, i, j) * m->recip_drF[k - 1] * W3(rhFacC, i, j, k);
       /* GAD_CALC_RHS */
       for (long p = 0; p < n2; p++) { fZon[p] = 0.0; fMer[p] = 0.0; fVerUp[p] = 0.0; df[p] = 0.0; }
-      if (m->tempAdvection) { /* GAD_C2_ADV_X */
+      if (calcAdvection) { /* GAD_C2_ADV_X */
         for (int j = 1 - OLy; j <= sNy + OLy; j++) {
           L(af, 1 - OLx, j) = 0.0;
           for (int i = 2 - OLx; i <= sNx + OLx; i++)
@@ -137,40 +269,48 @@ void oracle_thermodynamics(OModel *m) {
         }
         for (long p = 0; p < n2; p++) fZon[p] = fZon[p] + af[p];
       }
-      if (m->diffKhT != 0.0) { /* GAD_DIFF_X, cosFacU = 1 */
+      if (c->diffKh != 0.0) { /* GAD_DIFF_X, cosFacU = 1 */
         for (int j = 1 - OLy; j <= sNy + OLy; j++) {
           L(df, 1 - OLx, j) = 0.0;
           for (int i = 2 - OLx; i <= sNx + OLx; i++)
-            L(df, i, j) = -m->diffKhT * L(xA, i, j) * L(recip_dxC, i, j) * (W3(theta, i, j, k) - W3(theta, i - 1, j, k));
+            L(df, i, j) = -c->diffKh * L(xA, i, j) * L(recip_dxC, i, j) * (W3(theta, i, j, k) - W3(theta, i - 1, j, k));
         }
       } else {
         for (long p = 0; p < n2; p++) df[p] = 0.0;
       }
       for (long p = 0; p < n2; p++) fZon[p] = fZon[p] + df[p];
-      if (m->tempAdvection) { /* GAD_C2_ADV_Y */
+      if (calcAdvection) { /* GAD_C2_ADV_Y */
         for (int i = 1 - OLx; i <= sNx + OLx; i++) L(af, i, 1 - OLy) = 0.0;
         for (int j = 2 - OLy; j <= sNy + OLy; j++)
           for (int i = 1 - OLx; i <= sNx + OLx; i++)
             L(af, i, j) = L(vTrans, i, j) * (W3(theta, i, j, k) + W3(theta, i, j - 1, k)) * 0.5;
         for (long p = 0; p < n2; p++) fMer[p] = fMer[p] + af[p];
       }
-      if (m->diffKhT != 0.0) { /* GAD_DIFF_Y */
+      if (c->diffKh != 0.0) { /* GAD_DIFF_Y */
         for (int i = 1 - OLx; i <= sNx + OLx; i++) L(df, i, 1 - OLy) = 0.0;
         for (int j = 2 - OLy; j <= sNy + OLy; j++)
           for (int i = 1 - OLx; i <= sNx + OLx; i++)
-            L(df, i, j) = -m->diffKhT * L(yA, i, j) * L(recip_dyC, i, j) * (W3(theta, i, j, k) - W3(theta, i, j - 1, k));
+            L(df, i, j) = -c->diffKh * L(yA, i, j) * L(recip_dyC, i, j) * (W3(theta, i, j, k) - W3(theta, i, j - 1, k));
       } else {
         for (long p = 0; p < n2; p++) df[p] = 0.0;
       }
       for (long p = 0; p < n2; p++) fMer[p] = fMer[p] + df[p];
-      if (m->tempAdvection && k >= 2) { /* GAD_C2_ADV_R */
+      if (calcAdvection && k >= 2) { /* GAD_C2_ADV_R */
         for (int j = 1 - OLy; j <= sNy + OLy; j++)
           for (int i = 1 - OLx; i <= sNx + OLx; i++) {
             double wT = W3(maskC, i, j, kM1) * L(rTrans, i, j) * (W3(theta, i, j, k) + W3(theta, i, j, kM1)) * 0.5;
             L(fVerUp, i, j) = L(fVerUp, i, j) + wT * L(maskInC, i, j);
           }
       }
-      /* implicitDiffusion: explicit vertical diffusive flux df = 0 -> fVerT(kUp) + 0 */
+      /* vertical diffusive flux: 0 with implicitDiffusion, else GAD_DIFF_R */
+      for (int j = 1 - OLy; j <= sNy + OLy; j++)
+        for (int i = 1 - OLx; i <= sNx + OLx; i++) {
+          double dfr = 0.0;
+          if (!m->implicitDiffusion && k >= 2)
+            dfr = -W3(kappaRT, i, j, k) * L(maskUp, i, j) * L(rA, i, j) * m->recip_drC[k - 1] *
+                  (W3(theta, i, j, k) - W3(theta, i, j, kM1)) * m->rkSign;
+          L(fVerUp, i, j) = L(fVerUp, i, j) + dfr;
+        }
       for (int j = 1 - OLy; j <= sNy + OLy - 1; j++)
         for (int i = 1 - OLx; i <= sNx + OLx - 1; i++) {
           double T = W3(theta, i, j, k);
@@ -182,60 +322,77 @@ void oracle_thermodynamics(OModel *m) {
                T * ((L(uTrans, i + 1, j) - L(uTrans, i, j)) * advFac + (L(vTrans, i, j + 1) - L(vTrans, i, j)) * advFac +
                     (L(rTransKp, i, j) - L(rTrans, i, j)) * rAdvFac) * L(maskInC, i, j));
         }
-      /* temp_integrate.F: gT += gtForc (tracForcingOutAB = 0), then ADAMS_BASHFORTH2(k) */
+      /* gT += gtForc (tracForcingOutAB = 0), then ADAMS_BASHFORTH2(k) when AB is on */
       for (int j = 1 - OLy; j <= sNy + OLy; j++)
         for (int i = 1 - OLx; i <= sNx + OLx; i++) {
           W3(gT, i, j, k) = W3(gT, i, j, k) + L(gtForc, i, j);
-          double ab = abFac * (W3(gT, i, j, k) - W3(gtNm1, i, j, k));
-          W3(gtNm1, i, j, k) = W3(gT, i, j, k);
-          W3(gT, i, j, k) = W3(gT, i, j, k) + ab;
-        }
-    }
-    /* TIMESTEP_TRACER: gT = theta + dTtracerLev(k)*gT */
-    for (long p = 0; p < n3; p++) gT[p] = theta[p] + m->deltaTtracer * gT[p];
-    /* GAD_IMPLICIT_R, implicitDiffusion: b5d (sub), c5d (diag), d5d (super) on 1..sNx, 1..sNy */
-    for (long p = 0; p < n3; p++) { a3[p] = 0.0; b3[p] = 1.0; c3[p] = 0.0; }
-    for (int k = 1; k <= Nr; k++)
-      for (int j = 1; j <= sNy; j++)
-        for (int i = 1; i <= sNx; i++) {
-          double sub = 0.0, sup = 0.0;
-          if (k >= 2)
-            sub = -(m->deltaTtracer * W3(maskC, i, j, k - 1) * W3(rhFacC, i, j, k) * m->recip_drF[k - 1] *
-                    W3(kappaRT, i, j, k) * m->recip_drC[k - 1]);
-          if (k <= Nr - 1)
-            sup = -(m->deltaTtracer * W3(maskC, i, j, k + 1) * W3(rhFacC, i, j, k) * m->recip_drF[k - 1] *
-                    W3(kappaRT, i, j, k + 1) * m->recip_drC[k]);
-          W3(a3, i, j, k) = sub; W3(c3, i, j, k) = sup;
-          W3(b3, i, j, k) = 1.0 - (sub + sup);
-        }
-    /* SOLVE_TRIDIAGONAL (default: neither LOWMEMORY nor KINNER), whole tile */
-    for (int k = 1; k <= Nr; k++)
-      for (int j = 1 - OLy; j <= sNy + OLy; j++)
-        for (int i = 1 - OLx; i <= sNx + OLx; i++) {
-          double y = W3(gT, i, j, k);
-          if (k == 1) {
-            if (W3(b3, i, j, 1) != 0.0) {
-              double rec = 1.0 / W3(b3, i, j, 1);
-              W3(cp, i, j, 1) = W3(c3, i, j, 1) * rec;
-              W3(yp, i, j, 1) = y * rec;
-            } else { W3(cp, i, j, 1) = 0.0; W3(yp, i, j, 1) = 0.0; }
-          } else {
-            double tmp = W3(b3, i, j, k) - W3(a3, i, j, k) * W3(cp, i, j, k - 1);
-            if (tmp != 0.0) {
-              double rec = 1.0 / tmp;
-              W3(cp, i, j, k) = W3(c3, i, j, k) * rec;
-              W3(yp, i, j, k) = (y - W3(a3, i, j, k) * W3(yp, i, j, k - 1)) * rec;
-            } else { W3(cp, i, j, k) = 0.0; W3(yp, i, j, k) = 0.0; }
+          if (useAB) {
+            double ab = abFac * (W3(gT, i, j, k) - W3(gtNm1, i, j, k));
+            W3(gtNm1, i, j, k) = W3(gT, i, j, k);
+            W3(gT, i, j, k) = W3(gT, i, j, k) + ab;
           }
         }
-    for (int k = Nr; k >= 1; k--)
-      for (int j = 1 - OLy; j <= sNy + OLy; j++)
-        for (int i = 1 - OLx; i <= sNx + OLx; i++)
-          W3(gT, i, j, k) = (k == Nr) ? W3(yp, i, j, k) : W3(yp, i, j, k) - W3(cp, i, j, k) * W3(gT, i, j, k + 1);
+    }
+    /* TIMESTEP_TRACER: gT = tracer + dTtracerLev(k)*gT */
+    for (long p = 0; p < n3; p++) gT[p] = theta[p] + m->deltaTtracer * gT[p];
+    if (m->implicitDiffusion) {
+      /* GAD_IMPLICIT_R: b5d (sub), c5d (diag), d5d (super) on 1..sNx, 1..sNy */
+      for (long p = 0; p < n3; p++) { a3[p] = 0.0; b3[p] = 1.0; c3[p] = 0.0; }
+      for (int k = 1; k <= Nr; k++)
+        for (int j = 1; j <= sNy; j++)
+          for (int i = 1; i <= sNx; i++) {
+            double sub = 0.0, sup = 0.0;
+            if (k >= 2)
+              sub = -(m->deltaTtracer * W3(maskC, i, j, k - 1) * W3(rhFacC, i, j, k) * m->recip_drF[k - 1] *
+                      W3(kappaRT, i, j, k) * m->recip_drC[k - 1]);
+            if (k <= Nr - 1)
+              sup = -(m->deltaTtracer * W3(maskC, i, j, k + 1) * W3(rhFacC, i, j, k) * m->recip_drF[k - 1] *
+                      W3(kappaRT, i, j, k + 1) * m->recip_drC[k]);
+            W3(a3, i, j, k) = sub; W3(c3, i, j, k) = sup;
+            W3(b3, i, j, k) = 1.0 - (sub + sup);
+          }
+      /* SOLVE_TRIDIAGONAL (default: neither LOWMEMORY nor KINNER), whole tile */
+      for (int k = 1; k <= Nr; k++)
+        for (int j = 1 - OLy; j <= sNy + OLy; j++)
+          for (int i = 1 - OLx; i <= sNx + OLx; i++) {
+            double y = W3(gT, i, j, k);
+            if (k == 1) {
+              if (W3(b3, i, j, 1) != 0.0) {
+                double rec = 1.0 / W3(b3, i, j, 1);
+                W3(cp, i, j, 1) = W3(c3, i, j, 1) * rec;
+                W3(yp, i, j, 1) = y * rec;
+              } else { W3(cp, i, j, 1) = 0.0; W3(yp, i, j, 1) = 0.0; }
+            } else {
+              double tmp = W3(b3, i, j, k) - W3(a3, i, j, k) * W3(cp, i, j, k - 1);
+              if (tmp != 0.0) {
+                double rec = 1.0 / tmp;
+                W3(cp, i, j, k) = W3(c3, i, j, k) * rec;
+                W3(yp, i, j, k) = (y - W3(a3, i, j, k) * W3(yp, i, j, k - 1)) * rec;
+              } else { W3(cp, i, j, k) = 0.0; W3(yp, i, j, k) = 0.0; }
+            }
+          }
+      for (int k = Nr; k >= 1; k--)
+        for (int j = 1 - OLy; j <= sNy + OLy; j++)
+          for (int i = 1 - OLx; i <= sNx + OLx; i++)
+            W3(gT, i, j, k) = (k == Nr) ? W3(yp, i, j, k) : W3(yp, i, j, k) - W3(cp, i, j, k) * W3(gT, i, j, k + 1);
+    }
     /* CYCLE_TRACER */
     for (long p = 0; p < n3; p++) theta[p] = gT[p];
   }
   free(gT); free(kappaRT); free(a3); free(b3); free(c3); free(cp); free(yp);
   free(fVer[0]); free(fVer[1]); free(xA); free(yA); free(uTrans); free(vTrans); free(rTrans); free(rTransKp);
   free(maskUp); free(gtForc); free(fZon); free(fMer); free(af); free(df);
+}
+
+void oracle_thermodynamics(OModel *m) {
+  if (m->tempStepping) {
+    TracerSpec c = {m->theta, m->gtNm1, m->surfaceForcingT, m->diffKhT, m->diffKrT,
+                    m->tempAdvScheme, m->tempVertAdvScheme, m->tempAdvection, m->tempForcing};
+    tracer_integrate(m, &c);
+  }
+  if (m->saltStepping) {
+    TracerSpec c = {m->salt, m->gsNm1, m->surfaceForcingS, m->diffKhS, m->diffKrS,
+                    m->saltAdvScheme, m->saltVertAdvScheme, m->saltAdvection, m->saltForcing};
+    tracer_integrate(m, &c);
+  }
 }

@@ -24,6 +24,10 @@ EXPERIMENTS = {
         "inputs": ["input/bathy.bin", "input/windx_cosy.bin"],
         "output": "results/output.txt",
     },
+    "advect_xy": {
+        "inputs": [],
+        "output": "results/output.txt",
+    },
     "tutorial_baroclinic_gyre": {
         "inputs": ["input/bathy.bin", "input/windx_cosy.bin", "input/SST_relax.bin"],
         "output": "results/output.txt",

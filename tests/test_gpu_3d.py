@@ -134,3 +134,76 @@ def test_baroclinic_fields_vs_oracle_after_10_steps():
         sc = np.abs(ref).max()
         assert np.abs(dev - ref).max() <= 1e-10 * sc, (n, np.abs(dev - ref).max(), sc)
     m.close()
+
+
+def test_advect_xy_dst3fl_vs_oracle_and_reference(golden_dir):
+    """Multi-dim DST3FL advection on the device: bit-exact vs the oracle after 80
+    steps (interior), and the reference's salt statistics at print precision."""
+    from mitgcm_amd import configs
+    from oracle.harness import oracle_from_config
+    gold = json.load(open(os.path.join(golden_dir, "advect_xy", "monitor.json")))
+    o, g = oracle_from_config(configs.advect_xy)
+    m = configs.make_model(configs.advect_xy)
+    inner = (slice(None), slice(None)) + g.sl(1, g.sNx, 1, g.sNy)
+    for n in range(1, 81):
+        m.forward_step(1)
+        o.forward_step()
+        if n % 16:
+            continue
+        dev = m.get("salt")
+        ref = np.array(o.arr("salt")).reshape(dev.shape)
+        assert np.array_equal(dev[inner], ref[inner]), (n, np.abs(dev - ref)[inner].max())
+        st = o.stats(ref, 1, o.arr("hFacC"), 1, o.arr("maskInC"), o.arr("rA"), o.arr("drF")[:1].copy())
+        for v, k in zip(st[:4], ("min", "max", "mean", "sd")):
+            assert digits(v, gold[n // 16]["dynstat_salt_" + k]) >= 13.0, (n, k)
+    m.close()
+
+
+def _dst3_gyre(**kw):
+    from mitgcm_amd import configs
+    return configs.baroclinic_gyre(tempAdvScheme=33, **kw)
+
+
+def test_baroclinic_dst3fl_thermodynamics_bitexact_vs_oracle():
+    """tutorial_baroclinic_gyre with tempAdvScheme=33 (BASELINE config 4):
+    one THERMODYNAMICS call (3-D multi-dim DST3FL incl. the vertical pass) from
+    a stepped, convectively perturbed state, bit-exact against the oracle."""
+    from mitgcm_amd import configs
+    from mitgcm_amd._lib import lib
+    from oracle.harness import oracle_from_config
+    o, g = oracle_from_config(_dst3_gyre)
+    for _ in range(3):
+        o.forward_step()
+    o.arr("theta")[:, 1, 10:16, 8:20] += 12.0
+    m = configs.make_model(_dst3_gyre)
+    for n in ("uVel", "vVel", "wVel", "theta", "gtNm1", "etaN"):
+        m.put(n, np.array(o.arr(n)))
+    lib().mgcm_set_param(m.h, b"myIter", float(o.get("myIter")))
+    m.thermodynamics()
+    o.L.oracle_oceanic_phys(o.h)
+    o.L.oracle_thermodynamics(o.h)
+    inner = (slice(None), slice(None)) + g.sl(1, g.sNx, 1, g.sNy)
+    dev, ref = m.get("theta")[inner], np.array(o.arr("theta"))[inner]
+    assert np.array_equal(dev, ref), np.abs(dev - ref).max()
+    m.close()
+
+
+def test_baroclinic_dst3fl_10_steps_vs_oracle():
+    from mitgcm_amd import configs
+    from oracle.harness import oracle_from_config
+    o, g = oracle_from_config(_dst3_gyre)
+    m = configs.make_model(_dst3_gyre)
+    for _ in range(10):
+        o.forward_step()
+    m.forward_step(10)
+    m.sync()
+    st_o = o.dynstat()
+    from mitgcm_amd.model import dynstat
+    st_d = dynstat(m)
+    for n in ("uVel", "vVel", "wVel", "theta", "etaN"):
+        dev, ref = m.get(n), np.array(o.arr(n)).reshape(m.get(n).shape)
+        sc = np.abs(ref).max()
+        assert np.abs(dev - ref).max() <= 1e-10 * sc, (n, np.abs(dev - ref).max(), sc)
+    for k in ("dynstat_theta_sd", "dynstat_theta_max", "dynstat_uvel_sd"):
+        assert digits(st_d[k], st_o[k]) >= 11.0, k
+    m.close()
