@@ -35,8 +35,8 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=20)
-    ap.add_argument("--config", default="tutorial_baroclinic_gyre",
-                    choices=["tutorial_baroclinic_gyre", "tutorial_barotropic_gyre"])
+    ap.add_argument("--config", default="baroclinic_gyre_dst3",
+                    choices=["baroclinic_gyre_dst3", "tutorial_baroclinic_gyre", "tutorial_barotropic_gyre"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--pmc-summary", default=os.path.join(ROOT, "profiles", "r01", "pmc_summary.json"),
@@ -45,10 +45,22 @@ def parse():
 
 
 WORKLOADS = {
+    "baroclinic_gyre_dst3": "BASELINE config 4: tutorial_baroclinic_gyre 62x62x15 (4 tiles of 31x31, "
+                            "spherical-polar) with tempAdvScheme=33 (multi-dim DST3 flux-limited), full FORWARD_STEP "
+                            "on device (dt=1200 s)",
     "tutorial_baroclinic_gyre": "tutorial_baroclinic_gyre 62x62x15 (4 tiles of 31x31, spherical-polar), "
                                 "full FORWARD_STEP on device incl. THERMODYNAMICS (dt=1200 s)",
     "tutorial_barotropic_gyre": "tutorial_barotropic_gyre 62x62x1, 1 tile, full FORWARD_STEP on device (dt=1200 s)",
 }
+
+
+def config_fn(name):
+    """The mitgcm_amd.configs set-up behind a --config name."""
+    from mitgcm_amd import configs
+    if name == "baroclinic_gyre_dst3":
+        return lambda: configs.baroclinic_gyre(tempAdvScheme=33)
+    return {"tutorial_baroclinic_gyre": configs.baroclinic_gyre,
+            "tutorial_barotropic_gyre": configs.barotropic_gyre}[name]
 
 
 def cpu_baseline(config, seconds):
@@ -59,7 +71,7 @@ def cpu_baseline(config, seconds):
     if config == "tutorial_barotropic_gyre":
         o = gyre_oracle()
     else:
-        o, _ = oracle_from_config(configs.baroclinic_gyre)
+        o, _ = oracle_from_config(config_fn(config))
     o.forward_step()  # warm
     n, t0 = 0, time.perf_counter()
     while time.perf_counter() - t0 < seconds:
@@ -99,8 +111,7 @@ def main():
     from mitgcm_amd import configs
     from mitgcm_amd.model import dynstat
 
-    cfg = configs.baroclinic_gyre if a.config == "tutorial_baroclinic_gyre" else configs.barotropic_gyre
-    m = configs.make_model(cfg, device=local)
+    m = configs.make_model(config_fn(a.config), device=local)
     g = m.g
     dt_clock = m.params["deltaTClock"]
     npts = g.nTiles * g.sNx * g.sNy
@@ -157,7 +168,8 @@ def main():
         "vs_baseline": None,
         "dtype": "f64",
         "data": "reference input fields of verification/%s (bathy, wind%s), cold start"
-                % (a.config, ", SST_relax" if a.config == "tutorial_baroclinic_gyre" else ""),
+                % ("tutorial_barotropic_gyre" if a.config == "tutorial_barotropic_gyre" else "tutorial_baroclinic_gyre",
+                   "" if a.config == "tutorial_barotropic_gyre" else ", SST_relax"),
         "config": {"workload": WORKLOADS[a.config] + "; replicas only",
                    "tiles_per_gpu": g.nTiles, "points_per_tile": [g.sNx, g.sNy, g.Nr],
                    "parallelism": "replicas%d" % world},

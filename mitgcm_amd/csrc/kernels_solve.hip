@@ -322,17 +322,21 @@ __global__ void __launch_bounds__(CG_THREADS) k_cg2d_block(Dims d, Params p, Fie
 #undef pS1
 }
 
-// 2x2-blocked whole-solve CG2D (tiles with even sNx, sNy; <= 4096 points):
-// each thread owns the 2x2 block (i0..i0+1, j0..j0+1), i0 and j0 odd, of one
-// tile.  The block's four in-block neighbour values come from its own
-// registers; only the eight out-of-block ones (two per side) are LDS reads
-// through the neighbour table, and all 32 operator coefficients of the block
-// (aW/pW at i0..i0+2, aS/pS at j0..j0+2, aC, pC) stay in VGPRs.  Products are
-// FMA-contracted here: CG2D's parity bar is roundoff agreement (its global
-// sums are re-ordered anyway), not bit-exactness.
+// 2x2-blocked whole-solve CG2D (<= 4096 points): each thread owns a 2x2 block of
+// mutually adjacent interior points P[b][a] (row b, column a; P[0][1] east of
+// P[0][0], P[1][*] north of P[0][*]).  Blocks are formed on the global lat-lon
+// index space, so a block may straddle a tile edge and odd tile sizes work as
+// long as the global Nx, Ny are even; each point carries its own 2-D offset.
+// The block's four in-block neighbour values come from its own registers; only
+// the eight out-of-block ones (two per side) are LDS reads through the
+// neighbour table, and all 32 operator coefficients of the block (aW/pW of the
+// three W-E faces of each row, aS/pS of the three S-N faces of each column, aC,
+// pC) stay in VGPRs (pS, pC in LDS).  Products are FMA-contracted here: CG2D's
+// parity bar is roundoff agreement (its global sums are re-ordered anyway), not
+// bit-exactness.
 // nb4[4*T]: packed 16-bit compact indices (W0|W1<<16), (E0|E1<<16),
-// (S0|S1<<16), (N0|N1<<16); blk[T] = 2-D offset of (i0,j0) (T = #blocks,
-// padding blocks: offset of a real block, neighbours -> ZERO slot, inactive).
+// (S0|S1<<16), (N0|N1<<16); blk[4*T] = 2-D offsets of P00, P10(east), P01(north),
+// P11 (T = #blocks; padding blocks: offsets of a real block, inactive).
 template <bool MINRES>
 __global__ void __launch_bounds__(CG_THREADS) k_cg2d_blk2(Dims d, Params p, Fields f, const unsigned *__restrict__ nb4,
                                                          const int *__restrict__ blk, int nBlk, int maxIters,
@@ -346,13 +350,15 @@ __global__ void __launch_bounds__(CG_THREADS) k_cg2d_blk2(Dims d, Params p, Fiel
   const int tid = threadIdx.x;
   const bool act = tid < nBlk;
   const int bt = act ? tid : 0;
-  const long g = blk[bt];
   const long nx = d.nx;
-  // compact LDS slots of the block's own points: tile-major, row-major in the tile
-  const int t0 = (int)(g / d.n2), l0 = (int)(g % d.n2);
-  const int i0 = l0 % d.nx - d.OLx + 1, j0 = l0 / d.nx - d.OLy + 1;
-  const int c00 = act ? t0 * d.sNx * d.sNy + (j0 - 1) * d.sNx + (i0 - 1) : NP;
-  const int c10 = act ? c00 + 1 : NP, c01 = act ? c00 + d.sNx : NP, c11 = act ? c00 + d.sNx + 1 : NP;
+  // G[b][a]: 2-D offset of point P[b][a]; compact LDS slot: tile-major, row-major in the tile
+  const long G[2][2] = {{blk[4 * bt], blk[4 * bt + 1]}, {blk[4 * bt + 2], blk[4 * bt + 3]}};
+  auto slot_of = [&](long gg) {
+    const int tt = (int)(gg / d.n2), ll = (int)(gg % d.n2);
+    return tt * d.sNx * d.sNy + (ll / d.nx - d.OLy) * d.sNx + (ll % d.nx - d.OLx);
+  };
+  const int c00 = act ? slot_of(G[0][0]) : NP, c10 = act ? slot_of(G[0][1]) : NP;
+  const int c01 = act ? slot_of(G[1][0]) : NP, c11 = act ? slot_of(G[1][1]) : NP;
   const unsigned wW = nb4[4 * bt], wE = nb4[4 * bt + 1], wS = nb4[4 * bt + 2], wN = nb4[4 * bt + 3];
 #define LO(w) ((w) & 0xFFFFu)
 #define HI(w) ((w) >> 16)
@@ -363,21 +369,26 @@ __global__ void __launch_bounds__(CG_THREADS) k_cg2d_blk2(Dims d, Params p, Fiel
   // structure-of-arrays over threads (conflict-free), to stay under 128 VGPRs.
   double *pl = red + 4 * CG_WAVES;  // 10 * CG_THREADS
   double aW[2][3], pW[2][3], aS[2][3], aC[2][2];
+  // W-E faces of row b: west faces of P[b][0], P[b][1], and the east face of P[b][1]
+  // (its i+1 entry: the halo copy of the eastern neighbour's coefficient when P[b][1]
+  // is on a tile edge, exactly what the reference reads after EXCH_UV_XY_RS)
 #pragma unroll
   for (int b = 0; b < 2; b++)
 #pragma unroll
     for (int a = 0; a < 3; a++) {
-      aW[b][a] = az * f.aW2d[g + a + b * nx];
-      pW[b][a] = az * f.pW[g + a + b * nx];
-      aS[b][a] = az * f.aS2d[g + b + a * nx];  // [column b][row a]
-      pl[(b * 3 + a) * CG_THREADS + tid] = az * f.pS[g + b + a * nx];
+      const long gw = a < 2 ? G[b][a] : G[b][1] + 1;
+      const long gs = a < 2 ? G[a][b] : G[1][b] + nx;
+      aW[b][a] = az * f.aW2d[gw];
+      pW[b][a] = az * f.pW[gw];
+      aS[b][a] = az * f.aS2d[gs];  // [column b][row a]
+      pl[(b * 3 + a) * CG_THREADS + tid] = az * f.pS[gs];
     }
 #pragma unroll
   for (int b = 0; b < 2; b++)
 #pragma unroll
     for (int a = 0; a < 2; a++) {
-      aC[b][a] = az * f.aC2d[g + a + b * nx];   // [row b][col a]
-      pl[(6 + b * 2 + a) * CG_THREADS + tid] = az * f.pC[g + a + b * nx];
+      aC[b][a] = az * f.aC2d[G[b][a]];   // [row b][col a]
+      pl[(6 + b * 2 + a) * CG_THREADS + tid] = az * f.pC[G[b][a]];
     }
 #define pS(b, a) pl[((b) * 3 + (a)) * CG_THREADS + tid]
 #define pC(b, a) pl[(6 + (b) * 2 + (a)) * CG_THREADS + tid]
@@ -387,8 +398,8 @@ __global__ void __launch_bounds__(CG_THREADS) k_cg2d_blk2(Dims d, Params p, Fiel
   for (int b = 0; b < 2; b++)
 #pragma unroll
     for (int a = 0; a < 2; a++) {
-      b_[b][a] = act ? f.cg2d_b[g + a + b * nx] : 0.0;
-      x[b][a] = act ? f.cg2d_x[g + a + b * nx] : 0.0;
+      b_[b][a] = act ? f.cg2d_b[G[b][a]] : 0.0;
+      x[b][a] = act ? f.cg2d_x[G[b][a]] : 0.0;
       s[b][a] = 0.0;
     }
   if (tid == 0) { r_l[NP] = 0.0; s_l[NP] = 0.0; }
@@ -457,7 +468,7 @@ __global__ void __launch_bounds__(CG_THREADS) k_cg2d_blk2(Dims d, Params p, Fiel
 #pragma unroll
     for (int b = 0; b < 2; b++)
 #pragma unroll
-      for (int a = 0; a < 2; a++) f.cg2d_b[g + a + b * nx] = b_[b][a];
+      for (int a = 0; a < 2; a++) f.cg2d_b[G[b][a]] = b_[b][a];
   }
   double err_sq = block_sum(err, red, 1);
   const double sumRHS = block_sum(sumB, red, 2);
@@ -545,7 +556,7 @@ __global__ void __launch_bounds__(CG_THREADS) k_cg2d_blk2(Dims d, Params p, Fiel
       for (int a = 0; a < 2; a++) {
         double xv = x[b][a];
         if (p.cg2dNormaliseRHS) xv = xv / rhsNorm;
-        f.cg2d_x[g + a + b * nx] = xv;
+        f.cg2d_x[G[b][a]] = xv;
       }
   }
   if (tid == 0) {

@@ -133,6 +133,7 @@ struct mgcm_model {
   unsigned *d_nb4 = nullptr;
   int *d_blk = nullptr;
   int nBlk = 0;
+  bool latlonTopology = true;   // false once a custom halo map (e.g. EXCH2 cube) is installed
   // step counters: [0] = myIter, [1] = record slot
   int *d_ctr = nullptr;
   SolveRecord *d_rec = nullptr;
@@ -278,10 +279,13 @@ static int build_nbr(mgcm_model *m) {
   HIPCHK(hipMemcpy(m->d_nbr, nb.data(), nb.size() * sizeof(unsigned), hipMemcpyHostToDevice));
   HIPCHK(hipMalloc(&m->d_gofs, gofs.size() * sizeof(int)));
   HIPCHK(hipMemcpy(m->d_gofs, gofs.data(), gofs.size() * sizeof(int), hipMemcpyHostToDevice));
-  // 2x2 blocks: only for even tile sizes and <= 1024 blocks; ZERO slot = 4*1024
+  // 2x2 blocks (k_cg2d_blk2), formed on the global lat-lon index space so that odd
+  // tile sizes work: needs the default EXCH1 lat-lon topology, even global Nx and Ny,
+  // and <= 1024 blocks; the ZERO slot is 4*1024.
   m->nBlk = 0;
-  const int nBk = d.nTiles * (d.sNx / 2) * (d.sNy / 2);
-  if (d.sNx % 2 == 0 && d.sNy % 2 == 0 && nBk <= 1024 && !getenv("MGCM_CG2D_NOBLK")) {
+  const int Nx = d.sNx * d.nSx, Ny = d.sNy * d.nSy;
+  const int nBk = (Nx / 2) * (Ny / 2);
+  if (m->latlonTopology && Nx % 2 == 0 && Ny % 2 == 0 && nBk <= 1024 && !getenv("MGCM_CG2D_NOBLK")) {
     const unsigned Z = 4096u;
     auto cmp = [&](long g) -> unsigned {
       unsigned c = compact(g);
@@ -292,18 +296,27 @@ static int build_nbr(mgcm_model *m) {
       if (i < 1 || i > d.sNx || j < 1 || j > d.sNy) g = srcOf[g];
       return cmp(g);
     };
+    // global (I, J), 1-based -> tile-local point
+    auto gpt = [&](int I, int J, int &i, int &j, int &t) {
+      const int bi = (I - 1) / d.sNx, bj = (J - 1) / d.sNy;
+      t = bj * d.nSx + bi; i = (I - 1) % d.sNx + 1; j = (J - 1) % d.sNy + 1;
+    };
     std::vector<unsigned> nb4(4 * 1024, Z | (Z << 16));
-    std::vector<int> blk(1024, (int)MG_I2(d, 1, 1, 0));
+    std::vector<int> blk(4 * 1024, (int)MG_I2(d, 1, 1, 0));
     int q = 0;
-    for (int t = 0; t < d.nTiles; t++)
-      for (int j0 = 1; j0 <= d.sNy; j0 += 2)
-        for (int i0 = 1; i0 <= d.sNx; i0 += 2, q++) {
-          blk[q] = (int)MG_I2(d, i0, j0, t);
-          nb4[4 * q + 0] = nbv(i0 - 1, j0, t) | (nbv(i0 - 1, j0 + 1, t) << 16);
-          nb4[4 * q + 1] = nbv(i0 + 2, j0, t) | (nbv(i0 + 2, j0 + 1, t) << 16);
-          nb4[4 * q + 2] = nbv(i0, j0 - 1, t) | (nbv(i0 + 1, j0 - 1, t) << 16);
-          nb4[4 * q + 3] = nbv(i0, j0 + 2, t) | (nbv(i0 + 1, j0 + 2, t) << 16);
-        }
+    for (int J0 = 1; J0 <= Ny; J0 += 2)
+      for (int I0 = 1; I0 <= Nx; I0 += 2, q++) {
+        int ii[2][2], jj[2][2], tt[2][2];
+        for (int b = 0; b < 2; b++)
+          for (int a = 0; a < 2; a++) gpt(I0 + a, J0 + b, ii[b][a], jj[b][a], tt[b][a]);
+        for (int b = 0; b < 2; b++)
+          for (int a = 0; a < 2; a++) blk[4 * q + 2 * b + a] = (int)MG_I2(d, ii[b][a], jj[b][a], tt[b][a]);
+        // out-of-block neighbours, through each boundary point's own halo map
+        nb4[4 * q + 0] = nbv(ii[0][0] - 1, jj[0][0], tt[0][0]) | (nbv(ii[1][0] - 1, jj[1][0], tt[1][0]) << 16);
+        nb4[4 * q + 1] = nbv(ii[0][1] + 1, jj[0][1], tt[0][1]) | (nbv(ii[1][1] + 1, jj[1][1], tt[1][1]) << 16);
+        nb4[4 * q + 2] = nbv(ii[0][0], jj[0][0] - 1, tt[0][0]) | (nbv(ii[0][1], jj[0][1] - 1, tt[0][1]) << 16);
+        nb4[4 * q + 3] = nbv(ii[1][0], jj[1][0] + 1, tt[1][0]) | (nbv(ii[1][1], jj[1][1] + 1, tt[1][1]) << 16);
+      }
     if (m->d_nb4) (void)hipFree(m->d_nb4);
     if (m->d_blk) (void)hipFree(m->d_blk);
     HIPCHK(hipMalloc(&m->d_nb4, nb4.size() * sizeof(unsigned)));
@@ -470,11 +483,16 @@ int mgcm_set_halo_map(mgcm_model *m, const long *src_of_point, long count) {
   const long N2 = m->d.n2 * m->d.nTiles;
   if (count != N2) return set_err("mgcm_set_halo_map: count %ld != %ld", count, N2);
   m->h_halo.clear();
+  // a map identical to the default lat-lon one keeps the global-index CG2D blocking
+  build_latlon_halo(m);
+  std::vector<long> ll = m->h_halo;
+  m->h_halo.clear();
   for (long q = 0; q < N2; q++)
     if (src_of_point[q] >= 0 && src_of_point[q] != q) {
       m->h_halo.push_back(q);
       m->h_halo.push_back(src_of_point[q]);
     }
+  m->latlonTopology = (ll == m->h_halo);
   m->ready = false;
   return 0;
 }
