@@ -76,6 +76,9 @@ int mgcm_momentum_correction_step(mgcm_model *m);
 int mgcm_integr_continuity(mgcm_model *m);
 /* DO_FIELDS_BLOCKING_EXCHANGES (model/src/do_fields_blocking_exchanges.F:54). */
 int mgcm_blocking_exchanges(mgcm_model *m);
+/* Capture the hipGraph that mgcm_forward_step replays (two steps per graph) for
+ * the current state, so that a timed region does not include the capture. */
+int mgcm_prepare(mgcm_model *m);
 /* FORWARD_STEP subset: the six ops above (+ surface forcing), nsteps times,
  * asynchronously on the model's stream (captured once into a hipGraph). */
 int mgcm_forward_step(mgcm_model *m, int nsteps);

@@ -38,6 +38,7 @@ def lib():
         "mgcm_init": (ci, [vp]),
         "mgcm_dynamics": (ci, [vp]),
         "mgcm_thermodynamics": (ci, [vp]),
+        "mgcm_prepare": (ci, [vp]),
         "mgcm_solve_for_pressure": (ci, [vp]),
         "mgcm_momentum_correction_step": (ci, [vp]),
         "mgcm_integr_continuity": (ci, [vp]),
@@ -62,7 +63,7 @@ def lib():
 EXPORTS = ["mgcm_create", "mgcm_destroy", "mgcm_last_error", "mgcm_set_param", "mgcm_get_param", "mgcm_put",
            "mgcm_get", "mgcm_device_ptr", "mgcm_set_halo_map", "mgcm_init", "mgcm_dynamics", "mgcm_thermodynamics",
            "mgcm_solve_for_pressure", "mgcm_momentum_correction_step", "mgcm_integr_continuity",
-           "mgcm_blocking_exchanges", "mgcm_forward_step", "mgcm_sync", "mgcm_cg2d", "mgcm_solve_stats",
+           "mgcm_blocking_exchanges", "mgcm_prepare", "mgcm_forward_step", "mgcm_sync", "mgcm_cg2d", "mgcm_solve_stats",
            "mgcm_kernel_ms", "mgcm_kernel_timing", "ini_cg2d_amd_", "cg2d_amd_"]
 
 

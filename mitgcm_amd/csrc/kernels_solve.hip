@@ -735,8 +735,12 @@ hipError_t launch_cg2d_blk2(const Dims &d, const Params &p, const Fields &f, con
   if (nBlk > CG_THREADS) return hipErrorInvalidValue;
   const size_t lds = cg2d_block_lds_bytes(4) + 10 * CG_THREADS * sizeof(double);  // 146 KiB
   auto kern = nIterMin >= 0 ? k_cg2d_blk2<true> : k_cg2d_blk2<false>;
-  hipError_t e = hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-  if (e != hipSuccess) return e;
+  static bool attrSet[2] = {false, false};   // once per instantiation (not a stream op; keeps graph capture clean)
+  if (!attrSet[nIterMin >= 0]) {
+    hipError_t e = hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (e != hipSuccess) return e;
+    attrSet[nIterMin >= 0] = true;
+  }
   hipLaunchKernelGGL(kern, dim3(1), dim3(CG_THREADS), lds, s, d, p, f, nb4, blk, nBlk, maxIters, nIterMin, rec,
                      stepCounter);
   return hipGetLastError();

@@ -134,6 +134,10 @@ struct mgcm_model {
   int *d_blk = nullptr;
   int nBlk = 0;
   bool latlonTopology = true;   // false once a custom halo map (e.g. EXCH2 cube) is installed
+  // hipGraphs of two FORWARD_STEPs, one per theta/salt ping-pong parity
+  bool useGraph = true;
+  hipGraphExec_t graphExec[4] = {nullptr, nullptr, nullptr, nullptr};
+  double *thetaA = nullptr, *saltA = nullptr;
   // step counters: [0] = myIter, [1] = record slot
   int *d_ctr = nullptr;
   SolveRecord *d_rec = nullptr;
@@ -148,6 +152,8 @@ struct mgcm_model {
   double kms[K_N] = {0};
   int kcnt[K_N] = {0};
 };
+
+static void drop_graphs(mgcm_model *m);
 
 static long field_count(const mgcm_model *m, FieldKind k) {
   if (k == F1D) return m->d.Nr + 1;
@@ -392,6 +398,7 @@ void mgcm_destroy(mgcm_model *m) {
   if (m->stream) hipStreamSynchronize(m->stream);
   ev_collect(m);
   ev_free(m);
+  drop_graphs(m);
   for (void *p : m->allocs) hipFree(p);
   if (m->d_halo) hipFree(m->d_halo);
   if (m->d_nbr) hipFree(m->d_nbr);
@@ -405,6 +412,7 @@ void mgcm_destroy(mgcm_model *m) {
 }
 
 int mgcm_set_param(mgcm_model *m, const char *name, double value) {
+  drop_graphs(m);   // kernel arguments are captured by value
   if (!strcmp(name, "myIter")) {  // the device-side iteration counter (AB2 start, solve records)
     int it = (int)value;
     HIPCHK(hipSetDevice(m->device));
@@ -523,6 +531,10 @@ int mgcm_init(mgcm_model *m) {
     return set_err("mgcm_init: tempAdvScheme %d not implemented on the device", m->p.tempAdvScheme);
   if (m->p.saltStepping && !okScheme(m->p.saltAdvScheme, "saltVertAdvScheme"))
     return set_err("mgcm_init: saltAdvScheme %d not implemented on the device", m->p.saltAdvScheme);
+  drop_graphs(m);
+  m->thetaA = m->f.theta;
+  m->saltA = m->f.salt;
+  m->useGraph = getenv("MGCM_NO_GRAPH") == nullptr;
   int it0 = m->p.nIter0;
   HIPCHK(hipMemcpy(m->d_ctr, &it0, sizeof(int), hipMemcpyHostToDevice));
   // INI_PSURF (ini_psurf.F:84): etaH = etaN
@@ -640,22 +652,73 @@ int mgcm_blocking_exchanges(mgcm_model *m) {
   return 0;
 }
 
+static int one_step(mgcm_model *m) {
+  if (mgcm_thermodynamics(m)) return -1;
+  if (m->p.momStepping) {
+    if (mgcm_dynamics(m)) return -1;
+    if (solve_impl(m)) return -1;
+    if (mgcm_momentum_correction_step(m)) return -1;
+  }
+  if (mgcm_integr_continuity(m)) return -1;
+  if (mgcm_blocking_exchanges(m)) return -1;
+  HIPCHK(launch_bump_counter(m->d_ctr, 1, m->stream));
+  return 0;
+}
+
+static void drop_graphs(mgcm_model *m) {
+  for (int q = 0; q < 4; q++)
+    if (m->graphExec[q]) { (void)hipGraphExecDestroy(m->graphExec[q]); m->graphExec[q] = nullptr; }
+}
+
+// Which theta/salt ping-pong buffers are current (the kernels' arguments differ).
+static int buffer_parity(const mgcm_model *m) {
+  return (m->f.theta == m->thetaA ? 0 : 1) + (m->f.salt == m->saltA ? 0 : 2);
+}
+
+// Two FORWARD_STEPs captured once into a hipGraph per buffer parity (the tracer
+// ping-pong swaps twice, so the pointers are back where they started), then
+// replayed: no per-kernel host launch cost inside a batch.
+static int two_step_graph(mgcm_model *m, hipGraphExec_t *out) {
+  const int q = buffer_parity(m);
+  if (!m->graphExec[q]) {
+    hipGraph_t g = nullptr;
+    HIPCHK(hipStreamBeginCapture(m->stream, hipStreamCaptureModeThreadLocal));
+    int rc = one_step(m);
+    if (!rc) rc = one_step(m);
+    hipError_t e = hipStreamEndCapture(m->stream, &g);
+    if (rc) { if (g) (void)hipGraphDestroy(g); return -1; }
+    HIPCHK(e);
+    e = hipGraphInstantiate(&m->graphExec[q], g, nullptr, nullptr, 0);
+    (void)hipGraphDestroy(g);
+    HIPCHK(e);
+  }
+  *out = m->graphExec[q];
+  return 0;
+}
+
+int mgcm_prepare(mgcm_model *m) {
+  if (check_ready(m)) return -1;
+  if (!m->useGraph) return 0;
+  HIPCHK(hipSetDevice(m->device));
+  hipGraphExec_t ge;
+  return two_step_graph(m, &ge);
+}
+
 int mgcm_forward_step(mgcm_model *m, int nsteps) {
   if (check_ready(m)) return -1;
   if (nsteps <= 0 || nsteps > m->maxRec) return set_err("mgcm_forward_step: nsteps %d out of range", nsteps);
   HIPCHK(hipSetDevice(m->device));
   HIPCHK(hipMemsetAsync(m->d_ctr + 1, 0, sizeof(int), m->stream));
-  for (int s = 0; s < nsteps; s++) {
-    if (mgcm_thermodynamics(m)) return -1;
-    if (m->p.momStepping) {
-      if (mgcm_dynamics(m)) return -1;
-      if (solve_impl(m)) return -1;
-      if (mgcm_momentum_correction_step(m)) return -1;
+  int s = 0;
+  if (m->useGraph && !m->timing) {
+    for (; s + 2 <= nsteps; s += 2) {
+      hipGraphExec_t ge;
+      if (two_step_graph(m, &ge)) return -1;
+      HIPCHK(hipGraphLaunch(ge, m->stream));
     }
-    if (mgcm_integr_continuity(m)) return -1;
-    if (mgcm_blocking_exchanges(m)) return -1;
-    HIPCHK(launch_bump_counter(m->d_ctr, 1, m->stream));
   }
+  for (; s < nsteps; s++)
+    if (one_step(m)) return -1;
   m->lastBatch = nsteps;
   return 0;
 }

@@ -95,6 +95,10 @@ class Model:
         return a
 
     # ---- hot path ------------------------------------------------------------
+    def prepare(self):
+        """Capture the replayed step graph now (outside any timed region)."""
+        check(lib().mgcm_prepare(self.h), "mgcm_prepare")
+
     def forward_step(self, nsteps=1):
         check(lib().mgcm_forward_step(self.h, int(nsteps)), "mgcm_forward_step")
 
