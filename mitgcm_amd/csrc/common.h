@@ -79,6 +79,14 @@ struct TracerArgs {
   int advection, multiDim, useAB, forcing;
 };
 
+// Fields exchanged together by k_exchange_multi.
+#define MG_XMAX 6
+struct XFields {
+  double *p[MG_XMAX];
+  int nz[MG_XMAX];
+  int n;
+};
+
 // Per-solve record written by the device CG2D (one slot per time step).
 struct SolveRecord {
   double firstResidual, lastResidual, minResidualSq, rhsMax, sumRHS;

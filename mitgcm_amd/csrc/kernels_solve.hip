@@ -681,6 +681,114 @@ __global__ void __launch_bounds__(256) k_copy(double *dst, const double *src, lo
   if (q < n) dst[q] = src[q];
 }
 
+// DO_FIELDS_BLOCKING_EXCHANGES in one launch: up to MG_XMAX fields of nz[f] levels
+// through the halo map; the block (0,0,0) also advances the step counters (the
+// last kernel of a step: nothing later in the step reads them).
+__global__ void __launch_bounds__(256) k_exchange_multi(Dims d, XFields x, const long *__restrict__ map, int nHalo,
+                                                        int *ctr) {
+  const int h = (int)(blockIdx.x * blockDim.x + threadIdx.x);
+  const int k = (int)blockIdx.y, fi = (int)blockIdx.z;
+  if (ctr && h == 0 && k == 0 && fi == 0) { ctr[0] += 1; ctr[1] += 1; }
+  if (h >= nHalo || fi >= x.n || k >= x.nz[fi]) return;
+  const long dst = map[2 * h], src = map[2 * h + 1];
+  const long dt = dst / d.n2, dl = dst % d.n2, st = src / d.n2, sl = src % d.n2;
+  const long lvl = (long)d.n2 * x.nz[fi];
+  double *a = x.p[fi];
+  a[dt * lvl + (long)k * d.n2 + dl] = a[st * lvl + (long)k * d.n2 + sl];
+}
+
+// EXCH_XY_RL(cg2d_x) + etaN = recip_Bo*cg2d_x (solve_for_pressure.F:316, 377-385) in
+// one pass over every 2-D point; srcOf[q] = interior source of halo point q, or -1.
+__global__ void __launch_bounds__(256) k_exch_eta(Dims d, Fields f, const long *__restrict__ srcOf) {
+  const long q = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (q >= d.n2 * d.nTiles) return;
+  const long sq = srcOf[q];
+  double x = f.cg2d_x[q];
+  if (sq >= 0) { x = f.cg2d_x[sq]; f.cg2d_x[q] = x; }
+  f.etaN[q] = f.recip_Bo[q] * x;
+}
+
+// exactConserv end of INTEGR_CONTINUITY: EXCH_XY_RL of the new eta (held in cg2d_b
+// by k_corr_cont) into etaN, and UPDATE_ETAH (etaH = etaN) in one pass.
+__global__ void __launch_bounds__(256) k_exch_etaH(Dims d, Fields f, const long *__restrict__ srcOf) {
+  const long q = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (q >= d.n2 * d.nTiles) return;
+  const long sq = srcOf[q];
+  const double *e = f.cg2d_b;
+  double x;
+  if (sq >= 0) x = e[sq];
+  else {
+    // interior: the new eta; points that are neither interior nor mapped keep etaN
+    const long l = q % d.n2;
+    const int i = (int)(l % d.nx) - d.OLx + 1, j = (int)(l / d.nx) - d.OLy + 1;
+    x = (i >= 1 && i <= d.sNx && j >= 1 && j <= d.sNy) ? e[q] : f.etaN[q];
+  }
+  f.etaN[q] = x;
+  f.etaH[q] = x;
+}
+
+// MOMENTUM_CORRECTION_STEP fused with INTEGR_CONTINUITY for one interior column:
+// u, v = (u* + dt*gdPx)*mask (correction_step.F:152-234) for this column, the
+// east/north neighbours' corrected velocities recomputed inline (identical
+// expressions), then exactConserv's eta (into cg2d_b, see k_exch_etaH) and
+// INTEGRATE_FOR_W.  Halo velocities are left to the end-of-step EXCH.
+__global__ void __launch_bounds__(256) k_corr_cont(Dims d, Params p, Fields f) {
+  const int i = (int)(blockIdx.x * blockDim.x + threadIdx.x) + 1;
+  const int j = (int)(blockIdx.y * blockDim.y + threadIdx.y) + 1;
+  const int t = (int)blockIdx.z;
+  if (i > d.sNx || j > d.sNy) return;
+  const double psFac = p.pfFacMom * p.implicSurfPress;
+  auto phiX = [&](int ii, int jj) {
+    const long q = MG_I2(d, ii, jj, t);
+    return f.recip_dxC[q] * (f.Bo_surf[q] * f.etaN[q] - f.Bo_surf[MG_I2(d, ii - 1, jj, t)] * f.etaN[MG_I2(d, ii - 1, jj, t)]);
+  };
+  auto phiY = [&](int ii, int jj) {
+    const long q = MG_I2(d, ii, jj, t);
+    return f.recip_dyC[q] * (f.Bo_surf[q] * f.etaN[q] - f.Bo_surf[MG_I2(d, ii, jj - 1, t)] * f.etaN[MG_I2(d, ii, jj - 1, t)]);
+  };
+  const double pX0 = phiX(i, j), pX1 = phiX(i + 1, j), pY0 = phiY(i, j), pY1 = phiY(i, j + 1);
+  auto uCor = [&](int ii, int k, double phiSurfX) {
+    const long q3 = MG_I3(d, ii, j, k, t);
+    const double mW = f.maskW[q3];
+    return (f.gU[q3] + p.deltaTMom * (-psFac * phiSurfX * mW)) * mW;
+  };
+  auto vCor = [&](int jj, int k, double phiSurfY) {
+    const long q3 = MG_I3(d, i, jj, k, t);
+    const double mS = f.maskS[q3];
+    return (f.gV[q3] + p.deltaTMom * (-psFac * phiSurfY * mS)) * mS;
+  };
+  const long q = MG_I2(d, i, j, t);
+  auto div = [&](int k, double u0, double u1, double v0, double v1) {
+    const double drF = f.drF[k - 1];
+    const double uT1 = u1 * f.dyG[MG_I2(d, i + 1, j, t)] * drF * f.hFacW[MG_I3(d, i + 1, j, k, t)];
+    const double uT0 = u0 * f.dyG[q] * drF * f.hFacW[MG_I3(d, i, j, k, t)];
+    const double vT1 = v1 * f.dxG[MG_I2(d, i, j + 1, t)] * drF * f.hFacS[MG_I3(d, i, j + 1, k, t)];
+    const double vT0 = v0 * f.dxG[q] * drF * f.hFacS[MG_I3(d, i, j, k, t)];
+    return uT1 - uT0 + vT1 - vT0;
+  };
+  if (p.exactConserv) {
+    double hDiv = 0.0;
+    for (int k = 1; k <= d.Nr; k++) {
+      const double u0 = uCor(i, k, pX0), u1 = uCor(i + 1, k, pX1), v0 = vCor(j, k, pY0), v1 = vCor(j + 1, k, pY1);
+      hDiv = hDiv + f.maskC[MG_I3(d, i, j, k, t)] * div(k, u0, u1, v0, v1);
+    }
+    const double dEtaHdt = -(hDiv * f.recip_rA[q]) - 0.0 * 0.0;
+    f.cg2d_b[q] = f.etaH[q] + p.implicDiv2DFlow * dEtaHdt * p.deltaTFreeSurf;
+  }
+  double wBelow = 0.0;
+  for (int k = d.Nr; k >= 1; k--) {
+    const double u0 = uCor(i, k, pX0), u1 = uCor(i + 1, k, pX1), v0 = vCor(j, k, pY0), v1 = vCor(j + 1, k, pY1);
+    f.uVel[MG_I3(d, i, j, k, t)] = u0;
+    f.vVel[MG_I3(d, i, j, k, t)] = v0;
+    const double conv2d = -div(k, u0, u1, v0, v1);
+    double w;
+    if (k == d.Nr) w = conv2d * f.recip_rA[q] * f.maskC[MG_I3(d, i, j, k, t)];
+    else w = (wBelow + conv2d * f.recip_rA[q]) * f.maskC[MG_I3(d, i, j, k, t)];
+    f.wVel[MG_I3(d, i, j, k, t)] = w;
+    wBelow = w;
+  }
+}
+
 __global__ void k_bump_counter(int *c, int nIncr) {
   if (threadIdx.x == 0) { c[0] += nIncr; c[1] += 1; }
 }
@@ -779,6 +887,27 @@ hipError_t launch_continuity_ec(const Dims &d, const Params &p, const Fields &f,
 
 hipError_t launch_copy(double *dst, const double *src, long n, hipStream_t s) {
   hipLaunchKernelGGL(k_copy, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, dst, src, n);
+  return hipGetLastError();
+}
+
+hipError_t launch_exchange_multi(const Dims &d, const XFields &x, const long *map, int nHalo, int *ctr, hipStream_t s) {
+  int nzMax = 1;
+  for (int q = 0; q < x.n; q++) nzMax = x.nz[q] > nzMax ? x.nz[q] : nzMax;
+  dim3 blk(256), grd((unsigned)((nHalo > 0 ? nHalo : 1) + 255) / 256, nzMax, x.n);
+  hipLaunchKernelGGL(k_exchange_multi, grd, blk, 0, s, d, x, map, nHalo, ctr);
+  return hipGetLastError();
+}
+
+hipError_t launch_exch_eta(const Dims &d, const Fields &f, const long *srcOf, bool etaH, hipStream_t s) {
+  const long n = d.n2 * d.nTiles;
+  if (etaH) hipLaunchKernelGGL(k_exch_etaH, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, d, f, srcOf);
+  else hipLaunchKernelGGL(k_exch_eta, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, d, f, srcOf);
+  return hipGetLastError();
+}
+
+hipError_t launch_corr_cont(const Dims &d, const Params &p, const Fields &f, hipStream_t s) {
+  dim3 blk(64, 4, 1), grd((d.sNx + 63) / 64, (d.sNy + 3) / 4, d.nTiles);
+  hipLaunchKernelGGL(k_corr_cont, grd, blk, 0, s, d, p, f);
   return hipGetLastError();
 }
 

@@ -33,6 +33,9 @@ hipError_t launch_eta_update(const Dims &, const Fields &, hipStream_t);
 hipError_t launch_correction(const Dims &, const Params &, const Fields &, hipStream_t);
 hipError_t launch_continuity(const Dims &, const Fields &, hipStream_t);
 hipError_t launch_bump_counter(int *, int, hipStream_t);
+hipError_t launch_exchange_multi(const Dims &, const XFields &, const long *, int, int *, hipStream_t);
+hipError_t launch_exch_eta(const Dims &, const Fields &, const long *, bool, hipStream_t);
+hipError_t launch_corr_cont(const Dims &, const Params &, const Fields &, hipStream_t);
 hipError_t launch_oceanic_phys(const Dims &, const Params &, const Fields &, hipStream_t);
 hipError_t launch_tracer_step(const Dims &, const Params &, const Fields &, const TracerArgs &, const int *, hipStream_t);
 hipError_t launch_continuity_ec(const Dims &, const Params &, const Fields &, hipStream_t);
@@ -124,6 +127,7 @@ struct mgcm_model {
   std::map<std::string, double> extra;
   // halo map (2*nHalo longs) and CG2D neighbour table
   long *d_halo = nullptr;
+  long *d_srcOf = nullptr;    // per 2-D point: interior source of a halo point, -1 otherwise
   int nHalo = 0;
   std::vector<long> h_halo;
   unsigned *d_nbr = nullptr;  // packed (W|E<<16),(S|N<<16) compact neighbour indices, padded
@@ -233,7 +237,13 @@ static void build_latlon_halo(mgcm_model *m) {
 
 static int upload_halo(mgcm_model *m) {
   if (m->d_halo) { hipFree(m->d_halo); m->d_halo = nullptr; }
+  if (m->d_srcOf) { hipFree(m->d_srcOf); m->d_srcOf = nullptr; }
   m->nHalo = (int)(m->h_halo.size() / 2);
+  const long N2 = m->d.n2 * m->d.nTiles;
+  std::vector<long> srcOf(N2, -1);
+  for (size_t h = 0; h + 1 < m->h_halo.size(); h += 2) srcOf[m->h_halo[h]] = m->h_halo[h + 1];
+  HIPCHK(hipMalloc(&m->d_srcOf, N2 * sizeof(long)));
+  HIPCHK(hipMemcpy(m->d_srcOf, srcOf.data(), N2 * sizeof(long), hipMemcpyHostToDevice));
   if (m->nHalo == 0) return 0;
   HIPCHK(hipMalloc(&m->d_halo, m->h_halo.size() * sizeof(long)));
   HIPCHK(hipMemcpy(m->d_halo, m->h_halo.data(), m->h_halo.size() * sizeof(long), hipMemcpyHostToDevice));
@@ -401,6 +411,7 @@ void mgcm_destroy(mgcm_model *m) {
   drop_graphs(m);
   for (void *p : m->allocs) hipFree(p);
   if (m->d_halo) hipFree(m->d_halo);
+  if (m->d_srcOf) hipFree(m->d_srcOf);
   if (m->d_nbr) hipFree(m->d_nbr);
   if (m->d_gofs) hipFree(m->d_gofs);
   if (m->d_nb4) hipFree(m->d_nb4);
@@ -652,16 +663,27 @@ int mgcm_blocking_exchanges(mgcm_model *m) {
   return 0;
 }
 
+// One FORWARD_STEP with the fused end-of-step kernels: EXCH(cg2d_x)+etaN,
+// correction+continuity, EXCH(eta)+UPDATE_ETAH, and every blocking exchange plus
+// the counter bump in one launch.  Same arithmetic as the separate C-ABI ops.
 static int one_step(mgcm_model *m) {
   if (mgcm_thermodynamics(m)) return -1;
   if (m->p.momStepping) {
     if (mgcm_dynamics(m)) return -1;
-    if (solve_impl(m)) return -1;
-    if (mgcm_momentum_correction_step(m)) return -1;
+    TIMED(K_RHS, launch_sfp_rhs(m->d, m->p, m->f, m->stream));
+    TIMED(K_CG2D, launch_cg2d(m, m->p.cg2dMaxIters, m->p.cg2dUseMinResSol - 1));
+    TIMED(K_ETA, launch_exch_eta(m->d, m->f, m->d_srcOf, false, m->stream));
+    TIMED(K_CONT, launch_corr_cont(m->d, m->p, m->f, m->stream));
+    if (m->p.exactConserv) TIMED(K_ETA, launch_exch_eta(m->d, m->f, m->d_srcOf, true, m->stream));
+  } else {
+    if (mgcm_integr_continuity(m)) return -1;
   }
-  if (mgcm_integr_continuity(m)) return -1;
-  if (mgcm_blocking_exchanges(m)) return -1;
-  HIPCHK(launch_bump_counter(m->d_ctr, 1, m->stream));
+  XFields x{};
+  double *fl[] = {m->f.uVel, m->f.vVel, m->f.wVel, m->f.theta, m->f.salt};
+  const bool use[] = {true, true, true, m->p.tempStepping != 0, m->p.saltStepping != 0};
+  for (int q = 0; q < 5; q++)
+    if (use[q]) { x.p[x.n] = fl[q]; x.nz[x.n] = m->d.Nr; x.n++; }
+  TIMED(K_EXCH, launch_exchange_multi(m->d, x, m->d_halo, m->nHalo, m->d_ctr, m->stream));
   return 0;
 }
 
