@@ -69,6 +69,33 @@ struct Fields {
   ((long)((i) + (d).OLx - 1) + (long)((j) + (d).OLy - 1) * (d).nx + (long)((k) - 1) * (d).n2 + \
    (long)(t) * (d).n3)
 
+// Flattened, XCD-aware launch geometry.  A launch covers nz planes of ni*nj points
+// (i fastest, so a wave reads contiguous memory whatever the tile width); the
+// hardware deals workgroups round-robin over the 8 XCDs, so the linear block id
+// is remapped to give each XCD (own L2) one contiguous run of blocks: neighbouring
+// rows/levels, whose halos overlap, then hit the same L2.
+#define MG_NXCD 8
+__device__ __forceinline__ int mg_xcd_block() {
+  const int b = (int)blockIdx.x, n = (int)gridDim.x;
+  const int x = b % MG_NXCD, per = n / MG_NXCD, rem = n % MG_NXCD;
+  return x * per + (x < rem ? x : rem) + b / MG_NXCD;
+}
+#define MG_PLANE(i0, ni, j0, nj, zvar)                                                  \
+  int i, j, zvar;                                                                       \
+  {                                                                                     \
+    const int np_ = (ni) * (nj), nb_ = (np_ + (int)blockDim.x - 1) / (int)blockDim.x; \
+    const int lb_ = mg_xcd_block();                                                     \
+    const int q_ = (lb_ % nb_) * (int)blockDim.x + (int)threadIdx.x;                    \
+    zvar = lb_ / nb_;                                                                   \
+    if (q_ >= np_) return;                                                              \
+    i = (i0) + q_ % (ni);                                                               \
+    j = (j0) + q_ / (ni);                                                               \
+  }
+#define MG_PLANE_THREADS 256
+inline unsigned mg_plane_blocks(int ni, int nj, int nz) {
+  return (unsigned)(((ni) * (nj) + MG_PLANE_THREADS - 1) / MG_PLANE_THREADS * (nz));
+}
+
 // One tracer of TEMP_INTEGRATE / SALT_INTEGRATE (temp_integrate.F, salt_integrate.F).
 struct TracerArgs {
   const double *tr;     // tracer at the start of the step (halo-exchanged)

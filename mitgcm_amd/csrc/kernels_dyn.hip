@@ -28,9 +28,7 @@ __device__ __forceinline__ double hfacz(const Dims &d, const Fields &f, int i, i
 // CALC_PHI_HYD (calc_phi_hyd.F:175-327, OCEANIC, integr_GeoPot = 2, uniformFreeSurfLev,
 // gravFac = 1, alphaRho = rhoInSitu) on the dynamics range iMin..iMax = 0..sNx+1.
 __global__ void __launch_bounds__(256) k_phi_hyd(Dims d, Params p, Fields f) {
-  const int i = (int)(blockIdx.x * blockDim.x + threadIdx.x);
-  const int j = (int)(blockIdx.y * blockDim.y + threadIdx.y);
-  const int t = (int)blockIdx.z;
+  MG_PLANE(0, d.sNx + 2, 0, d.sNy + 2, t)
   if (i > d.sNx + 1 || j > d.sNy + 1) return;
   const double recip_rhoConst = 1.0 / p.rhoConst;
   double phF = 0.0;
@@ -47,10 +45,8 @@ __global__ void __launch_bounds__(256) k_phi_hyd(Dims d, Params p, Fields f) {
 }
 
 __global__ void __launch_bounds__(256) k_mom_step(Dims d, Params p, Fields f, const int *iterPtr) {
-  const int i = (int)(blockIdx.x * blockDim.x + threadIdx.x) + 1 - d.OLx;
-  const int j = (int)(blockIdx.y * blockDim.y + threadIdx.y) + 1 - d.OLy;
-  const int t = (int)blockIdx.z / d.Nr;
-  const int k = (int)blockIdx.z % d.Nr + 1;
+  MG_PLANE(1 - d.OLx, d.nx, 1 - d.OLy, d.ny, z)
+  const int t = z / d.Nr, k = z % d.Nr + 1;
   if (i > d.sNx + d.OLx || j > d.sNy + d.OLy) return;
   const int Nr = d.Nr;
   const int myIter = *iterPtr;
@@ -289,11 +285,8 @@ __global__ void __launch_bounds__(256) k_mom_step(Dims d, Params p, Fields f, co
 }
 
 hipError_t launch_mom_step(const Dims &d, const Params &p, const Fields &f, const int *iterPtr, hipStream_t s) {
-  dim3 pblk(64, 4, 1), pgrd((d.sNx + 2 + 63) / 64, (d.sNy + 2 + 3) / 4, d.nTiles);
-  hipLaunchKernelGGL(k_phi_hyd, pgrd, pblk, 0, s, d, p, f);
-  dim3 blk(64, 4, 1);
-  dim3 grd((d.nx + 63) / 64, (d.ny + 3) / 4, d.nTiles * d.Nr);
-  hipLaunchKernelGGL(k_mom_step, grd, blk, 0, s, d, p, f, iterPtr);
+  hipLaunchKernelGGL(k_phi_hyd, dim3(mg_plane_blocks(d.sNx + 2, d.sNy + 2, d.nTiles)), dim3(MG_PLANE_THREADS), 0, s, d, p, f);
+  hipLaunchKernelGGL(k_mom_step, dim3(mg_plane_blocks(d.nx, d.ny, d.nTiles * d.Nr)), dim3(MG_PLANE_THREADS), 0, s, d, p, f, iterPtr);
   return hipGetLastError();
 }
 

@@ -90,9 +90,7 @@ __device__ __forceinline__ double block_max(double v, double *red, int slot) {
 
 // CALC_DIV_GHAT over k = Nr..1 + free-surface term; cg2d_x = Bo_surf*etaN (full range).
 __global__ void __launch_bounds__(256) k_sfp_rhs(Dims d, Params p, Fields f) {
-  const int i = (int)(blockIdx.x * blockDim.x + threadIdx.x) + 1 - d.OLx;
-  const int j = (int)(blockIdx.y * blockDim.y + threadIdx.y) + 1 - d.OLy;
-  const int t = (int)blockIdx.z;
+  MG_PLANE(1 - d.OLx, d.nx, 1 - d.OLy, d.ny, t)
   if (i > d.sNx + d.OLx || j > d.sNy + d.OLy) return;
   const long q = MG_I2(d, i, j, t);
   f.cg2d_x[q] = f.Bo_surf[q] * f.etaN[q];
@@ -601,9 +599,7 @@ __global__ void __launch_bounds__(256) k_eta_update(Dims d, Fields f) {
 
 // MOMENTUM_CORRECTION_STEP over i=2-OLx..sNx+OLx, j=2-OLy..sNy+OLy, all k.
 __global__ void __launch_bounds__(256) k_correction(Dims d, Params p, Fields f) {
-  const int i = (int)(blockIdx.x * blockDim.x + threadIdx.x) + 2 - d.OLx;
-  const int j = (int)(blockIdx.y * blockDim.y + threadIdx.y) + 2 - d.OLy;
-  const int t = (int)blockIdx.z;
+  MG_PLANE(2 - d.OLx, d.nx - 1, 2 - d.OLy, d.ny - 1, t)
   if (i > d.sNx + d.OLx || j > d.sNy + d.OLy) return;
   const double psFac = p.pfFacMom * p.implicSurfPress;
   const long q = MG_I2(d, i, j, t);
@@ -623,9 +619,7 @@ __global__ void __launch_bounds__(256) k_correction(Dims d, Params p, Fields f) 
 
 // INTEGR_CONTINUITY -> INTEGRATE_FOR_W, interior columns, k = Nr..1.
 __global__ void __launch_bounds__(256) k_continuity(Dims d, Fields f) {
-  const int i = (int)(blockIdx.x * blockDim.x + threadIdx.x) + 1;
-  const int j = (int)(blockIdx.y * blockDim.y + threadIdx.y) + 1;
-  const int t = (int)blockIdx.z;
+  MG_PLANE(1, d.sNx, 1, d.sNy, t)
   if (i > d.sNx || j > d.sNy) return;
   const long q = MG_I2(d, i, j, t);
   double wBelow = 0.0;
@@ -648,9 +642,7 @@ __global__ void __launch_bounds__(256) k_continuity(Dims d, Fields f) {
 // no fresh-water flux): hDivFlow summed k = 1..Nr, dEtaHdt = -hDivFlow/rA,
 // etaN = etaH + implicDiv2Dflow*dEtaHdt*deltaTFreeSurf; then INTEGRATE_FOR_W as k_continuity.
 __global__ void __launch_bounds__(256) k_continuity_ec(Dims d, Params p, Fields f) {
-  const int i = (int)(blockIdx.x * blockDim.x + threadIdx.x) + 1;
-  const int j = (int)(blockIdx.y * blockDim.y + threadIdx.y) + 1;
-  const int t = (int)blockIdx.z;
+  MG_PLANE(1, d.sNx, 1, d.sNy, t)
   if (i > d.sNx || j > d.sNy) return;
   const long q = MG_I2(d, i, j, t);
   auto div = [&](int k) {
@@ -733,9 +725,7 @@ __global__ void __launch_bounds__(256) k_exch_etaH(Dims d, Fields f, const long 
 // expressions), then exactConserv's eta (into cg2d_b, see k_exch_etaH) and
 // INTEGRATE_FOR_W.  Halo velocities are left to the end-of-step EXCH.
 __global__ void __launch_bounds__(256) k_corr_cont(Dims d, Params p, Fields f) {
-  const int i = (int)(blockIdx.x * blockDim.x + threadIdx.x) + 1;
-  const int j = (int)(blockIdx.y * blockDim.y + threadIdx.y) + 1;
-  const int t = (int)blockIdx.z;
+  MG_PLANE(1, d.sNx, 1, d.sNy, t)
   if (i > d.sNx || j > d.sNy) return;
   const double psFac = p.pfFacMom * p.implicSurfPress;
   auto phiX = [&](int ii, int jj) {
@@ -795,7 +785,7 @@ __global__ void k_bump_counter(int *c, int nIncr) {
 
 // ------------------------------------------------------------------ launchers
 hipError_t launch_sfp_rhs(const Dims &d, const Params &p, const Fields &f, hipStream_t s) {
-  dim3 blk(64, 4, 1), grd((d.nx + 63) / 64, (d.ny + 3) / 4, d.nTiles);
+  const dim3 blk(MG_PLANE_THREADS), grd(mg_plane_blocks(d.nx, d.ny, d.nTiles));
   hipLaunchKernelGGL(k_sfp_rhs, grd, blk, 0, s, d, p, f);
   return hipGetLastError();
 }
@@ -868,19 +858,19 @@ hipError_t launch_eta_update(const Dims &d, const Fields &f, hipStream_t s) {
 }
 
 hipError_t launch_correction(const Dims &d, const Params &p, const Fields &f, hipStream_t s) {
-  dim3 blk(64, 4, 1), grd((d.sNx + 2 * d.OLx - 1 + 63) / 64, (d.sNy + 2 * d.OLy - 1 + 3) / 4, d.nTiles);
+  const dim3 blk(MG_PLANE_THREADS), grd(mg_plane_blocks(d.nx - 1, d.ny - 1, d.nTiles));
   hipLaunchKernelGGL(k_correction, grd, blk, 0, s, d, p, f);
   return hipGetLastError();
 }
 
 hipError_t launch_continuity(const Dims &d, const Fields &f, hipStream_t s) {
-  dim3 blk(64, 4, 1), grd((d.sNx + 63) / 64, (d.sNy + 3) / 4, d.nTiles);
+  const dim3 blk(MG_PLANE_THREADS), grd(mg_plane_blocks(d.sNx, d.sNy, d.nTiles));
   hipLaunchKernelGGL(k_continuity, grd, blk, 0, s, d, f);
   return hipGetLastError();
 }
 
 hipError_t launch_continuity_ec(const Dims &d, const Params &p, const Fields &f, hipStream_t s) {
-  dim3 blk(64, 4, 1), grd((d.sNx + 63) / 64, (d.sNy + 3) / 4, d.nTiles);
+  const dim3 blk(MG_PLANE_THREADS), grd(mg_plane_blocks(d.sNx, d.sNy, d.nTiles));
   hipLaunchKernelGGL(k_continuity_ec, grd, blk, 0, s, d, p, f);
   return hipGetLastError();
 }
@@ -906,7 +896,7 @@ hipError_t launch_exch_eta(const Dims &d, const Fields &f, const long *srcOf, bo
 }
 
 hipError_t launch_corr_cont(const Dims &d, const Params &p, const Fields &f, hipStream_t s) {
-  dim3 blk(64, 4, 1), grd((d.sNx + 63) / 64, (d.sNy + 3) / 4, d.nTiles);
+  const dim3 blk(MG_PLANE_THREADS), grd(mg_plane_blocks(d.sNx, d.sNy, d.nTiles));
   hipLaunchKernelGGL(k_corr_cont, grd, blk, 0, s, d, p, f);
   return hipGetLastError();
 }

@@ -33,9 +33,7 @@ __device__ __forceinline__ double rho_linear(const Params &p, const Fields &f, i
 }
 
 __global__ void __launch_bounds__(256) k_oceanic_phys(Dims d, Params p, Fields f) {
-  const int i = (int)(blockIdx.x * blockDim.x + threadIdx.x) + 1 - d.OLx;
-  const int j = (int)(blockIdx.y * blockDim.y + threadIdx.y) + 1 - d.OLy;
-  const int t = (int)blockIdx.z;
+  MG_PLANE(1 - d.OLx, d.nx, 1 - d.OLy, d.ny, t)
   if (i > d.sNx + d.OLx || j > d.sNy + d.OLy) return;
   const long q = MG_I2(d, i, j, t);
   f.surfaceForcingT[q] =
@@ -84,9 +82,8 @@ __device__ __forceinline__ double dst3fl_h(double uTr, double cfl, double tm2, d
 // loc1 = T - dT/(h drF rA) * (afx(i+1) - afx(i) - T*(uTrans(i+1) - uTrans(i))) * maskInC
 // on i = 2-OLx..sNx+OLx-1, every j; elsewhere loc1 = T.
 __global__ void __launch_bounds__(256) k_adv_x(Dims d, Fields f, TracerArgs a) {
-  const int i = (int)(blockIdx.x * blockDim.x + threadIdx.x) + 1 - d.OLx;
-  const int j = (int)(blockIdx.y * blockDim.y + threadIdx.y) + 1 - d.OLy;
-  const int t = (int)blockIdx.z / d.Nr, k = (int)blockIdx.z % d.Nr + 1;
+  MG_PLANE(1 - d.OLx, d.nx, 1 - d.OLy, d.ny, z)
+  const int t = z / d.Nr, k = z % d.Nr + 1;
   if (i > d.sNx + d.OLx || j > d.sNy + d.OLy) return;
   const double *__restrict__ T = a.tr;
   const long q3 = MG_I3(d, i, j, k, t);
@@ -111,9 +108,8 @@ __global__ void __launch_bounds__(256) k_adv_x(Dims d, Fields f, TracerArgs a) {
 // Y pass on the interior (the only rows the vertical pass and the tendency use):
 // loc2 = loc1 - dT/(h drF rA) * (afy(j+1) - afy(j) - T*(vTrans(j+1) - vTrans(j))) * maskInC
 __global__ void __launch_bounds__(256) k_adv_y(Dims d, Fields f, TracerArgs a) {
-  const int i = (int)(blockIdx.x * blockDim.x + threadIdx.x) + 1;
-  const int j = (int)(blockIdx.y * blockDim.y + threadIdx.y) + 1;
-  const int t = (int)blockIdx.z / d.Nr, k = (int)blockIdx.z % d.Nr + 1;
+  MG_PLANE(1, d.sNx, 1, d.sNy, z)
+  const int t = z / d.Nr, k = z % d.Nr + 1;
   if (i > d.sNx || j > d.sNy) return;
   const double *__restrict__ L1 = f.advScr1;
   const long q3 = MG_I3(d, i, j, k, t);
@@ -133,9 +129,8 @@ __global__ void __launch_bounds__(256) k_adv_y(Dims d, Fields f, TracerArgs a) {
 
 // vertical pass + advective tendency gAdv = (loc - T)/dT (gad_advection.F k = Nr..1 loop)
 __global__ void __launch_bounds__(256) k_adv_r(Dims d, Params p, Fields f, TracerArgs a) {
-  const int i = (int)(blockIdx.x * blockDim.x + threadIdx.x) + 1;
-  const int j = (int)(blockIdx.y * blockDim.y + threadIdx.y) + 1;
-  const int t = (int)blockIdx.z / d.Nr, k = (int)blockIdx.z % d.Nr + 1;
+  MG_PLANE(1, d.sNx, 1, d.sNy, z)
+  const int t = z / d.Nr, k = z % d.Nr + 1;
   if (i > d.sNx || j > d.sNy) return;
   const int Nr = d.Nr;
   const double *__restrict__ L2 = f.advScr2;
@@ -172,10 +167,8 @@ __global__ void __launch_bounds__(256) k_adv_r(Dims d, Params p, Fields f, Trace
 // writes gNm1 (AB tracers) and gTscr = tracer + dTtracer*gT (the right-hand side of
 // the implicit vertical solve, or the new tracer with explicit vertical diffusion).
 __global__ void __launch_bounds__(256) k_tracer_rhs(Dims d, Params p, Fields f, TracerArgs a, const int *iterPtr) {
-  const int i = (int)(blockIdx.x * blockDim.x + threadIdx.x) + 1;
-  const int j = (int)(blockIdx.y * blockDim.y + threadIdx.y) + 1;
-  const int t = (int)blockIdx.z / d.Nr;
-  const int k = (int)blockIdx.z % d.Nr + 1;
+  MG_PLANE(1, d.sNx, 1, d.sNy, z)
+  const int t = z / d.Nr, k = z % d.Nr + 1;
   if (i > d.sNx || j > d.sNy) return;
   const int Nr = d.Nr;
   const int myIter = *iterPtr;
@@ -262,9 +255,7 @@ __global__ void __launch_bounds__(256) k_tracer_rhs(Dims d, Params p, Fields f, 
 // GAD_IMPLICIT_R (implicitDiffusion) + SOLVE_TRIDIAGONAL (Thomas) + CYCLE_TRACER,
 // one thread per interior column; writes the new tracer into its other buffer.
 __global__ void __launch_bounds__(256) k_tracer_impl(Dims d, Params p, Fields f, TracerArgs a) {
-  const int i = (int)(blockIdx.x * blockDim.x + threadIdx.x) + 1;
-  const int j = (int)(blockIdx.y * blockDim.y + threadIdx.y) + 1;
-  const int t = (int)blockIdx.z;
+  MG_PLANE(1, d.sNx, 1, d.sNy, t)
   if (i > d.sNx || j > d.sNy) return;
   const int Nr = d.Nr;
 #define G3(a_, ii, jj, kk) f.a_[MG_I3(d, ii, jj, kk, t)]
@@ -305,23 +296,22 @@ __global__ void __launch_bounds__(256) k_tracer_impl(Dims d, Params p, Fields f,
 }
 
 hipError_t launch_oceanic_phys(const Dims &d, const Params &p, const Fields &f, hipStream_t s) {
-  dim3 blk(64, 4, 1), grd((d.nx + 63) / 64, (d.ny + 3) / 4, d.nTiles);
-  hipLaunchKernelGGL(k_oceanic_phys, grd, blk, 0, s, d, p, f);
+  hipLaunchKernelGGL(k_oceanic_phys, dim3(mg_plane_blocks(d.nx, d.ny, d.nTiles)), dim3(MG_PLANE_THREADS), 0, s, d, p, f);
   return hipGetLastError();
 }
 
 hipError_t launch_tracer_step(const Dims &d, const Params &p, const Fields &f, const TracerArgs &a, const int *iterPtr,
                               hipStream_t s) {
-  dim3 blk(64, 4, 1), grd((d.sNx + 63) / 64, (d.sNy + 3) / 4, d.nTiles * d.Nr);
+  const dim3 blk(MG_PLANE_THREADS), grd(mg_plane_blocks(d.sNx, d.sNy, d.nTiles * d.Nr));
   if (a.multiDim) {
-    dim3 fgrd((d.nx + 63) / 64, (d.ny + 3) / 4, d.nTiles * d.Nr);
+    const dim3 fgrd(mg_plane_blocks(d.nx, d.ny, d.nTiles * d.Nr));
     hipLaunchKernelGGL(k_adv_x, fgrd, blk, 0, s, d, f, a);
     hipLaunchKernelGGL(k_adv_y, grd, blk, 0, s, d, f, a);
     hipLaunchKernelGGL(k_adv_r, grd, blk, 0, s, d, p, f, a);
   }
   hipLaunchKernelGGL(k_tracer_rhs, grd, blk, 0, s, d, p, f, a, iterPtr);
   if (p.implicitDiffusion) {
-    dim3 cgrd((d.sNx + 63) / 64, (d.sNy + 3) / 4, d.nTiles);
+    const dim3 cgrd(mg_plane_blocks(d.sNx, d.sNy, d.nTiles));
     hipLaunchKernelGGL(k_tracer_impl, cgrd, blk, 0, s, d, p, f, a);
   }
   return hipGetLastError();
