@@ -34,9 +34,20 @@ constexpr int CG_WAVES = CG_THREADS / 64;
 // the row's sum, bit-identical across the row (each step adds a commuted pair).
 template <int CTRL>
 __device__ __forceinline__ double dpp_f64(double v) {
+  // every pattern used here reads a valid lane for every lane (row/bank masks 0xF),
+  // so the "old" operand is dead: tie it to the source instead of a zeroed register
   const long long b = __builtin_bit_cast(long long, v);
-  const int lo = __builtin_amdgcn_update_dpp(0, (int)(b & 0xffffffff), CTRL, 0xF, 0xF, false);
-  const int hi = __builtin_amdgcn_update_dpp(0, (int)(b >> 32), CTRL, 0xF, 0xF, false);
+  const int lo = __builtin_amdgcn_mov_dpp((int)(b & 0xffffffff), CTRL, 0xF, 0xF, true);
+  const int hi = __builtin_amdgcn_mov_dpp((int)(b >> 32), CTRL, 0xF, 0xF, true);
+  return __builtin_bit_cast(double, ((long long)hi << 32) | (unsigned)lo);
+}
+// row_bcast15 (rows 1,3 <- lane 15 of rows 0,2) / row_bcast31 (rows 2,3 <- lane 31);
+// rows outside ROWMASK receive +0.0, which leaves their partial unchanged.
+template <int CTRL, int ROWMASK>
+__device__ __forceinline__ double dpp_bcast_f64(double v) {
+  const long long b = __builtin_bit_cast(long long, v);
+  const int lo = __builtin_amdgcn_update_dpp(0, (int)(b & 0xffffffff), CTRL, ROWMASK, 0xF, false);
+  const int hi = __builtin_amdgcn_update_dpp(0, (int)(b >> 32), CTRL, ROWMASK, 0xF, false);
   return __builtin_bit_cast(double, ((long long)hi << 32) | (unsigned)lo);
 }
 __device__ __forceinline__ double row_sum16(double v) {
@@ -59,10 +70,14 @@ __device__ __forceinline__ double lane_f64(double v, int l) {
   const int hi = __builtin_amdgcn_readlane((int)(b >> 32), l);
   return __builtin_bit_cast(double, ((long long)hi << 32) | (unsigned)lo);
 }
-// wave sum, identical in every lane: rows by DPP, then (r0+r1)+(r2+r3)
+// wave sum, uniform (SGPR) result: rows by DPP, then row1 += row0, row3 += row2
+// (row_bcast15) and rows 2,3 += lane 31 (row_bcast31): lane 63 holds
+// (r3+r2)+(r1+r0), the same value as (r0+r1)+(r2+r3).
 __device__ __forceinline__ double wave_sum(double v) {
   v = row_sum16(v);
-  return (lane_f64(v, 0) + lane_f64(v, 16)) + (lane_f64(v, 32) + lane_f64(v, 48));
+  v = v + dpp_bcast_f64<0x142, 0xA>(v);
+  v = v + dpp_bcast_f64<0x143, 0xC>(v);
+  return lane_f64(v, 63);
 }
 __device__ __forceinline__ double wave_max(double v) {
   v = row_max16(v);
