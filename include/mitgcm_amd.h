@@ -83,6 +83,27 @@ int mgcm_prepare(mgcm_model *m);
  * asynchronously on the model's stream (captured once into a hipGraph). */
 int mgcm_forward_step(mgcm_model *m, int nsteps);
 /* Wait for all queued device work. */
+/* ---- tile-sharded runs (one process per GPU, mitgcm_amd/parallel.py) ----------
+ * Every process holds the whole domain's arrays; the 3-D kernels step only tiles
+ * [t0, t0+nT) (the reference's myBxLo..myBxHi / process tile set).
+ * The 2-D pressure solve is replicated on every process over the gathered RHS, so
+ * its sums are the single-GPU sums and results are bit-identical at any N. */
+int mgcm_set_tile_range(mgcm_model *m, int t0, int nT);
+/* Run on `stream` (a hipStream_t, e.g. the caller's collective stream); NULL = own. */
+int mgcm_set_stream(mgcm_model *m, void *stream);
+/* Number of fields DO_FIELDS_BLOCKING_EXCHANGES moves (u, v, w[, theta][, salt]). */
+int mgcm_exchange_nfields(mgcm_model *m);
+/* Gather (unpack=0) / scatter (unpack=1) those fields at n device-resident 2-D
+ * offsets idx (t*n2 + j*nx + i), all levels: buf[(f*Nr + k)*n + h]. */
+int mgcm_halo_pack(mgcm_model *m, const long *idx, long n, double *buf, int unpack);
+/* Device-to-device copy of tiles [t0, t0+nT) of a 2-D/3-D field to (toField=0) or
+ * from (toField=1) the device buffer buf, on the model's stream. */
+int mgcm_tile_copy(mgcm_model *m, const char *name, int t0, int nT, void *buf, int toField);
+/* Reset the per-step solve records before a sequence of mgcm_step_phase steps. */
+int mgcm_begin_steps(mgcm_model *m);
+/* One FORWARD_STEP split at its exchange points, phase = 1..4 (see model.hip). */
+int mgcm_step_phase(mgcm_model *m, int phase);
+
 int mgcm_sync(mgcm_model *m);
 
 /* Device CG2D on fields of this model (cg2d.F:13 semantics; b is normalised in

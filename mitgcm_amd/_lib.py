@@ -49,6 +49,13 @@ def lib():
         "mgcm_solve_stats": (ci, [vp, ci, PD, PD, PI, PD]),
         "mgcm_kernel_ms": (cd, [vp, cs, PI]),
         "mgcm_kernel_timing": (None, [vp, ci]),
+        "mgcm_set_tile_range": (ci, [vp, ci, ci]),
+        "mgcm_set_stream": (ci, [vp, vp]),
+        "mgcm_exchange_nfields": (ci, [vp]),
+        "mgcm_halo_pack": (ci, [vp, vp, cl, vp, ci]),
+        "mgcm_begin_steps": (ci, [vp]),
+        "mgcm_tile_copy": (ci, [vp, cs, ci, ci, vp, ci]),
+        "mgcm_step_phase": (ci, [vp, ci]),
         "ini_cg2d_amd_": (None, [PI] * 6 + [PD] * 8 + [PI]),
         "cg2d_amd_": (None, [PD, PD, PD, PD, PD, PI, PI, PI]),
     }
@@ -64,7 +71,9 @@ EXPORTS = ["mgcm_create", "mgcm_destroy", "mgcm_last_error", "mgcm_set_param", "
            "mgcm_get", "mgcm_device_ptr", "mgcm_set_halo_map", "mgcm_init", "mgcm_dynamics", "mgcm_thermodynamics",
            "mgcm_solve_for_pressure", "mgcm_momentum_correction_step", "mgcm_integr_continuity",
            "mgcm_blocking_exchanges", "mgcm_prepare", "mgcm_forward_step", "mgcm_sync", "mgcm_cg2d", "mgcm_solve_stats",
-           "mgcm_kernel_ms", "mgcm_kernel_timing", "ini_cg2d_amd_", "cg2d_amd_"]
+           "mgcm_kernel_ms", "mgcm_kernel_timing", "mgcm_set_tile_range", "mgcm_set_stream",
+           "mgcm_exchange_nfields", "mgcm_halo_pack", "mgcm_tile_copy", "mgcm_begin_steps", "mgcm_step_phase", "ini_cg2d_amd_",
+           "cg2d_amd_"]
 
 
 def check(rc, what):

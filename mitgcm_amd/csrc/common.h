@@ -14,6 +14,7 @@ namespace mgcm {
 
 struct Dims {
   int sNx, sNy, OLx, OLy, Nr, nSx, nSy, nTiles;
+  int t0, nT;   // tiles this process steps (tile-sharded runs); 0, nTiles otherwise
   int nx, ny;
   long n2, n3;
 };

@@ -28,7 +28,8 @@ __device__ __forceinline__ double hfacz(const Dims &d, const Fields &f, int i, i
 // CALC_PHI_HYD (calc_phi_hyd.F:175-327, OCEANIC, integr_GeoPot = 2, uniformFreeSurfLev,
 // gravFac = 1, alphaRho = rhoInSitu) on the dynamics range iMin..iMax = 0..sNx+1.
 __global__ void __launch_bounds__(256) k_phi_hyd(Dims d, Params p, Fields f) {
-  MG_PLANE(0, d.sNx + 2, 0, d.sNy + 2, t)
+  MG_PLANE(0, d.sNx + 2, 0, d.sNy + 2, tz)
+  const int t = d.t0 + tz;
   if (i > d.sNx + 1 || j > d.sNy + 1) return;
   const double recip_rhoConst = 1.0 / p.rhoConst;
   double phF = 0.0;
@@ -46,7 +47,7 @@ __global__ void __launch_bounds__(256) k_phi_hyd(Dims d, Params p, Fields f) {
 
 __global__ void __launch_bounds__(256) k_mom_step(Dims d, Params p, Fields f, const int *iterPtr) {
   MG_PLANE(1 - d.OLx, d.nx, 1 - d.OLy, d.ny, z)
-  const int t = z / d.Nr, k = z % d.Nr + 1;
+  const int t = d.t0 + z / d.Nr, k = z % d.Nr + 1;
   if (i > d.sNx + d.OLx || j > d.sNy + d.OLy) return;
   const int Nr = d.Nr;
   const int myIter = *iterPtr;
@@ -285,8 +286,8 @@ __global__ void __launch_bounds__(256) k_mom_step(Dims d, Params p, Fields f, co
 }
 
 hipError_t launch_mom_step(const Dims &d, const Params &p, const Fields &f, const int *iterPtr, hipStream_t s) {
-  hipLaunchKernelGGL(k_phi_hyd, dim3(mg_plane_blocks(d.sNx + 2, d.sNy + 2, d.nTiles)), dim3(MG_PLANE_THREADS), 0, s, d, p, f);
-  hipLaunchKernelGGL(k_mom_step, dim3(mg_plane_blocks(d.nx, d.ny, d.nTiles * d.Nr)), dim3(MG_PLANE_THREADS), 0, s, d, p, f, iterPtr);
+  hipLaunchKernelGGL(k_phi_hyd, dim3(mg_plane_blocks(d.sNx + 2, d.sNy + 2, d.nT)), dim3(MG_PLANE_THREADS), 0, s, d, p, f);
+  hipLaunchKernelGGL(k_mom_step, dim3(mg_plane_blocks(d.nx, d.ny, d.nT * d.Nr)), dim3(MG_PLANE_THREADS), 0, s, d, p, f, iterPtr);
   return hipGetLastError();
 }
 

@@ -105,7 +105,8 @@ __device__ __forceinline__ double block_max(double v, double *red, int slot) {
 
 // CALC_DIV_GHAT over k = Nr..1 + free-surface term; cg2d_x = Bo_surf*etaN (full range).
 __global__ void __launch_bounds__(256) k_sfp_rhs(Dims d, Params p, Fields f) {
-  MG_PLANE(1 - d.OLx, d.nx, 1 - d.OLy, d.ny, t)
+  MG_PLANE(1 - d.OLx, d.nx, 1 - d.OLy, d.ny, tz)
+  const int t = d.t0 + tz;
   if (i > d.sNx + d.OLx || j > d.sNy + d.OLy) return;
   const long q = MG_I2(d, i, j, t);
   f.cg2d_x[q] = f.Bo_surf[q] * f.etaN[q];
@@ -614,7 +615,8 @@ __global__ void __launch_bounds__(256) k_eta_update(Dims d, Fields f) {
 
 // MOMENTUM_CORRECTION_STEP over i=2-OLx..sNx+OLx, j=2-OLy..sNy+OLy, all k.
 __global__ void __launch_bounds__(256) k_correction(Dims d, Params p, Fields f) {
-  MG_PLANE(2 - d.OLx, d.nx - 1, 2 - d.OLy, d.ny - 1, t)
+  MG_PLANE(2 - d.OLx, d.nx - 1, 2 - d.OLy, d.ny - 1, tz)
+  const int t = d.t0 + tz;
   if (i > d.sNx + d.OLx || j > d.sNy + d.OLy) return;
   const double psFac = p.pfFacMom * p.implicSurfPress;
   const long q = MG_I2(d, i, j, t);
@@ -634,7 +636,8 @@ __global__ void __launch_bounds__(256) k_correction(Dims d, Params p, Fields f) 
 
 // INTEGR_CONTINUITY -> INTEGRATE_FOR_W, interior columns, k = Nr..1.
 __global__ void __launch_bounds__(256) k_continuity(Dims d, Fields f) {
-  MG_PLANE(1, d.sNx, 1, d.sNy, t)
+  MG_PLANE(1, d.sNx, 1, d.sNy, tz)
+  const int t = d.t0 + tz;
   if (i > d.sNx || j > d.sNy) return;
   const long q = MG_I2(d, i, j, t);
   double wBelow = 0.0;
@@ -657,7 +660,8 @@ __global__ void __launch_bounds__(256) k_continuity(Dims d, Fields f) {
 // no fresh-water flux): hDivFlow summed k = 1..Nr, dEtaHdt = -hDivFlow/rA,
 // etaN = etaH + implicDiv2Dflow*dEtaHdt*deltaTFreeSurf; then INTEGRATE_FOR_W as k_continuity.
 __global__ void __launch_bounds__(256) k_continuity_ec(Dims d, Params p, Fields f) {
-  MG_PLANE(1, d.sNx, 1, d.sNy, t)
+  MG_PLANE(1, d.sNx, 1, d.sNy, tz)
+  const int t = d.t0 + tz;
   if (i > d.sNx || j > d.sNy) return;
   const long q = MG_I2(d, i, j, t);
   auto div = [&](int k) {
@@ -740,7 +744,8 @@ __global__ void __launch_bounds__(256) k_exch_etaH(Dims d, Fields f, const long 
 // expressions), then exactConserv's eta (into cg2d_b, see k_exch_etaH) and
 // INTEGRATE_FOR_W.  Halo velocities are left to the end-of-step EXCH.
 __global__ void __launch_bounds__(256) k_corr_cont(Dims d, Params p, Fields f) {
-  MG_PLANE(1, d.sNx, 1, d.sNy, t)
+  MG_PLANE(1, d.sNx, 1, d.sNy, tz)
+  const int t = d.t0 + tz;
   if (i > d.sNx || j > d.sNy) return;
   const double psFac = p.pfFacMom * p.implicSurfPress;
   auto phiX = [&](int ii, int jj) {
@@ -794,13 +799,28 @@ __global__ void __launch_bounds__(256) k_corr_cont(Dims d, Params p, Fields f) {
   }
 }
 
+// Tile-sharded runs: gather (pack) / scatter (unpack) the halo-source points a peer
+// needs, for every exchanged field and level: buf[(f*Nr + k)*n + h] <-> field at 2-D
+// offset idx[h] (t*n2 + local) of level k.
+__global__ void __launch_bounds__(256) k_halo_pack(Dims d, XFields x, const long *__restrict__ idx, long n,
+                                                   double *__restrict__ buf, int unpack) {
+  const long h = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  const int k = (int)blockIdx.y, fi = (int)blockIdx.z;
+  if (h >= n || fi >= x.n || k >= x.nz[fi]) return;
+  const long g = idx[h], t = g / d.n2, l = g % d.n2;
+  double *a = x.p[fi] + t * d.n2 * x.nz[fi] + (long)k * d.n2 + l;
+  double *b = buf + ((long)fi * d.Nr + k) * n + h;
+  if (unpack) *a = *b;
+  else *b = *a;
+}
+
 __global__ void k_bump_counter(int *c, int nIncr) {
   if (threadIdx.x == 0) { c[0] += nIncr; c[1] += 1; }
 }
 
 // ------------------------------------------------------------------ launchers
 hipError_t launch_sfp_rhs(const Dims &d, const Params &p, const Fields &f, hipStream_t s) {
-  const dim3 blk(MG_PLANE_THREADS), grd(mg_plane_blocks(d.nx, d.ny, d.nTiles));
+  const dim3 blk(MG_PLANE_THREADS), grd(mg_plane_blocks(d.nx, d.ny, d.nT));
   hipLaunchKernelGGL(k_sfp_rhs, grd, blk, 0, s, d, p, f);
   return hipGetLastError();
 }
@@ -873,19 +893,19 @@ hipError_t launch_eta_update(const Dims &d, const Fields &f, hipStream_t s) {
 }
 
 hipError_t launch_correction(const Dims &d, const Params &p, const Fields &f, hipStream_t s) {
-  const dim3 blk(MG_PLANE_THREADS), grd(mg_plane_blocks(d.nx - 1, d.ny - 1, d.nTiles));
+  const dim3 blk(MG_PLANE_THREADS), grd(mg_plane_blocks(d.nx - 1, d.ny - 1, d.nT));
   hipLaunchKernelGGL(k_correction, grd, blk, 0, s, d, p, f);
   return hipGetLastError();
 }
 
 hipError_t launch_continuity(const Dims &d, const Fields &f, hipStream_t s) {
-  const dim3 blk(MG_PLANE_THREADS), grd(mg_plane_blocks(d.sNx, d.sNy, d.nTiles));
+  const dim3 blk(MG_PLANE_THREADS), grd(mg_plane_blocks(d.sNx, d.sNy, d.nT));
   hipLaunchKernelGGL(k_continuity, grd, blk, 0, s, d, f);
   return hipGetLastError();
 }
 
 hipError_t launch_continuity_ec(const Dims &d, const Params &p, const Fields &f, hipStream_t s) {
-  const dim3 blk(MG_PLANE_THREADS), grd(mg_plane_blocks(d.sNx, d.sNy, d.nTiles));
+  const dim3 blk(MG_PLANE_THREADS), grd(mg_plane_blocks(d.sNx, d.sNy, d.nT));
   hipLaunchKernelGGL(k_continuity_ec, grd, blk, 0, s, d, p, f);
   return hipGetLastError();
 }
@@ -911,8 +931,16 @@ hipError_t launch_exch_eta(const Dims &d, const Fields &f, const long *srcOf, bo
 }
 
 hipError_t launch_corr_cont(const Dims &d, const Params &p, const Fields &f, hipStream_t s) {
-  const dim3 blk(MG_PLANE_THREADS), grd(mg_plane_blocks(d.sNx, d.sNy, d.nTiles));
+  const dim3 blk(MG_PLANE_THREADS), grd(mg_plane_blocks(d.sNx, d.sNy, d.nT));
   hipLaunchKernelGGL(k_corr_cont, grd, blk, 0, s, d, p, f);
+  return hipGetLastError();
+}
+
+hipError_t launch_halo_pack(const Dims &d, const XFields &x, const long *idx, long n, double *buf, int unpack,
+                            hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_halo_pack, dim3((unsigned)((n + 255) / 256), d.Nr, x.n), dim3(256), 0, s, d, x, idx, n, buf,
+                     unpack);
   return hipGetLastError();
 }
 

@@ -33,7 +33,8 @@ __device__ __forceinline__ double rho_linear(const Params &p, const Fields &f, i
 }
 
 __global__ void __launch_bounds__(256) k_oceanic_phys(Dims d, Params p, Fields f) {
-  MG_PLANE(1 - d.OLx, d.nx, 1 - d.OLy, d.ny, t)
+  MG_PLANE(1 - d.OLx, d.nx, 1 - d.OLy, d.ny, tz)
+  const int t = d.t0 + tz;
   if (i > d.sNx + d.OLx || j > d.sNy + d.OLy) return;
   const long q = MG_I2(d, i, j, t);
   f.surfaceForcingT[q] =
@@ -83,7 +84,7 @@ __device__ __forceinline__ double dst3fl_h(double uTr, double cfl, double tm2, d
 // on i = 2-OLx..sNx+OLx-1, every j; elsewhere loc1 = T.
 __global__ void __launch_bounds__(256) k_adv_x(Dims d, Fields f, TracerArgs a) {
   MG_PLANE(1 - d.OLx, d.nx, 1 - d.OLy, d.ny, z)
-  const int t = z / d.Nr, k = z % d.Nr + 1;
+  const int t = d.t0 + z / d.Nr, k = z % d.Nr + 1;
   if (i > d.sNx + d.OLx || j > d.sNy + d.OLy) return;
   const double *__restrict__ T = a.tr;
   const long q3 = MG_I3(d, i, j, k, t);
@@ -109,7 +110,7 @@ __global__ void __launch_bounds__(256) k_adv_x(Dims d, Fields f, TracerArgs a) {
 // loc2 = loc1 - dT/(h drF rA) * (afy(j+1) - afy(j) - T*(vTrans(j+1) - vTrans(j))) * maskInC
 __global__ void __launch_bounds__(256) k_adv_y(Dims d, Fields f, TracerArgs a) {
   MG_PLANE(1, d.sNx, 1, d.sNy, z)
-  const int t = z / d.Nr, k = z % d.Nr + 1;
+  const int t = d.t0 + z / d.Nr, k = z % d.Nr + 1;
   if (i > d.sNx || j > d.sNy) return;
   const double *__restrict__ L1 = f.advScr1;
   const long q3 = MG_I3(d, i, j, k, t);
@@ -130,7 +131,7 @@ __global__ void __launch_bounds__(256) k_adv_y(Dims d, Fields f, TracerArgs a) {
 // vertical pass + advective tendency gAdv = (loc - T)/dT (gad_advection.F k = Nr..1 loop)
 __global__ void __launch_bounds__(256) k_adv_r(Dims d, Params p, Fields f, TracerArgs a) {
   MG_PLANE(1, d.sNx, 1, d.sNy, z)
-  const int t = z / d.Nr, k = z % d.Nr + 1;
+  const int t = d.t0 + z / d.Nr, k = z % d.Nr + 1;
   if (i > d.sNx || j > d.sNy) return;
   const int Nr = d.Nr;
   const double *__restrict__ L2 = f.advScr2;
@@ -168,7 +169,7 @@ __global__ void __launch_bounds__(256) k_adv_r(Dims d, Params p, Fields f, Trace
 // the implicit vertical solve, or the new tracer with explicit vertical diffusion).
 __global__ void __launch_bounds__(256) k_tracer_rhs(Dims d, Params p, Fields f, TracerArgs a, const int *iterPtr) {
   MG_PLANE(1, d.sNx, 1, d.sNy, z)
-  const int t = z / d.Nr, k = z % d.Nr + 1;
+  const int t = d.t0 + z / d.Nr, k = z % d.Nr + 1;
   if (i > d.sNx || j > d.sNy) return;
   const int Nr = d.Nr;
   const int myIter = *iterPtr;
@@ -255,7 +256,8 @@ __global__ void __launch_bounds__(256) k_tracer_rhs(Dims d, Params p, Fields f, 
 // GAD_IMPLICIT_R (implicitDiffusion) + SOLVE_TRIDIAGONAL (Thomas) + CYCLE_TRACER,
 // one thread per interior column; writes the new tracer into its other buffer.
 __global__ void __launch_bounds__(256) k_tracer_impl(Dims d, Params p, Fields f, TracerArgs a) {
-  MG_PLANE(1, d.sNx, 1, d.sNy, t)
+  MG_PLANE(1, d.sNx, 1, d.sNy, tz)
+  const int t = d.t0 + tz;
   if (i > d.sNx || j > d.sNy) return;
   const int Nr = d.Nr;
 #define G3(a_, ii, jj, kk) f.a_[MG_I3(d, ii, jj, kk, t)]
@@ -296,22 +298,22 @@ __global__ void __launch_bounds__(256) k_tracer_impl(Dims d, Params p, Fields f,
 }
 
 hipError_t launch_oceanic_phys(const Dims &d, const Params &p, const Fields &f, hipStream_t s) {
-  hipLaunchKernelGGL(k_oceanic_phys, dim3(mg_plane_blocks(d.nx, d.ny, d.nTiles)), dim3(MG_PLANE_THREADS), 0, s, d, p, f);
+  hipLaunchKernelGGL(k_oceanic_phys, dim3(mg_plane_blocks(d.nx, d.ny, d.nT)), dim3(MG_PLANE_THREADS), 0, s, d, p, f);
   return hipGetLastError();
 }
 
 hipError_t launch_tracer_step(const Dims &d, const Params &p, const Fields &f, const TracerArgs &a, const int *iterPtr,
                               hipStream_t s) {
-  const dim3 blk(MG_PLANE_THREADS), grd(mg_plane_blocks(d.sNx, d.sNy, d.nTiles * d.Nr));
+  const dim3 blk(MG_PLANE_THREADS), grd(mg_plane_blocks(d.sNx, d.sNy, d.nT * d.Nr));
   if (a.multiDim) {
-    const dim3 fgrd(mg_plane_blocks(d.nx, d.ny, d.nTiles * d.Nr));
+    const dim3 fgrd(mg_plane_blocks(d.nx, d.ny, d.nT * d.Nr));
     hipLaunchKernelGGL(k_adv_x, fgrd, blk, 0, s, d, f, a);
     hipLaunchKernelGGL(k_adv_y, grd, blk, 0, s, d, f, a);
     hipLaunchKernelGGL(k_adv_r, grd, blk, 0, s, d, p, f, a);
   }
   hipLaunchKernelGGL(k_tracer_rhs, grd, blk, 0, s, d, p, f, a, iterPtr);
   if (p.implicitDiffusion) {
-    const dim3 cgrd(mg_plane_blocks(d.sNx, d.sNy, d.nTiles));
+    const dim3 cgrd(mg_plane_blocks(d.sNx, d.sNy, d.nT));
     hipLaunchKernelGGL(k_tracer_impl, cgrd, blk, 0, s, d, p, f, a);
   }
   return hipGetLastError();

@@ -36,6 +36,7 @@ hipError_t launch_bump_counter(int *, int, hipStream_t);
 hipError_t launch_exchange_multi(const Dims &, const XFields &, const long *, int, int *, hipStream_t);
 hipError_t launch_exch_eta(const Dims &, const Fields &, const long *, bool, hipStream_t);
 hipError_t launch_corr_cont(const Dims &, const Params &, const Fields &, hipStream_t);
+hipError_t launch_halo_pack(const Dims &, const XFields &, const long *, long, double *, int, hipStream_t);
 hipError_t launch_oceanic_phys(const Dims &, const Params &, const Fields &, hipStream_t);
 hipError_t launch_tracer_step(const Dims &, const Params &, const Fields &, const TracerArgs &, const int *, hipStream_t);
 hipError_t launch_continuity_ec(const Dims &, const Params &, const Fields &, hipStream_t);
@@ -122,6 +123,7 @@ struct mgcm_model {
   Fields f{};
   int device = 0;
   hipStream_t stream = nullptr;
+  hipStream_t ownStream = nullptr;   // created by mgcm_create; `stream` may be a caller's
   std::vector<void *> allocs;
   // extra parameters kept on host only
   std::map<std::string, double> extra;
@@ -238,15 +240,21 @@ static void build_latlon_halo(mgcm_model *m) {
 static int upload_halo(mgcm_model *m) {
   if (m->d_halo) { hipFree(m->d_halo); m->d_halo = nullptr; }
   if (m->d_srcOf) { hipFree(m->d_srcOf); m->d_srcOf = nullptr; }
-  m->nHalo = (int)(m->h_halo.size() / 2);
   const long N2 = m->d.n2 * m->d.nTiles;
   std::vector<long> srcOf(N2, -1);
   for (size_t h = 0; h + 1 < m->h_halo.size(); h += 2) srcOf[m->h_halo[h]] = m->h_halo[h + 1];
   HIPCHK(hipMalloc(&m->d_srcOf, N2 * sizeof(long)));
   HIPCHK(hipMemcpy(m->d_srcOf, srcOf.data(), N2 * sizeof(long), hipMemcpyHostToDevice));
+  // the 3-D exchange kernels refresh the halos of this process's tiles only
+  // (tile-sharded runs receive the remote sources first, mgcm_halo_unpack)
+  std::vector<long> loc;
+  const long lo = (long)m->d.t0 * m->d.n2, hi = (long)(m->d.t0 + m->d.nT) * m->d.n2;
+  for (size_t h = 0; h + 1 < m->h_halo.size(); h += 2)
+    if (m->h_halo[h] >= lo && m->h_halo[h] < hi) { loc.push_back(m->h_halo[h]); loc.push_back(m->h_halo[h + 1]); }
+  m->nHalo = (int)(loc.size() / 2);
   if (m->nHalo == 0) return 0;
-  HIPCHK(hipMalloc(&m->d_halo, m->h_halo.size() * sizeof(long)));
-  HIPCHK(hipMemcpy(m->d_halo, m->h_halo.data(), m->h_halo.size() * sizeof(long), hipMemcpyHostToDevice));
+  HIPCHK(hipMalloc(&m->d_halo, loc.size() * sizeof(long)));
+  HIPCHK(hipMemcpy(m->d_halo, loc.data(), loc.size() * sizeof(long), hipMemcpyHostToDevice));
   return 0;
 }
 
@@ -365,6 +373,7 @@ mgcm_model *mgcm_create(int sNx, int sNy, int OLx, int OLy, int Nr, int nSx, int
   Dims &d = m->d;
   d.sNx = sNx; d.sNy = sNy; d.OLx = OLx; d.OLy = OLy; d.Nr = Nr; d.nSx = nSx; d.nSy = nSy; d.nTiles = nSx * nSy;
   d.nx = sNx + 2 * OLx; d.ny = sNy + 2 * OLy; d.n2 = (long)d.nx * d.ny; d.n3 = d.n2 * Nr;
+  d.t0 = 0; d.nT = d.nTiles;
   // defaults (model/src/set_defaults.F, resolved by ini_parms.F)
   Params &p = m->p;
   p.abEps = 0.01; p.rhoConst = 999.8; p.gBaro = 9.81; p.sideDragFactor = 2.0; p.freeSurfFac = 1.0;
@@ -376,11 +385,12 @@ mgcm_model *mgcm_create(int sNx, int sNy, int OLx, int OLy, int Nr, int nSx, int
   p.gravity = 9.81; p.gravitySign = -1.0; p.rhoNil = 999.8; p.tAlpha = 2.0e-4; p.tempAdvection = 1;
   p.tempForcing = 1; p.tempAdvScheme = 2; p.implicitDiffusion = 0;
   p.saltAdvection = 1; p.saltForcing = 1; p.saltAdvScheme = 2; p.multiDimAdvection = 1; p.momStepping = 1;
-  if (hipStreamCreateWithFlags(&m->stream, hipStreamNonBlocking) != hipSuccess) {
+  if (hipStreamCreateWithFlags(&m->ownStream, hipStreamNonBlocking) != hipSuccess) {
     set_err("mgcm_create: stream");
     delete m;
     return nullptr;
   }
+  m->stream = m->ownStream;
   for (auto &fd : FIELDS) {
     const long n = field_count(m, fd.kind);
     double *ptr = nullptr;
@@ -418,7 +428,7 @@ void mgcm_destroy(mgcm_model *m) {
   if (m->d_blk) hipFree(m->d_blk);
   if (m->d_ctr) hipFree(m->d_ctr);
   if (m->d_rec) hipFree(m->d_rec);
-  if (m->stream) hipStreamDestroy(m->stream);
+  if (m->ownStream) hipStreamDestroy(m->ownStream);
   delete m;
 }
 
@@ -663,6 +673,16 @@ int mgcm_blocking_exchanges(mgcm_model *m) {
   return 0;
 }
 
+// DO_FIELDS_BLOCKING_EXCHANGES field set (do_fields_blocking_exchanges.F:54-97).
+static XFields blocking_fields(const mgcm_model *m) {
+  XFields x{};
+  double *fl[] = {m->f.uVel, m->f.vVel, m->f.wVel, m->f.theta, m->f.salt};
+  const bool use[] = {true, true, true, m->p.tempStepping != 0, m->p.saltStepping != 0};
+  for (int q = 0; q < 5; q++)
+    if (use[q]) { x.p[x.n] = fl[q]; x.nz[x.n] = m->d.Nr; x.n++; }
+  return x;
+}
+
 // One FORWARD_STEP with the fused end-of-step kernels: EXCH(cg2d_x)+etaN,
 // correction+continuity, EXCH(eta)+UPDATE_ETAH, and every blocking exchange plus
 // the counter bump in one launch.  Same arithmetic as the separate C-ABI ops.
@@ -678,12 +698,7 @@ static int one_step(mgcm_model *m) {
   } else {
     if (mgcm_integr_continuity(m)) return -1;
   }
-  XFields x{};
-  double *fl[] = {m->f.uVel, m->f.vVel, m->f.wVel, m->f.theta, m->f.salt};
-  const bool use[] = {true, true, true, m->p.tempStepping != 0, m->p.saltStepping != 0};
-  for (int q = 0; q < 5; q++)
-    if (use[q]) { x.p[x.n] = fl[q]; x.nz[x.n] = m->d.Nr; x.n++; }
-  TIMED(K_EXCH, launch_exchange_multi(m->d, x, m->d_halo, m->nHalo, m->d_ctr, m->stream));
+  TIMED(K_EXCH, launch_exchange_multi(m->d, blocking_fields(m), m->d_halo, m->nHalo, m->d_ctr, m->stream));
   return 0;
 }
 
@@ -743,6 +758,86 @@ int mgcm_forward_step(mgcm_model *m, int nsteps) {
     if (one_step(m)) return -1;
   m->lastBatch = nsteps;
   return 0;
+}
+
+// ---- tile-sharded runs (mitgcm_amd/parallel.py drives the collectives) ----------
+int mgcm_set_tile_range(mgcm_model *m, int t0, int nT) {
+  if (t0 < 0 || nT < 1 || t0 + nT > m->d.nTiles)
+    return set_err("mgcm_set_tile_range: tiles [%d, %d) outside [0, %d)", t0, t0 + nT, m->d.nTiles);
+  m->d.t0 = t0;
+  m->d.nT = nT;
+  drop_graphs(m);
+  if (m->ready) {
+    HIPCHK(hipSetDevice(m->device));
+    HIPCHK(hipStreamSynchronize(m->stream));
+    if (upload_halo(m)) return -1;
+  }
+  return 0;
+}
+
+int mgcm_set_stream(mgcm_model *m, void *stream) {
+  HIPCHK(hipSetDevice(m->device));
+  HIPCHK(hipStreamSynchronize(m->stream));
+  drop_graphs(m);
+  m->stream = stream ? (hipStream_t)stream : m->ownStream;
+  return 0;
+}
+
+int mgcm_exchange_nfields(mgcm_model *m) { return blocking_fields(m).n; }
+
+int mgcm_halo_pack(mgcm_model *m, const long *idx, long n, double *buf, int unpack) {
+  if (check_ready(m)) return -1;
+  HIPCHK(launch_halo_pack(m->d, blocking_fields(m), idx, n, buf, unpack, m->stream));
+  return 0;
+}
+
+int mgcm_tile_copy(mgcm_model *m, const char *name, int t0, int nT, void *buf, int toField) {
+  const FieldDesc *fd = find_field(name);
+  if (!fd || fd->kind == F1D) return set_err("mgcm_tile_copy: no 2-D/3-D field '%s'", name);
+  if (t0 < 0 || nT < 0 || t0 + nT > m->d.nTiles) return set_err("mgcm_tile_copy: bad tile range");
+  const long per = fd->kind == F2D ? m->d.n2 : m->d.n3;
+  double *f = field_ptr(m, fd) + t0 * per;
+  const size_t bytes = (size_t)nT * per * sizeof(double);
+  HIPCHK(hipMemcpyAsync(toField ? f : buf, toField ? buf : f, bytes, hipMemcpyDeviceToDevice, m->stream));
+  return 0;
+}
+
+int mgcm_begin_steps(mgcm_model *m) {
+  if (check_ready(m)) return -1;
+  HIPCHK(hipSetDevice(m->device));
+  HIPCHK(hipMemsetAsync(m->d_ctr + 1, 0, sizeof(int), m->stream));
+  m->lastBatch = 0;
+  return 0;
+}
+
+// FORWARD_STEP split at its exchange points.  1: THERMODYNAMICS + DYNAMICS + the
+// SOLVE_FOR_PRESSURE right-hand side on this process's tiles; [gather cg2d_b/x];
+// 2: CG2D on the whole domain (replicated), EXCH+etaN everywhere, correction +
+// continuity on this process's tiles; [gather the new eta]; 3: EXCH eta +
+// UPDATE_ETAH everywhere; [send/recv 3-D halo sources]; 4: blocking exchanges of
+// this process's tiles, step counters.
+int mgcm_step_phase(mgcm_model *m, int phase) {
+  if (check_ready(m)) return -1;
+  if (!m->p.momStepping) return set_err("mgcm_step_phase: requires momStepping");
+  switch (phase) {
+    case 1:
+      if (mgcm_thermodynamics(m) || mgcm_dynamics(m)) return -1;
+      TIMED(K_RHS, launch_sfp_rhs(m->d, m->p, m->f, m->stream));
+      return 0;
+    case 2:
+      TIMED(K_CG2D, launch_cg2d(m, m->p.cg2dMaxIters, m->p.cg2dUseMinResSol - 1));
+      TIMED(K_ETA, launch_exch_eta(m->d, m->f, m->d_srcOf, false, m->stream));
+      TIMED(K_CONT, launch_corr_cont(m->d, m->p, m->f, m->stream));
+      return 0;
+    case 3:
+      if (m->p.exactConserv) TIMED(K_ETA, launch_exch_eta(m->d, m->f, m->d_srcOf, true, m->stream));
+      return 0;
+    case 4:
+      TIMED(K_EXCH, launch_exchange_multi(m->d, blocking_fields(m), m->d_halo, m->nHalo, m->d_ctr, m->stream));
+      m->lastBatch++;
+      return 0;
+  }
+  return set_err("mgcm_step_phase: no phase %d", phase);
 }
 
 int mgcm_sync(mgcm_model *m) {

@@ -1,0 +1,230 @@
+"""Tile-sharded FORWARD_STEP: one process per GPU over torch.distributed.
+
+The reference runs its tiles over MPI ranks: each rank steps its own tiles
+(myBxLo..myBxHi, eesupp/src/ini_procs.F), EXCH fills halos from neighbouring
+ranks (eesupp/src/exch1_rx.template:170-198 via MPI send/recv) and every CG2D
+iteration does three GLOBAL_SUM_TILE_RL (eesupp/src/global_sum_tile.F:14-237,
+an MPI_Allreduce of per-tile partials summed in tile order).
+
+The MI355X design keeps the 3-D work sharded and the 2-D solve replicated:
+
+* every process holds the WHOLE domain's arrays in HBM (memory is not the
+  constraint: the largest BASELINE grid is 13 x 98^2 x 50 points) and its
+  3-D kernels step only its contiguous tile range [t0, t0+nT)
+  (mgcm_set_tile_range);
+* per step the collectives are: one all-gather of the 2-D CG2D right-hand
+  side (cg2d_b, cg2d_x tile blocks), one all-gather of the new free surface
+  (exactConserv), and one point-to-point exchange of the 3-D halo sources
+  (u, v, w, theta, salt) with each neighbouring process;
+* CG2D itself runs on the gathered global problem on every GPU with the same
+  single-workgroup kernel as the 1-GPU path.  The solve is latency-bound
+  (~4k-6k points, ~35-125 iterations): a distributed CG would need 3 RCCL
+  all-reduces + 2 halo exchanges per iteration (~100 latency-bound
+  collectives per step); the replicated solve needs none, and its sums are
+  exactly the 1-GPU sums, so results are bit-identical at any GPU count
+  (SURVEY.md 8(c) parity item 6).
+
+Transport: backend "nccl" (RCCL over xGMI) moves device tensors directly on
+the model's stream; backend "gloo" stages through host memory (CPU tests,
+and several ranks sharing one GPU on a 1-GPU box).
+"""
+import ctypes
+
+import numpy as np
+
+
+class TilePartition:
+    """Contiguous balanced tile ranges in global tile order (SURVEY.md 8(e):
+    tile index -> device in global-tile order; C5: 13 tiles on 8 GPUs = two
+    tiles on GPUs 0-4)."""
+
+    def __init__(self, nTiles, world):
+        if world > nTiles:
+            raise ValueError("%d tiles cannot be sharded over %d processes" % (nTiles, world))
+        self.nTiles, self.world = nTiles, world
+        base, rem = divmod(nTiles, world)
+        self.counts = [base + (1 if r < rem else 0) for r in range(world)]
+        self.starts = [sum(self.counts[:r]) for r in range(world)]
+        self.maxT = max(self.counts)
+
+    def range(self, rank):
+        return self.starts[rank], self.counts[rank]
+
+    def owner(self, tile):
+        t = np.asarray(tile)
+        return np.searchsorted(np.asarray(self.starts), t, side="right") - 1
+
+
+class HaloPlan:
+    """Which interior points each pair of processes must exchange so that every
+    halo point of a process's tiles can be filled by the local halo map.
+
+    src_of_point: flat (t, j, i) source of every halo-inclusive 2-D point (the
+    topology's EXCH map, topology.py).  Values travel to the SAME global offset
+    on the receiver (every process holds the whole domain), so both sides list
+    source offsets, sorted: send[peer] (in my tiles, needed by peer) equals the
+    peer's recv[me]."""
+
+    def __init__(self, src_of_point, n2, part, rank):
+        src = np.asarray(src_of_point, dtype=np.int64)
+        dst = np.arange(src.size, dtype=np.int64)
+        halo = src != dst
+        dst, src = dst[halo], src[halo]
+        dst_owner = part.owner(dst // n2)
+        src_owner = part.owner(src // n2)
+        self.rank, self.part = rank, part
+        self.send, self.recv = {}, {}
+        for peer in range(part.world):
+            if peer == rank:
+                continue
+            s = np.unique(src[(src_owner == rank) & (dst_owner == peer)])
+            r = np.unique(src[(src_owner == peer) & (dst_owner == rank)])
+            if s.size:
+                self.send[peer] = s
+            if r.size:
+                self.recv[peer] = r
+
+    def peers(self):
+        return sorted(set(self.send) | set(self.recv))
+
+
+def exchange(dist, plan, pack, unpack, make_buf):
+    """Point-to-point exchange of halo sources with every neighbouring process.
+    pack(peer) -> tensor to send; make_buf(peer) -> receive tensor;
+    unpack(peer, tensor).  Grouped isend/irecv (one batch), lower rank posts first."""
+    ops, recvs = [], {}
+    for peer in plan.peers():
+        if peer in plan.send:
+            ops.append(dist.P2POp(dist.isend, pack(peer), peer))
+        if peer in plan.recv:
+            recvs[peer] = make_buf(peer)
+            ops.append(dist.P2POp(dist.irecv, recvs[peer], peer))
+    if ops:
+        for w in dist.batch_isend_irecv(ops):
+            w.wait()
+    for peer, buf in recvs.items():
+        unpack(peer, buf)
+
+
+class ShardedModel:
+    """A Model (model.py) stepped tile-sharded across the processes of the
+    default torch.distributed group.  Every process must construct the same
+    configuration; after init(), step()/forward_step() keep the tiles a
+    process owns bit-identical to a single-process run."""
+
+    def __init__(self, model, dist, device=None):
+        import torch
+        from ._lib import check, lib
+        self.torch, self.dist, self.m = torch, dist, model
+        self.L, self.check = lib(), check
+        g = model.g
+        self.g = g
+        self.rank, self.world = dist.get_rank(), dist.get_world_size()
+        self.part = TilePartition(g.nTiles, self.world)
+        self.t0, self.nT = self.part.range(self.rank)
+        self.backend = dist.get_backend()
+        self.dev = device if device is not None else torch.device("cuda", torch.cuda.current_device())
+        h = model.h
+        check(self.L.mgcm_set_tile_range(h, self.t0, self.nT), "mgcm_set_tile_range")
+        if self.backend == "nccl":
+            # RCCL orders its work after the current stream: run the model on it
+            check(self.L.mgcm_set_stream(h, ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)),
+                  "mgcm_set_stream")
+        n2 = g.nx * g.ny
+        self.n2 = n2
+        self.plan = HaloPlan(g.topo.src_of_point(), n2, self.part, self.rank)
+        self.nf = self.L.mgcm_exchange_nfields(h)
+        dv = self.dev
+        self.idx = {p: torch.as_tensor(v, device=dv) for p, v in
+                    list(self.plan.send.items()) + [(("r", q), w) for q, w in self.plan.recv.items()]}
+        self.sbuf = {p: torch.empty(self.nf * g.Nr * v.size, dtype=torch.float64, device=dv)
+                     for p, v in self.plan.send.items()}
+        self.rbuf = {p: torch.empty(self.nf * g.Nr * v.size, dtype=torch.float64, device=dv)
+                     for p, v in self.plan.recv.items()}
+        mt = self.part.maxT
+        self.g_in = torch.empty(mt * n2, dtype=torch.float64, device=dv)
+        self.g_out = torch.empty(self.world * mt * n2, dtype=torch.float64, device=dv)
+
+    # ---- transport -------------------------------------------------------------
+    def _gather_2d(self, name):
+        """all-gather the tile blocks of a 2-D field from their owners."""
+        L, h, n2 = self.L, self.m.h, self.n2
+        mt = self.part.maxT
+        self.check(L.mgcm_tile_copy(h, name.encode(), self.t0, self.nT, ctypes.c_void_p(self.g_in.data_ptr()), 0),
+                   "mgcm_tile_copy")
+        if self.backend == "gloo":
+            self.torch.cuda.synchronize(self.dev)
+            src = self.g_in.cpu()
+            out = [self.torch.empty_like(src) for _ in range(self.world)]
+            self.dist.all_gather(out, src)
+            self.g_out.copy_(self.torch.cat(out))
+            self.torch.cuda.synchronize(self.dev)
+        else:
+            self.dist.all_gather_into_tensor(self.g_out, self.g_in)
+        for r in range(self.world):
+            if r == self.rank:
+                continue
+            s, c = self.part.range(r)
+            buf = self.g_out[r * mt * n2:]
+            self.check(L.mgcm_tile_copy(h, name.encode(), s, c, ctypes.c_void_p(buf.data_ptr()), 1),
+                       "mgcm_tile_copy")
+
+    def _halo(self):
+        L, h = self.L, self.m.h
+
+        def pack(peer):
+            buf = self.sbuf[peer]
+            self.check(L.mgcm_halo_pack(h, ctypes.c_void_p(self.idx[peer].data_ptr()), self.plan.send[peer].size,
+                                        ctypes.c_void_p(buf.data_ptr()), 0), "mgcm_halo_pack")
+            if self.backend == "gloo":
+                self.torch.cuda.synchronize(self.dev)
+                return buf.cpu()
+            return buf
+
+        def make_buf(peer):
+            return self.rbuf[peer].cpu() if self.backend == "gloo" else self.rbuf[peer]
+
+        def unpack(peer, buf):
+            dev = self.rbuf[peer]
+            if buf is not dev:
+                dev.copy_(buf)
+                self.torch.cuda.synchronize(self.dev)
+            self.check(L.mgcm_halo_pack(h, ctypes.c_void_p(self.idx[("r", peer)].data_ptr()),
+                                        self.plan.recv[peer].size, ctypes.c_void_p(dev.data_ptr()), 1),
+                       "mgcm_halo_pack")
+
+        exchange(self.dist, self.plan, pack, unpack, make_buf)
+
+    # ---- stepping ----------------------------------------------------------------
+    def step(self):
+        L, h, ck = self.L, self.m.h, self.check
+        ck(L.mgcm_step_phase(h, 1), "mgcm_step_phase(1)")
+        self._gather_2d("cg2d_b")
+        self._gather_2d("cg2d_x")
+        ck(L.mgcm_step_phase(h, 2), "mgcm_step_phase(2)")
+        if self.m.params.get("exactConserv", 0):
+            self._gather_2d("cg2d_b")
+        ck(L.mgcm_step_phase(h, 3), "mgcm_step_phase(3)")
+        self._halo()
+        ck(L.mgcm_step_phase(h, 4), "mgcm_step_phase(4)")
+
+    def forward_step(self, nsteps=1):
+        self.check(self.L.mgcm_begin_steps(self.m.h), "mgcm_begin_steps")
+        for _ in range(nsteps):
+            self.step()
+
+    def gather_field(self, name):
+        """The whole-domain field assembled from every owner (host numpy), e.g.
+        for monitors / parity checks; collective."""
+        a = self.m.get(name)
+        t = self.torch.as_tensor(a.reshape(a.shape[0], -1))
+        if self.backend != "gloo":
+            t = t.to(self.dev)
+        out = [self.torch.empty_like(t) for _ in range(self.world)]
+        self.dist.all_gather(out, t)
+        out = [o.cpu() for o in out]
+        res = a.copy()
+        for r in range(self.world):
+            s, c = self.part.range(r)
+            res[s:s + c] = out[r].numpy().reshape(a.shape)[s:s + c]
+        return res

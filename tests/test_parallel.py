@@ -1,0 +1,133 @@
+"""Host logic of the tile-sharded path (mitgcm_amd/parallel.py) on CPU, gloo,
+world sizes 2 and 3: the tile partition, the halo plan and the point-to-point
+exchange reproduce the single-process EXCH (topology.py, restating
+eesupp/src/exch1_rx.template:170-198) on every process's tiles, and the 2-D
+block all-gather rebuilds the whole field.  Fields are numpy stand-ins for the
+device arrays; pack/unpack index exactly as k_halo_pack does
+(buf[(f*Nr + k)*n + h])."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from mitgcm_amd.parallel import HaloPlan, TilePartition, exchange
+from mitgcm_amd.topology import LatLonTopology
+
+LAYOUTS = [  # sNx, sNy, OLx, OLy, nSx, nSy
+    (31, 31, 2, 2, 2, 2),   # tutorial_baroclinic_gyre tiling (BASELINE config 4)
+    (15, 8, 3, 3, 3, 2),    # 6 tiles, wide overlap
+    (45, 40, 2, 2, 2, 1),   # tutorial_global_oce_latlon tiling
+]
+
+
+def test_partition():
+    p = TilePartition(13, 8)   # two tiles on GPUs 0-4
+    assert p.counts == [2, 2, 2, 2, 2, 1, 1, 1]
+    assert p.starts[5] == 10 and p.maxT == 2
+    assert list(p.owner(np.arange(13))) == [0, 0, 1, 1, 2, 2, 3, 3, 4, 4, 5, 6, 7]
+    with pytest.raises(ValueError):
+        TilePartition(4, 8)
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def _worker(rank, world, port, layout, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        sNx, sNy, OLx, OLy, nSx, nSy = layout
+        topo = LatLonTopology(sNx, sNy, OLx, OLy, nSx, nSy)
+        nT, ny, nx, nz, nf = topo.nTiles, topo.ny, topo.nx, 3, 2
+        n2 = nx * ny
+        rng = np.random.default_rng(7)
+        truth = [rng.standard_normal((nT, nz, ny, nx)) for _ in range(nf)]
+        expect = [topo.exchange(a) for a in truth]
+        part = TilePartition(nT, world)
+        t0, c = part.range(rank)
+        # this process: interior of its own tiles valid, everything else NaN
+        mine = []
+        for a in truth:
+            b = np.full_like(a, np.nan)
+            b[t0:t0 + c, :, OLy:OLy + sNy, OLx:OLx + sNx] = a[t0:t0 + c, :, OLy:OLy + sNy, OLx:OLx + sNx]
+            mine.append(b)
+        plan = HaloPlan(topo.src_of_point(), n2, part, rank)
+
+        def flat(f, k):   # level k of field f as a (nT*n2,) view
+            return mine[f][:, k].reshape(nT, n2)
+
+        def pack(peer):
+            idx = plan.send[peer]
+            buf = np.empty(nf * nz * idx.size)
+            for f in range(nf):
+                for k in range(nz):
+                    buf[(f * nz + k) * idx.size:(f * nz + k + 1) * idx.size] = flat(f, k).reshape(-1)[idx]
+            return torch.from_numpy(buf)
+
+        def make_buf(peer):
+            return torch.empty(nf * nz * plan.recv[peer].size, dtype=torch.float64)
+
+        def unpack(peer, buf):
+            idx, b = plan.recv[peer], buf.numpy()
+            for f in range(nf):
+                for k in range(nz):
+                    v = mine[f][:, k].reshape(-1)
+                    v[idx] = b[(f * nz + k) * idx.size:(f * nz + k + 1) * idx.size]
+                    mine[f][:, k] = v.reshape(nT, ny, nx)
+
+        exchange(dist, plan, pack, unpack, make_buf)
+        # local halo map restricted to this process's destination tiles (upload_halo)
+        src = topo.src_of_point()
+        dst = np.arange(src.size)
+        sel = (src != dst) & (dst // n2 >= t0) & (dst // n2 < t0 + c)
+        for f in range(nf):
+            for k in range(nz):
+                v = mine[f][:, k].reshape(-1)
+                v[dst[sel]] = v[src[sel]]
+                mine[f][:, k] = v.reshape(nT, ny, nx)
+        ok = all(np.array_equal(mine[f][t0:t0 + c], expect[f][t0:t0 + c]) for f in range(nf))
+        # 2-D block all-gather (ShardedModel._gather_2d, padded to maxT tiles)
+        e2 = truth[0][:, 0]
+        blk = np.zeros((part.maxT, ny, nx))
+        blk[:c] = e2[t0:t0 + c]
+        out = [torch.empty(part.maxT * n2, dtype=torch.float64) for _ in range(world)]
+        dist.all_gather(out, torch.from_numpy(blk.reshape(-1)))
+        full = np.full_like(e2, np.nan)
+        for r in range(world):
+            s, cc = part.range(r)
+            full[s:s + cc] = out[r].numpy().reshape(part.maxT, ny, nx)[:cc]
+        ok = ok and np.array_equal(full, e2)
+        nsend = sum(v.size for v in plan.send.values())
+        q.put((rank, ok, nsend))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("layout", LAYOUTS)
+@pytest.mark.parametrize("world", [2, 3])
+def test_sharded_exchange_matches_single_process(layout, world):
+    nT = layout[4] * layout[5]
+    if world > nT:
+        pytest.skip("more processes than tiles")
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, layout, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=120) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for rank, ok, nsend in res:
+        assert ok, "rank %d: sharded exchange differs from the single-process EXCH" % rank
+        assert nsend > 0
