@@ -38,6 +38,9 @@ def parse():
     ap.add_argument("--config", default="baroclinic_gyre_dst3",
                     choices=["baroclinic_gyre_dst3", "tutorial_baroclinic_gyre", "tutorial_barotropic_gyre"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--shard", action="store_true",
+                    help="N>1: shard the workload's tiles over the N processes (RCCL, strong scaling, "
+                         "mitgcm_amd/parallel.py) instead of running N replicas")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--pmc-summary", default=os.path.join(ROOT, "profiles", "r01", "pmc_summary.json"),
                     help="tools/pmc_summary.py output of rocprofv3 --pmc passes of this command (roofline.traffic)")
@@ -103,41 +106,62 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
+    shard = a.shard and world > 1
     if world > 1:
         import torch
         import torch.distributed as dist
-        dist.init_process_group("gloo")   # barrier + max-reduce of host timers only
+        if shard:
+            # MGCM_SHARD_BACKEND=gloo: host-staged transport, lets several ranks share
+            # one GPU (rehearsal on a 1-GPU box; RCCL refuses two ranks per device)
+            if os.environ.get("MGCM_SHARD_BACKEND", "nccl") == "gloo":
+                local = local % torch.cuda.device_count()
+                torch.cuda.set_device(local)
+                dist.init_process_group("gloo")
+            else:
+                torch.cuda.set_device(local)
+                dist.init_process_group("nccl", device_id=torch.device("cuda", local))   # RCCL over xGMI
+        else:
+            dist.init_process_group("gloo")   # replicas: barrier + max-reduce of host timers only
     import numpy as np
     from mitgcm_amd import configs
-    from mitgcm_amd.model import dynstat
 
     m = configs.make_model(config_fn(a.config), device=local)
     g = m.g
     dt_clock = m.params["deltaTClock"]
     npts = g.nTiles * g.sNx * g.sNy
+    stepper = m
+    if shard:
+        from mitgcm_amd.parallel import ShardedModel
+        stepper = ShardedModel(m, dist)
+
+    def sync():
+        m.sync()
+        if shard:
+            torch.cuda.synchronize(local)
 
     # warmup (untimed)
     if a.warmup > 0:
-        m.forward_step(a.warmup)
-    m.sync()
+        stepper.forward_step(a.warmup)
+    sync()
 
     def barrier():
         if dist is not None:
             dist.barrier()
 
-    m.prepare()
+    if not shard:
+        m.prepare()
     # timed region: K steps replayed from hipGraphs (kernel timing off)
     barrier()
-    m.sync()
+    sync()
     t0 = time.perf_counter()
-    m.forward_step(a.steps)
-    m.sync()
+    stepper.forward_step(a.steps)
+    sync()
     t1 = time.perf_counter()
     barrier()
     elapsed = t1 - t0
     if dist is not None:
-        import torch
-        t = torch.tensor([elapsed], dtype=torch.float64)
+        t = torch.tensor([elapsed], dtype=torch.float64,
+                         device="cuda" if shard and dist.get_backend() == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     iters = [m.solve_stats(back=b)["cg2d_iters"] for b in range(a.steps)]
@@ -145,8 +169,8 @@ def main():
     # recorded on the model's stream around every kernel (the graph path cannot be
     # bracketed by events); rocprofv3 of this command must agree (profiles/)
     m.kernel_timing(True)
-    m.forward_step(a.steps)
-    m.sync()
+    stepper.forward_step(a.steps)
+    sync()
     iters_t = [m.solve_stats(back=b)["cg2d_iters"] for b in range(a.steps)]
     cg_ms, cg_n = m.kernel_ms("cg2d")
     kern = {k: m.kernel_ms(k) for k in ("oceanic_phys", "temp_step", "mom_step", "sfp_rhs", "cg2d", "exchange",
@@ -158,9 +182,10 @@ def main():
     assert np.isfinite(eta).all() and stats["cg2d_last_res"] < 1e-6, stats
 
     model_days = a.steps * dt_clock / 86400.0
-    value = world * model_days / elapsed
+    copies = 1 if shard else world   # independent model integrations in the job
+    value = copies * model_days / elapsed
     iters_total = sum(iters)
-    cg2d_iters_per_s = world * iters_total / elapsed
+    cg2d_iters_per_s = copies * iters_total / elapsed
     bytes_per_launch = CG2D_BYTES_PER_POINT_ITER * npts * (sum(iters_t) / max(1, len(iters_t)))
     achieved = bytes_per_launch / (cg_ms * 1e-3) / 1e9 if cg_ms > 0 else 0.0
     out = {
@@ -172,15 +197,18 @@ def main():
         "warmup": a.warmup,
         "ms_per_step": 1e3 * elapsed / a.steps,
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": "strong" if shard else "weak",
         "vs_baseline": None,
         "dtype": "f64",
         "data": "reference input fields of verification/%s (bathy, wind%s), cold start"
                 % ("tutorial_barotropic_gyre" if a.config == "tutorial_barotropic_gyre" else "tutorial_baroclinic_gyre",
                    "" if a.config == "tutorial_barotropic_gyre" else ", SST_relax"),
-        "config": {"workload": WORKLOADS[a.config] + "; replicas only",
-                   "tiles_per_gpu": g.nTiles, "points_per_tile": [g.sNx, g.sNy, g.Nr],
-                   "parallelism": "replicas%d" % world},
+        "config": {"workload": WORKLOADS[a.config] + ("; tiles sharded over %d processes (%s)" % (
+                                                           world, "RCCL" if dist.get_backend() == "nccl" else
+                                                           "gloo, host-staged") if shard
+                                                       else "; replicas only"),
+                   "tiles_per_gpu": stepper.nT if shard else g.nTiles, "points_per_tile": [g.sNx, g.sNy, g.Nr],
+                   "parallelism": ("tiles%d" if shard else "replicas%d") % world},
         "cg2d_iters_per_s": cg2d_iters_per_s,
         "cg2d_mean_iters_per_solve": iters_total / max(1, len(iters)),
         "kernel_ms_mean": {k: v[0] for k, v in kern.items()},
