@@ -140,3 +140,86 @@ def make_model(cfg, device=0, **kw):
         m.put(k, v)
     m.init()
     return m
+
+
+LATLON_DELR = [50., 70., 100., 140., 190., 240., 290., 340., 390., 440., 490., 540., 590., 640., 690.]
+# monthly forcing files (12 records each, fp32 big-endian, 90x40) -> FFIELDS.h names
+LATLON_FORCING = {"taux": "trenberth_taux.bin", "tauy": "trenberth_tauy.bin", "Qnet": "ncep_qnet.bin",
+                  "EmPmR": "ncep_emp.bin", "SST": "lev_sst.bin", "SSS": "lev_sss.bin"}
+
+
+def _to_tiles(g, glob):
+    """Global (..., Ny, Nx) field -> tile layout (..., nTiles, ny, nx), halos exchanged."""
+    lead = glob.shape[:-2]
+    out = np.zeros(lead + (g.nTiles, g.ny, g.nx))
+    inner = g.sl(1, g.sNx, 1, g.sNy)
+    for t in range(g.nTiles):
+        bi, bj = t % g.nSx, t // g.nSx
+        out[(Ellipsis, t) + inner] = glob[..., bj * g.sNy:(bj + 1) * g.sNy, bi * g.sNx:(bi + 1) * g.sNx]
+    if out.ndim == 3:
+        return g.exch(out)
+    flat = out.reshape((-1,) + out.shape[-3:])
+    return np.stack([g.exch(f) for f in flat]).reshape(out.shape)
+
+
+def global_oce_latlon(nSx=2, nSy=1, OL=2, data_dir=None):
+    """verification/tutorial_global_oce_latlon: 90x40x15 on a 4-degree spherical-polar
+    grid (ygOrigin=-80), code/SIZE.h sNx=45, sNy=40, OL=2, nSx=2; input/data:
+    viscAh=5e5, viscAr=1e-3, diffKrT=diffKrS=3e-5, JMD95Z, ivdc_kappa=100,
+    implicitDiffusion, allowFreezing, exactConserv, useRealFreshWaterFlux, useCDscheme
+    (tauCD=321428), hFacMin=0.05, hFacMinDr=50, deltaTmom=1800, deltaTtracer=
+    deltaTClock=deltaTfreesurf=86400, abEps=0.1, monthly periodic forcing (period
+    2592000, cycle 31104000), SST/SSS relaxation (5184000 s, 15552000 s), GM-Redi
+    (data.gmredi).  Cold start from record 1 of lev_t/lev_s (INI_THETA / INI_SALT:
+    masked, theta >= -1.9).  Returns (grid, params, state, forcing) with forcing[name]
+    of shape (12, nTiles, ny, nx) (EXTERNAL_FIELDS_LOAD records; EmPmR already in
+    kg/m2/s, x rhoConstFresh)."""
+    d = data_dir or os.path.join(GOLDEN, "tutorial_global_oce_latlon")
+    Nx, Ny, Nr = 90, 40, 15
+    g = Grid(Nx // nSx, Ny // nSy, OL, OL, Nr, nSx, nSy)
+    g.ini_vertical_grid(LATLON_DELR)
+    g.ini_spherical_polar_grid(np.full(Nx, 4.0), np.full(Ny, 4.0), 0.0, -80.0)
+    g.ini_cori(selectCoriMap=2)
+    bathy = read_bin(os.path.join(d, "bathymetry.bin"), (Ny, Nx))
+    g.ini_depths_masks(bathy, hFacMin=0.05, hFacMinDr=50.0, gBaro=9.81)
+    g.ini_cg2d(1800.0, 86400.0, 1e-13)
+    rhoConstFresh = 1000.0
+    forcing = {}
+    for name, fn in LATLON_FORCING.items():
+        rec = read_bin(os.path.join(d, fn), (12, Ny, Nx))
+        if name == "EmPmR":
+            rec = rec * rhoConstFresh
+        forcing[name] = _to_tiles(g, rec)
+    mC = g.f["maskC"]
+    theta = _to_tiles(g, read_bin(os.path.join(d, "lev_t.bin"), (Nr, Ny, Nx)))
+    theta = np.moveaxis(theta, 0, 1).copy()            # (nTiles, Nr, ny, nx)
+    theta[mC == 0.0] = 0.0
+    theta = np.where(theta < -1.9, -1.9, theta)         # ini_theta.F: checkIniTemp .AND. allowFreezing
+    salt = np.moveaxis(_to_tiles(g, read_bin(os.path.join(d, "lev_s.bin"), (Nr, Ny, Nx))), 0, 1).copy()
+    salt[mC == 0.0] = 0.0
+    params = dict(deltaTMom=1800.0, deltaTFreeSurf=86400.0, deltaTClock=86400.0, deltaTtracer=86400.0,
+                  abEps=0.1, rhoConst=1035.0, rhoNil=1035.0, rhoConstFresh=rhoConstFresh, gravity=9.81,
+                  gBaro=9.81, viscAhD=5e5, viscAhZ=5e5, viscA4D=0.0, viscA4Z=0.0, viscAr=1e-3,
+                  sideDragFactor=2.0, selectCoriScheme=0, momForcingOutAB=0, momDissip_In_AB=1,
+                  cg2dMaxIters=500, cg2dUseMinResSol=0, nIter0=0, no_slip_sides=1, no_slip_bottom=1,
+                  exactConserv=1, tempStepping=1, tempAdvection=1, tempForcing=1, tempAdvScheme=2,
+                  tempVertAdvScheme=2, saltStepping=1, saltAdvection=1, saltForcing=1, saltAdvScheme=2,
+                  saltVertAdvScheme=2, diffKhT=0.0, diffKrT=3e-5, diffKhS=0.0, diffKrS=3e-5,
+                  ivdc_kappa=100.0, implicitDiffusion=1, usingSphericalPolarGrid=1, selectMetricTerms=1,
+                  rSphere=g.rSphere, integr_GeoPot=2, eosType=1, allowFreezing=1,
+                  useRealFreshWaterFlux=1, useCDscheme=1, tauCD=321428.0, rCD=1.0 - 1800.0 / 321428.0,
+                  epsAB_CD=0.1, HeatCapacity_Cp=3994.0, convertFW2Salt=-1.0, temp_EvPrRn=123456.7,
+                  salt_EvPrRn=0.0, periodicExternalForcing=1,
+                  externForcingPeriod=2592000.0, externForcingCycle=31104000.0, useGMRedi=1,
+                  GM_background_K=1e3, GM_isopycK=1e3, GM_skewflx=1.0, GM_maxSlope=1e-2, GM_Kmin_horiz=50.0)
+    # set_ref_state.F:92-97: pRef4EOS(k) = top_Pres + rhoConst*(rC(k)-rF(1))*gravity*gravitySign
+    pRef = np.array([0.0 + 1035.0 * (g.f["rC"][k] - g.f["rF"][0]) * 9.81 * -1.0 for k in range(Nr)])
+    lamT = np.full((g.nTiles, g.ny, g.nx), 1.0 / 5184000.0)    # ini_forcing.F
+    lamS = np.full((g.nTiles, g.ny, g.nx), 1.0 / 15552000.0)
+    state = {"theta": theta, "salt": salt, "tRef": np.full(Nr, 20.0), "sRef": np.full(Nr, 35.0),
+             "pRef4EOS": pRef,
+             "lambdaThetaClimRelax": lamT, "lambdaSaltClimRelax": lamS,
+             # INI_FORCING: record 1 of every file (the step-0 monitor shows these)
+             "fu": forcing["taux"][0], "fv": forcing["tauy"][0], "Qnet": forcing["Qnet"][0],
+             "EmPmR": forcing["EmPmR"][0], "SST": forcing["SST"][0], "SSS": forcing["SSS"][0]}
+    return g, params, state, forcing

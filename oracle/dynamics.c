@@ -379,7 +379,7 @@ void oracle_dynamics(OModel *m) {
           for (int i = iMin; i <= iMax; i++) W3(gV, i, j, k) = W3(gV, i, j, k) + m->mtFacMom * L(mT, i, j);
       }
       /* Coriolis (mom_fluxform.F:995-1022; mom_u_coriolis.F, mom_v_coriolis.F) */
-      if (m->useCoriolis) {
+      if (m->useCoriolis && !m->useCDscheme) {   /* CD scheme: Coriolis in timestep.F */
         const int sc = m->selectCoriScheme;
         for (int j = 1 - OLy; j <= sNy + OLy - 1; j++)
           for (int i = 2 - OLx; i <= sNx + OLx; i++) {
@@ -480,6 +480,75 @@ void oracle_dynamics(OModel *m) {
             L(gUtmp, i, j) = L(gUtmp, i, j) + L(guDiss, i, j);
             L(gVtmp, i, j) = L(gVtmp, i, j) + L(gvDiss, i, j);
           }
+      if (m->useCDscheme) {
+        /* CD_CODE_SCHEME (pkg/cd_code/cd_code_scheme.F:85-236), staggerTimeStep = F: phxFac = 0 */
+        const int ci0 = 1 - OLx + 1, ci1 = sNx + OLx - 1, cj0 = 1 - OLy + 1, cj1 = sNy + OLy - 1;
+        double *uVelD = m->uVelD + t * m->n3, *vVelD = m->vVelD + t * m->n3;
+        double *uNM1 = m->uNM1 + t * m->n3, *vNM1 = m->vNM1 + t * m->n3;
+        const double *etaNm1 = m->etaNm1 + t * n2, *etaN = m->etaN + t * n2, *Bo = m->Bo_surf + t * n2;
+        const double *fC = m->fCori + t * n2, *rdxC = m->recip_dxC + t * n2, *rdyC = m->recip_dyC + t * n2;
+        const double ab15 = m->myIter == 0 ? 1.0 : 1.5 + m->epsAB_CD;
+        const double ab05 = m->myIter == 0 ? -0.0 : -0.5 - m->epsAB_CD;
+        const double phxFac = 0.0, phyFac = 0.0;
+        double *pf = fZon, *af = fMer, *vfl = vF;     /* scratch (free at this point) */
+        for (int j = 1 - OLy; j <= sNy + OLy; j++)
+          for (int i = 1 - OLx; i <= sNx + OLx; i++)
+            L(pf, i, j) = L(Bo, i, j) * (ab15 * L(etaN, i, j) + ab05 * L(etaNm1, i, j));
+        for (int j = 1 - OLy + 1; j <= sNy + OLy; j++)
+          for (int i = 1 - OLx; i <= sNx + OLx; i++)
+            L(af, i, j) = (L(gVtmp, i, j) - (L(rdyC, i, j) * (L(pf, i, j) - L(pf, i, j - 1)) +
+                                              phyFac * L(dPhiHydY, i, j))) * W3(maskS, i, j, k);
+        for (int j = cj0; j <= cj1; j++)
+          for (int i = ci0; i <= ci1; i++)
+            L(vfl, i, j) = ((L(af, i, j) + L(af, i - 1, j + 1)) + (L(af, i - 1, j) + L(af, i, j + 1))) * 0.25 *
+                               W3(maskW, i, j, k) -
+                           (L(fC, i, j) + L(fC, i - 1, j)) * 0.5 * (ab15 * W3(uVel, i, j, k) + ab05 * W3(uNM1, i, j, k));
+        for (int j = cj0; j <= cj1; j++)
+          for (int i = ci0; i <= ci1; i++) W3(vVelD, i, j, k) = W3(vVelD, i, j, k) + m->deltaTMom * L(vfl, i, j);
+        for (int j = cj0; j <= cj1; j++)
+          for (int i = ci0; i <= ci1; i++)
+            W3(vVelD, i, j, k) =
+                (m->rCD * W3(vVelD, i, j, k) +
+                 (1.0 - m->rCD) *
+                     (ab15 * ((W3(vVel, i, j, k) + W3(vVel, i - 1, j + 1, k)) + (W3(vVel, i - 1, j, k) + W3(vVel, i, j + 1, k))) * 0.25 +
+                      ab05 * ((W3(vNM1, i, j, k) + W3(vNM1, i - 1, j + 1, k)) + (W3(vNM1, i - 1, j, k) + W3(vNM1, i, j + 1, k))) * 0.25)) *
+                W3(maskW, i, j, k);
+        for (int j = cj0; j <= cj1; j++)
+          for (int i = ci0; i <= ci1; i++)
+            L(uCf, i, j) = (L(fC, i, j) + L(fC, i - 1, j)) * 0.5 * W3(vVelD, i, j, k) * m->cfFacMom;   /* guCor */
+        for (int j = 1 - OLy; j <= sNy + OLy; j++)
+          for (int i = 1 - OLx + 1; i <= sNx + OLx; i++)
+            L(af, i, j) = (L(gUtmp, i, j) - (L(rdxC, i, j) * (L(pf, i, j) - L(pf, i - 1, j)) +
+                                              phxFac * L(dPhiHydX, i, j))) * W3(maskW, i, j, k);
+        for (int j = cj0; j <= cj1; j++)
+          for (int i = ci0; i <= ci1; i++)
+            L(vfl, i, j) = ((L(af, i, j) + L(af, i + 1, j - 1)) + (L(af, i + 1, j) + L(af, i, j - 1))) * 0.25 *
+                               W3(maskS, i, j, k) +
+                           (L(fC, i, j) + L(fC, i, j - 1)) * 0.5 * (ab15 * W3(vVel, i, j, k) + ab05 * W3(vNM1, i, j, k));
+        for (int j = cj0; j <= cj1; j++)
+          for (int i = ci0; i <= ci1; i++) W3(uVelD, i, j, k) = W3(uVelD, i, j, k) + m->deltaTMom * L(vfl, i, j);
+        for (int j = cj0; j <= cj1; j++)
+          for (int i = ci0; i <= ci1; i++)
+            W3(uVelD, i, j, k) =
+                (m->rCD * W3(uVelD, i, j, k) +
+                 (1.0 - m->rCD) *
+                     (ab15 * ((W3(uVel, i, j, k) + W3(uVel, i + 1, j - 1, k)) + (W3(uVel, i, j - 1, k) + W3(uVel, i + 1, j, k))) * 0.25 +
+                      ab05 * ((W3(uNM1, i, j, k) + W3(uNM1, i + 1, j - 1, k)) + (W3(uNM1, i, j - 1, k) + W3(uNM1, i + 1, j, k))) * 0.25)) *
+                W3(maskS, i, j, k);
+        for (int j = cj0; j <= cj1; j++)
+          for (int i = ci0; i <= ci1; i++)
+            L(vCf, i, j) = -(L(fC, i, j) + L(fC, i, j - 1)) * 0.5 * W3(uVelD, i, j, k) * m->cfFacMom;  /* gvCor */
+        for (int j = 1 - OLy; j <= sNy + OLy; j++)
+          for (int i = 1 - OLx; i <= sNx + OLx; i++) {
+            W3(uNM1, i, j, k) = W3(uVel, i, j, k);
+            W3(vNM1, i, j, k) = W3(vVel, i, j, k);
+          }
+        for (int j = jMin; j <= jMax; j++)
+          for (int i = iMin; i <= iMax; i++) {
+            L(gUtmp, i, j) = L(gUtmp, i, j) + L(uCf, i, j);
+            L(gVtmp, i, j) = L(gVtmp, i, j) + L(vCf, i, j);
+          }
+      }
       /* u* = u + dt*(gUtmp + gUdPx)*maskW, gUdPx = 0 for implicSurfPress = 1 (timestep.F:373-388) */
       for (int j = jMin; j <= jMax; j++)
         for (int i = iMin; i <= iMax; i++) {

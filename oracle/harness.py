@@ -146,7 +146,8 @@ class Oracle:
                 ("uvel", self.arr("uVel"), self.arr("hFacW"), 1, mW, self.arr("rAw"), drF, Nr),
                 ("vvel", self.arr("vVel"), self.arr("hFacS"), 1, mS, self.arr("rAs"), drF, Nr),
                 ("wvel", self.arr("wVel"), self.arr("maskC"), 1, mC, self.arr("rA"), drC, Nr),
-                ("theta", self.arr("theta"), self.arr("hFacC"), 1, mC, self.arr("rA"), drF, Nr)):
+                ("theta", self.arr("theta"), self.arr("hFacC"), 1, mC, self.arr("rA"), drF, Nr),
+                ("salt", self.arr("salt"), self.arr("hFacC"), 1, mC, self.arr("rA"), drF, Nr)):
             st = self.stats(fld, nr, hf, h3, mask, area, dr)
             for key, v in zip(("min", "max", "mean", "sd", "del2"), st[:5]):
                 res["dynstat_%s_%s" % (name, key)] = float(v)
@@ -189,6 +190,20 @@ def oracle_from_config(cfg, **kw):
           globalArea=g.globalArea)
     for k, v in state.items():
         o.arr(k).reshape(-1)[:len(np.ravel(v))] = np.ravel(v)
+    return o, g
+
+
+def latlon_oracle(**kw):
+    """verification/tutorial_global_oce_latlon as the oracle (mitgcm_amd.configs.global_oce_latlon):
+    parameters, grid, initial state, and the 12 monthly forcing records EXTERNAL_FIELDS_LOAD
+    interpolates."""
+    from mitgcm_amd import configs
+    g, params, state, forcing = configs.global_oce_latlon(**kw)
+    o, _ = oracle_from_config(lambda: (g, params, state))
+    names = {"taux": "forcTaux", "tauy": "forcTauy", "Qnet": "forcQnet", "EmPmR": "forcEmPmR", "SST": "forcSST",
+             "SSS": "forcSSS"}
+    for k, v in forcing.items():
+        o.arr(names[k])[:] = np.ravel(v)
     return o, g
 
 

@@ -33,6 +33,10 @@ OModel *oracle_new(int sNx, int sNy, int OLx, int OLy, int Nr, int nSx, int nSy)
   m->tempAdvScheme = 2; m->tempVertAdvScheme = 2; m->saltAdvScheme = 2; m->saltVertAdvScheme = 2;
   m->tempAdvection = 1; m->saltAdvection = 1; m->tempForcing = 1; m->saltForcing = 1; m->momStepping = 1;
   m->multiDimAdvection = 1;
+  m->rhoConstFresh = 999.8; m->HeatCapacity_Cp = 3994.0; m->convertFW2Salt = 35.0;
+  m->temp_EvPrRn = 123456.7; m->salt_EvPrRn = 0.0;          /* UNSET_RL = 1.234567D5 */
+  m->epsAB_CD = 0.0; m->nForcRec = 12;
+  m->GM_Small_Number = 1.0e-20; m->GM_slopeSqCutoff = 1.0e48; m->GM_skewflx = 1.0;
 
   m->drF = zalloc(Nr + 1); m->drC = zalloc(Nr + 1); m->rF = zalloc(Nr + 1); m->rC = zalloc(Nr + 1);
   m->recip_drF = zalloc(Nr + 1); m->recip_drC = zalloc(Nr + 1);
@@ -49,13 +53,20 @@ OModel *oracle_new(int sNx, int sNy, int OLx, int OLy, int Nr, int nSx, int nSy)
   A2(etaN); A2(fu); A2(fv); A2(surfaceForcingU); A2(surfaceForcingV);
   A2(fCoriCos); A2(tanPhiAtU); A2(tanPhiAtV); A2(surfaceForcingT); A2(SST); A2(lambdaThetaClimRelax);
   A2(etaH); A2(dEtaHdt); A2(surfaceForcingS);
+  A2(Qnet); A2(EmPmR); A2(SSS); A2(lambdaSaltClimRelax); A2(saltFlux); A2(etaNm1);
 #undef A2
+  m->pRef4EOS = zalloc(Nr);
+#define AF(f) m->f = zalloc(N2 * m->nForcRec)
+  AF(forcTaux); AF(forcTauy); AF(forcQnet); AF(forcEmPmR); AF(forcSST); AF(forcSSS);
+#undef AF
   m->kSurfC = izalloc(N2); m->kSurfW = izalloc(N2); m->kSurfS = izalloc(N2); m->kLowC = izalloc(N2);
 #define A3(f) m->f = zalloc(N3)
   A3(hFacC); A3(hFacW); A3(hFacS); A3(recip_hFacC); A3(recip_hFacW); A3(recip_hFacS);
   A3(maskC); A3(maskW); A3(maskS);
   A3(uVel); A3(vVel); A3(wVel); A3(theta); A3(salt); A3(gU); A3(gV); A3(guNm1); A3(gvNm1);
   A3(gtNm1); A3(gsNm1); A3(rhoInSitu); A3(IVDConvCount);
+  A3(Kwx); A3(Kwy); A3(Kwz); A3(Kux); A3(Kvy); A3(uVelD); A3(vVelD); A3(uNM1); A3(vNM1);
+  A3(sigmaX); A3(sigmaY); A3(sigmaR);
 #undef A3
   return m;
 }
@@ -75,7 +86,11 @@ void oracle_free(OModel *m) {
                    &m->vVel, &m->wVel, &m->theta, &m->salt, &m->gU, &m->gV, &m->guNm1, &m->gvNm1,
                    &m->tRef, &m->sRef, &m->fCoriCos, &m->tanPhiAtU, &m->tanPhiAtV, &m->surfaceForcingT,
                    &m->SST, &m->lambdaThetaClimRelax, &m->etaH, &m->dEtaHdt, &m->gtNm1, &m->rhoInSitu,
-                   &m->IVDConvCount, &m->gsNm1, &m->surfaceForcingS};
+                   &m->IVDConvCount, &m->gsNm1, &m->surfaceForcingS, &m->pRef4EOS, &m->Qnet, &m->EmPmR,
+                   &m->SSS, &m->lambdaSaltClimRelax, &m->saltFlux, &m->etaNm1, &m->Kwx, &m->Kwy, &m->Kwz,
+                   &m->Kux, &m->Kvy, &m->uVelD, &m->vVelD, &m->uNM1, &m->vNM1, &m->sigmaX, &m->sigmaY,
+                   &m->sigmaR, &m->forcTaux, &m->forcTauy, &m->forcQnet, &m->forcEmPmR, &m->forcSST,
+                   &m->forcSSS};
   for (size_t i = 0; i < sizeof(dp) / sizeof(dp[0]); i++) free(*dp[i]);
   free(m->kSurfC); free(m->kSurfW); free(m->kSurfS); free(m->kLowC);
   free(m);
@@ -103,6 +118,11 @@ static const PDesc PTAB[] = {
   PI_(saltStepping), PI_(saltAdvection), PI_(saltForcing), PI_(saltAdvScheme), PI_(saltVertAdvScheme),
   PI_(multiDimAdvection), PI_(momStepping), PD(diffKhS), PD(diffKrS),
   PD(rSphere), PD(deltaTtracer), PD(diffKhT), PD(diffKrT), PD(ivdc_kappa), PD(tAlpha), PD(sBeta), PD(gravitySign),
+  PI_(eosType), PI_(allowFreezing), PI_(useRealFreshWaterFlux), PI_(useCDscheme), PI_(useGMRedi),
+  PI_(periodicExternalForcing), PD(rhoConstFresh), PD(HeatCapacity_Cp), PD(convertFW2Salt), PD(temp_EvPrRn),
+  PD(salt_EvPrRn), PD(tauCD), PD(rCD), PD(epsAB_CD), PD(externForcingPeriod), PD(externForcingCycle),
+  PD(GM_background_K), PD(GM_isopycK), PD(GM_skewflx), PD(GM_maxSlope), PD(GM_Kmin_horiz),
+  PD(GM_Small_Number), PD(GM_slopeSqCutoff),
 };
 #undef PD
 #undef PI_
@@ -163,6 +183,15 @@ double *oracle_array(OModel *m, const char *name, long *count) {
     {"uVel", m->uVel, N3}, {"vVel", m->vVel, N3}, {"wVel", m->wVel, N3},
     {"theta", m->theta, N3}, {"salt", m->salt, N3}, {"gU", m->gU, N3}, {"gV", m->gV, N3},
     {"guNm1", m->guNm1, N3}, {"gvNm1", m->gvNm1, N3},
+    {"pRef4EOS", m->pRef4EOS, m->Nr}, {"Qnet", m->Qnet, N2}, {"EmPmR", m->EmPmR, N2}, {"SSS", m->SSS, N2},
+    {"lambdaSaltClimRelax", m->lambdaSaltClimRelax, N2}, {"saltFlux", m->saltFlux, N2},
+    {"etaNm1", m->etaNm1, N2}, {"Kwx", m->Kwx, N3}, {"Kwy", m->Kwy, N3}, {"Kwz", m->Kwz, N3},
+    {"Kux", m->Kux, N3}, {"Kvy", m->Kvy, N3}, {"uVelD", m->uVelD, N3}, {"vVelD", m->vVelD, N3},
+    {"uNM1", m->uNM1, N3}, {"vNM1", m->vNM1, N3}, {"sigmaX", m->sigmaX, N3}, {"sigmaY", m->sigmaY, N3},
+    {"sigmaR", m->sigmaR, N3},
+    {"forcTaux", m->forcTaux, N2 * m->nForcRec}, {"forcTauy", m->forcTauy, N2 * m->nForcRec},
+    {"forcQnet", m->forcQnet, N2 * m->nForcRec}, {"forcEmPmR", m->forcEmPmR, N2 * m->nForcRec},
+    {"forcSST", m->forcSST, N2 * m->nForcRec}, {"forcSSS", m->forcSSS, N2 * m->nForcRec},
   };
   for (size_t i = 0; i < sizeof(t) / sizeof(t[0]); i++)
     if (!strcmp(t[i].n, name)) { if (count) *count = t[i].c; return t[i].p; }

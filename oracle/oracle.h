@@ -81,6 +81,21 @@ typedef struct OModel {
   int myIter;
   double myTime;
 
+  /* --- ocean physics of the lat-lon / 90x40x15 set-ups (ocean.c) --- */
+  int eosType;            /* 0 LINEAR, 1 JMD95Z (ini_eos.F) */
+  int allowFreezing, useRealFreshWaterFlux, useCDscheme, useGMRedi, periodicExternalForcing, nForcRec;
+  double rhoConstFresh, HeatCapacity_Cp, convertFW2Salt, temp_EvPrRn, salt_EvPrRn;
+  double tauCD, rCD, epsAB_CD;
+  double externForcingPeriod, externForcingCycle;
+  double GM_background_K, GM_isopycK, GM_skewflx, GM_maxSlope, GM_Kmin_horiz, GM_Small_Number,
+         GM_slopeSqCutoff;
+  double *pRef4EOS;                                                       /* [Nr] */
+  double *Qnet, *EmPmR, *SSS, *lambdaSaltClimRelax, *saltFlux, *etaNm1;   /* 2-D */
+  double *Kwx, *Kwy, *Kwz, *Kux, *Kvy, *uVelD, *vVelD, *uNM1, *vNM1;      /* 3-D */
+  double *sigmaX, *sigmaY, *sigmaR;                                       /* 3-D */
+  /* EXTERNAL_FIELDS_LOAD records, nForcRec x (2-D field), halos exchanged */
+  double *forcTaux, *forcTauy, *forcQnet, *forcEmPmR, *forcSST, *forcSSS;
+
   /* --- outputs of the last SOLVE_FOR_PRESSURE --- */
   double firstResidual, minResidualSq, lastResidual, sumRHS, rhsMax;
   int numIters, nIterMin;
@@ -125,6 +140,13 @@ void oracle_integr_continuity(OModel *m);            /* integr_continuity.F:13 *
 void oracle_forward_step(OModel *m);
 void oracle_oceanic_phys(OModel *m);                 /* DO_OCEANIC_PHYS subset (do_oceanic_phys.F:555-882) */
 void oracle_thermodynamics(OModel *m);               /* THERMODYNAMICS -> TEMP_INTEGRATE (temp_integrate.F) */                 /* forward_step.F:64 (supported subset) */
+
+/* ocean physics (ocean.c) */
+void oracle_fields_load(OModel *m);                  /* EXTERNAL_FIELDS_LOAD (external_fields_load.F) */
+double oracle_find_rho(const OModel *m, int kRef, double t, double s);  /* FIND_RHO_2D, one point */
+void oracle_freeze_surface(OModel *m);               /* FREEZE_SURFACE (freeze_surface.F) */
+void oracle_external_forcing_surf(OModel *m);        /* EXTERNAL_FORCING_SURF (external_forcing_surf.F) */
+void oracle_gmredi_calc_tensor(OModel *m, int t);    /* GMREDI_CALC_TENSOR (gmredi_calc_tensor.F), gkw91 */
 
 /* monitor (pkg/monitor/mon_calc_stats_rl.F): out[6] = min,max,mean,sd,del2,vol */
 void oracle_mon_stats(OModel *m, const double *arr, int myNr, const double *arrhFac,

@@ -215,7 +215,21 @@ void oracle_solve_for_pressure(OModel *m) {
   const int sNx = m->sNx, sNy = m->sNy, OLx = m->OLx, OLy = m->OLy, Nr = m->Nr, nx = m->nx;
   const long N2 = m->n2 * m->nTiles, n2 = m->n2;
   double *cg2d_x = calloc(N2, 8), *cg2d_b = calloc(N2, 8), *pf = calloc(n2, 8);
-  for (long p = 0; p < N2; p++) { cg2d_x[p] = m->Bo_surf[p] * m->etaN[p]; cg2d_b[p] = 0.0; }
+  for (long p = 0; p < N2; p++) {
+    m->etaNm1[p] = m->etaN[p];   /* ALLOW_CD_CODE (solve_for_pressure.F:126-128) */
+    cg2d_x[p] = m->Bo_surf[p] * m->etaN[p];
+    cg2d_b[p] = 0.0;
+  }
+  /* solve_for_pressure.F:142-151: fresh-water volume flux */
+  if (m->useRealFreshWaterFlux) {
+    const double tmpFac = m->freeSurfFac * (1.0 / m->rhoConst) * m->implicDiv2DFlow;
+    for (int t = 0; t < m->nTiles; t++)
+      for (int j = 1; j <= m->sNy; j++)
+        for (int i = 1; i <= m->sNx; i++) {
+          const long p = O2(m, i, j, t);
+          cg2d_b[p] = tmpFac * m->rA[p] * m->EmPmR[p] / m->deltaTMom * m->maskInC[p];
+        }
+  }
 #define PF(i, j) pf[(long)((i) + OLx - 1) + (long)((j) + OLy - 1) * nx]
   for (int t = 0; t < m->nTiles; t++) {
     for (int k = Nr; k >= 1; k--) {
@@ -302,7 +316,8 @@ void oracle_integr_continuity(OModel *m) {
       for (int j = 1; j <= sNy; j++)
         for (int i = 1; i <= sNx; i++) {
           long p = O2(m, i, j, t);
-          m->dEtaHdt[p] = -(HD(i, j) * m->recip_rA[p]) - 0.0 * 0.0;  /* - facEmP*EmPmR, both 0 */
+          const double facEmP = m->useRealFreshWaterFlux ? 1.0 / m->rhoConst : 0.0;   /* mass2rUnit */
+          m->dEtaHdt[p] = -(HD(i, j) * m->recip_rA[p]) - facEmP * m->EmPmR[p];
           m->etaN[p] = m->etaH[p] + m->implicDiv2DFlow * m->dEtaHdt[p] * m->deltaTFreeSurf;
         }
 #undef HD
@@ -335,16 +350,12 @@ void oracle_integr_continuity(OModel *m) {
  * EXTERNAL_FORCING_SURF (momentum part) -> DYNAMICS -> SOLVE_FOR_PRESSURE ->
  * MOMENTUM_CORRECTION_STEP -> INTEGR_CONTINUITY -> DO_FIELDS_BLOCKING_EXCHANGES */
 void oracle_forward_step(OModel *m) {
-  const long N2 = m->n2 * m->nTiles;
-  /* external_forcing_surf.F:214-216: surfaceForcingU = fu*mass2rUnit */
-  const double mass2rUnit = 1.0 / m->rhoConst;
-  for (long p = 0; p < N2; p++) {
-    m->surfaceForcingU[p] = m->fu[p] * mass2rUnit;
-    m->surfaceForcingV[p] = m->fv[p] * mass2rUnit;
-  }
+  /* forward_step.F:542 LOAD_FIELDS_DRIVER -> EXTERNAL_FIELDS_LOAD (periodic forcing) */
+  oracle_fields_load(m);
+  /* forward_step.F:656 DO_OCEANIC_PHYS (always called: surface forcing, rhoInSitu, ...) */
+  oracle_oceanic_phys(m);
   if (m->tempStepping || m->saltStepping) {
-    /* forward_step.F:656 DO_OCEANIC_PHYS, :732 THERMODYNAMICS (staggerTimeStep = F) */
-    oracle_oceanic_phys(m);
+    /* forward_step.F:732 THERMODYNAMICS (staggerTimeStep = F) */
     oracle_thermodynamics(m);
   }
   if (m->momStepping) {

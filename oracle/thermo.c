@@ -28,44 +28,50 @@
 #define W3(a, i, j, k) (a)[(long)((i) + OLx - 1) + (long)((j) + OLy - 1) * nx + (long)((k) - 1) * n2]
 
 /* FIND_RHO_2D, equationOfState = 'LINEAR' (find_rho.F:125-136) */
-static double rho_linear(const OModel *m, int kRef, double t, double s) {
-  const double refTemp = m->tRef[kRef - 1], refSalt = m->sRef[kRef - 1];
-  const double dRho = m->rhoNil - m->rhoConst;
-  return m->rhoNil * (m->sBeta * (s - refSalt) - m->tAlpha * (t - refTemp)) + dRho;
-}
 
 void oracle_oceanic_phys(OModel *m) {
   const int sNx = m->sNx, sNy = m->sNy, OLx = m->OLx, OLy = m->OLy, Nr = m->Nr, nx = m->nx;
   const long n2 = m->n2;
+  /* do_oceanic_phys.F:548-553 FREEZE_SURFACE, :574 EXTERNAL_FORCING_SURF (full halo range) */
+  if (m->allowFreezing) oracle_freeze_surface(m);
+  oracle_external_forcing_surf(m);
+  const int calcConvect = m->ivdc_kappa != 0.0;
   for (int t = 0; t < m->nTiles; t++) {
     const double *theta = m->theta + t * m->n3, *salt = m->salt + t * m->n3;
-    const double *hFacC = m->hFacC + t * m->n3, *maskC = m->maskC + t * m->n3;
+    const double *maskC = m->maskC + t * m->n3, *maskW = m->maskW + t * m->n3, *maskS = m->maskS + t * m->n3;
+    const double *recip_dxC = m->recip_dxC + t * n2, *recip_dyC = m->recip_dyC + t * n2;
     double *rhoInSitu = m->rhoInSitu + t * m->n3, *conv = m->IVDConvCount + t * m->n3;
-    double *sfT = m->surfaceForcingT + t * n2;
-    const double *lam = m->lambdaThetaClimRelax + t * n2, *SST = m->SST + t * n2;
-    /* EXTERNAL_FORCING_SURF: surfaceForcingT = 0, then FORCING_SURF_RELAX (ks = 1),
-     * full range iMin..iMax = 1-OLx..sNx+OLx (do_oceanic_phys.F:555-558); Qnet = 0 */
-    for (int j = 1 - OLy; j <= sNy + OLy; j++)
-      for (int i = 1 - OLx; i <= sNx + OLx; i++)
-        L(sfT, i, j) = -(L(lam, i, j) * (W3(theta, i, j, 1) - L(SST, i, j)) * m->drF[0] * W3(hFacC, i, j, 1));
+    double *sigmaX = m->sigmaX + t * m->n3, *sigmaY = m->sigmaY + t * m->n3, *sigmaR = m->sigmaR + t * m->n3;
+    for (long p = 0; p < m->n3; p++) { sigmaX[p] = 0.0; sigmaY[p] = 0.0; sigmaR[p] = 0.0; conv[p] = 0.0; }
     /* FIND_RHO_2D for every level, kRef = k (do_oceanic_phys.F:753-761) */
     for (int k = 1; k <= Nr; k++)
       for (int j = 1 - OLy; j <= sNy + OLy; j++)
         for (int i = 1 - OLx; i <= sNx + OLx; i++)
-          W3(rhoInSitu, i, j, k) = rho_linear(m, k, W3(theta, i, j, k), W3(salt, i, j, k));
-    /* IVDConvCount = 0, then k = Nr..2: sigmaR from rho(k) and rho(theta(k-1), kRef = k) */
-    for (long p = 0; p < m->n3; p++) conv[p] = 0.0;
-    if (m->ivdc_kappa != 0.0) {
-      for (int k = Nr; k >= 2; k--)
+          W3(rhoInSitu, i, j, k) = oracle_find_rho(m, k, W3(theta, i, j, k), W3(salt, i, j, k));
+    /* k = Nr..1 (do_oceanic_phys.F:799-882): GRAD_SIGMA with rho(theta(k-1), kRef = k),
+     * CALC_IVDC */
+    if (m->useGMRedi || calcConvect) {
+      for (int k = Nr; k >= 1; k--) {
         for (int j = 1 - OLy; j <= sNy + OLy; j++)
-          for (int i = 1 - OLx; i <= sNx + OLx; i++) {
-            double rhoKp1 = W3(rhoInSitu, i, j, k);
-            double rhoKm1 = rho_linear(m, k, W3(theta, i, j, k - 1), W3(salt, i, j, k - 1));
-            double sigmaR = W3(maskC, i, j, k) * W3(maskC, i, j, k - 1) * m->recip_drC[k - 1] * m->rkSign *
-                            (rhoKp1 - rhoKm1);
-            W3(conv, i, j, k) = (-sigmaR * m->gravitySign > 0.0) ? 1.0 : 0.0;
-          }
+          for (int i = 1 - OLx + 1; i <= sNx + OLx; i++)
+            W3(sigmaX, i, j, k) = W3(maskW, i, j, k) * L(recip_dxC, i, j) *
+                                  (W3(rhoInSitu, i, j, k) - W3(rhoInSitu, i - 1, j, k));
+        for (int j = 1 - OLy + 1; j <= sNy + OLy; j++)
+          for (int i = 1 - OLx; i <= sNx + OLx; i++)
+            W3(sigmaY, i, j, k) = W3(maskS, i, j, k) * L(recip_dyC, i, j) *
+                                  (W3(rhoInSitu, i, j, k) - W3(rhoInSitu, i, j - 1, k));
+        if (k > 1)
+          for (int j = 1 - OLy; j <= sNy + OLy; j++)
+            for (int i = 1 - OLx; i <= sNx + OLx; i++) {
+              const double rhoKp1 = W3(rhoInSitu, i, j, k);
+              const double rhoKm1 = oracle_find_rho(m, k, W3(theta, i, j, k - 1), W3(salt, i, j, k - 1));
+              W3(sigmaR, i, j, k) = W3(maskC, i, j, k) * W3(maskC, i, j, k - 1) * m->recip_drC[k - 1] * m->rkSign *
+                                    (rhoKp1 - rhoKm1);
+              if (calcConvect) W3(conv, i, j, k) = (-W3(sigmaR, i, j, k) * m->gravitySign > 0.0) ? 1.0 : 0.0;
+            }
+      }
     }
+    if (m->useGMRedi) oracle_gmredi_calc_tensor(m, t);
   }
 }
 
@@ -225,12 +231,21 @@ static void tracer_integrate(OModel *m, const TracerSpec *c) {
     const double *recip_rA = m->recip_rA + t * n2, *recip_dxC = m->recip_dxC + t * n2;
     const double *recip_dyC = m->recip_dyC + t * n2, *maskInC = m->maskInC + t * n2;
     const double *sfT = c->sfc ? c->sfc + t * n2 : NULL;
+    const double *Kwx = m->Kwx + t * n3, *Kwy = m->Kwy + t * n3, *Kwz = m->Kwz + t * n3;
+    const double *Kux = m->Kux + t * n3, *Kvy = m->Kvy + t * n3, *maskW = m->maskW + t * n3;
+    const double *maskS = m->maskS + t * n3;
 
     /* CALC_3D_DIFFUSIVITY: KappaR = IVDConvCount*ivdc_kappa + KbryanLewis79(=0) + diffKrNr(k) */
     for (int k = 1; k <= Nr; k++)
       for (int j = 1 - OLy; j <= sNy + OLy; j++)
         for (int i = 1 - OLx; i <= sNx + OLx; i++)
           W3(kappaRT, i, j, k) = (W3(conv, i, j, k) * m->ivdc_kappa + 0.0) + c->diffKr;
+    /* GMREDI_CALC_DIFF (gmredi_calc_diff.F:57-70) over iMin..iMax = 0..sNx+1 */
+    if (m->useGMRedi)
+      for (int k = 1; k <= Nr; k++)
+        for (int j = 0; j <= sNy + 1; j++)
+          for (int i = 0; i <= sNx + 1; i++)
+            W3(kappaRT, i, j, k) = W3(kappaRT, i, j, k) + W3(Kwz, i, j, k) * L(maskInC, i, j);
     for (long p = 0; p < n3; p++) gT[p] = 0.0;
     if (multiDim) gad_advection_dst3fl(m, t, theta, uVel, vVel, wVel, gT, m->deltaTtracer);
     for (long p = 0; p < n2; p++) { fVer[0][p] = fVer[1][p] = 0.0; rTrans[p] = 0.0; }
@@ -278,6 +293,11 @@ static void tracer_integrate(OModel *m, const TracerSpec *c) {
       } else {
         for (long p = 0; p < n2; p++) df[p] = 0.0;
       }
+      if (m->useGMRedi) /* GMREDI_XTRANSPORT (gmredi_xtransport.F:94-101), i = iMin..iMax+1 */
+        for (int j = 0; j <= sNy + 1; j++)
+          for (int i = 0; i <= sNx + 2; i++)
+            L(df, i, j) = L(df, i, j) - L(xA, i, j) * W3(Kux, i, j, k) * L(recip_dxC, i, j) *
+                                            (W3(theta, i, j, k) - W3(theta, i - 1, j, k));
       for (long p = 0; p < n2; p++) fZon[p] = fZon[p] + df[p];
       if (calcAdvection) { /* GAD_C2_ADV_Y */
         for (int i = 1 - OLx; i <= sNx + OLx; i++) L(af, i, 1 - OLy) = 0.0;
@@ -294,6 +314,11 @@ static void tracer_integrate(OModel *m, const TracerSpec *c) {
       } else {
         for (long p = 0; p < n2; p++) df[p] = 0.0;
       }
+      if (m->useGMRedi) /* GMREDI_YTRANSPORT, j = jMin..jMax+1 */
+        for (int j = 0; j <= sNy + 2; j++)
+          for (int i = 0; i <= sNx + 1; i++)
+            L(df, i, j) = L(df, i, j) - L(yA, i, j) * W3(Kvy, i, j, k) * L(recip_dyC, i, j) *
+                                            (W3(theta, i, j, k) - W3(theta, i, j - 1, k));
       for (long p = 0; p < n2; p++) fMer[p] = fMer[p] + df[p];
       if (calcAdvection && k >= 2) { /* GAD_C2_ADV_R */
         for (int j = 1 - OLy; j <= sNy + OLy; j++)
@@ -309,8 +334,31 @@ static void tracer_integrate(OModel *m, const TracerSpec *c) {
           if (!m->implicitDiffusion && k >= 2)
             dfr = -W3(kappaRT, i, j, k) * L(maskUp, i, j) * L(rA, i, j) * m->recip_drC[k - 1] *
                   (W3(theta, i, j, k) - W3(theta, i, j, kM1)) * m->rkSign;
-          L(fVerUp, i, j) = L(fVerUp, i, j) + dfr;
+          L(df, i, j) = dfr;
         }
+      if (m->useGMRedi && k > 1) /* GMREDI_RTRANSPORT (gmredi_rtransport.F:75-130), iMin..iMax */
+        for (int j = 0; j <= sNy + 1; j++)
+          for (int i = 0; i <= sNx + 1; i++) {
+            const double dTdx = 0.5 * (0.5 * (W3(maskW, i + 1, j, k) * L(recip_dxC, i + 1, j) *
+                                                  (W3(theta, i + 1, j, k) - W3(theta, i, j, k)) +
+                                              W3(maskW, i, j, k) * L(recip_dxC, i, j) *
+                                                  (W3(theta, i, j, k) - W3(theta, i - 1, j, k))) +
+                                       0.5 * (W3(maskW, i + 1, j, k - 1) * L(recip_dxC, i + 1, j) *
+                                                  (W3(theta, i + 1, j, k - 1) - W3(theta, i, j, k - 1)) +
+                                              W3(maskW, i, j, k - 1) * L(recip_dxC, i, j) *
+                                                  (W3(theta, i, j, k - 1) - W3(theta, i - 1, j, k - 1))));
+            const double dTdy = 0.5 * (0.5 * (W3(maskS, i, j + 1, k) * L(recip_dyC, i, j + 1) *
+                                                  (W3(theta, i, j + 1, k) - W3(theta, i, j, k)) +
+                                              W3(maskS, i, j, k) * L(recip_dyC, i, j) *
+                                                  (W3(theta, i, j, k) - W3(theta, i, j - 1, k))) +
+                                       0.5 * (W3(maskS, i, j + 1, k - 1) * L(recip_dyC, i, j + 1) *
+                                                  (W3(theta, i, j + 1, k - 1) - W3(theta, i, j, k - 1)) +
+                                              W3(maskS, i, j, k - 1) * L(recip_dyC, i, j) *
+                                                  (W3(theta, i, j, k - 1) - W3(theta, i, j - 1, k - 1))));
+            L(df, i, j) = L(df, i, j) - L(rA, i, j) * L(maskInC, i, j) *
+                                            (W3(Kwx, i, j, k) * dTdx + W3(Kwy, i, j, k) * dTdy) * L(maskUp, i, j);
+          }
+      for (long p = 0; p < n2; p++) fVerUp[p] = fVerUp[p] + df[p];
       for (int j = 1 - OLy; j <= sNy + OLy - 1; j++)
         for (int i = 1 - OLx; i <= sNx + OLx - 1; i++) {
           double T = W3(theta, i, j, k);

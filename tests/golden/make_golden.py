@@ -32,6 +32,21 @@ EXPERIMENTS = {
         "inputs": ["input/bathy.bin", "input/windx_cosy.bin", "input/SST_relax.bin"],
         "output": "results/output.txt",
     },
+    # 90x40x15 lat-lon ocean, cold start: JMD95Z, GM-Redi, CD scheme, monthly forcing.
+    # lev_t/lev_s hold 12 monthly 3-D records; the run reads record 1 only, so only
+    # that record is kept (90*40*15 fp32 = 216000 bytes).
+    "tutorial_global_oce_latlon": {
+        "inputs": ["input/bathymetry.bin", ("input/lev_t.bin", 216000), ("input/lev_s.bin", 216000),
+                   "input/lev_sst.bin", "input/lev_sss.bin", "input/ncep_qnet.bin", "input/ncep_emp.bin",
+                   "input/trenberth_taux.bin", "input/trenberth_tauy.bin"],
+        "output": "results/output.txt",
+    },
+    # BASELINE config 2: same inputs (input/prepare_run links them from
+    # tutorial_global_oce_latlon) + the pickups it restarts from at nIter0 = 36000
+    "global_ocean.90x40x15": {
+        "inputs": ["input/pickup.0000036000", "input/pickup.0000036000.meta", "input/pickup_cd.0000036000"],
+        "output": "results/output.txt",
+    },
 }
 
 _num = r"[-+]?\d*\.?\d+(?:[EeDd][-+]?\d+)?"
@@ -122,6 +137,12 @@ def main():
         out = os.path.join(HERE, exp)
         os.makedirs(out, exist_ok=True)
         for rel in spec["inputs"]:
+            if isinstance(rel, tuple):   # (path, leading bytes kept)
+                rel, nbytes = rel
+                with open(os.path.join(REF, exp, rel), "rb") as fi, \
+                        open(os.path.join(out, os.path.basename(rel)), "wb") as fo:
+                    fo.write(fi.read(nbytes))
+                continue
             shutil.copyfile(os.path.join(REF, exp, rel), os.path.join(out, os.path.basename(rel)))
         res = os.path.join(REF, exp, spec["output"])
         with open(os.path.join(out, "monitor.json"), "w") as f:
