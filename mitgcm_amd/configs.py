@@ -134,10 +134,13 @@ def advect_xy(nSx=1, nSy=2):
 
 
 def make_model(cfg, device=0, **kw):
-    g, params, state = cfg(**kw)
+    out = cfg(**kw)
+    g, params, state = out[:3]
     m = Model(g, params, device=device)
     for k, v in state.items():
         m.put(k, v)
+    if len(out) > 3:
+        m.put_forcing(out[3])
     m.init()
     return m
 

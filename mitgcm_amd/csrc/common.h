@@ -36,6 +36,12 @@ struct Params {
   int metricSphere;   // usingSphericalPolarGrid && selectMetricTerms >= 1
   double diffKhS, diffKrS;
   int saltStepping, saltAdvection, saltForcing, saltAdvScheme, multiDimAdvection, momStepping;
+  // lat-lon ocean physics (tutorial_global_oce_latlon / global_ocean.90x40x15)
+  int eosType;   // 0 LINEAR, 1 JMD95Z
+  int allowFreezing, useRealFreshWaterFlux, useCDscheme, useGMRedi, periodicExternalForcing, nForcRec;
+  double HeatCapacity_Cp, convertFW2Salt, temp_EvPrRn, salt_EvPrRn, rCD, epsAB_CD;
+  double externForcingPeriod, externForcingCycle;
+  double GM_background_K, GM_isopycK, GM_skewflx, GM_maxSlope, GM_Kmin_horiz, GM_Small_Number, GM_slopeSqCutoff;
 };
 
 // Device pointers of every field the kernels touch.
@@ -46,7 +52,8 @@ struct Fields {
   const double *dxF, *dyF, *dxG, *dyG, *dxC, *dyC, *dxV, *dyU, *rA, *rAw, *rAs;
   const double *recip_dxF, *recip_dyF, *recip_dxC, *recip_dyC, *recip_dxV, *recip_dyU;
   const double *recip_rA, *recip_rAw, *recip_rAs, *fCori, *Bo_surf, *recip_Bo;
-  const double *tanPhiAtU, *tanPhiAtV, *maskInC, *SST, *lambdaThetaClimRelax;
+  const double *tanPhiAtU, *tanPhiAtV, *maskInC, *lambdaThetaClimRelax;
+  double *SST;   // interpolated by k_fields_load
   // 3-D masks
   const double *hFacC, *hFacW, *hFacS, *recip_hFacC, *recip_hFacW, *recip_hFacS, *maskC, *maskW, *maskS;
   // CG2D operator
@@ -54,12 +61,18 @@ struct Fields {
   // state
   double *uVel, *vVel, *wVel, *theta, *salt, *etaN;
   double *gU, *gV, *guNm1, *gvNm1;
-  const double *fu, *fv;
+  double *fu, *fv;
   double *etaH, *surfaceForcingT, *rhoInSitu, *IVDConvCount, *gtNm1;
   double *thetaNext, *gTscr, *cpScr;   // tracer ping-pong buffer and per-column scratch
   double *phiHydC;                     // CALC_PHI_HYD output at cell centres (k_phi_hyd)
   double *saltNext, *gsNm1, *surfaceForcingS;
   double *advScr1, *advScr2, *gAdv;     // multi-dim advection passes and its tendency
+  // lat-lon ocean physics
+  const double *pRef4EOS;                  // [Nr] reference pressure for the EOS (set_ref_state.F)
+  const double *forcRec;                   // [6][nForcRec][tiles*n2]: SST, SSS, taux, tauy, Qnet, EmPmR
+  double *Qnet, *EmPmR, *SSS, *lambdaSaltClimRelax, *etaNm1;   // 2-D
+  double *sigmaR, *Kwx, *Kwy, *Kwz, *Kux, *Kvy;                // 3-D GM/Redi
+  double *uVelD, *vVelD, *uNM1, *vNM1, *cdU, *cdV;             // 3-D CD scheme (+ gUtmp/gVtmp scratch)
   // solver work
   double *cg2d_b, *cg2d_x;
 };

@@ -211,8 +211,9 @@ __global__ void __launch_bounds__(256) k_mom_step(Dims d, Params p, Fields f, co
         const double mTv = -(p.recip_rSphere * 0.25 * ub * 0.25 * ub * G2(tanPhiAtV, i, j));
         gV = gV + p.mtFacMom * mTv;
       }
-      // ---------------- Coriolis (mom_u_coriolis.F, mom_v_coriolis.F)
-      if (p.useCoriolis) {
+      // ---------------- Coriolis (mom_u_coriolis.F, mom_v_coriolis.F); with the CD scheme
+      // it is applied in TIMESTEP instead (mom_fluxform.F:995, k_cd_scheme)
+      if (p.useCoriolis && !p.useCDscheme) {
         const int sc = p.selectCoriScheme;
         double c;
         if (sc >= 2)
@@ -267,14 +268,18 @@ __global__ void __launch_bounds__(256) k_mom_step(Dims d, Params p, Fields f, co
       f.gvNm1[q3] = gV;
       gV = gV + a;
     }
+    double gUtmp = 0.0, gVtmp = 0.0;   // timestep.F local arrays: 0 outside iMin..iMax, jMin..jMax
     if (inner) {
-      double gUtmp = gU, gVtmp = gV;
+      gUtmp = gU; gVtmp = gV;
       if (p.momForcing && p.momForcingOutAB == 1) { gUtmp = gUtmp + guExt; gVtmp = gVtmp + gvExt; }
       if (p.momViscosity && !p.momDissip_In_AB) { gUtmp = gUtmp + guDiss; gVtmp = gVtmp + gvDiss; }
-      // u* = u + dt*(gUtmp + gUdPx)*maskW  (timestep.F:373-388), gUdPx = 0 for implicSurfPress = 1
-      gU = U(i, j, k) + p.deltaTMom * (gUtmp + 0.0) * G3(maskW, i, j, k);
-      gV = V(i, j, k) + p.deltaTMom * (gVtmp + 0.0) * G3(maskS, i, j, k);
+      if (!p.useCDscheme) {
+        // u* = u + dt*(gUtmp + gUdPx)*maskW  (timestep.F:373-388), gUdPx = 0 for implicSurfPress = 1
+        gU = U(i, j, k) + p.deltaTMom * (gUtmp + 0.0) * G3(maskW, i, j, k);
+        gV = V(i, j, k) + p.deltaTMom * (gVtmp + 0.0) * G3(maskS, i, j, k);
+      }
     }
+    if (p.useCDscheme) { f.cdU[q3] = gUtmp; f.cdV[q3] = gVtmp; }   // k_cd_scheme finishes u*
     f.gU[q3] = gU;
     f.gV[q3] = gV;
   }
@@ -285,9 +290,65 @@ __global__ void __launch_bounds__(256) k_mom_step(Dims d, Params p, Fields f, co
 #undef G3
 }
 
+// CD_CODE_SCHEME (pkg/cd_code/cd_code_scheme.F:85-236, called from timestep.F:228-270;
+// staggerTimeStep = F so phxFac = phyFac = 0) for one (i,j,k) of 2-OL..sN+OL-1:
+// the D-grid velocities uVelD/vVelD are stepped and relaxed, the Coriolis terms
+// guCor/gvCor added to gUtmp/gVtmp (cdU/cdV from k_mom_step), and u* formed on the
+// TIMESTEP range 0..sN+1.  uNM1/vNM1 = u, v is done by k_sfp_rhs (after this kernel,
+// whose neighbours still read the old values).
+__global__ void __launch_bounds__(256) k_cd_scheme(Dims d, Params p, Fields f, const int *iterPtr) {
+  MG_PLANE(2 - d.OLx, d.nx - 2, 2 - d.OLy, d.ny - 2, z)
+  const int t = d.t0 + z / d.Nr, k = z % d.Nr + 1;
+  const int myIter = *iterPtr;
+  const double ab15 = myIter == 0 ? 1.0 : 1.5 + p.epsAB_CD;
+  const double ab05 = myIter == 0 ? -0.0 : -0.5 - p.epsAB_CD;
+#define G2(a_, ii, jj) f.a_[MG_I2(d, ii, jj, t)]
+#define G3(a_, ii, jj, kk) f.a_[MG_I3(d, ii, jj, kk, t)]
+  auto pf = [&](int ii, int jj) { return G2(Bo_surf, ii, jj) * (ab15 * G2(etaN, ii, jj) + ab05 * G2(etaNm1, ii, jj)); };
+  auto afV = [&](int ii, int jj) {
+    return (G3(cdV, ii, jj, k) - (G2(recip_dyC, ii, jj) * (pf(ii, jj) - pf(ii, jj - 1)) + 0.0)) * G3(maskS, ii, jj, k);
+  };
+  auto afU = [&](int ii, int jj) {
+    return (G3(cdU, ii, jj, k) - (G2(recip_dxC, ii, jj) * (pf(ii, jj) - pf(ii - 1, jj)) + 0.0)) * G3(maskW, ii, jj, k);
+  };
+  const long q3 = MG_I3(d, i, j, k, t);
+  // vVelD at this U point
+  double vf = ((afV(i, j) + afV(i - 1, j + 1)) + (afV(i - 1, j) + afV(i, j + 1))) * 0.25 * G3(maskW, i, j, k) -
+              (G2(fCori, i, j) + G2(fCori, i - 1, j)) * 0.5 * (ab15 * G3(uVel, i, j, k) + ab05 * G3(uNM1, i, j, k));
+  double vD = f.vVelD[q3] + p.deltaTMom * vf;
+  vD = (p.rCD * vD +
+        (1.0 - p.rCD) *
+            (ab15 * ((G3(vVel, i, j, k) + G3(vVel, i - 1, j + 1, k)) + (G3(vVel, i - 1, j, k) + G3(vVel, i, j + 1, k))) * 0.25 +
+             ab05 * ((G3(vNM1, i, j, k) + G3(vNM1, i - 1, j + 1, k)) + (G3(vNM1, i - 1, j, k) + G3(vNM1, i, j + 1, k))) * 0.25)) *
+       G3(maskW, i, j, k);
+  f.vVelD[q3] = vD;
+  const double guCor = (G2(fCori, i, j) + G2(fCori, i - 1, j)) * 0.5 * vD * p.cfFacMom;
+  // uVelD at this V point
+  vf = ((afU(i, j) + afU(i + 1, j - 1)) + (afU(i + 1, j) + afU(i, j - 1))) * 0.25 * G3(maskS, i, j, k) +
+       (G2(fCori, i, j) + G2(fCori, i, j - 1)) * 0.5 * (ab15 * G3(vVel, i, j, k) + ab05 * G3(vNM1, i, j, k));
+  double uD = f.uVelD[q3] + p.deltaTMom * vf;
+  uD = (p.rCD * uD +
+        (1.0 - p.rCD) *
+            (ab15 * ((G3(uVel, i, j, k) + G3(uVel, i + 1, j - 1, k)) + (G3(uVel, i, j - 1, k) + G3(uVel, i + 1, j, k))) * 0.25 +
+             ab05 * ((G3(uNM1, i, j, k) + G3(uNM1, i + 1, j - 1, k)) + (G3(uNM1, i, j - 1, k) + G3(uNM1, i + 1, j, k))) * 0.25)) *
+       G3(maskS, i, j, k);
+  f.uVelD[q3] = uD;
+  const double gvCor = -(G2(fCori, i, j) + G2(fCori, i, j - 1)) * 0.5 * uD * p.cfFacMom;
+  if (i >= 0 && i <= d.sNx + 1 && j >= 0 && j <= d.sNy + 1) {
+    const double gUtmp = f.cdU[q3] + guCor, gVtmp = f.cdV[q3] + gvCor;
+    f.gU[q3] = G3(uVel, i, j, k) + p.deltaTMom * (gUtmp + 0.0) * G3(maskW, i, j, k);
+    f.gV[q3] = G3(vVel, i, j, k) + p.deltaTMom * (gVtmp + 0.0) * G3(maskS, i, j, k);
+  }
+#undef G2
+#undef G3
+}
+
 hipError_t launch_mom_step(const Dims &d, const Params &p, const Fields &f, const int *iterPtr, hipStream_t s) {
   hipLaunchKernelGGL(k_phi_hyd, dim3(mg_plane_blocks(d.sNx + 2, d.sNy + 2, d.nT)), dim3(MG_PLANE_THREADS), 0, s, d, p, f);
   hipLaunchKernelGGL(k_mom_step, dim3(mg_plane_blocks(d.nx, d.ny, d.nT * d.Nr)), dim3(MG_PLANE_THREADS), 0, s, d, p, f, iterPtr);
+  if (p.useCDscheme)
+    hipLaunchKernelGGL(k_cd_scheme, dim3(mg_plane_blocks(d.nx - 2, d.ny - 2, d.nT * d.Nr)), dim3(MG_PLANE_THREADS), 0, s,
+                       d, p, f, iterPtr);
   return hipGetLastError();
 }
 

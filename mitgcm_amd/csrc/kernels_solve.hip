@@ -104,14 +104,30 @@ __device__ __forceinline__ double block_max(double v, double *red, int slot) {
 }
 
 // CALC_DIV_GHAT over k = Nr..1 + free-surface term; cg2d_x = Bo_surf*etaN (full range).
+// With useRealFreshWaterFlux the RHS starts from the E-P-R volume flux
+// (solve_for_pressure.F:142-151); with the CD scheme etaNm1 = etaN
+// (solve_for_pressure.F:126-128) and CD_CODE_SCHEME's uNM1, vNM1 = u, v
+// (cd_code_scheme.F:228-234) are saved here, after every k_cd_scheme read.
 __global__ void __launch_bounds__(256) k_sfp_rhs(Dims d, Params p, Fields f) {
   MG_PLANE(1 - d.OLx, d.nx, 1 - d.OLy, d.ny, tz)
   const int t = d.t0 + tz;
   if (i > d.sNx + d.OLx || j > d.sNy + d.OLy) return;
   const long q = MG_I2(d, i, j, t);
+  if (p.useCDscheme) {
+    f.etaNm1[q] = f.etaN[q];
+    for (int k = 1; k <= d.Nr; k++) {
+      const long q3 = MG_I3(d, i, j, k, t);
+      f.uNM1[q3] = f.uVel[q3];
+      f.vNM1[q3] = f.vVel[q3];
+    }
+  }
   f.cg2d_x[q] = f.Bo_surf[q] * f.etaN[q];
   double b = 0.0;
   if (i >= 1 && i <= d.sNx && j >= 1 && j <= d.sNy) {
+    if (p.useRealFreshWaterFlux) {
+      const double tmpFac = p.freeSurfFac * (1.0 / p.rhoConst) * p.implicDiv2DFlow;
+      b = tmpFac * f.rA[q] * f.EmPmR[q] / p.deltaTMom * f.maskInC[q];
+    }
     for (int k = d.Nr; k >= 1; k--) {
       const double drF = f.drF[k - 1];
       const double pfE = f.dyG[MG_I2(d, i + 1, j, t)] * drF * f.hFacW[MG_I3(d, i + 1, j, k, t)] *
@@ -674,7 +690,8 @@ __global__ void __launch_bounds__(256) k_continuity_ec(Dims d, Params p, Fields 
   };
   double hDiv = 0.0;
   for (int k = 1; k <= d.Nr; k++) hDiv = hDiv + f.maskC[MG_I3(d, i, j, k, t)] * div(k);
-  const double dEtaHdt = -(hDiv * f.recip_rA[q]) - 0.0 * 0.0;
+  const double facEmP = p.useRealFreshWaterFlux ? 1.0 / p.rhoConst : 0.0;
+  const double dEtaHdt = -(hDiv * f.recip_rA[q]) - facEmP * f.EmPmR[q];
   f.etaN[q] = f.etaH[q] + p.implicDiv2DFlow * dEtaHdt * p.deltaTFreeSurf;
   double wBelow = 0.0;
   for (int k = d.Nr; k >= 1; k--) {
@@ -782,7 +799,8 @@ __global__ void __launch_bounds__(256) k_corr_cont(Dims d, Params p, Fields f) {
       const double u0 = uCor(i, k, pX0), u1 = uCor(i + 1, k, pX1), v0 = vCor(j, k, pY0), v1 = vCor(j + 1, k, pY1);
       hDiv = hDiv + f.maskC[MG_I3(d, i, j, k, t)] * div(k, u0, u1, v0, v1);
     }
-    const double dEtaHdt = -(hDiv * f.recip_rA[q]) - 0.0 * 0.0;
+    const double facEmP = p.useRealFreshWaterFlux ? 1.0 / p.rhoConst : 0.0;   // integr_continuity.F:183-188
+    const double dEtaHdt = -(hDiv * f.recip_rA[q]) - facEmP * f.EmPmR[q];
     f.cg2d_b[q] = f.etaH[q] + p.implicDiv2DFlow * dEtaHdt * p.deltaTFreeSurf;
   }
   double wBelow = 0.0;

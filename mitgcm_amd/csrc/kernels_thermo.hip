@@ -26,35 +26,182 @@
 
 namespace mgcm {
 
-__device__ __forceinline__ double rho_linear(const Params &p, const Fields &f, int kRef, double t, double s) {
+// FIND_RHO_2D at one point (find_rho.F:84-99 LINEAR, :146-180 JMD95Z with
+// FIND_RHOP0 :274-409 and FIND_BULKMOD :411-590, coefficients ini_eos.F:113-160;
+// selectP_inEOS_Zc = 0: locPres = pRef4EOS(kRef), pressure_for_eos.F:88-96).
+__device__ __forceinline__ double jmd95_rho(const Params &p, double locPres, double t, double s) {
+  const double t2 = t * t, t3 = t2 * t, t4 = t3 * t;
+  double s3o2;
+  if (s > 0.0) s3o2 = s * sqrt(s);
+  else { s = 0.0; s3o2 = 0.0; }
+  const double rfresh = 999.842594 + 6.793952e-02 * t + -9.095290e-03 * t2 + 1.001685e-04 * t3 +
+                        -1.120083e-06 * t4 + 6.536332e-09 * t4 * t;
+  const double rsalt = s * (8.24493e-01 + -4.0899e-03 * t + 7.6438e-05 * t2 + -8.2467e-07 * t3 + 5.3875e-09 * t4) +
+                       s3o2 * (-5.72466e-03 + 1.0227e-04 * t + -1.6546e-06 * t2) + 4.8314e-04 * s * s;
+  const double rhoP0 = rfresh + rsalt;
+  const double pb = locPres * 1.0e-05, p2 = pb * pb;
+  const double bMfresh = 1.965933e+04 + 1.444304e+02 * t + -1.706103e+00 * t2 + 9.648704e-03 * t3 +
+                         -4.190253e-05 * t4;
+  const double bMsalt = s * (5.284855e+01 + -3.101089e-01 * t + 6.283263e-03 * t2 + -5.084188e-05 * t3) +
+                        s3o2 * (3.886640e-01 + 9.085835e-03 * t + -4.619924e-04 * t2);
+  const double bMpres = pb * (3.186519e+00 + 2.212276e-02 * t + -2.984642e-04 * t2 + 1.956415e-06 * t3) +
+                        pb * s * (6.704388e-03 + -1.847318e-04 * t + 2.059331e-07 * t2) + pb * s3o2 * 1.480266e-04 +
+                        p2 * (2.102898e-04 + -1.202016e-05 * t + 1.394680e-07 * t2) +
+                        p2 * s * (-2.040237e-06 + 6.128773e-08 * t + 6.207323e-10 * t2);
+  const double bulkMod = bMfresh + bMsalt + bMpres;
+  return rhoP0 / (1.0 - locPres * 1.0e-05 / bulkMod) - p.rhoConst;
+}
+__device__ __forceinline__ double find_rho(const Params &p, const Fields &f, int kRef, double t, double s) {
+  if (p.eosType == 1) return jmd95_rho(p, f.pRef4EOS[kRef - 1] + 0.0, t, s);
   const double refTemp = f.tRef[kRef - 1], refSalt = f.sRef[kRef - 1];
   const double dRho = p.rhoNil - p.rhoConst;
   return p.rhoNil * (p.sBeta * (s - refSalt) - p.tAlpha * (t - refTemp)) + dRho;
 }
 
+// EXTERNAL_FIELDS_LOAD (external_fields_load.F:56-330) with GET_PERIODIC_INTERVAL
+// (get_periodic_interval.F:106-117), at myTime = myIter*deltaTClock read from the
+// device step counter (the step's start time, as LOAD_FIELDS_DRIVER sees it).
+__global__ void __launch_bounds__(256) k_fields_load(Dims d, Params p, Fields f, const int *iterPtr) {
+  const long q = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  const long N2 = d.n2 * d.nTiles;
+  if (q >= N2) return;
+  const double cycleLength = p.externForcingCycle, recSpacing = p.externForcingPeriod;
+  const double currentTime = (double)(*iterPtr) * p.deltaTClock;
+  const int nbRec = (int)llround(cycleLength / recSpacing);
+  const double locTime = currentTime - recSpacing * 0.5 + cycleLength * (double)(2 - llround(currentTime / cycleLength));
+  const double tmpTime = fmod(locTime, cycleLength);
+  const int tRec1 = 1 + (int)(tmpTime / recSpacing);
+  const int tRec2 = 1 + tRec1 % nbRec;
+  const double aW = (tmpTime - recSpacing * (double)(tRec1 - 1)) / recSpacing;
+  const double bW = 1.0 - aW;
+  double *dst[6] = {f.SST, f.SSS, f.fu, f.fv, f.Qnet, f.EmPmR};
+#pragma unroll
+  for (int v = 0; v < 6; v++) {
+    const double *r = f.forcRec + (long)v * p.nForcRec * N2;
+    dst[v][q] = bW * r[(long)(tRec1 - 1) * N2 + q] + aW * r[(long)(tRec2 - 1) * N2 + q];
+  }
+}
+
+// DO_OCEANIC_PHYS (do_oceanic_phys.F:548-882) per column over the full halo range:
+// FREEZE_SURFACE (freeze_surface.F:55-66), EXTERNAL_FORCING_SURF with
+// FORCING_SURF_RELAX (external_forcing_surf.F:90-290, forcing_surf_relax.F:75-100;
+// linear free surface), FIND_RHO_2D at every level (kRef = k), GRAD_SIGMA's sigmaR with
+// rho(theta(k-1), kRef = k) (grad_sigma.F:103-117) and CALC_IVDC (calc_ivdc.F:60-71).
 __global__ void __launch_bounds__(256) k_oceanic_phys(Dims d, Params p, Fields f) {
   MG_PLANE(1 - d.OLx, d.nx, 1 - d.OLy, d.ny, tz)
   const int t = d.t0 + tz;
   if (i > d.sNx + d.OLx || j > d.sNy + d.OLy) return;
-  const long q = MG_I2(d, i, j, t);
-  f.surfaceForcingT[q] =
-      -(f.lambdaThetaClimRelax[q] * (f.theta[MG_I3(d, i, j, 1, t)] - f.SST[q]) * f.drF[0] * f.hFacC[MG_I3(d, i, j, 1, t)]);
-  double rhoUp = 0.0, thUp = 0.0, sUp = 0.0, mUp = 0.0;
+  const long q = MG_I2(d, i, j, t), q31 = MG_I3(d, i, j, 1, t);
+  if (p.allowFreezing && f.theta[q31] < -1.9) f.theta[q31] = -1.9;
+  const double mass2rUnit = 1.0 / p.rhoConst, recip_Cp = 1.0 / p.HeatCapacity_Cp;
+  const double th1 = f.theta[q31], s1 = f.salt[q31];
+  double sfT = -(f.lambdaThetaClimRelax[q] * (th1 - f.SST[q]) * f.drF[0] * f.hFacC[q31]);
+  double sfS = -(f.lambdaSaltClimRelax[q] * (s1 - f.SSS[q]) * f.drF[0] * f.hFacC[q31]);
+  sfT = sfT - f.Qnet[q] * recip_Cp * mass2rUnit;
+  sfS = sfS - 0.0 * mass2rUnit;   // saltFlux = 0
+  {
+    const double UNSET_RL = 123456.7;
+    if (p.convertFW2Salt == -1.0) {
+      if (p.temp_EvPrRn != UNSET_RL) sfT = sfT + f.EmPmR[q] * (th1 - p.temp_EvPrRn) * mass2rUnit;
+      if (p.salt_EvPrRn != UNSET_RL) sfS = sfS + f.EmPmR[q] * (s1 - p.salt_EvPrRn) * mass2rUnit;
+    } else {
+      if (p.temp_EvPrRn != UNSET_RL) sfT = sfT + f.EmPmR[q] * (f.tRef[0] - p.temp_EvPrRn) * mass2rUnit;
+      if (p.salt_EvPrRn != UNSET_RL) sfS = sfS + f.EmPmR[q] * (p.convertFW2Salt - p.salt_EvPrRn) * mass2rUnit;
+    }
+  }
+  f.surfaceForcingT[q] = sfT;
+  f.surfaceForcingS[q] = sfS;
+  const bool calcConvect = p.ivdc_kappa != 0.0;
+  double thUp = 0.0, sUp = 0.0, mUp = 0.0;
   for (int k = 1; k <= d.Nr; k++) {
     const long q3 = MG_I3(d, i, j, k, t);
     const double th = f.theta[q3], sa = f.salt[q3], mC = f.maskC[q3];
-    const double rho = rho_linear(p, f, k, th, sa);
+    const double rho = find_rho(p, f, k, th, sa);
     f.rhoInSitu[q3] = rho;
-    double conv = 0.0;
-    if (k >= 2 && p.ivdc_kappa != 0.0) {
-      const double rhoKm1 = rho_linear(p, f, k, thUp, sUp);
-      const double sigmaR = mC * mUp * f.recip_drC[k - 1] * p.rkSign * (rho - rhoKm1);
-      conv = (-sigmaR * p.gravitySign > 0.0) ? 1.0 : 0.0;
+    double conv = 0.0, sigmaR = 0.0;
+    if (k >= 2 && (calcConvect || p.useGMRedi)) {
+      const double rhoKm1 = find_rho(p, f, k, thUp, sUp);
+      sigmaR = mC * mUp * f.recip_drC[k - 1] * p.rkSign * (rho - rhoKm1);
+      if (calcConvect) conv = (-sigmaR * p.gravitySign > 0.0) ? 1.0 : 0.0;
     }
     f.IVDConvCount[q3] = conv;
-    rhoUp = rho; thUp = th; sUp = sa; mUp = mC;
+    if (p.useGMRedi) f.sigmaR[q3] = sigmaR;
+    thUp = th; sUp = sa; mUp = mC;
   }
-  (void)rhoUp;
+}
+
+// GMREDI_CALC_TENSOR (pkg/gmredi/gmredi_calc_tensor.F:231-790; skew flux, GM_ExtraDiag
+// = F, all isoFac/bolFac = 1) with GMREDI_SLOPE_LIMIT's gkw91 taper
+// (gmredi_slope_limit.F:280-370), one thread per (i,j,k) on i,j = 2-OL..sN+OL-1.
+// sigmaX/Y (GRAD_SIGMA, grad_sigma.F:80-101) are recomputed from rhoInSitu.
+__device__ __forceinline__ void gm_slope_gkw91(const Params &p, double dSx, double dSy, double dSr, double &SlopeX,
+                                               double &SlopeY, double &SlopeSqr, double &taper) {
+  const double GM_bigSlope = 1.0e+02, maxSlopeSqr = p.GM_maxSlope * p.GM_maxSlope;
+  if (dSr != 0.0 && dSr <= p.GM_Small_Number) dSr = p.GM_Small_Number;
+  if (dSr == 0.0) {
+    SlopeX = dSx != 0.0 ? copysign(GM_bigSlope, dSx) : 0.0;
+    SlopeY = dSy != 0.0 ? copysign(GM_bigSlope, dSy) : 0.0;
+  } else {
+    const double dRdSigmaLtd = 1.0 / dSr;
+    SlopeX = dSx * dRdSigmaLtd;
+    SlopeY = dSy * dRdSigmaLtd;
+  }
+  SlopeSqr = SlopeX * SlopeX + SlopeY * SlopeY;
+  taper = 1.0;
+  if (SlopeSqr >= p.GM_slopeSqCutoff) { SlopeSqr = p.GM_slopeSqCutoff; taper = 0.0; }
+  if (SlopeSqr == 0.0) taper = 1.0;
+  else if (SlopeSqr > maxSlopeSqr && SlopeSqr < p.GM_slopeSqCutoff) taper = maxSlopeSqr / SlopeSqr;
+}
+
+__global__ void __launch_bounds__(256) k_gm_tensor(Dims d, Params p, Fields f) {
+  MG_PLANE(2 - d.OLx, d.nx - 2, 2 - d.OLy, d.ny - 2, z)
+  const int t = d.t0 + z / d.Nr, k = z % d.Nr + 1;
+  const int Nr = d.Nr;
+  auto rho = [&](int ii, int jj, int kk) { return f.rhoInSitu[MG_I3(d, ii, jj, kk, t)]; };
+  auto sX = [&](int ii, int jj, int kk) {
+    return f.maskW[MG_I3(d, ii, jj, kk, t)] * f.recip_dxC[MG_I2(d, ii, jj, t)] * (rho(ii, jj, kk) - rho(ii - 1, jj, kk));
+  };
+  auto sY = [&](int ii, int jj, int kk) {
+    return f.maskS[MG_I3(d, ii, jj, kk, t)] * f.recip_dyC[MG_I2(d, ii, jj, t)] * (rho(ii, jj, kk) - rho(ii, jj - 1, kk));
+  };
+  auto sR = [&](int ii, int jj, int kk) { return f.sigmaR[MG_I3(d, ii, jj, kk, t)]; };
+  const double op25 = 0.25, op5 = 0.5, gs = p.gravitySign;
+  const long q3 = MG_I3(d, i, j, k, t);
+  const double isopycK = p.GM_isopycK * (1.0 + 1.0) * op5, bolus_K = p.GM_background_K * (1.0 + 1.0) * op5;
+  double SlopeX, SlopeY, SlopeSqr, taper;
+  // Kwx, Kwy, Kwz (W points, k >= 2; k = 1 stays 0)
+  double kwx = 0.0, kwy = 0.0, kwz = 0.0;
+  if (k >= 2) {
+    const double maskFk = f.maskC[MG_I3(d, i, j, k - 1, t)] * f.maskC[q3];
+    const double dSx = op25 * (sX(i + 1, j, k - 1) + sX(i, j, k - 1) + sX(i + 1, j, k) + sX(i, j, k)) * maskFk;
+    const double dSy = op25 * (sY(i, j + 1, k - 1) + sY(i, j, k - 1) + sY(i, j + 1, k) + sY(i, j, k)) * maskFk;
+    gm_slope_gkw91(p, dSx, dSy, gs * sR(i, j, k), SlopeX, SlopeY, SlopeSqr, taper);
+    kwx = -gs * SlopeX * taper;
+    kwy = -gs * SlopeY * taper;
+    kwz = SlopeSqr * taper;
+  }
+  const double Kgm_tmp = isopycK * 1.0 + p.GM_skewflx * bolus_K * 1.0;
+  f.Kwx[q3] = Kgm_tmp * kwx;
+  f.Kwy[q3] = Kgm_tmp * kwy;
+  f.Kwz[q3] = (isopycK * 1.0) * kwz;
+  const int kp1 = k + 1 < Nr ? k + 1 : Nr;
+  const double maskp1 = k >= Nr ? 0.0 : 1.0;
+  {  // Kux (U points)
+    const double mW = f.maskW[q3];
+    const double dSx = sX(i, j, k) * mW;
+    const double dSy = op25 * (sY(i - 1, j + 1, k) + sY(i, j + 1, k) + sY(i - 1, j, k) + sY(i, j, k)) * mW;
+    const double dSr = op25 * (sR(i - 1, j, k) + sR(i, j, k) + (sR(i - 1, j, kp1) + sR(i, j, kp1)) * maskp1) * mW * gs;
+    gm_slope_gkw91(p, dSx, dSy, dSr, SlopeX, SlopeY, SlopeSqr, taper);
+    f.Kux[q3] = fmax((p.GM_isopycK * 1.0 * op5 * (1.0 + 1.0)) * taper, p.GM_Kmin_horiz);
+  }
+  {  // Kvy (V points)
+    const double mS = f.maskS[q3];
+    const double dSx = op25 * (sX(i, j, k) + sX(i + 1, j, k) + sX(i, j - 1, k) + sX(i + 1, j - 1, k)) * mS;
+    const double dSy = sY(i, j, k) * mS;
+    const double dSr = op25 * (sR(i, j - 1, k) + sR(i, j, k) + (sR(i, j - 1, kp1) + sR(i, j, kp1)) * maskp1) * mS * gs;
+    gm_slope_gkw91(p, dSx, dSy, dSr, SlopeX, SlopeY, SlopeSqr, taper);
+    f.Kvy[q3] = fmax((p.GM_isopycK * 1.0 * op5 * (1.0 + 1.0)) * taper, p.GM_Kmin_horiz);
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -190,6 +337,8 @@ __global__ void __launch_bounds__(256) k_tracer_rhs(Dims d, Params p, Fields f, 
     if (calcAdv) fz = fz + (G3(uVel, ii, j, k) * xA) * (T3(ii, j, k) + T3(ii - 1, j, k)) * 0.5;
     double df = 0.0;
     if (a.diffKh != 0.0) df = -a.diffKh * xA * G2(recip_dxC, ii, j) * (T3(ii, j, k) - T3(ii - 1, j, k));
+    if (p.useGMRedi)   // GMREDI_XTRANSPORT (gmredi_xtransport.F:94-101)
+      df = df - xA * G3(Kux, ii, j, k) * G2(recip_dxC, ii, j) * (T3(ii, j, k) - T3(ii - 1, j, k));
     return fz + df;
   };
   auto fmer = [&](int jj) {
@@ -198,6 +347,8 @@ __global__ void __launch_bounds__(256) k_tracer_rhs(Dims d, Params p, Fields f, 
     if (calcAdv) fm = fm + (G3(vVel, i, jj, k) * yA) * (T3(i, jj, k) + T3(i, jj - 1, k)) * 0.5;
     double df = 0.0;
     if (a.diffKh != 0.0) df = -a.diffKh * yA * G2(recip_dyC, i, jj) * (T3(i, jj, k) - T3(i, jj - 1, k));
+    if (p.useGMRedi)   // GMREDI_YTRANSPORT
+      df = df - yA * G3(Kvy, i, jj, k) * G2(recip_dyC, i, jj) * (T3(i, jj, k) - T3(i, jj - 1, k));
     return fm + df;
   };
   // CALC_ADV_FLOW rTrans of level kk (0 at the surface and below the bottom level)
@@ -216,9 +367,24 @@ __global__ void __launch_bounds__(256) k_tracer_rhs(Dims d, Params p, Fields f, 
     }
     double dfr = 0.0;
     if (!p.implicitDiffusion && kk >= 2 && kk <= Nr) {
-      const double kap = (G3(IVDConvCount, i, j, kk) * p.ivdc_kappa + 0.0) + a.diffKr;
+      double kap = (G3(IVDConvCount, i, j, kk) * p.ivdc_kappa + 0.0) + a.diffKr;
+      if (p.useGMRedi) kap = kap + G3(Kwz, i, j, kk) * maskInC;
       const double maskUp = G3(maskC, i, j, kk - 1) * G3(maskC, i, j, kk);
       dfr = -kap * maskUp * rA * f.recip_drC[kk - 1] * (T3(i, j, kk) - T3(i, j, kk - 1)) * p.rkSign;
+    }
+    if (p.useGMRedi && kk >= 2 && kk <= Nr) {   // GMREDI_RTRANSPORT (gmredi_rtransport.F:75-130)
+      const double dTdx =
+          0.5 * (0.5 * (G3(maskW, i + 1, j, kk) * G2(recip_dxC, i + 1, j) * (T3(i + 1, j, kk) - T3(i, j, kk)) +
+                        G3(maskW, i, j, kk) * G2(recip_dxC, i, j) * (T3(i, j, kk) - T3(i - 1, j, kk))) +
+                 0.5 * (G3(maskW, i + 1, j, kk - 1) * G2(recip_dxC, i + 1, j) * (T3(i + 1, j, kk - 1) - T3(i, j, kk - 1)) +
+                        G3(maskW, i, j, kk - 1) * G2(recip_dxC, i, j) * (T3(i, j, kk - 1) - T3(i - 1, j, kk - 1))));
+      const double dTdy =
+          0.5 * (0.5 * (G3(maskS, i, j + 1, kk) * G2(recip_dyC, i, j + 1) * (T3(i, j + 1, kk) - T3(i, j, kk)) +
+                        G3(maskS, i, j, kk) * G2(recip_dyC, i, j) * (T3(i, j, kk) - T3(i, j - 1, kk))) +
+                 0.5 * (G3(maskS, i, j + 1, kk - 1) * G2(recip_dyC, i, j + 1) * (T3(i, j + 1, kk - 1) - T3(i, j, kk - 1)) +
+                        G3(maskS, i, j, kk - 1) * G2(recip_dyC, i, j) * (T3(i, j, kk - 1) - T3(i, j - 1, kk - 1))));
+      const double maskUp = G3(maskC, i, j, kk - 1) * G3(maskC, i, j, kk);
+      dfr = dfr - rA * maskInC * (G3(Kwx, i, j, kk) * dTdx + G3(Kwy, i, j, kk) * dTdy) * maskUp;
     }
     return fv + dfr;
   };
@@ -266,12 +432,17 @@ __global__ void __launch_bounds__(256) k_tracer_impl(Dims d, Params p, Fields f,
     const long q3 = MG_I3(d, i, j, k, t);
     const double rh = f.recip_hFacC[q3], rdrF = f.recip_drF[k - 1];
     double sub = 0.0, sup = 0.0;
+    const double mIn = f.maskInC[MG_I2(d, i, j, t)];
+    // KappaRT = (IVDConvCount*ivdc_kappa + BL79(=0)) + diffKrNr [+ Kwz*maskInC] (calc_3d_diffusivity.F)
+    auto kappa = [&](int kk) {
+      double kap = (G3(IVDConvCount, i, j, kk) * p.ivdc_kappa + 0.0) + a.diffKr;
+      if (p.useGMRedi) kap = kap + G3(Kwz, i, j, kk) * mIn;
+      return kap;
+    };
     if (k >= 2)
-      sub = -(p.deltaTtracer * G3(maskC, i, j, k - 1) * rh * rdrF *
-              ((G3(IVDConvCount, i, j, k) * p.ivdc_kappa + 0.0) + a.diffKr) * f.recip_drC[k - 1]);
+      sub = -(p.deltaTtracer * G3(maskC, i, j, k - 1) * rh * rdrF * kappa(k) * f.recip_drC[k - 1]);
     if (k <= Nr - 1)
-      sup = -(p.deltaTtracer * G3(maskC, i, j, k + 1) * rh * rdrF *
-              ((G3(IVDConvCount, i, j, k + 1) * p.ivdc_kappa + 0.0) + a.diffKr) * f.recip_drC[k]);
+      sup = -(p.deltaTtracer * G3(maskC, i, j, k + 1) * rh * rdrF * kappa(k + 1) * f.recip_drC[k]);
     const double diag = 1.0 - (sub + sup);
     const double y = f.gTscr[q3];
     double cp, yp;
@@ -297,8 +468,15 @@ __global__ void __launch_bounds__(256) k_tracer_impl(Dims d, Params p, Fields f,
 #undef G3
 }
 
-hipError_t launch_oceanic_phys(const Dims &d, const Params &p, const Fields &f, hipStream_t s) {
+hipError_t launch_oceanic_phys(const Dims &d, const Params &p, const Fields &f, const int *iterPtr, hipStream_t s) {
+  if (p.periodicExternalForcing) {
+    const long n = d.n2 * d.nTiles;
+    hipLaunchKernelGGL(k_fields_load, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, d, p, f, iterPtr);
+  }
   hipLaunchKernelGGL(k_oceanic_phys, dim3(mg_plane_blocks(d.nx, d.ny, d.nT)), dim3(MG_PLANE_THREADS), 0, s, d, p, f);
+  if (p.useGMRedi)
+    hipLaunchKernelGGL(k_gm_tensor, dim3(mg_plane_blocks(d.nx - 2, d.ny - 2, d.nT * d.Nr)), dim3(MG_PLANE_THREADS), 0,
+                       s, d, p, f);
   return hipGetLastError();
 }
 

@@ -37,7 +37,7 @@ hipError_t launch_exchange_multi(const Dims &, const XFields &, const long *, in
 hipError_t launch_exch_eta(const Dims &, const Fields &, const long *, bool, hipStream_t);
 hipError_t launch_corr_cont(const Dims &, const Params &, const Fields &, hipStream_t);
 hipError_t launch_halo_pack(const Dims &, const XFields &, const long *, long, double *, int, hipStream_t);
-hipError_t launch_oceanic_phys(const Dims &, const Params &, const Fields &, hipStream_t);
+hipError_t launch_oceanic_phys(const Dims &, const Params &, const Fields &, const int *, hipStream_t);
 hipError_t launch_tracer_step(const Dims &, const Params &, const Fields &, const TracerArgs &, const int *, hipStream_t);
 hipError_t launch_continuity_ec(const Dims &, const Params &, const Fields &, hipStream_t);
 hipError_t launch_copy(double *, const double *, long, hipStream_t);
@@ -61,7 +61,8 @@ static int set_err(const char *fmt, ...) {
     if (e_ != hipSuccess) return set_err("%s:%d %s: %s", __FILE__, __LINE__, #x, hipGetErrorString(e_)); \
   } while (0)
 
-enum FieldKind { F1D, F2D, F3D };
+enum FieldKind { F1D, F2D, F3D, FREC };   // FREC: 6 forcing fields x MG_MAXREC records of 2-D
+#define MG_MAXREC 12
 struct FieldDesc {
   const char *name;
   FieldKind kind;
@@ -86,6 +87,9 @@ static const FieldDesc FIELDS[] = {
     FD(thetaNext, F3D), FD(gTscr, F3D), FD(cpScr, F3D), FD(phiHydC, F3D), FD(saltNext, F3D), FD(gsNm1, F3D),
     FD(surfaceForcingS, F2D), FD(advScr1, F3D), FD(advScr2, F3D), FD(gAdv, F3D),
     FD(cg2d_b, F2D), FD(cg2d_x, F2D),
+    FD(pRef4EOS, F1D), FD(forcRec, FREC), FD(Qnet, F2D), FD(EmPmR, F2D), FD(SSS, F2D), FD(lambdaSaltClimRelax, F2D),
+    FD(etaNm1, F2D), FD(sigmaR, F3D), FD(Kwx, F3D), FD(Kwy, F3D), FD(Kwz, F3D), FD(Kux, F3D), FD(Kvy, F3D),
+    FD(uVelD, F3D), FD(vVelD, F3D), FD(uNM1, F3D), FD(vNM1, F3D), FD(cdU, F3D), FD(cdV, F3D),
 };
 #undef FD
 
@@ -108,6 +112,10 @@ static const PDesc PARAMS[] = {
     PD(deltaTtracer), PI_(exactConserv), PI_(tempStepping), PI_(tempAdvection), PI_(tempForcing),
     PI_(implicitDiffusion), PI_(tempAdvScheme), PI_(saltStepping), PI_(saltAdvection), PI_(saltForcing),
     PI_(saltAdvScheme), PD(diffKhS), PD(diffKrS), PI_(multiDimAdvection), PI_(momStepping),
+    PI_(eosType), PI_(allowFreezing), PI_(useRealFreshWaterFlux), PI_(useCDscheme), PI_(useGMRedi),
+    PI_(periodicExternalForcing), PI_(nForcRec), PD(HeatCapacity_Cp), PD(convertFW2Salt), PD(temp_EvPrRn),
+    PD(salt_EvPrRn), PD(rCD), PD(epsAB_CD), PD(externForcingPeriod), PD(externForcingCycle), PD(GM_background_K),
+    PD(GM_isopycK), PD(GM_skewflx), PD(GM_maxSlope), PD(GM_Kmin_horiz), PD(GM_Small_Number), PD(GM_slopeSqCutoff),
 };
 #undef PD
 #undef PI_
@@ -164,6 +172,7 @@ static void drop_graphs(mgcm_model *m);
 static long field_count(const mgcm_model *m, FieldKind k) {
   if (k == F1D) return m->d.Nr + 1;
   if (k == F2D) return m->d.n2 * m->d.nTiles;
+  if (k == FREC) return 6L * MG_MAXREC * m->d.n2 * m->d.nTiles;
   return m->d.n3 * m->d.nTiles;
 }
 static const FieldDesc *find_field(const char *name) {
@@ -385,6 +394,8 @@ mgcm_model *mgcm_create(int sNx, int sNy, int OLx, int OLy, int Nr, int nSx, int
   p.gravity = 9.81; p.gravitySign = -1.0; p.rhoNil = 999.8; p.tAlpha = 2.0e-4; p.tempAdvection = 1;
   p.tempForcing = 1; p.tempAdvScheme = 2; p.implicitDiffusion = 0;
   p.saltAdvection = 1; p.saltForcing = 1; p.saltAdvScheme = 2; p.multiDimAdvection = 1; p.momStepping = 1;
+  p.HeatCapacity_Cp = 3994.0; p.convertFW2Salt = 35.0; p.temp_EvPrRn = 123456.7; p.salt_EvPrRn = 0.0;
+  p.nForcRec = 12; p.GM_Small_Number = 1.0e-20; p.GM_slopeSqCutoff = 1.0e48; p.GM_skewflx = 1.0;
   if (hipStreamCreateWithFlags(&m->ownStream, hipStreamNonBlocking) != hipSuccess) {
     set_err("mgcm_create: stream");
     delete m;
@@ -450,9 +461,8 @@ int mgcm_set_param(mgcm_model *m, const char *name, double value) {
   // options the kernels do not implement are accepted only at their default
   // (inert) value; anything else is an explicit error, never silently ignored.
   static const char *inert[] = {"useBiharmonicVisc", "nonlinFreeSurf", "select_rStar",
-                                "useCDscheme", "vectorInvariantMomentum", "useNHMTerms",
-                                "staggerTimeStep",
-                                "implicitFreeSurface", "useRealFreshWaterFlux", "useGMRedi"};
+                                "vectorInvariantMomentum", "useNHMTerms", "staggerTimeStep",
+                                "implicitFreeSurface"};
   for (auto *n : inert)
     if (!strcmp(n, name)) {
       const bool isDefaultOff = (value == 0.0) || (!strcmp(n, "implicitFreeSurface") && value == 1.0);
@@ -552,6 +562,9 @@ int mgcm_init(mgcm_model *m) {
     return set_err("mgcm_init: tempAdvScheme %d not implemented on the device", m->p.tempAdvScheme);
   if (m->p.saltStepping && !okScheme(m->p.saltAdvScheme, "saltVertAdvScheme"))
     return set_err("mgcm_init: saltAdvScheme %d not implemented on the device", m->p.saltAdvScheme);
+  if (m->p.eosType != 0 && m->p.eosType != 1) return set_err("mgcm_init: eosType %d not implemented", m->p.eosType);
+  if (m->p.periodicExternalForcing && (m->p.nForcRec < 1 || m->p.nForcRec > MG_MAXREC))
+    return set_err("mgcm_init: nForcRec %d outside 1..%d", m->p.nForcRec, MG_MAXREC);
   drop_graphs(m);
   m->thetaA = m->f.theta;
   m->saltA = m->f.salt;
@@ -614,7 +627,7 @@ int mgcm_thermodynamics(mgcm_model *m) {
   if (check_ready(m)) return -1;
   if (!m->p.tempStepping && !m->p.saltStepping) return 0;
   // forward_step.F:656 DO_OCEANIC_PHYS, :732 THERMODYNAMICS (staggerTimeStep = F)
-  TIMED(K_PHYS, launch_oceanic_phys(m->d, m->p, m->f, m->stream));
+  TIMED(K_PHYS, launch_oceanic_phys(m->d, m->p, m->f, m->d_ctr, m->stream));
   if (m->p.tempStepping) {
     TIMED(K_TEMP, launch_tracer_step(m->d, m->p, m->f, tracer_args(m, false), m->d_ctr, m->stream));
     std::swap(m->f.theta, m->f.thetaNext);   // CYCLE_TRACER: the new theta is the other buffer

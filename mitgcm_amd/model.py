@@ -19,10 +19,13 @@ GRID_2D = ("dxF", "dyF", "dxG", "dyG", "dxC", "dyC", "dxV", "dyU", "rA", "rAw", 
            "aW2d", "aS2d", "aC2d", "pW", "pS", "pC", "maskInC", "tanPhiAtU", "tanPhiAtV")
 GRID_3D = ("hFacC", "hFacW", "hFacS", "recip_hFacC", "recip_hFacW", "recip_hFacS", "maskC", "maskW", "maskS")
 GRID_1D = ("drF", "drC", "recip_drF", "recip_drC", "rF", "rC")
-STATE_1D = ("tRef", "sRef")
+STATE_1D = ("tRef", "sRef", "pRef4EOS")
 STATE_3D = ("uVel", "vVel", "wVel", "theta", "salt", "gU", "gV", "guNm1", "gvNm1", "gtNm1", "gsNm1", "rhoInSitu",
-            "IVDConvCount")
-STATE_2D = ("etaN", "etaH", "fu", "fv", "SST", "lambdaThetaClimRelax", "surfaceForcingT", "surfaceForcingS")
+            "IVDConvCount", "sigmaR", "Kwx", "Kwy", "Kwz", "Kux", "Kvy", "uVelD", "vVelD", "uNM1", "vNM1")
+STATE_2D = ("etaN", "etaH", "fu", "fv", "SST", "lambdaThetaClimRelax", "surfaceForcingT", "surfaceForcingS",
+            "Qnet", "EmPmR", "SSS", "lambdaSaltClimRelax", "etaNm1")
+# EXTERNAL_FIELDS_LOAD records, in the device's forcRec order
+FORCING_ORDER = ("SST", "SSS", "taux", "tauy", "Qnet", "EmPmR")
 
 DEVICE_PARAMS = ("deltaTMom", "deltaTFreeSurf", "deltaTClock", "abEps", "rhoConst", "gBaro", "viscAhD",
                  "viscAhZ", "viscA4D", "viscA4Z", "viscAr", "sideDragFactor", "freeSurfFac", "implicSurfPress",
@@ -84,6 +87,12 @@ class Model:
         if name in GRID_3D or name in STATE_3D:
             return (g.nTiles, g.Nr, g.ny, g.nx)
         return (g.nTiles, g.ny, g.nx)
+
+    def put_forcing(self, forcing):
+        """Upload the periodic forcing records (configs: {name: (nRec, nTiles, ny, nx)})."""
+        recs = np.stack([np.asarray(forcing[n], dtype=np.float64) for n in FORCING_ORDER])
+        check(lib().mgcm_set_param(self.h, b"nForcRec", float(recs.shape[1])), "nForcRec")
+        self.put("forcRec", recs)
 
     def put(self, name, arr):
         a = np.ascontiguousarray(arr, dtype=np.float64)

@@ -44,7 +44,7 @@ def lib():
         L.oracle_ini_depths.restype = c_int
         for fn in ("oracle_dynamics", "oracle_solve_for_pressure", "oracle_momentum_correction_step",
                    "oracle_integr_continuity", "oracle_forward_step", "oracle_oceanic_phys",
-                   "oracle_thermodynamics"):
+                   "oracle_thermodynamics", "oracle_fields_load"):
             getattr(L, fn).argtypes = [vp]
         P = ctypes.POINTER(c_dbl)
         L.oracle_cg2d.argtypes = [vp, P, P, P, P, P, ctypes.POINTER(c_int), ctypes.POINTER(c_int)]
