@@ -35,8 +35,9 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=20)
-    ap.add_argument("--config", default="baroclinic_gyre_dst3",
-                    choices=["baroclinic_gyre_dst3", "tutorial_baroclinic_gyre", "tutorial_barotropic_gyre"])
+    ap.add_argument("--config", default="global_oce_latlon_90x40x15",
+                    choices=["global_oce_latlon_90x40x15", "tutorial_global_oce_latlon", "baroclinic_gyre_dst3",
+                             "tutorial_baroclinic_gyre", "tutorial_barotropic_gyre"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--shard", action="store_true",
                     help="N>1: shard the workload's tiles over the N processes (RCCL, strong scaling, "
@@ -48,6 +49,14 @@ def parse():
 
 
 WORKLOADS = {
+    "global_oce_latlon_90x40x15": "90x40x15 global lat-lon ocean (BASELINE config 2's grid, bathymetry, "
+                                  "monthly forcing and 1-tile layout sNx=90, sNy=40, OL=3) with the physics "
+                                  "verification/tutorial_global_oce_latlon pins: JMD95Z, GM/Redi gkw91, CD scheme, "
+                                  "SST/SSS relaxation, Qnet, real fresh-water flux, IVDC, implicit diffusion, "
+                                  "linear free surface (config 2 adds r*, JMD95P, biharmonic viscosity: not yet); "
+                                  "full FORWARD_STEP on device, 1 step = 1 model day",
+    "tutorial_global_oce_latlon": "tutorial_global_oce_latlon 90x40x15 as verified (2 tiles of 45x40, OL=2), "
+                                  "full FORWARD_STEP on device, 1 step = 1 model day",
     "baroclinic_gyre_dst3": "BASELINE config 4: tutorial_baroclinic_gyre 62x62x15 (4 tiles of 31x31, "
                             "spherical-polar) with tempAdvScheme=33 (multi-dim DST3 flux-limited), full FORWARD_STEP "
                             "on device (dt=1200 s)",
@@ -57,11 +66,25 @@ WORKLOADS = {
 }
 
 
+DATA = {
+    "global_oce_latlon_90x40x15": "reference input fields of verification/tutorial_global_oce_latlon (bathymetry, "
+                                  "lev_t/lev_s record 1, 12-month taux/tauy/Qnet/EmPmR/SST/SSS), cold start",
+    "tutorial_global_oce_latlon": "reference input fields of verification/tutorial_global_oce_latlon (bathymetry, "
+                                  "lev_t/lev_s record 1, 12-month taux/tauy/Qnet/EmPmR/SST/SSS), cold start",
+    "tutorial_barotropic_gyre": "reference input fields of verification/tutorial_barotropic_gyre (bathy, wind), "
+                                "cold start",
+}
+
+
 def config_fn(name):
     """The mitgcm_amd.configs set-up behind a --config name."""
     from mitgcm_amd import configs
     if name == "baroclinic_gyre_dst3":
         return lambda: configs.baroclinic_gyre(tempAdvScheme=33)
+    if name == "global_oce_latlon_90x40x15":
+        return lambda: configs.global_oce_latlon(nSx=1, nSy=1, OL=3)
+    if name == "tutorial_global_oce_latlon":
+        return configs.global_oce_latlon
     return {"tutorial_baroclinic_gyre": configs.baroclinic_gyre,
             "tutorial_barotropic_gyre": configs.barotropic_gyre}[name]
 
@@ -70,18 +93,23 @@ def cpu_baseline(config, seconds):
     """Oracle (CPU restatement, 1 thread) timed on the same workload: as many
     steps as fit in ~`seconds` of CPU time, reported in model-days/s."""
     from mitgcm_amd import configs
-    from oracle.harness import gyre_oracle, oracle_from_config
+    from oracle.harness import gyre_oracle, latlon_oracle, oracle_from_config
     if config == "tutorial_barotropic_gyre":
         o = gyre_oracle()
+    elif config == "global_oce_latlon_90x40x15":
+        o, _ = latlon_oracle(nSx=1, nSy=1, OL=3)
+    elif config == "tutorial_global_oce_latlon":
+        o, _ = latlon_oracle()
     else:
         o, _ = oracle_from_config(config_fn(config))
+    dt_clock = o.get("deltaTClock")
     o.forward_step()  # warm
     n, t0 = 0, time.perf_counter()
     while time.perf_counter() - t0 < seconds:
         o.forward_step()
         n += 1
     dt = time.perf_counter() - t0
-    return {"value": n * 1200.0 / 86400.0 / dt, "unit": "model-days/s", "cores": 1, "kind": "port",
+    return {"value": n * dt_clock / 86400.0 / dt, "unit": "model-days/s", "cores": 1, "kind": "port",
             "sample": "%d FORWARD_STEPs of %s on the oracle (oracle/*.c, gcc -O2, 1 thread), %.1f s"
                       % (n, config, dt)}
 
@@ -200,9 +228,8 @@ def main():
         "scaling": "strong" if shard else "weak",
         "vs_baseline": None,
         "dtype": "f64",
-        "data": "reference input fields of verification/%s (bathy, wind%s), cold start"
-                % ("tutorial_barotropic_gyre" if a.config == "tutorial_barotropic_gyre" else "tutorial_baroclinic_gyre",
-                   "" if a.config == "tutorial_barotropic_gyre" else ", SST_relax"),
+        "data": DATA.get(a.config, "reference input fields of verification/tutorial_baroclinic_gyre (bathy, wind, "
+                                   "SST_relax), cold start"),
         "config": {"workload": WORKLOADS[a.config] + ("; tiles sharded over %d processes (%s)" % (
                                                            world, "RCCL" if dist.get_backend() == "nccl" else
                                                            "gloo, host-staged") if shard
