@@ -43,7 +43,7 @@ def parse():
                     help="N>1: shard the workload's tiles over the N processes (RCCL, strong scaling, "
                          "mitgcm_amd/parallel.py) instead of running N replicas")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
-    ap.add_argument("--pmc-summary", default=os.path.join(ROOT, "profiles", "r01", "pmc_summary.json"),
+    ap.add_argument("--pmc-summary", default=os.path.join(ROOT, "profiles", "r01", "latlon", "pmc_summary.json"),
                     help="tools/pmc_summary.py output of rocprofv3 --pmc passes of this command (roofline.traffic)")
     return ap.parse_args()
 
@@ -241,8 +241,7 @@ def main():
         "kernel_ms_mean": {k: v[0] for k, v in kern.items()},
         "roofline": {"bound": "hbm", "kernel": "k_cg2d_" + m.cg2d_kernel(), "achieved": achieved, "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
-                     "traffic": pmc_traffic(a.pmc_summary, "k_cg2d_blk2" if m.cg2d_kernel() == "blk2" else
-                                            "k_cg2d_block"),
+                     "traffic": pmc_traffic(a.pmc_summary, "k_cg2d_" + m.cg2d_kernel()),
                      "traffic_unit": "bytes per launch (rocprofv3 --pmc, %s)" % os.path.relpath(a.pmc_summary, ROOT),
                      "bytes_per_launch": bytes_per_launch, "launch_ms": cg_ms, "launches": cg_n},
     }

@@ -609,6 +609,300 @@ __global__ void __launch_bounds__(CG_THREADS) k_cg2d_blk2(Dims d, Params p, Fiel
 #undef pC
 }
 
+// ---------------------------------------------------------------------------
+// k_cg2d_bxy<BX, BY, NT>: the same whole-solve CG2D with BX x BY points per thread
+// (i x j) and NT threads.  Fewer, fatter threads: the per-wave reduction cost
+// (DPP row sums, row broadcasts, the LDS partials and the barrier) is paid by
+// NT/64 waves instead of 16, more neighbours come from registers, and every
+// operator coefficient of the block (aW/pW of the BX+1 W-E faces of each row,
+// aS/pS of the BY+1 S-N faces of each column, aC, pC) stays in VGPRs
+// (NT = 512: 2 waves per SIMD, 256 VGPRs each).  Blocks are formed on the global
+// lat-lon index space as for k_cg2d_blk2; r and s live in LDS point-major
+// (slot = p*NT + block, p = b*BX + a), conflict-free for the thread-contiguous
+// gathers and scatters.  nbx[NB/2 per block] packs the
+// 2(BX+BY) out-of-block neighbour slots as 16-bit pairs in the order
+// W[0..BY-1], E[0..BY-1], S[0..BX-1], N[0..BX-1]; blkx[BX*BY per block] = the
+// 2-D offsets of P[b][a] (row b = j, column a = i).
+template <int NW>
+__device__ __forceinline__ double block_sum_nw(double v, double *red, int slot) {
+  v = wave_sum(v);
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  if (lane == 0) red[slot * 16 + wv] = v;
+  __syncthreads();
+  const int l = lane & 15;
+  return row_sum16(l < NW ? red[slot * 16 + l] : 0.0);
+}
+// two sums in one reduction (independent DPP chains interleave); each value is
+// reduced with exactly the operations block_sum_nw applies, so the results are the same
+template <int NW>
+__device__ __forceinline__ void block_sum2_nw(double &v0, double &v1, double *red, int slot) {
+  v0 = row_sum16(v0);
+  v1 = row_sum16(v1);
+  v0 = v0 + dpp_bcast_f64<0x142, 0xA>(v0);
+  v1 = v1 + dpp_bcast_f64<0x142, 0xA>(v1);
+  v0 = v0 + dpp_bcast_f64<0x143, 0xC>(v0);
+  v1 = v1 + dpp_bcast_f64<0x143, 0xC>(v1);
+  v0 = lane_f64(v0, 63);
+  v1 = lane_f64(v1, 63);
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  if (lane == 0) { red[slot * 16 + wv] = v0; red[(slot ^ 1) * 16 + wv] = v1; }
+  __syncthreads();
+  const int l = lane & 15;
+  v0 = row_sum16(l < NW ? red[slot * 16 + l] : 0.0);
+  v1 = row_sum16(l < NW ? red[(slot ^ 1) * 16 + l] : 0.0);
+}
+__device__ __forceinline__ double wave_max_u(double v) {
+  v = row_max16(v);
+  return fmax(fmax(lane_f64(v, 0), lane_f64(v, 16)), fmax(lane_f64(v, 32), lane_f64(v, 48)));
+}
+template <int NW>
+__device__ __forceinline__ double block_max_nw(double v, double *red, int slot) {
+  v = wave_max_u(v);
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  if (lane == 0) red[slot * 16 + wv] = v;
+  __syncthreads();
+  const int l = lane & 15;
+  return row_max16(l < NW ? red[slot * 16 + l] : 0.0);
+}
+
+template <int BX, int BY, int NT, bool MINRES>
+__global__ void __launch_bounds__(NT) k_cg2d_bxy(Dims d, Params p, Fields f, const unsigned *__restrict__ nbx,
+                                                 const int *__restrict__ blkx, int nBlk, int maxIters, int nIterMinIn,
+                                                 SolveRecord *rec, int *stepCounter) {
+#pragma clang fp contract(fast)
+  constexpr int NPT = BX * BY, NP = NPT * NT, NB = 2 * (BX + BY), NW = NT / 64;
+  extern __shared__ __attribute__((aligned(16))) double lds[];
+  double *r_l = lds;               // NP + 1 (last = ZERO slot)
+  double *s_l = lds + (NP + 1);
+  double *red = lds + 2 * (NP + 1);  // 4 x 16 partial slots
+  const int tid = threadIdx.x;
+  const bool act = tid < nBlk;
+  const int bt = act ? tid : 0;
+  const double az = act ? 1.0 : 0.0;
+  long G[BY][BX];
+  int cs[BY][BX];
+#pragma unroll
+  for (int b = 0; b < BY; b++)
+#pragma unroll
+    for (int a = 0; a < BX; a++) {
+      G[b][a] = blkx[NPT * bt + BX * b + a];
+      cs[b][a] = act ? (BX * b + a) * NT + tid : NP;   // point-major LDS slots (see build_nbr)
+    }
+  unsigned nbp[NB / 2];
+#pragma unroll
+  for (int q = 0; q < NB / 2; q++) nbp[q] = nbx[(NB / 2) * bt + q];
+  auto nbi = [&](int q) -> int { return (q & 1) ? (int)(nbp[q >> 1] >> 16) : (int)(nbp[q >> 1] & 0xFFFFu); };
+  // coefficients: W-E faces of row b (a = 0..BX: west face of P[b][a], a = BX: east face of
+  // P[b][BX-1], its i+1 entry), S-N faces of column a (b = 0..BY)
+  double aW[BY][BX + 1], pW[BY][BX + 1], aS[BX][BY + 1], pS[BX][BY + 1], aC[BY][BX], pC[BY][BX];
+  const long nx = d.nx;
+#pragma unroll
+  for (int b = 0; b < BY; b++)
+#pragma unroll
+    for (int a = 0; a <= BX; a++) {
+      const long g = a < BX ? G[b][a] : G[b][BX - 1] + 1;
+      aW[b][a] = az * f.aW2d[g];
+      pW[b][a] = az * f.pW[g];
+    }
+#pragma unroll
+  for (int a = 0; a < BX; a++)
+#pragma unroll
+    for (int b = 0; b <= BY; b++) {
+      const long g = b < BY ? G[b][a] : G[BY - 1][a] + nx;
+      aS[a][b] = az * f.aS2d[g];
+      pS[a][b] = az * f.pS[g];
+    }
+#pragma unroll
+  for (int b = 0; b < BY; b++)
+#pragma unroll
+    for (int a = 0; a < BX; a++) {
+      aC[b][a] = az * f.aC2d[G[b][a]];
+      pC[b][a] = az * f.pC[G[b][a]];
+    }
+  double x[BY][BX], r[BY][BX], sv[BY][BX], bb[BY][BX];
+#pragma unroll
+  for (int b = 0; b < BY; b++)
+#pragma unroll
+    for (int a = 0; a < BX; a++) {
+      bb[b][a] = act ? f.cg2d_b[G[b][a]] : 0.0;
+      x[b][a] = act ? f.cg2d_x[G[b][a]] : 0.0;
+      sv[b][a] = 0.0;
+    }
+  // operator application: out-of-block neighbours from LDS, in-block from registers
+  // (cg2d.F order: A = aW*vW + aW(i+1)*vE + aS*vS + aS(j+1)*vN + aC*v; M = pC*v + pW*vW + ...)
+  auto apply = [&](const double *arr, const double (&v)[BY][BX], double (&out)[BY][BX], bool isM) {
+    double vW[BY], vE[BY], vS[BX], vN[BX];
+#pragma unroll
+    for (int b = 0; b < BY; b++) { vW[b] = arr[nbi(b)]; vE[b] = arr[nbi(BY + b)]; }
+#pragma unroll
+    for (int a = 0; a < BX; a++) { vS[a] = arr[nbi(2 * BY + a)]; vN[a] = arr[nbi(2 * BY + BX + a)]; }
+#pragma unroll
+    for (int b = 0; b < BY; b++)
+#pragma unroll
+      for (int a = 0; a < BX; a++) {
+        const double w = a > 0 ? v[b][a - 1] : vW[b];
+        const double e = a < BX - 1 ? v[b][a + 1] : vE[b];
+        const double so = b > 0 ? v[b - 1][a] : vS[a];
+        const double no = b < BY - 1 ? v[b + 1][a] : vN[a];
+        if (isM)
+          out[b][a] = pC[b][a] * v[b][a] + pW[b][a] * w + pW[b][a + 1] * e + pS[a][b] * so + pS[a][b + 1] * no;
+        else
+          out[b][a] = aW[b][a] * w + aW[b][a + 1] * e + aS[a][b] * so + aS[a][b + 1] * no + aC[b][a] * v[b][a];
+      }
+  };
+  // cg2d.F:104-133: normalise the RHS
+  double rhsMax = 0.0;
+#pragma unroll
+  for (int b = 0; b < BY; b++)
+#pragma unroll
+    for (int a = 0; a < BX; a++) { bb[b][a] = bb[b][a] * p.cg2dNorm; rhsMax = fmax(fabs(bb[b][a]), rhsMax); }
+  rhsMax = block_max_nw<NW>(rhsMax, red, 0);
+  double rhsNorm = 1.0;
+  if (p.cg2dNormaliseRHS) {
+    if (rhsMax != 0.0) rhsNorm = 1.0 / rhsMax;
+#pragma unroll
+    for (int b = 0; b < BY; b++)
+#pragma unroll
+      for (int a = 0; a < BX; a++) { bb[b][a] = bb[b][a] * rhsNorm; x[b][a] = x[b][a] * rhsNorm; }
+  }
+#pragma unroll
+  for (int b = 0; b < BY; b++)
+#pragma unroll
+    for (int a = 0; a < BX; a++) s_l[cs[b][a]] = x[b][a];
+  if (tid == 0) { s_l[NP] = 0.0; r_l[NP] = 0.0; }
+  __syncthreads();
+  double err = 0.0, sumB = 0.0;
+  {
+    double ax[BY][BX];
+    apply(s_l, x, ax, false);
+#pragma unroll
+    for (int b = 0; b < BY; b++)
+#pragma unroll
+      for (int a = 0; a < BX; a++) {
+        r[b][a] = bb[b][a] - ax[b][a];
+        err = err + r[b][a] * r[b][a];
+        sumB = sumB + bb[b][a];
+      }
+  }
+  double xmin[BY][BX];
+  if (MINRES) {
+#pragma unroll
+    for (int b = 0; b < BY; b++)
+#pragma unroll
+      for (int a = 0; a < BX; a++) xmin[b][a] = x[b][a];
+  }
+  if (act) {
+#pragma unroll
+    for (int b = 0; b < BY; b++)
+#pragma unroll
+      for (int a = 0; a < BX; a++) f.cg2d_b[G[b][a]] = bb[b][a];
+  }
+  double err_sq = block_sum_nw<NW>(err, red, 1);
+  const double sumRHS = block_sum_nw<NW>(sumB, red, 2);
+#pragma unroll
+  for (int b = 0; b < BY; b++)
+#pragma unroll
+    for (int a = 0; a < BX; a++) { r_l[cs[b][a]] = r[b][a]; s_l[cs[b][a]] = 0.0; }
+  if (tid == 0) { r_l[NP] = 0.0; s_l[NP] = 0.0; }
+  const double firstResidual = sqrt(err_sq);
+  int nIterMin = nIterMinIn;
+  double minResidualSq = -1.0;
+  if (MINRES && nIterMin >= 0) { nIterMin = 0; minResidualSq = err_sq; }
+  int actualIts = 0;
+  double eta_qrNM1 = 1.0;
+  __syncthreads();
+  // slots: {0,1} for the paired (err_sq of iteration n, eta_qrN of n+1) sum, 2/3 alternate
+  // for alpha; the r_l writes of iteration n are fenced by an explicit barrier.  Same
+  // values and the same exit test as cg2d.F:211-352, one reduction fewer per iteration.
+  int aslot = 2;
+  if (!(err_sq < p.cg2dTolerance_sq)) {
+    double q[BY][BX];
+    apply(r_l, r, q, true);
+    double e = 0.0;
+#pragma unroll
+    for (int b = 0; b < BY; b++)
+#pragma unroll
+      for (int a = 0; a < BX; a++) e = e + q[b][a] * r[b][a];
+    double eta_qrN = block_sum_nw<NW>(e, red, 0);
+    for (int it2d = 1; it2d <= maxIters; it2d++) {
+      const double cgBeta = eta_qrN / eta_qrNM1;
+      eta_qrNM1 = eta_qrN;
+#pragma unroll
+      for (int b = 0; b < BY; b++)
+#pragma unroll
+        for (int a = 0; a < BX; a++) { sv[b][a] = q[b][a] + cgBeta * sv[b][a]; s_l[cs[b][a]] = sv[b][a]; }
+      __syncthreads();
+      apply(s_l, sv, q, false);
+      double aa = 0.0;
+#pragma unroll
+      for (int b = 0; b < BY; b++)
+#pragma unroll
+        for (int a = 0; a < BX; a++) aa = aa + sv[b][a] * q[b][a];
+      aslot = aslot ^ 1;
+      double alpha = block_sum_nw<NW>(aa, red, aslot);
+      alpha = eta_qrN / alpha;
+      double e2 = 0.0;
+#pragma unroll
+      for (int b = 0; b < BY; b++)
+#pragma unroll
+        for (int a = 0; a < BX; a++) {
+          x[b][a] = x[b][a] + alpha * sv[b][a];
+          r[b][a] = r[b][a] - alpha * q[b][a];
+          e2 = e2 + r[b][a] * r[b][a];
+          r_l[cs[b][a]] = r[b][a];
+        }
+      actualIts = it2d;
+      __syncthreads();
+      // next iteration's q = M r and (q, r), reduced together with this iteration's r.r
+      apply(r_l, r, q, true);
+      double en = 0.0;
+#pragma unroll
+      for (int b = 0; b < BY; b++)
+#pragma unroll
+        for (int a = 0; a < BX; a++) en = en + q[b][a] * r[b][a];
+      block_sum2_nw<NW>(e2, en, red, 0);
+      err_sq = e2;
+      eta_qrN = en;
+      if (err_sq < p.cg2dTolerance_sq) break;
+      if (MINRES && err_sq < minResidualSq) {
+        minResidualSq = err_sq;
+        nIterMin = it2d;
+#pragma unroll
+        for (int b = 0; b < BY; b++)
+#pragma unroll
+          for (int a = 0; a < BX; a++) xmin[b][a] = x[b][a];
+      }
+    }
+  }
+  if (MINRES && nIterMin >= 0 && err_sq > minResidualSq) {
+#pragma unroll
+    for (int b = 0; b < BY; b++)
+#pragma unroll
+      for (int a = 0; a < BX; a++) x[b][a] = xmin[b][a];
+  }
+  if (act) {
+#pragma unroll
+    for (int b = 0; b < BY; b++)
+#pragma unroll
+      for (int a = 0; a < BX; a++) {
+        double xv = x[b][a];
+        if (p.cg2dNormaliseRHS) xv = xv / rhsNorm;
+        f.cg2d_x[G[b][a]] = xv;
+      }
+  }
+  if (tid == 0) {
+    const int st = stepCounter ? *stepCounter : 0;
+    SolveRecord &R = rec[st];
+    R.firstResidual = firstResidual;
+    R.lastResidual = sqrt(err_sq);
+    R.minResidualSq = minResidualSq;
+    R.rhsMax = rhsMax;
+    R.sumRHS = sumRHS;
+    R.numIters = actualIts;
+    R.nIterMin = nIterMin;
+  }
+}
+
 // Halo exchange of `nz` levels through a precomputed map (EXCH1 / EXCH2 scalar).
 // map[2*h] = destination 2-D flat offset (t*n2+local), map[2*h+1] = source.
 __global__ void __launch_bounds__(256) k_exchange(Dims d, double *a, const long *__restrict__ map, int nHalo, int nz) {
@@ -878,6 +1172,25 @@ hipError_t launch_cg2d_block(const Dims &d, const Params &p, const Fields &f, co
     default: LAUNCH(8); break;
   }
 #undef LAUNCH
+  return hipGetLastError();
+}
+
+// 2 (i) x 4 (j) points per thread, 512 threads: up to 4096 points (90x40: 450 blocks)
+constexpr int CGX_BX = 2, CGX_BY = 4, CGX_NT = 512;
+int cg2d_bxy_geometry(int *bx, int *by, int *nt) { *bx = CGX_BX; *by = CGX_BY; *nt = CGX_NT; return 0; }
+hipError_t launch_cg2d_bxy(const Dims &d, const Params &p, const Fields &f, const unsigned *nbx, const int *blkx,
+                           int nBlk, int maxIters, int nIterMin, SolveRecord *rec, int *stepCounter, hipStream_t s) {
+  if (nBlk > CGX_NT) return hipErrorInvalidValue;
+  const size_t lds = (2 * ((size_t)CGX_BX * CGX_BY * CGX_NT + 1) + 4 * 16) * sizeof(double);
+  auto kern = nIterMin >= 0 ? k_cg2d_bxy<CGX_BX, CGX_BY, CGX_NT, true> : k_cg2d_bxy<CGX_BX, CGX_BY, CGX_NT, false>;
+  static bool attrSet[2] = {false, false};
+  if (!attrSet[nIterMin >= 0]) {
+    hipError_t e = hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (e != hipSuccess) return e;
+    attrSet[nIterMin >= 0] = true;
+  }
+  hipLaunchKernelGGL(kern, dim3(1), dim3(CGX_NT), lds, s, d, p, f, nbx, blkx, nBlk, maxIters, nIterMin, rec,
+                     stepCounter);
   return hipGetLastError();
 }
 

@@ -25,6 +25,9 @@ hipError_t launch_sfp_rhs(const Dims &, const Params &, const Fields &, hipStrea
 hipError_t launch_cg2d_block(const Dims &, const Params &, const Fields &, const unsigned *, const int *, int, int, int,
                              SolveRecord *, int *, hipStream_t);
 int cg2d_block_ppt(int nPts);
+hipError_t launch_cg2d_bxy(const Dims &, const Params &, const Fields &, const unsigned *, const int *, int, int, int,
+                           SolveRecord *, int *, hipStream_t);
+int cg2d_bxy_geometry(int *, int *, int *);
 hipError_t launch_cg2d_blk2(const Dims &, const Params &, const Fields &, const unsigned *, const int *, int, int, int,
                             SolveRecord *, int *, hipStream_t);
 int cg2d_block_max_points();
@@ -147,6 +150,10 @@ struct mgcm_model {
   unsigned *d_nb4 = nullptr;
   int *d_blk = nullptr;
   int nBlk = 0;
+  // BX x BY-blocked solver tables (k_cg2d_bxy; preferred when the global grid tiles into them)
+  unsigned *d_nbx = nullptr;
+  int *d_blkx = nullptr;
+  int nBlkX = 0;
   bool latlonTopology = true;   // false once a custom halo map (e.g. EXCH2 cube) is installed
   // hipGraphs of two FORWARD_STEPs, one per theta/salt ping-pong parity
   bool useGraph = true;
@@ -358,6 +365,73 @@ static int build_nbr(mgcm_model *m) {
     HIPCHK(hipMemcpy(m->d_blk, blk.data(), blk.size() * sizeof(int), hipMemcpyHostToDevice));
     m->nBlk = nBk;
   }
+  // BX x BY blocks (k_cg2d_bxy), same global-index construction
+  m->nBlkX = 0;
+  int BX, BY, NT;
+  cg2d_bxy_geometry(&BX, &BY, &NT);
+  const int nBx = (Nx % BX == 0 && Ny % BY == 0) ? (Nx / BX) * (Ny / BY) : 0;
+  if (m->latlonTopology && nBx > 0 && nBx <= NT && !getenv("MGCM_CG2D_NOBXY")) {
+    const int NPT = BX * BY, NB = 2 * (BX + BY);
+    const unsigned Z = (unsigned)(NPT * NT);
+    // LDS slot of an interior point: point-in-block major, block minor (p*NT + block),
+    // so that consecutive threads touch consecutive doubles (no LDS bank conflicts)
+    std::vector<unsigned> slotOf((size_t)m->nPts, Z);
+    {
+      int qb = 0;
+      for (int J0 = 1; J0 <= Ny; J0 += BY)
+        for (int I0 = 1; I0 <= Nx; I0 += BX, qb++)
+          for (int b = 0; b < BY; b++)
+            for (int a = 0; a < BX; a++) {
+              const int I = I0 + a, J = J0 + b, bi = (I - 1) / d.sNx, bj = (J - 1) / d.sNy;
+              const int t = bj * d.nSx + bi, i = (I - 1) % d.sNx + 1, j = (J - 1) % d.sNy + 1;
+              slotOf[(size_t)t * d.sNx * d.sNy + (size_t)(j - 1) * d.sNx + (i - 1)] = (unsigned)((b * BX + a) * NT + qb);
+            }
+    }
+    auto cmp = [&](long g) -> unsigned {
+      unsigned c = compact(g);
+      return c == ZERO ? Z : slotOf[c];
+    };
+    auto nbv = [&](int i, int j, int t) -> unsigned {
+      long g = MG_I2(d, i, j, t);
+      if (i < 1 || i > d.sNx || j < 1 || j > d.sNy) g = srcOf[g];
+      return cmp(g);
+    };
+    auto gpt = [&](int I, int J, int &i, int &j, int &t) {
+      const int bi = (I - 1) / d.sNx, bj = (J - 1) / d.sNy;
+      t = bj * d.nSx + bi; i = (I - 1) % d.sNx + 1; j = (J - 1) % d.sNy + 1;
+    };
+    std::vector<unsigned> nbx((size_t)(NB / 2) * NT, Z | (Z << 16));
+    std::vector<int> blkx((size_t)NPT * NT, (int)MG_I2(d, 1, 1, 0));
+    int q = 0;
+    for (int J0 = 1; J0 <= Ny; J0 += BY)
+      for (int I0 = 1; I0 <= Nx; I0 += BX, q++) {
+        std::vector<int> ii(NPT), jj(NPT), tt(NPT);
+        for (int b = 0; b < BY; b++)
+          for (int a = 0; a < BX; a++) {
+            gpt(I0 + a, J0 + b, ii[b * BX + a], jj[b * BX + a], tt[b * BX + a]);
+            blkx[(size_t)NPT * q + b * BX + a] = (int)MG_I2(d, ii[b * BX + a], jj[b * BX + a], tt[b * BX + a]);
+          }
+        std::vector<unsigned> v(NB);
+        for (int b = 0; b < BY; b++) {
+          const int w = b * BX, e = b * BX + BX - 1;
+          v[b] = nbv(ii[w] - 1, jj[w], tt[w]);
+          v[BY + b] = nbv(ii[e] + 1, jj[e], tt[e]);
+        }
+        for (int a = 0; a < BX; a++) {
+          const int so = a, no = (BY - 1) * BX + a;
+          v[2 * BY + a] = nbv(ii[so], jj[so] - 1, tt[so]);
+          v[2 * BY + BX + a] = nbv(ii[no], jj[no] + 1, tt[no]);
+        }
+        for (int k = 0; k < NB / 2; k++) nbx[(size_t)(NB / 2) * q + k] = v[2 * k] | (v[2 * k + 1] << 16);
+      }
+    if (m->d_nbx) (void)hipFree(m->d_nbx);
+    if (m->d_blkx) (void)hipFree(m->d_blkx);
+    HIPCHK(hipMalloc(&m->d_nbx, nbx.size() * sizeof(unsigned)));
+    HIPCHK(hipMemcpy(m->d_nbx, nbx.data(), nbx.size() * sizeof(unsigned), hipMemcpyHostToDevice));
+    HIPCHK(hipMalloc(&m->d_blkx, blkx.size() * sizeof(int)));
+    HIPCHK(hipMemcpy(m->d_blkx, blkx.data(), blkx.size() * sizeof(int), hipMemcpyHostToDevice));
+    m->nBlkX = nBx;
+  }
   return 0;
 }
 
@@ -437,6 +511,8 @@ void mgcm_destroy(mgcm_model *m) {
   if (m->d_gofs) hipFree(m->d_gofs);
   if (m->d_nb4) hipFree(m->d_nb4);
   if (m->d_blk) hipFree(m->d_blk);
+  if (m->d_nbx) hipFree(m->d_nbx);
+  if (m->d_blkx) hipFree(m->d_blkx);
   if (m->d_ctr) hipFree(m->d_ctr);
   if (m->d_rec) hipFree(m->d_rec);
   if (m->ownStream) hipStreamDestroy(m->ownStream);
@@ -480,7 +556,8 @@ double mgcm_get_param(mgcm_model *m, const char *name) {
     if (hipMemcpy(&it, m->d_ctr, sizeof(int), hipMemcpyDeviceToHost) != hipSuccess) return NAN;
     return it;
   }
-  if (!strcmp(name, "cg2dKernel")) return m->nBlk > 0 ? 2.0 : 1.0;  // 2: k_cg2d_blk2, 1: k_cg2d_block
+  // 3: k_cg2d_bxy, 2: k_cg2d_blk2, 1: k_cg2d_block
+  if (!strcmp(name, "cg2dKernel")) return m->nBlkX > 0 ? 3.0 : (m->nBlk > 0 ? 2.0 : 1.0);
   for (auto &pd : PARAMS)
     if (!strcmp(pd.name, name)) {
       const char *ptr = reinterpret_cast<const char *>(&m->p) + pd.off;
@@ -578,6 +655,9 @@ int mgcm_init(mgcm_model *m) {
 }
 
 static hipError_t launch_cg2d(mgcm_model *m, int maxIters, int nIterMin) {
+  if (m->nBlkX > 0)
+    return launch_cg2d_bxy(m->d, m->p, m->f, m->d_nbx, m->d_blkx, m->nBlkX, maxIters, nIterMin, m->d_rec, m->d_ctr + 1,
+                           m->stream);
   if (m->nBlk > 0)
     return launch_cg2d_blk2(m->d, m->p, m->f, m->d_nb4, m->d_blk, m->nBlk, maxIters, nIterMin, m->d_rec, m->d_ctr + 1,
                             m->stream);

@@ -141,8 +141,9 @@ class Model:
         return x, f.value, mn.value, la.value, it.value, itm.value
 
     def cg2d_kernel(self):
-        """Which CG2D kernel mgcm_init selected: 'blk2' (2x2-blocked) or 'block'."""
-        return "blk2" if lib().mgcm_get_param(self.h, b"cg2dKernel") == 2.0 else "block"
+        """Which CG2D kernel mgcm_init selected: 'bxy' (2x4 points/thread), 'blk2' (2x2) or 'block'."""
+        k = lib().mgcm_get_param(self.h, b"cg2dKernel")
+        return {3.0: "bxy", 2.0: "blk2"}.get(k, "block")
 
     def kernel_timing(self, enable):
         lib().mgcm_kernel_timing(self.h, 1 if enable else 0)

@@ -100,3 +100,25 @@ def test_latlon_20_steps_vs_reference_output(golden_dir):
           % (worst["check"] + worst["other"]))
     assert worst["check"][0] >= 11.0 and worst["other"][0] >= 10.0, worst
     m.close()
+
+
+def test_cg2d_bxy_vs_oracle():
+    """The 2x4-points-per-thread solver (k_cg2d_bxy, chosen for the 90x40 grid) on the
+    lat-lon operator: same iteration count, first residual within 1e-12 relative,
+    solution within 1e-12 of max|x|."""
+    from mitgcm_amd import configs
+    o, g = _stepped_oracle(0)
+    m = configs.make_model(configs.global_oce_latlon)
+    assert m.cg2d_kernel() == "bxy"
+    rng = np.random.default_rng(11)
+    b = np.zeros((g.nTiles, g.ny, g.nx))
+    inner = g.sl(1, g.sNx, 1, g.sNy)
+    for t in range(g.nTiles):
+        b[t][inner] = rng.standard_normal((g.sNy, g.sNx)) * g.f["maskInC"][t][inner]
+    x0 = np.zeros_like(b)
+    xo, fo, mo, lo, ito, imo = o.cg2d(b, x0, 500, -1)
+    xd, fd, md, ld, itd, imd = m.cg2d(b, x0, 500, -1)
+    assert itd == ito and abs(fd - fo) <= 1e-12 * abs(fo), (itd, ito, fd, fo)
+    sc = max(np.abs(xo[t][inner]).max() for t in range(g.nTiles))
+    assert max(np.abs(xd[t][inner] - xo[t][inner]).max() for t in range(g.nTiles)) <= 1e-12 * sc
+    m.close()
