@@ -106,6 +106,26 @@ __device__ __forceinline__ int mg_xcd_block() {
     j = (j0) + q_ / (ni);                                                               \
   }
 #define MG_PLANE_THREADS 256
+
+// Column blocks for the vertical recurrences (implicit solves, column sums, scans):
+// a 256-thread workgroup holds NC = 256/KP columns x KP >= Nr levels, thread
+// (c, kk) = threadIdx.x = kk*NC + c, so the k-parallel loads/stores of a level are
+// NC consecutive i (coalesced) and the serial part of a column runs out of LDS.
+// Threads past the last column stay resident (valid = false) for the barriers.
+__host__ __device__ inline int mg_col_kp(int Nr) { int kp = 1; while (kp < Nr) kp <<= 1; return kp; }
+#define MG_COLS(i0, ni, j0, nj, Nr)                                                    \
+  const int KP_ = mg_col_kp(Nr), NC_ = 256 / KP_;                                        \
+  const int cc = (int)threadIdx.x % NC_, kk = (int)threadIdx.x / NC_;                   \
+  const long col_ = (long)mg_xcd_block() * NC_ + cc;                                    \
+  const long npl_ = (long)(ni) * (nj);                                                  \
+  const bool valid = col_ < npl_ * d.nT;                                                \
+  const int t = d.t0 + (int)(valid ? col_ / npl_ : 0);                                  \
+  const int i = (i0) + (int)((valid ? col_ % npl_ : 0) % (ni));                         \
+  const int j = (j0) + (int)((valid ? col_ % npl_ : 0) / (ni));
+inline unsigned mg_col_blocks(int ni, int nj, int nT, int Nr) {
+  const int nc = 256 / mg_col_kp(Nr);
+  return (unsigned)(((long)ni * nj * nT + nc - 1) / nc);
+}
 inline unsigned mg_plane_blocks(int ni, int nj, int nz) {
   return (unsigned)(((ni) * (nj) + MG_PLANE_THREADS - 1) / MG_PLANE_THREADS * (nz));
 }

@@ -109,35 +109,41 @@ __device__ __forceinline__ double block_max(double v, double *red, int slot) {
 // (solve_for_pressure.F:126-128) and CD_CODE_SCHEME's uNM1, vNM1 = u, v
 // (cd_code_scheme.F:228-234) are saved here, after every k_cd_scheme read.
 __global__ void __launch_bounds__(256) k_sfp_rhs(Dims d, Params p, Fields f) {
-  MG_PLANE(1 - d.OLx, d.nx, 1 - d.OLy, d.ny, tz)
-  const int t = d.t0 + tz;
-  if (i > d.sNx + d.OLx || j > d.sNy + d.OLy) return;
+  __shared__ double sE[256], sW[256], sN[256], sS[256];
+  MG_COLS(1 - d.OLx, d.nx, 1 - d.OLy, d.ny, d.Nr)
+  const int k = kk + 1, me = kk * NC_ + cc;
+  const bool inner = i >= 1 && i <= d.sNx && j >= 1 && j <= d.sNy;
   const long q = MG_I2(d, i, j, t);
-  if (p.useCDscheme) {
-    f.etaNm1[q] = f.etaN[q];
-    for (int k = 1; k <= d.Nr; k++) {
+  if (valid && k <= d.Nr) {
+    if (p.useCDscheme) {
       const long q3 = MG_I3(d, i, j, k, t);
       f.uNM1[q3] = f.uVel[q3];
       f.vNM1[q3] = f.vVel[q3];
     }
+    if (inner) {   // CALC_DIV_GHAT flux terms of level k
+      const double drF = f.drF[k - 1];
+      sE[me] = f.dyG[MG_I2(d, i + 1, j, t)] * drF * f.hFacW[MG_I3(d, i + 1, j, k, t)] *
+               f.gU[MG_I3(d, i + 1, j, k, t)] / p.deltaTMom;
+      sW[me] = f.dyG[q] * drF * f.hFacW[MG_I3(d, i, j, k, t)] * f.gU[MG_I3(d, i, j, k, t)] / p.deltaTMom;
+      sN[me] = f.dxG[MG_I2(d, i, j + 1, t)] * drF * f.hFacS[MG_I3(d, i, j + 1, k, t)] *
+               f.gV[MG_I3(d, i, j + 1, k, t)] / p.deltaTMom;
+      sS[me] = f.dxG[q] * drF * f.hFacS[MG_I3(d, i, j, k, t)] * f.gV[MG_I3(d, i, j, k, t)] / p.deltaTMom;
+    }
   }
+  __syncthreads();
+  if (!valid || kk != 0) return;
+  if (p.useCDscheme) f.etaNm1[q] = f.etaN[q];
   f.cg2d_x[q] = f.Bo_surf[q] * f.etaN[q];
   double b = 0.0;
-  if (i >= 1 && i <= d.sNx && j >= 1 && j <= d.sNy) {
+  if (inner) {
     if (p.useRealFreshWaterFlux) {
       const double tmpFac = p.freeSurfFac * (1.0 / p.rhoConst) * p.implicDiv2DFlow;
       b = tmpFac * f.rA[q] * f.EmPmR[q] / p.deltaTMom * f.maskInC[q];
     }
-    for (int k = d.Nr; k >= 1; k--) {
-      const double drF = f.drF[k - 1];
-      const double pfE = f.dyG[MG_I2(d, i + 1, j, t)] * drF * f.hFacW[MG_I3(d, i + 1, j, k, t)] *
-                         f.gU[MG_I3(d, i + 1, j, k, t)] / p.deltaTMom;
-      const double pfW = f.dyG[q] * drF * f.hFacW[MG_I3(d, i, j, k, t)] * f.gU[MG_I3(d, i, j, k, t)] / p.deltaTMom;
-      b = b + pfE - pfW;
-      const double pfN = f.dxG[MG_I2(d, i, j + 1, t)] * drF * f.hFacS[MG_I3(d, i, j + 1, k, t)] *
-                         f.gV[MG_I3(d, i, j + 1, k, t)] / p.deltaTMom;
-      const double pfS = f.dxG[q] * drF * f.hFacS[MG_I3(d, i, j, k, t)] * f.gV[MG_I3(d, i, j, k, t)] / p.deltaTMom;
-      b = b + pfN - pfS;
+    for (int k2 = d.Nr; k2 >= 1; k2--) {
+      const int s2 = (k2 - 1) * NC_ + cc;
+      b = b + sE[s2] - sW[s2];
+      b = b + sN[s2] - sS[s2];
     }
     // solve_for_pressure.F:214-236 (linear free surface): etaH with exactConserv, else etaN
     b = b - p.freeSurfFac * f.rA[q] / p.deltaTMom / p.deltaTFreeSurf * (p.exactConserv ? f.etaH[q] : f.etaN[q]);
@@ -1055,60 +1061,64 @@ __global__ void __launch_bounds__(256) k_exch_etaH(Dims d, Fields f, const long 
 // expressions), then exactConserv's eta (into cg2d_b, see k_exch_etaH) and
 // INTEGRATE_FOR_W.  Halo velocities are left to the end-of-step EXCH.
 __global__ void __launch_bounds__(256) k_corr_cont(Dims d, Params p, Fields f) {
-  MG_PLANE(1, d.sNx, 1, d.sNy, tz)
-  const int t = d.t0 + tz;
-  if (i > d.sNx || j > d.sNy) return;
-  const double psFac = p.pfFacMom * p.implicSurfPress;
-  auto phiX = [&](int ii, int jj) {
-    const long q = MG_I2(d, ii, jj, t);
-    return f.recip_dxC[q] * (f.Bo_surf[q] * f.etaN[q] - f.Bo_surf[MG_I2(d, ii - 1, jj, t)] * f.etaN[MG_I2(d, ii - 1, jj, t)]);
-  };
-  auto phiY = [&](int ii, int jj) {
-    const long q = MG_I2(d, ii, jj, t);
-    return f.recip_dyC[q] * (f.Bo_surf[q] * f.etaN[q] - f.Bo_surf[MG_I2(d, ii, jj - 1, t)] * f.etaN[MG_I2(d, ii, jj - 1, t)]);
-  };
-  const double pX0 = phiX(i, j), pX1 = phiX(i + 1, j), pY0 = phiY(i, j), pY1 = phiY(i, j + 1);
-  auto uCor = [&](int ii, int k, double phiSurfX) {
-    const long q3 = MG_I3(d, ii, j, k, t);
-    const double mW = f.maskW[q3];
-    return (f.gU[q3] + p.deltaTMom * (-psFac * phiSurfX * mW)) * mW;
-  };
-  auto vCor = [&](int jj, int k, double phiSurfY) {
-    const long q3 = MG_I3(d, i, jj, k, t);
-    const double mS = f.maskS[q3];
-    return (f.gV[q3] + p.deltaTMom * (-psFac * phiSurfY * mS)) * mS;
-  };
+  __shared__ double sDiv[256], sMask[256];
+  MG_COLS(1, d.sNx, 1, d.sNy, d.Nr)
+  const int k = kk + 1, me = kk * NC_ + cc;
   const long q = MG_I2(d, i, j, t);
-  auto div = [&](int k, double u0, double u1, double v0, double v1) {
+  if (valid && k <= d.Nr) {
+    const double psFac = p.pfFacMom * p.implicSurfPress;
+    auto phiX = [&](int ii, int jj) {
+      const long qq = MG_I2(d, ii, jj, t);
+      return f.recip_dxC[qq] * (f.Bo_surf[qq] * f.etaN[qq] - f.Bo_surf[MG_I2(d, ii - 1, jj, t)] * f.etaN[MG_I2(d, ii - 1, jj, t)]);
+    };
+    auto phiY = [&](int ii, int jj) {
+      const long qq = MG_I2(d, ii, jj, t);
+      return f.recip_dyC[qq] * (f.Bo_surf[qq] * f.etaN[qq] - f.Bo_surf[MG_I2(d, ii, jj - 1, t)] * f.etaN[MG_I2(d, ii, jj - 1, t)]);
+    };
+    auto uCor = [&](int ii, double phiSurfX) {
+      const long q3 = MG_I3(d, ii, j, k, t);
+      const double mW = f.maskW[q3];
+      return (f.gU[q3] + p.deltaTMom * (-psFac * phiSurfX * mW)) * mW;
+    };
+    auto vCor = [&](int jj, double phiSurfY) {
+      const long q3 = MG_I3(d, i, jj, k, t);
+      const double mS = f.maskS[q3];
+      return (f.gV[q3] + p.deltaTMom * (-psFac * phiSurfY * mS)) * mS;
+    };
+    const double u0 = uCor(i, phiX(i, j)), u1 = uCor(i + 1, phiX(i + 1, j));
+    const double v0 = vCor(j, phiY(i, j)), v1 = vCor(j + 1, phiY(i, j + 1));
+    f.uVel[MG_I3(d, i, j, k, t)] = u0;
+    f.vVel[MG_I3(d, i, j, k, t)] = v0;
     const double drF = f.drF[k - 1];
     const double uT1 = u1 * f.dyG[MG_I2(d, i + 1, j, t)] * drF * f.hFacW[MG_I3(d, i + 1, j, k, t)];
     const double uT0 = u0 * f.dyG[q] * drF * f.hFacW[MG_I3(d, i, j, k, t)];
     const double vT1 = v1 * f.dxG[MG_I2(d, i, j + 1, t)] * drF * f.hFacS[MG_I3(d, i, j + 1, k, t)];
     const double vT0 = v0 * f.dxG[q] * drF * f.hFacS[MG_I3(d, i, j, k, t)];
-    return uT1 - uT0 + vT1 - vT0;
-  };
-  if (p.exactConserv) {
-    double hDiv = 0.0;
-    for (int k = 1; k <= d.Nr; k++) {
-      const double u0 = uCor(i, k, pX0), u1 = uCor(i + 1, k, pX1), v0 = vCor(j, k, pY0), v1 = vCor(j + 1, k, pY1);
-      hDiv = hDiv + f.maskC[MG_I3(d, i, j, k, t)] * div(k, u0, u1, v0, v1);
+    sDiv[me] = uT1 - uT0 + vT1 - vT0;
+    sMask[me] = f.maskC[MG_I3(d, i, j, k, t)];
+  }
+  __syncthreads();
+  if (valid && kk == 0) {
+    if (p.exactConserv) {
+      double hDiv = 0.0;
+      for (int k2 = 1; k2 <= d.Nr; k2++) hDiv = hDiv + sMask[(k2 - 1) * NC_ + cc] * sDiv[(k2 - 1) * NC_ + cc];
+      const double facEmP = p.useRealFreshWaterFlux ? 1.0 / p.rhoConst : 0.0;   // integr_continuity.F:183-188
+      const double dEtaHdt = -(hDiv * f.recip_rA[q]) - facEmP * f.EmPmR[q];
+      f.cg2d_b[q] = f.etaH[q] + p.implicDiv2DFlow * dEtaHdt * p.deltaTFreeSurf;
     }
-    const double facEmP = p.useRealFreshWaterFlux ? 1.0 / p.rhoConst : 0.0;   // integr_continuity.F:183-188
-    const double dEtaHdt = -(hDiv * f.recip_rA[q]) - facEmP * f.EmPmR[q];
-    f.cg2d_b[q] = f.etaH[q] + p.implicDiv2DFlow * dEtaHdt * p.deltaTFreeSurf;
+    double wBelow = 0.0;
+    for (int k2 = d.Nr; k2 >= 1; k2--) {
+      const int s2 = (k2 - 1) * NC_ + cc;
+      const double conv2d = -sDiv[s2];
+      double w;
+      if (k2 == d.Nr) w = conv2d * f.recip_rA[q] * sMask[s2];
+      else w = (wBelow + conv2d * f.recip_rA[q]) * sMask[s2];
+      sDiv[s2] = w;
+      wBelow = w;
+    }
   }
-  double wBelow = 0.0;
-  for (int k = d.Nr; k >= 1; k--) {
-    const double u0 = uCor(i, k, pX0), u1 = uCor(i + 1, k, pX1), v0 = vCor(j, k, pY0), v1 = vCor(j + 1, k, pY1);
-    f.uVel[MG_I3(d, i, j, k, t)] = u0;
-    f.vVel[MG_I3(d, i, j, k, t)] = v0;
-    const double conv2d = -div(k, u0, u1, v0, v1);
-    double w;
-    if (k == d.Nr) w = conv2d * f.recip_rA[q] * f.maskC[MG_I3(d, i, j, k, t)];
-    else w = (wBelow + conv2d * f.recip_rA[q]) * f.maskC[MG_I3(d, i, j, k, t)];
-    f.wVel[MG_I3(d, i, j, k, t)] = w;
-    wBelow = w;
-  }
+  __syncthreads();
+  if (valid && k <= d.Nr) f.wVel[MG_I3(d, i, j, k, t)] = sDiv[me];
 }
 
 // Tile-sharded runs: gather (pack) / scatter (unpack) the halo-source points a peer
@@ -1132,7 +1142,7 @@ __global__ void k_bump_counter(int *c, int nIncr) {
 
 // ------------------------------------------------------------------ launchers
 hipError_t launch_sfp_rhs(const Dims &d, const Params &p, const Fields &f, hipStream_t s) {
-  const dim3 blk(MG_PLANE_THREADS), grd(mg_plane_blocks(d.nx, d.ny, d.nT));
+  const dim3 blk(256), grd(mg_col_blocks(d.nx, d.ny, d.nT, d.Nr));
   hipLaunchKernelGGL(k_sfp_rhs, grd, blk, 0, s, d, p, f);
   return hipGetLastError();
 }
@@ -1262,7 +1272,7 @@ hipError_t launch_exch_eta(const Dims &d, const Fields &f, const long *srcOf, bo
 }
 
 hipError_t launch_corr_cont(const Dims &d, const Params &p, const Fields &f, hipStream_t s) {
-  const dim3 blk(MG_PLANE_THREADS), grd(mg_plane_blocks(d.sNx, d.sNy, d.nT));
+  const dim3 blk(256), grd(mg_col_blocks(d.sNx, d.sNy, d.nT, d.Nr));
   hipLaunchKernelGGL(k_corr_cont, grd, blk, 0, s, d, p, f);
   return hipGetLastError();
 }

@@ -88,18 +88,23 @@ __global__ void __launch_bounds__(256) k_fields_load(Dims d, Params p, Fields f,
 // linear free surface), FIND_RHO_2D at every level (kRef = k), GRAD_SIGMA's sigmaR with
 // rho(theta(k-1), kRef = k) (grad_sigma.F:103-117) and CALC_IVDC (calc_ivdc.F:60-71).
 __global__ void __launch_bounds__(256) k_oceanic_phys(Dims d, Params p, Fields f) {
-  MG_PLANE(1 - d.OLx, d.nx, 1 - d.OLy, d.ny, tz)
-  const int t = d.t0 + tz;
-  if (i > d.sNx + d.OLx || j > d.sNy + d.OLy) return;
+  // one thread per (i,j,k), full halo range: FREEZE_SURFACE only changes theta(k=1), so
+  // every reader of theta(k=1) applies the clamp itself and the k = 1 thread stores it
+  MG_PLANE(1 - d.OLx, d.nx, 1 - d.OLy, d.ny, z)
+  const int t = d.t0 + z / d.Nr, k = z % d.Nr + 1;
   const long q = MG_I2(d, i, j, t), q31 = MG_I3(d, i, j, 1, t);
-  if (p.allowFreezing && f.theta[q31] < -1.9) f.theta[q31] = -1.9;
-  const double mass2rUnit = 1.0 / p.rhoConst, recip_Cp = 1.0 / p.HeatCapacity_Cp;
-  const double th1 = f.theta[q31], s1 = f.salt[q31];
-  double sfT = -(f.lambdaThetaClimRelax[q] * (th1 - f.SST[q]) * f.drF[0] * f.hFacC[q31]);
-  double sfS = -(f.lambdaSaltClimRelax[q] * (s1 - f.SSS[q]) * f.drF[0] * f.hFacC[q31]);
-  sfT = sfT - f.Qnet[q] * recip_Cp * mass2rUnit;
-  sfS = sfS - 0.0 * mass2rUnit;   // saltFlux = 0
-  {
+  auto theta_at = [&](int kk) {
+    const double v = f.theta[MG_I3(d, i, j, kk, t)];
+    return (kk == 1 && p.allowFreezing && v < -1.9) ? -1.9 : v;
+  };
+  if (k == 1) {
+    const double th1 = theta_at(1), s1 = f.salt[q31];
+    if (p.allowFreezing) f.theta[q31] = th1;
+    const double mass2rUnit = 1.0 / p.rhoConst, recip_Cp = 1.0 / p.HeatCapacity_Cp;
+    double sfT = -(f.lambdaThetaClimRelax[q] * (th1 - f.SST[q]) * f.drF[0] * f.hFacC[q31]);
+    double sfS = -(f.lambdaSaltClimRelax[q] * (s1 - f.SSS[q]) * f.drF[0] * f.hFacC[q31]);
+    sfT = sfT - f.Qnet[q] * recip_Cp * mass2rUnit;
+    sfS = sfS - 0.0 * mass2rUnit;   // saltFlux = 0
     const double UNSET_RL = 123456.7;
     if (p.convertFW2Salt == -1.0) {
       if (p.temp_EvPrRn != UNSET_RL) sfT = sfT + f.EmPmR[q] * (th1 - p.temp_EvPrRn) * mass2rUnit;
@@ -108,26 +113,22 @@ __global__ void __launch_bounds__(256) k_oceanic_phys(Dims d, Params p, Fields f
       if (p.temp_EvPrRn != UNSET_RL) sfT = sfT + f.EmPmR[q] * (f.tRef[0] - p.temp_EvPrRn) * mass2rUnit;
       if (p.salt_EvPrRn != UNSET_RL) sfS = sfS + f.EmPmR[q] * (p.convertFW2Salt - p.salt_EvPrRn) * mass2rUnit;
     }
+    f.surfaceForcingT[q] = sfT;
+    f.surfaceForcingS[q] = sfS;
   }
-  f.surfaceForcingT[q] = sfT;
-  f.surfaceForcingS[q] = sfS;
+  const long q3 = MG_I3(d, i, j, k, t);
+  const double rho = find_rho(p, f, k, theta_at(k), f.salt[q3]);
+  f.rhoInSitu[q3] = rho;
   const bool calcConvect = p.ivdc_kappa != 0.0;
-  double thUp = 0.0, sUp = 0.0, mUp = 0.0;
-  for (int k = 1; k <= d.Nr; k++) {
-    const long q3 = MG_I3(d, i, j, k, t);
-    const double th = f.theta[q3], sa = f.salt[q3], mC = f.maskC[q3];
-    const double rho = find_rho(p, f, k, th, sa);
-    f.rhoInSitu[q3] = rho;
-    double conv = 0.0, sigmaR = 0.0;
-    if (k >= 2 && (calcConvect || p.useGMRedi)) {
-      const double rhoKm1 = find_rho(p, f, k, thUp, sUp);
-      sigmaR = mC * mUp * f.recip_drC[k - 1] * p.rkSign * (rho - rhoKm1);
-      if (calcConvect) conv = (-sigmaR * p.gravitySign > 0.0) ? 1.0 : 0.0;
-    }
-    f.IVDConvCount[q3] = conv;
-    if (p.useGMRedi) f.sigmaR[q3] = sigmaR;
-    thUp = th; sUp = sa; mUp = mC;
+  double conv = 0.0, sigmaR = 0.0;
+  if (k >= 2 && (calcConvect || p.useGMRedi)) {
+    const long q3u = MG_I3(d, i, j, k - 1, t);
+    const double rhoKm1 = find_rho(p, f, k, theta_at(k - 1), f.salt[q3u]);
+    sigmaR = f.maskC[q3] * f.maskC[q3u] * f.recip_drC[k - 1] * p.rkSign * (rho - rhoKm1);
+    if (calcConvect) conv = (-sigmaR * p.gravitySign > 0.0) ? 1.0 : 0.0;
   }
+  f.IVDConvCount[q3] = conv;
+  if (p.useGMRedi) f.sigmaR[q3] = sigmaR;
 }
 
 // GMREDI_CALC_TENSOR (pkg/gmredi/gmredi_calc_tensor.F:231-790; skew flux, GM_ExtraDiag
@@ -421,50 +422,68 @@ __global__ void __launch_bounds__(256) k_tracer_rhs(Dims d, Params p, Fields f, 
 
 // GAD_IMPLICIT_R (implicitDiffusion) + SOLVE_TRIDIAGONAL (Thomas) + CYCLE_TRACER,
 // one thread per interior column; writes the new tracer into its other buffer.
+// GAD_IMPLICIT_R + SOLVE_TRIDIAGONAL per column (gad_implicit_r.F:96-140, the
+// Thomas sweep of solve_tridiagonal.F): the coefficients and right-hand side of
+// every level are formed k-parallel into LDS, one thread per column then sweeps
+// down and up in LDS with the reference's operations, and the levels are
+// written back k-parallel.
 __global__ void __launch_bounds__(256) k_tracer_impl(Dims d, Params p, Fields f, TracerArgs a) {
-  MG_PLANE(1, d.sNx, 1, d.sNy, tz)
-  const int t = d.t0 + tz;
-  if (i > d.sNx || j > d.sNy) return;
+  __shared__ double sSub[256], sSup[256], sY[256], sOut[256];
+  MG_COLS(1, d.sNx, 1, d.sNy, d.Nr)
   const int Nr = d.Nr;
-#define G3(a_, ii, jj, kk) f.a_[MG_I3(d, ii, jj, kk, t)]
-  double cpPrev = 0.0, ypPrev = 0.0;
-  for (int k = 1; k <= Nr; k++) {
+  const int k = kk + 1;
+  const int me = kk * NC_ + cc;
+#define G3(a_, ii, jj, kk_) f.a_[MG_I3(d, ii, jj, kk_, t)]
+  if (valid && k <= Nr) {
     const long q3 = MG_I3(d, i, j, k, t);
     const double rh = f.recip_hFacC[q3], rdrF = f.recip_drF[k - 1];
-    double sub = 0.0, sup = 0.0;
     const double mIn = f.maskInC[MG_I2(d, i, j, t)];
     // KappaRT = (IVDConvCount*ivdc_kappa + BL79(=0)) + diffKrNr [+ Kwz*maskInC] (calc_3d_diffusivity.F)
-    auto kappa = [&](int kk) {
-      double kap = (G3(IVDConvCount, i, j, kk) * p.ivdc_kappa + 0.0) + a.diffKr;
-      if (p.useGMRedi) kap = kap + G3(Kwz, i, j, kk) * mIn;
+    auto kappa = [&](int k_) {
+      double kap = (G3(IVDConvCount, i, j, k_) * p.ivdc_kappa + 0.0) + a.diffKr;
+      if (p.useGMRedi) kap = kap + G3(Kwz, i, j, k_) * mIn;
       return kap;
     };
+    double sub = 0.0, sup = 0.0;
     if (k >= 2)
       sub = -(p.deltaTtracer * G3(maskC, i, j, k - 1) * rh * rdrF * kappa(k) * f.recip_drC[k - 1]);
     if (k <= Nr - 1)
       sup = -(p.deltaTtracer * G3(maskC, i, j, k + 1) * rh * rdrF * kappa(k + 1) * f.recip_drC[k]);
-    const double diag = 1.0 - (sub + sup);
-    const double y = f.gTscr[q3];
-    double cp, yp;
-    if (k == 1) {
-      if (diag != 0.0) { const double rec = 1.0 / diag; cp = sup * rec; yp = y * rec; }
-      else { cp = 0.0; yp = 0.0; }
-    } else {
-      const double tmp = diag - sub * cpPrev;
-      if (tmp != 0.0) { const double rec = 1.0 / tmp; cp = sup * rec; yp = (y - sub * ypPrev) * rec; }
-      else { cp = 0.0; yp = 0.0; }
+    sSub[me] = sub;
+    sSup[me] = sup;
+    sY[me] = f.gTscr[q3];
+  }
+  __syncthreads();
+  if (valid && kk == 0) {
+    double cpPrev = 0.0, ypPrev = 0.0;
+    for (int k2 = 1; k2 <= Nr; k2++) {
+      const int s2 = (k2 - 1) * NC_ + cc;
+      const double sub = sSub[s2], sup = sSup[s2];
+      const double diag = 1.0 - (sub + sup);
+      const double y = sY[s2];
+      double cp, yp;
+      if (k2 == 1) {
+        if (diag != 0.0) { const double rec = 1.0 / diag; cp = sup * rec; yp = y * rec; }
+        else { cp = 0.0; yp = 0.0; }
+      } else {
+        const double tmp = diag - sub * cpPrev;
+        if (tmp != 0.0) { const double rec = 1.0 / tmp; cp = sup * rec; yp = (y - sub * ypPrev) * rec; }
+        else { cp = 0.0; yp = 0.0; }
+      }
+      sSup[s2] = cp;   // reuse: the c' coefficients
+      sY[s2] = yp;
+      cpPrev = cp; ypPrev = yp;
     }
-    f.gTscr[q3] = yp;
-    f.cpScr[q3] = cp;
-    cpPrev = cp; ypPrev = yp;
+    double below = 0.0;
+    for (int k2 = Nr; k2 >= 1; k2--) {
+      const int s2 = (k2 - 1) * NC_ + cc;
+      const double v = (k2 == Nr) ? sY[s2] : sY[s2] - sSup[s2] * below;
+      sOut[s2] = v;
+      below = v;
+    }
   }
-  double below = 0.0;
-  for (int k = Nr; k >= 1; k--) {
-    const long q3 = MG_I3(d, i, j, k, t);
-    const double v = (k == Nr) ? f.gTscr[q3] : f.gTscr[q3] - f.cpScr[q3] * below;
-    a.trNext[q3] = v;
-    below = v;
-  }
+  __syncthreads();
+  if (valid && k <= Nr) a.trNext[MG_I3(d, i, j, k, t)] = sOut[me];
 #undef G3
 }
 
@@ -473,7 +492,8 @@ hipError_t launch_oceanic_phys(const Dims &d, const Params &p, const Fields &f, 
     const long n = d.n2 * d.nTiles;
     hipLaunchKernelGGL(k_fields_load, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, d, p, f, iterPtr);
   }
-  hipLaunchKernelGGL(k_oceanic_phys, dim3(mg_plane_blocks(d.nx, d.ny, d.nT)), dim3(MG_PLANE_THREADS), 0, s, d, p, f);
+  hipLaunchKernelGGL(k_oceanic_phys, dim3(mg_plane_blocks(d.nx, d.ny, d.nT * d.Nr)), dim3(MG_PLANE_THREADS), 0, s, d, p,
+                     f);
   if (p.useGMRedi)
     hipLaunchKernelGGL(k_gm_tensor, dim3(mg_plane_blocks(d.nx - 2, d.ny - 2, d.nT * d.Nr)), dim3(MG_PLANE_THREADS), 0,
                        s, d, p, f);
@@ -491,7 +511,7 @@ hipError_t launch_tracer_step(const Dims &d, const Params &p, const Fields &f, c
   }
   hipLaunchKernelGGL(k_tracer_rhs, grd, blk, 0, s, d, p, f, a, iterPtr);
   if (p.implicitDiffusion) {
-    const dim3 cgrd(mg_plane_blocks(d.sNx, d.sNy, d.nT));
+    const dim3 cgrd(mg_col_blocks(d.sNx, d.sNy, d.nT, d.Nr));
     hipLaunchKernelGGL(k_tracer_impl, cgrd, blk, 0, s, d, p, f, a);
   }
   return hipGetLastError();

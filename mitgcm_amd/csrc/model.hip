@@ -640,6 +640,7 @@ int mgcm_init(mgcm_model *m) {
   if (m->p.saltStepping && !okScheme(m->p.saltAdvScheme, "saltVertAdvScheme"))
     return set_err("mgcm_init: saltAdvScheme %d not implemented on the device", m->p.saltAdvScheme);
   if (m->p.eosType != 0 && m->p.eosType != 1) return set_err("mgcm_init: eosType %d not implemented", m->p.eosType);
+  if (m->d.Nr > 64) return set_err("mgcm_init: Nr = %d > 64 (column kernels hold a column in one workgroup)", m->d.Nr);
   if (m->p.periodicExternalForcing && (m->p.nForcRec < 1 || m->p.nForcRec > MG_MAXREC))
     return set_err("mgcm_init: nForcRec %d outside 1..%d", m->p.nForcRec, MG_MAXREC);
   drop_graphs(m);
