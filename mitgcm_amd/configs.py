@@ -226,3 +226,72 @@ def global_oce_latlon(nSx=2, nSy=1, OL=2, data_dir=None):
              "fu": forcing["taux"][0], "fv": forcing["tauy"][0], "Qnet": forcing["Qnet"][0],
              "EmPmR": forcing["EmPmR"][0], "SST": forcing["SST"][0], "SSS": forcing["SSS"][0]}
     return g, params, state, forcing
+
+
+PICKUP_FIELDS = ("uVel", "vVel", "theta", "salt", "guNm1", "gvNm1", "gtNm1", "gsNm1", "totPhiHyd")
+PICKUP_2D = ("etaN", "dEtaHdt", "etaH")
+PICKUP_CD = ("uVelD", "vVelD", "uNM1", "vNM1")
+
+
+def read_pickup(g, path, Nx, Ny):
+    """READ_PICKUP (model/src/read_pickup.F:170-300): the 12-field MDS pickup (fp64,
+    big-endian, global Nx x Ny records) -> tile layout with halos exchanged, as
+    READ_PICKUP's EXCH calls leave them (read_pickup.F:545-575)."""
+    Nr = g.Nr
+    raw = np.fromfile(path, dtype=">f8").astype(np.float64)
+    nrec = len(PICKUP_FIELDS) * Nr + len(PICKUP_2D)
+    if raw.size != nrec * Nx * Ny:
+        raise ValueError("%s: %d values, expected %d records of %dx%d" % (path, raw.size, nrec, Nx, Ny))
+    raw = raw.reshape(nrec, Ny, Nx)
+    out = {}
+    for n, name in enumerate(PICKUP_FIELDS):
+        out[name] = np.moveaxis(_to_tiles(g, raw[n * Nr:(n + 1) * Nr]), 0, 1).copy()
+    base = len(PICKUP_FIELDS) * Nr
+    for n, name in enumerate(PICKUP_2D):
+        out[name] = _to_tiles(g, raw[base + n])
+    return out
+
+
+def read_pickup_cd(g, path, Nx, Ny):
+    """CD_CODE_READ_PICKUP (pkg/cd_code/cd_code_read_pickup.F:53-69): uVelD, vVelD,
+    uNM1, vNM1 (Nr records each) and etaNm1 (record 4*Nr+1)."""
+    Nr = g.Nr
+    raw = np.fromfile(path, dtype=">f8").astype(np.float64).reshape(-1, Ny, Nx)
+    out = {}
+    for n, name in enumerate(PICKUP_CD):
+        out[name] = np.moveaxis(_to_tiles(g, raw[n * Nr:(n + 1) * Nr]), 0, 1).copy()
+    out["etaNm1"] = _to_tiles(g, raw[4 * Nr])
+    return out
+
+
+def global_ocean_90x40x15(nSx=1, nSy=1, OL=3, data_dir=None, pickup_dir=None):
+    """verification/global_ocean.90x40x15 (BASELINE config 2): the lat-lon grid, bathymetry
+    and monthly forcing of tutorial_global_oce_latlon (input/prepare_run links them),
+    restarted from pickup.0000036000 + pickup_cd.0000036000.  input/data differences:
+    viscA4=1e14 (biharmonic, needs OL >= 3), gravity=9.81, eosType='JMD95P'
+    (selectP_inEOS_Zc=2: pressure from totPhiHyd), ivdc_kappa=10, select_rStar=2,
+    nonlinFreeSurf=4 (r* coordinate, UPDATE_CG2D every step), hFacInf=0.2, hFacSup=2,
+    quasiHydrostatic + useNHMTerms (+ use3dCoriolis default), doResetHFactors,
+    nIter0=36000.  Returns (grid, params, state, forcing); state includes the pickups."""
+    d = data_dir or os.path.join(GOLDEN, "tutorial_global_oce_latlon")
+    pd = pickup_dir or os.path.join(GOLDEN, "global_ocean.90x40x15")
+    g, params, state, forcing = global_oce_latlon(nSx=nSx, nSy=nSy, OL=OL, data_dir=d)
+    Nx, Ny, Nr = 90, 40, 15
+    nIter0 = 36000
+    params.update(viscA4D=1e14, viscA4Z=1e14, ivdc_kappa=10.0, nIter0=nIter0, myIter=nIter0,
+                  myTime=nIter0 * 86400.0, selectP_inEOS_Zc=2, storePhiHyd4Phys=1, nonlinFreeSurf=4,
+                  select_rStar=2, hFacInf=0.2, hFacSup=2.0, quasiHydrostatic=1, useNHMTerms=1,
+                  select3dCoriScheme=1, cg2dPreCondFreq=1)
+    # set_ref_state.F:85-97 (top_Pres = 0, gravityFile = ' ')
+    rC, rF = g.f["rC"], g.f["rF"]
+    phiRef = np.zeros(2 * Nr + 1)
+    for k in range(Nr):
+        phiRef[2 * k + 1] = phiRef[0] + (rC[k] - rF[0]) * 9.81 * -1.0
+        phiRef[2 * k + 2] = phiRef[0] + (rF[k + 1] - rF[0]) * 9.81 * -1.0
+    state = {k: v for k, v in state.items() if k not in ("theta", "salt")}
+    state["phiRef"] = phiRef
+    state.update(read_pickup(g, os.path.join(pd, "pickup.%010d" % nIter0), Nx, Ny))
+    state.update(read_pickup_cd(g, os.path.join(pd, "pickup_cd.%010d" % nIter0), Nx, Ny))
+    for n in ("h0FacC", "h0FacW", "h0FacS", "recip_Rcol", "rLowW", "rLowS", "rSurfW", "rSurfS"):
+        state[n] = g.f[n]
+    return g, params, state, forcing

@@ -282,7 +282,22 @@ class Grid:
         for k in range(Nr - 1, -1, -1):
             kSurfW[hFacW[:, k] != 0.0] = k + 1
             kSurfS[hFacS[:, k] != 0.0] = k + 1
+        # ini_masks_etc.F:218-231 recip_Rcol; :325-399 rLow/rSurf at U and V points from the
+        # adjusted R_low / Ro_surf, rSurf = rLow + Sum_k drF*hFac (EXCH_UV_XY_RS afterwards)
+        col = Ro_surf - R_low
+        recip_Rcol = np.zeros_like(col)
+        recip_Rcol[col > 0.0] = 1.0 / col[col > 0.0]
+        rLowW, rLowS = self.z2(), self.z2()
+        rLowW[:, :, 1:] = np.maximum(R_low[:, :, :-1], R_low[:, :, 1:])
+        rLowS[:, 1:, :] = np.maximum(R_low[:, :-1, :], R_low[:, 1:, :])
+        tW, tS = np.zeros_like(R_low), np.zeros_like(R_low)
+        for k in range(Nr):
+            tW = tW + drF[k] * hFacW[:, k]
+            tS = tS + drF[k] * hFacS[:, k]
+        rSurfW, rSurfS = rLowW + tW, rLowS + tS
         f = self.f
+        f.update(recip_Rcol=recip_Rcol, rLowW=self.exch(rLowW), rLowS=self.exch(rLowS), rSurfW=self.exch(rSurfW),
+                 rSurfS=self.exch(rSurfS), h0FacC=hFacC.copy(), h0FacW=hFacW.copy(), h0FacS=hFacS.copy())
         f.update(R_low=R_low, Ro_surf=Ro_surf, hFacC=hFacC, hFacW=hFacW, hFacS=hFacS, maskInC=maskInC,
                  maskInW=np.where(kSurfW <= Nr, 1.0, 0.0), maskInS=np.where(kSurfS <= Nr, 1.0, 0.0))
         self.i.update(kSurfC=kSurfC, kLowC=kLowC, kSurfW=kSurfW, kSurfS=kSurfS)

@@ -15,8 +15,8 @@
 #define L(a, i, j) (a)[(long)((i) + OLx - 1) + (long)((j) + OLy - 1) * nx]
 
 static void check_supported(const OModel *m) {
-  if (m->useBiharmonicVisc || m->viscA4D != 0.0 || m->viscA4Z != 0.0) {
-    fprintf(stderr, "oracle_dynamics: biharmonic viscosity not yet restated\n"); abort();
+  if ((m->viscA4D != 0.0 || m->viscA4Z != 0.0) && m->OLx < 3) {
+    fprintf(stderr, "oracle_dynamics: biharmonic viscosity needs OLx, OLy >= 3\n"); abort();
   }
   if (m->implicitViscosity) { fprintf(stderr, "oracle_dynamics: implicitViscosity not yet restated\n"); abort(); }
   if (!m->usingCartesianGrid && !m->usingSphericalPolarGrid) {
@@ -40,7 +40,12 @@ void oracle_dynamics(OModel *m) {
   double *gUtmp = calloc(n2, 8), *gVtmp = calloc(n2, 8), *ab = calloc(n2, 8);
   double *kappaRU = calloc(n2 * (Nr + 1), 8), *kappaRV = calloc(n2 * (Nr + 1), 8);
   double *phiHydF = calloc(n2, 8), *phiHydC = calloc(n2, 8), *dPhiHydX = calloc(n2, 8), *dPhiHydY = calloc(n2, 8);
-  double *mT = calloc(n2, 8);
+  double *mT = calloc(n2, 8), *h0FacZ = calloc(n2, 8), *v4F = calloc(n2, 8), *d2Z = calloc(n2, 8), *d2M = calloc(n2, 8);
+  double *alphaRho = calloc(n2, 8), *varLoc = calloc(n2, 8);
+  double *dWtransC = calloc(n2, 8), *dWtransU = calloc(n2, 8), *dWtransV = calloc(n2, 8);
+  const int rstar = m->nonlinFreeSurf > 0 && m->select_rStar > 0;
+  const int biharm = m->viscA4D != 0.0 || m->viscA4Z != 0.0;   /* useBiharmonicVisc (set_parms.F:141) */
+  const int qh3d = m->quasiHydrostatic && (m->select3dCoriScheme >= 1 || m->useNHMTerms);
   const int metricSphere = m->usingSphericalPolarGrid && m->selectMetricTerms >= 1;
   const double recip_rSphere = m->usingSphericalPolarGrid ? 1.0 / m->rSphere : 0.0; /* ini_parms.F:1334 */
   const double recip_rhoConst = 1.0 / m->rhoConst;
@@ -70,6 +75,12 @@ void oracle_dynamics(OModel *m) {
     const double *recip_dxC = m->recip_dxC + t * n2, *recip_dyC = m->recip_dyC + t * n2;
     const double *rhoInSitu = m->rhoInSitu + t * m->n3;
     const double *sfU = m->surfaceForcingU + t * n2, *sfV = m->surfaceForcingV + t * n2;
+    const double *h0FacW = m->h0FacW + t * m->n3, *h0FacS = m->h0FacS + t * m->n3, *h0FacC = m->h0FacC + t * m->n3;
+    const double *rStarFacC = m->rStarFacC + t * n2, *rStarExpW = m->rStarExpW + t * n2, *rStarExpS = m->rStarExpS + t * n2;
+    const double *rStarDhCDt = m->rStarDhCDt + t * n2, *rStarDhWDt = m->rStarDhWDt + t * n2, *rStarDhSDt = m->rStarDhSDt + t * n2;
+    const double *etaH = m->etaH + t * n2, *recip_Rcol = m->recip_Rcol + t * n2, *Ro_surf = m->Ro_surf + t * n2;
+    const double *R_low = m->R_low + t * n2, *fCoriCos = m->fCoriCos + t * n2;
+    double *totPhiHyd = m->totPhiHyd + t * m->n3;
 #define W3(a, i, j, k) (a)[(long)((i) + OLx - 1) + (long)((j) + OLy - 1) * nx + (long)((k) - 1) * n2]
 
     /* dynamics.F:288-343: zero gU/gV and the ping-pong flux buffers */
@@ -87,23 +98,73 @@ void oracle_dynamics(OModel *m) {
       /* CALC_PHI_HYD (calc_phi_hyd.F:175-327), OCEANIC, integr_GeoPot = 2, uniformFreeSurfLev,
        * alphaRho = rhoInSitu from DO_OCEANIC_PHYS; gravFac* = 1; iMin..iMax = 0..sNx+1 */
       {
+        for (int j = jMin; j <= jMax; j++)
+          for (int i = iMin; i <= iMax; i++) L(alphaRho, i, j) = W3(rhoInSitu, i, j, k);
+        if (qh3d) {
+          /* MOM_QUASIHYDROSTATIC (pkg/mom_common/mom_quasihydrostatic.F:76-147), z-coords:
+           * scalingFactor = rhoConst*gravitySign/gravity; angleCosC = 1, angleSinC = 0 */
+          const double scalingFactor = m->rhoConst * m->gravitySign * (1.0 / m->gravity);
+          for (int j = jMin; j <= jMax; j++)
+            for (int i = iMin; i <= iMax; i++) {
+              double gW = 0.0;
+              if (m->select3dCoriScheme >= 1)
+                gW = L(fCoriCos, i, j) * (1.0 * 0.5 * (W3(uVel, i, j, k) + W3(uVel, i + 1, j, k)) -
+                                          0.0 * 0.5 * (W3(vVel, i, j, k) + W3(vVel, i, j + 1, k)));
+              if (m->useNHMTerms)
+                gW = gW + ((W3(uVel, i, j, k) * W3(uVel, i, j, k) + W3(uVel, i + 1, j, k) * W3(uVel, i + 1, j, k)) +
+                           (W3(vVel, i, j, k) * W3(vVel, i, j, k) + W3(vVel, i, j + 1, k) * W3(vVel, i, j + 1, k))) *
+                              0.5 * recip_rSphere;
+              L(alphaRho, i, j) = L(alphaRho, i, j) + scalingFactor * gW;
+            }
+        }
         double dRlocM = 0.5 * m->drC[k - 1];
         if (k == 1) dRlocM = m->rF[0] - m->rC[0];
         double dRlocP = (k == Nr) ? (m->rC[k - 1] - m->rF[k]) : 0.5 * m->drC[k];
         for (int j = jMin; j <= jMax; j++)
           for (int i = iMin; i <= iMax; i++) {
-            double a = W3(rhoInSitu, i, j, k);
+            double a = L(alphaRho, i, j);
             L(phiHydC, i, j) = L(phiHydF, i, j) + dRlocM * m->gravity * a * recip_rhoConst;
             L(phiHydF, i, j) = L(phiHydC, i, j) + dRlocP * m->gravity * a * recip_rhoConst;
           }
-        /* CALC_GRAD_PHI_HYD (calc_grad_phi_hyd.F:152-171), phi0surf = 0 */
+        /* CALC_GRAD_PHI_HYD (calc_grad_phi_hyd.F:92-171), phi0surf = 0 */
+        for (int j = jMin; j <= jMax; j++)
+          for (int i = iMin; i <= iMax; i++)
+            L(varLoc, i, j) = (rstar && m->select_rStar >= 2 && m->nonlinFreeSurf >= 4)
+                                  ? L(phiHydC, i, j) * L(rStarFacC, i, j) + 0.0
+                                  : L(phiHydC, i, j) + 0.0;
         for (long p = 0; p < n2; p++) dPhiHydX[p] = dPhiHydY[p] = 0.0;
         for (int j = jMin; j <= jMax; j++)
           for (int i = iMin + 1; i <= iMax; i++)
-            L(dPhiHydX, i, j) = L(recip_dxC, i, j) * ((L(phiHydC, i, j) + 0.0) - (L(phiHydC, i - 1, j) + 0.0));
+            L(dPhiHydX, i, j) = L(recip_dxC, i, j) * (L(varLoc, i, j) - L(varLoc, i - 1, j));
         for (int j = jMin + 1; j <= jMax; j++)
           for (int i = iMin; i <= iMax; i++)
-            L(dPhiHydY, i, j) = L(recip_dyC, i, j) * ((L(phiHydC, i, j) + 0.0) - (L(phiHydC, i, j - 1) + 0.0));
+            L(dPhiHydY, i, j) = L(recip_dyC, i, j) * (L(varLoc, i, j) - L(varLoc, i, j - 1));
+        if (rstar && m->select_rStar >= 2) {
+          /* calc_grad_phi_hyd.F:173-214: fluidIsWater, z-coords, generalForm = F */
+          const double factorP = m->gravity * recip_rhoConst * 0.5;
+          for (int j = jMin; j <= jMax; j++)
+            for (int i = iMin; i <= iMax; i++)
+              L(varLoc, i, j) = L(etaH, i, j) * (1.0 + m->rC[k - 1] * L(recip_Rcol, i, j));
+          for (int j = jMin; j <= jMax; j++)
+            for (int i = iMin + 1; i <= iMax; i++)
+              L(dPhiHydX, i, j) = L(dPhiHydX, i, j) + factorP * (L(alphaRho, i - 1, j) + L(alphaRho, i, j)) *
+                                                          (L(varLoc, i, j) - L(varLoc, i - 1, j)) * L(recip_dxC, i, j);
+          for (int j = jMin + 1; j <= jMax; j++)
+            for (int i = iMin; i <= iMax; i++)
+              L(dPhiHydY, i, j) = L(dPhiHydY, i, j) + factorP * (L(alphaRho, i, j - 1) + L(alphaRho, i, j)) *
+                                                          (L(varLoc, i, j) - L(varLoc, i, j - 1)) * L(recip_dyC, i, j);
+        }
+        /* DIAGS_PHI_HYD (diags_phi_hyd.F:60-120): totPhiHyd, phi0surf = 0 */
+        for (int j = jMin; j <= jMax; j++)
+          for (int i = iMin; i <= iMax; i++) {
+            if (rstar && m->nonlinFreeSurf >= 4) {
+              const double dPhiRef = (L(Ro_surf, i, j) - m->rC[k - 1]) * m->gravity;
+              W3(totPhiHyd, i, j, k) = L(phiHydC, i, j) * L(rStarFacC, i, j) +
+                                       fmax(dPhiRef, 0.0) * (L(rStarFacC, i, j) - 1.0) + 0.0;
+            } else {
+              W3(totPhiHyd, i, j, k) = L(phiHydC, i, j) + L(m->Bo_surf + t * n2, i, j) * L(m->etaN + t * n2, i, j) + 0.0;
+            }
+          }
       }
       for (long p = 0; p < n2; p++) {
         guDiss[p] = gvDiss[p] = 0.0; fZon[p] = fMer[p] = fVrUp[p] = fVrDw[p] = 0.0;
@@ -122,6 +183,14 @@ void oracle_dynamics(OModel *m) {
       for (int j = 1 - OLy; j <= sNy + OLy; j++)
         for (int i = 1 - OLx; i <= sNx + OLx; i++)
           L(r_hFacZ, i, j) = (L(hFacZ, i, j) == 0.0) ? 0.0 : 1.0 / L(hFacZ, i, j);
+      /* h0FacZ (mom_fluxform.F:290-307) */
+      for (long p = 0; p < n2; p++) h0FacZ[p] = hFacZ[p];
+      if (m->momViscosity && m->no_slip_sides && m->nonlinFreeSurf > 0)
+        for (int j = 2 - OLy; j <= sNy + OLy; j++)
+          for (int i = 2 - OLx; i <= sNx + OLx; i++)
+            L(h0FacZ, i, j) = fmin(fmin(W3(h0FacW, i, j, k), W3(h0FacW, i, j - 1, k)),
+                                   fmin(W3(h0FacS, i, j, k), W3(h0FacS, i - 1, j, k)));
+      for (long p = 0; p < n2; p++) v4F[p] = 0.0;
       /* xA, yA, uTrans, vTrans (mom_fluxform.F:287-327) */
       for (int j = 1 - OLy; j <= sNy + OLy; j++)
         for (int i = 1 - OLx; i <= sNx + OLx; i++) {
@@ -137,6 +206,16 @@ void oracle_dynamics(OModel *m) {
             L(rTransU, i, j) = 0.5 * (W3(wVel, i - 1, j, 1) * L(rA, i - 1, j) + W3(wVel, i, j, 1) * L(rA, i, j));
             L(rTransV, i, j) = 0.5 * (W3(wVel, i, j - 1, 1) * L(rA, i, j - 1) + W3(wVel, i, j, 1) * L(rA, i, j));
           }
+        if (rstar) {   /* mom_calc_rtrans.F:91-106 */
+          for (int j = 1 - OLy; j <= sNy + OLy; j++)
+            for (int i = 1 - OLx; i <= sNx + OLx; i++)
+              L(dWtransC, i, j) = L(rStarDhCDt, i, j) * (L(Ro_surf, i, j) - L(R_low, i, j)) * L(rA, i, j);
+          for (int j = 2 - OLy; j <= sNy + OLy; j++)
+            for (int i = 2 - OLx; i <= sNx + OLx; i++) {
+              L(dWtransU, i, j) = 0.5 * (L(dWtransC, i - 1, j) + L(dWtransC, i, j));
+              L(dWtransV, i, j) = 0.5 * (L(dWtransC, i, j - 1) + L(dWtransC, i, j));
+            }
+        }
         for (int j = 2 - OLy; j <= sNy + OLy; j++)
           for (int i = 2 - OLx; i <= sNx + OLx; i++) {
             L(fVerUkm, i, j) = L(rTransU, i, j) * W3(uVel, i, j, 1); /* mom_u_adv_wu.F:65-72 */
@@ -154,6 +233,22 @@ void oracle_dynamics(OModel *m) {
               L(rTransU, i, j) = 0.5 * (W3(wVel, i - 1, j, k + 1) * L(rA, i - 1, j) + W3(wVel, i, j, k + 1) * L(rA, i, j));
               L(rTransV, i, j) = 0.5 * (W3(wVel, i, j - 1, k + 1) * L(rA, i, j - 1) + W3(wVel, i, j, k + 1) * L(rA, i, j));
             }
+          if (rstar) {   /* mom_calc_rtrans.F:107-137, kk = k+1 <= Nr */
+            const int kk = k + 1;
+            for (int j = 1 - OLy; j <= sNy + OLy; j++)
+              for (int i = 1 - OLx; i <= sNx + OLx; i++)
+                L(dWtransC, i, j) = L(dWtransC, i, j) - L(rStarDhCDt, i, j) * m->drF[kk - 2] * W3(h0FacC, i, j, kk - 1) * L(rA, i, j);
+            for (int j = 2 - OLy; j <= sNy + OLy; j++)
+              for (int i = 2 - OLx; i <= sNx + OLx; i++) {
+                L(dWtransU, i, j) = L(dWtransU, i, j) - L(rStarDhWDt, i, j) * m->drF[kk - 2] * W3(h0FacW, i, j, kk - 1) * L(rAw, i, j);
+                L(dWtransV, i, j) = L(dWtransV, i, j) - L(rStarDhSDt, i, j) * m->drF[kk - 2] * W3(h0FacS, i, j, kk - 1) * L(rAs, i, j);
+              }
+            for (int j = 2 - OLy; j <= sNy + OLy; j++)
+              for (int i = 2 - OLx; i <= sNx + OLx; i++) {
+                L(rTransU, i, j) = L(rTransU, i, j) - L(dWtransU, i, j) + (L(dWtransC, i - 1, j) + L(dWtransC, i, j)) * 0.5;
+                L(rTransV, i, j) = L(rTransV, i, j) - L(dWtransV, i, j) + (L(dWtransC, i, j - 1) + L(dWtransC, i, j)) * 0.5;
+              }
+          }
         }
       }
       /* ================= U component ================= */
@@ -175,7 +270,7 @@ void oracle_dynamics(OModel *m) {
           for (int j = 2 - OLy; j <= sNy + OLy; j++)
             for (int i = 2 - OLx; i <= sNx + OLx; i++) {
               double f = L(rTransU, i, j) * (0.5 * (W3(uVel, i, j, kk) + W3(uVel, i, j, kk - 1)));
-              f = f + 0.25 * (W3(wVel, i, j, kk) * L(rA, i, j) * (W3(maskC, i, j, kk) - W3(maskC, i, j, kk - 1)) +
+              if (m->select_rStar == 0) f = f + 0.25 * (W3(wVel, i, j, kk) * L(rA, i, j) * (W3(maskC, i, j, kk) - W3(maskC, i, j, kk - 1)) +
                               W3(wVel, i - 1, j, kk) * L(rA, i - 1, j) * (W3(maskC, i - 1, j, kk) - W3(maskC, i - 1, j, kk - 1))) *
                           W3(uVel, i, j, kk);
               L(fVerUkp, i, j) = f;
@@ -188,22 +283,53 @@ void oracle_dynamics(OModel *m) {
                               ((L(fZon, i, j) - L(fZon, i - 1, j)) * uDudxFac +
                                (L(fMer, i, j + 1) - L(fMer, i, j)) * vDudyFac +
                                (L(fVerUkp, i, j) - L(fVerUkm, i, j)) * m->rkSign * rVelDudrFac);
+        if (rstar)   /* mom_fluxform.F:527-548 */
+          for (int j = jMin; j <= jMax; j++)
+            for (int i = iMin; i <= iMax; i++)
+              W3(gU, i, j, k) = W3(gU, i, j, k) - (L(rStarExpW, i, j) - 1.0) / m->deltaTFreeSurf * W3(uVel, i, j, k);
       } else {
         for (int j = 1 - OLy; j <= sNy + OLy; j++)
           for (int i = 1 - OLx; i <= sNx + OLx; i++) W3(gU, i, j, k) = 0.0;
       }
       if (m->momViscosity) {
-        /* MOM_U_XVISCFLUX (mom_u_xviscflux.F:51-68), del2u=0 (no biharmonic) */
+        if (biharm) {
+          /* MOM_U_DEL2U (pkg/mom_fluxform/mom_u_del2u.F:59-117), cosFac = 1, no OBCS */
+          for (int j = 2 - OLy; j <= sNy + OLy - 1; j++)
+            for (int i = 1 - OLx; i <= sNx + OLx - 1; i++)
+              L(d2Z, i, j) = m->drF[k - 1] * W3(hFacC, i, j, k) * L(dyF, i, j) * L(recip_dxF, i, j) *
+                             (W3(uVel, i + 1, j, k) - W3(uVel, i, j, k)) * 1.0;
+          for (int j = 2 - OLy; j <= sNy + OLy; j++)
+            for (int i = 2 - OLx; i <= sNx + OLx - 1; i++)
+              L(d2M, i, j) = m->drF[k - 1] * L(hFacZ, i, j) * L(dxV, i, j) * L(recip_dyU, i, j) *
+                             (W3(uVel, i, j, k) - W3(uVel, i, j - 1, k));
+          for (int j = 2 - OLy; j <= sNy + OLy - 1; j++)
+            for (int i = 2 - OLx; i <= sNx + OLx - 1; i++)
+              L(v4F, i, j) = m->recip_drF[k - 1] * W3(rhFacW, i, j, k) * L(recip_rAw, i, j) *
+                             (L(d2Z, i, j) - L(d2Z, i - 1, j) + L(d2M, i, j + 1) - L(d2M, i, j)) * W3(maskW, i, j, k);
+          if (m->no_slip_sides)
+            for (int j = 2 - OLy; j <= sNy + OLy - 1; j++)
+              for (int i = 2 - OLx; i <= sNx + OLx - 1; i++) {
+                const double hS = W3(h0FacW, i, j, k) - L(h0FacZ, i, j);
+                const double hN = W3(h0FacW, i, j, k) - L(h0FacZ, i, j + 1);
+                L(v4F, i, j) = L(v4F, i, j) - W3(rhFacW, i, j, k) * L(recip_rAw, i, j) *
+                                                  (hS * L(dxV, i, j) * L(recip_dyU, i, j) +
+                                                   hN * L(dxV, i, j + 1) * L(recip_dyU, i, j + 1)) *
+                                                  W3(uVel, i, j, k) * m->sideDragFactor * W3(maskW, i, j, k);
+              }
+        }
+        /* MOM_U_XVISCFLUX (mom_u_xviscflux.F:51-68), cosFacU = sqCosFacU = 1 */
         for (int j = 1 - OLy; j <= sNy + OLy - 1; j++)
           for (int i = 1 - OLx; i <= sNx + OLx - 1; i++)
             L(fZon, i, j) = L(dyF, i, j) * m->drF[k - 1] * W3(hFacC, i, j, k) *
-                            (-m->viscAhD * (W3(uVel, i + 1, j, k) - W3(uVel, i, j, k)) * 1.0 + m->viscA4D * 0.0 * 1.0) *
+                            (-m->viscAhD * (W3(uVel, i + 1, j, k) - W3(uVel, i, j, k)) * 1.0 +
+                             m->viscA4D * (L(v4F, i + 1, j) - L(v4F, i, j)) * 1.0) *
                             L(recip_dxF, i, j);
         /* MOM_U_YVISCFLUX (mom_u_yviscflux.F:52-73) */
         for (int j = 2 - OLy; j <= sNy + OLy; j++)
           for (int i = 1 - OLx; i <= sNx + OLx; i++)
             L(fMer, i, j) = L(dxV, i, j) * m->drF[k - 1] * L(hFacZ, i, j) *
-                            (-m->viscAhZ * (W3(uVel, i, j, k) - W3(uVel, i, j - 1, k)) + m->viscA4Z * 0.0) *
+                            (-m->viscAhZ * (W3(uVel, i, j, k) - W3(uVel, i, j - 1, k)) +
+                             m->viscA4Z * (L(v4F, i, j) - L(v4F, i, j - 1))) *
                             L(recip_dyU, i, j);
         /* MOM_U_RVISCFLUX(k) and (k+1) (mom_u_rviscflux.F) */
         for (int q = 0; q < 2; q++) {
@@ -229,11 +355,12 @@ void oracle_dynamics(OModel *m) {
           /* MOM_U_SIDEDRAG (pkg/mom_common/mom_u_sidedrag.F:100-145), variable-viscosity form */
           for (int j = 2 - OLy; j <= sNy + OLy - 1; j++)
             for (int i = 2 - OLx; i <= sNx + OLx - 1; i++) {
-              double hS = W3(hFacW, i, j, k) - L(hFacZ, i, j);
-              double hN = W3(hFacW, i, j, k) - L(hFacZ, i, j + 1);
+              /* NONLIN_FRSURF: h0FacW - h0FacZ (h0Fac = hFac for a linear free surface) */
+              double hS = W3(h0FacW, i, j, k) - L(h0FacZ, i, j);
+              double hN = W3(h0FacW, i, j, k) - L(h0FacZ, i, j + 1);
               L(vF, i, j) = -W3(rhFacW, i, j, k) * m->recip_drF[k - 1] * L(recip_rAw, i, j) *
-                            (hS * L(dxV, i, j) * L(recip_dyU, i, j) * (m->viscAhZ * W3(uVel, i, j, k) - m->viscA4Z * 0.0) +
-                             hN * L(dxV, i, j + 1) * L(recip_dyU, i, j + 1) * (m->viscAhZ * W3(uVel, i, j, k) - m->viscA4Z * 0.0)) *
+                            (hS * L(dxV, i, j) * L(recip_dyU, i, j) * (m->viscAhZ * W3(uVel, i, j, k) - m->viscA4Z * L(v4F, i, j)) +
+                             hN * L(dxV, i, j + 1) * L(recip_dyU, i, j + 1) * (m->viscAhZ * W3(uVel, i, j, k) - m->viscA4Z * L(v4F, i, j))) *
                             m->drF[k - 1] * m->sideDragFactor;
             }
           for (int j = jMin; j <= jMax; j++)
@@ -257,6 +384,17 @@ void oracle_dynamics(OModel *m) {
             for (int i = iMin; i <= iMax; i++)
               L(guDiss, i, j) = L(guDiss, i, j) - L(cDrag, i, j) * W3(uVel, i, j, k) * W3(rhFacW, i, j, k) * m->recip_drF[k - 1];
         }
+      }
+      if (m->useNHMTerms) {
+        /* MOM_U_METRIC_NH (pkg/mom_common/mom_u_metric_nh.F:56-68), rVel2wUnit = 1, mtNHFacU = 1 */
+        const int kp1 = k + 1 < Nr ? k + 1 : Nr;
+        const double ov = (k == Nr) ? 0.0 : 1.0;
+        for (int j = jMin; j <= jMax; j++)
+          for (int i = iMin; i <= iMax; i++)
+            W3(gU, i, j, k) = W3(gU, i, j, k) +
+                1.0 * (W3(uVel, i, j, k) * recip_rSphere * 0.25 *
+                       ((W3(wVel, i - 1, j, kp1) + W3(wVel, i, j, kp1)) * ov + (W3(wVel, i - 1, j, k) + W3(wVel, i, j, k))) *
+                       m->gravitySign);
       }
       if (metricSphere) {
         /* MOM_U_METRIC_SPHERE (pkg/mom_fluxform/mom_u_metric_sphere.F), mom_fluxform.F:714-721 */
@@ -287,7 +425,7 @@ void oracle_dynamics(OModel *m) {
           for (int j = 2 - OLy; j <= sNy + OLy; j++)
             for (int i = 2 - OLx; i <= sNx + OLx; i++) {
               double f = L(rTransV, i, j) * (0.5 * (W3(vVel, i, j, kk) + W3(vVel, i, j, kk - 1)));
-              f = f + 0.25 * (W3(wVel, i, j, kk) * L(rA, i, j) * (W3(maskC, i, j, kk) - W3(maskC, i, j, kk - 1)) +
+              if (m->select_rStar == 0) f = f + 0.25 * (W3(wVel, i, j, kk) * L(rA, i, j) * (W3(maskC, i, j, kk) - W3(maskC, i, j, kk - 1)) +
                               W3(wVel, i, j - 1, kk) * L(rA, i, j - 1) * (W3(maskC, i, j - 1, kk) - W3(maskC, i, j - 1, kk - 1))) *
                           W3(vVel, i, j, kk);
               L(fVerVkp, i, j) = f;
@@ -300,22 +438,53 @@ void oracle_dynamics(OModel *m) {
                               ((L(fZon, i + 1, j) - L(fZon, i, j)) * uDudxFac +
                                (L(fMer, i, j) - L(fMer, i, j - 1)) * vDudyFac +
                                (L(fVerVkp, i, j) - L(fVerVkm, i, j)) * m->rkSign * rVelDudrFac);
+        if (rstar)   /* mom_fluxform.F:787-808 */
+          for (int j = jMin; j <= jMax; j++)
+            for (int i = iMin; i <= iMax; i++)
+              W3(gV, i, j, k) = W3(gV, i, j, k) - (L(rStarExpS, i, j) - 1.0) / m->deltaTFreeSurf * W3(vVel, i, j, k);
       } else {
         for (int j = 1 - OLy; j <= sNy + OLy; j++)
           for (int i = 1 - OLx; i <= sNx + OLx; i++) W3(gV, i, j, k) = 0.0;
       }
       if (m->momViscosity) {
+        if (biharm) {
+          /* MOM_V_DEL2V (pkg/mom_fluxform/mom_v_del2v.F:59-117) */
+          for (int j = 2 - OLy; j <= sNy + OLy - 1; j++)
+            for (int i = 2 - OLx; i <= sNx + OLx; i++)
+              L(d2Z, i, j) = m->drF[k - 1] * L(hFacZ, i, j) * L(dyU, i, j) * L(recip_dxV, i, j) *
+                             (W3(vVel, i, j, k) - W3(vVel, i - 1, j, k)) * 1.0;
+          for (int j = 1 - OLy; j <= sNy + OLy - 1; j++)
+            for (int i = 2 - OLx; i <= sNx + OLx - 1; i++)
+              L(d2M, i, j) = m->drF[k - 1] * W3(hFacC, i, j, k) * L(dxF, i, j) * L(recip_dyF, i, j) *
+                             (W3(vVel, i, j + 1, k) - W3(vVel, i, j, k));
+          for (int j = 2 - OLy; j <= sNy + OLy - 1; j++)
+            for (int i = 2 - OLx; i <= sNx + OLx - 1; i++)
+              L(v4F, i, j) = m->recip_drF[k - 1] * W3(rhFacS, i, j, k) * L(recip_rAs, i, j) *
+                             (L(d2Z, i + 1, j) - L(d2Z, i, j) + L(d2M, i, j) - L(d2M, i, j - 1)) * W3(maskS, i, j, k);
+          if (m->no_slip_sides)
+            for (int j = 2 - OLy; j <= sNy + OLy - 1; j++)
+              for (int i = 2 - OLx; i <= sNx + OLx - 1; i++) {
+                const double hW = W3(h0FacS, i, j, k) - L(h0FacZ, i, j);
+                const double hE = W3(h0FacS, i, j, k) - L(h0FacZ, i + 1, j);
+                L(v4F, i, j) = L(v4F, i, j) - W3(rhFacS, i, j, k) * L(recip_rAs, i, j) *
+                                                  (hW * L(dyU, i, j) * L(recip_dxV, i, j) +
+                                                   hE * L(dyU, i + 1, j) * L(recip_dxV, i + 1, j)) *
+                                                  W3(vVel, i, j, k) * m->sideDragFactor * W3(maskS, i, j, k);
+              }
+        }
         /* MOM_V_XVISCFLUX (mom_v_xviscflux.F:52-69) */
         for (int j = 1 - OLy; j <= sNy + OLy; j++)
           for (int i = 2 - OLx; i <= sNx + OLx; i++)
             L(fZon, i, j) = L(dyU, i, j) * m->drF[k - 1] * L(hFacZ, i, j) *
-                            (-m->viscAhZ * (W3(vVel, i, j, k) - W3(vVel, i - 1, j, k)) * 1.0 + m->viscA4Z * 0.0 * 1.0) *
+                            (-m->viscAhZ * (W3(vVel, i, j, k) - W3(vVel, i - 1, j, k)) * 1.0 +
+                             m->viscA4Z * (L(v4F, i, j) - L(v4F, i - 1, j)) * 1.0) *
                             L(recip_dxV, i, j);
         /* MOM_V_YVISCFLUX (mom_v_yviscflux.F:51-73) */
         for (int j = 1 - OLy; j <= sNy + OLy - 1; j++)
           for (int i = 1 - OLx; i <= sNx + OLx - 1; i++)
             L(fMer, i, j) = L(dxF, i, j) * m->drF[k - 1] * W3(hFacC, i, j, k) *
-                            (-m->viscAhD * (W3(vVel, i, j + 1, k) - W3(vVel, i, j, k)) + m->viscA4D * 0.0) *
+                            (-m->viscAhD * (W3(vVel, i, j + 1, k) - W3(vVel, i, j, k)) +
+                             m->viscA4D * (L(v4F, i, j + 1) - L(v4F, i, j))) *
                             L(recip_dyF, i, j);
         for (int q = 0; q < 2; q++) {
           int kk = k + q; double *fl = q ? fVrDw : fVrUp;
@@ -340,11 +509,11 @@ void oracle_dynamics(OModel *m) {
           /* MOM_V_SIDEDRAG (pkg/mom_common/mom_v_sidedrag.F) */
           for (int j = 2 - OLy; j <= sNy + OLy - 1; j++)
             for (int i = 2 - OLx; i <= sNx + OLx - 1; i++) {
-              double hW = W3(hFacS, i, j, k) - L(hFacZ, i, j);
-              double hE = W3(hFacS, i, j, k) - L(hFacZ, i + 1, j);
+              double hW = W3(h0FacS, i, j, k) - L(h0FacZ, i, j);
+              double hE = W3(h0FacS, i, j, k) - L(h0FacZ, i + 1, j);
               L(vF, i, j) = -W3(rhFacS, i, j, k) * m->recip_drF[k - 1] * L(recip_rAs, i, j) *
-                            (hW * L(dyU, i, j) * L(recip_dxV, i, j) * (m->viscAhZ * W3(vVel, i, j, k) - m->viscA4Z * 0.0) +
-                             hE * L(dyU, i + 1, j) * L(recip_dxV, i + 1, j) * (m->viscAhZ * W3(vVel, i, j, k) - m->viscA4Z * 0.0)) *
+                            (hW * L(dyU, i, j) * L(recip_dxV, i, j) * (m->viscAhZ * W3(vVel, i, j, k) - m->viscA4Z * L(v4F, i, j)) +
+                             hE * L(dyU, i + 1, j) * L(recip_dxV, i + 1, j) * (m->viscAhZ * W3(vVel, i, j, k) - m->viscA4Z * L(v4F, i, j))) *
                             m->drF[k - 1] * m->sideDragFactor;
             }
           for (int j = jMin; j <= jMax; j++)
@@ -367,6 +536,17 @@ void oracle_dynamics(OModel *m) {
             for (int i = iMin; i <= iMax; i++)
               L(gvDiss, i, j) = L(gvDiss, i, j) - L(cDrag, i, j) * W3(vVel, i, j, k) * W3(rhFacS, i, j, k) * m->recip_drF[k - 1];
         }
+      }
+      if (m->useNHMTerms) {
+        /* MOM_V_METRIC_NH (pkg/mom_common/mom_v_metric_nh.F:56-68) */
+        const int kp1 = k + 1 < Nr ? k + 1 : Nr;
+        const double ov = (k == Nr) ? 0.0 : 1.0;
+        for (int j = jMin; j <= jMax; j++)
+          for (int i = iMin; i <= iMax; i++)
+            W3(gV, i, j, k) = W3(gV, i, j, k) +
+                1.0 * (W3(vVel, i, j, k) * recip_rSphere * 0.25 *
+                       ((W3(wVel, i, j - 1, kp1) + W3(wVel, i, j, kp1)) * ov + (W3(wVel, i, j - 1, k) + W3(wVel, i, j, k))) *
+                       m->gravitySign);
       }
       if (metricSphere) {
         /* MOM_V_METRIC_SPHERE (pkg/mom_fluxform/mom_v_metric_sphere.F), mom_fluxform.F:973-980 */
@@ -411,6 +591,19 @@ void oracle_dynamics(OModel *m) {
           for (int i = iMin; i <= iMax; i++) {
             W3(gU, i, j, k) = W3(gU, i, j, k) + fuFac * L(uCf, i, j);
             W3(gV, i, j, k) = W3(gV, i, j, k) + fvFac * L(vCf, i, j);
+          }
+      }
+      if (m->select3dCoriScheme >= 1) {
+        /* MOM_U_CORIOLIS_NH (pkg/mom_common/mom_u_coriolis_nh.F:60-76), angleCosC = 1, rVel2wUnit = 1;
+         * MOM_V_CORIOLIS_NH only on curvilinear / rotated grids (mom_fluxform.F:1031-1040) */
+        const int kp1 = k + 1 < Nr ? k + 1 : Nr;
+        const double wMsk = (k == Nr) ? 0.0 : 1.0;
+        for (int j = jMin; j <= jMax; j++)
+          for (int i = iMin; i <= iMax; i++) {
+            const double c = 0.5 * (L(fCoriCos, i, j) * 1.0 * 0.5 * (W3(wVel, i, j, k) + W3(wVel, i, j, kp1) * wMsk) +
+                                    L(fCoriCos, i - 1, j) * 1.0 * 0.5 * (W3(wVel, i - 1, j, k) + W3(wVel, i - 1, j, kp1) * wMsk)) *
+                             m->gravitySign;
+            W3(gU, i, j, k) = W3(gU, i, j, k) + fuFac * c;
           }
       }
       /* masks (mom_fluxform.F:1044-1051) */
@@ -549,6 +742,12 @@ void oracle_dynamics(OModel *m) {
             L(gVtmp, i, j) = L(gVtmp, i, j) + L(vCf, i, j);
           }
       }
+      if (rstar && m->nonlinFreeSurf > 1)   /* timestep.F:274-284 */
+        for (int j = jMin; j <= jMax; j++)
+          for (int i = iMin; i <= iMax; i++) {
+            L(gUtmp, i, j) = L(gUtmp, i, j) / L(rStarExpW, i, j);
+            L(gVtmp, i, j) = L(gVtmp, i, j) / L(rStarExpS, i, j);
+          }
       /* u* = u + dt*(gUtmp + gUdPx)*maskW, gUdPx = 0 for implicSurfPress = 1 (timestep.F:373-388) */
       for (int j = jMin; j <= jMax; j++)
         for (int i = iMin; i <= iMax; i++) {
@@ -565,4 +764,5 @@ void oracle_dynamics(OModel *m) {
   free(guDiss); free(gvDiss); free(guExt); free(gvExt); free(gUtmp); free(gVtmp); free(ab);
   free(kappaRU); free(kappaRV);
   free(phiHydF); free(phiHydC); free(dPhiHydX); free(dPhiHydY); free(mT);
+  free(h0FacZ); free(v4F); free(d2Z); free(d2M); free(alphaRho); free(varLoc); free(dWtransC); free(dWtransU); free(dWtransV);
 }

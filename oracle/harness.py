@@ -44,7 +44,8 @@ def lib():
         L.oracle_ini_depths.restype = c_int
         for fn in ("oracle_dynamics", "oracle_solve_for_pressure", "oracle_momentum_correction_step",
                    "oracle_integr_continuity", "oracle_forward_step", "oracle_oceanic_phys",
-                   "oracle_thermodynamics", "oracle_fields_load"):
+                   "oracle_thermodynamics", "oracle_fields_load", "oracle_ini_nlfs_pickup",
+                   "oracle_calc_r_star", "oracle_update_cg2d", "oracle_integr_continuity_init"):
             getattr(L, fn).argtypes = [vp]
         P = ctypes.POINTER(c_dbl)
         L.oracle_cg2d.argtypes = [vp, P, P, P, P, P, ctypes.POINTER(c_int), ctypes.POINTER(c_int)]
@@ -188,6 +189,9 @@ def oracle_from_config(cfg, **kw):
         o.iarr(n)[:] = g.i[n]
     o.set(cg2dNorm=g.cg2dNorm, cg2dTolerance_sq=g.cg2dTolerance_sq, cg2dNormaliseRHS=int(g.cg2dNormaliseRHS),
           globalArea=g.globalArea)
+    for n in ("h0FacC", "h0FacW", "h0FacS"):   # INI_MASKS_ETC: h0Fac = hFac at rest
+        if n not in state and n in g.f:
+            o.arr(n).reshape(-1)[:] = np.ravel(g.f[n])
     for k, v in state.items():
         o.arr(k).reshape(-1)[:len(np.ravel(v))] = np.ravel(v)
     return o, g
@@ -204,6 +208,21 @@ def latlon_oracle(**kw):
              "SSS": "forcSSS"}
     for k, v in forcing.items():
         o.arr(names[k])[:] = np.ravel(v)
+    return o, g
+
+
+def ocean90_oracle(**kw):
+    """verification/global_ocean.90x40x15 (BASELINE config 2) as the oracle, restarted from
+    its pickups; runs the INITIALISE_VARIA r* sequence (calc_r_star -> update_r_star ->
+    update_cg2d -> integr_continuity -> calc_r_star), so dynstat() is the nIter0 monitor."""
+    from mitgcm_amd import configs
+    g, params, state, forcing = configs.global_ocean_90x40x15(**kw)
+    o, _ = oracle_from_config(lambda: (g, params, state))
+    names = {"taux": "forcTaux", "tauy": "forcTauy", "Qnet": "forcQnet", "EmPmR": "forcEmPmR", "SST": "forcSST",
+             "SSS": "forcSSS"}
+    for k, v in forcing.items():
+        o.arr(names[k])[:] = np.ravel(v)
+    o.L.oracle_ini_nlfs_pickup(o.h)
     return o, g
 
 

@@ -54,7 +54,15 @@ OModel *oracle_new(int sNx, int sNy, int OLx, int OLy, int Nr, int nSx, int nSy)
   A2(fCoriCos); A2(tanPhiAtU); A2(tanPhiAtV); A2(surfaceForcingT); A2(SST); A2(lambdaThetaClimRelax);
   A2(etaH); A2(dEtaHdt); A2(surfaceForcingS);
   A2(Qnet); A2(EmPmR); A2(SSS); A2(lambdaSaltClimRelax); A2(saltFlux); A2(etaNm1);
+  A2(rStarFacC); A2(rStarFacW); A2(rStarFacS); A2(rStarFacNm1C); A2(rStarFacNm1W); A2(rStarFacNm1S);
+  A2(rStarExpC); A2(rStarExpW); A2(rStarExpS); A2(rStarDhCDt); A2(rStarDhWDt); A2(rStarDhSDt);
+  A2(rSurfW); A2(rSurfS); A2(rLowW); A2(rLowS); A2(recip_Rcol); A2(PmEpR);
 #undef A2
+  for (long p = 0; p < N2; p++)   /* ini_nlfs_vars.F:79-92 */
+    m->rStarFacC[p] = m->rStarFacW[p] = m->rStarFacS[p] = m->rStarFacNm1C[p] = m->rStarFacNm1W[p] =
+        m->rStarFacNm1S[p] = m->rStarExpC[p] = m->rStarExpW[p] = m->rStarExpS[p] = 1.0;
+  m->phiRef = zalloc(2 * Nr + 1);
+  m->hFacInf = 0.2; m->hFacSup = 2.0; m->cg2dPreCondFreq = 1;
   m->pRef4EOS = zalloc(Nr);
 #define AF(f) m->f = zalloc(N2 * m->nForcRec)
   AF(forcTaux); AF(forcTauy); AF(forcQnet); AF(forcEmPmR); AF(forcSST); AF(forcSSS);
@@ -66,7 +74,7 @@ OModel *oracle_new(int sNx, int sNy, int OLx, int OLy, int Nr, int nSx, int nSy)
   A3(uVel); A3(vVel); A3(wVel); A3(theta); A3(salt); A3(gU); A3(gV); A3(guNm1); A3(gvNm1);
   A3(gtNm1); A3(gsNm1); A3(rhoInSitu); A3(IVDConvCount);
   A3(Kwx); A3(Kwy); A3(Kwz); A3(Kux); A3(Kvy); A3(uVelD); A3(vVelD); A3(uNM1); A3(vNM1);
-  A3(sigmaX); A3(sigmaY); A3(sigmaR);
+  A3(sigmaX); A3(sigmaY); A3(sigmaR); A3(h0FacC); A3(h0FacW); A3(h0FacS); A3(totPhiHyd);
 #undef A3
   return m;
 }
@@ -90,7 +98,11 @@ void oracle_free(OModel *m) {
                    &m->SSS, &m->lambdaSaltClimRelax, &m->saltFlux, &m->etaNm1, &m->Kwx, &m->Kwy, &m->Kwz,
                    &m->Kux, &m->Kvy, &m->uVelD, &m->vVelD, &m->uNM1, &m->vNM1, &m->sigmaX, &m->sigmaY,
                    &m->sigmaR, &m->forcTaux, &m->forcTauy, &m->forcQnet, &m->forcEmPmR, &m->forcSST,
-                   &m->forcSSS};
+                   &m->forcSSS, &m->h0FacC, &m->h0FacW, &m->h0FacS, &m->totPhiHyd, &m->rStarFacC,
+                   &m->rStarFacW, &m->rStarFacS, &m->rStarFacNm1C, &m->rStarFacNm1W, &m->rStarFacNm1S,
+                   &m->rStarExpC, &m->rStarExpW, &m->rStarExpS, &m->rStarDhCDt, &m->rStarDhWDt,
+                   &m->rStarDhSDt, &m->rSurfW, &m->rSurfS, &m->rLowW, &m->rLowS, &m->recip_Rcol, &m->PmEpR,
+                   &m->phiRef};
   for (size_t i = 0; i < sizeof(dp) / sizeof(dp[0]); i++) free(*dp[i]);
   free(m->kSurfC); free(m->kSurfW); free(m->kSurfS); free(m->kLowC);
   free(m);
@@ -123,6 +135,8 @@ static const PDesc PTAB[] = {
   PD(salt_EvPrRn), PD(tauCD), PD(rCD), PD(epsAB_CD), PD(externForcingPeriod), PD(externForcingCycle),
   PD(GM_background_K), PD(GM_isopycK), PD(GM_skewflx), PD(GM_maxSlope), PD(GM_Kmin_horiz),
   PD(GM_Small_Number), PD(GM_slopeSqCutoff),
+  PI_(nonlinFreeSurf), PI_(select_rStar), PI_(quasiHydrostatic), PI_(useNHMTerms), PI_(select3dCoriScheme),
+  PI_(selectP_inEOS_Zc), PI_(storePhiHyd4Phys), PI_(cg2dPreCondFreq), PD(hFacInf), PD(hFacSup),
 };
 #undef PD
 #undef PI_
@@ -192,6 +206,14 @@ double *oracle_array(OModel *m, const char *name, long *count) {
     {"forcTaux", m->forcTaux, N2 * m->nForcRec}, {"forcTauy", m->forcTauy, N2 * m->nForcRec},
     {"forcQnet", m->forcQnet, N2 * m->nForcRec}, {"forcEmPmR", m->forcEmPmR, N2 * m->nForcRec},
     {"forcSST", m->forcSST, N2 * m->nForcRec}, {"forcSSS", m->forcSSS, N2 * m->nForcRec},
+    {"h0FacC", m->h0FacC, N3}, {"h0FacW", m->h0FacW, N3}, {"h0FacS", m->h0FacS, N3},
+    {"totPhiHyd", m->totPhiHyd, N3}, {"rStarFacC", m->rStarFacC, N2}, {"rStarFacW", m->rStarFacW, N2},
+    {"rStarFacS", m->rStarFacS, N2}, {"rStarFacNm1C", m->rStarFacNm1C, N2},
+    {"rStarFacNm1W", m->rStarFacNm1W, N2}, {"rStarFacNm1S", m->rStarFacNm1S, N2},
+    {"rStarExpC", m->rStarExpC, N2}, {"rStarExpW", m->rStarExpW, N2}, {"rStarExpS", m->rStarExpS, N2},
+    {"rStarDhCDt", m->rStarDhCDt, N2}, {"rStarDhWDt", m->rStarDhWDt, N2}, {"rStarDhSDt", m->rStarDhSDt, N2},
+    {"rSurfW", m->rSurfW, N2}, {"rSurfS", m->rSurfS, N2}, {"rLowW", m->rLowW, N2}, {"rLowS", m->rLowS, N2},
+    {"recip_Rcol", m->recip_Rcol, N2}, {"PmEpR", m->PmEpR, N2}, {"phiRef", m->phiRef, 2 * m->Nr + 1},
   };
   for (size_t i = 0; i < sizeof(t) / sizeof(t[0]); i++)
     if (!strcmp(t[i].n, name)) { if (count) *count = t[i].c; return t[i].p; }
@@ -493,6 +515,9 @@ int oracle_ini_depths(OModel *m, const double *bathyGlobal) {
     ga += tileA;
   }
   m->globalArea = ga;
+  for (long p = 0; p < m->n3 * m->nTiles; p++) {   /* h0Fac = hFac at rest (ini_masks_etc.F) */
+    m->h0FacC[p] = m->hFacC[p]; m->h0FacW[p] = m->hFacW[p]; m->h0FacS[p] = m->hFacS[p];
+  }
   free(rLowW); free(rLowS); free(rSurfW); free(rSurfS); free(tmp);
   return 0;
 }

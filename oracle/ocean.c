@@ -82,9 +82,12 @@ void oracle_external_forcing_surf(OModel *m) {
       m->surfaceForcingV[q] = m->fv[q] * mass2rUnit;
       sfT = sfT - m->Qnet[q] * recip_Cp * mass2rUnit;
       sfS = sfS - m->saltFlux[q] * mass2rUnit;
-      /* nonlinFreeSurf = 0: the convertFW2Salt branch (:254-290) applies whatever
-       * useRealFreshWaterFlux is */
-      {
+      if (m->nonlinFreeSurf > 0 && m->useRealFreshWaterFlux) {
+        /* external_forcing_surf.F:253-277: PmEpR changes the column height */
+        if (m->temp_EvPrRn != UNSET_RL) sfT = sfT + m->PmEpR[q] * (m->temp_EvPrRn - m->theta[q3]) * mass2rUnit;
+        if (m->salt_EvPrRn != UNSET_RL) sfS = sfS + m->PmEpR[q] * (m->salt_EvPrRn - m->salt[q3]) * mass2rUnit;
+      } else {
+        /* the convertFW2Salt branch (:278-310) */
         if (m->convertFW2Salt == -1.0) {
           if (m->temp_EvPrRn != UNSET_RL)
             sfT = sfT + m->EmPmR[q] * (m->theta[q3] - m->temp_EvPrRn) * mass2rUnit;
@@ -146,14 +149,25 @@ static double find_bulkmod(double locPres, double t, double s) {
   return bMfresh + bMsalt + bMpres;
 }
 
+/* PRESSURE_FOR_EOS (pressure_for_eos.F:51-105), z-coordinates, dpRef = 0:
+ * selectP_inEOS_Zc = 2 (JMD95P default): rhoConst*(totPhiHyd + phiRef(2k));
+ * 0/1: pRef4EOS(k).  p3 = flat 3-D offset of the point (level kRef). */
+double oracle_pressure_for_eos(const OModel *m, int kRef, long p3) {
+  if (m->selectP_inEOS_Zc == 2) return m->rhoConst * (m->totPhiHyd[p3] + m->phiRef[2 * kRef - 1]) + 0.0;
+  return m->pRef4EOS[kRef - 1] + 0.0;
+}
+
 double oracle_find_rho(const OModel *m, int kRef, double t, double s) {
+  return oracle_find_rho_p(m, kRef, t, s, m->pRef4EOS[kRef - 1] + 0.0);
+}
+
+double oracle_find_rho_p(const OModel *m, int kRef, double t, double s, double locPres) {
   if (m->eosType == 0) {
     /* LINEAR (find_rho.F:84-99) */
     const double dRho = m->rhoNil - m->rhoConst;
     return m->rhoNil * (m->sBeta * (s - m->sRef[kRef - 1]) - m->tAlpha * (t - m->tRef[kRef - 1])) + dRho;
   }
-  /* JMD95Z, selectP_inEOS_Zc = 0: locPres = pRef4EOS(kRef) + (surf_pRef - eosRefP0) = pRef4EOS(kRef) + 0 */
-  const double locPres = m->pRef4EOS[kRef - 1] + 0.0;
+  /* JMD95Z / JMD95P (find_rho.F:136-160): same formula, locPres from PRESSURE_FOR_EOS */
   const double rhoP0 = find_rhop0(t, s);
   const double bulkMod = find_bulkmod(locPres, t, s);
   return rhoP0 / (1.0 - locPres * SItoBar / bulkMod) - m->rhoConst;

@@ -96,6 +96,16 @@ typedef struct OModel {
   /* EXTERNAL_FIELDS_LOAD records, nForcRec x (2-D field), halos exchanged */
   double *forcTaux, *forcTauy, *forcQnet, *forcEmPmR, *forcSST, *forcSSS;
 
+  /* --- non-linear free surface, r* coordinate, QH / NH metric, JMD95P (global_ocean.90x40x15) --- */
+  int nonlinFreeSurf, select_rStar, quasiHydrostatic, useNHMTerms, select3dCoriScheme, selectP_inEOS_Zc;
+  int storePhiHyd4Phys, cg2dPreCondFreq;
+  double hFacInf, hFacSup;
+  double *h0FacC, *h0FacW, *h0FacS, *totPhiHyd;                            /* 3-D */
+  double *rStarFacC, *rStarFacW, *rStarFacS, *rStarFacNm1C, *rStarFacNm1W, *rStarFacNm1S;
+  double *rStarExpC, *rStarExpW, *rStarExpS, *rStarDhCDt, *rStarDhWDt, *rStarDhSDt;
+  double *rSurfW, *rSurfS, *rLowW, *rLowS, *recip_Rcol, *PmEpR;            /* 2-D */
+  double *phiRef;                                                          /* [2*Nr+1] */
+
   /* --- outputs of the last SOLVE_FOR_PRESSURE --- */
   double firstResidual, minResidualSq, lastResidual, sumRHS, rhsMax;
   int numIters, nIterMin;
@@ -136,17 +146,26 @@ void oracle_cg2d(OModel *m, double *cg2d_b, double *cg2d_x,
                  double *firstResidual, double *minResidualSq, double *lastResidual,
                  int *numIters, int *nIterMin);      /* CG2D (cg2d.F:13) */
 void oracle_momentum_correction_step(OModel *m);     /* momentum_correction_step.F:7 */
-void oracle_integr_continuity(OModel *m);            /* integr_continuity.F:13 */
+void oracle_integr_continuity(OModel *m);            /* integr_continuity.F:13, in FORWARD_STEP */
+void oracle_integr_continuity_init(OModel *m);       /* the INITIALISE_VARIA call (myIter = nIter0) */
 void oracle_forward_step(OModel *m);
 void oracle_oceanic_phys(OModel *m);                 /* DO_OCEANIC_PHYS subset (do_oceanic_phys.F:555-882) */
 void oracle_thermodynamics(OModel *m);               /* THERMODYNAMICS -> TEMP_INTEGRATE (temp_integrate.F) */                 /* forward_step.F:64 (supported subset) */
 
 /* ocean physics (ocean.c) */
 void oracle_fields_load(OModel *m);                  /* EXTERNAL_FIELDS_LOAD (external_fields_load.F) */
-double oracle_find_rho(const OModel *m, int kRef, double t, double s);  /* FIND_RHO_2D, one point */
+double oracle_find_rho(const OModel *m, int kRef, double t, double s);  /* FIND_RHO_2D, one point, pRef4EOS */
+double oracle_find_rho_p(const OModel *m, int kRef, double t, double s, double locPres);
+double oracle_pressure_for_eos(const OModel *m, int kRef, long p3);  /* PRESSURE_FOR_EOS, one point */
 void oracle_freeze_surface(OModel *m);               /* FREEZE_SURFACE (freeze_surface.F) */
 void oracle_external_forcing_surf(OModel *m);        /* EXTERNAL_FORCING_SURF (external_forcing_surf.F) */
 void oracle_gmredi_calc_tensor(OModel *m, int t);    /* GMREDI_CALC_TENSOR (gmredi_calc_tensor.F), gkw91 */
+
+/* non-linear free surface / r* (rstar.c) */
+void oracle_calc_r_star(OModel *m);                  /* CALC_R_STAR(etaH) (calc_r_star.F) */
+void oracle_update_r_star(OModel *m, int useLatest); /* UPDATE_R_STAR (update_r_star.F) */
+void oracle_update_cg2d(OModel *m);                  /* UPDATE_CG2D (update_cg2d.F) */
+void oracle_ini_nlfs_pickup(OModel *m);              /* INITIALISE_VARIA r* sequence after a pickup */
 
 /* monitor (pkg/monitor/mon_calc_stats_rl.F): out[6] = min,max,mean,sd,del2,vol */
 void oracle_mon_stats(OModel *m, const double *arr, int myNr, const double *arrhFac,

@@ -293,15 +293,19 @@ void oracle_momentum_correction_step(OModel *m) {
 }
 
 /* INTEGR_CONTINUITY (integr_continuity.F:66-314) -> INTEGRATE_FOR_W
- * (integrate_for_w.F:61-195), linear free surface.  With exactConserv
- * (EXACT_CONSERV defined, myIter > nIter0, no fresh-water flux, no OBCS):
- * dEtaHdt = -hDivFlow/rA, etaN = etaH + implicDiv2Dflow*dEtaHdt*dtFS on the
- * interior, EXCH, then UPDATE_ETAH (update_etah.F:55-73). */
-void oracle_integr_continuity(OModel *m) {
-  const int sNx = m->sNx, sNy = m->sNy, Nr = m->Nr;
+ * (integrate_for_w.F:61-195) -> UPDATE_ETAH (update_etah.F:55-73).
+ * atInit: the call from INITIALISE_VARIA (myIter = nIter0); otherwise the call in
+ * FORWARD_STEP, where myIter = nIter0 + iLoop > nIter0.  exactConserv: dEtaHdt
+ * from the column divergence (and fresh-water flux), etaN = etaH + dEtaHdt*dtFS;
+ * r* (select_rStar > 0): w includes -rStarDhDt*drF*h0FacC. */
+static void integr_continuity(OModel *m, int atInit) {
+  const int sNx = m->sNx, sNy = m->sNy, Nr = m->Nr, nx = m->nx;
   const long N2 = m->n2 * m->nTiles;
-  if (m->exactConserv) {
-    for (int t = 0; t < m->nTiles; t++) {
+  const int rstar = m->nonlinFreeSurf > 0 && m->select_rStar != 0;
+  double *rStarDhDt = calloc(m->n2, 8);
+#define RD(i, j) rStarDhDt[O2(m, i, j, 0)]
+  for (int t = 0; t < m->nTiles; t++) {
+    if (m->exactConserv) {
       double *hDiv = calloc(m->n2, 8);
 #define HD(i, j) hDiv[O2(m, i, j, 0)]
       for (int k = 1; k <= Nr; k++)
@@ -313,18 +317,42 @@ void oracle_integr_continuity(OModel *m) {
             double vT0 = m->vVel[O3(m, i, j, k, t)] * m->dxG[O2(m, i, j, t)] * m->drF[k - 1] * m->hFacS[O3(m, i, j, k, t)];
             HD(i, j) = HD(i, j) + m->maskC[O3(m, i, j, k, t)] * (uT1 - uT0 + vT1 - vT0);
           }
-      for (int j = 1; j <= sNy; j++)
-        for (int i = 1; i <= sNx; i++) {
-          long p = O2(m, i, j, t);
-          const double facEmP = m->useRealFreshWaterFlux ? 1.0 / m->rhoConst : 0.0;   /* mass2rUnit */
-          m->dEtaHdt[p] = -(HD(i, j) * m->recip_rA[p]) - facEmP * m->EmPmR[p];
-          m->etaN[p] = m->etaH[p] + m->implicDiv2DFlow * m->dEtaHdt[p] * m->deltaTFreeSurf;
-        }
+      const double facEmP = m->useRealFreshWaterFlux ? 1.0 / m->rhoConst : 0.0;   /* mass2rUnit */
+      if (atInit && m->nIter0 != 0 && m->useRealFreshWaterFlux) {
+        /* integr_continuity.F:117-136: PmEpR consistent with the pickup dEtaHdt */
+        for (int j = 1; j <= sNy; j++)
+          for (int i = 1; i <= sNx; i++) {
+            const long p = O2(m, i, j, t);
+            m->PmEpR[p] = m->dEtaHdt[p] + HD(i, j) * m->recip_rA[p];
+            m->PmEpR[p] = m->PmEpR[p] * m->rhoConst;                            /* rUnit2mass */
+          }
+      } else if (atInit) {
+        for (int j = 1; j <= sNy; j++)
+          for (int i = 1; i <= sNx; i++) {
+            const long p = O2(m, i, j, t);
+            m->PmEpR[p] = 0.0;
+            m->dEtaHdt[p] = -(HD(i, j) * m->recip_rA[p]);
+          }
+      } else {
+        for (long q = 0; q < m->n2; q++) m->PmEpR[t * m->n2 + q] = -m->EmPmR[t * m->n2 + q];
+        for (int j = 1; j <= sNy; j++)
+          for (int i = 1; i <= sNx; i++) {
+            const long p = O2(m, i, j, t);
+            m->dEtaHdt[p] = -(HD(i, j) * m->recip_rA[p]) - facEmP * m->EmPmR[p];
+          }
+      }
+      if (!atInit)
+        for (int j = 1; j <= sNy; j++)
+          for (int i = 1; i <= sNx; i++) {
+            const long p = O2(m, i, j, t);
+            m->etaN[p] = m->etaH[p] + m->implicDiv2DFlow * m->dEtaHdt[p] * m->deltaTFreeSurf;
+          }
 #undef HD
       free(hDiv);
+      if (rstar)   /* integr_continuity.F:171-183 (deepFac2F = rhoFacF = 1) */
+        for (int j = 1; j <= sNy; j++)
+          for (int i = 1; i <= sNx; i++) RD(i, j) = m->dEtaHdt[O2(m, i, j, t)] * m->recip_Rcol[O2(m, i, j, t)];
     }
-  }
-  for (int t = 0; t < m->nTiles; t++)
     for (int k = Nr; k >= 1; k--)
       for (int j = 1; j <= sNy; j++)
         for (int i = 1; i <= sNx; i++) {
@@ -334,17 +362,31 @@ void oracle_integr_continuity(OModel *m) {
           double vT1 = m->vVel[O3(m, i, j + 1, k, t)] * m->dxG[O2(m, i, j + 1, t)] * m->drF[k - 1] * m->hFacS[O3(m, i, j + 1, k, t)];
           double vT0 = m->vVel[O3(m, i, j, k, t)] * m->dxG[p] * m->drF[k - 1] * m->hFacS[O3(m, i, j, k, t)];
           double conv2d = -(uT1 - uT0 + vT1 - vT0);
-          if (k == Nr)
+          if (rstar) {   /* integrate_for_w.F:117-140 */
+            const double dh = RD(i, j) * m->drF[k - 1] * m->h0FacC[O3(m, i, j, k, t)];
+            if (k == Nr)
+              m->wVel[O3(m, i, j, k, t)] = (conv2d * m->recip_rA[p] - dh) * m->maskC[O3(m, i, j, k, t)];
+            else
+              m->wVel[O3(m, i, j, k, t)] =
+                  (m->wVel[O3(m, i, j, k + 1, t)] + conv2d * m->recip_rA[p] - dh) * m->maskC[O3(m, i, j, k, t)];
+          } else if (k == Nr) {
             m->wVel[O3(m, i, j, k, t)] = conv2d * m->recip_rA[p] * m->maskC[O3(m, i, j, k, t)];
-          else
+          } else {
             m->wVel[O3(m, i, j, k, t)] = (m->wVel[O3(m, i, j, k + 1, t)] + conv2d * m->recip_rA[p]) * m->maskC[O3(m, i, j, k, t)];
+          }
         }
-  if (m->exactConserv) {
-    oracle_exch_xy(m, m->etaN);
-    for (long p = 0; p < N2; p++) m->etaH[p] = m->etaN[p];   /* UPDATE_ETAH, implicDiv2Dflow = 1 */
   }
-  if (m->myIter == m->nIter0) oracle_exch_xyz(m, m->wVel, Nr);
+#undef RD
+  free(rStarDhDt);
+  if (m->exactConserv && !atInit) oracle_exch_xy(m, m->etaN);
+  if (atInit) oracle_exch_xyz(m, m->wVel, Nr);
+  if (m->exactConserv)
+    for (long p = 0; p < N2; p++) m->etaH[p] = m->etaN[p];   /* UPDATE_ETAH, implicDiv2Dflow = 1 */
+  (void)nx;
 }
+
+void oracle_integr_continuity(OModel *m) { integr_continuity(m, 0); }
+void oracle_integr_continuity_init(OModel *m) { integr_continuity(m, 1); }
 
 /* FORWARD_STEP (model/src/forward_step.F:64-1256) for the supported subset:
  * EXTERNAL_FORCING_SURF (momentum part) -> DYNAMICS -> SOLVE_FOR_PRESSURE ->
@@ -358,19 +400,35 @@ void oracle_forward_step(OModel *m) {
     /* forward_step.F:732 THERMODYNAMICS (staggerTimeStep = F) */
     oracle_thermodynamics(m);
   }
+  const int rstar = m->nonlinFreeSurf > 0 && m->select_rStar > 0;
   if (m->momStepping) {
     oracle_dynamics(m);
-    /* forward_step.F:806: myIter/myTime advance before SOLVE_FOR_PRESSURE */
+    /* forward_step.F:806: myIter/myTime advance before SOLVE_FOR_PRESSURE;
+     * :829-877 UPDATE_R_STAR(.TRUE.) + UPDATE_CG2D (nonlinFreeSurf > 2) */
+    if (rstar) {
+      oracle_update_r_star(m, 1);
+      if (m->nonlinFreeSurf > 2) oracle_update_cg2d(m);
+    }
     oracle_solve_for_pressure(m);
     oracle_momentum_correction_step(m);
   }
   oracle_integr_continuity(m);
+  /* forward_step.F:965-977 CALC_R_STAR(etaH(n+1)) */
+  if (rstar) oracle_calc_r_star(m);
   /* do_fields_blocking_exchanges.F:54-97 */
   oracle_exch_xyz(m, m->uVel, m->Nr);
   oracle_exch_xyz(m, m->vVel, m->Nr);
   oracle_exch_xyz(m, m->wVel, m->Nr);
   oracle_exch_xyz(m, m->theta, m->Nr);
   oracle_exch_xyz(m, m->salt, m->Nr);
+  if (m->useCDscheme) {   /* EXCH_UV_DGRID_3D_RL(uVelD, vVelD): lat-lon = scalar copies */
+    oracle_exch_xyz(m, m->uVelD, m->Nr);
+    oracle_exch_xyz(m, m->vVelD, m->Nr);
+  }
+  if (m->storePhiHyd4Phys) oracle_exch_xyz(m, m->totPhiHyd, m->Nr);
+  /* next step's RESET_NLFS_VARS + UPDATE_R_STAR(.FALSE.) (forward_step.F:463-498)
+   * restore hFac = h0Fac*rStarFacNm1, the values UPDATE_R_STAR(.TRUE.) set above */
+  if (rstar) oracle_update_r_star(m, 0);
   m->myIter = m->myIter + 1;
   m->myTime = m->myTime + m->deltaTClock;
 }

@@ -26,6 +26,7 @@
 
 #define L(a, i, j) (a)[(long)((i) + OLx - 1) + (long)((j) + OLy - 1) * nx]
 #define W3(a, i, j, k) (a)[(long)((i) + OLx - 1) + (long)((j) + OLy - 1) * nx + (long)((k) - 1) * n2]
+#define W3I(i, j, k) ((long)((i) + OLx - 1) + (long)((j) + OLy - 1) * nx + (long)((k) - 1) * n2)
 
 /* FIND_RHO_2D, equationOfState = 'LINEAR' (find_rho.F:125-136) */
 
@@ -47,7 +48,8 @@ void oracle_oceanic_phys(OModel *m) {
     for (int k = 1; k <= Nr; k++)
       for (int j = 1 - OLy; j <= sNy + OLy; j++)
         for (int i = 1 - OLx; i <= sNx + OLx; i++)
-          W3(rhoInSitu, i, j, k) = oracle_find_rho(m, k, W3(theta, i, j, k), W3(salt, i, j, k));
+          W3(rhoInSitu, i, j, k) = oracle_find_rho_p(m, k, W3(theta, i, j, k), W3(salt, i, j, k),
+                                                     oracle_pressure_for_eos(m, k, t * m->n3 + W3I(i, j, k)));
     /* k = Nr..1 (do_oceanic_phys.F:799-882): GRAD_SIGMA with rho(theta(k-1), kRef = k),
      * CALC_IVDC */
     if (m->useGMRedi || calcConvect) {
@@ -64,7 +66,8 @@ void oracle_oceanic_phys(OModel *m) {
           for (int j = 1 - OLy; j <= sNy + OLy; j++)
             for (int i = 1 - OLx; i <= sNx + OLx; i++) {
               const double rhoKp1 = W3(rhoInSitu, i, j, k);
-              const double rhoKm1 = oracle_find_rho(m, k, W3(theta, i, j, k - 1), W3(salt, i, j, k - 1));
+              const double rhoKm1 = oracle_find_rho_p(m, k, W3(theta, i, j, k - 1), W3(salt, i, j, k - 1),
+                                                      oracle_pressure_for_eos(m, k, t * m->n3 + W3I(i, j, k)));
               W3(sigmaR, i, j, k) = W3(maskC, i, j, k) * W3(maskC, i, j, k - 1) * m->recip_drC[k - 1] * m->rkSign *
                                     (rhoKp1 - rhoKm1);
               if (calcConvect) W3(conv, i, j, k) = (-W3(sigmaR, i, j, k) * m->gravitySign > 0.0) ? 1.0 : 0.0;
@@ -221,6 +224,7 @@ static void tracer_integrate(OModel *m, const TracerSpec *c) {
   const int calcAdvection = c->advection && !multiDim;
   const double advFac = calcAdvection ? 1.0 : 0.0, rAdvFac = m->rkSign * advFac;
   const double abFac = (m->myIter == m->nIter0 && m->nIter0 == 0) ? 0.0 : 0.5 + m->abEps; /* startAB = nIter0 */
+  const int rstar = m->nonlinFreeSurf > 0 && m->select_rStar > 0;
 
   for (int t = 0; t < m->nTiles; t++) {
     double *theta = c->tr + t * n3, *gtNm1 = c->gNm1 + t * n3;
@@ -234,6 +238,7 @@ static void tracer_integrate(OModel *m, const TracerSpec *c) {
     const double *Kwx = m->Kwx + t * n3, *Kwy = m->Kwy + t * n3, *Kwz = m->Kwz + t * n3;
     const double *Kux = m->Kux + t * n3, *Kvy = m->Kvy + t * n3, *maskW = m->maskW + t * n3;
     const double *maskS = m->maskS + t * n3;
+    const double *rStarExpC = m->rStarExpC + t * n2;
 
     /* CALC_3D_DIFFUSIVITY: KappaR = IVDConvCount*ivdc_kappa + KbryanLewis79(=0) + diffKrNr(k) */
     for (int k = 1; k <= Nr; k++)
@@ -380,6 +385,12 @@ static void tracer_integrate(OModel *m, const TracerSpec *c) {
             W3(gT, i, j, k) = W3(gT, i, j, k) + ab;
           }
         }
+      if (rstar)   /* FREESURF_RESCALE_G (freesurf_rescale_g.F:52-62) of gT and gtNm1 (temp_integrate.F:412-446) */
+        for (int j = 1 - OLy; j <= sNy + OLy; j++)
+          for (int i = 1 - OLx; i <= sNx + OLx; i++) {
+            W3(gT, i, j, k) = W3(gT, i, j, k) / L(rStarExpC, i, j);
+            if (useAB) W3(gtNm1, i, j, k) = W3(gtNm1, i, j, k) / L(rStarExpC, i, j);
+          }
     }
     /* TIMESTEP_TRACER: gT = tracer + dTtracerLev(k)*gT */
     for (long p = 0; p < n3; p++) gT[p] = theta[p] + m->deltaTtracer * gT[p];
@@ -390,11 +401,13 @@ static void tracer_integrate(OModel *m, const TracerSpec *c) {
         for (int j = 1; j <= sNy; j++)
           for (int i = 1; i <= sNx; i++) {
             double sub = 0.0, sup = 0.0;
+            /* recip_hFacNew (thermodynamics.F:198-210): recip_hFacC/rStarExpC under r* */
+            const double rhN = rstar ? W3(rhFacC, i, j, k) / L(rStarExpC, i, j) : W3(rhFacC, i, j, k);
             if (k >= 2)
-              sub = -(m->deltaTtracer * W3(maskC, i, j, k - 1) * W3(rhFacC, i, j, k) * m->recip_drF[k - 1] *
+              sub = -(m->deltaTtracer * W3(maskC, i, j, k - 1) * rhN * m->recip_drF[k - 1] *
                       W3(kappaRT, i, j, k) * m->recip_drC[k - 1]);
             if (k <= Nr - 1)
-              sup = -(m->deltaTtracer * W3(maskC, i, j, k + 1) * W3(rhFacC, i, j, k) * m->recip_drF[k - 1] *
+              sup = -(m->deltaTtracer * W3(maskC, i, j, k + 1) * rhN * m->recip_drF[k - 1] *
                       W3(kappaRT, i, j, k + 1) * m->recip_drC[k]);
             W3(a3, i, j, k) = sub; W3(c3, i, j, k) = sup;
             W3(b3, i, j, k) = 1.0 - (sub + sup);
