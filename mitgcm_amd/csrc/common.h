@@ -42,6 +42,10 @@ struct Params {
   double HeatCapacity_Cp, convertFW2Salt, temp_EvPrRn, salt_EvPrRn, rCD, epsAB_CD;
   double externForcingPeriod, externForcingCycle;
   double GM_background_K, GM_isopycK, GM_skewflx, GM_maxSlope, GM_Kmin_horiz, GM_Small_Number, GM_slopeSqCutoff;
+  // global_ocean.90x40x15: r* non-linear free surface, JMD95P, QH / NH metric, 3-D Coriolis
+  int nonlinFreeSurf, select_rStar, quasiHydrostatic, useNHMTerms, select3dCoriScheme, selectP_inEOS_Zc;
+  int storePhiHyd4Phys;
+  double hFacInf;
 };
 
 // Device pointers of every field the kernels touch.
@@ -55,9 +59,11 @@ struct Fields {
   const double *tanPhiAtU, *tanPhiAtV, *maskInC, *lambdaThetaClimRelax;
   double *SST;   // interpolated by k_fields_load
   // 3-D masks
-  const double *hFacC, *hFacW, *hFacS, *recip_hFacC, *recip_hFacW, *recip_hFacS, *maskC, *maskW, *maskS;
+  // (hFac and the CG2D operator are rewritten every step under r*: UPDATE_R_STAR, UPDATE_CG2D)
+  double *hFacC, *hFacW, *hFacS, *recip_hFacC, *recip_hFacW, *recip_hFacS;
+  const double *maskC, *maskW, *maskS;
   // CG2D operator
-  const double *aW2d, *aS2d, *aC2d, *pW, *pS, *pC;
+  double *aW2d, *aS2d, *aC2d, *pW, *pS, *pC;
   // state
   double *uVel, *vVel, *wVel, *theta, *salt, *etaN;
   double *gU, *gV, *guNm1, *gvNm1;
@@ -73,6 +79,13 @@ struct Fields {
   double *Qnet, *EmPmR, *SSS, *lambdaSaltClimRelax, *etaNm1;   // 2-D
   double *sigmaR, *Kwx, *Kwy, *Kwz, *Kux, *Kvy;                // 3-D GM/Redi
   double *uVelD, *vVelD, *uNM1, *vNM1, *cdU, *cdV;             // 3-D CD scheme (+ gUtmp/gVtmp scratch)
+  // r* coordinate (global_ocean.90x40x15): rest-state hFac, column geometry, the r* factors
+  const double *h0FacC, *h0FacW, *h0FacS;                                  // 3-D
+  const double *fCoriCos, *recip_Rcol, *rSurfW, *rSurfS, *rLowW, *rLowS, *Ro_surf, *R_low;   // 2-D
+  const double *phiRefC;                                                   // [Nr]: phiRef(2k)
+  double *totPhiHyd, *alphaRho, *del2u, *del2v;                            // 3-D
+  double *rStarFacC, *rStarFacW, *rStarFacS, *rStarExpC, *rStarExpW, *rStarExpS;   // 2-D
+  double *rStarDhCDt, *rStarDhWDt, *rStarDhSDt, *PmEpR, *dEtaHdt;          // 2-D
   // solver work
   double *cg2d_b, *cg2d_x;
 };
@@ -141,7 +154,7 @@ struct TracerArgs {
 };
 
 // Fields exchanged together by k_exchange_multi.
-#define MG_XMAX 6
+#define MG_XMAX 8
 struct XFields {
   double *p[MG_XMAX];
   int nz[MG_XMAX];

@@ -25,23 +25,114 @@ __device__ __forceinline__ double hfacz(const Dims &d, const Fields &f, int i, i
   return h;
 }
 
+// h0FacZ (mom_fluxform.F:290-307): from the rest-state h0FacW/S under the non-linear
+// free surface with no-slip walls, else hFacZ
+__device__ __forceinline__ double h0facz(const Dims &d, const Params &p, const Fields &f, int i, int j, int k, int t) {
+  if (!(p.momViscosity && p.no_slip_sides && p.nonlinFreeSurf > 0)) return hfacz(d, f, i, j, k, t);
+  if (i < 2 - d.OLx || j < 2 - d.OLy) return 0.0;
+  return fmin(fmin(f.h0FacW[MG_I3(d, i, j, k, t)], f.h0FacW[MG_I3(d, i, j - 1, k, t)]),
+              fmin(f.h0FacS[MG_I3(d, i, j, k, t)], f.h0FacS[MG_I3(d, i - 1, j, k, t)]));
+}
+
+// MOM_U_DEL2U / MOM_V_DEL2V (pkg/mom_fluxform/mom_u_del2u.F:59-117, mom_v_del2v.F:59-117,
+// cosFac = 1, no OBCS) for one (i,j,k) of 2-OL..sN+OL-1 (0 elsewhere, as the zeroed v4F):
+// the Laplacians of u and v the biharmonic viscous fluxes difference, with the no-slip
+// side-wall term from the rest-state h0Fac (NONLIN_FRSURF).
+__global__ void __launch_bounds__(256) k_del2uv(Dims d, Params p, Fields f) {
+  MG_PLANE(1 - d.OLx, d.nx, 1 - d.OLy, d.ny, z)
+  const int t = d.t0 + z / d.Nr, k = z % d.Nr + 1;
+  const long q3 = MG_I3(d, i, j, k, t);
+  if (i < 2 - d.OLx || i > d.sNx + d.OLx - 1 || j < 2 - d.OLy || j > d.sNy + d.OLy - 1) {
+    f.del2u[q3] = 0.0;
+    f.del2v[q3] = 0.0;
+    return;
+  }
+  const double drF = f.drF[k - 1];
+#define U(ii, jj) f.uVel[MG_I3(d, ii, jj, k, t)]
+#define V(ii, jj) f.vVel[MG_I3(d, ii, jj, k, t)]
+#define G2(a, ii, jj) f.a[MG_I2(d, ii, jj, t)]
+#define G3(a, ii, jj) f.a[MG_I3(d, ii, jj, k, t)]
+  {
+    auto fz = [&](int ii) { return drF * G3(hFacC, ii, j) * G2(dyF, ii, j) * G2(recip_dxF, ii, j) * (U(ii + 1, j) - U(ii, j)) * 1.0; };
+    auto fm = [&](int jj) {
+      return drF * hfacz(d, f, i, jj, k, t) * G2(dxV, i, jj) * G2(recip_dyU, i, jj) * (U(i, jj) - U(i, jj - 1));
+    };
+    double v4 = f.recip_drF[k - 1] * G3(recip_hFacW, i, j) * G2(recip_rAw, i, j) *
+                (fz(i) - fz(i - 1) + fm(j + 1) - fm(j)) * G3(maskW, i, j);
+    if (p.no_slip_sides) {
+      const double hS = G3(h0FacW, i, j) - h0facz(d, p, f, i, j, k, t);
+      const double hN = G3(h0FacW, i, j) - h0facz(d, p, f, i, j + 1, k, t);
+      v4 = v4 - G3(recip_hFacW, i, j) * G2(recip_rAw, i, j) *
+                    (hS * G2(dxV, i, j) * G2(recip_dyU, i, j) + hN * G2(dxV, i, j + 1) * G2(recip_dyU, i, j + 1)) * U(i, j) *
+                    p.sideDragFactor * G3(maskW, i, j);
+    }
+    f.del2u[q3] = v4;
+  }
+  {
+    auto fz = [&](int ii) {
+      return drF * hfacz(d, f, ii, j, k, t) * G2(dyU, ii, j) * G2(recip_dxV, ii, j) * (V(ii, j) - V(ii - 1, j)) * 1.0;
+    };
+    auto fm = [&](int jj) { return drF * G3(hFacC, i, jj) * G2(dxF, i, jj) * G2(recip_dyF, i, jj) * (V(i, jj + 1) - V(i, jj)); };
+    double v4 = f.recip_drF[k - 1] * G3(recip_hFacS, i, j) * G2(recip_rAs, i, j) *
+                (fz(i + 1) - fz(i) + fm(j) - fm(j - 1)) * G3(maskS, i, j);
+    if (p.no_slip_sides) {
+      const double hW = G3(h0FacS, i, j) - h0facz(d, p, f, i, j, k, t);
+      const double hE = G3(h0FacS, i, j) - h0facz(d, p, f, i + 1, j, k, t);
+      v4 = v4 - G3(recip_hFacS, i, j) * G2(recip_rAs, i, j) *
+                    (hW * G2(dyU, i, j) * G2(recip_dxV, i, j) + hE * G2(dyU, i + 1, j) * G2(recip_dxV, i + 1, j)) * V(i, j) *
+                    p.sideDragFactor * G3(maskS, i, j);
+    }
+    f.del2v[q3] = v4;
+  }
+#undef U
+#undef V
+#undef G2
+#undef G3
+}
+
 // CALC_PHI_HYD (calc_phi_hyd.F:175-327, OCEANIC, integr_GeoPot = 2, uniformFreeSurfLev,
-// gravFac = 1, alphaRho = rhoInSitu) on the dynamics range iMin..iMax = 0..sNx+1.
+// gravFac = 1) on the dynamics range iMin..iMax = 0..sNx+1.  alphaRho = rhoInSitu, plus
+// MOM_QUASIHYDROSTATIC's 3-D Coriolis / NH-metric buoyancy (mom_quasihydrostatic.F:76-147,
+// angleCosC = 1, angleSinC = 0), kept in alphaRho for CALC_GRAD_PHI_HYD's r* term;
+// DIAGS_PHI_HYD's totPhiHyd (diags_phi_hyd.F:60-120, phi0surf = 0) for the JMD95P EOS.
 __global__ void __launch_bounds__(256) k_phi_hyd(Dims d, Params p, Fields f) {
   MG_PLANE(0, d.sNx + 2, 0, d.sNy + 2, tz)
   const int t = d.t0 + tz;
   if (i > d.sNx + 1 || j > d.sNy + 1) return;
   const double recip_rhoConst = 1.0 / p.rhoConst;
+  const bool qh = p.quasiHydrostatic && (p.select3dCoriScheme >= 1 || p.useNHMTerms);
+  const bool rstar = p.nonlinFreeSurf > 0 && p.select_rStar > 0;
+  const double scalingFactor = p.rhoConst * p.gravitySign * (1.0 / p.gravity);
+  const long q2 = MG_I2(d, i, j, t);
   double phF = 0.0;
   for (int k = 1; k <= d.Nr; k++) {
     double dRlocM = 0.5 * f.drC[k - 1];
     if (k == 1) dRlocM = f.rF[0] - f.rC[0];
     const double dRlocP = (k == d.Nr) ? (f.rC[k - 1] - f.rF[k]) : 0.5 * f.drC[k];
     const long q3 = MG_I3(d, i, j, k, t);
-    const double a = f.rhoInSitu[q3];
+    double a = f.rhoInSitu[q3];
+    if (qh) {
+      const double u0 = f.uVel[q3], u1 = f.uVel[MG_I3(d, i + 1, j, k, t)];
+      const double v0 = f.vVel[q3], v1 = f.vVel[MG_I3(d, i, j + 1, k, t)];
+      double gW = 0.0;
+      if (p.select3dCoriScheme >= 1) gW = f.fCoriCos[q2] * (1.0 * 0.5 * (u0 + u1) - 0.0 * 0.5 * (v0 + v1));
+      if (p.useNHMTerms) gW = gW + ((u0 * u0 + u1 * u1) + (v0 * v0 + v1 * v1)) * 0.5 * p.recip_rSphere;
+      a = a + scalingFactor * gW;
+    }
+    if (rstar) f.alphaRho[q3] = a;
     const double phC = phF + dRlocM * p.gravity * a * recip_rhoConst;
     phF = phC + dRlocP * p.gravity * a * recip_rhoConst;
     f.phiHydC[q3] = phC;
+    if (p.storePhiHyd4Phys) {
+      double tot;
+      if (rstar && p.nonlinFreeSurf >= 4) {
+        const double dPhiRef = (f.Ro_surf[q2] - f.rC[k - 1]) * p.gravity;
+        tot = phC * f.rStarFacC[q2] + fmax(dPhiRef, 0.0) * (f.rStarFacC[q2] - 1.0) + 0.0;
+      } else {
+        tot = phC + f.Bo_surf[q2] * f.etaN[q2] + 0.0;
+      }
+      f.totPhiHyd[q3] = tot;
+    }
   }
 }
 
@@ -60,6 +151,7 @@ __global__ void __launch_bounds__(256) k_mom_step(Dims d, Params p, Fields f, co
   const double ArDudrFac = p.implicitViscosity ? 0.0 : p.vfFacMom;
   const double fuFac = p.cfFacMom, fvFac = p.cfFacMom;
   const long q2 = MG_I2(d, i, j, t);
+  const bool rstar = p.nonlinFreeSurf > 0 && p.select_rStar > 0;
 
 #define U(ii, jj, kk) f.uVel[MG_I3(d, ii, jj, kk, t)]
 #define V(ii, jj, kk) f.vVel[MG_I3(d, ii, jj, kk, t)]
@@ -69,10 +161,25 @@ __global__ void __launch_bounds__(256) k_mom_step(Dims d, Params p, Fields f, co
 
   // vertical advective flux of momentum through the top of level kk (fVerU/V(kUp)):
   // MOM_CALC_RTRANS + MOM_U/V_ADV_WU/WV (mom_fluxform.F:384-424), select_rStar = 0
+  // r*: MOM_CALC_RTRANS's dWtrans (mom_calc_rtrans.F:91-137): the column sums of the
+  // level-thickness tendency above level kk, in the reference's sequential order
   auto fverU = [&](int kk) -> double {
     if (kk > Nr) return 0.0;
-    const double rTU = 0.5 * (W(i - 1, j, kk) * G2(rA, i - 1, j) + W(i, j, kk) * G2(rA, i, j));
+    double rTU = 0.5 * (W(i - 1, j, kk) * G2(rA, i - 1, j) + W(i, j, kk) * G2(rA, i, j));
     if (kk == 1) return rTU * U(i, j, 1);
+    if (rstar) {
+      double c0 = G2(rStarDhCDt, i - 1, j) * (G2(Ro_surf, i - 1, j) - G2(R_low, i - 1, j)) * G2(rA, i - 1, j);
+      double c1 = G2(rStarDhCDt, i, j) * (G2(Ro_surf, i, j) - G2(R_low, i, j)) * G2(rA, i, j);
+      double dF = 0.5 * (c0 + c1);
+      for (int k2 = 1; k2 <= kk - 1; k2++) {
+        const double drF2 = f.drF[k2 - 1];
+        c0 = c0 - G2(rStarDhCDt, i - 1, j) * drF2 * G3(h0FacC, i - 1, j, k2) * G2(rA, i - 1, j);
+        c1 = c1 - G2(rStarDhCDt, i, j) * drF2 * G3(h0FacC, i, j, k2) * G2(rA, i, j);
+        dF = dF - G2(rStarDhWDt, i, j) * drF2 * G3(h0FacW, i, j, k2) * G2(rAw, i, j);
+      }
+      rTU = rTU - dF + (c0 + c1) * 0.5;
+      return rTU * (0.5 * (U(i, j, kk) + U(i, j, kk - 1)));
+    }
     double fu_ = rTU * (0.5 * (U(i, j, kk) + U(i, j, kk - 1)));
     fu_ = fu_ + 0.25 * (W(i, j, kk) * G2(rA, i, j) * (G3(maskC, i, j, kk) - G3(maskC, i, j, kk - 1)) +
                         W(i - 1, j, kk) * G2(rA, i - 1, j) * (G3(maskC, i - 1, j, kk) - G3(maskC, i - 1, j, kk - 1))) *
@@ -81,8 +188,21 @@ __global__ void __launch_bounds__(256) k_mom_step(Dims d, Params p, Fields f, co
   };
   auto fverV = [&](int kk) -> double {
     if (kk > Nr) return 0.0;
-    const double rTV = 0.5 * (W(i, j - 1, kk) * G2(rA, i, j - 1) + W(i, j, kk) * G2(rA, i, j));
+    double rTV = 0.5 * (W(i, j - 1, kk) * G2(rA, i, j - 1) + W(i, j, kk) * G2(rA, i, j));
     if (kk == 1) return rTV * V(i, j, 1);
+    if (rstar) {
+      double c0 = G2(rStarDhCDt, i, j - 1) * (G2(Ro_surf, i, j - 1) - G2(R_low, i, j - 1)) * G2(rA, i, j - 1);
+      double c1 = G2(rStarDhCDt, i, j) * (G2(Ro_surf, i, j) - G2(R_low, i, j)) * G2(rA, i, j);
+      double dF = 0.5 * (c0 + c1);
+      for (int k2 = 1; k2 <= kk - 1; k2++) {
+        const double drF2 = f.drF[k2 - 1];
+        c0 = c0 - G2(rStarDhCDt, i, j - 1) * drF2 * G3(h0FacC, i, j - 1, k2) * G2(rA, i, j - 1);
+        c1 = c1 - G2(rStarDhCDt, i, j) * drF2 * G3(h0FacC, i, j, k2) * G2(rA, i, j);
+        dF = dF - G2(rStarDhSDt, i, j) * drF2 * G3(h0FacS, i, j, k2) * G2(rAs, i, j);
+      }
+      rTV = rTV - dF + (c0 + c1) * 0.5;
+      return rTV * (0.5 * (V(i, j, kk) + V(i, j, kk - 1)));
+    }
     double fv_ = rTV * (0.5 * (V(i, j, kk) + V(i, j, kk - 1)));
     fv_ = fv_ + 0.25 * (W(i, j, kk) * G2(rA, i, j) * (G3(maskC, i, j, kk) - G3(maskC, i, j, kk - 1)) +
                         W(i, j - 1, kk) * G2(rA, i, j - 1) * (G3(maskC, i, j - 1, kk) - G3(maskC, i, j - 1, kk - 1))) *
@@ -96,9 +216,24 @@ __global__ void __launch_bounds__(256) k_mom_step(Dims d, Params p, Fields f, co
     double dPhiHydX = 0.0, dPhiHydY = 0.0;
     if (inner) {
       // CALC_GRAD_PHI_HYD (calc_grad_phi_hyd.F:152-171), phi0surf = 0
-      const double phC = G3(phiHydC, i, j, k);
-      if (i >= 1) dPhiHydX = G2(recip_dxC, i, j) * ((phC + 0.0) - (G3(phiHydC, i - 1, j, k) + 0.0));
-      if (j >= 1) dPhiHydY = G2(recip_dyC, i, j) * ((phC + 0.0) - (G3(phiHydC, i, j - 1, k) + 0.0));
+      // r* (select_rStar >= 2, nonlinFreeSurf >= 4): varLoc = phiHydC*rStarFacC + phi0surf (:30-47)
+      const bool rsc = rstar && p.select_rStar >= 2 && p.nonlinFreeSurf >= 4;
+      auto varLoc = [&](int ii, int jj) {
+        return rsc ? G3(phiHydC, ii, jj, k) * G2(rStarFacC, ii, jj) + 0.0 : G3(phiHydC, ii, jj, k) + 0.0;
+      };
+      const double vl = varLoc(i, j);
+      if (i >= 1) dPhiHydX = G2(recip_dxC, i, j) * (vl - varLoc(i - 1, j));
+      if (j >= 1) dPhiHydY = G2(recip_dyC, i, j) * (vl - varLoc(i, j - 1));
+      if (rstar && p.select_rStar >= 2) {
+        // calc_grad_phi_hyd.F:173-214 (fluidIsWater, z-coords, generalForm = F)
+        const double factorP = p.gravity * (1.0 / p.rhoConst) * 0.5, rCk = f.rC[k - 1];
+        auto vl2 = [&](int ii, int jj) { return G2(etaH, ii, jj) * (1.0 + rCk * G2(recip_Rcol, ii, jj)); };
+        const double e0 = vl2(i, j), a0 = G3(alphaRho, i, j, k);
+        if (i >= 1)
+          dPhiHydX = dPhiHydX + factorP * (G3(alphaRho, i - 1, j, k) + a0) * (e0 - vl2(i - 1, j)) * G2(recip_dxC, i, j);
+        if (j >= 1)
+          dPhiHydY = dPhiHydY + factorP * (G3(alphaRho, i, j - 1, k) + a0) * (e0 - vl2(i, j - 1)) * G2(recip_dyC, i, j);
+      }
     }
     if (inner) {
       const double rhFacW = G3(recip_hFacW, i, j, k), rhFacS = G3(recip_hFacS, i, j, k);
@@ -122,20 +257,32 @@ __global__ void __launch_bounds__(256) k_mom_step(Dims d, Params p, Fields f, co
         const double gMm = 0.25 * (VTR(i, j - 1) + VTR(i, j)) * (V(i, j - 1, k) + V(i, j, k));
         gV = -rhFacS * recip_drF * G2(recip_rAs, i, j) *
              ((gZp - gZi) * uDudxFac + (gMi - gMm) * vDudyFac + (fVerVkp - fVerVkm) * p.rkSign * rVelDudrFac);
+        if (rstar) {   // mom_fluxform.F:527-548, 787-808
+          gU = gU - (G2(rStarExpW, i, j) - 1.0) / p.deltaTFreeSurf * U(i, j, k);
+          gV = gV - (G2(rStarExpS, i, j) - 1.0) / p.deltaTFreeSurf * V(i, j, k);
+        }
 #undef UTR
 #undef VTR
       }
       // ---------------- viscosity (mom_u/v_x/y/rviscflux.F, sidedrag, botdrag)
       if (p.momViscosity) {
         // U: xviscflux at i and i-1, yviscflux at j+1 and j
+        // v4F = del2u / del2v from k_del2uv (0 without biharmonic viscosity)
+        const bool bh = p.viscA4D != 0.0 || p.viscA4Z != 0.0;
+        auto D2U = [&](int ii, int jj) { return bh ? G3(del2u, ii, jj, k) : 0.0; };
+        auto D2V = [&](int ii, int jj) { return bh ? G3(del2v, ii, jj, k) : 0.0; };
+        const double d2u = D2U(i, j), d2v = D2V(i, j);
         const double fZi = G2(dyF, i, j) * drF * G3(hFacC, i, j, k) *
-                           (-p.viscAhD * (U(i + 1, j, k) - U(i, j, k)) * 1.0 + p.viscA4D * 0.0 * 1.0) * G2(recip_dxF, i, j);
+                           (-p.viscAhD * (U(i + 1, j, k) - U(i, j, k)) * 1.0 + p.viscA4D * (D2U(i + 1, j) - d2u) * 1.0) *
+                           G2(recip_dxF, i, j);
         const double fZm = G2(dyF, i - 1, j) * drF * G3(hFacC, i - 1, j, k) *
-                           (-p.viscAhD * (U(i, j, k) - U(i - 1, j, k)) * 1.0 + p.viscA4D * 0.0 * 1.0) * G2(recip_dxF, i - 1, j);
+                           (-p.viscAhD * (U(i, j, k) - U(i - 1, j, k)) * 1.0 + p.viscA4D * (d2u - D2U(i - 1, j)) * 1.0) *
+                           G2(recip_dxF, i - 1, j);
         const double hZp = hfacz(d, f, i, j + 1, k, t);
-        const double fMp = G2(dxV, i, j + 1) * drF * hZp * (-p.viscAhZ * (U(i, j + 1, k) - U(i, j, k)) + p.viscA4Z * 0.0) *
+        const double fMp = G2(dxV, i, j + 1) * drF * hZp *
+                           (-p.viscAhZ * (U(i, j + 1, k) - U(i, j, k)) + p.viscA4Z * (D2U(i, j + 1) - d2u)) *
                            G2(recip_dyU, i, j + 1);
-        const double fMi = G2(dxV, i, j) * drF * hZ * (-p.viscAhZ * (U(i, j, k) - U(i, j - 1, k)) + p.viscA4Z * 0.0) *
+        const double fMi = G2(dxV, i, j) * drF * hZ * (-p.viscAhZ * (U(i, j, k) - U(i, j - 1, k)) + p.viscA4Z * (d2u - D2U(i, j - 1))) *
                            G2(recip_dyU, i, j);
         double fVrUp = 0.0, fVrDw = 0.0;
         if (k > 1)
@@ -147,12 +294,13 @@ __global__ void __launch_bounds__(256) k_mom_step(Dims d, Params p, Fields f, co
         guDiss = -rhFacW * recip_drF * G2(recip_rAw, i, j) *
                  ((fZi - fZm) * AhDudxFac + (fMp - fMi) * AhDudyFac + (fVrDw - fVrUp) * p.rkSign * ArDudrFac);
         if (p.no_slip_sides) {
-          const double hS = G3(hFacW, i, j, k) - hZ;
-          const double hN = G3(hFacW, i, j, k) - hZp;
+          // MOM_U_SIDEDRAG with NONLIN_FRSURF: h0FacW - h0FacZ (h0Fac = hFac at rest)
+          const double hS = G3(h0FacW, i, j, k) - h0facz(d, p, f, i, j, k, t);
+          const double hN = G3(h0FacW, i, j, k) - h0facz(d, p, f, i, j + 1, k, t);
           const double u0 = U(i, j, k);
           const double vF = -rhFacW * recip_drF * G2(recip_rAw, i, j) *
-                            (hS * G2(dxV, i, j) * G2(recip_dyU, i, j) * (p.viscAhZ * u0 - p.viscA4Z * 0.0) +
-                             hN * G2(dxV, i, j + 1) * G2(recip_dyU, i, j + 1) * (p.viscAhZ * u0 - p.viscA4Z * 0.0)) *
+                            (hS * G2(dxV, i, j) * G2(recip_dyU, i, j) * (p.viscAhZ * u0 - p.viscA4Z * d2u) +
+                             hN * G2(dxV, i, j + 1) * G2(recip_dyU, i, j + 1) * (p.viscAhZ * u0 - p.viscA4Z * d2u)) *
                             drF * p.sideDragFactor;
           guDiss = guDiss + vF;
         }
@@ -166,14 +314,17 @@ __global__ void __launch_bounds__(256) k_mom_step(Dims d, Params p, Fields f, co
         }
         // V: xviscflux at i+1 and i, yviscflux at j and j-1
         const double hZe = hfacz(d, f, i + 1, j, k, t);
-        const double gZp = G2(dyU, i + 1, j) * drF * hZe * (-p.viscAhZ * (V(i + 1, j, k) - V(i, j, k)) * 1.0 + p.viscA4Z * 0.0 * 1.0) *
+        const double gZp = G2(dyU, i + 1, j) * drF * hZe *
+                           (-p.viscAhZ * (V(i + 1, j, k) - V(i, j, k)) * 1.0 + p.viscA4Z * (D2V(i + 1, j) - d2v) * 1.0) *
                            G2(recip_dxV, i + 1, j);
-        const double gZi = G2(dyU, i, j) * drF * hZ * (-p.viscAhZ * (V(i, j, k) - V(i - 1, j, k)) * 1.0 + p.viscA4Z * 0.0 * 1.0) *
+        const double gZi = G2(dyU, i, j) * drF * hZ *
+                           (-p.viscAhZ * (V(i, j, k) - V(i - 1, j, k)) * 1.0 + p.viscA4Z * (d2v - D2V(i - 1, j)) * 1.0) *
                            G2(recip_dxV, i, j);
-        const double gMi = G2(dxF, i, j) * drF * G3(hFacC, i, j, k) * (-p.viscAhD * (V(i, j + 1, k) - V(i, j, k)) + p.viscA4D * 0.0) *
-                           G2(recip_dyF, i, j);
+        const double gMi = G2(dxF, i, j) * drF * G3(hFacC, i, j, k) *
+                           (-p.viscAhD * (V(i, j + 1, k) - V(i, j, k)) + p.viscA4D * (D2V(i, j + 1) - d2v)) * G2(recip_dyF, i, j);
         const double gMm = G2(dxF, i, j - 1) * drF * G3(hFacC, i, j - 1, k) *
-                           (-p.viscAhD * (V(i, j, k) - V(i, j - 1, k)) + p.viscA4D * 0.0) * G2(recip_dyF, i, j - 1);
+                           (-p.viscAhD * (V(i, j, k) - V(i, j - 1, k)) + p.viscA4D * (d2v - D2V(i, j - 1))) *
+                           G2(recip_dyF, i, j - 1);
         double gVrUp = 0.0, gVrDw = 0.0;
         if (k > 1)
           gVrUp = -p.viscAr * G2(rAs, i, j) * (V(i, j, k) - V(i, j, k - 1)) * p.rkSign * f.recip_drC[k - 1] *
@@ -184,12 +335,12 @@ __global__ void __launch_bounds__(256) k_mom_step(Dims d, Params p, Fields f, co
         gvDiss = -rhFacS * recip_drF * G2(recip_rAs, i, j) *
                  ((gZp - gZi) * AhDudxFac + (gMi - gMm) * AhDudyFac + (gVrDw - gVrUp) * p.rkSign * ArDudrFac);
         if (p.no_slip_sides) {
-          const double hW = G3(hFacS, i, j, k) - hZ;
-          const double hE = G3(hFacS, i, j, k) - hZe;
+          const double hW = G3(h0FacS, i, j, k) - h0facz(d, p, f, i, j, k, t);
+          const double hE = G3(h0FacS, i, j, k) - h0facz(d, p, f, i + 1, j, k, t);
           const double v0 = V(i, j, k);
           const double vF = -rhFacS * recip_drF * G2(recip_rAs, i, j) *
-                            (hW * G2(dyU, i, j) * G2(recip_dxV, i, j) * (p.viscAhZ * v0 - p.viscA4Z * 0.0) +
-                             hE * G2(dyU, i + 1, j) * G2(recip_dxV, i + 1, j) * (p.viscAhZ * v0 - p.viscA4Z * 0.0)) *
+                            (hW * G2(dyU, i, j) * G2(recip_dxV, i, j) * (p.viscAhZ * v0 - p.viscA4Z * d2v) +
+                             hE * G2(dyU, i + 1, j) * G2(recip_dxV, i + 1, j) * (p.viscAhZ * v0 - p.viscA4Z * d2v)) *
                             drF * p.sideDragFactor;
           gvDiss = gvDiss + vF;
         }
@@ -203,6 +354,15 @@ __global__ void __launch_bounds__(256) k_mom_step(Dims d, Params p, Fields f, co
         }
       }
       // ---------------- spherical metric terms (mom_u/v_metric_sphere.F, mom_fluxform.F:714-721, 973-980)
+      if (p.useNHMTerms) {
+        // MOM_U/V_METRIC_NH (pkg/mom_common/mom_u_metric_nh.F:56-68, mom_v_metric_nh.F), mtNHFac = 1
+        const int kp1 = k + 1 < Nr ? k + 1 : Nr;
+        const double ov = (k == Nr) ? 0.0 : 1.0;
+        gU = gU + 1.0 * (U(i, j, k) * p.recip_rSphere * 0.25 *
+                         ((W(i - 1, j, kp1) + W(i, j, kp1)) * ov + (W(i - 1, j, k) + W(i, j, k))) * p.gravitySign);
+        gV = gV + 1.0 * (V(i, j, k) * p.recip_rSphere * 0.25 *
+                         ((W(i, j - 1, kp1) + W(i, j, kp1)) * ov + (W(i, j - 1, k) + W(i, j, k))) * p.gravitySign);
+      }
       if (p.metricSphere) {
         const double mTu = U(i, j, k) * p.recip_rSphere * 0.25 *
                            (V(i, j, k) + V(i - 1, j, k) + V(i, j + 1, k) + V(i - 1, j + 1, k)) * G2(tanPhiAtU, i, j);
@@ -234,6 +394,16 @@ __global__ void __launch_bounds__(256) k_mom_step(Dims d, Params p, Fields f, co
         if (sc == 1 || sc == 3)
           c = c * 4.0 / fmax(1.0, G3(maskW, i, j, k) + G3(maskW, i + 1, j, k) + G3(maskW, i, j - 1, k) + G3(maskW, i + 1, j - 1, k));
         gV = gV + fvFac * c;
+      }
+      if (p.select3dCoriScheme >= 1) {
+        // MOM_U_CORIOLIS_NH (pkg/mom_common/mom_u_coriolis_nh.F:60-76), angleCosC = 1; the V
+        // component only on curvilinear / rotated grids (mom_fluxform.F:1025-1040)
+        const int kp1 = k + 1 < Nr ? k + 1 : Nr;
+        const double wMsk = (k == Nr) ? 0.0 : 1.0;
+        const double c = 0.5 * (G2(fCoriCos, i, j) * 1.0 * 0.5 * (W(i, j, k) + W(i, j, kp1) * wMsk) +
+                                G2(fCoriCos, i - 1, j) * 1.0 * 0.5 * (W(i - 1, j, k) + W(i - 1, j, kp1) * wMsk)) *
+                         p.gravitySign;
+        gU = gU + fuFac * c;
       }
       // mom_fluxform.F:1044-1051
       gU = gU * G3(maskW, i, j, k);
@@ -274,6 +444,10 @@ __global__ void __launch_bounds__(256) k_mom_step(Dims d, Params p, Fields f, co
       if (p.momForcing && p.momForcingOutAB == 1) { gUtmp = gUtmp + guExt; gVtmp = gVtmp + gvExt; }
       if (p.momViscosity && !p.momDissip_In_AB) { gUtmp = gUtmp + guDiss; gVtmp = gVtmp + gvDiss; }
       if (!p.useCDscheme) {
+        if (rstar && p.nonlinFreeSurf > 1) {   // timestep.F:274-284
+          gUtmp = gUtmp / G2(rStarExpW, i, j);
+          gVtmp = gVtmp / G2(rStarExpS, i, j);
+        }
         // u* = u + dt*(gUtmp + gUdPx)*maskW  (timestep.F:373-388), gUdPx = 0 for implicSurfPress = 1
         gU = U(i, j, k) + p.deltaTMom * (gUtmp + 0.0) * G3(maskW, i, j, k);
         gV = V(i, j, k) + p.deltaTMom * (gVtmp + 0.0) * G3(maskS, i, j, k);
@@ -335,7 +509,11 @@ __global__ void __launch_bounds__(256) k_cd_scheme(Dims d, Params p, Fields f, c
   f.uVelD[q3] = uD;
   const double gvCor = -(G2(fCori, i, j) + G2(fCori, i, j - 1)) * 0.5 * uD * p.cfFacMom;
   if (i >= 0 && i <= d.sNx + 1 && j >= 0 && j <= d.sNy + 1) {
-    const double gUtmp = f.cdU[q3] + guCor, gVtmp = f.cdV[q3] + gvCor;
+    double gUtmp = f.cdU[q3] + guCor, gVtmp = f.cdV[q3] + gvCor;
+    if (p.nonlinFreeSurf > 1 && p.select_rStar > 0) {   // timestep.F:274-284
+      gUtmp = gUtmp / G2(rStarExpW, i, j);
+      gVtmp = gVtmp / G2(rStarExpS, i, j);
+    }
     f.gU[q3] = G3(uVel, i, j, k) + p.deltaTMom * (gUtmp + 0.0) * G3(maskW, i, j, k);
     f.gV[q3] = G3(vVel, i, j, k) + p.deltaTMom * (gVtmp + 0.0) * G3(maskS, i, j, k);
   }
@@ -345,6 +523,8 @@ __global__ void __launch_bounds__(256) k_cd_scheme(Dims d, Params p, Fields f, c
 
 hipError_t launch_mom_step(const Dims &d, const Params &p, const Fields &f, const int *iterPtr, hipStream_t s) {
   hipLaunchKernelGGL(k_phi_hyd, dim3(mg_plane_blocks(d.sNx + 2, d.sNy + 2, d.nT)), dim3(MG_PLANE_THREADS), 0, s, d, p, f);
+  if (p.momViscosity && (p.viscA4D != 0.0 || p.viscA4Z != 0.0))
+    hipLaunchKernelGGL(k_del2uv, dim3(mg_plane_blocks(d.nx, d.ny, d.nT * d.Nr)), dim3(MG_PLANE_THREADS), 0, s, d, p, f);
   hipLaunchKernelGGL(k_mom_step, dim3(mg_plane_blocks(d.nx, d.ny, d.nT * d.Nr)), dim3(MG_PLANE_THREADS), 0, s, d, p, f, iterPtr);
   if (p.useCDscheme)
     hipLaunchKernelGGL(k_cd_scheme, dim3(mg_plane_blocks(d.nx - 2, d.ny - 2, d.nT * d.Nr)), dim3(MG_PLANE_THREADS), 0, s,

@@ -1038,9 +1038,12 @@ __global__ void __launch_bounds__(256) k_exch_eta(Dims d, Fields f, const long *
 
 // exactConserv end of INTEGR_CONTINUITY: EXCH_XY_RL of the new eta (held in cg2d_b
 // by k_corr_cont) into etaN, and UPDATE_ETAH (etaH = etaN) in one pass.
-__global__ void __launch_bounds__(256) k_exch_etaH(Dims d, Fields f, const long *__restrict__ srcOf) {
+// Under the non-linear free surface with real fresh-water flux (not at initialisation)
+// PmEpR = -EmPmR over the whole tile (integr_continuity.F:137-143) is set here too.
+__global__ void __launch_bounds__(256) k_exch_etaH(Dims d, Params p, Fields f, const long *__restrict__ srcOf, int atInit) {
   const long q = (long)blockIdx.x * blockDim.x + threadIdx.x;
   if (q >= d.n2 * d.nTiles) return;
+  if (!atInit && p.nonlinFreeSurf > 0 && p.useRealFreshWaterFlux) f.PmEpR[q] = -f.EmPmR[q];
   const long sq = srcOf[q];
   const double *e = f.cg2d_b;
   double x;
@@ -1060,12 +1063,28 @@ __global__ void __launch_bounds__(256) k_exch_etaH(Dims d, Fields f, const long 
 // east/north neighbours' corrected velocities recomputed inline (identical
 // expressions), then exactConserv's eta (into cg2d_b, see k_exch_etaH) and
 // INTEGRATE_FOR_W.  Halo velocities are left to the end-of-step EXCH.
-__global__ void __launch_bounds__(256) k_corr_cont(Dims d, Params p, Fields f) {
-  __shared__ double sDiv[256], sMask[256];
+// atInit: the INTEGR_CONTINUITY call of INITIALISE_VARIA (myIter = nIter0): no
+// correction (uVel, vVel as they are), dEtaHdt / PmEpR per integr_continuity.F:117-152,
+// no eta update (cg2d_b = etaN, so k_exch_etaH makes etaH = etaN: UPDATE_ETAH).
+// r* (select_rStar > 0): w includes -rStarDhDt*drF*h0FacC (integrate_for_w.F:117-140).
+__global__ void __launch_bounds__(256) k_corr_cont(Dims d, Params p, Fields f, int atInit) {
+  __shared__ double sDiv[256], sMask[256], sH0[256];
   MG_COLS(1, d.sNx, 1, d.sNy, d.Nr)
   const int k = kk + 1, me = kk * NC_ + cc;
   const long q = MG_I2(d, i, j, t);
-  if (valid && k <= d.Nr) {
+  const bool rstar = p.nonlinFreeSurf > 0 && p.select_rStar != 0;
+  if (valid && k <= d.Nr && atInit) {
+    const double drF = f.drF[k - 1];
+    const double u0 = f.uVel[MG_I3(d, i, j, k, t)], u1 = f.uVel[MG_I3(d, i + 1, j, k, t)];
+    const double v0 = f.vVel[MG_I3(d, i, j, k, t)], v1 = f.vVel[MG_I3(d, i, j + 1, k, t)];
+    const double uT1 = u1 * f.dyG[MG_I2(d, i + 1, j, t)] * drF * f.hFacW[MG_I3(d, i + 1, j, k, t)];
+    const double uT0 = u0 * f.dyG[q] * drF * f.hFacW[MG_I3(d, i, j, k, t)];
+    const double vT1 = v1 * f.dxG[MG_I2(d, i, j + 1, t)] * drF * f.hFacS[MG_I3(d, i, j + 1, k, t)];
+    const double vT0 = v0 * f.dxG[q] * drF * f.hFacS[MG_I3(d, i, j, k, t)];
+    sDiv[me] = uT1 - uT0 + vT1 - vT0;
+    sMask[me] = f.maskC[MG_I3(d, i, j, k, t)];
+    sH0[me] = rstar ? f.h0FacC[MG_I3(d, i, j, k, t)] : 0.0;
+  } else if (valid && k <= d.Nr) {
     const double psFac = p.pfFacMom * p.implicSurfPress;
     auto phiX = [&](int ii, int jj) {
       const long qq = MG_I2(d, ii, jj, t);
@@ -1096,23 +1115,47 @@ __global__ void __launch_bounds__(256) k_corr_cont(Dims d, Params p, Fields f) {
     const double vT0 = v0 * f.dxG[q] * drF * f.hFacS[MG_I3(d, i, j, k, t)];
     sDiv[me] = uT1 - uT0 + vT1 - vT0;
     sMask[me] = f.maskC[MG_I3(d, i, j, k, t)];
+    sH0[me] = rstar ? f.h0FacC[MG_I3(d, i, j, k, t)] : 0.0;
   }
   __syncthreads();
   if (valid && kk == 0) {
+    double rStarDhDt = 0.0;
     if (p.exactConserv) {
       double hDiv = 0.0;
       for (int k2 = 1; k2 <= d.Nr; k2++) hDiv = hDiv + sMask[(k2 - 1) * NC_ + cc] * sDiv[(k2 - 1) * NC_ + cc];
-      const double facEmP = p.useRealFreshWaterFlux ? 1.0 / p.rhoConst : 0.0;   // integr_continuity.F:183-188
-      const double dEtaHdt = -(hDiv * f.recip_rA[q]) - facEmP * f.EmPmR[q];
-      f.cg2d_b[q] = f.etaH[q] + p.implicDiv2DFlow * dEtaHdt * p.deltaTFreeSurf;
+      double dEtaHdt;
+      if (atInit && p.nIter0 != 0 && p.useRealFreshWaterFlux) {
+        // integr_continuity.F:117-136: PmEpR consistent with the pickup's dEtaHdt
+        dEtaHdt = f.dEtaHdt[q];
+        double pm = dEtaHdt + hDiv * f.recip_rA[q];
+        f.PmEpR[q] = pm * p.rhoConst;
+        f.cg2d_b[q] = f.etaN[q];
+      } else if (atInit) {
+        dEtaHdt = -(hDiv * f.recip_rA[q]);
+        if (f.PmEpR) f.PmEpR[q] = 0.0;
+        f.cg2d_b[q] = f.etaN[q];
+      } else {
+        const double facEmP = p.useRealFreshWaterFlux ? 1.0 / p.rhoConst : 0.0;   // integr_continuity.F:183-188
+        dEtaHdt = -(hDiv * f.recip_rA[q]) - facEmP * f.EmPmR[q];
+        f.cg2d_b[q] = f.etaH[q] + p.implicDiv2DFlow * dEtaHdt * p.deltaTFreeSurf;
+      }
+      if (f.dEtaHdt) f.dEtaHdt[q] = dEtaHdt;
+      if (rstar) rStarDhDt = dEtaHdt * f.recip_Rcol[q];   // integr_continuity.F:171-183
     }
     double wBelow = 0.0;
     for (int k2 = d.Nr; k2 >= 1; k2--) {
       const int s2 = (k2 - 1) * NC_ + cc;
       const double conv2d = -sDiv[s2];
       double w;
-      if (k2 == d.Nr) w = conv2d * f.recip_rA[q] * sMask[s2];
-      else w = (wBelow + conv2d * f.recip_rA[q]) * sMask[s2];
+      if (rstar) {
+        const double dh = rStarDhDt * f.drF[k2 - 1] * sH0[s2];
+        if (k2 == d.Nr) w = (conv2d * f.recip_rA[q] - dh) * sMask[s2];
+        else w = (wBelow + conv2d * f.recip_rA[q] - dh) * sMask[s2];
+      } else if (k2 == d.Nr) {
+        w = conv2d * f.recip_rA[q] * sMask[s2];
+      } else {
+        w = (wBelow + conv2d * f.recip_rA[q]) * sMask[s2];
+      }
       sDiv[s2] = w;
       wBelow = w;
     }
@@ -1264,16 +1307,17 @@ hipError_t launch_exchange_multi(const Dims &d, const XFields &x, const long *ma
   return hipGetLastError();
 }
 
-hipError_t launch_exch_eta(const Dims &d, const Fields &f, const long *srcOf, bool etaH, hipStream_t s) {
+hipError_t launch_exch_eta(const Dims &d, const Params &p, const Fields &f, const long *srcOf, bool etaH, int atInit,
+                           hipStream_t s) {
   const long n = d.n2 * d.nTiles;
-  if (etaH) hipLaunchKernelGGL(k_exch_etaH, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, d, f, srcOf);
+  if (etaH) hipLaunchKernelGGL(k_exch_etaH, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, d, p, f, srcOf, atInit);
   else hipLaunchKernelGGL(k_exch_eta, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, d, f, srcOf);
   return hipGetLastError();
 }
 
-hipError_t launch_corr_cont(const Dims &d, const Params &p, const Fields &f, hipStream_t s) {
+hipError_t launch_corr_cont(const Dims &d, const Params &p, const Fields &f, int atInit, hipStream_t s) {
   const dim3 blk(256), grd(mg_col_blocks(d.sNx, d.sNy, d.nT, d.Nr));
-  hipLaunchKernelGGL(k_corr_cont, grd, blk, 0, s, d, p, f);
+  hipLaunchKernelGGL(k_corr_cont, grd, blk, 0, s, d, p, f, atInit);
   return hipGetLastError();
 }
 

@@ -51,8 +51,16 @@ __device__ __forceinline__ double jmd95_rho(const Params &p, double locPres, dou
   const double bulkMod = bMfresh + bMsalt + bMpres;
   return rhoP0 / (1.0 - locPres * 1.0e-05 / bulkMod) - p.rhoConst;
 }
-__device__ __forceinline__ double find_rho(const Params &p, const Fields &f, int kRef, double t, double s) {
-  if (p.eosType == 1) return jmd95_rho(p, f.pRef4EOS[kRef - 1] + 0.0, t, s);
+// PRESSURE_FOR_EOS (pressure_for_eos.F:51-105), z-coordinates, dpRef = 0: JMD95P
+// (selectP_inEOS_Zc = 2) uses the hydrostatic pressure rhoConst*(totPhiHyd + phiRef(2k))
+// of the point q3 (level kRef); JMD95Z the reference profile pRef4EOS(kRef).
+__device__ __forceinline__ double pressure_for_eos(const Params &p, const Fields &f, int kRef, long q3) {
+  if (p.selectP_inEOS_Zc == 2) return p.rhoConst * (f.totPhiHyd[q3] + f.phiRefC[kRef - 1]) + 0.0;
+  return f.pRef4EOS[kRef - 1] + 0.0;
+}
+// q3: flat offset of the point at level kRef (for the JMD95P pressure)
+__device__ __forceinline__ double find_rho(const Params &p, const Fields &f, int kRef, long q3, double t, double s) {
+  if (p.eosType == 1) return jmd95_rho(p, pressure_for_eos(p, f, kRef, q3), t, s);
   const double refTemp = f.tRef[kRef - 1], refSalt = f.sRef[kRef - 1];
   const double dRho = p.rhoNil - p.rhoConst;
   return p.rhoNil * (p.sBeta * (s - refSalt) - p.tAlpha * (t - refTemp)) + dRho;
@@ -106,7 +114,11 @@ __global__ void __launch_bounds__(256) k_oceanic_phys(Dims d, Params p, Fields f
     sfT = sfT - f.Qnet[q] * recip_Cp * mass2rUnit;
     sfS = sfS - 0.0 * mass2rUnit;   // saltFlux = 0
     const double UNSET_RL = 123456.7;
-    if (p.convertFW2Salt == -1.0) {
+    if (p.nonlinFreeSurf > 0 && p.useRealFreshWaterFlux) {
+      // external_forcing_surf.F:253-277: PmEpR changes the column height
+      if (p.temp_EvPrRn != UNSET_RL) sfT = sfT + f.PmEpR[q] * (p.temp_EvPrRn - th1) * mass2rUnit;
+      if (p.salt_EvPrRn != UNSET_RL) sfS = sfS + f.PmEpR[q] * (p.salt_EvPrRn - s1) * mass2rUnit;
+    } else if (p.convertFW2Salt == -1.0) {
       if (p.temp_EvPrRn != UNSET_RL) sfT = sfT + f.EmPmR[q] * (th1 - p.temp_EvPrRn) * mass2rUnit;
       if (p.salt_EvPrRn != UNSET_RL) sfS = sfS + f.EmPmR[q] * (s1 - p.salt_EvPrRn) * mass2rUnit;
     } else {
@@ -117,13 +129,13 @@ __global__ void __launch_bounds__(256) k_oceanic_phys(Dims d, Params p, Fields f
     f.surfaceForcingS[q] = sfS;
   }
   const long q3 = MG_I3(d, i, j, k, t);
-  const double rho = find_rho(p, f, k, theta_at(k), f.salt[q3]);
+  const double rho = find_rho(p, f, k, q3, theta_at(k), f.salt[q3]);
   f.rhoInSitu[q3] = rho;
   const bool calcConvect = p.ivdc_kappa != 0.0;
   double conv = 0.0, sigmaR = 0.0;
   if (k >= 2 && (calcConvect || p.useGMRedi)) {
     const long q3u = MG_I3(d, i, j, k - 1, t);
-    const double rhoKm1 = find_rho(p, f, k, theta_at(k - 1), f.salt[q3u]);
+    const double rhoKm1 = find_rho(p, f, k, q3, theta_at(k - 1), f.salt[q3u]);
     sigmaR = f.maskC[q3] * f.maskC[q3u] * f.recip_drC[k - 1] * p.rkSign * (rho - rhoKm1);
     if (calcConvect) conv = (-sigmaR * p.gravitySign > 0.0) ? 1.0 : 0.0;
   }
@@ -408,9 +420,13 @@ __global__ void __launch_bounds__(256) k_tracer_rhs(Dims d, Params p, Fields f, 
   gT = gT + gtForc;
   if (a.useAB) {   // ADAMS_BASHFORTH2(k)
     const double ab = abFac * (gT - a.gNm1[q3]);
-    a.gNm1[q3] = gT;
+    double gN = gT;
     gT = gT + ab;
+    // FREESURF_RESCALE_G of gT and gtNm1 under r* (temp_integrate.F:412-446)
+    if (p.nonlinFreeSurf > 0 && p.select_rStar > 0) gN = gN / f.rStarExpC[q];
+    a.gNm1[q3] = gN;
   }
+  if (p.nonlinFreeSurf > 0 && p.select_rStar > 0) gT = gT / f.rStarExpC[q];
   // TIMESTEP_TRACER
   const double v = Tk + p.deltaTtracer * gT;
   if (p.implicitDiffusion) f.gTscr[q3] = v;
@@ -436,7 +452,10 @@ __global__ void __launch_bounds__(256) k_tracer_impl(Dims d, Params p, Fields f,
 #define G3(a_, ii, jj, kk_) f.a_[MG_I3(d, ii, jj, kk_, t)]
   if (valid && k <= Nr) {
     const long q3 = MG_I3(d, i, j, k, t);
-    const double rh = f.recip_hFacC[q3], rdrF = f.recip_drF[k - 1];
+    // recip_hFacNew (thermodynamics.F:198-210): recip_hFacC/rStarExpC under r*
+    const double rh = (p.nonlinFreeSurf > 0 && p.select_rStar > 0) ? f.recip_hFacC[q3] / f.rStarExpC[MG_I2(d, i, j, t)]
+                                                                    : f.recip_hFacC[q3];
+    const double rdrF = f.recip_drF[k - 1];
     const double mIn = f.maskInC[MG_I2(d, i, j, t)];
     // KappaRT = (IVDConvCount*ivdc_kappa + BL79(=0)) + diffKrNr [+ Kwz*maskInC] (calc_3d_diffusivity.F)
     auto kappa = [&](int k_) {

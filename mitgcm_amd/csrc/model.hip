@@ -37,8 +37,10 @@ hipError_t launch_correction(const Dims &, const Params &, const Fields &, hipSt
 hipError_t launch_continuity(const Dims &, const Fields &, hipStream_t);
 hipError_t launch_bump_counter(int *, int, hipStream_t);
 hipError_t launch_exchange_multi(const Dims &, const XFields &, const long *, int, int *, hipStream_t);
-hipError_t launch_exch_eta(const Dims &, const Fields &, const long *, bool, hipStream_t);
-hipError_t launch_corr_cont(const Dims &, const Params &, const Fields &, hipStream_t);
+hipError_t launch_exch_eta(const Dims &, const Params &, const Fields &, const long *, bool, int, hipStream_t);
+hipError_t launch_corr_cont(const Dims &, const Params &, const Fields &, int, hipStream_t);
+hipError_t launch_calc_r_star(const Dims &, const Params &, const Fields &, const long *, hipStream_t);
+hipError_t launch_update_r_star_cg2d(const Dims &, const Params &, const Fields &, const long *, hipStream_t);
 hipError_t launch_halo_pack(const Dims &, const XFields &, const long *, long, double *, int, hipStream_t);
 hipError_t launch_oceanic_phys(const Dims &, const Params &, const Fields &, const int *, hipStream_t);
 hipError_t launch_tracer_step(const Dims &, const Params &, const Fields &, const TracerArgs &, const int *, hipStream_t);
@@ -93,6 +95,11 @@ static const FieldDesc FIELDS[] = {
     FD(pRef4EOS, F1D), FD(forcRec, FREC), FD(Qnet, F2D), FD(EmPmR, F2D), FD(SSS, F2D), FD(lambdaSaltClimRelax, F2D),
     FD(etaNm1, F2D), FD(sigmaR, F3D), FD(Kwx, F3D), FD(Kwy, F3D), FD(Kwz, F3D), FD(Kux, F3D), FD(Kvy, F3D),
     FD(uVelD, F3D), FD(vVelD, F3D), FD(uNM1, F3D), FD(vNM1, F3D), FD(cdU, F3D), FD(cdV, F3D),
+    FD(h0FacC, F3D), FD(h0FacW, F3D), FD(h0FacS, F3D), FD(fCoriCos, F2D), FD(recip_Rcol, F2D), FD(rSurfW, F2D),
+    FD(rSurfS, F2D), FD(rLowW, F2D), FD(rLowS, F2D), FD(Ro_surf, F2D), FD(R_low, F2D), FD(phiRefC, F1D),
+    FD(totPhiHyd, F3D), FD(alphaRho, F3D), FD(del2u, F3D), FD(del2v, F3D), FD(rStarFacC, F2D), FD(rStarFacW, F2D),
+    FD(rStarFacS, F2D), FD(rStarExpC, F2D), FD(rStarExpW, F2D), FD(rStarExpS, F2D), FD(rStarDhCDt, F2D),
+    FD(rStarDhWDt, F2D), FD(rStarDhSDt, F2D), FD(PmEpR, F2D), FD(dEtaHdt, F2D),
 };
 #undef FD
 
@@ -119,14 +126,16 @@ static const PDesc PARAMS[] = {
     PI_(periodicExternalForcing), PI_(nForcRec), PD(HeatCapacity_Cp), PD(convertFW2Salt), PD(temp_EvPrRn),
     PD(salt_EvPrRn), PD(rCD), PD(epsAB_CD), PD(externForcingPeriod), PD(externForcingCycle), PD(GM_background_K),
     PD(GM_isopycK), PD(GM_skewflx), PD(GM_maxSlope), PD(GM_Kmin_horiz), PD(GM_Small_Number), PD(GM_slopeSqCutoff),
+    PI_(nonlinFreeSurf), PI_(select_rStar), PI_(quasiHydrostatic), PI_(useNHMTerms), PI_(select3dCoriScheme),
+    PI_(selectP_inEOS_Zc), PI_(storePhiHyd4Phys), PD(hFacInf),
 };
 #undef PD
 #undef PI_
 
 // kernel families timed with hipEvents when timing is enabled
-enum Kern { K_MOM, K_RHS, K_CG2D, K_EXCH, K_ETA, K_CORR, K_CONT, K_PHYS, K_TEMP, K_N };
-static const char *KNAMES[K_N] = {"mom_step", "sfp_rhs",    "cg2d",         "exchange", "eta_update",
-                                  "correction", "continuity", "oceanic_phys", "temp_step"};
+enum Kern { K_MOM, K_RHS, K_CG2D, K_EXCH, K_ETA, K_CORR, K_CONT, K_PHYS, K_TEMP, K_RSTAR, K_N };
+static const char *KNAMES[K_N] = {"mom_step",   "sfp_rhs",    "cg2d",         "exchange",  "eta_update",
+                                  "correction", "continuity", "oceanic_phys", "temp_step", "r_star"};
 
 struct mgcm_model {
   Dims d{};
@@ -536,9 +545,7 @@ int mgcm_set_param(mgcm_model *m, const char *name, double value) {
     }
   // options the kernels do not implement are accepted only at their default
   // (inert) value; anything else is an explicit error, never silently ignored.
-  static const char *inert[] = {"useBiharmonicVisc", "nonlinFreeSurf", "select_rStar",
-                                "vectorInvariantMomentum", "useNHMTerms", "staggerTimeStep",
-                                "implicitFreeSurface"};
+  static const char *inert[] = {"vectorInvariantMomentum", "staggerTimeStep", "implicitFreeSurface"};
   for (auto *n : inert)
     if (!strcmp(n, name)) {
       const bool isDefaultOff = (value == 0.0) || (!strcmp(n, "implicitFreeSurface") && value == 1.0);
@@ -620,8 +627,18 @@ int mgcm_init(mgcm_model *m) {
   if (m->nPts > cg2d_block_max_points())
     return set_err("mgcm_init: %d CG2D points per GPU exceed the single-workgroup solver (%d); "
                    "the multi-workgroup solver is not built yet", m->nPts, cg2d_block_max_points());
-  if (m->p.viscA4D != 0.0 || m->p.viscA4Z != 0.0)
-    return set_err("mgcm_init: biharmonic viscosity is not supported by the device path yet");
+  if ((m->p.viscA4D != 0.0 || m->p.viscA4Z != 0.0) && (m->d.OLx < 3 || m->d.OLy < 3))
+    return set_err("mgcm_init: biharmonic viscosity needs OLx, OLy >= 3 (del2u of the halo ring)");
+  const bool rstar = m->p.nonlinFreeSurf > 0;
+  if (rstar) {
+    if (m->p.nonlinFreeSurf != 4 || m->p.select_rStar != 2)
+      return set_err("mgcm_init: the non-linear free surface is implemented for nonlinFreeSurf=4, select_rStar=2 only");
+    if (!m->p.exactConserv) return set_err("mgcm_init: nonlinFreeSurf needs exactConserv");
+    if (m->d.nT != m->d.nTiles) return set_err("mgcm_init: r* is not implemented for tile-sharded runs yet");
+  }
+  if (m->p.selectP_inEOS_Zc > 2) return set_err("mgcm_init: selectP_inEOS_Zc = 3 needs the non-hydrostatic pressure");
+  if (m->p.selectP_inEOS_Zc == 2 && !m->p.storePhiHyd4Phys)
+    return set_err("mgcm_init: selectP_inEOS_Zc = 2 needs storePhiHyd4Phys (set_parms.F:297)");
   if (m->p.implicitViscosity) return set_err("mgcm_init: implicitViscosity not supported by the device path yet");
   if (m->p.implicSurfPress != 1.0 || m->p.implicDiv2DFlow != 1.0)
     return set_err("mgcm_init: implicSurfPress/implicDiv2DFlow != 1 not supported yet");
@@ -649,8 +666,20 @@ int mgcm_init(mgcm_model *m) {
   m->useGraph = getenv("MGCM_NO_GRAPH") == nullptr;
   int it0 = m->p.nIter0;
   HIPCHK(hipMemcpy(m->d_ctr, &it0, sizeof(int), hipMemcpyHostToDevice));
-  // INI_PSURF (ini_psurf.F:84): etaH = etaN
-  HIPCHK(hipMemcpy(m->f.etaH, m->f.etaN, m->d.n2 * m->d.nTiles * sizeof(double), hipMemcpyDeviceToDevice));
+  // INI_PSURF (ini_psurf.F:84) on a cold start: etaH = etaN (a pickup holds etaH)
+  if (m->p.nIter0 == 0)
+    HIPCHK(hipMemcpy(m->f.etaH, m->f.etaN, m->d.n2 * m->d.nTiles * sizeof(double), hipMemcpyDeviceToDevice));
+  if (rstar) {
+    // INITIALISE_VARIA (initialise_varia.F:299-349): CALC_R_STAR(etaH) -> UPDATE_R_STAR ->
+    // UPDATE_CG2D -> INTEGR_CONTINUITY(nIter0) (+ UPDATE_ETAH, EXCH w) -> CALC_R_STAR(etaH)
+    HIPCHK(launch_calc_r_star(m->d, m->p, m->f, m->d_srcOf, m->stream));
+    HIPCHK(launch_update_r_star_cg2d(m->d, m->p, m->f, m->d_srcOf, m->stream));
+    HIPCHK(launch_corr_cont(m->d, m->p, m->f, 1, m->stream));
+    HIPCHK(launch_exch_eta(m->d, m->p, m->f, m->d_srcOf, true, 1, m->stream));
+    HIPCHK(launch_exchange(m->d, m->f.wVel, m->d_halo, m->nHalo, m->d.Nr, m->stream));
+    HIPCHK(launch_calc_r_star(m->d, m->p, m->f, m->d_srcOf, m->stream));
+    HIPCHK(hipStreamSynchronize(m->stream));
+  }
   m->ready = true;
   return 0;
 }
@@ -770,9 +799,12 @@ int mgcm_blocking_exchanges(mgcm_model *m) {
 // DO_FIELDS_BLOCKING_EXCHANGES field set (do_fields_blocking_exchanges.F:54-97).
 static XFields blocking_fields(const mgcm_model *m) {
   XFields x{};
-  double *fl[] = {m->f.uVel, m->f.vVel, m->f.wVel, m->f.theta, m->f.salt};
-  const bool use[] = {true, true, true, m->p.tempStepping != 0, m->p.saltStepping != 0};
-  for (int q = 0; q < 5; q++)
+  // do_fields_blocking_exchanges.F:54-97 (+ EXCH_UV_DGRID of uVelD/vVelD with the CD scheme,
+  // totPhiHyd when the EOS reads it)
+  double *fl[] = {m->f.uVel, m->f.vVel, m->f.wVel, m->f.theta, m->f.salt, m->f.uVelD, m->f.vVelD, m->f.totPhiHyd};
+  const bool use[] = {true, true, true, m->p.tempStepping != 0, m->p.saltStepping != 0, m->p.useCDscheme != 0,
+                      m->p.useCDscheme != 0, m->p.storePhiHyd4Phys != 0};
+  for (int q = 0; q < 8; q++)
     if (use[q]) { x.p[x.n] = fl[q]; x.nz[x.n] = m->d.Nr; x.n++; }
   return x;
 }
@@ -784,11 +816,16 @@ static int one_step(mgcm_model *m) {
   if (mgcm_thermodynamics(m)) return -1;
   if (m->p.momStepping) {
     if (mgcm_dynamics(m)) return -1;
+    // forward_step.F:829-877: UPDATE_R_STAR(.TRUE.) + UPDATE_CG2D
+    if (m->p.nonlinFreeSurf > 0) TIMED(K_RSTAR, launch_update_r_star_cg2d(m->d, m->p, m->f, m->d_srcOf, m->stream));
     TIMED(K_RHS, launch_sfp_rhs(m->d, m->p, m->f, m->stream));
     TIMED(K_CG2D, launch_cg2d(m, m->p.cg2dMaxIters, m->p.cg2dUseMinResSol - 1));
-    TIMED(K_ETA, launch_exch_eta(m->d, m->f, m->d_srcOf, false, m->stream));
-    TIMED(K_CONT, launch_corr_cont(m->d, m->p, m->f, m->stream));
-    if (m->p.exactConserv) TIMED(K_ETA, launch_exch_eta(m->d, m->f, m->d_srcOf, true, m->stream));
+    TIMED(K_ETA, launch_exch_eta(m->d, m->p, m->f, m->d_srcOf, false, 0, m->stream));
+    TIMED(K_CONT, launch_corr_cont(m->d, m->p, m->f, 0, m->stream));
+    if (m->p.exactConserv) TIMED(K_ETA, launch_exch_eta(m->d, m->p, m->f, m->d_srcOf, true, 0, m->stream));
+    // forward_step.F:965-977: CALC_R_STAR(etaH(n+1)); the next step's RESET_NLFS_VARS +
+    // UPDATE_R_STAR(.FALSE.) restore the hFac in place, so they are not repeated here
+    if (m->p.nonlinFreeSurf > 0) TIMED(K_RSTAR, launch_calc_r_star(m->d, m->p, m->f, m->d_srcOf, m->stream));
   } else {
     if (mgcm_integr_continuity(m)) return -1;
   }
@@ -920,11 +957,11 @@ int mgcm_step_phase(mgcm_model *m, int phase) {
       return 0;
     case 2:
       TIMED(K_CG2D, launch_cg2d(m, m->p.cg2dMaxIters, m->p.cg2dUseMinResSol - 1));
-      TIMED(K_ETA, launch_exch_eta(m->d, m->f, m->d_srcOf, false, m->stream));
-      TIMED(K_CONT, launch_corr_cont(m->d, m->p, m->f, m->stream));
+      TIMED(K_ETA, launch_exch_eta(m->d, m->p, m->f, m->d_srcOf, false, 0, m->stream));
+      TIMED(K_CONT, launch_corr_cont(m->d, m->p, m->f, 0, m->stream));
       return 0;
     case 3:
-      if (m->p.exactConserv) TIMED(K_ETA, launch_exch_eta(m->d, m->f, m->d_srcOf, true, m->stream));
+      if (m->p.exactConserv) TIMED(K_ETA, launch_exch_eta(m->d, m->p, m->f, m->d_srcOf, true, 0, m->stream));
       return 0;
     case 4:
       TIMED(K_EXCH, launch_exchange_multi(m->d, blocking_fields(m), m->d_halo, m->nHalo, m->d_ctr, m->stream));

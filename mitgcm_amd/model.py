@@ -16,14 +16,18 @@ from ._lib import check, lib, MgcmError
 GRID_2D = ("dxF", "dyF", "dxG", "dyG", "dxC", "dyC", "dxV", "dyU", "rA", "rAw", "rAs",
            "recip_dxF", "recip_dyF", "recip_dxC", "recip_dyC", "recip_dxV", "recip_dyU",
            "recip_rA", "recip_rAw", "recip_rAs", "fCori", "Bo_surf", "recip_Bo",
-           "aW2d", "aS2d", "aC2d", "pW", "pS", "pC", "maskInC", "tanPhiAtU", "tanPhiAtV")
-GRID_3D = ("hFacC", "hFacW", "hFacS", "recip_hFacC", "recip_hFacW", "recip_hFacS", "maskC", "maskW", "maskS")
+           "aW2d", "aS2d", "aC2d", "pW", "pS", "pC", "maskInC", "tanPhiAtU", "tanPhiAtV",
+           "fCoriCos", "recip_Rcol", "rSurfW", "rSurfS", "rLowW", "rLowS", "Ro_surf", "R_low")
+GRID_3D = ("hFacC", "hFacW", "hFacS", "recip_hFacC", "recip_hFacW", "recip_hFacS", "maskC", "maskW", "maskS",
+           "h0FacC", "h0FacW", "h0FacS")
 GRID_1D = ("drF", "drC", "recip_drF", "recip_drC", "rF", "rC")
-STATE_1D = ("tRef", "sRef", "pRef4EOS")
+STATE_1D = ("tRef", "sRef", "pRef4EOS", "phiRefC")
 STATE_3D = ("uVel", "vVel", "wVel", "theta", "salt", "gU", "gV", "guNm1", "gvNm1", "gtNm1", "gsNm1", "rhoInSitu",
-            "IVDConvCount", "sigmaR", "Kwx", "Kwy", "Kwz", "Kux", "Kvy", "uVelD", "vVelD", "uNM1", "vNM1")
+            "IVDConvCount", "sigmaR", "Kwx", "Kwy", "Kwz", "Kux", "Kvy", "uVelD", "vVelD", "uNM1", "vNM1",
+            "totPhiHyd", "alphaRho", "del2u", "del2v")
 STATE_2D = ("etaN", "etaH", "fu", "fv", "SST", "lambdaThetaClimRelax", "surfaceForcingT", "surfaceForcingS",
-            "Qnet", "EmPmR", "SSS", "lambdaSaltClimRelax", "etaNm1")
+            "Qnet", "EmPmR", "SSS", "lambdaSaltClimRelax", "etaNm1", "rStarFacC", "rStarFacW", "rStarFacS",
+            "rStarExpC", "rStarExpW", "rStarExpS", "rStarDhCDt", "rStarDhWDt", "rStarDhSDt", "PmEpR", "dEtaHdt")
 # EXTERNAL_FIELDS_LOAD records, in the device's forcRec order
 FORCING_ORDER = ("SST", "SSS", "taux", "tauy", "Qnet", "EmPmR")
 
@@ -61,6 +65,9 @@ class Model:
         for n in GRID_2D + GRID_3D:
             if n in g.f:        # tanPhiAtU/V exist on spherical grids only
                 self.put(n, g.f[n])
+        # INI_NLFS_VARS (ini_nlfs_vars.F:79-92): r* factors start at 1
+        for n in ("rStarFacC", "rStarFacW", "rStarFacS", "rStarExpC", "rStarExpW", "rStarExpS"):
+            self.put(n, np.ones((g.nTiles, g.ny, g.nx)))
         src = np.ascontiguousarray(g.topo.src_of_point(), dtype=np.int64)
         check(L.mgcm_set_halo_map(self.h, src.ctypes.data_as(ctypes.POINTER(ctypes.c_long)), src.size),
               "mgcm_set_halo_map")
@@ -95,6 +102,10 @@ class Model:
         self.put("forcRec", recs)
 
     def put(self, name, arr):
+        if name == "phiRef":   # set_ref_state.F phiRef(1:2Nr+1): the device keeps phiRef(2k)
+            v = np.zeros(self.g.Nr + 1)
+            v[:self.g.Nr] = np.asarray(arr)[1:2 * self.g.Nr:2]
+            name, arr = "phiRefC", v
         a = np.ascontiguousarray(arr, dtype=np.float64)
         check(lib().mgcm_put(self.h, name.encode(), _dp(a), a.size), "mgcm_put(%s)" % name)
 
@@ -220,13 +231,15 @@ def dynstat(model):
     f = g.f
     out = {}
     eta = model.get("etaN")[:, None]
+    # the current hFac (r*: h0Fac*rStarFac, updated every step on the device)
+    hC, hW, hS = model.get("hFacC"), model.get("hFacW"), model.get("hFacS")
     for name, arr, hf, mask, area, dr in (
             ("eta", eta, f["maskInC"][:, None], f["maskInC"], f["rA"], f["drF"]),
-            ("uvel", model.get("uVel"), f["hFacW"], f["maskInW"], f["rAw"], f["drF"]),
-            ("vvel", model.get("vVel"), f["hFacS"], f["maskInS"], f["rAs"], f["drF"]),
+            ("uvel", model.get("uVel"), hW, f["maskInW"], f["rAw"], f["drF"]),
+            ("vvel", model.get("vVel"), hS, f["maskInS"], f["rAs"], f["drF"]),
             ("wvel", model.get("wVel"), f["maskC"], f["maskInC"], f["rA"], f["drC"]),
-            ("theta", model.get("theta"), f["hFacC"], f["maskInC"], f["rA"], f["drF"]),
-            ("salt", model.get("salt"), f["hFacC"], f["maskInC"], f["rA"], f["drF"])):
+            ("theta", model.get("theta"), hC, f["maskInC"], f["rA"], f["drF"]),
+            ("salt", model.get("salt"), hC, f["maskInC"], f["rA"], f["drF"])):
         st = mon_stats(g, arr, hf, mask, area, dr)
         for k, v in st.items():
             out["dynstat_%s_%s" % (name, k)] = float(v)

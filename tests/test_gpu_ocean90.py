@@ -1,0 +1,129 @@
+"""GPU parity of BASELINE config 2, verification/global_ocean.90x40x15, through the
+C-ABI: one 90 x 40 tile (OL = 3), restarted from the committed pickups, with the
+r* coordinate (CALC_R_STAR / UPDATE_R_STAR / UPDATE_CG2D every step), JMD95P,
+biharmonic viscosity, quasi-hydrostatic + NH metric + 3-D Coriolis terms on top of
+the lat-lon ocean physics (GM/Redi, CD scheme, forcing, IVDC, implicit diffusion).
+
+Bars:
+  * INITIALISE_VARIA's r* sequence (factors, hFac, CG2D operator, w, PmEpR, etaH):
+    bit-exact against the oracle (same one-tile layout);
+  * DO_OCEANIC_PHYS + THERMODYNAMICS and DYNAMICS (phi_hyd + QH, del2u, mom_fluxform
+    with r*, CD scheme) from the oracle's state after 2 steps: bit-exact;
+  * 10 steps against the oracle (one tile): cg2d_iters identical, >= 10 digits on the
+    dynstat values (the CG2D sums are tree reductions on the device), and against
+    results/output.txt (36 tiles): >= 9.5 digits except the near-zero eta mean and the
+    1e-13 last CG2D residual.
+"""
+import json
+import os
+
+import numpy as np
+import pytest
+
+from conftest import digits
+
+pytestmark = pytest.mark.gpu
+EXP = "global_ocean.90x40x15"
+
+STATE = ("uVel", "vVel", "wVel", "theta", "salt", "gtNm1", "gsNm1", "etaN", "etaH", "guNm1", "gvNm1", "etaNm1",
+         "uVelD", "vVelD", "uNM1", "vNM1", "totPhiHyd", "rStarFacC", "rStarFacW", "rStarFacS", "rStarExpC",
+         "rStarExpW", "rStarExpS", "rStarDhCDt", "rStarDhWDt", "rStarDhSDt", "PmEpR", "dEtaHdt", "hFacC", "hFacW",
+         "hFacS", "recip_hFacC", "recip_hFacW", "recip_hFacS", "aW2d", "aS2d", "aC2d", "pW", "pS", "pC")
+
+
+def _oracle(nsteps):
+    from oracle.harness import ocean90_oracle
+    o, g = ocean90_oracle()
+    for _ in range(nsteps):
+        o.forward_step()
+    return o, g
+
+
+def _model():
+    from mitgcm_amd import configs
+    return configs.make_model(configs.global_ocean_90x40x15)
+
+
+def _from_oracle(m, o, names):
+    from mitgcm_amd._lib import lib
+    for n in names:
+        m.put(n, np.array(o.arr(n)))
+    lib().mgcm_set_param(m.h, b"myIter", float(o.get("myIter")))
+
+
+def _cmp(m, o, names, region=None):
+    bad = []
+    for n in names:
+        dev, ref = m.get(n), np.array(o.arr(n)).reshape(m.get(n).shape)
+        if region is not None:
+            dev, ref = dev[region(dev)], ref[region(ref)]
+        if not np.array_equal(dev, ref):
+            bad.append((n, float(np.nanmax(np.abs(dev - ref)))))
+    return bad
+
+
+def test_ocean90_init_rstar_bitexact():
+    o, g = _oracle(0)
+    m = _model()
+    names = ("rStarFacC", "rStarFacW", "rStarFacS", "rStarExpC", "rStarExpW", "rStarExpS", "rStarDhCDt", "hFacC",
+             "hFacW", "hFacS", "recip_hFacC", "aW2d", "aS2d", "wVel", "PmEpR", "etaH", "etaN")
+    bad = _cmp(m, o, names)
+    inner = lambda a: (Ellipsis,) + g.sl(1, g.sNx + 1, 1, g.sNy + 1)
+    bad += _cmp(m, o, ("aC2d", "pC", "pW", "pS"), inner)
+    m.close()
+    assert not bad, bad
+
+
+def test_ocean90_oceanic_phys_and_thermodynamics_bitexact():
+    o, g = _oracle(2)
+    m = _model()
+    _from_oracle(m, o, STATE)
+    m.thermodynamics()
+    o.L.oracle_fields_load(o.h)
+    o.L.oracle_oceanic_phys(o.h)
+    bad = _cmp(m, o, ("surfaceForcingT", "surfaceForcingS", "rhoInSitu", "sigmaR", "IVDConvCount", "Kwx", "Kwy",
+                      "Kwz", "Kux", "Kvy"))
+    o.L.oracle_thermodynamics(o.h)
+    inner = lambda a: (slice(None), slice(None)) + g.sl(1, g.sNx, 1, g.sNy)
+    bad += _cmp(m, o, ("theta", "salt", "gtNm1", "gsNm1"), inner)
+    m.close()
+    assert not bad, bad
+
+
+def test_ocean90_dynamics_bitexact():
+    o, g = _oracle(2)
+    o.L.oracle_fields_load(o.h)
+    o.L.oracle_oceanic_phys(o.h)
+    m = _model()
+    _from_oracle(m, o, STATE + ("rhoInSitu", "fu", "fv"))
+    m.dynamics()
+    o.L.oracle_dynamics(o.h)
+    ring = lambda a: (Ellipsis,) + g.sl(0, g.sNx + 1, 0, g.sNy + 1)
+    bad = _cmp(m, o, ("gU", "gV", "uVelD", "vVelD"), ring)
+    bad += _cmp(m, o, ("totPhiHyd",), ring)
+    m.close()
+    assert not bad, bad
+
+
+def test_ocean90_10_steps(golden_dir):
+    o, g = _oracle(0)
+    m = _model()
+    gold = json.load(open(os.path.join(golden_dir, EXP, "monitor.json")))
+    from mitgcm_amd.model import dynstat
+    worst_o, worst_r = (99.0, None), (99.0, None)
+    for step in range(1, 11):
+        m.forward_step(1)
+        o.forward_step()
+        od = o.dynstat()
+        md = m.solve_stats()
+        md.update(dynstat(m))
+        assert md["cg2d_iters"] == od["cg2d_iters"], (step, md["cg2d_iters"], od["cg2d_iters"])
+        for k, v in md.items():
+            if k in od and k != "cg2d_iters" and not k.startswith("cg2d"):
+                worst_o = min(worst_o, (digits(v, od[k]), (step, k, v, od[k])))
+            if k in gold[step] and k not in ("cg2d_iters", "dynstat_eta_mean", "cg2d_last_res"):
+                worst_r = min(worst_r, (digits(v, gold[step][k]), (step, k, v, gold[step][k])))
+    m.close()
+    print("ocean90 device vs oracle: %.2f at %s; vs reference: %.2f at %s" % (worst_o + worst_r))
+    assert worst_o[0] >= 10.0, worst_o
+    assert worst_r[0] >= 9.5, worst_r
