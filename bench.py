@@ -35,20 +35,27 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=20)
-    ap.add_argument("--config", default="global_oce_latlon_90x40x15",
-                    choices=["global_oce_latlon_90x40x15", "tutorial_global_oce_latlon", "baroclinic_gyre_dst3",
+    ap.add_argument("--config", default="global_ocean.90x40x15",
+                    choices=["global_ocean.90x40x15", "global_oce_latlon_90x40x15", "tutorial_global_oce_latlon", "baroclinic_gyre_dst3",
                              "tutorial_baroclinic_gyre", "tutorial_barotropic_gyre"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--shard", action="store_true",
                     help="N>1: shard the workload's tiles over the N processes (RCCL, strong scaling, "
                          "mitgcm_amd/parallel.py) instead of running N replicas")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
-    ap.add_argument("--pmc-summary", default=os.path.join(ROOT, "profiles", "r01", "latlon", "pmc_summary.json"),
+    ap.add_argument("--pmc-summary", default=os.path.join(ROOT, "profiles", "r01", "ocean90", "pmc_summary.json"),
                     help="tools/pmc_summary.py output of rocprofv3 --pmc passes of this command (roofline.traffic)")
     return ap.parse_args()
 
 
 WORKLOADS = {
+    "global_ocean.90x40x15": "BASELINE config 2, verification/global_ocean.90x40x15 as verified: 90x40x15 "
+                             "global lat-lon ocean, 1 tile of 90x40 (OL=3) on 1 GPU, restarted from the committed "
+                             "pickup at nIter0=36000; r* coordinate with non-linear free surface (UPDATE_CG2D "
+                             "every step), JMD95P, GM/Redi gkw91, CD scheme, biharmonic + harmonic viscosity, "
+                             "quasi-hydrostatic + NH metric + 3-D Coriolis, implicit vertical diffusion, IVDC, "
+                             "monthly forcing with real fresh-water flux; full FORWARD_STEP on device, "
+                             "1 step = 1 model day",
     "global_oce_latlon_90x40x15": "90x40x15 global lat-lon ocean (BASELINE config 2's grid, bathymetry, "
                                   "monthly forcing and 1-tile layout sNx=90, sNy=40, OL=3) with the physics "
                                   "verification/tutorial_global_oce_latlon pins: JMD95Z, GM/Redi gkw91, CD scheme, "
@@ -67,6 +74,9 @@ WORKLOADS = {
 
 
 DATA = {
+    "global_ocean.90x40x15": "reference input fields of verification/tutorial_global_oce_latlon (bathymetry, "
+                             "12-month taux/tauy/Qnet/EmPmR/SST/SSS) and the committed pickup.0000036000 / "
+                             "pickup_cd.0000036000 of verification/global_ocean.90x40x15",
     "global_oce_latlon_90x40x15": "reference input fields of verification/tutorial_global_oce_latlon (bathymetry, "
                                   "lev_t/lev_s record 1, 12-month taux/tauy/Qnet/EmPmR/SST/SSS), cold start",
     "tutorial_global_oce_latlon": "reference input fields of verification/tutorial_global_oce_latlon (bathymetry, "
@@ -81,6 +91,8 @@ def config_fn(name):
     from mitgcm_amd import configs
     if name == "baroclinic_gyre_dst3":
         return lambda: configs.baroclinic_gyre(tempAdvScheme=33)
+    if name == "global_ocean.90x40x15":
+        return configs.global_ocean_90x40x15
     if name == "global_oce_latlon_90x40x15":
         return lambda: configs.global_oce_latlon(nSx=1, nSy=1, OL=3)
     if name == "tutorial_global_oce_latlon":
@@ -93,8 +105,10 @@ def cpu_baseline(config, seconds):
     """Oracle (CPU restatement, 1 thread) timed on the same workload: as many
     steps as fit in ~`seconds` of CPU time, reported in model-days/s."""
     from mitgcm_amd import configs
-    from oracle.harness import gyre_oracle, latlon_oracle, oracle_from_config
-    if config == "tutorial_barotropic_gyre":
+    from oracle.harness import gyre_oracle, latlon_oracle, ocean90_oracle, oracle_from_config
+    if config == "global_ocean.90x40x15":
+        o, _ = ocean90_oracle()
+    elif config == "tutorial_barotropic_gyre":
         o = gyre_oracle()
     elif config == "global_oce_latlon_90x40x15":
         o, _ = latlon_oracle(nSx=1, nSy=1, OL=3)
@@ -202,7 +216,7 @@ def main():
     iters_t = [m.solve_stats(back=b)["cg2d_iters"] for b in range(a.steps)]
     cg_ms, cg_n = m.kernel_ms("cg2d")
     kern = {k: m.kernel_ms(k) for k in ("oceanic_phys", "temp_step", "mom_step", "sfp_rhs", "cg2d", "exchange",
-                                         "eta_update", "correction", "continuity")}
+                                         "eta_update", "correction", "continuity", "r_star")}
     m.kernel_timing(False)
     # sanity: the solution is finite and the solver converged every step
     stats = m.solve_stats()
