@@ -86,6 +86,8 @@ struct Fields {
   double *totPhiHyd, *alphaRho, *del2u, *del2v;                            // 3-D
   double *rStarFacC, *rStarFacW, *rStarFacS, *rStarExpC, *rStarExpW, *rStarExpS;   // 2-D
   double *rStarDhCDt, *rStarDhWDt, *rStarDhSDt, *PmEpR, *dEtaHdt;          // 2-D
+  const double *maskInW, *maskInS;                                         // 2-D: kSurfW/S <= Nr
+  double *dWtC, *dWtU, *dWtV;   // 3-D: MOM_CALC_RTRANS's dWtransC/U/V at each level (k_phi_hyd)
   // solver work
   double *cg2d_b, *cg2d_x;
 };

@@ -91,27 +91,33 @@ __global__ void __launch_bounds__(256) k_del2uv(Dims d, Params p, Fields f) {
 }
 
 // CALC_PHI_HYD (calc_phi_hyd.F:175-327, OCEANIC, integr_GeoPot = 2, uniformFreeSurfLev,
-// gravFac = 1) on the dynamics range iMin..iMax = 0..sNx+1.  alphaRho = rhoInSitu, plus
-// MOM_QUASIHYDROSTATIC's 3-D Coriolis / NH-metric buoyancy (mom_quasihydrostatic.F:76-147,
-// angleCosC = 1, angleSinC = 0), kept in alphaRho for CALC_GRAD_PHI_HYD's r* term;
-// DIAGS_PHI_HYD's totPhiHyd (diags_phi_hyd.F:60-120, phi0surf = 0) for the JMD95P EOS.
+// gravFac = 1) per column, as the other column kernels (MG_COLS): alphaRho = rhoInSitu
+// plus MOM_QUASIHYDROSTATIC's 3-D Coriolis / NH-metric buoyancy (mom_quasihydrostatic.F:
+// 76-147, angleCosC = 1, angleSinC = 0) and the two half-level increments are formed
+// k-parallel into LDS, one thread per column runs the reference's sequential sum, and
+// phiHydC, DIAGS_PHI_HYD's totPhiHyd (diags_phi_hyd.F:60-120, phi0surf = 0) and alphaRho
+// (for CALC_GRAD_PHI_HYD's r* term) are stored k-parallel.  Under r* the same column pass
+// runs MOM_CALC_RTRANS's dWtransC/U/V recurrences (mom_calc_rtrans.F:91-137) and keeps
+// their value at every level for k_mom_step.  Columns cover -1..sNx+1 x -1..sNy+1 (the
+// dynamics range 0..sNx+1 plus the west/south neighbours dWtransC is needed at); phi and
+// totPhiHyd are stored on 0..sNx+1 only.
 __global__ void __launch_bounds__(256) k_phi_hyd(Dims d, Params p, Fields f) {
-  MG_PLANE(0, d.sNx + 2, 0, d.sNy + 2, tz)
-  const int t = d.t0 + tz;
-  if (i > d.sNx + 1 || j > d.sNy + 1) return;
-  const double recip_rhoConst = 1.0 / p.rhoConst;
+  __shared__ double sM[256], sP[256], sPh[256], sC[256], sU[256], sV[256];
+  MG_COLS(-1, d.sNx + 3, -1, d.sNy + 3, d.Nr)
+  const int Nr = d.Nr, k = kk + 1, me = kk * NC_ + cc;
   const bool qh = p.quasiHydrostatic && (p.select3dCoriScheme >= 1 || p.useNHMTerms);
   const bool rstar = p.nonlinFreeSurf > 0 && p.select_rStar > 0;
-  const double scalingFactor = p.rhoConst * p.gravitySign * (1.0 / p.gravity);
+  const bool ring = i >= 0 && j >= 0;
+  const double recip_rhoConst = 1.0 / p.rhoConst;
   const long q2 = MG_I2(d, i, j, t);
-  double phF = 0.0;
-  for (int k = 1; k <= d.Nr; k++) {
+  if (valid && k <= Nr) {
     double dRlocM = 0.5 * f.drC[k - 1];
     if (k == 1) dRlocM = f.rF[0] - f.rC[0];
-    const double dRlocP = (k == d.Nr) ? (f.rC[k - 1] - f.rF[k]) : 0.5 * f.drC[k];
+    const double dRlocP = (k == Nr) ? (f.rC[k - 1] - f.rF[k]) : 0.5 * f.drC[k];
     const long q3 = MG_I3(d, i, j, k, t);
     double a = f.rhoInSitu[q3];
     if (qh) {
+      const double scalingFactor = p.rhoConst * p.gravitySign * (1.0 / p.gravity);
       const double u0 = f.uVel[q3], u1 = f.uVel[MG_I3(d, i + 1, j, k, t)];
       const double v0 = f.vVel[q3], v1 = f.vVel[MG_I3(d, i, j + 1, k, t)];
       double gW = 0.0;
@@ -120,18 +126,65 @@ __global__ void __launch_bounds__(256) k_phi_hyd(Dims d, Params p, Fields f) {
       a = a + scalingFactor * gW;
     }
     if (rstar) f.alphaRho[q3] = a;
-    const double phC = phF + dRlocM * p.gravity * a * recip_rhoConst;
-    phF = phC + dRlocP * p.gravity * a * recip_rhoConst;
-    f.phiHydC[q3] = phC;
-    if (p.storePhiHyd4Phys) {
-      double tot;
-      if (rstar && p.nonlinFreeSurf >= 4) {
-        const double dPhiRef = (f.Ro_surf[q2] - f.rC[k - 1]) * p.gravity;
-        tot = phC * f.rStarFacC[q2] + fmax(dPhiRef, 0.0) * (f.rStarFacC[q2] - 1.0) + 0.0;
-      } else {
-        tot = phC + f.Bo_surf[q2] * f.etaN[q2] + 0.0;
+    sM[me] = dRlocM * p.gravity * a * recip_rhoConst;
+    sP[me] = dRlocP * p.gravity * a * recip_rhoConst;
+    if (rstar) {
+      const double drF = f.drF[k - 1];
+      sC[me] = f.rStarDhCDt[q2] * drF * f.h0FacC[q3] * f.rA[q2];
+      if (ring) {
+        sU[me] = f.rStarDhWDt[q2] * drF * f.h0FacW[q3] * f.rAw[q2];
+        sV[me] = f.rStarDhSDt[q2] * drF * f.h0FacS[q3] * f.rAs[q2];
       }
-      f.totPhiHyd[q3] = tot;
+    }
+  }
+  __syncthreads();
+  if (valid && kk == 0) {
+    double phF = 0.0;
+    for (int k2 = 1; k2 <= Nr; k2++) {
+      const int s2 = (k2 - 1) * NC_ + cc;
+      const double phC = phF + sM[s2];
+      phF = phC + sP[s2];
+      sPh[s2] = phC;
+    }
+    if (rstar) {
+      auto d0 = [&](long r) { return f.rStarDhCDt[r] * (f.Ro_surf[r] - f.R_low[r]) * f.rA[r]; };
+      double c = d0(q2);
+      double u = ring ? 0.5 * (d0(q2 - 1) + c) : 0.0, v = ring ? 0.5 * (d0(q2 - d.nx) + c) : 0.0;
+      for (int k2 = 1; k2 <= Nr; k2++) {   // value seen by MOM_CALC_RTRANS(k2): levels 1..k2-1 removed
+        const int s2 = (k2 - 1) * NC_ + cc;
+        const double cc2 = sC[s2];
+        sC[s2] = c;
+        c = c - cc2;
+        if (ring) {
+          const double uu = sU[s2], vv = sV[s2];
+          sU[s2] = u;
+          sV[s2] = v;
+          u = u - uu;
+          v = v - vv;
+        }
+      }
+    }
+  }
+  __syncthreads();
+  if (valid && k <= Nr) {
+    const long q3 = MG_I3(d, i, j, k, t);
+    if (rstar) {
+      f.dWtC[q3] = sC[me];
+      if (ring) { f.dWtU[q3] = sU[me]; f.dWtV[q3] = sV[me]; }
+    }
+    if (ring) {
+      const double phC = sPh[me];
+      f.phiHydC[q3] = phC;
+      if (p.storePhiHyd4Phys) {
+        double tot;
+        if (rstar && p.nonlinFreeSurf >= 4) {
+          const double dPhiRef = (f.Ro_surf[q2] - f.rC[k - 1]) * p.gravity;
+          tot = phC * f.rStarFacC[q2] + fmax(dPhiRef, 0.0) * (f.rStarFacC[q2] - 1.0) + 0.0;
+        } else {
+          tot = phC + f.Bo_surf[q2] * f.etaN[q2] + 0.0;
+        }
+        f.totPhiHyd[q3] = tot;
+      }
     }
   }
 }
@@ -167,17 +220,8 @@ __global__ void __launch_bounds__(256) k_mom_step(Dims d, Params p, Fields f, co
     if (kk > Nr) return 0.0;
     double rTU = 0.5 * (W(i - 1, j, kk) * G2(rA, i - 1, j) + W(i, j, kk) * G2(rA, i, j));
     if (kk == 1) return rTU * U(i, j, 1);
-    if (rstar) {
-      double c0 = G2(rStarDhCDt, i - 1, j) * (G2(Ro_surf, i - 1, j) - G2(R_low, i - 1, j)) * G2(rA, i - 1, j);
-      double c1 = G2(rStarDhCDt, i, j) * (G2(Ro_surf, i, j) - G2(R_low, i, j)) * G2(rA, i, j);
-      double dF = 0.5 * (c0 + c1);
-      for (int k2 = 1; k2 <= kk - 1; k2++) {
-        const double drF2 = f.drF[k2 - 1];
-        c0 = c0 - G2(rStarDhCDt, i - 1, j) * drF2 * G3(h0FacC, i - 1, j, k2) * G2(rA, i - 1, j);
-        c1 = c1 - G2(rStarDhCDt, i, j) * drF2 * G3(h0FacC, i, j, k2) * G2(rA, i, j);
-        dF = dF - G2(rStarDhWDt, i, j) * drF2 * G3(h0FacW, i, j, k2) * G2(rAw, i, j);
-      }
-      rTU = rTU - dF + (c0 + c1) * 0.5;
+    if (rstar) {   // dWtrans of this level from k_phi_hyd
+      rTU = rTU - G3(dWtU, i, j, kk) + (G3(dWtC, i - 1, j, kk) + G3(dWtC, i, j, kk)) * 0.5;
       return rTU * (0.5 * (U(i, j, kk) + U(i, j, kk - 1)));
     }
     double fu_ = rTU * (0.5 * (U(i, j, kk) + U(i, j, kk - 1)));
@@ -191,16 +235,7 @@ __global__ void __launch_bounds__(256) k_mom_step(Dims d, Params p, Fields f, co
     double rTV = 0.5 * (W(i, j - 1, kk) * G2(rA, i, j - 1) + W(i, j, kk) * G2(rA, i, j));
     if (kk == 1) return rTV * V(i, j, 1);
     if (rstar) {
-      double c0 = G2(rStarDhCDt, i, j - 1) * (G2(Ro_surf, i, j - 1) - G2(R_low, i, j - 1)) * G2(rA, i, j - 1);
-      double c1 = G2(rStarDhCDt, i, j) * (G2(Ro_surf, i, j) - G2(R_low, i, j)) * G2(rA, i, j);
-      double dF = 0.5 * (c0 + c1);
-      for (int k2 = 1; k2 <= kk - 1; k2++) {
-        const double drF2 = f.drF[k2 - 1];
-        c0 = c0 - G2(rStarDhCDt, i, j - 1) * drF2 * G3(h0FacC, i, j - 1, k2) * G2(rA, i, j - 1);
-        c1 = c1 - G2(rStarDhCDt, i, j) * drF2 * G3(h0FacC, i, j, k2) * G2(rA, i, j);
-        dF = dF - G2(rStarDhSDt, i, j) * drF2 * G3(h0FacS, i, j, k2) * G2(rAs, i, j);
-      }
-      rTV = rTV - dF + (c0 + c1) * 0.5;
+      rTV = rTV - G3(dWtV, i, j, kk) + (G3(dWtC, i, j - 1, kk) + G3(dWtC, i, j, kk)) * 0.5;
       return rTV * (0.5 * (V(i, j, kk) + V(i, j, kk - 1)));
     }
     double fv_ = rTV * (0.5 * (V(i, j, kk) + V(i, j, kk - 1)));
@@ -522,7 +557,7 @@ __global__ void __launch_bounds__(256) k_cd_scheme(Dims d, Params p, Fields f, c
 }
 
 hipError_t launch_mom_step(const Dims &d, const Params &p, const Fields &f, const int *iterPtr, hipStream_t s) {
-  hipLaunchKernelGGL(k_phi_hyd, dim3(mg_plane_blocks(d.sNx + 2, d.sNy + 2, d.nT)), dim3(MG_PLANE_THREADS), 0, s, d, p, f);
+  hipLaunchKernelGGL(k_phi_hyd, dim3(mg_col_blocks(d.sNx + 3, d.sNy + 3, d.nT, d.Nr)), dim3(256), 0, s, d, p, f);
   if (p.momViscosity && (p.viscA4D != 0.0 || p.viscA4Z != 0.0))
     hipLaunchKernelGGL(k_del2uv, dim3(mg_plane_blocks(d.nx, d.ny, d.nT * d.Nr)), dim3(MG_PLANE_THREADS), 0, s, d, p, f);
   hipLaunchKernelGGL(k_mom_step, dim3(mg_plane_blocks(d.nx, d.ny, d.nT * d.Nr)), dim3(MG_PLANE_THREADS), 0, s, d, p, f, iterPtr);

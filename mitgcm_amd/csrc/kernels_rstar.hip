@@ -13,65 +13,44 @@
 
 namespace mgcm {
 
-// CALC_R_STAR part 1: keep the old factors (rStarExp = rStarFac, calc_r_star.F:101-109)
-// and compute the new ones on the reference's ranges (:111-150); rStarAreaWeight = .TRUE.
-__global__ void __launch_bounds__(256) k_calc_r_star_a(Dims d, Params p, Fields f) {
+// CALC_R_STAR (calc_r_star.F:95-298) in one pass per 2-D point q: the new factors on
+// the reference's ranges (:111-150, rStarAreaWeight = .TRUE.), EXCH_XY_RL(rStarFacC) +
+// EXCH_UV_XY_RL(rStarFacW,S) by evaluating a halo point's factor at its interior source
+// (lat-lon / single facet: scalar copies), then rStarDh*Dt = (Fac - Fac_old)/dtFS and
+// rStarExp = Fac/Fac_old (:283-298).  Each thread reads and writes only its own point's
+// factors, so the old values need no second buffer.
+__global__ void __launch_bounds__(256) k_calc_r_star(Dims d, Params p, Fields f, const long *__restrict__ srcOf) {
   const long q = (long)blockIdx.x * blockDim.x + threadIdx.x;
   if (q >= d.n2 * d.nTiles) return;
   const int t = (int)(q / d.n2);
   if (t < d.t0 || t >= d.t0 + d.nT) return;
-  const long l = q % d.n2;
+  const long sq = srcOf[q], r = sq >= 0 ? sq : q;   // where the new value is computed
+  const long l = r % d.n2;
   const int i = (int)(l % d.nx) - d.OLx + 1, j = (int)(l / d.nx) - d.OLy + 1;
-  f.rStarExpC[q] = f.rStarFacC[q];
-  f.rStarExpW[q] = f.rStarFacW[q];
-  f.rStarExpS[q] = f.rStarFacS[q];
   const double *eta = f.etaH;
-  const int Nr = d.Nr;
-  (void)p;
-  if (i >= 0 && i <= d.sNx + 1 && j >= 0 && j <= d.sNy + 1) {
-    // kSurfC <= Nr  <=>  maskInC = 1 (ini_masks_etc.F)
-    f.rStarFacC[q] = (f.maskInC[q] != 0.0) ? (eta[q] + f.Ro_surf[q] - f.R_low[q]) * f.recip_Rcol[q] : 1.0;
-  }
+  const double oc = f.rStarFacC[q], ow = f.rStarFacW[q], os = f.rStarFacS[q];
+  double fc = oc, fw = ow, fs = os;
+  if (i >= 0 && i <= d.sNx + 1 && j >= 0 && j <= d.sNy + 1)   // kSurfC <= Nr <=> maskInC = 1
+    fc = (f.maskInC[r] != 0.0) ? (eta[r] + f.Ro_surf[r] - f.R_low[r]) * f.recip_Rcol[r] : 1.0;
   if (i >= 1 && i <= d.sNx + 1 && j >= 1 && j <= d.sNy) {
-    const long w = q - 1;
-    // kSurfW <= Nr  <=>  some level of hFacW is wet  <=>  maskW(k=kSurfW) = 1; use h0FacW
-    bool wet = false;
-    for (int k = 1; k <= Nr && !wet; k++) wet = f.h0FacW[MG_I3(d, i, j, k, t)] != 0.0;
-    if (wet) {
-      const double tmp = f.rSurfW[q] - f.rLowW[q];
-      f.rStarFacW[q] = (0.5 * (eta[w] * f.rA[w] + eta[q] * f.rA[q]) * f.recip_rAw[q] + tmp) / tmp;
+    if (f.maskInW[r] != 0.0) {
+      const double tmp = f.rSurfW[r] - f.rLowW[r];
+      fw = (0.5 * (eta[r - 1] * f.rA[r - 1] + eta[r] * f.rA[r]) * f.recip_rAw[r] + tmp) / tmp;
     } else {
-      f.rStarFacW[q] = 1.0;
+      fw = 1.0;
     }
   }
   if (i >= 1 && i <= d.sNx && j >= 1 && j <= d.sNy + 1) {
-    const long s = q - d.nx;
-    bool wet = false;
-    for (int k = 1; k <= Nr && !wet; k++) wet = f.h0FacS[MG_I3(d, i, j, k, t)] != 0.0;
-    if (wet) {
-      const double tmp = f.rSurfS[q] - f.rLowS[q];
-      f.rStarFacS[q] = (0.5 * (eta[s] * f.rA[s] + eta[q] * f.rA[q]) * f.recip_rAs[q] + tmp) / tmp;
+    if (f.maskInS[r] != 0.0) {
+      const double tmp = f.rSurfS[r] - f.rLowS[r];
+      fs = (0.5 * (eta[r - d.nx] * f.rA[r - d.nx] + eta[r] * f.rA[r]) * f.recip_rAs[r] + tmp) / tmp;
     } else {
-      f.rStarFacS[q] = 1.0;
+      fs = 1.0;
     }
   }
-}
-
-// CALC_R_STAR part 2: EXCH_XY_RL(rStarFacC) + EXCH_UV_XY_RL(rStarFacW,S) (halo from the
-// interior source; lat-lon / single-facet: scalar copies) and the expansion ratios
-// rStarDh*Dt = (Fac - Fac_old)/deltaTFreeSurf, rStarExp = Fac/Fac_old (:283-298).
-__global__ void __launch_bounds__(256) k_calc_r_star_b(Dims d, Params p, Fields f, const long *__restrict__ srcOf) {
-  const long q = (long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (q >= d.n2 * d.nTiles) return;
-  const int t = (int)(q / d.n2);
-  if (t < d.t0 || t >= d.t0 + d.nT) return;
-  const long sq = srcOf[q];
-  double fc = f.rStarFacC[q], fw = f.rStarFacW[q], fs = f.rStarFacS[q];
-  if (sq >= 0) {
-    fc = f.rStarFacC[sq]; fw = f.rStarFacW[sq]; fs = f.rStarFacS[sq];
-    f.rStarFacC[q] = fc; f.rStarFacW[q] = fw; f.rStarFacS[q] = fs;
-  }
-  const double oc = f.rStarExpC[q], ow = f.rStarExpW[q], os = f.rStarExpS[q];
+  f.rStarFacC[q] = fc;
+  f.rStarFacW[q] = fw;
+  f.rStarFacS[q] = fs;
   f.rStarDhCDt[q] = (fc - oc) / p.deltaTFreeSurf;
   f.rStarDhWDt[q] = (fw - ow) / p.deltaTFreeSurf;
   f.rStarDhSDt[q] = (fs - os) / p.deltaTFreeSurf;
@@ -80,47 +59,46 @@ __global__ void __launch_bounds__(256) k_calc_r_star_b(Dims d, Params p, Fields 
   f.rStarExpS[q] = fs / os;
 }
 
-// UPDATE_R_STAR(.TRUE.): hFac = h0Fac*rStarFac, recip_hFac = 1/hFac where wet
-// (USE_MASK_AND_NO_IF undefined: dry points keep their reciprocal, 0).
-__global__ void __launch_bounds__(256) k_update_r_star(Dims d, Fields f) {
-  MG_PLANE(1 - d.OLx, d.nx, 1 - d.OLy, d.ny, z)
-  const int t = d.t0 + z / d.Nr, k = z % d.Nr + 1;
-  const long q3 = MG_I3(d, i, j, k, t), q2 = MG_I2(d, i, j, t);
-  const double hC = f.h0FacC[q3] * f.rStarFacC[q2];
-  const double hW = f.h0FacW[q3] * f.rStarFacW[q2];
-  const double hS = f.h0FacS[q3] * f.rStarFacS[q2];
-  f.hFacC[q3] = hC;
-  f.hFacW[q3] = hW;
-  f.hFacS[q3] = hS;
-  if (f.maskC[q3] != 0.0) f.recip_hFacC[q3] = 1.0 / hC;
-  if (f.maskW[q3] != 0.0) f.recip_hFacW[q3] = 1.0 / hW;
-  if (f.maskS[q3] != 0.0) f.recip_hFacS[q3] = 1.0 / hS;
-}
-
-// UPDATE_CG2D part 1 (update_cg2d.F:82-143): aW2d, aS2d = Sum_k faceArea*recip_dx/yC on
-// 1..sNx+1 x 1..sNy+1 (in k order), scaled by cg2dNorm*implicSurfPress*implicDiv2DFlow;
-// 0 elsewhere.
-__global__ void __launch_bounds__(256) k_update_cg2d_a(Dims d, Params p, Fields f) {
+// UPDATE_R_STAR(.TRUE.) (update_r_star.F:60-92) and UPDATE_CG2D part 1
+// (update_cg2d.F:82-143) in one pass, one thread per 2-D point walking its column:
+// hFac = h0Fac*rStarFac and recip_hFac = 1/hFac where wet (USE_MASK_AND_NO_IF undefined)
+// at every level, and on 1..sNx+1 x 1..sNy+1 the operator sums aW2d, aS2d = Sum_k
+// faceArea*recip_dx/yC (k order) scaled by cg2dNorm*implicSurfPress*implicDiv2DFlow
+// (0 elsewhere).  Stores of a level are coalesced over i.
+__global__ void __launch_bounds__(256) k_update_r_star_cg2d_a(Dims d, Params p, Fields f) {
   const long q = (long)blockIdx.x * blockDim.x + threadIdx.x;
   if (q >= d.n2 * d.nTiles) return;
   const int t = (int)(q / d.n2);
   if (t < d.t0 || t >= d.t0 + d.nT) return;
   const long l = q % d.n2;
   const int i = (int)(l % d.nx) - d.OLx + 1, j = (int)(l / d.nx) - d.OLy + 1;
+  const bool op = p.nonlinFreeSurf > 2 && i >= 1 && i <= d.sNx + 1 && j >= 1 && j <= d.sNy + 1;
+  const double fc = f.rStarFacC[q], fw = f.rStarFacW[q], fs = f.rStarFacS[q];
   double aW = 0.0, aS = 0.0;
-  if (i >= 1 && i <= d.sNx + 1 && j >= 1 && j <= d.sNy + 1) {
-    for (int k = 1; k <= d.Nr; k++) {
-      const long q3 = MG_I3(d, i, j, k, t);
-      double faceArea = f.dyG[q] * f.drF[k - 1] * f.hFacW[q3];
+  for (int k = 1; k <= d.Nr; k++) {
+    const long q3 = q + (long)(k - 1) * d.n2 + (long)t * (d.n3 - d.n2);
+    const double hC = f.h0FacC[q3] * fc, hW = f.h0FacW[q3] * fw, hS = f.h0FacS[q3] * fs;
+    f.hFacC[q3] = hC;
+    f.hFacW[q3] = hW;
+    f.hFacS[q3] = hS;
+    if (f.maskC[q3] != 0.0) f.recip_hFacC[q3] = 1.0 / hC;
+    if (f.maskW[q3] != 0.0) f.recip_hFacW[q3] = 1.0 / hW;
+    if (f.maskS[q3] != 0.0) f.recip_hFacS[q3] = 1.0 / hS;
+    if (op) {
+      double faceArea = f.dyG[q] * f.drF[k - 1] * hW;
       aW = aW + faceArea * f.recip_dxC[q];
-      faceArea = f.dxG[q] * f.drF[k - 1] * f.hFacS[q3];
+      faceArea = f.dxG[q] * f.drF[k - 1] * hS;
       aS = aS + faceArea * f.recip_dyC[q];
     }
-    aW = aW * p.cg2dNorm * p.implicSurfPress * p.implicDiv2DFlow;
-    aS = aS * p.cg2dNorm * p.implicSurfPress * p.implicDiv2DFlow;
   }
-  f.aW2d[q] = aW;
-  f.aS2d[q] = aS;
+  if (p.nonlinFreeSurf > 2) {
+    if (op) {
+      aW = aW * p.cg2dNorm * p.implicSurfPress * p.implicDiv2DFlow;
+      aS = aS * p.cg2dNorm * p.implicSurfPress * p.implicDiv2DFlow;
+    }
+    f.aW2d[q] = aW;
+    f.aS2d[q] = aS;
+  }
 }
 
 // UPDATE_CG2D part 2 (update_cg2d.F:144-199): aC2d on the interior, EXCH_XY_RS(aC2d)
@@ -159,20 +137,15 @@ __global__ void __launch_bounds__(256) k_update_cg2d_p(Dims d, Params p, Fields 
 
 hipError_t launch_calc_r_star(const Dims &d, const Params &p, const Fields &f, const long *srcOf, hipStream_t s) {
   const long n = d.n2 * d.nTiles;
-  const unsigned nb = (unsigned)((n + 255) / 256);
-  hipLaunchKernelGGL(k_calc_r_star_a, dim3(nb), dim3(256), 0, s, d, p, f);
-  hipLaunchKernelGGL(k_calc_r_star_b, dim3(nb), dim3(256), 0, s, d, p, f, srcOf);
+  hipLaunchKernelGGL(k_calc_r_star, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, d, p, f, srcOf);
   return hipGetLastError();
 }
 
 hipError_t launch_update_r_star_cg2d(const Dims &d, const Params &p, const Fields &f, const long *srcOf, hipStream_t s) {
-  hipLaunchKernelGGL(k_update_r_star, dim3(mg_plane_blocks(d.nx, d.ny, d.nT * d.Nr)), dim3(MG_PLANE_THREADS), 0, s, d, f);
-  if (p.nonlinFreeSurf > 2) {
-    const long n = d.n2 * d.nTiles;
-    const unsigned nb = (unsigned)((n + 255) / 256);
-    hipLaunchKernelGGL(k_update_cg2d_a, dim3(nb), dim3(256), 0, s, d, p, f);
-    hipLaunchKernelGGL(k_update_cg2d_p, dim3(nb), dim3(256), 0, s, d, p, f, srcOf);
-  }
+  const long n = d.n2 * d.nTiles;
+  const unsigned nb = (unsigned)((n + 255) / 256);
+  hipLaunchKernelGGL(k_update_r_star_cg2d_a, dim3(nb), dim3(256), 0, s, d, p, f);
+  if (p.nonlinFreeSurf > 2) hipLaunchKernelGGL(k_update_cg2d_p, dim3(nb), dim3(256), 0, s, d, p, f, srcOf);
   return hipGetLastError();
 }
 

@@ -99,7 +99,8 @@ static const FieldDesc FIELDS[] = {
     FD(rSurfS, F2D), FD(rLowW, F2D), FD(rLowS, F2D), FD(Ro_surf, F2D), FD(R_low, F2D), FD(phiRefC, F1D),
     FD(totPhiHyd, F3D), FD(alphaRho, F3D), FD(del2u, F3D), FD(del2v, F3D), FD(rStarFacC, F2D), FD(rStarFacW, F2D),
     FD(rStarFacS, F2D), FD(rStarExpC, F2D), FD(rStarExpW, F2D), FD(rStarExpS, F2D), FD(rStarDhCDt, F2D),
-    FD(rStarDhWDt, F2D), FD(rStarDhSDt, F2D), FD(PmEpR, F2D), FD(dEtaHdt, F2D),
+    FD(rStarDhWDt, F2D), FD(rStarDhSDt, F2D), FD(PmEpR, F2D), FD(dEtaHdt, F2D), FD(maskInW, F2D),
+    FD(maskInS, F2D), FD(dWtC, F3D), FD(dWtU, F3D), FD(dWtV, F3D),
 };
 #undef FD
 

@@ -17,7 +17,7 @@ GRID_2D = ("dxF", "dyF", "dxG", "dyG", "dxC", "dyC", "dxV", "dyU", "rA", "rAw", 
            "recip_dxF", "recip_dyF", "recip_dxC", "recip_dyC", "recip_dxV", "recip_dyU",
            "recip_rA", "recip_rAw", "recip_rAs", "fCori", "Bo_surf", "recip_Bo",
            "aW2d", "aS2d", "aC2d", "pW", "pS", "pC", "maskInC", "tanPhiAtU", "tanPhiAtV",
-           "fCoriCos", "recip_Rcol", "rSurfW", "rSurfS", "rLowW", "rLowS", "Ro_surf", "R_low")
+           "fCoriCos", "recip_Rcol", "rSurfW", "rSurfS", "rLowW", "rLowS", "Ro_surf", "R_low", "maskInW", "maskInS")
 GRID_3D = ("hFacC", "hFacW", "hFacS", "recip_hFacC", "recip_hFacW", "recip_hFacS", "maskC", "maskW", "maskS",
            "h0FacC", "h0FacW", "h0FacS")
 GRID_1D = ("drF", "drC", "recip_drF", "recip_drC", "rF", "rC")
