@@ -145,6 +145,11 @@ struct mgcm_model {
   int device = 0;
   hipStream_t stream = nullptr;
   hipStream_t ownStream = nullptr;   // created by mgcm_create; `stream` may be a caller's
+  // THERMODYNAMICS runs on a second stream concurrently with DYNAMICS (fork after
+  // DO_OCEANIC_PHYS, join before UPDATE_R_STAR / SOLVE_FOR_PRESSURE; MGCM_NO_OVERLAP=1 off)
+  hipStream_t stream2 = nullptr;
+  hipEvent_t evFork = nullptr, evJoin = nullptr;
+  bool overlap = true;
   std::vector<void *> allocs;
   // extra parameters kept on host only
   std::map<std::string, double> extra;
@@ -486,6 +491,14 @@ mgcm_model *mgcm_create(int sNx, int sNy, int OLx, int OLy, int Nr, int nSx, int
     return nullptr;
   }
   m->stream = m->ownStream;
+  if (hipStreamCreateWithFlags(&m->stream2, hipStreamNonBlocking) != hipSuccess ||
+      hipEventCreateWithFlags(&m->evFork, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&m->evJoin, hipEventDisableTiming) != hipSuccess) {
+    set_err("mgcm_create: second stream / events");
+    delete m;
+    return nullptr;
+  }
+  m->overlap = getenv("MGCM_NO_OVERLAP") == nullptr;
   for (auto &fd : FIELDS) {
     const long n = field_count(m, fd.kind);
     double *ptr = nullptr;
@@ -526,6 +539,9 @@ void mgcm_destroy(mgcm_model *m) {
   if (m->d_ctr) hipFree(m->d_ctr);
   if (m->d_rec) hipFree(m->d_rec);
   if (m->ownStream) hipStreamDestroy(m->ownStream);
+  if (m->stream2) hipStreamDestroy(m->stream2);
+  if (m->evFork) hipEventDestroy(m->evFork);
+  if (m->evJoin) hipEventDestroy(m->evJoin);
   delete m;
 }
 
@@ -734,20 +750,25 @@ static TracerArgs tracer_args(mgcm_model *m, bool salt) {
   return a;
 }
 
+// TEMP_INTEGRATE / SALT_INTEGRATE on stream `st` (the theta/salt ping-pong swap is host-side)
+static int tracers_on(mgcm_model *m, hipStream_t st) {
+  if (m->p.tempStepping) {
+    TIMED(K_TEMP, launch_tracer_step(m->d, m->p, m->f, tracer_args(m, false), m->d_ctr, st));
+    std::swap(m->f.theta, m->f.thetaNext);   // CYCLE_TRACER: the new theta is the other buffer
+  }
+  if (m->p.saltStepping) {
+    TIMED(K_TEMP, launch_tracer_step(m->d, m->p, m->f, tracer_args(m, true), m->d_ctr, st));
+    std::swap(m->f.salt, m->f.saltNext);
+  }
+  return 0;
+}
+
 int mgcm_thermodynamics(mgcm_model *m) {
   if (check_ready(m)) return -1;
   if (!m->p.tempStepping && !m->p.saltStepping) return 0;
   // forward_step.F:656 DO_OCEANIC_PHYS, :732 THERMODYNAMICS (staggerTimeStep = F)
   TIMED(K_PHYS, launch_oceanic_phys(m->d, m->p, m->f, m->d_ctr, m->stream));
-  if (m->p.tempStepping) {
-    TIMED(K_TEMP, launch_tracer_step(m->d, m->p, m->f, tracer_args(m, false), m->d_ctr, m->stream));
-    std::swap(m->f.theta, m->f.thetaNext);   // CYCLE_TRACER: the new theta is the other buffer
-  }
-  if (m->p.saltStepping) {
-    TIMED(K_TEMP, launch_tracer_step(m->d, m->p, m->f, tracer_args(m, true), m->d_ctr, m->stream));
-    std::swap(m->f.salt, m->f.saltNext);
-  }
-  return 0;
+  return tracers_on(m, m->stream);
 }
 
 static int solve_impl(mgcm_model *m) {
@@ -814,9 +835,23 @@ static XFields blocking_fields(const mgcm_model *m) {
 // correction+continuity, EXCH(eta)+UPDATE_ETAH, and every blocking exchange plus
 // the counter bump in one launch.  Same arithmetic as the separate C-ABI ops.
 static int one_step(mgcm_model *m) {
-  if (mgcm_thermodynamics(m)) return -1;
+  // THERMODYNAMICS reads u, v, w, hFac and DO_OCEANIC_PHYS's outputs and writes only the
+  // tracers' other buffers and AB histories; DYNAMICS reads none of those.  So once
+  // DO_OCEANIC_PHYS is done the two run concurrently (second stream), joined before
+  // UPDATE_R_STAR / SOLVE_FOR_PRESSURE (which rewrite hFac, then u, v, w).
+  const bool fork = m->overlap && !m->timing && m->p.momStepping && (m->p.tempStepping || m->p.saltStepping);
+  if (fork) {
+    TIMED(K_PHYS, launch_oceanic_phys(m->d, m->p, m->f, m->d_ctr, m->stream));
+    HIPCHK(hipEventRecord(m->evFork, m->stream));
+    HIPCHK(hipStreamWaitEvent(m->stream2, m->evFork, 0));
+    if (tracers_on(m, m->stream2)) return -1;
+    HIPCHK(hipEventRecord(m->evJoin, m->stream2));
+  } else if (mgcm_thermodynamics(m)) {
+    return -1;
+  }
   if (m->p.momStepping) {
     if (mgcm_dynamics(m)) return -1;
+    if (fork) HIPCHK(hipStreamWaitEvent(m->stream, m->evJoin, 0));
     // forward_step.F:829-877: UPDATE_R_STAR(.TRUE.) + UPDATE_CG2D
     if (m->p.nonlinFreeSurf > 0) TIMED(K_RSTAR, launch_update_r_star_cg2d(m->d, m->p, m->f, m->d_srcOf, m->stream));
     TIMED(K_RHS, launch_sfp_rhs(m->d, m->p, m->f, m->stream));
