@@ -7,6 +7,7 @@ import os
 
 import numpy as np
 
+from .exch2 import cube_topology
 from .grid import Grid
 from .model import Model
 
@@ -295,3 +296,87 @@ def global_ocean_90x40x15(nSx=1, nSy=1, OL=3, data_dir=None, pickup_dir=None):
     for n in ("h0FacC", "h0FacW", "h0FacS", "recip_Rcol", "rLowW", "rLowS", "rSurfW", "rSurfS"):
         state[n] = g.f[n]
     return g, params, state, forcing
+
+
+def cs_global_to_tiles(g, glob):
+    """Global cube-sphere MDS field (W2_mapIO = 1: facets stacked in y, (..., 6*n, n),
+    w2_set_map_tiles.F:160-175) -> tile layout (..., nTiles, ny, nx), interiors only."""
+    topo = g.topo
+    lead = glob.shape[:-2]
+    out = np.zeros(lead + (g.nTiles, g.ny, g.nx))
+    inner = g.sl(1, g.sNx, 1, g.sNy)
+    gNx = glob.shape[-1]
+    for t in range(g.nTiles):
+        tid = t + 1
+        f = topo.face[tid]
+        nb = sum(fx * fy for fx, fy in topo.facet_dims[:f - 1])
+        ii = nb + topo.tBx[tid] + topo.tBy[tid] * topo.facet_dims[f - 1][0]
+        x0, y0 = ii % gNx, ii // gNx
+        out[(Ellipsis, t) + inner] = glob[..., y0:y0 + g.sNy, x0:x0 + g.sNx]
+    return out
+
+
+def solid_body_cs32(data_dir=None):
+    """verification/solid-body.cs-32x32x1: cubed sphere, 6 faces of 32x32 (one tile each,
+    OL=2, pkg/exch2), 1 level of an ideal-gas atmosphere in p-coordinates (delR=1e5 Pa,
+    tRef=300 = theta, so the hydrostatic anomaly is exactly zero), vector-invariant
+    momentum, no viscosity, implicit free surface (uniformLin_PhiSurf: Bo_surf =
+    1/rhoConst = 1), rotationPeriod=108000, rSphere=5500.4e3 with the grid of radius
+    6370e3 rescaled, deltaT=450, abEps=0.1, passive salt (C2 advection) from S_init.bin,
+    cg2dTargetResidual=1e-12.  Initial state: code/ini_vel.F (solid-body rotation from
+    psi = fac*fCoriG) and code/ini_psurf.F (balanced surface pressure)."""
+    from math import pi
+    d = data_dir or os.path.join(GOLDEN, "solid-body.cs-32x32x1")
+    topo = cube_topology(32, 32, 32, 2)
+    g = Grid(32, 32, 2, 2, 1, nSx=6, nSy=1, topology=topo)
+    g.usingCurvilinearGrid = True
+    g.ini_vertical_grid([1.0e5], Ro_SeaLevel=1.0e5)
+    recs = [np.fromfile(os.path.join(d, "tile%03d.mitgrid" % f), dtype=">f8").astype(np.float64).reshape(16, 33, 33)
+            for f in range(1, 7)]
+    rSphere = 5500.4e3
+    g.ini_curvilinear_grid(recs, radius_fromHorizGrid=6370.0e3, rSphere=rSphere, anglesFromFile=False)
+    omega = 2.0 * pi / 108000.0
+    g.ini_cori(selectCoriMap=2, omega=omega)
+    bathy = np.full((g.nTiles, g.ny, g.nx), g.f["rF"][1])     # no bathyFile: R_low = rF(Nr+1)
+    g.ini_depths_masks(bathy, hFacMin=1.0, hFacMinDr=0.0, gBaro=9.81)
+    rhoConst = 1.0
+    g.f["Bo_surf"] = np.full((g.nTiles, g.ny, g.nx), 1.0 / rhoConst)   # ini_linear_phisurf.F, uniformLin_PhiSurf
+    g.f["recip_Bo"] = np.full((g.nTiles, g.ny, g.nx), rhoConst)
+    g.ini_cg2d(450.0, 450.0, 1e-12)
+    params = dict(deltaTMom=450.0, deltaTFreeSurf=450.0, deltaTClock=450.0, deltaTtracer=450.0, abEps=0.1,
+                  rhoConst=rhoConst, rhoNil=rhoConst, gravity=9.81, gBaro=9.81, viscAhD=0.0, viscAhZ=0.0,
+                  viscA4D=0.0, viscA4Z=0.0, viscAr=0.0, sideDragFactor=2.0, no_slip_sides=0, no_slip_bottom=0,
+                  selectCoriScheme=0, vectorInvariantMomentum=1, selectVortScheme=1, selectKEscheme=0,
+                  momForcingOutAB=0, momDissip_In_AB=1, cg2dMaxIters=600, cg2dUseMinResSol=0, nIter0=0,
+                  exactConserv=0, tempStepping=0, saltStepping=1, saltAdvection=1, saltForcing=1,
+                  saltAdvScheme=2, saltVertAdvScheme=2, diffKhS=0.0, diffKrS=0.0, implicitDiffusion=0,
+                  ivdc_kappa=0.0, usingCurvilinearGrid=1, rSphere=rSphere, integr_GeoPot=2, gravitySign=1.0,
+                  eosType=0, tAlpha=0.0, sBeta=0.0)
+    # code/ini_vel.F: psi = fac*fCoriG, full halo range, then EXCH_UV_XYZ_RL(.TRUE.) and masks
+    omegaprime = 80.0 / rSphere
+    fac = -(rSphere * rSphere) * omegaprime / (2.0 * omega)
+    psi = fac * g.f["fCoriG"]
+    u = np.zeros((g.nTiles, 1, g.ny, g.nx))
+    v = np.zeros_like(u)
+    for t in range(g.nTiles):
+        for J in range(g.ny):
+            Jp = min(J + 1, g.ny - 1)
+            for I in range(g.nx):
+                Ip = min(I + 1, g.nx - 1)
+                u[t, 0, J, I] = 0.0 + (psi[t, J, I] - psi[t, Jp, I]) * g.f["recip_dyG"][t, J, I]
+                v[t, 0, J, I] = 0.0 + (psi[t, J, Ip] - psi[t, J, I]) * g.f["recip_dxG"][t, J, I]
+    u, v = topo.exchange_uv(u, v, True)
+    u = u * g.f["maskW"]
+    v = v * g.f["maskS"]
+    # code/ini_psurf.F
+    psFac = -(rSphere * rSphere) * omegaprime * (omega + omegaprime * 0.5)
+    snFac = 1.0 / (4.0 * omega * omega)
+    fC = g.f["fCori"]
+    etaN = 0.0 + psFac * (snFac * fC * fC - 1.0 / 3.0) * g.f["recip_Bo"]
+    salt = cs_global_to_tiles(g, np.fromfile(os.path.join(d, "S_init.bin"), dtype=">f8").astype(np.float64)
+                              .reshape(192, 32))[:, None]
+    salt = g.exch(salt) * g.f["maskC"]
+    state = {"uVel": u, "vVel": v, "etaN": etaN, "salt": salt,
+             "theta": np.full((g.nTiles, 1, g.ny, g.nx), 300.0), "tRef": np.array([300.0]),
+             "sRef": np.array([0.0])}
+    return g, params, state

@@ -44,8 +44,12 @@ class Grid:
     def exch(self, a):
         return self.topo.exchange(a)
 
+    def exch_uv(self, u, v, withSigns=False):
+        """EXCH_UV_XY(Z)_RS/RL of a C-grid vector pair (grid arrays: withSigns=.FALSE.)."""
+        return self.topo.exchange_uv(u, v, withSigns)
+
     # ---- vertical grid --------------------------------------------------------
-    def ini_vertical_grid(self, delR, rkSign=-1.0):
+    def ini_vertical_grid(self, delR, rkSign=-1.0, Ro_SeaLevel=0.0):
         Nr = self.Nr
         drF = np.array(delR, dtype=np.float64)
         drC = np.zeros(Nr + 1)
@@ -54,6 +58,7 @@ class Grid:
             drC[k] = 0.5 * (drF[k - 1] + drF[k])
         drC[Nr] = 0.5 * drF[Nr - 1]
         rF = np.zeros(Nr + 1)
+        rF[0] = Ro_SeaLevel               # p-coordinates: surface pressure (ini_vertical_grid.F)
         for k in range(Nr):
             rF[k + 1] = rF[k] + rkSign * drF[k]
         rC = np.zeros(Nr)
@@ -187,9 +192,75 @@ class Grid:
             f["rAw"][t, :, 1:] = 0.5 * (rA[:, 1:] + rA[:, :-1])
         self._reciprocals()
 
+    def ini_curvilinear_grid(self, facet_records, radius_fromHorizGrid, rSphere, anglesFromFile):
+        """INI_CURVILINEAR_GRID (model/src/ini_curvilinear_grid.F:238-340, OLD_GRID_IO
+        undefined) + CALC_GRID_ANGLES (calc_grid_angles.F).  facet_records[f] is the
+        (nrec, fNy+1, fNx+1) content of facet f's grid file (tileNNN.mitgrid or
+        <horizGridFile>.faceNNN.bin): XC YC DXF DYF RA XG YG DXV DYU RAZ DXC DYC RAW RAS
+        DXG DYG [AngleCS AngleSN].  MDS_FACEF_READ_RS (pkg/mdsio/mdsio_facef_read.F:83-99)
+        puts rows tBy+1..tBy+sNy+1, columns tBx+1..tBx+sNx+1 at (1..sNx+1, 1..sNy+1)."""
+        names = ("xC", "yC", "dxF", "dyF", "rA", "xG", "yG", "dxV", "dyU", "rAz", "dxC", "dyC", "rAw", "rAs",
+                 "dxG", "dyG", "angleCosC", "angleSinC")
+        topo = self.topo
+        f = {n: self.z2() for n in names}           # INI_GRID zeroes every array first
+        f["angleCosC"][:] = 1.0
+        nrec = 18 if anglesFromFile else 16
+        for t in range(self.nTiles):
+            tid = t + 1
+            rec = facet_records[topo.face[tid] - 1]
+            tbx, tby = topo.tBx[tid], topo.tBy[tid]
+            for r in range(nrec):
+                f[names[r]][t, self.OLy:self.OLy + self.sNy + 1, self.OLx:self.OLx + self.sNx + 1] = \
+                    rec[r, tby:tby + self.sNy + 1, tbx:tbx + self.sNx + 1]
+        f["xC"] = topo.exchange(f["xC"])
+        f["yC"] = topo.exchange(f["yC"])
+        f["dxF"], f["dyF"] = topo.exchange_uv_agrid(f["dxF"], f["dyF"], False)
+        f["rA"] = topo.exchange(f["rA"])
+        f["xG"] = topo.exchange_z(f["xG"])
+        f["yG"] = topo.exchange_z(f["yG"])
+        f["dxV"], f["dyU"] = topo.exchange_uv_bgrid(f["dxV"], f["dyU"], False)
+        f["rAz"] = topo.exchange_z(f["rAz"])
+        f["dxC"], f["dyC"] = topo.exchange_uv(f["dxC"], f["dyC"], False)
+        f["rAw"], f["rAs"] = topo.exchange_uv(f["rAw"], f["rAs"], False)
+        f["dyG"], f["dxG"] = topo.exchange_uv(f["dyG"], f["dxG"], False)
+        if rSphere != radius_fromHorizGrid:
+            fac = rSphere / radius_fromHorizGrid
+            fac2 = fac * fac
+            for n in ("dxC", "dyC", "dxG", "dyG", "dxF", "dyF", "dxV", "dyU"):
+                f[n] = f[n] * fac
+            for n in ("rA", "rAz", "rAw", "rAs"):
+                f[n] = f[n] * fac2
+        self.rSphere = rSphere
+        if not anglesFromFile:
+            # CALC_GRID_ANGLES (calc_grid_angles.F:70-110)
+            from math import sqrt
+            deg2rad = 2.0 * np.pi / 360.0      # PI = 2*ASIN(1), ini_parms.F
+            yG, dxG, dyG = f["yG"], f["dxG"], f["dyG"]
+            uP, vP = self.z2(), self.z2()
+            with np.errstate(divide="ignore", invalid="ignore"):
+                uP[:, :-1, :] = np.where(dyG[:, :-1, :] > 0.0,
+                                         -(yG[:, :-1, :] - yG[:, 1:, :]) * deg2rad / dyG[:, :-1, :], 0.0)
+                vP[:, :, :-1] = np.where(dxG[:, :, :-1] > 0.0,
+                                         (yG[:, :, :-1] - yG[:, :, 1:]) * deg2rad / dxG[:, :, :-1], 0.0)
+            cs, sn = f["angleCosC"], f["angleSinC"]
+            for t in range(self.nTiles):
+                for J in range(self.ny - 1):
+                    for I in range(self.nx - 1):
+                        uC = 0.5 * (uP[t, J, I] + uP[t, J, I + 1])
+                        vC = 0.5 * (vP[t, J, I] + vP[t, J + 1, I])
+                        un = sqrt(uC * uC + vC * vC)
+                        if un != 0.0:
+                            un = 1.0 / un
+                        cs[t, J, I] = uC * un
+                        sn[t, J, I] = -vC * un
+        f["angleSinC"], f["angleCosC"] = topo.exchange_uv_agrid(f["angleSinC"], f["angleCosC"], True)
+        self.f.update(f)
+        self._reciprocals()
+
     def _reciprocals(self):
         for n in ("dxG", "dyG", "dxC", "dyC", "dxF", "dyF", "dxV", "dyU", "rA", "rAs", "rAw", "rAz"):
             a = self.f[n]
+            # 1/x, unlike x*(1/x) shortcuts: same as ini_grid.F:78-101
             r = np.zeros_like(a)
             nz = a != 0.0
             r[nz] = 1.0 / a[nz]
@@ -220,14 +291,18 @@ class Grid:
 
     # ---- depths and masks -----------------------------------------------------
     def ini_depths_masks(self, bathy, hFacMin=1.0, hFacMinDr=0.0, gBaro=9.81):
-        """bathy: global (Ny, Nx) array, negative below sea level."""
+        """bathy: global (Ny, Nx) lat-lon array, or tile layout (nTiles, ny, nx) (interiors used);
+        negative below sea level."""
         sNx, sNy, Nr = self.sNx, self.sNy, self.Nr
         rF, drF, recip_drF = self.f["rF"], self.f["drF"], self.f["recip_drF"]
         R_low, Ro_surf = self.z2(), self.z2()
         inner = self.sl(1, sNx, 1, sNy)
         for t in range(self.nTiles):
             bi, bj = t % self.nSx, t // self.nSx
-            R_low[t][inner] = bathy[bj * sNy:(bj + 1) * sNy, bi * sNx:(bi + 1) * sNx]
+            if bathy.ndim == 3:
+                R_low[t][inner] = bathy[t][inner]
+            else:
+                R_low[t][inner] = bathy[bj * sNy:(bj + 1) * sNy, bi * sNx:(bi + 1) * sNx]
             Ro_surf[t][inner] = rF[0]
         R_low = self.exch(R_low)
         Ro_surf = self.exch(Ro_surf)
@@ -275,8 +350,7 @@ class Grid:
                 h2 = (rF[k] - rSurf) * recip_drF[k]
                 hl = h1 - np.maximum(h2, 0.0)
                 out[:, k] = np.where(hl < mn * 0.5, 0.0, np.maximum(hl, mn))
-        hFacW = self.exch(hFacW)
-        hFacS = self.exch(hFacS)
+        hFacW, hFacS = self.exch_uv(hFacW, hFacS)       # EXCH_UV_XYZ_RS(hFacW,hFacS,.FALSE.)
         kSurfW = np.full(R_low.shape, Nr + 1, dtype=np.int32)
         kSurfS = np.full(R_low.shape, Nr + 1, dtype=np.int32)
         for k in range(Nr - 1, -1, -1):
@@ -296,8 +370,10 @@ class Grid:
             tS = tS + drF[k] * hFacS[:, k]
         rSurfW, rSurfS = rLowW + tW, rLowS + tS
         f = self.f
-        f.update(recip_Rcol=recip_Rcol, rLowW=self.exch(rLowW), rLowS=self.exch(rLowS), rSurfW=self.exch(rSurfW),
-                 rSurfS=self.exch(rSurfS), h0FacC=hFacC.copy(), h0FacW=hFacW.copy(), h0FacS=hFacS.copy())
+        rLowW, rLowS = self.exch_uv(rLowW, rLowS)       # ini_masks_etc.F: EXCH_UV_XY_RS(.FALSE.)
+        rSurfW, rSurfS = self.exch_uv(rSurfW, rSurfS)
+        f.update(recip_Rcol=recip_Rcol, rLowW=rLowW, rLowS=rLowS, rSurfW=rSurfW,
+                 rSurfS=rSurfS, h0FacC=hFacC.copy(), h0FacW=hFacW.copy(), h0FacS=hFacS.copy())
         f.update(R_low=R_low, Ro_surf=Ro_surf, hFacC=hFacC, hFacW=hFacW, hFacS=hFacS, maskInC=maskInC,
                  maskInW=np.where(kSurfW <= Nr, 1.0, 0.0), maskInS=np.where(kSurfS <= Nr, 1.0, 0.0))
         self.i.update(kSurfC=kSurfC, kLowC=kLowC, kSurfW=kSurfW, kSurfS=kSurfS)
@@ -337,8 +413,7 @@ class Grid:
         myNorm = 1.0 / myNorm if myNorm != 0.0 else 1.0
         aW[(slice(None),) + inner] = aW[(slice(None),) + inner] * myNorm
         aS[(slice(None),) + inner] = aS[(slice(None),) + inner] * myNorm
-        aW = self.exch(aW)
-        aS = self.exch(aS)
+        aW, aS = self.exch_uv(aW, aS)                   # ini_cg2d.F:138 EXCH_UV_XY_RS(.FALSE.)
         self.cg2dNorm = myNorm
         self.cg2dNormaliseRHS = cg2dTargetResWunit <= 0.0
         tol = cg2dTargetResidual if self.cg2dNormaliseRHS else \
@@ -361,4 +436,5 @@ class Grid:
             pSv = np.where(aC + acs == 0.0, 0.0, -aS / (dS * dS))
         for dst, src in ((pC, pCv), (pW, pWv), (pS, pSv)):
             dst[(slice(None),) + inner] = src[(slice(None),) + inner]
-        f.update(aW2d=aW, aS2d=aS, aC2d=aC, pC=self.exch(pC), pW=self.exch(pW), pS=self.exch(pS))
+        pW, pS = self.exch_uv(pW, pS)                   # ini_cg2d.F:233-234
+        f.update(aW2d=aW, aS2d=aS, aC2d=aC, pC=self.exch(pC), pW=pW, pS=pS)

@@ -48,3 +48,14 @@ class LatLonTopology:
         b = np.moveaxis(a, 1, 0).reshape(nz, -1)   # (nz, nTiles*n2)
         b = b[:, src]
         return np.moveaxis(b.reshape(nz, nt, self.ny, self.nx), 0, 1).copy()
+
+    # vector / staggered variants: on the lat-lon (EXCH1) topology every component is a
+    # plain scalar copy (exch_uv_xy_rx.template:87-95, exch_z_3d_rx.template:71)
+    def exchange_uv(self, u, v, withSigns=True):
+        return self.exchange(u), self.exchange(v)
+
+    exchange_uv_agrid = exchange_uv
+    exchange_uv_bgrid = exchange_uv
+
+    def exchange_z(self, a):
+        return self.exchange(a)

@@ -19,8 +19,9 @@ static void check_supported(const OModel *m) {
     fprintf(stderr, "oracle_dynamics: biharmonic viscosity needs OLx, OLy >= 3\n"); abort();
   }
   if (m->implicitViscosity) { fprintf(stderr, "oracle_dynamics: implicitViscosity not yet restated\n"); abort(); }
-  if (!m->usingCartesianGrid && !m->usingSphericalPolarGrid) {
-    fprintf(stderr, "oracle_dynamics: only cartesian and spherical-polar grids restated\n"); abort();
+  if (!m->usingCartesianGrid && !m->usingSphericalPolarGrid &&
+      !(m->usingCurvilinearGrid && m->vectorInvariantMomentum)) {
+    fprintf(stderr, "oracle_dynamics: grid/momentum-scheme combination not restated\n"); abort();
   }
   if (m->integr_GeoPot != 2) { fprintf(stderr, "oracle_dynamics: integr_GeoPot=%d not restated\n", m->integr_GeoPot); abort(); }
 }
@@ -190,6 +191,12 @@ void oracle_dynamics(OModel *m) {
           for (int i = 2 - OLx; i <= sNx + OLx; i++)
             L(h0FacZ, i, j) = fmin(fmin(W3(h0FacW, i, j, k), W3(h0FacW, i, j - 1, k)),
                                    fmin(W3(h0FacS, i, j, k), W3(h0FacS, i - 1, j, k)));
+      if (m->vectorInvariantMomentum) {
+        /* MOM_VECINV (dynamics.F:517-530) replaces MOM_FLUXFORM; the ping-pong buffers carry
+         * the vertical viscous fluxes there */
+        oracle_mom_vecinv(m, t, k, hFacZ, r_hFacZ, h0FacZ, kappaRU, kappaRV, fVerUkm, fVerVkm,
+                          fVerUkp, fVerVkp, guDiss, gvDiss);
+      } else {
       for (long p = 0; p < n2; p++) v4F[p] = 0.0;
       /* xA, yA, uTrans, vTrans (mom_fluxform.F:287-327) */
       for (int j = 1 - OLy; j <= sNy + OLy; j++)
@@ -615,6 +622,7 @@ void oracle_dynamics(OModel *m) {
           L(gvDiss, i, j) = L(gvDiss, i, j) * W3(maskS, i, j, k);
         }
 
+      }   /* vectorInvariantMomentum */
       /* ======================== TIMESTEP (timestep.F) ======================== */
       for (long p = 0; p < n2; p++) guExt[p] = gvExt[p] = gUtmp[p] = gVtmp[p] = 0.0;
       if (m->momForcing) {

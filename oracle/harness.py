@@ -51,6 +51,11 @@ def lib():
         L.oracle_cg2d.argtypes = [vp, P, P, P, P, P, ctypes.POINTER(c_int), ctypes.POINTER(c_int)]
         L.oracle_mon_stats.argtypes = [vp, P, c_int, P, c_int, P, P, P, P]
         L.oracle_exch_xy.argtypes = [vp, P]
+        LP = ctypes.POINTER(ctypes.c_long)
+        IP = ctypes.POINTER(c_int)
+        L.oracle_set_exch2.argtypes = [vp, LP, LP, LP, LP, LP, IP, IP]
+        L.oracle_set_exch2.restype = c_int
+        L.oracle_exch_uv_xyz.argtypes = [vp, P, P, c_int, c_int]
         _lib = L
     return _lib
 
@@ -178,6 +183,10 @@ def oracle_from_config(cfg, **kw):
     o = Oracle(g.sNx, g.sNy, g.OLx, g.OLy, g.Nr, g.nSx, g.nSy)
     if getattr(g, "usingSphericalPolarGrid", False):
         o.set(usingCartesianGrid=0, usingSphericalPolarGrid=1)
+    if getattr(g, "usingCurvilinearGrid", False):
+        o.set(usingCartesianGrid=0, usingCurvilinearGrid=1)
+    if hasattr(g.topo, "uv_codes"):          # pkg/exch2 topology: install its halo maps
+        set_exch2(o, g.topo)
     for k, v in params.items():
         o.set(**{k: v})
     for n in ("drF", "drC", "rF", "rC", "recip_drF", "recip_drC"):
@@ -195,6 +204,21 @@ def oracle_from_config(cfg, **kw):
     for k, v in state.items():
         o.arr(k).reshape(-1)[:len(np.ravel(v))] = np.ravel(v)
     return o, g
+
+
+def set_exch2(o, topo):
+    """Hand the EXCH2 gather maps (mitgcm_amd/exch2.py) and tile face/edge flags to the oracle."""
+    c = lambda a: np.ascontiguousarray(a, dtype=np.int64)
+    LP = lambda a: a.ctypes.data_as(ctypes.POINTER(ctypes.c_long))
+    scal = c(topo.scalar_ids())
+    u1, v1 = (c(x) for x in topo.uv_codes(True))
+    u0, v0 = (c(x) for x in topo.uv_codes(False))
+    face = np.ascontiguousarray(topo.face[1:], dtype=np.int32)
+    edge = np.ascontiguousarray([topo.isN[t] | 2 * topo.isS[t] | 4 * topo.isE[t] | 8 * topo.isW[t]
+                                 for t in range(1, topo.nTiles + 1)], dtype=np.int32)
+    IP = lambda a: a.ctypes.data_as(ctypes.POINTER(ctypes.c_int))
+    assert o.L.oracle_set_exch2(o.h, LP(scal), LP(u1), LP(v1), LP(u0), LP(v0), IP(face), IP(edge)) == 0
+    o._keep = (scal, u1, v1, u0, v0, face, edge)
 
 
 def latlon_oracle(**kw):

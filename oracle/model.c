@@ -105,6 +105,8 @@ void oracle_free(OModel *m) {
                    &m->phiRef};
   for (size_t i = 0; i < sizeof(dp) / sizeof(dp[0]); i++) free(*dp[i]);
   free(m->kSurfC); free(m->kSurfW); free(m->kSurfS); free(m->kLowC);
+  free(m->exchS); free(m->exchU1); free(m->exchV1); free(m->exchU0); free(m->exchV0);
+  free(m->tileFace); free(m->tileEdge);
   free(m);
 }
 
@@ -137,6 +139,8 @@ static const PDesc PTAB[] = {
   PD(GM_Small_Number), PD(GM_slopeSqCutoff),
   PI_(nonlinFreeSurf), PI_(select_rStar), PI_(quasiHydrostatic), PI_(useNHMTerms), PI_(select3dCoriScheme),
   PI_(selectP_inEOS_Zc), PI_(storePhiHyd4Phys), PI_(cg2dPreCondFreq), PD(hFacInf), PD(hFacSup),
+  PI_(vectorInvariantMomentum), PI_(selectVortScheme), PI_(selectKEscheme), PI_(upwindShear),
+  PI_(usingCurvilinearGrid),
 };
 #undef PD
 #undef PI_
@@ -239,7 +243,67 @@ int *oracle_iarray(OModel *m, const char *name, long *count) {
  * interior rows, Y pass fills S/N halos over the full width (corners
  * included, :170-198).  For a periodic lat-lon layout this equals copying,
  * for every halo point, the interior point of the wrapped global index. */
+int oracle_set_exch2(OModel *m, const long *scal, const long *u1, const long *v1, const long *u0,
+                     const long *v0, const int *face, const int *edge) {
+  const long N2 = m->n2 * m->nTiles;
+  long **dst[5] = {&m->exchS, &m->exchU1, &m->exchV1, &m->exchU0, &m->exchV0};
+  const long *src[5] = {scal, u1, v1, u0, v0};
+  for (int q = 0; q < 5; q++) {
+    free(*dst[q]);
+    *dst[q] = (long *)malloc(N2 * sizeof(long));
+    memcpy(*dst[q], src[q], N2 * sizeof(long));
+  }
+  free(m->tileFace); free(m->tileEdge);
+  m->tileFace = (int *)malloc(m->nTiles * sizeof(int));
+  m->tileEdge = (int *)malloc(m->nTiles * sizeof(int));
+  memcpy(m->tileFace, face, m->nTiles * sizeof(int));
+  memcpy(m->tileEdge, edge, m->nTiles * sizeof(int));
+  m->useCubedSphereExchange = 1;
+  return 0;
+}
+
+/* pkg/exch2 exchanges as gathers: the maps are the composition of the reference's
+ * two EXCH2_RX1/RX2 passes and corner fix-ups (mitgcm_amd/exch2.py); every source is
+ * an interior point, so the gather may run in place. */
+static void exch2_scalar(OModel *m, double *a, int nz) {
+  const long N2 = m->n2 * m->nTiles;
+  for (int k = 0; k < nz; k++) {
+    double *tmp = (double *)malloc(N2 * sizeof(double));
+    for (long q = 0; q < N2; q++) {
+      const long s = m->exchS[q], st = s / m->n2, sl = s % m->n2;
+      tmp[q] = a[sl + (long)k * m->n2 + st * m->n2 * nz];
+    }
+    for (long q = 0; q < N2; q++) a[q % m->n2 + (long)k * m->n2 + (q / m->n2) * m->n2 * nz] = tmp[q];
+    free(tmp);
+  }
+}
+
+void oracle_exch_uv_xyz(OModel *m, double *u, double *v, int nz, int withSigns) {
+  if (!m->exchS) { oracle_exch_xyz(m, u, nz); oracle_exch_xyz(m, v, nz); return; }
+  const long N2 = m->n2 * m->nTiles;
+  const long *cu = withSigns ? m->exchU1 : m->exchU0, *cv = withSigns ? m->exchV1 : m->exchV0;
+  double *tu = (double *)malloc(N2 * sizeof(double)), *tv = (double *)malloc(N2 * sizeof(double));
+  for (int k = 0; k < nz; k++) {
+#define AT(f, q) (f)[(q) % m->n2 + (long)k * m->n2 + ((q) / m->n2) * m->n2 * nz]
+    for (int c = 0; c < 2; c++) {
+      const long *code = c ? cv : cu;
+      double *out = c ? tv : tu;
+      for (long q = 0; q < N2; q++) {
+        const long e = code[q];
+        if (e == 0) { out[q] = c ? AT(v, q) : AT(u, q); continue; }
+        const long s = (e > 0 ? e : -e) - 1;
+        const double val = s < N2 ? AT(u, s) : AT(v, s - N2);
+        out[q] = e > 0 ? val : -val;
+      }
+    }
+    for (long q = 0; q < N2; q++) { AT(u, q) = tu[q]; AT(v, q) = tv[q]; }
+#undef AT
+  }
+  free(tu); free(tv);
+}
+
 void oracle_exch_xyz(OModel *m, double *a, int nz) {
+  if (m->exchS) { exch2_scalar(m, a, nz); return; }
   const int sNx = m->sNx, sNy = m->sNy, OLx = m->OLx, OLy = m->OLy;
   const int Nx = sNx * m->nSx, Ny = sNy * m->nSy;
   for (int t = 0; t < m->nTiles; t++) {

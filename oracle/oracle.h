@@ -106,6 +106,14 @@ typedef struct OModel {
   double *rSurfW, *rSurfS, *rLowW, *rLowS, *recip_Rcol, *PmEpR;            /* 2-D */
   double *phiRef;                                                          /* [2*Nr+1] */
 
+  /* --- cubed sphere (pkg/exch2) and vector-invariant momentum (pkg/mom_vecinv) --- */
+  int vectorInvariantMomentum, selectVortScheme, selectKEscheme, upwindShear, usingCurvilinearGrid;
+  int useCubedSphereExchange;
+  long *exchS;              /* EXCH2_3D_RX map: source id of every point (N2), NULL = EXCH1 */
+  long *exchU1, *exchV1;    /* EXCH2_UV_3D_RX withSigns: 0 untouched, +-(src+1), src in [u | v] */
+  long *exchU0, *exchV0;    /* same, withSigns = .FALSE. */
+  int *tileFace, *tileEdge; /* exch2_myFace; edge bits N=1 S=2 E=4 W=8 (exch2_isNedge ...) */
+
   /* --- outputs of the last SOLVE_FOR_PRESSURE --- */
   double firstResidual, minResidualSq, lastResidual, sumRHS, rhsMax;
   int numIters, nIterMin;
@@ -138,6 +146,16 @@ int oracle_ini_cg2d(OModel *m);                      /* INI_CG2D */
 /* exchanges (EXCH1, lat-lon, periodic over the nSx x nSy tile layout) */
 void oracle_exch_xy(OModel *m, double *a);
 void oracle_exch_xyz(OModel *m, double *a, int nz);
+/* EXCH_UV_XYZ_RL / EXCH_UV_XY_RL (C-grid vector pair; EXCH1: two scalar exchanges) */
+void oracle_exch_uv_xyz(OModel *m, double *u, double *v, int nz, int withSigns);
+/* install the pkg/exch2 maps built by mitgcm_amd/exch2.py (copied) */
+int oracle_set_exch2(OModel *m, const long *scal, const long *u1, const long *v1, const long *u0,
+                     const long *v0, const int *face, const int *edge);
+/* MOM_VECINV (pkg/mom_vecinv/mom_vecinv.F) for tile t, level k (vecinv.c) */
+void oracle_mom_vecinv(OModel *m, int t, int k, const double *hFacZ, const double *r_hFacZ,
+                       const double *h0FacZ, const double *kappaRU, const double *kappaRV,
+                       const double *fVerUkm, const double *fVerVkm, double *fVerUkp, double *fVerVkp,
+                       double *guDiss, double *gvDiss);
 
 /* hot path */
 void oracle_dynamics(OModel *m);                     /* DYNAMICS  (dynamics.F:21)  */

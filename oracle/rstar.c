@@ -65,8 +65,7 @@ void oracle_calc_r_star(OModel *m) {
   }
   if (bad) { fprintf(stderr, "STOP in CALC_R_STAR : too SMALL rStarFac[C,W,S] !\n"); abort(); }
   oracle_exch_xy(m, m->rStarFacC);                    /* :256-257 */
-  oracle_exch_xy(m, m->rStarFacW);                    /* EXCH_UV_XY_RL: lat-lon = scalar copies */
-  oracle_exch_xy(m, m->rStarFacS);
+  oracle_exch_uv_xyz(m, m->rStarFacW, m->rStarFacS, 1, 0);   /* EXCH_UV_XY_RL(.FALSE.) */
   for (long p = 0; p < N2; p++) {                     /* :283-298 */
     m->rStarDhCDt[p] = (m->rStarFacC[p] - m->rStarExpC[p]) / m->deltaTFreeSurf;
     m->rStarDhWDt[p] = (m->rStarFacW[p] - m->rStarExpW[p]) / m->deltaTFreeSurf;

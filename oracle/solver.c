@@ -52,8 +52,7 @@ int oracle_ini_cg2d(OModel *m) {
         m->aW2d[O2(m, i, j, t)] = m->aW2d[O2(m, i, j, t)] * myNorm;
         m->aS2d[O2(m, i, j, t)] = m->aS2d[O2(m, i, j, t)] * myNorm;
       }
-  oracle_exch_xy(m, m->aW2d); /* EXCH_UV_XY_RS(aW2d,aS2d,.FALSE.): lat-lon = scalar copies */
-  oracle_exch_xy(m, m->aS2d);
+  oracle_exch_uv_xyz(m, m->aW2d, m->aS2d, 1, 0);   /* EXCH_UV_XY_RS(aW2d,aS2d,.FALSE.) */
   m->cg2dNorm = myNorm;
   m->cg2dNormaliseRHS = (m->cg2dTargetResWunit <= 0.0);
   double tol = m->cg2dNormaliseRHS ? m->cg2dTargetResidual
@@ -78,8 +77,7 @@ int oracle_ini_cg2d(OModel *m) {
       }
   }
   oracle_exch_xy(m, m->pC);
-  oracle_exch_xy(m, m->pW);
-  oracle_exch_xy(m, m->pS);
+  oracle_exch_uv_xyz(m, m->pW, m->pS, 1, 0);       /* ini_cg2d.F:233-234 */
   (void)OLx; (void)OLy;
   return 0;
 }
@@ -416,12 +414,12 @@ void oracle_forward_step(OModel *m) {
   /* forward_step.F:965-977 CALC_R_STAR(etaH(n+1)) */
   if (rstar) oracle_calc_r_star(m);
   /* do_fields_blocking_exchanges.F:54-97 */
-  oracle_exch_xyz(m, m->uVel, m->Nr);
-  oracle_exch_xyz(m, m->vVel, m->Nr);
+  oracle_exch_uv_xyz(m, m->uVel, m->vVel, m->Nr, 1);
   oracle_exch_xyz(m, m->wVel, m->Nr);
   oracle_exch_xyz(m, m->theta, m->Nr);
   oracle_exch_xyz(m, m->salt, m->Nr);
   if (m->useCDscheme) {   /* EXCH_UV_DGRID_3D_RL(uVelD, vVelD): lat-lon = scalar copies */
+    if (m->exchS) { fprintf(stderr, "oracle: CD scheme on an exch2 topology not restated\n"); abort(); }
     oracle_exch_xyz(m, m->uVelD, m->Nr);
     oracle_exch_xyz(m, m->vVelD, m->Nr);
   }

@@ -47,6 +47,22 @@ EXPERIMENTS = {
         "inputs": ["input/pickup.0000036000", "input/pickup.0000036000.meta", "input/pickup_cd.0000036000"],
         "output": "results/output.txt",
     },
+    # cubed sphere (pkg/exch2, 6 faces of 32x32, one tile each), 1 level, vector-invariant
+    # momentum, passive salt: solid-body rotation (code/ini_vel.F, code/ini_psurf.F)
+    "solid-body.cs-32x32x1": {
+        "inputs": ["input/tile00%d.mitgrid" % f for f in range(1, 7)] + ["input/S_init.bin"],
+        "output": "results/output.txt",
+    },
+    # BASELINE config 3 (cs32x15).  Its pickup.0000072000 is not in the checkout
+    # (.MISSING_LARGE_BLOBS), so the run is a cold start from lev_T/lev_S: only the grid
+    # statistics of output.txt pin it.  Grid files are linked by input/prepare_run.
+    "global_ocean.cs32x15": {
+        "inputs": ["input/bathy_Hmin50.bin", "input/lev_T_cs_15k.bin", "input/lev_S_cs_15k.bin",
+                   "input/lev_surfT_cs_12m.bin", "input/lev_surfS_cs_12m.bin", "input/shiQnet_cs32.bin",
+                   "input/shiEmPR_cs32.bin", "input/trenberth_taux.bin", "input/trenberth_tauy.bin"] +
+                  ["../tutorial_held_suarez_cs/input/grid_cs32.face00%d.bin" % f for f in range(1, 7)],
+        "output": "results/output.txt",
+    },
 }
 
 _num = r"[-+]?\d*\.?\d+(?:[EeDd][-+]?\d+)?"
