@@ -54,6 +54,14 @@ double *mgcm_device_ptr(mgcm_model *m, const char *name);
  * offset (tile,j,i) it copies from, or -1 to leave it untouched. */
 int mgcm_set_halo_map(mgcm_model *m, const long *src_of_point, long count);
 
+/* EXCH2 C-grid vector maps (pkg/exch2/exch2_uv_3d_rx.template), for EXCH_UV_XY(Z)_RL with
+ * withSigns = .TRUE. (u1, v1) and .FALSE. (u0, v0): per point of u and of v, 0 = untouched,
+ * +(src+1) / -(src+1) = copy (minus) the value at src, which indexes [u | v] (2*count);
+ * tileFace/tileEdge (exch2_myFace, edge bits N=1 S=2 E=4 W=8) drive the cube-corner
+ * vorticity of MOM_CALC_RELVORT3.  Built by mitgcm_amd/exch2.py. */
+int mgcm_set_uv_map(mgcm_model *m, const long *u1, const long *v1, const long *u0, const long *v0,
+                    const int *tileFace, const int *tileEdge, long count);
+
 /* Finish set-up after grid/mask/operator fields are in place: builds the CG2D
  * neighbour tables and checks that the option set is one the kernels support. */
 int mgcm_init(mgcm_model *m);

@@ -35,6 +35,7 @@ def lib():
         "mgcm_get": (ci, [vp, cs, PD, cl]),
         "mgcm_device_ptr": (vp, [vp, cs]),
         "mgcm_set_halo_map": (ci, [vp, PL, cl]),
+        "mgcm_set_uv_map": (ci, [vp, PL, PL, PL, PL, PI, PI, cl]),
         "mgcm_init": (ci, [vp]),
         "mgcm_dynamics": (ci, [vp]),
         "mgcm_thermodynamics": (ci, [vp]),
@@ -68,7 +69,7 @@ def lib():
 
 
 EXPORTS = ["mgcm_create", "mgcm_destroy", "mgcm_last_error", "mgcm_set_param", "mgcm_get_param", "mgcm_put",
-           "mgcm_get", "mgcm_device_ptr", "mgcm_set_halo_map", "mgcm_init", "mgcm_dynamics", "mgcm_thermodynamics",
+           "mgcm_get", "mgcm_device_ptr", "mgcm_set_halo_map", "mgcm_set_uv_map", "mgcm_init", "mgcm_dynamics", "mgcm_thermodynamics",
            "mgcm_solve_for_pressure", "mgcm_momentum_correction_step", "mgcm_integr_continuity",
            "mgcm_blocking_exchanges", "mgcm_prepare", "mgcm_forward_step", "mgcm_sync", "mgcm_cg2d", "mgcm_solve_stats",
            "mgcm_kernel_ms", "mgcm_kernel_timing", "mgcm_set_tile_range", "mgcm_set_stream",

@@ -46,6 +46,9 @@ struct Params {
   int nonlinFreeSurf, select_rStar, quasiHydrostatic, useNHMTerms, select3dCoriScheme, selectP_inEOS_Zc;
   int storePhiHyd4Phys;
   double hFacInf;
+  // cubed sphere (pkg/exch2) + vector-invariant momentum (pkg/mom_vecinv)
+  int vectorInvariantMomentum, selectVortScheme, selectKEscheme, upwindShear, cubeCorners;
+  int staggerTimeStep, tracForcingOutAB;   // forward_step.F:1003-1036; temp_integrate.F:373-410
 };
 
 // Device pointers of every field the kernels touch.
@@ -88,6 +91,9 @@ struct Fields {
   double *rStarDhCDt, *rStarDhWDt, *rStarDhSDt, *PmEpR, *dEtaHdt;          // 2-D
   const double *maskInW, *maskInS;                                         // 2-D: kSurfW/S <= Nr
   double *dWtC, *dWtU, *dWtV;   // 3-D: MOM_CALC_RTRANS's dWtransC/U/V at each level (k_phi_hyd)
+  // vector-invariant momentum on curvilinear / cube grids
+  const double *fCoriG, *recip_rAz, *recip_dxG, *recip_dyG;   // 2-D
+  const int *tileFace, *tileEdge;   // per tile: exch2_myFace, edge bits N=1 S=2 E=4 W=8
   // solver work
   double *cg2d_b, *cg2d_x;
 };

@@ -189,6 +189,300 @@ __global__ void __launch_bounds__(256) k_phi_hyd(Dims d, Params p, Fields f) {
   }
 }
 
+
+// MOM_VECINV (pkg/mom_vecinv/mom_vecinv.F:42-1064) for one output point (i,j,k) of the
+// DYNAMICS range 0..sN+1: every intermediate the reference keeps in 2-D scratch (KE,
+// vort3, hFacZ, hDiv, the vertical viscous flux ping-pong) is re-derived at the
+// neighbours it needs with the reference's expression and operand order, including
+// MOM_CALC_RELVORT3's cube-corner circulations.  Subset (mgcm_init checks it): no
+// useAbsVorticity / high-order / upwind vorticity, constant harmonic viscosity, explicit
+// vertical viscosity, no biharmonic, no 3-D Coriolis / NH metric.  deepFac = rhoFac = 1.
+__device__ void vecinv_tend(const Dims &d, const Params &p, const Fields &f, int i, int j, int k, int t, double &gU,
+                            double &gV, double &guDiss, double &gvDiss) {
+  const int Nr = d.Nr, OLx = d.OLx, OLy = d.OLy, sNx = d.sNx, sNy = d.sNy;
+#define U(ii, jj) f.uVel[MG_I3(d, ii, jj, k, t)]
+#define V(ii, jj) f.vVel[MG_I3(d, ii, jj, k, t)]
+#define U3(ii, jj, kk) f.uVel[MG_I3(d, ii, jj, kk, t)]
+#define V3(ii, jj, kk) f.vVel[MG_I3(d, ii, jj, kk, t)]
+#define W3(ii, jj, kk) f.wVel[MG_I3(d, ii, jj, kk, t)]
+#define G2(a, ii, jj) f.a[MG_I2(d, ii, jj, t)]
+#define G3(a, ii, jj, kk) f.a[MG_I3(d, ii, jj, kk, t)]
+  const double recip_drF = f.recip_drF[k - 1], drF = f.drF[k - 1];
+  // MOM_CALC_KE (mom_calc_ke.F:66-150), computed on 1-OL..sN+OL-1
+  auto KE = [&](int ii, int jj) -> double {
+    if (ii < 1 - OLx || ii > sNx + OLx - 1 || jj < 1 - OLy || jj > sNy + OLy - 1) return 0.0;
+    const double u0 = U(ii, jj), u1 = U(ii + 1, jj), v0 = V(ii, jj), v1 = V(ii, jj + 1);
+    switch (p.selectKEscheme) {
+      case 0: return 0.25 * ((u0 * u0 + u1 * u1) + (v0 * v0 + v1 * v1));
+      case 1:
+        return 0.25 * ((u0 * u0 * G2(rAw, ii, jj) + u1 * u1 * G2(rAw, ii + 1, jj)) +
+                       (v0 * v0 * G2(rAs, ii, jj) + v1 * v1 * G2(rAs, ii, jj + 1))) * G2(recip_rA, ii, jj);
+      case 2:
+        return 0.25 * ((u0 * u0 * G3(hFacW, ii, jj, k) + u1 * u1 * G3(hFacW, ii + 1, jj, k)) +
+                       (v0 * v0 * G3(hFacS, ii, jj, k) + v1 * v1 * G3(hFacS, ii, jj + 1, k))) *
+               G3(recip_hFacC, ii, jj, k);
+      default:
+        return 0.25 * ((u0 * u0 * G3(hFacW, ii, jj, k) * G2(rAw, ii, jj) +
+                        u1 * u1 * G3(hFacW, ii + 1, jj, k) * G2(rAw, ii + 1, jj)) +
+                       (v0 * v0 * G3(hFacS, ii, jj, k) * G2(rAs, ii, jj) +
+                        v1 * v1 * G3(hFacS, ii, jj + 1, k) * G2(rAs, ii, jj + 1))) *
+               G3(recip_hFacC, ii, jj, k) * G2(recip_rA, ii, jj);
+    }
+  };
+  // MOM_CALC_RELVORT3 (mom_calc_relvort3.F:72-233) on 2-OL..sN+OL, then 0 where hFacZ = 0
+  // (mom_vecinv.F:395-403); 0 outside the computed range
+  auto vort = [&](int ii, int jj) -> double {
+    if (ii < 2 - OLx || jj < 2 - OLy || ii > sNx + OLx || jj > sNy + OLy) return 0.0;
+    if (hfacz(d, f, ii, jj, k, t) == 0.0) return 0.0;
+#define UC(a, b) (U(a, b) * G2(dxC, a, b))
+#define VC(a, b) (V(a, b) * G2(dyC, a, b))
+    const double rz = G2(recip_rAz, ii, jj);
+    if (p.cubeCorners) {
+      const int face = f.tileFace[t], e = f.tileEdge[t];
+      const bool isN = e & 1, isS = e & 2, isE = e & 4, isW = e & 8;
+      if (ii == 1 && jj == 1 && isW && isS) return rz * ((VC(ii, jj) - UC(ii, jj)) + UC(ii, jj - 1));
+      if (ii == sNx + 1 && jj == 1 && isE && isS) {
+        if (face == 2) return rz * ((-UC(ii, jj) - VC(ii - 1, jj)) + UC(ii, jj - 1));
+        if (face == 4) return rz * ((-VC(ii - 1, jj) + UC(ii, jj - 1)) - UC(ii, jj));
+        return rz * ((UC(ii, jj - 1) - UC(ii, jj)) - VC(ii - 1, jj));
+      }
+      if (ii == 1 && jj == sNy + 1 && isW && isN) {
+        if (face == 1) return rz * ((UC(ii, jj - 1) + VC(ii, jj)) - UC(ii, jj));
+        if (face == 3) return rz * ((-UC(ii, jj) + UC(ii, jj - 1)) + VC(ii, jj));
+        return rz * ((VC(ii, jj) - UC(ii, jj)) + UC(ii, jj - 1));
+      }
+      if (ii == sNx + 1 && jj == sNy + 1 && isE && isN) {
+        if (face % 2 == 1) return rz * ((-UC(ii, jj) - VC(ii - 1, jj)) + UC(ii, jj - 1));
+        return rz * ((UC(ii, jj - 1) - UC(ii, jj)) - VC(ii - 1, jj));
+      }
+    }
+    return rz * ((VC(ii, jj) - VC(ii - 1, jj)) - (UC(ii, jj) - UC(ii, jj - 1)));
+#undef UC
+#undef VC
+  };
+  auto rhz = [&](int ii, int jj) -> double {   // r_hFacZ
+    const double h = hfacz(d, f, ii, jj, k, t);
+    return h == 0.0 ? 0.0 : 1.0 / h;
+  };
+  // MOM_CALC_HDIV(hDivScheme = 2) (mom_calc_hdiv.F:76-89) on 1-OL..sN+OL-1
+  auto hDiv = [&](int ii, int jj) -> double {
+    if (ii < 1 - OLx || ii > sNx + OLx - 1 || jj < 1 - OLy || jj > sNy + OLy - 1) return 0.0;
+    return ((U(ii + 1, jj) * G2(dyG, ii + 1, jj) * G3(hFacW, ii + 1, jj, k) - U(ii, jj) * G2(dyG, ii, jj) * G3(hFacW, ii, jj, k)) +
+            (V(ii, jj + 1) * G2(dxG, ii, jj + 1) * G3(hFacS, ii, jj + 1, k) - V(ii, jj) * G2(dxG, ii, jj) * G3(hFacS, ii, jj, k))) *
+           G2(recip_rA, ii, jj) * G3(recip_hFacC, ii, jj, k);
+  };
+  const double rhFacW = G3(recip_hFacW, i, j, k), rhFacS = G3(recip_hFacS, i, j, k);
+  const double hZ = hfacz(d, f, i, j, k, t), hZn = hfacz(d, f, i, j + 1, k, t), hZe = hfacz(d, f, i + 1, j, k, t);
+  const double vz = vort(i, j), vzn = vort(i, j + 1), vze = vort(i + 1, j);
+  guDiss = 0.0; gvDiss = 0.0;
+  if (p.momViscosity) {
+    // MOM_VI_HDISSIP (mom_vi_hdissip.F:105-131) on 2-OL..sN+OL-1, constant viscosity, cosFac = 1
+    if (i >= 2 - OLx && i <= sNx + OLx - 1 && j >= 2 - OLy && j <= sNy + OLy - 1 &&
+        (p.viscAhD != 0.0 || p.viscAhZ != 0.0)) {
+      const double Dij = hDiv(i, j), Dim = hDiv(i, j - 1), Dmj = hDiv(i - 1, j);
+      const double Zip = hZn * vzn, Zij = hZ * vz, Zpj = hZe * vze;
+      const double uD2 = p.viscAhD * 1.0 * (Dij - Dmj) * G2(recip_dxC, i, j) -
+                         p.viscAhZ * rhFacW * (Zip - Zij) * G2(recip_dyG, i, j);
+      const double vD2 = p.viscAhZ * rhFacS * 1.0 * (Zpj - Zij) * G2(recip_dxG, i, j) +
+                         p.viscAhD * (Dij - Dim) * G2(recip_dyC, i, j);
+      guDiss = uD2 * G3(maskW, i, j, k);
+      gvDiss = vD2 * G3(maskS, i, j, k);
+    }
+    // MOM_U/V_RVISCFLUX(k+1) into the fVerUkp ping-pong and its k-1 partner (mom_vecinv.F:546-563)
+    auto rvU = [&](int kk) -> double {
+      if (kk <= 1 || kk > Nr) return 0.0;
+      return p.vfFacMom * 1.0 * (-p.viscAr * G2(rAw, i, j) * (U3(i, j, kk) - U3(i, j, kk - 1)) * p.rkSign *
+                                 f.recip_drC[kk - 1] * G3(maskW, i, j, kk) * G3(maskW, i, j, kk - 1));
+    };
+    auto rvV = [&](int kk) -> double {
+      if (kk <= 1 || kk > Nr) return 0.0;
+      return p.vfFacMom * 1.0 * (-p.viscAr * G2(rAs, i, j) * (V3(i, j, kk) - V3(i, j, kk - 1)) * p.rkSign *
+                                 f.recip_drC[kk - 1] * G3(maskS, i, j, kk) * G3(maskS, i, j, kk - 1));
+    };
+    guDiss = guDiss - rhFacW * recip_drF * G2(recip_rAw, i, j) * (rvU(k + 1) - rvU(k)) * p.rkSign;
+    if (p.no_slip_sides) {
+      const double hS = G3(h0FacW, i, j, k) - h0facz(d, p, f, i, j, k, t);
+      const double hN = G3(h0FacW, i, j, k) - h0facz(d, p, f, i, j + 1, k, t);
+      const double u0 = U(i, j);
+      guDiss = guDiss + -rhFacW * recip_drF * G2(recip_rAw, i, j) *
+                            (hS * G2(dxV, i, j) * G2(recip_dyU, i, j) * (p.viscAhZ * u0 - p.viscA4Z * 0.0) +
+                             hN * G2(dxV, i, j + 1) * G2(recip_dyU, i, j + 1) * (p.viscAhZ * u0 - p.viscA4Z * 0.0)) *
+                            drF * p.sideDragFactor;
+    }
+    if (p.no_slip_bottom) {
+      const int kDn = (k + 1 < Nr) ? k + 1 : Nr, kLowF = k + 1;
+      const double recDrC = (k == Nr) ? recip_drF : f.recip_drC[kLowF - 1];
+      double cD = 0.0 * 1.0;
+      cD = cD + p.viscAr * recDrC * 2.0;
+      cD = (k == Nr) ? cD * G3(maskW, i, j, k) : cD * G3(maskW, i, j, k) * (1.0 - G3(maskW, i, j, kDn));
+      guDiss = guDiss + -cD * U(i, j) * rhFacW * recip_drF;
+    }
+    gvDiss = gvDiss - rhFacS * recip_drF * G2(recip_rAs, i, j) * (rvV(k + 1) - rvV(k)) * p.rkSign;
+    if (p.no_slip_sides) {
+      const double hW = G3(h0FacS, i, j, k) - h0facz(d, p, f, i, j, k, t);
+      const double hE = G3(h0FacS, i, j, k) - h0facz(d, p, f, i + 1, j, k, t);
+      const double v0 = V(i, j);
+      gvDiss = gvDiss + -rhFacS * recip_drF * G2(recip_rAs, i, j) *
+                            (hW * G2(dyU, i, j) * G2(recip_dxV, i, j) * (p.viscAhZ * v0 - p.viscA4Z * 0.0) +
+                             hE * G2(dyU, i + 1, j) * G2(recip_dxV, i + 1, j) * (p.viscAhZ * v0 - p.viscA4Z * 0.0)) *
+                            drF * p.sideDragFactor;
+    }
+    if (p.no_slip_bottom) {
+      const int kDn = (k + 1 < Nr) ? k + 1 : Nr, kLowF = k + 1;
+      const double recDrC = (k == Nr) ? recip_drF : f.recip_drC[kLowF - 1];
+      double cD = 0.0 * 1.0;
+      cD = cD + p.viscAr * recDrC * 2.0;
+      cD = (k == Nr) ? cD * G3(maskS, i, j, k) : cD * G3(maskS, i, j, k) * (1.0 - G3(maskS, i, j, kDn));
+      gvDiss = gvDiss + -cD * V(i, j) * rhFacS * recip_drF;
+    }
+  }
+#define VX(a, b) (V(a, b) * G2(dxG, a, b))
+#define VXH(a, b) (V(a, b) * G2(dxG, a, b) * G3(hFacS, a, b, k))
+#define UY(a, b) (U(a, b) * G2(dyG, a, b))
+#define UYH(a, b) (U(a, b) * G2(dyG, a, b) * G3(hFacW, a, b, k))
+  // MOM_VI_CORIOLIS (mom_vi_coriolis.F:60-190)
+  gU = 0.0; gV = 0.0;
+  if (p.useCoriolis) {
+    const int cs = p.selectCoriScheme;
+    const double epsil = 1.0e-9;
+    double c;
+    if (cs == 0) {
+      const double vb = 0.25 * ((VX(i, j) + VX(i - 1, j)) + (VX(i, j + 1) + VX(i - 1, j + 1)));
+      c = 0.5 * (G2(fCoriG, i, j) + G2(fCoriG, i, j + 1)) * vb * G2(recip_dxC, i, j) * G3(maskW, i, j, k);
+    } else if (cs == 1) {
+      const double vb = ((VXH(i, j) + VXH(i - 1, j)) + (VXH(i, j + 1) + VXH(i - 1, j + 1))) /
+                        fmax(epsil, (G3(hFacS, i, j, k) + G3(hFacS, i - 1, j, k)) + (G3(hFacS, i, j + 1, k) + G3(hFacS, i - 1, j + 1, k)));
+      c = 0.5 * (G2(fCoriG, i, j) + G2(fCoriG, i, j + 1)) * vb * G2(recip_dxC, i, j) * G3(maskW, i, j, k);
+    } else if (cs == 2) {
+      const double vb = 0.25 * ((VXH(i, j) + VXH(i - 1, j)) + (VXH(i, j + 1) + VXH(i - 1, j + 1)));
+      c = 0.5 * (G2(fCoriG, i, j) + G2(fCoriG, i, j + 1)) * vb * G2(recip_dxC, i, j) * rhFacW;
+    } else {
+      const double vm = 0.5 * (VXH(i, j) + VXH(i - 1, j)), vp = 0.5 * (VXH(i, j + 1) + VXH(i - 1, j + 1));
+      c = 0.5 * (vm * G2(fCoriG, i, j) + vp * G2(fCoriG, i, j + 1)) * G2(recip_dxC, i, j) * rhFacW;
+    }
+    gU = c;
+    if (cs == 0) {
+      const double ub = 0.25 * ((UY(i, j) + UY(i, j - 1)) + (UY(i + 1, j) + UY(i + 1, j - 1)));
+      c = -0.5 * (G2(fCoriG, i, j) + G2(fCoriG, i + 1, j)) * ub * G2(recip_dyC, i, j) * G3(maskS, i, j, k);
+    } else if (cs == 1) {
+      const double ub = ((UYH(i, j) + UYH(i, j - 1)) + (UYH(i + 1, j) + UYH(i + 1, j - 1))) /
+                        fmax(epsil, (G3(hFacW, i, j, k) + G3(hFacW, i, j - 1, k)) + (G3(hFacW, i + 1, j, k) + G3(hFacW, i + 1, j - 1, k)));
+      c = -0.5 * (G2(fCoriG, i, j) + G2(fCoriG, i + 1, j)) * ub * G2(recip_dyC, i, j) * G3(maskS, i, j, k);
+    } else if (cs == 2) {
+      const double ub = 0.25 * ((UYH(i, j) + UYH(i, j - 1)) + (UYH(i + 1, j) + UYH(i + 1, j - 1)));
+      c = -0.5 * (G2(fCoriG, i, j) + G2(fCoriG, i + 1, j)) * ub * G2(recip_dyC, i, j) * rhFacS;
+    } else {
+      const double um = 0.5 * (UYH(i, j) + UYH(i, j - 1)), up = 0.5 * (UYH(i + 1, j) + UYH(i + 1, j - 1));
+      c = -0.5 * (um * G2(fCoriG, i, j) + up * G2(fCoriG, i + 1, j)) * G2(recip_dyC, i, j) * rhFacS;
+    }
+    gV = c;
+  }
+  if (p.momAdvection) {
+    // MOM_VI_U/V_CORIOLIS with omega3 = vort3 (mom_vi_u_coriolis.F:70-190, mom_vi_v_coriolis.F)
+    const int vs = p.selectVortScheme;
+    const double epsil = 1.0e-9, oneThird = 1.0 / 3.0;
+    double c;
+    if (vs == 0) {
+      const double vb = 0.25 * ((VXH(i, j) + VXH(i - 1, j)) + (VXH(i, j + 1) + VXH(i - 1, j + 1)));
+      c = 0.5 * (vz * rhz(i, j) + vzn * rhz(i, j + 1)) * vb * G2(recip_dxC, i, j) * G3(maskW, i, j, k);
+    } else if (vs == 1) {
+      const double vb = 0.5 * ((VX(i, j) * hZ + VX(i - 1, j) * hZ) + (VX(i, j + 1) * hZn + VX(i - 1, j + 1) * hZn)) /
+                        fmax(epsil, hZ + hZn);
+      c = 0.5 * (vz + vzn) * vb * G2(recip_dxC, i, j) * G3(maskW, i, j, k);
+    } else if (vs == 2) {
+      const double vm = 0.5 * (VXH(i, j) + VXH(i - 1, j)), vp = 0.5 * (VXH(i, j + 1) + VXH(i - 1, j + 1));
+      c = (vm * rhz(i, j) * vz + vp * rhz(i, j + 1) * vzn) * 0.5 * G2(recip_dxC, i, j) * G3(maskW, i, j, k);
+    } else {
+      c = 0.0;
+      if (i <= sNx + OLx - 1) {
+        const double rzw = rhz(i - 1, j) * vort(i - 1, j), rzwn = rhz(i - 1, j + 1) * vort(i - 1, j + 1);
+        const double rze = rhz(i + 1, j) * vze, rzen = rhz(i + 1, j + 1) * vort(i + 1, j + 1);
+        const double r0 = rhz(i, j) * vz, rn = rhz(i, j + 1) * vzn;
+        const double mj = (r0 + (rn + rzw)) * oneThird * VXH(i - 1, j);
+        const double ij = (r0 + (rn + rze)) * oneThird * VXH(i, j);
+        const double mp = (rn + (r0 + rzwn)) * oneThird * VXH(i - 1, j + 1);
+        const double ip = (rn + (r0 + rzen)) * oneThird * VXH(i, j + 1);
+        c = ((mj + ij) + (mp + ip)) * 0.25 * G2(recip_dxC, i, j) * G3(maskW, i, j, k);
+      }
+    }
+    gU = gU + c;
+    if (vs == 0) {
+      const double ub = 0.25 * ((UYH(i, j) + UYH(i, j - 1)) + (UYH(i + 1, j) + UYH(i + 1, j - 1)));
+      c = -(0.5 * (vz * rhz(i, j) + vze * rhz(i + 1, j))) * ub * G2(recip_dyC, i, j) * G3(maskS, i, j, k);
+    } else if (vs == 1) {
+      const double ub = 0.5 * ((UY(i, j) * hZ + UY(i, j - 1) * hZ) + (UY(i + 1, j) * hZe + UY(i + 1, j - 1) * hZe)) /
+                        fmax(epsil, hZ + hZe);
+      c = -(0.5 * (vz + vze)) * ub * G2(recip_dyC, i, j) * G3(maskS, i, j, k);
+    } else if (vs == 2) {
+      const double um = 0.5 * (UYH(i, j) + UYH(i, j - 1)), up = 0.5 * (UYH(i + 1, j) + UYH(i + 1, j - 1));
+      c = -((um * rhz(i, j) * vz + up * rhz(i + 1, j) * vze) * 0.5) * G2(recip_dyC, i, j) * G3(maskS, i, j, k);
+    } else {
+      c = 0.0;
+      if (j <= sNy + OLy - 1) {
+        const double r0 = rhz(i, j) * vz, re = rhz(i + 1, j) * vze;
+        const double rs = rhz(i, j - 1) * vort(i, j - 1), rn = rhz(i, j + 1) * vzn;
+        const double res = rhz(i + 1, j - 1) * vort(i + 1, j - 1), ren = rhz(i + 1, j + 1) * vort(i + 1, j + 1);
+        const double im = (r0 + (re + rs)) * oneThird * UYH(i, j - 1);
+        const double ij = (r0 + (re + rn)) * oneThird * UYH(i, j);
+        const double pm = (re + (r0 + res)) * oneThird * UYH(i + 1, j - 1);
+        const double pj = (re + (r0 + ren)) * oneThird * UYH(i + 1, j);
+        c = -(((im + ij) + (pm + pj)) * 0.25) * G2(recip_dyC, i, j) * G3(maskS, i, j, k);
+      }
+    }
+    gV = gV + c;
+    // MOM_VI_U/V_VERTSHEAR (mom_vi_u_vertshear.F:60-110)
+    {
+      const int Kp1 = k + 1 < Nr ? k + 1 : Nr, Km1 = k - 1 > 1 ? k - 1 : 1;
+      const double mKp1 = (k == Nr) ? 0.0 : 1.0, mKm1 = (k == 1) ? 0.0 : 1.0;
+      const bool areaW = !(p.selectKEscheme == 1 || p.selectKEscheme == 3);
+      double wm, wp;
+      if (areaW) {
+        wm = 0.5 * (W3(i, j, k) * G2(rA, i, j) * G3(maskC, i, j, Km1) + W3(i - 1, j, k) * G2(rA, i - 1, j) * G3(maskC, i - 1, j, Km1)) *
+             mKm1 * G2(recip_rAw, i, j);
+        wp = 0.5 * (W3(i, j, Kp1) * G2(rA, i, j) + W3(i - 1, j, Kp1) * G2(rA, i - 1, j)) * mKp1 * G2(recip_rAw, i, j);
+      } else {
+        wm = 0.5 * (W3(i, j, k) * G3(maskC, i, j, Km1) + W3(i - 1, j, k) * G3(maskC, i - 1, j, Km1)) * mKm1;
+        wp = 0.5 * (W3(i, j, Kp1) + W3(i - 1, j, Kp1)) * mKp1;
+      }
+      double zm = (U3(i, j, k) - mKm1 * U3(i, j, Km1)) * p.rkSign;
+      double zp = (mKp1 * U3(i, j, Kp1) - U3(i, j, k)) * p.rkSign;
+      if (p.upwindShear) gU = gU + -0.5 * ((wp * zp + wm * zm) + (fabs(wp) * zp - fabs(wm) * zm)) * rhFacW * recip_drF;
+      else gU = gU + -0.5 * (wp * zp + wm * zm) * rhFacW * recip_drF;
+      if (areaW) {
+        wm = 0.5 * (W3(i, j, k) * G2(rA, i, j) * G3(maskC, i, j, Km1) + W3(i, j - 1, k) * G2(rA, i, j - 1) * G3(maskC, i, j - 1, Km1)) *
+             mKm1 * G2(recip_rAs, i, j);
+        wp = 0.5 * (W3(i, j, Kp1) * G2(rA, i, j) + W3(i, j - 1, Kp1) * G2(rA, i, j - 1)) * mKp1 * G2(recip_rAs, i, j);
+      } else {
+        wm = 0.5 * (W3(i, j, k) * G3(maskC, i, j, Km1) + W3(i, j - 1, k) * G3(maskC, i, j - 1, Km1)) * mKm1;
+        wp = 0.5 * (W3(i, j, Kp1) + W3(i, j - 1, Kp1)) * mKp1;
+      }
+      zm = (V3(i, j, k) - mKm1 * V3(i, j, Km1)) * p.rkSign;
+      zp = (mKp1 * V3(i, j, Kp1) - V3(i, j, k)) * p.rkSign;
+      if (p.upwindShear) gV = gV + -0.5 * ((wp * zp + wm * zm) + (fabs(wp) * zp - fabs(wm) * zm)) * rhFacS * recip_drF;
+      else gV = gV + -0.5 * (wp * zp + wm * zm) * rhFacS * recip_drF;
+    }
+    // MOM_VI_U/V_GRAD_KE (mom_vi_u_grad_ke.F:49-55)
+    const double ke = KE(i, j);
+    gU = gU + -G2(recip_dxC, i, j) * (ke - KE(i - 1, j)) * G3(maskW, i, j, k);
+    gV = gV + -G2(recip_dyC, i, j) * (ke - KE(i, j - 1)) * G3(maskS, i, j, k);
+  }
+#undef VX
+#undef VXH
+#undef UY
+#undef UYH
+  // mom_vecinv.F:1044-1051
+  gU = gU * G3(maskW, i, j, k);
+  gV = gV * G3(maskS, i, j, k);
+#undef U
+#undef V
+#undef U3
+#undef V3
+#undef W3
+#undef G2
+#undef G3
+}
+
+template <bool VI>
 __global__ void __launch_bounds__(256) k_mom_step(Dims d, Params p, Fields f, const int *iterPtr) {
   MG_PLANE(1 - d.OLx, d.nx, 1 - d.OLy, d.ny, z)
   const int t = d.t0 + z / d.Nr, k = z % d.Nr + 1;
@@ -273,6 +567,9 @@ __global__ void __launch_bounds__(256) k_mom_step(Dims d, Params p, Fields f, co
     if (inner) {
       const double rhFacW = G3(recip_hFacW, i, j, k), rhFacS = G3(recip_hFacS, i, j, k);
       const double hZ = hfacz(d, f, i, j, k, t);
+      if constexpr (VI) {
+        vecinv_tend(d, p, f, i, j, k, t, gU, gV, guDiss, gvDiss);
+      } else {
       // ---------------- advection (mom_u_adv_uu/vu/wu.F, mom_v_adv_uv/vv/wv.F)
       if (p.momAdvection) {
         const double fVerUkm = fverU(k), fVerUkp = fverU(k + 1);
@@ -445,6 +742,7 @@ __global__ void __launch_bounds__(256) k_mom_step(Dims d, Params p, Fields f, co
       guDiss = guDiss * G3(maskW, i, j, k);
       gV = gV * G3(maskS, i, j, k);
       gvDiss = gvDiss * G3(maskS, i, j, k);
+      }   // vectorInvariantMomentum
     }
     // ---------------- TIMESTEP (timestep.F:104-388)
     double guExt = 0.0, gvExt = 0.0;
@@ -560,7 +858,13 @@ hipError_t launch_mom_step(const Dims &d, const Params &p, const Fields &f, cons
   hipLaunchKernelGGL(k_phi_hyd, dim3(mg_col_blocks(d.sNx + 3, d.sNy + 3, d.nT, d.Nr)), dim3(256), 0, s, d, p, f);
   if (p.momViscosity && (p.viscA4D != 0.0 || p.viscA4Z != 0.0))
     hipLaunchKernelGGL(k_del2uv, dim3(mg_plane_blocks(d.nx, d.ny, d.nT * d.Nr)), dim3(MG_PLANE_THREADS), 0, s, d, p, f);
-  hipLaunchKernelGGL(k_mom_step, dim3(mg_plane_blocks(d.nx, d.ny, d.nT * d.Nr)), dim3(MG_PLANE_THREADS), 0, s, d, p, f, iterPtr);
+  // MOM_VECINV or MOM_FLUXFORM: separate instantiations (no register-pressure coupling)
+  if (p.vectorInvariantMomentum)
+    hipLaunchKernelGGL(k_mom_step<true>, dim3(mg_plane_blocks(d.nx, d.ny, d.nT * d.Nr)), dim3(MG_PLANE_THREADS), 0, s,
+                       d, p, f, iterPtr);
+  else
+    hipLaunchKernelGGL(k_mom_step<false>, dim3(mg_plane_blocks(d.nx, d.ny, d.nT * d.Nr)), dim3(MG_PLANE_THREADS), 0, s,
+                       d, p, f, iterPtr);
   if (p.useCDscheme)
     hipLaunchKernelGGL(k_cd_scheme, dim3(mg_plane_blocks(d.nx - 2, d.ny - 2, d.nT * d.Nr)), dim3(MG_PLANE_THREADS), 0, s,
                        d, p, f, iterPtr);

@@ -32,18 +32,23 @@ __global__ void __launch_bounds__(256) k_calc_r_star(Dims d, Params p, Fields f,
   double fc = oc, fw = ow, fs = os;
   if (i >= 0 && i <= d.sNx + 1 && j >= 0 && j <= d.sNy + 1)   // kSurfC <= Nr <=> maskInC = 1
     fc = (f.maskInC[r] != 0.0) ? (eta[r] + f.Ro_surf[r] - f.R_low[r]) * f.recip_Rcol[r] : 1.0;
-  if (i >= 1 && i <= d.sNx + 1 && j >= 1 && j <= d.sNy) {
-    if (f.maskInW[r] != 0.0) {
-      const double tmp = f.rSurfW[r] - f.rLowW[r];
-      fw = (0.5 * (eta[r - 1] * f.rA[r - 1] + eta[r] * f.rA[r]) * f.recip_rAw[r] + tmp) / tmp;
+  // W/S factors: at the EXCH1 source as above, or (EXCH2 topology) in place on the
+  // reference's ranges, their halos then refilled through the vector map (calc_r_star())
+  const long rv = p.cubeCorners ? q : r;
+  const long lv = rv % d.n2;
+  const int iv = (int)(lv % d.nx) - d.OLx + 1, jv = (int)(lv / d.nx) - d.OLy + 1;
+  if (iv >= 1 && iv <= d.sNx + 1 && jv >= 1 && jv <= d.sNy) {
+    if (f.maskInW[rv] != 0.0) {
+      const double tmp = f.rSurfW[rv] - f.rLowW[rv];
+      fw = (0.5 * (eta[rv - 1] * f.rA[rv - 1] + eta[rv] * f.rA[rv]) * f.recip_rAw[rv] + tmp) / tmp;
     } else {
       fw = 1.0;
     }
   }
-  if (i >= 1 && i <= d.sNx && j >= 1 && j <= d.sNy + 1) {
-    if (f.maskInS[r] != 0.0) {
-      const double tmp = f.rSurfS[r] - f.rLowS[r];
-      fs = (0.5 * (eta[r - d.nx] * f.rA[r - d.nx] + eta[r] * f.rA[r]) * f.recip_rAs[r] + tmp) / tmp;
+  if (iv >= 1 && iv <= d.sNx && jv >= 1 && jv <= d.sNy + 1) {
+    if (f.maskInS[rv] != 0.0) {
+      const double tmp = f.rSurfS[rv] - f.rLowS[rv];
+      fs = (0.5 * (eta[rv - d.nx] * f.rA[rv - d.nx] + eta[rv] * f.rA[rv]) * f.recip_rAs[rv] + tmp) / tmp;
     } else {
       fs = 1.0;
     }

@@ -1025,6 +1025,23 @@ __global__ void __launch_bounds__(256) k_exchange_multi(Dims d, XFields x, const
   a[dt * lvl + (long)k * d.n2 + dl] = a[st * lvl + (long)k * d.n2 + sl];
 }
 
+// EXCH2 C-grid vector exchange (EXCH2_UV_3D_RX, pkg/exch2/exch2_uv_3d_rx.template) as one
+// gather: entry h < nU writes u, the rest v; code = +-(src+1) with src indexing [u | v].
+// The maps only ever source interior points, so the gather runs in place.
+__global__ void __launch_bounds__(256) k_exchange_uv(Dims d, double *u, double *v, const long *__restrict__ map,
+                                                     int nU, int nV) {
+  const int h = (int)(blockIdx.x * blockDim.x + threadIdx.x);
+  const int k = (int)blockIdx.y;
+  if (h >= nU + nV) return;
+  const long dst = map[2 * h], code = map[2 * h + 1];
+  const long N2 = d.n2 * d.nTiles, s = (code > 0 ? code : -code) - 1;
+  const long lvl = (long)k * d.n2;
+  auto at = [&](long g) -> long { return (g / d.n2) * d.n3 + lvl + g % d.n2; };
+  // nz levels per tile: d.n3 = n2*Nr; a 2-D field is the nz = 1 case of the same layout
+  const double val = s < N2 ? u[at(s)] : v[at(s - N2)];
+  (h < nU ? u : v)[at(dst)] = code > 0 ? val : -val;
+}
+
 // EXCH_XY_RL(cg2d_x) + etaN = recip_Bo*cg2d_x (solve_for_pressure.F:316, 377-385) in
 // one pass over every 2-D point; srcOf[q] = interior source of halo point q, or -1.
 __global__ void __launch_bounds__(256) k_exch_eta(Dims d, Fields f, const long *__restrict__ srcOf) {
@@ -1304,6 +1321,16 @@ hipError_t launch_exchange_multi(const Dims &d, const XFields &x, const long *ma
   for (int q = 0; q < x.n; q++) nzMax = x.nz[q] > nzMax ? x.nz[q] : nzMax;
   dim3 blk(256), grd((unsigned)((nHalo > 0 ? nHalo : 1) + 255) / 256, nzMax, x.n);
   hipLaunchKernelGGL(k_exchange_multi, grd, blk, 0, s, d, x, map, nHalo, ctr);
+  return hipGetLastError();
+}
+
+hipError_t launch_exchange_uv(const Dims &d, double *u, double *v, const long *map, int nU, int nV, int nz,
+                              hipStream_t s) {
+  if (nU + nV <= 0) return hipSuccess;
+  Dims dz = d;
+  dz.n3 = d.n2 * nz;   // per-tile stride of an nz-level field
+  hipLaunchKernelGGL(k_exchange_uv, dim3((unsigned)((nU + nV + 255) / 256), nz), dim3(256), 0, s, dz, u, v, map, nU,
+                     nV);
   return hipGetLastError();
 }
 

@@ -417,7 +417,7 @@ __global__ void __launch_bounds__(256) k_tracer_rhs(Dims d, Params p, Fields f, 
                         Tk * ((uT1 - uT0) * advFac + (vT1 - vT0) * advFac + (rTransKp - rTrans) * rAdvFac) * maskInC);
   double gtForc = 0.0;
   if (a.forcing && a.sfc && k == 1) gtForc = gtForc + a.sfc[q] * f.recip_drF[0] * f.recip_hFacC[q3];
-  gT = gT + gtForc;
+  if (!p.tracForcingOutAB) gT = gT + gtForc;   // inside (0) / after (1) AB2: temp_integrate.F:373-410
   if (a.useAB) {   // ADAMS_BASHFORTH2(k)
     const double ab = abFac * (gT - a.gNm1[q3]);
     double gN = gT;
@@ -426,6 +426,7 @@ __global__ void __launch_bounds__(256) k_tracer_rhs(Dims d, Params p, Fields f, 
     if (p.nonlinFreeSurf > 0 && p.select_rStar > 0) gN = gN / f.rStarExpC[q];
     a.gNm1[q3] = gN;
   }
+  if (p.tracForcingOutAB) gT = gT + gtForc;
   if (p.nonlinFreeSurf > 0 && p.select_rStar > 0) gT = gT / f.rStarExpC[q];
   // TIMESTEP_TRACER
   const double v = Tk + p.deltaTtracer * gT;

@@ -37,6 +37,7 @@ hipError_t launch_correction(const Dims &, const Params &, const Fields &, hipSt
 hipError_t launch_continuity(const Dims &, const Fields &, hipStream_t);
 hipError_t launch_bump_counter(int *, int, hipStream_t);
 hipError_t launch_exchange_multi(const Dims &, const XFields &, const long *, int, int *, hipStream_t);
+hipError_t launch_exchange_uv(const Dims &, double *, double *, const long *, int, int, int, hipStream_t);
 hipError_t launch_exch_eta(const Dims &, const Params &, const Fields &, const long *, bool, int, hipStream_t);
 hipError_t launch_corr_cont(const Dims &, const Params &, const Fields &, int, hipStream_t);
 hipError_t launch_calc_r_star(const Dims &, const Params &, const Fields &, const long *, hipStream_t);
@@ -101,6 +102,7 @@ static const FieldDesc FIELDS[] = {
     FD(rStarFacS, F2D), FD(rStarExpC, F2D), FD(rStarExpW, F2D), FD(rStarExpS, F2D), FD(rStarDhCDt, F2D),
     FD(rStarDhWDt, F2D), FD(rStarDhSDt, F2D), FD(PmEpR, F2D), FD(dEtaHdt, F2D), FD(maskInW, F2D),
     FD(maskInS, F2D), FD(dWtC, F3D), FD(dWtU, F3D), FD(dWtV, F3D),
+    FD(fCoriG, F2D), FD(recip_rAz, F2D), FD(recip_dxG, F2D), FD(recip_dyG, F2D),
 };
 #undef FD
 
@@ -129,6 +131,8 @@ static const PDesc PARAMS[] = {
     PD(GM_isopycK), PD(GM_skewflx), PD(GM_maxSlope), PD(GM_Kmin_horiz), PD(GM_Small_Number), PD(GM_slopeSqCutoff),
     PI_(nonlinFreeSurf), PI_(select_rStar), PI_(quasiHydrostatic), PI_(useNHMTerms), PI_(select3dCoriScheme),
     PI_(selectP_inEOS_Zc), PI_(storePhiHyd4Phys), PD(hFacInf),
+    PI_(vectorInvariantMomentum), PI_(selectVortScheme), PI_(selectKEscheme), PI_(upwindShear),
+    PI_(staggerTimeStep), PI_(tracForcingOutAB),
 };
 #undef PD
 #undef PI_
@@ -170,6 +174,13 @@ struct mgcm_model {
   int *d_blkx = nullptr;
   int nBlkX = 0;
   bool latlonTopology = true;   // false once a custom halo map (e.g. EXCH2 cube) is installed
+  // EXCH2 C-grid vector maps (mgcm_set_uv_map): [withSigns] -> (dst, code) pairs of this
+  // process's tiles, u entries first; code = +-(src+1), src indexing [u | v]
+  bool uvMap = false;
+  std::vector<long> h_uv[2];
+  long *d_uv[2] = {nullptr, nullptr};
+  int nUvU[2] = {0, 0}, nUvV[2] = {0, 0};
+  int *d_tileInfo = nullptr;
   // hipGraphs of two FORWARD_STEPs, one per theta/salt ping-pong parity
   bool useGraph = true;
   hipGraphExec_t graphExec[4] = {nullptr, nullptr, nullptr, nullptr};
@@ -283,6 +294,26 @@ static int upload_halo(mgcm_model *m) {
   for (size_t h = 0; h + 1 < m->h_halo.size(); h += 2)
     if (m->h_halo[h] >= lo && m->h_halo[h] < hi) { loc.push_back(m->h_halo[h]); loc.push_back(m->h_halo[h + 1]); }
   m->nHalo = (int)(loc.size() / 2);
+  if (m->uvMap) {
+    const long N2 = m->d.n2 * m->d.nTiles;
+    for (int w = 0; w < 2; w++) {
+      if (m->d_uv[w]) { hipFree(m->d_uv[w]); m->d_uv[w] = nullptr; }
+      std::vector<long> e;
+      int nu = 0, nv = 0;
+      for (int c = 0; c < 2; c++)
+        for (long q = lo; q < hi; q++) {
+          const long code = m->h_uv[w][(size_t)c * N2 + q];
+          if (code == 0) continue;
+          e.push_back(q); e.push_back(code);
+          (c ? nv : nu)++;
+        }
+      m->nUvU[w] = nu; m->nUvV[w] = nv;
+      if (!e.empty()) {
+        HIPCHK(hipMalloc(&m->d_uv[w], e.size() * sizeof(long)));
+        HIPCHK(hipMemcpy(m->d_uv[w], e.data(), e.size() * sizeof(long), hipMemcpyHostToDevice));
+      }
+    }
+  }
   if (m->nHalo == 0) return 0;
   HIPCHK(hipMalloc(&m->d_halo, loc.size() * sizeof(long)));
   HIPCHK(hipMemcpy(m->d_halo, loc.data(), loc.size() * sizeof(long), hipMemcpyHostToDevice));
@@ -530,6 +561,9 @@ void mgcm_destroy(mgcm_model *m) {
   for (void *p : m->allocs) hipFree(p);
   if (m->d_halo) hipFree(m->d_halo);
   if (m->d_srcOf) hipFree(m->d_srcOf);
+  for (int q = 0; q < 2; q++)
+    if (m->d_uv[q]) hipFree(m->d_uv[q]);
+  if (m->d_tileInfo) hipFree(m->d_tileInfo);
   if (m->d_nbr) hipFree(m->d_nbr);
   if (m->d_gofs) hipFree(m->d_gofs);
   if (m->d_nb4) hipFree(m->d_nb4);
@@ -562,7 +596,7 @@ int mgcm_set_param(mgcm_model *m, const char *name, double value) {
     }
   // options the kernels do not implement are accepted only at their default
   // (inert) value; anything else is an explicit error, never silently ignored.
-  static const char *inert[] = {"vectorInvariantMomentum", "staggerTimeStep", "implicitFreeSurface"};
+  static const char *inert[] = {"implicitFreeSurface"};
   for (auto *n : inert)
     if (!strcmp(n, name)) {
       const bool isDefaultOff = (value == 0.0) || (!strcmp(n, "implicitFreeSurface") && value == 1.0);
@@ -637,6 +671,65 @@ int mgcm_set_halo_map(mgcm_model *m, const long *src_of_point, long count) {
   return 0;
 }
 
+int mgcm_set_uv_map(mgcm_model *m, const long *u1, const long *v1, const long *u0, const long *v0,
+                    const int *tileFace, const int *tileEdge, long count) {
+  const long N2 = m->d.n2 * m->d.nTiles;
+  if (count != N2) return set_err("mgcm_set_uv_map: count %ld != %ld", count, N2);
+  const long *src[2][2] = {{u0, v0}, {u1, v1}};
+  for (int w = 0; w < 2; w++) {
+    m->h_uv[w].assign((size_t)2 * N2, 0);
+    for (int c = 0; c < 2; c++)
+      for (long q = 0; q < N2; q++) {
+        const long code = src[w][c][q];
+        const long s = (code > 0 ? code : -code) - 1;
+        if (code != 0 && (s < 0 || s >= 2 * N2)) return set_err("mgcm_set_uv_map: bad code %ld at %ld", code, q);
+        m->h_uv[w][(size_t)c * N2 + q] = code;
+      }
+  }
+  std::vector<int> info(2 * (size_t)m->d.nTiles);
+  for (int t = 0; t < m->d.nTiles; t++) { info[t] = tileFace[t]; info[m->d.nTiles + t] = tileEdge[t]; }
+  HIPCHK(hipSetDevice(m->device));
+  if (m->d_tileInfo) (void)hipFree(m->d_tileInfo);
+  HIPCHK(hipMalloc(&m->d_tileInfo, info.size() * sizeof(int)));
+  HIPCHK(hipMemcpy(m->d_tileInfo, info.data(), info.size() * sizeof(int), hipMemcpyHostToDevice));
+  m->f.tileFace = m->d_tileInfo;
+  m->f.tileEdge = m->d_tileInfo + m->d.nTiles;
+  m->p.cubeCorners = 1;
+  m->uvMap = true;
+  m->ready = false;
+  drop_graphs(m);
+  return 0;
+}
+
+// EXCH_UV_XYZ_RL / EXCH_UV_XY_RL of a C-grid vector pair: the EXCH2 vector map when one
+// is installed, else the two components through the scalar (EXCH1) map.
+static int exchange_uv(mgcm_model *m, double *u, double *v, int nz, bool withSigns) {
+  if (!m->uvMap) {
+    HIPCHK(launch_exchange(m->d, u, m->d_halo, m->nHalo, nz, m->stream));
+    HIPCHK(launch_exchange(m->d, v, m->d_halo, m->nHalo, nz, m->stream));
+    return 0;
+  }
+  const int w = withSigns ? 1 : 0;
+  HIPCHK(launch_exchange_uv(m->d, u, v, m->d_uv[w], m->nUvU[w], m->nUvV[w], nz, m->stream));
+  return 0;
+}
+
+// CALC_R_STAR (calc_r_star.F): on an EXCH2 topology k_calc_r_star evaluates the W/S
+// factors in place and EXCH_UV_XY_RL(rStarFacW, rStarFacS, .FALSE.) (calc_r_star.F:256-257)
+// refills their halos through the vector map; rStarDh*Dt and rStarExp* are pointwise
+// functions of the new and old factors, so their halos are the same copies.
+static hipError_t calc_r_star(mgcm_model *m) {
+  hipError_t e = launch_calc_r_star(m->d, m->p, m->f, m->d_srcOf, m->stream);
+  if (e != hipSuccess || !m->uvMap) return e;
+  double *pairs[3][2] = {{m->f.rStarFacW, m->f.rStarFacS}, {m->f.rStarDhWDt, m->f.rStarDhSDt},
+                         {m->f.rStarExpW, m->f.rStarExpS}};
+  for (auto &pr : pairs) {
+    e = launch_exchange_uv(m->d, pr[0], pr[1], m->d_uv[0], m->nUvU[0], m->nUvV[0], 1, m->stream);
+    if (e != hipSuccess) return e;
+  }
+  return hipSuccess;
+}
+
 int mgcm_init(mgcm_model *m) {
   HIPCHK(hipSetDevice(m->device));
   if (upload_halo(m)) return -1;
@@ -657,6 +750,20 @@ int mgcm_init(mgcm_model *m) {
   if (m->p.selectP_inEOS_Zc == 2 && !m->p.storePhiHyd4Phys)
     return set_err("mgcm_init: selectP_inEOS_Zc = 2 needs storePhiHyd4Phys (set_parms.F:297)");
   if (m->p.implicitViscosity) return set_err("mgcm_init: implicitViscosity not supported by the device path yet");
+  if (m->p.vectorInvariantMomentum) {
+    // the MOM_VECINV subset k_mom_step implements (see kernels_dyn.hip)
+    if (m->d.OLx < 2 || m->d.OLy < 2) return set_err("mgcm_init: vector-invariant momentum needs OLx, OLy >= 2");
+    if (m->p.viscA4D != 0.0 || m->p.viscA4Z != 0.0)
+      return set_err("mgcm_init: biharmonic viscosity with vectorInvariantMomentum not implemented on the device");
+    if (m->p.useNHMTerms || m->p.select3dCoriScheme > 0 || m->p.useCDscheme)
+      return set_err("mgcm_init: NH metric / 3-D Coriolis / CD scheme with vectorInvariantMomentum not implemented");
+    if (m->p.selectVortScheme < 0 || m->p.selectVortScheme > 3 || m->p.selectKEscheme < 0 || m->p.selectKEscheme > 3 ||
+        m->p.selectCoriScheme < 0 || m->p.selectCoriScheme > 3)
+      return set_err("mgcm_init: selectVortScheme/selectKEscheme/selectCoriScheme outside 0..3");
+    auto e = m->extra.find("useAbsVorticity");
+    if (e != m->extra.end() && e->second != 0.0) return set_err("mgcm_init: useAbsVorticity not implemented");
+  }
+  if (m->uvMap && m->p.useCDscheme) return set_err("mgcm_init: CD scheme on an EXCH2 topology not implemented");
   if (m->p.implicSurfPress != 1.0 || m->p.implicDiv2DFlow != 1.0)
     return set_err("mgcm_init: implicSurfPress/implicDiv2DFlow != 1 not supported yet");
   auto ext = [&](const char *n, double dflt) { auto it = m->extra.find(n); return it == m->extra.end() ? dflt : it->second; };
@@ -689,12 +796,12 @@ int mgcm_init(mgcm_model *m) {
   if (rstar) {
     // INITIALISE_VARIA (initialise_varia.F:299-349): CALC_R_STAR(etaH) -> UPDATE_R_STAR ->
     // UPDATE_CG2D -> INTEGR_CONTINUITY(nIter0) (+ UPDATE_ETAH, EXCH w) -> CALC_R_STAR(etaH)
-    HIPCHK(launch_calc_r_star(m->d, m->p, m->f, m->d_srcOf, m->stream));
+    HIPCHK(calc_r_star(m));
     HIPCHK(launch_update_r_star_cg2d(m->d, m->p, m->f, m->d_srcOf, m->stream));
     HIPCHK(launch_corr_cont(m->d, m->p, m->f, 1, m->stream));
     HIPCHK(launch_exch_eta(m->d, m->p, m->f, m->d_srcOf, true, 1, m->stream));
     HIPCHK(launch_exchange(m->d, m->f.wVel, m->d_halo, m->nHalo, m->d.Nr, m->stream));
-    HIPCHK(launch_calc_r_star(m->d, m->p, m->f, m->d_srcOf, m->stream));
+    HIPCHK(calc_r_star(m));
     HIPCHK(hipStreamSynchronize(m->stream));
   }
   m->ready = true;
@@ -808,8 +915,7 @@ int mgcm_blocking_exchanges(mgcm_model *m) {
   if (check_ready(m)) return -1;
   // do_fields_blocking_exchanges.F:54-97: uVel, vVel, wVel, theta (salt is not
   // stepped by the supported configs, its halo is unchanged)
-  TIMED(K_EXCH, launch_exchange(m->d, m->f.uVel, m->d_halo, m->nHalo, m->d.Nr, m->stream));
-  TIMED(K_EXCH, launch_exchange(m->d, m->f.vVel, m->d_halo, m->nHalo, m->d.Nr, m->stream));
+  TIMED(K_EXCH, exchange_uv(m, m->f.uVel, m->f.vVel, m->d.Nr, true) ? hipErrorUnknown : hipSuccess);
   TIMED(K_EXCH, launch_exchange(m->d, m->f.wVel, m->d_halo, m->nHalo, m->d.Nr, m->stream));
   if (m->p.tempStepping)
     TIMED(K_EXCH, launch_exchange(m->d, m->f.theta, m->d_halo, m->nHalo, m->d.Nr, m->stream));
@@ -823,8 +929,9 @@ static XFields blocking_fields(const mgcm_model *m) {
   XFields x{};
   // do_fields_blocking_exchanges.F:54-97 (+ EXCH_UV_DGRID of uVelD/vVelD with the CD scheme,
   // totPhiHyd when the EOS reads it)
+  // (on an EXCH2 topology u, v go through the vector map instead: exchange_uv)
   double *fl[] = {m->f.uVel, m->f.vVel, m->f.wVel, m->f.theta, m->f.salt, m->f.uVelD, m->f.vVelD, m->f.totPhiHyd};
-  const bool use[] = {true, true, true, m->p.tempStepping != 0, m->p.saltStepping != 0, m->p.useCDscheme != 0,
+  const bool use[] = {!m->uvMap, !m->uvMap, true, m->p.tempStepping != 0, m->p.saltStepping != 0, m->p.useCDscheme != 0,
                       m->p.useCDscheme != 0, m->p.storePhiHyd4Phys != 0};
   for (int q = 0; q < 8; q++)
     if (use[q]) { x.p[x.n] = fl[q]; x.nz[x.n] = m->d.Nr; x.n++; }
@@ -839,8 +946,14 @@ static int one_step(mgcm_model *m) {
   // tracers' other buffers and AB histories; DYNAMICS reads none of those.  So once
   // DO_OCEANIC_PHYS is done the two run concurrently (second stream), joined before
   // UPDATE_R_STAR / SOLVE_FOR_PRESSURE (which rewrite hFac, then u, v, w).
-  const bool fork = m->overlap && !m->timing && m->p.momStepping && (m->p.tempStepping || m->p.saltStepping);
-  if (fork) {
+  // staggerTimeStep (forward_step.F:1003-1036): THERMODYNAMICS after the pressure solve and
+  // continuity, with the new velocities; DO_OCEANIC_PHYS still opens the step
+  const bool stagger = m->p.staggerTimeStep != 0 && m->p.momStepping;
+  const bool tracers = m->p.tempStepping || m->p.saltStepping;
+  const bool fork = !stagger && m->overlap && !m->timing && m->p.momStepping && tracers;
+  if (stagger) {
+    if (tracers) TIMED(K_PHYS, launch_oceanic_phys(m->d, m->p, m->f, m->d_ctr, m->stream));
+  } else if (fork) {
     TIMED(K_PHYS, launch_oceanic_phys(m->d, m->p, m->f, m->d_ctr, m->stream));
     HIPCHK(hipEventRecord(m->evFork, m->stream));
     HIPCHK(hipStreamWaitEvent(m->stream2, m->evFork, 0));
@@ -861,10 +974,17 @@ static int one_step(mgcm_model *m) {
     if (m->p.exactConserv) TIMED(K_ETA, launch_exch_eta(m->d, m->p, m->f, m->d_srcOf, true, 0, m->stream));
     // forward_step.F:965-977: CALC_R_STAR(etaH(n+1)); the next step's RESET_NLFS_VARS +
     // UPDATE_R_STAR(.FALSE.) restore the hFac in place, so they are not repeated here
-    if (m->p.nonlinFreeSurf > 0) TIMED(K_RSTAR, launch_calc_r_star(m->d, m->p, m->f, m->d_srcOf, m->stream));
+    if (m->p.nonlinFreeSurf > 0) TIMED(K_RSTAR, calc_r_star(m));
   } else {
     if (mgcm_integr_continuity(m)) return -1;
   }
+  if (stagger && tracers) {
+    // DO_STAGGER_FIELDS_EXCHANGES (do_stagger_fields_exchanges.F:37-43) + THERMODYNAMICS
+    TIMED(K_EXCH, exchange_uv(m, m->f.uVel, m->f.vVel, m->d.Nr, true) ? hipErrorUnknown : hipSuccess);
+    TIMED(K_EXCH, launch_exchange(m->d, m->f.wVel, m->d_halo, m->nHalo, m->d.Nr, m->stream));
+    if (tracers_on(m, m->stream)) return -1;
+  }
+  if (m->uvMap) TIMED(K_EXCH, exchange_uv(m, m->f.uVel, m->f.vVel, m->d.Nr, true) ? hipErrorUnknown : hipSuccess);
   TIMED(K_EXCH, launch_exchange_multi(m->d, blocking_fields(m), m->d_halo, m->nHalo, m->d_ctr, m->stream));
   return 0;
 }
@@ -986,6 +1106,7 @@ int mgcm_begin_steps(mgcm_model *m) {
 int mgcm_step_phase(mgcm_model *m, int phase) {
   if (check_ready(m)) return -1;
   if (!m->p.momStepping) return set_err("mgcm_step_phase: requires momStepping");
+  if (m->p.staggerTimeStep) return set_err("mgcm_step_phase: staggerTimeStep not implemented for tile-sharded runs");
   switch (phase) {
     case 1:
       if (mgcm_thermodynamics(m) || mgcm_dynamics(m)) return -1;

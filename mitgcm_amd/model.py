@@ -17,7 +17,8 @@ GRID_2D = ("dxF", "dyF", "dxG", "dyG", "dxC", "dyC", "dxV", "dyU", "rA", "rAw", 
            "recip_dxF", "recip_dyF", "recip_dxC", "recip_dyC", "recip_dxV", "recip_dyU",
            "recip_rA", "recip_rAw", "recip_rAs", "fCori", "Bo_surf", "recip_Bo",
            "aW2d", "aS2d", "aC2d", "pW", "pS", "pC", "maskInC", "tanPhiAtU", "tanPhiAtV",
-           "fCoriCos", "recip_Rcol", "rSurfW", "rSurfS", "rLowW", "rLowS", "Ro_surf", "R_low", "maskInW", "maskInS")
+           "fCoriCos", "recip_Rcol", "rSurfW", "rSurfS", "rLowW", "rLowS", "Ro_surf", "R_low", "maskInW", "maskInS",
+           "fCoriG", "recip_rAz", "recip_dxG", "recip_dyG")
 GRID_3D = ("hFacC", "hFacW", "hFacS", "recip_hFacC", "recip_hFacW", "recip_hFacS", "maskC", "maskW", "maskS",
            "h0FacC", "h0FacW", "h0FacS")
 GRID_1D = ("drF", "drC", "recip_drF", "recip_drC", "rF", "rC")
@@ -36,7 +37,8 @@ DEVICE_PARAMS = ("deltaTMom", "deltaTFreeSurf", "deltaTClock", "abEps", "rhoCons
                  "implicDiv2DFlow", "rkSign", "afFacMom", "vfFacMom", "pfFacMom", "cfFacMom", "foFacMom",
                  "mtFacMom", "momAdvection", "momViscosity", "momForcing", "useCoriolis", "no_slip_sides",
                  "no_slip_bottom", "selectCoriScheme", "momForcingOutAB", "momDissip_In_AB", "implicitViscosity",
-                 "cg2dMaxIters", "cg2dUseMinResSol", "nIter0")
+                 "cg2dMaxIters", "cg2dUseMinResSol", "nIter0", "vectorInvariantMomentum", "selectVortScheme",
+                 "selectKEscheme", "upwindShear")
 
 
 def _dp(a):
@@ -71,6 +73,17 @@ class Model:
         src = np.ascontiguousarray(g.topo.src_of_point(), dtype=np.int64)
         check(L.mgcm_set_halo_map(self.h, src.ctypes.data_as(ctypes.POINTER(ctypes.c_long)), src.size),
               "mgcm_set_halo_map")
+        if hasattr(g.topo, "uv_codes"):     # pkg/exch2 topology: C-grid vector maps + cube corners
+            topo = g.topo
+            LP = lambda a: a.ctypes.data_as(ctypes.POINTER(ctypes.c_long))
+            IP = lambda a: a.ctypes.data_as(ctypes.POINTER(ctypes.c_int))
+            u1, v1 = (np.ascontiguousarray(x, dtype=np.int64) for x in topo.uv_codes(True))
+            u0, v0 = (np.ascontiguousarray(x, dtype=np.int64) for x in topo.uv_codes(False))
+            face = np.ascontiguousarray(topo.face[1:], dtype=np.int32)
+            edge = np.ascontiguousarray([topo.isN[t] | 2 * topo.isS[t] | 4 * topo.isE[t] | 8 * topo.isW[t]
+                                         for t in range(1, topo.nTiles + 1)], dtype=np.int32)
+            check(L.mgcm_set_uv_map(self.h, LP(u1), LP(v1), LP(u0), LP(v0), IP(face), IP(edge), u1.size),
+                  "mgcm_set_uv_map")
 
     def init(self):
         check(lib().mgcm_init(self.h), "mgcm_init")

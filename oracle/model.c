@@ -140,7 +140,7 @@ static const PDesc PTAB[] = {
   PI_(nonlinFreeSurf), PI_(select_rStar), PI_(quasiHydrostatic), PI_(useNHMTerms), PI_(select3dCoriScheme),
   PI_(selectP_inEOS_Zc), PI_(storePhiHyd4Phys), PI_(cg2dPreCondFreq), PD(hFacInf), PD(hFacSup),
   PI_(vectorInvariantMomentum), PI_(selectVortScheme), PI_(selectKEscheme), PI_(upwindShear),
-  PI_(usingCurvilinearGrid),
+  PI_(usingCurvilinearGrid), PI_(staggerTimeStep), PI_(tracForcingOutAB),
 };
 #undef PD
 #undef PI_

@@ -109,6 +109,7 @@ typedef struct OModel {
   /* --- cubed sphere (pkg/exch2) and vector-invariant momentum (pkg/mom_vecinv) --- */
   int vectorInvariantMomentum, selectVortScheme, selectKEscheme, upwindShear, usingCurvilinearGrid;
   int useCubedSphereExchange;
+  int staggerTimeStep, tracForcingOutAB;   /* forward_step.F:724-1036; temp_integrate.F:373-410 */
   long *exchS;              /* EXCH2_3D_RX map: source id of every point (N2), NULL = EXCH1 */
   long *exchU1, *exchV1;    /* EXCH2_UV_3D_RX withSigns: 0 untouched, +-(src+1), src in [u | v] */
   long *exchU0, *exchV0;    /* same, withSigns = .FALSE. */

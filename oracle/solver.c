@@ -394,7 +394,7 @@ void oracle_forward_step(OModel *m) {
   oracle_fields_load(m);
   /* forward_step.F:656 DO_OCEANIC_PHYS (always called: surface forcing, rhoInSitu, ...) */
   oracle_oceanic_phys(m);
-  if (m->tempStepping || m->saltStepping) {
+  if ((m->tempStepping || m->saltStepping) && !m->staggerTimeStep) {
     /* forward_step.F:732 THERMODYNAMICS (staggerTimeStep = F) */
     oracle_thermodynamics(m);
   }
@@ -413,6 +413,13 @@ void oracle_forward_step(OModel *m) {
   oracle_integr_continuity(m);
   /* forward_step.F:965-977 CALC_R_STAR(etaH(n+1)) */
   if (rstar) oracle_calc_r_star(m);
+  if ((m->tempStepping || m->saltStepping) && m->staggerTimeStep) {
+    /* forward_step.F:1003-1036: DO_STAGGER_FIELDS_EXCHANGES (u, v, w;
+     * do_stagger_fields_exchanges.F:37-43), then THERMODYNAMICS with the new velocities */
+    oracle_exch_uv_xyz(m, m->uVel, m->vVel, m->Nr, 1);
+    oracle_exch_xyz(m, m->wVel, m->Nr);
+    oracle_thermodynamics(m);
+  }
   /* do_fields_blocking_exchanges.F:54-97 */
   oracle_exch_uv_xyz(m, m->uVel, m->vVel, m->Nr, 1);
   oracle_exch_xyz(m, m->wVel, m->Nr);

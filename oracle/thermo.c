@@ -375,15 +375,17 @@ static void tracer_integrate(OModel *m, const TracerSpec *c) {
                T * ((L(uTrans, i + 1, j) - L(uTrans, i, j)) * advFac + (L(vTrans, i, j + 1) - L(vTrans, i, j)) * advFac +
                     (L(rTransKp, i, j) - L(rTrans, i, j)) * rAdvFac) * L(maskInC, i, j));
         }
-      /* gT += gtForc (tracForcingOutAB = 0), then ADAMS_BASHFORTH2(k) when AB is on */
+      /* gT += gtForc inside (tracForcingOutAB = 0) or after (= 1) ADAMS_BASHFORTH2(k)
+       * (temp_integrate.F:373-410) */
       for (int j = 1 - OLy; j <= sNy + OLy; j++)
         for (int i = 1 - OLx; i <= sNx + OLx; i++) {
-          W3(gT, i, j, k) = W3(gT, i, j, k) + L(gtForc, i, j);
+          if (!m->tracForcingOutAB) W3(gT, i, j, k) = W3(gT, i, j, k) + L(gtForc, i, j);
           if (useAB) {
             double ab = abFac * (W3(gT, i, j, k) - W3(gtNm1, i, j, k));
             W3(gtNm1, i, j, k) = W3(gT, i, j, k);
             W3(gT, i, j, k) = W3(gT, i, j, k) + ab;
           }
+          if (m->tracForcingOutAB) W3(gT, i, j, k) = W3(gT, i, j, k) + L(gtForc, i, j);
         }
       if (rstar)   /* FREESURF_RESCALE_G (freesurf_rescale_g.F:52-62) of gT and gtNm1 (temp_integrate.F:412-446) */
         for (int j = 1 - OLy; j <= sNy + OLy; j++)
