@@ -380,3 +380,86 @@ def solid_body_cs32(data_dir=None):
              "theta": np.full((g.nTiles, 1, g.ny, g.nx), 300.0), "tRef": np.array([300.0]),
              "sRef": np.array([0.0])}
     return g, params, state
+
+
+CS32_FORCING = {"taux": "trenberth_taux.bin", "tauy": "trenberth_tauy.bin", "Qnet": "shiQnet_cs32.bin",
+                "EmPmR": "shiEmPR_cs32.bin", "SST": "lev_surfT_cs_12m.bin", "SSS": "lev_surfS_cs_12m.bin"}
+
+
+def global_ocean_cs32x15(data_dir=None):
+    """verification/global_ocean.cs32x15 (BASELINE config 2 on the cube): 6 faces of 32x32,
+    code/SIZE.h sNx=32, sNy=16, OL=4, nSx=12 (two tiles per face, pkg/exch2), 15 levels,
+    curvilinear grid from grid_cs32.faceNNN.bin (18 records incl. AngleCS/SN,
+    radius_fromHorizGrid=6370e3), bathy_Hmin50.bin.  input/data: viscAh=3e5, viscAr=1e-3,
+    diffKrT=diffKrS=3e-5, ivdc_kappa=10, implicitDiffusion, JMD95Z, staggerTimeStep,
+    vectorInvariantMomentum, exactConserv, r* (select_rStar=2, nonlinFreeSurf=4,
+    hFacInf=0.2, hFacSup=2), useRealFreshWaterFlux, allowFreezing, hFacMin=0.1,
+    hFacMinDr=20, cg2dMaxIters=200, cg2dTargetResWunit=1e-14, deltaTMom=1200,
+    deltaTtracer=deltaTFreeSurf=deltaTClock=86400, abEps=0.1, tracForcingOutAB=1, monthly
+    periodic forcing, SST/SSS relaxation (5184000 s, 62208000 s), GM-Redi K=800.
+    Cold start (nIter0=0) from lev_T/S_cs_15k (the reference restarts from
+    pickup.0000072000, which the reference tree does not hold); GM in skew-flux form
+    (the reference sets GM_AdvForm, not implemented here)."""
+    d = data_dir or os.path.join(GOLDEN, "global_ocean.cs32x15")
+    n, Nr = 32, 15
+    topo = cube_topology(n, 32, 16, 4)
+    g = Grid(32, 16, 4, 4, Nr, nSx=topo.nTiles, nSy=1, topology=topo)
+    g.usingCurvilinearGrid = True
+    g.ini_vertical_grid(LATLON_DELR)
+    recs = [np.fromfile(os.path.join(d, "grid_cs32.face%03d.bin" % f), dtype=">f8").astype(np.float64)
+            .reshape(18, n + 1, n + 1) for f in range(1, 7)]
+    g.ini_curvilinear_grid(recs, radius_fromHorizGrid=6370.0e3, rSphere=6370.0e3, anglesFromFile=True)
+    g.ini_cori(selectCoriMap=2)
+    rd = lambda fn, shp: np.fromfile(os.path.join(d, fn), dtype=">f8").astype(np.float64).reshape(shp)
+    bathy = cs_global_to_tiles(g, rd("bathy_Hmin50.bin", (6 * n, n)))
+    g.ini_depths_masks(bathy, hFacMin=0.1, hFacMinDr=20.0, gBaro=9.81)
+    g.ini_cg2d(1200.0, 86400.0, 1e-7, cg2dTargetResWunit=1e-14)
+    rhoConstFresh = 1000.0
+    forcing = {}
+    for name, fn in CS32_FORCING.items():
+        rec = np.moveaxis(cs_global_to_tiles(g, rd(fn, (12, 6 * n, n))), 0, 1).copy()   # (nTiles, 12, ny, nx)
+        if name == "EmPmR":
+            rec = rec * rhoConstFresh
+        if name in ("taux", "tauy"):
+            forcing[name] = rec
+        else:
+            forcing[name] = np.moveaxis(g.exch(rec), 1, 0).copy()
+    fu, fv = topo.exchange_uv(forcing.pop("taux"), forcing.pop("tauy"), True)   # EXCH_UV_XY_RS(fu,fv,.TRUE.)
+    forcing["taux"], forcing["tauy"] = np.moveaxis(fu, 1, 0).copy(), np.moveaxis(fv, 1, 0).copy()
+    mC = g.f["maskC"]
+    theta = g.exch(cs_global_to_tiles(g, rd("lev_T_cs_15k.bin", (Nr, 6 * n, n))).swapaxes(0, 1).copy())
+    theta[mC == 0.0] = 0.0
+    theta = np.where(theta < -1.9, -1.9, theta)         # ini_theta.F: checkIniTemp .AND. allowFreezing
+    salt = g.exch(cs_global_to_tiles(g, rd("lev_S_cs_15k.bin", (Nr, 6 * n, n))).swapaxes(0, 1).copy())
+    salt[mC == 0.0] = 0.0
+    params = dict(deltaTMom=1200.0, deltaTFreeSurf=86400.0, deltaTClock=86400.0, deltaTtracer=86400.0,
+                  abEps=0.1, rhoConst=1035.0, rhoNil=1035.0, rhoConstFresh=rhoConstFresh, gravity=9.81,
+                  gBaro=9.81, viscAhD=3e5, viscAhZ=3e5, viscA4D=0.0, viscA4Z=0.0, viscAr=1e-3,
+                  sideDragFactor=2.0, selectCoriScheme=0, vectorInvariantMomentum=1, selectVortScheme=1,
+                  selectKEscheme=0, momForcingOutAB=0, momDissip_In_AB=1, cg2dMaxIters=200, cg2dUseMinResSol=0,
+                  nIter0=0, no_slip_sides=1, no_slip_bottom=1, exactConserv=1, staggerTimeStep=1,
+                  tracForcingOutAB=1, tempStepping=1, tempAdvection=1, tempForcing=1, tempAdvScheme=2,
+                  tempVertAdvScheme=2, saltStepping=1, saltAdvection=1, saltForcing=1, saltAdvScheme=2,
+                  saltVertAdvScheme=2, diffKhT=0.0, diffKrT=3e-5, diffKhS=0.0, diffKrS=3e-5,
+                  ivdc_kappa=10.0, implicitDiffusion=1, usingCurvilinearGrid=1, rSphere=6370.0e3,
+                  integr_GeoPot=2, eosType=1, allowFreezing=1, useRealFreshWaterFlux=1, HeatCapacity_Cp=3994.0,
+                  convertFW2Salt=-1.0, temp_EvPrRn=123456.7, salt_EvPrRn=0.0, periodicExternalForcing=1,
+                  externForcingPeriod=2592000.0, externForcingCycle=31104000.0, useGMRedi=1,
+                  GM_background_K=800.0, GM_isopycK=800.0, GM_skewflx=1.0, GM_maxSlope=1e-2,
+                  GM_Kmin_horiz=50.0, nonlinFreeSurf=4, select_rStar=2, hFacInf=0.2, hFacSup=2.0,
+                  cg2dPreCondFreq=1)
+    pRef = np.array([0.0 + 1035.0 * (g.f["rC"][k] - g.f["rF"][0]) * 9.81 * -1.0 for k in range(Nr)])
+    rC, rF = g.f["rC"], g.f["rF"]
+    phiRef = np.zeros(2 * Nr + 1)
+    for k in range(Nr):
+        phiRef[2 * k + 1] = phiRef[0] + (rC[k] - rF[0]) * 9.81 * -1.0
+        phiRef[2 * k + 2] = phiRef[0] + (rF[k + 1] - rF[0]) * 9.81 * -1.0
+    lamT = np.full((g.nTiles, g.ny, g.nx), 1.0 / 5184000.0)
+    lamS = np.full((g.nTiles, g.ny, g.nx), 1.0 / 62208000.0)
+    state = {"theta": theta, "salt": salt, "tRef": np.full(Nr, 20.0), "sRef": np.full(Nr, 35.0),
+             "pRef4EOS": pRef, "phiRef": phiRef, "lambdaThetaClimRelax": lamT, "lambdaSaltClimRelax": lamS,
+             "fu": forcing["taux"][0], "fv": forcing["tauy"][0], "Qnet": forcing["Qnet"][0],
+             "EmPmR": forcing["EmPmR"][0], "SST": forcing["SST"][0], "SSS": forcing["SSS"][0]}
+    for nm in ("h0FacC", "h0FacW", "h0FacS", "recip_Rcol", "rLowW", "rLowS", "rSurfW", "rSurfS"):
+        state[nm] = g.f[nm]
+    return g, params, state, forcing

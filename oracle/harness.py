@@ -250,6 +250,20 @@ def ocean90_oracle(**kw):
     return o, g
 
 
+def cs32x15_oracle(**kw):
+    """verification/global_ocean.cs32x15 (cold start, mitgcm_amd.configs.global_ocean_cs32x15)
+    as the oracle, with the 12 forcing records and INITIALISE_VARIA's r* sequence."""
+    from mitgcm_amd import configs
+    g, params, state, forcing = configs.global_ocean_cs32x15(**kw)
+    o, _ = oracle_from_config(lambda: (g, params, state))
+    names = {"taux": "forcTaux", "tauy": "forcTauy", "Qnet": "forcQnet", "EmPmR": "forcEmPmR", "SST": "forcSST",
+             "SSS": "forcSSS"}
+    for k, v in forcing.items():
+        o.arr(names[k])[:] = np.ravel(v)
+    o.L.oracle_ini_nlfs_pickup(o.h)
+    return o, g
+
+
 def read_bin(path, shape, dtype=">f4"):
     return np.fromfile(path, dtype=dtype).astype(np.float64).reshape(shape)
 
