@@ -43,7 +43,7 @@ def parse():
                     help="N>1: shard the workload's tiles over the N processes (RCCL, strong scaling, "
                          "mitgcm_amd/parallel.py) instead of running N replicas")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
-    ap.add_argument("--pmc-summary", default=os.path.join(ROOT, "profiles", "r01", "ocean90", "pmc_summary.json"),
+    ap.add_argument("--pmc-summary", default=os.path.join(ROOT, "profiles", "r02", "ocean90", "pmc_summary.json"),
                     help="tools/pmc_summary.py output of rocprofv3 --pmc passes of this command (roofline.traffic)")
     return ap.parse_args()
 

@@ -298,9 +298,12 @@ def global_ocean_90x40x15(nSx=1, nSy=1, OL=3, data_dir=None, pickup_dir=None):
     return g, params, state, forcing
 
 
-def cs_global_to_tiles(g, glob):
-    """Global cube-sphere MDS field (W2_mapIO = 1: facets stacked in y, (..., 6*n, n),
-    w2_set_map_tiles.F:160-175) -> tile layout (..., nTiles, ny, nx), interiors only."""
+def cs_global_to_tiles(g, glob, mapIO=1):
+    """Global cube-sphere MDS field -> tile layout (..., nTiles, ny, nx), interiors only.
+    W2_SET_MAP_TILES (w2_set_map_tiles.F:136-205): W2_mapIO = 1 (compact, data.exch2 of
+    solid-body.cs-32x32x1) stacks the facets in y, (..., 6*n, n); W2_mapIO = -1 (the
+    default, w2_readparms.F:64, e.g. global_ocean.cs32x15 which has no data.exch2) puts
+    them one after the other in x, (..., n, 6*n)."""
     topo = g.topo
     lead = glob.shape[:-2]
     out = np.zeros(lead + (g.nTiles, g.ny, g.nx))
@@ -309,9 +312,13 @@ def cs_global_to_tiles(g, glob):
     for t in range(g.nTiles):
         tid = t + 1
         f = topo.face[tid]
-        nb = sum(fx * fy for fx, fy in topo.facet_dims[:f - 1])
-        ii = nb + topo.tBx[tid] + topo.tBy[tid] * topo.facet_dims[f - 1][0]
-        x0, y0 = ii % gNx, ii // gNx
+        if mapIO == -1:
+            x0 = sum(fx for fx, _ in topo.facet_dims[:f - 1]) + topo.tBx[tid]
+            y0 = topo.tBy[tid]
+        else:
+            nb = sum(fx * fy for fx, fy in topo.facet_dims[:f - 1])
+            ii = nb + topo.tBx[tid] + topo.tBy[tid] * topo.facet_dims[f - 1][0]
+            x0, y0 = ii % gNx, ii // gNx
         out[(Ellipsis, t) + inner] = glob[..., y0:y0 + g.sNy, x0:x0 + g.sNx]
     return out
 
@@ -386,9 +393,10 @@ CS32_FORCING = {"taux": "trenberth_taux.bin", "tauy": "trenberth_tauy.bin", "Qne
                 "EmPmR": "shiEmPR_cs32.bin", "SST": "lev_surfT_cs_12m.bin", "SSS": "lev_surfS_cs_12m.bin"}
 
 
-def global_ocean_cs32x15(data_dir=None):
-    """verification/global_ocean.cs32x15 (BASELINE config 2 on the cube): 6 faces of 32x32,
-    code/SIZE.h sNx=32, sNy=16, OL=4, nSx=12 (two tiles per face, pkg/exch2), 15 levels,
+def global_ocean_cs32x15(data_dir=None, sNy=32):
+    """verification/global_ocean.cs32x15 (BASELINE config 3): 6 faces of 32x32 on pkg/exch2,
+    one 32x32 tile per face at OL=4 (SURVEY 8(d) C3 layout; sNy=16 gives the reference's
+    code/SIZE.h tiling sNx=32, sNy=16, nSx=12, two tiles per face), 15 levels,
     curvilinear grid from grid_cs32.faceNNN.bin (18 records incl. AngleCS/SN,
     radius_fromHorizGrid=6370e3), bathy_Hmin50.bin.  input/data: viscAh=3e5, viscAr=1e-3,
     diffKrT=diffKrS=3e-5, ivdc_kappa=10, implicitDiffusion, JMD95Z, staggerTimeStep,
@@ -397,13 +405,14 @@ def global_ocean_cs32x15(data_dir=None):
     hFacMinDr=20, cg2dMaxIters=200, cg2dTargetResWunit=1e-14, deltaTMom=1200,
     deltaTtracer=deltaTFreeSurf=deltaTClock=86400, abEps=0.1, tracForcingOutAB=1, monthly
     periodic forcing, SST/SSS relaxation (5184000 s, 62208000 s), GM-Redi K=800.
+    GM-Redi in the advective (bolus stream-function) form, input/data.gmredi GM_AdvForm
+    (gmredi_readparms.F:243-250: GM_skewflx = 0, GM_ExtraDiag = GM_isopycK != 0).
     Cold start (nIter0=0) from lev_T/S_cs_15k (the reference restarts from
-    pickup.0000072000, which the reference tree does not hold); GM in skew-flux form
-    (the reference sets GM_AdvForm, not implemented here)."""
+    pickup.0000072000, which the reference tree does not hold)."""
     d = data_dir or os.path.join(GOLDEN, "global_ocean.cs32x15")
     n, Nr = 32, 15
-    topo = cube_topology(n, 32, 16, 4)
-    g = Grid(32, 16, 4, 4, Nr, nSx=topo.nTiles, nSy=1, topology=topo)
+    topo = cube_topology(n, 32, sNy, 4)
+    g = Grid(32, sNy, 4, 4, Nr, nSx=topo.nTiles, nSy=1, topology=topo)
     g.usingCurvilinearGrid = True
     g.ini_vertical_grid(LATLON_DELR)
     recs = [np.fromfile(os.path.join(d, "grid_cs32.face%03d.bin" % f), dtype=">f8").astype(np.float64)
@@ -411,13 +420,13 @@ def global_ocean_cs32x15(data_dir=None):
     g.ini_curvilinear_grid(recs, radius_fromHorizGrid=6370.0e3, rSphere=6370.0e3, anglesFromFile=True)
     g.ini_cori(selectCoriMap=2)
     rd = lambda fn, shp: np.fromfile(os.path.join(d, fn), dtype=">f8").astype(np.float64).reshape(shp)
-    bathy = cs_global_to_tiles(g, rd("bathy_Hmin50.bin", (6 * n, n)))
+    bathy = cs_global_to_tiles(g, rd("bathy_Hmin50.bin", (n, 6 * n)), mapIO=-1)   # no data.exch2
     g.ini_depths_masks(bathy, hFacMin=0.1, hFacMinDr=20.0, gBaro=9.81)
     g.ini_cg2d(1200.0, 86400.0, 1e-7, cg2dTargetResWunit=1e-14)
     rhoConstFresh = 1000.0
     forcing = {}
     for name, fn in CS32_FORCING.items():
-        rec = np.moveaxis(cs_global_to_tiles(g, rd(fn, (12, 6 * n, n))), 0, 1).copy()   # (nTiles, 12, ny, nx)
+        rec = np.moveaxis(cs_global_to_tiles(g, rd(fn, (12, n, 6 * n)), mapIO=-1), 0, 1).copy()   # (nTiles, 12, ny, nx)
         if name == "EmPmR":
             rec = rec * rhoConstFresh
         if name in ("taux", "tauy"):
@@ -427,10 +436,10 @@ def global_ocean_cs32x15(data_dir=None):
     fu, fv = topo.exchange_uv(forcing.pop("taux"), forcing.pop("tauy"), True)   # EXCH_UV_XY_RS(fu,fv,.TRUE.)
     forcing["taux"], forcing["tauy"] = np.moveaxis(fu, 1, 0).copy(), np.moveaxis(fv, 1, 0).copy()
     mC = g.f["maskC"]
-    theta = g.exch(cs_global_to_tiles(g, rd("lev_T_cs_15k.bin", (Nr, 6 * n, n))).swapaxes(0, 1).copy())
+    theta = g.exch(cs_global_to_tiles(g, rd("lev_T_cs_15k.bin", (Nr, n, 6 * n)), mapIO=-1).swapaxes(0, 1).copy())
     theta[mC == 0.0] = 0.0
     theta = np.where(theta < -1.9, -1.9, theta)         # ini_theta.F: checkIniTemp .AND. allowFreezing
-    salt = g.exch(cs_global_to_tiles(g, rd("lev_S_cs_15k.bin", (Nr, 6 * n, n))).swapaxes(0, 1).copy())
+    salt = g.exch(cs_global_to_tiles(g, rd("lev_S_cs_15k.bin", (Nr, n, 6 * n)), mapIO=-1).swapaxes(0, 1).copy())
     salt[mC == 0.0] = 0.0
     params = dict(deltaTMom=1200.0, deltaTFreeSurf=86400.0, deltaTClock=86400.0, deltaTtracer=86400.0,
                   abEps=0.1, rhoConst=1035.0, rhoNil=1035.0, rhoConstFresh=rhoConstFresh, gravity=9.81,
@@ -445,7 +454,8 @@ def global_ocean_cs32x15(data_dir=None):
                   integr_GeoPot=2, eosType=1, allowFreezing=1, useRealFreshWaterFlux=1, HeatCapacity_Cp=3994.0,
                   convertFW2Salt=-1.0, temp_EvPrRn=123456.7, salt_EvPrRn=0.0, periodicExternalForcing=1,
                   externForcingPeriod=2592000.0, externForcingCycle=31104000.0, useGMRedi=1,
-                  GM_background_K=800.0, GM_isopycK=800.0, GM_skewflx=1.0, GM_maxSlope=1e-2,
+                  GM_background_K=800.0, GM_isopycK=800.0, GM_skewflx=0.0, GM_AdvForm=1, GM_ExtraDiag=1,
+                  GM_maxSlope=1e-2,
                   GM_Kmin_horiz=50.0, nonlinFreeSurf=4, select_rStar=2, hFacInf=0.2, hFacSup=2.0,
                   cg2dPreCondFreq=1)
     pRef = np.array([0.0 + 1035.0 * (g.f["rC"][k] - g.f["rF"][0]) * 9.81 * -1.0 for k in range(Nr)])

@@ -367,9 +367,9 @@ __global__ void __launch_bounds__(CG_THREADS) k_cg2d_block(Dims d, Params p, Fie
 // the eight out-of-block ones (two per side) are LDS reads through the
 // neighbour table, and all 32 operator coefficients of the block (aW/pW of the
 // three W-E faces of each row, aS/pS of the three S-N faces of each column, aC,
-// pC) stay in VGPRs (pS, pC in LDS).  Products are FMA-contracted here: CG2D's
-// parity bar is roundoff agreement (its global sums are re-ordered anyway), not
-// bit-exactness.
+// pC) stay in VGPRs (pS, pC in LDS).  No FMA contraction (built -ffp-contract=off like
+// every kernel): each operator row is the reference's expression tree, so only the
+// order of the global sums differs from cg2d.F.
 // nb4[4*T]: packed 16-bit compact indices (W0|W1<<16), (E0|E1<<16),
 // (S0|S1<<16), (N0|N1<<16); blk[4*T] = 2-D offsets of P00, P10(east), P01(north),
 // P11 (T = #blocks; padding blocks: offsets of a real block, inactive).
@@ -377,7 +377,6 @@ template <bool MINRES>
 __global__ void __launch_bounds__(CG_THREADS) k_cg2d_blk2(Dims d, Params p, Fields f, const unsigned *__restrict__ nb4,
                                                          const int *__restrict__ blk, int nBlk, int maxIters,
                                                          int nIterMinIn, SolveRecord *rec, int *stepCounter) {
-#pragma clang fp contract(fast)
   constexpr int NP = 4 * CG_THREADS;
   extern __shared__ __attribute__((aligned(16))) double lds[];
   double *r_l = lds;                // NP + 1 (last = ZERO slot)
@@ -675,7 +674,6 @@ template <int BX, int BY, int NT, bool MINRES>
 __global__ void __launch_bounds__(NT) k_cg2d_bxy(Dims d, Params p, Fields f, const unsigned *__restrict__ nbx,
                                                  const int *__restrict__ blkx, int nBlk, int maxIters, int nIterMinIn,
                                                  SolveRecord *rec, int *stepCounter) {
-#pragma clang fp contract(fast)
   constexpr int NPT = BX * BY, NP = NPT * NT, NB = 2 * (BX + BY), NW = NT / 64;
   extern __shared__ __attribute__((aligned(16))) double lds[];
   double *r_l = lds;               // NP + 1 (last = ZERO slot)

@@ -776,6 +776,10 @@ int mgcm_init(mgcm_model *m) {
   auto okScheme = [&](int s, const char *vname) {
     return (s == 2 || s == 33) && ext(vname, (double)s) == (double)s;
   };
+  // the cube's multi-dimensional split is 3-pass and face-dependent with corner fills
+  // (gad_advection.F:339-367); only the lat-lon 2-pass split is on the device
+  if (m->uvMap && ((m->p.tempStepping && m->p.tempAdvScheme != 2) || (m->p.saltStepping && m->p.saltAdvScheme != 2)))
+    return set_err("mgcm_init: multi-dimensional advection on an EXCH2 (cube) topology is not implemented");
   if (m->p.tempStepping && !okScheme(m->p.tempAdvScheme, "tempVertAdvScheme"))
     return set_err("mgcm_init: tempAdvScheme %d not implemented on the device", m->p.tempAdvScheme);
   if (m->p.saltStepping && !okScheme(m->p.saltAdvScheme, "saltVertAdvScheme"))
@@ -872,8 +876,8 @@ static int tracers_on(mgcm_model *m, hipStream_t st) {
 
 int mgcm_thermodynamics(mgcm_model *m) {
   if (check_ready(m)) return -1;
-  if (!m->p.tempStepping && !m->p.saltStepping) return 0;
-  // forward_step.F:656 DO_OCEANIC_PHYS, :732 THERMODYNAMICS (staggerTimeStep = F)
+  // forward_step.F:656 DO_OCEANIC_PHYS (every step: forcing records, EOS, GM tensor),
+  // :732 THERMODYNAMICS (staggerTimeStep = F; the tracers only when stepped)
   TIMED(K_PHYS, launch_oceanic_phys(m->d, m->p, m->f, m->d_ctr, m->stream));
   return tracers_on(m, m->stream);
 }
@@ -952,7 +956,7 @@ static int one_step(mgcm_model *m) {
   const bool tracers = m->p.tempStepping || m->p.saltStepping;
   const bool fork = !stagger && m->overlap && !m->timing && m->p.momStepping && tracers;
   if (stagger) {
-    if (tracers) TIMED(K_PHYS, launch_oceanic_phys(m->d, m->p, m->f, m->d_ctr, m->stream));
+    TIMED(K_PHYS, launch_oceanic_phys(m->d, m->p, m->f, m->d_ctr, m->stream));
   } else if (fork) {
     TIMED(K_PHYS, launch_oceanic_phys(m->d, m->p, m->f, m->d_ctr, m->stream));
     HIPCHK(hipEventRecord(m->evFork, m->stream));

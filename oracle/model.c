@@ -74,7 +74,7 @@ OModel *oracle_new(int sNx, int sNy, int OLx, int OLy, int Nr, int nSx, int nSy)
   A3(uVel); A3(vVel); A3(wVel); A3(theta); A3(salt); A3(gU); A3(gV); A3(guNm1); A3(gvNm1);
   A3(gtNm1); A3(gsNm1); A3(rhoInSitu); A3(IVDConvCount);
   A3(Kwx); A3(Kwy); A3(Kwz); A3(Kux); A3(Kvy); A3(uVelD); A3(vVelD); A3(uNM1); A3(vNM1);
-  A3(sigmaX); A3(sigmaY); A3(sigmaR); A3(h0FacC); A3(h0FacW); A3(h0FacS); A3(totPhiHyd);
+  A3(sigmaX); A3(sigmaY); A3(sigmaR); A3(Kuz); A3(Kvz); A3(GM_PsiX); A3(GM_PsiY); A3(h0FacC); A3(h0FacW); A3(h0FacS); A3(totPhiHyd);
 #undef A3
   return m;
 }
@@ -97,7 +97,7 @@ void oracle_free(OModel *m) {
                    &m->IVDConvCount, &m->gsNm1, &m->surfaceForcingS, &m->pRef4EOS, &m->Qnet, &m->EmPmR,
                    &m->SSS, &m->lambdaSaltClimRelax, &m->saltFlux, &m->etaNm1, &m->Kwx, &m->Kwy, &m->Kwz,
                    &m->Kux, &m->Kvy, &m->uVelD, &m->vVelD, &m->uNM1, &m->vNM1, &m->sigmaX, &m->sigmaY,
-                   &m->sigmaR, &m->forcTaux, &m->forcTauy, &m->forcQnet, &m->forcEmPmR, &m->forcSST,
+                   &m->sigmaR, &m->Kuz, &m->Kvz, &m->GM_PsiX, &m->GM_PsiY, &m->forcTaux, &m->forcTauy, &m->forcQnet, &m->forcEmPmR, &m->forcSST,
                    &m->forcSSS, &m->h0FacC, &m->h0FacW, &m->h0FacS, &m->totPhiHyd, &m->rStarFacC,
                    &m->rStarFacW, &m->rStarFacS, &m->rStarFacNm1C, &m->rStarFacNm1W, &m->rStarFacNm1S,
                    &m->rStarExpC, &m->rStarExpW, &m->rStarExpS, &m->rStarDhCDt, &m->rStarDhWDt,
@@ -136,7 +136,7 @@ static const PDesc PTAB[] = {
   PI_(periodicExternalForcing), PD(rhoConstFresh), PD(HeatCapacity_Cp), PD(convertFW2Salt), PD(temp_EvPrRn),
   PD(salt_EvPrRn), PD(tauCD), PD(rCD), PD(epsAB_CD), PD(externForcingPeriod), PD(externForcingCycle),
   PD(GM_background_K), PD(GM_isopycK), PD(GM_skewflx), PD(GM_maxSlope), PD(GM_Kmin_horiz),
-  PD(GM_Small_Number), PD(GM_slopeSqCutoff),
+  PD(GM_Small_Number), PD(GM_slopeSqCutoff), PI_(GM_AdvForm), PI_(GM_ExtraDiag),
   PI_(nonlinFreeSurf), PI_(select_rStar), PI_(quasiHydrostatic), PI_(useNHMTerms), PI_(select3dCoriScheme),
   PI_(selectP_inEOS_Zc), PI_(storePhiHyd4Phys), PI_(cg2dPreCondFreq), PD(hFacInf), PD(hFacSup),
   PI_(vectorInvariantMomentum), PI_(selectVortScheme), PI_(selectKEscheme), PI_(upwindShear),
@@ -205,7 +205,8 @@ double *oracle_array(OModel *m, const char *name, long *count) {
     {"lambdaSaltClimRelax", m->lambdaSaltClimRelax, N2}, {"saltFlux", m->saltFlux, N2},
     {"etaNm1", m->etaNm1, N2}, {"Kwx", m->Kwx, N3}, {"Kwy", m->Kwy, N3}, {"Kwz", m->Kwz, N3},
     {"Kux", m->Kux, N3}, {"Kvy", m->Kvy, N3}, {"uVelD", m->uVelD, N3}, {"vVelD", m->vVelD, N3},
-    {"uNM1", m->uNM1, N3}, {"vNM1", m->vNM1, N3}, {"sigmaX", m->sigmaX, N3}, {"sigmaY", m->sigmaY, N3},
+    {"uNM1", m->uNM1, N3}, {"vNM1", m->vNM1, N3}, {"sigmaX", m->sigmaX, N3}, {"Kuz", m->Kuz, N3}, {"Kvz", m->Kvz, N3},
+    {"GM_PsiX", m->GM_PsiX, N3}, {"GM_PsiY", m->GM_PsiY, N3}, {"sigmaY", m->sigmaY, N3},
     {"sigmaR", m->sigmaR, N3},
     {"forcTaux", m->forcTaux, N2 * m->nForcRec}, {"forcTauy", m->forcTauy, N2 * m->nForcRec},
     {"forcQnet", m->forcQnet, N2 * m->nForcRec}, {"forcEmPmR", m->forcEmPmR, N2 * m->nForcRec},

@@ -210,6 +210,50 @@ static void slope_limit_gkw91(const OModel *m, const double *dSigmaDx, const dou
     }
 }
 
+/* GMREDI_CALC_PSI_B (gmredi_calc_psi_b.F:86-212) with GMREDI_SLOPE_PSI's gkw91 branch
+ * (gmredi_slope_psi.F:196-290): the bolus stream-function GM_PsiX/Y at the top face of
+ * level k = 2..Nr (level 1 stays 0), U / V points.  z-coordinates: wUnit2rVel = 1. */
+static void gmredi_calc_psi_b(OModel *m, int t) {
+  const int sNx = m->sNx, sNy = m->sNy, OLx = m->OLx, OLy = m->OLy, Nr = m->Nr, nx = m->nx;
+  const long n2 = m->n2, n3 = m->n3;
+  const double op25 = 0.25, halfRL = 0.5, halfSign = halfRL * m->gravitySign;
+  const double *sigmaX = m->sigmaX + t * n3, *sigmaY = m->sigmaY + t * n3, *sigmaR = m->sigmaR + t * n3;
+  const double *maskW = m->maskW + t * n3, *maskS = m->maskS + t * n3;
+  double *PsiX = m->GM_PsiX + t * n3, *PsiY = m->GM_PsiY + t * n3;
+  const double slopeCutoff = sqrt(m->GM_slopeSqCutoff);
+  const double loc_maxSlope = m->GM_maxSlope * 1.0, maxSlopeSqr = loc_maxSlope * loc_maxSlope;
+  for (int k = 2; k <= Nr; k++) {
+    const int km1 = k - 1;
+    const double half_K = m->GM_background_K * (1.0 + 1.0) * op25;
+    for (int j = 1 - OLy; j <= sNy + OLy; j++)
+      for (int i = 1 - OLx + 1; i <= sNx + OLx; i++) {
+        const double mk = W3(maskW, i, j, km1) * W3(maskW, i, j, k);
+        double SlopeX = (W3(sigmaX, i, j, km1) + W3(sigmaX, i, j, k)) * halfRL * mk;
+        double dSdr = (W3(sigmaR, i - 1, j, k) + W3(sigmaR, i, j, k)) * halfSign * mk;
+        if (dSdr <= m->GM_Small_Number) dSdr = m->GM_Small_Number;
+        SlopeX = SlopeX / dSdr;
+        double taper = 1.0;
+        if (fabs(SlopeX) >= slopeCutoff) { SlopeX = copysign(slopeCutoff, SlopeX); taper = 0.0; }
+        const double Smod = fabs(SlopeX);
+        if (Smod > loc_maxSlope && Smod < slopeCutoff) taper = maxSlopeSqr / (SlopeX * SlopeX + m->GM_Small_Number);
+        W3(PsiX, i, j, k) = SlopeX * taper * (half_K * (1.0 + 1.0));
+      }
+    for (int j = 1 - OLy + 1; j <= sNy + OLy; j++)
+      for (int i = 1 - OLx; i <= sNx + OLx; i++) {
+        const double mk = W3(maskS, i, j, km1) * W3(maskS, i, j, k);
+        double SlopeY = (W3(sigmaY, i, j, km1) + W3(sigmaY, i, j, k)) * halfRL * mk;
+        double dSdr = (W3(sigmaR, i, j - 1, k) + W3(sigmaR, i, j, k)) * halfSign * mk;
+        if (dSdr <= m->GM_Small_Number) dSdr = m->GM_Small_Number;
+        SlopeY = SlopeY / dSdr;
+        double taper = 1.0;
+        if (fabs(SlopeY) >= slopeCutoff) { SlopeY = copysign(slopeCutoff, SlopeY); taper = 0.0; }
+        const double Smod = fabs(SlopeY);
+        if (Smod > loc_maxSlope && Smod < slopeCutoff) taper = maxSlopeSqr / (SlopeY * SlopeY + m->GM_Small_Number);
+        W3(PsiY, i, j, k) = SlopeY * taper * (half_K * (1.0 + 1.0));
+      }
+  }
+}
+
 void oracle_gmredi_calc_tensor(OModel *m, int t) {
   const int sNx = m->sNx, sNy = m->sNy, OLx = m->OLx, OLy = m->OLy, Nr = m->Nr, nx = m->nx;
   const long n2 = m->n2, n3 = m->n3;
@@ -217,7 +261,7 @@ void oracle_gmredi_calc_tensor(OModel *m, int t) {
   const double *sigmaX = m->sigmaX + t * n3, *sigmaY = m->sigmaY + t * n3, *sigmaR = m->sigmaR + t * n3;
   const double *maskC = m->maskC + t * n3, *maskW = m->maskW + t * n3, *maskS = m->maskS + t * n3;
   double *Kwx = m->Kwx + t * n3, *Kwy = m->Kwy + t * n3, *Kwz = m->Kwz + t * n3;
-  double *Kux = m->Kux + t * n3, *Kvy = m->Kvy + t * n3;
+  double *Kux = m->Kux + t * n3, *Kvy = m->Kvy + t * n3, *Kuz = m->Kuz + t * n3, *Kvz = m->Kvz + t * n3;
   double *dSx = calloc(n2, 8), *dSy = calloc(n2, 8), *dSr = calloc(n2, 8), *maskFk = calloc(n2, 8);
   double *SlopeX = calloc(n2, 8), *SlopeY = calloc(n2, 8), *SlopeSqr = calloc(n2, 8), *taper = calloc(n2, 8);
   /* Kwx, Kwy, Kwz at W points, k = Nr..2 (gmredi_calc_tensor.F:259-405) */
@@ -271,6 +315,13 @@ void oracle_gmredi_calc_tensor(OModel *m, int t) {
         W3(Kux, i, j, k) = (m->GM_isopycK * 1.0 * op5 * (1.0 + 1.0)) * L(taper, i, j);
         W3(Kux, i, j, k) = fmax(W3(Kux, i, j, k), m->GM_Kmin_horiz);
       }
+    if (m->GM_ExtraDiag) /* GM_EXTRA_DIAGONAL (gmredi_calc_tensor.F:808-850) */
+      for (int j = 1 - OLy + 1; j <= sNy + OLy - 1; j++)
+        for (int i = 1 - OLx + 1; i <= sNx + OLx - 1; i++)
+          W3(Kuz, i, j, k) = -gravitySign *
+                             (m->GM_isopycK * 1.0 * op5 * (1.0 + 1.0) -
+                              m->GM_skewflx * m->GM_background_K * 1.0 * op5 * (1.0 + 1.0)) *
+                             L(SlopeX, i, j) * L(taper, i, j);
   }
   /* Kvy at V points (gmredi_calc_tensor.F:700-790) */
   for (int k = Nr; k >= 1; k--) {
@@ -291,6 +342,14 @@ void oracle_gmredi_calc_tensor(OModel *m, int t) {
         W3(Kvy, i, j, k) = (m->GM_isopycK * 1.0 * op5 * (1.0 + 1.0)) * L(taper, i, j);
         W3(Kvy, i, j, k) = fmax(W3(Kvy, i, j, k), m->GM_Kmin_horiz);
       }
+    if (m->GM_ExtraDiag) /* gmredi_calc_tensor.F:1053-1090 */
+      for (int j = 1 - OLy + 1; j <= sNy + OLy - 1; j++)
+        for (int i = 1 - OLx + 1; i <= sNx + OLx - 1; i++)
+          W3(Kvz, i, j, k) = -gravitySign *
+                             (m->GM_isopycK * 1.0 * op5 * (1.0 + 1.0) -
+                              m->GM_skewflx * m->GM_background_K * 1.0 * op5 * (1.0 + 1.0)) *
+                             L(SlopeY, i, j) * L(taper, i, j);
   }
+  if (m->GM_AdvForm) gmredi_calc_psi_b(m, t);
   free(dSx); free(dSy); free(dSr); free(maskFk); free(SlopeX); free(SlopeY); free(SlopeSqr); free(taper);
 }

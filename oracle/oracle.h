@@ -89,6 +89,8 @@ typedef struct OModel {
   double externForcingPeriod, externForcingCycle;
   double GM_background_K, GM_isopycK, GM_skewflx, GM_maxSlope, GM_Kmin_horiz, GM_Small_Number,
          GM_slopeSqCutoff;
+  int GM_AdvForm, GM_ExtraDiag;     /* gmredi_readparms.F:243-262: AdvForm => skewflx = 0, ExtraDiag */
+  double *Kuz, *Kvz, *GM_PsiX, *GM_PsiY;                                  /* 3-D (GM_AdvForm) */
   double *pRef4EOS;                                                       /* [Nr] */
   double *Qnet, *EmPmR, *SSS, *lambdaSaltClimRelax, *saltFlux, *etaNm1;   /* 2-D */
   double *Kwx, *Kwy, *Kwz, *Kux, *Kvy, *uVelD, *vVelD, *uNM1, *vNM1;      /* 3-D */

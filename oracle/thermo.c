@@ -221,6 +221,7 @@ static void tracer_integrate(OModel *m, const TracerSpec *c) {
   double *rTrans = calloc(n2, 8), *rTransKp = calloc(n2, 8), *maskUp = calloc(n2, 8), *gtForc = calloc(n2, 8);
   double *fZon = calloc(n2, 8), *fMer = calloc(n2, 8), *af = calloc(n2, 8), *df = calloc(n2, 8);
   fVer[0] = calloc(n2, 8); fVer[1] = calloc(n2, 8);
+  double *uRes = calloc(n3, 8), *vRes = calloc(n3, 8), *wRes = calloc(n3, 8), *dTdz = calloc(n2, 8);
   const int calcAdvection = c->advection && !multiDim;
   const double advFac = calcAdvection ? 1.0 : 0.0, rAdvFac = m->rkSign * advFac;
   const double abFac = (m->myIter == m->nIter0 && m->nIter0 == 0) ? 0.0 : 0.5 + m->abEps; /* startAB = nIter0 */
@@ -228,11 +229,38 @@ static void tracer_integrate(OModel *m, const TracerSpec *c) {
 
   for (int t = 0; t < m->nTiles; t++) {
     double *theta = c->tr + t * n3, *gtNm1 = c->gNm1 + t * n3;
-    const double *uVel = m->uVel + t * n3, *vVel = m->vVel + t * n3, *wVel = m->wVel + t * n3;
-    const double *hFacW = m->hFacW + t * n3, *hFacS = m->hFacS + t * n3, *maskC = m->maskC + t * n3;
-    const double *rhFacC = m->recip_hFacC + t * n3, *conv = m->IVDConvCount + t * n3;
     const double *dxG = m->dxG + t * n2, *dyG = m->dyG + t * n2, *rA = m->rA + t * n2;
     const double *recip_rA = m->recip_rA + t * n2, *recip_dxC = m->recip_dxC + t * n2;
+    const double *uVel = m->uVel + t * n3, *vVel = m->vVel + t * n3, *wVel = m->wVel + t * n3;
+    const double *hFacW = m->hFacW + t * n3, *hFacS = m->hFacS + t * n3, *maskC = m->maskC + t * n3;
+    if (m->useGMRedi && m->GM_AdvForm) {
+      /* thermodynamics.F:252-268: uFld = uVel (+ GMREDI_RESIDUAL_FLOW's bolus velocity,
+       * gmredi_residual_flow.F:58-97, z-coordinates: flipSign4LHCoord = -gravitySign = 1) */
+      const double *PsiX = m->GM_PsiX + t * n3, *PsiY = m->GM_PsiY + t * n3;
+      const double *rhW = m->recip_hFacW + t * n3, *rhS = m->recip_hFacS + t * n3;
+      const double flip = -m->gravitySign;
+      for (long p = 0; p < n3; p++) { uRes[p] = uVel[p]; vRes[p] = vVel[p]; wRes[p] = wVel[p]; }
+      for (int k = 1; k <= Nr; k++) {
+        const int kp1 = k + 1 < Nr ? k + 1 : Nr;
+        const double maskp1 = k >= Nr ? 0.0 : 1.0;
+        for (int j = 1 - OLy; j <= sNy + OLy; j++)
+          for (int i = 1 - OLx; i <= sNx + OLx; i++) {
+            double delPsi = W3(PsiX, i, j, kp1) * 1.0 * maskp1 - W3(PsiX, i, j, k) * 1.0;
+            W3(uRes, i, j, k) = W3(uRes, i, j, k) + delPsi * m->recip_drF[k - 1] * W3(rhW, i, j, k) * 1.0 * flip;
+            delPsi = W3(PsiY, i, j, kp1) * 1.0 * maskp1 - W3(PsiY, i, j, k) * 1.0;
+            W3(vRes, i, j, k) = W3(vRes, i, j, k) + delPsi * m->recip_drF[k - 1] * W3(rhS, i, j, k) * 1.0 * flip;
+          }
+        for (int j = 1 - OLy; j <= sNy + OLy - 1; j++)
+          for (int i = 1 - OLx; i <= sNx + OLx - 1; i++) {
+            const double delPsi = (L(dyG, i + 1, j) * W3(PsiX, i + 1, j, k) - L(dyG, i, j) * W3(PsiX, i, j, k) +
+                                   L(dxG, i, j + 1) * W3(PsiY, i, j + 1, k) - L(dxG, i, j) * W3(PsiY, i, j, k));
+            W3(wRes, i, j, k) = W3(wRes, i, j, k) + delPsi * L(recip_rA, i, j) * 1.0 * flip;
+          }
+      }
+      uVel = uRes; vVel = vRes; wVel = wRes;
+    }
+    const double *rhFacC = m->recip_hFacC + t * n3, *conv = m->IVDConvCount + t * n3;
+
     const double *recip_dyC = m->recip_dyC + t * n2, *maskInC = m->maskInC + t * n2;
     const double *sfT = c->sfc ? c->sfc + t * n2 : NULL;
     const double *Kwx = m->Kwx + t * n3, *Kwy = m->Kwy + t * n3, *Kwz = m->Kwz + t * n3;
@@ -303,6 +331,22 @@ static void tracer_integrate(OModel *m, const TracerSpec *c) {
           for (int i = 0; i <= sNx + 2; i++)
             L(df, i, j) = L(df, i, j) - L(xA, i, j) * W3(Kux, i, j, k) * L(recip_dxC, i, j) *
                                             (W3(theta, i, j, k) - W3(theta, i - 1, j, k));
+      if (m->useGMRedi && m->GM_ExtraDiag) { /* gmredi_xtransport.F:117-146 (maskFk = maskUp) */
+        const int km1 = k > 1 ? k - 1 : 1, kp1 = k + 1 < Nr ? k + 1 : Nr;
+        const double maskp1 = k >= Nr ? 0.0 : 1.0;
+        for (int j = 0; j <= sNy + 1; j++)
+          for (int i = 0; i <= sNx + 2; i++) {
+            L(dTdz, i, j) = 0.5 * (+0.5 * m->recip_drC[k - 1] *
+                                       (L(maskUp, i - 1, j) * (W3(theta, i - 1, j, km1) - W3(theta, i - 1, j, k)) +
+                                        L(maskUp, i, j) * (W3(theta, i, j, km1) - W3(theta, i, j, k))) +
+                                   0.5 * m->recip_drC[kp1 - 1] *
+                                       (W3(maskC, i - 1, j, k) * W3(maskC, i - 1, j, kp1) * maskp1 *
+                                            (W3(theta, i - 1, j, k) - W3(theta, i - 1, j, kp1)) +
+                                        W3(maskC, i, j, k) * W3(maskC, i, j, kp1) * maskp1 *
+                                            (W3(theta, i, j, k) - W3(theta, i, j, kp1))));
+            L(df, i, j) = L(df, i, j) - L(xA, i, j) * W3(m->Kuz + t * n3, i, j, k) * L(dTdz, i, j);
+          }
+      }
       for (long p = 0; p < n2; p++) fZon[p] = fZon[p] + df[p];
       if (calcAdvection) { /* GAD_C2_ADV_Y */
         for (int i = 1 - OLx; i <= sNx + OLx; i++) L(af, i, 1 - OLy) = 0.0;
@@ -324,6 +368,22 @@ static void tracer_integrate(OModel *m, const TracerSpec *c) {
           for (int i = 0; i <= sNx + 1; i++)
             L(df, i, j) = L(df, i, j) - L(yA, i, j) * W3(Kvy, i, j, k) * L(recip_dyC, i, j) *
                                             (W3(theta, i, j, k) - W3(theta, i, j - 1, k));
+      if (m->useGMRedi && m->GM_ExtraDiag) { /* gmredi_ytransport.F:117-146 */
+        const int km1 = k > 1 ? k - 1 : 1, kp1 = k + 1 < Nr ? k + 1 : Nr;
+        const double maskp1 = k >= Nr ? 0.0 : 1.0;
+        for (int j = 0; j <= sNy + 2; j++)
+          for (int i = 0; i <= sNx + 1; i++) {
+            L(dTdz, i, j) = 0.5 * (+0.5 * m->recip_drC[k - 1] *
+                                       (L(maskUp, i, j - 1) * (W3(theta, i, j - 1, km1) - W3(theta, i, j - 1, k)) +
+                                        L(maskUp, i, j) * (W3(theta, i, j, km1) - W3(theta, i, j, k))) +
+                                   0.5 * m->recip_drC[kp1 - 1] *
+                                       (W3(maskC, i, j - 1, k) * W3(maskC, i, j - 1, kp1) * maskp1 *
+                                            (W3(theta, i, j - 1, k) - W3(theta, i, j - 1, kp1)) +
+                                        W3(maskC, i, j, k) * W3(maskC, i, j, kp1) * maskp1 *
+                                            (W3(theta, i, j, k) - W3(theta, i, j, kp1))));
+            L(df, i, j) = L(df, i, j) - L(yA, i, j) * W3(m->Kvz + t * n3, i, j, k) * L(dTdz, i, j);
+          }
+      }
       for (long p = 0; p < n2; p++) fMer[p] = fMer[p] + df[p];
       if (calcAdvection && k >= 2) { /* GAD_C2_ADV_R */
         for (int j = 1 - OLy; j <= sNy + OLy; j++)
@@ -445,6 +505,7 @@ static void tracer_integrate(OModel *m, const TracerSpec *c) {
   free(gT); free(kappaRT); free(a3); free(b3); free(c3); free(cp); free(yp);
   free(fVer[0]); free(fVer[1]); free(xA); free(yA); free(uTrans); free(vTrans); free(rTrans); free(rTransKp);
   free(maskUp); free(gtForc); free(fZon); free(fMer); free(af); free(df);
+  free(uRes); free(vRes); free(wRes); free(dTdz);
 }
 
 void oracle_thermodynamics(OModel *m) {

@@ -20,7 +20,7 @@ GRID_NAMES = {"XC": "xC", "XG": "xG", "DXC": "dxC", "DXF": "dxF", "DXG": "dxG", 
 
 def test_cs32x15_grid_vs_reference_monitor(golden_dir):
     from mitgcm_amd import configs
-    g = configs.global_ocean_cs32x15()[0]
+    g = configs.global_ocean_cs32x15(sNy=16)[0]   # the reference SIZE.h tiling: its tile-ordered monitor sums
     gold = json.load(open(os.path.join(golden_dir, "global_ocean.cs32x15", "grid_monitor.json")))
     worst = (99.0, None)
     for mon, f in GRID_NAMES.items():
@@ -34,15 +34,37 @@ def test_cs32x15_grid_vs_reference_monitor(golden_dir):
 
 
 def test_cs32x15_oracle_steps():
+    """Cold start from lev_T/S_cs_15k: 8 steps stay physical with a converged CG2D.
+    The inputs are read with W2_mapIO = -1 (facets side by side in x: the experiment has
+    no data.exch2, w2_readparms.F:64); the round-1 reader stacked them in y, which
+    scrambled bathymetry, T/S and forcing with a period of 6 rows and blew up within
+    5 steps.  The stepped values are parity-unpinned against the reference (its
+    output.txt restarts from pickup.0000072000, absent from the reference tree)."""
     from oracle.harness import cs32x15_oracle
     o, g = cs32x15_oracle()
-    for _ in range(2):
+    for _ in range(8):
         o.forward_step()
-    r = o.dynstat()
-    assert 0 < r["cg2d_iters"] < 200, r["cg2d_iters"]
-    for n in ("uVel", "vVel", "theta", "salt", "etaN"):
+        r = o.dynstat()
+        assert 60 < r["cg2d_iters"] < 120, r["cg2d_iters"]
+        assert r["cg2d_last_res"] < r["cg2d_init_res"]
+        assert -2.5 < r["dynstat_theta_min"] and r["dynstat_theta_max"] < 35.0, r
+        assert r["dynstat_uvel_max"] < 1.0 and abs(r["dynstat_eta_max"]) < 5.0, r
+    for n in ("uVel", "vVel", "wVel", "theta", "salt", "etaN"):
         a = np.array(o.arr(n))
         assert np.isfinite(a).all(), n
-    th = np.array(o.arr("theta"))
-    assert -2.0 < th.min() and th.max() < 35.0
-    assert np.abs(np.array(o.arr("uVel"))).max() < 2.0
+
+
+def test_cs32x15_inputs_w2_mapio():
+    """The bathymetry read with the experiment's W2_mapIO = -1 layout is continuous across
+    the cube's face edges (a mis-read one is not): the wet/dry mask of each face's edge
+    row matches its neighbour's through the EXCH2 halo map to within coastline noise."""
+    from mitgcm_amd import configs
+    g = configs.global_ocean_cs32x15()[0]
+    mC = g.f["maskC"][:, 0]
+    ex = g.exch(mC.copy())
+    OL = g.OLx
+    agree = []
+    for t in range(g.nTiles):
+        # halo row just south of the tile vs the tile's own first row
+        agree.append(np.mean(ex[t, OL - 1, OL:OL + g.sNx] == mC[t, OL, OL:OL + g.sNx]))
+    assert np.mean(agree) > 0.8, agree
