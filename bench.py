@@ -36,7 +36,7 @@ def parse():
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--config", default="global_ocean.90x40x15",
-                    choices=["global_ocean.90x40x15", "global_oce_latlon_90x40x15", "tutorial_global_oce_latlon", "baroclinic_gyre_dst3",
+                    choices=["global_ocean.90x40x15", "global_ocean.cs32x15", "global_oce_latlon_90x40x15", "tutorial_global_oce_latlon", "baroclinic_gyre_dst3",
                              "tutorial_baroclinic_gyre", "tutorial_barotropic_gyre"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--shard", action="store_true",
@@ -56,6 +56,12 @@ WORKLOADS = {
                              "quasi-hydrostatic + NH metric + 3-D Coriolis, implicit vertical diffusion, IVDC, "
                              "monthly forcing with real fresh-water flux; full FORWARD_STEP on device, "
                              "1 step = 1 model day",
+    "global_ocean.cs32x15": "BASELINE config 3, verification/global_ocean.cs32x15: cubed sphere, 6 faces of "
+                            "32x32 as 6 tiles (OL=4, pkg/exch2 halo maps) on 1 GPU, 15 levels, cold start from "
+                            "lev_T/S_cs_15k; staggerTimeStep, vector-invariant momentum (harmonic viscosity), r* with "
+                            "non-linear free surface (UPDATE_CG2D every step), JMD95Z, GM/Redi advective form "
+                            "(GM_AdvForm), implicit vertical diffusion, IVDC, monthly forcing with real fresh-water "
+                            "flux; full FORWARD_STEP on device, 1 step = 1 model day",
     "global_oce_latlon_90x40x15": "90x40x15 global lat-lon ocean (BASELINE config 2's grid, bathymetry, "
                                   "monthly forcing and 1-tile layout sNx=90, sNy=40, OL=3) with the physics "
                                   "verification/tutorial_global_oce_latlon pins: JMD95Z, GM/Redi gkw91, CD scheme, "
@@ -74,6 +80,8 @@ WORKLOADS = {
 
 
 DATA = {
+    "global_ocean.cs32x15": "reference input fields of verification/global_ocean.cs32x15 (grid_cs32 facets, "
+                            "bathy_Hmin50, lev_T/S_cs_15k, 12-month taux/tauy/Qnet/EmPmR/SST/SSS), cold start",
     "global_ocean.90x40x15": "reference input fields of verification/tutorial_global_oce_latlon (bathymetry, "
                              "12-month taux/tauy/Qnet/EmPmR/SST/SSS) and the committed pickup.0000036000 / "
                              "pickup_cd.0000036000 of verification/global_ocean.90x40x15",
@@ -93,6 +101,8 @@ def config_fn(name):
         return lambda: configs.baroclinic_gyre(tempAdvScheme=33)
     if name == "global_ocean.90x40x15":
         return configs.global_ocean_90x40x15
+    if name == "global_ocean.cs32x15":
+        return configs.global_ocean_cs32x15
     if name == "global_oce_latlon_90x40x15":
         return lambda: configs.global_oce_latlon(nSx=1, nSy=1, OL=3)
     if name == "tutorial_global_oce_latlon":
@@ -105,9 +115,11 @@ def cpu_baseline(config, seconds):
     """Oracle (CPU restatement, 1 thread) timed on the same workload: as many
     steps as fit in ~`seconds` of CPU time, reported in model-days/s."""
     from mitgcm_amd import configs
-    from oracle.harness import gyre_oracle, latlon_oracle, ocean90_oracle, oracle_from_config
+    from oracle.harness import cs32x15_oracle, gyre_oracle, latlon_oracle, ocean90_oracle, oracle_from_config
     if config == "global_ocean.90x40x15":
         o, _ = ocean90_oracle()
+    elif config == "global_ocean.cs32x15":
+        o, _ = cs32x15_oracle()
     elif config == "tutorial_barotropic_gyre":
         o = gyre_oracle()
     elif config == "global_oce_latlon_90x40x15":

@@ -29,12 +29,31 @@ def needs_build():
 
 
 def build(force=False, verbose=False):
+    """Compile every translation unit to an object in parallel (mitgcm_amd/_build/), then
+    link the shared library."""
     if not force and not needs_build():
         return OUT
     hipcc = HIPCC if os.path.exists(HIPCC) else shutil.which("hipcc")
     if not hipcc:
         raise RuntimeError("hipcc not found: cannot build the MI355X library")
-    cmd = [hipcc] + FLAGS + ["-o", OUT + ".tmp"] + [os.path.join(CSRC, s) for s in SOURCES]
+    from concurrent.futures import ThreadPoolExecutor
+    bdir = os.path.join(HERE, "_build")
+    os.makedirs(bdir, exist_ok=True)
+    cflags = [f for f in FLAGS if f != "-shared"]
+    jobs = []
+    for src in SOURCES:
+        obj = os.path.join(bdir, src.replace(".hip", ".o"))
+        jobs.append((obj, [hipcc] + cflags + ["-c", os.path.join(CSRC, src), "-o", obj]))
+
+    def run(job):
+        if verbose:
+            print(" ".join(job[1]))
+        subprocess.check_call(job[1])
+        return job[0]
+
+    with ThreadPoolExecutor(max_workers=min(len(jobs), int(os.environ.get("MAX_JOBS", "8")))) as ex:
+        objs = list(ex.map(run, jobs))
+    cmd = [hipcc, "--offload-arch=gfx950", "-shared", "-fPIC", "-o", OUT + ".tmp"] + objs
     if verbose:
         print(" ".join(cmd))
     subprocess.check_call(cmd)

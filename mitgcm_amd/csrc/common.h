@@ -42,6 +42,7 @@ struct Params {
   double HeatCapacity_Cp, convertFW2Salt, temp_EvPrRn, salt_EvPrRn, rCD, epsAB_CD;
   double externForcingPeriod, externForcingCycle;
   double GM_background_K, GM_isopycK, GM_skewflx, GM_maxSlope, GM_Kmin_horiz, GM_Small_Number, GM_slopeSqCutoff;
+  int GM_AdvForm, GM_ExtraDiag;   // bolus advective form (gmredi_calc_psi_b.F) + extra-diagonal Redi terms
   // global_ocean.90x40x15: r* non-linear free surface, JMD95P, QH / NH metric, 3-D Coriolis
   int nonlinFreeSurf, select_rStar, quasiHydrostatic, useNHMTerms, select3dCoriScheme, selectP_inEOS_Zc;
   int storePhiHyd4Phys;
@@ -81,6 +82,7 @@ struct Fields {
   const double *forcRec;                   // [6][nForcRec][tiles*n2]: SST, SSS, taux, tauy, Qnet, EmPmR
   double *Qnet, *EmPmR, *SSS, *lambdaSaltClimRelax, *etaNm1;   // 2-D
   double *sigmaR, *Kwx, *Kwy, *Kwz, *Kux, *Kvy;                // 3-D GM/Redi
+  double *Kuz, *Kvz, *GM_PsiX, *GM_PsiY;                       // 3-D GM_ExtraDiag / GM_AdvForm
   double *uVelD, *vVelD, *uNM1, *vNM1, *cdU, *cdV;             // 3-D CD scheme (+ gUtmp/gVtmp scratch)
   // r* coordinate (global_ocean.90x40x15): rest-state hFac, column geometry, the r* factors
   const double *h0FacC, *h0FacW, *h0FacS;                                  // 3-D

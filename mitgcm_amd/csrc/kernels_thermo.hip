@@ -206,6 +206,9 @@ __global__ void __launch_bounds__(256) k_gm_tensor(Dims d, Params p, Fields f) {
     const double dSr = op25 * (sR(i - 1, j, k) + sR(i, j, k) + (sR(i - 1, j, kp1) + sR(i, j, kp1)) * maskp1) * mW * gs;
     gm_slope_gkw91(p, dSx, dSy, dSr, SlopeX, SlopeY, SlopeSqr, taper);
     f.Kux[q3] = fmax((p.GM_isopycK * 1.0 * op5 * (1.0 + 1.0)) * taper, p.GM_Kmin_horiz);
+    if (p.GM_ExtraDiag)   // GM_EXTRA_DIAGONAL Kuz (gmredi_calc_tensor.F:808-850)
+      f.Kuz[q3] = -gs * (p.GM_isopycK * 1.0 * op5 * (1.0 + 1.0) - p.GM_skewflx * p.GM_background_K * 1.0 * op5 * (1.0 + 1.0)) *
+                  SlopeX * taper;
   }
   {  // Kvy (V points)
     const double mS = f.maskS[q3];
@@ -214,6 +217,34 @@ __global__ void __launch_bounds__(256) k_gm_tensor(Dims d, Params p, Fields f) {
     const double dSr = op25 * (sR(i, j - 1, k) + sR(i, j, k) + (sR(i, j - 1, kp1) + sR(i, j, kp1)) * maskp1) * mS * gs;
     gm_slope_gkw91(p, dSx, dSy, dSr, SlopeX, SlopeY, SlopeSqr, taper);
     f.Kvy[q3] = fmax((p.GM_isopycK * 1.0 * op5 * (1.0 + 1.0)) * taper, p.GM_Kmin_horiz);
+    if (p.GM_ExtraDiag)   // Kvz (gmredi_calc_tensor.F:1053-1090)
+      f.Kvz[q3] = -gs * (p.GM_isopycK * 1.0 * op5 * (1.0 + 1.0) - p.GM_skewflx * p.GM_background_K * 1.0 * op5 * (1.0 + 1.0)) *
+                  SlopeY * taper;
+  }
+  if (p.GM_AdvForm) {
+    // GMREDI_CALC_PSI_B (gmredi_calc_psi_b.F:86-212) + GMREDI_SLOPE_PSI gkw91
+    // (gmredi_slope_psi.F:196-290): bolus stream-function at the top face of level k >= 2
+    double psx = 0.0, psy = 0.0;
+    if (k >= 2) {
+      const double halfRL = 0.5, halfSign = halfRL * gs, half_K = p.GM_background_K * (1.0 + 1.0) * op25;
+      const double slopeCutoff = sqrt(p.GM_slopeSqCutoff), loc_maxSlope = p.GM_maxSlope * 1.0;
+      const double maxSlopeSqr = loc_maxSlope * loc_maxSlope;
+      auto psi = [&](double Slope, double dSdr) {
+        if (dSdr <= p.GM_Small_Number) dSdr = p.GM_Small_Number;
+        Slope = Slope / dSdr;
+        double tp = 1.0;
+        if (fabs(Slope) >= slopeCutoff) { Slope = copysign(slopeCutoff, Slope); tp = 0.0; }
+        const double Smod = fabs(Slope);
+        if (Smod > loc_maxSlope && Smod < slopeCutoff) tp = maxSlopeSqr / (Slope * Slope + p.GM_Small_Number);
+        return Slope * tp * (half_K * (1.0 + 1.0));
+      };
+      const double mkW = f.maskW[MG_I3(d, i, j, k - 1, t)] * f.maskW[q3];
+      psx = psi((sX(i, j, k - 1) + sX(i, j, k)) * halfRL * mkW, (sR(i - 1, j, k) + sR(i, j, k)) * halfSign * mkW);
+      const double mkS = f.maskS[MG_I3(d, i, j, k - 1, t)] * f.maskS[q3];
+      psy = psi((sY(i, j, k - 1) + sY(i, j, k)) * halfRL * mkS, (sR(i, j - 1, k) + sR(i, j, k)) * halfSign * mkS);
+    }
+    f.GM_PsiX[q3] = psx;
+    f.GM_PsiY[q3] = psy;
   }
 }
 
@@ -343,32 +374,78 @@ __global__ void __launch_bounds__(256) k_tracer_rhs(Dims d, Params p, Fields f, 
 #define G2(a_, ii, jj) f.a_[MG_I2(d, ii, jj, t)]
 #define G3(a_, ii, jj, kk) f.a_[MG_I3(d, ii, jj, kk, t)]
   const double drF = f.drF[k - 1];
+  // uFld, vFld, wFld of thermodynamics.F:252-268: the Eulerian velocity plus, with
+  // GM_AdvForm, GMREDI_RESIDUAL_FLOW's bolus velocity (gmredi_residual_flow.F:58-97)
+  const bool bolus = p.useGMRedi && p.GM_AdvForm;
+  const double flip = -p.gravitySign;
+  const int kp1b = k + 1 < Nr ? k + 1 : Nr;
+  const double maskp1b = k >= Nr ? 0.0 : 1.0;
+  auto uFld = [&](int ii, int jj) {
+    double u = G3(uVel, ii, jj, k);
+    if (bolus) {
+      const double delPsi = G3(GM_PsiX, ii, jj, kp1b) * 1.0 * maskp1b - G3(GM_PsiX, ii, jj, k) * 1.0;
+      u = u + delPsi * f.recip_drF[k - 1] * G3(recip_hFacW, ii, jj, k) * 1.0 * flip;
+    }
+    return u;
+  };
+  auto vFld = [&](int ii, int jj) {
+    double v = G3(vVel, ii, jj, k);
+    if (bolus) {
+      const double delPsi = G3(GM_PsiY, ii, jj, kp1b) * 1.0 * maskp1b - G3(GM_PsiY, ii, jj, k) * 1.0;
+      v = v + delPsi * f.recip_drF[k - 1] * G3(recip_hFacS, ii, jj, k) * 1.0 * flip;
+    }
+    return v;
+  };
+  auto wFld = [&](int kk) {
+    double w = G3(wVel, i, j, kk);
+    if (bolus) {
+      const double delPsi = (G2(dyG, i + 1, j) * G3(GM_PsiX, i + 1, j, kk) - G2(dyG, i, j) * G3(GM_PsiX, i, j, kk) +
+                             G2(dxG, i, j + 1) * G3(GM_PsiY, i, j + 1, kk) - G2(dxG, i, j) * G3(GM_PsiY, i, j, kk));
+      w = w + delPsi * recip_rA * 1.0 * flip;
+    }
+    return w;
+  };
+  // GM_EXTRA_DIAGONAL vertical gradient at the west (dir 0) / south (dir 1) face of (ii, jj)
+  // (gmredi_xtransport.F:117-146, gmredi_ytransport.F; maskFk = CALC_ADV_FLOW's maskUp)
+  auto gm_dTdz = [&](int ii, int jj, int dir) {
+    const int km1 = k > 1 ? k - 1 : 1, kp1 = k + 1 < Nr ? k + 1 : Nr;
+    const double maskp1 = k >= Nr ? 0.0 : 1.0;
+    const int i0 = dir == 0 ? ii - 1 : ii, j0 = dir == 0 ? jj : jj - 1;
+    auto mUp = [&](int a, int b) { return k == 1 ? 0.0 : G3(maskC, a, b, k - 1) * G3(maskC, a, b, k); };
+    return 0.5 * (+0.5 * f.recip_drC[k - 1] *
+                      (mUp(i0, j0) * (T3(i0, j0, km1) - T3(i0, j0, k)) + mUp(ii, jj) * (T3(ii, jj, km1) - T3(ii, jj, k))) +
+                  0.5 * f.recip_drC[kp1 - 1] *
+                      (G3(maskC, i0, j0, k) * G3(maskC, i0, j0, kp1) * maskp1 * (T3(i0, j0, k) - T3(i0, j0, kp1)) +
+                       G3(maskC, ii, jj, k) * G3(maskC, ii, jj, kp1) * maskp1 * (T3(ii, jj, k) - T3(ii, jj, kp1))));
+  };
   // west / south face fluxes of the column (fZon, fMer): GAD_C2_ADV_X/Y + GAD_DIFF_X/Y
   auto fzon = [&](int ii) {
     const double xA = G2(dyG, ii, j) * drF * G3(hFacW, ii, j, k);
     double fz = 0.0;
-    if (calcAdv) fz = fz + (G3(uVel, ii, j, k) * xA) * (T3(ii, j, k) + T3(ii - 1, j, k)) * 0.5;
+    if (calcAdv) fz = fz + (uFld(ii, j) * xA) * (T3(ii, j, k) + T3(ii - 1, j, k)) * 0.5;
     double df = 0.0;
     if (a.diffKh != 0.0) df = -a.diffKh * xA * G2(recip_dxC, ii, j) * (T3(ii, j, k) - T3(ii - 1, j, k));
     if (p.useGMRedi)   // GMREDI_XTRANSPORT (gmredi_xtransport.F:94-101)
       df = df - xA * G3(Kux, ii, j, k) * G2(recip_dxC, ii, j) * (T3(ii, j, k) - T3(ii - 1, j, k));
+    if (p.useGMRedi && p.GM_ExtraDiag) df = df - xA * G3(Kuz, ii, j, k) * gm_dTdz(ii, j, 0);
     return fz + df;
   };
   auto fmer = [&](int jj) {
     const double yA = G2(dxG, i, jj) * drF * G3(hFacS, i, jj, k);
     double fm = 0.0;
-    if (calcAdv) fm = fm + (G3(vVel, i, jj, k) * yA) * (T3(i, jj, k) + T3(i, jj - 1, k)) * 0.5;
+    if (calcAdv) fm = fm + (vFld(i, jj) * yA) * (T3(i, jj, k) + T3(i, jj - 1, k)) * 0.5;
     double df = 0.0;
     if (a.diffKh != 0.0) df = -a.diffKh * yA * G2(recip_dyC, i, jj) * (T3(i, jj, k) - T3(i, jj - 1, k));
     if (p.useGMRedi)   // GMREDI_YTRANSPORT
       df = df - yA * G3(Kvy, i, jj, k) * G2(recip_dyC, i, jj) * (T3(i, jj, k) - T3(i, jj - 1, k));
+    if (p.useGMRedi && p.GM_ExtraDiag) df = df - yA * G3(Kvz, i, jj, k) * gm_dTdz(i, jj, 1);
     return fm + df;
   };
   // CALC_ADV_FLOW rTrans of level kk (0 at the surface and below the bottom level)
   auto rtrans = [&](int kk) {
     if (kk <= 1 || kk > Nr) return 0.0;
     const double maskUp = G3(maskC, i, j, kk - 1) * G3(maskC, i, j, kk);
-    return G3(wVel, i, j, kk) * rA * maskUp;
+    return wFld(kk) * rA * maskUp;
   };
   // fVerT through the top face of level kk: GAD_C2_ADV_R + vertical diffusive flux
   // (GAD_DIFF_R when diffusion is explicit, 0 with implicitDiffusion)
@@ -403,10 +480,10 @@ __global__ void __launch_bounds__(256) k_tracer_rhs(Dims d, Params p, Fields f, 
   };
   const long q3 = MG_I3(d, i, j, k, t);
   const double Tk = T[q3];
-  const double uT0 = G3(uVel, i, j, k) * (G2(dyG, i, j) * drF * G3(hFacW, i, j, k));
-  const double uT1 = G3(uVel, i + 1, j, k) * (G2(dyG, i + 1, j) * drF * G3(hFacW, i + 1, j, k));
-  const double vT0 = G3(vVel, i, j, k) * (G2(dxG, i, j) * drF * G3(hFacS, i, j, k));
-  const double vT1 = G3(vVel, i, j + 1, k) * (G2(dxG, i, j + 1) * drF * G3(hFacS, i, j + 1, k));
+  const double uT0 = uFld(i, j) * (G2(dyG, i, j) * drF * G3(hFacW, i, j, k));
+  const double uT1 = uFld(i + 1, j) * (G2(dyG, i + 1, j) * drF * G3(hFacW, i + 1, j, k));
+  const double vT0 = vFld(i, j) * (G2(dxG, i, j) * drF * G3(hFacS, i, j, k));
+  const double vT1 = vFld(i, j + 1) * (G2(dxG, i, j + 1) * drF * G3(hFacS, i, j + 1, k));
   const double rTrans = rtrans(k), rTransKp = rtrans(k + 1);
   const double fVerUp = fvert(k, rTrans), fVerDn = fvert(k + 1, rTransKp);
   const double fZi = fzon(i), fZe = fzon(i + 1);

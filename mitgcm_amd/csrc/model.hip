@@ -103,6 +103,7 @@ static const FieldDesc FIELDS[] = {
     FD(rStarDhWDt, F2D), FD(rStarDhSDt, F2D), FD(PmEpR, F2D), FD(dEtaHdt, F2D), FD(maskInW, F2D),
     FD(maskInS, F2D), FD(dWtC, F3D), FD(dWtU, F3D), FD(dWtV, F3D),
     FD(fCoriG, F2D), FD(recip_rAz, F2D), FD(recip_dxG, F2D), FD(recip_dyG, F2D),
+    FD(Kuz, F3D), FD(Kvz, F3D), FD(GM_PsiX, F3D), FD(GM_PsiY, F3D),
 };
 #undef FD
 
@@ -129,6 +130,7 @@ static const PDesc PARAMS[] = {
     PI_(periodicExternalForcing), PI_(nForcRec), PD(HeatCapacity_Cp), PD(convertFW2Salt), PD(temp_EvPrRn),
     PD(salt_EvPrRn), PD(rCD), PD(epsAB_CD), PD(externForcingPeriod), PD(externForcingCycle), PD(GM_background_K),
     PD(GM_isopycK), PD(GM_skewflx), PD(GM_maxSlope), PD(GM_Kmin_horiz), PD(GM_Small_Number), PD(GM_slopeSqCutoff),
+    PI_(GM_AdvForm), PI_(GM_ExtraDiag),
     PI_(nonlinFreeSurf), PI_(select_rStar), PI_(quasiHydrostatic), PI_(useNHMTerms), PI_(select3dCoriScheme),
     PI_(selectP_inEOS_Zc), PI_(storePhiHyd4Phys), PD(hFacInf),
     PI_(vectorInvariantMomentum), PI_(selectVortScheme), PI_(selectKEscheme), PI_(upwindShear),
@@ -784,6 +786,11 @@ int mgcm_init(mgcm_model *m) {
     return set_err("mgcm_init: tempAdvScheme %d not implemented on the device", m->p.tempAdvScheme);
   if (m->p.saltStepping && !okScheme(m->p.saltAdvScheme, "saltVertAdvScheme"))
     return set_err("mgcm_init: saltAdvScheme %d not implemented on the device", m->p.saltAdvScheme);
+  if (m->p.useGMRedi && m->p.GM_AdvForm && m->p.multiDimAdvection &&
+      ((m->p.tempStepping && m->p.tempAdvScheme != 2) || (m->p.saltStepping && m->p.saltAdvScheme != 2)))
+    return set_err("mgcm_init: GM_AdvForm with multi-dimensional advection is not implemented on the device");
+  if (m->p.useGMRedi && m->p.GM_AdvForm && m->p.GM_skewflx != 0.0)
+    return set_err("mgcm_init: GM_AdvForm needs GM_skewflx = 0 (gmredi_readparms.F:243-244)");
   if (m->p.eosType != 0 && m->p.eosType != 1) return set_err("mgcm_init: eosType %d not implemented", m->p.eosType);
   if (m->d.Nr > 64) return set_err("mgcm_init: Nr = %d > 64 (column kernels hold a column in one workgroup)", m->d.Nr);
   if (m->p.periodicExternalForcing && (m->p.nForcRec < 1 || m->p.nForcRec > MG_MAXREC))
@@ -1171,6 +1178,48 @@ double mgcm_kernel_ms(mgcm_model *m, const char *name, int *launches) {
     }
   if (launches) *launches = 0;
   return -1.0;
+}
+
+// The order in which the selected CG2D kernel forms its global sums (GLOBAL_SUM_TILE_RL's
+// replacement), for the oracle to restate it: thread tid accumulates the per-point terms of
+// plan[p*NT + tid] (2-D flat offsets; -1 = padding) for p = 0..PPT-1 in order, starting from
+// 0.0; the NT thread partials are then combined by the pairwise tree the DPP row sums,
+// row broadcasts and the cross-wave row sum implement (block_sum / block_sum_nw: lanes
+// (2i, 2i+1), then pairs of pairs, ..., in thread order, zero-padded to a power of two).
+int mgcm_cg2d_sum_plan(mgcm_model *m, int *plan, long capacity, int *NT, int *PPT) {
+  if (!m->ready) return set_err("mgcm_cg2d_sum_plan: model not initialised");
+  int nt, ppt;
+  std::vector<int> tab;
+  if (m->nBlkX > 0) {
+    int BX, BY;
+    cg2d_bxy_geometry(&BX, &BY, &nt);
+    ppt = BX * BY;
+    std::vector<int> blkx((size_t)ppt * nt);
+    HIPCHK(hipMemcpy(blkx.data(), m->d_blkx, blkx.size() * sizeof(int), hipMemcpyDeviceToHost));
+    tab.assign((size_t)ppt * nt, -1);
+    for (int t = 0; t < m->nBlkX; t++)
+      for (int q = 0; q < ppt; q++) tab[(size_t)q * nt + t] = blkx[(size_t)ppt * t + q];
+  } else if (m->nBlk > 0) {
+    nt = 1024; ppt = 4;
+    std::vector<int> blk((size_t)4 * nt);
+    HIPCHK(hipMemcpy(blk.data(), m->d_blk, blk.size() * sizeof(int), hipMemcpyDeviceToHost));
+    tab.assign((size_t)4 * nt, -1);
+    for (int t = 0; t < m->nBlk; t++)
+      for (int q = 0; q < 4; q++) tab[(size_t)q * nt + t] = blk[(size_t)4 * t + q];
+  } else {
+    nt = 1024; ppt = cg2d_block_ppt(m->nPts);
+    std::vector<int> gofs((size_t)ppt * nt);
+    HIPCHK(hipMemcpy(gofs.data(), m->d_gofs, gofs.size() * sizeof(int), hipMemcpyDeviceToHost));
+    tab.assign((size_t)ppt * nt, -1);
+    for (int q = 0; q < ppt; q++)
+      for (int t = 0; t < nt; t++)
+        if (t + q * nt < m->nPts) tab[(size_t)q * nt + t] = gofs[(size_t)t + (size_t)q * nt];
+  }
+  *NT = nt;
+  *PPT = ppt;
+  if ((long)tab.size() > capacity) return set_err("mgcm_cg2d_sum_plan: capacity %ld < %zu", capacity, tab.size());
+  memcpy(plan, tab.data(), tab.size() * sizeof(int));
+  return 0;
 }
 
 int mgcm_cg2d(mgcm_model *m, double *cg2d_b, double *cg2d_x, double *firstResidual, double *minResidualSq,

@@ -25,7 +25,7 @@ GRID_1D = ("drF", "drC", "recip_drF", "recip_drC", "rF", "rC")
 STATE_1D = ("tRef", "sRef", "pRef4EOS", "phiRefC")
 STATE_3D = ("uVel", "vVel", "wVel", "theta", "salt", "gU", "gV", "guNm1", "gvNm1", "gtNm1", "gsNm1", "rhoInSitu",
             "IVDConvCount", "sigmaR", "Kwx", "Kwy", "Kwz", "Kux", "Kvy", "uVelD", "vVelD", "uNM1", "vNM1",
-            "totPhiHyd", "alphaRho", "del2u", "del2v")
+            "totPhiHyd", "alphaRho", "del2u", "del2v", "Kuz", "Kvz", "GM_PsiX", "GM_PsiY")
 STATE_2D = ("etaN", "etaH", "fu", "fv", "SST", "lambdaThetaClimRelax", "surfaceForcingT", "surfaceForcingS",
             "Qnet", "EmPmR", "SSS", "lambdaSaltClimRelax", "etaNm1", "rStarFacC", "rStarFacW", "rStarFacS",
             "rStarExpC", "rStarExpW", "rStarExpS", "rStarDhCDt", "rStarDhWDt", "rStarDhSDt", "PmEpR", "dEtaHdt")
@@ -163,6 +163,15 @@ class Model:
         check(lib().mgcm_cg2d(self.h, _dp(b), _dp(x), ctypes.byref(f), ctypes.byref(mn), ctypes.byref(la),
                               ctypes.byref(it), ctypes.byref(itm)), "mgcm_cg2d")
         return x, f.value, mn.value, la.value, it.value, itm.value
+
+    def cg2d_sum_plan(self):
+        """(plan, NT, PPT): the device CG2D's summation order (mgcm_cg2d_sum_plan)."""
+        cap = 1 << 22
+        plan = np.zeros(cap, dtype=np.int32)
+        nt, ppt = ctypes.c_int(), ctypes.c_int()
+        check(lib().mgcm_cg2d_sum_plan(self.h, plan.ctypes.data_as(ctypes.POINTER(ctypes.c_int)), cap,
+                                       ctypes.byref(nt), ctypes.byref(ppt)), "mgcm_cg2d_sum_plan")
+        return plan[:nt.value * ppt.value].copy(), nt.value, ppt.value
 
     def cg2d_kernel(self):
         """Which CG2D kernel mgcm_init selected: 'bxy' (2x4 points/thread), 'blk2' (2x2) or 'block'."""

@@ -56,6 +56,8 @@ def lib():
         L.oracle_set_exch2.argtypes = [vp, LP, LP, LP, LP, LP, IP, IP]
         L.oracle_set_exch2.restype = c_int
         L.oracle_exch_uv_xyz.argtypes = [vp, P, P, c_int, c_int]
+        L.oracle_set_sum_plan.argtypes = [vp, IP, c_int, c_int, c_int]
+        L.oracle_set_sum_plan.restype = c_int
         _lib = L
     return _lib
 
@@ -82,6 +84,16 @@ class Oracle:
         for k, v in kw.items():
             if self.L.oracle_set_param(self.h, k.encode(), float(v)) != 0:
                 raise KeyError(k)
+
+    def set_sum_plan(self, plan, NT, PPT, NG=1):
+        """Sum the CG2D dot products in the device's order (mitgcm_amd Model.cg2d_sum_plan());
+        plan=None restores GLOBAL_SUM_TILE_RL's tile order."""
+        if plan is None:
+            assert self.L.oracle_set_sum_plan(self.h, None, 0, 0, 0) == 0
+            return
+        p = np.ascontiguousarray(plan, dtype=np.int32)
+        assert p.size == NT * PPT * NG
+        assert self.L.oracle_set_sum_plan(self.h, p.ctypes.data_as(ctypes.POINTER(ctypes.c_int)), NT, PPT, NG) == 0
 
     def get(self, name):
         return self.L.oracle_get_param(self.h, name.encode())

@@ -106,7 +106,7 @@ void oracle_free(OModel *m) {
   for (size_t i = 0; i < sizeof(dp) / sizeof(dp[0]); i++) free(*dp[i]);
   free(m->kSurfC); free(m->kSurfW); free(m->kSurfS); free(m->kLowC);
   free(m->exchS); free(m->exchU1); free(m->exchV1); free(m->exchU0); free(m->exchV0);
-  free(m->tileFace); free(m->tileEdge);
+  free(m->tileFace); free(m->tileEdge); free(m->sumPlan);
   free(m);
 }
 
@@ -254,7 +254,7 @@ int oracle_set_exch2(OModel *m, const long *scal, const long *u1, const long *v1
     *dst[q] = (long *)malloc(N2 * sizeof(long));
     memcpy(*dst[q], src[q], N2 * sizeof(long));
   }
-  free(m->tileFace); free(m->tileEdge);
+  free(m->tileFace); free(m->tileEdge); free(m->sumPlan);
   m->tileFace = (int *)malloc(m->nTiles * sizeof(int));
   m->tileEdge = (int *)malloc(m->nTiles * sizeof(int));
   memcpy(m->tileFace, face, m->nTiles * sizeof(int));

@@ -117,6 +117,9 @@ typedef struct OModel {
   long *exchU0, *exchV0;    /* same, withSigns = .FALSE. */
   int *tileFace, *tileEdge; /* exch2_myFace; edge bits N=1 S=2 E=4 W=8 (exch2_isNedge ...) */
 
+  /* --- summation order of the device CG2D (mgcm_cg2d_sum_plan), NULL = GLOBAL_SUM_TILE_RL --- */
+  int *sumPlan, planNT, planPPT, planNG;
+
   /* --- outputs of the last SOLVE_FOR_PRESSURE --- */
   double firstResidual, minResidualSq, lastResidual, sumRHS, rhsMax;
   int numIters, nIterMin;
@@ -163,6 +166,7 @@ void oracle_mom_vecinv(OModel *m, int t, int k, const double *hFacZ, const doubl
 /* hot path */
 void oracle_dynamics(OModel *m);                     /* DYNAMICS  (dynamics.F:21)  */
 void oracle_solve_for_pressure(OModel *m);           /* SOLVE_FOR_PRESSURE (solve_for_pressure.F:7) */
+int oracle_set_sum_plan(OModel *m, const int *plan, int NT, int PPT, int NG);
 void oracle_cg2d(OModel *m, double *cg2d_b, double *cg2d_x,
                  double *firstResidual, double *minResidualSq, double *lastResidual,
                  int *numIters, int *nIterMin);      /* CG2D (cg2d.F:13) */

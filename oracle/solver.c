@@ -24,6 +24,47 @@ static double gsum_tiles(const double *tile, int nTiles) {
   return s;
 }
 
+/* The device CG2D's summation order (include/mitgcm_amd.h, mgcm_cg2d_sum_plan): NG groups
+ * (workgroups) of NT threads; thread tid of group g accumulates, from 0.0, the terms at
+ * plan[(g*PPT + p)*NT + tid] for p = 0..PPT-1; the group partial is the pairwise tree over
+ * its threads in thread order (DPP row sums + row broadcasts + cross-wave row sum,
+ * zero-padded to a power of two); the total adds the group partials in group order.
+ * Test infrastructure: it lets a device solve be checked bit for bit. */
+int oracle_set_sum_plan(OModel *m, const int *plan, int NT, int PPT, int NG) {
+  free(m->sumPlan);
+  m->sumPlan = NULL;
+  if (!plan) return 0;
+  if (NT <= 0 || PPT <= 0 || NG <= 0) return -1;
+  const size_t n = (size_t)NT * PPT * NG;
+  m->sumPlan = malloc(n * sizeof(int));
+  memcpy(m->sumPlan, plan, n * sizeof(int));
+  m->planNT = NT; m->planPPT = PPT; m->planNG = NG;
+  return 0;
+}
+
+static double plan_sum(const OModel *m, const double *term) {
+  int np2 = 1;
+  while (np2 < m->planNT) np2 *= 2;
+  double *th = calloc((size_t)np2, sizeof(double));
+  double total = 0.0;
+  for (int g = 0; g < m->planNG; g++) {
+    for (int t = 0; t < np2; t++) th[t] = 0.0;
+    for (int t = 0; t < m->planNT; t++) {
+      double e = 0.0;
+      for (int p = 0; p < m->planPPT; p++) {
+        const int q = m->sumPlan[((size_t)g * m->planPPT + p) * m->planNT + t];
+        if (q >= 0) e = e + term[q];
+      }
+      th[t] = e;
+    }
+    for (int w = 1; w < np2; w *= 2)
+      for (int t = 0; t < np2; t += 2 * w) th[t] = th[t] + th[t + w];
+    total = total + th[0];
+  }
+  free(th);
+  return total;
+}
+
 int oracle_ini_cg2d(OModel *m) {
   const int sNx = m->sNx, sNy = m->sNy, OLx = m->OLx, OLy = m->OLy, Nr = m->Nr;
   long N2 = m->n2 * m->nTiles;
@@ -89,6 +130,8 @@ void oracle_cg2d(OModel *m, double *cg2d_b, double *cg2d_x, double *firstResidua
   const long N2 = m->n2 * nT;
   double *r = calloc(N2, 8), *s = calloc(N2, 8), *q = calloc(N2, 8), *xmin = calloc(N2, 8);
   double *tile = calloc(nT, 8), *tile2 = calloc(nT, 8);
+  double *term = calloc(N2, 8), *term2 = calloc(N2, 8);   /* per-point terms for a device sum plan */
+  const int dev = m->sumPlan != NULL;
   const double *aW = m->aW2d, *aS = m->aS2d, *aC = m->aC2d, *pW = m->pW, *pS = m->pS, *pC = m->pC;
   double err_sq, eta_qrN, eta_qrNM1 = 1.0, cgBeta, alpha, sumRHS, rhsMax = 0.0, rhsNorm = 1.0;
   int actualIts = 0;
@@ -125,13 +168,15 @@ void oracle_cg2d(OModel *m, double *cg2d_b, double *cg2d_x, double *firstResidua
                             aC[p] * cg2d_x[p]);
         errT = errT + r[p] * r[p];
         sumT = sumT + cg2d_b[p];
+        term[p] = r[p] * r[p];
+        term2[p] = cg2d_b[p];
       }
     tile[t] = errT; tile2[t] = sumT;
   }
   /* EXCH_S3D_RL(cg2d_r, 1): halo width 1 fill; the full-halo periodic copy is a superset */
   oracle_exch_xy(m, r);
-  err_sq = gsum_tiles(tile, nT);
-  sumRHS = gsum_tiles(tile2, nT);
+  err_sq = dev ? plan_sum(m, term) : gsum_tiles(tile, nT);
+  sumRHS = dev ? plan_sum(m, term2) : gsum_tiles(tile2, nT);
   *firstResidual = sqrt(err_sq);
   if (*nIterMin >= 0) { *nIterMin = 0; *minResidualSq = err_sq; }
   m->sumRHS = sumRHS; m->rhsMax = rhsMax;
@@ -145,10 +190,11 @@ void oracle_cg2d(OModel *m, double *cg2d_b, double *cg2d_x, double *firstResidua
             q[p] = pC[p] * r[p] + pW[p] * r[O2(m, i - 1, j, t)] + pW[O2(m, i + 1, j, t)] * r[O2(m, i + 1, j, t)] +
                    pS[p] * r[O2(m, i, j - 1, t)] + pS[O2(m, i, j + 1, t)] * r[O2(m, i, j + 1, t)];
             e = e + q[p] * r[p];
+            term[p] = q[p] * r[p];
           }
         tile[t] = e;
       }
-      eta_qrN = gsum_tiles(tile, nT);
+      eta_qrN = dev ? plan_sum(m, term) : gsum_tiles(tile, nT);
       cgBeta = eta_qrN / eta_qrNM1;
       eta_qrNM1 = eta_qrN;
       for (int t = 0; t < nT; t++)
@@ -166,10 +212,11 @@ void oracle_cg2d(OModel *m, double *cg2d_b, double *cg2d_x, double *firstResidua
             q[p] = aW[p] * s[O2(m, i - 1, j, t)] + aW[O2(m, i + 1, j, t)] * s[O2(m, i + 1, j, t)] +
                    aS[p] * s[O2(m, i, j - 1, t)] + aS[O2(m, i, j + 1, t)] * s[O2(m, i, j + 1, t)] + aC[p] * s[p];
             a = a + s[p] * q[p];
+            term[p] = s[p] * q[p];
           }
         tile[t] = a;
       }
-      alpha = gsum_tiles(tile, nT);
+      alpha = dev ? plan_sum(m, term) : gsum_tiles(tile, nT);
       alpha = eta_qrN / alpha;
       for (int t = 0; t < nT; t++) {
         double e = 0.0;
@@ -179,11 +226,12 @@ void oracle_cg2d(OModel *m, double *cg2d_b, double *cg2d_x, double *firstResidua
             cg2d_x[p] = cg2d_x[p] + alpha * s[p];
             r[p] = r[p] - alpha * q[p];
             e = e + r[p] * r[p];
+            term[p] = r[p] * r[p];
           }
         tile[t] = e;
       }
       actualIts = it2d;
-      err_sq = gsum_tiles(tile, nT);
+      err_sq = dev ? plan_sum(m, term) : gsum_tiles(tile, nT);
       if (err_sq < m->cg2dTolerance_sq) break;
       if (err_sq < *minResidualSq) {
         *minResidualSq = err_sq;
@@ -205,7 +253,7 @@ void oracle_cg2d(OModel *m, double *cg2d_b, double *cg2d_x, double *firstResidua
         for (int i = 1; i <= sNx; i++) cg2d_x[O2(m, i, j, t)] = cg2d_x[O2(m, i, j, t)] / rhsNorm;
   *lastResidual = sqrt(err_sq);
   *numIters = actualIts;
-  free(r); free(s); free(q); free(xmin); free(tile); free(tile2);
+  free(r); free(s); free(q); free(xmin); free(tile); free(tile2); free(term); free(term2);
 }
 
 /* SOLVE_FOR_PRESSURE (solve_for_pressure.F:122-385), hydrostatic, no OBCS, linear FS */

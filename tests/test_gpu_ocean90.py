@@ -9,10 +9,16 @@ Bars:
     bit-exact against the oracle (same one-tile layout);
   * DO_OCEANIC_PHYS + THERMODYNAMICS and DYNAMICS (phi_hyd + QH, del2u, mom_fluxform
     with r*, CD scheme) from the oracle's state after 2 steps: bit-exact;
-  * 10 steps against the oracle (one tile): cg2d_iters identical, >= 10 digits on the
-    dynstat values (the CG2D sums are tree reductions on the device), and against
-    results/output.txt (36 tiles): >= 9.5 digits except the near-zero eta mean and the
-    1e-13 last CG2D residual.
+  * 10 steps against the oracle summing CG2D's dot products in the device's order
+    (mgcm_cg2d_sum_plan -> oracle_set_sum_plan): every dynstat value, every CG2D
+    residual and iteration count and the state arrays identical, bit for bit;
+  * 10 steps against the oracle in the reference's own summation order (tile-ordered
+    sequential sums, 1 tile): cg2d_iters identical, >= 10 digits (measured 10.33 at
+    cg2d_init_res).  Since the device is bit-identical to the device-order oracle, this
+    is purely the problem's sensitivity to the order of CG2D's sums: the oracle against
+    itself in two summation orders differs by exactly as much;
+  * against results/output.txt (36 tiles): >= 10 digits except the near-zero eta mean
+    and the 1e-13 last CG2D residual.
 """
 import json
 import os
@@ -106,24 +112,37 @@ def test_ocean90_dynamics_bitexact():
 
 
 def test_ocean90_10_steps(golden_dir):
-    o, g = _oracle(0)
+    o, g = _oracle(0)            # reference summation order
     m = _model()
+    plan, NT, PPT = m.cg2d_sum_plan()
+    od_dev, _ = _oracle(0)       # the device's summation order
+    od_dev.set_sum_plan(plan, NT, PPT)
     gold = json.load(open(os.path.join(golden_dir, EXP, "monitor.json")))
     from mitgcm_amd.model import dynstat
     worst_o, worst_r = (99.0, None), (99.0, None)
     for step in range(1, 11):
         m.forward_step(1)
         o.forward_step()
-        od = o.dynstat()
+        od_dev.forward_step()
+        od, dd = o.dynstat(), od_dev.dynstat()
         md = m.solve_stats()
         md.update(dynstat(m))
         assert md["cg2d_iters"] == od["cg2d_iters"], (step, md["cg2d_iters"], od["cg2d_iters"])
         for k, v in md.items():
+            if k in dd:
+                assert v == dd[k], ("device-order oracle", step, k, v, dd[k])
             if k in od and k != "cg2d_iters" and not k.startswith("cg2d"):
                 worst_o = min(worst_o, (digits(v, od[k]), (step, k, v, od[k])))
             if k in gold[step] and k not in ("cg2d_iters", "dynstat_eta_mean", "cg2d_last_res"):
                 worst_r = min(worst_r, (digits(v, gold[step][k]), (step, k, v, gold[step][k])))
+        worst_o = min(worst_o, (digits(md["cg2d_init_res"], od["cg2d_init_res"]), (step, "cg2d_init_res")))
+    for n in ("uVel", "vVel", "wVel", "theta", "salt", "etaN", "etaH", "guNm1", "gvNm1", "gtNm1", "gsNm1"):
+        dev = m.get(n)
+        ref = np.array(od_dev.arr(n)).reshape(dev.shape)
+        inner = (Ellipsis,) + g.sl(1, g.sNx, 1, g.sNy)
+        assert np.array_equal(dev[inner], ref[inner]), (n, np.abs(dev - ref)[inner].max())
     m.close()
-    print("ocean90 device vs oracle: %.2f at %s; vs reference: %.2f at %s" % (worst_o + worst_r))
+    print("ocean90 10 steps: device == device-order oracle bit for bit; vs reference-order oracle %.2f at %s; "
+          "vs results/output.txt %.2f at %s" % (worst_o + worst_r))
     assert worst_o[0] >= 10.0, worst_o
-    assert worst_r[0] >= 9.5, worst_r
+    assert worst_r[0] >= 10.0, worst_r
