@@ -120,12 +120,14 @@ int mgcm_cg2d(mgcm_model *m, double *cg2d_b, double *cg2d_x, double *firstResidu
               double *minResidualSq, double *lastResidual, int *numIters, int *nIterMin);
 
 /* The summation order of the device CG2D's global sums (the GLOBAL_SUM_TILE_RL it
- * replaces, eesupp/src/global_sum_tile.F:161-191, sums tile partials in tile order): thread
- * tid accumulates the per-point terms at plan[p*NT + tid] (2-D flat offsets, -1 = none)
- * for p = 0..PPT-1, then the NT partials are added by a pairwise tree in thread order.
- * The oracle restates it (oracle_set_sum_plan) so that a device solve can be checked
- * bit for bit.  capacity = length of plan. */
-int mgcm_cg2d_sum_plan(mgcm_model *m, int *plan, long capacity, int *NT, int *PPT);
+ * replaces, eesupp/src/global_sum_tile.F:161-191, sums tile partials in tile order): NG
+ * workgroups of NT threads; thread tid of workgroup g accumulates, from 0.0, the per-point
+ * terms at plan[(g*PPT + p)*NT + tid] (2-D flat offsets, -1 = none) for p = 0..PPT-1; a
+ * workgroup's partial is the pairwise tree over its threads in thread order; lane l then
+ * adds the partials l, l+64, ... in order and the total is the pairwise tree over the 64
+ * lanes.  The oracle restates it (oracle_set_sum_plan) so that a device solve can be
+ * checked bit for bit.  capacity = length of plan. */
+int mgcm_cg2d_sum_plan(mgcm_model *m, int *plan, long capacity, int *NT, int *PPT, int *NG);
 
 /* Statistics of the most recent solve (what SOLVE_FOR_PRESSURE prints,
  * solve_for_pressure.F:333-351) for step `back` (0 = latest) of the last

@@ -47,7 +47,7 @@ def lib():
         "mgcm_forward_step": (ci, [vp, ci]),
         "mgcm_sync": (ci, [vp]),
         "mgcm_cg2d": (ci, [vp, PD, PD, PD, PD, PD, PI, PI]),
-        "mgcm_cg2d_sum_plan": (ci, [vp, PI, cl, PI, PI]),
+        "mgcm_cg2d_sum_plan": (ci, [vp, PI, cl, PI, PI, PI]),
         "mgcm_solve_stats": (ci, [vp, ci, PD, PD, PI, PD]),
         "mgcm_kernel_ms": (cd, [vp, cs, PI]),
         "mgcm_kernel_timing": (None, [vp, ci]),

@@ -171,6 +171,25 @@ struct XFields {
   int n;
 };
 
+// Multi-workgroup CG2D (kernels_cg2d_mwg.hip): tables of every part (a row strip of a tile,
+// one workgroup), built by build_mwg (model.hip); slot s = p*NT + tid.
+struct MwgTables {
+  const int *ownG;        // [G][OPT*NT] 2-D offset of the owned point (-1: none)
+  const int *ownC;        // [G][OPT*NT] compact point index (exchange buffer slot)
+  const unsigned *ownNb;  // [G][OPT*NT][2] LDS slots (W | E<<16), (S | N<<16)
+  const unsigned *ownExp; // [G][NT] bit p set: owned point p is in another part's rings
+  const int *ringG;       // [G][RPT*NT] 2-D offset of the ring-1 point (-1: none)
+  const unsigned *ringNb; // [G][RPT*NT][2]
+  const int *impC;        // [G][IMAX] compact index of ring-1 then ring-2 point (LDS slot NO + q)
+  const int *impG;        // [G][IMAX] its 2-D offset
+  const int *nImp;        // [G]
+  int G, IMAX, SZ;        // parts, import capacity, LDS slots before the ZERO slot
+  int pinned;             // 1: only blockIdx.x % 8 == 0 work (all parts on one XCD)
+  double *xs;             // [nPts] exchange buffer of s (sc1 stores / loads)
+  double *part;           // [2][3][G] workgroup partials (sc1)
+  unsigned *ctr;          // [0] arrival counter, [1] timeout word (zeroed before each launch)
+};
+
 // Per-solve record written by the device CG2D (one slot per time step).
 struct SolveRecord {
   double firstResidual, lastResidual, minResidualSq, rhsMax, sumRHS;

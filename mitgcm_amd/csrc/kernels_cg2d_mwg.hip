@@ -1,0 +1,372 @@
+// kernels_cg2d_mwg.hip -- CG2D (model/src/cg2d.F:13-415) as one persistent multi-workgroup
+// launch, for solves that do not fit one CU: the cube's 6 faces (6 144 points), the LLC
+// facets (105 300 points), anything past the single-workgroup kernels' 4 096 / 8 192.
+//
+// Decomposition.  Every tile is cut into parts (row strips) of <= OPT*NT points; one
+// workgroup owns one part (mgcm_model::mwg, built by build_mwg in model.hip).  A thread
+// holds OPT owned points: x, r, s, q and their 10 operator coefficients in VGPRs; r and s
+// of the part live in LDS.  The points of the neighbouring parts that the stencils reach
+// form two rings around the part:
+//   ring 1 = neighbours of owned points (through the halo map, EXCH_S3D_RL's copies),
+//   ring 2 = neighbours of ring-1 points.
+// A thread also holds RPT ring-1 points, for which the workgroup recomputes r redundantly
+// (r -= alpha*A s needs s on rings 1 and 2): the owner and the neighbour evaluate the same
+// expression on the same bytes, so the copies stay bit-identical and the exchange of r that
+// cg2d.F does after each update (EXCH_S3D_RL(cg2d_r), :337) needs no synchronisation.
+//
+// Per iteration three grid-wide hand-offs (Guideline 16, R1 form: payload stored sc1 and
+// drained with s_waitcnt vmcnt(0), one relaxed agent-scope add per workgroup on an arrival
+// counter, one lane polls relaxed with s_sleep, every load of handed-off bytes sc1):
+//   sync B  partials of (r,r) of iteration n and (M r, r) of n+1 (the reference's err_sq and
+//           eta_qrN, reduced together: same values, cg2d.F:211-243, 321-337);
+//   sync C  s exported (owned points that lie in another part's rings) -> imported;
+//   sync D  partials of (s, A s) -> alpha (cg2d.F:268-301).
+// Global sums in a fixed order, independent of placement and of how many GPUs share the
+// tiles: thread partials (OPT terms in order) -> pairwise tree over the NT threads -> per
+// workgroup partial; lane l of every wave adds partials l, l+64, ... in order, then the
+// pairwise tree over the 64 lanes.  mgcm_cg2d_sum_plan exports it for the oracle.
+#include "common.h"
+
+namespace mgcm {
+
+typedef __attribute__((address_space(1))) unsigned long long gu64;
+typedef __attribute__((address_space(1))) unsigned int gu32;
+#define RLX_AGENT __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT
+
+// ---- DPP sums (the same operations as kernels_solve.hip's block reductions) ----
+template <int CTRL>
+__device__ __forceinline__ double mw_dpp(double v) {
+  const long long b = __builtin_bit_cast(long long, v);
+  const int lo = __builtin_amdgcn_mov_dpp((int)(b & 0xffffffff), CTRL, 0xF, 0xF, true);
+  const int hi = __builtin_amdgcn_mov_dpp((int)(b >> 32), CTRL, 0xF, 0xF, true);
+  return __builtin_bit_cast(double, ((long long)hi << 32) | (unsigned)lo);
+}
+template <int CTRL, int ROWMASK>
+__device__ __forceinline__ double mw_bcast(double v) {
+  const long long b = __builtin_bit_cast(long long, v);
+  const int lo = __builtin_amdgcn_update_dpp(0, (int)(b & 0xffffffff), CTRL, ROWMASK, 0xF, false);
+  const int hi = __builtin_amdgcn_update_dpp(0, (int)(b >> 32), CTRL, ROWMASK, 0xF, false);
+  return __builtin_bit_cast(double, ((long long)hi << 32) | (unsigned)lo);
+}
+__device__ __forceinline__ double mw_lane(double v, int l) {
+  const long long b = __builtin_bit_cast(long long, v);
+  const int lo = __builtin_amdgcn_readlane((int)(b & 0xffffffff), l);
+  const int hi = __builtin_amdgcn_readlane((int)(b >> 32), l);
+  return __builtin_bit_cast(double, ((long long)hi << 32) | (unsigned)lo);
+}
+__device__ __forceinline__ double mw_row16(double v) {
+  v = v + mw_dpp<0xB1>(v);
+  v = v + mw_dpp<0x4E>(v);
+  v = v + mw_dpp<0x141>(v);
+  v = v + mw_dpp<0x140>(v);
+  return v;
+}
+__device__ __forceinline__ double mw_rowmax16(double v) {
+  v = fmax(v, mw_dpp<0xB1>(v));
+  v = fmax(v, mw_dpp<0x4E>(v));
+  v = fmax(v, mw_dpp<0x141>(v));
+  v = fmax(v, mw_dpp<0x140>(v));
+  return v;
+}
+// pairwise tree over the 64 lanes, uniform result
+__device__ __forceinline__ double mw_wave_sum(double v) {
+  v = mw_row16(v);
+  v = v + mw_bcast<0x142, 0xA>(v);
+  v = v + mw_bcast<0x143, 0xC>(v);
+  return mw_lane(v, 63);
+}
+__device__ __forceinline__ double mw_wave_max(double v) {
+  v = mw_rowmax16(v);
+  return fmax(fmax(mw_lane(v, 0), mw_lane(v, 16)), fmax(mw_lane(v, 32), mw_lane(v, 48)));
+}
+
+constexpr int MW_NT = 256, MW_OPT = 4, MW_RPT = 1, MW_NW = MW_NT / 64;
+constexpr int MW_NV = 3;   // values per reduction
+
+// One grid-wide hand-off: NV workgroup partials (a pairwise tree over the threads of
+// v[0..NV-1]) published and combined in the fixed order; MAXOP: combine by max instead.
+template <int NV, bool MAXOP>
+__device__ __forceinline__ bool mw_sync(double *v, const MwgTables &T, int g, int &nsync, double *red) {
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int par = nsync & 1;
+  gu64 *P = (gu64 *)(T.part + (size_t)par * MW_NV * T.G);
+  if (NV > 0) {
+    // workgroup partial: the pairwise tree over its threads (wave tree, then the row-16
+    // tree over the zero-padded wave values: the operations of block_sum_nw)
+#pragma unroll
+    for (int q = 0; q < NV; q++) {
+      const double w = MAXOP ? mw_wave_max(v[q]) : mw_wave_sum(v[q]);
+      if (lane == 0) red[q * 16 + wv] = w;
+    }
+    __syncthreads();
+    if (wv == 0) {
+#pragma unroll
+      for (int q = 0; q < NV; q++) {
+        const int l = lane & 15;
+        const double xw = l < MW_NW ? red[q * 16 + l] : 0.0;
+        const double wgp = MAXOP ? mw_rowmax16(xw) : mw_row16(xw);
+        if (lane == 0) __hip_atomic_store(P + (size_t)q * T.G + g, __builtin_bit_cast(unsigned long long, wgp), RLX_AGENT);
+      }
+    }
+  }
+  // every storing wave drains its sc1 stores (partials, exported s) before the arrival
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  nsync++;
+  if (tid == 0) {
+    gu32 *ctr = (gu32 *)T.ctr;
+    __hip_atomic_fetch_add(ctr, 1u, RLX_AGENT);
+    const unsigned target = (unsigned)(T.G * nsync);
+    unsigned spins = 0;
+    double okv = 1.0;
+    while (__hip_atomic_load(ctr, RLX_AGENT) < target) {
+      if (__hip_atomic_load(ctr + 1, RLX_AGENT) != 0u || ++spins > (1u << 24)) {
+        __hip_atomic_store(ctr + 1, 1u, RLX_AGENT);   // timeout word: every part gives up
+        okv = 0.0;
+        break;
+      }
+      __builtin_amdgcn_s_sleep(2);
+    }
+    red[15 * 16] = okv;
+  }
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");   // every handed-off byte is loaded sc1 below
+  __syncthreads();
+  const bool ok = red[15 * 16] != 0.0;
+  // combine: lane l adds partials l, l+64, ... in order, then the pairwise tree over the lanes
+#pragma unroll
+  for (int q = 0; q < NV; q++) {
+    double acc = 0.0;
+    for (int gg = lane; gg < T.G; gg += 64) {
+      const double xg = __builtin_bit_cast(double, __hip_atomic_load(P + (size_t)q * T.G + gg, RLX_AGENT));
+      acc = MAXOP ? fmax(acc, xg) : acc + xg;
+    }
+    v[q] = MAXOP ? mw_wave_max(acc) : mw_wave_sum(acc);
+  }
+  return ok;
+}
+
+template <bool PINNED>
+__global__ void __launch_bounds__(MW_NT) k_cg2d_mwg(Dims d, Params p, Fields f, MwgTables T, int maxIters,
+                                                    SolveRecord *rec, int *stepCounter) {
+  int g = (int)blockIdx.x;
+  if (PINNED) {
+    if (g % MG_NXCD) return;   // parts on XCD 0 only: their hand-offs stay in one L2
+    g /= MG_NXCD;
+  }
+  if (g >= T.G) return;
+  constexpr int NO = MW_OPT * MW_NT, NR = MW_RPT * MW_NT;
+  extern __shared__ __attribute__((aligned(16))) double lds[];
+  const int SZ = T.SZ;            // own + ring 1 + ring 2 slots; ZERO slot = SZ
+  double *s_l = lds;              // SZ + 1
+  double *r_l = lds + (SZ + 1);   // NO + NR used, + ZERO at SZ
+  double *red = lds + 2 * (SZ + 1);   // 16 x 16 scratch
+  const int tid = threadIdx.x;
+  int nsync = 0;
+  const size_t go = (size_t)g * NO, gr = (size_t)g * NR, gi = (size_t)g * T.IMAX;
+  // ---- owned points: offsets, neighbour slots, coefficients (cg2d.F operator rows)
+  int G2[MW_OPT];
+  unsigned nwe[MW_OPT], nsn[MW_OPT];
+  double aW0[MW_OPT], aW1[MW_OPT], aS0[MW_OPT], aS1[MW_OPT], aC[MW_OPT];
+  double pC[MW_OPT], pW0[MW_OPT], pW1[MW_OPT], pS0[MW_OPT], pS1[MW_OPT];
+  double x[MW_OPT], r[MW_OPT], s[MW_OPT], q[MW_OPT], b[MW_OPT];
+  const unsigned exp = T.ownExp[(size_t)g * MW_NT + tid];
+  const long nx = d.nx;
+#pragma unroll
+  for (int m = 0; m < MW_OPT; m++) {
+    const int sl = m * MW_NT + tid;
+    G2[m] = T.ownG[go + sl];
+    nwe[m] = T.ownNb[2 * (go + sl)];
+    nsn[m] = T.ownNb[2 * (go + sl) + 1];
+    const bool act = G2[m] >= 0;
+    const long gg = act ? G2[m] : 0;
+    const double az = act ? 1.0 : 0.0;
+    aW0[m] = az * f.aW2d[gg]; aW1[m] = az * f.aW2d[gg + 1]; aS0[m] = az * f.aS2d[gg]; aS1[m] = az * f.aS2d[gg + nx];
+    aC[m] = az * f.aC2d[gg];
+    pC[m] = az * f.pC[gg]; pW0[m] = az * f.pW[gg]; pW1[m] = az * f.pW[gg + 1]; pS0[m] = az * f.pS[gg];
+    pS1[m] = az * f.pS[gg + nx];
+    b[m] = act ? f.cg2d_b[gg] : 0.0;
+    x[m] = act ? f.cg2d_x[gg] : 0.0;
+    s[m] = 0.0;
+  }
+  // ---- ring-1 points (r kept redundantly)
+  int RG[MW_RPT];
+  unsigned rwe[MW_RPT], rsn[MW_RPT];
+  double raW0[MW_RPT], raW1[MW_RPT], raS0[MW_RPT], raS1[MW_RPT], raC[MW_RPT], rr[MW_RPT], rb[MW_RPT];
+#pragma unroll
+  for (int m = 0; m < MW_RPT; m++) {
+    const int sl = m * MW_NT + tid;
+    RG[m] = T.ringG[gr + sl];
+    rwe[m] = T.ringNb[2 * (gr + sl)];
+    rsn[m] = T.ringNb[2 * (gr + sl) + 1];
+    const bool act = RG[m] >= 0;
+    const long gg = act ? RG[m] : 0;
+    const double az = act ? 1.0 : 0.0;
+    raW0[m] = az * f.aW2d[gg]; raW1[m] = az * f.aW2d[gg + 1]; raS0[m] = az * f.aS2d[gg]; raS1[m] = az * f.aS2d[gg + nx];
+    raC[m] = az * f.aC2d[gg];
+    rb[m] = act ? f.cg2d_b[gg] : 0.0;
+  }
+  const int nImp = T.nImp[g];
+#define LO(w) ((w) & 0xFFFFu)
+#define HI(w) ((w) >> 16)
+
+  // cg2d.F:104-133: normalise the RHS by its global max
+  double rhsMaxV[1] = {0.0};
+#pragma unroll
+  for (int m = 0; m < MW_OPT; m++) { b[m] = b[m] * p.cg2dNorm; rhsMaxV[0] = fmax(fabs(b[m]), rhsMaxV[0]); }
+  bool ok = mw_sync<1, true>(rhsMaxV, T, g, nsync, red);
+  const double rhsMax = rhsMaxV[0];
+  double rhsNorm = 1.0;
+  if (p.cg2dNormaliseRHS) {
+    if (rhsMax != 0.0) rhsNorm = 1.0 / rhsMax;
+#pragma unroll
+    for (int m = 0; m < MW_OPT; m++) { b[m] = b[m] * rhsNorm; x[m] = x[m] * rhsNorm; }
+  }
+#pragma unroll
+  for (int m = 0; m < MW_RPT; m++) rb[m] = (rb[m] * p.cg2dNorm) * (p.cg2dNormaliseRHS ? rhsNorm : 1.0);
+  // EXCH_XY_RL(cg2d_x): x of owned points and of both rings into s_l (the ring values are read
+  // from cg2d_x, written before this launch, and scaled with the owner's arithmetic)
+#pragma unroll
+  for (int m = 0; m < MW_OPT; m++) s_l[m * MW_NT + tid] = x[m];
+  for (int qq = tid; qq < nImp; qq += MW_NT) {
+    const double xv = f.cg2d_x[T.impG[gi + qq]];
+    s_l[NO + qq] = p.cg2dNormaliseRHS ? xv * rhsNorm : xv;
+  }
+  if (tid == 0) { s_l[SZ] = 0.0; r_l[SZ] = 0.0; }
+  __syncthreads();
+  // cg2d.F:139-180: r = b - A x on owned points and ring 1
+  double v3[3] = {0.0, 0.0, 0.0};
+#pragma unroll
+  for (int m = 0; m < MW_OPT; m++) {
+    r[m] = b[m] - (aW0[m] * s_l[LO(nwe[m])] + aW1[m] * s_l[HI(nwe[m])] + aS0[m] * s_l[LO(nsn[m])] +
+                   aS1[m] * s_l[HI(nsn[m])] + aC[m] * x[m]);
+    v3[0] = v3[0] + r[m] * r[m];
+    v3[1] = v3[1] + b[m];
+  }
+#pragma unroll
+  for (int m = 0; m < MW_RPT; m++)
+    rr[m] = rb[m] - (raW0[m] * s_l[LO(rwe[m])] + raW1[m] * s_l[HI(rwe[m])] + raS0[m] * s_l[LO(rsn[m])] +
+                     raS1[m] * s_l[HI(rsn[m])] + raC[m] * s_l[NO + m * MW_NT + tid]);
+#pragma unroll
+  for (int m = 0; m < MW_OPT; m++)
+    if (G2[m] >= 0) f.cg2d_b[G2[m]] = b[m];   // cg2d_b is INOUT (normalised in place)
+#pragma unroll
+  for (int m = 0; m < MW_OPT; m++) r_l[m * MW_NT + tid] = r[m];
+#pragma unroll
+  for (int m = 0; m < MW_RPT; m++) r_l[NO + m * MW_NT + tid] = rr[m];
+  __syncthreads();
+  // q = M r and (q, r) of iteration 1, reduced with err_sq and sumRHS
+#pragma unroll
+  for (int m = 0; m < MW_OPT; m++) {
+    q[m] = pC[m] * r[m] + pW0[m] * r_l[LO(nwe[m])] + pW1[m] * r_l[HI(nwe[m])] + pS0[m] * r_l[LO(nsn[m])] +
+           pS1[m] * r_l[HI(nsn[m])];
+    v3[2] = v3[2] + q[m] * r[m];
+  }
+  ok = ok && mw_sync<3, false>(v3, T, g, nsync, red);
+  double err_sq = v3[0];
+  const double sumRHS = v3[1];
+  double eta_qrN = v3[2], eta_qrNM1 = 1.0;
+  const double firstResidual = sqrt(err_sq);
+  int actualIts = 0;
+  if (ok && !(err_sq < p.cg2dTolerance_sq)) {
+    gu64 *xs = (gu64 *)T.xs;
+    for (int it2d = 1; it2d <= maxIters; it2d++) {
+      const double cgBeta = eta_qrN / eta_qrNM1;
+      eta_qrNM1 = eta_qrN;
+      // s = q + beta*s; EXCH_S3D_RL(cg2d_s): export the points other parts read
+#pragma unroll
+      for (int m = 0; m < MW_OPT; m++) {
+        s[m] = q[m] + cgBeta * s[m];
+        s_l[m * MW_NT + tid] = s[m];
+        if ((exp >> m) & 1u) __hip_atomic_store(xs + T.ownC[go + m * MW_NT + tid], __builtin_bit_cast(unsigned long long, s[m]), RLX_AGENT);
+      }
+      ok = mw_sync<0, false>(nullptr, T, g, nsync, red);
+      if (!ok) break;
+      for (int qq = tid; qq < nImp; qq += MW_NT)
+        s_l[NO + qq] = __builtin_bit_cast(double, __hip_atomic_load(xs + T.impC[gi + qq], RLX_AGENT));
+      __syncthreads();
+      // q = A s (owned + ring 1); alpha = eta_qrN / (s, A s)
+      double av[1] = {0.0};
+#pragma unroll
+      for (int m = 0; m < MW_OPT; m++) {
+        q[m] = aW0[m] * s_l[LO(nwe[m])] + aW1[m] * s_l[HI(nwe[m])] + aS0[m] * s_l[LO(nsn[m])] + aS1[m] * s_l[HI(nsn[m])] +
+               aC[m] * s[m];
+        av[0] = av[0] + s[m] * q[m];
+      }
+      double rq[MW_RPT];
+#pragma unroll
+      for (int m = 0; m < MW_RPT; m++)
+        rq[m] = raW0[m] * s_l[LO(rwe[m])] + raW1[m] * s_l[HI(rwe[m])] + raS0[m] * s_l[LO(rsn[m])] +
+                raS1[m] * s_l[HI(rsn[m])] + raC[m] * s_l[NO + m * MW_NT + tid];
+      ok = mw_sync<1, false>(av, T, g, nsync, red);
+      if (!ok) break;
+      const double alpha = eta_qrN / av[0];
+      // x += alpha s ; r -= alpha q (owned and ring 1); err_sq and the next (M r, r)
+      double v2[2] = {0.0, 0.0};
+#pragma unroll
+      for (int m = 0; m < MW_OPT; m++) {
+        x[m] = x[m] + alpha * s[m];
+        r[m] = r[m] - alpha * q[m];
+        v2[0] = v2[0] + r[m] * r[m];
+        r_l[m * MW_NT + tid] = r[m];
+      }
+#pragma unroll
+      for (int m = 0; m < MW_RPT; m++) {
+        rr[m] = rr[m] - alpha * rq[m];
+        r_l[NO + m * MW_NT + tid] = rr[m];
+      }
+      actualIts = it2d;
+      __syncthreads();
+#pragma unroll
+      for (int m = 0; m < MW_OPT; m++) {
+        q[m] = pC[m] * r[m] + pW0[m] * r_l[LO(nwe[m])] + pW1[m] * r_l[HI(nwe[m])] + pS0[m] * r_l[LO(nsn[m])] +
+               pS1[m] * r_l[HI(nsn[m])];
+        v2[1] = v2[1] + q[m] * r[m];
+      }
+      ok = mw_sync<2, false>(v2, T, g, nsync, red);
+      if (!ok) break;
+      err_sq = v2[0];
+      eta_qrN = v2[1];
+      if (err_sq < p.cg2dTolerance_sq) break;
+    }
+  }
+#pragma unroll
+  for (int m = 0; m < MW_OPT; m++) {
+    double xv = x[m];
+    if (p.cg2dNormaliseRHS) xv = xv / rhsNorm;
+    if (G2[m] >= 0) f.cg2d_x[G2[m]] = xv;
+  }
+  if (g == 0 && tid == 0) {
+    const int st = stepCounter ? *stepCounter : 0;
+    SolveRecord &R = rec[st];
+    R.firstResidual = firstResidual;
+    R.lastResidual = sqrt(err_sq);
+    R.minResidualSq = -1.0;
+    R.rhsMax = rhsMax;
+    R.sumRHS = sumRHS;
+    R.numIters = ok ? actualIts : -1;   // -1: a grid hand-off timed out
+    R.nIterMin = -1;
+  }
+#undef LO
+#undef HI
+}
+
+int cg2d_mwg_geometry(int *nt, int *opt, int *rpt) { *nt = MW_NT; *opt = MW_OPT; *rpt = MW_RPT; return 0; }
+
+hipError_t launch_cg2d_mwg(const Dims &d, const Params &p, const Fields &f, const MwgTables &T, int maxIters,
+                           SolveRecord *rec, int *stepCounter, hipStream_t s) {
+  hipError_t e = hipMemsetAsync(T.ctr, 0, 16, s);   // arrival counter + timeout word, every launch
+  if (e != hipSuccess) return e;
+  const size_t lds = (size_t)(2 * (T.SZ + 1) + 16 * 16) * sizeof(double);
+  auto kern = T.pinned ? k_cg2d_mwg<true> : k_cg2d_mwg<false>;
+  static bool attrSet[2] = {false, false};
+  if (!attrSet[T.pinned]) {
+    e = hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    if (e != hipSuccess) return e;
+    attrSet[T.pinned] = true;
+  }
+  const unsigned grid = (unsigned)(T.pinned ? T.G * MG_NXCD : T.G);
+  hipLaunchKernelGGL(kern, dim3(grid), dim3(MW_NT), lds, s, d, p, f, T, maxIters, rec, stepCounter);
+  return hipGetLastError();
+}
+
+}  // namespace mgcm

@@ -11,6 +11,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <algorithm>
 #include <map>
 #include <utility>
 #include <string>
@@ -47,6 +48,9 @@ hipError_t launch_oceanic_phys(const Dims &, const Params &, const Fields &, con
 hipError_t launch_tracer_step(const Dims &, const Params &, const Fields &, const TracerArgs &, const int *, hipStream_t);
 hipError_t launch_continuity_ec(const Dims &, const Params &, const Fields &, hipStream_t);
 hipError_t launch_copy(double *, const double *, long, hipStream_t);
+int cg2d_mwg_geometry(int *, int *, int *);
+hipError_t launch_cg2d_mwg(const Dims &, const Params &, const Fields &, const MwgTables &, int, SolveRecord *, int *,
+                           hipStream_t);
 }  // namespace mgcm
 
 using namespace mgcm;
@@ -176,6 +180,11 @@ struct mgcm_model {
   int *d_blkx = nullptr;
   int nBlkX = 0;
   bool latlonTopology = true;   // false once a custom halo map (e.g. EXCH2 cube) is installed
+  // multi-workgroup CG2D (kernels_cg2d_mwg.hip): tables of every part, device buffers
+  bool useMwg = false;
+  MwgTables mwg{};
+  std::vector<void *> mwgAllocs;
+  std::vector<int> mwgPlan;   // summation plan for mgcm_cg2d_sum_plan: [(g*OPT + p)*NT + tid]
   // EXCH2 C-grid vector maps (mgcm_set_uv_map): [withSigns] -> (dst, code) pairs of this
   // process's tiles, u entries first; code = +-(src+1), src indexing [u | v]
   bool uvMap = false;
@@ -483,6 +492,148 @@ static int build_nbr(mgcm_model *m) {
   return 0;
 }
 
+// Multi-workgroup CG2D tables (kernels_cg2d_mwg.hip): every tile cut into row strips of
+// <= OPT*NT points (one workgroup each), the two rings of neighbouring-part points each
+// strip's stencils reach (through the halo map), LDS slot tables, export flags.
+template <typename T>
+static int mwg_upload(mgcm_model *m, const std::vector<T> &h, const T **out) {
+  T *dptr = nullptr;
+  HIPCHK(hipMalloc(&dptr, (h.empty() ? 1 : h.size()) * sizeof(T)));
+  if (!h.empty()) HIPCHK(hipMemcpy(dptr, h.data(), h.size() * sizeof(T), hipMemcpyHostToDevice));
+  m->mwgAllocs.push_back(dptr);
+  *out = dptr;
+  return 0;
+}
+
+static int build_mwg(mgcm_model *m) {
+  for (void *q : m->mwgAllocs) (void)hipFree(q);
+  m->mwgAllocs.clear();
+  m->useMwg = false;
+  const Dims &d = m->d;
+  int NT, OPT, RPT;
+  cg2d_mwg_geometry(&NT, &OPT, &RPT);
+  const int NO = NT * OPT, NR = NT * RPT;
+  if (d.sNx > NO) return set_err("build_mwg: sNx = %d > %d points per part", d.sNx, NO);
+  const long N2 = d.n2 * d.nTiles;
+  std::vector<long> srcOf(N2, -1);
+  for (size_t h = 0; h + 1 < m->h_halo.size(); h += 2) srcOf[m->h_halo[h]] = m->h_halo[h + 1];
+  const int ppTile = d.sNx * d.sNy;
+  auto comp = [&](int i, int j, int t) { return t * ppTile + (j - 1) * d.sNx + (i - 1); };
+  auto g2of = [&](int c) { const int t = c / ppTile, l = c % ppTile; return (int)MG_I2(d, l % d.sNx + 1, l / d.sNx + 1, t); };
+  // neighbour (dir 0 W, 1 E, 2 S, 3 N) of compact point c, through the halo map; -1 = none
+  auto nbr = [&](int c, int dir) -> int {
+    const int t = c / ppTile, l = c % ppTile, i = l % d.sNx + 1, j = l / d.sNx + 1;
+    const int ii = i + (dir == 0 ? -1 : dir == 1 ? 1 : 0), jj = j + (dir == 2 ? -1 : dir == 3 ? 1 : 0);
+    if (ii >= 1 && ii <= d.sNx && jj >= 1 && jj <= d.sNy) return comp(ii, jj, t);
+    const long src = srcOf[MG_I2(d, ii, jj, t)];
+    if (src < 0) return -1;
+    const int st = (int)(src / d.n2), sl = (int)(src % d.n2);
+    const int si = sl % d.nx - d.OLx + 1, sj = sl / d.nx - d.OLy + 1;
+    if (si < 1 || si > d.sNx || sj < 1 || sj > d.sNy) return -1;
+    return comp(si, sj, st);
+  };
+  // parts: row strips of each tile
+  int rows = NO / d.sNx;
+  while (rows > 1 && 2 * (d.sNx + rows) > NR) rows--;
+  if (rows > d.sNy) rows = d.sNy;
+  const int nPartsTile = (d.sNy + rows - 1) / rows;
+  std::vector<int> partOf((size_t)d.nTiles * ppTile);
+  std::vector<std::vector<int>> own;
+  for (int t = d.t0; t < d.t0 + d.nT; t++)
+    for (int k = 0; k < nPartsTile; k++) {
+      const int j0 = 1 + (k * d.sNy) / nPartsTile, j1 = ((k + 1) * d.sNy) / nPartsTile;
+      std::vector<int> pts;
+      for (int j = j0; j <= j1; j++)
+        for (int i = 1; i <= d.sNx; i++) { pts.push_back(comp(i, j, t)); partOf[comp(i, j, t)] = (int)own.size(); }
+      if ((int)pts.size() > NO) return set_err("build_mwg: part of %zu points > %d", pts.size(), NO);
+      own.push_back(pts);
+    }
+  const int G = (int)own.size();
+  std::vector<std::vector<int>> ring1(G), ring2(G);
+  std::vector<std::vector<char>> inAnyRing(1);   // compact -> exported?
+  std::vector<char> exported((size_t)d.nTiles * ppTile, 0);
+  int r2max = 0;
+  for (int g = 0; g < G; g++) {
+    std::map<int, int> seen;   // compact -> 0 own, 1 ring1, 2 ring2
+    for (int c : own[g]) seen[c] = 0;
+    for (int c : own[g])
+      for (int dir = 0; dir < 4; dir++) {
+        const int nb = nbr(c, dir);
+        if (nb >= 0 && !seen.count(nb)) { seen[nb] = 1; ring1[g].push_back(nb); }
+      }
+    for (int c : ring1[g])
+      for (int dir = 0; dir < 4; dir++) {
+        const int nb = nbr(c, dir);
+        if (nb >= 0 && !seen.count(nb)) { seen[nb] = 2; ring2[g].push_back(nb); }
+      }
+    if ((int)ring1[g].size() > NR) return set_err("build_mwg: ring of %zu points > %d", ring1[g].size(), NR);
+    for (int c : ring1[g]) exported[c] = 1;
+    for (int c : ring2[g]) exported[c] = 1;
+    r2max = std::max(r2max, (int)ring2[g].size());
+  }
+  const int IMAX = NR + ((r2max + 63) / 64) * 64, SZ = NO + IMAX;
+  if (SZ >= 65535) return set_err("build_mwg: %d LDS slots exceed 16-bit indices", SZ);
+  std::vector<int> ownG((size_t)G * NO, -1), ownC((size_t)G * NO, 0), ringG((size_t)G * NR, -1);
+  std::vector<unsigned> ownNb((size_t)G * NO * 2, (unsigned)SZ | ((unsigned)SZ << 16)), ringNb((size_t)G * NR * 2,
+                                                                                                 (unsigned)SZ | ((unsigned)SZ << 16));
+  std::vector<unsigned> ownExp((size_t)G * NT, 0u);
+  std::vector<int> impC((size_t)G * IMAX, 0), impG((size_t)G * IMAX, (int)MG_I2(d, 1, 1, d.t0)), nImp(G);
+  m->mwgPlan.assign((size_t)G * NO, -1);
+  for (int g = 0; g < G; g++) {
+    std::map<int, int> slot;
+    for (size_t n = 0; n < own[g].size(); n++) {
+      const int p = (int)n / NT, tid = (int)n % NT;
+      slot[own[g][n]] = p * NT + tid;
+    }
+    for (size_t n = 0; n < ring1[g].size(); n++) slot[ring1[g][n]] = NO + (int)n;   // n = p*NT + tid
+    for (size_t n = 0; n < ring2[g].size(); n++) slot[ring2[g][n]] = NO + NR + (int)n;
+    auto sl = [&](int c) -> unsigned { if (c < 0) return (unsigned)SZ; auto it = slot.find(c); return it == slot.end() ? (unsigned)SZ : (unsigned)it->second; };
+    for (size_t n = 0; n < own[g].size(); n++) {
+      const int c = own[g][n], q = (int)n;   // slot p*NT + tid == n
+      const size_t o = (size_t)g * NO + q;
+      ownG[o] = g2of(c);
+      ownC[o] = c;
+      ownNb[2 * o] = sl(nbr(c, 0)) | (sl(nbr(c, 1)) << 16);
+      ownNb[2 * o + 1] = sl(nbr(c, 2)) | (sl(nbr(c, 3)) << 16);
+      if (exported[c]) ownExp[(size_t)g * NT + q % NT] |= 1u << (q / NT);
+      m->mwgPlan[o] = ownG[o];
+    }
+    for (size_t n = 0; n < ring1[g].size(); n++) {
+      const int c = ring1[g][n];
+      const size_t o = (size_t)g * NR + n;
+      ringG[o] = g2of(c);
+      ringNb[2 * o] = sl(nbr(c, 0)) | (sl(nbr(c, 1)) << 16);
+      ringNb[2 * o + 1] = sl(nbr(c, 2)) | (sl(nbr(c, 3)) << 16);
+      impC[(size_t)g * IMAX + n] = c;
+      impG[(size_t)g * IMAX + n] = g2of(c);
+    }
+    for (size_t n = 0; n < ring2[g].size(); n++) {
+      impC[(size_t)g * IMAX + NR + n] = ring2[g][n];
+      impG[(size_t)g * IMAX + NR + n] = g2of(ring2[g][n]);
+    }
+    nImp[g] = NR + (int)ring2[g].size();
+  }
+  MwgTables &T = m->mwg;
+  T = MwgTables{};
+  if (mwg_upload(m, ownG, &T.ownG) || mwg_upload(m, ownC, &T.ownC) || mwg_upload(m, ownNb, &T.ownNb) ||
+      mwg_upload(m, ownExp, &T.ownExp) || mwg_upload(m, ringG, &T.ringG) || mwg_upload(m, ringNb, &T.ringNb) ||
+      mwg_upload(m, impC, &T.impC) || mwg_upload(m, impG, &T.impG) || mwg_upload(m, nImp, &T.nImp))
+    return -1;
+  T.G = G; T.IMAX = IMAX; T.SZ = SZ;
+  T.pinned = (G <= 32 && !getenv("MGCM_CG2D_SPREAD")) ? 1 : 0;
+  double *xs = nullptr, *part = nullptr;
+  unsigned *ctr = nullptr;
+  HIPCHK(hipMalloc(&xs, (size_t)d.nTiles * ppTile * sizeof(double)));
+  m->mwgAllocs.push_back(xs);
+  HIPCHK(hipMalloc(&part, (size_t)2 * 3 * G * sizeof(double)));
+  m->mwgAllocs.push_back(part);
+  HIPCHK(hipMalloc(&ctr, 64));
+  m->mwgAllocs.push_back(ctr);
+  T.xs = xs; T.part = part; T.ctr = ctr;
+  m->useMwg = true;
+  return 0;
+}
+
 // ------------------------------------------------------------------ C-ABI
 extern "C" {
 
@@ -574,6 +725,7 @@ void mgcm_destroy(mgcm_model *m) {
   if (m->d_blkx) hipFree(m->d_blkx);
   if (m->d_ctr) hipFree(m->d_ctr);
   if (m->d_rec) hipFree(m->d_rec);
+  for (void *q : m->mwgAllocs) hipFree(q);
   if (m->ownStream) hipStreamDestroy(m->ownStream);
   if (m->stream2) hipStreamDestroy(m->stream2);
   if (m->evFork) hipEventDestroy(m->evFork);
@@ -616,8 +768,9 @@ double mgcm_get_param(mgcm_model *m, const char *name) {
     if (hipMemcpy(&it, m->d_ctr, sizeof(int), hipMemcpyDeviceToHost) != hipSuccess) return NAN;
     return it;
   }
-  // 3: k_cg2d_bxy, 2: k_cg2d_blk2, 1: k_cg2d_block
-  if (!strcmp(name, "cg2dKernel")) return m->nBlkX > 0 ? 3.0 : (m->nBlk > 0 ? 2.0 : 1.0);
+  // 4: k_cg2d_mwg, 3: k_cg2d_bxy, 2: k_cg2d_blk2, 1: k_cg2d_block
+  if (!strcmp(name, "cg2dKernel")) return m->useMwg ? 4.0 : m->nBlkX > 0 ? 3.0 : (m->nBlk > 0 ? 2.0 : 1.0);
+  if (!strcmp(name, "cg2dParts")) return m->useMwg ? (double)m->mwg.G : 1.0;
   for (auto &pd : PARAMS)
     if (!strcmp(pd.name, name)) {
       const char *ptr = reinterpret_cast<const char *>(&m->p) + pd.off;
@@ -736,9 +889,14 @@ int mgcm_init(mgcm_model *m) {
   HIPCHK(hipSetDevice(m->device));
   if (upload_halo(m)) return -1;
   if (build_nbr(m)) return -1;
-  if (m->nPts > cg2d_block_max_points())
-    return set_err("mgcm_init: %d CG2D points per GPU exceed the single-workgroup solver (%d); "
-                   "the multi-workgroup solver is not built yet", m->nPts, cg2d_block_max_points());
+  // CG2D kernel: the single-workgroup blocked solvers on lat-lon grids that tile into their
+  // blocks; otherwise the multi-workgroup solver (MGCM_CG2D_SINGLE=1 keeps the generic
+  // single-workgroup one where it fits)
+  m->useMwg = false;
+  if (m->nBlkX == 0 && m->nBlk == 0 && !(getenv("MGCM_CG2D_SINGLE") && m->nPts <= cg2d_block_max_points())) {
+    if (build_mwg(m)) return -1;
+    if (m->p.cg2dUseMinResSol) return set_err("mgcm_init: cg2dUseMinResSol with the multi-workgroup CG2D not implemented");
+  }
   if ((m->p.viscA4D != 0.0 || m->p.viscA4Z != 0.0) && (m->d.OLx < 3 || m->d.OLy < 3))
     return set_err("mgcm_init: biharmonic viscosity needs OLx, OLy >= 3 (del2u of the halo ring)");
   const bool rstar = m->p.nonlinFreeSurf > 0;
@@ -820,6 +978,10 @@ int mgcm_init(mgcm_model *m) {
 }
 
 static hipError_t launch_cg2d(mgcm_model *m, int maxIters, int nIterMin) {
+  if (m->useMwg) {
+    if (nIterMin >= 0) return hipErrorInvalidValue;   // no min-residual solution in the multi-workgroup solver
+    return launch_cg2d_mwg(m->d, m->p, m->f, m->mwg, maxIters, m->d_rec, m->d_ctr + 1, m->stream);
+  }
   if (m->nBlkX > 0)
     return launch_cg2d_bxy(m->d, m->p, m->f, m->d_nbx, m->d_blkx, m->nBlkX, maxIters, nIterMin, m->d_rec, m->d_ctr + 1,
                            m->stream);
@@ -1186,11 +1348,16 @@ double mgcm_kernel_ms(mgcm_model *m, const char *name, int *launches) {
 // 0.0; the NT thread partials are then combined by the pairwise tree the DPP row sums,
 // row broadcasts and the cross-wave row sum implement (block_sum / block_sum_nw: lanes
 // (2i, 2i+1), then pairs of pairs, ..., in thread order, zero-padded to a power of two).
-int mgcm_cg2d_sum_plan(mgcm_model *m, int *plan, long capacity, int *NT, int *PPT) {
+int mgcm_cg2d_sum_plan(mgcm_model *m, int *plan, long capacity, int *NT, int *PPT, int *NG) {
   if (!m->ready) return set_err("mgcm_cg2d_sum_plan: model not initialised");
-  int nt, ppt;
+  int nt, ppt, ng = 1;
   std::vector<int> tab;
-  if (m->nBlkX > 0) {
+  if (m->useMwg) {
+    int rpt;
+    cg2d_mwg_geometry(&nt, &ppt, &rpt);
+    ng = m->mwg.G;
+    tab = m->mwgPlan;
+  } else if (m->nBlkX > 0) {
     int BX, BY;
     cg2d_bxy_geometry(&BX, &BY, &nt);
     ppt = BX * BY;
@@ -1217,6 +1384,7 @@ int mgcm_cg2d_sum_plan(mgcm_model *m, int *plan, long capacity, int *NT, int *PP
   }
   *NT = nt;
   *PPT = ppt;
+  *NG = ng;
   if ((long)tab.size() > capacity) return set_err("mgcm_cg2d_sum_plan: capacity %ld < %zu", capacity, tab.size());
   memcpy(plan, tab.data(), tab.size() * sizeof(int));
   return 0;

@@ -165,18 +165,19 @@ class Model:
         return x, f.value, mn.value, la.value, it.value, itm.value
 
     def cg2d_sum_plan(self):
-        """(plan, NT, PPT): the device CG2D's summation order (mgcm_cg2d_sum_plan)."""
-        cap = 1 << 22
+        """(plan, NT, PPT, NG): the device CG2D's summation order (mgcm_cg2d_sum_plan)."""
+        cap = 1 << 24
         plan = np.zeros(cap, dtype=np.int32)
-        nt, ppt = ctypes.c_int(), ctypes.c_int()
+        nt, ppt, ng = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
         check(lib().mgcm_cg2d_sum_plan(self.h, plan.ctypes.data_as(ctypes.POINTER(ctypes.c_int)), cap,
-                                       ctypes.byref(nt), ctypes.byref(ppt)), "mgcm_cg2d_sum_plan")
-        return plan[:nt.value * ppt.value].copy(), nt.value, ppt.value
+                                       ctypes.byref(nt), ctypes.byref(ppt), ctypes.byref(ng)), "mgcm_cg2d_sum_plan")
+        return plan[:nt.value * ppt.value * ng.value].copy(), nt.value, ppt.value, ng.value
 
     def cg2d_kernel(self):
-        """Which CG2D kernel mgcm_init selected: 'bxy' (2x4 points/thread), 'blk2' (2x2) or 'block'."""
+        """Which CG2D kernel mgcm_init selected: 'mwg' (multi-workgroup), 'bxy' (2x4 points/thread),
+        'blk2' (2x2) or 'block'."""
         k = lib().mgcm_get_param(self.h, b"cg2dKernel")
-        return {3.0: "bxy", 2.0: "blk2"}.get(k, "block")
+        return {4.0: "mwg", 3.0: "bxy", 2.0: "blk2"}.get(k, "block")
 
     def kernel_timing(self, enable):
         lib().mgcm_kernel_timing(self.h, 1 if enable else 0)

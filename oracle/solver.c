@@ -42,11 +42,17 @@ int oracle_set_sum_plan(OModel *m, const int *plan, int NT, int PPT, int NG) {
   return 0;
 }
 
+static double pairwise_tree(double *v, int n) {   /* n a power of two; destroys v */
+  for (int w = 1; w < n; w *= 2)
+    for (int t = 0; t < n; t += 2 * w) v[t] = v[t] + v[t + w];
+  return v[0];
+}
+
 static double plan_sum(const OModel *m, const double *term) {
   int np2 = 1;
   while (np2 < m->planNT) np2 *= 2;
-  double *th = calloc((size_t)np2, sizeof(double));
-  double total = 0.0;
+  double *th = calloc((size_t)np2, sizeof(double)), lanes[64];
+  for (int l = 0; l < 64; l++) lanes[l] = 0.0;
   for (int g = 0; g < m->planNG; g++) {
     for (int t = 0; t < np2; t++) th[t] = 0.0;
     for (int t = 0; t < m->planNT; t++) {
@@ -57,12 +63,11 @@ static double plan_sum(const OModel *m, const double *term) {
       }
       th[t] = e;
     }
-    for (int w = 1; w < np2; w *= 2)
-      for (int t = 0; t < np2; t += 2 * w) th[t] = th[t] + th[t + w];
-    total = total + th[0];
+    /* workgroup partial g, added into lane g % 64 in workgroup order */
+    lanes[g % 64] = lanes[g % 64] + pairwise_tree(th, np2);
   }
   free(th);
-  return total;
+  return pairwise_tree(lanes, 64);
 }
 
 int oracle_ini_cg2d(OModel *m) {

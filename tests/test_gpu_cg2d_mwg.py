@@ -1,0 +1,74 @@
+"""The multi-workgroup CG2D (kernels_cg2d_mwg.hip) through the C-ABI.
+
+Bars:
+  * BASELINE config 2 (90x40x15, 1 tile) with the single-workgroup solvers switched off
+    (4 row-strip parts): 6 steps bit-identical to the oracle summing CG2D in the device's
+    order (mgcm_cg2d_sum_plan: per-thread terms, pairwise trees, partials in part order);
+  * the same solve with every part pinned to one XCD and with the parts spread over the
+    chip: bit-identical (the sums do not depend on placement);
+  * cg2d_iters identical to the reference-order oracle.
+"""
+import os
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def _ocean90_mwg(spread=False):
+    from mitgcm_amd import configs
+    env = {"MGCM_CG2D_NOBXY": "1", "MGCM_CG2D_NOBLK": "1"}
+    if spread:
+        env["MGCM_CG2D_SPREAD"] = "1"
+    old = {k: os.environ.get(k) for k in env}
+    os.environ.update(env)
+    try:
+        m = configs.make_model(configs.global_ocean_90x40x15)
+    finally:
+        for k, v in old.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+    return m
+
+
+def test_mwg_ocean90_bitexact_vs_device_order_oracle():
+    from mitgcm_amd._lib import lib
+    from oracle.harness import ocean90_oracle
+    m = _ocean90_mwg()
+    assert m.cg2d_kernel() == "mwg"
+    assert lib().mgcm_get_param(m.h, b"cg2dParts") == 4.0
+    plan, NT, PPT, NG = m.cg2d_sum_plan()
+    assert NG == 4
+    od, g = ocean90_oracle()
+    od.set_sum_plan(plan, NT, PPT, NG)
+    o_ref, _ = ocean90_oracle()
+    for step in range(1, 7):
+        m.forward_step(1)
+        od.forward_step()
+        o_ref.forward_step()
+        st = m.solve_stats()
+        assert st["cg2d_iters"] == int(od.get("numIters")) == int(o_ref.get("numIters")), step
+        assert st["cg2d_init_res"] == od.get("firstResidual"), (step, st["cg2d_init_res"], od.get("firstResidual"))
+        assert st["cg2d_last_res"] == od.get("lastResidual"), step
+    inner = (Ellipsis,) + g.sl(1, g.sNx, 1, g.sNy)
+    for n in ("uVel", "vVel", "theta", "salt", "etaN"):
+        dev = m.get(n)
+        ref = np.array(od.arr(n)).reshape(dev.shape)
+        assert np.array_equal(dev[inner], ref[inner]), (n, np.abs(dev - ref)[inner].max())
+    m.close()
+
+
+def test_mwg_pinned_vs_spread_identical():
+    a = _ocean90_mwg(spread=False)
+    b = _ocean90_mwg(spread=True)
+    a.forward_step(3)
+    b.forward_step(3)
+    for n in ("etaN", "uVel", "theta"):
+        assert np.array_equal(a.get(n), b.get(n)), n
+    for k in range(3):
+        assert a.solve_stats(back=k) == b.solve_stats(back=k)
+    a.close()
+    b.close()

@@ -110,9 +110,9 @@ def test_cs32x15_8_steps_vs_oracle():
     the reference summation order (6 tile partials in tile order) >= 10 digits."""
     o, g = _oracle(0)
     m = _model()
-    plan, NT, PPT = m.cg2d_sum_plan()
+    plan, NT, PPT, NG = m.cg2d_sum_plan()
     od_dev, _ = _oracle(0)
-    od_dev.set_sum_plan(plan, NT, PPT)
+    od_dev.set_sum_plan(plan, NT, PPT, NG)
     from mitgcm_amd.model import dynstat
     worst = (99.0, None)
     for step in range(1, 9):

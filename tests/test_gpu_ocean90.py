@@ -114,9 +114,9 @@ def test_ocean90_dynamics_bitexact():
 def test_ocean90_10_steps(golden_dir):
     o, g = _oracle(0)            # reference summation order
     m = _model()
-    plan, NT, PPT = m.cg2d_sum_plan()
+    plan, NT, PPT, NG = m.cg2d_sum_plan()
     od_dev, _ = _oracle(0)       # the device's summation order
-    od_dev.set_sum_plan(plan, NT, PPT)
+    od_dev.set_sum_plan(plan, NT, PPT, NG)
     gold = json.load(open(os.path.join(golden_dir, EXP, "monitor.json")))
     from mitgcm_amd.model import dynstat
     worst_o, worst_r = (99.0, None), (99.0, None)
