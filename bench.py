@@ -36,7 +36,7 @@ def parse():
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--config", default="global_ocean.90x40x15",
-                    choices=["global_ocean.90x40x15", "global_ocean.cs32x15", "global_oce_latlon_90x40x15", "tutorial_global_oce_latlon", "baroclinic_gyre_dst3",
+                    choices=["global_ocean.90x40x15", "global_ocean.cs32x15", "llc90_synthetic", "global_oce_latlon_90x40x15", "tutorial_global_oce_latlon", "baroclinic_gyre_dst3",
                              "tutorial_baroclinic_gyre", "tutorial_barotropic_gyre"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--shard", action="store_true",
@@ -62,6 +62,12 @@ WORKLOADS = {
                             "non-linear free surface (UPDATE_CG2D every step), JMD95Z, GM/Redi advective form "
                             "(GM_AdvForm), implicit vertical diffusion, IVDC, monthly forcing with real fresh-water "
                             "flux; full FORWARD_STEP on device, 1 step = 1 model day",
+    "llc90_synthetic": "BASELINE config 5, the LLC-90-shaped synthetic of SURVEY.md 8(d): the 5 lat-lon-cap "
+                       "facets of data.exch2.llc_120_5f at n=90 (13 tiles of 90x90, OL=4, pkg/exch2 maps), 50 "
+                       "levels, uniform 100 km metrics, f-plane, cos-shaped bathymetry; vector-invariant momentum, "
+                       "linear free surface + exactConserv, LINEAR EOS, C2 tracers, implicit vertical diffusion, "
+                       "IVDC, zonal wind; multi-workgroup CG2D; full FORWARD_STEP on device, dt = 3600 s "
+                       "(1 step = 1/24 model day)",
     "global_oce_latlon_90x40x15": "90x40x15 global lat-lon ocean (BASELINE config 2's grid, bathymetry, "
                                   "monthly forcing and 1-tile layout sNx=90, sNy=40, OL=3) with the physics "
                                   "verification/tutorial_global_oce_latlon pins: JMD95Z, GM/Redi gkw91, CD scheme, "
@@ -80,6 +86,8 @@ WORKLOADS = {
 
 
 DATA = {
+    "llc90_synthetic": "synthetic (SURVEY.md 8(d) C5 recipe): cos-shaped bathymetry, T = tRef + 0.01 N(0,1), "
+                       "S = 35 + 0.001 N(0,1) from numpy default_rng(20261015), zonal wind -0.1 cos(2 pi y/L_y)",
     "global_ocean.cs32x15": "reference input fields of verification/global_ocean.cs32x15 (grid_cs32 facets, "
                             "bathy_Hmin50, lev_T/S_cs_15k, 12-month taux/tauy/Qnet/EmPmR/SST/SSS), cold start",
     "global_ocean.90x40x15": "reference input fields of verification/tutorial_global_oce_latlon (bathymetry, "
@@ -103,6 +111,8 @@ def config_fn(name):
         return configs.global_ocean_90x40x15
     if name == "global_ocean.cs32x15":
         return configs.global_ocean_cs32x15
+    if name == "llc90_synthetic":
+        return configs.llc_synthetic
     if name == "global_oce_latlon_90x40x15":
         return lambda: configs.global_oce_latlon(nSx=1, nSy=1, OL=3)
     if name == "tutorial_global_oce_latlon":

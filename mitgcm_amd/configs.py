@@ -473,3 +473,94 @@ def global_ocean_cs32x15(data_dir=None, sNy=32):
     for nm in ("h0FacC", "h0FacW", "h0FacS", "recip_Rcol", "rLowW", "rLowS", "rSurfW", "rSurfS"):
         state[nm] = g.f[nm]
     return g, params, state, forcing
+
+
+def llc_delr(Nr):
+    """Synthetic vertical grid of the LLC workload: delR growing linearly from 10 m to
+    160 m (Nr = 50: 4 250 m in all)."""
+    return [10.0 + 150.0 * k / max(1, Nr - 1) for k in range(Nr)]
+
+
+def llc_synthetic(n=90, Nr=50, OL=4, tile=None, seed=20261015):
+    """BASELINE config 5, the LLC-90-shaped synthetic of SURVEY.md 8(d): the 5 facets of
+    utils/exch2/input/data.exch2.llc_120_5f with 120 -> n (n x 3n, n x 3n, n x n, 3n x n,
+    3n x n), tiles of `tile` x `tile` (default n: 13 tiles), Nr levels, OL halo rows.
+      grid       uniform curvilinear metrics dx = dy = 1e5 m on every facet (the facet
+                 links carry the rotations), f-plane f0 = 1e-4;
+      bathymetry H = -4000 (0.6 + 0.4 cos(pi r)), r the facet-normalised distance from the
+                 facet centre, land on the open edges (south of facets 1, 2, east of 4, 5);
+      state      T = tRef(k) + 0.01 N(0,1), S = 35 + 0.001 N(0,1) (numpy default_rng(seed)),
+                 u = v = 0, eta = 0;
+      forcing    zonal (facet-x) wind stress -0.1 cos(2 pi y / L_y), facet coordinates;
+      physics    vector-invariant momentum (harmonic viscosity 1e4), linear free surface with
+                 exactConserv, LINEAR EOS, C2 tracers with implicit vertical diffusion and
+                 IVDC, deltaT = 3600 s (1/24 model day per step).
+    Returns (grid, params, state)."""
+    from math import cos, pi, sqrt
+    from .exch2 import llc_topology
+    ts = tile or n
+    topo = llc_topology(n, ts, ts, OL)
+    g = Grid(ts, ts, OL, OL, Nr, nSx=topo.nTiles, nSy=1, topology=topo)
+    g.usingCurvilinearGrid = True
+    g.ini_vertical_grid(llc_delr(Nr))
+    dx = 1.0e5
+    recs, bath_f, wind_f = [], [], []
+    for (fNx, fNy) in topo.facet_dims:
+        r = np.zeros((18, fNy + 1, fNx + 1))
+        jj, ii = np.meshgrid(np.arange(fNy + 1, dtype=np.float64), np.arange(fNx + 1, dtype=np.float64),
+                             indexing="ij")
+        r[0], r[1] = (ii + 0.5) * dx, (jj + 0.5) * dx        # XC, YC (m)
+        r[5], r[6] = ii * dx, jj * dx                        # XG, YG
+        for q in (2, 3, 7, 8, 10, 11, 14, 15):               # DXF DYF DXV DYU DXC DYC DXG DYG
+            r[q] = dx
+        for q in (4, 9, 12, 13):                             # RA RAZ RAW RAS
+            r[q] = dx * dx
+        r[16], r[17] = 1.0, 0.0                              # AngleCS, AngleSN
+        recs.append(r)
+        # bathymetry and wind on the facet's cell centres
+        yc, xc = np.meshgrid(np.arange(fNy) + 0.5, np.arange(fNx) + 0.5, indexing="ij")
+        rr = np.sqrt(((xc - fNx / 2.0) / (fNx / 2.0)) ** 2 + ((yc - fNy / 2.0) / (fNy / 2.0)) ** 2) / sqrt(2.0)
+        bath_f.append(-4000.0 * (0.6 + 0.4 * np.cos(pi * rr)))
+        wind_f.append(-0.1 * np.cos(2.0 * pi * yc / fNy))
+    # land on the disconnected (Antarctic) edges
+    bath_f[0][0, :] = 0.0
+    bath_f[1][0, :] = 0.0
+    bath_f[3][:, -1] = 0.0
+    bath_f[4][:, -1] = 0.0
+    g.ini_curvilinear_grid(recs, radius_fromHorizGrid=6370.0e3, rSphere=6370.0e3, anglesFromFile=True)
+    g.ini_cori(1.0e-4, 0.0, selectCoriMap=0)
+    g.f["fCoriCos"] = g.z2()
+
+    def facet_to_tiles(fld):
+        out = g.z2()
+        inner = g.sl(1, g.sNx, 1, g.sNy)
+        for t in range(g.nTiles):
+            tid = t + 1
+            f = topo.face[tid]
+            out[t][inner] = fld[f - 1][topo.tBy[tid]:topo.tBy[tid] + g.sNy, topo.tBx[tid]:topo.tBx[tid] + g.sNx]
+        return out
+    g.ini_depths_masks(facet_to_tiles(bath_f), hFacMin=0.1, hFacMinDr=20.0, gBaro=9.81)
+    dt = 3600.0
+    g.ini_cg2d(dt, dt, 1e-9)
+    rC = g.f["rC"][:Nr]
+    tRef = 2.0 + 18.0 * np.exp(rC / 1000.0)
+    rng = np.random.default_rng(seed)
+    shape = (g.nTiles, Nr, g.ny, g.nx)
+    theta = tRef[None, :, None, None] + 0.01 * rng.standard_normal(shape)
+    salt = 35.0 + 0.001 * rng.standard_normal(shape)
+    mC = g.f["maskC"]
+    theta = g.exch(np.where(mC > 0.0, theta, 0.0))
+    salt = g.exch(np.where(mC > 0.0, salt, 0.0))
+    fu = facet_to_tiles(wind_f)
+    fu, fv = topo.exchange_uv(fu[:, None], g.z2()[:, None], True)
+    params = dict(deltaTMom=dt, deltaTFreeSurf=dt, deltaTClock=dt, deltaTtracer=dt, abEps=0.1, rhoConst=1035.0,
+                  rhoNil=1035.0, gravity=9.81, gBaro=9.81, viscAhD=1.0e4, viscAhZ=1.0e4, viscA4D=0.0, viscA4Z=0.0,
+                  viscAr=1.0e-4, sideDragFactor=2.0, selectCoriScheme=0, vectorInvariantMomentum=1,
+                  selectVortScheme=1, selectKEscheme=0, momForcingOutAB=0, momDissip_In_AB=1, cg2dMaxIters=1000,
+                  cg2dUseMinResSol=0, nIter0=0, no_slip_sides=1, no_slip_bottom=1, exactConserv=1,
+                  tempStepping=1, tempAdvection=1, tempForcing=1, tempAdvScheme=2, tempVertAdvScheme=2,
+                  saltStepping=1, saltAdvection=1, saltForcing=1, saltAdvScheme=2, saltVertAdvScheme=2,
+                  diffKhT=0.0, diffKrT=1.0e-5, diffKhS=0.0, diffKrS=1.0e-5, ivdc_kappa=10.0, implicitDiffusion=1,
+                  usingCurvilinearGrid=1, rSphere=6370.0e3, integr_GeoPot=2, eosType=0, tAlpha=2.0e-4, sBeta=7.4e-4)
+    state = {"theta": theta, "salt": salt, "tRef": tRef, "sRef": np.full(Nr, 35.0), "fu": fu[:, 0], "fv": fv[:, 0]}
+    return g, params, state

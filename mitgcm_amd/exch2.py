@@ -665,3 +665,22 @@ class Exch2Topology:
 def cube_topology(nCube, sNx, sNy, OL):
     """6-face cube of nCube x nCube facets (preDefTopol=3 / default cube)."""
     return Exch2Topology([(nCube, nCube)] * 6, cs6_facet_links(), sNx, sNy, OL, OL)
+
+
+def llc5_facet_links():
+    """The 5-facet lat-lon-cap connectivity of utils/exch2/input/data.exch2.llc_120_5f
+    (preDefTopol = 0, facetEdgeLink(1:4, j) = N, S, E, W of facet j as face.edge, 0 = open):
+    facets 1, 2 (n x 3n), the Arctic cap 3 (n x n), facets 4, 5 (3n x n); the southern
+    edges of 1, 2 and the eastern edges of 4, 5 are disconnected (Antarctica)."""
+    N, S, E, W = EDGE_N, EDGE_S, EDGE_E, EDGE_W
+    return {1: [(3, W), (0, 0), (2, W), (5, N)],
+            2: [(3, S), (0, 0), (4, S), (1, E)],
+            3: [(5, W), (2, N), (4, W), (1, N)],
+            4: [(5, S), (2, E), (0, 0), (3, E)],
+            5: [(1, W), (4, N), (0, 0), (3, N)]}
+
+
+def llc_topology(n, sNx, sNy, OL):
+    """LLC facets of size n (LLC-n: 13 tiles of n x n when sNx = sNy = n)."""
+    dims = [(n, 3 * n), (n, 3 * n), (n, n), (3 * n, n), (3 * n, n)]
+    return Exch2Topology(dims, llc5_facet_links(), sNx, sNy, OL, OL)
