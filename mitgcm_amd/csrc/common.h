@@ -17,7 +17,34 @@ struct Dims {
   int t0, nT;   // tiles this process steps (tile-sharded runs); 0, nTiles otherwise
   int nx, ny;
   long n2, n3;
+  long N2all, N3all;   // n2 * nTiles, n3 * nTiles: the stride of one field in its arena
 };
+
+// Every 2-D and 3-D field of the model in one list each (X-macros): the order of the
+// per-kind arenas model.hip allocates (field n of a kind lives at arena + n * N2all / N3all),
+// so a kernel can address any field from ONE base pointer (AR2 / AR3 below) instead of
+// holding a pointer per field in scalar registers.  theta / salt and their ping-pong
+// partners swap pointers every step: address them through Fields, never by arena index.
+#define MG_F2D_LIST(X) X(dxF) X(dyF) X(dxG) X(dyG) X(dxC) X(dyC) X(dxV) X(dyU) X(rA) X(rAw) X(rAs) X(recip_dxF) \
+    X(recip_dyF) X(recip_dxC) X(recip_dyC) X(recip_dxV) X(recip_dyU) X(recip_rA) X(recip_rAw) X(recip_rAs) \
+    X(fCori) X(Bo_surf) X(recip_Bo) X(tanPhiAtU) X(tanPhiAtV) X(maskInC) X(SST) X(lambdaThetaClimRelax) X(aW2d) \
+    X(aS2d) X(aC2d) X(pW) X(pS) X(pC) X(etaN) X(fu) X(fv) X(etaH) X(surfaceForcingT) X(surfaceForcingS) \
+    X(cg2d_b) X(cg2d_x) X(Qnet) X(EmPmR) X(SSS) X(lambdaSaltClimRelax) X(etaNm1) X(fCoriCos) X(recip_Rcol) \
+    X(rSurfW) X(rSurfS) X(rLowW) X(rLowS) X(Ro_surf) X(R_low) X(rStarFacC) X(rStarFacW) X(rStarFacS) \
+    X(rStarExpC) X(rStarExpW) X(rStarExpS) X(rStarDhCDt) X(rStarDhWDt) X(rStarDhSDt) X(PmEpR) X(dEtaHdt) \
+    X(maskInW) X(maskInS) X(fCoriG) X(recip_rAz) X(recip_dxG) X(recip_dyG)
+#define MG_F3D_LIST(X) X(hFacC) X(hFacW) X(hFacS) X(recip_hFacC) X(recip_hFacW) X(recip_hFacS) X(maskC) X(maskW) \
+    X(maskS) X(uVel) X(vVel) X(wVel) X(theta) X(salt) X(gU) X(gV) X(guNm1) X(gvNm1) X(rhoInSitu) X(IVDConvCount) \
+    X(gtNm1) X(thetaNext) X(gTscr) X(cpScr) X(phiHydC) X(saltNext) X(gsNm1) X(advScr1) X(advScr2) X(gAdv) \
+    X(sigmaR) X(Kwx) X(Kwy) X(Kwz) X(Kux) X(Kvy) X(uVelD) X(vVelD) X(uNM1) X(vNM1) X(cdU) X(cdV) X(h0FacC) \
+    X(h0FacW) X(h0FacS) X(totPhiHyd) X(alphaRho) X(del2u) X(del2v) X(dWtC) X(dWtU) X(dWtV) X(Kuz) X(Kvz) \
+    X(GM_PsiX) X(GM_PsiY)
+#define MG_ENUM2(n) F2_##n,
+#define MG_ENUM3(n) F3_##n,
+enum F2Id { MG_F2D_LIST(MG_ENUM2) F2_COUNT };
+enum F3Id { MG_F3D_LIST(MG_ENUM3) F3_COUNT };
+#undef MG_ENUM2
+#undef MG_ENUM3
 
 // Run-time parameters needed on device (PARAMS.h names).
 struct Params {
@@ -98,7 +125,12 @@ struct Fields {
   const int *tileFace, *tileEdge;   // per tile: exch2_myFace, edge bits N=1 S=2 E=4 W=8
   // solver work
   double *cg2d_b, *cg2d_x;
+  // the 2-D and 3-D arenas (MG_F2D_LIST / MG_F3D_LIST order)
+  double *a2, *a3;
 };
+// field x at flat offset q of its kind's arena (one base pointer for every field)
+#define AR2(x, q) f.a2[(long)F2_##x * d.N2all + (q)]
+#define AR3(x, q) f.a3[(long)F3_##x * d.N3all + (q)]
 
 #define MG_I2(d, i, j, t) \
   ((long)((i) + (d).OLx - 1) + (long)((j) + (d).OLy - 1) * (d).nx + (long)(t) * (d).n2)

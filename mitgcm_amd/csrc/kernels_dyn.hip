@@ -12,6 +12,8 @@
 // neighbours' state with the same expression and operand order, so each point is
 // bit-identical to the loop-nest form (compiled with -ffp-contract=off).  The
 // kernel is HBM/latency bound (about 1 flop/B): no MFMA.
+#include <cstdlib>
+
 #include "common.h"
 
 namespace mgcm {
@@ -190,26 +192,37 @@ __global__ void __launch_bounds__(256) k_phi_hyd(Dims d, Params p, Fields f) {
 }
 
 
-// MOM_VECINV (pkg/mom_vecinv/mom_vecinv.F:42-1064) for one output point (i,j,k) of the
-// DYNAMICS range 0..sN+1: every intermediate the reference keeps in 2-D scratch (KE,
-// vort3, hFacZ, hDiv, the vertical viscous flux ping-pong) is re-derived at the
-// neighbours it needs with the reference's expression and operand order, including
-// MOM_CALC_RELVORT3's cube-corner circulations.  Subset (mgcm_init checks it): no
-// useAbsVorticity / high-order / upwind vorticity, constant harmonic viscosity, explicit
-// vertical viscosity, no biharmonic, no 3-D Coriolis / NH metric.  deepFac = rhoFac = 1.
-__device__ void vecinv_tend(const Dims &d, const Params &p, const Fields &f, int i, int j, int k, int t, double &gU,
-                            double &gV, double &guDiss, double &gvDiss) {
-  const int Nr = d.Nr, OLx = d.OLx, OLy = d.OLy, sNx = d.sNx, sNy = d.sNy;
-#define U(ii, jj) f.uVel[MG_I3(d, ii, jj, k, t)]
-#define V(ii, jj) f.vVel[MG_I3(d, ii, jj, k, t)]
-#define U3(ii, jj, kk) f.uVel[MG_I3(d, ii, jj, kk, t)]
-#define V3(ii, jj, kk) f.vVel[MG_I3(d, ii, jj, kk, t)]
-#define W3(ii, jj, kk) f.wVel[MG_I3(d, ii, jj, kk, t)]
-#define G2(a, ii, jj) f.a[MG_I2(d, ii, jj, t)]
-#define G3(a, ii, jj, kk) f.a[MG_I3(d, ii, jj, kk, t)]
-  const double recip_drF = f.recip_drF[k - 1], drF = f.drF[k - 1];
-  // MOM_CALC_KE (mom_calc_ke.F:66-150), computed on 1-OL..sN+OL-1
-  auto KE = [&](int ii, int jj) -> double {
+// ---- MOM_VECINV's per-level intermediates as functions of an accessor A of the level's
+// 3-D fields (uVel, vVel, hFacW, hFacS, recip_hFacC at (ii, jj, k)): VIGlobal reads them
+// from HBM, VITile from the LDS-staged tile of k_mom_vi_tiled; the expression trees are
+// shared, so both kernels produce the same bits.
+// hFacZ (pkg/mom_common/mom_calc_hfacz.F:158-225, hZoption = 0)
+template <class A>
+__device__ __forceinline__ double vi_hfacz(const A &a, const Dims &d, int ii, int jj, int k) {
+  if (ii < 2 - d.OLx || jj < 2 - d.OLy) return 0.0;
+  double h = fmin(a.hFacW(ii, jj, k), a.hFacW(ii, jj - 1, k));
+  h = fmin(a.hFacS(ii, jj, k), h);
+  h = fmin(a.hFacS(ii - 1, jj, k), h);
+  return h;
+}
+// h0FacZ (mom_fluxform.F:290-307 / mom_vecinv.F): rest-state h0FacW/S under the non-linear
+// free surface with no-slip walls, else hFacZ
+template <class A>
+__device__ __forceinline__ double vi_h0facz(const A &a, const Dims &d, const Params &p, int ii, int jj, int k) {
+  if (!(p.momViscosity && p.no_slip_sides && p.nonlinFreeSurf > 0)) return vi_hfacz(a, d, ii, jj, k);
+  if (ii < 2 - d.OLx || jj < 2 - d.OLy) return 0.0;
+  return fmin(fmin(a.h0FacW(ii, jj, k), a.h0FacW(ii, jj - 1, k)), fmin(a.h0FacS(ii, jj, k), a.h0FacS(ii - 1, jj, k)));
+}
+// MOM_CALC_KE (mom_calc_ke.F:66-150), computed on 1-OL..sN+OL-1
+template <class A>
+__device__ __forceinline__ double vi_KE(const A &a, const Dims &d, const Params &p, const Fields &f, int ii, int jj, int k, int t) {
+  const int OLx = d.OLx, OLy = d.OLy, sNx = d.sNx, sNy = d.sNy;
+  (void)OLx; (void)OLy; (void)sNx; (void)sNy;
+#define U(ii, jj) a.uVel(ii, jj, k)
+#define V(ii, jj) a.vVel(ii, jj, k)
+#define G2(x, ii, jj) AR2(x, MG_I2(d, ii, jj, t))
+#define G3(x, ii, jj, kk) a.x(ii, jj, kk)
+
     if (ii < 1 - OLx || ii > sNx + OLx - 1 || jj < 1 - OLy || jj > sNy + OLy - 1) return 0.0;
     const double u0 = U(ii, jj), u1 = U(ii + 1, jj), v0 = V(ii, jj), v1 = V(ii, jj + 1);
     switch (p.selectKEscheme) {
@@ -228,12 +241,24 @@ __device__ void vecinv_tend(const Dims &d, const Params &p, const Fields &f, int
                         v1 * v1 * G3(hFacS, ii, jj + 1, k) * G2(rAs, ii, jj + 1))) *
                G3(recip_hFacC, ii, jj, k) * G2(recip_rA, ii, jj);
     }
-  };
+  #undef U
+#undef V
+#undef G2
+#undef G3
+}
   // MOM_CALC_RELVORT3 (mom_calc_relvort3.F:72-233) on 2-OL..sN+OL, then 0 where hFacZ = 0
   // (mom_vecinv.F:395-403); 0 outside the computed range
-  auto vort = [&](int ii, int jj) -> double {
+  template <class A>
+__device__ __forceinline__ double vi_vort(const A &a, const Dims &d, const Params &p, const Fields &f, int ii, int jj, int k, int t) {
+  const int OLx = d.OLx, OLy = d.OLy, sNx = d.sNx, sNy = d.sNy;
+  (void)OLx; (void)OLy; (void)sNx; (void)sNy;
+#define U(ii, jj) a.uVel(ii, jj, k)
+#define V(ii, jj) a.vVel(ii, jj, k)
+#define G2(x, ii, jj) AR2(x, MG_I2(d, ii, jj, t))
+#define G3(x, ii, jj, kk) a.x(ii, jj, kk)
+
     if (ii < 2 - OLx || jj < 2 - OLy || ii > sNx + OLx || jj > sNy + OLy) return 0.0;
-    if (hfacz(d, f, ii, jj, k, t) == 0.0) return 0.0;
+    if (vi_hfacz(a, d, ii, jj, k) == 0.0) return 0.0;
 #define UC(a, b) (U(a, b) * G2(dxC, a, b))
 #define VC(a, b) (V(a, b) * G2(dyC, a, b))
     const double rz = G2(recip_rAz, ii, jj);
@@ -259,27 +284,77 @@ __device__ void vecinv_tend(const Dims &d, const Params &p, const Fields &f, int
     return rz * ((VC(ii, jj) - VC(ii - 1, jj)) - (UC(ii, jj) - UC(ii, jj - 1)));
 #undef UC
 #undef VC
-  };
-  auto rhz = [&](int ii, int jj) -> double {   // r_hFacZ
-    const double h = hfacz(d, f, ii, jj, k, t);
-    return h == 0.0 ? 0.0 : 1.0 / h;
-  };
+  #undef U
+#undef V
+#undef G2
+#undef G3
+}
   // MOM_CALC_HDIV(hDivScheme = 2) (mom_calc_hdiv.F:76-89) on 1-OL..sN+OL-1
-  auto hDiv = [&](int ii, int jj) -> double {
+  template <class A>
+__device__ __forceinline__ double vi_hdiv(const A &a, const Dims &d, const Params &p, const Fields &f, int ii, int jj, int k, int t) {
+  const int OLx = d.OLx, OLy = d.OLy, sNx = d.sNx, sNy = d.sNy;
+  (void)OLx; (void)OLy; (void)sNx; (void)sNy;
+#define U(ii, jj) a.uVel(ii, jj, k)
+#define V(ii, jj) a.vVel(ii, jj, k)
+#define G2(x, ii, jj) AR2(x, MG_I2(d, ii, jj, t))
+#define G3(x, ii, jj, kk) a.x(ii, jj, kk)
+
     if (ii < 1 - OLx || ii > sNx + OLx - 1 || jj < 1 - OLy || jj > sNy + OLy - 1) return 0.0;
     return ((U(ii + 1, jj) * G2(dyG, ii + 1, jj) * G3(hFacW, ii + 1, jj, k) - U(ii, jj) * G2(dyG, ii, jj) * G3(hFacW, ii, jj, k)) +
             (V(ii, jj + 1) * G2(dxG, ii, jj + 1) * G3(hFacS, ii, jj + 1, k) - V(ii, jj) * G2(dxG, ii, jj) * G3(hFacS, ii, jj, k))) *
            G2(recip_rA, ii, jj) * G3(recip_hFacC, ii, jj, k);
+  #undef U
+#undef V
+#undef G2
+#undef G3
+}
+
+// Accessor of HBM (the per-point k_mom_step<true>): every value read where it lies.
+struct VIGlobal {
+  const Dims &d; const Params &p; const Fields &f; int k, t;
+#define VIG(x) __device__ __forceinline__ double x(int ii, int jj, int kk) const { return AR3(x, MG_I3(d, ii, jj, kk, t)); }
+  VIG(uVel) VIG(vVel) VIG(wVel) VIG(hFacW) VIG(hFacS) VIG(recip_hFacC) VIG(recip_hFacW) VIG(recip_hFacS) VIG(maskW)
+  VIG(maskS) VIG(maskC) VIG(h0FacW) VIG(h0FacS)
+#undef VIG
+  __device__ __forceinline__ double hfz(int ii, int jj) const { return vi_hfacz(*this, d, ii, jj, k); }
+  __device__ __forceinline__ double h0fz(int ii, int jj) const { return vi_h0facz(*this, d, p, ii, jj, k); }
+  __device__ __forceinline__ double KE(int ii, int jj) const { return vi_KE(*this, d, p, f, ii, jj, k, t); }
+  __device__ __forceinline__ double vort(int ii, int jj) const { return vi_vort(*this, d, p, f, ii, jj, k, t); }
+  __device__ __forceinline__ double hDiv(int ii, int jj) const { return vi_hdiv(*this, d, p, f, ii, jj, k, t); }
+};
+
+// MOM_VECINV (pkg/mom_vecinv/mom_vecinv.F:42-1064) for one output point (i,j,k) of the
+// DYNAMICS range 0..sN+1: every intermediate the reference keeps in 2-D scratch (KE,
+// vort3, hFacZ, hDiv, the vertical viscous flux ping-pong) is re-derived at the
+// neighbours it needs with the reference's expression and operand order, including
+// MOM_CALC_RELVORT3's cube-corner circulations.  Subset (mgcm_init checks it): no
+// useAbsVorticity / high-order / upwind vorticity, constant harmonic viscosity, explicit
+// vertical viscosity, no biharmonic, no 3-D Coriolis / NH metric.  deepFac = rhoFac = 1.
+template <class A>
+__device__ __forceinline__ void vecinv_tend(const A &a, const Dims &d, const Params &p, const Fields &f, int i, int j, int k, int t, double &gU,
+                            double &gV, double &guDiss, double &gvDiss) {
+  const int Nr = d.Nr, OLx = d.OLx, OLy = d.OLy, sNx = d.sNx, sNy = d.sNy;
+#define U(ii, jj) a.uVel(ii, jj, k)
+#define V(ii, jj) a.vVel(ii, jj, k)
+#define U3(ii, jj, kk) a.uVel(ii, jj, kk)
+#define V3(ii, jj, kk) a.vVel(ii, jj, kk)
+#define W3(ii, jj, kk) a.wVel(ii, jj, kk)
+#define G2(x, ii, jj) AR2(x, MG_I2(d, ii, jj, t))
+#define G3(x, ii, jj, kk) a.x(ii, jj, kk)
+  const double recip_drF = f.recip_drF[k - 1], drF = f.drF[k - 1];
+  auto rhz = [&](int ii, int jj) -> double {   // r_hFacZ
+    const double h = a.hfz(ii, jj);
+    return h == 0.0 ? 0.0 : 1.0 / h;
   };
   const double rhFacW = G3(recip_hFacW, i, j, k), rhFacS = G3(recip_hFacS, i, j, k);
-  const double hZ = hfacz(d, f, i, j, k, t), hZn = hfacz(d, f, i, j + 1, k, t), hZe = hfacz(d, f, i + 1, j, k, t);
-  const double vz = vort(i, j), vzn = vort(i, j + 1), vze = vort(i + 1, j);
+  const double hZ = a.hfz(i, j), hZn = a.hfz(i, j + 1), hZe = a.hfz(i + 1, j);
+  const double vz = a.vort(i, j), vzn = a.vort(i, j + 1), vze = a.vort(i + 1, j);
   guDiss = 0.0; gvDiss = 0.0;
   if (p.momViscosity) {
     // MOM_VI_HDISSIP (mom_vi_hdissip.F:105-131) on 2-OL..sN+OL-1, constant viscosity, cosFac = 1
     if (i >= 2 - OLx && i <= sNx + OLx - 1 && j >= 2 - OLy && j <= sNy + OLy - 1 &&
         (p.viscAhD != 0.0 || p.viscAhZ != 0.0)) {
-      const double Dij = hDiv(i, j), Dim = hDiv(i, j - 1), Dmj = hDiv(i - 1, j);
+      const double Dij = a.hDiv(i, j), Dim = a.hDiv(i, j - 1), Dmj = a.hDiv(i - 1, j);
       const double Zip = hZn * vzn, Zij = hZ * vz, Zpj = hZe * vze;
       const double uD2 = p.viscAhD * 1.0 * (Dij - Dmj) * G2(recip_dxC, i, j) -
                          p.viscAhZ * rhFacW * (Zip - Zij) * G2(recip_dyG, i, j);
@@ -301,8 +376,8 @@ __device__ void vecinv_tend(const Dims &d, const Params &p, const Fields &f, int
     };
     guDiss = guDiss - rhFacW * recip_drF * G2(recip_rAw, i, j) * (rvU(k + 1) - rvU(k)) * p.rkSign;
     if (p.no_slip_sides) {
-      const double hS = G3(h0FacW, i, j, k) - h0facz(d, p, f, i, j, k, t);
-      const double hN = G3(h0FacW, i, j, k) - h0facz(d, p, f, i, j + 1, k, t);
+      const double hS = G3(h0FacW, i, j, k) - a.h0fz(i, j);
+      const double hN = G3(h0FacW, i, j, k) - a.h0fz(i, j + 1);
       const double u0 = U(i, j);
       guDiss = guDiss + -rhFacW * recip_drF * G2(recip_rAw, i, j) *
                             (hS * G2(dxV, i, j) * G2(recip_dyU, i, j) * (p.viscAhZ * u0 - p.viscA4Z * 0.0) +
@@ -319,8 +394,8 @@ __device__ void vecinv_tend(const Dims &d, const Params &p, const Fields &f, int
     }
     gvDiss = gvDiss - rhFacS * recip_drF * G2(recip_rAs, i, j) * (rvV(k + 1) - rvV(k)) * p.rkSign;
     if (p.no_slip_sides) {
-      const double hW = G3(h0FacS, i, j, k) - h0facz(d, p, f, i, j, k, t);
-      const double hE = G3(h0FacS, i, j, k) - h0facz(d, p, f, i + 1, j, k, t);
+      const double hW = G3(h0FacS, i, j, k) - a.h0fz(i, j);
+      const double hE = G3(h0FacS, i, j, k) - a.h0fz(i + 1, j);
       const double v0 = V(i, j);
       gvDiss = gvDiss + -rhFacS * recip_drF * G2(recip_rAs, i, j) *
                             (hW * G2(dyU, i, j) * G2(recip_dxV, i, j) * (p.viscAhZ * v0 - p.viscA4Z * 0.0) +
@@ -395,8 +470,8 @@ __device__ void vecinv_tend(const Dims &d, const Params &p, const Fields &f, int
     } else {
       c = 0.0;
       if (i <= sNx + OLx - 1) {
-        const double rzw = rhz(i - 1, j) * vort(i - 1, j), rzwn = rhz(i - 1, j + 1) * vort(i - 1, j + 1);
-        const double rze = rhz(i + 1, j) * vze, rzen = rhz(i + 1, j + 1) * vort(i + 1, j + 1);
+        const double rzw = rhz(i - 1, j) * a.vort(i - 1, j), rzwn = rhz(i - 1, j + 1) * a.vort(i - 1, j + 1);
+        const double rze = rhz(i + 1, j) * vze, rzen = rhz(i + 1, j + 1) * a.vort(i + 1, j + 1);
         const double r0 = rhz(i, j) * vz, rn = rhz(i, j + 1) * vzn;
         const double mj = (r0 + (rn + rzw)) * oneThird * VXH(i - 1, j);
         const double ij = (r0 + (rn + rze)) * oneThird * VXH(i, j);
@@ -420,8 +495,8 @@ __device__ void vecinv_tend(const Dims &d, const Params &p, const Fields &f, int
       c = 0.0;
       if (j <= sNy + OLy - 1) {
         const double r0 = rhz(i, j) * vz, re = rhz(i + 1, j) * vze;
-        const double rs = rhz(i, j - 1) * vort(i, j - 1), rn = rhz(i, j + 1) * vzn;
-        const double res = rhz(i + 1, j - 1) * vort(i + 1, j - 1), ren = rhz(i + 1, j + 1) * vort(i + 1, j + 1);
+        const double rs = rhz(i, j - 1) * a.vort(i, j - 1), rn = rhz(i, j + 1) * vzn;
+        const double res = rhz(i + 1, j - 1) * a.vort(i + 1, j - 1), ren = rhz(i + 1, j + 1) * a.vort(i + 1, j + 1);
         const double im = (r0 + (re + rs)) * oneThird * UYH(i, j - 1);
         const double ij = (r0 + (re + rn)) * oneThird * UYH(i, j);
         const double pm = (re + (r0 + res)) * oneThird * UYH(i + 1, j - 1);
@@ -462,9 +537,9 @@ __device__ void vecinv_tend(const Dims &d, const Params &p, const Fields &f, int
       else gV = gV + -0.5 * (wp * zp + wm * zm) * rhFacS * recip_drF;
     }
     // MOM_VI_U/V_GRAD_KE (mom_vi_u_grad_ke.F:49-55)
-    const double ke = KE(i, j);
-    gU = gU + -G2(recip_dxC, i, j) * (ke - KE(i - 1, j)) * G3(maskW, i, j, k);
-    gV = gV + -G2(recip_dyC, i, j) * (ke - KE(i, j - 1)) * G3(maskS, i, j, k);
+    const double ke = a.KE(i, j);
+    gU = gU + -G2(recip_dxC, i, j) * (ke - a.KE(i - 1, j)) * G3(maskW, i, j, k);
+    gV = gV + -G2(recip_dyC, i, j) * (ke - a.KE(i, j - 1)) * G3(maskS, i, j, k);
   }
 #undef VX
 #undef VXH
@@ -500,9 +575,9 @@ __global__ void __launch_bounds__(256) k_mom_step(Dims d, Params p, Fields f, co
   const long q2 = MG_I2(d, i, j, t);
   const bool rstar = p.nonlinFreeSurf > 0 && p.select_rStar > 0;
 
-#define U(ii, jj, kk) f.uVel[MG_I3(d, ii, jj, kk, t)]
-#define V(ii, jj, kk) f.vVel[MG_I3(d, ii, jj, kk, t)]
-#define W(ii, jj, kk) f.wVel[MG_I3(d, ii, jj, kk, t)]
+#define U(ii, jj, kk) AR3(uVel, MG_I3(d, ii, jj, kk, t))
+#define V(ii, jj, kk) AR3(vVel, MG_I3(d, ii, jj, kk, t))
+#define W(ii, jj, kk) AR3(wVel, MG_I3(d, ii, jj, kk, t))
 #define G2(a, ii, jj) f.a[MG_I2(d, ii, jj, t)]
 #define G3(a, ii, jj, kk) f.a[MG_I3(d, ii, jj, kk, t)]
 
@@ -568,7 +643,7 @@ __global__ void __launch_bounds__(256) k_mom_step(Dims d, Params p, Fields f, co
       const double rhFacW = G3(recip_hFacW, i, j, k), rhFacS = G3(recip_hFacS, i, j, k);
       const double hZ = hfacz(d, f, i, j, k, t);
       if constexpr (VI) {
-        vecinv_tend(d, p, f, i, j, k, t, gU, gV, guDiss, gvDiss);
+        vecinv_tend(VIGlobal{d, p, f, k, t}, d, p, f, i, j, k, t, gU, gV, guDiss, gvDiss);
       } else {
       // ---------------- advection (mom_u_adv_uu/vu/wu.F, mom_v_adv_uv/vv/wv.F)
       if (p.momAdvection) {
@@ -749,9 +824,9 @@ __global__ void __launch_bounds__(256) k_mom_step(Dims d, Params p, Fields f, co
     if (p.momForcing && k == 1) {
       // APPLY_FORCING_U/V (apply_forcing.F:81-88) on j=0..sNy+1,i=1..sNx+1 (U) / i=0..sNx+1,j=1..sNy+1 (V)
       if (j >= 0 && j <= d.sNy + 1 && i >= 1 && i <= d.sNx + 1)
-        guExt = guExt + p.foFacMom * (f.fu[q2] * mass2rUnit) * recip_drF * G3(recip_hFacW, i, j, k);
+        guExt = guExt + p.foFacMom * (AR2(fu, q2) * mass2rUnit) * recip_drF * G3(recip_hFacW, i, j, k);
       if (j >= 1 && j <= d.sNy + 1 && i >= 0 && i <= d.sNx + 1)
-        gvExt = gvExt + p.foFacMom * (f.fv[q2] * mass2rUnit) * recip_drF * G3(recip_hFacS, i, j, k);
+        gvExt = gvExt + p.foFacMom * (AR2(fv, q2) * mass2rUnit) * recip_drF * G3(recip_hFacS, i, j, k);
     }
     if (inner) {
       // timestep.F:116-126 synchronous time step: gU -= phFac*dPhiHydX
@@ -763,12 +838,12 @@ __global__ void __launch_bounds__(256) k_mom_step(Dims d, Params p, Fields f, co
     // ADAMS_BASHFORTH2 over the whole halo-inclusive slab (adams_bashforth2.F:81-88)
     const long q3 = MG_I3(d, i, j, k, t);
     {
-      const double gUo = f.guNm1[q3], gVo = f.gvNm1[q3];
+      const double gUo = AR3(guNm1, q3), gVo = AR3(gvNm1, q3);
       double a = abFac * (gU - gUo);
-      f.guNm1[q3] = gU;
+      AR3(guNm1, q3) = gU;
       gU = gU + a;
       a = abFac * (gV - gVo);
-      f.gvNm1[q3] = gV;
+      AR3(gvNm1, q3) = gV;
       gV = gV + a;
     }
     double gUtmp = 0.0, gVtmp = 0.0;   // timestep.F local arrays: 0 outside iMin..iMax, jMin..jMax
@@ -786,9 +861,9 @@ __global__ void __launch_bounds__(256) k_mom_step(Dims d, Params p, Fields f, co
         gV = V(i, j, k) + p.deltaTMom * (gVtmp + 0.0) * G3(maskS, i, j, k);
       }
     }
-    if (p.useCDscheme) { f.cdU[q3] = gUtmp; f.cdV[q3] = gVtmp; }   // k_cd_scheme finishes u*
-    f.gU[q3] = gU;
-    f.gV[q3] = gV;
+    if (p.useCDscheme) { AR3(cdU, q3) = gUtmp; AR3(cdV, q3) = gVtmp; }   // k_cd_scheme finishes u*
+    AR3(gU, q3) = gU;
+    AR3(gV, q3) = gV;
   }
 #undef U
 #undef V
@@ -822,36 +897,374 @@ __global__ void __launch_bounds__(256) k_cd_scheme(Dims d, Params p, Fields f, c
   // vVelD at this U point
   double vf = ((afV(i, j) + afV(i - 1, j + 1)) + (afV(i - 1, j) + afV(i, j + 1))) * 0.25 * G3(maskW, i, j, k) -
               (G2(fCori, i, j) + G2(fCori, i - 1, j)) * 0.5 * (ab15 * G3(uVel, i, j, k) + ab05 * G3(uNM1, i, j, k));
-  double vD = f.vVelD[q3] + p.deltaTMom * vf;
+  double vD = AR3(vVelD, q3) + p.deltaTMom * vf;
   vD = (p.rCD * vD +
         (1.0 - p.rCD) *
             (ab15 * ((G3(vVel, i, j, k) + G3(vVel, i - 1, j + 1, k)) + (G3(vVel, i - 1, j, k) + G3(vVel, i, j + 1, k))) * 0.25 +
              ab05 * ((G3(vNM1, i, j, k) + G3(vNM1, i - 1, j + 1, k)) + (G3(vNM1, i - 1, j, k) + G3(vNM1, i, j + 1, k))) * 0.25)) *
        G3(maskW, i, j, k);
-  f.vVelD[q3] = vD;
+  AR3(vVelD, q3) = vD;
   const double guCor = (G2(fCori, i, j) + G2(fCori, i - 1, j)) * 0.5 * vD * p.cfFacMom;
   // uVelD at this V point
   vf = ((afU(i, j) + afU(i + 1, j - 1)) + (afU(i + 1, j) + afU(i, j - 1))) * 0.25 * G3(maskS, i, j, k) +
        (G2(fCori, i, j) + G2(fCori, i, j - 1)) * 0.5 * (ab15 * G3(vVel, i, j, k) + ab05 * G3(vNM1, i, j, k));
-  double uD = f.uVelD[q3] + p.deltaTMom * vf;
+  double uD = AR3(uVelD, q3) + p.deltaTMom * vf;
   uD = (p.rCD * uD +
         (1.0 - p.rCD) *
             (ab15 * ((G3(uVel, i, j, k) + G3(uVel, i + 1, j - 1, k)) + (G3(uVel, i, j - 1, k) + G3(uVel, i + 1, j, k))) * 0.25 +
              ab05 * ((G3(uNM1, i, j, k) + G3(uNM1, i + 1, j - 1, k)) + (G3(uNM1, i, j - 1, k) + G3(uNM1, i + 1, j, k))) * 0.25)) *
        G3(maskS, i, j, k);
-  f.uVelD[q3] = uD;
+  AR3(uVelD, q3) = uD;
   const double gvCor = -(G2(fCori, i, j) + G2(fCori, i, j - 1)) * 0.5 * uD * p.cfFacMom;
   if (i >= 0 && i <= d.sNx + 1 && j >= 0 && j <= d.sNy + 1) {
-    double gUtmp = f.cdU[q3] + guCor, gVtmp = f.cdV[q3] + gvCor;
+    double gUtmp = AR3(cdU, q3) + guCor, gVtmp = AR3(cdV, q3) + gvCor;
     if (p.nonlinFreeSurf > 1 && p.select_rStar > 0) {   // timestep.F:274-284
       gUtmp = gUtmp / G2(rStarExpW, i, j);
       gVtmp = gVtmp / G2(rStarExpS, i, j);
     }
-    f.gU[q3] = G3(uVel, i, j, k) + p.deltaTMom * (gUtmp + 0.0) * G3(maskW, i, j, k);
-    f.gV[q3] = G3(vVel, i, j, k) + p.deltaTMom * (gVtmp + 0.0) * G3(maskS, i, j, k);
+    AR3(gU, q3) = G3(uVel, i, j, k) + p.deltaTMom * (gUtmp + 0.0) * G3(maskW, i, j, k);
+    AR3(gV, q3) = G3(vVel, i, j, k) + p.deltaTMom * (gVtmp + 0.0) * G3(maskS, i, j, k);
   }
 #undef G2
 #undef G3
+}
+
+// ---------------------------------------------------------------------------------------
+// MOM_VECINV + CALC_GRAD_PHI_HYD + TIMESTEP + ADAMS_BASHFORTH2 as a 2.5-D tiled sweep: one
+// workgroup owns a BX x BY block of the DYNAMICS range 0..sN+1 of one tile and marches
+// k = 1..Nr.  The level fields the stencils reach (u, v, w, hFacW, hFacS, hFacC on the
+// block plus one ring) are staged in LDS once per level: u, v, hFac in three rotating
+// slots (levels k-1, k, k+1: the vertical shear and the vertical viscous fluxes), w in
+// two; level k+1 is loaded while level k's intermediates are formed.  KE, vort3, hFacZ,
+// h0FacZ and hDiv are formed once per point of the block's (BX+1) x (BY+1) grid into LDS
+// instead of being re-derived by every neighbour.  Masks and reciprocal hFacs come from
+// the staged hFac (maskW = hFacW != 0, recip_hFacW = 1/hFacW: ini_masks_etc.F and
+// update_r_star.F define them so).  vecinv_tend is the same template as the per-point
+// kernel's (accessor VITile), so the two kernels agree bit for bit.
+constexpr int VT_NT = 256, VT_EMAX = 352, VT_IMAX = 304;
+
+struct VITile {
+  const Dims &d; const Params &p; const Fields &f; int k, t, i0, j0, EW, IW;
+  const double *sU, *sV, *sW, *sHW, *sHS, *sHC;   // [3][EMAX] / w [2][EMAX]
+  const double *sKE, *sVort, *sHfz, *sH0fz, *sHDiv;   // [IMAX]
+  __device__ __forceinline__ int e(int ii, int jj) const { return (jj - j0 + 1) * EW + (ii - i0 + 1); }
+  __device__ __forceinline__ int sl(int kk) const { return (kk % 3) * VT_EMAX; }
+  __device__ __forceinline__ double uVel(int ii, int jj, int kk) const { return sU[sl(kk) + e(ii, jj)]; }
+  __device__ __forceinline__ double vVel(int ii, int jj, int kk) const { return sV[sl(kk) + e(ii, jj)]; }
+  __device__ __forceinline__ double wVel(int ii, int jj, int kk) const { return sW[(kk & 1) * VT_EMAX + e(ii, jj)]; }
+  __device__ __forceinline__ double hFacW(int ii, int jj, int kk) const { return sHW[sl(kk) + e(ii, jj)]; }
+  __device__ __forceinline__ double hFacS(int ii, int jj, int kk) const { return sHS[sl(kk) + e(ii, jj)]; }
+  __device__ __forceinline__ double hFacC(int ii, int jj, int kk) const { return sHC[sl(kk) + e(ii, jj)]; }
+  __device__ __forceinline__ double maskW(int ii, int jj, int kk) const { return hFacW(ii, jj, kk) != 0.0 ? 1.0 : 0.0; }
+  __device__ __forceinline__ double maskS(int ii, int jj, int kk) const { return hFacS(ii, jj, kk) != 0.0 ? 1.0 : 0.0; }
+  __device__ __forceinline__ double maskC(int ii, int jj, int kk) const { return hFacC(ii, jj, kk) != 0.0 ? 1.0 : 0.0; }
+  __device__ __forceinline__ double recip_hFacW(int ii, int jj, int kk) const {
+    const double h = hFacW(ii, jj, kk); return h != 0.0 ? 1.0 / h : 0.0; }
+  __device__ __forceinline__ double recip_hFacS(int ii, int jj, int kk) const {
+    const double h = hFacS(ii, jj, kk); return h != 0.0 ? 1.0 / h : 0.0; }
+  __device__ __forceinline__ double recip_hFacC(int ii, int jj, int kk) const {
+    const double h = hFacC(ii, jj, kk); return h != 0.0 ? 1.0 / h : 0.0; }
+  __device__ __forceinline__ double h0FacW(int ii, int jj, int kk) const { return AR3(h0FacW, MG_I3(d, ii, jj, kk, t)); }
+  __device__ __forceinline__ double h0FacS(int ii, int jj, int kk) const { return AR3(h0FacS, MG_I3(d, ii, jj, kk, t)); }
+  __device__ __forceinline__ int iv(int ii, int jj) const { return (jj - j0) * IW + (ii - i0); }       // vort grid
+  __device__ __forceinline__ int id(int ii, int jj) const { return (jj - j0 + 1) * IW + (ii - i0 + 1); } // hDiv grid
+  __device__ __forceinline__ double hfz(int ii, int jj) const { return sHfz[iv(ii, jj)]; }
+  __device__ __forceinline__ double h0fz(int ii, int jj) const { return sH0fz[iv(ii, jj)]; }
+  __device__ __forceinline__ double vort(int ii, int jj) const { return sVort[iv(ii, jj)]; }
+  __device__ __forceinline__ double KE(int ii, int jj) const { return sKE[id(ii, jj)]; }
+  __device__ __forceinline__ double hDiv(int ii, int jj) const { return sHDiv[id(ii, jj)]; }
+};
+
+__global__ void __launch_bounds__(VT_NT) k_mom_vi_tiled(Dims d, Params p, Fields f, const int *iterPtr, int BX, int BY,
+                                                         int nbx, int nby, int KC, int nkc) {
+  __shared__ double sU[3 * VT_EMAX], sV[3 * VT_EMAX], sHW[3 * VT_EMAX], sHS[3 * VT_EMAX], sHC[3 * VT_EMAX];
+  __shared__ double sW[2 * VT_EMAX];
+  __shared__ double sKE[VT_IMAX], sVort[VT_IMAX], sHfz[VT_IMAX], sH0fz[VT_IMAX], sHDiv[VT_IMAX];
+  // block id: (i,j) block fastest, then the chunk of KC levels, then the tile
+  const int nb = nbx * nby, lb = mg_xcd_block();
+  const int t = d.t0 + lb / (nb * nkc), bxy = lb % nb, kb = 1 + ((lb / nb) % nkc) * KC;
+  const int ke = kb + KC - 1 < d.Nr ? kb + KC - 1 : d.Nr;
+  const int i0 = (bxy % nbx) * BX, j0 = (bxy / nbx) * BY;
+  const int tid = threadIdx.x;
+  const int EW = BX + 2, EN = (BX + 2) * (BY + 2), IW = BX + 1, IN = (BX + 1) * (BY + 1);
+  const int Nr = d.Nr;
+  const int i = i0 + tid % BX, j = j0 + tid / BX;
+  const bool act = tid < BX * BY && i <= d.sNx + 1 && j <= d.sNy + 1;
+  const int myIter = *iterPtr;
+  const double abFac = (myIter == p.nIter0 && p.nIter0 == 0) ? 0.0 : 0.5 + p.abEps;   // adams_bashforth2.F:61-65
+  const double mass2rUnit = 1.0 / p.rhoConst;
+  const bool rstar = p.nonlinFreeSurf > 0 && p.select_rStar > 0;
+  const long q2 = MG_I2(d, i, j, t);
+  VITile a{d, p, f, 1, t, i0, j0, EW, IW, sU, sV, sW, sHW, sHS, sHC, sKE, sVort, sHfz, sH0fz, sHDiv};
+  // the block's extent: i0-1..i0+BX, j0-1..j0+BY, clipped to the array (points past it are
+  // read by no active thread)
+  auto ext_q3 = [&](int ee, int kk, bool &in) -> long {
+    const int ii = i0 - 1 + ee % EW, jj = j0 - 1 + ee / EW;
+    in = ii <= d.sNx + d.OLx && jj <= d.sNy + d.OLy;
+    return MG_I3(d, in ? ii : 1, in ? jj : 1, kk, t);
+  };
+  double nU[2], nV[2], nW[2], nHW[2], nHS[2], nHC[2];
+  auto fetch = [&](int kk) {
+#pragma unroll
+    for (int r = 0; r < 2; r++) {
+      const int ee = tid + r * VT_NT;
+      bool in = false;
+      if (ee < EN) {
+        const long q = ext_q3(ee, kk, in);
+        nU[r] = in ? AR3(uVel, q) : 0.0; nV[r] = in ? AR3(vVel, q) : 0.0; nW[r] = in ? AR3(wVel, q) : 0.0;
+        nHW[r] = in ? AR3(hFacW, q) : 0.0; nHS[r] = in ? AR3(hFacS, q) : 0.0; nHC[r] = in ? AR3(hFacC, q) : 0.0;
+      }
+    }
+  };
+  auto stash = [&](int kk) {
+#pragma unroll
+    for (int r = 0; r < 2; r++) {
+      const int ee = tid + r * VT_NT;
+      if (ee < EN) {
+        const int o = (kk % 3) * VT_EMAX + ee;
+        sU[o] = nU[r]; sV[o] = nV[r]; sHW[o] = nHW[r]; sHS[o] = nHS[r]; sHC[o] = nHC[r];
+        sW[(kk & 1) * VT_EMAX + ee] = nW[r];
+      }
+    }
+  };
+  // levels kb-1 (the vertical shear / viscous flux partner above) and kb
+  if (kb > 1) { fetch(kb - 1); stash(kb - 1); }
+  fetch(kb);
+  stash(kb);
+  __syncthreads();
+  for (int k = kb; k <= ke; k++) {
+    a.k = k;
+    if (k < Nr) fetch(k + 1);   // in flight while level k's intermediates are formed
+    // per-level intermediates on the (BX+1) x (BY+1) grids
+    for (int q = tid; q < IN; q += VT_NT) {
+      const int ii = i0 + q % IW, jj = j0 + q / IW;          // vort / hFacZ grid: i0..i0+BX
+      const bool ok = ii <= d.sNx + d.OLx && jj <= d.sNy + d.OLy;
+      sHfz[q] = ok ? vi_hfacz(a, d, ii, jj, k) : 0.0;
+      sH0fz[q] = ok ? vi_h0facz(a, d, p, ii, jj, k) : 0.0;
+      sVort[q] = ok ? vi_vort(a, d, p, f, ii, jj, k, t) : 0.0;
+      const int ih = ii - 1, jh = jj - 1;                     // KE / hDiv grid: i0-1..i0+BX-1
+      sKE[q] = vi_KE(a, d, p, f, ih, jh, k, t);
+      sHDiv[q] = vi_hdiv(a, d, p, f, ih, jh, k, t);
+    }
+    if (k < Nr) stash(k + 1);
+    __syncthreads();
+    if (act) {
+      const long q3 = MG_I3(d, i, j, k, t);
+      const double recip_drF = f.recip_drF[k - 1];
+      double gU = 0.0, gV = 0.0, guDiss = 0.0, gvDiss = 0.0, dPhiHydX = 0.0, dPhiHydY = 0.0;
+      {  // CALC_GRAD_PHI_HYD (calc_grad_phi_hyd.F:152-214), as k_mom_step
+        const bool rsc = rstar && p.select_rStar >= 2 && p.nonlinFreeSurf >= 4;
+        auto varLoc = [&](int ii, int jj) {
+          return rsc ? AR3(phiHydC, MG_I3(d, ii, jj, k, t)) * AR2(rStarFacC, MG_I2(d, ii, jj, t)) + 0.0
+                     : AR3(phiHydC, MG_I3(d, ii, jj, k, t)) + 0.0;
+        };
+        const double vl = varLoc(i, j);
+        if (i >= 1) dPhiHydX = AR2(recip_dxC, q2) * (vl - varLoc(i - 1, j));
+        if (j >= 1) dPhiHydY = AR2(recip_dyC, q2) * (vl - varLoc(i, j - 1));
+        if (rstar && p.select_rStar >= 2) {
+          const double factorP = p.gravity * (1.0 / p.rhoConst) * 0.5, rCk = f.rC[k - 1];
+          auto vl2 = [&](int ii, int jj) { return AR2(etaH, MG_I2(d, ii, jj, t)) * (1.0 + rCk * AR2(recip_Rcol, MG_I2(d, ii, jj, t))); };
+          const double e0 = vl2(i, j), a0 = AR3(alphaRho, q3);
+          if (i >= 1)
+            dPhiHydX = dPhiHydX + factorP * (AR3(alphaRho, MG_I3(d, i - 1, j, k, t)) + a0) * (e0 - vl2(i - 1, j)) * AR2(recip_dxC, q2);
+          if (j >= 1)
+            dPhiHydY = dPhiHydY + factorP * (AR3(alphaRho, MG_I3(d, i, j - 1, k, t)) + a0) * (e0 - vl2(i, j - 1)) * AR2(recip_dyC, q2);
+        }
+      }
+      vecinv_tend(a, d, p, f, i, j, k, t, gU, gV, guDiss, gvDiss);
+      // TIMESTEP (timestep.F:104-388), as k_mom_step
+      double guExt = 0.0, gvExt = 0.0;
+      if (p.momForcing && k == 1) {
+        if (j >= 0 && j <= d.sNy + 1 && i >= 1 && i <= d.sNx + 1)
+          guExt = guExt + p.foFacMom * (AR2(fu, q2) * mass2rUnit) * recip_drF * a.recip_hFacW(i, j, k);
+        if (j >= 1 && j <= d.sNy + 1 && i >= 0 && i <= d.sNx + 1)
+          gvExt = gvExt + p.foFacMom * (AR2(fv, q2) * mass2rUnit) * recip_drF * a.recip_hFacS(i, j, k);
+      }
+      gU = gU - p.pfFacMom * dPhiHydX;
+      gV = gV - p.pfFacMom * dPhiHydY;
+      if (p.momViscosity && p.momDissip_In_AB) { gU = gU + guDiss; gV = gV + gvDiss; }
+      if (p.momForcing && p.momForcingOutAB != 1) { gU = gU + guExt; gV = gV + gvExt; }
+      {  // ADAMS_BASHFORTH2 (adams_bashforth2.F:81-88)
+        const double gUo = AR3(guNm1, q3), gVo = AR3(gvNm1, q3);
+        double ab = abFac * (gU - gUo);
+        AR3(guNm1, q3) = gU;
+        gU = gU + ab;
+        ab = abFac * (gV - gVo);
+        AR3(gvNm1, q3) = gV;
+        gV = gV + ab;
+      }
+      double gUtmp = gU, gVtmp = gV;
+      if (p.momForcing && p.momForcingOutAB == 1) { gUtmp = gUtmp + guExt; gVtmp = gVtmp + gvExt; }
+      if (p.momViscosity && !p.momDissip_In_AB) { gUtmp = gUtmp + guDiss; gVtmp = gVtmp + gvDiss; }
+      if (rstar && p.nonlinFreeSurf > 1) {
+        gUtmp = gUtmp / AR2(rStarExpW, q2);
+        gVtmp = gVtmp / AR2(rStarExpS, q2);
+      }
+      AR3(gU, q3) = a.uVel(i, j, k) + p.deltaTMom * (gUtmp + 0.0) * a.maskW(i, j, k);
+      AR3(gV, q3) = a.vVel(i, j, k) + p.deltaTMom * (gVtmp + 0.0) * a.maskS(i, j, k);
+    }
+    __syncthreads();
+  }
+}
+
+// One level per workgroup: level k of the block plus one ring staged in LDS (u, v, w,
+// hFacW, hFacS, hFacC), the intermediates formed once per point into LDS; the other
+// levels' values (vertical shear, vertical viscous fluxes, masks at k-1 / k+1, w(k+1))
+// are read where they lie.  No level march: many small workgroups, modest registers.
+struct VILevel {
+  const Dims &d; const Params &p; const Fields &f; int k, t, i0, j0, EW, IW;
+  const double *sU, *sV, *sW, *sHW, *sHS, *sHC;   // level k on the extent
+  const double *sKE, *sVort, *sHfz, *sH0fz, *sHDiv;
+  __device__ __forceinline__ int e(int ii, int jj) const { return (jj - j0 + 1) * EW + (ii - i0 + 1); }
+  __device__ __forceinline__ long g(int ii, int jj, int kk) const { return MG_I3(d, ii, jj, kk, t); }
+  __device__ __forceinline__ double uVel(int ii, int jj, int kk) const { return kk == k ? sU[e(ii, jj)] : AR3(uVel, g(ii, jj, kk)); }
+  __device__ __forceinline__ double vVel(int ii, int jj, int kk) const { return kk == k ? sV[e(ii, jj)] : AR3(vVel, g(ii, jj, kk)); }
+  __device__ __forceinline__ double wVel(int ii, int jj, int kk) const { return kk == k ? sW[e(ii, jj)] : AR3(wVel, g(ii, jj, kk)); }
+  __device__ __forceinline__ double hFacW(int ii, int jj, int kk) const { return kk == k ? sHW[e(ii, jj)] : AR3(hFacW, g(ii, jj, kk)); }
+  __device__ __forceinline__ double hFacS(int ii, int jj, int kk) const { return kk == k ? sHS[e(ii, jj)] : AR3(hFacS, g(ii, jj, kk)); }
+  __device__ __forceinline__ double hFacC(int ii, int jj, int kk) const { return kk == k ? sHC[e(ii, jj)] : AR3(hFacC, g(ii, jj, kk)); }
+  __device__ __forceinline__ double maskW(int ii, int jj, int kk) const { return hFacW(ii, jj, kk) != 0.0 ? 1.0 : 0.0; }
+  __device__ __forceinline__ double maskS(int ii, int jj, int kk) const { return hFacS(ii, jj, kk) != 0.0 ? 1.0 : 0.0; }
+  __device__ __forceinline__ double maskC(int ii, int jj, int kk) const { return hFacC(ii, jj, kk) != 0.0 ? 1.0 : 0.0; }
+  __device__ __forceinline__ double recip_hFacW(int ii, int jj, int kk) const {
+    const double h = hFacW(ii, jj, kk); return h != 0.0 ? 1.0 / h : 0.0; }
+  __device__ __forceinline__ double recip_hFacS(int ii, int jj, int kk) const {
+    const double h = hFacS(ii, jj, kk); return h != 0.0 ? 1.0 / h : 0.0; }
+  __device__ __forceinline__ double recip_hFacC(int ii, int jj, int kk) const {
+    const double h = hFacC(ii, jj, kk); return h != 0.0 ? 1.0 / h : 0.0; }
+  __device__ __forceinline__ double h0FacW(int ii, int jj, int kk) const { return AR3(h0FacW, g(ii, jj, kk)); }
+  __device__ __forceinline__ double h0FacS(int ii, int jj, int kk) const { return AR3(h0FacS, g(ii, jj, kk)); }
+  __device__ __forceinline__ int iv(int ii, int jj) const { return (jj - j0) * IW + (ii - i0); }
+  __device__ __forceinline__ int id(int ii, int jj) const { return (jj - j0 + 1) * IW + (ii - i0 + 1); }
+  __device__ __forceinline__ double hfz(int ii, int jj) const { return sHfz[iv(ii, jj)]; }
+  __device__ __forceinline__ double h0fz(int ii, int jj) const { return sH0fz[iv(ii, jj)]; }
+  __device__ __forceinline__ double vort(int ii, int jj) const { return sVort[iv(ii, jj)]; }
+  __device__ __forceinline__ double KE(int ii, int jj) const { return sKE[id(ii, jj)]; }
+  __device__ __forceinline__ double hDiv(int ii, int jj) const { return sHDiv[id(ii, jj)]; }
+};
+
+__global__ void __launch_bounds__(VT_NT) k_mom_vi_level(Dims d, Params p, Fields f, const int *iterPtr, int BX, int BY,
+                                                         int nbx, int nby) {
+  __shared__ double sU[VT_EMAX], sV[VT_EMAX], sW[VT_EMAX], sHW[VT_EMAX], sHS[VT_EMAX], sHC[VT_EMAX];
+  __shared__ double sKE[VT_IMAX], sVort[VT_IMAX], sHfz[VT_IMAX], sH0fz[VT_IMAX], sHDiv[VT_IMAX];
+  // block id: (i,j) block fastest, then the level, then the tile
+  const int nb = nbx * nby, lb = mg_xcd_block();
+  const int t = d.t0 + lb / (nb * d.Nr), bxy = lb % nb, k = 1 + (lb / nb) % d.Nr;
+  const int i0 = (bxy % nbx) * BX, j0 = (bxy / nbx) * BY;
+  const int tid = threadIdx.x;
+  const int EW = BX + 2, EN = (BX + 2) * (BY + 2), IW = BX + 1, IN = (BX + 1) * (BY + 1);
+  const int i = i0 + tid % BX, j = j0 + tid / BX;
+  const bool act = tid < BX * BY && i <= d.sNx + 1 && j <= d.sNy + 1;
+  VILevel a{d, p, f, k, t, i0, j0, EW, IW, sU, sV, sW, sHW, sHS, sHC, sKE, sVort, sHfz, sH0fz, sHDiv};
+  for (int ee = tid; ee < EN; ee += VT_NT) {
+    const int ii = i0 - 1 + ee % EW, jj = j0 - 1 + ee / EW;
+    const bool in = ii <= d.sNx + d.OLx && jj <= d.sNy + d.OLy;
+    const long q = MG_I3(d, in ? ii : 1, in ? jj : 1, k, t);
+    sU[ee] = in ? AR3(uVel, q) : 0.0; sV[ee] = in ? AR3(vVel, q) : 0.0; sW[ee] = in ? AR3(wVel, q) : 0.0;
+    sHW[ee] = in ? AR3(hFacW, q) : 0.0; sHS[ee] = in ? AR3(hFacS, q) : 0.0; sHC[ee] = in ? AR3(hFacC, q) : 0.0;
+  }
+  __syncthreads();
+  for (int q = tid; q < IN; q += VT_NT) {
+    const int ii = i0 + q % IW, jj = j0 + q / IW;
+    const bool ok = ii <= d.sNx + d.OLx && jj <= d.sNy + d.OLy;
+    sHfz[q] = ok ? vi_hfacz(a, d, ii, jj, k) : 0.0;
+    sH0fz[q] = ok ? vi_h0facz(a, d, p, ii, jj, k) : 0.0;
+    sVort[q] = ok ? vi_vort(a, d, p, f, ii, jj, k, t) : 0.0;
+    sKE[q] = vi_KE(a, d, p, f, ii - 1, jj - 1, k, t);
+    sHDiv[q] = vi_hdiv(a, d, p, f, ii - 1, jj - 1, k, t);
+  }
+  __syncthreads();
+  if (!act) return;
+  const int myIter = *iterPtr;
+  const double abFac = (myIter == p.nIter0 && p.nIter0 == 0) ? 0.0 : 0.5 + p.abEps;   // adams_bashforth2.F:61-65
+  const double mass2rUnit = 1.0 / p.rhoConst;
+  const bool rstar = p.nonlinFreeSurf > 0 && p.select_rStar > 0;
+  const long q2 = MG_I2(d, i, j, t), q3 = MG_I3(d, i, j, k, t);
+  const double recip_drF = f.recip_drF[k - 1];
+  double gU = 0.0, gV = 0.0, guDiss = 0.0, gvDiss = 0.0, dPhiHydX = 0.0, dPhiHydY = 0.0;
+  {  // CALC_GRAD_PHI_HYD (calc_grad_phi_hyd.F:152-214), as k_mom_step
+    const bool rsc = rstar && p.select_rStar >= 2 && p.nonlinFreeSurf >= 4;
+    auto varLoc = [&](int ii, int jj) {
+      return rsc ? AR3(phiHydC, MG_I3(d, ii, jj, k, t)) * AR2(rStarFacC, MG_I2(d, ii, jj, t)) + 0.0
+                 : AR3(phiHydC, MG_I3(d, ii, jj, k, t)) + 0.0;
+    };
+    const double vl = varLoc(i, j);
+    if (i >= 1) dPhiHydX = AR2(recip_dxC, q2) * (vl - varLoc(i - 1, j));
+    if (j >= 1) dPhiHydY = AR2(recip_dyC, q2) * (vl - varLoc(i, j - 1));
+    if (rstar && p.select_rStar >= 2) {
+      const double factorP = p.gravity * (1.0 / p.rhoConst) * 0.5, rCk = f.rC[k - 1];
+      auto vl2 = [&](int ii, int jj) { return AR2(etaH, MG_I2(d, ii, jj, t)) * (1.0 + rCk * AR2(recip_Rcol, MG_I2(d, ii, jj, t))); };
+      const double e0 = vl2(i, j), a0 = AR3(alphaRho, q3);
+      if (i >= 1)
+        dPhiHydX = dPhiHydX + factorP * (AR3(alphaRho, MG_I3(d, i - 1, j, k, t)) + a0) * (e0 - vl2(i - 1, j)) * AR2(recip_dxC, q2);
+      if (j >= 1)
+        dPhiHydY = dPhiHydY + factorP * (AR3(alphaRho, MG_I3(d, i, j - 1, k, t)) + a0) * (e0 - vl2(i, j - 1)) * AR2(recip_dyC, q2);
+    }
+  }
+  vecinv_tend(a, d, p, f, i, j, k, t, gU, gV, guDiss, gvDiss);
+  double guExt = 0.0, gvExt = 0.0;
+  if (p.momForcing && k == 1) {
+    if (j >= 0 && j <= d.sNy + 1 && i >= 1 && i <= d.sNx + 1)
+      guExt = guExt + p.foFacMom * (AR2(fu, q2) * mass2rUnit) * recip_drF * a.recip_hFacW(i, j, k);
+    if (j >= 1 && j <= d.sNy + 1 && i >= 0 && i <= d.sNx + 1)
+      gvExt = gvExt + p.foFacMom * (AR2(fv, q2) * mass2rUnit) * recip_drF * a.recip_hFacS(i, j, k);
+  }
+  gU = gU - p.pfFacMom * dPhiHydX;
+  gV = gV - p.pfFacMom * dPhiHydY;
+  if (p.momViscosity && p.momDissip_In_AB) { gU = gU + guDiss; gV = gV + gvDiss; }
+  if (p.momForcing && p.momForcingOutAB != 1) { gU = gU + guExt; gV = gV + gvExt; }
+  {
+    const double gUo = AR3(guNm1, q3), gVo = AR3(gvNm1, q3);
+    double ab = abFac * (gU - gUo);
+    AR3(guNm1, q3) = gU;
+    gU = gU + ab;
+    ab = abFac * (gV - gVo);
+    AR3(gvNm1, q3) = gV;
+    gV = gV + ab;
+  }
+  double gUtmp = gU, gVtmp = gV;
+  if (p.momForcing && p.momForcingOutAB == 1) { gUtmp = gUtmp + guExt; gVtmp = gVtmp + gvExt; }
+  if (p.momViscosity && !p.momDissip_In_AB) { gUtmp = gUtmp + guDiss; gVtmp = gVtmp + gvDiss; }
+  if (rstar && p.nonlinFreeSurf > 1) {
+    gUtmp = gUtmp / AR2(rStarExpW, q2);
+    gVtmp = gVtmp / AR2(rStarExpS, q2);
+  }
+  AR3(gU, q3) = a.uVel(i, j, k) + p.deltaTMom * (gUtmp + 0.0) * a.maskW(i, j, k);
+  AR3(gV, q3) = a.vVel(i, j, k) + p.deltaTMom * (gVtmp + 0.0) * a.maskS(i, j, k);
+}
+
+// The halo ring outside the DYNAMICS range (i or j outside 0..sN+1): no tendency, but
+// ADAMS_BASHFORTH2 runs over the whole slab (gU = abFac*(0 - guNm1), guNm1 = 0), as
+// k_mom_step does there.
+__global__ void __launch_bounds__(256) k_mom_halo_ab(Dims d, Params p, Fields f, const int *iterPtr) {
+  MG_PLANE(1 - d.OLx, d.nx, 1 - d.OLy, d.ny, z)
+  const int t = d.t0 + z / d.Nr, k = z % d.Nr + 1;
+  if (i > d.sNx + d.OLx || j > d.sNy + d.OLy) return;
+  if (i >= 0 && i <= d.sNx + 1 && j >= 0 && j <= d.sNy + 1) return;
+  const int myIter = *iterPtr;
+  const double abFac = (myIter == p.nIter0 && p.nIter0 == 0) ? 0.0 : 0.5 + p.abEps;
+  const long q3 = MG_I3(d, i, j, k, t);
+  double gU = 0.0, gV = 0.0;
+  const double gUo = AR3(guNm1, q3), gVo = AR3(gvNm1, q3);
+  double ab = abFac * (gU - gUo);
+  AR3(guNm1, q3) = gU;
+  gU = gU + ab;
+  ab = abFac * (gV - gVo);
+  AR3(gvNm1, q3) = gV;
+  gV = gV + ab;
+  AR3(gU, q3) = gU;
+  AR3(gV, q3) = gV;
+}
+
+// block shape of k_mom_vi_tiled: BX along i (a whole output row when it is short), BY rows
+static void vi_tile_shape(const Dims &d, int &BX, int &BY) {
+  const int W = d.sNx + 2, H = d.sNy + 2;
+  const int nbx = (W + 31) / 32;
+  BX = (W + nbx - 1) / nbx;                 // 92 -> 31, 34 -> 17 (two blocks), <= 32
+  BY = VT_NT / BX;
+  while (BY > 1 && ((BX + 2) * (BY + 2) > VT_EMAX || (BX + 1) * (BY + 1) > VT_IMAX)) BY--;
+  const int nby = (H + BY - 1) / BY;
+  BY = (H + nby - 1) / nby;                 // balance the rows over the blocks
 }
 
 hipError_t launch_mom_step(const Dims &d, const Params &p, const Fields &f, const int *iterPtr, hipStream_t s) {
@@ -859,7 +1272,25 @@ hipError_t launch_mom_step(const Dims &d, const Params &p, const Fields &f, cons
   if (p.momViscosity && (p.viscA4D != 0.0 || p.viscA4Z != 0.0))
     hipLaunchKernelGGL(k_del2uv, dim3(mg_plane_blocks(d.nx, d.ny, d.nT * d.Nr)), dim3(MG_PLANE_THREADS), 0, s, d, p, f);
   // MOM_VECINV or MOM_FLUXFORM: separate instantiations (no register-pressure coupling)
-  if (p.vectorInvariantMomentum)
+  static const bool viPoint = getenv("MGCM_VI_POINT") != nullptr;   // the per-point form, for comparison
+  if (p.vectorInvariantMomentum && !viPoint && d.OLx >= 2 && d.OLy >= 2 && p.selectVortScheme <= 2) {
+    int BX, BY;
+    vi_tile_shape(d, BX, BY);
+    const int nbx = (d.sNx + 2 + BX - 1) / BX, nby = (d.sNy + 2 + BY - 1) / BY;
+    // levels per workgroup: enough workgroups to fill the chip several times, few enough
+    // that the two extra staged levels per chunk stay a small overhead
+    static const int kcEnv = getenv("MGCM_VI_KC") ? atoi(getenv("MGCM_VI_KC")) : 0;
+    if (kcEnv <= 0) {   // one level per workgroup (default)
+      hipLaunchKernelGGL(k_mom_vi_level, dim3((unsigned)(nbx * nby * d.nT * d.Nr)), dim3(VT_NT), 0, s, d, p, f, iterPtr, BX,
+                         BY, nbx, nby);
+    } else {            // MGCM_VI_KC levels marched per workgroup
+      const int KC = kcEnv > d.Nr ? d.Nr : kcEnv, nkc = (d.Nr + KC - 1) / KC;
+      hipLaunchKernelGGL(k_mom_vi_tiled, dim3((unsigned)(nbx * nby * d.nT * nkc)), dim3(VT_NT), 0, s, d, p, f, iterPtr, BX,
+                         BY, nbx, nby, KC, nkc);
+    }
+    hipLaunchKernelGGL(k_mom_halo_ab, dim3(mg_plane_blocks(d.nx, d.ny, d.nT * d.Nr)), dim3(MG_PLANE_THREADS), 0, s, d, p,
+                       f, iterPtr);
+  } else if (p.vectorInvariantMomentum)
     hipLaunchKernelGGL(k_mom_step<true>, dim3(mg_plane_blocks(d.nx, d.ny, d.nT * d.Nr)), dim3(MG_PLANE_THREADS), 0, s,
                        d, p, f, iterPtr);
   else

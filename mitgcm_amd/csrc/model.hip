@@ -81,33 +81,14 @@ struct FieldDesc {
 
 #define FD(n, k) {#n, k, offsetof(Fields, n)}
 static const FieldDesc FIELDS[] = {
-    FD(drF, F1D), FD(drC, F1D), FD(recip_drF, F1D), FD(recip_drC, F1D), FD(rF, F1D), FD(rC, F1D),
-    FD(tRef, F1D), FD(sRef, F1D),
-    FD(dxF, F2D), FD(dyF, F2D), FD(dxG, F2D), FD(dyG, F2D), FD(dxC, F2D), FD(dyC, F2D), FD(dxV, F2D), FD(dyU, F2D),
-    FD(rA, F2D), FD(rAw, F2D), FD(rAs, F2D), FD(recip_dxF, F2D), FD(recip_dyF, F2D), FD(recip_dxC, F2D),
-    FD(recip_dyC, F2D), FD(recip_dxV, F2D), FD(recip_dyU, F2D), FD(recip_rA, F2D), FD(recip_rAw, F2D),
-    FD(recip_rAs, F2D), FD(fCori, F2D), FD(Bo_surf, F2D), FD(recip_Bo, F2D),
-    FD(tanPhiAtU, F2D), FD(tanPhiAtV, F2D), FD(maskInC, F2D), FD(SST, F2D), FD(lambdaThetaClimRelax, F2D),
-    FD(hFacC, F3D), FD(hFacW, F3D), FD(hFacS, F3D), FD(recip_hFacC, F3D), FD(recip_hFacW, F3D), FD(recip_hFacS, F3D),
-    FD(maskC, F3D), FD(maskW, F3D), FD(maskS, F3D),
-    FD(aW2d, F2D), FD(aS2d, F2D), FD(aC2d, F2D), FD(pW, F2D), FD(pS, F2D), FD(pC, F2D),
-    FD(uVel, F3D), FD(vVel, F3D), FD(wVel, F3D), FD(theta, F3D), FD(salt, F3D), FD(etaN, F2D),
-    FD(gU, F3D), FD(gV, F3D), FD(guNm1, F3D), FD(gvNm1, F3D), FD(fu, F2D), FD(fv, F2D),
-    FD(etaH, F2D), FD(surfaceForcingT, F2D), FD(rhoInSitu, F3D), FD(IVDConvCount, F3D), FD(gtNm1, F3D),
-    FD(thetaNext, F3D), FD(gTscr, F3D), FD(cpScr, F3D), FD(phiHydC, F3D), FD(saltNext, F3D), FD(gsNm1, F3D),
-    FD(surfaceForcingS, F2D), FD(advScr1, F3D), FD(advScr2, F3D), FD(gAdv, F3D),
-    FD(cg2d_b, F2D), FD(cg2d_x, F2D),
-    FD(pRef4EOS, F1D), FD(forcRec, FREC), FD(Qnet, F2D), FD(EmPmR, F2D), FD(SSS, F2D), FD(lambdaSaltClimRelax, F2D),
-    FD(etaNm1, F2D), FD(sigmaR, F3D), FD(Kwx, F3D), FD(Kwy, F3D), FD(Kwz, F3D), FD(Kux, F3D), FD(Kvy, F3D),
-    FD(uVelD, F3D), FD(vVelD, F3D), FD(uNM1, F3D), FD(vNM1, F3D), FD(cdU, F3D), FD(cdV, F3D),
-    FD(h0FacC, F3D), FD(h0FacW, F3D), FD(h0FacS, F3D), FD(fCoriCos, F2D), FD(recip_Rcol, F2D), FD(rSurfW, F2D),
-    FD(rSurfS, F2D), FD(rLowW, F2D), FD(rLowS, F2D), FD(Ro_surf, F2D), FD(R_low, F2D), FD(phiRefC, F1D),
-    FD(totPhiHyd, F3D), FD(alphaRho, F3D), FD(del2u, F3D), FD(del2v, F3D), FD(rStarFacC, F2D), FD(rStarFacW, F2D),
-    FD(rStarFacS, F2D), FD(rStarExpC, F2D), FD(rStarExpW, F2D), FD(rStarExpS, F2D), FD(rStarDhCDt, F2D),
-    FD(rStarDhWDt, F2D), FD(rStarDhSDt, F2D), FD(PmEpR, F2D), FD(dEtaHdt, F2D), FD(maskInW, F2D),
-    FD(maskInS, F2D), FD(dWtC, F3D), FD(dWtU, F3D), FD(dWtV, F3D),
-    FD(fCoriG, F2D), FD(recip_rAz, F2D), FD(recip_dxG, F2D), FD(recip_dyG, F2D),
-    FD(Kuz, F3D), FD(Kvz, F3D), FD(GM_PsiX, F3D), FD(GM_PsiY, F3D),
+    FD(drF, F1D), FD(drC, F1D), FD(recip_drF, F1D), FD(recip_drC, F1D), FD(rF, F1D), FD(rC, F1D), FD(tRef, F1D), FD(sRef, F1D), FD(pRef4EOS, F1D), FD(phiRefC, F1D),
+#define FD2(n) FD(n, F2D),
+#define FD3(n) FD(n, F3D),
+    MG_F2D_LIST(FD2)
+    MG_F3D_LIST(FD3)
+#undef FD2
+#undef FD3
+    FD(forcRec, FREC),
 };
 #undef FD
 
@@ -683,15 +664,35 @@ mgcm_model *mgcm_create(int sNx, int sNy, int OLx, int OLy, int Nr, int nSx, int
     return nullptr;
   }
   m->overlap = getenv("MGCM_NO_OVERLAP") == nullptr;
-  for (auto &fd : FIELDS) {
-    const long n = field_count(m, fd.kind);
-    double *ptr = nullptr;
-    if (hipMalloc(&ptr, n * sizeof(double)) != hipSuccess || hipMemset(ptr, 0, n * sizeof(double)) != hipSuccess) {
-      set_err("mgcm_create: hipMalloc %s (%ld doubles)", fd.name, n);
+  // one arena per kind for the 2-D and 3-D fields (MG_F2D_LIST / MG_F3D_LIST order, common.h)
+  d.N2all = d.n2 * d.nTiles;
+  d.N3all = d.n3 * d.nTiles;
+  double *arena[2] = {nullptr, nullptr};
+  const long arenaN[2] = {(long)F2_COUNT * d.N2all, (long)F3_COUNT * d.N3all};
+  for (int q = 0; q < 2; q++) {
+    if (hipMalloc(&arena[q], arenaN[q] * sizeof(double)) != hipSuccess ||
+        hipMemset(arena[q], 0, arenaN[q] * sizeof(double)) != hipSuccess) {
+      set_err("mgcm_create: hipMalloc of the %s arena (%ld doubles)", q ? "3-D" : "2-D", arenaN[q]);
       mgcm_destroy(m);
       return nullptr;
     }
-    m->allocs.push_back(ptr);
+    m->allocs.push_back(arena[q]);
+  }
+  m->f.a2 = arena[0];
+  m->f.a3 = arena[1];
+  int n2i = 0, n3i = 0;
+  for (auto &fd : FIELDS) {
+    const long n = field_count(m, fd.kind);
+    double *ptr = nullptr;
+    if (fd.kind == F2D) ptr = arena[0] + (long)(n2i++) * d.N2all;
+    else if (fd.kind == F3D) ptr = arena[1] + (long)(n3i++) * d.N3all;
+    else if (hipMalloc(&ptr, n * sizeof(double)) != hipSuccess || hipMemset(ptr, 0, n * sizeof(double)) != hipSuccess) {
+      set_err("mgcm_create: hipMalloc %s (%ld doubles)", fd.name, n);
+      mgcm_destroy(m);
+      return nullptr;
+    } else {
+      m->allocs.push_back(ptr);
+    }
     field_ptr(m, &fd) = ptr;
   }
   if (hipMalloc(&m->d_ctr, 2 * sizeof(int)) != hipSuccess || hipMemset(m->d_ctr, 0, 2 * sizeof(int)) != hipSuccess ||
