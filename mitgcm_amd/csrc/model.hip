@@ -172,6 +172,10 @@ struct mgcm_model {
   std::vector<long> h_uv[2];
   long *d_uv[2] = {nullptr, nullptr};
   int nUvU[2] = {0, 0}, nUvV[2] = {0, 0};
+  // the same maps over every tile (tile-sharded runs recompute the 2-D r* state of the whole
+  // domain redundantly: CALC_R_STAR's EXCH_UV of the W/S factors covers remote tiles too)
+  long *d_uvAll[2] = {nullptr, nullptr};
+  int nUvUAll[2] = {0, 0}, nUvVAll[2] = {0, 0};
   int *d_tileInfo = nullptr;
   // hipGraphs of two FORWARD_STEPs, one per theta/salt ping-pong parity
   bool useGraph = true;
@@ -288,23 +292,27 @@ static int upload_halo(mgcm_model *m) {
   m->nHalo = (int)(loc.size() / 2);
   if (m->uvMap) {
     const long N2 = m->d.n2 * m->d.nTiles;
-    for (int w = 0; w < 2; w++) {
-      if (m->d_uv[w]) { hipFree(m->d_uv[w]); m->d_uv[w] = nullptr; }
-      std::vector<long> e;
-      int nu = 0, nv = 0;
-      for (int c = 0; c < 2; c++)
-        for (long q = lo; q < hi; q++) {
-          const long code = m->h_uv[w][(size_t)c * N2 + q];
-          if (code == 0) continue;
-          e.push_back(q); e.push_back(code);
-          (c ? nv : nu)++;
+    for (int all = 0; all < 2; all++)
+      for (int w = 0; w < 2; w++) {
+        long *&dm = all ? m->d_uvAll[w] : m->d_uv[w];
+        if (dm) { hipFree(dm); dm = nullptr; }
+        const long l0 = all ? 0 : lo, l1 = all ? N2 : hi;
+        std::vector<long> e;
+        int nu = 0, nv = 0;
+        for (int c = 0; c < 2; c++)
+          for (long q = l0; q < l1; q++) {
+            const long code = m->h_uv[w][(size_t)c * N2 + q];
+            if (code == 0) continue;
+            e.push_back(q); e.push_back(code);
+            (c ? nv : nu)++;
+          }
+        (all ? m->nUvUAll : m->nUvU)[w] = nu;
+        (all ? m->nUvVAll : m->nUvV)[w] = nv;
+        if (!e.empty()) {
+          HIPCHK(hipMalloc(&dm, e.size() * sizeof(long)));
+          HIPCHK(hipMemcpy(dm, e.data(), e.size() * sizeof(long), hipMemcpyHostToDevice));
         }
-      m->nUvU[w] = nu; m->nUvV[w] = nv;
-      if (!e.empty()) {
-        HIPCHK(hipMalloc(&m->d_uv[w], e.size() * sizeof(long)));
-        HIPCHK(hipMemcpy(m->d_uv[w], e.data(), e.size() * sizeof(long), hipMemcpyHostToDevice));
       }
-    }
   }
   if (m->nHalo == 0) return 0;
   HIPCHK(hipMalloc(&m->d_halo, loc.size() * sizeof(long)));
@@ -702,6 +710,13 @@ mgcm_model *mgcm_create(int sNx, int sNy, int OLx, int OLy, int Nr, int nSx, int
     return nullptr;
   }
   build_latlon_halo(m);
+  // the zero fills above run on the null stream, which the model's non-blocking streams do
+  // not wait for: finish them before any stream-ordered upload (mgcm_put) can start
+  if (hipDeviceSynchronize() != hipSuccess) {
+    set_err("mgcm_create: zero fill");
+    mgcm_destroy(m);
+    return nullptr;
+  }
   return m;
 }
 
@@ -715,8 +730,10 @@ void mgcm_destroy(mgcm_model *m) {
   for (void *p : m->allocs) hipFree(p);
   if (m->d_halo) hipFree(m->d_halo);
   if (m->d_srcOf) hipFree(m->d_srcOf);
-  for (int q = 0; q < 2; q++)
+  for (int q = 0; q < 2; q++) {
     if (m->d_uv[q]) hipFree(m->d_uv[q]);
+    if (m->d_uvAll[q]) hipFree(m->d_uvAll[q]);
+  }
   if (m->d_tileInfo) hipFree(m->d_tileInfo);
   if (m->d_nbr) hipFree(m->d_nbr);
   if (m->d_gofs) hipFree(m->d_gofs);
@@ -739,7 +756,8 @@ int mgcm_set_param(mgcm_model *m, const char *name, double value) {
   if (!strcmp(name, "myIter")) {  // the device-side iteration counter (AB2 start, solve records)
     int it = (int)value;
     HIPCHK(hipSetDevice(m->device));
-    HIPCHK(hipMemcpy(m->d_ctr, &it, sizeof(int), hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpyAsync(m->d_ctr, &it, sizeof(int), hipMemcpyHostToDevice, m->stream));
+    HIPCHK(hipStreamSynchronize(m->stream));
     return 0;
   }
   for (auto &pd : PARAMS)
@@ -766,7 +784,9 @@ int mgcm_set_param(mgcm_model *m, const char *name, double value) {
 double mgcm_get_param(mgcm_model *m, const char *name) {
   if (!strcmp(name, "myIter")) {
     int it = 0;
-    if (hipMemcpy(&it, m->d_ctr, sizeof(int), hipMemcpyDeviceToHost) != hipSuccess) return NAN;
+    if (hipMemcpyAsync(&it, m->d_ctr, sizeof(int), hipMemcpyDeviceToHost, m->stream) != hipSuccess ||
+        hipStreamSynchronize(m->stream) != hipSuccess)
+      return NAN;
     return it;
   }
   // 4: k_cg2d_mwg, 3: k_cg2d_bxy, 2: k_cg2d_blk2, 1: k_cg2d_block
@@ -874,16 +894,26 @@ static int exchange_uv(mgcm_model *m, double *u, double *v, int nz, bool withSig
 // factors in place and EXCH_UV_XY_RL(rStarFacW, rStarFacS, .FALSE.) (calc_r_star.F:256-257)
 // refills their halos through the vector map; rStarDh*Dt and rStarExp* are pointwise
 // functions of the new and old factors, so their halos are the same copies.
+// In tile-sharded runs every process holds the whole 2-D state after the free-surface
+// gathers, so the r* state (factors, hFac, CG2D operator) is recomputed on EVERY tile,
+// redundantly and identically: no communication, and the replicated CG2D sees the global
+// operator.
+static Dims all_tiles(const Dims &d) { Dims a = d; a.t0 = 0; a.nT = d.nTiles; return a; }
+
 static hipError_t calc_r_star(mgcm_model *m) {
-  hipError_t e = launch_calc_r_star(m->d, m->p, m->f, m->d_srcOf, m->stream);
+  const Dims da = all_tiles(m->d);
+  hipError_t e = launch_calc_r_star(da, m->p, m->f, m->d_srcOf, m->stream);
   if (e != hipSuccess || !m->uvMap) return e;
   double *pairs[3][2] = {{m->f.rStarFacW, m->f.rStarFacS}, {m->f.rStarDhWDt, m->f.rStarDhSDt},
                          {m->f.rStarExpW, m->f.rStarExpS}};
   for (auto &pr : pairs) {
-    e = launch_exchange_uv(m->d, pr[0], pr[1], m->d_uv[0], m->nUvU[0], m->nUvV[0], 1, m->stream);
+    e = launch_exchange_uv(da, pr[0], pr[1], m->d_uvAll[0], m->nUvUAll[0], m->nUvVAll[0], 1, m->stream);
     if (e != hipSuccess) return e;
   }
   return hipSuccess;
+}
+static hipError_t update_r_star_cg2d(mgcm_model *m) {
+  return launch_update_r_star_cg2d(all_tiles(m->d), m->p, m->f, m->d_srcOf, m->stream);
 }
 
 int mgcm_init(mgcm_model *m) {
@@ -905,7 +935,6 @@ int mgcm_init(mgcm_model *m) {
     if (m->p.nonlinFreeSurf != 4 || m->p.select_rStar != 2)
       return set_err("mgcm_init: the non-linear free surface is implemented for nonlinFreeSurf=4, select_rStar=2 only");
     if (!m->p.exactConserv) return set_err("mgcm_init: nonlinFreeSurf needs exactConserv");
-    if (m->d.nT != m->d.nTiles) return set_err("mgcm_init: r* is not implemented for tile-sharded runs yet");
   }
   if (m->p.selectP_inEOS_Zc > 2) return set_err("mgcm_init: selectP_inEOS_Zc = 3 needs the non-hydrostatic pressure");
   if (m->p.selectP_inEOS_Zc == 2 && !m->p.storePhiHyd4Phys)
@@ -959,15 +988,18 @@ int mgcm_init(mgcm_model *m) {
   m->saltA = m->f.salt;
   m->useGraph = getenv("MGCM_NO_GRAPH") == nullptr;
   int it0 = m->p.nIter0;
-  HIPCHK(hipMemcpy(m->d_ctr, &it0, sizeof(int), hipMemcpyHostToDevice));
+  // every copy is ordered on the model's stream (a null-stream hipMemcpy does not wait for
+  // the non-blocking streams)
+  HIPCHK(hipMemcpyAsync(m->d_ctr, &it0, sizeof(int), hipMemcpyHostToDevice, m->stream));
   // INI_PSURF (ini_psurf.F:84) on a cold start: etaH = etaN (a pickup holds etaH)
   if (m->p.nIter0 == 0)
-    HIPCHK(hipMemcpy(m->f.etaH, m->f.etaN, m->d.n2 * m->d.nTiles * sizeof(double), hipMemcpyDeviceToDevice));
+    HIPCHK(hipMemcpyAsync(m->f.etaH, m->f.etaN, m->d.n2 * m->d.nTiles * sizeof(double), hipMemcpyDeviceToDevice,
+                          m->stream));
   if (rstar) {
     // INITIALISE_VARIA (initialise_varia.F:299-349): CALC_R_STAR(etaH) -> UPDATE_R_STAR ->
     // UPDATE_CG2D -> INTEGR_CONTINUITY(nIter0) (+ UPDATE_ETAH, EXCH w) -> CALC_R_STAR(etaH)
     HIPCHK(calc_r_star(m));
-    HIPCHK(launch_update_r_star_cg2d(m->d, m->p, m->f, m->d_srcOf, m->stream));
+    HIPCHK(update_r_star_cg2d(m));
     HIPCHK(launch_corr_cont(m->d, m->p, m->f, 1, m->stream));
     HIPCHK(launch_exch_eta(m->d, m->p, m->f, m->d_srcOf, true, 1, m->stream));
     HIPCHK(launch_exchange(m->d, m->f.wVel, m->d_halo, m->nHalo, m->d.Nr, m->stream));
@@ -1140,7 +1172,7 @@ static int one_step(mgcm_model *m) {
     if (mgcm_dynamics(m)) return -1;
     if (fork) HIPCHK(hipStreamWaitEvent(m->stream, m->evJoin, 0));
     // forward_step.F:829-877: UPDATE_R_STAR(.TRUE.) + UPDATE_CG2D
-    if (m->p.nonlinFreeSurf > 0) TIMED(K_RSTAR, launch_update_r_star_cg2d(m->d, m->p, m->f, m->d_srcOf, m->stream));
+    if (m->p.nonlinFreeSurf > 0) TIMED(K_RSTAR, update_r_star_cg2d(m));
     TIMED(K_RHS, launch_sfp_rhs(m->d, m->p, m->f, m->stream));
     TIMED(K_CG2D, launch_cg2d(m, m->p.cg2dMaxIters, m->p.cg2dUseMinResSol - 1));
     TIMED(K_ETA, launch_exch_eta(m->d, m->p, m->f, m->d_srcOf, false, 0, m->stream));
@@ -1244,11 +1276,24 @@ int mgcm_set_stream(mgcm_model *m, void *stream) {
   return 0;
 }
 
-int mgcm_exchange_nfields(mgcm_model *m) { return blocking_fields(m).n; }
+// The 3-D fields whose halo sources travel between processes: the blocking-exchange set
+// with u and v always included (on an EXCH2 topology the vector map may read either
+// component of a source point, exch2_uv_3d_rx.template).
+static XFields transfer_fields(const mgcm_model *m) {
+  XFields x{};
+  double *fl[] = {m->f.uVel, m->f.vVel, m->f.wVel, m->f.theta, m->f.salt, m->f.uVelD, m->f.vVelD, m->f.totPhiHyd};
+  const bool use[] = {true, true, true, m->p.tempStepping != 0, m->p.saltStepping != 0, m->p.useCDscheme != 0,
+                      m->p.useCDscheme != 0, m->p.storePhiHyd4Phys != 0};
+  for (int q = 0; q < 8; q++)
+    if (use[q]) { x.p[x.n] = fl[q]; x.nz[x.n] = m->d.Nr; x.n++; }
+  return x;
+}
+
+int mgcm_exchange_nfields(mgcm_model *m) { return transfer_fields(m).n; }
 
 int mgcm_halo_pack(mgcm_model *m, const long *idx, long n, double *buf, int unpack) {
   if (check_ready(m)) return -1;
-  HIPCHK(launch_halo_pack(m->d, blocking_fields(m), idx, n, buf, unpack, m->stream));
+  HIPCHK(launch_halo_pack(m->d, transfer_fields(m), idx, n, buf, unpack, m->stream));
   return 0;
 }
 
@@ -1271,19 +1316,28 @@ int mgcm_begin_steps(mgcm_model *m) {
   return 0;
 }
 
-// FORWARD_STEP split at its exchange points.  1: THERMODYNAMICS + DYNAMICS + the
-// SOLVE_FOR_PRESSURE right-hand side on this process's tiles; [gather cg2d_b/x];
-// 2: CG2D on the whole domain (replicated), EXCH+etaN everywhere, correction +
-// continuity on this process's tiles; [gather the new eta]; 3: EXCH eta +
-// UPDATE_ETAH everywhere; [send/recv 3-D halo sources]; 4: blocking exchanges of
-// this process's tiles, step counters.
+// FORWARD_STEP split at its exchange points (tile-sharded runs, mitgcm_amd/parallel.py
+// drives the collectives in between):
+//   1: DO_OCEANIC_PHYS, THERMODYNAMICS (staggerTimeStep = F), DYNAMICS, UPDATE_R_STAR +
+//      UPDATE_CG2D (r*, every tile), the SOLVE_FOR_PRESSURE right-hand side;
+//      [all-gather cg2d_b, cg2d_x]
+//   2: CG2D on the whole domain (replicated), EXCH + etaN everywhere, correction +
+//      continuity on this process's tiles;  [all-gather the new eta (exactConserv)]
+//   3: EXCH eta + UPDATE_ETAH everywhere, CALC_R_STAR (r*, every tile);
+//      [send/recv the 3-D halo sources]
+//   5: staggerTimeStep only: DO_STAGGER_FIELDS_EXCHANGES on this process's tiles, then
+//      THERMODYNAMICS with the new velocities;  [send/recv the 3-D halo sources again]
+//   4: DO_FIELDS_BLOCKING_EXCHANGES of this process's tiles, step counters.
 int mgcm_step_phase(mgcm_model *m, int phase) {
   if (check_ready(m)) return -1;
   if (!m->p.momStepping) return set_err("mgcm_step_phase: requires momStepping");
-  if (m->p.staggerTimeStep) return set_err("mgcm_step_phase: staggerTimeStep not implemented for tile-sharded runs");
+  const bool stagger = m->p.staggerTimeStep != 0;
   switch (phase) {
     case 1:
-      if (mgcm_thermodynamics(m) || mgcm_dynamics(m)) return -1;
+      TIMED(K_PHYS, launch_oceanic_phys(m->d, m->p, m->f, m->d_ctr, m->stream));
+      if (!stagger && tracers_on(m, m->stream)) return -1;
+      if (mgcm_dynamics(m)) return -1;
+      if (m->p.nonlinFreeSurf > 0) TIMED(K_RSTAR, update_r_star_cg2d(m));
       TIMED(K_RHS, launch_sfp_rhs(m->d, m->p, m->f, m->stream));
       return 0;
     case 2:
@@ -1293,8 +1347,15 @@ int mgcm_step_phase(mgcm_model *m, int phase) {
       return 0;
     case 3:
       if (m->p.exactConserv) TIMED(K_ETA, launch_exch_eta(m->d, m->p, m->f, m->d_srcOf, true, 0, m->stream));
+      if (m->p.nonlinFreeSurf > 0) TIMED(K_RSTAR, calc_r_star(m));
       return 0;
+    case 5:
+      if (!stagger) return 0;
+      TIMED(K_EXCH, exchange_uv(m, m->f.uVel, m->f.vVel, m->d.Nr, true) ? hipErrorUnknown : hipSuccess);
+      TIMED(K_EXCH, launch_exchange(m->d, m->f.wVel, m->d_halo, m->nHalo, m->d.Nr, m->stream));
+      return tracers_on(m, m->stream);
     case 4:
+      if (m->uvMap) TIMED(K_EXCH, exchange_uv(m, m->f.uVel, m->f.vVel, m->d.Nr, true) ? hipErrorUnknown : hipSuccess);
       TIMED(K_EXCH, launch_exchange_multi(m->d, blocking_fields(m), m->d_halo, m->nHalo, m->d_ctr, m->stream));
       m->lastBatch++;
       return 0;

@@ -15,7 +15,9 @@ The MI355X design keeps the 3-D work sharded and the 2-D solve replicated:
 * per step the collectives are: one all-gather of the 2-D CG2D right-hand
   side (cg2d_b, cg2d_x tile blocks), one all-gather of the new free surface
   (exactConserv), and one point-to-point exchange of the 3-D halo sources
-  (u, v, w, theta, salt) with each neighbouring process;
+  (u, v, w, theta, salt) with each neighbouring process (twice with
+  staggerTimeStep: the new velocities before THERMODYNAMICS, then the
+  tracers);
 * CG2D itself runs on the gathered global problem on every GPU with the same
   single-workgroup kernel as the 1-GPU path.  The solve is latency-bound
   (~4k-6k points, ~35-125 iterations): a distributed CG would need 3 RCCL
@@ -60,16 +62,26 @@ class HaloPlan:
     halo point of a process's tiles can be filled by the local halo map.
 
     src_of_point: flat (t, j, i) source of every halo-inclusive 2-D point (the
-    topology's EXCH map, topology.py).  Values travel to the SAME global offset
+    topology's EXCH map, topology.py); uv_codes: the pkg/exch2 vector maps
+    (exch2.py uv_codes), whose sources are added to the scalar ones.  Values travel to the SAME global offset
     on the receiver (every process holds the whole domain), so both sides list
     source offsets, sorted: send[peer] (in my tiles, needed by peer) equals the
     peer's recv[me]."""
 
-    def __init__(self, src_of_point, n2, part, rank):
+    def __init__(self, src_of_point, n2, part, rank, uv_codes=None):
         src = np.asarray(src_of_point, dtype=np.int64)
         dst = np.arange(src.size, dtype=np.int64)
         halo = src != dst
         dst, src = dst[halo], src[halo]
+        if uv_codes is not None:
+            # pkg/exch2 vector maps (exch2_uv_3d_rx.template): a u or v halo point reads
+            # u or v at (|code| - 1) mod N; both components travel, so only the point matters
+            N = src_of_point.size if hasattr(src_of_point, "size") else len(src_of_point)
+            for c in uv_codes:
+                c = np.asarray(c, dtype=np.int64)
+                d = np.nonzero(c)[0]
+                dst = np.concatenate([dst, d])
+                src = np.concatenate([src, (np.abs(c[d]) - 1) % N])
         dst_owner = part.owner(dst // n2)
         src_owner = part.owner(src // n2)
         self.rank, self.part = rank, part
@@ -132,7 +144,9 @@ class ShardedModel:
                   "mgcm_set_stream")
         n2 = g.nx * g.ny
         self.n2 = n2
-        self.plan = HaloPlan(g.topo.src_of_point(), n2, self.part, self.rank)
+        uv = g.topo.uv_codes(True) if hasattr(g.topo, "uv_codes") else None
+        self.plan = HaloPlan(g.topo.src_of_point(), n2, self.part, self.rank, uv)
+        self.stagger = bool(model.params.get("staggerTimeStep", 0))
         self.nf = self.L.mgcm_exchange_nfields(h)
         dv = self.dev
         self.idx = {p: torch.as_tensor(v, device=dv) for p, v in
@@ -206,6 +220,10 @@ class ShardedModel:
             self._gather_2d("cg2d_b")
         ck(L.mgcm_step_phase(h, 3), "mgcm_step_phase(3)")
         self._halo()
+        if self.stagger:
+            # DO_STAGGER_FIELDS_EXCHANGES, then THERMODYNAMICS with the new velocities
+            ck(L.mgcm_step_phase(h, 5), "mgcm_step_phase(5)")
+            self._halo()
         ck(L.mgcm_step_phase(h, 4), "mgcm_step_phase(4)")
 
     def forward_step(self, nsteps=1):

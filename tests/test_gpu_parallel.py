@@ -1,8 +1,11 @@
 """Tile-sharded device path (mitgcm_amd/parallel.py + the C-ABI phase API) on a
-real MI355X: 2 and 4 processes share cuda:0 over gloo (host-staged transport;
-RCCL refuses two ranks on one GPU) and step BASELINE config 4 (4 tiles) for 6
-steps; every process's tiles must be bit-identical to a single-process run
-(SURVEY.md 8(c) parity item 6: same results at any GPU count)."""
+real MI355X: 2 to 4 processes share cuda:0 over gloo (host-staged transport;
+RCCL refuses two ranks on one GPU) and step
+  * BASELINE config 4 (baroclinic gyre, 4 lat-lon tiles) for 6 steps, and
+  * BASELINE config 3 (global_ocean.cs32x15: 6 cube faces, pkg/exch2 vector maps and
+    corners, r* with UPDATE_CG2D, staggerTimeStep, GM_AdvForm) for 4 steps;
+every process's tiles must be bit-identical to a single-process run (SURVEY.md 8(c)
+parity item 6: same results at any GPU count)."""
 import os
 import socket
 
@@ -12,7 +15,6 @@ import pytest
 pytestmark = pytest.mark.gpu
 
 FIELDS = ("uVel", "vVel", "wVel", "theta", "salt", "etaN", "etaH")
-NSTEPS = 6
 
 
 def _free_port():
@@ -23,29 +25,35 @@ def _free_port():
     return port
 
 
-def _worker(rank, world, port, q):
+def _make(cfg):
+    from mitgcm_amd import configs
+    if cfg == "gyre":
+        return configs.make_model(configs.baroclinic_gyre, tempAdvScheme=33)
+    return configs.make_model(configs.global_ocean_cs32x15)
+
+
+def _worker(rank, world, port, cfg, nsteps, q):
     import torch
     import torch.distributed as dist
-    from mitgcm_amd import configs
     from mitgcm_amd.parallel import ShardedModel
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         torch.cuda.set_device(0)
-        m = configs.make_model(configs.baroclinic_gyre, tempAdvScheme=33)
+        m = _make(cfg)
         sm = ShardedModel(m, dist, device=torch.device("cuda", 0))
-        sm.forward_step(NSTEPS)
+        sm.forward_step(nsteps)
         m.sync()
         full = {n: sm.gather_field(n) for n in FIELDS}
-        stats = [m.solve_stats(back=b) for b in range(NSTEPS)]
+        stats = [m.solve_stats(back=b) for b in range(nsteps)]
         res = {"t0": sm.t0, "nT": sm.nT, "stats": stats}
         if rank == 0:
-            ref = configs.make_model(configs.baroclinic_gyre, tempAdvScheme=33)
-            ref.forward_step(NSTEPS)
+            ref = _make(cfg)
+            ref.forward_step(nsteps)
             ref.sync()
             res["diff"] = {n: float(np.max(np.abs(full[n] - ref.get(n)))) for n in FIELDS}
             res["equal"] = {n: bool(np.array_equal(full[n], ref.get(n))) for n in FIELDS}
-            res["ref_stats"] = [ref.solve_stats(back=b) for b in range(NSTEPS)]
+            res["ref_stats"] = [ref.solve_stats(back=b) for b in range(nsteps)]
             ref.close()
         m.close()
         q.put((rank, res))
@@ -53,13 +61,16 @@ def _worker(rank, world, port, q):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2, 4])
-def test_sharded_gyre_bit_identical(world):
+@pytest.mark.parametrize("cfg,world,nsteps,ntiles", [("gyre", 2, 6, 4), ("gyre", 4, 6, 4),
+                                                     ("cs32x15", 2, 4, 6), ("cs32x15", 4, 4, 6),
+                                                     ("cs32x15", 6, 4, 6)])
+def test_sharded_bit_identical(cfg, world, nsteps, ntiles):
     import torch.multiprocessing as mp
+    from mitgcm_amd.parallel import TilePartition
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, cfg, nsteps, q)) for r in range(world)]
     for p in procs:
         p.start()
     out = dict(q.get(timeout=300) for _ in procs)
@@ -67,8 +78,9 @@ def test_sharded_gyre_bit_identical(world):
         p.join(timeout=60)
         assert p.exitcode == 0
     r0 = out[0]
-    print("sharded x%d max |diff| vs 1 process:" % world, r0["diff"])
+    print("%s sharded x%d max |diff| vs 1 process:" % (cfg, world), r0["diff"])
     assert all(r0["equal"].values()), r0["diff"]
     for rank, r in out.items():
         assert r["stats"] == r0["ref_stats"], "rank %d: CG2D records differ" % rank
-    assert sorted((r["t0"], r["nT"]) for r in out.values()) == [(t, 4 // world) for t in range(0, 4, 4 // world)]
+    part = TilePartition(ntiles, world)
+    assert sorted((r["t0"], r["nT"]) for r in out.values()) == [part.range(r) for r in range(world)]

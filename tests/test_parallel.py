@@ -131,3 +131,73 @@ def test_sharded_exchange_matches_single_process(layout, world):
     for rank, ok, nsend in res:
         assert ok, "rank %d: sharded exchange differs from the single-process EXCH" % rank
         assert nsend > 0
+
+
+def _cube_worker(rank, world, port, q):
+    """cs cube (pkg/exch2, 6 or 24 tiles): u, v travel with the union of the scalar and
+    vector-map sources; the local vector map then reproduces EXCH2_UV_3D_RX on this
+    process's tiles (signs and cube corners included)."""
+    from mitgcm_amd.exch2 import cube_topology
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        ok = True
+        for sN, OL in ((8, 3), (4, 2)):
+            topo = cube_topology(8, sN, sN, OL)
+            nT, ny, nx = topo.nTiles, topo.ny, topo.nx
+            n2, N = nx * ny, topo.nTiles * topo.ny * topo.nx
+            rng = np.random.default_rng(11)
+            truth = []
+            for _ in range(2):
+                a = np.full((nT, ny, nx), np.nan)
+                a[:, OL:OL + sN, OL:OL + sN] = rng.standard_normal((nT, sN, sN))
+                truth.append(a)
+            eu, ev = topo.exchange_uv(truth[0], truth[1], True)
+            part = TilePartition(nT, world)
+            t0, c = part.range(rank)
+            mine = [np.full(N, np.nan) for _ in range(2)]
+            own = slice(t0 * n2, (t0 + c) * n2)
+            for f in range(2):
+                mine[f][own] = truth[f].reshape(-1)[own]
+            cu, cv = topo.uv_codes(True)
+            plan = HaloPlan(topo.src_of_point(), n2, part, rank, (cu, cv))
+
+            def pack(peer):
+                idx = plan.send[peer]
+                return torch.from_numpy(np.concatenate([mine[0][idx], mine[1][idx]]))
+
+            def make_buf(peer):
+                return torch.empty(2 * plan.recv[peer].size, dtype=torch.float64)
+
+            def unpack(peer, buf):
+                idx, b = plan.recv[peer], buf.numpy()
+                mine[0][idx], mine[1][idx] = b[:idx.size], b[idx.size:]
+
+            exchange(dist, plan, pack, unpack, make_buf)
+            uv = np.concatenate(mine)
+            out = [m.copy() for m in mine]
+            for f, code in enumerate((cu, cv)):
+                d = np.nonzero(code)[0]
+                d = d[(d // n2 >= t0) & (d // n2 < t0 + c)]
+                out[f][d] = np.sign(code[d]) * uv[np.abs(code[d]) - 1]
+            for f, e in enumerate((eu, ev)):
+                ok = ok and np.array_equal(out[f][own], e.reshape(-1)[own], equal_nan=True)
+        q.put((rank, ok, 1))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_sharded_cube_vector_exchange(world):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_cube_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=120) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for rank, ok, _ in res:
+        assert ok, "rank %d: sharded cube vector exchange differs from EXCH2_UV_3D_RX" % rank
