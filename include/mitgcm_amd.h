@@ -23,6 +23,8 @@
 #ifndef MITGCM_AMD_H
 #define MITGCM_AMD_H
 
+#include <stddef.h>
+
 #ifdef __cplusplus
 extern "C" {
 #endif
@@ -80,10 +82,32 @@ int mgcm_dynamics(mgcm_model *m);
 int mgcm_solve_for_pressure(mgcm_model *m);
 /* MOMENTUM_CORRECTION_STEP (model/src/momentum_correction_step.F:7). */
 int mgcm_momentum_correction_step(mgcm_model *m);
-/* INTEGR_CONTINUITY (model/src/integr_continuity.F:13): wVel. */
+/* INTEGR_CONTINUITY (model/src/integr_continuity.F:13): wVel (r* included), and with
+ * exactConserv the new etaN, EXCH, UPDATE_ETAH. */
 int mgcm_integr_continuity(mgcm_model *m);
-/* DO_FIELDS_BLOCKING_EXCHANGES (model/src/do_fields_blocking_exchanges.F:54). */
+/* UPDATE_R_STAR(.TRUE.) + UPDATE_CG2D (update_r_star.F:6, update_cg2d.F:7;
+ * forward_step.F:838-868); no-op unless nonlinFreeSurf > 0. */
+int mgcm_update_r_star(mgcm_model *m);
+/* CALC_R_STAR(etaH) (calc_r_star.F:10; forward_step.F:976); no-op unless nonlinFreeSurf > 0. */
+int mgcm_calc_r_star(mgcm_model *m);
+/* DO_FIELDS_BLOCKING_EXCHANGES (model/src/do_fields_blocking_exchanges.F:54): the set
+ * FORWARD_STEP exchanges (u, v through the vector map on EXCH2, w, the stepped tracers,
+ * uVelD/vVelD with the CD scheme); does not advance the step counter. */
 int mgcm_blocking_exchanges(mgcm_model *m);
+/* DO_OCEANIC_PHYS (model/src/do_oceanic_phys.F:43) alone: forcing records (when
+ * periodicExternalForcing), FREEZE_SURFACE, surface forcing, FIND_RHO_2D, GRAD_SIGMA,
+ * CALC_IVDC, the GM/Redi tensor. */
+int mgcm_oceanic_phys(mgcm_model *m);
+/* THERMODYNAMICS (model/src/thermodynamics.F:25) alone: TEMP/SALT_INTEGRATE + CYCLE_TRACER. */
+int mgcm_tracer_step(mgcm_model *m);
+/* EXCH_XY(Z)_RL / EXCH_UV_XY(Z)_RL (eesupp/src/exch_*_rx.template) on caller-owned host
+ * arrays of nz levels (u alone for a scalar; u, v with vector = 1 for a C-grid pair,
+ * withSigns as the reference's LOGICAL), with this model's halo maps. */
+int mgcm_exchange_host(mgcm_model *m, double *u, double *v, int nz, int vector, int withSigns);
+/* Name of run-time parameter i (0-based) that mgcm_set_param accepts; NULL past the end. */
+const char *mgcm_param_name(int i);
+/* Number of doubles of a named field (-1: unknown name). */
+long mgcm_field_count(mgcm_model *m, const char *name);
 /* Capture the hipGraph that mgcm_forward_step replays (two steps per graph) for
  * the current state, so that a timed region does not include the capture. */
 int mgcm_prepare(mgcm_model *m);
@@ -141,6 +165,41 @@ double mgcm_kernel_ms(mgcm_model *m, const char *name, int *launches);
 void mgcm_kernel_timing(mgcm_model *m, int enable);
 
 /* ------------------------------------------- Fortran drop-in (reference ABI) */
+/* Bound by the MODS-directory shims of mitgcm_amd/fortran/mods; all
+ * arguments by reference, CHARACTER lengths appended as size_t.  Implementation:
+ * mitgcm_amd/csrc/fortran_abi.hip. */
+/* SIZE.h tile set; nProcs = nPx*nPy and nThreads = nTx*nTy must be 1. */
+void mgcm_amd_setup_(const int *sNx, const int *sNy, const int *OLx, const int *OLy, const int *Nr,
+                     const int *nSx, const int *nSy, const int *nProcs, const int *nThreads);
+/* One PARAMS.h parameter (LOGICAL as 0/1). */
+void mgcm_amd_param_(const char *name, const double *value, size_t len);
+/* Register a COMMON-block array of `count` doubles as device field `name`; isStatic:
+ * upload once at init (phiRef(2Nr+1) binds the device's phiRefC). */
+void mgcm_amd_bind_(const char *name, double *array, const int *count, const int *isStatic, size_t len);
+/* Upload the bound arrays and finish the device set-up. */
+void mgcm_amd_init_(const int *myIter);
+/* Routine drop-ins: bound state uploaded before, downloaded after. */
+void do_oceanic_phys_amd_(const double *myTime, const int *myIter, const int *myThid);     /* do_oceanic_phys.F:43 */
+void thermodynamics_amd_(const double *myTime, const int *myIter, const int *myThid);      /* thermodynamics.F:25 */
+void dynamics_amd_(const double *myTime, const int *myIter, const int *myThid);            /* dynamics.F:21 */
+void update_r_star_amd_(const int *useLatest, const double *myTime, const int *myIter,
+                        const int *myThid);                                          /* update_r_star.F:6 */
+void update_cg2d_amd_(const double *myTime, const int *myIter, const int *myThid);        /* update_cg2d.F:7 */
+void calc_r_star_amd_(const double *etaFld, const double *myTime, const int *myIter,
+                      const int *myThid);                                            /* calc_r_star.F:10 */
+void solve_for_pressure_amd_(const double *myTime, const int *myIter, const int *myThid);  /* solve_for_pressure.F:7 */
+void momentum_correction_step_amd_(const double *myTime, const int *myIter,
+                                   const int *myThid);                   /* momentum_correction_step.F:7 */
+void integr_continuity_amd_(const double *uFld, const double *vFld, const double *myTime, const int *myIter,
+                            const int *myThid);                          /* integr_continuity.F:13 */
+void do_fields_blocking_exchanges_amd_(const int *myThid);             /* do_fields_blocking_exchanges.F:7 */
+/* Exchanges and the tile-ordered global sum on host arrays. */
+void exch_xy_rl_amd_(double *phi, const int *myThid);                          /* exch_xy_rx.template:9 */
+void exch_xyz_rl_amd_(double *phi, const int *myThid);                         /* exch_xyz_rx.template:8 */
+void exch_uv_xy_rl_amd_(double *u, double *v, const int *withSigns, const int *myThid);  /* exch_uv_xy_rx.template:11 */
+void exch_uv_xyz_rl_amd_(double *u, double *v, const int *withSigns,
+                         const int *myThid);                                   /* exch_uv_xyz_rx.template:12 */
+void global_sum_tile_rl_amd_(const double *phiTile, double *sumPhi, const int *myThid);  /* global_sum_tile.F:14 */
 /* Registers the CG2D operator of CG2D.h (ini_cg2d.F:61-237 outputs) for the
  * drop-in CG2D below.  Arrays are (1-OLx:sNx+OLx,1-OLy:sNy+OLy,nSx,nSy). */
 void ini_cg2d_amd_(const int *sNx, const int *sNy, const int *OLx, const int *OLy,

@@ -58,6 +58,13 @@ def lib():
         "mgcm_begin_steps": (ci, [vp]),
         "mgcm_tile_copy": (ci, [vp, cs, ci, ci, vp, ci]),
         "mgcm_step_phase": (ci, [vp, ci]),
+        "mgcm_oceanic_phys": (ci, [vp]),
+        "mgcm_tracer_step": (ci, [vp]),
+        "mgcm_exchange_host": (ci, [vp, PD, PD, ci, ci, ci]),
+        "mgcm_field_count": (cl, [vp, cs]),
+        "mgcm_param_name": (cs, [ci]),
+        "mgcm_update_r_star": (ci, [vp]),
+        "mgcm_calc_r_star": (ci, [vp]),
         "ini_cg2d_amd_": (None, [PI] * 6 + [PD] * 8 + [PI]),
         "cg2d_amd_": (None, [PD, PD, PD, PD, PD, PI, PI, PI]),
     }
@@ -75,7 +82,12 @@ EXPORTS = ["mgcm_create", "mgcm_destroy", "mgcm_last_error", "mgcm_set_param", "
            "mgcm_blocking_exchanges", "mgcm_prepare", "mgcm_forward_step", "mgcm_sync", "mgcm_cg2d", "mgcm_cg2d_sum_plan", "mgcm_solve_stats",
            "mgcm_kernel_ms", "mgcm_kernel_timing", "mgcm_set_tile_range", "mgcm_set_stream",
            "mgcm_exchange_nfields", "mgcm_halo_pack", "mgcm_tile_copy", "mgcm_begin_steps", "mgcm_step_phase", "ini_cg2d_amd_",
-           "cg2d_amd_"]
+           "cg2d_amd_", "mgcm_oceanic_phys", "mgcm_tracer_step", "mgcm_exchange_host", "mgcm_field_count", "mgcm_param_name",
+           "mgcm_amd_setup_", "mgcm_amd_param_", "mgcm_amd_bind_", "mgcm_amd_init_", "do_oceanic_phys_amd_",
+           "thermodynamics_amd_", "dynamics_amd_", "solve_for_pressure_amd_", "momentum_correction_step_amd_",
+           "integr_continuity_amd_", "do_fields_blocking_exchanges_amd_", "exch_xy_rl_amd_", "exch_xyz_rl_amd_",
+           "exch_uv_xy_rl_amd_", "exch_uv_xyz_rl_amd_", "global_sum_tile_rl_amd_",
+           "mgcm_update_r_star", "mgcm_calc_r_star", "update_r_star_amd_", "update_cg2d_amd_", "calc_r_star_amd_"]
 
 
 def check(rc, what):

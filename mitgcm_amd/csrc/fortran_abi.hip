@@ -1,0 +1,324 @@
+// fortran_abi.hip -- the Fortran side of the drop-in boundary.
+//
+// MITgcm's plugin mechanism is source shadowing: a file in a genmake2 `-mods` directory
+// replaces the same-named routine of model/src or eesupp/src (tools/genmake2:2231-2241).
+// The shims in mitgcm_amd/fortran/mods/ keep the reference's SUBROUTINE names and argument
+// lists and call the entry points below (lower case + '_', every argument by reference,
+// CHARACTER lengths appended as size_t -- amdflang's external convention).
+//
+// Coherence model (the "device mirror" keyed by COMMON-block address):
+//   * MGCM_AMD_BIND(name, array, count, isStatic) registers a host array -- a COMMON-block member
+//     of DYNVARS.h / GRID.h / SURFACE.h / FFIELDS.h / CG2D.h / GMREDI.h -- under the device
+//     field of the same name;
+//   * static arrays (grid metrics, masks that never change) are uploaded once, by
+//     MGCM_AMD_INIT;
+//   * around every routine drop-in (DYNAMICS_AMD, ...) the bound state arrays are uploaded
+//     before and downloaded after, so the host copy stays authoritative between calls and
+//     any host routine that is not shadowed (LOAD_FIELDS_DRIVER, UPDATE_R_STAR, MONITOR,
+//     pickup I/O) sees and produces ordinary COMMON-block data.
+// The copies are PCIe traffic around each routine; the resident, graph-captured path
+// (mgcm_forward_step) is the performance path, and the drop-ins are its parity/adoption
+// path: the device work inside each call is the same kernels.
+//
+// Errors: no return channel exists in the reference (it prints and STOPs), so every
+// failure prints "ABNORMAL END: <routine>: <reason>" and aborts.
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/mitgcm_amd.h"
+
+namespace {
+
+struct Bound {
+  std::string name;   // device field
+  double *host;
+  long count;         // doubles moved
+  bool isStatic;
+  int stride = 1, off = 0;   // host element q*stride + off <-> device element q
+};
+
+struct FortranSide {
+  mgcm_model *m = nullptr;
+  int dims[7] = {0, 0, 0, 0, 0, 0, 0};   // sNx sNy OLx OLy Nr nSx nSy
+  std::vector<Bound> bound;
+  bool ready = false;
+};
+FortranSide g;
+
+[[noreturn]] void die(const char *where, const char *why = nullptr) {
+  fprintf(stderr, "ABNORMAL END: %s: %s\n", where, why ? why : mgcm_last_error());
+  fflush(stderr);
+  abort();
+}
+
+std::string fstr(const char *s, size_t len) {   // Fortran CHARACTER: blank padded, no NUL
+  while (len > 0 && (s[len - 1] == ' ' || s[len - 1] == '\0')) len--;
+  return std::string(s, len);
+}
+
+mgcm_model *model(const char *where) {
+  if (!g.m) die(where, "called before MGCM_AMD_SETUP");
+  return g.m;
+}
+
+void set_iter(const char *where, int myIter) {
+  if (mgcm_set_param(g.m, "myIter", (double)myIter)) die(where);
+}
+
+void upload(const char *where, bool statics) {
+  std::vector<double> tmp;
+  for (auto &b : g.bound) {
+    if (b.isStatic != statics) continue;
+    const double *src = b.host;
+    if (b.stride != 1) {
+      tmp.resize(b.count);
+      for (long q = 0; q < b.count; q++) tmp[q] = b.host[q * b.stride + b.off];
+      src = tmp.data();
+    }
+    if (mgcm_put(g.m, b.name.c_str(), src, b.count)) die(where);
+  }
+}
+
+void download(const char *where) {
+  if (mgcm_sync(g.m)) die(where);
+  std::vector<double> tmp;
+  for (auto &b : g.bound) {
+    if (b.isStatic) continue;
+    if (b.stride == 1) {
+      if (mgcm_get(g.m, b.name.c_str(), b.host, b.count)) die(where);
+      continue;
+    }
+    tmp.resize(b.count);
+    if (mgcm_get(g.m, b.name.c_str(), tmp.data(), b.count)) die(where);
+    for (long q = 0; q < b.count; q++) b.host[q * b.stride + b.off] = tmp[q];
+  }
+}
+
+// One routine drop-in: state in, the device routine, state out.
+void routine(const char *where, int (*fn)(mgcm_model *), int myIter) {
+  model(where);
+  if (!g.ready) die(where, "called before MGCM_AMD_INIT");
+  upload(where, false);
+  set_iter(where, myIter);
+  if (fn(g.m)) die(where);
+  download(where);
+}
+
+const Bound *bound_at(const double *p) {
+  for (auto &b : g.bound)
+    if (b.host == p) return &b;
+  return nullptr;
+}
+
+}  // namespace
+
+extern "C" {
+
+// --------------------------------------------------------------------- set-up
+/* The tile set of SIZE.h; nProcs = nPx*nPy and nThreads = nTx*nTy must be 1 (one host
+ * process and thread per model, SURVEY.md 8(b) "Threading").  Re-creates the model when
+ * the sizes change. */
+void mgcm_amd_setup_(const int *sNx, const int *sNy, const int *OLx, const int *OLy, const int *Nr, const int *nSx,
+                     const int *nSy, const int *nProcs, const int *nThreads) {
+  if (*nProcs != 1 || *nThreads != 1) die("MGCM_AMD_SETUP", "the drop-ins need nPx*nPy = nTx*nTy = 1");
+  const int d[7] = {*sNx, *sNy, *OLx, *OLy, *Nr, *nSx, *nSy};
+  if (g.m && memcmp(d, g.dims, sizeof d) == 0) return;
+  if (g.m) mgcm_destroy(g.m);
+  g = FortranSide{};
+  g.m = mgcm_create(d[0], d[1], d[2], d[3], d[4], d[5], d[6], 0);
+  if (!g.m) die("MGCM_AMD_SETUP");
+  memcpy(g.dims, d, sizeof d);
+}
+
+/* One run-time parameter under its PARAMS.h name (LOGICALs as 0/1, INTEGERs as reals). */
+void mgcm_amd_param_(const char *name, const double *value, size_t len) {
+  model("MGCM_AMD_PARAM");
+  const std::string n = fstr(name, len);
+  if (mgcm_set_param(g.m, n.c_str(), *value)) die("MGCM_AMD_PARAM");
+  g.ready = false;
+}
+
+/* Register a host array (a COMMON-block member) of `count` doubles as the device field
+ * `name` (same name).  1-D profiles may be shorter than the device's Nr+1 (drF(Nr)).
+ * phiRef(2*Nr+1) of set_ref_state.F is bound as the device's phiRefC = phiRef(2k). */
+void mgcm_amd_bind_(const char *name, double *array, const int *count, const int *isStatic, size_t len) {
+  model("MGCM_AMD_BIND");
+  std::string n = fstr(name, len);
+  Bound nb{n, array, *count, *isStatic != 0};
+  if (n == "phiRef") {
+    const int Nr = g.dims[4];
+    if (*count != 2 * Nr + 1) die("MGCM_AMD_BIND", "phiRef must have 2*Nr+1 entries");
+    nb.name = "phiRefC";
+    nb.count = Nr;
+    nb.stride = 2;
+    nb.off = 1;
+  }
+  const long have = mgcm_field_count(g.m, nb.name.c_str());
+  if (have < 0) die("MGCM_AMD_BIND");
+  if (nb.count < 1 || nb.count > have) {
+    fprintf(stderr, "ABNORMAL END: MGCM_AMD_BIND: %s has %ld doubles, the device field %ld\n", n.c_str(), nb.count,
+            have);
+    abort();
+  }
+  for (auto &b : g.bound)
+    if (b.name == nb.name) {
+      b = nb;
+      return;
+    }
+  g.bound.push_back(nb);
+  g.ready = false;
+}
+
+/* Upload every bound array and finish the device set-up (mgcm_init); the host state
+ * stays authoritative: anything mgcm_init derives on the device is overwritten by the
+ * next routine's upload. */
+void mgcm_amd_init_(const int *myIter) {
+  model("MGCM_AMD_INIT");
+  upload("MGCM_AMD_INIT", true);
+  upload("MGCM_AMD_INIT", false);
+  set_iter("MGCM_AMD_INIT", *myIter);
+  if (mgcm_init(g.m)) die("MGCM_AMD_INIT");
+  upload("MGCM_AMD_INIT", false);
+  if (mgcm_sync(g.m)) die("MGCM_AMD_INIT");
+  g.ready = true;
+}
+
+// ------------------------------------------------------------ routine drop-ins
+/* SUBROUTINE DO_OCEANIC_PHYS(myTime, myIter, myThid)     model/src/do_oceanic_phys.F:43 */
+void do_oceanic_phys_amd_(const double *myTime, const int *myIter, const int *myThid) {
+  (void)myTime; (void)myThid;
+  routine("DO_OCEANIC_PHYS_AMD", mgcm_oceanic_phys, *myIter);
+}
+/* SUBROUTINE THERMODYNAMICS(myTime, myIter, myThid)      model/src/thermodynamics.F:25 */
+void thermodynamics_amd_(const double *myTime, const int *myIter, const int *myThid) {
+  (void)myTime; (void)myThid;
+  routine("THERMODYNAMICS_AMD", mgcm_tracer_step, *myIter);
+}
+/* SUBROUTINE DYNAMICS(myTime, myIter, myThid)            model/src/dynamics.F:21 */
+void dynamics_amd_(const double *myTime, const int *myIter, const int *myThid) {
+  (void)myTime; (void)myThid;
+  routine("DYNAMICS_AMD", mgcm_dynamics, *myIter);
+}
+/* SUBROUTINE UPDATE_R_STAR(useLatest, myTime, myIter, myThid)   model/src/update_r_star.F:6
+ * useLatest = .TRUE. (forward_step.F:838): the new r* factors and hFac, and UPDATE_CG2D's
+ * operator (update_cg2d.F:7, forward_step.F:868) with them -- one device pass.
+ * useLatest = .FALSE. (RESET_NLFS_VARS + UPDATE_R_STAR at the start of the step,
+ * forward_step.F:469-477) restores the hFac of the previous step's end, which the mirror
+ * already holds: nothing to do. */
+void update_r_star_amd_(const int *useLatest, const double *myTime, const int *myIter, const int *myThid) {
+  (void)myTime; (void)myThid;
+  if (*useLatest) routine("UPDATE_R_STAR_AMD", mgcm_update_r_star, *myIter);
+}
+/* SUBROUTINE UPDATE_CG2D(myTime, myIter, myThid)         model/src/update_cg2d.F:7
+ * Folded into UPDATE_R_STAR_AMD(.TRUE.), which FORWARD_STEP calls just before it. */
+void update_cg2d_amd_(const double *myTime, const int *myIter, const int *myThid) {
+  (void)myTime; (void)myIter; (void)myThid;
+  model("UPDATE_CG2D_AMD");
+}
+/* SUBROUTINE CALC_R_STAR(etaFld, myTime, myIter, myThid)  model/src/calc_r_star.F:10
+ * FORWARD_STEP passes etaH (forward_step.F:976): the bound array. */
+void calc_r_star_amd_(const double *etaFld, const double *myTime, const int *myIter, const int *myThid) {
+  (void)myTime; (void)myThid;
+  const Bound *b = bound_at(etaFld);
+  if (!b || b->name != "etaH") die("CALC_R_STAR_AMD", "etaFld must be the bound etaH");
+  routine("CALC_R_STAR_AMD", mgcm_calc_r_star, *myIter);
+}
+/* SUBROUTINE SOLVE_FOR_PRESSURE(myTime, myIter, myThid)  model/src/solve_for_pressure.F:7 */
+void solve_for_pressure_amd_(const double *myTime, const int *myIter, const int *myThid) {
+  (void)myTime; (void)myThid;
+  routine("SOLVE_FOR_PRESSURE_AMD", mgcm_solve_for_pressure, *myIter);
+}
+/* SUBROUTINE MOMENTUM_CORRECTION_STEP(myTime, myIter, myThid)
+ *                                                   model/src/momentum_correction_step.F:7 */
+void momentum_correction_step_amd_(const double *myTime, const int *myIter, const int *myThid) {
+  (void)myTime; (void)myThid;
+  routine("MOMENTUM_CORRECTION_STEP_AMD", mgcm_momentum_correction_step, *myIter);
+}
+/* SUBROUTINE INTEGR_CONTINUITY(uFld, vFld, myTime, myIter, myThid)
+ *                                                   model/src/integr_continuity.F:13
+ * FORWARD_STEP passes uVel, vVel (forward_step.F:955): the bound arrays. */
+void integr_continuity_amd_(const double *uFld, const double *vFld, const double *myTime, const int *myIter,
+                            const int *myThid) {
+  (void)myTime; (void)myThid;
+  const Bound *bu = bound_at(uFld), *bv = bound_at(vFld);
+  if (!bu || !bv || bu->name != "uVel" || bv->name != "vVel")
+    die("INTEGR_CONTINUITY_AMD", "uFld, vFld must be the bound uVel, vVel");
+  routine("INTEGR_CONTINUITY_AMD", mgcm_integr_continuity, *myIter);
+}
+/* SUBROUTINE DO_FIELDS_BLOCKING_EXCHANGES(myThid)   model/src/do_fields_blocking_exchanges.F:7 */
+void do_fields_blocking_exchanges_amd_(const int *myThid) {
+  (void)myThid;
+  routine("DO_FIELDS_BLOCKING_EXCHANGES_AMD", mgcm_blocking_exchanges, (int)mgcm_get_param(model("X"), "myIter"));
+}
+
+// -------------------------------------------------- exchanges and global sums
+/* SUBROUTINE EXCH_XY_RL(phi, myThid)             eesupp/src/exch_xy_rx.template:9 */
+void exch_xy_rl_amd_(double *phi, const int *myThid) {
+  (void)myThid;
+  if (mgcm_exchange_host(model("EXCH_XY_RL_AMD"), phi, nullptr, 1, 0, 0)) die("EXCH_XY_RL_AMD");
+}
+/* SUBROUTINE EXCH_XYZ_RL(phi, myThid)            eesupp/src/exch_xyz_rx.template:8 */
+void exch_xyz_rl_amd_(double *phi, const int *myThid) {
+  (void)myThid;
+  if (mgcm_exchange_host(model("EXCH_XYZ_RL_AMD"), phi, nullptr, g.dims[4], 0, 0)) die("EXCH_XYZ_RL_AMD");
+}
+/* SUBROUTINE EXCH_UV_XY_RL(uPhi, vPhi, withSigns, myThid)   eesupp/src/exch_uv_xy_rx.template:11 */
+void exch_uv_xy_rl_amd_(double *u, double *v, const int *withSigns, const int *myThid) {
+  (void)myThid;
+  if (mgcm_exchange_host(model("EXCH_UV_XY_RL_AMD"), u, v, 1, 1, *withSigns != 0)) die("EXCH_UV_XY_RL_AMD");
+}
+/* SUBROUTINE EXCH_UV_XYZ_RL(uPhi, vPhi, withSigns, myThid)  eesupp/src/exch_uv_xyz_rx.template:12 */
+void exch_uv_xyz_rl_amd_(double *u, double *v, const int *withSigns, const int *myThid) {
+  (void)myThid;
+  if (mgcm_exchange_host(model("EXCH_UV_XYZ_RL_AMD"), u, v, g.dims[4], 1, *withSigns != 0))
+    die("EXCH_UV_XYZ_RL_AMD");
+}
+/* SUBROUTINE GLOBAL_SUM_TILE_RL(phiTile, sumPhi, myThid)    eesupp/src/global_sum_tile.F:14
+ * One process: the tile partials summed in global tile order, bi fastest, from zero
+ * (global_sum_tile.F:150-156) -- the order every device reduction of the path keeps at
+ * the tile level. */
+void global_sum_tile_rl_amd_(const double *phiTile, double *sumPhi, const int *myThid) {
+  (void)myThid;
+  model("GLOBAL_SUM_TILE_RL_AMD");
+  const int n = g.dims[5] * g.dims[6];
+  double s = 0.0;
+  for (int t = 0; t < n; t++) s = s + phiTile[t];
+  *sumPhi = s;
+}
+
+// ------------------------------------------------------------------- CG2D
+/* Registers the CG2D operator of CG2D.h (ini_cg2d.F:61-237 outputs) for CG2D_AMD; a model
+ * made by MGCM_AMD_SETUP is reused when the sizes agree (Nr taken from it). */
+void ini_cg2d_amd_(const int *sNx, const int *sNy, const int *OLx, const int *OLy, const int *nSx, const int *nSy,
+                   const double *aW2d, const double *aS2d, const double *aC2d, const double *pW, const double *pS,
+                   const double *pC, const double *cg2dNorm, const double *cg2dTolerance_sq,
+                   const int *cg2dNormaliseRHS) {
+  const int one = 1, Nr = g.m ? g.dims[4] : 1;
+  if (!(g.m && g.dims[0] == *sNx && g.dims[1] == *sNy && g.dims[2] == *OLx && g.dims[3] == *OLy &&
+        g.dims[5] == *nSx && g.dims[6] == *nSy))
+    mgcm_amd_setup_(sNx, sNy, OLx, OLy, &Nr, nSx, nSy, &one, &one);
+  const long n = mgcm_field_count(g.m, "aW2d");
+  if (mgcm_put(g.m, "aW2d", aW2d, n) || mgcm_put(g.m, "aS2d", aS2d, n) || mgcm_put(g.m, "aC2d", aC2d, n) ||
+      mgcm_put(g.m, "pW", pW, n) || mgcm_put(g.m, "pS", pS, n) || mgcm_put(g.m, "pC", pC, n) ||
+      mgcm_set_param(g.m, "cg2dNorm", *cg2dNorm) || mgcm_set_param(g.m, "cg2dTolerance_sq", *cg2dTolerance_sq) ||
+      mgcm_set_param(g.m, "cg2dNormaliseRHS", (double)*cg2dNormaliseRHS))
+    die("INI_CG2D_AMD");
+  if (!g.ready) {
+    if (mgcm_init(g.m)) die("INI_CG2D_AMD");
+    g.ready = true;
+  }
+}
+
+/* SUBROUTINE CG2D(cg2d_b, cg2d_x, firstResidual, minResidualSq, lastResidual, numIters,
+ *                 nIterMin, myThid)                        model/src/cg2d.F:13-17 */
+void cg2d_amd_(double *cg2d_b, double *cg2d_x, double *firstResidual, double *minResidualSq, double *lastResidual,
+               int *numIters, int *nIterMin, const int *myThid) {
+  (void)myThid;
+  if (!g.m || !g.ready) die("CG2D_AMD", "called before INI_CG2D_AMD");
+  if (mgcm_cg2d(g.m, cg2d_b, cg2d_x, firstResidual, minResidualSq, lastResidual, numIters, nIterMin)) die("CG2D_AMD");
+}
+
+}  // extern "C"

@@ -919,14 +919,6 @@ __global__ void __launch_bounds__(256) k_exchange(Dims d, double *a, const long 
   a[dt * lvl + (long)k * d.n2 + dl] = a[st * lvl + (long)k * d.n2 + sl];
 }
 
-// After CG2D: EXCH_XY_RL(cg2d_x) (solve_for_pressure.F:316) is done by k_exchange on
-// cg2d_x; then etaN = recip_Bo * cg2d_x (solve_for_pressure.F:377-385).
-__global__ void __launch_bounds__(256) k_eta_update(Dims d, Fields f) {
-  const long q = (long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (q >= d.n2 * d.nTiles) return;
-  f.etaN[q] = f.recip_Bo[q] * f.cg2d_x[q];
-}
-
 // MOMENTUM_CORRECTION_STEP over i=2-OLx..sNx+OLx, j=2-OLy..sNy+OLy, all k.
 __global__ void __launch_bounds__(256) k_correction(Dims d, Params p, Fields f) {
   MG_PLANE(2 - d.OLx, d.nx - 1, 2 - d.OLy, d.ny - 1, tz)
@@ -946,65 +938,6 @@ __global__ void __launch_bounds__(256) k_correction(Dims d, Params p, Fields f) 
     f.uVel[q3] = (f.gU[q3] + p.deltaTMom * gU_dpx) * mW;
     f.vVel[q3] = (f.gV[q3] + p.deltaTMom * gV_dpy) * mS;
   }
-}
-
-// INTEGR_CONTINUITY -> INTEGRATE_FOR_W, interior columns, k = Nr..1.
-__global__ void __launch_bounds__(256) k_continuity(Dims d, Fields f) {
-  MG_PLANE(1, d.sNx, 1, d.sNy, tz)
-  const int t = d.t0 + tz;
-  if (i > d.sNx || j > d.sNy) return;
-  const long q = MG_I2(d, i, j, t);
-  double wBelow = 0.0;
-  for (int k = d.Nr; k >= 1; k--) {
-    const double drF = f.drF[k - 1];
-    const double uT1 = f.uVel[MG_I3(d, i + 1, j, k, t)] * f.dyG[MG_I2(d, i + 1, j, t)] * drF * f.hFacW[MG_I3(d, i + 1, j, k, t)];
-    const double uT0 = f.uVel[MG_I3(d, i, j, k, t)] * f.dyG[q] * drF * f.hFacW[MG_I3(d, i, j, k, t)];
-    const double vT1 = f.vVel[MG_I3(d, i, j + 1, k, t)] * f.dxG[MG_I2(d, i, j + 1, t)] * drF * f.hFacS[MG_I3(d, i, j + 1, k, t)];
-    const double vT0 = f.vVel[MG_I3(d, i, j, k, t)] * f.dxG[q] * drF * f.hFacS[MG_I3(d, i, j, k, t)];
-    const double conv2d = -(uT1 - uT0 + vT1 - vT0);
-    double w;
-    if (k == d.Nr) w = conv2d * f.recip_rA[q] * f.maskC[MG_I3(d, i, j, k, t)];
-    else w = (wBelow + conv2d * f.recip_rA[q]) * f.maskC[MG_I3(d, i, j, k, t)];
-    f.wVel[MG_I3(d, i, j, k, t)] = w;
-    wBelow = w;
-  }
-}
-
-// INTEGR_CONTINUITY with exactConserv (integr_continuity.F:66-150, myIter > nIter0,
-// no fresh-water flux): hDivFlow summed k = 1..Nr, dEtaHdt = -hDivFlow/rA,
-// etaN = etaH + implicDiv2Dflow*dEtaHdt*deltaTFreeSurf; then INTEGRATE_FOR_W as k_continuity.
-__global__ void __launch_bounds__(256) k_continuity_ec(Dims d, Params p, Fields f) {
-  MG_PLANE(1, d.sNx, 1, d.sNy, tz)
-  const int t = d.t0 + tz;
-  if (i > d.sNx || j > d.sNy) return;
-  const long q = MG_I2(d, i, j, t);
-  auto div = [&](int k) {
-    const double drF = f.drF[k - 1];
-    const double uT1 = f.uVel[MG_I3(d, i + 1, j, k, t)] * f.dyG[MG_I2(d, i + 1, j, t)] * drF * f.hFacW[MG_I3(d, i + 1, j, k, t)];
-    const double uT0 = f.uVel[MG_I3(d, i, j, k, t)] * f.dyG[q] * drF * f.hFacW[MG_I3(d, i, j, k, t)];
-    const double vT1 = f.vVel[MG_I3(d, i, j + 1, k, t)] * f.dxG[MG_I2(d, i, j + 1, t)] * drF * f.hFacS[MG_I3(d, i, j + 1, k, t)];
-    const double vT0 = f.vVel[MG_I3(d, i, j, k, t)] * f.dxG[q] * drF * f.hFacS[MG_I3(d, i, j, k, t)];
-    return uT1 - uT0 + vT1 - vT0;
-  };
-  double hDiv = 0.0;
-  for (int k = 1; k <= d.Nr; k++) hDiv = hDiv + f.maskC[MG_I3(d, i, j, k, t)] * div(k);
-  const double facEmP = p.useRealFreshWaterFlux ? 1.0 / p.rhoConst : 0.0;
-  const double dEtaHdt = -(hDiv * f.recip_rA[q]) - facEmP * f.EmPmR[q];
-  f.etaN[q] = f.etaH[q] + p.implicDiv2DFlow * dEtaHdt * p.deltaTFreeSurf;
-  double wBelow = 0.0;
-  for (int k = d.Nr; k >= 1; k--) {
-    const double conv2d = -div(k);
-    double w;
-    if (k == d.Nr) w = conv2d * f.recip_rA[q] * f.maskC[MG_I3(d, i, j, k, t)];
-    else w = (wBelow + conv2d * f.recip_rA[q]) * f.maskC[MG_I3(d, i, j, k, t)];
-    f.wVel[MG_I3(d, i, j, k, t)] = w;
-    wBelow = w;
-  }
-}
-
-__global__ void __launch_bounds__(256) k_copy(double *dst, const double *src, long n) {
-  const long q = (long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (q < n) dst[q] = src[q];
 }
 
 // DO_FIELDS_BLOCKING_EXCHANGES in one launch: up to MG_XMAX fields of nz[f] levels
@@ -1081,6 +1014,8 @@ __global__ void __launch_bounds__(256) k_exch_etaH(Dims d, Params p, Fields f, c
 // atInit: the INTEGR_CONTINUITY call of INITIALISE_VARIA (myIter = nIter0): no
 // correction (uVel, vVel as they are), dEtaHdt / PmEpR per integr_continuity.F:117-152,
 // no eta update (cg2d_b = etaN, so k_exch_etaH makes etaH = etaN: UPDATE_ETAH).
+// atInit = 2: INTEGR_CONTINUITY alone (the routine-level C-ABI, after a separate
+// MOMENTUM_CORRECTION_STEP): divergence of uVel, vVel as they are, stepping formulas.
 // r* (select_rStar > 0): w includes -rStarDhDt*drF*h0FacC (integrate_for_w.F:117-140).
 __global__ void __launch_bounds__(256) k_corr_cont(Dims d, Params p, Fields f, int atInit) {
   __shared__ double sDiv[256], sMask[256], sH0[256];
@@ -1088,7 +1023,7 @@ __global__ void __launch_bounds__(256) k_corr_cont(Dims d, Params p, Fields f, i
   const int k = kk + 1, me = kk * NC_ + cc;
   const long q = MG_I2(d, i, j, t);
   const bool rstar = p.nonlinFreeSurf > 0 && p.select_rStar != 0;
-  if (valid && k <= d.Nr && atInit) {
+  if (valid && k <= d.Nr && atInit != 0) {   // divergence of the velocities already in uVel, vVel
     const double drF = f.drF[k - 1];
     const double u0 = f.uVel[MG_I3(d, i, j, k, t)], u1 = f.uVel[MG_I3(d, i + 1, j, k, t)];
     const double v0 = f.vVel[MG_I3(d, i, j, k, t)], v1 = f.vVel[MG_I3(d, i, j + 1, k, t)];
@@ -1139,13 +1074,13 @@ __global__ void __launch_bounds__(256) k_corr_cont(Dims d, Params p, Fields f, i
       double hDiv = 0.0;
       for (int k2 = 1; k2 <= d.Nr; k2++) hDiv = hDiv + sMask[(k2 - 1) * NC_ + cc] * sDiv[(k2 - 1) * NC_ + cc];
       double dEtaHdt;
-      if (atInit && p.nIter0 != 0 && p.useRealFreshWaterFlux) {
+      if (atInit == 1 && p.nIter0 != 0 && p.useRealFreshWaterFlux) {
         // integr_continuity.F:117-136: PmEpR consistent with the pickup's dEtaHdt
         dEtaHdt = f.dEtaHdt[q];
         double pm = dEtaHdt + hDiv * f.recip_rA[q];
         f.PmEpR[q] = pm * p.rhoConst;
         f.cg2d_b[q] = f.etaN[q];
-      } else if (atInit) {
+      } else if (atInit == 1) {
         dEtaHdt = -(hDiv * f.recip_rA[q]);
         if (f.PmEpR) f.PmEpR[q] = 0.0;
         f.cg2d_b[q] = f.etaN[q];
@@ -1285,32 +1220,9 @@ hipError_t launch_exchange(const Dims &d, double *a, const long *map, int nHalo,
   return hipGetLastError();
 }
 
-hipError_t launch_eta_update(const Dims &d, const Fields &f, hipStream_t s) {
-  const long n = d.n2 * d.nTiles;
-  hipLaunchKernelGGL(k_eta_update, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, d, f);
-  return hipGetLastError();
-}
-
 hipError_t launch_correction(const Dims &d, const Params &p, const Fields &f, hipStream_t s) {
   const dim3 blk(MG_PLANE_THREADS), grd(mg_plane_blocks(d.nx - 1, d.ny - 1, d.nT));
   hipLaunchKernelGGL(k_correction, grd, blk, 0, s, d, p, f);
-  return hipGetLastError();
-}
-
-hipError_t launch_continuity(const Dims &d, const Fields &f, hipStream_t s) {
-  const dim3 blk(MG_PLANE_THREADS), grd(mg_plane_blocks(d.sNx, d.sNy, d.nT));
-  hipLaunchKernelGGL(k_continuity, grd, blk, 0, s, d, f);
-  return hipGetLastError();
-}
-
-hipError_t launch_continuity_ec(const Dims &d, const Params &p, const Fields &f, hipStream_t s) {
-  const dim3 blk(MG_PLANE_THREADS), grd(mg_plane_blocks(d.sNx, d.sNy, d.nT));
-  hipLaunchKernelGGL(k_continuity_ec, grd, blk, 0, s, d, p, f);
-  return hipGetLastError();
-}
-
-hipError_t launch_copy(double *dst, const double *src, long n, hipStream_t s) {
-  hipLaunchKernelGGL(k_copy, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, dst, src, n);
   return hipGetLastError();
 }
 

@@ -33,9 +33,7 @@ hipError_t launch_cg2d_blk2(const Dims &, const Params &, const Fields &, const 
                             SolveRecord *, int *, hipStream_t);
 int cg2d_block_max_points();
 hipError_t launch_exchange(const Dims &, double *, const long *, int, int, hipStream_t);
-hipError_t launch_eta_update(const Dims &, const Fields &, hipStream_t);
 hipError_t launch_correction(const Dims &, const Params &, const Fields &, hipStream_t);
-hipError_t launch_continuity(const Dims &, const Fields &, hipStream_t);
 hipError_t launch_bump_counter(int *, int, hipStream_t);
 hipError_t launch_exchange_multi(const Dims &, const XFields &, const long *, int, int *, hipStream_t);
 hipError_t launch_exchange_uv(const Dims &, double *, double *, const long *, int, int, int, hipStream_t);
@@ -46,8 +44,6 @@ hipError_t launch_update_r_star_cg2d(const Dims &, const Params &, const Fields 
 hipError_t launch_halo_pack(const Dims &, const XFields &, const long *, long, double *, int, hipStream_t);
 hipError_t launch_oceanic_phys(const Dims &, const Params &, const Fields &, const int *, hipStream_t);
 hipError_t launch_tracer_step(const Dims &, const Params &, const Fields &, const TracerArgs &, const int *, hipStream_t);
-hipError_t launch_continuity_ec(const Dims &, const Params &, const Fields &, hipStream_t);
-hipError_t launch_copy(double *, const double *, long, hipStream_t);
 int cg2d_mwg_geometry(int *, int *, int *);
 hipError_t launch_cg2d_mwg(const Dims &, const Params &, const Fields &, const MwgTables &, int, SolveRecord *, int *,
                            hipStream_t);
@@ -177,6 +173,9 @@ struct mgcm_model {
   long *d_uvAll[2] = {nullptr, nullptr};
   int nUvUAll[2] = {0, 0}, nUvVAll[2] = {0, 0};
   int *d_tileInfo = nullptr;
+  // device scratch of mgcm_exchange_host (EXCH_*_RL on caller arrays)
+  double *exchBuf[2] = {nullptr, nullptr};
+  long exchCap = 0;
   // hipGraphs of two FORWARD_STEPs, one per theta/salt ping-pong parity
   bool useGraph = true;
   hipGraphExec_t graphExec[4] = {nullptr, nullptr, nullptr, nullptr};
@@ -742,6 +741,8 @@ void mgcm_destroy(mgcm_model *m) {
   if (m->d_nbx) hipFree(m->d_nbx);
   if (m->d_blkx) hipFree(m->d_blkx);
   if (m->d_ctr) hipFree(m->d_ctr);
+  for (auto &q : m->exchBuf)
+    if (q) hipFree(q);
   if (m->d_rec) hipFree(m->d_rec);
   for (void *q : m->mwgAllocs) hipFree(q);
   if (m->ownStream) hipStreamDestroy(m->ownStream);
@@ -1084,12 +1085,15 @@ int mgcm_thermodynamics(mgcm_model *m) {
   return tracers_on(m, m->stream);
 }
 
+// The routine-level ops run the same kernels as one_step, split at the reference's
+// routine boundaries (forward_step.F:925-976), so a host that calls them in FORWARD_STEP
+// order reproduces mgcm_forward_step bit for bit.
 static int solve_impl(mgcm_model *m) {
   TIMED(K_RHS, launch_sfp_rhs(m->d, m->p, m->f, m->stream));
   const int nIterMin = m->p.cg2dUseMinResSol - 1;
   TIMED(K_CG2D, launch_cg2d(m, m->p.cg2dMaxIters, nIterMin));
-  TIMED(K_EXCH, launch_exchange(m->d, m->f.cg2d_x, m->d_halo, m->nHalo, 1, m->stream));
-  TIMED(K_ETA, launch_eta_update(m->d, m->f, m->stream));
+  // EXCH_XY_RL(cg2d_x) + etaN = recip_Bo*cg2d_x (solve_for_pressure.F:309-330)
+  TIMED(K_ETA, launch_exch_eta(m->d, m->p, m->f, m->d_srcOf, false, 0, m->stream));
   return 0;
 }
 
@@ -1106,31 +1110,97 @@ int mgcm_momentum_correction_step(mgcm_model *m) {
 
 int mgcm_integr_continuity(mgcm_model *m) {
   if (check_ready(m)) return -1;
-  if (m->p.exactConserv) {
-    // integr_continuity.F:66-150 + EXCH etaN + UPDATE_ETAH (update_etah.F:55-73)
-    TIMED(K_CONT, launch_continuity_ec(m->d, m->p, m->f, m->stream));
-    TIMED(K_EXCH, launch_exchange(m->d, m->f.etaN, m->d_halo, m->nHalo, 1, m->stream));
-    TIMED(K_ETA, launch_copy(m->f.etaH, m->f.etaN, m->d.n2 * m->d.nTiles, m->stream));
-  } else {
-    TIMED(K_CONT, launch_continuity(m->d, m->f, m->stream));
-  }
+  // integr_continuity.F:66-310 (exactConserv eta, INTEGRATE_FOR_W incl. r*) from the corrected
+  // uVel, vVel; :324-350 EXCH etaN + UPDATE_ETAH (PmEpR under real fresh water)
+  TIMED(K_CONT, launch_corr_cont(m->d, m->p, m->f, 2, m->stream));
+  if (m->p.exactConserv) TIMED(K_ETA, launch_exch_eta(m->d, m->p, m->f, m->d_srcOf, true, 0, m->stream));
   return 0;
 }
+
+int mgcm_update_r_star(mgcm_model *m) {
+  if (check_ready(m)) return -1;
+  // UPDATE_R_STAR(.TRUE.) + UPDATE_CG2D (forward_step.F:829-877)
+  if (m->p.nonlinFreeSurf > 0) TIMED(K_RSTAR, update_r_star_cg2d(m));
+  return 0;
+}
+
+int mgcm_calc_r_star(mgcm_model *m) {
+  if (check_ready(m)) return -1;
+  // CALC_R_STAR(etaH) (forward_step.F:965-977)
+  if (m->p.nonlinFreeSurf > 0) TIMED(K_RSTAR, calc_r_star(m));
+  return 0;
+}
+
+static XFields blocking_fields(const mgcm_model *m);
 
 int mgcm_blocking_exchanges(mgcm_model *m) {
   if (check_ready(m)) return -1;
-  // do_fields_blocking_exchanges.F:54-97: uVel, vVel, wVel, theta (salt is not
-  // stepped by the supported configs, its halo is unchanged)
-  TIMED(K_EXCH, exchange_uv(m, m->f.uVel, m->f.vVel, m->d.Nr, true) ? hipErrorUnknown : hipSuccess);
-  TIMED(K_EXCH, launch_exchange(m->d, m->f.wVel, m->d_halo, m->nHalo, m->d.Nr, m->stream));
-  if (m->p.tempStepping)
-    TIMED(K_EXCH, launch_exchange(m->d, m->f.theta, m->d_halo, m->nHalo, m->d.Nr, m->stream));
-  if (m->p.saltStepping)
-    TIMED(K_EXCH, launch_exchange(m->d, m->f.salt, m->d_halo, m->nHalo, m->d.Nr, m->stream));
+  // DO_FIELDS_BLOCKING_EXCHANGES (do_fields_blocking_exchanges.F:54-97): the set FORWARD_STEP
+  // exchanges (one_step), without advancing the step counter
+  if (m->uvMap) TIMED(K_EXCH, exchange_uv(m, m->f.uVel, m->f.vVel, m->d.Nr, true) ? hipErrorUnknown : hipSuccess);
+  TIMED(K_EXCH, launch_exchange_multi(m->d, blocking_fields(m), m->d_halo, m->nHalo, nullptr, m->stream));
   return 0;
 }
 
-// DO_FIELDS_BLOCKING_EXCHANGES field set (do_fields_blocking_exchanges.F:54-97).
+int mgcm_oceanic_phys(mgcm_model *m) {
+  if (check_ready(m)) return -1;
+  TIMED(K_PHYS, launch_oceanic_phys(m->d, m->p, m->f, m->d_ctr, m->stream));
+  return 0;
+}
+
+int mgcm_tracer_step(mgcm_model *m) {
+  if (check_ready(m)) return -1;
+  return tracers_on(m, m->stream);
+}
+
+// EXCH_XY_RL / EXCH_XYZ_RL / EXCH_UV_*_RL on a caller's (host) array: staged through a
+// device scratch pair, exchanged with the model's maps, copied back.
+static int exch_scratch(mgcm_model *m, int nz) {
+  const long need = (long)nz * m->d.n2 * m->d.nTiles;
+  if (need <= m->exchCap) return 0;
+  for (auto &q : m->exchBuf)
+    if (q) { hipFree(q); q = nullptr; }
+  HIPCHK(hipMalloc(&m->exchBuf[0], need * sizeof(double)));
+  HIPCHK(hipMalloc(&m->exchBuf[1], need * sizeof(double)));
+  m->exchCap = need;
+  return 0;
+}
+
+int mgcm_exchange_host(mgcm_model *m, double *u, double *v, int nz, int vector, int withSigns) {
+  // needs only the halo maps (usable before mgcm_init: the reference exchanges while
+  // initialising, e.g. INI_FIELDS)
+  if (!m->d_srcOf && upload_halo(m)) return -1;
+  if (nz < 1 || nz > m->d.Nr) return set_err("mgcm_exchange_host: nz = %d outside 1..%d", nz, m->d.Nr);
+  if (vector && !v) return set_err("mgcm_exchange_host: a vector exchange needs both components");
+  if (exch_scratch(m, nz)) return -1;
+  HIPCHK(hipSetDevice(m->device));
+  const size_t bytes = (size_t)nz * m->d.n2 * m->d.nTiles * sizeof(double);
+  double *host[2] = {u, v};
+  for (int c = 0; c < 2; c++)
+    if (host[c]) HIPCHK(hipMemcpyAsync(m->exchBuf[c], host[c], bytes, hipMemcpyHostToDevice, m->stream));
+  if (vector) {
+    if (exchange_uv(m, m->exchBuf[0], m->exchBuf[1], nz, withSigns != 0)) return -1;
+  } else {
+    for (int c = 0; c < 2; c++)
+      if (host[c]) HIPCHK(launch_exchange(m->d, m->exchBuf[c], m->d_halo, m->nHalo, nz, m->stream));
+  }
+  for (int c = 0; c < 2; c++)
+    if (host[c]) HIPCHK(hipMemcpyAsync(host[c], m->exchBuf[c], bytes, hipMemcpyDeviceToHost, m->stream));
+  HIPCHK(hipStreamSynchronize(m->stream));
+  return 0;
+}
+
+const char *mgcm_param_name(int i) {
+  const int n = (int)(sizeof(PARAMS) / sizeof(PARAMS[0]));
+  return (i >= 0 && i < n) ? PARAMS[i].name : nullptr;
+}
+
+long mgcm_field_count(mgcm_model *m, const char *name) {
+  const FieldDesc *fd = find_field(name);
+  if (!fd) { set_err("mgcm_field_count: unknown field %s", name); return -1; }
+  return field_count(m, fd->kind);
+}
+
 static XFields blocking_fields(const mgcm_model *m) {
   XFields x{};
   // do_fields_blocking_exchanges.F:54-97 (+ EXCH_UV_DGRID of uVelD/vVelD with the CD scheme,
@@ -1472,51 +1542,6 @@ int mgcm_cg2d(mgcm_model *m, double *cg2d_b, double *cg2d_x, double *firstResidu
   *numIters = r.numIters;
   *nIterMin = r.nIterMin;
   return 0;
-}
-
-// --------------------------------------------------- Fortran drop-in (CG2D)
-static mgcm_model *g_fortran_model = nullptr;
-
-static void fortran_die(const char *where) {
-  fprintf(stderr, "ABNORMAL END: %s: %s\n", where, g_err.c_str());
-  fflush(stderr);
-  abort();
-}
-
-void ini_cg2d_amd_(const int *sNx, const int *sNy, const int *OLx, const int *OLy, const int *nSx, const int *nSy,
-                   const double *aW2d, const double *aS2d, const double *aC2d, const double *pW, const double *pS,
-                   const double *pC, const double *cg2dNorm, const double *cg2dTolerance_sq,
-                   const int *cg2dNormaliseRHS) {
-  mgcm_model *m = g_fortran_model;
-  if (m && (m->d.sNx != *sNx || m->d.sNy != *sNy || m->d.OLx != *OLx || m->d.OLy != *OLy || m->d.nSx != *nSx ||
-            m->d.nSy != *nSy)) {
-    mgcm_destroy(m);
-    m = nullptr;
-  }
-  if (!m) {
-    m = mgcm_create(*sNx, *sNy, *OLx, *OLy, 1, *nSx, *nSy, 0);
-    if (!m) fortran_die("INI_CG2D_AMD");
-    g_fortran_model = m;
-  }
-  const long n = m->d.n2 * m->d.nTiles;
-  if (mgcm_put(m, "aW2d", aW2d, n) || mgcm_put(m, "aS2d", aS2d, n) || mgcm_put(m, "aC2d", aC2d, n) ||
-      mgcm_put(m, "pW", pW, n) || mgcm_put(m, "pS", pS, n) || mgcm_put(m, "pC", pC, n))
-    fortran_die("INI_CG2D_AMD");
-  m->p.cg2dNorm = *cg2dNorm;
-  m->p.cg2dTolerance_sq = *cg2dTolerance_sq;
-  m->p.cg2dNormaliseRHS = *cg2dNormaliseRHS;
-  if (mgcm_init(m)) fortran_die("INI_CG2D_AMD");
-}
-
-void cg2d_amd_(double *cg2d_b, double *cg2d_x, double *firstResidual, double *minResidualSq, double *lastResidual,
-               int *numIters, int *nIterMin, const int *myThid) {
-  (void)myThid;
-  if (!g_fortran_model) {
-    g_err = "CG2D_AMD called before INI_CG2D_AMD";
-    fortran_die("CG2D_AMD");
-  }
-  if (mgcm_cg2d(g_fortran_model, cg2d_b, cg2d_x, firstResidual, minResidualSq, lastResidual, numIters, nIterMin))
-    fortran_die("CG2D_AMD");
 }
 
 }  // extern "C"

@@ -1,0 +1,186 @@
+! fhost.F90 -- a Fortran host that drives a FORWARD_STEP through the routine drop-ins.
+!
+! It plays the role of the reference's model/src/forward_step.F with the MODS shims of
+! mitgcm_amd/fortran/mods in place: the host owns every array (declared, like the
+! COMMON-block members, as halo-inclusive (1-OLx:sNx+OLx, 1-OLy:sNy+OLy[, Nr], nSx, nSy)
+! storage), registers them with MGCM_AMD_BIND, and calls, per step, in forward_step.F's
+! order (staggerTimeStep = F):
+!   LOAD_FIELDS_DRIVER -> EXTERNAL_FIELDS_LOAD (host, restated below)   forward_step.F:542
+!   DO_OCEANIC_PHYS                                                     forward_step.F:656
+!   THERMODYNAMICS                                                      forward_step.F:732
+!   DYNAMICS                                                            forward_step.F:791
+!   UPDATE_R_STAR(.TRUE.), UPDATE_CG2D  (r*; no-ops otherwise)          forward_step.F:838,868
+!   SOLVE_FOR_PRESSURE                                                  forward_step.F:925
+!   MOMENTUM_CORRECTION_STEP                                            forward_step.F:941
+!   INTEGR_CONTINUITY(uVel, vVel)                                       forward_step.F:955
+!   CALC_R_STAR(etaH)                   (r*; no-op otherwise)           forward_step.F:976
+!   DO_FIELDS_BLOCKING_EXCHANGES                                        forward_step.F:1120
+! then checks EXCH_XYZ_RL, EXCH_UV_XYZ_RL, EXCH_XY_RL and GLOBAL_SUM_TILE_RL on host arrays.
+!
+! Input (stream, native endian, written by tests/test_gpu_fortran.py): sizes, parameters
+! (name, value), fields (name, count, isStatic, values), the forcing records; output: every
+! non-static field after the steps, plus the exchange / global-sum checks.
+program fhost
+  implicit none
+  type field
+    character(len=32) :: name
+    integer :: count, isStatic
+    real(8), allocatable :: a(:)
+  end type
+  integer :: sNx, sNy, OLx, OLy, Nr, nSx, nSy, nParams, nFields, nSteps, nIter0, nRec, periodic
+  integer :: u, i, k, step, myIter, myThid, one, withSigns, n2, n3, iT, iU, iV, iEtaH
+  real(8) :: myTime, deltaTClock, forcPeriod, forcCycle, v, sumPhi
+  character(len=32) :: pname
+  character(len=512) :: dir
+  type(field), allocatable :: f(:)
+  real(8), allocatable :: rec(:,:,:), tmp(:), tmpv(:), tile(:)
+  call get_command_argument(1, dir)
+  open(newunit=u, file=trim(dir)//'/fhost_in.bin', access='stream', form='unformatted', status='old')
+  read(u) sNx, sNy, OLx, OLy, Nr, nSx, nSy, nParams, nFields, nSteps, nIter0, nRec, periodic
+  read(u) deltaTClock, forcPeriod, forcCycle
+  one = 1
+  myThid = 1
+  call MGCM_AMD_SETUP(sNx, sNy, OLx, OLy, Nr, nSx, nSy, one, one)
+  do i = 1, nParams
+    read(u) pname, v
+    call MGCM_AMD_PARAM(trim(pname), v)
+  end do
+  allocate(f(nFields))
+  do i = 1, nFields
+    read(u) f(i)%name, f(i)%count, f(i)%isStatic
+    allocate(f(i)%a(f(i)%count))
+    read(u) f(i)%a
+  end do
+  n2 = (sNx + 2*OLx) * (sNy + 2*OLy) * nSx * nSy
+  n3 = n2 * Nr
+  if (periodic /= 0) then
+    allocate(rec(n2, nRec, 6))
+    read(u) rec
+  end if
+  close(u)
+  do i = 1, nFields
+    call MGCM_AMD_BIND(trim(f(i)%name), f(i)%a, f(i)%count, f(i)%isStatic)
+  end do
+  call MGCM_AMD_INIT(nIter0)
+  iT = find('theta')
+  iU = find('uVel')
+  iV = find('vVel')
+  iEtaH = find('etaH')
+  do step = 1, nSteps
+    myIter = nIter0 + step - 1
+    myTime = dble(myIter) * deltaTClock
+    if (periodic /= 0) call external_fields_load(myIter)
+    call DO_OCEANIC_PHYS_AMD(myTime, myIter, myThid)
+    call THERMODYNAMICS_AMD(myTime, myIter, myThid)
+    call DYNAMICS_AMD(myTime, myIter, myThid)
+    call UPDATE_R_STAR_AMD(one, myTime, myIter, myThid)
+    call UPDATE_CG2D_AMD(myTime, myIter, myThid)
+    call SOLVE_FOR_PRESSURE_AMD(myTime, myIter, myThid)
+    call MOMENTUM_CORRECTION_STEP_AMD(myTime, myIter, myThid)
+    call INTEGR_CONTINUITY_AMD(f(iU)%a, f(iV)%a, myTime, myIter, myThid)
+    call CALC_R_STAR_AMD(f(iEtaH)%a, myTime, myIter, myThid)
+    call DO_FIELDS_BLOCKING_EXCHANGES_AMD(myThid)
+  end do
+  ! exchanges on host copies whose halos were overwritten with a marker
+  allocate(tmp(n3), tmpv(n3), tile(nSx*nSy))
+  tmp = f(iT)%a
+  call poison(tmp, Nr)
+  call EXCH_XYZ_RL_AMD(tmp, myThid)
+  open(newunit=u, file=trim(dir)//'/fhost_out.bin', access='stream', form='unformatted', status='replace')
+  write(u) tmp
+  tmp = f(iU)%a
+  tmpv = f(iV)%a
+  call poison(tmp, Nr)
+  call poison(tmpv, Nr)
+  withSigns = 1
+  call EXCH_UV_XYZ_RL_AMD(tmp, tmpv, withSigns, myThid)
+  write(u) tmp, tmpv
+  call level1(f(iT)%a, tmp)
+  call poison(tmp, 1)
+  call EXCH_XY_RL_AMD(tmp, myThid)
+  write(u) tmp(1:n2)
+  ! GLOBAL_SUM_TILE_RL of per-tile interior sums of theta(k=1)
+  do k = 1, nSx*nSy
+    tile(k) = tile_sum(f(iT)%a, k)
+  end do
+  call GLOBAL_SUM_TILE_RL_AMD(tile, sumPhi, myThid)
+  write(u) tile, sumPhi
+  do i = 1, nFields
+    if (f(i)%isStatic == 0) write(u) f(i)%name, f(i)%count, f(i)%a
+  end do
+  close(u)
+  print '(A,I4,A)', ' fhost: ', nSteps, ' steps through the drop-ins done'
+
+contains
+
+  integer function find(name)
+    character(len=*), intent(in) :: name
+    integer :: q
+    do q = 1, nFields
+      if (trim(f(q)%name) == name) then
+        find = q
+        return
+      end if
+    end do
+    print *, 'fhost: no field ', name
+    stop 1
+  end function
+
+  ! EXTERNAL_FIELDS_LOAD (model/src/external_fields_load.F:7) for periodic monthly records:
+  ! the two records bracketing myTime and their linear weights
+  subroutine external_fields_load(it)
+    integer, intent(in) :: it
+    integer :: nbRec, tRec1, tRec2, vv, q, dst
+    real(8) :: currentTime, locTime, tmpTime, aW, bW
+    character(len=6), parameter :: names(6) = ['SST   ', 'SSS   ', 'fu    ', 'fv    ', 'Qnet  ', 'EmPmR ']
+    currentTime = dble(it) * deltaTClock
+    nbRec = nint(forcCycle / forcPeriod)
+    locTime = currentTime - forcPeriod * 0.5d0 + forcCycle * dble(2 - nint(currentTime / forcCycle))
+    tmpTime = mod(locTime, forcCycle)
+    tRec1 = 1 + int(tmpTime / forcPeriod)
+    tRec2 = 1 + mod(tRec1, nbRec)
+    aW = (tmpTime - forcPeriod * dble(tRec1 - 1)) / forcPeriod
+    bW = 1.0d0 - aW
+    do vv = 1, 6
+      dst = find(trim(names(vv)))
+      do q = 1, n2
+        f(dst)%a(q) = bW * rec(q, tRec1, vv) + aW * rec(q, tRec2, vv)
+      end do
+    end do
+  end subroutine
+
+  ! overwrite every halo point of an (nx, ny, nz, nTiles) array with a marker value
+  subroutine poison(a, nz)
+    real(8), intent(inout) :: a(1-OLx:sNx+OLx, 1-OLy:sNy+OLy, nz, nSx*nSy)
+    integer, intent(in) :: nz
+    integer :: ii, jj, kk, tt
+    do tt = 1, nSx*nSy
+      do kk = 1, nz
+        do jj = 1-OLy, sNy+OLy
+          do ii = 1-OLx, sNx+OLx
+            if (ii < 1 .or. ii > sNx .or. jj < 1 .or. jj > sNy) a(ii, jj, kk, tt) = -999.0d0
+          end do
+        end do
+      end do
+    end do
+  end subroutine
+
+  ! b(:,:,t) = a(:,:,1,t): the surface level as an EXCH_XY_RL (2-D) array
+  subroutine level1(a, b)
+    real(8), intent(in) :: a(1-OLx:sNx+OLx, 1-OLy:sNy+OLy, Nr, nSx*nSy)
+    real(8), intent(out) :: b(1-OLx:sNx+OLx, 1-OLy:sNy+OLy, nSx*nSy)
+    b(:, :, :) = a(:, :, 1, :)
+  end subroutine
+
+  real(8) function tile_sum(a, t)
+    real(8), intent(in) :: a(1-OLx:sNx+OLx, 1-OLy:sNy+OLy, Nr, nSx*nSy)
+    integer, intent(in) :: t
+    integer :: ii, jj
+    tile_sum = 0.0d0
+    do jj = 1, sNy
+      do ii = 1, sNx
+        tile_sum = tile_sum + a(ii, jj, 1, t)
+      end do
+    end do
+  end function
+end program fhost

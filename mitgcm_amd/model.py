@@ -106,6 +106,9 @@ class Model:
             return (g.Nr + 1,)
         if name in GRID_3D or name in STATE_3D:
             return (g.nTiles, g.Nr, g.ny, g.nx)
+        if name == "forcRec":   # 6 forcing fields x the device's record capacity, 2-D each
+            n = lib().mgcm_field_count(self.h, b"forcRec")
+            return (6, n // (6 * g.nTiles * g.ny * g.nx), g.nTiles, g.ny, g.nx)
         return (g.nTiles, g.ny, g.nx)
 
     def put_forcing(self, forcing):
