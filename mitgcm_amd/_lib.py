@@ -7,7 +7,8 @@ import ctypes
 import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIBPATH = os.path.join(HERE, "libmitgcm_amd.so")
+# MGCM_LIB: a diagnostic build of the same library (e.g. tools/cg_stamps.sh) -- never the default
+LIBPATH = os.environ.get("MGCM_LIB") or os.path.join(HERE, "libmitgcm_amd.so")
 _lib = None
 
 

@@ -670,6 +670,21 @@ __device__ __forceinline__ double block_max_nw(double v, double *red, int slot) 
   return row_max16(l < NW ? red[slot * 16 + l] : 0.0);
 }
 
+#ifdef MGCM_CG_STAMPS   // diagnostic build only: per-phase shader-cycle totals of one solve
+#define CG_STAMP(k)                                                                   \
+  do {                                                                                \
+    __builtin_amdgcn_sched_barrier(0);                                                \
+    unsigned long long t_;                                                            \
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");       \
+    __builtin_amdgcn_sched_barrier(0);                                                \
+    if ((k) > 0) stampAcc[(k) - 1] += t_ - stampPrev;                                 \
+    stampPrev = t_;                                                                   \
+  } while (0)
+#else
+#define CG_STAMP(k) \
+  do {              \
+  } while (0)
+#endif
 template <int BX, int BY, int NT, bool MINRES>
 __global__ void __launch_bounds__(NT) k_cg2d_bxy(Dims d, Params p, Fields f, const unsigned *__restrict__ nbx,
                                                  const int *__restrict__ blkx, int nBlk, int maxIters, int nIterMinIn,
@@ -828,6 +843,11 @@ __global__ void __launch_bounds__(NT) k_cg2d_bxy(Dims d, Params p, Fields f, con
 #pragma unroll
       for (int a = 0; a < BX; a++) e = e + q[b][a] * r[b][a];
     double eta_qrN = block_sum_nw<NW>(e, red, 0);
+#ifdef MGCM_CG_STAMPS
+    unsigned long long stampAcc[6] = {0, 0, 0, 0, 0, 0}, stampPrev = 0;
+    const unsigned long long stampT0 = __builtin_amdgcn_s_memtime(), stampR0 = __builtin_amdgcn_s_memrealtime();
+    __builtin_amdgcn_s_waitcnt(0xC07F);
+#endif
     for (int it2d = 1; it2d <= maxIters; it2d++) {
       const double cgBeta = eta_qrN / eta_qrNM1;
       eta_qrNM1 = eta_qrN;
@@ -835,7 +855,9 @@ __global__ void __launch_bounds__(NT) k_cg2d_bxy(Dims d, Params p, Fields f, con
       for (int b = 0; b < BY; b++)
 #pragma unroll
         for (int a = 0; a < BX; a++) { sv[b][a] = q[b][a] + cgBeta * sv[b][a]; s_l[cs[b][a]] = sv[b][a]; }
+      CG_STAMP(0);
       __syncthreads();
+      CG_STAMP(1);
       apply(s_l, sv, q, false);
       double aa = 0.0;
 #pragma unroll
@@ -843,7 +865,9 @@ __global__ void __launch_bounds__(NT) k_cg2d_bxy(Dims d, Params p, Fields f, con
 #pragma unroll
         for (int a = 0; a < BX; a++) aa = aa + sv[b][a] * q[b][a];
       aslot = aslot ^ 1;
+      CG_STAMP(2);
       double alpha = block_sum_nw<NW>(aa, red, aslot);
+      CG_STAMP(3);
       alpha = eta_qrN / alpha;
       double e2 = 0.0;
 #pragma unroll
@@ -856,6 +880,7 @@ __global__ void __launch_bounds__(NT) k_cg2d_bxy(Dims d, Params p, Fields f, con
           r_l[cs[b][a]] = r[b][a];
         }
       actualIts = it2d;
+      CG_STAMP(4);
       __syncthreads();
       // next iteration's q = M r and (q, r), reduced together with this iteration's r.r
       apply(r_l, r, q, true);
@@ -865,6 +890,7 @@ __global__ void __launch_bounds__(NT) k_cg2d_bxy(Dims d, Params p, Fields f, con
 #pragma unroll
         for (int a = 0; a < BX; a++) en = en + q[b][a] * r[b][a];
       block_sum2_nw<NW>(e2, en, red, 0);
+      CG_STAMP(5);
       err_sq = e2;
       eta_qrN = en;
       if (err_sq < p.cg2dTolerance_sq) break;
@@ -877,6 +903,12 @@ __global__ void __launch_bounds__(NT) k_cg2d_bxy(Dims d, Params p, Fields f, con
           for (int a = 0; a < BX; a++) xmin[b][a] = x[b][a];
       }
     }
+#ifdef MGCM_CG_STAMPS
+    if (tid == 0)
+      printf("CGSTAMP its %d total %llu real100MHz %llu | barS %llu applyA %llu sumA %llu div+upd %llu barR+applyM+sum2 %llu\n",
+             actualIts, __builtin_amdgcn_s_memtime() - stampT0, __builtin_amdgcn_s_memrealtime() - stampR0,
+             stampAcc[0], stampAcc[1], stampAcc[2], stampAcc[3], stampAcc[4]);
+#endif
   }
   if (MINRES && nIterMin >= 0 && err_sq > minResidualSq) {
 #pragma unroll
@@ -891,7 +923,7 @@ __global__ void __launch_bounds__(NT) k_cg2d_bxy(Dims d, Params p, Fields f, con
       for (int a = 0; a < BX; a++) {
         double xv = x[b][a];
         if (p.cg2dNormaliseRHS) xv = xv / rhsNorm;
-        f.cg2d_x[G[b][a]] = xv;
+        f.cg2d_x[blkx[NPT * bt + BX * b + a]] = xv;   // re-read: G is not kept live across the solve
       }
   }
   if (tid == 0) {
@@ -1178,23 +1210,46 @@ hipError_t launch_cg2d_block(const Dims &d, const Params &p, const Fields &f, co
   return hipGetLastError();
 }
 
-// 2 (i) x 4 (j) points per thread, 512 threads: up to 4096 points (90x40: 450 blocks)
-constexpr int CGX_BX = 2, CGX_BY = 4, CGX_NT = 512;
-int cg2d_bxy_geometry(int *bx, int *by, int *nt) { *bx = CGX_BX; *by = CGX_BY; *nt = CGX_NT; return 0; }
-hipError_t launch_cg2d_bxy(const Dims &d, const Params &p, const Fields &f, const unsigned *nbx, const int *blkx,
-                           int nBlk, int maxIters, int nIterMin, SolveRecord *rec, int *stepCounter, hipStream_t s) {
-  if (nBlk > CGX_NT) return hipErrorInvalidValue;
-  const size_t lds = (2 * ((size_t)CGX_BX * CGX_BY * CGX_NT + 1) + 4 * 16) * sizeof(double);
-  auto kern = nIterMin >= 0 ? k_cg2d_bxy<CGX_BX, CGX_BY, CGX_NT, true> : k_cg2d_bxy<CGX_BX, CGX_BY, CGX_NT, false>;
+// k_cg2d_bxy geometries (BX x BY points per thread, NT threads): variant v is chosen per
+// grid at set-up (model.hip build_nbr: the global lat-lon index space must tile into
+// BX x BY blocks, at most NT of them).  Fewer, fatter threads trade serial work per thread
+// for cheaper reductions and barriers (fewer waves).
+struct CgxGeom { int bx, by, nt; };
+// measured on global_ocean.90x40x15 (profiles/r02/ocean90/cg2d_geometry.txt): fatter threads
+// (3x4, 5x4, 3x8, 5x8) spill the per-point registers and run 1.5-8x slower per iteration
+static const CgxGeom CGX[] = {{2, 4, 512}, {2, 2, 1024}};
+constexpr int CGX_N = (int)(sizeof(CGX) / sizeof(CGX[0]));
+int cg2d_bxy_variants() { return CGX_N; }
+int cg2d_bxy_geometry(int v, int *bx, int *by, int *nt) {
+  if (v < 0 || v >= CGX_N) return -1;
+  *bx = CGX[v].bx; *by = CGX[v].by; *nt = CGX[v].nt;
+  return 0;
+}
+template <int BX, int BY, int NT>
+static hipError_t launch_bxy_t(const Dims &d, const Params &p, const Fields &f, const unsigned *nbx, const int *blkx,
+                               int nBlk, int maxIters, int nIterMin, SolveRecord *rec, int *stepCounter, hipStream_t s) {
+  if (nBlk > NT) return hipErrorInvalidValue;
+  const size_t lds = (2 * ((size_t)BX * BY * NT + 1) + 4 * 16) * sizeof(double);
+  auto kern = nIterMin >= 0 ? k_cg2d_bxy<BX, BY, NT, true> : k_cg2d_bxy<BX, BY, NT, false>;
   static bool attrSet[2] = {false, false};
   if (!attrSet[nIterMin >= 0]) {
     hipError_t e = hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return e;
     attrSet[nIterMin >= 0] = true;
   }
-  hipLaunchKernelGGL(kern, dim3(1), dim3(CGX_NT), lds, s, d, p, f, nbx, blkx, nBlk, maxIters, nIterMin, rec,
-                     stepCounter);
+  hipLaunchKernelGGL(kern, dim3(1), dim3(NT), lds, s, d, p, f, nbx, blkx, nBlk, maxIters, nIterMin, rec, stepCounter);
   return hipGetLastError();
+}
+hipError_t launch_cg2d_bxy(int v, const Dims &d, const Params &p, const Fields &f, const unsigned *nbx, const int *blkx,
+                           int nBlk, int maxIters, int nIterMin, SolveRecord *rec, int *stepCounter, hipStream_t s) {
+#define CGX_CASE(V, BX, BY, NT) \
+  case V: return launch_bxy_t<BX, BY, NT>(d, p, f, nbx, blkx, nBlk, maxIters, nIterMin, rec, stepCounter, s);
+  switch (v) {
+    CGX_CASE(0, 2, 4, 512)
+    CGX_CASE(1, 2, 2, 1024)
+  }
+#undef CGX_CASE
+  return hipErrorInvalidValue;
 }
 
 hipError_t launch_cg2d_blk2(const Dims &d, const Params &p, const Fields &f, const unsigned *nb4, const int *blk,

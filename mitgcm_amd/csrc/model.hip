@@ -26,9 +26,10 @@ hipError_t launch_sfp_rhs(const Dims &, const Params &, const Fields &, hipStrea
 hipError_t launch_cg2d_block(const Dims &, const Params &, const Fields &, const unsigned *, const int *, int, int, int,
                              SolveRecord *, int *, hipStream_t);
 int cg2d_block_ppt(int nPts);
-hipError_t launch_cg2d_bxy(const Dims &, const Params &, const Fields &, const unsigned *, const int *, int, int, int,
-                           SolveRecord *, int *, hipStream_t);
-int cg2d_bxy_geometry(int *, int *, int *);
+hipError_t launch_cg2d_bxy(int, const Dims &, const Params &, const Fields &, const unsigned *, const int *, int, int,
+                           int, SolveRecord *, int *, hipStream_t);
+int cg2d_bxy_geometry(int, int *, int *, int *);
+int cg2d_bxy_variants();
 hipError_t launch_cg2d_blk2(const Dims &, const Params &, const Fields &, const unsigned *, const int *, int, int, int,
                             SolveRecord *, int *, hipStream_t);
 int cg2d_block_max_points();
@@ -156,6 +157,7 @@ struct mgcm_model {
   unsigned *d_nbx = nullptr;
   int *d_blkx = nullptr;
   int nBlkX = 0;
+  int bxyVar = -1;              // k_cg2d_bxy geometry (kernels_solve.hip CGX[])
   bool latlonTopology = true;   // false once a custom halo map (e.g. EXCH2 cube) is installed
   // multi-workgroup CG2D (kernels_cg2d_mwg.hip): tables of every part, device buffers
   bool useMwg = false;
@@ -410,12 +412,23 @@ static int build_nbr(mgcm_model *m) {
     HIPCHK(hipMemcpy(m->d_blk, blk.data(), blk.size() * sizeof(int), hipMemcpyHostToDevice));
     m->nBlk = nBk;
   }
-  // BX x BY blocks (k_cg2d_bxy), same global-index construction
+  // BX x BY blocks (k_cg2d_bxy), same global-index construction; the first geometry of
+  // the preference list the grid tiles into (MGCM_CGX=v forces variant v)
   m->nBlkX = 0;
-  int BX, BY, NT;
-  cg2d_bxy_geometry(&BX, &BY, &NT);
-  const int nBx = (Nx % BX == 0 && Ny % BY == 0) ? (Nx / BX) * (Ny / BY) : 0;
-  if (m->latlonTopology && nBx > 0 && nBx <= NT && !getenv("MGCM_CG2D_NOBXY")) {
+  int BX = 0, BY = 0, NT = 0, nBx = 0;
+  m->bxyVar = -1;
+  {
+    static const int pref[] = {0, 1};
+    const char *force = getenv("MGCM_CGX");
+    for (int v : pref) {
+      if (force && atoi(force) != v) continue;
+      int bx, by, nt;
+      if (cg2d_bxy_geometry(v, &bx, &by, &nt)) continue;
+      const int n = (Nx % bx == 0 && Ny % by == 0) ? (Nx / bx) * (Ny / by) : 0;
+      if (n > 0 && n <= nt) { m->bxyVar = v; BX = bx; BY = by; NT = nt; nBx = n; break; }
+    }
+  }
+  if (m->latlonTopology && m->bxyVar >= 0 && !getenv("MGCM_CG2D_NOBXY")) {
     const int NPT = BX * BY, NB = 2 * (BX + BY);
     const unsigned Z = (unsigned)(NPT * NT);
     // LDS slot of an interior point: point-in-block major, block minor (p*NT + block),
@@ -793,6 +806,7 @@ double mgcm_get_param(mgcm_model *m, const char *name) {
   // 4: k_cg2d_mwg, 3: k_cg2d_bxy, 2: k_cg2d_blk2, 1: k_cg2d_block
   if (!strcmp(name, "cg2dKernel")) return m->useMwg ? 4.0 : m->nBlkX > 0 ? 3.0 : (m->nBlk > 0 ? 2.0 : 1.0);
   if (!strcmp(name, "cg2dParts")) return m->useMwg ? (double)m->mwg.G : 1.0;
+  if (!strcmp(name, "cg2dBxyVariant")) return (double)m->bxyVar;
   for (auto &pd : PARAMS)
     if (!strcmp(pd.name, name)) {
       const char *ptr = reinterpret_cast<const char *>(&m->p) + pd.off;
@@ -1017,7 +1031,8 @@ static hipError_t launch_cg2d(mgcm_model *m, int maxIters, int nIterMin) {
     return launch_cg2d_mwg(m->d, m->p, m->f, m->mwg, maxIters, m->d_rec, m->d_ctr + 1, m->stream);
   }
   if (m->nBlkX > 0)
-    return launch_cg2d_bxy(m->d, m->p, m->f, m->d_nbx, m->d_blkx, m->nBlkX, maxIters, nIterMin, m->d_rec, m->d_ctr + 1,
+    return launch_cg2d_bxy(m->bxyVar, m->d, m->p, m->f, m->d_nbx, m->d_blkx, m->nBlkX, maxIters, nIterMin, m->d_rec,
+                           m->d_ctr + 1,
                            m->stream);
   if (m->nBlk > 0)
     return launch_cg2d_blk2(m->d, m->p, m->f, m->d_nb4, m->d_blk, m->nBlk, maxIters, nIterMin, m->d_rec, m->d_ctr + 1,
@@ -1491,7 +1506,7 @@ int mgcm_cg2d_sum_plan(mgcm_model *m, int *plan, long capacity, int *NT, int *PP
     tab = m->mwgPlan;
   } else if (m->nBlkX > 0) {
     int BX, BY;
-    cg2d_bxy_geometry(&BX, &BY, &nt);
+    cg2d_bxy_geometry(m->bxyVar, &BX, &BY, &nt);
     ppt = BX * BY;
     std::vector<int> blkx((size_t)ppt * nt);
     HIPCHK(hipMemcpy(blkx.data(), m->d_blkx, blkx.size() * sizeof(int), hipMemcpyDeviceToHost));
