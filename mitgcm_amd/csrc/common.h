@@ -212,14 +212,17 @@ struct MwgTables {
   const unsigned *ownExp; // [G][NT] bit p set: owned point p is in another part's rings
   const int *ringG;       // [G][RPT*NT] 2-D offset of the ring-1 point (-1: none)
   const unsigned *ringNb; // [G][RPT*NT][2]
-  const int *impC;        // [G][IMAX] compact index of ring-1 then ring-2 point (LDS slot NO + q)
+  const int *impC;        // [G][IMAX] export slot of ring-1 then ring-2 point (LDS slot NO + q)
   const int *impG;        // [G][IMAX] its 2-D offset
   const int *nImp;        // [G]
   int G, IMAX, SZ;        // parts, import capacity, LDS slots before the ZERO slot
   int pinned;             // 1: only blockIdx.x % 8 == 0 work (all parts on one XCD)
-  double *xs;             // [nPts] exchange buffer of s (sc1 stores / loads)
-  double *part;           // [2][3][G] workgroup partials (sc1)
-  unsigned *ctr;          // [0] arrival counter, [1] timeout word (zeroed before each launch)
+  // hand-off state, one block zeroed before each launch (hsBytes from ctr): granules of
+  // {tag = phase + 1 (32 bits), half of an f64 (32 bits)}, two per value
+  unsigned *ctr;          // [1] timeout word
+  unsigned long long *part;   // [2 parities][3 values][G][2] workgroup partials
+  unsigned long long *xs;     // [exported points][2] q = M r of the points other parts' rings hold
+  size_t hsBytes;
 };
 
 // Per-solve record written by the device CG2D (one slot per time step).

@@ -14,13 +14,20 @@
 // expression on the same bytes, so the copies stay bit-identical and the exchange of r that
 // cg2d.F does after each update (EXCH_S3D_RL(cg2d_r), :337) needs no synchronisation.
 //
-// Per iteration three grid-wide hand-offs (Guideline 16, R1 form: payload stored sc1 and
-// drained with s_waitcnt vmcnt(0), one relaxed agent-scope add per workgroup on an arrival
-// counter, one lane polls relaxed with s_sleep, every load of handed-off bytes sc1):
+// Per iteration two grid-wide hand-offs, each in the data-is-the-flag form (Guideline 16,
+// R2): every handed-off f64 travels as two 8-byte granules {tag, half}, each written by ONE
+// relaxed agent-scope (sc1) store; a consumer re-reads its granules (relaxed, sc1) until every
+// tag equals the phase number.  No counter, no drain, no fence: one fabric round trip per
+// hand-off instead of a store-drain, an atomic add, a poll and a load.  Tags restart at 1 in
+// each launch (the hand-off block is zeroed before it); partials alternate between two
+// buffers (a part can run at most one phase ahead of the slowest reader):
 //   sync B  partials of (r,r) of iteration n and (M r, r) of n+1 (the reference's err_sq and
-//           eta_qrN, reduced together: same values, cg2d.F:211-243, 321-337);
-//   sync C  s exported (owned points that lie in another part's rings) -> imported;
+//           eta_qrN, reduced together: same values, cg2d.F:211-243, 321-337), and the
+//           q = M r of the owned points other parts' rings hold;
 //   sync D  partials of (s, A s) -> alpha (cg2d.F:268-301).
+// EXCH_S3D_RL(cg2d_s) (cg2d.F:260) needs no hand-off of its own: a part keeps the s of its
+// rings and updates them itself, s = q + beta*s with the q imported at sync B -- the
+// owner's expression on the owner's bytes, so the ring copies stay bit-identical.
 // Global sums in a fixed order, independent of placement and of how many GPUs share the
 // tiles: thread partials (OPT terms in order) -> pairwise tree over the NT threads -> per
 // workgroup partial; lane l of every wave adds partials l, l+64, ... in order, then the
@@ -83,67 +90,122 @@ __device__ __forceinline__ double mw_wave_max(double v) {
 constexpr int MW_NT = 256, MW_OPT = 4, MW_RPT = 1, MW_NW = MW_NT / 64;
 constexpr int MW_NV = 3;   // values per reduction
 
-// One grid-wide hand-off: NV workgroup partials (a pairwise tree over the threads of
-// v[0..NV-1]) published and combined in the fixed order; MAXOP: combine by max instead.
+// ---- granule hand-offs (Guideline 16 R2) -------------------------------------------
+__device__ __forceinline__ void gran_put(gu64 *g, unsigned tag, double v) {
+  const unsigned long long b = __builtin_bit_cast(unsigned long long, v), t = (unsigned long long)tag << 32;
+  __hip_atomic_store(g, t | (b & 0xffffffffull), RLX_AGENT);
+  __hip_atomic_store(g + 1, t | (b >> 32), RLX_AGENT);
+}
+__device__ __forceinline__ bool gran_get(gu64 *g, unsigned tag, double &v) {
+  const unsigned long long lo = __hip_atomic_load(g, RLX_AGENT), hi = __hip_atomic_load(g + 1, RLX_AGENT);
+  v = __builtin_bit_cast(double, ((hi & 0xffffffffull) << 32) | (lo & 0xffffffffull));
+  return (unsigned)(lo >> 32) == tag && (unsigned)(hi >> 32) == tag;
+}
+// bounded spin: after ~2^22 passes every part gives up (timeout word), so no wave hangs
+__device__ __forceinline__ bool spin_fail(unsigned &spins, gu32 *tmo) {
+  if (__hip_atomic_load(tmo, RLX_AGENT) != 0u || ++spins > (1u << 22)) {
+    __hip_atomic_store(tmo, 1u, RLX_AGENT);
+    return true;
+  }
+  __builtin_amdgcn_s_sleep(1);
+  return false;
+}
+
+// One grid-wide reduction: NV workgroup partials (a pairwise tree over the threads of
+// v[0..NV-1]) published as granules and combined by wave 0 in the fixed order, the results
+// broadcast through LDS; MAXOP: combine by max instead.
+// The q of this part's ring points (ring 1, then ring 2), handed off with a reduction: the
+// waves other than wave 0 sweep their granules into LDS while wave 0 combines the partials.
+struct MwImport {
+  size_t gi;       // first import slot of this part
+  int nImp;
+  double *imp_l;   // LDS staging, nImp doubles
+};
+
 template <int NV, bool MAXOP>
-__device__ __forceinline__ bool mw_sync(double *v, const MwgTables &T, int g, int &nsync, double *red) {
+__device__ __forceinline__ bool mw_sync(double *v, const MwgTables &T, int g, int &nsync, double *red,
+                                        const MwImport *imp = nullptr) {
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  const int par = nsync & 1;
-  gu64 *P = (gu64 *)(T.part + (size_t)par * MW_NV * T.G);
-  if (NV > 0) {
-    // workgroup partial: the pairwise tree over its threads (wave tree, then the row-16
-    // tree over the zero-padded wave values: the operations of block_sum_nw)
-#pragma unroll
-    for (int q = 0; q < NV; q++) {
-      const double w = MAXOP ? mw_wave_max(v[q]) : mw_wave_sum(v[q]);
-      if (lane == 0) red[q * 16 + wv] = w;
-    }
-    __syncthreads();
-    if (wv == 0) {
-#pragma unroll
-      for (int q = 0; q < NV; q++) {
-        const int l = lane & 15;
-        const double xw = l < MW_NW ? red[q * 16 + l] : 0.0;
-        const double wgp = MAXOP ? mw_rowmax16(xw) : mw_row16(xw);
-        if (lane == 0) __hip_atomic_store(P + (size_t)q * T.G + g, __builtin_bit_cast(unsigned long long, wgp), RLX_AGENT);
-      }
-    }
-  }
-  // every storing wave drains its sc1 stores (partials, exported s) before the arrival
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
   nsync++;
-  if (tid == 0) {
-    gu32 *ctr = (gu32 *)T.ctr;
-    __hip_atomic_fetch_add(ctr, 1u, RLX_AGENT);
-    const unsigned target = (unsigned)(T.G * nsync);
-    unsigned spins = 0;
-    double okv = 1.0;
-    while (__hip_atomic_load(ctr, RLX_AGENT) < target) {
-      if (__hip_atomic_load(ctr + 1, RLX_AGENT) != 0u || ++spins > (1u << 24)) {
-        __hip_atomic_store(ctr + 1, 1u, RLX_AGENT);   // timeout word: every part gives up
-        okv = 0.0;
-        break;
-      }
-      __builtin_amdgcn_s_sleep(2);
-    }
-    red[15 * 16] = okv;
-  }
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");   // every handed-off byte is loaded sc1 below
-  __syncthreads();
-  const bool ok = red[15 * 16] != 0.0;
-  // combine: lane l adds partials l, l+64, ... in order, then the pairwise tree over the lanes
+  const unsigned tag = (unsigned)nsync;
+  gu64 *P = (gu64 *)(T.part + (size_t)(nsync & 1) * MW_NV * T.G * 2);
+  // workgroup partial: the pairwise tree over its threads (wave tree, then the row-16 tree
+  // over the zero-padded wave values: the operations of block_sum_nw)
 #pragma unroll
   for (int q = 0; q < NV; q++) {
-    double acc = 0.0;
-    for (int gg = lane; gg < T.G; gg += 64) {
-      const double xg = __builtin_bit_cast(double, __hip_atomic_load(P + (size_t)q * T.G + gg, RLX_AGENT));
-      acc = MAXOP ? fmax(acc, xg) : acc + xg;
-    }
-    v[q] = MAXOP ? mw_wave_max(acc) : mw_wave_sum(acc);
+    const double w = MAXOP ? mw_wave_max(v[q]) : mw_wave_sum(v[q]);
+    if (lane == 0) red[q * 16 + wv] = w;
   }
-  return ok;
+  __syncthreads();
+  if (wv == 0) {
+    const int l = lane & 15;
+#pragma unroll
+    for (int q = 0; q < NV; q++) {
+      const double xw = l < MW_NW ? red[q * 16 + l] : 0.0;
+      const double wgp = MAXOP ? mw_rowmax16(xw) : mw_row16(xw);
+      if (lane == 0) gran_put(P + ((size_t)q * T.G + g) * 2, tag, wgp);
+    }
+    // combine: lane l adds partials l, l+64, ... in order, then the pairwise tree over the
+    // lanes; the whole sweep is repeated until every granule carries this phase's tag
+    double acc[NV];
+    unsigned spins = 0;
+    bool ok = true;
+    for (;;) {
+      bool good = true;
+#pragma unroll
+      for (int q = 0; q < NV; q++) {
+        acc[q] = 0.0;
+        for (int gg = lane; gg < T.G; gg += 64) {
+          double xg;
+          good = gran_get(P + ((size_t)q * T.G + gg) * 2, tag, xg) && good;
+          acc[q] = MAXOP ? fmax(acc[q], xg) : acc[q] + xg;
+        }
+      }
+      if (__all(good)) break;
+      if (spin_fail(spins, (gu32 *)T.ctr + 1)) { ok = false; break; }
+    }
+#pragma unroll
+    for (int q = 0; q < NV; q++) {
+      const double rv = MAXOP ? mw_wave_max(acc[q]) : mw_wave_sum(acc[q]);
+      if (lane == 0) red[(8 + q) * 16] = rv;
+    }
+    if (lane == 0) red[15 * 16] = ok ? 1.0 : 0.0;
+  } else if (imp) {
+    for (int q0 = 0; q0 < imp->nImp; q0 += MW_NT - 64) {
+      const int qq = q0 + tid - 64;
+      const bool act = qq < imp->nImp;
+      gu64 *src = (gu64 *)T.xs + (size_t)2 * (act ? T.impC[imp->gi + qq] : 0);
+      double xv = 0.0;
+      unsigned spins = 0;
+      for (;;) {
+        const bool good = !act || gran_get(src, tag, xv);
+        if (__all(good)) break;
+        if (spin_fail(spins, (gu32 *)T.ctr + 1)) break;   // the timeout word fails the solve
+      }
+      if (act) imp->imp_l[qq] = xv;
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int q = 0; q < NV; q++) v[q] = red[(8 + q) * 16];
+  return red[15 * 16] != 0.0;
 }
+
+#ifdef MGCM_CG_STAMPS   // diagnostic build only: per-phase shader-cycle totals of part 0
+#define MW_STAMP(k)                                                                   \
+  do {                                                                                \
+    __builtin_amdgcn_sched_barrier(0);                                                \
+    unsigned long long t_;                                                            \
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");       \
+    __builtin_amdgcn_sched_barrier(0);                                                \
+    if ((k) > 0) stampAcc[(k) - 1] += t_ - stampPrev;                                 \
+    stampPrev = t_;                                                                   \
+  } while (0)
+#else
+#define MW_STAMP(k) \
+  do {              \
+  } while (0)
+#endif
 
 template <bool PINNED>
 __global__ void __launch_bounds__(MW_NT) k_cg2d_mwg(Dims d, Params p, Fields f, MwgTables T, int maxIters,
@@ -160,6 +222,7 @@ __global__ void __launch_bounds__(MW_NT) k_cg2d_mwg(Dims d, Params p, Fields f, 
   double *s_l = lds;              // SZ + 1
   double *r_l = lds + (SZ + 1);   // NO + NR used, + ZERO at SZ
   double *red = lds + 2 * (SZ + 1);   // 16 x 16 scratch
+  double *imp_l = red + 16 * 16;      // IMAX: the ring q handed off at the last reduction
   const int tid = threadIdx.x;
   int nsync = 0;
   const size_t go = (size_t)g * NO, gr = (size_t)g * NR, gi = (size_t)g * T.IMAX;
@@ -206,6 +269,7 @@ __global__ void __launch_bounds__(MW_NT) k_cg2d_mwg(Dims d, Params p, Fields f, 
     rb[m] = act ? f.cg2d_b[gg] : 0.0;
   }
   const int nImp = T.nImp[g];
+  const MwImport imp{gi, nImp, imp_l};
 #define LO(w) ((w) & 0xFFFFu)
 #define HI(w) ((w) >> 16)
 
@@ -254,36 +318,44 @@ __global__ void __launch_bounds__(MW_NT) k_cg2d_mwg(Dims d, Params p, Fields f, 
 #pragma unroll
   for (int m = 0; m < MW_RPT; m++) r_l[NO + m * MW_NT + tid] = rr[m];
   __syncthreads();
-  // q = M r and (q, r) of iteration 1, reduced with err_sq and sumRHS
+  // q = M r and (q, r) of iteration 1, reduced with err_sq and sumRHS; q exported for the
+  // parts whose rings hold these points; the ring copies of s start at s = 0 like the owners'
+  gu64 *xs = (gu64 *)T.xs;
 #pragma unroll
   for (int m = 0; m < MW_OPT; m++) {
     q[m] = pC[m] * r[m] + pW0[m] * r_l[LO(nwe[m])] + pW1[m] * r_l[HI(nwe[m])] + pS0[m] * r_l[LO(nsn[m])] +
            pS1[m] * r_l[HI(nsn[m])];
     v3[2] = v3[2] + q[m] * r[m];
+    if ((exp >> m) & 1u) gran_put(xs + (size_t)2 * T.ownC[go + m * MW_NT + tid], (unsigned)(nsync + 1), q[m]);
   }
-  ok = ok && mw_sync<3, false>(v3, T, g, nsync, red);
+  for (int qq = tid; qq < nImp; qq += MW_NT) s_l[NO + qq] = 0.0;
+  ok = ok && mw_sync<3, false>(v3, T, g, nsync, red, &imp);
   double err_sq = v3[0];
   const double sumRHS = v3[1];
   double eta_qrN = v3[2], eta_qrNM1 = 1.0;
   const double firstResidual = sqrt(err_sq);
   int actualIts = 0;
   if (ok && !(err_sq < p.cg2dTolerance_sq)) {
-    gu64 *xs = (gu64 *)T.xs;
+#ifdef MGCM_CG_STAMPS
+    unsigned long long stampAcc[6] = {0, 0, 0, 0, 0, 0}, stampPrev = 0;
+    const unsigned long long stampT0 = __builtin_amdgcn_s_memtime();
+    __builtin_amdgcn_s_waitcnt(0xC07F);
+#endif
     for (int it2d = 1; it2d <= maxIters; it2d++) {
       const double cgBeta = eta_qrN / eta_qrNM1;
       eta_qrNM1 = eta_qrN;
-      // s = q + beta*s; EXCH_S3D_RL(cg2d_s): export the points other parts read
+      // s = q + beta*s on the owned points and, with the q handed off at sync B, on both rings
+      // (EXCH_S3D_RL(cg2d_s)); the next export of q comes after sync D, when every part has
+      // read this one
 #pragma unroll
       for (int m = 0; m < MW_OPT; m++) {
         s[m] = q[m] + cgBeta * s[m];
         s_l[m * MW_NT + tid] = s[m];
-        if ((exp >> m) & 1u) __hip_atomic_store(xs + T.ownC[go + m * MW_NT + tid], __builtin_bit_cast(unsigned long long, s[m]), RLX_AGENT);
       }
-      ok = mw_sync<0, false>(nullptr, T, g, nsync, red);
-      if (!ok) break;
-      for (int qq = tid; qq < nImp; qq += MW_NT)
-        s_l[NO + qq] = __builtin_bit_cast(double, __hip_atomic_load(xs + T.impC[gi + qq], RLX_AGENT));
+      MW_STAMP(0);
+      for (int qq = tid; qq < nImp; qq += MW_NT) s_l[NO + qq] = imp_l[qq] + cgBeta * s_l[NO + qq];
       __syncthreads();
+      MW_STAMP(1);
       // q = A s (owned + ring 1); alpha = eta_qrN / (s, A s)
       double av[1] = {0.0};
 #pragma unroll
@@ -297,7 +369,9 @@ __global__ void __launch_bounds__(MW_NT) k_cg2d_mwg(Dims d, Params p, Fields f, 
       for (int m = 0; m < MW_RPT; m++)
         rq[m] = raW0[m] * s_l[LO(rwe[m])] + raW1[m] * s_l[HI(rwe[m])] + raS0[m] * s_l[LO(rsn[m])] +
                 raS1[m] * s_l[HI(rsn[m])] + raC[m] * s_l[NO + m * MW_NT + tid];
+      MW_STAMP(2);
       ok = mw_sync<1, false>(av, T, g, nsync, red);
+      MW_STAMP(3);
       if (!ok) break;
       const double alpha = eta_qrN / av[0];
       // x += alpha s ; r -= alpha q (owned and ring 1); err_sq and the next (M r, r)
@@ -321,13 +395,22 @@ __global__ void __launch_bounds__(MW_NT) k_cg2d_mwg(Dims d, Params p, Fields f, 
         q[m] = pC[m] * r[m] + pW0[m] * r_l[LO(nwe[m])] + pW1[m] * r_l[HI(nwe[m])] + pS0[m] * r_l[LO(nsn[m])] +
                pS1[m] * r_l[HI(nsn[m])];
         v2[1] = v2[1] + q[m] * r[m];
+        if ((exp >> m) & 1u) gran_put(xs + (size_t)2 * T.ownC[go + m * MW_NT + tid], (unsigned)(nsync + 1), q[m]);
       }
-      ok = mw_sync<2, false>(v2, T, g, nsync, red);
+      MW_STAMP(4);
+      ok = mw_sync<2, false>(v2, T, g, nsync, red, &imp);
+      MW_STAMP(5);
       if (!ok) break;
       err_sq = v2[0];
       eta_qrN = v2[1];
       if (err_sq < p.cg2dTolerance_sq) break;
     }
+#ifdef MGCM_CG_STAMPS
+    if (g == 0 && threadIdx.x == 0)
+      printf("MWSTAMP G %d its %d total %llu | import %llu applyA %llu syncD %llu upd+applyM %llu syncB %llu\n", T.G,
+             actualIts, __builtin_amdgcn_s_memtime() - stampT0, stampAcc[0], stampAcc[1], stampAcc[2], stampAcc[3],
+             stampAcc[4]);
+#endif
   }
 #pragma unroll
   for (int m = 0; m < MW_OPT; m++) {
@@ -343,7 +426,8 @@ __global__ void __launch_bounds__(MW_NT) k_cg2d_mwg(Dims d, Params p, Fields f, 
     R.minResidualSq = -1.0;
     R.rhsMax = rhsMax;
     R.sumRHS = sumRHS;
-    R.numIters = ok ? actualIts : -1;   // -1: a grid hand-off timed out
+    const bool tmo = __hip_atomic_load((gu32 *)T.ctr + 1, RLX_AGENT) != 0u;
+    R.numIters = (ok && !tmo) ? actualIts : -1;   // -1: a grid hand-off timed out
     R.nIterMin = -1;
   }
 #undef LO
@@ -354,9 +438,9 @@ int cg2d_mwg_geometry(int *nt, int *opt, int *rpt) { *nt = MW_NT; *opt = MW_OPT;
 
 hipError_t launch_cg2d_mwg(const Dims &d, const Params &p, const Fields &f, const MwgTables &T, int maxIters,
                            SolveRecord *rec, int *stepCounter, hipStream_t s) {
-  hipError_t e = hipMemsetAsync(T.ctr, 0, 16, s);   // arrival counter + timeout word, every launch
+  hipError_t e = hipMemsetAsync(T.ctr, 0, T.hsBytes, s);   // timeout word + every granule, every launch
   if (e != hipSuccess) return e;
-  const size_t lds = (size_t)(2 * (T.SZ + 1) + 16 * 16) * sizeof(double);
+  const size_t lds = (size_t)(2 * (T.SZ + 1) + 16 * 16 + T.IMAX) * sizeof(double);
   auto kern = T.pinned ? k_cg2d_mwg<true> : k_cg2d_mwg<false>;
   static bool attrSet[2] = {false, false};
   if (!attrSet[T.pinned]) {

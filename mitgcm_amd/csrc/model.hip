@@ -580,6 +580,11 @@ static int build_mwg(mgcm_model *m) {
   std::vector<unsigned> ownExp((size_t)G * NT, 0u);
   std::vector<int> impC((size_t)G * IMAX, 0), impG((size_t)G * IMAX, (int)MG_I2(d, 1, 1, d.t0)), nImp(G);
   m->mwgPlan.assign((size_t)G * NO, -1);
+  // the exported points, numbered: their granules in the hand-off block
+  std::vector<int> expSlot(exported.size(), -1);
+  int nExp = 0;
+  for (size_t c = 0; c < exported.size(); c++)
+    if (exported[c]) expSlot[c] = nExp++;
   for (int g = 0; g < G; g++) {
     std::map<int, int> slot;
     for (size_t n = 0; n < own[g].size(); n++) {
@@ -593,7 +598,7 @@ static int build_mwg(mgcm_model *m) {
       const int c = own[g][n], q = (int)n;   // slot p*NT + tid == n
       const size_t o = (size_t)g * NO + q;
       ownG[o] = g2of(c);
-      ownC[o] = c;
+      ownC[o] = exported[c] ? expSlot[c] : 0;
       ownNb[2 * o] = sl(nbr(c, 0)) | (sl(nbr(c, 1)) << 16);
       ownNb[2 * o + 1] = sl(nbr(c, 2)) | (sl(nbr(c, 3)) << 16);
       if (exported[c]) ownExp[(size_t)g * NT + q % NT] |= 1u << (q / NT);
@@ -605,11 +610,11 @@ static int build_mwg(mgcm_model *m) {
       ringG[o] = g2of(c);
       ringNb[2 * o] = sl(nbr(c, 0)) | (sl(nbr(c, 1)) << 16);
       ringNb[2 * o + 1] = sl(nbr(c, 2)) | (sl(nbr(c, 3)) << 16);
-      impC[(size_t)g * IMAX + n] = c;
+      impC[(size_t)g * IMAX + n] = expSlot[c];
       impG[(size_t)g * IMAX + n] = g2of(c);
     }
     for (size_t n = 0; n < ring2[g].size(); n++) {
-      impC[(size_t)g * IMAX + NR + n] = ring2[g][n];
+      impC[(size_t)g * IMAX + NR + n] = expSlot[ring2[g][n]];
       impG[(size_t)g * IMAX + NR + n] = g2of(ring2[g][n]);
     }
     nImp[g] = NR + (int)ring2[g].size();
@@ -622,15 +627,16 @@ static int build_mwg(mgcm_model *m) {
     return -1;
   T.G = G; T.IMAX = IMAX; T.SZ = SZ;
   T.pinned = (G <= 32 && !getenv("MGCM_CG2D_SPREAD")) ? 1 : 0;
-  double *xs = nullptr, *part = nullptr;
-  unsigned *ctr = nullptr;
-  HIPCHK(hipMalloc(&xs, (size_t)d.nTiles * ppTile * sizeof(double)));
-  m->mwgAllocs.push_back(xs);
-  HIPCHK(hipMalloc(&part, (size_t)2 * 3 * G * sizeof(double)));
-  m->mwgAllocs.push_back(part);
-  HIPCHK(hipMalloc(&ctr, 64));
-  m->mwgAllocs.push_back(ctr);
-  T.xs = xs; T.part = part; T.ctr = ctr;
+  // hand-off block: 64 B of words, the partial granules, the export granules (zeroed by one
+  // memset before every launch, a multiple of 16 B from the allocation's start)
+  const size_t partGr = (size_t)2 * 3 * G * 2, hs = 64 + (partGr + (size_t)nExp * 2) * sizeof(unsigned long long);
+  char *blk = nullptr;
+  HIPCHK(hipMalloc(&blk, hs));
+  m->mwgAllocs.push_back(blk);
+  T.ctr = (unsigned *)blk;
+  T.part = (unsigned long long *)(blk + 64);
+  T.xs = T.part + partGr;
+  T.hsBytes = hs;
   m->useMwg = true;
   return 0;
 }

@@ -177,10 +177,14 @@ class Model:
         return plan[:nt.value * ppt.value * ng.value].copy(), nt.value, ppt.value, ng.value
 
     def cg2d_kernel(self):
-        """Which CG2D kernel mgcm_init selected: 'mwg' (multi-workgroup), 'bxy' (2x4 points/thread),
+        """Which CG2D kernel mgcm_init selected: 'mwg' (multi-workgroup), 'bxy' (BX x BY points/thread),
         'blk2' (2x2) or 'block'."""
         k = lib().mgcm_get_param(self.h, b"cg2dKernel")
         return {4.0: "mwg", 3.0: "bxy", 2.0: "blk2"}.get(k, "block")
+
+    def cg2d_parts(self):
+        """Workgroups (one per CU) the CG2D solve runs on."""
+        return int(lib().mgcm_get_param(self.h, b"cg2dParts"))
 
     def kernel_timing(self, enable):
         lib().mgcm_kernel_timing(self.h, 1 if enable else 0)
