@@ -9,6 +9,7 @@
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 
 namespace mgcm {
 
@@ -56,6 +57,7 @@ struct Params {
   int momAdvection, momViscosity, momForcing, useCoriolis, no_slip_sides, no_slip_bottom;
   int selectCoriScheme, momForcingOutAB, momDissip_In_AB, implicitViscosity;
   int cg2dMaxIters, cg2dUseMinResSol, cg2dNormaliseRHS, nIter0;
+  int cg2dUseFMA;   // CG2D in fused multiply-adds (device-order oracle: the same fma chains)
   // 3-D / tracer path
   double gravity, gravitySign, rhoNil, tAlpha, sBeta, ivdc_kappa, diffKhT, diffKrT, deltaTtracer;
   double recip_rSphere;
@@ -181,6 +183,43 @@ inline unsigned mg_col_blocks(int ni, int nj, int nT, int Nr) {
   const int nc = 256 / mg_col_kp(Nr);
   return (unsigned)(((long)ni * nj * nT + nc - 1) / nc);
 }
+// Column frame with a run-time column count: a 256-thread workgroup holds NC consecutive
+// columns (NC = 16, 32 or 64) and KW = 256/NC level slots; thread (c, w) = threadIdx.x =
+// w*NC + c stages levels k = w+1, w+1+KW, ... of column c (MG_COLF_K loop) into LDS slot
+// (k-1)*NC + c -- coalesced over i -- and thread (c, 0) runs column c's serial recurrence
+// out of LDS.  With NC = 64 the serial part of 64 columns runs in one full wave (MG_COLS
+// puts 4 columns per workgroup at Nr = 50, so its serial part ran on 4 lanes of 256).
+// The LDS arrays are dynamic: nArr slices of Nr*NC doubles (mg_colf_lds).
+#define MG_COLF(i0, ni, j0, nj, NCv)                                                   \
+  const int NC_ = (NCv), KW_ = 256 / NC_;                                              \
+  const int cc = (int)threadIdx.x % NC_, kk = (int)threadIdx.x / NC_;                  \
+  const long col_ = (long)mg_xcd_block() * NC_ + cc;                                   \
+  const long npl_ = (long)(ni) * (nj);                                                 \
+  const bool valid = col_ < npl_ * d.nT;                                               \
+  const int t = d.t0 + (int)(valid ? col_ / npl_ : 0);                                 \
+  const int i = (i0) + (int)((valid ? col_ % npl_ : 0) % (ni));                        \
+  const int j = (j0) + (int)((valid ? col_ % npl_ : 0) / (ni));
+// (the bodies keep global stores out of these loops, so that nothing orders a level's
+// loads behind the previous level's stores)
+#define MG_COLF_K(kvar) for (int kvar = kk + 1; kvar <= d.Nr; kvar += KW_)
+// NC for a launch: 16 columns x 16 level slots (measured on LLC-90, Nr = 50: the implicit
+// tracer solve 119 us at NC = 16, 201 at 32, 168 with MG_COLS' 4 columns x 64 levels; wider
+// column runs cost occupancy through their LDS); MGCM_COLF_NC=16|32|64 forces it (sweeps)
+inline int mg_colf_nc(long ncols, int Nr, int nArr) {
+  static const int force = getenv("MGCM_COLF_NC") ? atoi(getenv("MGCM_COLF_NC")) : 0;
+  (void)ncols; (void)Nr; (void)nArr;
+  if (force == 16 || force == 32 || force == 64) return force;
+  return 16;
+}
+inline size_t mg_colf_lds(int Nr, int nc, int nArr) { return (size_t)nArr * Nr * nc * sizeof(double); }
+// dynamic LDS above the 64 KB default needs the per-kernel attribute (set once)
+#define MG_ALLOW_LDS(kern)                                                                              \
+  do {                                                                                                  \
+    static const bool set_ = (hipFuncSetAttribute((const void *)(kern),                                 \
+                                                  hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) == hipSuccess); \
+    (void)set_;                                                                                         \
+  } while (0)
+inline unsigned mg_colf_blocks(long ncols, int nc) { return (unsigned)((ncols + nc - 1) / nc); }
 inline unsigned mg_plane_blocks(int ni, int nj, int nz) {
   return (unsigned)(((ni) * (nj) + MG_PLANE_THREADS - 1) / MG_PLANE_THREADS * (nz));
 }

@@ -108,19 +108,21 @@ __device__ __forceinline__ double block_max(double v, double *red, int slot) {
 // (solve_for_pressure.F:142-151); with the CD scheme etaNm1 = etaN
 // (solve_for_pressure.F:126-128) and CD_CODE_SCHEME's uNM1, vNM1 = u, v
 // (cd_code_scheme.F:228-234) are saved here, after every k_cd_scheme read.
-__global__ void __launch_bounds__(256) k_sfp_rhs(Dims d, Params p, Fields f) {
-  __shared__ double sE[256], sW[256], sN[256], sS[256];
-  MG_COLS(1 - d.OLx, d.nx, 1 - d.OLy, d.ny, d.Nr)
-  const int k = kk + 1, me = kk * NC_ + cc;
+__global__ void __launch_bounds__(256) k_sfp_rhs(Dims d, Params p, Fields f, int nc) {
+  extern __shared__ __attribute__((aligned(16))) double lds[];
+  MG_COLF(1 - d.OLx, d.nx, 1 - d.OLy, d.ny, nc)
+  const int NS = d.Nr * NC_;
+  double *sE = lds, *sW = lds + NS, *sN = lds + 2 * NS, *sS = lds + 3 * NS;
   const bool inner = i >= 1 && i <= d.sNx && j >= 1 && j <= d.sNy;
   const long q = MG_I2(d, i, j, t);
-  if (valid && k <= d.Nr) {
-    if (p.useCDscheme) {
-      const long q3 = MG_I3(d, i, j, k, t);
-      f.uNM1[q3] = f.uVel[q3];
-      f.vNM1[q3] = f.vVel[q3];
-    }
-    if (inner) {   // CALC_DIV_GHAT flux terms of level k
+  if (valid && p.useCDscheme) MG_COLF_K(k) {
+    const long q3 = MG_I3(d, i, j, k, t);
+    f.uNM1[q3] = f.uVel[q3];
+    f.vNM1[q3] = f.vVel[q3];
+  }
+  if (valid && inner) MG_COLF_K(k) {
+    const int me = (k - 1) * NC_ + cc;
+    {   // CALC_DIV_GHAT flux terms of level k
       const double drF = f.drF[k - 1];
       sE[me] = f.dyG[MG_I2(d, i + 1, j, t)] * drF * f.hFacW[MG_I3(d, i + 1, j, k, t)] *
                f.gU[MG_I3(d, i + 1, j, k, t)] / p.deltaTMom;
@@ -685,7 +687,9 @@ __device__ __forceinline__ double block_max_nw(double v, double *red, int slot) 
   do {              \
   } while (0)
 #endif
-template <int BX, int BY, int NT, bool MINRES>
+// FMA: the operator rows, dot products and vector updates as fused multiply-adds in a fixed
+// order (cg2dUseFMA; the oracle's device-order mode evaluates the same fma chains)
+template <int BX, int BY, int NT, bool MINRES, bool FMA>
 __global__ void __launch_bounds__(NT) k_cg2d_bxy(Dims d, Params p, Fields f, const unsigned *__restrict__ nbx,
                                                  const int *__restrict__ blkx, int nBlk, int maxIters, int nIterMinIn,
                                                  SolveRecord *rec, int *stepCounter) {
@@ -763,7 +767,14 @@ __global__ void __launch_bounds__(NT) k_cg2d_bxy(Dims d, Params p, Fields f, con
         const double e = a < BX - 1 ? v[b][a + 1] : vE[b];
         const double so = b > 0 ? v[b - 1][a] : vS[a];
         const double no = b < BY - 1 ? v[b + 1][a] : vN[a];
-        if (isM)
+        if (FMA) {   // the same terms, accumulated left to right by fma
+          if (isM)
+            out[b][a] = __builtin_fma(pS[a][b + 1], no, __builtin_fma(pS[a][b], so, __builtin_fma(pW[b][a + 1], e,
+                                      __builtin_fma(pW[b][a], w, pC[b][a] * v[b][a]))));
+          else
+            out[b][a] = __builtin_fma(aC[b][a], v[b][a], __builtin_fma(aS[a][b + 1], no, __builtin_fma(aS[a][b], so,
+                                      __builtin_fma(aW[b][a + 1], e, aW[b][a] * w))));
+        } else if (isM)
           out[b][a] = pC[b][a] * v[b][a] + pW[b][a] * w + pW[b][a + 1] * e + pS[a][b] * so + pS[a][b + 1] * no;
         else
           out[b][a] = aW[b][a] * w + aW[b][a + 1] * e + aS[a][b] * so + aS[a][b + 1] * no + aC[b][a] * v[b][a];
@@ -799,7 +810,7 @@ __global__ void __launch_bounds__(NT) k_cg2d_bxy(Dims d, Params p, Fields f, con
 #pragma unroll
       for (int a = 0; a < BX; a++) {
         r[b][a] = bb[b][a] - ax[b][a];
-        err = err + r[b][a] * r[b][a];
+        err = FMA ? __builtin_fma(r[b][a], r[b][a], err) : err + r[b][a] * r[b][a];
         sumB = sumB + bb[b][a];
       }
   }
@@ -841,7 +852,7 @@ __global__ void __launch_bounds__(NT) k_cg2d_bxy(Dims d, Params p, Fields f, con
 #pragma unroll
     for (int b = 0; b < BY; b++)
 #pragma unroll
-      for (int a = 0; a < BX; a++) e = e + q[b][a] * r[b][a];
+      for (int a = 0; a < BX; a++) e = FMA ? __builtin_fma(q[b][a], r[b][a], e) : e + q[b][a] * r[b][a];
     double eta_qrN = block_sum_nw<NW>(e, red, 0);
 #ifdef MGCM_CG_STAMPS
     unsigned long long stampAcc[6] = {0, 0, 0, 0, 0, 0}, stampPrev = 0;
@@ -854,7 +865,10 @@ __global__ void __launch_bounds__(NT) k_cg2d_bxy(Dims d, Params p, Fields f, con
 #pragma unroll
       for (int b = 0; b < BY; b++)
 #pragma unroll
-        for (int a = 0; a < BX; a++) { sv[b][a] = q[b][a] + cgBeta * sv[b][a]; s_l[cs[b][a]] = sv[b][a]; }
+        for (int a = 0; a < BX; a++) {
+          sv[b][a] = FMA ? __builtin_fma(cgBeta, sv[b][a], q[b][a]) : q[b][a] + cgBeta * sv[b][a];
+          s_l[cs[b][a]] = sv[b][a];
+        }
       CG_STAMP(0);
       __syncthreads();
       CG_STAMP(1);
@@ -863,7 +877,7 @@ __global__ void __launch_bounds__(NT) k_cg2d_bxy(Dims d, Params p, Fields f, con
 #pragma unroll
       for (int b = 0; b < BY; b++)
 #pragma unroll
-        for (int a = 0; a < BX; a++) aa = aa + sv[b][a] * q[b][a];
+        for (int a = 0; a < BX; a++) aa = FMA ? __builtin_fma(sv[b][a], q[b][a], aa) : aa + sv[b][a] * q[b][a];
       aslot = aslot ^ 1;
       CG_STAMP(2);
       double alpha = block_sum_nw<NW>(aa, red, aslot);
@@ -874,9 +888,9 @@ __global__ void __launch_bounds__(NT) k_cg2d_bxy(Dims d, Params p, Fields f, con
       for (int b = 0; b < BY; b++)
 #pragma unroll
         for (int a = 0; a < BX; a++) {
-          x[b][a] = x[b][a] + alpha * sv[b][a];
-          r[b][a] = r[b][a] - alpha * q[b][a];
-          e2 = e2 + r[b][a] * r[b][a];
+          x[b][a] = FMA ? __builtin_fma(alpha, sv[b][a], x[b][a]) : x[b][a] + alpha * sv[b][a];
+          r[b][a] = FMA ? __builtin_fma(-alpha, q[b][a], r[b][a]) : r[b][a] - alpha * q[b][a];
+          e2 = FMA ? __builtin_fma(r[b][a], r[b][a], e2) : e2 + r[b][a] * r[b][a];
           r_l[cs[b][a]] = r[b][a];
         }
       actualIts = it2d;
@@ -888,7 +902,7 @@ __global__ void __launch_bounds__(NT) k_cg2d_bxy(Dims d, Params p, Fields f, con
 #pragma unroll
       for (int b = 0; b < BY; b++)
 #pragma unroll
-        for (int a = 0; a < BX; a++) en = en + q[b][a] * r[b][a];
+        for (int a = 0; a < BX; a++) en = FMA ? __builtin_fma(q[b][a], r[b][a], en) : en + q[b][a] * r[b][a];
       block_sum2_nw<NW>(e2, en, red, 0);
       CG_STAMP(5);
       err_sq = e2;
@@ -1167,8 +1181,10 @@ __global__ void k_bump_counter(int *c, int nIncr) {
 
 // ------------------------------------------------------------------ launchers
 hipError_t launch_sfp_rhs(const Dims &d, const Params &p, const Fields &f, hipStream_t s) {
-  const dim3 blk(256), grd(mg_col_blocks(d.nx, d.ny, d.nT, d.Nr));
-  hipLaunchKernelGGL(k_sfp_rhs, grd, blk, 0, s, d, p, f);
+  const long ncol = (long)d.nx * d.ny * d.nT;
+  const int nc = mg_colf_nc(ncol, d.Nr, 4);
+  MG_ALLOW_LDS(k_sfp_rhs);
+  hipLaunchKernelGGL(k_sfp_rhs, dim3(mg_colf_blocks(ncol, nc)), dim3(256), mg_colf_lds(d.Nr, nc, 4), s, d, p, f, nc);
   return hipGetLastError();
 }
 
@@ -1230,12 +1246,14 @@ static hipError_t launch_bxy_t(const Dims &d, const Params &p, const Fields &f, 
                                int nBlk, int maxIters, int nIterMin, SolveRecord *rec, int *stepCounter, hipStream_t s) {
   if (nBlk > NT) return hipErrorInvalidValue;
   const size_t lds = (2 * ((size_t)BX * BY * NT + 1) + 4 * 16) * sizeof(double);
-  auto kern = nIterMin >= 0 ? k_cg2d_bxy<BX, BY, NT, true> : k_cg2d_bxy<BX, BY, NT, false>;
-  static bool attrSet[2] = {false, false};
-  if (!attrSet[nIterMin >= 0]) {
+  const bool mr = nIterMin >= 0, fm = p.cg2dUseFMA != 0;
+  auto kern = mr ? (fm ? k_cg2d_bxy<BX, BY, NT, true, true> : k_cg2d_bxy<BX, BY, NT, true, false>)
+                 : (fm ? k_cg2d_bxy<BX, BY, NT, false, true> : k_cg2d_bxy<BX, BY, NT, false, false>);
+  static bool attrSet[4] = {false, false, false, false};
+  if (!attrSet[2 * mr + fm]) {
     hipError_t e = hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return e;
-    attrSet[nIterMin >= 0] = true;
+    attrSet[2 * mr + fm] = true;
   }
   hipLaunchKernelGGL(kern, dim3(1), dim3(NT), lds, s, d, p, f, nbx, blkx, nBlk, maxIters, nIterMin, rec, stepCounter);
   return hipGetLastError();

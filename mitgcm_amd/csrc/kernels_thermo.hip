@@ -358,6 +358,7 @@ __global__ void __launch_bounds__(256) k_adv_r(Dims d, Params p, Fields f, Trace
 // GAD_CALC_RHS + forcing + AB2 + TIMESTEP_TRACER for one interior (i,j,k) point:
 // writes gNm1 (AB tracers) and gTscr = tracer + dTtracer*gT (the right-hand side of
 // the implicit vertical solve, or the new tracer with explicit vertical diffusion).
+template <bool GM>
 __global__ void __launch_bounds__(256) k_tracer_rhs(Dims d, Params p, Fields f, TracerArgs a, const int *iterPtr) {
   MG_PLANE(1, d.sNx, 1, d.sNy, z)
   const int t = d.t0 + z / d.Nr, k = z % d.Nr + 1;
@@ -376,7 +377,7 @@ __global__ void __launch_bounds__(256) k_tracer_rhs(Dims d, Params p, Fields f, 
   const double drF = f.drF[k - 1];
   // uFld, vFld, wFld of thermodynamics.F:252-268: the Eulerian velocity plus, with
   // GM_AdvForm, GMREDI_RESIDUAL_FLOW's bolus velocity (gmredi_residual_flow.F:58-97)
-  const bool bolus = p.useGMRedi && p.GM_AdvForm;
+  const bool bolus = GM && p.GM_AdvForm;
   const double flip = -p.gravitySign;
   const int kp1b = k + 1 < Nr ? k + 1 : Nr;
   const double maskp1b = k >= Nr ? 0.0 : 1.0;
@@ -425,9 +426,9 @@ __global__ void __launch_bounds__(256) k_tracer_rhs(Dims d, Params p, Fields f, 
     if (calcAdv) fz = fz + (uFld(ii, j) * xA) * (T3(ii, j, k) + T3(ii - 1, j, k)) * 0.5;
     double df = 0.0;
     if (a.diffKh != 0.0) df = -a.diffKh * xA * G2(recip_dxC, ii, j) * (T3(ii, j, k) - T3(ii - 1, j, k));
-    if (p.useGMRedi)   // GMREDI_XTRANSPORT (gmredi_xtransport.F:94-101)
+    if (GM)   // GMREDI_XTRANSPORT (gmredi_xtransport.F:94-101)
       df = df - xA * G3(Kux, ii, j, k) * G2(recip_dxC, ii, j) * (T3(ii, j, k) - T3(ii - 1, j, k));
-    if (p.useGMRedi && p.GM_ExtraDiag) df = df - xA * G3(Kuz, ii, j, k) * gm_dTdz(ii, j, 0);
+    if (GM && p.GM_ExtraDiag) df = df - xA * G3(Kuz, ii, j, k) * gm_dTdz(ii, j, 0);
     return fz + df;
   };
   auto fmer = [&](int jj) {
@@ -436,9 +437,9 @@ __global__ void __launch_bounds__(256) k_tracer_rhs(Dims d, Params p, Fields f, 
     if (calcAdv) fm = fm + (vFld(i, jj) * yA) * (T3(i, jj, k) + T3(i, jj - 1, k)) * 0.5;
     double df = 0.0;
     if (a.diffKh != 0.0) df = -a.diffKh * yA * G2(recip_dyC, i, jj) * (T3(i, jj, k) - T3(i, jj - 1, k));
-    if (p.useGMRedi)   // GMREDI_YTRANSPORT
+    if (GM)   // GMREDI_YTRANSPORT
       df = df - yA * G3(Kvy, i, jj, k) * G2(recip_dyC, i, jj) * (T3(i, jj, k) - T3(i, jj - 1, k));
-    if (p.useGMRedi && p.GM_ExtraDiag) df = df - yA * G3(Kvz, i, jj, k) * gm_dTdz(i, jj, 1);
+    if (GM && p.GM_ExtraDiag) df = df - yA * G3(Kvz, i, jj, k) * gm_dTdz(i, jj, 1);
     return fm + df;
   };
   // CALC_ADV_FLOW rTrans of level kk (0 at the surface and below the bottom level)
@@ -458,11 +459,11 @@ __global__ void __launch_bounds__(256) k_tracer_rhs(Dims d, Params p, Fields f, 
     double dfr = 0.0;
     if (!p.implicitDiffusion && kk >= 2 && kk <= Nr) {
       double kap = (G3(IVDConvCount, i, j, kk) * p.ivdc_kappa + 0.0) + a.diffKr;
-      if (p.useGMRedi) kap = kap + G3(Kwz, i, j, kk) * maskInC;
+      if (GM) kap = kap + G3(Kwz, i, j, kk) * maskInC;
       const double maskUp = G3(maskC, i, j, kk - 1) * G3(maskC, i, j, kk);
       dfr = -kap * maskUp * rA * f.recip_drC[kk - 1] * (T3(i, j, kk) - T3(i, j, kk - 1)) * p.rkSign;
     }
-    if (p.useGMRedi && kk >= 2 && kk <= Nr) {   // GMREDI_RTRANSPORT (gmredi_rtransport.F:75-130)
+    if (GM && kk >= 2 && kk <= Nr) {   // GMREDI_RTRANSPORT (gmredi_rtransport.F:75-130)
       const double dTdx =
           0.5 * (0.5 * (G3(maskW, i + 1, j, kk) * G2(recip_dxC, i + 1, j) * (T3(i + 1, j, kk) - T3(i, j, kk)) +
                         G3(maskW, i, j, kk) * G2(recip_dxC, i, j) * (T3(i, j, kk) - T3(i - 1, j, kk))) +
@@ -521,34 +522,38 @@ __global__ void __launch_bounds__(256) k_tracer_rhs(Dims d, Params p, Fields f, 
 // every level are formed k-parallel into LDS, one thread per column then sweeps
 // down and up in LDS with the reference's operations, and the levels are
 // written back k-parallel.
-__global__ void __launch_bounds__(256) k_tracer_impl(Dims d, Params p, Fields f, TracerArgs a) {
-  __shared__ double sSub[256], sSup[256], sY[256], sOut[256];
-  MG_COLS(1, d.sNx, 1, d.sNy, d.Nr)
-  const int Nr = d.Nr;
-  const int k = kk + 1;
-  const int me = kk * NC_ + cc;
+__global__ void __launch_bounds__(256) k_tracer_impl(Dims d, Params p, Fields f, TracerArgs a, int nc) {
+  extern __shared__ __attribute__((aligned(16))) double lds[];
+  MG_COLF(1, d.sNx, 1, d.sNy, nc)
+  const int Nr = d.Nr, NS = Nr * NC_;
+  double *sSub = lds, *sSup = lds + NS, *sY = lds + 2 * NS;   // sSub holds the solution after the sweeps
 #define G3(a_, ii, jj, kk_) f.a_[MG_I3(d, ii, jj, kk_, t)]
-  if (valid && k <= Nr) {
-    const long q3 = MG_I3(d, i, j, k, t);
+  if (valid) {
     // recip_hFacNew (thermodynamics.F:198-210): recip_hFacC/rStarExpC under r*
-    const double rh = (p.nonlinFreeSurf > 0 && p.select_rStar > 0) ? f.recip_hFacC[q3] / f.rStarExpC[MG_I2(d, i, j, t)]
-                                                                    : f.recip_hFacC[q3];
-    const double rdrF = f.recip_drF[k - 1];
-    const double mIn = f.maskInC[MG_I2(d, i, j, t)];
+    const bool rs = p.nonlinFreeSurf > 0 && p.select_rStar > 0;
+    const long q2 = MG_I2(d, i, j, t);
+    const double rsx = rs ? f.rStarExpC[q2] : 1.0;
+    const double mIn = f.maskInC[q2];
     // KappaRT = (IVDConvCount*ivdc_kappa + BL79(=0)) + diffKrNr [+ Kwz*maskInC] (calc_3d_diffusivity.F)
     auto kappa = [&](int k_) {
       double kap = (G3(IVDConvCount, i, j, k_) * p.ivdc_kappa + 0.0) + a.diffKr;
       if (p.useGMRedi) kap = kap + G3(Kwz, i, j, k_) * mIn;
       return kap;
     };
-    double sub = 0.0, sup = 0.0;
-    if (k >= 2)
-      sub = -(p.deltaTtracer * G3(maskC, i, j, k - 1) * rh * rdrF * kappa(k) * f.recip_drC[k - 1]);
-    if (k <= Nr - 1)
-      sup = -(p.deltaTtracer * G3(maskC, i, j, k + 1) * rh * rdrF * kappa(k + 1) * f.recip_drC[k]);
-    sSub[me] = sub;
-    sSup[me] = sup;
-    sY[me] = f.gTscr[q3];
+    MG_COLF_K(k) {
+      const int me = (k - 1) * NC_ + cc;
+      const long q3 = MG_I3(d, i, j, k, t);
+      const double rh = rs ? f.recip_hFacC[q3] / rsx : f.recip_hFacC[q3];
+      const double rdrF = f.recip_drF[k - 1];
+      double sub = 0.0, sup = 0.0;
+      if (k >= 2)
+        sub = -(p.deltaTtracer * G3(maskC, i, j, k - 1) * rh * rdrF * kappa(k) * f.recip_drC[k - 1]);
+      if (k <= Nr - 1)
+        sup = -(p.deltaTtracer * G3(maskC, i, j, k + 1) * rh * rdrF * kappa(k + 1) * f.recip_drC[k]);
+      sSub[me] = sub;
+      sSup[me] = sup;
+      sY[me] = f.gTscr[q3];
+    }
   }
   __syncthreads();
   if (valid && kk == 0) {
@@ -575,12 +580,12 @@ __global__ void __launch_bounds__(256) k_tracer_impl(Dims d, Params p, Fields f,
     for (int k2 = Nr; k2 >= 1; k2--) {
       const int s2 = (k2 - 1) * NC_ + cc;
       const double v = (k2 == Nr) ? sY[s2] : sY[s2] - sSup[s2] * below;
-      sOut[s2] = v;
+      sSub[s2] = v;
       below = v;
     }
   }
   __syncthreads();
-  if (valid && k <= Nr) a.trNext[MG_I3(d, i, j, k, t)] = sOut[me];
+  if (valid) MG_COLF_K(k) a.trNext[MG_I3(d, i, j, k, t)] = sSub[(k - 1) * NC_ + cc];
 #undef G3
 }
 
@@ -606,10 +611,14 @@ hipError_t launch_tracer_step(const Dims &d, const Params &p, const Fields &f, c
     hipLaunchKernelGGL(k_adv_y, grd, blk, 0, s, d, f, a);
     hipLaunchKernelGGL(k_adv_r, grd, blk, 0, s, d, p, f, a);
   }
-  hipLaunchKernelGGL(k_tracer_rhs, grd, blk, 0, s, d, p, f, a, iterPtr);
+  // GM/Redi fluxes as a template switch: without them the kernel holds half the registers
+  if (p.useGMRedi) hipLaunchKernelGGL(k_tracer_rhs<true>, grd, blk, 0, s, d, p, f, a, iterPtr);
+  else hipLaunchKernelGGL(k_tracer_rhs<false>, grd, blk, 0, s, d, p, f, a, iterPtr);
   if (p.implicitDiffusion) {
-    const dim3 cgrd(mg_col_blocks(d.sNx, d.sNy, d.nT, d.Nr));
-    hipLaunchKernelGGL(k_tracer_impl, cgrd, blk, 0, s, d, p, f, a);
+    const long ncol = (long)d.sNx * d.sNy * d.nT;
+    const int nc = mg_colf_nc(ncol, d.Nr, 3);
+    MG_ALLOW_LDS(k_tracer_impl);
+    hipLaunchKernelGGL(k_tracer_impl, dim3(mg_colf_blocks(ncol, nc)), blk, mg_colf_lds(d.Nr, nc, 3), s, d, p, f, a, nc);
   }
   return hipGetLastError();
 }

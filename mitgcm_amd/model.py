@@ -182,6 +182,11 @@ class Model:
         k = lib().mgcm_get_param(self.h, b"cg2dKernel")
         return {4.0: "mwg", 3.0: "bxy", 2.0: "blk2"}.get(k, "block")
 
+    def cg2d_fma(self):
+        """True when the selected CG2D kernel solves in fused multiply-adds (cg2dUseFMA): the
+        device-order oracle must then evaluate the same fma chains (Oracle.set_sum_plan(fma=))."""
+        return lib().mgcm_get_param(self.h, b"cg2dFMA") != 0.0
+
     def cg2d_parts(self):
         """Workgroups (one per CU) the CG2D solve runs on."""
         return int(lib().mgcm_get_param(self.h, b"cg2dParts"))

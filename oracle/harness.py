@@ -58,6 +58,8 @@ def lib():
         L.oracle_exch_uv_xyz.argtypes = [vp, P, P, c_int, c_int]
         L.oracle_set_sum_plan.argtypes = [vp, IP, c_int, c_int, c_int]
         L.oracle_set_sum_plan.restype = c_int
+        L.oracle_set_cg2d_fma.argtypes = [vp, c_int]
+        L.oracle_set_cg2d_fma.restype = c_int
         _lib = L
     return _lib
 
@@ -85,9 +87,11 @@ class Oracle:
             if self.L.oracle_set_param(self.h, k.encode(), float(v)) != 0:
                 raise KeyError(k)
 
-    def set_sum_plan(self, plan, NT, PPT, NG=1):
+    def set_sum_plan(self, plan, NT, PPT, NG=1, fma=False):
         """Sum the CG2D dot products in the device's order (mitgcm_amd Model.cg2d_sum_plan());
-        plan=None restores GLOBAL_SUM_TILE_RL's tile order."""
+        fma: the device solves with fused multiply-adds (Model.cg2d_fma()); plan=None restores
+        GLOBAL_SUM_TILE_RL's tile order."""
+        assert self.L.oracle_set_cg2d_fma(self.h, 1 if fma else 0) == 0
         if plan is None:
             assert self.L.oracle_set_sum_plan(self.h, None, 0, 0, 0) == 0
             return

@@ -119,6 +119,7 @@ typedef struct OModel {
 
   /* --- summation order of the device CG2D (mgcm_cg2d_sum_plan), NULL = GLOBAL_SUM_TILE_RL --- */
   int *sumPlan, planNT, planPPT, planNG;
+  int cg2dFMA;   /* device-order mode: the device kernel's fused multiply-add chains (cg2dUseFMA) */
 
   /* --- outputs of the last SOLVE_FOR_PRESSURE --- */
   double firstResidual, minResidualSq, lastResidual, sumRHS, rhsMax;
@@ -167,6 +168,7 @@ void oracle_mom_vecinv(OModel *m, int t, int k, const double *hFacZ, const doubl
 void oracle_dynamics(OModel *m);                     /* DYNAMICS  (dynamics.F:21)  */
 void oracle_solve_for_pressure(OModel *m);           /* SOLVE_FOR_PRESSURE (solve_for_pressure.F:7) */
 int oracle_set_sum_plan(OModel *m, const int *plan, int NT, int PPT, int NG);
+int oracle_set_cg2d_fma(OModel *m, int on);
 void oracle_cg2d(OModel *m, double *cg2d_b, double *cg2d_x,
                  double *firstResidual, double *minResidualSq, double *lastResidual,
                  int *numIters, int *nIterMin);      /* CG2D (cg2d.F:13) */

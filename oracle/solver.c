@@ -42,13 +42,25 @@ int oracle_set_sum_plan(OModel *m, const int *plan, int NT, int PPT, int NG) {
   return 0;
 }
 
+/* With cg2dUseFMA the device evaluates the CG2D operator rows, dot products and vector
+ * updates as fused multiply-adds (kernels_solve.hip k_cg2d_bxy<..., FMA>); the device-order
+ * mode then does the same, with C99 fma() (one rounding, as v_fma_f64). */
+int oracle_set_cg2d_fma(OModel *m, int on) {
+  m->cg2dFMA = on ? 1 : 0;
+  return 0;
+}
+
 static double pairwise_tree(double *v, int n) {   /* n a power of two; destroys v */
   for (int w = 1; w < n; w *= 2)
     for (int t = 0; t < n; t += 2 * w) v[t] = v[t] + v[t + w];
   return v[0];
 }
 
-static double plan_sum(const OModel *m, const double *term) {
+/* plan_dot: the same order with each thread accumulating fma(a, b, acc) (b = NULL: acc + a) */
+static double plan_dot(const OModel *m, const double *a, const double *b);
+static double plan_sum(const OModel *m, const double *term) { return plan_dot(m, term, NULL); }
+static double plan_dot(const OModel *m, const double *a, const double *b) {
+  const double *term = a;
   int np2 = 1;
   while (np2 < m->planNT) np2 *= 2;
   double *th = calloc((size_t)np2, sizeof(double)), lanes[64];
@@ -59,7 +71,7 @@ static double plan_sum(const OModel *m, const double *term) {
       double e = 0.0;
       for (int p = 0; p < m->planPPT; p++) {
         const int q = m->sumPlan[((size_t)g * m->planPPT + p) * m->planNT + t];
-        if (q >= 0) e = e + term[q];
+        if (q >= 0) e = b ? fma(term[q], b[q], e) : e + term[q];
       }
       th[t] = e;
     }
@@ -128,6 +140,14 @@ int oracle_ini_cg2d(OModel *m) {
   return 0;
 }
 
+/* A x at (i,j) as the device's fma chain: aW*w, then + aW(i+1)*e, aS*s, aS(j+1)*n, aC*v */
+static double applyA_fma(const OModel *m, const double *v, int i, int j, int t) {
+  const double *aW = m->aW2d, *aS = m->aS2d, *aC = m->aC2d;
+  const long p = O2(m, i, j, t);
+  return fma(aC[p], v[p], fma(aS[O2(m, i, j + 1, t)], v[O2(m, i, j + 1, t)], fma(aS[p], v[O2(m, i, j - 1, t)],
+             fma(aW[O2(m, i + 1, j, t)], v[O2(m, i + 1, j, t)], aW[p] * v[O2(m, i - 1, j, t)]))));
+}
+
 /* CG2D (model/src/cg2d.F:13-415), default branch (no CG2D_SINGLECPU_SUM) */
 void oracle_cg2d(OModel *m, double *cg2d_b, double *cg2d_x, double *firstResidual,
                  double *minResidualSq, double *lastResidual, int *numIters, int *nIterMin) {
@@ -136,7 +156,7 @@ void oracle_cg2d(OModel *m, double *cg2d_b, double *cg2d_x, double *firstResidua
   double *r = calloc(N2, 8), *s = calloc(N2, 8), *q = calloc(N2, 8), *xmin = calloc(N2, 8);
   double *tile = calloc(nT, 8), *tile2 = calloc(nT, 8);
   double *term = calloc(N2, 8), *term2 = calloc(N2, 8);   /* per-point terms for a device sum plan */
-  const int dev = m->sumPlan != NULL;
+  const int dev = m->sumPlan != NULL, fmaMode = dev && m->cg2dFMA;
   const double *aW = m->aW2d, *aS = m->aS2d, *aC = m->aC2d, *pW = m->pW, *pS = m->pS, *pC = m->pC;
   double err_sq, eta_qrN, eta_qrNM1 = 1.0, cgBeta, alpha, sumRHS, rhsMax = 0.0, rhsNorm = 1.0;
   int actualIts = 0;
@@ -168,9 +188,12 @@ void oracle_cg2d(OModel *m, double *cg2d_b, double *cg2d_x, double *firstResidua
     for (int j = 1; j <= sNy; j++)
       for (int i = 1; i <= sNx; i++) {
         long p = O2(m, i, j, t);
-        r[p] = cg2d_b[p] - (aW[p] * cg2d_x[O2(m, i - 1, j, t)] + aW[O2(m, i + 1, j, t)] * cg2d_x[O2(m, i + 1, j, t)] +
-                            aS[p] * cg2d_x[O2(m, i, j - 1, t)] + aS[O2(m, i, j + 1, t)] * cg2d_x[O2(m, i, j + 1, t)] +
-                            aC[p] * cg2d_x[p]);
+        if (fmaMode)
+          r[p] = cg2d_b[p] - applyA_fma(m, cg2d_x, i, j, t);
+        else
+          r[p] = cg2d_b[p] - (aW[p] * cg2d_x[O2(m, i - 1, j, t)] + aW[O2(m, i + 1, j, t)] * cg2d_x[O2(m, i + 1, j, t)] +
+                              aS[p] * cg2d_x[O2(m, i, j - 1, t)] + aS[O2(m, i, j + 1, t)] * cg2d_x[O2(m, i, j + 1, t)] +
+                              aC[p] * cg2d_x[p]);
         errT = errT + r[p] * r[p];
         sumT = sumT + cg2d_b[p];
         term[p] = r[p] * r[p];
@@ -180,7 +203,7 @@ void oracle_cg2d(OModel *m, double *cg2d_b, double *cg2d_x, double *firstResidua
   }
   /* EXCH_S3D_RL(cg2d_r, 1): halo width 1 fill; the full-halo periodic copy is a superset */
   oracle_exch_xy(m, r);
-  err_sq = dev ? plan_sum(m, term) : gsum_tiles(tile, nT);
+  err_sq = dev ? (fmaMode ? plan_dot(m, r, r) : plan_sum(m, term)) : gsum_tiles(tile, nT);
   sumRHS = dev ? plan_sum(m, term2) : gsum_tiles(tile2, nT);
   *firstResidual = sqrt(err_sq);
   if (*nIterMin >= 0) { *nIterMin = 0; *minResidualSq = err_sq; }
@@ -192,21 +215,25 @@ void oracle_cg2d(OModel *m, double *cg2d_b, double *cg2d_x, double *firstResidua
         for (int j = 1; j <= sNy; j++)
           for (int i = 1; i <= sNx; i++) {
             long p = O2(m, i, j, t);
-            q[p] = pC[p] * r[p] + pW[p] * r[O2(m, i - 1, j, t)] + pW[O2(m, i + 1, j, t)] * r[O2(m, i + 1, j, t)] +
-                   pS[p] * r[O2(m, i, j - 1, t)] + pS[O2(m, i, j + 1, t)] * r[O2(m, i, j + 1, t)];
+            if (fmaMode)
+              q[p] = fma(pS[O2(m, i, j + 1, t)], r[O2(m, i, j + 1, t)], fma(pS[p], r[O2(m, i, j - 1, t)],
+                     fma(pW[O2(m, i + 1, j, t)], r[O2(m, i + 1, j, t)], fma(pW[p], r[O2(m, i - 1, j, t)], pC[p] * r[p]))));
+            else
+              q[p] = pC[p] * r[p] + pW[p] * r[O2(m, i - 1, j, t)] + pW[O2(m, i + 1, j, t)] * r[O2(m, i + 1, j, t)] +
+                     pS[p] * r[O2(m, i, j - 1, t)] + pS[O2(m, i, j + 1, t)] * r[O2(m, i, j + 1, t)];
             e = e + q[p] * r[p];
             term[p] = q[p] * r[p];
           }
         tile[t] = e;
       }
-      eta_qrN = dev ? plan_sum(m, term) : gsum_tiles(tile, nT);
+      eta_qrN = dev ? (fmaMode ? plan_dot(m, q, r) : plan_sum(m, term)) : gsum_tiles(tile, nT);
       cgBeta = eta_qrN / eta_qrNM1;
       eta_qrNM1 = eta_qrN;
       for (int t = 0; t < nT; t++)
         for (int j = 1; j <= sNy; j++)
           for (int i = 1; i <= sNx; i++) {
             long p = O2(m, i, j, t);
-            s[p] = q[p] + cgBeta * s[p];
+            s[p] = fmaMode ? fma(cgBeta, s[p], q[p]) : q[p] + cgBeta * s[p];
           }
       oracle_exch_xy(m, s);
       for (int t = 0; t < nT; t++) {
@@ -214,29 +241,32 @@ void oracle_cg2d(OModel *m, double *cg2d_b, double *cg2d_x, double *firstResidua
         for (int j = 1; j <= sNy; j++)
           for (int i = 1; i <= sNx; i++) {
             long p = O2(m, i, j, t);
-            q[p] = aW[p] * s[O2(m, i - 1, j, t)] + aW[O2(m, i + 1, j, t)] * s[O2(m, i + 1, j, t)] +
-                   aS[p] * s[O2(m, i, j - 1, t)] + aS[O2(m, i, j + 1, t)] * s[O2(m, i, j + 1, t)] + aC[p] * s[p];
+            if (fmaMode)
+              q[p] = applyA_fma(m, s, i, j, t);
+            else
+              q[p] = aW[p] * s[O2(m, i - 1, j, t)] + aW[O2(m, i + 1, j, t)] * s[O2(m, i + 1, j, t)] +
+                     aS[p] * s[O2(m, i, j - 1, t)] + aS[O2(m, i, j + 1, t)] * s[O2(m, i, j + 1, t)] + aC[p] * s[p];
             a = a + s[p] * q[p];
             term[p] = s[p] * q[p];
           }
         tile[t] = a;
       }
-      alpha = dev ? plan_sum(m, term) : gsum_tiles(tile, nT);
+      alpha = dev ? (fmaMode ? plan_dot(m, s, q) : plan_sum(m, term)) : gsum_tiles(tile, nT);
       alpha = eta_qrN / alpha;
       for (int t = 0; t < nT; t++) {
         double e = 0.0;
         for (int j = 1; j <= sNy; j++)
           for (int i = 1; i <= sNx; i++) {
             long p = O2(m, i, j, t);
-            cg2d_x[p] = cg2d_x[p] + alpha * s[p];
-            r[p] = r[p] - alpha * q[p];
+            cg2d_x[p] = fmaMode ? fma(alpha, s[p], cg2d_x[p]) : cg2d_x[p] + alpha * s[p];
+            r[p] = fmaMode ? fma(-alpha, q[p], r[p]) : r[p] - alpha * q[p];
             e = e + r[p] * r[p];
             term[p] = r[p] * r[p];
           }
         tile[t] = e;
       }
       actualIts = it2d;
-      err_sq = dev ? plan_sum(m, term) : gsum_tiles(tile, nT);
+      err_sq = dev ? (fmaMode ? plan_dot(m, r, r) : plan_sum(m, term)) : gsum_tiles(tile, nT);
       if (err_sq < m->cg2dTolerance_sq) break;
       if (err_sq < *minResidualSq) {
         *minResidualSq = err_sq;

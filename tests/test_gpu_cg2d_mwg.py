@@ -43,7 +43,7 @@ def test_mwg_ocean90_bitexact_vs_device_order_oracle():
     plan, NT, PPT, NG = m.cg2d_sum_plan()
     assert NG == 4
     od, g = ocean90_oracle()
-    od.set_sum_plan(plan, NT, PPT, NG)
+    od.set_sum_plan(plan, NT, PPT, NG, fma=m.cg2d_fma())
     o_ref, _ = ocean90_oracle()
     for step in range(1, 7):
         m.forward_step(1)

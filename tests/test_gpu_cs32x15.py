@@ -112,7 +112,7 @@ def test_cs32x15_8_steps_vs_oracle():
     m = _model()
     plan, NT, PPT, NG = m.cg2d_sum_plan()
     od_dev, _ = _oracle(0)
-    od_dev.set_sum_plan(plan, NT, PPT, NG)
+    od_dev.set_sum_plan(plan, NT, PPT, NG, fma=m.cg2d_fma())
     from mitgcm_amd.model import dynstat
     worst = (99.0, None)
     for step in range(1, 9):

@@ -25,7 +25,7 @@ def test_llc30_8_steps_bitexact_vs_device_order_oracle():
     assert m.cg2d_kernel() == "mwg"
     plan, NT, PPT, NG = m.cg2d_sum_plan()
     od, g = oracle_from_config(cfg)
-    od.set_sum_plan(plan, NT, PPT, NG)
+    od.set_sum_plan(plan, NT, PPT, NG, fma=m.cg2d_fma())
     o_ref, _ = oracle_from_config(cfg)
     for step in range(1, 9):
         m.forward_step(1)

@@ -116,10 +116,11 @@ def test_ocean90_10_steps(golden_dir):
     m = _model()
     plan, NT, PPT, NG = m.cg2d_sum_plan()
     od_dev, _ = _oracle(0)       # the device's summation order
-    od_dev.set_sum_plan(plan, NT, PPT, NG)
+    fma = m.cg2d_fma()
+    od_dev.set_sum_plan(plan, NT, PPT, NG, fma=fma)
     gold = json.load(open(os.path.join(golden_dir, EXP, "monitor.json")))
     from mitgcm_amd.model import dynstat
-    worst_o, worst_r = (99.0, None), (99.0, None)
+    worst_o, worst_r, worst_d = (99.0, None), (99.0, None), (99.0, None)
     for step in range(1, 11):
         m.forward_step(1)
         o.forward_step()
@@ -133,6 +134,8 @@ def test_ocean90_10_steps(golden_dir):
                 assert v == dd[k], ("device-order oracle", step, k, v, dd[k])
             if k in od and k != "cg2d_iters" and not k.startswith("cg2d"):
                 worst_o = min(worst_o, (digits(v, od[k]), (step, k, v, od[k])))
+                if not k.endswith("_mean"):
+                    worst_d = min(worst_d, (digits(v, od[k]), (step, k)))
             if k in gold[step] and k not in ("cg2d_iters", "dynstat_eta_mean", "cg2d_last_res"):
                 worst_r = min(worst_r, (digits(v, gold[step][k]), (step, k, v, gold[step][k])))
         worst_o = min(worst_o, (digits(md["cg2d_init_res"], od["cg2d_init_res"]), (step, "cg2d_init_res")))
@@ -142,7 +145,8 @@ def test_ocean90_10_steps(golden_dir):
         inner = (Ellipsis,) + g.sl(1, g.sNx, 1, g.sNy)
         assert np.array_equal(dev[inner], ref[inner]), (n, np.abs(dev - ref)[inner].max())
     m.close()
-    print("ocean90 10 steps: device == device-order oracle bit for bit; vs reference-order oracle %.2f at %s; "
-          "vs results/output.txt %.2f at %s" % (worst_o + worst_r))
+    print("ocean90 10 steps (cg2dUseFMA=%d): device == device-order oracle bit for bit; vs reference-order oracle "
+          "%.2f at %s; vs results/output.txt %.2f at %s; dynstat series vs the oracle %.2f at %s" % (
+              (fma,) + worst_o + worst_r + worst_d))
     assert worst_o[0] >= 10.0, worst_o
     assert worst_r[0] >= 10.0, worst_r
