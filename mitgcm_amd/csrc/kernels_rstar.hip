@@ -65,45 +65,53 @@ __global__ void __launch_bounds__(256) k_calc_r_star(Dims d, Params p, Fields f,
 }
 
 // UPDATE_R_STAR(.TRUE.) (update_r_star.F:60-92) and UPDATE_CG2D part 1
-// (update_cg2d.F:82-143) in one pass, one thread per 2-D point walking its column:
-// hFac = h0Fac*rStarFac and recip_hFac = 1/hFac where wet (USE_MASK_AND_NO_IF undefined)
-// at every level, and on 1..sNx+1 x 1..sNy+1 the operator sums aW2d, aS2d = Sum_k
-// faceArea*recip_dx/yC (k order) scaled by cg2dNorm*implicSurfPress*implicDiv2DFlow
-// (0 elsewhere).  Stores of a level are coalesced over i.
-__global__ void __launch_bounds__(256) k_update_r_star_cg2d_a(Dims d, Params p, Fields f) {
-  const long q = (long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (q >= d.n2 * d.nTiles) return;
-  const int t = (int)(q / d.n2);
-  if (t < d.t0 || t >= d.t0 + d.nT) return;
-  const long l = q % d.n2;
-  const int i = (int)(l % d.nx) - d.OLx + 1, j = (int)(l / d.nx) - d.OLy + 1;
+// (update_cg2d.F:82-143) in one pass over the columns of every 2-D point (column frame,
+// common.h MG_COLF): each thread rewrites hFac = h0Fac*rStarFac and recip_hFac = 1/hFac
+// (where wet; USE_MASK_AND_NO_IF undefined) at its levels, k-parallel and coalesced over i,
+// and stages the operator terms faceArea*recip_dx/yC of its levels in LDS; thread (c, 0)
+// then sums aW2d, aS2d in k order on 1..sNx+1 x 1..sNy+1 and scales them by
+// cg2dNorm*implicSurfPress*implicDiv2DFlow (0 elsewhere).
+__global__ void __launch_bounds__(256) k_update_r_star_cg2d_a(Dims d, Params p, Fields f, int nc) {
+  extern __shared__ __attribute__((aligned(16))) double lds[];
+  MG_COLF(1 - d.OLx, d.nx, 1 - d.OLy, d.ny, nc)
+  const int NS = d.Nr * NC_;
+  double *sW = lds, *sS = lds + NS;
+  const long q = MG_I2(d, i, j, t);
   const bool op = p.nonlinFreeSurf > 2 && i >= 1 && i <= d.sNx + 1 && j >= 1 && j <= d.sNy + 1;
-  const double fc = f.rStarFacC[q], fw = f.rStarFacW[q], fs = f.rStarFacS[q];
+  if (valid) {
+    const double fc = f.rStarFacC[q], fw = f.rStarFacW[q], fs = f.rStarFacS[q];
+    MG_COLF_K(k) {
+      const long q3 = MG_I3(d, i, j, k, t);
+      const double hC = f.h0FacC[q3] * fc, hW = f.h0FacW[q3] * fw, hS = f.h0FacS[q3] * fs;
+      f.hFacC[q3] = hC;
+      f.hFacW[q3] = hW;
+      f.hFacS[q3] = hS;
+      if (f.maskC[q3] != 0.0) f.recip_hFacC[q3] = 1.0 / hC;
+      if (f.maskW[q3] != 0.0) f.recip_hFacW[q3] = 1.0 / hW;
+      if (f.maskS[q3] != 0.0) f.recip_hFacS[q3] = 1.0 / hS;
+      if (op) {
+        const int me = (k - 1) * NC_ + cc;
+        double faceArea = f.dyG[q] * f.drF[k - 1] * hW;
+        sW[me] = faceArea * f.recip_dxC[q];
+        faceArea = f.dxG[q] * f.drF[k - 1] * hS;
+        sS[me] = faceArea * f.recip_dyC[q];
+      }
+    }
+  }
+  __syncthreads();
+  if (!valid || kk != 0 || p.nonlinFreeSurf <= 2) return;
   double aW = 0.0, aS = 0.0;
-  for (int k = 1; k <= d.Nr; k++) {
-    const long q3 = q + (long)(k - 1) * d.n2 + (long)t * (d.n3 - d.n2);
-    const double hC = f.h0FacC[q3] * fc, hW = f.h0FacW[q3] * fw, hS = f.h0FacS[q3] * fs;
-    f.hFacC[q3] = hC;
-    f.hFacW[q3] = hW;
-    f.hFacS[q3] = hS;
-    if (f.maskC[q3] != 0.0) f.recip_hFacC[q3] = 1.0 / hC;
-    if (f.maskW[q3] != 0.0) f.recip_hFacW[q3] = 1.0 / hW;
-    if (f.maskS[q3] != 0.0) f.recip_hFacS[q3] = 1.0 / hS;
-    if (op) {
-      double faceArea = f.dyG[q] * f.drF[k - 1] * hW;
-      aW = aW + faceArea * f.recip_dxC[q];
-      faceArea = f.dxG[q] * f.drF[k - 1] * hS;
-      aS = aS + faceArea * f.recip_dyC[q];
+  if (op) {
+    for (int k = 1; k <= d.Nr; k++) {
+      const int me = (k - 1) * NC_ + cc;
+      aW = aW + sW[me];
+      aS = aS + sS[me];
     }
+    aW = aW * p.cg2dNorm * p.implicSurfPress * p.implicDiv2DFlow;
+    aS = aS * p.cg2dNorm * p.implicSurfPress * p.implicDiv2DFlow;
   }
-  if (p.nonlinFreeSurf > 2) {
-    if (op) {
-      aW = aW * p.cg2dNorm * p.implicSurfPress * p.implicDiv2DFlow;
-      aS = aS * p.cg2dNorm * p.implicSurfPress * p.implicDiv2DFlow;
-    }
-    f.aW2d[q] = aW;
-    f.aS2d[q] = aS;
-  }
+  f.aW2d[q] = aW;
+  f.aS2d[q] = aS;
 }
 
 // UPDATE_CG2D part 2 (update_cg2d.F:144-199): aC2d on the interior, EXCH_XY_RS(aC2d)
@@ -149,7 +157,11 @@ hipError_t launch_calc_r_star(const Dims &d, const Params &p, const Fields &f, c
 hipError_t launch_update_r_star_cg2d(const Dims &d, const Params &p, const Fields &f, const long *srcOf, hipStream_t s) {
   const long n = d.n2 * d.nTiles;
   const unsigned nb = (unsigned)((n + 255) / 256);
-  hipLaunchKernelGGL(k_update_r_star_cg2d_a, dim3(nb), dim3(256), 0, s, d, p, f);
+  const long ncol = (long)d.nx * d.ny * d.nT;
+  const int nc = mg_colf_nc(ncol, d.Nr, 2);
+  MG_ALLOW_LDS(k_update_r_star_cg2d_a);
+  hipLaunchKernelGGL(k_update_r_star_cg2d_a, dim3(mg_colf_blocks(ncol, nc)), dim3(256), mg_colf_lds(d.Nr, nc, 2), s, d, p,
+                     f, nc);
   if (p.nonlinFreeSurf > 2) hipLaunchKernelGGL(k_update_cg2d_p, dim3(nb), dim3(256), 0, s, d, p, f, srcOf);
   return hipGetLastError();
 }
