@@ -239,6 +239,8 @@ def read_pickup(g, path, Nx, Ny):
     big-endian, global Nx x Ny records) -> tile layout with halos exchanged, as
     READ_PICKUP's EXCH calls leave them (read_pickup.F:545-575)."""
     Nr = g.Nr
+    if not os.path.exists(path) and os.path.exists(path + ".data"):
+        path = path + ".data"   # written by pickup.write_pickup (MDS name); the fixture has none
     raw = np.fromfile(path, dtype=">f8").astype(np.float64)
     nrec = len(PICKUP_FIELDS) * Nr + len(PICKUP_2D)
     if raw.size != nrec * Nx * Ny:
@@ -257,6 +259,8 @@ def read_pickup_cd(g, path, Nx, Ny):
     """CD_CODE_READ_PICKUP (pkg/cd_code/cd_code_read_pickup.F:53-69): uVelD, vVelD,
     uNM1, vNM1 (Nr records each) and etaNm1 (record 4*Nr+1)."""
     Nr = g.Nr
+    if not os.path.exists(path) and os.path.exists(path + ".data"):
+        path = path + ".data"
     raw = np.fromfile(path, dtype=">f8").astype(np.float64).reshape(-1, Ny, Nx)
     out = {}
     for n, name in enumerate(PICKUP_CD):
@@ -265,7 +269,7 @@ def read_pickup_cd(g, path, Nx, Ny):
     return out
 
 
-def global_ocean_90x40x15(nSx=1, nSy=1, OL=3, data_dir=None, pickup_dir=None):
+def global_ocean_90x40x15(nSx=1, nSy=1, OL=3, data_dir=None, pickup_dir=None, nIter0=36000):
     """verification/global_ocean.90x40x15 (BASELINE config 2): the lat-lon grid, bathymetry
     and monthly forcing of tutorial_global_oce_latlon (input/prepare_run links them),
     restarted from pickup.0000036000 + pickup_cd.0000036000.  input/data differences:
@@ -273,12 +277,13 @@ def global_ocean_90x40x15(nSx=1, nSy=1, OL=3, data_dir=None, pickup_dir=None):
     (selectP_inEOS_Zc=2: pressure from totPhiHyd), ivdc_kappa=10, select_rStar=2,
     nonlinFreeSurf=4 (r* coordinate, UPDATE_CG2D every step), hFacInf=0.2, hFacSup=2,
     quasiHydrostatic + useNHMTerms (+ use3dCoriolis default), doResetHFactors,
-    nIter0=36000.  Returns (grid, params, state, forcing); state includes the pickups."""
+    nIter0=36000 (another nIter0 restarts from pickup(_cd).<nIter0> in pickup_dir, e.g. one
+    pickup.write_pickup wrote).  Returns (grid, params, state, forcing); state includes the
+    pickups."""
     d = data_dir or os.path.join(GOLDEN, "tutorial_global_oce_latlon")
     pd = pickup_dir or os.path.join(GOLDEN, "global_ocean.90x40x15")
     g, params, state, forcing = global_oce_latlon(nSx=nSx, nSy=nSy, OL=OL, data_dir=d)
     Nx, Ny, Nr = 90, 40, 15
-    nIter0 = 36000
     params.update(viscA4D=1e14, viscA4Z=1e14, ivdc_kappa=10.0, nIter0=nIter0, myIter=nIter0,
                   myTime=nIter0 * 86400.0, selectP_inEOS_Zc=2, storePhiHyd4Phys=1, nonlinFreeSurf=4,
                   select_rStar=2, hFacInf=0.2, hFacSup=2.0, quasiHydrostatic=1, useNHMTerms=1,

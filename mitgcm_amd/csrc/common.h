@@ -33,7 +33,7 @@ struct Dims {
     X(cg2d_b) X(cg2d_x) X(Qnet) X(EmPmR) X(SSS) X(lambdaSaltClimRelax) X(etaNm1) X(fCoriCos) X(recip_Rcol) \
     X(rSurfW) X(rSurfS) X(rLowW) X(rLowS) X(Ro_surf) X(R_low) X(rStarFacC) X(rStarFacW) X(rStarFacS) \
     X(rStarExpC) X(rStarExpW) X(rStarExpS) X(rStarDhCDt) X(rStarDhWDt) X(rStarDhSDt) X(PmEpR) X(dEtaHdt) \
-    X(maskInW) X(maskInS) X(fCoriG) X(recip_rAz) X(recip_dxG) X(recip_dyG)
+    X(maskInW) X(maskInS) X(fCoriG) X(recip_rAz) X(recip_dxG) X(recip_dyG) X(etaHnm1)
 #define MG_F3D_LIST(X) X(hFacC) X(hFacW) X(hFacS) X(recip_hFacC) X(recip_hFacW) X(recip_hFacS) X(maskC) X(maskW) \
     X(maskS) X(uVel) X(vVel) X(wVel) X(theta) X(salt) X(gU) X(gV) X(guNm1) X(gvNm1) X(rhoInSitu) X(IVDConvCount) \
     X(gtNm1) X(thetaNext) X(gTscr) X(cpScr) X(phiHydC) X(saltNext) X(gsNm1) X(advScr1) X(advScr2) X(gAdv) \
@@ -120,6 +120,7 @@ struct Fields {
   double *totPhiHyd, *alphaRho, *del2u, *del2v;                            // 3-D
   double *rStarFacC, *rStarFacW, *rStarFacS, *rStarExpC, *rStarExpW, *rStarExpS;   // 2-D
   double *rStarDhCDt, *rStarDhWDt, *rStarDhSDt, *PmEpR, *dEtaHdt;          // 2-D
+  double *etaHnm1;   // 2-D: etaH before UPDATE_ETAH (update_etah.F:49-53), WRITE_PICKUP's EtaH record
   const double *maskInW, *maskInS;                                         // 2-D: kSurfW/S <= Nr
   double *dWtC, *dWtU, *dWtV;   // 3-D: MOM_CALC_RTRANS's dWtransC/U/V at each level (k_phi_hyd)
   // vector-invariant momentum on curvilinear / cube grids

@@ -1048,6 +1048,7 @@ __global__ void __launch_bounds__(256) k_exch_etaH(Dims d, Params p, Fields f, c
     const int i = (int)(l % d.nx) - d.OLx + 1, j = (int)(l / d.nx) - d.OLy + 1;
     x = (i >= 1 && i <= d.sNx && j >= 1 && j <= d.sNy) ? e[q] : f.etaN[q];
   }
+  f.etaHnm1[q] = f.etaH[q];   // update_etah.F:49-53: the etaH being replaced (pickup EtaH record)
   f.etaN[q] = x;
   f.etaH[q] = x;
 }

@@ -147,6 +147,10 @@ class Model:
     def solve_for_pressure(self):
         check(lib().mgcm_solve_for_pressure(self.h), "mgcm_solve_for_pressure")
 
+    def my_iter(self):
+        """The device-side iteration counter (myIter of the state currently held)."""
+        return int(lib().mgcm_get_param(self.h, b"myIter"))
+
     def sync(self):
         check(lib().mgcm_sync(self.h), "mgcm_sync")
 
