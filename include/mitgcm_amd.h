@@ -159,6 +159,12 @@ int mgcm_cg2d_sum_plan(mgcm_model *m, int *plan, long capacity, int *NT, int *PP
 int mgcm_solve_stats(mgcm_model *m, int back, double *firstResidual, double *lastResidual,
                      int *numIters, double *rhsMax);
 
+/* MONITOR's dynstat block (pkg/monitor/monitor.F:103-129 -> MON_CALC_STATS_RL,
+ * mon_calc_stats_rl.F / mon_stats_rl.F:104-107) computed on the device, no field download:
+ * out[6*5] = (max, min, mean, sd, del2) of eta, uvel, vvel, wvel, theta, salt over this
+ * process's tiles (per-plane tree partials added in tile, level order). */
+int mgcm_monitor(mgcm_model *m, double *out);
+
 /* Average device time (ms) of each kernel family over the last timed region,
  * measured with hipEvents on the model's stream.  name: "mom_step", "cg2d", ... */
 double mgcm_kernel_ms(mgcm_model *m, const char *name, int *launches);

@@ -265,6 +265,18 @@ struct MwgTables {
   size_t hsBytes;
 };
 
+// MONITOR dynstat on the device (kernels_monitor.hip): one field's arrays; arr3d / hf3d:
+// 3-D (tile stride n3, level stride n2) or 2-D (tile stride n2)
+struct MonSpec {
+  const double *arr, *hfac, *mask, *area, *dr;
+  int nz, arr3d, hf3d;
+};
+constexpr int MON_NF = 6, MON_NV = 6;   // eta, u, v, w, theta, salt; plane values nb, del2, vol, sum, min, max
+struct MonSpecs {
+  MonSpec s[MON_NF];
+  double mean[MON_NF];
+};
+
 // Per-solve record written by the device CG2D (one slot per time step).
 struct SolveRecord {
   double firstResidual, lastResidual, minResidualSq, rhsMax, sumRHS;

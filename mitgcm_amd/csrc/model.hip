@@ -45,6 +45,7 @@ hipError_t launch_update_r_star_cg2d(const Dims &, const Params &, const Fields 
 hipError_t launch_halo_pack(const Dims &, const XFields &, const long *, long, double *, int, hipStream_t);
 hipError_t launch_oceanic_phys(const Dims &, const Params &, const Fields &, const int *, hipStream_t);
 hipError_t launch_tracer_step(const Dims &, const Params &, const Fields &, const TracerArgs &, const int *, hipStream_t);
+hipError_t launch_mon_stats(const Dims &, const MonSpecs &, int, double *, int, hipStream_t);
 int cg2d_mwg_geometry(int *, int *, int *);
 hipError_t launch_cg2d_mwg(const Dims &, const Params &, const Fields &, const MwgTables &, int, SolveRecord *, int *,
                            hipStream_t);
@@ -187,6 +188,8 @@ struct mgcm_model {
   SolveRecord *d_rec = nullptr;
   int maxRec = 4096;
   int lastBatch = 0;
+  double *monBuf = nullptr;   // MONITOR plane partials (mgcm_monitor)
+  size_t monCap = 0;
   bool ready = false;
   // timing
   bool timing = false;
@@ -750,6 +753,7 @@ void mgcm_destroy(mgcm_model *m) {
   ev_free(m);
   drop_graphs(m);
   for (void *p : m->allocs) hipFree(p);
+  if (m->monBuf) hipFree(m->monBuf);
   if (m->d_halo) hipFree(m->d_halo);
   if (m->d_srcOf) hipFree(m->d_srcOf);
   for (int q = 0; q < 2; q++) {
@@ -1479,6 +1483,63 @@ int mgcm_solve_stats(mgcm_model *m, int back, double *firstResidual, double *las
   if (lastResidual) *lastResidual = r.lastResidual;
   if (numIters) *numIters = r.numIters;
   if (rhsMax) *rhsMax = r.rhsMax;
+  return 0;
+}
+
+// MONITOR's dynstat block (pkg/monitor/monitor.F:103-129, MON_CALC_STATS_RL) on the device:
+// plane partials by k_mon_stats, added here in (tile, level) order; out[6][5] = (max, min,
+// mean, sd, del2) of eta, uvel, vvel, wvel, theta, salt over this process's tiles.
+int mgcm_monitor(mgcm_model *m, double *out) {
+  if (check_ready(m)) return -1;
+  HIPCHK(hipSetDevice(m->device));
+  const Dims &d = m->d;
+  const Fields &f = m->f;
+  const int nzmax = d.Nr;
+  const size_t nval = (size_t)MON_NF * d.nT * nzmax * MON_NV;
+  if (m->monCap < nval) {
+    if (m->monBuf) (void)hipFree(m->monBuf);
+    m->monBuf = nullptr;
+    HIPCHK(hipMalloc(&m->monBuf, nval * sizeof(double)));
+    m->monCap = nval;
+  }
+  MonSpecs S{};
+  S.s[0] = MonSpec{f.etaN, f.maskInC, f.maskInC, f.rA, f.drF, 1, 0, 0};
+  S.s[1] = MonSpec{f.uVel, f.hFacW, f.maskInW, f.rAw, f.drF, d.Nr, 1, 1};
+  S.s[2] = MonSpec{f.vVel, f.hFacS, f.maskInS, f.rAs, f.drF, d.Nr, 1, 1};
+  S.s[3] = MonSpec{f.wVel, f.maskC, f.maskInC, f.rA, f.drC, d.Nr, 1, 1};
+  S.s[4] = MonSpec{f.theta, f.hFacC, f.maskInC, f.rA, f.drF, d.Nr, 1, 1};
+  S.s[5] = MonSpec{f.salt, f.hFacC, f.maskInC, f.rA, f.drF, d.Nr, 1, 1};
+  std::vector<double> h(nval);
+  double nb[MON_NF], d2[MON_NF], vol[MON_NF], sum[MON_NF], mn[MON_NF], mx[MON_NF], sd[MON_NF];
+  for (int pass = 0; pass < 2; pass++) {
+    HIPCHK(launch_mon_stats(d, S, nzmax, m->monBuf, pass, m->stream));
+    HIPCHK(hipMemcpyAsync(h.data(), m->monBuf, nval * sizeof(double), hipMemcpyDeviceToHost, m->stream));
+    HIPCHK(hipStreamSynchronize(m->stream));
+    for (int fi = 0; fi < MON_NF; fi++) {
+      double a[MON_NV] = {0.0, 0.0, 0.0, 0.0, INFINITY, -INFINITY};
+      for (int t = 0; t < d.nT; t++)
+        for (int k = 0; k < S.s[fi].nz; k++) {
+          const double *v = &h[(((size_t)fi * d.nT + t) * nzmax + k) * MON_NV];
+          for (int q = 0; q < 4; q++) a[q] = a[q] + v[q];
+          a[4] = fmin(a[4], v[4]);
+          a[5] = fmax(a[5], v[5]);
+        }
+      if (pass == 0) {
+        nb[fi] = a[0]; d2[fi] = a[1]; vol[fi] = a[2]; sum[fi] = a[3]; mn[fi] = a[4]; mx[fi] = a[5];
+        S.mean[fi] = vol[fi] > 0.0 ? sum[fi] / vol[fi] : 0.0;
+      } else {
+        sd[fi] = vol[fi] > 0.0 ? sqrt(a[3] / vol[fi]) : 0.0;
+      }
+    }
+  }
+  for (int fi = 0; fi < MON_NF; fi++) {
+    const bool any = nb[fi] > 0.0;   // mon_calc_stats_rl.F: min = max = 0 with no wet point
+    out[fi * 5 + 0] = any ? mx[fi] : 0.0;
+    out[fi * 5 + 1] = any ? mn[fi] : 0.0;
+    out[fi * 5 + 2] = S.mean[fi];
+    out[fi * 5 + 3] = sd[fi];
+    out[fi * 5 + 4] = any ? sqrt(d2[fi]) / nb[fi] : 0.0;
+  }
   return 0;
 }
 

@@ -204,6 +204,19 @@ class Model:
         return ms, n.value
 
 
+MON_FIELDS = ("eta", "uvel", "vvel", "wvel", "theta", "salt")
+MON_STATS = ("max", "min", "mean", "sd", "del2")
+
+
+def monitor(model):
+    """The dynstat block of MONITOR computed on the device (mgcm_monitor): the same keys as
+    dynstat(), without downloading the fields."""
+    out = np.zeros(len(MON_FIELDS) * len(MON_STATS))
+    check(lib().mgcm_monitor(model.h, _dp(out)), "mgcm_monitor")
+    return {"dynstat_%s_%s" % (f, s): float(out[i * 5 + j]) for i, f in enumerate(MON_FIELDS)
+            for j, s in enumerate(MON_STATS)}
+
+
 def mon_stats(g, arr, hfac, mask, area, dr):
     """MON_CALC_STATS_RL (pkg/monitor/mon_calc_stats_rl.F) -- host-side monitor of
     downloaded fields; arr/hfac (nTiles, nz, ny, nx), mask/area (nTiles, ny, nx).
