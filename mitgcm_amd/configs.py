@@ -394,6 +394,62 @@ def solid_body_cs32(data_dir=None):
     return g, params, state
 
 
+def advect_cs(data_dir=None, grid_dir=None):
+    """verification/advect_cs: cubed sphere, 6 faces of 32x32 (pkg/exch2, code/SIZE.h
+    sNx=sNy=32, OL=4, one tile per face), 1 level (delR=1e5, Ro_SeaLevel=1e5: no bathymetry),
+    momStepping=F: the solid-body rotation of code/ini_vel.F (psi = fac*fCoriG with
+    omegaprime = 38.60328935834681/rSphere) advects theta from T.init with the DST3
+    flux-limited multi-dimensional scheme (tempAdvScheme=33: the cube's 3-pass split,
+    gad_advection.F:339-367) and GAD_MULTIDIM_COMPRESSIBLE (code/GAD_OPTIONS.h); deltaT=2700,
+    no diffusion.  The grid is grid_cs32.faceNNN.bin (input/prepare_run; the same files as
+    global_ocean.cs32x15).  Salt uses scheme 80 in the reference and does not feed back: it is
+    not stepped here."""
+    from math import pi
+    d = data_dir or os.path.join(GOLDEN, "advect_cs")
+    gd = grid_dir or os.path.join(GOLDEN, "global_ocean.cs32x15")
+    n = 32
+    topo = cube_topology(n, 32, 32, 4)
+    g = Grid(32, 32, 4, 4, 1, nSx=6, nSy=1, topology=topo)
+    g.usingCurvilinearGrid = True
+    g.ini_vertical_grid([1.0e5], Ro_SeaLevel=1.0e5)
+    recs = [np.fromfile(os.path.join(gd, "grid_cs32.face%03d.bin" % f), dtype=">f8").astype(np.float64)
+            .reshape(18, n + 1, n + 1) for f in range(1, 7)]
+    rSphere = 6370.0e3
+    g.ini_curvilinear_grid(recs, radius_fromHorizGrid=6370.0e3, rSphere=rSphere, anglesFromFile=True)
+    omega = 2.0 * pi / 86164.0
+    g.ini_cori(selectCoriMap=2, omega=omega)
+    bathy = np.full((g.nTiles, g.ny, g.nx), g.f["rF"][1])     # no bathyFile: R_low = rF(Nr+1)
+    g.ini_depths_masks(bathy, hFacMin=1.0, hFacMinDr=1.0, gBaro=9.81)
+    g.ini_cg2d(2700.0, 2700.0, 1e-12)
+    params = dict(deltaTMom=2700.0, deltaTFreeSurf=2700.0, deltaTClock=2700.0, deltaTtracer=2700.0, abEps=0.1,
+                  rhoConst=999.8, rhoNil=999.8, gravity=9.81, gBaro=9.81, momStepping=0, tempStepping=1,
+                  tempAdvection=1, tempForcing=0, tempAdvScheme=33, tempVertAdvScheme=33, multiDimAdvection=1,
+                  multiDimCompressible=1, saltStepping=0, diffKhT=0.0, diffKrT=0.0, implicitDiffusion=0,
+                  ivdc_kappa=0.0, exactConserv=0, cg2dMaxIters=600, usingCurvilinearGrid=1, rSphere=rSphere,
+                  nIter0=0)
+    # code/ini_vel.F: psi = fac*fCoriG over the full halo range, EXCH_UV_XYZ_RL(.TRUE.), masks
+    omegaprime = 38.60328935834681 / rSphere
+    fac = -(rSphere * rSphere) * omegaprime / (2.0 * omega)
+    psi = fac * g.f["fCoriG"]
+    u = np.zeros((g.nTiles, 1, g.ny, g.nx))
+    v = np.zeros_like(u)
+    for t in range(g.nTiles):
+        for J in range(g.ny):
+            Jp = min(J + 1, g.ny - 1)
+            for I in range(g.nx):
+                Ip = min(I + 1, g.nx - 1)
+                u[t, 0, J, I] = 0.0 + (psi[t, J, I] - psi[t, Jp, I]) * g.f["recip_dyG"][t, J, I]
+                v[t, 0, J, I] = 0.0 + (psi[t, J, Ip] - psi[t, J, I]) * g.f["recip_dxG"][t, J, I]
+    u, v = topo.exchange_uv(u, v, True)
+    u = u * g.f["maskW"]
+    v = v * g.f["maskS"]
+    rd = lambda fn: np.fromfile(os.path.join(d, fn), dtype=">f8").astype(np.float64).reshape(n, 6 * n)
+    theta = g.exch(cs_global_to_tiles(g, rd("T.init"), mapIO=-1)[:, None].copy()) * g.f["maskC"]
+    salt = g.exch(cs_global_to_tiles(g, rd("S.init"), mapIO=-1)[:, None].copy()) * g.f["maskC"]
+    state = {"uVel": u, "vVel": v, "theta": theta, "salt": salt, "tRef": np.array([0.0]), "sRef": np.array([0.0])}
+    return g, params, state
+
+
 CS32_FORCING = {"taux": "trenberth_taux.bin", "tauy": "trenberth_tauy.bin", "Qnet": "shiQnet_cs32.bin",
                 "EmPmR": "shiEmPR_cs32.bin", "SST": "lev_surfT_cs_12m.bin", "SSS": "lev_surfS_cs_12m.bin"}
 

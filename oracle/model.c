@@ -130,7 +130,7 @@ static const PDesc PTAB[] = {
   PI_(usingSphericalPolarGrid), PI_(selectMetricTerms), PI_(integr_GeoPot), PI_(tempStepping),
   PI_(tempAdvection), PI_(tempForcing), PI_(tempAdvScheme), PI_(tempVertAdvScheme), PI_(implicitDiffusion),
   PI_(saltStepping), PI_(saltAdvection), PI_(saltForcing), PI_(saltAdvScheme), PI_(saltVertAdvScheme),
-  PI_(multiDimAdvection), PI_(momStepping), PD(diffKhS), PD(diffKrS),
+  PI_(multiDimAdvection), PI_(multiDimCompressible), PI_(momStepping), PD(diffKhS), PD(diffKrS),
   PD(rSphere), PD(deltaTtracer), PD(diffKhT), PD(diffKrT), PD(ivdc_kappa), PD(tAlpha), PD(sBeta), PD(gravitySign),
   PI_(eosType), PI_(allowFreezing), PI_(useRealFreshWaterFlux), PI_(useCDscheme), PI_(useGMRedi),
   PI_(periodicExternalForcing), PD(rhoConstFresh), PD(HeatCapacity_Cp), PD(convertFW2Salt), PD(temp_EvPrRn),

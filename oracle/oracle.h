@@ -45,6 +45,7 @@ typedef struct OModel {
   int usingSphericalPolarGrid, selectMetricTerms, integr_GeoPot;
   int tempStepping, tempAdvection, tempForcing, tempAdvScheme, tempVertAdvScheme, implicitDiffusion;
   int saltStepping, saltAdvection, saltForcing, saltAdvScheme, saltVertAdvScheme, multiDimAdvection, momStepping;
+  int multiDimCompressible;   /* GAD_MULTIDIM_COMPRESSIBLE (GAD_OPTIONS.h; e.g. verification/advect_cs) */
   double diffKhS, diffKrS;
   double rSphere, deltaTtracer, diffKhT, diffKrT, ivdc_kappa, tAlpha, sBeta, gravitySign;
 

@@ -105,20 +105,79 @@ static double dst3fl_h(double uTr, double cfl, double tm2, double tm1, double t0
   return 0.5 * (uTr + fabs(uTr)) * (tm1 + psiP * Rj) + 0.5 * (uTr - fabs(uTr)) * (t0 - psiM * Rj);
 }
 
-/* GAD_ADVECTION (gad_advection.F) for one tile, lat-lon (npass = 2: X then Y),
- * GAD_MULTIDIM_COMPRESSIBLE undefined, explicit; advectionScheme = 33 only.
- * Writes the advective tendency into gTr (whole tile, as the reference). */
+/* FILL_CS_CORNER_TR_RL (eesupp/src/fill_cs_corner_tr_rl.F): the halo corners of a cube
+ * tile filled from the neighbouring halo strip, for X (dir 1) or Y (dir 2) stencils. */
+static void fill_cs_corner_tr(const OModel *m, int dir, double *a, int edges) {
+  const int sNx = m->sNx, sNy = m->sNy, OLx = m->OLx, OLy = m->OLy, nx = m->nx;
+  const int N = edges & 1, S = edges & 2, E = edges & 4, W = edges & 8;
+  for (int j = 1; j <= OLy; j++)
+    for (int i = 1; i <= OLx; i++) {
+      if (W && S) L(a, 1 - i, 1 - j) = dir == 1 ? L(a, 1 - j, i) : L(a, j, 1 - i);
+      if (E && S) L(a, sNx + i, 1 - j) = dir == 1 ? L(a, sNx + j, i) : L(a, sNx + 1 - j, 1 - i);
+      if (W && N) L(a, 1 - i, sNy + j) = dir == 1 ? L(a, 1 - j, sNy + 1 - i) : L(a, j, sNy + i);
+      if (E && N) L(a, sNx + i, sNy + j) = dir == 1 ? L(a, sNx + j, sNy + 1 - i) : L(a, sNx + 1 - j, sNy + i);
+    }
+}
+/* FILL_CS_CORNER_UV_RS(withSigns = .FALSE.) (eesupp/src/fill_cs_corner_uv_rs.F) on the
+ * local masks maskLocW (u) and maskLocS (v), corner by corner in the reference's order. */
+static void fill_cs_corner_uv(const OModel *m, double *u, double *v, int edges) {
+  const int sNx = m->sNx, sNy = m->sNy, OLx = m->OLx, OLy = m->OLy, nx = m->nx;
+  const int N = edges & 1, S = edges & 2, E = edges & 4, W = edges & 8;
+  if (W && S) {
+    for (int j = 1; j <= OLy; j++) for (int i = 1; i <= OLx; i++) L(u, 1 - i, 1 - j) = L(v, 1 - j, 1 + i);
+    for (int j = 1; j <= OLy; j++) for (int i = 1; i <= OLx; i++) L(v, 1 - i, 1 - j) = L(u, 1 + j, 1 - i);
+  }
+  if (E && S) {
+    for (int j = 1; j <= OLy; j++) for (int i = 2; i <= OLx; i++) L(u, sNx + i, 1 - j) = L(v, sNx + j, i);
+    for (int j = 1; j <= OLy; j++) for (int i = 1; i <= OLx; i++) L(v, sNx + i, 1 - j) = L(u, sNx + 1 - j, 1 - i);
+  }
+  if (W && N) {
+    for (int j = 1; j <= OLy; j++) for (int i = 1; i <= OLx; i++) L(u, 1 - i, sNy + j) = L(v, 1 - j, sNy + 1 - i);
+    for (int j = 2; j <= OLy; j++) for (int i = 1; i <= OLx; i++) L(v, 1 - i, sNy + j) = L(u, j, sNy + i);
+  }
+  if (E && N) {
+    for (int j = 1; j <= OLy; j++) for (int i = 2; i <= OLx; i++) L(u, sNx + i, sNy + j) = L(v, sNx + j, sNy + 2 - i);
+    for (int j = 2; j <= OLy; j++) for (int i = 1; i <= OLx; i++) L(v, sNx + i, sNy + j) = L(u, sNx + 2 - j, sNy + i);
+  }
+}
+
+/* GAD_ADVECTION (gad_advection.F:292-1097) for one tile, explicit, advectionScheme = 33.
+ * Lat-lon: npass = 2 (X then Y).  Cube (EXCH2 tiles, useCubedSphereExchange): npass = 3,
+ * the direction of each pass and whether it updates the tile's interior, its overlap only,
+ * or both chosen by the tile's face (:339-367), with FILL_CS_CORNER_TR_RL before / after the
+ * fluxes of overlap-only passes and FILL_CS_CORNER_UV_RS on the local masks.
+ * GAD_MULTIDIM_COMPRESSIBLE (m->multiDimCompressible): the volume-weighted update with the
+ * local volume carried through the passes.  Writes the advective tendency into gTr. */
 static void gad_advection_dst3fl(const OModel *m, int t, const double *tr, const double *uVel, const double *vVel,
                                  const double *wVel, double *gTr, double dT) {
   const int sNx = m->sNx, sNy = m->sNy, OLx = m->OLx, OLy = m->OLy, Nr = m->Nr, nx = m->nx;
   const long n2 = m->n2, n3 = m->n3;
+  const int cube = m->tileFace != NULL, comp = m->multiDimCompressible;
+  const int face = cube ? m->tileFace[t] : 0, edges = cube ? m->tileEdge[t] : 0;
+  const int Ned = edges & 1, Sed = edges & 2, Eed = edges & 4, Wed = edges & 8;
   const double *hFacW = m->hFacW + t * n3, *hFacS = m->hFacS + t * n3, *maskW = m->maskW + t * n3;
   const double *maskS = m->maskS + t * n3, *maskC = m->maskC + t * n3, *rhFacC = m->recip_hFacC + t * n3;
+  const double *hFacC = m->hFacC + t * n3;
   const double *dxG = m->dxG + t * n2, *dyG = m->dyG + t * n2, *rA = m->rA + t * n2, *recip_rA = m->recip_rA + t * n2;
   const double *recip_dxC = m->recip_dxC + t * n2, *recip_dyC = m->recip_dyC + t * n2, *maskInC = m->maskInC + t * n2;
   double *uTrans = calloc(n2, 8), *vTrans = calloc(n2, 8), *loc = calloc(n2, 8), *af = calloc(n2, 8);
   double *locT3d = calloc(n3, 8), *rTrans = calloc(n2, 8), *rTransKp = calloc(n2, 8), *fV[2];
+  double *vol = calloc(n2, 8), *vol3d = calloc(n3, 8), *mLW = calloc(n2, 8), *mLS = calloc(n2, 8);
   fV[0] = calloc(n2, 8); fV[1] = calloc(n2, 8);
+  /* one cell's update by the X (dir 0) or Y (dir 1) flux divergence */
+#define UPD(i, j, dir)                                                                                         \
+  do {                                                                                                         \
+    const double dF = dir ? L(af, i, (j) + 1) - L(af, i, j) : L(af, (i) + 1, j) - L(af, i, j);                 \
+    const double dU = dir ? L(vTrans, i, (j) + 1) - L(vTrans, i, j) : L(uTrans, (i) + 1, j) - L(uTrans, i, j); \
+    if (comp) {                                                                                                \
+      const double tmpTrac = L(loc, i, j) * L(vol, i, j) - dT * dF * L(maskInC, i, j);                        \
+      L(vol, i, j) = L(vol, i, j) - dT * dU * L(maskInC, i, j);                                                \
+      L(loc, i, j) = tmpTrac / L(vol, i, j);                                                                   \
+    } else {                                                                                                   \
+      L(loc, i, j) = L(loc, i, j) - dT * W3(rhFacC, i, j, k) * m->recip_drF[k - 1] * L(recip_rA, i, j) *      \
+                                        (dF - W3(tr, i, j, k) * dU) * L(maskInC, i, j);                        \
+    }                                                                                                          \
+  } while (0)
   for (int k = 1; k <= Nr; k++) {
     for (int j = 1 - OLy; j <= sNy + OLy; j++)
       for (int i = 1 - OLx; i <= sNx + OLx; i++) {
@@ -127,37 +186,80 @@ static void gad_advection_dst3fl(const OModel *m, int t, const double *tr, const
         L(uTrans, i, j) = W3(uVel, i, j, k) * xA;
         L(vTrans, i, j) = W3(vVel, i, j, k) * yA;
         L(loc, i, j) = W3(tr, i, j, k);
+        if (comp) L(vol, i, j) = L(rA, i, j) * m->drF[k - 1] * W3(hFacC, i, j, k) + (1.0 - W3(maskC, i, j, k));
+        L(mLW, i, j) = W3(maskW, i, j, k);
+        L(mLS, i, j) = W3(maskS, i, j, k);
       }
-    /* ipass 1: X fluxes (uT = 0 at i = 1-OLx, 2-OLx, sNx+OLx), update j = all, i = 2-OLx..sNx+OLx-1 */
-    for (long p = 0; p < n2; p++) af[p] = 0.0;
-    for (int j = 1 - OLy; j <= sNy + OLy; j++)
-      for (int i = 3 - OLx; i <= sNx + OLx - 1; i++) {
-        const double cfl = fabs(W3(uVel, i, j, k) * dT * L(recip_dxC, i, j));
-        L(af, i, j) = dst3fl_h(L(uTrans, i, j), cfl, L(loc, i - 2, j), L(loc, i - 1, j), L(loc, i, j), L(loc, i + 1, j),
-                               W3(maskW, i - 1, j, k), W3(maskW, i, j, k), W3(maskW, i + 1, j, k));
+    if (cube) fill_cs_corner_uv(m, mLW, mLS, edges);
+    const int npass = cube ? 3 : 2;
+    for (int ipass = 1; ipass <= npass; ipass++) {
+      int overlapOnly = 0, interiorOnly = 0, calcX, calcY;
+      if (cube) {
+        if (ipass == 1) {
+          overlapOnly = face % 3 == 0; interiorOnly = face % 3 != 0;
+          calcX = face == 6 || face == 1 || face == 2; calcY = face == 3 || face == 4 || face == 5;
+        } else if (ipass == 2) {
+          overlapOnly = face % 3 == 2; interiorOnly = face % 3 == 1;
+          calcX = face == 2 || face == 3 || face == 4; calcY = face == 5 || face == 6 || face == 1;
+        } else {
+          interiorOnly = 1;
+          calcX = face == 5 || face == 6; calcY = face == 2 || face == 3;
+        }
+      } else {
+        calcX = ipass % 2 == 1; calcY = !calcX;
       }
+      /* X direction: GAD_DST3FL_ADV_X over i = 3-OLx..sNx+OLx-1 (af = 0 elsewhere) */
+      if (calcX) {
+        if (!overlapOnly || Ned || Sed) {
+          if (overlapOnly) fill_cs_corner_tr(m, 1, loc, edges);
+          for (long p = 0; p < n2; p++) af[p] = 0.0;
+          for (int j = 1 - OLy; j <= sNy + OLy; j++)
+            for (int i = 3 - OLx; i <= sNx + OLx - 1; i++) {
+              const double cfl = fabs(W3(uVel, i, j, k) * dT * L(recip_dxC, i, j));
+              L(af, i, j) = dst3fl_h(L(uTrans, i, j), cfl, L(loc, i - 2, j), L(loc, i - 1, j), L(loc, i, j),
+                                     L(loc, i + 1, j), L(mLW, i - 1, j), L(mLW, i, j), L(mLW, i + 1, j));
+            }
+          if (overlapOnly && ipass == 1) fill_cs_corner_tr(m, 2, loc, edges);
+        }
+        if (overlapOnly) {
+          const int iMin = Wed ? 1 : 2 - OLx, iMax = Eed ? sNx : sNx + OLx - 1;
+          if (Sed) for (int j = 1 - OLy; j <= 0; j++) for (int i = iMin; i <= iMax; i++) UPD(i, j, 0);
+          if (Ned) for (int j = sNy + 1; j <= sNy + OLy; j++) for (int i = iMin; i <= iMax; i++) UPD(i, j, 0);
+        } else {
+          const int jMin = (interiorOnly && Sed) ? 1 : 1 - OLy, jMax = (interiorOnly && Ned) ? sNy : sNy + OLy;
+          for (int j = jMin; j <= jMax; j++) for (int i = 2 - OLx; i <= sNx + OLx - 1; i++) UPD(i, j, 0);
+        }
+      }
+      /* Y direction: GAD_DST3FL_ADV_Y over j = 3-OLy..sNy+OLy-1 */
+      for (long p = 0; p < n2; p++) af[p] = 0.0;
+      if (calcY) {
+        if (!overlapOnly || Eed || Wed) {
+          if (overlapOnly) fill_cs_corner_tr(m, 2, loc, edges);
+          for (long p = 0; p < n2; p++) af[p] = 0.0;
+          for (int j = 3 - OLy; j <= sNy + OLy - 1; j++)
+            for (int i = 1 - OLx; i <= sNx + OLx; i++) {
+              const double cfl = fabs(W3(vVel, i, j, k) * dT * L(recip_dyC, i, j));
+              L(af, i, j) = dst3fl_h(L(vTrans, i, j), cfl, L(loc, i, j - 2), L(loc, i, j - 1), L(loc, i, j),
+                                     L(loc, i, j + 1), L(mLS, i, j - 1), L(mLS, i, j), L(mLS, i, j + 1));
+            }
+          if (overlapOnly && ipass == 1) fill_cs_corner_tr(m, 1, loc, edges);
+        }
+        if (overlapOnly) {
+          const int jMin = Sed ? 1 : 2 - OLy, jMax = Ned ? sNy : sNy + OLy - 1;
+          if (Wed) for (int j = jMin; j <= jMax; j++) for (int i = 1 - OLx; i <= 0; i++) UPD(i, j, 1);
+          if (Eed) for (int j = jMin; j <= jMax; j++) for (int i = sNx + 1; i <= sNx + OLx; i++) UPD(i, j, 1);
+        } else {
+          const int iMin = (interiorOnly && Wed) ? 1 : 1 - OLx, iMax = (interiorOnly && Eed) ? sNx : sNx + OLx;
+          for (int j = 2 - OLy; j <= sNy + OLy - 1; j++) for (int i = iMin; i <= iMax; i++) UPD(i, j, 1);
+        }
+      }
+    }
+#undef UPD
     for (int j = 1 - OLy; j <= sNy + OLy; j++)
-      for (int i = 2 - OLx; i <= sNx + OLx - 1; i++)
-        L(loc, i, j) = L(loc, i, j) - dT * W3(rhFacC, i, j, k) * m->recip_drF[k - 1] * L(recip_rA, i, j) *
-                                          (L(af, i + 1, j) - L(af, i, j) -
-                                           W3(tr, i, j, k) * (L(uTrans, i + 1, j) - L(uTrans, i, j))) *
-                                          L(maskInC, i, j);
-    /* ipass 2: Y fluxes (vT = 0 at j = 1-OLy, 2-OLy, sNy+OLy), update j = 2-OLy..sNy+OLy-1, i = all */
-    for (long p = 0; p < n2; p++) af[p] = 0.0;
-    for (int j = 3 - OLy; j <= sNy + OLy - 1; j++)
       for (int i = 1 - OLx; i <= sNx + OLx; i++) {
-        const double cfl = fabs(W3(vVel, i, j, k) * dT * L(recip_dyC, i, j));
-        L(af, i, j) = dst3fl_h(L(vTrans, i, j), cfl, L(loc, i, j - 2), L(loc, i, j - 1), L(loc, i, j), L(loc, i, j + 1),
-                               W3(maskS, i, j - 1, k), W3(maskS, i, j, k), W3(maskS, i, j + 1, k));
+        W3(locT3d, i, j, k) = L(loc, i, j);
+        if (comp) W3(vol3d, i, j, k) = L(vol, i, j);
       }
-    for (int j = 2 - OLy; j <= sNy + OLy - 1; j++)
-      for (int i = 1 - OLx; i <= sNx + OLx; i++)
-        L(loc, i, j) = L(loc, i, j) - dT * W3(rhFacC, i, j, k) * m->recip_drF[k - 1] * L(recip_rA, i, j) *
-                                          (L(af, i, j + 1) - L(af, i, j) -
-                                           W3(tr, i, j, k) * (L(vTrans, i, j + 1) - L(vTrans, i, j))) *
-                                          L(maskInC, i, j);
-    for (int j = 1 - OLy; j <= sNy + OLy; j++)
-      for (int i = 1 - OLx; i <= sNx + OLx; i++) W3(locT3d, i, j, k) = L(loc, i, j);
   }
   /* vertical: k = Nr..1, GAD_DST3FL_ADV_R on the horizontally-updated tracer */
   for (long p = 0; p < n2; p++) { rTrans[p] = 0.0; fV[0][p] = fV[1][p] = 0.0; }
@@ -189,6 +291,14 @@ static void gad_advection_dst3fl(const OModel *m, int t, const double *tr, const
       }
     for (int j = 1 - OLy; j <= sNy + OLy; j++)
       for (int i = 1 - OLx; i <= sNx + OLx; i++) {
+        if (comp) {   /* gad_advection.F:1036-1057 */
+          const double tmpTrac = W3(locT3d, i, j, k) * W3(vol3d, i, j, k) -
+                                 dT * (L(fDn, i, j) - L(fUp, i, j)) * m->rkSign * L(maskInC, i, j);
+          const double lv = W3(vol3d, i, j, k) - dT * (L(rTransKp, i, j) - L(rTrans, i, j)) * m->rkSign * L(maskInC, i, j);
+          W3(gTr, i, j, k) = (tmpTrac - W3(tr, i, j, k) * lv) * L(recip_rA, i, j) * m->recip_drF[k - 1] *
+                             W3(rhFacC, i, j, k) / dT;
+          continue;
+        }
         const double lt = W3(locT3d, i, j, k) -
                           dT * W3(rhFacC, i, j, k) * m->recip_drF[k - 1] * L(recip_rA, i, j) *
                               (L(fDn, i, j) - L(fUp, i, j) - W3(tr, i, j, k) * (L(rTransKp, i, j) - L(rTrans, i, j))) *
@@ -197,6 +307,7 @@ static void gad_advection_dst3fl(const OModel *m, int t, const double *tr, const
       }
   }
   free(uTrans); free(vTrans); free(loc); free(af); free(locT3d); free(rTrans); free(rTransKp); free(fV[0]); free(fV[1]);
+  free(vol); free(vol3d); free(mLW); free(mLS);
 }
 
 /* One tracer through TEMP_INTEGRATE / SALT_INTEGRATE (temp_integrate.F, salt_integrate.F). */

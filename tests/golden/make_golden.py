@@ -53,6 +53,14 @@ EXPERIMENTS = {
         "inputs": ["input/tile00%d.mitgrid" % f for f in range(1, 7)] + ["input/S_init.bin"],
         "output": "results/output.txt",
     },
+    # cubed sphere (pkg/exch2, 6 faces of 32x32, OL=4), 1 level, momStepping=F: solid-body
+    # rotation (code/ini_vel.F) advecting theta with DST3 flux-limited multi-dimensional
+    # advection (tempAdvScheme=33, 3-pass cube split), GAD_MULTIDIM_COMPRESSIBLE; the grid is
+    # global_ocean.cs32x15's grid_cs32 faces (input/prepare_run links the same files)
+    "advect_cs": {
+        "inputs": ["input/T.init", "input/S.init"],
+        "output": "results/output.txt",
+    },
     # BASELINE config 3 (cs32x15).  Its pickup.0000072000 is not in the checkout
     # (.MISSING_LARGE_BLOBS), so the run is a cold start from lev_T/lev_S: only the grid
     # statistics of output.txt pin it.  Grid files are linked by input/prepare_run.
@@ -149,7 +157,10 @@ def parse_params(path):
 
 
 def main():
+    only = sys.argv[1:]   # optional: experiment names to (re)extract
     for exp, spec in EXPERIMENTS.items():
+        if only and exp not in only:
+            continue
         out = os.path.join(HERE, exp)
         os.makedirs(out, exist_ok=True)
         for rel in spec["inputs"]:
