@@ -65,6 +65,7 @@ struct Params {
   int metricSphere;   // usingSphericalPolarGrid && selectMetricTerms >= 1
   double diffKhS, diffKrS;
   int saltStepping, saltAdvection, saltForcing, saltAdvScheme, multiDimAdvection, momStepping;
+  int multiDimCompressible;   // GAD_MULTIDIM_COMPRESSIBLE (GAD_OPTIONS.h)
   // lat-lon ocean physics (tutorial_global_oce_latlon / global_ocean.90x40x15)
   int eosType;   // 0 LINEAR, 1 JMD95Z
   int allowFreezing, useRealFreshWaterFlux, useCDscheme, useGMRedi, periodicExternalForcing, nForcRec;

@@ -319,13 +319,16 @@ __global__ void __launch_bounds__(256) k_adv_y(Dims d, Fields f, TracerArgs a) {
                                (afy(j + 1) - afy(j) - a.tr[q3] * (vTr(j + 1) - vTr(j))) * f.maskInC[q];
 }
 
-// vertical pass + advective tendency gAdv = (loc - T)/dT (gad_advection.F k = Nr..1 loop)
-__global__ void __launch_bounds__(256) k_adv_r(Dims d, Params p, Fields f, TracerArgs a) {
+// vertical pass + advective tendency (gad_advection.F k = Nr..1 loop) on the horizontally
+// advected tracer L (and, GAD_MULTIDIM_COMPRESSIBLE, the local volume V, :1036-1057):
+// gAdv = (loc - T)/dT, or (tmpTrac - T*vol)/(rA drF hFac dT) in the compressible form
+template <bool COMP>
+__global__ void __launch_bounds__(256) k_adv_r(Dims d, Params p, Fields f, TracerArgs a, const double *__restrict__ L2,
+                                               const double *__restrict__ V) {
   MG_PLANE(1, d.sNx, 1, d.sNy, z)
   const int t = d.t0 + z / d.Nr, k = z % d.Nr + 1;
   if (i > d.sNx || j > d.sNy) return;
   const int Nr = d.Nr;
-  const double *__restrict__ L2 = f.advScr2;
   const long q = MG_I2(d, i, j, t), q3 = MG_I3(d, i, j, k, t);
   const double rA = f.rA[q], dT = a.dT;
 #define MC(kk) f.maskC[MG_I3(d, i, j, kk, t)]
@@ -348,11 +351,184 @@ __global__ void __launch_bounds__(256) k_adv_r(Dims d, Params p, Fields f, Trace
   const double kp1Msk = (k == Nr) ? 0.0 : 1.0;
   const double rTrans = rtr(k), rTransKp = kp1Msk * rtr(k + 1);
   const double fUp = fver(k), fDn = fver(k + 1);
-  const double lt = LT(k) - dT * f.recip_hFacC[q3] * f.recip_drF[k - 1] * f.recip_rA[q] *
-                                (fDn - fUp - a.tr[q3] * (rTransKp - rTrans)) * p.rkSign * f.maskInC[q];
-  f.gAdv[q3] = (lt - a.tr[q3]) / dT;
+  if (COMP) {
+    const double tmpTrac = LT(k) * V[q3] - dT * (fDn - fUp) * p.rkSign * f.maskInC[q];
+    const double lv = V[q3] - dT * (rTransKp - rTrans) * p.rkSign * f.maskInC[q];
+    f.gAdv[q3] = (tmpTrac - a.tr[q3] * lv) * f.recip_rA[q] * f.recip_drF[k - 1] * f.recip_hFacC[q3] / dT;
+  } else {
+    const double lt = LT(k) - dT * f.recip_hFacC[q3] * f.recip_drF[k - 1] * f.recip_rA[q] *
+                                  (fDn - fUp - a.tr[q3] * (rTransKp - rTrans)) * p.rkSign * f.maskInC[q];
+    f.gAdv[q3] = (lt - a.tr[q3]) / dT;
+  }
 #undef MC
 #undef LT
+}
+
+// ---------------------------------------------------------------------------
+// GAD_ADVECTION in its general form (gad_advection.F:292-811): cube tiles (3 passes whose
+// direction and overlap-only / interior-only updates depend on the tile's face, :339-367,
+// with FILL_CS_CORNER_TR_RL around the overlap-only fluxes and FILL_CS_CORNER_UV_RS on the
+// masks) and/or GAD_MULTIDIM_COMPRESSIBLE (the local volume carried through the passes).
+// The passes run as explicit steps over the whole slab: loc (advScr1) and vol (advScr2)
+// are updated in place, the face fluxes of a pass go to gTscr (free until k_tracer_rhs).
+struct AdvCfg { bool ov, in, cx, cy; };
+__device__ __forceinline__ AdvCfg adv_cfg(bool cube, int face, int ipass) {
+  AdvCfg c{false, false, false, false};
+  if (cube) {
+    if (ipass == 1) {
+      c.ov = face % 3 == 0; c.in = face % 3 != 0;
+      c.cx = face == 6 || face == 1 || face == 2; c.cy = face == 3 || face == 4 || face == 5;
+    } else if (ipass == 2) {
+      c.ov = face % 3 == 2; c.in = face % 3 == 1;
+      c.cx = face == 2 || face == 3 || face == 4; c.cy = face == 5 || face == 6 || face == 1;
+    } else {
+      c.in = true;
+      c.cx = face == 5 || face == 6; c.cy = face == 2 || face == 3;
+    }
+  } else {
+    c.cx = ipass % 2 == 1; c.cy = !c.cx;
+  }
+  return c;
+}
+// maskLocW / maskLocS after FILL_CS_CORNER_UV_RS(withSigns = .FALSE.): corner halo points
+// take the other component's mask at the rotated position (the sources are never corners)
+__device__ __forceinline__ double mask_loc(const Dims &d, const Fields &f, bool cube, int edges, bool isW, int i, int j,
+                                           int k, int t) {
+  const int sNx = d.sNx, sNy = d.sNy;
+  const bool N = edges & 1, S = edges & 2, E = edges & 4, W = edges & 8;
+  if (cube) {
+    const double *other = isW ? f.maskS : f.maskW;
+    int si = 0, sj = 0;
+    bool hit = false;
+    if (i <= 0 && j <= 0 && W && S) { hit = true; if (isW) { si = j; sj = 2 - i; } else { si = 2 - j; sj = i; } }
+    else if (i > sNx && j <= 0 && E && S) {
+      if (isW) { if (i >= sNx + 2) { hit = true; si = sNx + 1 - j; sj = i - sNx; } }
+      else { hit = true; si = sNx + j; sj = 1 + sNx - i; }
+    } else if (i <= 0 && j > sNy && W && N) {
+      if (isW) { hit = true; si = 1 + sNy - j; sj = sNy + i; }
+      else if (j >= sNy + 2) { hit = true; si = j - sNy; sj = sNy + 1 - i; }
+    } else if (i > sNx && j > sNy && E && N) {
+      if (isW) { if (i >= sNx + 2) { hit = true; si = sNx + j - sNy; sj = sNy + sNx + 2 - i; } }
+      else if (j >= sNy + 2) { hit = true; si = sNx + sNy + 2 - j; sj = sNy + i - sNx; }
+    }
+    if (hit) return other[MG_I3(d, si, sj, k, t)];
+  }
+  return (isW ? f.maskW : f.maskS)[MG_I3(d, i, j, k, t)];
+}
+
+__global__ void __launch_bounds__(256) k_advg_init(Dims d, Fields f, TracerArgs a, int comp) {
+  MG_PLANE(1 - d.OLx, d.nx, 1 - d.OLy, d.ny, z)
+  const int t = d.t0 + z / d.Nr, k = z % d.Nr + 1;
+  if (i > d.sNx + d.OLx || j > d.sNy + d.OLy) return;
+  const long q3 = MG_I3(d, i, j, k, t);
+  f.advScr1[q3] = a.tr[q3];
+  if (comp)
+    f.advScr2[q3] = f.rA[MG_I2(d, i, j, t)] * f.drF[k - 1] * f.hFacC[q3] + (1.0 - f.maskC[q3]);
+}
+
+// FILL_CS_CORNER_TR_RL(dir) on loc for the tiles whose pass calls it at this stage:
+// stage 0 X-before (X flux, overlap-only, N/S edge), 1 X-after (+ ipass = 1), 2 Y-before
+// (Y flux, overlap-only, E/W edge), 3 Y-after (+ ipass = 1); one thread per corner point
+__global__ void __launch_bounds__(256) k_advg_fill(Dims d, Fields f, int ipass, int stage) {
+  const int OLx = d.OLx, OLy = d.OLy, per = 4 * OLx * OLy;
+  const long g = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (g >= (long)per * d.nT * d.Nr) return;
+  const int c = (int)(g % per), z = (int)(g / per);
+  const int t = d.t0 + z / d.Nr, k = z % d.Nr + 1;
+  const int face = f.tileFace[t], edges = f.tileEdge[t];
+  const bool N = edges & 1, S = edges & 2, E = edges & 4, W = edges & 8;
+  const AdvCfg cf = adv_cfg(true, face, ipass);
+  bool run;
+  if (stage < 2) run = cf.cx && cf.ov && (N || S) && (stage == 0 || ipass == 1);
+  else run = cf.cy && cf.ov && (E || W) && (stage == 2 || ipass == 1);
+  if (!run) return;
+  const int dir = (stage == 0 || stage == 3) ? 1 : 2;
+  const int corner = c / (OLx * OLy), ii = c % OLx + 1, jj = (c / OLx) % OLy + 1;
+  const int sNx = d.sNx, sNy = d.sNy;
+  int di, dj, si, sj;
+  if (corner == 0) { if (!(W && S)) return; di = 1 - ii; dj = 1 - jj; if (dir == 1) { si = 1 - jj; sj = ii; } else { si = jj; sj = 1 - ii; } }
+  else if (corner == 1) { if (!(E && S)) return; di = sNx + ii; dj = 1 - jj; if (dir == 1) { si = sNx + jj; sj = ii; } else { si = sNx + 1 - jj; sj = 1 - ii; } }
+  else if (corner == 2) { if (!(W && N)) return; di = 1 - ii; dj = sNy + jj; if (dir == 1) { si = 1 - jj; sj = sNy + 1 - ii; } else { si = jj; sj = sNy + ii; } }
+  else { if (!(E && N)) return; di = sNx + ii; dj = sNy + jj; if (dir == 1) { si = sNx + jj; sj = sNy + 1 - ii; } else { si = sNx + 1 - jj; sj = sNy + ii; } }
+  f.advScr1[MG_I3(d, di, dj, k, t)] = f.advScr1[MG_I3(d, si, sj, k, t)];
+}
+
+// the X (ydir = 0) or Y (1) DST3FL face fluxes of a pass into gTscr, on the tiles that
+// compute them (GAD_DST3FL_ADV_X over i = 3-OLx..sNx+OLx-1, _Y over j = 3-OLy..sNy+OLy-1)
+__global__ void __launch_bounds__(256) k_advg_flux(Dims d, Fields f, TracerArgs a, int ipass, int ydir, int cube) {
+  MG_PLANE(1 - d.OLx, d.nx, 1 - d.OLy, d.ny, z)
+  const int t = d.t0 + z / d.Nr, k = z % d.Nr + 1;
+  if (i > d.sNx + d.OLx || j > d.sNy + d.OLy) return;
+  const int face = cube ? f.tileFace[t] : 0, edges = cube ? f.tileEdge[t] : 0;
+  const bool N = edges & 1, S = edges & 2, E = edges & 4, W = edges & 8;
+  const AdvCfg cf = adv_cfg(cube, face, ipass);
+  if (ydir ? !(cf.cy && (!cf.ov || E || W)) : !(cf.cx && (!cf.ov || N || S))) return;
+  const double *__restrict__ Lc = f.advScr1;
+  const long q3 = MG_I3(d, i, j, k, t);
+  const double dT = a.dT, drF = f.drF[k - 1];
+  double af = 0.0;
+  if (!ydir && i >= 3 - d.OLx && i <= d.sNx + d.OLx - 1) {
+    const double uTr = f.uVel[q3] * (f.dyG[MG_I2(d, i, j, t)] * drF * f.hFacW[q3]);
+    const double cfl = fabs(f.uVel[q3] * dT * f.recip_dxC[MG_I2(d, i, j, t)]);
+    af = dst3fl_h(uTr, cfl, Lc[MG_I3(d, i - 2, j, k, t)], Lc[MG_I3(d, i - 1, j, k, t)], Lc[q3], Lc[MG_I3(d, i + 1, j, k, t)],
+                  mask_loc(d, f, cube, edges, true, i - 1, j, k, t), mask_loc(d, f, cube, edges, true, i, j, k, t),
+                  mask_loc(d, f, cube, edges, true, i + 1, j, k, t));
+  } else if (ydir && j >= 3 - d.OLy && j <= d.sNy + d.OLy - 1) {
+    const double vTr = f.vVel[q3] * (f.dxG[MG_I2(d, i, j, t)] * drF * f.hFacS[q3]);
+    const double cfl = fabs(f.vVel[q3] * dT * f.recip_dyC[MG_I2(d, i, j, t)]);
+    af = dst3fl_h(vTr, cfl, Lc[MG_I3(d, i, j - 2, k, t)], Lc[MG_I3(d, i, j - 1, k, t)], Lc[q3], Lc[MG_I3(d, i, j + 1, k, t)],
+                  mask_loc(d, f, cube, edges, false, i, j - 1, k, t), mask_loc(d, f, cube, edges, false, i, j, k, t),
+                  mask_loc(d, f, cube, edges, false, i, j + 1, k, t));
+  }
+  f.gTscr[q3] = af;
+}
+
+// the update of loc (and vol) by the X / Y flux divergence on the pass's update region
+__global__ void __launch_bounds__(256) k_advg_upd(Dims d, Fields f, TracerArgs a, int ipass, int ydir, int cube, int comp) {
+  MG_PLANE(1 - d.OLx, d.nx, 1 - d.OLy, d.ny, z)
+  const int t = d.t0 + z / d.Nr, k = z % d.Nr + 1;
+  if (i > d.sNx + d.OLx || j > d.sNy + d.OLy) return;
+  const int face = cube ? f.tileFace[t] : 0, edges = cube ? f.tileEdge[t] : 0;
+  const bool N = edges & 1, S = edges & 2, E = edges & 4, W = edges & 8;
+  const AdvCfg cf = adv_cfg(cube, face, ipass);
+  const int sNx = d.sNx, sNy = d.sNy, OLx = d.OLx, OLy = d.OLy;
+  bool upd = false;
+  if (!ydir) {
+    if (!cf.cx) return;
+    if (cf.ov) {
+      const int iMin = W ? 1 : 2 - OLx, iMax = E ? sNx : sNx + OLx - 1;
+      upd = i >= iMin && i <= iMax && ((S && j <= 0) || (N && j >= sNy + 1));
+    } else {
+      const int jMin = (cf.in && S) ? 1 : 1 - OLy, jMax = (cf.in && N) ? sNy : sNy + OLy;
+      upd = j >= jMin && j <= jMax && i >= 2 - OLx && i <= sNx + OLx - 1;
+    }
+  } else {
+    if (!cf.cy) return;
+    if (cf.ov) {
+      const int jMin = S ? 1 : 2 - OLy, jMax = N ? sNy : sNy + OLy - 1;
+      upd = j >= jMin && j <= jMax && ((W && i <= 0) || (E && i >= sNx + 1));
+    } else {
+      const int iMin = (cf.in && W) ? 1 : 1 - OLx, iMax = (cf.in && E) ? sNx : sNx + OLx;
+      upd = i >= iMin && i <= iMax && j >= 2 - OLy && j <= sNy + OLy - 1;
+    }
+  }
+  if (!upd) return;
+  const long q3 = MG_I3(d, i, j, k, t), q = MG_I2(d, i, j, t);
+  const double dT = a.dT, drF = f.drF[k - 1];
+  const long q3n = ydir ? MG_I3(d, i, j + 1, k, t) : MG_I3(d, i + 1, j, k, t);
+  const double dF = f.gTscr[q3n] - f.gTscr[q3];
+  double dU;
+  if (ydir) dU = f.vVel[q3n] * (f.dxG[MG_I2(d, i, j + 1, t)] * drF * f.hFacS[q3n]) - f.vVel[q3] * (f.dxG[q] * drF * f.hFacS[q3]);
+  else dU = f.uVel[q3n] * (f.dyG[MG_I2(d, i + 1, j, t)] * drF * f.hFacW[q3n]) - f.uVel[q3] * (f.dyG[q] * drF * f.hFacW[q3]);
+  if (comp) {
+    const double tmpTrac = f.advScr1[q3] * f.advScr2[q3] - dT * dF * f.maskInC[q];
+    const double vol = f.advScr2[q3] - dT * dU * f.maskInC[q];
+    f.advScr2[q3] = vol;
+    f.advScr1[q3] = tmpTrac / vol;
+  } else {
+    f.advScr1[q3] = f.advScr1[q3] - dT * f.recip_hFacC[q3] * f.recip_drF[k - 1] * f.recip_rA[q] *
+                                        (dF - a.tr[q3] * dU) * f.maskInC[q];
+  }
 }
 
 // GAD_CALC_RHS + forcing + AB2 + TIMESTEP_TRACER for one interior (i,j,k) point:
@@ -607,9 +783,24 @@ hipError_t launch_tracer_step(const Dims &d, const Params &p, const Fields &f, c
   const dim3 blk(MG_PLANE_THREADS), grd(mg_plane_blocks(d.sNx, d.sNy, d.nT * d.Nr));
   if (a.multiDim) {
     const dim3 fgrd(mg_plane_blocks(d.nx, d.ny, d.nT * d.Nr));
-    hipLaunchKernelGGL(k_adv_x, fgrd, blk, 0, s, d, f, a);
-    hipLaunchKernelGGL(k_adv_y, grd, blk, 0, s, d, f, a);
-    hipLaunchKernelGGL(k_adv_r, grd, blk, 0, s, d, p, f, a);
+    const bool cube = p.cubeCorners != 0, comp = p.multiDimCompressible != 0;
+    if (!cube && !comp) {   // lat-lon, 2 passes: fused per-point X and Y passes
+      hipLaunchKernelGGL(k_adv_x, fgrd, blk, 0, s, d, f, a);
+      hipLaunchKernelGGL(k_adv_y, grd, blk, 0, s, d, f, a);
+      hipLaunchKernelGGL(k_adv_r<false>, grd, blk, 0, s, d, p, f, a, f.advScr2, f.advScr2);
+    } else {                // the general form: explicit passes over the whole slab
+      hipLaunchKernelGGL(k_advg_init, fgrd, blk, 0, s, d, f, a, (int)comp);
+      const unsigned cgrd = (unsigned)((4L * d.OLx * d.OLy * d.nT * d.Nr + 255) / 256);
+      for (int ipass = 1; ipass <= (cube ? 3 : 2); ipass++)
+        for (int ydir = 0; ydir < 2; ydir++) {
+          if (cube) hipLaunchKernelGGL(k_advg_fill, dim3(cgrd), blk, 0, s, d, f, ipass, 2 * ydir);
+          hipLaunchKernelGGL(k_advg_flux, fgrd, blk, 0, s, d, f, a, ipass, ydir, (int)cube);
+          if (cube) hipLaunchKernelGGL(k_advg_fill, dim3(cgrd), blk, 0, s, d, f, ipass, 2 * ydir + 1);
+          hipLaunchKernelGGL(k_advg_upd, fgrd, blk, 0, s, d, f, a, ipass, ydir, (int)cube, (int)comp);
+        }
+      if (comp) hipLaunchKernelGGL(k_adv_r<true>, grd, blk, 0, s, d, p, f, a, f.advScr1, f.advScr2);
+      else hipLaunchKernelGGL(k_adv_r<false>, grd, blk, 0, s, d, p, f, a, f.advScr1, f.advScr1);
+    }
   }
   // GM/Redi fluxes as a template switch: without them the kernel holds half the registers
   if (p.useGMRedi) hipLaunchKernelGGL(k_tracer_rhs<true>, grd, blk, 0, s, d, p, f, a, iterPtr);

@@ -108,7 +108,7 @@ static const PDesc PARAMS[] = {
     PD(gravity), PD(gravitySign), PD(rhoNil), PD(tAlpha), PD(sBeta), PD(ivdc_kappa), PD(diffKhT), PD(diffKrT),
     PD(deltaTtracer), PI_(exactConserv), PI_(tempStepping), PI_(tempAdvection), PI_(tempForcing),
     PI_(implicitDiffusion), PI_(tempAdvScheme), PI_(saltStepping), PI_(saltAdvection), PI_(saltForcing),
-    PI_(saltAdvScheme), PD(diffKhS), PD(diffKrS), PI_(multiDimAdvection), PI_(momStepping),
+    PI_(saltAdvScheme), PD(diffKhS), PD(diffKrS), PI_(multiDimAdvection), PI_(multiDimCompressible), PI_(momStepping),
     PI_(eosType), PI_(allowFreezing), PI_(useRealFreshWaterFlux), PI_(useCDscheme), PI_(useGMRedi),
     PI_(periodicExternalForcing), PI_(nForcRec), PD(HeatCapacity_Cp), PD(convertFW2Salt), PD(temp_EvPrRn),
     PD(salt_EvPrRn), PD(rCD), PD(epsAB_CD), PD(externForcingPeriod), PD(externForcingCycle), PD(GM_background_K),
@@ -997,10 +997,13 @@ int mgcm_init(mgcm_model *m) {
   auto okScheme = [&](int s, const char *vname) {
     return (s == 2 || s == 33) && ext(vname, (double)s) == (double)s;
   };
-  // the cube's multi-dimensional split is 3-pass and face-dependent with corner fills
-  // (gad_advection.F:339-367); only the lat-lon 2-pass split is on the device
-  if (m->uvMap && ((m->p.tempStepping && m->p.tempAdvScheme != 2) || (m->p.saltStepping && m->p.saltAdvScheme != 2)))
-    return set_err("mgcm_init: multi-dimensional advection on an EXCH2 (cube) topology is not implemented");
+  // the cube's multi-dimensional split (3 face-dependent passes with corner fills,
+  // gad_advection.F:339-367) runs the general pass kernels (kernels_thermo.hip k_advg_*),
+  // which need the tile face / edge table of the EXCH2 topology and OLx = OLy (corner fills)
+  if (m->uvMap && ((m->p.tempStepping && m->p.tempAdvScheme != 2) || (m->p.saltStepping && m->p.saltAdvScheme != 2))) {
+    if (!m->f.tileFace) return set_err("mgcm_init: multi-dimensional advection on EXCH2 needs the tile face table");
+    if (m->d.OLx != m->d.OLy) return set_err("mgcm_init: cube multi-dimensional advection needs OLx = OLy");
+  }
   if (m->p.tempStepping && !okScheme(m->p.tempAdvScheme, "tempVertAdvScheme"))
     return set_err("mgcm_init: tempAdvScheme %d not implemented on the device", m->p.tempAdvScheme);
   if (m->p.saltStepping && !okScheme(m->p.saltAdvScheme, "saltVertAdvScheme"))
