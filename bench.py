@@ -320,7 +320,7 @@ def main():
                          "bytes_per_point": mom_bpp, "launch_ms": mom_ms,
                          "traffic": pmc_traffic(a.pmc_summary, "k_mom_")},
     }
-    if rank == 0 and not a.no_cpu_baseline:
+    if rank == 0 and world == 1 and not a.no_cpu_baseline:   # the CPU baseline is an N=1 line
         out["cpu_baseline"] = cpu_baseline(a.config, a.cpu_seconds)
     if rank == 0:
         print(json.dumps(out), flush=True)
