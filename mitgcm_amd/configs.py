@@ -454,7 +454,7 @@ CS32_FORCING = {"taux": "trenberth_taux.bin", "tauy": "trenberth_tauy.bin", "Qne
                 "EmPmR": "shiEmPR_cs32.bin", "SST": "lev_surfT_cs_12m.bin", "SSS": "lev_surfS_cs_12m.bin"}
 
 
-def global_ocean_cs32x15(data_dir=None, sNy=32):
+def global_ocean_cs32x15(data_dir=None, sNy=32, params_over=None):
     """verification/global_ocean.cs32x15 (BASELINE config 3): 6 faces of 32x32 on pkg/exch2,
     one 32x32 tile per face at OL=4 (SURVEY 8(d) C3 layout; sNy=16 gives the reference's
     code/SIZE.h tiling sNx=32, sNy=16, nSx=12, two tiles per face), 15 levels,
@@ -533,6 +533,7 @@ def global_ocean_cs32x15(data_dir=None, sNy=32):
              "EmPmR": forcing["EmPmR"][0], "SST": forcing["SST"][0], "SSS": forcing["SSS"][0]}
     for nm in ("h0FacC", "h0FacW", "h0FacS", "recip_Rcol", "rLowW", "rLowS", "rSurfW", "rSurfS"):
         state[nm] = g.f[nm]
+    params.update(params_over or {})   # option variants for parity tests
     return g, params, state, forcing
 
 

@@ -234,6 +234,7 @@ struct TracerArgs {
   const double *sfc;    // surface forcing (surfaceForcingT/S), or null
   double diffKh, diffKr, dT;
   int advection, multiDim, useAB, forcing;
+  int limiter;          // multi-dim face fluxes: 1 DST3FL (scheme 33), 0 DST3 (scheme 30)
 };
 
 // Fields exchanged together by k_exchange_multi.

@@ -374,7 +374,8 @@ __device__ __forceinline__ void vecinv_tend(const A &a, const Dims &d, const Par
       return p.vfFacMom * 1.0 * (-p.viscAr * G2(rAs, i, j) * (V3(i, j, kk) - V3(i, j, kk - 1)) * p.rkSign *
                                  f.recip_drC[kk - 1] * G3(maskS, i, j, kk) * G3(maskS, i, j, kk - 1));
     };
-    guDiss = guDiss - rhFacW * recip_drF * G2(recip_rAw, i, j) * (rvU(k + 1) - rvU(k)) * p.rkSign;
+    // skipped with implicitViscosity (mom_vecinv.F:444): k_mom_impl solves it after the k loop
+    if (!p.implicitViscosity) guDiss = guDiss - rhFacW * recip_drF * G2(recip_rAw, i, j) * (rvU(k + 1) - rvU(k)) * p.rkSign;
     if (p.no_slip_sides) {
       const double hS = G3(h0FacW, i, j, k) - a.h0fz(i, j);
       const double hN = G3(h0FacW, i, j, k) - a.h0fz(i, j + 1);
@@ -392,7 +393,7 @@ __device__ __forceinline__ void vecinv_tend(const A &a, const Dims &d, const Par
       cD = (k == Nr) ? cD * G3(maskW, i, j, k) : cD * G3(maskW, i, j, k) * (1.0 - G3(maskW, i, j, kDn));
       guDiss = guDiss + -cD * U(i, j) * rhFacW * recip_drF;
     }
-    gvDiss = gvDiss - rhFacS * recip_drF * G2(recip_rAs, i, j) * (rvV(k + 1) - rvV(k)) * p.rkSign;
+    if (!p.implicitViscosity) gvDiss = gvDiss - rhFacS * recip_drF * G2(recip_rAs, i, j) * (rvV(k + 1) - rvV(k)) * p.rkSign;
     if (p.no_slip_sides) {
       const double hW = G3(h0FacS, i, j, k) - a.h0fz(i, j);
       const double hE = G3(h0FacS, i, j, k) - a.h0fz(i + 1, j);
@@ -1267,6 +1268,69 @@ static void vi_tile_shape(const Dims &d, int &BX, int &BY) {
   BY = (H + nby - 1) / nby;                 // balance the rows over the blocks
 }
 
+// MOM_U_IMPLICIT_R / MOM_V_IMPLICIT_R (pkg/mom_common/mom_u_implicit_r.F:118-160,
+// mom_v_implicit_r.F) with implicitViscosity only (momImplVertAdv = F, selectImplicitDrag
+// = 0), after the DYNAMICS k loop (dynamics.F:568-580): the tri-diagonal system of the
+// vertical viscosity on u* (V = false: i = 1..sNx+1, j = 1..sNy) or v* (V = true:
+// i = 1..sNx, j = 1..sNy+1), solved in place with SOLVE_TRIDIAGONAL's default recurrence
+// (solve_tridiagonal.F:224-297); outside that range the system is the identity.  Column
+// frame as k_tracer_impl: k-parallel coefficients into LDS, one thread per column sweeps.
+template <bool V>
+__global__ void __launch_bounds__(256) k_mom_impl(Dims d, Params p, Fields f, int nc) {
+  extern __shared__ __attribute__((aligned(16))) double lds[];
+  MG_COLF(1, V ? d.sNx : d.sNx + 1, 1, V ? d.sNy + 1 : d.sNy, nc)
+  const int Nr = d.Nr, NS = Nr * NC_;
+  double *sSub = lds, *sSup = lds + NS, *sY = lds + 2 * NS;
+  double *g = V ? f.a3 + (long)F3_gV * d.N3all : f.a3 + (long)F3_gU * d.N3all;
+  const double *msk = V ? f.a3 + (long)F3_maskS * d.N3all : f.a3 + (long)F3_maskW * d.N3all;
+  const double *rh = V ? f.a3 + (long)F3_recip_hFacS * d.N3all : f.a3 + (long)F3_recip_hFacW * d.N3all;
+  if (valid) {
+    MG_COLF_K(k) {
+      const int me = (k - 1) * NC_ + cc;
+      const long q3 = MG_I3(d, i, j, k, t);
+      double sub = 0.0, sup = 0.0;   // kappaRU = kappaRV = viscArNr(k) (calc_viscosity.F)
+      if (k >= 2 && msk[MG_I3(d, i, j, k - 1, t)] == 1.0)
+        sub = -(p.deltaTMom * rh[q3] * f.recip_drF[k - 1] * p.viscAr * f.recip_drC[k - 1]);
+      if (k <= Nr - 1 && msk[MG_I3(d, i, j, k + 1, t)] == 1.0)
+        sup = -(p.deltaTMom * rh[q3] * f.recip_drF[k - 1] * p.viscAr * f.recip_drC[k]);
+      sSub[me] = sub;
+      sSup[me] = sup;
+      sY[me] = g[q3];
+    }
+  }
+  __syncthreads();
+  if (valid && kk == 0) {
+    double cpPrev = 0.0, ypPrev = 0.0;
+    for (int k2 = 1; k2 <= Nr; k2++) {
+      const int s2 = (k2 - 1) * NC_ + cc;
+      const double sub = sSub[s2], sup = sSup[s2];
+      const double diag = 1.0 - (sub + sup);
+      const double y = sY[s2];
+      double cp, yp;
+      if (k2 == 1) {
+        if (diag != 0.0) { const double rec = 1.0 / diag; cp = sup * rec; yp = y * rec; }
+        else { cp = 0.0; yp = 0.0; }
+      } else {
+        const double tmp = diag - sub * cpPrev;
+        if (tmp != 0.0) { const double rec = 1.0 / tmp; cp = sup * rec; yp = (y - sub * ypPrev) * rec; }
+        else { cp = 0.0; yp = 0.0; }
+      }
+      sSup[s2] = cp;
+      sY[s2] = yp;
+      cpPrev = cp; ypPrev = yp;
+    }
+    double below = 0.0;
+    for (int k2 = Nr; k2 >= 1; k2--) {
+      const int s2 = (k2 - 1) * NC_ + cc;
+      const double v = (k2 == Nr) ? sY[s2] : sY[s2] - sSup[s2] * below;
+      sSub[s2] = v;
+      below = v;
+    }
+  }
+  __syncthreads();
+  if (valid) MG_COLF_K(k) g[MG_I3(d, i, j, k, t)] = sSub[(k - 1) * NC_ + cc];
+}
+
 hipError_t launch_mom_step(const Dims &d, const Params &p, const Fields &f, const int *iterPtr, hipStream_t s) {
   hipLaunchKernelGGL(k_phi_hyd, dim3(mg_col_blocks(d.sNx + 3, d.sNy + 3, d.nT, d.Nr)), dim3(256), 0, s, d, p, f);
   if (p.momViscosity && (p.viscA4D != 0.0 || p.viscA4Z != 0.0))
@@ -1299,6 +1363,14 @@ hipError_t launch_mom_step(const Dims &d, const Params &p, const Fields &f, cons
   if (p.useCDscheme)
     hipLaunchKernelGGL(k_cd_scheme, dim3(mg_plane_blocks(d.nx - 2, d.ny - 2, d.nT * d.Nr)), dim3(MG_PLANE_THREADS), 0, s,
                        d, p, f, iterPtr);
+  if (p.implicitViscosity && d.Nr > 1) {   // dynamics.F:568-580
+    const long ncU = (long)(d.sNx + 1) * d.sNy * d.nT, ncV = (long)d.sNx * (d.sNy + 1) * d.nT;
+    const int nc = mg_colf_nc(ncU, d.Nr, 3);
+    MG_ALLOW_LDS(k_mom_impl<false>);
+    MG_ALLOW_LDS(k_mom_impl<true>);
+    hipLaunchKernelGGL(k_mom_impl<false>, dim3(mg_colf_blocks(ncU, nc)), dim3(256), mg_colf_lds(d.Nr, nc, 3), s, d, p, f, nc);
+    hipLaunchKernelGGL(k_mom_impl<true>, dim3(mg_colf_blocks(ncV, nc)), dim3(256), mg_colf_lds(d.Nr, nc, 3), s, d, p, f, nc);
+  }
   return hipGetLastError();
 }
 

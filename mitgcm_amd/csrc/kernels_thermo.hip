@@ -259,12 +259,15 @@ __device__ __forceinline__ double dst3fl_theta(double Rj, double Rother) {
   if (fabs(Rj) * thetaMax <= fabs(Rother)) return copysign(thetaMax, Rother * Rj);
   return Rother / Rj;
 }
-// face flux between cells m1 (upstream for positive transport) and p0
+// face flux between cells m1 (upstream for positive transport) and p0; lim = 0 is
+// GAD_DST3_ADV_X/Y (gad_dst3_adv_x.F:71-118, not OLD_DST3_FORMULATION): no limiter
 __device__ __forceinline__ double dst3fl_h(double uTr, double cfl, double tm2, double tm1, double t0, double tp1,
-                                           double mWm1, double mW0, double mWp1) {
+                                           double mWm1, double mW0, double mWp1, int lim = 1) {
   const double oneSixth = 1.0 / 6.0;
   const double Rjp = (tp1 - t0) * mWp1, Rj = (t0 - tm1) * mW0, Rjm = (tm1 - tm2) * mWm1;
   const double d0 = (2.0 - cfl) * (1.0 - cfl) * oneSixth, d1 = (1.0 - cfl * cfl) * oneSixth;
+  if (!lim)
+    return 0.5 * (uTr + fabs(uTr)) * (tm1 + (d0 * Rj + d1 * Rjm)) + 0.5 * (uTr - fabs(uTr)) * (t0 - (d0 * Rj + d1 * Rjp));
   const double psiP = dst3fl_limit(d0, d1, dst3fl_theta(Rj, Rjm), cfl);
   const double psiM = dst3fl_limit(d0, d1, dst3fl_theta(Rj, Rjp), cfl);
   return 0.5 * (uTr + fabs(uTr)) * (tm1 + psiP * Rj) + 0.5 * (uTr - fabs(uTr)) * (t0 - psiM * Rj);
@@ -288,7 +291,7 @@ __global__ void __launch_bounds__(256) k_adv_x(Dims d, Fields f, TracerArgs a) {
       const double cfl = fabs(f.uVel[MG_I3(d, ii, j, k, t)] * dT * f.recip_dxC[MG_I2(d, ii, j, t)]);
       return dst3fl_h(uTr(ii), cfl, T[MG_I3(d, ii - 2, j, k, t)], T[MG_I3(d, ii - 1, j, k, t)], T[MG_I3(d, ii, j, k, t)],
                       T[MG_I3(d, ii + 1, j, k, t)], f.maskW[MG_I3(d, ii - 1, j, k, t)], f.maskW[MG_I3(d, ii, j, k, t)],
-                      f.maskW[MG_I3(d, ii + 1, j, k, t)]);
+                      f.maskW[MG_I3(d, ii + 1, j, k, t)], a.limiter);
     };
     const long q = MG_I2(d, i, j, t);
     v = v - dT * f.recip_hFacC[q3] * f.recip_drF[k - 1] * f.recip_rA[q] *
@@ -312,7 +315,7 @@ __global__ void __launch_bounds__(256) k_adv_y(Dims d, Fields f, TracerArgs a) {
     const double cfl = fabs(f.vVel[MG_I3(d, i, jj, k, t)] * dT * f.recip_dyC[MG_I2(d, i, jj, t)]);
     return dst3fl_h(vTr(jj), cfl, L1[MG_I3(d, i, jj - 2, k, t)], L1[MG_I3(d, i, jj - 1, k, t)], L1[MG_I3(d, i, jj, k, t)],
                     L1[MG_I3(d, i, jj + 1, k, t)], f.maskS[MG_I3(d, i, jj - 1, k, t)], f.maskS[MG_I3(d, i, jj, k, t)],
-                    f.maskS[MG_I3(d, i, jj + 1, k, t)]);
+                    f.maskS[MG_I3(d, i, jj + 1, k, t)], a.limiter);
   };
   const long q = MG_I2(d, i, j, t);
   f.advScr2[q3] = L1[q3] - dT * f.recip_hFacC[q3] * f.recip_drF[k - 1] * f.recip_rA[q] *
@@ -343,9 +346,11 @@ __global__ void __launch_bounds__(256) k_adv_r(Dims d, Params p, Fields f, Trace
     const double cfl = fabs(f.wVel[MG_I3(d, i, j, kk, t)] * dT * f.recip_drC[kk - 1]);
     const double oneSixth = 1.0 / 6.0;
     const double d0 = (2.0 - cfl) * (1.0 - cfl) * oneSixth, d1 = (1.0 - cfl * cfl) * oneSixth;
+    const double rT = rtr(kk);
+    if (!a.limiter)   // GAD_DST3_ADV_R (gad_dst3_adv_r.F:70-119)
+      return 0.5 * (rT + fabs(rT)) * (LT(kk) + (d0 * Rj + d1 * Rjp)) + 0.5 * (rT - fabs(rT)) * (LT(km1) - (d0 * Rj + d1 * Rjm));
     const double psiP = dst3fl_limit(d0, d1, dst3fl_theta(Rj, Rjm), cfl);
     const double psiM = dst3fl_limit(d0, d1, dst3fl_theta(Rj, Rjp), cfl);
-    const double rT = rtr(kk);
     return 0.5 * (rT + fabs(rT)) * (LT(kk) + psiM * Rj) + 0.5 * (rT - fabs(rT)) * (LT(km1) - psiP * Rj);
   };
   const double kp1Msk = (k == Nr) ? 0.0 : 1.0;
@@ -472,13 +477,13 @@ __global__ void __launch_bounds__(256) k_advg_flux(Dims d, Fields f, TracerArgs 
     const double cfl = fabs(f.uVel[q3] * dT * f.recip_dxC[MG_I2(d, i, j, t)]);
     af = dst3fl_h(uTr, cfl, Lc[MG_I3(d, i - 2, j, k, t)], Lc[MG_I3(d, i - 1, j, k, t)], Lc[q3], Lc[MG_I3(d, i + 1, j, k, t)],
                   mask_loc(d, f, cube, edges, true, i - 1, j, k, t), mask_loc(d, f, cube, edges, true, i, j, k, t),
-                  mask_loc(d, f, cube, edges, true, i + 1, j, k, t));
+                  mask_loc(d, f, cube, edges, true, i + 1, j, k, t), a.limiter);
   } else if (ydir && j >= 3 - d.OLy && j <= d.sNy + d.OLy - 1) {
     const double vTr = f.vVel[q3] * (f.dxG[MG_I2(d, i, j, t)] * drF * f.hFacS[q3]);
     const double cfl = fabs(f.vVel[q3] * dT * f.recip_dyC[MG_I2(d, i, j, t)]);
     af = dst3fl_h(vTr, cfl, Lc[MG_I3(d, i, j - 2, k, t)], Lc[MG_I3(d, i, j - 1, k, t)], Lc[q3], Lc[MG_I3(d, i, j + 1, k, t)],
                   mask_loc(d, f, cube, edges, false, i, j - 1, k, t), mask_loc(d, f, cube, edges, false, i, j, k, t),
-                  mask_loc(d, f, cube, edges, false, i, j + 1, k, t));
+                  mask_loc(d, f, cube, edges, false, i, j + 1, k, t), a.limiter);
   }
   f.gTscr[q3] = af;
 }

@@ -948,6 +948,7 @@ static hipError_t update_r_star_cg2d(mgcm_model *m) {
 }
 
 int mgcm_init(mgcm_model *m) {
+  auto ext = [&](const char *n, double dflt) { auto it = m->extra.find(n); return it == m->extra.end() ? dflt : it->second; };
   HIPCHK(hipSetDevice(m->device));
   if (upload_halo(m)) return -1;
   if (build_nbr(m)) return -1;
@@ -970,7 +971,12 @@ int mgcm_init(mgcm_model *m) {
   if (m->p.selectP_inEOS_Zc > 2) return set_err("mgcm_init: selectP_inEOS_Zc = 3 needs the non-hydrostatic pressure");
   if (m->p.selectP_inEOS_Zc == 2 && !m->p.storePhiHyd4Phys)
     return set_err("mgcm_init: selectP_inEOS_Zc = 2 needs storePhiHyd4Phys (set_parms.F:297)");
-  if (m->p.implicitViscosity) return set_err("mgcm_init: implicitViscosity not supported by the device path yet");
+  // implicitViscosity: MOM_U/V_IMPLICIT_R (k_mom_impl); with the CD scheme the reference
+  // also runs IMPLDIFF on uVelD/vVelD (dynamics.F:614-634), not built
+  if (m->p.implicitViscosity && m->p.useCDscheme)
+    return set_err("mgcm_init: implicitViscosity with the CD scheme not implemented on the device");
+  if (m->p.implicitViscosity && (ext("momImplVertAdv", 0.0) != 0.0 || ext("selectImplicitDrag", 0.0) != 0.0))
+    return set_err("mgcm_init: momImplVertAdv / selectImplicitDrag not implemented on the device");
   if (m->p.vectorInvariantMomentum) {
     // the MOM_VECINV subset k_mom_step implements (see kernels_dyn.hip)
     if (m->d.OLx < 2 || m->d.OLy < 2) return set_err("mgcm_init: vector-invariant momentum needs OLx, OLy >= 2");
@@ -987,15 +993,14 @@ int mgcm_init(mgcm_model *m) {
   if (m->uvMap && m->p.useCDscheme) return set_err("mgcm_init: CD scheme on an EXCH2 topology not implemented");
   if (m->p.implicSurfPress != 1.0 || m->p.implicDiv2DFlow != 1.0)
     return set_err("mgcm_init: implicSurfPress/implicDiv2DFlow != 1 not supported yet");
-  auto ext = [&](const char *n, double dflt) { auto it = m->extra.find(n); return it == m->extra.end() ? dflt : it->second; };
   const bool sph = ext("usingSphericalPolarGrid", 0.0) != 0.0;
   m->p.metricSphere = sph && ext("selectMetricTerms", 1.0) >= 1.0;
   m->p.recip_rSphere = sph ? 1.0 / ext("rSphere", 6370.0e3) : 0.0;   // ini_parms.F:1334
   if (ext("integr_GeoPot", 2.0) != 2.0) return set_err("mgcm_init: only integr_GeoPot = 2 is implemented");
-  // tracer advection schemes implemented on the device: 2 (C2, AB2) and 33 (DST3 flux-limited,
-  // multi-dimensional); the vertical scheme must match the horizontal one
+  // tracer advection schemes implemented on the device: 2 (C2, AB2), 30 (DST3) and 33 (DST3
+  // flux-limited), the last two multi-dimensional; the vertical scheme must match the horizontal one
   auto okScheme = [&](int s, const char *vname) {
-    return (s == 2 || s == 33) && ext(vname, (double)s) == (double)s;
+    return (s == 2 || ((s == 30 || s == 33) && m->p.multiDimAdvection)) && ext(vname, (double)s) == (double)s;
   };
   // the cube's multi-dimensional split (3 face-dependent passes with corner fills,
   // gad_advection.F:339-367) runs the general pass kernels (kernels_thermo.hip k_advg_*),
@@ -1095,6 +1100,7 @@ static TracerArgs tracer_args(mgcm_model *m, bool salt) {
   // gad_init_fixed.F:126-162: multi-dim advection for non-C2 schemes, AB2 on the tendency for C2
   a.multiDim = p.multiDimAdvection && a.advection && scheme != 2;
   a.useAB = scheme == 2;
+  a.limiter = scheme == 33;   // DST3 (30) without, DST3FL (33) with the flux limiter
   return a;
 }
 

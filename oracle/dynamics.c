@@ -18,12 +18,61 @@ static void check_supported(const OModel *m) {
   if ((m->viscA4D != 0.0 || m->viscA4Z != 0.0) && m->OLx < 3) {
     fprintf(stderr, "oracle_dynamics: biharmonic viscosity needs OLx, OLy >= 3\n"); abort();
   }
-  if (m->implicitViscosity) { fprintf(stderr, "oracle_dynamics: implicitViscosity not yet restated\n"); abort(); }
+  if (m->implicitViscosity && m->useCDscheme) {   /* dynamics.F:614-634 would IMPLDIFF uVelD/vVelD */
+    fprintf(stderr, "oracle_dynamics: implicitViscosity with the CD scheme not restated\n"); abort();
+  }
   if (!m->usingCartesianGrid && !m->usingSphericalPolarGrid &&
       !(m->usingCurvilinearGrid && m->vectorInvariantMomentum)) {
     fprintf(stderr, "oracle_dynamics: grid/momentum-scheme combination not restated\n"); abort();
   }
   if (m->integr_GeoPot != 2) { fprintf(stderr, "oracle_dynamics: integr_GeoPot=%d not restated\n", m->integr_GeoPot); abort(); }
+}
+
+/* MOM_U_IMPLICIT_R / MOM_V_IMPLICIT_R (pkg/mom_common/mom_u_implicit_r.F:118-160,
+ * mom_v_implicit_r.F), implicitViscosity only (momImplVertAdv = F, selectImplicitDrag = 0;
+ * deepFac = rhoFac = 1): tri-diagonal coefficients on i0..i1 x j0..j1 (U: 1..sNx+1 x 1..sNy,
+ * V: 1..sNx x 1..sNy+1), identity elsewhere, then SOLVE_TRIDIAGONAL's default branch
+ * (solve_tridiagonal.F:224-297) over the whole tile, in place on g (= u* or v*). */
+static void mom_implicit_r(const OModel *m, double *g, const double *mask, const double *rhFac,
+                           const double *kappa, int i0, int i1, int j0, int j1) {
+  const int sNx = m->sNx, sNy = m->sNy, OLx = m->OLx, OLy = m->OLy, Nr = m->Nr, nx = m->nx;
+  const long n2 = m->n2;
+  double *sub = malloc(sizeof(double) * Nr), *sup = malloc(sizeof(double) * Nr);
+  double *cp = malloc(sizeof(double) * Nr), *yp = malloc(sizeof(double) * Nr);
+#define W3(a, i, j, k) (a)[(long)((i) + OLx - 1) + (long)((j) + OLy - 1) * nx + (long)((k) - 1) * n2]
+#define KAP(i, j, k) kappa[(long)((k) - 1) * n2 + ((i) + OLx - 1) + (long)((j) + OLy - 1) * nx]
+  for (int j = 1 - OLy; j <= sNy + OLy; j++)
+    for (int i = 1 - OLx; i <= sNx + OLx; i++) {
+      const int in = i >= i0 && i <= i1 && j >= j0 && j <= j1;
+      for (int k = 1; k <= Nr; k++) {
+        double b = 0.0, dd = 0.0;
+        if (in && k >= 2 && W3(mask, i, j, k - 1) == 1.0)   /* 1rst lower diagonal (:123-133) */
+          b = -(m->deltaTMom * W3(rhFac, i, j, k) * m->recip_drF[k - 1] * KAP(i, j, k) * m->recip_drC[k - 1]);
+        if (in && k <= Nr - 1 && W3(mask, i, j, k + 1) == 1.0)   /* 1rst upper diagonal (:135-145) */
+          dd = -(m->deltaTMom * W3(rhFac, i, j, k) * m->recip_drF[k - 1] * KAP(i, j, k + 1) * m->recip_drC[k]);
+        sub[k - 1] = b; sup[k - 1] = dd;
+      }
+      for (int k = 1; k <= Nr; k++) {
+        const double c = 1.0 - (sub[k - 1] + sup[k - 1]);   /* main diagonal (:147-153) */
+        const double y = W3(g, i, j, k);
+        if (k == 1) {
+          if (c != 0.0) { const double rec = 1.0 / c; cp[0] = sup[0] * rec; yp[0] = y * rec; }
+          else { cp[0] = 0.0; yp[0] = 0.0; }
+        } else {
+          const double tmp = c - sub[k - 1] * cp[k - 2];
+          if (tmp != 0.0) {
+            const double rec = 1.0 / tmp;
+            cp[k - 1] = sup[k - 1] * rec;
+            yp[k - 1] = (y - sub[k - 1] * yp[k - 2]) * rec;
+          } else { cp[k - 1] = 0.0; yp[k - 1] = 0.0; }
+        }
+      }
+      for (int k = Nr; k >= 1; k--)
+        W3(g, i, j, k) = (k == Nr) ? yp[k - 1] : yp[k - 1] - cp[k - 1] * W3(g, i, j, k + 1);
+    }
+#undef W3
+#undef KAP
+  free(sub); free(sup); free(cp); free(yp);
 }
 
 void oracle_dynamics(OModel *m) {
@@ -764,6 +813,10 @@ void oracle_dynamics(OModel *m) {
         }
     }
 #undef W3
+    if (m->implicitViscosity && Nr > 1) {   /* dynamics.F:568-580 */
+      mom_implicit_r(m, gU, maskW, rhFacW, kappaRU, 1, sNx + 1, 1, sNy);
+      mom_implicit_r(m, gV, maskS, rhFacS, kappaRV, 1, sNx, 1, sNy + 1);
+    }
   }
   (void)ab;
   for (int q = 0; q < 2; q++) { free(fVerU[q]); free(fVerV[q]); }

@@ -96,10 +96,14 @@ static double dst3fl_theta(double Rj, double Rother) {
   return Rother / Rj;
 }
 /* horizontal: Rjp = (T(i+1)-T(i))*mW(i+1), Rj = (T(i)-T(i-1))*mW(i), Rjm = (T(i-1)-T(i-2))*mW(i-1) */
+/* lim = 0: GAD_DST3_ADV_X/Y (gad_dst3_adv_x.F:71-118, scheme 30; OLD_DST3_FORMULATION undefined) */
+static int dst3_lim = 1;   /* set per tracer by gad_advection_dst3fl */
 static double dst3fl_h(double uTr, double cfl, double tm2, double tm1, double t0, double tp1,
                        double mWm1, double mW0, double mWp1) {
   const double Rjp = (tp1 - t0) * mWp1, Rj = (t0 - tm1) * mW0, Rjm = (tm1 - tm2) * mWm1;
   const double d0 = (2.0 - cfl) * (1.0 - cfl) * oneSixth, d1 = (1.0 - cfl * cfl) * oneSixth;
+  if (!dst3_lim)
+    return 0.5 * (uTr + fabs(uTr)) * (tm1 + (d0 * Rj + d1 * Rjm)) + 0.5 * (uTr - fabs(uTr)) * (t0 - (d0 * Rj + d1 * Rjp));
   const double psiP = dst3fl_limit(d0, d1, dst3fl_theta(Rj, Rjm), cfl);
   const double psiM = dst3fl_limit(d0, d1, dst3fl_theta(Rj, Rjp), cfl);
   return 0.5 * (uTr + fabs(uTr)) * (tm1 + psiP * Rj) + 0.5 * (uTr - fabs(uTr)) * (t0 - psiM * Rj);
@@ -282,9 +286,14 @@ static void gad_advection_dst3fl(const OModel *m, int t, const double *tr, const
           const double Rjm = (W3(locT3d, i, j, km2) - W3(locT3d, i, j, km1)) * W3(maskC, i, j, km1);
           const double cfl = fabs(W3(wVel, i, j, k) * dT * m->recip_drC[k - 1]);
           const double d0 = (2.0 - cfl) * (1.0 - cfl) * oneSixth, d1 = (1.0 - cfl * cfl) * oneSixth;
+          const double rT = L(rTrans, i, j);
+          if (!dst3_lim) {   /* GAD_DST3_ADV_R (gad_dst3_adv_r.F:70-119) */
+            L(fUp, i, j) = 0.5 * (rT + fabs(rT)) * (W3(locT3d, i, j, k) + (d0 * Rj + d1 * Rjp)) +
+                           0.5 * (rT - fabs(rT)) * (W3(locT3d, i, j, km1) - (d0 * Rj + d1 * Rjm));
+            continue;
+          }
           const double psiP = dst3fl_limit(d0, d1, dst3fl_theta(Rj, Rjm), cfl);
           const double psiM = dst3fl_limit(d0, d1, dst3fl_theta(Rj, Rjp), cfl);
-          const double rT = L(rTrans, i, j);
           L(fUp, i, j) = 0.5 * (rT + fabs(rT)) * (W3(locT3d, i, j, k) + psiM * Rj) +
                          0.5 * (rT - fabs(rT)) * (W3(locT3d, i, j, km1) - psiP * Rj);
         }
@@ -323,7 +332,7 @@ static void tracer_integrate(OModel *m, const TracerSpec *c) {
   const long n2 = m->n2, n3 = m->n3;
   const int multiDim = m->multiDimAdvection && c->advection && c->advScheme != 2 && c->advScheme != 3 && c->advScheme != 4;
   const int useAB = (c->advScheme == 2 || c->advScheme == 3 || c->advScheme == 4);   /* gad_init_fixed.F:144-162 */
-  if (!(c->advScheme == 2 || c->advScheme == 33) || c->vAdvScheme != c->advScheme) {
+  if (!(c->advScheme == 2 || ((c->advScheme == 30 || c->advScheme == 33) && multiDim)) || c->vAdvScheme != c->advScheme) {
     fprintf(stderr, "oracle tracer_integrate: advection scheme %d/%d not restated\n", c->advScheme, c->vAdvScheme); abort();
   }
   double *gT = calloc(n3, 8), *kappaRT = calloc(n3, 8);
@@ -391,6 +400,7 @@ static void tracer_integrate(OModel *m, const TracerSpec *c) {
           for (int i = 0; i <= sNx + 1; i++)
             W3(kappaRT, i, j, k) = W3(kappaRT, i, j, k) + W3(Kwz, i, j, k) * L(maskInC, i, j);
     for (long p = 0; p < n3; p++) gT[p] = 0.0;
+    dst3_lim = c->advScheme == 33;
     if (multiDim) gad_advection_dst3fl(m, t, theta, uVel, vVel, wVel, gT, m->deltaTtracer);
     for (long p = 0; p < n2; p++) { fVer[0][p] = fVer[1][p] = 0.0; rTrans[p] = 0.0; }
 

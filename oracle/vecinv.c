@@ -25,7 +25,7 @@ void oracle_mom_vecinv(OModel *m, int t, int k, const double *hFacZ, const doubl
   const int sNx = m->sNx, sNy = m->sNy, OLx = m->OLx, OLy = m->OLy, Nr = m->Nr, nx = m->nx;
   const long n2 = m->n2;
   const int iMin = 0, iMax = sNx + 1, jMin = 0, jMax = sNy + 1;
-  if (m->viscA4D != 0.0 || m->viscA4Z != 0.0 || m->implicitViscosity || m->useNHMTerms ||
+  if (m->viscA4D != 0.0 || m->viscA4Z != 0.0 || m->useNHMTerms ||
       m->select3dCoriScheme > 0 || m->useCDscheme) {
     fprintf(stderr, "oracle_mom_vecinv: option outside the restated subset\n");
     abort();
@@ -167,8 +167,9 @@ void oracle_mom_vecinv(OModel *m, int t, int k, const double *hFacZ, const doubl
           L(gvDiss, i, j) = 0.0;
         }
       }
-    /* MOM_U_RVISCFLUX(k+1) (pkg/mom_common/mom_u_rviscflux.F) -> fVerUkp; mom_vecinv.F:546-563 */
-    {
+    /* MOM_U_RVISCFLUX(k+1) (pkg/mom_common/mom_u_rviscflux.F) -> fVerUkp; mom_vecinv.F:444-463,
+     * skipped with implicitViscosity (MOM_U_IMPLICIT_R solves it after the k loop) */
+    if (!m->implicitViscosity) {
       const int kk = k + 1;
       for (long p = 0; p < n2; p++) vrF[p] = 0.0;
       if (kk > 1 && kk <= Nr)
@@ -216,8 +217,9 @@ void oracle_mom_vecinv(OModel *m, int t, int k, const double *hFacZ, const doubl
         for (int i = iMin; i <= iMax; i++)
           L(guDiss, i, j) = L(guDiss, i, j) + -L(cDrag, i, j) * L(uFld, i, j) * W3(rhFacW, i, j, k) * m->recip_drF[k - 1];
     }
-    /* V: MOM_V_RVISCFLUX(k+1), MOM_V_SIDEDRAG, MOM_V_BOTDRAG_COEFF (mom_vecinv.F:630-720) */
-    {
+    /* V: MOM_V_RVISCFLUX(k+1), MOM_V_SIDEDRAG, MOM_V_BOTDRAG_COEFF (mom_vecinv.F:556-575, 630-720);
+     * the vertical viscous flux is skipped with implicitViscosity */
+    if (!m->implicitViscosity) {
       const int kk = k + 1;
       for (long p = 0; p < n2; p++) vrF[p] = 0.0;
       if (kk > 1 && kk <= Nr)
