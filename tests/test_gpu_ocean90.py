@@ -121,6 +121,7 @@ def test_ocean90_10_steps(golden_dir):
     gold = json.load(open(os.path.join(golden_dir, EXP, "monitor.json")))
     from mitgcm_amd.model import dynstat
     worst_o, worst_r, worst_d = (99.0, None), (99.0, None), (99.0, None)
+    worst_c = (99.0, None)   # SURVEY 8(c)-3 check list: theta/salt/uvel/vvel min, max, sd
     for step in range(1, 11):
         m.forward_step(1)
         o.forward_step()
@@ -136,6 +137,9 @@ def test_ocean90_10_steps(golden_dir):
                 worst_o = min(worst_o, (digits(v, od[k]), (step, k, v, od[k])))
                 if not k.endswith("_mean"):
                     worst_d = min(worst_d, (digits(v, od[k]), (step, k)))
+                f = k.split("_")
+                if len(f) == 3 and f[1] in ("theta", "salt", "uvel", "vvel") and f[2] in ("min", "max", "sd"):
+                    worst_c = min(worst_c, (digits(v, od[k]), (step, k)))
             if k in gold[step] and k not in ("cg2d_iters", "dynstat_eta_mean", "cg2d_last_res"):
                 worst_r = min(worst_r, (digits(v, gold[step][k]), (step, k, v, gold[step][k])))
         worst_o = min(worst_o, (digits(md["cg2d_init_res"], od["cg2d_init_res"]), (step, "cg2d_init_res")))
@@ -146,7 +150,8 @@ def test_ocean90_10_steps(golden_dir):
         assert np.array_equal(dev[inner], ref[inner]), (n, np.abs(dev - ref)[inner].max())
     m.close()
     print("ocean90 10 steps (cg2dUseFMA=%d): device == device-order oracle bit for bit; vs reference-order oracle "
-          "%.2f at %s; vs results/output.txt %.2f at %s; dynstat series vs the oracle %.2f at %s" % (
-              (fma,) + worst_o + worst_r + worst_d))
+          "%.2f at %s; vs results/output.txt %.2f at %s; dynstat series vs the oracle %.2f at %s; "
+          "theta/salt/uvel/vvel min/max/sd %.2f at %s" % ((fma,) + worst_o + worst_r + worst_d + worst_c))
+    assert worst_c[0] >= 12.0, worst_c      # SURVEY 8(c)-3 bar on the check list
     assert worst_o[0] >= 10.0, worst_o
     assert worst_r[0] >= 10.0, worst_r
