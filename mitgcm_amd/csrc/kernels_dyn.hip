@@ -15,6 +15,7 @@
 #include <cstdlib>
 
 #include "common.h"
+#include <cstring>
 
 namespace mgcm {
 
@@ -220,7 +221,7 @@ __device__ __forceinline__ double vi_KE(const A &a, const Dims &d, const Params 
   (void)OLx; (void)OLy; (void)sNx; (void)sNy;
 #define U(ii, jj) a.uVel(ii, jj, k)
 #define V(ii, jj) a.vVel(ii, jj, k)
-#define G2(x, ii, jj) AR2(x, MG_I2(d, ii, jj, t))
+#define G2(x, ii, jj) a.template g2<F2_##x>(ii, jj)
 #define G3(x, ii, jj, kk) a.x(ii, jj, kk)
 
     if (ii < 1 - OLx || ii > sNx + OLx - 1 || jj < 1 - OLy || jj > sNy + OLy - 1) return 0.0;
@@ -254,7 +255,7 @@ __device__ __forceinline__ double vi_vort(const A &a, const Dims &d, const Param
   (void)OLx; (void)OLy; (void)sNx; (void)sNy;
 #define U(ii, jj) a.uVel(ii, jj, k)
 #define V(ii, jj) a.vVel(ii, jj, k)
-#define G2(x, ii, jj) AR2(x, MG_I2(d, ii, jj, t))
+#define G2(x, ii, jj) a.template g2<F2_##x>(ii, jj)
 #define G3(x, ii, jj, kk) a.x(ii, jj, kk)
 
     if (ii < 2 - OLx || jj < 2 - OLy || ii > sNx + OLx || jj > sNy + OLy) return 0.0;
@@ -296,7 +297,7 @@ __device__ __forceinline__ double vi_hdiv(const A &a, const Dims &d, const Param
   (void)OLx; (void)OLy; (void)sNx; (void)sNy;
 #define U(ii, jj) a.uVel(ii, jj, k)
 #define V(ii, jj) a.vVel(ii, jj, k)
-#define G2(x, ii, jj) AR2(x, MG_I2(d, ii, jj, t))
+#define G2(x, ii, jj) a.template g2<F2_##x>(ii, jj)
 #define G3(x, ii, jj, kk) a.x(ii, jj, kk)
 
     if (ii < 1 - OLx || ii > sNx + OLx - 1 || jj < 1 - OLy || jj > sNy + OLy - 1) return 0.0;
@@ -316,6 +317,7 @@ struct VIGlobal {
   VIG(uVel) VIG(vVel) VIG(wVel) VIG(hFacW) VIG(hFacS) VIG(recip_hFacC) VIG(recip_hFacW) VIG(recip_hFacS) VIG(maskW)
   VIG(maskS) VIG(maskC) VIG(h0FacW) VIG(h0FacS)
 #undef VIG
+  template <int F> __device__ __forceinline__ double g2(int ii, int jj) const { return f.a2[(long)F * d.N2all + MG_I2(d, ii, jj, t)]; }
   __device__ __forceinline__ double hfz(int ii, int jj) const { return vi_hfacz(*this, d, ii, jj, k); }
   __device__ __forceinline__ double h0fz(int ii, int jj) const { return vi_h0facz(*this, d, p, ii, jj, k); }
   __device__ __forceinline__ double KE(int ii, int jj) const { return vi_KE(*this, d, p, f, ii, jj, k, t); }
@@ -339,7 +341,7 @@ __device__ __forceinline__ void vecinv_tend(const A &a, const Dims &d, const Par
 #define U3(ii, jj, kk) a.uVel(ii, jj, kk)
 #define V3(ii, jj, kk) a.vVel(ii, jj, kk)
 #define W3(ii, jj, kk) a.wVel(ii, jj, kk)
-#define G2(x, ii, jj) AR2(x, MG_I2(d, ii, jj, t))
+#define G2(x, ii, jj) a.template g2<F2_##x>(ii, jj)
 #define G3(x, ii, jj, kk) a.x(ii, jj, kk)
   const double recip_drF = f.recip_drF[k - 1], drF = f.drF[k - 1];
   auto rhz = [&](int ii, int jj) -> double {   // r_hFacZ
@@ -949,6 +951,7 @@ struct VITile {
   const double *sU, *sV, *sW, *sHW, *sHS, *sHC;   // [3][EMAX] / w [2][EMAX]
   const double *sKE, *sVort, *sHfz, *sH0fz, *sHDiv;   // [IMAX]
   __device__ __forceinline__ int e(int ii, int jj) const { return (jj - j0 + 1) * EW + (ii - i0 + 1); }
+  template <int F> __device__ __forceinline__ double g2(int ii, int jj) const { return f.a2[(long)F * d.N2all + MG_I2(d, ii, jj, t)]; }
   __device__ __forceinline__ int sl(int kk) const { return (kk % 3) * VT_EMAX; }
   __device__ __forceinline__ double uVel(int ii, int jj, int kk) const { return sU[sl(kk) + e(ii, jj)]; }
   __device__ __forceinline__ double vVel(int ii, int jj, int kk) const { return sV[sl(kk) + e(ii, jj)]; }
@@ -1118,6 +1121,7 @@ struct VILevel {
   const double *sKE, *sVort, *sHfz, *sH0fz, *sHDiv;
   __device__ __forceinline__ int e(int ii, int jj) const { return (jj - j0 + 1) * EW + (ii - i0 + 1); }
   __device__ __forceinline__ long g(int ii, int jj, int kk) const { return MG_I3(d, ii, jj, kk, t); }
+  template <int F> __device__ __forceinline__ double g2(int ii, int jj) const { return f.a2[(long)F * d.N2all + MG_I2(d, ii, jj, t)]; }
   __device__ __forceinline__ double uVel(int ii, int jj, int kk) const { return kk == k ? sU[e(ii, jj)] : AR3(uVel, g(ii, jj, kk)); }
   __device__ __forceinline__ double vVel(int ii, int jj, int kk) const { return kk == k ? sV[e(ii, jj)] : AR3(vVel, g(ii, jj, kk)); }
   __device__ __forceinline__ double wVel(int ii, int jj, int kk) const { return kk == k ? sW[e(ii, jj)] : AR3(wVel, g(ii, jj, kk)); }
@@ -1234,6 +1238,303 @@ __global__ void __launch_bounds__(VT_NT) k_mom_vi_level(Dims d, Params p, Fields
   AR3(gV, q3) = a.vVel(i, j, k) + p.deltaTMom * (gVtmp + 0.0) * a.maskS(i, j, k);
 }
 
+// ---------------------------------------------------------------------------------------
+// MOM_VECINV + CALC_GRAD_PHI_HYD + TIMESTEP + ADAMS_BASHFORTH2 as a register-pipelined
+// k-march (default for VI): a workgroup owns a BX x BY block of the DYNAMICS range of one
+// tile and marches KC levels.  What stays constant down the column is fetched once: the
+// 2-D metrics the ring-point intermediates and the Coriolis averages reach (dxC, dyC,
+// recAz, dxG, dyG, recip_rA) are staged in LDS over the block extent, the output point's
+// own metrics (reciprocal spacings, areas, side-drag lengths, f at the three corners, rA
+// of the three w points) live in registers.  Per level only the level itself is staged:
+// u, v, hFacW, hFacS over the extent, hFacC in a 2-slot ring (maskC at k-1) and w in a
+// 2-slot ring (w at k+1); the vertical neighbours the output point needs (u, v, hFacW,
+// hFacS at k-1 and k+1) are its own column's values, carried in registers.  Level k+1
+// (and w at k+2) is fetched into registers while level k is computed, every load
+// unconditional with clamped indices, so a level's loads issue together.  The expression
+// trees are vecinv_tend's (accessor VIMarch), so the result is bit-identical to the
+// per-point and per-level kernels.
+struct VIMarchRegs {   // the output point's own 2-D values (i,j); n = (i,j+1), e = (i+1,j), w = (i-1,j), s = (i,j-1)
+  double recip_dxC, recip_dyC, recip_dxG, recip_dyG, rAw, rAs, recip_rAw, recip_rAs;
+  double dxV, dxVn, recip_dyU, recip_dyUn, dyU, dyUe, recip_dxV, recip_dxVe;
+  double fCoriG, fCoriGn, fCoriGe, rA, rAw_w, rA_s;
+};
+#ifndef MGCM_VM_PREFETCH
+#define MGCM_VM_PREFETCH 1
+#endif
+constexpr int VM_S2 = 6;   // LDS-staged 2-D fields: dxC, dyC, recip_rAz, dxG, dyG, recip_rA
+struct VIMarch {
+  const Dims &d; const Params &p; const Fields &f; int k, t, i0, j0, EW, IW, i, j;
+  const double *sU, *sV, *sHW, *sHS, *sHC, *sW, *s2;
+  const double *sKE, *sVort, *sHfz, *sH0fz, *sHDiv;
+  const VIMarchRegs &c;
+  double uM, uP, vM, vP, hwM, hwP, hsM, hsP;   // own column at k-1 and k+1
+  __device__ __forceinline__ int e(int ii, int jj) const { return (jj - j0 + 1) * EW + (ii - i0 + 1); }
+  __device__ __forceinline__ long g(int ii, int jj, int kk) const { return MG_I3(d, ii, jj, kk, t); }
+  __device__ __forceinline__ bool own(int ii, int jj) const { return ii == i && jj == j; }
+  // u, v, hFacW, hFacS: level k anywhere on the extent (LDS), other levels at the own point
+  // only (k-1 / k+1 registers) -- the only places MOM_VECINV reaches them; hFacC at k-1, k
+  // and w at k, k+1 from the 2-slot rings.  Selects, not branches: no fallback loads.
+  __device__ __forceinline__ double lvl(const double *sl, double m_, double p_, int ii, int jj, int kk) const {
+    if (!own(ii, jj)) return sl[e(ii, jj)];
+    return kk == k ? sl[e(ii, jj)] : (kk < k ? m_ : p_);
+  }
+  __device__ __forceinline__ double uVel(int ii, int jj, int kk) const { return lvl(sU, uM, uP, ii, jj, kk); }
+  __device__ __forceinline__ double vVel(int ii, int jj, int kk) const { return lvl(sV, vM, vP, ii, jj, kk); }
+  __device__ __forceinline__ double hFacW(int ii, int jj, int kk) const { return lvl(sHW, hwM, hwP, ii, jj, kk); }
+  __device__ __forceinline__ double hFacS(int ii, int jj, int kk) const { return lvl(sHS, hsM, hsP, ii, jj, kk); }
+  __device__ __forceinline__ double hFacC(int ii, int jj, int kk) const { return sHC[(kk & 1) * VT_EMAX + e(ii, jj)]; }
+  __device__ __forceinline__ double wVel(int ii, int jj, int kk) const { return sW[(kk & 1) * VT_EMAX + e(ii, jj)]; }
+  __device__ __forceinline__ double maskW(int ii, int jj, int kk) const { return hFacW(ii, jj, kk) != 0.0 ? 1.0 : 0.0; }
+  __device__ __forceinline__ double maskS(int ii, int jj, int kk) const { return hFacS(ii, jj, kk) != 0.0 ? 1.0 : 0.0; }
+  __device__ __forceinline__ double maskC(int ii, int jj, int kk) const { return hFacC(ii, jj, kk) != 0.0 ? 1.0 : 0.0; }
+  __device__ __forceinline__ double recip_hFacW(int ii, int jj, int kk) const {
+    const double h = hFacW(ii, jj, kk); return h != 0.0 ? 1.0 / h : 0.0; }
+  __device__ __forceinline__ double recip_hFacS(int ii, int jj, int kk) const {
+    const double h = hFacS(ii, jj, kk); return h != 0.0 ? 1.0 / h : 0.0; }
+  __device__ __forceinline__ double recip_hFacC(int ii, int jj, int kk) const {
+    const double h = hFacC(ii, jj, kk); return h != 0.0 ? 1.0 / h : 0.0; }
+  __device__ __forceinline__ double h0FacW(int ii, int jj, int kk) const { return AR3(h0FacW, g(ii, jj, kk)); }
+  __device__ __forceinline__ double h0FacS(int ii, int jj, int kk) const { return AR3(h0FacS, g(ii, jj, kk)); }
+  template <int F> __device__ __forceinline__ double g2(int ii, int jj) const {
+    const int di = ii - i, dj = jj - j;
+    if constexpr (F == F2_dxC) return s2[0 * VT_EMAX + e(ii, jj)];
+    else if constexpr (F == F2_dyC) return s2[1 * VT_EMAX + e(ii, jj)];
+    else if constexpr (F == F2_recip_rAz) return s2[2 * VT_EMAX + e(ii, jj)];
+    else if constexpr (F == F2_dxG) return s2[3 * VT_EMAX + e(ii, jj)];
+    else if constexpr (F == F2_dyG) return s2[4 * VT_EMAX + e(ii, jj)];
+    else if constexpr (F == F2_recip_rA) return s2[5 * VT_EMAX + e(ii, jj)];
+    else {
+#define VM_R(name, DI, DJ, reg) if constexpr (F == F2_##name) { if (di == (DI) && dj == (DJ)) return c.reg; }
+      VM_R(recip_dxC, 0, 0, recip_dxC) VM_R(recip_dyC, 0, 0, recip_dyC) VM_R(recip_dxG, 0, 0, recip_dxG)
+      VM_R(recip_dyG, 0, 0, recip_dyG) VM_R(rAw, 0, 0, rAw) VM_R(rAs, 0, 0, rAs) VM_R(recip_rAw, 0, 0, recip_rAw)
+      VM_R(recip_rAs, 0, 0, recip_rAs) VM_R(dxV, 0, 0, dxV) VM_R(dxV, 0, 1, dxVn) VM_R(recip_dyU, 0, 0, recip_dyU)
+      VM_R(recip_dyU, 0, 1, recip_dyUn) VM_R(dyU, 0, 0, dyU) VM_R(dyU, 1, 0, dyUe) VM_R(recip_dxV, 0, 0, recip_dxV)
+      VM_R(recip_dxV, 1, 0, recip_dxVe) VM_R(fCoriG, 0, 0, fCoriG) VM_R(fCoriG, 0, 1, fCoriGn)
+      VM_R(fCoriG, 1, 0, fCoriGe) VM_R(rA, 0, 0, rA) VM_R(rA, -1, 0, rAw_w) VM_R(rA, 0, -1, rA_s)
+#undef VM_R
+      return f.a2[(long)F * d.N2all + MG_I2(d, ii, jj, t)];   // anything else: where it lies
+    }
+  }
+  __device__ __forceinline__ int iv(int ii, int jj) const { return (jj - j0) * IW + (ii - i0); }
+  __device__ __forceinline__ int id(int ii, int jj) const { return (jj - j0 + 1) * IW + (ii - i0 + 1); }
+  __device__ __forceinline__ double hfz(int ii, int jj) const { return sHfz[iv(ii, jj)]; }
+  __device__ __forceinline__ double h0fz(int ii, int jj) const { return sH0fz[iv(ii, jj)]; }
+  __device__ __forceinline__ double vort(int ii, int jj) const { return sVort[iv(ii, jj)]; }
+  __device__ __forceinline__ double KE(int ii, int jj) const { return sKE[id(ii, jj)]; }
+  __device__ __forceinline__ double hDiv(int ii, int jj) const { return sHDiv[id(ii, jj)]; }
+};
+
+__global__ void __launch_bounds__(VT_NT) k_mom_vi_march(Dims d, Params p, Fields f, const int *iterPtr, int BX, int BY,
+                                                         int nbx, int nby, int KC, int nkc) {
+  __shared__ double sU[VT_EMAX], sV[VT_EMAX], sHW[VT_EMAX], sHS[VT_EMAX], sHC[2 * VT_EMAX], sW[2 * VT_EMAX];
+  __shared__ double s2[VM_S2 * VT_EMAX];
+  __shared__ double sKE[VT_IMAX], sVort[VT_IMAX], sHfz[VT_IMAX], sH0fz[VT_IMAX], sHDiv[VT_IMAX];
+  // block id: (i,j) block fastest, then the chunk of KC levels, then the tile
+  const int nb = nbx * nby, lb = mg_xcd_block();
+  const int t = d.t0 + lb / (nb * nkc), bxy = lb % nb, kb = 1 + ((lb / nb) % nkc) * KC;
+  const int Nr = d.Nr, ke = kb + KC - 1 < Nr ? kb + KC - 1 : Nr;
+  const int i0 = (bxy % nbx) * BX, j0 = (bxy / nbx) * BY;
+  const int tid = threadIdx.x;
+  const int EW = BX + 2, EN = (BX + 2) * (BY + 2), IW = BX + 1, IN = (BX + 1) * (BY + 1);
+  const int i = i0 + tid % BX, j = j0 + tid / BX;
+  const bool act = tid < BX * BY && i <= d.sNx + 1 && j <= d.sNy + 1;
+  const int ic = act ? i : 1, jc = act ? j : 1;   // in-range stand-in for idle threads' loads
+  const long q2 = MG_I2(d, ic, jc, t);
+  // the extent i0-1..i0+BX x j0-1..j0+BY, clipped to the array (points past it are read by
+  // no active thread): element r of this thread, its flat 2-D offset and whether it exists
+  long eq[2];
+  bool ein[2];
+#pragma unroll
+  for (int r = 0; r < 2; r++) {
+    const int ee = tid + r * VT_NT;
+    const int ii = i0 - 1 + ee % EW, jj = j0 - 1 + ee / EW;
+    ein[r] = ee < EN && ii <= d.sNx + d.OLx && jj <= d.sNy + d.OLy;
+    eq[r] = MG_I2(d, ein[r] ? ii : 1, ein[r] ? jj : 1, t);
+  }
+  // 2-D staging (once per workgroup)
+  {
+    const int ids[VM_S2] = {F2_dxC, F2_dyC, F2_recip_rAz, F2_dxG, F2_dyG, F2_recip_rA};
+#pragma unroll
+    for (int n = 0; n < VM_S2; n++)
+#pragma unroll
+      for (int r = 0; r < 2; r++) {
+        const int ee = tid + r * VT_NT;
+        const double v = f.a2[(long)ids[n] * d.N2all + eq[r]];
+        if (ee < EN) s2[n * VT_EMAX + ee] = ein[r] ? v : 0.0;
+      }
+  }
+  VIMarchRegs c;
+  {
+    const long qn = q2 + d.nx, qe = q2 + 1, qw = q2 - 1, qs = q2 - d.nx;
+    c.recip_dxC = AR2(recip_dxC, q2); c.recip_dyC = AR2(recip_dyC, q2);
+    c.recip_dxG = AR2(recip_dxG, q2); c.recip_dyG = AR2(recip_dyG, q2);
+    c.rAw = AR2(rAw, q2); c.rAs = AR2(rAs, q2); c.recip_rAw = AR2(recip_rAw, q2); c.recip_rAs = AR2(recip_rAs, q2);
+    c.dxV = AR2(dxV, q2); c.dxVn = AR2(dxV, qn); c.recip_dyU = AR2(recip_dyU, q2); c.recip_dyUn = AR2(recip_dyU, qn);
+    c.dyU = AR2(dyU, q2); c.dyUe = AR2(dyU, qe); c.recip_dxV = AR2(recip_dxV, q2); c.recip_dxVe = AR2(recip_dxV, qe);
+    c.fCoriG = AR2(fCoriG, q2); c.fCoriGn = AR2(fCoriG, qn); c.fCoriGe = AR2(fCoriG, qe);
+    c.rA = AR2(rA, q2); c.rAw_w = AR2(rA, qw); c.rA_s = AR2(rA, qs);
+  }
+  // level fetches into registers (unconditional loads, masked where the element is absent),
+  // addressed as uniform field base + 32-bit byte offset (the global_load saddr form)
+  const long t3 = (long)t * (d.n3 - d.n2);   // MG_I3 = MG_I2 + (k-1)*n2 + t*(n3-n2)
+  const unsigned lvB = (unsigned)(d.n2 * 8);
+  unsigned eb[2];
+#pragma unroll
+  for (int r = 0; r < 2; r++) eb[r] = (unsigned)((eq[r] + t3) * 8);
+  const unsigned ob = (unsigned)((q2 + t3) * 8);
+  const char *bU = (const char *)(f.a3 + (long)F3_uVel * d.N3all), *bV = (const char *)(f.a3 + (long)F3_vVel * d.N3all);
+  const char *bHW = (const char *)(f.a3 + (long)F3_hFacW * d.N3all), *bHS = (const char *)(f.a3 + (long)F3_hFacS * d.N3all);
+  const char *bHC = (const char *)(f.a3 + (long)F3_hFacC * d.N3all), *bW = (const char *)(f.a3 + (long)F3_wVel * d.N3all);
+  auto ld = [](const char *b, unsigned off) { return *(const double *)(b + off); };
+  double nU[2], nV[2], nHW[2], nHS[2], nHC[2], nW[2], oU, oV, oHW, oHS;
+  auto fetch = [&](int kk) {   // level kk over the extent + the own column's u, v, hFacW, hFacS
+    const unsigned lo = (unsigned)(kk - 1) * lvB;
+#pragma unroll
+    for (int r = 0; r < 2; r++) {
+      const unsigned o = eb[r] + lo;
+      nU[r] = ld(bU, o); nV[r] = ld(bV, o); nHW[r] = ld(bHW, o); nHS[r] = ld(bHS, o); nHC[r] = ld(bHC, o);
+    }
+    const unsigned o = ob + lo;
+    oU = ld(bU, o); oV = ld(bV, o); oHW = ld(bHW, o); oHS = ld(bHS, o);
+  };
+  auto fetchW = [&](int kk) {
+    const unsigned lo = (unsigned)(kk - 1) * lvB;
+#pragma unroll
+    for (int r = 0; r < 2; r++) nW[r] = ld(bW, eb[r] + lo);
+  };
+  auto stash = [&](int kk) {
+#pragma unroll
+    for (int r = 0; r < 2; r++) {
+      const int ee = tid + r * VT_NT;
+      if (ee < EN) {
+        sU[ee] = ein[r] ? nU[r] : 0.0; sV[ee] = ein[r] ? nV[r] : 0.0;
+        sHW[ee] = ein[r] ? nHW[r] : 0.0; sHS[ee] = ein[r] ? nHS[r] : 0.0;
+        sHC[(kk & 1) * VT_EMAX + ee] = ein[r] ? nHC[r] : 0.0;
+      }
+    }
+  };
+  auto stashW = [&](int kk) {
+#pragma unroll
+    for (int r = 0; r < 2; r++) {
+      const int ee = tid + r * VT_NT;
+      if (ee < EN) sW[(kk & 1) * VT_EMAX + ee] = (ein[r] && kk <= Nr) ? nW[r] : 0.0;
+    }
+  };
+  // prologue: own column at kb-1; hFacC at kb-1; level kb; w at kb and kb+1
+  double uM = 0.0, vM = 0.0, hwM = 0.0, hsM = 0.0;
+  if (kb > 1) {
+    fetch(kb - 1);
+    uM = oU; vM = oV; hwM = oHW; hsM = oHS;
+#pragma unroll
+    for (int r = 0; r < 2; r++) {
+      const int ee = tid + r * VT_NT;
+      if (ee < EN) sHC[((kb - 1) & 1) * VT_EMAX + ee] = ein[r] ? nHC[r] : 0.0;
+    }
+  }
+  fetchW(kb);
+  stashW(kb);
+  fetchW(kb + 1 <= Nr ? kb + 1 : Nr);
+  stashW(kb + 1);
+  fetch(kb);
+  stash(kb);
+  const int myIter = *iterPtr;
+  const double abFac = (myIter == p.nIter0 && p.nIter0 == 0) ? 0.0 : 0.5 + p.abEps;   // adams_bashforth2.F:61-65
+  const double mass2rUnit = 1.0 / p.rhoConst;
+  const bool rstar = p.nonlinFreeSurf > 0 && p.select_rStar > 0;
+  __syncthreads();
+  for (int k = kb; k <= ke; k++) {
+    const int kn = k + 1 <= Nr ? k + 1 : Nr, kw = k + 2 <= Nr ? k + 2 : Nr;
+#if MGCM_VM_PREFETCH
+    fetch(kn);    // level k+1 and the own column at k+1, in flight during level k
+    fetchW(kw);
+#else
+    {   // own column at k+1 only; the level itself is fetched after the output
+      const unsigned o = ob + (unsigned)(kn - 1) * lvB;
+      oU = ld(bU, o); oV = ld(bV, o); oHW = ld(bHW, o); oHS = ld(bHS, o);
+    }
+#endif
+    // the output point's accessor, and one for the ring-point intermediates whose own point
+    // matches nothing (they read level k only; an idle thread's registers hold (1,1)'s values)
+    VIMarch a{d, p, f, k, t, i0, j0, EW, IW, i, j, sU, sV, sHW, sHS, sHC, sW, s2, sKE, sVort, sHfz, sH0fz, sHDiv, c,
+              uM, k < Nr ? oU : 0.0, vM, k < Nr ? oV : 0.0, hwM, k < Nr ? oHW : 0.0, hsM, k < Nr ? oHS : 0.0};
+    VIMarch ai{d, p, f, k, t, i0, j0, EW, IW, -1000000, -1000000, sU, sV, sHW, sHS, sHC, sW, s2, sKE, sVort, sHfz, sH0fz,
+               sHDiv, c, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
+    for (int q = tid; q < IN; q += VT_NT) {
+      const int ii = i0 + q % IW, jj = j0 + q / IW;          // vort / hFacZ grid: i0..i0+BX
+      const bool ok = ii <= d.sNx + d.OLx && jj <= d.sNy + d.OLy;
+      sHfz[q] = ok ? vi_hfacz(ai, d, ii, jj, k) : 0.0;
+      sH0fz[q] = ok ? vi_h0facz(ai, d, p, ii, jj, k) : 0.0;
+      sVort[q] = ok ? vi_vort(ai, d, p, f, ii, jj, k, t) : 0.0;
+      sKE[q] = vi_KE(ai, d, p, f, ii - 1, jj - 1, k, t);     // KE / hDiv grid: i0-1..i0+BX-1
+      sHDiv[q] = vi_hdiv(ai, d, p, f, ii - 1, jj - 1, k, t);
+    }
+    __syncthreads();
+    if (act) {
+      auto q3of = [&](long qq2, int kk) { return qq2 + (long)(kk - 1) * d.n2 + t3; };
+      const long q3 = q3of(q2, k);
+      const double recip_drF = f.recip_drF[k - 1];
+      double gU = 0.0, gV = 0.0, guDiss = 0.0, gvDiss = 0.0, dPhiHydX = 0.0, dPhiHydY = 0.0;
+      {  // CALC_GRAD_PHI_HYD (calc_grad_phi_hyd.F:152-214), as k_mom_step
+        const bool rsc = rstar && p.select_rStar >= 2 && p.nonlinFreeSurf >= 4;
+        auto varLoc = [&](long qq2) {
+          return rsc ? AR3(phiHydC, q3of(qq2, k)) * AR2(rStarFacC, qq2) + 0.0 : AR3(phiHydC, q3of(qq2, k)) + 0.0;
+        };
+        const double vl = varLoc(q2);
+        if (i >= 1) dPhiHydX = c.recip_dxC * (vl - varLoc(q2 - 1));
+        if (j >= 1) dPhiHydY = c.recip_dyC * (vl - varLoc(q2 - d.nx));
+        if (rstar && p.select_rStar >= 2) {
+          const double factorP = p.gravity * (1.0 / p.rhoConst) * 0.5, rCk = f.rC[k - 1];
+          auto vl2 = [&](long qq2) { return AR2(etaH, qq2) * (1.0 + rCk * AR2(recip_Rcol, qq2)); };
+          const double e0 = vl2(q2), a0 = AR3(alphaRho, q3);
+          if (i >= 1) dPhiHydX = dPhiHydX + factorP * (AR3(alphaRho, q3 - 1) + a0) * (e0 - vl2(q2 - 1)) * c.recip_dxC;
+          if (j >= 1) dPhiHydY = dPhiHydY + factorP * (AR3(alphaRho, q3 - d.nx) + a0) * (e0 - vl2(q2 - d.nx)) * c.recip_dyC;
+        }
+      }
+      vecinv_tend(a, d, p, f, i, j, k, t, gU, gV, guDiss, gvDiss);
+      double guExt = 0.0, gvExt = 0.0;
+      if (p.momForcing && k == 1) {
+        if (j >= 0 && j <= d.sNy + 1 && i >= 1 && i <= d.sNx + 1)
+          guExt = guExt + p.foFacMom * (AR2(fu, q2) * mass2rUnit) * recip_drF * a.recip_hFacW(i, j, k);
+        if (j >= 1 && j <= d.sNy + 1 && i >= 0 && i <= d.sNx + 1)
+          gvExt = gvExt + p.foFacMom * (AR2(fv, q2) * mass2rUnit) * recip_drF * a.recip_hFacS(i, j, k);
+      }
+      gU = gU - p.pfFacMom * dPhiHydX;
+      gV = gV - p.pfFacMom * dPhiHydY;
+      if (p.momViscosity && p.momDissip_In_AB) { gU = gU + guDiss; gV = gV + gvDiss; }
+      if (p.momForcing && p.momForcingOutAB != 1) { gU = gU + guExt; gV = gV + gvExt; }
+      {  // ADAMS_BASHFORTH2 (adams_bashforth2.F:81-88)
+        const double gUo = AR3(guNm1, q3), gVo = AR3(gvNm1, q3);
+        double ab = abFac * (gU - gUo);
+        AR3(guNm1, q3) = gU;
+        gU = gU + ab;
+        ab = abFac * (gV - gVo);
+        AR3(gvNm1, q3) = gV;
+        gV = gV + ab;
+      }
+      double gUtmp = gU, gVtmp = gV;
+      if (p.momForcing && p.momForcingOutAB == 1) { gUtmp = gUtmp + guExt; gVtmp = gVtmp + gvExt; }
+      if (p.momViscosity && !p.momDissip_In_AB) { gUtmp = gUtmp + guDiss; gVtmp = gVtmp + gvDiss; }
+      if (rstar && p.nonlinFreeSurf > 1) {
+        gUtmp = gUtmp / AR2(rStarExpW, q2);
+        gVtmp = gVtmp / AR2(rStarExpS, q2);
+      }
+      AR3(gU, q3) = a.uVel(i, j, k) + p.deltaTMom * (gUtmp + 0.0) * a.maskW(i, j, k);
+      AR3(gV, q3) = a.vVel(i, j, k) + p.deltaTMom * (gVtmp + 0.0) * a.maskS(i, j, k);
+    }
+    if (k == ke) break;
+    // the own column moves down: level k becomes k-1 (read before level k+1 overwrites it)
+    if (act) { const int eo = a.e(i, j); uM = sU[eo]; vM = sV[eo]; hwM = sHW[eo]; hsM = sHS[eo]; }
+#if !MGCM_VM_PREFETCH
+    fetch(kn);
+    fetchW(kw);
+#endif
+    __syncthreads();
+    stash(k + 1);
+    stashW(k + 2);
+    __syncthreads();
+  }
+}
+
 // The halo ring outside the DYNAMICS range (i or j outside 0..sN+1): no tendency, but
 // ADAMS_BASHFORTH2 runs over the whole slab (gU = abFac*(0 - guNm1), guNm1 = 0), as
 // k_mom_step does there.
@@ -1344,7 +1645,20 @@ hipError_t launch_mom_step(const Dims &d, const Params &p, const Fields &f, cons
     // levels per workgroup: enough workgroups to fill the chip several times, few enough
     // that the two extra staged levels per chunk stay a small overhead
     static const int kcEnv = getenv("MGCM_VI_KC") ? atoi(getenv("MGCM_VI_KC")) : 0;
-    if (kcEnv <= 0) {   // one level per workgroup (default)
+    static const char *viEnv = getenv("MGCM_VI_KERNEL");   // march | level | tiled (sweeps)
+    // the k-march (MGCM_VI_KERNEL=march; chunk MGCM_VI_KC, default: >= 3072 workgroups):
+    // measured on LLC-90 at the same time as the per-level kernel (25 % fewer VALU
+    // instructions, 29 % fewer HBM bytes, but 227-251 VGPRs: 2 waves/SIMD against 4), so the
+    // per-level kernel stays the default
+    const int nbt = nbx * nby * d.nT;
+    int KCm = (d.Nr + (3072 / nbt > 0 ? 3072 / nbt : 1) - 1) / (3072 / nbt > 0 ? 3072 / nbt : 1);
+    if (kcEnv > 0) KCm = kcEnv > d.Nr ? d.Nr : kcEnv;
+    const bool march = viEnv && !strcmp(viEnv, "march");
+    if (march) {
+      const int nkc = (d.Nr + KCm - 1) / KCm;
+      hipLaunchKernelGGL(k_mom_vi_march, dim3((unsigned)(nbt * nkc)), dim3(VT_NT), 0, s, d, p, f, iterPtr, BX, BY, nbx,
+                         nby, KCm, nkc);
+    } else if (kcEnv <= 0 || (viEnv && !strcmp(viEnv, "level"))) {   // one level per workgroup
       hipLaunchKernelGGL(k_mom_vi_level, dim3((unsigned)(nbx * nby * d.nT * d.Nr)), dim3(VT_NT), 0, s, d, p, f, iterPtr, BX,
                          BY, nbx, nby);
     } else {            // MGCM_VI_KC levels marched per workgroup
