@@ -54,6 +54,9 @@ def parse():
     ap.add_argument("--shard", action="store_true",
                     help="N>1: shard the workload's tiles over the N processes (RCCL, strong scaling, "
                          "mitgcm_amd/parallel.py) instead of running N replicas")
+    ap.add_argument("--cg2d", choices=["replicated", "distributed"], default="replicated",
+                    help="with --shard: CG2D replicated on every GPU (default) or the reference's distributed "
+                         "CG2D with GLOBAL_SUM_TILE_RL over the collective (mitgcm_amd/parallel.py)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--pmc-summary", default=None,
                     help="tools/pmc_summary.py output of rocprofv3 --pmc passes of this command (roofline.traffic); "
@@ -209,7 +212,7 @@ def main():
     stepper = m
     if shard:
         from mitgcm_amd.parallel import ShardedModel
-        stepper = ShardedModel(m, dist)
+        stepper = ShardedModel(m, dist, cg2d=a.cg2d)
 
     def sync():
         m.sync()
@@ -297,7 +300,8 @@ def main():
                                                            "gloo, host-staged") if shard
                                                        else "; replicas only"),
                    "tiles_per_gpu": stepper.nT if shard else g.nTiles, "points_per_tile": [g.sNx, g.sNy, g.Nr],
-                   "parallelism": ("tiles%d" if shard else "replicas%d") % world},
+                   "parallelism": ("tiles%d" if shard else "replicas%d") % world,
+                   "cg2d": a.cg2d if shard else "single-GPU kernel"},
         "cg2d_iters_per_s": cg2d_iters_per_s,
         "cg2d_mean_iters_per_solve": iters_total / max(1, len(iters)),
         "kernel_ms_mean": {k: v[0] for k, v in kern.items()},

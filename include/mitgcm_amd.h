@@ -135,6 +135,21 @@ int mgcm_tile_copy(mgcm_model *m, const char *name, int t0, int nT, void *buf, i
 int mgcm_begin_steps(mgcm_model *m);
 /* One FORWARD_STEP split at its exchange points, phase = 1..4 (see model.hip). */
 int mgcm_step_phase(mgcm_model *m, int phase);
+/* Distributed CG2D (mitgcm_amd/parallel.py, cg2dMode = "distributed"): one operation of
+ * model/src/cg2d.F:100-415 over this process's tiles (op 0 normalise + max, 1 scale by a0,
+ * 2 initial residual, 3 preconditioner, 4 s = q + a0*s, 5 A s, 6 x/r update with a0,
+ * 7 un-normalise), per-tile partials to the device buffer part[2*nTiles] -- the per-tile
+ * values GLOBAL_SUM_TILE_RL (eesupp/src/global_sum_tile.F:14-17,161-191) sums in tile order.
+ * Phase 6 of mgcm_step_phase finishes phase 2 after such a solve. */
+int mgcm_cg2d_op(mgcm_model *m, int op, double a0, double *part);
+/* Store CG2D's output arguments (cg2d.F:13-17) as this step's solve record. */
+int mgcm_cg2d_record(mgcm_model *m, double firstResidual, double lastResidual, double rhsMax, double sumRHS,
+                     int numIters);
+/* Gather (unpack=0) / scatter (1) a 2-D field at n device-resident flat offsets idx. */
+int mgcm_field_pack(mgcm_model *m, const char *name, const long *idx, long n, double *buf, int unpack);
+/* EXCH of one field from this process's copy of the domain (EXCH_XY_RL / EXCH_S3D_RL with
+ * the model's halo map; the cross-process sources must have been delivered first). */
+int mgcm_exchange_field(mgcm_model *m, const char *name);
 
 int mgcm_sync(mgcm_model *m);
 

@@ -60,6 +60,10 @@ def lib():
         "mgcm_begin_steps": (ci, [vp]),
         "mgcm_tile_copy": (ci, [vp, cs, ci, ci, vp, ci]),
         "mgcm_step_phase": (ci, [vp, ci]),
+        "mgcm_cg2d_op": (ci, [vp, ci, cd, vp]),
+        "mgcm_cg2d_record": (ci, [vp, cd, cd, cd, cd, ci]),
+        "mgcm_field_pack": (ci, [vp, cs, vp, cl, vp, ci]),
+        "mgcm_exchange_field": (ci, [vp, cs]),
         "mgcm_oceanic_phys": (ci, [vp]),
         "mgcm_tracer_step": (ci, [vp]),
         "mgcm_exchange_host": (ci, [vp, PD, PD, ci, ci, ci]),
@@ -83,7 +87,8 @@ EXPORTS = ["mgcm_create", "mgcm_destroy", "mgcm_last_error", "mgcm_set_param", "
            "mgcm_solve_for_pressure", "mgcm_momentum_correction_step", "mgcm_integr_continuity",
            "mgcm_blocking_exchanges", "mgcm_prepare", "mgcm_forward_step", "mgcm_sync", "mgcm_cg2d", "mgcm_cg2d_sum_plan", "mgcm_solve_stats", "mgcm_monitor",
            "mgcm_kernel_ms", "mgcm_kernel_timing", "mgcm_set_tile_range", "mgcm_set_stream",
-           "mgcm_exchange_nfields", "mgcm_halo_pack", "mgcm_tile_copy", "mgcm_begin_steps", "mgcm_step_phase", "ini_cg2d_amd_",
+           "mgcm_exchange_nfields", "mgcm_halo_pack", "mgcm_tile_copy", "mgcm_begin_steps", "mgcm_step_phase", "mgcm_cg2d_op",
+           "mgcm_cg2d_record", "mgcm_field_pack", "mgcm_exchange_field", "ini_cg2d_amd_",
            "cg2d_amd_", "mgcm_oceanic_phys", "mgcm_tracer_step", "mgcm_exchange_host", "mgcm_field_count", "mgcm_param_name",
            "mgcm_amd_setup_", "mgcm_amd_param_", "mgcm_amd_bind_", "mgcm_amd_init_", "do_oceanic_phys_amd_",
            "thermodynamics_amd_", "dynamics_amd_", "solve_for_pressure_amd_", "momentum_correction_step_amd_",

@@ -33,7 +33,7 @@ struct Dims {
     X(cg2d_b) X(cg2d_x) X(Qnet) X(EmPmR) X(SSS) X(lambdaSaltClimRelax) X(etaNm1) X(fCoriCos) X(recip_Rcol) \
     X(rSurfW) X(rSurfS) X(rLowW) X(rLowS) X(Ro_surf) X(R_low) X(rStarFacC) X(rStarFacW) X(rStarFacS) \
     X(rStarExpC) X(rStarExpW) X(rStarExpS) X(rStarDhCDt) X(rStarDhWDt) X(rStarDhSDt) X(PmEpR) X(dEtaHdt) \
-    X(maskInW) X(maskInS) X(fCoriG) X(recip_rAz) X(recip_dxG) X(recip_dyG) X(etaHnm1)
+    X(maskInW) X(maskInS) X(fCoriG) X(recip_rAz) X(recip_dxG) X(recip_dyG) X(etaHnm1) X(cg2d_r) X(cg2d_s) X(cg2d_q)
 #define MG_F3D_LIST(X) X(hFacC) X(hFacW) X(hFacS) X(recip_hFacC) X(recip_hFacW) X(recip_hFacS) X(maskC) X(maskW) \
     X(maskS) X(uVel) X(vVel) X(wVel) X(theta) X(salt) X(gU) X(gV) X(guNm1) X(gvNm1) X(rhoInSitu) X(IVDConvCount) \
     X(gtNm1) X(thetaNext) X(gTscr) X(cpScr) X(phiHydC) X(saltNext) X(gsNm1) X(advScr1) X(advScr2) X(gAdv) \
@@ -129,6 +129,7 @@ struct Fields {
   const int *tileFace, *tileEdge;   // per tile: exch2_myFace, edge bits N=1 S=2 E=4 W=8
   // solver work
   double *cg2d_b, *cg2d_x;
+  double *cg2d_r, *cg2d_s, *cg2d_q;   // distributed CG2D work vectors (kernels_cg2d_dist.hip)
   // the 2-D and 3-D arenas (MG_F2D_LIST / MG_F3D_LIST order)
   double *a2, *a3;
 };

@@ -34,6 +34,9 @@ hipError_t launch_cg2d_blk2(const Dims &, const Params &, const Fields &, const 
                             SolveRecord *, int *, hipStream_t);
 int cg2d_block_max_points();
 hipError_t launch_exchange(const Dims &, double *, const long *, int, int, hipStream_t);
+hipError_t launch_cgd(const Dims &, const Params &, const Fields &, int, double, double *, hipStream_t);
+hipError_t launch_cgd_record(SolveRecord *, const int *, double, double, double, double, int, hipStream_t);
+hipError_t launch_field_pack(double *, const long *, long, double *, int, hipStream_t);
 hipError_t launch_correction(const Dims &, const Params &, const Fields &, hipStream_t);
 hipError_t launch_bump_counter(int *, int, hipStream_t);
 hipError_t launch_exchange_multi(const Dims &, const XFields &, const long *, int, int *, hipStream_t);
@@ -1455,6 +1458,10 @@ int mgcm_step_phase(mgcm_model *m, int phase) {
       TIMED(K_ETA, launch_exch_eta(m->d, m->p, m->f, m->d_srcOf, false, 0, m->stream));
       TIMED(K_CONT, launch_corr_cont(m->d, m->p, m->f, 0, m->stream));
       return 0;
+    case 6:   // phase 2 after a CG2D driven by the caller (mgcm_cg2d_op: distributed CG2D)
+      TIMED(K_ETA, launch_exch_eta(m->d, m->p, m->f, m->d_srcOf, false, 0, m->stream));
+      TIMED(K_CONT, launch_corr_cont(m->d, m->p, m->f, 0, m->stream));
+      return 0;
     case 3:
       if (m->p.exactConserv) TIMED(K_ETA, launch_exch_eta(m->d, m->p, m->f, m->d_srcOf, true, 0, m->stream));
       if (m->p.nonlinFreeSurf > 0) TIMED(K_RSTAR, calc_r_star(m));
@@ -1471,6 +1478,37 @@ int mgcm_step_phase(mgcm_model *m, int phase) {
       return 0;
   }
   return set_err("mgcm_step_phase: no phase %d", phase);
+}
+
+// Distributed CG2D building blocks (kernels_cg2d_dist.hip): one op of cg2d.F over this
+// process's tiles, per-tile partial sums into the device buffer part[2*nTiles].
+int mgcm_cg2d_op(mgcm_model *m, int op, double a0, double *part) {
+  if (check_ready(m)) return -1;
+  if (op < 0 || op > 7) return set_err("mgcm_cg2d_op: no op %d", op);
+  if (m->p.cg2dUseMinResSol) return set_err("mgcm_cg2d_op: cg2dUseMinResSol not implemented in the distributed CG2D");
+  HIPCHK(launch_cgd(m->d, m->p, m->f, op, a0, part, m->stream));
+  return 0;
+}
+
+int mgcm_cg2d_record(mgcm_model *m, double firstResidual, double lastResidual, double rhsMax, double sumRHS,
+                     int numIters) {
+  if (check_ready(m)) return -1;
+  HIPCHK(launch_cgd_record(m->d_rec, m->d_ctr + 1, firstResidual, lastResidual, rhsMax, sumRHS, numIters, m->stream));
+  return 0;
+}
+
+int mgcm_field_pack(mgcm_model *m, const char *name, const long *idx, long n, double *buf, int unpack) {
+  const FieldDesc *fd = find_field(name);
+  if (!fd || fd->kind != F2D) return set_err("mgcm_field_pack: no 2-D field '%s'", name);
+  HIPCHK(launch_field_pack(field_ptr(m, fd), idx, n, buf, unpack, m->stream));
+  return 0;
+}
+
+int mgcm_exchange_field(mgcm_model *m, const char *name) {
+  const FieldDesc *fd = find_field(name);
+  if (!fd || fd->kind == F1D) return set_err("mgcm_exchange_field: no 2-D/3-D field '%s'", name);
+  HIPCHK(launch_exchange(m->d, field_ptr(m, fd), m->d_halo, m->nHalo, fd->kind == F2D ? 1 : m->d.Nr, m->stream));
+  return 0;
 }
 
 int mgcm_sync(mgcm_model *m) {

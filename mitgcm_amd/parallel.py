@@ -18,13 +18,20 @@ The MI355X design keeps the 3-D work sharded and the 2-D solve replicated:
   (u, v, w, theta, salt) with each neighbouring process (twice with
   staggerTimeStep: the new velocities before THERMODYNAMICS, then the
   tracers);
-* CG2D itself runs on the gathered global problem on every GPU with the same
-  single-workgroup kernel as the 1-GPU path.  The solve is latency-bound
-  (~4k-6k points, ~35-125 iterations): a distributed CG would need 3 RCCL
-  all-reduces + 2 halo exchanges per iteration (~100 latency-bound
-  collectives per step); the replicated solve needs none, and its sums are
-  exactly the 1-GPU sums, so results are bit-identical at any GPU count
-  (SURVEY.md 8(c) parity item 6).
+* CG2D, by default (cg2d="replicated"), runs on the gathered global problem on
+  every GPU with the same kernel as the 1-GPU path.  The solve is latency-bound
+  (~4k-105k points, ~35-125 iterations): the replicated solve needs no
+  collective inside the iteration, and its sums are exactly the 1-GPU sums, so
+  results are bit-identical at any GPU count (SURVEY.md 8(c) parity item 6);
+* cg2d="distributed" is the reference's own distributed CG2D (cg2d.F:100-415):
+  each process iterates on its own tiles only (mgcm_cg2d_op), the three global
+  sums per iteration are GLOBAL_SUM_TILE_RL -- an all-gather of the per-tile
+  partials, added in global tile order on every process
+  (global_sum_tile.F:161-191, tile_sum below) -- and the two width-1 EXCH_S3D_RL
+  of r and s are point-to-point exchanges of the halo sources.  Its iterates do
+  not depend on the process count either (the per-tile partials are fixed-order
+  device sums); 5 collectives per iteration make it latency-bound on RCCL, which
+  is why the replicated solve is the default.
 
 Transport: backend "nccl" (RCCL over xGMI) moves device tensors directly on
 the model's stream; backend "gloo" stages through host memory (CPU tests,
@@ -118,13 +125,45 @@ def exchange(dist, plan, pack, unpack, make_buf):
         unpack(peer, buf)
 
 
+def tile_sum(partials):
+    """GLOBAL_SUM_TILE_RL's final sum (eesupp/src/global_sum_tile.F:185-190): sumAllP = 0,
+    then + every tile's partial in global tile order (Python floats are IEEE doubles, one
+    rounding per addition, as the reference)."""
+    acc = 0.0
+    for v in partials:
+        acc = acc + float(v)
+    return acc
+
+
+def gather_tile_partials(dist, part, local, t0, nT, world, maxT, nTiles, backend):
+    """All-gather the per-tile partials of every process's tile range [t0, t0+nT):
+    local is (maxT, m) on this process (rows 0..nT-1 valid); returns the (nTiles, m)
+    global-tile-indexed buffer (host numpy), the same on every process."""
+    import torch
+    m = local.shape[1]
+    if backend == "gloo":
+        src = local.cpu() if local.is_cuda else local
+        out = [torch.empty_like(src) for _ in range(world)]
+        dist.all_gather(out, src)
+        allp = torch.cat(out)
+    else:
+        allp = torch.empty((world * maxT, m), dtype=local.dtype, device=local.device)
+        dist.all_gather_into_tensor(allp, local)
+    allp = allp.cpu().numpy().reshape(world, maxT, m)
+    res = np.empty((nTiles, m))
+    for r in range(world):
+        s, c = part.range(r)
+        res[s:s + c] = allp[r, :c]
+    return res
+
+
 class ShardedModel:
     """A Model (model.py) stepped tile-sharded across the processes of the
     default torch.distributed group.  Every process must construct the same
     configuration; after init(), step()/forward_step() keep the tiles a
     process owns bit-identical to a single-process run."""
 
-    def __init__(self, model, dist, device=None):
+    def __init__(self, model, dist, device=None, cg2d="replicated"):
         import torch
         from ._lib import check, lib
         self.torch, self.dist, self.m = torch, dist, model
@@ -158,6 +197,15 @@ class ShardedModel:
         mt = self.part.maxT
         self.g_in = torch.empty(mt * n2, dtype=torch.float64, device=dv)
         self.g_out = torch.empty(self.world * mt * n2, dtype=torch.float64, device=dv)
+        if cg2d not in ("replicated", "distributed"):
+            raise ValueError("cg2d must be 'replicated' or 'distributed'")
+        self.cg2d = cg2d
+        if cg2d == "distributed":
+            self.cg_part = torch.zeros(2 * g.nTiles, dtype=torch.float64, device=dv)   # part[2*tile + s]
+            self.cg_local = torch.zeros((mt, 2), dtype=torch.float64, device=dv)
+            self.sbuf2 = {p: torch.empty(v.size, dtype=torch.float64, device=dv) for p, v in self.plan.send.items()}
+            self.rbuf2 = {p: torch.empty(v.size, dtype=torch.float64, device=dv) for p, v in self.plan.recv.items()}
+            self.cg_iters = []   # iterations of every distributed solve (host record)
 
     # ---- transport -------------------------------------------------------------
     def _gather_2d(self, name):
@@ -209,13 +257,103 @@ class ShardedModel:
 
         exchange(self.dist, self.plan, pack, unpack, make_buf)
 
+    def _exch_2d(self, name):
+        """EXCH of one 2-D field across processes: the sources of my tiles' halo points
+        arrive from their owners (HaloPlan point lists, one value per point), then the
+        local halo fill (EXCH_XY_RL / EXCH_S3D_RL on this process's copy)."""
+        L, h, ck, torch = self.L, self.m.h, self.check, self.torch
+        gloo = self.backend == "gloo"
+        nm = name.encode()
+
+        def pack(peer):
+            buf = self.sbuf2[peer]
+            ck(L.mgcm_field_pack(h, nm, ctypes.c_void_p(self.idx[peer].data_ptr()), self.plan.send[peer].size,
+                                 ctypes.c_void_p(buf.data_ptr()), 0), "mgcm_field_pack")
+            if gloo:
+                torch.cuda.synchronize(self.dev)
+                return buf.cpu()
+            return buf
+
+        def make_buf(peer):
+            return self.rbuf2[peer].cpu() if gloo else self.rbuf2[peer]
+
+        def unpack(peer, buf):
+            dev = self.rbuf2[peer]
+            if buf is not dev:
+                dev.copy_(buf)
+                torch.cuda.synchronize(self.dev)
+            ck(L.mgcm_field_pack(h, nm, ctypes.c_void_p(self.idx[("r", peer)].data_ptr()), self.plan.recv[peer].size,
+                                 ctypes.c_void_p(dev.data_ptr()), 1), "mgcm_field_pack")
+
+        exchange(self.dist, self.plan, pack, unpack, make_buf)
+        ck(L.mgcm_exchange_field(h, nm), "mgcm_exchange_field")
+
+    def _tile_sums(self, op, a0=0.0):
+        """One cg2d.F operation on my tiles, then GLOBAL_SUM_TILE_RL's collection of the
+        per-tile partials: the (nTiles, 2) buffer, identical on every process."""
+        L, h = self.L, self.m.h
+        self.check(L.mgcm_cg2d_op(h, op, float(a0), ctypes.c_void_p(self.cg_part.data_ptr())), "mgcm_cg2d_op(%d)" % op)
+        if self.backend == "gloo":   # the model runs on its own stream: wait for the partials
+            self.torch.cuda.synchronize(self.dev)
+        if self.nT:
+            self.cg_local[:self.nT].copy_(self.cg_part[2 * self.t0:2 * (self.t0 + self.nT)].view(self.nT, 2))
+        if self.backend == "gloo":
+            self.torch.cuda.synchronize(self.dev)
+        return gather_tile_partials(self.dist, self.part, self.cg_local, self.t0, self.nT, self.world,
+                                    self.part.maxT, self.g.nTiles, self.backend)
+
+    def _cg2d_distributed(self):
+        """CG2D (model/src/cg2d.F:100-415) over the processes' tiles: 3 GLOBAL_SUM_TILE_RL
+        and 2 EXCH_S3D_RL per iteration, scalars (beta, alpha, the residual) on the host
+        in the reference's arithmetic."""
+        import math
+        L, h, ck = self.L, self.m.h, self.check
+        prm = lambda n: L.mgcm_get_param(h, n.encode())
+        normalise = prm("cg2dNormaliseRHS") != 0.0
+        tol_sq, maxit = prm("cg2dTolerance_sq"), int(prm("cg2dMaxIters"))
+        P = self._tile_sums(0)                         # cg2d.F:104-114, rhsMax per tile
+        rhsMax = float(np.max(P[:, 0]))                # _GLOBAL_MAX_RL (order-free)
+        rhsNorm = 1.0
+        if normalise:                                  # cg2d.F:116-133
+            if rhsMax != 0.0:
+                rhsNorm = 1.0 / rhsMax
+            ck(L.mgcm_cg2d_op(h, 1, rhsNorm, ctypes.c_void_p(self.cg_part.data_ptr())), "mgcm_cg2d_op(1)")
+        self._exch_2d("cg2d_x")                        # EXCH_XY_RL(cg2d_x), cg2d.F:135
+        P = self._tile_sums(2)                         # r = b - A x, cg2d.F:136-179
+        err_sq, sumRHS = tile_sum(P[:, 0]), tile_sum(P[:, 1])
+        first, its = math.sqrt(err_sq), 0
+        self._exch_2d("cg2d_r")
+        eta_qrNM1 = 1.0
+        if not err_sq < tol_sq:
+            for it in range(1, maxit + 1):
+                eta_qrN = tile_sum(self._tile_sums(3)[:, 0])   # q = M r, (q, r)
+                beta = eta_qrN / eta_qrNM1
+                eta_qrNM1 = eta_qrN
+                ck(L.mgcm_cg2d_op(h, 4, beta, ctypes.c_void_p(self.cg_part.data_ptr())), "mgcm_cg2d_op(4)")
+                self._exch_2d("cg2d_s")
+                alpha = eta_qrN / tile_sum(self._tile_sums(5)[:, 0])   # q = A s, (s, q)
+                err_sq = tile_sum(self._tile_sums(6, alpha)[:, 0])     # x, r update, (r, r)
+                its = it
+                if err_sq < tol_sq:
+                    break
+                self._exch_2d("cg2d_r")
+        if normalise:                                  # un-normalise, cg2d.F:372-385
+            ck(L.mgcm_cg2d_op(h, 7, rhsNorm, ctypes.c_void_p(self.cg_part.data_ptr())), "mgcm_cg2d_op(7)")
+        ck(L.mgcm_cg2d_record(h, first, math.sqrt(err_sq), rhsMax, sumRHS, its), "mgcm_cg2d_record")
+        self.cg_iters.append(its)
+
     # ---- stepping ----------------------------------------------------------------
     def step(self):
         L, h, ck = self.L, self.m.h, self.check
         ck(L.mgcm_step_phase(h, 1), "mgcm_step_phase(1)")
-        self._gather_2d("cg2d_b")
-        self._gather_2d("cg2d_x")
-        ck(L.mgcm_step_phase(h, 2), "mgcm_step_phase(2)")
+        if self.cg2d == "distributed":
+            self._cg2d_distributed()
+            self._exch_2d("cg2d_x")      # the halo sources of the new x before etaN everywhere
+            ck(L.mgcm_step_phase(h, 6), "mgcm_step_phase(6)")
+        else:
+            self._gather_2d("cg2d_b")
+            self._gather_2d("cg2d_x")
+            ck(L.mgcm_step_phase(h, 2), "mgcm_step_phase(2)")
         if self.m.params.get("exactConserv", 0):
             self._gather_2d("cg2d_b")
         ck(L.mgcm_step_phase(h, 3), "mgcm_step_phase(3)")

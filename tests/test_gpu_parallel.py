@@ -32,7 +32,7 @@ def _make(cfg):
     return configs.make_model(configs.global_ocean_cs32x15)
 
 
-def _worker(rank, world, port, cfg, nsteps, q):
+def _worker(rank, world, port, cfg, nsteps, q, cg2d="replicated"):
     import torch
     import torch.distributed as dist
     from mitgcm_amd.parallel import ShardedModel
@@ -41,12 +41,16 @@ def _worker(rank, world, port, cfg, nsteps, q):
     try:
         torch.cuda.set_device(0)
         m = _make(cfg)
-        sm = ShardedModel(m, dist, device=torch.device("cuda", 0))
+        sm = ShardedModel(m, dist, device=torch.device("cuda", 0), cg2d=cg2d)
         sm.forward_step(nsteps)
         m.sync()
         full = {n: sm.gather_field(n) for n in FIELDS}
         stats = [m.solve_stats(back=b) for b in range(nsteps)]
         res = {"t0": sm.t0, "nT": sm.nT, "stats": stats}
+        if cg2d == "distributed":
+            res["iters"] = list(sm.cg_iters)
+            if rank == 0:
+                res["full"] = full
         if rank == 0:
             ref = _make(cfg)
             ref.forward_step(nsteps)
@@ -57,6 +61,10 @@ def _worker(rank, world, port, cfg, nsteps, q):
             ref.close()
         m.close()
         q.put((rank, res))
+    except Exception:
+        import traceback
+        q.put((rank, {"error": traceback.format_exc()}))
+        raise
     finally:
         dist.destroy_process_group()
 
@@ -84,3 +92,48 @@ def test_sharded_bit_identical(cfg, world, nsteps, ntiles):
         assert r["stats"] == r0["ref_stats"], "rank %d: CG2D records differ" % rank
     part = TilePartition(ntiles, world)
     assert sorted((r["t0"], r["nT"]) for r in out.values()) == [part.range(r) for r in range(world)]
+
+
+def _spawn(cfg, world, nsteps, cg2d):
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, cfg, nsteps, q, cg2d)) for r in range(world)]
+    for p in procs:
+        p.start()
+    out = {}
+    for _ in procs:
+        rank, res = q.get(timeout=300)
+        assert "error" not in res, "rank %d: %s" % (rank, res["error"])
+        out[rank] = res
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    return out
+
+
+@pytest.mark.parametrize("cfg,worlds,nsteps", [("gyre", (1, 2, 4), 4), ("cs32x15", (1, 3, 6), 3)])
+def test_distributed_cg2d(cfg, worlds, nsteps):
+    """cg2d="distributed": the reference's CG2D over the processes' tiles, its global sums
+    GLOBAL_SUM_TILE_RL (all-gather of per-tile partials, added in tile order).  Bars: the
+    fields and every solve record identical bit for bit at every process count; against
+    the replicated single-process solve (other summation order) the same iteration counts
+    and fields within 1e-10 of their maximum."""
+    runs = {w: _spawn(cfg, w, nsteps, "distributed") for w in worlds}
+    base = runs[worlds[0]][0]
+    for w in worlds[1:]:
+        r0 = runs[w][0]
+        for n in FIELDS:
+            assert np.array_equal(r0["full"][n], base["full"][n]), (w, n, np.abs(r0["full"][n] - base["full"][n]).max())
+        for rank, r in runs[w].items():
+            assert r["stats"] == base["stats"], (w, rank)
+            assert r["iters"] == base["iters"], (w, rank)
+    its_rep = [s["cg2d_iters"] for s in base["ref_stats"]]
+    its_dist = [s["cg2d_iters"] for s in base["stats"]]
+    print("%s distributed CG2D iterations %s (replicated %s); max |diff| vs replicated %s" % (
+        cfg, its_dist, its_rep, base["diff"]))
+    assert its_dist == its_rep
+    for n in FIELDS:
+        sc = max(np.abs(base["full"][n]).max(), 1e-300)
+        assert base["diff"][n] <= 1e-10 * sc, (n, base["diff"][n], sc)

@@ -201,3 +201,51 @@ def test_sharded_cube_vector_exchange(world):
         assert p.exitcode == 0
     for rank, ok, _ in res:
         assert ok, "rank %d: sharded cube vector exchange differs from EXCH2_UV_3D_RX" % rank
+
+
+def _tilesum_worker(rank, world, port, nTiles, q):
+    """GLOBAL_SUM_TILE_RL over gloo: every process contributes the partials of its own
+    tiles; the gathered buffer and its tile-ordered sum must be the single-process ones."""
+    from mitgcm_amd.parallel import gather_tile_partials, tile_sum
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        rng = np.random.default_rng(11)
+        allp = rng.standard_normal((nTiles, 2)) * 10.0 ** rng.integers(-8, 8, size=(nTiles, 2))
+        part = TilePartition(nTiles, world)
+        t0, nT = part.range(rank)
+        local = torch.zeros((part.maxT, 2), dtype=torch.float64)
+        local[:nT] = torch.as_tensor(allp[t0:t0 + nT])
+        got = gather_tile_partials(dist, part, local, t0, nT, world, part.maxT, nTiles, "gloo")
+        q.put((rank, got, [tile_sum(got[:, k]) for k in range(2)]))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,nTiles", [(2, 6), (3, 6), (3, 13)])
+def test_global_sum_tile_order_independent_of_world(world, nTiles):
+    """The distributed CG2D's sums (parallel.tile_sum over gather_tile_partials) equal the
+    sequential tile-order sum of global_sum_tile.F:185-190 on one process, bit for bit."""
+    from mitgcm_amd.parallel import tile_sum
+    ctx = mp.get_context("spawn")
+    qq = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_tilesum_worker, args=(r, world, port, nTiles, qq)) for r in range(world)]
+    for p in procs:
+        p.start()
+    out = dict((r, (g, s)) for r, g, s in (qq.get(timeout=120) for _ in procs))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    rng = np.random.default_rng(11)
+    allp = rng.standard_normal((nTiles, 2)) * 10.0 ** rng.integers(-8, 8, size=(nTiles, 2))
+    ref = []
+    for k in range(2):
+        acc = 0.0
+        for t in range(nTiles):
+            acc = acc + allp[t, k]
+        ref.append(acc)
+    assert tile_sum(allp[:, 0]) == ref[0]
+    for r, (g, s) in out.items():
+        assert np.array_equal(g, allp), r
+        assert s == ref, (r, s, ref)
