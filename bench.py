@@ -284,6 +284,8 @@ def main():
     out = {
         "metric": "model-days/wallclock-sec",
         "value": value,
+        # replica mode: value sums the N independent integrations; one integration's rate
+        "value_per_integration": model_days / elapsed,
         "unit": "model-days/s",
         "n_gpus": world,
         "steps": a.steps,
