@@ -94,7 +94,7 @@ __global__ void __launch_bounds__(256) k_del2uv(Dims d, Params p, Fields f) {
 }
 
 // CALC_PHI_HYD (calc_phi_hyd.F:175-327, OCEANIC, integr_GeoPot = 2, uniformFreeSurfLev,
-// gravFac = 1) per column, as the other column kernels (MG_COLS): alphaRho = rhoInSitu
+// gravFac = 1) per column, as the other column kernels (MG_COLF): alphaRho = rhoInSitu
 // plus MOM_QUASIHYDROSTATIC's 3-D Coriolis / NH-metric buoyancy (mom_quasihydrostatic.F:
 // 76-147, angleCosC = 1, angleSinC = 0) and the two half-level increments are formed
 // k-parallel into LDS, one thread per column runs the reference's sequential sum, and
@@ -104,16 +104,18 @@ __global__ void __launch_bounds__(256) k_del2uv(Dims d, Params p, Fields f) {
 // their value at every level for k_mom_step.  Columns cover -1..sNx+1 x -1..sNy+1 (the
 // dynamics range 0..sNx+1 plus the west/south neighbours dWtransC is needed at); phi and
 // totPhiHyd are stored on 0..sNx+1 only.
-__global__ void __launch_bounds__(256) k_phi_hyd(Dims d, Params p, Fields f) {
-  __shared__ double sM[256], sP[256], sPh[256], sC[256], sU[256], sV[256];
-  MG_COLS(-1, d.sNx + 3, -1, d.sNy + 3, d.Nr)
-  const int Nr = d.Nr, k = kk + 1, me = kk * NC_ + cc;
+__global__ void __launch_bounds__(256) k_phi_hyd(Dims d, Params p, Fields f, int nc) {
+  extern __shared__ __attribute__((aligned(16))) double lds[];
+  MG_COLF(-1, d.sNx + 3, -1, d.sNy + 3, nc)
+  const int Nr = d.Nr, NS = Nr * NC_;
+  double *sM = lds, *sP = lds + NS, *sPh = lds + 2 * NS, *sC = lds + 3 * NS, *sU = lds + 4 * NS, *sV = lds + 5 * NS;
   const bool qh = p.quasiHydrostatic && (p.select3dCoriScheme >= 1 || p.useNHMTerms);
   const bool rstar = p.nonlinFreeSurf > 0 && p.select_rStar > 0;
   const bool ring = i >= 0 && j >= 0;
   const double recip_rhoConst = 1.0 / p.rhoConst;
   const long q2 = MG_I2(d, i, j, t);
-  if (valid && k <= Nr) {
+  if (valid) MG_COLF_K(k) {
+    const int me = (k - 1) * NC_ + cc;
     double dRlocM = 0.5 * f.drC[k - 1];
     if (k == 1) dRlocM = f.rF[0] - f.rC[0];
     const double dRlocP = (k == Nr) ? (f.rC[k - 1] - f.rF[k]) : 0.5 * f.drC[k];
@@ -169,7 +171,8 @@ __global__ void __launch_bounds__(256) k_phi_hyd(Dims d, Params p, Fields f) {
     }
   }
   __syncthreads();
-  if (valid && k <= Nr) {
+  if (valid) MG_COLF_K(k) {
+    const int me = (k - 1) * NC_ + cc;
     const long q3 = MG_I3(d, i, j, k, t);
     if (rstar) {
       f.dWtC[q3] = sC[me];
@@ -1633,7 +1636,12 @@ __global__ void __launch_bounds__(256) k_mom_impl(Dims d, Params p, Fields f, in
 }
 
 hipError_t launch_mom_step(const Dims &d, const Params &p, const Fields &f, const int *iterPtr, hipStream_t s) {
-  hipLaunchKernelGGL(k_phi_hyd, dim3(mg_col_blocks(d.sNx + 3, d.sNy + 3, d.nT, d.Nr)), dim3(256), 0, s, d, p, f);
+  {
+    const long ncol = (long)(d.sNx + 3) * (d.sNy + 3) * d.nT;
+    const int nc = mg_colf_nc(ncol, d.Nr, 6);
+    MG_ALLOW_LDS(k_phi_hyd);
+    hipLaunchKernelGGL(k_phi_hyd, dim3(mg_colf_blocks(ncol, nc)), dim3(256), mg_colf_lds(d.Nr, nc, 6), s, d, p, f, nc);
+  }
   if (p.momViscosity && (p.viscA4D != 0.0 || p.viscA4Z != 0.0))
     hipLaunchKernelGGL(k_del2uv, dim3(mg_plane_blocks(d.nx, d.ny, d.nT * d.Nr)), dim3(MG_PLANE_THREADS), 0, s, d, p, f);
   // MOM_VECINV or MOM_FLUXFORM: separate instantiations (no register-pressure coupling)
