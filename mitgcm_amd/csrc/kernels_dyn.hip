@@ -1261,9 +1261,6 @@ struct VIMarchRegs {   // the output point's own 2-D values (i,j); n = (i,j+1), 
   double dxV, dxVn, recip_dyU, recip_dyUn, dyU, dyUe, recip_dxV, recip_dxVe;
   double fCoriG, fCoriGn, fCoriGe, rA, rAw_w, rA_s;
 };
-#ifndef MGCM_VM_PREFETCH
-#define MGCM_VM_PREFETCH 1
-#endif
 constexpr int VM_S2 = 6;   // LDS-staged 2-D fields: dxC, dyC, recip_rAz, dxG, dyG, recip_rA
 struct VIMarch {
   const Dims &d; const Params &p; const Fields &f; int k, t, i0, j0, EW, IW, i, j;
@@ -1327,6 +1324,9 @@ struct VIMarch {
   __device__ __forceinline__ double hDiv(int ii, int jj) const { return sHDiv[id(ii, jj)]; }
 };
 
+// PF: fetch level k+1 into registers during level k (else after it); CREG: the output
+// point's metrics held in registers across the march (else re-read every level)
+template <bool PF, bool CREG>
 __global__ void __launch_bounds__(VT_NT) k_mom_vi_march(Dims d, Params p, Fields f, const int *iterPtr, int BX, int BY,
                                                          int nbx, int nby, int KC, int nkc) {
   __shared__ double sU[VT_EMAX], sV[VT_EMAX], sHW[VT_EMAX], sHS[VT_EMAX], sHC[2 * VT_EMAX], sW[2 * VT_EMAX];
@@ -1366,8 +1366,7 @@ __global__ void __launch_bounds__(VT_NT) k_mom_vi_march(Dims d, Params p, Fields
         if (ee < EN) s2[n * VT_EMAX + ee] = ein[r] ? v : 0.0;
       }
   }
-  VIMarchRegs c;
-  {
+  auto load_c = [&](VIMarchRegs &c, const long q2) {
     const long qn = q2 + d.nx, qe = q2 + 1, qw = q2 - 1, qs = q2 - d.nx;
     c.recip_dxC = AR2(recip_dxC, q2); c.recip_dyC = AR2(recip_dyC, q2);
     c.recip_dxG = AR2(recip_dxG, q2); c.recip_dyG = AR2(recip_dyG, q2);
@@ -1376,7 +1375,9 @@ __global__ void __launch_bounds__(VT_NT) k_mom_vi_march(Dims d, Params p, Fields
     c.dyU = AR2(dyU, q2); c.dyUe = AR2(dyU, qe); c.recip_dxV = AR2(recip_dxV, q2); c.recip_dxVe = AR2(recip_dxV, qe);
     c.fCoriG = AR2(fCoriG, q2); c.fCoriGn = AR2(fCoriG, qn); c.fCoriGe = AR2(fCoriG, qe);
     c.rA = AR2(rA, q2); c.rAw_w = AR2(rA, qw); c.rA_s = AR2(rA, qs);
-  }
+  };
+  VIMarchRegs c0;   // CREG: loaded once, live in registers across the march
+  if constexpr (CREG) load_c(c0, q2);
   // level fetches into registers (unconditional loads, masked where the element is absent),
   // addressed as uniform field base + 32-bit byte offset (the global_load saddr form)
   const long t3 = (long)t * (d.n3 - d.n2);   // MG_I3 = MG_I2 + (k-1)*n2 + t*(n3-n2)
@@ -1446,16 +1447,24 @@ __global__ void __launch_bounds__(VT_NT) k_mom_vi_march(Dims d, Params p, Fields
   const bool rstar = p.nonlinFreeSurf > 0 && p.select_rStar > 0;
   __syncthreads();
   for (int k = kb; k <= ke; k++) {
+    // the thread's coordinates re-materialised each level (an empty asm the compiler cannot
+    // see through): the addresses derived from them are recomputed per level instead of
+    // hoisted out of the march and held in registers across it
+    int iL = i, jL = j;
+    long q2L = q2;
+    asm volatile("" : "+v"(iL), "+v"(jL), "+v"(q2L));
+    [&](const int i, const int j, const long q2) {
+    VIMarchRegs c1;   // !CREG: re-read every level (cache hits) instead of held across the march
+    if constexpr (!CREG) load_c(c1, q2);
+    const VIMarchRegs &c = CREG ? c0 : c1;
     const int kn = k + 1 <= Nr ? k + 1 : Nr, kw = k + 2 <= Nr ? k + 2 : Nr;
-#if MGCM_VM_PREFETCH
-    fetch(kn);    // level k+1 and the own column at k+1, in flight during level k
-    fetchW(kw);
-#else
-    {   // own column at k+1 only; the level itself is fetched after the output
+    if constexpr (PF) {
+      fetch(kn);    // level k+1 and the own column at k+1, in flight during level k
+      fetchW(kw);
+    } else {   // own column at k+1 only; the level itself is fetched after the output
       const unsigned o = ob + (unsigned)(kn - 1) * lvB;
       oU = ld(bU, o); oV = ld(bV, o); oHW = ld(bHW, o); oHS = ld(bHS, o);
     }
-#endif
     // the output point's accessor, and one for the ring-point intermediates whose own point
     // matches nothing (they read level k only; an idle thread's registers hold (1,1)'s values)
     VIMarch a{d, p, f, k, t, i0, j0, EW, IW, i, j, sU, sV, sHW, sHS, sHC, sW, s2, sKE, sVort, sHfz, sH0fz, sHDiv, c,
@@ -1524,13 +1533,14 @@ __global__ void __launch_bounds__(VT_NT) k_mom_vi_march(Dims d, Params p, Fields
       AR3(gU, q3) = a.uVel(i, j, k) + p.deltaTMom * (gUtmp + 0.0) * a.maskW(i, j, k);
       AR3(gV, q3) = a.vVel(i, j, k) + p.deltaTMom * (gVtmp + 0.0) * a.maskS(i, j, k);
     }
+    }(iL, jL, q2L);
     if (k == ke) break;
     // the own column moves down: level k becomes k-1 (read before level k+1 overwrites it)
-    if (act) { const int eo = a.e(i, j); uM = sU[eo]; vM = sV[eo]; hwM = sHW[eo]; hsM = sHS[eo]; }
-#if !MGCM_VM_PREFETCH
-    fetch(kn);
-    fetchW(kw);
-#endif
+    if (act) { const int eo = (j - j0 + 1) * EW + (i - i0 + 1); uM = sU[eo]; vM = sV[eo]; hwM = sHW[eo]; hsM = sHS[eo]; }
+    if constexpr (!PF) {
+      fetch(k + 1 <= Nr ? k + 1 : Nr);
+      fetchW(k + 2 <= Nr ? k + 2 : Nr);
+    }
     __syncthreads();
     stash(k + 1);
     stashW(k + 2);
@@ -1635,13 +1645,17 @@ __global__ void __launch_bounds__(256) k_mom_impl(Dims d, Params p, Fields f, in
   if (valid) MG_COLF_K(k) g[MG_I3(d, i, j, k, t)] = sSub[(k - 1) * NC_ + cc];
 }
 
+hipError_t launch_phi_hyd(const Dims &d, const Params &p, const Fields &f, hipStream_t s) {
+  const long ncol = (long)(d.sNx + 3) * (d.sNy + 3) * d.nT;
+  const int nc = mg_colf_nc(ncol, d.Nr, 6);
+  MG_ALLOW_LDS(k_phi_hyd);
+  hipLaunchKernelGGL(k_phi_hyd, dim3(mg_colf_blocks(ncol, nc)), dim3(256), mg_colf_lds(d.Nr, nc, 6), s, d, p, f, nc);
+  return hipGetLastError();
+}
+
+// DYNAMICS after CALC_PHI_HYD (launch_phi_hyd): momentum tendencies, TIMESTEP, AB2, CD scheme,
+// implicit vertical viscosity
 hipError_t launch_mom_step(const Dims &d, const Params &p, const Fields &f, const int *iterPtr, hipStream_t s) {
-  {
-    const long ncol = (long)(d.sNx + 3) * (d.sNy + 3) * d.nT;
-    const int nc = mg_colf_nc(ncol, d.Nr, 6);
-    MG_ALLOW_LDS(k_phi_hyd);
-    hipLaunchKernelGGL(k_phi_hyd, dim3(mg_colf_blocks(ncol, nc)), dim3(256), mg_colf_lds(d.Nr, nc, 6), s, d, p, f, nc);
-  }
   if (p.momViscosity && (p.viscA4D != 0.0 || p.viscA4Z != 0.0))
     hipLaunchKernelGGL(k_del2uv, dim3(mg_plane_blocks(d.nx, d.ny, d.nT * d.Nr)), dim3(MG_PLANE_THREADS), 0, s, d, p, f);
   // MOM_VECINV or MOM_FLUXFORM: separate instantiations (no register-pressure coupling)
@@ -1654,18 +1668,22 @@ hipError_t launch_mom_step(const Dims &d, const Params &p, const Fields &f, cons
     // that the two extra staged levels per chunk stay a small overhead
     static const int kcEnv = getenv("MGCM_VI_KC") ? atoi(getenv("MGCM_VI_KC")) : 0;
     static const char *viEnv = getenv("MGCM_VI_KERNEL");   // march | level | tiled (sweeps)
-    // the k-march (MGCM_VI_KERNEL=march; chunk MGCM_VI_KC, default: >= 3072 workgroups):
-    // measured on LLC-90 at the same time as the per-level kernel (25 % fewer VALU
-    // instructions, 29 % fewer HBM bytes, but 227-251 VGPRs: 2 waves/SIMD against 4), so the
-    // per-level kernel stays the default
+    // the k-march for deep grids (Nr >= 30 with >= 256 workgroups per level chunk): two
+    // chunks of Nr/2 levels.  Measured on LLC-90: alone it is ~10 % slower than
+    // the per-level kernel, but its ~900 workgroups at 3 waves/SIMD leave room for the
+    // concurrent THERMODYNAMICS stream and the graph-replayed step is 3-4 % faster (2.31-2.34
+    // vs 2.40 ms).  MGCM_VI_KERNEL=level|march|tiled and MGCM_VI_KC override (sweeps).
     const int nbt = nbx * nby * d.nT;
-    int KCm = (d.Nr + (3072 / nbt > 0 ? 3072 / nbt : 1) - 1) / (3072 / nbt > 0 ? 3072 / nbt : 1);
+    int KCm = (d.Nr + 1) / 2;
     if (kcEnv > 0) KCm = kcEnv > d.Nr ? d.Nr : kcEnv;
-    const bool march = viEnv && !strcmp(viEnv, "march");
+    const bool march = viEnv ? !strcmp(viEnv, "march") : (d.Nr >= 30 && nbt >= 256);
     if (march) {
       const int nkc = (d.Nr + KCm - 1) / KCm;
-      hipLaunchKernelGGL(k_mom_vi_march, dim3((unsigned)(nbt * nkc)), dim3(VT_NT), 0, s, d, p, f, iterPtr, BX, BY, nbx,
-                         nby, KCm, nkc);
+      static const int var = getenv("MGCM_VI_MARCH_VAR") ? atoi(getenv("MGCM_VI_MARCH_VAR")) : 0;
+      auto kern = var == 1 ? k_mom_vi_march<true, true> : var == 2 ? k_mom_vi_march<true, false>
+                : var == 3 ? k_mom_vi_march<false, true> : k_mom_vi_march<false, false>;
+      hipLaunchKernelGGL(kern, dim3((unsigned)(nbt * nkc)), dim3(VT_NT), 0, s, d, p, f, iterPtr, BX, BY, nbx, nby, KCm,
+                         nkc);
     } else if (kcEnv <= 0 || (viEnv && !strcmp(viEnv, "level"))) {   // one level per workgroup
       hipLaunchKernelGGL(k_mom_vi_level, dim3((unsigned)(nbx * nby * d.nT * d.Nr)), dim3(VT_NT), 0, s, d, p, f, iterPtr, BX,
                          BY, nbx, nby);

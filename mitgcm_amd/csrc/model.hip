@@ -22,6 +22,7 @@
 
 namespace mgcm {
 hipError_t launch_mom_step(const Dims &, const Params &, const Fields &, const int *, hipStream_t);
+hipError_t launch_phi_hyd(const Dims &, const Params &, const Fields &, hipStream_t);
 hipError_t launch_sfp_rhs(const Dims &, const Params &, const Fields &, hipStream_t);
 hipError_t launch_cg2d_block(const Dims &, const Params &, const Fields &, const unsigned *, const int *, int, int, int,
                              SolveRecord *, int *, hipStream_t);
@@ -126,9 +127,9 @@ static const PDesc PARAMS[] = {
 #undef PI_
 
 // kernel families timed with hipEvents when timing is enabled
-enum Kern { K_MOM, K_RHS, K_CG2D, K_EXCH, K_ETA, K_CORR, K_CONT, K_PHYS, K_TEMP, K_RSTAR, K_N };
+enum Kern { K_MOM, K_RHS, K_CG2D, K_EXCH, K_ETA, K_CORR, K_CONT, K_PHYS, K_TEMP, K_RSTAR, K_PHI, K_N };
 static const char *KNAMES[K_N] = {"mom_step",   "sfp_rhs",    "cg2d",         "exchange",  "eta_update",
-                                  "correction", "continuity", "oceanic_phys", "temp_step", "r_star"};
+                                  "correction", "continuity", "oceanic_phys", "temp_step", "r_star", "phi_hyd"};
 
 struct mgcm_model {
   Dims d{};
@@ -1083,6 +1084,7 @@ static int check_ready(mgcm_model *m) {
 
 int mgcm_dynamics(mgcm_model *m) {
   if (check_ready(m)) return -1;
+  TIMED(K_PHI, launch_phi_hyd(m->d, m->p, m->f, m->stream));   // CALC_PHI_HYD (dynamics.F:462)
   TIMED(K_MOM, launch_mom_step(m->d, m->p, m->f, m->d_ctr, m->stream));
   return 0;
 }
