@@ -696,6 +696,90 @@ __global__ void __launch_bounds__(256) k_tracer_rhs(Dims d, Params p, Fields f, 
 #undef G3
 }
 
+// k_tracer_rhs without GM/Redi, every load issued up front: the same expression trees as
+// k_tracer_rhs<false> (bit-identical), but the 35 operands of a point are fetched before any
+// arithmetic, unconditionally (vertical neighbours at clamped levels, whose terms the
+// reference's kk >= 2 / kk <= Nr conditions then drop; 2-D/3-D fields the options do not
+// use read and discarded), so a wave waits on memory once instead of once per branch.
+__global__ void __launch_bounds__(256) k_tracer_rhs_flat(Dims d, Params p, Fields f, TracerArgs a, const int *iterPtr) {
+  MG_PLANE(1, d.sNx, 1, d.sNy, z)
+  const int t = d.t0 + z / d.Nr, k = z % d.Nr + 1;
+  if (i > d.sNx || j > d.sNy) return;
+  const int Nr = d.Nr;
+  const long nx = d.nx, q = MG_I2(d, i, j, t), q3 = MG_I3(d, i, j, k, t);
+  const long dku = (k > 1 ? -1L : 0L) * d.n2, dkd = (k < Nr ? 1L : 0L) * d.n2;
+  const double *__restrict__ T = a.tr;
+  // ---- loads
+  const double T0 = T[q3], Tw = T[q3 - 1], Te = T[q3 + 1], Ts = T[q3 - nx], Tn = T[q3 + nx];
+  const double Tu = T[q3 + dku], Td = T[q3 + dkd];
+  const double u0 = f.uVel[q3], u1 = f.uVel[q3 + 1], v0 = f.vVel[q3], v1 = f.vVel[q3 + nx];
+  const double w0 = f.wVel[q3], w1 = f.wVel[q3 + dkd];
+  const double hW0 = f.hFacW[q3], hW1 = f.hFacW[q3 + 1], hS0 = f.hFacS[q3], hS1 = f.hFacS[q3 + nx];
+  const double mCu = f.maskC[q3 + dku], mC0 = f.maskC[q3], mCd = f.maskC[q3 + dkd];
+  const double ivd0 = f.IVDConvCount[q3], ivd1 = f.IVDConvCount[q3 + dkd];
+  const double dyG0 = f.dyG[q], dyG1 = f.dyG[q + 1], dxG0 = f.dxG[q], dxG1 = f.dxG[q + nx];
+  const double rdxC0 = f.recip_dxC[q], rdxC1 = f.recip_dxC[q + 1], rdyC0 = f.recip_dyC[q], rdyC1 = f.recip_dyC[q + nx];
+  const double maskInC = f.maskInC[q], recip_rA = f.recip_rA[q], rA = f.rA[q];
+  const double rhC = f.recip_hFacC[q3], gAdv = f.gAdv[q3], gOld = a.gNm1[q3];
+  const double sfc = a.sfc ? a.sfc[q] : 0.0, rsx = f.rStarExpC[q];
+  const int myIter = *iterPtr;
+  // ---- arithmetic (k_tracer_rhs<false>'s, term for term)
+  const double abFac = (myIter == p.nIter0 && p.nIter0 == 0) ? 0.0 : 0.5 + p.abEps;
+  const bool calcAdv = a.advection && !a.multiDim;
+  const double advFac = calcAdv ? 1.0 : 0.0, rAdvFac = p.rkSign * advFac;
+  const double drF = f.drF[k - 1];
+  auto face = [&](double vel, double g, double h, double rd, double tp, double tm) {   // fzon / fmer
+    const double A = g * drF * h;
+    double fz = 0.0;
+    if (calcAdv) fz = fz + (vel * A) * (tp + tm) * 0.5;
+    double df = 0.0;
+    if (a.diffKh != 0.0) df = -a.diffKh * A * rd * (tp - tm);
+    return fz + df;
+  };
+  const double rTrans = k <= 1 ? 0.0 : w0 * rA * (mCu * mC0);
+  const double rTransKp = k + 1 > Nr ? 0.0 : w1 * rA * (mC0 * mCd);
+  auto fvert = [&](int kk, double rTr, double mUpper, double mLower, double tLower, double tUpper, double ivd) {
+    double fv = 0.0;
+    if (kk >= 2 && kk <= Nr && calcAdv) {
+      const double wT = mUpper * rTr * (tLower + tUpper) * 0.5;
+      fv = fv + wT * maskInC;
+    }
+    double dfr = 0.0;
+    if (!p.implicitDiffusion && kk >= 2 && kk <= Nr) {
+      const double kap = (ivd * p.ivdc_kappa + 0.0) + a.diffKr;
+      const double maskUp = mUpper * mLower;
+      dfr = -kap * maskUp * rA * f.recip_drC[kk - 1] * (tLower - tUpper) * p.rkSign;
+    }
+    return fv + dfr;
+  };
+  const double uT0 = u0 * (dyG0 * drF * hW0), uT1 = u1 * (dyG1 * drF * hW1);
+  const double vT0 = v0 * (dxG0 * drF * hS0), vT1 = v1 * (dxG1 * drF * hS1);
+  const double fVerUp = fvert(k, rTrans, mCu, mC0, T0, Tu, ivd0);
+  const double fVerDn = fvert(k + 1, rTransKp, mC0, mCd, Td, T0, ivd1);
+  const double fZi = face(u0, dyG0, hW0, rdxC0, T0, Tw), fZe = face(u1, dyG1, hW1, rdxC1, Te, T0);
+  const double fMi = face(v0, dxG0, hS0, rdyC0, T0, Ts), fMn = face(v1, dxG1, hS1, rdyC1, Tn, T0);
+  const double g0 = a.multiDim ? gAdv : 0.0;
+  double gT = g0 - rhC * f.recip_drF[k - 1] * recip_rA *
+                       ((fZe - fZi) * maskInC + (fMn - fMi) * maskInC + (fVerDn - fVerUp) * p.rkSign -
+                        T0 * ((uT1 - uT0) * advFac + (vT1 - vT0) * advFac + (rTransKp - rTrans) * rAdvFac) * maskInC);
+  double gtForc = 0.0;
+  if (a.forcing && a.sfc && k == 1) gtForc = gtForc + sfc * f.recip_drF[0] * rhC;
+  if (!p.tracForcingOutAB) gT = gT + gtForc;
+  const bool rs = p.nonlinFreeSurf > 0 && p.select_rStar > 0;
+  if (a.useAB) {
+    const double ab = abFac * (gT - gOld);
+    double gN = gT;
+    gT = gT + ab;
+    if (rs) gN = gN / rsx;
+    a.gNm1[q3] = gN;
+  }
+  if (p.tracForcingOutAB) gT = gT + gtForc;
+  if (rs) gT = gT / rsx;
+  const double v = T0 + p.deltaTtracer * gT;
+  if (p.implicitDiffusion) f.gTscr[q3] = v;
+  else a.trNext[q3] = v;
+}
+
 // GAD_IMPLICIT_R (implicitDiffusion) + SOLVE_TRIDIAGONAL (Thomas) + CYCLE_TRACER,
 // one thread per interior column; writes the new tracer into its other buffer.
 // GAD_IMPLICIT_R + SOLVE_TRIDIAGONAL per column (gad_implicit_r.F:96-140, the
@@ -808,8 +892,10 @@ hipError_t launch_tracer_step(const Dims &d, const Params &p, const Fields &f, c
     }
   }
   // GM/Redi fluxes as a template switch: without them the kernel holds half the registers
+  static const bool flatOff = getenv("MGCM_TRACER_FLAT") && atoi(getenv("MGCM_TRACER_FLAT")) == 0;
   if (p.useGMRedi) hipLaunchKernelGGL(k_tracer_rhs<true>, grd, blk, 0, s, d, p, f, a, iterPtr);
-  else hipLaunchKernelGGL(k_tracer_rhs<false>, grd, blk, 0, s, d, p, f, a, iterPtr);
+  else if (flatOff) hipLaunchKernelGGL(k_tracer_rhs<false>, grd, blk, 0, s, d, p, f, a, iterPtr);
+  else hipLaunchKernelGGL(k_tracer_rhs_flat, grd, blk, 0, s, d, p, f, a, iterPtr);
   if (p.implicitDiffusion) {
     const long ncol = (long)d.sNx * d.sNy * d.nT;
     const int nc = mg_colf_nc(ncol, d.Nr, 3);
