@@ -165,6 +165,18 @@ __device__ __forceinline__ int mg_xcd_block() {
     i = (i0) + q_ % (ni);                                                               \
     j = (j0) + q_ / (ni);                                                               \
   }
+// MG_PLANE with an explicit logical block id (kernels that split their grid between bodies)
+#define MG_PLANE_LB(i0, ni, j0, nj, zvar, LB)                                           \
+  int i, j, zvar;                                                                       \
+  {                                                                                     \
+    const int np_ = (ni) * (nj), nb_ = (np_ + (int)blockDim.x - 1) / (int)blockDim.x; \
+    const int lb_ = (LB);                                                               \
+    const int q_ = (lb_ % nb_) * (int)blockDim.x + (int)threadIdx.x;                    \
+    zvar = lb_ / nb_;                                                                   \
+    if (q_ >= np_) return;                                                              \
+    i = (i0) + q_ % (ni);                                                               \
+    j = (j0) + q_ / (ni);                                                               \
+  }
 #define MG_PLANE_THREADS 256
 
 // Column blocks for the vertical recurrences (implicit solves, column sums, scans):

@@ -563,9 +563,13 @@ __device__ __forceinline__ void vecinv_tend(const A &a, const Dims &d, const Par
 #undef G3
 }
 
-template <bool VI>
-__global__ void __launch_bounds__(256) k_mom_step(Dims d, Params p, Fields f, const int *iterPtr) {
-  MG_PLANE(1 - d.OLx, d.nx, 1 - d.OLy, d.ny, z)
+// One point of DYNAMICS' momentum block.  COMP = 0 stores both components; 1 only the U
+// outputs (gU, guNm1, cdU), 2 only the V outputs: the other component's arithmetic is then
+// dead and compiled out, so k_mom_step_uv runs the two halves as separate, shorter threads.
+template <bool VI, int COMP>
+__device__ __forceinline__ void mom_step_point(const Dims &d, const Params &p, const Fields &f, const int *iterPtr,
+                                               int lblock) {
+  MG_PLANE_LB(1 - d.OLx, d.nx, 1 - d.OLy, d.ny, z, lblock)
   const int t = d.t0 + z / d.Nr, k = z % d.Nr + 1;
   if (i > d.sNx + d.OLx || j > d.sNy + d.OLy) return;
   const int Nr = d.Nr;
@@ -844,12 +848,12 @@ __global__ void __launch_bounds__(256) k_mom_step(Dims d, Params p, Fields f, co
     // ADAMS_BASHFORTH2 over the whole halo-inclusive slab (adams_bashforth2.F:81-88)
     const long q3 = MG_I3(d, i, j, k, t);
     {
-      const double gUo = AR3(guNm1, q3), gVo = AR3(gvNm1, q3);
+      const double gUo = COMP != 2 ? AR3(guNm1, q3) : 0.0, gVo = COMP != 1 ? AR3(gvNm1, q3) : 0.0;
       double a = abFac * (gU - gUo);
-      AR3(guNm1, q3) = gU;
+      if (COMP != 2) AR3(guNm1, q3) = gU;
       gU = gU + a;
       a = abFac * (gV - gVo);
-      AR3(gvNm1, q3) = gV;
+      if (COMP != 1) AR3(gvNm1, q3) = gV;
       gV = gV + a;
     }
     double gUtmp = 0.0, gVtmp = 0.0;   // timestep.F local arrays: 0 outside iMin..iMax, jMin..jMax
@@ -867,15 +871,31 @@ __global__ void __launch_bounds__(256) k_mom_step(Dims d, Params p, Fields f, co
         gV = V(i, j, k) + p.deltaTMom * (gVtmp + 0.0) * G3(maskS, i, j, k);
       }
     }
-    if (p.useCDscheme) { AR3(cdU, q3) = gUtmp; AR3(cdV, q3) = gVtmp; }   // k_cd_scheme finishes u*
-    AR3(gU, q3) = gU;
-    AR3(gV, q3) = gV;
+    if (p.useCDscheme) {   // k_cd_scheme finishes u*
+      if (COMP != 2) AR3(cdU, q3) = gUtmp;
+      if (COMP != 1) AR3(cdV, q3) = gVtmp;
+    }
+    if (COMP != 2) AR3(gU, q3) = gU;
+    if (COMP != 1) AR3(gV, q3) = gV;
   }
 #undef U
 #undef V
 #undef W
 #undef G2
 #undef G3
+}
+
+template <bool VI>
+__global__ void __launch_bounds__(256) k_mom_step(Dims d, Params p, Fields f, const int *iterPtr) {
+  mom_step_point<VI, 0>(d, p, f, iterPtr, mg_xcd_block());
+}
+// the U and V halves as separate threads: even logical blocks U, odd V of the same plane
+// range (neighbouring blocks, so both halves of a region share an XCD's L2)
+template <bool VI>
+__global__ void __launch_bounds__(256) k_mom_step_uv(Dims d, Params p, Fields f, const int *iterPtr) {
+  const int lb = mg_xcd_block();
+  if (lb & 1) mom_step_point<VI, 2>(d, p, f, iterPtr, lb >> 1);
+  else mom_step_point<VI, 1>(d, p, f, iterPtr, lb >> 1);
 }
 
 // CD_CODE_SCHEME (pkg/cd_code/cd_code_scheme.F:85-236, called from timestep.F:228-270;
@@ -1697,9 +1717,12 @@ hipError_t launch_mom_step(const Dims &d, const Params &p, const Fields &f, cons
   } else if (p.vectorInvariantMomentum)
     hipLaunchKernelGGL(k_mom_step<true>, dim3(mg_plane_blocks(d.nx, d.ny, d.nT * d.Nr)), dim3(MG_PLANE_THREADS), 0, s,
                        d, p, f, iterPtr);
-  else
+  else if (getenv("MGCM_MOM_NOSPLIT"))
     hipLaunchKernelGGL(k_mom_step<false>, dim3(mg_plane_blocks(d.nx, d.ny, d.nT * d.Nr)), dim3(MG_PLANE_THREADS), 0, s,
                        d, p, f, iterPtr);
+  else   // MOM_FLUXFORM: U and V halves as separate threads (twice the workgroups, half the chain)
+    hipLaunchKernelGGL(k_mom_step_uv<false>, dim3(2 * mg_plane_blocks(d.nx, d.ny, d.nT * d.Nr)), dim3(MG_PLANE_THREADS), 0,
+                       s, d, p, f, iterPtr);
   if (p.useCDscheme)
     hipLaunchKernelGGL(k_cd_scheme, dim3(mg_plane_blocks(d.nx - 2, d.ny - 2, d.nT * d.Nr)), dim3(MG_PLANE_THREADS), 0, s,
                        d, p, f, iterPtr);

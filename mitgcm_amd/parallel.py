@@ -178,9 +178,12 @@ class ShardedModel:
         h = model.h
         check(self.L.mgcm_set_tile_range(h, self.t0, self.nT), "mgcm_set_tile_range")
         if self.backend == "nccl":
-            # RCCL orders its work after the current stream: run the model on it
-            check(self.L.mgcm_set_stream(h, ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)),
-                  "mgcm_set_stream")
+            # RCCL orders its work after the current stream: run the model and every torch op of
+            # this process on one dedicated stream (the legacy default stream's handle is NULL,
+            # which mgcm_set_stream reads as "the model's own stream")
+            self.stream = torch.cuda.Stream(self.dev)
+            torch.cuda.set_stream(self.stream)
+            check(self.L.mgcm_set_stream(h, ctypes.c_void_p(self.stream.cuda_stream)), "mgcm_set_stream")
         n2 = g.nx * g.ny
         self.n2 = n2
         uv = g.topo.uv_codes(True) if hasattr(g.topo, "uv_codes") else None
@@ -363,6 +366,36 @@ class ShardedModel:
             ck(L.mgcm_step_phase(h, 5), "mgcm_step_phase(5)")
             self._halo()
         ck(L.mgcm_step_phase(h, 4), "mgcm_step_phase(4)")
+
+    def capture_step(self):
+        """Capture two steps (replicated CG2D; RCCL all-gathers and point-to-point exchanges
+        included) into a HIP graph via torch.cuda.graph, for replay(): the model runs on a
+        side stream that is also the capture stream.  Two, because CYCLE_TRACER swaps the
+        theta/salt buffers on the host: after two steps the kernels' pointers are back where
+        they started.  Runs one warm-up step eagerly first (so the communicators exist before
+        capture): the model advances by that step."""
+        if self.backend != "nccl" or self.cg2d != "replicated":
+            raise ValueError("graph capture needs the nccl (RCCL) backend and the replicated CG2D "
+                             "(the distributed solve decides on the host each iteration)")
+        torch, L, h = self.torch, self.L, self.m.h
+        s = torch.cuda.Stream(self.dev)
+        self.check(L.mgcm_set_stream(h, ctypes.c_void_p(s.cuda_stream)), "mgcm_set_stream")
+        with torch.cuda.stream(s):
+            self.check(L.mgcm_begin_steps(h), "mgcm_begin_steps")
+            self.step()
+        torch.cuda.synchronize(self.dev)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g, stream=s):
+            self.step()
+            self.step()
+        self._graph, self._gstream = g, s
+
+    def replay(self, npairs=1):
+        """Replay the captured pair of steps npairs times (the device's per-step record ring
+        restarts at the first replay)."""
+        self.check(self.L.mgcm_begin_steps(self.m.h), "mgcm_begin_steps")
+        for _ in range(npairs):
+            self._graph.replay()
 
     def forward_step(self, nsteps=1):
         self.check(self.L.mgcm_begin_steps(self.m.h), "mgcm_begin_steps")
