@@ -1487,6 +1487,7 @@ int mgcm_step_phase(mgcm_model *m, int phase) {
 int mgcm_cg2d_op(mgcm_model *m, int op, double a0, double *part) {
   if (check_ready(m)) return -1;
   if (op < 0 || op > 7) return set_err("mgcm_cg2d_op: no op %d", op);
+  if (!part && op != 1 && op != 4 && op != 7) return set_err("mgcm_cg2d_op: op %d needs the partials buffer", op);
   if (m->p.cg2dUseMinResSol) return set_err("mgcm_cg2d_op: cg2dUseMinResSol not implemented in the distributed CG2D");
   HIPCHK(launch_cgd(m->d, m->p, m->f, op, a0, part, m->stream));
   return 0;
