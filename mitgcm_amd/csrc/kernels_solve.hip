@@ -689,7 +689,13 @@ __device__ __forceinline__ double block_max_nw(double v, double *red, int slot) 
 #endif
 // FMA: the operator rows, dot products and vector updates as fused multiply-adds in a fixed
 // order (cg2dUseFMA; the oracle's device-order mode evaluates the same fma chains)
-template <int BX, int BY, int NT, bool MINRES, bool FMA>
+// RC (recompute): no barrier before the two operator applications.  A thread derives the
+// out-of-block neighbour values it needs from the neighbour's inputs in LDS with the owner's
+// own expression -- s = q + beta*s from (q, s_old), r = r - alpha*A s from (r_old, A s) -- so
+// the values are the owner's bits, and only the two reduction barriers stay per iteration
+// (4 LDS arrays: r, s, q = M r, A s; the owner's own r and s are written after the barrier
+// that retires their readers).
+template <int BX, int BY, int NT, bool MINRES, bool FMA, bool RC = false>
 __global__ void __launch_bounds__(NT) k_cg2d_bxy(Dims d, Params p, Fields f, const unsigned *__restrict__ nbx,
                                                  const int *__restrict__ blkx, int nBlk, int maxIters, int nIterMinIn,
                                                  SolveRecord *rec, int *stepCounter) {
@@ -698,6 +704,7 @@ __global__ void __launch_bounds__(NT) k_cg2d_bxy(Dims d, Params p, Fields f, con
   double *r_l = lds;               // NP + 1 (last = ZERO slot)
   double *s_l = lds + (NP + 1);
   double *red = lds + 2 * (NP + 1);  // 4 x 16 partial slots
+  double *q_l = red + 64, *as_l = q_l + (NP + 1);   // RC only: q = M r and A s
   const int tid = threadIdx.x;
   const bool act = tid < nBlk;
   const int bt = act ? tid : 0;
@@ -753,12 +760,12 @@ __global__ void __launch_bounds__(NT) k_cg2d_bxy(Dims d, Params p, Fields f, con
     }
   // operator application: out-of-block neighbours from LDS, in-block from registers
   // (cg2d.F order: A = aW*vW + aW(i+1)*vE + aS*vS + aS(j+1)*vN + aC*v; M = pC*v + pW*vW + ...)
-  auto apply = [&](const double *arr, const double (&v)[BY][BX], double (&out)[BY][BX], bool isM) {
+  auto apply_nb = [&](auto nbv, const double (&v)[BY][BX], double (&out)[BY][BX], bool isM) {
     double vW[BY], vE[BY], vS[BX], vN[BX];
 #pragma unroll
-    for (int b = 0; b < BY; b++) { vW[b] = arr[nbi(b)]; vE[b] = arr[nbi(BY + b)]; }
+    for (int b = 0; b < BY; b++) { vW[b] = nbv(nbi(b)); vE[b] = nbv(nbi(BY + b)); }
 #pragma unroll
-    for (int a = 0; a < BX; a++) { vS[a] = arr[nbi(2 * BY + a)]; vN[a] = arr[nbi(2 * BY + BX + a)]; }
+    for (int a = 0; a < BX; a++) { vS[a] = nbv(nbi(2 * BY + a)); vN[a] = nbv(nbi(2 * BY + BX + a)); }
 #pragma unroll
     for (int b = 0; b < BY; b++)
 #pragma unroll
@@ -779,6 +786,9 @@ __global__ void __launch_bounds__(NT) k_cg2d_bxy(Dims d, Params p, Fields f, con
         else
           out[b][a] = aW[b][a] * w + aW[b][a + 1] * e + aS[a][b] * so + aS[a][b + 1] * no + aC[b][a] * v[b][a];
       }
+  };
+  auto apply = [&](const double *arr, const double (&v)[BY][BX], double (&out)[BY][BX], bool isM) {
+    apply_nb([&](int sl) { return arr[sl]; }, v, out, isM);
   };
   // cg2d.F:104-133: normalise the RHS
   double rhsMax = 0.0;
@@ -834,6 +844,7 @@ __global__ void __launch_bounds__(NT) k_cg2d_bxy(Dims d, Params p, Fields f, con
 #pragma unroll
     for (int a = 0; a < BX; a++) { r_l[cs[b][a]] = r[b][a]; s_l[cs[b][a]] = 0.0; }
   if (tid == 0) { r_l[NP] = 0.0; s_l[NP] = 0.0; }
+  if (RC && tid == 0) { q_l[NP] = 0.0; as_l[NP] = 0.0; }
   const double firstResidual = sqrt(err_sq);
   int nIterMin = nIterMinIn;
   double minResidualSq = -1.0;
@@ -848,6 +859,12 @@ __global__ void __launch_bounds__(NT) k_cg2d_bxy(Dims d, Params p, Fields f, con
   if (!(err_sq < p.cg2dTolerance_sq)) {
     double q[BY][BX];
     apply(r_l, r, q, true);
+    if (RC) {
+#pragma unroll
+      for (int b = 0; b < BY; b++)
+#pragma unroll
+        for (int a = 0; a < BX; a++) q_l[cs[b][a]] = q[b][a];
+    }
     double e = 0.0;
 #pragma unroll
     for (int b = 0; b < BY; b++)
@@ -862,6 +879,67 @@ __global__ void __launch_bounds__(NT) k_cg2d_bxy(Dims d, Params p, Fields f, con
     for (int it2d = 1; it2d <= maxIters; it2d++) {
       const double cgBeta = eta_qrN / eta_qrNM1;
       eta_qrNM1 = eta_qrN;
+      if constexpr (RC) {
+        if (it2d > 1) {   // the previous iteration's r, now that its neighbour readers are past D
+#pragma unroll
+          for (int b = 0; b < BY; b++)
+#pragma unroll
+            for (int a = 0; a < BX; a++) r_l[cs[b][a]] = r[b][a];
+        }
+#pragma unroll
+        for (int b = 0; b < BY; b++)
+#pragma unroll
+          for (int a = 0; a < BX; a++) sv[b][a] = FMA ? __builtin_fma(cgBeta, sv[b][a], q[b][a]) : q[b][a] + cgBeta * sv[b][a];
+        // A s with the neighbours' s = q + beta*s_old formed here from their (q, s_old)
+        apply_nb([&](int sl) { return FMA ? __builtin_fma(cgBeta, s_l[sl], q_l[sl]) : q_l[sl] + cgBeta * s_l[sl]; }, sv, q,
+                 false);
+        double aa = 0.0;
+#pragma unroll
+        for (int b = 0; b < BY; b++)
+#pragma unroll
+          for (int a = 0; a < BX; a++) {
+            as_l[cs[b][a]] = q[b][a];
+            aa = FMA ? __builtin_fma(sv[b][a], q[b][a], aa) : aa + sv[b][a] * q[b][a];
+          }
+        aslot = aslot ^ 1;
+        double alpha = block_sum_nw<NW>(aa, red, aslot);   // barrier B
+        alpha = eta_qrN / alpha;
+        double e2 = 0.0;
+#pragma unroll
+        for (int b = 0; b < BY; b++)
+#pragma unroll
+          for (int a = 0; a < BX; a++) {
+            s_l[cs[b][a]] = sv[b][a];   // for the next iteration's neighbours (read after D)
+            x[b][a] = FMA ? __builtin_fma(alpha, sv[b][a], x[b][a]) : x[b][a] + alpha * sv[b][a];
+            r[b][a] = FMA ? __builtin_fma(-alpha, q[b][a], r[b][a]) : r[b][a] - alpha * q[b][a];
+            e2 = FMA ? __builtin_fma(r[b][a], r[b][a], e2) : e2 + r[b][a] * r[b][a];
+          }
+        actualIts = it2d;
+        // M r with the neighbours' r = r_old - alpha*(A s) formed here from their (r_old, A s)
+        apply_nb([&](int sl) { return FMA ? __builtin_fma(-alpha, as_l[sl], r_l[sl]) : r_l[sl] - alpha * as_l[sl]; }, r, q,
+                 true);
+        double en = 0.0;
+#pragma unroll
+        for (int b = 0; b < BY; b++)
+#pragma unroll
+          for (int a = 0; a < BX; a++) {
+            q_l[cs[b][a]] = q[b][a];
+            en = FMA ? __builtin_fma(q[b][a], r[b][a], en) : en + q[b][a] * r[b][a];
+          }
+        block_sum2_nw<NW>(e2, en, red, 0);   // barrier D
+        err_sq = e2;
+        eta_qrN = en;
+        if (err_sq < p.cg2dTolerance_sq) break;
+        if (MINRES && err_sq < minResidualSq) {
+          minResidualSq = err_sq;
+          nIterMin = it2d;
+#pragma unroll
+          for (int b = 0; b < BY; b++)
+#pragma unroll
+            for (int a = 0; a < BX; a++) xmin[b][a] = x[b][a];
+        }
+        continue;
+      }
 #pragma unroll
       for (int b = 0; b < BY; b++)
 #pragma unroll
@@ -1246,10 +1324,16 @@ template <int BX, int BY, int NT>
 static hipError_t launch_bxy_t(const Dims &d, const Params &p, const Fields &f, const unsigned *nbx, const int *blkx,
                                int nBlk, int maxIters, int nIterMin, SolveRecord *rec, int *stepCounter, hipStream_t s) {
   if (nBlk > NT) return hipErrorInvalidValue;
-  const size_t lds = (2 * ((size_t)BX * BY * NT + 1) + 4 * 16) * sizeof(double);
+  // the recompute form (RC) only with MGCM_CG2D_RC=1: on config 2 it is bit-identical but
+  // 2.54 us/iteration against 1.82 (256 VGPRs + 29 spilled, twice the neighbour LDS reads):
+  // the two barriers it removes cost less than the recomputation (tools/cg2d_rc_ab.sh)
+  static const bool rc = getenv("MGCM_CG2D_RC") && atoi(getenv("MGCM_CG2D_RC")) == 1;
+  const size_t lds = ((rc ? 4 : 2) * ((size_t)BX * BY * NT + 1) + 4 * 16) * sizeof(double);
   const bool mr = nIterMin >= 0, fm = p.cg2dUseFMA != 0;
-  auto kern = mr ? (fm ? k_cg2d_bxy<BX, BY, NT, true, true> : k_cg2d_bxy<BX, BY, NT, true, false>)
-                 : (fm ? k_cg2d_bxy<BX, BY, NT, false, true> : k_cg2d_bxy<BX, BY, NT, false, false>);
+  auto kern = rc ? (mr ? (fm ? k_cg2d_bxy<BX, BY, NT, true, true, true> : k_cg2d_bxy<BX, BY, NT, true, false, true>)
+                       : (fm ? k_cg2d_bxy<BX, BY, NT, false, true, true> : k_cg2d_bxy<BX, BY, NT, false, false, true>))
+                 : (mr ? (fm ? k_cg2d_bxy<BX, BY, NT, true, true> : k_cg2d_bxy<BX, BY, NT, true, false>)
+                       : (fm ? k_cg2d_bxy<BX, BY, NT, false, true> : k_cg2d_bxy<BX, BY, NT, false, false>));
   static bool attrSet[4] = {false, false, false, false};
   if (!attrSet[2 * mr + fm]) {
     hipError_t e = hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
