@@ -66,36 +66,17 @@ __device__ __forceinline__ double find_rho(const Params &p, const Fields &f, int
   return p.rhoNil * (p.sBeta * (s - refSalt) - p.tAlpha * (t - refTemp)) + dRho;
 }
 
-// EXTERNAL_FIELDS_LOAD (external_fields_load.F:56-330) with GET_PERIODIC_INTERVAL
-// (get_periodic_interval.F:106-117), at myTime = myIter*deltaTClock read from the
-// device step counter (the step's start time, as LOAD_FIELDS_DRIVER sees it).
-__global__ void __launch_bounds__(256) k_fields_load(Dims d, Params p, Fields f, const int *iterPtr) {
-  const long q = (long)blockIdx.x * blockDim.x + threadIdx.x;
-  const long N2 = d.n2 * d.nTiles;
-  if (q >= N2) return;
-  const double cycleLength = p.externForcingCycle, recSpacing = p.externForcingPeriod;
-  const double currentTime = (double)(*iterPtr) * p.deltaTClock;
-  const int nbRec = (int)llround(cycleLength / recSpacing);
-  const double locTime = currentTime - recSpacing * 0.5 + cycleLength * (double)(2 - llround(currentTime / cycleLength));
-  const double tmpTime = fmod(locTime, cycleLength);
-  const int tRec1 = 1 + (int)(tmpTime / recSpacing);
-  const int tRec2 = 1 + tRec1 % nbRec;
-  const double aW = (tmpTime - recSpacing * (double)(tRec1 - 1)) / recSpacing;
-  const double bW = 1.0 - aW;
-  double *dst[6] = {f.SST, f.SSS, f.fu, f.fv, f.Qnet, f.EmPmR};
-#pragma unroll
-  for (int v = 0; v < 6; v++) {
-    const double *r = f.forcRec + (long)v * p.nForcRec * N2;
-    dst[v][q] = bW * r[(long)(tRec1 - 1) * N2 + q] + aW * r[(long)(tRec2 - 1) * N2 + q];
-  }
-}
-
 // DO_OCEANIC_PHYS (do_oceanic_phys.F:548-882) per column over the full halo range:
 // FREEZE_SURFACE (freeze_surface.F:55-66), EXTERNAL_FORCING_SURF with
 // FORCING_SURF_RELAX (external_forcing_surf.F:90-290, forcing_surf_relax.F:75-100;
 // linear free surface), FIND_RHO_2D at every level (kRef = k), GRAD_SIGMA's sigmaR with
 // rho(theta(k-1), kRef = k) (grad_sigma.F:103-117) and CALC_IVDC (calc_ivdc.F:60-71).
-__global__ void __launch_bounds__(256) k_oceanic_phys(Dims d, Params p, Fields f) {
+// LOAD_FIELDS_DRIVER's EXTERNAL_FIELDS_LOAD (external_fields_load.F:56-330, with
+// GET_PERIODIC_INTERVAL get_periodic_interval.F:106-117, at myTime = myIter*deltaTClock read
+// from the device step counter) is folded in: the k = 1 thread of each column interpolates
+// the six monthly records at its point -- the only point DO_OCEANIC_PHYS reads them at --
+// and stores them for the later readers (momentum, continuity): one launch fewer per step.
+__global__ void __launch_bounds__(256) k_oceanic_phys(Dims d, Params p, Fields f, const int *iterPtr) {
   // one thread per (i,j,k), full halo range: FREEZE_SURFACE only changes theta(k=1), so
   // every reader of theta(k=1) applies the clamp itself and the k = 1 thread stores it
   MG_PLANE(1 - d.OLx, d.nx, 1 - d.OLy, d.ny, z)
@@ -105,6 +86,24 @@ __global__ void __launch_bounds__(256) k_oceanic_phys(Dims d, Params p, Fields f
     const double v = f.theta[MG_I3(d, i, j, kk, t)];
     return (kk == 1 && p.allowFreezing && v < -1.9) ? -1.9 : v;
   };
+  if (k == 1 && p.periodicExternalForcing) {
+    const long N2 = d.n2 * d.nTiles;
+    const double cycleLength = p.externForcingCycle, recSpacing = p.externForcingPeriod;
+    const double currentTime = (double)(*iterPtr) * p.deltaTClock;
+    const int nbRec = (int)llround(cycleLength / recSpacing);
+    const double locTime = currentTime - recSpacing * 0.5 + cycleLength * (double)(2 - llround(currentTime / cycleLength));
+    const double tmpTime = fmod(locTime, cycleLength);
+    const int tRec1 = 1 + (int)(tmpTime / recSpacing);
+    const int tRec2 = 1 + tRec1 % nbRec;
+    const double aW = (tmpTime - recSpacing * (double)(tRec1 - 1)) / recSpacing;
+    const double bW = 1.0 - aW;
+    double *dst[6] = {f.SST, f.SSS, f.fu, f.fv, f.Qnet, f.EmPmR};
+#pragma unroll
+    for (int v = 0; v < 6; v++) {
+      const double *r = f.forcRec + (long)v * p.nForcRec * N2;
+      dst[v][q] = bW * r[(long)(tRec1 - 1) * N2 + q] + aW * r[(long)(tRec2 - 1) * N2 + q];
+    }
+  }
   if (k == 1) {
     const double th1 = theta_at(1), s1 = f.salt[q31];
     if (p.allowFreezing) f.theta[q31] = th1;
@@ -855,12 +854,8 @@ __global__ void __launch_bounds__(256) k_tracer_impl(Dims d, Params p, Fields f,
 }
 
 hipError_t launch_oceanic_phys(const Dims &d, const Params &p, const Fields &f, const int *iterPtr, hipStream_t s) {
-  if (p.periodicExternalForcing) {
-    const long n = d.n2 * d.nTiles;
-    hipLaunchKernelGGL(k_fields_load, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, d, p, f, iterPtr);
-  }
   hipLaunchKernelGGL(k_oceanic_phys, dim3(mg_plane_blocks(d.nx, d.ny, d.nT * d.Nr)), dim3(MG_PLANE_THREADS), 0, s, d, p,
-                     f);
+                     f, iterPtr);
   if (p.useGMRedi)
     hipLaunchKernelGGL(k_gm_tensor, dim3(mg_plane_blocks(d.nx - 2, d.ny - 2, d.nT * d.Nr)), dim3(MG_PLANE_THREADS), 0,
                        s, d, p, f);
