@@ -126,7 +126,7 @@ static const PDesc PTAB[] = {
   PI_(no_slip_bottom), PI_(selectCoriScheme), PI_(momForcingOutAB), PI_(momDissip_In_AB),
   PI_(useHarmonicVisc), PI_(useBiharmonicVisc), PI_(implicitViscosity), PI_(selectCoriMap),
   PI_(cg2dMaxIters), PI_(cg2dUseMinResSol), PI_(exactConserv), PI_(nIter0), PI_(usingCartesianGrid),
-  PI_(cg2dNormaliseRHS), PI_(myIter), PI_(numIters), PI_(nIterMin),
+  PI_(cg2dNormaliseRHS), PI_(useSRCGSolver), PI_(myIter), PI_(numIters), PI_(nIterMin),
   PI_(usingSphericalPolarGrid), PI_(selectMetricTerms), PI_(integr_GeoPot), PI_(tempStepping),
   PI_(tempAdvection), PI_(tempForcing), PI_(tempAdvScheme), PI_(tempVertAdvScheme), PI_(implicitDiffusion),
   PI_(saltStepping), PI_(saltAdvection), PI_(saltForcing), PI_(saltAdvScheme), PI_(saltVertAdvScheme),

@@ -71,6 +71,7 @@ typedef struct OModel {
   double *aW2d, *aS2d, *aC2d, *pW, *pS, *pC;
   double cg2dNorm, cg2dTolerance_sq, globalArea;
   int cg2dNormaliseRHS;
+  int useSRCGSolver;   /* CG2D_SR (cg2d_sr.F) instead of CG2D */
 
   /* --- state (DYNVARS.h, FFIELDS.h, SURFACE.h) --- */
   double *uVel, *vVel, *wVel, *theta, *salt, *etaN;

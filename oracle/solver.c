@@ -148,9 +148,135 @@ static double applyA_fma(const OModel *m, const double *v, int i, int j, int t) 
              fma(aW[O2(m, i + 1, j, t)], v[O2(m, i + 1, j, t)], aW[p] * v[O2(m, i - 1, j, t)]))));
 }
 
+/* A v and M v at (i,j) in the reference's operand order (cg2d.F:155-161, 212-217), or as the
+ * device's fma chains (fmaMode) */
+static double cg_applyA(const OModel *m, const double *v, int i, int j, int t, int fmaMode) {
+  if (fmaMode) return applyA_fma(m, v, i, j, t);
+  const double *aW = m->aW2d, *aS = m->aS2d, *aC = m->aC2d;
+  const long p = O2(m, i, j, t);
+  return aW[p] * v[O2(m, i - 1, j, t)] + aW[O2(m, i + 1, j, t)] * v[O2(m, i + 1, j, t)] + aS[p] * v[O2(m, i, j - 1, t)] +
+         aS[O2(m, i, j + 1, t)] * v[O2(m, i, j + 1, t)] + aC[p] * v[p];
+}
+static double cg_applyM(const OModel *m, const double *r, int i, int j, int t, int fmaMode) {
+  const double *pW = m->pW, *pS = m->pS, *pC = m->pC;
+  const long p = O2(m, i, j, t);
+  if (fmaMode)
+    return fma(pS[O2(m, i, j + 1, t)], r[O2(m, i, j + 1, t)], fma(pS[p], r[O2(m, i, j - 1, t)],
+               fma(pW[O2(m, i + 1, j, t)], r[O2(m, i + 1, j, t)], fma(pW[p], r[O2(m, i - 1, j, t)], pC[p] * r[p]))));
+  return pC[p] * r[p] + pW[p] * r[O2(m, i - 1, j, t)] + pW[O2(m, i + 1, j, t)] * r[O2(m, i + 1, j, t)] +
+         pS[p] * r[O2(m, i, j - 1, t)] + pS[O2(m, i, j + 1, t)] * r[O2(m, i, j + 1, t)];
+}
+/* sum of a[p]*b[p] over the interior: per-tile sequential partials in tile order
+ * (GLOBAL_SUM_TILE_RL / GLOBAL_SUM_VECTOR_RL), or the device's order (sum plan) */
+static double cg_dot(const OModel *m, const double *a, const double *b, double *term, int dev, int fmaMode) {
+  const int sNx = m->sNx, sNy = m->sNy, nT = m->nTiles;
+  double acc = 0.0;
+  for (int t = 0; t < nT; t++) {
+    double e = 0.0;
+    for (int j = 1; j <= sNy; j++)
+      for (int i = 1; i <= sNx; i++) {
+        const long p = O2(m, i, j, t);
+        e = e + a[p] * b[p];
+        term[p] = a[p] * b[p];
+      }
+    acc = acc + e;
+  }
+  if (dev) return fmaMode ? plan_dot(m, a, b) : plan_sum(m, term);
+  return acc;
+}
+
+/* CG2D_SR (model/src/cg2d_sr.F:100-440; solve_for_pressure.F:289, useSRCGSolver): the
+ * single-reduction conjugate gradient -- one standard step, then per iteration y = M r,
+ * v = A y and the three sums (y.r, y.v, r.r) in one GLOBAL_SUM_VECTOR_RL; the residual of the
+ * exit test is that of the previous update. */
+static void cg2d_sr(OModel *m, double *cg2d_b, double *cg2d_x, double *firstResidual, double *minResidualSq,
+                    double *lastResidual, int *numIters, int *nIterMin) {
+  const int sNx = m->sNx, sNy = m->sNy, nT = m->nTiles;
+  const long N2 = m->n2 * nT;
+  double *r = calloc(N2, 8), *s = calloc(N2, 8), *q = calloc(N2, 8), *y = calloc(N2, 8), *v = calloc(N2, 8);
+  double *xmin = calloc(N2, 8), *term = calloc(N2, 8);
+  const int dev = m->sumPlan != NULL, fmaMode = dev && m->cg2dFMA;
+  double rhsMax = 0.0, rhsNorm = 1.0;
+  *minResidualSq = -1.0;
+#define LOOP for (int t = 0; t < nT; t++) for (int j = 1; j <= sNy; j++) for (int i = 1; i <= sNx; i++)
+  LOOP { const long p = O2(m, i, j, t); cg2d_b[p] = cg2d_b[p] * m->cg2dNorm; rhsMax = fmax(fabs(cg2d_b[p]), rhsMax); }
+  if (m->cg2dNormaliseRHS) {   /* cg2d_sr.F:113-130 */
+    if (rhsMax != 0.0) rhsNorm = 1.0 / rhsMax;
+    LOOP { const long p = O2(m, i, j, t); cg2d_b[p] = cg2d_b[p] * rhsNorm; cg2d_x[p] = cg2d_x[p] * rhsNorm; }
+  }
+  oracle_exch_xy(m, cg2d_x);
+  if (*nIterMin >= 0) LOOP xmin[O2(m, i, j, t)] = cg2d_x[O2(m, i, j, t)];
+  LOOP { const long p = O2(m, i, j, t); r[p] = cg2d_b[p] - cg_applyA(m, cg2d_x, i, j, t, fmaMode); }
+  oracle_exch_xy(m, r);
+  {   /* sumRHS, err_sq (cg2d_sr.F:167-170) */
+    double *ones = calloc(N2, 8);
+    LOOP ones[O2(m, i, j, t)] = 1.0;
+    const double sumRHS = dev ? plan_sum(m, cg2d_b) : cg_dot(m, cg2d_b, ones, term, 0, 0);
+    m->sumRHS = sumRHS; m->rhsMax = rhsMax;
+    free(ones);
+  }
+  double err_sq = cg_dot(m, r, r, term, dev, fmaMode);
+  int it2d = 0;
+  *firstResidual = sqrt(err_sq);
+  if (*nIterMin >= 0) { *nIterMin = 0; *minResidualSq = err_sq; }
+  if (!(err_sq < m->cg2dTolerance_sq)) {
+    /* the standard first step (cg2d_sr.F:190-260) */
+    LOOP { const long p = O2(m, i, j, t); y[p] = cg_applyM(m, r, i, j, t, fmaMode); s[p] = y[p]; }
+    oracle_exch_xy(m, s);
+    double eta_qrN = cg_dot(m, y, r, term, dev, fmaMode), eta_qrNM1 = eta_qrN;
+    LOOP { const long p = O2(m, i, j, t); q[p] = cg_applyA(m, s, i, j, t, fmaMode); }
+    double alpha = cg_dot(m, s, q, term, dev, fmaMode);
+    double sigma = eta_qrN / alpha;
+    LOOP {
+      const long p = O2(m, i, j, t);
+      cg2d_x[p] = fmaMode ? fma(sigma, s[p], cg2d_x[p]) : cg2d_x[p] + sigma * s[p];
+      r[p] = fmaMode ? fma(-sigma, q[p], r[p]) : r[p] - sigma * q[p];
+    }
+    oracle_exch_xy(m, r);
+    int converged = 0;
+    for (it2d = 1; it2d <= *numIters - 1; it2d++) {   /* cg2d_sr.F:262-370 */
+      LOOP y[O2(m, i, j, t)] = cg_applyM(m, r, i, j, t, fmaMode);
+      oracle_exch_xy(m, y);
+      LOOP v[O2(m, i, j, t)] = cg_applyA(m, y, i, j, t, fmaMode);
+      eta_qrN = cg_dot(m, y, r, term, dev, fmaMode);
+      const double delta = cg_dot(m, y, v, term, dev, fmaMode);
+      err_sq = cg_dot(m, r, r, term, dev, fmaMode);
+      if (err_sq < m->cg2dTolerance_sq) { converged = 1; break; }
+      if (err_sq < *minResidualSq) {
+        *minResidualSq = err_sq;
+        *nIterMin = it2d;
+        LOOP xmin[O2(m, i, j, t)] = cg2d_x[O2(m, i, j, t)];
+      }
+      const double cgBeta = eta_qrN / eta_qrNM1;
+      eta_qrNM1 = eta_qrN;
+      alpha = delta - (cgBeta * cgBeta) * alpha;
+      sigma = eta_qrN / alpha;
+      LOOP {
+        const long p = O2(m, i, j, t);
+        s[p] = fmaMode ? fma(cgBeta, s[p], y[p]) : y[p] + cgBeta * s[p];
+        cg2d_x[p] = fmaMode ? fma(sigma, s[p], cg2d_x[p]) : cg2d_x[p] + sigma * s[p];
+        q[p] = fmaMode ? fma(cgBeta, q[p], v[p]) : v[p] + cgBeta * q[p];
+        r[p] = fmaMode ? fma(-sigma, q[p], r[p]) : r[p] - sigma * q[p];
+      }
+      oracle_exch_xy(m, r);
+    }
+    if (!converged) err_sq = cg_dot(m, r, r, term, dev, fmaMode);   /* cg2d_sr.F:372-382 */
+  }
+  if (*nIterMin >= 0 && err_sq > *minResidualSq) LOOP cg2d_x[O2(m, i, j, t)] = xmin[O2(m, i, j, t)];
+  if (m->cg2dNormaliseRHS) LOOP cg2d_x[O2(m, i, j, t)] = cg2d_x[O2(m, i, j, t)] / rhsNorm;
+#undef LOOP
+  *lastResidual = sqrt(err_sq);
+  *numIters = it2d;   /* cg2d_sr.F:410: the loop index at exit */
+  free(r); free(s); free(q); free(y); free(v); free(xmin); free(term);
+}
+
 /* CG2D (model/src/cg2d.F:13-415), default branch (no CG2D_SINGLECPU_SUM) */
 void oracle_cg2d(OModel *m, double *cg2d_b, double *cg2d_x, double *firstResidual,
                  double *minResidualSq, double *lastResidual, int *numIters, int *nIterMin) {
+  if (m->useSRCGSolver) {
+    cg2d_sr(m, cg2d_b, cg2d_x, firstResidual, minResidualSq, lastResidual, numIters, nIterMin);
+    return;
+  }
   const int sNx = m->sNx, sNy = m->sNy, nT = m->nTiles;
   const long N2 = m->n2 * nT;
   double *r = calloc(N2, 8), *s = calloc(N2, 8), *q = calloc(N2, 8), *xmin = calloc(N2, 8);
