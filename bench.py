@@ -58,6 +58,9 @@ def parse():
                     help="with --shard: CG2D replicated on every GPU (default) or the reference's distributed "
                          "CG2D with GLOBAL_SUM_TILE_RL over the collective (mitgcm_amd/parallel.py)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--set", action="append", default=[], metavar="NAME=VALUE",
+                    help="override a namelist parameter of the GPU model (A/B runs, e.g. useSRCGSolver=1); "
+                         "recorded in config.params_over")
     ap.add_argument("--pmc-summary", default=None,
                     help="tools/pmc_summary.py output of rocprofv3 --pmc passes of this command (roofline.traffic); "
                          "default profiles/r02/<config tag>/pmc_summary.json")
@@ -205,7 +208,14 @@ def main():
     import numpy as np
     from mitgcm_amd import configs
 
-    m = configs.make_model(config_fn(a.config), device=local)
+    over = {}
+    for kv in a.set:
+        k, v = kv.split("=", 1)
+        over[k] = float(v)
+    cfn = config_fn(a.config)
+    if over:
+        cfn = (lambda f: lambda: (lambda r: (r[0], {**r[1], **over}) + tuple(r[2:]))(f()))(cfn)
+    m = configs.make_model(cfn, device=local)
     g = m.g
     dt_clock = m.params["deltaTClock"]
     npts = g.nTiles * g.sNx * g.sNy
@@ -303,7 +313,8 @@ def main():
                                                        else "; replicas only"),
                    "tiles_per_gpu": stepper.nT if shard else g.nTiles, "points_per_tile": [g.sNx, g.sNy, g.Nr],
                    "parallelism": ("tiles%d" if shard else "replicas%d") % world,
-                   "cg2d": a.cg2d if shard else "single-GPU kernel"},
+                   "cg2d": a.cg2d if shard else "single-GPU kernel",
+                   **({"params_over": over} if over else {})},
         "cg2d_iters_per_s": cg2d_iters_per_s,
         "cg2d_mean_iters_per_solve": iters_total / max(1, len(iters)),
         "kernel_ms_mean": {k: v[0] for k, v in kern.items()},

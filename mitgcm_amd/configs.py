@@ -269,7 +269,7 @@ def read_pickup_cd(g, path, Nx, Ny):
     return out
 
 
-def global_ocean_90x40x15(nSx=1, nSy=1, OL=3, data_dir=None, pickup_dir=None, nIter0=36000):
+def global_ocean_90x40x15(nSx=1, nSy=1, OL=3, data_dir=None, pickup_dir=None, nIter0=36000, params_over=None):
     """verification/global_ocean.90x40x15 (BASELINE config 2): the lat-lon grid, bathymetry
     and monthly forcing of tutorial_global_oce_latlon (input/prepare_run links them),
     restarted from pickup.0000036000 + pickup_cd.0000036000.  input/data differences:
@@ -300,6 +300,7 @@ def global_ocean_90x40x15(nSx=1, nSy=1, OL=3, data_dir=None, pickup_dir=None, nI
     state.update(read_pickup_cd(g, os.path.join(pd, "pickup_cd.%010d" % nIter0), Nx, Ny))
     for n in ("h0FacC", "h0FacW", "h0FacS", "recip_Rcol", "rLowW", "rLowS", "rSurfW", "rSurfS"):
         state[n] = g.f[n]
+    params.update(params_over or {})   # option variants for parity tests
     return g, params, state, forcing
 
 

@@ -658,6 +658,29 @@ __device__ __forceinline__ void block_sum2_nw(double &v0, double &v1, double *re
   v0 = row_sum16(l < NW ? red[slot * 16 + l] : 0.0);
   v1 = row_sum16(l < NW ? red[(slot ^ 1) * 16 + l] : 0.0);
 }
+// three sums in one reduction (slots 0, 1, 2), each reduced as block_sum_nw does
+template <int NW>
+__device__ __forceinline__ void block_sum3_nw(double &v0, double &v1, double &v2, double *red) {
+  v0 = row_sum16(v0);
+  v1 = row_sum16(v1);
+  v2 = row_sum16(v2);
+  v0 = v0 + dpp_bcast_f64<0x142, 0xA>(v0);
+  v1 = v1 + dpp_bcast_f64<0x142, 0xA>(v1);
+  v2 = v2 + dpp_bcast_f64<0x142, 0xA>(v2);
+  v0 = v0 + dpp_bcast_f64<0x143, 0xC>(v0);
+  v1 = v1 + dpp_bcast_f64<0x143, 0xC>(v1);
+  v2 = v2 + dpp_bcast_f64<0x143, 0xC>(v2);
+  v0 = lane_f64(v0, 63);
+  v1 = lane_f64(v1, 63);
+  v2 = lane_f64(v2, 63);
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  if (lane == 0) { red[wv] = v0; red[16 + wv] = v1; red[32 + wv] = v2; }
+  __syncthreads();
+  const int l = lane & 15;
+  v0 = row_sum16(l < NW ? red[l] : 0.0);
+  v1 = row_sum16(l < NW ? red[16 + l] : 0.0);
+  v2 = row_sum16(l < NW ? red[32 + l] : 0.0);
+}
 __device__ __forceinline__ double wave_max_u(double v) {
   v = row_max16(v);
   return fmax(fmax(lane_f64(v, 0), lane_f64(v, 16)), fmax(lane_f64(v, 32), lane_f64(v, 48)));
@@ -695,7 +718,10 @@ __device__ __forceinline__ double block_max_nw(double v, double *red, int slot) 
 // the values are the owner's bits, and only the two reduction barriers stay per iteration
 // (4 LDS arrays: r, s, q = M r, A s; the owner's own r and s are written after the barrier
 // that retires their readers).
-template <int BX, int BY, int NT, bool MINRES, bool FMA, bool RC = false>
+// SR: CG2D_SR (cg2d_sr.F, useSRCGSolver) -- one standard step, then per iteration y = M r,
+// v = A y and the three sums (y.r, y.v, r.r) in one reduction: three barriers per iteration
+// (y, the reduction, r) instead of four; s_l holds y.
+template <int BX, int BY, int NT, bool MINRES, bool FMA, bool RC = false, bool SR = false>
 __global__ void __launch_bounds__(NT) k_cg2d_bxy(Dims d, Params p, Fields f, const unsigned *__restrict__ nbx,
                                                  const int *__restrict__ blkx, int nBlk, int maxIters, int nIterMinIn,
                                                  SolveRecord *rec, int *stepCounter) {
@@ -856,7 +882,97 @@ __global__ void __launch_bounds__(NT) k_cg2d_bxy(Dims d, Params p, Fields f, con
   // for alpha; the r_l writes of iteration n are fenced by an explicit barrier.  Same
   // values and the same exit test as cg2d.F:211-352, one reduction fewer per iteration.
   int aslot = 2;
-  if (!(err_sq < p.cg2dTolerance_sq)) {
+  if (SR && !(err_sq < p.cg2dTolerance_sq)) {
+    // the standard first step (cg2d_sr.F:190-260): y = M r, s = y, eta = y.r, q = A s
+    double q[BY][BX], y[BY][BX];
+    apply(r_l, r, y, true);
+    double e = 0.0;
+#pragma unroll
+    for (int b = 0; b < BY; b++)
+#pragma unroll
+      for (int a = 0; a < BX; a++) {
+        sv[b][a] = y[b][a];
+        s_l[cs[b][a]] = y[b][a];
+        e = FMA ? __builtin_fma(y[b][a], r[b][a], e) : e + y[b][a] * r[b][a];
+      }
+    double eta_qrN = block_sum_nw<NW>(e, red, 0);   // also fences s_l
+    eta_qrNM1 = eta_qrN;
+    apply(s_l, sv, q, false);
+    double aa = 0.0;
+#pragma unroll
+    for (int b = 0; b < BY; b++)
+#pragma unroll
+      for (int a = 0; a < BX; a++) aa = FMA ? __builtin_fma(sv[b][a], q[b][a], aa) : aa + sv[b][a] * q[b][a];
+    double alpha = block_sum_nw<NW>(aa, red, 1);
+    double sigma = eta_qrN / alpha;
+#pragma unroll
+    for (int b = 0; b < BY; b++)
+#pragma unroll
+      for (int a = 0; a < BX; a++) {
+        x[b][a] = FMA ? __builtin_fma(sigma, sv[b][a], x[b][a]) : x[b][a] + sigma * sv[b][a];
+        r[b][a] = FMA ? __builtin_fma(-sigma, q[b][a], r[b][a]) : r[b][a] - sigma * q[b][a];
+        r_l[cs[b][a]] = r[b][a];
+      }
+    __syncthreads();
+    bool conv = false;
+    int it2d = 1;
+    for (; it2d <= maxIters - 1; it2d++) {   // cg2d_sr.F:262-370
+      apply(r_l, r, y, true);
+#pragma unroll
+      for (int b = 0; b < BY; b++)
+#pragma unroll
+        for (int a = 0; a < BX; a++) s_l[cs[b][a]] = y[b][a];
+      __syncthreads();
+      double v[BY][BX];
+      apply(s_l, y, v, false);
+      double eyr = 0.0, eyv = 0.0, err = 0.0;
+#pragma unroll
+      for (int b = 0; b < BY; b++)
+#pragma unroll
+        for (int a = 0; a < BX; a++) {
+          eyr = FMA ? __builtin_fma(y[b][a], r[b][a], eyr) : eyr + y[b][a] * r[b][a];
+          eyv = FMA ? __builtin_fma(y[b][a], v[b][a], eyv) : eyv + y[b][a] * v[b][a];
+          err = FMA ? __builtin_fma(r[b][a], r[b][a], err) : err + r[b][a] * r[b][a];
+        }
+      block_sum3_nw<NW>(eyr, eyv, err, red);
+      err_sq = err;
+      if (err_sq < p.cg2dTolerance_sq) { conv = true; break; }
+      if (MINRES && err_sq < minResidualSq) {
+        minResidualSq = err_sq;
+        nIterMin = it2d;
+#pragma unroll
+        for (int b = 0; b < BY; b++)
+#pragma unroll
+          for (int a = 0; a < BX; a++) xmin[b][a] = x[b][a];
+      }
+      eta_qrN = eyr;
+      const double cgBeta = eta_qrN / eta_qrNM1;
+      eta_qrNM1 = eta_qrN;
+      alpha = eyv - (cgBeta * cgBeta) * alpha;
+      sigma = eta_qrN / alpha;
+#pragma unroll
+      for (int b = 0; b < BY; b++)
+#pragma unroll
+        for (int a = 0; a < BX; a++) {
+          sv[b][a] = FMA ? __builtin_fma(cgBeta, sv[b][a], y[b][a]) : y[b][a] + cgBeta * sv[b][a];
+          x[b][a] = FMA ? __builtin_fma(sigma, sv[b][a], x[b][a]) : x[b][a] + sigma * sv[b][a];
+          q[b][a] = FMA ? __builtin_fma(cgBeta, q[b][a], v[b][a]) : v[b][a] + cgBeta * q[b][a];
+          r[b][a] = FMA ? __builtin_fma(-sigma, q[b][a], r[b][a]) : r[b][a] - sigma * q[b][a];
+          r_l[cs[b][a]] = r[b][a];
+        }
+      __syncthreads();
+    }
+    if (!conv) {   // cg2d_sr.F:372-382: the residual of the last update
+      double err = 0.0;
+#pragma unroll
+      for (int b = 0; b < BY; b++)
+#pragma unroll
+        for (int a = 0; a < BX; a++) err = FMA ? __builtin_fma(r[b][a], r[b][a], err) : err + r[b][a] * r[b][a];
+      err_sq = block_sum_nw<NW>(err, red, 0);
+    }
+    actualIts = it2d;
+  }
+  if (!SR && !(err_sq < p.cg2dTolerance_sq)) {
     double q[BY][BX];
     apply(r_l, r, q, true);
     if (RC) {
@@ -1329,16 +1445,20 @@ static hipError_t launch_bxy_t(const Dims &d, const Params &p, const Fields &f, 
   // the two barriers it removes cost less than the recomputation (tools/cg2d_rc_ab.sh)
   static const bool rc = getenv("MGCM_CG2D_RC") && atoi(getenv("MGCM_CG2D_RC")) == 1;
   const size_t lds = ((rc ? 4 : 2) * ((size_t)BX * BY * NT + 1) + 4 * 16) * sizeof(double);
-  const bool mr = nIterMin >= 0, fm = p.cg2dUseFMA != 0;
-  auto kern = rc ? (mr ? (fm ? k_cg2d_bxy<BX, BY, NT, true, true, true> : k_cg2d_bxy<BX, BY, NT, true, false, true>)
-                       : (fm ? k_cg2d_bxy<BX, BY, NT, false, true, true> : k_cg2d_bxy<BX, BY, NT, false, false, true>))
-                 : (mr ? (fm ? k_cg2d_bxy<BX, BY, NT, true, true> : k_cg2d_bxy<BX, BY, NT, true, false>)
-                       : (fm ? k_cg2d_bxy<BX, BY, NT, false, true> : k_cg2d_bxy<BX, BY, NT, false, false>));
-  static bool attrSet[4] = {false, false, false, false};
-  if (!attrSet[2 * mr + fm]) {
+  const bool mr = nIterMin >= 0, fm = p.cg2dUseFMA != 0, sr = p.useSRCGSolver != 0;
+  auto kern = sr   ? (mr ? (fm ? k_cg2d_bxy<BX, BY, NT, true, true, false, true> : k_cg2d_bxy<BX, BY, NT, true, false, false, true>)
+                         : (fm ? k_cg2d_bxy<BX, BY, NT, false, true, false, true>
+                               : k_cg2d_bxy<BX, BY, NT, false, false, false, true>))
+              : rc ? (mr ? (fm ? k_cg2d_bxy<BX, BY, NT, true, true, true> : k_cg2d_bxy<BX, BY, NT, true, false, true>)
+                         : (fm ? k_cg2d_bxy<BX, BY, NT, false, true, true> : k_cg2d_bxy<BX, BY, NT, false, false, true>))
+                   : (mr ? (fm ? k_cg2d_bxy<BX, BY, NT, true, true> : k_cg2d_bxy<BX, BY, NT, true, false>)
+                         : (fm ? k_cg2d_bxy<BX, BY, NT, false, true> : k_cg2d_bxy<BX, BY, NT, false, false>));
+  static bool attrSet[8] = {false, false, false, false, false, false, false, false};
+  const int ai = 4 * sr + 2 * mr + fm;
+  if (!attrSet[ai]) {
     hipError_t e = hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return e;
-    attrSet[2 * mr + fm] = true;
+    attrSet[ai] = true;
   }
   hipLaunchKernelGGL(kern, dim3(1), dim3(NT), lds, s, d, p, f, nbx, blkx, nBlk, maxIters, nIterMin, rec, stepCounter);
   return hipGetLastError();

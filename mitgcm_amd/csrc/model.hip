@@ -108,7 +108,7 @@ static const PDesc PARAMS[] = {
     PD(mtFacMom), PD(cg2dNorm), PD(cg2dTolerance_sq),
     PI_(momAdvection), PI_(momViscosity), PI_(momForcing), PI_(useCoriolis), PI_(no_slip_sides),
     PI_(no_slip_bottom), PI_(selectCoriScheme), PI_(momForcingOutAB), PI_(momDissip_In_AB),
-    PI_(implicitViscosity), PI_(cg2dMaxIters), PI_(cg2dUseMinResSol), PI_(cg2dNormaliseRHS), PI_(nIter0), PI_(cg2dUseFMA),
+    PI_(implicitViscosity), PI_(cg2dMaxIters), PI_(cg2dUseMinResSol), PI_(cg2dNormaliseRHS), PI_(nIter0), PI_(cg2dUseFMA), PI_(useSRCGSolver),
     PD(gravity), PD(gravitySign), PD(rhoNil), PD(tAlpha), PD(sBeta), PD(ivdc_kappa), PD(diffKhT), PD(diffKrT),
     PD(deltaTtracer), PI_(exactConserv), PI_(tempStepping), PI_(tempAdvection), PI_(tempForcing),
     PI_(implicitDiffusion), PI_(tempAdvScheme), PI_(saltStepping), PI_(saltAdvection), PI_(saltForcing),
@@ -964,6 +964,8 @@ int mgcm_init(mgcm_model *m) {
     if (build_mwg(m)) return -1;
     if (m->p.cg2dUseMinResSol) return set_err("mgcm_init: cg2dUseMinResSol with the multi-workgroup CG2D not implemented");
   }
+  if (m->p.useSRCGSolver && (m->useMwg || m->nBlkX == 0))
+    return set_err("mgcm_init: useSRCGSolver (CG2D_SR) is implemented in the blocked single-workgroup CG2D only");
   if ((m->p.viscA4D != 0.0 || m->p.viscA4Z != 0.0) && (m->d.OLx < 3 || m->d.OLy < 3))
     return set_err("mgcm_init: biharmonic viscosity needs OLx, OLy >= 3 (del2u of the halo ring)");
   const bool rstar = m->p.nonlinFreeSurf > 0;

@@ -203,6 +203,8 @@ class ShardedModel:
         if cg2d not in ("replicated", "distributed"):
             raise ValueError("cg2d must be 'replicated' or 'distributed'")
         self.cg2d = cg2d
+        if cg2d == "distributed" and model.params.get("useSRCGSolver", 0):
+            raise NotImplementedError("useSRCGSolver (CG2D_SR) with the distributed CG2D not implemented")
         if cg2d == "distributed":
             self.cg_part = torch.zeros(2 * g.nTiles, dtype=torch.float64, device=dv)   # part[2*tile + s]
             self.cg_local = torch.zeros((mt, 2), dtype=torch.float64, device=dv)
