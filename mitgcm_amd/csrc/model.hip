@@ -960,7 +960,8 @@ int mgcm_init(mgcm_model *m) {
   // blocks; otherwise the multi-workgroup solver (MGCM_CG2D_SINGLE=1 keeps the generic
   // single-workgroup one where it fits)
   m->useMwg = false;
-  if (m->nBlkX == 0 && m->nBlk == 0 && !(getenv("MGCM_CG2D_SINGLE") && m->nPts <= cg2d_block_max_points())) {
+  const bool single = getenv("MGCM_CG2D_SINGLE") && atoi(getenv("MGCM_CG2D_SINGLE")) == 1;
+  if (m->nBlkX == 0 && m->nBlk == 0 && !(single && m->nPts <= cg2d_block_max_points())) {
     if (build_mwg(m)) return -1;
     if (m->p.cg2dUseMinResSol) return set_err("mgcm_init: cg2dUseMinResSol with the multi-workgroup CG2D not implemented");
   }
