@@ -87,7 +87,17 @@ __device__ __forceinline__ double mw_wave_max(double v) {
   return fmax(fmax(mw_lane(v, 0), mw_lane(v, 16)), fmax(mw_lane(v, 32), mw_lane(v, 48)));
 }
 
-constexpr int MW_NT = 256, MW_OPT = 4, MW_RPT = 1, MW_NW = MW_NT / 64;
+// workgroup geometry: NT threads x OPT points per thread = 1024 points per part.  Swept with
+// tools/mwg_geom_ab.sh (profiles/r02/mwg_geometry.txt): 1024 x 1 (16 waves, 104 VGPRs) hides
+// the hand-off and LDS latencies best -- 4.25 / 7.39 us per iteration on cs32x15 / LLC-90
+// against 6.02 / 8.70 for 256 x 4; the MGCM_MW_* macros build the other variants
+#ifndef MGCM_MW_NT
+#define MGCM_MW_NT 1024
+#endif
+#ifndef MGCM_MW_OPT
+#define MGCM_MW_OPT 1
+#endif
+constexpr int MW_NT = MGCM_MW_NT, MW_OPT = MGCM_MW_OPT, MW_RPT = 1, MW_NW = MW_NT / 64;
 constexpr int MW_NV = 3;   // values per reduction
 
 // ---- granule hand-offs (Guideline 16 R2) -------------------------------------------

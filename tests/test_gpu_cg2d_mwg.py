@@ -2,7 +2,7 @@
 
 Bars:
   * BASELINE config 2 (90x40x15, 1 tile) with the single-workgroup solvers switched off
-    (4 row-strip parts): 6 steps bit-identical to the oracle summing CG2D in the device's
+    (row-strip parts of NT x OPT points: 4 at the default 256 x 4): 6 steps bit-identical to the oracle summing CG2D in the device's
     order (mgcm_cg2d_sum_plan: per-thread terms, pairwise trees, partials in part order);
   * the same solve with every part pinned to one XCD and with the parts spread over the
     chip: bit-identical (the sums do not depend on placement);
@@ -39,9 +39,9 @@ def test_mwg_ocean90_bitexact_vs_device_order_oracle():
     from oracle.harness import ocean90_oracle
     m = _ocean90_mwg()
     assert m.cg2d_kernel() == "mwg"
-    assert lib().mgcm_get_param(m.h, b"cg2dParts") == 4.0
     plan, NT, PPT, NG = m.cg2d_sum_plan()
-    assert NG == 4
+    parts = -(-40 // ((NT * PPT) // 90))   # row strips of the 90 x 40 tile, NT*PPT points each
+    assert lib().mgcm_get_param(m.h, b"cg2dParts") == float(parts) and NG == parts, (NG, parts)
     od, g = ocean90_oracle()
     od.set_sum_plan(plan, NT, PPT, NG, fma=m.cg2d_fma())
     o_ref, _ = ocean90_oracle()
