@@ -121,6 +121,12 @@ DATA = {
 }
 
 
+def _overlap_info(m):
+    from mitgcm_amd._lib import lib
+    g = lambda n: lib().mgcm_get_param(m.h, n)
+    return {"on": int(g(b"overlap")), "trial_ms_on": round(g(b"ovlMsOn"), 4), "trial_ms_off": round(g(b"ovlMsOff"), 4)}
+
+
 def config_fn(name):
     """The mitgcm_amd.configs set-up behind a --config name."""
     from mitgcm_amd import configs
@@ -316,6 +322,9 @@ def main():
                    "cg2d": a.cg2d if shard else "single-GPU kernel",
                    **({"params_over": over} if over else {})},
         "cg2d_iters_per_s": cg2d_iters_per_s,
+        # THERMODYNAMICS on a second stream beside DYNAMICS: picked per workload by timing both
+        # graphs over the first 20 graph-replayed steps (results identical either way)
+        "thermo_overlap": _overlap_info(m),
         "cg2d_mean_iters_per_solve": iters_total / max(1, len(iters)),
         "kernel_ms_mean": {k: v[0] for k, v in kern.items()},
         # dominant kernel: the whole-solve CG2D.  It is not HBM-bound: its working set sits in

@@ -185,7 +185,11 @@ struct mgcm_model {
   long exchCap = 0;
   // hipGraphs of two FORWARD_STEPs, one per theta/salt ping-pong parity
   bool useGraph = true;
-  hipGraphExec_t graphExec[4] = {nullptr, nullptr, nullptr, nullptr};
+  hipGraphExec_t graphExec[2][4] = {};   // [THERMODYNAMICS overlap off/on][tracer buffer parity]
+  // overlap auto-selection (ovl_trial): both graphs timed on a copy of the state
+  bool ovlAuto = false, ovlDecided = false;
+  float ovlMs[2] = {0.f, 0.f};
+  hipEvent_t ovlEv[2] = {nullptr, nullptr};
   double *thetaA = nullptr, *saltA = nullptr;
   // step counters: [0] = myIter, [1] = record slot
   int *d_ctr = nullptr;
@@ -695,12 +699,15 @@ mgcm_model *mgcm_create(int sNx, int sNy, int OLx, int OLy, int Nr, int nSx, int
   m->stream = m->ownStream;
   if (hipStreamCreateWithFlags(&m->stream2, hipStreamNonBlocking) != hipSuccess ||
       hipEventCreateWithFlags(&m->evFork, hipEventDisableTiming) != hipSuccess ||
-      hipEventCreateWithFlags(&m->evJoin, hipEventDisableTiming) != hipSuccess) {
+      hipEventCreateWithFlags(&m->evJoin, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreate(&m->ovlEv[0]) != hipSuccess || hipEventCreate(&m->ovlEv[1]) != hipSuccess) {
     set_err("mgcm_create: second stream / events");
     delete m;
     return nullptr;
   }
   m->overlap = getenv("MGCM_NO_OVERLAP") == nullptr;
+  // MGCM_OVERLAP=1 forces the second stream on; otherwise the graph path picks by timing
+  m->ovlAuto = m->overlap && !(getenv("MGCM_OVERLAP") && atoi(getenv("MGCM_OVERLAP")) == 1);
   // one arena per kind for the 2-D and 3-D fields (MG_F2D_LIST / MG_F3D_LIST order, common.h)
   d.N2all = d.n2 * d.nTiles;
   d.N3all = d.n3 * d.nTiles;
@@ -780,6 +787,8 @@ void mgcm_destroy(mgcm_model *m) {
   if (m->stream2) hipStreamDestroy(m->stream2);
   if (m->evFork) hipEventDestroy(m->evFork);
   if (m->evJoin) hipEventDestroy(m->evJoin);
+  for (auto &ev : m->ovlEv)
+    if (ev) hipEventDestroy(ev);
   delete m;
 }
 
@@ -824,6 +833,11 @@ double mgcm_get_param(mgcm_model *m, const char *name) {
   // 4: k_cg2d_mwg, 3: k_cg2d_bxy, 2: k_cg2d_blk2, 1: k_cg2d_block
   if (!strcmp(name, "cg2dKernel")) return m->useMwg ? 4.0 : m->nBlkX > 0 ? 3.0 : (m->nBlk > 0 ? 2.0 : 1.0);
   if (!strcmp(name, "cg2dParts")) return m->useMwg ? (double)m->mwg.G : 1.0;
+  // THERMODYNAMICS on the second stream: 1 on, 0 off; -1 while the graph path is still timing
+  // both (ovlMsOn / ovlMsOff: ovl_trial's event times of the two graphs, 8 steps each)
+  if (!strcmp(name, "overlap")) return (m->ovlAuto && !m->ovlDecided) ? -1.0 : (m->overlap ? 1.0 : 0.0);
+  if (!strcmp(name, "ovlMsOn")) return m->ovlMs[1];
+  if (!strcmp(name, "ovlMsOff")) return m->ovlMs[0];
   if (!strcmp(name, "cg2dBxyVariant")) return (double)m->bxyVar;
   // whether the selected kernel solves with fused multiply-adds (k_cg2d_bxy honours cg2dUseFMA)
   if (!strcmp(name, "cg2dFMA")) return (!m->useMwg && m->nBlkX > 0 && m->p.cg2dUseFMA) ? 1.0 : 0.0;
@@ -1314,8 +1328,9 @@ static int one_step(mgcm_model *m) {
 }
 
 static void drop_graphs(mgcm_model *m) {
-  for (int q = 0; q < 4; q++)
-    if (m->graphExec[q]) { (void)hipGraphExecDestroy(m->graphExec[q]); m->graphExec[q] = nullptr; }
+  for (auto &row : m->graphExec)
+    for (auto &ge : row)
+      if (ge) { (void)hipGraphExecDestroy(ge); ge = nullptr; }
 }
 
 // Which theta/salt ping-pong buffers are current (the kernels' arguments differ).
@@ -1327,8 +1342,8 @@ static int buffer_parity(const mgcm_model *m) {
 // ping-pong swaps twice, so the pointers are back where they started), then
 // replayed: no per-kernel host launch cost inside a batch.
 static int two_step_graph(mgcm_model *m, hipGraphExec_t *out) {
-  const int q = buffer_parity(m);
-  if (!m->graphExec[q]) {
+  const int q = buffer_parity(m), o = m->overlap ? 1 : 0;
+  if (!m->graphExec[o][q]) {
     hipGraph_t g = nullptr;
     HIPCHK(hipStreamBeginCapture(m->stream, hipStreamCaptureModeThreadLocal));
     int rc = one_step(m);
@@ -1336,11 +1351,11 @@ static int two_step_graph(mgcm_model *m, hipGraphExec_t *out) {
     hipError_t e = hipStreamEndCapture(m->stream, &g);
     if (rc) { if (g) (void)hipGraphDestroy(g); return -1; }
     HIPCHK(e);
-    e = hipGraphInstantiate(&m->graphExec[q], g, nullptr, nullptr, 0);
+    e = hipGraphInstantiate(&m->graphExec[o][q], g, nullptr, nullptr, 0);
     (void)hipGraphDestroy(g);
     HIPCHK(e);
   }
-  *out = m->graphExec[q];
+  *out = m->graphExec[o][q];
   return 0;
 }
 
@@ -1352,6 +1367,59 @@ int mgcm_prepare(mgcm_model *m) {
   return two_step_graph(m, &ge);
 }
 
+// THERMODYNAMICS overlap auto-selection: the device state (both field arenas, the other
+// fields, counters, solve records) is copied aside, 20 steps run through the two graphs --
+// on, off (one two-step graph each: builds and warms them), then on, off, on, off of two
+// graphs each, bracketed by events -- and the state is copied back, so the caller's steps
+// are untouched; the faster graph is kept.  Both graphs compute identical results.
+static int ovl_trial(mgcm_model *m) {
+  const bool forkable = !m->p.staggerTimeStep && m->p.momStepping && (m->p.tempStepping || m->p.saltStepping);
+  if (!forkable) { m->ovlDecided = true; return 0; }   // one_step never forks: nothing to choose
+  std::vector<std::pair<void *, size_t>> parts = {
+      {m->f.a2, (size_t)F2_COUNT * m->d.N2all * sizeof(double)},
+      {m->f.a3, (size_t)F3_COUNT * m->d.N3all * sizeof(double)},
+      {m->d_ctr, 2 * sizeof(int)},
+      {m->d_rec, (size_t)m->maxRec * sizeof(SolveRecord)}};
+  for (auto &fd : FIELDS)
+    if (fd.kind != F2D && fd.kind != F3D && field_ptr(m, &fd))
+      parts.push_back({field_ptr(m, &fd), (size_t)field_count(m, fd.kind) * sizeof(double)});
+  size_t total = 0;
+  for (auto &pr : parts) total += (pr.second + 255) & ~(size_t)255;
+  char *save = nullptr;
+  HIPCHK(hipMalloc(&save, total));
+  size_t off = 0;
+  for (auto &pr : parts) {
+    HIPCHK(hipMemcpyAsync(save + off, pr.first, pr.second, hipMemcpyDeviceToDevice, m->stream));
+    off += (pr.second + 255) & ~(size_t)255;
+  }
+  const bool ovl0 = m->overlap;
+  int rc = 0;
+  for (int ph = 0; ph < 6 && !rc; ph++) {
+    const int pairs = ph < 2 ? 1 : 2, mode = (ph & 1) ? 0 : 1;
+    m->overlap = mode != 0;
+    hipGraphExec_t ge;
+    if (two_step_graph(m, &ge)) { rc = -1; break; }   // built before the events (same parity after a pair)
+    if (hipEventRecord(m->ovlEv[0], m->stream) != hipSuccess) { rc = -1; break; }
+    for (int r = 0; r < pairs && !rc; r++)
+      if (two_step_graph(m, &ge) || hipGraphLaunch(ge, m->stream) != hipSuccess) rc = -1;
+    float ms = 0.f;
+    if (rc || hipEventRecord(m->ovlEv[1], m->stream) != hipSuccess || hipEventSynchronize(m->ovlEv[1]) != hipSuccess ||
+        hipEventElapsedTime(&ms, m->ovlEv[0], m->ovlEv[1]) != hipSuccess) { rc = -1; break; }
+    if (ph >= 2) m->ovlMs[mode] += ms;
+  }
+  off = 0;
+  for (auto &pr : parts) {
+    HIPCHK(hipMemcpyAsync(pr.first, save + off, pr.second, hipMemcpyDeviceToDevice, m->stream));
+    off += (pr.second + 255) & ~(size_t)255;
+  }
+  HIPCHK(hipStreamSynchronize(m->stream));
+  (void)hipFree(save);
+  if (rc) { m->overlap = ovl0; return set_err("ovl_trial: graph replay failed"); }
+  m->ovlDecided = true;
+  m->overlap = m->ovlMs[1] <= m->ovlMs[0];
+  return 0;
+}
+
 int mgcm_forward_step(mgcm_model *m, int nsteps) {
   if (check_ready(m)) return -1;
   if (nsteps <= 0 || nsteps > m->maxRec) return set_err("mgcm_forward_step: nsteps %d out of range", nsteps);
@@ -1359,6 +1427,7 @@ int mgcm_forward_step(mgcm_model *m, int nsteps) {
   HIPCHK(hipMemsetAsync(m->d_ctr + 1, 0, sizeof(int), m->stream));
   int s = 0;
   if (m->useGraph && !m->timing) {
+    if (m->ovlAuto && !m->ovlDecided && nsteps >= 2 && ovl_trial(m)) return -1;
     for (; s + 2 <= nsteps; s += 2) {
       hipGraphExec_t ge;
       if (two_step_graph(m, &ge)) return -1;

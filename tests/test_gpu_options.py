@@ -129,3 +129,25 @@ def test_cs32x15_dst3_scheme30_and_implicit_viscosity_4_steps_vs_oracle():
         sc = np.abs(ref).max()
         assert np.abs(dev - ref).max() <= 1e-10 * sc, (n, np.abs(dev - ref).max(), sc)
     m.close()
+
+
+def test_overlap_trial_leaves_the_state_untouched():
+    """The THERMODYNAMICS-overlap auto-selection (model.hip ovl_trial) times both step graphs
+    on the live state and copies it back: a 10-step graph batch after it equals ten single
+    steps of a model that never ran the trial, bit for bit."""
+    from mitgcm_amd import configs
+    from mitgcm_amd._lib import lib
+    cfg = _gyre(33)
+    a, b = configs.make_model(cfg), configs.make_model(cfg)
+    a.forward_step(10)
+    for _ in range(10):
+        b.forward_step(1)
+    a.sync()
+    b.sync()
+    assert lib().mgcm_get_param(a.h, b"overlap") in (0.0, 1.0)
+    assert lib().mgcm_get_param(b.h, b"overlap") == -1.0   # b never ran a graph batch
+    for n in ("uVel", "vVel", "wVel", "theta", "salt", "etaN"):
+        assert np.array_equal(a.get(n), b.get(n)), n
+    assert a.solve_stats() == b.solve_stats()
+    a.close()
+    b.close()
