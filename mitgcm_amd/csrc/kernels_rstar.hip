@@ -19,19 +19,42 @@ namespace mgcm {
 // (lat-lon / single facet: scalar copies), then rStarDh*Dt = (Fac - Fac_old)/dtFS and
 // rStarExp = Fac/Fac_old (:283-298).  Each thread reads and writes only its own point's
 // factors, so the old values need no second buffer.
+// The new etaH of k_exch_etaH at point q: EXCH_XY_RL of the eta k_corr_cont left in cg2d_b
+// (the interior source of a halo point; the point itself inside; etaN where neither).
+__device__ __forceinline__ double eta_exch(const Dims &d, const Fields &f, const long *srcOf, long q) {
+  const long sq = srcOf[q];
+  if (sq >= 0) return f.cg2d_b[sq];
+  const long l = q % d.n2;
+  const int i = (int)(l % d.nx) - d.OLx + 1, j = (int)(l / d.nx) - d.OLy + 1;
+  return (i >= 1 && i <= d.sNx && j >= 1 && j <= d.sNy) ? f.cg2d_b[q] : f.etaN[q];
+}
+
+// fuseEtaH: k_exch_etaH in the same pass (the FORWARD_STEP order exch_etaH -> CALC_R_STAR):
+// each thread stores its own point's etaN, etaH, etaHnm1 (and PmEpR) and takes the etaH of
+// the neighbours it reads from eta_exch, the same values k_exch_etaH stores.  The only
+// cross-thread location both read and written is etaN at points neither interior nor
+// mapped, which is rewritten with the value it holds.
+template <bool FUSE>
 __global__ void __launch_bounds__(256) k_calc_r_star(Dims d, Params p, Fields f, const long *__restrict__ srcOf) {
   const long q = (long)blockIdx.x * blockDim.x + threadIdx.x;
   if (q >= d.n2 * d.nTiles) return;
   const int t = (int)(q / d.n2);
   if (t < d.t0 || t >= d.t0 + d.nT) return;
+  if constexpr (FUSE) {   // k_exch_etaH (kernels_solve.hip), atInit = 0
+    if (p.nonlinFreeSurf > 0 && p.useRealFreshWaterFlux) f.PmEpR[q] = -f.EmPmR[q];
+    const double x = eta_exch(d, f, srcOf, q);
+    f.etaHnm1[q] = f.etaH[q];
+    f.etaN[q] = x;
+    f.etaH[q] = x;
+  }
   const long sq = srcOf[q], r = sq >= 0 ? sq : q;   // where the new value is computed
   const long l = r % d.n2;
   const int i = (int)(l % d.nx) - d.OLx + 1, j = (int)(l / d.nx) - d.OLy + 1;
-  const double *eta = f.etaH;
+  auto eta = [&](long qq) { return FUSE ? eta_exch(d, f, srcOf, qq) : f.etaH[qq]; };
   const double oc = f.rStarFacC[q], ow = f.rStarFacW[q], os = f.rStarFacS[q];
   double fc = oc, fw = ow, fs = os;
   if (i >= 0 && i <= d.sNx + 1 && j >= 0 && j <= d.sNy + 1)   // kSurfC <= Nr <=> maskInC = 1
-    fc = (f.maskInC[r] != 0.0) ? (eta[r] + f.Ro_surf[r] - f.R_low[r]) * f.recip_Rcol[r] : 1.0;
+    fc = (f.maskInC[r] != 0.0) ? (eta(r) + f.Ro_surf[r] - f.R_low[r]) * f.recip_Rcol[r] : 1.0;
   // W/S factors: at the EXCH1 source as above, or (EXCH2 topology) in place on the
   // reference's ranges, their halos then refilled through the vector map (calc_r_star())
   const long rv = p.cubeCorners ? q : r;
@@ -40,7 +63,7 @@ __global__ void __launch_bounds__(256) k_calc_r_star(Dims d, Params p, Fields f,
   if (iv >= 1 && iv <= d.sNx + 1 && jv >= 1 && jv <= d.sNy) {
     if (f.maskInW[rv] != 0.0) {
       const double tmp = f.rSurfW[rv] - f.rLowW[rv];
-      fw = (0.5 * (eta[rv - 1] * f.rA[rv - 1] + eta[rv] * f.rA[rv]) * f.recip_rAw[rv] + tmp) / tmp;
+      fw = (0.5 * (eta(rv - 1) * f.rA[rv - 1] + eta(rv) * f.rA[rv]) * f.recip_rAw[rv] + tmp) / tmp;
     } else {
       fw = 1.0;
     }
@@ -48,7 +71,7 @@ __global__ void __launch_bounds__(256) k_calc_r_star(Dims d, Params p, Fields f,
   if (iv >= 1 && iv <= d.sNx && jv >= 1 && jv <= d.sNy + 1) {
     if (f.maskInS[rv] != 0.0) {
       const double tmp = f.rSurfS[rv] - f.rLowS[rv];
-      fs = (0.5 * (eta[rv - d.nx] * f.rA[rv - d.nx] + eta[rv] * f.rA[rv]) * f.recip_rAs[rv] + tmp) / tmp;
+      fs = (0.5 * (eta(rv - d.nx) * f.rA[rv - d.nx] + eta(rv) * f.rA[rv]) * f.recip_rAs[rv] + tmp) / tmp;
     } else {
       fs = 1.0;
     }
@@ -148,9 +171,11 @@ __global__ void __launch_bounds__(256) k_update_cg2d_p(Dims d, Params p, Fields 
   }
 }
 
-hipError_t launch_calc_r_star(const Dims &d, const Params &p, const Fields &f, const long *srcOf, hipStream_t s) {
+hipError_t launch_calc_r_star(const Dims &d, const Params &p, const Fields &f, const long *srcOf, hipStream_t s,
+                              bool fuseEtaH) {
   const long n = d.n2 * d.nTiles;
-  hipLaunchKernelGGL(k_calc_r_star, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, d, p, f, srcOf);
+  hipLaunchKernelGGL(fuseEtaH ? k_calc_r_star<true> : k_calc_r_star<false>, dim3((unsigned)((n + 255) / 256)), dim3(256),
+                     0, s, d, p, f, srcOf);
   return hipGetLastError();
 }
 

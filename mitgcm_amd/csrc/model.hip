@@ -44,7 +44,7 @@ hipError_t launch_exchange_multi(const Dims &, const XFields &, const long *, in
 hipError_t launch_exchange_uv(const Dims &, double *, double *, const long *, int, int, int, hipStream_t);
 hipError_t launch_exch_eta(const Dims &, const Params &, const Fields &, const long *, bool, int, hipStream_t);
 hipError_t launch_corr_cont(const Dims &, const Params &, const Fields &, int, hipStream_t);
-hipError_t launch_calc_r_star(const Dims &, const Params &, const Fields &, const long *, hipStream_t);
+hipError_t launch_calc_r_star(const Dims &, const Params &, const Fields &, const long *, hipStream_t, bool fuseEtaH = false);
 hipError_t launch_update_r_star_cg2d(const Dims &, const Params &, const Fields &, const long *, hipStream_t);
 hipError_t launch_halo_pack(const Dims &, const XFields &, const long *, long, double *, int, hipStream_t);
 hipError_t launch_oceanic_phys(const Dims &, const Params &, const Fields &, const int *, hipStream_t);
@@ -949,9 +949,9 @@ static int exchange_uv(mgcm_model *m, double *u, double *v, int nz, bool withSig
 // operator.
 static Dims all_tiles(const Dims &d) { Dims a = d; a.t0 = 0; a.nT = d.nTiles; return a; }
 
-static hipError_t calc_r_star(mgcm_model *m) {
+static hipError_t calc_r_star(mgcm_model *m, bool fuseEtaH = false) {
   const Dims da = all_tiles(m->d);
-  hipError_t e = launch_calc_r_star(da, m->p, m->f, m->d_srcOf, m->stream);
+  hipError_t e = launch_calc_r_star(da, m->p, m->f, m->d_srcOf, m->stream, fuseEtaH);
   if (e != hipSuccess || !m->uvMap) return e;
   double *pairs[3][2] = {{m->f.rStarFacW, m->f.rStarFacS}, {m->f.rStarDhWDt, m->f.rStarDhSDt},
                          {m->f.rStarExpW, m->f.rStarExpS}};
@@ -1309,10 +1309,14 @@ static int one_step(mgcm_model *m) {
     TIMED(K_CG2D, launch_cg2d(m, m->p.cg2dMaxIters, m->p.cg2dUseMinResSol - 1));
     TIMED(K_ETA, launch_exch_eta(m->d, m->p, m->f, m->d_srcOf, false, 0, m->stream));
     TIMED(K_CONT, launch_corr_cont(m->d, m->p, m->f, 0, m->stream));
-    if (m->p.exactConserv) TIMED(K_ETA, launch_exch_eta(m->d, m->p, m->f, m->d_srcOf, true, 0, m->stream));
     // forward_step.F:965-977: CALC_R_STAR(etaH(n+1)); the next step's RESET_NLFS_VARS +
-    // UPDATE_R_STAR(.FALSE.) restore the hFac in place, so they are not repeated here
-    if (m->p.nonlinFreeSurf > 0) TIMED(K_RSTAR, calc_r_star(m));
+    // UPDATE_R_STAR(.FALSE.) restore the hFac in place, so they are not repeated here.
+    // Under r* the exactConserv EXCH(eta) + UPDATE_ETAH runs inside CALC_R_STAR's pass
+    // (k_calc_r_star<FUSE>; MGCM_NO_ETAH_FUSE=1 keeps the two launches)
+    static const bool noFuse = getenv("MGCM_NO_ETAH_FUSE") && atoi(getenv("MGCM_NO_ETAH_FUSE")) == 1;
+    const bool fuseEtaH = m->p.exactConserv && m->p.nonlinFreeSurf > 0 && !noFuse;
+    if (m->p.exactConserv && !fuseEtaH) TIMED(K_ETA, launch_exch_eta(m->d, m->p, m->f, m->d_srcOf, true, 0, m->stream));
+    if (m->p.nonlinFreeSurf > 0) TIMED(K_RSTAR, calc_r_star(m, fuseEtaH));
   } else {
     if (mgcm_integr_continuity(m)) return -1;
   }
