@@ -1744,7 +1744,14 @@ int mgcm_cg2d(mgcm_model *m, double *cg2d_b, double *cg2d_x, double *firstResidu
   HIPCHK(hipMemcpyAsync(m->f.cg2d_b, cg2d_b, n * sizeof(double), hipMemcpyHostToDevice, m->stream));
   HIPCHK(hipMemcpyAsync(m->f.cg2d_x, cg2d_x, n * sizeof(double), hipMemcpyHostToDevice, m->stream));
   HIPCHK(hipMemsetAsync(m->d_ctr + 1, 0, sizeof(int), m->stream));
-  TIMED(K_CG2D, launch_cg2d(m, *numIters, *nIterMin));
+  // CG2D itself (cg2d.F): useSRCGSolver selects CG2D_SR only in SOLVE_FOR_PRESSURE
+  const int sr = m->p.useSRCGSolver;
+  m->p.useSRCGSolver = 0;
+  const int ev = ev_begin(m, K_CG2D);
+  const hipError_t le = launch_cg2d(m, *numIters, *nIterMin);
+  ev_end(m, K_CG2D, ev);
+  m->p.useSRCGSolver = sr;
+  HIPCHK(le);
   HIPCHK(hipMemcpyAsync(cg2d_b, m->f.cg2d_b, n * sizeof(double), hipMemcpyDeviceToHost, m->stream));
   HIPCHK(hipMemcpyAsync(cg2d_x, m->f.cg2d_x, n * sizeof(double), hipMemcpyDeviceToHost, m->stream));
   SolveRecord r;
