@@ -111,10 +111,15 @@ __device__ __forceinline__ bool gran_get(gu64 *g, unsigned tag, double &v) {
   v = __builtin_bit_cast(double, ((hi & 0xffffffffull) << 32) | (lo & 0xffffffffull));
   return (unsigned)(lo >> 32) == tag && (unsigned)(hi >> 32) == tag;
 }
+// Launch epochs: ctr[0] holds the epoch, read by every part at its start and advanced by
+// part 0 after the last hand-off (every part has read it by then); a granule's tag is
+// (epoch mod 2^16) << 16 | phase, so no memset is needed between launches.  The timeout
+// word ctr[1] holds epoch + 1 of a launch that gave up.
+__device__ __forceinline__ unsigned mw_tag(unsigned ep, int phase) { return ((ep & 0xffffu) << 16) | (unsigned)phase; }
 // bounded spin: after ~2^22 passes every part gives up (timeout word), so no wave hangs
-__device__ __forceinline__ bool spin_fail(unsigned &spins, gu32 *tmo) {
-  if (__hip_atomic_load(tmo, RLX_AGENT) != 0u || ++spins > (1u << 22)) {
-    __hip_atomic_store(tmo, 1u, RLX_AGENT);
+__device__ __forceinline__ bool spin_fail(unsigned &spins, gu32 *tmo, unsigned ep) {
+  if (__hip_atomic_load(tmo, RLX_AGENT) == ep + 1u || ++spins > (1u << 22)) {
+    __hip_atomic_store(tmo, ep + 1u, RLX_AGENT);
     return true;
   }
   __builtin_amdgcn_s_sleep(1);
@@ -133,11 +138,11 @@ struct MwImport {
 };
 
 template <int NV, bool MAXOP>
-__device__ __forceinline__ bool mw_sync(double *v, const MwgTables &T, int g, int &nsync, double *red,
+__device__ __forceinline__ bool mw_sync(double *v, const MwgTables &T, int g, int &nsync, double *red, unsigned ep,
                                         const MwImport *imp = nullptr) {
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   nsync++;
-  const unsigned tag = (unsigned)nsync;
+  const unsigned tag = mw_tag(ep, nsync);
   gu64 *P = (gu64 *)(T.part + (size_t)(nsync & 1) * MW_NV * T.G * 2);
   // workgroup partial: the pairwise tree over its threads (wave tree, then the row-16 tree
   // over the zero-padded wave values: the operations of block_sum_nw)
@@ -172,7 +177,7 @@ __device__ __forceinline__ bool mw_sync(double *v, const MwgTables &T, int g, in
         }
       }
       if (__all(good)) break;
-      if (spin_fail(spins, (gu32 *)T.ctr + 1)) { ok = false; break; }
+      if (spin_fail(spins, (gu32 *)T.ctr + 1, ep)) { ok = false; break; }
     }
 #pragma unroll
     for (int q = 0; q < NV; q++) {
@@ -190,7 +195,7 @@ __device__ __forceinline__ bool mw_sync(double *v, const MwgTables &T, int g, in
       for (;;) {
         const bool good = !act || gran_get(src, tag, xv);
         if (__all(good)) break;
-        if (spin_fail(spins, (gu32 *)T.ctr + 1)) break;   // the timeout word fails the solve
+        if (spin_fail(spins, (gu32 *)T.ctr + 1, ep)) break;   // the timeout word fails the solve
       }
       if (act) imp->imp_l[qq] = xv;
     }
@@ -235,6 +240,7 @@ __global__ void __launch_bounds__(MW_NT) k_cg2d_mwg(Dims d, Params p, Fields f, 
   double *imp_l = red + 16 * 16;      // IMAX: the ring q handed off at the last reduction
   const int tid = threadIdx.x;
   int nsync = 0;
+  const unsigned ep = __hip_atomic_load((gu32 *)T.ctr, RLX_AGENT);
   const size_t go = (size_t)g * NO, gr = (size_t)g * NR, gi = (size_t)g * T.IMAX;
   // ---- owned points: offsets, neighbour slots, coefficients (cg2d.F operator rows)
   int G2[MW_OPT];
@@ -287,7 +293,7 @@ __global__ void __launch_bounds__(MW_NT) k_cg2d_mwg(Dims d, Params p, Fields f, 
   double rhsMaxV[1] = {0.0};
 #pragma unroll
   for (int m = 0; m < MW_OPT; m++) { b[m] = b[m] * p.cg2dNorm; rhsMaxV[0] = fmax(fabs(b[m]), rhsMaxV[0]); }
-  bool ok = mw_sync<1, true>(rhsMaxV, T, g, nsync, red);
+  bool ok = mw_sync<1, true>(rhsMaxV, T, g, nsync, red, ep);
   const double rhsMax = rhsMaxV[0];
   double rhsNorm = 1.0;
   if (p.cg2dNormaliseRHS) {
@@ -336,10 +342,10 @@ __global__ void __launch_bounds__(MW_NT) k_cg2d_mwg(Dims d, Params p, Fields f, 
     q[m] = pC[m] * r[m] + pW0[m] * r_l[LO(nwe[m])] + pW1[m] * r_l[HI(nwe[m])] + pS0[m] * r_l[LO(nsn[m])] +
            pS1[m] * r_l[HI(nsn[m])];
     v3[2] = v3[2] + q[m] * r[m];
-    if ((exp >> m) & 1u) gran_put(xs + (size_t)2 * T.ownC[go + m * MW_NT + tid], (unsigned)(nsync + 1), q[m]);
+    if ((exp >> m) & 1u) gran_put(xs + (size_t)2 * T.ownC[go + m * MW_NT + tid], mw_tag(ep, nsync + 1), q[m]);
   }
   for (int qq = tid; qq < nImp; qq += MW_NT) s_l[NO + qq] = 0.0;
-  ok = ok && mw_sync<3, false>(v3, T, g, nsync, red, &imp);
+  ok = ok && mw_sync<3, false>(v3, T, g, nsync, red, ep, &imp);
   double err_sq = v3[0];
   const double sumRHS = v3[1];
   double eta_qrN = v3[2], eta_qrNM1 = 1.0;
@@ -380,7 +386,7 @@ __global__ void __launch_bounds__(MW_NT) k_cg2d_mwg(Dims d, Params p, Fields f, 
         rq[m] = raW0[m] * s_l[LO(rwe[m])] + raW1[m] * s_l[HI(rwe[m])] + raS0[m] * s_l[LO(rsn[m])] +
                 raS1[m] * s_l[HI(rsn[m])] + raC[m] * s_l[NO + m * MW_NT + tid];
       MW_STAMP(2);
-      ok = mw_sync<1, false>(av, T, g, nsync, red);
+      ok = mw_sync<1, false>(av, T, g, nsync, red, ep);
       MW_STAMP(3);
       if (!ok) break;
       const double alpha = eta_qrN / av[0];
@@ -405,10 +411,10 @@ __global__ void __launch_bounds__(MW_NT) k_cg2d_mwg(Dims d, Params p, Fields f, 
         q[m] = pC[m] * r[m] + pW0[m] * r_l[LO(nwe[m])] + pW1[m] * r_l[HI(nwe[m])] + pS0[m] * r_l[LO(nsn[m])] +
                pS1[m] * r_l[HI(nsn[m])];
         v2[1] = v2[1] + q[m] * r[m];
-        if ((exp >> m) & 1u) gran_put(xs + (size_t)2 * T.ownC[go + m * MW_NT + tid], (unsigned)(nsync + 1), q[m]);
+        if ((exp >> m) & 1u) gran_put(xs + (size_t)2 * T.ownC[go + m * MW_NT + tid], mw_tag(ep, nsync + 1), q[m]);
       }
       MW_STAMP(4);
-      ok = mw_sync<2, false>(v2, T, g, nsync, red, &imp);
+      ok = mw_sync<2, false>(v2, T, g, nsync, red, ep, &imp);
       MW_STAMP(5);
       if (!ok) break;
       err_sq = v2[0];
@@ -436,9 +442,10 @@ __global__ void __launch_bounds__(MW_NT) k_cg2d_mwg(Dims d, Params p, Fields f, 
     R.minResidualSq = -1.0;
     R.rhsMax = rhsMax;
     R.sumRHS = sumRHS;
-    const bool tmo = __hip_atomic_load((gu32 *)T.ctr + 1, RLX_AGENT) != 0u;
+    const bool tmo = __hip_atomic_load((gu32 *)T.ctr + 1, RLX_AGENT) == ep + 1u;
     R.numIters = (ok && !tmo) ? actualIts : -1;   // -1: a grid hand-off timed out
     R.nIterMin = -1;
+    __hip_atomic_store((gu32 *)T.ctr, ep + 1u, RLX_AGENT);   // the next launch's epoch
   }
 #undef LO
 #undef HI
@@ -448,8 +455,9 @@ int cg2d_mwg_geometry(int *nt, int *opt, int *rpt) { *nt = MW_NT; *opt = MW_OPT;
 
 hipError_t launch_cg2d_mwg(const Dims &d, const Params &p, const Fields &f, const MwgTables &T, int maxIters,
                            SolveRecord *rec, int *stepCounter, hipStream_t s) {
-  hipError_t e = hipMemsetAsync(T.ctr, 0, T.hsBytes, s);   // timeout word + every granule, every launch
-  if (e != hipSuccess) return e;
+  // phases per launch: 2 + 2 per iteration, below 2^16 (the tag's phase field)
+  if (maxIters < 0 || maxIters > 30000) return hipErrorInvalidValue;
+  hipError_t e = hipSuccess;
   const size_t lds = (size_t)(2 * (T.SZ + 1) + 16 * 16 + T.IMAX) * sizeof(double);
   auto kern = T.pinned ? k_cg2d_mwg<true> : k_cg2d_mwg<false>;
   static bool attrSet[2] = {false, false};

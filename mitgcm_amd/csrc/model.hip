@@ -638,11 +638,13 @@ static int build_mwg(mgcm_model *m) {
     return -1;
   T.G = G; T.IMAX = IMAX; T.SZ = SZ;
   T.pinned = (G <= 32 && !getenv("MGCM_CG2D_SPREAD")) ? 1 : 0;
-  // hand-off block: 64 B of words, the partial granules, the export granules (zeroed by one
-  // memset before every launch, a multiple of 16 B from the allocation's start)
+  // hand-off block: 64 B of words (launch epoch, timeout word), the partial granules, the
+  // export granules; zeroed once here -- granule tags carry the launch epoch, so a launch
+  // never matches an earlier launch's granules (a multiple of 16 B from the start)
   const size_t partGr = (size_t)2 * 3 * G * 2, hs = 64 + (partGr + (size_t)nExp * 2) * sizeof(unsigned long long);
   char *blk = nullptr;
   HIPCHK(hipMalloc(&blk, hs));
+  HIPCHK(hipMemset(blk, 0, hs));
   m->mwgAllocs.push_back(blk);
   T.ctr = (unsigned *)blk;
   T.part = (unsigned long long *)(blk + 64);
