@@ -1213,6 +1213,24 @@ __global__ void __launch_bounds__(256) k_exchange_uv(Dims d, double *u, double *
   (h < nU ? u : v)[at(dst)] = code > 0 ? val : -val;
 }
 
+// Several 2-D C-grid vector pairs through the same map in one launch (blockIdx.y = pair):
+// CALC_R_STAR's three EXCH_UV_XY_RL calls (calc_r_star.F:256-257 and the Dh/Exp pairs)
+struct UVPairs {
+  double *u[3], *v[3];
+  int n;
+};
+__global__ void __launch_bounds__(256) k_exchange_uv_pairs(Dims d, UVPairs pr, const long *__restrict__ map, int nU,
+                                                           int nV) {
+  const int h = (int)(blockIdx.x * blockDim.x + threadIdx.x);
+  const int c = (int)blockIdx.y;
+  if (h >= nU + nV || c >= pr.n) return;
+  double *u = pr.u[c], *v = pr.v[c];
+  const long dst = map[2 * h], code = map[2 * h + 1];
+  const long N2 = d.n2 * d.nTiles, s = (code > 0 ? code : -code) - 1;
+  const double val = s < N2 ? u[s] : v[s - N2];
+  (h < nU ? u : v)[dst] = code > 0 ? val : -val;
+}
+
 // EXCH_XY_RL(cg2d_x) + etaN = recip_Bo*cg2d_x (solve_for_pressure.F:316, 377-385) in
 // one pass over every 2-D point; srcOf[q] = interior source of halo point q, or -1.
 __global__ void __launch_bounds__(256) k_exch_eta(Dims d, Fields f, const long *__restrict__ srcOf) {
@@ -1518,6 +1536,18 @@ hipError_t launch_exchange_uv(const Dims &d, double *u, double *v, const long *m
   Dims dz = d;
   dz.n3 = d.n2 * nz;   // per-tile stride of an nz-level field
   hipLaunchKernelGGL(k_exchange_uv, dim3((unsigned)((nU + nV + 255) / 256), nz), dim3(256), 0, s, dz, u, v, map, nU,
+                     nV);
+  return hipGetLastError();
+}
+
+hipError_t launch_exchange_uv_pairs(const Dims &d, double *const *u, double *const *v, int n, const long *map, int nU,
+                                   int nV, hipStream_t s) {
+  if (nU + nV <= 0 || n <= 0) return hipSuccess;
+  if (n > 3) return hipErrorInvalidValue;
+  UVPairs pr{};
+  for (int c = 0; c < n; c++) { pr.u[c] = u[c]; pr.v[c] = v[c]; }
+  pr.n = n;
+  hipLaunchKernelGGL(k_exchange_uv_pairs, dim3((unsigned)((nU + nV + 255) / 256), n), dim3(256), 0, s, d, pr, map, nU,
                      nV);
   return hipGetLastError();
 }

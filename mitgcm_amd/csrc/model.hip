@@ -42,6 +42,8 @@ hipError_t launch_correction(const Dims &, const Params &, const Fields &, hipSt
 hipError_t launch_bump_counter(int *, int, hipStream_t);
 hipError_t launch_exchange_multi(const Dims &, const XFields &, const long *, int, int *, hipStream_t);
 hipError_t launch_exchange_uv(const Dims &, double *, double *, const long *, int, int, int, hipStream_t);
+hipError_t launch_exchange_uv_pairs(const Dims &, double *const *, double *const *, int, const long *, int, int,
+                                   hipStream_t);
 hipError_t launch_exch_eta(const Dims &, const Params &, const Fields &, const long *, bool, int, hipStream_t);
 hipError_t launch_corr_cont(const Dims &, const Params &, const Fields &, int, hipStream_t);
 hipError_t launch_calc_r_star(const Dims &, const Params &, const Fields &, const long *, hipStream_t, bool fuseEtaH = false);
@@ -955,13 +957,9 @@ static hipError_t calc_r_star(mgcm_model *m, bool fuseEtaH = false) {
   const Dims da = all_tiles(m->d);
   hipError_t e = launch_calc_r_star(da, m->p, m->f, m->d_srcOf, m->stream, fuseEtaH);
   if (e != hipSuccess || !m->uvMap) return e;
-  double *pairs[3][2] = {{m->f.rStarFacW, m->f.rStarFacS}, {m->f.rStarDhWDt, m->f.rStarDhSDt},
-                         {m->f.rStarExpW, m->f.rStarExpS}};
-  for (auto &pr : pairs) {
-    e = launch_exchange_uv(da, pr[0], pr[1], m->d_uvAll[0], m->nUvUAll[0], m->nUvVAll[0], 1, m->stream);
-    if (e != hipSuccess) return e;
-  }
-  return hipSuccess;
+  double *us[3] = {m->f.rStarFacW, m->f.rStarDhWDt, m->f.rStarExpW}, *vs[3] = {m->f.rStarFacS, m->f.rStarDhSDt,
+                                                                                 m->f.rStarExpS};
+  return launch_exchange_uv_pairs(da, us, vs, 3, m->d_uvAll[0], m->nUvUAll[0], m->nUvVAll[0], m->stream);
 }
 static hipError_t update_r_star_cg2d(mgcm_model *m) {
   return launch_update_r_star_cg2d(all_tiles(m->d), m->p, m->f, m->d_srcOf, m->stream);
