@@ -1231,6 +1231,35 @@ __global__ void __launch_bounds__(256) k_exchange_uv_pairs(Dims d, UVPairs pr, c
   (h < nU ? u : v)[dst] = code > 0 ? val : -val;
 }
 
+// EXCH2 vector pair (u, v; nz levels, vector map) and the scalar fields x (scalar map) in one
+// launch: blockIdx.z = 0 the pair, z = 1.. field z-1 (the bodies of k_exchange_uv and
+// k_exchange_multi, counter bump included).  DO_FIELDS_BLOCKING_EXCHANGES on a cube/LLC
+// topology and DO_STAGGER_FIELDS_EXCHANGES (u, v and w).
+__global__ void __launch_bounds__(256) k_exchange_mixed(Dims d, double *u, double *v, int nzUV,
+                                                        const long *__restrict__ uvMap, int nU, int nV, XFields x,
+                                                        const long *__restrict__ map, int nHalo, int *ctr) {
+  const int h = (int)(blockIdx.x * blockDim.x + threadIdx.x);
+  const int k = (int)blockIdx.y, z = (int)blockIdx.z;
+  if (ctr && h == 0 && k == 0 && z == 0) { ctr[0] += 1; ctr[1] += 1; }
+  if (z == 0) {
+    if (h >= nU + nV || k >= nzUV) return;
+    const long dst = uvMap[2 * h], code = uvMap[2 * h + 1];
+    const long N2 = d.n2 * d.nTiles, s = (code > 0 ? code : -code) - 1;
+    const long n3 = d.n2 * nzUV, lvl = (long)k * d.n2;
+    auto at = [&](long g) -> long { return (g / d.n2) * n3 + lvl + g % d.n2; };
+    const double val = s < N2 ? u[at(s)] : v[at(s - N2)];
+    (h < nU ? u : v)[at(dst)] = code > 0 ? val : -val;
+    return;
+  }
+  const int fi = z - 1;
+  if (h >= nHalo || fi >= x.n || k >= x.nz[fi]) return;
+  const long dst = map[2 * h], src = map[2 * h + 1];
+  const long dt = dst / d.n2, dl = dst % d.n2, st = src / d.n2, sl = src % d.n2;
+  const long lvl = (long)d.n2 * x.nz[fi];
+  double *a = x.p[fi];
+  a[dt * lvl + (long)k * d.n2 + dl] = a[st * lvl + (long)k * d.n2 + sl];
+}
+
 // EXCH_XY_RL(cg2d_x) + etaN = recip_Bo*cg2d_x (solve_for_pressure.F:316, 377-385) in
 // one pass over every 2-D point; srcOf[q] = interior source of halo point q, or -1.
 __global__ void __launch_bounds__(256) k_exch_eta(Dims d, Fields f, const long *__restrict__ srcOf) {
@@ -1527,6 +1556,16 @@ hipError_t launch_exchange_multi(const Dims &d, const XFields &x, const long *ma
   for (int q = 0; q < x.n; q++) nzMax = x.nz[q] > nzMax ? x.nz[q] : nzMax;
   dim3 blk(256), grd((unsigned)((nHalo > 0 ? nHalo : 1) + 255) / 256, nzMax, x.n);
   hipLaunchKernelGGL(k_exchange_multi, grd, blk, 0, s, d, x, map, nHalo, ctr);
+  return hipGetLastError();
+}
+
+hipError_t launch_exchange_mixed(const Dims &d, double *u, double *v, int nzUV, const long *uvMap, int nU, int nV,
+                                 const XFields &x, const long *map, int nHalo, int *ctr, hipStream_t s) {
+  int nzMax = nzUV;
+  for (int q = 0; q < x.n; q++) nzMax = x.nz[q] > nzMax ? x.nz[q] : nzMax;
+  const int nh = (nU + nV) > nHalo ? nU + nV : nHalo;
+  dim3 blk(256), grd((unsigned)((nh > 0 ? nh : 1) + 255) / 256, nzMax, 1 + x.n);
+  hipLaunchKernelGGL(k_exchange_mixed, grd, blk, 0, s, d, u, v, nzUV, uvMap, nU, nV, x, map, nHalo, ctr);
   return hipGetLastError();
 }
 

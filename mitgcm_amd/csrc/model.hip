@@ -42,6 +42,8 @@ hipError_t launch_correction(const Dims &, const Params &, const Fields &, hipSt
 hipError_t launch_bump_counter(int *, int, hipStream_t);
 hipError_t launch_exchange_multi(const Dims &, const XFields &, const long *, int, int *, hipStream_t);
 hipError_t launch_exchange_uv(const Dims &, double *, double *, const long *, int, int, int, hipStream_t);
+hipError_t launch_exchange_mixed(const Dims &, double *, double *, int, const long *, int, int, const XFields &,
+                                 const long *, int, int *, hipStream_t);
 hipError_t launch_exchange_uv_pairs(const Dims &, double *const *, double *const *, int, const long *, int, int,
                                    hipStream_t);
 hipError_t launch_exch_eta(const Dims &, const Params &, const Fields &, const long *, bool, int, hipStream_t);
@@ -1322,12 +1324,22 @@ static int one_step(mgcm_model *m) {
   }
   if (stagger && tracers) {
     // DO_STAGGER_FIELDS_EXCHANGES (do_stagger_fields_exchanges.F:37-43) + THERMODYNAMICS
-    TIMED(K_EXCH, exchange_uv(m, m->f.uVel, m->f.vVel, m->d.Nr, true) ? hipErrorUnknown : hipSuccess);
-    TIMED(K_EXCH, launch_exchange(m->d, m->f.wVel, m->d_halo, m->nHalo, m->d.Nr, m->stream));
+    if (m->uvMap) {   // u, v through the vector map and w through the scalar map, one launch
+      XFields xw{};
+      xw.p[0] = m->f.wVel; xw.nz[0] = m->d.Nr; xw.n = 1;
+      TIMED(K_EXCH, launch_exchange_mixed(m->d, m->f.uVel, m->f.vVel, m->d.Nr, m->d_uv[1], m->nUvU[1], m->nUvV[1], xw,
+                                          m->d_halo, m->nHalo, nullptr, m->stream));
+    } else {
+      TIMED(K_EXCH, exchange_uv(m, m->f.uVel, m->f.vVel, m->d.Nr, true) ? hipErrorUnknown : hipSuccess);
+      TIMED(K_EXCH, launch_exchange(m->d, m->f.wVel, m->d_halo, m->nHalo, m->d.Nr, m->stream));
+    }
     if (tracers_on(m, m->stream)) return -1;
   }
-  if (m->uvMap) TIMED(K_EXCH, exchange_uv(m, m->f.uVel, m->f.vVel, m->d.Nr, true) ? hipErrorUnknown : hipSuccess);
-  TIMED(K_EXCH, launch_exchange_multi(m->d, blocking_fields(m), m->d_halo, m->nHalo, m->d_ctr, m->stream));
+  if (m->uvMap)   // the vector pair and the scalar fields in one launch
+    TIMED(K_EXCH, launch_exchange_mixed(m->d, m->f.uVel, m->f.vVel, m->d.Nr, m->d_uv[1], m->nUvU[1], m->nUvV[1],
+                                        blocking_fields(m), m->d_halo, m->nHalo, m->d_ctr, m->stream));
+  else
+    TIMED(K_EXCH, launch_exchange_multi(m->d, blocking_fields(m), m->d_halo, m->nHalo, m->d_ctr, m->stream));
   return 0;
 }
 
