@@ -1571,11 +1571,26 @@ __global__ void __launch_bounds__(VT_NT) k_mom_vi_march(Dims d, Params p, Fields
 // The halo ring outside the DYNAMICS range (i or j outside 0..sN+1): no tendency, but
 // ADAMS_BASHFORTH2 runs over the whole slab (gU = abFac*(0 - guNm1), guNm1 = 0), as
 // k_mom_step does there.
+// One thread per ring point (blockIdx.y = level, blockIdx.z = tile): the OLy-1 full rows
+// below and above, then the OLx-1 columns left and right of the rows 0..sNy+1.
+__device__ __forceinline__ int mom_halo_ring_count(const Dims &d) {
+  return 2 * (d.OLy - 1) * d.nx + (d.sNy + 2) * 2 * (d.OLx - 1);
+}
 __global__ void __launch_bounds__(256) k_mom_halo_ab(Dims d, Params p, Fields f, const int *iterPtr) {
-  MG_PLANE(1 - d.OLx, d.nx, 1 - d.OLy, d.ny, z)
-  const int t = d.t0 + z / d.Nr, k = z % d.Nr + 1;
-  if (i > d.sNx + d.OLx || j > d.sNy + d.OLy) return;
-  if (i >= 0 && i <= d.sNx + 1 && j >= 0 && j <= d.sNy + 1) return;
+  const int r = (int)(blockIdx.x * blockDim.x + threadIdx.x);
+  if (r >= mom_halo_ring_count(d)) return;
+  const int t = d.t0 + (int)blockIdx.z, k = (int)blockIdx.y + 1;
+  const int nb = (d.OLy - 1) * d.nx, cw = 2 * (d.OLx - 1);
+  int i, j;
+  if (r < 2 * nb) {
+    const int r2 = r < nb ? r : r - nb;
+    j = (r < nb ? 1 - d.OLy : d.sNy + 2) + r2 / d.nx;
+    i = 1 - d.OLx + r2 % d.nx;
+  } else {
+    const int r2 = r - 2 * nb, c = r2 % cw;
+    j = r2 / cw;
+    i = c < d.OLx - 1 ? 1 - d.OLx + c : d.sNx + 2 + (c - (d.OLx - 1));
+  }
   const int myIter = *iterPtr;
   const double abFac = (myIter == p.nIter0 && p.nIter0 == 0) ? 0.0 : 0.5 + p.abEps;
   const long q3 = MG_I3(d, i, j, k, t);
@@ -1712,8 +1727,10 @@ hipError_t launch_mom_step(const Dims &d, const Params &p, const Fields &f, cons
       hipLaunchKernelGGL(k_mom_vi_tiled, dim3((unsigned)(nbx * nby * d.nT * nkc)), dim3(VT_NT), 0, s, d, p, f, iterPtr, BX,
                          BY, nbx, nby, KC, nkc);
     }
-    hipLaunchKernelGGL(k_mom_halo_ab, dim3(mg_plane_blocks(d.nx, d.ny, d.nT * d.Nr)), dim3(MG_PLANE_THREADS), 0, s, d, p,
-                       f, iterPtr);
+    const int ring = 2 * (d.OLy - 1) * d.nx + (d.sNy + 2) * 2 * (d.OLx - 1);
+    if (ring > 0)
+      hipLaunchKernelGGL(k_mom_halo_ab, dim3((unsigned)((ring + 255) / 256), d.Nr, d.nT), dim3(256), 0, s, d, p, f,
+                         iterPtr);
   } else if (p.vectorInvariantMomentum)
     hipLaunchKernelGGL(k_mom_step<true>, dim3(mg_plane_blocks(d.nx, d.ny, d.nT * d.Nr)), dim3(MG_PLANE_THREADS), 0, s,
                        d, p, f, iterPtr);
