@@ -1402,7 +1402,11 @@ static int ovl_trial(mgcm_model *m) {
   size_t total = 0;
   for (auto &pr : parts) total += (pr.second + 255) & ~(size_t)255;
   char *save = nullptr;
-  HIPCHK(hipMalloc(&save, total));
+  if (hipMalloc(&save, total) != hipSuccess) {   // no room for the copy: keep the overlap on, untimed
+    (void)hipGetLastError();
+    m->ovlDecided = true;
+    return 0;
+  }
   size_t off = 0;
   for (auto &pr : parts) {
     HIPCHK(hipMemcpyAsync(save + off, pr.first, pr.second, hipMemcpyDeviceToDevice, m->stream));
