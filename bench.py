@@ -175,18 +175,34 @@ def cpu_baseline(config, seconds):
                       % (n, config, dt)}
 
 
-def pmc_traffic(path, kernel_prefix):
-    """HBM bytes per launch of the dominant kernel from the committed PMC passes
-    (FETCH_SIZE x2 + WRITE_SIZE, tools/pmc_summary.py); None when absent."""
+def pmc_traffic(path, kernel_keys):
+    """HBM bytes per launch from the committed PMC passes (FETCH_SIZE x2 + WRITE_SIZE,
+    tools/pmc_summary.py), summed over every kernel whose name contains one of
+    `kernel_keys` (the launches of one timed block); (total, {kernel: bytes}) or
+    (None, {}) when absent."""
     try:
         import json as _j
         ks = _j.load(open(path))["kernels"]
     except (OSError, ValueError, KeyError):
-        return None
-    for k, v in ks.items():
-        if kernel_prefix in k:
-            return v["hbm_bytes_per_launch"]
-    return None
+        return None, {}
+    if isinstance(kernel_keys, str):
+        kernel_keys = (kernel_keys,)
+    per = {k: v["hbm_bytes_per_launch"] for k, v in ks.items() if any(key in k for key in kernel_keys)}
+    return (sum(per.values()) if per else None), per
+
+
+def default_pmc_summary(config):
+    """The newest committed PMC summary of this workload (profiles/r0N/<tag>/)."""
+    tag = PMC_TAG.get(config, config)
+    for rnd in ("r03", "r02"):
+        p = os.path.join(ROOT, "profiles", rnd, tag, "pmc_summary.json")
+        if os.path.exists(p):
+            return p
+    return os.path.join(ROOT, "profiles", "r03", tag, "pmc_summary.json")
+
+
+def cg_kernel_key(m):
+    return "k_cg2d_" + m.cg2d_kernel().replace("_ref", "")
 
 
 def main():
@@ -277,8 +293,18 @@ def main():
     eta = m.get("etaN")
     assert np.isfinite(eta).all() and stats["cg2d_last_res"] < 1e-6, stats
 
+    # every solve of both batches converged without a hand-off timeout (numIters = -1 marks
+    # a multi-workgroup CG2D that gave up; a graph batch would otherwise carry on silently)
+    failed = [i for i in iters + iters_t if i < 0]
+    if failed:
+        raise SystemExit("bench: %d of %d CG2D solves failed (numIters < 0): %s" % (len(failed), len(iters + iters_t),
+                                                                                   iters + iters_t))
     if a.pmc_summary is None:
-        a.pmc_summary = os.path.join(ROOT, "profiles", "r02", PMC_TAG.get(a.config, a.config), "pmc_summary.json")
+        a.pmc_summary = default_pmc_summary(a.config)
+    cg_traffic, _ = pmc_traffic(a.pmc_summary, cg_kernel_key(m))
+    # the momentum block's launches (launch_mom_step: del2uv, the MOM_FLUXFORM / MOM_VECINV
+    # kernel, the VI halo AB pass, the CD scheme, the implicit viscosity columns)
+    mom_traffic, mom_traffic_per = pmc_traffic(a.pmc_summary, ("k_del2uv", "k_mom_", "k_cd_scheme"))
     model_days = a.steps * dt_clock / 86400.0
     copies = 1 if shard else world   # independent model integrations in the job
     value = copies * model_days / elapsed
@@ -334,7 +360,7 @@ def main():
         # profiles/r02/ocean90/cg2d_geometry.txt)
         "roofline": {"bound": "latency", "kernel": cg_kernel, "achieved": achieved, "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
-                     "traffic": pmc_traffic(a.pmc_summary, cg_kernel),
+                     "traffic": cg_traffic,
                      "traffic_unit": "bytes per launch (rocprofv3 --pmc, %s)" % os.path.relpath(a.pmc_summary, ROOT),
                      "bytes_per_launch": bytes_per_launch, "launch_ms": cg_ms, "launches": cg_n,
                      "us_per_iteration": us_per_it, "cus_used": cus,
@@ -346,7 +372,8 @@ def main():
                          "achieved": mom_gbs,
                          "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": mom_gbs / HBM_PEAK_GBS,
                          "bytes_per_point": mom_bpp, "launch_ms": mom_ms,
-                         "traffic": pmc_traffic(a.pmc_summary, "k_mom_")},
+                         "traffic": mom_traffic,
+                         "traffic_per_kernel": {k.split("(")[0]: v for k, v in mom_traffic_per.items()}},
     }
     if rank == 0 and world == 1 and not a.no_cpu_baseline:   # the CPU baseline is an N=1 line
         out["cpu_baseline"] = cpu_baseline(a.config, a.cpu_seconds)

@@ -43,6 +43,11 @@ const char *mgcm_last_error(void);
 int mgcm_set_param(mgcm_model *m, const char *name, double value);
 double mgcm_get_param(mgcm_model *m, const char *name);
 
+/* The device's iteration counter (myIter: AB2's first step, the CD scheme's start),
+ * written in stream order without a host synchronisation (mgcm_set_param("myIter")
+ * synchronises). */
+int mgcm_set_iter(mgcm_model *m, int myIter);
+
 /* Host <-> device copies of named fields (DYNVARS/GRID/CG2D/FFIELDS names,
  * e.g. "uVel", "hFacW", "aW2d", "fu").  count = number of doubles. */
 int mgcm_put(mgcm_model *m, const char *name, const double *host, long count);
@@ -194,12 +199,20 @@ void mgcm_amd_setup_(const int *sNx, const int *sNy, const int *OLx, const int *
                      const int *nSx, const int *nSy, const int *nProcs, const int *nThreads);
 /* One PARAMS.h parameter (LOGICAL as 0/1). */
 void mgcm_amd_param_(const char *name, const double *value, size_t len);
-/* Register a COMMON-block array of `count` doubles as device field `name`; isStatic:
- * upload once at init (phiRef(2Nr+1) binds the device's phiRefC). */
-void mgcm_amd_bind_(const char *name, double *array, const int *count, const int *isStatic, size_t len);
+/* Register a COMMON-block array of `count` doubles as device field `name`; kind 1 static
+ * (uploaded once at init), 0 state, 2 host input (uploaded before every DO_OCEANIC_PHYS);
+ * phiRef(2Nr+1) binds the device's phiRefC. */
+void mgcm_amd_bind_(const char *name, double *array, const int *count, const int *kind, size_t len);
 /* Upload the bound arrays and finish the device set-up. */
 void mgcm_amd_init_(const int *myIter);
-/* Routine drop-ins: bound state uploaded before, downloaded after. */
+/* The device-authoritative mirror (fortran_abi.hip): bring the state down for a host
+ * reader / push a host-modified state up; whole-array copies made so far. */
+void mgcm_amd_host_sync_(const int *myThid);
+void mgcm_amd_device_sync_(const int *myThid);
+void mgcm_amd_transfer_stats_(int *nUploads, int *nDownloads, double *bytesUp, double *bytesDown);
+/* Routine drop-ins: during initialisation the bound state is uploaded before and
+ * downloaded after each; from the first DO_OCEANIC_PHYS / THERMODYNAMICS / DYNAMICS on, the
+ * device copy is authoritative (forcing up every step, state down for host readers). */
 void do_oceanic_phys_amd_(const double *myTime, const int *myIter, const int *myThid);     /* do_oceanic_phys.F:43 */
 void thermodynamics_amd_(const double *myTime, const int *myIter, const int *myThid);      /* thermodynamics.F:25 */
 void dynamics_amd_(const double *myTime, const int *myIter, const int *myThid);            /* dynamics.F:21 */

@@ -31,6 +31,7 @@ def lib():
         "mgcm_destroy": (None, [vp]),
         "mgcm_last_error": (cs, []),
         "mgcm_set_param": (ci, [vp, cs, cd]),
+        "mgcm_set_iter": (ci, [vp, ci]),
         "mgcm_get_param": (cd, [vp, cs]),
         "mgcm_put": (ci, [vp, cs, PD, cl]),
         "mgcm_get": (ci, [vp, cs, PD, cl]),
@@ -94,7 +95,8 @@ EXPORTS = ["mgcm_create", "mgcm_destroy", "mgcm_last_error", "mgcm_set_param", "
            "thermodynamics_amd_", "dynamics_amd_", "solve_for_pressure_amd_", "momentum_correction_step_amd_",
            "integr_continuity_amd_", "do_fields_blocking_exchanges_amd_", "exch_xy_rl_amd_", "exch_xyz_rl_amd_",
            "exch_uv_xy_rl_amd_", "exch_uv_xyz_rl_amd_", "global_sum_tile_rl_amd_",
-           "mgcm_update_r_star", "mgcm_calc_r_star", "update_r_star_amd_", "update_cg2d_amd_", "calc_r_star_amd_"]
+           "mgcm_update_r_star", "mgcm_calc_r_star", "update_r_star_amd_", "update_cg2d_amd_", "calc_r_star_amd_",
+           "mgcm_set_iter", "mgcm_amd_host_sync_", "mgcm_amd_device_sync_", "mgcm_amd_transfer_stats_"]
 
 
 def check(rc, what):

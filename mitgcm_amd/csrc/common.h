@@ -59,6 +59,7 @@ struct Params {
   int cg2dMaxIters, cg2dUseMinResSol, cg2dNormaliseRHS, nIter0;
   int cg2dUseFMA;   // CG2D in fused multiply-adds (device-order oracle: the same fma chains)
   int useSRCGSolver;   // CG2D_SR (cg2d_sr.F): single-reduction CG, k_cg2d_bxy only
+  int cg2dRefOrder;    // CG2D sums in the reference's order (per-tile sequential, tile order): parity mode
   // 3-D / tracer path
   double gravity, gravitySign, rhoNil, tAlpha, sBeta, ivdc_kappa, diffKhT, diffKrT, deltaTtracer;
   double recip_rSphere;

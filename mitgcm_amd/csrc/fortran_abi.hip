@@ -7,21 +7,29 @@
 // CHARACTER lengths appended as size_t -- amdflang's external convention).
 //
 // Coherence model (the "device mirror" keyed by COMMON-block address):
-//   * MGCM_AMD_BIND(name, array, count, isStatic) registers a host array -- a COMMON-block member
+//   * MGCM_AMD_BIND(name, array, count, kind) registers a host array -- a COMMON-block member
 //     of DYNVARS.h / GRID.h / SURFACE.h / FFIELDS.h / CG2D.h / GMREDI.h -- under the device
-//     field of the same name;
-//   * static arrays (grid metrics, masks that never change) are uploaded once, by
-//     MGCM_AMD_INIT;
-//   * around every routine drop-in (DYNAMICS_AMD, ...) the bound state arrays are uploaded
-//     before and downloaded after, so the host copy stays authoritative between calls and
-//     any host routine that is not shadowed (LOAD_FIELDS_DRIVER, UPDATE_R_STAR, MONITOR,
-//     pickup I/O) sees and produces ordinary COMMON-block data.
-// The copies are PCIe traffic around each routine; the resident, graph-captured path
-// (mgcm_forward_step) is the performance path, and the drop-ins are its parity/adoption
-// path: the device work inside each call is the same kernels.
+//     field of the same name, in one of three kinds: 1 static (grid metrics, masks: uploaded
+//     once, by MGCM_AMD_INIT), 0 state, 2 host input (what the host's LOAD_FIELDS_DRIVER
+//     writes every step: the forcing fields);
+//   * while the model initialises (INITIALISE_VARIA runs UPDATE_CG2D, CALC_R_STAR,
+//     UPDATE_R_STAR, INTEGR_CONTINUITY through the drop-ins, interleaved with host INI_*
+//     routines) the host copy is authoritative: each drop-in uploads the state before and
+//     downloads it after;
+//   * from the first DO_OCEANIC_PHYS / THERMODYNAMICS / DYNAMICS -- routines only
+//     FORWARD_STEP calls -- the device copy is authoritative: the state is uploaded once,
+//     each step uploads only the host input (before DO_OCEANIC_PHYS), and the state comes
+//     back only after the DO_FIELDS_BLOCKING_EXCHANGES of a step whose end a host routine
+//     reads (MONITOR, DO_THE_MODEL_IO, DO_WRITE_PICKUP: monitorFreq, dumpFreq, chkPtFreq,
+//     pChkPtFreq by the reference's DIFFERENT_MULTIPLE test, and the last iteration
+//     nEndIter), or when the host asks (MGCM_AMD_HOST_SYNC; MGCM_AMD_DEVICE_SYNC pushes a
+//     host-modified state back).  A step in between moves the forcing fields (6 2-D arrays)
+//     and nothing else across PCIe.
+// mgcm_amd_transfer_stats_ counts the copies, so a host can check the schedule.
 //
 // Errors: no return channel exists in the reference (it prints and STOPs), so every
 // failure prints "ABNORMAL END: <routine>: <reason>" and aborts.
+#include <cmath>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -36,8 +44,15 @@ struct Bound {
   std::string name;   // device field
   double *host;
   long count;         // doubles moved
-  bool isStatic;
+  int kind;           // 0 state, 1 static, 2 host input (MGCM_AMD_BIND)
   int stride = 1, off = 0;   // host element q*stride + off <-> device element q
+};
+
+// When a host routine reads the state at the end of a step (the device-authoritative
+// mirror downloads it then): the frequencies of PARAMS.h, in seconds, and nEndIter.
+struct Readers {
+  double monitorFreq = 0.0, dumpFreq = 0.0, chkPtFreq = 0.0, pChkPtFreq = 0.0, deltaTClock = 0.0;
+  int nEndIter = -1;
 };
 
 struct FortranSide {
@@ -45,6 +60,13 @@ struct FortranSide {
   int dims[7] = {0, 0, 0, 0, 0, 0, 0};   // sNx sNy OLx OLy Nr nSx nSy
   std::vector<Bound> bound;
   bool ready = false;
+  bool deviceAuth = false;   // the device copy of the state is authoritative (time loop)
+  long devIter = -1;         // the iteration counter last written to the device (-1: unknown)
+  double lastTime = 0.0;     // myTime / myIter of the latest routine drop-in
+  int lastIter = 0;
+  Readers rd;
+  long nUp = 0, nDown = 0;   // copies of whole bound arrays, for mgcm_amd_transfer_stats_
+  double bytesUp = 0.0, bytesDown = 0.0;
 };
 FortranSide g;
 
@@ -64,14 +86,20 @@ mgcm_model *model(const char *where) {
   return g.m;
 }
 
+// The device's iteration counter (AB2's first step, the CD scheme's start), written only
+// when it changes (FORWARD_STEP advances myIter after DYNAMICS, forward_step.F:806), in
+// stream order: no host synchronisation.
 void set_iter(const char *where, int myIter) {
-  if (mgcm_set_param(g.m, "myIter", (double)myIter)) die(where);
+  if (g.devIter == myIter) return;
+  if (mgcm_set_iter(g.m, myIter)) die(where);
+  g.devIter = myIter;
 }
 
-void upload(const char *where, bool statics) {
+// kinds: bit k set = move the arrays of kind k
+void upload(const char *where, unsigned kinds) {
   std::vector<double> tmp;
   for (auto &b : g.bound) {
-    if (b.isStatic != statics) continue;
+    if (!((kinds >> b.kind) & 1u)) continue;
     const double *src = b.host;
     if (b.stride != 1) {
       tmp.resize(b.count);
@@ -79,6 +107,8 @@ void upload(const char *where, bool statics) {
       src = tmp.data();
     }
     if (mgcm_put(g.m, b.name.c_str(), src, b.count)) die(where);
+    g.nUp++;
+    g.bytesUp += 8.0 * b.count;
   }
 }
 
@@ -86,7 +116,9 @@ void download(const char *where) {
   if (mgcm_sync(g.m)) die(where);
   std::vector<double> tmp;
   for (auto &b : g.bound) {
-    if (b.isStatic) continue;
+    if (b.kind != 0) continue;   // static and host-input arrays are never written on the device
+    g.nDown++;
+    g.bytesDown += 8.0 * b.count;
     if (b.stride == 1) {
       if (mgcm_get(g.m, b.name.c_str(), b.host, b.count)) die(where);
       continue;
@@ -97,14 +129,54 @@ void download(const char *where) {
   }
 }
 
-// One routine drop-in: state in, the device routine, state out.
-void routine(const char *where, int (*fn)(mgcm_model *), int myIter) {
+constexpr unsigned K_STATE = 1u << 0, K_STATIC = 1u << 1, K_INPUT = 1u << 2;
+
+// The time loop has begun (a routine only FORWARD_STEP calls): the host's state goes up
+// once and the device copy becomes the authoritative one.
+void enter_time_loop(const char *where) {
+  if (g.deviceAuth) return;
+  upload(where, K_STATE | K_INPUT);
+  g.deviceAuth = true;
+}
+
+// One routine drop-in.  Host-authoritative (initialisation): state in, the device
+// routine, state out.  Device-authoritative: the host input first when `input`.
+void routine(const char *where, int (*fn)(mgcm_model *), int myIter, double myTime, bool input = false) {
   model(where);
   if (!g.ready) die(where, "called before MGCM_AMD_INIT");
-  upload(where, false);
+  g.lastIter = myIter;
+  g.lastTime = myTime;
+  if (!g.deviceAuth) {
+    upload(where, K_STATE | K_INPUT);
+    set_iter(where, myIter);
+    if (fn(g.m)) die(where);
+    download(where);
+    return;
+  }
+  if (input) upload(where, K_INPUT);
   set_iter(where, myIter);
   if (fn(g.m)) die(where);
-  download(where);
+}
+
+// eesupp/src/different_multiple.F: is val1 the step nearest to a multiple of freq?
+bool different_multiple(double freq, double val1, double step) {
+  if (freq == 0.0) return false;
+  if (fabs(step) > freq) return true;
+  const double v1 = val1, v2 = val1 - step, v3 = val1 + step;
+  const double v4 = nearbyint(v1 / freq) * freq;
+  const double d1 = v1 - v4, d2 = v2 - v4, d3 = v3 - v4;
+  return fabs(d1) < fabs(d2) && fabs(d1) <= fabs(d3);
+}
+
+// Does a host routine read the state at the end of this step?  MONITOR
+// (monitor.F:48), DO_THE_MODEL_IO (do_the_model_io.F:106), DO_WRITE_PICKUP
+// (do_write_pickup.F:61-63, modelEnd) -- a superset is harmless, a miss is not.
+bool host_reads_state(double myTime, int myIter) {
+  const Readers &r = g.rd;
+  return myIter == r.nEndIter || different_multiple(r.monitorFreq, myTime, r.deltaTClock) ||
+         different_multiple(r.dumpFreq, myTime, r.deltaTClock) ||
+         different_multiple(r.chkPtFreq, myTime, r.deltaTClock) ||
+         different_multiple(r.pChkPtFreq, myTime, r.deltaTClock);
 }
 
 const Bound *bound_at(const double *p) {
@@ -137,17 +209,26 @@ void mgcm_amd_setup_(const int *sNx, const int *sNy, const int *OLx, const int *
 void mgcm_amd_param_(const char *name, const double *value, size_t len) {
   model("MGCM_AMD_PARAM");
   const std::string n = fstr(name, len);
+  // the host-side schedule of state readers stays here (no device meaning)
+  Readers &r = g.rd;
+  if (n == "monitorFreq") { r.monitorFreq = *value; return; }
+  if (n == "dumpFreq") { r.dumpFreq = *value; return; }
+  if (n == "chkPtFreq") { r.chkPtFreq = *value; return; }
+  if (n == "pChkPtFreq") { r.pChkPtFreq = *value; return; }
+  if (n == "nEndIter") { r.nEndIter = (int)*value; return; }
+  if (n == "deltaTClock") r.deltaTClock = *value;
   if (mgcm_set_param(g.m, n.c_str(), *value)) die("MGCM_AMD_PARAM");
   g.ready = false;
 }
 
 /* Register a host array (a COMMON-block member) of `count` doubles as the device field
- * `name` (same name).  1-D profiles may be shorter than the device's Nr+1 (drF(Nr)).
+ * `name` (same name), of kind 0 (state), 1 (static) or 2 (host input), see above.  1-D profiles may be shorter than the device's Nr+1 (drF(Nr)).
  * phiRef(2*Nr+1) of set_ref_state.F is bound as the device's phiRefC = phiRef(2k). */
-void mgcm_amd_bind_(const char *name, double *array, const int *count, const int *isStatic, size_t len) {
+void mgcm_amd_bind_(const char *name, double *array, const int *count, const int *kind, size_t len) {
   model("MGCM_AMD_BIND");
   std::string n = fstr(name, len);
-  Bound nb{n, array, *count, *isStatic != 0};
+  if (*kind < 0 || *kind > 2) die("MGCM_AMD_BIND", "kind must be 0 (state), 1 (static) or 2 (host input)");
+  Bound nb{n, array, *count, *kind};
   if (n == "phiRef") {
     const int Nr = g.dims[4];
     if (*count != 2 * Nr + 1) die("MGCM_AMD_BIND", "phiRef must have 2*Nr+1 entries");
@@ -173,34 +254,61 @@ void mgcm_amd_bind_(const char *name, double *array, const int *count, const int
 }
 
 /* Upload every bound array and finish the device set-up (mgcm_init); the host state
- * stays authoritative: anything mgcm_init derives on the device is overwritten by the
- * next routine's upload. */
+ * stays authoritative until the time loop: anything mgcm_init derives on the device is
+ * overwritten by the host's state again. */
 void mgcm_amd_init_(const int *myIter) {
   model("MGCM_AMD_INIT");
-  upload("MGCM_AMD_INIT", true);
-  upload("MGCM_AMD_INIT", false);
-  set_iter("MGCM_AMD_INIT", *myIter);
+  upload("MGCM_AMD_INIT", K_STATIC | K_STATE | K_INPUT);
+  if (mgcm_set_param(g.m, "myIter", (double)*myIter)) die("MGCM_AMD_INIT");
   if (mgcm_init(g.m)) die("MGCM_AMD_INIT");
-  upload("MGCM_AMD_INIT", false);
-  if (mgcm_sync(g.m)) die("MGCM_AMD_INIT");
+  upload("MGCM_AMD_INIT", K_STATE | K_INPUT);
+  if (mgcm_set_param(g.m, "myIter", (double)*myIter)) die("MGCM_AMD_INIT");
+  g.devIter = *myIter;
+  g.deviceAuth = false;
   g.ready = true;
+}
+
+/* The host reads the state now (a host routine outside the shadowed set): the device
+ * copy comes down if it is the authoritative one. */
+void mgcm_amd_host_sync_(const int *myThid) {
+  (void)myThid;
+  model("MGCM_AMD_HOST_SYNC");
+  if (g.ready && g.deviceAuth) download("MGCM_AMD_HOST_SYNC");
+}
+
+/* The host has changed the state (e.g. re-read a pickup): it goes up to the device. */
+void mgcm_amd_device_sync_(const int *myThid) {
+  (void)myThid;
+  model("MGCM_AMD_DEVICE_SYNC");
+  if (g.ready && g.deviceAuth) upload("MGCM_AMD_DEVICE_SYNC", K_STATE | K_INPUT);
+}
+
+/* Whole-array copies so far (uploads, downloads) and their bytes. */
+void mgcm_amd_transfer_stats_(int *nUploads, int *nDownloads, double *bytesUp, double *bytesDown) {
+  *nUploads = (int)g.nUp;
+  *nDownloads = (int)g.nDown;
+  *bytesUp = g.bytesUp;
+  *bytesDown = g.bytesDown;
 }
 
 // ------------------------------------------------------------ routine drop-ins
 /* SUBROUTINE DO_OCEANIC_PHYS(myTime, myIter, myThid)     model/src/do_oceanic_phys.F:43 */
 void do_oceanic_phys_amd_(const double *myTime, const int *myIter, const int *myThid) {
-  (void)myTime; (void)myThid;
-  routine("DO_OCEANIC_PHYS_AMD", mgcm_oceanic_phys, *myIter);
+  (void)myThid;
+  enter_time_loop("DO_OCEANIC_PHYS_AMD");
+  routine("DO_OCEANIC_PHYS_AMD", mgcm_oceanic_phys, *myIter, *myTime, true);
 }
 /* SUBROUTINE THERMODYNAMICS(myTime, myIter, myThid)      model/src/thermodynamics.F:25 */
 void thermodynamics_amd_(const double *myTime, const int *myIter, const int *myThid) {
-  (void)myTime; (void)myThid;
-  routine("THERMODYNAMICS_AMD", mgcm_tracer_step, *myIter);
+  (void)myThid;
+  enter_time_loop("THERMODYNAMICS_AMD");
+  routine("THERMODYNAMICS_AMD", mgcm_tracer_step, *myIter, *myTime);
 }
 /* SUBROUTINE DYNAMICS(myTime, myIter, myThid)            model/src/dynamics.F:21 */
 void dynamics_amd_(const double *myTime, const int *myIter, const int *myThid) {
-  (void)myTime; (void)myThid;
-  routine("DYNAMICS_AMD", mgcm_dynamics, *myIter);
+  (void)myThid;
+  enter_time_loop("DYNAMICS_AMD");
+  routine("DYNAMICS_AMD", mgcm_dynamics, *myIter, *myTime);
 }
 /* SUBROUTINE UPDATE_R_STAR(useLatest, myTime, myIter, myThid)   model/src/update_r_star.F:6
  * useLatest = .TRUE. (forward_step.F:838): the new r* factors and hFac, and UPDATE_CG2D's
@@ -209,8 +317,8 @@ void dynamics_amd_(const double *myTime, const int *myIter, const int *myThid) {
  * forward_step.F:469-477) restores the hFac of the previous step's end, which the mirror
  * already holds: nothing to do. */
 void update_r_star_amd_(const int *useLatest, const double *myTime, const int *myIter, const int *myThid) {
-  (void)myTime; (void)myThid;
-  if (*useLatest) routine("UPDATE_R_STAR_AMD", mgcm_update_r_star, *myIter);
+  (void)myThid;
+  if (*useLatest) routine("UPDATE_R_STAR_AMD", mgcm_update_r_star, *myIter, *myTime);
 }
 /* SUBROUTINE UPDATE_CG2D(myTime, myIter, myThid)         model/src/update_cg2d.F:7
  * Folded into UPDATE_R_STAR_AMD(.TRUE.), which FORWARD_STEP calls just before it. */
@@ -221,37 +329,43 @@ void update_cg2d_amd_(const double *myTime, const int *myIter, const int *myThid
 /* SUBROUTINE CALC_R_STAR(etaFld, myTime, myIter, myThid)  model/src/calc_r_star.F:10
  * FORWARD_STEP passes etaH (forward_step.F:976): the bound array. */
 void calc_r_star_amd_(const double *etaFld, const double *myTime, const int *myIter, const int *myThid) {
-  (void)myTime; (void)myThid;
+  (void)myThid;
   const Bound *b = bound_at(etaFld);
   if (!b || b->name != "etaH") die("CALC_R_STAR_AMD", "etaFld must be the bound etaH");
-  routine("CALC_R_STAR_AMD", mgcm_calc_r_star, *myIter);
+  routine("CALC_R_STAR_AMD", mgcm_calc_r_star, *myIter, *myTime);
 }
 /* SUBROUTINE SOLVE_FOR_PRESSURE(myTime, myIter, myThid)  model/src/solve_for_pressure.F:7 */
 void solve_for_pressure_amd_(const double *myTime, const int *myIter, const int *myThid) {
-  (void)myTime; (void)myThid;
-  routine("SOLVE_FOR_PRESSURE_AMD", mgcm_solve_for_pressure, *myIter);
+  (void)myThid;
+  routine("SOLVE_FOR_PRESSURE_AMD", mgcm_solve_for_pressure, *myIter, *myTime);
 }
 /* SUBROUTINE MOMENTUM_CORRECTION_STEP(myTime, myIter, myThid)
  *                                                   model/src/momentum_correction_step.F:7 */
 void momentum_correction_step_amd_(const double *myTime, const int *myIter, const int *myThid) {
-  (void)myTime; (void)myThid;
-  routine("MOMENTUM_CORRECTION_STEP_AMD", mgcm_momentum_correction_step, *myIter);
+  (void)myThid;
+  routine("MOMENTUM_CORRECTION_STEP_AMD", mgcm_momentum_correction_step, *myIter, *myTime);
 }
 /* SUBROUTINE INTEGR_CONTINUITY(uFld, vFld, myTime, myIter, myThid)
  *                                                   model/src/integr_continuity.F:13
  * FORWARD_STEP passes uVel, vVel (forward_step.F:955): the bound arrays. */
 void integr_continuity_amd_(const double *uFld, const double *vFld, const double *myTime, const int *myIter,
                             const int *myThid) {
-  (void)myTime; (void)myThid;
+  (void)myThid;
   const Bound *bu = bound_at(uFld), *bv = bound_at(vFld);
   if (!bu || !bv || bu->name != "uVel" || bv->name != "vVel")
     die("INTEGR_CONTINUITY_AMD", "uFld, vFld must be the bound uVel, vVel");
-  routine("INTEGR_CONTINUITY_AMD", mgcm_integr_continuity, *myIter);
+  routine("INTEGR_CONTINUITY_AMD", mgcm_integr_continuity, *myIter, *myTime);
 }
 /* SUBROUTINE DO_FIELDS_BLOCKING_EXCHANGES(myThid)   model/src/do_fields_blocking_exchanges.F:7 */
+/* The last device routine of a step: the state comes down when a host routine reads it
+ * next (MONITOR / DO_THE_MODEL_IO / DO_WRITE_PICKUP at this step's end time, known from
+ * the step's earlier drop-ins, which FORWARD_STEP calls with the advanced myTime). */
 void do_fields_blocking_exchanges_amd_(const int *myThid) {
   (void)myThid;
-  routine("DO_FIELDS_BLOCKING_EXCHANGES_AMD", mgcm_blocking_exchanges, (int)mgcm_get_param(model("X"), "myIter"));
+  const int it = g.lastIter;
+  const double t = g.lastTime;
+  routine("DO_FIELDS_BLOCKING_EXCHANGES_AMD", mgcm_blocking_exchanges, it, t);
+  if (g.deviceAuth && host_reads_state(t, it)) download("DO_FIELDS_BLOCKING_EXCHANGES_AMD");
 }
 
 // -------------------------------------------------- exchanges and global sums

@@ -114,7 +114,7 @@ __device__ __forceinline__ bool gran_get(gu64 *g, unsigned tag, double &v) {
 // Launch epochs: ctr[0] holds the epoch, read by every part at its start and advanced by
 // part 0 after the last hand-off (every part has read it by then); a granule's tag is
 // (epoch mod 2^16) << 16 | phase, so no memset is needed between launches.  The timeout
-// word ctr[1] holds epoch + 1 of a launch that gave up.
+// word ctr[1] holds epoch + 1 of a launch that gave up (the epoch then advances by 2).
 __device__ __forceinline__ unsigned mw_tag(unsigned ep, int phase) { return ((ep & 0xffffu) << 16) | (unsigned)phase; }
 // bounded spin: after ~2^22 passes every part gives up (timeout word), so no wave hangs
 __device__ __forceinline__ bool spin_fail(unsigned &spins, gu32 *tmo, unsigned ep) {
@@ -445,7 +445,10 @@ __global__ void __launch_bounds__(MW_NT) k_cg2d_mwg(Dims d, Params p, Fields f, 
     const bool tmo = __hip_atomic_load((gu32 *)T.ctr + 1, RLX_AGENT) == ep + 1u;
     R.numIters = (ok && !tmo) ? actualIts : -1;   // -1: a grid hand-off timed out
     R.nIterMin = -1;
-    __hip_atomic_store((gu32 *)T.ctr, ep + 1u, RLX_AGENT);   // the next launch's epoch
+    // the next launch's epoch; after a timeout it skips one, so a part of this launch that
+    // starts late (reading ep + 1, tagging with it, failing into the timeout word as ep + 2)
+    // can neither match the next launch's tags nor fail it
+    __hip_atomic_store((gu32 *)T.ctr, R.numIters < 0 ? ep + 2u : ep + 1u, RLX_AGENT);
   }
 #undef LO
 #undef HI

@@ -103,6 +103,32 @@ __device__ __forceinline__ double block_max(double v, double *red, int slot) {
   return row_max16(red[slot * CG_WAVES + (lane & 15)]);
 }
 
+// GLOBAL_SUM_TILE_RL in the reference's own order (cg2d.F:211-243 / 305-337 +
+// global_sum_tile.F:161-191): every tile's interior terms added sequentially, j outer and
+// i inner, from 0.0, then the tile partials added in tile order (bi fastest), from 0.0.
+// The per-point terms go through LDS at their compact index (tile, j, i: build_nbr's
+// order), one thread per tile sums them, and every thread adds the tile partials itself
+// (identical values, no broadcast).  Costs two barriers and a serial chain of sNx*sNy adds
+// per sum: the parity mode, not the performance path (cg2dRefOrder).
+template <int PPT>
+__device__ __forceinline__ double ref_sum(const double (&v)[PPT], double *term_l, double *tile_l, int nTiles,
+                                          int tilePts) {
+  const int tid = threadIdx.x;
+#pragma unroll
+  for (int m = 0; m < PPT; m++) term_l[tid + m * CG_THREADS] = v[m];
+  __syncthreads();
+  for (int t = tid; t < nTiles; t += CG_THREADS) {
+    const double *tp = term_l + (size_t)t * tilePts;
+    double e = 0.0;
+    for (int q = 0; q < tilePts; q++) e = e + tp[q];
+    tile_l[t] = e;
+  }
+  __syncthreads();
+  double sum = 0.0;
+  for (int t = 0; t < nTiles; t++) sum = sum + tile_l[t];
+  return sum;
+}
+
 // CALC_DIV_GHAT over k = Nr..1 + free-surface term; cg2d_x = Bo_surf*etaN (full range).
 // With useRealFreshWaterFlux the RHS starts from the E-P-R volume flux
 // (solve_for_pressure.F:142-151); with the CD scheme etaNm1 = etaN
@@ -161,7 +187,7 @@ __global__ void __launch_bounds__(256) k_sfp_rhs(Dims d, Params p, Fields f, int
 // neighbour is a halo point, the index is the interior point the halo is a copy
 // of (EXCH_S3D_RL / EXCH_XY_RL).  CREG: how many of the two 5-coefficient sets
 // (A, then M) stay in VGPRs; the rest is re-read each use from L2.
-template <int PPT, bool MINRES, int CREG>
+template <int PPT, bool MINRES, int CREG, bool REFSUM = false>
 __global__ void __launch_bounds__(CG_THREADS) k_cg2d_block(Dims d, Params p, Fields f, const unsigned *__restrict__ nbr,
                                                           const int *__restrict__ gofs, int nPts, int maxIters,
                                                           int nIterMinIn, SolveRecord *rec, int *stepCounter) {
@@ -170,6 +196,10 @@ __global__ void __launch_bounds__(CG_THREADS) k_cg2d_block(Dims d, Params p, Fie
   double *r_l = lds;                // NP + 1 (last = ZERO slot)
   double *s_l = lds + (NP + 1);     // NP + 1
   double *red = lds + 2 * (NP + 1); // 4 * CG_WAVES
+  // REFSUM (cg2dRefOrder): per-point terms and tile partials of the reference-order sums
+  double *term_l = red + 4 * CG_WAVES;   // NP
+  double *tile_l = term_l + NP;          // nTiles
+  const int nTilesR = d.nTiles, tilePts = d.sNx * d.sNy;
   const int tid = threadIdx.x;
   constexpr int RA = (CREG >= 1) ? PPT : 1, RM = (CREG >= 2) ? PPT : 1, RX = MINRES ? PPT : 1;
 
@@ -244,20 +274,27 @@ __global__ void __launch_bounds__(CG_THREADS) k_cg2d_block(Dims d, Params p, Fie
   for (int m = 0; m < PPT; m++) s_l[tid + m * CG_THREADS] = x[m];
   __syncthreads();
   // cg2d.F:139-180: r = b - A x ; err_sq, sumRHS
-  double err = 0.0, sumB = 0.0;
+  double err = 0.0, sumB = 0.0, tq[PPT];
 #pragma unroll
   for (int m = 0; m < PPT; m++) {
     r[m] = b[m] - (aW0(m) * s_l[LO(nwe[m])] + aW1(m) * s_l[HI(nwe[m])] + aS0(m) * s_l[LO(nsn[m])] +
                    aS1(m) * s_l[HI(nsn[m])] + aC(m) * x[m]);
     err = err + r[m] * r[m];
     sumB = sumB + b[m];
+    tq[m] = r[m] * r[m];
     if (MINRES) xmin[MINRES ? m : 0] = x[m];
   }
 #pragma unroll
   for (int m = 0; m < PPT; m++)
     if (ACT(m)) STO(f.cg2d_b, g[m]) = b[m];  // cg2d_b is INOUT (normalised in place)
-  double err_sq = block_sum(err, red, 1);
-  const double sumRHS = block_sum(sumB, red, 2);
+  double err_sq, sumRHS;
+  if (REFSUM) {
+    err_sq = ref_sum<PPT>(tq, term_l, tile_l, nTilesR, tilePts);
+    sumRHS = ref_sum<PPT>(b, term_l, tile_l, nTilesR, tilePts);
+  } else {
+    err_sq = block_sum(err, red, 1);
+    sumRHS = block_sum(sumB, red, 2);
+  }
   // EXCH_S3D_RL(cg2d_r): r into LDS; s_l re-zeroed for s = q + beta*s
 #pragma unroll
   for (int m = 0; m < PPT; m++) { r_l[tid + m * CG_THREADS] = r[m]; s_l[tid + m * CG_THREADS] = 0.0; }
@@ -281,9 +318,10 @@ __global__ void __launch_bounds__(CG_THREADS) k_cg2d_block(Dims d, Params p, Fie
         q[m] = pC(m) * r[m] + pW0(m) * r_l[LO(nwe[m])] + pW1(m) * r_l[HI(nwe[m])] + pS0(m) * r_l[LO(nsn[m])] +
                pS1(m) * r_l[HI(nsn[m])];
         e = e + q[m] * r[m];
+        tq[m] = q[m] * r[m];
       }
       slot = (slot + 1) & 3;
-      const double eta_qrN = block_sum(e, red, slot);
+      const double eta_qrN = REFSUM ? ref_sum<PPT>(tq, term_l, tile_l, nTilesR, tilePts) : block_sum(e, red, slot);
       const double cgBeta = eta_qrN / eta_qrNM1;
       eta_qrNM1 = eta_qrN;
       // s = q + beta*s ; EXCH_S3D_RL(cg2d_s)
@@ -297,9 +335,10 @@ __global__ void __launch_bounds__(CG_THREADS) k_cg2d_block(Dims d, Params p, Fie
         q[m] = aW0(m) * s_l[LO(nwe[m])] + aW1(m) * s_l[HI(nwe[m])] + aS0(m) * s_l[LO(nsn[m])] +
                aS1(m) * s_l[HI(nsn[m])] + aC(m) * s[m];
         a = a + s[m] * q[m];
+        tq[m] = s[m] * q[m];
       }
       slot = (slot + 1) & 3;
-      double alpha = block_sum(a, red, slot);
+      double alpha = REFSUM ? ref_sum<PPT>(tq, term_l, tile_l, nTilesR, tilePts) : block_sum(a, red, slot);
       alpha = eta_qrN / alpha;
       // x += alpha s ; r -= alpha q ; err_sq   (cg2d.F:305-328)
       double e2 = 0.0;
@@ -308,11 +347,13 @@ __global__ void __launch_bounds__(CG_THREADS) k_cg2d_block(Dims d, Params p, Fie
         x[m] = x[m] + alpha * s[m];
         r[m] = r[m] - alpha * q[m];
         e2 = e2 + r[m] * r[m];
+        tq[m] = r[m] * r[m];
         r_l[tid + m * CG_THREADS] = r[m];
       }
       actualIts = it2d;
       slot = (slot + 1) & 3;
-      err_sq = block_sum(e2, red, slot);  // its barrier also publishes r_l (EXCH_S3D_RL(cg2d_r))
+      // the barrier of either sum also publishes r_l (EXCH_S3D_RL(cg2d_r))
+      err_sq = REFSUM ? ref_sum<PPT>(tq, term_l, tile_l, nTilesR, tilePts) : block_sum(e2, red, slot);
       if (err_sq < p.cg2dTolerance_sq) break;
       if (MINRES && err_sq < minResidualSq) {
         minResidualSq = err_sq;
@@ -1438,8 +1479,36 @@ int cg2d_block_ppt(int nPts) {
 size_t cg2d_block_lds_bytes(int ppt) { return (size_t)(2 * (ppt * CG_THREADS + 1) + 4 * CG_WAVES) * sizeof(double); }
 int cg2d_block_max_points() { return 8 * CG_THREADS; }  // LDS: 2*8193*8 B = 128 KiB
 
+// cg2dRefOrder: the reference-order sums need NP + nTiles more doubles of LDS (PPT <= 4)
+int cg2d_ref_max_points() { return 4 * CG_THREADS; }
+static hipError_t launch_cg2d_ref(const Dims &d, const Params &p, const Fields &f, const unsigned *nbr, const int *gofs,
+                                  int nPts, int maxIters, int nIterMin, SolveRecord *rec, int *stepCounter,
+                                  hipStream_t s) {
+  const int ppt = cg2d_block_ppt(nPts);
+  if (!ppt || ppt > 4 || d.nTiles > nPts) return hipErrorInvalidValue;
+  const size_t lds = cg2d_block_lds_bytes(ppt) + (size_t)(ppt * CG_THREADS + d.nTiles) * sizeof(double);
+  const bool mr = nIterMin >= 0;
+#define LAUNCH(PPT)                                                                                          \
+  do {                                                                                                       \
+    auto kern = mr ? k_cg2d_block<PPT, true, 0, true> : k_cg2d_block<PPT, false, 0, true>;                   \
+    hipError_t e_ = hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds); \
+    if (e_ != hipSuccess) return e_;                                                                         \
+    hipLaunchKernelGGL(kern, dim3(1), dim3(CG_THREADS), lds, s, d, p, f, nbr, gofs, nPts, maxIters, nIterMin, rec, \
+                       stepCounter);                                                                         \
+  } while (0)
+  switch (ppt) {
+    case 1: LAUNCH(1); break;
+    case 2: LAUNCH(2); break;
+    default: LAUNCH(4); break;
+  }
+#undef LAUNCH
+  return hipGetLastError();
+}
+
 hipError_t launch_cg2d_block(const Dims &d, const Params &p, const Fields &f, const unsigned *nbr, const int *gofs,
                              int nPts, int maxIters, int nIterMin, SolveRecord *rec, int *stepCounter, hipStream_t s) {
+  if (p.cg2dRefOrder)
+    return launch_cg2d_ref(d, p, f, nbr, gofs, nPts, maxIters, nIterMin, rec, stepCounter, s);
   const int ppt = cg2d_block_ppt(nPts);
   if (!ppt) return hipErrorInvalidValue;
   const size_t lds = cg2d_block_lds_bytes(ppt);

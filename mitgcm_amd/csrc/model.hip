@@ -27,6 +27,7 @@ hipError_t launch_sfp_rhs(const Dims &, const Params &, const Fields &, hipStrea
 hipError_t launch_cg2d_block(const Dims &, const Params &, const Fields &, const unsigned *, const int *, int, int, int,
                              SolveRecord *, int *, hipStream_t);
 int cg2d_block_ppt(int nPts);
+int cg2d_ref_max_points();
 hipError_t launch_cg2d_bxy(int, const Dims &, const Params &, const Fields &, const unsigned *, const int *, int, int,
                            int, SolveRecord *, int *, hipStream_t);
 int cg2d_bxy_geometry(int, int *, int *, int *);
@@ -112,7 +113,7 @@ static const PDesc PARAMS[] = {
     PD(mtFacMom), PD(cg2dNorm), PD(cg2dTolerance_sq),
     PI_(momAdvection), PI_(momViscosity), PI_(momForcing), PI_(useCoriolis), PI_(no_slip_sides),
     PI_(no_slip_bottom), PI_(selectCoriScheme), PI_(momForcingOutAB), PI_(momDissip_In_AB),
-    PI_(implicitViscosity), PI_(cg2dMaxIters), PI_(cg2dUseMinResSol), PI_(cg2dNormaliseRHS), PI_(nIter0), PI_(cg2dUseFMA), PI_(useSRCGSolver),
+    PI_(implicitViscosity), PI_(cg2dMaxIters), PI_(cg2dUseMinResSol), PI_(cg2dNormaliseRHS), PI_(nIter0), PI_(cg2dUseFMA), PI_(useSRCGSolver), PI_(cg2dRefOrder),
     PD(gravity), PD(gravitySign), PD(rhoNil), PD(tAlpha), PD(sBeta), PD(ivdc_kappa), PD(diffKhT), PD(diffKrT),
     PD(deltaTtracer), PI_(exactConserv), PI_(tempStepping), PI_(tempAdvection), PI_(tempForcing),
     PI_(implicitDiffusion), PI_(tempAdvScheme), PI_(saltStepping), PI_(saltAdvection), PI_(saltForcing),
@@ -828,6 +829,19 @@ int mgcm_set_param(mgcm_model *m, const char *name, double value) {
   return 0;
 }
 
+namespace mgcm {
+__global__ void k_set_iter(int *ctr, int v) {
+  if (threadIdx.x == 0) ctr[0] = v;
+}
+}  // namespace mgcm
+
+int mgcm_set_iter(mgcm_model *m, int myIter) {
+  HIPCHK(hipSetDevice(m->device));
+  hipLaunchKernelGGL(mgcm::k_set_iter, dim3(1), dim3(64), 0, m->stream, m->d_ctr, myIter);
+  HIPCHK(hipGetLastError());
+  return 0;
+}
+
 double mgcm_get_param(mgcm_model *m, const char *name) {
   if (!strcmp(name, "myIter")) {
     int it = 0;
@@ -836,8 +850,9 @@ double mgcm_get_param(mgcm_model *m, const char *name) {
       return NAN;
     return it;
   }
-  // 4: k_cg2d_mwg, 3: k_cg2d_bxy, 2: k_cg2d_blk2, 1: k_cg2d_block
-  if (!strcmp(name, "cg2dKernel")) return m->useMwg ? 4.0 : m->nBlkX > 0 ? 3.0 : (m->nBlk > 0 ? 2.0 : 1.0);
+  // 5: k_cg2d_block in the reference order (cg2dRefOrder), 4: k_cg2d_mwg, 3: k_cg2d_bxy, 2: k_cg2d_blk2, 1: k_cg2d_block
+  if (!strcmp(name, "cg2dKernel"))
+    return m->p.cg2dRefOrder ? 5.0 : m->useMwg ? 4.0 : m->nBlkX > 0 ? 3.0 : (m->nBlk > 0 ? 2.0 : 1.0);
   if (!strcmp(name, "cg2dParts")) return m->useMwg ? (double)m->mwg.G : 1.0;
   // THERMODYNAMICS on the second stream: 1 on, 0 off; -1 while the graph path is still timing
   // both (ovlMsOn / ovlMsOff: ovl_trial's event times of the two graphs, 8 steps each)
@@ -846,7 +861,7 @@ double mgcm_get_param(mgcm_model *m, const char *name) {
   if (!strcmp(name, "ovlMsOff")) return m->ovlMs[0];
   if (!strcmp(name, "cg2dBxyVariant")) return (double)m->bxyVar;
   // whether the selected kernel solves with fused multiply-adds (k_cg2d_bxy honours cg2dUseFMA)
-  if (!strcmp(name, "cg2dFMA")) return (!m->useMwg && m->nBlkX > 0 && m->p.cg2dUseFMA) ? 1.0 : 0.0;
+  if (!strcmp(name, "cg2dFMA")) return (!m->p.cg2dRefOrder && !m->useMwg && m->nBlkX > 0 && m->p.cg2dUseFMA) ? 1.0 : 0.0;
   for (auto &pd : PARAMS)
     if (!strcmp(pd.name, name)) {
       const char *ptr = reinterpret_cast<const char *>(&m->p) + pd.off;
@@ -977,7 +992,14 @@ int mgcm_init(mgcm_model *m) {
   // single-workgroup one where it fits)
   m->useMwg = false;
   const bool single = getenv("MGCM_CG2D_SINGLE") && atoi(getenv("MGCM_CG2D_SINGLE")) == 1;
-  if (m->nBlkX == 0 && m->nBlk == 0 && !(single && m->nPts <= cg2d_block_max_points())) {
+  // cg2dRefOrder: the generic single-workgroup kernel with the reference's summation order
+  // (parity runs on the reference's own tiling; refused where it does not fit one workgroup)
+  if (m->p.cg2dRefOrder) {
+    if (m->nPts > cg2d_ref_max_points())
+      return set_err("mgcm_init: cg2dRefOrder needs <= %d interior points (one workgroup), have %d",
+                     cg2d_ref_max_points(), m->nPts);
+    if (m->p.useSRCGSolver) return set_err("mgcm_init: cg2dRefOrder with useSRCGSolver not implemented");
+  } else if (m->nBlkX == 0 && m->nBlk == 0 && !(single && m->nPts <= cg2d_block_max_points())) {
     if (build_mwg(m)) return -1;
     if (m->p.cg2dUseMinResSol) return set_err("mgcm_init: cg2dUseMinResSol with the multi-workgroup CG2D not implemented");
   }
@@ -1073,6 +1095,9 @@ int mgcm_init(mgcm_model *m) {
 }
 
 static hipError_t launch_cg2d(mgcm_model *m, int maxIters, int nIterMin) {
+  if (m->p.cg2dRefOrder)
+    return launch_cg2d_block(m->d, m->p, m->f, m->d_nbr, m->d_gofs, m->nPts, maxIters, nIterMin, m->d_rec, m->d_ctr + 1,
+                             m->stream);
   if (m->useMwg) {
     if (nIterMin >= 0) return hipErrorInvalidValue;   // no min-residual solution in the multi-workgroup solver
     return launch_cg2d_mwg(m->d, m->p, m->f, m->mwg, maxIters, m->d_rec, m->d_ctr + 1, m->stream);
@@ -1375,10 +1400,16 @@ static int two_step_graph(mgcm_model *m, hipGraphExec_t *out) {
   return 0;
 }
 
+static int ovl_trial(mgcm_model *m);
+
+// Builds the graphs of the next batch and, when the THERMODYNAMICS overlap is still
+// undecided, runs its trial now (on a copy of the state) so that no later timed batch
+// contains the trial's 20 steps.
 int mgcm_prepare(mgcm_model *m) {
   if (check_ready(m)) return -1;
   if (!m->useGraph) return 0;
   HIPCHK(hipSetDevice(m->device));
+  if (m->ovlAuto && !m->ovlDecided && ovl_trial(m)) return -1;
   hipGraphExec_t ge;
   return two_step_graph(m, &ge);
 }
@@ -1407,13 +1438,15 @@ static int ovl_trial(mgcm_model *m) {
     m->ovlDecided = true;
     return 0;
   }
-  size_t off = 0;
-  for (auto &pr : parts) {
-    HIPCHK(hipMemcpyAsync(save + off, pr.first, pr.second, hipMemcpyDeviceToDevice, m->stream));
-    off += (pr.second + 255) & ~(size_t)255;
-  }
+  // one exit path: the copy is always restored and freed, the overlap mode always reset
+  // when the trial fails
   const bool ovl0 = m->overlap;
   int rc = 0;
+  size_t off = 0;
+  for (auto &pr : parts) {
+    if (!rc && hipMemcpyAsync(save + off, pr.first, pr.second, hipMemcpyDeviceToDevice, m->stream) != hipSuccess) rc = -1;
+    off += (pr.second + 255) & ~(size_t)255;
+  }
   for (int ph = 0; ph < 6 && !rc; ph++) {
     const int pairs = ph < 2 ? 1 : 2, mode = (ph & 1) ? 0 : 1;
     m->overlap = mode != 0;
@@ -1427,14 +1460,18 @@ static int ovl_trial(mgcm_model *m) {
         hipEventElapsedTime(&ms, m->ovlEv[0], m->ovlEv[1]) != hipSuccess) { rc = -1; break; }
     if (ph >= 2) m->ovlMs[mode] += ms;
   }
+  int rs = 0;
   off = 0;
   for (auto &pr : parts) {
-    HIPCHK(hipMemcpyAsync(pr.first, save + off, pr.second, hipMemcpyDeviceToDevice, m->stream));
+    if (hipMemcpyAsync(pr.first, save + off, pr.second, hipMemcpyDeviceToDevice, m->stream) != hipSuccess) rs = -1;
     off += (pr.second + 255) & ~(size_t)255;
   }
-  HIPCHK(hipStreamSynchronize(m->stream));
+  if (hipStreamSynchronize(m->stream) != hipSuccess) rs = -1;
   (void)hipFree(save);
-  if (rc) { m->overlap = ovl0; return set_err("ovl_trial: graph replay failed"); }
+  if (rc || rs) {
+    m->overlap = ovl0;
+    return set_err(rs ? "ovl_trial: restoring the saved state failed" : "ovl_trial: graph replay failed");
+  }
   m->ovlDecided = true;
   m->overlap = m->ovlMs[1] <= m->ovlMs[0];
   return 0;

@@ -18,8 +18,9 @@
 ! then checks EXCH_XYZ_RL, EXCH_UV_XYZ_RL, EXCH_XY_RL and GLOBAL_SUM_TILE_RL on host arrays.
 !
 ! Input (stream, native endian, written by tests/test_gpu_fortran.py): sizes, parameters
-! (name, value), fields (name, count, isStatic, values), the forcing records; output: every
-! non-static field after the steps, plus the exchange / global-sum checks.
+! (name, value), fields (name, count, kind: 0 state / 1 static / 2 host input, values), the
+! forcing records; output: every state field after the steps, plus the exchange /
+! global-sum checks.
 program fhost
   implicit none
   type field
@@ -81,6 +82,8 @@ program fhost
     call CALC_R_STAR_AMD(f(iEtaH)%a, myTime, myIter, myThid)
     call DO_FIELDS_BLOCKING_EXCHANGES_AMD(myThid)
   end do
+  ! the device copy is authoritative inside the time loop: bring the state down
+  call MGCM_AMD_HOST_SYNC(myThid)
   ! exchanges on host copies whose halos were overwritten with a marker
   allocate(tmp(n3), tmpv(n3), tile(nSx*nSy))
   tmp = f(iT)%a

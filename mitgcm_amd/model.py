@@ -182,9 +182,10 @@ class Model:
 
     def cg2d_kernel(self):
         """Which CG2D kernel mgcm_init selected: 'mwg' (multi-workgroup), 'bxy' (BX x BY points/thread),
-        'blk2' (2x2) or 'block'."""
+        'blk2' (2x2), 'block', or 'block_ref' (k_cg2d_block summing in the reference's order,
+        cg2dRefOrder)."""
         k = lib().mgcm_get_param(self.h, b"cg2dKernel")
-        return {4.0: "mwg", 3.0: "bxy", 2.0: "blk2"}.get(k, "block")
+        return {5.0: "block_ref", 4.0: "mwg", 3.0: "bxy", 2.0: "blk2"}.get(k, "block")
 
     def cg2d_fma(self):
         """True when the selected CG2D kernel solves in fused multiply-adds (cg2dUseFMA): the

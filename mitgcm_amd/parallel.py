@@ -390,14 +390,20 @@ class ShardedModel:
         with torch.cuda.graph(g, stream=s):
             self.step()
             self.step()
+        torch.cuda.synchronize(self.dev)
+        # back onto the model's stream (torch's current one, where the collectives of eager
+        # steps and replay() run): begin_steps' memset and eager steps after a capture are
+        # then ordered with the replays and the RCCL calls on one stream
+        self.check(L.mgcm_set_stream(h, ctypes.c_void_p(self.stream.cuda_stream)), "mgcm_set_stream")
         self._graph, self._gstream = g, s
 
     def replay(self, npairs=1):
         """Replay the captured pair of steps npairs times (the device's per-step record ring
         restarts at the first replay)."""
-        self.check(self.L.mgcm_begin_steps(self.m.h), "mgcm_begin_steps")
-        for _ in range(npairs):
-            self._graph.replay()
+        self.check(self.L.mgcm_begin_steps(self.m.h), "mgcm_begin_steps")   # on self.stream
+        with self.torch.cuda.stream(self.stream):
+            for _ in range(npairs):
+                self._graph.replay()
 
     def forward_step(self, nsteps=1):
         self.check(self.L.mgcm_begin_steps(self.m.h), "mgcm_begin_steps")

@@ -80,3 +80,23 @@ def test_fortran_hosts_link_library():
     for exe in ("cg2d_host", "fhost"):
         out = subprocess.run(["ldd", os.path.join(fdir, exe)], check=True, capture_output=True, text=True).stdout
         assert "libmitgcm_amd.so" in out and "not found" not in out, exe
+
+
+@pytest.mark.skipif(not (os.path.isdir(REF) and os.path.exists(FC) and shutil.which("cpp")),
+                    reason="needs the reference headers and amdflang")
+def test_refhost_builds_against_reference_headers():
+    """mitgcm_amd/fortran/refhost: the MODS drop-ins + the harness main program + the
+    generated COMMON-block fill routines compile against the reference's headers (its own
+    SIZE.h and the one-tile layout) and link the library."""
+    import sys
+    sys.path.insert(0, os.path.join(ROOT, "mitgcm_amd", "fortran"))
+    import build_refhost
+    params, fields = build_refhost.mirror_calls()
+    assert ("R", "monitorFreq") in params and ("I", "nEndIter") in params
+    assert {n for n, k in fields if k == 2} == {"fu", "fv", "Qnet", "EmPmR", "SST", "SSS"}
+    for exe in build_refhost.build():
+        out = subprocess.run(["ldd", exe], check=True, capture_output=True, text=True).stdout
+        assert "libmitgcm_amd.so" in out and "not found" not in out, exe
+        syms = subprocess.run(["nm", exe], check=True, capture_output=True, text=True).stdout
+        for s in ("dynamics_", "mgcm_amd_mirror_", "refhost_param_", "refhost_field_"):
+            assert re.search(r" T %s$" % s, syms, re.M), (exe, s)

@@ -23,6 +23,7 @@ pytestmark = pytest.mark.gpu
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 FHOST = os.path.join(ROOT, "mitgcm_amd", "fortran", "fhost")
+FORCING = ("fu", "fv", "Qnet", "EmPmR", "SST", "SSS")
 CHECK = ("uVel", "vVel", "wVel", "theta", "salt", "etaN", "etaH", "gU", "gV", "guNm1", "gvNm1", "gtNm1", "gsNm1",
          "rhoInSitu", "surfaceForcingT", "Kwx", "totPhiHyd")
 
@@ -51,6 +52,8 @@ def _write_blob(path, m, nsteps):
     fields = [(n, 1) for n in GRID_1D] + [(n, 0) for n in STATE_1D]
     fields += [(n, 0 if n in operator else 1) for n in GRID_2D] + [(n, 0) for n in STATE_2D]
     fields += [(n, 0) for n in GRID_3D + STATE_3D]
+    # what the host's LOAD_FIELDS_DRIVER writes every step: host input (kind 2)
+    fields = [(n, 2 if n in FORCING else st) for n, st in fields]
     with open(path, "wb") as fh:
         fh.write(np.array([g.sNx, g.sNy, g.OLx, g.OLy, g.Nr, g.nSx, g.nSy, len(params), len(fields), nsteps,
                            int(params["nIter0"]), nRec, periodic], dtype=np.int32).tobytes())

@@ -5,9 +5,10 @@ multi-workgroup CG2D), through the C-ABI.
 Bars:
   * LLC-30 (13 tiles of 30 x 30, 10 levels, OL = 4): 8 steps bit-identical to the oracle
     summing CG2D in the device's order; cg2d_iters identical to the reference-order oracle;
-  * LLC-90 as benched (13 tiles of 90 x 90, 50 levels): the initial state round-trips, 4
-    steps stay finite with a converged CG2D, and the first solve's iteration count equals
-    the reference-order oracle's.  The synthetic set-up has no reference output: parity
+  * LLC-90 as benched (13 tiles of 90 x 90, 50 levels): the initial state round-trips; the
+    first step's monitored values (dynstat, CG2D residuals and iterations) are bit-identical
+    to the device-order oracle's at full size, and its iteration count equals the
+    reference-order oracle's; 4 steps stay finite with a converged CG2D.  The synthetic set-up has no reference output: parity
     unpinned against the reference, pinned device-vs-oracle.
 """
 import numpy as np
@@ -48,12 +49,31 @@ def test_llc30_8_steps_bitexact_vs_device_order_oracle():
 
 def test_llc90_full_size_steps():
     from mitgcm_amd import configs
+    from mitgcm_amd.model import dynstat
+    from oracle.harness import oracle_from_config
     g, params, state = configs.llc_synthetic()
     m = configs.make_model(lambda: (g, params, state))
     assert np.array_equal(m.get("theta"), state["theta"])
-    m.forward_step(4)
+    # the first step against the oracle at full size: iterations equal to the reference-order
+    # oracle's, and every monitored value bit-identical to the device-order oracle's
+    plan, NT, PPT, NG = m.cg2d_sum_plan()
+    od, _ = oracle_from_config(configs.llc_synthetic)
+    od.set_sum_plan(plan, NT, PPT, NG, fma=m.cg2d_fma())
+    o_ref, _ = oracle_from_config(configs.llc_synthetic)
+    m.forward_step(1)
+    od.forward_step()
+    o_ref.forward_step()
+    md = m.solve_stats()
+    md.update(dynstat(m))
+    dd = od.dynstat()
+    assert md["cg2d_iters"] == dd["cg2d_iters"] == int(o_ref.get("numIters")), (
+        md["cg2d_iters"], dd["cg2d_iters"], o_ref.get("numIters"))
+    for k, v in md.items():
+        if k in dd:
+            assert v == dd[k], (k, v, dd[k])
+    m.forward_step(3)
     m.sync()
-    iters = [m.solve_stats(back=b)["cg2d_iters"] for b in range(4)]
+    iters = [md["cg2d_iters"]] + [m.solve_stats(back=b)["cg2d_iters"] for b in range(3)]   # records of the last batch
     st = m.solve_stats()
     assert all(0 < i < params["cg2dMaxIters"] for i in iters), iters
     assert st["cg2d_last_res"] < st["cg2d_init_res"]

@@ -6,7 +6,8 @@ node runs the same calls with peers.  BASELINE config 4 (baroclinic gyre + DST3-
   * the distributed CG2D (GLOBAL_SUM_TILE_RL as an RCCL all-gather of per-tile partials):
     iteration counts of the replicated solve, fields within 1e-10;
   * two steps captured into a HIP graph with their RCCL collectives (torch.cuda.graph on
-    the model's stream) and replayed: bit-identical to stepping eagerly."""
+    a side stream) and replayed: bit-identical to stepping eagerly; an eager step after
+    the replays (back on the collectives' stream) stays bit-identical."""
 import os
 import socket
 
@@ -48,6 +49,9 @@ def _worker(port, q):
         ref.forward_step(1)
         ref.sync()
         want5 = {n: ref.get(n) for n in FIELDS}
+        ref.forward_step(1)
+        ref.sync()
+        want6 = {n: ref.get(n) for n in FIELDS}
         ref.close()
         # eager, replicated CG2D
         m = _make()
@@ -72,6 +76,10 @@ def _worker(port, q):
         sm.replay(2)
         torch.cuda.synchronize()
         res["graph"] = {n: bool(np.array_equal(sm.gather_field(n), want5[n])) for n in FIELDS}
+        # an eager step after the replays: the model is back on the stream of the collectives
+        sm.forward_step(1)
+        torch.cuda.synchronize()
+        res["eager_after_graph"] = {n: bool(np.array_equal(sm.gather_field(n), want6[n])) for n in FIELDS}
         m.close()
         dist.destroy_process_group()
         q.put(res)
@@ -92,6 +100,7 @@ def test_rccl_world1_eager_distributed_and_graph():
     print("RCCL world 1:", res)
     assert all(res["eager"].values()), res["eager"]
     its, ref_its = res["dist_iters"]
-    assert sorted(its) == sorted(ref_its), res["dist_iters"]
+    assert its == ref_its, res["dist_iters"]   # per step, most recent first in both lists
     assert max(res["dist_diff"].values()) <= 1e-10, res["dist_diff"]
     assert all(res["graph"].values()), res["graph"]
+    assert all(res["eager_after_graph"].values()), res["eager_after_graph"]
