@@ -210,6 +210,8 @@ void mgcm_amd_init_(const int *myIter);
 void mgcm_amd_host_sync_(const int *myThid);
 void mgcm_amd_device_sync_(const int *myThid);
 void mgcm_amd_transfer_stats_(int *nUploads, int *nDownloads, double *bytesUp, double *bytesDown);
+/* Wait for the device work issued so far (hosts that clock their steps). */
+void mgcm_amd_step_fence_(const int *myThid);
 /* Routine drop-ins: during initialisation the bound state is uploaded before and
  * downloaded after each; from the first DO_OCEANIC_PHYS / THERMODYNAMICS / DYNAMICS on, the
  * device copy is authoritative (forcing up every step, state down for host readers). */

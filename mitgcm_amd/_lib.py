@@ -96,7 +96,8 @@ EXPORTS = ["mgcm_create", "mgcm_destroy", "mgcm_last_error", "mgcm_set_param", "
            "integr_continuity_amd_", "do_fields_blocking_exchanges_amd_", "exch_xy_rl_amd_", "exch_xyz_rl_amd_",
            "exch_uv_xy_rl_amd_", "exch_uv_xyz_rl_amd_", "global_sum_tile_rl_amd_",
            "mgcm_update_r_star", "mgcm_calc_r_star", "update_r_star_amd_", "update_cg2d_amd_", "calc_r_star_amd_",
-           "mgcm_set_iter", "mgcm_amd_host_sync_", "mgcm_amd_device_sync_", "mgcm_amd_transfer_stats_"]
+           "mgcm_set_iter", "mgcm_amd_host_sync_", "mgcm_amd_device_sync_", "mgcm_amd_transfer_stats_",
+           "mgcm_amd_step_fence_"]
 
 
 def check(rc, what):

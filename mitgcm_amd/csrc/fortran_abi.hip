@@ -258,6 +258,10 @@ void mgcm_amd_bind_(const char *name, double *array, const int *count, const int
  * overwritten by the host's state again. */
 void mgcm_amd_init_(const int *myIter) {
   model("MGCM_AMD_INIT");
+  // device options with no PARAMS.h counterpart, from the environment:
+  // MGCM_CG2D_REFORDER=1 sums CG2D in the reference's order (cg2dRefOrder, parity runs)
+  if (const char *e = getenv("MGCM_CG2D_REFORDER"))
+    if (mgcm_set_param(g.m, "cg2dRefOrder", atof(e))) die("MGCM_AMD_INIT");
   upload("MGCM_AMD_INIT", K_STATIC | K_STATE | K_INPUT);
   if (mgcm_set_param(g.m, "myIter", (double)*myIter)) die("MGCM_AMD_INIT");
   if (mgcm_init(g.m)) die("MGCM_AMD_INIT");
@@ -281,6 +285,12 @@ void mgcm_amd_device_sync_(const int *myThid) {
   (void)myThid;
   model("MGCM_AMD_DEVICE_SYNC");
   if (g.ready && g.deviceAuth) upload("MGCM_AMD_DEVICE_SYNC", K_STATE | K_INPUT);
+}
+
+/* Waits for the device work issued so far (a timing aid for hosts that clock steps). */
+void mgcm_amd_step_fence_(const int *myThid) {
+  (void)myThid;
+  if (mgcm_sync(model("MGCM_AMD_STEP_FENCE"))) die("MGCM_AMD_STEP_FENCE");
 }
 
 /* Whole-array copies so far (uploads, downloads) and their bytes. */

@@ -1346,13 +1346,19 @@ __global__ void __launch_bounds__(256) k_exch_etaH(Dims d, Params p, Fields f, c
 // atInit = 2: INTEGR_CONTINUITY alone (the routine-level C-ABI, after a separate
 // MOMENTUM_CORRECTION_STEP): divergence of uVel, vVel as they are, stepping formulas.
 // r* (select_rStar > 0): w includes -rStarDhDt*drF*h0FacC (integrate_for_w.F:117-140).
-__global__ void __launch_bounds__(256) k_corr_cont(Dims d, Params p, Fields f, int atInit) {
-  __shared__ double sDiv[256], sMask[256], sH0[256];
-  MG_COLS(1, d.sNx, 1, d.sNy, d.Nr)
-  const int k = kk + 1, me = kk * NC_ + cc;
+// Column frame (MG_COLF): NC columns x KW level slots per workgroup, the levels of a
+// column staged k-parallel into LDS and its serial parts (the exactConserv column sum, the
+// upward w recurrence) run by one thread per column out of LDS; the corrected velocities go
+// through LDS too, so no global store sits between a level's loads and the next level's.
+__global__ void __launch_bounds__(256) k_corr_cont(Dims d, Params p, Fields f, int atInit, int nc) {
+  extern __shared__ __attribute__((aligned(16))) double lds[];
+  MG_COLF(1, d.sNx, 1, d.sNy, nc)
+  const int NS = d.Nr * NC_;
+  double *sDiv = lds, *sMask = lds + NS, *sH0 = lds + 2 * NS, *sU = lds + 3 * NS, *sV = lds + 4 * NS;
   const long q = MG_I2(d, i, j, t);
   const bool rstar = p.nonlinFreeSurf > 0 && p.select_rStar != 0;
-  if (valid && k <= d.Nr && atInit != 0) {   // divergence of the velocities already in uVel, vVel
+  if (valid && atInit != 0) MG_COLF_K(k) {   // divergence of the velocities already in uVel, vVel
+    const int me = (k - 1) * NC_ + cc;
     const double drF = f.drF[k - 1];
     const double u0 = f.uVel[MG_I3(d, i, j, k, t)], u1 = f.uVel[MG_I3(d, i + 1, j, k, t)];
     const double v0 = f.vVel[MG_I3(d, i, j, k, t)], v1 = f.vVel[MG_I3(d, i, j + 1, k, t)];
@@ -1363,7 +1369,7 @@ __global__ void __launch_bounds__(256) k_corr_cont(Dims d, Params p, Fields f, i
     sDiv[me] = uT1 - uT0 + vT1 - vT0;
     sMask[me] = f.maskC[MG_I3(d, i, j, k, t)];
     sH0[me] = rstar ? f.h0FacC[MG_I3(d, i, j, k, t)] : 0.0;
-  } else if (valid && k <= d.Nr) {
+  } else if (valid) {
     const double psFac = p.pfFacMom * p.implicSurfPress;
     auto phiX = [&](int ii, int jj) {
       const long qq = MG_I2(d, ii, jj, t);
@@ -1373,28 +1379,33 @@ __global__ void __launch_bounds__(256) k_corr_cont(Dims d, Params p, Fields f, i
       const long qq = MG_I2(d, ii, jj, t);
       return f.recip_dyC[qq] * (f.Bo_surf[qq] * f.etaN[qq] - f.Bo_surf[MG_I2(d, ii, jj - 1, t)] * f.etaN[MG_I2(d, ii, jj - 1, t)]);
     };
-    auto uCor = [&](int ii, double phiSurfX) {
-      const long q3 = MG_I3(d, ii, j, k, t);
-      const double mW = f.maskW[q3];
-      return (f.gU[q3] + p.deltaTMom * (-psFac * phiSurfX * mW)) * mW;
-    };
-    auto vCor = [&](int jj, double phiSurfY) {
-      const long q3 = MG_I3(d, i, jj, k, t);
-      const double mS = f.maskS[q3];
-      return (f.gV[q3] + p.deltaTMom * (-psFac * phiSurfY * mS)) * mS;
-    };
-    const double u0 = uCor(i, phiX(i, j)), u1 = uCor(i + 1, phiX(i + 1, j));
-    const double v0 = vCor(j, phiY(i, j)), v1 = vCor(j + 1, phiY(i, j + 1));
-    f.uVel[MG_I3(d, i, j, k, t)] = u0;
-    f.vVel[MG_I3(d, i, j, k, t)] = v0;
-    const double drF = f.drF[k - 1];
-    const double uT1 = u1 * f.dyG[MG_I2(d, i + 1, j, t)] * drF * f.hFacW[MG_I3(d, i + 1, j, k, t)];
-    const double uT0 = u0 * f.dyG[q] * drF * f.hFacW[MG_I3(d, i, j, k, t)];
-    const double vT1 = v1 * f.dxG[MG_I2(d, i, j + 1, t)] * drF * f.hFacS[MG_I3(d, i, j + 1, k, t)];
-    const double vT0 = v0 * f.dxG[q] * drF * f.hFacS[MG_I3(d, i, j, k, t)];
-    sDiv[me] = uT1 - uT0 + vT1 - vT0;
-    sMask[me] = f.maskC[MG_I3(d, i, j, k, t)];
-    sH0[me] = rstar ? f.h0FacC[MG_I3(d, i, j, k, t)] : 0.0;
+    // the column's surface-pressure gradients (2-D, the same at every level)
+    const double pX0 = phiX(i, j), pX1 = phiX(i + 1, j), pY0 = phiY(i, j), pY1 = phiY(i, j + 1);
+    MG_COLF_K(k) {
+      const int me = (k - 1) * NC_ + cc;
+      auto uCor = [&](int ii, double phiSurfX) {
+        const long q3 = MG_I3(d, ii, j, k, t);
+        const double mW = f.maskW[q3];
+        return (f.gU[q3] + p.deltaTMom * (-psFac * phiSurfX * mW)) * mW;
+      };
+      auto vCor = [&](int jj, double phiSurfY) {
+        const long q3 = MG_I3(d, i, jj, k, t);
+        const double mS = f.maskS[q3];
+        return (f.gV[q3] + p.deltaTMom * (-psFac * phiSurfY * mS)) * mS;
+      };
+      const double u0 = uCor(i, pX0), u1 = uCor(i + 1, pX1);
+      const double v0 = vCor(j, pY0), v1 = vCor(j + 1, pY1);
+      sU[me] = u0;
+      sV[me] = v0;
+      const double drF = f.drF[k - 1];
+      const double uT1 = u1 * f.dyG[MG_I2(d, i + 1, j, t)] * drF * f.hFacW[MG_I3(d, i + 1, j, k, t)];
+      const double uT0 = u0 * f.dyG[q] * drF * f.hFacW[MG_I3(d, i, j, k, t)];
+      const double vT1 = v1 * f.dxG[MG_I2(d, i, j + 1, t)] * drF * f.hFacS[MG_I3(d, i, j + 1, k, t)];
+      const double vT0 = v0 * f.dxG[q] * drF * f.hFacS[MG_I3(d, i, j, k, t)];
+      sDiv[me] = uT1 - uT0 + vT1 - vT0;
+      sMask[me] = f.maskC[MG_I3(d, i, j, k, t)];
+      sH0[me] = rstar ? f.h0FacC[MG_I3(d, i, j, k, t)] : 0.0;
+    }
   }
   __syncthreads();
   if (valid && kk == 0) {
@@ -1422,25 +1433,31 @@ __global__ void __launch_bounds__(256) k_corr_cont(Dims d, Params p, Fields f, i
       if (rstar) rStarDhDt = dEtaHdt * f.recip_Rcol[q];   // integr_continuity.F:171-183
     }
     double wBelow = 0.0;
+    const double rA1 = f.recip_rA[q];
     for (int k2 = d.Nr; k2 >= 1; k2--) {
       const int s2 = (k2 - 1) * NC_ + cc;
       const double conv2d = -sDiv[s2];
       double w;
       if (rstar) {
         const double dh = rStarDhDt * f.drF[k2 - 1] * sH0[s2];
-        if (k2 == d.Nr) w = (conv2d * f.recip_rA[q] - dh) * sMask[s2];
-        else w = (wBelow + conv2d * f.recip_rA[q] - dh) * sMask[s2];
+        if (k2 == d.Nr) w = (conv2d * rA1 - dh) * sMask[s2];
+        else w = (wBelow + conv2d * rA1 - dh) * sMask[s2];
       } else if (k2 == d.Nr) {
-        w = conv2d * f.recip_rA[q] * sMask[s2];
+        w = conv2d * rA1 * sMask[s2];
       } else {
-        w = (wBelow + conv2d * f.recip_rA[q]) * sMask[s2];
+        w = (wBelow + conv2d * rA1) * sMask[s2];
       }
       sDiv[s2] = w;
       wBelow = w;
     }
   }
   __syncthreads();
-  if (valid && k <= d.Nr) f.wVel[MG_I3(d, i, j, k, t)] = sDiv[me];
+  if (valid) MG_COLF_K(k) {
+    const int me = (k - 1) * NC_ + cc;
+    const long q3 = MG_I3(d, i, j, k, t);
+    f.wVel[q3] = sDiv[me];
+    if (atInit == 0) { f.uVel[q3] = sU[me]; f.vVel[q3] = sV[me]; }
+  }
 }
 
 // Tile-sharded runs: gather (pack) / scatter (unpack) the halo-source points a peer
@@ -1669,8 +1686,11 @@ hipError_t launch_exch_eta(const Dims &d, const Params &p, const Fields &f, cons
 }
 
 hipError_t launch_corr_cont(const Dims &d, const Params &p, const Fields &f, int atInit, hipStream_t s) {
-  const dim3 blk(256), grd(mg_col_blocks(d.sNx, d.sNy, d.nT, d.Nr));
-  hipLaunchKernelGGL(k_corr_cont, grd, blk, 0, s, d, p, f, atInit);
+  const long ncol = (long)d.sNx * d.sNy * d.nT;
+  const int nc = mg_colf_nc(ncol, d.Nr, 5);
+  MG_ALLOW_LDS(k_corr_cont);
+  hipLaunchKernelGGL(k_corr_cont, dim3(mg_colf_blocks(ncol, nc)), dim3(256), mg_colf_lds(d.Nr, nc, 5), s, d, p, f, atInit,
+                     nc);
   return hipGetLastError();
 }
 

@@ -95,11 +95,12 @@ def _write_blob(path, m, nsteps, monitor_days):
     return [n for n, k, a in blob_fields if k == 0]
 
 
-def _read_out(path, state_names):
+def _read_out(path, state_names, nsteps):
     raw = open(path, "rb").read()
     nfs, nup, ndown = np.frombuffer(raw, dtype=np.int32, count=3)
     secs, bup, bdown = np.frombuffer(raw, dtype=np.float64, count=3, offset=12)
-    off = 36
+    step_s = np.frombuffer(raw, dtype=np.float64, count=nsteps, offset=36)
+    off = 36 + 8 * nsteps
     out = {}
     for _ in state_names:
         name = raw[off:off + 32].decode().strip()
@@ -109,7 +110,7 @@ def _read_out(path, state_names):
         off += 8 * cnt
     assert off == len(raw)
     return out, {"steps_timed": int(nfs), "uploads": int(nup), "downloads": int(ndown), "seconds": float(secs),
-                 "bytes_up": float(bup), "bytes_down": float(bdown)}
+                 "bytes_up": float(bup), "bytes_down": float(bdown), "step_ms": [1e3 * x for x in step_s]}
 
 
 @pytest.mark.parametrize("layout,refOrder", [("ref", 0), ("ref", 1), ("1t", 0)])
@@ -125,11 +126,13 @@ def test_refhost_mods_dropins_bitexact(layout, refOrder, tmp_path):
         return g, params, state, forcing
     m = configs.make_model(cfg)
     state = _write_blob(tmp_path / "refhost_in.bin", m, NSTEPS, monitor_days=2)
-    r = subprocess.run([exe, str(tmp_path)], capture_output=True, text=True, timeout=300)
+    env = dict(os.environ, MGCM_CG2D_REFORDER=str(refOrder))
+    r = subprocess.run([exe, str(tmp_path)], capture_output=True, text=True, timeout=300, env=env)
     assert r.returncode == 0, r.stdout + r.stderr
-    out, st = _read_out(tmp_path / "refhost_out.bin", state)
+    out, st = _read_out(tmp_path / "refhost_out.bin", state, NSTEPS)
     # the same configuration stepped by the graph-replayed resident path
-    m.forward_step(1)     # warm (first step, graph capture)
+    m.forward_step(1)     # warm (first step)
+    m.prepare()           # graphs built, overlap trial done: outside the timed steps
     m.sync()
     t0 = time.perf_counter()
     m.forward_step(NSTEPS - 1)
@@ -144,7 +147,10 @@ def test_refhost_mods_dropins_bitexact(layout, refOrder, tmp_path):
             bad.append((n, float(np.abs(out[n] - dev).max())))
     m.close()
     ms = 1e3 * st["seconds"] / max(1, st["steps_timed"])
-    rec = {"layout": layout, "cg2dRefOrder": refOrder, "dropin_ms_per_step": ms, "graph_ms_per_step": graph_ms,
+    # steps 3 and 5 end without a host reader: no state download, only the forcing upload
+    quiet = [st["step_ms"][i] for i in (2, 4)]
+    rec = {"layout": layout, "cg2dRefOrder": refOrder, "dropin_ms_per_step_mean": ms,
+           "dropin_ms_per_step_no_download": float(np.mean(quiet)), "graph_ms_per_step": graph_ms,
            "mirror": st, "state_fields": len(state)}
     print("refhost %s refOrder=%d: %s" % (layout, refOrder, json.dumps(rec)))
     if os.path.isdir(os.path.join(ROOT, "gpurun_out")):
