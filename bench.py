@@ -54,9 +54,10 @@ def parse():
     ap.add_argument("--shard", action="store_true",
                     help="N>1: shard the workload's tiles over the N processes (RCCL, strong scaling, "
                          "mitgcm_amd/parallel.py) instead of running N replicas")
-    ap.add_argument("--cg2d", choices=["replicated", "distributed"], default="replicated",
-                    help="with --shard: CG2D replicated on every GPU (default) or the reference's distributed "
-                         "CG2D with GLOBAL_SUM_TILE_RL over the collective (mitgcm_amd/parallel.py)")
+    ap.add_argument("--cg2d", choices=["replicated", "distributed", "device"], default="replicated",
+                    help="with --shard: CG2D replicated on every GPU (default), the reference's distributed "
+                         "CG2D with GLOBAL_SUM_TILE_RL over the collective, or the device CG2D whose parts run in "
+                         "every process on one IPC-shared hand-off block (mitgcm_amd/parallel.py)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--set", action="append", default=[], metavar="NAME=VALUE",
                     help="override a namelist parameter of the GPU model (A/B runs, e.g. useSRCGSolver=1); "
@@ -207,12 +208,28 @@ def cg_kernel_key(m):
 
 def main():
     a = parse()
+    # stdout carries ONE JSON line: whatever libraries print (RCCL's version banner at
+    # communicator creation, ...) goes to stderr
+    json_fd = os.dup(1)
+    os.dup2(2, 1)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
-    shard = a.shard and world > 1
-    if world > 1:
+    # --shard at N = 1 runs the sharded driver over a one-rank RCCL group: its per-step
+    # overhead against the resident graph is then measured on one GPU
+    shard = a.shard
+    if shard and world == 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        if "MASTER_PORT" not in os.environ:
+            import socket
+            sk = socket.socket()
+            sk.bind(("127.0.0.1", 0))
+            os.environ["MASTER_PORT"] = str(sk.getsockname()[1])
+            sk.close()
+        os.environ.setdefault("RANK", "0")
+        os.environ.setdefault("WORLD_SIZE", "1")
+    if world > 1 or shard:
         import torch
         import torch.distributed as dist
         if shard:
@@ -235,6 +252,8 @@ def main():
         k, v = kv.split("=", 1)
         over[k] = float(v)
     cfn = config_fn(a.config)
+    if shard and a.cg2d == "device":
+        over.setdefault("cg2dForceMwg", 1.0)   # the device CG2D runs the multi-workgroup solver's parts
     if over:
         cfn = (lambda f: lambda: (lambda r: (r[0], {**r[1], **over}) + tuple(r[2:]))(f()))(cfn)
     m = configs.make_model(cfn, device=local)
@@ -251,8 +270,18 @@ def main():
         if shard:
             torch.cuda.synchronize(local)
 
+    # the sharded step over RCCL with the replicated solve is graph-captured (two steps per
+    # graph, collectives included: ShardedModel.capture_step) and replayed, as the resident
+    # path is; gloo and the host-driven distributed CG2D step eagerly
+    graph_shard = shard and dist.get_backend() == "nccl" and a.cg2d != "distributed"
+    if graph_shard and a.steps % 2:
+        raise SystemExit("bench: --shard over RCCL replays pairs of steps: --steps must be even")
+
     # warmup (untimed)
-    if a.warmup > 0:
+    if graph_shard:
+        stepper.capture_step()            # one eager step, then the capture
+        stepper.replay(max(1, a.warmup // 2))
+    elif a.warmup > 0:
         stepper.forward_step(a.warmup)
     sync()
 
@@ -266,7 +295,10 @@ def main():
     barrier()
     sync()
     t0 = time.perf_counter()
-    stepper.forward_step(a.steps)
+    if graph_shard:
+        stepper.replay(a.steps // 2)
+    else:
+        stepper.forward_step(a.steps)
     sync()
     t1 = time.perf_counter()
     barrier()
@@ -346,6 +378,8 @@ def main():
                    "tiles_per_gpu": stepper.nT if shard else g.nTiles, "points_per_tile": [g.sNx, g.sNy, g.Nr],
                    "parallelism": ("tiles%d" if shard else "replicas%d") % world,
                    "cg2d": a.cg2d if shard else "single-GPU kernel",
+                   **({"step_path": "graph-replayed sharded step (RCCL collectives captured)" if graph_shard
+                       else "eager sharded step"} if shard else {}),
                    **({"params_over": over} if over else {})},
         "cg2d_iters_per_s": cg2d_iters_per_s,
         # THERMODYNAMICS on a second stream beside DYNAMICS: picked per workload by timing both
@@ -378,7 +412,8 @@ def main():
     if rank == 0 and world == 1 and not a.no_cpu_baseline:   # the CPU baseline is an N=1 line
         out["cpu_baseline"] = cpu_baseline(a.config, a.cpu_seconds)
     if rank == 0:
-        print(json.dumps(out), flush=True)
+        sys.stdout.flush()
+        os.write(json_fd, (json.dumps(out) + "\n").encode())
     m.close()
     if dist is not None:
         dist.destroy_process_group()

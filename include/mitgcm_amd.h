@@ -133,12 +133,27 @@ int mgcm_exchange_nfields(mgcm_model *m);
 /* Gather (unpack=0) / scatter (unpack=1) those fields at n device-resident 2-D
  * offsets idx (t*n2 + j*nx + i), all levels: buf[(f*Nr + k)*n + h]. */
 int mgcm_halo_pack(mgcm_model *m, const long *idx, long n, double *buf, int unpack);
+/* The same for a group of them: 0 all, 1 the tracers (final after THERMODYNAMICS, so their
+ * exchange can overlap DYNAMICS and the solve: pkg/exch2/exch2_rx1_cube.template:118-247's
+ * PUT/send ... recv/GET split), 2 the rest; -1 from the count for a bad group. */
+int mgcm_exchange_nfields_group(mgcm_model *m, int group);
+int mgcm_halo_pack_group(mgcm_model *m, int group, const long *idx, long n, double *buf, int unpack);
+/* Order the model's stream against a caller's stream `other` (a hipStream_t): direction 0
+ * = `other` waits for the model's work so far (its outputs are then readable there), 1 =
+ * the model waits for `other`'s work so far (e.g. a received buffer).  No-op when they are
+ * the same stream. */
+int mgcm_stream_handoff(mgcm_model *m, void *other, int direction);
 /* Device-to-device copy of tiles [t0, t0+nT) of a 2-D/3-D field to (toField=0) or
  * from (toField=1) the device buffer buf, on the model's stream. */
 int mgcm_tile_copy(mgcm_model *m, const char *name, int t0, int nT, void *buf, int toField);
 /* Reset the per-step solve records before a sequence of mgcm_step_phase steps. */
 int mgcm_begin_steps(mgcm_model *m);
-/* One FORWARD_STEP split at its exchange points, phase = 1..4 (see model.hip). */
+/* After replaying caller-captured steps: the batch recorded nsteps solve records. */
+int mgcm_end_steps(mgcm_model *m, int nsteps);
+/* One FORWARD_STEP split at its exchange points (model.hip): 1 = 8 + 9; 8 DO_OCEANIC_PHYS +
+ * THERMODYNAMICS; 9 DYNAMICS + UPDATE_R_STAR/CG2D + CALC_DIV_GHAT; 2 CG2D + correction +
+ * continuity; 10 the device CG2D over this process's parts; 6 = 2 after a CG2D done
+ * outside phase 2; 3 r*; 5 staggered tracers; 4 exchanges. */
 int mgcm_step_phase(mgcm_model *m, int phase);
 /* Distributed CG2D (mitgcm_amd/parallel.py, cg2dMode = "distributed"): one operation of
  * model/src/cg2d.F:100-415 over this process's tiles (op 0 normalise + max, 1 scale by a0,
@@ -147,6 +162,15 @@ int mgcm_step_phase(mgcm_model *m, int phase);
  * values GLOBAL_SUM_TILE_RL (eesupp/src/global_sum_tile.F:14-17,161-191) sums in tile order.
  * Phase 6 of mgcm_step_phase finishes phase 2 after such a solve. */
 int mgcm_cg2d_op(mgcm_model *m, int op, double a0, double *part);
+/* The tile-sharded device CG2D (parallel.py cg2d="device", phase 10 of mgcm_step_phase):
+ * the multi-workgroup solver's parts of this process's tiles, on one hand-off block shared
+ * by all processes -- exported (IPC handle of mgcm_cg2d_shared_bytes bytes) by one process
+ * and mapped by the others; the solve's sums are the single-process sums, no host step
+ * inside an iteration.  Needs whole-domain multi-workgroup tables (param cg2dForceMwg on
+ * grids the single-workgroup kernels would take). */
+int mgcm_cg2d_shared_bytes(mgcm_model *m);
+int mgcm_cg2d_shared_export(mgcm_model *m, void *handle);
+int mgcm_cg2d_shared_import(mgcm_model *m, const void *handle);
 /* Store CG2D's output arguments (cg2d.F:13-17) as this step's solve record. */
 int mgcm_cg2d_record(mgcm_model *m, double firstResidual, double lastResidual, double rhsMax, double sumRHS,
                      int numIters);

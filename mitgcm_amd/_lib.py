@@ -58,7 +58,14 @@ def lib():
         "mgcm_set_stream": (ci, [vp, vp]),
         "mgcm_exchange_nfields": (ci, [vp]),
         "mgcm_halo_pack": (ci, [vp, vp, cl, vp, ci]),
+        "mgcm_halo_pack_group": (ci, [vp, ci, vp, cl, vp, ci]),
+        "mgcm_exchange_nfields_group": (ci, [vp, ci]),
+        "mgcm_stream_handoff": (ci, [vp, vp, ci]),
         "mgcm_begin_steps": (ci, [vp]),
+        "mgcm_end_steps": (ci, [vp, ci]),
+        "mgcm_cg2d_shared_bytes": (ci, [vp]),
+        "mgcm_cg2d_shared_export": (ci, [vp, vp]),
+        "mgcm_cg2d_shared_import": (ci, [vp, vp]),
         "mgcm_tile_copy": (ci, [vp, cs, ci, ci, vp, ci]),
         "mgcm_step_phase": (ci, [vp, ci]),
         "mgcm_cg2d_op": (ci, [vp, ci, cd, vp]),
@@ -97,7 +104,8 @@ EXPORTS = ["mgcm_create", "mgcm_destroy", "mgcm_last_error", "mgcm_set_param", "
            "exch_uv_xy_rl_amd_", "exch_uv_xyz_rl_amd_", "global_sum_tile_rl_amd_",
            "mgcm_update_r_star", "mgcm_calc_r_star", "update_r_star_amd_", "update_cg2d_amd_", "calc_r_star_amd_",
            "mgcm_set_iter", "mgcm_amd_host_sync_", "mgcm_amd_device_sync_", "mgcm_amd_transfer_stats_",
-           "mgcm_amd_step_fence_"]
+           "mgcm_amd_step_fence_", "mgcm_halo_pack_group", "mgcm_exchange_nfields_group", "mgcm_stream_handoff",
+           "mgcm_end_steps", "mgcm_cg2d_shared_bytes", "mgcm_cg2d_shared_export", "mgcm_cg2d_shared_import"]
 
 
 def check(rc, what):

@@ -39,6 +39,10 @@ namespace mgcm {
 typedef __attribute__((address_space(1))) unsigned long long gu64;
 typedef __attribute__((address_space(1))) unsigned int gu32;
 #define RLX_AGENT __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT
+// SYS: the hand-off block is shared with other processes' launches (the tile-sharded
+// device CG2D, parallel.py cg2d="device"; mapped by IPC, possibly on a peer GPU): every
+// granule access at system scope
+#define RLX_SCOPE(SYS) __ATOMIC_RELAXED, ((SYS) ? __HIP_MEMORY_SCOPE_SYSTEM : __HIP_MEMORY_SCOPE_AGENT)
 
 // ---- DPP sums (the same operations as kernels_solve.hip's block reductions) ----
 template <int CTRL>
@@ -101,13 +105,15 @@ constexpr int MW_NT = MGCM_MW_NT, MW_OPT = MGCM_MW_OPT, MW_RPT = 1, MW_NW = MW_N
 constexpr int MW_NV = 3;   // values per reduction
 
 // ---- granule hand-offs (Guideline 16 R2) -------------------------------------------
+template <bool SYS = false>
 __device__ __forceinline__ void gran_put(gu64 *g, unsigned tag, double v) {
   const unsigned long long b = __builtin_bit_cast(unsigned long long, v), t = (unsigned long long)tag << 32;
-  __hip_atomic_store(g, t | (b & 0xffffffffull), RLX_AGENT);
-  __hip_atomic_store(g + 1, t | (b >> 32), RLX_AGENT);
+  __hip_atomic_store(g, t | (b & 0xffffffffull), RLX_SCOPE(SYS));
+  __hip_atomic_store(g + 1, t | (b >> 32), RLX_SCOPE(SYS));
 }
+template <bool SYS = false>
 __device__ __forceinline__ bool gran_get(gu64 *g, unsigned tag, double &v) {
-  const unsigned long long lo = __hip_atomic_load(g, RLX_AGENT), hi = __hip_atomic_load(g + 1, RLX_AGENT);
+  const unsigned long long lo = __hip_atomic_load(g, RLX_SCOPE(SYS)), hi = __hip_atomic_load(g + 1, RLX_SCOPE(SYS));
   v = __builtin_bit_cast(double, ((hi & 0xffffffffull) << 32) | (lo & 0xffffffffull));
   return (unsigned)(lo >> 32) == tag && (unsigned)(hi >> 32) == tag;
 }
@@ -117,9 +123,10 @@ __device__ __forceinline__ bool gran_get(gu64 *g, unsigned tag, double &v) {
 // word ctr[1] holds epoch + 1 of a launch that gave up (the epoch then advances by 2).
 __device__ __forceinline__ unsigned mw_tag(unsigned ep, int phase) { return ((ep & 0xffffu) << 16) | (unsigned)phase; }
 // bounded spin: after ~2^22 passes every part gives up (timeout word), so no wave hangs
+template <bool SYS = false>
 __device__ __forceinline__ bool spin_fail(unsigned &spins, gu32 *tmo, unsigned ep) {
-  if (__hip_atomic_load(tmo, RLX_AGENT) == ep + 1u || ++spins > (1u << 22)) {
-    __hip_atomic_store(tmo, ep + 1u, RLX_AGENT);
+  if (__hip_atomic_load(tmo, RLX_SCOPE(SYS)) == ep + 1u || ++spins > (1u << 22)) {
+    __hip_atomic_store(tmo, ep + 1u, RLX_SCOPE(SYS));
     return true;
   }
   __builtin_amdgcn_s_sleep(1);
@@ -137,7 +144,7 @@ struct MwImport {
   double *imp_l;   // LDS staging, nImp doubles
 };
 
-template <int NV, bool MAXOP>
+template <int NV, bool MAXOP, bool SYS = false>
 __device__ __forceinline__ bool mw_sync(double *v, const MwgTables &T, int g, int &nsync, double *red, unsigned ep,
                                         const MwImport *imp = nullptr) {
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
@@ -158,7 +165,7 @@ __device__ __forceinline__ bool mw_sync(double *v, const MwgTables &T, int g, in
     for (int q = 0; q < NV; q++) {
       const double xw = l < MW_NW ? red[q * 16 + l] : 0.0;
       const double wgp = MAXOP ? mw_rowmax16(xw) : mw_row16(xw);
-      if (lane == 0) gran_put(P + ((size_t)q * T.G + g) * 2, tag, wgp);
+      if (lane == 0) gran_put<SYS>(P + ((size_t)q * T.G + g) * 2, tag, wgp);
     }
     // combine: lane l adds partials l, l+64, ... in order, then the pairwise tree over the
     // lanes; the whole sweep is repeated until every granule carries this phase's tag
@@ -172,12 +179,12 @@ __device__ __forceinline__ bool mw_sync(double *v, const MwgTables &T, int g, in
         acc[q] = 0.0;
         for (int gg = lane; gg < T.G; gg += 64) {
           double xg;
-          good = gran_get(P + ((size_t)q * T.G + gg) * 2, tag, xg) && good;
+          good = gran_get<SYS>(P + ((size_t)q * T.G + gg) * 2, tag, xg) && good;
           acc[q] = MAXOP ? fmax(acc[q], xg) : acc[q] + xg;
         }
       }
       if (__all(good)) break;
-      if (spin_fail(spins, (gu32 *)T.ctr + 1, ep)) { ok = false; break; }
+      if (spin_fail<SYS>(spins, (gu32 *)T.ctr + 1, ep)) { ok = false; break; }
     }
 #pragma unroll
     for (int q = 0; q < NV; q++) {
@@ -193,9 +200,9 @@ __device__ __forceinline__ bool mw_sync(double *v, const MwgTables &T, int g, in
       double xv = 0.0;
       unsigned spins = 0;
       for (;;) {
-        const bool good = !act || gran_get(src, tag, xv);
+        const bool good = !act || gran_get<SYS>(src, tag, xv);
         if (__all(good)) break;
-        if (spin_fail(spins, (gu32 *)T.ctr + 1, ep)) break;   // the timeout word fails the solve
+        if (spin_fail<SYS>(spins, (gu32 *)T.ctr + 1, ep)) break;   // the timeout word fails the solve
       }
       if (act) imp->imp_l[qq] = xv;
     }
@@ -222,15 +229,19 @@ __device__ __forceinline__ bool mw_sync(double *v, const MwgTables &T, int g, in
   } while (0)
 #endif
 
-template <bool PINNED>
+// g0, gN: this launch runs parts g0 .. g0+gN-1 of the T.G (all of them in one process; a
+// process's tiles' parts in the tile-sharded device CG2D, whose other parts run in the other
+// processes' launches on the same hand-off block)
+template <bool PINNED, bool SYS>
 __global__ void __launch_bounds__(MW_NT) k_cg2d_mwg(Dims d, Params p, Fields f, MwgTables T, int maxIters,
-                                                    SolveRecord *rec, int *stepCounter) {
+                                                    SolveRecord *rec, int *stepCounter, int g0, int gN) {
   int g = (int)blockIdx.x;
   if (PINNED) {
     if (g % MG_NXCD) return;   // parts on XCD 0 only: their hand-offs stay in one L2
     g /= MG_NXCD;
   }
-  if (g >= T.G) return;
+  if (g >= gN) return;
+  g += g0;
   constexpr int NO = MW_OPT * MW_NT, NR = MW_RPT * MW_NT;
   extern __shared__ __attribute__((aligned(16))) double lds[];
   const int SZ = T.SZ;            // own + ring 1 + ring 2 slots; ZERO slot = SZ
@@ -240,7 +251,7 @@ __global__ void __launch_bounds__(MW_NT) k_cg2d_mwg(Dims d, Params p, Fields f, 
   double *imp_l = red + 16 * 16;      // IMAX: the ring q handed off at the last reduction
   const int tid = threadIdx.x;
   int nsync = 0;
-  const unsigned ep = __hip_atomic_load((gu32 *)T.ctr, RLX_AGENT);
+  const unsigned ep = __hip_atomic_load((gu32 *)T.ctr, RLX_SCOPE(SYS));
   const size_t go = (size_t)g * NO, gr = (size_t)g * NR, gi = (size_t)g * T.IMAX;
   // ---- owned points: offsets, neighbour slots, coefficients (cg2d.F operator rows)
   int G2[MW_OPT];
@@ -293,7 +304,7 @@ __global__ void __launch_bounds__(MW_NT) k_cg2d_mwg(Dims d, Params p, Fields f, 
   double rhsMaxV[1] = {0.0};
 #pragma unroll
   for (int m = 0; m < MW_OPT; m++) { b[m] = b[m] * p.cg2dNorm; rhsMaxV[0] = fmax(fabs(b[m]), rhsMaxV[0]); }
-  bool ok = mw_sync<1, true>(rhsMaxV, T, g, nsync, red, ep);
+  bool ok = mw_sync<1, true, SYS>(rhsMaxV, T, g, nsync, red, ep);
   const double rhsMax = rhsMaxV[0];
   double rhsNorm = 1.0;
   if (p.cg2dNormaliseRHS) {
@@ -342,10 +353,10 @@ __global__ void __launch_bounds__(MW_NT) k_cg2d_mwg(Dims d, Params p, Fields f, 
     q[m] = pC[m] * r[m] + pW0[m] * r_l[LO(nwe[m])] + pW1[m] * r_l[HI(nwe[m])] + pS0[m] * r_l[LO(nsn[m])] +
            pS1[m] * r_l[HI(nsn[m])];
     v3[2] = v3[2] + q[m] * r[m];
-    if ((exp >> m) & 1u) gran_put(xs + (size_t)2 * T.ownC[go + m * MW_NT + tid], mw_tag(ep, nsync + 1), q[m]);
+    if ((exp >> m) & 1u) gran_put<SYS>(xs + (size_t)2 * T.ownC[go + m * MW_NT + tid], mw_tag(ep, nsync + 1), q[m]);
   }
   for (int qq = tid; qq < nImp; qq += MW_NT) s_l[NO + qq] = 0.0;
-  ok = ok && mw_sync<3, false>(v3, T, g, nsync, red, ep, &imp);
+  ok = ok && mw_sync<3, false, SYS>(v3, T, g, nsync, red, ep, &imp);
   double err_sq = v3[0];
   const double sumRHS = v3[1];
   double eta_qrN = v3[2], eta_qrNM1 = 1.0;
@@ -386,7 +397,7 @@ __global__ void __launch_bounds__(MW_NT) k_cg2d_mwg(Dims d, Params p, Fields f, 
         rq[m] = raW0[m] * s_l[LO(rwe[m])] + raW1[m] * s_l[HI(rwe[m])] + raS0[m] * s_l[LO(rsn[m])] +
                 raS1[m] * s_l[HI(rsn[m])] + raC[m] * s_l[NO + m * MW_NT + tid];
       MW_STAMP(2);
-      ok = mw_sync<1, false>(av, T, g, nsync, red, ep);
+      ok = mw_sync<1, false, SYS>(av, T, g, nsync, red, ep);
       MW_STAMP(3);
       if (!ok) break;
       const double alpha = eta_qrN / av[0];
@@ -411,10 +422,10 @@ __global__ void __launch_bounds__(MW_NT) k_cg2d_mwg(Dims d, Params p, Fields f, 
         q[m] = pC[m] * r[m] + pW0[m] * r_l[LO(nwe[m])] + pW1[m] * r_l[HI(nwe[m])] + pS0[m] * r_l[LO(nsn[m])] +
                pS1[m] * r_l[HI(nsn[m])];
         v2[1] = v2[1] + q[m] * r[m];
-        if ((exp >> m) & 1u) gran_put(xs + (size_t)2 * T.ownC[go + m * MW_NT + tid], mw_tag(ep, nsync + 1), q[m]);
+        if ((exp >> m) & 1u) gran_put<SYS>(xs + (size_t)2 * T.ownC[go + m * MW_NT + tid], mw_tag(ep, nsync + 1), q[m]);
       }
       MW_STAMP(4);
-      ok = mw_sync<2, false>(v2, T, g, nsync, red, ep, &imp);
+      ok = mw_sync<2, false, SYS>(v2, T, g, nsync, red, ep, &imp);
       MW_STAMP(5);
       if (!ok) break;
       err_sq = v2[0];
@@ -434,7 +445,9 @@ __global__ void __launch_bounds__(MW_NT) k_cg2d_mwg(Dims d, Params p, Fields f, 
     if (p.cg2dNormaliseRHS) xv = xv / rhsNorm;
     if (G2[m] >= 0) f.cg2d_x[G2[m]] = xv;
   }
-  if (g == 0 && tid == 0) {
+  // the record by the launch's first part (every part holds the same reduced values); the
+  // epoch by part 0 of the whole solve
+  if (g == g0 && tid == 0) {
     const int st = stepCounter ? *stepCounter : 0;
     SolveRecord &R = rec[st];
     R.firstResidual = firstResidual;
@@ -442,13 +455,14 @@ __global__ void __launch_bounds__(MW_NT) k_cg2d_mwg(Dims d, Params p, Fields f, 
     R.minResidualSq = -1.0;
     R.rhsMax = rhsMax;
     R.sumRHS = sumRHS;
-    const bool tmo = __hip_atomic_load((gu32 *)T.ctr + 1, RLX_AGENT) == ep + 1u;
+    const bool tmo = __hip_atomic_load((gu32 *)T.ctr + 1, RLX_SCOPE(SYS)) == ep + 1u;
     R.numIters = (ok && !tmo) ? actualIts : -1;   // -1: a grid hand-off timed out
     R.nIterMin = -1;
+    if (g != 0) return;
     // the next launch's epoch; after a timeout it skips one, so a part of this launch that
     // starts late (reading ep + 1, tagging with it, failing into the timeout word as ep + 2)
     // can neither match the next launch's tags nor fail it
-    __hip_atomic_store((gu32 *)T.ctr, R.numIters < 0 ? ep + 2u : ep + 1u, RLX_AGENT);
+    __hip_atomic_store((gu32 *)T.ctr, R.numIters < 0 ? ep + 2u : ep + 1u, RLX_SCOPE(SYS));
   }
 #undef LO
 #undef HI
@@ -457,20 +471,25 @@ __global__ void __launch_bounds__(MW_NT) k_cg2d_mwg(Dims d, Params p, Fields f, 
 int cg2d_mwg_geometry(int *nt, int *opt, int *rpt) { *nt = MW_NT; *opt = MW_OPT; *rpt = MW_RPT; return 0; }
 
 hipError_t launch_cg2d_mwg(const Dims &d, const Params &p, const Fields &f, const MwgTables &T, int maxIters,
-                           SolveRecord *rec, int *stepCounter, hipStream_t s) {
+                           SolveRecord *rec, int *stepCounter, hipStream_t s, int g0, int gN) {
   // phases per launch: 2 + 2 per iteration, below 2^16 (the tag's phase field)
   if (maxIters < 0 || maxIters > 30000) return hipErrorInvalidValue;
+  if (gN < 0) { g0 = 0; gN = T.G; }
+  if (g0 < 0 || gN < 1 || g0 + gN > T.G) return hipErrorInvalidValue;
   hipError_t e = hipSuccess;
   const size_t lds = (size_t)(2 * (T.SZ + 1) + 16 * 16 + T.IMAX) * sizeof(double);
-  auto kern = T.pinned ? k_cg2d_mwg<true> : k_cg2d_mwg<false>;
-  static bool attrSet[2] = {false, false};
-  if (!attrSet[T.pinned]) {
+  const bool pinned = T.pinned && !T.sys && gN == T.G;
+  const int v = (pinned ? 1 : 0) + (T.sys ? 2 : 0);
+  auto kern = v == 3 ? k_cg2d_mwg<true, true> : v == 2 ? k_cg2d_mwg<false, true>
+            : v == 1 ? k_cg2d_mwg<true, false> : k_cg2d_mwg<false, false>;
+  static bool attrSet[4] = {false, false, false, false};
+  if (!attrSet[v]) {
     e = hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     if (e != hipSuccess) return e;
-    attrSet[T.pinned] = true;
+    attrSet[v] = true;
   }
-  const unsigned grid = (unsigned)(T.pinned ? T.G * MG_NXCD : T.G);
-  hipLaunchKernelGGL(kern, dim3(grid), dim3(MW_NT), lds, s, d, p, f, T, maxIters, rec, stepCounter);
+  const unsigned grid = (unsigned)(pinned ? gN * MG_NXCD : gN);
+  hipLaunchKernelGGL(kern, dim3(grid), dim3(MW_NT), lds, s, d, p, f, T, maxIters, rec, stepCounter, g0, gN);
   return hipGetLastError();
 }
 

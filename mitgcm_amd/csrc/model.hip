@@ -57,7 +57,7 @@ hipError_t launch_tracer_step(const Dims &, const Params &, const Fields &, cons
 hipError_t launch_mon_stats(const Dims &, const MonSpecs &, int, double *, int, hipStream_t);
 int cg2d_mwg_geometry(int *, int *, int *);
 hipError_t launch_cg2d_mwg(const Dims &, const Params &, const Fields &, const MwgTables &, int, SolveRecord *, int *,
-                           hipStream_t);
+                           hipStream_t, int g0 = 0, int gN = -1);
 }  // namespace mgcm
 
 using namespace mgcm;
@@ -147,6 +147,7 @@ struct mgcm_model {
   // DO_OCEANIC_PHYS, join before UPDATE_R_STAR / SOLVE_FOR_PRESSURE; MGCM_NO_OVERLAP=1 off)
   hipStream_t stream2 = nullptr;
   hipEvent_t evFork = nullptr, evJoin = nullptr;
+  hipEvent_t evHand = nullptr;   // mgcm_stream_handoff
   bool overlap = true;
   std::vector<void *> allocs;
   // extra parameters kept on host only
@@ -173,6 +174,7 @@ struct mgcm_model {
   bool useMwg = false;
   MwgTables mwg{};
   std::vector<void *> mwgAllocs;
+  void *mwgShared = nullptr;   // another process's hand-off block, opened by IPC (mgcm_cg2d_shared_import)
   std::vector<int> mwgPlan;   // summation plan for mgcm_cg2d_sum_plan: [(g*OPT + p)*NT + tid]
   // EXCH2 C-grid vector maps (mgcm_set_uv_map): [withSigns] -> (dst, code) pairs of this
   // process's tiles, u entries first; code = +-(src+1), src indexing [u | v]
@@ -643,6 +645,8 @@ static int build_mwg(mgcm_model *m) {
     return -1;
   T.G = G; T.IMAX = IMAX; T.SZ = SZ;
   T.pinned = (G <= 32 && !getenv("MGCM_CG2D_SPREAD")) ? 1 : 0;
+  T.sys = 0;
+  T.partsPerTile = (d.t0 == 0 && d.nT == d.nTiles) ? nPartsTile : 0;   // part ranges: whole-domain tables only
   // hand-off block: 64 B of words (launch epoch, timeout word), the partial granules, the
   // export granules; zeroed once here -- granule tags carry the launch epoch, so a launch
   // never matches an earlier launch's granules (a multiple of 16 B from the start)
@@ -706,6 +710,7 @@ mgcm_model *mgcm_create(int sNx, int sNy, int OLx, int OLy, int Nr, int nSx, int
   m->stream = m->ownStream;
   if (hipStreamCreateWithFlags(&m->stream2, hipStreamNonBlocking) != hipSuccess ||
       hipEventCreateWithFlags(&m->evFork, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&m->evHand, hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&m->evJoin, hipEventDisableTiming) != hipSuccess ||
       hipEventCreate(&m->ovlEv[0]) != hipSuccess || hipEventCreate(&m->ovlEv[1]) != hipSuccess) {
     set_err("mgcm_create: second stream / events");
@@ -789,10 +794,12 @@ void mgcm_destroy(mgcm_model *m) {
   for (auto &q : m->exchBuf)
     if (q) hipFree(q);
   if (m->d_rec) hipFree(m->d_rec);
+  if (m->mwgShared) (void)hipIpcCloseMemHandle(m->mwgShared);
   for (void *q : m->mwgAllocs) hipFree(q);
   if (m->ownStream) hipStreamDestroy(m->ownStream);
   if (m->stream2) hipStreamDestroy(m->stream2);
   if (m->evFork) hipEventDestroy(m->evFork);
+  if (m->evHand) hipEventDestroy(m->evHand);
   if (m->evJoin) hipEventDestroy(m->evJoin);
   for (auto &ev : m->ovlEv)
     if (ev) hipEventDestroy(ev);
@@ -999,7 +1006,12 @@ int mgcm_init(mgcm_model *m) {
       return set_err("mgcm_init: cg2dRefOrder needs <= %d interior points (one workgroup), have %d",
                      cg2d_ref_max_points(), m->nPts);
     if (m->p.useSRCGSolver) return set_err("mgcm_init: cg2dRefOrder with useSRCGSolver not implemented");
-  } else if (m->nBlkX == 0 && m->nBlk == 0 && !(single && m->nPts <= cg2d_block_max_points())) {
+  } else if ((m->nBlkX == 0 && m->nBlk == 0 && !(single && m->nPts <= cg2d_block_max_points())) ||
+             ext("cg2dForceMwg", 0.0) != 0.0) {
+    // cg2dForceMwg: the multi-workgroup solver on a grid the single-workgroup kernels would
+    // take (the tile-sharded device CG2D runs its parts in several processes)
+    m->nBlkX = 0;
+    m->nBlk = 0;
     if (build_mwg(m)) return -1;
     if (m->p.cg2dUseMinResSol) return set_err("mgcm_init: cg2dUseMinResSol with the multi-workgroup CG2D not implemented");
   }
@@ -1523,21 +1535,51 @@ int mgcm_set_stream(mgcm_model *m, void *stream) {
 // The 3-D fields whose halo sources travel between processes: the blocking-exchange set
 // with u and v always included (on an EXCH2 topology the vector map may read either
 // component of a source point, exch2_uv_3d_rx.template).
-static XFields transfer_fields(const mgcm_model *m) {
+// group 0: all of them; 1: the tracers (final once THERMODYNAMICS has run, so their
+// exchange can travel while DYNAMICS and the solve compute); 2: the rest.
+static XFields transfer_fields(const mgcm_model *m, int group = 0) {
   XFields x{};
   double *fl[] = {m->f.uVel, m->f.vVel, m->f.wVel, m->f.theta, m->f.salt, m->f.uVelD, m->f.vVelD, m->f.totPhiHyd};
   const bool use[] = {true, true, true, m->p.tempStepping != 0, m->p.saltStepping != 0, m->p.useCDscheme != 0,
                       m->p.useCDscheme != 0, m->p.storePhiHyd4Phys != 0};
+  const bool tracer[] = {false, false, false, true, true, false, false, false};
   for (int q = 0; q < 8; q++)
-    if (use[q]) { x.p[x.n] = fl[q]; x.nz[x.n] = m->d.Nr; x.n++; }
+    if (use[q] && (group == 0 || (group == 1) == tracer[q])) { x.p[x.n] = fl[q]; x.nz[x.n] = m->d.Nr; x.n++; }
   return x;
 }
 
 int mgcm_exchange_nfields(mgcm_model *m) { return transfer_fields(m).n; }
+int mgcm_exchange_nfields_group(mgcm_model *m, int group) {
+  if (group < 0 || group > 2) return -1;
+  return transfer_fields(m, group).n;
+}
 
 int mgcm_halo_pack(mgcm_model *m, const long *idx, long n, double *buf, int unpack) {
+  return mgcm_halo_pack_group(m, 0, idx, n, buf, unpack);
+}
+
+int mgcm_halo_pack_group(mgcm_model *m, int group, const long *idx, long n, double *buf, int unpack) {
   if (check_ready(m)) return -1;
-  HIPCHK(launch_halo_pack(m->d, transfer_fields(m), idx, n, buf, unpack, m->stream));
+  if (group < 0 || group > 2) return set_err("mgcm_halo_pack_group: no group %d", group);
+  HIPCHK(launch_halo_pack(m->d, transfer_fields(m, group), idx, n, buf, unpack, m->stream));
+  return 0;
+}
+
+// Cross-stream ordering for callers whose collectives run on another stream: direction 0
+// makes `other` wait for the work issued on the model's stream so far (the model's outputs,
+// e.g. a packed halo buffer or tile partials, are then safe to read there); 1 makes the
+// model's stream wait for the work issued on `other` so far (e.g. a received buffer).
+int mgcm_stream_handoff(mgcm_model *m, void *other, int direction) {
+  hipStream_t o = (hipStream_t)other;
+  if (o == m->stream) return 0;
+  HIPCHK(hipSetDevice(m->device));
+  if (direction == 0) {
+    HIPCHK(hipEventRecord(m->evHand, m->stream));
+    HIPCHK(hipStreamWaitEvent(o, m->evHand, 0));
+  } else {
+    HIPCHK(hipEventRecord(m->evHand, o));
+    HIPCHK(hipStreamWaitEvent(m->stream, m->evHand, 0));
+  }
   return 0;
 }
 
@@ -1549,6 +1591,52 @@ int mgcm_tile_copy(mgcm_model *m, const char *name, int t0, int nT, void *buf, i
   double *f = field_ptr(m, fd) + t0 * per;
   const size_t bytes = (size_t)nT * per * sizeof(double);
   HIPCHK(hipMemcpyAsync(toField ? f : buf, toField ? buf : f, bytes, hipMemcpyDeviceToDevice, m->stream));
+  return 0;
+}
+
+// The tile-sharded device CG2D: every process launches the multi-workgroup solver's parts
+// of its own tiles, all on ONE hand-off block (granules, epoch, timeout word), which the
+// first process exports by IPC and the others map; every granule access is then at system
+// scope.  The sums keep the single-launch order, so the solve is the 1-process solve.
+int mgcm_cg2d_shared_export(mgcm_model *m, void *handle) {
+  if (!m->useMwg || m->mwg.partsPerTile <= 0)
+    return set_err("mgcm_cg2d_shared_export: needs the multi-workgroup CG2D on whole-domain tables (cg2dForceMwg)");
+  HIPCHK(hipSetDevice(m->device));
+  HIPCHK(hipStreamSynchronize(m->stream));
+  hipIpcMemHandle_t h;
+  HIPCHK(hipIpcGetMemHandle(&h, (void *)m->mwg.ctr));
+  memcpy(handle, &h, sizeof h);
+  m->mwg.sys = 1;
+  return 0;
+}
+
+int mgcm_cg2d_shared_import(mgcm_model *m, const void *handle) {
+  if (!m->useMwg || m->mwg.partsPerTile <= 0)
+    return set_err("mgcm_cg2d_shared_import: needs the multi-workgroup CG2D on whole-domain tables (cg2dForceMwg)");
+  HIPCHK(hipSetDevice(m->device));
+  HIPCHK(hipStreamSynchronize(m->stream));
+  if (m->mwgShared) { (void)hipIpcCloseMemHandle(m->mwgShared); m->mwgShared = nullptr; }
+  hipIpcMemHandle_t h;
+  memcpy(&h, handle, sizeof h);
+  void *p = nullptr;
+  HIPCHK(hipIpcOpenMemHandle(&p, h, hipIpcMemLazyEnablePeerAccess));
+  m->mwgShared = p;
+  const size_t partGr = (size_t)2 * 3 * m->mwg.G * 2;
+  m->mwg.ctr = (unsigned *)p;
+  m->mwg.part = (unsigned long long *)((char *)p + 64);
+  m->mwg.xs = m->mwg.part + partGr;
+  m->mwg.sys = 1;
+  drop_graphs(m);
+  return 0;
+}
+
+int mgcm_cg2d_shared_bytes(mgcm_model *m) { return m->useMwg ? (int)sizeof(hipIpcMemHandle_t) : -1; }
+
+// After a caller replays its own captured steps (ShardedModel.replay): the number of steps
+// the batch recorded, so mgcm_solve_stats finds them.
+int mgcm_end_steps(mgcm_model *m, int nsteps) {
+  if (nsteps < 0 || nsteps > m->maxRec) return set_err("mgcm_end_steps: nsteps %d out of range", nsteps);
+  m->lastBatch = nsteps;
   return 0;
 }
 
@@ -1577,9 +1665,13 @@ int mgcm_step_phase(mgcm_model *m, int phase) {
   if (!m->p.momStepping) return set_err("mgcm_step_phase: requires momStepping");
   const bool stagger = m->p.staggerTimeStep != 0;
   switch (phase) {
-    case 1:
+    case 1:   // = 8 then 9
+    case 8:   // DO_OCEANIC_PHYS + THERMODYNAMICS (non-staggered): the tracers are final
       TIMED(K_PHYS, launch_oceanic_phys(m->d, m->p, m->f, m->d_ctr, m->stream));
       if (!stagger && tracers_on(m, m->stream)) return -1;
+      if (phase == 8) return 0;
+      [[fallthrough]];
+    case 9:   // DYNAMICS, UPDATE_R_STAR + UPDATE_CG2D, CALC_DIV_GHAT
       if (mgcm_dynamics(m)) return -1;
       if (m->p.nonlinFreeSurf > 0) TIMED(K_RSTAR, update_r_star_cg2d(m));
       TIMED(K_RHS, launch_sfp_rhs(m->d, m->p, m->f, m->stream));
@@ -1588,6 +1680,14 @@ int mgcm_step_phase(mgcm_model *m, int phase) {
       TIMED(K_CG2D, launch_cg2d(m, m->p.cg2dMaxIters, m->p.cg2dUseMinResSol - 1));
       TIMED(K_ETA, launch_exch_eta(m->d, m->p, m->f, m->d_srcOf, false, 0, m->stream));
       TIMED(K_CONT, launch_corr_cont(m->d, m->p, m->f, 0, m->stream));
+      return 0;
+    case 10:  // the device CG2D over this process's parts (hand-off block shared by IPC)
+      if (!m->useMwg || m->mwg.partsPerTile <= 0)
+        return set_err("mgcm_step_phase(10): needs the multi-workgroup CG2D on whole-domain tables (cg2dForceMwg)");
+      if (m->d.nT < m->d.nTiles && !m->mwg.sys)
+        return set_err("mgcm_step_phase(10): a tile subset needs the shared hand-off block (mgcm_cg2d_shared_*)");
+      TIMED(K_CG2D, launch_cg2d_mwg(m->d, m->p, m->f, m->mwg, m->p.cg2dMaxIters, m->d_rec, m->d_ctr + 1, m->stream,
+                                    m->d.t0 * m->mwg.partsPerTile, m->d.nT * m->mwg.partsPerTile));
       return 0;
     case 6:   // phase 2 after a CG2D driven by the caller (mgcm_cg2d_op: distributed CG2D)
       TIMED(K_ETA, launch_exch_eta(m->d, m->p, m->f, m->d_srcOf, false, 0, m->stream));

@@ -23,6 +23,11 @@ The MI355X design keeps the 3-D work sharded and the 2-D solve replicated:
   (~4k-105k points, ~35-125 iterations): the replicated solve needs no
   collective inside the iteration, and its sums are exactly the 1-GPU sums, so
   results are bit-identical at any GPU count (SURVEY.md 8(c) parity item 6);
+* cg2d="device": the multi-workgroup CG2D (kernels_cg2d_mwg.hip) with every process
+  launching only the parts of its own tiles; all parts meet on ONE hand-off block (rank 0's,
+  mapped into the others by IPC, system-scope granules).  No host step and no collective
+  inside an iteration; its sums keep the single-launch order, so the solve is the
+  1-process multi-workgroup solve bit for bit, at any process count;
 * cg2d="distributed" is the reference's own distributed CG2D (cg2d.F:100-415):
   each process iterates on its own tiles only (mgcm_cg2d_op), the three global
   sums per iteration are GLOBAL_SUM_TILE_RL -- an all-gather of the per-tile
@@ -111,6 +116,14 @@ def exchange(dist, plan, pack, unpack, make_buf):
     """Point-to-point exchange of halo sources with every neighbouring process.
     pack(peer) -> tensor to send; make_buf(peer) -> receive tensor;
     unpack(peer, tensor).  Grouped isend/irecv (one batch), lower rank posts first."""
+    start_exchange(dist, plan, pack, unpack, make_buf)()
+
+
+def start_exchange(dist, plan, pack, unpack, make_buf):
+    """exchange() split at the reference's PUT/send | recv/GET boundary
+    (pkg/exch2/exch2_rx1_cube.template:118-247): the sends and receives are posted now,
+    and the returned finish() waits for them and unpacks -- work issued in between
+    overlaps the transfer."""
     ops, recvs = [], {}
     for peer in plan.peers():
         if peer in plan.send:
@@ -118,11 +131,14 @@ def exchange(dist, plan, pack, unpack, make_buf):
         if peer in plan.recv:
             recvs[peer] = make_buf(peer)
             ops.append(dist.P2POp(dist.irecv, recvs[peer], peer))
-    if ops:
-        for w in dist.batch_isend_irecv(ops):
+    works = dist.batch_isend_irecv(ops) if ops else []
+
+    def finish():
+        for w in works:
             w.wait()
-    for peer, buf in recvs.items():
-        unpack(peer, buf)
+        for peer, buf in recvs.items():
+            unpack(peer, buf)
+    return finish
 
 
 def tile_sum(partials):
@@ -163,7 +179,7 @@ class ShardedModel:
     configuration; after init(), step()/forward_step() keep the tiles a
     process owns bit-identical to a single-process run."""
 
-    def __init__(self, model, dist, device=None, cg2d="replicated"):
+    def __init__(self, model, dist, device=None, cg2d="replicated", overlap=True, model_stream="shared"):
         import torch
         from ._lib import check, lib
         self.torch, self.dist, self.m = torch, dist, model
@@ -177,48 +193,91 @@ class ShardedModel:
         self.dev = device if device is not None else torch.device("cuda", torch.cuda.current_device())
         h = model.h
         check(self.L.mgcm_set_tile_range(h, self.t0, self.nT), "mgcm_set_tile_range")
+        if model_stream not in ("shared", "own"):
+            raise ValueError("model_stream must be 'shared' or 'own'")
+        self.model_stream = model_stream
         if self.backend == "nccl":
-            # RCCL orders its work after the current stream: run the model and every torch op of
-            # this process on one dedicated stream (the legacy default stream's handle is NULL,
-            # which mgcm_set_stream reads as "the model's own stream")
+            # RCCL orders its work after the current stream: torch runs on one dedicated stream;
+            # the model shares it ("shared", mgcm_set_stream -- the legacy default stream's
+            # handle is NULL, which mgcm_set_stream reads as "the model's own stream") or keeps
+            # its own ("own").  Either way every buffer crosses between the two through
+            # mgcm_stream_handoff (_publish / _consume), so correctness does not rest on the
+            # streams being one.
             self.stream = torch.cuda.Stream(self.dev)
             torch.cuda.set_stream(self.stream)
-            check(self.L.mgcm_set_stream(h, ctypes.c_void_p(self.stream.cuda_stream)), "mgcm_set_stream")
+            if model_stream == "shared":
+                check(self.L.mgcm_set_stream(h, ctypes.c_void_p(self.stream.cuda_stream)), "mgcm_set_stream")
         n2 = g.nx * g.ny
         self.n2 = n2
         uv = g.topo.uv_codes(True) if hasattr(g.topo, "uv_codes") else None
         self.plan = HaloPlan(g.topo.src_of_point(), n2, self.part, self.rank, uv)
         self.stagger = bool(model.params.get("staggerTimeStep", 0))
         self.nf = self.L.mgcm_exchange_nfields(h)
+        # the halo field groups (mgcm_halo_pack_group): 0 all, 1 the tracers, 2 the rest
+        self.nfg = {grp: self.L.mgcm_exchange_nfields_group(h, grp) for grp in (0, 1, 2)}
+        # non-staggered steps: the tracers' exchange travels while DYNAMICS and the solve run
+        self.overlap = bool(overlap) and not self.stagger and self.nfg[1] > 0
         dv = self.dev
         self.idx = {p: torch.as_tensor(v, device=dv) for p, v in
                     list(self.plan.send.items()) + [(("r", q), w) for q, w in self.plan.recv.items()]}
-        self.sbuf = {p: torch.empty(self.nf * g.Nr * v.size, dtype=torch.float64, device=dv)
-                     for p, v in self.plan.send.items()}
-        self.rbuf = {p: torch.empty(self.nf * g.Nr * v.size, dtype=torch.float64, device=dv)
-                     for p, v in self.plan.recv.items()}
+        self.sbuf = {grp: {p: torch.empty(max(1, self.nfg[grp]) * g.Nr * v.size, dtype=torch.float64, device=dv)
+                           for p, v in self.plan.send.items()} for grp in (0, 1, 2)}
+        self.rbuf = {grp: {p: torch.empty(max(1, self.nfg[grp]) * g.Nr * v.size, dtype=torch.float64, device=dv)
+                           for p, v in self.plan.recv.items()} for grp in (0, 1, 2)}
         mt = self.part.maxT
         self.g_in = torch.empty(mt * n2, dtype=torch.float64, device=dv)
         self.g_out = torch.empty(self.world * mt * n2, dtype=torch.float64, device=dv)
-        if cg2d not in ("replicated", "distributed"):
-            raise ValueError("cg2d must be 'replicated' or 'distributed'")
+        if cg2d not in ("replicated", "distributed", "device"):
+            raise ValueError("cg2d must be 'replicated', 'distributed' or 'device'")
         self.cg2d = cg2d
+        if cg2d == "device":
+            self._share_cg2d_handoff()
         if cg2d == "distributed" and model.params.get("useSRCGSolver", 0):
             raise NotImplementedError("useSRCGSolver (CG2D_SR) with the distributed CG2D not implemented")
         if cg2d == "distributed":
             self.cg_part = torch.zeros(2 * g.nTiles, dtype=torch.float64, device=dv)   # part[2*tile + s]
             self.cg_local = torch.zeros((mt, 2), dtype=torch.float64, device=dv)
+            self.cg_iters = []   # iterations of every distributed solve (host record)
+        if cg2d in ("distributed", "device"):
             self.sbuf2 = {p: torch.empty(v.size, dtype=torch.float64, device=dv) for p, v in self.plan.send.items()}
             self.rbuf2 = {p: torch.empty(v.size, dtype=torch.float64, device=dv) for p, v in self.plan.recv.items()}
-            self.cg_iters = []   # iterations of every distributed solve (host record)
+
+    def _share_cg2d_handoff(self):
+        """cg2d="device": the multi-workgroup CG2D's hand-off block of rank 0 (granules,
+        launch epoch, timeout word) mapped into every process by IPC, so that each process
+        launches only its own tiles' parts and all of them meet on one block."""
+        L, h, ck = self.L, self.m.h, self.check
+        if self.m.cg2d_kernel() != "mwg":
+            raise ValueError('cg2d="device" needs the multi-workgroup CG2D (set the parameter cg2dForceMwg=1)')
+        nb = L.mgcm_cg2d_shared_bytes(h)
+        buf = ctypes.create_string_buffer(nb)
+        if self.rank == 0:
+            ck(L.mgcm_cg2d_shared_export(h, buf), "mgcm_cg2d_shared_export")
+        obj = [buf.raw if self.rank == 0 else None]
+        self.dist.broadcast_object_list(obj, src=0)
+        if self.rank != 0:
+            ck(L.mgcm_cg2d_shared_import(h, ctypes.create_string_buffer(obj[0], nb)), "mgcm_cg2d_shared_import")
+        self.dist.barrier()
 
     # ---- transport -------------------------------------------------------------
+    def _cur(self):
+        return ctypes.c_void_p(self.torch.cuda.current_stream(self.dev).cuda_stream)
+
+    def _publish(self):
+        """torch's stream waits for the model's work so far (its outputs become readable)."""
+        self.check(self.L.mgcm_stream_handoff(self.m.h, self._cur(), 0), "mgcm_stream_handoff")
+
+    def _consume(self):
+        """the model's stream waits for torch's work so far (received buffers)."""
+        self.check(self.L.mgcm_stream_handoff(self.m.h, self._cur(), 1), "mgcm_stream_handoff")
+
     def _gather_2d(self, name):
         """all-gather the tile blocks of a 2-D field from their owners."""
         L, h, n2 = self.L, self.m.h, self.n2
         mt = self.part.maxT
         self.check(L.mgcm_tile_copy(h, name.encode(), self.t0, self.nT, ctypes.c_void_p(self.g_in.data_ptr()), 0),
                    "mgcm_tile_copy")
+        self._publish()
         if self.backend == "gloo":
             self.torch.cuda.synchronize(self.dev)
             src = self.g_in.cpu()
@@ -228,6 +287,7 @@ class ShardedModel:
             self.torch.cuda.synchronize(self.dev)
         else:
             self.dist.all_gather_into_tensor(self.g_out, self.g_in)
+        self._consume()
         for r in range(self.world):
             if r == self.rank:
                 continue
@@ -236,31 +296,40 @@ class ShardedModel:
             self.check(L.mgcm_tile_copy(h, name.encode(), s, c, ctypes.c_void_p(buf.data_ptr()), 1),
                        "mgcm_tile_copy")
 
-    def _halo(self):
+    def _halo(self, group=0, start_only=False):
+        """The 3-D halo sources of a field group with every neighbouring process; with
+        start_only the transfer is posted and the finish() that completes it returned."""
         L, h = self.L, self.m.h
 
         def pack(peer):
-            buf = self.sbuf[peer]
-            self.check(L.mgcm_halo_pack(h, ctypes.c_void_p(self.idx[peer].data_ptr()), self.plan.send[peer].size,
-                                        ctypes.c_void_p(buf.data_ptr()), 0), "mgcm_halo_pack")
+            buf = self.sbuf[group][peer]
+            self.check(L.mgcm_halo_pack_group(h, group, ctypes.c_void_p(self.idx[peer].data_ptr()),
+                                              self.plan.send[peer].size, ctypes.c_void_p(buf.data_ptr()), 0),
+                       "mgcm_halo_pack_group")
+            self._publish()
             if self.backend == "gloo":
                 self.torch.cuda.synchronize(self.dev)
                 return buf.cpu()
             return buf
 
         def make_buf(peer):
-            return self.rbuf[peer].cpu() if self.backend == "gloo" else self.rbuf[peer]
+            return self.rbuf[group][peer].cpu() if self.backend == "gloo" else self.rbuf[group][peer]
 
         def unpack(peer, buf):
-            dev = self.rbuf[peer]
+            dev = self.rbuf[group][peer]
             if buf is not dev:
                 dev.copy_(buf)
                 self.torch.cuda.synchronize(self.dev)
-            self.check(L.mgcm_halo_pack(h, ctypes.c_void_p(self.idx[("r", peer)].data_ptr()),
-                                        self.plan.recv[peer].size, ctypes.c_void_p(dev.data_ptr()), 1),
-                       "mgcm_halo_pack")
+            self._consume()
+            self.check(L.mgcm_halo_pack_group(h, group, ctypes.c_void_p(self.idx[("r", peer)].data_ptr()),
+                                              self.plan.recv[peer].size, ctypes.c_void_p(dev.data_ptr()), 1),
+                       "mgcm_halo_pack_group")
 
-        exchange(self.dist, self.plan, pack, unpack, make_buf)
+        fin = start_exchange(self.dist, self.plan, pack, unpack, make_buf)
+        if start_only:
+            return fin
+        fin()
+        return None
 
     def _exch_2d(self, name):
         """EXCH of one 2-D field across processes: the sources of my tiles' halo points
@@ -274,6 +343,7 @@ class ShardedModel:
             buf = self.sbuf2[peer]
             ck(L.mgcm_field_pack(h, nm, ctypes.c_void_p(self.idx[peer].data_ptr()), self.plan.send[peer].size,
                                  ctypes.c_void_p(buf.data_ptr()), 0), "mgcm_field_pack")
+            self._publish()
             if gloo:
                 torch.cuda.synchronize(self.dev)
                 return buf.cpu()
@@ -287,6 +357,7 @@ class ShardedModel:
             if buf is not dev:
                 dev.copy_(buf)
                 torch.cuda.synchronize(self.dev)
+            self._consume()
             ck(L.mgcm_field_pack(h, nm, ctypes.c_void_p(self.idx[("r", peer)].data_ptr()), self.plan.recv[peer].size,
                                  ctypes.c_void_p(dev.data_ptr()), 1), "mgcm_field_pack")
 
@@ -298,6 +369,7 @@ class ShardedModel:
         per-tile partials: the (nTiles, 2) buffer, identical on every process."""
         L, h = self.L, self.m.h
         self.check(L.mgcm_cg2d_op(h, op, float(a0), ctypes.c_void_p(self.cg_part.data_ptr())), "mgcm_cg2d_op(%d)" % op)
+        self._publish()
         if self.backend == "gloo":   # the model runs on its own stream: wait for the partials
             self.torch.cuda.synchronize(self.dev)
         if self.nT:
@@ -350,10 +422,25 @@ class ShardedModel:
     # ---- stepping ----------------------------------------------------------------
     def step(self):
         L, h, ck = self.L, self.m.h, self.check
-        ck(L.mgcm_step_phase(h, 1), "mgcm_step_phase(1)")
+        fin_tracers = None
+        if self.overlap:
+            # DO_OCEANIC_PHYS + THERMODYNAMICS, then the tracers' halo sources leave while
+            # DYNAMICS, the solve and the continuity step compute
+            ck(L.mgcm_step_phase(h, 8), "mgcm_step_phase(8)")
+            fin_tracers = self._halo(1, start_only=True)
+            ck(L.mgcm_step_phase(h, 9), "mgcm_step_phase(9)")
+        else:
+            ck(L.mgcm_step_phase(h, 1), "mgcm_step_phase(1)")
         if self.cg2d == "distributed":
             self._cg2d_distributed()
             self._exch_2d("cg2d_x")      # the halo sources of the new x before etaN everywhere
+            ck(L.mgcm_step_phase(h, 6), "mgcm_step_phase(6)")
+        elif self.cg2d == "device":
+            # the parts' rings reach into the neighbours' tiles: their b and x first
+            self._exch_2d("cg2d_b")
+            self._exch_2d("cg2d_x")
+            ck(L.mgcm_step_phase(h, 10), "mgcm_step_phase(10)")   # this process's parts
+            self._exch_2d("cg2d_x")
             ck(L.mgcm_step_phase(h, 6), "mgcm_step_phase(6)")
         else:
             self._gather_2d("cg2d_b")
@@ -362,7 +449,11 @@ class ShardedModel:
         if self.m.params.get("exactConserv", 0):
             self._gather_2d("cg2d_b")
         ck(L.mgcm_step_phase(h, 3), "mgcm_step_phase(3)")
-        self._halo()
+        if fin_tracers is not None:
+            fin_tracers()
+            self._halo(2)
+        else:
+            self._halo(0)
         if self.stagger:
             # DO_STAGGER_FIELDS_EXCHANGES, then THERMODYNAMICS with the new velocities
             ck(L.mgcm_step_phase(h, 5), "mgcm_step_phase(5)")
@@ -376,9 +467,9 @@ class ShardedModel:
         theta/salt buffers on the host: after two steps the kernels' pointers are back where
         they started.  Runs one warm-up step eagerly first (so the communicators exist before
         capture): the model advances by that step."""
-        if self.backend != "nccl" or self.cg2d != "replicated":
-            raise ValueError("graph capture needs the nccl (RCCL) backend and the replicated CG2D "
-                             "(the distributed solve decides on the host each iteration)")
+        if self.backend != "nccl" or self.cg2d == "distributed":
+            raise ValueError("graph capture needs the nccl (RCCL) backend and a device-decided CG2D "
+                             "(the host-distributed solve decides on the host each iteration)")
         torch, L, h = self.torch, self.L, self.m.h
         s = torch.cuda.Stream(self.dev)
         self.check(L.mgcm_set_stream(h, ctypes.c_void_p(s.cuda_stream)), "mgcm_set_stream")
@@ -394,16 +485,22 @@ class ShardedModel:
         # back onto the model's stream (torch's current one, where the collectives of eager
         # steps and replay() run): begin_steps' memset and eager steps after a capture are
         # then ordered with the replays and the RCCL calls on one stream
-        self.check(L.mgcm_set_stream(h, ctypes.c_void_p(self.stream.cuda_stream)), "mgcm_set_stream")
+        self.check(L.mgcm_set_stream(h, ctypes.c_void_p(self.stream.cuda_stream) if self.model_stream == "shared"
+                                     else None), "mgcm_set_stream")
         self._graph, self._gstream = g, s
 
     def replay(self, npairs=1):
         """Replay the captured pair of steps npairs times (the device's per-step record ring
         restarts at the first replay)."""
         self.check(self.L.mgcm_begin_steps(self.m.h), "mgcm_begin_steps")   # on self.stream
+        if self.model_stream != "shared":
+            self._publish()   # the record reset (model stream) before the replays (torch's)
         with self.torch.cuda.stream(self.stream):
             for _ in range(npairs):
                 self._graph.replay()
+        if self.model_stream != "shared":
+            self._consume()   # the model's later work after the replays
+        self.check(self.L.mgcm_end_steps(self.m.h, 2 * npairs), "mgcm_end_steps")
 
     def forward_step(self, nsteps=1):
         self.check(self.L.mgcm_begin_steps(self.m.h), "mgcm_begin_steps")

@@ -1,9 +1,11 @@
 """Tile-sharded device path (mitgcm_amd/parallel.py + the C-ABI phase API) on a
-real MI355X: 2 to 4 processes share cuda:0 over gloo (host-staged transport;
+real MI355X: 2 to 6 processes share cuda:0 over gloo (host-staged transport;
 RCCL refuses two ranks on one GPU) and step
-  * BASELINE config 4 (baroclinic gyre, 4 lat-lon tiles) for 6 steps, and
+  * BASELINE config 4 (baroclinic gyre, 4 lat-lon tiles) for 6 steps,
   * BASELINE config 3 (global_ocean.cs32x15: 6 cube faces, pkg/exch2 vector maps and
-    corners, r* with UPDATE_CG2D, staggerTimeStep, GM_AdvForm) for 4 steps;
+    corners, r* with UPDATE_CG2D, staggerTimeStep, GM_AdvForm) for 4 steps, and
+  * BASELINE config 5's LLC topology (13 tiles on 5 facets) at n = 30 for 4 steps, with
+    the tracers' halo exchange overlapping DYNAMICS and the solve;
 every process's tiles must be bit-identical to a single-process run (SURVEY.md 8(c)
 parity item 6: same results at any GPU count)."""
 import os
@@ -25,14 +27,20 @@ def _free_port():
     return port
 
 
-def _make(cfg):
+def _make(cfg, force_mwg=False):
     from mitgcm_amd import configs
     if cfg == "gyre":
-        return configs.make_model(configs.baroclinic_gyre, tempAdvScheme=33)
-    return configs.make_model(configs.global_ocean_cs32x15)
+        fn = lambda: configs.baroclinic_gyre(tempAdvScheme=33)
+    elif cfg == "llc30":   # BASELINE config 5's LLC topology at n = 30 (13 tiles, pkg/exch2 facets)
+        fn = lambda: configs.llc_synthetic(n=30, Nr=10)
+    else:
+        fn = configs.global_ocean_cs32x15
+    if force_mwg:   # the multi-workgroup CG2D also where a single-workgroup kernel would be chosen
+        fn = (lambda f: lambda: (lambda r: (r[0], {**r[1], "cg2dForceMwg": 1}) + tuple(r[2:]))(f()))(fn)
+    return configs.make_model(fn)
 
 
-def _worker(rank, world, port, cfg, nsteps, q, cg2d="replicated"):
+def _worker(rank, world, port, cfg, nsteps, q, cg2d="replicated", overlap=True):
     import torch
     import torch.distributed as dist
     from mitgcm_amd.parallel import ShardedModel
@@ -40,19 +48,20 @@ def _worker(rank, world, port, cfg, nsteps, q, cg2d="replicated"):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         torch.cuda.set_device(0)
-        m = _make(cfg)
-        sm = ShardedModel(m, dist, device=torch.device("cuda", 0), cg2d=cg2d)
+        dev_cg = cg2d == "device"
+        m = _make(cfg, dev_cg)
+        sm = ShardedModel(m, dist, device=torch.device("cuda", 0), cg2d=cg2d, overlap=overlap)
         sm.forward_step(nsteps)
         m.sync()
         full = {n: sm.gather_field(n) for n in FIELDS}
         stats = [m.solve_stats(back=b) for b in range(nsteps)]
-        res = {"t0": sm.t0, "nT": sm.nT, "stats": stats}
+        res = {"t0": sm.t0, "nT": sm.nT, "stats": stats, "overlap": sm.overlap}
         if cg2d == "distributed":
             res["iters"] = list(sm.cg_iters)
-            if rank == 0:
-                res["full"] = full
+        if cg2d in ("distributed", "device") and rank == 0:
+            res["full"] = full
         if rank == 0:
-            ref = _make(cfg)
+            ref = _make(cfg, dev_cg)
             ref.forward_step(nsteps)
             ref.sync()
             res["diff"] = {n: float(np.max(np.abs(full[n] - ref.get(n)))) for n in FIELDS}
@@ -69,16 +78,23 @@ def _worker(rank, world, port, cfg, nsteps, q, cg2d="replicated"):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("cfg,world,nsteps,ntiles", [("gyre", 2, 6, 4), ("gyre", 4, 6, 4),
-                                                     ("cs32x15", 2, 4, 6), ("cs32x15", 4, 4, 6),
-                                                     ("cs32x15", 6, 4, 6)])
-def test_sharded_bit_identical(cfg, world, nsteps, ntiles):
+@pytest.mark.parametrize("cfg,world,nsteps,ntiles,overlap", [("gyre", 2, 6, 4, True), ("gyre", 4, 6, 4, True),
+                                                             ("gyre", 2, 6, 4, False),
+                                                             ("cs32x15", 2, 4, 6, True), ("cs32x15", 4, 4, 6, True),
+                                                             ("cs32x15", 6, 4, 6, True),
+                                                             ("llc30", 2, 4, 13, True), ("llc30", 4, 4, 13, True)])
+def test_sharded_bit_identical(cfg, world, nsteps, ntiles, overlap):
+    """llc30: BASELINE config 5's 13-tile LLC topology (5 facets, rotated pkg/exch2 maps) at
+    n = 30.  overlap: the non-staggered configurations exchange the tracers' halo sources
+    while DYNAMICS, the solve and the continuity step run (parallel.ShardedModel.step); the
+    staggered cs32x15 keeps one exchange after the step."""
     import torch.multiprocessing as mp
     from mitgcm_amd.parallel import TilePartition
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, cfg, nsteps, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, cfg, nsteps, q, "replicated", overlap))
+             for r in range(world)]
     for p in procs:
         p.start()
     out = dict(q.get(timeout=300) for _ in procs)
@@ -86,7 +102,9 @@ def test_sharded_bit_identical(cfg, world, nsteps, ntiles):
         p.join(timeout=60)
         assert p.exitcode == 0
     r0 = out[0]
-    print("%s sharded x%d max |diff| vs 1 process:" % (cfg, world), r0["diff"])
+    assert "error" not in r0, r0["error"]
+    assert r0["overlap"] == (overlap and cfg != "cs32x15"), r0["overlap"]
+    print("%s sharded x%d (overlap %s) max |diff| vs 1 process:" % (cfg, world, r0["overlap"]), r0["diff"])
     assert all(r0["equal"].values()), r0["diff"]
     for rank, r in out.items():
         assert r["stats"] == r0["ref_stats"], "rank %d: CG2D records differ" % rank
@@ -137,3 +155,22 @@ def test_distributed_cg2d(cfg, worlds, nsteps):
     for n in FIELDS:
         sc = max(np.abs(base["full"][n]).max(), 1e-300)
         assert base["diff"][n] <= 1e-10 * sc, (n, base["diff"][n], sc)
+
+
+@pytest.mark.parametrize("cfg,worlds,nsteps", [("cs32x15", (1, 2, 3), 3), ("llc30", (1, 2, 4), 3),
+                                               ("gyre", (1, 2, 4), 4)])
+def test_device_cg2d_across_processes(cfg, worlds, nsteps):
+    """cg2d="device": each process launches the multi-workgroup CG2D's parts of its own tiles,
+    all meeting on rank 0's hand-off block mapped by IPC (system-scope granules); nothing on
+    the host inside an iteration.  Bars: at every process count the fields and every solve
+    record are bit-identical to the single-process model running the same multi-workgroup
+    solver (its sums keep the single-launch order)."""
+    for w in worlds:
+        out = _spawn(cfg, w, nsteps, "device")
+        r0 = out[0]
+        its = [s["cg2d_iters"] for s in r0["stats"]]
+        print("%s device CG2D x%d: iterations %s, max |diff| vs 1 process %s" % (cfg, w, its, r0["diff"]))
+        assert all(r0["equal"].values()), (w, r0["diff"])
+        for rank, r in out.items():
+            assert r["stats"] == r0["ref_stats"], (w, rank, r["stats"], r0["ref_stats"])
+        assert all(i > 0 for i in its), its

@@ -2,7 +2,9 @@
 backend (RCCL) at world size 1 -- the only RCCL world a 1-GPU box can host; the multi-GPU
 node runs the same calls with peers.  BASELINE config 4 (baroclinic gyre + DST3-FL, 4 tiles):
   * eager sharded stepping over RCCL (device all-gathers of the CG2D right-hand side and
-    of eta): bit-identical to the single-process model;
+    of eta, the tracers' halo exchange overlapping DYNAMICS): bit-identical to the
+    single-process model, with the model on torch's stream and on its own stream (ordered
+    by mgcm_stream_handoff events only);
   * the distributed CG2D (GLOBAL_SUM_TILE_RL as an RCCL all-gather of per-tile partials):
     iteration counts of the replicated solve, fields within 1e-10;
   * two steps captured into a HIP graph with their RCCL collectives (torch.cuda.graph on
@@ -60,6 +62,14 @@ def _worker(port, q):
         torch.cuda.synchronize()
         res["eager"] = {n: bool(np.array_equal(sm.gather_field(n), want[n])) for n in FIELDS}
         m.close()
+        # the model on its own stream, torch's collectives on another: every buffer crosses
+        # through mgcm_stream_handoff
+        m = _make()
+        sm = ShardedModel(m, dist, model_stream="own")
+        sm.forward_step(4)
+        torch.cuda.synchronize()
+        res["own_stream"] = {n: bool(np.array_equal(sm.gather_field(n), want[n])) for n in FIELDS}
+        m.close()
         # distributed CG2D over RCCL
         m = _make()
         sm = ShardedModel(m, dist, cg2d="distributed")
@@ -99,6 +109,7 @@ def test_rccl_world1_eager_distributed_and_graph():
     assert "error" not in res, res.get("error")
     print("RCCL world 1:", res)
     assert all(res["eager"].values()), res["eager"]
+    assert all(res["own_stream"].values()), res["own_stream"]
     its, ref_its = res["dist_iters"]
     assert its == ref_its, res["dist_iters"]   # per step, most recent first in both lists
     assert max(res["dist_diff"].values()) <= 1e-10, res["dist_diff"]
