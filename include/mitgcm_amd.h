@@ -221,6 +221,11 @@ void mgcm_kernel_timing(mgcm_model *m, int enable);
 /* SIZE.h tile set; nProcs = nPx*nPy and nThreads = nTx*nTy must be 1. */
 void mgcm_amd_setup_(const int *sNx, const int *sNy, const int *OLx, const int *OLy, const int *Nr,
                      const int *nSx, const int *nSy, const int *nProcs, const int *nThreads);
+/* The halo maps of a pkg/exch2 topology, derived by MGCM_AMD_EXCH2_MAPS from the
+ * reference's own EXCH2_3D_RL / EXCH2_UV_CGRID_3D_RL on index arrays (mods/mgcm_amd_exch2.F):
+ * ids = source index per point, u1/v1/u0/v0 = +-(source+1) codes, per-tile face and edges. */
+void mgcm_amd_set_maps_(const double *ids, const double *u1, const double *v1, const double *u0, const double *v0,
+                        const int *tFace, const int *tEdge, const int *nPts);
 /* One PARAMS.h parameter (LOGICAL as 0/1). */
 void mgcm_amd_param_(const char *name, const double *value, size_t len);
 /* Register a COMMON-block array of `count` doubles as device field `name`; kind 1 static

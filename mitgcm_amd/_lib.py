@@ -105,7 +105,8 @@ EXPORTS = ["mgcm_create", "mgcm_destroy", "mgcm_last_error", "mgcm_set_param", "
            "mgcm_update_r_star", "mgcm_calc_r_star", "update_r_star_amd_", "update_cg2d_amd_", "calc_r_star_amd_",
            "mgcm_set_iter", "mgcm_amd_host_sync_", "mgcm_amd_device_sync_", "mgcm_amd_transfer_stats_",
            "mgcm_amd_step_fence_", "mgcm_halo_pack_group", "mgcm_exchange_nfields_group", "mgcm_stream_handoff",
-           "mgcm_end_steps", "mgcm_cg2d_shared_bytes", "mgcm_cg2d_shared_export", "mgcm_cg2d_shared_import"]
+           "mgcm_end_steps", "mgcm_cg2d_shared_bytes", "mgcm_cg2d_shared_export", "mgcm_cg2d_shared_import",
+           "mgcm_amd_set_maps_"]
 
 
 def check(rc, what):

@@ -205,6 +205,24 @@ void mgcm_amd_setup_(const int *sNx, const int *sNy, const int *OLx, const int *
   memcpy(g.dims, d, sizeof d);
 }
 
+/* The halo maps of a pkg/exch2 topology (MGCM_AMD_EXCH2_MAPS, mods/mgcm_amd_exch2.F): the
+ * reference's own EXCH2_3D_RL / EXCH2_UV_CGRID_3D_RL run on index arrays.  ids: per point
+ * the flat index of the point it copies (its own when untouched); u1/v1 (withSigns) and
+ * u0/v0: 0 or +-(source+1) into [u | v]; per tile its face and facet-edge bits. */
+void mgcm_amd_set_maps_(const double *ids, const double *u1, const double *v1, const double *u0, const double *v0,
+                        const int *tFace, const int *tEdge, const int *nPts) {
+  model("MGCM_AMD_SET_MAPS");
+  const long n = *nPts;
+  std::vector<long> src(n), cu1(n), cv1(n), cu0(n), cv0(n);
+  for (long q = 0; q < n; q++) {
+    src[q] = (long)ids[q];
+    cu1[q] = (long)u1[q]; cv1[q] = (long)v1[q]; cu0[q] = (long)u0[q]; cv0[q] = (long)v0[q];
+  }
+  if (mgcm_set_halo_map(g.m, src.data(), n)) die("MGCM_AMD_SET_MAPS");
+  if (mgcm_set_uv_map(g.m, cu1.data(), cv1.data(), cu0.data(), cv0.data(), tFace, tEdge, n)) die("MGCM_AMD_SET_MAPS");
+  g.ready = false;
+}
+
 /* One run-time parameter under its PARAMS.h name (LOGICALs as 0/1, INTEGERs as reals). */
 void mgcm_amd_param_(const char *name, const double *value, size_t len) {
   model("MGCM_AMD_PARAM");

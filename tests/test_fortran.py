@@ -32,12 +32,14 @@ SHADOWS = {"cg2d.F": "cg2d_", "dynamics.F": "dynamics_", "thermodynamics.F": "th
            "do_fields_blocking_exchanges.F": "do_fields_blocking_exchanges_", "exch_xy_rl.F": "exch_xy_rl_",
            "exch_xyz_rl.F": "exch_xyz_rl_", "exch_uv_xy_rl.F": "exch_uv_xy_rl_",
            "exch_uv_xyz_rl.F": "exch_uv_xyz_rl_", "global_sum_tile.F": "global_sum_tile_rl_",
-           "mgcm_amd_mirror.F": "mgcm_amd_mirror_"}
+           "mgcm_amd_mirror.F": "mgcm_amd_mirror_", "mgcm_amd_exch2.F": "mgcm_amd_exch2_maps_"}
+# compiled on the reference's cube-sphere experiment with pkg/exch2 on (its only branch)
+EXCH2_ONLY = {"mgcm_amd_exch2.F": "global_ocean.cs32x15"}
 
 
-def _compile(src, tmp_path, exp):
+def _compile(src, tmp_path, exp, pkgs=("pkg/gmredi", "pkg/cd_code")):
     inc = ["-I" + str(tmp_path)] + ["-I" + os.path.join(REF, p) for p in (
-        "verification/%s/code" % exp, "model/inc", "eesupp/inc", "pkg/gmredi", "pkg/cd_code")]
+        "verification/%s/code" % exp, "model/inc", "eesupp/inc") + tuple(pkgs)]
     pre = subprocess.run(["cpp", "-traditional", "-P", "-DWORDLENGTH=4"] + inc + [src],
                          check=True, capture_output=True, text=True).stdout
     base = os.path.basename(src)[:-2]
@@ -64,8 +66,14 @@ def test_mods_dropins_compile_against_reference_headers(tmp_path):
     assert set(files) == set(SHADOWS), files
     defined_here = set(SHADOWS.values()) | {"mgcm_amd_exch_setup_", "mgcm_amd_rparam_", "mgcm_amd_lparam_",
                                             "mgcm_amd_iparam_"}
+    x2 = tmp_path / "exch2"
+    x2.mkdir()
+    (x2 / "PACKAGES_CONFIG.h").write_text("#define ALLOW_EXCH2\n")
     for f in files:
-        syms = _compile(os.path.join(MODS, f), tmp_path, "global_ocean.90x40x15")
+        if f in EXCH2_ONLY:
+            syms = _compile(os.path.join(MODS, f), x2, EXCH2_ONLY[f], pkgs=("pkg/exch2",))
+        else:
+            syms = _compile(os.path.join(MODS, f), tmp_path, "global_ocean.90x40x15")
         assert re.search(r" T %s$" % SHADOWS[f], syms, re.M), (f, syms)
         calls = set(re.findall(r" U (\w+_amd_\w*)$", syms, re.M))
         assert calls, f
