@@ -308,14 +308,14 @@ def main():
                          device="cuda" if shard and dist.get_backend() == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-    iters = [m.solve_stats(back=b)["cg2d_iters"] for b in range(a.steps)]
+    iters = [int(v) for v in m.solve_history(a.steps)[0]]
     # per-kernel durations: the same K steps again, launched eagerly with HIP events
     # recorded on the model's stream around every kernel (the graph path cannot be
     # bracketed by events); rocprofv3 of this command must agree (profiles/)
     m.kernel_timing(True)
     stepper.forward_step(a.steps)
     sync()
-    iters_t = [m.solve_stats(back=b)["cg2d_iters"] for b in range(a.steps)]
+    iters_t = [int(v) for v in m.solve_history(a.steps)[0]]
     cg_ms, cg_n = m.kernel_ms("cg2d")
     kern = {k: m.kernel_ms(k) for k in ("oceanic_phys", "temp_step", "phi_hyd", "mom_step", "sfp_rhs", "cg2d", "exchange",
                                          "eta_update", "correction", "continuity", "r_star")}

@@ -202,6 +202,9 @@ int mgcm_cg2d_sum_plan(mgcm_model *m, int *plan, long capacity, int *NT, int *PP
  * mgcm_forward_step call. */
 int mgcm_solve_stats(mgcm_model *m, int back, double *firstResidual, double *lastResidual,
                      int *numIters, double *rhsMax);
+/* The same records for the last n steps of the last batch in one device-to-host copy,
+ * oldest first (any output pointer may be NULL). */
+int mgcm_solve_history(mgcm_model *m, int n, int *numIters, double *firstResidual, double *lastResidual);
 
 /* MONITOR's dynstat block (pkg/monitor/monitor.F:103-129 -> MON_CALC_STATS_RL,
  * mon_calc_stats_rl.F / mon_stats_rl.F:104-107) computed on the device, no field download:

@@ -216,6 +216,16 @@ inline unsigned mg_col_blocks(int ni, int nj, int nT, int Nr) {
   const int t = d.t0 + (int)(valid ? col_ / npl_ : 0);                                 \
   const int i = (i0) + (int)((valid ? col_ % npl_ : 0) % (ni));                        \
   const int j = (j0) + (int)((valid ? col_ % npl_ : 0) / (ni));
+// MG_COLF with an explicit logical block id (kernels that split their grid between bodies)
+#define MG_COLF_LB(i0, ni, j0, nj, NCv, LB)                                            \
+  const int NC_ = (NCv), KW_ = 256 / NC_;                                              \
+  const int cc = (int)threadIdx.x % NC_, kk = (int)threadIdx.x / NC_;                  \
+  const long col_ = (long)(LB) * NC_ + cc;                                             \
+  const long npl_ = (long)(ni) * (nj);                                                 \
+  const bool valid = col_ < npl_ * d.nT;                                               \
+  const int t = d.t0 + (int)(valid ? col_ / npl_ : 0);                                 \
+  const int i = (i0) + (int)((valid ? col_ % npl_ : 0) % (ni));                        \
+  const int j = (j0) + (int)((valid ? col_ % npl_ : 0) / (ni));
 // (the bodies keep global stores out of these loops, so that nothing orders a level's
 // loads behind the previous level's stores)
 #define MG_COLF_K(kvar) for (int kvar = kk + 1; kvar <= d.Nr; kvar += KW_)
@@ -237,8 +247,47 @@ inline size_t mg_colf_lds(int Nr, int nc, int nArr) { return (size_t)nArr * Nr *
     (void)set_;                                                                                         \
   } while (0)
 inline unsigned mg_colf_blocks(long ncols, int nc) { return (unsigned)((ncols + nc - 1) / nc); }
+// Launch fusions of FORWARD_STEP, each switchable for A/B runs: MGCM_STEP_FUSE = bit mask of
+// the enabled ones (default all): MG_FUSE_SFP CALC_DIV_GHAT in the r* column pass,
+// MG_FUSE_ETA EXCH(cg2d_x) + etaN in the single-workgroup CG2D, MG_FUSE_PHI CALC_PHI_HYD +
+// del2uv in one grid, MG_FUSE_END CALC_R_STAR + the blocking exchanges in one grid.
+enum { MG_FUSE_SFP = 1, MG_FUSE_ETA = 2, MG_FUSE_PHI = 4, MG_FUSE_END = 8 };
+inline bool mg_fuse_on(int bit) {
+  static const int mask = getenv("MGCM_STEP_FUSE") ? atoi(getenv("MGCM_STEP_FUSE")) : MG_FUSE_SFP | MG_FUSE_PHI | MG_FUSE_END;
+  return (mask & bit) != 0;
+}
+// Horizontal launch fusion of two independent latency-bound kernels into one grid: on the
+// small configurations only (up to 2^21 grid points), where each launch is a few us of latency
+inline bool mg_hfuse(int bit, long nx, long ny, long nT, long Nr) {
+  return mg_fuse_on(bit) && nx * ny * nT * Nr <= (1L << 21);
+}
 inline unsigned mg_plane_blocks(int ni, int nj, int nz) {
   return (unsigned)(((ni) * (nj) + MG_PLANE_THREADS - 1) / MG_PLANE_THREADS * (nz));
+}
+
+// The serial end of SOLVE_FOR_PRESSURE's right-hand side for one column (k_sfp_rhs and the
+// fused r* pass k_update_r_star_cg2d_a<SFP>): etaNm1 (CD scheme), cg2d_x = Bo_surf*etaN and
+// cg2d_b = CALC_DIV_GHAT's k = Nr..1 sum of the staged flux terms + the free-surface term.
+__device__ __forceinline__ void sfp_rhs_column(const Dims &d, const Params &p, const Fields &f, long q, bool inner,
+                                               const double *sE, const double *sW, const double *sN, const double *sS,
+                                               int NC_, int cc) {
+  if (p.useCDscheme) f.etaNm1[q] = f.etaN[q];
+  f.cg2d_x[q] = f.Bo_surf[q] * f.etaN[q];
+  double b = 0.0;
+  if (inner) {
+    if (p.useRealFreshWaterFlux) {
+      const double tmpFac = p.freeSurfFac * (1.0 / p.rhoConst) * p.implicDiv2DFlow;
+      b = tmpFac * f.rA[q] * f.EmPmR[q] / p.deltaTMom * f.maskInC[q];
+    }
+    for (int k2 = d.Nr; k2 >= 1; k2--) {
+      const int s2 = (k2 - 1) * NC_ + cc;
+      b = b + sE[s2] - sW[s2];
+      b = b + sN[s2] - sS[s2];
+    }
+    // solve_for_pressure.F:214-236 (linear free surface): etaH with exactConserv, else etaN
+    b = b - p.freeSurfFac * f.rA[q] / p.deltaTMom / p.deltaTFreeSurf * (p.exactConserv ? f.etaH[q] : f.etaN[q]);
+  }
+  f.cg2d_b[q] = b;
 }
 
 // One tracer of TEMP_INTEGRATE / SALT_INTEGRATE (temp_integrate.F, salt_integrate.F).
@@ -259,6 +308,21 @@ struct XFields {
   int nz[MG_XMAX];
   int n;
 };
+
+// DO_FIELDS_BLOCKING_EXCHANGES' copies for one (halo block hb, level k, field fi) of
+// k_exchange_multi's grid; the block (0,0,0) also advances the step counters (the last
+// kernel of a step: nothing later in the step reads them).
+__device__ __forceinline__ void exchange_multi_body(const Dims &d, const XFields &x, const long *__restrict__ map,
+                                                    int nHalo, int *ctr, int hb, int k, int fi) {
+  const int h = hb * (int)blockDim.x + (int)threadIdx.x;
+  if (ctr && h == 0 && k == 0 && fi == 0) { ctr[0] += 1; ctr[1] += 1; }
+  if (h >= nHalo || fi >= x.n || k >= x.nz[fi]) return;
+  const long dst = map[2 * h], src = map[2 * h + 1];
+  const long dt = dst / d.n2, dl = dst % d.n2, st = src / d.n2, sl = src % d.n2;
+  const long lvl = (long)d.n2 * x.nz[fi];
+  double *a = x.p[fi];
+  a[dt * lvl + (long)k * d.n2 + dl] = a[st * lvl + (long)k * d.n2 + sl];
+}
 
 // Multi-workgroup CG2D (kernels_cg2d_mwg.hip): tables of every part (a row strip of a tile,
 // one workgroup), built by build_mwg (model.hip); slot s = p*NT + tid.

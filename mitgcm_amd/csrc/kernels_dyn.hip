@@ -41,8 +41,8 @@ __device__ __forceinline__ double h0facz(const Dims &d, const Params &p, const F
 // cosFac = 1, no OBCS) for one (i,j,k) of 2-OL..sN+OL-1 (0 elsewhere, as the zeroed v4F):
 // the Laplacians of u and v the biharmonic viscous fluxes difference, with the no-slip
 // side-wall term from the rest-state h0Fac (NONLIN_FRSURF).
-__global__ void __launch_bounds__(256) k_del2uv(Dims d, Params p, Fields f) {
-  MG_PLANE(1 - d.OLx, d.nx, 1 - d.OLy, d.ny, z)
+__device__ __forceinline__ void del2uv_body(const Dims &d, const Params &p, const Fields &f, int lb) {
+  MG_PLANE_LB(1 - d.OLx, d.nx, 1 - d.OLy, d.ny, z, lb)
   const int t = d.t0 + z / d.Nr, k = z % d.Nr + 1;
   const long q3 = MG_I3(d, i, j, k, t);
   if (i < 2 - d.OLx || i > d.sNx + d.OLx - 1 || j < 2 - d.OLy || j > d.sNy + d.OLy - 1) {
@@ -92,6 +92,7 @@ __global__ void __launch_bounds__(256) k_del2uv(Dims d, Params p, Fields f) {
 #undef G2
 #undef G3
 }
+__global__ void __launch_bounds__(256) k_del2uv(Dims d, Params p, Fields f) { del2uv_body(d, p, f, mg_xcd_block()); }
 
 // CALC_PHI_HYD (calc_phi_hyd.F:175-327, OCEANIC, integr_GeoPot = 2, uniformFreeSurfLev,
 // gravFac = 1) per column, as the other column kernels (MG_COLF): alphaRho = rhoInSitu
@@ -104,9 +105,9 @@ __global__ void __launch_bounds__(256) k_del2uv(Dims d, Params p, Fields f) {
 // their value at every level for k_mom_step.  Columns cover -1..sNx+1 x -1..sNy+1 (the
 // dynamics range 0..sNx+1 plus the west/south neighbours dWtransC is needed at); phi and
 // totPhiHyd are stored on 0..sNx+1 only.
-__global__ void __launch_bounds__(256) k_phi_hyd(Dims d, Params p, Fields f, int nc) {
+__device__ __forceinline__ void phi_hyd_body(const Dims &d, const Params &p, const Fields &f, int nc, int lb) {
   extern __shared__ __attribute__((aligned(16))) double lds[];
-  MG_COLF(-1, d.sNx + 3, -1, d.sNy + 3, nc)
+  MG_COLF_LB(-1, d.sNx + 3, -1, d.sNy + 3, nc, lb)
   const int Nr = d.Nr, NS = Nr * NC_;
   double *sM = lds, *sP = lds + NS, *sPh = lds + 2 * NS, *sC = lds + 3 * NS, *sU = lds + 4 * NS, *sV = lds + 5 * NS;
   const bool qh = p.quasiHydrostatic && (p.select3dCoriScheme >= 1 || p.useNHMTerms);
@@ -193,6 +194,17 @@ __global__ void __launch_bounds__(256) k_phi_hyd(Dims d, Params p, Fields f, int
       }
     }
   }
+}
+__global__ void __launch_bounds__(256) k_phi_hyd(Dims d, Params p, Fields f, int nc) {
+  phi_hyd_body(d, p, f, nc, mg_xcd_block());
+}
+// CALC_PHI_HYD and MOM_U_DEL2U / MOM_V_DEL2V in one grid (independent: each reads only the
+// state DYNAMICS starts from): the first nbPhi logical blocks are k_phi_hyd's, the rest
+// k_del2uv's; each body's barriers are block-uniform
+__global__ void __launch_bounds__(256) k_phi_del2(Dims d, Params p, Fields f, int nc, int nbPhi) {
+  const int lb = mg_xcd_block();
+  if (lb < nbPhi) phi_hyd_body(d, p, f, nc, lb);
+  else del2uv_body(d, p, f, lb - nbPhi);
 }
 
 
@@ -1680,9 +1692,19 @@ __global__ void __launch_bounds__(256) k_mom_impl(Dims d, Params p, Fields f, in
   if (valid) MG_COLF_K(k) g[MG_I3(d, i, j, k, t)] = sSub[(k - 1) * NC_ + cc];
 }
 
+static bool del2_needed(const Params &p) { return p.momViscosity && (p.viscA4D != 0.0 || p.viscA4Z != 0.0); }
+// k_del2uv rides in CALC_PHI_HYD's launch (k_phi_del2) on the small grids
+static bool phi_del2_fused(const Dims &d, const Params &p) { return del2_needed(p) && mg_hfuse(MG_FUSE_PHI, d.nx, d.ny, d.nT, d.Nr); }
+
 hipError_t launch_phi_hyd(const Dims &d, const Params &p, const Fields &f, hipStream_t s) {
   const long ncol = (long)(d.sNx + 3) * (d.sNy + 3) * d.nT;
   const int nc = mg_colf_nc(ncol, d.Nr, 6);
+  if (phi_del2_fused(d, p)) {
+    MG_ALLOW_LDS(k_phi_del2);
+    const unsigned nbPhi = mg_colf_blocks(ncol, nc), nbDel = mg_plane_blocks(d.nx, d.ny, d.nT * d.Nr);
+    hipLaunchKernelGGL(k_phi_del2, dim3(nbPhi + nbDel), dim3(256), mg_colf_lds(d.Nr, nc, 6), s, d, p, f, nc, (int)nbPhi);
+    return hipGetLastError();
+  }
   MG_ALLOW_LDS(k_phi_hyd);
   hipLaunchKernelGGL(k_phi_hyd, dim3(mg_colf_blocks(ncol, nc)), dim3(256), mg_colf_lds(d.Nr, nc, 6), s, d, p, f, nc);
   return hipGetLastError();
@@ -1691,7 +1713,7 @@ hipError_t launch_phi_hyd(const Dims &d, const Params &p, const Fields &f, hipSt
 // DYNAMICS after CALC_PHI_HYD (launch_phi_hyd): momentum tendencies, TIMESTEP, AB2, CD scheme,
 // implicit vertical viscosity
 hipError_t launch_mom_step(const Dims &d, const Params &p, const Fields &f, const int *iterPtr, hipStream_t s) {
-  if (p.momViscosity && (p.viscA4D != 0.0 || p.viscA4Z != 0.0))
+  if (del2_needed(p) && !phi_del2_fused(d, p))
     hipLaunchKernelGGL(k_del2uv, dim3(mg_plane_blocks(d.nx, d.ny, d.nT * d.Nr)), dim3(MG_PLANE_THREADS), 0, s, d, p, f);
   // MOM_VECINV or MOM_FLUXFORM: separate instantiations (no register-pressure coupling)
   static const bool viPoint = getenv("MGCM_VI_POINT") != nullptr;   // the per-point form, for comparison

@@ -35,8 +35,9 @@ __device__ __forceinline__ double eta_exch(const Dims &d, const Fields &f, const
 // cross-thread location both read and written is etaN at points neither interior nor
 // mapped, which is rewritten with the value it holds.
 template <bool FUSE>
-__global__ void __launch_bounds__(256) k_calc_r_star(Dims d, Params p, Fields f, const long *__restrict__ srcOf) {
-  const long q = (long)blockIdx.x * blockDim.x + threadIdx.x;
+__device__ __forceinline__ void calc_r_star_body(const Dims &d, const Params &p, const Fields &f,
+                                                 const long *__restrict__ srcOf, int lb) {
+  const long q = (long)lb * blockDim.x + threadIdx.x;
   if (q >= d.n2 * d.nTiles) return;
   const int t = (int)(q / d.n2);
   if (t < d.t0 || t >= d.t0 + d.nT) return;
@@ -86,6 +87,23 @@ __global__ void __launch_bounds__(256) k_calc_r_star(Dims d, Params p, Fields f,
   f.rStarExpW[q] = fw / ow;
   f.rStarExpS[q] = fs / os;
 }
+template <bool FUSE>
+__global__ void __launch_bounds__(256) k_calc_r_star(Dims d, Params p, Fields f, const long *__restrict__ srcOf) {
+  calc_r_star_body<FUSE>(d, p, f, srcOf, (int)blockIdx.x);
+}
+// The end of FORWARD_STEP in one grid: CALC_R_STAR (with EXCH(eta) + UPDATE_ETAH, FUSE) on
+// the first nbR blocks and DO_FIELDS_BLOCKING_EXCHANGES (k_exchange_multi's nbX x nz x nF
+// grid, flattened) on the rest -- independent: CALC_R_STAR reads eta and writes the 2-D r*
+// factors, the exchanges copy the 3-D state's halos.
+template <bool FUSE>
+__global__ void __launch_bounds__(256) k_rstar_exch(Dims d, Params p, Fields f, const long *__restrict__ srcOf, int nbR,
+                                                    XFields x, const long *__restrict__ map, int nHalo, int *ctr, int nbX,
+                                                    int nzMax) {
+  const int b = (int)blockIdx.x;
+  if (b < nbR) { calc_r_star_body<FUSE>(d, p, f, srcOf, b); return; }
+  const int r = b - nbR;
+  exchange_multi_body(d, x, map, nHalo, ctr, r % nbX, (r / nbX) % nzMax, r / (nbX * nzMax));
+}
 
 // UPDATE_R_STAR(.TRUE.) (update_r_star.F:60-92) and UPDATE_CG2D part 1
 // (update_cg2d.F:82-143) in one pass over the columns of every 2-D point (column frame,
@@ -94,15 +112,24 @@ __global__ void __launch_bounds__(256) k_calc_r_star(Dims d, Params p, Fields f,
 // and stages the operator terms faceArea*recip_dx/yC of its levels in LDS; thread (c, 0)
 // then sums aW2d, aS2d in k order on 1..sNx+1 x 1..sNy+1 and scales them by
 // cg2dNorm*implicSurfPress*implicDiv2DFlow (0 elsewhere).
+// SFP: SOLVE_FOR_PRESSURE's right-hand side (k_sfp_rhs, kernels_solve.hip) in the same
+// column pass (FORWARD_STEP: UPDATE_R_STAR + UPDATE_CG2D, then CALC_DIV_GHAT): the flux terms
+// read hFacW(i+1) / hFacS(j+1) of the neighbouring columns, which this pass is rewriting, so
+// they are formed from h0Fac*rStarFac there (the expression that column stores: same bits).
+template <bool SFP>
 __global__ void __launch_bounds__(256) k_update_r_star_cg2d_a(Dims d, Params p, Fields f, int nc) {
   extern __shared__ __attribute__((aligned(16))) double lds[];
   MG_COLF(1 - d.OLx, d.nx, 1 - d.OLy, d.ny, nc)
   const int NS = d.Nr * NC_;
   double *sW = lds, *sS = lds + NS;
+  double *fE = lds + 2 * NS, *fW = lds + 3 * NS, *fN = lds + 4 * NS, *fS = lds + 5 * NS;   // SFP only
   const long q = MG_I2(d, i, j, t);
   const bool op = p.nonlinFreeSurf > 2 && i >= 1 && i <= d.sNx + 1 && j >= 1 && j <= d.sNy + 1;
+  const bool inner = i >= 1 && i <= d.sNx && j >= 1 && j <= d.sNy;
   if (valid) {
     const double fc = f.rStarFacC[q], fw = f.rStarFacW[q], fs = f.rStarFacS[q];
+    double fwE = 0.0, fsN = 0.0;
+    if (SFP && inner) { fwE = f.rStarFacW[MG_I2(d, i + 1, j, t)]; fsN = f.rStarFacS[MG_I2(d, i, j + 1, t)]; }
     MG_COLF_K(k) {
       const long q3 = MG_I3(d, i, j, k, t);
       const double hC = f.h0FacC[q3] * fc, hW = f.h0FacW[q3] * fw, hS = f.h0FacS[q3] * fs;
@@ -112,29 +139,46 @@ __global__ void __launch_bounds__(256) k_update_r_star_cg2d_a(Dims d, Params p, 
       if (f.maskC[q3] != 0.0) f.recip_hFacC[q3] = 1.0 / hC;
       if (f.maskW[q3] != 0.0) f.recip_hFacW[q3] = 1.0 / hW;
       if (f.maskS[q3] != 0.0) f.recip_hFacS[q3] = 1.0 / hS;
+      const int me = (k - 1) * NC_ + cc;
       if (op) {
-        const int me = (k - 1) * NC_ + cc;
         double faceArea = f.dyG[q] * f.drF[k - 1] * hW;
         sW[me] = faceArea * f.recip_dxC[q];
         faceArea = f.dxG[q] * f.drF[k - 1] * hS;
         sS[me] = faceArea * f.recip_dyC[q];
       }
+      if (SFP) {
+        if (p.useCDscheme) {
+          f.uNM1[q3] = f.uVel[q3];
+          f.vNM1[q3] = f.vVel[q3];
+        }
+        if (inner) {   // k_sfp_rhs's CALC_DIV_GHAT flux terms of level k
+          const double drF = f.drF[k - 1];
+          const long qE = MG_I3(d, i + 1, j, k, t), qN = MG_I3(d, i, j + 1, k, t);
+          fE[me] = f.dyG[MG_I2(d, i + 1, j, t)] * drF * (f.h0FacW[qE] * fwE) * f.gU[qE] / p.deltaTMom;
+          fW[me] = f.dyG[q] * drF * hW * f.gU[q3] / p.deltaTMom;
+          fN[me] = f.dxG[MG_I2(d, i, j + 1, t)] * drF * (f.h0FacS[qN] * fsN) * f.gV[qN] / p.deltaTMom;
+          fS[me] = f.dxG[q] * drF * hS * f.gV[q3] / p.deltaTMom;
+        }
+      }
     }
   }
   __syncthreads();
-  if (!valid || kk != 0 || p.nonlinFreeSurf <= 2) return;
-  double aW = 0.0, aS = 0.0;
-  if (op) {
-    for (int k = 1; k <= d.Nr; k++) {
-      const int me = (k - 1) * NC_ + cc;
-      aW = aW + sW[me];
-      aS = aS + sS[me];
+  if (!valid || kk != 0) return;
+  if (p.nonlinFreeSurf > 2) {
+    double aW = 0.0, aS = 0.0;
+    if (op) {
+      for (int k = 1; k <= d.Nr; k++) {
+        const int me = (k - 1) * NC_ + cc;
+        aW = aW + sW[me];
+        aS = aS + sS[me];
+      }
+      aW = aW * p.cg2dNorm * p.implicSurfPress * p.implicDiv2DFlow;
+      aS = aS * p.cg2dNorm * p.implicSurfPress * p.implicDiv2DFlow;
     }
-    aW = aW * p.cg2dNorm * p.implicSurfPress * p.implicDiv2DFlow;
-    aS = aS * p.cg2dNorm * p.implicSurfPress * p.implicDiv2DFlow;
+    f.aW2d[q] = aW;
+    f.aS2d[q] = aS;
   }
-  f.aW2d[q] = aW;
-  f.aS2d[q] = aS;
+  if (SFP) sfp_rhs_column(d, p, f, q, inner, fE, fW, fN, fS, NC_, cc);
 }
 
 // UPDATE_CG2D part 2 (update_cg2d.F:144-199): aC2d on the interior, EXCH_XY_RS(aC2d)
@@ -179,14 +223,30 @@ hipError_t launch_calc_r_star(const Dims &d, const Params &p, const Fields &f, c
   return hipGetLastError();
 }
 
-hipError_t launch_update_r_star_cg2d(const Dims &d, const Params &p, const Fields &f, const long *srcOf, hipStream_t s) {
+hipError_t launch_rstar_exch(const Dims &d, const Params &p, const Fields &f, const long *srcOf, bool fuseEtaH,
+                             const XFields &x, const long *map, int nHalo, int *ctr, hipStream_t s) {
+  const long n = d.n2 * d.nTiles;
+  const int nbR = (int)((n + 255) / 256);
+  int nzMax = 1;
+  for (int q = 0; q < x.n; q++) nzMax = x.nz[q] > nzMax ? x.nz[q] : nzMax;
+  const int nbX = ((nHalo > 0 ? nHalo : 1) + 255) / 256;
+  const unsigned nb = (unsigned)(nbR + nbX * nzMax * (x.n > 0 ? x.n : 1));
+  hipLaunchKernelGGL(fuseEtaH ? k_rstar_exch<true> : k_rstar_exch<false>, dim3(nb), dim3(256), 0, s, d, p, f, srcOf, nbR, x,
+                     map, nHalo, ctr, nbX, nzMax);
+  return hipGetLastError();
+}
+
+hipError_t launch_update_r_star_cg2d(const Dims &d, const Params &p, const Fields &f, const long *srcOf, hipStream_t s,
+                                     bool sfp) {
   const long n = d.n2 * d.nTiles;
   const unsigned nb = (unsigned)((n + 255) / 256);
   const long ncol = (long)d.nx * d.ny * d.nT;
-  const int nc = mg_colf_nc(ncol, d.Nr, 2);
-  MG_ALLOW_LDS(k_update_r_star_cg2d_a);
-  hipLaunchKernelGGL(k_update_r_star_cg2d_a, dim3(mg_colf_blocks(ncol, nc)), dim3(256), mg_colf_lds(d.Nr, nc, 2), s, d, p,
-                     f, nc);
+  const int nArr = sfp ? 6 : 2;
+  const int nc = mg_colf_nc(ncol, d.Nr, nArr);
+  MG_ALLOW_LDS(k_update_r_star_cg2d_a<false>);
+  MG_ALLOW_LDS(k_update_r_star_cg2d_a<true>);
+  hipLaunchKernelGGL(sfp ? k_update_r_star_cg2d_a<true> : k_update_r_star_cg2d_a<false>, dim3(mg_colf_blocks(ncol, nc)),
+                     dim3(256), mg_colf_lds(d.Nr, nc, nArr), s, d, p, f, nc);
   if (p.nonlinFreeSurf > 2) hipLaunchKernelGGL(k_update_cg2d_p, dim3(nb), dim3(256), 0, s, d, p, f, srcOf);
   return hipGetLastError();
 }

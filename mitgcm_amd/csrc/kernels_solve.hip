@@ -160,23 +160,7 @@ __global__ void __launch_bounds__(256) k_sfp_rhs(Dims d, Params p, Fields f, int
   }
   __syncthreads();
   if (!valid || kk != 0) return;
-  if (p.useCDscheme) f.etaNm1[q] = f.etaN[q];
-  f.cg2d_x[q] = f.Bo_surf[q] * f.etaN[q];
-  double b = 0.0;
-  if (inner) {
-    if (p.useRealFreshWaterFlux) {
-      const double tmpFac = p.freeSurfFac * (1.0 / p.rhoConst) * p.implicDiv2DFlow;
-      b = tmpFac * f.rA[q] * f.EmPmR[q] / p.deltaTMom * f.maskInC[q];
-    }
-    for (int k2 = d.Nr; k2 >= 1; k2--) {
-      const int s2 = (k2 - 1) * NC_ + cc;
-      b = b + sE[s2] - sW[s2];
-      b = b + sN[s2] - sS[s2];
-    }
-    // solve_for_pressure.F:214-236 (linear free surface): etaH with exactConserv, else etaN
-    b = b - p.freeSurfFac * f.rA[q] / p.deltaTMom / p.deltaTFreeSurf * (p.exactConserv ? f.etaH[q] : f.etaN[q]);
-  }
-  f.cg2d_b[q] = b;
+  sfp_rhs_column(d, p, f, q, inner, sE, sW, sN, sS, NC_, cc);
 }
 
 // Whole-solve CG2D in one workgroup.  PPT = interior points per thread.
@@ -765,7 +749,8 @@ __device__ __forceinline__ double block_max_nw(double v, double *red, int slot) 
 template <int BX, int BY, int NT, bool MINRES, bool FMA, bool RC = false, bool SR = false>
 __global__ void __launch_bounds__(NT) k_cg2d_bxy(Dims d, Params p, Fields f, const unsigned *__restrict__ nbx,
                                                  const int *__restrict__ blkx, int nBlk, int maxIters, int nIterMinIn,
-                                                 SolveRecord *rec, int *stepCounter) {
+                                                 SolveRecord *rec, int *stepCounter, const int *__restrict__ slot2,
+                                                 const long *__restrict__ srcOf) {
   constexpr int NPT = BX * BY, NP = NPT * NT, NB = 2 * (BX + BY), NW = NT / 64;
   extern __shared__ __attribute__((aligned(16))) double lds[];
   double *r_l = lds;               // NP + 1 (last = ZERO slot)
@@ -1165,7 +1150,34 @@ __global__ void __launch_bounds__(NT) k_cg2d_bxy(Dims d, Params p, Fields f, con
 #pragma unroll
       for (int a = 0; a < BX; a++) x[b][a] = xmin[b][a];
   }
-  if (act) {
+  if (slot2) {
+    // SOLVE_FOR_PRESSURE's EXCH_XY_RL(cg2d_x) + etaN = recip_Bo*cg2d_x (k_exch_eta) as the
+    // epilogue: the solution through LDS (r_l, every reader of it is past the last barrier of
+    // the loop once this one is passed), then every 2-D point takes its own value or its
+    // interior source's and is stored with its etaN
+    __syncthreads();
+#pragma unroll
+    for (int b = 0; b < BY; b++)
+#pragma unroll
+      for (int a = 0; a < BX; a++) {
+        double xv = x[b][a];
+        if (p.cg2dNormaliseRHS) xv = xv / rhsNorm;
+        if (act) r_l[cs[b][a]] = xv;
+      }
+    __syncthreads();
+    const long n2 = d.n2 * d.nTiles;
+    for (long q = tid; q < n2; q += NT) {
+      const int sl = slot2[q];
+      double xq;
+      if (sl >= 0) xq = r_l[sl];
+      else {   // neither in a block nor mapped onto one: as k_exch_eta, from global memory
+        const long sq = srcOf[q];
+        xq = f.cg2d_x[sq >= 0 ? sq : q];
+      }
+      f.cg2d_x[q] = xq;
+      f.etaN[q] = f.recip_Bo[q] * xq;
+    }
+  } else if (act) {
 #pragma unroll
     for (int b = 0; b < BY; b++)
 #pragma unroll
@@ -1222,19 +1234,10 @@ __global__ void __launch_bounds__(256) k_correction(Dims d, Params p, Fields f) 
 }
 
 // DO_FIELDS_BLOCKING_EXCHANGES in one launch: up to MG_XMAX fields of nz[f] levels
-// through the halo map; the block (0,0,0) also advances the step counters (the
-// last kernel of a step: nothing later in the step reads them).
+// through the halo map (exchange_multi_body, common.h).
 __global__ void __launch_bounds__(256) k_exchange_multi(Dims d, XFields x, const long *__restrict__ map, int nHalo,
                                                         int *ctr) {
-  const int h = (int)(blockIdx.x * blockDim.x + threadIdx.x);
-  const int k = (int)blockIdx.y, fi = (int)blockIdx.z;
-  if (ctr && h == 0 && k == 0 && fi == 0) { ctr[0] += 1; ctr[1] += 1; }
-  if (h >= nHalo || fi >= x.n || k >= x.nz[fi]) return;
-  const long dst = map[2 * h], src = map[2 * h + 1];
-  const long dt = dst / d.n2, dl = dst % d.n2, st = src / d.n2, sl = src % d.n2;
-  const long lvl = (long)d.n2 * x.nz[fi];
-  double *a = x.p[fi];
-  a[dt * lvl + (long)k * d.n2 + dl] = a[st * lvl + (long)k * d.n2 + sl];
+  exchange_multi_body(d, x, map, nHalo, ctr, (int)blockIdx.x, (int)blockIdx.y, (int)blockIdx.z);
 }
 
 // EXCH2 C-grid vector exchange (EXCH2_UV_3D_RX, pkg/exch2/exch2_uv_3d_rx.template) as one
@@ -1571,7 +1574,8 @@ int cg2d_bxy_geometry(int v, int *bx, int *by, int *nt) {
 }
 template <int BX, int BY, int NT>
 static hipError_t launch_bxy_t(const Dims &d, const Params &p, const Fields &f, const unsigned *nbx, const int *blkx,
-                               int nBlk, int maxIters, int nIterMin, SolveRecord *rec, int *stepCounter, hipStream_t s) {
+                               int nBlk, int maxIters, int nIterMin, SolveRecord *rec, int *stepCounter, const int *slot2,
+                               const long *srcOf, hipStream_t s) {
   if (nBlk > NT) return hipErrorInvalidValue;
   // the recompute form (RC) only with MGCM_CG2D_RC=1: on config 2 it is bit-identical but
   // 2.54 us/iteration against 1.82 (256 VGPRs + 29 spilled, twice the neighbour LDS reads):
@@ -1593,13 +1597,16 @@ static hipError_t launch_bxy_t(const Dims &d, const Params &p, const Fields &f, 
     if (e != hipSuccess) return e;
     attrSet[ai] = true;
   }
-  hipLaunchKernelGGL(kern, dim3(1), dim3(NT), lds, s, d, p, f, nbx, blkx, nBlk, maxIters, nIterMin, rec, stepCounter);
+  hipLaunchKernelGGL(kern, dim3(1), dim3(NT), lds, s, d, p, f, nbx, blkx, nBlk, maxIters, nIterMin, rec, stepCounter, slot2,
+                     srcOf);
   return hipGetLastError();
 }
+// slot2 (or nullptr): the 2-D point -> LDS slot map of the fused EXCH(cg2d_x) + etaN epilogue
 hipError_t launch_cg2d_bxy(int v, const Dims &d, const Params &p, const Fields &f, const unsigned *nbx, const int *blkx,
-                           int nBlk, int maxIters, int nIterMin, SolveRecord *rec, int *stepCounter, hipStream_t s) {
+                           int nBlk, int maxIters, int nIterMin, SolveRecord *rec, int *stepCounter, const int *slot2,
+                           const long *srcOf, hipStream_t s) {
 #define CGX_CASE(V, BX, BY, NT) \
-  case V: return launch_bxy_t<BX, BY, NT>(d, p, f, nbx, blkx, nBlk, maxIters, nIterMin, rec, stepCounter, s);
+  case V: return launch_bxy_t<BX, BY, NT>(d, p, f, nbx, blkx, nBlk, maxIters, nIterMin, rec, stepCounter, slot2, srcOf, s);
   switch (v) {
     CGX_CASE(0, 2, 4, 512)
     CGX_CASE(1, 2, 2, 1024)

@@ -700,10 +700,8 @@ __global__ void __launch_bounds__(256) k_tracer_rhs(Dims d, Params p, Fields f, 
 // arithmetic, unconditionally (vertical neighbours at clamped levels, whose terms the
 // reference's kk >= 2 / kk <= Nr conditions then drop; 2-D/3-D fields the options do not
 // use read and discarded), so a wave waits on memory once instead of once per branch.
-__global__ void __launch_bounds__(256) k_tracer_rhs_flat(Dims d, Params p, Fields f, TracerArgs a, const int *iterPtr) {
-  MG_PLANE(1, d.sNx, 1, d.sNy, z)
-  const int t = d.t0 + z / d.Nr, k = z % d.Nr + 1;
-  if (i > d.sNx || j > d.sNy) return;
+__device__ __forceinline__ double tracer_flat_point(const Dims &d, const Params &p, const Fields &f, const TracerArgs &a,
+                                                   int i, int j, int k, int t, int myIter) {
   const int Nr = d.Nr;
   const long nx = d.nx, q = MG_I2(d, i, j, t), q3 = MG_I3(d, i, j, k, t);
   const long dku = (k > 1 ? -1L : 0L) * d.n2, dkd = (k < Nr ? 1L : 0L) * d.n2;
@@ -721,7 +719,6 @@ __global__ void __launch_bounds__(256) k_tracer_rhs_flat(Dims d, Params p, Field
   const double maskInC = f.maskInC[q], recip_rA = f.recip_rA[q], rA = f.rA[q];
   const double rhC = f.recip_hFacC[q3], gAdv = f.gAdv[q3], gOld = a.gNm1[q3];
   const double sfc = a.sfc ? a.sfc[q] : 0.0, rsx = f.rStarExpC[q];
-  const int myIter = *iterPtr;
   // ---- arithmetic (k_tracer_rhs<false>'s, term for term)
   const double abFac = (myIter == p.nIter0 && p.nIter0 == 0) ? 0.0 : 0.5 + p.abEps;
   const bool calcAdv = a.advection && !a.multiDim;
@@ -774,9 +771,98 @@ __global__ void __launch_bounds__(256) k_tracer_rhs_flat(Dims d, Params p, Field
   }
   if (p.tracForcingOutAB) gT = gT + gtForc;
   if (rs) gT = gT / rsx;
-  const double v = T0 + p.deltaTtracer * gT;
+  return T0 + p.deltaTtracer * gT;
+}
+
+__global__ void __launch_bounds__(256) k_tracer_rhs_flat(Dims d, Params p, Fields f, TracerArgs a, const int *iterPtr) {
+  MG_PLANE(1, d.sNx, 1, d.sNy, z)
+  const int t = d.t0 + z / d.Nr, k = z % d.Nr + 1;
+  if (i > d.sNx || j > d.sNy) return;
+  const long q3 = MG_I3(d, i, j, k, t);
+  const double v = tracer_flat_point(d, p, f, a, i, j, k, t, *iterPtr);
   if (p.implicitDiffusion) f.gTscr[q3] = v;
   else a.trNext[q3] = v;
+}
+
+// k_tracer_rhs_flat + k_tracer_impl in one column-frame launch (implicitDiffusion without
+// GM/Redi): the k-parallel threads of a column compute T* = T + dt*gT of every level (the
+// flat kernel's expression trees) straight into the LDS right-hand side of the tridiagonal
+// system, beside its coefficients; one thread per column then runs the Thomas sweep
+// (GAD_IMPLICIT_R + SOLVE_TRIDIAGONAL, as k_tracer_impl) and the levels are written back
+// k-parallel.  T* never travels through HBM (no gTscr store and re-load), and the
+// coefficients' operands are the ones the right-hand side just read.  Bit-identical to the
+// two launches.
+__device__ __forceinline__ void tracer_col_body(const Dims &d, const Params &p, const Fields &f, const TracerArgs &a,
+                                                const int *iterPtr, int nc) {
+  extern __shared__ __attribute__((aligned(16))) double lds[];
+  MG_COLF(1, d.sNx, 1, d.sNy, nc)
+  const int Nr = d.Nr, NS = Nr * NC_;
+  double *sSub = lds, *sSup = lds + NS, *sY = lds + 2 * NS;   // sSub holds the solution after the sweeps
+  const int myIter = *iterPtr;
+#define G3(a_, ii, jj, kk_) f.a_[MG_I3(d, ii, jj, kk_, t)]
+  if (valid) {
+    const bool rs = p.nonlinFreeSurf > 0 && p.select_rStar > 0;
+    const long q2 = MG_I2(d, i, j, t);
+    const double rsx = rs ? f.rStarExpC[q2] : 1.0;
+    auto kappa = [&](int k_) { return (G3(IVDConvCount, i, j, k_) * p.ivdc_kappa + 0.0) + a.diffKr; };
+    // one level per pass (not unrolled: the point's operands then fit 4 waves per SIMD)
+#pragma unroll 1
+    MG_COLF_K(k) {
+      const int me = (k - 1) * NC_ + cc;
+      sY[me] = tracer_flat_point(d, p, f, a, i, j, k, t, myIter);
+      const long q3 = MG_I3(d, i, j, k, t);
+      const double rh = rs ? f.recip_hFacC[q3] / rsx : f.recip_hFacC[q3];
+      const double rdrF = f.recip_drF[k - 1];
+      double sub = 0.0, sup = 0.0;
+      if (k >= 2)
+        sub = -(p.deltaTtracer * G3(maskC, i, j, k - 1) * rh * rdrF * kappa(k) * f.recip_drC[k - 1]);
+      if (k <= Nr - 1)
+        sup = -(p.deltaTtracer * G3(maskC, i, j, k + 1) * rh * rdrF * kappa(k + 1) * f.recip_drC[k]);
+      sSub[me] = sub;
+      sSup[me] = sup;
+    }
+  }
+  __syncthreads();
+  if (valid && kk == 0) {
+    double cpPrev = 0.0, ypPrev = 0.0;
+    for (int k2 = 1; k2 <= Nr; k2++) {
+      const int s2 = (k2 - 1) * NC_ + cc;
+      const double sub = sSub[s2], sup = sSup[s2];
+      const double diag = 1.0 - (sub + sup);
+      const double y = sY[s2];
+      double cp, yp;
+      if (k2 == 1) {
+        if (diag != 0.0) { const double rec = 1.0 / diag; cp = sup * rec; yp = y * rec; }
+        else { cp = 0.0; yp = 0.0; }
+      } else {
+        const double tmp = diag - sub * cpPrev;
+        if (tmp != 0.0) { const double rec = 1.0 / tmp; cp = sup * rec; yp = (y - sub * ypPrev) * rec; }
+        else { cp = 0.0; yp = 0.0; }
+      }
+      sSup[s2] = cp;
+      sY[s2] = yp;
+      cpPrev = cp; ypPrev = yp;
+    }
+    double below = 0.0;
+    for (int k2 = Nr; k2 >= 1; k2--) {
+      const int s2 = (k2 - 1) * NC_ + cc;
+      const double v = (k2 == Nr) ? sY[s2] : sY[s2] - sSup[s2] * below;
+      sSub[s2] = v;
+      below = v;
+    }
+  }
+  __syncthreads();
+  if (valid) MG_COLF_K(k) a.trNext[MG_I3(d, i, j, k, t)] = sSub[(k - 1) * NC_ + cc];
+#undef G3
+}
+__global__ void __launch_bounds__(256) k_tracer_col(Dims d, Params p, Fields f, TracerArgs a, const int *iterPtr, int nc) {
+  tracer_col_body(d, p, f, a, iterPtr, nc);
+}
+// the same with the registers capped for 4 waves per SIMD (MGCM_TRACER_COL=4: A/B)
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) k_tracer_col4(Dims d, Params p, Fields f,
+                                                                                              TracerArgs a,
+                                                                                              const int *iterPtr, int nc) {
+  tracer_col_body(d, p, f, a, iterPtr, nc);
 }
 
 // GAD_IMPLICIT_R (implicitDiffusion) + SOLVE_TRIDIAGONAL (Thomas) + CYCLE_TRACER,
@@ -890,7 +976,21 @@ hipError_t launch_tracer_step(const Dims &d, const Params &p, const Fields &f, c
   static const bool flatOff = getenv("MGCM_TRACER_FLAT") && atoi(getenv("MGCM_TRACER_FLAT")) == 0;
   if (p.useGMRedi) hipLaunchKernelGGL(k_tracer_rhs<true>, grd, blk, 0, s, d, p, f, a, iterPtr);
   else if (flatOff) hipLaunchKernelGGL(k_tracer_rhs<false>, grd, blk, 0, s, d, p, f, a, iterPtr);
-  else hipLaunchKernelGGL(k_tracer_rhs_flat, grd, blk, 0, s, d, p, f, a, iterPtr);
+  else if (p.implicitDiffusion && getenv("MGCM_TRACER_COL") && atoi(getenv("MGCM_TRACER_COL")) > 0) {
+    // the right-hand side and the implicit vertical solve in one column-frame launch: opt-in
+    // (MGCM_TRACER_COL=1, =4 with the registers capped).  Bit-identical, but on LLC-90 it
+    // is slower than the flat right-hand side + k_tracer_impl pair it replaces: 331 against
+    // 256 us per tracer, step 2.16 against 2.09 ms (profiles/r03/tracer_col/): the serial
+    // per-column flux sweep at 170 VGPRs costs more than the second launch saves
+    const long ncol = (long)d.sNx * d.sNy * d.nT;
+    const int nc = mg_colf_nc(ncol, d.Nr, 3);
+    static const bool col4 = getenv("MGCM_TRACER_COL") && atoi(getenv("MGCM_TRACER_COL")) == 4;
+    MG_ALLOW_LDS(k_tracer_col);
+    MG_ALLOW_LDS(k_tracer_col4);
+    hipLaunchKernelGGL(col4 ? k_tracer_col4 : k_tracer_col, dim3(mg_colf_blocks(ncol, nc)), blk, mg_colf_lds(d.Nr, nc, 3), s,
+                       d, p, f, a, iterPtr, nc);
+    return hipGetLastError();
+  } else hipLaunchKernelGGL(k_tracer_rhs_flat, grd, blk, 0, s, d, p, f, a, iterPtr);
   if (p.implicitDiffusion) {
     const long ncol = (long)d.sNx * d.sNy * d.nT;
     const int nc = mg_colf_nc(ncol, d.Nr, 3);

@@ -29,7 +29,7 @@ hipError_t launch_cg2d_block(const Dims &, const Params &, const Fields &, const
 int cg2d_block_ppt(int nPts);
 int cg2d_ref_max_points();
 hipError_t launch_cg2d_bxy(int, const Dims &, const Params &, const Fields &, const unsigned *, const int *, int, int,
-                           int, SolveRecord *, int *, hipStream_t);
+                           int, SolveRecord *, int *, const int *, const long *, hipStream_t);
 int cg2d_bxy_geometry(int, int *, int *, int *);
 int cg2d_bxy_variants();
 hipError_t launch_cg2d_blk2(const Dims &, const Params &, const Fields &, const unsigned *, const int *, int, int, int,
@@ -50,7 +50,9 @@ hipError_t launch_exchange_uv_pairs(const Dims &, double *const *, double *const
 hipError_t launch_exch_eta(const Dims &, const Params &, const Fields &, const long *, bool, int, hipStream_t);
 hipError_t launch_corr_cont(const Dims &, const Params &, const Fields &, int, hipStream_t);
 hipError_t launch_calc_r_star(const Dims &, const Params &, const Fields &, const long *, hipStream_t, bool fuseEtaH = false);
-hipError_t launch_update_r_star_cg2d(const Dims &, const Params &, const Fields &, const long *, hipStream_t);
+hipError_t launch_rstar_exch(const Dims &, const Params &, const Fields &, const long *, bool, const XFields &, const long *,
+                             int, int *, hipStream_t);
+hipError_t launch_update_r_star_cg2d(const Dims &, const Params &, const Fields &, const long *, hipStream_t, bool sfp = false);
 hipError_t launch_halo_pack(const Dims &, const XFields &, const long *, long, double *, int, hipStream_t);
 hipError_t launch_oceanic_phys(const Dims &, const Params &, const Fields &, const int *, hipStream_t);
 hipError_t launch_tracer_step(const Dims &, const Params &, const Fields &, const TracerArgs &, const int *, hipStream_t);
@@ -169,6 +171,7 @@ struct mgcm_model {
   int *d_blkx = nullptr;
   int nBlkX = 0;
   int bxyVar = -1;              // k_cg2d_bxy geometry (kernels_solve.hip CGX[])
+  int *d_slot2 = nullptr;       // per 2-D point: k_cg2d_bxy's LDS slot of its value after EXCH, or -1
   bool latlonTopology = true;   // false once a custom halo map (e.g. EXCH2 cube) is installed
   // multi-workgroup CG2D (kernels_cg2d_mwg.hip): tables of every part, device buffers
   bool useMwg = false;
@@ -500,6 +503,20 @@ static int build_nbr(mgcm_model *m) {
         }
         for (int k = 0; k < NB / 2; k++) nbx[(size_t)(NB / 2) * q + k] = v[2 * k] | (v[2 * k + 1] << 16);
       }
+    // the epilogue's EXCH_XY_RL(cg2d_x): every 2-D point's value is the slot of itself
+    // (interior) or of its interior source (halo), -1 where neither (kept as it is)
+    std::vector<int> slot2((size_t)d.n2 * d.nTiles, -1);
+    for (int J = 1; J <= Ny; J++)
+      for (int I = 1; I <= Nx; I++) {
+        int i, j, t;
+        gpt(I, J, i, j, t);
+        slot2[(size_t)MG_I2(d, i, j, t)] = (int)slotOf[(size_t)t * d.sNx * d.sNy + (size_t)(j - 1) * d.sNx + (i - 1)];
+      }
+    for (size_t g = 0; g < slot2.size(); g++)
+      if (srcOf[g] >= 0) slot2[g] = slot2[(size_t)srcOf[g]];
+    if (m->d_slot2) (void)hipFree(m->d_slot2);
+    HIPCHK(hipMalloc(&m->d_slot2, slot2.size() * sizeof(int)));
+    HIPCHK(hipMemcpy(m->d_slot2, slot2.data(), slot2.size() * sizeof(int), hipMemcpyHostToDevice));
     if (m->d_nbx) (void)hipFree(m->d_nbx);
     if (m->d_blkx) (void)hipFree(m->d_blkx);
     HIPCHK(hipMalloc(&m->d_nbx, nbx.size() * sizeof(unsigned)));
@@ -790,6 +807,7 @@ void mgcm_destroy(mgcm_model *m) {
   if (m->d_blk) hipFree(m->d_blk);
   if (m->d_nbx) hipFree(m->d_nbx);
   if (m->d_blkx) hipFree(m->d_blkx);
+  if (m->d_slot2) hipFree(m->d_slot2);
   if (m->d_ctr) hipFree(m->d_ctr);
   for (auto &q : m->exchBuf)
     if (q) hipFree(q);
@@ -985,8 +1003,10 @@ static hipError_t calc_r_star(mgcm_model *m, bool fuseEtaH = false) {
                                                                                  m->f.rStarExpS};
   return launch_exchange_uv_pairs(da, us, vs, 3, m->d_uvAll[0], m->nUvUAll[0], m->nUvVAll[0], m->stream);
 }
-static hipError_t update_r_star_cg2d(mgcm_model *m) {
-  return launch_update_r_star_cg2d(all_tiles(m->d), m->p, m->f, m->d_srcOf, m->stream);
+// sfp: k_sfp_rhs fused into the r* column pass (FORWARD_STEP on the whole domain only: in a
+// tile-sharded run the r* pass covers every tile and the right-hand side this process's own)
+static hipError_t update_r_star_cg2d(mgcm_model *m, bool sfp = false) {
+  return launch_update_r_star_cg2d(all_tiles(m->d), m->p, m->f, m->d_srcOf, m->stream, sfp);
 }
 
 int mgcm_init(mgcm_model *m) {
@@ -1106,7 +1126,13 @@ int mgcm_init(mgcm_model *m) {
   return 0;
 }
 
-static hipError_t launch_cg2d(mgcm_model *m, int maxIters, int nIterMin) {
+// EXCH_XY_RL(cg2d_x) + etaN (k_exch_eta) inside the CG2D launch: the single-workgroup
+// blocked solver holds the whole solution, so its epilogue writes every point's value
+static bool cg2d_fuses_eta(const mgcm_model *m) {
+  return !m->p.cg2dRefOrder && !m->useMwg && m->nBlkX > 0 && m->d_slot2 && m->d.nT == m->d.nTiles;
+}
+
+static hipError_t launch_cg2d(mgcm_model *m, int maxIters, int nIterMin, bool fuseEta = false) {
   if (m->p.cg2dRefOrder)
     return launch_cg2d_block(m->d, m->p, m->f, m->d_nbr, m->d_gofs, m->nPts, maxIters, nIterMin, m->d_rec, m->d_ctr + 1,
                              m->stream);
@@ -1116,8 +1142,7 @@ static hipError_t launch_cg2d(mgcm_model *m, int maxIters, int nIterMin) {
   }
   if (m->nBlkX > 0)
     return launch_cg2d_bxy(m->bxyVar, m->d, m->p, m->f, m->d_nbx, m->d_blkx, m->nBlkX, maxIters, nIterMin, m->d_rec,
-                           m->d_ctr + 1,
-                           m->stream);
+                           m->d_ctr + 1, fuseEta ? m->d_slot2 : nullptr, m->d_srcOf, m->stream);
   if (m->nBlk > 0)
     return launch_cg2d_blk2(m->d, m->p, m->f, m->d_nb4, m->d_blk, m->nBlk, maxIters, nIterMin, m->d_rec, m->d_ctr + 1,
                             m->stream);
@@ -1328,6 +1353,7 @@ static int one_step(mgcm_model *m) {
   const bool stagger = m->p.staggerTimeStep != 0 && m->p.momStepping;
   const bool tracers = m->p.tempStepping || m->p.saltStepping;
   const bool fork = !stagger && m->overlap && !m->timing && m->p.momStepping && tracers;
+  bool endFused = false;   // CALC_R_STAR + blocking exchanges in one launch (below)
   if (stagger) {
     TIMED(K_PHYS, launch_oceanic_phys(m->d, m->p, m->f, m->d_ctr, m->stream));
   } else if (fork) {
@@ -1343,10 +1369,15 @@ static int one_step(mgcm_model *m) {
     if (mgcm_dynamics(m)) return -1;
     if (fork) HIPCHK(hipStreamWaitEvent(m->stream, m->evJoin, 0));
     // forward_step.F:829-877: UPDATE_R_STAR(.TRUE.) + UPDATE_CG2D
-    if (m->p.nonlinFreeSurf > 0) TIMED(K_RSTAR, update_r_star_cg2d(m));
-    TIMED(K_RHS, launch_sfp_rhs(m->d, m->p, m->f, m->stream));
-    TIMED(K_CG2D, launch_cg2d(m, m->p.cg2dMaxIters, m->p.cg2dUseMinResSol - 1));
-    TIMED(K_ETA, launch_exch_eta(m->d, m->p, m->f, m->d_srcOf, false, 0, m->stream));
+    // (launch fusions, common.h MGCM_STEP_FUSE: CALC_DIV_GHAT in the r* column pass;
+    // EXCH(cg2d_x) + etaN in the single-workgroup CG2D's epilogue -- off by default: one CU
+    // walking every 2-D point costs more than the launch it saves)
+    const bool sfpFused = mg_fuse_on(MG_FUSE_SFP) && m->p.nonlinFreeSurf > 0 && m->d.nT == m->d.nTiles;
+    if (m->p.nonlinFreeSurf > 0) TIMED(K_RSTAR, update_r_star_cg2d(m, sfpFused));
+    if (!sfpFused) TIMED(K_RHS, launch_sfp_rhs(m->d, m->p, m->f, m->stream));
+    const bool etaFused = mg_fuse_on(MG_FUSE_ETA) && cg2d_fuses_eta(m);
+    TIMED(K_CG2D, launch_cg2d(m, m->p.cg2dMaxIters, m->p.cg2dUseMinResSol - 1, etaFused));
+    if (!etaFused) TIMED(K_ETA, launch_exch_eta(m->d, m->p, m->f, m->d_srcOf, false, 0, m->stream));
     TIMED(K_CONT, launch_corr_cont(m->d, m->p, m->f, 0, m->stream));
     // forward_step.F:965-977: CALC_R_STAR(etaH(n+1)); the next step's RESET_NLFS_VARS +
     // UPDATE_R_STAR(.FALSE.) restore the hFac in place, so they are not repeated here.
@@ -1355,7 +1386,14 @@ static int one_step(mgcm_model *m) {
     static const bool noFuse = getenv("MGCM_NO_ETAH_FUSE") && atoi(getenv("MGCM_NO_ETAH_FUSE")) == 1;
     const bool fuseEtaH = m->p.exactConserv && m->p.nonlinFreeSurf > 0 && !noFuse;
     if (m->p.exactConserv && !fuseEtaH) TIMED(K_ETA, launch_exch_eta(m->d, m->p, m->f, m->d_srcOf, true, 0, m->stream));
-    if (m->p.nonlinFreeSurf > 0) TIMED(K_RSTAR, calc_r_star(m, fuseEtaH));
+    // CALC_R_STAR and the blocking exchanges in one grid on the small lat-lon grids
+    // (k_rstar_exch; independent, and nothing between them in the non-staggered step)
+    endFused = m->p.nonlinFreeSurf > 0 && !stagger && !m->uvMap && m->d.nT == m->d.nTiles &&
+               mg_hfuse(MG_FUSE_END, m->d.nx, m->d.ny, m->d.nT, m->d.Nr);
+    if (endFused)
+      TIMED(K_RSTAR, launch_rstar_exch(m->d, m->p, m->f, m->d_srcOf, fuseEtaH, blocking_fields(m), m->d_halo, m->nHalo,
+                                       m->d_ctr, m->stream));
+    else if (m->p.nonlinFreeSurf > 0) TIMED(K_RSTAR, calc_r_star(m, fuseEtaH));
   } else {
     if (mgcm_integr_continuity(m)) return -1;
   }
@@ -1372,6 +1410,7 @@ static int one_step(mgcm_model *m) {
     }
     if (tracers_on(m, m->stream)) return -1;
   }
+  if (endFused) return 0;
   if (m->uvMap)   // the vector pair and the scalar fields in one launch
     TIMED(K_EXCH, launch_exchange_mixed(m->d, m->f.uVel, m->f.vVel, m->d.Nr, m->d_uv[1], m->nUvU[1], m->nUvV[1],
                                         blocking_fields(m), m->d_halo, m->nHalo, m->d_ctr, m->stream));
@@ -1762,6 +1801,22 @@ int mgcm_solve_stats(mgcm_model *m, int back, double *firstResidual, double *las
   if (lastResidual) *lastResidual = r.lastResidual;
   if (numIters) *numIters = r.numIters;
   if (rhsMax) *rhsMax = r.rhsMax;
+  return 0;
+}
+
+// The last n steps' solve records in one copy (oldest first): what a caller checks after a
+// batch without a device-to-host transfer per step.
+int mgcm_solve_history(mgcm_model *m, int n, int *numIters, double *firstResidual, double *lastResidual) {
+  HIPCHK(hipStreamSynchronize(m->stream));
+  if (n < 0 || n > m->lastBatch) return set_err("mgcm_solve_history: %d steps asked, %d in the last batch", n, m->lastBatch);
+  if (n == 0) return 0;
+  std::vector<SolveRecord> r((size_t)n);
+  HIPCHK(hipMemcpy(r.data(), m->d_rec + (m->lastBatch - n), (size_t)n * sizeof(SolveRecord), hipMemcpyDeviceToHost));
+  for (int q = 0; q < n; q++) {
+    if (numIters) numIters[q] = r[q].numIters;
+    if (firstResidual) firstResidual[q] = r[q].firstResidual;
+    if (lastResidual) lastResidual[q] = r[q].lastResidual;
+  }
   return 0;
 }
 

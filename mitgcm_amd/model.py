@@ -162,6 +162,15 @@ class Model:
         return {"cg2d_init_res": f.value, "cg2d_last_res": la.value, "cg2d_iters": it.value,
                 "cg2d_rhs_max": rm.value}
 
+    def solve_history(self, n):
+        """numIters, firstResidual, lastResidual of the last n steps (oldest first), one copy."""
+        it = np.zeros(n, dtype=np.int32)
+        fr = np.zeros(n)
+        lr = np.zeros(n)
+        check(lib().mgcm_solve_history(self.h, n, it.ctypes.data_as(ctypes.POINTER(ctypes.c_int)), _dp(fr), _dp(lr)),
+              "mgcm_solve_history")
+        return it, fr, lr
+
     def cg2d(self, b, x, maxIters, nIterMin=-1):
         b = np.ascontiguousarray(b, dtype=np.float64).copy()
         x = np.ascontiguousarray(x, dtype=np.float64).copy()
