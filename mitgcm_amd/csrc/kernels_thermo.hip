@@ -700,26 +700,25 @@ __global__ void __launch_bounds__(256) k_tracer_rhs(Dims d, Params p, Fields f, 
 // arithmetic, unconditionally (vertical neighbours at clamped levels, whose terms the
 // reference's kk >= 2 / kk <= Nr conditions then drop; 2-D/3-D fields the options do not
 // use read and discarded), so a wave waits on memory once instead of once per branch.
-__device__ __forceinline__ double tracer_flat_point(const Dims &d, const Params &p, const Fields &f, const TracerArgs &a,
-                                                   int i, int j, int k, int t, int myIter) {
-  const int Nr = d.Nr;
-  const long nx = d.nx, q = MG_I2(d, i, j, t), q3 = MG_I3(d, i, j, k, t);
-  const long dku = (k > 1 ? -1L : 0L) * d.n2, dkd = (k < Nr ? 1L : 0L) * d.n2;
-  const double *__restrict__ T = a.tr;
-  // ---- loads
-  const double T0 = T[q3], Tw = T[q3 - 1], Te = T[q3 + 1], Ts = T[q3 - nx], Tn = T[q3 + nx];
-  const double Tu = T[q3 + dku], Td = T[q3 + dkd];
-  const double u0 = f.uVel[q3], u1 = f.uVel[q3 + 1], v0 = f.vVel[q3], v1 = f.vVel[q3 + nx];
-  const double w0 = f.wVel[q3], w1 = f.wVel[q3 + dkd];
-  const double hW0 = f.hFacW[q3], hW1 = f.hFacW[q3 + 1], hS0 = f.hFacS[q3], hS1 = f.hFacS[q3 + nx];
-  const double mCu = f.maskC[q3 + dku], mC0 = f.maskC[q3], mCd = f.maskC[q3 + dkd];
-  const double ivd0 = f.IVDConvCount[q3], ivd1 = f.IVDConvCount[q3 + dkd];
-  const double dyG0 = f.dyG[q], dyG1 = f.dyG[q + 1], dxG0 = f.dxG[q], dxG1 = f.dxG[q + nx];
-  const double rdxC0 = f.recip_dxC[q], rdxC1 = f.recip_dxC[q + 1], rdyC0 = f.recip_dyC[q], rdyC1 = f.recip_dyC[q + nx];
-  const double maskInC = f.maskInC[q], recip_rA = f.recip_rA[q], rA = f.rA[q];
-  const double rhC = f.recip_hFacC[q3], gAdv = f.gAdv[q3], gOld = a.gNm1[q3];
-  const double sfc = a.sfc ? a.sfc[q] : 0.0, rsx = f.rStarExpC[q];
-  // ---- arithmetic (k_tracer_rhs<false>'s, term for term)
+// The operands of one point: 2-D (k-invariant) and 3-D at levels k-1, k, k+1.
+struct TrCol {   // the k-invariant operands of a column
+  double dyG0, dyG1, dxG0, dxG1, rdxC0, rdxC1, rdyC0, rdyC1, maskInC, recip_rA, rA, sfc, rsx;
+};
+struct TrLev {   // level k's operands (Tu/mCu/... at k-1 and Td/w1/mCd/ivd1 at k+1, clamped)
+  double T0, Tw, Te, Ts, Tn, Tu, Td, u0, u1, v0, v1, w0, w1, hW0, hW1, hS0, hS1, mCu, mC0, mCd, ivd0, ivd1, rhC, gAdv,
+      gOld;
+};
+__device__ __forceinline__ void tracer_load_col(const Dims &d, const Fields &f, const TracerArgs &a, long q, TrCol &c) {
+  const long nx = d.nx;
+  c.dyG0 = f.dyG[q]; c.dyG1 = f.dyG[q + 1]; c.dxG0 = f.dxG[q]; c.dxG1 = f.dxG[q + nx];
+  c.rdxC0 = f.recip_dxC[q]; c.rdxC1 = f.recip_dxC[q + 1]; c.rdyC0 = f.recip_dyC[q]; c.rdyC1 = f.recip_dyC[q + nx];
+  c.maskInC = f.maskInC[q]; c.recip_rA = f.recip_rA[q]; c.rA = f.rA[q];
+  c.sfc = a.sfc ? a.sfc[q] : 0.0; c.rsx = f.rStarExpC[q];
+}
+// T*, and (useAB) the new AB history value into *gN, from the operands: k_tracer_rhs<false>'s
+// arithmetic, term for term
+__device__ __forceinline__ double tracer_flat_arith(const Params &p, const Fields &f, const TracerArgs &a, int Nr, int k,
+                                                    int myIter, const TrCol &c, const TrLev &o, double *gN) {
   const double abFac = (myIter == p.nIter0 && p.nIter0 == 0) ? 0.0 : 0.5 + p.abEps;
   const bool calcAdv = a.advection && !a.multiDim;
   const double advFac = calcAdv ? 1.0 : 0.0, rAdvFac = p.rkSign * advFac;
@@ -732,46 +731,257 @@ __device__ __forceinline__ double tracer_flat_point(const Dims &d, const Params 
     if (a.diffKh != 0.0) df = -a.diffKh * A * rd * (tp - tm);
     return fz + df;
   };
-  const double rTrans = k <= 1 ? 0.0 : w0 * rA * (mCu * mC0);
-  const double rTransKp = k + 1 > Nr ? 0.0 : w1 * rA * (mC0 * mCd);
+  const double rTrans = k <= 1 ? 0.0 : o.w0 * c.rA * (o.mCu * o.mC0);
+  const double rTransKp = k + 1 > Nr ? 0.0 : o.w1 * c.rA * (o.mC0 * o.mCd);
   auto fvert = [&](int kk, double rTr, double mUpper, double mLower, double tLower, double tUpper, double ivd) {
     double fv = 0.0;
     if (kk >= 2 && kk <= Nr && calcAdv) {
       const double wT = mUpper * rTr * (tLower + tUpper) * 0.5;
-      fv = fv + wT * maskInC;
+      fv = fv + wT * c.maskInC;
     }
     double dfr = 0.0;
     if (!p.implicitDiffusion && kk >= 2 && kk <= Nr) {
       const double kap = (ivd * p.ivdc_kappa + 0.0) + a.diffKr;
       const double maskUp = mUpper * mLower;
-      dfr = -kap * maskUp * rA * f.recip_drC[kk - 1] * (tLower - tUpper) * p.rkSign;
+      dfr = -kap * maskUp * c.rA * f.recip_drC[kk - 1] * (tLower - tUpper) * p.rkSign;
     }
     return fv + dfr;
   };
-  const double uT0 = u0 * (dyG0 * drF * hW0), uT1 = u1 * (dyG1 * drF * hW1);
-  const double vT0 = v0 * (dxG0 * drF * hS0), vT1 = v1 * (dxG1 * drF * hS1);
-  const double fVerUp = fvert(k, rTrans, mCu, mC0, T0, Tu, ivd0);
-  const double fVerDn = fvert(k + 1, rTransKp, mC0, mCd, Td, T0, ivd1);
-  const double fZi = face(u0, dyG0, hW0, rdxC0, T0, Tw), fZe = face(u1, dyG1, hW1, rdxC1, Te, T0);
-  const double fMi = face(v0, dxG0, hS0, rdyC0, T0, Ts), fMn = face(v1, dxG1, hS1, rdyC1, Tn, T0);
-  const double g0 = a.multiDim ? gAdv : 0.0;
-  double gT = g0 - rhC * f.recip_drF[k - 1] * recip_rA *
-                       ((fZe - fZi) * maskInC + (fMn - fMi) * maskInC + (fVerDn - fVerUp) * p.rkSign -
-                        T0 * ((uT1 - uT0) * advFac + (vT1 - vT0) * advFac + (rTransKp - rTrans) * rAdvFac) * maskInC);
+  const double uT0 = o.u0 * (c.dyG0 * drF * o.hW0), uT1 = o.u1 * (c.dyG1 * drF * o.hW1);
+  const double vT0 = o.v0 * (c.dxG0 * drF * o.hS0), vT1 = o.v1 * (c.dxG1 * drF * o.hS1);
+  const double fVerUp = fvert(k, rTrans, o.mCu, o.mC0, o.T0, o.Tu, o.ivd0);
+  const double fVerDn = fvert(k + 1, rTransKp, o.mC0, o.mCd, o.Td, o.T0, o.ivd1);
+  const double fZi = face(o.u0, c.dyG0, o.hW0, c.rdxC0, o.T0, o.Tw), fZe = face(o.u1, c.dyG1, o.hW1, c.rdxC1, o.Te, o.T0);
+  const double fMi = face(o.v0, c.dxG0, o.hS0, c.rdyC0, o.T0, o.Ts), fMn = face(o.v1, c.dxG1, o.hS1, c.rdyC1, o.Tn, o.T0);
+  const double g0 = a.multiDim ? o.gAdv : 0.0;
+  double gT = g0 - o.rhC * f.recip_drF[k - 1] * c.recip_rA *
+                       ((fZe - fZi) * c.maskInC + (fMn - fMi) * c.maskInC + (fVerDn - fVerUp) * p.rkSign -
+                        o.T0 * ((uT1 - uT0) * advFac + (vT1 - vT0) * advFac + (rTransKp - rTrans) * rAdvFac) * c.maskInC);
   double gtForc = 0.0;
-  if (a.forcing && a.sfc && k == 1) gtForc = gtForc + sfc * f.recip_drF[0] * rhC;
+  if (a.forcing && a.sfc && k == 1) gtForc = gtForc + c.sfc * f.recip_drF[0] * o.rhC;
   if (!p.tracForcingOutAB) gT = gT + gtForc;
   const bool rs = p.nonlinFreeSurf > 0 && p.select_rStar > 0;
   if (a.useAB) {
-    const double ab = abFac * (gT - gOld);
-    double gN = gT;
+    const double ab = abFac * (gT - o.gOld);
+    double gNv = gT;
     gT = gT + ab;
-    if (rs) gN = gN / rsx;
-    a.gNm1[q3] = gN;
+    if (rs) gNv = gNv / c.rsx;
+    *gN = gNv;
   }
   if (p.tracForcingOutAB) gT = gT + gtForc;
-  if (rs) gT = gT / rsx;
-  return T0 + p.deltaTtracer * gT;
+  if (rs) gT = gT / c.rsx;
+  return o.T0 + p.deltaTtracer * gT;
+}
+__device__ __forceinline__ double tracer_flat_point(const Dims &d, const Params &p, const Fields &f, const TracerArgs &a,
+                                                   int i, int j, int k, int t, int myIter) {
+  const int Nr = d.Nr;
+  const long nx = d.nx, q = MG_I2(d, i, j, t), q3 = MG_I3(d, i, j, k, t);
+  const long dku = (k > 1 ? -1L : 0L) * d.n2, dkd = (k < Nr ? 1L : 0L) * d.n2;
+  const double *__restrict__ T = a.tr;
+  TrLev o;
+  o.T0 = T[q3]; o.Tw = T[q3 - 1]; o.Te = T[q3 + 1]; o.Ts = T[q3 - nx]; o.Tn = T[q3 + nx];
+  o.Tu = T[q3 + dku]; o.Td = T[q3 + dkd];
+  o.u0 = f.uVel[q3]; o.u1 = f.uVel[q3 + 1]; o.v0 = f.vVel[q3]; o.v1 = f.vVel[q3 + nx];
+  o.w0 = f.wVel[q3]; o.w1 = f.wVel[q3 + dkd];
+  o.hW0 = f.hFacW[q3]; o.hW1 = f.hFacW[q3 + 1]; o.hS0 = f.hFacS[q3]; o.hS1 = f.hFacS[q3 + nx];
+  o.mCu = f.maskC[q3 + dku]; o.mC0 = f.maskC[q3]; o.mCd = f.maskC[q3 + dkd];
+  o.ivd0 = f.IVDConvCount[q3]; o.ivd1 = f.IVDConvCount[q3 + dkd];
+  TrCol c;
+  tracer_load_col(d, f, a, q, c);
+  o.rhC = f.recip_hFacC[q3]; o.gAdv = f.gAdv[q3]; o.gOld = a.gNm1[q3];
+  double gN = 0.0;
+  const double v = tracer_flat_arith(p, f, a, Nr, k, myIter, c, o, &gN);
+  if (a.useAB) a.gNm1[q3] = gN;
+  return v;
+}
+
+// The flat right-hand side as a k-march (LLC-sized grids): a workgroup owns a 32 x 8 (i, j)
+// tile of one tile's interior and walks levels k0..k0+KC-1, each thread one column.  The
+// column's k-invariant operands are loaded once, its own T, w, maskC and IVDConvCount at k-1,
+// k, k+1 are carried in registers from level to level (one new level per step instead of
+// three), so the vertical neighbours are never re-fetched by another workgroup -- the flat
+// kernel's over-fetch (616 MB HBM for 173 MB of operands on LLC-90).  Same operands, same
+// arithmetic (tracer_flat_arith): bit-identical.
+constexpr int TRM_TX = 32, TRM_TY = 8;
+__global__ void __launch_bounds__(256) k_tracer_march(Dims d, Params p, Fields f, TracerArgs a, const int *iterPtr, int KC,
+                                                     int nkc, int ntx, int nty) {
+  int b = mg_xcd_block();
+  const int kc = b % nkc;
+  b /= nkc;
+  const int tx = b % ntx, ty = (b / ntx) % nty, t = d.t0 + b / (ntx * nty);
+  const int i = 1 + tx * TRM_TX + (int)(threadIdx.x % TRM_TX), j = 1 + ty * TRM_TY + (int)(threadIdx.x / TRM_TX);
+  if (i > d.sNx || j > d.sNy) return;
+  const int Nr = d.Nr, k0 = 1 + kc * KC, k1 = min(Nr, k0 + KC - 1);
+  const int myIter = *iterPtr;
+  const long nx = d.nx, n2 = d.n2, q = MG_I2(d, i, j, t);
+  const double *__restrict__ T = a.tr;
+  TrCol c;
+  tracer_load_col(d, f, a, q, c);
+  long q3 = MG_I3(d, i, j, k0, t);
+  const long qu = k0 > 1 ? q3 - n2 : q3;
+  double Tu = T[qu], mCu = f.maskC[qu];
+  double T0 = T[q3], mC0 = f.maskC[q3], w0 = f.wVel[q3], ivd0 = f.IVDConvCount[q3];
+  for (int k = k0; k <= k1; k++, q3 += n2) {
+    const long qd = k < Nr ? q3 + n2 : q3;
+    TrLev o;
+    o.T0 = T0; o.Tu = Tu; o.mC0 = mC0; o.mCu = mCu; o.w0 = w0; o.ivd0 = ivd0;
+    o.Td = T[qd]; o.mCd = f.maskC[qd]; o.w1 = f.wVel[qd]; o.ivd1 = f.IVDConvCount[qd];
+    o.Tw = T[q3 - 1]; o.Te = T[q3 + 1]; o.Ts = T[q3 - nx]; o.Tn = T[q3 + nx];
+    o.u0 = f.uVel[q3]; o.u1 = f.uVel[q3 + 1]; o.v0 = f.vVel[q3]; o.v1 = f.vVel[q3 + nx];
+    o.hW0 = f.hFacW[q3]; o.hW1 = f.hFacW[q3 + 1]; o.hS0 = f.hFacS[q3]; o.hS1 = f.hFacS[q3 + nx];
+    o.rhC = f.recip_hFacC[q3]; o.gAdv = a.multiDim ? f.gAdv[q3] : 0.0; o.gOld = a.useAB ? a.gNm1[q3] : 0.0;
+    double gN = 0.0;
+    const double v = tracer_flat_arith(p, f, a, Nr, k, myIter, c, o, &gN);
+    if (a.useAB) a.gNm1[q3] = gN;
+    if (p.implicitDiffusion) f.gTscr[q3] = v;
+    else a.trNext[q3] = v;
+    Tu = T0; T0 = o.Td; mCu = mC0; mC0 = o.mCd; w0 = o.w1; ivd0 = o.ivd1;
+  }
+}
+
+// TEMP_INTEGRATE and SALT_INTEGRATE together (both stepped, no GM/Redi, no multi-dimensional
+// advection: LLC-90's C2 tracers): the k-march of k_tracer_march over the two tracers at
+// once, so the operands they share -- u, v, w, hFacW/S, maskC, IVDConvCount, recip_hFacC and
+// the column's metrics -- are fetched once for both (12 3-D loads per point instead of 20).
+// T* of theta goes to gTscr, of salt to cpScr, for k_tracer2_impl.  Each tracer's arithmetic
+// is tracer_flat_arith's: bit-identical to the two separate launches.
+__device__ __forceinline__ void tracer2_march_body(const Dims &d, const Params &p, const Fields &f, const TracerArgs &aT,
+                                                   const TracerArgs &aS, const int *iterPtr, int KC, int nkc, int ntx,
+                                                   int nty) {
+  int b = mg_xcd_block();
+  const int kc = b % nkc;
+  b /= nkc;
+  const int tx = b % ntx, ty = (b / ntx) % nty, t = d.t0 + b / (ntx * nty);
+  const int i = 1 + tx * TRM_TX + (int)(threadIdx.x % TRM_TX), j = 1 + ty * TRM_TY + (int)(threadIdx.x / TRM_TX);
+  if (i > d.sNx || j > d.sNy) return;
+  const int Nr = d.Nr, k0 = 1 + kc * KC, k1 = min(Nr, k0 + KC - 1);
+  const int myIter = *iterPtr;
+  const long nx = d.nx, n2 = d.n2, q = MG_I2(d, i, j, t);
+  const double *__restrict__ T = aT.tr;
+  const double *__restrict__ S = aS.tr;
+  TrCol cT, cS;
+  tracer_load_col(d, f, aT, q, cT);
+  cS = cT;
+  cS.sfc = aS.sfc ? aS.sfc[q] : 0.0;
+  long q3 = MG_I3(d, i, j, k0, t);
+  const long qu = k0 > 1 ? q3 - n2 : q3;
+  double Tu = T[qu], Su = S[qu], mCu = f.maskC[qu];
+  double T0 = T[q3], S0 = S[q3], mC0 = f.maskC[q3], w0 = f.wVel[q3], ivd0 = f.IVDConvCount[q3];
+  const bool impl = p.implicitDiffusion != 0;
+  for (int k = k0; k <= k1; k++, q3 += n2) {
+    const long qd = k < Nr ? q3 + n2 : q3;
+    TrLev o;
+    o.mC0 = mC0; o.mCu = mCu; o.w0 = w0; o.ivd0 = ivd0;
+    o.mCd = f.maskC[qd]; o.w1 = f.wVel[qd]; o.ivd1 = f.IVDConvCount[qd];
+    o.u0 = f.uVel[q3]; o.u1 = f.uVel[q3 + 1]; o.v0 = f.vVel[q3]; o.v1 = f.vVel[q3 + nx];
+    o.hW0 = f.hFacW[q3]; o.hW1 = f.hFacW[q3 + 1]; o.hS0 = f.hFacS[q3]; o.hS1 = f.hFacS[q3 + nx];
+    o.rhC = f.recip_hFacC[q3]; o.gAdv = 0.0;
+    TrLev oS = o;
+    o.T0 = T0; o.Tu = Tu; o.Td = T[qd];
+    o.Tw = T[q3 - 1]; o.Te = T[q3 + 1]; o.Ts = T[q3 - nx]; o.Tn = T[q3 + nx];
+    o.gOld = aT.useAB ? aT.gNm1[q3] : 0.0;
+    oS.T0 = S0; oS.Tu = Su; oS.Td = S[qd];
+    oS.Tw = S[q3 - 1]; oS.Te = S[q3 + 1]; oS.Ts = S[q3 - nx]; oS.Tn = S[q3 + nx];
+    oS.gOld = aS.useAB ? aS.gNm1[q3] : 0.0;
+    double gNT = 0.0, gNS = 0.0;
+    const double vT = tracer_flat_arith(p, f, aT, Nr, k, myIter, cT, o, &gNT);
+    const double vS = tracer_flat_arith(p, f, aS, Nr, k, myIter, cS, oS, &gNS);
+    if (aT.useAB) aT.gNm1[q3] = gNT;
+    if (aS.useAB) aS.gNm1[q3] = gNS;
+    if (impl) { f.gTscr[q3] = vT; f.cpScr[q3] = vS; }
+    else { aT.trNext[q3] = vT; aS.trNext[q3] = vS; }
+    Tu = T0; T0 = o.Td; Su = S0; S0 = oS.Td;
+    mCu = mC0; mC0 = o.mCd; w0 = o.w1; ivd0 = o.ivd1;
+  }
+}
+__global__ void __launch_bounds__(256) k_tracer2_march(Dims d, Params p, Fields f, TracerArgs aT, TracerArgs aS,
+                                                      const int *iterPtr, int KC, int nkc, int ntx, int nty) {
+  tracer2_march_body(d, p, f, aT, aS, iterPtr, KC, nkc, ntx, nty);
+}
+// registers capped for 3 / 4 waves per SIMD (MGCM_TR2_WAVES=3|4: A/B)
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3)))
+k_tracer2_march_w3(Dims d, Params p, Fields f, TracerArgs aT, TracerArgs aS, const int *iterPtr, int KC, int nkc, int ntx,
+                   int nty) {
+  tracer2_march_body(d, p, f, aT, aS, iterPtr, KC, nkc, ntx, nty);
+}
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4)))
+k_tracer2_march_w4(Dims d, Params p, Fields f, TracerArgs aT, TracerArgs aS, const int *iterPtr, int KC, int nkc, int ntx,
+                   int nty) {
+  tracer2_march_body(d, p, f, aT, aS, iterPtr, KC, nkc, ntx, nty);
+}
+
+// GAD_IMPLICIT_R + SOLVE_TRIDIAGONAL of both tracers per column (k_tracer_impl twice, without
+// GM/Redi): maskC, IVDConvCount and recip_hFacC fetched once; thread (c, 0) sweeps theta's
+// system and thread (c, 1) salt's, concurrently.
+__global__ void __launch_bounds__(256) k_tracer2_impl(Dims d, Params p, Fields f, TracerArgs aT, TracerArgs aS, int nc) {
+  extern __shared__ __attribute__((aligned(16))) double lds[];
+  MG_COLF(1, d.sNx, 1, d.sNy, nc)
+  const int Nr = d.Nr, NS = Nr * NC_;
+  double *sl[2][3] = {{lds, lds + NS, lds + 2 * NS}, {lds + 3 * NS, lds + 4 * NS, lds + 5 * NS}};   // sub, sup, y
+#define G3(a_, ii, jj, kk_) f.a_[MG_I3(d, ii, jj, kk_, t)]
+  if (valid) {
+    const bool rs = p.nonlinFreeSurf > 0 && p.select_rStar > 0;
+    const long q2 = MG_I2(d, i, j, t);
+    const double rsx = rs ? f.rStarExpC[q2] : 1.0;
+    MG_COLF_K(k) {
+      const int me = (k - 1) * NC_ + cc;
+      const long q3 = MG_I3(d, i, j, k, t);
+      const double rh = rs ? f.recip_hFacC[q3] / rsx : f.recip_hFacC[q3];
+      const double rdrF = f.recip_drF[k - 1];
+      const double ivK = G3(IVDConvCount, i, j, k) * p.ivdc_kappa + 0.0;
+      const double ivK1 = k <= Nr - 1 ? G3(IVDConvCount, i, j, k + 1) * p.ivdc_kappa + 0.0 : 0.0;
+      const double mU = k >= 2 ? G3(maskC, i, j, k - 1) : 0.0, mD = k <= Nr - 1 ? G3(maskC, i, j, k + 1) : 0.0;
+#pragma unroll
+      for (int c2 = 0; c2 < 2; c2++) {
+        const double kr = c2 ? aS.diffKr : aT.diffKr;
+        double sub = 0.0, sup = 0.0;
+        if (k >= 2) sub = -(p.deltaTtracer * mU * rh * rdrF * (ivK + kr) * f.recip_drC[k - 1]);
+        if (k <= Nr - 1) sup = -(p.deltaTtracer * mD * rh * rdrF * (ivK1 + kr) * f.recip_drC[k]);
+        sl[c2][0][me] = sub;
+        sl[c2][1][me] = sup;
+      }
+      sl[0][2][me] = f.gTscr[q3];
+      sl[1][2][me] = f.cpScr[q3];
+    }
+  }
+  __syncthreads();
+  if (valid && kk < 2) {
+    double *sSub = sl[kk][0], *sSup = sl[kk][1], *sY = sl[kk][2];
+    double cpPrev = 0.0, ypPrev = 0.0;
+    for (int k2 = 1; k2 <= Nr; k2++) {
+      const int s2 = (k2 - 1) * NC_ + cc;
+      const double sub = sSub[s2], sup = sSup[s2];
+      const double diag = 1.0 - (sub + sup);
+      const double y = sY[s2];
+      double cp, yp;
+      if (k2 == 1) {
+        if (diag != 0.0) { const double rec = 1.0 / diag; cp = sup * rec; yp = y * rec; }
+        else { cp = 0.0; yp = 0.0; }
+      } else {
+        const double tmp = diag - sub * cpPrev;
+        if (tmp != 0.0) { const double rec = 1.0 / tmp; cp = sup * rec; yp = (y - sub * ypPrev) * rec; }
+        else { cp = 0.0; yp = 0.0; }
+      }
+      sSup[s2] = cp;
+      sY[s2] = yp;
+      cpPrev = cp; ypPrev = yp;
+    }
+    double below = 0.0;
+    for (int k2 = Nr; k2 >= 1; k2--) {
+      const int s2 = (k2 - 1) * NC_ + cc;
+      const double v = (k2 == Nr) ? sY[s2] : sY[s2] - sSup[s2] * below;
+      sSub[s2] = v;
+      below = v;
+    }
+  }
+  __syncthreads();
+  if (valid) MG_COLF_K(k) {
+    const int me = (k - 1) * NC_ + cc;
+    const long q3 = MG_I3(d, i, j, k, t);
+    aT.trNext[q3] = sl[0][0][me];
+    aS.trNext[q3] = sl[1][0][me];
+  }
+#undef G3
 }
 
 __global__ void __launch_bounds__(256) k_tracer_rhs_flat(Dims d, Params p, Fields f, TracerArgs a, const int *iterPtr) {
@@ -948,6 +1158,40 @@ hipError_t launch_oceanic_phys(const Dims &d, const Params &p, const Fields &f, 
   return hipGetLastError();
 }
 
+static bool tracer_march_on(const Dims &d) {
+  const char *e = getenv("MGCM_TRACER_MARCH");   // read per launch (tests switch it per model)
+  if (e) return atoi(e) != 0;
+  return d.Nr >= 30;
+}
+
+// Both tracers in one pair of launches (k_tracer2_march + k_tracer2_impl) where the options
+// allow it (tracer_pair_ok): the deep-grid k-march path without GM/Redi or multi-dimensional
+// advection.  MGCM_TRACER_PAIR=0 keeps one tracer at a time.
+bool tracer_pair_ok(const Dims &d, const Params &p, const TracerArgs &aT, const TracerArgs &aS) {
+  const char *e = getenv("MGCM_TRACER_PAIR");
+  if (e && atoi(e) == 0) return false;
+  return p.tempStepping && p.saltStepping && !p.useGMRedi && !aT.multiDim && !aS.multiDim && tracer_march_on(d) &&
+         !(getenv("MGCM_TRACER_FLAT") && atoi(getenv("MGCM_TRACER_FLAT")) == 0);
+}
+
+hipError_t launch_tracer_pair(const Dims &d, const Params &p, const Fields &f, const TracerArgs &aT, const TracerArgs &aS,
+                              const int *iterPtr, hipStream_t s) {
+  const dim3 blk(MG_PLANE_THREADS);
+  const int kcEnv = getenv("MGCM_TR_KC") ? atoi(getenv("MGCM_TR_KC")) : 0;
+  const int KC = kcEnv > 0 ? (kcEnv > d.Nr ? d.Nr : kcEnv) : (d.Nr + 4) / 5;
+  const int nkc = (d.Nr + KC - 1) / KC, ntx = (d.sNx + TRM_TX - 1) / TRM_TX, nty = (d.sNy + TRM_TY - 1) / TRM_TY;
+  const int wv = getenv("MGCM_TR2_WAVES") ? atoi(getenv("MGCM_TR2_WAVES")) : 0;
+  hipLaunchKernelGGL(wv == 3 ? k_tracer2_march_w3 : wv == 4 ? k_tracer2_march_w4 : k_tracer2_march,
+                     dim3((unsigned)(nkc * ntx * nty * d.nT)), blk, 0, s, d, p, f, aT, aS, iterPtr, KC, nkc, ntx, nty);
+  if (p.implicitDiffusion) {
+    const long ncol = (long)d.sNx * d.sNy * d.nT;
+    const int nc = mg_colf_nc(ncol, d.Nr, 6);
+    MG_ALLOW_LDS(k_tracer2_impl);
+    hipLaunchKernelGGL(k_tracer2_impl, dim3(mg_colf_blocks(ncol, nc)), blk, mg_colf_lds(d.Nr, nc, 6), s, d, p, f, aT, aS, nc);
+  }
+  return hipGetLastError();
+}
+
 hipError_t launch_tracer_step(const Dims &d, const Params &p, const Fields &f, const TracerArgs &a, const int *iterPtr,
                               hipStream_t s) {
   const dim3 blk(MG_PLANE_THREADS), grd(mg_plane_blocks(d.sNx, d.sNy, d.nT * d.Nr));
@@ -990,6 +1234,13 @@ hipError_t launch_tracer_step(const Dims &d, const Params &p, const Fields &f, c
     hipLaunchKernelGGL(col4 ? k_tracer_col4 : k_tracer_col, dim3(mg_colf_blocks(ncol, nc)), blk, mg_colf_lds(d.Nr, nc, 3), s,
                        d, p, f, a, iterPtr, nc);
     return hipGetLastError();
+  } else if (tracer_march_on(d)) {
+    // the k-march (deep grids; MGCM_TRACER_MARCH=0|1 overrides, MGCM_TR_KC levels per workgroup)
+    const int kcEnv = getenv("MGCM_TR_KC") ? atoi(getenv("MGCM_TR_KC")) : 0;
+    const int KC = kcEnv > 0 ? (kcEnv > d.Nr ? d.Nr : kcEnv) : (d.Nr + 4) / 5;
+    const int nkc = (d.Nr + KC - 1) / KC, ntx = (d.sNx + TRM_TX - 1) / TRM_TX, nty = (d.sNy + TRM_TY - 1) / TRM_TY;
+    hipLaunchKernelGGL(k_tracer_march, dim3((unsigned)(nkc * ntx * nty * d.nT)), blk, 0, s, d, p, f, a, iterPtr, KC, nkc,
+                       ntx, nty);
   } else hipLaunchKernelGGL(k_tracer_rhs_flat, grd, blk, 0, s, d, p, f, a, iterPtr);
   if (p.implicitDiffusion) {
     const long ncol = (long)d.sNx * d.sNy * d.nT;

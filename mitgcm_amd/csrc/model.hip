@@ -56,6 +56,9 @@ hipError_t launch_update_r_star_cg2d(const Dims &, const Params &, const Fields 
 hipError_t launch_halo_pack(const Dims &, const XFields &, const long *, long, double *, int, hipStream_t);
 hipError_t launch_oceanic_phys(const Dims &, const Params &, const Fields &, const int *, hipStream_t);
 hipError_t launch_tracer_step(const Dims &, const Params &, const Fields &, const TracerArgs &, const int *, hipStream_t);
+bool tracer_pair_ok(const Dims &, const Params &, const TracerArgs &, const TracerArgs &);
+hipError_t launch_tracer_pair(const Dims &, const Params &, const Fields &, const TracerArgs &, const TracerArgs &,
+                              const int *, hipStream_t);
 hipError_t launch_mon_stats(const Dims &, const MonSpecs &, int, double *, int, hipStream_t);
 int cg2d_mwg_geometry(int *, int *, int *);
 hipError_t launch_cg2d_mwg(const Dims &, const Params &, const Fields &, const MwgTables &, int, SolveRecord *, int *,
@@ -1192,6 +1195,13 @@ static TracerArgs tracer_args(mgcm_model *m, bool salt) {
 
 // TEMP_INTEGRATE / SALT_INTEGRATE on stream `st` (the theta/salt ping-pong swap is host-side)
 static int tracers_on(mgcm_model *m, hipStream_t st) {
+  const TracerArgs aT = tracer_args(m, false), aS = tracer_args(m, true);
+  if (tracer_pair_ok(m->d, m->p, aT, aS)) {   // both tracers in one pair of launches
+    TIMED(K_TEMP, launch_tracer_pair(m->d, m->p, m->f, aT, aS, m->d_ctr, st));
+    std::swap(m->f.theta, m->f.thetaNext);
+    std::swap(m->f.salt, m->f.saltNext);
+    return 0;
+  }
   if (m->p.tempStepping) {
     TIMED(K_TEMP, launch_tracer_step(m->d, m->p, m->f, tracer_args(m, false), m->d_ctr, st));
     std::swap(m->f.theta, m->f.thetaNext);   // CYCLE_TRACER: the new theta is the other buffer
@@ -1354,20 +1364,38 @@ static int one_step(mgcm_model *m) {
   const bool tracers = m->p.tempStepping || m->p.saltStepping;
   const bool fork = !stagger && m->overlap && !m->timing && m->p.momStepping && tracers;
   bool endFused = false;   // CALC_R_STAR + blocking exchanges in one launch (below)
+  // Under the linear free surface nothing between DYNAMICS and the correction step touches
+  // what THERMODYNAMICS reads or writes (no r* rewrite of hFac; SOLVE_FOR_PRESSURE and CG2D
+  // read gU, gV, hFac and eta, write the solver's vectors and etaN), so the tracers may run
+  // beside the pressure solve too and join before MOMENTUM_CORRECTION_STEP rewrites u, v, w.
+  // thermoAt (MGCM_THERMO_AT): 0 fork after DO_OCEANIC_PHYS (beside DYNAMICS), 1 fork after
+  // DYNAMICS (beside SOLVE_FOR_PRESSURE: the multi-workgroup CG2D leaves most CUs idle while
+  // DYNAMICS, alone, has the chip); 1 only under the linear free surface
+  const int thermoAtEnv = getenv("MGCM_THERMO_AT") ? atoi(getenv("MGCM_THERMO_AT")) : 0;
+  const bool lateJoin = fork && m->p.nonlinFreeSurf <= 0;
+  const bool thermoLate = lateJoin && thermoAtEnv == 1;
   if (stagger) {
     TIMED(K_PHYS, launch_oceanic_phys(m->d, m->p, m->f, m->d_ctr, m->stream));
   } else if (fork) {
     TIMED(K_PHYS, launch_oceanic_phys(m->d, m->p, m->f, m->d_ctr, m->stream));
-    HIPCHK(hipEventRecord(m->evFork, m->stream));
-    HIPCHK(hipStreamWaitEvent(m->stream2, m->evFork, 0));
-    if (tracers_on(m, m->stream2)) return -1;
-    HIPCHK(hipEventRecord(m->evJoin, m->stream2));
+    if (!thermoLate) {
+      HIPCHK(hipEventRecord(m->evFork, m->stream));
+      HIPCHK(hipStreamWaitEvent(m->stream2, m->evFork, 0));
+      if (tracers_on(m, m->stream2)) return -1;
+      HIPCHK(hipEventRecord(m->evJoin, m->stream2));
+    }
   } else if (mgcm_thermodynamics(m)) {
     return -1;
   }
   if (m->p.momStepping) {
     if (mgcm_dynamics(m)) return -1;
-    if (fork) HIPCHK(hipStreamWaitEvent(m->stream, m->evJoin, 0));
+    if (thermoLate) {
+      HIPCHK(hipEventRecord(m->evFork, m->stream));
+      HIPCHK(hipStreamWaitEvent(m->stream2, m->evFork, 0));
+      if (tracers_on(m, m->stream2)) return -1;
+      HIPCHK(hipEventRecord(m->evJoin, m->stream2));
+    }
+    if (fork && !lateJoin) HIPCHK(hipStreamWaitEvent(m->stream, m->evJoin, 0));
     // forward_step.F:829-877: UPDATE_R_STAR(.TRUE.) + UPDATE_CG2D
     // (launch fusions, common.h MGCM_STEP_FUSE: CALC_DIV_GHAT in the r* column pass;
     // EXCH(cg2d_x) + etaN in the single-workgroup CG2D's epilogue -- off by default: one CU
@@ -1378,6 +1406,7 @@ static int one_step(mgcm_model *m) {
     const bool etaFused = mg_fuse_on(MG_FUSE_ETA) && cg2d_fuses_eta(m);
     TIMED(K_CG2D, launch_cg2d(m, m->p.cg2dMaxIters, m->p.cg2dUseMinResSol - 1, etaFused));
     if (!etaFused) TIMED(K_ETA, launch_exch_eta(m->d, m->p, m->f, m->d_srcOf, false, 0, m->stream));
+    if (lateJoin) HIPCHK(hipStreamWaitEvent(m->stream, m->evJoin, 0));
     TIMED(K_CONT, launch_corr_cont(m->d, m->p, m->f, 0, m->stream));
     // forward_step.F:965-977: CALC_R_STAR(etaH(n+1)); the next step's RESET_NLFS_VARS +
     // UPDATE_R_STAR(.FALSE.) restore the hFac in place, so they are not repeated here.

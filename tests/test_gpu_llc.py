@@ -4,7 +4,8 @@ multi-workgroup CG2D), through the C-ABI.
 
 Bars:
   * LLC-30 (13 tiles of 30 x 30, 10 levels, OL = 4): 8 steps bit-identical to the oracle
-    summing CG2D in the device's order; cg2d_iters identical to the reference-order oracle;
+    summing CG2D in the device's order, with the flat and the k-march tracer kernels;
+    cg2d_iters identical to the reference-order oracle;
   * LLC-90 as benched (13 tiles of 90 x 90, 50 levels): the initial state round-trips; the
     first step's monitored values (dynstat, CG2D residuals and iterations) are bit-identical
     to the device-order oracle's at full size, and its iteration count equals the
@@ -17,7 +18,18 @@ import pytest
 pytestmark = pytest.mark.gpu
 
 
-def test_llc30_8_steps_bitexact_vs_device_order_oracle():
+@pytest.mark.parametrize("march", [None, "1:2", "1:10", "1:3:single"])
+def test_llc30_8_steps_bitexact_vs_device_order_oracle(march, monkeypatch):
+    """march = "on:KC[:single]": the tracer right-hand side as the k-march (the LLC-90
+    default) with KC levels per workgroup -- 5 chunks, 1, 4 uneven -- for both tracers in one
+    launch pair (k_tracer2_march + k_tracer2_impl) or one tracer at a time (k_tracer_march),
+    instead of the flat kernel."""
+    if march:
+        on, kc = march.split(":")[:2]
+        monkeypatch.setenv("MGCM_TRACER_MARCH", on)
+        monkeypatch.setenv("MGCM_TR_KC", kc)
+        if march.endswith("single"):
+            monkeypatch.setenv("MGCM_TRACER_PAIR", "0")
     from mitgcm_amd import configs
     from mitgcm_amd.model import dynstat
     from oracle.harness import oracle_from_config
@@ -80,3 +92,26 @@ def test_llc90_full_size_steps():
     for n in ("uVel", "vVel", "theta", "etaN"):
         assert np.isfinite(m.get(n)).all(), n
     m.close()
+
+
+@pytest.mark.parametrize("thermo_at", ["0", "1"])
+def test_llc30_thermodynamics_overlap_bit_identical(thermo_at, monkeypatch):
+    """THERMODYNAMICS on the second stream (forced on) -- under the linear free surface forked
+    after DO_OCEANIC_PHYS (thermo_at 0) or after DYNAMICS (1), joined before the correction
+    step -- against one stream (forced off): 8 graph-replayed steps bit-identical."""
+    from mitgcm_amd import configs
+    cfg = lambda: configs.llc_synthetic(n=30, Nr=10)
+    out = {}
+    monkeypatch.setenv("MGCM_THERMO_AT", thermo_at)
+    for mode in ("on", "off"):
+        monkeypatch.delenv("MGCM_NO_OVERLAP", raising=False)
+        monkeypatch.delenv("MGCM_OVERLAP", raising=False)
+        monkeypatch.setenv("MGCM_OVERLAP" if mode == "on" else "MGCM_NO_OVERLAP", "1")
+        m = configs.make_model(cfg)
+        m.forward_step(8)
+        m.sync()
+        out[mode] = {n: m.get(n) for n in ("uVel", "vVel", "wVel", "theta", "salt", "etaN")}
+        out[mode]["iters"] = [int(v) for v in m.solve_history(8)[0]]
+        m.close()
+    for n in out["on"]:
+        assert np.array_equal(out["on"][n], out["off"][n]), n
