@@ -340,6 +340,7 @@ struct MwgTables {
   int pinned;             // 1: only blockIdx.x % 8 == 0 work (all parts on one XCD)
   int sys;                // 1: the hand-off block is shared across processes (system scope)
   int partsPerTile;       // parts of tile t: t*partsPerTile .. (t+1)*partsPerTile - 1
+  int exclusive;          // 1: every part claims its CU's whole LDS (no co-resident workgroups)
   // hand-off state, one block zeroed before each launch (hsBytes from ctr): granules of
   // {tag = phase + 1 (32 bits), half of an f64 (32 bits)}, two per value
   unsigned *ctr;          // [1] timeout word

@@ -1725,13 +1725,12 @@ hipError_t launch_mom_step(const Dims &d, const Params &p, const Fields &f, cons
     // that the two extra staged levels per chunk stay a small overhead
     static const int kcEnv = getenv("MGCM_VI_KC") ? atoi(getenv("MGCM_VI_KC")) : 0;
     static const char *viEnv = getenv("MGCM_VI_KERNEL");   // march | level | tiled (sweeps)
-    // the k-march for deep grids (Nr >= 30 with >= 256 workgroups per level chunk): two
-    // chunks of Nr/2 levels.  Measured on LLC-90: alone it is ~10 % slower than
-    // the per-level kernel, but its ~900 workgroups at 3 waves/SIMD leave room for the
-    // concurrent THERMODYNAMICS stream and the graph-replayed step is 3-4 % faster (2.31-2.34
-    // vs 2.40 ms).  MGCM_VI_KERNEL=level|march|tiled and MGCM_VI_KC override (sweeps).
+    // the k-march for deep grids (Nr >= 30 with >= 256 workgroups per level chunk), in five
+    // chunks of levels: 527 us alone on LLC-90 against 634 with two chunks and ~640 for the
+    // per-level kernel (profiles/r03/ab/).  MGCM_VI_KERNEL=level|march|tiled and MGCM_VI_KC
+    // override (sweeps).
     const int nbt = nbx * nby * d.nT;
-    int KCm = (d.Nr + 1) / 2;
+    int KCm = (d.Nr + 4) / 5;
     if (kcEnv > 0) KCm = kcEnv > d.Nr ? d.Nr : kcEnv;
     const bool march = viEnv ? !strcmp(viEnv, "march") : (d.Nr >= 30 && nbt >= 256);
     if (march) {

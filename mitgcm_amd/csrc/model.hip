@@ -666,6 +666,7 @@ static int build_mwg(mgcm_model *m) {
   T.G = G; T.IMAX = IMAX; T.SZ = SZ;
   T.pinned = (G <= 32 && !getenv("MGCM_CG2D_SPREAD")) ? 1 : 0;
   T.sys = 0;
+  T.exclusive = 0;
   T.partsPerTile = (d.t0 == 0 && d.nT == d.nTiles) ? nPartsTile : 0;   // part ranges: whole-domain tables only
   // hand-off block: 64 B of words (launch epoch, timeout word), the partial granules, the
   // export granules; zeroed once here -- granule tags carry the launch epoch, so a launch
@@ -1369,32 +1370,33 @@ static int one_step(mgcm_model *m) {
   // read gU, gV, hFac and eta, write the solver's vectors and etaN), so the tracers may run
   // beside the pressure solve too and join before MOMENTUM_CORRECTION_STEP rewrites u, v, w.
   // thermoAt (MGCM_THERMO_AT): 0 fork after DO_OCEANIC_PHYS (beside DYNAMICS), 1 fork after
-  // DYNAMICS (beside SOLVE_FOR_PRESSURE: the multi-workgroup CG2D leaves most CUs idle while
-  // DYNAMICS, alone, has the chip); 1 only under the linear free surface
-  const int thermoAtEnv = getenv("MGCM_THERMO_AT") ? atoi(getenv("MGCM_THERMO_AT")) : 0;
+  // DYNAMICS (beside SOLVE_FOR_PRESSURE: the pressure solve leaves most CUs idle while
+  // DYNAMICS, alone, has the chip), 2 fork after CALC_DIV_GHAT (beside CG2D alone); 1 and 2
+  // only under the linear free surface.  LLC-90 (profiles/r03/thermo_at/): 1.98 ms at 0,
+  // 1.86 at 1, 1.88 at 2 -- 1 is the default where it applies
+  const int thermoAtEnv = getenv("MGCM_THERMO_AT") ? atoi(getenv("MGCM_THERMO_AT")) : 1;
   const bool lateJoin = fork && m->p.nonlinFreeSurf <= 0;
-  const bool thermoLate = lateJoin && thermoAtEnv == 1;
+  const bool thermoLate = lateJoin && thermoAtEnv >= 1;
+  auto fork_thermo = [&]() -> int {
+    HIPCHK(hipEventRecord(m->evFork, m->stream));
+    HIPCHK(hipStreamWaitEvent(m->stream2, m->evFork, 0));
+    if (tracers_on(m, m->stream2)) return -1;
+    HIPCHK(hipEventRecord(m->evJoin, m->stream2));
+    return 0;
+  };
+  // the multi-workgroup CG2D keeps its CUs to itself while the tracers run beside it
+  m->mwg.exclusive = thermoLate ? 1 : 0;
   if (stagger) {
     TIMED(K_PHYS, launch_oceanic_phys(m->d, m->p, m->f, m->d_ctr, m->stream));
   } else if (fork) {
     TIMED(K_PHYS, launch_oceanic_phys(m->d, m->p, m->f, m->d_ctr, m->stream));
-    if (!thermoLate) {
-      HIPCHK(hipEventRecord(m->evFork, m->stream));
-      HIPCHK(hipStreamWaitEvent(m->stream2, m->evFork, 0));
-      if (tracers_on(m, m->stream2)) return -1;
-      HIPCHK(hipEventRecord(m->evJoin, m->stream2));
-    }
+    if (!thermoLate && fork_thermo()) return -1;
   } else if (mgcm_thermodynamics(m)) {
     return -1;
   }
   if (m->p.momStepping) {
     if (mgcm_dynamics(m)) return -1;
-    if (thermoLate) {
-      HIPCHK(hipEventRecord(m->evFork, m->stream));
-      HIPCHK(hipStreamWaitEvent(m->stream2, m->evFork, 0));
-      if (tracers_on(m, m->stream2)) return -1;
-      HIPCHK(hipEventRecord(m->evJoin, m->stream2));
-    }
+    if (thermoLate && thermoAtEnv == 1 && fork_thermo()) return -1;
     if (fork && !lateJoin) HIPCHK(hipStreamWaitEvent(m->stream, m->evJoin, 0));
     // forward_step.F:829-877: UPDATE_R_STAR(.TRUE.) + UPDATE_CG2D
     // (launch fusions, common.h MGCM_STEP_FUSE: CALC_DIV_GHAT in the r* column pass;
@@ -1403,6 +1405,7 @@ static int one_step(mgcm_model *m) {
     const bool sfpFused = mg_fuse_on(MG_FUSE_SFP) && m->p.nonlinFreeSurf > 0 && m->d.nT == m->d.nTiles;
     if (m->p.nonlinFreeSurf > 0) TIMED(K_RSTAR, update_r_star_cg2d(m, sfpFused));
     if (!sfpFused) TIMED(K_RHS, launch_sfp_rhs(m->d, m->p, m->f, m->stream));
+    if (thermoLate && thermoAtEnv == 2 && fork_thermo()) return -1;
     const bool etaFused = mg_fuse_on(MG_FUSE_ETA) && cg2d_fuses_eta(m);
     TIMED(K_CG2D, launch_cg2d(m, m->p.cg2dMaxIters, m->p.cg2dUseMinResSol - 1, etaFused));
     if (!etaFused) TIMED(K_ETA, launch_exch_eta(m->d, m->p, m->f, m->d_srcOf, false, 0, m->stream));

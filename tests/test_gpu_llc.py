@@ -94,11 +94,12 @@ def test_llc90_full_size_steps():
     m.close()
 
 
-@pytest.mark.parametrize("thermo_at", ["0", "1"])
+@pytest.mark.parametrize("thermo_at", ["0", "1", "2"])
 def test_llc30_thermodynamics_overlap_bit_identical(thermo_at, monkeypatch):
     """THERMODYNAMICS on the second stream (forced on) -- under the linear free surface forked
-    after DO_OCEANIC_PHYS (thermo_at 0) or after DYNAMICS (1), joined before the correction
-    step -- against one stream (forced off): 8 graph-replayed steps bit-identical."""
+    after DO_OCEANIC_PHYS (thermo_at 0), after DYNAMICS (1) or after CALC_DIV_GHAT (2, beside
+    the multi-workgroup CG2D on CUs it keeps to itself), joined before the correction step --
+    against one stream (forced off): 8 graph-replayed steps bit-identical."""
     from mitgcm_amd import configs
     cfg = lambda: configs.llc_synthetic(n=30, Nr=10)
     out = {}
