@@ -16,6 +16,7 @@
 
 #include "common.h"
 #include <cstring>
+#include <cstdio>
 
 namespace mgcm {
 
@@ -223,15 +224,15 @@ __device__ __forceinline__ double vi_hfacz(const A &a, const Dims &d, int ii, in
 }
 // h0FacZ (mom_fluxform.F:290-307 / mom_vecinv.F): rest-state h0FacW/S under the non-linear
 // free surface with no-slip walls, else hFacZ
-template <class A>
-__device__ __forceinline__ double vi_h0facz(const A &a, const Dims &d, const Params &p, int ii, int jj, int k) {
+template <class A, class P>
+__device__ __forceinline__ double vi_h0facz(const A &a, const Dims &d, const P &p, int ii, int jj, int k) {
   if (!(p.momViscosity && p.no_slip_sides && p.nonlinFreeSurf > 0)) return vi_hfacz(a, d, ii, jj, k);
   if (ii < 2 - d.OLx || jj < 2 - d.OLy) return 0.0;
   return fmin(fmin(a.h0FacW(ii, jj, k), a.h0FacW(ii, jj - 1, k)), fmin(a.h0FacS(ii, jj, k), a.h0FacS(ii - 1, jj, k)));
 }
 // MOM_CALC_KE (mom_calc_ke.F:66-150), computed on 1-OL..sN+OL-1
-template <class A>
-__device__ __forceinline__ double vi_KE(const A &a, const Dims &d, const Params &p, const Fields &f, int ii, int jj, int k, int t) {
+template <class A, class P>
+__device__ __forceinline__ double vi_KE(const A &a, const Dims &d, const P &p, const Fields &f, int ii, int jj, int k, int t) {
   const int OLx = d.OLx, OLy = d.OLy, sNx = d.sNx, sNy = d.sNy;
   (void)OLx; (void)OLy; (void)sNx; (void)sNy;
 #define U(ii, jj) a.uVel(ii, jj, k)
@@ -264,8 +265,8 @@ __device__ __forceinline__ double vi_KE(const A &a, const Dims &d, const Params 
 }
   // MOM_CALC_RELVORT3 (mom_calc_relvort3.F:72-233) on 2-OL..sN+OL, then 0 where hFacZ = 0
   // (mom_vecinv.F:395-403); 0 outside the computed range
-  template <class A>
-__device__ __forceinline__ double vi_vort(const A &a, const Dims &d, const Params &p, const Fields &f, int ii, int jj, int k, int t) {
+  template <class A, class P>
+__device__ __forceinline__ double vi_vort(const A &a, const Dims &d, const P &p, const Fields &f, int ii, int jj, int k, int t) {
   const int OLx = d.OLx, OLy = d.OLy, sNx = d.sNx, sNy = d.sNy;
   (void)OLx; (void)OLy; (void)sNx; (void)sNy;
 #define U(ii, jj) a.uVel(ii, jj, k)
@@ -306,8 +307,8 @@ __device__ __forceinline__ double vi_vort(const A &a, const Dims &d, const Param
 #undef G3
 }
   // MOM_CALC_HDIV(hDivScheme = 2) (mom_calc_hdiv.F:76-89) on 1-OL..sN+OL-1
-  template <class A>
-__device__ __forceinline__ double vi_hdiv(const A &a, const Dims &d, const Params &p, const Fields &f, int ii, int jj, int k, int t) {
+  template <class A, class P>
+__device__ __forceinline__ double vi_hdiv(const A &a, const Dims &d, const P &p, const Fields &f, int ii, int jj, int k, int t) {
   const int OLx = d.OLx, OLy = d.OLy, sNx = d.sNx, sNy = d.sNy;
   (void)OLx; (void)OLy; (void)sNx; (void)sNy;
 #define U(ii, jj) a.uVel(ii, jj, k)
@@ -347,8 +348,8 @@ struct VIGlobal {
 // MOM_CALC_RELVORT3's cube-corner circulations.  Subset (mgcm_init checks it): no
 // useAbsVorticity / high-order / upwind vorticity, constant harmonic viscosity, explicit
 // vertical viscosity, no biharmonic, no 3-D Coriolis / NH metric.  deepFac = rhoFac = 1.
-template <class A>
-__device__ __forceinline__ void vecinv_tend(const A &a, const Dims &d, const Params &p, const Fields &f, int i, int j, int k, int t, double &gU,
+template <class A, class P>
+__device__ __forceinline__ void vecinv_tend(const A &a, const Dims &d, const P &p, const Fields &f, int i, int j, int k, int t, double &gU,
                             double &gV, double &guDiss, double &gvDiss) {
   const int Nr = d.Nr, OLx = d.OLx, OLy = d.OLy, sNx = d.sNx, sNy = d.sNy;
 #define U(ii, jj) a.uVel(ii, jj, k)
@@ -1580,6 +1581,340 @@ __global__ void __launch_bounds__(VT_NT) k_mom_vi_march(Dims d, Params p, Fields
   }
 }
 
+// ---------------------------------------------------------------------------------------
+// The k-march specialised at compile time (k_mom_vi_m2): the block shape BX x BY and
+// MOM_VECINV's option switches (VIP<C>, C = vi_opt_code of the run's Params) are template
+// constants, so the LDS neighbour offsets fold into ds_read immediates, untaken scheme
+// branches vanish and the run-time parameters left are the dozen coefficients VIP carries
+// (the generic k_mom_vi_march keeps the whole Params live in scalar registers and spills
+// them to VGPR lanes inside the march: ~300 v_readlane per level body).  vecinv_tend and the
+// vi_* intermediates are the same templates reading p.x, so the expression trees -- and the
+// bits -- are those of every other MOM_VECINV kernel.  Used when the run's option code and
+// block shape have an instantiation (vi_m2_kernel), else the generic march.
+template <unsigned C>
+struct VIP {
+  static constexpr int selectVortScheme = C & 3, selectCoriScheme = (C >> 2) & 3, selectKEscheme = (C >> 4) & 3;
+  static constexpr int momViscosity = (C >> 6) & 1, no_slip_sides = (C >> 7) & 1, no_slip_bottom = (C >> 8) & 1;
+  static constexpr int implicitViscosity = (C >> 9) & 1, useCoriolis = (C >> 10) & 1, momAdvection = (C >> 11) & 1;
+  static constexpr int upwindShear = (C >> 12) & 1, cubeCorners = (C >> 13) & 1, momForcing = (C >> 14) & 1;
+  static constexpr int momDissip_In_AB = (C >> 15) & 1, momForcingOutAB = (C >> 16) & 1;
+  static constexpr int nonlinFreeSurf = (C >> 17) & 7, select_rStar = (C >> 20) & 3;
+  double rkSign, sideDragFactor, vfFacMom, viscA4Z, viscAhD, viscAhZ, viscAr;
+  double abEps, deltaTMom, foFacMom, gravity, pfFacMom, rhoConst;
+  int nIter0;
+};
+// the option code of a run: every switch the VI kernels branch on, clamped to the values
+// those branches distinguish (nonlinFreeSurf: > 0, > 1, >= 4; select_rStar: > 0, >= 2;
+// momForcingOutAB: == 1)
+static unsigned vi_opt_code(const Params &p) {
+  auto cl = [](int v, int hi) { return (unsigned)(v < 0 ? 0 : v > hi ? hi : v); };
+  auto b = [](int v) { return v != 0 ? 1u : 0u; };
+  return cl(p.selectVortScheme, 3) | cl(p.selectCoriScheme, 3) << 2 | cl(p.selectKEscheme, 3) << 4 |
+         b(p.momViscosity) << 6 | b(p.no_slip_sides) << 7 | b(p.no_slip_bottom) << 8 | b(p.implicitViscosity) << 9 |
+         b(p.useCoriolis) << 10 | b(p.momAdvection) << 11 | b(p.upwindShear) << 12 | b(p.cubeCorners) << 13 |
+         b(p.momForcing) << 14 | b(p.momDissip_In_AB) << 15 | (p.momForcingOutAB == 1 ? 1u : 0u) << 16 |
+         cl(p.nonlinFreeSurf, 7) << 17 | cl(p.select_rStar, 3) << 20;
+}
+template <unsigned C>
+static VIP<C> vi_params(const Params &p) {
+  VIP<C> v;
+  v.rkSign = p.rkSign; v.sideDragFactor = p.sideDragFactor; v.vfFacMom = p.vfFacMom; v.viscA4Z = p.viscA4Z;
+  v.viscAhD = p.viscAhD; v.viscAhZ = p.viscAhZ; v.viscAr = p.viscAr; v.abEps = p.abEps; v.deltaTMom = p.deltaTMom;
+  v.foFacMom = p.foFacMom; v.gravity = p.gravity; v.pfFacMom = p.pfFacMom; v.rhoConst = p.rhoConst;
+  v.nIter0 = p.nIter0;
+  return v;
+}
+
+// Accessor of k_mom_vi_m2.  OWN: the output point (i,j), whose column's k-1 / k+1 values of
+// u, v, hFacW, hFacS sit in registers and whose own 2-D metrics in VIMarchRegs; !OWN: the
+// ring-point intermediates, which read level k only (no own-point selects at all).
+template <int BX, int BY, class P, bool OWN>
+struct VIM2 {
+  static constexpr int EW = BX + 2, IW = BX + 1;
+  const Dims &d; const P &p; const Fields &f; int k, t, i0, j0, i, j;
+  const double *sU, *sV, *sHW, *sHS, *sHC, *sW, *s2;
+  const double *sKE, *sVort, *sHfz, *sH0fz, *sHDiv;
+  const VIMarchRegs &c;
+  double uM, uP, vM, vP, hwM, hwP, hsM, hsP;
+  __device__ __forceinline__ int e(int ii, int jj) const { return (jj - j0 + 1) * EW + (ii - i0 + 1); }
+  __device__ __forceinline__ long g(int ii, int jj, int kk) const { return MG_I3(d, ii, jj, kk, t); }
+  __device__ __forceinline__ double lvl(const double *sl, double m_, double p_, int ii, int jj, int kk) const {
+    if constexpr (OWN) {
+      if (ii == i && jj == j && kk != k) return kk < k ? m_ : p_;
+    }
+    return sl[e(ii, jj)];
+  }
+  __device__ __forceinline__ double uVel(int ii, int jj, int kk) const { return lvl(sU, uM, uP, ii, jj, kk); }
+  __device__ __forceinline__ double vVel(int ii, int jj, int kk) const { return lvl(sV, vM, vP, ii, jj, kk); }
+  __device__ __forceinline__ double hFacW(int ii, int jj, int kk) const { return lvl(sHW, hwM, hwP, ii, jj, kk); }
+  __device__ __forceinline__ double hFacS(int ii, int jj, int kk) const { return lvl(sHS, hsM, hsP, ii, jj, kk); }
+  __device__ __forceinline__ double hFacC(int ii, int jj, int kk) const { return sHC[(kk & 1) * (EW * (BY + 2)) + e(ii, jj)]; }
+  __device__ __forceinline__ double wVel(int ii, int jj, int kk) const { return sW[(kk & 1) * (EW * (BY + 2)) + e(ii, jj)]; }
+  __device__ __forceinline__ double maskW(int ii, int jj, int kk) const { return hFacW(ii, jj, kk) != 0.0 ? 1.0 : 0.0; }
+  __device__ __forceinline__ double maskS(int ii, int jj, int kk) const { return hFacS(ii, jj, kk) != 0.0 ? 1.0 : 0.0; }
+  __device__ __forceinline__ double maskC(int ii, int jj, int kk) const { return hFacC(ii, jj, kk) != 0.0 ? 1.0 : 0.0; }
+  __device__ __forceinline__ double recip_hFacW(int ii, int jj, int kk) const {
+    const double h = hFacW(ii, jj, kk); return h != 0.0 ? 1.0 / h : 0.0; }
+  __device__ __forceinline__ double recip_hFacS(int ii, int jj, int kk) const {
+    const double h = hFacS(ii, jj, kk); return h != 0.0 ? 1.0 / h : 0.0; }
+  __device__ __forceinline__ double recip_hFacC(int ii, int jj, int kk) const {
+    const double h = hFacC(ii, jj, kk); return h != 0.0 ? 1.0 / h : 0.0; }
+  __device__ __forceinline__ double h0FacW(int ii, int jj, int kk) const { return AR3(h0FacW, g(ii, jj, kk)); }
+  __device__ __forceinline__ double h0FacS(int ii, int jj, int kk) const { return AR3(h0FacS, g(ii, jj, kk)); }
+  template <int F> __device__ __forceinline__ double g2(int ii, int jj) const {
+    constexpr int EN = EW * (BY + 2);
+    if constexpr (F == F2_dxC) return s2[0 * EN + e(ii, jj)];
+    else if constexpr (F == F2_dyC) return s2[1 * EN + e(ii, jj)];
+    else if constexpr (F == F2_recip_rAz) return s2[2 * EN + e(ii, jj)];
+    else if constexpr (F == F2_dxG) return s2[3 * EN + e(ii, jj)];
+    else if constexpr (F == F2_dyG) return s2[4 * EN + e(ii, jj)];
+    else if constexpr (F == F2_recip_rA) return s2[5 * EN + e(ii, jj)];
+    else {
+      if constexpr (OWN) {
+        const int di = ii - i, dj = jj - j;
+#define VM_R(name, DI, DJ, reg) if constexpr (F == F2_##name) { if (di == (DI) && dj == (DJ)) return c.reg; }
+        VM_R(recip_dxC, 0, 0, recip_dxC) VM_R(recip_dyC, 0, 0, recip_dyC) VM_R(recip_dxG, 0, 0, recip_dxG)
+        VM_R(recip_dyG, 0, 0, recip_dyG) VM_R(rAw, 0, 0, rAw) VM_R(rAs, 0, 0, rAs) VM_R(recip_rAw, 0, 0, recip_rAw)
+        VM_R(recip_rAs, 0, 0, recip_rAs) VM_R(dxV, 0, 0, dxV) VM_R(dxV, 0, 1, dxVn) VM_R(recip_dyU, 0, 0, recip_dyU)
+        VM_R(recip_dyU, 0, 1, recip_dyUn) VM_R(dyU, 0, 0, dyU) VM_R(dyU, 1, 0, dyUe) VM_R(recip_dxV, 0, 0, recip_dxV)
+        VM_R(recip_dxV, 1, 0, recip_dxVe) VM_R(fCoriG, 0, 0, fCoriG) VM_R(fCoriG, 0, 1, fCoriGn)
+        VM_R(fCoriG, 1, 0, fCoriGe) VM_R(rA, 0, 0, rA) VM_R(rA, -1, 0, rAw_w) VM_R(rA, 0, -1, rA_s)
+#undef VM_R
+      }
+      return f.a2[(long)F * d.N2all + MG_I2(d, ii, jj, t)];   // anything else: where it lies
+    }
+  }
+  __device__ __forceinline__ int iv(int ii, int jj) const { return (jj - j0) * IW + (ii - i0); }
+  __device__ __forceinline__ int id(int ii, int jj) const { return (jj - j0 + 1) * IW + (ii - i0 + 1); }
+  __device__ __forceinline__ double hfz(int ii, int jj) const { return sHfz[iv(ii, jj)]; }
+  __device__ __forceinline__ double h0fz(int ii, int jj) const { return sH0fz[iv(ii, jj)]; }
+  __device__ __forceinline__ double vort(int ii, int jj) const { return sVort[iv(ii, jj)]; }
+  __device__ __forceinline__ double KE(int ii, int jj) const { return sKE[id(ii, jj)]; }
+  __device__ __forceinline__ double hDiv(int ii, int jj) const { return sHDiv[id(ii, jj)]; }
+};
+
+// The k-march of k_mom_vi_march<PF, CREG> (same phases, same staging), on VIM2 / VIP<C>.
+template <int BX, int BY, unsigned C, bool PF, bool CREG>
+__global__ void __launch_bounds__(VT_NT) k_mom_vi_m2(Dims d, VIP<C> p, Fields f, const int *iterPtr, int nbx, int nby,
+                                                      int KC, int nkc) {
+  using P = VIP<C>;
+  constexpr int EW = BX + 2, EN = (BX + 2) * (BY + 2), IW = BX + 1, IN = (BX + 1) * (BY + 1);
+  constexpr int NR = (EN + VT_NT - 1) / VT_NT;   // extent elements per thread
+  static_assert(BX * BY <= VT_NT && EN <= 2 * VT_NT, "block shape");
+  __shared__ double sU[EN], sV[EN], sHW[EN], sHS[EN], sHC[2 * EN], sW[2 * EN];
+  __shared__ double s2[VM_S2 * EN];
+  __shared__ double sKE[IN], sVort[IN], sHfz[IN], sH0fz[IN], sHDiv[IN];
+  const int nb = nbx * nby, lb = mg_xcd_block();
+  const int t = d.t0 + lb / (nb * nkc), bxy = lb % nb, kb = 1 + ((lb / nb) % nkc) * KC;
+  const int Nr = d.Nr, ke = kb + KC - 1 < Nr ? kb + KC - 1 : Nr;
+  const int i0 = (bxy % nbx) * BX, j0 = (bxy / nbx) * BY;
+  const int tid = threadIdx.x;
+  const int i = i0 + tid % BX, j = j0 + tid / BX;
+  const bool act = tid < BX * BY && i <= d.sNx + 1 && j <= d.sNy + 1;
+  const int ic = act ? i : 1, jc = act ? j : 1;
+  const long q2 = MG_I2(d, ic, jc, t);
+  long eq[NR];
+  bool ein[NR];
+#pragma unroll
+  for (int r = 0; r < NR; r++) {
+    const int ee = tid + r * VT_NT;
+    const int ii = i0 - 1 + ee % EW, jj = j0 - 1 + ee / EW;
+    ein[r] = ee < EN && ii <= d.sNx + d.OLx && jj <= d.sNy + d.OLy;
+    eq[r] = MG_I2(d, ein[r] ? ii : 1, ein[r] ? jj : 1, t);
+  }
+  {
+    const int ids[VM_S2] = {F2_dxC, F2_dyC, F2_recip_rAz, F2_dxG, F2_dyG, F2_recip_rA};
+#pragma unroll
+    for (int n = 0; n < VM_S2; n++)
+#pragma unroll
+      for (int r = 0; r < NR; r++) {
+        const int ee = tid + r * VT_NT;
+        const double v = f.a2[(long)ids[n] * d.N2all + eq[r]];
+        if (ee < EN) s2[n * EN + ee] = ein[r] ? v : 0.0;
+      }
+  }
+  auto load_c = [&](VIMarchRegs &c, const long q2) {
+    const long qn = q2 + d.nx, qe = q2 + 1, qw = q2 - 1, qs = q2 - d.nx;
+    c.recip_dxC = AR2(recip_dxC, q2); c.recip_dyC = AR2(recip_dyC, q2);
+    c.recip_dxG = AR2(recip_dxG, q2); c.recip_dyG = AR2(recip_dyG, q2);
+    c.rAw = AR2(rAw, q2); c.rAs = AR2(rAs, q2); c.recip_rAw = AR2(recip_rAw, q2); c.recip_rAs = AR2(recip_rAs, q2);
+    c.dxV = AR2(dxV, q2); c.dxVn = AR2(dxV, qn); c.recip_dyU = AR2(recip_dyU, q2); c.recip_dyUn = AR2(recip_dyU, qn);
+    c.dyU = AR2(dyU, q2); c.dyUe = AR2(dyU, qe); c.recip_dxV = AR2(recip_dxV, q2); c.recip_dxVe = AR2(recip_dxV, qe);
+    c.fCoriG = AR2(fCoriG, q2); c.fCoriGn = AR2(fCoriG, qn); c.fCoriGe = AR2(fCoriG, qe);
+    c.rA = AR2(rA, q2); c.rAw_w = AR2(rA, qw); c.rA_s = AR2(rA, qs);
+  };
+  VIMarchRegs c0;
+  if constexpr (CREG) load_c(c0, q2);
+  const long t3 = (long)t * (d.n3 - d.n2);
+  const unsigned lvB = (unsigned)(d.n2 * 8);
+  unsigned eb[NR];
+#pragma unroll
+  for (int r = 0; r < NR; r++) eb[r] = (unsigned)((eq[r] + t3) * 8);
+  const unsigned ob = (unsigned)((q2 + t3) * 8);
+  const char *bU = (const char *)(f.a3 + (long)F3_uVel * d.N3all), *bV = (const char *)(f.a3 + (long)F3_vVel * d.N3all);
+  const char *bHW = (const char *)(f.a3 + (long)F3_hFacW * d.N3all), *bHS = (const char *)(f.a3 + (long)F3_hFacS * d.N3all);
+  const char *bHC = (const char *)(f.a3 + (long)F3_hFacC * d.N3all), *bW = (const char *)(f.a3 + (long)F3_wVel * d.N3all);
+  auto ld = [](const char *b, unsigned off) { return *(const double *)(b + off); };
+  double nU[NR], nV[NR], nHW[NR], nHS[NR], nHC[NR], nW[NR], oU, oV, oHW, oHS;
+  auto fetch = [&](int kk) {
+    const unsigned lo = (unsigned)(kk - 1) * lvB;
+#pragma unroll
+    for (int r = 0; r < NR; r++) {
+      const unsigned o = eb[r] + lo;
+      nU[r] = ld(bU, o); nV[r] = ld(bV, o); nHW[r] = ld(bHW, o); nHS[r] = ld(bHS, o); nHC[r] = ld(bHC, o);
+    }
+    const unsigned o = ob + lo;
+    oU = ld(bU, o); oV = ld(bV, o); oHW = ld(bHW, o); oHS = ld(bHS, o);
+  };
+  auto fetchW = [&](int kk) {
+    const unsigned lo = (unsigned)(kk - 1) * lvB;
+#pragma unroll
+    for (int r = 0; r < NR; r++) nW[r] = ld(bW, eb[r] + lo);
+  };
+  auto stash = [&](int kk) {
+#pragma unroll
+    for (int r = 0; r < NR; r++) {
+      const int ee = tid + r * VT_NT;
+      if (ee < EN) {
+        sU[ee] = ein[r] ? nU[r] : 0.0; sV[ee] = ein[r] ? nV[r] : 0.0;
+        sHW[ee] = ein[r] ? nHW[r] : 0.0; sHS[ee] = ein[r] ? nHS[r] : 0.0;
+        sHC[(kk & 1) * EN + ee] = ein[r] ? nHC[r] : 0.0;
+      }
+    }
+  };
+  auto stashW = [&](int kk) {
+#pragma unroll
+    for (int r = 0; r < NR; r++) {
+      const int ee = tid + r * VT_NT;
+      if (ee < EN) sW[(kk & 1) * EN + ee] = (ein[r] && kk <= Nr) ? nW[r] : 0.0;
+    }
+  };
+  double uM = 0.0, vM = 0.0, hwM = 0.0, hsM = 0.0;
+  if (kb > 1) {
+    fetch(kb - 1);
+    uM = oU; vM = oV; hwM = oHW; hsM = oHS;
+#pragma unroll
+    for (int r = 0; r < NR; r++) {
+      const int ee = tid + r * VT_NT;
+      if (ee < EN) sHC[((kb - 1) & 1) * EN + ee] = ein[r] ? nHC[r] : 0.0;
+    }
+  }
+  fetchW(kb);
+  stashW(kb);
+  fetchW(kb + 1 <= Nr ? kb + 1 : Nr);
+  stashW(kb + 1);
+  fetch(kb);
+  stash(kb);
+  const int myIter = *iterPtr;
+  const double abFac = (myIter == p.nIter0 && p.nIter0 == 0) ? 0.0 : 0.5 + p.abEps;   // adams_bashforth2.F:61-65
+  const double mass2rUnit = 1.0 / p.rhoConst;
+  constexpr bool rstar = P::nonlinFreeSurf > 0 && P::select_rStar > 0;
+  __syncthreads();
+  for (int k = kb; k <= ke; k++) {
+    int iL = i, jL = j;
+    long q2L = q2;
+    asm volatile("" : "+v"(iL), "+v"(jL), "+v"(q2L));
+    [&](const int i, const int j, const long q2) {
+    // the arena bases and strides re-materialised per level too: every field address derived
+    // from them is then formed where it is used instead of hoisted out of the march and held
+    // in scalar registers (which spill to VGPR lanes)
+    Fields fl = f;
+    Dims dl = d;
+    asm volatile("" : "+s"(fl.a2), "+s"(fl.a3), "+s"(dl.N2all), "+s"(dl.N3all));
+    const Fields &f = fl;
+    const Dims &d = dl;
+    VIMarchRegs c1;
+    if constexpr (!CREG) load_c(c1, q2);
+    const VIMarchRegs &c = CREG ? c0 : c1;
+    const int kn = k + 1 <= Nr ? k + 1 : Nr, kw = k + 2 <= Nr ? k + 2 : Nr;
+    if constexpr (PF) {
+      fetch(kn);
+      fetchW(kw);
+    } else {
+      const unsigned o = ob + (unsigned)(kn - 1) * lvB;
+      oU = ld(bU, o); oV = ld(bV, o); oHW = ld(bHW, o); oHS = ld(bHS, o);
+    }
+    VIM2<BX, BY, P, true> a{d, p, f, k, t, i0, j0, i, j, sU, sV, sHW, sHS, sHC, sW, s2, sKE, sVort, sHfz, sH0fz, sHDiv, c,
+                            uM, k < Nr ? oU : 0.0, vM, k < Nr ? oV : 0.0, hwM, k < Nr ? oHW : 0.0, hsM, k < Nr ? oHS : 0.0};
+    VIM2<BX, BY, P, false> ai{d, p, f, k, t, i0, j0, 0, 0, sU, sV, sHW, sHS, sHC, sW, s2, sKE, sVort, sHfz, sH0fz, sHDiv, c,
+                              0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
+    for (int q = tid; q < IN; q += VT_NT) {
+      const int ii = i0 + q % IW, jj = j0 + q / IW;          // vort / hFacZ grid: i0..i0+BX
+      const bool ok = ii <= d.sNx + d.OLx && jj <= d.sNy + d.OLy;
+      sHfz[q] = ok ? vi_hfacz(ai, d, ii, jj, k) : 0.0;
+      sH0fz[q] = ok ? vi_h0facz(ai, d, p, ii, jj, k) : 0.0;
+      sVort[q] = ok ? vi_vort(ai, d, p, f, ii, jj, k, t) : 0.0;
+      sKE[q] = vi_KE(ai, d, p, f, ii - 1, jj - 1, k, t);     // KE / hDiv grid: i0-1..i0+BX-1
+      sHDiv[q] = vi_hdiv(ai, d, p, f, ii - 1, jj - 1, k, t);
+    }
+    __syncthreads();
+    if (act) {
+      auto q3of = [&](long qq2, int kk) { return qq2 + (long)(kk - 1) * d.n2 + t3; };
+      const long q3 = q3of(q2, k);
+      const double recip_drF = f.recip_drF[k - 1];
+      double gU = 0.0, gV = 0.0, guDiss = 0.0, gvDiss = 0.0, dPhiHydX = 0.0, dPhiHydY = 0.0;
+      {  // CALC_GRAD_PHI_HYD (calc_grad_phi_hyd.F:152-214), as k_mom_step
+        constexpr bool rsc = rstar && P::select_rStar >= 2 && P::nonlinFreeSurf >= 4;
+        auto varLoc = [&](long qq2) {
+          if constexpr (rsc) return AR3(phiHydC, q3of(qq2, k)) * AR2(rStarFacC, qq2) + 0.0;
+          else return AR3(phiHydC, q3of(qq2, k)) + 0.0;
+        };
+        const double vl = varLoc(q2);
+        if (i >= 1) dPhiHydX = c.recip_dxC * (vl - varLoc(q2 - 1));
+        if (j >= 1) dPhiHydY = c.recip_dyC * (vl - varLoc(q2 - d.nx));
+        if constexpr (rstar && P::select_rStar >= 2) {
+          const double factorP = p.gravity * (1.0 / p.rhoConst) * 0.5, rCk = f.rC[k - 1];
+          auto vl2 = [&](long qq2) { return AR2(etaH, qq2) * (1.0 + rCk * AR2(recip_Rcol, qq2)); };
+          const double e0 = vl2(q2), a0 = AR3(alphaRho, q3);
+          if (i >= 1) dPhiHydX = dPhiHydX + factorP * (AR3(alphaRho, q3 - 1) + a0) * (e0 - vl2(q2 - 1)) * c.recip_dxC;
+          if (j >= 1) dPhiHydY = dPhiHydY + factorP * (AR3(alphaRho, q3 - d.nx) + a0) * (e0 - vl2(q2 - d.nx)) * c.recip_dyC;
+        }
+      }
+      vecinv_tend(a, d, p, f, i, j, k, t, gU, gV, guDiss, gvDiss);
+      double guExt = 0.0, gvExt = 0.0;
+      if (P::momForcing && k == 1) {
+        if (j >= 0 && j <= d.sNy + 1 && i >= 1 && i <= d.sNx + 1)
+          guExt = guExt + p.foFacMom * (AR2(fu, q2) * mass2rUnit) * recip_drF * a.recip_hFacW(i, j, k);
+        if (j >= 1 && j <= d.sNy + 1 && i >= 0 && i <= d.sNx + 1)
+          gvExt = gvExt + p.foFacMom * (AR2(fv, q2) * mass2rUnit) * recip_drF * a.recip_hFacS(i, j, k);
+      }
+      gU = gU - p.pfFacMom * dPhiHydX;
+      gV = gV - p.pfFacMom * dPhiHydY;
+      if (P::momViscosity && P::momDissip_In_AB) { gU = gU + guDiss; gV = gV + gvDiss; }
+      if (P::momForcing && P::momForcingOutAB != 1) { gU = gU + guExt; gV = gV + gvExt; }
+      {  // ADAMS_BASHFORTH2 (adams_bashforth2.F:81-88)
+        const double gUo = AR3(guNm1, q3), gVo = AR3(gvNm1, q3);
+        double ab = abFac * (gU - gUo);
+        AR3(guNm1, q3) = gU;
+        gU = gU + ab;
+        ab = abFac * (gV - gVo);
+        AR3(gvNm1, q3) = gV;
+        gV = gV + ab;
+      }
+      double gUtmp = gU, gVtmp = gV;
+      if (P::momForcing && P::momForcingOutAB == 1) { gUtmp = gUtmp + guExt; gVtmp = gVtmp + gvExt; }
+      if (P::momViscosity && !P::momDissip_In_AB) { gUtmp = gUtmp + guDiss; gVtmp = gVtmp + gvDiss; }
+      if constexpr (rstar && P::nonlinFreeSurf > 1) {
+        gUtmp = gUtmp / AR2(rStarExpW, q2);
+        gVtmp = gVtmp / AR2(rStarExpS, q2);
+      }
+      AR3(gU, q3) = a.uVel(i, j, k) + p.deltaTMom * (gUtmp + 0.0) * a.maskW(i, j, k);
+      AR3(gV, q3) = a.vVel(i, j, k) + p.deltaTMom * (gVtmp + 0.0) * a.maskS(i, j, k);
+    }
+    }(iL, jL, q2L);
+    if (k == ke) break;
+    if (act) { const int eo = (j - j0 + 1) * EW + (i - i0 + 1); uM = sU[eo]; vM = sV[eo]; hwM = sHW[eo]; hsM = sHS[eo]; }
+    if constexpr (!PF) {
+      fetch(k + 1 <= Nr ? k + 1 : Nr);
+      fetchW(k + 2 <= Nr ? k + 2 : Nr);
+    }
+    __syncthreads();
+    stash(k + 1);
+    stashW(k + 2);
+    __syncthreads();
+  }
+}
+
 // The halo ring outside the DYNAMICS range (i or j outside 0..sN+1): no tendency, but
 // ADAMS_BASHFORTH2 runs over the whole slab (gU = abFac*(0 - guNm1), guNm1 = 0), as
 // k_mom_step does there.
@@ -1616,6 +1951,45 @@ __global__ void __launch_bounds__(256) k_mom_halo_ab(Dims d, Params p, Fields f,
   gV = gV + ab;
   AR3(gU, q3) = gU;
   AR3(gV, q3) = gV;
+}
+
+// k_mom_vi_m2's instantiations: (BX, BY, option code) of the workloads that run the k-march
+// -- the LLC-90 synthetic (BASELINE config 5: 92-wide DYNAMICS range -> 31 x 8 blocks) and
+// its LLC-30 shrink (32 x 8) with the same namelist.  Anything else runs k_mom_vi_march.
+constexpr unsigned vi_code(int vs, int cs, int ks, int visc, int nss, int nsb, int impl, int cor, int adv, int upw,
+                           int cube, int forc, int dissAB, int outAB1, int nlfs, int rstar) {
+  return (unsigned)vs | (unsigned)cs << 2 | (unsigned)ks << 4 | (unsigned)visc << 6 | (unsigned)nss << 7 |
+         (unsigned)nsb << 8 | (unsigned)impl << 9 | (unsigned)cor << 10 | (unsigned)adv << 11 | (unsigned)upw << 12 |
+         (unsigned)cube << 13 | (unsigned)forc << 14 | (unsigned)dissAB << 15 | (unsigned)outAB1 << 16 |
+         (unsigned)nlfs << 17 | (unsigned)rstar << 20;
+}
+constexpr unsigned VI_CODE_LLC = vi_code(1, 0, 0, 1, 1, 1, 0, 1, 1, 0, 1, 1, 1, 0, 0, 0);
+template <int BX, int BY, unsigned C>
+static void vi_m2_go(const Dims &d, const Params &p, const Fields &f, const int *iterPtr, int nbx, int nby, int KC,
+                     int nkc, hipStream_t s, int var) {
+  const dim3 g((unsigned)(nbx * nby * d.nT * nkc)), b(VT_NT);
+  const VIP<C> vp = vi_params<C>(p);
+  if (var == 1) hipLaunchKernelGGL((k_mom_vi_m2<BX, BY, C, true, true>), g, b, 0, s, d, vp, f, iterPtr, nbx, nby, KC, nkc);
+  else if (var == 2) hipLaunchKernelGGL((k_mom_vi_m2<BX, BY, C, true, false>), g, b, 0, s, d, vp, f, iterPtr, nbx, nby, KC, nkc);
+  else if (var == 3) hipLaunchKernelGGL((k_mom_vi_m2<BX, BY, C, false, true>), g, b, 0, s, d, vp, f, iterPtr, nbx, nby, KC, nkc);
+  else hipLaunchKernelGGL((k_mom_vi_m2<BX, BY, C, false, false>), g, b, 0, s, d, vp, f, iterPtr, nbx, nby, KC, nkc);
+}
+// MGCM_VI_M2=0 keeps the generic march (A/B); MGCM_VI_MARCH_VAR picks the PF/CREG variant as
+// for k_mom_vi_march
+static bool vi_m2_launch(const Dims &d, const Params &p, const Fields &f, const int *iterPtr, int BX, int BY, int nbx,
+                         int nby, int KC, int nkc, hipStream_t s) {
+  // read per launch (tests switch them per model)
+  const bool on = !getenv("MGCM_VI_M2") || atoi(getenv("MGCM_VI_M2")) != 0;
+  // default: the output point's metrics held in registers across the march (CREG), level
+  // k+1 fetched after level k (LLC-90: 487 us against 534 with neither, 527 for the generic
+  // march; profiles/r03/vi_m2/)
+  const int var = getenv("MGCM_VI_MARCH_VAR") ? atoi(getenv("MGCM_VI_MARCH_VAR")) : 3;
+  if (!on) return false;
+  const unsigned code = vi_opt_code(p);
+  if (getenv("MGCM_VI_M2_DEBUG")) fprintf(stderr, "vi_m2: BX %d BY %d code %#x (LLC %#x)\n", BX, BY, code, VI_CODE_LLC);
+  if (code == VI_CODE_LLC && BX == 31 && BY == 8) { vi_m2_go<31, 8, VI_CODE_LLC>(d, p, f, iterPtr, nbx, nby, KC, nkc, s, var); return true; }
+  if (code == VI_CODE_LLC && BX == 32 && BY == 8) { vi_m2_go<32, 8, VI_CODE_LLC>(d, p, f, iterPtr, nbx, nby, KC, nkc, s, var); return true; }
+  return false;
 }
 
 // block shape of k_mom_vi_tiled: BX along i (a whole output row when it is short), BY rows
@@ -1723,8 +2097,8 @@ hipError_t launch_mom_step(const Dims &d, const Params &p, const Fields &f, cons
     const int nbx = (d.sNx + 2 + BX - 1) / BX, nby = (d.sNy + 2 + BY - 1) / BY;
     // levels per workgroup: enough workgroups to fill the chip several times, few enough
     // that the two extra staged levels per chunk stay a small overhead
-    static const int kcEnv = getenv("MGCM_VI_KC") ? atoi(getenv("MGCM_VI_KC")) : 0;
-    static const char *viEnv = getenv("MGCM_VI_KERNEL");   // march | level | tiled (sweeps)
+    const int kcEnv = getenv("MGCM_VI_KC") ? atoi(getenv("MGCM_VI_KC")) : 0;
+    const char *viEnv = getenv("MGCM_VI_KERNEL");   // march | level | tiled (sweeps; read per launch)
     // the k-march for deep grids (Nr >= 30 with >= 256 workgroups per level chunk), in five
     // chunks of levels: 527 us alone on LLC-90 against 634 with two chunks and ~640 for the
     // per-level kernel (profiles/r03/ab/).  MGCM_VI_KERNEL=level|march|tiled and MGCM_VI_KC
@@ -1735,11 +2109,13 @@ hipError_t launch_mom_step(const Dims &d, const Params &p, const Fields &f, cons
     const bool march = viEnv ? !strcmp(viEnv, "march") : (d.Nr >= 30 && nbt >= 256);
     if (march) {
       const int nkc = (d.Nr + KCm - 1) / KCm;
-      static const int var = getenv("MGCM_VI_MARCH_VAR") ? atoi(getenv("MGCM_VI_MARCH_VAR")) : 0;
-      auto kern = var == 1 ? k_mom_vi_march<true, true> : var == 2 ? k_mom_vi_march<true, false>
-                : var == 3 ? k_mom_vi_march<false, true> : k_mom_vi_march<false, false>;
-      hipLaunchKernelGGL(kern, dim3((unsigned)(nbt * nkc)), dim3(VT_NT), 0, s, d, p, f, iterPtr, BX, BY, nbx, nby, KCm,
-                         nkc);
+      if (!vi_m2_launch(d, p, f, iterPtr, BX, BY, nbx, nby, KCm, nkc, s)) {
+        const int var = getenv("MGCM_VI_MARCH_VAR") ? atoi(getenv("MGCM_VI_MARCH_VAR")) : 0;
+        auto kern = var == 1 ? k_mom_vi_march<true, true> : var == 2 ? k_mom_vi_march<true, false>
+                  : var == 3 ? k_mom_vi_march<false, true> : k_mom_vi_march<false, false>;
+        hipLaunchKernelGGL(kern, dim3((unsigned)(nbt * nkc)), dim3(VT_NT), 0, s, d, p, f, iterPtr, BX, BY, nbx, nby, KCm,
+                           nkc);
+      }
     } else if (kcEnv <= 0 || (viEnv && !strcmp(viEnv, "level"))) {   // one level per workgroup
       hipLaunchKernelGGL(k_mom_vi_level, dim3((unsigned)(nbx * nby * d.nT * d.Nr)), dim3(VT_NT), 0, s, d, p, f, iterPtr, BX,
                          BY, nbx, nby);
