@@ -18,7 +18,7 @@ for arm in $ARMS; do
     eval "PC=\$P$pn"
     ok=1; for c in $PC; do grep -qx "$c" $OUT/sq_avail.txt || { echo "counter $c not listed"; ok=0; }; done
     [ $ok = 1 ] || continue
-    MGCM_VI_M2=$m2 MGCM_VI_MARCH_VAR=$var timeout -s KILL 180 rocprofv3 --pmc $PC -d $OUT/p${pn}_$kind$var -o run --output-format csv -- python3 bench.py --config llc90_synthetic --steps 6 --warmup 1 --no-cpu-baseline > $OUT/b${pn}_$kind$var.json 2> $OUT/p${pn}_$kind$var.err || { echo "pmc $arm pass $pn failed"; tail -5 $OUT/p${pn}_$kind$var.err; exit 1; }
+    MGCM_VI_M2=$m2 MGCM_VI_M2_VAR=$var MGCM_VI_MARCH_VAR=$var timeout -s KILL 180 rocprofv3 --pmc $PC -d $OUT/p${pn}_$kind$var -o run --output-format csv -- python3 bench.py --config llc90_synthetic --steps 6 --warmup 1 --no-cpu-baseline > $OUT/b${pn}_$kind$var.json 2> $OUT/p${pn}_$kind$var.err || { echo "pmc $arm pass $pn failed"; tail -5 $OUT/p${pn}_$kind$var.err; exit 1; }
     python tools/sq_summary.py $OUT/p${pn}_$kind$var > $OUT/sq${pn}_$kind$var.txt
     echo "== $arm pass $pn"; grep -E "kernel|vi_m|vi_march" $OUT/sq${pn}_$kind$var.txt
   done
