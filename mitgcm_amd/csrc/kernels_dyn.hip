@@ -1966,236 +1966,6 @@ __global__ void __launch_bounds__(VT_NT, LBW) k_mom_vi_m2(Dims d, VIP<C> p, Fiel
 #endif
 }
 
-// MOM_VECINV k-march with the two velocity components on separate threads (k_mom_vi_uv): a
-// 512-thread workgroup per BX x BY block, threads 0..255 compute the U points of the block and
-// 256..511 its V points, over the level fields and intermediates staged once for both (one
-// extent element and at most one intermediate point per thread: no second, mostly idle
-// pass).  Each thread carries only its component's column (velocity and hFac at k-1, k+1)
-// and metrics, so its arithmetic -- vecinv_tend with the other component's results dead and
-// compiled out -- needs about half the registers of k_mom_vi_m2's thread.  The staging, the
-// phases and the expression trees are k_mom_vi_m2's (EARLY and CREG forms): same bits.
-// PF: level k+1 fetched into registers at the start of level k and stashed into the other
-// slot of double-buffered level arrays (u, v, hFacW, hFacS: 2 slots; hFacC, w: 3) right
-// after the level's output, so its HBM latency hides behind both phases and a level costs
-// two barriers instead of three.
-template <int BX, int BY, unsigned C, int LBW, bool PF = false>
-__global__ void __launch_bounds__(2 * VT_NT, LBW) k_mom_vi_uv(Dims d, VIP<C> p, Fields f, const int *iterPtr, int nbx,
-                                                              int nby, int KC, int nkc) {
-  using P = VIP<C>;
-  constexpr int NT = 2 * VT_NT;
-  constexpr int EW = BX + 2, EN = (BX + 2) * (BY + 2), IW = BX + 1, IN = (BX + 1) * (BY + 1);
-  static_assert(BX * BY <= VT_NT && EN <= NT && IN <= NT, "block shape");
-  constexpr int LS = PF ? 2 : 1, HR = PF ? 3 : 2;   // level-array slots, hFacC / w ring slots
-  __shared__ double sU[LS * EN], sV[LS * EN], sHW[LS * EN], sHS[LS * EN], sHC[HR * EN], sW[HR * EN];
-  __shared__ double s2[VM_S2 * EN];
-  __shared__ double sKE[IN], sVort[IN], sHfz[IN], sH0fz[IN], sHDiv[IN];
-  const int nb = nbx * nby, lb = mg_xcd_block();
-  const int t = d.t0 + lb / (nb * nkc), bxy = lb % nb, kb = 1 + ((lb / nb) % nkc) * KC;
-  const int Nr = d.Nr, ke = kb + KC - 1 < Nr ? kb + KC - 1 : Nr;
-  const int i0 = (bxy % nbx) * BX, j0 = (bxy / nbx) * BY;
-  const int tid = threadIdx.x, comp = tid / VT_NT, pt = tid % VT_NT;   // comp: wave-uniform
-  const int i = i0 + pt % BX, j = j0 + pt / BX;
-  const bool act = pt < BX * BY && i <= d.sNx + 1 && j <= d.sNy + 1;
-  const int ic = act ? i : 1, jc = act ? j : 1;
-  const long q2 = MG_I2(d, ic, jc, t);
-  // this thread's extent element
-  const int eI = i0 - 1 + tid % EW, eJ = j0 - 1 + tid / EW;
-  const bool ein = tid < EN && eI <= d.sNx + d.OLx && eJ <= d.sNy + d.OLy;
-  const long eq = MG_I2(d, ein ? eI : 1, ein ? eJ : 1, t);
-  {
-    const int ids[VM_S2] = {F2_dxC, F2_dyC, F2_recip_rAz, F2_dxG, F2_dyG, F2_recip_rA};
-#pragma unroll
-    for (int n = 0; n < VM_S2; n++) {
-      const double v = f.a2[(long)ids[n] * d.N2all + eq];
-      if (tid < EN) s2[n * EN + tid] = ein ? v : 0.0;
-    }
-  }
-  // the output point's 2-D metrics: the twelve its component reads (VIMarchRegs fields),
-  // held across the march in the same registers for both components
-  double cr[12];
-  {
-    const long qn = q2 + d.nx, qe = q2 + 1, qw = q2 - 1, qs = q2 - d.nx;
-    if (comp == 0) {
-      cr[0] = AR2(recip_dxC, q2); cr[1] = AR2(recip_dyG, q2); cr[2] = AR2(rAw, q2); cr[3] = AR2(recip_rAw, q2);
-      cr[4] = AR2(dxV, q2); cr[5] = AR2(dxV, qn); cr[6] = AR2(recip_dyU, q2); cr[7] = AR2(recip_dyU, qn);
-      cr[8] = AR2(fCoriG, q2); cr[9] = AR2(fCoriG, qn); cr[10] = AR2(rA, q2); cr[11] = AR2(rA, qw);
-    } else {
-      cr[0] = AR2(recip_dyC, q2); cr[1] = AR2(recip_dxG, q2); cr[2] = AR2(rAs, q2); cr[3] = AR2(recip_rAs, q2);
-      cr[4] = AR2(dyU, q2); cr[5] = AR2(dyU, qe); cr[6] = AR2(recip_dxV, q2); cr[7] = AR2(recip_dxV, qe);
-      cr[8] = AR2(fCoriG, q2); cr[9] = AR2(fCoriG, qe); cr[10] = AR2(rA, q2); cr[11] = AR2(rA, qs);
-    }
-  }
-  const long t3 = (long)t * (d.n3 - d.n2);
-  const unsigned lvB = (unsigned)(d.n2 * 8);
-  const unsigned eb = (unsigned)((eq + t3) * 8), ob = (unsigned)((q2 + t3) * 8);
-  const char *bU = (const char *)(f.a3 + (long)F3_uVel * d.N3all), *bV = (const char *)(f.a3 + (long)F3_vVel * d.N3all);
-  const char *bHW = (const char *)(f.a3 + (long)F3_hFacW * d.N3all), *bHS = (const char *)(f.a3 + (long)F3_hFacS * d.N3all);
-  const char *bHC = (const char *)(f.a3 + (long)F3_hFacC * d.N3all), *bW = (const char *)(f.a3 + (long)F3_wVel * d.N3all);
-  // this component's velocity / hFac fields (own-column values)
-  const char *bX = comp ? bV : bU, *bH = comp ? bHS : bHW;
-  auto ld = [](const char *b, unsigned off) { return *(const double *)(b + off); };
-  double nU, nV, nHW, nHS, nHC, nW;
-  auto fetch = [&](int kk) {
-    const unsigned o = eb + (unsigned)(kk - 1) * lvB;
-    nU = ld(bU, o); nV = ld(bV, o); nHW = ld(bHW, o); nHS = ld(bHS, o); nHC = ld(bHC, o);
-  };
-  auto fetchW = [&](int kk) { nW = ld(bW, eb + (unsigned)(kk - 1) * lvB); };
-  auto lsl = [&](int kk) { return PF ? (kk & 1) * EN : 0; };   // level kk's slot of sU, sV, sHW, sHS
-  auto stash = [&](int kk) {
-    if (tid < EN) {
-      const int o = lsl(kk) + tid;
-      sU[o] = ein ? nU : 0.0; sV[o] = ein ? nV : 0.0; sHW[o] = ein ? nHW : 0.0; sHS[o] = ein ? nHS : 0.0;
-      sHC[(kk % HR) * EN + tid] = ein ? nHC : 0.0;
-    }
-  };
-  auto stashW = [&](int kk) {
-    if (tid < EN) sW[(kk % HR) * EN + tid] = (ein && kk <= Nr) ? nW : 0.0;
-  };
-  // own column at k-1 of this component: velocity and hFac
-  double xM = 0.0, hM = 0.0;
-  if (kb > 1) {
-    fetch(kb - 1);
-    const unsigned o = ob + (unsigned)(kb - 2) * lvB;
-    xM = ld(bX, o); hM = ld(bH, o);
-    if (tid < EN) sHC[((kb - 1) % HR) * EN + tid] = ein ? nHC : 0.0;
-  }
-  fetchW(kb);
-  stashW(kb);
-  fetchW(kb + 1 <= Nr ? kb + 1 : Nr);
-  stashW(kb + 1);
-  fetch(kb);
-  stash(kb);
-  const int myIter = *iterPtr;
-  const double abFac = (myIter == p.nIter0 && p.nIter0 == 0) ? 0.0 : 0.5 + p.abEps;   // adams_bashforth2.F:61-65
-  const double mass2rUnit = 1.0 / p.rhoConst;
-  constexpr bool rstar = P::nonlinFreeSurf > 0 && P::select_rStar > 0;
-  constexpr bool rsc = rstar && P::select_rStar >= 2 && P::nonlinFreeSurf >= 4;
-  __syncthreads();
-  for (int k = kb; k <= ke; k++) {
-    int iL = i, jL = j;
-    long q2L = q2;
-    asm volatile("" : "+v"(iL), "+v"(jL), "+v"(q2L));
-    [&](const int i, const int j, const long q2) {
-      Fields fl = f;
-      Dims dl = d;
-      asm volatile("" : "+s"(fl.a2), "+s"(fl.a3), "+s"(dl.N2all), "+s"(dl.N3all));
-      const Fields &f = fl;
-      const Dims &d = dl;
-      const int kn = k + 1 <= Nr ? k + 1 : Nr;
-      const long q3 = q2 + (long)(k - 1) * d.n2 + t3;
-      if constexpr (PF) {   // level k+1 (and w at k+2) in flight during both phases
-        if (k < ke) { fetch(kn); fetchW(k + 2 <= Nr ? k + 2 : Nr); }
-      }
-      const double *lU = sU + lsl(k), *lV = sV + lsl(k), *lHW = sHW + lsl(k), *lHS = sHS + lsl(k);
-      // this thread's HBM reads of level k, issued before the intermediates' barrier: its
-      // column at k+1, the AB2 history and the pressure-gradient phi_hyd pair
-      const unsigned on = ob + (unsigned)(kn - 1) * lvB;
-      const double xP = ld(bX, on), hP = ld(bH, on);
-      const double gOld = comp ? AR3(gvNm1, q3) : AR3(guNm1, q3);
-      double ePhi0 = 0.0, ePhi1 = 0.0;
-      if constexpr (!rsc) { ePhi0 = AR3(phiHydC, q3); ePhi1 = AR3(phiHydC, comp ? q3 - d.nx : q3 - 1); }
-      const VIMarchRegs cNone{};   // the ring-point accessor reads no own-point metric
-      VIM2<BX, BY, P, false, HR> ai{d, p, f, k, t, i0, j0, 0, 0, lU, lV, lHW, lHS, sHC, sW, s2, sKE, sVort, sHfz, sH0fz,
-                                    sHDiv, cNone, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
-      if (tid < IN) {
-        const int q = tid;
-        const int ii = i0 + q % IW, jj = j0 + q / IW;          // vort / hFacZ grid: i0..i0+BX
-        const bool ok = ii <= d.sNx + d.OLx && jj <= d.sNy + d.OLy;
-        sHfz[q] = ok ? vi_hfacz(ai, d, ii, jj, k) : 0.0;
-        sH0fz[q] = ok ? vi_h0facz(ai, d, p, ii, jj, k) : 0.0;
-        sVort[q] = ok ? vi_vort(ai, d, p, f, ii, jj, k, t) : 0.0;
-        sKE[q] = vi_KE(ai, d, p, f, ii - 1, jj - 1, k, t);     // KE / hDiv grid: i0-1..i0+BX-1
-        sHDiv[q] = vi_hdiv(ai, d, p, f, ii - 1, jj - 1, k, t);
-      }
-      __syncthreads();
-      if (act) {
-      const double recip_drF = f.recip_drF[k - 1];
-      auto body = [&](auto compTag) {
-        constexpr int CP = decltype(compTag)::value;
-        const double kp = k < Nr ? xP : 0.0, hkp = k < Nr ? hP : 0.0;
-        // this component's metrics; the other component's fields are never read on this path
-        // (a read would take a zero and break the bit-exact tests)
-        VIMarchRegs c{};
-        if constexpr (CP == 0) {
-          c.recip_dxC = cr[0]; c.recip_dyG = cr[1]; c.rAw = cr[2]; c.recip_rAw = cr[3]; c.dxV = cr[4]; c.dxVn = cr[5];
-          c.recip_dyU = cr[6]; c.recip_dyUn = cr[7]; c.fCoriG = cr[8]; c.fCoriGn = cr[9]; c.rA = cr[10]; c.rAw_w = cr[11];
-        } else {
-          c.recip_dyC = cr[0]; c.recip_dxG = cr[1]; c.rAs = cr[2]; c.recip_rAs = cr[3]; c.dyU = cr[4]; c.dyUe = cr[5];
-          c.recip_dxV = cr[6]; c.recip_dxVe = cr[7]; c.fCoriG = cr[8]; c.fCoriGe = cr[9]; c.rA = cr[10]; c.rA_s = cr[11];
-        }
-        VIM2<BX, BY, P, true, HR> a{d, p, f, k, t, i0, j0, i, j, lU, lV, lHW, lHS, sHC, sW, s2, sKE, sVort, sHfz, sH0fz, sHDiv, c,
-                                CP == 0 ? xM : 0.0, CP == 0 ? kp : 0.0, CP == 1 ? xM : 0.0, CP == 1 ? kp : 0.0,
-                                CP == 0 ? hM : 0.0, CP == 0 ? hkp : 0.0, CP == 1 ? hM : 0.0, CP == 1 ? hkp : 0.0};
-        double gU = 0.0, gV = 0.0, guDiss = 0.0, gvDiss = 0.0, dPhiHyd = 0.0;
-        {  // CALC_GRAD_PHI_HYD (calc_grad_phi_hyd.F:152-214), as k_mom_step
-          auto varLoc = [&](long qq2) {
-            if constexpr (rsc) return AR3(phiHydC, qq2 + (long)(k - 1) * d.n2 + t3) * AR2(rStarFacC, qq2) + 0.0;
-            else return AR3(phiHydC, qq2 + (long)(k - 1) * d.n2 + t3) + 0.0;
-          };
-          const long qo = CP == 0 ? q2 - 1 : q2 - d.nx;   // the other point of this component's gradient
-          double vl, vo;
-          if constexpr (rsc) { vl = varLoc(q2); vo = varLoc(qo); }
-          else { vl = ePhi0 + 0.0; vo = ePhi1 + 0.0; }
-          if (CP == 0 ? i >= 1 : j >= 1) dPhiHyd = (CP == 0 ? c.recip_dxC : c.recip_dyC) * (vl - vo);
-          if constexpr (rstar && P::select_rStar >= 2) {
-            const double factorP = p.gravity * (1.0 / p.rhoConst) * 0.5, rCk = f.rC[k - 1];
-            auto vl2 = [&](long qq2) { return AR2(etaH, qq2) * (1.0 + rCk * AR2(recip_Rcol, qq2)); };
-            const double e0 = vl2(q2), a0 = AR3(alphaRho, q3);
-            const long qo3 = CP == 0 ? q3 - 1 : q3 - d.nx;
-            if (CP == 0 ? i >= 1 : j >= 1)
-              dPhiHyd = dPhiHyd + factorP * (AR3(alphaRho, qo3) + a0) * (e0 - vl2(qo)) * (CP == 0 ? c.recip_dxC : c.recip_dyC);
-          }
-        }
-        vecinv_tend(a, d, p, f, i, j, k, t, gU, gV, guDiss, gvDiss);
-        double g = CP == 0 ? gU : gV, gDiss = CP == 0 ? guDiss : gvDiss, gExt = 0.0;
-        if (P::momForcing && k == 1) {
-          if (CP == 0) {
-            if (j >= 0 && j <= d.sNy + 1 && i >= 1 && i <= d.sNx + 1)
-              gExt = gExt + p.foFacMom * (AR2(fu, q2) * mass2rUnit) * recip_drF * a.recip_hFacW(i, j, k);
-          } else {
-            if (j >= 1 && j <= d.sNy + 1 && i >= 0 && i <= d.sNx + 1)
-              gExt = gExt + p.foFacMom * (AR2(fv, q2) * mass2rUnit) * recip_drF * a.recip_hFacS(i, j, k);
-          }
-        }
-        g = g - p.pfFacMom * dPhiHyd;
-        if (P::momViscosity && P::momDissip_In_AB) g = g + gDiss;
-        if (P::momForcing && P::momForcingOutAB != 1) g = g + gExt;
-        // ADAMS_BASHFORTH2 (adams_bashforth2.F:81-88)
-        const double ab = abFac * (g - gOld);
-        if (CP == 0) AR3(guNm1, q3) = g; else AR3(gvNm1, q3) = g;
-        g = g + ab;
-        double gtmp = g;
-        if (P::momForcing && P::momForcingOutAB == 1) gtmp = gtmp + gExt;
-        if (P::momViscosity && !P::momDissip_In_AB) gtmp = gtmp + gDiss;
-        if constexpr (rstar && P::nonlinFreeSurf > 1) gtmp = gtmp / (CP == 0 ? AR2(rStarExpW, q2) : AR2(rStarExpS, q2));
-        if (CP == 0) AR3(gU, q3) = a.uVel(i, j, k) + p.deltaTMom * (gtmp + 0.0) * a.maskW(i, j, k);
-        else AR3(gV, q3) = a.vVel(i, j, k) + p.deltaTMom * (gtmp + 0.0) * a.maskS(i, j, k);
-      };
-      if (comp == 0) body(std::integral_constant<int, 0>{});
-      else body(std::integral_constant<int, 1>{});
-      }
-      if (PF && k < ke) {   // level k+1 into the free slots: nobody reads them during level k
-        stash(k + 1);
-        stashW(k + 2);
-      }
-    }(iL, jL, q2L);
-    if (k == ke) break;
-    if (act) {   // the own column moves down: level k becomes k-1
-      const int eo = lsl(k) + (j - j0 + 1) * EW + (i - i0 + 1);
-      xM = comp ? sV[eo] : sU[eo];
-      hM = comp ? sHS[eo] : sHW[eo];
-    }
-    if constexpr (!PF) {
-      fetch(k + 1 <= Nr ? k + 1 : Nr);
-      fetchW(k + 2 <= Nr ? k + 2 : Nr);
-      __syncthreads();
-      stash(k + 1);
-      stashW(k + 2);
-    }
-    __syncthreads();
-  }
-}
-
 // The halo ring outside the DYNAMICS range (i or j outside 0..sN+1): no tendency, but
 // ADAMS_BASHFORTH2 runs over the whole slab (gU = abFac*(0 - guNm1), guNm1 = 0), as
 // k_mom_step does there.
@@ -2266,16 +2036,6 @@ static bool vi_m2_go(const Dims &d, const Params &p, const Fields &f, const int 
     case 11: vi_m2_one<BX, BY, C, 11>(d, vp, f, iterPtr, nbx, nby, KC, nkc, s); return true;
     case 14: vi_m2_one<BX, BY, C, 14>(d, vp, f, iterPtr, nbx, nby, KC, nkc, s); return true;
     case 15: vi_m2_one<BX, BY, C, 15>(d, vp, f, iterPtr, nbx, nby, KC, nkc, s); return true;
-    case 16: hipLaunchKernelGGL((k_mom_vi_uv<BX, BY, C, 1>), dim3((unsigned)(nbx * nby * d.nT * nkc)), dim3(2 * VT_NT), 0, s,
-                                d, vp, f, iterPtr, nbx, nby, KC, nkc); return true;
-    case 17: hipLaunchKernelGGL((k_mom_vi_uv<BX, BY, C, 3>), dim3((unsigned)(nbx * nby * d.nT * nkc)), dim3(2 * VT_NT), 0, s,
-                                d, vp, f, iterPtr, nbx, nby, KC, nkc); return true;
-    case 18: hipLaunchKernelGGL((k_mom_vi_uv<BX, BY, C, 4>), dim3((unsigned)(nbx * nby * d.nT * nkc)), dim3(2 * VT_NT), 0, s,
-                                d, vp, f, iterPtr, nbx, nby, KC, nkc); return true;
-    case 24: hipLaunchKernelGGL((k_mom_vi_uv<BX, BY, C, 1, true>), dim3((unsigned)(nbx * nby * d.nT * nkc)), dim3(2 * VT_NT), 0,
-                                s, d, vp, f, iterPtr, nbx, nby, KC, nkc); return true;
-    case 26: hipLaunchKernelGGL((k_mom_vi_uv<BX, BY, C, 4, true>), dim3((unsigned)(nbx * nby * d.nT * nkc)), dim3(2 * VT_NT), 0,
-                                s, d, vp, f, iterPtr, nbx, nby, KC, nkc); return true;
     default: return false;
   }
 }
@@ -2289,8 +2049,9 @@ static bool vi_m2_launch(const Dims &d, const Params &p, const Fields &f, const 
   // registers across the march (CREG), its own HBM reads of a level issued at the level's
   // start (EARLY), registers capped for 2 waves per SIMD, level k+1 fetched after level k
   // (LLC-90: 456-459 us; CREG alone 487, neither 534, the generic march 527; prefetching
-  // level k+1 into registers 513-740 (1 wave per SIMD or spills); the U/V-split k_mom_vi_uv
-  // 492, with a double-buffered prefetch 501: profiles/r03/vi_m2/)
+  // level k+1 into registers 513-740 (1 wave per SIMD or spills); measured and dropped: a
+  // U/V-split 512-thread form 492, the same with a double-buffered prefetch 501, a two-pass
+  // form (intermediates through HBM, per-point tendencies) 585: profiles/r03/vi_m2/)
   const int var = getenv("MGCM_VI_M2_VAR") ? atoi(getenv("MGCM_VI_M2_VAR")) : 14;
   if (!on) return false;
   const unsigned code = vi_opt_code(p);
