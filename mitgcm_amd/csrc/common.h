@@ -248,12 +248,16 @@ inline size_t mg_colf_lds(int Nr, int nc, int nArr) { return (size_t)nArr * Nr *
   } while (0)
 inline unsigned mg_colf_blocks(long ncols, int nc) { return (unsigned)((ncols + nc - 1) / nc); }
 // Launch fusions of FORWARD_STEP, each switchable for A/B runs: MGCM_STEP_FUSE = bit mask of
-// the enabled ones (default all): MG_FUSE_SFP CALC_DIV_GHAT in the r* column pass,
+// the enabled ones (default SFP | PHI | END): MG_FUSE_SFP CALC_DIV_GHAT in the r* column pass,
 // MG_FUSE_ETA EXCH(cg2d_x) + etaN in the single-workgroup CG2D, MG_FUSE_PHI CALC_PHI_HYD +
-// del2uv in one grid, MG_FUSE_END CALC_R_STAR + the blocking exchanges in one grid.
-enum { MG_FUSE_SFP = 1, MG_FUSE_ETA = 2, MG_FUSE_PHI = 4, MG_FUSE_END = 8 };
+// del2uv in one grid, MG_FUSE_END CALC_R_STAR + the blocking exchanges in one grid,
+// MG_FUSE_PHYS DO_OCEANIC_PHYS + CALC_PHI_HYD in one column pass (bit-identical, but on LLC-90
+// 226-313 us against 75 + 77 for the two launches: the per-point EOS loads lose their
+// plane-wide parallelism inside the column frame; profiles/r03/phys/).
+enum { MG_FUSE_SFP = 1, MG_FUSE_ETA = 2, MG_FUSE_PHI = 4, MG_FUSE_END = 8, MG_FUSE_PHYS = 16 };
 inline bool mg_fuse_on(int bit) {
-  static const int mask = getenv("MGCM_STEP_FUSE") ? atoi(getenv("MGCM_STEP_FUSE")) : MG_FUSE_SFP | MG_FUSE_PHI | MG_FUSE_END;
+  // read per call (tests switch it per model)
+  const int mask = getenv("MGCM_STEP_FUSE") ? atoi(getenv("MGCM_STEP_FUSE")) : MG_FUSE_SFP | MG_FUSE_PHI | MG_FUSE_END;
   return (mask & bit) != 0;
 }
 // Horizontal launch fusion of two independent latency-bound kernels into one grid: on the

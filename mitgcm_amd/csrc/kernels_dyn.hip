@@ -15,6 +15,7 @@
 #include <cstdlib>
 
 #include "common.h"
+#include "phys.h"
 #include <cstring>
 #include <cstdio>
 #include <type_traits>
@@ -107,14 +108,23 @@ __global__ void __launch_bounds__(256) k_del2uv(Dims d, Params p, Fields f) { de
 // their value at every level for k_mom_step.  Columns cover -1..sNx+1 x -1..sNy+1 (the
 // dynamics range 0..sNx+1 plus the west/south neighbours dWtransC is needed at); phi and
 // totPhiHyd are stored on 0..sNx+1 only.
-__device__ __forceinline__ void phi_hyd_body(const Dims &d, const Params &p, const Fields &f, int nc, int lb) {
+// PHYS: DO_OCEANIC_PHYS's per-point work (phys.h) done in the same column pass, whose frame
+// then covers the whole halo range (the range DO_OCEANIC_PHYS fills); the rho each point
+// computes feeds the phi_hyd sums directly and the phi_hyd stores keep to -1..sN+1 / 0..sN+1
+// (k_phys_phi: DO_OCEANIC_PHYS and CALC_PHI_HYD in one launch where nothing between them
+// reads DO_OCEANIC_PHYS's output at a neighbour -- no GM/Redi tensor -- and phi is not
+// already fused with del2uv)
+template <bool PHYS = false>
+__device__ __forceinline__ void phi_hyd_body(const Dims &d, const Params &p, const Fields &f, int nc, int lb,
+                                             const int *iterPtr = nullptr) {
   extern __shared__ __attribute__((aligned(16))) double lds[];
-  MG_COLF_LB(-1, d.sNx + 3, -1, d.sNy + 3, nc, lb)
+  MG_COLF_LB(PHYS ? 1 - d.OLx : -1, PHYS ? d.nx : d.sNx + 3, PHYS ? 1 - d.OLy : -1, PHYS ? d.ny : d.sNy + 3, nc, lb)
   const int Nr = d.Nr, NS = Nr * NC_;
   double *sM = lds, *sP = lds + NS, *sPh = lds + 2 * NS, *sC = lds + 3 * NS, *sU = lds + 4 * NS, *sV = lds + 5 * NS;
   const bool qh = p.quasiHydrostatic && (p.select3dCoriScheme >= 1 || p.useNHMTerms);
   const bool rstar = p.nonlinFreeSurf > 0 && p.select_rStar > 0;
-  const bool ring = i >= 0 && j >= 0;
+  const bool inPhi = !PHYS || (i >= -1 && i <= d.sNx + 1 && j >= -1 && j <= d.sNy + 1);
+  const bool ring = inPhi && i >= 0 && j >= 0;
   const double recip_rhoConst = 1.0 / p.rhoConst;
   const long q2 = MG_I2(d, i, j, t);
   if (valid) MG_COLF_K(k) {
@@ -123,7 +133,9 @@ __device__ __forceinline__ void phi_hyd_body(const Dims &d, const Params &p, con
     if (k == 1) dRlocM = f.rF[0] - f.rC[0];
     const double dRlocP = (k == Nr) ? (f.rC[k - 1] - f.rF[k]) : 0.5 * f.drC[k];
     const long q3 = MG_I3(d, i, j, k, t);
-    double a = f.rhoInSitu[q3];
+    double a;
+    if constexpr (PHYS) a = oceanic_phys_point(d, p, f, iterPtr, i, j, k, t);
+    else a = f.rhoInSitu[q3];
     if (qh) {
       const double scalingFactor = p.rhoConst * p.gravitySign * (1.0 / p.gravity);
       const double u0 = f.uVel[q3], u1 = f.uVel[MG_I3(d, i + 1, j, k, t)];
@@ -133,7 +145,7 @@ __device__ __forceinline__ void phi_hyd_body(const Dims &d, const Params &p, con
       if (p.useNHMTerms) gW = gW + ((u0 * u0 + u1 * u1) + (v0 * v0 + v1 * v1)) * 0.5 * p.recip_rSphere;
       a = a + scalingFactor * gW;
     }
-    if (rstar) f.alphaRho[q3] = a;
+    if (rstar && inPhi) f.alphaRho[q3] = a;
     sM[me] = dRlocM * p.gravity * a * recip_rhoConst;
     sP[me] = dRlocP * p.gravity * a * recip_rhoConst;
     if (rstar) {
@@ -177,7 +189,7 @@ __device__ __forceinline__ void phi_hyd_body(const Dims &d, const Params &p, con
   if (valid) MG_COLF_K(k) {
     const int me = (k - 1) * NC_ + cc;
     const long q3 = MG_I3(d, i, j, k, t);
-    if (rstar) {
+    if (rstar && inPhi) {
       f.dWtC[q3] = sC[me];
       if (ring) { f.dWtU[q3] = sU[me]; f.dWtV[q3] = sV[me]; }
     }
@@ -199,6 +211,9 @@ __device__ __forceinline__ void phi_hyd_body(const Dims &d, const Params &p, con
 }
 __global__ void __launch_bounds__(256) k_phi_hyd(Dims d, Params p, Fields f, int nc) {
   phi_hyd_body(d, p, f, nc, mg_xcd_block());
+}
+__global__ void __launch_bounds__(256) k_phys_phi(Dims d, Params p, Fields f, int nc, const int *iterPtr) {
+  phi_hyd_body<true>(d, p, f, nc, mg_xcd_block(), iterPtr);
 }
 // CALC_PHI_HYD and MOM_U_DEL2U / MOM_V_DEL2V in one grid (independent: each reads only the
 // state DYNAMICS starts from): the first nbPhi logical blocks are k_phi_hyd's, the rest
@@ -2138,6 +2153,24 @@ __global__ void __launch_bounds__(256) k_mom_impl(Dims d, Params p, Fields f, in
 static bool del2_needed(const Params &p) { return p.momViscosity && (p.viscA4D != 0.0 || p.viscA4Z != 0.0); }
 // k_del2uv rides in CALC_PHI_HYD's launch (k_phi_del2) on the small grids
 static bool phi_del2_fused(const Dims &d, const Params &p) { return del2_needed(p) && mg_hfuse(MG_FUSE_PHI, d.nx, d.ny, d.nT, d.Nr); }
+
+// DO_OCEANIC_PHYS + CALC_PHI_HYD in one column pass (k_phys_phi) when that is exact: no
+// GM/Redi tensor between them (it reads rhoInSitu at neighbours) and phi not already sharing
+// a grid with del2uv; MGCM_STEP_FUSE bit MG_FUSE_PHYS.  Returns false when not applicable.
+bool phys_phi_fusable(const Dims &d, const Params &p) {
+  return mg_fuse_on(MG_FUSE_PHYS) && !p.useGMRedi && !phi_del2_fused(d, p);
+}
+hipError_t launch_phys_phi(const Dims &d, const Params &p, const Fields &f, const int *iterPtr, hipStream_t s) {
+  const long ncol = (long)d.nx * d.ny * d.nT;
+  // columns per workgroup (MGCM_PHYS_NC = 16 | 32 | 64; the per-point DO_OCEANIC_PHYS loads
+  // want long runs along i)
+  const int ncEnv = getenv("MGCM_PHYS_NC") ? atoi(getenv("MGCM_PHYS_NC")) : 16;
+  const int nc = (ncEnv == 16 || ncEnv == 32 || ncEnv == 64) ? ncEnv : 16;
+  MG_ALLOW_LDS(k_phys_phi);
+  hipLaunchKernelGGL(k_phys_phi, dim3(mg_colf_blocks(ncol, nc)), dim3(256), mg_colf_lds(d.Nr, nc, 6), s, d, p, f, nc,
+                     iterPtr);
+  return hipGetLastError();
+}
 
 hipError_t launch_phi_hyd(const Dims &d, const Params &p, const Fields &f, hipStream_t s) {
   const long ncol = (long)(d.sNx + 3) * (d.sNy + 3) * d.nT;

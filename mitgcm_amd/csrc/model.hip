@@ -23,6 +23,8 @@
 namespace mgcm {
 hipError_t launch_mom_step(const Dims &, const Params &, const Fields &, const int *, hipStream_t);
 hipError_t launch_phi_hyd(const Dims &, const Params &, const Fields &, hipStream_t);
+bool phys_phi_fusable(const Dims &, const Params &);
+hipError_t launch_phys_phi(const Dims &, const Params &, const Fields &, const int *, hipStream_t);
 hipError_t launch_sfp_rhs(const Dims &, const Params &, const Fields &, hipStream_t);
 hipError_t launch_cg2d_block(const Dims &, const Params &, const Fields &, const unsigned *, const int *, int, int, int,
                              SolveRecord *, int *, hipStream_t);
@@ -1386,16 +1388,24 @@ static int one_step(mgcm_model *m) {
   };
   // the multi-workgroup CG2D keeps its CUs to itself while the tracers run beside it
   m->mwg.exclusive = thermoLate ? 1 : 0;
-  if (stagger) {
-    TIMED(K_PHYS, launch_oceanic_phys(m->d, m->p, m->f, m->d_ctr, m->stream));
-  } else if (fork) {
-    TIMED(K_PHYS, launch_oceanic_phys(m->d, m->p, m->f, m->d_ctr, m->stream));
-    if (!thermoLate && fork_thermo()) return -1;
-  } else if (mgcm_thermodynamics(m)) {
-    return -1;
+  // DO_OCEANIC_PHYS + DYNAMICS' CALC_PHI_HYD in one column pass where exact (phys_phi_fusable:
+  // THERMODYNAMICS, between them in FORWARD_STEP, reads DO_OCEANIC_PHYS's output and writes
+  // nothing CALC_PHI_HYD reads)
+  const bool physPhi = !stagger && m->p.momStepping && phys_phi_fusable(m->d, m->p);
+  auto phys = [&]() -> int {
+    if (physPhi) TIMED(K_PHYS, launch_phys_phi(m->d, m->p, m->f, m->d_ctr, m->stream));
+    else TIMED(K_PHYS, launch_oceanic_phys(m->d, m->p, m->f, m->d_ctr, m->stream));
+    return 0;
+  };
+  if (stagger || fork) {
+    if (phys()) return -1;
+    if (fork && !thermoLate && fork_thermo()) return -1;
+  } else {
+    if (phys() || tracers_on(m, m->stream)) return -1;
   }
   if (m->p.momStepping) {
-    if (mgcm_dynamics(m)) return -1;
+    if (physPhi) TIMED(K_MOM, launch_mom_step(m->d, m->p, m->f, m->d_ctr, m->stream));
+    else if (mgcm_dynamics(m)) return -1;
     if (thermoLate && thermoAtEnv == 1 && fork_thermo()) return -1;
     if (fork && !lateJoin) HIPCHK(hipStreamWaitEvent(m->stream, m->evJoin, 0));
     // forward_step.F:829-877: UPDATE_R_STAR(.TRUE.) + UPDATE_CG2D

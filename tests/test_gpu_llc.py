@@ -18,15 +18,18 @@ import pytest
 pytestmark = pytest.mark.gpu
 
 
-@pytest.mark.parametrize("march", [None, "1:2", "1:10", "1:3:single", "vi:4", "vi:3:generic"])
+@pytest.mark.parametrize("march", [None, "1:2", "1:10", "1:3:single", "vi:4", "vi:3:generic", "fuse:29"])
 def test_llc30_8_steps_bitexact_vs_device_order_oracle(march, monkeypatch):
     """march = "on:KC[:single]": the tracer right-hand side as the k-march (the LLC-90
     default) with KC levels per workgroup -- 5 chunks, 1, 4 uneven -- for both tracers in one
     launch pair (k_tracer2_march + k_tracer2_impl) or one tracer at a time (k_tracer_march),
     instead of the flat kernel.  "vi:KC[:generic|uv]": MOM_VECINV as the k-march (the LLC-90
     default; LLC-30 has too few blocks to pick it by itself) with KC levels per workgroup, in
-    its compile-time specialisation (k_mom_vi_m2<32, 8, LLC options>) or the generic kernel."""
-    if march and march.startswith("vi:"):
+    its compile-time specialisation (k_mom_vi_m2<32, 8, LLC options>) or the generic kernel.
+    "fuse:MASK": the MGCM_STEP_FUSE launch fusions (29: the opt-in k_phys_phi pass)."""
+    if march and march.startswith("fuse:"):   # MGCM_STEP_FUSE mask: 29 adds DO_OCEANIC_PHYS + CALC_PHI_HYD in one pass
+        monkeypatch.setenv("MGCM_STEP_FUSE", march.split(":")[1])
+    elif march and march.startswith("vi:"):
         monkeypatch.setenv("MGCM_VI_KERNEL", "march")
         monkeypatch.setenv("MGCM_VI_KC", march.split(":")[1])
         monkeypatch.setenv("MGCM_VI_M2", "0" if march.endswith("generic") else "1")
