@@ -253,8 +253,12 @@ inline unsigned mg_colf_blocks(long ncols, int nc) { return (unsigned)((ncols + 
 // del2uv in one grid, MG_FUSE_END CALC_R_STAR + the blocking exchanges in one grid,
 // MG_FUSE_PHYS DO_OCEANIC_PHYS + CALC_PHI_HYD in one column pass (bit-identical, but on LLC-90
 // 226-313 us against 75 + 77 for the two launches: the per-point EOS loads lose their
-// plane-wide parallelism inside the column frame; profiles/r03/phys/).
-enum { MG_FUSE_SFP = 1, MG_FUSE_ETA = 2, MG_FUSE_PHI = 4, MG_FUSE_END = 8, MG_FUSE_PHYS = 16 };
+// plane-wide parallelism inside the column frame; profiles/r03/phys/), MG_FUSE_ETAA
+// SOLVE_FOR_PRESSURE's EXCH(cg2d_x) + etaN off the critical path (exactConserv: beside the
+// correction step, which derives the eta it needs from cg2d_x itself; bit-identical, but the
+// third stream's fork and join cost more than the launch they hide: config 2 0.343 against
+// 0.330 ms/step, config 3 0.454 against 0.429; profiles/r03/fuseab/).
+enum { MG_FUSE_SFP = 1, MG_FUSE_ETA = 2, MG_FUSE_PHI = 4, MG_FUSE_END = 8, MG_FUSE_PHYS = 16, MG_FUSE_ETAA = 32 };
 inline bool mg_fuse_on(int bit) {
   // read per call (tests switch it per model)
   const int mask = getenv("MGCM_STEP_FUSE") ? atoi(getenv("MGCM_STEP_FUSE")) : MG_FUSE_SFP | MG_FUSE_PHI | MG_FUSE_END;

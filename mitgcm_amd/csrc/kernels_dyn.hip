@@ -2174,15 +2174,20 @@ hipError_t launch_phys_phi(const Dims &d, const Params &p, const Fields &f, cons
 
 hipError_t launch_phi_hyd(const Dims &d, const Params &p, const Fields &f, hipStream_t s) {
   const long ncol = (long)(d.sNx + 3) * (d.sNy + 3) * d.nT;
-  const int nc = mg_colf_nc(ncol, d.Nr, 6);
+  // LDS slices: the phi sums need 3 (sM, sP, sPh); r* adds MOM_CALC_RTRANS's 3.  Columns per
+  // workgroup: MGCM_PHI_NC = 16 | 32 | 64 (sweeps), else mg_colf_nc's
+  const bool rstar = p.nonlinFreeSurf > 0 && p.select_rStar > 0;
+  const int nArr = rstar ? 6 : 3;
+  const int ncEnv = getenv("MGCM_PHI_NC") ? atoi(getenv("MGCM_PHI_NC")) : 0;
+  const int nc = (ncEnv == 16 || ncEnv == 32 || ncEnv == 64) ? ncEnv : mg_colf_nc(ncol, d.Nr, nArr);
   if (phi_del2_fused(d, p)) {
     MG_ALLOW_LDS(k_phi_del2);
     const unsigned nbPhi = mg_colf_blocks(ncol, nc), nbDel = mg_plane_blocks(d.nx, d.ny, d.nT * d.Nr);
-    hipLaunchKernelGGL(k_phi_del2, dim3(nbPhi + nbDel), dim3(256), mg_colf_lds(d.Nr, nc, 6), s, d, p, f, nc, (int)nbPhi);
+    hipLaunchKernelGGL(k_phi_del2, dim3(nbPhi + nbDel), dim3(256), mg_colf_lds(d.Nr, nc, nArr), s, d, p, f, nc, (int)nbPhi);
     return hipGetLastError();
   }
   MG_ALLOW_LDS(k_phi_hyd);
-  hipLaunchKernelGGL(k_phi_hyd, dim3(mg_colf_blocks(ncol, nc)), dim3(256), mg_colf_lds(d.Nr, nc, 6), s, d, p, f, nc);
+  hipLaunchKernelGGL(k_phi_hyd, dim3(mg_colf_blocks(ncol, nc)), dim3(256), mg_colf_lds(d.Nr, nc, nArr), s, d, p, f, nc);
   return hipGetLastError();
 }
 

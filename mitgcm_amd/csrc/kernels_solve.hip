@@ -1353,7 +1353,12 @@ __global__ void __launch_bounds__(256) k_exch_etaH(Dims d, Params p, Fields f, c
 // column staged k-parallel into LDS and its serial parts (the exactConserv column sum, the
 // upward w recurrence) run by one thread per column out of LDS; the corrected velocities go
 // through LDS too, so no global store sits between a level's loads and the next level's.
-__global__ void __launch_bounds__(256) k_corr_cont(Dims d, Params p, Fields f, int atInit, int nc) {
+// etaSrc (the step path): the surface-pressure gradient reads recip_Bo * cg2d_x at the
+// exchange source of each point -- exactly the etaN that SOLVE_FOR_PRESSURE's EXCH_XY_RL +
+// etaN = recip_Bo*cg2d_x (k_exch_eta) stores -- so k_exch_eta runs beside this kernel instead
+// of before it (it writes only etaN and cg2d_x's halo, which this kernel then does not read).
+__global__ void __launch_bounds__(256) k_corr_cont(Dims d, Params p, Fields f, int atInit, int nc,
+                                                   const long *__restrict__ etaSrc) {
   extern __shared__ __attribute__((aligned(16))) double lds[];
   MG_COLF(1, d.sNx, 1, d.sNy, nc)
   const int NS = d.Nr * NC_;
@@ -1374,13 +1379,18 @@ __global__ void __launch_bounds__(256) k_corr_cont(Dims d, Params p, Fields f, i
     sH0[me] = rstar ? f.h0FacC[MG_I3(d, i, j, k, t)] : 0.0;
   } else if (valid) {
     const double psFac = p.pfFacMom * p.implicSurfPress;
+    auto eta = [&](long qq) {
+      if (!etaSrc) return f.etaN[qq];
+      const long sq = etaSrc[qq];
+      return f.recip_Bo[qq] * f.cg2d_x[sq >= 0 ? sq : qq];
+    };
     auto phiX = [&](int ii, int jj) {
       const long qq = MG_I2(d, ii, jj, t);
-      return f.recip_dxC[qq] * (f.Bo_surf[qq] * f.etaN[qq] - f.Bo_surf[MG_I2(d, ii - 1, jj, t)] * f.etaN[MG_I2(d, ii - 1, jj, t)]);
+      return f.recip_dxC[qq] * (f.Bo_surf[qq] * eta(qq) - f.Bo_surf[MG_I2(d, ii - 1, jj, t)] * eta(MG_I2(d, ii - 1, jj, t)));
     };
     auto phiY = [&](int ii, int jj) {
       const long qq = MG_I2(d, ii, jj, t);
-      return f.recip_dyC[qq] * (f.Bo_surf[qq] * f.etaN[qq] - f.Bo_surf[MG_I2(d, ii, jj - 1, t)] * f.etaN[MG_I2(d, ii, jj - 1, t)]);
+      return f.recip_dyC[qq] * (f.Bo_surf[qq] * eta(qq) - f.Bo_surf[MG_I2(d, ii, jj - 1, t)] * eta(MG_I2(d, ii, jj - 1, t)));
     };
     // the column's surface-pressure gradients (2-D, the same at every level)
     const double pX0 = phiX(i, j), pX1 = phiX(i + 1, j), pY0 = phiY(i, j), pY1 = phiY(i, j + 1);
@@ -1692,12 +1702,13 @@ hipError_t launch_exch_eta(const Dims &d, const Params &p, const Fields &f, cons
   return hipGetLastError();
 }
 
-hipError_t launch_corr_cont(const Dims &d, const Params &p, const Fields &f, int atInit, hipStream_t s) {
+hipError_t launch_corr_cont(const Dims &d, const Params &p, const Fields &f, int atInit, hipStream_t s,
+                            const long *etaSrc) {
   const long ncol = (long)d.sNx * d.sNy * d.nT;
   const int nc = mg_colf_nc(ncol, d.Nr, 5);
   MG_ALLOW_LDS(k_corr_cont);
   hipLaunchKernelGGL(k_corr_cont, dim3(mg_colf_blocks(ncol, nc)), dim3(256), mg_colf_lds(d.Nr, nc, 5), s, d, p, f, atInit,
-                     nc);
+                     nc, etaSrc);
   return hipGetLastError();
 }
 

@@ -50,7 +50,7 @@ hipError_t launch_exchange_mixed(const Dims &, double *, double *, int, const lo
 hipError_t launch_exchange_uv_pairs(const Dims &, double *const *, double *const *, int, const long *, int, int,
                                    hipStream_t);
 hipError_t launch_exch_eta(const Dims &, const Params &, const Fields &, const long *, bool, int, hipStream_t);
-hipError_t launch_corr_cont(const Dims &, const Params &, const Fields &, int, hipStream_t);
+hipError_t launch_corr_cont(const Dims &, const Params &, const Fields &, int, hipStream_t, const long *etaSrc = nullptr);
 hipError_t launch_calc_r_star(const Dims &, const Params &, const Fields &, const long *, hipStream_t, bool fuseEtaH = false);
 hipError_t launch_rstar_exch(const Dims &, const Params &, const Fields &, const long *, bool, const XFields &, const long *,
                              int, int *, hipStream_t);
@@ -154,6 +154,8 @@ struct mgcm_model {
   // DO_OCEANIC_PHYS, join before UPDATE_R_STAR / SOLVE_FOR_PRESSURE; MGCM_NO_OVERLAP=1 off)
   hipStream_t stream2 = nullptr;
   hipEvent_t evFork = nullptr, evJoin = nullptr;
+  hipStream_t stream3 = nullptr;                  // EXCH(cg2d_x) + etaN beside the correction step
+  hipEvent_t evEta0 = nullptr, evEta1 = nullptr;
   hipEvent_t evHand = nullptr;   // mgcm_stream_handoff
   bool overlap = true;
   std::vector<void *> allocs;
@@ -734,6 +736,9 @@ mgcm_model *mgcm_create(int sNx, int sNy, int OLx, int OLy, int Nr, int nSx, int
   if (hipStreamCreateWithFlags(&m->stream2, hipStreamNonBlocking) != hipSuccess ||
       hipEventCreateWithFlags(&m->evFork, hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&m->evHand, hipEventDisableTiming) != hipSuccess ||
+      hipStreamCreateWithFlags(&m->stream3, hipStreamNonBlocking) != hipSuccess ||
+      hipEventCreateWithFlags(&m->evEta0, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&m->evEta1, hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&m->evJoin, hipEventDisableTiming) != hipSuccess ||
       hipEventCreate(&m->ovlEv[0]) != hipSuccess || hipEventCreate(&m->ovlEv[1]) != hipSuccess) {
     set_err("mgcm_create: second stream / events");
@@ -824,6 +829,9 @@ void mgcm_destroy(mgcm_model *m) {
   if (m->stream2) hipStreamDestroy(m->stream2);
   if (m->evFork) hipEventDestroy(m->evFork);
   if (m->evHand) hipEventDestroy(m->evHand);
+  if (m->stream3) hipStreamDestroy(m->stream3);
+  if (m->evEta0) hipEventDestroy(m->evEta0);
+  if (m->evEta1) hipEventDestroy(m->evEta1);
   if (m->evJoin) hipEventDestroy(m->evJoin);
   for (auto &ev : m->ovlEv)
     if (ev) hipEventDestroy(ev);
@@ -1418,9 +1426,24 @@ static int one_step(mgcm_model *m) {
     if (thermoLate && thermoAtEnv == 2 && fork_thermo()) return -1;
     const bool etaFused = mg_fuse_on(MG_FUSE_ETA) && cg2d_fuses_eta(m);
     TIMED(K_CG2D, launch_cg2d(m, m->p.cg2dMaxIters, m->p.cg2dUseMinResSol - 1, etaFused));
-    if (!etaFused) TIMED(K_ETA, launch_exch_eta(m->d, m->p, m->f, m->d_srcOf, false, 0, m->stream));
+    // Under exactConserv the etaN of EXCH_XY_RL(cg2d_x) + etaN = recip_Bo*cg2d_x
+    // (solve_for_pressure.F:309-330) is read only by MOMENTUM_CORRECTION_STEP's gradient before
+    // INTEGR_CONTINUITY's EXCH(eta) + UPDATE_ETAH replaces it; k_corr_cont derives that eta from
+    // cg2d_x at the exchange sources itself, so k_exch_eta runs on a third stream beside it
+    // (MG_FUSE_ETAA), joined before the etaN rewrite
+    const bool etaAside = !etaFused && m->p.exactConserv && !m->timing && mg_fuse_on(MG_FUSE_ETAA) &&
+                          m->d.nT == m->d.nTiles;
+    if (etaAside) {
+      HIPCHK(hipEventRecord(m->evEta0, m->stream));
+      HIPCHK(hipStreamWaitEvent(m->stream3, m->evEta0, 0));
+      HIPCHK(launch_exch_eta(m->d, m->p, m->f, m->d_srcOf, false, 0, m->stream3));
+      HIPCHK(hipEventRecord(m->evEta1, m->stream3));
+    } else if (!etaFused) {
+      TIMED(K_ETA, launch_exch_eta(m->d, m->p, m->f, m->d_srcOf, false, 0, m->stream));
+    }
     if (lateJoin) HIPCHK(hipStreamWaitEvent(m->stream, m->evJoin, 0));
-    TIMED(K_CONT, launch_corr_cont(m->d, m->p, m->f, 0, m->stream));
+    TIMED(K_CONT, launch_corr_cont(m->d, m->p, m->f, 0, m->stream, etaAside ? m->d_srcOf : nullptr));
+    if (etaAside) HIPCHK(hipStreamWaitEvent(m->stream, m->evEta1, 0));
     // forward_step.F:965-977: CALC_R_STAR(etaH(n+1)); the next step's RESET_NLFS_VARS +
     // UPDATE_R_STAR(.FALSE.) restore the hFac in place, so they are not repeated here.
     // Under r* the exactConserv EXCH(eta) + UPDATE_ETAH runs inside CALC_R_STAR's pass
