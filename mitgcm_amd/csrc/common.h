@@ -257,8 +257,11 @@ inline unsigned mg_colf_blocks(long ncols, int nc) { return (unsigned)((ncols + 
 // SOLVE_FOR_PRESSURE's EXCH(cg2d_x) + etaN off the critical path (exactConserv: beside the
 // correction step, which derives the eta it needs from cg2d_x itself; bit-identical, but the
 // third stream's fork and join cost more than the launch they hide: config 2 0.343 against
-// 0.330 ms/step, config 3 0.454 against 0.429; profiles/r03/fuseab/).
-enum { MG_FUSE_SFP = 1, MG_FUSE_ETA = 2, MG_FUSE_PHI = 4, MG_FUSE_END = 8, MG_FUSE_PHYS = 16, MG_FUSE_ETAA = 32 };
+// 0.330 ms/step, config 3 0.454 against 0.429; profiles/r03/fuseab/), MG_FUSE_TREX the
+// tracers' halo exchange on their own stream beside the pressure solve (late join only;
+// bit-identical, no measurable change on LLC-90: 1.851 against 1.851-1.854 ms/step).
+enum { MG_FUSE_SFP = 1, MG_FUSE_ETA = 2, MG_FUSE_PHI = 4, MG_FUSE_END = 8, MG_FUSE_PHYS = 16, MG_FUSE_ETAA = 32,
+       MG_FUSE_TREX = 64 };
 inline bool mg_fuse_on(int bit) {
   // read per call (tests switch it per model)
   const int mask = getenv("MGCM_STEP_FUSE") ? atoi(getenv("MGCM_STEP_FUSE")) : MG_FUSE_SFP | MG_FUSE_PHI | MG_FUSE_END;

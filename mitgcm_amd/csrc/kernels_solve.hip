@@ -1362,7 +1362,8 @@ __global__ void __launch_bounds__(256) k_corr_cont(Dims d, Params p, Fields f, i
   extern __shared__ __attribute__((aligned(16))) double lds[];
   MG_COLF(1, d.sNx, 1, d.sNy, nc)
   const int NS = d.Nr * NC_;
-  double *sDiv = lds, *sMask = lds + NS, *sH0 = lds + 2 * NS, *sU = lds + 3 * NS, *sV = lds + 4 * NS;
+  // sH0 (r* only) last: launch_corr_cont allocates it only under r*
+  double *sDiv = lds, *sMask = lds + NS, *sU = lds + 2 * NS, *sV = lds + 3 * NS, *sH0 = lds + 4 * NS;
   const long q = MG_I2(d, i, j, t);
   const bool rstar = p.nonlinFreeSurf > 0 && p.select_rStar != 0;
   if (valid && atInit != 0) MG_COLF_K(k) {   // divergence of the velocities already in uVel, vVel
@@ -1376,7 +1377,7 @@ __global__ void __launch_bounds__(256) k_corr_cont(Dims d, Params p, Fields f, i
     const double vT0 = v0 * f.dxG[q] * drF * f.hFacS[MG_I3(d, i, j, k, t)];
     sDiv[me] = uT1 - uT0 + vT1 - vT0;
     sMask[me] = f.maskC[MG_I3(d, i, j, k, t)];
-    sH0[me] = rstar ? f.h0FacC[MG_I3(d, i, j, k, t)] : 0.0;
+    if (rstar) sH0[me] = f.h0FacC[MG_I3(d, i, j, k, t)];
   } else if (valid) {
     const double psFac = p.pfFacMom * p.implicSurfPress;
     auto eta = [&](long qq) {
@@ -1417,7 +1418,7 @@ __global__ void __launch_bounds__(256) k_corr_cont(Dims d, Params p, Fields f, i
       const double vT0 = v0 * f.dxG[q] * drF * f.hFacS[MG_I3(d, i, j, k, t)];
       sDiv[me] = uT1 - uT0 + vT1 - vT0;
       sMask[me] = f.maskC[MG_I3(d, i, j, k, t)];
-      sH0[me] = rstar ? f.h0FacC[MG_I3(d, i, j, k, t)] : 0.0;
+      if (rstar) sH0[me] = f.h0FacC[MG_I3(d, i, j, k, t)];
     }
   }
   __syncthreads();
@@ -1705,10 +1706,16 @@ hipError_t launch_exch_eta(const Dims &d, const Params &p, const Fields &f, cons
 hipError_t launch_corr_cont(const Dims &d, const Params &p, const Fields &f, int atInit, hipStream_t s,
                             const long *etaSrc) {
   const long ncol = (long)d.sNx * d.sNy * d.nT;
-  const int nc = mg_colf_nc(ncol, d.Nr, 5);
+  const int nArr = (p.nonlinFreeSurf > 0 && p.select_rStar != 0) ? 5 : 4;   // sH0 under r* only
+  // deep grids: 32 columns per workgroup (LLC-90: 123 us against 140 at 16,
+  // profiles/r03/colfnc/); shallow: 16 (config 2: 0.328-0.331 ms/step against 0.333 at 32,
+  // profiles/r03/ab_trex_corrnc/); MGCM_CORR_NC / MGCM_COLF_NC override
+  const int ncDef = d.Nr >= 30 ? 32 : 16;
+  const int ncEnv = getenv("MGCM_CORR_NC") ? atoi(getenv("MGCM_CORR_NC")) : getenv("MGCM_COLF_NC") ? atoi(getenv("MGCM_COLF_NC")) : ncDef;
+  const int nc = (ncEnv == 16 || ncEnv == 32 || ncEnv == 64) ? ncEnv : ncDef;
   MG_ALLOW_LDS(k_corr_cont);
-  hipLaunchKernelGGL(k_corr_cont, dim3(mg_colf_blocks(ncol, nc)), dim3(256), mg_colf_lds(d.Nr, nc, 5), s, d, p, f, atInit,
-                     nc, etaSrc);
+  hipLaunchKernelGGL(k_corr_cont, dim3(mg_colf_blocks(ncol, nc)), dim3(256), mg_colf_lds(d.Nr, nc, nArr), s, d, p, f,
+                     atInit, nc, etaSrc);
   return hipGetLastError();
 }
 

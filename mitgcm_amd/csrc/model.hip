@@ -1278,7 +1278,7 @@ int mgcm_calc_r_star(mgcm_model *m) {
   return 0;
 }
 
-static XFields blocking_fields(const mgcm_model *m);
+static XFields blocking_fields(const mgcm_model *m, int tracers = 1);
 
 int mgcm_blocking_exchanges(mgcm_model *m) {
   if (check_ready(m)) return -1;
@@ -1348,7 +1348,9 @@ long mgcm_field_count(mgcm_model *m, const char *name) {
   return field_count(m, fd->kind);
 }
 
-static XFields blocking_fields(const mgcm_model *m) {
+// tracers: 1 every field (the reference's set), 0 without theta/salt (exchanged beside the
+// pressure solve, one_step), 2 theta/salt only
+static XFields blocking_fields(const mgcm_model *m, int tracers) {
   XFields x{};
   // do_fields_blocking_exchanges.F:54-97 (+ EXCH_UV_DGRID of uVelD/vVelD with the CD scheme,
   // totPhiHyd when the EOS reads it)
@@ -1356,8 +1358,10 @@ static XFields blocking_fields(const mgcm_model *m) {
   double *fl[] = {m->f.uVel, m->f.vVel, m->f.wVel, m->f.theta, m->f.salt, m->f.uVelD, m->f.vVelD, m->f.totPhiHyd};
   const bool use[] = {!m->uvMap, !m->uvMap, true, m->p.tempStepping != 0, m->p.saltStepping != 0, m->p.useCDscheme != 0,
                       m->p.useCDscheme != 0, m->p.storePhiHyd4Phys != 0};
-  for (int q = 0; q < 8; q++)
-    if (use[q]) { x.p[x.n] = fl[q]; x.nz[x.n] = m->d.Nr; x.n++; }
+  for (int q = 0; q < 8; q++) {
+    const bool tr = q == 3 || q == 4;
+    if (use[q] && (tracers == 1 || (tracers == 2) == tr)) { x.p[x.n] = fl[q]; x.nz[x.n] = m->d.Nr; x.n++; }
+  }
   return x;
 }
 
@@ -1387,10 +1391,19 @@ static int one_step(mgcm_model *m) {
   const int thermoAtEnv = getenv("MGCM_THERMO_AT") ? atoi(getenv("MGCM_THERMO_AT")) : 1;
   const bool lateJoin = fork && m->p.nonlinFreeSurf <= 0;
   const bool thermoLate = lateJoin && thermoAtEnv >= 1;
+  // With the late join (THERMODYNAMICS beside the pressure solve) the new tracers' halos are
+  // filled on the tracers' stream right after them -- DO_FIELDS_BLOCKING_EXCHANGES' theta and
+  // salt, which nothing before it reads -- so the end-of-step exchange carries only the
+  // velocities (MG_FUSE_TREX)
+  const bool trEx = lateJoin && thermoAtEnv >= 1 && mg_fuse_on(MG_FUSE_TREX);
   auto fork_thermo = [&]() -> int {
     HIPCHK(hipEventRecord(m->evFork, m->stream));
     HIPCHK(hipStreamWaitEvent(m->stream2, m->evFork, 0));
     if (tracers_on(m, m->stream2)) return -1;
+    if (trEx) {
+      const XFields xt = blocking_fields(m, 2);
+      if (xt.n > 0) HIPCHK(launch_exchange_multi(m->d, xt, m->d_halo, m->nHalo, nullptr, m->stream2));
+    }
     HIPCHK(hipEventRecord(m->evJoin, m->stream2));
     return 0;
   };
@@ -1476,11 +1489,12 @@ static int one_step(mgcm_model *m) {
     if (tracers_on(m, m->stream)) return -1;
   }
   if (endFused) return 0;
+  const XFields xEnd = blocking_fields(m, trEx ? 0 : 1);
   if (m->uvMap)   // the vector pair and the scalar fields in one launch
-    TIMED(K_EXCH, launch_exchange_mixed(m->d, m->f.uVel, m->f.vVel, m->d.Nr, m->d_uv[1], m->nUvU[1], m->nUvV[1],
-                                        blocking_fields(m), m->d_halo, m->nHalo, m->d_ctr, m->stream));
+    TIMED(K_EXCH, launch_exchange_mixed(m->d, m->f.uVel, m->f.vVel, m->d.Nr, m->d_uv[1], m->nUvU[1], m->nUvV[1], xEnd,
+                                        m->d_halo, m->nHalo, m->d_ctr, m->stream));
   else
-    TIMED(K_EXCH, launch_exchange_multi(m->d, blocking_fields(m), m->d_halo, m->nHalo, m->d_ctr, m->stream));
+    TIMED(K_EXCH, launch_exchange_multi(m->d, xEnd, m->d_halo, m->nHalo, m->d_ctr, m->stream));
   return 0;
 }
 

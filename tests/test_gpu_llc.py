@@ -18,7 +18,7 @@ import pytest
 pytestmark = pytest.mark.gpu
 
 
-@pytest.mark.parametrize("march", [None, "1:2", "1:10", "1:3:single", "vi:4", "vi:3:generic", "fuse:29", "fuse:45"])
+@pytest.mark.parametrize("march", [None, "1:2", "1:10", "1:3:single", "vi:4", "vi:3:generic", "fuse:29", "fuse:45", "fuse:77"])
 def test_llc30_8_steps_bitexact_vs_device_order_oracle(march, monkeypatch):
     """march = "on:KC[:single]": the tracer right-hand side as the k-march (the LLC-90
     default) with KC levels per workgroup -- 5 chunks, 1, 4 uneven -- for both tracers in one
@@ -27,7 +27,8 @@ def test_llc30_8_steps_bitexact_vs_device_order_oracle(march, monkeypatch):
     default; LLC-30 has too few blocks to pick it by itself) with KC levels per workgroup, in
     its compile-time specialisation (k_mom_vi_m2<32, 8, LLC options>) or the generic kernel.
     "fuse:MASK": the MGCM_STEP_FUSE launch fusions (29: the opt-in k_phys_phi pass; 45: the
-    opt-in EXCH(cg2d_x) + etaN beside the correction step)."""
+    opt-in EXCH(cg2d_x) + etaN beside the correction step; 77: the tracers' halo exchange on
+    their own stream)."""
     if march and march.startswith("fuse:"):   # MGCM_STEP_FUSE mask: 29 adds DO_OCEANIC_PHYS + CALC_PHI_HYD in one pass
         monkeypatch.setenv("MGCM_STEP_FUSE", march.split(":")[1])
     elif march and march.startswith("vi:"):
