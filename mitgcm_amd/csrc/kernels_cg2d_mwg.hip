@@ -168,23 +168,54 @@ __device__ __forceinline__ bool mw_sync(double *v, const MwgTables &T, int g, in
       if (lane == 0) gran_put<SYS>(P + ((size_t)q * T.G + g) * 2, tag, wgp);
     }
     // combine: lane l adds partials l, l+64, ... in order, then the pairwise tree over the
-    // lanes; the whole sweep is repeated until every granule carries this phase's tag
+    // lanes; the whole sweep is repeated until every granule carries this phase's tag.  Up
+    // to MW_KG partials per lane (G <= 64*MW_KG) the sweep is unrolled: every granule load
+    // of a sweep is issued before the first is used, so a sweep costs one round trip rather
+    // than one per partial (a run-time loop waits for each load before its add)
     double acc[NV];
     unsigned spins = 0;
     bool ok = true;
-    for (;;) {
-      bool good = true;
+    constexpr int MW_KG = 2;
+    if (T.G <= 64 * MW_KG) {
+      for (;;) {
+        double xs[NV][MW_KG];
+        bool gd[NV][MW_KG];
 #pragma unroll
-      for (int q = 0; q < NV; q++) {
-        acc[q] = 0.0;
-        for (int gg = lane; gg < T.G; gg += 64) {
-          double xg;
-          good = gran_get<SYS>(P + ((size_t)q * T.G + gg) * 2, tag, xg) && good;
-          acc[q] = MAXOP ? fmax(acc[q], xg) : acc[q] + xg;
+        for (int q = 0; q < NV; q++)
+#pragma unroll
+          for (int r = 0; r < MW_KG; r++) {
+            const int gg = lane + 64 * r;
+            xs[q][r] = 0.0;
+            gd[q][r] = gg < T.G ? gran_get<SYS>(P + ((size_t)q * T.G + gg) * 2, tag, xs[q][r]) : true;
+          }
+        bool good = true;
+#pragma unroll
+        for (int q = 0; q < NV; q++) {
+          acc[q] = 0.0;
+#pragma unroll
+          for (int r = 0; r < MW_KG; r++) {
+            good = good && gd[q][r];
+            if (lane + 64 * r < T.G) acc[q] = MAXOP ? fmax(acc[q], xs[q][r]) : acc[q] + xs[q][r];
+          }
         }
+        if (__all(good)) break;
+        if (spin_fail<SYS>(spins, (gu32 *)T.ctr + 1, ep)) { ok = false; break; }
       }
-      if (__all(good)) break;
-      if (spin_fail<SYS>(spins, (gu32 *)T.ctr + 1, ep)) { ok = false; break; }
+    } else {
+      for (;;) {
+        bool good = true;
+#pragma unroll
+        for (int q = 0; q < NV; q++) {
+          acc[q] = 0.0;
+          for (int gg = lane; gg < T.G; gg += 64) {
+            double xg;
+            good = gran_get<SYS>(P + ((size_t)q * T.G + gg) * 2, tag, xg) && good;
+            acc[q] = MAXOP ? fmax(acc[q], xg) : acc[q] + xg;
+          }
+        }
+        if (__all(good)) break;
+        if (spin_fail<SYS>(spins, (gu32 *)T.ctr + 1, ep)) { ok = false; break; }
+      }
     }
 #pragma unroll
     for (int q = 0; q < NV; q++) {
