@@ -2191,6 +2191,7 @@ hipError_t launch_phi_hyd(const Dims &d, const Params &p, const Fields &f, hipSt
   return hipGetLastError();
 }
 
+static hipError_t launch_mom_tail(const Dims &d, const Params &p, const Fields &f, const int *iterPtr, hipStream_t s);
 // DYNAMICS after CALC_PHI_HYD (launch_phi_hyd): momentum tendencies, TIMESTEP, AB2, CD scheme,
 // implicit vertical viscosity
 hipError_t launch_mom_step(const Dims &d, const Params &p, const Fields &f, const int *iterPtr, hipStream_t s) {
@@ -2244,6 +2245,11 @@ hipError_t launch_mom_step(const Dims &d, const Params &p, const Fields &f, cons
   else   // MOM_FLUXFORM: U and V halves as separate threads (twice the workgroups, half the chain)
     hipLaunchKernelGGL(k_mom_step_uv<false>, dim3(2 * mg_plane_blocks(d.nx, d.ny, d.nT * d.Nr)), dim3(MG_PLANE_THREADS), 0,
                        s, d, p, f, iterPtr);
+  return launch_mom_tail(d, p, f, iterPtr, s);
+}
+
+// the end of DYNAMICS after the tendencies: CD scheme, implicit vertical viscosity
+static hipError_t launch_mom_tail(const Dims &d, const Params &p, const Fields &f, const int *iterPtr, hipStream_t s) {
   if (p.useCDscheme)
     hipLaunchKernelGGL(k_cd_scheme, dim3(mg_plane_blocks(d.nx - 2, d.ny - 2, d.nT * d.Nr)), dim3(MG_PLANE_THREADS), 0, s,
                        d, p, f, iterPtr);

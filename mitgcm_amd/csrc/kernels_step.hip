@@ -1,0 +1,92 @@
+// kernels_step.hip -- DYNAMICS and THERMODYNAMICS in one translation unit, and the launches
+// that fold the two into shared grids.
+//
+// forward_step.F:732-760 runs THERMODYNAMICS then DYNAMICS; neither reads what the other
+// writes (THERMODYNAMICS: the tracers' other buffers, their AB histories and T* scratch;
+// DYNAMICS: phiHyd, gU/gV, the momentum AB histories, the CD-scheme fields), so on a small
+// grid -- where every launch is a few microseconds of latency and one kernel cannot fill the
+// chip -- their kernels of the same depth share one grid (horizontal launch fusion, split by
+// logical block id as k_phi_del2 does) instead of running on two streams joined by events:
+//
+//   front: CALC_PHI_HYD | MOM del2 (biharmonic) | GAD_CALC_RHS+AB2+TIMESTEP (theta) | (salt)
+//   back:  MOM_FLUXFORM+TIMESTEP (U and V halves) | GAD_IMPLICIT_R + SOLVE_TRIDIAGONAL (theta) | (salt)
+//   then:  CD_CODE_SCHEME, implicit viscosity (launch_mom_tail)
+//
+// Every body is the same device function the separate kernels run, so the results are the
+// same bits.  The two source files are included rather than linked: hipcc builds without
+// relocatable device code, and the fused kernels need both files' bodies.
+#include "kernels_dyn.hip"
+#include "kernels_thermo.hip"
+
+namespace mgcm {
+
+// CALC_PHI_HYD | del2uv | rhs(theta) | rhs(salt): logical blocks [0, nbPhi) phi's column frame,
+// then nbDel del2uv planes, then nbTr planes of each tracer (barriers stay block-uniform)
+template <bool GM>
+__global__ void __launch_bounds__(256) k_dt_front(Dims d, Params p, Fields f, TracerArgs aT, TracerArgs aS,
+                                                  const int *iterPtr, int nc, int nbPhi, int nbDel, int nbTr) {
+  int lb = mg_xcd_block();
+  if (lb < nbPhi) { phi_hyd_body(d, p, f, nc, lb); return; }
+  lb -= nbPhi;
+  if (lb < nbDel) { del2uv_body(d, p, f, lb); return; }
+  lb -= nbDel;
+  if (lb < nbTr) tracer_rhs_body<GM>(d, p, f, aT, iterPtr, lb);
+  else tracer_rhs_body<GM>(d, p, f, aS, iterPtr, lb - nbTr);
+}
+
+// MOM_FLUXFORM U | V (k_mom_step_uv's split: even logical blocks U, odd V) | implicit solve
+// (theta) | (salt)
+__global__ void __launch_bounds__(256) k_dt_back(Dims d, Params p, Fields f, TracerArgs aT, TracerArgs aS,
+                                                 const int *iterPtr, int nc, int nbMom, int nbImp) {
+  int lb = mg_xcd_block();
+  if (lb < nbMom) {
+    if (lb & 1) mom_step_point<false, 2>(d, p, f, iterPtr, lb >> 1);
+    else mom_step_point<false, 1>(d, p, f, iterPtr, lb >> 1);
+    return;
+  }
+  lb -= nbMom;
+  if (lb < nbImp) tracer_impl_body(d, p, f, aT, nc, lb);
+  else tracer_impl_body(d, p, f, aS, nc, lb - nbImp);
+}
+
+// Where the fold is exact and applies: both tracers stepped with the per-point right-hand
+// side (GM/Redi; no multi-dimensional advection) and the implicit vertical solve, flux-form
+// momentum split into U and V halves, on the small grids (mg_hfuse: <= 2^21 points), and
+// MGCM_STEP_FUSE bit MG_FUSE_DT
+bool dyn_thermo_fusable(const Dims &d, const Params &p, const TracerArgs &aT, const TracerArgs &aS) {
+  return mg_hfuse(MG_FUSE_DT, d.nx, d.ny, d.nT, d.Nr) && p.momStepping && p.tempStepping && p.saltStepping &&
+         p.useGMRedi && p.implicitDiffusion && !aT.multiDim && !aS.multiDim && !p.vectorInvariantMomentum &&
+         !getenv("MGCM_MOM_NOSPLIT") && aT.scr != aS.scr;
+}
+
+// CALC_PHI_HYD + THERMODYNAMICS' tracers + DYNAMICS in three launches on one stream
+// (after DO_OCEANIC_PHYS; dyn_thermo_fusable must hold)
+hipError_t launch_dyn_thermo(const Dims &d, const Params &p, const Fields &f, const TracerArgs &aT, const TracerArgs &aS,
+                             const int *iterPtr, hipStream_t s) {
+  const dim3 blk(256);
+  // front: phi's column frame (launch_phi_hyd's columns and LDS), del2uv's and the tracers' planes
+  const long ncolPhi = (long)(d.sNx + 3) * (d.sNy + 3) * d.nT;
+  const bool rstar = p.nonlinFreeSurf > 0 && p.select_rStar > 0;
+  const int nArrPhi = rstar ? 6 : 3;
+  const int ncEnv = getenv("MGCM_PHI_NC") ? atoi(getenv("MGCM_PHI_NC")) : 0;
+  const int ncPhi = (ncEnv == 16 || ncEnv == 32 || ncEnv == 64) ? ncEnv : mg_colf_nc(ncolPhi, d.Nr, nArrPhi);
+  const int nbPhi = (int)mg_colf_blocks(ncolPhi, ncPhi);
+  const int nbDel = del2_needed(p) ? (int)mg_plane_blocks(d.nx, d.ny, d.nT * d.Nr) : 0;
+  const int nbTr = (int)mg_plane_blocks(d.sNx, d.sNy, d.nT * d.Nr);
+  MG_ALLOW_LDS(k_dt_front<true>);
+  hipLaunchKernelGGL(k_dt_front<true>, dim3((unsigned)(nbPhi + nbDel + 2 * nbTr)), blk,
+                     mg_colf_lds(d.Nr, ncPhi, nArrPhi), s, d, p, f, aT, aS, iterPtr, ncPhi, nbPhi, nbDel, nbTr);
+  // back: the momentum halves and the implicit solves (k_tracer_impl's columns and LDS)
+  const int nbMom = 2 * (int)mg_plane_blocks(d.nx, d.ny, d.nT * d.Nr);
+  const long ncolTr = (long)d.sNx * d.sNy * d.nT;
+  const int ncTr = mg_colf_nc(ncolTr, d.Nr, 3);
+  const int nbImp = (int)mg_colf_blocks(ncolTr, ncTr);
+  MG_ALLOW_LDS(k_dt_back);
+  hipLaunchKernelGGL(k_dt_back, dim3((unsigned)(nbMom + 2 * nbImp)), blk, mg_colf_lds(d.Nr, ncTr, 3), s, d, p, f, aT, aS,
+                     iterPtr, ncTr, nbMom, nbImp);
+  const hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  return launch_mom_tail(d, p, f, iterPtr, s);
+}
+
+}  // namespace mgcm

@@ -428,11 +428,12 @@ __global__ void __launch_bounds__(256) k_advg_upd(Dims d, Fields f, TracerArgs a
 }
 
 // GAD_CALC_RHS + forcing + AB2 + TIMESTEP_TRACER for one interior (i,j,k) point:
-// writes gNm1 (AB tracers) and gTscr = tracer + dTtracer*gT (the right-hand side of
+// writes gNm1 (AB tracers) and a.scr = tracer + dTtracer*gT (the right-hand side of
 // the implicit vertical solve, or the new tracer with explicit vertical diffusion).
 template <bool GM>
-__global__ void __launch_bounds__(256) k_tracer_rhs(Dims d, Params p, Fields f, TracerArgs a, const int *iterPtr) {
-  MG_PLANE(1, d.sNx, 1, d.sNy, z)
+__device__ __forceinline__ void tracer_rhs_body(const Dims &d, const Params &p, const Fields &f, const TracerArgs &a,
+                                                const int *iterPtr, int lb) {
+  MG_PLANE_LB(1, d.sNx, 1, d.sNy, z, lb)
   const int t = d.t0 + z / d.Nr, k = z % d.Nr + 1;
   if (i > d.sNx || j > d.sNy) return;
   const int Nr = d.Nr;
@@ -580,11 +581,15 @@ __global__ void __launch_bounds__(256) k_tracer_rhs(Dims d, Params p, Fields f, 
   if (p.nonlinFreeSurf > 0 && p.select_rStar > 0) gT = gT / f.rStarExpC[q];
   // TIMESTEP_TRACER
   const double v = Tk + p.deltaTtracer * gT;
-  if (p.implicitDiffusion) f.gTscr[q3] = v;
+  if (p.implicitDiffusion) a.scr[q3] = v;
   else a.trNext[q3] = v;   // CYCLE_TRACER directly
 #undef T3
 #undef G2
 #undef G3
+}
+template <bool GM>
+__global__ void __launch_bounds__(256) k_tracer_rhs(Dims d, Params p, Fields f, TracerArgs a, const int *iterPtr) {
+  tracer_rhs_body<GM>(d, p, f, a, iterPtr, mg_xcd_block());
 }
 
 // k_tracer_rhs without GM/Redi, every load issued up front: the same expression trees as
@@ -725,7 +730,7 @@ __global__ void __launch_bounds__(256) k_tracer_march(Dims d, Params p, Fields f
     double gN = 0.0;
     const double v = tracer_flat_arith(p, f, a, Nr, k, myIter, c, o, &gN);
     if (a.useAB) a.gNm1[q3] = gN;
-    if (p.implicitDiffusion) f.gTscr[q3] = v;
+    if (p.implicitDiffusion) a.scr[q3] = v;
     else a.trNext[q3] = v;
     Tu = T0; T0 = o.Td; mCu = mC0; mC0 = o.mCd; w0 = o.w1; ivd0 = o.ivd1;
   }
@@ -882,7 +887,7 @@ __global__ void __launch_bounds__(256) k_tracer_rhs_flat(Dims d, Params p, Field
   if (i > d.sNx || j > d.sNy) return;
   const long q3 = MG_I3(d, i, j, k, t);
   const double v = tracer_flat_point(d, p, f, a, i, j, k, t, *iterPtr);
-  if (p.implicitDiffusion) f.gTscr[q3] = v;
+  if (p.implicitDiffusion) a.scr[q3] = v;
   else a.trNext[q3] = v;
 }
 
@@ -974,9 +979,10 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) k
 // every level are formed k-parallel into LDS, one thread per column then sweeps
 // down and up in LDS with the reference's operations, and the levels are
 // written back k-parallel.
-__global__ void __launch_bounds__(256) k_tracer_impl(Dims d, Params p, Fields f, TracerArgs a, int nc) {
+__device__ __forceinline__ void tracer_impl_body(const Dims &d, const Params &p, const Fields &f, const TracerArgs &a, int nc,
+                                                 int lb) {
   extern __shared__ __attribute__((aligned(16))) double lds[];
-  MG_COLF(1, d.sNx, 1, d.sNy, nc)
+  MG_COLF_LB(1, d.sNx, 1, d.sNy, nc, lb)
   const int Nr = d.Nr, NS = Nr * NC_;
   double *sSub = lds, *sSup = lds + NS, *sY = lds + 2 * NS;   // sSub holds the solution after the sweeps
 #define G3(a_, ii, jj, kk_) f.a_[MG_I3(d, ii, jj, kk_, t)]
@@ -1004,7 +1010,7 @@ __global__ void __launch_bounds__(256) k_tracer_impl(Dims d, Params p, Fields f,
         sup = -(p.deltaTtracer * G3(maskC, i, j, k + 1) * rh * rdrF * kappa(k + 1) * f.recip_drC[k]);
       sSub[me] = sub;
       sSup[me] = sup;
-      sY[me] = f.gTscr[q3];
+      sY[me] = a.scr[q3];
     }
   }
   __syncthreads();
@@ -1039,6 +1045,9 @@ __global__ void __launch_bounds__(256) k_tracer_impl(Dims d, Params p, Fields f,
   __syncthreads();
   if (valid) MG_COLF_K(k) a.trNext[MG_I3(d, i, j, k, t)] = sSub[(k - 1) * NC_ + cc];
 #undef G3
+}
+__global__ void __launch_bounds__(256) k_tracer_impl(Dims d, Params p, Fields f, TracerArgs a, int nc) {
+  tracer_impl_body(d, p, f, a, nc, mg_xcd_block());
 }
 
 hipError_t launch_oceanic_phys(const Dims &d, const Params &p, const Fields &f, const int *iterPtr, hipStream_t s) {

@@ -59,6 +59,9 @@ hipError_t launch_halo_pack(const Dims &, const XFields &, const long *, long, d
 hipError_t launch_oceanic_phys(const Dims &, const Params &, const Fields &, const int *, hipStream_t);
 hipError_t launch_tracer_step(const Dims &, const Params &, const Fields &, const TracerArgs &, const int *, hipStream_t);
 bool tracer_pair_ok(const Dims &, const Params &, const TracerArgs &, const TracerArgs &);
+bool dyn_thermo_fusable(const Dims &, const Params &, const TracerArgs &, const TracerArgs &);
+hipError_t launch_dyn_thermo(const Dims &, const Params &, const Fields &, const TracerArgs &, const TracerArgs &, const int *,
+                             hipStream_t);
 hipError_t launch_tracer_pair(const Dims &, const Params &, const Fields &, const TracerArgs &, const TracerArgs &,
                               const int *, hipStream_t);
 hipError_t launch_mon_stats(const Dims &, const MonSpecs &, int, double *, int, hipStream_t);
@@ -1191,6 +1194,7 @@ static TracerArgs tracer_args(mgcm_model *m, bool salt) {
   a.tr = salt ? m->f.salt : m->f.theta;
   a.trNext = salt ? m->f.saltNext : m->f.thetaNext;
   a.gNm1 = salt ? m->f.gsNm1 : m->f.gtNm1;
+  a.scr = salt ? m->f.cpScr : m->f.gTscr;   // own scratch each: the two may run concurrently
   a.sfc = salt ? m->f.surfaceForcingS : m->f.surfaceForcingT;
   a.diffKh = salt ? p.diffKhS : p.diffKhT;
   a.diffKr = salt ? p.diffKrS : p.diffKrT;
@@ -1407,6 +1411,10 @@ static int one_step(mgcm_model *m) {
     HIPCHK(hipEventRecord(m->evJoin, m->stream2));
     return 0;
   };
+  // Early fork on a small grid: THERMODYNAMICS' tracer kernels share DYNAMICS' launches
+  // (kernels_step.hip, MG_FUSE_DT) instead of running on the second stream -- no fork, no join
+  const TracerArgs aT = tracer_args(m, false), aS = tracer_args(m, true);
+  const bool dtFused = fork && !lateJoin && !tracer_pair_ok(m->d, m->p, aT, aS) && dyn_thermo_fusable(m->d, m->p, aT, aS);
   // the multi-workgroup CG2D keeps its CUs to itself while the tracers run beside it
   m->mwg.exclusive = thermoLate ? 1 : 0;
   // DO_OCEANIC_PHYS + DYNAMICS' CALC_PHI_HYD in one column pass where exact (phys_phi_fusable:
@@ -1420,15 +1428,19 @@ static int one_step(mgcm_model *m) {
   };
   if (stagger || fork) {
     if (phys()) return -1;
-    if (fork && !thermoLate && fork_thermo()) return -1;
+    if (fork && !thermoLate && !dtFused && fork_thermo()) return -1;
   } else {
     if (phys() || tracers_on(m, m->stream)) return -1;
   }
   if (m->p.momStepping) {
-    if (physPhi) TIMED(K_MOM, launch_mom_step(m->d, m->p, m->f, m->d_ctr, m->stream));
+    if (dtFused) {
+      TIMED(K_MOM, launch_dyn_thermo(m->d, m->p, m->f, aT, aS, m->d_ctr, m->stream));
+      std::swap(m->f.theta, m->f.thetaNext);   // CYCLE_TRACER: the new tracers are the other buffers
+      std::swap(m->f.salt, m->f.saltNext);
+    } else if (physPhi) TIMED(K_MOM, launch_mom_step(m->d, m->p, m->f, m->d_ctr, m->stream));
     else if (mgcm_dynamics(m)) return -1;
     if (thermoLate && thermoAtEnv == 1 && fork_thermo()) return -1;
-    if (fork && !lateJoin) HIPCHK(hipStreamWaitEvent(m->stream, m->evJoin, 0));
+    if (fork && !lateJoin && !dtFused) HIPCHK(hipStreamWaitEvent(m->stream, m->evJoin, 0));
     // forward_step.F:829-877: UPDATE_R_STAR(.TRUE.) + UPDATE_CG2D
     // (launch fusions, common.h MGCM_STEP_FUSE: CALC_DIV_GHAT in the r* column pass;
     // EXCH(cg2d_x) + etaN in the single-workgroup CG2D's epilogue -- off by default: one CU

@@ -111,7 +111,15 @@ def test_ocean90_dynamics_bitexact():
     assert not bad, bad
 
 
-def test_ocean90_10_steps(golden_dir):
+@pytest.mark.parametrize("variant", [None, "fork"])
+def test_ocean90_10_steps(golden_dir, monkeypatch, variant):
+    """variant None: the default step (THERMODYNAMICS' tracer kernels folded into DYNAMICS'
+    launches, kernels_step.hip); "fork": the tracers on the second stream beside DYNAMICS
+    (MGCM_STEP_FUSE without MG_FUSE_DT).  The overlap is forced on, so neither depends on
+    the auto-selection's timing."""
+    monkeypatch.setenv("MGCM_OVERLAP", "1")
+    if variant == "fork":
+        monkeypatch.setenv("MGCM_STEP_FUSE", "13")
     o, g = _oracle(0)            # reference summation order
     m = _model()
     plan, NT, PPT, NG = m.cg2d_sum_plan()
