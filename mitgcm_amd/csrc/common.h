@@ -248,7 +248,7 @@ inline size_t mg_colf_lds(int Nr, int nc, int nArr) { return (size_t)nArr * Nr *
   } while (0)
 inline unsigned mg_colf_blocks(long ncols, int nc) { return (unsigned)((ncols + nc - 1) / nc); }
 // Launch fusions of FORWARD_STEP, each switchable for A/B runs: MGCM_STEP_FUSE = bit mask of
-// the enabled ones (default SFP | PHI | END | DT): MG_FUSE_SFP CALC_DIV_GHAT in the r* column pass,
+// the enabled ones (default SFP | PHI | END | DT | ETAX): MG_FUSE_SFP CALC_DIV_GHAT in the r* column pass,
 // MG_FUSE_ETA EXCH(cg2d_x) + etaN in the single-workgroup CG2D, MG_FUSE_PHI CALC_PHI_HYD +
 // del2uv in one grid, MG_FUSE_END CALC_R_STAR + the blocking exchanges in one grid,
 // MG_FUSE_PHYS DO_OCEANIC_PHYS + CALC_PHI_HYD in one column pass (bit-identical, but on LLC-90
@@ -261,13 +261,14 @@ inline unsigned mg_colf_blocks(long ncols, int nc) { return (unsigned)((ncols + 
 // tracers' halo exchange on their own stream beside the pressure solve (late join only;
 // bit-identical, no measurable change on LLC-90: 1.851 against 1.851-1.854 ms/step).
 // MG_FUSE_DT THERMODYNAMICS' tracer kernels folded into DYNAMICS' launches instead of a
-// second stream beside them (kernels_step.hip; early fork only, small grids).
+// second stream beside them (kernels_step.hip; early fork only, small grids), MG_FUSE_ETAX
+// no separate EXCH(cg2d_x) + etaN under exactConserv (one_step).
 enum { MG_FUSE_SFP = 1, MG_FUSE_ETA = 2, MG_FUSE_PHI = 4, MG_FUSE_END = 8, MG_FUSE_PHYS = 16, MG_FUSE_ETAA = 32,
-       MG_FUSE_TREX = 64, MG_FUSE_DT = 128 };
+       MG_FUSE_TREX = 64, MG_FUSE_DT = 128, MG_FUSE_ETAX = 256 };
 inline bool mg_fuse_on(int bit) {
   // read per call (tests switch it per model)
   const int mask = getenv("MGCM_STEP_FUSE") ? atoi(getenv("MGCM_STEP_FUSE"))
-                                            : MG_FUSE_SFP | MG_FUSE_PHI | MG_FUSE_END | MG_FUSE_DT;
+                                            : MG_FUSE_SFP | MG_FUSE_PHI | MG_FUSE_END | MG_FUSE_DT | MG_FUSE_ETAX;
   return (mask & bit) != 0;
 }
 // Horizontal launch fusion of two independent latency-bound kernels into one grid: on the

@@ -20,13 +20,16 @@ namespace mgcm {
 // rStarExp = Fac/Fac_old (:283-298).  Each thread reads and writes only its own point's
 // factors, so the old values need no second buffer.
 // The new etaH of k_exch_etaH at point q: EXCH_XY_RL of the eta k_corr_cont left in cg2d_b
-// (the interior source of a halo point; the point itself inside; etaN where neither).
-__device__ __forceinline__ double eta_exch(const Dims &d, const Fields &f, const long *srcOf, long q) {
+// (the interior source of a halo point; the point itself inside; etaN where neither --
+// fromX: the etaN SOLVE_FOR_PRESSURE's EXCH(cg2d_x) + etaN = recip_Bo*cg2d_x leaves there,
+// recip_Bo*cg2d_x of the point itself, when that launch was skipped, see one_step).
+__device__ __forceinline__ double eta_exch(const Dims &d, const Fields &f, const long *srcOf, long q, int fromX) {
   const long sq = srcOf[q];
   if (sq >= 0) return f.cg2d_b[sq];
   const long l = q % d.n2;
   const int i = (int)(l % d.nx) - d.OLx + 1, j = (int)(l / d.nx) - d.OLy + 1;
-  return (i >= 1 && i <= d.sNx && j >= 1 && j <= d.sNy) ? f.cg2d_b[q] : f.etaN[q];
+  if (i >= 1 && i <= d.sNx && j >= 1 && j <= d.sNy) return f.cg2d_b[q];
+  return fromX ? f.recip_Bo[q] * f.cg2d_x[q] : f.etaN[q];
 }
 
 // fuseEtaH: k_exch_etaH in the same pass (the FORWARD_STEP order exch_etaH -> CALC_R_STAR):
@@ -36,14 +39,14 @@ __device__ __forceinline__ double eta_exch(const Dims &d, const Fields &f, const
 // mapped, which is rewritten with the value it holds.
 template <bool FUSE>
 __device__ __forceinline__ void calc_r_star_body(const Dims &d, const Params &p, const Fields &f,
-                                                 const long *__restrict__ srcOf, int lb) {
+                                                 const long *__restrict__ srcOf, int lb, int fromX) {
   const long q = (long)lb * blockDim.x + threadIdx.x;
   if (q >= d.n2 * d.nTiles) return;
   const int t = (int)(q / d.n2);
   if (t < d.t0 || t >= d.t0 + d.nT) return;
   if constexpr (FUSE) {   // k_exch_etaH (kernels_solve.hip), atInit = 0
     if (p.nonlinFreeSurf > 0 && p.useRealFreshWaterFlux) f.PmEpR[q] = -f.EmPmR[q];
-    const double x = eta_exch(d, f, srcOf, q);
+    const double x = eta_exch(d, f, srcOf, q, fromX);
     f.etaHnm1[q] = f.etaH[q];
     f.etaN[q] = x;
     f.etaH[q] = x;
@@ -51,7 +54,7 @@ __device__ __forceinline__ void calc_r_star_body(const Dims &d, const Params &p,
   const long sq = srcOf[q], r = sq >= 0 ? sq : q;   // where the new value is computed
   const long l = r % d.n2;
   const int i = (int)(l % d.nx) - d.OLx + 1, j = (int)(l / d.nx) - d.OLy + 1;
-  auto eta = [&](long qq) { return FUSE ? eta_exch(d, f, srcOf, qq) : f.etaH[qq]; };
+  auto eta = [&](long qq) { return FUSE ? eta_exch(d, f, srcOf, qq, fromX) : f.etaH[qq]; };
   const double oc = f.rStarFacC[q], ow = f.rStarFacW[q], os = f.rStarFacS[q];
   double fc = oc, fw = ow, fs = os;
   if (i >= 0 && i <= d.sNx + 1 && j >= 0 && j <= d.sNy + 1)   // kSurfC <= Nr <=> maskInC = 1
@@ -88,8 +91,8 @@ __device__ __forceinline__ void calc_r_star_body(const Dims &d, const Params &p,
   f.rStarExpS[q] = fs / os;
 }
 template <bool FUSE>
-__global__ void __launch_bounds__(256) k_calc_r_star(Dims d, Params p, Fields f, const long *__restrict__ srcOf) {
-  calc_r_star_body<FUSE>(d, p, f, srcOf, (int)blockIdx.x);
+__global__ void __launch_bounds__(256) k_calc_r_star(Dims d, Params p, Fields f, const long *__restrict__ srcOf, int fromX) {
+  calc_r_star_body<FUSE>(d, p, f, srcOf, (int)blockIdx.x, fromX);
 }
 // The end of FORWARD_STEP in one grid: CALC_R_STAR (with EXCH(eta) + UPDATE_ETAH, FUSE) on
 // the first nbR blocks and DO_FIELDS_BLOCKING_EXCHANGES (k_exchange_multi's nbX x nz x nF
@@ -98,9 +101,9 @@ __global__ void __launch_bounds__(256) k_calc_r_star(Dims d, Params p, Fields f,
 template <bool FUSE>
 __global__ void __launch_bounds__(256) k_rstar_exch(Dims d, Params p, Fields f, const long *__restrict__ srcOf, int nbR,
                                                     XFields x, const long *__restrict__ map, int nHalo, int *ctr, int nbX,
-                                                    int nzMax) {
+                                                    int nzMax, int fromX) {
   const int b = (int)blockIdx.x;
-  if (b < nbR) { calc_r_star_body<FUSE>(d, p, f, srcOf, b); return; }
+  if (b < nbR) { calc_r_star_body<FUSE>(d, p, f, srcOf, b, fromX); return; }
   const int r = b - nbR;
   exchange_multi_body(d, x, map, nHalo, ctr, r % nbX, (r / nbX) % nzMax, r / (nbX * nzMax));
 }
@@ -216,15 +219,15 @@ __global__ void __launch_bounds__(256) k_update_cg2d_p(Dims d, Params p, Fields 
 }
 
 hipError_t launch_calc_r_star(const Dims &d, const Params &p, const Fields &f, const long *srcOf, hipStream_t s,
-                              bool fuseEtaH) {
+                              bool fuseEtaH, int fromX) {
   const long n = d.n2 * d.nTiles;
   hipLaunchKernelGGL(fuseEtaH ? k_calc_r_star<true> : k_calc_r_star<false>, dim3((unsigned)((n + 255) / 256)), dim3(256),
-                     0, s, d, p, f, srcOf);
+                     0, s, d, p, f, srcOf, fromX);
   return hipGetLastError();
 }
 
 hipError_t launch_rstar_exch(const Dims &d, const Params &p, const Fields &f, const long *srcOf, bool fuseEtaH,
-                             const XFields &x, const long *map, int nHalo, int *ctr, hipStream_t s) {
+                             const XFields &x, const long *map, int nHalo, int *ctr, hipStream_t s, int fromX) {
   const long n = d.n2 * d.nTiles;
   const int nbR = (int)((n + 255) / 256);
   int nzMax = 1;
@@ -232,7 +235,7 @@ hipError_t launch_rstar_exch(const Dims &d, const Params &p, const Fields &f, co
   const int nbX = ((nHalo > 0 ? nHalo : 1) + 255) / 256;
   const unsigned nb = (unsigned)(nbR + nbX * nzMax * (x.n > 0 ? x.n : 1));
   hipLaunchKernelGGL(fuseEtaH ? k_rstar_exch<true> : k_rstar_exch<false>, dim3(nb), dim3(256), 0, s, d, p, f, srcOf, nbR, x,
-                     map, nHalo, ctr, nbX, nzMax);
+                     map, nHalo, ctr, nbX, nzMax, fromX);
   return hipGetLastError();
 }
 

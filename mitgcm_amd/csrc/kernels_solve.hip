@@ -1319,7 +1319,10 @@ __global__ void __launch_bounds__(256) k_exch_eta(Dims d, Fields f, const long *
 // by k_corr_cont) into etaN, and UPDATE_ETAH (etaH = etaN) in one pass.
 // Under the non-linear free surface with real fresh-water flux (not at initialisation)
 // PmEpR = -EmPmR over the whole tile (integr_continuity.F:137-143) is set here too.
-__global__ void __launch_bounds__(256) k_exch_etaH(Dims d, Params p, Fields f, const long *__restrict__ srcOf, int atInit) {
+// fromX: SOLVE_FOR_PRESSURE's k_exch_eta was skipped (one_step), so the etaN it would have left at
+// points neither interior nor mapped is formed here: recip_Bo*cg2d_x of the point.
+__global__ void __launch_bounds__(256) k_exch_etaH(Dims d, Params p, Fields f, const long *__restrict__ srcOf, int atInit,
+                                                   int fromX) {
   const long q = (long)blockIdx.x * blockDim.x + threadIdx.x;
   if (q >= d.n2 * d.nTiles) return;
   if (!atInit && p.nonlinFreeSurf > 0 && p.useRealFreshWaterFlux) f.PmEpR[q] = -f.EmPmR[q];
@@ -1331,7 +1334,7 @@ __global__ void __launch_bounds__(256) k_exch_etaH(Dims d, Params p, Fields f, c
     // interior: the new eta; points that are neither interior nor mapped keep etaN
     const long l = q % d.n2;
     const int i = (int)(l % d.nx) - d.OLx + 1, j = (int)(l / d.nx) - d.OLy + 1;
-    x = (i >= 1 && i <= d.sNx && j >= 1 && j <= d.sNy) ? e[q] : f.etaN[q];
+    x = (i >= 1 && i <= d.sNx && j >= 1 && j <= d.sNy) ? e[q] : fromX ? f.recip_Bo[q] * f.cg2d_x[q] : f.etaN[q];
   }
   f.etaHnm1[q] = f.etaH[q];   // update_etah.F:49-53: the etaH being replaced (pickup EtaH record)
   f.etaN[q] = x;
@@ -1696,9 +1699,9 @@ hipError_t launch_exchange_uv_pairs(const Dims &d, double *const *u, double *con
 }
 
 hipError_t launch_exch_eta(const Dims &d, const Params &p, const Fields &f, const long *srcOf, bool etaH, int atInit,
-                           hipStream_t s) {
+                           hipStream_t s, int fromX) {
   const long n = d.n2 * d.nTiles;
-  if (etaH) hipLaunchKernelGGL(k_exch_etaH, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, d, p, f, srcOf, atInit);
+  if (etaH) hipLaunchKernelGGL(k_exch_etaH, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, d, p, f, srcOf, atInit, fromX);
   else hipLaunchKernelGGL(k_exch_eta, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, d, f, srcOf);
   return hipGetLastError();
 }

@@ -49,11 +49,13 @@ hipError_t launch_exchange_mixed(const Dims &, double *, double *, int, const lo
                                  const long *, int, int *, hipStream_t);
 hipError_t launch_exchange_uv_pairs(const Dims &, double *const *, double *const *, int, const long *, int, int,
                                    hipStream_t);
-hipError_t launch_exch_eta(const Dims &, const Params &, const Fields &, const long *, bool, int, hipStream_t);
+hipError_t launch_exch_eta(const Dims &, const Params &, const Fields &, const long *, bool, int, hipStream_t,
+                           int fromX = 0);
 hipError_t launch_corr_cont(const Dims &, const Params &, const Fields &, int, hipStream_t, const long *etaSrc = nullptr);
-hipError_t launch_calc_r_star(const Dims &, const Params &, const Fields &, const long *, hipStream_t, bool fuseEtaH = false);
+hipError_t launch_calc_r_star(const Dims &, const Params &, const Fields &, const long *, hipStream_t, bool fuseEtaH = false,
+                              int fromX = 0);
 hipError_t launch_rstar_exch(const Dims &, const Params &, const Fields &, const long *, bool, const XFields &, const long *,
-                             int, int *, hipStream_t);
+                             int, int *, hipStream_t, int fromX = 0);
 hipError_t launch_update_r_star_cg2d(const Dims &, const Params &, const Fields &, const long *, hipStream_t, bool sfp = false);
 hipError_t launch_halo_pack(const Dims &, const XFields &, const long *, long, double *, int, hipStream_t);
 hipError_t launch_oceanic_phys(const Dims &, const Params &, const Fields &, const int *, hipStream_t);
@@ -1012,9 +1014,9 @@ static int exchange_uv(mgcm_model *m, double *u, double *v, int nz, bool withSig
 // operator.
 static Dims all_tiles(const Dims &d) { Dims a = d; a.t0 = 0; a.nT = d.nTiles; return a; }
 
-static hipError_t calc_r_star(mgcm_model *m, bool fuseEtaH = false) {
+static hipError_t calc_r_star(mgcm_model *m, bool fuseEtaH = false, int fromX = 0) {
   const Dims da = all_tiles(m->d);
-  hipError_t e = launch_calc_r_star(da, m->p, m->f, m->d_srcOf, m->stream, fuseEtaH);
+  hipError_t e = launch_calc_r_star(da, m->p, m->f, m->d_srcOf, m->stream, fuseEtaH, fromX);
   if (e != hipSuccess || !m->uvMap) return e;
   double *us[3] = {m->f.rStarFacW, m->f.rStarDhWDt, m->f.rStarExpW}, *vs[3] = {m->f.rStarFacS, m->f.rStarDhSDt,
                                                                                  m->f.rStarExpS};
@@ -1456,9 +1458,17 @@ static int one_step(mgcm_model *m) {
     // INTEGR_CONTINUITY's EXCH(eta) + UPDATE_ETAH replaces it; k_corr_cont derives that eta from
     // cg2d_x at the exchange sources itself, so k_exch_eta runs on a third stream beside it
     // (MG_FUSE_ETAA), joined before the etaN rewrite
-    const bool etaAside = !etaFused && m->p.exactConserv && !m->timing && mg_fuse_on(MG_FUSE_ETAA) &&
+    // Under exactConserv nothing else reads that etaN either: INTEGR_CONTINUITY's EXCH(eta) +
+    // UPDATE_ETAH overwrites it everywhere but at points neither interior nor mapped, where it
+    // keeps recip_Bo*cg2d_x -- so with MG_FUSE_ETAX k_exch_eta is not launched at all: k_corr_cont
+    // reads eta from cg2d_x as above and the UPDATE_ETAH pass forms those points' etaN itself
+    // (fromX; cg2d_x's halo is left unexchanged: the next SOLVE_FOR_PRESSURE rewrites cg2d_x
+    // everywhere before anything reads it)
+    const bool etaX = !etaFused && m->p.exactConserv && mg_fuse_on(MG_FUSE_ETAX) && m->d.nT == m->d.nTiles;
+    const bool etaAside = !etaX && !etaFused && m->p.exactConserv && !m->timing && mg_fuse_on(MG_FUSE_ETAA) &&
                           m->d.nT == m->d.nTiles;
-    if (etaAside) {
+    if (etaX) {
+    } else if (etaAside) {
       HIPCHK(hipEventRecord(m->evEta0, m->stream));
       HIPCHK(hipStreamWaitEvent(m->stream3, m->evEta0, 0));
       HIPCHK(launch_exch_eta(m->d, m->p, m->f, m->d_srcOf, false, 0, m->stream3));
@@ -1467,7 +1477,7 @@ static int one_step(mgcm_model *m) {
       TIMED(K_ETA, launch_exch_eta(m->d, m->p, m->f, m->d_srcOf, false, 0, m->stream));
     }
     if (lateJoin) HIPCHK(hipStreamWaitEvent(m->stream, m->evJoin, 0));
-    TIMED(K_CONT, launch_corr_cont(m->d, m->p, m->f, 0, m->stream, etaAside ? m->d_srcOf : nullptr));
+    TIMED(K_CONT, launch_corr_cont(m->d, m->p, m->f, 0, m->stream, (etaAside || etaX) ? m->d_srcOf : nullptr));
     if (etaAside) HIPCHK(hipStreamWaitEvent(m->stream, m->evEta1, 0));
     // forward_step.F:965-977: CALC_R_STAR(etaH(n+1)); the next step's RESET_NLFS_VARS +
     // UPDATE_R_STAR(.FALSE.) restore the hFac in place, so they are not repeated here.
@@ -1475,15 +1485,16 @@ static int one_step(mgcm_model *m) {
     // (k_calc_r_star<FUSE>; MGCM_NO_ETAH_FUSE=1 keeps the two launches)
     static const bool noFuse = getenv("MGCM_NO_ETAH_FUSE") && atoi(getenv("MGCM_NO_ETAH_FUSE")) == 1;
     const bool fuseEtaH = m->p.exactConserv && m->p.nonlinFreeSurf > 0 && !noFuse;
-    if (m->p.exactConserv && !fuseEtaH) TIMED(K_ETA, launch_exch_eta(m->d, m->p, m->f, m->d_srcOf, true, 0, m->stream));
+    if (m->p.exactConserv && !fuseEtaH)
+      TIMED(K_ETA, launch_exch_eta(m->d, m->p, m->f, m->d_srcOf, true, 0, m->stream, etaX ? 1 : 0));
     // CALC_R_STAR and the blocking exchanges in one grid on the small lat-lon grids
     // (k_rstar_exch; independent, and nothing between them in the non-staggered step)
     endFused = m->p.nonlinFreeSurf > 0 && !stagger && !m->uvMap && m->d.nT == m->d.nTiles &&
                mg_hfuse(MG_FUSE_END, m->d.nx, m->d.ny, m->d.nT, m->d.Nr);
     if (endFused)
       TIMED(K_RSTAR, launch_rstar_exch(m->d, m->p, m->f, m->d_srcOf, fuseEtaH, blocking_fields(m), m->d_halo, m->nHalo,
-                                       m->d_ctr, m->stream));
-    else if (m->p.nonlinFreeSurf > 0) TIMED(K_RSTAR, calc_r_star(m, fuseEtaH));
+                                       m->d_ctr, m->stream, etaX ? 1 : 0));
+    else if (m->p.nonlinFreeSurf > 0) TIMED(K_RSTAR, calc_r_star(m, fuseEtaH, etaX ? 1 : 0));
   } else {
     if (mgcm_integr_continuity(m)) return -1;
   }

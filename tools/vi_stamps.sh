@@ -7,8 +7,8 @@ cd "$(dirname "$0")/.."
 D=mitgcm_amd/_build/diag
 mkdir -p $D
 F="--offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -Wno-unused-result -Wno-unused-value"
-/opt/rocm/bin/hipcc $F -DMGCM_VI_STAMPS -c mitgcm_amd/csrc/kernels_dyn.hip -o $D/kernels_dyn.o
+/opt/rocm/bin/hipcc $F -DMGCM_VI_STAMPS -c mitgcm_amd/csrc/kernels_step.hip -o $D/kernels_step.o
 objs=""
-for o in mitgcm_amd/_build/*.o; do case "$(basename $o)" in kernels_dyn.o) ;; *) objs="$objs $o";; esac; done
-/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o $D/libmitgcm_amd_vistamps.so $objs $D/kernels_dyn.o
+for o in mitgcm_amd/_build/*.o; do case "$(basename $o)" in kernels_step.o) ;; *) objs="$objs $o";; esac; done
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o $D/libmitgcm_amd_vistamps.so $objs $D/kernels_step.o
 echo $D/libmitgcm_amd_vistamps.so
