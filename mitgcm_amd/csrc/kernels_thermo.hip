@@ -700,7 +700,15 @@ __device__ __forceinline__ double tracer_flat_point(const Dims &d, const Params 
 // kernel's over-fetch (616 MB HBM for 173 MB of operands on LLC-90).  Same operands, same
 // arithmetic (tracer_flat_arith): bit-identical.
 constexpr int TRM_TX = 32, TRM_TY = 8;
-__global__ void __launch_bounds__(256) k_tracer_march(Dims d, Params p, Fields f, TracerArgs a, const int *iterPtr, int KC,
+// At most 2 waves per SIMD (MGCM_TRM_WPE; tools/wpe_variant.sh builds other caps): alone the
+// k-march takes the same time at 2, 3 or 4 (HBM-bound), but beside the multi-workgroup CG2D
+// (the late join) its fourth wave per SIMD costs the solve's hand-offs more than it gains:
+// LLC-90 1.81 ms/step uncapped, 1.715 at 3, 1.714 at 2, 1.79 at 1 (profiles/r03/wpe/)
+#ifndef MGCM_TRM_WPE
+#define MGCM_TRM_WPE 2
+#endif
+#define TRM_ATTR __attribute__((amdgpu_waves_per_eu(1, MGCM_TRM_WPE)))
+__global__ void __launch_bounds__(256) TRM_ATTR k_tracer_march(Dims d, Params p, Fields f, TracerArgs a, const int *iterPtr, int KC,
                                                      int nkc, int ntx, int nty) {
   int b = mg_xcd_block();
   const int kc = b % nkc;
@@ -1046,7 +1054,12 @@ __device__ __forceinline__ void tracer_impl_body(const Dims &d, const Params &p,
   if (valid) MG_COLF_K(k) a.trNext[MG_I3(d, i, j, k, t)] = sSub[(k - 1) * NC_ + cc];
 #undef G3
 }
-__global__ void __launch_bounds__(256) k_tracer_impl(Dims d, Params p, Fields f, TracerArgs a, int nc) {
+#ifdef MGCM_TRI_WPE
+#define TRI_ATTR __attribute__((amdgpu_waves_per_eu(1, MGCM_TRI_WPE)))
+#else
+#define TRI_ATTR
+#endif
+__global__ void __launch_bounds__(256) TRI_ATTR k_tracer_impl(Dims d, Params p, Fields f, TracerArgs a, int nc) {
   tracer_impl_body(d, p, f, a, nc, mg_xcd_block());
 }
 
