@@ -933,8 +933,9 @@ __global__ void __launch_bounds__(256) k_mom_step_uv(Dims d, Params p, Fields f,
 // guCor/gvCor added to gUtmp/gVtmp (cdU/cdV from k_mom_step), and u* formed on the
 // TIMESTEP range 0..sN+1.  uNM1/vNM1 = u, v is done by k_sfp_rhs (after this kernel,
 // whose neighbours still read the old values).
-__global__ void __launch_bounds__(256) k_cd_scheme(Dims d, Params p, Fields f, const int *iterPtr) {
-  MG_PLANE(2 - d.OLx, d.nx - 2, 2 - d.OLy, d.ny - 2, z)
+__device__ __forceinline__ void cd_scheme_body(const Dims &d, const Params &p, const Fields &f, const int *iterPtr,
+                                               int lb) {
+  MG_PLANE_LB(2 - d.OLx, d.nx - 2, 2 - d.OLy, d.ny - 2, z, lb)
   const int t = d.t0 + z / d.Nr, k = z % d.Nr + 1;
   const int myIter = *iterPtr;
   const double ab15 = myIter == 0 ? 1.0 : 1.5 + p.epsAB_CD;
@@ -982,6 +983,9 @@ __global__ void __launch_bounds__(256) k_cd_scheme(Dims d, Params p, Fields f, c
   }
 #undef G2
 #undef G3
+}
+__global__ void __launch_bounds__(256) k_cd_scheme(Dims d, Params p, Fields f, const int *iterPtr) {
+  cd_scheme_body(d, p, f, iterPtr, mg_xcd_block());
 }
 
 // ---------------------------------------------------------------------------------------

@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """One step's kernel timeline from a rocprofv3 --kernel-trace csv: start offset, duration and
-the gap before each kernel, for the last complete step (steps open with FIRST, a kernel-name
-substring).   python tools/step_timeline.py <trace dir> [FIRST]"""
+the gap before each kernel, for the shortest complete step (steps open with FIRST, a
+kernel-name substring).   python tools/step_timeline.py <trace dir> [FIRST]"""
 import csv
 import glob
 import sys
@@ -16,7 +16,10 @@ def main():
     opens = [n for n, r in enumerate(rows) if first in r[2]]
     if len(opens) < 3:
         print("fewer than 3 steps found"); return
-    a, b = opens[-3], opens[-2]
+    # the shortest complete step (graph replays; bench.py's eager per-kernel timing pass
+    # synchronises around every launch)
+    spans = [(rows[opens[n + 1]][0] - rows[opens[n]][0], opens[n], opens[n + 1]) for n in range(len(opens) - 1)]
+    _, a, b = min(spans)
     t0, prev = rows[a][0], rows[a][0]
     busy = 0
     for s, e, name in rows[a:b]:
