@@ -1,11 +1,16 @@
 #!/bin/bash
-# generic A/B of an environment switch on one config: ENVVAR=name CONFIG=... STEPS=...
+# A/B of environment settings (ARMS="name:VAR=val,VAR2=val ..."; "base:" = none) on CONFIG,
+# alternating.   OUT=gpurun_out/envab
 set -o pipefail
 cd "$GRAFT_REPO_ROOT" 2>/dev/null || cd /root/repo
-mkdir -p gpurun_out/envab
-c=${CONFIG:-global_ocean.90x40x15}
-for v in 0 1 0 1 0 1; do
-  if [ $v = 1 ]; then export $ENVVAR=1; else unset $ENVVAR; fi
-  timeout -k 10 200 python bench.py --config $c --steps ${STEPS:-300} --warmup 20 --no-cpu-baseline > gpurun_out/envab/b$v.json 2> gpurun_out/envab/e$v.err || { echo fail; tail -5 gpurun_out/envab/e$v.err; exit 1; }
-  python3 -c "import json; d=json.load(open('gpurun_out/envab/b$v.json')); print('$c $ENVVAR=$v', round(d['ms_per_step'],4), round(d['value'],2))"
+OUT=${OUT:-gpurun_out/envab}
+CONFIG=${CONFIG:-llc90_synthetic}
+st=400; [ $CONFIG = global_ocean.cs32x15 ] && st=200; [ $CONFIG = llc90_synthetic ] && st=30
+mkdir -p $OUT
+for r in 1 2; do
+  for a in ${ARMS:-base:}; do
+    n=${a%%:*}; e=${a#*:}
+    env ${e//,/ } timeout -k 10 200 python bench.py --config $CONFIG --steps $st --warmup 10 --no-cpu-baseline > $OUT/b_${n}_$r.json 2> $OUT/e_${n}_$r.err || { echo "bench $n failed"; tail -5 $OUT/e_${n}_$r.err; exit 1; }
+    python3 -c "import json; d=json.load(open('$OUT/b_${n}_$r.json')); print('$CONFIG', '$n', $r, round(d['ms_per_step'],4))"
+  done
 done
