@@ -1109,8 +1109,30 @@ hipError_t launch_tracer_pair(const Dims &d, const Params &p, const Fields &f, c
   return hipGetLastError();
 }
 
+// Both tracers' implicit vertical solves in one launch (k_tracer2_impl: theta's and salt's
+// sweeps side by side per column), after the two single-tracer right-hand sides (their T* in
+// gTscr / cpScr, TracerArgs.scr).  Where it applies: both stepped, implicit diffusion, no
+// GM/Redi (k_tracer2_impl has no Kwz term).  MGCM_TRACER_IMPL2=0|1 (read per call).
+bool tracer_impl2_ok(const Params &p, const Fields &f, const TracerArgs &aT, const TracerArgs &aS) {
+  const char *e = getenv("MGCM_TRACER_IMPL2");
+  if (!e || atoi(e) == 0) return false;
+  // (multi-dimensional advection uses gTscr as its face-flux scratch: excluded)
+  return p.tempStepping && p.saltStepping && p.implicitDiffusion && !p.useGMRedi && !aT.multiDim && !aS.multiDim &&
+         aT.scr == f.gTscr && aS.scr == f.cpScr;
+}
+hipError_t launch_tracer2_impl(const Dims &d, const Params &p, const Fields &f, const TracerArgs &aT, const TracerArgs &aS,
+                               hipStream_t s) {
+  const long ncol = (long)d.sNx * d.sNy * d.nT;
+  const int nc = mg_colf_nc(ncol, d.Nr, 6);
+  MG_ALLOW_LDS(k_tracer2_impl);
+  hipLaunchKernelGGL(k_tracer2_impl, dim3(mg_colf_blocks(ncol, nc)), dim3(MG_PLANE_THREADS), mg_colf_lds(d.Nr, nc, 6), s, d,
+                     p, f, aT, aS, nc);
+  return hipGetLastError();
+}
+
+// impl = false: the right-hand side only (the implicit solve follows in launch_tracer2_impl)
 hipError_t launch_tracer_step(const Dims &d, const Params &p, const Fields &f, const TracerArgs &a, const int *iterPtr,
-                              hipStream_t s) {
+                              hipStream_t s, bool impl) {
   const dim3 blk(MG_PLANE_THREADS), grd(mg_plane_blocks(d.sNx, d.sNy, d.nT * d.Nr));
   if (a.multiDim) {
     const dim3 fgrd(mg_plane_blocks(d.nx, d.ny, d.nT * d.Nr));
@@ -1159,7 +1181,7 @@ hipError_t launch_tracer_step(const Dims &d, const Params &p, const Fields &f, c
     hipLaunchKernelGGL(k_tracer_march, dim3((unsigned)(nkc * ntx * nty * d.nT)), blk, 0, s, d, p, f, a, iterPtr, KC, nkc,
                        ntx, nty);
   } else hipLaunchKernelGGL(k_tracer_rhs_flat, grd, blk, 0, s, d, p, f, a, iterPtr);
-  if (p.implicitDiffusion) {
+  if (p.implicitDiffusion && impl) {
     const long ncol = (long)d.sNx * d.sNy * d.nT;
     const int nc = mg_colf_nc(ncol, d.Nr, 3);
     MG_ALLOW_LDS(k_tracer_impl);

@@ -59,7 +59,11 @@ hipError_t launch_rstar_exch(const Dims &, const Params &, const Fields &, const
 hipError_t launch_update_r_star_cg2d(const Dims &, const Params &, const Fields &, const long *, hipStream_t, bool sfp = false);
 hipError_t launch_halo_pack(const Dims &, const XFields &, const long *, long, double *, int, hipStream_t);
 hipError_t launch_oceanic_phys(const Dims &, const Params &, const Fields &, const int *, hipStream_t);
-hipError_t launch_tracer_step(const Dims &, const Params &, const Fields &, const TracerArgs &, const int *, hipStream_t);
+hipError_t launch_tracer_step(const Dims &, const Params &, const Fields &, const TracerArgs &, const int *, hipStream_t,
+                              bool impl = true);
+bool tracer_impl2_ok(const Params &, const Fields &, const TracerArgs &, const TracerArgs &);
+hipError_t launch_tracer2_impl(const Dims &, const Params &, const Fields &, const TracerArgs &, const TracerArgs &,
+                               hipStream_t);
 bool tracer_pair_ok(const Dims &, const Params &, const TracerArgs &, const TracerArgs &);
 bool dyn_thermo_fusable(const Dims &, const Params &, const TracerArgs &, const TracerArgs &);
 hipError_t launch_dyn_thermo(const Dims &, const Params &, const Fields &, const TracerArgs &, const TracerArgs &, const int *,
@@ -1215,6 +1219,14 @@ static int tracers_on(mgcm_model *m, hipStream_t st) {
   const TracerArgs aT = tracer_args(m, false), aS = tracer_args(m, true);
   if (tracer_pair_ok(m->d, m->p, aT, aS)) {   // both tracers in one pair of launches
     TIMED(K_TEMP, launch_tracer_pair(m->d, m->p, m->f, aT, aS, m->d_ctr, st));
+    std::swap(m->f.theta, m->f.thetaNext);
+    std::swap(m->f.salt, m->f.saltNext);
+    return 0;
+  }
+  if (tracer_impl2_ok(m->p, m->f, aT, aS)) {   // two right-hand sides, one paired implicit solve
+    TIMED(K_TEMP, launch_tracer_step(m->d, m->p, m->f, aT, m->d_ctr, st, false));
+    TIMED(K_TEMP, launch_tracer_step(m->d, m->p, m->f, aS, m->d_ctr, st, false));
+    TIMED(K_TEMP, launch_tracer2_impl(m->d, m->p, m->f, aT, aS, st));
     std::swap(m->f.theta, m->f.thetaNext);
     std::swap(m->f.salt, m->f.saltNext);
     return 0;

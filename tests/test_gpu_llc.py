@@ -18,7 +18,8 @@ import pytest
 pytestmark = pytest.mark.gpu
 
 
-@pytest.mark.parametrize("march", [None, "1:2", "1:10", "1:3:single", "vi:4", "vi:3:generic", "fuse:29", "fuse:45", "fuse:77"])
+@pytest.mark.parametrize("march", [None, "1:2", "1:10", "1:3:single", "vi:4", "vi:3:generic", "fuse:29", "fuse:45", "fuse:77",
+                                   "impl2:1", "impl2:0"])
 def test_llc30_8_steps_bitexact_vs_device_order_oracle(march, monkeypatch):
     """march = "on:KC[:single]": the tracer right-hand side as the k-march (the LLC-90
     default) with KC levels per workgroup -- 5 chunks, 1, 4 uneven -- for both tracers in one
@@ -28,8 +29,12 @@ def test_llc30_8_steps_bitexact_vs_device_order_oracle(march, monkeypatch):
     its compile-time specialisation (k_mom_vi_m2<32, 8, LLC options>) or the generic kernel.
     "fuse:MASK": the MGCM_STEP_FUSE launch fusions (29: the opt-in k_phys_phi pass; 45: the
     opt-in EXCH(cg2d_x) + etaN beside the correction step; 77: the tracers' halo exchange on
-    their own stream)."""
-    if march and march.startswith("fuse:"):   # MGCM_STEP_FUSE mask: 29 adds DO_OCEANIC_PHYS + CALC_PHI_HYD in one pass
+    their own stream).  "impl2:ON": both tracers' implicit solves in one launch
+    (k_tracer2_impl) after the single-tracer right-hand sides, k-march ON = 1 or flat 0."""
+    if march and march.startswith("impl2:"):
+        monkeypatch.setenv("MGCM_TRACER_IMPL2", "1")
+        monkeypatch.setenv("MGCM_TRACER_MARCH", march.split(":")[1])
+    elif march and march.startswith("fuse:"):   # MGCM_STEP_FUSE mask: 29 adds DO_OCEANIC_PHYS + CALC_PHI_HYD in one pass
         monkeypatch.setenv("MGCM_STEP_FUSE", march.split(":")[1])
     elif march and march.startswith("vi:"):
         monkeypatch.setenv("MGCM_VI_KERNEL", "march")
