@@ -49,6 +49,48 @@ __global__ void __launch_bounds__(256) k_dt_back(Dims d, Params p, Fields f, Tra
   else tracer_impl_body(d, p, f, aS, nc, lb - nbImp);
 }
 
+// The default layout (MGCM_DT_LAYOUT=3; 2 = front/back above): GMREDI_CALC_TENSOR leaves
+// DO_OCEANIC_PHYS' launch for the first grid (it and CALC_PHI_HYD both read only DO_OCEANIC_PHYS'
+// rhoInSitu / sigmaR), the right-hand sides (which read the tensor) move one grid later beside
+// the momentum tendencies, the implicit solves beside the CD scheme:
+//   1: GMREDI_CALC_TENSOR | CALC_PHI_HYD | del2uv
+//   2: MOM_FLUXFORM U | V | rhs(theta) | rhs(salt)
+//   3: CD_CODE_SCHEME | implicit solve (theta) | (salt)
+__global__ void __launch_bounds__(256) k_dt_l1(Dims d, Params p, Fields f, int nc, int nbGm, int nbPhi) {
+  int lb = mg_xcd_block();
+  if (lb < nbGm) { gm_tensor_body(d, p, f, lb); return; }
+  lb -= nbGm;
+  if (lb < nbPhi) { phi_hyd_body(d, p, f, nc, lb); return; }
+  del2uv_body(d, p, f, lb - nbPhi);
+}
+template <bool GM>
+__global__ void __launch_bounds__(256) k_dt_l2(Dims d, Params p, Fields f, TracerArgs aT, TracerArgs aS,
+                                               const int *iterPtr, int nbMom, int nbTr) {
+  int lb = mg_xcd_block();
+  if (lb < nbMom) {
+    if (lb & 1) mom_step_point<false, 2>(d, p, f, iterPtr, lb >> 1);
+    else mom_step_point<false, 1>(d, p, f, iterPtr, lb >> 1);
+    return;
+  }
+  lb -= nbMom;
+  if (lb < nbTr) tracer_rhs_body<GM>(d, p, f, aT, iterPtr, lb);
+  else tracer_rhs_body<GM>(d, p, f, aS, iterPtr, lb - nbTr);
+}
+__global__ void __launch_bounds__(256) k_dt_l3(Dims d, Params p, Fields f, TracerArgs aT, TracerArgs aS,
+                                               const int *iterPtr, int nc, int nbCd, int nbImp) {
+  int lb = mg_xcd_block();
+  if (lb < nbCd) { cd_scheme_body(d, p, f, iterPtr, lb); return; }
+  lb -= nbCd;
+  if (lb < nbImp) tracer_impl_body(d, p, f, aT, nc, lb);
+  else tracer_impl_body(d, p, f, aS, nc, lb - nbImp);
+}
+// whether launch_dyn_thermo runs GMREDI_CALC_TENSOR itself (one_step then launches
+// DO_OCEANIC_PHYS without it)
+bool dyn_thermo_takes_gm(const Params &p) {
+  const char *e = getenv("MGCM_DT_LAYOUT");   // read per call (A/B runs)
+  return p.useGMRedi && p.useCDscheme && !(p.implicitViscosity) && !(e && atoi(e) == 2);
+}
+
 // Where the fold is exact and applies: both tracers stepped with the per-point right-hand
 // side (GM/Redi; no multi-dimensional advection) and the implicit vertical solve, flux-form
 // momentum split into U and V halves, on the small grids (mg_hfuse: <= 2^21 points), and
@@ -73,6 +115,22 @@ hipError_t launch_dyn_thermo(const Dims &d, const Params &p, const Fields &f, co
   const int nbPhi = (int)mg_colf_blocks(ncolPhi, ncPhi);
   const int nbDel = del2_needed(p) ? (int)mg_plane_blocks(d.nx, d.ny, d.nT * d.Nr) : 0;
   const int nbTr = (int)mg_plane_blocks(d.sNx, d.sNy, d.nT * d.Nr);
+  if (dyn_thermo_takes_gm(p)) {
+    const int nbGm = (int)mg_plane_blocks(d.nx - 2, d.ny - 2, d.nT * d.Nr);
+    MG_ALLOW_LDS(k_dt_l1);
+    hipLaunchKernelGGL(k_dt_l1, dim3((unsigned)(nbGm + nbPhi + nbDel)), blk, mg_colf_lds(d.Nr, ncPhi, nArrPhi), s, d, p, f,
+                       ncPhi, nbGm, nbPhi);
+    const int nbMom = 2 * (int)mg_plane_blocks(d.nx, d.ny, d.nT * d.Nr);
+    hipLaunchKernelGGL(k_dt_l2<true>, dim3((unsigned)(nbMom + 2 * nbTr)), blk, 0, s, d, p, f, aT, aS, iterPtr, nbMom, nbTr);
+    const long ncolTr = (long)d.sNx * d.sNy * d.nT;
+    const int ncTr = mg_colf_nc(ncolTr, d.Nr, 3);
+    const int nbImp = (int)mg_colf_blocks(ncolTr, ncTr);
+    const int nbCd = (int)mg_plane_blocks(d.nx - 2, d.ny - 2, d.nT * d.Nr);
+    MG_ALLOW_LDS(k_dt_l3);
+    hipLaunchKernelGGL(k_dt_l3, dim3((unsigned)(nbCd + 2 * nbImp)), blk, mg_colf_lds(d.Nr, ncTr, 3), s, d, p, f, aT, aS,
+                       iterPtr, ncTr, nbCd, nbImp);
+    return hipGetLastError();
+  }
   MG_ALLOW_LDS(k_dt_front<true>);
   hipLaunchKernelGGL(k_dt_front<true>, dim3((unsigned)(nbPhi + nbDel + 2 * nbTr)), blk,
                      mg_colf_lds(d.Nr, ncPhi, nArrPhi), s, d, p, f, aT, aS, iterPtr, ncPhi, nbPhi, nbDel, nbTr);

@@ -57,8 +57,8 @@ __device__ __forceinline__ void gm_slope_gkw91(const Params &p, double dSx, doub
   else if (SlopeSqr > maxSlopeSqr && SlopeSqr < p.GM_slopeSqCutoff) taper = maxSlopeSqr / SlopeSqr;
 }
 
-__global__ void __launch_bounds__(256) k_gm_tensor(Dims d, Params p, Fields f) {
-  MG_PLANE(2 - d.OLx, d.nx - 2, 2 - d.OLy, d.ny - 2, z)
+__device__ __forceinline__ void gm_tensor_body(const Dims &d, const Params &p, const Fields &f, int lb) {
+  MG_PLANE_LB(2 - d.OLx, d.nx - 2, 2 - d.OLy, d.ny - 2, z, lb)
   const int t = d.t0 + z / d.Nr, k = z % d.Nr + 1;
   const int Nr = d.Nr;
   auto rho = [&](int ii, int jj, int kk) { return f.rhoInSitu[MG_I3(d, ii, jj, kk, t)]; };
@@ -138,6 +138,7 @@ __global__ void __launch_bounds__(256) k_gm_tensor(Dims d, Params p, Fields f) {
     f.GM_PsiY[q3] = psy;
   }
 }
+__global__ void __launch_bounds__(256) k_gm_tensor(Dims d, Params p, Fields f) { gm_tensor_body(d, p, f, mg_xcd_block()); }
 
 // ---------------------------------------------------------------------------
 // GAD_DST3FL_ADV_X/Y/R (gad_dst3fl_adv_x.F:47-99, _y.F, _r.F:70-119)
@@ -1063,10 +1064,11 @@ __global__ void __launch_bounds__(256) TRI_ATTR k_tracer_impl(Dims d, Params p, 
   tracer_impl_body(d, p, f, a, nc, mg_xcd_block());
 }
 
-hipError_t launch_oceanic_phys(const Dims &d, const Params &p, const Fields &f, const int *iterPtr, hipStream_t s) {
+// gm = false: without GMREDI_CALC_TENSOR (it then rides in the next launch, launch_dyn_thermo)
+hipError_t launch_oceanic_phys(const Dims &d, const Params &p, const Fields &f, const int *iterPtr, hipStream_t s, bool gm) {
   hipLaunchKernelGGL(k_oceanic_phys, dim3(mg_plane_blocks(d.nx, d.ny, d.nT * d.Nr)), dim3(MG_PLANE_THREADS), 0, s, d, p,
                      f, iterPtr);
-  if (p.useGMRedi)
+  if (p.useGMRedi && gm)
     hipLaunchKernelGGL(k_gm_tensor, dim3(mg_plane_blocks(d.nx - 2, d.ny - 2, d.nT * d.Nr)), dim3(MG_PLANE_THREADS), 0,
                        s, d, p, f);
   return hipGetLastError();

@@ -58,7 +58,7 @@ hipError_t launch_rstar_exch(const Dims &, const Params &, const Fields &, const
                              int, int *, hipStream_t, int fromX = 0);
 hipError_t launch_update_r_star_cg2d(const Dims &, const Params &, const Fields &, const long *, hipStream_t, bool sfp = false);
 hipError_t launch_halo_pack(const Dims &, const XFields &, const long *, long, double *, int, hipStream_t);
-hipError_t launch_oceanic_phys(const Dims &, const Params &, const Fields &, const int *, hipStream_t);
+hipError_t launch_oceanic_phys(const Dims &, const Params &, const Fields &, const int *, hipStream_t, bool gm = true);
 hipError_t launch_tracer_step(const Dims &, const Params &, const Fields &, const TracerArgs &, const int *, hipStream_t,
                               bool impl = true);
 bool tracer_impl2_ok(const Params &, const Fields &, const TracerArgs &, const TracerArgs &);
@@ -68,6 +68,7 @@ bool tracer_pair_ok(const Dims &, const Params &, const TracerArgs &, const Trac
 bool dyn_thermo_fusable(const Dims &, const Params &, const TracerArgs &, const TracerArgs &);
 hipError_t launch_dyn_thermo(const Dims &, const Params &, const Fields &, const TracerArgs &, const TracerArgs &, const int *,
                              hipStream_t);
+bool dyn_thermo_takes_gm(const Params &);
 hipError_t launch_tracer_pair(const Dims &, const Params &, const Fields &, const TracerArgs &, const TracerArgs &,
                               const int *, hipStream_t);
 hipError_t launch_mon_stats(const Dims &, const MonSpecs &, int, double *, int, hipStream_t);
@@ -1437,7 +1438,8 @@ static int one_step(mgcm_model *m) {
   const bool physPhi = !stagger && m->p.momStepping && phys_phi_fusable(m->d, m->p);
   auto phys = [&]() -> int {
     if (physPhi) TIMED(K_PHYS, launch_phys_phi(m->d, m->p, m->f, m->d_ctr, m->stream));
-    else TIMED(K_PHYS, launch_oceanic_phys(m->d, m->p, m->f, m->d_ctr, m->stream));
+    // (GMREDI_CALC_TENSOR in launch_dyn_thermo's first grid when it takes it)
+    else TIMED(K_PHYS, launch_oceanic_phys(m->d, m->p, m->f, m->d_ctr, m->stream, !(dtFused && dyn_thermo_takes_gm(m->p))));
     return 0;
   };
   if (stagger || fork) {
