@@ -101,18 +101,77 @@ bool dyn_thermo_fusable(const Dims &d, const Params &p, const TracerArgs &aT, co
          !getenv("MGCM_MOM_NOSPLIT") && aT.scr != aS.scr;
 }
 
+// CALC_PHI_HYD's column frame as launch_phi_hyd sizes it
+static void phi_frame(const Dims &d, const Params &p, int &nc, int &nArr, int &nb) {
+  const long ncol = (long)(d.sNx + 3) * (d.sNy + 3) * d.nT;
+  nArr = (p.nonlinFreeSurf > 0 && p.select_rStar > 0) ? 6 : 3;
+  const int ncEnv = getenv("MGCM_PHI_NC") ? atoi(getenv("MGCM_PHI_NC")) : 0;
+  nc = (ncEnv == 16 || ncEnv == 32 || ncEnv == 64) ? ncEnv : mg_colf_nc(ncol, d.Nr, nArr);
+  nb = (int)mg_colf_blocks(ncol, nc);
+}
+
+// Outside the fold (e.g. the staggered step): GMREDI_CALC_TENSOR beside CALC_PHI_HYD (+ del2uv
+// where it shares phi's grid, phi_del2_fused) in k_dt_l1 -- both read only DO_OCEANIC_PHYS'
+// output -- on the small grids; DO_OCEANIC_PHYS then launches without the tensor
+bool gm_phi_fusable(const Dims &d, const Params &p) {
+  return mg_hfuse(MG_FUSE_DT, d.nx, d.ny, d.nT, d.Nr) && p.useGMRedi && p.momStepping;
+}
+hipError_t launch_gm_phi(const Dims &d, const Params &p, const Fields &f, hipStream_t s) {
+  int nc, nArr, nbPhi;
+  phi_frame(d, p, nc, nArr, nbPhi);
+  const int nbGm = (int)mg_plane_blocks(d.nx - 2, d.ny - 2, d.nT * d.Nr);
+  const int nbDel = phi_del2_fused(d, p) ? (int)mg_plane_blocks(d.nx, d.ny, d.nT * d.Nr) : 0;
+  MG_ALLOW_LDS(k_dt_l1);
+  hipLaunchKernelGGL(k_dt_l1, dim3((unsigned)(nbGm + nbPhi + nbDel)), dim3(256), mg_colf_lds(d.Nr, nc, nArr), s, d, p, f,
+                     nc, nbGm, nbPhi);
+  return hipGetLastError();
+}
+
+// Both tracers of THERMODYNAMICS in two launches instead of four (small grids, outside the
+// fold, e.g. after the pressure solve in the staggered step): [rhs(theta) | rhs(salt)], then
+// [implicit solve (theta) | (salt)]; theta's T* in gTscr, salt's in cpScr
+template <bool GM>
+__global__ void __launch_bounds__(256) k_tr_rhs_pair(Dims d, Params p, Fields f, TracerArgs aT, TracerArgs aS,
+                                                     const int *iterPtr, int nbTr) {
+  const int lb = mg_xcd_block();
+  if (lb < nbTr) tracer_rhs_body<GM>(d, p, f, aT, iterPtr, lb);
+  else tracer_rhs_body<GM>(d, p, f, aS, iterPtr, lb - nbTr);
+}
+__global__ void __launch_bounds__(256) k_tr_impl_pair(Dims d, Params p, Fields f, TracerArgs aT, TracerArgs aS, int nc,
+                                                      int nbImp) {
+  const int lb = mg_xcd_block();
+  if (lb < nbImp) tracer_impl_body(d, p, f, aT, nc, lb);
+  else tracer_impl_body(d, p, f, aS, nc, lb - nbImp);
+}
+bool tracer_hpair_ok(const Dims &d, const Params &p, const TracerArgs &aT, const TracerArgs &aS) {
+  return mg_hfuse(MG_FUSE_DT, d.nx, d.ny, d.nT, d.Nr) && p.tempStepping && p.saltStepping && p.implicitDiffusion &&
+         !aT.multiDim && !aS.multiDim && aT.scr != aS.scr && !tracer_march_on(d);
+}
+hipError_t launch_tracer_hpair(const Dims &d, const Params &p, const Fields &f, const TracerArgs &aT, const TracerArgs &aS,
+                               const int *iterPtr, hipStream_t s) {
+  const int nbTr = (int)mg_plane_blocks(d.sNx, d.sNy, d.nT * d.Nr);
+  // (without GM/Redi k_tracer_rhs<false>'s body: bit-identical to the flat kernel the single
+  // path runs)
+  if (p.useGMRedi) hipLaunchKernelGGL(k_tr_rhs_pair<true>, dim3((unsigned)(2 * nbTr)), dim3(256), 0, s, d, p, f, aT, aS,
+                                      iterPtr, nbTr);
+  else hipLaunchKernelGGL(k_tr_rhs_pair<false>, dim3((unsigned)(2 * nbTr)), dim3(256), 0, s, d, p, f, aT, aS, iterPtr, nbTr);
+  const long ncol = (long)d.sNx * d.sNy * d.nT;
+  const int nc = mg_colf_nc(ncol, d.Nr, 3);
+  const int nbImp = (int)mg_colf_blocks(ncol, nc);
+  MG_ALLOW_LDS(k_tr_impl_pair);
+  hipLaunchKernelGGL(k_tr_impl_pair, dim3((unsigned)(2 * nbImp)), dim3(256), mg_colf_lds(d.Nr, nc, 3), s, d, p, f, aT, aS, nc,
+                     nbImp);
+  return hipGetLastError();
+}
+
 // CALC_PHI_HYD + THERMODYNAMICS' tracers + DYNAMICS in three launches on one stream
 // (after DO_OCEANIC_PHYS; dyn_thermo_fusable must hold)
 hipError_t launch_dyn_thermo(const Dims &d, const Params &p, const Fields &f, const TracerArgs &aT, const TracerArgs &aS,
                              const int *iterPtr, hipStream_t s) {
   const dim3 blk(256);
   // front: phi's column frame (launch_phi_hyd's columns and LDS), del2uv's and the tracers' planes
-  const long ncolPhi = (long)(d.sNx + 3) * (d.sNy + 3) * d.nT;
-  const bool rstar = p.nonlinFreeSurf > 0 && p.select_rStar > 0;
-  const int nArrPhi = rstar ? 6 : 3;
-  const int ncEnv = getenv("MGCM_PHI_NC") ? atoi(getenv("MGCM_PHI_NC")) : 0;
-  const int ncPhi = (ncEnv == 16 || ncEnv == 32 || ncEnv == 64) ? ncEnv : mg_colf_nc(ncolPhi, d.Nr, nArrPhi);
-  const int nbPhi = (int)mg_colf_blocks(ncolPhi, ncPhi);
+  int ncPhi, nArrPhi, nbPhi;
+  phi_frame(d, p, ncPhi, nArrPhi, nbPhi);
   const int nbDel = del2_needed(p) ? (int)mg_plane_blocks(d.nx, d.ny, d.nT * d.Nr) : 0;
   const int nbTr = (int)mg_plane_blocks(d.sNx, d.sNy, d.nT * d.Nr);
   if (dyn_thermo_takes_gm(p)) {

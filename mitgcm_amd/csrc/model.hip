@@ -69,6 +69,11 @@ bool dyn_thermo_fusable(const Dims &, const Params &, const TracerArgs &, const 
 hipError_t launch_dyn_thermo(const Dims &, const Params &, const Fields &, const TracerArgs &, const TracerArgs &, const int *,
                              hipStream_t);
 bool dyn_thermo_takes_gm(const Params &);
+bool gm_phi_fusable(const Dims &, const Params &);
+hipError_t launch_gm_phi(const Dims &, const Params &, const Fields &, hipStream_t);
+bool tracer_hpair_ok(const Dims &, const Params &, const TracerArgs &, const TracerArgs &);
+hipError_t launch_tracer_hpair(const Dims &, const Params &, const Fields &, const TracerArgs &, const TracerArgs &,
+                               const int *, hipStream_t);
 hipError_t launch_tracer_pair(const Dims &, const Params &, const Fields &, const TracerArgs &, const TracerArgs &,
                               const int *, hipStream_t);
 hipError_t launch_mon_stats(const Dims &, const MonSpecs &, int, double *, int, hipStream_t);
@@ -1224,6 +1229,12 @@ static int tracers_on(mgcm_model *m, hipStream_t st) {
     std::swap(m->f.salt, m->f.saltNext);
     return 0;
   }
+  if (tracer_hpair_ok(m->d, m->p, aT, aS)) {   // small grids: both tracers per launch
+    TIMED(K_TEMP, launch_tracer_hpair(m->d, m->p, m->f, aT, aS, m->d_ctr, st));
+    std::swap(m->f.theta, m->f.thetaNext);
+    std::swap(m->f.salt, m->f.saltNext);
+    return 0;
+  }
   if (tracer_impl2_ok(m->p, m->f, aT, aS)) {   // two right-hand sides, one paired implicit solve
     TIMED(K_TEMP, launch_tracer_step(m->d, m->p, m->f, aT, m->d_ctr, st, false));
     TIMED(K_TEMP, launch_tracer_step(m->d, m->p, m->f, aS, m->d_ctr, st, false));
@@ -1436,10 +1447,14 @@ static int one_step(mgcm_model *m) {
   // THERMODYNAMICS, between them in FORWARD_STEP, reads DO_OCEANIC_PHYS's output and writes
   // nothing CALC_PHI_HYD reads)
   const bool physPhi = !stagger && m->p.momStepping && phys_phi_fusable(m->d, m->p);
+  // GMREDI_CALC_TENSOR beside CALC_PHI_HYD (launch_gm_phi) where THERMODYNAMICS, its reader,
+  // runs after DYNAMICS (staggered, or forked after DYNAMICS) and the fold does not apply
+  const bool gmPhi = (stagger || thermoLate) && !dtFused && !physPhi && !m->timing && gm_phi_fusable(m->d, m->p);
   auto phys = [&]() -> int {
     if (physPhi) TIMED(K_PHYS, launch_phys_phi(m->d, m->p, m->f, m->d_ctr, m->stream));
     // (GMREDI_CALC_TENSOR in launch_dyn_thermo's first grid when it takes it)
-    else TIMED(K_PHYS, launch_oceanic_phys(m->d, m->p, m->f, m->d_ctr, m->stream, !(dtFused && dyn_thermo_takes_gm(m->p))));
+    else TIMED(K_PHYS, launch_oceanic_phys(m->d, m->p, m->f, m->d_ctr, m->stream,
+                                           !(dtFused && dyn_thermo_takes_gm(m->p)) && !gmPhi));
     return 0;
   };
   if (stagger || fork) {
@@ -1454,7 +1469,10 @@ static int one_step(mgcm_model *m) {
       std::swap(m->f.theta, m->f.thetaNext);   // CYCLE_TRACER: the new tracers are the other buffers
       std::swap(m->f.salt, m->f.saltNext);
     } else if (physPhi) TIMED(K_MOM, launch_mom_step(m->d, m->p, m->f, m->d_ctr, m->stream));
-    else if (mgcm_dynamics(m)) return -1;
+    else if (gmPhi) {
+      TIMED(K_PHI, launch_gm_phi(m->d, m->p, m->f, m->stream));
+      TIMED(K_MOM, launch_mom_step(m->d, m->p, m->f, m->d_ctr, m->stream));
+    } else if (mgcm_dynamics(m)) return -1;
     if (thermoLate && thermoAtEnv == 1 && fork_thermo()) return -1;
     if (fork && !lateJoin && !dtFused) HIPCHK(hipStreamWaitEvent(m->stream, m->evJoin, 0));
     // forward_step.F:829-877: UPDATE_R_STAR(.TRUE.) + UPDATE_CG2D

@@ -105,9 +105,15 @@ def test_cs32x15_dynamics_vecinv_viscous_rstar_bitexact():
     assert not bad, bad
 
 
-def test_cs32x15_8_steps_vs_oracle():
+@pytest.mark.parametrize("fuse", [None, "269"])
+def test_cs32x15_8_steps_vs_oracle(monkeypatch, fuse):
     """8 steps: bit for bit against the oracle summing CG2D in the device's order; against
-    the reference summation order (6 tile partials in tile order) >= 10 digits."""
+    the reference summation order (6 tile partials in tile order) >= 10 digits.  fuse None:
+    the default step (GMREDI_CALC_TENSOR beside CALC_PHI_HYD, both tracers per launch);
+    "269": MGCM_STEP_FUSE without MG_FUSE_DT (the tensor in DO_OCEANIC_PHYS' launch, one
+    tracer per launch)."""
+    if fuse:
+        monkeypatch.setenv("MGCM_STEP_FUSE", fuse)
     o, g = _oracle(0)
     m = _model()
     plan, NT, PPT, NG = m.cg2d_sum_plan()
