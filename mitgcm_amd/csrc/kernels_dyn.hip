@@ -212,6 +212,45 @@ __device__ __forceinline__ void phi_hyd_body(const Dims &d, const Params &p, con
 __global__ void __launch_bounds__(256) k_phi_hyd(Dims d, Params p, Fields f, int nc) {
   phi_hyd_body(d, p, f, nc, mg_xcd_block());
 }
+// CALC_PHI_HYD without r* and without the quasi-hydrostatic terms (phi_hyd_body's other
+// cases), one thread per column of 0..sNx+1 x 0..sNy+1, consecutive threads along i: the
+// column's rhoInSitu is fetched PHI_CH levels at a time, every load of a chunk in flight
+// before the chunk's sequential sum, and phiHydC / totPhiHyd stored as the sum passes --
+// no LDS, no barrier, no thread idle during the serial part.  The same expressions in the
+// same order as phi_hyd_body: bit-identical.
+constexpr int PHI_CH = 10;
+__global__ void __launch_bounds__(256) k_phi_flat(Dims d, Params p, Fields f) {
+  const int W = d.sNx + 2, H = d.sNy + 2;
+  const long col = (long)mg_xcd_block() * 256 + threadIdx.x, npl = (long)W * H;
+  if (col >= npl * d.nT) return;
+  const int t = d.t0 + (int)(col / npl), r = (int)(col % npl);
+  const int i = r % W, j = r / W;
+  const int Nr = d.Nr;
+  const double recip_rhoConst = 1.0 / p.rhoConst;
+  const long q2 = MG_I2(d, i, j, t);
+  const double bEta = p.storePhiHyd4Phys ? f.Bo_surf[q2] * f.etaN[q2] : 0.0;
+  double phF = 0.0;
+  for (int k0 = 1; k0 <= Nr; k0 += PHI_CH) {
+    double a[PHI_CH];
+#pragma unroll
+    for (int c = 0; c < PHI_CH; c++) a[c] = k0 + c <= Nr ? f.rhoInSitu[MG_I3(d, i, j, k0 + c, t)] : 0.0;
+#pragma unroll
+    for (int c = 0; c < PHI_CH; c++) {
+      const int k = k0 + c;
+      if (k > Nr) continue;
+      double dRlocM = 0.5 * f.drC[k - 1];
+      if (k == 1) dRlocM = f.rF[0] - f.rC[0];
+      const double dRlocP = (k == Nr) ? (f.rC[k - 1] - f.rF[k]) : 0.5 * f.drC[k];
+      const double sM = dRlocM * p.gravity * a[c] * recip_rhoConst;
+      const double sP = dRlocP * p.gravity * a[c] * recip_rhoConst;
+      const double phC = phF + sM;
+      phF = phC + sP;
+      const long q3 = MG_I3(d, i, j, k, t);
+      f.phiHydC[q3] = phC;
+      if (p.storePhiHyd4Phys) f.totPhiHyd[q3] = phC + bEta + 0.0;
+    }
+  }
+}
 __global__ void __launch_bounds__(256) k_phys_phi(Dims d, Params p, Fields f, int nc, const int *iterPtr) {
   phi_hyd_body<true>(d, p, f, nc, mg_xcd_block(), iterPtr);
 }
@@ -2188,6 +2227,14 @@ hipError_t launch_phi_hyd(const Dims &d, const Params &p, const Fields &f, hipSt
     MG_ALLOW_LDS(k_phi_del2);
     const unsigned nbPhi = mg_colf_blocks(ncol, nc), nbDel = mg_plane_blocks(d.nx, d.ny, d.nT * d.Nr);
     hipLaunchKernelGGL(k_phi_del2, dim3(nbPhi + nbDel), dim3(256), mg_colf_lds(d.Nr, nc, nArr), s, d, p, f, nc, (int)nbPhi);
+    return hipGetLastError();
+  }
+  // the flat per-column form where it applies (MGCM_PHI_FLAT=0 keeps the column frame)
+  const bool qh = p.quasiHydrostatic && (p.select3dCoriScheme >= 1 || p.useNHMTerms);
+  const char *fe = getenv("MGCM_PHI_FLAT");
+  if (!rstar && !qh && !(fe && atoi(fe) == 0)) {
+    const long ncolF = (long)(d.sNx + 2) * (d.sNy + 2) * d.nT;
+    hipLaunchKernelGGL(k_phi_flat, dim3((unsigned)((ncolF + 255) / 256)), dim3(256), 0, s, d, p, f);
     return hipGetLastError();
   }
   MG_ALLOW_LDS(k_phi_hyd);
