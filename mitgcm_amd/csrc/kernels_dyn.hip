@@ -212,44 +212,128 @@ __device__ __forceinline__ void phi_hyd_body(const Dims &d, const Params &p, con
 __global__ void __launch_bounds__(256) k_phi_hyd(Dims d, Params p, Fields f, int nc) {
   phi_hyd_body(d, p, f, nc, mg_xcd_block());
 }
-// CALC_PHI_HYD without r* and without the quasi-hydrostatic terms (phi_hyd_body's other
-// cases), one thread per column of 0..sNx+1 x 0..sNy+1, consecutive threads along i: the
-// column's rhoInSitu is fetched PHI_CH levels at a time, every load of a chunk in flight
-// before the chunk's sequential sum, and phiHydC / totPhiHyd stored as the sum passes --
-// no LDS, no barrier, no thread idle during the serial part.  The same expressions in the
-// same order as phi_hyd_body: bit-identical.
-constexpr int PHI_CH = 10;
-__global__ void __launch_bounds__(256) k_phi_flat(Dims d, Params p, Fields f) {
-  const int W = d.sNx + 2, H = d.sNy + 2;
-  const long col = (long)mg_xcd_block() * 256 + threadIdx.x, npl = (long)W * H;
+// CALC_PHI_HYD as a flat per-column pass (phi_hyd_body's non-PHYS cases; RS = r*, QH = the
+// quasi-hydrostatic buoyancy terms): one thread per column, consecutive threads along i,
+// over phi_hyd_body's columns (-1..sN+1 under r*, whose dWtrans the west/south neighbours
+// need; 0..sN+1 otherwise).  The column's operands are fetched PHI_CH levels at a time, every
+// load of a chunk in flight before the chunk's sequential sums, and each level's results
+// stored as the sums pass -- no LDS staging, no barrier, no thread idle while one thread per
+// column sums.  The same expressions in the same order as phi_hyd_body: bit-identical.
+constexpr int PHI_CH = 10;   // levels per chunk (5 with the r* / QH operands)
+template <bool RS, bool QH>
+__device__ __forceinline__ void phi_flat_body(const Dims &d, const Params &p, const Fields &f, int lb) {
+  constexpr int o = RS ? 1 : 0;
+  const int W = d.sNx + 2 + o, H = d.sNy + 2 + o;
+  const long col = (long)lb * 256 + threadIdx.x, npl = (long)W * H;
   if (col >= npl * d.nT) return;
   const int t = d.t0 + (int)(col / npl), r = (int)(col % npl);
-  const int i = r % W, j = r / W;
+  const int i = r % W - o, j = r / W - o;
+  const bool ring = i >= 0 && j >= 0;
   const int Nr = d.Nr;
+  constexpr int CH = (RS || QH) ? 5 : PHI_CH;   // (8 operand arrays per level under r* + QH)
   const double recip_rhoConst = 1.0 / p.rhoConst;
+  const double scalingFactor = p.rhoConst * p.gravitySign * (1.0 / p.gravity);
   const long q2 = MG_I2(d, i, j, t);
-  const double bEta = p.storePhiHyd4Phys ? f.Bo_surf[q2] * f.etaN[q2] : 0.0;
+  // MOM_CALC_RTRANS's recurrences (phi_hyd_body: d0 and the k2 loop)
+  double c = 0.0, u = 0.0, v = 0.0, dCdt = 0.0, dWdt = 0.0, dSdt = 0.0, rA = 0.0, rAw = 0.0, rAs = 0.0;
+  if (RS) {
+    auto d0 = [&](long rr) { return f.rStarDhCDt[rr] * (f.Ro_surf[rr] - f.R_low[rr]) * f.rA[rr]; };
+    c = d0(q2);
+    u = ring ? 0.5 * (d0(q2 - 1) + c) : 0.0;
+    v = ring ? 0.5 * (d0(q2 - d.nx) + c) : 0.0;
+    dCdt = f.rStarDhCDt[q2]; rA = f.rA[q2];
+    if (ring) { dWdt = f.rStarDhWDt[q2]; dSdt = f.rStarDhSDt[q2]; rAw = f.rAw[q2]; rAs = f.rAs[q2]; }
+  }
+  const bool tot = p.storePhiHyd4Phys && ring;
+  const bool totR = RS && p.nonlinFreeSurf >= 4;
+  const double bEta = tot && !totR ? f.Bo_surf[q2] * f.etaN[q2] : 0.0;
+  const double fac = tot && totR ? f.rStarFacC[q2] : 0.0, roS = tot && totR ? f.Ro_surf[q2] : 0.0;
+  const double fCos = QH ? f.fCoriCos[q2] : 0.0;
   double phF = 0.0;
-  for (int k0 = 1; k0 <= Nr; k0 += PHI_CH) {
-    double a[PHI_CH];
+  for (int k0 = 1; k0 <= Nr; k0 += CH) {
+    double a[CH], u0[CH], u1[CH], v0[CH], v1[CH], hC[CH], hW[CH], hS[CH];
 #pragma unroll
-    for (int c = 0; c < PHI_CH; c++) a[c] = k0 + c <= Nr ? f.rhoInSitu[MG_I3(d, i, j, k0 + c, t)] : 0.0;
+    for (int cc = 0; cc < CH; cc++) {
+      const int k = k0 + cc <= Nr ? k0 + cc : Nr;   // (clamped: the extra levels are not used)
+      const long q3 = MG_I3(d, i, j, k, t);
+      a[cc] = f.rhoInSitu[q3];
+      if (QH) {
+        u0[cc] = f.uVel[q3]; u1[cc] = f.uVel[MG_I3(d, i + 1, j, k, t)];
+        v0[cc] = f.vVel[q3]; v1[cc] = f.vVel[MG_I3(d, i, j + 1, k, t)];
+      }
+      if (RS) {
+        hC[cc] = f.h0FacC[q3];
+        if (ring) { hW[cc] = f.h0FacW[q3]; hS[cc] = f.h0FacS[q3]; }
+      }
+    }
 #pragma unroll
-    for (int c = 0; c < PHI_CH; c++) {
-      const int k = k0 + c;
+    for (int cc = 0; cc < CH; cc++) {
+      const int k = k0 + cc;
       if (k > Nr) continue;
+      const long q3 = MG_I3(d, i, j, k, t);
       double dRlocM = 0.5 * f.drC[k - 1];
       if (k == 1) dRlocM = f.rF[0] - f.rC[0];
       const double dRlocP = (k == Nr) ? (f.rC[k - 1] - f.rF[k]) : 0.5 * f.drC[k];
-      const double sM = dRlocM * p.gravity * a[c] * recip_rhoConst;
-      const double sP = dRlocP * p.gravity * a[c] * recip_rhoConst;
+      double al = a[cc];
+      if (QH) {
+        double gW = 0.0;
+        if (p.select3dCoriScheme >= 1) gW = fCos * (1.0 * 0.5 * (u0[cc] + u1[cc]) - 0.0 * 0.5 * (v0[cc] + v1[cc]));
+        if (p.useNHMTerms)
+          gW = gW + ((u0[cc] * u0[cc] + u1[cc] * u1[cc]) + (v0[cc] * v0[cc] + v1[cc] * v1[cc])) * 0.5 * p.recip_rSphere;
+        al = al + scalingFactor * gW;
+      }
+      if (RS) f.alphaRho[q3] = al;
+      const double sM = dRlocM * p.gravity * al * recip_rhoConst;
+      const double sP = dRlocP * p.gravity * al * recip_rhoConst;
       const double phC = phF + sM;
       phF = phC + sP;
-      const long q3 = MG_I3(d, i, j, k, t);
-      f.phiHydC[q3] = phC;
-      if (p.storePhiHyd4Phys) f.totPhiHyd[q3] = phC + bEta + 0.0;
+      if (RS) {
+        const double drF = f.drF[k - 1];
+        const double cc2 = dCdt * drF * hC[cc] * rA;
+        f.dWtC[q3] = c;
+        c = c - cc2;
+        if (ring) {
+          const double uu = dWdt * drF * hW[cc] * rAw, vv = dSdt * drF * hS[cc] * rAs;
+          f.dWtU[q3] = u;
+          f.dWtV[q3] = v;
+          u = u - uu;
+          v = v - vv;
+        }
+      }
+      if (ring) {
+        f.phiHydC[q3] = phC;
+        if (tot) {
+          if (totR) {
+            const double dPhiRef = (roS - f.rC[k - 1]) * p.gravity;
+            f.totPhiHyd[q3] = phC * fac + fmax(dPhiRef, 0.0) * (fac - 1.0) + 0.0;
+          } else {
+            f.totPhiHyd[q3] = phC + bEta + 0.0;
+          }
+        }
+      }
     }
   }
+}
+template <bool RS, bool QH>
+__global__ void __launch_bounds__(256) k_phi_flat(Dims d, Params p, Fields f) {
+  phi_flat_body<RS, QH>(d, p, f, mg_xcd_block());
+}
+// whether CALC_PHI_HYD runs the flat pass: by default where neither r* nor the QH terms add
+// their per-level operands (LLC-90: 63 -> 30 us; with them, on the small r* grids, the one
+// serial thread per column is slower than the column frame: config 2 0.319 against 0.309
+// ms/step, config 3 0.414 against 0.411, profiles/r03/phiflat/).  MGCM_PHI_FLAT=0 never,
+// 2 always (read per launch)
+inline bool phi_flat_on(const Params &p) {
+  const char *e = getenv("MGCM_PHI_FLAT");
+  const int v = e ? atoi(e) : 1;
+  if (v == 0 || v == 2) return v == 2;
+  const bool rs = p.nonlinFreeSurf > 0 && p.select_rStar > 0;
+  const bool qh = p.quasiHydrostatic && (p.select3dCoriScheme >= 1 || p.useNHMTerms);
+  return !rs && !qh;
+}
+inline int phi_flat_blocks(const Dims &d, const Params &p) {
+  const int o = (p.nonlinFreeSurf > 0 && p.select_rStar > 0) ? 1 : 0;
+  return (int)(((long)(d.sNx + 2 + o) * (d.sNy + 2 + o) * d.nT + 255) / 256);
 }
 __global__ void __launch_bounds__(256) k_phys_phi(Dims d, Params p, Fields f, int nc, const int *iterPtr) {
   phi_hyd_body<true>(d, p, f, nc, mg_xcd_block(), iterPtr);
@@ -2229,12 +2313,12 @@ hipError_t launch_phi_hyd(const Dims &d, const Params &p, const Fields &f, hipSt
     hipLaunchKernelGGL(k_phi_del2, dim3(nbPhi + nbDel), dim3(256), mg_colf_lds(d.Nr, nc, nArr), s, d, p, f, nc, (int)nbPhi);
     return hipGetLastError();
   }
-  // the flat per-column form where it applies (MGCM_PHI_FLAT=0 keeps the column frame)
-  const bool qh = p.quasiHydrostatic && (p.select3dCoriScheme >= 1 || p.useNHMTerms);
-  const char *fe = getenv("MGCM_PHI_FLAT");
-  if (!rstar && !qh && !(fe && atoi(fe) == 0)) {
-    const long ncolF = (long)(d.sNx + 2) * (d.sNy + 2) * d.nT;
-    hipLaunchKernelGGL(k_phi_flat, dim3((unsigned)((ncolF + 255) / 256)), dim3(256), 0, s, d, p, f);
+  // the flat per-column form (phi_flat_on)
+  if (phi_flat_on(p)) {
+    const bool qh = p.quasiHydrostatic && (p.select3dCoriScheme >= 1 || p.useNHMTerms);
+    auto kern = rstar ? (qh ? k_phi_flat<true, true> : k_phi_flat<true, false>)
+                      : (qh ? k_phi_flat<false, true> : k_phi_flat<false, false>);
+    hipLaunchKernelGGL(kern, dim3((unsigned)phi_flat_blocks(d, p)), dim3(256), 0, s, d, p, f);
     return hipGetLastError();
   }
   MG_ALLOW_LDS(k_phi_hyd);

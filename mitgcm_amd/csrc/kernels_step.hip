@@ -63,6 +63,34 @@ __global__ void __launch_bounds__(256) k_dt_l1(Dims d, Params p, Fields f, int n
   if (lb < nbPhi) { phi_hyd_body(d, p, f, nc, lb); return; }
   del2uv_body(d, p, f, lb - nbPhi);
 }
+static void phi_frame(const Dims &d, const Params &p, int &nc, int &nArr, int &nb);
+// k_dt_l1 with CALC_PHI_HYD's flat per-column pass (kernels_dyn.hip phi_flat_body)
+template <bool RS, bool QH>
+__global__ void __launch_bounds__(256) k_dt_l1f(Dims d, Params p, Fields f, int nbGm, int nbPhi) {
+  int lb = mg_xcd_block();
+  if (lb < nbGm) { gm_tensor_body(d, p, f, lb); return; }
+  lb -= nbGm;
+  if (lb < nbPhi) { phi_flat_body<RS, QH>(d, p, f, lb); return; }
+  del2uv_body(d, p, f, lb - nbPhi);
+}
+// launch [GMREDI_CALC_TENSOR | CALC_PHI_HYD | del2uv (nbDel blocks, 0 = none)]
+static void launch_l1(const Dims &d, const Params &p, const Fields &f, int nbDel, hipStream_t s) {
+  const int nbGm = (int)mg_plane_blocks(d.nx - 2, d.ny - 2, d.nT * d.Nr);
+  if (phi_flat_on(p)) {
+    const bool rs = p.nonlinFreeSurf > 0 && p.select_rStar > 0;
+    const bool qh = p.quasiHydrostatic && (p.select3dCoriScheme >= 1 || p.useNHMTerms);
+    auto kern = rs ? (qh ? k_dt_l1f<true, true> : k_dt_l1f<true, false>)
+                   : (qh ? k_dt_l1f<false, true> : k_dt_l1f<false, false>);
+    const int nbPhi = phi_flat_blocks(d, p);
+    hipLaunchKernelGGL(kern, dim3((unsigned)(nbGm + nbPhi + nbDel)), dim3(256), 0, s, d, p, f, nbGm, nbPhi);
+    return;
+  }
+  int nc, nArr, nbPhi;
+  phi_frame(d, p, nc, nArr, nbPhi);
+  MG_ALLOW_LDS(k_dt_l1);
+  hipLaunchKernelGGL(k_dt_l1, dim3((unsigned)(nbGm + nbPhi + nbDel)), dim3(256), mg_colf_lds(d.Nr, nc, nArr), s, d, p, f, nc,
+                     nbGm, nbPhi);
+}
 template <bool GM>
 __global__ void __launch_bounds__(256) k_dt_l2(Dims d, Params p, Fields f, TracerArgs aT, TracerArgs aS,
                                                const int *iterPtr, int nbMom, int nbTr) {
@@ -117,13 +145,7 @@ bool gm_phi_fusable(const Dims &d, const Params &p) {
   return mg_hfuse(MG_FUSE_DT, d.nx, d.ny, d.nT, d.Nr) && p.useGMRedi && p.momStepping;
 }
 hipError_t launch_gm_phi(const Dims &d, const Params &p, const Fields &f, hipStream_t s) {
-  int nc, nArr, nbPhi;
-  phi_frame(d, p, nc, nArr, nbPhi);
-  const int nbGm = (int)mg_plane_blocks(d.nx - 2, d.ny - 2, d.nT * d.Nr);
-  const int nbDel = phi_del2_fused(d, p) ? (int)mg_plane_blocks(d.nx, d.ny, d.nT * d.Nr) : 0;
-  MG_ALLOW_LDS(k_dt_l1);
-  hipLaunchKernelGGL(k_dt_l1, dim3((unsigned)(nbGm + nbPhi + nbDel)), dim3(256), mg_colf_lds(d.Nr, nc, nArr), s, d, p, f,
-                     nc, nbGm, nbPhi);
+  launch_l1(d, p, f, phi_del2_fused(d, p) ? (int)mg_plane_blocks(d.nx, d.ny, d.nT * d.Nr) : 0, s);
   return hipGetLastError();
 }
 
@@ -175,10 +197,7 @@ hipError_t launch_dyn_thermo(const Dims &d, const Params &p, const Fields &f, co
   const int nbDel = del2_needed(p) ? (int)mg_plane_blocks(d.nx, d.ny, d.nT * d.Nr) : 0;
   const int nbTr = (int)mg_plane_blocks(d.sNx, d.sNy, d.nT * d.Nr);
   if (dyn_thermo_takes_gm(p)) {
-    const int nbGm = (int)mg_plane_blocks(d.nx - 2, d.ny - 2, d.nT * d.Nr);
-    MG_ALLOW_LDS(k_dt_l1);
-    hipLaunchKernelGGL(k_dt_l1, dim3((unsigned)(nbGm + nbPhi + nbDel)), blk, mg_colf_lds(d.Nr, ncPhi, nArrPhi), s, d, p, f,
-                       ncPhi, nbGm, nbPhi);
+    launch_l1(d, p, f, nbDel, s);
     const int nbMom = 2 * (int)mg_plane_blocks(d.nx, d.ny, d.nT * d.Nr);
     hipLaunchKernelGGL(k_dt_l2<true>, dim3((unsigned)(nbMom + 2 * nbTr)), blk, 0, s, d, p, f, aT, aS, iterPtr, nbMom, nbTr);
     const long ncolTr = (long)d.sNx * d.sNy * d.nT;
