@@ -718,12 +718,19 @@ __device__ __forceinline__ void vecinv_tend(const A &a, const Dims &d, const P &
 // One point of DYNAMICS' momentum block.  COMP = 0 stores both components; 1 only the U
 // outputs (gU, guNm1, cdU), 2 only the V outputs: the other component's arithmetic is then
 // dead and compiled out, so k_mom_step_uv runs the two halves as separate, shorter threads.
-template <bool VI, int COMP>
-__device__ __forceinline__ void mom_step_point(const Dims &d, const Params &p, const Fields &f, const int *iterPtr,
-                                               int lblock) {
-  MG_PLANE_LB(1 - d.OLx, d.nx, 1 - d.OLy, d.ny, z, lblock)
+// PART (flux form only, k_mom_ff4 / mom_ff4_body): 0 the whole point; 1 every term but the
+// viscous ones, whose sum guDiss / gvDiss it takes from *sD after the workgroup barrier; 2 the
+// viscous terms only, stored to *sD before that barrier (the other role's wave of the same
+// points).  valid = false: no arithmetic, only the barrier (PART 1 / 2 reach it on every lane).
+template <bool VI, int COMP, int PART = 0>
+__device__ __forceinline__ void mom_step_ijz(const Dims &d, const Params &p, const Fields &f, const int *iterPtr, int i,
+                                             int j, int z, bool valid, double *sD) {
+  static_assert(PART == 0 || (!VI && COMP != 0), "the viscous split is per component, flux form");
+  valid = valid && !(i > d.sNx + d.OLx || j > d.sNy + d.OLy);
+  if constexpr (PART == 0) {
+    if (!valid) return;
+  }
   const int t = d.t0 + z / d.Nr, k = z % d.Nr + 1;
-  if (i > d.sNx + d.OLx || j > d.sNy + d.OLy) return;
   const int Nr = d.Nr;
   const int myIter = *iterPtr;
   // adams_bashforth2.F:61-65 (mom_StartAB = nIter0 for a cold start)
@@ -780,7 +787,7 @@ __device__ __forceinline__ void mom_step_point(const Dims &d, const Params &p, c
     const double drF = f.drF[k - 1], recip_drF = f.recip_drF[k - 1];
     double gU = 0.0, gV = 0.0, guDiss = 0.0, gvDiss = 0.0;
     double dPhiHydX = 0.0, dPhiHydY = 0.0;
-    if (inner) {
+    if (valid && inner && PART != 2) {
       // CALC_GRAD_PHI_HYD (calc_grad_phi_hyd.F:152-171), phi0surf = 0
       // r* (select_rStar >= 2, nonlinFreeSurf >= 4): varLoc = phiHydC*rStarFacC + phi0surf (:30-47)
       const bool rsc = rstar && p.select_rStar >= 2 && p.nonlinFreeSurf >= 4;
@@ -801,14 +808,14 @@ __device__ __forceinline__ void mom_step_point(const Dims &d, const Params &p, c
           dPhiHydY = dPhiHydY + factorP * (G3(alphaRho, i, j - 1, k) + a0) * (e0 - vl2(i, j - 1)) * G2(recip_dyC, i, j);
       }
     }
-    if (inner) {
+    if (valid && inner) {
       const double rhFacW = G3(recip_hFacW, i, j, k), rhFacS = G3(recip_hFacS, i, j, k);
       const double hZ = hfacz(d, f, i, j, k, t);
       if constexpr (VI) {
         vecinv_tend(VIGlobal{d, p, f, k, t}, d, p, f, i, j, k, t, gU, gV, guDiss, gvDiss);
       } else {
       // ---------------- advection (mom_u_adv_uu/vu/wu.F, mom_v_adv_uv/vv/wv.F)
-      if (p.momAdvection) {
+      if (PART != 2 && p.momAdvection) {
         const double fVerUkm = fverU(k), fVerUkp = fverU(k + 1);
         const double fVerVkm = fverV(k), fVerVkp = fverV(k + 1);
         // uTrans / vTrans (mom_fluxform.F:287-327)
@@ -834,7 +841,7 @@ __device__ __forceinline__ void mom_step_point(const Dims &d, const Params &p, c
 #undef VTR
       }
       // ---------------- viscosity (mom_u/v_x/y/rviscflux.F, sidedrag, botdrag)
-      if (p.momViscosity) {
+      if (PART != 1 && p.momViscosity) {
         // U: xviscflux at i and i-1, yviscflux at j+1 and j
         // v4F = del2u / del2v from k_del2uv (0 without biharmonic viscosity)
         const bool bh = p.viscA4D != 0.0 || p.viscA4Z != 0.0;
@@ -923,7 +930,7 @@ __device__ __forceinline__ void mom_step_point(const Dims &d, const Params &p, c
         }
       }
       // ---------------- spherical metric terms (mom_u/v_metric_sphere.F, mom_fluxform.F:714-721, 973-980)
-      if (p.useNHMTerms) {
+      if (PART != 2 && p.useNHMTerms) {
         // MOM_U/V_METRIC_NH (pkg/mom_common/mom_u_metric_nh.F:56-68, mom_v_metric_nh.F), mtNHFac = 1
         const int kp1 = k + 1 < Nr ? k + 1 : Nr;
         const double ov = (k == Nr) ? 0.0 : 1.0;
@@ -932,7 +939,7 @@ __device__ __forceinline__ void mom_step_point(const Dims &d, const Params &p, c
         gV = gV + 1.0 * (V(i, j, k) * p.recip_rSphere * 0.25 *
                          ((W(i, j - 1, kp1) + W(i, j, kp1)) * ov + (W(i, j - 1, k) + W(i, j, k))) * p.gravitySign);
       }
-      if (p.metricSphere) {
+      if (PART != 2 && p.metricSphere) {
         const double mTu = U(i, j, k) * p.recip_rSphere * 0.25 *
                            (V(i, j, k) + V(i - 1, j, k) + V(i, j + 1, k) + V(i - 1, j + 1, k)) * G2(tanPhiAtU, i, j);
         gU = gU + p.mtFacMom * mTu;
@@ -942,7 +949,7 @@ __device__ __forceinline__ void mom_step_point(const Dims &d, const Params &p, c
       }
       // ---------------- Coriolis (mom_u_coriolis.F, mom_v_coriolis.F); with the CD scheme
       // it is applied in TIMESTEP instead (mom_fluxform.F:995, k_cd_scheme)
-      if (p.useCoriolis && !p.useCDscheme) {
+      if (PART != 2 && p.useCoriolis && !p.useCDscheme) {
         const int sc = p.selectCoriScheme;
         double c;
         if (sc >= 2)
@@ -964,7 +971,7 @@ __device__ __forceinline__ void mom_step_point(const Dims &d, const Params &p, c
           c = c * 4.0 / fmax(1.0, G3(maskW, i, j, k) + G3(maskW, i + 1, j, k) + G3(maskW, i, j - 1, k) + G3(maskW, i + 1, j - 1, k));
         gV = gV + fvFac * c;
       }
-      if (p.select3dCoriScheme >= 1) {
+      if (PART != 2 && p.select3dCoriScheme >= 1) {
         // MOM_U_CORIOLIS_NH (pkg/mom_common/mom_u_coriolis_nh.F:60-76), angleCosC = 1; the V
         // component only on curvilinear / rotated grids (mom_fluxform.F:1025-1040)
         const int kp1 = k + 1 < Nr ? k + 1 : Nr;
@@ -980,6 +987,17 @@ __device__ __forceinline__ void mom_step_point(const Dims &d, const Params &p, c
       gV = gV * G3(maskS, i, j, k);
       gvDiss = gvDiss * G3(maskS, i, j, k);
       }   // vectorInvariantMomentum
+    }
+    if constexpr (PART == 2) {   // hand the viscous sum to the PART 1 wave of the same point
+      *sD = COMP == 1 ? guDiss : gvDiss;
+      __syncthreads();
+      return;
+    }
+    if constexpr (PART == 1) {
+      __syncthreads();
+      if (COMP == 1) guDiss = *sD;
+      else gvDiss = *sD;
+      if (!valid) return;
     }
     // ---------------- TIMESTEP (timestep.F:104-388)
     double guExt = 0.0, gvExt = 0.0;
@@ -1035,6 +1053,45 @@ __device__ __forceinline__ void mom_step_point(const Dims &d, const Params &p, c
 #undef W
 #undef G2
 #undef G3
+}
+template <bool VI, int COMP>
+__device__ __forceinline__ void mom_step_point(const Dims &d, const Params &p, const Fields &f, const int *iterPtr,
+                                               int lblock) {
+  MG_PLANE_LB(1 - d.OLx, d.nx, 1 - d.OLy, d.ny, z, lblock)
+  mom_step_ijz<VI, COMP>(d, p, f, iterPtr, i, j, z, true, nullptr);
+}
+// MOM_FLUXFORM + TIMESTEP + AB2 with four threads per point: wave 0 the U component's
+// advective / metric / Coriolis / pressure terms, wave 1 its viscous terms, waves 2, 3 the
+// same for V -- 64 points per workgroup, the viscous sums handed over through LDS; each
+// thread's dependency chain is about half of k_mom_step_uv's.  The same expressions, summed in
+// the same order: bit-identical.
+__host__ __device__ __forceinline__ int mom_ff4_blocks(const Dims &d) { return (d.nx * d.ny + 63) / 64 * d.Nr * d.nT; }
+// whether the flux-form momentum runs four threads per point (MGCM_MOM_FF4=0 never, 1 default,
+// 2 also inside config 2's fused grid; read per launch).  Measured (profiles/r03/ff4/): config
+// 4 0.1438 against 0.1458 ms/step with the U/V halves; inside k_dt_l2 beside the tracer
+// right-hand sides (config 2) 0.3215 against 0.3092 -- there the U/V halves stay
+inline bool mom_ff4_on(bool fused = false) {
+  const char *e = getenv("MGCM_MOM_FF4");
+  const int v = e ? atoi(e) : 1;
+  return fused ? v == 2 : v != 0;
+}
+__device__ __forceinline__ void mom_ff4_body(const Dims &d, const Params &p, const Fields &f, const int *iterPtr, int lb) {
+  __shared__ double sD[128];
+  const int np = d.nx * d.ny, nbp = (np + 63) / 64;
+  const int z = lb / nbp, lane = (int)threadIdx.x & 63, w = (int)threadIdx.x >> 6;
+  const int q = (lb % nbp) * 64 + lane;
+  const bool valid = q < np;
+  const int i = 1 - d.OLx + (valid ? q % d.nx : 0), j = 1 - d.OLy + (valid ? q / d.nx : 0);
+  double *slot = sD + (w >> 1) * 64 + lane;
+  switch (w) {
+    case 0: mom_step_ijz<false, 1, 1>(d, p, f, iterPtr, i, j, z, valid, slot); break;
+    case 1: mom_step_ijz<false, 1, 2>(d, p, f, iterPtr, i, j, z, valid, slot); break;
+    case 2: mom_step_ijz<false, 2, 1>(d, p, f, iterPtr, i, j, z, valid, slot); break;
+    default: mom_step_ijz<false, 2, 2>(d, p, f, iterPtr, i, j, z, valid, slot); break;
+  }
+}
+__global__ void __launch_bounds__(256) k_mom_ff4(Dims d, Params p, Fields f, const int *iterPtr) {
+  mom_ff4_body(d, p, f, iterPtr, mg_xcd_block());
 }
 
 template <bool VI>
@@ -2377,6 +2434,8 @@ hipError_t launch_mom_step(const Dims &d, const Params &p, const Fields &f, cons
   else if (getenv("MGCM_MOM_NOSPLIT"))
     hipLaunchKernelGGL(k_mom_step<false>, dim3(mg_plane_blocks(d.nx, d.ny, d.nT * d.Nr)), dim3(MG_PLANE_THREADS), 0, s,
                        d, p, f, iterPtr);
+  else if (mom_ff4_on())   // MOM_FLUXFORM: four threads per point (U, V x viscous or not)
+    hipLaunchKernelGGL(k_mom_ff4, dim3((unsigned)mom_ff4_blocks(d)), dim3(256), 0, s, d, p, f, iterPtr);
   else   // MOM_FLUXFORM: U and V halves as separate threads (twice the workgroups, half the chain)
     hipLaunchKernelGGL(k_mom_step_uv<false>, dim3(2 * mg_plane_blocks(d.nx, d.ny, d.nT * d.Nr)), dim3(MG_PLANE_THREADS), 0,
                        s, d, p, f, iterPtr);

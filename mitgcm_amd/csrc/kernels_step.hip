@@ -91,12 +91,13 @@ static void launch_l1(const Dims &d, const Params &p, const Fields &f, int nbDel
   hipLaunchKernelGGL(k_dt_l1, dim3((unsigned)(nbGm + nbPhi + nbDel)), dim3(256), mg_colf_lds(d.Nr, nc, nArr), s, d, p, f, nc,
                      nbGm, nbPhi);
 }
-template <bool GM>
+template <bool GM, bool FF4>
 __global__ void __launch_bounds__(256) k_dt_l2(Dims d, Params p, Fields f, TracerArgs aT, TracerArgs aS,
                                                const int *iterPtr, int nbMom, int nbTr) {
   int lb = mg_xcd_block();
   if (lb < nbMom) {
-    if (lb & 1) mom_step_point<false, 2>(d, p, f, iterPtr, lb >> 1);
+    if constexpr (FF4) mom_ff4_body(d, p, f, iterPtr, lb);
+    else if (lb & 1) mom_step_point<false, 2>(d, p, f, iterPtr, lb >> 1);
     else mom_step_point<false, 1>(d, p, f, iterPtr, lb >> 1);
     return;
   }
@@ -198,8 +199,10 @@ hipError_t launch_dyn_thermo(const Dims &d, const Params &p, const Fields &f, co
   const int nbTr = (int)mg_plane_blocks(d.sNx, d.sNy, d.nT * d.Nr);
   if (dyn_thermo_takes_gm(p)) {
     launch_l1(d, p, f, nbDel, s);
-    const int nbMom = 2 * (int)mg_plane_blocks(d.nx, d.ny, d.nT * d.Nr);
-    hipLaunchKernelGGL(k_dt_l2<true>, dim3((unsigned)(nbMom + 2 * nbTr)), blk, 0, s, d, p, f, aT, aS, iterPtr, nbMom, nbTr);
+    const bool ff4 = mom_ff4_on(true);
+    const int nbMom = ff4 ? mom_ff4_blocks(d) : 2 * (int)mg_plane_blocks(d.nx, d.ny, d.nT * d.Nr);
+    auto l2 = ff4 ? k_dt_l2<true, true> : k_dt_l2<true, false>;
+    hipLaunchKernelGGL(l2, dim3((unsigned)(nbMom + 2 * nbTr)), blk, 0, s, d, p, f, aT, aS, iterPtr, nbMom, nbTr);
     const long ncolTr = (long)d.sNx * d.sNy * d.nT;
     const int ncTr = mg_colf_nc(ncolTr, d.Nr, 3);
     const int nbImp = (int)mg_colf_blocks(ncolTr, ncTr);
