@@ -6,11 +6,18 @@
 // DYNAMICS: phiHyd, gU/gV, the momentum AB histories, the CD-scheme fields), so on a small
 // grid -- where every launch is a few microseconds of latency and one kernel cannot fill the
 // chip -- their kernels of the same depth share one grid (horizontal launch fusion, split by
-// logical block id as k_phi_del2 does) instead of running on two streams joined by events:
+// logical block id as k_phi_del2 does) instead of running on two streams joined by events.
+// The default layout (k_dt_l1..l3, config 2: 0.3097 against 0.3218 ms/step for the layout
+// below it and 0.334 for two streams):
 //
-//   front: CALC_PHI_HYD | MOM del2 (biharmonic) | GAD_CALC_RHS+AB2+TIMESTEP (theta) | (salt)
-//   back:  MOM_FLUXFORM+TIMESTEP (U and V halves) | GAD_IMPLICIT_R + SOLVE_TRIDIAGONAL (theta) | (salt)
-//   then:  CD_CODE_SCHEME, implicit viscosity (launch_mom_tail)
+//   1: GMREDI_CALC_TENSOR | CALC_PHI_HYD | MOM del2 (biharmonic)
+//   2: MOM_FLUXFORM+TIMESTEP (U and V halves) | GAD_CALC_RHS+AB2+TIMESTEP (theta) | (salt)
+//   3: CD_CODE_SCHEME | GAD_IMPLICIT_R + SOLVE_TRIDIAGONAL (theta) | (salt)
+//
+// and the front/back layout (k_dt_front / k_dt_back, MGCM_DT_LAYOUT=2): [CALC_PHI_HYD | del2 |
+// rhs theta | rhs salt], [MOM U | V | implicit theta | salt], then the CD scheme.  Outside the
+// fold, on the small grids: GMREDI_CALC_TENSOR beside CALC_PHI_HYD (launch_gm_phi) and both
+// tracers per launch (launch_tracer_hpair) for the staggered step.
 //
 // Every body is the same device function the separate kernels run, so the results are the
 // same bits.  The two source files are included rather than linked: hipcc builds without
