@@ -655,56 +655,85 @@ __global__ void __launch_bounds__(CG_THREADS) k_cg2d_blk2(Dims d, Params p, Fiel
 // 2(BX+BY) out-of-block neighbour slots as 16-bit pairs in the order
 // W[0..BY-1], E[0..BY-1], S[0..BX-1], N[0..BX-1]; blkx[BX*BY per block] = the
 // 2-D offsets of P[b][a] (row b = j, column a = i).
+// The block sums of k_cg2d_bxy (NW waves): the pairwise tree over the wave's 64 lanes, then
+// the pairwise tree over the 16 wave slots (slots >= NW are +0.0) -- the order
+// mgcm_cg2d_sum_plan exports.  Cheaper evaluation of the same tree, bit for bit:
+//   * wave stage: the row trees (row_sum16), then row 3 += lane 47 (row_bcast15) and
+//     row 3 += lane 31 (row_bcast31) by plain DPP moves: only lane 63's value is used, so the
+//     other rows' lanes may take any source and need no zeroed "old" operand; lane 63 stores
+//     its own value (no readlane to a scalar and back);
+//   * slot stage: every lane reads the NW slots (LDS broadcast, 16-byte reads) and adds them in
+//     the tree's order in registers -- the row_sum16 of the zero-padded slots computes
+//     (((s0+s1)+(s2+s3))+((s4+s5)+(s6+s7))) + (upper half) in every lane, each addition
+//     commuted at most, which is exact -- instead of four DPP steps.
+__device__ __forceinline__ double wave_tree63(double v) {
+  v = row_sum16(v);
+  v = v + dpp_f64<0x142>(v);   // lanes 48..63 += lane 47 (row 2's sum)
+  v = v + dpp_f64<0x143>(v);   // lanes 48..63 += lane 31 (rows 0+1)
+  return v;                    // lane 63: (r3 + r2) + (r1 + r0)
+}
+template <int NW>
+__device__ __forceinline__ double slot_tree(const double *red_slot) {
+  static_assert(NW >= 1 && NW <= 16 && (NW % 2 == 0 || NW == 1), "slot_tree: NW");
+  double s[16];
+#pragma unroll
+  for (int q = 0; q < 16; q += 2) {
+    if (q + 1 < NW) {
+      const double2 w = *reinterpret_cast<const double2 *>(red_slot + q);
+      s[q] = w.x; s[q + 1] = w.y;
+    } else {
+      s[q] = q < NW ? red_slot[q] : 0.0;
+      s[q + 1] = 0.0;
+    }
+  }
+  double t8[8], t4[4];
+#pragma unroll
+  for (int q = 0; q < 8; q++) t8[q] = s[2 * q] + s[2 * q + 1];
+#pragma unroll
+  for (int q = 0; q < 4; q++) t4[q] = t8[2 * q] + t8[2 * q + 1];
+  return (t4[0] + t4[1]) + (t4[2] + t4[3]);
+}
 template <int NW>
 __device__ __forceinline__ double block_sum_nw(double v, double *red, int slot) {
-  v = wave_sum(v);
+  v = wave_tree63(v);
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  if (lane == 0) red[slot * 16 + wv] = v;
+  if (lane == 63) red[slot * 16 + wv] = v;
   __syncthreads();
-  const int l = lane & 15;
-  return row_sum16(l < NW ? red[slot * 16 + l] : 0.0);
+  return slot_tree<NW>(red + slot * 16);
 }
-// two sums in one reduction (independent DPP chains interleave); each value is
-// reduced with exactly the operations block_sum_nw applies, so the results are the same
+// two sums in one reduction (independent chains interleave), each as block_sum_nw
 template <int NW>
 __device__ __forceinline__ void block_sum2_nw(double &v0, double &v1, double *red, int slot) {
   v0 = row_sum16(v0);
   v1 = row_sum16(v1);
-  v0 = v0 + dpp_bcast_f64<0x142, 0xA>(v0);
-  v1 = v1 + dpp_bcast_f64<0x142, 0xA>(v1);
-  v0 = v0 + dpp_bcast_f64<0x143, 0xC>(v0);
-  v1 = v1 + dpp_bcast_f64<0x143, 0xC>(v1);
-  v0 = lane_f64(v0, 63);
-  v1 = lane_f64(v1, 63);
+  v0 = v0 + dpp_f64<0x142>(v0);
+  v1 = v1 + dpp_f64<0x142>(v1);
+  v0 = v0 + dpp_f64<0x143>(v0);
+  v1 = v1 + dpp_f64<0x143>(v1);
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  if (lane == 0) { red[slot * 16 + wv] = v0; red[(slot ^ 1) * 16 + wv] = v1; }
+  if (lane == 63) { red[slot * 16 + wv] = v0; red[(slot ^ 1) * 16 + wv] = v1; }
   __syncthreads();
-  const int l = lane & 15;
-  v0 = row_sum16(l < NW ? red[slot * 16 + l] : 0.0);
-  v1 = row_sum16(l < NW ? red[(slot ^ 1) * 16 + l] : 0.0);
+  v0 = slot_tree<NW>(red + slot * 16);
+  v1 = slot_tree<NW>(red + (slot ^ 1) * 16);
 }
-// three sums in one reduction (slots 0, 1, 2), each reduced as block_sum_nw does
+// three sums in one reduction (slots 0, 1, 2), each as block_sum_nw
 template <int NW>
 __device__ __forceinline__ void block_sum3_nw(double &v0, double &v1, double &v2, double *red) {
   v0 = row_sum16(v0);
   v1 = row_sum16(v1);
   v2 = row_sum16(v2);
-  v0 = v0 + dpp_bcast_f64<0x142, 0xA>(v0);
-  v1 = v1 + dpp_bcast_f64<0x142, 0xA>(v1);
-  v2 = v2 + dpp_bcast_f64<0x142, 0xA>(v2);
-  v0 = v0 + dpp_bcast_f64<0x143, 0xC>(v0);
-  v1 = v1 + dpp_bcast_f64<0x143, 0xC>(v1);
-  v2 = v2 + dpp_bcast_f64<0x143, 0xC>(v2);
-  v0 = lane_f64(v0, 63);
-  v1 = lane_f64(v1, 63);
-  v2 = lane_f64(v2, 63);
+  v0 = v0 + dpp_f64<0x142>(v0);
+  v1 = v1 + dpp_f64<0x142>(v1);
+  v2 = v2 + dpp_f64<0x142>(v2);
+  v0 = v0 + dpp_f64<0x143>(v0);
+  v1 = v1 + dpp_f64<0x143>(v1);
+  v2 = v2 + dpp_f64<0x143>(v2);
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  if (lane == 0) { red[wv] = v0; red[16 + wv] = v1; red[32 + wv] = v2; }
+  if (lane == 63) { red[wv] = v0; red[16 + wv] = v1; red[32 + wv] = v2; }
   __syncthreads();
-  const int l = lane & 15;
-  v0 = row_sum16(l < NW ? red[l] : 0.0);
-  v1 = row_sum16(l < NW ? red[16 + l] : 0.0);
-  v2 = row_sum16(l < NW ? red[32 + l] : 0.0);
+  v0 = slot_tree<NW>(red);
+  v1 = slot_tree<NW>(red + 16);
+  v2 = slot_tree<NW>(red + 32);
 }
 __device__ __forceinline__ double wave_max_u(double v) {
   v = row_max16(v);
@@ -1018,10 +1047,10 @@ __global__ void __launch_bounds__(NT) k_cg2d_bxy(Dims d, Params p, Fields f, con
     const unsigned long long stampT0 = __builtin_amdgcn_s_memtime(), stampR0 = __builtin_amdgcn_s_memrealtime();
     __builtin_amdgcn_s_waitcnt(0xC07F);
 #endif
-    for (int it2d = 1; it2d <= maxIters; it2d++) {
+    if constexpr (RC) for (int it2d = 1; it2d <= maxIters; it2d++) {
       const double cgBeta = eta_qrN / eta_qrNM1;
       eta_qrNM1 = eta_qrN;
-      if constexpr (RC) {
+      {
         if (it2d > 1) {   // the previous iteration's r, now that its neighbour readers are past D
 #pragma unroll
           for (int b = 0; b < BY; b++)
@@ -1080,8 +1109,13 @@ __global__ void __launch_bounds__(NT) k_cg2d_bxy(Dims d, Params p, Fields f, con
 #pragma unroll
             for (int a = 0; a < BX; a++) xmin[b][a] = x[b][a];
         }
-        continue;
       }
+    }
+    // the standard iteration, unrolled by two: the loop-carried s and q then need no register
+    // copies at the back edge (each copy of the body may hold them in the other's registers)
+    auto iter = [&](int it2d) -> bool {
+      const double cgBeta = eta_qrN / eta_qrNM1;
+      eta_qrNM1 = eta_qrN;
 #pragma unroll
       for (int b = 0; b < BY; b++)
 #pragma unroll
@@ -1127,7 +1161,7 @@ __global__ void __launch_bounds__(NT) k_cg2d_bxy(Dims d, Params p, Fields f, con
       CG_STAMP(5);
       err_sq = e2;
       eta_qrN = en;
-      if (err_sq < p.cg2dTolerance_sq) break;
+      if (err_sq < p.cg2dTolerance_sq) return true;
       if (MINRES && err_sq < minResidualSq) {
         minResidualSq = err_sq;
         nIterMin = it2d;
@@ -1136,6 +1170,13 @@ __global__ void __launch_bounds__(NT) k_cg2d_bxy(Dims d, Params p, Fields f, con
 #pragma unroll
           for (int a = 0; a < BX; a++) xmin[b][a] = x[b][a];
       }
+      return false;
+    };
+    if constexpr (!RC) {
+      bool done = false;
+      int it2d = 1;
+      for (; !done && it2d + 1 <= maxIters; it2d += 2) done = iter(it2d) || iter(it2d + 1);
+      if (!done && it2d <= maxIters) iter(it2d);
     }
 #ifdef MGCM_CG_STAMPS
     if (tid == 0)
