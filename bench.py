@@ -54,10 +54,12 @@ def parse():
     ap.add_argument("--shard", action="store_true",
                     help="N>1: shard the workload's tiles over the N processes (RCCL, strong scaling, "
                          "mitgcm_amd/parallel.py) instead of running N replicas")
-    ap.add_argument("--cg2d", choices=["replicated", "distributed", "device"], default="replicated",
-                    help="with --shard: CG2D replicated on every GPU (default), the reference's distributed "
-                         "CG2D with GLOBAL_SUM_TILE_RL over the collective, or the device CG2D whose parts run in "
-                         "every process on one IPC-shared hand-off block (mitgcm_amd/parallel.py)")
+    ap.add_argument("--cg2d", choices=["auto", "replicated", "distributed", "device"], default="auto",
+                    help="with --shard: auto (default: the device CG2D where the solver is the multi-workgroup "
+                         "one, replicated where it is a single-CU kernel), CG2D replicated on every GPU, the "
+                         "reference's distributed CG2D with GLOBAL_SUM_TILE_RL over the collective, or the device "
+                         "CG2D whose parts run in every process on one IPC-shared hand-off block "
+                         "(mitgcm_amd/parallel.py)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--set", action="append", default=[], metavar="NAME=VALUE",
                     help="override a namelist parameter of the GPU model (A/B runs, e.g. useSRCGSolver=1); "
@@ -273,7 +275,7 @@ def main():
     # the sharded step over RCCL with the replicated solve is graph-captured (two steps per
     # graph, collectives included: ShardedModel.capture_step) and replayed, as the resident
     # path is; gloo and the host-driven distributed CG2D step eagerly
-    graph_shard = shard and dist.get_backend() == "nccl" and a.cg2d != "distributed"
+    graph_shard = shard and dist.get_backend() == "nccl" and stepper.cg2d != "distributed"
     if graph_shard and a.steps % 2:
         raise SystemExit("bench: --shard over RCCL replays pairs of steps: --steps must be even")
 
@@ -377,7 +379,7 @@ def main():
                                                        else "; replicas only"),
                    "tiles_per_gpu": stepper.nT if shard else g.nTiles, "points_per_tile": [g.sNx, g.sNy, g.Nr],
                    "parallelism": ("tiles%d" if shard else "replicas%d") % world,
-                   "cg2d": a.cg2d if shard else "single-GPU kernel",
+                   "cg2d": stepper.cg2d if shard else "single-GPU kernel",
                    **({"step_path": "graph-replayed sharded step (RCCL collectives captured)" if graph_shard
                        else "eager sharded step"} if shard else {}),
                    **({"params_over": over} if over else {})},

@@ -119,11 +119,13 @@ int mgcm_prepare(mgcm_model *m);
 /* FORWARD_STEP subset: the six ops above (+ surface forcing), nsteps times,
  * asynchronously on the model's stream (captured once into a hipGraph). */
 int mgcm_forward_step(mgcm_model *m, int nsteps);
-/* Wait for all queued device work. */
-/* ---- tile-sharded runs (one process per GPU, mitgcm_amd/parallel.py) ----------
+/* ---- tile-sharded runs (one process per GPU, mitgcm_amd/parallel.py; or several models
+ * of one Fortran host process, fortran_abi.hip) -------------------------------------------
  * Every process holds the whole domain's arrays; the 3-D kernels step only tiles
  * [t0, t0+nT) (the reference's myBxLo..myBxHi / process tile set).
- * The 2-D pressure solve is replicated on every process over the gathered RHS, so
+ * The 2-D pressure solve runs either as the device CG2D -- the multi-workgroup solver's
+ * parts of each process's tiles on one shared hand-off block (phase 10, mgcm_cg2d_shared_*)
+ * -- or replicated on every process over the gathered right-hand side (phase 2); either way
  * its sums are the single-GPU sums and results are bit-identical at any N. */
 int mgcm_set_tile_range(mgcm_model *m, int t0, int nT);
 /* Run on `stream` (a hipStream_t, e.g. the caller's collective stream); NULL = own. */
@@ -171,6 +173,22 @@ int mgcm_cg2d_op(mgcm_model *m, int op, double a0, double *part);
 int mgcm_cg2d_shared_bytes(mgcm_model *m);
 int mgcm_cg2d_shared_export(mgcm_model *m, void *handle);
 int mgcm_cg2d_shared_import(mgcm_model *m, const void *handle);
+/* Several models stepped by ONE host process (fortran_abi.hip: the Fortran drop-ins with
+ * MGCM_AMD_MODELS = N), each over its own tile range:
+ *   mgcm_get_stream    the model's current hipStream_t (cross-model ordering by events);
+ *   mgcm_halo_sources  the interior points outside tiles [t0, t0+nT) that their halos copy
+ *                      (scalar map + EXCH2 vector maps), sorted; returns the count (writes at
+ *                      most cap) -- what the models stepping those points deliver;
+ *   mgcm_cg2d_tiles    the device CG2D's parts of tiles [t0, t0+nT) on this model's arrays;
+ *   mgcm_cg2d_share    m polls owner's hand-off block (uncached, system scope; peer access
+ *                      between GPUs) -- the in-process form of mgcm_cg2d_shared_export/import.
+ * mgcm_step_phase adds the routine-level phases 11 (CALC_DIV_GHAT right-hand side), 12 (CG2D
+ * on the gathered domain + EXCH(cg2d_x) + etaN), 13 (EXCH(cg2d_x) + etaN), 14 (INTEGR_CONTINUITY's
+ * column pass after MOMENTUM_CORRECTION_STEP) and 15 (EXCH(eta) + UPDATE_ETAH). */
+void *mgcm_get_stream(mgcm_model *m);
+long mgcm_halo_sources(mgcm_model *m, int t0, int nT, long *out, long cap);
+int mgcm_cg2d_tiles(mgcm_model *m, int t0, int nT);
+int mgcm_cg2d_share(mgcm_model *m, mgcm_model *owner);
 /* Store CG2D's output arguments (cg2d.F:13-17) as this step's solve record. */
 int mgcm_cg2d_record(mgcm_model *m, double firstResidual, double lastResidual, double rhsMax, double sumRHS,
                      int numIters);
@@ -180,6 +198,7 @@ int mgcm_field_pack(mgcm_model *m, const char *name, const long *idx, long n, do
  * the model's halo map; the cross-process sources must have been delivered first). */
 int mgcm_exchange_field(mgcm_model *m, const char *name);
 
+/* Wait for all queued device work. */
 int mgcm_sync(mgcm_model *m);
 
 /* Device CG2D on fields of this model (cg2d.F:13 semantics; b is normalised in

@@ -80,6 +80,10 @@ def lib():
         "mgcm_param_name": (cs, [ci]),
         "mgcm_update_r_star": (ci, [vp]),
         "mgcm_calc_r_star": (ci, [vp]),
+        "mgcm_get_stream": (vp, [vp]),
+        "mgcm_halo_sources": (cl, [vp, ci, ci, PL, cl]),
+        "mgcm_cg2d_tiles": (ci, [vp, ci, ci]),
+        "mgcm_cg2d_share": (ci, [vp, vp]),
         "ini_cg2d_amd_": (None, [PI] * 6 + [PD] * 8 + [PI]),
         "cg2d_amd_": (None, [PD, PD, PD, PD, PD, PI, PI, PI]),
     }
@@ -107,7 +111,7 @@ EXPORTS = ["mgcm_create", "mgcm_destroy", "mgcm_last_error", "mgcm_set_param", "
            "mgcm_set_iter", "mgcm_amd_host_sync_", "mgcm_amd_device_sync_", "mgcm_amd_transfer_stats_",
            "mgcm_amd_step_fence_", "mgcm_halo_pack_group", "mgcm_exchange_nfields_group", "mgcm_stream_handoff",
            "mgcm_end_steps", "mgcm_cg2d_shared_bytes", "mgcm_cg2d_shared_export", "mgcm_cg2d_shared_import",
-           "mgcm_amd_set_maps_"]
+           "mgcm_amd_set_maps_", "mgcm_get_stream", "mgcm_halo_sources", "mgcm_cg2d_tiles", "mgcm_cg2d_share"]
 
 
 def check(rc, what):

@@ -359,7 +359,9 @@ struct MwgTables {
   int exclusive;          // 1: every part claims its CU's whole LDS (no co-resident workgroups)
   // hand-off state, one block zeroed before each launch (hsBytes from ctr): granules of
   // {tag = phase + 1 (32 bits), half of an f64 (32 bits)}, two per value
-  unsigned *ctr;          // [1] timeout word
+  unsigned *ctr;          // [1] timeout word (hand-off block, shared by every launch of the solve)
+  unsigned *epoch;        // launch epoch of THIS process's launches (its own memory, never shared):
+                          // read by its parts at their start, advanced by its first part at the end
   unsigned long long *part;   // [2 parities][3 values][G][2] workgroup partials
   unsigned long long *xs;     // [exported points][2] q = M r of the points other parts' rings hold
   size_t hsBytes;

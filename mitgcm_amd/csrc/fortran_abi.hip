@@ -27,8 +27,35 @@
 //     and nothing else across PCIe.
 // mgcm_amd_transfer_stats_ counts the copies, so a host can check the schedule.
 //
+// Tiles over GPUs (the reference's tile set of one process spread over device models, SURVEY
+// 8(e) "tiles shard one-per-GPU" with the host staying one Fortran process): MGCM_AMD_MODELS =
+// N (or "auto" = min(tiles, GPUs); default 1) device models, model i owning the contiguous,
+// balanced tile range i of the global tile order (bi fastest) on GPU MGCM_AMD_DEVICES[i]
+// (default: contiguous blocks of models per GPU, one model per GPU when N <= GPUs).  Every
+// model holds the whole domain's arrays; its 3-D kernels step its own tiles.  A routine
+// drop-in runs the routine on every model, with the exchange points of the MPI reference in
+// between -- where an MPI rank would EXCH or GLOBAL_SUM, the models copy device to device:
+//   * DO_FIELDS_BLOCKING_EXCHANGES: the 3-D halo sources a model's halos read from another
+//     model's tiles (exch1_rx.template:170-198 / exch2_rx1_cube.template:118-247's send/recv),
+//     packed, copied GPU to GPU, unpacked, then each model's local halo fill;
+//   * SOLVE_FOR_PRESSURE: the right-hand side's tile blocks to every model, then CG2D --
+//     the multi-workgroup device CG2D, launched once per GPU over the tiles of that GPU's
+//     models on ONE hand-off block shared by the GPUs (uncached, system scope), the
+//     solution's blocks back to every model; or, where the solver is a single-CU kernel,
+//     the whole (gathered) solve on every model -- same sums as one model, bit for bit;
+//   * INTEGR_CONTINUITY (exactConserv): the new free surface's blocks to every model before
+//     EXCH(eta) + UPDATE_ETAH; the r* passes (UPDATE_R_STAR, CALC_R_STAR) run on every tile
+//     of every model (2-D, identical inputs).
+// Copies move only tile blocks and halo-source points; the host state comes down from each
+// tile's owner.  Results are bit-identical to one model at any N (tests/test_gpu_refhost.py).
+// The device ordering between models is by events (every exchange point is a cross-stream
+// barrier), so no host synchronisation enters a step.
+//
 // Errors: no return channel exists in the reference (it prints and STOPs), so every
 // failure prints "ABNORMAL END: <routine>: <reason>" and aborts.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -53,10 +80,38 @@ struct Bound {
 struct Readers {
   double monitorFreq = 0.0, dumpFreq = 0.0, chkPtFreq = 0.0, pChkPtFreq = 0.0, deltaTClock = 0.0;
   int nEndIter = -1;
+  bool everyStep = false;   // a host routine reads the state after every step (useSBO, state diagnostics)
+};
+
+// One device model of the host's tile set: tiles [t0, t0+nT) on GPU dev.
+struct Shard {
+  mgcm_model *m = nullptr;
+  int dev = 0, t0 = 0, nT = 0;
+  hipEvent_t ev = nullptr;   // cross-model barriers
+};
+// The halo sources model s's tiles deliver to model d (sorted 2-D offsets, the same on both
+// sides: every model holds the domain at the same offsets), with a send buffer on s's GPU and
+// a receive buffer on d's.
+struct Link {
+  int s = 0, d = 0;
+  long n = 0;
+  long *idxS = nullptr, *idxD = nullptr;
+  double *sbuf = nullptr, *rbuf = nullptr;
+  hipEvent_t ev = nullptr;   // on s: the copy into rbuf is done
+};
+// Per GPU: the model that launches the device CG2D over the tiles of all that GPU's models.
+struct CgLead {
+  int shard = 0, t0 = 0, nT = 0;
 };
 
 struct FortranSide {
-  mgcm_model *m = nullptr;
+  mgcm_model *m = nullptr;               // model 0: the tile set's single-model entries (EXCH_*, CG2D)
+  std::vector<Shard> sh;                 // every device model (sh[0].m == m)
+  std::vector<Link> links;
+  std::vector<CgLead> cgLeads;
+  bool cgDevice = false;                 // CG2D: device multi-workgroup solve (else replicated)
+  bool exactConserv = false;
+  std::vector<void *> devAllocs;         // (device, pointer) pairs of the links' buffers
   int dims[7] = {0, 0, 0, 0, 0, 0, 0};   // sNx sNy OLx OLy Nr nSx nSy
   std::vector<Bound> bound;
   bool ready = false;
@@ -64,6 +119,12 @@ struct FortranSide {
   long devIter = -1;         // the iteration counter last written to the device (-1: unknown)
   double lastTime = 0.0;     // myTime / myIter of the latest routine drop-in
   int lastIter = 0;
+  // myTime / myIter after FORWARD_STEP advances them (forward_step.F:806-807), from a drop-in
+  // FORWARD_STEP calls after that line in the current step (SOLVE_FOR_PRESSURE, ...); unset
+  // (advValid false) until one runs
+  bool advValid = false;
+  double advTime = 0.0;
+  int advIter = 0;
   Readers rd;
   long nUp = 0, nDown = 0;   // copies of whole bound arrays, for mgcm_amd_transfer_stats_
   double bytesUp = 0.0, bytesDown = 0.0;
@@ -86,16 +147,145 @@ mgcm_model *model(const char *where) {
   return g.m;
 }
 
+void hipchk(hipError_t e, const char *where) {
+  if (e != hipSuccess) die(where, hipGetErrorString(e));
+}
+hipStream_t stream_of(const Shard &s) { return (hipStream_t)mgcm_get_stream(s.m); }
+bool multi() { return g.sh.size() > 1; }
+long n2() { return (long)(g.dims[0] + 2 * g.dims[2]) * (g.dims[1] + 2 * g.dims[3]); }
+long nTiles() { return (long)g.dims[5] * g.dims[6]; }
+
+// every model runs fn (its own tiles; the r* passes every tile)
+void run_all(const char *where, int (*fn)(mgcm_model *)) {
+  for (auto &s : g.sh) {
+    hipchk(hipSetDevice(s.dev), where);
+    if (fn(s.m)) die(where);
+  }
+}
+void phase_all(const char *where, int phase) {
+  for (auto &s : g.sh) {
+    hipchk(hipSetDevice(s.dev), where);
+    if (mgcm_step_phase(s.m, phase)) die(where);
+  }
+}
+
+// Cross-model barrier on the device: every model's stream waits for the work every other
+// model has issued so far (no host synchronisation).
+void barrier_all(const char *where) {
+  if (!multi()) return;
+  for (auto &s : g.sh) {
+    hipchk(hipSetDevice(s.dev), where);
+    hipchk(hipEventRecord(s.ev, stream_of(s)), where);
+  }
+  for (auto &a : g.sh) {
+    hipchk(hipSetDevice(a.dev), where);
+    for (auto &b : g.sh)
+      if (&a != &b) hipchk(hipStreamWaitEvent(stream_of(a), b.ev, 0), where);
+  }
+}
+
+// The tile blocks [t0, t0+nT) of a 2-D field from model `from` to every other model.
+void copy_blocks(const char *where, const char *name, int from, int t0, int nT) {
+  const Shard &a = g.sh[from];
+  const long per = n2();
+  const double *src = mgcm_device_ptr(a.m, name);
+  if (!src) die(where);
+  hipchk(hipSetDevice(a.dev), where);
+  for (size_t j = 0; j < g.sh.size(); j++) {
+    if ((int)j == from) continue;
+    double *dst = mgcm_device_ptr(g.sh[j].m, name);
+    if (!dst) die(where);
+    hipchk(hipMemcpyAsync(dst + t0 * per, src + t0 * per, (size_t)nT * per * sizeof(double), hipMemcpyDeviceToDevice,
+                          stream_of(a)),
+           where);
+  }
+}
+// GLOBAL all-gather of a 2-D field's tile blocks: every model's own tiles to every other model
+void gather2d(const char *where, const char *name) {
+  barrier_all(where);
+  for (size_t i = 0; i < g.sh.size(); i++) copy_blocks(where, name, (int)i, g.sh[i].t0, g.sh[i].nT);
+  barrier_all(where);
+}
+
+// The 3-D halo sources of a field group (mgcm_halo_pack_group: 0 all of
+// DO_FIELDS_BLOCKING_EXCHANGES' fields) along every link: pack on the owner, copy GPU to GPU,
+// unpack on the reader -- then each model's local halo fill reads them.
+void xfer3d(const char *where, int group) {
+  barrier_all(where);
+  const int Nr = g.dims[4];
+  for (auto &L : g.links) {
+    const Shard &a = g.sh[L.s], &b = g.sh[L.d];
+    const int nf = mgcm_exchange_nfields_group(a.m, group);
+    if (nf <= 0) continue;
+    hipchk(hipSetDevice(a.dev), where);
+    if (mgcm_halo_pack_group(a.m, group, L.idxS, L.n, L.sbuf, 0)) die(where);
+    hipchk(hipMemcpyAsync(L.rbuf, L.sbuf, (size_t)nf * Nr * L.n * sizeof(double), hipMemcpyDeviceToDevice,
+                          stream_of(a)),
+           where);
+    hipchk(hipEventRecord(L.ev, stream_of(a)), where);
+    hipchk(hipSetDevice(b.dev), where);
+    hipchk(hipStreamWaitEvent(stream_of(b), L.ev, 0), where);
+    if (mgcm_halo_pack_group(b.m, group, L.idxD, L.n, L.rbuf, 1)) die(where);
+  }
+  barrier_all(where);
+}
+
+// ---- the device routines a drop-in runs (on every model, with the exchange points) ------
+void op_oceanic_phys(const char *w) { run_all(w, mgcm_oceanic_phys); }
+void op_tracer_step(const char *w) { run_all(w, mgcm_tracer_step); }
+void op_dynamics(const char *w) { run_all(w, mgcm_dynamics); }
+void op_update_r_star(const char *w) { run_all(w, mgcm_update_r_star); }
+void op_calc_r_star(const char *w) { run_all(w, mgcm_calc_r_star); }
+void op_correction(const char *w) { run_all(w, mgcm_momentum_correction_step); }
+// SOLVE_FOR_PRESSURE: CALC_DIV_GHAT on the own tiles, the right-hand side and the first
+// guess (cg2d_x = Bo_surf*etaN, set with it: solve_for_pressure.F:129,176-177) to every model,
+// CG2D, EXCH(cg2d_x) + etaN everywhere
+void op_solve(const char *w) {
+  if (!multi()) return run_all(w, mgcm_solve_for_pressure);
+  phase_all(w, 11);
+  gather2d(w, "cg2d_b");
+  gather2d(w, "cg2d_x");
+  if (!g.cgDevice) return phase_all(w, 12);   // the single-CU solve of the gathered domain, on every model
+  // the device CG2D: one launch per GPU over its models' tiles (its lead's arrays hold the
+  // gathered right-hand side), all launches on one hand-off block; then each GPU's solution
+  // blocks to every other model
+  for (auto &c : g.cgLeads) {
+    hipchk(hipSetDevice(g.sh[c.shard].dev), w);
+    if (mgcm_cg2d_tiles(g.sh[c.shard].m, c.t0, c.nT)) die(w);
+  }
+  barrier_all(w);
+  for (auto &c : g.cgLeads) copy_blocks(w, "cg2d_x", c.shard, c.t0, c.nT);
+  barrier_all(w);
+  phase_all(w, 13);
+}
+// INTEGR_CONTINUITY: the column pass on the own tiles, then (exactConserv) the new free
+// surface's blocks to every model and EXCH(eta) + UPDATE_ETAH everywhere
+void op_continuity(const char *w) {
+  if (!multi()) return run_all(w, mgcm_integr_continuity);
+  phase_all(w, 14);
+  if (!g.exactConserv) return;
+  gather2d(w, "cg2d_b");
+  phase_all(w, 15);
+}
+// DO_FIELDS_BLOCKING_EXCHANGES: the halo sources between models, then every local fill
+void op_blocking(const char *w) {
+  if (multi()) xfer3d(w, 0);
+  run_all(w, mgcm_blocking_exchanges);
+}
+
 // The device's iteration counter (AB2's first step, the CD scheme's start), written only
 // when it changes (FORWARD_STEP advances myIter after DYNAMICS, forward_step.F:806), in
 // stream order: no host synchronisation.
 void set_iter(const char *where, int myIter) {
   if (g.devIter == myIter) return;
-  if (mgcm_set_iter(g.m, myIter)) die(where);
+  for (auto &s : g.sh) {
+    hipchk(hipSetDevice(s.dev), where);
+    if (mgcm_set_iter(s.m, myIter)) die(where);
+  }
   g.devIter = myIter;
 }
 
-// kinds: bit k set = move the arrays of kind k
+// kinds: bit k set = move the arrays of kind k (to every model: each holds the domain)
 void upload(const char *where, unsigned kinds) {
   std::vector<double> tmp;
   for (auto &b : g.bound) {
@@ -106,19 +296,42 @@ void upload(const char *where, unsigned kinds) {
       for (long q = 0; q < b.count; q++) tmp[q] = b.host[q * b.stride + b.off];
       src = tmp.data();
     }
-    if (mgcm_put(g.m, b.name.c_str(), src, b.count)) die(where);
+    for (auto &s : g.sh) {
+      hipchk(hipSetDevice(s.dev), where);
+      if (mgcm_put(s.m, b.name.c_str(), src, b.count)) die(where);
+    }
     g.nUp++;
     g.bytesUp += 8.0 * b.count;
   }
 }
 
+void sync_all(const char *where) {
+  for (auto &s : g.sh)
+    if (mgcm_sync(s.m)) die(where);
+}
+
+// The state down: a tiled array (2-D or 3-D, tile-major) block by block from each tile's
+// owner, anything else (1-D profiles) from model 0.
 void download(const char *where) {
-  if (mgcm_sync(g.m)) die(where);
+  sync_all(where);
+  const long per2 = n2(), per3 = per2 * g.dims[4], nt = nTiles();
   std::vector<double> tmp;
   for (auto &b : g.bound) {
     if (b.kind != 0) continue;   // static and host-input arrays are never written on the device
     g.nDown++;
     g.bytesDown += 8.0 * b.count;
+    const long per = b.count == per2 * nt ? per2 : b.count == per3 * nt ? per3 : 0;
+    if (multi() && per && b.stride == 1) {
+      for (auto &s : g.sh) {
+        const double *dp = mgcm_device_ptr(s.m, b.name.c_str());
+        if (!dp) die(where);
+        hipchk(hipSetDevice(s.dev), where);
+        hipchk(hipMemcpy(b.host + s.t0 * per, dp + s.t0 * per, (size_t)s.nT * per * sizeof(double),
+                         hipMemcpyDeviceToHost),
+               where);
+      }
+      continue;
+    }
     if (b.stride == 1) {
       if (mgcm_get(g.m, b.name.c_str(), b.host, b.count)) die(where);
       continue;
@@ -141,7 +354,7 @@ void enter_time_loop(const char *where) {
 
 // One routine drop-in.  Host-authoritative (initialisation): state in, the device
 // routine, state out.  Device-authoritative: the host input first when `input`.
-void routine(const char *where, int (*fn)(mgcm_model *), int myIter, double myTime, bool input = false) {
+void routine(const char *where, void (*op)(const char *), int myIter, double myTime, bool input = false) {
   model(where);
   if (!g.ready) die(where, "called before MGCM_AMD_INIT");
   g.lastIter = myIter;
@@ -149,13 +362,121 @@ void routine(const char *where, int (*fn)(mgcm_model *), int myIter, double myTi
   if (!g.deviceAuth) {
     upload(where, K_STATE | K_INPUT);
     set_iter(where, myIter);
-    if (fn(g.m)) die(where);
+    op(where);
     download(where);
     return;
   }
   if (input) upload(where, K_INPUT);
   set_iter(where, myIter);
-  if (fn(g.m)) die(where);
+  op(where);
+}
+
+// Partition and wiring of N device models (MGCM_AMD_MODELS), after mgcm_init of each: tile
+// ranges, the CG2D mode and its per-GPU leads, the halo-source links, the barrier events.
+void setup_shards(const char *where) {
+  const int N = (int)g.sh.size(), nt = (int)nTiles();
+  const int base = nt / N, rem = nt % N;
+  for (int i = 0, t = 0; i < N; i++) {
+    Shard &s = g.sh[i];
+    s.t0 = t;
+    s.nT = base + (i < rem ? 1 : 0);
+    t += s.nT;
+    hipchk(hipSetDevice(s.dev), where);
+    if (!s.ev) hipchk(hipEventCreateWithFlags(&s.ev, hipEventDisableTiming), where);
+    if (mgcm_set_tile_range(s.m, s.t0, s.nT)) die(where);
+  }
+  g.exactConserv = mgcm_get_param(g.m, "exactConserv") != 0.0;
+  // CG2D: the multi-workgroup solver runs tile-sharded (one launch per GPU); a single-CU
+  // kernel solves the gathered domain on every model
+  g.cgDevice = mgcm_get_param(g.m, "cg2dKernel") == 4.0;
+  g.cgLeads.clear();
+  for (int i = 0; i < N; i++) {
+    if (!g.cgLeads.empty() && g.sh[g.cgLeads.back().shard].dev == g.sh[i].dev) {
+      g.cgLeads.back().nT += g.sh[i].nT;
+      continue;
+    }
+    for (auto &c : g.cgLeads)
+      if (g.sh[c.shard].dev == g.sh[i].dev) die(where, "the models of one GPU must own contiguous tiles (MGCM_AMD_DEVICES)");
+    g.cgLeads.push_back(CgLead{i, g.sh[i].t0, g.sh[i].nT});
+  }
+  if (g.cgDevice && g.cgLeads.size() > 1)
+    for (auto &c : g.cgLeads)
+      if (mgcm_cg2d_share(g.sh[c.shard].m, g.sh[g.cgLeads[0].shard].m)) die(where);
+  // peer access between the GPUs in use (device-to-device copies)
+  for (auto &a : g.sh)
+    for (auto &b : g.sh)
+      if (a.dev != b.dev) {
+        hipchk(hipSetDevice(a.dev), where);
+        const hipError_t e = hipDeviceEnablePeerAccess(b.dev, 0);
+        if (e != hipSuccess && e != hipErrorPeerAccessAlreadyEnabled) die(where, hipGetErrorString(e));
+        (void)hipGetLastError();
+      }
+  // links: for every model d, the sources its halos read in another model's tiles
+  const int Nr = g.dims[4];
+  int nfMax = 0;
+  for (int grp = 0; grp < 3; grp++) nfMax = std::max(nfMax, mgcm_exchange_nfields_group(g.m, grp));
+  const long per2 = n2();
+  for (int d = 0; d < N; d++) {
+    const Shard &sd = g.sh[d];
+    const long cnt = mgcm_halo_sources(sd.m, sd.t0, sd.nT, nullptr, 0);
+    if (cnt < 0) die(where);
+    std::vector<long> src((size_t)cnt);
+    if (cnt && mgcm_halo_sources(sd.m, sd.t0, sd.nT, src.data(), cnt) != cnt) die(where);
+    for (int sIdx = 0; sIdx < N; sIdx++) {
+      if (sIdx == d) continue;
+      const Shard &ss = g.sh[sIdx];
+      std::vector<long> mine;
+      for (long v : src)
+        if (v >= ss.t0 * per2 && v < (ss.t0 + ss.nT) * per2) mine.push_back(v);
+      if (mine.empty()) continue;
+      Link L;
+      L.s = sIdx;
+      L.d = d;
+      L.n = (long)mine.size();
+      const size_t ib = mine.size() * sizeof(long), bb = (size_t)std::max(1, nfMax) * Nr * mine.size() * sizeof(double);
+      hipchk(hipSetDevice(ss.dev), where);
+      hipchk(hipMalloc(&L.idxS, ib), where);
+      hipchk(hipMalloc(&L.sbuf, bb), where);
+      hipchk(hipMemcpy(L.idxS, mine.data(), ib, hipMemcpyHostToDevice), where);
+      hipchk(hipEventCreateWithFlags(&L.ev, hipEventDisableTiming), where);
+      hipchk(hipSetDevice(sd.dev), where);
+      hipchk(hipMalloc(&L.idxD, ib), where);
+      hipchk(hipMalloc(&L.rbuf, bb), where);
+      hipchk(hipMemcpy(L.idxD, mine.data(), ib, hipMemcpyHostToDevice), where);
+      g.links.push_back(L);
+    }
+  }
+}
+
+void free_links() {
+  for (auto &L : g.links) {
+    (void)hipSetDevice(g.sh[L.s].dev);
+    (void)hipFree(L.idxS);
+    (void)hipFree(L.sbuf);
+    if (L.ev) (void)hipEventDestroy(L.ev);
+    (void)hipSetDevice(g.sh[L.d].dev);
+    (void)hipFree(L.idxD);
+    (void)hipFree(L.rbuf);
+  }
+  g.links.clear();
+  g.cgLeads.clear();
+}
+void free_shards() {
+  free_links();
+  for (auto &s : g.sh) {
+    if (s.ev) { (void)hipSetDevice(s.dev); (void)hipEventDestroy(s.ev); }
+    if (s.m) mgcm_destroy(s.m);
+  }
+  g.sh.clear();
+  g.m = nullptr;
+}
+
+// A drop-in FORWARD_STEP calls after it advances myIter / myTime (forward_step.F:806-807):
+// the step's end time, for the host-reader test of DO_FIELDS_BLOCKING_EXCHANGES.
+void advanced(int myIter, double myTime) {
+  g.advValid = true;
+  g.advIter = myIter;
+  g.advTime = myTime;
 }
 
 // eesupp/src/different_multiple.F: is val1 the step nearest to a multiple of freq?
@@ -163,7 +484,7 @@ bool different_multiple(double freq, double val1, double step) {
   if (freq == 0.0) return false;
   if (fabs(step) > freq) return true;
   const double v1 = val1, v2 = val1 - step, v3 = val1 + step;
-  const double v4 = nearbyint(v1 / freq) * freq;
+  const double v4 = round(v1 / freq) * freq;   // NINT: half away from zero
   const double d1 = v1 - v4, d2 = v2 - v4, d3 = v3 - v4;
   return fabs(d1) < fabs(d2) && fabs(d1) <= fabs(d3);
 }
@@ -173,7 +494,7 @@ bool different_multiple(double freq, double val1, double step) {
 // (do_write_pickup.F:61-63, modelEnd) -- a superset is harmless, a miss is not.
 bool host_reads_state(double myTime, int myIter) {
   const Readers &r = g.rd;
-  return myIter == r.nEndIter || different_multiple(r.monitorFreq, myTime, r.deltaTClock) ||
+  return r.everyStep || myIter == r.nEndIter || different_multiple(r.monitorFreq, myTime, r.deltaTClock) ||
          different_multiple(r.dumpFreq, myTime, r.deltaTClock) ||
          different_multiple(r.chkPtFreq, myTime, r.deltaTClock) ||
          different_multiple(r.pChkPtFreq, myTime, r.deltaTClock);
@@ -191,17 +512,45 @@ extern "C" {
 
 // --------------------------------------------------------------------- set-up
 /* The tile set of SIZE.h; nProcs = nPx*nPy and nThreads = nTx*nTy must be 1 (one host
- * process and thread per model, SURVEY.md 8(b) "Threading").  Re-creates the model when
- * the sizes change. */
+ * process and thread: the MPI decomposition of eesupp is not taken over, SURVEY.md 8(b)
+ * "Threading"; the tiles go over GPUs inside the process instead: MGCM_AMD_MODELS device
+ * models, see the top of this file).  Re-creates the models when the sizes change. */
 void mgcm_amd_setup_(const int *sNx, const int *sNy, const int *OLx, const int *OLy, const int *Nr, const int *nSx,
                      const int *nSy, const int *nProcs, const int *nThreads) {
-  if (*nProcs != 1 || *nThreads != 1) die("MGCM_AMD_SETUP", "the drop-ins need nPx*nPy = nTx*nTy = 1");
+  if (*nProcs != 1 || *nThreads != 1)
+    die("MGCM_AMD_SETUP", "the drop-ins need nPx*nPy = nTx*nTy = 1 (tiles go over GPUs by MGCM_AMD_MODELS)");
   const int d[7] = {*sNx, *sNy, *OLx, *OLy, *Nr, *nSx, *nSy};
   if (g.m && memcmp(d, g.dims, sizeof d) == 0) return;
-  if (g.m) mgcm_destroy(g.m);
+  if (g.m) free_shards();
   g = FortranSide{};
-  g.m = mgcm_create(d[0], d[1], d[2], d[3], d[4], d[5], d[6], 0);
-  if (!g.m) die("MGCM_AMD_SETUP");
+  const int nt = d[5] * d[6];
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev < 1) die("MGCM_AMD_SETUP", "no HIP device");
+  int N = 1;
+  if (const char *e = getenv("MGCM_AMD_MODELS")) N = strcmp(e, "auto") == 0 ? std::min(nt, ndev) : atoi(e);
+  if (N < 1 || N > nt) die("MGCM_AMD_SETUP", "MGCM_AMD_MODELS must be 1 .. the number of tiles (or auto)");
+  std::vector<int> devs((size_t)N);
+  for (int i = 0; i < N; i++) devs[i] = (int)(((long)i * ndev) / N);   // contiguous blocks of models per GPU
+  if (const char *e = getenv("MGCM_AMD_DEVICES")) {
+    std::string l(e);
+    size_t pos = 0;
+    for (int i = 0; i < N; i++) {
+      if (pos > l.size()) die("MGCM_AMD_SETUP", "MGCM_AMD_DEVICES: one GPU per model (comma separated)");
+      const size_t c = l.find(',', pos);
+      devs[i] = atoi(l.substr(pos, c == std::string::npos ? std::string::npos : c - pos).c_str());
+      pos = c == std::string::npos ? l.size() + 1 : c + 1;
+      if (devs[i] < 0 || devs[i] >= ndev) die("MGCM_AMD_SETUP", "MGCM_AMD_DEVICES names a GPU that does not exist");
+    }
+  }
+  for (int i = 0; i < N; i++) {
+    Shard s;
+    s.dev = devs[i];
+    s.m = mgcm_create(d[0], d[1], d[2], d[3], d[4], d[5], d[6], s.dev);
+    if (!s.m) die("MGCM_AMD_SETUP");
+    s.nT = nt;
+    g.sh.push_back(s);
+  }
+  g.m = g.sh[0].m;
   memcpy(g.dims, d, sizeof d);
 }
 
@@ -218,8 +567,10 @@ void mgcm_amd_set_maps_(const double *ids, const double *u1, const double *v1, c
     src[q] = (long)ids[q];
     cu1[q] = (long)u1[q]; cv1[q] = (long)v1[q]; cu0[q] = (long)u0[q]; cv0[q] = (long)v0[q];
   }
-  if (mgcm_set_halo_map(g.m, src.data(), n)) die("MGCM_AMD_SET_MAPS");
-  if (mgcm_set_uv_map(g.m, cu1.data(), cv1.data(), cu0.data(), cv0.data(), tFace, tEdge, n)) die("MGCM_AMD_SET_MAPS");
+  for (auto &s : g.sh) {
+    if (mgcm_set_halo_map(s.m, src.data(), n)) die("MGCM_AMD_SET_MAPS");
+    if (mgcm_set_uv_map(s.m, cu1.data(), cv1.data(), cu0.data(), cv0.data(), tFace, tEdge, n)) die("MGCM_AMD_SET_MAPS");
+  }
   g.ready = false;
 }
 
@@ -234,8 +585,23 @@ void mgcm_amd_param_(const char *name, const double *value, size_t len) {
   if (n == "chkPtFreq") { r.chkPtFreq = *value; return; }
   if (n == "pChkPtFreq") { r.pChkPtFreq = *value; return; }
   if (n == "nEndIter") { r.nEndIter = (int)*value; return; }
+  if (n == "useSBO") { r.everyStep = r.everyStep || *value != 0.0; return; }
+  if (n == "useDiagnostics") {
+    if (*value == 0.0) return;
+    // DO_STATEVARS_DIAGS (forward_step.F:513) reads the state each step; the fills inside the
+    // shadowed routines (DYNAMICS, THERMODYNAMICS, DO_OCEANIC_PHYS) are not made on the device
+    const char *e = getenv("MGCM_AMD_DIAGNOSTICS");
+    if (!e || strcmp(e, "state") != 0)
+      die("MGCM_AMD_PARAM", "useDiagnostics: the device routines do not fill diagnostics (set "
+                            "MGCM_AMD_DIAGNOSTICS=state for the state variables only, downloaded every step)");
+    fprintf(stderr, "MGCM_AMD: useDiagnostics with MGCM_AMD_DIAGNOSTICS=state: state diagnostics only, "
+                    "the state comes down after every step\n");
+    r.everyStep = true;
+    return;
+  }
   if (n == "deltaTClock") r.deltaTClock = *value;
-  if (mgcm_set_param(g.m, n.c_str(), *value)) die("MGCM_AMD_PARAM");
+  for (auto &s : g.sh)
+    if (mgcm_set_param(s.m, n.c_str(), *value)) die("MGCM_AMD_PARAM");
   g.ready = false;
 }
 
@@ -278,13 +644,27 @@ void mgcm_amd_init_(const int *myIter) {
   model("MGCM_AMD_INIT");
   // device options with no PARAMS.h counterpart, from the environment:
   // MGCM_CG2D_REFORDER=1 sums CG2D in the reference's order (cg2dRefOrder, parity runs)
-  if (const char *e = getenv("MGCM_CG2D_REFORDER"))
-    if (mgcm_set_param(g.m, "cg2dRefOrder", atof(e))) die("MGCM_AMD_INIT");
+  // (several models: each is set up on the whole domain -- the CG2D tables too -- and only
+  // then restricted to its tiles, setup_shards)
+  free_links();
+  for (auto &s : g.sh) {
+    if (const char *e = getenv("MGCM_CG2D_REFORDER"))
+      if (mgcm_set_param(s.m, "cg2dRefOrder", atof(e))) die("MGCM_AMD_INIT");
+    // MGCM_CG2D_MWG=1: the multi-workgroup CG2D where a single-CU kernel would solve (the
+    // device-sharded solve on a small grid: tests, rehearsals)
+    if (const char *e = getenv("MGCM_CG2D_MWG"))
+      if (mgcm_set_param(s.m, "cg2dForceMwg", atof(e))) die("MGCM_AMD_INIT");
+    if (multi() && mgcm_set_tile_range(s.m, 0, (int)nTiles())) die("MGCM_AMD_INIT");
+  }
   upload("MGCM_AMD_INIT", K_STATIC | K_STATE | K_INPUT);
-  if (mgcm_set_param(g.m, "myIter", (double)*myIter)) die("MGCM_AMD_INIT");
-  if (mgcm_init(g.m)) die("MGCM_AMD_INIT");
+  for (auto &s : g.sh) {
+    if (mgcm_set_param(s.m, "myIter", (double)*myIter)) die("MGCM_AMD_INIT");
+    if (mgcm_init(s.m)) die("MGCM_AMD_INIT");
+  }
   upload("MGCM_AMD_INIT", K_STATE | K_INPUT);
-  if (mgcm_set_param(g.m, "myIter", (double)*myIter)) die("MGCM_AMD_INIT");
+  for (auto &s : g.sh)
+    if (mgcm_set_param(s.m, "myIter", (double)*myIter)) die("MGCM_AMD_INIT");
+  if (multi()) setup_shards("MGCM_AMD_INIT");
   g.devIter = *myIter;
   g.deviceAuth = false;
   g.ready = true;
@@ -308,7 +688,8 @@ void mgcm_amd_device_sync_(const int *myThid) {
 /* Waits for the device work issued so far (a timing aid for hosts that clock steps). */
 void mgcm_amd_step_fence_(const int *myThid) {
   (void)myThid;
-  if (mgcm_sync(model("MGCM_AMD_STEP_FENCE"))) die("MGCM_AMD_STEP_FENCE");
+  model("MGCM_AMD_STEP_FENCE");
+  sync_all("MGCM_AMD_STEP_FENCE");
 }
 
 /* Whole-array copies so far (uploads, downloads) and their bytes. */
@@ -324,19 +705,20 @@ void mgcm_amd_transfer_stats_(int *nUploads, int *nDownloads, double *bytesUp, d
 void do_oceanic_phys_amd_(const double *myTime, const int *myIter, const int *myThid) {
   (void)myThid;
   enter_time_loop("DO_OCEANIC_PHYS_AMD");
-  routine("DO_OCEANIC_PHYS_AMD", mgcm_oceanic_phys, *myIter, *myTime, true);
+  g.advValid = false;   // a new step: its end time is not known yet
+  routine("DO_OCEANIC_PHYS_AMD", op_oceanic_phys, *myIter, *myTime, true);
 }
 /* SUBROUTINE THERMODYNAMICS(myTime, myIter, myThid)      model/src/thermodynamics.F:25 */
 void thermodynamics_amd_(const double *myTime, const int *myIter, const int *myThid) {
   (void)myThid;
   enter_time_loop("THERMODYNAMICS_AMD");
-  routine("THERMODYNAMICS_AMD", mgcm_tracer_step, *myIter, *myTime);
+  routine("THERMODYNAMICS_AMD", op_tracer_step, *myIter, *myTime);
 }
 /* SUBROUTINE DYNAMICS(myTime, myIter, myThid)            model/src/dynamics.F:21 */
 void dynamics_amd_(const double *myTime, const int *myIter, const int *myThid) {
   (void)myThid;
   enter_time_loop("DYNAMICS_AMD");
-  routine("DYNAMICS_AMD", mgcm_dynamics, *myIter, *myTime);
+  routine("DYNAMICS_AMD", op_dynamics, *myIter, *myTime);
 }
 /* SUBROUTINE UPDATE_R_STAR(useLatest, myTime, myIter, myThid)   model/src/update_r_star.F:6
  * useLatest = .TRUE. (forward_step.F:838): the new r* factors and hFac, and UPDATE_CG2D's
@@ -346,7 +728,10 @@ void dynamics_amd_(const double *myTime, const int *myIter, const int *myThid) {
  * already holds: nothing to do. */
 void update_r_star_amd_(const int *useLatest, const double *myTime, const int *myIter, const int *myThid) {
   (void)myThid;
-  if (*useLatest) routine("UPDATE_R_STAR_AMD", mgcm_update_r_star, *myIter, *myTime);
+  if (*useLatest) {
+    advanced(*myIter, *myTime);
+    routine("UPDATE_R_STAR_AMD", op_update_r_star, *myIter, *myTime);
+  }
 }
 /* SUBROUTINE UPDATE_CG2D(myTime, myIter, myThid)         model/src/update_cg2d.F:7
  * Folded into UPDATE_R_STAR_AMD(.TRUE.), which FORWARD_STEP calls just before it. */
@@ -360,18 +745,21 @@ void calc_r_star_amd_(const double *etaFld, const double *myTime, const int *myI
   (void)myThid;
   const Bound *b = bound_at(etaFld);
   if (!b || b->name != "etaH") die("CALC_R_STAR_AMD", "etaFld must be the bound etaH");
-  routine("CALC_R_STAR_AMD", mgcm_calc_r_star, *myIter, *myTime);
+  advanced(*myIter, *myTime);
+  routine("CALC_R_STAR_AMD", op_calc_r_star, *myIter, *myTime);
 }
 /* SUBROUTINE SOLVE_FOR_PRESSURE(myTime, myIter, myThid)  model/src/solve_for_pressure.F:7 */
 void solve_for_pressure_amd_(const double *myTime, const int *myIter, const int *myThid) {
   (void)myThid;
-  routine("SOLVE_FOR_PRESSURE_AMD", mgcm_solve_for_pressure, *myIter, *myTime);
+  advanced(*myIter, *myTime);
+  routine("SOLVE_FOR_PRESSURE_AMD", op_solve, *myIter, *myTime);
 }
 /* SUBROUTINE MOMENTUM_CORRECTION_STEP(myTime, myIter, myThid)
  *                                                   model/src/momentum_correction_step.F:7 */
 void momentum_correction_step_amd_(const double *myTime, const int *myIter, const int *myThid) {
   (void)myThid;
-  routine("MOMENTUM_CORRECTION_STEP_AMD", mgcm_momentum_correction_step, *myIter, *myTime);
+  advanced(*myIter, *myTime);
+  routine("MOMENTUM_CORRECTION_STEP_AMD", op_correction, *myIter, *myTime);
 }
 /* SUBROUTINE INTEGR_CONTINUITY(uFld, vFld, myTime, myIter, myThid)
  *                                                   model/src/integr_continuity.F:13
@@ -382,17 +770,19 @@ void integr_continuity_amd_(const double *uFld, const double *vFld, const double
   const Bound *bu = bound_at(uFld), *bv = bound_at(vFld);
   if (!bu || !bv || bu->name != "uVel" || bv->name != "vVel")
     die("INTEGR_CONTINUITY_AMD", "uFld, vFld must be the bound uVel, vVel");
-  routine("INTEGR_CONTINUITY_AMD", mgcm_integr_continuity, *myIter, *myTime);
+  advanced(*myIter, *myTime);
+  routine("INTEGR_CONTINUITY_AMD", op_continuity, *myIter, *myTime);
 }
 /* SUBROUTINE DO_FIELDS_BLOCKING_EXCHANGES(myThid)   model/src/do_fields_blocking_exchanges.F:7 */
 /* The last device routine of a step: the state comes down when a host routine reads it
- * next (MONITOR / DO_THE_MODEL_IO / DO_WRITE_PICKUP at this step's end time, known from
- * the step's earlier drop-ins, which FORWARD_STEP calls with the advanced myTime). */
+ * next (MONITOR / DO_THE_MODEL_IO / DO_WRITE_PICKUP at this step's end time: the advanced
+ * myTime / myIter of the step's drop-ins after forward_step.F:806, or, when none of them ran
+ * -- momStepping and calc_wVelocity both off -- one deltaTClock past the step's start). */
 void do_fields_blocking_exchanges_amd_(const int *myThid) {
   (void)myThid;
-  const int it = g.lastIter;
-  const double t = g.lastTime;
-  routine("DO_FIELDS_BLOCKING_EXCHANGES_AMD", mgcm_blocking_exchanges, it, t);
+  const int it = g.advValid ? g.advIter : g.lastIter + 1;
+  const double t = g.advValid ? g.advTime : g.lastTime + g.rd.deltaTClock;
+  routine("DO_FIELDS_BLOCKING_EXCHANGES_AMD", op_blocking, it, t);
   if (g.deviceAuth && host_reads_state(t, it)) download("DO_FIELDS_BLOCKING_EXCHANGES_AMD");
 }
 

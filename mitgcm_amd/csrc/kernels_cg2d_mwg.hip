@@ -117,10 +117,14 @@ __device__ __forceinline__ bool gran_get(gu64 *g, unsigned tag, double &v) {
   v = __builtin_bit_cast(double, ((hi & 0xffffffffull) << 32) | (lo & 0xffffffffull));
   return (unsigned)(lo >> 32) == tag && (unsigned)(hi >> 32) == tag;
 }
-// Launch epochs: ctr[0] holds the epoch, read by every part at its start and advanced by
-// part 0 after the last hand-off (every part has read it by then); a granule's tag is
-// (epoch mod 2^16) << 16 | phase, so no memset is needed between launches.  The timeout
-// word ctr[1] holds epoch + 1 of a launch that gave up (the epoch then advances by 2).
+// Launch epochs: each process keeps its own epoch word (T.epoch, never shared), read by its
+// parts at their start and advanced by its launch's first part g0 after the last hand-off
+// (every part of the solve has read its epoch by then: g0's last hand-off needs every part's
+// partial).  Every process launches the same solves in the same order, so the epochs agree
+// without any process reading another's counter (a shared counter advanced by one process
+// could be read stale by a process whose next launch starts first).  A granule's tag is
+// (epoch mod 2^16) << 16 | phase, so no memset is needed between launches.  The timeout word
+// ctr[1] (shared) holds epoch + 1 of a launch that gave up (the epoch then advances by 2).
 __device__ __forceinline__ unsigned mw_tag(unsigned ep, int phase) { return ((ep & 0xffffu) << 16) | (unsigned)phase; }
 // bounded spin: after ~2^22 passes every part gives up (timeout word), so no wave hangs
 template <bool SYS = false>
@@ -282,7 +286,7 @@ __global__ void __launch_bounds__(MW_NT) k_cg2d_mwg(Dims d, Params p, Fields f, 
   double *imp_l = red + 16 * 16;      // IMAX: the ring q handed off at the last reduction
   const int tid = threadIdx.x;
   int nsync = 0;
-  const unsigned ep = __hip_atomic_load((gu32 *)T.ctr, RLX_SCOPE(SYS));
+  const unsigned ep = __hip_atomic_load((gu32 *)T.epoch, RLX_AGENT);
   const size_t go = (size_t)g * NO, gr = (size_t)g * NR, gi = (size_t)g * T.IMAX;
   // ---- owned points: offsets, neighbour slots, coefficients (cg2d.F operator rows)
   int G2[MW_OPT];
@@ -476,8 +480,8 @@ __global__ void __launch_bounds__(MW_NT) k_cg2d_mwg(Dims d, Params p, Fields f, 
     if (p.cg2dNormaliseRHS) xv = xv / rhsNorm;
     if (G2[m] >= 0) f.cg2d_x[G2[m]] = xv;
   }
-  // the record by the launch's first part (every part holds the same reduced values); the
-  // epoch by part 0 of the whole solve
+  // the record and this process's next epoch by the launch's first part (every part holds the
+  // same reduced values)
   if (g == g0 && tid == 0) {
     const int st = stepCounter ? *stepCounter : 0;
     SolveRecord &R = rec[st];
@@ -489,11 +493,10 @@ __global__ void __launch_bounds__(MW_NT) k_cg2d_mwg(Dims d, Params p, Fields f, 
     const bool tmo = __hip_atomic_load((gu32 *)T.ctr + 1, RLX_SCOPE(SYS)) == ep + 1u;
     R.numIters = (ok && !tmo) ? actualIts : -1;   // -1: a grid hand-off timed out
     R.nIterMin = -1;
-    if (g != 0) return;
     // the next launch's epoch; after a timeout it skips one, so a part of this launch that
     // starts late (reading ep + 1, tagging with it, failing into the timeout word as ep + 2)
     // can neither match the next launch's tags nor fail it
-    __hip_atomic_store((gu32 *)T.ctr, R.numIters < 0 ? ep + 2u : ep + 1u, RLX_SCOPE(SYS));
+    __hip_atomic_store((gu32 *)T.epoch, R.numIters < 0 ? ep + 2u : ep + 1u, RLX_AGENT);
   }
 #undef LO
 #undef HI

@@ -180,6 +180,8 @@ struct mgcm_model {
   long *d_halo = nullptr;
   long *d_srcOf = nullptr;    // per 2-D point: interior source of a halo point, -1 otherwise
   int nHalo = 0;
+  long *d_haloAll = nullptr;  // the map of EVERY tile's halo when this model steps a tile subset
+  int nHaloAll = 0;           // (EXCH_*_RL on host arrays, mgcm_exchange_host, covers the domain)
   std::vector<long> h_halo;
   unsigned *d_nbr = nullptr;  // packed (W|E<<16),(S|N<<16) compact neighbour indices, padded
   int *d_gofs = nullptr;      // 2-D flat offset of each (padded) interior point
@@ -200,6 +202,7 @@ struct mgcm_model {
   MwgTables mwg{};
   std::vector<void *> mwgAllocs;
   void *mwgShared = nullptr;   // another process's hand-off block, opened by IPC (mgcm_cg2d_shared_import)
+  void *mwgBlock = nullptr;    // this model's own hand-off block (hipMalloc, or uncached once shared)
   std::vector<int> mwgPlan;   // summation plan for mgcm_cg2d_sum_plan: [(g*OPT + p)*NT + tid]
   // EXCH2 C-grid vector maps (mgcm_set_uv_map): [withSigns] -> (dst, code) pairs of this
   // process's tiles, u entries first; code = +-(src+1), src indexing [u | v]
@@ -334,6 +337,13 @@ static int upload_halo(mgcm_model *m) {
   for (size_t h = 0; h + 1 < m->h_halo.size(); h += 2)
     if (m->h_halo[h] >= lo && m->h_halo[h] < hi) { loc.push_back(m->h_halo[h]); loc.push_back(m->h_halo[h + 1]); }
   m->nHalo = (int)(loc.size() / 2);
+  if (m->d_haloAll) { hipFree(m->d_haloAll); m->d_haloAll = nullptr; }
+  m->nHaloAll = 0;
+  if (m->d.nT < m->d.nTiles && !m->h_halo.empty()) {
+    HIPCHK(hipMalloc(&m->d_haloAll, m->h_halo.size() * sizeof(long)));
+    HIPCHK(hipMemcpy(m->d_haloAll, m->h_halo.data(), m->h_halo.size() * sizeof(long), hipMemcpyHostToDevice));
+    m->nHaloAll = (int)(m->h_halo.size() / 2);
+  }
   if (m->uvMap) {
     const long N2 = m->d.n2 * m->d.nTiles;
     for (int all = 0; all < 2; all++)
@@ -695,6 +705,13 @@ static int build_mwg(mgcm_model *m) {
   HIPCHK(hipMalloc(&blk, hs));
   HIPCHK(hipMemset(blk, 0, hs));
   m->mwgAllocs.push_back(blk);
+  m->mwgBlock = blk;
+  // this process's launch epoch: its own word (not in the hand-off block an IPC import replaces)
+  unsigned *ep = nullptr;
+  HIPCHK(hipMalloc(&ep, 64));
+  HIPCHK(hipMemset(ep, 0, 64));
+  m->mwgAllocs.push_back(ep);
+  T.epoch = ep;
   T.ctr = (unsigned *)blk;
   T.part = (unsigned long long *)(blk + 64);
   T.xs = T.part + partGr;
@@ -822,6 +839,7 @@ void mgcm_destroy(mgcm_model *m) {
   if (m->monBuf) hipFree(m->monBuf);
   if (m->d_halo) hipFree(m->d_halo);
   if (m->d_srcOf) hipFree(m->d_srcOf);
+  if (m->d_haloAll) hipFree(m->d_haloAll);
   for (int q = 0; q < 2; q++) {
     if (m->d_uv[q]) hipFree(m->d_uv[q]);
     if (m->d_uvAll[q]) hipFree(m->d_uvAll[q]);
@@ -1355,11 +1373,16 @@ int mgcm_exchange_host(mgcm_model *m, double *u, double *v, int nz, int vector, 
   double *host[2] = {u, v};
   for (int c = 0; c < 2; c++)
     if (host[c]) HIPCHK(hipMemcpyAsync(m->exchBuf[c], host[c], bytes, hipMemcpyHostToDevice, m->stream));
-  if (vector) {
-    if (exchange_uv(m, m->exchBuf[0], m->exchBuf[1], nz, withSigns != 0)) return -1;
+  // every tile's halo, also when this model steps a tile subset (the host array is the domain)
+  const long *hmap = m->d_haloAll ? m->d_haloAll : m->d_halo;
+  const int nh = m->d_haloAll ? m->nHaloAll : m->nHalo;
+  if (vector && m->uvMap) {
+    const int w = withSigns ? 1 : 0;
+    HIPCHK(launch_exchange_uv(m->d, m->exchBuf[0], m->exchBuf[1], m->d_uvAll[w], m->nUvUAll[w], m->nUvVAll[w], nz,
+                              m->stream));
   } else {
     for (int c = 0; c < 2; c++)
-      if (host[c]) HIPCHK(launch_exchange(m->d, m->exchBuf[c], m->d_halo, m->nHalo, nz, m->stream));
+      if (host[c]) HIPCHK(launch_exchange(m->d, m->exchBuf[c], hmap, nh, nz, m->stream));
   }
   for (int c = 0; c < 2; c++)
     if (host[c]) HIPCHK(hipMemcpyAsync(host[c], m->exchBuf[c], bytes, hipMemcpyDeviceToHost, m->stream));
@@ -1767,6 +1790,8 @@ int mgcm_tile_copy(mgcm_model *m, const char *name, int t0, int nT, void *buf, i
   return 0;
 }
 
+static int mwg_block_uncached(mgcm_model *m);
+
 // The tile-sharded device CG2D: every process launches the multi-workgroup solver's parts
 // of its own tiles, all on ONE hand-off block (granules, epoch, timeout word), which the
 // first process exports by IPC and the others map; every granule access is then at system
@@ -1776,10 +1801,11 @@ int mgcm_cg2d_shared_export(mgcm_model *m, void *handle) {
     return set_err("mgcm_cg2d_shared_export: needs the multi-workgroup CG2D on whole-domain tables (cg2dForceMwg)");
   HIPCHK(hipSetDevice(m->device));
   HIPCHK(hipStreamSynchronize(m->stream));
+  // the importers' launches may run on other GPUs: an uncached block (mwg_block_uncached)
+  if (mwg_block_uncached(m)) return -1;
   hipIpcMemHandle_t h;
   HIPCHK(hipIpcGetMemHandle(&h, (void *)m->mwg.ctr));
   memcpy(handle, &h, sizeof h);
-  m->mwg.sys = 1;
   return 0;
 }
 
@@ -1880,8 +1906,120 @@ int mgcm_step_phase(mgcm_model *m, int phase) {
       TIMED(K_EXCH, launch_exchange_multi(m->d, blocking_fields(m), m->d_halo, m->nHalo, m->d_ctr, m->stream));
       m->lastBatch++;
       return 0;
+    // the routine-level split of a sharded step (one Fortran host stepping several models,
+    // fortran_abi.hip: the reference's routine boundaries with the cross-model copies between)
+    case 11:  // SOLVE_FOR_PRESSURE's right-hand side (CALC_DIV_GHAT) on this model's tiles
+      TIMED(K_RHS, launch_sfp_rhs(m->d, m->p, m->f, m->stream));
+      return 0;
+    case 12:  // CG2D on the whole (gathered) domain + EXCH_XY_RL(cg2d_x) + etaN everywhere
+      TIMED(K_CG2D, launch_cg2d(m, m->p.cg2dMaxIters, m->p.cg2dUseMinResSol - 1));
+      [[fallthrough]];
+    case 13:  // EXCH_XY_RL(cg2d_x) + etaN everywhere, after a CG2D done by phase 10 / mgcm_cg2d_tiles
+      TIMED(K_ETA, launch_exch_eta(m->d, m->p, m->f, m->d_srcOf, false, 0, m->stream));
+      return 0;
+    case 14:  // INTEGR_CONTINUITY's column pass (after MOMENTUM_CORRECTION_STEP) on this model's tiles
+      TIMED(K_CONT, launch_corr_cont(m->d, m->p, m->f, 2, m->stream));
+      return 0;
+    case 15:  // INTEGR_CONTINUITY's EXCH(eta) + UPDATE_ETAH everywhere (exactConserv; gathered eta)
+      if (m->p.exactConserv) TIMED(K_ETA, launch_exch_eta(m->d, m->p, m->f, m->d_srcOf, true, 0, m->stream));
+      return 0;
   }
   return set_err("mgcm_step_phase: no phase %d", phase);
+}
+
+// ---- several models stepped by one host (fortran_abi.hip's tile-sharded drop-ins) ---------
+void *mgcm_get_stream(mgcm_model *m) { return (void *)m->stream; }
+
+// The interior points whose values the halos of tiles [t0, t0+nT) copy (the scalar EXCH map
+// and, on EXCH2 topologies, both vector maps), outside those tiles: what another model that
+// steps them must deliver before this one's local halo fill (the in-process HaloPlan).
+long mgcm_halo_sources(mgcm_model *m, int t0, int nT, long *out, long cap) {
+  if (t0 < 0 || nT < 1 || t0 + nT > m->d.nTiles) return set_err("mgcm_halo_sources: bad tile range");
+  const long n2 = m->d.n2, N2 = n2 * m->d.nTiles, lo = (long)t0 * n2, hi = (long)(t0 + nT) * n2;
+  std::vector<long> src;
+  for (size_t h = 0; h + 1 < m->h_halo.size(); h += 2)
+    if (m->h_halo[h] >= lo && m->h_halo[h] < hi) src.push_back(m->h_halo[h + 1]);
+  if (m->uvMap)
+    for (int w = 0; w < 2; w++)
+      for (int c = 0; c < 2; c++)
+        for (long q = lo; q < hi; q++) {
+          const long code = m->h_uv[w][(size_t)c * N2 + q];
+          if (code != 0) src.push_back(((code < 0 ? -code : code) - 1) % N2);
+        }
+  std::sort(src.begin(), src.end());
+  src.erase(std::unique(src.begin(), src.end()), src.end());
+  long n = 0;
+  for (long v : src)
+    if (v < lo || v >= hi) {
+      if (out && n < cap) out[n] = v;
+      n++;
+    }
+  return n;
+}
+
+// The device CG2D's parts of tiles [t0, t0+nT) on this model's stream and arrays (its
+// cg2d_b, cg2d_x and operator must hold those tiles' values): a host stepping several models
+// on one GPU launches one model's arrays for all of them (the gathered right-hand side), on
+// several GPUs one launch per GPU on one shared hand-off block (mgcm_cg2d_share).
+int mgcm_cg2d_tiles(mgcm_model *m, int t0, int nT) {
+  if (check_ready(m)) return -1;
+  if (!m->useMwg || m->mwg.partsPerTile <= 0)
+    return set_err("mgcm_cg2d_tiles: needs the multi-workgroup CG2D on whole-domain tables (cg2dForceMwg)");
+  if (t0 < 0 || nT < 1 || t0 + nT > m->d.nTiles) return set_err("mgcm_cg2d_tiles: bad tile range");
+  if (nT < m->d.nTiles && !m->mwg.sys)
+    return set_err("mgcm_cg2d_tiles: a tile subset needs the shared hand-off block (mgcm_cg2d_share)");
+  HIPCHK(hipSetDevice(m->device));
+  TIMED(K_CG2D, launch_cg2d_mwg(m->d, m->p, m->f, m->mwg, m->p.cg2dMaxIters, m->d_rec, m->d_ctr + 1, m->stream,
+                                t0 * m->mwg.partsPerTile, nT * m->mwg.partsPerTile));
+  return 0;
+}
+
+// A hand-off block that other launches poll from another GPU: uncached device memory, so no
+// GPU's L2 holds a stale copy of a granule (coarse-grained hipMalloc memory is coherent only at
+// kernel boundaries); every granule access is then at system scope (T.sys).
+static int mwg_block_uncached(mgcm_model *m) {
+  if (m->mwg.sys) return 0;
+  const size_t partGr = (size_t)2 * 3 * m->mwg.G * 2;
+  char *blk = nullptr;
+  if (hipExtMallocWithFlags((void **)&blk, m->mwg.hsBytes, hipDeviceMallocUncached) != hipSuccess)
+    HIPCHK(hipExtMallocWithFlags((void **)&blk, m->mwg.hsBytes, hipDeviceMallocFinegrained));
+  HIPCHK(hipMemset(blk, 0, m->mwg.hsBytes));
+  HIPCHK(hipDeviceSynchronize());
+  for (auto &q : m->mwgAllocs)
+    if (q == m->mwgBlock) { (void)hipFree(q); q = blk; }
+  m->mwgBlock = blk;
+  m->mwg.ctr = (unsigned *)blk;
+  m->mwg.part = (unsigned long long *)(blk + 64);
+  m->mwg.xs = m->mwg.part + partGr;
+  m->mwg.sys = 1;
+  drop_graphs(m);
+  return 0;
+}
+
+// In-process sharing of `owner`'s hand-off block by m (another model of the same host, on
+// another GPU): the block becomes uncached device memory of the owner's GPU, m's launches map
+// it by peer access, and both poll at system scope.  m == owner prepares the owner only.
+int mgcm_cg2d_share(mgcm_model *m, mgcm_model *owner) {
+  if (!m->useMwg || !owner->useMwg || m->mwg.partsPerTile <= 0 || m->mwg.G != owner->mwg.G)
+    return set_err("mgcm_cg2d_share: both models need the same whole-domain multi-workgroup CG2D (cg2dForceMwg)");
+  HIPCHK(hipSetDevice(owner->device));
+  HIPCHK(hipStreamSynchronize(owner->stream));
+  if (mwg_block_uncached(owner)) return -1;
+  if (m == owner) return 0;
+  HIPCHK(hipSetDevice(m->device));
+  HIPCHK(hipStreamSynchronize(m->stream));
+  if (m->device != owner->device) {
+    hipError_t e = hipDeviceEnablePeerAccess(owner->device, 0);
+    if (e != hipSuccess && e != hipErrorPeerAccessAlreadyEnabled) return set_err("mgcm_cg2d_share: peer access %d -> %d: %s",
+                                                                                  m->device, owner->device, hipGetErrorString(e));
+    (void)hipGetLastError();
+  }
+  m->mwg.ctr = owner->mwg.ctr;
+  m->mwg.part = owner->mwg.part;
+  m->mwg.xs = owner->mwg.xs;
+  m->mwg.sys = 1;
+  drop_graphs(m);
+  return 0;
 }
 
 // Distributed CG2D building blocks (kernels_cg2d_dist.hip): one op of cg2d.F over this

@@ -6,28 +6,30 @@ ranks (eesupp/src/exch1_rx.template:170-198 via MPI send/recv) and every CG2D
 iteration does three GLOBAL_SUM_TILE_RL (eesupp/src/global_sum_tile.F:14-237,
 an MPI_Allreduce of per-tile partials summed in tile order).
 
-The MI355X design keeps the 3-D work sharded and the 2-D solve replicated:
+The MI355X design keeps the 3-D work sharded; the 2-D solve runs where it is fastest:
 
 * every process holds the WHOLE domain's arrays in HBM (memory is not the
   constraint: the largest BASELINE grid is 13 x 98^2 x 50 points) and its
   3-D kernels step only its contiguous tile range [t0, t0+nT)
   (mgcm_set_tile_range);
-* per step the collectives are: one all-gather of the 2-D CG2D right-hand
-  side (cg2d_b, cg2d_x tile blocks), one all-gather of the new free surface
-  (exactConserv), and one point-to-point exchange of the 3-D halo sources
+* per step the collectives are: the CG2D right-hand side's halo sources (device solve) or
+  an all-gather of its tile blocks (replicated solve), one all-gather of the new free
+  surface (exactConserv), and one point-to-point exchange of the 3-D halo sources
   (u, v, w, theta, salt) with each neighbouring process (twice with
   staggerTimeStep: the new velocities before THERMODYNAMICS, then the
   tracers);
-* CG2D, by default (cg2d="replicated"), runs on the gathered global problem on
-  every GPU with the same kernel as the 1-GPU path.  The solve is latency-bound
-  (~4k-105k points, ~35-125 iterations): the replicated solve needs no
-  collective inside the iteration, and its sums are exactly the 1-GPU sums, so
-  results are bit-identical at any GPU count (SURVEY.md 8(c) parity item 6);
+* cg2d="auto" (the default) picks "device" where the model's solver is the multi-workgroup
+  one (C3, C5: the grids too large for one CU) and "replicated" where it is a single-CU
+  kernel (C2, C4: ~4k points, where one CU's solve at ~1.8 us per iteration beats any
+  solve whose iteration crosses GPUs);
 * cg2d="device": the multi-workgroup CG2D (kernels_cg2d_mwg.hip) with every process
   launching only the parts of its own tiles; all parts meet on ONE hand-off block (rank 0's,
   mapped into the others by IPC, system-scope granules).  No host step and no collective
   inside an iteration; its sums keep the single-launch order, so the solve is the
   1-process multi-workgroup solve bit for bit, at any process count;
+* cg2d="replicated": every GPU solves the gathered global problem with the 1-GPU kernel.
+  No collective inside the iteration, and its sums are exactly the 1-GPU sums, so results
+  are bit-identical at any GPU count (SURVEY.md 8(c) parity item 6);
 * cg2d="distributed" is the reference's own distributed CG2D (cg2d.F:100-415):
   each process iterates on its own tiles only (mgcm_cg2d_op), the three global
   sums per iteration are GLOBAL_SUM_TILE_RL -- an all-gather of the per-tile
@@ -35,8 +37,8 @@ The MI355X design keeps the 3-D work sharded and the 2-D solve replicated:
   (global_sum_tile.F:161-191, tile_sum below) -- and the two width-1 EXCH_S3D_RL
   of r and s are point-to-point exchanges of the halo sources.  Its iterates do
   not depend on the process count either (the per-tile partials are fixed-order
-  device sums); 5 collectives per iteration make it latency-bound on RCCL, which
-  is why the replicated solve is the default.
+  device sums); 5 collectives per iteration make it latency-bound on RCCL: the
+  reference-faithful option, kept for parity.
 
 Transport: backend "nccl" (RCCL over xGMI) moves device tensors directly on
 the model's stream; backend "gloo" stages through host memory (CPU tests,
@@ -179,7 +181,7 @@ class ShardedModel:
     configuration; after init(), step()/forward_step() keep the tiles a
     process owns bit-identical to a single-process run."""
 
-    def __init__(self, model, dist, device=None, cg2d="replicated", overlap=True, model_stream="shared"):
+    def __init__(self, model, dist, device=None, cg2d="auto", overlap=True, model_stream="shared"):
         import torch
         from ._lib import check, lib
         self.torch, self.dist, self.m = torch, dist, model
@@ -227,8 +229,10 @@ class ShardedModel:
         mt = self.part.maxT
         self.g_in = torch.empty(mt * n2, dtype=torch.float64, device=dv)
         self.g_out = torch.empty(self.world * mt * n2, dtype=torch.float64, device=dv)
-        if cg2d not in ("replicated", "distributed", "device"):
-            raise ValueError("cg2d must be 'replicated', 'distributed' or 'device'")
+        if cg2d not in ("auto", "replicated", "distributed", "device"):
+            raise ValueError("cg2d must be 'auto', 'replicated', 'distributed' or 'device'")
+        if cg2d == "auto":
+            cg2d = "device" if model.cg2d_kernel() == "mwg" else "replicated"
         self.cg2d = cg2d
         if cg2d == "device":
             self._share_cg2d_handoff()
@@ -489,9 +493,32 @@ class ShardedModel:
                                      else None), "mgcm_set_stream")
         self._graph, self._gstream = g, s
 
-    def replay(self, npairs=1):
+    def _check_records(self, nsteps):
+        """Refuse a batch whose solves wrote past the device's record ring (mgcm_end_steps
+        validates nsteps against it) -- checked BEFORE the steps run."""
+        self.check(self.L.mgcm_end_steps(self.m.h, nsteps), "mgcm_end_steps")
+
+    def check_solves(self, nsteps):
+        """Raise if any solve of the last nsteps steps failed: a device CG2D whose grid
+        hand-off timed out records numIters = -1 (kernels_cg2d_mwg.hip) and leaves cg2d_x
+        unconverged.  The device CG2D's parts spin-wait for each other across processes, so
+        every process must launch its parts of a solve while the others' are running (host
+        work between steps -- Python, gloo staging -- delays a launch; past ~2^22 polls every
+        part gives up rather than hang)."""
+        if nsteps <= 0:
+            return
+        its = (ctypes.c_int * nsteps)()
+        self.check(self.L.mgcm_solve_history(self.m.h, nsteps, its, None, None), "mgcm_solve_history")
+        bad = [i for i, n in enumerate(its) if n < 0]
+        if bad:
+            raise RuntimeError("CG2D failed (grid hand-off timeout, numIters = -1) in step(s) %s of the last %d"
+                               % (bad, nsteps))
+
+    def replay(self, npairs=1, check=True):
         """Replay the captured pair of steps npairs times (the device's per-step record ring
-        restarts at the first replay)."""
+        restarts at the first replay); with check, the batch's solve records are read back
+        and a failed solve raises (check_solves)."""
+        self._check_records(2 * npairs)
         self.check(self.L.mgcm_begin_steps(self.m.h), "mgcm_begin_steps")   # on self.stream
         if self.model_stream != "shared":
             self._publish()   # the record reset (model stream) before the replays (torch's)
@@ -501,11 +528,17 @@ class ShardedModel:
         if self.model_stream != "shared":
             self._consume()   # the model's later work after the replays
         self.check(self.L.mgcm_end_steps(self.m.h, 2 * npairs), "mgcm_end_steps")
+        if check:
+            self.check_solves(2 * npairs)
 
-    def forward_step(self, nsteps=1):
+    def forward_step(self, nsteps=1, check=True):
+        """nsteps sharded FORWARD_STEPs; with check, a failed solve raises (check_solves)."""
+        self._check_records(nsteps)
         self.check(self.L.mgcm_begin_steps(self.m.h), "mgcm_begin_steps")
         for _ in range(nsteps):
             self.step()
+        if check:
+            self.check_solves(nsteps)
 
     def gather_field(self, name):
         """The whole-domain field assembled from every owner (host numpy), e.g.

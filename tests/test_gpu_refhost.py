@@ -14,6 +14,10 @@ Bars, BASELINE config 2 (global_ocean.90x40x15 from its pickups):
     cg2dRefOrder (the order results/output.txt was summed in, tests/test_gpu_refpin.py),
     and on one 90 x 40 tile: the state after 6 steps through the MODS drop-ins is
     bit-identical to the device-resident, graph-replayed mgcm_forward_step;
+  * the same with the 36 tiles over 2, 3 and 4 device models of the one host process
+    (MGCM_AMD_MODELS: tiles over GPUs, the models' halo sources and right-hand-side / free-
+    surface blocks copied between them at the reference's exchange points), with the gathered
+    single-CU CG2D and with the device-sharded multi-workgroup CG2D: bit-identical to one model;
   * the mirror moves the state down only after the steps a host routine reads
     (monitorFreq = 2 days, nEndIter) -- 3 of 6 -- and otherwise only the 6 forcing fields up;
   * ms/step through the drop-ins is recorded beside the graph path's.
@@ -71,7 +75,8 @@ def _write_blob(path, m, nsteps, monitor_days):
             missing.append(n)
     # parameters this configuration leaves at the reference's default (not in the device's
     # table because no kernel branches on them here)
-    assert set(missing) <= {"GM_ExtraDiag", "useAbsVorticity", "upwindShear", "GM_AdvForm"}, missing
+    assert set(missing) <= {"GM_ExtraDiag", "useAbsVorticity", "upwindShear", "GM_AdvForm", "useSBO",
+                            "useDiagnostics"}, missing
     periodic = int(dev.get("periodicExternalForcing", 0))
     nRec = int(dev["nForcRec"]) if periodic else 0
     blob_fields = []
@@ -113,8 +118,15 @@ def _read_out(path, state_names, nsteps):
                  "bytes_up": float(bup), "bytes_down": float(bdown), "step_ms": [1e3 * x for x in step_s]}
 
 
-@pytest.mark.parametrize("layout,refOrder", [("ref", 0), ("ref", 1), ("1t", 0)])
-def test_refhost_mods_dropins_bitexact(layout, refOrder, tmp_path):
+# models > 1: the host's 36 tiles over that many device models (MGCM_AMD_MODELS; all on the
+# one GPU of the test box), stepped through the same drop-ins with the models' halo sources,
+# right-hand-side blocks and free-surface blocks copied between them at the reference's
+# exchange points (fortran_abi.hip); mwg = 1: the device-sharded multi-workgroup CG2D
+# (MGCM_CG2D_MWG) instead of the gathered single-CU solve
+@pytest.mark.parametrize("layout,refOrder,models,mwg", [("ref", 0, 1, 0), ("ref", 1, 1, 0), ("1t", 0, 1, 0),
+                                                        ("ref", 0, 2, 0), ("ref", 0, 4, 0), ("ref", 1, 4, 0),
+                                                        ("ref", 0, 1, 1), ("ref", 0, 3, 1)])
+def test_refhost_mods_dropins_bitexact(layout, refOrder, models, mwg, tmp_path):
     from mitgcm_amd import configs
     exe = os.path.join(RH, "refhost_" + layout)
     assert os.path.exists(exe), "refhost not built (mitgcm_amd/fortran/build_refhost.py, __graft_entry__.build())"
@@ -123,10 +135,12 @@ def test_refhost_mods_dropins_bitexact(layout, refOrder, tmp_path):
     def cfg():
         g, params, state, forcing = configs.global_ocean_90x40x15(nSx=tiles[0], nSy=tiles[1])
         params["cg2dRefOrder"] = refOrder
+        if mwg:
+            params["cg2dForceMwg"] = 1
         return g, params, state, forcing
     m = configs.make_model(cfg)
     state = _write_blob(tmp_path / "refhost_in.bin", m, NSTEPS, monitor_days=2)
-    env = dict(os.environ, MGCM_CG2D_REFORDER=str(refOrder))
+    env = dict(os.environ, MGCM_CG2D_REFORDER=str(refOrder), MGCM_AMD_MODELS=str(models), MGCM_CG2D_MWG=str(mwg))
     r = subprocess.run([exe, str(tmp_path)], capture_output=True, text=True, timeout=300, env=env)
     assert r.returncode == 0, r.stdout + r.stderr
     out, st = _read_out(tmp_path / "refhost_out.bin", state, NSTEPS)
@@ -149,12 +163,14 @@ def test_refhost_mods_dropins_bitexact(layout, refOrder, tmp_path):
     ms = 1e3 * st["seconds"] / max(1, st["steps_timed"])
     # steps 3 and 5 end without a host reader: no state download, only the forcing upload
     quiet = [st["step_ms"][i] for i in (2, 4)]
-    rec = {"layout": layout, "cg2dRefOrder": refOrder, "dropin_ms_per_step_mean": ms,
+    rec = {"layout": layout, "cg2dRefOrder": refOrder, "models": models, "cg2dForceMwg": mwg,
+           "dropin_ms_per_step_mean": ms,
            "dropin_ms_per_step_no_download": float(np.mean(quiet)), "graph_ms_per_step": graph_ms,
            "mirror": st, "state_fields": len(state)}
-    print("refhost %s refOrder=%d: %s" % (layout, refOrder, json.dumps(rec)))
+    print("refhost %s refOrder=%d models=%d mwg=%d: %s" % (layout, refOrder, models, mwg, json.dumps(rec)))
     if os.path.isdir(os.path.join(ROOT, "gpurun_out")):
-        with open(os.path.join(ROOT, "gpurun_out", "refhost_%s_%d.json" % (layout, refOrder)), "w") as f:
+        with open(os.path.join(ROOT, "gpurun_out", "refhost_%s_%d_m%d_w%d.json" % (layout, refOrder, models, mwg)),
+                  "w") as f:
             json.dump(rec, f)
     assert not bad, bad
     assert len([n for n in CHECK if n in out]) >= 20
