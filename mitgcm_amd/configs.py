@@ -202,7 +202,7 @@ def global_oce_latlon(nSx=2, nSy=1, OL=2, data_dir=None):
     salt = np.moveaxis(_to_tiles(g, read_bin(os.path.join(d, "lev_s.bin"), (Nr, Ny, Nx))), 0, 1).copy()
     salt[mC == 0.0] = 0.0
     params = dict(deltaTMom=1800.0, deltaTFreeSurf=86400.0, deltaTClock=86400.0, deltaTtracer=86400.0,
-                  abEps=0.1, rhoConst=1035.0, rhoNil=1035.0, rhoConstFresh=rhoConstFresh, gravity=9.81,
+                  abEps=0.1, rhoConst=1035.0, rhoConstFresh=rhoConstFresh, gravity=9.81,
                   gBaro=9.81, viscAhD=5e5, viscAhZ=5e5, viscA4D=0.0, viscA4Z=0.0, viscAr=1e-3,
                   sideDragFactor=2.0, selectCoriScheme=0, momForcingOutAB=0, momDissip_In_AB=1,
                   cg2dMaxIters=500, cg2dUseMinResSol=0, nIter0=0, no_slip_sides=1, no_slip_bottom=1,
@@ -504,7 +504,7 @@ def global_ocean_cs32x15(data_dir=None, sNy=32, params_over=None):
     salt = g.exch(cs_global_to_tiles(g, rd("lev_S_cs_15k.bin", (Nr, n, 6 * n)), mapIO=-1).swapaxes(0, 1).copy())
     salt[mC == 0.0] = 0.0
     params = dict(deltaTMom=1200.0, deltaTFreeSurf=86400.0, deltaTClock=86400.0, deltaTtracer=86400.0,
-                  abEps=0.1, rhoConst=1035.0, rhoNil=1035.0, rhoConstFresh=rhoConstFresh, gravity=9.81,
+                  abEps=0.1, rhoConst=1035.0, rhoConstFresh=rhoConstFresh, gravity=9.81,
                   gBaro=9.81, viscAhD=3e5, viscAhZ=3e5, viscA4D=0.0, viscA4Z=0.0, viscAr=1e-3,
                   sideDragFactor=2.0, selectCoriScheme=0, vectorInvariantMomentum=1, selectVortScheme=1,
                   selectKEscheme=0, momForcingOutAB=0, momDissip_In_AB=1, cg2dMaxIters=200, cg2dUseMinResSol=0,

@@ -126,6 +126,13 @@ struct FortranSide {
   double advTime = 0.0;
   int advIter = 0;
   Readers rd;
+  // Graph-replayed steps (one model): the drop-in sequence of a device-authoritative step is
+  // recorded; once one has run eagerly in FORWARD_STEP's order, every later step runs as ONE
+  // replay of the captured step at its DO_OCEANIC_PHYS (after the forcing upload), and the
+  // step's other drop-ins only check that they come in the recorded order (fusedPos)
+  std::vector<std::string> seq, fusedSeq;
+  bool recording = false, canFuse = false, fused = false;
+  size_t fusedPos = 0;
   long nUp = 0, nDown = 0;   // copies of whole bound arrays, for mgcm_amd_transfer_stats_
   double bytesUp = 0.0, bytesDown = 0.0;
 };
@@ -479,6 +486,43 @@ void advanced(int myIter, double myTime) {
   g.advTime = myTime;
 }
 
+// Is the recorded step FORWARD_STEP's non-staggered order, which mgcm_forward_step replays
+// bit for bit (forward_step.F:656-1120; tests/test_gpu_refhost.py)?  Each routine once, in
+// the order DO_OCEANIC_PHYS, THERMODYNAMICS, DYNAMICS, [UPDATE_R_STAR, UPDATE_CG2D],
+// SOLVE_FOR_PRESSURE, MOMENTUM_CORRECTION_STEP, INTEGR_CONTINUITY, [CALC_R_STAR],
+// DO_FIELDS_BLOCKING_EXCHANGES; the bracketed ones iff the r* free surface.
+bool canonical_step(const std::vector<std::string> &q) {
+  const bool rstar = mgcm_get_param(g.m, "nonlinFreeSurf") > 0.0;
+  if (mgcm_get_param(g.m, "staggerTimeStep") != 0.0 || mgcm_get_param(g.m, "momStepping") == 0.0) return false;
+  std::vector<std::string> want = {"DO_OCEANIC_PHYS", "THERMODYNAMICS", "DYNAMICS"};
+  if (rstar) { want.push_back("UPDATE_R_STAR"); want.push_back("UPDATE_CG2D"); }
+  want.push_back("SOLVE_FOR_PRESSURE");
+  want.push_back("MOMENTUM_CORRECTION_STEP");
+  want.push_back("INTEGR_CONTINUITY");
+  if (rstar) want.push_back("CALC_R_STAR");
+  want.push_back("DO_FIELDS_BLOCKING_EXCHANGES");
+  return q == want;
+}
+bool fuse_allowed() {
+  const char *e = getenv("MGCM_AMD_EAGER");
+  return !multi() && !(e && atoi(e) == 1);
+}
+// A routine drop-in of a device-authoritative step: true when its work already ran inside
+// the step's replay (then it only checks its place in the recorded order).
+bool absorbed(const char *name) {
+  if (!g.fused) {
+    if (g.recording) g.seq.push_back(name);
+    return false;
+  }
+  if (g.fusedPos >= g.fusedSeq.size() || g.fusedSeq[g.fusedPos] != name) {
+    fprintf(stderr, "ABNORMAL END: %s_AMD: the step's drop-ins left the recorded FORWARD_STEP order while the step "
+                    "ran as one graph replay (MGCM_AMD_EAGER=1 steps routine by routine)\n", name);
+    abort();
+  }
+  g.fusedPos++;
+  return true;
+}
+
 // eesupp/src/different_multiple.F: is val1 the step nearest to a multiple of freq?
 bool different_multiple(double freq, double val1, double step) {
   if (freq == 0.0) return false;
@@ -665,6 +709,7 @@ void mgcm_amd_init_(const int *myIter) {
   for (auto &s : g.sh)
     if (mgcm_set_param(s.m, "myIter", (double)*myIter)) die("MGCM_AMD_INIT");
   if (multi()) setup_shards("MGCM_AMD_INIT");
+  g.canFuse = g.fused = g.recording = false;   // the step is learned again
   g.devIter = *myIter;
   g.deviceAuth = false;
   g.ready = true;
@@ -706,18 +751,36 @@ void do_oceanic_phys_amd_(const double *myTime, const int *myIter, const int *my
   (void)myThid;
   enter_time_loop("DO_OCEANIC_PHYS_AMD");
   g.advValid = false;   // a new step: its end time is not known yet
+  if (g.fused) die("DO_OCEANIC_PHYS_AMD", "a step began before the previous one's DO_FIELDS_BLOCKING_EXCHANGES");
+  if (g.canFuse && fuse_allowed() && g.ready) {
+    // the whole step as one replay of the captured FORWARD_STEP (mgcm_forward_step), after
+    // this step's forcing; the counter the device advances at the step's end is known
+    g.lastIter = *myIter;
+    g.lastTime = *myTime;
+    upload("DO_OCEANIC_PHYS_AMD", K_INPUT);
+    set_iter("DO_OCEANIC_PHYS_AMD", *myIter);
+    if (mgcm_forward_step(g.m, 1)) die("DO_OCEANIC_PHYS_AMD");
+    g.devIter = *myIter + 1;
+    g.fused = true;
+    g.fusedPos = 1;
+    return;
+  }
+  g.seq.assign(1, "DO_OCEANIC_PHYS");
+  g.recording = g.deviceAuth && fuse_allowed();
   routine("DO_OCEANIC_PHYS_AMD", op_oceanic_phys, *myIter, *myTime, true);
 }
 /* SUBROUTINE THERMODYNAMICS(myTime, myIter, myThid)      model/src/thermodynamics.F:25 */
 void thermodynamics_amd_(const double *myTime, const int *myIter, const int *myThid) {
   (void)myThid;
   enter_time_loop("THERMODYNAMICS_AMD");
+  if (absorbed("THERMODYNAMICS")) return;
   routine("THERMODYNAMICS_AMD", op_tracer_step, *myIter, *myTime);
 }
 /* SUBROUTINE DYNAMICS(myTime, myIter, myThid)            model/src/dynamics.F:21 */
 void dynamics_amd_(const double *myTime, const int *myIter, const int *myThid) {
   (void)myThid;
   enter_time_loop("DYNAMICS_AMD");
+  if (absorbed("DYNAMICS")) return;
   routine("DYNAMICS_AMD", op_dynamics, *myIter, *myTime);
 }
 /* SUBROUTINE UPDATE_R_STAR(useLatest, myTime, myIter, myThid)   model/src/update_r_star.F:6
@@ -730,6 +793,7 @@ void update_r_star_amd_(const int *useLatest, const double *myTime, const int *m
   (void)myThid;
   if (*useLatest) {
     advanced(*myIter, *myTime);
+    if (absorbed("UPDATE_R_STAR")) return;
     routine("UPDATE_R_STAR_AMD", op_update_r_star, *myIter, *myTime);
   }
 }
@@ -738,6 +802,7 @@ void update_r_star_amd_(const int *useLatest, const double *myTime, const int *m
 void update_cg2d_amd_(const double *myTime, const int *myIter, const int *myThid) {
   (void)myTime; (void)myIter; (void)myThid;
   model("UPDATE_CG2D_AMD");
+  (void)absorbed("UPDATE_CG2D");
 }
 /* SUBROUTINE CALC_R_STAR(etaFld, myTime, myIter, myThid)  model/src/calc_r_star.F:10
  * FORWARD_STEP passes etaH (forward_step.F:976): the bound array. */
@@ -746,12 +811,14 @@ void calc_r_star_amd_(const double *etaFld, const double *myTime, const int *myI
   const Bound *b = bound_at(etaFld);
   if (!b || b->name != "etaH") die("CALC_R_STAR_AMD", "etaFld must be the bound etaH");
   advanced(*myIter, *myTime);
+  if (absorbed("CALC_R_STAR")) return;
   routine("CALC_R_STAR_AMD", op_calc_r_star, *myIter, *myTime);
 }
 /* SUBROUTINE SOLVE_FOR_PRESSURE(myTime, myIter, myThid)  model/src/solve_for_pressure.F:7 */
 void solve_for_pressure_amd_(const double *myTime, const int *myIter, const int *myThid) {
   (void)myThid;
   advanced(*myIter, *myTime);
+  if (absorbed("SOLVE_FOR_PRESSURE")) return;
   routine("SOLVE_FOR_PRESSURE_AMD", op_solve, *myIter, *myTime);
 }
 /* SUBROUTINE MOMENTUM_CORRECTION_STEP(myTime, myIter, myThid)
@@ -759,6 +826,7 @@ void solve_for_pressure_amd_(const double *myTime, const int *myIter, const int 
 void momentum_correction_step_amd_(const double *myTime, const int *myIter, const int *myThid) {
   (void)myThid;
   advanced(*myIter, *myTime);
+  if (absorbed("MOMENTUM_CORRECTION_STEP")) return;
   routine("MOMENTUM_CORRECTION_STEP_AMD", op_correction, *myIter, *myTime);
 }
 /* SUBROUTINE INTEGR_CONTINUITY(uFld, vFld, myTime, myIter, myThid)
@@ -771,6 +839,7 @@ void integr_continuity_amd_(const double *uFld, const double *vFld, const double
   if (!bu || !bv || bu->name != "uVel" || bv->name != "vVel")
     die("INTEGR_CONTINUITY_AMD", "uFld, vFld must be the bound uVel, vVel");
   advanced(*myIter, *myTime);
+  if (absorbed("INTEGR_CONTINUITY")) return;
   routine("INTEGR_CONTINUITY_AMD", op_continuity, *myIter, *myTime);
 }
 /* SUBROUTINE DO_FIELDS_BLOCKING_EXCHANGES(myThid)   model/src/do_fields_blocking_exchanges.F:7 */
@@ -782,7 +851,20 @@ void do_fields_blocking_exchanges_amd_(const int *myThid) {
   (void)myThid;
   const int it = g.advValid ? g.advIter : g.lastIter + 1;
   const double t = g.advValid ? g.advTime : g.lastTime + g.rd.deltaTClock;
-  routine("DO_FIELDS_BLOCKING_EXCHANGES_AMD", op_blocking, it, t);
+  if (absorbed("DO_FIELDS_BLOCKING_EXCHANGES")) {
+    if (g.fusedPos != g.fusedSeq.size()) die("DO_FIELDS_BLOCKING_EXCHANGES_AMD", "drop-ins of the replayed step missing");
+    g.fused = false;
+    g.lastIter = it;
+    g.lastTime = t;
+  } else {
+    routine("DO_FIELDS_BLOCKING_EXCHANGES_AMD", op_blocking, it, t);
+    // a step that ran routine by routine in FORWARD_STEP's order: later ones replay it
+    if (g.recording && canonical_step(g.seq)) {
+      g.fusedSeq = g.seq;
+      g.canFuse = true;
+    }
+    g.recording = false;
+  }
   if (g.deviceAuth && host_reads_state(t, it)) download("DO_FIELDS_BLOCKING_EXCHANGES_AMD");
 }
 

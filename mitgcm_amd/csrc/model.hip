@@ -221,6 +221,8 @@ struct mgcm_model {
   // hipGraphs of two FORWARD_STEPs, one per theta/salt ping-pong parity
   bool useGraph = true;
   hipGraphExec_t graphExec[2][4] = {};   // [THERMODYNAMICS overlap off/on][tracer buffer parity]
+  hipGraphExec_t graph1Exec[2][4] = {};  // ONE step (callers that step one at a time: the Fortran drop-ins)
+  double *graph1Tr[2][4][4] = {};        // its tracer pointers after the step: theta, thetaNext, salt, saltNext
   // overlap auto-selection (ovl_trial): both graphs timed on a copy of the state
   bool ovlAuto = false, ovlDecided = false;
   float ovlMs[2] = {0.f, 0.f};
@@ -1580,6 +1582,9 @@ static void drop_graphs(mgcm_model *m) {
   for (auto &row : m->graphExec)
     for (auto &ge : row)
       if (ge) { (void)hipGraphExecDestroy(ge); ge = nullptr; }
+  for (auto &row : m->graph1Exec)
+    for (auto &ge : row)
+      if (ge) { (void)hipGraphExecDestroy(ge); ge = nullptr; }
 }
 
 // Which theta/salt ping-pong buffers are current (the kernels' arguments differ).
@@ -1606,6 +1611,37 @@ static int two_step_graph(mgcm_model *m, hipGraphExec_t *out) {
   }
   *out = m->graphExec[o][q];
   return 0;
+}
+
+// One FORWARD_STEP captured per buffer parity (the tracer ping-pong flips it, so consecutive
+// single steps alternate between two of these graphs): a caller that steps one at a time --
+// the Fortran drop-ins, with host work between steps -- still replays instead of launching.
+static int one_step_graph(mgcm_model *m, hipGraphExec_t *out) {
+  const int q = buffer_parity(m), o = m->overlap ? 1 : 0;
+  if (!m->graph1Exec[o][q]) {
+    double *pre[4] = {m->f.theta, m->f.thetaNext, m->f.salt, m->f.saltNext};
+    hipGraph_t g = nullptr;
+    HIPCHK(hipStreamBeginCapture(m->stream, hipStreamCaptureModeThreadLocal));
+    const int rc = one_step(m);
+    hipError_t e = hipStreamEndCapture(m->stream, &g);
+    if (rc) { if (g) (void)hipGraphDestroy(g); return -1; }
+    HIPCHK(e);
+    e = hipGraphInstantiate(&m->graph1Exec[o][q], g, nullptr, nullptr, 0);
+    (void)hipGraphDestroy(g);
+    HIPCHK(e);
+    // the capture ran one_step's host side (CYCLE_TRACER's pointer swaps) without launching:
+    // keep the pointers it leaves for every replay, and undo them until the replay
+    double **tr[4] = {&m->f.theta, &m->f.thetaNext, &m->f.salt, &m->f.saltNext};
+    for (int k = 0; k < 4; k++) m->graph1Tr[o][q][k] = *tr[k];
+    m->f.theta = pre[0]; m->f.thetaNext = pre[1]; m->f.salt = pre[2]; m->f.saltNext = pre[3];
+  }
+  *out = m->graph1Exec[o][q];
+  return 0;
+}
+// after a one-step replay: the tracer pointers one_step would have left
+static void one_step_graph_done(mgcm_model *m, int o, int q) {
+  m->f.theta = m->graph1Tr[o][q][0]; m->f.thetaNext = m->graph1Tr[o][q][1];
+  m->f.salt = m->graph1Tr[o][q][2]; m->f.saltNext = m->graph1Tr[o][q][3];
 }
 
 static int ovl_trial(mgcm_model *m);
@@ -1698,6 +1734,15 @@ int mgcm_forward_step(mgcm_model *m, int nsteps) {
       if (two_step_graph(m, &ge)) return -1;
       HIPCHK(hipGraphLaunch(ge, m->stream));
     }
+  }
+  // an odd step (a caller stepping one at a time): the one-step graph of this parity
+  if (s < nsteps && m->useGraph && !m->timing) {
+    const int q = buffer_parity(m), o = m->overlap ? 1 : 0;
+    hipGraphExec_t ge;
+    if (one_step_graph(m, &ge)) return -1;
+    HIPCHK(hipGraphLaunch(ge, m->stream));
+    one_step_graph_done(m, o, q);
+    s++;
   }
   for (; s < nsteps; s++)
     if (one_step(m)) return -1;

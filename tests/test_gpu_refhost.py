@@ -7,7 +7,11 @@ THERMODYNAMICS, DYNAMICS, UPDATE_R_STAR(.TRUE., ...), UPDATE_CG2D, SOLVE_FOR_PRE
 MOMENTUM_CORRECTION_STEP, INTEGR_CONTINUITY(uVel, vVel, ...), CALC_R_STAR(etaH, ...),
 DO_FIELDS_BLOCKING_EXCHANGES(myThid) -- with its own EXTERNAL_FIELDS_LOAD in between.  So
 MGCM_AMD_MIRROR binds the COMMON blocks and runs, with eosType = 'JMD95P' (BASELINE
-config 2's EOS), and the mirror is device-authoritative inside the time loop.
+config 2's EOS), and the mirror is device-authoritative inside the time loop.  The run-time
+parameters are the experiment's own namelist files (input/data, data.pkg, data.gmredi)
+resolved by refhost (refhost_parms.F, pinned against the reference's own parameter dump by
+tests/test_refhost_params.py) -- not the device model's table; the harness input carries
+the arrays and the run's control only.
 
 Bars, BASELINE config 2 (global_ocean.90x40x15 from its pickups):
   * on the reference's SIZE.h (9 x 4 tiles of 10 x 10), with the performance CG2D and with
@@ -18,6 +22,9 @@ Bars, BASELINE config 2 (global_ocean.90x40x15 from its pickups):
     (MGCM_AMD_MODELS: tiles over GPUs, the models' halo sources and right-hand-side / free-
     surface blocks copied between them at the reference's exchange points), with the gathered
     single-CU CG2D and with the device-sharded multi-workgroup CG2D: bit-identical to one model;
+  * with one model, the steps after the first run as ONE graph replay each at their
+    DO_OCEANIC_PHYS (the recorded FORWARD_STEP order, the forcing uploaded first), still
+    bit-identical; MGCM_AMD_EAGER=1 keeps the routine-by-routine path, tested too;
   * the mirror moves the state down only after the steps a host routine reads
     (monitorFreq = 2 days, nEndIter) -- 3 of 6 -- and otherwise only the 6 forcing fields up;
   * ms/step through the drop-ins is recorded beside the graph path's.
@@ -50,35 +57,26 @@ def _name(s):
     return s.encode().ljust(32)
 
 
-def _write_blob(path, m, nsteps, monitor_days):
-    from mitgcm_amd._lib import lib
-    L, g = lib(), m.g
-    pnames, fields = _mirror_calls()
-    dev = {}
-    i = 0
-    while L.mgcm_param_name(i):
-        n = L.mgcm_param_name(i).decode()
-        dev[n] = L.mgcm_get_param(m.h, n.encode())
-        i += 1
-    for n, v in m.params.items():   # options the device reads at set-up beyond its table
-        dev.setdefault(n, float(v))
-    dtc = dev["deltaTClock"]
-    host = {"monitorFreq": monitor_days * dtc, "dumpFreq": 0.0, "chkPtFreq": 0.0, "pChkPtFreq": 0.0,
-            "nEndIter": float(int(dev["nIter0"]) + nsteps)}
-    params, missing = [], []
-    for kind, n in pnames:
-        if n in host:
-            params.append((n, host[n]))
-        elif n in dev:
-            params.append((n, float(dev[n])))
-        else:
-            missing.append(n)
-    # parameters this configuration leaves at the reference's default (not in the device's
-    # table because no kernel branches on them here)
-    assert set(missing) <= {"GM_ExtraDiag", "useAbsVorticity", "upwindShear", "GM_AdvForm", "useSBO",
-                            "useDiagnostics"}, missing
-    periodic = int(dev.get("periodicExternalForcing", 0))
-    nRec = int(dev["nForcRec"]) if periodic else 0
+# The experiment's own namelist files (verification/global_ocean.90x40x15/input: data,
+# data.pkg, data.gmredi, fixtures): refhost reads its run-time parameters from them
+# (refhost_parms.F), never from the device model's table or configs.py.
+PARAM_DIR = os.path.join(ROOT, "tests", "golden", "global_ocean.90x40x15", "input")
+
+
+def _write_blob(path, m, nsteps, monitor_days, packages_off=True):
+    """refhost_in.bin: sizes, the run's control (the only parameters it carries: the run length,
+    the monitor schedule, and -- packages_off -- pkg/sbo and pkg/diagnostics switched off for
+    the run), the COMMON-block arrays (grid, masks and the restart state) and the forcing
+    records."""
+    g = m.g
+    _, fields = _mirror_calls()
+    dtc = m.params["deltaTClock"]
+    nIter0 = int(m.params["nIter0"])
+    params = [("monitorFreq", monitor_days * dtc), ("nEndIter", float(nIter0 + nsteps))]
+    if packages_off:
+        params += [("useSBO", 0.0), ("useDiagnostics", 0.0)]
+    periodic = int(m.params.get("periodicExternalForcing", 0))
+    nRec = int(m.params.get("nForcRec", 12)) if periodic else 0
     blob_fields = []
     for n, kind in fields:
         if n == "phiRef":      # phiRef(2*Nr+1) of set_ref_state.F; the device holds phiRef(2k)
@@ -89,8 +87,9 @@ def _write_blob(path, m, nsteps, monitor_days):
         blob_fields.append((n, kind, a))
     with open(path, "wb") as fh:
         fh.write(np.array([g.sNx, g.sNy, g.OLx, g.OLy, g.Nr, g.nSx, g.nSy, len(params), len(blob_fields), nsteps,
-                           int(dev["nIter0"]), nRec, periodic], dtype=np.int32).tobytes())
-        fh.write(np.array([dtc, dev.get("externForcingPeriod", 0.0), dev.get("externForcingCycle", 0.0)]).tobytes())
+                           nIter0, nRec, periodic], dtype=np.int32).tobytes())
+        fh.write(np.array([dtc, m.params.get("externForcingPeriod", 0.0),
+                           m.params.get("externForcingCycle", 0.0)]).tobytes())
         for n, v in params:
             fh.write(_name(n) + np.float64(v).tobytes())
         for n, kind, a in blob_fields:
@@ -123,10 +122,17 @@ def _read_out(path, state_names, nsteps):
 # right-hand-side blocks and free-surface blocks copied between them at the reference's
 # exchange points (fortran_abi.hip); mwg = 1: the device-sharded multi-workgroup CG2D
 # (MGCM_CG2D_MWG) instead of the gathered single-CU solve
-@pytest.mark.parametrize("layout,refOrder,models,mwg", [("ref", 0, 1, 0), ("ref", 1, 1, 0), ("1t", 0, 1, 0),
-                                                        ("ref", 0, 2, 0), ("ref", 0, 4, 0), ("ref", 1, 4, 0),
-                                                        ("ref", 0, 1, 1), ("ref", 0, 3, 1)])
-def test_refhost_mods_dropins_bitexact(layout, refOrder, models, mwg, tmp_path):
+# eager = 1: every step routine by routine (MGCM_AMD_EAGER); otherwise, with one model, the
+# steps after the first run as one graph replay each (fortran_abi.hip: the first
+# device-authoritative step is recorded in FORWARD_STEP's order, later ones replay it)
+# packages = 1: data.pkg as the experiment has it -- pkg/sbo and pkg/diagnostics read the
+# state every step, so it comes down after every step (MGCM_AMD_DIAGNOSTICS=state: state
+# diagnostics only; the mirror refuses useDiagnostics otherwise)
+@pytest.mark.parametrize("layout,refOrder,models,mwg,eager,packages", [
+    ("ref", 0, 1, 0, 0, 0), ("ref", 1, 1, 0, 0, 0), ("1t", 0, 1, 0, 0, 0), ("1t", 0, 1, 0, 1, 0),
+    ("ref", 0, 1, 0, 1, 0), ("ref", 0, 2, 0, 0, 0), ("ref", 0, 4, 0, 0, 0), ("ref", 1, 4, 0, 0, 0),
+    ("ref", 0, 1, 1, 0, 0), ("ref", 0, 3, 1, 0, 0), ("1t", 0, 1, 0, 0, 1)])
+def test_refhost_mods_dropins_bitexact(layout, refOrder, models, mwg, eager, packages, tmp_path):
     from mitgcm_amd import configs
     exe = os.path.join(RH, "refhost_" + layout)
     assert os.path.exists(exe), "refhost not built (mitgcm_amd/fortran/build_refhost.py, __graft_entry__.build())"
@@ -139,9 +145,12 @@ def test_refhost_mods_dropins_bitexact(layout, refOrder, models, mwg, tmp_path):
             params["cg2dForceMwg"] = 1
         return g, params, state, forcing
     m = configs.make_model(cfg)
-    state = _write_blob(tmp_path / "refhost_in.bin", m, NSTEPS, monitor_days=2)
-    env = dict(os.environ, MGCM_CG2D_REFORDER=str(refOrder), MGCM_AMD_MODELS=str(models), MGCM_CG2D_MWG=str(mwg))
-    r = subprocess.run([exe, str(tmp_path)], capture_output=True, text=True, timeout=300, env=env)
+    state = _write_blob(tmp_path / "refhost_in.bin", m, NSTEPS, monitor_days=2, packages_off=not packages)
+    env = dict(os.environ, MGCM_CG2D_REFORDER=str(refOrder), MGCM_AMD_MODELS=str(models), MGCM_CG2D_MWG=str(mwg),
+               MGCM_AMD_EAGER=str(eager))
+    if packages:
+        env["MGCM_AMD_DIAGNOSTICS"] = "state"
+    r = subprocess.run([exe, str(tmp_path), PARAM_DIR], capture_output=True, text=True, timeout=300, env=env)
     assert r.returncode == 0, r.stdout + r.stderr
     out, st = _read_out(tmp_path / "refhost_out.bin", state, NSTEPS)
     # the same configuration stepped by the graph-replayed resident path
@@ -163,16 +172,19 @@ def test_refhost_mods_dropins_bitexact(layout, refOrder, models, mwg, tmp_path):
     ms = 1e3 * st["seconds"] / max(1, st["steps_timed"])
     # steps 3 and 5 end without a host reader: no state download, only the forcing upload
     quiet = [st["step_ms"][i] for i in (2, 4)]
-    rec = {"layout": layout, "cg2dRefOrder": refOrder, "models": models, "cg2dForceMwg": mwg,
+    rec = {"layout": layout, "cg2dRefOrder": refOrder, "models": models, "cg2dForceMwg": mwg, "eager": eager,
+           "packages": packages,
            "dropin_ms_per_step_mean": ms,
            "dropin_ms_per_step_no_download": float(np.mean(quiet)), "graph_ms_per_step": graph_ms,
            "mirror": st, "state_fields": len(state)}
-    print("refhost %s refOrder=%d models=%d mwg=%d: %s" % (layout, refOrder, models, mwg, json.dumps(rec)))
+    print("refhost %s refOrder=%d models=%d mwg=%d eager=%d: %s" % (layout, refOrder, models, mwg, eager,
+                                                                   json.dumps(rec)))
     if os.path.isdir(os.path.join(ROOT, "gpurun_out")):
-        with open(os.path.join(ROOT, "gpurun_out", "refhost_%s_%d_m%d_w%d.json" % (layout, refOrder, models, mwg)),
-                  "w") as f:
+        with open(os.path.join(ROOT, "gpurun_out", "refhost_%s_%d_m%d_w%d_e%d_p%d.json" % (
+                layout, refOrder, models, mwg, eager, packages)), "w") as f:
             json.dump(rec, f)
     assert not bad, bad
     assert len([n for n in CHECK if n in out]) >= 20
-    # the state came down after steps 2, 4 and 6 only (monitorFreq = 2 days, nEndIter = 6)
-    assert st["downloads"] == 3 * len(state), (st, len(state))
+    # the state came down after steps 2, 4 and 6 only (monitorFreq = 2 days, nEndIter = 6),
+    # or after every step when pkg/sbo and pkg/diagnostics read it (packages)
+    assert st["downloads"] == (NSTEPS if packages else 3) * len(state), (st, len(state))
