@@ -336,9 +336,15 @@ def main():
     if a.pmc_summary is None:
         a.pmc_summary = default_pmc_summary(a.config)
     cg_traffic, _ = pmc_traffic(a.pmc_summary, cg_kernel_key(m))
-    # the momentum block's launches (launch_mom_step: del2uv, the MOM_FLUXFORM / MOM_VECINV
-    # kernel, the VI halo AB pass, the CD scheme, the implicit viscosity columns)
-    mom_traffic, mom_traffic_per = pmc_traffic(a.pmc_summary, ("k_del2uv", "k_mom_", "k_cd_scheme"))
+    # the momentum block's launches as the timed graph runs them: on small grids with
+    # THERMODYNAMICS folded into DYNAMICS' grids (config 2) the three fused grids k_dt_l1/l2/l3
+    # (GM tensor | CALC_PHI_HYD | del2uv, MOM U | V | tracer right-hand sides, CD scheme |
+    # implicit tracer solves); otherwise launch_mom_step's (del2uv, the MOM_FLUXFORM /
+    # MOM_VECINV kernel, the VI halo AB pass, the CD scheme, the implicit viscosity columns)
+    layout = m.step_layout()
+    dt_fused = layout["dyn_thermo_fused"]
+    mom_kernels = ("k_dt_l",) if dt_fused else ("k_del2uv", "k_mom_", "k_cd_scheme")
+    mom_traffic, mom_traffic_per = pmc_traffic(a.pmc_summary, mom_kernels)
     model_days = a.steps * dt_clock / 86400.0
     copies = 1 if shard else world   # independent model integrations in the job
     value = copies * model_days / elapsed
@@ -356,6 +362,9 @@ def main():
     mom_ms = kern["mom_step"][0]
     mom_bpp = MOM_BYTES_PER_POINT.get(g.Nr, 104.0 + 24 * 8.0 / g.Nr)
     mom_bytes = mom_bpp * npts * g.Nr
+    if dt_fused:   # + the stepped tracers' right-hand sides and solves (64 B + 96/Nr B a point)
+        ntr = int(m.params.get("tempStepping", 1) != 0) + int(m.params.get("saltStepping", 1) != 0)
+        mom_bytes += ntr * (64.0 + 96.0 / g.Nr) * npts * g.Nr
     mom_gbs = mom_bytes / (mom_ms * 1e-3) / 1e9 if mom_ms > 0 else 0.0
     out = {
         "metric": "model-days/wallclock-sec",
@@ -389,6 +398,10 @@ def main():
         "thermo_overlap": _overlap_info(m),
         "cg2d_mean_iters_per_solve": iters_total / max(1, len(iters)),
         "kernel_ms_mean": {k: v[0] for k, v in kern.items()},
+        # those times: an eager pass of the same steps with events around every launch, in the
+        # launch layout the timed graph replays (one stream: a second-stream THERMODYNAMICS,
+        # C5's, is serialised there); with the fused grids "mom_step" is k_dt_l1+l2+l3
+        "kernel_ms_layout": {"eager_pass_of_the_graph_layout": True, **layout},
         # dominant kernel: the whole-solve CG2D.  It is not HBM-bound: its working set sits in
         # LDS/VGPRs of the workgroup(s) it runs on, so the chip-level HBM fraction below is
         # reported for completeness; the bound that holds it is latency -- the f64 VALU issue of
@@ -403,8 +416,12 @@ def main():
                      "valu_floor_us_per_iter": valu_us,
                      "valu_frac": valu_us / us_per_it if us_per_it > 0 else 0.0},
         # the dominant 3-D stencil kernel (DYNAMICS) against the HBM roofline
-        "roofline_hbm": {"bound": "hbm", "kernel": "DYNAMICS momentum block (MOM_FLUXFORM/MOM_VECINV + TIMESTEP + AB2; "
-                                                   "CALC_PHI_HYD timed apart as phi_hyd), streams serialised",
+        "roofline_hbm": {"bound": "hbm",
+                         "kernel": ("fused DYNAMICS + THERMODYNAMICS grids k_dt_l1/l2/l3 (the launches the timed graph "
+                                    "runs; bytes: momentum + the stepped tracers)" if dt_fused else
+                                    "DYNAMICS momentum block (MOM_FLUXFORM/MOM_VECINV + TIMESTEP + AB2; "
+                                    "CALC_PHI_HYD timed apart as phi_hyd), streams serialised"),
+                         "kernels": list(mom_kernels), "bytes_per_launch": mom_bytes,
                          "achieved": mom_gbs,
                          "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": mom_gbs / HBM_PEAK_GBS,
                          "bytes_per_point": mom_bpp, "launch_ms": mom_ms,

@@ -228,6 +228,7 @@ struct mgcm_model {
   float ovlMs[2] = {0.f, 0.f};
   hipEvent_t ovlEv[2] = {nullptr, nullptr};
   double *thetaA = nullptr, *saltA = nullptr;
+  int stepLayout = 0;   // one_step's launch layout (mgcm_get_param "stepLayout")
   // step counters: [0] = myIter, [1] = record slot
   int *d_ctr = nullptr;
   SolveRecord *d_rec = nullptr;
@@ -934,6 +935,10 @@ double mgcm_get_param(mgcm_model *m, const char *name) {
   if (!strcmp(name, "ovlMsOn")) return m->ovlMs[1];
   if (!strcmp(name, "ovlMsOff")) return m->ovlMs[0];
   if (!strcmp(name, "cg2dBxyVariant")) return (double)m->bxyVar;
+  // the launch layout of the last FORWARD_STEP built (one_step): bit 0 THERMODYNAMICS folded
+  // into DYNAMICS' grids (k_dt_l1/l2/l3), 1 DO_OCEANIC_PHYS + CALC_PHI_HYD in one pass,
+  // 2 the tracers on the second stream, 3 joined only before the correction step
+  if (!strcmp(name, "stepLayout")) return (double)m->stepLayout;
   // whether the selected kernel solves with fused multiply-adds (k_cg2d_bxy honours cg2dUseFMA)
   if (!strcmp(name, "cg2dFMA")) return (!m->p.cg2dRefOrder && !m->useMwg && m->nBlkX > 0 && m->p.cg2dUseFMA) ? 1.0 : 0.0;
   for (auto &pd : PARAMS)
@@ -1465,13 +1470,20 @@ static int one_step(mgcm_model *m) {
   // Early fork on a small grid: THERMODYNAMICS' tracer kernels share DYNAMICS' launches
   // (kernels_step.hip, MG_FUSE_DT) instead of running on the second stream -- no fork, no join
   const TracerArgs aT = tracer_args(m, false), aS = tracer_args(m, true);
-  const bool dtFused = fork && !lateJoin && !tracer_pair_ok(m->d, m->p, aT, aS) && dyn_thermo_fusable(m->d, m->p, aT, aS);
+  // (decided without the timing switch: one stream, so the eager timed pass runs the layout
+  // the graph replays -- bench.py's per-kernel times and PMC attribution then describe it)
+  const bool forkable = !stagger && m->overlap && m->p.momStepping && tracers;
+  const bool dtFused = forkable && m->p.nonlinFreeSurf > 0 && !tracer_pair_ok(m->d, m->p, aT, aS) &&
+                       dyn_thermo_fusable(m->d, m->p, aT, aS);
   // the multi-workgroup CG2D keeps its CUs to itself while the tracers run beside it
   m->mwg.exclusive = thermoLate ? 1 : 0;
   // DO_OCEANIC_PHYS + DYNAMICS' CALC_PHI_HYD in one column pass where exact (phys_phi_fusable:
   // THERMODYNAMICS, between them in FORWARD_STEP, reads DO_OCEANIC_PHYS's output and writes
   // nothing CALC_PHI_HYD reads)
   const bool physPhi = !stagger && m->p.momStepping && phys_phi_fusable(m->d, m->p);
+  // (the graph's layout: the eager timed pass, one stream, serialises a fork it reports here)
+  m->stepLayout = (dtFused ? 1 : 0) | (physPhi ? 2 : 0) | (forkable && !dtFused ? 4 : 0) |
+                  (forkable && m->p.nonlinFreeSurf <= 0 ? 8 : 0);
   // GMREDI_CALC_TENSOR beside CALC_PHI_HYD (launch_gm_phi) where THERMODYNAMICS, its reader,
   // runs after DYNAMICS (staggered, or forked after DYNAMICS) and the fold does not apply
   const bool gmPhi = (stagger || thermoLate) && !dtFused && !physPhi && !m->timing && gm_phi_fusable(m->d, m->p);
@@ -1482,7 +1494,7 @@ static int one_step(mgcm_model *m) {
                                            !(dtFused && dyn_thermo_takes_gm(m->p)) && !gmPhi));
     return 0;
   };
-  if (stagger || fork) {
+  if (stagger || fork || dtFused) {
     if (phys()) return -1;
     if (fork && !thermoLate && !dtFused && fork_thermo()) return -1;
   } else {

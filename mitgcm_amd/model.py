@@ -196,6 +196,13 @@ class Model:
         k = lib().mgcm_get_param(self.h, b"cg2dKernel")
         return {5.0: "block_ref", 4.0: "mwg", 3.0: "bxy", 2.0: "blk2"}.get(k, "block")
 
+    def step_layout(self):
+        """The launch layout of the last step built (mgcm_get_param 'stepLayout'): which
+        fusions of one_step (model.hip) the timed graph and the eager timed pass run."""
+        b = int(lib().mgcm_get_param(self.h, b"stepLayout"))
+        return {"dyn_thermo_fused": bool(b & 1), "phys_phi_fused": bool(b & 2), "thermo_second_stream": bool(b & 4),
+                "late_join": bool(b & 8)}
+
     def cg2d_fma(self):
         """True when the selected CG2D kernel solves in fused multiply-adds (cg2dUseFMA): the
         device-order oracle must then evaluate the same fma chains (Oracle.set_sum_plan(fma=))."""
