@@ -52,6 +52,12 @@ int mgcm_set_iter(mgcm_model *m, int myIter);
  * e.g. "uVel", "hFacW", "aW2d", "fu").  count = number of doubles. */
 int mgcm_put(mgcm_model *m, const char *name, const double *host, long count);
 int mgcm_get(mgcm_model *m, const char *name, double *host, long count);
+/* mgcm_put in stream order, without a host synchronisation: the host arrays are staged in
+ * pinned memory (two slots) and may be reused as soon as the call returns; a batch of n
+ * fields goes up as one copy and one scatter launch. */
+int mgcm_put_async(mgcm_model *m, const char *name, const double *host, long count);
+int mgcm_put_batch_async(mgcm_model *m, int n, const char *const *names, const double *const *hosts,
+                         const long *counts);
 /* Device pointer of a named field (for zero-copy interop, e.g. torch tensors). */
 double *mgcm_device_ptr(mgcm_model *m, const char *name);
 

@@ -34,6 +34,8 @@ def lib():
         "mgcm_set_iter": (ci, [vp, ci]),
         "mgcm_get_param": (cd, [vp, cs]),
         "mgcm_put": (ci, [vp, cs, PD, cl]),
+        "mgcm_put_async": (ci, [vp, cs, PD, cl]),
+        "mgcm_put_batch_async": (ci, [vp, ctypes.c_int, ctypes.POINTER(cs), ctypes.POINTER(PD), ctypes.POINTER(cl)]),
         "mgcm_get": (ci, [vp, cs, PD, cl]),
         "mgcm_device_ptr": (vp, [vp, cs]),
         "mgcm_set_halo_map": (ci, [vp, PL, cl]),
@@ -95,7 +97,7 @@ def lib():
     return L
 
 
-EXPORTS = ["mgcm_create", "mgcm_destroy", "mgcm_last_error", "mgcm_set_param", "mgcm_get_param", "mgcm_put",
+EXPORTS = ["mgcm_create", "mgcm_destroy", "mgcm_last_error", "mgcm_set_param", "mgcm_get_param", "mgcm_put", "mgcm_put_async", "mgcm_put_batch_async",
            "mgcm_get", "mgcm_device_ptr", "mgcm_set_halo_map", "mgcm_set_uv_map", "mgcm_init", "mgcm_dynamics", "mgcm_thermodynamics",
            "mgcm_solve_for_pressure", "mgcm_momentum_correction_step", "mgcm_integr_continuity",
            "mgcm_blocking_exchanges", "mgcm_prepare", "mgcm_forward_step", "mgcm_sync", "mgcm_cg2d", "mgcm_cg2d_sum_plan", "mgcm_solve_stats", "mgcm_solve_history", "mgcm_monitor",

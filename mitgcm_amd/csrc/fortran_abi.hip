@@ -134,6 +134,10 @@ struct FortranSide {
   bool recording = false, canFuse = false, fused = false;
   size_t fusedPos = 0;
   long nUp = 0, nDown = 0;   // copies of whole bound arrays, for mgcm_amd_transfer_stats_
+  // the state arrays' host pages, registered with HIP once the time loop begins (downloads
+  // then go straight to the COMMON blocks by DMA); false when registration was refused
+  bool hostRegistered = false, regTried = false;
+  std::vector<std::vector<double>> strided;   // downloads of the strided bound arrays
   double bytesUp = 0.0, bytesDown = 0.0;
 };
 FortranSide g;
@@ -292,23 +296,32 @@ void set_iter(const char *where, int myIter) {
   g.devIter = myIter;
 }
 
-// kinds: bit k set = move the arrays of kind k (to every model: each holds the domain)
+// kinds: bit k set = move the arrays of kind k (to every model: each holds the domain), as
+// one staged batch per model in stream order (mgcm_put_batch_async: no host wait)
 void upload(const char *where, unsigned kinds) {
-  std::vector<double> tmp;
+  std::vector<std::vector<double>> tmp;
+  std::vector<const char *> names;
+  std::vector<const double *> src;
+  std::vector<long> cnt;
+  tmp.reserve(g.bound.size());
   for (auto &b : g.bound) {
     if (!((kinds >> b.kind) & 1u)) continue;
-    const double *src = b.host;
+    const double *p = b.host;
     if (b.stride != 1) {
-      tmp.resize(b.count);
-      for (long q = 0; q < b.count; q++) tmp[q] = b.host[q * b.stride + b.off];
-      src = tmp.data();
+      tmp.emplace_back(b.count);
+      for (long q = 0; q < b.count; q++) tmp.back()[q] = b.host[q * b.stride + b.off];
+      p = tmp.back().data();
     }
-    for (auto &s : g.sh) {
-      hipchk(hipSetDevice(s.dev), where);
-      if (mgcm_put(s.m, b.name.c_str(), src, b.count)) die(where);
-    }
+    names.push_back(b.name.c_str());
+    src.push_back(p);
+    cnt.push_back(b.count);
     g.nUp++;
     g.bytesUp += 8.0 * b.count;
+  }
+  if (names.empty()) return;
+  for (auto &s : g.sh) {
+    hipchk(hipSetDevice(s.dev), where);
+    if (mgcm_put_batch_async(s.m, (int)names.size(), names.data(), src.data(), cnt.data())) die(where);
   }
 }
 
@@ -317,35 +330,84 @@ void sync_all(const char *where) {
     if (mgcm_sync(s.m)) die(where);
 }
 
+// The state arrays' pages registered for DMA (page-rounded, overlapping ranges merged): a
+// download is then one copy engine transfer straight into the COMMON block instead of a
+// staged copy.  A refusal leaves them unregistered (the copies still work, staged by HIP).
+void register_host() {
+  if (g.regTried) return;
+  g.regTried = true;
+  if (getenv("MGCM_AMD_REGISTER") && atoi(getenv("MGCM_AMD_REGISTER")) == 0) return;
+  const uintptr_t pg = 4096;
+  std::vector<std::pair<uintptr_t, uintptr_t>> iv;
+  for (auto &b : g.bound)
+    if (b.kind == 0) {
+      const uintptr_t a = (uintptr_t)b.host, e = a + (uintptr_t)(b.count * b.stride) * sizeof(double);
+      iv.push_back({a & ~(pg - 1), (e + pg - 1) & ~(pg - 1)});
+    }
+  std::sort(iv.begin(), iv.end());
+  std::vector<std::pair<uintptr_t, uintptr_t>> merged;
+  for (auto &r : iv)
+    if (!merged.empty() && r.first <= merged.back().second) merged.back().second = std::max(merged.back().second, r.second);
+    else merged.push_back(r);
+  size_t done = 0;
+  for (auto &r : merged) {
+    if (hipHostRegister((void *)r.first, r.second - r.first, hipHostRegisterPortable) != hipSuccess) {
+      (void)hipGetLastError();
+      break;
+    }
+    done++;
+  }
+  size_t bytes = 0;
+  for (auto &r : merged) bytes += r.second - r.first;
+  if (done != merged.size()) {   // all or nothing
+    for (size_t i = 0; i < done; i++) (void)hipHostUnregister((void *)merged[i].first);
+    fprintf(stderr, "MGCM_AMD: state pages not registered (range %zu of %zu refused); downloads staged\n", done + 1,
+            merged.size());
+    return;
+  }
+  g.hostRegistered = true;
+  fprintf(stderr, "MGCM_AMD: state pages registered for DMA: %zu ranges, %.1f MB\n", merged.size(), bytes / 1e6);
+}
+
 // The state down: a tiled array (2-D or 3-D, tile-major) block by block from each tile's
-// owner, anything else (1-D profiles) from model 0.
+// owner, anything else (1-D profiles) from model 0.  Every copy is queued first (each
+// model's stream, behind the step), then one wait.
 void download(const char *where) {
-  sync_all(where);
   const long per2 = n2(), per3 = per2 * g.dims[4], nt = nTiles();
-  std::vector<double> tmp;
-  for (auto &b : g.bound) {
+  if (g.strided.size() != g.bound.size()) g.strided.resize(g.bound.size());
+  for (size_t i = 0; i < g.bound.size(); i++) {
+    Bound &b = g.bound[i];
     if (b.kind != 0) continue;   // static and host-input arrays are never written on the device
     g.nDown++;
     g.bytesDown += 8.0 * b.count;
     const long per = b.count == per2 * nt ? per2 : b.count == per3 * nt ? per3 : 0;
-    if (multi() && per && b.stride == 1) {
+    double *dst = b.host;
+    if (b.stride != 1) {
+      g.strided[i].resize(b.count);
+      dst = g.strided[i].data();
+    }
+    if (multi() && per) {
       for (auto &s : g.sh) {
         const double *dp = mgcm_device_ptr(s.m, b.name.c_str());
         if (!dp) die(where);
         hipchk(hipSetDevice(s.dev), where);
-        hipchk(hipMemcpy(b.host + s.t0 * per, dp + s.t0 * per, (size_t)s.nT * per * sizeof(double),
-                         hipMemcpyDeviceToHost),
+        hipchk(hipMemcpyAsync(dst + s.t0 * per, dp + s.t0 * per, (size_t)s.nT * per * sizeof(double),
+                              hipMemcpyDeviceToHost, stream_of(s)),
                where);
       }
       continue;
     }
-    if (b.stride == 1) {
-      if (mgcm_get(g.m, b.name.c_str(), b.host, b.count)) die(where);
-      continue;
-    }
-    tmp.resize(b.count);
-    if (mgcm_get(g.m, b.name.c_str(), tmp.data(), b.count)) die(where);
-    for (long q = 0; q < b.count; q++) b.host[q * b.stride + b.off] = tmp[q];
+    const double *dp = mgcm_device_ptr(g.m, b.name.c_str());
+    if (!dp) die(where);
+    hipchk(hipSetDevice(g.sh[0].dev), where);
+    hipchk(hipMemcpyAsync(dst, dp, (size_t)b.count * sizeof(double), hipMemcpyDeviceToHost, stream_of(g.sh[0])),
+           where);
+  }
+  sync_all(where);
+  for (size_t i = 0; i < g.bound.size(); i++) {
+    Bound &b = g.bound[i];
+    if (b.kind != 0 || b.stride == 1) continue;
+    for (long q = 0; q < b.count; q++) b.host[q * b.stride + b.off] = g.strided[i][q];
   }
 }
 
@@ -357,6 +419,7 @@ void enter_time_loop(const char *where) {
   if (g.deviceAuth) return;
   upload(where, K_STATE | K_INPUT);
   g.deviceAuth = true;
+  register_host();
 }
 
 // One routine drop-in.  Host-authoritative (initialisation): state in, the device
@@ -734,6 +797,8 @@ void mgcm_amd_device_sync_(const int *myThid) {
 void mgcm_amd_step_fence_(const int *myThid) {
   (void)myThid;
   model("MGCM_AMD_STEP_FENCE");
+  static const bool off = getenv("MGCM_AMD_STEP_FENCE") && atoi(getenv("MGCM_AMD_STEP_FENCE")) == 0;
+  if (off) return;   // per-step times then measure the host's side (the steps pipeline)
   sync_all("MGCM_AMD_STEP_FENCE");
 }
 

@@ -229,6 +229,13 @@ struct mgcm_model {
   hipEvent_t ovlEv[2] = {nullptr, nullptr};
   double *thetaA = nullptr, *saltA = nullptr;
   int stepLayout = 0;   // one_step's launch layout (mgcm_get_param "stepLayout")
+  // mgcm_put_batch_async: two pinned host slots (each with the event of its last copy) and
+  // one device buffer; a batch travels as [header | values] in one copy, then one scatter
+  char *stHost[2] = {nullptr, nullptr};
+  hipEvent_t stEv[2] = {nullptr, nullptr};
+  size_t stCap = 0;
+  int stNext = 0;
+  char *stDev = nullptr;
   // step counters: [0] = myIter, [1] = record slot
   int *d_ctr = nullptr;
   SolveRecord *d_rec = nullptr;
@@ -861,6 +868,11 @@ void mgcm_destroy(mgcm_model *m) {
   if (m->d_rec) hipFree(m->d_rec);
   if (m->mwgShared) (void)hipIpcCloseMemHandle(m->mwgShared);
   for (void *q : m->mwgAllocs) hipFree(q);
+  for (int q = 0; q < 2; q++) {
+    if (m->stHost[q]) hipHostFree(m->stHost[q]);
+    if (m->stEv[q]) hipEventDestroy(m->stEv[q]);
+  }
+  if (m->stDev) hipFree(m->stDev);
   if (m->ownStream) hipStreamDestroy(m->ownStream);
   if (m->stream2) hipStreamDestroy(m->stream2);
   if (m->evFork) hipEventDestroy(m->evFork);
@@ -959,6 +971,85 @@ int mgcm_put(mgcm_model *m, const char *name, const double *host, long count) {
   HIPCHK(hipMemcpyAsync(field_ptr(m, fd), host, count * sizeof(double), hipMemcpyHostToDevice, m->stream));
   HIPCHK(hipStreamSynchronize(m->stream));
   return 0;
+}
+
+namespace mgcm {
+// The values of a staged batch to their fields: blockIdx.y = the field, its header entry
+// (destination, start) read from the batch itself
+__global__ void __launch_bounds__(256) k_put_scatter(const char *batch) {
+  const long *hdr = reinterpret_cast<const long *>(batch);
+  const long n = hdr[0];
+  const int y = blockIdx.y;
+  if (y >= n) return;
+  double *dst = reinterpret_cast<double *>(hdr[1 + y]);
+  const long o0 = hdr[1 + n + y], o1 = hdr[2 + n + y];
+  const double *src = reinterpret_cast<const double *>(batch) + 2 + 2 * n;
+  for (long i = o0 + blockIdx.x * 256L + threadIdx.x; i < o1; i += (long)gridDim.x * 256L) dst[i - o0] = src[i];
+}
+}  // namespace mgcm
+
+// mgcm_put of n fields in stream order, without a host synchronisation: the host arrays are
+// copied into a pinned slot as [n | destinations | starts | values], which goes up in one
+// copy and is scattered to the fields by one launch.  A slot is reused only after its
+// previous copy (two calls back) completed, so a step's upload never waits on the step before
+// it; the host arrays may be reused as soon as the call returns.
+int mgcm_put_batch_async(mgcm_model *m, int n, const char *const *names, const double *const *hosts,
+                         const long *counts) {
+  if (n <= 0) return 0;
+  std::vector<double *> dst(n);
+  long total = 0, maxc = 0;
+  for (int i = 0; i < n; i++) {
+    const FieldDesc *fd = find_field(names[i]);
+    if (!fd) return set_err("mgcm_put_batch_async: unknown field %s", names[i]);
+    const long lim = field_count(m, fd->kind);
+    if (counts[i] > lim || counts[i] <= 0)
+      return set_err("mgcm_put_batch_async: %s count %ld > %ld", names[i], counts[i], lim);
+    dst[i] = field_ptr(m, fd);
+    total += counts[i];
+    maxc = std::max(maxc, counts[i]);
+  }
+  HIPCHK(hipSetDevice(m->device));
+  const size_t bytes = (size_t)(2 + 2 * n + total) * sizeof(double);
+  if (m->stCap < bytes) {
+    for (int q = 0; q < 2; q++) {
+      if (m->stEv[q]) HIPCHK(hipEventSynchronize(m->stEv[q]));
+      if (m->stHost[q]) HIPCHK(hipHostFree(m->stHost[q]));
+      m->stHost[q] = nullptr;
+      HIPCHK(hipHostMalloc((void **)&m->stHost[q], bytes, hipHostMallocDefault));
+      if (!m->stEv[q]) HIPCHK(hipEventCreateWithFlags(&m->stEv[q], hipEventDisableTiming));
+    }
+    if (m->stDev) {
+      HIPCHK(hipStreamSynchronize(m->stream));
+      HIPCHK(hipFree(m->stDev));
+    }
+    m->stDev = nullptr;
+    HIPCHK(hipMalloc((void **)&m->stDev, bytes));
+    m->stCap = bytes;
+  }
+  const int q = m->stNext;
+  m->stNext ^= 1;
+  HIPCHK(hipEventSynchronize(m->stEv[q]));
+  long *hdr = reinterpret_cast<long *>(m->stHost[q]);
+  double *vals = reinterpret_cast<double *>(m->stHost[q]) + 2 + 2 * n;
+  hdr[0] = n;
+  long o = 0;
+  for (int i = 0; i < n; i++) {
+    hdr[1 + i] = reinterpret_cast<long>(dst[i]);
+    hdr[1 + n + i] = o;
+    memcpy(vals + o, hosts[i], counts[i] * sizeof(double));
+    o += counts[i];
+  }
+  hdr[1 + 2 * n] = o;
+  HIPCHK(hipMemcpyAsync(m->stDev, m->stHost[q], bytes, hipMemcpyHostToDevice, m->stream));
+  HIPCHK(hipEventRecord(m->stEv[q], m->stream));
+  const unsigned gx = (unsigned)std::min<long>(64, (maxc + 255) / 256);
+  hipLaunchKernelGGL(mgcm::k_put_scatter, dim3(gx, n), dim3(256), 0, m->stream, m->stDev);
+  HIPCHK(hipGetLastError());
+  return 0;
+}
+
+int mgcm_put_async(mgcm_model *m, const char *name, const double *host, long count) {
+  return mgcm_put_batch_async(m, 1, &name, &host, &count);
 }
 
 int mgcm_get(mgcm_model *m, const char *name, double *host, long count) {

@@ -63,7 +63,7 @@ def _name(s):
 PARAM_DIR = os.path.join(ROOT, "tests", "golden", "global_ocean.90x40x15", "input")
 
 
-def _write_blob(path, m, nsteps, monitor_days, packages_off=True):
+def _write_blob(path, m, nsteps, monitor_days, packages_off=True, extra=()):
     """refhost_in.bin: sizes, the run's control (the only parameters it carries: the run length,
     the monitor schedule, and -- packages_off -- pkg/sbo and pkg/diagnostics switched off for
     the run), the COMMON-block arrays (grid, masks and the restart state) and the forcing
@@ -75,6 +75,7 @@ def _write_blob(path, m, nsteps, monitor_days, packages_off=True):
     params = [("monitorFreq", monitor_days * dtc), ("nEndIter", float(nIter0 + nsteps))]
     if packages_off:
         params += [("useSBO", 0.0), ("useDiagnostics", 0.0)]
+    params += list(extra)
     periodic = int(m.params.get("periodicExternalForcing", 0))
     nRec = int(m.params.get("nForcRec", 12)) if periodic else 0
     blob_fields = []
@@ -188,3 +189,50 @@ def test_refhost_mods_dropins_bitexact(layout, refOrder, models, mwg, eager, pac
     # the state came down after steps 2, 4 and 6 only (monitorFreq = 2 days, nEndIter = 6),
     # or after every step when pkg/sbo and pkg/diagnostics read it (packages)
     assert st["downloads"] == (NSTEPS if packages else 3) * len(state), (st, len(state))
+
+
+# Throughput of the drop-in path over a longer run: 60 steps, every step after the recorded
+# one a replay whose forcing goes up in stream order (mgcm_put_async) while the previous step
+# still runs -- no per-step fence (MGCM_AMD_STEP_FENCE=0), so the host's Fortran side of step
+# n+1 overlaps the device's step n.  io = "namelist": the experiment's own output schedule
+# (dumpFreq = 10 days: the state comes down after every 10th step, into the registered COMMON
+# pages); io = "off": dumpFreq = 0, the state comes down after the last step only.  The state
+# after the run is bit-identical to the resident graph path's; both rates are recorded
+# (INTEGRATION.md section 3).
+@pytest.mark.parametrize("io,register", [("namelist", 1), ("off", 1), ("namelist", 0)])
+def test_refhost_dropin_throughput(io, register, tmp_path):
+    from mitgcm_amd import configs
+    nsteps = 60
+    exe = os.path.join(RH, "refhost_ref")
+    assert os.path.exists(exe), "refhost not built (mitgcm_amd/fortran/build_refhost.py, __graft_entry__.build())"
+    m = configs.make_model(lambda: configs.global_ocean_90x40x15(nSx=9, nSy=4))
+    extra = [("dumpFreq", 0.0)] if io == "off" else []
+    state = _write_blob(tmp_path / "refhost_in.bin", m, nsteps, monitor_days=10 * nsteps, extra=extra)
+    env = dict(os.environ, MGCM_AMD_MODELS="1", MGCM_AMD_EAGER="0", MGCM_AMD_STEP_FENCE="0",
+               MGCM_AMD_REGISTER=str(register))
+    r = subprocess.run([exe, str(tmp_path), PARAM_DIR], capture_output=True, text=True, timeout=300, env=env)
+    assert r.returncode == 0, r.stdout + r.stderr
+    out, st = _read_out(tmp_path / "refhost_out.bin", state, nsteps)
+    m.forward_step(1)
+    m.prepare()
+    m.sync()
+    t0 = time.perf_counter()
+    m.forward_step(nsteps - 1)
+    m.sync()
+    graph_ms = 1e3 * (time.perf_counter() - t0) / (nsteps - 1)
+    bad = [(n, float(np.abs(out[n] - m.get(n).reshape(-1)[:out[n].size]).max())) for n in CHECK
+           if n in out and not np.array_equal(out[n], m.get(n).reshape(-1)[:out[n].size])]
+    m.close()
+    rec = {"steps": nsteps, "io": io, "register": register, "dropin_ms_per_step": 1e3 * st["seconds"] / max(1, st["steps_timed"]),
+           "graph_ms_per_step": graph_ms, "uploads": st["uploads"], "downloads": st["downloads"],
+           "bytes_down": st["bytes_down"],
+           "dropin_ms_per_step_steady": float(np.median(st["step_ms"][5:-1])),
+           "registered": [ln for ln in r.stderr.splitlines() if ln.startswith("MGCM_AMD: state pages")],
+           "host_side_step_ms": [round(x, 4) for x in st["step_ms"]]}
+    print("refhost throughput: %s" % json.dumps(rec))
+    if os.path.isdir(os.path.join(ROOT, "gpurun_out")):
+        with open(os.path.join(ROOT, "gpurun_out", "refhost_throughput_%s_r%d.json" % (io, register)), "w") as f:
+            json.dump(rec, f)
+    assert not bad, bad
+    # the state came down after steps 10, 20, ..., 60 (dumpFreq) or after the last only
+    assert st["downloads"] == (nsteps // 10 if io == "namelist" else 1) * len(state), st
