@@ -229,6 +229,10 @@ struct mgcm_model {
   hipEvent_t ovlEv[2] = {nullptr, nullptr};
   double *thetaA = nullptr, *saltA = nullptr;
   int stepLayout = 0;   // one_step's launch layout (mgcm_get_param "stepLayout")
+  // THERMODYNAMICS of a sharded step on the second stream (mgcm_step_phase 16): 1 forked after
+  // DO_OCEANIC_PHYS (joined before UPDATE_R_STAR), 2 to fork after DYNAMICS, 3 forked after
+  // DYNAMICS (joined before the correction step), 0 none pending
+  int shardFork = 0;
   // mgcm_put_batch_async: two pinned host slots (each with the event of its last copy) and
   // one device buffer; a batch travels as [header | values] in one copy, then one scatter
   char *stHost[2] = {nullptr, nullptr};
@@ -583,6 +587,7 @@ static int mwg_upload(mgcm_model *m, const std::vector<T> &h, const T **out) {
   return 0;
 }
 
+static int mwg_block_realloc(mgcm_model *m, int mem, bool sys);
 static int build_mwg(mgcm_model *m) {
   for (void *q : m->mwgAllocs) (void)hipFree(q);
   m->mwgAllocs.clear();
@@ -727,6 +732,16 @@ static int build_mwg(mgcm_model *m) {
   T.xs = T.part + partGr;
   T.hsBytes = hs;
   m->useMwg = true;
+  // The hand-off block's memory: where the parts spread over the XCDs (not pinned), uncached
+  // device memory -- a granule store is then visible to the other XCDs' polls without an L2
+  // round of its own: LLC-90 1.591 ms/step against 1.688 with the coarse-grained block, 117
+  // parts, ~1 us per CG iteration (profiles/r04/mwgmem/); the XCD-pinned parts (cube, <= 32
+  // parts, one XCD's L2) keep coarse-grained memory (cs32x15 0.416 against 0.421-0.455).
+  // MGCM_MWG_BLOCK=coarse|uncached|fine overrides, MGCM_MWG_SYS=1 for system-scope accesses.
+  const char *bk = getenv("MGCM_MWG_BLOCK");
+  const int mem = bk ? (!strcmp(bk, "uncached") ? 1 : !strcmp(bk, "fine") ? 2 : 0) : (T.pinned ? 0 : 1);
+  const bool sys = getenv("MGCM_MWG_SYS") && atoi(getenv("MGCM_MWG_SYS")) == 1;
+  if (mem && mwg_block_realloc(m, mem, sys)) return -1;
   return 0;
 }
 
@@ -2007,11 +2022,45 @@ int mgcm_begin_steps(mgcm_model *m) {
 //   5: staggerTimeStep only: DO_STAGGER_FIELDS_EXCHANGES on this process's tiles, then
 //      THERMODYNAMICS with the new velocities;  [send/recv the 3-D halo sources again]
 //   4: DO_FIELDS_BLOCKING_EXCHANGES of this process's tiles, step counters.
+// THERMODYNAMICS onto the second stream (after the model stream's work so far) and its join
+static int shard_fork_thermo(mgcm_model *m) {
+  HIPCHK(hipEventRecord(m->evFork, m->stream));
+  HIPCHK(hipStreamWaitEvent(m->stream2, m->evFork, 0));
+  if (tracers_on(m, m->stream2)) return -1;
+  HIPCHK(hipEventRecord(m->evJoin, m->stream2));
+  return 0;
+}
+static int shard_join_thermo(mgcm_model *m) {
+  if (m->shardFork == 1 || m->shardFork == 3) HIPCHK(hipStreamWaitEvent(m->stream, m->evJoin, 0));
+  m->shardFork = 0;
+  m->mwg.exclusive = 0;
+  return 0;
+}
+
 int mgcm_step_phase(mgcm_model *m, int phase) {
   if (check_ready(m)) return -1;
   if (!m->p.momStepping) return set_err("mgcm_step_phase: requires momStepping");
   const bool stagger = m->p.staggerTimeStep != 0;
+  const bool tracers = m->p.tempStepping || m->p.saltStepping;
   switch (phase) {
+    case 16:  // DO_OCEANIC_PHYS, THERMODYNAMICS on the second stream as the resident step forks it
+              // (one_step): beside DYNAMICS under r* (joined before UPDATE_R_STAR, which rewrites
+              // hFac), beside the pressure solve under the linear free surface (forked after
+              // DYNAMICS, joined before MOMENTUM_CORRECTION_STEP rewrites u, v, w)
+      if (stagger || !tracers || m->timing) {   // nothing to fork (the timed pass: one stream)
+        phase = 8;
+      } else {
+        if (m->shardFork) return set_err("mgcm_step_phase(16): the previous step's THERMODYNAMICS not joined");
+        TIMED(K_PHYS, launch_oceanic_phys(m->d, m->p, m->f, m->d_ctr, m->stream));
+        if (m->p.nonlinFreeSurf > 0) {
+          if (shard_fork_thermo(m)) return -1;
+          m->shardFork = 1;
+        } else {
+          m->shardFork = 2;
+        }
+        return 0;
+      }
+      [[fallthrough]];
     case 1:   // = 8 then 9
     case 8:   // DO_OCEANIC_PHYS + THERMODYNAMICS (non-staggered): the tracers are final
       TIMED(K_PHYS, launch_oceanic_phys(m->d, m->p, m->f, m->d_ctr, m->stream));
@@ -2020,12 +2069,18 @@ int mgcm_step_phase(mgcm_model *m, int phase) {
       [[fallthrough]];
     case 9:   // DYNAMICS, UPDATE_R_STAR + UPDATE_CG2D, CALC_DIV_GHAT
       if (mgcm_dynamics(m)) return -1;
+      if (m->shardFork == 2) {
+        if (shard_fork_thermo(m)) return -1;
+        m->shardFork = 3;
+        m->mwg.exclusive = 1;   // the multi-workgroup CG2D keeps its CUs while the tracers run
+      } else if (m->shardFork == 1 && shard_join_thermo(m)) return -1;
       if (m->p.nonlinFreeSurf > 0) TIMED(K_RSTAR, update_r_star_cg2d(m));
       TIMED(K_RHS, launch_sfp_rhs(m->d, m->p, m->f, m->stream));
       return 0;
     case 2:
       TIMED(K_CG2D, launch_cg2d(m, m->p.cg2dMaxIters, m->p.cg2dUseMinResSol - 1));
       TIMED(K_ETA, launch_exch_eta(m->d, m->p, m->f, m->d_srcOf, false, 0, m->stream));
+      if (shard_join_thermo(m)) return -1;
       TIMED(K_CONT, launch_corr_cont(m->d, m->p, m->f, 0, m->stream));
       return 0;
     case 10:  // the device CG2D over this process's parts (hand-off block shared by IPC)
@@ -2038,9 +2093,11 @@ int mgcm_step_phase(mgcm_model *m, int phase) {
       return 0;
     case 6:   // phase 2 after a CG2D driven by the caller (mgcm_cg2d_op: distributed CG2D)
       TIMED(K_ETA, launch_exch_eta(m->d, m->p, m->f, m->d_srcOf, false, 0, m->stream));
+      if (shard_join_thermo(m)) return -1;
       TIMED(K_CONT, launch_corr_cont(m->d, m->p, m->f, 0, m->stream));
       return 0;
     case 3:
+      if (shard_join_thermo(m)) return -1;
       if (m->p.exactConserv) TIMED(K_ETA, launch_exch_eta(m->d, m->p, m->f, m->d_srcOf, true, 0, m->stream));
       if (m->p.nonlinFreeSurf > 0) TIMED(K_RSTAR, calc_r_star(m));
       return 0;
@@ -2122,15 +2179,13 @@ int mgcm_cg2d_tiles(mgcm_model *m, int t0, int nT) {
   return 0;
 }
 
-// A hand-off block that other launches poll from another GPU: uncached device memory, so no
-// GPU's L2 holds a stale copy of a granule (coarse-grained hipMalloc memory is coherent only at
-// kernel boundaries); every granule access is then at system scope (T.sys).
-static int mwg_block_uncached(mgcm_model *m) {
-  if (m->mwg.sys) return 0;
+// The hand-off block re-allocated as uncached (mem 1) or fine-grained (mem 2) device memory,
+// its granules accessed at system scope (sys) or agent scope.
+static int mwg_block_realloc(mgcm_model *m, int mem, bool sys) {
   const size_t partGr = (size_t)2 * 3 * m->mwg.G * 2;
   char *blk = nullptr;
-  if (hipExtMallocWithFlags((void **)&blk, m->mwg.hsBytes, hipDeviceMallocUncached) != hipSuccess)
-    HIPCHK(hipExtMallocWithFlags((void **)&blk, m->mwg.hsBytes, hipDeviceMallocFinegrained));
+  if (mem != 2 && hipExtMallocWithFlags((void **)&blk, m->mwg.hsBytes, hipDeviceMallocUncached) != hipSuccess) blk = nullptr;
+  if (!blk) HIPCHK(hipExtMallocWithFlags((void **)&blk, m->mwg.hsBytes, hipDeviceMallocFinegrained));
   HIPCHK(hipMemset(blk, 0, m->mwg.hsBytes));
   HIPCHK(hipDeviceSynchronize());
   for (auto &q : m->mwgAllocs)
@@ -2139,9 +2194,17 @@ static int mwg_block_uncached(mgcm_model *m) {
   m->mwg.ctr = (unsigned *)blk;
   m->mwg.part = (unsigned long long *)(blk + 64);
   m->mwg.xs = m->mwg.part + partGr;
-  m->mwg.sys = 1;
+  m->mwg.sys = sys ? 1 : 0;
   drop_graphs(m);
   return 0;
+}
+
+// A hand-off block that other launches poll from another GPU: uncached device memory, so no
+// GPU's L2 holds a stale copy of a granule (coarse-grained hipMalloc memory is coherent only at
+// kernel boundaries); every granule access is then at system scope (T.sys).
+static int mwg_block_uncached(mgcm_model *m) {
+  if (m->mwg.sys) return 0;
+  return mwg_block_realloc(m, 1, true);
 }
 
 // In-process sharing of `owner`'s hand-off block by m (another model of the same host, on

@@ -181,7 +181,7 @@ class ShardedModel:
     configuration; after init(), step()/forward_step() keep the tiles a
     process owns bit-identical to a single-process run."""
 
-    def __init__(self, model, dist, device=None, cg2d="auto", overlap=True, model_stream="shared"):
+    def __init__(self, model, dist, device=None, cg2d="auto", overlap="thermo", model_stream="shared"):
         import torch
         from ._lib import check, lib
         self.torch, self.dist, self.m = torch, dist, model
@@ -217,8 +217,20 @@ class ShardedModel:
         self.nf = self.L.mgcm_exchange_nfields(h)
         # the halo field groups (mgcm_halo_pack_group): 0 all, 1 the tracers, 2 the rest
         self.nfg = {grp: self.L.mgcm_exchange_nfields_group(h, grp) for grp in (0, 1, 2)}
-        # non-staggered steps: the tracers' exchange travels while DYNAMICS and the solve run
-        self.overlap = bool(overlap) and not self.stagger and self.nfg[1] > 0
+        # overlap (non-staggered steps):
+        #   "thermo" (default, True): THERMODYNAMICS on the model's second stream as the resident
+        #     step runs it -- beside DYNAMICS under r*, beside the pressure solve under the linear
+        #     free surface (mgcm_step_phase 16) -- and the halos leave together at the step's end;
+        #   "halo": THERMODYNAMICS first, then the tracers' halo sources travel while DYNAMICS,
+        #     the solve and the continuity step compute;
+        #   False: one stream, one exchange at the step's end.
+        if overlap is True:
+            overlap = "thermo"
+        if overlap not in (False, None, "thermo", "halo"):
+            raise ValueError("overlap must be 'thermo', 'halo' or False")
+        tracers = bool(model.params.get("tempStepping", 1)) or bool(model.params.get("saltStepping", 1))
+        self.fork = overlap == "thermo" and not self.stagger and tracers
+        self.overlap = overlap == "halo" and not self.stagger and self.nfg[1] > 0
         dv = self.dev
         self.idx = {p: torch.as_tensor(v, device=dv) for p, v in
                     list(self.plan.send.items()) + [(("r", q), w) for q, w in self.plan.recv.items()]}
@@ -427,7 +439,10 @@ class ShardedModel:
     def step(self):
         L, h, ck = self.L, self.m.h, self.check
         fin_tracers = None
-        if self.overlap:
+        if self.fork:
+            ck(L.mgcm_step_phase(h, 16), "mgcm_step_phase(16)")
+            ck(L.mgcm_step_phase(h, 9), "mgcm_step_phase(9)")
+        elif self.overlap:
             # DO_OCEANIC_PHYS + THERMODYNAMICS, then the tracers' halo sources leave while
             # DYNAMICS, the solve and the continuity step compute
             ck(L.mgcm_step_phase(h, 8), "mgcm_step_phase(8)")

@@ -40,7 +40,7 @@ def _make(cfg, force_mwg=False):
     return configs.make_model(fn)
 
 
-def _worker(rank, world, port, cfg, nsteps, q, cg2d="replicated", overlap=True):
+def _worker(rank, world, port, cfg, nsteps, q, cg2d="replicated", overlap="thermo"):
     import torch
     import torch.distributed as dist
     from mitgcm_amd.parallel import ShardedModel
@@ -55,7 +55,7 @@ def _worker(rank, world, port, cfg, nsteps, q, cg2d="replicated", overlap=True):
         m.sync()
         full = {n: sm.gather_field(n) for n in FIELDS}
         stats = [m.solve_stats(back=b) for b in range(nsteps)]
-        res = {"t0": sm.t0, "nT": sm.nT, "stats": stats, "overlap": sm.overlap}
+        res = {"t0": sm.t0, "nT": sm.nT, "stats": stats, "overlap": sm.overlap, "fork": sm.fork}
         if cg2d == "distributed":
             res["iters"] = list(sm.cg_iters)
         if cg2d in ("distributed", "device") and rank == 0:
@@ -78,16 +78,19 @@ def _worker(rank, world, port, cfg, nsteps, q, cg2d="replicated", overlap=True):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("cfg,world,nsteps,ntiles,overlap", [("gyre", 2, 6, 4, True), ("gyre", 4, 6, 4, True),
-                                                             ("gyre", 2, 6, 4, False),
-                                                             ("cs32x15", 2, 4, 6, True), ("cs32x15", 4, 4, 6, True),
-                                                             ("cs32x15", 6, 4, 6, True),
-                                                             ("llc30", 2, 4, 13, True), ("llc30", 4, 4, 13, True)])
+@pytest.mark.parametrize("cfg,world,nsteps,ntiles,overlap", [("gyre", 2, 6, 4, "thermo"), ("gyre", 4, 6, 4, "thermo"),
+                                                             ("gyre", 2, 6, 4, "halo"), ("gyre", 2, 6, 4, False),
+                                                             ("cs32x15", 2, 4, 6, "thermo"),
+                                                             ("cs32x15", 4, 4, 6, "thermo"),
+                                                             ("cs32x15", 6, 4, 6, "thermo"),
+                                                             ("llc30", 2, 4, 13, "thermo"), ("llc30", 4, 4, 13, "thermo"),
+                                                             ("llc30", 2, 4, 13, "halo")])
 def test_sharded_bit_identical(cfg, world, nsteps, ntiles, overlap):
     """llc30: BASELINE config 5's 13-tile LLC topology (5 facets, rotated pkg/exch2 maps) at
-    n = 30.  overlap: the non-staggered configurations exchange the tracers' halo sources
-    while DYNAMICS, the solve and the continuity step run (parallel.ShardedModel.step); the
-    staggered cs32x15 keeps one exchange after the step."""
+    n = 30.  overlap (parallel.ShardedModel.step), non-staggered configurations: "thermo" runs
+    THERMODYNAMICS on the model's second stream as the resident step does (mgcm_step_phase
+    16), "halo" exchanges the tracers' halo sources while DYNAMICS, the solve and the
+    continuity step run; the staggered cs32x15 keeps one stream and one exchange."""
     import torch.multiprocessing as mp
     from mitgcm_amd.parallel import TilePartition
     ctx = mp.get_context("spawn")
@@ -103,8 +106,9 @@ def test_sharded_bit_identical(cfg, world, nsteps, ntiles, overlap):
         assert p.exitcode == 0
     r0 = out[0]
     assert "error" not in r0, r0["error"]
-    assert r0["overlap"] == (overlap and cfg != "cs32x15"), r0["overlap"]
-    print("%s sharded x%d (overlap %s) max |diff| vs 1 process:" % (cfg, world, r0["overlap"]), r0["diff"])
+    assert r0["overlap"] == (overlap == "halo" and cfg != "cs32x15"), r0["overlap"]
+    assert r0["fork"] == (overlap == "thermo" and cfg != "cs32x15"), r0["fork"]
+    print("%s sharded x%d (overlap %s) max |diff| vs 1 process:" % (cfg, world, overlap), r0["diff"])
     assert all(r0["equal"].values()), r0["diff"]
     for rank, r in out.items():
         assert r["stats"] == r0["ref_stats"], "rank %d: CG2D records differ" % rank

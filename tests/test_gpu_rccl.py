@@ -9,7 +9,9 @@ node runs the same calls with peers.  BASELINE config 4 (baroclinic gyre + DST3-
     iteration counts of the replicated solve, fields within 1e-10;
   * two steps captured into a HIP graph with their RCCL collectives (torch.cuda.graph on
     a side stream) and replayed: bit-identical to stepping eagerly; an eager step after
-    the replays (back on the collectives' stream) stays bit-identical."""
+    the replays (back on the collectives' stream) stays bit-identical;
+  * BASELINE config 5's LLC topology at n = 30 with the device multi-workgroup CG2D and
+    THERMODYNAMICS on the second stream, captured and replayed: bit-identical."""
 import os
 import socket
 
@@ -32,6 +34,12 @@ def _free_port():
 def _make():
     from mitgcm_amd import configs
     return configs.make_model(configs.baroclinic_gyre, tempAdvScheme=33)
+
+
+def _make_llc():
+    from mitgcm_amd import configs
+    return configs.make_model(lambda: (lambda r: (r[0], {**r[1], "cg2dForceMwg": 1}) + tuple(r[2:]))(
+        configs.llc_synthetic(n=30, Nr=10)))
 
 
 def _worker(port, q):
@@ -91,6 +99,23 @@ def _worker(port, q):
         torch.cuda.synchronize()
         res["eager_after_graph"] = {n: bool(np.array_equal(sm.gather_field(n), want6[n])) for n in FIELDS}
         m.close()
+        # BASELINE config 5's LLC topology (n = 30, 13 tiles): the device multi-workgroup CG2D
+        # (cg2d="device", its hand-off block exported by IPC), THERMODYNAMICS on the second
+        # stream beside the solve (overlap="thermo"), captured with the collectives and replayed
+        ref = _make_llc()
+        ref.forward_step(5)
+        ref.sync()
+        want_llc = {n: ref.get(n) for n in FIELDS}
+        ref.close()
+        m = _make_llc()
+        sm = ShardedModel(m, dist, cg2d="device")
+        res["llc_cg2d"] = sm.cg2d
+        res["llc_fork"] = sm.fork
+        sm.capture_step()
+        sm.replay(2)
+        torch.cuda.synchronize()
+        res["llc_graph"] = {n: bool(np.array_equal(sm.gather_field(n), want_llc[n])) for n in FIELDS}
+        m.close()
         dist.destroy_process_group()
         q.put(res)
     except Exception:
@@ -115,3 +140,5 @@ def test_rccl_world1_eager_distributed_and_graph():
     assert max(res["dist_diff"].values()) <= 1e-10, res["dist_diff"]
     assert all(res["graph"].values()), res["graph"]
     assert all(res["eager_after_graph"].values()), res["eager_after_graph"]
+    assert res["llc_cg2d"] == "device" and res["llc_fork"], res
+    assert all(res["llc_graph"].values()), res["llc_graph"]
