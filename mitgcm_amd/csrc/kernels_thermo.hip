@@ -34,6 +34,52 @@ __global__ void __launch_bounds__(256) k_oceanic_phys(Dims d, Params p, Fields f
   oceanic_phys_point(d, p, f, iterPtr, i, j, k, t);
 }
 
+// k_oceanic_phys with 16-byte accesses: a thread takes two consecutive points of a level's
+// full-halo plane (contiguous in memory: i fastest over the whole nx, then j), so every load
+// and store of levels k >= 2 is one double2 per lane instead of one double -- the stream
+// kernels' 8-B-lane rate (3.3-4.9 TB/s) against the 16-B copy rate (MI355X_MICROARCH.md).
+// Same per-point arithmetic (find_rho, the sigmaR / IVDC expressions of oceanic_phys_point);
+// the surface level keeps oceanic_phys_point itself (forcing, FREEZE_SURFACE).  Launched where
+// n2 is even and the fields are 16-B aligned (launch_oceanic_phys).
+__global__ void __launch_bounds__(256) k_oceanic_phys2(Dims d, Params p, Fields f, const int *iterPtr) {
+  const int h2 = (int)(d.n2 >> 1), nb = (h2 + 255) / 256, lb = mg_xcd_block();
+  const int z = lb / nb, pr = (lb % nb) * 256 + (int)threadIdx.x;
+  if (pr >= h2) return;
+  const int t = d.t0 + z / d.Nr, k = z % d.Nr + 1;
+  const long q2 = 2L * pr;   // 2-D offset inside the tile
+  if (k == 1) {
+#pragma unroll
+    for (int e = 0; e < 2; e++) {
+      const int ii = (int)((q2 + e) % d.nx) + 1 - d.OLx, jj = (int)((q2 + e) / d.nx) + 1 - d.OLy;
+      oceanic_phys_point(d, p, f, iterPtr, ii, jj, 1, t);
+    }
+    return;
+  }
+  const long q3 = (long)t * d.n3 + (long)(k - 1) * d.n2 + q2, q3u = q3 - d.n2;
+  typedef __attribute__((ext_vector_type(2))) double d2;
+  auto ld2 = [](const double *a, long q) { return *reinterpret_cast<const d2 *>(a + q); };
+  auto st2 = [](double *a, long q, double x, double y) { d2 v; v.x = x; v.y = y; *reinterpret_cast<d2 *>(a + q) = v; };
+  const d2 th = ld2(f.theta, q3), sa = ld2(f.salt, q3);
+  const bool calcConvect = p.ivdc_kappa != 0.0, sig = calcConvect || p.useGMRedi;
+  d2 thU = th, saU = sa, mC = th, mCu = th;
+  if (sig) { thU = ld2(f.theta, q3u); saU = ld2(f.salt, q3u); mC = ld2(f.maskC, q3); mCu = ld2(f.maskC, q3u); }
+  auto clampU = [&](double v) { return (k - 1 == 1 && p.allowFreezing && v < -1.9) ? -1.9 : v; };
+  double rho[2], conv[2] = {0.0, 0.0}, sigmaR[2] = {0.0, 0.0};
+#pragma unroll
+  for (int e = 0; e < 2; e++) {
+    const double tk = e ? th.y : th.x, sk = e ? sa.y : sa.x;
+    rho[e] = find_rho(p, f, k, q3 + e, tk, sk);
+    if (sig) {
+      const double rhoKm1 = find_rho(p, f, k, q3 + e, clampU(e ? thU.y : thU.x), e ? saU.y : saU.x);
+      sigmaR[e] = (e ? mC.y : mC.x) * (e ? mCu.y : mCu.x) * f.recip_drC[k - 1] * p.rkSign * (rho[e] - rhoKm1);
+      if (calcConvect) conv[e] = (-sigmaR[e] * p.gravitySign > 0.0) ? 1.0 : 0.0;
+    }
+  }
+  st2(f.rhoInSitu, q3, rho[0], rho[1]);
+  st2(f.IVDConvCount, q3, conv[0], conv[1]);
+  if (p.useGMRedi) st2(f.sigmaR, q3, sigmaR[0], sigmaR[1]);
+}
+
 // GMREDI_CALC_TENSOR (pkg/gmredi/gmredi_calc_tensor.F:231-790; skew flux, GM_ExtraDiag
 // = F, all isoFac/bolFac = 1) with GMREDI_SLOPE_LIMIT's gkw91 taper
 // (gmredi_slope_limit.F:280-370), one thread per (i,j,k) on i,j = 2-OL..sN+OL-1.
@@ -1066,8 +1112,17 @@ __global__ void __launch_bounds__(256) TRI_ATTR k_tracer_impl(Dims d, Params p, 
 
 // gm = false: without GMREDI_CALC_TENSOR (it then rides in the next launch, launch_dyn_thermo)
 hipError_t launch_oceanic_phys(const Dims &d, const Params &p, const Fields &f, const int *iterPtr, hipStream_t s, bool gm) {
-  hipLaunchKernelGGL(k_oceanic_phys, dim3(mg_plane_blocks(d.nx, d.ny, d.nT * d.Nr)), dim3(MG_PLANE_THREADS), 0, s, d, p,
-                     f, iterPtr);
+  auto al = [](const void *q) { return ((uintptr_t)q & 15u) == 0; };
+  static const int v2Env = getenv("MGCM_PHYS_V2") ? atoi(getenv("MGCM_PHYS_V2")) : 1;
+  const bool v2 = v2Env != 0 && (d.n2 & 1) == 0 && (d.n3 & 1) == 0 && al(f.theta) && al(f.salt) && al(f.maskC) &&
+                  al(f.rhoInSitu) && al(f.IVDConvCount) && (!p.useGMRedi || al(f.sigmaR)) &&
+                  (p.eosType != 1 || p.selectP_inEOS_Zc != 2 || al(f.totPhiHyd));
+  if (v2) {
+    const unsigned nb = (unsigned)(((d.n2 >> 1) + 255) / 256);
+    hipLaunchKernelGGL(k_oceanic_phys2, dim3(nb * (unsigned)(d.nT * d.Nr)), dim3(256), 0, s, d, p, f, iterPtr);
+  } else
+    hipLaunchKernelGGL(k_oceanic_phys, dim3(mg_plane_blocks(d.nx, d.ny, d.nT * d.Nr)), dim3(MG_PLANE_THREADS), 0, s, d, p,
+                       f, iterPtr);
   if (p.useGMRedi && gm)
     hipLaunchKernelGGL(k_gm_tensor, dim3(mg_plane_blocks(d.nx - 2, d.ny - 2, d.nT * d.Nr)), dim3(MG_PLANE_THREADS), 0,
                        s, d, p, f);
