@@ -1518,6 +1518,129 @@ __global__ void __launch_bounds__(256) k_corr_cont(Dims d, Params p, Fields f, i
   }
 }
 
+// k_corr_cont (atInit = 0, the step path) with 16-byte accesses: a thread slot owns two
+// adjacent columns (i, i+1), i odd, so every 3-D load and store of the level loop is one
+// double2 per lane (the 8-B-lane rate of the one-column form, 3.1 TB/s on LLC-90, against the
+// 16-B rate).  u at i+1 is the corrected u1 of column i and the u0 of column i+1: one
+// uCor, the same bits.  The LDS slices hold (column pair, level) as double2; the serial
+// column sums and the upward w recurrence run both columns in one thread, interleaved.
+// Same expressions in the same order as k_corr_cont: bit-identical.  Launched where sNx and
+// OLx are even and the fields 16-B aligned (launch_corr_cont).
+typedef __attribute__((ext_vector_type(2))) double dbl2;
+__global__ void __launch_bounds__(256) k_corr_cont2(Dims d, Params p, Fields f, int nc, const long *__restrict__ etaSrc) {
+  extern __shared__ __attribute__((aligned(16))) double lds[];
+  const int NC_ = nc, KW_ = 256 / NC_;
+  const int cc = (int)threadIdx.x % NC_, kk = (int)threadIdx.x / NC_;
+  const int hx = d.sNx >> 1;
+  const long pr_ = (long)mg_xcd_block() * NC_ + cc, npl = (long)hx * d.sNy;
+  const bool valid = pr_ < npl * d.nT;
+  const int t = d.t0 + (int)(valid ? pr_ / npl : 0);
+  const long rr = valid ? pr_ % npl : 0;
+  const int i = 1 + 2 * (int)(rr % hx), j = 1 + (int)(rr / hx);
+  const int NS = d.Nr * NC_;   // double2 slots per slice
+  dbl2 *sDiv = reinterpret_cast<dbl2 *>(lds), *sMask = sDiv + NS, *sU = sDiv + 2 * NS, *sV = sDiv + 3 * NS,
+       *sH0 = sDiv + 4 * NS;
+  auto ld2 = [](const double *a, long q) { return *reinterpret_cast<const dbl2 *>(a + q); };
+  const long q = MG_I2(d, i, j, t);
+  const bool rstar = p.nonlinFreeSurf > 0 && p.select_rStar != 0;
+  if (valid) {
+    const double psFac = p.pfFacMom * p.implicSurfPress;
+    auto eta = [&](long qq) {
+      if (!etaSrc) return f.etaN[qq];
+      const long sq = etaSrc[qq];
+      return f.recip_Bo[qq] * f.cg2d_x[sq >= 0 ? sq : qq];
+    };
+    auto phiX = [&](int ii, int jj) {
+      const long qq = MG_I2(d, ii, jj, t);
+      return f.recip_dxC[qq] * (f.Bo_surf[qq] * eta(qq) - f.Bo_surf[MG_I2(d, ii - 1, jj, t)] * eta(MG_I2(d, ii - 1, jj, t)));
+    };
+    auto phiY = [&](int ii, int jj) {
+      const long qq = MG_I2(d, ii, jj, t);
+      return f.recip_dyC[qq] * (f.Bo_surf[qq] * eta(qq) - f.Bo_surf[MG_I2(d, ii, jj - 1, t)] * eta(MG_I2(d, ii, jj - 1, t)));
+    };
+    // the pair's surface-pressure gradients: u at i, i+1, i+2; v at j, j+1 of both columns
+    const double pX0 = phiX(i, j), pX1 = phiX(i + 1, j), pX2 = phiX(i + 2, j);
+    const double pY0a = phiY(i, j), pY0b = phiY(i + 1, j), pY1a = phiY(i, j + 1), pY1b = phiY(i + 1, j + 1);
+    const double dyG0 = f.dyG[q], dyG1 = f.dyG[q + 1], dyG2 = f.dyG[q + 2];
+    const double dxG0a = f.dxG[q], dxG0b = f.dxG[q + 1], dxG1a = f.dxG[q + d.nx], dxG1b = f.dxG[q + d.nx + 1];
+    for (int k = kk + 1; k <= d.Nr; k += KW_) {
+      const int me = (k - 1) * NC_ + cc;
+      const long q3 = MG_I3(d, i, j, k, t), q3n = q3 + d.nx;
+      const dbl2 gU01 = ld2(f.gU, q3), gU23 = ld2(f.gU, q3 + 2), mW01 = ld2(f.maskW, q3), mW23 = ld2(f.maskW, q3 + 2);
+      const dbl2 gV0 = ld2(f.gV, q3), gV1 = ld2(f.gV, q3n), mS0 = ld2(f.maskS, q3), mS1 = ld2(f.maskS, q3n);
+      const dbl2 hW01 = ld2(f.hFacW, q3), hW23 = ld2(f.hFacW, q3 + 2), hS0 = ld2(f.hFacS, q3), hS1 = ld2(f.hFacS, q3n);
+      const dbl2 mC = ld2(f.maskC, q3);
+      auto cor = [&](double g, double m, double ps) { return (g + p.deltaTMom * (-psFac * ps * m)) * m; };
+      const double u0 = cor(gU01.x, mW01.x, pX0), u1 = cor(gU01.y, mW01.y, pX1), u2 = cor(gU23.x, mW23.x, pX2);
+      const double v0a = cor(gV0.x, mS0.x, pY0a), v0b = cor(gV0.y, mS0.y, pY0b);
+      const double v1a = cor(gV1.x, mS1.x, pY1a), v1b = cor(gV1.y, mS1.y, pY1b);
+      sU[me] = dbl2{u0, u1};
+      sV[me] = dbl2{v0a, v0b};
+      const double drF = f.drF[k - 1];
+      const double uT1a = u1 * dyG1 * drF * hW01.y, uT0a = u0 * dyG0 * drF * hW01.x;
+      const double vT1a = v1a * dxG1a * drF * hS1.x, vT0a = v0a * dxG0a * drF * hS0.x;
+      const double uT1b = u2 * dyG2 * drF * hW23.x, uT0b = u1 * dyG1 * drF * hW01.y;
+      const double vT1b = v1b * dxG1b * drF * hS1.y, vT0b = v0b * dxG0b * drF * hS0.y;
+      sDiv[me] = dbl2{uT1a - uT0a + vT1a - vT0a, uT1b - uT0b + vT1b - vT0b};
+      sMask[me] = mC;
+      if (rstar) sH0[me] = ld2(f.h0FacC, q3);
+    }
+  }
+  __syncthreads();
+  if (valid && kk == 0) {
+    double rStarDhDt[2] = {0.0, 0.0};
+    if (p.exactConserv) {
+      double hDiv[2] = {0.0, 0.0};
+      for (int k2 = 1; k2 <= d.Nr; k2++) {
+        const dbl2 m2 = sMask[(k2 - 1) * NC_ + cc], v2 = sDiv[(k2 - 1) * NC_ + cc];
+        hDiv[0] = hDiv[0] + m2.x * v2.x;
+        hDiv[1] = hDiv[1] + m2.y * v2.y;
+      }
+#pragma unroll
+      for (int e = 0; e < 2; e++) {
+        const long qe = q + e;
+        const double facEmP = p.useRealFreshWaterFlux ? 1.0 / p.rhoConst : 0.0;   // integr_continuity.F:183-188
+        const double dEtaHdt = -(hDiv[e] * f.recip_rA[qe]) - facEmP * f.EmPmR[qe];
+        f.cg2d_b[qe] = f.etaH[qe] + p.implicDiv2DFlow * dEtaHdt * p.deltaTFreeSurf;
+        if (f.dEtaHdt) f.dEtaHdt[qe] = dEtaHdt;
+        if (rstar) rStarDhDt[e] = dEtaHdt * f.recip_Rcol[qe];   // integr_continuity.F:171-183
+      }
+    }
+    double wBelow[2] = {0.0, 0.0};
+    const double rA1[2] = {f.recip_rA[q], f.recip_rA[q + 1]};
+    for (int k2 = d.Nr; k2 >= 1; k2--) {
+      const int s2 = (k2 - 1) * NC_ + cc;
+      const dbl2 dv = sDiv[s2], mk = sMask[s2];
+      const dbl2 h0 = rstar ? sH0[s2] : dbl2{0.0, 0.0};
+      double w[2];
+#pragma unroll
+      for (int e = 0; e < 2; e++) {
+        const double conv2d = -(e ? dv.y : dv.x), msk = e ? mk.y : mk.x;
+        if (rstar) {
+          const double dh = rStarDhDt[e] * f.drF[k2 - 1] * (e ? h0.y : h0.x);
+          if (k2 == d.Nr) w[e] = (conv2d * rA1[e] - dh) * msk;
+          else w[e] = (wBelow[e] + conv2d * rA1[e] - dh) * msk;
+        } else if (k2 == d.Nr) {
+          w[e] = conv2d * rA1[e] * msk;
+        } else {
+          w[e] = (wBelow[e] + conv2d * rA1[e]) * msk;
+        }
+        wBelow[e] = w[e];
+      }
+      sDiv[s2] = dbl2{w[0], w[1]};
+    }
+  }
+  __syncthreads();
+  if (valid)
+    for (int k = kk + 1; k <= d.Nr; k += KW_) {
+      const int me = (k - 1) * NC_ + cc;
+      const long q3 = MG_I3(d, i, j, k, t);
+      *reinterpret_cast<dbl2 *>(f.wVel + q3) = sDiv[me];
+      *reinterpret_cast<dbl2 *>(f.uVel + q3) = sU[me];
+      *reinterpret_cast<dbl2 *>(f.vVel + q3) = sV[me];
+    }
+}
+
 // Tile-sharded runs: gather (pack) / scatter (unpack) the halo-source points a peer
 // needs, for every exchanged field and level: buf[(f*Nr + k)*n + h] <-> field at 2-D
 // offset idx[h] (t*n2 + local) of level k.
@@ -1757,6 +1880,21 @@ hipError_t launch_corr_cont(const Dims &d, const Params &p, const Fields &f, int
   const int ncDef = d.Nr >= 30 ? 32 : 16;
   const int ncEnv = getenv("MGCM_CORR_NC") ? atoi(getenv("MGCM_CORR_NC")) : getenv("MGCM_COLF_NC") ? atoi(getenv("MGCM_COLF_NC")) : ncDef;
   const int nc = (ncEnv == 16 || ncEnv == 32 || ncEnv == 64) ? ncEnv : ncDef;
+  // the two-column form on the step path (atInit = 0) where pairs stay aligned: 16 column
+  // pairs per workgroup, the same LDS as 32 single columns.  Opt-in (MGCM_CORR2=1): bit-identical
+  // but slower on LLC-90, 151 against 137 us (profiles/r04/corr2/) -- the column frame is bound
+  // by its serial column sums and LDS round trips, not by the width of its loads
+  static const int c2Env = getenv("MGCM_CORR2") ? atoi(getenv("MGCM_CORR2")) : 0;
+  auto al = [](const void *q) { return ((uintptr_t)q & 15u) == 0; };
+  if (c2Env != 0 && atInit == 0 && (d.sNx & 1) == 0 && (d.OLx & 1) == 0 && (d.nx & 1) == 0 && (d.n3 & 1) == 0 &&
+      al(f.gU) && al(f.gV) && al(f.maskW) && al(f.maskS) && al(f.hFacW) && al(f.hFacS) && al(f.maskC) && al(f.uVel) &&
+      al(f.vVel) && al(f.wVel) && (nArr < 5 || al(f.h0FacC))) {
+    const int nc2 = 16;   // 32 columns x 16 level slots
+    MG_ALLOW_LDS(k_corr_cont2);
+    hipLaunchKernelGGL(k_corr_cont2, dim3(mg_colf_blocks(ncol / 2, nc2)), dim3(256), mg_colf_lds(d.Nr, 2 * nc2, nArr), s, d,
+                       p, f, nc2, etaSrc);
+    return hipGetLastError();
+  }
   MG_ALLOW_LDS(k_corr_cont);
   hipLaunchKernelGGL(k_corr_cont, dim3(mg_colf_blocks(ncol, nc)), dim3(256), mg_colf_lds(d.Nr, nc, nArr), s, d, p, f,
                      atInit, nc, etaSrc);
