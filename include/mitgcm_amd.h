@@ -227,6 +227,9 @@ int mgcm_cg2d_sum_plan(mgcm_model *m, int *plan, long capacity, int *NT, int *PP
  * mgcm_forward_step call. */
 int mgcm_solve_stats(mgcm_model *m, int back, double *firstResidual, double *lastResidual,
                      int *numIters, double *rhsMax);
+/* The same step's min-residual bookkeeping (cg2dUseMinResSol, cg2d.F:190-193, 338-347):
+ * minResidualSq and nIterMin (both -1 when the option is off). */
+int mgcm_solve_minres(mgcm_model *m, int back, double *minResidualSq, int *nIterMin);
 /* The same records for the last n steps of the last batch in one device-to-host copy,
  * oldest first (any output pointer may be NULL). */
 int mgcm_solve_history(mgcm_model *m, int n, int *numIters, double *firstResidual, double *lastResidual);

@@ -353,6 +353,7 @@ struct MwgTables {
   const int *impG;        // [G][IMAX] its 2-D offset
   const int *nImp;        // [G]
   int G, IMAX, SZ;        // parts, import capacity, LDS slots before the ZERO slot
+  int nExp;               // exported points (the xs granule pairs of one export buffer)
   int pinned;             // 1: only blockIdx.x % 8 == 0 work (all parts on one XCD)
   int sys;                // 1: the hand-off block is shared across processes (system scope)
   int partsPerTile;       // parts of tile t: t*partsPerTile .. (t+1)*partsPerTile - 1
@@ -363,7 +364,8 @@ struct MwgTables {
   unsigned *epoch;        // launch epoch of THIS process's launches (its own memory, never shared):
                           // read by its parts at their start, advanced by its first part at the end
   unsigned long long *part;   // [2 parities][3 values][G][2] workgroup partials
-  unsigned long long *xs;     // [exported points][2] q = M r of the points other parts' rings hold
+  unsigned long long *xs;     // [2 buffers][exported points][2] q = M r (CG2D_SR: r, q, v) of the points
+                              // other parts' rings hold (the standard solve uses buffer 0 only)
   size_t hsBytes;
 };
 

@@ -146,6 +146,7 @@ struct MwImport {
   size_t gi;       // first import slot of this part
   int nImp;
   double *imp_l;   // LDS staging, nImp doubles
+  const gu64 *src; // the export granules read (T.xs; CG2D_SR alternates two buffers)
 };
 
 template <int NV, bool MAXOP, bool SYS = false>
@@ -231,7 +232,7 @@ __device__ __forceinline__ bool mw_sync(double *v, const MwgTables &T, int g, in
     for (int q0 = 0; q0 < imp->nImp; q0 += MW_NT - 64) {
       const int qq = q0 + tid - 64;
       const bool act = qq < imp->nImp;
-      gu64 *src = (gu64 *)T.xs + (size_t)2 * (act ? T.impC[imp->gi + qq] : 0);
+      gu64 *src = (gu64 *)imp->src + (size_t)2 * (act ? T.impC[imp->gi + qq] : 0);
       double xv = 0.0;
       unsigned spins = 0;
       for (;;) {
@@ -269,7 +270,7 @@ __device__ __forceinline__ bool mw_sync(double *v, const MwgTables &T, int g, in
 // processes' launches on the same hand-off block)
 template <bool PINNED, bool SYS>
 __global__ void __launch_bounds__(MW_NT) k_cg2d_mwg(Dims d, Params p, Fields f, MwgTables T, int maxIters,
-                                                    SolveRecord *rec, int *stepCounter, int g0, int gN) {
+                                                    int nIterMinIn, SolveRecord *rec, int *stepCounter, int g0, int gN) {
   int g = (int)blockIdx.x;
   if (PINNED) {
     if (g % MG_NXCD) return;   // parts on XCD 0 only: their hand-offs stay in one L2
@@ -330,8 +331,19 @@ __global__ void __launch_bounds__(MW_NT) k_cg2d_mwg(Dims d, Params p, Fields f, 
     raC[m] = az * f.aC2d[gg];
     rb[m] = act ? f.cg2d_b[gg] : 0.0;
   }
+  // CG2D_SR forms y = M r on ring 1 too: the ring points' preconditioner rows
+  const bool SR = p.useSRCGSolver != 0;
+  double rpC[MW_RPT], rpW0[MW_RPT], rpW1[MW_RPT], rpS0[MW_RPT], rpS1[MW_RPT];
+#pragma unroll
+  for (int m = 0; m < MW_RPT; m++) {
+    const bool act = SR && RG[m] >= 0;
+    const long gg = act ? RG[m] : 0;
+    const double az = act ? 1.0 : 0.0;
+    rpC[m] = az * f.pC[gg]; rpW0[m] = az * f.pW[gg]; rpW1[m] = az * f.pW[gg + 1]; rpS0[m] = az * f.pS[gg];
+    rpS1[m] = az * f.pS[gg + nx];
+  }
   const int nImp = T.nImp[g];
-  const MwImport imp{gi, nImp, imp_l};
+  const MwImport imp{gi, nImp, imp_l, (const gu64 *)T.xs};
 #define LO(w) ((w) & 0xFFFFu)
 #define HI(w) ((w) >> 16)
 
@@ -349,6 +361,12 @@ __global__ void __launch_bounds__(MW_NT) k_cg2d_mwg(Dims d, Params p, Fields f, 
   }
 #pragma unroll
   for (int m = 0; m < MW_RPT; m++) rb[m] = (rb[m] * p.cg2dNorm) * (p.cg2dNormaliseRHS ? rhsNorm : 1.0);
+  // cgUseMinResSol (cg2d.F:148-155, 190-193, 338-347, 358-368): the lowest-residual solution,
+  // saved from the normalised first guess on (every part tests the same reduced err_sq)
+  const bool minRes = nIterMinIn >= 0;
+  double xmin[MW_OPT];
+#pragma unroll
+  for (int m = 0; m < MW_OPT; m++) xmin[m] = x[m];
   // EXCH_XY_RL(cg2d_x): x of owned points and of both rings into s_l (the ring values are read
   // from cg2d_x, written before this launch, and scaled with the owner's arithmetic)
 #pragma unroll
@@ -380,103 +398,253 @@ __global__ void __launch_bounds__(MW_NT) k_cg2d_mwg(Dims d, Params p, Fields f, 
 #pragma unroll
   for (int m = 0; m < MW_RPT; m++) r_l[NO + m * MW_NT + tid] = rr[m];
   __syncthreads();
-  // q = M r and (q, r) of iteration 1, reduced with err_sq and sumRHS; q exported for the
-  // parts whose rings hold these points; the ring copies of s start at s = 0 like the owners'
   gu64 *xs = (gu64 *)T.xs;
-#pragma unroll
-  for (int m = 0; m < MW_OPT; m++) {
-    q[m] = pC[m] * r[m] + pW0[m] * r_l[LO(nwe[m])] + pW1[m] * r_l[HI(nwe[m])] + pS0[m] * r_l[LO(nsn[m])] +
-           pS1[m] * r_l[HI(nsn[m])];
-    v3[2] = v3[2] + q[m] * r[m];
-    if ((exp >> m) & 1u) gran_put<SYS>(xs + (size_t)2 * T.ownC[go + m * MW_NT + tid], mw_tag(ep, nsync + 1), q[m]);
-  }
-  for (int qq = tid; qq < nImp; qq += MW_NT) s_l[NO + qq] = 0.0;
-  ok = ok && mw_sync<3, false, SYS>(v3, T, g, nsync, red, ep, &imp);
-  double err_sq = v3[0];
-  const double sumRHS = v3[1];
-  double eta_qrN = v3[2], eta_qrNM1 = 1.0;
-  const double firstResidual = sqrt(err_sq);
+  double err_sq, sumRHS, firstResidual;
   int actualIts = 0;
-  if (ok && !(err_sq < p.cg2dTolerance_sq)) {
-#ifdef MGCM_CG_STAMPS
-    unsigned long long stampAcc[6] = {0, 0, 0, 0, 0, 0}, stampPrev = 0;
-    const unsigned long long stampT0 = __builtin_amdgcn_s_memtime();
-    __builtin_amdgcn_s_waitcnt(0xC07F);
-#endif
-    for (int it2d = 1; it2d <= maxIters; it2d++) {
-      const double cgBeta = eta_qrN / eta_qrNM1;
-      eta_qrNM1 = eta_qrN;
-      // s = q + beta*s on the owned points and, with the q handed off at sync B, on both rings
-      // (EXCH_S3D_RL(cg2d_s)); the next export of q comes after sync D, when every part has
-      // read this one
+  int nIterMin = nIterMinIn;
+  double minResidualSq = -1.0;
+  if (SR) {
+    // CG2D_SR (cg2d_sr.F:100-440; the oracle's cg2d_sr): ONE grid hand-off per iteration.
+    // Each part keeps r and q on both rings as copies (r -= sigma*q, q = v + beta*q: the
+    // owner's expressions on the owner's bytes), forms y = M r on its points and ring 1 and
+    // v = A y on its points, and hands off v of its exported points with the three partials
+    // (y.r, y.v, r.r): the rings' v arrive with the sums.  The exports alternate between two
+    // buffers (a fast part exports for the next hand-off while a slow one still reads this one).
+    // The ring-2 r cannot be formed locally (it needs x on ring 3): it arrives with the first
+    // residual's sums.
+    gu64 *xsb[2] = {xs, xs + (size_t)2 * T.nExp};
+    double *qr_l = imp_l + T.IMAX;   // the rings' q (nImp)
+    auto exportv = [&](const double (&val)[MW_OPT]) {
+#pragma unroll
+      for (int m = 0; m < MW_OPT; m++)
+        if ((exp >> m) & 1u)
+          gran_put<SYS>(xsb[(nsync + 1) & 1] + (size_t)2 * T.ownC[go + m * MW_NT + tid], mw_tag(ep, nsync + 1), val[m]);
+    };
+    auto impOf = [&]() { return MwImport{gi, nImp, imp_l, (const gu64 *)xsb[(nsync + 1) & 1]}; };
+    exportv(r);
+    double v2[2] = {v3[0], v3[1]};
+    {
+      const MwImport ir = impOf();
+      ok = ok && mw_sync<2, false, SYS>(v2, T, g, nsync, red, ep, &ir);
+    }
+    err_sq = v2[0];
+    sumRHS = v2[1];
+    firstResidual = sqrt(err_sq);
+    if (minRes) { nIterMin = 0; minResidualSq = err_sq; }
+    for (int qq = tid; qq < nImp; qq += MW_NT) r_l[NO + qq] = imp_l[qq];
+    __syncthreads();
+    // y = M r on the owned points and ring 1, into s_l
+    double y[MW_OPT];
+    auto form_y = [&]() {
 #pragma unroll
       for (int m = 0; m < MW_OPT; m++) {
-        s[m] = q[m] + cgBeta * s[m];
-        s_l[m * MW_NT + tid] = s[m];
+        y[m] = pC[m] * r[m] + pW0[m] * r_l[LO(nwe[m])] + pW1[m] * r_l[HI(nwe[m])] + pS0[m] * r_l[LO(nsn[m])] +
+               pS1[m] * r_l[HI(nsn[m])];
+        s_l[m * MW_NT + tid] = y[m];
       }
-      MW_STAMP(0);
-      for (int qq = tid; qq < nImp; qq += MW_NT) s_l[NO + qq] = imp_l[qq] + cgBeta * s_l[NO + qq];
-      __syncthreads();
-      MW_STAMP(1);
-      // q = A s (owned + ring 1); alpha = eta_qrN / (s, A s)
-      double av[1] = {0.0};
-#pragma unroll
-      for (int m = 0; m < MW_OPT; m++) {
-        q[m] = aW0[m] * s_l[LO(nwe[m])] + aW1[m] * s_l[HI(nwe[m])] + aS0[m] * s_l[LO(nsn[m])] + aS1[m] * s_l[HI(nsn[m])] +
-               aC[m] * s[m];
-        av[0] = av[0] + s[m] * q[m];
-      }
-      double rq[MW_RPT];
 #pragma unroll
       for (int m = 0; m < MW_RPT; m++)
-        rq[m] = raW0[m] * s_l[LO(rwe[m])] + raW1[m] * s_l[HI(rwe[m])] + raS0[m] * s_l[LO(rsn[m])] +
-                raS1[m] * s_l[HI(rsn[m])] + raC[m] * s_l[NO + m * MW_NT + tid];
-      MW_STAMP(2);
-      ok = mw_sync<1, false, SYS>(av, T, g, nsync, red, ep);
-      MW_STAMP(3);
-      if (!ok) break;
-      const double alpha = eta_qrN / av[0];
-      // x += alpha s ; r -= alpha q (owned and ring 1); err_sq and the next (M r, r)
-      double v2[2] = {0.0, 0.0};
+        s_l[NO + m * MW_NT + tid] = rpC[m] * r_l[NO + m * MW_NT + tid] + rpW0[m] * r_l[LO(rwe[m])] +
+                                    rpW1[m] * r_l[HI(rwe[m])] + rpS0[m] * r_l[LO(rsn[m])] + rpS1[m] * r_l[HI(rsn[m])];
+    };
+    auto apply_A = [&](double (&out)[MW_OPT]) {   // A (s_l) on the owned points
+#pragma unroll
+      for (int m = 0; m < MW_OPT; m++)
+        out[m] = aW0[m] * s_l[LO(nwe[m])] + aW1[m] * s_l[HI(nwe[m])] + aS0[m] * s_l[LO(nsn[m])] +
+                 aS1[m] * s_l[HI(nsn[m])] + aC[m] * y[m];
+    };
+    int it2d = 0;
+    bool conv = false;
+    if (ok && !(err_sq < p.cg2dTolerance_sq)) {
+      // the standard first step (cg2d_sr.F:190-260): y = M r, s = y, eta = y.r, q = A s,
+      // alpha = s.q -- both sums in one hand-off, with the rings' q
+      form_y();
+      double ev[2] = {0.0, 0.0};
+#pragma unroll
+      for (int m = 0; m < MW_OPT; m++) { s[m] = y[m]; ev[0] = ev[0] + y[m] * r[m]; }
+      __syncthreads();
+      apply_A(q);
+#pragma unroll
+      for (int m = 0; m < MW_OPT; m++) ev[1] = ev[1] + s[m] * q[m];
+      exportv(q);
+      {
+        const MwImport iq = impOf();
+        ok = mw_sync<2, false, SYS>(ev, T, g, nsync, red, ep, &iq);
+      }
+      double eta_qrN = ev[0], eta_qrNM1 = eta_qrN, alpha = ev[1];
+      double sigma = eta_qrN / alpha;
 #pragma unroll
       for (int m = 0; m < MW_OPT; m++) {
-        x[m] = x[m] + alpha * s[m];
-        r[m] = r[m] - alpha * q[m];
-        v2[0] = v2[0] + r[m] * r[m];
+        x[m] = x[m] + sigma * s[m];
+        r[m] = r[m] - sigma * q[m];
         r_l[m * MW_NT + tid] = r[m];
       }
-#pragma unroll
-      for (int m = 0; m < MW_RPT; m++) {
-        rr[m] = rr[m] - alpha * rq[m];
-        r_l[NO + m * MW_NT + tid] = rr[m];
+      for (int qq = tid; qq < nImp; qq += MW_NT) {
+        qr_l[qq] = imp_l[qq];
+        r_l[NO + qq] = r_l[NO + qq] - sigma * qr_l[qq];
       }
-      actualIts = it2d;
       __syncthreads();
+      for (it2d = 1; ok && it2d <= maxIters - 1; it2d++) {   // cg2d_sr.F:262-370
+        form_y();
+        __syncthreads();
+        double v[MW_OPT];
+        apply_A(v);
+        double sv[3] = {0.0, 0.0, 0.0};
 #pragma unroll
-      for (int m = 0; m < MW_OPT; m++) {
-        q[m] = pC[m] * r[m] + pW0[m] * r_l[LO(nwe[m])] + pW1[m] * r_l[HI(nwe[m])] + pS0[m] * r_l[LO(nsn[m])] +
-               pS1[m] * r_l[HI(nsn[m])];
-        v2[1] = v2[1] + q[m] * r[m];
-        if ((exp >> m) & 1u) gran_put<SYS>(xs + (size_t)2 * T.ownC[go + m * MW_NT + tid], mw_tag(ep, nsync + 1), q[m]);
+        for (int m = 0; m < MW_OPT; m++) sv[0] = sv[0] + y[m] * r[m];
+#pragma unroll
+        for (int m = 0; m < MW_OPT; m++) sv[1] = sv[1] + y[m] * v[m];
+#pragma unroll
+        for (int m = 0; m < MW_OPT; m++) sv[2] = sv[2] + r[m] * r[m];
+        exportv(v);
+        {
+          const MwImport iv = impOf();
+          ok = mw_sync<3, false, SYS>(sv, T, g, nsync, red, ep, &iv);
+        }
+        if (!ok) break;
+        eta_qrN = sv[0];
+        const double delta = sv[1];
+        err_sq = sv[2];
+        if (err_sq < p.cg2dTolerance_sq) { conv = true; break; }
+        if (minRes && err_sq < minResidualSq) {
+          minResidualSq = err_sq;
+          nIterMin = it2d;
+#pragma unroll
+          for (int m = 0; m < MW_OPT; m++) xmin[m] = x[m];
+        }
+        const double cgBeta = eta_qrN / eta_qrNM1;
+        eta_qrNM1 = eta_qrN;
+        alpha = delta - (cgBeta * cgBeta) * alpha;
+        sigma = eta_qrN / alpha;
+#pragma unroll
+        for (int m = 0; m < MW_OPT; m++) {
+          s[m] = y[m] + cgBeta * s[m];
+          x[m] = x[m] + sigma * s[m];
+          q[m] = v[m] + cgBeta * q[m];
+          r[m] = r[m] - sigma * q[m];
+          r_l[m * MW_NT + tid] = r[m];
+        }
+        for (int qq = tid; qq < nImp; qq += MW_NT) {
+          const double qn = imp_l[qq] + cgBeta * qr_l[qq];
+          qr_l[qq] = qn;
+          r_l[NO + qq] = r_l[NO + qq] - sigma * qn;
+        }
+        __syncthreads();
       }
-      MW_STAMP(4);
-      ok = mw_sync<2, false, SYS>(v2, T, g, nsync, red, ep, &imp);
-      MW_STAMP(5);
-      if (!ok) break;
-      err_sq = v2[0];
-      eta_qrN = v2[1];
-      if (err_sq < p.cg2dTolerance_sq) break;
+      if (ok && !conv) {   // cg2d_sr.F:372-382: the residual of the last update
+        double e1[1] = {0.0};
+#pragma unroll
+        for (int m = 0; m < MW_OPT; m++) e1[0] = e1[0] + r[m] * r[m];
+        ok = mw_sync<1, false, SYS>(e1, T, g, nsync, red, ep);
+        err_sq = e1[0];
+      }
     }
-#ifdef MGCM_CG_STAMPS
-    if (g == 0 && threadIdx.x == 0)
-      printf("MWSTAMP G %d its %d total %llu | import %llu applyA %llu syncD %llu upd+applyM %llu syncB %llu\n", T.G,
-             actualIts, __builtin_amdgcn_s_memtime() - stampT0, stampAcc[0], stampAcc[1], stampAcc[2], stampAcc[3],
-             stampAcc[4]);
-#endif
+    actualIts = it2d;   // cg2d_sr.F:410: the loop index at exit
+  } else {
+    // q = M r and (q, r) of iteration 1, reduced with err_sq and sumRHS; q exported for the
+    // parts whose rings hold these points; the ring copies of s start at s = 0 like the owners'
+  #pragma unroll
+    for (int m = 0; m < MW_OPT; m++) {
+      q[m] = pC[m] * r[m] + pW0[m] * r_l[LO(nwe[m])] + pW1[m] * r_l[HI(nwe[m])] + pS0[m] * r_l[LO(nsn[m])] +
+             pS1[m] * r_l[HI(nsn[m])];
+      v3[2] = v3[2] + q[m] * r[m];
+      if ((exp >> m) & 1u) gran_put<SYS>(xs + (size_t)2 * T.ownC[go + m * MW_NT + tid], mw_tag(ep, nsync + 1), q[m]);
+    }
+    for (int qq = tid; qq < nImp; qq += MW_NT) s_l[NO + qq] = 0.0;
+    ok = ok && mw_sync<3, false, SYS>(v3, T, g, nsync, red, ep, &imp);
+    err_sq = v3[0];
+    sumRHS = v3[1];
+    double eta_qrN = v3[2], eta_qrNM1 = 1.0;
+    firstResidual = sqrt(err_sq);
+    if (minRes) { nIterMin = 0; minResidualSq = err_sq; }
+    if (ok && !(err_sq < p.cg2dTolerance_sq)) {
+  #ifdef MGCM_CG_STAMPS
+      unsigned long long stampAcc[6] = {0, 0, 0, 0, 0, 0}, stampPrev = 0;
+      const unsigned long long stampT0 = __builtin_amdgcn_s_memtime();
+      __builtin_amdgcn_s_waitcnt(0xC07F);
+  #endif
+      for (int it2d = 1; it2d <= maxIters; it2d++) {
+        const double cgBeta = eta_qrN / eta_qrNM1;
+        eta_qrNM1 = eta_qrN;
+        // s = q + beta*s on the owned points and, with the q handed off at sync B, on both rings
+        // (EXCH_S3D_RL(cg2d_s)); the next export of q comes after sync D, when every part has
+        // read this one
+  #pragma unroll
+        for (int m = 0; m < MW_OPT; m++) {
+          s[m] = q[m] + cgBeta * s[m];
+          s_l[m * MW_NT + tid] = s[m];
+        }
+        MW_STAMP(0);
+        for (int qq = tid; qq < nImp; qq += MW_NT) s_l[NO + qq] = imp_l[qq] + cgBeta * s_l[NO + qq];
+        __syncthreads();
+        MW_STAMP(1);
+        // q = A s (owned + ring 1); alpha = eta_qrN / (s, A s)
+        double av[1] = {0.0};
+  #pragma unroll
+        for (int m = 0; m < MW_OPT; m++) {
+          q[m] = aW0[m] * s_l[LO(nwe[m])] + aW1[m] * s_l[HI(nwe[m])] + aS0[m] * s_l[LO(nsn[m])] + aS1[m] * s_l[HI(nsn[m])] +
+                 aC[m] * s[m];
+          av[0] = av[0] + s[m] * q[m];
+        }
+        double rq[MW_RPT];
+  #pragma unroll
+        for (int m = 0; m < MW_RPT; m++)
+          rq[m] = raW0[m] * s_l[LO(rwe[m])] + raW1[m] * s_l[HI(rwe[m])] + raS0[m] * s_l[LO(rsn[m])] +
+                  raS1[m] * s_l[HI(rsn[m])] + raC[m] * s_l[NO + m * MW_NT + tid];
+        MW_STAMP(2);
+        ok = mw_sync<1, false, SYS>(av, T, g, nsync, red, ep);
+        MW_STAMP(3);
+        if (!ok) break;
+        const double alpha = eta_qrN / av[0];
+        // x += alpha s ; r -= alpha q (owned and ring 1); err_sq and the next (M r, r)
+        double v2[2] = {0.0, 0.0};
+  #pragma unroll
+        for (int m = 0; m < MW_OPT; m++) {
+          x[m] = x[m] + alpha * s[m];
+          r[m] = r[m] - alpha * q[m];
+          v2[0] = v2[0] + r[m] * r[m];
+          r_l[m * MW_NT + tid] = r[m];
+        }
+  #pragma unroll
+        for (int m = 0; m < MW_RPT; m++) {
+          rr[m] = rr[m] - alpha * rq[m];
+          r_l[NO + m * MW_NT + tid] = rr[m];
+        }
+        actualIts = it2d;
+        __syncthreads();
+  #pragma unroll
+        for (int m = 0; m < MW_OPT; m++) {
+          q[m] = pC[m] * r[m] + pW0[m] * r_l[LO(nwe[m])] + pW1[m] * r_l[HI(nwe[m])] + pS0[m] * r_l[LO(nsn[m])] +
+                 pS1[m] * r_l[HI(nsn[m])];
+          v2[1] = v2[1] + q[m] * r[m];
+          if ((exp >> m) & 1u) gran_put<SYS>(xs + (size_t)2 * T.ownC[go + m * MW_NT + tid], mw_tag(ep, nsync + 1), q[m]);
+        }
+        MW_STAMP(4);
+        ok = mw_sync<2, false, SYS>(v2, T, g, nsync, red, ep, &imp);
+        MW_STAMP(5);
+        if (!ok) break;
+        err_sq = v2[0];
+        eta_qrN = v2[1];
+        if (err_sq < p.cg2dTolerance_sq) break;
+        if (minRes && err_sq < minResidualSq) {
+          minResidualSq = err_sq;
+          nIterMin = it2d;
+  #pragma unroll
+          for (int m = 0; m < MW_OPT; m++) xmin[m] = x[m];
+        }
+      }
+  #ifdef MGCM_CG_STAMPS
+      if (g == 0 && threadIdx.x == 0)
+        printf("MWSTAMP G %d its %d total %llu | import %llu applyA %llu syncD %llu upd+applyM %llu syncB %llu\n", T.G,
+               actualIts, __builtin_amdgcn_s_memtime() - stampT0, stampAcc[0], stampAcc[1], stampAcc[2], stampAcc[3],
+               stampAcc[4]);
+  #endif
+    }
   }
+  const bool useMin = minRes && err_sq > minResidualSq;
 #pragma unroll
   for (int m = 0; m < MW_OPT; m++) {
-    double xv = x[m];
+    double xv = useMin ? xmin[m] : x[m];
     if (p.cg2dNormaliseRHS) xv = xv / rhsNorm;
     if (G2[m] >= 0) f.cg2d_x[G2[m]] = xv;
   }
@@ -487,12 +655,12 @@ __global__ void __launch_bounds__(MW_NT) k_cg2d_mwg(Dims d, Params p, Fields f, 
     SolveRecord &R = rec[st];
     R.firstResidual = firstResidual;
     R.lastResidual = sqrt(err_sq);
-    R.minResidualSq = -1.0;
+    R.minResidualSq = minResidualSq;
     R.rhsMax = rhsMax;
     R.sumRHS = sumRHS;
     const bool tmo = __hip_atomic_load((gu32 *)T.ctr + 1, RLX_SCOPE(SYS)) == ep + 1u;
     R.numIters = (ok && !tmo) ? actualIts : -1;   // -1: a grid hand-off timed out
-    R.nIterMin = -1;
+    R.nIterMin = nIterMin;
     // the next launch's epoch; after a timeout it skips one, so a part of this launch that
     // starts late (reading ep + 1, tagging with it, failing into the timeout word as ep + 2)
     // can neither match the next launch's tags nor fail it
@@ -505,13 +673,13 @@ __global__ void __launch_bounds__(MW_NT) k_cg2d_mwg(Dims d, Params p, Fields f, 
 int cg2d_mwg_geometry(int *nt, int *opt, int *rpt) { *nt = MW_NT; *opt = MW_OPT; *rpt = MW_RPT; return 0; }
 
 hipError_t launch_cg2d_mwg(const Dims &d, const Params &p, const Fields &f, const MwgTables &T, int maxIters,
-                           SolveRecord *rec, int *stepCounter, hipStream_t s, int g0, int gN) {
+                           int nIterMin, SolveRecord *rec, int *stepCounter, hipStream_t s, int g0, int gN) {
   // phases per launch: 2 + 2 per iteration, below 2^16 (the tag's phase field)
   if (maxIters < 0 || maxIters > 30000) return hipErrorInvalidValue;
   if (gN < 0) { g0 = 0; gN = T.G; }
   if (g0 < 0 || gN < 1 || g0 + gN > T.G) return hipErrorInvalidValue;
   hipError_t e = hipSuccess;
-  size_t lds = (size_t)(2 * (T.SZ + 1) + 16 * 16 + T.IMAX) * sizeof(double);
+  size_t lds = (size_t)(2 * (T.SZ + 1) + 16 * 16 + (p.useSRCGSolver ? 2 : 1) * T.IMAX) * sizeof(double);
   // a part may claim its CU's whole LDS so that no other kernel's workgroup shares the CU
   // (THERMODYNAMICS running beside the solve, model.hip one_step): MGCM_MWG_EXCL=1|0
   const char *ex = getenv("MGCM_MWG_EXCL");
@@ -527,7 +695,7 @@ hipError_t launch_cg2d_mwg(const Dims &d, const Params &p, const Fields &f, cons
     attrSet[v] = true;
   }
   const unsigned grid = (unsigned)(pinned ? gN * MG_NXCD : gN);
-  hipLaunchKernelGGL(kern, dim3(grid), dim3(MW_NT), lds, s, d, p, f, T, maxIters, rec, stepCounter, g0, gN);
+  hipLaunchKernelGGL(kern, dim3(grid), dim3(MW_NT), lds, s, d, p, f, T, maxIters, nIterMin, rec, stepCounter, g0, gN);
   return hipGetLastError();
 }
 

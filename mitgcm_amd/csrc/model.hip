@@ -78,7 +78,7 @@ hipError_t launch_tracer_pair(const Dims &, const Params &, const Fields &, cons
                               const int *, hipStream_t);
 hipError_t launch_mon_stats(const Dims &, const MonSpecs &, int, double *, int, hipStream_t);
 int cg2d_mwg_geometry(int *, int *, int *);
-hipError_t launch_cg2d_mwg(const Dims &, const Params &, const Fields &, const MwgTables &, int, SolveRecord *, int *,
+hipError_t launch_cg2d_mwg(const Dims &, const Params &, const Fields &, const MwgTables &, int, int, SolveRecord *, int *,
                            hipStream_t, int g0 = 0, int gN = -1);
 }  // namespace mgcm
 
@@ -707,7 +707,7 @@ static int build_mwg(mgcm_model *m) {
       mwg_upload(m, ownExp, &T.ownExp) || mwg_upload(m, ringG, &T.ringG) || mwg_upload(m, ringNb, &T.ringNb) ||
       mwg_upload(m, impC, &T.impC) || mwg_upload(m, impG, &T.impG) || mwg_upload(m, nImp, &T.nImp))
     return -1;
-  T.G = G; T.IMAX = IMAX; T.SZ = SZ;
+  T.G = G; T.IMAX = IMAX; T.SZ = SZ; T.nExp = nExp;
   T.pinned = (G <= 32 && !getenv("MGCM_CG2D_SPREAD")) ? 1 : 0;
   T.sys = 0;
   T.exclusive = 0;
@@ -715,7 +715,7 @@ static int build_mwg(mgcm_model *m) {
   // hand-off block: 64 B of words (launch epoch, timeout word), the partial granules, the
   // export granules; zeroed once here -- granule tags carry the launch epoch, so a launch
   // never matches an earlier launch's granules (a multiple of 16 B from the start)
-  const size_t partGr = (size_t)2 * 3 * G * 2, hs = 64 + (partGr + (size_t)nExp * 2) * sizeof(unsigned long long);
+  const size_t partGr = (size_t)2 * 3 * G * 2, hs = 64 + (partGr + (size_t)nExp * 4) * sizeof(unsigned long long);
   char *blk = nullptr;
   HIPCHK(hipMalloc(&blk, hs));
   HIPCHK(hipMemset(blk, 0, hs));
@@ -1193,10 +1193,10 @@ int mgcm_init(mgcm_model *m) {
     m->nBlkX = 0;
     m->nBlk = 0;
     if (build_mwg(m)) return -1;
-    if (m->p.cg2dUseMinResSol) return set_err("mgcm_init: cg2dUseMinResSol with the multi-workgroup CG2D not implemented");
   }
-  if (m->p.useSRCGSolver && (m->useMwg || m->nBlkX == 0))
-    return set_err("mgcm_init: useSRCGSolver (CG2D_SR) is implemented in the blocked single-workgroup CG2D only");
+  if (m->p.useSRCGSolver && !m->useMwg && m->nBlkX == 0)
+    return set_err("mgcm_init: useSRCGSolver (CG2D_SR) is implemented in the blocked single-workgroup and the "
+                   "multi-workgroup CG2D only");
   if ((m->p.viscA4D != 0.0 || m->p.viscA4Z != 0.0) && (m->d.OLx < 3 || m->d.OLy < 3))
     return set_err("mgcm_init: biharmonic viscosity needs OLx, OLy >= 3 (del2u of the halo ring)");
   const bool rstar = m->p.nonlinFreeSurf > 0;
@@ -1297,8 +1297,7 @@ static hipError_t launch_cg2d(mgcm_model *m, int maxIters, int nIterMin, bool fu
     return launch_cg2d_block(m->d, m->p, m->f, m->d_nbr, m->d_gofs, m->nPts, maxIters, nIterMin, m->d_rec, m->d_ctr + 1,
                              m->stream);
   if (m->useMwg) {
-    if (nIterMin >= 0) return hipErrorInvalidValue;   // no min-residual solution in the multi-workgroup solver
-    return launch_cg2d_mwg(m->d, m->p, m->f, m->mwg, maxIters, m->d_rec, m->d_ctr + 1, m->stream);
+    return launch_cg2d_mwg(m->d, m->p, m->f, m->mwg, maxIters, nIterMin, m->d_rec, m->d_ctr + 1, m->stream);
   }
   if (m->nBlkX > 0)
     return launch_cg2d_bxy(m->bxyVar, m->d, m->p, m->f, m->d_nbx, m->d_blkx, m->nBlkX, maxIters, nIterMin, m->d_rec,
@@ -2088,7 +2087,7 @@ int mgcm_step_phase(mgcm_model *m, int phase) {
         return set_err("mgcm_step_phase(10): needs the multi-workgroup CG2D on whole-domain tables (cg2dForceMwg)");
       if (m->d.nT < m->d.nTiles && !m->mwg.sys)
         return set_err("mgcm_step_phase(10): a tile subset needs the shared hand-off block (mgcm_cg2d_shared_*)");
-      TIMED(K_CG2D, launch_cg2d_mwg(m->d, m->p, m->f, m->mwg, m->p.cg2dMaxIters, m->d_rec, m->d_ctr + 1, m->stream,
+      TIMED(K_CG2D, launch_cg2d_mwg(m->d, m->p, m->f, m->mwg, m->p.cg2dMaxIters, m->p.cg2dUseMinResSol - 1, m->d_rec, m->d_ctr + 1, m->stream,
                                     m->d.t0 * m->mwg.partsPerTile, m->d.nT * m->mwg.partsPerTile));
       return 0;
     case 6:   // phase 2 after a CG2D driven by the caller (mgcm_cg2d_op: distributed CG2D)
@@ -2174,7 +2173,7 @@ int mgcm_cg2d_tiles(mgcm_model *m, int t0, int nT) {
   if (nT < m->d.nTiles && !m->mwg.sys)
     return set_err("mgcm_cg2d_tiles: a tile subset needs the shared hand-off block (mgcm_cg2d_share)");
   HIPCHK(hipSetDevice(m->device));
-  TIMED(K_CG2D, launch_cg2d_mwg(m->d, m->p, m->f, m->mwg, m->p.cg2dMaxIters, m->d_rec, m->d_ctr + 1, m->stream,
+  TIMED(K_CG2D, launch_cg2d_mwg(m->d, m->p, m->f, m->mwg, m->p.cg2dMaxIters, m->p.cg2dUseMinResSol - 1, m->d_rec, m->d_ctr + 1, m->stream,
                                 t0 * m->mwg.partsPerTile, nT * m->mwg.partsPerTile));
   return 0;
 }
@@ -2284,6 +2283,20 @@ int mgcm_solve_stats(mgcm_model *m, int back, double *firstResidual, double *las
   if (lastResidual) *lastResidual = r.lastResidual;
   if (numIters) *numIters = r.numIters;
   if (rhsMax) *rhsMax = r.rhsMax;
+  return 0;
+}
+
+// The min-residual bookkeeping of a step's solve (cg2dUseMinResSol): the lowest squared
+// residual reached and its iteration (cg2d.F minResidualSq, nIterMin; -1 / -1 when off).
+int mgcm_solve_minres(mgcm_model *m, int back, double *minResidualSq, int *nIterMin) {
+  HIPCHK(hipStreamSynchronize(m->stream));
+  int slot = m->lastBatch - 1 - back;
+  if (m->lastBatch == 0) slot = 0;
+  if (slot < 0) return set_err("mgcm_solve_minres: no such step");
+  SolveRecord r;
+  HIPCHK(hipMemcpy(&r, m->d_rec + slot, sizeof r, hipMemcpyDeviceToHost));
+  if (minResidualSq) *minResidualSq = r.minResidualSq;
+  if (nIterMin) *nIterMin = r.nIterMin;
   return 0;
 }
 

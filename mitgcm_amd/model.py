@@ -162,6 +162,12 @@ class Model:
         return {"cg2d_init_res": f.value, "cg2d_last_res": la.value, "cg2d_iters": it.value,
                 "cg2d_rhs_max": rm.value}
 
+    def solve_minres(self, back=0):
+        """cg2dUseMinResSol's record of a step's solve: (minResidualSq, nIterMin), -1 when off."""
+        r, n = ctypes.c_double(), ctypes.c_int()
+        check(lib().mgcm_solve_minres(self.h, back, ctypes.byref(r), ctypes.byref(n)), "mgcm_solve_minres")
+        return r.value, n.value
+
     def solve_history(self, n):
         """numIters, firstResidual, lastResidual of the last n steps (oldest first), one copy."""
         it = np.zeros(n, dtype=np.int32)

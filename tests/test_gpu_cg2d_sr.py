@@ -2,6 +2,9 @@
 useSRCGSolver): the single-reduction conjugate gradient in k_cg2d_bxy<..., SR> on BASELINE
 config 2 (global_ocean.90x40x15) with useSRCGSolver = 1.
 
+The multi-workgroup solver runs it too (kernels_cg2d_mwg.hip, one grid hand-off per
+iteration): config 3 on the cube below, config 2 in tests/test_gpu_cg2d_mwg.py.
+
 Bars: 10 steps against the oracle's CG2D_SR summing in the device's order
 (mgcm_cg2d_sum_plan -> oracle_set_sum_plan): iteration counts, residuals and the state arrays
 identical, bit for bit; against the oracle's CG2D_SR in the reference's order: the same
@@ -53,7 +56,29 @@ def test_ocean90_cg2d_sr_10_steps():
     assert worst[0] >= 10.0, worst
 
 
-def test_cg2d_sr_refused_on_the_multi_workgroup_solver():
+def test_cs32x15_cg2d_sr_multi_workgroup():
+    """CG2D_SR in the multi-workgroup solver on the cube (BASELINE config 3: 6 faces, EXCH2
+    maps, parts pinned to one XCD): one grid hand-off per iteration; 4 steps bit-identical to
+    the oracle's CG2D_SR summing in the device's order (iterations, residuals, every dynstat
+    value)."""
     from mitgcm_amd import configs
-    with pytest.raises(Exception, match="useSRCGSolver"):
-        configs.make_model(configs.global_ocean_cs32x15, params_over=OVER)
+    from mitgcm_amd.model import dynstat
+    from oracle.harness import cs32x15_oracle
+    m = configs.make_model(configs.global_ocean_cs32x15, params_over=OVER)
+    assert m.cg2d_kernel() == "mwg"
+    od, g = cs32x15_oracle(params_over=OVER)
+    plan, NT, PPT, NG = m.cg2d_sum_plan()
+    od.set_sum_plan(plan, NT, PPT, NG, fma=m.cg2d_fma())
+    its = []
+    for step in range(1, 5):
+        m.forward_step(1)
+        od.forward_step()
+        md = m.solve_stats()
+        md.update(dynstat(m))
+        sd = od.dynstat()
+        its.append(md["cg2d_iters"])
+        for k, v in md.items():
+            if k in sd:
+                assert v == sd[k], ("device-order oracle", step, k, v, sd[k])
+    m.close()
+    print("cs32x15 CG2D_SR on the multi-workgroup solver: iterations %s, bit for bit" % its)
