@@ -264,7 +264,7 @@ inline unsigned mg_colf_blocks(long ncols, int nc) { return (unsigned)((ncols + 
 // second stream beside them (kernels_step.hip; early fork only, small grids), MG_FUSE_ETAX
 // no separate EXCH(cg2d_x) + etaN under exactConserv (one_step).
 enum { MG_FUSE_SFP = 1, MG_FUSE_ETA = 2, MG_FUSE_PHI = 4, MG_FUSE_END = 8, MG_FUSE_PHYS = 16, MG_FUSE_ETAA = 32,
-       MG_FUSE_TREX = 64, MG_FUSE_DT = 128, MG_FUSE_ETAX = 256 };
+       MG_FUSE_TREX = 64, MG_FUSE_DT = 128, MG_FUSE_ETAX = 256, MG_FUSE_TCG = 512 };
 inline bool mg_fuse_on(int bit) {
   // read per call (tests switch it per model)
   const int mask = getenv("MGCM_STEP_FUSE") ? atoi(getenv("MGCM_STEP_FUSE"))

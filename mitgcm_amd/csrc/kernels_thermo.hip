@@ -1111,6 +1111,42 @@ __global__ void __launch_bounds__(256) TRI_ATTR k_tracer_impl(Dims d, Params p, 
 }
 
 // gm = false: without GMREDI_CALC_TENSOR (it then rides in the next launch, launch_dyn_thermo)
+// GMREDI_CALC_TENSOR alone (THERMODYNAMICS' first launch when it runs on its own stream)
+hipError_t launch_gm_tensor(const Dims &d, const Params &p, const Fields &f, hipStream_t s) {
+  if (!p.useGMRedi) return hipSuccess;
+  hipLaunchKernelGGL(k_gm_tensor, dim3(mg_plane_blocks(d.nx - 2, d.ny - 2, d.nT * d.Nr)), dim3(MG_PLANE_THREADS), 0, s, d,
+                     p, f);
+  return hipGetLastError();
+}
+
+// The hFac THERMODYNAMICS reads, copied before UPDATE_R_STAR(.TRUE.) rewrites them (one_step's
+// MG_FUSE_TCG layout): hFacC, hFacW, hFacS and their reciprocals into snap[6 x N3all]; the
+// tracer kernels then get the Fields with those six pointers moved to the copy.
+struct Snap6 {
+  const double *src[6];
+  double *dst[6];
+};
+__global__ void __launch_bounds__(256) k_hfac_snapshot(Snap6 sn, long n) {
+  const long q = (long)blockIdx.x * 256 + threadIdx.x;
+  if (q >= n) return;
+  const int a = (int)blockIdx.y;
+  sn.dst[a][q] = sn.src[a][q];
+}
+Fields hfac_snapshot_fields(const Dims &d, const Fields &f, double *snap) {
+  Fields g = f;
+  g.hFacC = snap; g.hFacW = snap + d.N3all; g.hFacS = snap + 2 * d.N3all;
+  g.recip_hFacC = snap + 3 * d.N3all; g.recip_hFacW = snap + 4 * d.N3all; g.recip_hFacS = snap + 5 * d.N3all;
+  return g;
+}
+hipError_t launch_hfac_snapshot(const Dims &d, const Fields &f, double *snap, hipStream_t s) {
+  const Fields g = hfac_snapshot_fields(d, f, snap);
+  Snap6 sn{{f.hFacC, f.hFacW, f.hFacS, f.recip_hFacC, f.recip_hFacW, f.recip_hFacS},
+           {g.hFacC, g.hFacW, g.hFacS, g.recip_hFacC, g.recip_hFacW, g.recip_hFacS}};
+  const long n = d.N3all;
+  hipLaunchKernelGGL(k_hfac_snapshot, dim3((unsigned)((n + 255) / 256), 6), dim3(256), 0, s, sn, n);
+  return hipGetLastError();
+}
+
 hipError_t launch_oceanic_phys(const Dims &d, const Params &p, const Fields &f, const int *iterPtr, hipStream_t s, bool gm) {
   auto al = [](const void *q) { return ((uintptr_t)q & 15u) == 0; };
   static const int v2Env = getenv("MGCM_PHYS_V2") ? atoi(getenv("MGCM_PHYS_V2")) : 1;

@@ -69,6 +69,9 @@ bool dyn_thermo_fusable(const Dims &, const Params &, const TracerArgs &, const 
 hipError_t launch_dyn_thermo(const Dims &, const Params &, const Fields &, const TracerArgs &, const TracerArgs &, const int *,
                              hipStream_t);
 bool dyn_thermo_takes_gm(const Params &);
+hipError_t launch_gm_tensor(const Dims &, const Params &, const Fields &, hipStream_t);
+hipError_t launch_hfac_snapshot(const Dims &, const Fields &, double *, hipStream_t);
+Fields hfac_snapshot_fields(const Dims &, const Fields &, double *);
 bool gm_phi_fusable(const Dims &, const Params &);
 hipError_t launch_gm_phi(const Dims &, const Params &, const Fields &, hipStream_t);
 bool tracer_hpair_ok(const Dims &, const Params &, const TracerArgs &, const TracerArgs &);
@@ -169,6 +172,8 @@ struct mgcm_model {
   // DO_OCEANIC_PHYS, join before UPDATE_R_STAR / SOLVE_FOR_PRESSURE; MGCM_NO_OVERLAP=1 off)
   hipStream_t stream2 = nullptr;
   hipEvent_t evFork = nullptr, evJoin = nullptr;
+  hipEvent_t evSnap = nullptr;   // the hFac snapshot of THERMODYNAMICS beside the solve under r* (MG_FUSE_TCG)
+  double *snapH = nullptr;        // hFacC, hFacW, hFacS, recip_hFacC, recip_hFacW, recip_hFacS (6 x N3all)
   hipStream_t stream3 = nullptr;                  // EXCH(cg2d_x) + etaN beside the correction step
   hipEvent_t evEta0 = nullptr, evEta1 = nullptr;
   hipEvent_t evHand = nullptr;   // mgcm_stream_handoff
@@ -797,6 +802,7 @@ mgcm_model *mgcm_create(int sNx, int sNy, int OLx, int OLy, int Nr, int nSx, int
       hipEventCreateWithFlags(&m->evEta0, hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&m->evEta1, hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&m->evJoin, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&m->evSnap, hipEventDisableTiming) != hipSuccess ||
       hipEventCreate(&m->ovlEv[0]) != hipSuccess || hipEventCreate(&m->ovlEv[1]) != hipSuccess) {
     set_err("mgcm_create: second stream / events");
     delete m;
@@ -891,6 +897,7 @@ void mgcm_destroy(mgcm_model *m) {
   if (m->ownStream) hipStreamDestroy(m->ownStream);
   if (m->stream2) hipStreamDestroy(m->stream2);
   if (m->evFork) hipEventDestroy(m->evFork);
+  if (m->evSnap) hipEventDestroy(m->evSnap);
   if (m->evHand) hipEventDestroy(m->evHand);
   if (m->stream3) hipStreamDestroy(m->stream3);
   if (m->evEta0) hipEventDestroy(m->evEta0);
@@ -1172,6 +1179,11 @@ static hipError_t update_r_star_cg2d(mgcm_model *m, bool sfp = false) {
 int mgcm_init(mgcm_model *m) {
   auto ext = [&](const char *n, double dflt) { auto it = m->extra.find(n); return it == m->extra.end() ? dflt : it->second; };
   HIPCHK(hipSetDevice(m->device));
+  // the hFac snapshot THERMODYNAMICS reads beside the pressure solve under r* (one_step)
+  if (!m->snapH && m->p.nonlinFreeSurf > 0 && m->p.select_rStar > 0 && (m->p.tempStepping || m->p.saltStepping)) {
+    HIPCHK(hipMalloc(&m->snapH, 6 * (size_t)m->d.N3all * sizeof(double)));
+    m->allocs.push_back(m->snapH);
+  }
   if (upload_halo(m)) return -1;
   if (build_nbr(m)) return -1;
   // CG2D kernel: the single-workgroup blocked solvers on lat-lon grids that tile into their
@@ -1351,34 +1363,35 @@ static TracerArgs tracer_args(mgcm_model *m, bool salt) {
 }
 
 // TEMP_INTEGRATE / SALT_INTEGRATE on stream `st` (the theta/salt ping-pong swap is host-side)
-static int tracers_on(mgcm_model *m, hipStream_t st) {
+static int tracers_on(mgcm_model *m, hipStream_t st, const Fields *fo = nullptr) {
   const TracerArgs aT = tracer_args(m, false), aS = tracer_args(m, true);
+  const Fields &F = fo ? *fo : m->f;   // the fields the kernels read (fo: the hFac snapshot)
   if (tracer_pair_ok(m->d, m->p, aT, aS)) {   // both tracers in one pair of launches
-    TIMED(K_TEMP, launch_tracer_pair(m->d, m->p, m->f, aT, aS, m->d_ctr, st));
+    TIMED(K_TEMP, launch_tracer_pair(m->d, m->p, F, aT, aS, m->d_ctr, st));
     std::swap(m->f.theta, m->f.thetaNext);
     std::swap(m->f.salt, m->f.saltNext);
     return 0;
   }
   if (tracer_hpair_ok(m->d, m->p, aT, aS)) {   // small grids: both tracers per launch
-    TIMED(K_TEMP, launch_tracer_hpair(m->d, m->p, m->f, aT, aS, m->d_ctr, st));
+    TIMED(K_TEMP, launch_tracer_hpair(m->d, m->p, F, aT, aS, m->d_ctr, st));
     std::swap(m->f.theta, m->f.thetaNext);
     std::swap(m->f.salt, m->f.saltNext);
     return 0;
   }
-  if (tracer_impl2_ok(m->p, m->f, aT, aS)) {   // two right-hand sides, one paired implicit solve
-    TIMED(K_TEMP, launch_tracer_step(m->d, m->p, m->f, aT, m->d_ctr, st, false));
-    TIMED(K_TEMP, launch_tracer_step(m->d, m->p, m->f, aS, m->d_ctr, st, false));
-    TIMED(K_TEMP, launch_tracer2_impl(m->d, m->p, m->f, aT, aS, st));
+  if (tracer_impl2_ok(m->p, F, aT, aS)) {   // two right-hand sides, one paired implicit solve
+    TIMED(K_TEMP, launch_tracer_step(m->d, m->p, F, aT, m->d_ctr, st, false));
+    TIMED(K_TEMP, launch_tracer_step(m->d, m->p, F, aS, m->d_ctr, st, false));
+    TIMED(K_TEMP, launch_tracer2_impl(m->d, m->p, F, aT, aS, st));
     std::swap(m->f.theta, m->f.thetaNext);
     std::swap(m->f.salt, m->f.saltNext);
     return 0;
   }
   if (m->p.tempStepping) {
-    TIMED(K_TEMP, launch_tracer_step(m->d, m->p, m->f, tracer_args(m, false), m->d_ctr, st));
+    TIMED(K_TEMP, launch_tracer_step(m->d, m->p, F, tracer_args(m, false), m->d_ctr, st));
     std::swap(m->f.theta, m->f.thetaNext);   // CYCLE_TRACER: the new theta is the other buffer
   }
   if (m->p.saltStepping) {
-    TIMED(K_TEMP, launch_tracer_step(m->d, m->p, m->f, tracer_args(m, true), m->d_ctr, st));
+    TIMED(K_TEMP, launch_tracer_step(m->d, m->p, F, tracer_args(m, true), m->d_ctr, st));
     std::swap(m->f.salt, m->f.saltNext);
   }
   return 0;
@@ -1578,8 +1591,30 @@ static int one_step(mgcm_model *m) {
   // (decided without the timing switch: one stream, so the eager timed pass runs the layout
   // the graph replays -- bench.py's per-kernel times and PMC attribution then describe it)
   const bool forkable = !stagger && m->overlap && m->p.momStepping && tracers;
-  const bool dtFused = forkable && m->p.nonlinFreeSurf > 0 && !tracer_pair_ok(m->d, m->p, aT, aS) &&
+  // THERMODYNAMICS beside the pressure solve under r* too (MG_FUSE_TCG): UPDATE_R_STAR(.TRUE.)
+  // rewrites the hFac it reads before the solve, so it reads a copy taken on its own stream
+  // right after the fork -- the hFac of the step's start, the values FORWARD_STEP's order
+  // gives it.  DYNAMICS runs alone (no fold), UPDATE_R_STAR waits only for the copy, the
+  // correction step for the tracers.  Opt-in (MGCM_STEP_FUSE |= 512): bit-identical, but on
+  // config 2 the fold into DYNAMICS' launches stays faster, 0.2885 against 0.307 ms/step
+  // (profiles/r04/tcg/): the tracers' launches beside DYNAMICS cost more than the 190 us
+  // single-CU solve they could hide behind
+  const bool tcg = forkable && m->p.nonlinFreeSurf > 0 && m->p.select_rStar > 0 && m->snapH &&
+                   mg_fuse_on(MG_FUSE_TCG) && !tracer_pair_ok(m->d, m->p, aT, aS);
+  const bool tcgFork = tcg && fork;
+  const bool dtFused = forkable && !tcg && m->p.nonlinFreeSurf > 0 && !tracer_pair_ok(m->d, m->p, aT, aS) &&
                        dyn_thermo_fusable(m->d, m->p, aT, aS);
+  auto fork_tcg = [&]() -> int {
+    HIPCHK(hipEventRecord(m->evFork, m->stream));
+    HIPCHK(hipStreamWaitEvent(m->stream2, m->evFork, 0));
+    HIPCHK(launch_hfac_snapshot(m->d, m->f, m->snapH, m->stream2));
+    HIPCHK(hipEventRecord(m->evSnap, m->stream2));
+    HIPCHK(launch_gm_tensor(m->d, m->p, m->f, m->stream2));
+    const Fields fT = hfac_snapshot_fields(m->d, m->f, m->snapH);
+    if (tracers_on(m, m->stream2, &fT)) return -1;
+    HIPCHK(hipEventRecord(m->evJoin, m->stream2));
+    return 0;
+  };
   // the multi-workgroup CG2D keeps its CUs to itself while the tracers run beside it
   m->mwg.exclusive = thermoLate ? 1 : 0;
   // DO_OCEANIC_PHYS + DYNAMICS' CALC_PHI_HYD in one column pass where exact (phys_phi_fusable:
@@ -1588,7 +1623,7 @@ static int one_step(mgcm_model *m) {
   const bool physPhi = !stagger && m->p.momStepping && phys_phi_fusable(m->d, m->p);
   // (the graph's layout: the eager timed pass, one stream, serialises a fork it reports here)
   m->stepLayout = (dtFused ? 1 : 0) | (physPhi ? 2 : 0) | (forkable && !dtFused ? 4 : 0) |
-                  (forkable && m->p.nonlinFreeSurf <= 0 ? 8 : 0);
+                  ((forkable && m->p.nonlinFreeSurf <= 0) || tcg ? 8 : 0);
   // GMREDI_CALC_TENSOR beside CALC_PHI_HYD (launch_gm_phi) where THERMODYNAMICS, its reader,
   // runs after DYNAMICS (staggered, or forked after DYNAMICS) and the fold does not apply
   const bool gmPhi = (stagger || thermoLate) && !dtFused && !physPhi && !m->timing && gm_phi_fusable(m->d, m->p);
@@ -1596,12 +1631,14 @@ static int one_step(mgcm_model *m) {
     if (physPhi) TIMED(K_PHYS, launch_phys_phi(m->d, m->p, m->f, m->d_ctr, m->stream));
     // (GMREDI_CALC_TENSOR in launch_dyn_thermo's first grid when it takes it)
     else TIMED(K_PHYS, launch_oceanic_phys(m->d, m->p, m->f, m->d_ctr, m->stream,
-                                           !(dtFused && dyn_thermo_takes_gm(m->p)) && !gmPhi));
+                                           !(dtFused && dyn_thermo_takes_gm(m->p)) && !gmPhi && !tcgFork));
     return 0;
   };
   if (stagger || fork || dtFused) {
     if (phys()) return -1;
-    if (fork && !thermoLate && !dtFused && fork_thermo()) return -1;
+    if (tcgFork) {
+      if (fork_tcg()) return -1;
+    } else if (fork && !thermoLate && !dtFused && fork_thermo()) return -1;
   } else {
     if (phys() || tracers_on(m, m->stream)) return -1;
   }
@@ -1616,7 +1653,8 @@ static int one_step(mgcm_model *m) {
       TIMED(K_MOM, launch_mom_step(m->d, m->p, m->f, m->d_ctr, m->stream));
     } else if (mgcm_dynamics(m)) return -1;
     if (thermoLate && thermoAtEnv == 1 && fork_thermo()) return -1;
-    if (fork && !lateJoin && !dtFused) HIPCHK(hipStreamWaitEvent(m->stream, m->evJoin, 0));
+    if (tcgFork) HIPCHK(hipStreamWaitEvent(m->stream, m->evSnap, 0));   // the copy before hFac is rewritten
+    else if (fork && !lateJoin && !dtFused) HIPCHK(hipStreamWaitEvent(m->stream, m->evJoin, 0));
     // forward_step.F:829-877: UPDATE_R_STAR(.TRUE.) + UPDATE_CG2D
     // (launch fusions, common.h MGCM_STEP_FUSE: CALC_DIV_GHAT in the r* column pass;
     // EXCH(cg2d_x) + etaN in the single-workgroup CG2D's epilogue -- off by default: one CU
@@ -1650,7 +1688,7 @@ static int one_step(mgcm_model *m) {
     } else if (!etaFused) {
       TIMED(K_ETA, launch_exch_eta(m->d, m->p, m->f, m->d_srcOf, false, 0, m->stream));
     }
-    if (lateJoin) HIPCHK(hipStreamWaitEvent(m->stream, m->evJoin, 0));
+    if (lateJoin || tcgFork) HIPCHK(hipStreamWaitEvent(m->stream, m->evJoin, 0));
     TIMED(K_CONT, launch_corr_cont(m->d, m->p, m->f, 0, m->stream, (etaAside || etaX) ? m->d_srcOf : nullptr));
     if (etaAside) HIPCHK(hipStreamWaitEvent(m->stream, m->evEta1, 0));
     // forward_step.F:965-977: CALC_R_STAR(etaH(n+1)); the next step's RESET_NLFS_VARS +
