@@ -204,6 +204,31 @@ def default_pmc_summary(config):
     return os.path.join(ROOT, "profiles", "r04", tag, "pmc_summary.json")
 
 
+def stream_triad_gbs(device, n=64 << 20, reps=8):
+    """SURVEY.md 8(d)'s roofline denominator measured on the box: a STREAM triad
+    a = b + s*c over three fp64 arrays of n doubles (512 MB each at the default), best of
+    `reps`, in GB/s (24 bytes per element).  torch's elementwise kernel, run after the timed
+    region -- a reference rate for the fractions, not part of the product."""
+    import torch
+    dev = torch.device("cuda", device)
+    b = torch.rand(n, dtype=torch.float64, device=dev)
+    c = torch.rand(n, dtype=torch.float64, device=dev)
+    a = torch.empty_like(b)
+    torch.add(b, c, alpha=3.0, out=a)
+    torch.cuda.synchronize(dev)
+    best = float("inf")
+    for _ in range(reps):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        torch.add(b, c, alpha=3.0, out=a)
+        e1.record()
+        torch.cuda.synchronize(dev)
+        best = min(best, e0.elapsed_time(e1) * 1e-3)
+    del a, b, c
+    torch.cuda.empty_cache()
+    return 24.0 * n / best / 1e9
+
+
 def cg_kernel_key(m):
     return "k_cg2d_" + m.cg2d_kernel().replace("_ref", "")
 
@@ -428,6 +453,14 @@ def main():
                          "traffic": mom_traffic,
                          "traffic_per_kernel": {k.split("(")[0]: v for k, v in mom_traffic_per.items()}},
     }
+    # the measured STREAM triad of this box beside the 8 TB/s spec
+    try:
+        triad = stream_triad_gbs(local)
+        out["roofline_hbm"]["stream_triad_gbs"] = triad
+        out["roofline_hbm"]["frac_of_triad"] = mom_gbs / triad
+    except Exception as e:   # a reference number only: its absence does not fail the bench
+        out["roofline_hbm"]["stream_triad_gbs"] = None
+        print("bench: stream triad not measured: %s" % e, file=sys.stderr)
     if rank == 0 and world == 1 and not a.no_cpu_baseline:   # the CPU baseline is an N=1 line
         out["cpu_baseline"] = cpu_baseline(a.config, a.cpu_seconds)
     if rank == 0:

@@ -318,6 +318,63 @@ template <bool RS, bool QH>
 __global__ void __launch_bounds__(256) k_phi_flat(Dims d, Params p, Fields f) {
   phi_flat_body<RS, QH>(d, p, f, mg_xcd_block());
 }
+// phi_flat_body<false, false> with 16-byte accesses: a thread takes two adjacent columns
+// (i, i+1) with i + OLx even, so each level's rhoInSitu load and phiHydC / totPhiHyd store is one
+// double2 per lane; the pairs cover i = -1 .. sNx+2 and the columns outside the reference's
+// 0..sNx+1 are computed but not stored.  Each column's recurrence is phi_flat_body's, the two
+// chains interleaved: bit-identical.  Launched where OLx is even and nx even (launch_phi_hyd).
+__global__ void __launch_bounds__(256) k_phi_flat2(Dims d, Params p, Fields f) {
+  const int hp = (d.sNx + 4) / 2, H = d.sNy + 2;   // pairs per row: i = -1 .. sNx+2
+  const long pr = (long)mg_xcd_block() * 256 + threadIdx.x, npl = (long)hp * H;
+  if (pr >= npl * d.nT) return;
+  const int t = d.t0 + (int)(pr / npl), r = (int)(pr % npl);
+  const int i = -1 + 2 * (r % hp), j = r / hp;   // columns i, i+1 of row j (0..sNy+1)
+  const int Nr = d.Nr;
+  const bool in0 = i >= 0, in1 = i + 1 <= d.sNx + 1;   // stored columns
+  const double recip_rhoConst = 1.0 / p.rhoConst;
+  const long q2 = MG_I2(d, i, j, t);
+  const bool tot = p.storePhiHyd4Phys != 0;
+  double bEta[2] = {0.0, 0.0};
+  if (tot) { bEta[0] = f.Bo_surf[q2] * f.etaN[q2]; bEta[1] = f.Bo_surf[q2 + 1] * f.etaN[q2 + 1]; }
+  typedef __attribute__((ext_vector_type(2))) double d2;
+  double phF[2] = {0.0, 0.0};
+  for (int k0 = 1; k0 <= Nr; k0 += PHI_CH) {
+    d2 a[PHI_CH];
+#pragma unroll
+    for (int cc = 0; cc < PHI_CH; cc++) {
+      const int k = k0 + cc <= Nr ? k0 + cc : Nr;
+      a[cc] = *reinterpret_cast<const d2 *>(f.rhoInSitu + MG_I3(d, i, j, k, t));
+    }
+#pragma unroll
+    for (int cc = 0; cc < PHI_CH; cc++) {
+      const int k = k0 + cc;
+      if (k > Nr) continue;
+      const long q3 = MG_I3(d, i, j, k, t);
+      double dRlocM = 0.5 * f.drC[k - 1];
+      if (k == 1) dRlocM = f.rF[0] - f.rC[0];
+      const double dRlocP = (k == Nr) ? (f.rC[k - 1] - f.rF[k]) : 0.5 * f.drC[k];
+      double phC[2];
+#pragma unroll
+      for (int e = 0; e < 2; e++) {
+        const double al = e ? a[cc].y : a[cc].x;
+        const double sM = dRlocM * p.gravity * al * recip_rhoConst;
+        const double sP = dRlocP * p.gravity * al * recip_rhoConst;
+        phC[e] = phF[e] + sM;
+        phF[e] = phC[e] + sP;
+      }
+      if (in0 && in1) {
+        d2 v; v.x = phC[0]; v.y = phC[1];
+        *reinterpret_cast<d2 *>(f.phiHydC + q3) = v;
+        if (tot) { d2 w; w.x = phC[0] + bEta[0] + 0.0; w.y = phC[1] + bEta[1] + 0.0; *reinterpret_cast<d2 *>(f.totPhiHyd + q3) = w; }
+      } else {
+        const int e = in0 ? 0 : 1;
+        f.phiHydC[q3 + e] = phC[e];
+        if (tot) f.totPhiHyd[q3 + e] = phC[e] + bEta[e] + 0.0;
+      }
+    }
+  }
+}
+
 // whether CALC_PHI_HYD runs the flat pass: by default where neither r* nor the QH terms add
 // their per-level operands (LLC-90: 63 -> 30 us; with them, on the small r* grids, the one
 // serial thread per column is slower than the column frame: config 2 0.319 against 0.309
@@ -2373,6 +2430,14 @@ hipError_t launch_phi_hyd(const Dims &d, const Params &p, const Fields &f, hipSt
   // the flat per-column form (phi_flat_on)
   if (phi_flat_on(p)) {
     const bool qh = p.quasiHydrostatic && (p.select3dCoriScheme >= 1 || p.useNHMTerms);
+    auto al = [](const void *q) { return ((uintptr_t)q & 15u) == 0; };
+    const int v2Env = getenv("MGCM_PHI_V2") ? atoi(getenv("MGCM_PHI_V2")) : 1;
+    if (!rstar && !qh && v2Env != 0 && (d.OLx & 1) == 0 && (d.nx & 1) == 0 && (d.n3 & 1) == 0 && al(f.rhoInSitu) &&
+        al(f.phiHydC) && al(f.totPhiHyd)) {
+      const long np = (long)((d.sNx + 4) / 2) * (d.sNy + 2) * d.nT;
+      hipLaunchKernelGGL(k_phi_flat2, dim3((unsigned)((np + 255) / 256)), dim3(256), 0, s, d, p, f);
+      return hipGetLastError();
+    }
     auto kern = rstar ? (qh ? k_phi_flat<true, true> : k_phi_flat<true, false>)
                       : (qh ? k_phi_flat<false, true> : k_phi_flat<false, false>);
     hipLaunchKernelGGL(kern, dim3((unsigned)phi_flat_blocks(d, p)), dim3(256), 0, s, d, p, f);

@@ -1884,7 +1884,7 @@ hipError_t launch_corr_cont(const Dims &d, const Params &p, const Fields &f, int
   // pairs per workgroup, the same LDS as 32 single columns.  Opt-in (MGCM_CORR2=1): bit-identical
   // but slower on LLC-90, 151 against 137 us (profiles/r04/corr2/) -- the column frame is bound
   // by its serial column sums and LDS round trips, not by the width of its loads
-  static const int c2Env = getenv("MGCM_CORR2") ? atoi(getenv("MGCM_CORR2")) : 0;
+  const int c2Env = getenv("MGCM_CORR2") ? atoi(getenv("MGCM_CORR2")) : 0;
   auto al = [](const void *q) { return ((uintptr_t)q & 15u) == 0; };
   if (c2Env != 0 && atInit == 0 && (d.sNx & 1) == 0 && (d.OLx & 1) == 0 && (d.nx & 1) == 0 && (d.n3 & 1) == 0 &&
       al(f.gU) && al(f.gV) && al(f.maskW) && al(f.maskS) && al(f.hFacW) && al(f.hFacS) && al(f.maskC) && al(f.uVel) &&

@@ -791,6 +791,71 @@ __global__ void __launch_bounds__(256) TRM_ATTR k_tracer_march(Dims d, Params p,
   }
 }
 
+// k_tracer_march with 16-byte accesses: a thread marches two adjacent columns (i, i+1), i odd
+// (with OLx even the pair starts 16-B aligned), so the level's loads of the column pair are
+// double2 per lane -- T, T(j-1), T(j+1), v(j), v(j+1), hFacS(j), hFacS(j+1), w, maskC,
+// IVDConvCount, recip_hFacC, the AB history, the stores of T* and the history -- and only
+// T(i-1), T(i+2), u(i+2), hFacW(i+2) are single doubles.  A workgroup covers whole rows of
+// the tile (sNx/2 pairs x 256/(sNx/2) rows), so a wave reads contiguous row segments.  Each
+// column's arithmetic is tracer_flat_arith on its own operands: bit-identical.
+typedef __attribute__((ext_vector_type(2))) double trd2;
+__global__ void __launch_bounds__(256) TRM_ATTR k_tracer_march2(Dims d, Params p, Fields f, TracerArgs a, const int *iterPtr,
+                                                                int KC, int nkc, int nty) {
+  int b = mg_xcd_block();
+  const int kc = b % nkc;
+  b /= nkc;
+  const int hx = d.sNx >> 1, TY = 256 / hx;
+  const int ty = b % nty, t = d.t0 + b / nty;
+  const int px = (int)threadIdx.x % hx, jy = (int)threadIdx.x / hx;
+  if (jy >= TY) return;
+  const int i = 1 + 2 * px, j = 1 + ty * TY + jy;
+  if (j > d.sNy) return;
+  const int Nr = d.Nr, k0 = 1 + kc * KC, k1 = min(Nr, k0 + KC - 1);
+  const int myIter = *iterPtr;
+  const long nx = d.nx, n2 = d.n2, q = MG_I2(d, i, j, t);
+  const double *__restrict__ T = a.tr;
+  auto L2 = [](const double *x, long o) { return *reinterpret_cast<const trd2 *>(x + o); };
+  TrCol c[2];
+  tracer_load_col(d, f, a, q, c[0]);
+  tracer_load_col(d, f, a, q + 1, c[1]);
+  long q3 = MG_I3(d, i, j, k0, t);
+  const long qu = k0 > 1 ? q3 - n2 : q3;
+  trd2 Tu = L2(T, qu), mCu = L2(f.maskC, qu);
+  trd2 T0 = L2(T, q3), mC0 = L2(f.maskC, q3), w0 = L2(f.wVel, q3), ivd0 = L2(f.IVDConvCount, q3);
+  for (int k = k0; k <= k1; k++, q3 += n2) {
+    const long qd = k < Nr ? q3 + n2 : q3;
+    const trd2 Td = L2(T, qd), mCd = L2(f.maskC, qd), w1 = L2(f.wVel, qd), ivd1 = L2(f.IVDConvCount, qd);
+    const trd2 Ts = L2(T, q3 - nx), Tn = L2(T, q3 + nx);
+    const double Tw = T[q3 - 1], Te = T[q3 + 2];
+    const trd2 u01 = L2(f.uVel, q3), v0 = L2(f.vVel, q3), v1 = L2(f.vVel, q3 + nx);
+    const double u2 = f.uVel[q3 + 2], hW2 = f.hFacW[q3 + 2];
+    const trd2 hW01 = L2(f.hFacW, q3), hS0 = L2(f.hFacS, q3), hS1 = L2(f.hFacS, q3 + nx);
+    const trd2 rhC = L2(f.recip_hFacC, q3);
+    const trd2 gA = a.multiDim ? L2(f.gAdv, q3) : trd2{0.0, 0.0};
+    const trd2 gO = a.useAB ? L2(a.gNm1, q3) : trd2{0.0, 0.0};
+    double v[2], gN[2] = {0.0, 0.0};
+#pragma unroll
+    for (int e = 0; e < 2; e++) {
+      TrLev o;
+      o.T0 = e ? T0.y : T0.x; o.Tu = e ? Tu.y : Tu.x; o.Td = e ? Td.y : Td.x;
+      o.Tw = e ? T0.x : Tw; o.Te = e ? Te : T0.y;
+      o.Ts = e ? Ts.y : Ts.x; o.Tn = e ? Tn.y : Tn.x;
+      o.u0 = e ? u01.y : u01.x; o.u1 = e ? u2 : u01.y;
+      o.v0 = e ? v0.y : v0.x; o.v1 = e ? v1.y : v1.x;
+      o.w0 = e ? w0.y : w0.x; o.w1 = e ? w1.y : w1.x;
+      o.hW0 = e ? hW01.y : hW01.x; o.hW1 = e ? hW2 : hW01.y;
+      o.hS0 = e ? hS0.y : hS0.x; o.hS1 = e ? hS1.y : hS1.x;
+      o.mCu = e ? mCu.y : mCu.x; o.mC0 = e ? mC0.y : mC0.x; o.mCd = e ? mCd.y : mCd.x;
+      o.ivd0 = e ? ivd0.y : ivd0.x; o.ivd1 = e ? ivd1.y : ivd1.x;
+      o.rhC = e ? rhC.y : rhC.x; o.gAdv = e ? gA.y : gA.x; o.gOld = e ? gO.y : gO.x;
+      v[e] = tracer_flat_arith(p, f, a, Nr, k, myIter, c[e], o, &gN[e]);
+    }
+    if (a.useAB) *reinterpret_cast<trd2 *>(a.gNm1 + q3) = trd2{gN[0], gN[1]};
+    *reinterpret_cast<trd2 *>((p.implicitDiffusion ? a.scr : a.trNext) + q3) = trd2{v[0], v[1]};
+    Tu = T0; T0 = Td; mCu = mC0; mC0 = mCd; w0 = w1; ivd0 = ivd1;
+  }
+}
+
 // TEMP_INTEGRATE and SALT_INTEGRATE together (both stepped, no GM/Redi, no multi-dimensional
 // advection: LLC-90's C2 tracers): the k-march of k_tracer_march over the two tracers at
 // once, so the operands they share -- u, v, w, hFacW/S, maskC, IVDConvCount, recip_hFacC and
@@ -1149,7 +1214,7 @@ hipError_t launch_hfac_snapshot(const Dims &d, const Fields &f, double *snap, hi
 
 hipError_t launch_oceanic_phys(const Dims &d, const Params &p, const Fields &f, const int *iterPtr, hipStream_t s, bool gm) {
   auto al = [](const void *q) { return ((uintptr_t)q & 15u) == 0; };
-  static const int v2Env = getenv("MGCM_PHYS_V2") ? atoi(getenv("MGCM_PHYS_V2")) : 1;
+  const int v2Env = getenv("MGCM_PHYS_V2") ? atoi(getenv("MGCM_PHYS_V2")) : 1;
   const bool v2 = v2Env != 0 && (d.n2 & 1) == 0 && (d.n3 & 1) == 0 && al(f.theta) && al(f.salt) && al(f.maskC) &&
                   al(f.rhoInSitu) && al(f.IVDConvCount) && (!p.useGMRedi || al(f.sigmaR)) &&
                   (p.eosType != 1 || p.selectP_inEOS_Zc != 2 || al(f.totPhiHyd));
@@ -1271,8 +1336,17 @@ hipError_t launch_tracer_step(const Dims &d, const Params &p, const Fields &f, c
     const int kcEnv = getenv("MGCM_TR_KC") ? atoi(getenv("MGCM_TR_KC")) : 0;
     const int KC = kcEnv > 0 ? (kcEnv > d.Nr ? d.Nr : kcEnv) : (d.Nr + 4) / 5;
     const int nkc = (d.Nr + KC - 1) / KC, ntx = (d.sNx + TRM_TX - 1) / TRM_TX, nty = (d.sNy + TRM_TY - 1) / TRM_TY;
-    hipLaunchKernelGGL(k_tracer_march, dim3((unsigned)(nkc * ntx * nty * d.nT)), blk, 0, s, d, p, f, a, iterPtr, KC, nkc,
-                       ntx, nty);
+    auto al = [](const void *x) { return ((uintptr_t)x & 15u) == 0; };
+    const int m2Env = getenv("MGCM_TRACER_MARCH2") ? atoi(getenv("MGCM_TRACER_MARCH2")) : 1;
+    const int hx = d.sNx / 2;
+    if (m2Env != 0 && (d.sNx & 1) == 0 && (d.OLx & 1) == 0 && (d.nx & 1) == 0 && (d.n3 & 1) == 0 && hx <= 256 && al(a.tr) &&
+        al(a.trNext) && al(a.scr) && al(a.gNm1) && al(f.maskC) && al(f.wVel) && al(f.IVDConvCount) && al(f.uVel) &&
+        al(f.vVel) && al(f.hFacW) && al(f.hFacS) && al(f.recip_hFacC) && (!a.multiDim || al(f.gAdv))) {
+      const int TY = 256 / hx, nty2 = (d.sNy + TY - 1) / TY;
+      hipLaunchKernelGGL(k_tracer_march2, dim3((unsigned)(nkc * nty2 * d.nT)), blk, 0, s, d, p, f, a, iterPtr, KC, nkc, nty2);
+    } else
+      hipLaunchKernelGGL(k_tracer_march, dim3((unsigned)(nkc * ntx * nty * d.nT)), blk, 0, s, d, p, f, a, iterPtr, KC, nkc,
+                         ntx, nty);
   } else hipLaunchKernelGGL(k_tracer_rhs_flat, grd, blk, 0, s, d, p, f, a, iterPtr);
   if (p.implicitDiffusion && impl) {
     const long ncol = (long)d.sNx * d.sNy * d.nT;

@@ -18,8 +18,8 @@ import pytest
 pytestmark = pytest.mark.gpu
 
 
-@pytest.mark.parametrize("march", [None, "1:2", "1:10", "1:3:single", "vi:4", "vi:3:generic", "fuse:29", "fuse:45", "fuse:77",
-                                   "impl2:1", "impl2:0"])
+@pytest.mark.parametrize("march", [None, "1:2", "1:10", "1:3:single", "1:3:single:v1", "vi:4", "vi:3:generic", "fuse:29",
+                                   "fuse:45", "fuse:77", "impl2:1", "impl2:0"])
 def test_llc30_8_steps_bitexact_vs_device_order_oracle(march, monkeypatch):
     """march = "on:KC[:single]": the tracer right-hand side as the k-march (the LLC-90
     default) with KC levels per workgroup -- 5 chunks, 1, 4 uneven -- for both tracers in one
@@ -30,7 +30,13 @@ def test_llc30_8_steps_bitexact_vs_device_order_oracle(march, monkeypatch):
     "fuse:MASK": the MGCM_STEP_FUSE launch fusions (29: the opt-in k_phys_phi pass; 45: the
     opt-in EXCH(cg2d_x) + etaN beside the correction step; 77: the tracers' halo exchange on
     their own stream).  "impl2:ON": both tracers' implicit solves in one launch
-    (k_tracer2_impl) after the single-tracer right-hand sides, k-march ON = 1 or flat 0."""
+    (k_tracer2_impl) after the single-tracer right-hand sides, k-march ON = 1 or flat 0.
+    ":v1": the one-column (8-byte) forms of the single-tracer k-march, DO_OCEANIC_PHYS and the
+    flat CALC_PHI_HYD instead of their two-column 16-byte forms (the defaults)."""
+    if march and march.endswith(":v1"):
+        for k in ("MGCM_TRACER_MARCH2", "MGCM_PHYS_V2", "MGCM_PHI_V2"):
+            monkeypatch.setenv(k, "0")
+        march = march[:-3]
     if march and march.startswith("impl2:"):
         monkeypatch.setenv("MGCM_TRACER_IMPL2", "1")
         monkeypatch.setenv("MGCM_TRACER_MARCH", march.split(":")[1])
