@@ -206,27 +206,14 @@ def default_pmc_summary(config):
 
 def stream_triad_gbs(device, n=64 << 20, reps=8):
     """SURVEY.md 8(d)'s roofline denominator measured on the box: a STREAM triad
-    a = b + s*c over three fp64 arrays of n doubles (512 MB each at the default), best of
-    `reps`, in GB/s (24 bytes per element).  torch's elementwise kernel, run after the timed
-    region -- a reference rate for the fractions, not part of the product."""
-    import torch
-    dev = torch.device("cuda", device)
-    b = torch.rand(n, dtype=torch.float64, device=dev)
-    c = torch.rand(n, dtype=torch.float64, device=dev)
-    a = torch.empty_like(b)
-    torch.add(b, c, alpha=3.0, out=a)
-    torch.cuda.synchronize(dev)
-    best = float("inf")
-    for _ in range(reps):
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        e0.record()
-        torch.add(b, c, alpha=3.0, out=a)
-        e1.record()
-        torch.cuda.synchronize(dev)
-        best = min(best, e0.elapsed_time(e1) * 1e-3)
-    del a, b, c
-    torch.cuda.empty_cache()
-    return 24.0 * n / best / 1e9
+    a = b + s*c over three fp64 arrays of n doubles (512 MB each at the default), 16 B per
+    lane, best of `reps` (mgcm_stream_triad), in GB/s -- run after the timed region, a
+    reference rate for the fractions."""
+    import ctypes
+    from mitgcm_amd._lib import check, lib
+    g = ctypes.c_double()
+    check(lib().mgcm_stream_triad(device, n, reps, ctypes.byref(g)), "mgcm_stream_triad")
+    return g.value
 
 
 def cg_kernel_key(m):

@@ -227,6 +227,10 @@ int mgcm_cg2d_sum_plan(mgcm_model *m, int *plan, long capacity, int *NT, int *PP
  * mgcm_forward_step call. */
 int mgcm_solve_stats(mgcm_model *m, int back, double *firstResidual, double *lastResidual,
                      int *numIters, double *rhsMax);
+/* The box's reference HBM rate: a STREAM triad a = b + s*c over three fp64 arrays of n
+ * doubles on `device` (16 B per lane), best of `reps`, in GB/s (24 bytes per element). */
+int mgcm_stream_triad(int device, long n, int reps, double *gbs);
+
 /* The same step's min-residual bookkeeping (cg2dUseMinResSol, cg2d.F:190-193, 338-347):
  * minResidualSq and nIterMin (both -1 when the option is off). */
 int mgcm_solve_minres(mgcm_model *m, int back, double *minResidualSq, int *nIterMin);

@@ -54,6 +54,7 @@ def lib():
         "mgcm_cg2d_sum_plan": (ci, [vp, PI, cl, PI, PI, PI]),
         "mgcm_solve_stats": (ci, [vp, ci, PD, PD, PI, PD]),
         "mgcm_solve_minres": (ci, [vp, ci, PD, PI]),
+        "mgcm_stream_triad": (ci, [ci, cl, ci, PD]),
         "mgcm_solve_history": (ci, [vp, ci, PI, PD, PD]),
         "mgcm_monitor": (ci, [vp, PD]),
         "mgcm_kernel_ms": (cd, [vp, cs, PI]),
@@ -101,7 +102,7 @@ def lib():
 EXPORTS = ["mgcm_create", "mgcm_destroy", "mgcm_last_error", "mgcm_set_param", "mgcm_get_param", "mgcm_put", "mgcm_put_async", "mgcm_put_batch_async",
            "mgcm_get", "mgcm_device_ptr", "mgcm_set_halo_map", "mgcm_set_uv_map", "mgcm_init", "mgcm_dynamics", "mgcm_thermodynamics",
            "mgcm_solve_for_pressure", "mgcm_momentum_correction_step", "mgcm_integr_continuity",
-           "mgcm_blocking_exchanges", "mgcm_prepare", "mgcm_forward_step", "mgcm_sync", "mgcm_cg2d", "mgcm_cg2d_sum_plan", "mgcm_solve_stats", "mgcm_solve_minres", "mgcm_solve_history", "mgcm_monitor",
+           "mgcm_blocking_exchanges", "mgcm_prepare", "mgcm_forward_step", "mgcm_sync", "mgcm_cg2d", "mgcm_cg2d_sum_plan", "mgcm_solve_stats", "mgcm_solve_minres", "mgcm_stream_triad", "mgcm_solve_history", "mgcm_monitor",
            "mgcm_kernel_ms", "mgcm_kernel_timing", "mgcm_set_tile_range", "mgcm_set_stream",
            "mgcm_exchange_nfields", "mgcm_halo_pack", "mgcm_tile_copy", "mgcm_begin_steps", "mgcm_step_phase", "mgcm_cg2d_op",
            "mgcm_cg2d_record", "mgcm_field_pack", "mgcm_exchange_field", "ini_cg2d_amd_",

@@ -2431,7 +2431,9 @@ hipError_t launch_phi_hyd(const Dims &d, const Params &p, const Fields &f, hipSt
   if (phi_flat_on(p)) {
     const bool qh = p.quasiHydrostatic && (p.select3dCoriScheme >= 1 || p.useNHMTerms);
     auto al = [](const void *q) { return ((uintptr_t)q & 15u) == 0; };
-    const int v2Env = getenv("MGCM_PHI_V2") ? atoi(getenv("MGCM_PHI_V2")) : 1;
+    // opt-in (MGCM_PHI_V2=1): bit-identical but slower on LLC-90, 32.8 against 30.4 us -- half
+    // the threads of a one-thread-per-column pass leave the chip under-filled (220 workgroups)
+    const int v2Env = getenv("MGCM_PHI_V2") ? atoi(getenv("MGCM_PHI_V2")) : 0;
     if (!rstar && !qh && v2Env != 0 && (d.OLx & 1) == 0 && (d.nx & 1) == 0 && (d.n3 & 1) == 0 && al(f.rhoInSitu) &&
         al(f.phiHydC) && al(f.totPhiHyd)) {
       const long np = (long)((d.sNx + 4) / 2) * (d.sNy + 2) * d.nT;

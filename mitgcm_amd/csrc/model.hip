@@ -2133,6 +2133,18 @@ int mgcm_step_phase(mgcm_model *m, int phase) {
       if (shard_join_thermo(m)) return -1;
       TIMED(K_CONT, launch_corr_cont(m->d, m->p, m->f, 0, m->stream));
       return 0;
+    // phase 2 / 6 split at the THERMODYNAMICS join, so the caller can send the new tracers'
+    // halo sources while the correction step runs: 19 the replicated CG2D alone, 17 EXCH(x) +
+    // etaN and the join, 18 the correction + continuity pass
+    case 19:
+      TIMED(K_CG2D, launch_cg2d(m, m->p.cg2dMaxIters, m->p.cg2dUseMinResSol - 1));
+      return 0;
+    case 17:
+      TIMED(K_ETA, launch_exch_eta(m->d, m->p, m->f, m->d_srcOf, false, 0, m->stream));
+      return shard_join_thermo(m);
+    case 18:
+      TIMED(K_CONT, launch_corr_cont(m->d, m->p, m->f, 0, m->stream));
+      return 0;
     case 3:
       if (shard_join_thermo(m)) return -1;
       if (m->p.exactConserv) TIMED(K_ETA, launch_exch_eta(m->d, m->p, m->f, m->d_srcOf, true, 0, m->stream));
@@ -2167,6 +2179,52 @@ int mgcm_step_phase(mgcm_model *m, int phase) {
       return 0;
   }
   return set_err("mgcm_step_phase: no phase %d", phase);
+}
+
+// ---- the box's HBM reference rate (bench.py: SURVEY.md 8(d)'s roofline denominator) ---------
+namespace mgcm {
+__global__ void __launch_bounds__(256) k_triad(double2 *__restrict__ a, const double2 *__restrict__ b,
+                                               const double2 *__restrict__ c, double s, long n2) {
+  for (long q = (long)blockIdx.x * 256 + threadIdx.x; q < n2; q += (long)gridDim.x * 256) {
+    const double2 x = b[q], y = c[q];
+    a[q] = make_double2(x.x + s * y.x, x.y + s * y.y);
+  }
+}
+}  // namespace mgcm
+// STREAM triad a = b + s*c over three fp64 arrays of n doubles on `device`, 16 B per lane,
+// best of `reps` (event-timed): GB/s at 24 bytes per element.
+int mgcm_stream_triad(int device, long n, int reps, double *gbs) {
+  if (n <= 0 || (n & 1) || reps <= 0 || !gbs) return set_err("mgcm_stream_triad: bad arguments");
+  HIPCHK(hipSetDevice(device));
+  double *a = nullptr, *b = nullptr, *c = nullptr;
+  hipStream_t st = nullptr;
+  hipEvent_t e0 = nullptr, e1 = nullptr;
+  int rc = 0;
+  float best = 1e30f;
+  if (hipMalloc(&a, n * sizeof(double)) != hipSuccess || hipMalloc(&b, n * sizeof(double)) != hipSuccess ||
+      hipMalloc(&c, n * sizeof(double)) != hipSuccess || hipStreamCreate(&st) != hipSuccess ||
+      hipEventCreate(&e0) != hipSuccess || hipEventCreate(&e1) != hipSuccess ||
+      hipMemsetAsync(b, 0, n * sizeof(double), st) != hipSuccess || hipMemsetAsync(c, 0, n * sizeof(double), st) != hipSuccess)
+    rc = set_err("mgcm_stream_triad: allocation");
+  const unsigned grid = 256 * 16;   // 16 workgroups per CU, grid-stride
+  for (int r = -1; rc == 0 && r < reps; r++) {   // r = -1: warm-up
+    hipEventRecord(e0, st);
+    hipLaunchKernelGGL(mgcm::k_triad, dim3(grid), dim3(256), 0, st, (double2 *)a, (const double2 *)b, (const double2 *)c, 3.0,
+                       n / 2);
+    hipEventRecord(e1, st);
+    if (hipEventSynchronize(e1) != hipSuccess) { rc = set_err("mgcm_stream_triad: kernel"); break; }
+    float ms = 0.f;
+    hipEventElapsedTime(&ms, e0, e1);
+    if (r >= 0 && ms < best) best = ms;
+  }
+  if (rc == 0) *gbs = 24.0 * (double)n / (best * 1e-3) / 1e9;
+  if (e0) hipEventDestroy(e0);
+  if (e1) hipEventDestroy(e1);
+  if (st) hipStreamDestroy(st);
+  if (a) hipFree(a);
+  if (b) hipFree(b);
+  if (c) hipFree(c);
+  return rc;
 }
 
 // ---- several models stepped by one host (fortran_abi.hip's tile-sharded drop-ins) ---------

@@ -450,21 +450,38 @@ class ShardedModel:
             ck(L.mgcm_step_phase(h, 9), "mgcm_step_phase(9)")
         else:
             ck(L.mgcm_step_phase(h, 1), "mgcm_step_phase(1)")
+        # with THERMODYNAMICS forked, the correction step is split off its phase (17 | 18): the
+        # new tracers' halo sources leave at the join and travel while the correction and
+        # continuity pass runs (the velocities' follow it)
+        split = self.fork
+
+        def after_solve(p6):
+            nonlocal fin_tracers
+            if split:
+                ck(L.mgcm_step_phase(h, 17), "mgcm_step_phase(17)")
+                fin_tracers = self._halo(1, start_only=True)
+                ck(L.mgcm_step_phase(h, 18), "mgcm_step_phase(18)")
+            else:
+                ck(L.mgcm_step_phase(h, p6), "mgcm_step_phase(%d)" % p6)
         if self.cg2d == "distributed":
             self._cg2d_distributed()
             self._exch_2d("cg2d_x")      # the halo sources of the new x before etaN everywhere
-            ck(L.mgcm_step_phase(h, 6), "mgcm_step_phase(6)")
+            after_solve(6)
         elif self.cg2d == "device":
             # the parts' rings reach into the neighbours' tiles: their b and x first
             self._exch_2d("cg2d_b")
             self._exch_2d("cg2d_x")
             ck(L.mgcm_step_phase(h, 10), "mgcm_step_phase(10)")   # this process's parts
             self._exch_2d("cg2d_x")
-            ck(L.mgcm_step_phase(h, 6), "mgcm_step_phase(6)")
+            after_solve(6)
         else:
             self._gather_2d("cg2d_b")
             self._gather_2d("cg2d_x")
-            ck(L.mgcm_step_phase(h, 2), "mgcm_step_phase(2)")
+            if split:
+                ck(L.mgcm_step_phase(h, 19), "mgcm_step_phase(19)")
+                after_solve(None)
+            else:
+                ck(L.mgcm_step_phase(h, 2), "mgcm_step_phase(2)")
         if self.m.params.get("exactConserv", 0):
             self._gather_2d("cg2d_b")
         ck(L.mgcm_step_phase(h, 3), "mgcm_step_phase(3)")
