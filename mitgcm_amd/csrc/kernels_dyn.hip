@@ -2324,6 +2324,14 @@ static void vi_tile_shape(const Dims &d, int &BX, int &BY) {
   BX = (W + nbx - 1) / nbx;                 // 92 -> 31, 34 -> 17 (two blocks), <= 32
   BY = VT_NT / BX;
   while (BY > 1 && ((BX + 2) * (BY + 2) > VT_EMAX || (BX + 1) * (BY + 1) > VT_IMAX)) BY--;
+  // MGCM_VI_BY caps the rows (A/B).  7 keeps a 31-wide block's (BX+1)(BY+1) intermediate
+  // points within one pass of the 256 threads, but the specialised k-march at 31 x 7 (more
+  // blocks, more spills) measured slower on LLC-90: 1.58-1.60 against 1.54-1.56 ms/step
+  // (profiles/r04/viby/), so only 31 x 8 / 32 x 8 are instantiated
+  if (const char *e = getenv("MGCM_VI_BY")) {
+    const int cap = atoi(e);
+    if (cap >= 1 && cap < BY) BY = cap;
+  }
   const int nby = (H + BY - 1) / BY;
   BY = (H + nby - 1) / nby;                 // balance the rows over the blocks
 }

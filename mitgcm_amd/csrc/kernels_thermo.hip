@@ -1215,7 +1215,11 @@ hipError_t launch_hfac_snapshot(const Dims &d, const Fields &f, double *snap, hi
 hipError_t launch_oceanic_phys(const Dims &d, const Params &p, const Fields &f, const int *iterPtr, hipStream_t s, bool gm) {
   auto al = [](const void *q) { return ((uintptr_t)q & 15u) == 0; };
   const int v2Env = getenv("MGCM_PHYS_V2") ? atoi(getenv("MGCM_PHYS_V2")) : 1;
-  const bool v2 = v2Env != 0 && (d.n2 & 1) == 0 && (d.n3 & 1) == 0 && al(f.theta) && al(f.salt) && al(f.maskC) &&
+  // (large grids only: on config 2's 70 k points per level set, half the threads cost more
+  // than the wider accesses save -- 12.9 against 10.1 us, the surface level's forcing
+  // interpolation then serial in each thread)
+  const bool big = (long)d.n2 * d.nT * d.Nr >= (1L << 21);
+  const bool v2 = v2Env != 0 && (big || v2Env == 2) && (d.n2 & 1) == 0 && (d.n3 & 1) == 0 && al(f.theta) && al(f.salt) && al(f.maskC) &&
                   al(f.rhoInSitu) && al(f.IVDConvCount) && (!p.useGMRedi || al(f.sigmaR)) &&
                   (p.eosType != 1 || p.selectP_inEOS_Zc != 2 || al(f.totPhiHyd));
   if (v2) {
