@@ -31,12 +31,13 @@ def test_llc30_8_steps_bitexact_vs_device_order_oracle(march, monkeypatch):
     opt-in EXCH(cg2d_x) + etaN beside the correction step; 77: the tracers' halo exchange on
     their own stream).  "impl2:ON": both tracers' implicit solves in one launch
     (k_tracer2_impl) after the single-tracer right-hand sides, k-march ON = 1 or flat 0.
-    ":v1": the one-column (8-byte) forms of the single-tracer k-march and DO_OCEANIC_PHYS
-    (the defaults are their two-column 16-byte forms) and the opt-in two-column flat
-    CALC_PHI_HYD."""
+    ":v1": the other forms of the 16-byte switches -- the one-column single-tracer k-march
+    (the default is its two-column form), the two-column DO_OCEANIC_PHYS forced (at full
+    size the default; below 2^21 points the one-column form runs) and the opt-in two-column
+    flat CALC_PHI_HYD."""
     if march and march.endswith(":v1"):
-        for k in ("MGCM_TRACER_MARCH2", "MGCM_PHYS_V2"):
-            monkeypatch.setenv(k, "0")
+        monkeypatch.setenv("MGCM_TRACER_MARCH2", "0")
+        monkeypatch.setenv("MGCM_PHYS_V2", "2")
         monkeypatch.setenv("MGCM_PHI_V2", "1")
         march = march[:-3]
     if march and march.startswith("impl2:"):
