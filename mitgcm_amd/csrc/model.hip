@@ -241,10 +241,12 @@ struct mgcm_model {
   // mgcm_put_batch_async: two pinned host slots (each with the event of its last copy) and
   // one device buffer; a batch travels as [header | values] in one copy, then one scatter
   char *stHost[2] = {nullptr, nullptr};
-  hipEvent_t stEv[2] = {nullptr, nullptr};
+  hipEvent_t stEv[2] = {nullptr, nullptr};    // slot q's scatter done (its pinned and device buffers free)
+  hipEvent_t stCopied[2] = {nullptr, nullptr};   // slot q's copy done (the scatter may read it)
   size_t stCap = 0;
   int stNext = 0;
-  char *stDev = nullptr;
+  char *stDev[2] = {nullptr, nullptr};
+  hipStream_t stCopy = nullptr;   // the uploads' copy stream: a step's copy overlaps the step before
   // step counters: [0] = myIter, [1] = record slot
   int *d_ctr = nullptr;
   SolveRecord *d_rec = nullptr;
@@ -892,8 +894,10 @@ void mgcm_destroy(mgcm_model *m) {
   for (int q = 0; q < 2; q++) {
     if (m->stHost[q]) hipHostFree(m->stHost[q]);
     if (m->stEv[q]) hipEventDestroy(m->stEv[q]);
+    if (m->stCopied[q]) hipEventDestroy(m->stCopied[q]);
+    if (m->stDev[q]) hipFree(m->stDev[q]);
   }
-  if (m->stDev) hipFree(m->stDev);
+  if (m->stCopy) hipStreamDestroy(m->stCopy);
   if (m->ownStream) hipStreamDestroy(m->ownStream);
   if (m->stream2) hipStreamDestroy(m->stream2);
   if (m->evFork) hipEventDestroy(m->evFork);
@@ -1033,24 +1037,24 @@ int mgcm_put_batch_async(mgcm_model *m, int n, const char *const *names, const d
   HIPCHK(hipSetDevice(m->device));
   const size_t bytes = (size_t)(2 + 2 * n + total) * sizeof(double);
   if (m->stCap < bytes) {
+    HIPCHK(hipStreamSynchronize(m->stream));
+    if (m->stCopy) HIPCHK(hipStreamSynchronize(m->stCopy));
+    else HIPCHK(hipStreamCreateWithFlags(&m->stCopy, hipStreamNonBlocking));
     for (int q = 0; q < 2; q++) {
-      if (m->stEv[q]) HIPCHK(hipEventSynchronize(m->stEv[q]));
       if (m->stHost[q]) HIPCHK(hipHostFree(m->stHost[q]));
+      if (m->stDev[q]) HIPCHK(hipFree(m->stDev[q]));
       m->stHost[q] = nullptr;
+      m->stDev[q] = nullptr;
       HIPCHK(hipHostMalloc((void **)&m->stHost[q], bytes, hipHostMallocDefault));
+      HIPCHK(hipMalloc((void **)&m->stDev[q], bytes));
       if (!m->stEv[q]) HIPCHK(hipEventCreateWithFlags(&m->stEv[q], hipEventDisableTiming));
+      if (!m->stCopied[q]) HIPCHK(hipEventCreateWithFlags(&m->stCopied[q], hipEventDisableTiming));
     }
-    if (m->stDev) {
-      HIPCHK(hipStreamSynchronize(m->stream));
-      HIPCHK(hipFree(m->stDev));
-    }
-    m->stDev = nullptr;
-    HIPCHK(hipMalloc((void **)&m->stDev, bytes));
     m->stCap = bytes;
   }
   const int q = m->stNext;
   m->stNext ^= 1;
-  HIPCHK(hipEventSynchronize(m->stEv[q]));
+  HIPCHK(hipEventSynchronize(m->stEv[q]));   // slot q's previous scatter (two calls back) is done
   long *hdr = reinterpret_cast<long *>(m->stHost[q]);
   double *vals = reinterpret_cast<double *>(m->stHost[q]) + 2 + 2 * n;
   hdr[0] = n;
@@ -1062,11 +1066,15 @@ int mgcm_put_batch_async(mgcm_model *m, int n, const char *const *names, const d
     o += counts[i];
   }
   hdr[1 + 2 * n] = o;
-  HIPCHK(hipMemcpyAsync(m->stDev, m->stHost[q], bytes, hipMemcpyHostToDevice, m->stream));
-  HIPCHK(hipEventRecord(m->stEv[q], m->stream));
+  // the copy on the copy stream (beside whatever the model stream still runs), the scatter
+  // in the model stream's order after it
+  HIPCHK(hipMemcpyAsync(m->stDev[q], m->stHost[q], bytes, hipMemcpyHostToDevice, m->stCopy));
+  HIPCHK(hipEventRecord(m->stCopied[q], m->stCopy));
+  HIPCHK(hipStreamWaitEvent(m->stream, m->stCopied[q], 0));
   const unsigned gx = (unsigned)std::min<long>(64, (maxc + 255) / 256);
-  hipLaunchKernelGGL(mgcm::k_put_scatter, dim3(gx, n), dim3(256), 0, m->stream, m->stDev);
+  hipLaunchKernelGGL(mgcm::k_put_scatter, dim3(gx, n), dim3(256), 0, m->stream, m->stDev[q]);
   HIPCHK(hipGetLastError());
+  HIPCHK(hipEventRecord(m->stEv[q], m->stream));
   return 0;
 }
 
