@@ -262,13 +262,15 @@ inline unsigned mg_colf_blocks(long ncols, int nc) { return (unsigned)((ncols + 
 // bit-identical, no measurable change on LLC-90: 1.851 against 1.851-1.854 ms/step).
 // MG_FUSE_DT THERMODYNAMICS' tracer kernels folded into DYNAMICS' launches instead of a
 // second stream beside them (kernels_step.hip; early fork only, small grids), MG_FUSE_ETAX
-// no separate EXCH(cg2d_x) + etaN under exactConserv (one_step).
+// no separate EXCH(cg2d_x) + etaN under exactConserv (one_step), MG_FUSE_OPE UPDATE_CG2D's
+// operator and preconditioner in the fold's first two grids (ucg2d.h; r*, with MG_FUSE_DT).
 enum { MG_FUSE_SFP = 1, MG_FUSE_ETA = 2, MG_FUSE_PHI = 4, MG_FUSE_END = 8, MG_FUSE_PHYS = 16, MG_FUSE_ETAA = 32,
-       MG_FUSE_TREX = 64, MG_FUSE_DT = 128, MG_FUSE_ETAX = 256, MG_FUSE_TCG = 512 };
+       MG_FUSE_TREX = 64, MG_FUSE_DT = 128, MG_FUSE_ETAX = 256, MG_FUSE_TCG = 512, MG_FUSE_OPE = 1024 };
 inline bool mg_fuse_on(int bit) {
   // read per call (tests switch it per model)
   const int mask = getenv("MGCM_STEP_FUSE") ? atoi(getenv("MGCM_STEP_FUSE"))
-                                            : MG_FUSE_SFP | MG_FUSE_PHI | MG_FUSE_END | MG_FUSE_DT | MG_FUSE_ETAX;
+                                            : MG_FUSE_SFP | MG_FUSE_PHI | MG_FUSE_END | MG_FUSE_DT | MG_FUSE_ETAX |
+                                                MG_FUSE_OPE;
   return (mask & bit) != 0;
 }
 // Horizontal launch fusion of two independent latency-bound kernels into one grid: on the

@@ -10,6 +10,7 @@
 // source (srcOf, the EXCH map of the tile topology) inside the same pass, because
 // EXCH copies values that are computed by the same expression as the source's.
 #include "common.h"
+#include "ucg2d.h"
 
 namespace mgcm {
 
@@ -119,15 +120,16 @@ __global__ void __launch_bounds__(256) k_rstar_exch(Dims d, Params p, Fields f, 
 // column pass (FORWARD_STEP: UPDATE_R_STAR + UPDATE_CG2D, then CALC_DIV_GHAT): the flux terms
 // read hFacW(i+1) / hFacS(j+1) of the neighbouring columns, which this pass is rewriting, so
 // they are formed from h0Fac*rStarFac there (the expression that column stores: same bits).
+// opIn = 0: the operator was built at the start of the step (ucg2d.h, MG_FUSE_OPE) -- hFac only.
 template <bool SFP>
-__global__ void __launch_bounds__(256) k_update_r_star_cg2d_a(Dims d, Params p, Fields f, int nc) {
+__global__ void __launch_bounds__(256) k_update_r_star_cg2d_a(Dims d, Params p, Fields f, int nc, int opIn) {
   extern __shared__ __attribute__((aligned(16))) double lds[];
   MG_COLF(1 - d.OLx, d.nx, 1 - d.OLy, d.ny, nc)
   const int NS = d.Nr * NC_;
   double *sW = lds, *sS = lds + NS;
   double *fE = lds + 2 * NS, *fW = lds + 3 * NS, *fN = lds + 4 * NS, *fS = lds + 5 * NS;   // SFP only
   const long q = MG_I2(d, i, j, t);
-  const bool op = p.nonlinFreeSurf > 2 && i >= 1 && i <= d.sNx + 1 && j >= 1 && j <= d.sNy + 1;
+  const bool op = opIn && p.nonlinFreeSurf > 2 && i >= 1 && i <= d.sNx + 1 && j >= 1 && j <= d.sNy + 1;
   const bool inner = i >= 1 && i <= d.sNx && j >= 1 && j <= d.sNy;
   if (valid) {
     const double fc = f.rStarFacC[q], fw = f.rStarFacW[q], fs = f.rStarFacS[q];
@@ -167,7 +169,7 @@ __global__ void __launch_bounds__(256) k_update_r_star_cg2d_a(Dims d, Params p, 
   }
   __syncthreads();
   if (!valid || kk != 0) return;
-  if (p.nonlinFreeSurf > 2) {
+  if (opIn && p.nonlinFreeSurf > 2) {
     double aW = 0.0, aS = 0.0;
     if (op) {
       for (int k = 1; k <= d.Nr; k++) {
@@ -184,38 +186,9 @@ __global__ void __launch_bounds__(256) k_update_r_star_cg2d_a(Dims d, Params p, 
   if (SFP) sfp_rhs_column(d, p, f, q, inner, fE, fW, fN, fS, NC_, cc);
 }
 
-// UPDATE_CG2D part 2 (update_cg2d.F:144-199): aC2d on the interior, EXCH_XY_RS(aC2d)
-// (halo = the source's aC, recomputed here by the same expression), and the
-// preconditioner pC, pW, pS on 1..sNx+1 x 1..sNy+1 (cg2dPreCondFreq = 1).
+// UPDATE_CG2D part 2 (ucg2d.h ucg2d_p_point)
 __global__ void __launch_bounds__(256) k_update_cg2d_p(Dims d, Params p, Fields f, const long *__restrict__ srcOf) {
-  const long q = (long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (q >= d.n2 * d.nTiles) return;
-  const int t = (int)(q / d.n2);
-  if (t < d.t0 || t >= d.t0 + d.nT) return;
-  const long l = q % d.n2;
-  const int i = (int)(l % d.nx) - d.OLx + 1, j = (int)(l / d.nx) - d.OLy + 1;
-  const long nx = d.nx;
-  auto aCat = [&](long r) {   // aC2d at an interior point r
-    return -(f.aW2d[r] + f.aW2d[r + 1] + f.aS2d[r] + f.aS2d[r + nx] +
-             p.freeSurfFac * p.cg2dNorm * f.recip_Bo[r] * f.rA[r] / p.deltaTMom / p.deltaTFreeSurf);
-  };
-  auto aCx = [&](long r) {    // after EXCH: interior value, or the interior source's
-    const long s = srcOf[r];
-    return aCat(s >= 0 ? s : r);
-  };
-  const bool interior = i >= 1 && i <= d.sNx && j >= 1 && j <= d.sNy;
-  const long sq = srcOf[q];
-  if (interior || sq >= 0) f.aC2d[q] = aCat(sq >= 0 ? sq : q);
-  if (i >= 1 && i <= d.sNx + 1 && j >= 1 && j <= d.sNy + 1) {
-    const double aC = aCx(q), aCw = aCx(q - 1), aCs = aCx(q - nx);
-    f.pC[q] = (aC == 0.0) ? 1.0 : 1.0 / aC;
-    const double pWt = aC + aCw;
-    if (pWt == 0.0) f.pW[q] = 0.0;
-    else { const double dd = 0.51 * pWt; f.pW[q] = -f.aW2d[q] / (dd * dd); }   // cg2dpcOffDFac = 0.51
-    const double pSt = aC + aCs;
-    if (pSt == 0.0) f.pS[q] = 0.0;
-    else { const double dd = 0.51 * pSt; f.pS[q] = -f.aS2d[q] / (dd * dd); }
-  }
+  ucg2d_p_point(d, p, f, srcOf, (int)blockIdx.x);
 }
 
 hipError_t launch_calc_r_star(const Dims &d, const Params &p, const Fields &f, const long *srcOf, hipStream_t s,
@@ -239,8 +212,9 @@ hipError_t launch_rstar_exch(const Dims &d, const Params &p, const Fields &f, co
   return hipGetLastError();
 }
 
+// opEarly: the operator and preconditioner were built beside DYNAMICS (launch_dyn_thermo)
 hipError_t launch_update_r_star_cg2d(const Dims &d, const Params &p, const Fields &f, const long *srcOf, hipStream_t s,
-                                     bool sfp) {
+                                     bool sfp, bool opEarly) {
   const long n = d.n2 * d.nTiles;
   const unsigned nb = (unsigned)((n + 255) / 256);
   const long ncol = (long)d.nx * d.ny * d.nT;
@@ -249,8 +223,8 @@ hipError_t launch_update_r_star_cg2d(const Dims &d, const Params &p, const Field
   MG_ALLOW_LDS(k_update_r_star_cg2d_a<false>);
   MG_ALLOW_LDS(k_update_r_star_cg2d_a<true>);
   hipLaunchKernelGGL(sfp ? k_update_r_star_cg2d_a<true> : k_update_r_star_cg2d_a<false>, dim3(mg_colf_blocks(ncol, nc)),
-                     dim3(256), mg_colf_lds(d.Nr, nc, nArr), s, d, p, f, nc);
-  if (p.nonlinFreeSurf > 2) hipLaunchKernelGGL(k_update_cg2d_p, dim3(nb), dim3(256), 0, s, d, p, f, srcOf);
+                     dim3(256), mg_colf_lds(d.Nr, nc, nArr), s, d, p, f, nc, opEarly ? 0 : 1);
+  if (p.nonlinFreeSurf > 2 && !opEarly) hipLaunchKernelGGL(k_update_cg2d_p, dim3(nb), dim3(256), 0, s, d, p, f, srcOf);
   return hipGetLastError();
 }
 

@@ -24,6 +24,7 @@
 // relocatable device code, and the fused kernels need both files' bodies.
 #include "kernels_dyn.hip"
 #include "kernels_thermo.hip"
+#include "ucg2d.h"
 
 namespace mgcm {
 
@@ -63,8 +64,12 @@ __global__ void __launch_bounds__(256) k_dt_back(Dims d, Params p, Fields f, Tra
 //   1: GMREDI_CALC_TENSOR | CALC_PHI_HYD | del2uv
 //   2: MOM_FLUXFORM U | V | rhs(theta) | rhs(salt)
 //   3: CD_CODE_SCHEME | implicit solve (theta) | (salt)
-__global__ void __launch_bounds__(256) k_dt_l1(Dims d, Params p, Fields f, int nc, int nbGm, int nbPhi) {
+// and under r* with MG_FUSE_OPE UPDATE_CG2D's operator (nbOp blocks, ucg2d.h) at the head of 1,
+// its preconditioner (nbPc blocks) at the tail of 2 -- the operator of the step, built early
+__global__ void __launch_bounds__(256) k_dt_l1(Dims d, Params p, Fields f, int nc, int nbGm, int nbPhi, int nbOp) {
   int lb = mg_xcd_block();
+  if (lb < nbOp) { ucg2d_op_point(d, p, f, lb); return; }
+  lb -= nbOp;
   if (lb < nbGm) { gm_tensor_body(d, p, f, lb); return; }
   lb -= nbGm;
   if (lb < nbPhi) { phi_hyd_body(d, p, f, nc, lb); return; }
@@ -73,15 +78,18 @@ __global__ void __launch_bounds__(256) k_dt_l1(Dims d, Params p, Fields f, int n
 static void phi_frame(const Dims &d, const Params &p, int &nc, int &nArr, int &nb);
 // k_dt_l1 with CALC_PHI_HYD's flat per-column pass (kernels_dyn.hip phi_flat_body)
 template <bool RS, bool QH>
-__global__ void __launch_bounds__(256) k_dt_l1f(Dims d, Params p, Fields f, int nbGm, int nbPhi) {
+__global__ void __launch_bounds__(256) k_dt_l1f(Dims d, Params p, Fields f, int nbGm, int nbPhi, int nbOp) {
   int lb = mg_xcd_block();
+  if (lb < nbOp) { ucg2d_op_point(d, p, f, lb); return; }
+  lb -= nbOp;
   if (lb < nbGm) { gm_tensor_body(d, p, f, lb); return; }
   lb -= nbGm;
   if (lb < nbPhi) { phi_flat_body<RS, QH>(d, p, f, lb); return; }
   del2uv_body(d, p, f, lb - nbPhi);
 }
-// launch [GMREDI_CALC_TENSOR | CALC_PHI_HYD | del2uv (nbDel blocks, 0 = none)]
-static void launch_l1(const Dims &d, const Params &p, const Fields &f, int nbDel, hipStream_t s) {
+// launch [UPDATE_CG2D operator (nbOp blocks, 0 = none) | GMREDI_CALC_TENSOR | CALC_PHI_HYD |
+// del2uv (nbDel blocks, 0 = none)]
+static void launch_l1(const Dims &d, const Params &p, const Fields &f, int nbDel, hipStream_t s, int nbOp = 0) {
   const int nbGm = (int)mg_plane_blocks(d.nx - 2, d.ny - 2, d.nT * d.Nr);
   if (phi_flat_on(p)) {
     const bool rs = p.nonlinFreeSurf > 0 && p.select_rStar > 0;
@@ -89,19 +97,23 @@ static void launch_l1(const Dims &d, const Params &p, const Fields &f, int nbDel
     auto kern = rs ? (qh ? k_dt_l1f<true, true> : k_dt_l1f<true, false>)
                    : (qh ? k_dt_l1f<false, true> : k_dt_l1f<false, false>);
     const int nbPhi = phi_flat_blocks(d, p);
-    hipLaunchKernelGGL(kern, dim3((unsigned)(nbGm + nbPhi + nbDel)), dim3(256), 0, s, d, p, f, nbGm, nbPhi);
+    hipLaunchKernelGGL(kern, dim3((unsigned)(nbOp + nbGm + nbPhi + nbDel)), dim3(256), 0, s, d, p, f, nbGm, nbPhi,
+                       nbOp);
     return;
   }
   int nc, nArr, nbPhi;
   phi_frame(d, p, nc, nArr, nbPhi);
   MG_ALLOW_LDS(k_dt_l1);
-  hipLaunchKernelGGL(k_dt_l1, dim3((unsigned)(nbGm + nbPhi + nbDel)), dim3(256), mg_colf_lds(d.Nr, nc, nArr), s, d, p, f, nc,
-                     nbGm, nbPhi);
+  hipLaunchKernelGGL(k_dt_l1, dim3((unsigned)(nbOp + nbGm + nbPhi + nbDel)), dim3(256), mg_colf_lds(d.Nr, nc, nArr), s, d, p,
+                     f, nc, nbGm, nbPhi, nbOp);
 }
 template <bool GM, bool FF4>
 __global__ void __launch_bounds__(256) k_dt_l2(Dims d, Params p, Fields f, TracerArgs aT, TracerArgs aS,
-                                               const int *iterPtr, int nbMom, int nbTr) {
+                                               const int *iterPtr, int nbMom, int nbTr, const long *__restrict__ srcOf,
+                                               int nbPc) {
   int lb = mg_xcd_block();
+  if (lb < nbPc) { ucg2d_p_point(d, p, f, srcOf, lb); return; }
+  lb -= nbPc;
   if (lb < nbMom) {
     if constexpr (FF4) mom_ff4_body(d, p, f, iterPtr, lb);
     else if (lb & 1) mom_step_point<false, 2>(d, p, f, iterPtr, lb >> 1);
@@ -195,9 +207,11 @@ hipError_t launch_tracer_hpair(const Dims &d, const Params &p, const Fields &f, 
 }
 
 // CALC_PHI_HYD + THERMODYNAMICS' tracers + DYNAMICS in three launches on one stream
-// (after DO_OCEANIC_PHYS; dyn_thermo_fusable must hold)
+// (after DO_OCEANIC_PHYS; dyn_thermo_fusable must hold).  srcOf != nullptr (default layout,
+// nonlinFreeSurf > 2, every tile): UPDATE_CG2D in the first two grids as well (ucg2d.h), and
+// launch_update_r_star_cg2d then runs with opEarly
 hipError_t launch_dyn_thermo(const Dims &d, const Params &p, const Fields &f, const TracerArgs &aT, const TracerArgs &aS,
-                             const int *iterPtr, hipStream_t s) {
+                             const int *iterPtr, hipStream_t s, const long *srcOf) {
   const dim3 blk(256);
   // front: phi's column frame (launch_phi_hyd's columns and LDS), del2uv's and the tracers' planes
   int ncPhi, nArrPhi, nbPhi;
@@ -205,11 +219,13 @@ hipError_t launch_dyn_thermo(const Dims &d, const Params &p, const Fields &f, co
   const int nbDel = del2_needed(p) ? (int)mg_plane_blocks(d.nx, d.ny, d.nT * d.Nr) : 0;
   const int nbTr = (int)mg_plane_blocks(d.sNx, d.sNy, d.nT * d.Nr);
   if (dyn_thermo_takes_gm(p)) {
-    launch_l1(d, p, f, nbDel, s);
+    const int nbU = srcOf ? ucg2d_blocks(d) : 0;
+    launch_l1(d, p, f, nbDel, s, nbU);
     const bool ff4 = mom_ff4_on(true);
     const int nbMom = ff4 ? mom_ff4_blocks(d) : 2 * (int)mg_plane_blocks(d.nx, d.ny, d.nT * d.Nr);
     auto l2 = ff4 ? k_dt_l2<true, true> : k_dt_l2<true, false>;
-    hipLaunchKernelGGL(l2, dim3((unsigned)(nbMom + 2 * nbTr)), blk, 0, s, d, p, f, aT, aS, iterPtr, nbMom, nbTr);
+    hipLaunchKernelGGL(l2, dim3((unsigned)(nbU + nbMom + 2 * nbTr)), blk, 0, s, d, p, f, aT, aS, iterPtr, nbMom, nbTr, srcOf,
+                       nbU);
     const long ncolTr = (long)d.sNx * d.sNy * d.nT;
     const int ncTr = mg_colf_nc(ncolTr, d.Nr, 3);
     const int nbImp = (int)mg_colf_blocks(ncolTr, ncTr);
@@ -219,6 +235,7 @@ hipError_t launch_dyn_thermo(const Dims &d, const Params &p, const Fields &f, co
                        iterPtr, ncTr, nbCd, nbImp);
     return hipGetLastError();
   }
+  if (srcOf) return hipErrorInvalidValue;   // (the operator rides only in the default layout)
   MG_ALLOW_LDS(k_dt_front<true>);
   hipLaunchKernelGGL(k_dt_front<true>, dim3((unsigned)(nbPhi + nbDel + 2 * nbTr)), blk,
                      mg_colf_lds(d.Nr, ncPhi, nArrPhi), s, d, p, f, aT, aS, iterPtr, ncPhi, nbPhi, nbDel, nbTr);

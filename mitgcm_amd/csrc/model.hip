@@ -56,7 +56,8 @@ hipError_t launch_calc_r_star(const Dims &, const Params &, const Fields &, cons
                               int fromX = 0);
 hipError_t launch_rstar_exch(const Dims &, const Params &, const Fields &, const long *, bool, const XFields &, const long *,
                              int, int *, hipStream_t, int fromX = 0);
-hipError_t launch_update_r_star_cg2d(const Dims &, const Params &, const Fields &, const long *, hipStream_t, bool sfp = false);
+hipError_t launch_update_r_star_cg2d(const Dims &, const Params &, const Fields &, const long *, hipStream_t, bool sfp = false,
+                                     bool opEarly = false);
 hipError_t launch_halo_pack(const Dims &, const XFields &, const long *, long, double *, int, hipStream_t);
 hipError_t launch_oceanic_phys(const Dims &, const Params &, const Fields &, const int *, hipStream_t, bool gm = true);
 hipError_t launch_tracer_step(const Dims &, const Params &, const Fields &, const TracerArgs &, const int *, hipStream_t,
@@ -67,7 +68,7 @@ hipError_t launch_tracer2_impl(const Dims &, const Params &, const Fields &, con
 bool tracer_pair_ok(const Dims &, const Params &, const TracerArgs &, const TracerArgs &);
 bool dyn_thermo_fusable(const Dims &, const Params &, const TracerArgs &, const TracerArgs &);
 hipError_t launch_dyn_thermo(const Dims &, const Params &, const Fields &, const TracerArgs &, const TracerArgs &, const int *,
-                             hipStream_t);
+                             hipStream_t, const long *srcOf = nullptr);
 bool dyn_thermo_takes_gm(const Params &);
 hipError_t launch_gm_tensor(const Dims &, const Params &, const Fields &, hipStream_t);
 hipError_t launch_hfac_snapshot(const Dims &, const Fields &, double *, hipStream_t);
@@ -1180,8 +1181,8 @@ static hipError_t calc_r_star(mgcm_model *m, bool fuseEtaH = false, int fromX = 
 }
 // sfp: k_sfp_rhs fused into the r* column pass (FORWARD_STEP on the whole domain only: in a
 // tile-sharded run the r* pass covers every tile and the right-hand side this process's own)
-static hipError_t update_r_star_cg2d(mgcm_model *m, bool sfp = false) {
-  return launch_update_r_star_cg2d(all_tiles(m->d), m->p, m->f, m->d_srcOf, m->stream, sfp);
+static hipError_t update_r_star_cg2d(mgcm_model *m, bool sfp = false, bool opEarly = false) {
+  return launch_update_r_star_cg2d(all_tiles(m->d), m->p, m->f, m->d_srcOf, m->stream, sfp, opEarly);
 }
 
 int mgcm_init(mgcm_model *m) {
@@ -1650,9 +1651,13 @@ static int one_step(mgcm_model *m) {
   } else {
     if (phys() || tracers_on(m, m->stream)) return -1;
   }
+  // UPDATE_CG2D beside DYNAMICS (ucg2d.h, MG_FUSE_OPE): the operator from h0Fac*rStarFac in
+  // the fold's first grid, the preconditioner in its second; UPDATE_R_STAR then rewrites hFac only
+  const bool opEarly = dtFused && m->p.nonlinFreeSurf > 2 && dyn_thermo_takes_gm(m->p) && m->d.nT == m->d.nTiles &&
+                       mg_fuse_on(MG_FUSE_OPE);
   if (m->p.momStepping) {
     if (dtFused) {
-      TIMED(K_MOM, launch_dyn_thermo(m->d, m->p, m->f, aT, aS, m->d_ctr, m->stream));
+      TIMED(K_MOM, launch_dyn_thermo(m->d, m->p, m->f, aT, aS, m->d_ctr, m->stream, opEarly ? m->d_srcOf : nullptr));
       std::swap(m->f.theta, m->f.thetaNext);   // CYCLE_TRACER: the new tracers are the other buffers
       std::swap(m->f.salt, m->f.saltNext);
     } else if (physPhi) TIMED(K_MOM, launch_mom_step(m->d, m->p, m->f, m->d_ctr, m->stream));
@@ -1668,7 +1673,7 @@ static int one_step(mgcm_model *m) {
     // EXCH(cg2d_x) + etaN in the single-workgroup CG2D's epilogue -- off by default: one CU
     // walking every 2-D point costs more than the launch it saves)
     const bool sfpFused = mg_fuse_on(MG_FUSE_SFP) && m->p.nonlinFreeSurf > 0 && m->d.nT == m->d.nTiles;
-    if (m->p.nonlinFreeSurf > 0) TIMED(K_RSTAR, update_r_star_cg2d(m, sfpFused));
+    if (m->p.nonlinFreeSurf > 0) TIMED(K_RSTAR, update_r_star_cg2d(m, sfpFused, opEarly));
     if (!sfpFused) TIMED(K_RHS, launch_sfp_rhs(m->d, m->p, m->f, m->stream));
     if (thermoLate && thermoAtEnv == 2 && fork_thermo()) return -1;
     const bool etaFused = mg_fuse_on(MG_FUSE_ETA) && cg2d_fuses_eta(m);
