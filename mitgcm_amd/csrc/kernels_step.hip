@@ -110,10 +110,12 @@ static void launch_l1(const Dims &d, const Params &p, const Fields &f, int nbDel
 template <bool GM, bool FF4>
 __global__ void __launch_bounds__(256) k_dt_l2(Dims d, Params p, Fields f, TracerArgs aT, TracerArgs aS,
                                                const int *iterPtr, int nbMom, int nbTr, const long *__restrict__ srcOf,
-                                               int nbPc) {
+                                               int nbPc, int nbOp) {
   int lb = mg_xcd_block();
   if (lb < nbPc) { ucg2d_p_point(d, p, f, srcOf, lb); return; }
   lb -= nbPc;
+  if (lb < nbOp) { ucg2d_op_point(d, p, f, lb); return; }
+  lb -= nbOp;
   if (lb < nbMom) {
     if constexpr (FF4) mom_ff4_body(d, p, f, iterPtr, lb);
     else if (lb & 1) mom_step_point<false, 2>(d, p, f, iterPtr, lb >> 1);
@@ -125,8 +127,11 @@ __global__ void __launch_bounds__(256) k_dt_l2(Dims d, Params p, Fields f, Trace
   else tracer_rhs_body<GM>(d, p, f, aS, iterPtr, lb - nbTr);
 }
 __global__ void __launch_bounds__(256) k_dt_l3(Dims d, Params p, Fields f, TracerArgs aT, TracerArgs aS,
-                                               const int *iterPtr, int nc, int nbCd, int nbImp) {
+                                               const int *iterPtr, int nc, int nbCd, int nbImp, const long *__restrict__ srcOf,
+                                               int nbPc) {
   int lb = mg_xcd_block();
+  if (lb < nbPc) { ucg2d_p_point(d, p, f, srcOf, lb); return; }
+  lb -= nbPc;
   if (lb < nbCd) { cd_scheme_body(d, p, f, iterPtr, lb); return; }
   lb -= nbCd;
   if (lb < nbImp) tracer_impl_body(d, p, f, aT, nc, lb);
@@ -219,20 +224,25 @@ hipError_t launch_dyn_thermo(const Dims &d, const Params &p, const Fields &f, co
   const int nbDel = del2_needed(p) ? (int)mg_plane_blocks(d.nx, d.ny, d.nT * d.Nr) : 0;
   const int nbTr = (int)mg_plane_blocks(d.sNx, d.sNy, d.nT * d.Nr);
   if (dyn_thermo_takes_gm(p)) {
+    // MGCM_OPE_AT (read per launch, A/B): 1 operator in grid 1, preconditioner in grid 2
+    // (default); 2 operator in grid 2, preconditioner in grid 3
+    const int opeAt = getenv("MGCM_OPE_AT") ? atoi(getenv("MGCM_OPE_AT")) : 1;
     const int nbU = srcOf ? ucg2d_blocks(d) : 0;
-    launch_l1(d, p, f, nbDel, s, nbU);
+    const int nbOp1 = opeAt == 2 ? 0 : nbU, nbPc2 = opeAt == 2 ? 0 : nbU, nbOp2 = opeAt == 2 ? nbU : 0,
+              nbPc3 = opeAt == 2 ? nbU : 0;
+    launch_l1(d, p, f, nbDel, s, nbOp1);
     const bool ff4 = mom_ff4_on(true);
     const int nbMom = ff4 ? mom_ff4_blocks(d) : 2 * (int)mg_plane_blocks(d.nx, d.ny, d.nT * d.Nr);
     auto l2 = ff4 ? k_dt_l2<true, true> : k_dt_l2<true, false>;
-    hipLaunchKernelGGL(l2, dim3((unsigned)(nbU + nbMom + 2 * nbTr)), blk, 0, s, d, p, f, aT, aS, iterPtr, nbMom, nbTr, srcOf,
-                       nbU);
+    hipLaunchKernelGGL(l2, dim3((unsigned)(nbPc2 + nbOp2 + nbMom + 2 * nbTr)), blk, 0, s, d, p, f, aT, aS, iterPtr, nbMom, nbTr,
+                       srcOf, nbPc2, nbOp2);
     const long ncolTr = (long)d.sNx * d.sNy * d.nT;
     const int ncTr = mg_colf_nc(ncolTr, d.Nr, 3);
     const int nbImp = (int)mg_colf_blocks(ncolTr, ncTr);
     const int nbCd = (int)mg_plane_blocks(d.nx - 2, d.ny - 2, d.nT * d.Nr);
     MG_ALLOW_LDS(k_dt_l3);
-    hipLaunchKernelGGL(k_dt_l3, dim3((unsigned)(nbCd + 2 * nbImp)), blk, mg_colf_lds(d.Nr, ncTr, 3), s, d, p, f, aT, aS,
-                       iterPtr, ncTr, nbCd, nbImp);
+    hipLaunchKernelGGL(k_dt_l3, dim3((unsigned)(nbPc3 + nbCd + 2 * nbImp)), blk, mg_colf_lds(d.Nr, ncTr, 3), s, d, p, f, aT,
+                       aS, iterPtr, ncTr, nbCd, nbImp, srcOf, nbPc3);
     return hipGetLastError();
   }
   if (srcOf) return hipErrorInvalidValue;   // (the operator rides only in the default layout)

@@ -484,12 +484,15 @@ class ShardedModel:
                 ck(L.mgcm_step_phase(h, 2), "mgcm_step_phase(2)")
         if self.m.params.get("exactConserv", 0):
             self._gather_2d("cg2d_b")
+        # the velocities' halo sources (u, v, w, the CD-scheme copies, phi) are final after the
+        # correction step: they leave before the end of FORWARD_STEP's 2-D work (EXCH eta +
+        # UPDATE_ETAH, CALC_R_STAR -- phase 3 touches no 3-D field) and are received after it,
+        # the reference's PUT/send -> recv/GET split (exch2_rx1_cube.template:118-247)
+        fin_rest = self._halo(2 if fin_tracers is not None else 0, start_only=True)
         ck(L.mgcm_step_phase(h, 3), "mgcm_step_phase(3)")
         if fin_tracers is not None:
             fin_tracers()
-            self._halo(2)
-        else:
-            self._halo(0)
+        fin_rest()
         if self.stagger:
             # DO_STAGGER_FIELDS_EXCHANGES, then THERMODYNAMICS with the new velocities
             ck(L.mgcm_step_phase(h, 5), "mgcm_step_phase(5)")

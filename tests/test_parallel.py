@@ -249,3 +249,82 @@ def test_global_sum_tile_order_independent_of_world(world, nTiles):
     for r, (g, s) in out.items():
         assert np.array_equal(g, allp), r
         assert s == ref, (r, s, ref)
+
+
+def _overlap_worker(rank, world, port, q):
+    """The sharded step's exchange order (ShardedModel.step, THERMODYNAMICS forked): the
+    tracers' halo batch posted at the join, a 2-D all-gather, the velocities' batch posted
+    after the correction step, work in between, then both finished -- two outstanding
+    isend/irecv batches per peer pair.  Every field's halo must equal the single-process
+    EXCH, as with one exchange at the step's end."""
+    from mitgcm_amd.parallel import start_exchange
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        topo = LatLonTopology(6, 5, 2, 2, 3, 2)
+        nT, ny, nx = topo.nTiles, topo.ny, topo.nx
+        n2 = nx * ny
+        rng = np.random.default_rng(5)
+        truth = [rng.standard_normal((nT, ny, nx)) for _ in range(4)]   # theta, salt | u, v
+        expect = [topo.exchange(a[:, None])[:, 0] for a in truth]
+        part = TilePartition(nT, world)
+        t0, c = part.range(rank)
+        mine = []
+        for a in truth:
+            b = np.full(a.size, np.nan)
+            own = slice(t0 * n2, (t0 + c) * n2)
+            b[own] = a.reshape(-1)[own]
+            mine.append(b)
+        plan = HaloPlan(topo.src_of_point(), n2, part, rank)
+
+        def group(fields):
+            def pack(peer):
+                idx = plan.send[peer]
+                return torch.from_numpy(np.concatenate([mine[f][idx] for f in fields]))
+
+            def make_buf(peer):
+                return torch.empty(len(fields) * plan.recv[peer].size, dtype=torch.float64)
+
+            def unpack(peer, buf):
+                idx, b = plan.recv[peer], buf.numpy()
+                for n, f in enumerate(fields):
+                    mine[f][idx] = b[n * idx.size:(n + 1) * idx.size]
+            return pack, unpack, make_buf
+
+        pk, up, mk = group((0, 1))
+        fin_tr = start_exchange(dist, plan, pk, up, mk)          # at the THERMODYNAMICS join
+        eta = torch.full((part.maxT * n2,), float(rank))
+        out = [torch.empty_like(eta) for _ in range(world)]
+        dist.all_gather(out, eta)                                 # exactConserv's eta gather
+        pk, up, mk = group((2, 3))
+        fin_vel = start_exchange(dist, plan, pk, up, mk)          # after the correction step
+        work = sum(float(o[0]) for o in out)                      # phase 3 stands here
+        fin_tr()
+        fin_vel()
+        src = topo.src_of_point()
+        dst = np.arange(src.size)
+        sel = (src != dst) & (dst // n2 >= t0) & (dst // n2 < t0 + c)
+        ok = work == sum(range(world))
+        for f in range(4):
+            mine[f][dst[sel]] = mine[f][src[sel]]
+            own = slice(t0 * n2, (t0 + c) * n2)
+            ok = ok and np.array_equal(mine[f][own], expect[f].reshape(-1)[own])
+        q.put((rank, ok))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_overlapped_group_exchanges(world):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_overlap_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=120) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for rank, ok in res:
+        assert ok, "rank %d: overlapped tracer / velocity exchanges differ from the single-process EXCH" % rank
