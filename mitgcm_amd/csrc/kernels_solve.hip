@@ -1401,6 +1401,9 @@ __global__ void __launch_bounds__(256) k_exch_etaH(Dims d, Params p, Fields f, c
 // exchange source of each point -- exactly the etaN that SOLVE_FOR_PRESSURE's EXCH_XY_RL +
 // etaN = recip_Bo*cg2d_x (k_exch_eta) stores -- so k_exch_eta runs beside this kernel instead
 // of before it (it writes only etaN and cg2d_x's halo, which this kernel then does not read).
+// UNR: the level loop of the step path unrolled UNR times (every level's loads of a thread in
+// flight together instead of one memory round trip per level; MGCM_CORR_UNR)
+template <int UNR>
 __global__ void __launch_bounds__(256) k_corr_cont(Dims d, Params p, Fields f, int atInit, int nc,
                                                    const long *__restrict__ etaSrc) {
   extern __shared__ __attribute__((aligned(16))) double lds[];
@@ -1439,6 +1442,7 @@ __global__ void __launch_bounds__(256) k_corr_cont(Dims d, Params p, Fields f, i
     };
     // the column's surface-pressure gradients (2-D, the same at every level)
     const double pX0 = phiX(i, j), pX1 = phiX(i + 1, j), pY0 = phiY(i, j), pY1 = phiY(i, j + 1);
+#pragma unroll UNR
     MG_COLF_K(k) {
       const int me = (k - 1) * NC_ + cc;
       auto uCor = [&](int ii, double phiSurfX) {
@@ -1895,9 +1899,14 @@ hipError_t launch_corr_cont(const Dims &d, const Params &p, const Fields &f, int
                        p, f, nc2, etaSrc);
     return hipGetLastError();
   }
-  MG_ALLOW_LDS(k_corr_cont);
-  hipLaunchKernelGGL(k_corr_cont, dim3(mg_colf_blocks(ncol, nc)), dim3(256), mg_colf_lds(d.Nr, nc, nArr), s, d, p, f,
-                     atInit, nc, etaSrc);
+  // MGCM_CORR_UNR = 1 | 2 | 4 (read per launch, A/B)
+  const int unr = getenv("MGCM_CORR_UNR") ? atoi(getenv("MGCM_CORR_UNR")) : 1;
+  auto kern = unr == 4 ? k_corr_cont<4> : unr == 2 ? k_corr_cont<2> : k_corr_cont<1>;
+  MG_ALLOW_LDS(k_corr_cont<1>);
+  MG_ALLOW_LDS(k_corr_cont<2>);
+  MG_ALLOW_LDS(k_corr_cont<4>);
+  hipLaunchKernelGGL(kern, dim3(mg_colf_blocks(ncol, nc)), dim3(256), mg_colf_lds(d.Nr, nc, nArr), s, d, p, f, atInit, nc,
+                     etaSrc);
   return hipGetLastError();
 }
 
