@@ -263,14 +263,16 @@ inline unsigned mg_colf_blocks(long ncols, int nc) { return (unsigned)((ncols + 
 // MG_FUSE_DT THERMODYNAMICS' tracer kernels folded into DYNAMICS' launches instead of a
 // second stream beside them (kernels_step.hip; early fork only, small grids), MG_FUSE_ETAX
 // no separate EXCH(cg2d_x) + etaN under exactConserv (one_step), MG_FUSE_OPE UPDATE_CG2D's
-// operator and preconditioner in the fold's first two grids (ucg2d.h; r*, with MG_FUSE_DT).
+// operator and preconditioner in the fold's first two grids (ucg2d.h; r*, with MG_FUSE_DT),
+// MG_FUSE_RING the VI path's halo-ring AB2 on the tracers' stream (late fork, one_step).
 enum { MG_FUSE_SFP = 1, MG_FUSE_ETA = 2, MG_FUSE_PHI = 4, MG_FUSE_END = 8, MG_FUSE_PHYS = 16, MG_FUSE_ETAA = 32,
-       MG_FUSE_TREX = 64, MG_FUSE_DT = 128, MG_FUSE_ETAX = 256, MG_FUSE_TCG = 512, MG_FUSE_OPE = 1024 };
+       MG_FUSE_TREX = 64, MG_FUSE_DT = 128, MG_FUSE_ETAX = 256, MG_FUSE_TCG = 512, MG_FUSE_OPE = 1024,
+       MG_FUSE_RING = 2048 };
 inline bool mg_fuse_on(int bit) {
   // read per call (tests switch it per model)
   const int mask = getenv("MGCM_STEP_FUSE") ? atoi(getenv("MGCM_STEP_FUSE"))
                                             : MG_FUSE_SFP | MG_FUSE_PHI | MG_FUSE_END | MG_FUSE_DT | MG_FUSE_ETAX |
-                                                MG_FUSE_OPE;
+                                                MG_FUSE_OPE | MG_FUSE_RING;
   return (mask & bit) != 0;
 }
 // Horizontal launch fusion of two independent latency-bound kernels into one grid: on the

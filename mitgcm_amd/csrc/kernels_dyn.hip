@@ -2481,12 +2481,30 @@ hipError_t launch_phi_hyd(const Dims &d, const Params &p, const Fields &f, hipSt
 static hipError_t launch_mom_tail(const Dims &d, const Params &p, const Fields &f, const int *iterPtr, hipStream_t s);
 // DYNAMICS after CALC_PHI_HYD (launch_phi_hyd): momentum tendencies, TIMESTEP, AB2, CD scheme,
 // implicit vertical viscosity
-hipError_t launch_mom_step(const Dims &d, const Params &p, const Fields &f, const int *iterPtr, hipStream_t s) {
+// The VI path's ADAMS_BASHFORTH2 on the halo ring (k_mom_halo_ab) as a launch of its own:
+// nothing of the step reads the ring's gU/gV before the end-of-step exchange overwrites the
+// halos, and nothing else of DYNAMICS writes it (the CD scheme excepted, whose range reaches
+// it), so the resident step may run it on the second stream beside the pressure solve
+// (one_step, MG_FUSE_RING).  ring = false: launch_mom_step leaves it to launch_mom_ring.
+static bool vi_march_path(const Dims &d, const Params &p) {
+  static const bool viPoint = getenv("MGCM_VI_POINT") != nullptr;
+  return p.vectorInvariantMomentum && !viPoint && d.OLx >= 2 && d.OLy >= 2 && p.selectVortScheme <= 2;
+}
+bool mom_ring_separable(const Dims &d, const Params &p) {
+  return vi_march_path(d, p) && !p.useCDscheme && 2 * (d.OLy - 1) * d.nx + (d.sNy + 2) * 2 * (d.OLx - 1) > 0;
+}
+hipError_t launch_mom_ring(const Dims &d, const Params &p, const Fields &f, const int *iterPtr, hipStream_t s) {
+  const int ring = 2 * (d.OLy - 1) * d.nx + (d.sNy + 2) * 2 * (d.OLx - 1);
+  if (ring > 0)
+    hipLaunchKernelGGL(k_mom_halo_ab, dim3((unsigned)((ring + 255) / 256), d.Nr, d.nT), dim3(256), 0, s, d, p, f, iterPtr);
+  return hipGetLastError();
+}
+hipError_t launch_mom_step(const Dims &d, const Params &p, const Fields &f, const int *iterPtr, hipStream_t s, bool ring) {
   if (del2_needed(p) && !phi_del2_fused(d, p))
     hipLaunchKernelGGL(k_del2uv, dim3(mg_plane_blocks(d.nx, d.ny, d.nT * d.Nr)), dim3(MG_PLANE_THREADS), 0, s, d, p, f);
-  // MOM_VECINV or MOM_FLUXFORM: separate instantiations (no register-pressure coupling)
-  static const bool viPoint = getenv("MGCM_VI_POINT") != nullptr;   // the per-point form, for comparison
-  if (p.vectorInvariantMomentum && !viPoint && d.OLx >= 2 && d.OLy >= 2 && p.selectVortScheme <= 2) {
+  // MOM_VECINV or MOM_FLUXFORM: separate instantiations (no register-pressure coupling);
+  // MGCM_VI_POINT: the per-point form, for comparison
+  if (vi_march_path(d, p)) {
     int BX, BY;
     vi_tile_shape(d, BX, BY);
     const int nbx = (d.sNx + 2 + BX - 1) / BX, nby = (d.sNy + 2 + BY - 1) / BY;
@@ -2519,10 +2537,7 @@ hipError_t launch_mom_step(const Dims &d, const Params &p, const Fields &f, cons
       hipLaunchKernelGGL(k_mom_vi_tiled, dim3((unsigned)(nbx * nby * d.nT * nkc)), dim3(VT_NT), 0, s, d, p, f, iterPtr, BX,
                          BY, nbx, nby, KC, nkc);
     }
-    const int ring = 2 * (d.OLy - 1) * d.nx + (d.sNy + 2) * 2 * (d.OLx - 1);
-    if (ring > 0)
-      hipLaunchKernelGGL(k_mom_halo_ab, dim3((unsigned)((ring + 255) / 256), d.Nr, d.nT), dim3(256), 0, s, d, p, f,
-                         iterPtr);
+    if (ring || p.useCDscheme) launch_mom_ring(d, p, f, iterPtr, s);
   } else if (p.vectorInvariantMomentum)
     hipLaunchKernelGGL(k_mom_step<true>, dim3(mg_plane_blocks(d.nx, d.ny, d.nT * d.Nr)), dim3(MG_PLANE_THREADS), 0, s,
                        d, p, f, iterPtr);

@@ -21,7 +21,9 @@
 #include "common.h"
 
 namespace mgcm {
-hipError_t launch_mom_step(const Dims &, const Params &, const Fields &, const int *, hipStream_t);
+hipError_t launch_mom_step(const Dims &, const Params &, const Fields &, const int *, hipStream_t, bool ring = true);
+bool mom_ring_separable(const Dims &, const Params &);
+hipError_t launch_mom_ring(const Dims &, const Params &, const Fields &, const int *, hipStream_t);
 hipError_t launch_phi_hyd(const Dims &, const Params &, const Fields &, hipStream_t);
 bool phys_phi_fusable(const Dims &, const Params &);
 hipError_t launch_phys_phi(const Dims &, const Params &, const Fields &, const int *, hipStream_t);
@@ -1343,11 +1345,14 @@ static int check_ready(mgcm_model *m) {
     if (e_ != hipSuccess) return set_err("%s: %s", KNAMES[K], hipGetErrorString(e_)); \
   } while (0)
 
+static int dynamics_on(mgcm_model *m, bool ring) {
+  TIMED(K_PHI, launch_phi_hyd(m->d, m->p, m->f, m->stream));   // CALC_PHI_HYD (dynamics.F:462)
+  TIMED(K_MOM, launch_mom_step(m->d, m->p, m->f, m->d_ctr, m->stream, ring));
+  return 0;
+}
 int mgcm_dynamics(mgcm_model *m) {
   if (check_ready(m)) return -1;
-  TIMED(K_PHI, launch_phi_hyd(m->d, m->p, m->f, m->stream));   // CALC_PHI_HYD (dynamics.F:462)
-  TIMED(K_MOM, launch_mom_step(m->d, m->p, m->f, m->d_ctr, m->stream));
-  return 0;
+  return dynamics_on(m, true);
 }
 
 static TracerArgs tracer_args(mgcm_model *m, bool salt) {
@@ -1583,9 +1588,13 @@ static int one_step(mgcm_model *m) {
   // salt, which nothing before it reads -- so the end-of-step exchange carries only the
   // velocities (MG_FUSE_TREX)
   const bool trEx = lateJoin && thermoAtEnv >= 1 && mg_fuse_on(MG_FUSE_TREX);
+  // the VI path's halo-ring AB2 (launch_mom_ring) on the tracers' stream with them, when they
+  // fork right after DYNAMICS (MG_FUSE_RING; joined with them before the correction step)
+  const bool ringAside = thermoLate && thermoAtEnv == 1 && mom_ring_separable(m->d, m->p) && mg_fuse_on(MG_FUSE_RING);
   auto fork_thermo = [&]() -> int {
     HIPCHK(hipEventRecord(m->evFork, m->stream));
     HIPCHK(hipStreamWaitEvent(m->stream2, m->evFork, 0));
+    if (ringAside) HIPCHK(launch_mom_ring(m->d, m->p, m->f, m->d_ctr, m->stream2));
     if (tracers_on(m, m->stream2)) return -1;
     if (trEx) {
       const XFields xt = blocking_fields(m, 2);
@@ -1660,11 +1669,11 @@ static int one_step(mgcm_model *m) {
       TIMED(K_MOM, launch_dyn_thermo(m->d, m->p, m->f, aT, aS, m->d_ctr, m->stream, opEarly ? m->d_srcOf : nullptr));
       std::swap(m->f.theta, m->f.thetaNext);   // CYCLE_TRACER: the new tracers are the other buffers
       std::swap(m->f.salt, m->f.saltNext);
-    } else if (physPhi) TIMED(K_MOM, launch_mom_step(m->d, m->p, m->f, m->d_ctr, m->stream));
+    } else if (physPhi) TIMED(K_MOM, launch_mom_step(m->d, m->p, m->f, m->d_ctr, m->stream, !ringAside));
     else if (gmPhi) {
       TIMED(K_PHI, launch_gm_phi(m->d, m->p, m->f, m->stream));
-      TIMED(K_MOM, launch_mom_step(m->d, m->p, m->f, m->d_ctr, m->stream));
-    } else if (mgcm_dynamics(m)) return -1;
+      TIMED(K_MOM, launch_mom_step(m->d, m->p, m->f, m->d_ctr, m->stream, !ringAside));
+    } else if (dynamics_on(m, !ringAside)) return -1;
     if (thermoLate && thermoAtEnv == 1 && fork_thermo()) return -1;
     if (tcgFork) HIPCHK(hipStreamWaitEvent(m->stream, m->evSnap, 0));   // the copy before hFac is rewritten
     else if (fork && !lateJoin && !dtFused) HIPCHK(hipStreamWaitEvent(m->stream, m->evJoin, 0));
