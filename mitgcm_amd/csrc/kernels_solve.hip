@@ -134,6 +134,8 @@ __device__ __forceinline__ double ref_sum(const double (&v)[PPT], double *term_l
 // (solve_for_pressure.F:142-151); with the CD scheme etaNm1 = etaN
 // (solve_for_pressure.F:126-128) and CD_CODE_SCHEME's uNM1, vNM1 = u, v
 // (cd_code_scheme.F:228-234) are saved here, after every k_cd_scheme read.
+// UNR: the flux level loop unrolled UNR times (MGCM_SFP_UNR, A/B)
+template <int UNR>
 __global__ void __launch_bounds__(256) k_sfp_rhs(Dims d, Params p, Fields f, int nc) {
   extern __shared__ __attribute__((aligned(16))) double lds[];
   MG_COLF(1 - d.OLx, d.nx, 1 - d.OLy, d.ny, nc)
@@ -146,9 +148,11 @@ __global__ void __launch_bounds__(256) k_sfp_rhs(Dims d, Params p, Fields f, int
     f.uNM1[q3] = f.uVel[q3];
     f.vNM1[q3] = f.vVel[q3];
   }
-  if (valid && inner) MG_COLF_K(k) {
-    const int me = (k - 1) * NC_ + cc;
-    {   // CALC_DIV_GHAT flux terms of level k
+  if (valid && inner) {
+#pragma unroll UNR
+    MG_COLF_K(k) {
+      const int me = (k - 1) * NC_ + cc;
+      // CALC_DIV_GHAT flux terms of level k
       const double drF = f.drF[k - 1];
       sE[me] = f.dyG[MG_I2(d, i + 1, j, t)] * drF * f.hFacW[MG_I3(d, i + 1, j, k, t)] *
                f.gU[MG_I3(d, i + 1, j, k, t)] / p.deltaTMom;
@@ -1668,8 +1672,12 @@ __global__ void k_bump_counter(int *c, int nIncr) {
 hipError_t launch_sfp_rhs(const Dims &d, const Params &p, const Fields &f, hipStream_t s) {
   const long ncol = (long)d.nx * d.ny * d.nT;
   const int nc = mg_colf_nc(ncol, d.Nr, 4);
-  MG_ALLOW_LDS(k_sfp_rhs);
-  hipLaunchKernelGGL(k_sfp_rhs, dim3(mg_colf_blocks(ncol, nc)), dim3(256), mg_colf_lds(d.Nr, nc, 4), s, d, p, f, nc);
+  const int unr = getenv("MGCM_SFP_UNR") ? atoi(getenv("MGCM_SFP_UNR")) : 1;   // read per launch (A/B)
+  auto kern = unr == 4 ? k_sfp_rhs<4> : unr == 2 ? k_sfp_rhs<2> : k_sfp_rhs<1>;
+  MG_ALLOW_LDS(k_sfp_rhs<1>);
+  MG_ALLOW_LDS(k_sfp_rhs<2>);
+  MG_ALLOW_LDS(k_sfp_rhs<4>);
+  hipLaunchKernelGGL(kern, dim3(mg_colf_blocks(ncol, nc)), dim3(256), mg_colf_lds(d.Nr, nc, 4), s, d, p, f, nc);
   return hipGetLastError();
 }
 
