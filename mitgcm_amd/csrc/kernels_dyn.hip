@@ -1969,7 +1969,7 @@ struct VIM2 {   // HR: slots of the hFacC / wVel level rings (level kk in slot k
   do {              \
   } while (0)
 #endif
-template <int BX, int BY, unsigned C, bool PF, bool CREG, bool EARLY, int LBW, bool TAILV = false>
+template <int BX, int BY, unsigned C, bool PF, bool CREG, bool EARLY, int LBW>
 __global__ void __launch_bounds__(VT_NT, LBW) k_mom_vi_m2(Dims d, VIP<C> p, Fields f, const int *iterPtr, int nbx, int nby,
                                                       int KC, int nkc) {
   using P = VIP<C>;
@@ -2127,12 +2127,7 @@ __global__ void __launch_bounds__(VT_NT, LBW) k_mom_vi_m2(Dims d, VIP<C> p, Fiel
                             uM, k < Nr ? oU : 0.0, vM, k < Nr ? oV : 0.0, hwM, k < Nr ? oHW : 0.0, hsM, k < Nr ? oHS : 0.0};
     VIM2<BX, BY, P, false> ai{d, p, f, k, t, i0, j0, 0, 0, sU, sV, sHW, sHS, sHC, sW, s2, sKE, sVort, sHfz, sH0fz, sHDiv, c,
                               0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
-    // TAIL (IN - VT_NT <= 64 intermediate points past the first pass, e.g. 31 x 8: 288): the
-    // leftover points' five intermediates are dealt out by quantity, one wave each (wave-uniform,
-    // no divergence), instead of one wave computing all five while the other three wait at the
-    // barrier; each value is the same function of the same inputs, so the same bits
-    constexpr bool TAIL = TAILV && IN > VT_NT && IN - VT_NT <= 64 && VT_NT == 256;
-    for (int q = tid; q < (TAIL ? VT_NT : IN); q += VT_NT) {
+    for (int q = tid; q < IN; q += VT_NT) {
       const int ii = i0 + q % IW, jj = j0 + q / IW;          // vort / hFacZ grid: i0..i0+BX
       const bool ok = ii <= d.sNx + d.OLx && jj <= d.sNy + d.OLy;
       sHfz[q] = ok ? vi_hfacz(ai, d, ii, jj, k) : 0.0;
@@ -2140,19 +2135,6 @@ __global__ void __launch_bounds__(VT_NT, LBW) k_mom_vi_m2(Dims d, VIP<C> p, Fiel
       sVort[q] = ok ? vi_vort(ai, d, p, f, ii, jj, k, t) : 0.0;
       sKE[q] = vi_KE(ai, d, p, f, ii - 1, jj - 1, k, t);     // KE / hDiv grid: i0-1..i0+BX-1
       sHDiv[q] = vi_hdiv(ai, d, p, f, ii - 1, jj - 1, k, t);
-    }
-    if constexpr (TAIL) {
-      const int q = VT_NT + (tid & 63), w = __builtin_amdgcn_readfirstlane(tid >> 6);
-      if (q < IN) {
-        const int ii = i0 + q % IW, jj = j0 + q / IW;
-        const bool ok = ii <= d.sNx + d.OLx && jj <= d.sNy + d.OLy;
-        if (w == 0) sVort[q] = ok ? vi_vort(ai, d, p, f, ii, jj, k, t) : 0.0;
-        else if (w == 1) {
-          sHfz[q] = ok ? vi_hfacz(ai, d, ii, jj, k) : 0.0;
-          sH0fz[q] = ok ? vi_h0facz(ai, d, p, ii, jj, k) : 0.0;
-        } else if (w == 2) sKE[q] = vi_KE(ai, d, p, f, ii - 1, jj - 1, k, t);
-        else sHDiv[q] = vi_hdiv(ai, d, p, f, ii - 1, jj - 1, k, t);
-      }
     }
     VI_STAMP(1);
     __syncthreads();
@@ -2292,11 +2274,10 @@ constexpr unsigned VI_CODE_LLC = vi_code(1, 0, 0, 1, 1, 1, 0, 1, 1, 0, 1, 1, 1, 
 template <int BX, int BY, unsigned C, int V>
 static void vi_m2_one(const Dims &d, const VIP<C> &vp, const Fields &f, const int *iterPtr, int nbx, int nby, int KC,
                       int nkc, hipStream_t s) {
-  hipLaunchKernelGGL((k_mom_vi_m2<BX, BY, C, (V & 1) != 0, (V & 2) != 0, (V & 4) != 0, (V & 8) ? 2 : 1, (V & 16) != 0>),
+  hipLaunchKernelGGL((k_mom_vi_m2<BX, BY, C, (V & 1) != 0, (V & 2) != 0, (V & 4) != 0, (V & 8) ? 2 : 1>),
                      dim3((unsigned)(nbx * nby * d.nT * nkc)), dim3(VT_NT), 0, s, d, vp, f, iterPtr, nbx, nby, KC, nkc);
 }
-// var: bit mask, 1 PF, 2 CREG, 4 EARLY, 8 at least 2 waves per SIMD, 16 the intermediates'
-// tail dealt out by quantity over the waves (the instantiated set)
+// var: bit mask, 1 PF, 2 CREG, 4 EARLY, 8 at least 2 waves per SIMD (the instantiated set)
 template <int BX, int BY, unsigned C>
 static bool vi_m2_go(const Dims &d, const Params &p, const Fields &f, const int *iterPtr, int nbx, int nby, int KC,
                      int nkc, hipStream_t s, int var) {
@@ -2311,7 +2292,6 @@ static bool vi_m2_go(const Dims &d, const Params &p, const Fields &f, const int 
     case 11: vi_m2_one<BX, BY, C, 11>(d, vp, f, iterPtr, nbx, nby, KC, nkc, s); return true;
     case 14: vi_m2_one<BX, BY, C, 14>(d, vp, f, iterPtr, nbx, nby, KC, nkc, s); return true;
     case 15: vi_m2_one<BX, BY, C, 15>(d, vp, f, iterPtr, nbx, nby, KC, nkc, s); return true;
-    case 30: vi_m2_one<BX, BY, C, 30>(d, vp, f, iterPtr, nbx, nby, KC, nkc, s); return true;
     default: return false;
   }
 }
@@ -2321,6 +2301,8 @@ static bool vi_m2_launch(const Dims &d, const Params &p, const Fields &f, const 
                          int nby, int KC, int nkc, hipStream_t s) {
   // read per launch (tests switch them per model)
   const bool on = !getenv("MGCM_VI_M2") || atoi(getenv("MGCM_VI_M2")) != 0;
+  // (round 4, measured and dropped, profiles/r04/llc_ab/: the ring-point intermediates of the
+  // 31 x 8 block's second pass dealt out by quantity over the four waves, 459 -> 518 us)
   // MGCM_VI_M2_VAR (bit mask, vi_m2_go); default 14: the output point's metrics held in
   // registers across the march (CREG), its own HBM reads of a level issued at the level's
   // start (EARLY), registers capped for 2 waves per SIMD, level k+1 fetched after level k

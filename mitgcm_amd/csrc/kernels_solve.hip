@@ -134,8 +134,6 @@ __device__ __forceinline__ double ref_sum(const double (&v)[PPT], double *term_l
 // (solve_for_pressure.F:142-151); with the CD scheme etaNm1 = etaN
 // (solve_for_pressure.F:126-128) and CD_CODE_SCHEME's uNM1, vNM1 = u, v
 // (cd_code_scheme.F:228-234) are saved here, after every k_cd_scheme read.
-// UNR: the flux level loop unrolled UNR times (MGCM_SFP_UNR, A/B)
-template <int UNR>
 __global__ void __launch_bounds__(256) k_sfp_rhs(Dims d, Params p, Fields f, int nc) {
   extern __shared__ __attribute__((aligned(16))) double lds[];
   MG_COLF(1 - d.OLx, d.nx, 1 - d.OLy, d.ny, nc)
@@ -148,11 +146,9 @@ __global__ void __launch_bounds__(256) k_sfp_rhs(Dims d, Params p, Fields f, int
     f.uNM1[q3] = f.uVel[q3];
     f.vNM1[q3] = f.vVel[q3];
   }
-  if (valid && inner) {
-#pragma unroll UNR
-    MG_COLF_K(k) {
-      const int me = (k - 1) * NC_ + cc;
-      // CALC_DIV_GHAT flux terms of level k
+  if (valid && inner) MG_COLF_K(k) {
+    const int me = (k - 1) * NC_ + cc;
+    {   // CALC_DIV_GHAT flux terms of level k
       const double drF = f.drF[k - 1];
       sE[me] = f.dyG[MG_I2(d, i + 1, j, t)] * drF * f.hFacW[MG_I3(d, i + 1, j, k, t)] *
                f.gU[MG_I3(d, i + 1, j, k, t)] / p.deltaTMom;
@@ -1405,9 +1401,6 @@ __global__ void __launch_bounds__(256) k_exch_etaH(Dims d, Params p, Fields f, c
 // exchange source of each point -- exactly the etaN that SOLVE_FOR_PRESSURE's EXCH_XY_RL +
 // etaN = recip_Bo*cg2d_x (k_exch_eta) stores -- so k_exch_eta runs beside this kernel instead
 // of before it (it writes only etaN and cg2d_x's halo, which this kernel then does not read).
-// UNR: the level loop of the step path unrolled UNR times (every level's loads of a thread in
-// flight together instead of one memory round trip per level; MGCM_CORR_UNR)
-template <int UNR>
 __global__ void __launch_bounds__(256) k_corr_cont(Dims d, Params p, Fields f, int atInit, int nc,
                                                    const long *__restrict__ etaSrc) {
   extern __shared__ __attribute__((aligned(16))) double lds[];
@@ -1446,7 +1439,6 @@ __global__ void __launch_bounds__(256) k_corr_cont(Dims d, Params p, Fields f, i
     };
     // the column's surface-pressure gradients (2-D, the same at every level)
     const double pX0 = phiX(i, j), pX1 = phiX(i + 1, j), pY0 = phiY(i, j), pY1 = phiY(i, j + 1);
-#pragma unroll UNR
     MG_COLF_K(k) {
       const int me = (k - 1) * NC_ + cc;
       auto uCor = [&](int ii, double phiSurfX) {
@@ -1672,12 +1664,8 @@ __global__ void k_bump_counter(int *c, int nIncr) {
 hipError_t launch_sfp_rhs(const Dims &d, const Params &p, const Fields &f, hipStream_t s) {
   const long ncol = (long)d.nx * d.ny * d.nT;
   const int nc = mg_colf_nc(ncol, d.Nr, 4);
-  const int unr = getenv("MGCM_SFP_UNR") ? atoi(getenv("MGCM_SFP_UNR")) : 1;   // read per launch (A/B)
-  auto kern = unr == 4 ? k_sfp_rhs<4> : unr == 2 ? k_sfp_rhs<2> : k_sfp_rhs<1>;
-  MG_ALLOW_LDS(k_sfp_rhs<1>);
-  MG_ALLOW_LDS(k_sfp_rhs<2>);
-  MG_ALLOW_LDS(k_sfp_rhs<4>);
-  hipLaunchKernelGGL(kern, dim3(mg_colf_blocks(ncol, nc)), dim3(256), mg_colf_lds(d.Nr, nc, 4), s, d, p, f, nc);
+  MG_ALLOW_LDS(k_sfp_rhs);
+  hipLaunchKernelGGL(k_sfp_rhs, dim3(mg_colf_blocks(ncol, nc)), dim3(256), mg_colf_lds(d.Nr, nc, 4), s, d, p, f, nc);
   return hipGetLastError();
 }
 
@@ -1907,14 +1895,9 @@ hipError_t launch_corr_cont(const Dims &d, const Params &p, const Fields &f, int
                        p, f, nc2, etaSrc);
     return hipGetLastError();
   }
-  // MGCM_CORR_UNR = 1 | 2 | 4 (read per launch, A/B)
-  const int unr = getenv("MGCM_CORR_UNR") ? atoi(getenv("MGCM_CORR_UNR")) : 1;
-  auto kern = unr == 4 ? k_corr_cont<4> : unr == 2 ? k_corr_cont<2> : k_corr_cont<1>;
-  MG_ALLOW_LDS(k_corr_cont<1>);
-  MG_ALLOW_LDS(k_corr_cont<2>);
-  MG_ALLOW_LDS(k_corr_cont<4>);
-  hipLaunchKernelGGL(kern, dim3(mg_colf_blocks(ncol, nc)), dim3(256), mg_colf_lds(d.Nr, nc, nArr), s, d, p, f, atInit, nc,
-                     etaSrc);
+  MG_ALLOW_LDS(k_corr_cont);
+  hipLaunchKernelGGL(k_corr_cont, dim3(mg_colf_blocks(ncol, nc)), dim3(256), mg_colf_lds(d.Nr, nc, nArr), s, d, p, f,
+                     atInit, nc, etaSrc);
   return hipGetLastError();
 }
 

@@ -64,8 +64,9 @@ __global__ void __launch_bounds__(256) k_dt_back(Dims d, Params p, Fields f, Tra
 //   1: GMREDI_CALC_TENSOR | CALC_PHI_HYD | del2uv
 //   2: MOM_FLUXFORM U | V | rhs(theta) | rhs(salt)
 //   3: CD_CODE_SCHEME | implicit solve (theta) | (salt)
-// and under r* with MG_FUSE_OPE UPDATE_CG2D's operator (nbOp blocks, ucg2d.h) at the head of 1,
-// its preconditioner (nbPc blocks) at the tail of 2 -- the operator of the step, built early
+// and under r* with MG_FUSE_OPE UPDATE_CG2D's operator (nbOp blocks, ucg2d.h) and its
+// preconditioner (nbPc blocks) at the head of 2 and 3 (MGCM_OPE_AT=1: 1 and 2) -- the
+// operator of the step, built early
 __global__ void __launch_bounds__(256) k_dt_l1(Dims d, Params p, Fields f, int nc, int nbGm, int nbPhi, int nbOp) {
   int lb = mg_xcd_block();
   if (lb < nbOp) { ucg2d_op_point(d, p, f, lb); return; }
@@ -224,9 +225,11 @@ hipError_t launch_dyn_thermo(const Dims &d, const Params &p, const Fields &f, co
   const int nbDel = del2_needed(p) ? (int)mg_plane_blocks(d.nx, d.ny, d.nT * d.Nr) : 0;
   const int nbTr = (int)mg_plane_blocks(d.sNx, d.sNy, d.nT * d.Nr);
   if (dyn_thermo_takes_gm(p)) {
-    // MGCM_OPE_AT (read per launch, A/B): 1 operator in grid 1, preconditioner in grid 2
-    // (default); 2 operator in grid 2, preconditioner in grid 3
-    const int opeAt = getenv("MGCM_OPE_AT") ? atoi(getenv("MGCM_OPE_AT")) : 1;
+    // MGCM_OPE_AT (read per launch, A/B): 2 operator in grid 2, preconditioner in grid 3 (the
+    // default: config 2 0.2821-0.2832 ms/step), 1 operator in grid 1, preconditioner in grid 2
+    // (0.2852-0.2857 on the same box; profiles/r04/ope_at/) -- the longest grid (the momentum
+    // chain) hides the operator's blocks best
+    const int opeAt = getenv("MGCM_OPE_AT") ? atoi(getenv("MGCM_OPE_AT")) : 2;
     const int nbU = srcOf ? ucg2d_blocks(d) : 0;
     const int nbOp1 = opeAt == 2 ? 0 : nbU, nbPc2 = opeAt == 2 ? 0 : nbU, nbOp2 = opeAt == 2 ? nbU : 0,
               nbPc3 = opeAt == 2 ? nbU : 0;
