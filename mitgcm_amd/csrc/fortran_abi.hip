@@ -65,6 +65,11 @@
 
 #include "../../include/mitgcm_amd.h"
 
+namespace mgcm {   // model.hip: the registered host ranges host<->device copies split at
+void mg_host_ranges_set(const uintptr_t *lo, const uintptr_t *hi, size_t n);
+hipError_t mg_host_copy(void *dst, const void *src, size_t bytes, hipMemcpyKind kind, hipStream_t s);
+}
+
 namespace {
 
 struct Bound {
@@ -366,6 +371,9 @@ void register_host() {
     return;
   }
   g.hostRegistered = true;
+  std::vector<uintptr_t> lo, hi;
+  for (auto &r : merged) { lo.push_back(r.first); hi.push_back(r.second); }
+  mgcm::mg_host_ranges_set(lo.data(), hi.data(), merged.size());
   fprintf(stderr, "MGCM_AMD: state pages registered for DMA: %zu ranges, %.1f MB\n", merged.size(), bytes / 1e6);
 }
 
@@ -391,8 +399,8 @@ void download(const char *where) {
         const double *dp = mgcm_device_ptr(s.m, b.name.c_str());
         if (!dp) die(where);
         hipchk(hipSetDevice(s.dev), where);
-        hipchk(hipMemcpyAsync(dst + s.t0 * per, dp + s.t0 * per, (size_t)s.nT * per * sizeof(double),
-                              hipMemcpyDeviceToHost, stream_of(s)),
+        hipchk(mgcm::mg_host_copy(dst + s.t0 * per, dp + s.t0 * per, (size_t)s.nT * per * sizeof(double),
+                                  hipMemcpyDeviceToHost, stream_of(s)),
                where);
       }
       continue;
@@ -400,7 +408,7 @@ void download(const char *where) {
     const double *dp = mgcm_device_ptr(g.m, b.name.c_str());
     if (!dp) die(where);
     hipchk(hipSetDevice(g.sh[0].dev), where);
-    hipchk(hipMemcpyAsync(dst, dp, (size_t)b.count * sizeof(double), hipMemcpyDeviceToHost, stream_of(g.sh[0])),
+    hipchk(mgcm::mg_host_copy(dst, dp, (size_t)b.count * sizeof(double), hipMemcpyDeviceToHost, stream_of(g.sh[0])),
            where);
   }
   sync_all(where);

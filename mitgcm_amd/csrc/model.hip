@@ -21,6 +21,37 @@
 #include "common.h"
 
 namespace mgcm {
+// Host ranges the Fortran mirror registered for DMA (fortran_abi.hip register_host: the
+// page-rounded extents of its bound COMMON arrays).  An unbound host array that shares an
+// edge page is then partly registered, and the runtime refuses a copy that spans the edge of
+// a registered range ("invalid argument"): mg_host_copy splits a host<->device copy at every
+// registered-range edge, so each piece lies wholly inside or wholly outside one.
+static std::vector<std::pair<uintptr_t, uintptr_t>> g_hostReg;
+void mg_host_ranges_set(const uintptr_t *lo, const uintptr_t *hi, size_t n) {
+  g_hostReg.clear();
+  for (size_t i = 0; i < n; i++) g_hostReg.push_back({lo[i], hi[i]});
+  std::sort(g_hostReg.begin(), g_hostReg.end());
+}
+hipError_t mg_host_copy(void *dst, const void *src, size_t bytes, hipMemcpyKind kind, hipStream_t s) {
+  if (g_hostReg.empty() || bytes == 0) return hipMemcpyAsync(dst, src, bytes, kind, s);
+  const uintptr_t h = (uintptr_t)(kind == hipMemcpyHostToDevice ? src : dst), end = h + bytes;
+  size_t off = 0;
+  while (h + off < end) {
+    const uintptr_t cur = h + off;
+    uintptr_t cut = end;
+    for (const auto &r : g_hostReg) {
+      if (r.first > cur && r.first < cut) cut = r.first;
+      if (r.second > cur && r.second < cut) cut = r.second;
+    }
+    const hipError_t e = hipMemcpyAsync((char *)dst + off, (const char *)src + off, cut - cur, kind, s);
+    if (e != hipSuccess) return e;
+    off += cut - cur;
+  }
+  return hipSuccess;
+}
+}  // namespace mgcm
+
+namespace mgcm {
 hipError_t launch_mom_step(const Dims &, const Params &, const Fields &, const int *, hipStream_t, bool ring = true);
 bool mom_ring_separable(const Dims &, const Params &);
 hipError_t launch_mom_ring(const Dims &, const Params &, const Fields &, const int *, hipStream_t);
@@ -997,7 +1028,7 @@ int mgcm_put(mgcm_model *m, const char *name, const double *host, long count) {
   const long n = field_count(m, fd->kind);
   if (count > n || count <= 0) return set_err("mgcm_put: %s count %ld > %ld", name, count, n);
   HIPCHK(hipSetDevice(m->device));
-  HIPCHK(hipMemcpyAsync(field_ptr(m, fd), host, count * sizeof(double), hipMemcpyHostToDevice, m->stream));
+  HIPCHK(mg_host_copy(field_ptr(m, fd), host, count * sizeof(double), hipMemcpyHostToDevice, m->stream));
   HIPCHK(hipStreamSynchronize(m->stream));
   return 0;
 }
@@ -1091,7 +1122,7 @@ int mgcm_get(mgcm_model *m, const char *name, double *host, long count) {
   const long n = field_count(m, fd->kind);
   if (count > n || count <= 0) return set_err("mgcm_get: %s count %ld > %ld", name, count, n);
   HIPCHK(hipSetDevice(m->device));
-  HIPCHK(hipMemcpyAsync(host, field_ptr(m, fd), count * sizeof(double), hipMemcpyDeviceToHost, m->stream));
+  HIPCHK(mg_host_copy(host, field_ptr(m, fd), count * sizeof(double), hipMemcpyDeviceToHost, m->stream));
   HIPCHK(hipStreamSynchronize(m->stream));
   return 0;
 }
@@ -1511,7 +1542,7 @@ int mgcm_exchange_host(mgcm_model *m, double *u, double *v, int nz, int vector, 
   const size_t bytes = (size_t)nz * m->d.n2 * m->d.nTiles * sizeof(double);
   double *host[2] = {u, v};
   for (int c = 0; c < 2; c++)
-    if (host[c]) HIPCHK(hipMemcpyAsync(m->exchBuf[c], host[c], bytes, hipMemcpyHostToDevice, m->stream));
+    if (host[c]) HIPCHK(mg_host_copy(m->exchBuf[c], host[c], bytes, hipMemcpyHostToDevice, m->stream));
   // every tile's halo, also when this model steps a tile subset (the host array is the domain)
   const long *hmap = m->d_haloAll ? m->d_haloAll : m->d_halo;
   const int nh = m->d_haloAll ? m->nHaloAll : m->nHalo;
@@ -1524,7 +1555,7 @@ int mgcm_exchange_host(mgcm_model *m, double *u, double *v, int nz, int vector, 
       if (host[c]) HIPCHK(launch_exchange(m->d, m->exchBuf[c], hmap, nh, nz, m->stream));
   }
   for (int c = 0; c < 2; c++)
-    if (host[c]) HIPCHK(hipMemcpyAsync(host[c], m->exchBuf[c], bytes, hipMemcpyDeviceToHost, m->stream));
+    if (host[c]) HIPCHK(mg_host_copy(host[c], m->exchBuf[c], bytes, hipMemcpyDeviceToHost, m->stream));
   HIPCHK(hipStreamSynchronize(m->stream));
   return 0;
 }
@@ -2563,8 +2594,8 @@ int mgcm_cg2d(mgcm_model *m, double *cg2d_b, double *cg2d_x, double *firstResidu
   if (check_ready(m)) return -1;
   const long n = m->d.n2 * m->d.nTiles;
   HIPCHK(hipSetDevice(m->device));
-  HIPCHK(hipMemcpyAsync(m->f.cg2d_b, cg2d_b, n * sizeof(double), hipMemcpyHostToDevice, m->stream));
-  HIPCHK(hipMemcpyAsync(m->f.cg2d_x, cg2d_x, n * sizeof(double), hipMemcpyHostToDevice, m->stream));
+  HIPCHK(mg_host_copy(m->f.cg2d_b, cg2d_b, n * sizeof(double), hipMemcpyHostToDevice, m->stream));
+  HIPCHK(mg_host_copy(m->f.cg2d_x, cg2d_x, n * sizeof(double), hipMemcpyHostToDevice, m->stream));
   HIPCHK(hipMemsetAsync(m->d_ctr + 1, 0, sizeof(int), m->stream));
   // CG2D itself (cg2d.F): useSRCGSolver selects CG2D_SR only in SOLVE_FOR_PRESSURE
   const int sr = m->p.useSRCGSolver;
@@ -2574,8 +2605,8 @@ int mgcm_cg2d(mgcm_model *m, double *cg2d_b, double *cg2d_x, double *firstResidu
   ev_end(m, K_CG2D, ev);
   m->p.useSRCGSolver = sr;
   HIPCHK(le);
-  HIPCHK(hipMemcpyAsync(cg2d_b, m->f.cg2d_b, n * sizeof(double), hipMemcpyDeviceToHost, m->stream));
-  HIPCHK(hipMemcpyAsync(cg2d_x, m->f.cg2d_x, n * sizeof(double), hipMemcpyDeviceToHost, m->stream));
+  HIPCHK(mg_host_copy(cg2d_b, m->f.cg2d_b, n * sizeof(double), hipMemcpyDeviceToHost, m->stream));
+  HIPCHK(mg_host_copy(cg2d_x, m->f.cg2d_x, n * sizeof(double), hipMemcpyDeviceToHost, m->stream));
   SolveRecord r;
   HIPCHK(hipMemcpyAsync(&r, m->d_rec, sizeof r, hipMemcpyDeviceToHost, m->stream));
   HIPCHK(hipStreamSynchronize(m->stream));
