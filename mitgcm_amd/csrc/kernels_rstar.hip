@@ -121,10 +121,17 @@ __global__ void __launch_bounds__(256) k_rstar_exch(Dims d, Params p, Fields f, 
 // read hFacW(i+1) / hFacS(j+1) of the neighbouring columns, which this pass is rewriting, so
 // they are formed from h0Fac*rStarFac there (the expression that column stores: same bits).
 // opIn = 0: the operator was built at the start of the step (ucg2d.h, MG_FUSE_OPE) -- hFac only.
+// nbPc > 0: the operator was built in an earlier launch of the step (opIn = 0) and UPDATE_CG2D's
+// preconditioner rides here, on the first nbPc logical blocks (ucg2d_p_point; the column
+// frame on the rest)
 template <bool SFP>
-__global__ void __launch_bounds__(256) k_update_r_star_cg2d_a(Dims d, Params p, Fields f, int nc, int opIn) {
+__global__ void __launch_bounds__(256) k_update_r_star_cg2d_a(Dims d, Params p, Fields f, int nc, int opIn,
+                                                              const long *__restrict__ srcOf, int nbPc) {
   extern __shared__ __attribute__((aligned(16))) double lds[];
-  MG_COLF(1 - d.OLx, d.nx, 1 - d.OLy, d.ny, nc)
+  int lb = mg_xcd_block();
+  if (lb < nbPc) { ucg2d_p_point(d, p, f, srcOf, lb); return; }
+  lb -= nbPc;
+  MG_COLF_LB(1 - d.OLx, d.nx, 1 - d.OLy, d.ny, nc, lb)
   const int NS = d.Nr * NC_;
   double *sW = lds, *sS = lds + NS;
   double *fE = lds + 2 * NS, *fW = lds + 3 * NS, *fN = lds + 4 * NS, *fS = lds + 5 * NS;   // SFP only
@@ -212,9 +219,10 @@ hipError_t launch_rstar_exch(const Dims &d, const Params &p, const Fields &f, co
   return hipGetLastError();
 }
 
-// opEarly: the operator and preconditioner were built beside DYNAMICS (launch_dyn_thermo)
+// opEarly: the operator and preconditioner were built beside DYNAMICS (launch_dyn_thermo);
+// pcHere (with opEarly): only the operator was, the preconditioner rides in this launch
 hipError_t launch_update_r_star_cg2d(const Dims &d, const Params &p, const Fields &f, const long *srcOf, hipStream_t s,
-                                     bool sfp, bool opEarly) {
+                                     bool sfp, bool opEarly, bool pcHere) {
   const long n = d.n2 * d.nTiles;
   const unsigned nb = (unsigned)((n + 255) / 256);
   const long ncol = (long)d.nx * d.ny * d.nT;
@@ -222,8 +230,10 @@ hipError_t launch_update_r_star_cg2d(const Dims &d, const Params &p, const Field
   const int nc = mg_colf_nc(ncol, d.Nr, nArr);
   MG_ALLOW_LDS(k_update_r_star_cg2d_a<false>);
   MG_ALLOW_LDS(k_update_r_star_cg2d_a<true>);
-  hipLaunchKernelGGL(sfp ? k_update_r_star_cg2d_a<true> : k_update_r_star_cg2d_a<false>, dim3(mg_colf_blocks(ncol, nc)),
-                     dim3(256), mg_colf_lds(d.Nr, nc, nArr), s, d, p, f, nc, opEarly ? 0 : 1);
+  const int nbPc = (opEarly && pcHere && p.nonlinFreeSurf > 2) ? (int)nb : 0;
+  hipLaunchKernelGGL(sfp ? k_update_r_star_cg2d_a<true> : k_update_r_star_cg2d_a<false>,
+                     dim3(mg_colf_blocks(ncol, nc) + (unsigned)nbPc), dim3(256), mg_colf_lds(d.Nr, nc, nArr), s, d, p, f, nc,
+                     opEarly ? 0 : 1, srcOf, nbPc);
   if (p.nonlinFreeSurf > 2 && !opEarly) hipLaunchKernelGGL(k_update_cg2d_p, dim3(nb), dim3(256), 0, s, d, p, f, srcOf);
   return hipGetLastError();
 }

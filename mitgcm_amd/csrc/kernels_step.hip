@@ -170,8 +170,10 @@ static void phi_frame(const Dims &d, const Params &p, int &nc, int &nArr, int &n
 bool gm_phi_fusable(const Dims &d, const Params &p) {
   return mg_hfuse(MG_FUSE_DT, d.nx, d.ny, d.nT, d.Nr) && p.useGMRedi && p.momStepping;
 }
-hipError_t launch_gm_phi(const Dims &d, const Params &p, const Fields &f, hipStream_t s) {
-  launch_l1(d, p, f, phi_del2_fused(d, p) ? (int)mg_plane_blocks(d.nx, d.ny, d.nT * d.Nr) : 0, s);
+// op: UPDATE_CG2D's operator in the same grid (ucg2d.h; its preconditioner then rides in the r*
+// pass, launch_update_r_star_cg2d pcHere)
+hipError_t launch_gm_phi(const Dims &d, const Params &p, const Fields &f, hipStream_t s, bool op) {
+  launch_l1(d, p, f, phi_del2_fused(d, p) ? (int)mg_plane_blocks(d.nx, d.ny, d.nT * d.Nr) : 0, s, op ? ucg2d_blocks(d) : 0);
   return hipGetLastError();
 }
 

@@ -90,7 +90,7 @@ hipError_t launch_calc_r_star(const Dims &, const Params &, const Fields &, cons
 hipError_t launch_rstar_exch(const Dims &, const Params &, const Fields &, const long *, bool, const XFields &, const long *,
                              int, int *, hipStream_t, int fromX = 0);
 hipError_t launch_update_r_star_cg2d(const Dims &, const Params &, const Fields &, const long *, hipStream_t, bool sfp = false,
-                                     bool opEarly = false);
+                                     bool opEarly = false, bool pcHere = false);
 hipError_t launch_halo_pack(const Dims &, const XFields &, const long *, long, double *, int, hipStream_t);
 hipError_t launch_oceanic_phys(const Dims &, const Params &, const Fields &, const int *, hipStream_t, bool gm = true);
 hipError_t launch_tracer_step(const Dims &, const Params &, const Fields &, const TracerArgs &, const int *, hipStream_t,
@@ -107,7 +107,7 @@ hipError_t launch_gm_tensor(const Dims &, const Params &, const Fields &, hipStr
 hipError_t launch_hfac_snapshot(const Dims &, const Fields &, double *, hipStream_t);
 Fields hfac_snapshot_fields(const Dims &, const Fields &, double *);
 bool gm_phi_fusable(const Dims &, const Params &);
-hipError_t launch_gm_phi(const Dims &, const Params &, const Fields &, hipStream_t);
+hipError_t launch_gm_phi(const Dims &, const Params &, const Fields &, hipStream_t, bool op = false);
 bool tracer_hpair_ok(const Dims &, const Params &, const TracerArgs &, const TracerArgs &);
 hipError_t launch_tracer_hpair(const Dims &, const Params &, const Fields &, const TracerArgs &, const TracerArgs &,
                                const int *, hipStream_t);
@@ -1214,8 +1214,8 @@ static hipError_t calc_r_star(mgcm_model *m, bool fuseEtaH = false, int fromX = 
 }
 // sfp: k_sfp_rhs fused into the r* column pass (FORWARD_STEP on the whole domain only: in a
 // tile-sharded run the r* pass covers every tile and the right-hand side this process's own)
-static hipError_t update_r_star_cg2d(mgcm_model *m, bool sfp = false, bool opEarly = false) {
-  return launch_update_r_star_cg2d(all_tiles(m->d), m->p, m->f, m->d_srcOf, m->stream, sfp, opEarly);
+static hipError_t update_r_star_cg2d(mgcm_model *m, bool sfp = false, bool opEarly = false, bool pcHere = false) {
+  return launch_update_r_star_cg2d(all_tiles(m->d), m->p, m->f, m->d_srcOf, m->stream, sfp, opEarly, pcHere);
 }
 
 int mgcm_init(mgcm_model *m) {
@@ -1695,6 +1695,13 @@ static int one_step(mgcm_model *m) {
   // the fold's first grid, the preconditioner in its second; UPDATE_R_STAR then rewrites hFac only
   const bool opEarly = dtFused && m->p.nonlinFreeSurf > 2 && dyn_thermo_takes_gm(m->p) && m->d.nT == m->d.nTiles &&
                        mg_fuse_on(MG_FUSE_OPE);
+  // the same outside the fold where GMREDI_CALC_TENSOR shares CALC_PHI_HYD's grid (gmPhi, e.g.
+  // the staggered cube): the operator there, the preconditioner in the r* pass.  Opt-in
+  // (MGCM_OPE_GM=1, read per step): bit-identical, but config 3 steps slower with it, 0.4235-0.4257
+  // against 0.4165-0.4234 ms/step (profiles/r04/ope_cs/) -- the operator's serial level loop
+  // lengthens the tensor + CALC_PHI_HYD grid more than the launch it saves
+  const bool opGm = gmPhi && m->p.nonlinFreeSurf > 2 && m->d.nT == m->d.nTiles && mg_fuse_on(MG_FUSE_OPE) &&
+                    getenv("MGCM_OPE_GM") && atoi(getenv("MGCM_OPE_GM")) == 1;
   if (m->p.momStepping) {
     if (dtFused) {
       TIMED(K_MOM, launch_dyn_thermo(m->d, m->p, m->f, aT, aS, m->d_ctr, m->stream, opEarly ? m->d_srcOf : nullptr));
@@ -1702,7 +1709,7 @@ static int one_step(mgcm_model *m) {
       std::swap(m->f.salt, m->f.saltNext);
     } else if (physPhi) TIMED(K_MOM, launch_mom_step(m->d, m->p, m->f, m->d_ctr, m->stream, !ringAside));
     else if (gmPhi) {
-      TIMED(K_PHI, launch_gm_phi(m->d, m->p, m->f, m->stream));
+      TIMED(K_PHI, launch_gm_phi(m->d, m->p, m->f, m->stream, opGm));
       TIMED(K_MOM, launch_mom_step(m->d, m->p, m->f, m->d_ctr, m->stream, !ringAside));
     } else if (dynamics_on(m, !ringAside)) return -1;
     if (thermoLate && thermoAtEnv == 1 && fork_thermo()) return -1;
@@ -1713,7 +1720,7 @@ static int one_step(mgcm_model *m) {
     // EXCH(cg2d_x) + etaN in the single-workgroup CG2D's epilogue -- off by default: one CU
     // walking every 2-D point costs more than the launch it saves)
     const bool sfpFused = mg_fuse_on(MG_FUSE_SFP) && m->p.nonlinFreeSurf > 0 && m->d.nT == m->d.nTiles;
-    if (m->p.nonlinFreeSurf > 0) TIMED(K_RSTAR, update_r_star_cg2d(m, sfpFused, opEarly));
+    if (m->p.nonlinFreeSurf > 0) TIMED(K_RSTAR, update_r_star_cg2d(m, sfpFused, opEarly || opGm, opGm));
     if (!sfpFused) TIMED(K_RHS, launch_sfp_rhs(m->d, m->p, m->f, m->stream));
     if (thermoLate && thermoAtEnv == 2 && fork_thermo()) return -1;
     const bool etaFused = mg_fuse_on(MG_FUSE_ETA) && cg2d_fuses_eta(m);
