@@ -2120,9 +2120,10 @@ int mgcm_begin_steps(mgcm_model *m) {
 //      THERMODYNAMICS with the new velocities;  [send/recv the 3-D halo sources again]
 //   4: DO_FIELDS_BLOCKING_EXCHANGES of this process's tiles, step counters.
 // THERMODYNAMICS onto the second stream (after the model stream's work so far) and its join
-static int shard_fork_thermo(mgcm_model *m) {
+static int shard_fork_thermo(mgcm_model *m, bool ring = false) {
   HIPCHK(hipEventRecord(m->evFork, m->stream));
   HIPCHK(hipStreamWaitEvent(m->stream2, m->evFork, 0));
+  if (ring) HIPCHK(launch_mom_ring(m->d, m->p, m->f, m->d_ctr, m->stream2));   // as one_step (MG_FUSE_RING)
   if (tracers_on(m, m->stream2)) return -1;
   HIPCHK(hipEventRecord(m->evJoin, m->stream2));
   return 0;
@@ -2164,16 +2165,18 @@ int mgcm_step_phase(mgcm_model *m, int phase) {
       if (!stagger && tracers_on(m, m->stream)) return -1;
       if (phase == 8) return 0;
       [[fallthrough]];
-    case 9:   // DYNAMICS, UPDATE_R_STAR + UPDATE_CG2D, CALC_DIV_GHAT
-      if (mgcm_dynamics(m)) return -1;
+    case 9: {   // DYNAMICS, UPDATE_R_STAR + UPDATE_CG2D, CALC_DIV_GHAT
+      const bool ringAside = m->shardFork == 2 && mom_ring_separable(m->d, m->p) && mg_fuse_on(MG_FUSE_RING);
+      if (dynamics_on(m, !ringAside)) return -1;
       if (m->shardFork == 2) {
-        if (shard_fork_thermo(m)) return -1;
+        if (shard_fork_thermo(m, ringAside)) return -1;
         m->shardFork = 3;
         m->mwg.exclusive = 1;   // the multi-workgroup CG2D keeps its CUs while the tracers run
       } else if (m->shardFork == 1 && shard_join_thermo(m)) return -1;
       if (m->p.nonlinFreeSurf > 0) TIMED(K_RSTAR, update_r_star_cg2d(m));
       TIMED(K_RHS, launch_sfp_rhs(m->d, m->p, m->f, m->stream));
       return 0;
+    }
     case 2:
       TIMED(K_CG2D, launch_cg2d(m, m->p.cg2dMaxIters, m->p.cg2dUseMinResSol - 1));
       TIMED(K_ETA, launch_exch_eta(m->d, m->p, m->f, m->d_srcOf, false, 0, m->stream));
