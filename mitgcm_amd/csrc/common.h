@@ -275,6 +275,13 @@ inline bool mg_fuse_on(int bit) {
                                                 MG_FUSE_OPE | MG_FUSE_RING;
   return (mask & bit) != 0;
 }
+// Where the fold carries UPDATE_CG2D (MG_FUSE_OPE; MGCM_OPE_AT, read per call): 1 operator in
+// grid 1, preconditioner in grid 2; 2 (default) operator in grid 2, preconditioner in grid 3;
+// 3 operator in grid 2, preconditioner in the r* pass
+inline int mg_ope_at() {
+  const int v = getenv("MGCM_OPE_AT") ? atoi(getenv("MGCM_OPE_AT")) : 2;
+  return (v >= 1 && v <= 3) ? v : 2;
+}
 // Horizontal launch fusion of two independent latency-bound kernels into one grid: on the
 // small configurations only (up to 2^21 grid points), where each launch is a few us of latency
 inline bool mg_hfuse(int bit, long nx, long ny, long nT, long Nr) {

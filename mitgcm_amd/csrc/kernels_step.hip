@@ -227,13 +227,13 @@ hipError_t launch_dyn_thermo(const Dims &d, const Params &p, const Fields &f, co
   const int nbDel = del2_needed(p) ? (int)mg_plane_blocks(d.nx, d.ny, d.nT * d.Nr) : 0;
   const int nbTr = (int)mg_plane_blocks(d.sNx, d.sNy, d.nT * d.Nr);
   if (dyn_thermo_takes_gm(p)) {
-    // MGCM_OPE_AT (read per launch, A/B): 2 operator in grid 2, preconditioner in grid 3 (the
-    // default: config 2 0.2821-0.2832 ms/step), 1 operator in grid 1, preconditioner in grid 2
+    // MGCM_OPE_AT (mg_ope_at): 2 (default; config 2 0.2821-0.2832 ms/step) against 1
     // (0.2852-0.2857 on the same box; profiles/r04/ope_at/) -- the longest grid (the momentum
-    // chain) hides the operator's blocks best
-    const int opeAt = getenv("MGCM_OPE_AT") ? atoi(getenv("MGCM_OPE_AT")) : 2;
+    // chain) hides the operator's blocks best; 3 leaves the preconditioner to the r* pass
+    // (0.2825-0.2829 against 0.2815-0.2819 for 2 on one box, profiles/r04/ope_at3/)
+    const int opeAt = mg_ope_at();
     const int nbU = srcOf ? ucg2d_blocks(d) : 0;
-    const int nbOp1 = opeAt == 2 ? 0 : nbU, nbPc2 = opeAt == 2 ? 0 : nbU, nbOp2 = opeAt == 2 ? nbU : 0,
+    const int nbOp1 = opeAt == 1 ? nbU : 0, nbPc2 = opeAt == 1 ? nbU : 0, nbOp2 = opeAt == 1 ? 0 : nbU,
               nbPc3 = opeAt == 2 ? nbU : 0;
     launch_l1(d, p, f, nbDel, s, nbOp1);
     const bool ff4 = mom_ff4_on(true);

@@ -1720,7 +1720,8 @@ static int one_step(mgcm_model *m) {
     // EXCH(cg2d_x) + etaN in the single-workgroup CG2D's epilogue -- off by default: one CU
     // walking every 2-D point costs more than the launch it saves)
     const bool sfpFused = mg_fuse_on(MG_FUSE_SFP) && m->p.nonlinFreeSurf > 0 && m->d.nT == m->d.nTiles;
-    if (m->p.nonlinFreeSurf > 0) TIMED(K_RSTAR, update_r_star_cg2d(m, sfpFused, opEarly || opGm, opGm));
+    if (m->p.nonlinFreeSurf > 0)
+      TIMED(K_RSTAR, update_r_star_cg2d(m, sfpFused, opEarly || opGm, opGm || (opEarly && mg_ope_at() == 3)));
     if (!sfpFused) TIMED(K_RHS, launch_sfp_rhs(m->d, m->p, m->f, m->stream));
     if (thermoLate && thermoAtEnv == 2 && fork_thermo()) return -1;
     const bool etaFused = mg_fuse_on(MG_FUSE_ETA) && cg2d_fuses_eta(m);
