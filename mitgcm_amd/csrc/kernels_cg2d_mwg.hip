@@ -126,14 +126,27 @@ __device__ __forceinline__ bool gran_get(gu64 *g, unsigned tag, double &v) {
 // (epoch mod 2^16) << 16 | phase, so no memset is needed between launches.  The timeout word
 // ctr[1] (shared) holds epoch + 1 of a launch that gave up (the epoch then advances by 2).
 __device__ __forceinline__ unsigned mw_tag(unsigned ep, int phase) { return ((ep & 0xffffu) << 16) | (unsigned)phase; }
-// bounded spin: after ~2^22 passes every part gives up (timeout word), so no wave hangs
+// bounded spin: after ~2^22 passes every part gives up (timeout word), so no wave hangs.
+// The timeout word is read every MGCM_MW_TMO_EVERY-th pass only: read every pass, its load
+// (a second memory round trip behind the granule loads) doubled each poll's period.
+// MGCM_MW_SLEEP: the s_sleep argument between passes (0: none).  Build-time switches (A/B
+// libraries, tools/lib_ab.sh).
+#ifndef MGCM_MW_TMO_EVERY
+#define MGCM_MW_TMO_EVERY 64
+#endif
+#ifndef MGCM_MW_SLEEP
+#define MGCM_MW_SLEEP 1
+#endif
 template <bool SYS = false>
 __device__ __forceinline__ bool spin_fail(unsigned &spins, gu32 *tmo, unsigned ep) {
-  if (__hip_atomic_load(tmo, RLX_SCOPE(SYS)) == ep + 1u || ++spins > (1u << 22)) {
-    __hip_atomic_store(tmo, ep + 1u, RLX_SCOPE(SYS));
-    return true;
+  ++spins;
+  if (spins % MGCM_MW_TMO_EVERY == 0u || spins > (1u << 22)) {
+    if (__hip_atomic_load(tmo, RLX_SCOPE(SYS)) == ep + 1u || spins > (1u << 22)) {
+      __hip_atomic_store(tmo, ep + 1u, RLX_SCOPE(SYS));
+      return true;
+    }
   }
-  __builtin_amdgcn_s_sleep(1);
+  if (MGCM_MW_SLEEP > 0) __builtin_amdgcn_s_sleep(MGCM_MW_SLEEP);
   return false;
 }
 
