@@ -2498,8 +2498,11 @@ hipError_t launch_mom_step(const Dims &d, const Params &p, const Fields &f, cons
     // chunks of levels: 527 us alone on LLC-90 against 634 with two chunks and ~640 for the
     // per-level kernel (profiles/r03/ab/).  MGCM_VI_KERNEL=level|march|tiled and MGCM_VI_KC
     // override (sweeps).
+    // (round 4, k_mom_vi_m2: two chunks are now the faster split, LLC-90 448-456 us against
+    // 460 at five and 453-460 at three, step 1.531-1.545 against 1.550-1.552 ms,
+    // profiles/r04/vikc/)
     const int nbt = nbx * nby * d.nT;
-    int KCm = (d.Nr + 4) / 5;
+    int KCm = (d.Nr + 1) / 2;
     if (kcEnv > 0) KCm = kcEnv > d.Nr ? d.Nr : kcEnv;
     const bool march = viEnv ? !strcmp(viEnv, "march") : (d.Nr >= 30 && nbt >= 256);
     if (march) {
