@@ -2494,9 +2494,9 @@ hipError_t launch_mom_step(const Dims &d, const Params &p, const Fields &f, cons
     // that the two extra staged levels per chunk stay a small overhead
     const int kcEnv = getenv("MGCM_VI_KC") ? atoi(getenv("MGCM_VI_KC")) : 0;
     const char *viEnv = getenv("MGCM_VI_KERNEL");   // march | level | tiled (sweeps; read per launch)
-    // the k-march for deep grids (Nr >= 30 with >= 256 workgroups per level chunk), in five
-    // chunks of levels: 527 us alone on LLC-90 against 634 with two chunks and ~640 for the
-    // per-level kernel (profiles/r03/ab/).  MGCM_VI_KERNEL=level|march|tiled and MGCM_VI_KC
+    // the k-march for deep grids (Nr >= 30 with >= 256 workgroups per level chunk); round 3's
+    // generic march ran best in five chunks of levels (527 us alone on LLC-90 against 634 with
+    // two and ~640 for the per-level kernel, profiles/r03/ab/).  MGCM_VI_KERNEL=level|march|tiled and MGCM_VI_KC
     // override (sweeps).
     // (round 4, k_mom_vi_m2: two chunks are now the faster split, LLC-90 448-456 us against
     // 460 at five and 453-460 at three, step 1.531-1.545 against 1.550-1.552 ms,
