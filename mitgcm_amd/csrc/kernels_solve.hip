@@ -1663,7 +1663,9 @@ __global__ void k_bump_counter(int *c, int nIncr) {
 // ------------------------------------------------------------------ launchers
 hipError_t launch_sfp_rhs(const Dims &d, const Params &p, const Fields &f, hipStream_t s) {
   const long ncol = (long)d.nx * d.ny * d.nT;
-  const int nc = mg_colf_nc(ncol, d.Nr, 4);
+  // MGCM_SFP_NC = 16 | 32 | 64 (read per launch, A/B), else mg_colf_nc's
+  const int ncEnv = getenv("MGCM_SFP_NC") ? atoi(getenv("MGCM_SFP_NC")) : 0;
+  const int nc = (ncEnv == 16 || ncEnv == 32 || ncEnv == 64) ? ncEnv : mg_colf_nc(ncol, d.Nr, 4);
   MG_ALLOW_LDS(k_sfp_rhs);
   hipLaunchKernelGGL(k_sfp_rhs, dim3(mg_colf_blocks(ncol, nc)), dim3(256), mg_colf_lds(d.Nr, nc, 4), s, d, p, f, nc);
   return hipGetLastError();
