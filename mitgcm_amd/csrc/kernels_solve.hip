@@ -1663,7 +1663,8 @@ __global__ void k_bump_counter(int *c, int nIncr) {
 // ------------------------------------------------------------------ launchers
 hipError_t launch_sfp_rhs(const Dims &d, const Params &p, const Fields &f, hipStream_t s) {
   const long ncol = (long)d.nx * d.ny * d.nT;
-  // MGCM_SFP_NC = 16 | 32 | 64 (read per launch, A/B), else mg_colf_nc's
+  // MGCM_SFP_NC = 16 | 32 | 64 (read per launch, A/B), else mg_colf_nc's 16 (LLC-90: 63 us at
+  // 16, 69 at 32, 115 at 64; profiles/r04/sfpnc/, where the correction pass's 32 is confirmed too)
   const int ncEnv = getenv("MGCM_SFP_NC") ? atoi(getenv("MGCM_SFP_NC")) : 0;
   const int nc = (ncEnv == 16 || ncEnv == 32 || ncEnv == 64) ? ncEnv : mg_colf_nc(ncol, d.Nr, 4);
   MG_ALLOW_LDS(k_sfp_rhs);
