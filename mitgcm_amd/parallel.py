@@ -246,8 +246,12 @@ class ShardedModel:
         if cg2d == "auto":
             cg2d = "device" if model.cg2d_kernel() == "mwg" else "replicated"
         self.cg2d = cg2d
-        if cg2d == "device":
+        if cg2d == "device" and self.world > 1:
+            # (one process: the model's own hand-off block as the resident solve uses it --
+            # coarse-grained and one-XCD-pinned where that is faster, e.g. the cube -- nothing to map)
             self._share_cg2d_handoff()
+        elif cg2d == "device" and self.m.cg2d_kernel() != "mwg":
+            raise ValueError('cg2d="device" needs the multi-workgroup CG2D (set the parameter cg2dForceMwg=1)')
         if cg2d == "distributed" and model.params.get("useSRCGSolver", 0):
             raise NotImplementedError("useSRCGSolver (CG2D_SR) with the distributed CG2D not implemented")
         if cg2d == "distributed":
