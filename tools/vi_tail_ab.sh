@@ -1,4 +1,6 @@
 # A/B on LLC-90: the VI k-march's intermediates tail dealt out over the waves (MGCM_VI_M2_VAR 30
+# (historical: the var-30 tail and the MGCM_CORR_UNR / MGCM_SFP_UNR variants were measured slower and
+# removed after this A/B -- profiles/r04/llc_ab/ holds its results)
 # vs 14), the correction pass's level loop unrolled (MGCM_CORR_UNR 1 / 2 / 4) and the halo-ring
 # AB2 beside the solve (MGCM_STEP_FUSE 3469 default vs 1421 without MG_FUSE_RING)
 set -o pipefail
