@@ -129,13 +129,15 @@ __device__ __forceinline__ unsigned mw_tag(unsigned ep, int phase) { return ((ep
 // bounded spin: after ~2^22 passes every part gives up (timeout word), so no wave hangs.
 // The timeout word is read every MGCM_MW_TMO_EVERY-th pass only: read every pass, its load
 // (a second memory round trip behind the granule loads) doubled each poll's period.
-// MGCM_MW_SLEEP: the s_sleep argument between passes (0: none).  Build-time switches (A/B
-// libraries, tools/lib_ab.sh).
+// MGCM_MW_SLEEP: the s_sleep argument between passes (0: none): 2 by default -- cs32x15's
+// one-XCD parts 4.13 against 4.22 us/iteration at 1 and worse at 0, LLC-90 unchanged
+// (6.12 against 6.02-6.19), 4 slower there (profiles/r04/mwsleep/, profiles/r04/mwpoll/).
+// Build-time switches (A/B libraries, tools/lib_ab.sh).
 #ifndef MGCM_MW_TMO_EVERY
 #define MGCM_MW_TMO_EVERY 64
 #endif
 #ifndef MGCM_MW_SLEEP
-#define MGCM_MW_SLEEP 1
+#define MGCM_MW_SLEEP 2
 #endif
 template <bool SYS = false>
 __device__ __forceinline__ bool spin_fail(unsigned &spins, gu32 *tmo, unsigned ep) {
