@@ -6,9 +6,9 @@
 A "step" is one FORWARD_STEP of the device-resident hot path (DYNAMICS ->
 SOLVE_FOR_PRESSURE/CG2D -> MOMENTUM_CORRECTION_STEP -> INTEGR_CONTINUITY ->
 blocking exchanges) on inputs already resident in HBM.  Rank 0 prints ONE JSON
-line.  N>1: one process per GPU (torch.distributed.run); the supported
-workloads are single-tile, so every rank runs an independent replica
-("replicas only") and value = the sum over ranks.
+line.  `value` is BASELINE config 2 (90x40x15, one tile): at N>1 (one process per
+GPU, torch.distributed.run) every rank runs an independent replica ("replicas
+only") and value = the sum over ranks.
 
 Fields of the JSON line beyond the driver contract:
   roofline     dominant kernel (the whole-solve CG2D): bound "latency" -- the f64
@@ -18,6 +18,12 @@ Fields of the JSON line beyond the driver contract:
                over its mean HIP-event duration against the 8 TB/s HBM peak
   roofline_hbm the DYNAMICS momentum kernel(s) against the HBM roofline
                (SURVEY.md 8(d) algorithmic bytes per 3-D point)
+  cs32x15      N=1: BASELINE config 3 (the other half of the metric), resident,
+               the same steps/warmup, with its own rooflines
+  sharded      N>1: the tile-sharded path -- cs32x15 over min(N,6) ranks and the
+               LLC-90 synthetic over N ranks (RCCL subgroups, graph-replayed), each
+               with the resident 1-GPU ms/step beside it and the CG2D placement
+               chosen by parallel.cg2d_policy
   cpu_baseline the oracle (oracle/, C restatement, 1 core) on a bounded sample
                of the same workload, rank 0 only
 """
@@ -61,6 +67,10 @@ def parse():
                          "CG2D whose parts run in every process on one IPC-shared hand-off block "
                          "(mitgcm_amd/parallel.py)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--no-cs32", action="store_true", help="N = 1: skip the cs32x15 sub-record")
+    ap.add_argument("--no-sharded", action="store_true", help="N > 1: skip the sharded cs32x15 / LLC-90 records")
+    ap.add_argument("--sharded-timeout", type=float, default=300.0,
+                    help="N > 1: seconds the sharded records may take before the line is printed without them")
     ap.add_argument("--set", action="append", default=[], metavar="NAME=VALUE",
                     help="override a namelist parameter of the GPU model (A/B runs, e.g. useSRCGSolver=1); "
                          "recorded in config.params_over")
@@ -220,6 +230,184 @@ def cg_kernel_key(m):
     return "k_cg2d_" + m.cg2d_kernel().replace("_ref", "")
 
 
+def attribution(m, stepper, steps, config, pmc_summary, sync):
+    """Per-kernel attribution of the timed workload: the same `steps` again, launched eagerly
+    with HIP events recorded on the model's stream around every kernel (the graph path cannot
+    be bracketed by events; rocprofv3 of the command must agree, profiles/), then the two
+    roofline objects -- the dominant kernel (the whole-solve CG2D, latency-bound) and the
+    DYNAMICS momentum block against the HBM roofline (SURVEY.md 8(d) algorithmic bytes)."""
+    g = m.g
+    npts = g.nTiles * g.sNx * g.sNy
+    m.kernel_timing(True)
+    stepper.forward_step(steps)
+    sync()
+    iters_t = [int(v) for v in m.solve_history(steps)[0]]
+    cg_ms, cg_n = m.kernel_ms("cg2d")
+    kern = {k: m.kernel_ms(k) for k in ("oceanic_phys", "temp_step", "phi_hyd", "mom_step", "sfp_rhs", "cg2d", "exchange",
+                                         "eta_update", "correction", "continuity", "r_star")}
+    m.kernel_timing(False)
+    cg_traffic, _ = pmc_traffic(pmc_summary, cg_kernel_key(m))
+    # the momentum block's launches as the timed graph runs them: on small grids with
+    # THERMODYNAMICS folded into DYNAMICS' grids (config 2) the three fused grids k_dt_l1/l2/l3
+    # (GM tensor | CALC_PHI_HYD | del2uv, MOM U | V | tracer right-hand sides, CD scheme |
+    # implicit tracer solves); otherwise launch_mom_step's (del2uv, the MOM_FLUXFORM /
+    # MOM_VECINV kernel, the VI halo AB pass, the CD scheme, the implicit viscosity columns)
+    layout = m.step_layout()
+    dt_fused = layout["dyn_thermo_fused"]
+    mom_kernels = ("k_dt_l",) if dt_fused else ("k_del2uv", "k_mom_", "k_cd_scheme")
+    mom_traffic, mom_traffic_per = pmc_traffic(pmc_summary, mom_kernels)
+    its_per_solve = sum(iters_t) / max(1, len(iters_t))
+    bytes_per_launch = CG2D_BYTES_PER_POINT_ITER * npts * its_per_solve
+    achieved = bytes_per_launch / (cg_ms * 1e-3) / 1e9 if cg_ms > 0 else 0.0
+    us_per_it = 1e3 * cg_ms / its_per_solve if its_per_solve > 0 else 0.0
+    cus = int(m.cg2d_parts())
+    # the f64 VALU bound of the CUs the solve runs on (one workgroup per CU)
+    valu_us = CG2D_F64_OPS_PER_POINT_ITER * npts / (CU_F64_LANE_OPS_PER_CLK * cus * CLOCK_GHZ * 1e3)
+    mom_ms = kern["mom_step"][0]
+    mom_bpp = MOM_BYTES_PER_POINT.get(g.Nr, 104.0 + 24 * 8.0 / g.Nr)
+    mom_bytes = mom_bpp * npts * g.Nr
+    if dt_fused:   # + the stepped tracers' right-hand sides and solves (SURVEY.md 8(d): 64 B + 96/Nr B a point)
+        ntr = int(m.params.get("tempStepping", 1) != 0) + int(m.params.get("saltStepping", 1) != 0)
+        mom_bytes += ntr * (64.0 + 96.0 / g.Nr) * npts * g.Nr
+    mom_gbs = mom_bytes / (mom_ms * 1e-3) / 1e9 if mom_ms > 0 else 0.0
+    # dominant kernel: the whole-solve CG2D.  It is not HBM-bound: its working set sits in
+    # LDS/VGPRs of the workgroup(s) it runs on, so the chip-level HBM fraction is reported for
+    # completeness; the bound that holds it is latency -- the f64 VALU issue of its CU(s) plus
+    # the barriers/cross-wave sums (one CU) or grid hand-offs (many) of each iteration
+    # (valu_floor_us_per_iter, profiles/r02/ocean90/cg2d_geometry.txt)
+    roofline = {"bound": "latency", "kernel": "k_cg2d_" + m.cg2d_kernel(), "achieved": achieved, "peak": HBM_PEAK_GBS,
+                "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
+                "traffic": cg_traffic,
+                "traffic_unit": "bytes per launch (rocprofv3 --pmc, %s)" % os.path.relpath(pmc_summary, ROOT),
+                "bytes_per_launch": bytes_per_launch, "launch_ms": cg_ms, "launches": cg_n,
+                "us_per_iteration": us_per_it, "cus_used": cus,
+                "valu_floor_us_per_iter": valu_us,
+                "valu_frac": valu_us / us_per_it if us_per_it > 0 else 0.0}
+    roofline_hbm = {"bound": "hbm",
+                    "kernel": ("fused DYNAMICS + THERMODYNAMICS grids k_dt_l1/l2/l3 (the launches the timed graph "
+                               "runs; bytes: momentum + the stepped tracers)" if dt_fused else
+                               "DYNAMICS momentum block (MOM_FLUXFORM/MOM_VECINV + TIMESTEP + AB2; "
+                               "CALC_PHI_HYD timed apart as phi_hyd), streams serialised"),
+                    "kernels": list(mom_kernels), "bytes_per_launch": mom_bytes,
+                    "achieved": mom_gbs,
+                    "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": mom_gbs / HBM_PEAK_GBS,
+                    "bytes_per_point": mom_bpp, "launch_ms": mom_ms,
+                    "traffic": mom_traffic,
+                    "traffic_per_kernel": {k.split("(")[0]: v for k, v in mom_traffic_per.items()}}
+    return iters_t, kern, layout, roofline, roofline_hbm
+
+
+def check_iters(iters, what):
+    """numIters = -1 marks a multi-workgroup CG2D that gave up (hand-off timeout): a graph
+    batch would otherwise carry on silently."""
+    failed = [i for i in iters if i < 0]
+    if failed:
+        raise SystemExit("bench: %s: %d of %d CG2D solves failed (numIters < 0): %s" % (what, len(failed), len(iters),
+                                                                                         iters))
+
+
+def resident_ms(config, steps, warmup, device):
+    """ms/step of the resident (1-GPU, graph-replayed) path of a workload, and its model;
+    the caller closes the model."""
+    from mitgcm_amd import configs
+    m = configs.make_model(config_fn(config), device=device)
+    if warmup > 0:
+        m.forward_step(warmup)
+    m.sync()
+    m.prepare()
+    m.sync()
+    t0 = time.perf_counter()
+    m.forward_step(steps)
+    m.sync()
+    el = time.perf_counter() - t0
+    iters = [int(v) for v in m.solve_history(steps)[0]]
+    check_iters(iters, config)
+    return m, 1e3 * el / steps, iters, el
+
+
+def cs32x15_record(a, device):
+    """BASELINE config 3 (the other half of BASELINE.json's metric) at N = 1: the resident
+    graph-replayed step, `steps` timed after `warmup`, with its own attribution pass and
+    rooflines.  Reported beside `value` (config 2), not instead of it."""
+    cfg = "global_ocean.cs32x15"
+    steps, warmup = max(2, a.steps), a.warmup
+    m, ms, iters, el = resident_ms(cfg, steps, warmup, device)
+    dt_clock = m.params["deltaTClock"]
+    iters_t, kern, layout, roof, roof_hbm = attribution(m, m, steps, cfg, default_pmc_summary(cfg), m.sync)
+    check_iters(iters_t, cfg)
+    st = m.solve_stats()
+    assert st["cg2d_last_res"] < 1e-6, st
+    m.close()
+    return {"config": cfg, "workload": WORKLOADS[cfg], "steps": steps, "warmup": warmup, "ms_per_step": ms,
+            "value": steps * dt_clock / 86400.0 / el, "unit": "model-days/s",
+            "cg2d_iters_per_s": sum(iters) / el, "cg2d_mean_iters_per_solve": sum(iters) / max(1, len(iters)),
+            "kernel_ms_mean": {k: v[0] for k, v in kern.items()}, "roofline": roof, "roofline_hbm": roof_hbm}
+
+
+def sharded_records(a, dist, world, rank, local, backend):
+    """N > 1: the tile-sharded path the north_star scales -- cs32x15 over min(N, 6) ranks (one
+    cube face per GPU) and the LLC-90 synthetic over N ranks (13 tiles) -- each stepped by
+    mitgcm_amd.parallel.ShardedModel over a subgroup (RCCL; gloo when MGCM_SHARD_BACKEND=gloo
+    rehearses on one GPU), graph-replayed over RCCL, `steps` (rounded up to even) timed after
+    `warmup`, max over the subgroup's ranks; beside each the same workload's resident 1-GPU
+    ms/step (rank 0).  Strong scaling: the work is the whole workload at every N."""
+    import torch
+    from mitgcm_amd import configs
+    from mitgcm_amd.parallel import ShardedModel
+    steps = a.steps + (a.steps & 1)
+    warm = max(2, a.warmup + (a.warmup & 1))
+    out = []
+    for cfg, n in (("global_ocean.cs32x15", min(world, 6)), ("llc90_synthetic", world)):
+        rec = {"config": cfg, "ranks": n, "transport": "RCCL" if backend == "nccl" else "gloo (host-staged)"}
+        sub = dist.new_group(list(range(n)), backend=backend)   # collective over every rank
+        try:
+            if rank == 0:
+                m1, ms1, _, _ = resident_ms(cfg, steps, warm, local)
+                m1.close()
+                rec["resident_1gpu_ms_per_step"] = ms1
+            if rank < n:
+                m = configs.make_model(config_fn(cfg), device=local)
+                sm = ShardedModel(m, dist, cg2d=a.cg2d, group=sub)
+                graph = backend == "nccl"
+                if graph:
+                    sm.capture_step()
+                    sm.replay(warm // 2)
+                else:
+                    sm.forward_step(warm)
+                m.sync()
+                torch.cuda.synchronize(local)
+                sm.dist.barrier()
+                t0 = time.perf_counter()
+                if graph:
+                    sm.replay(steps // 2, check=False)
+                else:
+                    sm.forward_step(steps, check=False)
+                m.sync()
+                torch.cuda.synchronize(local)
+                el = time.perf_counter() - t0
+                sm.dist.barrier()
+                t = torch.tensor([el], dtype=torch.float64, device="cuda" if backend == "nccl" else "cpu")
+                sm.dist.all_reduce(t, op=dist.ReduceOp.MAX)
+                el = float(t.item())
+                iters = [int(v) for v in m.solve_history(steps)[0]]
+                check_iters(iters, cfg + " sharded")
+                dt_clock = m.params["deltaTClock"]
+                rec.update({"ms_per_step": 1e3 * el / steps, "value": steps * dt_clock / 86400.0 / el,
+                            "unit": "model-days/s", "steps": steps, "warmup": warm,
+                            "tiles_per_rank": sm.part.counts, "cg2d": sm.cg2d, "cg2d_policy": sm.cg2d_reason,
+                            "step_path": "graph-replayed (collectives captured)" if graph else "eager",
+                            "cg2d_mean_iters_per_solve": sum(iters) / max(1, len(iters))})
+                if "resident_1gpu_ms_per_step" in rec:
+                    rec["speedup_vs_resident_1gpu"] = rec["resident_1gpu_ms_per_step"] / rec["ms_per_step"]
+                m.close()
+        except Exception as e:   # reported in the record; the headline line stands
+            rec["error"] = "%s: %s" % (type(e).__name__, e)
+            print("bench: sharded %s failed on rank %d: %r" % (cfg, rank, e), file=sys.stderr)
+        dist.barrier()
+        out.append(rec)
+    return out
+
+
 def main():
     a = parse()
     # stdout carries ONE JSON line: whatever libraries print (RCCL's version banner at
@@ -243,21 +431,35 @@ def main():
             sk.close()
         os.environ.setdefault("RANK", "0")
         os.environ.setdefault("WORLD_SIZE", "1")
+    # MGCM_SHARD_BACKEND=gloo: host-staged transport, lets several ranks share one GPU
+    # (rehearsal on a 1-GPU box; RCCL refuses two ranks per device)
+    shard_backend = os.environ.get("MGCM_SHARD_BACKEND", "nccl")
+    sharded_rec = world > 1 and not shard and not a.no_sharded
     if world > 1 or shard:
         import torch
         import torch.distributed as dist
+        if shard_backend == "gloo":
+            local = local % torch.cuda.device_count()
+        torch.cuda.set_device(local)
         if shard:
-            # MGCM_SHARD_BACKEND=gloo: host-staged transport, lets several ranks share
-            # one GPU (rehearsal on a 1-GPU box; RCCL refuses two ranks per device)
-            if os.environ.get("MGCM_SHARD_BACKEND", "nccl") == "gloo":
-                local = local % torch.cuda.device_count()
-                torch.cuda.set_device(local)
+            if shard_backend == "gloo":
                 dist.init_process_group("gloo")
             else:
-                torch.cuda.set_device(local)
                 dist.init_process_group("nccl", device_id=torch.device("cuda", local))   # RCCL over xGMI
         else:
             dist.init_process_group("gloo")   # replicas: barrier + max-reduce of host timers only
+    # the sharded records run after the headline; a hang there (a collective a failed rank never
+    # joins) must not cost the line: past the deadline rank 0 prints what it has and every
+    # rank leaves
+    emitted = {"done": False}
+    out = {}
+
+    def emit():
+        if rank == 0 and not emitted["done"]:
+            emitted["done"] = True
+            sys.stdout.flush()
+            os.write(json_fd, (json.dumps(out) + "\n").encode())
+
     import numpy as np
     from mitgcm_amd import configs
 
@@ -273,7 +475,6 @@ def main():
     m = configs.make_model(cfn, device=local)
     g = m.g
     dt_clock = m.params["deltaTClock"]
-    npts = g.nTiles * g.sNx * g.sNy
     stepper = m
     if shard:
         from mitgcm_amd.parallel import ShardedModel
@@ -323,62 +524,21 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     iters = [int(v) for v in m.solve_history(a.steps)[0]]
-    # per-kernel durations: the same K steps again, launched eagerly with HIP events
-    # recorded on the model's stream around every kernel (the graph path cannot be
-    # bracketed by events); rocprofv3 of this command must agree (profiles/)
-    m.kernel_timing(True)
-    stepper.forward_step(a.steps)
-    sync()
-    iters_t = [int(v) for v in m.solve_history(a.steps)[0]]
-    cg_ms, cg_n = m.kernel_ms("cg2d")
-    kern = {k: m.kernel_ms(k) for k in ("oceanic_phys", "temp_step", "phi_hyd", "mom_step", "sfp_rhs", "cg2d", "exchange",
-                                         "eta_update", "correction", "continuity", "r_star")}
-    m.kernel_timing(False)
+    if a.pmc_summary is None:
+        a.pmc_summary = default_pmc_summary(a.config)
+    iters_t, kern, layout, roofline, roofline_hbm = attribution(m, stepper, a.steps, a.config, a.pmc_summary, sync)
     # sanity: the solution is finite and the solver converged every step
     stats = m.solve_stats()
     eta = m.get("etaN")
     assert np.isfinite(eta).all() and stats["cg2d_last_res"] < 1e-6, stats
-
-    # every solve of both batches converged without a hand-off timeout (numIters = -1 marks
-    # a multi-workgroup CG2D that gave up; a graph batch would otherwise carry on silently)
-    failed = [i for i in iters + iters_t if i < 0]
-    if failed:
-        raise SystemExit("bench: %d of %d CG2D solves failed (numIters < 0): %s" % (len(failed), len(iters + iters_t),
-                                                                                   iters + iters_t))
-    if a.pmc_summary is None:
-        a.pmc_summary = default_pmc_summary(a.config)
-    cg_traffic, _ = pmc_traffic(a.pmc_summary, cg_kernel_key(m))
-    # the momentum block's launches as the timed graph runs them: on small grids with
-    # THERMODYNAMICS folded into DYNAMICS' grids (config 2) the three fused grids k_dt_l1/l2/l3
-    # (GM tensor | CALC_PHI_HYD | del2uv, MOM U | V | tracer right-hand sides, CD scheme |
-    # implicit tracer solves); otherwise launch_mom_step's (del2uv, the MOM_FLUXFORM /
-    # MOM_VECINV kernel, the VI halo AB pass, the CD scheme, the implicit viscosity columns)
-    layout = m.step_layout()
-    dt_fused = layout["dyn_thermo_fused"]
-    mom_kernels = ("k_dt_l",) if dt_fused else ("k_del2uv", "k_mom_", "k_cd_scheme")
-    mom_traffic, mom_traffic_per = pmc_traffic(a.pmc_summary, mom_kernels)
+    # every solve of both batches converged without a hand-off timeout
+    check_iters(iters + iters_t, a.config)
     model_days = a.steps * dt_clock / 86400.0
     copies = 1 if shard else world   # independent model integrations in the job
     value = copies * model_days / elapsed
     iters_total = sum(iters)
     cg2d_iters_per_s = copies * iters_total / elapsed
-    its_per_solve = sum(iters_t) / max(1, len(iters_t))
-    bytes_per_launch = CG2D_BYTES_PER_POINT_ITER * npts * its_per_solve
-    achieved = bytes_per_launch / (cg_ms * 1e-3) / 1e9 if cg_ms > 0 else 0.0
-    us_per_it = 1e3 * cg_ms / its_per_solve if its_per_solve > 0 else 0.0
-    cg_kernel = "k_cg2d_" + m.cg2d_kernel()
-    cus = int(m.cg2d_parts())
-    # the f64 VALU bound of the CUs the solve runs on (one workgroup per CU)
-    valu_us = CG2D_F64_OPS_PER_POINT_ITER * npts / (CU_F64_LANE_OPS_PER_CLK * cus * CLOCK_GHZ * 1e3)
-    # the dominant stencil kernel against the HBM roofline (algorithmic bytes)
-    mom_ms = kern["mom_step"][0]
-    mom_bpp = MOM_BYTES_PER_POINT.get(g.Nr, 104.0 + 24 * 8.0 / g.Nr)
-    mom_bytes = mom_bpp * npts * g.Nr
-    if dt_fused:   # + the stepped tracers' right-hand sides and solves (64 B + 96/Nr B a point)
-        ntr = int(m.params.get("tempStepping", 1) != 0) + int(m.params.get("saltStepping", 1) != 0)
-        mom_bytes += ntr * (64.0 + 96.0 / g.Nr) * npts * g.Nr
-    mom_gbs = mom_bytes / (mom_ms * 1e-3) / 1e9 if mom_ms > 0 else 0.0
-    out = {
+    out.update({
         "metric": "model-days/wallclock-sec",
         "value": value,
         # replica mode: value sums the N independent integrations; one integration's rate
@@ -414,46 +574,36 @@ def main():
         # launch layout the timed graph replays (one stream: a second-stream THERMODYNAMICS,
         # C5's, is serialised there); with the fused grids "mom_step" is k_dt_l1+l2+l3
         "kernel_ms_layout": {"eager_pass_of_the_graph_layout": True, **layout},
-        # dominant kernel: the whole-solve CG2D.  It is not HBM-bound: its working set sits in
-        # LDS/VGPRs of the workgroup(s) it runs on, so the chip-level HBM fraction below is
-        # reported for completeness; the bound that holds it is latency -- the f64 VALU issue of
-        # its CU(s) plus the barriers/cross-wave sums of each iteration (valu_floor_us_per_iter,
-        # profiles/r02/ocean90/cg2d_geometry.txt)
-        "roofline": {"bound": "latency", "kernel": cg_kernel, "achieved": achieved, "peak": HBM_PEAK_GBS,
-                     "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
-                     "traffic": cg_traffic,
-                     "traffic_unit": "bytes per launch (rocprofv3 --pmc, %s)" % os.path.relpath(a.pmc_summary, ROOT),
-                     "bytes_per_launch": bytes_per_launch, "launch_ms": cg_ms, "launches": cg_n,
-                     "us_per_iteration": us_per_it, "cus_used": cus,
-                     "valu_floor_us_per_iter": valu_us,
-                     "valu_frac": valu_us / us_per_it if us_per_it > 0 else 0.0},
-        # the dominant 3-D stencil kernel (DYNAMICS) against the HBM roofline
-        "roofline_hbm": {"bound": "hbm",
-                         "kernel": ("fused DYNAMICS + THERMODYNAMICS grids k_dt_l1/l2/l3 (the launches the timed graph "
-                                    "runs; bytes: momentum + the stepped tracers)" if dt_fused else
-                                    "DYNAMICS momentum block (MOM_FLUXFORM/MOM_VECINV + TIMESTEP + AB2; "
-                                    "CALC_PHI_HYD timed apart as phi_hyd), streams serialised"),
-                         "kernels": list(mom_kernels), "bytes_per_launch": mom_bytes,
-                         "achieved": mom_gbs,
-                         "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": mom_gbs / HBM_PEAK_GBS,
-                         "bytes_per_point": mom_bpp, "launch_ms": mom_ms,
-                         "traffic": mom_traffic,
-                         "traffic_per_kernel": {k.split("(")[0]: v for k, v in mom_traffic_per.items()}},
-    }
+        "roofline": roofline,
+        "roofline_hbm": roofline_hbm,
+    })
+    m.close()
     # the measured STREAM triad of this box beside the 8 TB/s spec
     try:
         triad = stream_triad_gbs(local)
         out["roofline_hbm"]["stream_triad_gbs"] = triad
-        out["roofline_hbm"]["frac_of_triad"] = mom_gbs / triad
+        out["roofline_hbm"]["frac_of_triad"] = out["roofline_hbm"]["achieved"] / triad
     except Exception as e:   # a reference number only: its absence does not fail the bench
         out["roofline_hbm"]["stream_triad_gbs"] = None
         print("bench: stream triad not measured: %s" % e, file=sys.stderr)
+    if rank == 0 and world == 1 and not shard and a.config != "global_ocean.cs32x15" and not a.no_cs32:
+        # the other half of BASELINE.json's metric, timed in the same run
+        out["cs32x15"] = cs32x15_record(a, local)
     if rank == 0 and world == 1 and not a.no_cpu_baseline:   # the CPU baseline is an N=1 line
         out["cpu_baseline"] = cpu_baseline(a.config, a.cpu_seconds)
-    if rank == 0:
-        sys.stdout.flush()
-        os.write(json_fd, (json.dumps(out) + "\n").encode())
-    m.close()
+    if sharded_rec:
+        import threading
+        out["sharded"] = [{"error": "not finished within %d s" % a.sharded_timeout}]
+
+        def deadline():
+            emit()
+            os._exit(0)
+        timer = threading.Timer(a.sharded_timeout, deadline)
+        timer.daemon = True
+        timer.start()
+        out["sharded"] = sharded_records(a, dist, world, rank, local, shard_backend)
+        timer.cancel()
+    emit()
     if dist is not None:
         dist.destroy_process_group()
 

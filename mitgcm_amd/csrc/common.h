@@ -231,11 +231,9 @@ inline unsigned mg_col_blocks(int ni, int nj, int nT, int Nr) {
 #define MG_COLF_K(kvar) for (int kvar = kk + 1; kvar <= d.Nr; kvar += KW_)
 // NC for a launch: 16 columns x 16 level slots (measured on LLC-90, Nr = 50: the implicit
 // tracer solve 119 us at NC = 16, 201 at 32, 168 with MG_COLS' 4 columns x 64 levels; wider
-// column runs cost occupancy through their LDS); MGCM_COLF_NC=16|32|64 forces it (sweeps)
+// column runs cost occupancy through their LDS)
 inline int mg_colf_nc(long ncols, int Nr, int nArr) {
-  static const int force = getenv("MGCM_COLF_NC") ? atoi(getenv("MGCM_COLF_NC")) : 0;
   (void)ncols; (void)Nr; (void)nArr;
-  if (force == 16 || force == 32 || force == 64) return force;
   return 16;
 }
 inline size_t mg_colf_lds(int Nr, int nc, int nArr) { return (size_t)nArr * Nr * nc * sizeof(double); }
@@ -274,13 +272,6 @@ inline bool mg_fuse_on(int bit) {
                                             : MG_FUSE_SFP | MG_FUSE_PHI | MG_FUSE_END | MG_FUSE_DT | MG_FUSE_ETAX |
                                                 MG_FUSE_OPE | MG_FUSE_RING;
   return (mask & bit) != 0;
-}
-// Where the fold carries UPDATE_CG2D (MG_FUSE_OPE; MGCM_OPE_AT, read per call): 1 operator in
-// grid 1, preconditioner in grid 2; 2 (default) operator in grid 2, preconditioner in grid 3;
-// 3 operator in grid 2, preconditioner in the r* pass
-inline int mg_ope_at() {
-  const int v = getenv("MGCM_OPE_AT") ? atoi(getenv("MGCM_OPE_AT")) : 2;
-  return (v >= 1 && v <= 3) ? v : 2;
 }
 // Horizontal launch fusion of two independent latency-bound kernels into one grid: on the
 // small configurations only (up to 2^21 grid points), where each launch is a few us of latency

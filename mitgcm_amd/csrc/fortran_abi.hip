@@ -377,6 +377,23 @@ void register_host() {
   fprintf(stderr, "MGCM_AMD: state pages registered for DMA: %zu ranges, %.1f MB\n", merged.size(), bytes / 1e6);
 }
 
+// A solve that gave up -- a grid hand-off of the multi-workgroup CG2D timed out: numIters =
+// -1, cg2d_x unconverged, and on a shared hand-off block the sharers' launch epochs may
+// disagree from then on (model.hip, mwg_restart_epoch) -- stops the run, read where the host
+// waits for the device anyway (a download, the step fence).  Each device-CG2D lead records
+// its own launch.
+void check_solve(const char *where) {
+  auto chk = [&](mgcm_model *m) {
+    int it = 0;
+    if (mgcm_solve_stats(m, 0, nullptr, nullptr, &it, nullptr)) die(where);
+    if (it < 0) die(where, "CG2D gave up: a grid hand-off of the multi-workgroup solve timed out (numIters = -1)");
+  };
+  if (multi() && g.cgDevice)
+    for (auto &c : g.cgLeads) chk(g.sh[c.shard].m);
+  else
+    chk(g.m);
+}
+
 // The state down: a tiled array (2-D or 3-D, tile-major) block by block from each tile's
 // owner, anything else (1-D profiles) from model 0.  Every copy is queued first (each
 // model's stream, behind the step), then one wait.
@@ -412,6 +429,7 @@ void download(const char *where) {
            where);
   }
   sync_all(where);
+  check_solve(where);
   for (size_t i = 0; i < g.bound.size(); i++) {
     Bound &b = g.bound[i];
     if (b.kind != 0 || b.stride == 1) continue;
@@ -808,6 +826,8 @@ void mgcm_amd_step_fence_(const int *myThid) {
   static const bool off = getenv("MGCM_AMD_STEP_FENCE") && atoi(getenv("MGCM_AMD_STEP_FENCE")) == 0;
   if (off) return;   // per-step times then measure the host's side (the steps pipeline)
   sync_all("MGCM_AMD_STEP_FENCE");
+  static unsigned nFence = 0;
+  if ((nFence++ & 7u) == 0) check_solve("MGCM_AMD_STEP_FENCE");   // every 8th fence (one small copy)
 }
 
 /* Whole-array copies so far (uploads, downloads) and their bytes. */

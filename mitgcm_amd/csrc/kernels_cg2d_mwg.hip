@@ -696,9 +696,8 @@ hipError_t launch_cg2d_mwg(const Dims &d, const Params &p, const Fields &f, cons
   hipError_t e = hipSuccess;
   size_t lds = (size_t)(2 * (T.SZ + 1) + 16 * 16 + (p.useSRCGSolver ? 2 : 1) * T.IMAX) * sizeof(double);
   // a part may claim its CU's whole LDS so that no other kernel's workgroup shares the CU
-  // (THERMODYNAMICS running beside the solve, model.hip one_step): MGCM_MWG_EXCL=1|0
-  const char *ex = getenv("MGCM_MWG_EXCL");
-  if (ex ? atoi(ex) == 1 : T.exclusive) lds = 160 * 1024;
+  // (THERMODYNAMICS running beside the solve, model.hip one_step)
+  if (T.exclusive) lds = 160 * 1024;
   const bool pinned = T.pinned && !T.sys && gN == T.G;
   const int v = (pinned ? 1 : 0) + (T.sys ? 2 : 0);
   auto kern = v == 3 ? k_cg2d_mwg<true, true> : v == 2 ? k_cg2d_mwg<false, true>

@@ -318,62 +318,6 @@ template <bool RS, bool QH>
 __global__ void __launch_bounds__(256) k_phi_flat(Dims d, Params p, Fields f) {
   phi_flat_body<RS, QH>(d, p, f, mg_xcd_block());
 }
-// phi_flat_body<false, false> with 16-byte accesses: a thread takes two adjacent columns
-// (i, i+1) with i + OLx even, so each level's rhoInSitu load and phiHydC / totPhiHyd store is one
-// double2 per lane; the pairs cover i = -1 .. sNx+2 and the columns outside the reference's
-// 0..sNx+1 are computed but not stored.  Each column's recurrence is phi_flat_body's, the two
-// chains interleaved: bit-identical.  Launched where OLx is even and nx even (launch_phi_hyd).
-__global__ void __launch_bounds__(256) k_phi_flat2(Dims d, Params p, Fields f) {
-  const int hp = (d.sNx + 4) / 2, H = d.sNy + 2;   // pairs per row: i = -1 .. sNx+2
-  const long pr = (long)mg_xcd_block() * 256 + threadIdx.x, npl = (long)hp * H;
-  if (pr >= npl * d.nT) return;
-  const int t = d.t0 + (int)(pr / npl), r = (int)(pr % npl);
-  const int i = -1 + 2 * (r % hp), j = r / hp;   // columns i, i+1 of row j (0..sNy+1)
-  const int Nr = d.Nr;
-  const bool in0 = i >= 0, in1 = i + 1 <= d.sNx + 1;   // stored columns
-  const double recip_rhoConst = 1.0 / p.rhoConst;
-  const long q2 = MG_I2(d, i, j, t);
-  const bool tot = p.storePhiHyd4Phys != 0;
-  double bEta[2] = {0.0, 0.0};
-  if (tot) { bEta[0] = f.Bo_surf[q2] * f.etaN[q2]; bEta[1] = f.Bo_surf[q2 + 1] * f.etaN[q2 + 1]; }
-  typedef __attribute__((ext_vector_type(2))) double d2;
-  double phF[2] = {0.0, 0.0};
-  for (int k0 = 1; k0 <= Nr; k0 += PHI_CH) {
-    d2 a[PHI_CH];
-#pragma unroll
-    for (int cc = 0; cc < PHI_CH; cc++) {
-      const int k = k0 + cc <= Nr ? k0 + cc : Nr;
-      a[cc] = *reinterpret_cast<const d2 *>(f.rhoInSitu + MG_I3(d, i, j, k, t));
-    }
-#pragma unroll
-    for (int cc = 0; cc < PHI_CH; cc++) {
-      const int k = k0 + cc;
-      if (k > Nr) continue;
-      const long q3 = MG_I3(d, i, j, k, t);
-      double dRlocM = 0.5 * f.drC[k - 1];
-      if (k == 1) dRlocM = f.rF[0] - f.rC[0];
-      const double dRlocP = (k == Nr) ? (f.rC[k - 1] - f.rF[k]) : 0.5 * f.drC[k];
-      double phC[2];
-#pragma unroll
-      for (int e = 0; e < 2; e++) {
-        const double al = e ? a[cc].y : a[cc].x;
-        const double sM = dRlocM * p.gravity * al * recip_rhoConst;
-        const double sP = dRlocP * p.gravity * al * recip_rhoConst;
-        phC[e] = phF[e] + sM;
-        phF[e] = phC[e] + sP;
-      }
-      if (in0 && in1) {
-        d2 v; v.x = phC[0]; v.y = phC[1];
-        *reinterpret_cast<d2 *>(f.phiHydC + q3) = v;
-        if (tot) { d2 w; w.x = phC[0] + bEta[0] + 0.0; w.y = phC[1] + bEta[1] + 0.0; *reinterpret_cast<d2 *>(f.totPhiHyd + q3) = w; }
-      } else {
-        const int e = in0 ? 0 : 1;
-        f.phiHydC[q3 + e] = phC[e];
-        if (tot) f.totPhiHyd[q3 + e] = phC[e] + bEta[e] + 0.0;
-      }
-    }
-  }
-}
 
 // whether CALC_PHI_HYD runs the flat pass: by default where neither r* nor the QH terms add
 // their per-level operands (LLC-90: 63 -> 30 us; with them, on the small r* grids, the one
@@ -2277,45 +2221,26 @@ static void vi_m2_one(const Dims &d, const VIP<C> &vp, const Fields &f, const in
   hipLaunchKernelGGL((k_mom_vi_m2<BX, BY, C, (V & 1) != 0, (V & 2) != 0, (V & 4) != 0, (V & 8) ? 2 : 1>),
                      dim3((unsigned)(nbx * nby * d.nT * nkc)), dim3(VT_NT), 0, s, d, vp, f, iterPtr, nbx, nby, KC, nkc);
 }
-// var: bit mask, 1 PF, 2 CREG, 4 EARLY, 8 at least 2 waves per SIMD (the instantiated set)
-template <int BX, int BY, unsigned C>
-static bool vi_m2_go(const Dims &d, const Params &p, const Fields &f, const int *iterPtr, int nbx, int nby, int KC,
-                     int nkc, hipStream_t s, int var) {
-  const VIP<C> vp = vi_params<C>(p);
-  switch (var) {
-    case 0: vi_m2_one<BX, BY, C, 0>(d, vp, f, iterPtr, nbx, nby, KC, nkc, s); return true;
-    case 2: vi_m2_one<BX, BY, C, 2>(d, vp, f, iterPtr, nbx, nby, KC, nkc, s); return true;
-    case 3: vi_m2_one<BX, BY, C, 3>(d, vp, f, iterPtr, nbx, nby, KC, nkc, s); return true;
-    case 6: vi_m2_one<BX, BY, C, 6>(d, vp, f, iterPtr, nbx, nby, KC, nkc, s); return true;
-    case 7: vi_m2_one<BX, BY, C, 7>(d, vp, f, iterPtr, nbx, nby, KC, nkc, s); return true;
-    case 10: vi_m2_one<BX, BY, C, 10>(d, vp, f, iterPtr, nbx, nby, KC, nkc, s); return true;
-    case 11: vi_m2_one<BX, BY, C, 11>(d, vp, f, iterPtr, nbx, nby, KC, nkc, s); return true;
-    case 14: vi_m2_one<BX, BY, C, 14>(d, vp, f, iterPtr, nbx, nby, KC, nkc, s); return true;
-    case 15: vi_m2_one<BX, BY, C, 15>(d, vp, f, iterPtr, nbx, nby, KC, nkc, s); return true;
-    default: return false;
-  }
-}
-// MGCM_VI_M2=0 keeps the generic march (A/B); MGCM_VI_MARCH_VAR picks the PF/CREG variant as
-// for k_mom_vi_march
+// k_mom_vi_m2 as launched: the output point's metrics held in registers across the march
+// (CREG), its own HBM reads of a level issued at the level's start (EARLY), registers capped
+// for 2 waves per SIMD, level k+1 fetched after level k (LLC-90: 456-459 us; CREG alone 487,
+// neither 534, the generic march 527; prefetching level k+1 into registers 513-740 (1 wave per
+// SIMD or spills); a U/V-split 512-thread form 492, the same with a double-buffered prefetch
+// 501, a two-pass form (intermediates through HBM, per-point tendencies) 585:
+// profiles/r03/vi_m2/; the ring-point intermediates of the 31 x 8 block's second pass dealt
+// out by quantity over the four waves 459 -> 518 us, profiles/r04/llc_ab/).  false where the
+// run's option code or block shape has no instantiation (the generic march runs then).
 static bool vi_m2_launch(const Dims &d, const Params &p, const Fields &f, const int *iterPtr, int BX, int BY, int nbx,
                          int nby, int KC, int nkc, hipStream_t s) {
-  // read per launch (tests switch them per model)
-  const bool on = !getenv("MGCM_VI_M2") || atoi(getenv("MGCM_VI_M2")) != 0;
-  // (round 4, measured and dropped, profiles/r04/llc_ab/: the ring-point intermediates of the
-  // 31 x 8 block's second pass dealt out by quantity over the four waves, 459 -> 518 us)
-  // MGCM_VI_M2_VAR (bit mask, vi_m2_go); default 14: the output point's metrics held in
-  // registers across the march (CREG), its own HBM reads of a level issued at the level's
-  // start (EARLY), registers capped for 2 waves per SIMD, level k+1 fetched after level k
-  // (LLC-90: 456-459 us; CREG alone 487, neither 534, the generic march 527; prefetching
-  // level k+1 into registers 513-740 (1 wave per SIMD or spills); measured and dropped: a
-  // U/V-split 512-thread form 492, the same with a double-buffered prefetch 501, a two-pass
-  // form (intermediates through HBM, per-point tendencies) 585: profiles/r03/vi_m2/)
-  const int var = getenv("MGCM_VI_M2_VAR") ? atoi(getenv("MGCM_VI_M2_VAR")) : 14;
-  if (!on) return false;
   const unsigned code = vi_opt_code(p);
-  if (getenv("MGCM_VI_M2_DEBUG")) fprintf(stderr, "vi_m2: BX %d BY %d code %#x (LLC %#x)\n", BX, BY, code, VI_CODE_LLC);
-  if (code == VI_CODE_LLC && BX == 31 && BY == 8) return vi_m2_go<31, 8, VI_CODE_LLC>(d, p, f, iterPtr, nbx, nby, KC, nkc, s, var);
-  if (code == VI_CODE_LLC && BX == 32 && BY == 8) return vi_m2_go<32, 8, VI_CODE_LLC>(d, p, f, iterPtr, nbx, nby, KC, nkc, s, var);
+  if (code == VI_CODE_LLC && BX == 31 && BY == 8) {
+    vi_m2_one<31, 8, VI_CODE_LLC, 14>(d, vi_params<VI_CODE_LLC>(p), f, iterPtr, nbx, nby, KC, nkc, s);
+    return true;
+  }
+  if (code == VI_CODE_LLC && BX == 32 && BY == 8) {
+    vi_m2_one<32, 8, VI_CODE_LLC, 14>(d, vi_params<VI_CODE_LLC>(p), f, iterPtr, nbx, nby, KC, nkc, s);
+    return true;
+  }
   return false;
 }
 
@@ -2326,14 +2251,9 @@ static void vi_tile_shape(const Dims &d, int &BX, int &BY) {
   BX = (W + nbx - 1) / nbx;                 // 92 -> 31, 34 -> 17 (two blocks), <= 32
   BY = VT_NT / BX;
   while (BY > 1 && ((BX + 2) * (BY + 2) > VT_EMAX || (BX + 1) * (BY + 1) > VT_IMAX)) BY--;
-  // MGCM_VI_BY caps the rows (A/B).  7 keeps a 31-wide block's (BX+1)(BY+1) intermediate
-  // points within one pass of the 256 threads, but the specialised k-march at 31 x 7 (more
-  // blocks, more spills) measured slower on LLC-90: 1.58-1.60 against 1.54-1.56 ms/step
-  // (profiles/r04/viby/), so only 31 x 8 / 32 x 8 are instantiated
-  if (const char *e = getenv("MGCM_VI_BY")) {
-    const int cap = atoi(e);
-    if (cap >= 1 && cap < BY) BY = cap;
-  }
+  // (7 rows keep a 31-wide block's (BX+1)(BY+1) intermediate points within one pass of the
+  // 256 threads, but the specialised k-march at 31 x 7 (more blocks, more spills) measured
+  // slower on LLC-90: 1.58-1.60 against 1.54-1.56 ms/step, profiles/r04/viby/)
   const int nby = (H + BY - 1) / BY;
   BY = (H + nby - 1) / nby;                 // balance the rows over the blocks
 }
@@ -2413,10 +2333,7 @@ bool phys_phi_fusable(const Dims &d, const Params &p) {
 }
 hipError_t launch_phys_phi(const Dims &d, const Params &p, const Fields &f, const int *iterPtr, hipStream_t s) {
   const long ncol = (long)d.nx * d.ny * d.nT;
-  // columns per workgroup (MGCM_PHYS_NC = 16 | 32 | 64; the per-point DO_OCEANIC_PHYS loads
-  // want long runs along i)
-  const int ncEnv = getenv("MGCM_PHYS_NC") ? atoi(getenv("MGCM_PHYS_NC")) : 16;
-  const int nc = (ncEnv == 16 || ncEnv == 32 || ncEnv == 64) ? ncEnv : 16;
+  const int nc = 16;   // columns per workgroup
   MG_ALLOW_LDS(k_phys_phi);
   hipLaunchKernelGGL(k_phys_phi, dim3(mg_colf_blocks(ncol, nc)), dim3(256), mg_colf_lds(d.Nr, nc, 6), s, d, p, f, nc,
                      iterPtr);
@@ -2425,12 +2342,10 @@ hipError_t launch_phys_phi(const Dims &d, const Params &p, const Fields &f, cons
 
 hipError_t launch_phi_hyd(const Dims &d, const Params &p, const Fields &f, hipStream_t s) {
   const long ncol = (long)(d.sNx + 3) * (d.sNy + 3) * d.nT;
-  // LDS slices: the phi sums need 3 (sM, sP, sPh); r* adds MOM_CALC_RTRANS's 3.  Columns per
-  // workgroup: MGCM_PHI_NC = 16 | 32 | 64 (sweeps), else mg_colf_nc's
+  // LDS slices: the phi sums need 3 (sM, sP, sPh); r* adds MOM_CALC_RTRANS's 3
   const bool rstar = p.nonlinFreeSurf > 0 && p.select_rStar > 0;
   const int nArr = rstar ? 6 : 3;
-  const int ncEnv = getenv("MGCM_PHI_NC") ? atoi(getenv("MGCM_PHI_NC")) : 0;
-  const int nc = (ncEnv == 16 || ncEnv == 32 || ncEnv == 64) ? ncEnv : mg_colf_nc(ncol, d.Nr, nArr);
+  const int nc = mg_colf_nc(ncol, d.Nr, nArr);
   if (phi_del2_fused(d, p)) {
     MG_ALLOW_LDS(k_phi_del2);
     const unsigned nbPhi = mg_colf_blocks(ncol, nc), nbDel = mg_plane_blocks(d.nx, d.ny, d.nT * d.Nr);
@@ -2440,16 +2355,8 @@ hipError_t launch_phi_hyd(const Dims &d, const Params &p, const Fields &f, hipSt
   // the flat per-column form (phi_flat_on)
   if (phi_flat_on(p)) {
     const bool qh = p.quasiHydrostatic && (p.select3dCoriScheme >= 1 || p.useNHMTerms);
-    auto al = [](const void *q) { return ((uintptr_t)q & 15u) == 0; };
-    // opt-in (MGCM_PHI_V2=1): bit-identical but slower on LLC-90, 32.8 against 30.4 us -- half
-    // the threads of a one-thread-per-column pass leave the chip under-filled (220 workgroups)
-    const int v2Env = getenv("MGCM_PHI_V2") ? atoi(getenv("MGCM_PHI_V2")) : 0;
-    if (!rstar && !qh && v2Env != 0 && (d.OLx & 1) == 0 && (d.nx & 1) == 0 && (d.n3 & 1) == 0 && al(f.rhoInSitu) &&
-        al(f.phiHydC) && al(f.totPhiHyd)) {
-      const long np = (long)((d.sNx + 4) / 2) * (d.sNy + 2) * d.nT;
-      hipLaunchKernelGGL(k_phi_flat2, dim3((unsigned)((np + 255) / 256)), dim3(256), 0, s, d, p, f);
-      return hipGetLastError();
-    }
+    // (round 4: a two-columns-per-thread form was bit-identical but slower on LLC-90, 32.8
+    // against 30.4 us -- half the threads leave the chip under-filled; removed in round 5)
     auto kern = rstar ? (qh ? k_phi_flat<true, true> : k_phi_flat<true, false>)
                       : (qh ? k_phi_flat<false, true> : k_phi_flat<false, false>);
     hipLaunchKernelGGL(kern, dim3((unsigned)phi_flat_blocks(d, p)), dim3(256), 0, s, d, p, f);
@@ -2469,8 +2376,7 @@ static hipError_t launch_mom_tail(const Dims &d, const Params &p, const Fields &
 // it), so the resident step may run it on the second stream beside the pressure solve
 // (one_step, MG_FUSE_RING).  ring = false: launch_mom_step leaves it to launch_mom_ring.
 static bool vi_march_path(const Dims &d, const Params &p) {
-  static const bool viPoint = getenv("MGCM_VI_POINT") != nullptr;
-  return p.vectorInvariantMomentum && !viPoint && d.OLx >= 2 && d.OLy >= 2 && p.selectVortScheme <= 2;
+  return p.vectorInvariantMomentum && d.OLx >= 2 && d.OLy >= 2 && p.selectVortScheme <= 2;
 }
 bool mom_ring_separable(const Dims &d, const Params &p) {
   return vi_march_path(d, p) && !p.useCDscheme && 2 * (d.OLy - 1) * d.nx + (d.sNy + 2) * 2 * (d.OLx - 1) > 0;
@@ -2484,50 +2390,40 @@ hipError_t launch_mom_ring(const Dims &d, const Params &p, const Fields &f, cons
 hipError_t launch_mom_step(const Dims &d, const Params &p, const Fields &f, const int *iterPtr, hipStream_t s, bool ring) {
   if (del2_needed(p) && !phi_del2_fused(d, p))
     hipLaunchKernelGGL(k_del2uv, dim3(mg_plane_blocks(d.nx, d.ny, d.nT * d.Nr)), dim3(MG_PLANE_THREADS), 0, s, d, p, f);
-  // MOM_VECINV or MOM_FLUXFORM: separate instantiations (no register-pressure coupling);
-  // MGCM_VI_POINT: the per-point form, for comparison
+  // MOM_VECINV or MOM_FLUXFORM: separate instantiations (no register-pressure coupling)
   if (vi_march_path(d, p)) {
     int BX, BY;
     vi_tile_shape(d, BX, BY);
     const int nbx = (d.sNx + 2 + BX - 1) / BX, nby = (d.sNy + 2 + BY - 1) / BY;
     // levels per workgroup: enough workgroups to fill the chip several times, few enough
-    // that the two extra staged levels per chunk stay a small overhead
-    const int kcEnv = getenv("MGCM_VI_KC") ? atoi(getenv("MGCM_VI_KC")) : 0;
-    const char *viEnv = getenv("MGCM_VI_KERNEL");   // march | level | tiled (sweeps; read per launch)
-    // the k-march for deep grids (Nr >= 30 with >= 256 workgroups per level chunk); round 3's
-    // generic march ran best in five chunks of levels (527 us alone on LLC-90 against 634 with
-    // two and ~640 for the per-level kernel, profiles/r03/ab/).  MGCM_VI_KERNEL=level|march|tiled and MGCM_VI_KC
-    // override (sweeps).
-    // (round 4, k_mom_vi_m2: two chunks are now the faster split, LLC-90 448-456 us against
-    // 460 at five and 453-460 at three, step 1.531-1.545 against 1.550-1.552 ms,
-    // profiles/r04/vikc/)
+    // that the two extra staged levels per chunk stay a small overhead.  The k-march for deep
+    // grids (Nr >= 30 with >= 256 workgroups per level chunk), in two chunks of levels (round
+    // 4, k_mom_vi_m2: LLC-90 448-456 us against 460 at five and 453-460 at three, step
+    // 1.531-1.545 against 1.550-1.552 ms, profiles/r04/vikc/); otherwise one level per
+    // workgroup.  MGCM_VI_KERNEL = march | march_generic | level | tiled forces a form (the
+    // tests run each: march_generic is the generic k-march that serves option sets without
+    // a k_mom_vi_m2 instantiation; read per launch)
+    const char *viEnv = getenv("MGCM_VI_KERNEL");
     const int nbt = nbx * nby * d.nT;
-    int KCm = (d.Nr + 1) / 2;
-    if (kcEnv > 0) KCm = kcEnv > d.Nr ? d.Nr : kcEnv;
-    const bool march = viEnv ? !strcmp(viEnv, "march") : (d.Nr >= 30 && nbt >= 256);
+    const int KCm = (d.Nr + 1) / 2;
+    const bool generic = viEnv && !strcmp(viEnv, "march_generic");
+    const bool march = viEnv ? (!strcmp(viEnv, "march") || generic) : (d.Nr >= 30 && nbt >= 256);
     if (march) {
       const int nkc = (d.Nr + KCm - 1) / KCm;
-      if (!vi_m2_launch(d, p, f, iterPtr, BX, BY, nbx, nby, KCm, nkc, s)) {
-        const int var = getenv("MGCM_VI_MARCH_VAR") ? atoi(getenv("MGCM_VI_MARCH_VAR")) : 0;
-        auto kern = var == 1 ? k_mom_vi_march<true, true> : var == 2 ? k_mom_vi_march<true, false>
-                  : var == 3 ? k_mom_vi_march<false, true> : k_mom_vi_march<false, false>;
-        hipLaunchKernelGGL(kern, dim3((unsigned)(nbt * nkc)), dim3(VT_NT), 0, s, d, p, f, iterPtr, BX, BY, nbx, nby, KCm,
-                           nkc);
-      }
-    } else if (kcEnv <= 0 || (viEnv && !strcmp(viEnv, "level"))) {   // one level per workgroup
+      if (generic || !vi_m2_launch(d, p, f, iterPtr, BX, BY, nbx, nby, KCm, nkc, s))
+        hipLaunchKernelGGL((k_mom_vi_march<false, false>), dim3((unsigned)(nbt * nkc)), dim3(VT_NT), 0, s, d, p, f, iterPtr,
+                           BX, BY, nbx, nby, KCm, nkc);
+    } else if (!(viEnv && !strcmp(viEnv, "tiled"))) {   // one level per workgroup
       hipLaunchKernelGGL(k_mom_vi_level, dim3((unsigned)(nbx * nby * d.nT * d.Nr)), dim3(VT_NT), 0, s, d, p, f, iterPtr, BX,
                          BY, nbx, nby);
-    } else {            // MGCM_VI_KC levels marched per workgroup
-      const int KC = kcEnv > d.Nr ? d.Nr : kcEnv, nkc = (d.Nr + KC - 1) / KC;
-      hipLaunchKernelGGL(k_mom_vi_tiled, dim3((unsigned)(nbx * nby * d.nT * nkc)), dim3(VT_NT), 0, s, d, p, f, iterPtr, BX,
-                         BY, nbx, nby, KC, nkc);
+    } else {            // KCm levels marched per workgroup, the tiled form
+      const int nkc = (d.Nr + KCm - 1) / KCm;
+      hipLaunchKernelGGL(k_mom_vi_tiled, dim3((unsigned)(nbt * nkc)), dim3(VT_NT), 0, s, d, p, f, iterPtr, BX, BY, nbx,
+                         nby, KCm, nkc);
     }
     if (ring || p.useCDscheme) launch_mom_ring(d, p, f, iterPtr, s);
   } else if (p.vectorInvariantMomentum)
     hipLaunchKernelGGL(k_mom_step<true>, dim3(mg_plane_blocks(d.nx, d.ny, d.nT * d.Nr)), dim3(MG_PLANE_THREADS), 0, s,
-                       d, p, f, iterPtr);
-  else if (getenv("MGCM_MOM_NOSPLIT"))
-    hipLaunchKernelGGL(k_mom_step<false>, dim3(mg_plane_blocks(d.nx, d.ny, d.nT * d.Nr)), dim3(MG_PLANE_THREADS), 0, s,
                        d, p, f, iterPtr);
   else if (mom_ff4_on())   // MOM_FLUXFORM: four threads per point (U, V x viscous or not)
     hipLaunchKernelGGL(k_mom_ff4, dim3((unsigned)mom_ff4_blocks(d)), dim3(256), 0, s, d, p, f, iterPtr);

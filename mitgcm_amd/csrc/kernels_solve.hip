@@ -766,16 +766,13 @@ __device__ __forceinline__ double block_max_nw(double v, double *red, int slot) 
 #endif
 // FMA: the operator rows, dot products and vector updates as fused multiply-adds in a fixed
 // order (cg2dUseFMA; the oracle's device-order mode evaluates the same fma chains)
-// RC (recompute): no barrier before the two operator applications.  A thread derives the
-// out-of-block neighbour values it needs from the neighbour's inputs in LDS with the owner's
-// own expression -- s = q + beta*s from (q, s_old), r = r - alpha*A s from (r_old, A s) -- so
-// the values are the owner's bits, and only the two reduction barriers stay per iteration
-// (4 LDS arrays: r, s, q = M r, A s; the owner's own r and s are written after the barrier
-// that retires their readers).
+// (round 3 measured a recompute form without the barrier before the two operator
+// applications -- out-of-block neighbour values re-derived from their inputs: bit-identical
+// but 2.54 us/iteration against 1.82, 256 VGPRs + 29 spilled; removed in round 5)
 // SR: CG2D_SR (cg2d_sr.F, useSRCGSolver) -- one standard step, then per iteration y = M r,
 // v = A y and the three sums (y.r, y.v, r.r) in one reduction: three barriers per iteration
 // (y, the reduction, r) instead of four; s_l holds y.
-template <int BX, int BY, int NT, bool MINRES, bool FMA, bool RC = false, bool SR = false>
+template <int BX, int BY, int NT, bool MINRES, bool FMA, bool SR = false>
 __global__ void __launch_bounds__(NT) k_cg2d_bxy(Dims d, Params p, Fields f, const unsigned *__restrict__ nbx,
                                                  const int *__restrict__ blkx, int nBlk, int maxIters, int nIterMinIn,
                                                  SolveRecord *rec, int *stepCounter, const int *__restrict__ slot2,
@@ -785,7 +782,6 @@ __global__ void __launch_bounds__(NT) k_cg2d_bxy(Dims d, Params p, Fields f, con
   double *r_l = lds;               // NP + 1 (last = ZERO slot)
   double *s_l = lds + (NP + 1);
   double *red = lds + 2 * (NP + 1);  // 4 x 16 partial slots
-  double *q_l = red + 64, *as_l = q_l + (NP + 1);   // RC only: q = M r and A s
   const int tid = threadIdx.x;
   const bool act = tid < nBlk;
   const int bt = act ? tid : 0;
@@ -925,7 +921,6 @@ __global__ void __launch_bounds__(NT) k_cg2d_bxy(Dims d, Params p, Fields f, con
 #pragma unroll
     for (int a = 0; a < BX; a++) { r_l[cs[b][a]] = r[b][a]; s_l[cs[b][a]] = 0.0; }
   if (tid == 0) { r_l[NP] = 0.0; s_l[NP] = 0.0; }
-  if (RC && tid == 0) { q_l[NP] = 0.0; as_l[NP] = 0.0; }
   const double firstResidual = sqrt(err_sq);
   int nIterMin = nIterMinIn;
   double minResidualSq = -1.0;
@@ -1030,12 +1025,6 @@ __global__ void __launch_bounds__(NT) k_cg2d_bxy(Dims d, Params p, Fields f, con
   if (!SR && !(err_sq < p.cg2dTolerance_sq)) {
     double q[BY][BX];
     apply(r_l, r, q, true);
-    if (RC) {
-#pragma unroll
-      for (int b = 0; b < BY; b++)
-#pragma unroll
-        for (int a = 0; a < BX; a++) q_l[cs[b][a]] = q[b][a];
-    }
     double e = 0.0;
 #pragma unroll
     for (int b = 0; b < BY; b++)
@@ -1047,70 +1036,6 @@ __global__ void __launch_bounds__(NT) k_cg2d_bxy(Dims d, Params p, Fields f, con
     const unsigned long long stampT0 = __builtin_amdgcn_s_memtime(), stampR0 = __builtin_amdgcn_s_memrealtime();
     __builtin_amdgcn_s_waitcnt(0xC07F);
 #endif
-    if constexpr (RC) for (int it2d = 1; it2d <= maxIters; it2d++) {
-      const double cgBeta = eta_qrN / eta_qrNM1;
-      eta_qrNM1 = eta_qrN;
-      {
-        if (it2d > 1) {   // the previous iteration's r, now that its neighbour readers are past D
-#pragma unroll
-          for (int b = 0; b < BY; b++)
-#pragma unroll
-            for (int a = 0; a < BX; a++) r_l[cs[b][a]] = r[b][a];
-        }
-#pragma unroll
-        for (int b = 0; b < BY; b++)
-#pragma unroll
-          for (int a = 0; a < BX; a++) sv[b][a] = FMA ? __builtin_fma(cgBeta, sv[b][a], q[b][a]) : q[b][a] + cgBeta * sv[b][a];
-        // A s with the neighbours' s = q + beta*s_old formed here from their (q, s_old)
-        apply_nb([&](int sl) { return FMA ? __builtin_fma(cgBeta, s_l[sl], q_l[sl]) : q_l[sl] + cgBeta * s_l[sl]; }, sv, q,
-                 false);
-        double aa = 0.0;
-#pragma unroll
-        for (int b = 0; b < BY; b++)
-#pragma unroll
-          for (int a = 0; a < BX; a++) {
-            as_l[cs[b][a]] = q[b][a];
-            aa = FMA ? __builtin_fma(sv[b][a], q[b][a], aa) : aa + sv[b][a] * q[b][a];
-          }
-        aslot = aslot ^ 1;
-        double alpha = block_sum_nw<NW>(aa, red, aslot);   // barrier B
-        alpha = eta_qrN / alpha;
-        double e2 = 0.0;
-#pragma unroll
-        for (int b = 0; b < BY; b++)
-#pragma unroll
-          for (int a = 0; a < BX; a++) {
-            s_l[cs[b][a]] = sv[b][a];   // for the next iteration's neighbours (read after D)
-            x[b][a] = FMA ? __builtin_fma(alpha, sv[b][a], x[b][a]) : x[b][a] + alpha * sv[b][a];
-            r[b][a] = FMA ? __builtin_fma(-alpha, q[b][a], r[b][a]) : r[b][a] - alpha * q[b][a];
-            e2 = FMA ? __builtin_fma(r[b][a], r[b][a], e2) : e2 + r[b][a] * r[b][a];
-          }
-        actualIts = it2d;
-        // M r with the neighbours' r = r_old - alpha*(A s) formed here from their (r_old, A s)
-        apply_nb([&](int sl) { return FMA ? __builtin_fma(-alpha, as_l[sl], r_l[sl]) : r_l[sl] - alpha * as_l[sl]; }, r, q,
-                 true);
-        double en = 0.0;
-#pragma unroll
-        for (int b = 0; b < BY; b++)
-#pragma unroll
-          for (int a = 0; a < BX; a++) {
-            q_l[cs[b][a]] = q[b][a];
-            en = FMA ? __builtin_fma(q[b][a], r[b][a], en) : en + q[b][a] * r[b][a];
-          }
-        block_sum2_nw<NW>(e2, en, red, 0);   // barrier D
-        err_sq = e2;
-        eta_qrN = en;
-        if (err_sq < p.cg2dTolerance_sq) break;
-        if (MINRES && err_sq < minResidualSq) {
-          minResidualSq = err_sq;
-          nIterMin = it2d;
-#pragma unroll
-          for (int b = 0; b < BY; b++)
-#pragma unroll
-            for (int a = 0; a < BX; a++) xmin[b][a] = x[b][a];
-        }
-      }
-    }
     // the standard iteration, unrolled by two: the loop-carried s and q then need no register
     // copies at the back edge (each copy of the body may hold them in the other's registers)
     auto iter = [&](int it2d) -> bool {
@@ -1172,7 +1097,7 @@ __global__ void __launch_bounds__(NT) k_cg2d_bxy(Dims d, Params p, Fields f, con
       }
       return false;
     };
-    if constexpr (!RC) {
+    {
       bool done = false;
       int it2d = 1;
       for (; !done && it2d + 1 <= maxIters; it2d += 2) done = iter(it2d) || iter(it2d + 1);
@@ -1518,129 +1443,6 @@ __global__ void __launch_bounds__(256) k_corr_cont(Dims d, Params p, Fields f, i
   }
 }
 
-// k_corr_cont (atInit = 0, the step path) with 16-byte accesses: a thread slot owns two
-// adjacent columns (i, i+1), i odd, so every 3-D load and store of the level loop is one
-// double2 per lane (the 8-B-lane rate of the one-column form, 3.1 TB/s on LLC-90, against the
-// 16-B rate).  u at i+1 is the corrected u1 of column i and the u0 of column i+1: one
-// uCor, the same bits.  The LDS slices hold (column pair, level) as double2; the serial
-// column sums and the upward w recurrence run both columns in one thread, interleaved.
-// Same expressions in the same order as k_corr_cont: bit-identical.  Launched where sNx and
-// OLx are even and the fields 16-B aligned (launch_corr_cont).
-typedef __attribute__((ext_vector_type(2))) double dbl2;
-__global__ void __launch_bounds__(256) k_corr_cont2(Dims d, Params p, Fields f, int nc, const long *__restrict__ etaSrc) {
-  extern __shared__ __attribute__((aligned(16))) double lds[];
-  const int NC_ = nc, KW_ = 256 / NC_;
-  const int cc = (int)threadIdx.x % NC_, kk = (int)threadIdx.x / NC_;
-  const int hx = d.sNx >> 1;
-  const long pr_ = (long)mg_xcd_block() * NC_ + cc, npl = (long)hx * d.sNy;
-  const bool valid = pr_ < npl * d.nT;
-  const int t = d.t0 + (int)(valid ? pr_ / npl : 0);
-  const long rr = valid ? pr_ % npl : 0;
-  const int i = 1 + 2 * (int)(rr % hx), j = 1 + (int)(rr / hx);
-  const int NS = d.Nr * NC_;   // double2 slots per slice
-  dbl2 *sDiv = reinterpret_cast<dbl2 *>(lds), *sMask = sDiv + NS, *sU = sDiv + 2 * NS, *sV = sDiv + 3 * NS,
-       *sH0 = sDiv + 4 * NS;
-  auto ld2 = [](const double *a, long q) { return *reinterpret_cast<const dbl2 *>(a + q); };
-  const long q = MG_I2(d, i, j, t);
-  const bool rstar = p.nonlinFreeSurf > 0 && p.select_rStar != 0;
-  if (valid) {
-    const double psFac = p.pfFacMom * p.implicSurfPress;
-    auto eta = [&](long qq) {
-      if (!etaSrc) return f.etaN[qq];
-      const long sq = etaSrc[qq];
-      return f.recip_Bo[qq] * f.cg2d_x[sq >= 0 ? sq : qq];
-    };
-    auto phiX = [&](int ii, int jj) {
-      const long qq = MG_I2(d, ii, jj, t);
-      return f.recip_dxC[qq] * (f.Bo_surf[qq] * eta(qq) - f.Bo_surf[MG_I2(d, ii - 1, jj, t)] * eta(MG_I2(d, ii - 1, jj, t)));
-    };
-    auto phiY = [&](int ii, int jj) {
-      const long qq = MG_I2(d, ii, jj, t);
-      return f.recip_dyC[qq] * (f.Bo_surf[qq] * eta(qq) - f.Bo_surf[MG_I2(d, ii, jj - 1, t)] * eta(MG_I2(d, ii, jj - 1, t)));
-    };
-    // the pair's surface-pressure gradients: u at i, i+1, i+2; v at j, j+1 of both columns
-    const double pX0 = phiX(i, j), pX1 = phiX(i + 1, j), pX2 = phiX(i + 2, j);
-    const double pY0a = phiY(i, j), pY0b = phiY(i + 1, j), pY1a = phiY(i, j + 1), pY1b = phiY(i + 1, j + 1);
-    const double dyG0 = f.dyG[q], dyG1 = f.dyG[q + 1], dyG2 = f.dyG[q + 2];
-    const double dxG0a = f.dxG[q], dxG0b = f.dxG[q + 1], dxG1a = f.dxG[q + d.nx], dxG1b = f.dxG[q + d.nx + 1];
-    for (int k = kk + 1; k <= d.Nr; k += KW_) {
-      const int me = (k - 1) * NC_ + cc;
-      const long q3 = MG_I3(d, i, j, k, t), q3n = q3 + d.nx;
-      const dbl2 gU01 = ld2(f.gU, q3), gU23 = ld2(f.gU, q3 + 2), mW01 = ld2(f.maskW, q3), mW23 = ld2(f.maskW, q3 + 2);
-      const dbl2 gV0 = ld2(f.gV, q3), gV1 = ld2(f.gV, q3n), mS0 = ld2(f.maskS, q3), mS1 = ld2(f.maskS, q3n);
-      const dbl2 hW01 = ld2(f.hFacW, q3), hW23 = ld2(f.hFacW, q3 + 2), hS0 = ld2(f.hFacS, q3), hS1 = ld2(f.hFacS, q3n);
-      const dbl2 mC = ld2(f.maskC, q3);
-      auto cor = [&](double g, double m, double ps) { return (g + p.deltaTMom * (-psFac * ps * m)) * m; };
-      const double u0 = cor(gU01.x, mW01.x, pX0), u1 = cor(gU01.y, mW01.y, pX1), u2 = cor(gU23.x, mW23.x, pX2);
-      const double v0a = cor(gV0.x, mS0.x, pY0a), v0b = cor(gV0.y, mS0.y, pY0b);
-      const double v1a = cor(gV1.x, mS1.x, pY1a), v1b = cor(gV1.y, mS1.y, pY1b);
-      sU[me] = dbl2{u0, u1};
-      sV[me] = dbl2{v0a, v0b};
-      const double drF = f.drF[k - 1];
-      const double uT1a = u1 * dyG1 * drF * hW01.y, uT0a = u0 * dyG0 * drF * hW01.x;
-      const double vT1a = v1a * dxG1a * drF * hS1.x, vT0a = v0a * dxG0a * drF * hS0.x;
-      const double uT1b = u2 * dyG2 * drF * hW23.x, uT0b = u1 * dyG1 * drF * hW01.y;
-      const double vT1b = v1b * dxG1b * drF * hS1.y, vT0b = v0b * dxG0b * drF * hS0.y;
-      sDiv[me] = dbl2{uT1a - uT0a + vT1a - vT0a, uT1b - uT0b + vT1b - vT0b};
-      sMask[me] = mC;
-      if (rstar) sH0[me] = ld2(f.h0FacC, q3);
-    }
-  }
-  __syncthreads();
-  if (valid && kk == 0) {
-    double rStarDhDt[2] = {0.0, 0.0};
-    if (p.exactConserv) {
-      double hDiv[2] = {0.0, 0.0};
-      for (int k2 = 1; k2 <= d.Nr; k2++) {
-        const dbl2 m2 = sMask[(k2 - 1) * NC_ + cc], v2 = sDiv[(k2 - 1) * NC_ + cc];
-        hDiv[0] = hDiv[0] + m2.x * v2.x;
-        hDiv[1] = hDiv[1] + m2.y * v2.y;
-      }
-#pragma unroll
-      for (int e = 0; e < 2; e++) {
-        const long qe = q + e;
-        const double facEmP = p.useRealFreshWaterFlux ? 1.0 / p.rhoConst : 0.0;   // integr_continuity.F:183-188
-        const double dEtaHdt = -(hDiv[e] * f.recip_rA[qe]) - facEmP * f.EmPmR[qe];
-        f.cg2d_b[qe] = f.etaH[qe] + p.implicDiv2DFlow * dEtaHdt * p.deltaTFreeSurf;
-        if (f.dEtaHdt) f.dEtaHdt[qe] = dEtaHdt;
-        if (rstar) rStarDhDt[e] = dEtaHdt * f.recip_Rcol[qe];   // integr_continuity.F:171-183
-      }
-    }
-    double wBelow[2] = {0.0, 0.0};
-    const double rA1[2] = {f.recip_rA[q], f.recip_rA[q + 1]};
-    for (int k2 = d.Nr; k2 >= 1; k2--) {
-      const int s2 = (k2 - 1) * NC_ + cc;
-      const dbl2 dv = sDiv[s2], mk = sMask[s2];
-      const dbl2 h0 = rstar ? sH0[s2] : dbl2{0.0, 0.0};
-      double w[2];
-#pragma unroll
-      for (int e = 0; e < 2; e++) {
-        const double conv2d = -(e ? dv.y : dv.x), msk = e ? mk.y : mk.x;
-        if (rstar) {
-          const double dh = rStarDhDt[e] * f.drF[k2 - 1] * (e ? h0.y : h0.x);
-          if (k2 == d.Nr) w[e] = (conv2d * rA1[e] - dh) * msk;
-          else w[e] = (wBelow[e] + conv2d * rA1[e] - dh) * msk;
-        } else if (k2 == d.Nr) {
-          w[e] = conv2d * rA1[e] * msk;
-        } else {
-          w[e] = (wBelow[e] + conv2d * rA1[e]) * msk;
-        }
-        wBelow[e] = w[e];
-      }
-      sDiv[s2] = dbl2{w[0], w[1]};
-    }
-  }
-  __syncthreads();
-  if (valid)
-    for (int k = kk + 1; k <= d.Nr; k += KW_) {
-      const int me = (k - 1) * NC_ + cc;
-      const long q3 = MG_I3(d, i, j, k, t);
-      *reinterpret_cast<dbl2 *>(f.wVel + q3) = sDiv[me];
-      *reinterpret_cast<dbl2 *>(f.uVel + q3) = sU[me];
-      *reinterpret_cast<dbl2 *>(f.vVel + q3) = sV[me];
-    }
-}
-
 // Tile-sharded runs: gather (pack) / scatter (unpack) the halo-source points a peer
 // needs, for every exchanged field and level: buf[(f*Nr + k)*n + h] <-> field at 2-D
 // offset idx[h] (t*n2 + local) of level k.
@@ -1663,10 +1465,9 @@ __global__ void k_bump_counter(int *c, int nIncr) {
 // ------------------------------------------------------------------ launchers
 hipError_t launch_sfp_rhs(const Dims &d, const Params &p, const Fields &f, hipStream_t s) {
   const long ncol = (long)d.nx * d.ny * d.nT;
-  // MGCM_SFP_NC = 16 | 32 | 64 (read per launch, A/B), else mg_colf_nc's 16 (LLC-90: 63 us at
-  // 16, 69 at 32, 115 at 64; profiles/r04/sfpnc/, where the correction pass's 32 is confirmed too)
-  const int ncEnv = getenv("MGCM_SFP_NC") ? atoi(getenv("MGCM_SFP_NC")) : 0;
-  const int nc = (ncEnv == 16 || ncEnv == 32 || ncEnv == 64) ? ncEnv : mg_colf_nc(ncol, d.Nr, 4);
+  // mg_colf_nc's 16 columns (LLC-90: 63 us at 16, 69 at 32, 115 at 64; profiles/r04/sfpnc/,
+  // where the correction pass's 32 is confirmed too)
+  const int nc = mg_colf_nc(ncol, d.Nr, 4);
   MG_ALLOW_LDS(k_sfp_rhs);
   hipLaunchKernelGGL(k_sfp_rhs, dim3(mg_colf_blocks(ncol, nc)), dim3(256), mg_colf_lds(d.Nr, nc, 4), s, d, p, f, nc);
   return hipGetLastError();
@@ -1714,15 +1515,10 @@ hipError_t launch_cg2d_block(const Dims &d, const Params &p, const Fields &f, co
   if (!ppt) return hipErrorInvalidValue;
   const size_t lds = cg2d_block_lds_bytes(ppt);
   const bool mr = nIterMin >= 0;
-  // experiment knob: MGCM_CG2D_CREG=0/1/2 forces the coefficient caching tier at PPT=4
-  static int creg_override = [] { const char *e = getenv("MGCM_CG2D_CREG"); return e ? atoi(e) : -1; }();
 #define LAUNCH(PPT)                                                                                        \
   do {                                                                                                     \
     constexpr int CR = (PPT <= 2) ? 2 : (PPT <= 4 ? 1 : 0);                                                                 \
     auto kern = mr ? k_cg2d_block<PPT, true, CR> : k_cg2d_block<PPT, false, CR>;                           \
-    if (PPT == 4 && creg_override >= 0)                                                                    \
-      kern = creg_override == 2 ? (mr ? k_cg2d_block<4, true, 2> : k_cg2d_block<4, false, 2>)             \
-           : creg_override == 1 ? (mr ? k_cg2d_block<4, true, 1> : k_cg2d_block<4, false, 1>) : kern;     \
     hipError_t e_ = hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds); \
     if (e_ != hipSuccess) return e_;                                                                       \
     hipLaunchKernelGGL(kern, dim3(1), dim3(CG_THREADS), lds, s, d, p, f, nbr, gofs, nPts, maxIters, nIterMin, rec, \
@@ -1758,18 +1554,12 @@ static hipError_t launch_bxy_t(const Dims &d, const Params &p, const Fields &f, 
                                int nBlk, int maxIters, int nIterMin, SolveRecord *rec, int *stepCounter, const int *slot2,
                                const long *srcOf, hipStream_t s) {
   if (nBlk > NT) return hipErrorInvalidValue;
-  // the recompute form (RC) only with MGCM_CG2D_RC=1: on config 2 it is bit-identical but
-  // 2.54 us/iteration against 1.82 (256 VGPRs + 29 spilled, twice the neighbour LDS reads):
-  // the two barriers it removes cost less than the recomputation (tools/cg2d_rc_ab.sh)
-  static const bool rc = getenv("MGCM_CG2D_RC") && atoi(getenv("MGCM_CG2D_RC")) == 1;
-  const size_t lds = ((rc ? 4 : 2) * ((size_t)BX * BY * NT + 1) + 4 * 16) * sizeof(double);
+  const size_t lds = (2 * ((size_t)BX * BY * NT + 1) + 4 * 16) * sizeof(double);
   const bool mr = nIterMin >= 0, fm = p.cg2dUseFMA != 0, sr = p.useSRCGSolver != 0;
-  auto kern = sr   ? (mr ? (fm ? k_cg2d_bxy<BX, BY, NT, true, true, false, true> : k_cg2d_bxy<BX, BY, NT, true, false, false, true>)
-                         : (fm ? k_cg2d_bxy<BX, BY, NT, false, true, false, true>
-                               : k_cg2d_bxy<BX, BY, NT, false, false, false, true>))
-              : rc ? (mr ? (fm ? k_cg2d_bxy<BX, BY, NT, true, true, true> : k_cg2d_bxy<BX, BY, NT, true, false, true>)
-                         : (fm ? k_cg2d_bxy<BX, BY, NT, false, true, true> : k_cg2d_bxy<BX, BY, NT, false, false, true>))
-                   : (mr ? (fm ? k_cg2d_bxy<BX, BY, NT, true, true> : k_cg2d_bxy<BX, BY, NT, true, false>)
+  auto kern = sr   ? (mr ? (fm ? k_cg2d_bxy<BX, BY, NT, true, true, true> : k_cg2d_bxy<BX, BY, NT, true, false, true>)
+                         : (fm ? k_cg2d_bxy<BX, BY, NT, false, true, true>
+                               : k_cg2d_bxy<BX, BY, NT, false, false, true>))
+              : (mr ? (fm ? k_cg2d_bxy<BX, BY, NT, true, true> : k_cg2d_bxy<BX, BY, NT, true, false>)
                          : (fm ? k_cg2d_bxy<BX, BY, NT, false, true> : k_cg2d_bxy<BX, BY, NT, false, false>));
   static bool attrSet[8] = {false, false, false, false, false, false, false, false};
   const int ai = 4 * sr + 2 * mr + fm;
@@ -1879,25 +1669,11 @@ hipError_t launch_corr_cont(const Dims &d, const Params &p, const Fields &f, int
   const int nArr = (p.nonlinFreeSurf > 0 && p.select_rStar != 0) ? 5 : 4;   // sH0 under r* only
   // deep grids: 32 columns per workgroup (LLC-90: 123 us against 140 at 16,
   // profiles/r03/colfnc/); shallow: 16 (config 2: 0.328-0.331 ms/step against 0.333 at 32,
-  // profiles/r03/ab_trex_corrnc/); MGCM_CORR_NC / MGCM_COLF_NC override
-  const int ncDef = d.Nr >= 30 ? 32 : 16;
-  const int ncEnv = getenv("MGCM_CORR_NC") ? atoi(getenv("MGCM_CORR_NC")) : getenv("MGCM_COLF_NC") ? atoi(getenv("MGCM_COLF_NC")) : ncDef;
-  const int nc = (ncEnv == 16 || ncEnv == 32 || ncEnv == 64) ? ncEnv : ncDef;
-  // the two-column form on the step path (atInit = 0) where pairs stay aligned: 16 column
-  // pairs per workgroup, the same LDS as 32 single columns.  Opt-in (MGCM_CORR2=1): bit-identical
-  // but slower on LLC-90, 151 against 137 us (profiles/r04/corr2/) -- the column frame is bound
-  // by its serial column sums and LDS round trips, not by the width of its loads
-  const int c2Env = getenv("MGCM_CORR2") ? atoi(getenv("MGCM_CORR2")) : 0;
-  auto al = [](const void *q) { return ((uintptr_t)q & 15u) == 0; };
-  if (c2Env != 0 && atInit == 0 && (d.sNx & 1) == 0 && (d.OLx & 1) == 0 && (d.nx & 1) == 0 && (d.n3 & 1) == 0 &&
-      al(f.gU) && al(f.gV) && al(f.maskW) && al(f.maskS) && al(f.hFacW) && al(f.hFacS) && al(f.maskC) && al(f.uVel) &&
-      al(f.vVel) && al(f.wVel) && (nArr < 5 || al(f.h0FacC))) {
-    const int nc2 = 16;   // 32 columns x 16 level slots
-    MG_ALLOW_LDS(k_corr_cont2);
-    hipLaunchKernelGGL(k_corr_cont2, dim3(mg_colf_blocks(ncol / 2, nc2)), dim3(256), mg_colf_lds(d.Nr, 2 * nc2, nArr), s, d,
-                       p, f, nc2, etaSrc);
-    return hipGetLastError();
-  }
+  // profiles/r03/ab_trex_corrnc/)
+  const int nc = d.Nr >= 30 ? 32 : 16;
+  // (round 4: a two-column form with 16-byte loads was bit-identical but slower on LLC-90,
+  // 151 against 137 us, profiles/r04/corr2/ -- the column frame is bound by its serial column
+  // sums and LDS round trips, not by the width of its loads; removed in round 5)
   MG_ALLOW_LDS(k_corr_cont);
   hipLaunchKernelGGL(k_corr_cont, dim3(mg_colf_blocks(ncol, nc)), dim3(256), mg_colf_lds(d.Nr, nc, nArr), s, d, p, f,
                      atInit, nc, etaSrc);

@@ -152,15 +152,14 @@ bool dyn_thermo_takes_gm(const Params &p) {
 bool dyn_thermo_fusable(const Dims &d, const Params &p, const TracerArgs &aT, const TracerArgs &aS) {
   return mg_hfuse(MG_FUSE_DT, d.nx, d.ny, d.nT, d.Nr) && p.momStepping && p.tempStepping && p.saltStepping &&
          p.useGMRedi && p.implicitDiffusion && !aT.multiDim && !aS.multiDim && !p.vectorInvariantMomentum &&
-         !getenv("MGCM_MOM_NOSPLIT") && aT.scr != aS.scr;
+         aT.scr != aS.scr;
 }
 
 // CALC_PHI_HYD's column frame as launch_phi_hyd sizes it
 static void phi_frame(const Dims &d, const Params &p, int &nc, int &nArr, int &nb) {
   const long ncol = (long)(d.sNx + 3) * (d.sNy + 3) * d.nT;
   nArr = (p.nonlinFreeSurf > 0 && p.select_rStar > 0) ? 6 : 3;
-  const int ncEnv = getenv("MGCM_PHI_NC") ? atoi(getenv("MGCM_PHI_NC")) : 0;
-  nc = (ncEnv == 16 || ncEnv == 32 || ncEnv == 64) ? ncEnv : mg_colf_nc(ncol, d.Nr, nArr);
+  nc = mg_colf_nc(ncol, d.Nr, nArr);
   nb = (int)mg_colf_blocks(ncol, nc);
 }
 
@@ -227,14 +226,13 @@ hipError_t launch_dyn_thermo(const Dims &d, const Params &p, const Fields &f, co
   const int nbDel = del2_needed(p) ? (int)mg_plane_blocks(d.nx, d.ny, d.nT * d.Nr) : 0;
   const int nbTr = (int)mg_plane_blocks(d.sNx, d.sNy, d.nT * d.Nr);
   if (dyn_thermo_takes_gm(p)) {
-    // MGCM_OPE_AT (mg_ope_at): 2 (default; config 2 0.2821-0.2832 ms/step) against 1
-    // (0.2852-0.2857 on the same box; profiles/r04/ope_at/) -- the longest grid (the momentum
-    // chain) hides the operator's blocks best; 3 leaves the preconditioner to the r* pass
-    // (0.2825-0.2829 against 0.2815-0.2819 for 2 on one box, profiles/r04/ope_at3/)
-    const int opeAt = mg_ope_at();
+    // UPDATE_CG2D's operator in grid 2, its preconditioner in grid 3 (config 2 0.2821-0.2832
+    // ms/step; the operator in grid 1 and the preconditioner in grid 2 0.2852-0.2857 on the same
+    // box, profiles/r04/ope_at/; the preconditioner in the r* pass 0.2825-0.2829 against
+    // 0.2815-0.2819, profiles/r04/ope_at3/) -- the longest grid (the momentum chain) hides the
+    // operator's blocks best
     const int nbU = srcOf ? ucg2d_blocks(d) : 0;
-    const int nbOp1 = opeAt == 1 ? nbU : 0, nbPc2 = opeAt == 1 ? nbU : 0, nbOp2 = opeAt == 1 ? 0 : nbU,
-              nbPc3 = opeAt == 2 ? nbU : 0;
+    const int nbOp1 = 0, nbPc2 = 0, nbOp2 = nbU, nbPc3 = nbU;
     launch_l1(d, p, f, nbDel, s, nbOp1);
     const bool ff4 = mom_ff4_on(true);
     const int nbMom = ff4 ? mom_ff4_blocks(d) : 2 * (int)mg_plane_blocks(d.nx, d.ny, d.nT * d.Nr);

@@ -856,150 +856,6 @@ __global__ void __launch_bounds__(256) TRM_ATTR k_tracer_march2(Dims d, Params p
   }
 }
 
-// TEMP_INTEGRATE and SALT_INTEGRATE together (both stepped, no GM/Redi, no multi-dimensional
-// advection: LLC-90's C2 tracers): the k-march of k_tracer_march over the two tracers at
-// once, so the operands they share -- u, v, w, hFacW/S, maskC, IVDConvCount, recip_hFacC and
-// the column's metrics -- are fetched once for both (12 3-D loads per point instead of 20).
-// T* of theta goes to gTscr, of salt to cpScr, for k_tracer2_impl.  Each tracer's arithmetic
-// is tracer_flat_arith's: bit-identical to the two separate launches.
-__device__ __forceinline__ void tracer2_march_body(const Dims &d, const Params &p, const Fields &f, const TracerArgs &aT,
-                                                   const TracerArgs &aS, const int *iterPtr, int KC, int nkc, int ntx,
-                                                   int nty) {
-  int b = mg_xcd_block();
-  const int kc = b % nkc;
-  b /= nkc;
-  const int tx = b % ntx, ty = (b / ntx) % nty, t = d.t0 + b / (ntx * nty);
-  const int i = 1 + tx * TRM_TX + (int)(threadIdx.x % TRM_TX), j = 1 + ty * TRM_TY + (int)(threadIdx.x / TRM_TX);
-  if (i > d.sNx || j > d.sNy) return;
-  const int Nr = d.Nr, k0 = 1 + kc * KC, k1 = min(Nr, k0 + KC - 1);
-  const int myIter = *iterPtr;
-  const long nx = d.nx, n2 = d.n2, q = MG_I2(d, i, j, t);
-  const double *__restrict__ T = aT.tr;
-  const double *__restrict__ S = aS.tr;
-  TrCol cT, cS;
-  tracer_load_col(d, f, aT, q, cT);
-  cS = cT;
-  cS.sfc = aS.sfc ? aS.sfc[q] : 0.0;
-  long q3 = MG_I3(d, i, j, k0, t);
-  const long qu = k0 > 1 ? q3 - n2 : q3;
-  double Tu = T[qu], Su = S[qu], mCu = f.maskC[qu];
-  double T0 = T[q3], S0 = S[q3], mC0 = f.maskC[q3], w0 = f.wVel[q3], ivd0 = f.IVDConvCount[q3];
-  const bool impl = p.implicitDiffusion != 0;
-  for (int k = k0; k <= k1; k++, q3 += n2) {
-    const long qd = k < Nr ? q3 + n2 : q3;
-    TrLev o;
-    o.mC0 = mC0; o.mCu = mCu; o.w0 = w0; o.ivd0 = ivd0;
-    o.mCd = f.maskC[qd]; o.w1 = f.wVel[qd]; o.ivd1 = f.IVDConvCount[qd];
-    o.u0 = f.uVel[q3]; o.u1 = f.uVel[q3 + 1]; o.v0 = f.vVel[q3]; o.v1 = f.vVel[q3 + nx];
-    o.hW0 = f.hFacW[q3]; o.hW1 = f.hFacW[q3 + 1]; o.hS0 = f.hFacS[q3]; o.hS1 = f.hFacS[q3 + nx];
-    o.rhC = f.recip_hFacC[q3]; o.gAdv = 0.0;
-    TrLev oS = o;
-    o.T0 = T0; o.Tu = Tu; o.Td = T[qd];
-    o.Tw = T[q3 - 1]; o.Te = T[q3 + 1]; o.Ts = T[q3 - nx]; o.Tn = T[q3 + nx];
-    o.gOld = aT.useAB ? aT.gNm1[q3] : 0.0;
-    oS.T0 = S0; oS.Tu = Su; oS.Td = S[qd];
-    oS.Tw = S[q3 - 1]; oS.Te = S[q3 + 1]; oS.Ts = S[q3 - nx]; oS.Tn = S[q3 + nx];
-    oS.gOld = aS.useAB ? aS.gNm1[q3] : 0.0;
-    double gNT = 0.0, gNS = 0.0;
-    const double vT = tracer_flat_arith(p, f, aT, Nr, k, myIter, cT, o, &gNT);
-    const double vS = tracer_flat_arith(p, f, aS, Nr, k, myIter, cS, oS, &gNS);
-    if (aT.useAB) aT.gNm1[q3] = gNT;
-    if (aS.useAB) aS.gNm1[q3] = gNS;
-    if (impl) { f.gTscr[q3] = vT; f.cpScr[q3] = vS; }
-    else { aT.trNext[q3] = vT; aS.trNext[q3] = vS; }
-    Tu = T0; T0 = o.Td; Su = S0; S0 = oS.Td;
-    mCu = mC0; mC0 = o.mCd; w0 = o.w1; ivd0 = o.ivd1;
-  }
-}
-__global__ void __launch_bounds__(256) k_tracer2_march(Dims d, Params p, Fields f, TracerArgs aT, TracerArgs aS,
-                                                      const int *iterPtr, int KC, int nkc, int ntx, int nty) {
-  tracer2_march_body(d, p, f, aT, aS, iterPtr, KC, nkc, ntx, nty);
-}
-// registers capped for 3 / 4 waves per SIMD (MGCM_TR2_WAVES=3|4: A/B)
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3)))
-k_tracer2_march_w3(Dims d, Params p, Fields f, TracerArgs aT, TracerArgs aS, const int *iterPtr, int KC, int nkc, int ntx,
-                   int nty) {
-  tracer2_march_body(d, p, f, aT, aS, iterPtr, KC, nkc, ntx, nty);
-}
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4)))
-k_tracer2_march_w4(Dims d, Params p, Fields f, TracerArgs aT, TracerArgs aS, const int *iterPtr, int KC, int nkc, int ntx,
-                   int nty) {
-  tracer2_march_body(d, p, f, aT, aS, iterPtr, KC, nkc, ntx, nty);
-}
-
-// GAD_IMPLICIT_R + SOLVE_TRIDIAGONAL of both tracers per column (k_tracer_impl twice, without
-// GM/Redi): maskC, IVDConvCount and recip_hFacC fetched once; thread (c, 0) sweeps theta's
-// system and thread (c, 1) salt's, concurrently.
-__global__ void __launch_bounds__(256) k_tracer2_impl(Dims d, Params p, Fields f, TracerArgs aT, TracerArgs aS, int nc) {
-  extern __shared__ __attribute__((aligned(16))) double lds[];
-  MG_COLF(1, d.sNx, 1, d.sNy, nc)
-  const int Nr = d.Nr, NS = Nr * NC_;
-  double *sl[2][3] = {{lds, lds + NS, lds + 2 * NS}, {lds + 3 * NS, lds + 4 * NS, lds + 5 * NS}};   // sub, sup, y
-#define G3(a_, ii, jj, kk_) f.a_[MG_I3(d, ii, jj, kk_, t)]
-  if (valid) {
-    const bool rs = p.nonlinFreeSurf > 0 && p.select_rStar > 0;
-    const long q2 = MG_I2(d, i, j, t);
-    const double rsx = rs ? f.rStarExpC[q2] : 1.0;
-    MG_COLF_K(k) {
-      const int me = (k - 1) * NC_ + cc;
-      const long q3 = MG_I3(d, i, j, k, t);
-      const double rh = rs ? f.recip_hFacC[q3] / rsx : f.recip_hFacC[q3];
-      const double rdrF = f.recip_drF[k - 1];
-      const double ivK = G3(IVDConvCount, i, j, k) * p.ivdc_kappa + 0.0;
-      const double ivK1 = k <= Nr - 1 ? G3(IVDConvCount, i, j, k + 1) * p.ivdc_kappa + 0.0 : 0.0;
-      const double mU = k >= 2 ? G3(maskC, i, j, k - 1) : 0.0, mD = k <= Nr - 1 ? G3(maskC, i, j, k + 1) : 0.0;
-#pragma unroll
-      for (int c2 = 0; c2 < 2; c2++) {
-        const double kr = c2 ? aS.diffKr : aT.diffKr;
-        double sub = 0.0, sup = 0.0;
-        if (k >= 2) sub = -(p.deltaTtracer * mU * rh * rdrF * (ivK + kr) * f.recip_drC[k - 1]);
-        if (k <= Nr - 1) sup = -(p.deltaTtracer * mD * rh * rdrF * (ivK1 + kr) * f.recip_drC[k]);
-        sl[c2][0][me] = sub;
-        sl[c2][1][me] = sup;
-      }
-      sl[0][2][me] = f.gTscr[q3];
-      sl[1][2][me] = f.cpScr[q3];
-    }
-  }
-  __syncthreads();
-  if (valid && kk < 2) {
-    double *sSub = sl[kk][0], *sSup = sl[kk][1], *sY = sl[kk][2];
-    double cpPrev = 0.0, ypPrev = 0.0;
-    for (int k2 = 1; k2 <= Nr; k2++) {
-      const int s2 = (k2 - 1) * NC_ + cc;
-      const double sub = sSub[s2], sup = sSup[s2];
-      const double diag = 1.0 - (sub + sup);
-      const double y = sY[s2];
-      double cp, yp;
-      if (k2 == 1) {
-        if (diag != 0.0) { const double rec = 1.0 / diag; cp = sup * rec; yp = y * rec; }
-        else { cp = 0.0; yp = 0.0; }
-      } else {
-        const double tmp = diag - sub * cpPrev;
-        if (tmp != 0.0) { const double rec = 1.0 / tmp; cp = sup * rec; yp = (y - sub * ypPrev) * rec; }
-        else { cp = 0.0; yp = 0.0; }
-      }
-      sSup[s2] = cp;
-      sY[s2] = yp;
-      cpPrev = cp; ypPrev = yp;
-    }
-    double below = 0.0;
-    for (int k2 = Nr; k2 >= 1; k2--) {
-      const int s2 = (k2 - 1) * NC_ + cc;
-      const double v = (k2 == Nr) ? sY[s2] : sY[s2] - sSup[s2] * below;
-      sSub[s2] = v;
-      below = v;
-    }
-  }
-  __syncthreads();
-  if (valid) MG_COLF_K(k) {
-    const int me = (k - 1) * NC_ + cc;
-    const long q3 = MG_I3(d, i, j, k, t);
-    aT.trNext[q3] = sl[0][0][me];
-    aS.trNext[q3] = sl[1][0][me];
-  }
-#undef G3
-}
 
 __global__ void __launch_bounds__(256) k_tracer_rhs_flat(Dims d, Params p, Fields f, TracerArgs a, const int *iterPtr) {
   MG_PLANE(1, d.sNx, 1, d.sNy, z)
@@ -1011,86 +867,6 @@ __global__ void __launch_bounds__(256) k_tracer_rhs_flat(Dims d, Params p, Field
   else a.trNext[q3] = v;
 }
 
-// k_tracer_rhs_flat + k_tracer_impl in one column-frame launch (implicitDiffusion without
-// GM/Redi): the k-parallel threads of a column compute T* = T + dt*gT of every level (the
-// flat kernel's expression trees) straight into the LDS right-hand side of the tridiagonal
-// system, beside its coefficients; one thread per column then runs the Thomas sweep
-// (GAD_IMPLICIT_R + SOLVE_TRIDIAGONAL, as k_tracer_impl) and the levels are written back
-// k-parallel.  T* never travels through HBM (no gTscr store and re-load), and the
-// coefficients' operands are the ones the right-hand side just read.  Bit-identical to the
-// two launches.
-__device__ __forceinline__ void tracer_col_body(const Dims &d, const Params &p, const Fields &f, const TracerArgs &a,
-                                                const int *iterPtr, int nc) {
-  extern __shared__ __attribute__((aligned(16))) double lds[];
-  MG_COLF(1, d.sNx, 1, d.sNy, nc)
-  const int Nr = d.Nr, NS = Nr * NC_;
-  double *sSub = lds, *sSup = lds + NS, *sY = lds + 2 * NS;   // sSub holds the solution after the sweeps
-  const int myIter = *iterPtr;
-#define G3(a_, ii, jj, kk_) f.a_[MG_I3(d, ii, jj, kk_, t)]
-  if (valid) {
-    const bool rs = p.nonlinFreeSurf > 0 && p.select_rStar > 0;
-    const long q2 = MG_I2(d, i, j, t);
-    const double rsx = rs ? f.rStarExpC[q2] : 1.0;
-    auto kappa = [&](int k_) { return (G3(IVDConvCount, i, j, k_) * p.ivdc_kappa + 0.0) + a.diffKr; };
-    // one level per pass (not unrolled: the point's operands then fit 4 waves per SIMD)
-#pragma unroll 1
-    MG_COLF_K(k) {
-      const int me = (k - 1) * NC_ + cc;
-      sY[me] = tracer_flat_point(d, p, f, a, i, j, k, t, myIter);
-      const long q3 = MG_I3(d, i, j, k, t);
-      const double rh = rs ? f.recip_hFacC[q3] / rsx : f.recip_hFacC[q3];
-      const double rdrF = f.recip_drF[k - 1];
-      double sub = 0.0, sup = 0.0;
-      if (k >= 2)
-        sub = -(p.deltaTtracer * G3(maskC, i, j, k - 1) * rh * rdrF * kappa(k) * f.recip_drC[k - 1]);
-      if (k <= Nr - 1)
-        sup = -(p.deltaTtracer * G3(maskC, i, j, k + 1) * rh * rdrF * kappa(k + 1) * f.recip_drC[k]);
-      sSub[me] = sub;
-      sSup[me] = sup;
-    }
-  }
-  __syncthreads();
-  if (valid && kk == 0) {
-    double cpPrev = 0.0, ypPrev = 0.0;
-    for (int k2 = 1; k2 <= Nr; k2++) {
-      const int s2 = (k2 - 1) * NC_ + cc;
-      const double sub = sSub[s2], sup = sSup[s2];
-      const double diag = 1.0 - (sub + sup);
-      const double y = sY[s2];
-      double cp, yp;
-      if (k2 == 1) {
-        if (diag != 0.0) { const double rec = 1.0 / diag; cp = sup * rec; yp = y * rec; }
-        else { cp = 0.0; yp = 0.0; }
-      } else {
-        const double tmp = diag - sub * cpPrev;
-        if (tmp != 0.0) { const double rec = 1.0 / tmp; cp = sup * rec; yp = (y - sub * ypPrev) * rec; }
-        else { cp = 0.0; yp = 0.0; }
-      }
-      sSup[s2] = cp;
-      sY[s2] = yp;
-      cpPrev = cp; ypPrev = yp;
-    }
-    double below = 0.0;
-    for (int k2 = Nr; k2 >= 1; k2--) {
-      const int s2 = (k2 - 1) * NC_ + cc;
-      const double v = (k2 == Nr) ? sY[s2] : sY[s2] - sSup[s2] * below;
-      sSub[s2] = v;
-      below = v;
-    }
-  }
-  __syncthreads();
-  if (valid) MG_COLF_K(k) a.trNext[MG_I3(d, i, j, k, t)] = sSub[(k - 1) * NC_ + cc];
-#undef G3
-}
-__global__ void __launch_bounds__(256) k_tracer_col(Dims d, Params p, Fields f, TracerArgs a, const int *iterPtr, int nc) {
-  tracer_col_body(d, p, f, a, iterPtr, nc);
-}
-// the same with the registers capped for 4 waves per SIMD (MGCM_TRACER_COL=4: A/B)
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) k_tracer_col4(Dims d, Params p, Fields f,
-                                                                                              TracerArgs a,
-                                                                                              const int *iterPtr, int nc) {
-  tracer_col_body(d, p, f, a, iterPtr, nc);
-}
 
 // GAD_IMPLICIT_R (implicitDiffusion) + SOLVE_TRIDIAGONAL (Thomas) + CYCLE_TRACER,
 // one thread per interior column; writes the new tracer into its other buffer.
@@ -1240,59 +1016,7 @@ static bool tracer_march_on(const Dims &d) {
   return d.Nr >= 30;
 }
 
-// Both tracers in one pair of launches (k_tracer2_march + k_tracer2_impl) where the options
-// allow it (tracer_pair_ok): the deep-grid k-march path without GM/Redi or multi-dimensional
-// advection.  MGCM_TRACER_PAIR=0 keeps one tracer at a time.
-bool tracer_pair_ok(const Dims &d, const Params &p, const TracerArgs &aT, const TracerArgs &aS) {
-  // opt-in (MGCM_TRACER_PAIR=1): 389 us for both tracers against 2 x 238 alone on LLC-90,
-  // but at 172 VGPRs it shares the chip worse -- beside DYNAMICS 1.98 ms/step against 2.06
-  // with the single-tracer march, beside the pressure solve (the default) 1.92 against 1.86
-  const char *e = getenv("MGCM_TRACER_PAIR");
-  if (!e || atoi(e) == 0) return false;
-  return p.tempStepping && p.saltStepping && !p.useGMRedi && !aT.multiDim && !aS.multiDim && tracer_march_on(d) &&
-         !(getenv("MGCM_TRACER_FLAT") && atoi(getenv("MGCM_TRACER_FLAT")) == 0);
-}
-
-hipError_t launch_tracer_pair(const Dims &d, const Params &p, const Fields &f, const TracerArgs &aT, const TracerArgs &aS,
-                              const int *iterPtr, hipStream_t s) {
-  const dim3 blk(MG_PLANE_THREADS);
-  const int kcEnv = getenv("MGCM_TR_KC") ? atoi(getenv("MGCM_TR_KC")) : 0;
-  const int KC = kcEnv > 0 ? (kcEnv > d.Nr ? d.Nr : kcEnv) : (d.Nr + 4) / 5;
-  const int nkc = (d.Nr + KC - 1) / KC, ntx = (d.sNx + TRM_TX - 1) / TRM_TX, nty = (d.sNy + TRM_TY - 1) / TRM_TY;
-  const int wv = getenv("MGCM_TR2_WAVES") ? atoi(getenv("MGCM_TR2_WAVES")) : 0;
-  hipLaunchKernelGGL(wv == 3 ? k_tracer2_march_w3 : wv == 4 ? k_tracer2_march_w4 : k_tracer2_march,
-                     dim3((unsigned)(nkc * ntx * nty * d.nT)), blk, 0, s, d, p, f, aT, aS, iterPtr, KC, nkc, ntx, nty);
-  if (p.implicitDiffusion) {
-    const long ncol = (long)d.sNx * d.sNy * d.nT;
-    const int nc = mg_colf_nc(ncol, d.Nr, 6);
-    MG_ALLOW_LDS(k_tracer2_impl);
-    hipLaunchKernelGGL(k_tracer2_impl, dim3(mg_colf_blocks(ncol, nc)), blk, mg_colf_lds(d.Nr, nc, 6), s, d, p, f, aT, aS, nc);
-  }
-  return hipGetLastError();
-}
-
-// Both tracers' implicit vertical solves in one launch (k_tracer2_impl: theta's and salt's
-// sweeps side by side per column), after the two single-tracer right-hand sides (their T* in
-// gTscr / cpScr, TracerArgs.scr).  Where it applies: both stepped, implicit diffusion, no
-// GM/Redi (k_tracer2_impl has no Kwz term).  MGCM_TRACER_IMPL2=0|1 (read per call).
-bool tracer_impl2_ok(const Params &p, const Fields &f, const TracerArgs &aT, const TracerArgs &aS) {
-  const char *e = getenv("MGCM_TRACER_IMPL2");
-  if (!e || atoi(e) == 0) return false;
-  // (multi-dimensional advection uses gTscr as its face-flux scratch: excluded)
-  return p.tempStepping && p.saltStepping && p.implicitDiffusion && !p.useGMRedi && !aT.multiDim && !aS.multiDim &&
-         aT.scr == f.gTscr && aS.scr == f.cpScr;
-}
-hipError_t launch_tracer2_impl(const Dims &d, const Params &p, const Fields &f, const TracerArgs &aT, const TracerArgs &aS,
-                               hipStream_t s) {
-  const long ncol = (long)d.sNx * d.sNy * d.nT;
-  const int nc = mg_colf_nc(ncol, d.Nr, 6);
-  MG_ALLOW_LDS(k_tracer2_impl);
-  hipLaunchKernelGGL(k_tracer2_impl, dim3(mg_colf_blocks(ncol, nc)), dim3(MG_PLANE_THREADS), mg_colf_lds(d.Nr, nc, 6), s, d,
-                     p, f, aT, aS, nc);
-  return hipGetLastError();
-}
-
-// impl = false: the right-hand side only (the implicit solve follows in launch_tracer2_impl)
+// impl = false: the right-hand side only (the implicit solve is launched by the caller)
 hipError_t launch_tracer_step(const Dims &d, const Params &p, const Fields &f, const TracerArgs &a, const int *iterPtr,
                               hipStream_t s, bool impl) {
   const dim3 blk(MG_PLANE_THREADS), grd(mg_plane_blocks(d.sNx, d.sNy, d.nT * d.Nr));
@@ -1318,29 +1042,15 @@ hipError_t launch_tracer_step(const Dims &d, const Params &p, const Fields &f, c
     }
   }
   // GM/Redi fluxes as a template switch: without them the kernel holds half the registers
-  static const bool flatOff = getenv("MGCM_TRACER_FLAT") && atoi(getenv("MGCM_TRACER_FLAT")) == 0;
   if (p.useGMRedi) hipLaunchKernelGGL(k_tracer_rhs<true>, grd, blk, 0, s, d, p, f, a, iterPtr);
-  else if (flatOff) hipLaunchKernelGGL(k_tracer_rhs<false>, grd, blk, 0, s, d, p, f, a, iterPtr);
-  else if (p.implicitDiffusion && getenv("MGCM_TRACER_COL") && atoi(getenv("MGCM_TRACER_COL")) > 0) {
-    // the right-hand side and the implicit vertical solve in one column-frame launch: opt-in
-    // (MGCM_TRACER_COL=1, =4 with the registers capped).  Bit-identical, but on LLC-90 it
-    // is slower than the flat right-hand side + k_tracer_impl pair it replaces: 331 against
-    // 256 us per tracer, step 2.16 against 2.09 ms (profiles/r03/tracer_col/): the serial
-    // per-column flux sweep at 170 VGPRs costs more than the second launch saves
-    const long ncol = (long)d.sNx * d.sNy * d.nT;
-    const int nc = mg_colf_nc(ncol, d.Nr, 3);
-    static const bool col4 = getenv("MGCM_TRACER_COL") && atoi(getenv("MGCM_TRACER_COL")) == 4;
-    MG_ALLOW_LDS(k_tracer_col);
-    MG_ALLOW_LDS(k_tracer_col4);
-    hipLaunchKernelGGL(col4 ? k_tracer_col4 : k_tracer_col, dim3(mg_colf_blocks(ncol, nc)), blk, mg_colf_lds(d.Nr, nc, 3), s,
-                       d, p, f, a, iterPtr, nc);
-    return hipGetLastError();
-  } else if (tracer_march_on(d)) {
-    // the k-march (deep grids; MGCM_TRACER_MARCH=0|1 overrides, MGCM_TR_KC levels per workgroup)
-    const int kcEnv = getenv("MGCM_TR_KC") ? atoi(getenv("MGCM_TR_KC")) : 0;
-    const int KC = kcEnv > 0 ? (kcEnv > d.Nr ? d.Nr : kcEnv) : (d.Nr + 4) / 5;
+  else if (tracer_march_on(d)) {
+    // the k-march (deep grids; MGCM_TRACER_MARCH=0|1 overrides): KC levels per workgroup, five
+    // chunks (round 3: LLC-90 fastest among 1/2/5/10 chunks, profiles/r03/)
+    const int KC = (d.Nr + 4) / 5;
     const int nkc = (d.Nr + KC - 1) / KC, ntx = (d.sNx + TRM_TX - 1) / TRM_TX, nty = (d.sNy + TRM_TY - 1) / TRM_TY;
     auto al = [](const void *x) { return ((uintptr_t)x & 15u) == 0; };
+    // the two-column form (double2 accesses) where the slab's layout allows it; MGCM_TRACER_MARCH2=0
+    // forces the one-column form the other layouts run (tests cover both)
     const int m2Env = getenv("MGCM_TRACER_MARCH2") ? atoi(getenv("MGCM_TRACER_MARCH2")) : 1;
     const int hx = d.sNx / 2;
     if (m2Env != 0 && (d.sNx & 1) == 0 && (d.OLx & 1) == 0 && (d.nx & 1) == 0 && (d.n3 & 1) == 0 && hx <= 256 && al(a.tr) &&

@@ -95,10 +95,6 @@ hipError_t launch_halo_pack(const Dims &, const XFields &, const long *, long, d
 hipError_t launch_oceanic_phys(const Dims &, const Params &, const Fields &, const int *, hipStream_t, bool gm = true);
 hipError_t launch_tracer_step(const Dims &, const Params &, const Fields &, const TracerArgs &, const int *, hipStream_t,
                               bool impl = true);
-bool tracer_impl2_ok(const Params &, const Fields &, const TracerArgs &, const TracerArgs &);
-hipError_t launch_tracer2_impl(const Dims &, const Params &, const Fields &, const TracerArgs &, const TracerArgs &,
-                               hipStream_t);
-bool tracer_pair_ok(const Dims &, const Params &, const TracerArgs &, const TracerArgs &);
 bool dyn_thermo_fusable(const Dims &, const Params &, const TracerArgs &, const TracerArgs &);
 hipError_t launch_dyn_thermo(const Dims &, const Params &, const Fields &, const TracerArgs &, const TracerArgs &, const int *,
                              hipStream_t, const long *srcOf = nullptr);
@@ -111,8 +107,6 @@ hipError_t launch_gm_phi(const Dims &, const Params &, const Fields &, hipStream
 bool tracer_hpair_ok(const Dims &, const Params &, const TracerArgs &, const TracerArgs &);
 hipError_t launch_tracer_hpair(const Dims &, const Params &, const Fields &, const TracerArgs &, const TracerArgs &,
                                const int *, hipStream_t);
-hipError_t launch_tracer_pair(const Dims &, const Params &, const Fields &, const TracerArgs &, const TracerArgs &,
-                              const int *, hipStream_t);
 hipError_t launch_mon_stats(const Dims &, const MonSpecs &, int, double *, int, hipStream_t);
 int cg2d_mwg_geometry(int *, int *, int *);
 hipError_t launch_cg2d_mwg(const Dims &, const Params &, const Fields &, const MwgTables &, int, int, SolveRecord *, int *,
@@ -480,7 +474,7 @@ static int build_nbr(mgcm_model *m) {
   m->nBlk = 0;
   const int Nx = d.sNx * d.nSx, Ny = d.sNy * d.nSy;
   const int nBk = (Nx / 2) * (Ny / 2);
-  if (m->latlonTopology && Nx % 2 == 0 && Ny % 2 == 0 && nBk <= 1024 && !getenv("MGCM_CG2D_NOBLK")) {
+  if (m->latlonTopology && Nx % 2 == 0 && Ny % 2 == 0 && nBk <= 1024 && !getenv("MGCM_CG2D_NOBLOCKED")) {
     const unsigned Z = 4096u;
     auto cmp = [&](long g) -> unsigned {
       unsigned c = compact(g);
@@ -521,22 +515,20 @@ static int build_nbr(mgcm_model *m) {
     m->nBlk = nBk;
   }
   // BX x BY blocks (k_cg2d_bxy), same global-index construction; the first geometry of
-  // the preference list the grid tiles into (MGCM_CGX=v forces variant v)
+  // the preference list the grid tiles into
   m->nBlkX = 0;
   int BX = 0, BY = 0, NT = 0, nBx = 0;
   m->bxyVar = -1;
   {
     static const int pref[] = {0, 1};
-    const char *force = getenv("MGCM_CGX");
     for (int v : pref) {
-      if (force && atoi(force) != v) continue;
       int bx, by, nt;
       if (cg2d_bxy_geometry(v, &bx, &by, &nt)) continue;
       const int n = (Nx % bx == 0 && Ny % by == 0) ? (Nx / bx) * (Ny / by) : 0;
       if (n > 0 && n <= nt) { m->bxyVar = v; BX = bx; BY = by; NT = nt; nBx = n; break; }
     }
   }
-  if (m->latlonTopology && m->bxyVar >= 0 && !getenv("MGCM_CG2D_NOBXY")) {
+  if (m->latlonTopology && m->bxyVar >= 0 && !getenv("MGCM_CG2D_NOBLOCKED")) {
     const int NPT = BX * BY, NB = 2 * (BX + BY);
     const unsigned Z = (unsigned)(NPT * NT);
     // LDS slot of an interior point: point-in-block major, block minor (p*NT + block),
@@ -778,11 +770,9 @@ static int build_mwg(mgcm_model *m) {
   // round of its own: LLC-90 1.591 ms/step against 1.688 with the coarse-grained block, 117
   // parts, ~1 us per CG iteration (profiles/r04/mwgmem/); the XCD-pinned parts (cube, <= 32
   // parts, one XCD's L2) keep coarse-grained memory (cs32x15 0.416 against 0.421-0.455).
-  // MGCM_MWG_BLOCK=coarse|uncached|fine overrides, MGCM_MWG_SYS=1 for system-scope accesses.
-  const char *bk = getenv("MGCM_MWG_BLOCK");
-  const int mem = bk ? (!strcmp(bk, "uncached") ? 1 : !strcmp(bk, "fine") ? 2 : 0) : (T.pinned ? 0 : 1);
-  const bool sys = getenv("MGCM_MWG_SYS") && atoi(getenv("MGCM_MWG_SYS")) == 1;
-  if (mem && mwg_block_realloc(m, mem, sys)) return -1;
+  // (fine-grained memory measured no better than coarse, system-scope accesses alike:
+  // profiles/r04/mwgmem/)
+  if (!T.pinned && mwg_block_realloc(m, 1, false)) return -1;
   return 0;
 }
 
@@ -819,7 +809,6 @@ mgcm_model *mgcm_create(int sNx, int sNy, int OLx, int OLy, int Nr, int nSx, int
   // CG2D in fused multiply-adds where the kernel supports it (k_cg2d_bxy): 2.14 -> 1.83 us per
   // iteration on global_ocean.90x40x15; the device-order oracle evaluates the same fma chains
   p.cg2dUseFMA = 1;
-  if (getenv("MGCM_CG2D_FMA")) p.cg2dUseFMA = atoi(getenv("MGCM_CG2D_FMA"));
   p.gravity = 9.81; p.gravitySign = -1.0; p.rhoNil = 999.8; p.tAlpha = 2.0e-4; p.tempAdvection = 1;
   p.tempForcing = 1; p.tempAdvScheme = 2; p.implicitDiffusion = 0;
   p.saltAdvection = 1; p.saltForcing = 1; p.saltAdvScheme = 2; p.multiDimAdvection = 1; p.momStepping = 1;
@@ -844,9 +833,10 @@ mgcm_model *mgcm_create(int sNx, int sNy, int OLx, int OLy, int Nr, int nSx, int
     delete m;
     return nullptr;
   }
-  m->overlap = getenv("MGCM_NO_OVERLAP") == nullptr;
-  // MGCM_OVERLAP=1 forces the second stream on; otherwise the graph path picks by timing
-  m->ovlAuto = m->overlap && !(getenv("MGCM_OVERLAP") && atoi(getenv("MGCM_OVERLAP")) == 1);
+  // MGCM_OVERLAP=1 forces the second stream on, =0 off; otherwise the graph path picks by timing
+  const char *ov = getenv("MGCM_OVERLAP");
+  m->overlap = !(ov && atoi(ov) == 0);
+  m->ovlAuto = !ov;
   // one arena per kind for the 2-D and 3-D fields (MG_F2D_LIST / MG_F3D_LIST order, common.h)
   d.N2all = d.n2 * d.nTiles;
   d.N3all = d.n3 * d.nTiles;
@@ -1001,6 +991,8 @@ double mgcm_get_param(mgcm_model *m, const char *name) {
   if (!strcmp(name, "cg2dKernel"))
     return m->p.cg2dRefOrder ? 5.0 : m->useMwg ? 4.0 : m->nBlkX > 0 ? 3.0 : (m->nBlk > 0 ? 2.0 : 1.0);
   if (!strcmp(name, "cg2dParts")) return m->useMwg ? (double)m->mwg.G : 1.0;
+  // 1 when the multi-workgroup solve's parts are placed on one XCD (one L2: ~1 us hand-offs)
+  if (!strcmp(name, "cg2dPinned")) return m->useMwg ? (double)m->mwg.pinned : 0.0;
   // THERMODYNAMICS on the second stream: 1 on, 0 off; -1 while the graph path is still timing
   // both (ovlMsOn / ovlMsOff: ovl_trial's event times of the two graphs, 8 steps each)
   if (!strcmp(name, "overlap")) return (m->ovlAuto && !m->ovlDecided) ? -1.0 : (m->overlap ? 1.0 : 0.0);
@@ -1229,10 +1221,9 @@ int mgcm_init(mgcm_model *m) {
   if (upload_halo(m)) return -1;
   if (build_nbr(m)) return -1;
   // CG2D kernel: the single-workgroup blocked solvers on lat-lon grids that tile into their
-  // blocks; otherwise the multi-workgroup solver (MGCM_CG2D_SINGLE=1 keeps the generic
-  // single-workgroup one where it fits)
+  // blocks; otherwise the multi-workgroup solver (the generic single-workgroup kernel measured
+  // 12.7 against 4.2 us/iteration on the cube, round 3)
   m->useMwg = false;
-  const bool single = getenv("MGCM_CG2D_SINGLE") && atoi(getenv("MGCM_CG2D_SINGLE")) == 1;
   // cg2dRefOrder: the generic single-workgroup kernel with the reference's summation order
   // (parity runs on the reference's own tiling; refused where it does not fit one workgroup)
   if (m->p.cg2dRefOrder) {
@@ -1240,7 +1231,7 @@ int mgcm_init(mgcm_model *m) {
       return set_err("mgcm_init: cg2dRefOrder needs <= %d interior points (one workgroup), have %d",
                      cg2d_ref_max_points(), m->nPts);
     if (m->p.useSRCGSolver) return set_err("mgcm_init: cg2dRefOrder with useSRCGSolver not implemented");
-  } else if ((m->nBlkX == 0 && m->nBlk == 0 && !(single && m->nPts <= cg2d_block_max_points())) ||
+  } else if ((m->nBlkX == 0 && m->nBlk == 0) ||
              ext("cg2dForceMwg", 0.0) != 0.0) {
     // cg2dForceMwg: the multi-workgroup solver on a grid the single-workgroup kernels would
     // take (the tile-sharded device CG2D runs its parts in several processes)
@@ -1316,7 +1307,7 @@ int mgcm_init(mgcm_model *m) {
   drop_graphs(m);
   m->thetaA = m->f.theta;
   m->saltA = m->f.salt;
-  m->useGraph = getenv("MGCM_NO_GRAPH") == nullptr;
+  m->useGraph = true;
   int it0 = m->p.nIter0;
   // every copy is ordered on the model's stream (a null-stream hipMemcpy does not wait for
   // the non-blocking streams)
@@ -1411,22 +1402,8 @@ static TracerArgs tracer_args(mgcm_model *m, bool salt) {
 static int tracers_on(mgcm_model *m, hipStream_t st, const Fields *fo = nullptr) {
   const TracerArgs aT = tracer_args(m, false), aS = tracer_args(m, true);
   const Fields &F = fo ? *fo : m->f;   // the fields the kernels read (fo: the hFac snapshot)
-  if (tracer_pair_ok(m->d, m->p, aT, aS)) {   // both tracers in one pair of launches
-    TIMED(K_TEMP, launch_tracer_pair(m->d, m->p, F, aT, aS, m->d_ctr, st));
-    std::swap(m->f.theta, m->f.thetaNext);
-    std::swap(m->f.salt, m->f.saltNext);
-    return 0;
-  }
   if (tracer_hpair_ok(m->d, m->p, aT, aS)) {   // small grids: both tracers per launch
     TIMED(K_TEMP, launch_tracer_hpair(m->d, m->p, F, aT, aS, m->d_ctr, st));
-    std::swap(m->f.theta, m->f.thetaNext);
-    std::swap(m->f.salt, m->f.saltNext);
-    return 0;
-  }
-  if (tracer_impl2_ok(m->p, F, aT, aS)) {   // two right-hand sides, one paired implicit solve
-    TIMED(K_TEMP, launch_tracer_step(m->d, m->p, F, aT, m->d_ctr, st, false));
-    TIMED(K_TEMP, launch_tracer_step(m->d, m->p, F, aS, m->d_ctr, st, false));
-    TIMED(K_TEMP, launch_tracer2_impl(m->d, m->p, F, aT, aS, st));
     std::swap(m->f.theta, m->f.thetaNext);
     std::swap(m->f.salt, m->f.saltNext);
     return 0;
@@ -1606,22 +1583,20 @@ static int one_step(mgcm_model *m) {
   // what THERMODYNAMICS reads or writes (no r* rewrite of hFac; SOLVE_FOR_PRESSURE and CG2D
   // read gU, gV, hFac and eta, write the solver's vectors and etaN), so the tracers may run
   // beside the pressure solve too and join before MOMENTUM_CORRECTION_STEP rewrites u, v, w.
-  // thermoAt (MGCM_THERMO_AT): 0 fork after DO_OCEANIC_PHYS (beside DYNAMICS), 1 fork after
-  // DYNAMICS (beside SOLVE_FOR_PRESSURE: the pressure solve leaves most CUs idle while
-  // DYNAMICS, alone, has the chip), 2 fork after CALC_DIV_GHAT (beside CG2D alone); 1 and 2
-  // only under the linear free surface.  LLC-90 (profiles/r03/thermo_at/): 1.98 ms at 0,
-  // 1.86 at 1, 1.88 at 2 -- 1 is the default where it applies
-  const int thermoAtEnv = getenv("MGCM_THERMO_AT") ? atoi(getenv("MGCM_THERMO_AT")) : 1;
+  // The fork comes after DYNAMICS (beside SOLVE_FOR_PRESSURE: the pressure solve leaves most
+  // CUs idle while DYNAMICS, alone, has the chip), under the linear free surface only.
+  // LLC-90 (profiles/r03/thermo_at/): 1.98 ms forked after DO_OCEANIC_PHYS, 1.86 after
+  // DYNAMICS, 1.88 after CALC_DIV_GHAT (round 5 removed the two slower placements)
   const bool lateJoin = fork && m->p.nonlinFreeSurf <= 0;
-  const bool thermoLate = lateJoin && thermoAtEnv >= 1;
+  const bool thermoLate = lateJoin;
   // With the late join (THERMODYNAMICS beside the pressure solve) the new tracers' halos are
   // filled on the tracers' stream right after them -- DO_FIELDS_BLOCKING_EXCHANGES' theta and
   // salt, which nothing before it reads -- so the end-of-step exchange carries only the
   // velocities (MG_FUSE_TREX)
-  const bool trEx = lateJoin && thermoAtEnv >= 1 && mg_fuse_on(MG_FUSE_TREX);
+  const bool trEx = lateJoin && mg_fuse_on(MG_FUSE_TREX);
   // the VI path's halo-ring AB2 (launch_mom_ring) on the tracers' stream with them, when they
   // fork right after DYNAMICS (MG_FUSE_RING; joined with them before the correction step)
-  const bool ringAside = thermoLate && thermoAtEnv == 1 && mom_ring_separable(m->d, m->p) && mg_fuse_on(MG_FUSE_RING);
+  const bool ringAside = thermoLate && mom_ring_separable(m->d, m->p) && mg_fuse_on(MG_FUSE_RING);
   auto fork_thermo = [&]() -> int {
     HIPCHK(hipEventRecord(m->evFork, m->stream));
     HIPCHK(hipStreamWaitEvent(m->stream2, m->evFork, 0));
@@ -1649,9 +1624,9 @@ static int one_step(mgcm_model *m) {
   // (profiles/r04/tcg/): the tracers' launches beside DYNAMICS cost more than the 190 us
   // single-CU solve they could hide behind
   const bool tcg = forkable && m->p.nonlinFreeSurf > 0 && m->p.select_rStar > 0 && m->snapH &&
-                   mg_fuse_on(MG_FUSE_TCG) && !tracer_pair_ok(m->d, m->p, aT, aS);
+                   mg_fuse_on(MG_FUSE_TCG);
   const bool tcgFork = tcg && fork;
-  const bool dtFused = forkable && !tcg && m->p.nonlinFreeSurf > 0 && !tracer_pair_ok(m->d, m->p, aT, aS) &&
+  const bool dtFused = forkable && !tcg && m->p.nonlinFreeSurf > 0 &&
                        dyn_thermo_fusable(m->d, m->p, aT, aS);
   auto fork_tcg = [&]() -> int {
     HIPCHK(hipEventRecord(m->evFork, m->stream));
@@ -1695,13 +1670,9 @@ static int one_step(mgcm_model *m) {
   // the fold's first grid, the preconditioner in its second; UPDATE_R_STAR then rewrites hFac only
   const bool opEarly = dtFused && m->p.nonlinFreeSurf > 2 && dyn_thermo_takes_gm(m->p) && m->d.nT == m->d.nTiles &&
                        mg_fuse_on(MG_FUSE_OPE);
-  // the same outside the fold where GMREDI_CALC_TENSOR shares CALC_PHI_HYD's grid (gmPhi, e.g.
-  // the staggered cube): the operator there, the preconditioner in the r* pass.  Opt-in
-  // (MGCM_OPE_GM=1, read per step): bit-identical, but config 3 steps slower with it, 0.4235-0.4257
-  // against 0.4165-0.4234 ms/step (profiles/r04/ope_cs/) -- the operator's serial level loop
-  // lengthens the tensor + CALC_PHI_HYD grid more than the launch it saves
-  const bool opGm = gmPhi && m->p.nonlinFreeSurf > 2 && m->d.nT == m->d.nTiles && mg_fuse_on(MG_FUSE_OPE) &&
-                    getenv("MGCM_OPE_GM") && atoi(getenv("MGCM_OPE_GM")) == 1;
+  // (round 4 measured the operator also in GMREDI_CALC_TENSOR + CALC_PHI_HYD's grid on the
+  // staggered cube: slower, 0.4235-0.4257 against 0.4165-0.4234 ms/step, profiles/r04/ope_cs/;
+  // removed in round 5)
   if (m->p.momStepping) {
     if (dtFused) {
       TIMED(K_MOM, launch_dyn_thermo(m->d, m->p, m->f, aT, aS, m->d_ctr, m->stream, opEarly ? m->d_srcOf : nullptr));
@@ -1709,10 +1680,10 @@ static int one_step(mgcm_model *m) {
       std::swap(m->f.salt, m->f.saltNext);
     } else if (physPhi) TIMED(K_MOM, launch_mom_step(m->d, m->p, m->f, m->d_ctr, m->stream, !ringAside));
     else if (gmPhi) {
-      TIMED(K_PHI, launch_gm_phi(m->d, m->p, m->f, m->stream, opGm));
+      TIMED(K_PHI, launch_gm_phi(m->d, m->p, m->f, m->stream));
       TIMED(K_MOM, launch_mom_step(m->d, m->p, m->f, m->d_ctr, m->stream, !ringAside));
     } else if (dynamics_on(m, !ringAside)) return -1;
-    if (thermoLate && thermoAtEnv == 1 && fork_thermo()) return -1;
+    if (thermoLate && fork_thermo()) return -1;
     if (tcgFork) HIPCHK(hipStreamWaitEvent(m->stream, m->evSnap, 0));   // the copy before hFac is rewritten
     else if (fork && !lateJoin && !dtFused) HIPCHK(hipStreamWaitEvent(m->stream, m->evJoin, 0));
     // forward_step.F:829-877: UPDATE_R_STAR(.TRUE.) + UPDATE_CG2D
@@ -1721,9 +1692,8 @@ static int one_step(mgcm_model *m) {
     // walking every 2-D point costs more than the launch it saves)
     const bool sfpFused = mg_fuse_on(MG_FUSE_SFP) && m->p.nonlinFreeSurf > 0 && m->d.nT == m->d.nTiles;
     if (m->p.nonlinFreeSurf > 0)
-      TIMED(K_RSTAR, update_r_star_cg2d(m, sfpFused, opEarly || opGm, opGm || (opEarly && mg_ope_at() == 3)));
+      TIMED(K_RSTAR, update_r_star_cg2d(m, sfpFused, opEarly, false));
     if (!sfpFused) TIMED(K_RHS, launch_sfp_rhs(m->d, m->p, m->f, m->stream));
-    if (thermoLate && thermoAtEnv == 2 && fork_thermo()) return -1;
     const bool etaFused = mg_fuse_on(MG_FUSE_ETA) && cg2d_fuses_eta(m);
     TIMED(K_CG2D, launch_cg2d(m, m->p.cg2dMaxIters, m->p.cg2dUseMinResSol - 1, etaFused));
     // Under exactConserv the etaN of EXCH_XY_RL(cg2d_x) + etaN = recip_Bo*cg2d_x
@@ -1755,9 +1725,8 @@ static int one_step(mgcm_model *m) {
     // forward_step.F:965-977: CALC_R_STAR(etaH(n+1)); the next step's RESET_NLFS_VARS +
     // UPDATE_R_STAR(.FALSE.) restore the hFac in place, so they are not repeated here.
     // Under r* the exactConserv EXCH(eta) + UPDATE_ETAH runs inside CALC_R_STAR's pass
-    // (k_calc_r_star<FUSE>; MGCM_NO_ETAH_FUSE=1 keeps the two launches)
-    static const bool noFuse = getenv("MGCM_NO_ETAH_FUSE") && atoi(getenv("MGCM_NO_ETAH_FUSE")) == 1;
-    const bool fuseEtaH = m->p.exactConserv && m->p.nonlinFreeSurf > 0 && !noFuse;
+    // (k_calc_r_star<FUSE>)
+    const bool fuseEtaH = m->p.exactConserv && m->p.nonlinFreeSurf > 0;
     if (m->p.exactConserv && !fuseEtaH)
       TIMED(K_ETA, launch_exch_eta(m->d, m->p, m->f, m->d_srcOf, true, 0, m->stream, etaX ? 1 : 0));
     // CALC_R_STAR and the blocking exchanges in one grid on the small lat-lon grids
@@ -2053,6 +2022,20 @@ int mgcm_tile_copy(mgcm_model *m, const char *name, int t0, int nT, void *buf, i
 
 static int mwg_block_uncached(mgcm_model *m);
 
+// Everyone sharing a hand-off block must tag with the same launch epoch: the epoch words
+// (each process's / model's own, T.epoch) restart at 0 wherever a block is shared, and the
+// block itself is zeroed by its owner then, so granules an earlier solve of one sharer left
+// (tagged with that sharer's epochs) match no tag of the shared solves.  A hand-off that
+// times out in a shared solve is fatal for the run (the epochs may then diverge: each sharer's
+// first part reads the shared timeout word at its own time): ShardedModel.check_solves raises,
+// the Fortran drop-ins die (fortran_abi.hip); re-sharing restarts both words.
+static int mwg_restart_epoch(mgcm_model *m, bool zeroBlock) {
+  if (zeroBlock) HIPCHK(hipMemset(m->mwg.ctr, 0, m->mwg.hsBytes));
+  HIPCHK(hipMemset(m->mwg.epoch, 0, 64));
+  HIPCHK(hipDeviceSynchronize());
+  return 0;
+}
+
 // The tile-sharded device CG2D: every process launches the multi-workgroup solver's parts
 // of its own tiles, all on ONE hand-off block (granules, epoch, timeout word), which the
 // first process exports by IPC and the others map; every granule access is then at system
@@ -2063,7 +2046,7 @@ int mgcm_cg2d_shared_export(mgcm_model *m, void *handle) {
   HIPCHK(hipSetDevice(m->device));
   HIPCHK(hipStreamSynchronize(m->stream));
   // the importers' launches may run on other GPUs: an uncached block (mwg_block_uncached)
-  if (mwg_block_uncached(m)) return -1;
+  if (mwg_block_uncached(m) || mwg_restart_epoch(m, true)) return -1;
   hipIpcMemHandle_t h;
   HIPCHK(hipIpcGetMemHandle(&h, (void *)m->mwg.ctr));
   memcpy(handle, &h, sizeof h);
@@ -2086,6 +2069,7 @@ int mgcm_cg2d_shared_import(mgcm_model *m, const void *handle) {
   m->mwg.part = (unsigned long long *)((char *)p + 64);
   m->mwg.xs = m->mwg.part + partGr;
   m->mwg.sys = 1;
+  if (mwg_restart_epoch(m, false)) return -1;
   drop_graphs(m);
   return 0;
 }
@@ -2375,7 +2359,7 @@ int mgcm_cg2d_share(mgcm_model *m, mgcm_model *owner) {
   HIPCHK(hipSetDevice(owner->device));
   HIPCHK(hipStreamSynchronize(owner->stream));
   if (mwg_block_uncached(owner)) return -1;
-  if (m == owner) return 0;
+  if (m == owner) return mwg_restart_epoch(owner, true);
   HIPCHK(hipSetDevice(m->device));
   HIPCHK(hipStreamSynchronize(m->stream));
   if (m->device != owner->device) {
@@ -2388,6 +2372,7 @@ int mgcm_cg2d_share(mgcm_model *m, mgcm_model *owner) {
   m->mwg.part = owner->mwg.part;
   m->mwg.xs = owner->mwg.xs;
   m->mwg.sys = 1;
+  if (mwg_restart_epoch(m, false)) return -1;
   drop_graphs(m);
   return 0;
 }

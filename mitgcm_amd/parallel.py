@@ -18,10 +18,12 @@ The MI355X design keeps the 3-D work sharded; the 2-D solve runs where it is fas
   (u, v, w, theta, salt) with each neighbouring process (twice with
   staggerTimeStep: the new velocities before THERMODYNAMICS, then the
   tracers);
-* cg2d="auto" (the default) picks "device" where the model's solver is the multi-workgroup
-  one (C3, C5: the grids too large for one CU) and "replicated" where it is a single-CU
-  kernel (C2, C4: ~4k points, where one CU's solve at ~1.8 us per iteration beats any
-  solve whose iteration crosses GPUs);
+* cg2d="auto" (the default) decides by the cost model of cg2d_policy: "replicated" for a
+  single-CU kernel (C2, C4: ~4k points, one CU's solve at ~1.6 us per iteration beats any
+  iteration that crosses GPUs) and, across processes, for the multi-workgroup solve too
+  whenever its two hand-offs per iteration over the fabric cost more than the iteration
+  work a 1/N share of the parts saves (C3: 6 parts on one XCD, ~1 us hand-offs; C5: 117
+  parts chip-wide, ~0.9 us of compute per ~6 us iteration); "device" with one process;
 * cg2d="device": the multi-workgroup CG2D (kernels_cg2d_mwg.hip) with every process
   launching only the parts of its own tiles; all parts meet on ONE hand-off block (rank 0's,
   mapped into the others by IPC, system-scope granules).  No host step and no collective
@@ -114,6 +116,82 @@ class HaloPlan:
         return sorted(set(self.send) | set(self.recv))
 
 
+class Comm:
+    """torch.distributed bound to one process group: the default group, or a subgroup (bench.py
+    shards cs32x15 over min(N, 6) of N ranks).  It offers the module functions this file calls,
+    with ranks local to the group (point-to-point peers are translated to global ranks), so
+    the exchange helpers below take either this or the torch.distributed module itself."""
+
+    def __init__(self, dist, group=None):
+        self.d, self.group = dist, group
+        self.rank = dist.get_rank(group)
+        self.world = dist.get_world_size(group)
+        self.isend, self.irecv = dist.isend, dist.irecv
+
+    def get_rank(self):
+        return self.rank
+
+    def get_world_size(self):
+        return self.world
+
+    def get_backend(self):
+        return self.d.get_backend(self.group)
+
+    def _g(self, r):
+        return r if self.group is None else self.d.get_global_rank(self.group, r)
+
+    def P2POp(self, op, tensor, peer):
+        return self.d.P2POp(op, tensor, self._g(peer), group=self.group)
+
+    def batch_isend_irecv(self, ops):
+        return self.d.batch_isend_irecv(ops)
+
+    def all_gather(self, out, t):
+        return self.d.all_gather(out, t, group=self.group)
+
+    def all_gather_into_tensor(self, out, t):
+        return self.d.all_gather_into_tensor(out, t, group=self.group)
+
+    def all_reduce(self, t, op=None):
+        return self.d.all_reduce(t, op=op if op is not None else self.d.ReduceOp.SUM, group=self.group)
+
+    def broadcast_object_list(self, obj, src=0):
+        return self.d.broadcast_object_list(obj, src=self._g(src), group=self.group)
+
+    def barrier(self):
+        return self.d.barrier(group=self.group)
+
+
+# CG2D placement across processes (cg2d="auto").  Per iteration the multi-workgroup solve makes
+# two grid-wide hand-offs (kernels_cg2d_mwg.hip); its compute per iteration is small against
+# them (LLC-90: ~2 150 of ~17 750 shader cycles, profiles/r03/mwg_stamps/).  Across processes
+# the hand-off block lives on ONE GPU, so every part off that GPU polls it over the fabric: each
+# hand-off costs at least a fabric round trip instead of an on-chip one, while the work that
+# sharding removes is only that small compute share.  Replicated, every GPU runs the one-GPU
+# solve on the gathered right-hand side (one all-gather of cg2d_b per step, no fabric inside an
+# iteration).  The policy compares the two per solve with these constants (us):
+HANDOFF_ONCHIP_US = {"pinned": 1.0, "spread": 3.0}   # one-XCD / chip-wide hand-off (DESIGN.md §3)
+HANDOFF_FABRIC_US = 5.0    # one hand-off polled across xGMI: >= one round trip (MI355X_MICROARCH.md)
+MWG_COMPUTE_US_PER_ITER = 0.9   # LLC-90: ~2 150 shader cycles of an iteration's own work at 2.4 GHz
+
+
+def cg2d_policy(solver, world, parts=0, pinned=False, compute_us=0.0):
+    """(mode, reason) for cg2d="auto".  solver: the model's CG2D kernel ('mwg' or a single-CU
+    one); parts: workgroups of the multi-workgroup solve; compute_us: its per-iteration compute
+    (the part of an iteration that a 1/world share of the parts shrinks)."""
+    if solver != "mwg":
+        return "replicated", "single-CU CG2D: one CU's solve beats any iteration that crosses GPUs"
+    if world <= 1:
+        return "device", "one process: the resident multi-workgroup solve"
+    h1 = HANDOFF_ONCHIP_US["pinned" if pinned else "spread"]
+    replicated = 2 * h1 + compute_us
+    device = 2 * HANDOFF_FABRIC_US + compute_us / world
+    if device < replicated:
+        return "device", "modelled %.1f us/iteration across %d GPUs < %.1f replicated" % (device, world, replicated)
+    return "replicated", ("modelled %.1f us/iteration replicated <= %.1f with the hand-offs across %d GPUs "
+                          "(%d parts, %s)" % (replicated, device, world, parts, "one XCD" if pinned else "chip-wide"))
+
+
 def exchange(dist, plan, pack, unpack, make_buf):
     """Point-to-point exchange of halo sources with every neighbouring process.
     pack(peer) -> tensor to send; make_buf(peer) -> receive tensor;
@@ -181,9 +259,10 @@ class ShardedModel:
     configuration; after init(), step()/forward_step() keep the tiles a
     process owns bit-identical to a single-process run."""
 
-    def __init__(self, model, dist, device=None, cg2d="auto", overlap="thermo", model_stream="shared"):
+    def __init__(self, model, dist, device=None, cg2d="auto", overlap="thermo", model_stream="shared", group=None):
         import torch
         from ._lib import check, lib
+        dist = dist if isinstance(dist, Comm) else Comm(dist, group)
         self.torch, self.dist, self.m = torch, dist, model
         self.L, self.check = lib(), check
         g = model.g
@@ -243,8 +322,11 @@ class ShardedModel:
         self.g_out = torch.empty(self.world * mt * n2, dtype=torch.float64, device=dv)
         if cg2d not in ("auto", "replicated", "distributed", "device"):
             raise ValueError("cg2d must be 'auto', 'replicated', 'distributed' or 'device'")
+        self.cg2d_reason = "requested"
         if cg2d == "auto":
-            cg2d = "device" if model.cg2d_kernel() == "mwg" else "replicated"
+            pinned = self.L.mgcm_get_param(model.h, b"cg2dPinned") != 0.0
+            cg2d, self.cg2d_reason = cg2d_policy(model.cg2d_kernel(), self.world, model.cg2d_parts(), pinned,
+                                                 MWG_COMPUTE_US_PER_ITER)
         self.cg2d = cg2d
         if cg2d == "device" and self.world > 1:
             # (one process: the model's own hand-off block as the resident solve uses it --
@@ -553,10 +635,11 @@ class ShardedModel:
             raise RuntimeError("CG2D failed (grid hand-off timeout, numIters = -1) in step(s) %s of the last %d"
                                % (bad, nsteps))
 
-    def replay(self, npairs=1, check=True):
+    def replay(self, npairs=1, check=None):
         """Replay the captured pair of steps npairs times (the device's per-step record ring
         restarts at the first replay); with check, the batch's solve records are read back
-        and a failed solve raises (check_solves)."""
+        and a failed solve raises (check_solves).  check=None: only for the device CG2D, the
+        one solver whose hand-offs can time out (the read-back synchronises the host)."""
         self._check_records(2 * npairs)
         self.check(self.L.mgcm_begin_steps(self.m.h), "mgcm_begin_steps")   # on self.stream
         if self.model_stream != "shared":
@@ -567,16 +650,17 @@ class ShardedModel:
         if self.model_stream != "shared":
             self._consume()   # the model's later work after the replays
         self.check(self.L.mgcm_end_steps(self.m.h, 2 * npairs), "mgcm_end_steps")
-        if check:
+        if check or (check is None and self.cg2d == "device"):
             self.check_solves(2 * npairs)
 
-    def forward_step(self, nsteps=1, check=True):
-        """nsteps sharded FORWARD_STEPs; with check, a failed solve raises (check_solves)."""
+    def forward_step(self, nsteps=1, check=None):
+        """nsteps sharded FORWARD_STEPs; with check, a failed solve raises (check_solves);
+        check=None: only for the device CG2D (as replay)."""
         self._check_records(nsteps)
         self.check(self.L.mgcm_begin_steps(self.m.h), "mgcm_begin_steps")
         for _ in range(nsteps):
             self.step()
-        if check:
+        if check or (check is None and self.cg2d == "device"):
             self.check_solves(nsteps)
 
     def gather_field(self, name):

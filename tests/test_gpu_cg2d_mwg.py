@@ -18,7 +18,7 @@ pytestmark = pytest.mark.gpu
 
 def _ocean90_mwg(spread=False):
     from mitgcm_amd import configs
-    env = {"MGCM_CG2D_NOBXY": "1", "MGCM_CG2D_NOBLK": "1"}
+    env = {"MGCM_CG2D_NOBLOCKED": "1"}
     if spread:
         env["MGCM_CG2D_SPREAD"] = "1"
     old = {k: os.environ.get(k) for k in env}

@@ -6,10 +6,10 @@ Bars:
   * LLC-30 (13 tiles of 30 x 30, 10 levels, OL = 4): 8 steps bit-identical to the oracle
     summing CG2D in the device's order, with the flat and the k-march tracer kernels;
     cg2d_iters identical to the reference-order oracle;
-  * LLC-90 as benched (13 tiles of 90 x 90, 50 levels): the initial state round-trips; the
-    first step's monitored values (dynstat, CG2D residuals and iterations) are bit-identical
-    to the device-order oracle's at full size, and its iteration count equals the
-    reference-order oracle's; 4 steps stay finite with a converged CG2D.  The synthetic set-up has no reference output: parity
+  * LLC-90 as benched (13 tiles of 90 x 90, 50 levels): the initial state round-trips; 4
+    steps' monitored values (dynstat, CG2D residuals and iterations) and the final fields
+    are bit-identical to the device-order oracle's at full size, and every iteration count
+    equals the reference-order oracle's.  The synthetic set-up has no reference output: parity
     unpinned against the reference, pinned device-vs-oracle.
 """
 import numpy as np
@@ -18,43 +18,29 @@ import pytest
 pytestmark = pytest.mark.gpu
 
 
-@pytest.mark.parametrize("march", [None, "1:2", "1:10", "1:3:single", "1:3:single:v1", "vi:4", "vi:3:generic", "fuse:29",
-                                   "fuse:45", "fuse:77", "impl2:1", "impl2:0"])
+@pytest.mark.parametrize("march", [None, "tracer", "tracer:v1", "vi", "vi:generic", "fuse:29", "fuse:45", "fuse:77"])
 def test_llc30_8_steps_bitexact_vs_device_order_oracle(march, monkeypatch):
-    """march = "on:KC[:single]": the tracer right-hand side as the k-march (the LLC-90
-    default) with KC levels per workgroup -- 5 chunks, 1, 4 uneven -- for both tracers in one
-    launch pair (k_tracer2_march + k_tracer2_impl) or one tracer at a time (k_tracer_march),
-    instead of the flat kernel.  "vi:KC[:generic|uv]": MOM_VECINV as the k-march (the LLC-90
-    default; LLC-30 has too few blocks to pick it by itself) with KC levels per workgroup, in
-    its compile-time specialisation (k_mom_vi_m2<32, 8, LLC options>) or the generic kernel.
-    "fuse:MASK": the MGCM_STEP_FUSE launch fusions (29: the opt-in k_phys_phi pass; 45: the
-    opt-in EXCH(cg2d_x) + etaN beside the correction step; 77: the tracers' halo exchange on
-    their own stream).  "impl2:ON": both tracers' implicit solves in one launch
-    (k_tracer2_impl) after the single-tracer right-hand sides, k-march ON = 1 or flat 0.
-    ":v1": the other forms of the 16-byte switches -- the one-column single-tracer k-march
-    (the default is its two-column form), the two-column DO_OCEANIC_PHYS forced (at full
-    size the default; below 2^21 points the one-column form runs) and the opt-in two-column
-    flat CALC_PHI_HYD."""
+    """march: the LLC-90 default kernel forms forced on LLC-30 (too small to pick them by
+    itself).  "tracer": the tracer right-hand side as the k-march (MGCM_TRACER_MARCH=1, five
+    level chunks) instead of the flat kernel; ":v1" the other forms of the 16-byte switches --
+    the one-column k-march (the default is its two-column form) and the two-column
+    DO_OCEANIC_PHYS forced (at full size the default; below 2^21 points the one-column form
+    runs).  "vi": MOM_VECINV as the k-march in its compile-time specialisation
+    (k_mom_vi_m2<32, 8, LLC options>), "vi:generic" the generic k-march that serves option sets
+    without an instantiation (MGCM_VI_KERNEL=march | march_generic).  "fuse:MASK": the
+    MGCM_STEP_FUSE launch fusions (29: the opt-in k_phys_phi pass; 45: the opt-in
+    EXCH(cg2d_x) + etaN beside the correction step; 77: the tracers' halo exchange on their own
+    stream)."""
     if march and march.endswith(":v1"):
         monkeypatch.setenv("MGCM_TRACER_MARCH2", "0")
         monkeypatch.setenv("MGCM_PHYS_V2", "2")
-        monkeypatch.setenv("MGCM_PHI_V2", "1")
         march = march[:-3]
-    if march and march.startswith("impl2:"):
-        monkeypatch.setenv("MGCM_TRACER_IMPL2", "1")
-        monkeypatch.setenv("MGCM_TRACER_MARCH", march.split(":")[1])
-    elif march and march.startswith("fuse:"):   # MGCM_STEP_FUSE mask: 29 adds DO_OCEANIC_PHYS + CALC_PHI_HYD in one pass
+    if march and march.startswith("fuse:"):   # MGCM_STEP_FUSE mask: 29 adds DO_OCEANIC_PHYS + CALC_PHI_HYD in one pass
         monkeypatch.setenv("MGCM_STEP_FUSE", march.split(":")[1])
-    elif march and march.startswith("vi:"):
-        monkeypatch.setenv("MGCM_VI_KERNEL", "march")
-        monkeypatch.setenv("MGCM_VI_KC", march.split(":")[1])
-        monkeypatch.setenv("MGCM_VI_M2", "0" if march.endswith("generic") else "1")
-    elif march:
-        on, kc = march.split(":")[:2]
-        monkeypatch.setenv("MGCM_TRACER_MARCH", on)
-        monkeypatch.setenv("MGCM_TR_KC", kc)
-        if march.endswith("single"):
-            monkeypatch.setenv("MGCM_TRACER_PAIR", "0")
+    elif march and march.startswith("vi"):
+        monkeypatch.setenv("MGCM_VI_KERNEL", "march_generic" if march.endswith("generic") else "march")
+    elif march == "tracer":
+        monkeypatch.setenv("MGCM_TRACER_MARCH", "1")
     from mitgcm_amd import configs
     from mitgcm_amd.model import dynstat
     from oracle.harness import oracle_from_config
@@ -97,20 +83,26 @@ def test_llc90_full_size_steps():
     od, _ = oracle_from_config(configs.llc_synthetic)
     od.set_sum_plan(plan, NT, PPT, NG, fma=m.cg2d_fma())
     o_ref, _ = oracle_from_config(configs.llc_synthetic)
-    m.forward_step(1)
-    od.forward_step()
-    o_ref.forward_step()
-    md = m.solve_stats()
-    md.update(dynstat(m))
-    dd = od.dynstat()
-    assert md["cg2d_iters"] == dd["cg2d_iters"] == int(o_ref.get("numIters")), (
-        md["cg2d_iters"], dd["cg2d_iters"], o_ref.get("numIters"))
-    for k, v in md.items():
-        if k in dd:
-            assert v == dd[k], (k, v, dd[k])
-    m.forward_step(3)
-    m.sync()
-    iters = [md["cg2d_iters"]] + [m.solve_stats(back=b)["cg2d_iters"] for b in range(3)]   # records of the last batch
+    iters = []
+    for step in range(1, 5):   # 4 steps, each compared with both oracles
+        m.forward_step(1)
+        od.forward_step()
+        o_ref.forward_step()
+        md = m.solve_stats()
+        md.update(dynstat(m))
+        dd = od.dynstat()
+        assert md["cg2d_iters"] == dd["cg2d_iters"] == int(o_ref.get("numIters")), (
+            step, md["cg2d_iters"], dd["cg2d_iters"], o_ref.get("numIters"))
+        for k, v in md.items():
+            if k in dd:
+                assert v == dd[k], (step, k, v, dd[k])
+        iters.append(md["cg2d_iters"])
+    g = m.g
+    inner = (Ellipsis,) + g.sl(1, g.sNx, 1, g.sNy)
+    for n in ("uVel", "vVel", "wVel", "theta", "salt", "etaN"):
+        dev = m.get(n)
+        ref = np.array(od.arr(n)).reshape(dev.shape)
+        assert np.array_equal(dev[inner], ref[inner]), (n, np.abs(dev - ref)[inner].max())
     st = m.solve_stats()
     assert all(0 < i < params["cg2dMaxIters"] for i in iters), iters
     assert st["cg2d_last_res"] < st["cg2d_init_res"]
@@ -119,20 +111,15 @@ def test_llc90_full_size_steps():
     m.close()
 
 
-@pytest.mark.parametrize("thermo_at", ["0", "1", "2"])
-def test_llc30_thermodynamics_overlap_bit_identical(thermo_at, monkeypatch):
-    """THERMODYNAMICS on the second stream (forced on) -- under the linear free surface forked
-    after DO_OCEANIC_PHYS (thermo_at 0), after DYNAMICS (1) or after CALC_DIV_GHAT (2, beside
-    the multi-workgroup CG2D on CUs it keeps to itself), joined before the correction step --
-    against one stream (forced off): 8 graph-replayed steps bit-identical."""
+def test_llc30_thermodynamics_overlap_bit_identical(monkeypatch):
+    """THERMODYNAMICS on the second stream (forced on: under the linear free surface forked
+    after DYNAMICS, beside the pressure solve, joined before the correction step) against one
+    stream (forced off): 8 graph-replayed steps bit-identical."""
     from mitgcm_amd import configs
     cfg = lambda: configs.llc_synthetic(n=30, Nr=10)
     out = {}
-    monkeypatch.setenv("MGCM_THERMO_AT", thermo_at)
     for mode in ("on", "off"):
-        monkeypatch.delenv("MGCM_NO_OVERLAP", raising=False)
-        monkeypatch.delenv("MGCM_OVERLAP", raising=False)
-        monkeypatch.setenv("MGCM_OVERLAP" if mode == "on" else "MGCM_NO_OVERLAP", "1")
+        monkeypatch.setenv("MGCM_OVERLAP", "1" if mode == "on" else "0")
         m = configs.make_model(cfg)
         m.forward_step(8)
         m.sync()

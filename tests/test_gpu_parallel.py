@@ -33,6 +33,8 @@ def _make(cfg, force_mwg=False):
         fn = lambda: configs.baroclinic_gyre(tempAdvScheme=33)
     elif cfg == "llc30":   # BASELINE config 5's LLC topology at n = 30 (13 tiles, pkg/exch2 facets)
         fn = lambda: configs.llc_synthetic(n=30, Nr=10)
+    elif cfg == "llc90":   # BASELINE config 5 at full size
+        fn = configs.llc_synthetic
     else:
         fn = configs.global_ocean_cs32x15
     if force_mwg:   # the multi-workgroup CG2D also where a single-workgroup kernel would be chosen
@@ -40,7 +42,7 @@ def _make(cfg, force_mwg=False):
     return configs.make_model(fn)
 
 
-def _worker(rank, world, port, cfg, nsteps, q, cg2d="replicated", overlap="thermo"):
+def _worker(rank, world, port, cfg, nsteps, q, cg2d="replicated", overlap="thermo", keep_full=True, pre_solve=False):
     import torch
     import torch.distributed as dist
     from mitgcm_amd.parallel import ShardedModel
@@ -50,6 +52,13 @@ def _worker(rank, world, port, cfg, nsteps, q, cg2d="replicated", overlap="therm
         torch.cuda.set_device(0)
         dev_cg = cg2d == "device"
         m = _make(cfg, dev_cg)
+        if pre_solve and rank == 0:
+            # a multi-workgroup solve on this rank only before the block is shared: its launch
+            # epoch advances and its granules stay in the block the others then map
+            n = m.g.nTiles * m.g.ny * m.g.nx
+            b = np.zeros(n)
+            b[n // 2] = 1.0e-3
+            m.cg2d(b, np.zeros(n), 5)
         sm = ShardedModel(m, dist, device=torch.device("cuda", 0), cg2d=cg2d, overlap=overlap)
         sm.forward_step(nsteps)
         m.sync()
@@ -58,7 +67,7 @@ def _worker(rank, world, port, cfg, nsteps, q, cg2d="replicated", overlap="therm
         res = {"t0": sm.t0, "nT": sm.nT, "stats": stats, "overlap": sm.overlap, "fork": sm.fork}
         if cg2d == "distributed":
             res["iters"] = list(sm.cg_iters)
-        if cg2d in ("distributed", "device") and rank == 0:
+        if cg2d in ("distributed", "device") and rank == 0 and keep_full:
             res["full"] = full
         if rank == 0:
             ref = _make(cfg, dev_cg)
@@ -178,3 +187,70 @@ def test_device_cg2d_across_processes(cfg, worlds, nsteps):
         for rank, r in out.items():
             assert r["stats"] == r0["ref_stats"], (w, rank, r["stats"], r0["ref_stats"])
         assert all(i > 0 for i in its), its
+
+
+@pytest.mark.timeout(600)
+@pytest.mark.parametrize("cg2d", ["replicated", "device"])
+def test_llc90_eight_way_partition(cg2d):
+    """BASELINE config 5 at full size (13 tiles of 90 x 90 x 50) in the exact partition of
+    the 8-GPU node -- tiles 2,2,2,2,2,1,1,1 over 8 processes, rehearsed here on one GPU over
+    gloo -- for 2 steps with the replicated CG2D (what cg2d="auto" picks across GPUs,
+    parallel.cg2d_policy) and with the device CG2D (117 parts launched by 8 processes on one
+    IPC-shared hand-off block).  Bars: every field bit-identical to one process, every solve
+    record equal."""
+    import torch.multiprocessing as mp
+    from mitgcm_amd.parallel import TilePartition
+    world, nsteps = 8, 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, "llc90", nsteps, q, cg2d, "thermo", False))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    out = {}
+    for _ in procs:
+        rank, res = q.get(timeout=540)
+        assert "error" not in res, "rank %d: %s" % (rank, res["error"])
+        out[rank] = res
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    r0 = out[0]
+    print("llc90 x8 (%s CG2D): iterations %s, max |diff| vs 1 process %s" % (
+        cg2d, [s["cg2d_iters"] for s in r0["stats"]], r0["diff"]))
+    assert all(r0["equal"].values()), r0["diff"]
+    for rank, r in out.items():
+        assert r["stats"] == r0["ref_stats"], (rank, r["stats"], r0["ref_stats"])
+    part = TilePartition(13, world)
+    assert part.counts == [2, 2, 2, 2, 2, 1, 1, 1]
+    assert sorted((r["t0"], r["nT"]) for r in out.values()) == [part.range(r) for r in range(world)]
+
+
+def test_device_cg2d_after_unshared_solve():
+    """Rank 0 runs a multi-workgroup solve of its own before ShardedModel shares its hand-off
+    block: sharing restarts every sharer's launch epoch and zeroes the block
+    (mgcm_cg2d_shared_export / _import), so the shared solves still match tag for tag and the
+    run stays bit-identical to one process."""
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    world, nsteps = 2, 2
+    procs = [ctx.Process(target=_worker, args=(r, world, port, "llc30", nsteps, q, "device", "thermo", False, True))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    out = {}
+    for _ in procs:
+        rank, res = q.get(timeout=300)
+        assert "error" not in res, "rank %d: %s" % (rank, res["error"])
+        out[rank] = res
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    r0 = out[0]
+    assert all(r0["equal"].values()), r0["diff"]
+    for rank, r in out.items():
+        assert r["stats"] == r0["ref_stats"], (rank, r["stats"], r0["ref_stats"])
+    assert all(s["cg2d_iters"] > 0 for s in r0["stats"])

@@ -328,3 +328,77 @@ def test_overlapped_group_exchanges(world):
         assert p.exitcode == 0
     for rank, ok in res:
         assert ok, "rank %d: overlapped tracer / velocity exchanges differ from the single-process EXCH" % rank
+
+
+def _sub_worker(rank, world, port, q):
+    """A subgroup of the default group (bench.py shards cs32x15 over min(N, 6) of N ranks):
+    ranks 1 and 2 of 3 exchange halos and gather partials through parallel.Comm, whose
+    group-local peers must map to the right global ranks."""
+    from mitgcm_amd.parallel import Comm, gather_tile_partials, start_exchange
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        sub = dist.new_group([1, 2], backend="gloo")   # collective over the default group
+        if rank == 0:
+            q.put((rank, True))
+            return
+        comm = Comm(dist, sub)
+        me, w = comm.get_rank(), comm.get_world_size()
+        topo = LatLonTopology(15, 8, 3, 3, 2, 2)
+        nT, ny, nx = topo.nTiles, topo.ny, topo.nx
+        n2 = nx * ny
+        truth = np.random.default_rng(3).standard_normal((nT, ny, nx))
+        part = TilePartition(nT, w)
+        t0, c = part.range(me)
+        mine = np.full_like(truth, np.nan)
+        mine[t0:t0 + c, 3:11, 3:18] = truth[t0:t0 + c, 3:11, 3:18]
+        plan = HaloPlan(topo.src_of_point(), n2, part, me)
+        flat = mine.reshape(-1)
+
+        def unpack(peer, buf):
+            flat[plan.recv[peer]] = buf.numpy()
+        start_exchange(comm, plan, lambda p: torch.from_numpy(flat[plan.send[p]].copy()), unpack,
+                       lambda p: torch.empty(plan.recv[p].size, dtype=torch.float64))()
+        src = topo.src_of_point()
+        dst = np.arange(src.size)
+        sel = (src != dst) & (dst // n2 >= t0) & (dst // n2 < t0 + c)
+        flat[dst[sel]] = flat[src[sel]]
+        ok = np.array_equal(mine[t0:t0 + c], topo.exchange(truth[:, None])[:, 0][t0:t0 + c])
+        local = torch.zeros((part.maxT, 2), dtype=torch.float64)
+        for i in range(c):
+            local[i] = torch.tensor([t0 + i, 10.0 * (t0 + i)])
+        allp = gather_tile_partials(comm, part, local, t0, c, w, part.maxT, nT, "gloo")
+        ok = ok and np.array_equal(allp[:, 0], np.arange(nT)) and comm.get_backend() == "gloo"
+        obj = ["from local rank 0" if me == 0 else None]
+        comm.broadcast_object_list(obj, src=0)
+        comm.barrier()
+        q.put((rank, ok and obj[0] == "from local rank 0"))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_comm_subgroup():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_sub_worker, args=(r, 3, port, q)) for r in range(3)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=120) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert all(res.values()), res
+
+
+def test_cg2d_policy():
+    """cg2d="auto" (parallel.cg2d_policy): a single-CU solver stays replicated; the
+    multi-workgroup solve stays on the device with one process and is replicated across
+    GPUs while its hand-offs dominate an iteration (C3 pinned, C5 chip-wide), device only
+    when the iteration work a 1/N share saves outweighs the fabric hand-offs."""
+    from mitgcm_amd.parallel import MWG_COMPUTE_US_PER_ITER, cg2d_policy
+    assert cg2d_policy("bxy", 8)[0] == "replicated"
+    assert cg2d_policy("mwg", 1, 117)[0] == "device"
+    assert cg2d_policy("mwg", 6, 6, pinned=True, compute_us=MWG_COMPUTE_US_PER_ITER)[0] == "replicated"
+    assert cg2d_policy("mwg", 8, 117, pinned=False, compute_us=MWG_COMPUTE_US_PER_ITER)[0] == "replicated"
+    assert cg2d_policy("mwg", 8, 4096, pinned=False, compute_us=100.0)[0] == "device"

@@ -4,7 +4,6 @@ import os
 import sys
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-os.environ["MGCM_NO_GRAPH"] = "1"
 from mitgcm_amd import configs  # noqa: E402
 
 cfg = sys.argv[1] if len(sys.argv) > 1 else "ocean90"

@@ -1,7 +1,7 @@
 #!/bin/bash
 # Diagnostic build with per-phase s_memtime stamps in k_mom_vi_m2 (MGCM_VI_STAMPS) into
 # mitgcm_amd/_build/diag/libmitgcm_amd_vistamps.so; run with MGCM_LIB pointing at it:
-#   MGCM_LIB=mitgcm_amd/_build/diag/libmitgcm_amd_vistamps.so MGCM_VI_M2_VAR=14 python bench.py ...
+#   MGCM_LIB=mitgcm_amd/_build/diag/libmitgcm_amd_vistamps.so python bench.py ...
 set -e
 cd "$(dirname "$0")/.."
 D=mitgcm_amd/_build/diag
