@@ -159,33 +159,85 @@ def config_fn(name):
             "tutorial_barotropic_gyre": configs.barotropic_gyre}[name]
 
 
-def cpu_baseline(config, seconds):
-    """Oracle (CPU restatement, 1 thread) timed on the same workload: as many
-    steps as fit in ~`seconds` of CPU time, reported in model-days/s."""
-    from mitgcm_amd import configs
+def _host_cpu():
+    """(model name, cores this process may use): the affinity set, capped by OMP_NUM_THREADS
+    (16 on the GPU box, whose os.cpu_count() reports the whole machine)."""
+    model = "unknown"
+    try:
+        for ln in open("/proc/cpuinfo"):
+            if ln.startswith("model name"):
+                model = ln.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    try:
+        n = min(n, int(os.environ.get("OMP_NUM_THREADS", n)))
+    except ValueError:
+        pass
+    return model, max(1, n)
+
+
+def _oracle_for(config, omp=False, **kw):
+    from oracle import harness
     from oracle.harness import cs32x15_oracle, gyre_oracle, latlon_oracle, ocean90_oracle, oracle_from_config
-    if config == "global_ocean.90x40x15":
-        o, _ = ocean90_oracle()
-    elif config == "global_ocean.cs32x15":
-        o, _ = cs32x15_oracle()
-    elif config == "tutorial_barotropic_gyre":
-        o = gyre_oracle()
-    elif config == "global_oce_latlon_90x40x15":
-        o, _ = latlon_oracle(nSx=1, nSy=1, OL=3)
-    elif config == "tutorial_global_oce_latlon":
-        o, _ = latlon_oracle()
-    else:
-        o, _ = oracle_from_config(config_fn(config))
-    dt_clock = o.get("deltaTClock")
+    harness.USE_OMP = omp
+    try:
+        if config == "global_ocean.90x40x15":
+            return ocean90_oracle(**kw)[0]
+        if config == "global_ocean.cs32x15":
+            return cs32x15_oracle(**kw)[0]
+        if config == "tutorial_barotropic_gyre":
+            return gyre_oracle()
+        if config == "global_oce_latlon_90x40x15":
+            return latlon_oracle(nSx=1, nSy=1, OL=3)[0]
+        if config == "tutorial_global_oce_latlon":
+            return latlon_oracle()[0]
+        return oracle_from_config(config_fn(config))[0]
+    finally:
+        harness.USE_OMP = False
+
+
+def _time_oracle(o, seconds):
     o.forward_step()  # warm
     n, t0 = 0, time.perf_counter()
     while time.perf_counter() - t0 < seconds:
         o.forward_step()
         n += 1
-    dt = time.perf_counter() - t0
-    return {"value": n * dt_clock / 86400.0 / dt, "unit": "model-days/s", "cores": 1, "kind": "port",
-            "sample": "%d FORWARD_STEPs of %s on the oracle (oracle/*.c, gcc -O2, 1 thread), %.1f s"
-                      % (n, config, dt)}
+    return n, time.perf_counter() - t0
+
+
+# the reference's own MPI decomposition of a workload (its verification SIZE.h), whose tiles the
+# multi-core baseline spreads over threads (global_sum_tile.F:161-191 keeps the tile order)
+REF_TILING = {"global_ocean.90x40x15": {"nSx": 9, "nSy": 4}}
+
+
+def cpu_baseline(config, seconds):
+    """The oracle (CPU restatement) timed on the same workload: as many steps as fit in
+    ~`seconds`, in model-days/s.  `value`: one core on the benched tiling (the sequential
+    build).  `all_cores`: the OpenMP build with the tiles over every core this process may
+    use, on the reference's own MPI tiling where it has one (REF_TILING) -- the tile loops of
+    DYNAMICS, THERMODYNAMICS and DO_OCEANIC_PHYS in parallel, the CG2D and the exchanges
+    sequential; bit-identical to one thread."""
+    o = _oracle_for(config)
+    dt_clock = o.get("deltaTClock")
+    n, dt = _time_oracle(o, seconds)
+    del o
+    cpu, cores = _host_cpu()
+    out = {"value": n * dt_clock / 86400.0 / dt, "unit": "model-days/s", "cores": 1, "kind": "port",
+           "sample": "%d FORWARD_STEPs of %s on the oracle (oracle/*.c, gcc -O2, 1 thread), %.1f s"
+                     % (n, config, dt), "cpu_model": cpu}
+    if cores > 1:
+        tiling = REF_TILING.get(config, {})
+        o = _oracle_for(config, omp=True, **tiling)
+        o.set(nThreads=cores)
+        n2, dt2 = _time_oracle(o, seconds)
+        del o
+        out["all_cores"] = {"value": n2 * dt_clock / 86400.0 / dt2, "unit": "model-days/s", "cores": cores,
+                            "kind": "port", "tiling": tiling or "the benched tiling",
+                            "sample": "%d FORWARD_STEPs of %s on the OpenMP oracle build (tiles over %d threads), "
+                                      "%.1f s" % (n2, config, cores, dt2)}
+    return out
 
 
 def pmc_traffic(path, kernel_keys):

@@ -80,6 +80,10 @@ void oracle_dynamics(OModel *m) {
   const int sNx = m->sNx, sNy = m->sNy, OLx = m->OLx, OLy = m->OLy, Nr = m->Nr, nx = m->nx;
   const long n2 = m->n2;
   const int iMin = 0, iMax = sNx + 1, jMin = 0, jMax = sNy + 1; /* dynamics.F:191-192 */
+  /* tiles in parallel (OpenMP; one thread = the sequential restatement): every tile's work
+     reads and writes its own slabs only, each thread keeps its own scratch */
+#pragma omp parallel if (m->nThreads > 1) num_threads(m->nThreads > 1 ? m->nThreads : 1)
+  {
   double *fVerU[2], *fVerV[2];
   for (int q = 0; q < 2; q++) { fVerU[q] = calloc(n2, 8); fVerV[q] = calloc(n2, 8); }
   double *hFacZ = calloc(n2, 8), *r_hFacZ = calloc(n2, 8), *xA = calloc(n2, 8), *yA = calloc(n2, 8);
@@ -107,6 +111,7 @@ void oracle_dynamics(OModel *m) {
   const double fuFac = m->cfFacMom, fvFac = m->cfFacMom;
   const int bottomDragTerms = m->no_slip_bottom; /* selectBotDragQuadr=-1, bottomDragLinear=0 */
 
+#pragma omp for schedule(dynamic, 1)
   for (int t = 0; t < m->nTiles; t++) {
     double *gU = m->gU + t * m->n3, *gV = m->gV + t * m->n3;
     double *uVel = m->uVel + t * m->n3, *vVel = m->vVel + t * m->n3, *wVel = m->wVel + t * m->n3;
@@ -826,4 +831,5 @@ void oracle_dynamics(OModel *m) {
   free(kappaRU); free(kappaRV);
   free(phiHydF); free(phiHydC); free(dPhiHydX); free(dPhiHydY); free(mT);
   free(h0FacZ); free(v4F); free(d2Z); free(d2M); free(alphaRho); free(varLoc); free(dWtransC); free(dWtransU); free(dWtransV);
+  }   /* omp parallel */
 }

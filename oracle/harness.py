@@ -12,7 +12,12 @@ import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB = os.path.join(HERE, "liboracle.so")
-_lib = None
+# the same sources built with -fopenmp: tiles over OpenMP threads (Oracle.set(nThreads=...)),
+# bit-identical to the sequential build; loaded while USE_OMP is set (bench.py cpu_baseline's
+# multi-core figure), the sequential build otherwise
+LIB_OMP = os.path.join(HERE, "liboracle_omp.so")
+USE_OMP = False
+_libs = {}
 
 
 def build():
@@ -20,11 +25,12 @@ def build():
 
 
 def lib():
-    global _lib
-    if _lib is None:
-        if not os.path.exists(LIB):
+    key = bool(USE_OMP)
+    if key not in _libs:
+        path = LIB_OMP if key else LIB
+        if not os.path.exists(path):
             build()
-        L = ctypes.CDLL(LIB)
+        L = ctypes.CDLL(path)
         vp, c_int, c_dbl, c_char_p = ctypes.c_void_p, ctypes.c_int, ctypes.c_double, ctypes.c_char_p
         L.oracle_new.restype = vp
         L.oracle_new.argtypes = [c_int] * 7
@@ -60,8 +66,8 @@ def lib():
         L.oracle_set_sum_plan.restype = c_int
         L.oracle_set_cg2d_fma.argtypes = [vp, c_int]
         L.oracle_set_cg2d_fma.restype = c_int
-        _lib = L
-    return _lib
+        _libs[key] = L
+    return _libs[key]
 
 
 def _dp(a):

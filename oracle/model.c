@@ -122,7 +122,7 @@ static const PDesc PTAB[] = {
   PD(pfFacMom), PD(cfFacMom), PD(foFacMom), PD(mtFacMom), PD(hFacMin), PD(hFacMinDr), PD(xgOrigin),
   PD(ygOrigin), PD(cg2dNorm), PD(cg2dTolerance_sq), PD(globalArea), PD(myTime),
   PD(firstResidual), PD(minResidualSq), PD(lastResidual), PD(sumRHS), PD(rhsMax),
-  PI_(momAdvection), PI_(momViscosity), PI_(momForcing), PI_(useCoriolis), PI_(no_slip_sides),
+  PI_(nThreads), PI_(momAdvection), PI_(momViscosity), PI_(momForcing), PI_(useCoriolis), PI_(no_slip_sides),
   PI_(no_slip_bottom), PI_(selectCoriScheme), PI_(momForcingOutAB), PI_(momDissip_In_AB),
   PI_(useHarmonicVisc), PI_(useBiharmonicVisc), PI_(implicitViscosity), PI_(selectCoriMap),
   PI_(cg2dMaxIters), PI_(cg2dUseMinResSol), PI_(exactConserv), PI_(nIter0), PI_(usingCartesianGrid),

@@ -24,6 +24,7 @@
 typedef struct OModel {
   /* --- sizes (SIZE.h) --- */
   int sNx, sNy, OLx, OLy, Nr, nSx, nSy, nTiles;
+  int nThreads;   /* OpenMP threads over the tiles (<= 1: sequential); bench.py cpu_baseline */
   int nx, ny;          /* halo-inclusive tile extents */
   long n2, n3;         /* points per tile: 2-D, 3-D */
 

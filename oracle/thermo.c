@@ -37,6 +37,7 @@ void oracle_oceanic_phys(OModel *m) {
   if (m->allowFreezing) oracle_freeze_surface(m);
   oracle_external_forcing_surf(m);
   const int calcConvect = m->ivdc_kappa != 0.0;
+#pragma omp parallel for schedule(dynamic, 1) if (m->nThreads > 1) num_threads(m->nThreads > 1 ? m->nThreads : 1)
   for (int t = 0; t < m->nTiles; t++) {
     const double *theta = m->theta + t * m->n3, *salt = m->salt + t * m->n3;
     const double *maskC = m->maskC + t * m->n3, *maskW = m->maskW + t * m->n3, *maskS = m->maskS + t * m->n3;
@@ -335,6 +336,8 @@ static void tracer_integrate(OModel *m, const TracerSpec *c) {
   if (!(c->advScheme == 2 || ((c->advScheme == 30 || c->advScheme == 33) && multiDim)) || c->vAdvScheme != c->advScheme) {
     fprintf(stderr, "oracle tracer_integrate: advection scheme %d/%d not restated\n", c->advScheme, c->vAdvScheme); abort();
   }
+#pragma omp parallel if (m->nThreads > 1) num_threads(m->nThreads > 1 ? m->nThreads : 1)
+  {
   double *gT = calloc(n3, 8), *kappaRT = calloc(n3, 8);
   double *a3 = calloc(n3, 8), *b3 = calloc(n3, 8), *c3 = calloc(n3, 8), *cp = calloc(n3, 8), *yp = calloc(n3, 8);
   double *fVer[2], *xA = calloc(n2, 8), *yA = calloc(n2, 8), *uTrans = calloc(n2, 8), *vTrans = calloc(n2, 8);
@@ -347,6 +350,7 @@ static void tracer_integrate(OModel *m, const TracerSpec *c) {
   const double abFac = (m->myIter == m->nIter0 && m->nIter0 == 0) ? 0.0 : 0.5 + m->abEps; /* startAB = nIter0 */
   const int rstar = m->nonlinFreeSurf > 0 && m->select_rStar > 0;
 
+#pragma omp for schedule(dynamic, 1)
   for (int t = 0; t < m->nTiles; t++) {
     double *theta = c->tr + t * n3, *gtNm1 = c->gNm1 + t * n3;
     const double *dxG = m->dxG + t * n2, *dyG = m->dyG + t * n2, *rA = m->rA + t * n2;
@@ -627,6 +631,7 @@ static void tracer_integrate(OModel *m, const TracerSpec *c) {
   free(fVer[0]); free(fVer[1]); free(xA); free(yA); free(uTrans); free(vTrans); free(rTrans); free(rTransKp);
   free(maskUp); free(gtForc); free(fZon); free(fMer); free(af); free(df);
   free(uRes); free(vRes); free(wRes); free(dTdz);
+  }   /* omp parallel */
 }
 
 void oracle_thermodynamics(OModel *m) {

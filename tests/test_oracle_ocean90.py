@@ -58,3 +58,27 @@ def test_oracle_one_tile_layout(golden_dir, nsteps):
     print("global_ocean.90x40x15, 1 tile: worst digits %.2f at %s" % (worst[0], worst[1:]))
     assert worst[0] >= 10.0, worst
     assert min(r[0] for r in res if r[2] in loose) >= 6.0
+
+
+def test_openmp_oracle_bit_identical():
+    """The OpenMP build of the oracle (liboracle_omp.so: DYNAMICS, THERMODYNAMICS and
+    DO_OCEANIC_PHYS over the tiles in parallel; bench.py's multi-core CPU baseline) is
+    bit-identical to the sequential restatement on the reference's 9 x 4 tiling."""
+    import numpy as np
+    from oracle import harness
+    from oracle.harness import ocean90_oracle
+    out = {}
+    for omp in (False, True):
+        harness.USE_OMP = omp
+        try:
+            o, _ = ocean90_oracle(nSx=9, nSy=4)
+        finally:
+            harness.USE_OMP = False
+        if omp:
+            o.set(nThreads=4)
+        for _ in range(3):
+            o.forward_step()
+        out[omp] = {n: np.array(o.arr(n)).copy() for n in ("uVel", "vVel", "wVel", "theta", "salt", "etaN")}
+        out[omp]["iters"] = o.get("numIters")
+    for n in out[False]:
+        assert np.array_equal(out[False][n], out[True][n]), n
