@@ -39,6 +39,19 @@ mgcm_model *mgcm_create(int sNx, int sNy, int OLx, int OLy, int Nr, int nSx, int
 void mgcm_destroy(mgcm_model *m);
 const char *mgcm_last_error(void);
 
+/* pkg/exch2 halo maps from the W2_EXCH2_TOPOLOGY.h arrays W2_E2SETUP fills (host only, no
+ * model, no device): the copies of EXCH2_3D_RL (exch2_3d_rx.template) and
+ * EXCH2_UV_CGRID_3D_RL with (u1, v1) and without (u0, v0) signs, as the gather maps of
+ * mgcm_set_halo_map / mgcm_set_uv_map, over nTiles tiles of sNx x sNy with overlap OL.
+ * Per-neighbour arrays in Fortran layout (ldNb = W2_maxNeighbours, ldT = W2_maxNbTiles), pij
+ * (4, ldNb, ldT); tile ids 1-based as W2 numbers them.  Outputs hold nTiles*(sNx+2OL)*(sNy+2OL)
+ * entries.  Returns -1 on an inconsistent topology.  (exch2_maps.hip) */
+int mgcm_exch2_maps(int sNx, int sNy, int OL, int nTiles, int ldNb, int ldT, const int *tBasex, const int *tBasey,
+                    const int *isNedge, const int *isSedge, const int *isEedge, const int *isWedge,
+                    const int *nNeighbours, const int *neighbourId, const int *opposingSend, const int *pij,
+                    const int *oi, const int *oj, const int *iLo, const int *iHi, const int *jLo, const int *jHi,
+                    long *src, long *u1, long *v1, long *u0, long *v0);
+
 /* Run-time parameters (PARAMS.h names, already resolved as ini_parms.F does). */
 int mgcm_set_param(mgcm_model *m, const char *name, double value);
 double mgcm_get_param(mgcm_model *m, const char *name);
@@ -47,6 +60,15 @@ double mgcm_get_param(mgcm_model *m, const char *name);
  * written in stream order without a host synchronisation (mgcm_set_param("myIter")
  * synchronises). */
 int mgcm_set_iter(mgcm_model *m, int myIter);
+/* myIter += inc on the device, in stream order: FORWARD_STEP's advance of myIter
+ * (forward_step.F:806) inside a captured step, where mgcm_set_iter's value would be baked in
+ * (fortran_abi.hip's multi-model step replay). */
+int mgcm_add_iter(mgcm_model *m, int inc);
+/* Which of the theta / salt ping-pong buffers are current (CYCLE_TRACER is a pointer swap,
+ * cycle_tracer.F): bit 0 theta, bit 1 salt, 0 = the first-allocated buffer.  set < 0 returns
+ * the current parity; set = 0..3 makes that parity current (a replayed step whose capture
+ * already ran the host-side swaps: fortran_abi.hip). */
+int mgcm_tracer_parity(mgcm_model *m, int set);
 
 /* Host <-> device copies of named fields (DYNVARS/GRID/CG2D/FFIELDS names,
  * e.g. "uVel", "hFacW", "aW2d", "fu").  count = number of doubles. */
@@ -111,6 +133,10 @@ int mgcm_blocking_exchanges(mgcm_model *m);
 int mgcm_oceanic_phys(mgcm_model *m);
 /* THERMODYNAMICS (model/src/thermodynamics.F:25) alone: TEMP/SALT_INTEGRATE + CYCLE_TRACER. */
 int mgcm_tracer_step(mgcm_model *m);
+/* DO_STAGGER_FIELDS_EXCHANGES (model/src/do_stagger_fields_exchanges.F:7; forward_step.F:1010,
+ * staggerTimeStep): EXCH_UV_3D_RL(uVel, vVel, .TRUE.) + EXCH_3D_RL(wVel) before the staggered
+ * THERMODYNAMICS. */
+int mgcm_stagger_exchanges(mgcm_model *m);
 /* EXCH_XY(Z)_RL / EXCH_UV_XY(Z)_RL (eesupp/src/exch_*_rx.template) on caller-owned host
  * arrays of nz levels (u alone for a scalar; u, v with vector = 1 for a C-grid pair,
  * withSigns as the reference's LOGICAL), with this model's halo maps. */
@@ -256,11 +282,17 @@ void mgcm_kernel_timing(mgcm_model *m, int enable);
 /* SIZE.h tile set; nProcs = nPx*nPy and nThreads = nTx*nTy must be 1. */
 void mgcm_amd_setup_(const int *sNx, const int *sNy, const int *OLx, const int *OLy, const int *Nr,
                      const int *nSx, const int *nSy, const int *nProcs, const int *nThreads);
-/* The halo maps of a pkg/exch2 topology, derived by MGCM_AMD_EXCH2_MAPS from the
- * reference's own EXCH2_3D_RL / EXCH2_UV_CGRID_3D_RL on index arrays (mods/mgcm_amd_exch2.F):
- * ids = source index per point, u1/v1/u0/v0 = +-(source+1) codes, per-tile face and edges. */
+/* Halo maps given point by point: ids = source index per point, u1/v1/u0/v0 = +-(source+1)
+ * codes, per-tile face and edges (a host that derives them itself). */
 void mgcm_amd_set_maps_(const double *ids, const double *u1, const double *v1, const double *u0, const double *v0,
                         const int *tFace, const int *tEdge, const int *nPts);
+/* The halo maps of a pkg/exch2 topology from the W2_EXCH2_TOPOLOGY.h COMMON arrays
+ * W2_E2SETUP fills (mods/mgcm_amd_exch2.F; derived by mgcm_exch2_maps): one process holding
+ * every tile in W2's order; ldNb = W2_maxNeighbours, ldT = W2_maxNbTiles. */
+void mgcm_amd_set_w2_(const int *nTiles, const int *ldNb, const int *ldT, const int *myFace, const int *tBasex,
+                      const int *tBasey, const int *isN, const int *isS, const int *isE, const int *isW, const int *nNb,
+                      const int *nbId, const int *opp, const int *pij, const int *oi, const int *oj, const int *iLo,
+                      const int *iHi, const int *jLo, const int *jHi);
 /* One PARAMS.h parameter (LOGICAL as 0/1). */
 void mgcm_amd_param_(const char *name, const double *value, size_t len);
 /* Register a COMMON-block array of `count` doubles as device field `name`; kind 1 static
@@ -293,6 +325,8 @@ void momentum_correction_step_amd_(const double *myTime, const int *myIter,
 void integr_continuity_amd_(const double *uFld, const double *vFld, const double *myTime, const int *myIter,
                             const int *myThid);                          /* integr_continuity.F:13 */
 void do_fields_blocking_exchanges_amd_(const int *myThid);             /* do_fields_blocking_exchanges.F:7 */
+void do_stagger_fields_exchanges_amd_(const double *myTime, const int *myIter,
+                                       const int *myThid);              /* do_stagger_fields_exchanges.F:7 */
 /* Exchanges and the tile-ordered global sum on host arrays. */
 void exch_xy_rl_amd_(double *phi, const int *myThid);                          /* exch_xy_rx.template:9 */
 void exch_xyz_rl_amd_(double *phi, const int *myThid);                         /* exch_xyz_rx.template:8 */

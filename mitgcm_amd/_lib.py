@@ -32,6 +32,9 @@ def lib():
         "mgcm_last_error": (cs, []),
         "mgcm_set_param": (ci, [vp, cs, cd]),
         "mgcm_set_iter": (ci, [vp, ci]),
+        "mgcm_add_iter": (ci, [vp, ci]),
+        "mgcm_exch2_maps": (ci, [ci] * 6 + [PI] * 16 + [PL] * 5),
+        "mgcm_tracer_parity": (ci, [vp, ci]),
         "mgcm_get_param": (cd, [vp, cs]),
         "mgcm_put": (ci, [vp, cs, PD, cl]),
         "mgcm_put_async": (ci, [vp, cs, PD, cl]),
@@ -79,6 +82,7 @@ def lib():
         "mgcm_exchange_field": (ci, [vp, cs]),
         "mgcm_oceanic_phys": (ci, [vp]),
         "mgcm_tracer_step": (ci, [vp]),
+        "mgcm_stagger_exchanges": (ci, [vp]),
         "mgcm_exchange_host": (ci, [vp, PD, PD, ci, ci, ci]),
         "mgcm_field_count": (cl, [vp, cs]),
         "mgcm_param_name": (cs, [ci]),
@@ -106,16 +110,16 @@ EXPORTS = ["mgcm_create", "mgcm_destroy", "mgcm_last_error", "mgcm_set_param", "
            "mgcm_kernel_ms", "mgcm_kernel_timing", "mgcm_set_tile_range", "mgcm_set_stream",
            "mgcm_exchange_nfields", "mgcm_halo_pack", "mgcm_tile_copy", "mgcm_begin_steps", "mgcm_step_phase", "mgcm_cg2d_op",
            "mgcm_cg2d_record", "mgcm_field_pack", "mgcm_exchange_field", "ini_cg2d_amd_",
-           "cg2d_amd_", "mgcm_oceanic_phys", "mgcm_tracer_step", "mgcm_exchange_host", "mgcm_field_count", "mgcm_param_name",
+           "cg2d_amd_", "mgcm_oceanic_phys", "mgcm_tracer_step", "mgcm_stagger_exchanges", "mgcm_exchange_host", "mgcm_field_count", "mgcm_param_name",
            "mgcm_amd_setup_", "mgcm_amd_param_", "mgcm_amd_bind_", "mgcm_amd_init_", "do_oceanic_phys_amd_",
            "thermodynamics_amd_", "dynamics_amd_", "solve_for_pressure_amd_", "momentum_correction_step_amd_",
-           "integr_continuity_amd_", "do_fields_blocking_exchanges_amd_", "exch_xy_rl_amd_", "exch_xyz_rl_amd_",
+           "integr_continuity_amd_", "do_fields_blocking_exchanges_amd_", "do_stagger_fields_exchanges_amd_", "exch_xy_rl_amd_", "exch_xyz_rl_amd_",
            "exch_uv_xy_rl_amd_", "exch_uv_xyz_rl_amd_", "global_sum_tile_rl_amd_",
            "mgcm_update_r_star", "mgcm_calc_r_star", "update_r_star_amd_", "update_cg2d_amd_", "calc_r_star_amd_",
-           "mgcm_set_iter", "mgcm_amd_host_sync_", "mgcm_amd_device_sync_", "mgcm_amd_transfer_stats_",
+           "mgcm_set_iter", "mgcm_add_iter", "mgcm_tracer_parity", "mgcm_exch2_maps", "mgcm_amd_host_sync_", "mgcm_amd_device_sync_", "mgcm_amd_transfer_stats_",
            "mgcm_amd_step_fence_", "mgcm_halo_pack_group", "mgcm_exchange_nfields_group", "mgcm_stream_handoff",
            "mgcm_end_steps", "mgcm_cg2d_shared_bytes", "mgcm_cg2d_shared_export", "mgcm_cg2d_shared_import",
-           "mgcm_amd_set_maps_", "mgcm_get_stream", "mgcm_halo_sources", "mgcm_cg2d_tiles", "mgcm_cg2d_share"]
+           "mgcm_amd_set_maps_", "mgcm_amd_set_w2_", "mgcm_get_stream", "mgcm_halo_sources", "mgcm_cg2d_tiles", "mgcm_cg2d_share"]
 
 
 def check(rc, what):

@@ -15,7 +15,8 @@ CSRC = os.path.join(HERE, "csrc")
 OUT = os.path.join(HERE, "libmitgcm_amd.so")
 # kernels_step.hip includes kernels_dyn.hip and kernels_thermo.hip (one unit: the fused launches need both)
 SOURCES = ["model.hip", "kernels_step.hip", "kernels_solve.hip", "kernels_rstar.hip",
-           "kernels_cg2d_mwg.hip", "kernels_monitor.hip", "kernels_cg2d_dist.hip", "fortran_abi.hip"]
+           "kernels_cg2d_mwg.hip", "kernels_monitor.hip", "kernels_cg2d_dist.hip", "fortran_abi.hip",
+           "exch2_maps.hip"]
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared", "-ffp-contract=off",
          "-Wno-unused-result", "-Wno-unused-value"]

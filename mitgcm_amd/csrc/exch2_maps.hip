@@ -1,0 +1,233 @@
+// exch2_maps.hip -- pkg/exch2's halo exchanges as gather maps, derived from the
+// W2_EXCH2_TOPOLOGY.h arrays (host code, no kernels).
+//
+// A MITgcm host on a cube or lat-lon-cap grid holds its tile connectivity in the COMMON
+// blocks of pkg/exch2/W2_EXCH2_TOPOLOGY.h, filled by W2_E2SETUP (w2_e2setup.F ->
+// w2_set_map_tiles.F, w2_set_tile2tiles.F): per tile its facet base (exch2_tBasex/y), facet
+// edge flags, and per neighbour its id, the opposing connection, the index transform
+// (exch2_pij, exch2_oi, exch2_oj) and the halo range (exch2_iLo/iHi/jLo/jHi).  The
+// reference's exchanges copy halo strips along those connections:
+//   scalar   EXCH2_3D_RX -> two EXCH2_RX1_CUBE passes, "ignore corners" then "update
+//            corners" (exch2_3d_rx.template:60-70, exch2_rx1_cube.template:92-258), the
+//            bounds of EXCH2_GET_SCAL_BOUNDS (exch2_get_scal_bounds.F:56-133);
+//   C-grid   EXCH2_UV_3D_RX -> two EXCH2_RX2_CUBE passes (exch2_uv_3d_rx.template:60-226,
+//   vector   exch2_put_rx2.template:98-225), the bounds of EXCH2_GET_UV_BOUNDS
+//            (exch2_get_uv_bounds.F:84-262), then the cube-corner fix-ups.
+// Running that sequence on arrays of point ids instead of values gives, for every halo point,
+// the point (and for vectors the component and sign) it ends up holding: the maps the device
+// exchange kernels replay (mgcm_set_halo_map, mgcm_set_uv_map).  Every PUT of a pass reads
+// the array before any GET of the pass writes it, so each pass reads a snapshot.
+//
+// The same derivation in Python (mitgcm_amd/exch2.py, pinned through the cube and LLC
+// experiments against the reference's output.txt) is the test oracle of this one
+// (tests/test_host.py::test_exch2_maps_from_w2_arrays).
+#include <cstdlib>
+#include <vector>
+
+#include "../../include/mitgcm_amd.h"
+
+namespace {
+
+struct W2 {
+  int sNx, sNy, OL, nT, ldNb, ldT;
+  const int *tBx, *tBy, *isN, *isS, *isE, *isW, *nNb, *nbId, *opp, *pij, *oi, *oj, *iLo, *iHi, *jLo, *jHi;
+  // neighbour n (0-based) of tile t (1-based): Fortran (n+1, t) of arrays (ldNb, ldT)
+  int at(const int *a, int t, int n) const { return a[(size_t)(t - 1) * ldNb + n]; }
+  int p(int t, int n, int q) const { return pij[((size_t)(t - 1) * ldNb + n) * 4 + q]; }
+  long nx() const { return sNx + 2 * OL; }
+  long n2() const { return nx() * (sNy + 2 * OL); }
+  long g(int t, int i, int j) const { return (long)(t - 1) * n2() + (long)(j + OL - 1) * nx() + (i + OL - 1); }
+  bool inb(int i, int j) const { return i >= 1 - OL && i <= sNx + OL && j >= 1 - OL && j <= sNy + OL; }
+};
+
+// inclusive range lo..hi with step st (empty when it runs the other way)
+template <class F>
+void rng(int lo, int hi, int st, F f) {
+  if ((long)(hi - lo) * st < 0) return;
+  for (int v = lo; st > 0 ? v <= hi : v >= hi; v += st) f(v);
+}
+
+// EXCH2_GET_SCAL_BOUNDS (exch2_get_scal_bounds.F:56-133): the halo strip of neighbour n of
+// tile t, widened to the exchange width eW; upd: the "update corners" pass
+void scal_bounds(const W2 &w, int t, int n, int eW, bool upd, int &iLo, int &iHi, int &jLo, int &jHi, int &si, int &sj) {
+  iLo = w.at(w.iLo, t, n); iHi = w.at(w.iHi, t, n); jLo = w.at(w.jLo, t, n); jHi = w.at(w.jHi, t, n);
+  si = sj = 1;
+  auto widen = [&](int &lo, int &hi, int &s, int oLo, int oHi) {
+    s = oLo <= oHi ? 1 : -1;
+    if (upd) { lo = oLo - s * (eW - 1); hi = oHi + s * (eW - 1); }
+    else { lo = oLo + s; hi = oHi - s; }
+  };
+  if (iLo == iHi && iLo == 0) { iLo = 1 - eW; si = 1; widen(jLo, jHi, sj, jLo, jHi); }
+  if (iLo == iHi && iLo > 1) { iHi = iHi + eW - 1; si = 1; widen(jLo, jHi, sj, jLo, jHi); }
+  if (jLo == jHi && jLo == 0) { jLo = 1 - eW; sj = 1; widen(iLo, iHi, si, iLo, iHi); }
+  if (jLo == jHi && jLo > 1) { jHi = jHi + eW - 1; sj = 1; widen(iLo, iHi, si, iLo, iHi); }
+}
+
+// one EXCH2_RX1_CUBE pass over every tile's neighbours
+bool rx1_pass(const W2 &w, std::vector<long> &ids, bool upd) {
+  const std::vector<long> snap = ids;
+  const int eW = w.OL;
+  for (int t = 1; t <= w.nT; t++)
+    for (int n = 0; n < w.nNb[t - 1]; n++) {
+      const int S = w.at(w.nbId, t, n), sn = w.at(w.opp, t, n) - 1;
+      const int p0 = w.p(S, sn, 0), p1 = w.p(S, sn, 1), p2 = w.p(S, sn, 2), p3 = w.p(S, sn, 3);
+      const int oi = w.at(w.oi, S, sn), oj = w.at(w.oj, S, sn);
+      int iLo, iHi, jLo, jHi, si, sj;
+      scal_bounds(w, t, n, eW, upd, iLo, iHi, jLo, jHi, si, sj);
+      bool ok = true;
+      rng(jLo, jHi, sj, [&](int jl) {
+        rng(iLo, iHi, si, [&](int il) {
+          const int itc = il + w.tBx[t - 1], jtc = jl + w.tBy[t - 1];
+          const int isl = p0 * itc + p1 * jtc + oi - w.tBx[S - 1], jsl = p2 * itc + p3 * jtc + oj - w.tBy[S - 1];
+          if (!w.inb(isl, jsl)) { ok = false; return; }
+          ids[w.g(t, il, jl)] = snap[w.g(S, isl, jsl)];
+        });
+      });
+      if (!ok) return false;
+    }
+  return true;
+}
+
+// EXCH2_GET_UV_BOUNDS (exch2_get_uv_bounds.F:84-262), C-grid: the u and v strips of neighbour
+// n of tile t, the loop steps, and the transform of the source's opposing connection
+struct UVB {
+  int r1[4], r2[4], si, sj, oi1, oj1, oi2, oj2, p[4], S;
+};
+UVB uv_bounds(const W2 &w, int t, int n, int eW, bool upd) {
+  UVB b{};
+  const int tIlo = w.at(w.iLo, t, n), tIhi = w.at(w.iHi, t, n), tJlo = w.at(w.jLo, t, n), tJhi = w.at(w.jHi, t, n);
+  b.S = w.at(w.nbId, t, n);
+  const int sn = w.at(w.opp, t, n) - 1;
+  for (int q = 0; q < 4; q++) b.p[q] = w.p(b.S, sn, q);
+  b.oi1 = b.oi2 = w.at(w.oi, b.S, sn);
+  b.oj1 = b.oj2 = w.at(w.oj, b.S, sn);
+  b.si = b.sj = 1;
+  int i1 = 0, i1h = 0, j1 = 0, j1h = 0;
+  auto widen = [&](int &lo, int &hi, int &s, int oLo, int oHi) {
+    s = oLo <= oHi ? 1 : -1;
+    if (upd) { lo = oLo - s * (eW - 1); hi = oHi + s * (eW - 1); }
+    else { lo = oLo + s; hi = oHi - s; }
+  };
+  if (tIlo == tIhi && tIlo == 0) { i1 = 1 - eW; i1h = 0; b.si = 1; widen(j1, j1h, b.sj, tJlo, tJhi); }
+  if (tIlo == tIhi && tIlo > 1) { i1 = tIlo; i1h = tIhi + eW - 1; b.si = 1; widen(j1, j1h, b.sj, tJlo, tJhi); }
+  if (tJlo == tJhi && tJlo == 0) { j1 = 1 - eW; j1h = 0; b.sj = 1; widen(i1, i1h, b.si, tIlo, tIhi); }
+  if (tJlo == tJhi && tJlo > 1) { j1 = tJlo; j1h = tJhi + eW - 1; b.sj = 1; widen(i1, i1h, b.si, tIlo, tIhi); }
+  int i2 = i1, i2h = i1h, j2 = j1, j2h = j1h;
+  const int *p = b.p;
+  if (p[0] == -1) b.oi1 += 1;
+  if (p[2] == -1) b.oj1 += 1;
+  if (p[1] == -1) b.oi2 += 1;
+  if (p[3] == -1) b.oj2 += 1;
+  if (upd) {
+    if (p[0] == -1 || p[2] == -1) i1 += 1;
+    if (p[1] == -1 || p[3] == -1) j2 += 1;
+    if (tIlo == tIhi && tIlo > 1) {
+      if (w.isS[t - 1]) { j1 = tJlo + 1; j2 = tJlo + 1; }
+      if (w.isN[t - 1]) { j1h = tJhi - 1; j2h = tJhi; }
+    }
+    if (tJlo == tJhi && tJlo > 1) {
+      if (w.isW[t - 1]) { i1 = tIlo + 1; i2 = tIlo + 1; }
+      if (w.isE[t - 1]) { i1h = tIhi; i2h = tIhi - 1; }
+    }
+  } else {
+    if (p[0] == -1 || p[2] == -1) { i1 += 1; i1h += 1; }
+    if (p[1] == -1 || p[3] == -1) { j2 += 1; j2h += 1; }
+  }
+  b.r1[0] = i1; b.r1[1] = i1h; b.r1[2] = j1; b.r1[3] = j1h;
+  b.r2[0] = i2; b.r2[1] = i2h; b.r2[2] = j2; b.r2[3] = j2h;
+  return b;
+}
+
+// one EXCH2_RX2_CUBE pass (C-grid): ids index [u | v] over 2N points, sg the signs
+bool rx2_pass(const W2 &w, std::vector<long> &u, std::vector<int> &us, std::vector<long> &v, std::vector<int> &vs,
+              bool upd, bool withSigns) {
+  const std::vector<long> su = u, sv = v;
+  const std::vector<int> sus = us, svs = vs;
+  const int eW = w.OL;
+  bool ok = true;
+  for (int t = 1; t <= w.nT && ok; t++)
+    for (int n = 0; n < w.nNb[t - 1] && ok; n++) {
+      const UVB b = uv_bounds(w, t, n, eW, upd);
+      for (int comp = 0; comp < 2 && ok; comp++) {
+        const int *r = comp == 0 ? b.r1 : b.r2;
+        const int oi = comp == 0 ? b.oi1 : b.oi2, oj = comp == 0 ? b.oj1 : b.oj2;
+        int sa1 = comp == 0 ? b.p[0] : b.p[1], sa2 = comp == 0 ? b.p[2] : b.p[3];
+        if (!withSigns) { sa1 = std::abs(sa1); sa2 = std::abs(sa2); }
+        std::vector<long> &did = comp == 0 ? u : v;
+        std::vector<int> &dsg = comp == 0 ? us : vs;
+        rng(r[2], r[3], b.sj, [&](int jl) {
+          rng(r[0], r[1], b.si, [&](int il) {
+            const int itc = il + w.tBx[t - 1], jtc = jl + w.tBy[t - 1];
+            const int isl = b.p[0] * itc + b.p[1] * jtc + oi - w.tBx[b.S - 1];
+            const int jsl = b.p[2] * itc + b.p[3] * jtc + oj - w.tBy[b.S - 1];
+            if (!w.inb(isl, jsl)) { ok = false; return; }
+            const long d = w.g(t, il, jl), s = w.g(b.S, isl, jsl);
+            if (sa1 != 0) { did[d] = su[s]; dsg[d] = sus[s] * sa1; }
+            else { did[d] = sv[s]; dsg[d] = svs[s] * sa2; }
+          });
+        });
+      }
+    }
+  return ok;
+}
+
+}  // namespace
+
+extern "C" int mgcm_exch2_maps(int sNx, int sNy, int OL, int nTiles, int ldNb, int ldT, const int *tBasex,
+                               const int *tBasey, const int *isNedge, const int *isSedge, const int *isEedge,
+                               const int *isWedge, const int *nNeighbours, const int *neighbourId,
+                               const int *opposingSend, const int *pij, const int *oi, const int *oj, const int *iLo,
+                               const int *iHi, const int *jLo, const int *jHi, long *src, long *u1, long *v1, long *u0,
+                               long *v0) {
+  if (sNx < 1 || sNy < 1 || OL < 1 || nTiles < 1 || ldNb < 1 || ldT < nTiles) return -1;
+  const W2 w{sNx, sNy, OL, nTiles, ldNb, ldT, tBasex, tBasey, isNedge, isSedge, isEedge, isWedge, nNeighbours,
+             neighbourId, opposingSend, pij, oi, oj, iLo, iHi, jLo, jHi};
+  for (int t = 1; t <= nTiles; t++) {
+    if (nNeighbours[t - 1] < 0 || nNeighbours[t - 1] > ldNb) return -1;
+    for (int n = 0; n < nNeighbours[t - 1]; n++) {
+      const int S = w.at(neighbourId, t, n), sn = w.at(opposingSend, t, n);
+      if (S < 1 || S > nTiles || sn < 1 || sn > nNeighbours[S - 1]) return -1;
+    }
+  }
+  const long N = (long)nTiles * w.n2();
+  // scalar: EXCH2_3D_RX, ignore-corners then update-corners pass
+  std::vector<long> ids(N);
+  for (long q = 0; q < N; q++) ids[q] = q;
+  if (!rx1_pass(w, ids, false) || !rx1_pass(w, ids, true)) return -1;
+  for (long q = 0; q < N; q++) src[q] = ids[q];
+  // C-grid vectors, with and without signs (EXCH2_UV_3D_RX, W2_USE_R1_ONLY undefined)
+  for (int signs = 1; signs >= 0; signs--) {
+    std::vector<long> u(N), v(N);
+    std::vector<int> us(N, 1), vs(N, 1);
+    for (long q = 0; q < N; q++) { u[q] = q; v[q] = N + q; }
+    if (!rx2_pass(w, u, us, v, vs, false, signs) || !rx2_pass(w, u, us, v, vs, true, signs)) return -1;
+    // the cube-corner values of u / v outside the facet edges (exch2_uv_3d_rx.template:130-226)
+    const int nX = sNx, nY = sNy, neg = signs ? -1 : 1;
+    auto cp = [&](std::vector<long> &dst, std::vector<int> &dsg, long d, const std::vector<long> &s_, const std::vector<int> &ssg,
+                  long s, int f) { dst[d] = s_[s]; dsg[d] = ssg[s] * f; };
+    for (int t = 1; t <= nTiles; t++) {
+      auto G = [&](int i, int j) { return w.g(t, i, j); };
+      const bool sW = isWedge[t - 1], sE = isEedge[t - 1], sS = isSedge[t - 1], sN = isNedge[t - 1];
+      if (OL >= 2 && sW && sS) { cp(u, us, G(0, 0), v, vs, G(1, 0), 1); cp(v, vs, G(0, 0), u, us, G(0, 1), 1); }
+      if (OL >= 2 && sW && sN) {
+        cp(u, us, G(0, nY + 1), v, vs, G(1, nY + 2), neg);
+        cp(v, vs, G(0, nY + 2), u, us, G(0, nY), neg);
+      }
+      if (OL >= 2 && sE && sS) {
+        cp(u, us, G(nX + 2, 0), v, vs, G(nX, 0), neg);
+        cp(v, vs, G(nX + 1, 0), u, us, G(nX + 2, 1), neg);
+      }
+      if (OL >= 2 && sE && sN) {
+        cp(u, us, G(nX + 2, nY + 1), v, vs, G(nX, nY + 2), 1);
+        cp(v, vs, G(nX + 1, nY + 2), u, us, G(nX + 2, nY), 1);
+      }
+    }
+    // the codes of mgcm_set_uv_map: 0 untouched, +-(source + 1) into [u | v]
+    long *cu = signs ? u1 : u0, *cv = signs ? v1 : v0;
+    for (long q = 0; q < N; q++) {
+      cu[q] = u[q] == q ? 0 : (u[q] + 1) * us[q];
+      cv[q] = v[q] == N + q ? 0 : (v[q] + 1) * vs[q];
+    }
+  }
+  return 0;
+}

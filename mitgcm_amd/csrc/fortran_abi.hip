@@ -138,6 +138,15 @@ struct FortranSide {
   std::vector<std::string> seq, fusedSeq;
   bool recording = false, canFuse = false, fused = false;
   size_t fusedPos = 0;
+  // N > 1 models: the recorded step captured across every model's stream (the cross-model
+  // copies as memcpy nodes, the barriers as event edges) into one graph per tracer-buffer
+  // parity, and the parity each model is left at by the captured step's host-side swaps
+  struct MultiGraph {
+    hipGraphExec_t exec = nullptr;
+    std::vector<int> post;
+  } mg[4];
+  bool capturing = false;     // set_iter inside a capture: device increments, not values
+  bool multiGraphOff = false; // a capture failed: the multi-model steps stay eager
   long nUp = 0, nDown = 0;   // copies of whole bound arrays, for mgcm_amd_transfer_stats_
   // the state arrays' host pages, registered with HIP once the time loop begins (downloads
   // then go straight to the COMMON blocks by DMA); false when registration was refused
@@ -288,6 +297,12 @@ void op_blocking(const char *w) {
   if (multi()) xfer3d(w, 0);
   run_all(w, mgcm_blocking_exchanges);
 }
+// DO_STAGGER_FIELDS_EXCHANGES: the velocities' halo sources between models (group 2: the
+// non-tracer fields), then every local uVel, vVel, wVel fill
+void op_stagger(const char *w) {
+  if (multi()) xfer3d(w, 2);
+  run_all(w, mgcm_stagger_exchanges);
+}
 
 // The device's iteration counter (AB2's first step, the CD scheme's start), written only
 // when it changes (FORWARD_STEP advances myIter after DYNAMICS, forward_step.F:806), in
@@ -296,7 +311,8 @@ void set_iter(const char *where, int myIter) {
   if (g.devIter == myIter) return;
   for (auto &s : g.sh) {
     hipchk(hipSetDevice(s.dev), where);
-    if (mgcm_set_iter(s.m, myIter)) die(where);
+    // inside a capture the step's advance is an increment (the graph replays at any myIter)
+    if (g.capturing ? mgcm_add_iter(s.m, myIter - (int)g.devIter) : mgcm_set_iter(s.m, myIter)) die(where);
   }
   g.devIter = myIter;
 }
@@ -575,26 +591,122 @@ void advanced(int myIter, double myTime) {
   g.advTime = myTime;
 }
 
-// Is the recorded step FORWARD_STEP's non-staggered order, which mgcm_forward_step replays
-// bit for bit (forward_step.F:656-1120; tests/test_gpu_refhost.py)?  Each routine once, in
-// the order DO_OCEANIC_PHYS, THERMODYNAMICS, DYNAMICS, [UPDATE_R_STAR, UPDATE_CG2D],
+// staggerTimeStep: THERMODYNAMICS after the pressure solve (forward_step.F:1003-1036)
+bool staggered() { return mgcm_get_param(g.m, "staggerTimeStep") != 0.0; }
+
+// Is the recorded step FORWARD_STEP's order, which mgcm_forward_step replays bit for bit
+// (forward_step.F:656-1120; tests/test_gpu_refhost.py)?  Each routine once, in the order
+// DO_OCEANIC_PHYS, THERMODYNAMICS, DYNAMICS, [UPDATE_R_STAR, UPDATE_CG2D],
 // SOLVE_FOR_PRESSURE, MOMENTUM_CORRECTION_STEP, INTEGR_CONTINUITY, [CALC_R_STAR],
-// DO_FIELDS_BLOCKING_EXCHANGES; the bracketed ones iff the r* free surface.
+// DO_FIELDS_BLOCKING_EXCHANGES -- the bracketed ones iff the r* free surface -- or, under
+// staggerTimeStep, THERMODYNAMICS moved after DO_STAGGER_FIELDS_EXCHANGES, which follows
+// INTEGR_CONTINUITY / CALC_R_STAR.
 bool canonical_step(const std::vector<std::string> &q) {
-  const bool rstar = mgcm_get_param(g.m, "nonlinFreeSurf") > 0.0;
-  if (mgcm_get_param(g.m, "staggerTimeStep") != 0.0 || mgcm_get_param(g.m, "momStepping") == 0.0) return false;
-  std::vector<std::string> want = {"DO_OCEANIC_PHYS", "THERMODYNAMICS", "DYNAMICS"};
+  const bool rstar = mgcm_get_param(g.m, "nonlinFreeSurf") > 0.0, st = staggered();
+  if (mgcm_get_param(g.m, "momStepping") == 0.0) return false;
+  std::vector<std::string> want = {"DO_OCEANIC_PHYS"};
+  if (!st) want.push_back("THERMODYNAMICS");
+  want.push_back("DYNAMICS");
   if (rstar) { want.push_back("UPDATE_R_STAR"); want.push_back("UPDATE_CG2D"); }
   want.push_back("SOLVE_FOR_PRESSURE");
   want.push_back("MOMENTUM_CORRECTION_STEP");
   want.push_back("INTEGR_CONTINUITY");
   if (rstar) want.push_back("CALC_R_STAR");
+  if (st) { want.push_back("DO_STAGGER_FIELDS_EXCHANGES"); want.push_back("THERMODYNAMICS"); }
   want.push_back("DO_FIELDS_BLOCKING_EXCHANGES");
   return q == want;
 }
 bool fuse_allowed() {
   const char *e = getenv("MGCM_AMD_EAGER");
-  return !multi() && !(e && atoi(e) == 1);
+  return !(e && atoi(e) == 1) && !(multi() && g.multiGraphOff);
+}
+
+// The device work of the recorded step's drop-ins, in their order, with the iteration
+// counter advanced where FORWARD_STEP advances myIter (forward_step.F:806: every drop-in
+// after DYNAMICS runs at myIter + 1 -- but THERMODYNAMICS, staggered or not, steps the
+// tracers' Adams-Bashforth at the step's start, temp_integrate.F:154-155).
+void run_recorded_step(const char *w, int myIter) {
+  for (auto &nm : g.fusedSeq) {
+    const bool late = nm != "DO_OCEANIC_PHYS" && nm != "THERMODYNAMICS" && nm != "DYNAMICS";
+    set_iter(w, late ? myIter + 1 : myIter);
+    if (nm == "DO_OCEANIC_PHYS") op_oceanic_phys(w);
+    else if (nm == "THERMODYNAMICS") op_tracer_step(w);
+    else if (nm == "DYNAMICS") op_dynamics(w);
+    else if (nm == "UPDATE_R_STAR") op_update_r_star(w);
+    else if (nm == "UPDATE_CG2D") continue;   // folded into UPDATE_R_STAR
+    else if (nm == "SOLVE_FOR_PRESSURE") op_solve(w);
+    else if (nm == "MOMENTUM_CORRECTION_STEP") op_correction(w);
+    else if (nm == "INTEGR_CONTINUITY") op_continuity(w);
+    else if (nm == "CALC_R_STAR") op_calc_r_star(w);
+    else if (nm == "DO_STAGGER_FIELDS_EXCHANGES") op_stagger(w);
+    else if (nm == "DO_FIELDS_BLOCKING_EXCHANGES") op_blocking(w);
+    else die(w, "unknown drop-in in the recorded step");
+  }
+}
+
+// model 0's stream waits for every other model's work so far (join), or every other model's
+// stream for model 0's (fork)
+void join_into_0(const char *w) {
+  for (size_t i = 1; i < g.sh.size(); i++) {
+    hipchk(hipSetDevice(g.sh[i].dev), w);
+    hipchk(hipEventRecord(g.sh[i].ev, stream_of(g.sh[i])), w);
+  }
+  hipchk(hipSetDevice(g.sh[0].dev), w);
+  for (size_t i = 1; i < g.sh.size(); i++) hipchk(hipStreamWaitEvent(stream_of(g.sh[0]), g.sh[i].ev, 0), w);
+}
+void fork_from_0(const char *w) {
+  hipchk(hipSetDevice(g.sh[0].dev), w);
+  hipchk(hipEventRecord(g.sh[0].ev, stream_of(g.sh[0])), w);
+  for (size_t i = 1; i < g.sh.size(); i++) {
+    hipchk(hipSetDevice(g.sh[i].dev), w);
+    hipchk(hipStreamWaitEvent(stream_of(g.sh[i]), g.sh[0].ev, 0), w);
+  }
+}
+
+// One FORWARD_STEP of N device models (the recorded drop-in sequence) as a graph replay:
+// the forcing goes up and myIter is set outside the graph; the graph of model 0's tracer
+// parity is captured on first use -- every model's stream joins model 0's capture, the
+// cross-model copies and event barriers of the ops become graph edges -- and launched; a
+// replay then leaves every model at the parity its captured step's host-side CYCLE_TRACER
+// swaps left (mgcm_tracer_parity).  false: the capture failed (the step then runs eagerly
+// and later steps stay eager).
+bool multi_replay(const char *w, int myIter) {
+  const int q = mgcm_tracer_parity(g.m, -1);
+  if (q < 0 || q > 3) die(w);
+  auto &G = g.mg[q];
+  join_into_0(w);   // the forcing uploads of every model before the graph
+  if (!G.exec) {
+    hipStream_t s0 = stream_of(g.sh[0]);
+    hipchk(hipSetDevice(g.sh[0].dev), w);
+    if (hipStreamBeginCapture(s0, hipStreamCaptureModeGlobal) != hipSuccess) {
+      (void)hipGetLastError();
+      return false;
+    }
+    fork_from_0(w);
+    g.capturing = true;
+    g.devIter = myIter;   // the graph's increments are relative to this
+    run_recorded_step(w, myIter);
+    g.capturing = false;
+    join_into_0(w);
+    hipGraph_t gr = nullptr;
+    hipchk(hipSetDevice(g.sh[0].dev), w);
+    hipError_t e = hipStreamEndCapture(s0, &gr);
+    if (e == hipSuccess) e = hipGraphInstantiate(&G.exec, gr, nullptr, nullptr, 0);
+    if (gr) (void)hipGraphDestroy(gr);
+    // the capture ran the step's host side (the CYCLE_TRACER swaps) without its device work:
+    // nothing consistent to fall back to
+    if (e != hipSuccess) die(w, hipGetErrorString(e));
+    G.post.clear();
+    for (auto &s : g.sh) G.post.push_back(mgcm_tracer_parity(s.m, -1));
+  } else {
+    for (size_t i = 0; i < g.sh.size(); i++)
+      if (mgcm_tracer_parity(g.sh[i].m, G.post[i]) < 0) die(w);
+  }
+  hipchk(hipSetDevice(g.sh[0].dev), w);
+  hipchk(hipGraphLaunch(G.exec, stream_of(g.sh[0])), w);
+  fork_from_0(w);   // every model's later work (downloads, the next step) after the graph
+  g.devIter = -1;   // the graph advanced the counters: set again before the next use
+  return true;
 }
 // A routine drop-in of a device-authoritative step: true when its work already ran inside
 // the step's replay (then it only checks its place in the recorded order).
@@ -703,6 +815,34 @@ void mgcm_amd_set_maps_(const double *ids, const double *u1, const double *v1, c
   for (auto &s : g.sh) {
     if (mgcm_set_halo_map(s.m, src.data(), n)) die("MGCM_AMD_SET_MAPS");
     if (mgcm_set_uv_map(s.m, cu1.data(), cv1.data(), cu0.data(), cv0.data(), tFace, tEdge, n)) die("MGCM_AMD_SET_MAPS");
+  }
+  g.ready = false;
+}
+
+/* The halo maps of a pkg/exch2 topology from the W2_EXCH2_TOPOLOGY.h arrays
+ * (mods/mgcm_amd_exch2.F; the derivation: exch2_maps.hip), set on every device model with
+ * the tile faces and facet-edge flags (N=1 S=2 E=4 W=8) of the cube-corner vorticity. */
+void mgcm_amd_set_w2_(const int *nTilesW2, const int *ldNb, const int *ldT, const int *myFace, const int *tBasex,
+                      const int *tBasey, const int *isN, const int *isS, const int *isE, const int *isW, const int *nNb,
+                      const int *nbId, const int *opp, const int *pij, const int *oi, const int *oj, const int *iLo,
+                      const int *iHi, const int *jLo, const int *jHi) {
+  model("MGCM_AMD_SET_W2");
+  const int nt = *nTilesW2;
+  if (nt != (int)nTiles()) die("MGCM_AMD_SET_W2", "exch2_nTiles differs from nSx*nSy");
+  const long n = (long)nt * n2();
+  std::vector<long> src(n), cu1(n), cv1(n), cu0(n), cv0(n);
+  if (mgcm_exch2_maps(g.dims[0], g.dims[1], g.dims[2], nt, *ldNb, *ldT, tBasex, tBasey, isN, isS, isE, isW, nNb, nbId,
+                      opp, pij, oi, oj, iLo, iHi, jLo, jHi, src.data(), cu1.data(), cv1.data(), cu0.data(), cv0.data()))
+    die("MGCM_AMD_SET_W2", "inconsistent W2_EXCH2_TOPOLOGY arrays");
+  std::vector<int> face(nt), edge(nt);
+  for (int t = 0; t < nt; t++) {
+    face[t] = myFace[t];
+    edge[t] = isN[t] + 2 * isS[t] + 4 * isE[t] + 8 * isW[t];
+  }
+  for (auto &s : g.sh) {
+    if (mgcm_set_halo_map(s.m, src.data(), n)) die("MGCM_AMD_SET_W2");
+    if (mgcm_set_uv_map(s.m, cu1.data(), cv1.data(), cu0.data(), cv0.data(), face.data(), edge.data(), n))
+      die("MGCM_AMD_SET_W2");
   }
   g.ready = false;
 }
@@ -846,28 +986,46 @@ void do_oceanic_phys_amd_(const double *myTime, const int *myIter, const int *my
   g.advValid = false;   // a new step: its end time is not known yet
   if (g.fused) die("DO_OCEANIC_PHYS_AMD", "a step began before the previous one's DO_FIELDS_BLOCKING_EXCHANGES");
   if (g.canFuse && fuse_allowed() && g.ready) {
-    // the whole step as one replay of the captured FORWARD_STEP (mgcm_forward_step), after
-    // this step's forcing; the counter the device advances at the step's end is known
+    // the whole step as one replay of the captured FORWARD_STEP (mgcm_forward_step; with N
+    // models multi_replay), after this step's forcing; the counter the device advances at the
+    // step's end is known
     g.lastIter = *myIter;
     g.lastTime = *myTime;
     upload("DO_OCEANIC_PHYS_AMD", K_INPUT);
     set_iter("DO_OCEANIC_PHYS_AMD", *myIter);
-    if (mgcm_forward_step(g.m, 1)) die("DO_OCEANIC_PHYS_AMD");
-    g.devIter = *myIter + 1;
-    g.fused = true;
-    g.fusedPos = 1;
-    return;
+    bool replayed = true;
+    if (multi()) {
+      replayed = multi_replay("DO_OCEANIC_PHYS_AMD", *myIter);
+      if (!replayed) {   // the stream refused the capture before anything ran: stay eager
+        fprintf(stderr, "MGCM_AMD: stream capture of the %zu-model step refused; steps run routine by routine\n",
+                g.sh.size());
+        g.multiGraphOff = true;
+      }
+    } else {
+      if (mgcm_forward_step(g.m, 1)) die("DO_OCEANIC_PHYS_AMD");
+      g.devIter = *myIter + 1;
+    }
+    if (replayed) {
+      g.fused = true;
+      g.fusedPos = 1;
+      return;
+    }
   }
   g.seq.assign(1, "DO_OCEANIC_PHYS");
   g.recording = g.deviceAuth && fuse_allowed();
   routine("DO_OCEANIC_PHYS_AMD", op_oceanic_phys, *myIter, *myTime, true);
 }
-/* SUBROUTINE THERMODYNAMICS(myTime, myIter, myThid)      model/src/thermodynamics.F:25 */
+/* SUBROUTINE THERMODYNAMICS(myTime, myIter, myThid)      model/src/thermodynamics.F:25
+ * Under staggerTimeStep FORWARD_STEP calls it after advancing myIter (forward_step.F:806,
+ * 1032) and TEMP/SALT_INTEGRATE step the Adams-Bashforth terms at iterNb = myIter - 1
+ * (temp_integrate.F:154-155): the device's counter is the step's start either way. */
 void thermodynamics_amd_(const double *myTime, const int *myIter, const int *myThid) {
   (void)myThid;
   enter_time_loop("THERMODYNAMICS_AMD");
   if (absorbed("THERMODYNAMICS")) return;
-  routine("THERMODYNAMICS_AMD", op_tracer_step, *myIter, *myTime);
+  const bool late = staggered();
+  routine("THERMODYNAMICS_AMD", op_tracer_step, late ? *myIter - 1 : *myIter,
+          late ? *myTime - g.rd.deltaTClock : *myTime);
 }
 /* SUBROUTINE DYNAMICS(myTime, myIter, myThid)            model/src/dynamics.F:21 */
 void dynamics_amd_(const double *myTime, const int *myIter, const int *myThid) {
@@ -959,6 +1117,19 @@ void do_fields_blocking_exchanges_amd_(const int *myThid) {
     g.recording = false;
   }
   if (g.deviceAuth && host_reads_state(t, it)) download("DO_FIELDS_BLOCKING_EXCHANGES_AMD");
+}
+
+/* SUBROUTINE DO_STAGGER_FIELDS_EXCHANGES(myTime, myIter, myThid)
+ *                                            model/src/do_stagger_fields_exchanges.F:7
+ * staggerTimeStep (forward_step.F:1010): the new uVel, vVel, wVel exchanged before the
+ * staggered THERMODYNAMICS reads them. */
+void do_stagger_fields_exchanges_amd_(const double *myTime, const int *myIter, const int *myThid) {
+  (void)myThid;
+  model("DO_STAGGER_FIELDS_EXCHANGES_AMD");
+  if (!staggered()) return;   // do_stagger_fields_exchanges.F:37 (implicitIntGravWave: refused)
+  advanced(*myIter, *myTime);
+  if (absorbed("DO_STAGGER_FIELDS_EXCHANGES")) return;
+  routine("DO_STAGGER_FIELDS_EXCHANGES_AMD", op_stagger, *myIter, *myTime);
 }
 
 // -------------------------------------------------- exchanges and global sums

@@ -970,7 +970,17 @@ namespace mgcm {
 __global__ void k_set_iter(int *ctr, int v) {
   if (threadIdx.x == 0) ctr[0] = v;
 }
+__global__ void k_add_iter(int *ctr, int inc) {
+  if (threadIdx.x == 0) ctr[0] += inc;
+}
 }  // namespace mgcm
+
+int mgcm_add_iter(mgcm_model *m, int inc) {
+  HIPCHK(hipSetDevice(m->device));
+  hipLaunchKernelGGL(mgcm::k_add_iter, dim3(1), dim3(64), 0, m->stream, m->d_ctr, inc);
+  HIPCHK(hipGetLastError());
+  return 0;
+}
 
 int mgcm_set_iter(mgcm_model *m, int myIter) {
   HIPCHK(hipSetDevice(m->device));
@@ -1484,6 +1494,23 @@ int mgcm_blocking_exchanges(mgcm_model *m) {
   return 0;
 }
 
+int mgcm_stagger_exchanges(mgcm_model *m) {
+  if (check_ready(m)) return -1;
+  // DO_STAGGER_FIELDS_EXCHANGES (do_stagger_fields_exchanges.F:37-43): EXCH_UV_3D_RL(uVel,
+  // vVel, .TRUE.) and EXCH_3D_RL(wVel) before the staggered THERMODYNAMICS -- the exchange
+  // one_step makes there
+  if (m->uvMap) {
+    XFields xw{};
+    xw.p[0] = m->f.wVel; xw.nz[0] = m->d.Nr; xw.n = 1;
+    TIMED(K_EXCH, launch_exchange_mixed(m->d, m->f.uVel, m->f.vVel, m->d.Nr, m->d_uv[1], m->nUvU[1], m->nUvV[1], xw,
+                                        m->d_halo, m->nHalo, nullptr, m->stream));
+  } else {
+    TIMED(K_EXCH, exchange_uv(m, m->f.uVel, m->f.vVel, m->d.Nr, true) ? hipErrorUnknown : hipSuccess);
+    TIMED(K_EXCH, launch_exchange(m->d, m->f.wVel, m->d_halo, m->nHalo, m->d.Nr, m->stream));
+  }
+  return 0;
+}
+
 int mgcm_oceanic_phys(mgcm_model *m) {
   if (check_ready(m)) return -1;
   TIMED(K_PHYS, launch_oceanic_phys(m->d, m->p, m->f, m->d_ctr, m->stream));
@@ -1823,6 +1850,18 @@ static int one_step_graph(mgcm_model *m, hipGraphExec_t *out) {
   *out = m->graph1Exec[o][q];
   return 0;
 }
+int mgcm_tracer_parity(mgcm_model *m, int set) {
+  if (set < 0) return buffer_parity(m);
+  if (set > 3) return set_err("mgcm_tracer_parity: parity %d outside 0..3", set);
+  double *tB = m->f.theta == m->thetaA ? m->f.thetaNext : m->f.theta;
+  double *sB = m->f.salt == m->saltA ? m->f.saltNext : m->f.salt;
+  m->f.theta = (set & 1) ? tB : m->thetaA;
+  m->f.thetaNext = (set & 1) ? m->thetaA : tB;
+  m->f.salt = (set & 2) ? sB : m->saltA;
+  m->f.saltNext = (set & 2) ? m->saltA : sB;
+  return set;
+}
+
 // after a one-step replay: the tracer pointers one_step would have left
 static void one_step_graph_done(mgcm_model *m, int o, int q) {
   m->f.theta = m->graph1Tr[o][q][0]; m->f.thetaNext = m->graph1Tr[o][q][1];

@@ -207,6 +207,42 @@ class Exch2Topology:
                     raise ValueError("exch2: tile %d neighbour %d: %d opposing connections" % (is_, ns, len(opp)))
                 nb["opp"] = opp[0]
 
+    # ------------------------------------------------- W2_EXCH2_TOPOLOGY.h arrays
+    def w2_arrays(self, ldNb=None, ldT=None):
+        """The topology as the COMMON blocks of pkg/exch2/W2_EXCH2_TOPOLOGY.h hold it after
+        W2_E2SETUP (w2_e2setup.F -> w2_set_map_tiles.F, w2_set_tile2tiles.F), Fortran layout
+        (first index fastest): exch2_myFace, exch2_tBasex/y, exch2_is{N,S,E,W}edge,
+        exch2_nNeighbours (nTiles); exch2_neighbourId, exch2_opposingSend, exch2_neighbourDir,
+        exch2_oi/oj, exch2_iLo/iHi/jLo/jHi (ldNb, ldT); exch2_pij (4, ldNb, ldT) -- int32
+        arrays, what a Fortran host passes to the device library (mgcm_exch2_maps)."""
+        n = self.nTiles_
+        maxNb = max(len(self.nbr[t]) for t in range(1, n + 1))
+        ldNb = ldNb or maxNb
+        ldT = ldT or n
+        if maxNb > ldNb or n > ldT:
+            raise ValueError("w2_arrays: %d tiles / %d neighbours exceed (%d, %d)" % (n, maxNb, ldT, ldNb))
+        z = lambda *shape: np.zeros(shape, dtype=np.int32)
+        a = {"exch2_myFace": z(ldT), "exch2_tBasex": z(ldT), "exch2_tBasey": z(ldT), "exch2_isNedge": z(ldT),
+             "exch2_isSedge": z(ldT), "exch2_isEedge": z(ldT), "exch2_isWedge": z(ldT), "exch2_nNeighbours": z(ldT)}
+        for k in ("neighbourId", "opposingSend", "neighbourDir", "oi", "oj", "iLo", "iHi", "jLo", "jHi"):
+            a["exch2_" + k] = z(ldT, ldNb)
+        a["exch2_pij"] = z(ldT, ldNb, 4)
+        for t in range(1, n + 1):
+            a["exch2_myFace"][t - 1] = self.face[t]
+            a["exch2_tBasex"][t - 1], a["exch2_tBasey"][t - 1] = self.tBx[t], self.tBy[t]
+            a["exch2_isNedge"][t - 1], a["exch2_isSedge"][t - 1] = self.isN[t], self.isS[t]
+            a["exch2_isEedge"][t - 1], a["exch2_isWedge"][t - 1] = self.isE[t], self.isW[t]
+            a["exch2_nNeighbours"][t - 1] = len(self.nbr[t])
+            for q, nb in enumerate(self.nbr[t]):
+                a["exch2_neighbourId"][t - 1, q] = nb["tile"]
+                a["exch2_opposingSend"][t - 1, q] = nb["opp"] + 1
+                a["exch2_neighbourDir"][t - 1, q] = nb["e2e"] // 10
+                a["exch2_pij"][t - 1, q] = nb["pij"]
+                for k in ("oi", "oj", "iLo", "iHi", "jLo", "jHi"):
+                    a["exch2_" + k][t - 1, q] = nb[k]
+        a["ldNb"], a["ldT"] = ldNb, ldT
+        return a
+
     # ---------------------------------------------------------- index helpers
     def g(self, t, i, j):
         """flat offset of local point (i, j) (1-based, halo-inclusive) of 1-based tile t"""

@@ -45,6 +45,7 @@ EXPERIMENTS = {
     # tutorial_global_oce_latlon) + the pickups it restarts from at nIter0 = 36000
     "global_ocean.90x40x15": {
         "inputs": ["input/pickup.0000036000", "input/pickup.0000036000.meta", "input/pickup_cd.0000036000"],
+        "namelists": ["input/data", "input/data.pkg", "input/data.gmredi"],
         "output": "results/output.txt",
     },
     # cubed sphere (pkg/exch2, 6 faces of 32x32, one tile each), 1 level, vector-invariant
@@ -69,6 +70,7 @@ EXPERIMENTS = {
                    "input/lev_surfT_cs_12m.bin", "input/lev_surfS_cs_12m.bin", "input/shiQnet_cs32.bin",
                    "input/shiEmPR_cs32.bin", "input/trenberth_taux.bin", "input/trenberth_tauy.bin"] +
                   ["../tutorial_held_suarez_cs/input/grid_cs32.face00%d.bin" % f for f in range(1, 7)],
+        "namelists": ["input/data", "input/data.pkg", "input/data.gmredi"],
         "output": "results/output.txt",
     },
 }
@@ -171,6 +173,11 @@ def main():
                     fo.write(fi.read(nbytes))
                 continue
             shutil.copyfile(os.path.join(REF, exp, rel), os.path.join(out, os.path.basename(rel)))
+        # the experiment's namelist files (data: the run-time parameters the reference-host
+        # harness reads, refhost_parms.F), verbatim under <exp>/input/
+        for rel in spec.get("namelists", []):
+            os.makedirs(os.path.join(out, "input"), exist_ok=True)
+            shutil.copyfile(os.path.join(REF, exp, rel), os.path.join(out, "input", os.path.basename(rel)))
         res = os.path.join(REF, exp, spec["output"])
         with open(os.path.join(out, "monitor.json"), "w") as f:
             json.dump(parse_monitor(res), f, indent=1)

@@ -29,7 +29,8 @@ SHADOWS = {"cg2d.F": "cg2d_", "dynamics.F": "dynamics_", "thermodynamics.F": "th
            "do_oceanic_phys.F": "do_oceanic_phys_", "solve_for_pressure.F": "solve_for_pressure_",
            "momentum_correction_step.F": "momentum_correction_step_", "integr_continuity.F": "integr_continuity_",
            "update_r_star.F": "update_r_star_", "update_cg2d.F": "update_cg2d_", "calc_r_star.F": "calc_r_star_",
-           "do_fields_blocking_exchanges.F": "do_fields_blocking_exchanges_", "exch_xy_rl.F": "exch_xy_rl_",
+           "do_fields_blocking_exchanges.F": "do_fields_blocking_exchanges_",
+           "do_stagger_fields_exchanges.F": "do_stagger_fields_exchanges_", "exch_xy_rl.F": "exch_xy_rl_",
            "exch_xyz_rl.F": "exch_xyz_rl_", "exch_uv_xy_rl.F": "exch_uv_xy_rl_",
            "exch_uv_xyz_rl.F": "exch_uv_xyz_rl_", "global_sum_tile.F": "global_sum_tile_rl_",
            "mgcm_amd_mirror.F": "mgcm_amd_mirror_", "mgcm_amd_exch2.F": "mgcm_amd_exch2_maps_"}

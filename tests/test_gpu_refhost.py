@@ -47,10 +47,10 @@ CHECK = ("uVel", "vVel", "wVel", "theta", "salt", "etaN", "etaH", "gU", "gV", "g
 NSTEPS = 6
 
 
-def _mirror_calls():
+def _mirror_calls(undef=()):
     sys.path.insert(0, os.path.join(ROOT, "mitgcm_amd", "fortran"))
     import build_refhost
-    return build_refhost.mirror_calls()
+    return build_refhost.mirror_calls(undef)
 
 
 def _name(s):
@@ -63,13 +63,14 @@ def _name(s):
 PARAM_DIR = os.path.join(ROOT, "tests", "golden", "global_ocean.90x40x15", "input")
 
 
-def _write_blob(path, m, nsteps, monitor_days, packages_off=True, extra=()):
+def _write_blob(path, m, nsteps, monitor_days, packages_off=True, extra=(), w2=None, undef=()):
     """refhost_in.bin: sizes, the run's control (the only parameters it carries: the run length,
     the monitor schedule, and -- packages_off -- pkg/sbo and pkg/diagnostics switched off for
-    the run), the COMMON-block arrays (grid, masks and the restart state) and the forcing
-    records."""
+    the run), the COMMON-block arrays (grid, masks and the restart state), the forcing records
+    and -- w2, a pkg/exch2 topology (Exch2Topology.w2_arrays at W2_EXCH2_SIZE.h's leading
+    dimensions) -- the W2_EXCH2_TOPOLOGY.h arrays (refhost.F REFHOST_W2_READ)."""
     g = m.g
-    _, fields = _mirror_calls()
+    _, fields = _mirror_calls(undef)
     dtc = m.params["deltaTClock"]
     nIter0 = int(m.params["nIter0"])
     params = [("monitorFreq", monitor_days * dtc), ("nEndIter", float(nIter0 + nsteps))]
@@ -88,7 +89,7 @@ def _write_blob(path, m, nsteps, monitor_days, packages_off=True, extra=()):
         blob_fields.append((n, kind, a))
     with open(path, "wb") as fh:
         fh.write(np.array([g.sNx, g.sNy, g.OLx, g.OLy, g.Nr, g.nSx, g.nSy, len(params), len(blob_fields), nsteps,
-                           nIter0, nRec, periodic], dtype=np.int32).tobytes())
+                           nIter0, nRec, periodic, g.nTiles if w2 else 0], dtype=np.int32).tobytes())
         fh.write(np.array([dtc, m.params.get("externForcingPeriod", 0.0),
                            m.params.get("externForcingCycle", 0.0)]).tobytes())
         for n, v in params:
@@ -97,6 +98,11 @@ def _write_blob(path, m, nsteps, monitor_days, packages_off=True, extra=()):
             fh.write(_name(n) + np.array([a.size, kind], dtype=np.int32).tobytes() + a.tobytes())
         if periodic:
             fh.write(np.ascontiguousarray(m.get("forcRec").reshape(-1)[:6 * nRec * g.nTiles * g.nx * g.ny]).tobytes())
+        if w2:
+            fh.write(np.array([w2["ldNb"], w2["ldT"]], dtype=np.int32).tobytes())
+            for k in ("myFace", "tBasex", "tBasey", "isNedge", "isSedge", "isEedge", "isWedge", "nNeighbours",
+                      "neighbourId", "opposingSend", "neighbourDir", "pij", "oi", "oj", "iLo", "iHi", "jLo", "jHi"):
+                fh.write(np.ascontiguousarray(w2["exch2_" + k], dtype=np.int32).tobytes())
     return [n for n, k, a in blob_fields if k == 0]
 
 
@@ -236,3 +242,77 @@ def test_refhost_dropin_throughput(io, register, tmp_path):
     assert not bad, bad
     # the state came down after steps 10, 20, ..., 60 (dumpFreq) or after the last only
     assert st["downloads"] == (nsteps // 10 if io == "namelist" else 1) * len(state), st
+
+
+# BASELINE config 3 through the drop-ins: verification/global_ocean.cs32x15 on the reference's
+# own code/SIZE.h (12 tiles of 32 x 16, OL = 4) under pkg/exch2.  The harness is built against
+# the experiment's headers (build_refhost.py layout "cs32": W2_EXCH2_SIZE.h, staggerTimeStep,
+# no CD code) and fills the W2_EXCH2_TOPOLOGY.h COMMON blocks as W2_E2SETUP leaves them
+# (W2's default topology: no data.exch2); MGCM_AMD_EXCH2_MAPS hands those arrays to the
+# library, which derives the device's halo and vector maps itself (csrc/exch2_maps.hip:
+# EXCH2_3D_RL / EXCH2_UV_CGRID_3D_RL restated on point ids).  FORWARD_STEP runs in the
+# staggered order (DO_STAGGER_FIELDS_EXCHANGES, then THERMODYNAMICS after the continuity
+# step).  The experiment's namelists with nIter0 = 0 (a cold start: the reference tree does
+# not hold pickup.0000072000) and taveFreq = 0 (pkg/timeave: refused by the mirror).  Bar: the
+# state after 4 steps, with the 12 tiles on 1, 2, 3 and 6 device models (and eager, and the
+# device-sharded CG2D), is bit-identical to configs.global_ocean_cs32x15's
+# mgcm_forward_step.
+CS32_DIR = os.path.join(ROOT, "tests", "golden", "global_ocean.cs32x15", "input")
+
+
+def _cs32_namelists(dst):
+    import re
+    os.makedirs(dst, exist_ok=True)
+    for fn in ("data", "data.pkg", "data.gmredi"):
+        txt = open(os.path.join(CS32_DIR, fn)).read()
+        if fn == "data":
+            txt, n0 = re.subn(r"(?m)^(\s*)nIter0\s*=\s*\d+\s*,", r"\1nIter0=0,", txt)
+            txt, n1 = re.subn(r"(?m)^(\s*)taveFreq\s*=\s*[0-9.eE+]+\s*,", r"\1taveFreq=0.,", txt)
+            assert n0 == 1 and n1 == 1, (n0, n1)
+        open(os.path.join(dst, fn), "w").write(txt)
+    return dst
+
+
+@pytest.mark.parametrize("models,mwg,eager", [(1, 0, 0), (1, 0, 1), (2, 0, 0), (3, 0, 0), (6, 0, 0), (3, 1, 0)])
+def test_refhost_cs32_exch2_bitexact(models, mwg, eager, tmp_path):
+    from mitgcm_amd import configs
+    exe = os.path.join(RH, "refhost_cs32")
+    assert os.path.exists(exe), "refhost not built (mitgcm_amd/fortran/build_refhost.py, __graft_entry__.build())"
+    nsteps = 4
+
+    def cfg():
+        g, params, state, forcing = configs.global_ocean_cs32x15(sNy=16)
+        if mwg:
+            params["cg2dForceMwg"] = 1
+        return g, params, state, forcing
+    m = configs.make_model(cfg)
+    assert (m.g.nSx, m.g.nSy, m.g.sNx, m.g.sNy, m.g.OLx) == (12, 1, 32, 16, 4)
+    pdir = _cs32_namelists(str(tmp_path / "input"))
+    w2 = m.g.topo.w2_arrays(ldNb=8, ldT=2 * m.g.nTiles)   # W2_EXCH2_SIZE.h: W2_maxNeighbours, W2_maxNbTiles
+    state = _write_blob(tmp_path / "refhost_in.bin", m, nsteps, monitor_days=2, w2=w2, undef=("ALLOW_CD_CODE",))
+    env = dict(os.environ, MGCM_AMD_MODELS=str(models), MGCM_CG2D_MWG=str(mwg), MGCM_AMD_EAGER=str(eager))
+    r = subprocess.run([exe, str(tmp_path), pdir], capture_output=True, text=True, timeout=300, env=env)
+    assert r.returncode == 0, r.stdout + r.stderr
+    out, st = _read_out(tmp_path / "refhost_out.bin", state, nsteps)
+    m.forward_step(1)
+    m.prepare()
+    m.sync()
+    t0 = time.perf_counter()
+    m.forward_step(nsteps - 1)
+    m.sync()
+    graph_ms = 1e3 * (time.perf_counter() - t0) / (nsteps - 1)
+    bad = [(n, float(np.abs(out[n] - m.get(n).reshape(-1)[:out[n].size]).max())) for n in CHECK
+           if n in out and not np.array_equal(out[n], m.get(n).reshape(-1)[:out[n].size])]
+    m.close()
+    rec = {"layout": "cs32", "models": models, "cg2dForceMwg": mwg, "eager": eager,
+           "dropin_ms_per_step_mean": 1e3 * st["seconds"] / max(1, st["steps_timed"]),
+           "dropin_ms_per_step_no_download": st["step_ms"][2], "graph_ms_per_step": graph_ms, "mirror": st,
+           "state_fields": len(state)}
+    print("refhost cs32 models=%d mwg=%d eager=%d: %s" % (models, mwg, eager, json.dumps(rec)))
+    if os.path.isdir(os.path.join(ROOT, "gpurun_out")):
+        with open(os.path.join(ROOT, "gpurun_out", "refhost_cs32_m%d_w%d_e%d.json" % (models, mwg, eager)), "w") as f:
+            json.dump(rec, f)
+    assert not bad, bad
+    assert len([n for n in CHECK if n in out]) >= 18
+    # the state came down after steps 2 and 4 only (monitorFreq = 2 days, nEndIter = 4)
+    assert st["downloads"] == 2 * len(state), (st, len(state))

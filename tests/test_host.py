@@ -60,3 +60,41 @@ def test_library_exports_every_header_symbol():
     for sym in sorted(declared):
         assert hasattr(L, sym), sym
     assert declared == set(_lib.EXPORTS)
+
+
+def _w2_maps(topo):
+    """mgcm_exch2_maps (the library's derivation from the W2_EXCH2_TOPOLOGY.h arrays, host
+    only) on the arrays of an exch2.py topology."""
+    import ctypes
+    from mitgcm_amd._lib import lib
+    a = topo.w2_arrays()
+    IP = lambda x: np.ascontiguousarray(x, dtype=np.int32).ctypes.data_as(ctypes.POINTER(ctypes.c_int))
+    keep = {k: np.ascontiguousarray(v, dtype=np.int32) for k, v in a.items() if k.startswith("exch2_")}
+    N = topo.nTiles_ * topo.n2
+    out = [np.zeros(N, dtype=np.int64) for _ in range(5)]
+    LP = lambda x: x.ctypes.data_as(ctypes.POINTER(ctypes.c_long))
+    args = [keep[k] for k in ("exch2_tBasex", "exch2_tBasey", "exch2_isNedge", "exch2_isSedge", "exch2_isEedge",
+                              "exch2_isWedge", "exch2_nNeighbours", "exch2_neighbourId", "exch2_opposingSend",
+                              "exch2_pij", "exch2_oi", "exch2_oj", "exch2_iLo", "exch2_iHi", "exch2_jLo", "exch2_jHi")]
+    rc = lib().mgcm_exch2_maps(topo.sNx, topo.sNy, topo.OLx, topo.nTiles_, a["ldNb"], a["ldT"],
+                               *[IP(x) for x in args], *[LP(x) for x in out])
+    assert rc == 0
+    return out
+
+
+@pytest.mark.parametrize("kind,n,sNx,sNy,OL", [("cube", 32, 32, 32, 4), ("cube", 32, 32, 16, 4), ("cube", 32, 16, 16, 3),
+                                               ("llc", 30, 30, 30, 4), ("llc", 90, 90, 90, 4), ("llc", 30, 15, 30, 3)])
+def test_exch2_maps_from_w2_arrays(kind, n, sNx, sNy, OL):
+    """The library's pkg/exch2 map derivation from the W2_EXCH2_TOPOLOGY.h arrays
+    (csrc/exch2_maps.hip, what the Fortran mirror hands it) reproduces, point for point, the
+    maps of mitgcm_amd/exch2.py -- the restatement the cube and LLC tests pin to the
+    reference's output.txt (solid-body.cs-32x32x1, advect_cs, global_ocean.cs32x15's grid) --
+    for the cube at 6, 12 and 24 tiles and the LLC at 13 and 26 tiles."""
+    from mitgcm_amd import exch2
+    topo = exch2.cube_topology(n, sNx, sNy, OL) if kind == "cube" else exch2.llc_topology(n, sNx, sNy, OL)
+    src, u1, v1, u0, v0 = _w2_maps(topo)
+    assert np.array_equal(src, topo.src_of_point())
+    cu, cv = topo.uv_codes(True)
+    assert np.array_equal(u1, cu) and np.array_equal(v1, cv)
+    cu, cv = topo.uv_codes(False)
+    assert np.array_equal(u0, cu) and np.array_equal(v0, cv)
