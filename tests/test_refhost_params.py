@@ -8,9 +8,11 @@
   namelist files (refhost_parms.F: set_defaults.F, ini_parms.F PARM01-PARM04, data.pkg,
   data.gmredi, set_parms.F / ini_eos.F / gmredi_readparms.F derivations).  `refhost --params`
   writes what the mirror would pass; every value is pinned against the reference's own dump
-  of its resolved parameters (verification/global_ocean.90x40x15/results/output.txt, parsed
-  into tests/golden/global_ocean.90x40x15/params.json by tests/golden/make_golden.py) and
-  against the device-side configuration of the same experiment (mitgcm_amd/configs.py).
+  of its resolved parameters (verification/<exp>/results/output.txt, parsed into
+  tests/golden/<exp>/params.json by tests/golden/make_golden.py) and against the device-side
+  configuration of the same experiment (mitgcm_amd/configs.py), for global_ocean.90x40x15
+  and global_ocean.cs32x15 (BASELINE configs 2 and 3; the cube-sphere harness is built on
+  pkg/exch2, build_refhost.py layout "cs32").
 """
 import json
 import os
@@ -60,10 +62,23 @@ def _dump_value(v):
     return float(v)
 
 
-@pytest.mark.skipif(not os.path.exists(EXE), reason="refhost not built (needs the reference headers)")
-def test_refhost_resolves_the_namelist_as_the_reference(tmp_path):
+# experiment -> (harness layout, names the reference leaves UNSET, device-config differences):
+# global_ocean.cs32x15 (BASELINE config 3, pkg/exch2, staggerTimeStep, no CD scheme: epsAB_CD
+# stays unset; the device configuration is its cold start, nIter0 = 0, where the namelist
+# restarts from pickup.0000072000)
+EXPERIMENTS = {"global_ocean.90x40x15": ("ref", {"selectVortScheme", "temp_EvPrRn"}, ()),
+               "global_ocean.cs32x15": ("cs32", {"temp_EvPrRn", "epsAB_CD"}, ("nIter0",))}
+
+
+@pytest.mark.parametrize("exp", sorted(EXPERIMENTS))
+def test_refhost_resolves_the_namelist_as_the_reference(exp, tmp_path):
+    layout, unset_ok, cfg_skip = EXPERIMENTS[exp]
+    exe = os.path.join(ROOT, "mitgcm_amd", "fortran", "refhost", "refhost_" + layout)
+    if not os.path.exists(exe):
+        pytest.skip("refhost not built (needs the reference headers)")
     out = tmp_path / "params.txt"
-    r = subprocess.run([EXE, "--params", PARAM_DIR, str(out)], capture_output=True, text=True, timeout=60)
+    pdir = os.path.join(ROOT, "tests", "golden", exp, "input")
+    r = subprocess.run([exe, "--params", pdir, str(out)], capture_output=True, text=True, timeout=60)
     assert r.returncode == 0, r.stdout + r.stderr
     got = {}
     for line in open(out):
@@ -76,10 +91,10 @@ def test_refhost_resolves_the_namelist_as_the_reference(tmp_path):
     # momentum (set_parms.F), and temp_EvPrRn, whose UNSET_RL means "at the local SST"
     # (the reference's dump prints 1.234567E+05 too)
     unset = {n for n, v in got.items() if v in (1.234567e5, 123456789.0)}
-    assert unset <= {"selectVortScheme", "temp_EvPrRn"}, unset
-    assert got["vectorInvariantMomentum"] == 0.0
+    assert unset <= unset_ok, unset
+    assert got["vectorInvariantMomentum"] == (1.0 if exp == "global_ocean.cs32x15" else 0.0)
     # pinned against the reference's own resolved-parameter dump
-    ref = json.load(open(os.path.join(ROOT, "tests", "golden", "global_ocean.90x40x15", "params.json")))
+    ref = json.load(open(os.path.join(ROOT, "tests", "golden", exp, "params.json")))
     compared, bad = 0, []
     for n, v in got.items():
         key = DUMP_NAMES.get(n, n)
@@ -95,7 +110,7 @@ def test_refhost_resolves_the_namelist_as_the_reference(tmp_path):
     assert compared >= 70, compared
     # and against the device-side configuration of the same experiment (configs.py)
     from mitgcm_amd import configs
-    _, params, _, _ = configs.global_ocean_90x40x15()
-    shared = [n for n in got if n in params and n not in ("monitorFreq", "nEndIter")]
+    _, params, _, _ = (configs.global_ocean_90x40x15() if layout == "ref" else configs.global_ocean_cs32x15(sNy=16))
+    shared = [n for n in got if n in params and n not in ("monitorFreq", "nEndIter") + cfg_skip]
     diff = [(n, got[n], float(params[n])) for n in shared if got[n] != float(params[n])]
     assert len(shared) >= 40 and not diff, (len(shared), diff)
