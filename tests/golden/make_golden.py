@@ -9,6 +9,12 @@ What it writes (data only -- inputs and expected outputs, no reference source):
                                       committed verification/<exp>/results/output.txt
   tests/golden/<exp>/params.json      resolved run-time parameters parsed from the
                                       "Model configuration" dump of the same output.txt
+  tests/golden/adjustment.cs-32x32x1/w2_topology.json
+                                      the "W2 TILE TOPLOGY" lists (per tile, its neighbours'
+                                      tile ids in W2's order) the reference printed for its
+                                      default 6-face cube of 32 x 32 on 48 tiles of 16 x 8
+                                      (results/output.txt) and 6 tiles of 32 x 32
+                                      (results/output.nlfs.txt), with the tile sizes
 """
 import json
 import os
@@ -158,8 +164,37 @@ def parse_params(path):
     return params
 
 
+W2_TOPOLOGY = ("adjustment.cs-32x32x1", ["results/output.txt", "results/output.nlfs.txt"])
+
+
+def parse_w2_topology(path):
+    """The tile sizes and, per tile, the neighbour tile ids of the 'W2 TILE TOPLOGY' print
+    (pkg/exch2 w2_print_e2setup.F, W2_printMsg)."""
+    txt = open(path).read()
+    size = {k: int(re.search(r"\b%s =\s+(\d+) ;" % k, txt).group(1)) for k in ("sNx", "sNy", "nSx", "nSy", "OLx")}
+    tiles = {}
+    cur = None
+    for line in txt.splitlines():
+        m = re.search(r"^\(PID\.TID 0000\.0001\)\s+TILE:\s+(\d+)\s*$", line)
+        if m:
+            cur = int(m.group(1))
+            tiles[cur] = []
+            continue
+        m = re.search(r"NEIGHBOUR\s+(\d+) = TILE\s+(\d+)", line)
+        if m and cur is not None:
+            assert int(m.group(1)) == len(tiles[cur]) + 1
+            tiles[cur].append(int(m.group(2)))
+    return dict(size, neighbours=[tiles[t] for t in sorted(tiles)])
+
+
 def main():
     only = sys.argv[1:]   # optional: experiment names to (re)extract
+    if not only or "w2" in only:
+        exp, outs = W2_TOPOLOGY
+        os.makedirs(os.path.join(HERE, exp), exist_ok=True)
+        with open(os.path.join(HERE, exp, "w2_topology.json"), "w") as f:
+            json.dump({o: parse_w2_topology(os.path.join(REF, exp, o)) for o in outs}, f)
+        print("wrote", os.path.join(HERE, exp, "w2_topology.json"))
     for exp, spec in EXPERIMENTS.items():
         if only and exp not in only:
             continue

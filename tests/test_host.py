@@ -1,6 +1,7 @@
 """CPU tests: host-side initialisation vs the oracle, topology, and the C-ABI
 library's exported symbols (no GPU compute here)."""
 import ctypes
+import json
 import os
 import re
 
@@ -98,3 +99,20 @@ def test_exch2_maps_from_w2_arrays(kind, n, sNx, sNy, OL):
     assert np.array_equal(u1, cu) and np.array_equal(v1, cv)
     cu, cv = topo.uv_codes(False)
     assert np.array_equal(u0, cu) and np.array_equal(v0, cv)
+
+
+@pytest.mark.parametrize("out", ["results/output.txt", "results/output.nlfs.txt"])
+def test_w2_default_cube_topology_pinned(out):
+    """The W2 topology the cs32 harness fills W2_EXCH2_TOPOLOGY.h with (exch2.py's restatement
+    of W2_E2SETUP for the default 6-face cube, no data.exch2: w2_set_cs6_facets.F,
+    w2_set_map_tiles.F, w2_set_tile2tiles.F) against the reference's own print of it:
+    verification/adjustment.cs-32x32x1 lists, per tile, its neighbours' tile ids in W2's order
+    for the cube of 32 x 32 faces on 48 tiles of 16 x 8 and on 6 tiles of 32 x 32
+    (tests/golden/adjustment.cs-32x32x1/w2_topology.json, make_golden.py)."""
+    from mitgcm_amd import exch2
+    fx = json.load(open(os.path.join(ROOT, "tests", "golden", "adjustment.cs-32x32x1", "w2_topology.json")))[out]
+    topo = exch2.cube_topology(32, fx["sNx"], fx["sNy"], fx["OLx"])
+    assert topo.nTiles_ == fx["nSx"] * fx["nSy"] == len(fx["neighbours"])
+    w2 = topo.w2_arrays()
+    got = [list(w2["exch2_neighbourId"][t, :w2["exch2_nNeighbours"][t]]) for t in range(topo.nTiles_)]
+    assert got == fx["neighbours"]
