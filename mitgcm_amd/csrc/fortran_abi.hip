@@ -53,7 +53,10 @@
 //
 // Errors: no return channel exists in the reference (it prints and STOPs), so every
 // failure prints "ABNORMAL END: <routine>: <reason>" and aborts.
+#include <execinfo.h>
 #include <hip/hip_runtime.h>
+#include <signal.h>
+#include <unistd.h>
 
 #include <algorithm>
 #include <cmath>
@@ -162,6 +165,31 @@ FortranSide g;
   abort();
 }
 
+// A fault in the host process (SIGSEGV, SIGBUS) prints the host stack, then hands the signal
+// to whatever handled it before (the Fortran runtime's, the HIP runtime's, or the default
+// action): the reference's hosts have no other channel for it.  Installed by MGCM_AMD_INIT,
+// after the HIP runtime has set up its own.
+struct sigaction g_oldSegv, g_oldBus;
+void fatal_signal(int sig) {
+  static const char msg[] = "ABNORMAL END: MGCM_AMD: fatal signal in the host process; stack:\n";
+  (void)!write(2, msg, sizeof msg - 1);
+  void *fr[64];
+  const int n = backtrace(fr, 64);
+  backtrace_symbols_fd(fr, n, 2);
+  sigaction(sig, sig == SIGSEGV ? &g_oldSegv : &g_oldBus, nullptr);
+  raise(sig);
+}
+void install_fault_report() {
+  static bool done = false;
+  if (done) return;
+  done = true;
+  struct sigaction sa {};
+  sa.sa_handler = fatal_signal;
+  sigemptyset(&sa.sa_mask);
+  sigaction(SIGSEGV, &sa, &g_oldSegv);
+  sigaction(SIGBUS, &sa, &g_oldBus);
+}
+
 std::string fstr(const char *s, size_t len) {   // Fortran CHARACTER: blank padded, no NUL
   while (len > 0 && (s[len - 1] == ' ' || s[len - 1] == '\0')) len--;
   return std::string(s, len);
@@ -234,7 +262,10 @@ void gather2d(const char *where, const char *name) {
 
 // The 3-D halo sources of a field group (mgcm_halo_pack_group: 0 all of
 // DO_FIELDS_BLOCKING_EXCHANGES' fields) along every link: pack on the owner, copy GPU to GPU,
-// unpack on the reader -- then each model's local halo fill reads them.
+// unpack on the reader -- then each model's local halo fill reads them.  The barrier before
+// keeps a link's receive buffer from being refilled while its reader still unpacks the
+// previous transfer; after it, each reader's stream has waited for its own links' copies
+// (per-link events) and needs nothing from the others.
 void xfer3d(const char *where, int group) {
   barrier_all(where);
   const int Nr = g.dims[4];
@@ -252,7 +283,6 @@ void xfer3d(const char *where, int group) {
     hipchk(hipStreamWaitEvent(stream_of(b), L.ev, 0), where);
     if (mgcm_halo_pack_group(b.m, group, L.idxD, L.n, L.rbuf, 1)) die(where);
   }
-  barrier_all(where);
 }
 
 // ---- the device routines a drop-in runs (on every model, with the exchange points) ------
@@ -677,6 +707,11 @@ bool multi_replay(const char *w, int myIter) {
   join_into_0(w);   // the forcing uploads of every model before the graph
   if (!G.exec) {
     hipStream_t s0 = stream_of(g.sh[0]);
+    bool one = getenv("MGCM_AMD_CAPTURE_ONE") && atoi(getenv("MGCM_AMD_CAPTURE_ONE")) != 0;   // (diagnostic)
+    for (auto &s : g.sh) one = one && s.dev == g.sh[0].dev;
+    if (one)
+      for (size_t i = 1; i < g.sh.size(); i++)
+        if (mgcm_set_stream(g.sh[i].m, s0)) die(w);
     hipchk(hipSetDevice(g.sh[0].dev), w);
     if (hipStreamBeginCapture(s0, hipStreamCaptureModeGlobal) != hipSuccess) {
       (void)hipGetLastError();
@@ -693,6 +728,9 @@ bool multi_replay(const char *w, int myIter) {
     hipError_t e = hipStreamEndCapture(s0, &gr);
     if (e == hipSuccess) e = hipGraphInstantiate(&G.exec, gr, nullptr, nullptr, 0);
     if (gr) (void)hipGraphDestroy(gr);
+    if (one)
+      for (size_t i = 1; i < g.sh.size(); i++)
+        if (mgcm_set_stream(g.sh[i].m, nullptr)) die(w);
     // the capture ran the step's host side (the CYCLE_TRACER swaps) without its device work:
     // nothing consistent to fall back to
     if (e != hipSuccess) die(w, hipGetErrorString(e));
@@ -915,6 +953,7 @@ void mgcm_amd_bind_(const char *name, double *array, const int *count, const int
  * overwritten by the host's state again. */
 void mgcm_amd_init_(const int *myIter) {
   model("MGCM_AMD_INIT");
+  install_fault_report();
   // device options with no PARAMS.h counterpart, from the environment:
   // MGCM_CG2D_REFORDER=1 sums CG2D in the reference's order (cg2dRefOrder, parity runs)
   // (several models: each is set up on the whole domain -- the CG2D tables too -- and only

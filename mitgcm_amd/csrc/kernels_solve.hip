@@ -772,6 +772,10 @@ __device__ __forceinline__ double block_max_nw(double v, double *red, int slot) 
 // SR: CG2D_SR (cg2d_sr.F, useSRCGSolver) -- one standard step, then per iteration y = M r,
 // v = A y and the three sums (y.r, y.v, r.r) in one reduction: three barriers per iteration
 // (y, the reduction, r) instead of four; s_l holds y.
+// (round 5 measured lifting the s- and r-update barriers by re-deriving the out-of-block
+// neighbours' s_n = beta*s_{n-1} + M r and r_n = r_{n-1} - alpha*A s from values published
+// before the reductions: bit-identical, but the extra live values spill -- 2.89-4.30 against
+// 1.64 us/iteration, profiles/r05/cg_lb/)
 template <int BX, int BY, int NT, bool MINRES, bool FMA, bool SR = false>
 __global__ void __launch_bounds__(NT) k_cg2d_bxy(Dims d, Params p, Fields f, const unsigned *__restrict__ nbx,
                                                  const int *__restrict__ blkx, int nBlk, int maxIters, int nIterMinIn,
@@ -793,7 +797,9 @@ __global__ void __launch_bounds__(NT) k_cg2d_bxy(Dims d, Params p, Fields f, con
 #pragma unroll
     for (int a = 0; a < BX; a++) {
       G[b][a] = blkx[NPT * bt + BX * b + a];
-      cs[b][a] = act ? (BX * b + a) * NT + tid : NP;   // point-major LDS slots (see build_nbr)
+      // point-major LDS slots (see build_nbr); an idle thread (tid >= nBlk, all its values 0)
+      // keeps its own slots, which no block's neighbour table names
+      cs[b][a] = (BX * b + a) * NT + tid;
     }
   unsigned nbp[NB / 2];
 #pragma unroll
@@ -1366,25 +1372,28 @@ __global__ void __launch_bounds__(256) k_corr_cont(Dims d, Params p, Fields f, i
     const double pX0 = phiX(i, j), pX1 = phiX(i + 1, j), pY0 = phiY(i, j), pY1 = phiY(i, j + 1);
     MG_COLF_K(k) {
       const int me = (k - 1) * NC_ + cc;
-      auto uCor = [&](int ii, double phiSurfX) {
-        const long q3 = MG_I3(d, ii, j, k, t);
-        const double mW = f.maskW[q3];
+      // maskW / maskS are hFacW / hFacS != 0 at every point (ini_masks_etc.F:467-479, after the
+      // hFac exchange; r* rescales hFac by positive factors): taken from the thicknesses the
+      // transports read anyway -- two fewer 3-D streams
+      const long q3c = MG_I3(d, i, j, k, t), q3e = MG_I3(d, i + 1, j, k, t), q3n = MG_I3(d, i, j + 1, k, t);
+      const double hW0 = f.hFacW[q3c], hW1 = f.hFacW[q3e], hS0 = f.hFacS[q3c], hS1 = f.hFacS[q3n];
+      auto uCor = [&](long q3, double hW, double phiSurfX) {
+        const double mW = hW != 0.0 ? 1.0 : 0.0;
         return (f.gU[q3] + p.deltaTMom * (-psFac * phiSurfX * mW)) * mW;
       };
-      auto vCor = [&](int jj, double phiSurfY) {
-        const long q3 = MG_I3(d, i, jj, k, t);
-        const double mS = f.maskS[q3];
+      auto vCor = [&](long q3, double hS, double phiSurfY) {
+        const double mS = hS != 0.0 ? 1.0 : 0.0;
         return (f.gV[q3] + p.deltaTMom * (-psFac * phiSurfY * mS)) * mS;
       };
-      const double u0 = uCor(i, pX0), u1 = uCor(i + 1, pX1);
-      const double v0 = vCor(j, pY0), v1 = vCor(j + 1, pY1);
+      const double u0 = uCor(q3c, hW0, pX0), u1 = uCor(q3e, hW1, pX1);
+      const double v0 = vCor(q3c, hS0, pY0), v1 = vCor(q3n, hS1, pY1);
       sU[me] = u0;
       sV[me] = v0;
       const double drF = f.drF[k - 1];
-      const double uT1 = u1 * f.dyG[MG_I2(d, i + 1, j, t)] * drF * f.hFacW[MG_I3(d, i + 1, j, k, t)];
-      const double uT0 = u0 * f.dyG[q] * drF * f.hFacW[MG_I3(d, i, j, k, t)];
-      const double vT1 = v1 * f.dxG[MG_I2(d, i, j + 1, t)] * drF * f.hFacS[MG_I3(d, i, j + 1, k, t)];
-      const double vT0 = v0 * f.dxG[q] * drF * f.hFacS[MG_I3(d, i, j, k, t)];
+      const double uT1 = u1 * f.dyG[MG_I2(d, i + 1, j, t)] * drF * hW1;
+      const double uT0 = u0 * f.dyG[q] * drF * hW0;
+      const double vT1 = v1 * f.dxG[MG_I2(d, i, j + 1, t)] * drF * hS1;
+      const double vT0 = v0 * f.dxG[q] * drF * hS0;
       sDiv[me] = uT1 - uT0 + vT1 - vT0;
       sMask[me] = f.maskC[MG_I3(d, i, j, k, t)];
       if (rstar) sH0[me] = f.h0FacC[MG_I3(d, i, j, k, t)];

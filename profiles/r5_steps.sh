@@ -1,0 +1,34 @@
+#!/bin/bash
+# Round-5 GPU call driver: runs the named steps in order; a step that fails its tests goes on
+# to the next, one that times out, aborts or faults (124, 134, 137, 139) ends the call.
+#   bash profiles/r5_steps.sh <out-tag> refhost_multi | parity | cg_lb | refhost_all | all_gpu ...
+set -o pipefail
+cd "$GRAFT_REPO_ROOT" 2>/dev/null || cd /root/repo
+export TMPDIR=/tmp
+T=$1
+shift
+O=gpurun_out/$T
+mkdir -p $O
+PY="python -u -m pytest -v --timeout 300 --timeout-method thread"
+worst=0
+for s in "$@"; do
+  case $s in
+    refhost_multi) timeout -k 10 400 $PY tests/test_gpu_refhost.py -k "ref-0-4 or 6-0 or 3-1" > $O/refhost_multi.log 2>&1 ;;
+    refhost_m4) timeout -k 10 300 $PY tests/test_gpu_refhost.py -k "ref-0-4-0-0-0 or 6-0-0" > $O/refhost_m4.log 2>&1 ;;
+    refhost_m4_one) MGCM_AMD_CAPTURE_ONE=1 timeout -k 10 300 $PY tests/test_gpu_refhost.py -k "ref-0-4-0-0-0 or 6-0-0 or throughput" > $O/refhost_m4_one.log 2>&1 ;;
+    refhost_tp) timeout -k 10 300 $PY tests/test_gpu_refhost.py -k "throughput" > $O/refhost_tp.log 2>&1 ;;
+    refhost_all) timeout -k 10 600 $PY tests/test_gpu_refhost.py > $O/refhost_all.log 2>&1 ;;
+    parity) timeout -k 10 500 $PY -x tests/test_gpu_llc.py tests/test_gpu_ocean90.py tests/test_gpu_cs32x15.py > $O/parity.log 2>&1 ;;
+    all_gpu) timeout -k 10 1000 $PY tests -m gpu > $O/all_gpu.log 2>&1 ;;
+    cg_lb) bash profiles/cg_lb.sh $T/cg_lb > $O/cg_lb.log 2>&1 ;;
+    bench) bash profiles/r5_check.sh $T/bench bench > $O/bench.log 2>&1 ;;
+    *) echo "unknown step $s"; exit 2 ;;
+  esac
+  rc=$?
+  echo "step $s rc=$rc"
+  f=$(ls -t $O/*.log 2>/dev/null | head -1)
+  [ -n "$f" ] && tail -4 $f
+  case $rc in 124|134|137|139) echo "stopping after $s (rc $rc)"; exit $rc ;; esac
+  [ $rc -ne 0 ] && worst=$rc
+done
+exit $worst

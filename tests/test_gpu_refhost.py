@@ -137,7 +137,7 @@ def _read_out(path, state_names, nsteps):
 # diagnostics only; the mirror refuses useDiagnostics otherwise)
 @pytest.mark.parametrize("layout,refOrder,models,mwg,eager,packages", [
     ("ref", 0, 1, 0, 0, 0), ("ref", 1, 1, 0, 0, 0), ("1t", 0, 1, 0, 0, 0), ("1t", 0, 1, 0, 1, 0),
-    ("ref", 0, 1, 0, 1, 0), ("ref", 0, 2, 0, 0, 0), ("ref", 0, 4, 0, 0, 0), ("ref", 1, 4, 0, 0, 0),
+    ("ref", 0, 1, 0, 1, 0), ("ref", 0, 2, 0, 0, 0), ("ref", 0, 4, 0, 1, 0), ("ref", 0, 4, 0, 0, 0), ("ref", 1, 4, 0, 0, 0),
     ("ref", 0, 1, 1, 0, 0), ("ref", 0, 3, 1, 0, 0), ("1t", 0, 1, 0, 0, 1)])
 def test_refhost_mods_dropins_bitexact(layout, refOrder, models, mwg, eager, packages, tmp_path):
     from mitgcm_amd import configs
@@ -204,9 +204,12 @@ def test_refhost_mods_dropins_bitexact(layout, refOrder, models, mwg, eager, pac
 # (dumpFreq = 10 days: the state comes down after every 10th step, into the registered COMMON
 # pages); io = "off": dumpFreq = 0, the state comes down after the last step only.  The state
 # after the run is bit-identical to the resident graph path's; both rates are recorded
-# (INTEGRATION.md section 3).
-@pytest.mark.parametrize("io,register", [("namelist", 1), ("off", 1), ("namelist", 0)])
-def test_refhost_dropin_throughput(io, register, tmp_path):
+# (INTEGRATION.md section 3).  models > 1: the 36 tiles over that many device models of the
+# one GPU, every step after the recorded one ONE replay of the graph captured across the
+# models' streams.
+@pytest.mark.parametrize("io,register,models", [("namelist", 1, 1), ("off", 1, 1), ("namelist", 0, 1), ("off", 1, 2),
+                                                ("off", 1, 3), ("off", 1, 4)])
+def test_refhost_dropin_throughput(io, register, models, tmp_path):
     from mitgcm_amd import configs
     nsteps = 60
     exe = os.path.join(RH, "refhost_ref")
@@ -214,7 +217,7 @@ def test_refhost_dropin_throughput(io, register, tmp_path):
     m = configs.make_model(lambda: configs.global_ocean_90x40x15(nSx=9, nSy=4))
     extra = [("dumpFreq", 0.0)] if io == "off" else []
     state = _write_blob(tmp_path / "refhost_in.bin", m, nsteps, monitor_days=10 * nsteps, extra=extra)
-    env = dict(os.environ, MGCM_AMD_MODELS="1", MGCM_AMD_EAGER="0", MGCM_AMD_STEP_FENCE="0",
+    env = dict(os.environ, MGCM_AMD_MODELS=str(models), MGCM_AMD_EAGER="0", MGCM_AMD_STEP_FENCE="0",
                MGCM_AMD_REGISTER=str(register))
     r = subprocess.run([exe, str(tmp_path), PARAM_DIR], capture_output=True, text=True, timeout=300, env=env)
     assert r.returncode == 0, r.stdout + r.stderr
@@ -229,7 +232,8 @@ def test_refhost_dropin_throughput(io, register, tmp_path):
     bad = [(n, float(np.abs(out[n] - m.get(n).reshape(-1)[:out[n].size]).max())) for n in CHECK
            if n in out and not np.array_equal(out[n], m.get(n).reshape(-1)[:out[n].size])]
     m.close()
-    rec = {"steps": nsteps, "io": io, "register": register, "dropin_ms_per_step": 1e3 * st["seconds"] / max(1, st["steps_timed"]),
+    rec = {"steps": nsteps, "io": io, "register": register, "models": models,
+           "dropin_ms_per_step": 1e3 * st["seconds"] / max(1, st["steps_timed"]),
            "graph_ms_per_step": graph_ms, "uploads": st["uploads"], "downloads": st["downloads"],
            "bytes_down": st["bytes_down"],
            "dropin_ms_per_step_steady": float(np.median(st["step_ms"][5:-1])),
@@ -237,7 +241,7 @@ def test_refhost_dropin_throughput(io, register, tmp_path):
            "host_side_step_ms": [round(x, 4) for x in st["step_ms"]]}
     print("refhost throughput: %s" % json.dumps(rec))
     if os.path.isdir(os.path.join(ROOT, "gpurun_out")):
-        with open(os.path.join(ROOT, "gpurun_out", "refhost_throughput_%s_r%d.json" % (io, register)), "w") as f:
+        with open(os.path.join(ROOT, "gpurun_out", "refhost_throughput_%s_r%d_m%d.json" % (io, register, models)), "w") as f:
             json.dump(rec, f)
     assert not bad, bad
     # the state came down after steps 10, 20, ..., 60 (dumpFreq) or after the last only
@@ -273,7 +277,7 @@ def _cs32_namelists(dst):
     return dst
 
 
-@pytest.mark.parametrize("models,mwg,eager", [(1, 0, 0), (1, 0, 1), (2, 0, 0), (3, 0, 0), (6, 0, 0), (3, 1, 0)])
+@pytest.mark.parametrize("models,mwg,eager", [(1, 0, 0), (1, 0, 1), (2, 0, 0), (3, 0, 0), (6, 0, 1), (6, 0, 0), (3, 1, 0)])
 def test_refhost_cs32_exch2_bitexact(models, mwg, eager, tmp_path):
     from mitgcm_amd import configs
     exe = os.path.join(RH, "refhost_cs32")
