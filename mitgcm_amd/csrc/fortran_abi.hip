@@ -300,7 +300,27 @@ void op_solve(const char *w) {
   phase_all(w, 11);
   gather2d(w, "cg2d_b");
   gather2d(w, "cg2d_x");
-  if (!g.cgDevice) return phase_all(w, 12);   // the single-CU solve of the gathered domain, on every model
+  if (!g.cgDevice) {
+    // the single-CU solve of the gathered domain + EXCH(cg2d_x) + etaN, once per GPU (its lead
+    // model: every model of a GPU would solve the same problem to the same bits), the result
+    // copied to that GPU's other models
+    const size_t bytes = (size_t)n2() * nTiles() * sizeof(double);
+    for (auto &c : g.cgLeads) {
+      const Shard &L = g.sh[c.shard];
+      hipchk(hipSetDevice(L.dev), w);
+      if (mgcm_step_phase(L.m, 12)) die(w);
+      for (size_t j = 0; j < g.sh.size(); j++) {
+        if ((int)j == c.shard || g.sh[j].dev != L.dev) continue;
+        for (const char *nm : {"cg2d_x", "etaN"}) {
+          const double *src = mgcm_device_ptr(L.m, nm);
+          double *dst = mgcm_device_ptr(g.sh[j].m, nm);
+          if (!src || !dst) die(w);
+          hipchk(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToDevice, stream_of(L)), w);
+        }
+      }
+    }
+    return barrier_all(w);
+  }
   // the device CG2D: one launch per GPU over its models' tiles (its lead's arrays hold the
   // gathered right-hand side), all launches on one hand-off block; then each GPU's solution
   // blocks to every other model
@@ -646,9 +666,15 @@ bool canonical_step(const std::vector<std::string> &q) {
   want.push_back("DO_FIELDS_BLOCKING_EXCHANGES");
   return q == want;
 }
+// Replay: one model, or N models on one GPU (captured onto one stream, multi_replay); models
+// spread over several GPUs step routine by routine (a graph spanning GPUs is not captured)
 bool fuse_allowed() {
   const char *e = getenv("MGCM_AMD_EAGER");
-  return !(e && atoi(e) == 1) && !(multi() && g.multiGraphOff);
+  if (e && atoi(e) == 1) return false;
+  if (!multi()) return true;
+  for (auto &s : g.sh)
+    if (s.dev != g.sh[0].dev) return false;
+  return !g.multiGraphOff;
 }
 
 // The device work of the recorded step's drop-ins, in their order, with the iteration
@@ -707,14 +733,20 @@ bool multi_replay(const char *w, int myIter) {
   join_into_0(w);   // the forcing uploads of every model before the graph
   if (!G.exec) {
     hipStream_t s0 = stream_of(g.sh[0]);
-    bool one = getenv("MGCM_AMD_CAPTURE_ONE") && atoi(getenv("MGCM_AMD_CAPTURE_ONE")) != 0;   // (diagnostic)
-    for (auto &s : g.sh) one = one && s.dev == g.sh[0].dev;
-    if (one)
-      for (size_t i = 1; i < g.sh.size(); i++)
-        if (mgcm_set_stream(g.sh[i].m, s0)) die(w);
+    // every model issues on model 0's stream while capturing: the graph is one chain of the
+    // models' work in the recorded order (graphs captured across two or more streams of one GPU
+    // faulted in the HIP runtime's own threads -- SIGSEGV, no host frame -- once 4 or more models
+    // were in them, with any grouping of the models onto 2, 3 or 6 streams and with chained or
+    // all-to-all barriers; with 2 or 3 models they replayed correctly but no faster than the
+    // one-stream graph: 0.60 against 0.58 ms/step at 2 models, 0.74-0.88 against 0.83 at 3,
+    // profiles/r05/capture_ab/)
+    for (size_t i = 1; i < g.sh.size(); i++)
+      if (mgcm_set_stream(g.sh[i].m, s0)) die(w);
     hipchk(hipSetDevice(g.sh[0].dev), w);
     if (hipStreamBeginCapture(s0, hipStreamCaptureModeGlobal) != hipSuccess) {
       (void)hipGetLastError();
+      for (size_t i = 1; i < g.sh.size(); i++)
+        if (mgcm_set_stream(g.sh[i].m, nullptr)) die(w);
       return false;
     }
     fork_from_0(w);
@@ -728,9 +760,8 @@ bool multi_replay(const char *w, int myIter) {
     hipError_t e = hipStreamEndCapture(s0, &gr);
     if (e == hipSuccess) e = hipGraphInstantiate(&G.exec, gr, nullptr, nullptr, 0);
     if (gr) (void)hipGraphDestroy(gr);
-    if (one)
-      for (size_t i = 1; i < g.sh.size(); i++)
-        if (mgcm_set_stream(g.sh[i].m, nullptr)) die(w);
+    for (size_t i = 1; i < g.sh.size(); i++)   // each model back on its own stream
+      if (mgcm_set_stream(g.sh[i].m, nullptr)) die(w);
     // the capture ran the step's host side (the CYCLE_TRACER swaps) without its device work:
     // nothing consistent to fall back to
     if (e != hipSuccess) die(w, hipGetErrorString(e));

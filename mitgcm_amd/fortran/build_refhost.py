@@ -18,6 +18,8 @@ Layouts:
   cs32  verification/global_ocean.cs32x15/code/SIZE.h as committed: 12 tiles of 32 x 16,
         OL = 4, on pkg/exch2 (the cube's six 32 x 32 faces, two tiles each: W2's default
         topology, the experiment has no data.exch2), staggerTimeStep
+  cs32_6t  the same experiment on six 32 x 32 tiles, one per face (the device's bench layout;
+        refhost/SIZE.h.cs32_6t)
 """
 import os
 import re
@@ -37,7 +39,8 @@ RH = os.path.join(HERE, "refhost")
 OCEAN90 = ("global_ocean.90x40x15", "#define ALLOW_GMREDI\n#define ALLOW_CD_CODE\n")
 CS32 = ("global_ocean.cs32x15", "#define ALLOW_GMREDI\n#define ALLOW_EXCH2\n")
 # layout -> (experiment, PACKAGES_CONFIG.h, SIZE.h replacing the experiment's or None)
-LAYOUTS = {"ref": OCEAN90 + (None,), "1t": OCEAN90 + (os.path.join(RH, "SIZE.h.1t"),), "cs32": CS32 + (None,)}
+LAYOUTS = {"ref": OCEAN90 + (None,), "1t": OCEAN90 + (os.path.join(RH, "SIZE.h.1t"),), "cs32": CS32 + (None,),
+           "cs32_6t": CS32 + (os.path.join(RH, "SIZE.h.cs32_6t"),)}
 
 
 def available():
@@ -182,7 +185,7 @@ def _pre(src, tmp, incdirs):
     return f
 
 
-def build(layouts=("ref", "1t", "cs32"), verbose=False):
+def build(layouts=("ref", "1t", "cs32", "cs32_6t"), verbose=False):
     if not available():
         raise RuntimeError("build_refhost needs /root/reference (headers), amdflang and cpp")
     lib = os.path.join(ROOT, "mitgcm_amd", "libmitgcm_amd.so")

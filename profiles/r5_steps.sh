@@ -15,10 +15,10 @@ for s in "$@"; do
   case $s in
     refhost_multi) timeout -k 10 400 $PY tests/test_gpu_refhost.py -k "ref-0-4 or 6-0 or 3-1" > $O/refhost_multi.log 2>&1 ;;
     refhost_m4) timeout -k 10 300 $PY tests/test_gpu_refhost.py -k "ref-0-4-0-0-0 or 6-0-0" > $O/refhost_m4.log 2>&1 ;;
-    refhost_m4_one) MGCM_AMD_CAPTURE_ONE=1 timeout -k 10 300 $PY tests/test_gpu_refhost.py -k "ref-0-4-0-0-0 or 6-0-0 or throughput" > $O/refhost_m4_one.log 2>&1 ;;
     refhost_tp) timeout -k 10 300 $PY tests/test_gpu_refhost.py -k "throughput" > $O/refhost_tp.log 2>&1 ;;
     refhost_all) timeout -k 10 600 $PY tests/test_gpu_refhost.py > $O/refhost_all.log 2>&1 ;;
     parity) timeout -k 10 500 $PY -x tests/test_gpu_llc.py tests/test_gpu_ocean90.py tests/test_gpu_cs32x15.py > $O/parity.log 2>&1 ;;
+    auto_policy) timeout -k 10 400 $PY tests/test_gpu_parallel.py -k "auto" > $O/auto_policy.log 2>&1 ;;
     all_gpu) timeout -k 10 1000 $PY tests -m gpu > $O/all_gpu.log 2>&1 ;;
     cg_lb) bash profiles/cg_lb.sh $T/cg_lb > $O/cg_lb.log 2>&1 ;;
     bench) bash profiles/r5_check.sh $T/bench bench > $O/bench.log 2>&1 ;;

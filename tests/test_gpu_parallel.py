@@ -50,7 +50,7 @@ def _worker(rank, world, port, cfg, nsteps, q, cg2d="replicated", overlap="therm
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         torch.cuda.set_device(0)
-        dev_cg = cg2d == "device"
+        dev_cg = cg2d in ("device", "auto")
         m = _make(cfg, dev_cg)
         if pre_solve and rank == 0:
             # a multi-workgroup solve on this rank only before the block is shared: its launch
@@ -64,7 +64,8 @@ def _worker(rank, world, port, cfg, nsteps, q, cg2d="replicated", overlap="therm
         m.sync()
         full = {n: sm.gather_field(n) for n in FIELDS}
         stats = [m.solve_stats(back=b) for b in range(nsteps)]
-        res = {"t0": sm.t0, "nT": sm.nT, "stats": stats, "overlap": sm.overlap, "fork": sm.fork}
+        res = {"t0": sm.t0, "nT": sm.nT, "stats": stats, "overlap": sm.overlap, "fork": sm.fork, "cg2d": sm.cg2d,
+               "cg2d_reason": sm.cg2d_reason}
         if cg2d == "distributed":
             res["iters"] = list(sm.cg_iters)
         if cg2d in ("distributed", "device") and rank == 0 and keep_full:
@@ -254,3 +255,17 @@ def test_device_cg2d_after_unshared_solve():
     for rank, r in out.items():
         assert r["stats"] == r0["ref_stats"], (rank, r["stats"], r0["ref_stats"])
     assert all(s["cg2d_iters"] > 0 for s in r0["stats"])
+
+
+@pytest.mark.parametrize("cfg,world,want", [("cs32x15", 2, "replicated"), ("llc30", 2, "replicated")])
+def test_auto_cg2d_policy(cfg, world, want):
+    """cg2d="auto" (ShardedModel's default) on the multi-workgroup grids: the cost model
+    (parallel.cg2d_policy) picks the replicated solve across processes on C3 and the LLC, and
+    the run stays bit-identical to one process with the same solver."""
+    out = _spawn(cfg, world, 3, "auto")
+    r0 = out[0]
+    print("%s x%d cg2d=auto -> %s (%s)" % (cfg, world, r0["cg2d"], r0["cg2d_reason"]))
+    assert all(r["cg2d"] == want for r in out.values()), [r["cg2d"] for r in out.values()]
+    assert all(r0["equal"].values()), r0["diff"]
+    for rank, r in out.items():
+        assert r["stats"] == r0["ref_stats"], (rank, r["stats"], r0["ref_stats"])

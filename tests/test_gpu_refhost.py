@@ -249,7 +249,8 @@ def test_refhost_dropin_throughput(io, register, models, tmp_path):
 
 
 # BASELINE config 3 through the drop-ins: verification/global_ocean.cs32x15 on the reference's
-# own code/SIZE.h (12 tiles of 32 x 16, OL = 4) under pkg/exch2.  The harness is built against
+# own code/SIZE.h (12 tiles of 32 x 16, OL = 4) under pkg/exch2, and on six 32 x 32 tiles (one per
+# face, layout "cs32_6t": the device's bench layout).  The harness is built against
 # the experiment's headers (build_refhost.py layout "cs32": W2_EXCH2_SIZE.h, staggerTimeStep,
 # no CD code) and fills the W2_EXCH2_TOPOLOGY.h COMMON blocks as W2_E2SETUP leaves them
 # (W2's default topology: no data.exch2); MGCM_AMD_EXCH2_MAPS hands those arrays to the
@@ -258,9 +259,9 @@ def test_refhost_dropin_throughput(io, register, models, tmp_path):
 # staggered order (DO_STAGGER_FIELDS_EXCHANGES, then THERMODYNAMICS after the continuity
 # step).  The experiment's namelists with nIter0 = 0 (a cold start: the reference tree does
 # not hold pickup.0000072000) and taveFreq = 0 (pkg/timeave: refused by the mirror).  Bar: the
-# state after 4 steps, with the 12 tiles on 1, 2, 3 and 6 device models (and eager, and the
+# state after 4 steps, with the tiles on 1, 2, 3 and 6 device models (and eager, and the
 # device-sharded CG2D), is bit-identical to configs.global_ocean_cs32x15's
-# mgcm_forward_step.
+# mgcm_forward_step on the same tiling.
 CS32_DIR = os.path.join(ROOT, "tests", "golden", "global_ocean.cs32x15", "input")
 
 
@@ -277,20 +278,23 @@ def _cs32_namelists(dst):
     return dst
 
 
-@pytest.mark.parametrize("models,mwg,eager", [(1, 0, 0), (1, 0, 1), (2, 0, 0), (3, 0, 0), (6, 0, 1), (6, 0, 0), (3, 1, 0)])
-def test_refhost_cs32_exch2_bitexact(models, mwg, eager, tmp_path):
+@pytest.mark.parametrize("layout,models,mwg,eager", [
+    ("cs32", 1, 0, 0), ("cs32", 1, 0, 1), ("cs32", 2, 0, 0), ("cs32", 3, 0, 0), ("cs32", 6, 0, 1), ("cs32", 6, 0, 0),
+    ("cs32", 3, 1, 0), ("cs32_6t", 1, 0, 0), ("cs32_6t", 2, 0, 0), ("cs32_6t", 3, 0, 0), ("cs32_6t", 6, 0, 0)])
+def test_refhost_cs32_exch2_bitexact(layout, models, mwg, eager, tmp_path):
     from mitgcm_amd import configs
-    exe = os.path.join(RH, "refhost_cs32")
+    exe = os.path.join(RH, "refhost_" + layout)
     assert os.path.exists(exe), "refhost not built (mitgcm_amd/fortran/build_refhost.py, __graft_entry__.build())"
     nsteps = 4
+    sNy = 16 if layout == "cs32" else 32
 
     def cfg():
-        g, params, state, forcing = configs.global_ocean_cs32x15(sNy=16)
+        g, params, state, forcing = configs.global_ocean_cs32x15(sNy=sNy)
         if mwg:
             params["cg2dForceMwg"] = 1
         return g, params, state, forcing
     m = configs.make_model(cfg)
-    assert (m.g.nSx, m.g.nSy, m.g.sNx, m.g.sNy, m.g.OLx) == (12, 1, 32, 16, 4)
+    assert (m.g.nSx, m.g.nSy, m.g.sNx, m.g.sNy, m.g.OLx) == (12 if sNy == 16 else 6, 1, 32, sNy, 4)
     pdir = _cs32_namelists(str(tmp_path / "input"))
     w2 = m.g.topo.w2_arrays(ldNb=8, ldT=2 * m.g.nTiles)   # W2_EXCH2_SIZE.h: W2_maxNeighbours, W2_maxNbTiles
     state = _write_blob(tmp_path / "refhost_in.bin", m, nsteps, monitor_days=2, w2=w2, undef=("ALLOW_CD_CODE",))
@@ -308,13 +312,13 @@ def test_refhost_cs32_exch2_bitexact(models, mwg, eager, tmp_path):
     bad = [(n, float(np.abs(out[n] - m.get(n).reshape(-1)[:out[n].size]).max())) for n in CHECK
            if n in out and not np.array_equal(out[n], m.get(n).reshape(-1)[:out[n].size])]
     m.close()
-    rec = {"layout": "cs32", "models": models, "cg2dForceMwg": mwg, "eager": eager,
+    rec = {"layout": layout, "models": models, "cg2dForceMwg": mwg, "eager": eager,
            "dropin_ms_per_step_mean": 1e3 * st["seconds"] / max(1, st["steps_timed"]),
            "dropin_ms_per_step_no_download": st["step_ms"][2], "graph_ms_per_step": graph_ms, "mirror": st,
            "state_fields": len(state)}
-    print("refhost cs32 models=%d mwg=%d eager=%d: %s" % (models, mwg, eager, json.dumps(rec)))
+    print("refhost %s models=%d mwg=%d eager=%d: %s" % (layout, models, mwg, eager, json.dumps(rec)))
     if os.path.isdir(os.path.join(ROOT, "gpurun_out")):
-        with open(os.path.join(ROOT, "gpurun_out", "refhost_cs32_m%d_w%d_e%d.json" % (models, mwg, eager)), "w") as f:
+        with open(os.path.join(ROOT, "gpurun_out", "refhost_%s_m%d_w%d_e%d.json" % (layout, models, mwg, eager)), "w") as f:
             json.dump(rec, f)
     assert not bad, bad
     assert len([n for n in CHECK if n in out]) >= 18
