@@ -259,11 +259,11 @@ def pmc_traffic(path, kernel_keys):
 def default_pmc_summary(config):
     """The newest committed PMC summary of this workload (profiles/r0N/<tag>/)."""
     tag = PMC_TAG.get(config, config)
-    for rnd in ("r04", "r03", "r02"):
+    for rnd in ("r05", "r04", "r03", "r02"):
         p = os.path.join(ROOT, "profiles", rnd, tag, "pmc_summary.json")
         if os.path.exists(p):
             return p
-    return os.path.join(ROOT, "profiles", "r04", tag, "pmc_summary.json")
+    return os.path.join(ROOT, "profiles", "r05", tag, "pmc_summary.json")
 
 
 def stream_triad_gbs(device, n=64 << 20, reps=8):

@@ -10,6 +10,7 @@ MODE=${MODE:-all}
 CONFIG=${CONFIG:-global_ocean.90x40x15}
 TAG=${TAG:-ocean90}
 BENCH_ARGS=${BENCH_ARGS:-"--steps 200 --warmup 20"}
+PMC_ARGS=${PMC_ARGS:-}   # extra bench arguments of the PMC passes (round 5: --no-cs32)
 PT=${PT:-tests}
 O=gpurun_out/$TAG
 mkdir -p $O
@@ -25,8 +26,8 @@ if [ "$MODE" = bench ] || [ "$MODE" = all ] || [ "$MODE" = prof ]; then
 fi
 if [ "$MODE" = prof ] || [ "$MODE" = all ]; then
   timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $O/prof -o run --output-format csv -- python3 bench.py --config $CONFIG $BENCH_ARGS --no-cpu-baseline > $O/prof_bench.json 2> $O/prof.err || { echo rocprof failed; tail -30 $O/prof.err; exit 1; }
-  timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE -d $O/pmc_fetch -o run --output-format csv -- python3 bench.py --config $CONFIG --steps 20 --warmup 2 --no-cpu-baseline > $O/pmc_fetch.json 2> $O/pmc_fetch.err || { echo pmc fetch failed; tail -30 $O/pmc_fetch.err; exit 1; }
-  timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE -d $O/pmc_write -o run --output-format csv -- python3 bench.py --config $CONFIG --steps 20 --warmup 2 --no-cpu-baseline > $O/pmc_write.json 2> $O/pmc_write.err || { echo pmc write failed; tail -30 $O/pmc_write.err; exit 1; }
+  timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE -d $O/pmc_fetch -o run --output-format csv -- python3 bench.py --config $CONFIG --steps 20 --warmup 2 --no-cpu-baseline $PMC_ARGS > $O/pmc_fetch.json 2> $O/pmc_fetch.err || { echo pmc fetch failed; tail -30 $O/pmc_fetch.err; exit 1; }
+  timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE -d $O/pmc_write -o run --output-format csv -- python3 bench.py --config $CONFIG --steps 20 --warmup 2 --no-cpu-baseline $PMC_ARGS > $O/pmc_write.json 2> $O/pmc_write.err || { echo pmc write failed; tail -30 $O/pmc_write.err; exit 1; }
   if [ -x tools/pmc_calib ]; then
     timeout -s KILL 60 rocprofv3 --pmc FETCH_SIZE -d $O/calib_fetch -o run --output-format csv -- tools/pmc_calib > $O/calib.log 2>&1 || { echo calib fetch failed; tail $O/calib.log; exit 1; }
     timeout -s KILL 60 rocprofv3 --pmc WRITE_SIZE -d $O/calib_write -o run --output-format csv -- tools/pmc_calib >> $O/calib.log 2>&1 || { echo calib write failed; tail $O/calib.log; exit 1; }
