@@ -63,12 +63,15 @@ def test_library_exports_every_header_symbol():
     assert declared == set(_lib.EXPORTS)
 
 
-def _w2_maps(topo):
+def _w2_maps(topo, ldNb=None, ldT=None, mutate=None, want_rc=0):
     """mgcm_exch2_maps (the library's derivation from the W2_EXCH2_TOPOLOGY.h arrays, host
-    only) on the arrays of an exch2.py topology."""
+    only) on the arrays of an exch2.py topology (at leading dimensions ldNb, ldT; mutate(a)
+    edits them first)."""
     import ctypes
     from mitgcm_amd._lib import lib
-    a = topo.w2_arrays()
+    a = topo.w2_arrays(ldNb, ldT)
+    if mutate:
+        mutate(a)
     IP = lambda x: np.ascontiguousarray(x, dtype=np.int32).ctypes.data_as(ctypes.POINTER(ctypes.c_int))
     keep = {k: np.ascontiguousarray(v, dtype=np.int32) for k, v in a.items() if k.startswith("exch2_")}
     N = topo.nTiles_ * topo.n2
@@ -79,7 +82,7 @@ def _w2_maps(topo):
                               "exch2_pij", "exch2_oi", "exch2_oj", "exch2_iLo", "exch2_iHi", "exch2_jLo", "exch2_jHi")]
     rc = lib().mgcm_exch2_maps(topo.sNx, topo.sNy, topo.OLx, topo.nTiles_, a["ldNb"], a["ldT"],
                                *[IP(x) for x in args], *[LP(x) for x in out])
-    assert rc == 0
+    assert rc == want_rc
     return out
 
 
@@ -116,3 +119,28 @@ def test_w2_default_cube_topology_pinned(out):
     w2 = topo.w2_arrays()
     got = [list(w2["exch2_neighbourId"][t, :w2["exch2_nNeighbours"][t]]) for t in range(topo.nTiles_)]
     assert got == fx["neighbours"]
+
+
+def test_exch2_maps_padded_and_refused():
+    """The Fortran mirror passes the W2 arrays at their declared leading dimensions
+    (W2_maxNeighbours = 8, W2_maxNbTiles = 2 x the tiles): the maps are those of the unpadded
+    arrays.  Inconsistent arrays -- a neighbour id or opposing connection out of range, more
+    neighbours than the leading dimension -- are refused (-1), so MGCM_AMD_SET_W2 stops with
+    ABNORMAL END instead of setting wrong maps."""
+    from mitgcm_amd import exch2
+    topo = exch2.cube_topology(32, 32, 16, 4)
+    base = _w2_maps(topo)
+    padded = _w2_maps(topo, ldNb=8, ldT=2 * topo.nTiles_)
+    for x, y in zip(base, padded):
+        assert np.array_equal(x, y)
+
+    def bad_id(a):
+        a["exch2_neighbourId"][0, 0] = topo.nTiles_ + 1
+
+    def bad_opp(a):
+        a["exch2_opposingSend"][1, 0] = 9
+
+    def bad_count(a):
+        a["exch2_nNeighbours"][2] = a["ldNb"] + 1
+    for m in (bad_id, bad_opp, bad_count):
+        _w2_maps(topo, mutate=m, want_rc=-1)
