@@ -263,8 +263,8 @@ struct mgcm_model {
   double *thetaA = nullptr, *saltA = nullptr;
   int stepLayout = 0;   // one_step's launch layout (mgcm_get_param "stepLayout")
   // THERMODYNAMICS of a sharded step on the second stream (mgcm_step_phase 16): 1 forked after
-  // DO_OCEANIC_PHYS (joined before UPDATE_R_STAR), 2 to fork after DYNAMICS, 3 forked after
-  // DYNAMICS (joined before the correction step), 0 none pending
+  // DO_OCEANIC_PHYS (joined before UPDATE_R_STAR), 2 to fork after CALC_DIV_GHAT, 3 forked
+  // after it (joined before the correction step), 0 none pending
   int shardFork = 0;
   // mgcm_put_batch_async: two pinned host slots (each with the event of its last copy) and
   // one device buffer; a batch travels as [header | values] in one copy, then one scatter
@@ -1610,10 +1610,11 @@ static int one_step(mgcm_model *m) {
   // what THERMODYNAMICS reads or writes (no r* rewrite of hFac; SOLVE_FOR_PRESSURE and CG2D
   // read gU, gV, hFac and eta, write the solver's vectors and etaN), so the tracers may run
   // beside the pressure solve too and join before MOMENTUM_CORRECTION_STEP rewrites u, v, w.
-  // The fork comes after DYNAMICS (beside SOLVE_FOR_PRESSURE: the pressure solve leaves most
-  // CUs idle while DYNAMICS, alone, has the chip), under the linear free surface only.
-  // LLC-90 (profiles/r03/thermo_at/): 1.98 ms forked after DO_OCEANIC_PHYS, 1.86 after
-  // DYNAMICS, 1.88 after CALC_DIV_GHAT (round 5 removed the two slower placements)
+  // The fork comes after CALC_DIV_GHAT (beside the CG2D: the pressure solve leaves most CUs
+  // idle while DYNAMICS and CALC_DIV_GHAT, alone, have the chip), under the linear free
+  // surface only.  LLC-90 round 3 (profiles/r03/thermo_at/): 1.98 ms forked after
+  // DO_OCEANIC_PHYS, 1.86 after DYNAMICS, 1.88 after CALC_DIV_GHAT; round 5, with the faster
+  // solve, after CALC_DIV_GHAT wins (below)
   const bool lateJoin = fork && m->p.nonlinFreeSurf <= 0;
   const bool thermoLate = lateJoin;
   // With the late join (THERMODYNAMICS beside the pressure solve) the new tracers' halos are
@@ -1676,7 +1677,7 @@ static int one_step(mgcm_model *m) {
   m->stepLayout = (dtFused ? 1 : 0) | (physPhi ? 2 : 0) | (forkable && !dtFused ? 4 : 0) |
                   ((forkable && m->p.nonlinFreeSurf <= 0) || tcg ? 8 : 0);
   // GMREDI_CALC_TENSOR beside CALC_PHI_HYD (launch_gm_phi) where THERMODYNAMICS, its reader,
-  // runs after DYNAMICS (staggered, or forked after DYNAMICS) and the fold does not apply
+  // runs after DYNAMICS (staggered, or forked after CALC_DIV_GHAT) and the fold does not apply
   const bool gmPhi = (stagger || thermoLate) && !dtFused && !physPhi && !m->timing && gm_phi_fusable(m->d, m->p);
   auto phys = [&]() -> int {
     if (physPhi) TIMED(K_PHYS, launch_phys_phi(m->d, m->p, m->f, m->d_ctr, m->stream));
@@ -1710,7 +1711,7 @@ static int one_step(mgcm_model *m) {
       TIMED(K_PHI, launch_gm_phi(m->d, m->p, m->f, m->stream));
       TIMED(K_MOM, launch_mom_step(m->d, m->p, m->f, m->d_ctr, m->stream, !ringAside));
     } else if (dynamics_on(m, !ringAside)) return -1;
-    if (thermoLate && fork_thermo()) return -1;
+    // (the late fork comes after CALC_DIV_GHAT, below)
     if (tcgFork) HIPCHK(hipStreamWaitEvent(m->stream, m->evSnap, 0));   // the copy before hFac is rewritten
     else if (fork && !lateJoin && !dtFused) HIPCHK(hipStreamWaitEvent(m->stream, m->evJoin, 0));
     // forward_step.F:829-877: UPDATE_R_STAR(.TRUE.) + UPDATE_CG2D
@@ -1721,6 +1722,10 @@ static int one_step(mgcm_model *m) {
     if (m->p.nonlinFreeSurf > 0)
       TIMED(K_RSTAR, update_r_star_cg2d(m, sfpFused, opEarly, false));
     if (!sfpFused) TIMED(K_RHS, launch_sfp_rhs(m->d, m->p, m->f, m->stream));
+    // the late fork: THERMODYNAMICS beside the CG2D only, CALC_DIV_GHAT (an HBM stream, on the
+    // critical path) alone before it -- LLC-90 1.528-1.532 -> 1.474-1.476 ms/step, alternating
+    // on one box (profiles/r05/thermo_at/); the tracers still finish inside the solve
+    if (thermoLate && fork_thermo()) return -1;
     const bool etaFused = mg_fuse_on(MG_FUSE_ETA) && cg2d_fuses_eta(m);
     TIMED(K_CG2D, launch_cg2d(m, m->p.cg2dMaxIters, m->p.cg2dUseMinResSol - 1, etaFused));
     // Under exactConserv the etaN of EXCH_XY_RL(cg2d_x) + etaN = recip_Bo*cg2d_x
@@ -2192,13 +2197,14 @@ int mgcm_step_phase(mgcm_model *m, int phase) {
     case 9: {   // DYNAMICS, UPDATE_R_STAR + UPDATE_CG2D, CALC_DIV_GHAT
       const bool ringAside = m->shardFork == 2 && mom_ring_separable(m->d, m->p) && mg_fuse_on(MG_FUSE_RING);
       if (dynamics_on(m, !ringAside)) return -1;
-      if (m->shardFork == 2) {
+      if (m->shardFork == 1 && shard_join_thermo(m)) return -1;
+      if (m->p.nonlinFreeSurf > 0) TIMED(K_RSTAR, update_r_star_cg2d(m));
+      TIMED(K_RHS, launch_sfp_rhs(m->d, m->p, m->f, m->stream));
+      if (m->shardFork == 2) {   // after CALC_DIV_GHAT, as one_step forks it
         if (shard_fork_thermo(m, ringAside)) return -1;
         m->shardFork = 3;
         m->mwg.exclusive = 1;   // the multi-workgroup CG2D keeps its CUs while the tracers run
-      } else if (m->shardFork == 1 && shard_join_thermo(m)) return -1;
-      if (m->p.nonlinFreeSurf > 0) TIMED(K_RSTAR, update_r_star_cg2d(m));
-      TIMED(K_RHS, launch_sfp_rhs(m->d, m->p, m->f, m->stream));
+      }
       return 0;
     }
     case 2:

@@ -19,6 +19,9 @@ for s in "$@"; do
     refhost_all) timeout -k 10 600 $PY tests/test_gpu_refhost.py > $O/refhost_all.log 2>&1 ;;
     parity) timeout -k 10 500 $PY -x tests/test_gpu_llc.py tests/test_gpu_ocean90.py tests/test_gpu_cs32x15.py > $O/parity.log 2>&1 ;;
     auto_policy) timeout -k 10 400 $PY tests/test_gpu_parallel.py -k "auto" > $O/auto_policy.log 2>&1 ;;
+    parallel) timeout -k 10 1000 $PY tests/test_gpu_parallel.py tests/test_gpu_rccl.py > $O/parallel.log 2>&1 ;;
+    llc) timeout -k 10 500 $PY -x tests/test_gpu_llc.py > $O/llc.log 2>&1 ;;
+    bench_llc) timeout -k 10 300 python bench.py --config llc90_synthetic --steps 30 --warmup 4 --no-cs32 --no-cpu-baseline > $O/bench_llc.json 2> $O/bench_llc.err; tail -c 300 $O/bench_llc.json ;;
     all_gpu) timeout -k 10 1000 $PY tests -m gpu > $O/all_gpu.log 2>&1 ;;
     cg_lb) bash profiles/cg_lb.sh $T/cg_lb > $O/cg_lb.log 2>&1 ;;
     bench) bash profiles/r5_check.sh $T/bench bench > $O/bench.log 2>&1 ;;

@@ -1,0 +1,18 @@
+#!/bin/bash
+# Round-5 A/B: THERMODYNAMICS forked after DYNAMICS (default) or after CALC_DIV_GHAT
+# (MGCM_THERMO_AFTER_RHS=1) on LLC-90, alternating, then the LLC parity tests with the latter.
+#   bash profiles/thermo_at.sh <out-tag>
+set -o pipefail
+cd "$GRAFT_REPO_ROOT" 2>/dev/null || cd /root/repo
+export TMPDIR=/tmp
+O=gpurun_out/$1
+mkdir -p $O
+for v in 0 1 0 1 0 1; do
+  MGCM_THERMO_AFTER_RHS=$v timeout -k 10 200 python bench.py --config llc90_synthetic --steps 40 --warmup 4 --no-cs32 \
+    --no-cpu-baseline > $O/bench_$v.json 2> $O/bench_$v.err || { tail -20 $O/bench_$v.err; exit 1; }
+  python -c "
+import json; d=json.loads(open('$O/bench_$v.json').read().strip().splitlines()[-1])
+print('after_rhs=$v', round(d['ms_per_step'],4), d['kernel_ms_mean'].get('cg2d'), d['kernel_ms_mean'].get('sfp_rhs'))"
+done
+MGCM_THERMO_AFTER_RHS=1 timeout -k 10 500 python -u -m pytest -x -q --timeout 400 --timeout-method thread tests/test_gpu_llc.py \
+  > $O/llc_parity.log 2>&1; tail -2 $O/llc_parity.log
