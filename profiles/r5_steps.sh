@@ -22,6 +22,7 @@ for s in "$@"; do
     parallel) timeout -k 10 1000 $PY tests/test_gpu_parallel.py tests/test_gpu_rccl.py > $O/parallel.log 2>&1 ;;
     llc) timeout -k 10 500 $PY -x tests/test_gpu_llc.py > $O/llc.log 2>&1 ;;
     bench_llc) timeout -k 10 300 python bench.py --config llc90_synthetic --steps 30 --warmup 4 --no-cs32 --no-cpu-baseline > $O/bench_llc.json 2> $O/bench_llc.err; tail -c 300 $O/bench_llc.json ;;
+    vi_gl) bash profiles/vi_gl.sh $T/vi_gl > $O/vi_gl.log 2>&1 ;;
     all_gpu) timeout -k 10 1000 $PY tests -m gpu > $O/all_gpu.log 2>&1 ;;
     cg_lb) bash profiles/cg_lb.sh $T/cg_lb > $O/cg_lb.log 2>&1 ;;
     bench) bash profiles/r5_check.sh $T/bench bench > $O/bench.log 2>&1 ;;
