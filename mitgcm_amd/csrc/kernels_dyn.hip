@@ -1829,16 +1829,15 @@ static VIP<C> vi_params(const Params &p) {
 // Accessor of k_mom_vi_m2.  OWN: the output point (i,j), whose column's k-1 / k+1 values of
 // u, v, hFacW, hFacS sit in registers and whose own 2-D metrics in VIMarchRegs; !OWN: the
 // ring-point intermediates, which read level k only (no own-point selects at all).
-template <int BX, int BY, class P, bool OWN, int HR = 2, int EWT = BX + 2>
-struct VIM2 {   // HR: slots of the hFacC / wVel level rings (level kk in slot kk % HR); EWT: extent
-                // row width, sh: the block's extent starts sh columns before i0 - 1 (GL staging)
-  static constexpr int EW = EWT, IW = BX + 1;
-  const Dims &d; const P &p; const Fields &f; int k, t, i0, j0, i, j, sh;
+template <int BX, int BY, class P, bool OWN, int HR = 2>
+struct VIM2 {   // HR: slots of the hFacC / wVel level rings (level kk in slot kk % HR)
+  static constexpr int EW = BX + 2, IW = BX + 1;
+  const Dims &d; const P &p; const Fields &f; int k, t, i0, j0, i, j;
   const double *sU, *sV, *sHW, *sHS, *sHC, *sW, *s2;
   const double *sKE, *sVort, *sHfz, *sH0fz, *sHDiv;
   const VIMarchRegs &c;
   double uM, uP, vM, vP, hwM, hwP, hsM, hsP;
-  __device__ __forceinline__ int e(int ii, int jj) const { return (jj - j0 + 1) * EW + (ii - i0 + 1) + sh; }
+  __device__ __forceinline__ int e(int ii, int jj) const { return (jj - j0 + 1) * EW + (ii - i0 + 1); }
   __device__ __forceinline__ long g(int ii, int jj, int kk) const { return MG_I3(d, ii, jj, kk, t); }
   __device__ __forceinline__ double lvl(const double *sl, double m_, double p_, int ii, int jj, int kk) const {
     if constexpr (OWN) {
@@ -1914,31 +1913,20 @@ struct VIM2 {   // HR: slots of the hFacC / wVel level rings (level kk in slot k
   do {              \
   } while (0)
 #endif
-// GL: the extent of level k+1 (u, v, hFacW, hFacS, hFacC; wVel of k+2) staged by LDS-DMA
-// (global_load_lds, 16 bytes = two adjacent points per lane) issued at the start of level k into
-// a second set of LDS slots (u, v, hFacW, hFacS: level parity; hFacC, wVel: rings of three), so
-// no register holds it and nothing waits for it until the level's closing barrier.  An extent
-// row is EWG doubles from the column ib = i0 - 1 - sh at or before i0 - 1 whose element sits at
-// an even flat index (16-byte aligned: vi_m2_gl_ok); pairs reaching outside the tile's halo are
-// written by ordinary stores (zeros where the point is outside, as the register path's stash).
-template <int BX, int BY, unsigned C, bool PF, bool CREG, bool EARLY, int LBW, bool GL = false>
+template <int BX, int BY, unsigned C, bool PF, bool CREG, bool EARLY, int LBW>
 __global__ void __launch_bounds__(VT_NT, LBW) k_mom_vi_m2(Dims d, VIP<C> p, Fields f, const int *iterPtr, int nbx, int nby,
                                                       int KC, int nkc) {
   using P = VIP<C>;
-  constexpr int EWG = (BX + 4) & ~1, PR = EWG / 2, NPAIR = PR * (BY + 2);
-  constexpr int EW = GL ? EWG : BX + 2, EN = EW * (BY + 2), IW = BX + 1, IN = (BX + 1) * (BY + 1);
+  constexpr int EW = BX + 2, EN = (BX + 2) * (BY + 2), IW = BX + 1, IN = (BX + 1) * (BY + 1);
   constexpr int NR = (EN + VT_NT - 1) / VT_NT;   // extent elements per thread
-  constexpr int NB4 = GL ? 2 : 1, HR = GL ? 3 : 2;   // slots of u/v/hFacW/hFacS and of hFacC/wVel
-  static_assert(BX * BY <= VT_NT && EN <= 2 * VT_NT && (!GL || NPAIR <= VT_NT), "block shape");
-  __shared__ __attribute__((aligned(16))) double sU[NB4 * EN], sV[NB4 * EN], sHW[NB4 * EN], sHS[NB4 * EN];
-  __shared__ __attribute__((aligned(16))) double sHC[HR * EN], sW[HR * EN];
+  static_assert(BX * BY <= VT_NT && EN <= 2 * VT_NT, "block shape");
+  __shared__ double sU[EN], sV[EN], sHW[EN], sHS[EN], sHC[2 * EN], sW[2 * EN];
   __shared__ double s2[VM_S2 * EN];
   __shared__ double sKE[IN], sVort[IN], sHfz[IN], sH0fz[IN], sHDiv[IN];
   const int nb = nbx * nby, lb = mg_xcd_block();
   const int t = d.t0 + lb / (nb * nkc), bxy = lb % nb, kb = 1 + ((lb / nb) % nkc) * KC;
   const int Nr = d.Nr, ke = kb + KC - 1 < Nr ? kb + KC - 1 : Nr;
   const int i0 = (bxy % nbx) * BX, j0 = (bxy / nbx) * BY;
-  const int sh = GL ? ((i0 - 1 + d.OLx - 1) & 1) : 0, ib = i0 - 1 - sh;   // the extent's first column
   const int tid = threadIdx.x;
   const int i = i0 + tid % BX, j = j0 + tid / BX;
   const bool act = tid < BX * BY && i <= d.sNx + 1 && j <= d.sNy + 1;
@@ -1949,7 +1937,7 @@ __global__ void __launch_bounds__(VT_NT, LBW) k_mom_vi_m2(Dims d, VIP<C> p, Fiel
 #pragma unroll
   for (int r = 0; r < NR; r++) {
     const int ee = tid + r * VT_NT;
-    const int ii = ib + ee % EW, jj = j0 - 1 + ee / EW;
+    const int ii = i0 - 1 + ee % EW, jj = j0 - 1 + ee / EW;
     ein[r] = ee < EN && ii <= d.sNx + d.OLx && jj <= d.sNy + d.OLy;
     eq[r] = MG_I2(d, ein[r] ? ii : 1, ein[r] ? jj : 1, t);
   }
@@ -2020,66 +2008,22 @@ __global__ void __launch_bounds__(VT_NT, LBW) k_mom_vi_m2(Dims d, VIP<C> p, Fiel
       if (ee < EN) sW[(kk & 1) * EN + ee] = (ein[r] && kk <= Nr) ? nW[r] : 0.0;
     }
   };
-  // GL: one field's extent of level kk into dst (this thread: the point pair of slots 2*tid, +1)
-  const int gRow = GL ? tid / PR : 0, gCol = GL ? ib + 2 * (tid - gRow * PR) : 0, gJ = j0 - 1 + gRow;
-  const bool gAct = GL && tid < NPAIR;
-  const bool gIn0 = gAct && gCol <= d.sNx + d.OLx && gJ <= d.sNy + d.OLy;
-  const bool gIn1 = gAct && gCol + 1 <= d.sNx + d.OLx && gJ <= d.sNy + d.OLy;
-  // byte offset of the pair's first point at level 1 (a point inside the tile where it is not)
-  const unsigned gOb = (unsigned)(MG_I3(d, gIn0 ? gCol : 1, gIn0 ? gJ : 1, 1, t) * 8);
-  auto gl_issue = [&](double *dst, const char *base, int kk) {
-    if constexpr (GL) {
-      if (!gAct) return;
-      const double *src = (const double *)(base + gOb + (unsigned)(kk - 1) * lvB);
-      if (gIn1) {
-        __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void *)src,
-                                         (__attribute__((address_space(3))) void *)(dst + (tid >> 6) * 128), 16, 0, 0);
-      } else {   // the halo's edge: as the register path's stash
-        dst[2 * tid] = gIn0 ? src[0] : 0.0;
-        dst[2 * tid + 1] = 0.0;
-      }
-    }
-  };
-  auto gl_level = [&](int kk) {   // u, v, hFacW, hFacS, hFacC of level kk
-    gl_issue(sU + (kk & 1) * EN, bU, kk);
-    gl_issue(sV + (kk & 1) * EN, bV, kk);
-    gl_issue(sHW + (kk & 1) * EN, bHW, kk);
-    gl_issue(sHS + (kk & 1) * EN, bHS, kk);
-    gl_issue(sHC + (kk % 3) * EN, bHC, kk);
-  };
-  auto gl_w = [&](int kk) {   // wVel of level kk (0 below the bottom)
-    if (kk <= Nr) gl_issue(sW + (kk % 3) * EN, bW, kk);
-    else
-      for (int ee = tid; ee < EN; ee += VT_NT) sW[(kk % 3) * EN + ee] = 0.0;
-  };
   double uM = 0.0, vM = 0.0, hwM = 0.0, hsM = 0.0;
-  if constexpr (GL) {
-    if (kb > 1) {
-      const unsigned o = ob + (unsigned)(kb - 2) * lvB;
-      uM = ld(bU, o); vM = ld(bV, o); hwM = ld(bHW, o); hsM = ld(bHS, o);
-      gl_issue(sHC + ((kb - 1) % 3) * EN, bHC, kb - 1);
-    }
-    gl_level(kb);
-    gl_w(kb);
-    gl_w(kb + 1);
-    __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0): this wave's LDS-DMA landed (the barrier below)
-  } else {
-    if (kb > 1) {
-      fetch(kb - 1);
-      uM = oU; vM = oV; hwM = oHW; hsM = oHS;
+  if (kb > 1) {
+    fetch(kb - 1);
+    uM = oU; vM = oV; hwM = oHW; hsM = oHS;
 #pragma unroll
-      for (int r = 0; r < NR; r++) {
-        const int ee = tid + r * VT_NT;
-        if (ee < EN) sHC[((kb - 1) & 1) * EN + ee] = ein[r] ? nHC[r] : 0.0;
-      }
+    for (int r = 0; r < NR; r++) {
+      const int ee = tid + r * VT_NT;
+      if (ee < EN) sHC[((kb - 1) & 1) * EN + ee] = ein[r] ? nHC[r] : 0.0;
     }
-    fetchW(kb);
-    stashW(kb);
-    fetchW(kb + 1 <= Nr ? kb + 1 : Nr);
-    stashW(kb + 1);
-    fetch(kb);
-    stash(kb);
   }
+  fetchW(kb);
+  stashW(kb);
+  fetchW(kb + 1 <= Nr ? kb + 1 : Nr);
+  stashW(kb + 1);
+  fetch(kb);
+  stash(kb);
   const int myIter = *iterPtr;
   const double abFac = (myIter == p.nIter0 && p.nIter0 == 0) ? 0.0 : 0.5 + p.abEps;   // adams_bashforth2.F:61-65
   const double mass2rUnit = 1.0 / p.rhoConst;
@@ -2107,12 +2051,6 @@ __global__ void __launch_bounds__(VT_NT, LBW) k_mom_vi_m2(Dims d, VIP<C> p, Fiel
     if constexpr (!CREG) load_c(c1, q2);
     const VIMarchRegs &c = CREG ? c0 : c1;
     const int kn = k + 1 <= Nr ? k + 1 : Nr, kw = k + 2 <= Nr ? k + 2 : Nr;
-    if constexpr (GL) {   // level k+1's extent (wVel: k+2) in flight through the whole level
-      if (k < ke) {
-        gl_level(k + 1);
-        gl_w(k + 2);
-      }
-    }
     if constexpr (PF) {
       fetch(kn);
       fetchW(kw);
@@ -2129,12 +2067,10 @@ __global__ void __launch_bounds__(VT_NT, LBW) k_mom_vi_m2(Dims d, VIP<C> p, Fiel
       eGuo = AR3(guNm1, q3e); eGvo = AR3(gvNm1, q3e);
       if constexpr (!rscE) { ePhi0 = AR3(phiHydC, q3e); ePhiX = AR3(phiHydC, q3e - 1); ePhiY = AR3(phiHydC, q3e - d.nx); }
     }
-    const int lo = GL ? (k & 1) * EN : 0;   // this level's u/v/hFacW/hFacS slot
-    VIM2<BX, BY, P, true, HR, EW> a{d, p, f, k, t, i0, j0, i, j, sh, sU + lo, sV + lo, sHW + lo, sHS + lo, sHC, sW, s2,
-                                    sKE, sVort, sHfz, sH0fz, sHDiv, c, uM, k < Nr ? oU : 0.0, vM, k < Nr ? oV : 0.0, hwM,
-                                    k < Nr ? oHW : 0.0, hsM, k < Nr ? oHS : 0.0};
-    VIM2<BX, BY, P, false, HR, EW> ai{d, p, f, k, t, i0, j0, 0, 0, sh, sU + lo, sV + lo, sHW + lo, sHS + lo, sHC, sW, s2,
-                                      sKE, sVort, sHfz, sH0fz, sHDiv, c, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
+    VIM2<BX, BY, P, true> a{d, p, f, k, t, i0, j0, i, j, sU, sV, sHW, sHS, sHC, sW, s2, sKE, sVort, sHfz, sH0fz, sHDiv, c,
+                            uM, k < Nr ? oU : 0.0, vM, k < Nr ? oV : 0.0, hwM, k < Nr ? oHW : 0.0, hsM, k < Nr ? oHS : 0.0};
+    VIM2<BX, BY, P, false> ai{d, p, f, k, t, i0, j0, 0, 0, sU, sV, sHW, sHS, sHC, sW, s2, sKE, sVort, sHfz, sH0fz, sHDiv, c,
+                              0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
     for (int q = tid; q < IN; q += VT_NT) {
       const int ii = i0 + q % IW, jj = j0 + q / IW;          // vort / hFacZ grid: i0..i0+BX
       const bool ok = ii <= d.sNx + d.OLx && jj <= d.sNy + d.OLy;
@@ -2145,13 +2081,7 @@ __global__ void __launch_bounds__(VT_NT, LBW) k_mom_vi_m2(Dims d, VIP<C> p, Fiel
       sHDiv[q] = vi_hdiv(ai, d, p, f, ii - 1, jj - 1, k, t);
     }
     VI_STAMP(1);
-    if constexpr (GL) {   // the intermediates' LDS stores only: no vmcnt(0), the LDS-DMA stays in flight
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      __builtin_amdgcn_s_barrier();
-      asm volatile("" ::: "memory");
-    } else {
-      __syncthreads();
-    }
+    __syncthreads();
     VI_STAMP(2);
     if (act) {
       auto q3of = [&](long qq2, int kk) { return qq2 + (long)(kk - 1) * d.n2 + t3; };
@@ -2215,15 +2145,7 @@ __global__ void __launch_bounds__(VT_NT, LBW) k_mom_vi_m2(Dims d, VIP<C> p, Fiel
     VI_STAMP(3);
     }(iL, jL, q2L);
     if (k == ke) break;
-    if (act) {
-      const int eo = (j - j0 + 1) * EW + (i - i0 + 1) + sh + (GL ? (k & 1) * EN : 0);
-      uM = sU[eo]; vM = sV[eo]; hwM = sHW[eo]; hsM = sHS[eo];
-    }
-    if constexpr (GL) {
-      __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0): level k+1's LDS-DMA landed
-      __syncthreads();
-      continue;
-    }
+    if (act) { const int eo = (j - j0 + 1) * EW + (i - i0 + 1); uM = sU[eo]; vM = sV[eo]; hwM = sHW[eo]; hsM = sHS[eo]; }
     if constexpr (!PF) {
       fetch(k + 1 <= Nr ? k + 1 : Nr);
       fetchW(k + 2 <= Nr ? k + 2 : Nr);
@@ -2296,7 +2218,7 @@ constexpr unsigned VI_CODE_LLC = vi_code(1, 0, 0, 1, 1, 1, 0, 1, 1, 0, 1, 1, 1, 
 template <int BX, int BY, unsigned C, int V>
 static void vi_m2_one(const Dims &d, const VIP<C> &vp, const Fields &f, const int *iterPtr, int nbx, int nby, int KC,
                       int nkc, hipStream_t s) {
-  hipLaunchKernelGGL((k_mom_vi_m2<BX, BY, C, (V & 1) != 0, (V & 2) != 0, (V & 4) != 0, (V & 8) ? 2 : 1, (V & 16) != 0>),
+  hipLaunchKernelGGL((k_mom_vi_m2<BX, BY, C, (V & 1) != 0, (V & 2) != 0, (V & 4) != 0, (V & 8) ? 2 : 1>),
                      dim3((unsigned)(nbx * nby * d.nT * nkc)), dim3(VT_NT), 0, s, d, vp, f, iterPtr, nbx, nby, KC, nkc);
 }
 // k_mom_vi_m2 as launched: the output point's metrics held in registers across the march
@@ -2308,26 +2230,15 @@ static void vi_m2_one(const Dims &d, const VIP<C> &vp, const Fields &f, const in
 // profiles/r03/vi_m2/; the ring-point intermediates of the 31 x 8 block's second pass dealt
 // out by quantity over the four waves 459 -> 518 us, profiles/r04/llc_ab/).  false where the
 // run's option code or block shape has no instantiation (the generic march runs then).
-// The LDS-DMA staging (GL) needs 16-byte pairs: every level and row of a field starts at an
-// even flat index (even nx, n2, n3, N3all, a 16-byte-aligned arena) and the extent's first
-// column, one before i0 - 1 at most, inside the halo (OLx >= 3)
-static bool vi_m2_gl_ok(const Dims &d, const Fields &f) {
-  return (d.nx & 1) == 0 && (d.n2 & 1) == 0 && (d.n3 & 1) == 0 && (d.N3all & 1) == 0 &&
-         ((uintptr_t)f.a3 & 15u) == 0 && d.OLx >= 3 && d.OLy >= 2;
-}
 static bool vi_m2_launch(const Dims &d, const Params &p, const Fields &f, const int *iterPtr, int BX, int BY, int nbx,
                          int nby, int KC, int nkc, hipStream_t s) {
   const unsigned code = vi_opt_code(p);
-  static const int glEnv = getenv("MGCM_VI_GL") ? atoi(getenv("MGCM_VI_GL")) : 0;   // (A/B)
-  const bool gl = glEnv != 0 && vi_m2_gl_ok(d, f);
   if (code == VI_CODE_LLC && BX == 31 && BY == 8) {
-    if (gl) vi_m2_one<31, 8, VI_CODE_LLC, 30>(d, vi_params<VI_CODE_LLC>(p), f, iterPtr, nbx, nby, KC, nkc, s);
-    else vi_m2_one<31, 8, VI_CODE_LLC, 14>(d, vi_params<VI_CODE_LLC>(p), f, iterPtr, nbx, nby, KC, nkc, s);
+    vi_m2_one<31, 8, VI_CODE_LLC, 14>(d, vi_params<VI_CODE_LLC>(p), f, iterPtr, nbx, nby, KC, nkc, s);
     return true;
   }
   if (code == VI_CODE_LLC && BX == 32 && BY == 8) {
-    if (gl) vi_m2_one<32, 8, VI_CODE_LLC, 30>(d, vi_params<VI_CODE_LLC>(p), f, iterPtr, nbx, nby, KC, nkc, s);
-    else vi_m2_one<32, 8, VI_CODE_LLC, 14>(d, vi_params<VI_CODE_LLC>(p), f, iterPtr, nbx, nby, KC, nkc, s);
+    vi_m2_one<32, 8, VI_CODE_LLC, 14>(d, vi_params<VI_CODE_LLC>(p), f, iterPtr, nbx, nby, KC, nkc, s);
     return true;
   }
   return false;
