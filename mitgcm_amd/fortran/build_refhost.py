@@ -20,6 +20,10 @@ Layouts:
         topology, the experiment has no data.exch2), staggerTimeStep
   cs32_6t  the same experiment on six 32 x 32 tiles, one per face (the device's bench layout;
         refhost/SIZE.h.cs32_6t)
+  llc30 BASELINE config 5's lat-lon-cap topology at n = 30 (13 tiles of 30 x 30, OL = 4, 50
+        levels; refhost/SIZE.h.llc30) on global_ocean.cs32x15's code/ options and packages: the
+        synthetic LLC workload has no reference experiment, its namelist is written by the test
+        from mitgcm_amd/configs.py llc_synthetic
 """
 import os
 import re
@@ -40,7 +44,8 @@ OCEAN90 = ("global_ocean.90x40x15", "#define ALLOW_GMREDI\n#define ALLOW_CD_CODE
 CS32 = ("global_ocean.cs32x15", "#define ALLOW_GMREDI\n#define ALLOW_EXCH2\n")
 # layout -> (experiment, PACKAGES_CONFIG.h, SIZE.h replacing the experiment's or None)
 LAYOUTS = {"ref": OCEAN90 + (None,), "1t": OCEAN90 + (os.path.join(RH, "SIZE.h.1t"),), "cs32": CS32 + (None,),
-           "cs32_6t": CS32 + (os.path.join(RH, "SIZE.h.cs32_6t"),)}
+           "cs32_6t": CS32 + (os.path.join(RH, "SIZE.h.cs32_6t"),),
+           "llc30": CS32 + (os.path.join(RH, "SIZE.h.llc30"),)}
 
 
 def available():
@@ -185,7 +190,7 @@ def _pre(src, tmp, incdirs):
     return f
 
 
-def build(layouts=("ref", "1t", "cs32", "cs32_6t"), verbose=False):
+def build(layouts=("ref", "1t", "cs32", "cs32_6t", "llc30"), verbose=False):
     if not available():
         raise RuntimeError("build_refhost needs /root/reference (headers), amdflang and cpp")
     lib = os.path.join(ROOT, "mitgcm_amd", "libmitgcm_amd.so")

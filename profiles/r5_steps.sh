@@ -17,6 +17,7 @@ for s in "$@"; do
     refhost_m4) timeout -k 10 300 $PY tests/test_gpu_refhost.py -k "ref-0-4-0-0-0 or 6-0-0" > $O/refhost_m4.log 2>&1 ;;
     refhost_tp) timeout -k 10 300 $PY tests/test_gpu_refhost.py -k "throughput" > $O/refhost_tp.log 2>&1 ;;
     refhost_all) timeout -k 10 600 $PY tests/test_gpu_refhost.py > $O/refhost_all.log 2>&1 ;;
+    refhost_llc) timeout -k 10 300 $PY tests/test_gpu_refhost.py -k "llc30" > $O/refhost_llc.log 2>&1 ;;
     parity) timeout -k 10 500 $PY -x tests/test_gpu_llc.py tests/test_gpu_ocean90.py tests/test_gpu_cs32x15.py > $O/parity.log 2>&1 ;;
     auto_policy) timeout -k 10 400 $PY tests/test_gpu_parallel.py -k "auto" > $O/auto_policy.log 2>&1 ;;
     parallel) timeout -k 10 1000 $PY tests/test_gpu_parallel.py tests/test_gpu_rccl.py > $O/parallel.log 2>&1 ;;

@@ -324,3 +324,108 @@ def test_refhost_cs32_exch2_bitexact(layout, models, mwg, eager, tmp_path):
     assert len([n for n in CHECK if n in out]) >= 18
     # the state came down after steps 2 and 4 only (monitorFreq = 2 days, nEndIter = 4)
     assert st["downloads"] == 2 * len(state), (st, len(state))
+
+
+# BASELINE config 5 (the LLC-90-shaped synthetic, configs.llc_synthetic) through the drop-ins,
+# at n = 30: the 5 lat-lon-cap facets as 13 tiles of 30 x 30 (OL = 4, 50 levels) under
+# pkg/exch2 (build_refhost.py layout "llc30", refhost/SIZE.h.llc30).  The synthetic has no
+# reference experiment, so its namelist is written here from the configuration's own
+# parameters (_llc_namelists: each into the group the reference reads it from, refhost_parms.F
+# NAMELIST /PARM01/../PARM04/), and refhost resolves it like any other; the W2 arrays are the
+# LLC topology's (Exch2Topology.w2_arrays, the facet links with their rotations).  Bars: every
+# parameter refhost hands the mirror equals the device configuration's own, and the state after
+# 4 steps on 1 and 3 device models -- the vector-invariant step with C2 tracers, implicit vertical
+# diffusion and IVDC, linear free surface with exactConserv -- is bit-identical to
+# mgcm_forward_step on the same tiling.
+LLC_LOGICAL = {"vectorInvariantMomentum", "momDissip_In_AB", "no_slip_sides", "no_slip_bottom", "exactConserv",
+               "tempStepping", "tempAdvection", "tempForcing", "saltStepping", "saltAdvection", "saltForcing",
+               "implicitDiffusion", "usingCurvilinearGrid"}
+LLC_INTEGER = {"selectCoriScheme", "selectVortScheme", "selectKEscheme", "momForcingOutAB", "cg2dMaxIters",
+               "cg2dUseMinResSol", "nIter0", "tempAdvScheme", "tempVertAdvScheme", "saltAdvScheme",
+               "saltVertAdvScheme", "integr_GeoPot"}
+
+
+def _namelist_groups():
+    """refhost_parms.F's NAMELIST statements: group -> the names it reads."""
+    import re
+    src = open(os.path.join(RH, "refhost_parms.F")).read()
+    groups = {}
+    for m in re.finditer(r"NAMELIST /(\w+)/\n((?:     & .*\n)+)", src):
+        groups[m.group(1)] = {n.strip() for n in m.group(2).replace("     & ", "").replace("\n", ",").split(",")
+                              if n.strip()}
+    return groups
+
+
+def _llc_namelists(dst, params, tRef, sRef, delR):
+    os.makedirs(dst, exist_ok=True)
+    groups = _namelist_groups()
+    fmt = lambda n, v: (".TRUE." if v else ".FALSE.") if n in LLC_LOGICAL else \
+        str(int(v)) if n in LLC_INTEGER else repr(float(v))
+    body = {g: [] for g in ("PARM01", "PARM02", "PARM03", "PARM04")}
+    for n, v in params.items():
+        if n == "eosType":
+            assert v == 0
+            body["PARM01"].append(" eosType='LINEAR',")
+            continue
+        grp = [g for g in body if n in groups[g]]
+        assert len(grp) == 1, (n, grp)
+        body[grp[0]].append(" %s=%s," % (n, fmt(n, v)))
+    body["PARM01"].append(" tRef=%s," % ", ".join(repr(float(x)) for x in tRef))
+    body["PARM01"].append(" sRef=%s," % ", ".join(repr(float(x)) for x in sRef))
+    body["PARM01"].append(" implicitFreeSurface=.TRUE.,")
+    body["PARM01"].append(" plotLevel=0,")
+    body["PARM04"].append(" delR=%s," % ", ".join(repr(float(x)) for x in delR))
+    with open(os.path.join(dst, "data"), "w") as f:
+        for g, lines in body.items():
+            f.write(" &%s\n%s\n &\n\n" % (g, "\n".join(lines)))
+    with open(os.path.join(dst, "data.pkg"), "w") as f:
+        f.write(" &PACKAGES\n useGMRedi=.FALSE.,\n &\n")
+    return dst
+
+
+@pytest.mark.parametrize("models", [1, 3])
+def test_refhost_llc30_exch2_bitexact(models, tmp_path):
+    from mitgcm_amd import configs
+    exe = os.path.join(RH, "refhost_llc30")
+    assert os.path.exists(exe), "refhost not built (mitgcm_amd/fortran/build_refhost.py, __graft_entry__.build())"
+    nsteps = 4
+    out3 = configs.llc_synthetic(n=30)
+    g0, params, st0 = out3
+    assert (g0.nTiles, g0.sNx, g0.sNy, g0.OLx, g0.Nr) == (13, 30, 30, 4, 50)
+    pdir = _llc_namelists(str(tmp_path / "input"), params, st0["tRef"], st0["sRef"], configs.llc_delr(50))
+    r = subprocess.run([exe, "--params", pdir, str(tmp_path / "params.txt")], capture_output=True, text=True,
+                       timeout=60)
+    assert r.returncode == 0, r.stdout + r.stderr
+    got = {ln.split()[0]: float(ln.split()[1]) for ln in open(tmp_path / "params.txt")}
+    m = configs.make_model(lambda: out3)
+    from mitgcm_amd._lib import lib
+    skip = ("monitorFreq", "nEndIter", "cg2dNorm", "cg2dTolerance_sq", "cg2dNormaliseRHS")
+    pdiff = [(n, v, lib().mgcm_get_param(m.h, n.encode())) for n, v in got.items()
+             if n not in skip and v != lib().mgcm_get_param(m.h, n.encode())]
+    w2 = m.g.topo.w2_arrays(ldNb=8, ldT=2 * m.g.nTiles)
+    state = _write_blob(tmp_path / "refhost_in.bin", m, nsteps, monitor_days=2, w2=w2, undef=("ALLOW_CD_CODE",))
+    env = dict(os.environ, MGCM_AMD_MODELS=str(models), MGCM_AMD_EAGER="0")
+    r = subprocess.run([exe, str(tmp_path), pdir], capture_output=True, text=True, timeout=300, env=env)
+    assert r.returncode == 0, r.stdout + r.stderr
+    out, st = _read_out(tmp_path / "refhost_out.bin", state, nsteps)
+    m.forward_step(1)
+    m.prepare()
+    m.sync()
+    t0 = time.perf_counter()
+    m.forward_step(nsteps - 1)
+    m.sync()
+    graph_ms = 1e3 * (time.perf_counter() - t0) / (nsteps - 1)
+    bad = [(n, float(np.abs(out[n] - m.get(n).reshape(-1)[:out[n].size]).max())) for n in CHECK
+           if n in out and not np.array_equal(out[n], m.get(n).reshape(-1)[:out[n].size])]
+    m.close()
+    rec = {"layout": "llc30", "models": models, "params_compared": len(got) - len(skip), "param_diff": pdiff,
+           "dropin_ms_per_step_mean": 1e3 * st["seconds"] / max(1, st["steps_timed"]),
+           "graph_ms_per_step": graph_ms, "mirror": st, "state_fields": len(state)}
+    print("refhost llc30 models=%d: %s" % (models, json.dumps(rec)))
+    if os.path.isdir(os.path.join(ROOT, "gpurun_out")):
+        with open(os.path.join(ROOT, "gpurun_out", "refhost_llc30_m%d.json" % models), "w") as f:
+            json.dump(rec, f)
+    assert not pdiff, pdiff
+    assert not bad, bad
+    assert len([n for n in CHECK if n in out]) >= 18
+    assert st["downloads"] == 2 * len(state), (st, len(state))

@@ -114,3 +114,24 @@ def test_refhost_resolves_the_namelist_as_the_reference(exp, tmp_path):
     shared = [n for n in got if n in params and n not in ("monitorFreq", "nEndIter") + cfg_skip]
     diff = [(n, got[n], float(params[n])) for n in shared if got[n] != float(params[n])]
     assert len(shared) >= 40 and not diff, (len(shared), diff)
+
+
+def test_refhost_resolves_the_llc_namelist_as_configured(tmp_path):
+    """BASELINE config 5 has no reference experiment: tests/test_gpu_refhost.py writes its
+    namelist from configs.llc_synthetic's parameters; refhost (layout "llc30") must resolve it
+    back to the same values (the GPU test then pins every mirror parameter against the device
+    model's own)."""
+    exe = os.path.join(ROOT, "mitgcm_amd", "fortran", "refhost", "refhost_llc30")
+    if not os.path.exists(exe):
+        pytest.skip("refhost not built (needs the reference headers)")
+    from mitgcm_amd import configs
+    from test_gpu_refhost import _llc_namelists
+    _, params, st = configs.llc_synthetic(n=30)
+    pdir = _llc_namelists(str(tmp_path / "input"), params, st["tRef"], st["sRef"], configs.llc_delr(50))
+    out = tmp_path / "params.txt"
+    r = subprocess.run([exe, "--params", pdir, str(out)], capture_output=True, text=True, timeout=60)
+    assert r.returncode == 0, r.stdout + r.stderr
+    got = {ln.split()[0]: float(ln.split()[1]) for ln in open(out)}
+    shared = [n for n in got if n in params]
+    diff = [(n, got[n], float(params[n])) for n in shared if got[n] != float(params[n])]
+    assert len(shared) >= 45 and not diff, (len(shared), diff)
