@@ -332,11 +332,11 @@ def test_refhost_cs32_exch2_bitexact(layout, models, mwg, eager, tmp_path):
 # reference experiment, so its namelist is written here from the configuration's own
 # parameters (_llc_namelists: each into the group the reference reads it from, refhost_parms.F
 # NAMELIST /PARM01/../PARM04/), and refhost resolves it like any other; the W2 arrays are the
-# LLC topology's (Exch2Topology.w2_arrays, the facet links with their rotations).  Bars: every
-# parameter refhost hands the mirror equals the device configuration's own, and the state after
-# 4 steps on 1 and 3 device models -- the vector-invariant step with C2 tracers, implicit vertical
-# diffusion and IVDC, linear free surface with exactConserv -- is bit-identical to
-# mgcm_forward_step on the same tiling.
+# LLC topology's (Exch2Topology.w2_arrays, the facet links with their rotations).  Bars: each
+# configured parameter refhost hands the mirror equals the device model's own, and the state
+# after 4 steps on 1, 3, 4 and 13 device models (and eager) -- the vector-invariant step with
+# C2 tracers, implicit vertical diffusion and IVDC, linear free surface with exactConserv
+#  -- is bit-identical to mgcm_forward_step on the same tiling.
 LLC_LOGICAL = {"vectorInvariantMomentum", "momDissip_In_AB", "no_slip_sides", "no_slip_bottom", "exactConserv",
                "tempStepping", "tempAdvection", "tempForcing", "saltStepping", "saltAdvection", "saltForcing",
                "implicitDiffusion", "usingCurvilinearGrid"}
@@ -356,8 +356,12 @@ def _namelist_groups():
     return groups
 
 
-def _llc_namelists(dst, params, tRef, sRef, delR):
+def _llc_namelists(dst, params, tRef, sRef, delR, g):
+    """data / data.pkg for configs.llc_synthetic's parameters; the CG2D target residual is the
+    one its grid's INI_CG2D took (Grid.ini_cg2d: cg2dTargetResidual with the RHS normalised)."""
     os.makedirs(dst, exist_ok=True)
+    assert g.cg2dNormaliseRHS and g.cg2dTolerance_sq == 1e-9 * 1e-9
+    cg2dTargetResidual = 1e-9
     groups = _namelist_groups()
     fmt = lambda n, v: (".TRUE." if v else ".FALSE.") if n in LLC_LOGICAL else \
         str(int(v)) if n in LLC_INTEGER else repr(float(v))
@@ -374,6 +378,7 @@ def _llc_namelists(dst, params, tRef, sRef, delR):
     body["PARM01"].append(" sRef=%s," % ", ".join(repr(float(x)) for x in sRef))
     body["PARM01"].append(" implicitFreeSurface=.TRUE.,")
     body["PARM01"].append(" plotLevel=0,")
+    body["PARM02"].append(" cg2dTargetResidual=%r," % cg2dTargetResidual)
     body["PARM04"].append(" delR=%s," % ", ".join(repr(float(x)) for x in delR))
     with open(os.path.join(dst, "data"), "w") as f:
         for g, lines in body.items():
@@ -383,8 +388,8 @@ def _llc_namelists(dst, params, tRef, sRef, delR):
     return dst
 
 
-@pytest.mark.parametrize("models", [1, 3])
-def test_refhost_llc30_exch2_bitexact(models, tmp_path):
+@pytest.mark.parametrize("models,eager", [(1, 0), (1, 1), (3, 0), (4, 0), (13, 0)])
+def test_refhost_llc30_exch2_bitexact(models, eager, tmp_path):
     from mitgcm_amd import configs
     exe = os.path.join(RH, "refhost_llc30")
     assert os.path.exists(exe), "refhost not built (mitgcm_amd/fortran/build_refhost.py, __graft_entry__.build())"
@@ -392,7 +397,7 @@ def test_refhost_llc30_exch2_bitexact(models, tmp_path):
     out3 = configs.llc_synthetic(n=30)
     g0, params, st0 = out3
     assert (g0.nTiles, g0.sNx, g0.sNy, g0.OLx, g0.Nr) == (13, 30, 30, 4, 50)
-    pdir = _llc_namelists(str(tmp_path / "input"), params, st0["tRef"], st0["sRef"], configs.llc_delr(50))
+    pdir = _llc_namelists(str(tmp_path / "input"), params, st0["tRef"], st0["sRef"], configs.llc_delr(50), g0)
     r = subprocess.run([exe, "--params", pdir, str(tmp_path / "params.txt")], capture_output=True, text=True,
                        timeout=60)
     assert r.returncode == 0, r.stdout + r.stderr
@@ -400,11 +405,15 @@ def test_refhost_llc30_exch2_bitexact(models, tmp_path):
     m = configs.make_model(lambda: out3)
     from mitgcm_amd._lib import lib
     skip = ("monitorFreq", "nEndIter", "cg2dNorm", "cg2dTolerance_sq", "cg2dNormaliseRHS")
-    pdiff = [(n, v, lib().mgcm_get_param(m.h, n.encode())) for n, v in got.items()
-             if n not in skip and v != lib().mgcm_get_param(m.h, n.encode())]
+    # the configuration's own parameters as the device model holds them (the mirror passes
+    # every other one too, as the reference resolved it: those the device model left at its
+    # defaults are recorded, and the state comparison below is their bar)
+    dev = {n: lib().mgcm_get_param(m.h, n.encode()) for n in got if n not in skip}
+    pdiff = [(n, got[n], dev[n]) for n in dev if n in params and got[n] != dev[n]]
+    pother = [(n, got[n], dev[n]) for n in dev if n not in params and got[n] != dev[n] and dev[n] == dev[n]]
     w2 = m.g.topo.w2_arrays(ldNb=8, ldT=2 * m.g.nTiles)
     state = _write_blob(tmp_path / "refhost_in.bin", m, nsteps, monitor_days=2, w2=w2, undef=("ALLOW_CD_CODE",))
-    env = dict(os.environ, MGCM_AMD_MODELS=str(models), MGCM_AMD_EAGER="0")
+    env = dict(os.environ, MGCM_AMD_MODELS=str(models), MGCM_AMD_EAGER=str(eager))
     r = subprocess.run([exe, str(tmp_path), pdir], capture_output=True, text=True, timeout=300, env=env)
     assert r.returncode == 0, r.stdout + r.stderr
     out, st = _read_out(tmp_path / "refhost_out.bin", state, nsteps)
@@ -418,12 +427,13 @@ def test_refhost_llc30_exch2_bitexact(models, tmp_path):
     bad = [(n, float(np.abs(out[n] - m.get(n).reshape(-1)[:out[n].size]).max())) for n in CHECK
            if n in out and not np.array_equal(out[n], m.get(n).reshape(-1)[:out[n].size])]
     m.close()
-    rec = {"layout": "llc30", "models": models, "params_compared": len(got) - len(skip), "param_diff": pdiff,
+    rec = {"layout": "llc30", "models": models, "eager": eager, "params_compared": len(got) - len(skip), "param_diff": pdiff,
+           "params_left_at_device_default_resolved_otherwise": pother,
            "dropin_ms_per_step_mean": 1e3 * st["seconds"] / max(1, st["steps_timed"]),
            "graph_ms_per_step": graph_ms, "mirror": st, "state_fields": len(state)}
-    print("refhost llc30 models=%d: %s" % (models, json.dumps(rec)))
+    print("refhost llc30 models=%d eager=%d: %s" % (models, eager, json.dumps(rec)))
     if os.path.isdir(os.path.join(ROOT, "gpurun_out")):
-        with open(os.path.join(ROOT, "gpurun_out", "refhost_llc30_m%d.json" % models), "w") as f:
+        with open(os.path.join(ROOT, "gpurun_out", "refhost_llc30_m%d_e%d.json" % (models, eager)), "w") as f:
             json.dump(rec, f)
     assert not pdiff, pdiff
     assert not bad, bad

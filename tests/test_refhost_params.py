@@ -126,8 +126,8 @@ def test_refhost_resolves_the_llc_namelist_as_configured(tmp_path):
         pytest.skip("refhost not built (needs the reference headers)")
     from mitgcm_amd import configs
     from test_gpu_refhost import _llc_namelists
-    _, params, st = configs.llc_synthetic(n=30)
-    pdir = _llc_namelists(str(tmp_path / "input"), params, st["tRef"], st["sRef"], configs.llc_delr(50))
+    g, params, st = configs.llc_synthetic(n=30)
+    pdir = _llc_namelists(str(tmp_path / "input"), params, st["tRef"], st["sRef"], configs.llc_delr(50), g)
     out = tmp_path / "params.txt"
     r = subprocess.run([exe, "--params", pdir, str(out)], capture_output=True, text=True, timeout=60)
     assert r.returncode == 0, r.stdout + r.stderr
