@@ -192,7 +192,10 @@ int mgcm_step_phase(mgcm_model *m, int phase);
 /* Distributed CG2D (mitgcm_amd/parallel.py, cg2dMode = "distributed"): one operation of
  * model/src/cg2d.F:100-415 over this process's tiles (op 0 normalise + max, 1 scale by a0,
  * 2 initial residual, 3 preconditioner, 4 s = q + a0*s, 5 A s, 6 x/r update with a0,
- * 7 un-normalise), per-tile partials to the device buffer part[2*nTiles] -- the per-tile
+ * 7 un-normalise, 8 save x as the lowest-residual solution, 9 restore it: cg2dUseMinResSol;
+ * CG2D_SR, cg2d_sr.F: 10 y = M r, s = y, 11 x/r update with a0, 12 y = M r, 13 v = A y,
+ * 14 sum r*r, 15 s/q update with a0),
+ * per-tile partials to the device buffer part[2*nTiles] -- the per-tile
  * values GLOBAL_SUM_TILE_RL (eesupp/src/global_sum_tile.F:14-17,161-191) sums in tile order.
  * Phase 6 of mgcm_step_phase finishes phase 2 after such a solve. */
 int mgcm_cg2d_op(mgcm_model *m, int op, double a0, double *part);
@@ -221,9 +224,10 @@ void *mgcm_get_stream(mgcm_model *m);
 long mgcm_halo_sources(mgcm_model *m, int t0, int nT, long *out, long cap);
 int mgcm_cg2d_tiles(mgcm_model *m, int t0, int nT);
 int mgcm_cg2d_share(mgcm_model *m, mgcm_model *owner);
-/* Store CG2D's output arguments (cg2d.F:13-17) as this step's solve record. */
+/* Store CG2D's output arguments (cg2d.F:13-17) as this step's solve record (minResidualSq,
+ * nIterMin: -1, -1 without cg2dUseMinResSol). */
 int mgcm_cg2d_record(mgcm_model *m, double firstResidual, double lastResidual, double rhsMax, double sumRHS,
-                     int numIters);
+                     int numIters, double minResidualSq, int nIterMin);
 /* Gather (unpack=0) / scatter (1) a 2-D field at n device-resident flat offsets idx. */
 int mgcm_field_pack(mgcm_model *m, const char *name, const long *idx, long n, double *buf, int unpack);
 /* EXCH of one field from this process's copy of the domain (EXCH_XY_RL / EXCH_S3D_RL with

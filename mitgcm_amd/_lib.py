@@ -77,7 +77,7 @@ def lib():
         "mgcm_tile_copy": (ci, [vp, cs, ci, ci, vp, ci]),
         "mgcm_step_phase": (ci, [vp, ci]),
         "mgcm_cg2d_op": (ci, [vp, ci, cd, vp]),
-        "mgcm_cg2d_record": (ci, [vp, cd, cd, cd, cd, ci]),
+        "mgcm_cg2d_record": (ci, [vp, cd, cd, cd, cd, ci, cd, ci]),
         "mgcm_field_pack": (ci, [vp, cs, vp, cl, vp, ci]),
         "mgcm_exchange_field": (ci, [vp, cs]),
         "mgcm_oceanic_phys": (ci, [vp]),

@@ -33,7 +33,8 @@ struct Dims {
     X(cg2d_b) X(cg2d_x) X(Qnet) X(EmPmR) X(SSS) X(lambdaSaltClimRelax) X(etaNm1) X(fCoriCos) X(recip_Rcol) \
     X(rSurfW) X(rSurfS) X(rLowW) X(rLowS) X(Ro_surf) X(R_low) X(rStarFacC) X(rStarFacW) X(rStarFacS) \
     X(rStarExpC) X(rStarExpW) X(rStarExpS) X(rStarDhCDt) X(rStarDhWDt) X(rStarDhSDt) X(PmEpR) X(dEtaHdt) \
-    X(maskInW) X(maskInS) X(fCoriG) X(recip_rAz) X(recip_dxG) X(recip_dyG) X(etaHnm1) X(cg2d_r) X(cg2d_s) X(cg2d_q)
+    X(maskInW) X(maskInS) X(fCoriG) X(recip_rAz) X(recip_dxG) X(recip_dyG) X(etaHnm1) X(cg2d_r) X(cg2d_s) X(cg2d_q) \
+    X(cg2d_min) X(cg2d_y) X(cg2d_v)
 #define MG_F3D_LIST(X) X(hFacC) X(hFacW) X(hFacS) X(recip_hFacC) X(recip_hFacW) X(recip_hFacS) X(maskC) X(maskW) \
     X(maskS) X(uVel) X(vVel) X(wVel) X(theta) X(salt) X(gU) X(gV) X(guNm1) X(gvNm1) X(rhoInSitu) X(IVDConvCount) \
     X(gtNm1) X(thetaNext) X(gTscr) X(cpScr) X(phiHydC) X(saltNext) X(gsNm1) X(advScr1) X(advScr2) X(gAdv) \
@@ -132,6 +133,8 @@ struct Fields {
   // solver work
   double *cg2d_b, *cg2d_x;
   double *cg2d_r, *cg2d_s, *cg2d_q;   // distributed CG2D work vectors (kernels_cg2d_dist.hip)
+  double *cg2d_min;                   // its lowest-residual solution (cg2dUseMinResSol, cg2d.F:148-155, 338-369)
+  double *cg2d_y, *cg2d_v;            // CG2D_SR's y = M r and v = A y (cg2d_sr.F:102-104)
   // the 2-D and 3-D arenas (MG_F2D_LIST / MG_F3D_LIST order)
   double *a2, *a3;
 };

@@ -15,6 +15,17 @@
 //   op 5  q = A s; partial sum s*q                           (cg2d.F:262-287)
 //   op 6  x = x + alpha*s, r = r - alpha*q; partial sum r*r  (a0 = alpha, cg2d.F:297-318)
 //   op 7  x = x/rhsNorm  (a0 = rhsNorm)                      (cg2d.F:372-385)
+//   op 8  cg2d_min = x  (the lowest-residual solution so far, cg2dUseMinResSol; cg2d.F:148-155, 338-351)
+//   op 9  x = cg2d_min  (the solve ended above its lowest residual, cg2d.F:358-369)
+// CG2D_SR (cg2d_sr.F, useSRCGSolver): the same ops 0-2, 5, 7-9 and
+//   op 10 y = M r, s = y; partial sum y*r                   (cg2d_sr.F:223-243)
+//   op 11 x = x + a0*s, r = r - a0*q  (a0 = sigma)           (cg2d_sr.F:279-288, 396-401)
+//   op 12 y = M r                                            (cg2d_sr.F:300-316)
+//   op 13 v = A y; partials sum y*r, sum y*v                 (cg2d_sr.F:324-347)
+//   op 14 partial sum r*r                                    (cg2d_sr.F:344-345, 411-422)
+//   op 15 s = y + a0*s, q = v + a0*q  (a0 = cgBeta)          (cg2d_sr.F:394-399)
+// (the reference's one GLOBAL_SUM_VECTOR_RL of three per-tile values, cg2d_sr.F:348-358, is
+// three tile-ordered sums: ops 13 and 14 hand the host the same per-tile partials)
 // The width-1 EXCH_S3D_RL of r and s (cg2d.F:175,255,353) and EXCH_XY_RL of x (:135) are
 // the host's point-to-point exchange plus mgcm_exchange_field.
 #include "common.h"
@@ -46,6 +57,7 @@ __global__ void __launch_bounds__(CGD_NT) k_cgd(Dims d, Params p, Fields f, int 
       const int i = q % (sNx + 2), j = q / (sNx + 2);
       A2(cg2d_r, i, j) = 0.0;
       A2(cg2d_s, i, j) = 0.0;
+      A2(cg2d_y, i, j) = 0.0;
     }
     __syncthreads();
   }
@@ -104,27 +116,68 @@ __global__ void __launch_bounds__(CGD_NT) k_cgd(Dims d, Params p, Fields f, int 
       case 7:
         A2(cg2d_x, i, j) = A2(cg2d_x, i, j) / a0;
         break;
+      case 8:
+        A2(cg2d_min, i, j) = A2(cg2d_x, i, j);
+        break;
+      case 9:
+        A2(cg2d_x, i, j) = A2(cg2d_min, i, j);
+        break;
+      case 10:
+      case 12: {
+        const double r = A2(cg2d_r, i, j);
+        const double y = A2(pC, i, j) * r + A2(pW, i, j) * A2(cg2d_r, i - 1, j) + A2(pW, i + 1, j) * A2(cg2d_r, i + 1, j) +
+                         A2(pS, i, j) * A2(cg2d_r, i, j - 1) + A2(pS, i, j + 1) * A2(cg2d_r, i, j + 1);
+        A2(cg2d_y, i, j) = y;
+        if (op == 10) {
+          A2(cg2d_s, i, j) = y;
+          s0 = s0 + y * r;
+        }
+        break;
+      }
+      case 11:
+        A2(cg2d_x, i, j) = A2(cg2d_x, i, j) + a0 * A2(cg2d_s, i, j);
+        A2(cg2d_r, i, j) = A2(cg2d_r, i, j) - a0 * A2(cg2d_q, i, j);
+        break;
+      case 13: {
+        const double y = A2(cg2d_y, i, j);
+        const double v = A2(aW2d, i, j) * A2(cg2d_y, i - 1, j) + A2(aW2d, i + 1, j) * A2(cg2d_y, i + 1, j) +
+                         A2(aS2d, i, j) * A2(cg2d_y, i, j - 1) + A2(aS2d, i, j + 1) * A2(cg2d_y, i, j + 1) +
+                         A2(aC2d, i, j) * y;
+        A2(cg2d_v, i, j) = v;
+        s0 = s0 + y * A2(cg2d_r, i, j);
+        s1 = s1 + y * v;
+        break;
+      }
+      case 14: {
+        const double r = A2(cg2d_r, i, j);
+        s0 = s0 + r * r;
+        break;
+      }
+      case 15:
+        A2(cg2d_s, i, j) = A2(cg2d_y, i, j) + a0 * A2(cg2d_s, i, j);
+        A2(cg2d_q, i, j) = A2(cg2d_v, i, j) + a0 * A2(cg2d_q, i, j);
+        break;
     }
   }
 #undef A2
-  if (op == 1 || op == 4 || op == 7) return;
+  if (op == 1 || op == 4 || (op >= 7 && op <= 9) || op == 11 || op == 12 || op == 15) return;
   const double v0 = cgd_tree(s0, sh, op == 0);
-  const double v1 = op == 2 ? cgd_tree(s1, sh, false) : 0.0;
+  const double v1 = (op == 2 || op == 13) ? cgd_tree(s1, sh, false) : 0.0;
   if (tid == 0) { part[2 * t] = v0; part[2 * t + 1] = v1; }
 }
 
 // the SolveRecord of this step (cg2d.F's output arguments), written where the device
 // solvers write theirs
 __global__ void k_cgd_record(SolveRecord *rec, const int *stepCounter, double first, double last, double rhsMax,
-                             double sumRHS, int iters) {
+                             double sumRHS, int iters, double minResidualSq, int nIterMin) {
   SolveRecord &R = rec[stepCounter ? *stepCounter : 0];
   R.firstResidual = first;
   R.lastResidual = last;
-  R.minResidualSq = -1.0;
+  R.minResidualSq = minResidualSq;
   R.rhsMax = rhsMax;
   R.sumRHS = sumRHS;
   R.numIters = iters;
-  R.nIterMin = -1;
+  R.nIterMin = nIterMin;
 }
 
 // gather (unpack = 0) or scatter (1) one 2-D field at whole-domain flat offsets idx[0..n)
@@ -142,8 +195,9 @@ hipError_t launch_cgd(const Dims &d, const Params &p, const Fields &f, int op, d
 }
 
 hipError_t launch_cgd_record(SolveRecord *rec, const int *stepCounter, double first, double last, double rhsMax,
-                             double sumRHS, int iters, hipStream_t s) {
-  hipLaunchKernelGGL(k_cgd_record, dim3(1), dim3(1), 0, s, rec, stepCounter, first, last, rhsMax, sumRHS, iters);
+                             double sumRHS, int iters, double minResidualSq, int nIterMin, hipStream_t s) {
+  hipLaunchKernelGGL(k_cgd_record, dim3(1), dim3(1), 0, s, rec, stepCounter, first, last, rhsMax, sumRHS, iters,
+                     minResidualSq, nIterMin);
   return hipGetLastError();
 }
 

@@ -2321,6 +2321,73 @@ __global__ void __launch_bounds__(256) k_mom_impl(Dims d, Params p, Fields f, in
   if (valid) MG_COLF_K(k) g[MG_I3(d, i, j, k, t)] = sSub[(k - 1) * NC_ + cc];
 }
 
+// IMPLDIFF (model/src/impldiff.F:24-245, tracerId = 0: deltaTMom) on the CD scheme's D-grid
+// velocities after the DYNAMICS k loop (dynamics.F:614-634): V = false vVelD with kappaRU and
+// recip_hFacW, V = true uVelD with kappaRV and recip_hFacS (the reference's pairing: vVelD
+// sits on u points), on i = 0..sNx+1, j = 0..sNy+1.  IMPLDIFF's own recurrence, not
+// SOLVE_TRIDIAGONAL's: a(k) / c(k) vanish where recip_hFac of the level above / below is 0,
+// bet = 1 (gam = c*bet) where a pivot is 0.  Column frame as k_mom_impl: k-parallel
+// coefficients into LDS, one thread per column sweeps (gam overwrites c, the forward
+// solution the right-hand side).
+template <bool V>
+__global__ void __launch_bounds__(256) k_impldiff_cd(Dims d, Params p, Fields f, int nc) {
+  extern __shared__ __attribute__((aligned(16))) double lds[];
+  MG_COLF(0, d.sNx + 2, 0, d.sNy + 2, nc)
+  const int Nr = d.Nr, NS = Nr * NC_;
+  double *sA = lds, *sC = lds + NS, *sY = lds + 2 * NS;
+  double *g = V ? f.uVelD : f.vVelD;
+  const double *rh = V ? f.recip_hFacS : f.recip_hFacW;
+  if (valid) {
+    MG_COLF_K(k) {
+      const int me = (k - 1) * NC_ + cc;
+      const long q3 = MG_I3(d, i, j, k, t);
+      double a = 0.0, c = 0.0;   // kappaRU = kappaRV = viscArNr(k) (calc_viscosity.F)
+      if (k >= 2) {
+        a = -(p.deltaTMom * rh[q3] * f.recip_drF[k - 1] * p.viscAr * f.recip_drC[k - 1]);
+        if (rh[MG_I3(d, i, j, k - 1, t)] == 0.0) a = 0.0;
+      }
+      if (k <= Nr - 1) {
+        c = -(p.deltaTMom * rh[q3] * f.recip_drF[k - 1] * p.viscAr * f.recip_drC[k]);
+        if (rh[MG_I3(d, i, j, k + 1, t)] == 0.0) c = 0.0;
+      }
+      sA[me] = a;
+      sC[me] = c;
+      sY[me] = g[q3];
+    }
+  }
+  __syncthreads();
+  if (valid && kk == 0) {
+    double betPrev = 1.0, ltPrev = 0.0, cPrev = 0.0;
+    for (int k2 = 1; k2 <= Nr; k2++) {
+      const int s2 = (k2 - 1) * NC_ + cc;
+      const double a = sA[s2], c = sC[s2];
+      const double b = 1.0 - (a + c);
+      double bet = 1.0, gam = 0.0;
+      if (Nr > 1) {
+        if (k2 == 1) {
+          if (b != 0.0) bet = 1.0 / b;
+        } else {
+          gam = cPrev * betPrev;
+          if ((b - a * gam) != 0.0) bet = 1.0 / (b - a * gam);
+        }
+      }
+      const double lt = (k2 == 1) ? sY[s2] * bet : bet * (sY[s2] - a * ltPrev);
+      sY[s2] = lt;
+      sC[s2] = gam;   // gam(k2): read by level k2 - 1 on the way up
+      betPrev = bet; ltPrev = lt; cPrev = c;
+    }
+    double above = sY[(Nr - 1) * NC_ + cc];
+    for (int k2 = Nr - 1; k2 >= 1; k2--) {
+      const int s2 = (k2 - 1) * NC_ + cc;
+      const double v = sY[s2] - sC[s2 + NC_] * above;
+      sY[s2] = v;
+      above = v;
+    }
+  }
+  __syncthreads();
+  if (valid) MG_COLF_K(k) g[MG_I3(d, i, j, k, t)] = sY[(k - 1) * NC_ + cc];
+}
+
 static bool del2_needed(const Params &p) { return p.momViscosity && (p.viscA4D != 0.0 || p.viscA4Z != 0.0); }
 // k_del2uv rides in CALC_PHI_HYD's launch (k_phi_del2) on the small grids
 static bool phi_del2_fused(const Dims &d, const Params &p) { return del2_needed(p) && mg_hfuse(MG_FUSE_PHI, d.nx, d.ny, d.nT, d.Nr); }
@@ -2445,6 +2512,14 @@ static hipError_t launch_mom_tail(const Dims &d, const Params &p, const Fields &
     MG_ALLOW_LDS(k_mom_impl<true>);
     hipLaunchKernelGGL(k_mom_impl<false>, dim3(mg_colf_blocks(ncU, nc)), dim3(256), mg_colf_lds(d.Nr, nc, 3), s, d, p, f, nc);
     hipLaunchKernelGGL(k_mom_impl<true>, dim3(mg_colf_blocks(ncV, nc)), dim3(256), mg_colf_lds(d.Nr, nc, 3), s, d, p, f, nc);
+  }
+  if (p.implicitViscosity && p.useCDscheme) {   // dynamics.F:614-634
+    const long ncD = (long)(d.sNx + 2) * (d.sNy + 2) * d.nT;
+    const int nc = mg_colf_nc(ncD, d.Nr, 3);
+    MG_ALLOW_LDS(k_impldiff_cd<false>);
+    MG_ALLOW_LDS(k_impldiff_cd<true>);
+    hipLaunchKernelGGL(k_impldiff_cd<false>, dim3(mg_colf_blocks(ncD, nc)), dim3(256), mg_colf_lds(d.Nr, nc, 3), s, d, p, f, nc);
+    hipLaunchKernelGGL(k_impldiff_cd<true>, dim3(mg_colf_blocks(ncD, nc)), dim3(256), mg_colf_lds(d.Nr, nc, 3), s, d, p, f, nc);
   }
   return hipGetLastError();
 }

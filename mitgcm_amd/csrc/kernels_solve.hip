@@ -1452,6 +1452,93 @@ __global__ void __launch_bounds__(256) k_corr_cont(Dims d, Params p, Fields f, i
   }
 }
 
+// k_corr_cont as a k-march (deep grids, the step's call: atInit = 0, no r*): one thread per
+// interior column walks k = Nr..1 -- INTEGRATE_FOR_W's upward order -- forming the level's
+// corrected u, v (and the east / north neighbours', the same expressions), its divergence and w
+// in registers and storing them at once; the exactConserv column sum runs k = 1..Nr over the
+// maskC * divergence terms kept in registers (NRM slots, the unrolled loop's constant
+// indices).  No LDS round trip, no serial phase with one thread in eight busy.  The column's
+// operands arrive as __restrict__ parameters, so the next level's loads issue ahead of this
+// level's stores.  The same expression trees as k_corr_cont: bit-identical.
+template <int NR>
+__device__ __forceinline__ void corr_cont_column(const Dims &d, const Params &p, long q, long q3b, long nx, long n2,
+                                                 double pX0, double pX1, double pY0, double pY1, double dyG0, double dyG1,
+                                                 double dxG0, double dxG1, double rA1, const double *__restrict__ gU,
+                                                 const double *__restrict__ gV, const double *__restrict__ hFacW,
+                                                 const double *__restrict__ hFacS, const double *__restrict__ maskC,
+                                                 const double *__restrict__ drFv, double *__restrict__ uVel,
+                                                 double *__restrict__ vVel, double *__restrict__ wVel, double &hDiv) {
+  const double psFac = p.pfFacMom * p.implicSurfPress;
+  auto uCor = [&](long q3, double hW, double phiSurfX) {
+    const double mW = hW != 0.0 ? 1.0 : 0.0;
+    return (gU[q3] + p.deltaTMom * (-psFac * phiSurfX * mW)) * mW;
+  };
+  auto vCor = [&](long q3, double hS, double phiSurfY) {
+    const double mS = hS != 0.0 ? 1.0 : 0.0;
+    return (gV[q3] + p.deltaTMom * (-psFac * phiSurfY * mS)) * mS;
+  };
+  double prod[NR];
+  double wBelow = 0.0;
+#pragma unroll
+  for (int m = 0; m < NR; m++) {
+    const int k = NR - m;
+    const long q3c = q3b + (long)(k - 1) * n2, q3e = q3c + 1, q3n = q3c + nx;
+    const double hW0 = hFacW[q3c], hW1 = hFacW[q3e], hS0 = hFacS[q3c], hS1 = hFacS[q3n];
+    const double u0 = uCor(q3c, hW0, pX0), u1 = uCor(q3e, hW1, pX1);
+    const double v0 = vCor(q3c, hS0, pY0), v1 = vCor(q3n, hS1, pY1);
+    const double drF = drFv[k - 1];
+    const double uT1 = u1 * dyG1 * drF * hW1;
+    const double uT0 = u0 * dyG0 * drF * hW0;
+    const double vT1 = v1 * dxG1 * drF * hS1;
+    const double vT0 = v0 * dxG0 * drF * hS0;
+    const double div = uT1 - uT0 + vT1 - vT0;
+    const double mask = maskC[q3c];
+    prod[m] = mask * div;
+    const double conv2d = -div;
+    const double w = (m == 0) ? conv2d * rA1 * mask : (wBelow + conv2d * rA1) * mask;
+    wBelow = w;
+    wVel[q3c] = w;
+    uVel[q3c] = u0;
+    vVel[q3c] = v0;
+  }
+  hDiv = 0.0;
+#pragma unroll
+  for (int m = NR - 1; m >= 0; m--) hDiv = hDiv + prod[m];
+}
+template <int NR>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 2))) k_corr_cont_march(Dims d, Params p, Fields f, const long *__restrict__ etaSrc) {
+  const long g = (long)mg_xcd_block() * 256 + threadIdx.x;
+  const long nI = (long)d.sNx * d.sNy;
+  if (g >= nI * d.nT) return;
+  const int t = d.t0 + (int)(g / nI), l = (int)(g % nI);
+  const int i = 1 + l % d.sNx, j = 1 + l / d.sNx;
+  const long q = MG_I2(d, i, j, t), nx = d.nx;
+  auto eta = [&](long qq) {
+    if (!etaSrc) return f.etaN[qq];
+    const long sq = etaSrc[qq];
+    return f.recip_Bo[qq] * f.cg2d_x[sq >= 0 ? sq : qq];
+  };
+  auto phiX = [&](int ii, int jj) {
+    const long qq = MG_I2(d, ii, jj, t);
+    return f.recip_dxC[qq] * (f.Bo_surf[qq] * eta(qq) - f.Bo_surf[MG_I2(d, ii - 1, jj, t)] * eta(MG_I2(d, ii - 1, jj, t)));
+  };
+  auto phiY = [&](int ii, int jj) {
+    const long qq = MG_I2(d, ii, jj, t);
+    return f.recip_dyC[qq] * (f.Bo_surf[qq] * eta(qq) - f.Bo_surf[MG_I2(d, ii, jj - 1, t)] * eta(MG_I2(d, ii, jj - 1, t)));
+  };
+  const double pX0 = phiX(i, j), pX1 = phiX(i + 1, j), pY0 = phiY(i, j), pY1 = phiY(i, j + 1);
+  const double rA1 = f.recip_rA[q];
+  double hDiv;
+  corr_cont_column<NR>(d, p, q, MG_I3(d, i, j, 1, t), nx, d.n2, pX0, pX1, pY0, pY1, f.dyG[q], f.dyG[q + 1], f.dxG[q],
+                        f.dxG[q + nx], rA1, f.gU, f.gV, f.hFacW, f.hFacS, f.maskC, f.drF, f.uVel, f.vVel, f.wVel, hDiv);
+  if (p.exactConserv) {
+    const double facEmP = p.useRealFreshWaterFlux ? 1.0 / p.rhoConst : 0.0;   // integr_continuity.F:183-188
+    const double dEtaHdt = -(hDiv * rA1) - facEmP * f.EmPmR[q];
+    f.cg2d_b[q] = f.etaH[q] + p.implicDiv2DFlow * dEtaHdt * p.deltaTFreeSurf;
+    if (f.dEtaHdt) f.dEtaHdt[q] = dEtaHdt;
+  }
+}
+
 // Tile-sharded runs: gather (pack) / scatter (unpack) the halo-source points a peer
 // needs, for every exchanged field and level: buf[(f*Nr + k)*n + h] <-> field at 2-D
 // offset idx[h] (t*n2 + local) of level k.
@@ -1679,6 +1766,11 @@ hipError_t launch_corr_cont(const Dims &d, const Params &p, const Fields &f, int
   // deep grids: 32 columns per workgroup (LLC-90: 123 us against 140 at 16,
   // profiles/r03/colfnc/); shallow: 16 (config 2: 0.328-0.331 ms/step against 0.333 at 32,
   // profiles/r03/ab_trex_corrnc/)
+  const char *mEnv = getenv("MGCM_CORR_MARCH");
+  if (atInit == 0 && !(p.nonlinFreeSurf > 0 && p.select_rStar != 0) && d.Nr == 50 && (mEnv ? atoi(mEnv) != 0 : true)) {
+    hipLaunchKernelGGL(k_corr_cont_march<50>, dim3((unsigned)((ncol + 255) / 256)), dim3(256), 0, s, d, p, f, etaSrc);
+    return hipGetLastError();
+  }
   const int nc = d.Nr >= 30 ? 32 : 16;
   // (round 4: a two-column form with 16-byte loads was bit-identical but slower on LLC-90,
   // 151 against 137 us, profiles/r04/corr2/ -- the column frame is bound by its serial column

@@ -72,7 +72,7 @@ hipError_t launch_cg2d_blk2(const Dims &, const Params &, const Fields &, const 
 int cg2d_block_max_points();
 hipError_t launch_exchange(const Dims &, double *, const long *, int, int, hipStream_t);
 hipError_t launch_cgd(const Dims &, const Params &, const Fields &, int, double, double *, hipStream_t);
-hipError_t launch_cgd_record(SolveRecord *, const int *, double, double, double, double, int, hipStream_t);
+hipError_t launch_cgd_record(SolveRecord *, const int *, double, double, double, double, int, double, int, hipStream_t);
 hipError_t launch_field_pack(double *, const long *, long, double *, int, hipStream_t);
 hipError_t launch_correction(const Dims &, const Params &, const Fields &, hipStream_t);
 hipError_t launch_bump_counter(int *, int, hipStream_t);
@@ -1263,10 +1263,8 @@ int mgcm_init(mgcm_model *m) {
   if (m->p.selectP_inEOS_Zc > 2) return set_err("mgcm_init: selectP_inEOS_Zc = 3 needs the non-hydrostatic pressure");
   if (m->p.selectP_inEOS_Zc == 2 && !m->p.storePhiHyd4Phys)
     return set_err("mgcm_init: selectP_inEOS_Zc = 2 needs storePhiHyd4Phys (set_parms.F:297)");
-  // implicitViscosity: MOM_U/V_IMPLICIT_R (k_mom_impl); with the CD scheme the reference
-  // also runs IMPLDIFF on uVelD/vVelD (dynamics.F:614-634), not built
-  if (m->p.implicitViscosity && m->p.useCDscheme)
-    return set_err("mgcm_init: implicitViscosity with the CD scheme not implemented on the device");
+  // implicitViscosity: MOM_U/V_IMPLICIT_R (k_mom_impl); with the CD scheme also IMPLDIFF on
+  // vVelD / uVelD (dynamics.F:614-634, k_impldiff_cd)
   if (m->p.implicitViscosity && (ext("momImplVertAdv", 0.0) != 0.0 || ext("selectImplicitDrag", 0.0) != 0.0))
     return set_err("mgcm_init: momImplVertAdv / selectImplicitDrag not implemented on the device");
   if (m->p.vectorInvariantMomentum) {
@@ -2426,17 +2424,18 @@ int mgcm_cg2d_share(mgcm_model *m, mgcm_model *owner) {
 // process's tiles, per-tile partial sums into the device buffer part[2*nTiles].
 int mgcm_cg2d_op(mgcm_model *m, int op, double a0, double *part) {
   if (check_ready(m)) return -1;
-  if (op < 0 || op > 7) return set_err("mgcm_cg2d_op: no op %d", op);
-  if (!part && op != 1 && op != 4 && op != 7) return set_err("mgcm_cg2d_op: op %d needs the partials buffer", op);
-  if (m->p.cg2dUseMinResSol) return set_err("mgcm_cg2d_op: cg2dUseMinResSol not implemented in the distributed CG2D");
+  if (op < 0 || op > 15) return set_err("mgcm_cg2d_op: no op %d", op);
+  const bool sums = op == 0 || op == 2 || op == 3 || op == 5 || op == 6 || op == 10 || op == 13 || op == 14;
+  if (!part && sums) return set_err("mgcm_cg2d_op: op %d needs the partials buffer", op);
   HIPCHK(launch_cgd(m->d, m->p, m->f, op, a0, part, m->stream));
   return 0;
 }
 
 int mgcm_cg2d_record(mgcm_model *m, double firstResidual, double lastResidual, double rhsMax, double sumRHS,
-                     int numIters) {
+                     int numIters, double minResidualSq, int nIterMin) {
   if (check_ready(m)) return -1;
-  HIPCHK(launch_cgd_record(m->d_rec, m->d_ctr + 1, firstResidual, lastResidual, rhsMax, sumRHS, numIters, m->stream));
+  HIPCHK(launch_cgd_record(m->d_rec, m->d_ctr + 1, firstResidual, lastResidual, rhsMax, sumRHS, numIters, minResidualSq,
+                           nIterMin, m->stream));
   return 0;
 }
 

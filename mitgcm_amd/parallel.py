@@ -334,8 +334,6 @@ class ShardedModel:
             self._share_cg2d_handoff()
         elif cg2d == "device" and self.m.cg2d_kernel() != "mwg":
             raise ValueError('cg2d="device" needs the multi-workgroup CG2D (set the parameter cg2dForceMwg=1)')
-        if cg2d == "distributed" and model.params.get("useSRCGSolver", 0):
-            raise NotImplementedError("useSRCGSolver (CG2D_SR) with the distributed CG2D not implemented")
         if cg2d == "distributed":
             self.cg_part = torch.zeros(2 * g.nTiles, dtype=torch.float64, device=dv)   # part[2*tile + s]
             self.cg_local = torch.zeros((mt, 2), dtype=torch.float64, device=dv)
@@ -484,12 +482,19 @@ class ShardedModel:
     def _cg2d_distributed(self):
         """CG2D (model/src/cg2d.F:100-415) over the processes' tiles: 3 GLOBAL_SUM_TILE_RL
         and 2 EXCH_S3D_RL per iteration, scalars (beta, alpha, the residual) on the host
-        in the reference's arithmetic."""
+        in the reference's arithmetic; with useSRCGSolver CG2D_SR (cg2d_sr.F): one exchange
+        (y) and one round of sums per iteration; cg2dUseMinResSol keeps the lowest-residual
+        solution in both."""
         import math
         L, h, ck = self.L, self.m.h, self.check
         prm = lambda n: L.mgcm_get_param(h, n.encode())
         normalise = prm("cg2dNormaliseRHS") != 0.0
         tol_sq, maxit = prm("cg2dTolerance_sq"), int(prm("cg2dMaxIters"))
+        # cg2dUseMinResSol: SOLVE_FOR_PRESSURE passes nIterMin = cg2dUseMinResSol - 1, >= 0 keeps
+        # the lowest-residual solution (cg2d.F:148-155, 190-193, 338-351, 358-369)
+        keepMin = int(prm("cg2dUseMinResSol")) - 1 >= 0
+        sr = prm("useSRCGSolver") != 0.0
+        minResSq, nIterMin = -1.0, -1
         P = self._tile_sums(0)                         # cg2d.F:104-114, rhsMax per tile
         rhsMax = float(np.max(P[:, 0]))                # _GLOBAL_MAX_RL (order-free)
         rhsNorm = 1.0
@@ -499,11 +504,47 @@ class ShardedModel:
             ck(L.mgcm_cg2d_op(h, 1, rhsNorm, ctypes.c_void_p(self.cg_part.data_ptr())), "mgcm_cg2d_op(1)")
         self._exch_2d("cg2d_x")                        # EXCH_XY_RL(cg2d_x), cg2d.F:135
         P = self._tile_sums(2)                         # r = b - A x, cg2d.F:136-179
+        if keepMin:
+            ck(L.mgcm_cg2d_op(h, 8, 0.0, None), "mgcm_cg2d_op(8)")
         err_sq, sumRHS = tile_sum(P[:, 0]), tile_sum(P[:, 1])
         first, its = math.sqrt(err_sq), 0
+        if keepMin:
+            minResSq, nIterMin = err_sq, 0
         self._exch_2d("cg2d_r")
         eta_qrNM1 = 1.0
-        if not err_sq < tol_sq:
+        if sr and not err_sq < tol_sq:                 # CG2D_SR, cg2d_sr.F:220-422
+            eta_qrN = tile_sum(self._tile_sums(10)[:, 0])      # y = M r, s = y, (y, r)
+            self._exch_2d("cg2d_s")
+            eta_qrNM1 = eta_qrN
+            alpha = tile_sum(self._tile_sums(5)[:, 0])         # q = A s, (s, q)
+            sigma = eta_qrN / alpha
+            ck(L.mgcm_cg2d_op(h, 11, sigma, None), "mgcm_cg2d_op(11)")
+            self._exch_2d("cg2d_r")
+            conv, it = False, 1
+            while it <= maxit - 1:
+                ck(L.mgcm_cg2d_op(h, 12, 0.0, None), "mgcm_cg2d_op(12)")   # y = M r
+                self._exch_2d("cg2d_y")
+                P = self._tile_sums(13)                        # v = A y, (y, r), (y, v)
+                eta_qrN, delta = tile_sum(P[:, 0]), tile_sum(P[:, 1])
+                err_sq = tile_sum(self._tile_sums(14)[:, 0])   # (r, r)
+                if err_sq < tol_sq:
+                    conv = True
+                    break
+                if err_sq < minResSq:
+                    minResSq, nIterMin = err_sq, it
+                    ck(L.mgcm_cg2d_op(h, 8, 0.0, None), "mgcm_cg2d_op(8)")
+                cgBeta = eta_qrN / eta_qrNM1
+                eta_qrNM1 = eta_qrN
+                alpha = delta - (cgBeta * cgBeta) * alpha
+                sigma = eta_qrN / alpha
+                ck(L.mgcm_cg2d_op(h, 15, cgBeta, None), "mgcm_cg2d_op(15)")
+                ck(L.mgcm_cg2d_op(h, 11, sigma, None), "mgcm_cg2d_op(11)")
+                self._exch_2d("cg2d_r")
+                it += 1
+            if not conv:                               # the residual of the last update
+                err_sq = tile_sum(self._tile_sums(14)[:, 0])
+            its = it                                   # numIters = it2d (cg2d_sr.F:449)
+        elif not err_sq < tol_sq:
             for it in range(1, maxit + 1):
                 eta_qrN = tile_sum(self._tile_sums(3)[:, 0])   # q = M r, (q, r)
                 beta = eta_qrN / eta_qrNM1
@@ -515,10 +556,15 @@ class ShardedModel:
                 its = it
                 if err_sq < tol_sq:
                     break
+                if err_sq < minResSq:
+                    minResSq, nIterMin = err_sq, it
+                    ck(L.mgcm_cg2d_op(h, 8, 0.0, None), "mgcm_cg2d_op(8)")
                 self._exch_2d("cg2d_r")
+        if nIterMin >= 0 and err_sq > minResSq:
+            ck(L.mgcm_cg2d_op(h, 9, 0.0, None), "mgcm_cg2d_op(9)")
         if normalise:                                  # un-normalise, cg2d.F:372-385
             ck(L.mgcm_cg2d_op(h, 7, rhsNorm, ctypes.c_void_p(self.cg_part.data_ptr())), "mgcm_cg2d_op(7)")
-        ck(L.mgcm_cg2d_record(h, first, math.sqrt(err_sq), rhsMax, sumRHS, its), "mgcm_cg2d_record")
+        ck(L.mgcm_cg2d_record(h, first, math.sqrt(err_sq), rhsMax, sumRHS, its, minResSq, nIterMin), "mgcm_cg2d_record")
         self.cg_iters.append(its)
 
     # ---- stepping ----------------------------------------------------------------

@@ -18,9 +18,6 @@ static void check_supported(const OModel *m) {
   if ((m->viscA4D != 0.0 || m->viscA4Z != 0.0) && m->OLx < 3) {
     fprintf(stderr, "oracle_dynamics: biharmonic viscosity needs OLx, OLy >= 3\n"); abort();
   }
-  if (m->implicitViscosity && m->useCDscheme) {   /* dynamics.F:614-634 would IMPLDIFF uVelD/vVelD */
-    fprintf(stderr, "oracle_dynamics: implicitViscosity with the CD scheme not restated\n"); abort();
-  }
   if (!m->usingCartesianGrid && !m->usingSphericalPolarGrid &&
       !(m->usingCurvilinearGrid && m->vectorInvariantMomentum)) {
     fprintf(stderr, "oracle_dynamics: grid/momentum-scheme combination not restated\n"); abort();
@@ -73,6 +70,48 @@ static void mom_implicit_r(const OModel *m, double *g, const double *mask, const
 #undef W3
 #undef KAP
   free(sub); free(sup); free(cp); free(yp);
+}
+
+/* IMPLDIFF (model/src/impldiff.F:24-245) with tracerId = 0 (deltaTX = deltaTMom; deepFac =
+ * rhoFac = 1): the implicit vertical viscosity DYNAMICS applies to the CD scheme's D-grid
+ * velocities (dynamics.F:614-634) on i0..i1 x j0..j1, in place on g -- its own recurrence
+ * (bet, gam), not SOLVE_TRIDIAGONAL's: a(k) and c(k) vanish where recip_hFac of the level
+ * above / below is 0 (impldiff.F:109-145), bet = 1 / gam = 0 where a pivot is 0 (:147-201). */
+static void impldiff(const OModel *m, double *g, const double *rhFac, const double *kappa, int i0, int i1, int j0, int j1) {
+  const int OLx = m->OLx, OLy = m->OLy, Nr = m->Nr, nx = m->nx;
+  const long n2 = m->n2;
+  double *a = malloc(sizeof(double) * Nr), *c = malloc(sizeof(double) * Nr), *b = malloc(sizeof(double) * Nr);
+  double *bet = malloc(sizeof(double) * Nr), *gam = malloc(sizeof(double) * Nr), *lt = malloc(sizeof(double) * Nr);
+#define W3(a_, i, j, k) (a_)[(long)((i) + OLx - 1) + (long)((j) + OLy - 1) * nx + (long)((k) - 1) * n2]
+#define KAP(i, j, k) kappa[(long)((k) - 1) * n2 + ((i) + OLx - 1) + (long)((j) + OLy - 1) * nx]
+  for (int j = j0; j <= j1; j++)
+    for (int i = i0; i <= i1; i++) {
+      a[0] = 0.0;
+      for (int k = 2; k <= Nr; k++) {
+        a[k - 1] = -(m->deltaTMom * W3(rhFac, i, j, k) * m->recip_drF[k - 1] * KAP(i, j, k) * m->recip_drC[k - 1]);
+        if (W3(rhFac, i, j, k - 1) == 0.0) a[k - 1] = 0.0;
+      }
+      for (int k = 1; k <= Nr - 1; k++) {
+        c[k - 1] = -(m->deltaTMom * W3(rhFac, i, j, k) * m->recip_drF[k - 1] * KAP(i, j, k + 1) * m->recip_drC[k]);
+        if (W3(rhFac, i, j, k + 1) == 0.0) c[k - 1] = 0.0;
+      }
+      c[Nr - 1] = 0.0;
+      for (int k = 1; k <= Nr; k++) { b[k - 1] = 1.0 - (a[k - 1] + c[k - 1]); bet[k - 1] = 1.0; gam[k - 1] = 0.0; }
+      if (Nr > 1) {
+        if (b[0] != 0.0) bet[0] = 1.0 / b[0];
+        for (int k = 2; k <= Nr; k++) {
+          gam[k - 1] = c[k - 2] * bet[k - 2];
+          if ((b[k - 1] - a[k - 1] * gam[k - 1]) != 0.0) bet[k - 1] = 1.0 / (b[k - 1] - a[k - 1] * gam[k - 1]);
+        }
+      }
+      lt[0] = W3(g, i, j, 1) * bet[0];
+      for (int k = 2; k <= Nr; k++) lt[k - 1] = bet[k - 1] * (W3(g, i, j, k) - a[k - 1] * lt[k - 2]);
+      for (int k = Nr - 1; k >= 1; k--) lt[k - 1] = lt[k - 1] - gam[k] * lt[k];
+      for (int k = 1; k <= Nr; k++) W3(g, i, j, k) = lt[k - 1];
+    }
+#undef W3
+#undef KAP
+  free(a); free(c); free(b); free(bet); free(gam); free(lt);
 }
 
 void oracle_dynamics(OModel *m) {
@@ -821,6 +860,10 @@ void oracle_dynamics(OModel *m) {
     if (m->implicitViscosity && Nr > 1) {   /* dynamics.F:568-580 */
       mom_implicit_r(m, gU, maskW, rhFacW, kappaRU, 1, sNx + 1, 1, sNy);
       mom_implicit_r(m, gV, maskS, rhFacS, kappaRV, 1, sNx, 1, sNy + 1);
+    }
+    if (m->implicitViscosity && m->useCDscheme) {   /* dynamics.F:614-634: D-grid velocities */
+      impldiff(m, m->vVelD + t * m->n3, rhFacW, kappaRU, iMin, iMax, jMin, jMax);
+      impldiff(m, m->uVelD + t * m->n3, rhFacS, kappaRV, iMin, iMax, jMin, jMax);
     }
   }
   (void)ab;

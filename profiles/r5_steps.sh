@@ -20,6 +20,11 @@ for s in "$@"; do
     refhost_llc) timeout -k 10 300 $PY tests/test_gpu_refhost.py -k "llc30" > $O/refhost_llc.log 2>&1 ;;
     parity) timeout -k 10 500 $PY -x tests/test_gpu_llc.py tests/test_gpu_ocean90.py tests/test_gpu_cs32x15.py > $O/parity.log 2>&1 ;;
     auto_policy) timeout -k 10 400 $PY tests/test_gpu_parallel.py -k "auto" > $O/auto_policy.log 2>&1 ;;
+    dist_cg) timeout -k 10 600 $PY tests/test_gpu_parallel.py -k "distributed_cg2d" > $O/dist_cg.log 2>&1 ;;
+    march) bash profiles/march_ab.sh $T/march > $O/march.log 2>&1 ;;
+    options) timeout -k 10 600 $PY tests/test_gpu_options.py > $O/options.log 2>&1 ;;
+    rest) timeout -k 10 1000 $PY tests -m gpu --ignore=tests/test_gpu_refhost.py --ignore=tests/test_gpu_parallel.py \
+            --ignore=tests/test_gpu_rccl.py > $O/rest.log 2>&1 ;;
     parallel) timeout -k 10 1000 $PY tests/test_gpu_parallel.py tests/test_gpu_rccl.py > $O/parallel.log 2>&1 ;;
     llc) timeout -k 10 500 $PY -x tests/test_gpu_llc.py > $O/llc.log 2>&1 ;;
     bench_llc) timeout -k 10 300 python bench.py --config llc90_synthetic --steps 30 --warmup 4 --no-cs32 --no-cpu-baseline > $O/bench_llc.json 2> $O/bench_llc.err; tail -c 300 $O/bench_llc.json ;;

@@ -4,6 +4,8 @@ implements on top of them:
   * implicitViscosity: MOM_U_IMPLICIT_R / MOM_V_IMPLICIT_R (pkg/mom_common/mom_u_implicit_r.F,
     dynamics.F:568-580) on the flux-form (tutorial_baroclinic_gyre) and vector-invariant
     (global_ocean.cs32x15: cube, r*, stagger) momentum paths;
+  * implicitViscosity with the CD scheme: IMPLDIFF on the D-grid velocities (impldiff.F,
+    dynamics.F:614-634) on global_ocean.90x40x15;
   * tempAdvScheme = 30: DST3 without limiter (gad_dst3_adv_x.F:71-118, gad_dst3_adv_r.F:70-119)
     through the multi-dimensional split, lat-lon (baroclinic gyre) and cube (cs32x15).
 
@@ -151,3 +153,49 @@ def test_overlap_trial_leaves_the_state_untouched():
     assert a.solve_stats() == b.solve_stats()
     a.close()
     b.close()
+
+
+# implicitViscosity with the CD scheme (BASELINE config 2 carries useCDscheme): after
+# MOM_U/V_IMPLICIT_R on gU, gV, DYNAMICS runs IMPLDIFF on the D-grid velocities vVelD
+# (kappaRU, recip_hFacW) and uVelD (kappaRV, recip_hFacS) (dynamics.F:614-634, impldiff.F);
+# k_impldiff_cd against the oracle's restatement: one DYNAMICS bit-exact on the ring
+# 0..sN+1, and 4 steps within 1e-10 of each field's maximum.
+def test_ocean90_cd_implicit_viscosity_dynamics_bitexact():
+    from mitgcm_amd import configs
+    from oracle.harness import ocean90_oracle
+    over = {"implicitViscosity": 1}
+    o, g = ocean90_oracle(params_over=over)
+    for _ in range(2):
+        o.forward_step()
+    o.L.oracle_fields_load(o.h)
+    o.L.oracle_oceanic_phys(o.h)
+    m = configs.make_model(lambda: configs.global_ocean_90x40x15(params_over=over))
+    from test_gpu_ocean90 import STATE
+    _put_state(m, o, STATE + ("rhoInSitu", "fu", "fv"))
+    m.dynamics()
+    o.L.oracle_dynamics(o.h)
+    ring = (Ellipsis,) + g.sl(0, g.sNx + 1, 0, g.sNy + 1)
+    bad = []
+    for n in ("gU", "gV", "uVelD", "vVelD"):
+        dev, ref = m.get(n), np.array(o.arr(n)).reshape(m.get(n).shape)
+        if not np.array_equal(dev[ring], ref[ring]):
+            bad.append((n, float(np.abs(dev[ring] - ref[ring]).max())))
+    m.close()
+    assert not bad, bad
+
+
+def test_ocean90_cd_implicit_viscosity_4_steps_vs_oracle():
+    from mitgcm_amd import configs
+    from oracle.harness import ocean90_oracle
+    over = {"implicitViscosity": 1}
+    o, g = ocean90_oracle(params_over=over)
+    m = configs.make_model(lambda: configs.global_ocean_90x40x15(params_over=over))
+    for _ in range(4):
+        o.forward_step()
+    m.forward_step(4)
+    m.sync()
+    for n in ("uVel", "vVel", "theta", "salt", "etaN", "uVelD", "vVelD"):
+        dev, ref = m.get(n), np.array(o.arr(n)).reshape(m.get(n).shape)
+        sc = np.abs(ref).max()
+        assert np.abs(dev - ref).max() <= 1e-10 * sc, (n, np.abs(dev - ref).max(), sc)
+    m.close()

@@ -27,8 +27,18 @@ def _free_port():
     return port
 
 
+# option variants of the solver: cfg + "_minres" keeps the lowest-residual solution
+# (cg2dUseMinResSol, 8 iterations at most so that the solve stops above its minimum),
+# cfg + "_sr" solves with CG2D_SR (useSRCGSolver)
+SOLVER_VARIANTS = {"minres": {"cg2dUseMinResSol": 1, "cg2dMaxIters": 8}, "sr": {"useSRCGSolver": 1}}
+
+
 def _make(cfg, force_mwg=False):
     from mitgcm_amd import configs
+    over = {}
+    for v, o in SOLVER_VARIANTS.items():
+        if cfg.endswith("_" + v):
+            cfg, over = cfg[:-len(v) - 1], o
     if cfg == "gyre":
         fn = lambda: configs.baroclinic_gyre(tempAdvScheme=33)
     elif cfg == "llc30":   # BASELINE config 5's LLC topology at n = 30 (13 tiles, pkg/exch2 facets)
@@ -38,7 +48,9 @@ def _make(cfg, force_mwg=False):
     else:
         fn = configs.global_ocean_cs32x15
     if force_mwg:   # the multi-workgroup CG2D also where a single-workgroup kernel would be chosen
-        fn = (lambda f: lambda: (lambda r: (r[0], {**r[1], "cg2dForceMwg": 1}) + tuple(r[2:]))(f()))(fn)
+        over = {**over, "cg2dForceMwg": 1}
+    if over:
+        fn = (lambda f: lambda: (lambda r: (r[0], {**r[1], **over}) + tuple(r[2:]))(f()))(fn)
     return configs.make_model(fn)
 
 
@@ -64,7 +76,8 @@ def _worker(rank, world, port, cfg, nsteps, q, cg2d="replicated", overlap="therm
         m.sync()
         full = {n: sm.gather_field(n) for n in FIELDS}
         stats = [m.solve_stats(back=b) for b in range(nsteps)]
-        res = {"t0": sm.t0, "nT": sm.nT, "stats": stats, "overlap": sm.overlap, "fork": sm.fork, "cg2d": sm.cg2d,
+        minres = [m.solve_minres(back=b) for b in range(nsteps)]
+        res = {"t0": sm.t0, "nT": sm.nT, "stats": stats, "minres": minres, "overlap": sm.overlap, "fork": sm.fork, "cg2d": sm.cg2d,
                "cg2d_reason": sm.cg2d_reason}
         if cg2d == "distributed":
             res["iters"] = list(sm.cg_iters)
@@ -77,6 +90,7 @@ def _worker(rank, world, port, cfg, nsteps, q, cg2d="replicated", overlap="therm
             res["diff"] = {n: float(np.max(np.abs(full[n] - ref.get(n)))) for n in FIELDS}
             res["equal"] = {n: bool(np.array_equal(full[n], ref.get(n))) for n in FIELDS}
             res["ref_stats"] = [ref.solve_stats(back=b) for b in range(nsteps)]
+            res["ref_minres"] = [ref.solve_minres(back=b) for b in range(nsteps)]
             ref.close()
         m.close()
         q.put((rank, res))
@@ -145,13 +159,15 @@ def _spawn(cfg, world, nsteps, cg2d):
     return out
 
 
-@pytest.mark.parametrize("cfg,worlds,nsteps", [("gyre", (1, 2, 4), 4), ("cs32x15", (1, 3, 6), 3)])
+@pytest.mark.parametrize("cfg,worlds,nsteps", [("gyre", (1, 2, 4), 4), ("cs32x15", (1, 3, 6), 3),
+                                               ("gyre_minres", (1, 2, 4), 3), ("cs32x15_sr", (1, 2, 3), 3)])
 def test_distributed_cg2d(cfg, worlds, nsteps):
     """cg2d="distributed": the reference's CG2D over the processes' tiles, its global sums
-    GLOBAL_SUM_TILE_RL (all-gather of per-tile partials, added in tile order).  Bars: the
+    GLOBAL_SUM_TILE_RL (all-gather of per-tile partials, added in tile order); also with
+    cg2dUseMinResSol (cg2d.F:148-155, 338-369) and with CG2D_SR (cg2d_sr.F).  Bars: the
     fields and every solve record identical bit for bit at every process count; against
-    the replicated single-process solve (other summation order) the same iteration counts
-    and fields within 1e-10 of their maximum."""
+    the replicated single-process solve (other summation order) the same iteration counts,
+    the same lowest-residual iteration, and fields within 1e-10 of their maximum."""
     runs = {w: _spawn(cfg, w, nsteps, "distributed") for w in worlds}
     base = runs[worlds[0]][0]
     for w in worlds[1:]:
@@ -161,7 +177,11 @@ def test_distributed_cg2d(cfg, worlds, nsteps):
         for rank, r in runs[w].items():
             assert r["stats"] == base["stats"], (w, rank)
             assert r["iters"] == base["iters"], (w, rank)
+            assert r["minres"] == base["minres"], (w, rank)
     its_rep = [s["cg2d_iters"] for s in base["ref_stats"]]
+    assert [n for _, n in base["minres"]] == [n for _, n in base["ref_minres"]], (base["minres"], base["ref_minres"])
+    if cfg.endswith("_minres"):
+        assert all(n >= 0 for _, n in base["minres"]), base["minres"]
     its_dist = [s["cg2d_iters"] for s in base["stats"]]
     print("%s distributed CG2D iterations %s (replicated %s); max |diff| vs replicated %s" % (
         cfg, its_dist, its_rep, base["diff"]))

@@ -43,3 +43,4 @@ def test_dst3_scheme30_differs_from_33_and_stays_bounded():
     assert np.isfinite(t30).all()
     assert not np.array_equal(t30[inner], t33[inner])
     assert np.abs(t30[inner] - t33[inner]).max() < 1e-3
+
