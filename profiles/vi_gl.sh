@@ -1,6 +1,7 @@
 #!/bin/bash
 # Round-5 A/B: the VI k-march with its next level staged by LDS-DMA (MGCM_VI_GL=1) against the
 # register path, LLC-90 alternating; then the LLC parity tests with the DMA form.
+# (the recipe of profiles/r05/vi_gl/; the MGCM_VI_GL variant was measured slower and removed)
 #   bash profiles/vi_gl.sh <out-tag>
 set -o pipefail
 cd "$GRAFT_REPO_ROOT" 2>/dev/null || cd /root/repo
