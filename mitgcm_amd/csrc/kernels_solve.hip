@@ -163,6 +163,61 @@ __global__ void __launch_bounds__(256) k_sfp_rhs(Dims d, Params p, Fields f, int
   sfp_rhs_column(d, p, f, q, inner, sE, sW, sN, sS, NC_, cc);
 }
 
+// k_sfp_rhs as a k-march at a fixed depth NR (A/B against the frame): one thread per column,
+// k = NR..1 fully unrolled (sfp_rhs_column's order), the four face terms in registers.  The
+// same expression trees as k_sfp_rhs + sfp_rhs_column: bit-identical.
+template <int NR>
+__device__ __forceinline__ double sfp_column_sum(double b, long q3b, long nx, long n2, double dyW, double dyE, double dxS,
+                                                 double dxN, double dT, const double *__restrict__ drFv,
+                                                 const double *__restrict__ hFacW, const double *__restrict__ hFacS,
+                                                 const double *__restrict__ gU, const double *__restrict__ gV) {
+  // batches of SB levels: the batch's 8*SB operands are loaded before its first sum
+  constexpr int SB = 10;
+  static_assert(NR % SB == 0, "whole batches");
+#pragma unroll
+  for (int k0 = NR; k0 >= 1; k0 -= SB) {
+    double hWe[SB], hWw[SB], uE[SB], uW[SB], hSn[SB], hSs[SB], vN[SB], vS[SB];
+#pragma unroll
+    for (int m = 0; m < SB; m++) {
+      const long q3 = q3b + (long)(k0 - m - 1) * n2;
+      hWe[m] = hFacW[q3 + 1]; uE[m] = gU[q3 + 1]; hWw[m] = hFacW[q3]; uW[m] = gU[q3];
+      hSn[m] = hFacS[q3 + nx]; vN[m] = gV[q3 + nx]; hSs[m] = hFacS[q3]; vS[m] = gV[q3];
+    }
+#pragma unroll
+    for (int m = 0; m < SB; m++) {
+      const double drF = drFv[k0 - m - 1];
+      const double sE = dyE * drF * hWe[m] * uE[m] / dT;
+      const double sW = dyW * drF * hWw[m] * uW[m] / dT;
+      const double sN = dxN * drF * hSn[m] * vN[m] / dT;
+      const double sS = dxS * drF * hSs[m] * vS[m] / dT;
+      b = b + sE - sW;
+      b = b + sN - sS;
+    }
+  }
+  return b;
+}
+template <int NR>
+__global__ void __launch_bounds__(256) k_sfp_rhs_march(Dims d, Params p, Fields f) {
+  const long g = (long)mg_xcd_block() * 256 + threadIdx.x;
+  if (g >= d.n2 * d.nT) return;
+  const int t = d.t0 + (int)(g / d.n2);
+  const long r = g % d.n2, nx = d.nx, n2 = d.n2;
+  const int i = (int)(r % nx) + 1 - d.OLx, j = (int)(r / nx) + 1 - d.OLy;
+  const long q = (long)t * n2 + r;
+  double b = 0.0;
+  if (i >= 1 && i <= d.sNx && j >= 1 && j <= d.sNy) {
+    if (p.useRealFreshWaterFlux) {
+      const double tmpFac = p.freeSurfFac * (1.0 / p.rhoConst) * p.implicDiv2DFlow;
+      b = tmpFac * f.rA[q] * f.EmPmR[q] / p.deltaTMom * f.maskInC[q];
+    }
+    b = sfp_column_sum<NR>(b, (long)t * d.n3 + r, nx, n2, f.dyG[q], f.dyG[q + 1], f.dxG[q], f.dxG[q + nx], p.deltaTMom,
+                           f.drF, f.hFacW, f.hFacS, f.gU, f.gV);
+    b = b - p.freeSurfFac * f.rA[q] / p.deltaTMom / p.deltaTFreeSurf * (p.exactConserv ? f.etaH[q] : f.etaN[q]);
+  }
+  f.cg2d_x[q] = f.Bo_surf[q] * f.etaN[q];
+  f.cg2d_b[q] = b;
+}
+
 // Whole-solve CG2D in one workgroup.  PPT = interior points per thread.
 // Points are padded to NP = PPT*1024: a padding point has x = b = 0, every
 // neighbour index pointing at the ZERO slot (index NP, never written), so it
@@ -1561,6 +1616,10 @@ __global__ void k_bump_counter(int *c, int nIncr) {
 // ------------------------------------------------------------------ launchers
 hipError_t launch_sfp_rhs(const Dims &d, const Params &p, const Fields &f, hipStream_t s) {
   const long ncol = (long)d.nx * d.ny * d.nT;
+  if (!p.useCDscheme && d.Nr == 50 && getenv("MGCM_SFP_MARCH") && atoi(getenv("MGCM_SFP_MARCH")) != 0) {
+    hipLaunchKernelGGL(k_sfp_rhs_march<50>, dim3((unsigned)((ncol + 255) / 256)), dim3(256), 0, s, d, p, f);
+    return hipGetLastError();
+  }
   // mg_colf_nc's 16 columns (LLC-90: 63 us at 16, 69 at 32, 115 at 64; profiles/r04/sfpnc/,
   // where the correction pass's 32 is confirmed too)
   const int nc = mg_colf_nc(ncol, d.Nr, 4);
@@ -1766,8 +1825,9 @@ hipError_t launch_corr_cont(const Dims &d, const Params &p, const Fields &f, int
   // deep grids: 32 columns per workgroup (LLC-90: 123 us against 140 at 16,
   // profiles/r03/colfnc/); shallow: 16 (config 2: 0.328-0.331 ms/step against 0.333 at 32,
   // profiles/r03/ab_trex_corrnc/)
-  const char *mEnv = getenv("MGCM_CORR_MARCH");
-  if (atInit == 0 && !(p.nonlinFreeSurf > 0 && p.select_rStar != 0) && d.Nr == 50 && (mEnv ? atoi(mEnv) != 0 : true)) {
+  // the k-march at BASELINE config 5's depth (round 5: LLC-90 1.445 against 1.475-1.481 ms/step
+  // for the frame, alternating on one box, profiles/r05/corr_march/)
+  if (atInit == 0 && !(p.nonlinFreeSurf > 0 && p.select_rStar != 0) && d.Nr == 50) {
     hipLaunchKernelGGL(k_corr_cont_march<50>, dim3((unsigned)((ncol + 255) / 256)), dim3(256), 0, s, d, p, f, etaSrc);
     return hipGetLastError();
   }

@@ -1,6 +1,7 @@
 #!/bin/bash
 # Round-5 A/B on LLC-90: the correction + continuity pass as an LDS column frame or a k-march
-# (MGCM_CORR_MARCH = 0 | 1; MGCM_SFP_MARCH: the CALC_DIV_GHAT k-march, since removed), alternating, then the
+# (MGCM_SFP_MARCH = 0 | 1 at fixed depth, round 5; MGCM_CORR_MARCH: the correction pass, whose k-march
+# became the default), alternating, then the
 # LLC parity tests with both k-marches.
 #   bash profiles/march_ab.sh <out-tag>
 set -o pipefail
@@ -8,7 +9,7 @@ cd "$GRAFT_REPO_ROOT" 2>/dev/null || cd /root/repo
 export TMPDIR=/tmp
 O=gpurun_out/$1
 mkdir -p $O
-for v in 00 01 00 01 00 01; do
+for v in 00 10 00 10 00 10; do
   MGCM_SFP_MARCH=${v:0:1} MGCM_CORR_MARCH=${v:1:1} timeout -k 10 200 python bench.py --config llc90_synthetic --steps 40 \
     --warmup 4 --no-cs32 --no-cpu-baseline > $O/bench_$v.json 2> $O/bench_$v.err || { tail -20 $O/bench_$v.err; exit 1; }
   python -c "
