@@ -163,9 +163,11 @@ __global__ void __launch_bounds__(256) k_sfp_rhs(Dims d, Params p, Fields f, int
   sfp_rhs_column(d, p, f, q, inner, sE, sW, sN, sS, NC_, cc);
 }
 
-// k_sfp_rhs as a k-march at a fixed depth NR (A/B against the frame): one thread per column,
-// k = NR..1 fully unrolled (sfp_rhs_column's order), the four face terms in registers.  The
-// same expression trees as k_sfp_rhs + sfp_rhs_column: bit-identical.
+// k_sfp_rhs as a k-march at a fixed depth NR: one thread per column, k = NR..1 fully unrolled
+// (sfp_rhs_column's order), each batch of levels' operands loaded before its sums (about 40
+// loads in flight per wave: the 105 300 columns of LLC-90 give only 1.6 waves per SIMD), the
+// four face terms in registers.  The same expression trees as k_sfp_rhs + sfp_rhs_column:
+// bit-identical.
 template <int NR>
 __device__ __forceinline__ double sfp_column_sum(double b, long q3b, long nx, long n2, double dyW, double dyE, double dxS,
                                                  double dxN, double dT, const double *__restrict__ drFv,
@@ -1616,7 +1618,10 @@ __global__ void k_bump_counter(int *c, int nIncr) {
 // ------------------------------------------------------------------ launchers
 hipError_t launch_sfp_rhs(const Dims &d, const Params &p, const Fields &f, hipStream_t s) {
   const long ncol = (long)d.nx * d.ny * d.nT;
-  if (!p.useCDscheme && d.Nr == 50 && getenv("MGCM_SFP_MARCH") && atoi(getenv("MGCM_SFP_MARCH")) != 0) {
+  // the k-march at BASELINE config 5's depth (round 5: LLC-90 45.5 against 63.4 us, step 1.419-1.420
+  // against 1.438-1.443 ms, profiles/r05/sfp_march2/; the same march with a run-time loop kept one
+  // level of loads in flight and took 138 us, profiles/r05/sfp_march/)
+  if (!p.useCDscheme && d.Nr == 50) {
     hipLaunchKernelGGL(k_sfp_rhs_march<50>, dim3((unsigned)((ncol + 255) / 256)), dim3(256), 0, s, d, p, f);
     return hipGetLastError();
   }
