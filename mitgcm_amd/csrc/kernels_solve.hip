@@ -1563,7 +1563,7 @@ __device__ __forceinline__ void corr_cont_column(const Dims &d, const Params &p,
   for (int m = NR - 1; m >= 0; m--) hDiv = hDiv + prod[m];
 }
 template <int NR>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 2))) k_corr_cont_march(Dims d, Params p, Fields f, const long *__restrict__ etaSrc) {
+__global__ void __launch_bounds__(256) k_corr_cont_march(Dims d, Params p, Fields f, const long *__restrict__ etaSrc) {
   const long g = (long)mg_xcd_block() * 256 + threadIdx.x;
   const long nI = (long)d.sNx * d.sNy;
   if (g >= nI * d.nT) return;
@@ -1833,6 +1833,8 @@ hipError_t launch_corr_cont(const Dims &d, const Params &p, const Fields &f, int
   // the k-march at BASELINE config 5's depth (round 5: LLC-90 1.445 against 1.475-1.481 ms/step
   // for the frame, alternating on one box, profiles/r05/corr_march/)
   if (atInit == 0 && !(p.nonlinFreeSurf > 0 && p.select_rStar != 0) && d.Nr == 50) {
+    // (levels one at a time: loading batches of 5 or 10 levels ahead measured slower, 103
+    // against 87 us, profiles/r05/corr_sb/)
     hipLaunchKernelGGL(k_corr_cont_march<50>, dim3((unsigned)((ncol + 255) / 256)), dim3(256), 0, s, d, p, f, etaSrc);
     return hipGetLastError();
   }

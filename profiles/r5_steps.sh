@@ -22,6 +22,8 @@ for s in "$@"; do
     auto_policy) timeout -k 10 400 $PY tests/test_gpu_parallel.py -k "auto" > $O/auto_policy.log 2>&1 ;;
     dist_cg) timeout -k 10 600 $PY tests/test_gpu_parallel.py -k "distributed_cg2d" > $O/dist_cg.log 2>&1 ;;
     march) bash profiles/march_ab.sh $T/march > $O/march.log 2>&1 ;;
+    corr_sb) bash profiles/corr_sb.sh $T/corr_sb > $O/corr_sb.log 2>&1 ;;
+    vlead) bash profiles/vlead_ab.sh $T/vlead > $O/vlead.log 2>&1 ;;
     options) timeout -k 10 600 $PY tests/test_gpu_options.py > $O/options.log 2>&1 ;;
     rest) timeout -k 10 1000 $PY tests -m gpu --ignore=tests/test_gpu_refhost.py --ignore=tests/test_gpu_parallel.py \
             --ignore=tests/test_gpu_rccl.py > $O/rest.log 2>&1 ;;
