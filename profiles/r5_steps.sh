@@ -24,6 +24,7 @@ for s in "$@"; do
     march) bash profiles/march_ab.sh $T/march > $O/march.log 2>&1 ;;
     corr_sb) bash profiles/corr_sb.sh $T/corr_sb > $O/corr_sb.log 2>&1 ;;
     vlead) bash profiles/vlead_ab.sh $T/vlead > $O/vlead.log 2>&1 ;;
+    phi_ab) bash profiles/env_ab2.sh $T/phi_ab MGCM_PHI_N50 > $O/phi_ab.log 2>&1 ;;
     options) timeout -k 10 600 $PY tests/test_gpu_options.py > $O/options.log 2>&1 ;;
     rest) timeout -k 10 1000 $PY tests -m gpu --ignore=tests/test_gpu_refhost.py --ignore=tests/test_gpu_parallel.py \
             --ignore=tests/test_gpu_rccl.py > $O/rest.log 2>&1 ;;
