@@ -138,9 +138,13 @@ struct Fields {
   // the 2-D and 3-D arenas (MG_F2D_LIST / MG_F3D_LIST order)
   double *a2, *a3;
 };
-// field x at flat offset q of its kind's arena (one base pointer for every field)
-#define AR2(x, q) f.a2[(long)F2_##x * d.N2all + (q)]
-#define AR3(x, q) f.a3[(long)F3_##x * d.N3all + (q)]
+// field x at flat offset q of its kind's arena (one base pointer for every field), addressed as
+// global memory: a kernel that launders the arena bases through an asm statement (k_mom_vi_m2)
+// would otherwise reach them with flat instructions, which count on the LDS counter too, so
+// every LDS wait after such a store waits for the store
+typedef __attribute__((address_space(1))) double mg_gdouble;
+#define AR2(x, q) ((mg_gdouble *)f.a2)[(long)F2_##x * d.N2all + (q)]
+#define AR3(x, q) ((mg_gdouble *)f.a3)[(long)F3_##x * d.N3all + (q)]
 
 #define MG_I2(d, i, j, t) \
   ((long)((i) + (d).OLx - 1) + (long)((j) + (d).OLy - 1) * (d).nx + (long)(t) * (d).n2)

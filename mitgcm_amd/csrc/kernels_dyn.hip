@@ -220,7 +220,7 @@ __global__ void __launch_bounds__(256) k_phi_hyd(Dims d, Params p, Fields f, int
 // stored as the sums pass -- no LDS staging, no barrier, no thread idle while one thread per
 // column sums.  The same expressions in the same order as phi_hyd_body: bit-identical.
 constexpr int PHI_CH = 10;   // levels per chunk (5 with the r* / QH operands)
-template <bool RS, bool QH>
+template <bool RS, bool QH, int NRC = 0>
 __device__ __forceinline__ void phi_flat_body(const Dims &d, const Params &p, const Fields &f, int lb) {
   constexpr int o = RS ? 1 : 0;
   const int W = d.sNx + 2 + o, H = d.sNy + 2 + o;
@@ -229,7 +229,7 @@ __device__ __forceinline__ void phi_flat_body(const Dims &d, const Params &p, co
   const int t = d.t0 + (int)(col / npl), r = (int)(col % npl);
   const int i = r % W - o, j = r / W - o;
   const bool ring = i >= 0 && j >= 0;
-  const int Nr = d.Nr;
+  const int Nr = NRC > 0 ? NRC : d.Nr;   // NRC: the depth as a constant (the chunk loop unrolled)
   constexpr int CH = (RS || QH) ? 5 : PHI_CH;   // (8 operand arrays per level under r* + QH)
   const double recip_rhoConst = 1.0 / p.rhoConst;
   const double scalingFactor = p.rhoConst * p.gravitySign * (1.0 / p.gravity);
@@ -250,13 +250,20 @@ __device__ __forceinline__ void phi_flat_body(const Dims &d, const Params &p, co
   const double fac = tot && totR ? f.rStarFacC[q2] : 0.0, roS = tot && totR ? f.Ro_surf[q2] : 0.0;
   const double fCos = QH ? f.fCoriCos[q2] : 0.0;
   double phF = 0.0;
-  for (int k0 = 1; k0 <= Nr; k0 += CH) {
-    double a[CH], u0[CH], u1[CH], v0[CH], v1[CH], hC[CH], hW[CH], hS[CH];
+  auto chunk = [&](const int k0) {
+    double a[CH], u0[CH], u1[CH], v0[CH], v1[CH], hC[CH], hW[CH], hS[CH], dM[CH], dP[CH];
 #pragma unroll
     for (int cc = 0; cc < CH; cc++) {
       const int k = k0 + cc <= Nr ? k0 + cc : Nr;   // (clamped: the extra levels are not used)
       const long q3 = MG_I3(d, i, j, k, t);
       a[cc] = f.rhoInSitu[q3];
+      if constexpr (NRC > 0) {
+        // at a constant depth the level's half-cell thicknesses are fetched with the chunk's
+        // operands: a 1-D load between the level's stores would wait for them (vmcnt counts
+        // stores too)
+        dM[cc] = (k == 1) ? f.rF[0] - f.rC[0] : 0.5 * f.drC[k - 1];
+        dP[cc] = (k == Nr) ? (f.rC[k - 1] - f.rF[k]) : 0.5 * f.drC[k];
+      }
       if (QH) {
         u0[cc] = f.uVel[q3]; u1[cc] = f.uVel[MG_I3(d, i + 1, j, k, t)];
         v0[cc] = f.vVel[q3]; v1[cc] = f.vVel[MG_I3(d, i, j + 1, k, t)];
@@ -271,9 +278,15 @@ __device__ __forceinline__ void phi_flat_body(const Dims &d, const Params &p, co
       const int k = k0 + cc;
       if (k > Nr) continue;
       const long q3 = MG_I3(d, i, j, k, t);
-      double dRlocM = 0.5 * f.drC[k - 1];
-      if (k == 1) dRlocM = f.rF[0] - f.rC[0];
-      const double dRlocP = (k == Nr) ? (f.rC[k - 1] - f.rF[k]) : 0.5 * f.drC[k];
+      double dRlocM, dRlocP;
+      if constexpr (NRC > 0) {
+        dRlocM = dM[cc];
+        dRlocP = dP[cc];
+      } else {
+        dRlocM = 0.5 * f.drC[k - 1];
+        if (k == 1) dRlocM = f.rF[0] - f.rC[0];
+        dRlocP = (k == Nr) ? (f.rC[k - 1] - f.rF[k]) : 0.5 * f.drC[k];
+      }
       double al = a[cc];
       if (QH) {
         double gW = 0.0;
@@ -312,11 +325,17 @@ __device__ __forceinline__ void phi_flat_body(const Dims &d, const Params &p, co
         }
       }
     }
+  };
+  if constexpr (NRC > 0) {
+#pragma unroll
+    for (int k0 = 1; k0 <= NRC; k0 += CH) chunk(k0);
+  } else {
+    for (int k0 = 1; k0 <= Nr; k0 += CH) chunk(k0);
   }
 }
-template <bool RS, bool QH>
+template <bool RS, bool QH, int NRC = 0>
 __global__ void __launch_bounds__(256) k_phi_flat(Dims d, Params p, Fields f) {
-  phi_flat_body<RS, QH>(d, p, f, mg_xcd_block());
+  phi_flat_body<RS, QH, NRC>(d, p, f, mg_xcd_block());
 }
 
 // whether CALC_PHI_HYD runs the flat pass: by default where neither r* nor the QH terms add
@@ -2426,6 +2445,9 @@ hipError_t launch_phi_hyd(const Dims &d, const Params &p, const Fields &f, hipSt
     // against 30.4 us -- half the threads leave the chip under-filled; removed in round 5)
     auto kern = rstar ? (qh ? k_phi_flat<true, true> : k_phi_flat<true, false>)
                       : (qh ? k_phi_flat<false, true> : k_phi_flat<false, false>);
+    // at BASELINE config 5's depth the chunk loop unrolled (round 5: LLC-90 24.3 against 30 us,
+    // step 1.416-1.418 ms, profiles/r05/phi_n50/)
+    if (!rstar && !qh && d.Nr == 50) kern = k_phi_flat<false, false, 50>;
     hipLaunchKernelGGL(kern, dim3((unsigned)phi_flat_blocks(d, p)), dim3(256), 0, s, d, p, f);
     return hipGetLastError();
   }

@@ -25,6 +25,9 @@ for s in "$@"; do
     corr_sb) bash profiles/corr_sb.sh $T/corr_sb > $O/corr_sb.log 2>&1 ;;
     vlead) bash profiles/vlead_ab.sh $T/vlead > $O/vlead.log 2>&1 ;;
     phi_ab) bash profiles/env_ab2.sh $T/phi_ab MGCM_PHI_N50 > $O/phi_ab.log 2>&1 ;;
+    libab) OUT=$O/libab CONFIGS="llc90_synthetic global_ocean.90x40x15 global_ocean.cs32x15" \
+             LIBS="default flat:mitgcm_amd/_build/diag/libmitgcm_amd_flat.so" bash tools/lib_ab.sh > $O/libab.log 2>&1 ;;
+    llc_par) timeout -k 10 500 $PY -x tests/test_gpu_llc.py > $O/llc_par.log 2>&1 ;;
     options) timeout -k 10 600 $PY tests/test_gpu_options.py > $O/options.log 2>&1 ;;
     rest) timeout -k 10 1000 $PY tests -m gpu --ignore=tests/test_gpu_refhost.py --ignore=tests/test_gpu_parallel.py \
             --ignore=tests/test_gpu_rccl.py > $O/rest.log 2>&1 ;;
