@@ -368,6 +368,19 @@ __global__ void __launch_bounds__(256) k_phi_del2(Dims d, Params p, Fields f, in
 }
 
 
+// Values the VI helpers read outside the level's staged fields -- the tile's face and edge
+// bits, the vertical grid's 1-D factors, the own point's rest-state thicknesses -- through
+// these functions of the accessor: by default where they lie; k_mom_vi_m2's accessor
+// (overloads after VIM2) hands them over from registers filled at the level's start, so no
+// load of them waits behind the level's stores (vmcnt counts stores too).
+template <class A> __device__ __forceinline__ int vi_tile_face(const A &, const Fields &f, int t) { return f.tileFace[t]; }
+template <class A> __device__ __forceinline__ int vi_tile_edge(const A &, const Fields &f, int t) { return f.tileEdge[t]; }
+template <class A> __device__ __forceinline__ double vi_rdrC(const A &, const Fields &f, int kk) { return f.recip_drC[kk - 1]; }
+template <class A> __device__ __forceinline__ double vi_rdrF(const A &, const Fields &f, int kk) { return f.recip_drF[kk - 1]; }
+template <class A> __device__ __forceinline__ double vi_drF(const A &, const Fields &f, int kk) { return f.drF[kk - 1]; }
+template <class A> __device__ __forceinline__ double vi_h0W_own(const A &a, int i, int j, int k) { return a.h0FacW(i, j, k); }
+template <class A> __device__ __forceinline__ double vi_h0S_own(const A &a, int i, int j, int k) { return a.h0FacS(i, j, k); }
+
 // ---- MOM_VECINV's per-level intermediates as functions of an accessor A of the level's
 // 3-D fields (uVel, vVel, hFacW, hFacS, recip_hFacC at (ii, jj, k)): VIGlobal reads them
 // from HBM, VITile from the LDS-staged tile of k_mom_vi_tiled; the expression trees are
@@ -439,7 +452,7 @@ __device__ __forceinline__ double vi_vort(const A &a, const Dims &d, const P &p,
 #define VC(a, b) (V(a, b) * G2(dyC, a, b))
     const double rz = G2(recip_rAz, ii, jj);
     if (p.cubeCorners) {
-      const int face = f.tileFace[t], e = f.tileEdge[t];
+      const int face = vi_tile_face(a, f, t), e = vi_tile_edge(a, f, t);
       const bool isN = e & 1, isS = e & 2, isE = e & 4, isW = e & 8;
       if (ii == 1 && jj == 1 && isW && isS) return rz * ((VC(ii, jj) - UC(ii, jj)) + UC(ii, jj - 1));
       if (ii == sNx + 1 && jj == 1 && isE && isS) {
@@ -518,7 +531,7 @@ __device__ __forceinline__ void vecinv_tend(const A &a, const Dims &d, const P &
 #define W3(ii, jj, kk) a.wVel(ii, jj, kk)
 #define G2(x, ii, jj) a.template g2<F2_##x>(ii, jj)
 #define G3(x, ii, jj, kk) a.x(ii, jj, kk)
-  const double recip_drF = f.recip_drF[k - 1], drF = f.drF[k - 1];
+  const double recip_drF = vi_rdrF(a, f, k), drF = vi_drF(a, f, k);
   auto rhz = [&](int ii, int jj) -> double {   // r_hFacZ
     const double h = a.hfz(ii, jj);
     return h == 0.0 ? 0.0 : 1.0 / h;
@@ -544,18 +557,19 @@ __device__ __forceinline__ void vecinv_tend(const A &a, const Dims &d, const P &
     auto rvU = [&](int kk) -> double {
       if (kk <= 1 || kk > Nr) return 0.0;
       return p.vfFacMom * 1.0 * (-p.viscAr * G2(rAw, i, j) * (U3(i, j, kk) - U3(i, j, kk - 1)) * p.rkSign *
-                                 f.recip_drC[kk - 1] * G3(maskW, i, j, kk) * G3(maskW, i, j, kk - 1));
+                                 vi_rdrC(a, f, kk) * G3(maskW, i, j, kk) * G3(maskW, i, j, kk - 1));
     };
     auto rvV = [&](int kk) -> double {
       if (kk <= 1 || kk > Nr) return 0.0;
       return p.vfFacMom * 1.0 * (-p.viscAr * G2(rAs, i, j) * (V3(i, j, kk) - V3(i, j, kk - 1)) * p.rkSign *
-                                 f.recip_drC[kk - 1] * G3(maskS, i, j, kk) * G3(maskS, i, j, kk - 1));
+                                 vi_rdrC(a, f, kk) * G3(maskS, i, j, kk) * G3(maskS, i, j, kk - 1));
     };
     // skipped with implicitViscosity (mom_vecinv.F:444): k_mom_impl solves it after the k loop
     if (!p.implicitViscosity) guDiss = guDiss - rhFacW * recip_drF * G2(recip_rAw, i, j) * (rvU(k + 1) - rvU(k)) * p.rkSign;
     if (p.no_slip_sides) {
-      const double hS = G3(h0FacW, i, j, k) - a.h0fz(i, j);
-      const double hN = G3(h0FacW, i, j, k) - a.h0fz(i, j + 1);
+      const double h0W = vi_h0W_own(a, i, j, k);
+      const double hS = h0W - a.h0fz(i, j);
+      const double hN = h0W - a.h0fz(i, j + 1);
       const double u0 = U(i, j);
       guDiss = guDiss + -rhFacW * recip_drF * G2(recip_rAw, i, j) *
                             (hS * G2(dxV, i, j) * G2(recip_dyU, i, j) * (p.viscAhZ * u0 - p.viscA4Z * 0.0) +
@@ -564,7 +578,7 @@ __device__ __forceinline__ void vecinv_tend(const A &a, const Dims &d, const P &
     }
     if (p.no_slip_bottom) {
       const int kDn = (k + 1 < Nr) ? k + 1 : Nr, kLowF = k + 1;
-      const double recDrC = (k == Nr) ? recip_drF : f.recip_drC[kLowF - 1];
+      const double recDrC = (k == Nr) ? recip_drF : vi_rdrC(a, f, kLowF);
       double cD = 0.0 * 1.0;
       cD = cD + p.viscAr * recDrC * 2.0;
       cD = (k == Nr) ? cD * G3(maskW, i, j, k) : cD * G3(maskW, i, j, k) * (1.0 - G3(maskW, i, j, kDn));
@@ -572,8 +586,9 @@ __device__ __forceinline__ void vecinv_tend(const A &a, const Dims &d, const P &
     }
     if (!p.implicitViscosity) gvDiss = gvDiss - rhFacS * recip_drF * G2(recip_rAs, i, j) * (rvV(k + 1) - rvV(k)) * p.rkSign;
     if (p.no_slip_sides) {
-      const double hW = G3(h0FacS, i, j, k) - a.h0fz(i, j);
-      const double hE = G3(h0FacS, i, j, k) - a.h0fz(i + 1, j);
+      const double h0S = vi_h0S_own(a, i, j, k);
+      const double hW = h0S - a.h0fz(i, j);
+      const double hE = h0S - a.h0fz(i + 1, j);
       const double v0 = V(i, j);
       gvDiss = gvDiss + -rhFacS * recip_drF * G2(recip_rAs, i, j) *
                             (hW * G2(dyU, i, j) * G2(recip_dxV, i, j) * (p.viscAhZ * v0 - p.viscA4Z * 0.0) +
@@ -582,7 +597,7 @@ __device__ __forceinline__ void vecinv_tend(const A &a, const Dims &d, const P &
     }
     if (p.no_slip_bottom) {
       const int kDn = (k + 1 < Nr) ? k + 1 : Nr, kLowF = k + 1;
-      const double recDrC = (k == Nr) ? recip_drF : f.recip_drC[kLowF - 1];
+      const double recDrC = (k == Nr) ? recip_drF : vi_rdrC(a, f, kLowF);
       double cD = 0.0 * 1.0;
       cD = cD + p.viscAr * recDrC * 2.0;
       cD = (k == Nr) ? cD * G3(maskS, i, j, k) : cD * G3(maskS, i, j, k) * (1.0 - G3(maskS, i, j, kDn));
@@ -1856,6 +1871,10 @@ struct VIM2 {   // HR: slots of the hFacC / wVel level rings (level kk in slot k
   const double *sKE, *sVort, *sHfz, *sH0fz, *sHDiv;
   const VIMarchRegs &c;
   double uM, uP, vM, vP, hwM, hwP, hsM, hsP;
+  // filled at the level's start (vi_tile_face ... overloads below): the tile's face / edge
+  // bits, recip_drC(k), recip_drC(k+1), recip_drF(k), drF(k), the own point's h0FacW / h0FacS
+  int face = 0, edge = 0;
+  double rdrCk = 0.0, rdrCk1 = 0.0, rdrFk = 0.0, drFk = 0.0, h0W = 0.0, h0S = 0.0;
   __device__ __forceinline__ int e(int ii, int jj) const { return (jj - j0 + 1) * EW + (ii - i0 + 1); }
   __device__ __forceinline__ long g(int ii, int jj, int kk) const { return MG_I3(d, ii, jj, kk, t); }
   __device__ __forceinline__ double lvl(const double *sl, double m_, double p_, int ii, int jj, int kk) const {
@@ -1912,6 +1931,22 @@ struct VIM2 {   // HR: slots of the hFacC / wVel level rings (level kk in slot k
   __device__ __forceinline__ double KE(int ii, int jj) const { return sKE[id(ii, jj)]; }
   __device__ __forceinline__ double hDiv(int ii, int jj) const { return sHDiv[id(ii, jj)]; }
 };
+template <int BX, int BY, class P, bool OWN, int HR>
+__device__ __forceinline__ int vi_tile_face(const VIM2<BX, BY, P, OWN, HR> &a, const Fields &, int) { return a.face; }
+template <int BX, int BY, class P, bool OWN, int HR>
+__device__ __forceinline__ int vi_tile_edge(const VIM2<BX, BY, P, OWN, HR> &a, const Fields &, int) { return a.edge; }
+template <int BX, int BY, class P, bool OWN, int HR>   // (called at kk = k and k + 1 only)
+__device__ __forceinline__ double vi_rdrC(const VIM2<BX, BY, P, OWN, HR> &a, const Fields &, int kk) {
+  return kk == a.k ? a.rdrCk : a.rdrCk1;
+}
+template <int BX, int BY, class P, bool OWN, int HR>
+__device__ __forceinline__ double vi_rdrF(const VIM2<BX, BY, P, OWN, HR> &a, const Fields &, int) { return a.rdrFk; }
+template <int BX, int BY, class P, bool OWN, int HR>
+__device__ __forceinline__ double vi_drF(const VIM2<BX, BY, P, OWN, HR> &a, const Fields &, int) { return a.drFk; }
+template <int BX, int BY, class P, bool OWN, int HR>
+__device__ __forceinline__ double vi_h0W_own(const VIM2<BX, BY, P, OWN, HR> &a, int, int, int) { return a.h0W; }
+template <int BX, int BY, class P, bool OWN, int HR>
+__device__ __forceinline__ double vi_h0S_own(const VIM2<BX, BY, P, OWN, HR> &a, int, int, int) { return a.h0S; }
 
 // The k-march of k_mom_vi_march<PF, CREG> (same phases, same staging), on VIM2 / VIP<C>.
 // EARLY: the output point's own HBM reads of level k (phi_hyd at the three points of the
@@ -1983,6 +2018,7 @@ __global__ void __launch_bounds__(VT_NT, LBW) k_mom_vi_m2(Dims d, VIP<C> p, Fiel
   };
   VIMarchRegs c0;
   if constexpr (CREG) load_c(c0, q2);
+  const int tFace = P::cubeCorners ? f.tileFace[t] : 0, tEdge = P::cubeCorners ? f.tileEdge[t] : 0;
   const long t3 = (long)t * (d.n3 - d.n2);
   const unsigned lvB = (unsigned)(d.n2 * 8);
   unsigned eb[NR];
@@ -2090,6 +2126,19 @@ __global__ void __launch_bounds__(VT_NT, LBW) k_mom_vi_m2(Dims d, VIP<C> p, Fiel
                             uM, k < Nr ? oU : 0.0, vM, k < Nr ? oV : 0.0, hwM, k < Nr ? oHW : 0.0, hsM, k < Nr ? oHS : 0.0};
     VIM2<BX, BY, P, false> ai{d, p, f, k, t, i0, j0, 0, 0, sU, sV, sHW, sHS, sHC, sW, s2, sKE, sVort, sHfz, sH0fz, sHDiv, c,
                               0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
+    // the level's 1-D factors and the own point's rest-state thicknesses, fetched here with
+    // the level's other reads (vi_rdrC ... overloads)
+    a.face = ai.face = tFace;
+    a.edge = ai.edge = tEdge;
+    a.rdrCk = f.recip_drC[k - 1];
+    a.rdrCk1 = k < Nr ? f.recip_drC[k] : 0.0;
+    a.rdrFk = f.recip_drF[k - 1];
+    a.drFk = f.drF[k - 1];
+    if constexpr (P::momViscosity && P::no_slip_sides) {
+      const long q3h = q2 + (long)(k - 1) * d.n2 + t3;
+      a.h0W = AR3(h0FacW, q3h);
+      a.h0S = AR3(h0FacS, q3h);
+    }
     for (int q = tid; q < IN; q += VT_NT) {
       const int ii = i0 + q % IW, jj = j0 + q / IW;          // vort / hFacZ grid: i0..i0+BX
       const bool ok = ii <= d.sNx + d.OLx && jj <= d.sNy + d.OLy;
@@ -2105,7 +2154,7 @@ __global__ void __launch_bounds__(VT_NT, LBW) k_mom_vi_m2(Dims d, VIP<C> p, Fiel
     if (act) {
       auto q3of = [&](long qq2, int kk) { return qq2 + (long)(kk - 1) * d.n2 + t3; };
       const long q3 = q3of(q2, k);
-      const double recip_drF = f.recip_drF[k - 1];
+      const double recip_drF = a.rdrFk;
       double gU = 0.0, gV = 0.0, guDiss = 0.0, gvDiss = 0.0, dPhiHydX = 0.0, dPhiHydY = 0.0;
       {  // CALC_GRAD_PHI_HYD (calc_grad_phi_hyd.F:152-214), as k_mom_step
         constexpr bool rsc = rstar && P::select_rStar >= 2 && P::nonlinFreeSurf >= 4;

@@ -28,6 +28,8 @@ for s in "$@"; do
     libab) OUT=$O/libab CONFIGS="llc90_synthetic global_ocean.90x40x15 global_ocean.cs32x15" \
              LIBS="default flat:mitgcm_amd/_build/diag/libmitgcm_amd_flat.so" bash tools/lib_ab.sh > $O/libab.log 2>&1 ;;
     llc_par) timeout -k 10 500 $PY -x tests/test_gpu_llc.py > $O/llc_par.log 2>&1 ;;
+    vi_ab) OUT=$O/vi_ab CONFIGS="llc90_synthetic llc90_synthetic" \
+             LIBS="default base:mitgcm_amd/_build/diag/libmitgcm_amd_base.so" bash tools/lib_ab.sh > $O/vi_ab.log 2>&1 ;;
     options) timeout -k 10 600 $PY tests/test_gpu_options.py > $O/options.log 2>&1 ;;
     rest) timeout -k 10 1000 $PY tests -m gpu --ignore=tests/test_gpu_refhost.py --ignore=tests/test_gpu_parallel.py \
             --ignore=tests/test_gpu_rccl.py > $O/rest.log 2>&1 ;;
