@@ -38,8 +38,8 @@ __global__ void __launch_bounds__(256) k_dt_front(Dims d, Params p, Fields f, Tr
   lb -= nbPhi;
   if (lb < nbDel) { del2uv_body(d, p, f, lb); return; }
   lb -= nbDel;
-  if (lb < nbTr) tracer_rhs_body<GM>(d, p, f, aT, iterPtr, lb);
-  else tracer_rhs_body<GM>(d, p, f, aS, iterPtr, lb - nbTr);
+  if (lb < nbTr) tracer_rhs_body_br<GM>(d, p, f, aT, iterPtr, lb);
+  else tracer_rhs_body_br<GM>(d, p, f, aS, iterPtr, lb - nbTr);
 }
 
 // MOM_FLUXFORM U | V (k_mom_step_uv's split: even logical blocks U, odd V) | implicit solve
@@ -124,8 +124,8 @@ __global__ void __launch_bounds__(256) k_dt_l2(Dims d, Params p, Fields f, Trace
     return;
   }
   lb -= nbMom;
-  if (lb < nbTr) tracer_rhs_body<GM>(d, p, f, aT, iterPtr, lb);
-  else tracer_rhs_body<GM>(d, p, f, aS, iterPtr, lb - nbTr);
+  if (lb < nbTr) tracer_rhs_body_br<GM>(d, p, f, aT, iterPtr, lb);
+  else tracer_rhs_body_br<GM>(d, p, f, aS, iterPtr, lb - nbTr);
 }
 __global__ void __launch_bounds__(256) k_dt_l3(Dims d, Params p, Fields f, TracerArgs aT, TracerArgs aS,
                                                const int *iterPtr, int nc, int nbCd, int nbImp, const long *__restrict__ srcOf,

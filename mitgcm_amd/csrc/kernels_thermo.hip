@@ -474,11 +474,13 @@ __global__ void __launch_bounds__(256) k_advg_upd(Dims d, Fields f, TracerArgs a
   }
 }
 
-// GAD_CALC_RHS + forcing + AB2 + TIMESTEP_TRACER for one interior (i,j,k) point:
-// writes gNm1 (AB tracers) and a.scr = tracer + dTtracer*gT (the right-hand side of
-// the implicit vertical solve, or the new tracer with explicit vertical diffusion).
+// tracer_rhs_body with its operands loaded behind the reference's conditions: the form the
+// fused 2-D kernels (k_dt_front, k_dt_l2) keep. There the unconditional loads below raise
+// the fused kernel from 125 to 196 VGPRs (4 -> 2 waves per SIMD) and C2 measured 1.5 %
+// slower (0.2901 against 0.2852 ms/step); capping the kernel at 128 spills
+// (profiles/r05/gm_loads/). Same arithmetic, bit-identical results.
 template <bool GM>
-__device__ __forceinline__ void tracer_rhs_body(const Dims &d, const Params &p, const Fields &f, const TracerArgs &a,
+__device__ __forceinline__ void tracer_rhs_body_br(const Dims &d, const Params &p, const Fields &f, const TracerArgs &a,
                                                 const int *iterPtr, int lb) {
   MG_PLANE_LB(1, d.sNx, 1, d.sNy, z, lb)
   const int t = d.t0 + z / d.Nr, k = z % d.Nr + 1;
@@ -596,6 +598,193 @@ __device__ __forceinline__ void tracer_rhs_body(const Dims &d, const Params &p, 
                         G3(maskS, i, j, kk - 1) * G2(recip_dyC, i, j) * (T3(i, j, kk - 1) - T3(i, j - 1, kk - 1))));
       const double maskUp = G3(maskC, i, j, kk - 1) * G3(maskC, i, j, kk);
       dfr = dfr - rA * maskInC * (G3(Kwx, i, j, kk) * dTdx + G3(Kwy, i, j, kk) * dTdy) * maskUp;
+    }
+    return fv + dfr;
+  };
+  const long q3 = MG_I3(d, i, j, k, t);
+  const double Tk = T[q3];
+  const double uT0 = uFld(i, j) * (G2(dyG, i, j) * drF * G3(hFacW, i, j, k));
+  const double uT1 = uFld(i + 1, j) * (G2(dyG, i + 1, j) * drF * G3(hFacW, i + 1, j, k));
+  const double vT0 = vFld(i, j) * (G2(dxG, i, j) * drF * G3(hFacS, i, j, k));
+  const double vT1 = vFld(i, j + 1) * (G2(dxG, i, j + 1) * drF * G3(hFacS, i, j + 1, k));
+  const double rTrans = rtrans(k), rTransKp = rtrans(k + 1);
+  const double fVerUp = fvert(k, rTrans), fVerDn = fvert(k + 1, rTransKp);
+  const double fZi = fzon(i), fZe = fzon(i + 1);
+  const double fMi = fmer(j), fMn = fmer(j + 1);
+  const double g0 = a.multiDim ? f.gAdv[q3] : 0.0;
+  double gT = g0 - f.recip_hFacC[q3] * f.recip_drF[k - 1] * recip_rA *
+                       ((fZe - fZi) * maskInC + (fMn - fMi) * maskInC + (fVerDn - fVerUp) * p.rkSign -
+                        Tk * ((uT1 - uT0) * advFac + (vT1 - vT0) * advFac + (rTransKp - rTrans) * rAdvFac) * maskInC);
+  double gtForc = 0.0;
+  if (a.forcing && a.sfc && k == 1) gtForc = gtForc + a.sfc[q] * f.recip_drF[0] * f.recip_hFacC[q3];
+  if (!p.tracForcingOutAB) gT = gT + gtForc;   // inside (0) / after (1) AB2: temp_integrate.F:373-410
+  if (a.useAB) {   // ADAMS_BASHFORTH2(k)
+    const double ab = abFac * (gT - a.gNm1[q3]);
+    double gN = gT;
+    gT = gT + ab;
+    // FREESURF_RESCALE_G of gT and gtNm1 under r* (temp_integrate.F:412-446)
+    if (p.nonlinFreeSurf > 0 && p.select_rStar > 0) gN = gN / f.rStarExpC[q];
+    a.gNm1[q3] = gN;
+  }
+  if (p.tracForcingOutAB) gT = gT + gtForc;
+  if (p.nonlinFreeSurf > 0 && p.select_rStar > 0) gT = gT / f.rStarExpC[q];
+  // TIMESTEP_TRACER
+  const double v = Tk + p.deltaTtracer * gT;
+  if (p.implicitDiffusion) a.scr[q3] = v;
+  else a.trNext[q3] = v;   // CYCLE_TRACER directly
+#undef T3
+#undef G2
+#undef G3
+}
+
+// GAD_CALC_RHS + forcing + AB2 + TIMESTEP_TRACER for one interior (i,j,k) point:
+// writes gNm1 (AB tracers) and a.scr = tracer + dTtracer*gT (the right-hand side of
+// the implicit vertical solve, or the new tracer with explicit vertical diffusion).
+template <bool GM>
+__device__ __forceinline__ void tracer_rhs_body(const Dims &d, const Params &p, const Fields &f, const TracerArgs &a,
+                                                const int *iterPtr, int lb) {
+  MG_PLANE_LB(1, d.sNx, 1, d.sNy, z, lb)
+  const int t = d.t0 + z / d.Nr, k = z % d.Nr + 1;
+  if (i > d.sNx || j > d.sNy) return;
+  const int Nr = d.Nr;
+  const int myIter = *iterPtr;
+  const double abFac = (myIter == p.nIter0 && p.nIter0 == 0) ? 0.0 : 0.5 + p.abEps;
+  const bool calcAdv = a.advection && !a.multiDim;
+  const double advFac = calcAdv ? 1.0 : 0.0, rAdvFac = p.rkSign * advFac;
+  const double *__restrict__ T = a.tr;
+  const long q = MG_I2(d, i, j, t);
+  const double maskInC = f.maskInC[q], recip_rA = f.recip_rA[q], rA = f.rA[q];
+#define T3(ii, jj, kk) T[MG_I3(d, ii, jj, kk, t)]
+#define G2(a_, ii, jj) f.a_[MG_I2(d, ii, jj, t)]
+#define G3(a_, ii, jj, kk) f.a_[MG_I3(d, ii, jj, kk, t)]
+  const double drF = f.drF[k - 1];
+  // uFld, vFld, wFld of thermodynamics.F:252-268: the Eulerian velocity plus, with
+  // GM_AdvForm, GMREDI_RESIDUAL_FLOW's bolus velocity (gmredi_residual_flow.F:58-97)
+  const bool bolus = GM && p.GM_AdvForm;
+  const double flip = -p.gravitySign;
+  const int kp1b = k + 1 < Nr ? k + 1 : Nr;
+  const double maskp1b = k >= Nr ? 0.0 : 1.0;
+  // (every operand below is loaded unconditionally, at clamped levels where the reference's
+  // condition would not reach it, and the conditions then select among the values: the same
+  // arithmetic, but no load waits behind a branch -- vmcnt counts stores too)
+  auto uFld = [&](int ii, int jj) {
+    double u = G3(uVel, ii, jj, k);
+    const double ps1 = G3(GM_PsiX, ii, jj, kp1b), ps0 = G3(GM_PsiX, ii, jj, k), rdr = f.recip_drF[k - 1];
+    const double rh = G3(recip_hFacW, ii, jj, k);
+    if (bolus) {
+      const double delPsi = ps1 * 1.0 * maskp1b - ps0 * 1.0;
+      u = u + delPsi * rdr * rh * 1.0 * flip;
+    }
+    return u;
+  };
+  auto vFld = [&](int ii, int jj) {
+    double v = G3(vVel, ii, jj, k);
+    const double ps1 = G3(GM_PsiY, ii, jj, kp1b), ps0 = G3(GM_PsiY, ii, jj, k), rdr = f.recip_drF[k - 1];
+    const double rh = G3(recip_hFacS, ii, jj, k);
+    if (bolus) {
+      const double delPsi = ps1 * 1.0 * maskp1b - ps0 * 1.0;
+      v = v + delPsi * rdr * rh * 1.0 * flip;
+    }
+    return v;
+  };
+  auto wFld = [&](int kk) {   // (kk in 1..Nr)
+    double w = G3(wVel, i, j, kk);
+    const double dyE = G2(dyG, i + 1, j), pxE = G3(GM_PsiX, i + 1, j, kk), dyW = G2(dyG, i, j), pxW = G3(GM_PsiX, i, j, kk);
+    const double dxN = G2(dxG, i, j + 1), pyN = G3(GM_PsiY, i, j + 1, kk), dxS = G2(dxG, i, j), pyS = G3(GM_PsiY, i, j, kk);
+    if (bolus) {
+      const double delPsi = (dyE * pxE - dyW * pxW + dxN * pyN - dxS * pyS);
+      w = w + delPsi * recip_rA * 1.0 * flip;
+    }
+    return w;
+  };
+  // GM_EXTRA_DIAGONAL vertical gradient at the west (dir 0) / south (dir 1) face of (ii, jj)
+  // (gmredi_xtransport.F:117-146, gmredi_ytransport.F; maskFk = CALC_ADV_FLOW's maskUp)
+  auto gm_dTdz = [&](int ii, int jj, int dir) {
+    const int km1 = k > 1 ? k - 1 : 1, kp1 = k + 1 < Nr ? k + 1 : Nr;
+    const double maskp1 = k >= Nr ? 0.0 : 1.0;
+    const int i0 = dir == 0 ? ii - 1 : ii, j0 = dir == 0 ? jj : jj - 1;
+    auto mUp = [&](int a_, int b_) {
+      const double mm = G3(maskC, a_, b_, km1), m0 = G3(maskC, a_, b_, k);
+      return k == 1 ? 0.0 : mm * m0;
+    };
+    const double rdc0 = f.recip_drC[k - 1], rdc1 = f.recip_drC[kp1 - 1];
+    return 0.5 * (+0.5 * rdc0 *
+                      (mUp(i0, j0) * (T3(i0, j0, km1) - T3(i0, j0, k)) + mUp(ii, jj) * (T3(ii, jj, km1) - T3(ii, jj, k))) +
+                  0.5 * rdc1 *
+                      (G3(maskC, i0, j0, k) * G3(maskC, i0, j0, kp1) * maskp1 * (T3(i0, j0, k) - T3(i0, j0, kp1)) +
+                       G3(maskC, ii, jj, k) * G3(maskC, ii, jj, kp1) * maskp1 * (T3(ii, jj, k) - T3(ii, jj, kp1))));
+  };
+  // west / south face fluxes of the column (fZon, fMer): GAD_C2_ADV_X/Y + GAD_DIFF_X/Y
+  auto fzon = [&](int ii) {
+    const double xA = G2(dyG, ii, j) * drF * G3(hFacW, ii, j, k);
+    const double uf = uFld(ii, j), t0 = T3(ii, j, k), tw = T3(ii - 1, j, k), rdx = G2(recip_dxC, ii, j);
+    const double ku = G3(Kux, ii, j, k), kz = G3(Kuz, ii, j, k);
+    const double dz = GM ? gm_dTdz(ii, j, 0) : 0.0;
+    double fz = 0.0;
+    if (calcAdv) fz = fz + (uf * xA) * (t0 + tw) * 0.5;
+    double df = 0.0;
+    if (a.diffKh != 0.0) df = -a.diffKh * xA * rdx * (t0 - tw);
+    if (GM)   // GMREDI_XTRANSPORT (gmredi_xtransport.F:94-101)
+      df = df - xA * ku * rdx * (t0 - tw);
+    if (GM && p.GM_ExtraDiag) df = df - xA * kz * dz;
+    return fz + df;
+  };
+  auto fmer = [&](int jj) {
+    const double yA = G2(dxG, i, jj) * drF * G3(hFacS, i, jj, k);
+    const double vf = vFld(i, jj), t0 = T3(i, jj, k), ts = T3(i, jj - 1, k), rdy = G2(recip_dyC, i, jj);
+    const double kv = G3(Kvy, i, jj, k), kz = G3(Kvz, i, jj, k);
+    const double dz = GM ? gm_dTdz(i, jj, 1) : 0.0;
+    double fm = 0.0;
+    if (calcAdv) fm = fm + (vf * yA) * (t0 + ts) * 0.5;
+    double df = 0.0;
+    if (a.diffKh != 0.0) df = -a.diffKh * yA * rdy * (t0 - ts);
+    if (GM)   // GMREDI_YTRANSPORT
+      df = df - yA * kv * rdy * (t0 - ts);
+    if (GM && p.GM_ExtraDiag) df = df - yA * kz * dz;
+    return fm + df;
+  };
+  // CALC_ADV_FLOW rTrans of level kk (0 at the surface and below the bottom level)
+  auto rtrans = [&](int kk) {
+    const int kc = kk < 2 ? 2 : (kk > Nr ? Nr : kk), kcm = kc > 1 ? kc - 1 : 1;   // (clamped; Nr = 1: 1, 1)
+    const double mm = G3(maskC, i, j, kcm), m0 = G3(maskC, i, j, kc);
+    const double w = wFld(kc);
+    if (kk <= 1 || kk > Nr) return 0.0;
+    const double maskUp = mm * m0;
+    return w * rA * maskUp;
+  };
+  // fVerT through the top face of level kk: GAD_C2_ADV_R + vertical diffusive flux
+  // (GAD_DIFF_R when diffusion is explicit, 0 with implicitDiffusion)
+  auto fvert = [&](int kk, double rTr) {
+    const int kc = kk < 2 ? 2 : (kk > Nr ? Nr : kk), kcm = kc > 1 ? kc - 1 : 1;
+    const bool in = kk >= 2 && kk <= Nr;
+    const double mm = G3(maskC, i, j, kcm), m0 = G3(maskC, i, j, kc);
+    const double tk = T3(i, j, kc), tm = T3(i, j, kcm);
+    const double ivd = G3(IVDConvCount, i, j, kc), kwz = G3(Kwz, i, j, kc), rdc = f.recip_drC[kcm];
+    double fv = 0.0;
+    if (in && calcAdv) {
+      const double wT = mm * rTr * (tk + tm) * 0.5;
+      fv = fv + wT * maskInC;
+    }
+    double dfr = 0.0;
+    if (!p.implicitDiffusion && in) {
+      double kap = (ivd * p.ivdc_kappa + 0.0) + a.diffKr;
+      if (GM) kap = kap + kwz * maskInC;
+      const double maskUp = mm * m0;
+      dfr = -kap * maskUp * rA * rdc * (tk - tm) * p.rkSign;
+    }
+    if (GM && in) {   // GMREDI_RTRANSPORT (gmredi_rtransport.F:75-130)
+      const double dTdx =
+          0.5 * (0.5 * (G3(maskW, i + 1, j, kc) * G2(recip_dxC, i + 1, j) * (T3(i + 1, j, kc) - T3(i, j, kc)) +
+                        G3(maskW, i, j, kc) * G2(recip_dxC, i, j) * (T3(i, j, kc) - T3(i - 1, j, kc))) +
+                 0.5 * (G3(maskW, i + 1, j, kcm) * G2(recip_dxC, i + 1, j) * (T3(i + 1, j, kcm) - T3(i, j, kcm)) +
+                        G3(maskW, i, j, kcm) * G2(recip_dxC, i, j) * (T3(i, j, kcm) - T3(i - 1, j, kcm))));
+      const double dTdy =
+          0.5 * (0.5 * (G3(maskS, i, j + 1, kc) * G2(recip_dyC, i, j + 1) * (T3(i, j + 1, kc) - T3(i, j, kc)) +
+                        G3(maskS, i, j, kc) * G2(recip_dyC, i, j) * (T3(i, j, kc) - T3(i, j - 1, kc))) +
+                 0.5 * (G3(maskS, i, j + 1, kcm) * G2(recip_dyC, i, j + 1) * (T3(i, j + 1, kcm) - T3(i, j, kcm)) +
+                        G3(maskS, i, j, kcm) * G2(recip_dyC, i, j) * (T3(i, j, kcm) - T3(i, j - 1, kcm))));
+      const double maskUp = mm * m0;
+      dfr = dfr - rA * maskInC * (G3(Kwx, i, j, kc) * dTdx + G3(Kwy, i, j, kc) * dTdy) * maskUp;
     }
     return fv + dfr;
   };

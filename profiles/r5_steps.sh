@@ -28,6 +28,15 @@ for s in "$@"; do
     libab) OUT=$O/libab CONFIGS="llc90_synthetic global_ocean.90x40x15 global_ocean.cs32x15" \
              LIBS="default flat:mitgcm_amd/_build/diag/libmitgcm_amd_flat.so" bash tools/lib_ab.sh > $O/libab.log 2>&1 ;;
     llc_par) timeout -k 10 500 $PY -x tests/test_gpu_llc.py > $O/llc_par.log 2>&1 ;;
+    gm_ab) OUT=$O/gm_ab CONFIGS="global_ocean.90x40x15 global_ocean.cs32x15" \
+             LIBS="default base:mitgcm_amd/_build/diag/libmitgcm_amd_base.so" bash tools/lib_ab.sh > $O/gm_ab.log 2>&1 ;;
+    c23_par) timeout -k 10 800 $PY -x tests/test_gpu_ocean90.py tests/test_gpu_cs32x15.py tests/test_gpu_options.py \
+               tests/test_gpu_3d.py tests/test_gpu_refpin.py > $O/c23_par.log 2>&1 ;;
+    fver_ab) OUT=$O/fver_ab CONFIGS="global_ocean.90x40x15 global_ocean.cs32x15" \
+             LIBS="default fver:mitgcm_amd/_build/diag/libmitgcm_amd_fver.so base:mitgcm_amd/_build/diag/libmitgcm_amd_base.so" \
+             bash tools/lib_ab.sh > $O/fver_ab.log 2>&1 ;;
+    fver_par) MGCM_LIB=mitgcm_amd/_build/diag/libmitgcm_amd_fver.so timeout -k 10 800 $PY -x tests/test_gpu_ocean90.py \
+               tests/test_gpu_cs32x15.py tests/test_gpu_options.py tests/test_gpu_3d.py > $O/fver_par.log 2>&1 ;;
     vi_ab) OUT=$O/vi_ab CONFIGS="llc90_synthetic llc90_synthetic" \
              LIBS="default base:mitgcm_amd/_build/diag/libmitgcm_amd_base.so" bash tools/lib_ab.sh > $O/vi_ab.log 2>&1 ;;
     options) timeout -k 10 600 $PY tests/test_gpu_options.py > $O/options.log 2>&1 ;;
