@@ -1995,16 +1995,16 @@ __global__ void __launch_bounds__(VT_NT, LBW) k_mom_vi_m2(Dims d, VIP<C> p, Fiel
     ein[r] = ee < EN && ii <= d.sNx + d.OLx && jj <= d.sNy + d.OLy;
     eq[r] = MG_I2(d, ein[r] ? ii : 1, ein[r] ? jj : 1, t);
   }
+  // the prologue's HBM reads are all issued before any of its LDS stores: a store behind the
+  // `ee < EN` branch ends the basic block, and a load placed after it waited for every earlier
+  // one (vmcnt(0)) -- about fifteen serial memory round trips per workgroup before the march
+  double v2[VM_S2][NR];
   {
     const int ids[VM_S2] = {F2_dxC, F2_dyC, F2_recip_rAz, F2_dxG, F2_dyG, F2_recip_rA};
 #pragma unroll
     for (int n = 0; n < VM_S2; n++)
 #pragma unroll
-      for (int r = 0; r < NR; r++) {
-        const int ee = tid + r * VT_NT;
-        const double v = f.a2[(long)ids[n] * d.N2all + eq[r]];
-        if (ee < EN) s2[n * EN + ee] = ein[r] ? v : 0.0;
-      }
+      for (int r = 0; r < NR; r++) v2[n][r] = f.a2[(long)ids[n] * d.N2all + eq[r]];
   }
   auto load_c = [&](VIMarchRegs &c, const long q2) {
     const long qn = q2 + d.nx, qe = q2 + 1, qw = q2 - 1, qs = q2 - d.nx;
@@ -2063,21 +2063,39 @@ __global__ void __launch_bounds__(VT_NT, LBW) k_mom_vi_m2(Dims d, VIP<C> p, Fiel
       if (ee < EN) sW[(kk & 1) * EN + ee] = (ein[r] && kk <= Nr) ? nW[r] : 0.0;
     }
   };
-  double uM = 0.0, vM = 0.0, hwM = 0.0, hsM = 0.0;
+  double uM = 0.0, vM = 0.0, hwM = 0.0, hsM = 0.0, hcM[NR];
   if (kb > 1) {
     fetch(kb - 1);
     uM = oU; vM = oV; hwM = oHW; hsM = oHS;
 #pragma unroll
-    for (int r = 0; r < NR; r++) {
-      const int ee = tid + r * VT_NT;
-      if (ee < EN) sHC[((kb - 1) & 1) * EN + ee] = ein[r] ? nHC[r] : 0.0;
-    }
+    for (int r = 0; r < NR; r++) hcM[r] = nHC[r];
   }
   fetchW(kb);
-  stashW(kb);
+  double w0[NR];
+#pragma unroll
+  for (int r = 0; r < NR; r++) w0[r] = nW[r];
   fetchW(kb + 1 <= Nr ? kb + 1 : Nr);
-  stashW(kb + 1);
   fetch(kb);
+#pragma unroll
+  for (int n = 0; n < VM_S2; n++)
+#pragma unroll
+    for (int r = 0; r < NR; r++) {
+      const int ee = tid + r * VT_NT;
+      if (ee < EN) s2[n * EN + ee] = ein[r] ? v2[n][r] : 0.0;
+    }
+#pragma unroll
+  for (int r = 0; r < NR; r++) {
+    const int ee = tid + r * VT_NT;
+    if (ee < EN) sW[(kb & 1) * EN + ee] = (ein[r] && kb <= Nr) ? w0[r] : 0.0;
+  }
+  if (kb > 1) {
+#pragma unroll
+    for (int r = 0; r < NR; r++) {
+      const int ee = tid + r * VT_NT;
+      if (ee < EN) sHC[((kb - 1) & 1) * EN + ee] = ein[r] ? hcM[r] : 0.0;
+    }
+  }
+  stashW(kb + 1);
   stash(kb);
   const int myIter = *iterPtr;
   const double abFac = (myIter == p.nIter0 && p.nIter0 == 0) ? 0.0 : 0.5 + p.abEps;   // adams_bashforth2.F:61-65
