@@ -206,17 +206,21 @@ __global__ void __launch_bounds__(256) k_sfp_rhs_march(Dims d, Params p, Fields 
   const long r = g % d.n2, nx = d.nx, n2 = d.n2;
   const int i = (int)(r % nx) + 1 - d.OLx, j = (int)(r / nx) + 1 - d.OLy;
   const long q = (long)t * n2 + r;
+  // the point's own 2-D operands read up front (every 2-D field spans the whole slab), so none
+  // waits behind the column sum's batches
+  const double rAq = f.rA[q], emp = f.EmPmR[q], mIn = f.maskInC[q], etaNq = f.etaN[q], Bo = f.Bo_surf[q];
+  const double etaB = (p.exactConserv ? f.etaH : f.etaN)[q];
   double b = 0.0;
   if (i >= 1 && i <= d.sNx && j >= 1 && j <= d.sNy) {
     if (p.useRealFreshWaterFlux) {
       const double tmpFac = p.freeSurfFac * (1.0 / p.rhoConst) * p.implicDiv2DFlow;
-      b = tmpFac * f.rA[q] * f.EmPmR[q] / p.deltaTMom * f.maskInC[q];
+      b = tmpFac * rAq * emp / p.deltaTMom * mIn;
     }
     b = sfp_column_sum<NR>(b, (long)t * d.n3 + r, nx, n2, f.dyG[q], f.dyG[q + 1], f.dxG[q], f.dxG[q + nx], p.deltaTMom,
                            f.drF, f.hFacW, f.hFacS, f.gU, f.gV);
-    b = b - p.freeSurfFac * f.rA[q] / p.deltaTMom / p.deltaTFreeSurf * (p.exactConserv ? f.etaH[q] : f.etaN[q]);
+    b = b - p.freeSurfFac * rAq / p.deltaTMom / p.deltaTFreeSurf * etaB;
   }
-  f.cg2d_x[q] = f.Bo_surf[q] * f.etaN[q];
+  f.cg2d_x[q] = Bo * etaNq;
   f.cg2d_b[q] = b;
 }
 
@@ -1570,20 +1574,23 @@ __global__ void __launch_bounds__(256) k_corr_cont_march(Dims d, Params p, Field
   const int t = d.t0 + (int)(g / nI), l = (int)(g % nI);
   const int i = 1 + l % d.sNx, j = 1 + l / d.sNx;
   const long q = MG_I2(d, i, j, t), nx = d.nx;
-  auto eta = [&](long qq) {
-    if (!etaSrc) return f.etaN[qq];
-    const long sq = etaSrc[qq];
-    return f.recip_Bo[qq] * f.cg2d_x[sq >= 0 ? sq : qq];
-  };
-  auto phiX = [&](int ii, int jj) {
-    const long qq = MG_I2(d, ii, jj, t);
-    return f.recip_dxC[qq] * (f.Bo_surf[qq] * eta(qq) - f.Bo_surf[MG_I2(d, ii - 1, jj, t)] * eta(MG_I2(d, ii - 1, jj, t)));
-  };
-  auto phiY = [&](int ii, int jj) {
-    const long qq = MG_I2(d, ii, jj, t);
-    return f.recip_dyC[qq] * (f.Bo_surf[qq] * eta(qq) - f.Bo_surf[MG_I2(d, ii, jj - 1, t)] * eta(MG_I2(d, ii, jj - 1, t)));
-  };
-  const double pX0 = phiX(i, j), pX1 = phiX(i + 1, j), pY0 = phiY(i, j), pY1 = phiY(i, j + 1);
+  // eta at the point and its four neighbours: the five source indices loaded together, then
+  // the five values (one dependent round trip, not one per eta() evaluation)
+  const long qs[5] = {q, q - 1, q + 1, q - nx, q + nx};
+  double e[5];
+  if (!etaSrc) {
+#pragma unroll
+    for (int n = 0; n < 5; n++) e[n] = f.etaN[qs[n]];
+  } else {
+    long sq[5];
+#pragma unroll
+    for (int n = 0; n < 5; n++) sq[n] = etaSrc[qs[n]];
+#pragma unroll
+    for (int n = 0; n < 5; n++) e[n] = f.recip_Bo[qs[n]] * f.cg2d_x[sq[n] >= 0 ? sq[n] : qs[n]];
+  }
+  auto phi = [&](const double *rdc, int a, int b) { return rdc[qs[a]] * (f.Bo_surf[qs[a]] * e[a] - f.Bo_surf[qs[b]] * e[b]); };
+  const double pX0 = phi(f.recip_dxC, 0, 1), pX1 = phi(f.recip_dxC, 2, 0), pY0 = phi(f.recip_dyC, 0, 3),
+               pY1 = phi(f.recip_dyC, 4, 0);
   const double rA1 = f.recip_rA[q];
   double hDiv;
   corr_cont_column<NR>(d, p, q, MG_I3(d, i, j, 1, t), nx, d.n2, pX0, pX1, pY0, pY1, f.dyG[q], f.dyG[q + 1], f.dxG[q],
