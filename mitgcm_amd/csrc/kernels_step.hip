@@ -53,8 +53,8 @@ __global__ void __launch_bounds__(256) k_dt_back(Dims d, Params p, Fields f, Tra
     return;
   }
   lb -= nbMom;
-  if (lb < nbImp) tracer_impl_body(d, p, f, aT, nc, lb);
-  else tracer_impl_body(d, p, f, aS, nc, lb - nbImp);
+  if (lb < nbImp) tracer_impl_body<false>(d, p, f, aT, nc, lb);
+  else tracer_impl_body<false>(d, p, f, aS, nc, lb - nbImp);
 }
 
 // The default layout (MGCM_DT_LAYOUT=3; 2 = front/back above): GMREDI_CALC_TENSOR leaves
@@ -135,8 +135,8 @@ __global__ void __launch_bounds__(256) k_dt_l3(Dims d, Params p, Fields f, Trace
   lb -= nbPc;
   if (lb < nbCd) { cd_scheme_body(d, p, f, iterPtr, lb); return; }
   lb -= nbCd;
-  if (lb < nbImp) tracer_impl_body(d, p, f, aT, nc, lb);
-  else tracer_impl_body(d, p, f, aS, nc, lb - nbImp);
+  if (lb < nbImp) tracer_impl_body<false>(d, p, f, aT, nc, lb);
+  else tracer_impl_body<false>(d, p, f, aS, nc, lb - nbImp);
 }
 // whether launch_dyn_thermo runs GMREDI_CALC_TENSOR itself (one_step then launches
 // DO_OCEANIC_PHYS without it)
@@ -189,8 +189,8 @@ __global__ void __launch_bounds__(256) k_tr_rhs_pair(Dims d, Params p, Fields f,
 __global__ void __launch_bounds__(256) k_tr_impl_pair(Dims d, Params p, Fields f, TracerArgs aT, TracerArgs aS, int nc,
                                                       int nbImp) {
   const int lb = mg_xcd_block();
-  if (lb < nbImp) tracer_impl_body(d, p, f, aT, nc, lb);
-  else tracer_impl_body(d, p, f, aS, nc, lb - nbImp);
+  if (lb < nbImp) tracer_impl_body<false>(d, p, f, aT, nc, lb);
+  else tracer_impl_body<false>(d, p, f, aS, nc, lb - nbImp);
 }
 bool tracer_hpair_ok(const Dims &d, const Params &p, const TracerArgs &aT, const TracerArgs &aS) {
   return mg_hfuse(MG_FUSE_DT, d.nx, d.ny, d.nT, d.Nr) && p.tempStepping && p.saltStepping && p.implicitDiffusion &&

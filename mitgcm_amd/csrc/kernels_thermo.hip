@@ -866,7 +866,10 @@ __device__ __forceinline__ double tracer_flat_arith(const Params &p, const Field
   };
   const double rTrans = k <= 1 ? 0.0 : o.w0 * c.rA * (o.mCu * o.mC0);
   const double rTransKp = k + 1 > Nr ? 0.0 : o.w1 * c.rA * (o.mC0 * o.mCd);
-  auto fvert = [&](int kk, double rTr, double mUpper, double mLower, double tLower, double tUpper, double ivd) {
+  // the level's 1-D factors read at its start (behind the branches each load waited alone)
+  const double rdcUp = f.recip_drC[k - 1], rdcDn = f.recip_drC[k < Nr ? k : Nr - 1];
+  const double rdrFk = f.recip_drF[k - 1], rdrF0 = f.recip_drF[0];
+  auto fvert = [&](int kk, double rTr, double mUpper, double mLower, double tLower, double tUpper, double ivd, double rdc) {
     double fv = 0.0;
     if (kk >= 2 && kk <= Nr && calcAdv) {
       const double wT = mUpper * rTr * (tLower + tUpper) * 0.5;
@@ -876,22 +879,22 @@ __device__ __forceinline__ double tracer_flat_arith(const Params &p, const Field
     if (!p.implicitDiffusion && kk >= 2 && kk <= Nr) {
       const double kap = (ivd * p.ivdc_kappa + 0.0) + a.diffKr;
       const double maskUp = mUpper * mLower;
-      dfr = -kap * maskUp * c.rA * f.recip_drC[kk - 1] * (tLower - tUpper) * p.rkSign;
+      dfr = -kap * maskUp * c.rA * rdc * (tLower - tUpper) * p.rkSign;
     }
     return fv + dfr;
   };
   const double uT0 = o.u0 * (c.dyG0 * drF * o.hW0), uT1 = o.u1 * (c.dyG1 * drF * o.hW1);
   const double vT0 = o.v0 * (c.dxG0 * drF * o.hS0), vT1 = o.v1 * (c.dxG1 * drF * o.hS1);
-  const double fVerUp = fvert(k, rTrans, o.mCu, o.mC0, o.T0, o.Tu, o.ivd0);
-  const double fVerDn = fvert(k + 1, rTransKp, o.mC0, o.mCd, o.Td, o.T0, o.ivd1);
+  const double fVerUp = fvert(k, rTrans, o.mCu, o.mC0, o.T0, o.Tu, o.ivd0, rdcUp);
+  const double fVerDn = fvert(k + 1, rTransKp, o.mC0, o.mCd, o.Td, o.T0, o.ivd1, rdcDn);
   const double fZi = face(o.u0, c.dyG0, o.hW0, c.rdxC0, o.T0, o.Tw), fZe = face(o.u1, c.dyG1, o.hW1, c.rdxC1, o.Te, o.T0);
   const double fMi = face(o.v0, c.dxG0, o.hS0, c.rdyC0, o.T0, o.Ts), fMn = face(o.v1, c.dxG1, o.hS1, c.rdyC1, o.Tn, o.T0);
   const double g0 = a.multiDim ? o.gAdv : 0.0;
-  double gT = g0 - o.rhC * f.recip_drF[k - 1] * c.recip_rA *
+  double gT = g0 - o.rhC * rdrFk * c.recip_rA *
                        ((fZe - fZi) * c.maskInC + (fMn - fMi) * c.maskInC + (fVerDn - fVerUp) * p.rkSign -
                         o.T0 * ((uT1 - uT0) * advFac + (vT1 - vT0) * advFac + (rTransKp - rTrans) * rAdvFac) * c.maskInC);
   double gtForc = 0.0;
-  if (a.forcing && a.sfc && k == 1) gtForc = gtForc + c.sfc * f.recip_drF[0] * o.rhC;
+  if (a.forcing && a.sfc && k == 1) gtForc = gtForc + c.sfc * rdrF0 * o.rhC;
   if (!p.tracForcingOutAB) gT = gT + gtForc;
   const bool rs = p.nonlinFreeSurf > 0 && p.select_rStar > 0;
   if (a.useAB) {
@@ -1064,6 +1067,11 @@ __global__ void __launch_bounds__(256) k_tracer_rhs_flat(Dims d, Params p, Field
 // every level are formed k-parallel into LDS, one thread per column then sweeps
 // down and up in LDS with the reference's operations, and the levels are
 // written back k-parallel.
+// UL: every coefficient operand loaded unconditionally at clamped levels (the standalone
+// kernel on deep columns: LLC-90 1.226-1.241 against 1.265-1.267 ms/step with the tracer
+// march's hoisted factors, profiles/r05/tracer_loads/); the fused C2 / C3 kernels keep the
+// branch form (0.3-0.9 % slower there with UL, more VGPRs for the few levels each thread forms)
+template <bool UL>
 __device__ __forceinline__ void tracer_impl_body(const Dims &d, const Params &p, const Fields &f, const TracerArgs &a, int nc,
                                                  int lb) {
   extern __shared__ __attribute__((aligned(16))) double lds[];
@@ -1078,24 +1086,45 @@ __device__ __forceinline__ void tracer_impl_body(const Dims &d, const Params &p,
     const double rsx = rs ? f.rStarExpC[q2] : 1.0;
     const double mIn = f.maskInC[q2];
     // KappaRT = (IVDConvCount*ivdc_kappa + BL79(=0)) + diffKrNr [+ Kwz*maskInC] (calc_3d_diffusivity.F)
-    auto kappa = [&](int k_) {
-      double kap = (G3(IVDConvCount, i, j, k_) * p.ivdc_kappa + 0.0) + a.diffKr;
-      if (p.useGMRedi) kap = kap + G3(Kwz, i, j, k_) * mIn;
+    auto kappa = [&](double ivd, double kwz) {
+      double kap = (ivd * p.ivdc_kappa + 0.0) + a.diffKr;
+      if (p.useGMRedi) kap = kap + kwz * mIn;
       return kap;
     };
-    MG_COLF_K(k) {
+    if constexpr (!UL) MG_COLF_K(k) {
       const int me = (k - 1) * NC_ + cc;
       const long q3 = MG_I3(d, i, j, k, t);
       const double rh = rs ? f.recip_hFacC[q3] / rsx : f.recip_hFacC[q3];
       const double rdrF = f.recip_drF[k - 1];
       double sub = 0.0, sup = 0.0;
       if (k >= 2)
-        sub = -(p.deltaTtracer * G3(maskC, i, j, k - 1) * rh * rdrF * kappa(k) * f.recip_drC[k - 1]);
+        sub = -(p.deltaTtracer * G3(maskC, i, j, k - 1) * rh * rdrF *
+                kappa(G3(IVDConvCount, i, j, k), p.useGMRedi ? G3(Kwz, i, j, k) : 0.0) * f.recip_drC[k - 1]);
       if (k <= Nr - 1)
-        sup = -(p.deltaTtracer * G3(maskC, i, j, k + 1) * rh * rdrF * kappa(k + 1) * f.recip_drC[k]);
+        sup = -(p.deltaTtracer * G3(maskC, i, j, k + 1) * rh * rdrF *
+                kappa(G3(IVDConvCount, i, j, k + 1), p.useGMRedi ? G3(Kwz, i, j, k + 1) : 0.0) * f.recip_drC[k]);
       sSub[me] = sub;
       sSup[me] = sup;
       sY[me] = a.scr[q3];
+    }
+    else MG_COLF_K(k) {
+      // every operand loaded unconditionally (the levels above / below clamped into the
+      // column), then the reference's conditions select: no load waits behind a branch
+      const int me = (k - 1) * NC_ + cc;
+      const int km = k >= 2 ? k - 1 : 1, kp = k <= Nr - 1 ? k + 1 : Nr;
+      const long q3 = MG_I3(d, i, j, k, t);
+      const double rhc = f.recip_hFacC[q3], y = a.scr[q3];
+      const double mM = G3(maskC, i, j, km), mP = G3(maskC, i, j, kp);
+      const double ivK = G3(IVDConvCount, i, j, k), ivP = G3(IVDConvCount, i, j, kp);
+      const double kwK = p.useGMRedi ? G3(Kwz, i, j, k) : 0.0, kwP = p.useGMRedi ? G3(Kwz, i, j, kp) : 0.0;
+      const double rdrF = f.recip_drF[k - 1], rdcK = f.recip_drC[k - 1], rdcP = f.recip_drC[kp - 1];
+      const double rh = rs ? rhc / rsx : rhc;
+      double sub = 0.0, sup = 0.0;
+      if (k >= 2) sub = -(p.deltaTtracer * mM * rh * rdrF * kappa(ivK, kwK) * rdcK);
+      if (k <= Nr - 1) sup = -(p.deltaTtracer * mP * rh * rdrF * kappa(ivP, kwP) * rdcP);
+      sSub[me] = sub;
+      sSup[me] = sup;
+      sY[me] = y;
     }
   }
   __syncthreads();
@@ -1136,8 +1165,9 @@ __device__ __forceinline__ void tracer_impl_body(const Dims &d, const Params &p,
 #else
 #define TRI_ATTR
 #endif
+template <bool UL>
 __global__ void __launch_bounds__(256) TRI_ATTR k_tracer_impl(Dims d, Params p, Fields f, TracerArgs a, int nc) {
-  tracer_impl_body(d, p, f, a, nc, mg_xcd_block());
+  tracer_impl_body<UL>(d, p, f, a, nc, mg_xcd_block());
 }
 
 // gm = false: without GMREDI_CALC_TENSOR (it then rides in the next launch, launch_dyn_thermo)
@@ -1254,8 +1284,12 @@ hipError_t launch_tracer_step(const Dims &d, const Params &p, const Fields &f, c
   if (p.implicitDiffusion && impl) {
     const long ncol = (long)d.sNx * d.sNy * d.nT;
     const int nc = mg_colf_nc(ncol, d.Nr, 3);
-    MG_ALLOW_LDS(k_tracer_impl);
-    hipLaunchKernelGGL(k_tracer_impl, dim3(mg_colf_blocks(ncol, nc)), blk, mg_colf_lds(d.Nr, nc, 3), s, d, p, f, a, nc);
+    MG_ALLOW_LDS(k_tracer_impl<false>);
+    MG_ALLOW_LDS(k_tracer_impl<true>);
+    if (d.Nr >= 30)
+      hipLaunchKernelGGL(k_tracer_impl<true>, dim3(mg_colf_blocks(ncol, nc)), blk, mg_colf_lds(d.Nr, nc, 3), s, d, p, f, a, nc);
+    else
+      hipLaunchKernelGGL(k_tracer_impl<false>, dim3(mg_colf_blocks(ncol, nc)), blk, mg_colf_lds(d.Nr, nc, 3), s, d, p, f, a, nc);
   }
   return hipGetLastError();
 }
