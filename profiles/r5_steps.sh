@@ -39,6 +39,11 @@ for s in "$@"; do
                tests/test_gpu_cs32x15.py tests/test_gpu_options.py tests/test_gpu_3d.py > $O/fver_par.log 2>&1 ;;
     tr_ab) OUT=$O/tr_ab CONFIGS="global_ocean.90x40x15 global_ocean.cs32x15 llc90_synthetic" \
              LIBS="default base:mitgcm_amd/_build/diag/libmitgcm_amd_base.so" bash tools/lib_ab.sh > $O/tr_ab.log 2>&1 ;;
+    kc_ab) OUT=$O/kc_ab CONFIGS="llc90_synthetic" \
+             LIBS="default kc3:mitgcm_amd/_build/diag/libmitgcm_amd_kc3.so kc4:mitgcm_amd/_build/diag/libmitgcm_amd_kc4.so" \
+             bash tools/lib_ab.sh > $O/kc_ab.log 2>&1 ;;
+    x_ab) OUT=$O/x_ab CONFIGS="llc90_synthetic global_ocean.cs32x15" \
+             LIBS="default base:mitgcm_amd/_build/diag/libmitgcm_amd_base.so" bash tools/lib_ab.sh > $O/x_ab.log 2>&1 ;;
     vi_ab) OUT=$O/vi_ab CONFIGS="llc90_synthetic llc90_synthetic" \
              LIBS="default base:mitgcm_amd/_build/diag/libmitgcm_amd_base.so" bash tools/lib_ab.sh > $O/vi_ab.log 2>&1 ;;
     options) timeout -k 10 600 $PY tests/test_gpu_options.py > $O/options.log 2>&1 ;;
