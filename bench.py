@@ -50,7 +50,9 @@ PMC_TAG = {"global_ocean.90x40x15": "ocean90", "global_ocean.cs32x15": "cs32x15"
 
 def parse():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=1,
+                    help="N > 1: one process per GPU; launched under torch.distributed.run (WORLD_SIZE set) or, "
+                         "without a launcher, bench.py starts the N ranks itself (spawn_ranks)")
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--config", default="global_ocean.90x40x15",
@@ -61,11 +63,14 @@ def parse():
                     help="N>1: shard the workload's tiles over the N processes (RCCL, strong scaling, "
                          "mitgcm_amd/parallel.py) instead of running N replicas")
     ap.add_argument("--cg2d", choices=["auto", "replicated", "distributed", "device"], default="auto",
-                    help="with --shard: auto (default: the device CG2D where the solver is the multi-workgroup "
-                         "one, replicated where it is a single-CU kernel), CG2D replicated on every GPU, the "
-                         "reference's distributed CG2D with GLOBAL_SUM_TILE_RL over the collective, or the device "
-                         "CG2D whose parts run in every process on one IPC-shared hand-off block "
-                         "(mitgcm_amd/parallel.py)")
+                    help="sharded runs (--shard, and the N > 1 sharded records): auto (default: "
+                         "parallel.cg2d_policy's cost model -- one process keeps its resident solve; across "
+                         "GPUs a single-CU kernel is always replicated, and the multi-workgroup solve is "
+                         "replicated unless a 1/N share of its per-iteration work outweighs two fabric "
+                         "hand-offs, which is the case for none of the BASELINE configs), CG2D replicated on "
+                         "every GPU, the reference's distributed CG2D with GLOBAL_SUM_TILE_RL over the "
+                         "collective, or the device CG2D whose parts run in every process on one IPC-shared "
+                         "hand-off block (mitgcm_amd/parallel.py)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cs32", action="store_true", help="N = 1: skip the cs32x15 sub-record")
     ap.add_argument("--no-sharded", action="store_true", help="N > 1: skip the sharded cs32x15 / LLC-90 records")
@@ -462,8 +467,55 @@ def sharded_records(a, dist, world, rank, local, backend):
     return out
 
 
+def spawn_ranks(n, argv, script=None):
+    """`--gpus N` (N > 1) without a launcher: start N fresh worker processes of this same
+    command, one per GPU, with RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* set the way
+    torch.distributed.run sets them (127.0.0.1, a free port), and exit with the first failing
+    rank's status.  The parent has touched no GPU (nothing above imports torch), so the workers
+    are plain children, not an exec of a GPU process.  Rank 0's stdout (the one JSON line) is
+    the parent's; the other ranks print nothing there."""
+    import signal
+    import socket
+    import subprocess
+    sk = socket.socket()
+    sk.bind(("127.0.0.1", 0))
+    port = sk.getsockname()[1]
+    sk.close()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, script or os.path.abspath(__file__)] + list(argv), env=env,
+                                      stdout=None if r == 0 else sys.stderr.fileno()))
+    rc = 0
+    try:
+        pending = list(procs)
+        while pending:
+            for p in list(pending):
+                c = p.poll()
+                if c is None:
+                    continue
+                pending.remove(p)
+                if c != 0 and rc == 0:
+                    rc = c if c > 0 else 128 - c
+                    print("bench: rank %d exited with %d; stopping the others" % (procs.index(p), c), file=sys.stderr)
+                    for q in pending:
+                        q.send_signal(signal.SIGTERM)
+            time.sleep(0.05)
+    except KeyboardInterrupt:
+        for p in procs:
+            p.send_signal(signal.SIGTERM)
+        raise
+    return rc
+
+
 def main():
     a = parse()
+    if a.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(spawn_ranks(a.gpus, sys.argv[1:]))
+    if a.gpus != int(os.environ.get("WORLD_SIZE", "1")):
+        raise SystemExit("bench: --gpus %d but WORLD_SIZE=%s: launch one process per GPU (or give --gpus alone)"
+                         % (a.gpus, os.environ.get("WORLD_SIZE", "1")))
     # stdout carries ONE JSON line: whatever libraries print (RCCL's version banner at
     # communicator creation, ...) goes to stderr
     json_fd = os.dup(1)
@@ -502,6 +554,12 @@ def main():
                 dist.init_process_group("nccl", device_id=torch.device("cuda", local))   # RCCL over xGMI
         else:
             dist.init_process_group("gloo")   # replicas: barrier + max-reduce of host timers only
+    # the GPUs the job's ranks actually run on (a gloo rehearsal puts several ranks on one)
+    devices_used = 1
+    if world > 1:
+        devs = [None] * world
+        dist.all_gather_object(devs, "%s:%d" % (os.uname()[1], local))
+        devices_used = len(set(devs))
     # the sharded records run after the headline; a hang there (a collective a failed rank never
     # joins) must not cost the line: past the deadline rank 0 prints what it has and every
     # rank leaves
@@ -599,6 +657,8 @@ def main():
         "value_per_integration": model_days / elapsed,
         "unit": "model-days/s",
         "n_gpus": world,
+        "ranks": world,
+        "distinct_gpus": devices_used,
         "steps": a.steps,
         "warmup": a.warmup,
         "ms_per_step": 1e3 * elapsed / a.steps,

@@ -45,12 +45,14 @@ const char *mgcm_last_error(void);
  * mgcm_set_halo_map / mgcm_set_uv_map, over nTiles tiles of sNx x sNy with overlap OL.
  * Per-neighbour arrays in Fortran layout (ldNb = W2_maxNeighbours, ldT = W2_maxNbTiles), pij
  * (4, ldNb, ldT); tile ids 1-based as W2 numbers them.  Outputs hold nTiles*(sNx+2OL)*(sNy+2OL)
- * entries.  Returns -1 on an inconsistent topology.  (exch2_maps.hip) */
+ * entries.  useCubedSphereExchange (EEPARAMS.h, 0/1) gates the cube-corner u/v fix-ups as
+ * the reference's IF does (exch2_uv_3d_rx.template:79).  Returns -1 on an inconsistent
+ * topology.  (exch2_maps.hip) */
 int mgcm_exch2_maps(int sNx, int sNy, int OL, int nTiles, int ldNb, int ldT, const int *tBasex, const int *tBasey,
                     const int *isNedge, const int *isSedge, const int *isEedge, const int *isWedge,
                     const int *nNeighbours, const int *neighbourId, const int *opposingSend, const int *pij,
                     const int *oi, const int *oj, const int *iLo, const int *iHi, const int *jLo, const int *jHi,
-                    long *src, long *u1, long *v1, long *u0, long *v0);
+                    int useCubedSphereExchange, long *src, long *u1, long *v1, long *u0, long *v0);
 
 /* Run-time parameters (PARAMS.h names, already resolved as ini_parms.F does). */
 int mgcm_set_param(mgcm_model *m, const char *name, double value);
@@ -292,11 +294,12 @@ void mgcm_amd_set_maps_(const double *ids, const double *u1, const double *v1, c
                         const int *tFace, const int *tEdge, const int *nPts);
 /* The halo maps of a pkg/exch2 topology from the W2_EXCH2_TOPOLOGY.h COMMON arrays
  * W2_E2SETUP fills (mods/mgcm_amd_exch2.F; derived by mgcm_exch2_maps): one process holding
- * every tile in W2's order; ldNb = W2_maxNeighbours, ldT = W2_maxNbTiles. */
+ * every tile in W2's order; ldNb = W2_maxNeighbours, ldT = W2_maxNbTiles; useCS = the host's
+ * useCubedSphereExchange (0/1). */
 void mgcm_amd_set_w2_(const int *nTiles, const int *ldNb, const int *ldT, const int *myFace, const int *tBasex,
                       const int *tBasey, const int *isN, const int *isS, const int *isE, const int *isW, const int *nNb,
                       const int *nbId, const int *opp, const int *pij, const int *oi, const int *oj, const int *iLo,
-                      const int *iHi, const int *jLo, const int *jHi);
+                      const int *iHi, const int *jLo, const int *jHi, const int *useCS);
 /* One PARAMS.h parameter (LOGICAL as 0/1). */
 void mgcm_amd_param_(const char *name, const double *value, size_t len);
 /* Register a COMMON-block array of `count` doubles as device field `name`; kind 1 static

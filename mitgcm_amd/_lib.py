@@ -33,7 +33,7 @@ def lib():
         "mgcm_set_param": (ci, [vp, cs, cd]),
         "mgcm_set_iter": (ci, [vp, ci]),
         "mgcm_add_iter": (ci, [vp, ci]),
-        "mgcm_exch2_maps": (ci, [ci] * 6 + [PI] * 16 + [PL] * 5),
+        "mgcm_exch2_maps": (ci, [ci] * 6 + [PI] * 16 + [ci] + [PL] * 5),
         "mgcm_tracer_parity": (ci, [vp, ci]),
         "mgcm_get_param": (cd, [vp, cs]),
         "mgcm_put": (ci, [vp, cs, PD, cl]),

@@ -12,7 +12,8 @@
 //            bounds of EXCH2_GET_SCAL_BOUNDS (exch2_get_scal_bounds.F:56-133);
 //   C-grid   EXCH2_UV_3D_RX -> two EXCH2_RX2_CUBE passes (exch2_uv_3d_rx.template:60-226,
 //   vector   exch2_put_rx2.template:98-225), the bounds of EXCH2_GET_UV_BOUNDS
-//            (exch2_get_uv_bounds.F:84-262), then the cube-corner fix-ups.
+//            (exch2_get_uv_bounds.F:84-262), then the cube-corner fix-ups
+//            (under useCubedSphereExchange, exch2_uv_3d_rx.template:79).
 // Running that sequence on arrays of point ids instead of values gives, for every halo point,
 // the point (and for vectors the component and sign) it ends up holding: the maps the device
 // exchange kernels replay (mgcm_set_halo_map, mgcm_set_uv_map).  Every PUT of a pass reads
@@ -177,8 +178,8 @@ extern "C" int mgcm_exch2_maps(int sNx, int sNy, int OL, int nTiles, int ldNb, i
                                const int *tBasey, const int *isNedge, const int *isSedge, const int *isEedge,
                                const int *isWedge, const int *nNeighbours, const int *neighbourId,
                                const int *opposingSend, const int *pij, const int *oi, const int *oj, const int *iLo,
-                               const int *iHi, const int *jLo, const int *jHi, long *src, long *u1, long *v1, long *u0,
-                               long *v0) {
+                               const int *iHi, const int *jLo, const int *jHi, int useCubedSphereExchange, long *src,
+                               long *u1, long *v1, long *u0, long *v0) {
   if (sNx < 1 || sNy < 1 || OL < 1 || nTiles < 1 || ldNb < 1 || ldT < nTiles) return -1;
   const W2 w{sNx, sNy, OL, nTiles, ldNb, ldT, tBasex, tBasey, isNedge, isSedge, isEedge, isWedge, nNeighbours,
              neighbourId, opposingSend, pij, oi, oj, iLo, iHi, jLo, jHi};
@@ -201,11 +202,12 @@ extern "C" int mgcm_exch2_maps(int sNx, int sNy, int OL, int nTiles, int ldNb, i
     std::vector<int> us(N, 1), vs(N, 1);
     for (long q = 0; q < N; q++) { u[q] = q; v[q] = N + q; }
     if (!rx2_pass(w, u, us, v, vs, false, signs) || !rx2_pass(w, u, us, v, vs, true, signs)) return -1;
-    // the cube-corner values of u / v outside the facet edges (exch2_uv_3d_rx.template:130-226)
+    // the cube-corner values of u / v outside the facet edges (exch2_uv_3d_rx.template:130-226),
+    // inside the reference's IF ( useCubedSphereExchange ) (exch2_uv_3d_rx.template:79)
     const int nX = sNx, nY = sNy, neg = signs ? -1 : 1;
     auto cp = [&](std::vector<long> &dst, std::vector<int> &dsg, long d, const std::vector<long> &s_, const std::vector<int> &ssg,
                   long s, int f) { dst[d] = s_[s]; dsg[d] = ssg[s] * f; };
-    for (int t = 1; t <= nTiles; t++) {
+    for (int t = 1; useCubedSphereExchange && t <= nTiles; t++) {
       auto G = [&](int i, int j) { return w.g(t, i, j); };
       const bool sW = isWedge[t - 1], sE = isEedge[t - 1], sS = isSedge[t - 1], sN = isNedge[t - 1];
       if (OL >= 2 && sW && sS) { cp(u, us, G(0, 0), v, vs, G(1, 0), 1); cp(v, vs, G(0, 0), u, us, G(0, 1), 1); }

@@ -146,7 +146,7 @@ struct FortranSide {
   // parity, and the parity each model is left at by the captured step's host-side swaps
   struct MultiGraph {
     hipGraphExec_t exec = nullptr;
-    std::vector<int> post;
+    std::vector<int> pre, post;   // every model's tracer parity before / after the captured step
   } mg[4];
   bool capturing = false;     // set_iter inside a capture: device increments, not values
   bool multiGraphOff = false; // a capture failed: the multi-model steps stay eager
@@ -515,21 +515,27 @@ void enter_time_loop(const char *where) {
 }
 
 // One routine drop-in.  Host-authoritative (initialisation): state in, the device
-// routine, state out.  Device-authoritative: the host input first when `input`.
-void routine(const char *where, void (*op)(const char *), int myIter, double myTime, bool input = false) {
+// routine, state out.  Device-authoritative: the host input first when `input`.  myIter /
+// myTime are the values the reference passes the routine; the device's counter (AB2's
+// first-step rule, the CD scheme's start) is set to devIter when given (staggered
+// THERMODYNAMICS lags only that index, temp_integrate.F:154-155).
+constexpr int kNoIter = -2147483647 - 1;
+void routine(const char *where, void (*op)(const char *), int myIter, double myTime, bool input = false,
+             int devIter = kNoIter) {
   model(where);
   if (!g.ready) die(where, "called before MGCM_AMD_INIT");
   g.lastIter = myIter;
   g.lastTime = myTime;
+  const int it = devIter == kNoIter ? myIter : devIter;
   if (!g.deviceAuth) {
     upload(where, K_STATE | K_INPUT);
-    set_iter(where, myIter);
+    set_iter(where, it);
     op(where);
     download(where);
     return;
   }
   if (input) upload(where, K_INPUT);
-  set_iter(where, myIter);
+  set_iter(where, it);
   op(where);
 }
 
@@ -730,8 +736,11 @@ bool multi_replay(const char *w, int myIter) {
   const int q = mgcm_tracer_parity(g.m, -1);
   if (q < 0 || q > 3) die(w);
   auto &G = g.mg[q];
+  std::vector<int> pre;
+  for (auto &s : g.sh) pre.push_back(mgcm_tracer_parity(s.m, -1));
   join_into_0(w);   // the forcing uploads of every model before the graph
   if (!G.exec) {
+    G.pre = pre;
     hipStream_t s0 = stream_of(g.sh[0]);
     // every model issues on model 0's stream while capturing: the graph is one chain of the
     // models' work in the recorded order (graphs captured across two or more streams of one GPU
@@ -768,6 +777,9 @@ bool multi_replay(const char *w, int myIter) {
     G.post.clear();
     for (auto &s : g.sh) G.post.push_back(mgcm_tracer_parity(s.m, -1));
   } else {
+    // the graph holds the theta/salt buffer pointers of the parities it was captured at: every
+    // model must start there (a model stepped apart -- eagerly -- would drift)
+    if (pre != G.pre) die(w, "a device model's tracer parity differs from the captured step's");
     for (size_t i = 0; i < g.sh.size(); i++)
       if (mgcm_tracer_parity(g.sh[i].m, G.post[i]) < 0) die(w);
   }
@@ -894,14 +906,15 @@ void mgcm_amd_set_maps_(const double *ids, const double *u1, const double *v1, c
 void mgcm_amd_set_w2_(const int *nTilesW2, const int *ldNb, const int *ldT, const int *myFace, const int *tBasex,
                       const int *tBasey, const int *isN, const int *isS, const int *isE, const int *isW, const int *nNb,
                       const int *nbId, const int *opp, const int *pij, const int *oi, const int *oj, const int *iLo,
-                      const int *iHi, const int *jLo, const int *jHi) {
+                      const int *iHi, const int *jLo, const int *jHi, const int *useCS) {
   model("MGCM_AMD_SET_W2");
   const int nt = *nTilesW2;
   if (nt != (int)nTiles()) die("MGCM_AMD_SET_W2", "exch2_nTiles differs from nSx*nSy");
   const long n = (long)nt * n2();
   std::vector<long> src(n), cu1(n), cv1(n), cu0(n), cv0(n);
   if (mgcm_exch2_maps(g.dims[0], g.dims[1], g.dims[2], nt, *ldNb, *ldT, tBasex, tBasey, isN, isS, isE, isW, nNb, nbId,
-                      opp, pij, oi, oj, iLo, iHi, jLo, jHi, src.data(), cu1.data(), cv1.data(), cu0.data(), cv0.data()))
+                      opp, pij, oi, oj, iLo, iHi, jLo, jHi, *useCS != 0, src.data(), cu1.data(), cv1.data(), cu0.data(),
+                      cv0.data()))
     die("MGCM_AMD_SET_W2", "inconsistent W2_EXCH2_TOPOLOGY arrays");
   std::vector<int> face(nt), edge(nt);
   for (int t = 0; t < nt; t++) {
@@ -1088,14 +1101,16 @@ void do_oceanic_phys_amd_(const double *myTime, const int *myIter, const int *my
 /* SUBROUTINE THERMODYNAMICS(myTime, myIter, myThid)      model/src/thermodynamics.F:25
  * Under staggerTimeStep FORWARD_STEP calls it after advancing myIter (forward_step.F:806,
  * 1032) and TEMP/SALT_INTEGRATE step the Adams-Bashforth terms at iterNb = myIter - 1
- * (temp_integrate.F:154-155): the device's counter is the step's start either way. */
+ * (temp_integrate.F:154-155) while everything else keeps the advanced myIter / myTime
+ * (temp_integrate.F:275-543): only the device's AB counter is lagged, to the step's start.
+ * The advanced values are the step's end, as after forward_step.F:806. */
 void thermodynamics_amd_(const double *myTime, const int *myIter, const int *myThid) {
   (void)myThid;
   enter_time_loop("THERMODYNAMICS_AMD");
-  if (absorbed("THERMODYNAMICS")) return;
   const bool late = staggered();
-  routine("THERMODYNAMICS_AMD", op_tracer_step, late ? *myIter - 1 : *myIter,
-          late ? *myTime - g.rd.deltaTClock : *myTime);
+  if (late) advanced(*myIter, *myTime);
+  if (absorbed("THERMODYNAMICS")) return;
+  routine("THERMODYNAMICS_AMD", op_tracer_step, *myIter, *myTime, false, late ? *myIter - 1 : kNoIter);
 }
 /* SUBROUTINE DYNAMICS(myTime, myIter, myThid)            model/src/dynamics.F:21 */
 void dynamics_amd_(const double *myTime, const int *myIter, const int *myThid) {

@@ -684,8 +684,10 @@ class ShardedModel:
     def replay(self, npairs=1, check=None):
         """Replay the captured pair of steps npairs times (the device's per-step record ring
         restarts at the first replay); with check, the batch's solve records are read back
-        and a failed solve raises (check_solves).  check=None: only for the device CG2D, the
-        one solver whose hand-offs can time out (the read-back synchronises the host)."""
+        and a failed solve raises (check_solves).  check=None: whenever the model's solver is
+        the multi-workgroup one (its grid hand-offs can time out, numIters = -1), whether it
+        runs across processes (cg2d="device") or replicated per process (phases 2 / 19);
+        the single-CU kernels cannot time out (the read-back synchronises the host)."""
         self._check_records(2 * npairs)
         self.check(self.L.mgcm_begin_steps(self.m.h), "mgcm_begin_steps")   # on self.stream
         if self.model_stream != "shared":
@@ -696,18 +698,24 @@ class ShardedModel:
         if self.model_stream != "shared":
             self._consume()   # the model's later work after the replays
         self.check(self.L.mgcm_end_steps(self.m.h, 2 * npairs), "mgcm_end_steps")
-        if check or (check is None and self.cg2d == "device"):
+        if check or (check is None and self._may_time_out()):
             self.check_solves(2 * npairs)
 
     def forward_step(self, nsteps=1, check=None):
         """nsteps sharded FORWARD_STEPs; with check, a failed solve raises (check_solves);
-        check=None: only for the device CG2D (as replay)."""
+        check=None: whenever the solver is the multi-workgroup one (as replay)."""
         self._check_records(nsteps)
         self.check(self.L.mgcm_begin_steps(self.m.h), "mgcm_begin_steps")
         for _ in range(nsteps):
             self.step()
-        if check or (check is None and self.cg2d == "device"):
+        if check or (check is None and self._may_time_out()):
             self.check_solves(nsteps)
+
+    def _may_time_out(self):
+        """The solves whose records must be read back: the multi-workgroup CG2D's grid
+        hand-off can time out in the device and the replicated mode alike; the distributed
+        solve is decided on the host and raises there."""
+        return self.cg2d != "distributed" and (self.cg2d == "device" or self.m.cg2d_kernel() == "mwg")
 
     def gather_field(self, name):
         """The whole-domain field assembled from every owner (host numpy), e.g.

@@ -101,7 +101,7 @@ def test_gyre_10_steps_vs_reference_output(gyre, golden_dir):
     from mitgcm_amd.model import dynstat
     gold = json.load(open(os.path.join(golden_dir, "tutorial_barotropic_gyre", "monitor.json")))
     m = gyre.make_model(gyre.barotropic_gyre)
-    worst = {"check": (99.0, None), "other": (99.0, None)}
+    worst = {"slice": (99.0, None), "check": (99.0, None), "other": (99.0, None)}
     for n in range(1, 11):
         m.forward_step(1)
         r = m.solve_stats()
@@ -111,13 +111,16 @@ def test_gyre_10_steps_vs_reference_output(gyre, golden_dir):
         for k, v in r.items():
             if k not in gstep or k == "cg2d_iters" or k.endswith("_mean") or k == "cg2d_last_res":
                 continue
-            cls = "check" if (k == "cg2d_init_res" or (k.split("_")[1] in ("uvel", "vvel", "theta", "salt")
-                                                       and not k.endswith("del2"))) else "other"
+            # SURVEY 7's minimum slice: cg2d_init_res and dynstat_eta_* >= 12; testreport's check
+            # list (u/v/theta/salt statistics) >= 11
+            cls = "slice" if (k == "cg2d_init_res" or k.startswith("dynstat_eta_")) else (
+                "check" if (k.split("_")[1] in ("uvel", "vvel", "theta", "salt") and not k.endswith("del2")) else "other")
             dg = digits(v, gstep[k])
             if dg < worst[cls][0]:
                 worst[cls] = (dg, (n, k))
-    print("gyre 10 steps: worst digits on testreport's check list %.2f at %s; other dynstat %.2f at %s"
-          % (worst["check"] + worst["other"]))
+    print("gyre 10 steps: worst digits on cg2d_init_res + dynstat_eta_* %.2f at %s; testreport's check list %.2f "
+          "at %s; other dynstat %.2f at %s" % (worst["slice"] + worst["check"] + worst["other"]))
+    assert worst["slice"][0] >= 12.0, worst["slice"]
     assert worst["check"][0] >= 11.0, worst["check"]
     assert worst["other"][0] >= 10.0, worst["other"]
     m.close()

@@ -63,7 +63,7 @@ def test_library_exports_every_header_symbol():
     assert declared == set(_lib.EXPORTS)
 
 
-def _w2_maps(topo, ldNb=None, ldT=None, mutate=None, want_rc=0):
+def _w2_maps(topo, ldNb=None, ldT=None, mutate=None, want_rc=0, cubed=1):
     """mgcm_exch2_maps (the library's derivation from the W2_EXCH2_TOPOLOGY.h arrays, host
     only) on the arrays of an exch2.py topology (at leading dimensions ldNb, ldT; mutate(a)
     edits them first)."""
@@ -81,7 +81,7 @@ def _w2_maps(topo, ldNb=None, ldT=None, mutate=None, want_rc=0):
                               "exch2_isWedge", "exch2_nNeighbours", "exch2_neighbourId", "exch2_opposingSend",
                               "exch2_pij", "exch2_oi", "exch2_oj", "exch2_iLo", "exch2_iHi", "exch2_jLo", "exch2_jHi")]
     rc = lib().mgcm_exch2_maps(topo.sNx, topo.sNy, topo.OLx, topo.nTiles_, a["ldNb"], a["ldT"],
-                               *[IP(x) for x in args], *[LP(x) for x in out])
+                               *[IP(x) for x in args], cubed, *[LP(x) for x in out])
     assert rc == want_rc
     return out
 
@@ -144,3 +144,29 @@ def test_exch2_maps_padded_and_refused():
         a["exch2_nNeighbours"][2] = a["ldNb"] + 1
     for m in (bad_id, bad_opp, bad_count):
         _w2_maps(topo, mutate=m, want_rc=-1)
+
+
+def test_exch2_maps_corners_follow_use_cubed_sphere_exchange():
+    """The cube-corner u/v fix-ups sit inside the reference's IF ( useCubedSphereExchange )
+    (exch2_uv_3d_rx.template:79): with the flag off the library's maps are those of the two
+    EXCH2_RX2_CUBE passes alone -- identical to the flag-on maps everywhere except at the
+    corner halo points of tiles with two facet edges, and the scalar map is unchanged."""
+    from mitgcm_amd import exch2
+    topo = exch2.cube_topology(32, 32, 32, 4)
+    on = _w2_maps(topo)
+    off = _w2_maps(topo, cubed=0)
+    assert np.array_equal(on[0], off[0])
+    nx = topo.sNx + 2 * topo.OLx
+    corners = set()
+    for t in range(topo.nTiles_):
+        for i, j in ((0, 0), (1, 0), (0, 1), (0, topo.sNy + 1), (0, topo.sNy + 2), (1, topo.sNy + 2),
+                     (topo.sNx + 2, 0), (topo.sNx, 0), (topo.sNx + 1, 0), (topo.sNx + 2, 1),
+                     (topo.sNx + 2, topo.sNy + 1), (topo.sNx + 1, topo.sNy + 2), (topo.sNx + 2, topo.sNy),
+                     (topo.sNx, topo.sNy + 2)):
+            corners.add(t * topo.n2 + (j + topo.OLx - 1) * nx + (i + topo.OLx - 1))
+    ndiff = 0
+    for a, b in zip(on[1:], off[1:]):
+        d = set(np.nonzero(a != b)[0].tolist())
+        assert d and d <= corners
+        ndiff += len(d)
+    assert ndiff > 0

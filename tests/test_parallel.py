@@ -402,3 +402,26 @@ def test_cg2d_policy():
     assert cg2d_policy("mwg", 6, 6, pinned=True, compute_us=MWG_COMPUTE_US_PER_ITER)[0] == "replicated"
     assert cg2d_policy("mwg", 8, 117, pinned=False, compute_us=MWG_COMPUTE_US_PER_ITER)[0] == "replicated"
     assert cg2d_policy("mwg", 8, 4096, pinned=False, compute_us=100.0)[0] == "device"
+
+
+def test_solve_check_default():
+    """ShardedModel.replay / forward_step with check=None read the solve records back whenever
+    the solver is the multi-workgroup one -- replicated (phases 2 / 19 launch it too, and its
+    hand-off can time out) as well as across processes -- and not for a single-CU kernel or
+    the host-decided distributed solve."""
+    from mitgcm_amd.parallel import ShardedModel
+
+    class _M:
+        def __init__(self, k):
+            self.k = k
+
+        def cg2d_kernel(self):
+            return self.k
+
+    def may(kernel, mode):
+        sm = ShardedModel.__new__(ShardedModel)   # no process group: only the predicate
+        sm.m, sm.cg2d = _M(kernel), mode
+        return sm._may_time_out()
+
+    assert may("mwg", "replicated") and may("mwg", "device") and may("bxy", "device")
+    assert not may("bxy", "replicated") and not may("mwg", "distributed")
