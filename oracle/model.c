@@ -270,10 +270,12 @@ static void exch2_scalar(OModel *m, double *a, int nz) {
   const long N2 = m->n2 * m->nTiles;
   for (int k = 0; k < nz; k++) {
     double *tmp = (double *)malloc(N2 * sizeof(double));
+#pragma omp parallel for schedule(static) if (m->nThreads > 1) num_threads(m->nThreads > 1 ? m->nThreads : 1)
     for (long q = 0; q < N2; q++) {
       const long s = m->exchS[q], st = s / m->n2, sl = s % m->n2;
       tmp[q] = a[sl + (long)k * m->n2 + st * m->n2 * nz];
     }
+#pragma omp parallel for schedule(static) if (m->nThreads > 1) num_threads(m->nThreads > 1 ? m->nThreads : 1)
     for (long q = 0; q < N2; q++) a[q % m->n2 + (long)k * m->n2 + (q / m->n2) * m->n2 * nz] = tmp[q];
     free(tmp);
   }
@@ -289,6 +291,7 @@ void oracle_exch_uv_xyz(OModel *m, double *u, double *v, int nz, int withSigns) 
     for (int c = 0; c < 2; c++) {
       const long *code = c ? cv : cu;
       double *out = c ? tv : tu;
+#pragma omp parallel for schedule(static) if (m->nThreads > 1) num_threads(m->nThreads > 1 ? m->nThreads : 1)
       for (long q = 0; q < N2; q++) {
         const long e = code[q];
         if (e == 0) { out[q] = c ? AT(v, q) : AT(u, q); continue; }
@@ -297,35 +300,59 @@ void oracle_exch_uv_xyz(OModel *m, double *u, double *v, int nz, int withSigns) 
         out[q] = e > 0 ? val : -val;
       }
     }
+#pragma omp parallel for schedule(static) if (m->nThreads > 1) num_threads(m->nThreads > 1 ? m->nThreads : 1)
     for (long q = 0; q < N2; q++) { AT(u, q) = tu[q]; AT(v, q) = tv[q]; }
 #undef AT
   }
   free(tu); free(tv);
 }
 
-void oracle_exch_xyz(OModel *m, double *a, int nz) {
-  if (m->exchS) { exch2_scalar(m, a, nz); return; }
+/* EXCH1's periodic lat-lon copies into the halo of destination tile t (levels 1..nz) */
+static void exch_tile(OModel *m, double *a, int nz, int t) {
   const int sNx = m->sNx, sNy = m->sNy, OLx = m->OLx, OLy = m->OLy;
   const int Nx = sNx * m->nSx, Ny = sNy * m->nSy;
-  for (int t = 0; t < m->nTiles; t++) {
-    int bi = t % m->nSx, bj = t / m->nSx;
-    for (int k = 1; k <= nz; k++)
-      for (int j = 1 - OLy; j <= sNy + OLy; j++)
-        for (int i = 1 - OLx; i <= sNx + OLx; i++) {
-          if (i >= 1 && i <= sNx && j >= 1 && j <= sNy) continue;
-          int iG = bi * sNx + i - 1, jG = bj * sNy + j - 1;
-          iG = ((iG % Nx) + Nx) % Nx; jG = ((jG % Ny) + Ny) % Ny;
-          int st = (jG / sNy) * m->nSx + iG / sNx;
-          int si = iG % sNx + 1, sj = jG % sNy + 1;
-          long dst = (long)(i + OLx - 1) + (long)(j + OLy - 1) * m->nx + (long)(k - 1) * m->n2 +
-                     (long)t * m->n2 * nz;
-          long src = (long)(si + OLx - 1) + (long)(sj + OLy - 1) * m->nx + (long)(k - 1) * m->n2 +
-                     (long)st * m->n2 * nz;
-          a[dst] = a[src];
-        }
-  }
+  int bi = t % m->nSx, bj = t / m->nSx;
+  for (int k = 1; k <= nz; k++)
+    for (int j = 1 - OLy; j <= sNy + OLy; j++)
+      for (int i = 1 - OLx; i <= sNx + OLx; i++) {
+        if (i >= 1 && i <= sNx && j >= 1 && j <= sNy) continue;
+        int iG = bi * sNx + i - 1, jG = bj * sNy + j - 1;
+        iG = ((iG % Nx) + Nx) % Nx; jG = ((jG % Ny) + Ny) % Ny;
+        int st = (jG / sNy) * m->nSx + iG / sNx;
+        int si = iG % sNx + 1, sj = jG % sNy + 1;
+        long dst = (long)(i + OLx - 1) + (long)(j + OLy - 1) * m->nx + (long)(k - 1) * m->n2 +
+                   (long)t * m->n2 * nz;
+        long src = (long)(si + OLx - 1) + (long)(sj + OLy - 1) * m->nx + (long)(k - 1) * m->n2 +
+                   (long)st * m->n2 * nz;
+        a[dst] = a[src];
+      }
+}
+
+/* every source is an interior point and every destination a halo one: the copies of all
+ * destination tiles are independent, so the tiles go over the threads (OpenMP build) */
+void oracle_exch_xyz(OModel *m, double *a, int nz) {
+  if (m->exchS) { exch2_scalar(m, a, nz); return; }
+#pragma omp parallel for schedule(static) if (m->nThreads > 1) num_threads(m->nThreads > 1 ? m->nThreads : 1)
+  for (int t = 0; t < m->nTiles; t++) exch_tile(m, a, nz, t);
 }
 void oracle_exch_xy(OModel *m, double *a) { oracle_exch_xyz(m, a, 1); }
+
+/* oracle_exch_xy inside an enclosing OpenMP parallel region (the CG2D's): an orphaned
+ * work-shared loop, with the barrier at its end; sequential outside one.  The exch2 gather
+ * runs in place here (interior sources, halo destinations: the same values as the staged copy). */
+void oracle_exch_xy_for(OModel *m, double *a) {
+  if (m->exchS) {
+    const long N2 = m->n2 * m->nTiles;
+#pragma omp for schedule(static)
+    for (long q = 0; q < N2; q++) {
+      const long s = m->exchS[q];
+      if (s != q) a[q] = a[s];
+    }
+    return;
+  }
+#pragma omp for schedule(static)
+  for (int t = 0; t < m->nTiles; t++) exch_tile(m, a, 1, t);
+}
 
 /* ---------------------------------------------------------- grid & masks */
 int oracle_ini_grid(OModel *m) {

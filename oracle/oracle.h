@@ -155,6 +155,7 @@ int oracle_ini_cg2d(OModel *m);                      /* INI_CG2D */
 
 /* exchanges (EXCH1, lat-lon, periodic over the nSx x nSy tile layout) */
 void oracle_exch_xy(OModel *m, double *a);
+void oracle_exch_xy_for(OModel *m, double *a);   /* inside an OpenMP parallel region */
 void oracle_exch_xyz(OModel *m, double *a, int nz);
 /* EXCH_UV_XYZ_RL / EXCH_UV_XY_RL (C-grid vector pair; EXCH1: two scalar exchanges) */
 void oracle_exch_uv_xyz(OModel *m, double *u, double *v, int nz, int withSigns);

@@ -306,8 +306,18 @@ void oracle_cg2d(OModel *m, double *cg2d_b, double *cg2d_x, double *firstResidua
         }
   }
   oracle_exch_xy(m, cg2d_x);
+  /* OpenMP (bench.py's multi-core baseline): every tile loop below over threads, one tile per
+   * iteration; each tile's partial is summed sequentially inside its thread and the partials in
+   * tile order by one thread (GLOBAL_SUM_TILE_RL), the halo fills split over destination tiles:
+   * bit-identical to one thread.  The scalars are shared, set in `single` blocks (whose barrier
+   * publishes them), so every thread takes the same exit. */
+  const int minRes = *nIterMin >= 0, maxIts = *numIters;
+  int stop = 0;
+#pragma omp parallel if (m->nThreads > 1) num_threads(m->nThreads > 1 ? m->nThreads : 1)
+  {
+#pragma omp for schedule(static)
   for (int t = 0; t < nT; t++) {
-    if (*nIterMin >= 0)
+    if (minRes)
       for (int j = 1; j <= sNy; j++)
         for (int i = 1; i <= sNx; i++) xmin[O2(m, i, j, t)] = cg2d_x[O2(m, i, j, t)];
     double sumT = 0.0, errT = 0.0;
@@ -328,81 +338,103 @@ void oracle_cg2d(OModel *m, double *cg2d_b, double *cg2d_x, double *firstResidua
     tile[t] = errT; tile2[t] = sumT;
   }
   /* EXCH_S3D_RL(cg2d_r, 1): halo width 1 fill; the full-halo periodic copy is a superset */
-  oracle_exch_xy(m, r);
+  oracle_exch_xy_for(m, r);
+#pragma omp single
+  {
   err_sq = dev ? (fmaMode ? plan_dot(m, r, r) : plan_sum(m, term)) : gsum_tiles(tile, nT);
   sumRHS = dev ? plan_sum(m, term2) : gsum_tiles(tile2, nT);
   *firstResidual = sqrt(err_sq);
-  if (*nIterMin >= 0) { *nIterMin = 0; *minResidualSq = err_sq; }
+  if (minRes) { *nIterMin = 0; *minResidualSq = err_sq; }
   m->sumRHS = sumRHS; m->rhsMax = rhsMax;
-  if (!(err_sq < m->cg2dTolerance_sq)) {
-    for (int it2d = 1; it2d <= *numIters; it2d++) {
-      for (int t = 0; t < nT; t++) {
-        double e = 0.0;
-        for (int j = 1; j <= sNy; j++)
-          for (int i = 1; i <= sNx; i++) {
-            long p = O2(m, i, j, t);
-            if (fmaMode)
-              q[p] = fma(pS[O2(m, i, j + 1, t)], r[O2(m, i, j + 1, t)], fma(pS[p], r[O2(m, i, j - 1, t)],
-                     fma(pW[O2(m, i + 1, j, t)], r[O2(m, i + 1, j, t)], fma(pW[p], r[O2(m, i - 1, j, t)], pC[p] * r[p]))));
-            else
-              q[p] = pC[p] * r[p] + pW[p] * r[O2(m, i - 1, j, t)] + pW[O2(m, i + 1, j, t)] * r[O2(m, i + 1, j, t)] +
-                     pS[p] * r[O2(m, i, j - 1, t)] + pS[O2(m, i, j + 1, t)] * r[O2(m, i, j + 1, t)];
-            e = e + q[p] * r[p];
-            term[p] = q[p] * r[p];
-          }
-        tile[t] = e;
-      }
-      eta_qrN = dev ? (fmaMode ? plan_dot(m, q, r) : plan_sum(m, term)) : gsum_tiles(tile, nT);
-      cgBeta = eta_qrN / eta_qrNM1;
-      eta_qrNM1 = eta_qrN;
+  stop = !(err_sq < m->cg2dTolerance_sq) ? 0 : 1;
+  }
+  for (int it2d = 1; !stop && it2d <= maxIts; it2d++) {
+#pragma omp for schedule(static)
+    for (int t = 0; t < nT; t++) {
+      double e = 0.0;
+      for (int j = 1; j <= sNy; j++)
+        for (int i = 1; i <= sNx; i++) {
+          long p = O2(m, i, j, t);
+          if (fmaMode)
+            q[p] = fma(pS[O2(m, i, j + 1, t)], r[O2(m, i, j + 1, t)], fma(pS[p], r[O2(m, i, j - 1, t)],
+                   fma(pW[O2(m, i + 1, j, t)], r[O2(m, i + 1, j, t)], fma(pW[p], r[O2(m, i - 1, j, t)], pC[p] * r[p]))));
+          else
+            q[p] = pC[p] * r[p] + pW[p] * r[O2(m, i - 1, j, t)] + pW[O2(m, i + 1, j, t)] * r[O2(m, i + 1, j, t)] +
+                   pS[p] * r[O2(m, i, j - 1, t)] + pS[O2(m, i, j + 1, t)] * r[O2(m, i, j + 1, t)];
+          e = e + q[p] * r[p];
+          term[p] = q[p] * r[p];
+        }
+      tile[t] = e;
+    }
+#pragma omp single
+    {
+    eta_qrN = dev ? (fmaMode ? plan_dot(m, q, r) : plan_sum(m, term)) : gsum_tiles(tile, nT);
+    cgBeta = eta_qrN / eta_qrNM1;
+    eta_qrNM1 = eta_qrN;
+    }
+#pragma omp for schedule(static)
+    for (int t = 0; t < nT; t++)
+      for (int j = 1; j <= sNy; j++)
+        for (int i = 1; i <= sNx; i++) {
+          long p = O2(m, i, j, t);
+          s[p] = fmaMode ? fma(cgBeta, s[p], q[p]) : q[p] + cgBeta * s[p];
+        }
+    oracle_exch_xy_for(m, s);
+#pragma omp for schedule(static)
+    for (int t = 0; t < nT; t++) {
+      double a = 0.0;
+      for (int j = 1; j <= sNy; j++)
+        for (int i = 1; i <= sNx; i++) {
+          long p = O2(m, i, j, t);
+          if (fmaMode)
+            q[p] = applyA_fma(m, s, i, j, t);
+          else
+            q[p] = aW[p] * s[O2(m, i - 1, j, t)] + aW[O2(m, i + 1, j, t)] * s[O2(m, i + 1, j, t)] +
+                   aS[p] * s[O2(m, i, j - 1, t)] + aS[O2(m, i, j + 1, t)] * s[O2(m, i, j + 1, t)] + aC[p] * s[p];
+          a = a + s[p] * q[p];
+          term[p] = s[p] * q[p];
+        }
+      tile[t] = a;
+    }
+#pragma omp single
+    {
+    alpha = dev ? (fmaMode ? plan_dot(m, s, q) : plan_sum(m, term)) : gsum_tiles(tile, nT);
+    alpha = eta_qrN / alpha;
+    }
+#pragma omp for schedule(static)
+    for (int t = 0; t < nT; t++) {
+      double e = 0.0;
+      for (int j = 1; j <= sNy; j++)
+        for (int i = 1; i <= sNx; i++) {
+          long p = O2(m, i, j, t);
+          cg2d_x[p] = fmaMode ? fma(alpha, s[p], cg2d_x[p]) : cg2d_x[p] + alpha * s[p];
+          r[p] = fmaMode ? fma(-alpha, q[p], r[p]) : r[p] - alpha * q[p];
+          e = e + r[p] * r[p];
+          term[p] = r[p] * r[p];
+        }
+      tile[t] = e;
+    }
+    int save = 0;
+#pragma omp single copyprivate(save)
+    {
+    actualIts = it2d;
+    err_sq = dev ? (fmaMode ? plan_dot(m, r, r) : plan_sum(m, term)) : gsum_tiles(tile, nT);
+    if (err_sq < m->cg2dTolerance_sq) stop = 1;
+    else if (err_sq < *minResidualSq) {
+      *minResidualSq = err_sq;
+      *nIterMin = it2d;
+      save = 1;
+    }
+    }
+    if (stop) break;
+    if (save) {
+#pragma omp for schedule(static)
       for (int t = 0; t < nT; t++)
         for (int j = 1; j <= sNy; j++)
-          for (int i = 1; i <= sNx; i++) {
-            long p = O2(m, i, j, t);
-            s[p] = fmaMode ? fma(cgBeta, s[p], q[p]) : q[p] + cgBeta * s[p];
-          }
-      oracle_exch_xy(m, s);
-      for (int t = 0; t < nT; t++) {
-        double a = 0.0;
-        for (int j = 1; j <= sNy; j++)
-          for (int i = 1; i <= sNx; i++) {
-            long p = O2(m, i, j, t);
-            if (fmaMode)
-              q[p] = applyA_fma(m, s, i, j, t);
-            else
-              q[p] = aW[p] * s[O2(m, i - 1, j, t)] + aW[O2(m, i + 1, j, t)] * s[O2(m, i + 1, j, t)] +
-                     aS[p] * s[O2(m, i, j - 1, t)] + aS[O2(m, i, j + 1, t)] * s[O2(m, i, j + 1, t)] + aC[p] * s[p];
-            a = a + s[p] * q[p];
-            term[p] = s[p] * q[p];
-          }
-        tile[t] = a;
-      }
-      alpha = dev ? (fmaMode ? plan_dot(m, s, q) : plan_sum(m, term)) : gsum_tiles(tile, nT);
-      alpha = eta_qrN / alpha;
-      for (int t = 0; t < nT; t++) {
-        double e = 0.0;
-        for (int j = 1; j <= sNy; j++)
-          for (int i = 1; i <= sNx; i++) {
-            long p = O2(m, i, j, t);
-            cg2d_x[p] = fmaMode ? fma(alpha, s[p], cg2d_x[p]) : cg2d_x[p] + alpha * s[p];
-            r[p] = fmaMode ? fma(-alpha, q[p], r[p]) : r[p] - alpha * q[p];
-            e = e + r[p] * r[p];
-            term[p] = r[p] * r[p];
-          }
-        tile[t] = e;
-      }
-      actualIts = it2d;
-      err_sq = dev ? (fmaMode ? plan_dot(m, r, r) : plan_sum(m, term)) : gsum_tiles(tile, nT);
-      if (err_sq < m->cg2dTolerance_sq) break;
-      if (err_sq < *minResidualSq) {
-        *minResidualSq = err_sq;
-        *nIterMin = it2d;
-        for (int t = 0; t < nT; t++)
-          for (int j = 1; j <= sNy; j++)
-            for (int i = 1; i <= sNx; i++) xmin[O2(m, i, j, t)] = cg2d_x[O2(m, i, j, t)];
-      }
-      oracle_exch_xy(m, r);
+          for (int i = 1; i <= sNx; i++) xmin[O2(m, i, j, t)] = cg2d_x[O2(m, i, j, t)];
     }
+    oracle_exch_xy_for(m, r);
+  }
   }
   if (*nIterMin >= 0 && err_sq > *minResidualSq)
     for (int t = 0; t < nT; t++)

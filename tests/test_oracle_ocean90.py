@@ -60,18 +60,23 @@ def test_oracle_one_tile_layout(golden_dir, nsteps):
     assert min(r[0] for r in res if r[2] in loose) >= 6.0
 
 
-def test_openmp_oracle_bit_identical():
+@pytest.mark.parametrize("case", ["ocean90_9x4", "ocean90_3x2", "cs32x15"])
+def test_openmp_oracle_bit_identical(case):
     """The OpenMP build of the oracle (liboracle_omp.so: DYNAMICS, THERMODYNAMICS and
-    DO_OCEANIC_PHYS over the tiles in parallel; bench.py's multi-core CPU baseline) is
-    bit-identical to the sequential restatement on the reference's 9 x 4 tiling."""
+    DO_OCEANIC_PHYS over the tiles in parallel, the CG2D's tile loops and every halo exchange
+    too; bench.py's multi-core CPU baseline) is bit-identical to the sequential restatement:
+    config 2 on the reference's 9 x 4 tiling and on 3 x 2, config 3 on its 6 faces (exch2)."""
     import numpy as np
     from oracle import harness
-    from oracle.harness import ocean90_oracle
+    from oracle.harness import cs32x15_oracle, ocean90_oracle
     out = {}
     for omp in (False, True):
         harness.USE_OMP = omp
         try:
-            o, _ = ocean90_oracle(nSx=9, nSy=4)
+            if case == "cs32x15":
+                o, _ = cs32x15_oracle()
+            else:
+                o, _ = ocean90_oracle(nSx=int(case[-3]), nSy=int(case[-1]))
         finally:
             harness.USE_OMP = False
         if omp:
@@ -80,5 +85,6 @@ def test_openmp_oracle_bit_identical():
             o.forward_step()
         out[omp] = {n: np.array(o.arr(n)).copy() for n in ("uVel", "vVel", "wVel", "theta", "salt", "etaN")}
         out[omp]["iters"] = o.get("numIters")
+        out[omp]["res"] = (o.get("firstResidual"), o.get("lastResidual"))
     for n in out[False]:
         assert np.array_equal(out[False][n], out[True][n]), n
