@@ -1967,7 +1967,7 @@ __device__ __forceinline__ double vi_h0S_own(const VIM2<BX, BY, P, OWN, HR> &a, 
   do {              \
   } while (0)
 #endif
-template <int BX, int BY, unsigned C, bool PF, bool CREG, bool EARLY, int LBW>
+template <int BX, int BY, unsigned C, bool PF, bool CREG, bool EARLY, int LBW, bool SPLIT>
 __global__ void __launch_bounds__(VT_NT, LBW) k_mom_vi_m2(Dims d, VIP<C> p, Fields f, const int *iterPtr, int nbx, int nby,
                                                       int KC, int nkc) {
   using P = VIP<C>;
@@ -2173,60 +2173,64 @@ __global__ void __launch_bounds__(VT_NT, LBW) k_mom_vi_m2(Dims d, VIP<C> p, Fiel
       auto q3of = [&](long qq2, int kk) { return qq2 + (long)(kk - 1) * d.n2 + t3; };
       const long q3 = q3of(q2, k);
       const double recip_drF = a.rdrFk;
-      double gU = 0.0, gV = 0.0, guDiss = 0.0, gvDiss = 0.0, dPhiHydX = 0.0, dPhiHydY = 0.0;
-      {  // CALC_GRAD_PHI_HYD (calc_grad_phi_hyd.F:152-214), as k_mom_step
-        constexpr bool rsc = rstar && P::select_rStar >= 2 && P::nonlinFreeSurf >= 4;
-        auto varLoc = [&](long qq2) {
-          if constexpr (rsc) return AR3(phiHydC, q3of(qq2, k)) * AR2(rStarFacC, qq2) + 0.0;
-          else return AR3(phiHydC, q3of(qq2, k)) + 0.0;
-        };
-        if constexpr (EARLY && !rsc) {
-          const double vl = ePhi0 + 0.0;
-          if (i >= 1) dPhiHydX = c.recip_dxC * (vl - (ePhiX + 0.0));
-          if (j >= 1) dPhiHydY = c.recip_dyC * (vl - (ePhiY + 0.0));
-        } else {
-          const double vl = varLoc(q2);
-          if (i >= 1) dPhiHydX = c.recip_dxC * (vl - varLoc(q2 - 1));
-          if (j >= 1) dPhiHydY = c.recip_dyC * (vl - varLoc(q2 - d.nx));
+      // one component at a time (CC 1: U, 2: V): tendency, AB2, store, each from its own
+      // vecinv_tend call whose other outputs are dead (the compiler drops their arithmetic;
+      // the common reads are shared).  SPLIT: a scheduling barrier between the two, so the
+      // halves' live values do not overlap (215 against 247 VGPRs at 2 waves per SIMD)
+      auto comp = [&](auto tagC) {
+        constexpr int CC = decltype(tagC)::value;   // 1: U, 2: V
+        double gU = 0.0, gV = 0.0, guDiss = 0.0, gvDiss = 0.0, dPhiHydX = 0.0, dPhiHydY = 0.0;
+        {  // CALC_GRAD_PHI_HYD (calc_grad_phi_hyd.F:152-214), as k_mom_step
+          constexpr bool rsc = rstar && P::select_rStar >= 2 && P::nonlinFreeSurf >= 4;
+          auto varLoc = [&](long qq2) {
+            if constexpr (rsc) return AR3(phiHydC, q3of(qq2, k)) * AR2(rStarFacC, qq2) + 0.0;
+            else return AR3(phiHydC, q3of(qq2, k)) + 0.0;
+          };
+          if constexpr (EARLY && !rsc) {
+            const double vl = ePhi0 + 0.0;
+            if (CC == 1 && i >= 1) dPhiHydX = c.recip_dxC * (vl - (ePhiX + 0.0));
+            if (CC == 2 && j >= 1) dPhiHydY = c.recip_dyC * (vl - (ePhiY + 0.0));
+          } else {
+            const double vl = varLoc(q2);
+            if (CC == 1 && i >= 1) dPhiHydX = c.recip_dxC * (vl - varLoc(q2 - 1));
+            if (CC == 2 && j >= 1) dPhiHydY = c.recip_dyC * (vl - varLoc(q2 - d.nx));
+          }
+          if constexpr (rstar && P::select_rStar >= 2) {
+            const double factorP = p.gravity * (1.0 / p.rhoConst) * 0.5, rCk = f.rC[k - 1];
+            auto vl2 = [&](long qq2) { return AR2(etaH, qq2) * (1.0 + rCk * AR2(recip_Rcol, qq2)); };
+            const double e0 = vl2(q2), a0 = AR3(alphaRho, q3);
+            if (CC == 1 && i >= 1) dPhiHydX = dPhiHydX + factorP * (AR3(alphaRho, q3 - 1) + a0) * (e0 - vl2(q2 - 1)) * c.recip_dxC;
+            if (CC == 2 && j >= 1) dPhiHydY = dPhiHydY + factorP * (AR3(alphaRho, q3 - d.nx) + a0) * (e0 - vl2(q2 - d.nx)) * c.recip_dyC;
+          }
         }
-        if constexpr (rstar && P::select_rStar >= 2) {
-          const double factorP = p.gravity * (1.0 / p.rhoConst) * 0.5, rCk = f.rC[k - 1];
-          auto vl2 = [&](long qq2) { return AR2(etaH, qq2) * (1.0 + rCk * AR2(recip_Rcol, qq2)); };
-          const double e0 = vl2(q2), a0 = AR3(alphaRho, q3);
-          if (i >= 1) dPhiHydX = dPhiHydX + factorP * (AR3(alphaRho, q3 - 1) + a0) * (e0 - vl2(q2 - 1)) * c.recip_dxC;
-          if (j >= 1) dPhiHydY = dPhiHydY + factorP * (AR3(alphaRho, q3 - d.nx) + a0) * (e0 - vl2(q2 - d.nx)) * c.recip_dyC;
+        vecinv_tend(a, d, p, f, i, j, k, t, gU, gV, guDiss, gvDiss);
+        double guExt = 0.0, gvExt = 0.0;
+        if (P::momForcing && k == 1) {
+          if (CC == 1 && j >= 0 && j <= d.sNy + 1 && i >= 1 && i <= d.sNx + 1)
+            guExt = guExt + p.foFacMom * (AR2(fu, q2) * mass2rUnit) * recip_drF * a.recip_hFacW(i, j, k);
+          if (CC == 2 && j >= 1 && j <= d.sNy + 1 && i >= 0 && i <= d.sNx + 1)
+            gvExt = gvExt + p.foFacMom * (AR2(fv, q2) * mass2rUnit) * recip_drF * a.recip_hFacS(i, j, k);
         }
-      }
-      vecinv_tend(a, d, p, f, i, j, k, t, gU, gV, guDiss, gvDiss);
-      double guExt = 0.0, gvExt = 0.0;
-      if (P::momForcing && k == 1) {
-        if (j >= 0 && j <= d.sNy + 1 && i >= 1 && i <= d.sNx + 1)
-          guExt = guExt + p.foFacMom * (AR2(fu, q2) * mass2rUnit) * recip_drF * a.recip_hFacW(i, j, k);
-        if (j >= 1 && j <= d.sNy + 1 && i >= 0 && i <= d.sNx + 1)
-          gvExt = gvExt + p.foFacMom * (AR2(fv, q2) * mass2rUnit) * recip_drF * a.recip_hFacS(i, j, k);
-      }
-      gU = gU - p.pfFacMom * dPhiHydX;
-      gV = gV - p.pfFacMom * dPhiHydY;
-      if (P::momViscosity && P::momDissip_In_AB) { gU = gU + guDiss; gV = gV + gvDiss; }
-      if (P::momForcing && P::momForcingOutAB != 1) { gU = gU + guExt; gV = gV + gvExt; }
-      {  // ADAMS_BASHFORTH2 (adams_bashforth2.F:81-88)
-        const double gUo = EARLY ? eGuo : AR3(guNm1, q3), gVo = EARLY ? eGvo : AR3(gvNm1, q3);
-        double ab = abFac * (gU - gUo);
-        AR3(guNm1, q3) = gU;
-        gU = gU + ab;
-        ab = abFac * (gV - gVo);
-        AR3(gvNm1, q3) = gV;
-        gV = gV + ab;
-      }
-      double gUtmp = gU, gVtmp = gV;
-      if (P::momForcing && P::momForcingOutAB == 1) { gUtmp = gUtmp + guExt; gVtmp = gVtmp + gvExt; }
-      if (P::momViscosity && !P::momDissip_In_AB) { gUtmp = gUtmp + guDiss; gVtmp = gVtmp + gvDiss; }
-      if constexpr (rstar && P::nonlinFreeSurf > 1) {
-        gUtmp = gUtmp / AR2(rStarExpW, q2);
-        gVtmp = gVtmp / AR2(rStarExpS, q2);
-      }
-      AR3(gU, q3) = a.uVel(i, j, k) + p.deltaTMom * (gUtmp + 0.0) * a.maskW(i, j, k);
-      AR3(gV, q3) = a.vVel(i, j, k) + p.deltaTMom * (gVtmp + 0.0) * a.maskS(i, j, k);
+        double g = CC == 1 ? gU - p.pfFacMom * dPhiHydX : gV - p.pfFacMom * dPhiHydY;
+        const double gDiss = CC == 1 ? guDiss : gvDiss, gExt = CC == 1 ? guExt : gvExt;
+        if (P::momViscosity && P::momDissip_In_AB) g = g + gDiss;
+        if (P::momForcing && P::momForcingOutAB != 1) g = g + gExt;
+        {  // ADAMS_BASHFORTH2 (adams_bashforth2.F:81-88)
+          const double go = CC == 1 ? (EARLY ? eGuo : AR3(guNm1, q3)) : (EARLY ? eGvo : AR3(gvNm1, q3));
+          const double ab = abFac * (g - go);
+          if (CC == 1) AR3(guNm1, q3) = g; else AR3(gvNm1, q3) = g;
+          g = g + ab;
+        }
+        double gtmp = g;
+        if (P::momForcing && P::momForcingOutAB == 1) gtmp = gtmp + gExt;
+        if (P::momViscosity && !P::momDissip_In_AB) gtmp = gtmp + gDiss;
+        if constexpr (rstar && P::nonlinFreeSurf > 1) gtmp = gtmp / (CC == 1 ? AR2(rStarExpW, q2) : AR2(rStarExpS, q2));
+        if (CC == 1) AR3(gU, q3) = a.uVel(i, j, k) + p.deltaTMom * (gtmp + 0.0) * a.maskW(i, j, k);
+        else AR3(gV, q3) = a.vVel(i, j, k) + p.deltaTMom * (gtmp + 0.0) * a.maskS(i, j, k);
+      };
+      comp(std::integral_constant<int, 1>{});
+      if constexpr (SPLIT) __builtin_amdgcn_sched_barrier(0);   // U's chain before V's
+      comp(std::integral_constant<int, 2>{});
     }
     VI_STAMP(3);
     }(iL, jL, q2L);
@@ -2304,7 +2308,8 @@ constexpr unsigned VI_CODE_LLC = vi_code(1, 0, 0, 1, 1, 1, 0, 1, 1, 0, 1, 1, 1, 
 template <int BX, int BY, unsigned C, int V>
 static void vi_m2_one(const Dims &d, const VIP<C> &vp, const Fields &f, const int *iterPtr, int nbx, int nby, int KC,
                       int nkc, hipStream_t s) {
-  hipLaunchKernelGGL((k_mom_vi_m2<BX, BY, C, (V & 1) != 0, (V & 2) != 0, (V & 4) != 0, (V & 8) ? 2 : 1>),
+  hipLaunchKernelGGL((k_mom_vi_m2<BX, BY, C, (V & 1) != 0, (V & 2) != 0, (V & 4) != 0, (V & 32) ? 3 : (V & 8) ? 2 : 1,
+                                   (V & 16) != 0>),
                      dim3((unsigned)(nbx * nby * d.nT * nkc)), dim3(VT_NT), 0, s, d, vp, f, iterPtr, nbx, nby, KC, nkc);
 }
 // k_mom_vi_m2 as launched: the output point's metrics held in registers across the march
@@ -2319,12 +2324,20 @@ static void vi_m2_one(const Dims &d, const VIP<C> &vp, const Fields &f, const in
 static bool vi_m2_launch(const Dims &d, const Params &p, const Fields &f, const int *iterPtr, int BX, int BY, int nbx,
                          int nby, int KC, int nkc, hipStream_t s) {
   const unsigned code = vi_opt_code(p);
+  // MGCM_VI_SPLIT (A/B): 0 both components' chains interleaved, 1 U then V (2 waves per SIMD),
+  // 3 U then V with registers capped for 3 waves per SIMD
+  const char *se = getenv("MGCM_VI_SPLIT");
+  const int split = se ? atoi(se) : 0;
   if (code == VI_CODE_LLC && BX == 31 && BY == 8) {
-    vi_m2_one<31, 8, VI_CODE_LLC, 14>(d, vi_params<VI_CODE_LLC>(p), f, iterPtr, nbx, nby, KC, nkc, s);
+    if (split == 3) vi_m2_one<31, 8, VI_CODE_LLC, 2 | 4 | 16 | 32>(d, vi_params<VI_CODE_LLC>(p), f, iterPtr, nbx, nby, KC, nkc, s);
+    else if (split == 1) vi_m2_one<31, 8, VI_CODE_LLC, 14 | 16>(d, vi_params<VI_CODE_LLC>(p), f, iterPtr, nbx, nby, KC, nkc, s);
+    else vi_m2_one<31, 8, VI_CODE_LLC, 14>(d, vi_params<VI_CODE_LLC>(p), f, iterPtr, nbx, nby, KC, nkc, s);
     return true;
   }
   if (code == VI_CODE_LLC && BX == 32 && BY == 8) {
-    vi_m2_one<32, 8, VI_CODE_LLC, 14>(d, vi_params<VI_CODE_LLC>(p), f, iterPtr, nbx, nby, KC, nkc, s);
+    if (split == 3) vi_m2_one<32, 8, VI_CODE_LLC, 2 | 4 | 16 | 32>(d, vi_params<VI_CODE_LLC>(p), f, iterPtr, nbx, nby, KC, nkc, s);
+    else if (split == 1) vi_m2_one<32, 8, VI_CODE_LLC, 14 | 16>(d, vi_params<VI_CODE_LLC>(p), f, iterPtr, nbx, nby, KC, nkc, s);
+    else vi_m2_one<32, 8, VI_CODE_LLC, 14>(d, vi_params<VI_CODE_LLC>(p), f, iterPtr, nbx, nby, KC, nkc, s);
     return true;
   }
   return false;
