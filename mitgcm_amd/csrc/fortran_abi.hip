@@ -149,6 +149,15 @@ struct FortranSide {
     std::vector<int> pre, post;   // every model's tracer parity before / after the captured step
   } mg[4];
   bool capturing = false;     // set_iter inside a capture: device increments, not values
+  // Events recorded inside a multi-model capture: with the pool on (the default), every
+  // record of a captured step takes an event of its own from evPool (filled before the
+  // capture, kept for the graphs' life), so no hipEvent_t is recorded twice in one graph
+  struct EvPool {
+    int dev = 0;
+    std::vector<hipEvent_t> ev;
+    size_t next = 0;
+  };
+  std::vector<EvPool> evPools;
   bool multiGraphOff = false; // a capture failed: the multi-model steps stay eager
   long nUp = 0, nDown = 0;   // copies of whole bound arrays, for mgcm_amd_transfer_stats_
   // the state arrays' host pages, registered with HIP once the time loop begins (downloads
@@ -204,6 +213,38 @@ void hipchk(hipError_t e, const char *where) {
   if (e != hipSuccess) die(where, hipGetErrorString(e));
 }
 hipStream_t stream_of(const Shard &s) { return (hipStream_t)mgcm_get_stream(s.m); }
+
+bool cap_pool_on() {
+  static const bool off = getenv("MGCM_AMD_CAPTURE_POOL") && atoi(getenv("MGCM_AMD_CAPTURE_POOL")) == 0;
+  return !off;
+}
+// the event a record on device `dev` uses: outside a capture (or with the pool off) the
+// caller's own; inside one, a fresh event of that device's pool
+hipEvent_t rec_event(int dev, hipEvent_t own, const char *where) {
+  if (!g.capturing || !cap_pool_on()) return own;
+  for (auto &p : g.evPools)
+    if (p.dev == dev) {
+      if (p.next >= p.ev.size()) die(where, "capture event pool exhausted");
+      return p.ev[p.next++];
+    }
+  die(where, "no capture event pool for the device");
+}
+// before a capture: every device's pool holds at least `per` events not yet handed out
+void fill_pools(int per, const char *where) {
+  for (auto &s : g.sh) {
+    bool have = false;
+    for (auto &p : g.evPools) have = have || p.dev == s.dev;
+    if (!have) g.evPools.push_back(FortranSide::EvPool{s.dev, {}, 0});
+  }
+  for (auto &p : g.evPools) {
+    hipchk(hipSetDevice(p.dev), where);
+    while (p.ev.size() < p.next + (size_t)per) {
+      hipEvent_t e;
+      hipchk(hipEventCreateWithFlags(&e, hipEventDisableTiming), where);
+      p.ev.push_back(e);
+    }
+  }
+}
 bool multi() { return g.sh.size() > 1; }
 long n2() { return (long)(g.dims[0] + 2 * g.dims[2]) * (g.dims[1] + 2 * g.dims[3]); }
 long nTiles() { return (long)g.dims[5] * g.dims[6]; }
@@ -226,14 +267,17 @@ void phase_all(const char *where, int phase) {
 // model has issued so far (no host synchronisation).
 void barrier_all(const char *where) {
   if (!multi()) return;
-  for (auto &s : g.sh) {
+  std::vector<hipEvent_t> ev(g.sh.size());
+  for (size_t i = 0; i < g.sh.size(); i++) {
+    const Shard &s = g.sh[i];
     hipchk(hipSetDevice(s.dev), where);
-    hipchk(hipEventRecord(s.ev, stream_of(s)), where);
+    ev[i] = rec_event(s.dev, s.ev, where);
+    hipchk(hipEventRecord(ev[i], stream_of(s)), where);
   }
-  for (auto &a : g.sh) {
-    hipchk(hipSetDevice(a.dev), where);
-    for (auto &b : g.sh)
-      if (&a != &b) hipchk(hipStreamWaitEvent(stream_of(a), b.ev, 0), where);
+  for (size_t i = 0; i < g.sh.size(); i++) {
+    hipchk(hipSetDevice(g.sh[i].dev), where);
+    for (size_t j = 0; j < g.sh.size(); j++)
+      if (i != j) hipchk(hipStreamWaitEvent(stream_of(g.sh[i]), ev[j], 0), where);
   }
 }
 
@@ -278,9 +322,10 @@ void xfer3d(const char *where, int group) {
     hipchk(hipMemcpyAsync(L.rbuf, L.sbuf, (size_t)nf * Nr * L.n * sizeof(double), hipMemcpyDeviceToDevice,
                           stream_of(a)),
            where);
-    hipchk(hipEventRecord(L.ev, stream_of(a)), where);
+    const hipEvent_t le = rec_event(a.dev, L.ev, where);
+    hipchk(hipEventRecord(le, stream_of(a)), where);
     hipchk(hipSetDevice(b.dev), where);
-    hipchk(hipStreamWaitEvent(stream_of(b), L.ev, 0), where);
+    hipchk(hipStreamWaitEvent(stream_of(b), le, 0), where);
     if (mgcm_halo_pack_group(b.m, group, L.idxD, L.n, L.rbuf, 1)) die(where);
   }
 }
@@ -631,6 +676,11 @@ void free_links() {
 }
 void free_shards() {
   free_links();
+  for (auto &p : g.evPools) {
+    (void)hipSetDevice(p.dev);
+    for (auto e : p.ev) (void)hipEventDestroy(e);
+  }
+  g.evPools.clear();
   for (auto &s : g.sh) {
     if (s.ev) { (void)hipSetDevice(s.dev); (void)hipEventDestroy(s.ev); }
     if (s.m) mgcm_destroy(s.m);
@@ -709,19 +759,22 @@ void run_recorded_step(const char *w, int myIter) {
 // model 0's stream waits for every other model's work so far (join), or every other model's
 // stream for model 0's (fork)
 void join_into_0(const char *w) {
+  std::vector<hipEvent_t> ev(g.sh.size());
   for (size_t i = 1; i < g.sh.size(); i++) {
     hipchk(hipSetDevice(g.sh[i].dev), w);
-    hipchk(hipEventRecord(g.sh[i].ev, stream_of(g.sh[i])), w);
+    ev[i] = rec_event(g.sh[i].dev, g.sh[i].ev, w);
+    hipchk(hipEventRecord(ev[i], stream_of(g.sh[i])), w);
   }
   hipchk(hipSetDevice(g.sh[0].dev), w);
-  for (size_t i = 1; i < g.sh.size(); i++) hipchk(hipStreamWaitEvent(stream_of(g.sh[0]), g.sh[i].ev, 0), w);
+  for (size_t i = 1; i < g.sh.size(); i++) hipchk(hipStreamWaitEvent(stream_of(g.sh[0]), ev[i], 0), w);
 }
 void fork_from_0(const char *w) {
   hipchk(hipSetDevice(g.sh[0].dev), w);
-  hipchk(hipEventRecord(g.sh[0].ev, stream_of(g.sh[0])), w);
+  const hipEvent_t e0 = rec_event(g.sh[0].dev, g.sh[0].ev, w);
+  hipchk(hipEventRecord(e0, stream_of(g.sh[0])), w);
   for (size_t i = 1; i < g.sh.size(); i++) {
     hipchk(hipSetDevice(g.sh[i].dev), w);
-    hipchk(hipStreamWaitEvent(stream_of(g.sh[i]), g.sh[0].ev, 0), w);
+    hipchk(hipStreamWaitEvent(stream_of(g.sh[i]), e0, 0), w);
   }
 }
 
@@ -742,6 +795,12 @@ bool multi_replay(const char *w, int myIter) {
   if (!G.exec) {
     G.pre = pre;
     hipStream_t s0 = stream_of(g.sh[0]);
+    // MGCM_AMD_CAPTURE=multi: every model keeps its own stream in the capture (the graph then
+    // has a branch per model, joined at the exchange points); default: one stream
+    static const bool multiStream = getenv("MGCM_AMD_CAPTURE") && !strcmp(getenv("MGCM_AMD_CAPTURE"), "multi");
+    static const hipStreamCaptureMode mode = getenv("MGCM_AMD_CAPTURE_MODE") &&
+        !strcmp(getenv("MGCM_AMD_CAPTURE_MODE"), "relaxed") ? hipStreamCaptureModeRelaxed : hipStreamCaptureModeGlobal;
+    fill_pools(4096, w);
     // every model issues on model 0's stream while capturing: the graph is one chain of the
     // models' work in the recorded order (graphs captured across two or more streams of one GPU
     // faulted in the HIP runtime's own threads -- SIGSEGV, no host frame -- once 4 or more models
@@ -749,21 +808,22 @@ bool multi_replay(const char *w, int myIter) {
     // all-to-all barriers; with 2 or 3 models they replayed correctly but no faster than the
     // one-stream graph: 0.60 against 0.58 ms/step at 2 models, 0.74-0.88 against 0.83 at 3,
     // profiles/r05/capture_ab/)
-    for (size_t i = 1; i < g.sh.size(); i++)
-      if (mgcm_set_stream(g.sh[i].m, s0)) die(w);
+    if (!multiStream)
+      for (size_t i = 1; i < g.sh.size(); i++)
+        if (mgcm_set_stream(g.sh[i].m, s0)) die(w);
     hipchk(hipSetDevice(g.sh[0].dev), w);
-    if (hipStreamBeginCapture(s0, hipStreamCaptureModeGlobal) != hipSuccess) {
+    if (hipStreamBeginCapture(s0, mode) != hipSuccess) {
       (void)hipGetLastError();
       for (size_t i = 1; i < g.sh.size(); i++)
         if (mgcm_set_stream(g.sh[i].m, nullptr)) die(w);
       return false;
     }
+    g.capturing = true;   // (the pool's events from here: the fork's record is the capture's first node)
     fork_from_0(w);
-    g.capturing = true;
     g.devIter = myIter;   // the graph's increments are relative to this
     run_recorded_step(w, myIter);
-    g.capturing = false;
     join_into_0(w);
+    g.capturing = false;
     hipGraph_t gr = nullptr;
     hipchk(hipSetDevice(g.sh[0].dev), w);
     hipError_t e = hipStreamEndCapture(s0, &gr);

@@ -811,6 +811,7 @@ __device__ __forceinline__ double block_max_nw(double v, double *red, int slot) 
 }
 
 #ifdef MGCM_CG_STAMPS   // diagnostic build only: per-phase shader-cycle totals of one solve
+#define CG_NSTAMP 12
 #define CG_STAMP(k)                                                                   \
   do {                                                                                \
     __builtin_amdgcn_sched_barrier(0);                                                \
@@ -1099,8 +1100,9 @@ __global__ void __launch_bounds__(NT) k_cg2d_bxy(Dims d, Params p, Fields f, con
       for (int a = 0; a < BX; a++) e = FMA ? __builtin_fma(q[b][a], r[b][a], e) : e + q[b][a] * r[b][a];
     double eta_qrN = block_sum_nw<NW>(e, red, 0);
 #ifdef MGCM_CG_STAMPS
-    unsigned long long stampAcc[6] = {0, 0, 0, 0, 0, 0}, stampPrev = 0;
+    unsigned long long stampAcc[CG_NSTAMP] = {0};
     const unsigned long long stampT0 = __builtin_amdgcn_s_memtime(), stampR0 = __builtin_amdgcn_s_memrealtime();
+    unsigned long long stampPrev = stampT0;
     __builtin_amdgcn_s_waitcnt(0xC07F);
 #endif
     // the standard iteration, unrolled by two: the loop-carried s and q then need no register
@@ -1115,7 +1117,7 @@ __global__ void __launch_bounds__(NT) k_cg2d_bxy(Dims d, Params p, Fields f, con
           sv[b][a] = FMA ? __builtin_fma(cgBeta, sv[b][a], q[b][a]) : q[b][a] + cgBeta * sv[b][a];
           s_l[cs[b][a]] = sv[b][a];
         }
-      CG_STAMP(0);
+      CG_STAMP(12);
       __syncthreads();
       CG_STAMP(1);
       apply(s_l, sv, q, false);
@@ -1126,7 +1128,19 @@ __global__ void __launch_bounds__(NT) k_cg2d_bxy(Dims d, Params p, Fields f, con
         for (int a = 0; a < BX; a++) aa = FMA ? __builtin_fma(sv[b][a], q[b][a], aa) : aa + sv[b][a] * q[b][a];
       aslot = aslot ^ 1;
       CG_STAMP(2);
+#ifdef MGCM_CG_STAMPS
+      double alpha;
+      {   // block_sum_nw, stamped: wave tree | LDS store + barrier | slot tree
+        double v = wave_tree63(aa);
+        CG_STAMP(6);
+        if ((tid & 63) == 63) red[aslot * 16 + (tid >> 6)] = v;
+        __syncthreads();
+        CG_STAMP(7);
+        alpha = slot_tree<NW>(red + aslot * 16);
+      }
+#else
       double alpha = block_sum_nw<NW>(aa, red, aslot);
+#endif
       CG_STAMP(3);
       alpha = eta_qrN / alpha;
       double e2 = 0.0;
@@ -1142,6 +1156,7 @@ __global__ void __launch_bounds__(NT) k_cg2d_bxy(Dims d, Params p, Fields f, con
       actualIts = it2d;
       CG_STAMP(4);
       __syncthreads();
+      CG_STAMP(8);
       // next iteration's q = M r and (q, r), reduced together with this iteration's r.r
       apply(r_l, r, q, true);
       double en = 0.0;
@@ -1149,6 +1164,7 @@ __global__ void __launch_bounds__(NT) k_cg2d_bxy(Dims d, Params p, Fields f, con
       for (int b = 0; b < BY; b++)
 #pragma unroll
         for (int a = 0; a < BX; a++) en = FMA ? __builtin_fma(q[b][a], r[b][a], en) : en + q[b][a] * r[b][a];
+      CG_STAMP(9);
       block_sum2_nw<NW>(e2, en, red, 0);
       CG_STAMP(5);
       err_sq = e2;
@@ -1172,9 +1188,11 @@ __global__ void __launch_bounds__(NT) k_cg2d_bxy(Dims d, Params p, Fields f, con
     }
 #ifdef MGCM_CG_STAMPS
     if (tid == 0)
-      printf("CGSTAMP its %d total %llu real100MHz %llu | barS %llu applyA %llu sumA %llu div+upd %llu barR+applyM+sum2 %llu\n",
+      printf("CGSTAMP its %d total %llu real100MHz %llu | beta+s+store %llu barS %llu applyA+dot %llu sumA(slot tree) %llu "
+             "div+upd+store %llu sum2 %llu sumA.wave %llu sumA.bar %llu barR %llu applyM+dot %llu\n",
              actualIts, __builtin_amdgcn_s_memtime() - stampT0, __builtin_amdgcn_s_memrealtime() - stampR0,
-             stampAcc[0], stampAcc[1], stampAcc[2], stampAcc[3], stampAcc[4]);
+             stampAcc[11], stampAcc[0], stampAcc[1], stampAcc[2], stampAcc[3], stampAcc[4], stampAcc[5], stampAcc[6],
+             stampAcc[7], stampAcc[8]);
 #endif
   }
   if (MINRES && nIterMin >= 0 && err_sq > minResidualSq) {
@@ -1980,11 +1998,15 @@ int cg2d_bxy_geometry(int v, int *bx, int *by, int *nt) {
   *bx = CGX[v].bx; *by = CGX[v].by; *nt = CGX[v].nt;
   return 0;
 }
-// k_cg2d_hr replaces k_cg2d_bxy for the standard solver (no CG2D_SR, no minimum-residual
-// solution) in the 2 x 4 x 512 geometry; MGCM_CG2D_HR=0 keeps k_cg2d_bxy (A/B, tests)
+// k_cg2d_hr in place of k_cg2d_bxy (MGCM_CG2D_HR=1, opt-in) for the standard solver (no
+// CG2D_SR, no minimum-residual solution) in the 2 x 4 x 512 geometry.  Measured slower on
+// config 2 (round 6: 1.705 against 1.64 us/iteration, profiles/r06/ab_hr/): the barriers it
+// removes cost less than the halo copies' LDS reads, the centre coefficients read from LDS
+// and the 20-26 VGPRs it spills -- the iteration is bound by its two reductions' latency
+// chains and the f64 VALU, not by the halo barriers
 bool cg2d_hr_on(int BX, int BY, int NT, bool sr, bool mr) {
   const char *e = getenv("MGCM_CG2D_HR");
-  if (e && atoi(e) == 0) return false;
+  if (!e || atoi(e) == 0) return false;
   return BX == 2 && BY == 4 && NT == 512 && !sr && !mr;
 }
 template <int BX, int BY, int NT>

@@ -197,7 +197,7 @@ class Model:
 
     def cg2d_kernel(self):
         """Which CG2D kernel mgcm_init selected: 'mwg' (multi-workgroup), 'hr' (k_cg2d_bxy's 2 x 4 blocks with
-        two barriers per iteration), 'bxy' (BX x BY points/thread),
+        two barriers per iteration, opt-in MGCM_CG2D_HR=1), 'bxy' (BX x BY points/thread),
         'blk2' (2x2), 'block', or 'block_ref' (k_cg2d_block summing in the reference's order,
         cg2dRefOrder)."""
         k = lib().mgcm_get_param(self.h, b"cg2dKernel")

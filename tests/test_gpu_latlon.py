@@ -104,8 +104,8 @@ def test_latlon_20_steps_vs_reference_output(golden_dir):
 
 @pytest.mark.parametrize("hr", ["1", "0"])
 def test_cg2d_bxy_vs_oracle(hr, monkeypatch):
-    """The 2x4-points-per-thread solvers chosen for the 90x40 grid -- k_cg2d_hr (two barriers
-    per iteration, the default) and k_cg2d_bxy (MGCM_CG2D_HR=0) -- on the lat-lon operator:
+    """The 2x4-points-per-thread solvers for the 90x40 grid -- k_cg2d_bxy (the default) and
+    k_cg2d_hr (two barriers per iteration, MGCM_CG2D_HR=1) -- on the lat-lon operator:
     same iteration count, first residual within 1e-12 relative, solution within 1e-12 of
     max|x|."""
     from mitgcm_amd import configs

@@ -439,3 +439,40 @@ def test_refhost_llc30_exch2_bitexact(models, eager, tmp_path):
     assert not bad, bad
     assert len([n for n in CHECK if n in out]) >= 18
     assert st["downloads"] == 2 * len(state), (st, len(state))
+
+
+# The multi-model step captured across the models' own streams (MGCM_AMD_CAPTURE=multi: one
+# graph branch per model, joined at every exchange point) instead of on one stream.  Round 5
+# saw this form die with SIGSEGV inside the HIP runtime's threads at >= 4 models; each record
+# of a captured step now takes an event of its own from a pool filled before the capture
+# (fortran_abi.hip rec_event), where before every fork, join and barrier point re-recorded
+# the models' single events.  Bit-identical to the one-stream graph at 4 and 6 models.
+@pytest.mark.parametrize("layout,models", [("ref", 4), ("cs32_6t", 6), ("cs32", 4)])
+def test_refhost_multistream_capture(layout, models, tmp_path):
+    from mitgcm_amd import configs
+    exe = os.path.join(RH, "refhost_" + layout)
+    assert os.path.exists(exe), "refhost not built (mitgcm_amd/fortran/build_refhost.py, __graft_entry__.build())"
+    nsteps = 4
+    if layout == "ref":
+        m = configs.make_model(lambda: configs.global_ocean_90x40x15(nSx=9, nSy=4))
+        state = _write_blob(tmp_path / "refhost_in.bin", m, nsteps, monitor_days=2, packages_off=True)
+        pdir = PARAM_DIR
+    else:
+        m = configs.make_model(lambda: configs.global_ocean_cs32x15(sNy=16 if layout == "cs32" else 32))
+        pdir = _cs32_namelists(str(tmp_path / "input"))
+        w2 = m.g.topo.w2_arrays(ldNb=8, ldT=2 * m.g.nTiles)
+        state = _write_blob(tmp_path / "refhost_in.bin", m, nsteps, monitor_days=2, w2=w2, undef=("ALLOW_CD_CODE",))
+    m.close()
+    outs, times = {}, {}
+    for mode in ("one", "multi"):
+        env = dict(os.environ, MGCM_AMD_MODELS=str(models), MGCM_AMD_EAGER="0", MGCM_CG2D_MWG="0")
+        if mode == "multi":
+            env["MGCM_AMD_CAPTURE"] = "multi"
+        r = subprocess.run([exe, str(tmp_path), pdir], capture_output=True, text=True, timeout=300, env=env)
+        assert r.returncode == 0, (mode, r.returncode, r.stdout + r.stderr)
+        outs[mode], st = _read_out(tmp_path / "refhost_out.bin", state, nsteps)
+        times[mode] = st["step_ms"]
+    bad = [n for n in outs["one"] if not np.array_equal(outs["one"][n], outs["multi"][n])]
+    print("refhost %s models=%d step ms one-stream %s multi-stream %s" % (layout, models, times["one"], times["multi"]))
+    assert not bad, bad
+    assert len(outs["one"]) >= 18
