@@ -95,6 +95,7 @@ struct Readers {
 struct Shard {
   mgcm_model *m = nullptr;
   int dev = 0, t0 = 0, nT = 0;
+  int gpu = 0;   // the GPU the model stands for (== dev, except under MGCM_AMD_VIRTUAL_GPUS)
   hipEvent_t ev = nullptr;   // cross-model barriers
 };
 // The halo sources model s's tiles deliver to model d (sorted 2-D offsets, the same on both
@@ -355,7 +356,7 @@ void op_solve(const char *w) {
       hipchk(hipSetDevice(L.dev), w);
       if (mgcm_step_phase(L.m, 12)) die(w);
       for (size_t j = 0; j < g.sh.size(); j++) {
-        if ((int)j == c.shard || g.sh[j].dev != L.dev) continue;
+        if ((int)j == c.shard || g.sh[j].gpu != L.gpu) continue;
         for (const char *nm : {"cg2d_x", "etaN"}) {
           const double *src = mgcm_device_ptr(L.m, nm);
           double *dst = mgcm_device_ptr(g.sh[j].m, nm);
@@ -604,12 +605,12 @@ void setup_shards(const char *where) {
   g.cgDevice = mgcm_get_param(g.m, "cg2dKernel") == 4.0;
   g.cgLeads.clear();
   for (int i = 0; i < N; i++) {
-    if (!g.cgLeads.empty() && g.sh[g.cgLeads.back().shard].dev == g.sh[i].dev) {
+    if (!g.cgLeads.empty() && g.sh[g.cgLeads.back().shard].gpu == g.sh[i].gpu) {
       g.cgLeads.back().nT += g.sh[i].nT;
       continue;
     }
     for (auto &c : g.cgLeads)
-      if (g.sh[c.shard].dev == g.sh[i].dev) die(where, "the models of one GPU must own contiguous tiles (MGCM_AMD_DEVICES)");
+      if (g.sh[c.shard].gpu == g.sh[i].gpu) die(where, "the models of one GPU must own contiguous tiles (MGCM_AMD_DEVICES)");
     g.cgLeads.push_back(CgLead{i, g.sh[i].t0, g.sh[i].nT});
   }
   if (g.cgDevice && g.cgLeads.size() > 1)
@@ -729,7 +730,7 @@ bool fuse_allowed() {
   if (e && atoi(e) == 1) return false;
   if (!multi()) return true;
   for (auto &s : g.sh)
-    if (s.dev != g.sh[0].dev) return false;
+    if (s.gpu != g.sh[0].gpu) return false;
   return !g.multiGraphOff;
 }
 
@@ -925,12 +926,21 @@ void mgcm_amd_setup_(const int *sNx, const int *sNy, const int *OLx, const int *
       const size_t c = l.find(',', pos);
       devs[i] = atoi(l.substr(pos, c == std::string::npos ? std::string::npos : c - pos).c_str());
       pos = c == std::string::npos ? l.size() + 1 : c + 1;
-      if (devs[i] < 0 || devs[i] >= ndev) die("MGCM_AMD_SETUP", "MGCM_AMD_DEVICES names a GPU that does not exist");
+      const bool virtIds = getenv("MGCM_AMD_VIRTUAL_GPUS") && atoi(getenv("MGCM_AMD_VIRTUAL_GPUS")) != 0;
+      if (devs[i] < 0 || (!virtIds && devs[i] >= ndev)) die("MGCM_AMD_SETUP", "MGCM_AMD_DEVICES names a GPU that does not exist");
     }
   }
+  // MGCM_AMD_VIRTUAL_GPUS=1 (test hook): the GPU ids above are logical -- every model runs on
+  // device 0, but the models are grouped, sharded, solved and stepped exactly as on that many
+  // GPUs (per-GPU CG2D leads, cross-GPU copies, the routine-by-routine multi-GPU step), so the
+  // code an 8-GPU node runs is exercised on one
+  const bool virt = getenv("MGCM_AMD_VIRTUAL_GPUS") && atoi(getenv("MGCM_AMD_VIRTUAL_GPUS")) != 0;
+  if (virt && !getenv("MGCM_AMD_DEVICES"))
+    for (int i = 0; i < N; i++) devs[i] = i;   // one logical GPU per model
   for (int i = 0; i < N; i++) {
     Shard s;
-    s.dev = devs[i];
+    s.gpu = devs[i];
+    s.dev = virt ? 0 : devs[i];
     s.m = mgcm_create(d[0], d[1], d[2], d[3], d[4], d[5], d[6], s.dev);
     if (!s.m) die("MGCM_AMD_SETUP");
     s.nT = nt;

@@ -476,3 +476,52 @@ def test_refhost_multistream_capture(layout, models, tmp_path):
     print("refhost %s models=%d step ms one-stream %s multi-stream %s" % (layout, models, times["one"], times["multi"]))
     assert not bad, bad
     assert len(outs["one"]) >= 18
+
+
+# The drop-ins' multi-GPU path on the one GPU of the test box (MGCM_AMD_VIRTUAL_GPUS=1: the
+# models stand for that many GPUs but all run on device 0): per-GPU CG2D leads, the
+# cross-GPU copies of the gathered right-hand side and solution, the halo-source links, and
+# the routine-by-routine step the drop-ins run when the models span GPUs -- the code path an
+# 8-GPU node takes -- bit-identical to one model; mwg = 1: the multi-workgroup CG2D launched
+# once per "GPU" on one shared hand-off block.  The eager multi-GPU ms/step is recorded.
+@pytest.mark.parametrize("layout,models,mwg", [("ref", 2, 0), ("ref", 4, 0), ("cs32_6t", 6, 0), ("cs32_6t", 3, 1)])
+def test_refhost_virtual_gpus(layout, models, mwg, tmp_path):
+    from mitgcm_amd import configs
+    exe = os.path.join(RH, "refhost_" + layout)
+    assert os.path.exists(exe), "refhost not built (mitgcm_amd/fortran/build_refhost.py, __graft_entry__.build())"
+    nsteps = 4
+
+    def cfg():
+        if layout == "ref":
+            g, params, state, forcing = configs.global_ocean_90x40x15(nSx=9, nSy=4)
+        else:
+            g, params, state, forcing = configs.global_ocean_cs32x15(sNy=32)
+        if mwg:
+            params["cg2dForceMwg"] = 1
+        return g, params, state, forcing
+    m = configs.make_model(cfg)
+    if layout == "ref":
+        state = _write_blob(tmp_path / "refhost_in.bin", m, nsteps, monitor_days=2, packages_off=True)
+        pdir = PARAM_DIR
+    else:
+        pdir = _cs32_namelists(str(tmp_path / "input"))
+        w2 = m.g.topo.w2_arrays(ldNb=8, ldT=2 * m.g.nTiles)
+        state = _write_blob(tmp_path / "refhost_in.bin", m, nsteps, monitor_days=2, w2=w2, undef=("ALLOW_CD_CODE",))
+    m.close()
+    outs, times = {}, {}
+    for n, virt in ((1, "0"), (models, "1")):
+        env = dict(os.environ, MGCM_AMD_MODELS=str(n), MGCM_AMD_VIRTUAL_GPUS=virt, MGCM_CG2D_MWG=str(mwg),
+                   MGCM_AMD_EAGER="0")
+        r = subprocess.run([exe, str(tmp_path), pdir], capture_output=True, text=True, timeout=300, env=env)
+        assert r.returncode == 0, (n, r.returncode, r.stdout + r.stderr)
+        outs[n], st = _read_out(tmp_path / "refhost_out.bin", state, nsteps)
+        times[n] = st["step_ms"]
+    bad = [k for k in outs[1] if not np.array_equal(outs[1][k], outs[models][k])]
+    rec = {"layout": layout, "virtual_gpus": models, "mwg": mwg, "step_ms_1_model": times[1],
+           "step_ms_virtual_gpus": times[models]}
+    print("refhost virtual GPUs: %s" % json.dumps(rec))
+    if os.path.isdir(os.path.join(ROOT, "gpurun_out")):
+        with open(os.path.join(ROOT, "gpurun_out", "refhost_vgpu_%s_m%d_w%d.json" % (layout, models, mwg)), "w") as f:
+            json.dump(rec, f)
+    assert not bad, bad
+    assert len(outs[1]) >= 18
