@@ -320,6 +320,8 @@ struct TracerArgs {
   double *trNext;       // where CYCLE_TRACER writes the new tracer (ping-pong partner)
   double *gNm1;         // AB2 history of the tendency
   double *scr;          // T* for the implicit vertical solve (gTscr for theta, cpScr for salt)
+  double *cp;           // the Thomas sweep's c' (k_tracer_march2<true>; advScr1 / advScr2, unused without
+                        // multi-dimensional advection), or null
   const double *sfc;    // surface forcing (surfaceForcingT/S), or null
   double diffKh, diffKr, dT;
   int advection, multiDim, useAB, forcing;

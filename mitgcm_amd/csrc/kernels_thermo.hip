@@ -990,7 +990,14 @@ __global__ void __launch_bounds__(256) TRM_ATTR k_tracer_march(Dims d, Params p,
 // T(i-1), T(i+2), u(i+2), hFacW(i+2) are single doubles.  A workgroup covers whole rows of
 // the tile (sNx/2 pairs x 256/(sNx/2) rows), so a wave reads contiguous row segments.  Each
 // column's arithmetic is tracer_flat_arith on its own operands: bit-identical.
+// FWD (whole columns, KC = Nr): GAD_IMPLICIT_R's coefficients of each level (from the level's
+// own operands, already in registers: maskC at k-1 / k+1, IVDConvCount at k / k+1,
+// recip_hFacC) and SOLVE_TRIDIAGONAL's forward elimination ride in the march, in
+// tracer_impl_body's expressions and order; the march stores (c', y') instead of T*, and
+// k_tracer_backsub finishes the column.  No T* round trip, no second pass over the
+// coefficient operands.
 typedef __attribute__((ext_vector_type(2))) double trd2;
+template <bool FWD>
 __global__ void __launch_bounds__(256) TRM_ATTR k_tracer_march2(Dims d, Params p, Fields f, TracerArgs a, const int *iterPtr,
                                                                 int KC, int nkc, int nty) {
   int b = mg_xcd_block();
@@ -1014,9 +1021,17 @@ __global__ void __launch_bounds__(256) TRM_ATTR k_tracer_march2(Dims d, Params p
   const long qu = k0 > 1 ? q3 - n2 : q3;
   trd2 Tu = L2(T, qu), mCu = L2(f.maskC, qu);
   trd2 T0 = L2(T, q3), mC0 = L2(f.maskC, q3), w0 = L2(f.wVel, q3), ivd0 = L2(f.IVDConvCount, q3);
+  double cpPrev[2] = {0.0, 0.0}, ypPrev[2] = {0.0, 0.0};   // FWD: the sweep's previous level
+  const bool rs = p.nonlinFreeSurf > 0 && p.select_rStar > 0;
   for (int k = k0; k <= k1; k++, q3 += n2) {
     const long qd = k < Nr ? q3 + n2 : q3;
     const trd2 Td = L2(T, qd), mCd = L2(f.maskC, qd), w1 = L2(f.wVel, qd), ivd1 = L2(f.IVDConvCount, qd);
+    double rdrFk = 0.0, rdcK = 0.0, rdcP = 0.0;
+    if constexpr (FWD) {
+      rdrFk = f.recip_drF[k - 1];
+      rdcK = f.recip_drC[k - 1];
+      rdcP = f.recip_drC[(k <= Nr - 1 ? k + 1 : Nr) - 1];
+    }
     const trd2 Ts = L2(T, q3 - nx), Tn = L2(T, q3 + nx);
     const double Tw = T[q3 - 1], Te = T[q3 + 2];
     const trd2 u01 = L2(f.uVel, q3), v0 = L2(f.vVel, q3), v1 = L2(f.vVel, q3 + nx);
@@ -1025,7 +1040,7 @@ __global__ void __launch_bounds__(256) TRM_ATTR k_tracer_march2(Dims d, Params p
     const trd2 rhC = L2(f.recip_hFacC, q3);
     const trd2 gA = a.multiDim ? L2(f.gAdv, q3) : trd2{0.0, 0.0};
     const trd2 gO = a.useAB ? L2(a.gNm1, q3) : trd2{0.0, 0.0};
-    double v[2], gN[2] = {0.0, 0.0};
+    double v[2], gN[2] = {0.0, 0.0}, cpo[2] = {0.0, 0.0};
 #pragma unroll
     for (int e = 0; e < 2; e++) {
       TrLev o;
@@ -1041,13 +1056,76 @@ __global__ void __launch_bounds__(256) TRM_ATTR k_tracer_march2(Dims d, Params p
       o.ivd0 = e ? ivd0.y : ivd0.x; o.ivd1 = e ? ivd1.y : ivd1.x;
       o.rhC = e ? rhC.y : rhC.x; o.gAdv = e ? gA.y : gA.x; o.gOld = e ? gO.y : gO.x;
       v[e] = tracer_flat_arith(p, f, a, Nr, k, myIter, c[e], o, &gN[e]);
+      if constexpr (FWD) {   // tracer_impl_body<true>'s coefficients, then its forward step
+        const double rh = rs ? o.rhC / c[e].rsx : o.rhC;
+        auto kappa = [&](double ivd) { return (ivd * p.ivdc_kappa + 0.0) + a.diffKr; };
+        double sub = 0.0, sup = 0.0;
+        if (k >= 2) sub = -(p.deltaTtracer * o.mCu * rh * rdrFk * kappa(o.ivd0) * rdcK);
+        if (k <= Nr - 1) sup = -(p.deltaTtracer * o.mCd * rh * rdrFk * kappa(o.ivd1) * rdcP);
+        const double diag = 1.0 - (sub + sup), y = v[e];
+        double cp, yp;
+        if (k == 1) {
+          if (diag != 0.0) { const double rec = 1.0 / diag; cp = sup * rec; yp = y * rec; }
+          else { cp = 0.0; yp = 0.0; }
+        } else {
+          const double tmp = diag - sub * cpPrev[e];
+          if (tmp != 0.0) { const double rec = 1.0 / tmp; cp = sup * rec; yp = (y - sub * ypPrev[e]) * rec; }
+          else { cp = 0.0; yp = 0.0; }
+        }
+        cpPrev[e] = cp; ypPrev[e] = yp;
+        cpo[e] = cp; v[e] = yp;
+      }
     }
     if (a.useAB) *reinterpret_cast<trd2 *>(a.gNm1 + q3) = trd2{gN[0], gN[1]};
     *reinterpret_cast<trd2 *>((p.implicitDiffusion ? a.scr : a.trNext) + q3) = trd2{v[0], v[1]};
+    if constexpr (FWD) *reinterpret_cast<trd2 *>(a.cp + q3) = trd2{cpo[0], cpo[1]};
     Tu = T0; T0 = Td; mCu = mC0; mC0 = mCd; w0 = w1; ivd0 = ivd1;
   }
 }
 
+
+// SOLVE_TRIDIAGONAL's back substitution (tracer_impl_body's upward sweep) from the (c', y')
+// k_tracer_march2<true> stored: one thread per interior column pair (16-byte accesses), all
+// levels' loads issued before the recurrence (they do not depend on it), the new tracer
+// written to its other buffer (CYCLE_TRACER).
+__global__ void __launch_bounds__(256) k_tracer_backsub(Dims d, TracerArgs a, int nty) {
+  const int b = mg_xcd_block();
+  const int hx = d.sNx >> 1, TY = 256 / hx;
+  const int ty = b % nty, t = d.t0 + b / nty;
+  const int px = (int)threadIdx.x % hx, jy = (int)threadIdx.x / hx;
+  if (jy >= TY) return;
+  const int i = 1 + 2 * px, j = 1 + ty * TY + jy;
+  if (j > d.sNy) return;
+  const int Nr = d.Nr;
+  const long n2 = d.n2, q1 = MG_I3(d, i, j, 1, t);
+  auto L2 = [](const double *x, long o) { return *reinterpret_cast<const trd2 *>(x + o); };
+  constexpr int CH = 10;   // levels per batch of loads
+  trd2 below = {0.0, 0.0};
+  for (int k1 = Nr; k1 >= 1; k1 -= CH) {
+    const int k0 = k1 - CH + 1 > 1 ? k1 - CH + 1 : 1;
+    trd2 cpv[CH], ypv[CH];
+#pragma unroll
+    for (int u = 0; u < CH; u++) {
+      const int k = k1 - u;
+      if (k >= k0) {
+        const long q3 = q1 + (long)(k - 1) * n2;
+        cpv[u] = L2(a.cp, q3);
+        ypv[u] = L2(a.scr, q3);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < CH; u++) {
+      const int k = k1 - u;
+      if (k >= k0) {
+        trd2 v;
+        if (k == Nr) v = ypv[u];
+        else { v.x = ypv[u].x - cpv[u].x * below.x; v.y = ypv[u].y - cpv[u].y * below.y; }
+        *reinterpret_cast<trd2 *>(a.trNext + q1 + (long)(k - 1) * n2) = v;
+        below = v;
+      }
+    }
+  }
+}
 
 __global__ void __launch_bounds__(256) k_tracer_rhs_flat(Dims d, Params p, Fields f, TracerArgs a, const int *iterPtr) {
   MG_PLANE(1, d.sNx, 1, d.sNy, z)
@@ -1229,6 +1307,12 @@ hipError_t launch_oceanic_phys(const Dims &d, const Params &p, const Fields &f, 
   return hipGetLastError();
 }
 
+// the implicit solve's forward sweep fused into a whole-column march (k_tracer_march2<true> +
+// k_tracer_backsub): MGCM_TRACER_FWD=1 (read per launch)
+static bool tracer_fwd_on() {
+  const char *e = getenv("MGCM_TRACER_FWD");
+  return e && atoi(e) != 0;
+}
 static bool tracer_march_on(const Dims &d) {
   const char *e = getenv("MGCM_TRACER_MARCH");   // read per launch (tests switch it per model)
   if (e) return atoi(e) != 0;
@@ -1276,7 +1360,16 @@ hipError_t launch_tracer_step(const Dims &d, const Params &p, const Fields &f, c
         al(a.trNext) && al(a.scr) && al(a.gNm1) && al(f.maskC) && al(f.wVel) && al(f.IVDConvCount) && al(f.uVel) &&
         al(f.vVel) && al(f.hFacW) && al(f.hFacS) && al(f.recip_hFacC) && (!a.multiDim || al(f.gAdv))) {
       const int TY = 256 / hx, nty2 = (d.sNy + TY - 1) / TY;
-      hipLaunchKernelGGL(k_tracer_march2, dim3((unsigned)(nkc * nty2 * d.nT)), blk, 0, s, d, p, f, a, iterPtr, KC, nkc, nty2);
+      // the implicit solve's forward elimination inside a whole-column march, then the back
+      // substitution (MGCM_TRACER_FWD=1; tracer_fwd_on): no T* round trip
+      if (impl && p.implicitDiffusion && !p.useGMRedi && tracer_fwd_on() && !a.multiDim && a.cp && al(a.cp) && d.Nr > 1) {
+        hipLaunchKernelGGL(k_tracer_march2<true>, dim3((unsigned)(nty2 * d.nT)), blk, 0, s, d, p, f, a, iterPtr, d.Nr, 1,
+                           nty2);
+        hipLaunchKernelGGL(k_tracer_backsub, dim3((unsigned)(nty2 * d.nT)), blk, 0, s, d, a, nty2);
+        return hipGetLastError();
+      }
+      hipLaunchKernelGGL(k_tracer_march2<false>, dim3((unsigned)(nkc * nty2 * d.nT)), blk, 0, s, d, p, f, a, iterPtr, KC, nkc,
+                         nty2);
     } else
       hipLaunchKernelGGL(k_tracer_march, dim3((unsigned)(nkc * ntx * nty * d.nT)), blk, 0, s, d, p, f, a, iterPtr, KC, nkc,
                          ntx, nty);

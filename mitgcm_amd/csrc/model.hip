@@ -1402,6 +1402,7 @@ static TracerArgs tracer_args(mgcm_model *m, bool salt) {
   a.trNext = salt ? m->f.saltNext : m->f.thetaNext;
   a.gNm1 = salt ? m->f.gsNm1 : m->f.gtNm1;
   a.scr = salt ? m->f.cpScr : m->f.gTscr;   // own scratch each: the two may run concurrently
+  a.cp = salt ? m->f.advScr2 : m->f.advScr1;
   a.sfc = salt ? m->f.surfaceForcingS : m->f.surfaceForcingT;
   a.diffKh = salt ? p.diffKhS : p.diffKhT;
   a.diffKr = salt ? p.diffKrS : p.diffKrT;
