@@ -786,6 +786,16 @@ void fork_from_0(const char *w) {
 // replay then leaves every model at the parity its captured step's host-side CYCLE_TRACER
 // swaps left (mgcm_tracer_parity).  false: the capture failed (the step then runs eagerly
 // and later steps stay eager).
+// MGCM_AMD_CAPTURE_DEBUG=1: each stage of a multi-model capture and replay printed (and the
+// replay waited for), to place a fault inside the runtime
+void cap_dbg(const char *what, int q) {
+  static const bool on = getenv("MGCM_AMD_CAPTURE_DEBUG") && atoi(getenv("MGCM_AMD_CAPTURE_DEBUG")) != 0;
+  if (on) { fprintf(stderr, "MGCM_AMD capture[%d]: %s\n", q, what); fflush(stderr); }
+}
+bool cap_dbg_on() {
+  static const bool on = getenv("MGCM_AMD_CAPTURE_DEBUG") && atoi(getenv("MGCM_AMD_CAPTURE_DEBUG")) != 0;
+  return on;
+}
 bool multi_replay(const char *w, int myIter) {
   const int q = mgcm_tracer_parity(g.m, -1);
   if (q < 0 || q > 3) die(w);
@@ -819,6 +829,7 @@ bool multi_replay(const char *w, int myIter) {
         if (mgcm_set_stream(g.sh[i].m, nullptr)) die(w);
       return false;
     }
+    cap_dbg("begin capture", q);
     g.capturing = true;   // (the pool's events from here: the fork's record is the capture's first node)
     fork_from_0(w);
     g.devIter = myIter;   // the graph's increments are relative to this
@@ -828,7 +839,14 @@ bool multi_replay(const char *w, int myIter) {
     hipGraph_t gr = nullptr;
     hipchk(hipSetDevice(g.sh[0].dev), w);
     hipError_t e = hipStreamEndCapture(s0, &gr);
+    cap_dbg("end capture", q);
+    if (e == hipSuccess && cap_dbg_on()) {
+      size_t nn = 0;
+      (void)hipGraphGetNodes(gr, nullptr, &nn);
+      fprintf(stderr, "MGCM_AMD capture[%d]: %zu nodes\n", q, nn);
+    }
     if (e == hipSuccess) e = hipGraphInstantiate(&G.exec, gr, nullptr, nullptr, 0);
+    cap_dbg("instantiated", q);
     if (gr) (void)hipGraphDestroy(gr);
     for (size_t i = 1; i < g.sh.size(); i++)   // each model back on its own stream
       if (mgcm_set_stream(g.sh[i].m, nullptr)) die(w);
@@ -845,7 +863,12 @@ bool multi_replay(const char *w, int myIter) {
       if (mgcm_tracer_parity(g.sh[i].m, G.post[i]) < 0) die(w);
   }
   hipchk(hipSetDevice(g.sh[0].dev), w);
+  cap_dbg("launch", q);
   hipchk(hipGraphLaunch(G.exec, stream_of(g.sh[0])), w);
+  if (cap_dbg_on()) {
+    hipchk(hipStreamSynchronize(stream_of(g.sh[0])), w);
+    cap_dbg("replay done", q);
+  }
   fork_from_0(w);   // every model's later work (downloads, the next step) after the graph
   g.devIter = -1;   // the graph advanced the counters: set again before the next use
   return true;
