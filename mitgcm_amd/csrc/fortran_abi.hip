@@ -215,6 +215,20 @@ void hipchk(hipError_t e, const char *where) {
 }
 hipStream_t stream_of(const Shard &s) { return (hipStream_t)mgcm_get_stream(s.m); }
 
+// MGCM_AMD_CAPTURE_DEBUG=1: each stage of a multi-model capture and replay printed (and the
+// replay waited for), down to the device operations of the captured drop-ins, to place a
+// fault inside the runtime
+bool cap_dbg_on() {
+  static const bool on = getenv("MGCM_AMD_CAPTURE_DEBUG") && atoi(getenv("MGCM_AMD_CAPTURE_DEBUG")) != 0;
+  return on;
+}
+void cap_dbg(const char *what, int q) {
+  if (cap_dbg_on()) { fprintf(stderr, "MGCM_AMD capture[%d]: %s\n", q, what); fflush(stderr); }
+}
+void cap_op(const char *what, int model) {
+  if (cap_dbg_on() && g.capturing) { fprintf(stderr, "MGCM_AMD   op %s model %d\n", what, model); fflush(stderr); }
+}
+
 bool cap_pool_on() {
   static const bool off = getenv("MGCM_AMD_CAPTURE_POOL") && atoi(getenv("MGCM_AMD_CAPTURE_POOL")) == 0;
   return !off;
@@ -252,13 +266,17 @@ long nTiles() { return (long)g.dims[5] * g.dims[6]; }
 
 // every model runs fn (its own tiles; the r* passes every tile)
 void run_all(const char *where, int (*fn)(mgcm_model *)) {
-  for (auto &s : g.sh) {
+  for (size_t i = 0; i < g.sh.size(); i++) {
+    auto &s = g.sh[i];
+    cap_op(where, (int)i);
     hipchk(hipSetDevice(s.dev), where);
     if (fn(s.m)) die(where);
   }
 }
 void phase_all(const char *where, int phase) {
-  for (auto &s : g.sh) {
+  for (size_t i = 0; i < g.sh.size(); i++) {
+    auto &s = g.sh[i];
+    if (cap_dbg_on() && g.capturing) { fprintf(stderr, "MGCM_AMD   op %s phase %d model %zu\n", where, phase, i); fflush(stderr); }
     hipchk(hipSetDevice(s.dev), where);
     if (mgcm_step_phase(s.m, phase)) die(where);
   }
@@ -268,6 +286,7 @@ void phase_all(const char *where, int phase) {
 // model has issued so far (no host synchronisation).
 void barrier_all(const char *where) {
   if (!multi()) return;
+  cap_op("barrier", -1);
   std::vector<hipEvent_t> ev(g.sh.size());
   for (size_t i = 0; i < g.sh.size(); i++) {
     const Shard &s = g.sh[i];
@@ -284,6 +303,7 @@ void barrier_all(const char *where) {
 
 // The tile blocks [t0, t0+nT) of a 2-D field from model `from` to every other model.
 void copy_blocks(const char *where, const char *name, int from, int t0, int nT) {
+  cap_op(name, from);
   const Shard &a = g.sh[from];
   const long per = n2();
   const double *src = mgcm_device_ptr(a.m, name);
@@ -313,6 +333,7 @@ void gather2d(const char *where, const char *name) {
 // (per-link events) and needs nothing from the others.
 void xfer3d(const char *where, int group) {
   barrier_all(where);
+  cap_op("xfer3d", group);
   const int Nr = g.dims[4];
   for (auto &L : g.links) {
     const Shard &a = g.sh[L.s], &b = g.sh[L.d];
@@ -786,16 +807,6 @@ void fork_from_0(const char *w) {
 // replay then leaves every model at the parity its captured step's host-side CYCLE_TRACER
 // swaps left (mgcm_tracer_parity).  false: the capture failed (the step then runs eagerly
 // and later steps stay eager).
-// MGCM_AMD_CAPTURE_DEBUG=1: each stage of a multi-model capture and replay printed (and the
-// replay waited for), to place a fault inside the runtime
-void cap_dbg(const char *what, int q) {
-  static const bool on = getenv("MGCM_AMD_CAPTURE_DEBUG") && atoi(getenv("MGCM_AMD_CAPTURE_DEBUG")) != 0;
-  if (on) { fprintf(stderr, "MGCM_AMD capture[%d]: %s\n", q, what); fflush(stderr); }
-}
-bool cap_dbg_on() {
-  static const bool on = getenv("MGCM_AMD_CAPTURE_DEBUG") && atoi(getenv("MGCM_AMD_CAPTURE_DEBUG")) != 0;
-  return on;
-}
 bool multi_replay(const char *w, int myIter) {
   const int q = mgcm_tracer_parity(g.m, -1);
   if (q < 0 || q > 3) die(w);
