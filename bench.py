@@ -302,12 +302,12 @@ def default_pmc_summary(config):
     """The newest committed PMC summary of this workload (profiles/r0N/<tag>_final/, then
     profiles/r0N/<tag>/)."""
     tag = PMC_TAG.get(config, config)
-    for rnd in ("r05", "r04", "r03", "r02"):
+    for rnd in ("r06", "r05", "r04", "r03", "r02"):
         for sub in (tag + "_final", tag):
             p = os.path.join(ROOT, "profiles", rnd, sub, "pmc_summary.json")
             if os.path.exists(p):
                 return p
-    return os.path.join(ROOT, "profiles", "r05", tag, "pmc_summary.json")
+    return os.path.join(ROOT, "profiles", "r06", tag, "pmc_summary.json")
 
 
 def stream_triad_gbs(device, n=64 << 20, reps=8):

@@ -2324,10 +2324,11 @@ static void vi_m2_one(const Dims &d, const VIP<C> &vp, const Fields &f, const in
 static bool vi_m2_launch(const Dims &d, const Params &p, const Fields &f, const int *iterPtr, int BX, int BY, int nbx,
                          int nby, int KC, int nkc, hipStream_t s) {
   const unsigned code = vi_opt_code(p);
-  // MGCM_VI_SPLIT (A/B): 0 both components' chains interleaved, 1 U then V (2 waves per SIMD),
-  // 3 U then V with registers capped for 3 waves per SIMD
+  // MGCM_VI_SPLIT: 1 (default) U's chain then V's, 2 waves per SIMD (215 VGPRs: LLC-90's VI
+  // 319-320 against 323.7-323.8 us interleaved, profiles/r06/ab_hr_vi/); 0 both chains
+  // interleaved (247 VGPRs); 3 U then V capped for 3 waves per SIMD (43 VGPRs spilled: 605 us)
   const char *se = getenv("MGCM_VI_SPLIT");
-  const int split = se ? atoi(se) : 0;
+  const int split = se ? atoi(se) : 1;
   if (code == VI_CODE_LLC && BX == 31 && BY == 8) {
     if (split == 3) vi_m2_one<31, 8, VI_CODE_LLC, 2 | 4 | 16 | 32>(d, vi_params<VI_CODE_LLC>(p), f, iterPtr, nbx, nby, KC, nkc, s);
     else if (split == 1) vi_m2_one<31, 8, VI_CODE_LLC, 14 | 16>(d, vi_params<VI_CODE_LLC>(p), f, iterPtr, nbx, nby, KC, nkc, s);
