@@ -160,6 +160,17 @@ struct FortranSide {
   };
   std::vector<EvPool> evPools;
   bool multiGraphOff = false; // a capture failed: the multi-model steps stay eager
+  // Models over several GPUs: the recorded step as per-GPU graphs cut at every cross-GPU
+  // exchange point (segments): segment k of GPU group j is captured on that group's lead
+  // stream (the group's other models issue there too), and a replay launches segment k of
+  // every group, then the cross-GPU barrier as plain events, then segment k+1 (seg_replay)
+  struct SegGraphs {
+    std::vector<std::vector<hipGraphExec_t>> seg;   // [segment][group]
+    std::vector<int> pre, post;
+  } sgr[4];
+  bool segMode = false, segFail = false;            // inside a segmented capture / it failed
+  std::vector<hipGraphExec_t> segCur;               // the open segment's graphs (one per group)
+  std::vector<std::vector<hipGraphExec_t>> segAll;
   long nUp = 0, nDown = 0;   // copies of whole bound arrays, for mgcm_amd_transfer_stats_
   // the state arrays' host pages, registered with HIP once the time loop begins (downloads
   // then go straight to the COMMON blocks by DMA); false when registration was refused
@@ -284,8 +295,10 @@ void phase_all(const char *where, int phase) {
 
 // Cross-model barrier on the device: every model's stream waits for the work every other
 // model has issued so far (no host synchronisation).
+void seg_boundary(const char *where);
 void barrier_all(const char *where) {
   if (!multi()) return;
+  if (g.segMode) return seg_boundary(where);   // segmented capture: the barrier is a cut
   cap_op("barrier", -1);
   std::vector<hipEvent_t> ev(g.sh.size());
   for (size_t i = 0; i < g.sh.size(); i++) {
@@ -335,6 +348,27 @@ void xfer3d(const char *where, int group) {
   barrier_all(where);
   cap_op("xfer3d", group);
   const int Nr = g.dims[4];
+  if (g.segMode) {   // the senders' packs and copies, a cut, then the receivers' unpacks
+    for (auto &L : g.links) {
+      const Shard &a = g.sh[L.s];
+      const int nf = mgcm_exchange_nfields_group(a.m, group);
+      if (nf <= 0) continue;
+      hipchk(hipSetDevice(a.dev), where);
+      if (mgcm_halo_pack_group(a.m, group, L.idxS, L.n, L.sbuf, 0)) die(where);
+      hipchk(hipMemcpyAsync(L.rbuf, L.sbuf, (size_t)nf * Nr * L.n * sizeof(double), hipMemcpyDeviceToDevice,
+                            stream_of(a)),
+             where);
+    }
+    seg_boundary(where);
+    for (auto &L : g.links) {
+      const Shard &b = g.sh[L.d];
+      const int nf = mgcm_exchange_nfields_group(b.m, group);
+      if (nf <= 0) continue;
+      hipchk(hipSetDevice(b.dev), where);
+      if (mgcm_halo_pack_group(b.m, group, L.idxD, L.n, L.rbuf, 1)) die(where);
+    }
+    return;
+  }
   for (auto &L : g.links) {
     const Shard &a = g.sh[L.s], &b = g.sh[L.d];
     const int nf = mgcm_exchange_nfields_group(a.m, group);
@@ -696,8 +730,15 @@ void free_links() {
   g.links.clear();
   g.cgLeads.clear();
 }
+void seg_destroy(FortranSide::SegGraphs &S) {
+  for (auto &v : S.seg)
+    for (auto e : v)
+      if (e) (void)hipGraphExecDestroy(e);
+  S.seg.clear();
+}
 void free_shards() {
   free_links();
+  for (auto &S : g.sgr) seg_destroy(S);
   for (auto &p : g.evPools) {
     (void)hipSetDevice(p.dev);
     for (auto e : p.ev) (void)hipEventDestroy(e);
@@ -744,14 +785,13 @@ bool canonical_step(const std::vector<std::string> &q) {
   want.push_back("DO_FIELDS_BLOCKING_EXCHANGES");
   return q == want;
 }
-// Replay: one model, or N models on one GPU (captured onto one stream, multi_replay); models
-// spread over several GPUs step routine by routine (a graph spanning GPUs is not captured)
+// Replay: one model, N models on one GPU (captured onto one stream, multi_replay), or models
+// over several GPUs (per-GPU segment graphs, seg_replay); MGCM_AMD_EAGER=1 steps routine by
+// routine
 bool fuse_allowed() {
   const char *e = getenv("MGCM_AMD_EAGER");
   if (e && atoi(e) == 1) return false;
   if (!multi()) return true;
-  for (auto &s : g.sh)
-    if (s.gpu != g.sh[0].gpu) return false;
   return !g.multiGraphOff;
 }
 
@@ -882,6 +922,137 @@ bool multi_replay(const char *w, int myIter) {
   }
   fork_from_0(w);   // every model's later work (downloads, the next step) after the graph
   g.devIter = -1;   // the graph advanced the counters: set again before the next use
+  return true;
+}
+bool spans_gpus() {
+  for (auto &s : g.sh)
+    if (s.gpu != g.sh[0].gpu) return true;
+  return false;
+}
+hipStream_t lead_stream(size_t j) { return stream_of(g.sh[g.cgLeads[j].shard]); }
+int lead_dev(size_t j) { return g.sh[g.cgLeads[j].shard].dev; }
+// open one capture per GPU group (Relaxed: several captures in flight on this thread)
+void seg_begin(const char *w) {
+  for (size_t j = 0; j < g.cgLeads.size(); j++) {
+    hipchk(hipSetDevice(lead_dev(j)), w);
+    if (hipStreamBeginCapture(lead_stream(j), hipStreamCaptureModeRelaxed) != hipSuccess) {
+      (void)hipGetLastError();
+      g.segFail = true;
+    }
+  }
+}
+// close every group's capture into the open segment's graphs
+void seg_end(const char *w) {
+  std::vector<hipGraphExec_t> cur(g.cgLeads.size(), nullptr);
+  for (size_t j = 0; j < g.cgLeads.size(); j++) {
+    hipchk(hipSetDevice(lead_dev(j)), w);
+    hipGraph_t gr = nullptr;
+    hipError_t e = hipStreamEndCapture(lead_stream(j), &gr);
+    if (e == hipSuccess) e = hipGraphInstantiate(&cur[j], gr, nullptr, nullptr, 0);
+    if (gr) (void)hipGraphDestroy(gr);
+    if (e != hipSuccess) {
+      (void)hipGetLastError();
+      g.segFail = true;
+    }
+  }
+  g.segAll.push_back(cur);
+}
+void seg_boundary(const char *w) {
+  cap_op("segment cut", (int)g.segAll.size());
+  seg_end(w);
+  seg_begin(w);
+}
+// every group's lead stream waits for every other's work so far (between segments)
+void group_barrier(const char *w) {
+  const size_t G = g.cgLeads.size();
+  for (size_t j = 0; j < G; j++) {
+    hipchk(hipSetDevice(lead_dev(j)), w);
+    hipchk(hipEventRecord(g.sh[g.cgLeads[j].shard].ev, lead_stream(j)), w);
+  }
+  for (size_t j = 0; j < G; j++) {
+    hipchk(hipSetDevice(lead_dev(j)), w);
+    for (size_t i = 0; i < G; i++)
+      if (i != j) hipchk(hipStreamWaitEvent(lead_stream(j), g.sh[g.cgLeads[i].shard].ev, 0), w);
+  }
+}
+// within each group: the lead stream after the group's models' own streams (join), or they
+// after it (fork)
+void group_join(const char *w, bool fork) {
+  for (size_t j = 0; j < g.cgLeads.size(); j++) {
+    const int L = g.cgLeads[j].shard;
+    for (size_t i = 0; i < g.sh.size(); i++) {
+      if ((int)i == L || g.sh[i].gpu != g.sh[L].gpu) continue;
+      const Shard &from = fork ? g.sh[L] : g.sh[i], &to = fork ? g.sh[i] : g.sh[L];
+      hipchk(hipSetDevice(from.dev), w);
+      hipchk(hipEventRecord(from.ev, stream_of(from)), w);
+      hipchk(hipSetDevice(to.dev), w);
+      hipchk(hipStreamWaitEvent(stream_of(to), from.ev, 0), w);
+    }
+  }
+}
+// One FORWARD_STEP of models over several GPUs as per-GPU segment graphs (the recorded drop-in
+// sequence, captured on first use per tracer-buffer parity of model 0).  false: the capture
+// failed -- every model is put back at the tracer parity it had, and this and later steps run
+// routine by routine.
+bool seg_replay(const char *w, int myIter) {
+  const int q = mgcm_tracer_parity(g.m, -1);
+  if (q < 0 || q > 3) die(w);
+  auto &S = g.sgr[q];
+  std::vector<int> pre;
+  for (auto &s : g.sh) pre.push_back(mgcm_tracer_parity(s.m, -1));
+  const size_t G = g.cgLeads.size();
+  group_join(w, false);   // the forcing uploads of every model before its group's graphs
+  group_barrier(w);       // and the previous step's work of every group
+  if (S.seg.empty()) {
+    S.pre = pre;
+    for (size_t i = 0; i < g.sh.size(); i++) {   // every model issues on its group's lead stream
+      const int L = g.cgLeads[0].shard;
+      (void)L;
+      for (size_t j = 0; j < G; j++)
+        if (g.sh[g.cgLeads[j].shard].gpu == g.sh[i].gpu && (int)i != g.cgLeads[j].shard)
+          if (mgcm_set_stream(g.sh[i].m, lead_stream(j))) die(w);
+    }
+    g.segAll.clear();
+    g.segFail = false;
+    cap_dbg("begin segmented capture", q);
+    seg_begin(w);
+    g.capturing = g.segMode = true;
+    g.devIter = myIter;
+    if (!g.segFail) run_recorded_step(w, myIter);
+    g.capturing = g.segMode = false;
+    seg_end(w);
+    for (size_t i = 0; i < g.sh.size(); i++)   // each model back on its own stream
+      if (mgcm_set_stream(g.sh[i].m, nullptr)) die(w);
+    if (g.segFail) {
+      for (auto &v : g.segAll)
+        for (auto e : v)
+          if (e) (void)hipGraphExecDestroy(e);
+      g.segAll.clear();
+      for (size_t i = 0; i < g.sh.size(); i++)
+        if (mgcm_tracer_parity(g.sh[i].m, pre[i]) < 0) die(w);
+      g.devIter = -1;
+      return false;
+    }
+    S.seg = g.segAll;
+    g.segAll.clear();
+    S.post.clear();
+    for (auto &s : g.sh) S.post.push_back(mgcm_tracer_parity(s.m, -1));
+    if (cap_dbg_on()) fprintf(stderr, "MGCM_AMD capture[%d]: %zu segments x %zu GPUs\n", q, S.seg.size(), G);
+  } else {
+    if (pre != S.pre) die(w, "a device model's tracer parity differs from the captured step's");
+    for (size_t i = 0; i < g.sh.size(); i++)
+      if (mgcm_tracer_parity(g.sh[i].m, S.post[i]) < 0) die(w);
+  }
+  for (size_t k = 0; k < S.seg.size(); k++) {
+    if (k > 0) group_barrier(w);
+    for (size_t j = 0; j < G; j++) {
+      hipchk(hipSetDevice(lead_dev(j)), w);
+      hipchk(hipGraphLaunch(S.seg[k][j], lead_stream(j)), w);
+    }
+  }
+  group_barrier(w);
+  group_join(w, true);   // every model's later work (downloads, the next step) after the graphs
+  g.devIter = -1;
   return true;
 }
 // A routine drop-in of a device-authoritative step: true when its work already ran inside
@@ -1182,8 +1353,8 @@ void do_oceanic_phys_amd_(const double *myTime, const int *myIter, const int *my
     set_iter("DO_OCEANIC_PHYS_AMD", *myIter);
     bool replayed = true;
     if (multi()) {
-      replayed = multi_replay("DO_OCEANIC_PHYS_AMD", *myIter);
-      if (!replayed) {   // the stream refused the capture before anything ran: stay eager
+      replayed = spans_gpus() ? seg_replay("DO_OCEANIC_PHYS_AMD", *myIter) : multi_replay("DO_OCEANIC_PHYS_AMD", *myIter);
+      if (!replayed) {   // the stream refused the capture: stay eager
         fprintf(stderr, "MGCM_AMD: stream capture of the %zu-model step refused; steps run routine by routine\n",
                 g.sh.size());
         g.multiGraphOff = true;

@@ -482,9 +482,10 @@ def test_refhost_multistream_capture(layout, models, tmp_path):
 # The drop-ins' multi-GPU path on the one GPU of the test box (MGCM_AMD_VIRTUAL_GPUS=1: the
 # models stand for that many GPUs but all run on device 0): per-GPU CG2D leads, the
 # cross-GPU copies of the gathered right-hand side and solution, the halo-source links, and
-# the routine-by-routine step the drop-ins run when the models span GPUs -- the code path an
-# 8-GPU node takes -- bit-identical to one model; mwg = 1: the multi-workgroup CG2D launched
-# once per "GPU" on one shared hand-off block.  The eager multi-GPU ms/step is recorded.
+# the step the drop-ins run when the models span GPUs -- the per-GPU segment graphs replayed
+# with event barriers between segments (seg_replay), and routine by routine (MGCM_AMD_EAGER=1)
+# -- the code an 8-GPU node runs, bit-identical to one model; mwg = 1: the multi-workgroup
+# CG2D launched once per "GPU" on one shared hand-off block.  Both forms' ms/step recorded.
 @pytest.mark.parametrize("layout,models,mwg", [("ref", 2, 0), ("ref", 4, 0), ("cs32_6t", 6, 0), ("cs32_6t", 3, 1)])
 def test_refhost_virtual_gpus(layout, models, mwg, tmp_path):
     from mitgcm_amd import configs
@@ -510,19 +511,21 @@ def test_refhost_virtual_gpus(layout, models, mwg, tmp_path):
         state = _write_blob(tmp_path / "refhost_in.bin", m, nsteps, monitor_days=2, w2=w2, undef=("ALLOW_CD_CODE",))
     m.close()
     outs, times = {}, {}
-    for n, virt in ((1, "0"), (models, "1")):
+    for tag, n, virt, eager in (("one", 1, "0", "0"), ("seg", models, "1", "0"), ("eager", models, "1", "1")):
         env = dict(os.environ, MGCM_AMD_MODELS=str(n), MGCM_AMD_VIRTUAL_GPUS=virt, MGCM_CG2D_MWG=str(mwg),
-                   MGCM_AMD_EAGER="0")
+                   MGCM_AMD_EAGER=eager, MGCM_AMD_CAPTURE_DEBUG="1")
         r = subprocess.run([exe, str(tmp_path), pdir], capture_output=True, text=True, timeout=300, env=env)
-        assert r.returncode == 0, (n, r.returncode, r.stdout + r.stderr)
-        outs[n], st = _read_out(tmp_path / "refhost_out.bin", state, nsteps)
-        times[n] = st["step_ms"]
-    bad = [k for k in outs[1] if not np.array_equal(outs[1][k], outs[models][k])]
-    rec = {"layout": layout, "virtual_gpus": models, "mwg": mwg, "step_ms_1_model": times[1],
-           "step_ms_virtual_gpus": times[models]}
+        assert r.returncode == 0, (tag, r.returncode, r.stdout + r.stderr)
+        if tag == "seg":   # the segment graphs were captured and replayed (no fallback to eager)
+            assert "segments x %d GPUs" % models in r.stderr and "routine by routine" not in r.stderr, r.stderr[-2000:]
+        outs[tag], st = _read_out(tmp_path / "refhost_out.bin", state, nsteps)
+        times[tag] = st["step_ms"]
+    bad = [(t, k) for t in ("seg", "eager") for k in outs["one"] if not np.array_equal(outs["one"][k], outs[t][k])]
+    rec = {"layout": layout, "virtual_gpus": models, "mwg": mwg, "step_ms_1_model": times["one"],
+           "step_ms_segment_graphs": times["seg"], "step_ms_eager": times["eager"]}
     print("refhost virtual GPUs: %s" % json.dumps(rec))
     if os.path.isdir(os.path.join(ROOT, "gpurun_out")):
         with open(os.path.join(ROOT, "gpurun_out", "refhost_vgpu_%s_m%d_w%d.json" % (layout, models, mwg)), "w") as f:
             json.dump(rec, f)
     assert not bad, bad
-    assert len(outs[1]) >= 18
+    assert len(outs["one"]) >= 18
