@@ -887,6 +887,7 @@ bool multi_replay(const char *w, int myIter) {
     run_recorded_step(w, myIter);
     join_into_0(w);
     g.capturing = false;
+    cap_dbg("joined; ending capture", q);
     hipGraph_t gr = nullptr;
     hipchk(hipSetDevice(g.sh[0].dev), w);
     hipError_t e = hipStreamEndCapture(s0, &gr);
