@@ -95,7 +95,7 @@ struct Readers {
 struct Shard {
   mgcm_model *m = nullptr;
   int dev = 0, t0 = 0, nT = 0;
-  int gpu = 0;   // the GPU the model stands for (== dev, except under MGCM_AMD_VIRTUAL_GPUS)
+  int gpu = 0;   // the GPU the model stands for (== dev, except under MGCM_AMD_DEVICES=virtual)
   hipEvent_t ev = nullptr;   // cross-model barriers
 };
 // The halo sources model s's tiles deliver to model d (sorted 2-D offsets, the same on both
@@ -226,11 +226,12 @@ void hipchk(hipError_t e, const char *where) {
 }
 hipStream_t stream_of(const Shard &s) { return (hipStream_t)mgcm_get_stream(s.m); }
 
-// MGCM_AMD_CAPTURE_DEBUG=1: each stage of a multi-model capture and replay printed (and the
+// MGCM_AMD_CAPTURE=debug: each stage of a multi-model capture and replay printed (and the
 // replay waited for), down to the device operations of the captured drop-ins, to place a
 // fault inside the runtime
+bool cap_opt(const char *tok);
 bool cap_dbg_on() {
-  static const bool on = getenv("MGCM_AMD_CAPTURE_DEBUG") && atoi(getenv("MGCM_AMD_CAPTURE_DEBUG")) != 0;
+  static const bool on = cap_opt("debug");
   return on;
 }
 void cap_dbg(const char *what, int q) {
@@ -240,8 +241,24 @@ void cap_op(const char *what, int model) {
   if (cap_dbg_on() && g.capturing) { fprintf(stderr, "MGCM_AMD   op %s model %d\n", what, model); fflush(stderr); }
 }
 
+// MGCM_AMD_CAPTURE: comma-separated options of the multi-model step capture -- "multi" (each
+// model keeps its own stream in the capture; default: all on model 0's), "relaxed" (capture
+// mode), "nopool" (events re-recorded instead of one per record), "debug" (stage prints)
+bool cap_opt(const char *tok) {
+  const char *e = getenv("MGCM_AMD_CAPTURE");
+  if (!e) return false;
+  const size_t n = strlen(tok);
+  for (const char *p = e; *p;) {
+    const char *c = strchr(p, ',');
+    const size_t len = c ? (size_t)(c - p) : strlen(p);
+    if (len == n && !strncmp(p, tok, n)) return true;
+    if (!c) break;
+    p = c + 1;
+  }
+  return false;
+}
 bool cap_pool_on() {
-  static const bool off = getenv("MGCM_AMD_CAPTURE_POOL") && atoi(getenv("MGCM_AMD_CAPTURE_POOL")) == 0;
+  static const bool off = cap_opt("nopool");
   return !off;
 }
 // the event a record on device `dev` uses: outside a capture (or with the pool off) the
@@ -283,6 +300,7 @@ void run_all(const char *where, int (*fn)(mgcm_model *)) {
     hipchk(hipSetDevice(s.dev), where);
     if (fn(s.m)) die(where);
   }
+  cap_op("(issued)", -1);
 }
 void phase_all(const char *where, int phase) {
   for (size_t i = 0; i < g.sh.size(); i++) {
@@ -821,6 +839,7 @@ void run_recorded_step(const char *w, int myIter) {
 // model 0's stream waits for every other model's work so far (join), or every other model's
 // stream for model 0's (fork)
 void join_into_0(const char *w) {
+  cap_op("join into model 0", -1);
   std::vector<hipEvent_t> ev(g.sh.size());
   for (size_t i = 1; i < g.sh.size(); i++) {
     hipchk(hipSetDevice(g.sh[i].dev), w);
@@ -859,9 +878,8 @@ bool multi_replay(const char *w, int myIter) {
     hipStream_t s0 = stream_of(g.sh[0]);
     // MGCM_AMD_CAPTURE=multi: every model keeps its own stream in the capture (the graph then
     // has a branch per model, joined at the exchange points); default: one stream
-    static const bool multiStream = getenv("MGCM_AMD_CAPTURE") && !strcmp(getenv("MGCM_AMD_CAPTURE"), "multi");
-    static const hipStreamCaptureMode mode = getenv("MGCM_AMD_CAPTURE_MODE") &&
-        !strcmp(getenv("MGCM_AMD_CAPTURE_MODE"), "relaxed") ? hipStreamCaptureModeRelaxed : hipStreamCaptureModeGlobal;
+    static const bool multiStream = cap_opt("multi");
+    static const hipStreamCaptureMode mode = cap_opt("relaxed") ? hipStreamCaptureModeRelaxed : hipStreamCaptureModeGlobal;
     fill_pools(4096, w);
     // every model issues on model 0's stream while capturing: the graph is one chain of the
     // models' work in the recorded order (graphs captured across two or more streams of one GPU
@@ -1124,7 +1142,17 @@ void mgcm_amd_setup_(const int *sNx, const int *sNy, const int *OLx, const int *
   if (N < 1 || N > nt) die("MGCM_AMD_SETUP", "MGCM_AMD_MODELS must be 1 .. the number of tiles (or auto)");
   std::vector<int> devs((size_t)N);
   for (int i = 0; i < N; i++) devs[i] = (int)(((long)i * ndev) / N);   // contiguous blocks of models per GPU
-  if (const char *e = getenv("MGCM_AMD_DEVICES")) {
+  // MGCM_AMD_DEVICES=virtual[:ids] (test hook): the GPU ids are logical -- every model runs on
+  // device 0, but the models are grouped, sharded, solved and stepped exactly as on that many
+  // GPUs (per-GPU CG2D leads, cross-GPU copies, the multi-GPU step and its segment graphs), so
+  // the code an 8-GPU node runs is exercised on one; "virtual" alone: one GPU per model
+  const char *dv = getenv("MGCM_AMD_DEVICES");
+  const bool virt = dv && !strncmp(dv, "virtual", 7);
+  if (virt) {
+    for (int i = 0; i < N; i++) devs[i] = i;
+    dv = dv[7] == ':' ? dv + 8 : nullptr;
+  }
+  if (const char *e = dv) {
     std::string l(e);
     size_t pos = 0;
     for (int i = 0; i < N; i++) {
@@ -1132,17 +1160,9 @@ void mgcm_amd_setup_(const int *sNx, const int *sNy, const int *OLx, const int *
       const size_t c = l.find(',', pos);
       devs[i] = atoi(l.substr(pos, c == std::string::npos ? std::string::npos : c - pos).c_str());
       pos = c == std::string::npos ? l.size() + 1 : c + 1;
-      const bool virtIds = getenv("MGCM_AMD_VIRTUAL_GPUS") && atoi(getenv("MGCM_AMD_VIRTUAL_GPUS")) != 0;
-      if (devs[i] < 0 || (!virtIds && devs[i] >= ndev)) die("MGCM_AMD_SETUP", "MGCM_AMD_DEVICES names a GPU that does not exist");
+      if (devs[i] < 0 || (!virt && devs[i] >= ndev)) die("MGCM_AMD_SETUP", "MGCM_AMD_DEVICES names a GPU that does not exist");
     }
   }
-  // MGCM_AMD_VIRTUAL_GPUS=1 (test hook): the GPU ids above are logical -- every model runs on
-  // device 0, but the models are grouped, sharded, solved and stepped exactly as on that many
-  // GPUs (per-GPU CG2D leads, cross-GPU copies, the routine-by-routine multi-GPU step), so the
-  // code an 8-GPU node runs is exercised on one
-  const bool virt = getenv("MGCM_AMD_VIRTUAL_GPUS") && atoi(getenv("MGCM_AMD_VIRTUAL_GPUS")) != 0;
-  if (virt && !getenv("MGCM_AMD_DEVICES"))
-    for (int i = 0; i < N; i++) devs[i] = i;   // one logical GPU per model
   for (int i = 0; i < N; i++) {
     Shard s;
     s.gpu = devs[i];

@@ -1967,7 +1967,7 @@ __device__ __forceinline__ double vi_h0S_own(const VIM2<BX, BY, P, OWN, HR> &a, 
   do {              \
   } while (0)
 #endif
-template <int BX, int BY, unsigned C, bool PF, bool CREG, bool EARLY, int LBW, bool SPLIT>
+template <int BX, int BY, unsigned C, bool PF, bool CREG, bool EARLY, int LBW>
 __global__ void __launch_bounds__(VT_NT, LBW) k_mom_vi_m2(Dims d, VIP<C> p, Fields f, const int *iterPtr, int nbx, int nby,
                                                       int KC, int nkc) {
   using P = VIP<C>;
@@ -2175,8 +2175,10 @@ __global__ void __launch_bounds__(VT_NT, LBW) k_mom_vi_m2(Dims d, VIP<C> p, Fiel
       const double recip_drF = a.rdrFk;
       // one component at a time (CC 1: U, 2: V): tendency, AB2, store, each from its own
       // vecinv_tend call whose other outputs are dead (the compiler drops their arithmetic;
-      // the common reads are shared).  SPLIT: a scheduling barrier between the two, so the
-      // halves' live values do not overlap (215 against 247 VGPRs at 2 waves per SIMD)
+      // the common reads are shared), a scheduling barrier between the two so the halves' live
+      // values do not overlap: 215 against 247 VGPRs at 2 waves per SIMD, LLC-90's VI 319-320
+      // against 323.7-323.8 us with both chains interleaved (round 6, profiles/r06/ab_hr_vi/);
+      // capped for 3 waves per SIMD the split form still spills 43 VGPRs (605 us)
       auto comp = [&](auto tagC) {
         constexpr int CC = decltype(tagC)::value;   // 1: U, 2: V
         double gU = 0.0, gV = 0.0, guDiss = 0.0, gvDiss = 0.0, dPhiHydX = 0.0, dPhiHydY = 0.0;
@@ -2229,7 +2231,7 @@ __global__ void __launch_bounds__(VT_NT, LBW) k_mom_vi_m2(Dims d, VIP<C> p, Fiel
         else AR3(gV, q3) = a.vVel(i, j, k) + p.deltaTMom * (gtmp + 0.0) * a.maskS(i, j, k);
       };
       comp(std::integral_constant<int, 1>{});
-      if constexpr (SPLIT) __builtin_amdgcn_sched_barrier(0);   // U's chain before V's
+      __builtin_amdgcn_sched_barrier(0);   // U's chain before V's
       comp(std::integral_constant<int, 2>{});
     }
     VI_STAMP(3);
@@ -2308,8 +2310,7 @@ constexpr unsigned VI_CODE_LLC = vi_code(1, 0, 0, 1, 1, 1, 0, 1, 1, 0, 1, 1, 1, 
 template <int BX, int BY, unsigned C, int V>
 static void vi_m2_one(const Dims &d, const VIP<C> &vp, const Fields &f, const int *iterPtr, int nbx, int nby, int KC,
                       int nkc, hipStream_t s) {
-  hipLaunchKernelGGL((k_mom_vi_m2<BX, BY, C, (V & 1) != 0, (V & 2) != 0, (V & 4) != 0, (V & 32) ? 3 : (V & 8) ? 2 : 1,
-                                   (V & 16) != 0>),
+  hipLaunchKernelGGL((k_mom_vi_m2<BX, BY, C, (V & 1) != 0, (V & 2) != 0, (V & 4) != 0, (V & 8) ? 2 : 1>),
                      dim3((unsigned)(nbx * nby * d.nT * nkc)), dim3(VT_NT), 0, s, d, vp, f, iterPtr, nbx, nby, KC, nkc);
 }
 // k_mom_vi_m2 as launched: the output point's metrics held in registers across the march
@@ -2324,21 +2325,12 @@ static void vi_m2_one(const Dims &d, const VIP<C> &vp, const Fields &f, const in
 static bool vi_m2_launch(const Dims &d, const Params &p, const Fields &f, const int *iterPtr, int BX, int BY, int nbx,
                          int nby, int KC, int nkc, hipStream_t s) {
   const unsigned code = vi_opt_code(p);
-  // MGCM_VI_SPLIT: 1 (default) U's chain then V's, 2 waves per SIMD (215 VGPRs: LLC-90's VI
-  // 319-320 against 323.7-323.8 us interleaved, profiles/r06/ab_hr_vi/); 0 both chains
-  // interleaved (247 VGPRs); 3 U then V capped for 3 waves per SIMD (43 VGPRs spilled: 605 us)
-  const char *se = getenv("MGCM_VI_SPLIT");
-  const int split = se ? atoi(se) : 1;
   if (code == VI_CODE_LLC && BX == 31 && BY == 8) {
-    if (split == 3) vi_m2_one<31, 8, VI_CODE_LLC, 2 | 4 | 16 | 32>(d, vi_params<VI_CODE_LLC>(p), f, iterPtr, nbx, nby, KC, nkc, s);
-    else if (split == 1) vi_m2_one<31, 8, VI_CODE_LLC, 14 | 16>(d, vi_params<VI_CODE_LLC>(p), f, iterPtr, nbx, nby, KC, nkc, s);
-    else vi_m2_one<31, 8, VI_CODE_LLC, 14>(d, vi_params<VI_CODE_LLC>(p), f, iterPtr, nbx, nby, KC, nkc, s);
+    vi_m2_one<31, 8, VI_CODE_LLC, 14>(d, vi_params<VI_CODE_LLC>(p), f, iterPtr, nbx, nby, KC, nkc, s);
     return true;
   }
   if (code == VI_CODE_LLC && BX == 32 && BY == 8) {
-    if (split == 3) vi_m2_one<32, 8, VI_CODE_LLC, 2 | 4 | 16 | 32>(d, vi_params<VI_CODE_LLC>(p), f, iterPtr, nbx, nby, KC, nkc, s);
-    else if (split == 1) vi_m2_one<32, 8, VI_CODE_LLC, 14 | 16>(d, vi_params<VI_CODE_LLC>(p), f, iterPtr, nbx, nby, KC, nkc, s);
-    else vi_m2_one<32, 8, VI_CODE_LLC, 14>(d, vi_params<VI_CODE_LLC>(p), f, iterPtr, nbx, nby, KC, nkc, s);
+    vi_m2_one<32, 8, VI_CODE_LLC, 14>(d, vi_params<VI_CODE_LLC>(p), f, iterPtr, nbx, nby, KC, nkc, s);
     return true;
   }
   return false;

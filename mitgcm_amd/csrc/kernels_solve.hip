@@ -834,6 +834,10 @@ __device__ __forceinline__ double block_max_nw(double v, double *red, int slot) 
 // SR: CG2D_SR (cg2d_sr.F, useSRCGSolver) -- one standard step, then per iteration y = M r,
 // v = A y and the three sums (y.r, y.v, r.r) in one reduction: three barriers per iteration
 // (y, the reduction, r) instead of four; s_l holds y.
+// (round 6 measured k_cg2d_hr, the same blocks with two barriers per iteration -- every
+// thread advancing its own copies of the out-of-block neighbours' s and r from the q = M r and
+// A s the owners publish before the reductions, aC / pC in LDS: bit-identical, 1.705 against
+// 1.64 us/iteration, 20-26 VGPRs spilled; removed, profiles/r06/ab_hr_vi/)
 // (round 5 measured lifting the s- and r-update barriers by re-deriving the out-of-block
 // neighbours' s_n = beta*s_{n-1} + M r and r_n = r_{n-1} - alpha*A s from values published
 // before the reductions: bit-identical, but the extra live values spill -- 2.89-4.30 against
@@ -1248,270 +1252,6 @@ __global__ void __launch_bounds__(NT) k_cg2d_bxy(Dims d, Params p, Fields f, con
     R.sumRHS = sumRHS;
     R.numIters = actualIts;
     R.nIterMin = nIterMin;
-  }
-}
-
-// ---------------------------------------------------------------------------
-// k_cg2d_hr<BX, BY, NT, FMA>: k_cg2d_bxy's standard iteration with TWO workgroup barriers
-// per iteration instead of four -- the two global sums (cg2d.F:211-243 / 321-337; one of
-// them carrying the previous residual norm) -- and no barrier for the width-1 halo
-// exchanges of s and r (cg2d.F:260,337).  Every thread keeps its own copy of the
-// out-of-block neighbours' s and r (sH, rH: 2(BX+BY) values each) and advances them with the
-// owner's own expressions, s = q + beta*s and r = r - alpha*(A s), from the q = M r and A s
-// the owners publish to LDS (qL, aL) before the reduction barrier that follows them: the
-// copies are the owners' values bit for bit, so the iterates, the sums (mgcm_cg2d_sum_plan,
-// unchanged: the same threads, points and trees as k_cg2d_bxy) and the exit are
-// k_cg2d_bxy's.  aC / pC (read once per operator row) live in LDS, which frees the
-// registers the copies take (2 waves per SIMD, 256 VGPRs).  Tables: k_cg2d_bxy's (nbx,
-// blkx); the standard solver without the minimum-residual solution (otherwise bxy runs).
-template <int BX, int BY, int NT, bool FMA>
-__global__ void __launch_bounds__(NT) k_cg2d_hr(Dims d, Params p, Fields f, const unsigned *__restrict__ nbx,
-                                                const int *__restrict__ blkx, int nBlk, int maxIters, SolveRecord *rec,
-                                                int *stepCounter, const int *__restrict__ slot2,
-                                                const long *__restrict__ srcOf) {
-  constexpr int NPT = BX * BY, NP = NPT * NT, NB = 2 * (BX + BY), NW = NT / 64;
-  extern __shared__ __attribute__((aligned(16))) double lds[];
-  double *qL = lds;                  // NP + 1 (last = ZERO slot): M r (and x, r at the start)
-  double *aL = lds + (NP + 1);       // NP + 1: A s
-  double *cA = lds + 2 * (NP + 1);   // NP: aC by slot
-  double *cP = cA + NP;              // NP: pC by slot
-  double *red = cP + NP;             // 4 x 16 partial slots
-  const int tid = threadIdx.x;
-  const bool act = tid < nBlk;
-  const int bt = act ? tid : 0;
-  const double az = act ? 1.0 : 0.0;
-  // slot of point (b, a) of this thread: (BX*b + a)*NT + tid (point-major, conflict-free)
-  auto cs = [&](int b, int a) { return (BX * b + a) * NT + tid; };
-  unsigned nbp[NB / 2];
-#pragma unroll
-  for (int q = 0; q < NB / 2; q++) nbp[q] = nbx[(NB / 2) * bt + q];
-  auto nbi = [&](int q) -> int { return (q & 1) ? (int)(nbp[q >> 1] >> 16) : (int)(nbp[q >> 1] & 0xFFFFu); };
-  double aW[BY][BX + 1], pW[BY][BX + 1], aS[BX][BY + 1], pS[BX][BY + 1];
-  const long nx = d.nx;
-  double x[BY][BX], r[BY][BX], sv[BY][BX], q[BY][BX];
-  double rhsMax = 0.0, sumB = 0.0;
-  {
-    long G[BY][BX];
-#pragma unroll
-    for (int b = 0; b < BY; b++)
-#pragma unroll
-      for (int a = 0; a < BX; a++) G[b][a] = blkx[NPT * bt + BX * b + a];
-#pragma unroll
-    for (int b = 0; b < BY; b++)
-#pragma unroll
-      for (int a = 0; a <= BX; a++) {
-        const long g = a < BX ? G[b][a] : G[b][BX - 1] + 1;
-        aW[b][a] = az * f.aW2d[g];
-        pW[b][a] = az * f.pW[g];
-      }
-#pragma unroll
-    for (int a = 0; a < BX; a++)
-#pragma unroll
-      for (int b = 0; b <= BY; b++) {
-        const long g = b < BY ? G[b][a] : G[BY - 1][a] + nx;
-        aS[a][b] = az * f.aS2d[g];
-        pS[a][b] = az * f.pS[g];
-      }
-#pragma unroll
-    for (int b = 0; b < BY; b++)
-#pragma unroll
-      for (int a = 0; a < BX; a++) {
-        cA[cs(b, a)] = az * f.aC2d[G[b][a]];
-        cP[cs(b, a)] = az * f.pC[G[b][a]];
-        q[b][a] = act ? f.cg2d_b[G[b][a]] : 0.0;   // b (the right-hand side) until r is formed
-        x[b][a] = act ? f.cg2d_x[G[b][a]] : 0.0;
-        sv[b][a] = 0.0;
-      }
-    // cg2d.F:104-133: normalise the RHS
-#pragma unroll
-    for (int b = 0; b < BY; b++)
-#pragma unroll
-      for (int a = 0; a < BX; a++) { q[b][a] = q[b][a] * p.cg2dNorm; rhsMax = fmax(fabs(q[b][a]), rhsMax); }
-  }
-  rhsMax = block_max_nw<NW>(rhsMax, red, 0);
-  double rhsNorm = 1.0;
-  if (p.cg2dNormaliseRHS) {
-    if (rhsMax != 0.0) rhsNorm = 1.0 / rhsMax;
-#pragma unroll
-    for (int b = 0; b < BY; b++)
-#pragma unroll
-      for (int a = 0; a < BX; a++) { q[b][a] = q[b][a] * rhsNorm; x[b][a] = x[b][a] * rhsNorm; }
-  }
-  // one operator row: in-block neighbours from registers, out-of-block ones from nb[] (order
-  // W[0..BY-1], E[0..BY-1], S[0..BX-1], N[0..BX-1]); the centre coefficient from LDS
-  auto apply = [&](const double (&nb)[NB], const double (&v)[BY][BX], double (&out)[BY][BX], bool isM) {
-#pragma unroll
-    for (int b = 0; b < BY; b++)
-#pragma unroll
-      for (int a = 0; a < BX; a++) {
-        const double w = a > 0 ? v[b][a - 1] : nb[b];
-        const double e = a < BX - 1 ? v[b][a + 1] : nb[BY + b];
-        const double so = b > 0 ? v[b - 1][a] : nb[2 * BY + a];
-        const double no = b < BY - 1 ? v[b + 1][a] : nb[2 * BY + BX + a];
-        const double cc = isM ? cP[cs(b, a)] : cA[cs(b, a)];
-        if (FMA) {
-          if (isM)
-            out[b][a] = __builtin_fma(pS[a][b + 1], no, __builtin_fma(pS[a][b], so, __builtin_fma(pW[b][a + 1], e,
-                                      __builtin_fma(pW[b][a], w, cc * v[b][a]))));
-          else
-            out[b][a] = __builtin_fma(cc, v[b][a], __builtin_fma(aS[a][b + 1], no, __builtin_fma(aS[a][b], so,
-                                      __builtin_fma(aW[b][a + 1], e, aW[b][a] * w))));
-        } else if (isM)
-          out[b][a] = cc * v[b][a] + pW[b][a] * w + pW[b][a + 1] * e + pS[a][b] * so + pS[a][b + 1] * no;
-        else
-          out[b][a] = aW[b][a] * w + aW[b][a + 1] * e + aS[a][b] * so + aS[a][b + 1] * no + cc * v[b][a];
-      }
-  };
-  auto publish = [&](double *arr, const double (&v)[BY][BX]) {
-#pragma unroll
-    for (int b = 0; b < BY; b++)
-#pragma unroll
-      for (int a = 0; a < BX; a++) arr[cs(b, a)] = v[b][a];
-  };
-  double sH[NB], rH[NB];
-  // r = b - A x: x's out-of-block neighbours through qL
-  publish(qL, x);
-  if (tid == 0) { qL[NP] = 0.0; aL[NP] = 0.0; }
-  __syncthreads();   // (also orders the cA / cP stores before their first reads)
-#pragma unroll
-  for (int h = 0; h < NB; h++) sH[h] = qL[nbi(h)];   // x's neighbours, for the one product below
-  double err = 0.0;
-  {
-    double ax[BY][BX];
-    apply(sH, x, ax, false);
-#pragma unroll
-    for (int b = 0; b < BY; b++)
-#pragma unroll
-      for (int a = 0; a < BX; a++) {
-        const double bv = q[b][a];
-        r[b][a] = bv - ax[b][a];
-        err = FMA ? __builtin_fma(r[b][a], r[b][a], err) : err + r[b][a] * r[b][a];
-        sumB = sumB + bv;
-      }
-  }
-  if (act) {   // the normalised right-hand side back, as cg2d.F leaves it
-    for (int b = 0; b < BY; b++)
-      for (int a = 0; a < BX; a++) f.cg2d_b[blkx[NPT * bt + BX * b + a]] = q[b][a];
-  }
-  publish(aL, r);   // r's neighbours for the first M r (aL is free until the first A s)
-  double err_sq = block_sum_nw<NW>(err, red, 1);   // also fences qL's x reads and aL's r stores
-  const double sumRHS = block_sum_nw<NW>(sumB, red, 2);
-#pragma unroll
-  for (int h = 0; h < NB; h++) { rH[h] = aL[nbi(h)]; sH[h] = 0.0; }
-  const double firstResidual = sqrt(err_sq);
-  int actualIts = 0;
-  double eta_qrNM1 = 1.0;
-  if (!(err_sq < p.cg2dTolerance_sq)) {
-    apply(rH, r, q, true);
-    double e = 0.0;
-#pragma unroll
-    for (int b = 0; b < BY; b++)
-#pragma unroll
-      for (int a = 0; a < BX; a++) e = FMA ? __builtin_fma(q[b][a], r[b][a], e) : e + q[b][a] * r[b][a];
-    publish(qL, q);   // x's reads of qL are behind the barriers above
-    double eta_qrN = block_sum_nw<NW>(e, red, 0);
-    int aslot = 2;
-    auto iter = [&](int it2d) -> bool {
-      const double cgBeta = eta_qrN / eta_qrNM1;
-      eta_qrNM1 = eta_qrN;
-      // s = q + beta*s on the own points and, from the owners' published q, on the copies
-#pragma unroll
-      for (int b = 0; b < BY; b++)
-#pragma unroll
-        for (int a = 0; a < BX; a++) sv[b][a] = FMA ? __builtin_fma(cgBeta, sv[b][a], q[b][a]) : q[b][a] + cgBeta * sv[b][a];
-#pragma unroll
-      for (int h = 0; h < NB; h++) {
-        const double qn = qL[nbi(h)];
-        sH[h] = FMA ? __builtin_fma(cgBeta, sH[h], qn) : qn + cgBeta * sH[h];
-      }
-      apply(sH, sv, q, false);   // q = A s
-      double aa = 0.0;
-#pragma unroll
-      for (int b = 0; b < BY; b++)
-#pragma unroll
-        for (int a = 0; a < BX; a++) aa = FMA ? __builtin_fma(sv[b][a], q[b][a], aa) : aa + sv[b][a] * q[b][a];
-      publish(aL, q);
-      aslot = aslot ^ 1;
-      double alpha = block_sum_nw<NW>(aa, red, aslot);
-      alpha = eta_qrN / alpha;
-      double e2 = 0.0;
-#pragma unroll
-      for (int b = 0; b < BY; b++)
-#pragma unroll
-        for (int a = 0; a < BX; a++) {
-          x[b][a] = FMA ? __builtin_fma(alpha, sv[b][a], x[b][a]) : x[b][a] + alpha * sv[b][a];
-          r[b][a] = FMA ? __builtin_fma(-alpha, q[b][a], r[b][a]) : r[b][a] - alpha * q[b][a];
-          e2 = FMA ? __builtin_fma(r[b][a], r[b][a], e2) : e2 + r[b][a] * r[b][a];
-        }
-#pragma unroll
-      for (int h = 0; h < NB; h++) {
-        const double an = aL[nbi(h)];
-        rH[h] = FMA ? __builtin_fma(-alpha, an, rH[h]) : rH[h] - alpha * an;
-      }
-      actualIts = it2d;
-      // next iteration's q = M r and (q, r), reduced together with this iteration's r.r
-      apply(rH, r, q, true);
-      double en = 0.0;
-#pragma unroll
-      for (int b = 0; b < BY; b++)
-#pragma unroll
-        for (int a = 0; a < BX; a++) en = FMA ? __builtin_fma(q[b][a], r[b][a], en) : en + q[b][a] * r[b][a];
-      publish(qL, q);
-      block_sum2_nw<NW>(e2, en, red, 0);
-      err_sq = e2;
-      eta_qrN = en;
-      return err_sq < p.cg2dTolerance_sq;
-    };
-    bool done = false;
-    int it2d = 1;
-    for (; !done && it2d + 1 <= maxIters; it2d += 2) done = iter(it2d) || iter(it2d + 1);
-    if (!done && it2d <= maxIters) iter(it2d);
-  }
-  if (slot2) {
-    // SOLVE_FOR_PRESSURE's EXCH_XY_RL(cg2d_x) + etaN as the epilogue (as k_cg2d_bxy): the
-    // solution through LDS, then every 2-D point takes its own value or its source's
-    __syncthreads();
-#pragma unroll
-    for (int b = 0; b < BY; b++)
-#pragma unroll
-      for (int a = 0; a < BX; a++) {
-        double xv = x[b][a];
-        if (p.cg2dNormaliseRHS) xv = xv / rhsNorm;
-        if (act) qL[cs(b, a)] = xv;
-      }
-    __syncthreads();
-    const long n2 = d.n2 * d.nTiles;
-    for (long qq = tid; qq < n2; qq += NT) {
-      const int sl = slot2[qq];
-      double xq;
-      if (sl >= 0) xq = qL[sl];
-      else {
-        const long sq = srcOf[qq];
-        xq = f.cg2d_x[sq >= 0 ? sq : qq];
-      }
-      f.cg2d_x[qq] = xq;
-      f.etaN[qq] = f.recip_Bo[qq] * xq;
-    }
-  } else if (act) {
-#pragma unroll
-    for (int b = 0; b < BY; b++)
-#pragma unroll
-      for (int a = 0; a < BX; a++) {
-        double xv = x[b][a];
-        if (p.cg2dNormaliseRHS) xv = xv / rhsNorm;
-        f.cg2d_x[blkx[NPT * bt + BX * b + a]] = xv;
-      }
-  }
-  if (tid == 0) {
-    const int st = stepCounter ? *stepCounter : 0;
-    SolveRecord &R = rec[st];
-    R.firstResidual = firstResidual;
-    R.lastResidual = sqrt(err_sq);
-    R.minResidualSq = -1.0;
-    R.rhsMax = rhsMax;
-    R.sumRHS = sumRHS;
-    R.numIters = actualIts;
-    R.nIterMin = -1;
   }
 }
 
@@ -1998,37 +1738,12 @@ int cg2d_bxy_geometry(int v, int *bx, int *by, int *nt) {
   *bx = CGX[v].bx; *by = CGX[v].by; *nt = CGX[v].nt;
   return 0;
 }
-// k_cg2d_hr in place of k_cg2d_bxy (MGCM_CG2D_HR=1, opt-in) for the standard solver (no
-// CG2D_SR, no minimum-residual solution) in the 2 x 4 x 512 geometry.  Measured slower on
-// config 2 (round 6: 1.705 against 1.64 us/iteration, profiles/r06/ab_hr/): the barriers it
-// removes cost less than the halo copies' LDS reads, the centre coefficients read from LDS
-// and the 20-26 VGPRs it spills -- the iteration is bound by its two reductions' latency
-// chains and the f64 VALU, not by the halo barriers
-bool cg2d_hr_on(int BX, int BY, int NT, bool sr, bool mr) {
-  const char *e = getenv("MGCM_CG2D_HR");
-  if (!e || atoi(e) == 0) return false;
-  return BX == 2 && BY == 4 && NT == 512 && !sr && !mr;
-}
 template <int BX, int BY, int NT>
 static hipError_t launch_bxy_t(const Dims &d, const Params &p, const Fields &f, const unsigned *nbx, const int *blkx,
                                int nBlk, int maxIters, int nIterMin, SolveRecord *rec, int *stepCounter, const int *slot2,
                                const long *srcOf, hipStream_t s) {
   if (nBlk > NT) return hipErrorInvalidValue;
   const bool mr = nIterMin >= 0, fm = p.cg2dUseFMA != 0, sr = p.useSRCGSolver != 0;
-  if constexpr (BX == 2 && BY == 4 && NT == 512) {
-  if (cg2d_hr_on(BX, BY, NT, sr, mr)) {   // the two-barrier iteration (k_cg2d_hr)
-    const size_t lds = (2 * ((size_t)BX * BY * NT + 1) + 2 * (size_t)BX * BY * NT + 4 * 16) * sizeof(double);
-    auto kern = fm ? k_cg2d_hr<BX, BY, NT, true> : k_cg2d_hr<BX, BY, NT, false>;
-    static bool hrAttr[2] = {false, false};
-    if (!hrAttr[fm]) {
-      hipError_t e = hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-      if (e != hipSuccess) return e;
-      hrAttr[fm] = true;
-    }
-    hipLaunchKernelGGL(kern, dim3(1), dim3(NT), lds, s, d, p, f, nbx, blkx, nBlk, maxIters, rec, stepCounter, slot2, srcOf);
-    return hipGetLastError();
-  }
-  }
   const size_t lds = (2 * ((size_t)BX * BY * NT + 1) + 4 * 16) * sizeof(double);
   auto kern = sr   ? (mr ? (fm ? k_cg2d_bxy<BX, BY, NT, true, true, true> : k_cg2d_bxy<BX, BY, NT, true, false, true>)
                          : (fm ? k_cg2d_bxy<BX, BY, NT, false, true, true>

@@ -1308,10 +1308,12 @@ hipError_t launch_oceanic_phys(const Dims &d, const Params &p, const Fields &f, 
 }
 
 // the implicit solve's forward sweep fused into a whole-column march (k_tracer_march2<true> +
-// k_tracer_backsub): MGCM_TRACER_FWD=1 (read per launch)
+// k_tracer_backsub): MGCM_TRACER_MARCH=2 (read per launch).  Round 6: per tracer 171 + 47 us
+// against 161 + 105 (march + implicit solve), but LLC-90's step 1.239 against 1.233 ms -- the
+// tracers run beside the pressure solve there, which bounds the step -- so not the default
 static bool tracer_fwd_on() {
-  const char *e = getenv("MGCM_TRACER_FWD");
-  return e && atoi(e) != 0;
+  const char *e = getenv("MGCM_TRACER_MARCH");
+  return e && atoi(e) == 2;
 }
 static bool tracer_march_on(const Dims &d) {
   const char *e = getenv("MGCM_TRACER_MARCH");   // read per launch (tests switch it per model)
@@ -1361,7 +1363,7 @@ hipError_t launch_tracer_step(const Dims &d, const Params &p, const Fields &f, c
         al(f.vVel) && al(f.hFacW) && al(f.hFacS) && al(f.recip_hFacC) && (!a.multiDim || al(f.gAdv))) {
       const int TY = 256 / hx, nty2 = (d.sNy + TY - 1) / TY;
       // the implicit solve's forward elimination inside a whole-column march, then the back
-      // substitution (MGCM_TRACER_FWD=1; tracer_fwd_on): no T* round trip
+      // substitution (MGCM_TRACER_MARCH=2; tracer_fwd_on): no T* round trip
       if (impl && p.implicitDiffusion && !p.useGMRedi && tracer_fwd_on() && !a.multiDim && a.cp && al(a.cp) && d.Nr > 1) {
         hipLaunchKernelGGL(k_tracer_march2<true>, dim3((unsigned)(nty2 * d.nT)), blk, 0, s, d, p, f, a, iterPtr, d.Nr, 1,
                            nty2);

@@ -66,7 +66,6 @@ int cg2d_ref_max_points();
 hipError_t launch_cg2d_bxy(int, const Dims &, const Params &, const Fields &, const unsigned *, const int *, int, int,
                            int, SolveRecord *, int *, const int *, const long *, hipStream_t);
 int cg2d_bxy_geometry(int, int *, int *, int *);
-bool cg2d_hr_on(int, int, int, bool, bool);
 int cg2d_bxy_variants();
 hipError_t launch_cg2d_blk2(const Dims &, const Params &, const Fields &, const unsigned *, const int *, int, int, int,
                             SolveRecord *, int *, hipStream_t);
@@ -998,17 +997,9 @@ double mgcm_get_param(mgcm_model *m, const char *name) {
       return NAN;
     return it;
   }
-  // 6: k_cg2d_hr (k_cg2d_bxy's tables, two barriers per iteration), 5: k_cg2d_block in the
-  // reference order (cg2dRefOrder), 4: k_cg2d_mwg, 3: k_cg2d_bxy, 2: k_cg2d_blk2, 1: k_cg2d_block
-  if (!strcmp(name, "cg2dKernel")) {
-    if (!m->p.cg2dRefOrder && !m->useMwg && m->nBlkX > 0) {
-      int bx, by, nt;
-      if (!cg2d_bxy_geometry(m->bxyVar, &bx, &by, &nt) &&
-          cg2d_hr_on(bx, by, nt, m->p.useSRCGSolver != 0, m->p.cg2dUseMinResSol - 1 >= 0))
-        return 6.0;
-    }
+  // 5: k_cg2d_block in the reference order (cg2dRefOrder), 4: k_cg2d_mwg, 3: k_cg2d_bxy, 2: k_cg2d_blk2, 1: k_cg2d_block
+  if (!strcmp(name, "cg2dKernel"))
     return m->p.cg2dRefOrder ? 5.0 : m->useMwg ? 4.0 : m->nBlkX > 0 ? 3.0 : (m->nBlk > 0 ? 2.0 : 1.0);
-  }
   if (!strcmp(name, "cg2dParts")) return m->useMwg ? (double)m->mwg.G : 1.0;
   // 1 when the multi-workgroup solve's parts are placed on one XCD (one L2: ~1 us hand-offs)
   if (!strcmp(name, "cg2dPinned")) return m->useMwg ? (double)m->mwg.pinned : 0.0;

@@ -196,12 +196,11 @@ class Model:
         return plan[:nt.value * ppt.value * ng.value].copy(), nt.value, ppt.value, ng.value
 
     def cg2d_kernel(self):
-        """Which CG2D kernel mgcm_init selected: 'mwg' (multi-workgroup), 'hr' (k_cg2d_bxy's 2 x 4 blocks with
-        two barriers per iteration, opt-in MGCM_CG2D_HR=1), 'bxy' (BX x BY points/thread),
+        """Which CG2D kernel mgcm_init selected: 'mwg' (multi-workgroup), 'bxy' (BX x BY points/thread),
         'blk2' (2x2), 'block', or 'block_ref' (k_cg2d_block summing in the reference's order,
         cg2dRefOrder)."""
         k = lib().mgcm_get_param(self.h, b"cg2dKernel")
-        return {6.0: "hr", 5.0: "block_ref", 4.0: "mwg", 3.0: "bxy", 2.0: "blk2"}.get(k, "block")
+        return {5.0: "block_ref", 4.0: "mwg", 3.0: "bxy", 2.0: "blk2"}.get(k, "block")
 
     def step_layout(self):
         """The launch layout of the last step built (mgcm_get_param 'stepLayout'): which

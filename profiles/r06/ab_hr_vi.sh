@@ -1,4 +1,6 @@
 #!/bin/bash
+# (historical: MGCM_CG2D_HR and MGCM_VI_SPLIT were removed after this A/B -- k_cg2d_hr
+# measured slower and was dropped, the VI U-then-V split became the only form)
 # Round 6 A/B: CG2D k_cg2d_hr vs k_cg2d_bxy on config 2; VI U/V split variants on LLC-90.
 # Parity first (the tests that cover both), then alternating bench runs.
 set -o pipefail

@@ -1,4 +1,5 @@
 #!/bin/bash
+# (historical: MGCM_AMD_CAPTURE_POOL=0 is now MGCM_AMD_CAPTURE=multi,nopool)
 # Round 6: (1) k_cg2d_bxy per-phase s_memtime stamps on config 2 (diagnostic library);
 # (2) the multi-model step captured across the models' own streams with per-record events
 # (MGCM_AMD_CAPTURE=multi), 4 and 6 models, bit-identical to the one-stream graph;

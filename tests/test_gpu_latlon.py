@@ -102,17 +102,14 @@ def test_latlon_20_steps_vs_reference_output(golden_dir):
     m.close()
 
 
-@pytest.mark.parametrize("hr", ["1", "0"])
-def test_cg2d_bxy_vs_oracle(hr, monkeypatch):
-    """The 2x4-points-per-thread solvers for the 90x40 grid -- k_cg2d_bxy (the default) and
-    k_cg2d_hr (two barriers per iteration, MGCM_CG2D_HR=1) -- on the lat-lon operator:
-    same iteration count, first residual within 1e-12 relative, solution within 1e-12 of
-    max|x|."""
+def test_cg2d_bxy_vs_oracle():
+    """The 2x4-points-per-thread solver (k_cg2d_bxy, chosen for the 90x40 grid) on the
+    lat-lon operator: same iteration count, first residual within 1e-12 relative,
+    solution within 1e-12 of max|x|."""
     from mitgcm_amd import configs
-    monkeypatch.setenv("MGCM_CG2D_HR", hr)
     o, g = _stepped_oracle(0)
     m = configs.make_model(configs.global_oce_latlon)
-    assert m.cg2d_kernel() == ("hr" if hr == "1" else "bxy")
+    assert m.cg2d_kernel() == "bxy"
     rng = np.random.default_rng(11)
     b = np.zeros((g.nTiles, g.ny, g.nx))
     inner = g.sl(1, g.sNx, 1, g.sNy)

@@ -111,18 +111,15 @@ def test_ocean90_dynamics_bitexact():
     assert not bad, bad
 
 
-@pytest.mark.parametrize("variant", [None, "layout2", "fork", "phiflat", "ff4", "hr"])
+@pytest.mark.parametrize("variant", [None, "layout2", "fork", "phiflat", "ff4"])
 def test_ocean90_10_steps(golden_dir, monkeypatch, variant):
     """variant None: the default step (THERMODYNAMICS' tracer kernels folded into DYNAMICS'
     launches, kernels_step.hip, with GMREDI_CALC_TENSOR in the first of them); "layout2": the
     fold's front/back layout (MGCM_DT_LAYOUT=2); "fork": the tracers on the second stream
     beside DYNAMICS (MGCM_STEP_FUSE without MG_FUSE_DT); "phiflat": CALC_PHI_HYD's flat
     per-column pass with the r* and quasi-hydrostatic operands (MGCM_PHI_FLAT=2); "ff4": the
-    momentum with four threads per point inside the fused grid (MGCM_MOM_FF4=2); "hr": the CG2D
-    as k_cg2d_hr (two barriers per iteration, halo copies advanced by every reader;
-    MGCM_CG2D_HR=1) instead of the default k_cg2d_bxy (four) -- the same sum plan, so both equal
-    the device-order oracle bit for bit.  The overlap is forced on, so neither depends on
-    the auto-selection's timing."""
+    momentum with four threads per point inside the fused grid (MGCM_MOM_FF4=2).  The overlap is
+    forced on, so neither depends on the auto-selection's timing."""
     monkeypatch.setenv("MGCM_OVERLAP", "1")
     if variant == "fork":
         monkeypatch.setenv("MGCM_STEP_FUSE", "13")
@@ -132,11 +129,9 @@ def test_ocean90_10_steps(golden_dir, monkeypatch, variant):
         monkeypatch.setenv("MGCM_PHI_FLAT", "2")
     if variant == "ff4":
         monkeypatch.setenv("MGCM_MOM_FF4", "2")
-    if variant == "hr":
-        monkeypatch.setenv("MGCM_CG2D_HR", "1")
     o, g = _oracle(0)            # reference summation order
     m = _model()
-    assert m.cg2d_kernel() == ("hr" if variant == "hr" else "bxy")
+    assert m.cg2d_kernel() == "bxy"
     plan, NT, PPT, NG = m.cg2d_sum_plan()
     od_dev, _ = _oracle(0)       # the device's summation order
     fma = m.cg2d_fma()

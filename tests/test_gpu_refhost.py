@@ -479,14 +479,17 @@ def test_refhost_multistream_capture(layout, models, tmp_path):
     assert len(outs["one"]) >= 18
 
 
-# The drop-ins' multi-GPU path on the one GPU of the test box (MGCM_AMD_VIRTUAL_GPUS=1: the
+# The drop-ins' multi-GPU path on the one GPU of the test box (MGCM_AMD_DEVICES=virtual: the
 # models stand for that many GPUs but all run on device 0): per-GPU CG2D leads, the
 # cross-GPU copies of the gathered right-hand side and solution, the halo-source links, and
 # the step the drop-ins run when the models span GPUs -- the per-GPU segment graphs replayed
 # with event barriers between segments (seg_replay), and routine by routine (MGCM_AMD_EAGER=1)
 # -- the code an 8-GPU node runs, bit-identical to one model; mwg = 1: the multi-workgroup
 # CG2D launched once per "GPU" on one shared hand-off block.  Both forms' ms/step recorded.
-@pytest.mark.parametrize("layout,models,mwg", [("ref", 2, 0), ("ref", 4, 0), ("cs32_6t", 6, 0), ("cs32_6t", 3, 1)])
+# (the cube's CG2D is the multi-workgroup solve whatever mwg says: its per-"GPU" launches must
+# run together on the one device, so at most GPU_MAX_HW_QUEUES (4 on the box) virtual GPUs --
+# on a real node each GPU has its own queues)
+@pytest.mark.parametrize("layout,models,mwg", [("ref", 2, 0), ("ref", 4, 0), ("cs32_6t", 2, 0), ("cs32_6t", 3, 1)])
 def test_refhost_virtual_gpus(layout, models, mwg, tmp_path):
     from mitgcm_amd import configs
     exe = os.path.join(RH, "refhost_" + layout)
@@ -512,8 +515,10 @@ def test_refhost_virtual_gpus(layout, models, mwg, tmp_path):
     m.close()
     outs, times = {}, {}
     for tag, n, virt, eager in (("one", 1, "0", "0"), ("seg", models, "1", "0"), ("eager", models, "1", "1")):
-        env = dict(os.environ, MGCM_AMD_MODELS=str(n), MGCM_AMD_VIRTUAL_GPUS=virt, MGCM_CG2D_MWG=str(mwg),
-                   MGCM_AMD_EAGER=eager, MGCM_AMD_CAPTURE_DEBUG="1")
+        env = dict(os.environ, MGCM_AMD_MODELS=str(n), MGCM_CG2D_MWG=str(mwg), MGCM_AMD_EAGER=eager,
+                   MGCM_AMD_CAPTURE="debug")
+        if virt == "1":
+            env["MGCM_AMD_DEVICES"] = "virtual"
         r = subprocess.run([exe, str(tmp_path), pdir], capture_output=True, text=True, timeout=300, env=env)
         assert r.returncode == 0, (tag, r.returncode, r.stdout + r.stderr)
         if tag == "seg":   # the segment graphs were captured and replayed (no fallback to eager)
