@@ -4,7 +4,10 @@
 // barriers cross the streams, every stream joins back, then hipStreamEndCapture, instantiate,
 // launch, synchronise.  Prints each stage; pass N and B on the command line.
 //   hipcc --offload-arch=gfx950 -O2 tools/capture_repro.hip -o tools/capture_repro
-//   tools/capture_repro N B
+//   tools/capture_repro N B [kc|k|c] [global|relaxed]
+// The third argument keeps the kernels (k), the copies (c) or both (kc, default); the fourth
+// picks the capture mode.
+#include <cstring>
 #include <hip/hip_runtime.h>
 #include <cstdio>
 #include <cstdlib>
@@ -26,6 +29,9 @@ __global__ void k_axpy(double *y, const double *x, int n) {
 
 int main(int argc, char **argv) {
   const int N = argc > 1 ? atoi(argv[1]) : 4, B = argc > 2 ? atoi(argv[2]) : 4, n = 1 << 16;
+  const char *what = argc > 3 ? argv[3] : "kc";
+  const bool kern = strchr(what, 'k') != nullptr, copy = strchr(what, 'c') != nullptr;
+  const bool relaxed = argc > 4 && strcmp(argv[4], "relaxed") == 0;
   std::vector<hipStream_t> s(N);
   std::vector<double *> a(N), b(N);
   for (int i = 0; i < N; i++) {
@@ -43,16 +49,16 @@ int main(int argc, char **argv) {
     return e;
   };
   CK(hipDeviceSynchronize());
-  printf("N=%d B=%d: begin capture\n", N, B);
+  printf("N=%d B=%d %s %s: begin capture\n", N, B, what, relaxed ? "relaxed" : "global");
   fflush(stdout);
-  CK(hipStreamBeginCapture(s[0], hipStreamCaptureModeGlobal));
+  CK(hipStreamBeginCapture(s[0], relaxed ? hipStreamCaptureModeRelaxed : hipStreamCaptureModeGlobal));
   hipEvent_t f = newev();
   CK(hipEventRecord(f, s[0]));
   for (int i = 1; i < N; i++) CK(hipStreamWaitEvent(s[i], f, 0));
   for (int r = 0; r < B; r++) {
     for (int i = 0; i < N; i++) {
-      hipLaunchKernelGGL(k_axpy, dim3(n / 256), dim3(256), 0, s[i], a[i], b[i], n);
-      CK(hipMemcpyAsync(b[(i + 1) % N], a[i], n * sizeof(double), hipMemcpyDeviceToDevice, s[i]));
+      if (kern) hipLaunchKernelGGL(k_axpy, dim3(n / 256), dim3(256), 0, s[i], a[i], b[i], n);
+      if (copy) CK(hipMemcpyAsync(b[(i + 1) % N], a[i], n * sizeof(double), hipMemcpyDeviceToDevice, s[i]));
     }
     std::vector<hipEvent_t> e(N);
     for (int i = 0; i < N; i++) {
