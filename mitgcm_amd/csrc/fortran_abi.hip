@@ -150,6 +150,7 @@ struct FortranSide {
     std::vector<int> pre, post;   // every model's tracer parity before / after the captured step
   } mg[4];
   bool capturing = false;     // set_iter inside a capture: device increments, not values
+  bool capMulti = false;      // ... with every model on its own stream (MGCM_AMD_CAPTURE=multi)
   // Events recorded inside a multi-model capture: with the pool on (the default), every
   // record of a captured step takes an event of its own from evPool (filled before the
   // capture, kept for the graphs' life), so no hipEvent_t is recorded twice in one graph
@@ -241,8 +242,9 @@ void cap_op(const char *what, int model) {
   if (cap_dbg_on() && g.capturing) { fprintf(stderr, "MGCM_AMD   op %s model %d\n", what, model); fflush(stderr); }
 }
 
-// MGCM_AMD_CAPTURE: comma-separated options of the multi-model step capture -- "multi" (each
-// model keeps its own stream in the capture; default: all on model 0's), "relaxed" (capture
+// MGCM_AMD_CAPTURE: comma-separated options of the multi-model step capture -- "multi" / "one"
+// (each model keeps its own stream in the capture / all on model 0's; default: multi from 4
+// models on), "relaxed" (capture
 // mode), "nopool" (events re-recorded instead of one per record), "debug" (stage prints)
 bool cap_opt(const char *tok) {
   const char *e = getenv("MGCM_AMD_CAPTURE");
@@ -314,10 +316,38 @@ void phase_all(const char *where, int phase) {
 // Cross-model barrier on the device: every model's stream waits for the work every other
 // model has issued so far (no host synchronisation).
 void seg_boundary(const char *where);
+__global__ void k_capture_join() {}
 void barrier_all(const char *where) {
   if (!multi()) return;
   if (g.segMode) return seg_boundary(where);   // segmented capture: the barrier is a cut
   cap_op("barrier", -1);
+  if (g.capturing && g.capMulti) {
+    // captured across the models' streams: through model 0 -- it waits for every other model,
+    // runs an empty kernel, and every other model waits for that.  The all-to-all form below,
+    // captured over 4 or more streams, makes hipStreamEndCapture fault (SIGSEGV inside the HIP
+    // runtime, ROCm 7.2) -- reproduced by tools/capture_repro.hip alone, with kernels only and
+    // one barrier; fan-in, fan-out and this gather form capture and replay at 4 and 6 streams
+    // (profiles/r06/cap_repro/)
+    const Shard &s0 = g.sh[0];
+    for (size_t i = 1; i < g.sh.size(); i++) {
+      const Shard &s = g.sh[i];
+      hipchk(hipSetDevice(s.dev), where);
+      const hipEvent_t e = rec_event(s.dev, s.ev, where);
+      hipchk(hipEventRecord(e, stream_of(s)), where);
+      hipchk(hipSetDevice(s0.dev), where);
+      hipchk(hipStreamWaitEvent(stream_of(s0), e, 0), where);
+    }
+    hipchk(hipSetDevice(s0.dev), where);
+    hipLaunchKernelGGL(k_capture_join, dim3(1), dim3(64), 0, stream_of(s0));
+    hipchk(hipGetLastError(), where);
+    const hipEvent_t e0 = rec_event(s0.dev, s0.ev, where);
+    hipchk(hipEventRecord(e0, stream_of(s0)), where);
+    for (size_t i = 1; i < g.sh.size(); i++) {
+      hipchk(hipSetDevice(g.sh[i].dev), where);
+      hipchk(hipStreamWaitEvent(stream_of(g.sh[i]), e0, 0), where);
+    }
+    return;
+  }
   std::vector<hipEvent_t> ev(g.sh.size());
   for (size_t i = 0; i < g.sh.size(); i++) {
     const Shard &s = g.sh[i];
@@ -366,7 +396,11 @@ void xfer3d(const char *where, int group) {
   barrier_all(where);
   cap_op("xfer3d", group);
   const int Nr = g.dims[4];
-  if (g.segMode) {   // the senders' packs and copies, a cut, then the receivers' unpacks
+  if (g.segMode || (g.capturing && g.capMulti)) {
+    // the senders' packs and copies, a cut (segmented capture) or a barrier through model 0
+    // (multi-stream capture: per-link events over 6 streams -- each model waiting for its 4
+    // cube neighbours -- fault the runtime's capture as the all-to-all barrier does), then the
+    // receivers' unpacks
     for (auto &L : g.links) {
       const Shard &a = g.sh[L.s];
       const int nf = mgcm_exchange_nfields_group(a.m, group);
@@ -377,7 +411,7 @@ void xfer3d(const char *where, int group) {
                             stream_of(a)),
              where);
     }
-    seg_boundary(where);
+    barrier_all(where);   // (a segment cut under segMode)
     for (auto &L : g.links) {
       const Shard &b = g.sh[L.d];
       const int nf = mgcm_exchange_nfields_group(b.m, group);
@@ -876,18 +910,17 @@ bool multi_replay(const char *w, int myIter) {
   if (!G.exec) {
     G.pre = pre;
     hipStream_t s0 = stream_of(g.sh[0]);
-    // MGCM_AMD_CAPTURE=multi: every model keeps its own stream in the capture (the graph then
-    // has a branch per model, joined at the exchange points); default: one stream
-    static const bool multiStream = cap_opt("multi");
+    // every model keeps its own stream in the capture (the graph then has a branch per model,
+    // joined at the exchange points) from 4 models on, or with MGCM_AMD_CAPTURE=multi; else (or
+    // with MGCM_AMD_CAPTURE=one) every model issues on model 0's stream.  Config 2's 36 tiles
+    // over 60 steps (test_refhost_dropin_throughput): 4 models 0.76 against 1.42 ms/step, 6
+    // models 1.35 against 3.40, 2 models 0.63 against 0.61 (profiles/r06/cap_repro/)
+    const bool multiStream = cap_opt("multi") || (!cap_opt("one") && g.sh.size() >= 4);
     static const hipStreamCaptureMode mode = cap_opt("relaxed") ? hipStreamCaptureModeRelaxed : hipStreamCaptureModeGlobal;
     fill_pools(4096, w);
-    // every model issues on model 0's stream while capturing: the graph is one chain of the
-    // models' work in the recorded order (graphs captured across two or more streams of one GPU
-    // faulted in the HIP runtime's own threads -- SIGSEGV, no host frame -- once 4 or more models
-    // were in them, with any grouping of the models onto 2, 3 or 6 streams and with chained or
-    // all-to-all barriers; with 2 or 3 models they replayed correctly but no faster than the
-    // one-stream graph: 0.60 against 0.58 ms/step at 2 models, 0.74-0.88 against 0.83 at 3,
-    // profiles/r05/capture_ab/)
+    // one stream: the graph is one chain of the models' work in the recorded order.  The
+    // multi-stream form's barriers go through model 0 (barrier_all: the runtime's capture of an
+    // all-to-all event barrier over 4 or more streams faults)
     if (!multiStream)
       for (size_t i = 1; i < g.sh.size(); i++)
         if (mgcm_set_stream(g.sh[i].m, s0)) die(w);
@@ -900,11 +933,12 @@ bool multi_replay(const char *w, int myIter) {
     }
     cap_dbg("begin capture", q);
     g.capturing = true;   // (the pool's events from here: the fork's record is the capture's first node)
+    g.capMulti = multiStream;
     fork_from_0(w);
     g.devIter = myIter;   // the graph's increments are relative to this
     run_recorded_step(w, myIter);
     join_into_0(w);
-    g.capturing = false;
+    g.capturing = g.capMulti = false;
     cap_dbg("joined; ending capture", q);
     hipGraph_t gr = nullptr;
     hipchk(hipSetDevice(g.sh[0].dev), w);

@@ -206,10 +206,13 @@ def test_refhost_mods_dropins_bitexact(layout, refOrder, models, mwg, eager, pac
 # after the run is bit-identical to the resident graph path's; both rates are recorded
 # (INTEGRATION.md section 3).  models > 1: the 36 tiles over that many device models of the
 # one GPU, every step after the recorded one ONE replay of the graph captured across the
-# models' streams.
-@pytest.mark.parametrize("io,register,models", [("namelist", 1, 1), ("off", 1, 1), ("namelist", 0, 1), ("off", 1, 2),
-                                                ("off", 1, 3), ("off", 1, 4)])
-def test_refhost_dropin_throughput(io, register, models, tmp_path):
+# models' own streams (the default from 4 models on, cap = "multi") or with every model on model
+# 0's stream (the default below 4, cap = "one").
+@pytest.mark.parametrize("io,register,models,cap", [("namelist", 1, 1, ""), ("off", 1, 1, ""), ("namelist", 0, 1, ""),
+                                                    ("off", 1, 2, ""), ("off", 1, 3, ""), ("off", 1, 4, ""),
+                                                    ("off", 1, 6, ""), ("off", 1, 2, "multi"), ("off", 1, 4, "one"),
+                                                    ("off", 1, 6, "one")])
+def test_refhost_dropin_throughput(io, register, models, cap, tmp_path):
     from mitgcm_amd import configs
     nsteps = 60
     exe = os.path.join(RH, "refhost_ref")
@@ -218,7 +221,7 @@ def test_refhost_dropin_throughput(io, register, models, tmp_path):
     extra = [("dumpFreq", 0.0)] if io == "off" else []
     state = _write_blob(tmp_path / "refhost_in.bin", m, nsteps, monitor_days=10 * nsteps, extra=extra)
     env = dict(os.environ, MGCM_AMD_MODELS=str(models), MGCM_AMD_EAGER="0", MGCM_AMD_STEP_FENCE="0",
-               MGCM_AMD_REGISTER=str(register))
+               MGCM_AMD_REGISTER=str(register), MGCM_AMD_CAPTURE=cap)
     r = subprocess.run([exe, str(tmp_path), PARAM_DIR], capture_output=True, text=True, timeout=300, env=env)
     assert r.returncode == 0, r.stdout + r.stderr
     out, st = _read_out(tmp_path / "refhost_out.bin", state, nsteps)
@@ -233,6 +236,7 @@ def test_refhost_dropin_throughput(io, register, models, tmp_path):
            if n in out and not np.array_equal(out[n], m.get(n).reshape(-1)[:out[n].size])]
     m.close()
     rec = {"steps": nsteps, "io": io, "register": register, "models": models,
+           "capture": cap or ("multi" if models >= 4 else "one"),
            "dropin_ms_per_step": 1e3 * st["seconds"] / max(1, st["steps_timed"]),
            "graph_ms_per_step": graph_ms, "uploads": st["uploads"], "downloads": st["downloads"],
            "bytes_down": st["bytes_down"],
@@ -241,7 +245,7 @@ def test_refhost_dropin_throughput(io, register, models, tmp_path):
            "host_side_step_ms": [round(x, 4) for x in st["step_ms"]]}
     print("refhost throughput: %s" % json.dumps(rec))
     if os.path.isdir(os.path.join(ROOT, "gpurun_out")):
-        with open(os.path.join(ROOT, "gpurun_out", "refhost_throughput_%s_r%d_m%d.json" % (io, register, models)), "w") as f:
+        with open(os.path.join(ROOT, "gpurun_out", "refhost_throughput_%s_r%d_m%d%s.json" % (io, register, models, "_" + cap if cap else "")), "w") as f:
             json.dump(rec, f)
     assert not bad, bad
     # the state came down after steps 10, 20, ..., 60 (dumpFreq) or after the last only
@@ -441,14 +445,14 @@ def test_refhost_llc30_exch2_bitexact(models, eager, tmp_path):
     assert st["downloads"] == 2 * len(state), (st, len(state))
 
 
-# The multi-model step captured across the models' own streams (MGCM_AMD_CAPTURE=multi: one
-# graph branch per model, joined at every exchange point) instead of on one stream (the
-# default), with every record of the captured step on an event of its own (fortran_abi.hip
-# rec_event): bit-identical to the one-stream graph at 2 and 3 models.  From 4 models on this
-# form dies with SIGSEGV inside the HIP runtime while the capture is being recorded (round 6
-# diagnosis; profiles/r06/cap_diag/), whatever the event handling, capture
-# mode or runtime queue settings -- the one-stream capture the drop-ins use is unaffected.
-@pytest.mark.parametrize("layout,models", [("ref", 2), ("ref", 3), ("cs32_6t", 3)])
+# The multi-model step captured across the models' own streams (MGCM_AMD_CAPTURE=multi, the
+# default from 4 models on: one graph branch per model, joined at every exchange point through
+# model 0 -- barrier_all's gather form) against on one stream (MGCM_AMD_CAPTURE=one), with
+# every record of the captured step on an event of its own (fortran_abi.hip rec_event):
+# bit-identical at 2, 3, 4 and 6 models.  (An all-to-all event barrier captured over 4 or more
+# streams makes hipStreamEndCapture fault inside the HIP runtime -- tools/capture_repro.hip
+# reproduces it without the library; DESIGN.md section 5, profiles/r06/cap_repro/.)
+@pytest.mark.parametrize("layout,models", [("ref", 2), ("ref", 3), ("ref", 4), ("cs32_6t", 3), ("cs32_6t", 6)])
 def test_refhost_multistream_capture(layout, models, tmp_path):
     from mitgcm_amd import configs
     exe = os.path.join(RH, "refhost_" + layout)
@@ -466,9 +470,8 @@ def test_refhost_multistream_capture(layout, models, tmp_path):
     m.close()
     outs, times = {}, {}
     for mode in ("one", "multi"):
-        env = dict(os.environ, MGCM_AMD_MODELS=str(models), MGCM_AMD_EAGER="0", MGCM_CG2D_MWG="0")
-        if mode == "multi":
-            env["MGCM_AMD_CAPTURE"] = "multi"
+        env = dict(os.environ, MGCM_AMD_MODELS=str(models), MGCM_AMD_EAGER="0", MGCM_CG2D_MWG="0",
+                   MGCM_AMD_CAPTURE=mode)
         r = subprocess.run([exe, str(tmp_path), pdir], capture_output=True, text=True, timeout=300, env=env)
         assert r.returncode == 0, (mode, r.returncode, r.stdout + r.stderr)
         outs[mode], st = _read_out(tmp_path / "refhost_out.bin", state, nsteps)
