@@ -994,21 +994,28 @@ void seg_begin(const char *w) {
     }
   }
 }
-// close every group's capture into the open segment's graphs
+// close every group's capture into the open segment's graphs.  A group with nothing captured
+// since the last cut gets no graph (nothing launched); a segment empty on every group is
+// dropped -- the barriers either side of it are then one (two cuts in a row: the barrier after
+// one gather and the one before the next)
 void seg_end(const char *w) {
   std::vector<hipGraphExec_t> cur(g.cgLeads.size(), nullptr);
+  bool any = false;
   for (size_t j = 0; j < g.cgLeads.size(); j++) {
     hipchk(hipSetDevice(lead_dev(j)), w);
     hipGraph_t gr = nullptr;
     hipError_t e = hipStreamEndCapture(lead_stream(j), &gr);
-    if (e == hipSuccess) e = hipGraphInstantiate(&cur[j], gr, nullptr, nullptr, 0);
+    size_t nn = 0;
+    if (e == hipSuccess) e = hipGraphGetNodes(gr, nullptr, &nn);
+    if (e == hipSuccess && nn > 0) e = hipGraphInstantiate(&cur[j], gr, nullptr, nullptr, 0);
     if (gr) (void)hipGraphDestroy(gr);
     if (e != hipSuccess) {
       (void)hipGetLastError();
       g.segFail = true;
     }
+    any = any || nn > 0;
   }
-  g.segAll.push_back(cur);
+  if (any) g.segAll.push_back(cur);
 }
 void seg_boundary(const char *w) {
   cap_op("segment cut", (int)g.segAll.size());
@@ -1099,6 +1106,7 @@ bool seg_replay(const char *w, int myIter) {
   for (size_t k = 0; k < S.seg.size(); k++) {
     if (k > 0) group_barrier(w);
     for (size_t j = 0; j < G; j++) {
+      if (!S.seg[k][j]) continue;   // nothing of this GPU's in the segment
       hipchk(hipSetDevice(lead_dev(j)), w);
       hipchk(hipGraphLaunch(S.seg[k][j], lead_stream(j)), w);
     }

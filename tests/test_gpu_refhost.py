@@ -207,11 +207,14 @@ def test_refhost_mods_dropins_bitexact(layout, refOrder, models, mwg, eager, pac
 # (INTEGRATION.md section 3).  models > 1: the 36 tiles over that many device models of the
 # one GPU, every step after the recorded one ONE replay of the graph captured across the
 # models' own streams (the default from 4 models on, cap = "multi") or with every model on model
-# 0's stream (the default below 4, cap = "one").
+# 0's stream (the default below 4, cap = "one"); cap = "virtual": the models stand for that
+# many GPUs, all on device 0 (MGCM_AMD_DEVICES=virtual) -- the per-GPU segment graphs, or
+# routine by routine ("virtual-eager").
 @pytest.mark.parametrize("io,register,models,cap", [("namelist", 1, 1, ""), ("off", 1, 1, ""), ("namelist", 0, 1, ""),
                                                     ("off", 1, 2, ""), ("off", 1, 3, ""), ("off", 1, 4, ""),
                                                     ("off", 1, 6, ""), ("off", 1, 2, "multi"), ("off", 1, 4, "one"),
-                                                    ("off", 1, 6, "one")])
+                                                    ("off", 1, 6, "one"), ("off", 1, 2, "virtual"),
+                                                    ("off", 1, 4, "virtual"), ("off", 1, 4, "virtual-eager")])
 def test_refhost_dropin_throughput(io, register, models, cap, tmp_path):
     from mitgcm_amd import configs
     nsteps = 60
@@ -221,7 +224,9 @@ def test_refhost_dropin_throughput(io, register, models, cap, tmp_path):
     extra = [("dumpFreq", 0.0)] if io == "off" else []
     state = _write_blob(tmp_path / "refhost_in.bin", m, nsteps, monitor_days=10 * nsteps, extra=extra)
     env = dict(os.environ, MGCM_AMD_MODELS=str(models), MGCM_AMD_EAGER="0", MGCM_AMD_STEP_FENCE="0",
-               MGCM_AMD_REGISTER=str(register), MGCM_AMD_CAPTURE=cap)
+               MGCM_AMD_REGISTER=str(register), MGCM_AMD_CAPTURE=cap if cap in ("one", "multi") else "")
+    if cap.startswith("virtual"):
+        env.update(MGCM_AMD_DEVICES="virtual", MGCM_AMD_EAGER="1" if cap == "virtual-eager" else "0")
     r = subprocess.run([exe, str(tmp_path), PARAM_DIR], capture_output=True, text=True, timeout=300, env=env)
     assert r.returncode == 0, r.stdout + r.stderr
     out, st = _read_out(tmp_path / "refhost_out.bin", state, nsteps)
@@ -236,7 +241,7 @@ def test_refhost_dropin_throughput(io, register, models, cap, tmp_path):
            if n in out and not np.array_equal(out[n], m.get(n).reshape(-1)[:out[n].size])]
     m.close()
     rec = {"steps": nsteps, "io": io, "register": register, "models": models,
-           "capture": cap or ("multi" if models >= 4 else "one"),
+           "capture": cap or ("multi" if models >= 4 else "one"),  # virtual: segment graphs per "GPU"
            "dropin_ms_per_step": 1e3 * st["seconds"] / max(1, st["steps_timed"]),
            "graph_ms_per_step": graph_ms, "uploads": st["uploads"], "downloads": st["downloads"],
            "bytes_down": st["bytes_down"],
@@ -517,7 +522,7 @@ def test_refhost_virtual_gpus(layout, models, mwg, tmp_path):
         w2 = m.g.topo.w2_arrays(ldNb=8, ldT=2 * m.g.nTiles)
         state = _write_blob(tmp_path / "refhost_in.bin", m, nsteps, monitor_days=2, w2=w2, undef=("ALLOW_CD_CODE",))
     m.close()
-    outs, times = {}, {}
+    outs, times, nseg = {}, {}, []
     for tag, n, virt, eager in (("one", 1, "0", "0"), ("seg", models, "1", "0"), ("eager", models, "1", "1")):
         env = dict(os.environ, MGCM_AMD_MODELS=str(n), MGCM_CG2D_MWG=str(mwg), MGCM_AMD_EAGER=eager,
                    MGCM_AMD_CAPTURE="debug")
@@ -527,11 +532,13 @@ def test_refhost_virtual_gpus(layout, models, mwg, tmp_path):
         assert r.returncode == 0, (tag, r.returncode, r.stdout + r.stderr)
         if tag == "seg":   # the segment graphs were captured and replayed (no fallback to eager)
             assert "segments x %d GPUs" % models in r.stderr and "routine by routine" not in r.stderr, r.stderr[-2000:]
+            nseg = [int(ln.split()[2]) for ln in r.stderr.splitlines() if ln.endswith("segments x %d GPUs" % models)]
         outs[tag], st = _read_out(tmp_path / "refhost_out.bin", state, nsteps)
         times[tag] = st["step_ms"]
     bad = [(t, k) for t in ("seg", "eager") for k in CHECK
            if k in outs["one"] and not np.array_equal(outs["one"][k], outs[t][k])]
-    rec = {"layout": layout, "virtual_gpus": models, "mwg": mwg, "step_ms_1_model": times["one"],
+    rec = {"layout": layout, "virtual_gpus": models, "mwg": mwg, "segments_per_parity": nseg,
+           "step_ms_1_model": times["one"],
            "step_ms_segment_graphs": times["seg"], "step_ms_eager": times["eager"]}
     print("refhost virtual GPUs: %s" % json.dumps(rec))
     if os.path.isdir(os.path.join(ROOT, "gpurun_out")):
