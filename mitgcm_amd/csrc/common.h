@@ -269,15 +269,18 @@ inline unsigned mg_colf_blocks(long ncols, int nc) { return (unsigned)((ncols + 
 // second stream beside them (kernels_step.hip; early fork only, small grids), MG_FUSE_ETAX
 // no separate EXCH(cg2d_x) + etaN under exactConserv (one_step), MG_FUSE_OPE UPDATE_CG2D's
 // operator and preconditioner in the fold's first two grids (ucg2d.h; r*, with MG_FUSE_DT),
-// MG_FUSE_RING the VI path's halo-ring AB2 on the tracers' stream (late fork, one_step).
+// MG_FUSE_RING the VI path's halo-ring AB2 on the tracers' stream (late fork, one_step),
+// MG_FUSE_RINGP that ring in DO_OCEANIC_PHYS's grid instead where there is no late fork
+// (k_phys_ring: the staggered cube), MG_FUSE_ENDS CALC_R_STAR and
+// DO_STAGGER_FIELDS_EXCHANGES' u, v, w in one grid (k_rstar_exmix: the staggered cube).
 enum { MG_FUSE_SFP = 1, MG_FUSE_ETA = 2, MG_FUSE_PHI = 4, MG_FUSE_END = 8, MG_FUSE_PHYS = 16, MG_FUSE_ETAA = 32,
        MG_FUSE_TREX = 64, MG_FUSE_DT = 128, MG_FUSE_ETAX = 256, MG_FUSE_TCG = 512, MG_FUSE_OPE = 1024,
-       MG_FUSE_RING = 2048 };
+       MG_FUSE_RING = 2048, MG_FUSE_RINGP = 4096, MG_FUSE_ENDS = 8192 };
 inline bool mg_fuse_on(int bit) {
   // read per call (tests switch it per model)
   const int mask = getenv("MGCM_STEP_FUSE") ? atoi(getenv("MGCM_STEP_FUSE"))
                                             : MG_FUSE_SFP | MG_FUSE_PHI | MG_FUSE_END | MG_FUSE_DT | MG_FUSE_ETAX |
-                                                MG_FUSE_OPE | MG_FUSE_RING;
+                                                MG_FUSE_OPE | MG_FUSE_RING | MG_FUSE_RINGP | MG_FUSE_ENDS;
   return (mask & bit) != 0;
 }
 // Horizontal launch fusion of two independent latency-bound kernels into one grid: on the
@@ -343,6 +346,35 @@ __device__ __forceinline__ void exchange_multi_body(const Dims &d, const XFields
                                                     int nHalo, int *ctr, int hb, int k, int fi) {
   const int h = hb * (int)blockDim.x + (int)threadIdx.x;
   if (ctr && h == 0 && k == 0 && fi == 0) { ctr[0] += 1; ctr[1] += 1; }
+  if (h >= nHalo || fi >= x.n || k >= x.nz[fi]) return;
+  const long dst = map[2 * h], src = map[2 * h + 1];
+  const long dt = dst / d.n2, dl = dst % d.n2, st = src / d.n2, sl = src % d.n2;
+  const long lvl = (long)d.n2 * x.nz[fi];
+  double *a = x.p[fi];
+  a[dt * lvl + (long)k * d.n2 + dl] = a[st * lvl + (long)k * d.n2 + sl];
+}
+
+// k_exchange_mixed's copies for one (halo block hb, level k, slice z) of its grid: z = 0 the
+// vector pair u, v through the vector map (codes: +-(source+1), v's sources offset by the
+// 2-D size of every tile), z = 1.. the scalar field z-1 through the scalar map; the block
+// (0,0,0) advances the step counters when ctr is given.
+__device__ __forceinline__ void exchange_mixed_body(const Dims &d, double *u, double *v, int nzUV,
+                                                    const long *__restrict__ uvMap, int nU, int nV, const XFields &x,
+                                                    const long *__restrict__ map, int nHalo, int *ctr, int hb, int k,
+                                                    int z) {
+  const int h = hb * (int)blockDim.x + (int)threadIdx.x;
+  if (ctr && h == 0 && k == 0 && z == 0) { ctr[0] += 1; ctr[1] += 1; }
+  if (z == 0) {
+    if (h >= nU + nV || k >= nzUV) return;
+    const long dst = uvMap[2 * h], code = uvMap[2 * h + 1];
+    const long N2 = d.n2 * d.nTiles, s = (code > 0 ? code : -code) - 1;
+    const long n3 = d.n2 * nzUV, lvl = (long)k * d.n2;
+    auto at = [&](long g) -> long { return (g / d.n2) * n3 + lvl + g % d.n2; };
+    const double val = s < N2 ? u[at(s)] : v[at(s - N2)];
+    (h < nU ? u : v)[at(dst)] = code > 0 ? val : -val;
+    return;
+  }
+  const int fi = z - 1;
   if (h >= nHalo || fi >= x.n || k >= x.nz[fi]) return;
   const long dst = map[2 * h], src = map[2 * h + 1];
   const long dt = dst / d.n2, dl = dst % d.n2, st = src / d.n2, sl = src % d.n2;

@@ -2263,13 +2263,13 @@ __global__ void __launch_bounds__(VT_NT, LBW) k_mom_vi_m2(Dims d, VIP<C> p, Fiel
 // k_mom_step does there.
 // One thread per ring point (blockIdx.y = level, blockIdx.z = tile): the OLy-1 full rows
 // below and above, then the OLx-1 columns left and right of the rows 0..sNy+1.
+static int mom_halo_ring_count_host(const Dims &d) { return 2 * (d.OLy - 1) * d.nx + (d.sNy + 2) * 2 * (d.OLx - 1); }
 __device__ __forceinline__ int mom_halo_ring_count(const Dims &d) {
   return 2 * (d.OLy - 1) * d.nx + (d.sNy + 2) * 2 * (d.OLx - 1);
 }
-__global__ void __launch_bounds__(256) k_mom_halo_ab(Dims d, Params p, Fields f, const int *iterPtr) {
-  const int r = (int)(blockIdx.x * blockDim.x + threadIdx.x);
+__device__ __forceinline__ void mom_halo_ab_at(const Dims &d, const Params &p, const Fields &f, const int *iterPtr, int r,
+                                               int k, int t) {
   if (r >= mom_halo_ring_count(d)) return;
-  const int t = d.t0 + (int)blockIdx.z, k = (int)blockIdx.y + 1;
   const int nb = (d.OLy - 1) * d.nx, cw = 2 * (d.OLx - 1);
   int i, j;
   if (r < 2 * nb) {
@@ -2294,6 +2294,33 @@ __global__ void __launch_bounds__(256) k_mom_halo_ab(Dims d, Params p, Fields f,
   gV = gV + ab;
   AR3(gU, q3) = gU;
   AR3(gV, q3) = gV;
+}
+__global__ void __launch_bounds__(256) k_mom_halo_ab(Dims d, Params p, Fields f, const int *iterPtr) {
+  mom_halo_ab_at(d, p, f, iterPtr, (int)(blockIdx.x * blockDim.x + threadIdx.x), (int)blockIdx.y + 1,
+                 d.t0 + (int)blockIdx.z);
+}
+// DO_OCEANIC_PHYS's per-point pass (k_oceanic_phys) with the halo ring's AB2 in extra
+// workgroups of the same grid (nbRing per level and tile, after the nbPhys of the pass): the
+// ring's gU/gV/guNm1/gvNm1 are read and written by nothing else of the step (launch_mom_ring),
+// so its launch may be any of the step's -- one fewer launch on the staggered cube
+// (one_step, MG_FUSE_RINGP)
+__global__ void __launch_bounds__(256) k_phys_ring(Dims d, Params p, Fields f, const int *iterPtr, int nbPhys, int nbRing) {
+  const int lb = mg_xcd_block();
+  if (lb >= nbPhys) {
+    const int l = lb - nbPhys, z = l / nbRing;
+    mom_halo_ab_at(d, p, f, iterPtr, (l % nbRing) * (int)blockDim.x + (int)threadIdx.x, z % d.Nr + 1, d.t0 + z / d.Nr);
+    return;
+  }
+  MG_PLANE_LB(1 - d.OLx, d.nx, 1 - d.OLy, d.ny, z, lb)
+  const int t = d.t0 + z / d.Nr, k = z % d.Nr + 1;
+  oceanic_phys_point(d, p, f, iterPtr, i, j, k, t);
+}
+hipError_t launch_phys_ring(const Dims &d, const Params &p, const Fields &f, const int *iterPtr, hipStream_t s) {
+  const unsigned nbPhys = mg_plane_blocks(d.nx, d.ny, d.nT * d.Nr);
+  const int nbRing = (mom_halo_ring_count_host(d) + 255) / 256;
+  hipLaunchKernelGGL(k_phys_ring, dim3(nbPhys + (unsigned)(nbRing * d.Nr * d.nT)), dim3(256), 0, s, d, p, f, iterPtr,
+                     (int)nbPhys, nbRing);
+  return hipGetLastError();
 }
 
 // k_mom_vi_m2's instantiations: (BX, BY, option code) of the workloads that run the k-march

@@ -109,6 +109,21 @@ __global__ void __launch_bounds__(256) k_rstar_exch(Dims d, Params p, Fields f, 
   exchange_multi_body(d, x, map, nHalo, ctr, r % nbX, (r / nbX) % nzMax, r / (nbX * nzMax));
 }
 
+// CALC_R_STAR (with EXCH(eta) + UPDATE_ETAH, FUSE) on the first nbR blocks and
+// DO_STAGGER_FIELDS_EXCHANGES (k_exchange_mixed's nbH x nz x (1 + x.n) grid, flattened: the
+// vector pair u, v and the scalar fields) on the rest, in one grid -- independent: CALC_R_STAR
+// reads eta and writes the 2-D r* factors, the exchanges copy u, v, w's halos
+template <bool FUSE>
+__global__ void __launch_bounds__(256) k_rstar_exmix(Dims d, Params p, Fields f, const long *__restrict__ srcOf, int nbR,
+                                                     int fromX, double *u, double *v, int nzUV,
+                                                     const long *__restrict__ uvMap, int nU, int nV, XFields x,
+                                                     const long *__restrict__ map, int nHalo, int nbH, int nzMax) {
+  const int b = (int)blockIdx.x;
+  if (b < nbR) { calc_r_star_body<FUSE>(d, p, f, srcOf, b, fromX); return; }
+  const int r = b - nbR;
+  exchange_mixed_body(d, u, v, nzUV, uvMap, nU, nV, x, map, nHalo, nullptr, r % nbH, (r / nbH) % nzMax, r / (nbH * nzMax));
+}
+
 // UPDATE_R_STAR(.TRUE.) (update_r_star.F:60-92) and UPDATE_CG2D part 1
 // (update_cg2d.F:82-143) in one pass over the columns of every 2-D point (column frame,
 // common.h MG_COLF): each thread rewrites hFac = h0Fac*rStarFac and recip_hFac = 1/hFac
@@ -216,6 +231,21 @@ hipError_t launch_rstar_exch(const Dims &d, const Params &p, const Fields &f, co
   const unsigned nb = (unsigned)(nbR + nbX * nzMax * (x.n > 0 ? x.n : 1));
   hipLaunchKernelGGL(fuseEtaH ? k_rstar_exch<true> : k_rstar_exch<false>, dim3(nb), dim3(256), 0, s, d, p, f, srcOf, nbR, x,
                      map, nHalo, ctr, nbX, nzMax, fromX);
+  return hipGetLastError();
+}
+
+hipError_t launch_rstar_exmix(const Dims &d, const Params &p, const Fields &f, const long *srcOf, bool fuseEtaH, int fromX,
+                              double *u, double *v, int nzUV, const long *uvMap, int nU, int nV, const XFields &x,
+                              const long *map, int nHalo, hipStream_t s) {
+  const long n = d.n2 * d.nTiles;
+  const int nbR = (int)((n + 255) / 256);
+  int nzMax = nzUV;
+  for (int q = 0; q < x.n; q++) nzMax = x.nz[q] > nzMax ? x.nz[q] : nzMax;
+  const int nh = (nU + nV) > nHalo ? nU + nV : nHalo;
+  const int nbH = ((nh > 0 ? nh : 1) + 255) / 256;
+  const unsigned nb = (unsigned)(nbR + nbH * nzMax * (1 + x.n));
+  hipLaunchKernelGGL(fuseEtaH ? k_rstar_exmix<true> : k_rstar_exmix<false>, dim3(nb), dim3(256), 0, s, d, p, f, srcOf, nbR,
+                     fromX, u, v, nzUV, uvMap, nU, nV, x, map, nHalo, nbH, nzMax);
   return hipGetLastError();
 }
 

@@ -1337,26 +1337,7 @@ __global__ void __launch_bounds__(256) k_exchange_uv_pairs(Dims d, UVPairs pr, c
 __global__ void __launch_bounds__(256) k_exchange_mixed(Dims d, double *u, double *v, int nzUV,
                                                         const long *__restrict__ uvMap, int nU, int nV, XFields x,
                                                         const long *__restrict__ map, int nHalo, int *ctr) {
-  const int h = (int)(blockIdx.x * blockDim.x + threadIdx.x);
-  const int k = (int)blockIdx.y, z = (int)blockIdx.z;
-  if (ctr && h == 0 && k == 0 && z == 0) { ctr[0] += 1; ctr[1] += 1; }
-  if (z == 0) {
-    if (h >= nU + nV || k >= nzUV) return;
-    const long dst = uvMap[2 * h], code = uvMap[2 * h + 1];
-    const long N2 = d.n2 * d.nTiles, s = (code > 0 ? code : -code) - 1;
-    const long n3 = d.n2 * nzUV, lvl = (long)k * d.n2;
-    auto at = [&](long g) -> long { return (g / d.n2) * n3 + lvl + g % d.n2; };
-    const double val = s < N2 ? u[at(s)] : v[at(s - N2)];
-    (h < nU ? u : v)[at(dst)] = code > 0 ? val : -val;
-    return;
-  }
-  const int fi = z - 1;
-  if (h >= nHalo || fi >= x.n || k >= x.nz[fi]) return;
-  const long dst = map[2 * h], src = map[2 * h + 1];
-  const long dt = dst / d.n2, dl = dst % d.n2, st = src / d.n2, sl = src % d.n2;
-  const long lvl = (long)d.n2 * x.nz[fi];
-  double *a = x.p[fi];
-  a[dt * lvl + (long)k * d.n2 + dl] = a[st * lvl + (long)k * d.n2 + sl];
+  exchange_mixed_body(d, u, v, nzUV, uvMap, nU, nV, x, map, nHalo, ctr, (int)blockIdx.x, (int)blockIdx.y, (int)blockIdx.z);
 }
 
 // EXCH_XY_RL(cg2d_x) + etaN = recip_Bo*cg2d_x (solve_for_pressure.F:316, 377-385) in

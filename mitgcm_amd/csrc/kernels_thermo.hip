@@ -1285,7 +1285,11 @@ hipError_t launch_hfac_snapshot(const Dims &d, const Fields &f, double *snap, hi
   return hipGetLastError();
 }
 
-hipError_t launch_oceanic_phys(const Dims &d, const Params &p, const Fields &f, const int *iterPtr, hipStream_t s, bool gm) {
+hipError_t launch_phys_ring(const Dims &d, const Params &p, const Fields &f, const int *iterPtr, hipStream_t s);
+// ringDone non-null: the per-point form takes the VI path's halo-ring AB2 into its grid
+// (k_phys_ring) and sets *ringDone; the 16-byte form does not
+hipError_t launch_oceanic_phys(const Dims &d, const Params &p, const Fields &f, const int *iterPtr, hipStream_t s, bool gm,
+                               bool *ringDone) {
   auto al = [](const void *q) { return ((uintptr_t)q & 15u) == 0; };
   const int v2Env = getenv("MGCM_PHYS_V2") ? atoi(getenv("MGCM_PHYS_V2")) : 1;
   // (large grids only: on config 2's 70 k points per level set, half the threads cost more
@@ -1298,6 +1302,10 @@ hipError_t launch_oceanic_phys(const Dims &d, const Params &p, const Fields &f, 
   if (v2) {
     const unsigned nb = (unsigned)(((d.n2 >> 1) + 255) / 256);
     hipLaunchKernelGGL(k_oceanic_phys2, dim3(nb * (unsigned)(d.nT * d.Nr)), dim3(256), 0, s, d, p, f, iterPtr);
+  } else if (ringDone) {
+    const hipError_t e = launch_phys_ring(d, p, f, iterPtr, s);
+    if (e != hipSuccess) return e;
+    *ringDone = true;
   } else
     hipLaunchKernelGGL(k_oceanic_phys, dim3(mg_plane_blocks(d.nx, d.ny, d.nT * d.Nr)), dim3(MG_PLANE_THREADS), 0, s, d, p,
                        f, iterPtr);

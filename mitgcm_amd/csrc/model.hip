@@ -87,12 +87,15 @@ hipError_t launch_exch_eta(const Dims &, const Params &, const Fields &, const l
 hipError_t launch_corr_cont(const Dims &, const Params &, const Fields &, int, hipStream_t, const long *etaSrc = nullptr);
 hipError_t launch_calc_r_star(const Dims &, const Params &, const Fields &, const long *, hipStream_t, bool fuseEtaH = false,
                               int fromX = 0);
+hipError_t launch_rstar_exmix(const Dims &, const Params &, const Fields &, const long *, bool, int, double *, double *, int,
+                              const long *, int, int, const XFields &, const long *, int, hipStream_t);
 hipError_t launch_rstar_exch(const Dims &, const Params &, const Fields &, const long *, bool, const XFields &, const long *,
                              int, int *, hipStream_t, int fromX = 0);
 hipError_t launch_update_r_star_cg2d(const Dims &, const Params &, const Fields &, const long *, hipStream_t, bool sfp = false,
                                      bool opEarly = false, bool pcHere = false);
 hipError_t launch_halo_pack(const Dims &, const XFields &, const long *, long, double *, int, hipStream_t);
-hipError_t launch_oceanic_phys(const Dims &, const Params &, const Fields &, const int *, hipStream_t, bool gm = true);
+hipError_t launch_oceanic_phys(const Dims &, const Params &, const Fields &, const int *, hipStream_t, bool gm = true,
+                               bool *ringDone = nullptr);
 hipError_t launch_tracer_step(const Dims &, const Params &, const Fields &, const TracerArgs &, const int *, hipStream_t,
                               bool impl = true);
 bool dyn_thermo_fusable(const Dims &, const Params &, const TracerArgs &, const TracerArgs &);
@@ -1206,9 +1209,18 @@ static int exchange_uv(mgcm_model *m, double *u, double *v, int nz, bool withSig
 // operator.
 static Dims all_tiles(const Dims &d) { Dims a = d; a.t0 = 0; a.nT = d.nTiles; return a; }
 
-static hipError_t calc_r_star(mgcm_model *m, bool fuseEtaH = false, int fromX = 0) {
+// stagEx (cube/LLC maps, the whole domain): DO_STAGGER_FIELDS_EXCHANGES' u, v, w ride in
+// CALC_R_STAR's grid (k_rstar_exmix, MG_FUSE_ENDS)
+static hipError_t calc_r_star(mgcm_model *m, bool fuseEtaH = false, int fromX = 0, bool stagEx = false) {
   const Dims da = all_tiles(m->d);
-  hipError_t e = launch_calc_r_star(da, m->p, m->f, m->d_srcOf, m->stream, fuseEtaH, fromX);
+  hipError_t e;
+  if (stagEx) {
+    XFields xw{};
+    xw.p[0] = m->f.wVel; xw.nz[0] = m->d.Nr; xw.n = 1;
+    e = launch_rstar_exmix(da, m->p, m->f, m->d_srcOf, fuseEtaH, fromX, m->f.uVel, m->f.vVel, m->d.Nr, m->d_uv[1],
+                           m->nUvU[1], m->nUvV[1], xw, m->d_halo, m->nHalo, m->stream);
+  } else
+    e = launch_calc_r_star(da, m->p, m->f, m->d_srcOf, m->stream, fuseEtaH, fromX);
   if (e != hipSuccess || !m->uvMap) return e;
   double *us[3] = {m->f.rStarFacW, m->f.rStarDhWDt, m->f.rStarExpW}, *vs[3] = {m->f.rStarFacS, m->f.rStarDhSDt,
                                                                                  m->f.rStarExpS};
@@ -1605,6 +1617,7 @@ static int one_step(mgcm_model *m) {
   const bool tracers = m->p.tempStepping || m->p.saltStepping;
   const bool fork = !stagger && m->overlap && !m->timing && m->p.momStepping && tracers;
   bool endFused = false;   // CALC_R_STAR + blocking exchanges in one launch (below)
+  bool stagEx = false;     // CALC_R_STAR + the staggered exchanges in one launch (below)
   // Under the linear free surface nothing between DYNAMICS and the correction step touches
   // what THERMODYNAMICS reads or writes (no r* rewrite of hFac; SOLVE_FOR_PRESSURE and CG2D
   // read gU, gV, hFac and eta, write the solver's vectors and etaN), so the tracers may run
@@ -1678,11 +1691,16 @@ static int one_step(mgcm_model *m) {
   // GMREDI_CALC_TENSOR beside CALC_PHI_HYD (launch_gm_phi) where THERMODYNAMICS, its reader,
   // runs after DYNAMICS (staggered, or forked after CALC_DIV_GHAT) and the fold does not apply
   const bool gmPhi = (stagger || thermoLate) && !dtFused && !physPhi && !m->timing && gm_phi_fusable(m->d, m->p);
+  // the VI path's halo-ring AB2 in DO_OCEANIC_PHYS's grid where it is not beside the solve
+  // (k_phys_ring, MG_FUSE_RINGP: the staggered cube)
+  bool ringPhys = false;
+  const bool ringPhysOk = !ringAside && !physPhi && mom_ring_separable(m->d, m->p) && mg_fuse_on(MG_FUSE_RINGP);
   auto phys = [&]() -> int {
     if (physPhi) TIMED(K_PHYS, launch_phys_phi(m->d, m->p, m->f, m->d_ctr, m->stream));
     // (GMREDI_CALC_TENSOR in launch_dyn_thermo's first grid when it takes it)
     else TIMED(K_PHYS, launch_oceanic_phys(m->d, m->p, m->f, m->d_ctr, m->stream,
-                                           !(dtFused && dyn_thermo_takes_gm(m->p)) && !gmPhi && !tcgFork));
+                                           !(dtFused && dyn_thermo_takes_gm(m->p)) && !gmPhi && !tcgFork,
+                                           ringPhysOk ? &ringPhys : nullptr));
     return 0;
   };
   if (stagger || fork || dtFused) {
@@ -1705,11 +1723,11 @@ static int one_step(mgcm_model *m) {
       TIMED(K_MOM, launch_dyn_thermo(m->d, m->p, m->f, aT, aS, m->d_ctr, m->stream, opEarly ? m->d_srcOf : nullptr));
       std::swap(m->f.theta, m->f.thetaNext);   // CYCLE_TRACER: the new tracers are the other buffers
       std::swap(m->f.salt, m->f.saltNext);
-    } else if (physPhi) TIMED(K_MOM, launch_mom_step(m->d, m->p, m->f, m->d_ctr, m->stream, !ringAside));
+    } else if (physPhi) TIMED(K_MOM, launch_mom_step(m->d, m->p, m->f, m->d_ctr, m->stream, !ringAside && !ringPhys));
     else if (gmPhi) {
       TIMED(K_PHI, launch_gm_phi(m->d, m->p, m->f, m->stream));
-      TIMED(K_MOM, launch_mom_step(m->d, m->p, m->f, m->d_ctr, m->stream, !ringAside));
-    } else if (dynamics_on(m, !ringAside)) return -1;
+      TIMED(K_MOM, launch_mom_step(m->d, m->p, m->f, m->d_ctr, m->stream, !ringAside && !ringPhys));
+    } else if (dynamics_on(m, !ringAside && !ringPhys)) return -1;
     // (the late fork comes after CALC_DIV_GHAT, below)
     if (tcgFork) HIPCHK(hipStreamWaitEvent(m->stream, m->evSnap, 0));   // the copy before hFac is rewritten
     else if (fork && !lateJoin && !dtFused) HIPCHK(hipStreamWaitEvent(m->stream, m->evJoin, 0));
@@ -1767,13 +1785,18 @@ static int one_step(mgcm_model *m) {
     if (endFused)
       TIMED(K_RSTAR, launch_rstar_exch(m->d, m->p, m->f, m->d_srcOf, fuseEtaH, blocking_fields(m), m->d_halo, m->nHalo,
                                        m->d_ctr, m->stream, etaX ? 1 : 0));
-    else if (m->p.nonlinFreeSurf > 0) TIMED(K_RSTAR, calc_r_star(m, fuseEtaH, etaX ? 1 : 0));
+    else if (m->p.nonlinFreeSurf > 0) {
+      stagEx = stagger && tracers && m->uvMap && m->d.nT == m->d.nTiles &&
+               mg_hfuse(MG_FUSE_ENDS, m->d.nx, m->d.ny, m->d.nT, m->d.Nr);
+      TIMED(K_RSTAR, calc_r_star(m, fuseEtaH, etaX ? 1 : 0, stagEx));
+    }
   } else {
     if (mgcm_integr_continuity(m)) return -1;
   }
   if (stagger && tracers) {
     // DO_STAGGER_FIELDS_EXCHANGES (do_stagger_fields_exchanges.F:37-43) + THERMODYNAMICS
-    if (m->uvMap) {   // u, v through the vector map and w through the scalar map, one launch
+    if (stagEx) {     // (in CALC_R_STAR's grid, above)
+    } else if (m->uvMap) {   // u, v through the vector map and w through the scalar map, one launch
       XFields xw{};
       xw.p[0] = m->f.wVel; xw.nz[0] = m->d.Nr; xw.n = 1;
       TIMED(K_EXCH, launch_exchange_mixed(m->d, m->f.uVel, m->f.vVel, m->d.Nr, m->d_uv[1], m->nUvU[1], m->nUvV[1], xw,
