@@ -997,7 +997,43 @@ __global__ void __launch_bounds__(256) TRM_ATTR k_tracer_march(Dims d, Params p,
 // k_tracer_backsub finishes the column.  No T* round trip, no second pass over the
 // coefficient operands.
 typedef __attribute__((ext_vector_type(2))) double trd2;
-template <bool FWD>
+// SOLVE_TRIDIAGONAL's back substitution of one column pair (first level's offset q1) from
+// the (c', y') k_tracer_march2<true> stored: all of a batch's loads issued before its part of
+// the recurrence (they do not depend on it), the new tracer written level by level
+__device__ __forceinline__ void tracer_backsub_pair(const Dims &d, const TracerArgs &a, long q1) {
+  const int Nr = d.Nr;
+  const long n2 = d.n2;
+  auto L2 = [](const double *x, long o) { return *reinterpret_cast<const trd2 *>(x + o); };
+  constexpr int CH = 10;   // levels per batch of loads
+  trd2 below = {0.0, 0.0};
+  for (int k1 = Nr; k1 >= 1; k1 -= CH) {
+    const int k0 = k1 - CH + 1 > 1 ? k1 - CH + 1 : 1;
+    trd2 cpv[CH], ypv[CH];
+#pragma unroll
+    for (int u = 0; u < CH; u++) {
+      const int k = k1 - u;
+      if (k >= k0) {
+        const long q3 = q1 + (long)(k - 1) * n2;
+        cpv[u] = L2(a.cp, q3);
+        ypv[u] = L2(a.scr, q3);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < CH; u++) {
+      const int k = k1 - u;
+      if (k >= k0) {
+        trd2 v;
+        if (k == Nr) v = ypv[u];
+        else { v.x = ypv[u].x - cpv[u].x * below.x; v.y = ypv[u].y - cpv[u].y * below.y; }
+        *reinterpret_cast<trd2 *>(a.trNext + q1 + (long)(k - 1) * n2) = v;
+        below = v;
+      }
+    }
+  }
+}
+// BACK (with FWD): the back substitution too, by the same thread right after its column's
+// forward sweep (tracer_backsub_pair: the (c', y') it just stored, read back from the caches)
+template <bool FWD, bool BACK = false>
 __global__ void __launch_bounds__(256) TRM_ATTR k_tracer_march2(Dims d, Params p, Fields f, TracerArgs a, const int *iterPtr,
                                                                 int KC, int nkc, int nty) {
   int b = mg_xcd_block();
@@ -1081,6 +1117,7 @@ __global__ void __launch_bounds__(256) TRM_ATTR k_tracer_march2(Dims d, Params p
     if constexpr (FWD) *reinterpret_cast<trd2 *>(a.cp + q3) = trd2{cpo[0], cpo[1]};
     Tu = T0; T0 = Td; mCu = mC0; mC0 = mCd; w0 = w1; ivd0 = ivd1;
   }
+  if constexpr (FWD && BACK) tracer_backsub_pair(d, a, MG_I3(d, i, j, 1, t));
 }
 
 
@@ -1096,35 +1133,7 @@ __global__ void __launch_bounds__(256) k_tracer_backsub(Dims d, TracerArgs a, in
   if (jy >= TY) return;
   const int i = 1 + 2 * px, j = 1 + ty * TY + jy;
   if (j > d.sNy) return;
-  const int Nr = d.Nr;
-  const long n2 = d.n2, q1 = MG_I3(d, i, j, 1, t);
-  auto L2 = [](const double *x, long o) { return *reinterpret_cast<const trd2 *>(x + o); };
-  constexpr int CH = 10;   // levels per batch of loads
-  trd2 below = {0.0, 0.0};
-  for (int k1 = Nr; k1 >= 1; k1 -= CH) {
-    const int k0 = k1 - CH + 1 > 1 ? k1 - CH + 1 : 1;
-    trd2 cpv[CH], ypv[CH];
-#pragma unroll
-    for (int u = 0; u < CH; u++) {
-      const int k = k1 - u;
-      if (k >= k0) {
-        const long q3 = q1 + (long)(k - 1) * n2;
-        cpv[u] = L2(a.cp, q3);
-        ypv[u] = L2(a.scr, q3);
-      }
-    }
-#pragma unroll
-    for (int u = 0; u < CH; u++) {
-      const int k = k1 - u;
-      if (k >= k0) {
-        trd2 v;
-        if (k == Nr) v = ypv[u];
-        else { v.x = ypv[u].x - cpv[u].x * below.x; v.y = ypv[u].y - cpv[u].y * below.y; }
-        *reinterpret_cast<trd2 *>(a.trNext + q1 + (long)(k - 1) * n2) = v;
-        below = v;
-      }
-    }
-  }
+  tracer_backsub_pair(d, a, MG_I3(d, i, j, 1, t));
 }
 
 __global__ void __launch_bounds__(256) k_tracer_rhs_flat(Dims d, Params p, Fields f, TracerArgs a, const int *iterPtr) {
@@ -1315,13 +1324,18 @@ hipError_t launch_oceanic_phys(const Dims &d, const Params &p, const Fields &f, 
   return hipGetLastError();
 }
 
-// the implicit solve's forward sweep fused into a whole-column march (k_tracer_march2<true> +
-// k_tracer_backsub): MGCM_TRACER_MARCH=2 (read per launch).  Round 6: per tracer 171 + 47 us
-// against 161 + 105 (march + implicit solve), but LLC-90's step 1.239 against 1.233 ms -- the
-// tracers run beside the pressure solve there, which bounds the step -- so not the default
-static bool tracer_fwd_on() {
-  const char *e = getenv("MGCM_TRACER_MARCH");
-  return e && atoi(e) == 2;
+// the implicit solve inside the whole-column march (deep grids, where the k-march runs): its
+// forward sweep, then its back substitution by the same thread (k_tracer_march2<true, true>,
+// the default; MGCM_TRACER_MARCH=3), or the back substitution as a kernel of its own
+// (k_tracer_backsub; =2).  Round 6, LLC-90 per tracer: one kernel 216 us and 734 MB
+// (rocprofv3 time, FETCH+WRITE), against 161 + 105 us and 596 + 228 MB for the chunked
+// march + k_tracer_impl (=1) and 171 + 47 us for =2; step 1.2326-1.2330 ms against
+// 1.2330-1.2455 (=1) and 1.2495 (=2), alternating on one box (profiles/r06/fwdback/)
+static int tracer_fwd_form(const Dims &d) {
+  const char *e = getenv("MGCM_TRACER_MARCH");   // read per launch (tests switch it per model)
+  if (!e) return d.Nr >= 30 ? 3 : 0;
+  const int v = atoi(e);
+  return v == 2 || v == 3 ? v : 0;
 }
 static bool tracer_march_on(const Dims &d) {
   const char *e = getenv("MGCM_TRACER_MARCH");   // read per launch (tests switch it per model)
@@ -1370,16 +1384,21 @@ hipError_t launch_tracer_step(const Dims &d, const Params &p, const Fields &f, c
         al(a.trNext) && al(a.scr) && al(a.gNm1) && al(f.maskC) && al(f.wVel) && al(f.IVDConvCount) && al(f.uVel) &&
         al(f.vVel) && al(f.hFacW) && al(f.hFacS) && al(f.recip_hFacC) && (!a.multiDim || al(f.gAdv))) {
       const int TY = 256 / hx, nty2 = (d.sNy + TY - 1) / TY;
-      // the implicit solve's forward elimination inside a whole-column march, then the back
-      // substitution (MGCM_TRACER_MARCH=2; tracer_fwd_on): no T* round trip
-      if (impl && p.implicitDiffusion && !p.useGMRedi && tracer_fwd_on() && !a.multiDim && a.cp && al(a.cp) && d.Nr > 1) {
-        hipLaunchKernelGGL(k_tracer_march2<true>, dim3((unsigned)(nty2 * d.nT)), blk, 0, s, d, p, f, a, iterPtr, d.Nr, 1,
-                           nty2);
+      // the implicit solve inside a whole-column march (tracer_fwd_form): no T* round trip
+      const int fwd = tracer_fwd_form(d);
+      if (impl && p.implicitDiffusion && !p.useGMRedi && fwd && !a.multiDim && a.cp && al(a.cp) && d.Nr > 1) {
+        if (fwd == 3) {
+          hipLaunchKernelGGL((k_tracer_march2<true, true>), dim3((unsigned)(nty2 * d.nT)), blk, 0, s, d, p, f, a, iterPtr,
+                             d.Nr, 1, nty2);
+          return hipGetLastError();
+        }
+        hipLaunchKernelGGL((k_tracer_march2<true, false>), dim3((unsigned)(nty2 * d.nT)), blk, 0, s, d, p, f, a, iterPtr,
+                           d.Nr, 1, nty2);
         hipLaunchKernelGGL(k_tracer_backsub, dim3((unsigned)(nty2 * d.nT)), blk, 0, s, d, a, nty2);
         return hipGetLastError();
       }
-      hipLaunchKernelGGL(k_tracer_march2<false>, dim3((unsigned)(nkc * nty2 * d.nT)), blk, 0, s, d, p, f, a, iterPtr, KC, nkc,
-                         nty2);
+      hipLaunchKernelGGL((k_tracer_march2<false, false>), dim3((unsigned)(nkc * nty2 * d.nT)), blk, 0, s, d, p, f, a, iterPtr,
+                         KC, nkc, nty2);
     } else
       hipLaunchKernelGGL(k_tracer_march, dim3((unsigned)(nkc * ntx * nty * d.nT)), blk, 0, s, d, p, f, a, iterPtr, KC, nkc,
                          ntx, nty);
