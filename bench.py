@@ -310,6 +310,19 @@ def default_pmc_summary(config):
     return os.path.join(ROOT, "profiles", "r06", tag, "pmc_summary.json")
 
 
+def device_free_bytes(device):
+    """hipMemGetInfo's free bytes of the device (None where the HIP runtime is not loadable)."""
+    import ctypes
+    try:
+        hip = ctypes.CDLL("libamdhip64.so")
+        free, total = ctypes.c_size_t(), ctypes.c_size_t()
+        if hip.hipSetDevice(device) != 0 or hip.hipMemGetInfo(ctypes.byref(free), ctypes.byref(total)) != 0:
+            return None
+        return free.value
+    except OSError:
+        return None
+
+
 def stream_triad_gbs(device, n=64 << 20, reps=8):
     """SURVEY.md 8(d)'s roofline denominator measured on the box: a STREAM triad
     a = b + s*c over three fp64 arrays of n doubles (512 MB each at the default), 16 B per
@@ -624,8 +637,13 @@ def main():
         over.setdefault("cg2dForceMwg", 1.0)   # the device CG2D runs the multi-workgroup solver's parts
     if over:
         cfn = (lambda f: lambda: (lambda r: (r[0], {**r[1], **over}) + tuple(r[2:]))(f()))(cfn)
+    free0 = device_free_bytes(local)
     m = configs.make_model(cfn, device=local)
     g = m.g
+    # the model's device footprint (the whole domain on every GPU): free HBM before
+    # and after building it
+    free1 = device_free_bytes(local)
+    model_gb = (free0 - free1) / 1e9 if free0 is not None and free1 is not None else None
     dt_clock = m.params["deltaTClock"]
     stepper = m
     if shard:
@@ -719,6 +737,7 @@ def main():
                        else "eager sharded step"} if shard else {}),
                    **({"params_over": over} if over else {})},
         "cg2d_iters_per_s": cg2d_iters_per_s,
+        "device_model_gb": model_gb,
         # THERMODYNAMICS on a second stream beside DYNAMICS: picked per workload by timing both
         # graphs over the first 20 graph-replayed steps (results identical either way)
         "thermo_overlap": _overlap_info(m),
