@@ -5,6 +5,8 @@ parameter dump of the committed results/output.txt).
 """
 import os
 
+import math
+
 import numpy as np
 
 from .exch2 import cube_topology
@@ -54,6 +56,31 @@ def barotropic_gyre(nSx=1, nSy=1, data_dir=None, bathy=None, wind=None):
 
 BAROCLINIC_DELR = [50., 60., 70., 80., 90., 100., 110., 120., 130., 140., 150., 160., 170., 180., 190.]
 BAROCLINIC_TREF = [30., 27., 24., 21., 18., 15., 13., 11., 9., 7., 6., 5., 4., 3., 2.]
+
+
+def advect_xy_ab3_c4(nSx=1, nSy=2):
+    """verification/advect_xy with input.ab3_c4 (results/output.ab3_c4.txt): the same box and
+    flow as advect_xy, theta AND salt advected with the centred 4th-order scheme
+    (tempAdvScheme = saltAdvScheme = 4, not multi-dimensional: gad_c4_adv_x/y.F inside
+    GAD_CALC_RHS), the tendencies stepped with ADAMS_BASHFORTH3 (code/CPP_OPTIONS.h defines
+    ALLOW_ADAMSBASHFORTH_3; alph_AB = 0.5, beta_AB = 0.281105), deltaT = 2750, theta a Gaussian
+    bump exp(-(rD/20 km)^2/2) (code/ini_theta.F), salt the +1 psu disc (code/ini_salt.F)."""
+    g, params, state = advect_xy(nSx, nSy)
+    g.ini_cg2d(2750.0, 2750.0, 1e-13)
+    params.update(deltaTMom=2750.0, deltaTFreeSurf=2750.0, deltaTClock=2750.0, deltaTtracer=2750.0, abEps=0.01,
+                  tempStepping=1, tempAdvection=1, tempForcing=0, tempAdvScheme=4, tempVertAdvScheme=4,
+                  saltAdvScheme=4, saltVertAdvScheme=4, diffKhT=0.0, diffKrT=0.0, useAB3=1, alph_AB=0.5,
+                  beta_AB=0.281105)
+    rC = g.f["rC"][0]
+    theta = np.full((g.nTiles, 1, g.ny, g.nx), 20.0)   # tRef in the halo before the exchange
+    for t in range(g.nTiles):
+        for J in range(g.OLy, g.OLy + g.sNy):
+            for I in range(g.OLx, g.OLx + g.sNx):
+                x, y = g.f["xC"][t, J, I], g.f["yC"][t, J, I]
+                rD = math.sqrt((x - 40.0e3) ** 2 + (y - 40.0e3) ** 2 + (rC + 50.0e3) ** 2)
+                theta[t, 0, J, I] = math.exp(-0.5 * (rD / 20.0e3) ** 2)
+    state["theta"] = g.exch(theta)
+    return g, params, state
 
 
 def baroclinic_gyre(nSx=2, nSy=2, data_dir=None, tempAdvScheme=2):

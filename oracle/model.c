@@ -20,7 +20,7 @@ OModel *oracle_new(int sNx, int sNy, int OLx, int OLy, int Nr, int nSx, int nSy)
   long N2 = m->n2 * m->nTiles, N3 = m->n3 * m->nTiles;
   int Nx = sNx * nSx, Ny = sNy * nSy;
   /* defaults of set_defaults.F / ini_parms.F resolution for the supported subset */
-  m->abEps = 0.01; m->gravity = 9.81; m->rhoNil = 999.8; m->rhoConst = 999.8; m->gBaro = 9.81;
+  m->abEps = 0.01; m->alph_AB = 0.5; m->beta_AB = 5.0 / 12.0; m->gravity = 9.81; m->rhoNil = 999.8; m->rhoConst = 999.8; m->gBaro = 9.81;
   m->f0 = 1.e-4; m->beta = 1.e-11; m->sideDragFactor = 2.0;
   m->cg2dTargetResWunit = -1.0; m->cg2dpcOffDFac = 0.51; m->cg2dMaxIters = 150;
   m->freeSurfFac = 1.0; m->implicSurfPress = 1.0; m->implicDiv2DFlow = 1.0; m->rkSign = -1.0;
@@ -72,7 +72,7 @@ OModel *oracle_new(int sNx, int sNy, int OLx, int OLy, int Nr, int nSx, int nSy)
   A3(hFacC); A3(hFacW); A3(hFacS); A3(recip_hFacC); A3(recip_hFacW); A3(recip_hFacS);
   A3(maskC); A3(maskW); A3(maskS);
   A3(uVel); A3(vVel); A3(wVel); A3(theta); A3(salt); A3(gU); A3(gV); A3(guNm1); A3(gvNm1);
-  A3(gtNm1); A3(gsNm1); A3(rhoInSitu); A3(IVDConvCount);
+  A3(gtNm1); A3(gsNm1); A3(gtNm2); A3(gsNm2); A3(rhoInSitu); A3(IVDConvCount);
   A3(Kwx); A3(Kwy); A3(Kwz); A3(Kux); A3(Kvy); A3(uVelD); A3(vVelD); A3(uNM1); A3(vNM1);
   A3(sigmaX); A3(sigmaY); A3(sigmaR); A3(Kuz); A3(Kvz); A3(GM_PsiX); A3(GM_PsiY); A3(h0FacC); A3(h0FacW); A3(h0FacS); A3(totPhiHyd);
 #undef A3
@@ -94,7 +94,7 @@ void oracle_free(OModel *m) {
                    &m->vVel, &m->wVel, &m->theta, &m->salt, &m->gU, &m->gV, &m->guNm1, &m->gvNm1,
                    &m->tRef, &m->sRef, &m->fCoriCos, &m->tanPhiAtU, &m->tanPhiAtV, &m->surfaceForcingT,
                    &m->SST, &m->lambdaThetaClimRelax, &m->etaH, &m->dEtaHdt, &m->gtNm1, &m->rhoInSitu,
-                   &m->IVDConvCount, &m->gsNm1, &m->surfaceForcingS, &m->pRef4EOS, &m->Qnet, &m->EmPmR,
+                   &m->IVDConvCount, &m->gsNm1, &m->gtNm2, &m->gsNm2, &m->surfaceForcingS, &m->pRef4EOS, &m->Qnet, &m->EmPmR,
                    &m->SSS, &m->lambdaSaltClimRelax, &m->saltFlux, &m->etaNm1, &m->Kwx, &m->Kwy, &m->Kwz,
                    &m->Kux, &m->Kvy, &m->uVelD, &m->vVelD, &m->uNM1, &m->vNM1, &m->sigmaX, &m->sigmaY,
                    &m->sigmaR, &m->Kuz, &m->Kvz, &m->GM_PsiX, &m->GM_PsiY, &m->forcTaux, &m->forcTauy, &m->forcQnet, &m->forcEmPmR, &m->forcSST,
@@ -115,7 +115,8 @@ typedef struct { const char *name; size_t off; int isint; } PDesc;
 #define PD(f) {#f, offsetof(OModel, f), 0}
 #define PI_(f) {#f, offsetof(OModel, f), 1}
 static const PDesc PTAB[] = {
-  PD(deltaTMom), PD(deltaTFreeSurf), PD(deltaTClock), PD(abEps), PD(gBaro), PD(gravity),
+  PD(deltaTMom), PD(deltaTFreeSurf), PD(deltaTClock), PD(abEps), PD(alph_AB), PD(beta_AB), PI_(useAB3),
+  PD(gBaro), PD(gravity),
   PD(rhoConst), PD(rhoNil), PD(f0), PD(beta), PD(viscAhD), PD(viscAhZ), PD(viscA4D), PD(viscA4Z),
   PD(viscAr), PD(sideDragFactor), PD(cg2dTargetResidual), PD(cg2dTargetResWunit), PD(cg2dpcOffDFac),
   PD(freeSurfFac), PD(implicSurfPress), PD(implicDiv2DFlow), PD(rkSign), PD(afFacMom), PD(vfFacMom),
@@ -177,7 +178,8 @@ double *oracle_array(OModel *m, const char *name, long *count) {
     {"lambdaThetaClimRelax", m->lambdaThetaClimRelax, N2}, {"etaH", m->etaH, N2},
     {"dEtaHdt", m->dEtaHdt, N2}, {"surfaceForcingU", m->surfaceForcingU, N2},
     {"surfaceForcingV", m->surfaceForcingV, N2}, {"gtNm1", m->gtNm1, N3}, {"rhoInSitu", m->rhoInSitu, N3},
-    {"IVDConvCount", m->IVDConvCount, N3}, {"gsNm1", m->gsNm1, N3}, {"surfaceForcingS", m->surfaceForcingS, N2},
+    {"IVDConvCount", m->IVDConvCount, N3}, {"gsNm1", m->gsNm1, N3},
+    {"gtNm2", m->gtNm2, N3}, {"gsNm2", m->gsNm2, N3}, {"surfaceForcingS", m->surfaceForcingS, N2},
     {"delX", m->delX, (long)m->sNx * m->nSx}, {"delY", m->delY, (long)m->sNy * m->nSy},
     {"xC", m->xC, N2}, {"yC", m->yC, N2}, {"xG", m->xG, N2}, {"yG", m->yG, N2},
     {"dxF", m->dxF, N2}, {"dyF", m->dyF, N2}, {"dxG", m->dxG, N2}, {"dyG", m->dyG, N2},

@@ -80,6 +80,9 @@ typedef struct OModel {
   double *fu, *fv, *surfaceForcingU, *surfaceForcingV;
   double *surfaceForcingT, *SST, *lambdaThetaClimRelax, *etaH, *dEtaHdt;   /* 2-D */
   double *gtNm1, *gsNm1, *rhoInSitu, *IVDConvCount;                        /* 3-D */
+  double *gtNm2, *gsNm2;   /* 3-D: ADAMS_BASHFORTH3's second tendency history (gtNm(:,:,:,2)) */
+  double alph_AB, beta_AB; /* ALLOW_ADAMSBASHFORTH_3 (PARAMS.h: alph_AB, beta_AB) */
+  int useAB3;              /* tracers stepped with ADAMS_BASHFORTH3 (the build's ALLOW_ADAMSBASHFORTH_3) */
   double *surfaceForcingS;                                                 /* 2-D */
   int myIter;
   double myTime;

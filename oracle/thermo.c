@@ -322,7 +322,8 @@ static void gad_advection_dst3fl(const OModel *m, int t, const double *tr, const
 
 /* One tracer through TEMP_INTEGRATE / SALT_INTEGRATE (temp_integrate.F, salt_integrate.F). */
 typedef struct {
-  double *tr, *gNm1;        /* tracer, its AB2 tendency history */
+  double *tr, *gNm1;        /* tracer, its AB2 tendency history (AB3: gtNm(:,:,:,1)) */
+  double *gNm2;             /* AB3: gtNm(:,:,:,2) */
   const double *sfc;        /* surface forcing (surfaceForcingT/S), may be NULL */
   double diffKh, diffKr;
   int advScheme, vAdvScheme, advection, forcing;
@@ -333,7 +334,8 @@ static void tracer_integrate(OModel *m, const TracerSpec *c) {
   const long n2 = m->n2, n3 = m->n3;
   const int multiDim = m->multiDimAdvection && c->advection && c->advScheme != 2 && c->advScheme != 3 && c->advScheme != 4;
   const int useAB = (c->advScheme == 2 || c->advScheme == 3 || c->advScheme == 4);   /* gad_init_fixed.F:144-162 */
-  if (!(c->advScheme == 2 || ((c->advScheme == 30 || c->advScheme == 33) && multiDim)) || c->vAdvScheme != c->advScheme) {
+  if (!(c->advScheme == 2 || c->advScheme == 3 || c->advScheme == 4 ||
+        ((c->advScheme == 30 || c->advScheme == 33) && multiDim)) || c->vAdvScheme != c->advScheme) {
     fprintf(stderr, "oracle tracer_integrate: advection scheme %d/%d not restated\n", c->advScheme, c->vAdvScheme); abort();
   }
 #pragma omp parallel if (m->nThreads > 1) num_threads(m->nThreads > 1 ? m->nThreads : 1)
@@ -348,11 +350,23 @@ static void tracer_integrate(OModel *m, const TracerSpec *c) {
   const int calcAdvection = c->advection && !multiDim;
   const double advFac = calcAdvection ? 1.0 : 0.0, rAdvFac = m->rkSign * advFac;
   const double abFac = (m->myIter == m->nIter0 && m->nIter0 == 0) ? 0.0 : 0.5 + m->abEps; /* startAB = nIter0 */
+  /* ADAMS_BASHFORTH3 (adams_bashforth3.F:60-78): startAB = nIter0 (ini_model_io.F:117), history
+   * slots m1 = 1 + MOD(iter+1,2), m2 = 1 + MOD(iter,2) of gtNm(:,:,:,1:2) = (gNm1, gNm2) */
+  double ab0 = 0.0, ab1 = 0.0, ab2 = 0.0;
+  {
+    const int it = m->myIter, n0 = m->nIter0, startAB = m->nIter0;
+    if (it == n0 && startAB == 0) { ab0 = 0.0; ab1 = 0.0; ab2 = 0.0; }
+    else if ((it == n0 && startAB == 1) || (it == 1 + n0 && startAB == 0)) { ab0 = m->alph_AB; ab1 = -m->alph_AB; ab2 = 0.0; }
+    else { ab0 = m->alph_AB + m->beta_AB; ab1 = -m->alph_AB - 2. * m->beta_AB; ab2 = m->beta_AB; }
+  }
+  const int abM1 = 1 + (m->myIter + 1) % 2;
   const int rstar = m->nonlinFreeSurf > 0 && m->select_rStar > 0;
 
 #pragma omp for schedule(dynamic, 1)
   for (int t = 0; t < m->nTiles; t++) {
     double *theta = c->tr + t * n3, *gtNm1 = c->gNm1 + t * n3;
+    double *gtA = m->useAB3 ? (abM1 == 1 ? gtNm1 : c->gNm2 + t * n3) : NULL;   /* gtNm(m1) */
+    double *gtB = m->useAB3 ? (abM1 == 1 ? c->gNm2 + t * n3 : gtNm1) : NULL;   /* gtNm(m2) */
     const double *dxG = m->dxG + t * n2, *dyG = m->dyG + t * n2, *rA = m->rA + t * n2;
     const double *recip_rA = m->recip_rA + t * n2, *recip_dxC = m->recip_dxC + t * n2;
     const double *uVel = m->uVel + t * n3, *vVel = m->vVel + t * n3, *wVel = m->wVel + t * n3;
@@ -434,11 +448,31 @@ static void tracer_integrate(OModel *m, const TracerSpec *c) {
             L(gtForc, i, j) = L(gtForc, i, j) + L(sfT, i, j) * m->recip_drF[k - 1] * W3(rhFacC, i, j, k);
       /* GAD_CALC_RHS */
       for (long p = 0; p < n2; p++) { fZon[p] = 0.0; fMer[p] = 0.0; fVerUp[p] = 0.0; df[p] = 0.0; }
-      if (calcAdvection) { /* GAD_C2_ADV_X */
+      if (calcAdvection && c->advScheme == 2) { /* GAD_C2_ADV_X */
         for (int j = 1 - OLy; j <= sNy + OLy; j++) {
           L(af, 1 - OLx, j) = 0.0;
           for (int i = 2 - OLx; i <= sNx + OLx; i++)
             L(af, i, j) = L(uTrans, i, j) * (W3(theta, i, j, k) + W3(theta, i - 1, j, k)) * 0.5;
+        }
+        for (long p = 0; p < n2; p++) fZon[p] = fZon[p] + af[p];
+      } else if (calcAdvection) {
+        /* GAD_U3_ADV_X (gad_u3_adv_x.F:70-92) / GAD_C4_ADV_X (gad_c4_adv_x.F:70-93); maskLocW =
+         * maskW(k) (gad_calc_rhs.F:262-268, no OBCS) */
+        const double oneSixth = 1.0 / 6.0;
+        for (int j = 1 - OLy; j <= sNy + OLy; j++) {
+          L(af, 1 - OLx, j) = 0.0; L(af, 2 - OLx, j) = 0.0; L(af, sNx + OLx, j) = 0.0;
+          for (int i = 1 - OLx + 2; i <= sNx + OLx - 1; i++) {
+            const double Rjp = (W3(theta, i + 1, j, k) - W3(theta, i, j, k)) * W3(maskW, i + 1, j, k);
+            const double Rj = (W3(theta, i, j, k) - W3(theta, i - 1, j, k)) * W3(maskW, i, j, k);
+            const double Rjm = (W3(theta, i - 1, j, k) - W3(theta, i - 2, j, k)) * W3(maskW, i - 1, j, k);
+            const double Rjjp = Rjp - Rj, Rjjm = Rj - Rjm;
+            const double uTr = L(uTrans, i, j);
+            double v = uTr * (W3(theta, i, j, k) + W3(theta, i - 1, j, k) - oneSixth * (Rjjp + Rjjm)) * 0.5;
+            if (c->advScheme == 3) v = v + fabs(uTr) * 0.5 * oneSixth * (Rjjp - Rjjm);
+            else v = v + fabs(uTr) * 0.5 * oneSixth * (Rjjp - Rjjm) *
+                             (1.0 - W3(maskW, i - 1, j, k) * W3(maskW, i + 1, j, k));
+            L(af, i, j) = v;
+          }
         }
         for (long p = 0; p < n2; p++) fZon[p] = fZon[p] + af[p];
       }
@@ -473,11 +507,30 @@ static void tracer_integrate(OModel *m, const TracerSpec *c) {
           }
       }
       for (long p = 0; p < n2; p++) fZon[p] = fZon[p] + df[p];
-      if (calcAdvection) { /* GAD_C2_ADV_Y */
+      if (calcAdvection && c->advScheme == 2) { /* GAD_C2_ADV_Y */
         for (int i = 1 - OLx; i <= sNx + OLx; i++) L(af, i, 1 - OLy) = 0.0;
         for (int j = 2 - OLy; j <= sNy + OLy; j++)
           for (int i = 1 - OLx; i <= sNx + OLx; i++)
             L(af, i, j) = L(vTrans, i, j) * (W3(theta, i, j, k) + W3(theta, i, j - 1, k)) * 0.5;
+        for (long p = 0; p < n2; p++) fMer[p] = fMer[p] + af[p];
+      } else if (calcAdvection) {   /* GAD_U3_ADV_Y / GAD_C4_ADV_Y (maskLocS = maskS(k)) */
+        const double oneSixth = 1.0 / 6.0;
+        for (int i = 1 - OLx; i <= sNx + OLx; i++) {
+          L(af, i, 1 - OLy) = 0.0; L(af, i, 2 - OLy) = 0.0; L(af, i, sNy + OLy) = 0.0;
+        }
+        for (int j = 1 - OLy + 2; j <= sNy + OLy - 1; j++)
+          for (int i = 1 - OLx; i <= sNx + OLx; i++) {
+            const double Rjp = (W3(theta, i, j + 1, k) - W3(theta, i, j, k)) * W3(maskS, i, j + 1, k);
+            const double Rj = (W3(theta, i, j, k) - W3(theta, i, j - 1, k)) * W3(maskS, i, j, k);
+            const double Rjm = (W3(theta, i, j - 1, k) - W3(theta, i, j - 2, k)) * W3(maskS, i, j - 1, k);
+            const double Rjjp = Rjp - Rj, Rjjm = Rj - Rjm;
+            const double vTr = L(vTrans, i, j);
+            double v = vTr * (W3(theta, i, j, k) + W3(theta, i, j - 1, k) - oneSixth * (Rjjp + Rjjm)) * 0.5;
+            if (c->advScheme == 3) v = v + fabs(vTr) * 0.5 * oneSixth * (Rjjp - Rjjm);
+            else v = v + fabs(vTr) * 0.5 * oneSixth * (Rjjp - Rjjm) *
+                             (1.0 - W3(maskS, i, j - 1, k) * W3(maskS, i, j + 1, k));
+            L(af, i, j) = v;
+          }
         for (long p = 0; p < n2; p++) fMer[p] = fMer[p] + af[p];
       }
       if (c->diffKh != 0.0) { /* GAD_DIFF_Y */
@@ -510,10 +563,36 @@ static void tracer_integrate(OModel *m, const TracerSpec *c) {
           }
       }
       for (long p = 0; p < n2; p++) fMer[p] = fMer[p] + df[p];
-      if (calcAdvection && k >= 2) { /* GAD_C2_ADV_R */
+      if (calcAdvection && k >= 2 && c->advScheme == 2) { /* GAD_C2_ADV_R */
         for (int j = 1 - OLy; j <= sNy + OLy; j++)
           for (int i = 1 - OLx; i <= sNx + OLx; i++) {
             double wT = W3(maskC, i, j, kM1) * L(rTrans, i, j) * (W3(theta, i, j, k) + W3(theta, i, j, kM1)) * 0.5;
+            L(fVerUp, i, j) = L(fVerUp, i, j) + wT * L(maskInC, i, j);
+          }
+      } else if (calcAdvection && k >= 2) {
+        /* GAD_U3_ADV_R (gad_u3_adv_r.F:58-88) / GAD_C4_ADV_R (gad_c4_adv_r.F:58-92): km2 = max(1,k-2),
+         * kp1 = min(Nr,k+1); U3's Rjm masked at km2, C4's at km1 with C4's boundary term */
+        const double oneSixth = 1.0 / 6.0;
+        const int km2 = k - 2 > 1 ? k - 2 : 1, km1 = kM1, kp1 = k + 1 < Nr ? k + 1 : Nr;
+        const double maskPM = (k <= 2 || k >= Nr) ? 0.0 : 1.0;
+        for (int j = 1 - OLy; j <= sNy + OLy; j++)
+          for (int i = 1 - OLx; i <= sNx + OLx; i++) {
+            const double Rjp = (W3(theta, i, j, kp1) - W3(theta, i, j, k)) * W3(maskC, i, j, kp1);
+            const double Rj = (W3(theta, i, j, k) - W3(theta, i, j, km1));
+            const double Rjm = (W3(theta, i, j, km1) - W3(theta, i, j, km2)) *
+                               (c->advScheme == 3 ? W3(maskC, i, j, km2) : W3(maskC, i, j, km1));
+            const double Rjjp = Rjp - Rj, Rjjm = Rj - Rjm, rTr = L(rTrans, i, j);
+            double wT;
+            if (c->advScheme == 3)
+              wT = W3(maskC, i, j, km1) * (rTr * ((W3(theta, i, j, k) + W3(theta, i, j, km1)) * 0.5 -
+                                                  oneSixth * (Rjjm + Rjjp) * 0.5) +
+                                           fabs(rTr) * oneSixth * (Rjjm - Rjjp) * 0.5);
+            else {
+              const double maskBound = maskPM * W3(maskC, i, j, km2) * W3(maskC, i, j, kp1);
+              wT = W3(maskC, i, j, km1) * (rTr * ((W3(theta, i, j, k) + W3(theta, i, j, km1)) * 0.5 -
+                                                  oneSixth * (Rjjm + Rjjp) * 0.5) +
+                                           fabs(rTr) * oneSixth * (Rjjm - Rjjp) * 0.5 * (1.0 - maskBound));
+            }
             L(fVerUp, i, j) = L(fVerUp, i, j) + wT * L(maskInC, i, j);
           }
       }
@@ -565,7 +644,12 @@ static void tracer_integrate(OModel *m, const TracerSpec *c) {
       for (int j = 1 - OLy; j <= sNy + OLy; j++)
         for (int i = 1 - OLx; i <= sNx + OLx; i++) {
           if (!m->tracForcingOutAB) W3(gT, i, j, k) = W3(gT, i, j, k) + L(gtForc, i, j);
-          if (useAB) {
+          if (useAB && m->useAB3) {   /* ADAMS_BASHFORTH3(k) (adams_bashforth3.F:91-103) */
+            const double g = W3(gT, i, j, k);
+            const double abG = ab0 * g + ab1 * W3(gtA, i, j, k) + ab2 * W3(gtB, i, j, k);
+            W3(gtB, i, j, k) = g;
+            W3(gT, i, j, k) = g + abG;
+          } else if (useAB) {
             double ab = abFac * (W3(gT, i, j, k) - W3(gtNm1, i, j, k));
             W3(gtNm1, i, j, k) = W3(gT, i, j, k);
             W3(gT, i, j, k) = W3(gT, i, j, k) + ab;
@@ -636,12 +720,12 @@ static void tracer_integrate(OModel *m, const TracerSpec *c) {
 
 void oracle_thermodynamics(OModel *m) {
   if (m->tempStepping) {
-    TracerSpec c = {m->theta, m->gtNm1, m->surfaceForcingT, m->diffKhT, m->diffKrT,
+    TracerSpec c = {m->theta, m->gtNm1, m->gtNm2, m->surfaceForcingT, m->diffKhT, m->diffKrT,
                     m->tempAdvScheme, m->tempVertAdvScheme, m->tempAdvection, m->tempForcing};
     tracer_integrate(m, &c);
   }
   if (m->saltStepping) {
-    TracerSpec c = {m->salt, m->gsNm1, m->surfaceForcingS, m->diffKhS, m->diffKrS,
+    TracerSpec c = {m->salt, m->gsNm1, m->gsNm2, m->surfaceForcingS, m->diffKhS, m->diffKrS,
                     m->saltAdvScheme, m->saltVertAdvScheme, m->saltAdvection, m->saltForcing};
     tracer_integrate(m, &c);
   }

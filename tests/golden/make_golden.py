@@ -9,6 +9,9 @@ What it writes (data only -- inputs and expected outputs, no reference source):
                                       committed verification/<exp>/results/output.txt
   tests/golden/<exp>/params.json      resolved run-time parameters parsed from the
                                       "Model configuration" dump of the same output.txt
+  tests/golden/<exp>/monitor.<tag>.json, params.<tag>.json
+                                      the same from another committed output of the
+                                      experiment (results/output.<tag>.txt)
   tests/golden/adjustment.cs-32x32x1/w2_topology.json
                                       the "W2 TILE TOPLOGY" lists (per tile, its neighbours'
                                       tile ids in W2's order) the reference printed for its
@@ -33,6 +36,9 @@ EXPERIMENTS = {
     "advect_xy": {
         "inputs": [],
         "output": "results/output.txt",
+        # input.ab3_c4: centred 4th-order advection (scheme 4) of theta and salt with
+        # ADAMS_BASHFORTH3 (code/CPP_OPTIONS.h defines ALLOW_ADAMSBASHFORTH_3)
+        "extra_outputs": {"ab3_c4": "results/output.ab3_c4.txt"},
     },
     "tutorial_baroclinic_gyre": {
         "inputs": ["input/bathy.bin", "input/windx_cosy.bin", "input/SST_relax.bin"],
@@ -220,6 +226,12 @@ def main():
             json.dump(parse_grid_monitor(res), f, indent=1)
         with open(os.path.join(out, "params.json"), "w") as f:
             json.dump(parse_params(res), f, indent=1, sort_keys=True)
+        for tag, rel in spec.get("extra_outputs", {}).items():   # other runs of the same experiment
+            res = os.path.join(REF, exp, rel)
+            with open(os.path.join(out, "monitor.%s.json" % tag), "w") as f:
+                json.dump(parse_monitor(res), f, indent=1)
+            with open(os.path.join(out, "params.%s.json" % tag), "w") as f:
+                json.dump(parse_params(res), f, indent=1, sort_keys=True)
         print("wrote", out)
 
 
