@@ -40,7 +40,7 @@ struct Dims {
     X(gtNm1) X(thetaNext) X(gTscr) X(cpScr) X(phiHydC) X(saltNext) X(gsNm1) X(advScr1) X(advScr2) X(gAdv) \
     X(sigmaR) X(Kwx) X(Kwy) X(Kwz) X(Kux) X(Kvy) X(uVelD) X(vVelD) X(uNM1) X(vNM1) X(cdU) X(cdV) X(h0FacC) \
     X(h0FacW) X(h0FacS) X(totPhiHyd) X(alphaRho) X(del2u) X(del2v) X(dWtC) X(dWtU) X(dWtV) X(Kuz) X(Kvz) \
-    X(GM_PsiX) X(GM_PsiY)
+    X(GM_PsiX) X(GM_PsiY) X(gtNm2) X(gsNm2)
 #define MG_ENUM2(n) F2_##n,
 #define MG_ENUM3(n) F3_##n,
 enum F2Id { MG_F2D_LIST(MG_ENUM2) F2_COUNT };
@@ -83,6 +83,9 @@ struct Params {
   // cubed sphere (pkg/exch2) + vector-invariant momentum (pkg/mom_vecinv)
   int vectorInvariantMomentum, selectVortScheme, selectKEscheme, upwindShear, cubeCorners;
   int staggerTimeStep, tracForcingOutAB;   // forward_step.F:1003-1036; temp_integrate.F:373-410
+  // ALLOW_ADAMSBASHFORTH_3 for the tracers (adams_bashforth3.F; momStepping off, init refuses the rest)
+  double alph_AB, beta_AB;
+  int useAB3;
 };
 
 // Device pointers of every field the kernels touch.
@@ -109,6 +112,7 @@ struct Fields {
   double *thetaNext, *gTscr, *cpScr;   // tracer ping-pong buffer and per-column scratch
   double *phiHydC;                     // CALC_PHI_HYD output at cell centres (k_phi_hyd)
   double *saltNext, *gsNm1, *surfaceForcingS;
+  double *gtNm2, *gsNm2;                // ADAMS_BASHFORTH3's second tendency history (gtNm(:,:,:,2))
   double *advScr1, *advScr2, *gAdv;     // multi-dim advection passes and its tendency
   // lat-lon ocean physics
   const double *pRef4EOS;                  // [Nr] reference pressure for the EOS (set_ref_state.F)
@@ -329,6 +333,8 @@ struct TracerArgs {
   double diffKh, diffKr, dT;
   int advection, multiDim, useAB, forcing;
   int limiter;          // multi-dim face fluxes: 1 DST3FL (scheme 33), 0 DST3 (scheme 30)
+  int scheme;           // the advection scheme (2 C2, 3 U3, 4 C4 inside GAD_CALC_RHS; 30/33 multi-dim)
+  double *gNm2;         // ADAMS_BASHFORTH3: gtNm(:,:,:,2) (gNm1 is slot 1)
 };
 
 // Fields exchanged together by k_exchange_multi.

@@ -152,7 +152,7 @@ bool dyn_thermo_takes_gm(const Params &p) {
 bool dyn_thermo_fusable(const Dims &d, const Params &p, const TracerArgs &aT, const TracerArgs &aS) {
   return mg_hfuse(MG_FUSE_DT, d.nx, d.ny, d.nT, d.Nr) && p.momStepping && p.tempStepping && p.saltStepping &&
          p.useGMRedi && p.implicitDiffusion && !aT.multiDim && !aS.multiDim && !p.vectorInvariantMomentum &&
-         aT.scr != aS.scr;
+         aT.scr != aS.scr && aT.scheme == 2 && aS.scheme == 2 && !p.useAB3;   // (tracer_rhs_body_br: C2, AB2)
 }
 
 // CALC_PHI_HYD's column frame as launch_phi_hyd sizes it

@@ -640,6 +640,35 @@ __device__ __forceinline__ void tracer_rhs_body_br(const Dims &d, const Params &
 // GAD_CALC_RHS + forcing + AB2 + TIMESTEP_TRACER for one interior (i,j,k) point:
 // writes gNm1 (AB tracers) and a.scr = tracer + dTtracer*gT (the right-hand side of
 // the implicit vertical solve, or the new tracer with explicit vertical diffusion).
+// GAD_U3_ADV_X/Y (gad_u3_adv_x.F:70-92, scheme 3) and GAD_C4_ADV_X/Y (gad_c4_adv_x.F:70-93,
+// scheme 4) at one face: transport uTr, the tracer at the two cells either side (tm2, tm1 | t0,
+// tp1) and maskLocW (= maskW(k) without OBCS, gad_calc_rhs.F:262-268) at the faces i-1, i, i+1
+__device__ __forceinline__ double gad_u3c4_face(bool c4, double uTr, double tm2, double tm1, double t0, double tp1,
+                                                double mm1, double m0, double mp1) {
+  const double oneSixth = 1.0 / 6.0;
+  const double Rjp = (tp1 - t0) * mp1, Rj = (t0 - tm1) * m0, Rjm = (tm1 - tm2) * mm1;
+  const double Rjjp = Rjp - Rj, Rjjm = Rj - Rjm;
+  double v = uTr * (t0 + tm1 - oneSixth * (Rjjp + Rjjm)) * 0.5;
+  if (c4) v = v + fabs(uTr) * 0.5 * oneSixth * (Rjjp - Rjjm) * (1.0 - mm1 * mp1);
+  else v = v + fabs(uTr) * 0.5 * oneSixth * (Rjjp - Rjjm);
+  return v;
+}
+// GAD_U3_ADV_R (gad_u3_adv_r.F:58-88) / GAD_C4_ADV_R (gad_c4_adv_r.F:58-92) through the top face of
+// level k (2 <= k <= Nr): km1 = k-1, km2 = max(1, k-2), kp1 = min(Nr, k+1); U3 masks Rjm at km2,
+// C4 at km1 and adds its boundary factor
+__device__ __forceinline__ double gad_u3c4_r(bool c4, int k, int Nr, double rTr, double tkm2, double tkm1, double tk,
+                                             double tkp1, double mkm2, double mkm1, double mkp1) {
+  const double oneSixth = 1.0 / 6.0;
+  const double Rjp = (tkp1 - tk) * mkp1, Rj = (tk - tkm1), Rjm = (tkm1 - tkm2) * (c4 ? mkm1 : mkm2);
+  const double Rjjp = Rjp - Rj, Rjjm = Rj - Rjm;
+  if (c4) {
+    const double maskPM = (k <= 2 || k >= Nr) ? 0.0 : 1.0;
+    const double maskBound = maskPM * mkm2 * mkp1;
+    return mkm1 * (rTr * ((tk + tkm1) * 0.5 - oneSixth * (Rjjm + Rjjp) * 0.5) +
+                   fabs(rTr) * oneSixth * (Rjjm - Rjjp) * 0.5 * (1.0 - maskBound));
+  }
+  return mkm1 * (rTr * ((tk + tkm1) * 0.5 - oneSixth * (Rjjm + Rjjp) * 0.5) + fabs(rTr) * oneSixth * (Rjjm - Rjjp) * 0.5);
+}
 template <bool GM>
 __device__ __forceinline__ void tracer_rhs_body(const Dims &d, const Params &p, const Fields &f, const TracerArgs &a,
                                                 const int *iterPtr, int lb) {
@@ -721,7 +750,10 @@ __device__ __forceinline__ void tracer_rhs_body(const Dims &d, const Params &p, 
     const double ku = G3(Kux, ii, j, k), kz = G3(Kuz, ii, j, k);
     const double dz = GM ? gm_dTdz(ii, j, 0) : 0.0;
     double fz = 0.0;
-    if (calcAdv) fz = fz + (uf * xA) * (t0 + tw) * 0.5;
+    if (calcAdv && a.scheme == 2) fz = fz + (uf * xA) * (t0 + tw) * 0.5;
+    else if (calcAdv)
+      fz = fz + gad_u3c4_face(a.scheme == 4, uf * xA, T3(ii - 2, j, k), tw, t0, T3(ii + 1, j, k), G3(maskW, ii - 1, j, k),
+                              G3(maskW, ii, j, k), G3(maskW, ii + 1, j, k));
     double df = 0.0;
     if (a.diffKh != 0.0) df = -a.diffKh * xA * rdx * (t0 - tw);
     if (GM)   // GMREDI_XTRANSPORT (gmredi_xtransport.F:94-101)
@@ -735,7 +767,10 @@ __device__ __forceinline__ void tracer_rhs_body(const Dims &d, const Params &p, 
     const double kv = G3(Kvy, i, jj, k), kz = G3(Kvz, i, jj, k);
     const double dz = GM ? gm_dTdz(i, jj, 1) : 0.0;
     double fm = 0.0;
-    if (calcAdv) fm = fm + (vf * yA) * (t0 + ts) * 0.5;
+    if (calcAdv && a.scheme == 2) fm = fm + (vf * yA) * (t0 + ts) * 0.5;
+    else if (calcAdv)
+      fm = fm + gad_u3c4_face(a.scheme == 4, vf * yA, T3(i, jj - 2, k), ts, t0, T3(i, jj + 1, k), G3(maskS, i, jj - 1, k),
+                              G3(maskS, i, jj, k), G3(maskS, i, jj + 1, k));
     double df = 0.0;
     if (a.diffKh != 0.0) df = -a.diffKh * yA * rdy * (t0 - ts);
     if (GM)   // GMREDI_YTRANSPORT
@@ -762,7 +797,13 @@ __device__ __forceinline__ void tracer_rhs_body(const Dims &d, const Params &p, 
     const double ivd = G3(IVDConvCount, i, j, kc), kwz = G3(Kwz, i, j, kc), rdc = f.recip_drC[kcm];
     double fv = 0.0;
     if (in && calcAdv) {
-      const double wT = mm * rTr * (tk + tm) * 0.5;
+      double wT;
+      if (a.scheme == 2) wT = mm * rTr * (tk + tm) * 0.5;
+      else {
+        const int kp = kc + 1 <= Nr ? kc + 1 : Nr, km2 = kc - 2 >= 1 ? kc - 2 : 1;
+        wT = gad_u3c4_r(a.scheme == 4, kc, Nr, rTr, T3(i, j, km2), tm, tk, T3(i, j, kp), G3(maskC, i, j, km2), mm,
+                        G3(maskC, i, j, kp));
+      }
       fv = fv + wT * maskInC;
     }
     double dfr = 0.0;
@@ -805,7 +846,19 @@ __device__ __forceinline__ void tracer_rhs_body(const Dims &d, const Params &p, 
   double gtForc = 0.0;
   if (a.forcing && a.sfc && k == 1) gtForc = gtForc + a.sfc[q] * f.recip_drF[0] * f.recip_hFacC[q3];
   if (!p.tracForcingOutAB) gT = gT + gtForc;   // inside (0) / after (1) AB2: temp_integrate.F:373-410
-  if (a.useAB) {   // ADAMS_BASHFORTH2(k)
+  if (a.useAB && p.useAB3) {   // ADAMS_BASHFORTH3(k) (adams_bashforth3.F:60-103; startAB = nIter0)
+    const int n0 = p.nIter0, startAB = p.nIter0;
+    double ab0, ab1, ab2;
+    if (myIter == n0 && startAB == 0) { ab0 = 0.0; ab1 = 0.0; ab2 = 0.0; }
+    else if ((myIter == n0 && startAB == 1) || (myIter == 1 + n0 && startAB == 0)) { ab0 = p.alph_AB; ab1 = -p.alph_AB; ab2 = 0.0; }
+    else { ab0 = p.alph_AB + p.beta_AB; ab1 = -p.alph_AB - 2. * p.beta_AB; ab2 = p.beta_AB; }
+    const bool m1first = (myIter + 1) % 2 == 0;   // m1 = 1 + MOD(myIter+1, 2): slot 1 is gNm1, slot 2 gNm2
+    double *gA = m1first ? a.gNm1 : a.gNm2, *gB = m1first ? a.gNm2 : a.gNm1;
+    const double g = gT;
+    const double abG = ab0 * g + ab1 * gA[q3] + ab2 * gB[q3];
+    gB[q3] = g;
+    gT = g + abG;
+  } else if (a.useAB) {   // ADAMS_BASHFORTH2(k)
     const double ab = abFac * (gT - a.gNm1[q3]);
     double gN = gT;
     gT = gT + ab;
@@ -1370,6 +1423,8 @@ hipError_t launch_tracer_step(const Dims &d, const Params &p, const Fields &f, c
   }
   // GM/Redi fluxes as a template switch: without them the kernel holds half the registers
   if (p.useGMRedi) hipLaunchKernelGGL(k_tracer_rhs<true>, grd, blk, 0, s, d, p, f, a, iterPtr);
+  else if (a.scheme != 2 || p.useAB3)   // U3 / C4 and ADAMS_BASHFORTH3: the generic body only
+    hipLaunchKernelGGL(k_tracer_rhs<false>, grd, blk, 0, s, d, p, f, a, iterPtr);
   else if (tracer_march_on(d)) {
     // the k-march (deep grids; MGCM_TRACER_MARCH=0|1 overrides): KC levels per workgroup, five
     // chunks (round 3: LLC-90 fastest among 1/2/5/10 chunks, profiles/r03/)

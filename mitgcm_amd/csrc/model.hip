@@ -163,7 +163,7 @@ struct PDesc {
 #define PD(n) {#n, offsetof(Params, n), false}
 #define PI_(n) {#n, offsetof(Params, n), true}
 static const PDesc PARAMS[] = {
-    PD(deltaTMom), PD(deltaTFreeSurf), PD(deltaTClock), PD(abEps), PD(rhoConst), PD(gBaro), PD(viscAhD), PD(viscAhZ),
+    PD(deltaTMom), PD(deltaTFreeSurf), PD(deltaTClock), PD(abEps), PD(alph_AB), PD(beta_AB), PI_(useAB3), PD(rhoConst), PD(gBaro), PD(viscAhD), PD(viscAhZ),
     PD(viscA4D), PD(viscA4Z), PD(viscAr), PD(sideDragFactor), PD(freeSurfFac), PD(implicSurfPress),
     PD(implicDiv2DFlow), PD(rkSign), PD(afFacMom), PD(vfFacMom), PD(pfFacMom), PD(cfFacMom), PD(foFacMom),
     PD(mtFacMom), PD(cg2dNorm), PD(cg2dTolerance_sq),
@@ -803,7 +803,7 @@ mgcm_model *mgcm_create(int sNx, int sNy, int OLx, int OLy, int Nr, int nSx, int
   d.t0 = 0; d.nT = d.nTiles;
   // defaults (model/src/set_defaults.F, resolved by ini_parms.F)
   Params &p = m->p;
-  p.abEps = 0.01; p.rhoConst = 999.8; p.gBaro = 9.81; p.sideDragFactor = 2.0; p.freeSurfFac = 1.0;
+  p.abEps = 0.01; p.alph_AB = 0.5; p.beta_AB = 5.0 / 12.0; p.useAB3 = 0; p.rhoConst = 999.8; p.gBaro = 9.81; p.sideDragFactor = 2.0; p.freeSurfFac = 1.0;
   p.implicSurfPress = 1.0; p.implicDiv2DFlow = 1.0; p.rkSign = -1.0;
   p.afFacMom = p.vfFacMom = p.pfFacMom = p.cfFacMom = p.foFacMom = p.mtFacMom = 1.0;
   p.momAdvection = p.momViscosity = p.momForcing = p.useCoriolis = 1;
@@ -1299,15 +1299,25 @@ int mgcm_init(mgcm_model *m) {
   m->p.metricSphere = sph && ext("selectMetricTerms", 1.0) >= 1.0;
   m->p.recip_rSphere = sph ? 1.0 / ext("rSphere", 6370.0e3) : 0.0;   // ini_parms.F:1334
   if (ext("integr_GeoPot", 2.0) != 2.0) return set_err("mgcm_init: only integr_GeoPot = 2 is implemented");
-  // tracer advection schemes implemented on the device: 2 (C2, AB2), 30 (DST3) and 33 (DST3
-  // flux-limited), the last two multi-dimensional; the vertical scheme must match the horizontal one
+  // tracer advection schemes implemented on the device: 2 (C2), 3 (U3) and 4 (C4) inside
+  // GAD_CALC_RHS with Adams-Bashforth on the tendency, 30 (DST3) and 33 (DST3 flux-limited)
+  // multi-dimensional; the vertical scheme must match the horizontal one
   auto okScheme = [&](int s, const char *vname) {
-    return (s == 2 || ((s == 30 || s == 33) && m->p.multiDimAdvection)) && ext(vname, (double)s) == (double)s;
+    return (s == 2 || s == 3 || s == 4 || ((s == 30 || s == 33) && m->p.multiDimAdvection)) &&
+           ext(vname, (double)s) == (double)s;
   };
+  auto wideScheme = [&](int s) { return s == 3 || s == 4; };
+  if (((m->p.tempStepping && wideScheme(m->p.tempAdvScheme)) || (m->p.saltStepping && wideScheme(m->p.saltAdvScheme))) &&
+      (m->uvMap || m->d.OLx < 2 || m->d.OLy < 2))
+    return set_err("mgcm_init: advection schemes 3 / 4 need OLx, OLy >= 2 and a lat-lon topology on the device");
+  // ADAMS_BASHFORTH3 (ALLOW_ADAMSBASHFORTH_3) is restated for the tracers' tendencies only
+  if (m->p.useAB3 && (m->p.momStepping || (m->p.nonlinFreeSurf > 0 && m->p.select_rStar > 0) || m->p.staggerTimeStep))
+    return set_err("mgcm_init: ADAMS_BASHFORTH3 only for the tracers (momStepping off, no r*, not staggered)");
   // the cube's multi-dimensional split (3 face-dependent passes with corner fills,
   // gad_advection.F:339-367) runs the general pass kernels (kernels_thermo.hip k_advg_*),
   // which need the tile face / edge table of the EXCH2 topology and OLx = OLy (corner fills)
-  if (m->uvMap && ((m->p.tempStepping && m->p.tempAdvScheme != 2) || (m->p.saltStepping && m->p.saltAdvScheme != 2))) {
+  auto mdScheme = [&](int s) { return s == 30 || s == 33; };
+  if (m->uvMap && ((m->p.tempStepping && mdScheme(m->p.tempAdvScheme)) || (m->p.saltStepping && mdScheme(m->p.saltAdvScheme)))) {
     if (!m->f.tileFace) return set_err("mgcm_init: multi-dimensional advection on EXCH2 needs the tile face table");
     if (m->d.OLx != m->d.OLy) return set_err("mgcm_init: cube multi-dimensional advection needs OLx = OLy");
   }
@@ -1316,7 +1326,7 @@ int mgcm_init(mgcm_model *m) {
   if (m->p.saltStepping && !okScheme(m->p.saltAdvScheme, "saltVertAdvScheme"))
     return set_err("mgcm_init: saltAdvScheme %d not implemented on the device", m->p.saltAdvScheme);
   if (m->p.useGMRedi && m->p.GM_AdvForm && m->p.multiDimAdvection &&
-      ((m->p.tempStepping && m->p.tempAdvScheme != 2) || (m->p.saltStepping && m->p.saltAdvScheme != 2)))
+      ((m->p.tempStepping && mdScheme(m->p.tempAdvScheme)) || (m->p.saltStepping && mdScheme(m->p.saltAdvScheme))))
     return set_err("mgcm_init: GM_AdvForm with multi-dimensional advection is not implemented on the device");
   if (m->p.useGMRedi && m->p.GM_AdvForm && m->p.GM_skewflx != 0.0)
     return set_err("mgcm_init: GM_AdvForm needs GM_skewflx = 0 (gmredi_readparms.F:243-244)");
@@ -1412,10 +1422,14 @@ static TracerArgs tracer_args(mgcm_model *m, bool salt) {
   a.dT = p.deltaTtracer;
   a.advection = salt ? p.saltAdvection : p.tempAdvection;
   a.forcing = salt ? p.saltForcing : p.tempForcing;
-  // gad_init_fixed.F:126-162: multi-dim advection for non-C2 schemes, AB2 on the tendency for C2
-  a.multiDim = p.multiDimAdvection && a.advection && scheme != 2;
-  a.useAB = scheme == 2;
+  // gad_init_fixed.F:126-162: multi-dim advection for the schemes that are not
+  // Adams-Bashforth ones; AB (2 or 3) on the tendency for C2, U3 and C4
+  const bool abScheme = scheme == 2 || scheme == 3 || scheme == 4;
+  a.multiDim = p.multiDimAdvection && a.advection && !abScheme;
+  a.useAB = abScheme;
   a.limiter = scheme == 33;   // DST3 (30) without, DST3FL (33) with the flux limiter
+  a.scheme = scheme;
+  a.gNm2 = salt ? m->f.gsNm2 : m->f.gtNm2;
   return a;
 }
 

@@ -207,3 +207,72 @@ def test_baroclinic_dst3fl_10_steps_vs_oracle():
     for k in ("dynstat_theta_sd", "dynstat_theta_max", "dynstat_uvel_sd"):
         assert digits(st_d[k], st_o[k]) >= 11.0, k
     m.close()
+
+
+def test_advect_xy_ab3_c4_vs_oracle_and_reference(golden_dir):
+    """verification/advect_xy/input.ab3_c4 on the device: theta and salt with the centred
+    4th-order scheme (GAD_C4_ADV_X/Y) stepped by ADAMS_BASHFORTH3 -- bit-exact vs the oracle
+    every 10 steps over 100 (interior), and the reference's min/max/mean/sd of both tracers
+    (results/output.ab3_c4.txt) at print precision."""
+    from mitgcm_amd import configs
+    from oracle.harness import oracle_from_config
+    gold = json.load(open(os.path.join(golden_dir, "advect_xy", "monitor.ab3_c4.json")))
+    o, g = oracle_from_config(configs.advect_xy_ab3_c4)
+    m = configs.make_model(configs.advect_xy_ab3_c4)
+    inner = (slice(None), slice(None)) + g.sl(1, g.sNx, 1, g.sNy)
+    worst = (99.0, None)
+    for n in range(1, 101):
+        m.forward_step(1)
+        o.forward_step()
+        if n % 10:
+            continue
+        for tr in ("theta", "salt"):
+            dev = m.get(tr)
+            ref = np.array(o.arr(tr)).reshape(dev.shape)
+            assert np.array_equal(dev[inner], ref[inner]), (n, tr, np.abs(dev - ref)[inner].max())
+            st = o.stats(ref, 1, o.arr("hFacC"), 1, o.arr("maskInC"), o.arr("rA"), o.arr("drF")[:1].copy())
+            for v, k in zip(st[:4], ("min", "max", "mean", "sd")):
+                worst = min(worst, (digits(v, gold[n // 10]["dynstat_%s_%s" % (tr, k)]), (n, tr, k)))
+    m.close()
+    print("advect_xy ab3_c4: device == oracle bit for bit; vs output.ab3_c4.txt worst %.2f digits at %s" % worst)
+    assert worst[0] >= 13.0, worst
+
+
+@pytest.mark.parametrize("scheme", [3, 4])
+def test_baroclinic_u3c4_thermodynamics_bitexact_vs_oracle(scheme):
+    """tutorial_baroclinic_gyre with tempAdvScheme = 3 (GAD_U3_ADV_X/Y/R) or 4 (GAD_C4_ADV_X/Y/R),
+    Adams-Bashforth 2 on the tendency: one THERMODYNAMICS call from a stepped, convectively
+    perturbed state over the bathymetry's masks (the vertical scheme's km2 / kp1 masks and
+    C4's boundary factor included), bit-exact against the oracle; then 10 steps within the
+    CG2D's summation-order tolerance (parity unpinned against the reference: no committed
+    output for these schemes on this experiment)."""
+    from mitgcm_amd import configs
+    from mitgcm_amd._lib import lib
+    from oracle.harness import oracle_from_config
+    cfg = lambda **kw: configs.baroclinic_gyre(tempAdvScheme=scheme, **kw)
+    o, g = oracle_from_config(cfg)
+    for _ in range(3):
+        o.forward_step()
+    o.arr("theta")[:, 1, 10:16, 8:20] += 12.0
+    m = configs.make_model(cfg)
+    for n in ("uVel", "vVel", "wVel", "theta", "gtNm1", "etaN"):
+        m.put(n, np.array(o.arr(n)))
+    lib().mgcm_set_param(m.h, b"myIter", float(o.get("myIter")))
+    m.thermodynamics()
+    o.L.oracle_oceanic_phys(o.h)
+    o.L.oracle_thermodynamics(o.h)
+    inner = (slice(None), slice(None)) + g.sl(1, g.sNx, 1, g.sNy)
+    dev, ref = m.get("theta")[inner], np.array(o.arr("theta"))[inner]
+    assert np.array_equal(dev, ref), np.abs(dev - ref).max()
+    m.close()
+    o, g = oracle_from_config(cfg)
+    m = configs.make_model(cfg)
+    for _ in range(10):
+        o.forward_step()
+    m.forward_step(10)
+    m.sync()
+    for n in ("uVel", "vVel", "theta", "etaN"):
+        dev, ref = m.get(n), np.array(o.arr(n)).reshape(m.get(n).shape)
+        sc = np.abs(ref).max()
+        assert np.abs(dev - ref).max() <= 1e-10 * sc, (n, np.abs(dev - ref).max(), sc)
+    m.close()
