@@ -1313,6 +1313,8 @@ int mgcm_init(mgcm_model *m) {
   // ADAMS_BASHFORTH3 (ALLOW_ADAMSBASHFORTH_3) is restated for the tracers' tendencies only
   if (m->p.useAB3 && (m->p.momStepping || (m->p.nonlinFreeSurf > 0 && m->p.select_rStar > 0) || m->p.staggerTimeStep))
     return set_err("mgcm_init: ADAMS_BASHFORTH3 only for the tracers (momStepping off, no r*, not staggered)");
+  // (a restart would need both history slots, gtNm(:,:,:,1:2), which the pickup path does not carry)
+  if (m->p.useAB3 && m->p.nIter0 != 0) return set_err("mgcm_init: ADAMS_BASHFORTH3 from a pickup (nIter0 != 0) not supported");
   // the cube's multi-dimensional split (3 face-dependent passes with corner fills,
   // gad_advection.F:339-367) runs the general pass kernels (kernels_thermo.hip k_advg_*),
   // which need the tile face / edge table of the EXCH2 topology and OLx = OLy (corner fills)
