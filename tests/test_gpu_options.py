@@ -199,3 +199,32 @@ def test_ocean90_cd_implicit_viscosity_4_steps_vs_oracle():
         sc = np.abs(ref).max()
         assert np.abs(dev - ref).max() <= 1e-10 * sc, (n, np.abs(dev - ref).max(), sc)
     m.close()
+
+
+# Options the device does not restate are refused at mgcm_init with the reason, never run
+# silently: ADAMS_BASHFORTH3 with momentum stepping or from
+# a pickup, the U3 / C4 schemes on a pkg/exch2 topology, a scheme the device does not carry.
+@pytest.mark.parametrize("case", ["ab3_momentum", "ab3_pickup", "c4_cube", "os7mp"])
+def test_unsupported_options_refused(case):
+    from mitgcm_amd import configs
+    from mitgcm_amd._lib import MgcmError
+
+    def cfg():
+        if case == "c4_cube":
+            g, p, s = configs.global_ocean_cs32x15(sNy=32)[:3]
+            p.update(tempAdvScheme=4, tempVertAdvScheme=4)
+            return g, p, s
+        g, p, s = configs.advect_xy_ab3_c4()
+        if case == "ab3_momentum":
+            p["momStepping"] = 1
+        elif case == "ab3_pickup":
+            p["nIter0"] = 10
+        elif case == "os7mp":
+            p.update(useAB3=0, saltAdvScheme=7, saltVertAdvScheme=7)
+        return g, p, s
+    with pytest.raises(MgcmError) as e:
+        configs.make_model(cfg)
+    msg = str(e.value)
+    want = {"ab3_momentum": "ADAMS_BASHFORTH3", "ab3_pickup": "ADAMS_BASHFORTH3", "c4_cube": "schemes 3 / 4",
+            "os7mp": "saltAdvScheme 7"}[case]
+    assert want in msg, msg
