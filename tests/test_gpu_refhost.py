@@ -213,7 +213,7 @@ def test_refhost_mods_dropins_bitexact(layout, refOrder, models, mwg, eager, pac
 @pytest.mark.parametrize("io,register,models,cap", [("namelist", 1, 1, ""), ("off", 1, 1, ""), ("namelist", 0, 1, ""),
                                                     ("off", 1, 2, ""), ("off", 1, 3, ""), ("off", 1, 4, ""),
                                                     ("off", 1, 6, ""), ("off", 1, 2, "multi"), ("off", 1, 4, "one"),
-                                                    ("off", 1, 6, "one"), ("off", 1, 2, "virtual"),
+                                                    ("off", 1, 6, "one"), ("off", 1, 3, "multi"), ("off", 1, 2, "virtual"),
                                                     ("off", 1, 4, "virtual"), ("off", 1, 4, "virtual-eager")])
 def test_refhost_dropin_throughput(io, register, models, cap, tmp_path):
     from mitgcm_amd import configs
