@@ -1092,12 +1092,27 @@ __global__ void __launch_bounds__(256) TRM_ATTR k_tracer_march2(Dims d, Params p
   int b = mg_xcd_block();
   const int kc = b % nkc;
   b /= nkc;
-  const int hx = d.sNx >> 1, TY = 256 / hx;
-  const int ty = b % nty, t = d.t0 + b / nty;
-  const int px = (int)threadIdx.x % hx, jy = (int)threadIdx.x / hx;
-  if (jy >= TY) return;
-  const int i = 1 + 2 * px, j = 1 + ty * TY + jy;
-  if (j > d.sNy) return;
+  const int hx = d.sNx >> 1;
+  int i, j, t;
+  if (nty < 0) {   // flat: -nty consecutive column pairs of the slab's interior per workgroup
+    const int pw = -nty, np = hx * d.sNy;
+    if ((int)threadIdx.x >= pw) return;
+    const long gid = (long)b * pw + threadIdx.x;
+    if (gid >= (long)np * d.nT) return;
+    const int rem = (int)(gid % np);
+    t = d.t0 + (int)(gid / np);
+    j = 1 + rem / hx;
+    i = 1 + 2 * (rem % hx);
+  } else {         // whole rows of one tile: sNx/2 pairs x 256/(sNx/2) rows
+    const int TY = 256 / hx;
+    const int ty = b % nty;
+    t = d.t0 + b / nty;
+    const int px = (int)threadIdx.x % hx, jy = (int)threadIdx.x / hx;
+    if (jy >= TY) return;
+    i = 1 + 2 * px;
+    j = 1 + ty * TY + jy;
+    if (j > d.sNy) return;
+  }
   const int Nr = d.Nr, k0 = 1 + kc * KC, k1 = min(Nr, k0 + KC - 1);
   const int myIter = *iterPtr;
   const long nx = d.nx, n2 = d.n2, q = MG_I2(d, i, j, t);
@@ -1432,8 +1447,11 @@ hipError_t launch_tracer_step(const Dims &d, const Params &p, const Fields &f, c
     const int nkc = (d.Nr + KC - 1) / KC, ntx = (d.sNx + TRM_TX - 1) / TRM_TX, nty = (d.sNy + TRM_TY - 1) / TRM_TY;
     auto al = [](const void *x) { return ((uintptr_t)x & 15u) == 0; };
     // the two-column form (double2 accesses) where the slab's layout allows it; MGCM_TRACER_MARCH2=0
-    // forces the one-column form the other layouts run (tests cover both)
-    const int m2Env = getenv("MGCM_TRACER_MARCH2") ? atoi(getenv("MGCM_TRACER_MARCH2")) : 1;
+    // forces the one-column form the other layouts run, =1 the whole-column march with whole
+    // tile rows per workgroup instead of its column pairs dealt evenly over one workgroup per
+    // CU (2, the default: LLC-90 211 against 216 us per tracer, step unchanged, 1.2495-1.2500
+    // against 1.2492-1.2500 ms alternating on one box, profiles/r06/trflat/; tests cover all)
+    const int m2Env = getenv("MGCM_TRACER_MARCH2") ? atoi(getenv("MGCM_TRACER_MARCH2")) : 2;
     const int hx = d.sNx / 2;
     if (m2Env != 0 && (d.sNx & 1) == 0 && (d.OLx & 1) == 0 && (d.nx & 1) == 0 && (d.n3 & 1) == 0 && hx <= 256 && al(a.tr) &&
         al(a.trNext) && al(a.scr) && al(a.gNm1) && al(f.maskC) && al(f.wVel) && al(f.IVDConvCount) && al(f.uVel) &&
@@ -1443,6 +1461,18 @@ hipError_t launch_tracer_step(const Dims &d, const Params &p, const Fields &f, c
       const int fwd = tracer_fwd_form(d);
       if (impl && p.implicitDiffusion && !p.useGMRedi && fwd && !a.multiDim && a.cp && al(a.cp) && d.Nr > 1) {
         if (fwd == 3) {
+          if (m2Env == 2) {   // flat: the column pairs dealt evenly over one workgroup per CU
+            static int nCU = 0;
+            int dev = 0;
+            if (!nCU && (hipGetDevice(&dev) != hipSuccess ||
+                         hipDeviceGetAttribute(&nCU, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || nCU < 1))
+              nCU = 256;
+            const long np = (long)hx * d.sNy * d.nT;
+            const int pw = (int)std::min<long>(256, (np + nCU - 1) / nCU);
+            hipLaunchKernelGGL((k_tracer_march2<true, true>), dim3((unsigned)((np + pw - 1) / pw)), blk, 0, s, d, p, f, a,
+                               iterPtr, d.Nr, 1, -pw);
+            return hipGetLastError();
+          }
           hipLaunchKernelGGL((k_tracer_march2<true, true>), dim3((unsigned)(nty2 * d.nT)), blk, 0, s, d, p, f, a, iterPtr,
                              d.Nr, 1, nty2);
           return hipGetLastError();

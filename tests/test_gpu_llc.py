@@ -18,8 +18,8 @@ import pytest
 pytestmark = pytest.mark.gpu
 
 
-@pytest.mark.parametrize("march", [None, "tracer", "tracer:v1", "tracer:fwd", "tracer:fwdback", "vi", "vi:generic",
-                                   "fuse:29", "fuse:45", "fuse:77"])
+@pytest.mark.parametrize("march", [None, "tracer", "tracer:v1", "tracer:fwd", "tracer:fwdback", "tracer:rows", "vi",
+                                   "vi:generic", "fuse:29", "fuse:45", "fuse:77"])
 def test_llc30_8_steps_bitexact_vs_device_order_oracle(march, monkeypatch):
     """march: the LLC-90 default kernel forms forced on LLC-30 (too small to pick them by
     itself).  "tracer": the tracer right-hand side as the k-march (MGCM_TRACER_MARCH=1, five
@@ -32,9 +32,13 @@ def test_llc30_8_steps_bitexact_vs_device_order_oracle(march, monkeypatch):
     MGCM_STEP_FUSE launch fusions (29: the opt-in k_phys_phi pass; 45: the opt-in
     EXCH(cg2d_x) + etaN beside the correction step; 77: the tracers' halo exchange on their own
     stream)."""
-    if march in ("tracer:fwd", "tracer:fwdback"):   # the implicit solve's forward sweep inside the whole-column
-        # march, then the back substitution as a kernel of its own (2) or by the same threads (3)
+    if march in ("tracer:fwd", "tracer:fwdback", "tracer:rows"):   # the implicit solve's forward sweep inside the
+        # whole-column march, then the back substitution as a kernel of its own (2) or by the same
+        # threads (3, its column pairs dealt evenly over the workgroups); "rows": (3) with whole
+        # tile rows per workgroup (MGCM_TRACER_MARCH2=1)
         monkeypatch.setenv("MGCM_TRACER_MARCH", "2" if march == "tracer:fwd" else "3")
+        if march == "tracer:rows":
+            monkeypatch.setenv("MGCM_TRACER_MARCH2", "1")
         march = None
     if march and march.endswith(":v1"):
         monkeypatch.setenv("MGCM_TRACER_MARCH2", "0")
@@ -75,7 +79,13 @@ def test_llc30_8_steps_bitexact_vs_device_order_oracle(march, monkeypatch):
     m.close()
 
 
-def test_llc90_full_size_steps():
+@pytest.mark.parametrize("pairs", [None, "1"])
+def test_llc90_full_size_steps(pairs, monkeypatch):
+    """pairs "1": the tracers' whole-column march with whole tile rows per workgroup
+    (MGCM_TRACER_MARCH2=1) instead of its column pairs dealt evenly over the workgroups (the
+    default)."""
+    if pairs:
+        monkeypatch.setenv("MGCM_TRACER_MARCH2", pairs)
     from mitgcm_amd import configs
     from mitgcm_amd.model import dynstat
     from oracle.harness import oracle_from_config
