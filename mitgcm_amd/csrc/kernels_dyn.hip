@@ -2584,17 +2584,22 @@ hipError_t launch_mom_step(const Dims &d, const Params &p, const Fields &f, cons
     int BX, BY;
     vi_tile_shape(d, BX, BY);
     const int nbx = (d.sNx + 2 + BX - 1) / BX, nby = (d.sNy + 2 + BY - 1) / BY;
-    // levels per workgroup: enough workgroups to fill the chip several times, few enough
-    // that the two extra staged levels per chunk stay a small overhead.  The k-march for deep
-    // grids (Nr >= 30 with >= 256 workgroups per level chunk), in two chunks of levels (round
-    // 4, k_mom_vi_m2: LLC-90 448-456 us against 460 at five and 453-460 at three, step
-    // 1.531-1.545 against 1.550-1.552 ms, profiles/r04/vikc/); otherwise one level per
+    // levels per workgroup: enough workgroups to fill the chip, few enough that the two extra
+    // staged levels per chunk stay a small overhead.  The k-march for deep grids (Nr >= 30
+    // with >= 256 workgroups per level chunk), in two chunks of levels (round 4, k_mom_vi_m2:
+    // LLC-90 448-456 us against 460 at five and 453-460 at three, step 1.531-1.545 against
+    // 1.550-1.552 ms, profiles/r04/vikc/) or one (below); otherwise one level per
     // workgroup.  MGCM_VI_KERNEL = march | march_generic | level | tiled forces a form (the
     // tests run each: march_generic is the generic k-march that serves option sets without
     // a k_mom_vi_m2 instantiation; read per launch)
     const char *viEnv = getenv("MGCM_VI_KERNEL");
     const int nbt = nbx * nby * d.nT;
-    const int KCm = (d.Nr + 1) / 2;
+    // Round 6: the whole column per workgroup where the blocks then fit one resident round (2
+    // workgroups of k_mom_vi_m2 per CU, 256 CUs): LLC-90's 468 blocks, 313 against 319-320 us
+    // for two chunks (936 workgroups, 1.83 rounds) and 321 for three (profiles/r06/vikc/);
+    // MGCM_VI_KC forces the levels per workgroup (tests: ragged chunks)
+    const char *kcEnv = getenv("MGCM_VI_KC");
+    const int KCm = kcEnv ? std::max(1, atoi(kcEnv)) : (nbx * nby * d.nT <= 512 ? d.Nr : (d.Nr + 1) / 2);
     const bool generic = viEnv && !strcmp(viEnv, "march_generic");
     const bool march = viEnv ? (!strcmp(viEnv, "march") || generic) : (d.Nr >= 30 && nbt >= 256);
     if (march) {

@@ -19,7 +19,7 @@ pytestmark = pytest.mark.gpu
 
 
 @pytest.mark.parametrize("march", [None, "tracer", "tracer:v1", "tracer:fwd", "tracer:fwdback", "tracer:rows", "vi",
-                                   "vi:generic", "fuse:29", "fuse:45", "fuse:77"])
+                                   "vi:kc3", "vi:generic", "fuse:29", "fuse:45", "fuse:77"])
 def test_llc30_8_steps_bitexact_vs_device_order_oracle(march, monkeypatch):
     """march: the LLC-90 default kernel forms forced on LLC-30 (too small to pick them by
     itself).  "tracer": the tracer right-hand side as the k-march (MGCM_TRACER_MARCH=1, five
@@ -27,7 +27,7 @@ def test_llc30_8_steps_bitexact_vs_device_order_oracle(march, monkeypatch):
     the one-column k-march (the default is its two-column form) and the two-column
     DO_OCEANIC_PHYS forced (at full size the default; below 2^21 points the one-column form
     runs).  "vi": MOM_VECINV as the k-march in its compile-time specialisation
-    (k_mom_vi_m2<32, 8, LLC options>), "vi:generic" the generic k-march that serves option sets
+    (k_mom_vi_m2<32, 8, LLC options>; ":kc3" in chunks of 3 levels), "vi:generic" the generic k-march that serves option sets
     without an instantiation (MGCM_VI_KERNEL=march | march_generic).  "fuse:MASK": the
     MGCM_STEP_FUSE launch fusions (29: the opt-in k_phys_phi pass; 45: the opt-in
     EXCH(cg2d_x) + etaN beside the correction step; 77: the tracers' halo exchange on their own
@@ -48,6 +48,8 @@ def test_llc30_8_steps_bitexact_vs_device_order_oracle(march, monkeypatch):
         monkeypatch.setenv("MGCM_STEP_FUSE", march.split(":")[1])
     elif march and march.startswith("vi"):
         monkeypatch.setenv("MGCM_VI_KERNEL", "march_generic" if march.endswith("generic") else "march")
+        if march.endswith(":kc3"):   # ragged level chunks (3, 3, 3, 1) instead of the whole column
+            monkeypatch.setenv("MGCM_VI_KC", "3")
     elif march == "tracer":
         monkeypatch.setenv("MGCM_TRACER_MARCH", "1")
     from mitgcm_amd import configs
