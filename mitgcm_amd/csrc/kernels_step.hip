@@ -67,8 +67,26 @@ __global__ void __launch_bounds__(256) k_dt_back(Dims d, Params p, Fields f, Tra
 // and under r* with MG_FUSE_OPE UPDATE_CG2D's operator (nbOp blocks, ucg2d.h) and its
 // preconditioner (nbPc blocks) at the head of 2 and 3 (MGCM_OPE_AT=1: 1 and 2) -- the
 // operator of the step, built early
-__global__ void __launch_bounds__(256) k_dt_l1(Dims d, Params p, Fields f, int nc, int nbGm, int nbPhi, int nbOp) {
+// the fused grids' logical-block order: the longest bodies (CALC_PHI_HYD's and the implicit
+// solves' column sweeps, the tracers' right-hand sides) first, so they are not the dispatch's
+// tail (config 2: 0.2893-0.2897 against 0.2906-0.2911 ms/step for the order listed above,
+// alternating on one box, the fused grids 54.4 against 55.8 us, profiles/r06/dtorder/);
+// MGCM_DT_LAYOUT=4 runs the listed order
+static int dt_long_first() {
+  const char *e = getenv("MGCM_DT_LAYOUT");   // read per launch (A/B runs)
+  return !(e && atoi(e) == 4);
+}
+__global__ void __launch_bounds__(256) k_dt_l1(Dims d, Params p, Fields f, int nc, int nbGm, int nbPhi, int nbOp, int lf) {
   int lb = mg_xcd_block();
+  if (lf) {   // long first: CALC_PHI_HYD's column sweeps at the head of the dispatch
+    if (lb < nbPhi) { phi_hyd_body(d, p, f, nc, lb); return; }
+    lb -= nbPhi;
+    if (lb < nbOp) { ucg2d_op_point(d, p, f, lb); return; }
+    lb -= nbOp;
+    if (lb < nbGm) { gm_tensor_body(d, p, f, lb); return; }
+    del2uv_body(d, p, f, lb - nbGm);
+    return;
+  }
   if (lb < nbOp) { ucg2d_op_point(d, p, f, lb); return; }
   lb -= nbOp;
   if (lb < nbGm) { gm_tensor_body(d, p, f, lb); return; }
@@ -106,13 +124,21 @@ static void launch_l1(const Dims &d, const Params &p, const Fields &f, int nbDel
   phi_frame(d, p, nc, nArr, nbPhi);
   MG_ALLOW_LDS(k_dt_l1);
   hipLaunchKernelGGL(k_dt_l1, dim3((unsigned)(nbOp + nbGm + nbPhi + nbDel)), dim3(256), mg_colf_lds(d.Nr, nc, nArr), s, d, p,
-                     f, nc, nbGm, nbPhi, nbOp);
+                     f, nc, nbGm, nbPhi, nbOp, dt_long_first());
 }
 template <bool GM, bool FF4>
 __global__ void __launch_bounds__(256) k_dt_l2(Dims d, Params p, Fields f, TracerArgs aT, TracerArgs aS,
                                                const int *iterPtr, int nbMom, int nbTr, const long *__restrict__ srcOf,
-                                               int nbPc, int nbOp) {
+                                               int nbPc, int nbOp, int lf) {
   int lb = mg_xcd_block();
+  if (lf) {   // long first: the tracers' right-hand sides at the head of the dispatch
+    if (lb < 2 * nbTr) {
+      if (lb < nbTr) tracer_rhs_body_br<GM>(d, p, f, aT, iterPtr, lb);
+      else tracer_rhs_body_br<GM>(d, p, f, aS, iterPtr, lb - nbTr);
+      return;
+    }
+    lb -= 2 * nbTr;
+  }
   if (lb < nbPc) { ucg2d_p_point(d, p, f, srcOf, lb); return; }
   lb -= nbPc;
   if (lb < nbOp) { ucg2d_op_point(d, p, f, lb); return; }
@@ -129,8 +155,19 @@ __global__ void __launch_bounds__(256) k_dt_l2(Dims d, Params p, Fields f, Trace
 }
 __global__ void __launch_bounds__(256) k_dt_l3(Dims d, Params p, Fields f, TracerArgs aT, TracerArgs aS,
                                                const int *iterPtr, int nc, int nbCd, int nbImp, const long *__restrict__ srcOf,
-                                               int nbPc) {
+                                               int nbPc, int lf) {
   int lb = mg_xcd_block();
+  if (lf) {   // long first: the implicit solves' column sweeps at the head of the dispatch
+    if (lb < 2 * nbImp) {
+      if (lb < nbImp) tracer_impl_body<false>(d, p, f, aT, nc, lb);
+      else tracer_impl_body<false>(d, p, f, aS, nc, lb - nbImp);
+      return;
+    }
+    lb -= 2 * nbImp;
+    if (lb < nbPc) { ucg2d_p_point(d, p, f, srcOf, lb); return; }
+    cd_scheme_body(d, p, f, iterPtr, lb - nbPc);
+    return;
+  }
   if (lb < nbPc) { ucg2d_p_point(d, p, f, srcOf, lb); return; }
   lb -= nbPc;
   if (lb < nbCd) { cd_scheme_body(d, p, f, iterPtr, lb); return; }
@@ -238,14 +275,14 @@ hipError_t launch_dyn_thermo(const Dims &d, const Params &p, const Fields &f, co
     const int nbMom = ff4 ? mom_ff4_blocks(d) : 2 * (int)mg_plane_blocks(d.nx, d.ny, d.nT * d.Nr);
     auto l2 = ff4 ? k_dt_l2<true, true> : k_dt_l2<true, false>;
     hipLaunchKernelGGL(l2, dim3((unsigned)(nbPc2 + nbOp2 + nbMom + 2 * nbTr)), blk, 0, s, d, p, f, aT, aS, iterPtr, nbMom, nbTr,
-                       srcOf, nbPc2, nbOp2);
+                       srcOf, nbPc2, nbOp2, dt_long_first());
     const long ncolTr = (long)d.sNx * d.sNy * d.nT;
     const int ncTr = mg_colf_nc(ncolTr, d.Nr, 3);
     const int nbImp = (int)mg_colf_blocks(ncolTr, ncTr);
     const int nbCd = (int)mg_plane_blocks(d.nx - 2, d.ny - 2, d.nT * d.Nr);
     MG_ALLOW_LDS(k_dt_l3);
     hipLaunchKernelGGL(k_dt_l3, dim3((unsigned)(nbPc3 + nbCd + 2 * nbImp)), blk, mg_colf_lds(d.Nr, ncTr, 3), s, d, p, f, aT,
-                       aS, iterPtr, ncTr, nbCd, nbImp, srcOf, nbPc3);
+                       aS, iterPtr, ncTr, nbCd, nbImp, srcOf, nbPc3, dt_long_first());
     return hipGetLastError();
   }
   if (srcOf) return hipErrorInvalidValue;   // (the operator rides only in the default layout)

@@ -111,11 +111,12 @@ def test_ocean90_dynamics_bitexact():
     assert not bad, bad
 
 
-@pytest.mark.parametrize("variant", [None, "layout2", "fork", "phiflat", "ff4"])
+@pytest.mark.parametrize("variant", [None, "layout2", "order", "fork", "phiflat", "ff4"])
 def test_ocean90_10_steps(golden_dir, monkeypatch, variant):
     """variant None: the default step (THERMODYNAMICS' tracer kernels folded into DYNAMICS'
     launches, kernels_step.hip, with GMREDI_CALC_TENSOR in the first of them); "layout2": the
-    fold's front/back layout (MGCM_DT_LAYOUT=2); "fork": the tracers on the second stream
+    fold's front/back layout (MGCM_DT_LAYOUT=2); "order": the default layout's grids in their
+    listed logical-block order instead of the longest bodies first (MGCM_DT_LAYOUT=4); "fork": the tracers on the second stream
     beside DYNAMICS (MGCM_STEP_FUSE without MG_FUSE_DT); "phiflat": CALC_PHI_HYD's flat
     per-column pass with the r* and quasi-hydrostatic operands (MGCM_PHI_FLAT=2); "ff4": the
     momentum with four threads per point inside the fused grid (MGCM_MOM_FF4=2).  The overlap is
@@ -123,8 +124,8 @@ def test_ocean90_10_steps(golden_dir, monkeypatch, variant):
     monkeypatch.setenv("MGCM_OVERLAP", "1")
     if variant == "fork":
         monkeypatch.setenv("MGCM_STEP_FUSE", "13")
-    if variant == "layout2":
-        monkeypatch.setenv("MGCM_DT_LAYOUT", "2")
+    if variant in ("layout2", "order"):
+        monkeypatch.setenv("MGCM_DT_LAYOUT", "2" if variant == "layout2" else "4")
     if variant == "phiflat":
         monkeypatch.setenv("MGCM_PHI_FLAT", "2")
     if variant == "ff4":
