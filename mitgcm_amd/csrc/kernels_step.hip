@@ -70,7 +70,8 @@ __global__ void __launch_bounds__(256) k_dt_back(Dims d, Params p, Fields f, Tra
 // the fused grids' logical-block order: the longest bodies (CALC_PHI_HYD's and the implicit
 // solves' column sweeps, the tracers' right-hand sides) first, so they are not the dispatch's
 // tail (config 2: 0.2893-0.2897 against 0.2906-0.2911 ms/step for the order listed above,
-// alternating on one box, the fused grids 54.4 against 55.8 us, profiles/r06/dtorder/);
+// alternating on one box, the fused grids 54.4 against 55.8 us; rocprofv3 on another box, the
+// three grids 51.7-52.5 against 53.8-54.0 us, each grid faster, profiles/r06/dtorder/);
 // MGCM_DT_LAYOUT=4 runs the listed order
 static int dt_long_first() {
   const char *e = getenv("MGCM_DT_LAYOUT");   // read per launch (A/B runs)
